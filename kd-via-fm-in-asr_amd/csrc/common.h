@@ -1,0 +1,101 @@
+// kdfm — shared device/host helpers for the gfx950 kernels behind libkdfm.so.
+//
+// Storage convention: every activation/gradient tensor is fp32 in HBM, channels-last
+// (rows = utterance-major frames, columns = features). MFMA operands are converted to bf16
+// (throughput mode) or fed as exact f32 (parity mode) at LDS-staging time.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+
+#include "../../include/kdfm.h"
+
+namespace kdfm {
+
+// ---- error handling -------------------------------------------------------------------------
+void set_error(const std::string& msg);
+int check_launch(const char* what);
+
+#define KDFM_REQUIRE(cond, msg)                                  \
+  do {                                                           \
+    if (!(cond)) {                                               \
+      ::kdfm::set_error(std::string(__func__) + ": " + (msg));   \
+      return KDFM_EINVAL;                                        \
+    }                                                            \
+  } while (0)
+
+// ---- small math -------------------------------------------------------------------------------
+__host__ __device__ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  // round-to-nearest-even; NaN handled by the plain cast path in hipcc (v_cvt_pk_bf16_f32)
+  __bf16 h = (__bf16)f;
+  return __builtin_bit_cast(uint16_t, h);
+}
+
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
+__device__ __forceinline__ float siluf_(float x) { return x * sigmoidf_(x); }
+__device__ __forceinline__ float dsiluf_(float x) {
+  float s = sigmoidf_(x);
+  return s * (1.f + x * (1.f - s));
+}
+
+// ---- counter-based RNG (dropout masks, SpecAugment draws, NoiseAdapter eps) -----------------
+// splitmix64-style finaliser over (seed, stream, index): the same triple always yields the same
+// bits, so backward kernels regenerate the forward's dropout mask instead of storing it.
+__host__ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+__device__ __forceinline__ uint64_t rng_bits(uint64_t seed, uint64_t stream, uint64_t idx) {
+  return mix64(seed ^ mix64(stream * 0x2545F4914F6CDD1Dull + idx));
+}
+__device__ __forceinline__ float rng_uniform(uint64_t seed, uint64_t stream, uint64_t idx) {
+  return (float)(rng_bits(seed, stream, idx) >> 40) * (1.0f / 16777216.0f);  // [0,1)
+}
+__device__ __forceinline__ float rng_normal(uint64_t seed, uint64_t stream, uint64_t idx) {
+  uint64_t b = rng_bits(seed, stream, idx);
+  float u1 = ((float)(b >> 40) + 1.0f) * (1.0f / 16777217.0f);  // (0,1]
+  float u2 = (float)((b >> 16) & 0xFFFFFF) * (1.0f / 16777216.0f);
+  return sqrtf(-2.f * __logf(u1)) * __cosf(6.283185307179586f * u2);
+}
+// dropout keep test: keep iff u >= p
+__device__ __forceinline__ bool dropout_keep(uint64_t seed, uint64_t stream, uint64_t idx, float p) {
+  return rng_uniform(seed, stream, idx) >= p;
+}
+__device__ __forceinline__ uint64_t load_seed(const uint64_t* seed_ptr) { return seed_ptr ? *seed_ptr : 0ull; }
+
+// ---- wave64 reductions --------------------------------------------------------------------------
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// block-wide sum for blockDim.x multiple of 64 (<= 1024); `red` must hold >= 16 floats
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  float t = 0.f;
+  for (int i = 0; i < nw; ++i) t += red[i];
+  return t;
+}
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+}  // namespace kdfm

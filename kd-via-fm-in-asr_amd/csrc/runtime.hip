@@ -1,0 +1,86 @@
+// Library identity, error reporting and small reductions shared by all ops.
+#include <cstring>
+#include <string>
+
+#include "common.h"
+
+namespace kdfm {
+
+static thread_local std::string g_last_error;
+
+void set_error(const std::string& msg) { g_last_error = msg; }
+
+int check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error(std::string(what) + ": " + hipGetErrorString(e));
+    return KDFM_ELAUNCH;
+  }
+  return KDFM_OK;
+}
+
+namespace {
+// out[n] (+)= sum_{m<M} X[m*ld + n]; grid.x over column blocks of 64, grid.y splits M; atomics
+// combine the row slabs (bias gradients: N <= 1024, M up to ~2e5 rows).
+__global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ X, float* __restrict__ out,
+                                                     int64_t M, int64_t N, int64_t ld, int64_t rows_per) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t n = (int64_t)blockIdx.x * 64 + lane;
+  const int64_t mb = (int64_t)blockIdx.y * rows_per;
+  const int64_t me = (mb + rows_per < M) ? mb + rows_per : M;
+  float s = 0.f;
+  if (n < N)
+    for (int64_t m = mb + w; m < me; m += 4) s += X[m * ld + n];
+  red[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && n < N) atomicAdd(out + n, red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane]);
+}
+
+__global__ void zero_kernel(float* out, int64_t n) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = 0.f;
+}
+}  // namespace
+
+}  // namespace kdfm
+
+extern "C" {
+
+const char* kdfm_version(void) { return "kdfm 0.1.0 (gfx950)"; }
+
+const char* kdfm_last_error(void) { return kdfm::g_last_error.c_str(); }
+
+int kdfm_device_arch(char* buf, int64_t len) {
+  KDFM_REQUIRE(buf && len > 0, "null buffer");
+  int dev = 0;
+  hipDeviceProp_t prop;
+  if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) {
+    kdfm::set_error("kdfm_device_arch: no HIP device");
+    return KDFM_ELAUNCH;
+  }
+  std::strncpy(buf, prop.gcnArchName, (size_t)len - 1);
+  buf[len - 1] = 0;
+  return KDFM_OK;
+}
+
+int kdfm_colsum(const float* X, float* out, int64_t M, int64_t N, int64_t ld, int32_t accumulate, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(X && out, "null pointer");
+  KDFM_REQUIRE(M >= 0 && N >= 0 && ld >= N, "bad shape");
+  hipStream_t st = as_stream(stream);
+  if (!accumulate) {
+    hipLaunchKernelGGL(zero_kernel, dim3((unsigned)ceil_div(N, 256)), dim3(256), 0, st, out, N);
+    int rc = check_launch("kdfm_colsum(zero)");
+    if (rc) return rc;
+  }
+  if (M == 0 || N == 0) return KDFM_OK;
+  const int64_t gx = ceil_div(N, 64);
+  int64_t gy = ceil_div(M, 512);
+  if (gy > 1024) gy = 1024;
+  const int64_t rows_per = ceil_div(M, gy);
+  hipLaunchKernelGGL(colsum_kernel, dim3((unsigned)gx, (unsigned)gy), dim3(256), 0, st, X, out, M, N, ld, rows_per);
+  return check_launch("kdfm_colsum");
+}
+
+}  // extern "C"

@@ -1,0 +1,93 @@
+"""ctypes binding of libkdfm.so (include/kdfm.h).
+
+The library is loaded AFTER torch so that its DT_NEEDED libamdhip64.so.7 resolves to the HIP
+runtime torch already mapped (one runtime per process: torch streams are valid in our calls).
+There is no fallback: if the library is missing or fails to load, every op raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import torch  # noqa: F401  (must be imported first, see module docstring)
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libkdfm.so")
+
+KDFM_MATH_F32 = 0
+KDFM_MATH_BF16 = 1
+
+LD_KC, LD_XC, LD_CONV = 0, 1, 2
+
+EPI_BIAS = 1 << 0
+EPI_STORE_PRE = 1 << 1
+EPI_RELU = 1 << 2
+EPI_SILU = 1 << 3
+EPI_DROPOUT = 1 << 4
+EPI_DRELU = 1 << 5
+EPI_DSILU = 1 << 6
+EPI_RESID = 1 << 7
+EPI_BETA = 1 << 8
+EPI_ATOMIC = 1 << 9
+
+_i64 = C.c_int64
+_i32 = C.c_int32
+_f32 = C.c_float
+_vp = C.c_void_p
+
+
+class GemmDesc(C.Structure):
+    _fields_ = [
+        ("A", _vp), ("B", _vp), ("C", _vp), ("bias", _vp), ("R", _vp), ("aux", _vp), ("Cpre", _vp),
+        ("M", _i64), ("N", _i64), ("K", _i64),
+        ("sAm", _i64), ("sAk", _i64), ("sBk", _i64), ("sBn", _i64), ("sCm", _i64), ("sCn", _i64),
+        ("batch1", _i64), ("batch2", _i64),
+        ("bA1", _i64), ("bA2", _i64), ("bB1", _i64), ("bB2", _i64), ("bC1", _i64), ("bC2", _i64),
+        ("alpha", _f32), ("beta", _f32), ("rscale", _f32), ("dropout_p", _f32),
+        ("seed", _vp), ("rng_stream", C.c_uint64),
+        ("amode", _i32), ("bmode", _i32), ("epi", _i32), ("math", _i32),
+        ("splitk", _i32),
+        ("conv_taps", _i32), ("conv_pad", _i32),
+        ("conv_c", _i64), ("conv_t", _i64),
+    ]
+
+
+# Every symbol include/kdfm.h declares, with its ctypes signature.  tests/test_abi.py checks this
+# table against the header so the two cannot drift.
+P = _vp
+SIGNATURES: dict[str, tuple] = {
+    "kdfm_version": (C.c_char_p, []),
+    "kdfm_last_error": (C.c_char_p, []),
+    "kdfm_device_arch": (_i32, [C.c_char_p, _i64]),
+    "kdfm_gemm": (_i32, [C.POINTER(GemmDesc), P]),
+    "kdfm_colsum": (_i32, [P, P, _i64, _i64, _i64, _i32, P]),
+}
+
+_LIB = None
+
+
+class KdfmError(RuntimeError):
+    pass
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise KdfmError(f"libkdfm.so not built ({LIB_PATH}); run __graft_entry__.build()")
+        h = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(h, name)
+            fn.restype = res
+            fn.argtypes = args
+        _LIB = h
+    return _LIB
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = lib().kdfm_last_error().decode(errors="replace")
+        raise KdfmError(f"{what} failed (status {rc}): {msg}")
+
+
+def call(name: str, *args) -> None:
+    check(getattr(lib(), name)(*args), name)
