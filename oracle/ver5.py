@@ -1,0 +1,500 @@
+"""ORACLE — CPU restatement of the ver5 flow-matching distillation training step.
+
+TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg
+may import this module, and only as the checker / CPU baseline; the product path
+(kd-via-fm-in-asr_amd/kdfm) never imports it.
+
+What it restates (reference = /root/reference, snapshot 2025-09-19):
+  * KD heads — literal re-expression of asr_train_diffm.py:400-497 (TeacherAutoEncoder,
+    StudentProjector, NoiseAdapter, SimpleDenoiser, FMLatent), :852-856 (rectified schedule
+    derivative) and :1270-1427 (FlowMatchingModule, meta_encoder 'mlp', shape_transform 'linear').
+    PINNED: tests/test_oracle_golden.py compares it with vectors produced by the reference's own
+    classes (tests/golden/make_golden.py, AST-extracted in the survey container).
+  * The step — DistilFlowMatchingCTCModelBPE.forward/_compute_v_losses_one_layer/training_step
+    (asr_train_diffm.py:606-643, 645-729 [ver5 697-702], 731-828): CTC + 0.1*KL(T=1) +
+    sum_16(recon) + sum_16(fm_post).
+  * NeMo modules whose sources are present: AudioToMelSpectrogramPreprocessor
+    (NeMo/.../modules/audio_preprocessing.py:214-300), ConformerEncoder orchestration
+    (conformer_encoder.py:549-850), ConvASRDecoder (conv_asr.py:445-468), CTCLoss
+    (losses/ctc.py:25-82, mean_batch + zero_infinity from ctc_models.py:81-85).
+  * NeMo leaf modules whose sources are ABSENT (asr/parts/**):
+    FilterbankFeatures, ConvSubsampling, RelPositionalEncoding, ConformerLayer and its
+    sub-modules.  Restated from the Appendix A contract; pinned only by the invariants of
+    NeMo/tests (seq_len = L // hop, zero constant STFT padding); absolute values are
+    "parity unpinned" beyond the build's own fixtures.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from .mel import mel_filterbank
+
+
+@dataclass
+class StepConfig:
+    n_layers: int = 16
+    d_student: int = 88
+    heads_student: int = 2
+    d_teacher: int = 176
+    heads_teacher: int = 4
+    latent: int = 96
+    vocab: int = 128            # BPE vocabulary; decoder has vocab + 1 classes (blank = vocab)
+    conv_kernel: int = 31
+    ff_expansion: int = 4
+    sample_rate: int = 16000
+    n_fft: int = 512
+    win: int = 400
+    hop: int = 160
+    nfilt: int = 80
+    preemph: float = 0.97
+    dither: float = 1e-5
+    fm_steps: int = 8
+    denoiser_steps: int = 9
+    time_embed_dim: int = 32
+    kd_alpha: float = 0.1
+    kd_temperature: float = 1.0
+    subsampling_mask: bool = True
+    bn_momentum: float = 0.1
+    ln_eps: float = 1e-5
+    bn_eps: float = 1e-5
+
+
+# ------------------------------------------------------------------------------------------
+# Parameter initialisation (NeMo state-dict key names)
+# ------------------------------------------------------------------------------------------
+
+def _lin(g, n_out, n_in, bias=True, scale=None):
+    s = scale if scale is not None else 1.0 / math.sqrt(n_in)
+    w = (torch.rand(n_out, n_in, generator=g) * 2 - 1) * s
+    b = (torch.rand(n_out, generator=g) * 2 - 1) * s if bias else None
+    return w, b
+
+
+def encoder_param_shapes(cfg: StepConfig, d: int, h: int) -> dict:
+    dk = d // h
+    C = d
+    shapes = {
+        "pre_encode.conv.0.weight": (C, 1, 3, 3), "pre_encode.conv.0.bias": (C,),
+        "pre_encode.conv.2.weight": (C, C, 3, 3), "pre_encode.conv.2.bias": (C,),
+        "pre_encode.out.weight": (d, C * (cfg.nfilt // 4)), "pre_encode.out.bias": (d,),
+    }
+    ff = cfg.ff_expansion * d
+    for i in range(cfg.n_layers):
+        L = f"layers.{i}."
+        for n in ("norm_feed_forward1", "norm_self_att", "norm_conv", "norm_feed_forward2", "norm_out"):
+            shapes[L + n + ".weight"] = (d,)
+            shapes[L + n + ".bias"] = (d,)
+        for f in ("feed_forward1", "feed_forward2"):
+            shapes[L + f + ".linear1.weight"] = (ff, d)
+            shapes[L + f + ".linear1.bias"] = (ff,)
+            shapes[L + f + ".linear2.weight"] = (d, ff)
+            shapes[L + f + ".linear2.bias"] = (d,)
+        for q in ("linear_q", "linear_k", "linear_v", "linear_out"):
+            shapes[L + f"self_attn.{q}.weight"] = (d, d)
+            shapes[L + f"self_attn.{q}.bias"] = (d,)
+        shapes[L + "self_attn.linear_pos.weight"] = (d, d)
+        shapes[L + "self_attn.pos_bias_u"] = (h, dk)
+        shapes[L + "self_attn.pos_bias_v"] = (h, dk)
+        shapes[L + "conv.pointwise_conv1.weight"] = (2 * d, d, 1)
+        shapes[L + "conv.pointwise_conv1.bias"] = (2 * d,)
+        shapes[L + "conv.depthwise_conv.weight"] = (d, 1, cfg.conv_kernel)
+        shapes[L + "conv.depthwise_conv.bias"] = (d,)
+        shapes[L + "conv.batch_norm.weight"] = (d,)
+        shapes[L + "conv.batch_norm.bias"] = (d,)
+        shapes[L + "conv.pointwise_conv2.weight"] = (d, d, 1)
+        shapes[L + "conv.pointwise_conv2.bias"] = (d,)
+    return shapes
+
+
+def init_encoder(cfg: StepConfig, d: int, h: int, seed: int, prefix: str = "encoder.") -> dict:
+    g = torch.Generator().manual_seed(seed)
+    out = {}
+    for name, shp in encoder_param_shapes(cfg, d, h).items():
+        if name.endswith("norm_feed_forward1.weight") or ".norm_" in name and name.endswith(".weight"):
+            t = 1.0 + 0.1 * (torch.rand(shp, generator=g) * 2 - 1)
+        elif "batch_norm.weight" in name:
+            t = 1.0 + 0.1 * (torch.rand(shp, generator=g) * 2 - 1)
+        elif "pos_bias" in name:
+            t = 0.1 * torch.randn(shp, generator=g)
+        else:
+            fan_in = int(np.prod(shp[1:])) if len(shp) > 1 else shp[0]
+            s = 1.0 / math.sqrt(max(1, fan_in))
+            t = (torch.rand(shp, generator=g) * 2 - 1) * s
+        out[prefix + name] = t.float()
+    n_bn = [k for k in out if k.endswith("batch_norm.weight")]
+    for k in n_bn:
+        base = k[: -len("weight")]
+        dd = out[k].shape[0]
+        out[base + "running_mean"] = 0.1 * torch.randn(dd, generator=g)
+        out[base + "running_var"] = 1.0 + 0.2 * torch.rand(dd, generator=g)
+        out[base + "num_batches_tracked"] = torch.zeros((), dtype=torch.int64)
+    return out
+
+
+def init_decoder(cfg: StepConfig, d: int, seed: int, prefix: str = "decoder.") -> dict:
+    g = torch.Generator().manual_seed(seed)
+    w, b = _lin(g, cfg.vocab + 1, d)
+    return {prefix + "decoder_layers.0.weight": w.unsqueeze(-1), prefix + "decoder_layers.0.bias": b}
+
+
+def init_heads(cfg: StepConfig, seed: int) -> dict:
+    """ver5 head parameters with the reference's module names (asr_train_diffm.py:559-564)."""
+    g = torch.Generator().manual_seed(seed)
+    L, Ct, Cs, E = cfg.latent, cfg.d_teacher, cfg.d_student, cfg.time_embed_dim
+    p = {}
+
+    def conv(name, cout, cin, k):
+        w, b = _lin(g, cout, cin * k)
+        p[name + ".weight"] = w.view(cout, cin, k)
+        p[name + ".bias"] = b
+
+    conv("tae.enc", L, Ct, 1)
+    conv("tae.dec", Ct, L, 1)
+    conv("sproj.proj", L, Cs, 1)
+    conv("adapter.gamma_head.0", L, L, 1)
+    conv("adapter.gamma_head.2", 1, L, 1)
+    conv("denoiser.net.0", L, L, 3)
+    conv("denoiser.net.2", L, L, 3)
+    for fm in ("fm_latent.fm.", "fm_latent_2.fm."):
+        w, b = _lin(g, E, 1)
+        p[fm + "time_embed.weight"], p[fm + "time_embed.bias"] = w, b
+        w, b = _lin(g, L, L + E)
+        p[fm + "meta_encoder.0.weight"], p[fm + "meta_encoder.0.bias"] = w, b
+        w, b = _lin(g, L, L)
+        p[fm + "meta_encoder.2.weight"], p[fm + "meta_encoder.2.bias"] = w, b
+        w, b = _lin(g, L, L)
+        p[fm + "shape_transformation_function.weight"] = w
+        p[fm + "shape_transformation_function.bias"] = b
+    return p
+
+
+def frontend_buffers(cfg: StepConfig, prefix: str = "preprocessor.featurizer.") -> dict:
+    return {
+        prefix + "window": torch.hann_window(cfg.win, periodic=False),
+        prefix + "fb": torch.tensor(mel_filterbank(cfg.sample_rate, cfg.n_fft, cfg.nfilt, 0.0,
+                                                   cfg.sample_rate / 2)).unsqueeze(0),
+    }
+
+
+def init_all(cfg: StepConfig, teacher_seed=0, student_seed=1, heads_seed=2) -> dict:
+    p = {}
+    p.update(frontend_buffers(cfg))
+    p.update(init_encoder(cfg, cfg.d_student, cfg.heads_student, student_seed))
+    p.update(init_decoder(cfg, cfg.d_student, student_seed + 100))
+    p.update(init_heads(cfg, heads_seed))
+    p.update(frontend_buffers(cfg, "teacher.preprocessor.featurizer."))
+    p.update(init_encoder(cfg, cfg.d_teacher, cfg.heads_teacher, teacher_seed, "teacher.encoder."))
+    p.update(init_decoder(cfg, cfg.d_teacher, teacher_seed + 100, "teacher.decoder."))
+    return p
+
+
+# ------------------------------------------------------------------------------------------
+# Frontend (Appendix A.1; NeMo audio_preprocessing.py:93-103, 214-300)
+# ------------------------------------------------------------------------------------------
+
+def preprocess(wav, lengths, window, fb, cfg: StepConfig, dither_noise=None):
+    seq_len = torch.div(lengths, cfg.hop, rounding_mode="floor")      # pinned: frames - 1
+    x = wav.float()
+    if dither_noise is not None:
+        x = x + cfg.dither * dither_noise
+    timemask = torch.arange(x.shape[1]).unsqueeze(0) < lengths.unsqueeze(1)
+    x = torch.cat((x[:, :1], x[:, 1:] - cfg.preemph * x[:, :-1]), dim=1)
+    x = x.masked_fill(~timemask, 0.0)
+    X = torch.stft(x, n_fft=cfg.n_fft, hop_length=cfg.hop, win_length=cfg.win, window=window, center=True,
+                   pad_mode="constant", return_complex=True)
+    X = torch.view_as_real(X)
+    x = torch.sqrt(X.pow(2).sum(-1))
+    x = x.pow(2.0)
+    x = torch.matmul(fb.to(x.dtype), x)
+    x = torch.log(x + 2 ** -24)
+    # normalize_batch(per_feature): mean/std over valid frames, (n-1) denominator, std += 1e-5
+    B, _, T = x.shape
+    valid = torch.arange(T).unsqueeze(0).expand(B, T) < seq_len.unsqueeze(1)
+    num = torch.where(valid.unsqueeze(1), x, 0.0).sum(2)
+    den = valid.sum(1)
+    mean = num / den.unsqueeze(1)
+    std = torch.sqrt(torch.sum(torch.where(valid.unsqueeze(1), x - mean.unsqueeze(2), 0.0) ** 2, 2)
+                     / (den.unsqueeze(1) - 1.0))
+    std = std.masked_fill(std.isnan(), 0.0) + 1e-5
+    x = (x - mean.unsqueeze(2)) / std.unsqueeze(2)
+    mask = torch.arange(T).repeat(B, 1) >= seq_len.unsqueeze(1)
+    x = x.masked_fill(mask.unsqueeze(1), 0.0)
+    return x, seq_len
+
+
+# ------------------------------------------------------------------------------------------
+# Encoder (conformer_encoder.py:549-850 + Appendix A.3-A.8)
+# ------------------------------------------------------------------------------------------
+
+def _conv_len(l):
+    return torch.floor((l.float() - 1.0) / 2.0 + 1.0).long()
+
+
+def _time_mask(x, lengths, tdim):
+    T = x.shape[tdim]
+    m = torch.arange(T).unsqueeze(0) < lengths.unsqueeze(1)   # (B,T)
+    shape = [x.shape[0]] + [1] * (x.dim() - 1)
+    shape[tdim] = T
+    return x * m.view(shape).to(x.dtype)
+
+
+def subsampling(x_btf, lengths, p, pre, cfg: StepConfig):
+    """ConvSubsampling 'striding' factor 4 (A.3)."""
+    x = x_btf.unsqueeze(1)                         # (B,1,T,F)
+    l1 = _conv_len(lengths)
+    l2 = _conv_len(l1)
+    if cfg.subsampling_mask:
+        x = _time_mask(x, lengths, 2)
+    x = F.relu(F.conv2d(x, p[pre + "conv.0.weight"], p[pre + "conv.0.bias"], stride=2, padding=1))
+    if cfg.subsampling_mask:
+        x = _time_mask(x, l1, 2)
+    x = F.relu(F.conv2d(x, p[pre + "conv.2.weight"], p[pre + "conv.2.bias"], stride=2, padding=1))
+    if cfg.subsampling_mask:
+        x = _time_mask(x, l2, 2)
+    b, c, t, f = x.shape
+    x = x.transpose(1, 2).reshape(b, t, c * f)
+    x = F.linear(x, p[pre + "out.weight"], p[pre + "out.bias"])
+    return x, l2
+
+
+def rel_pos_emb(T, d):
+    """RelPositionalEncoding (A.4): sinusoids for relative positions T-1 ... -(T-1)."""
+    pos = torch.arange(T - 1, -T, -1, dtype=torch.float32).unsqueeze(1)
+    div = torch.exp(torch.arange(0, d, 2, dtype=torch.float32) * -(math.log(10000.0) / d))
+    pe = torch.zeros(pos.shape[0], d)
+    pe[:, 0::2] = torch.sin(pos * div)
+    pe[:, 1::2] = torch.cos(pos * div)
+    return pe.unsqueeze(0)
+
+
+def rel_shift(x):
+    """NeMo RelPositionMultiHeadAttention.rel_shift (A.7), literal pad/view form."""
+    b, h, qlen, pos_len = x.size()
+    x = F.pad(x, pad=(1, 0))
+    x = x.view(b, h, -1, qlen)
+    x = x[:, :, 1:].view(b, h, qlen, pos_len)
+    return x
+
+
+def rel_mha(x, pos_emb, att_mask, p, L, h):
+    B, T, d = x.shape
+    dk = d // h
+    q = F.linear(x, p[L + "linear_q.weight"], p[L + "linear_q.bias"]).view(B, T, h, dk)
+    k = F.linear(x, p[L + "linear_k.weight"], p[L + "linear_k.bias"]).view(B, T, h, dk).transpose(1, 2)
+    v = F.linear(x, p[L + "linear_v.weight"], p[L + "linear_v.bias"]).view(B, T, h, dk).transpose(1, 2)
+    pp = F.linear(pos_emb, p[L + "linear_pos.weight"]).view(1, -1, h, dk).transpose(1, 2)
+    qu = (q + p[L + "pos_bias_u"]).transpose(1, 2)
+    qv = (q + p[L + "pos_bias_v"]).transpose(1, 2)
+    bd = rel_shift(torch.matmul(qv, pp.transpose(-2, -1)))
+    ac = torch.matmul(qu, k.transpose(-2, -1))
+    bd = bd[:, :, :, : ac.size(-1)]
+    scores = (ac + bd) / math.sqrt(dk)
+    m = att_mask.unsqueeze(1)
+    scores = scores.masked_fill(m, -10000.0)
+    attn = torch.softmax(scores, dim=-1).masked_fill(m, 0.0)
+    o = torch.matmul(attn, v).transpose(1, 2).reshape(B, T, d)
+    return F.linear(o, p[L + "linear_out.weight"], p[L + "linear_out.bias"])
+
+
+def ffn(x, p, L):
+    h = F.silu(F.linear(x, p[L + "linear1.weight"], p[L + "linear1.bias"]))
+    return F.linear(h, p[L + "linear2.weight"], p[L + "linear2.bias"])
+
+
+def conv_module(x, pad_mask, p, L, training, bn_state, cfg: StepConfig):
+    x = x.transpose(1, 2)
+    x = F.conv1d(x, p[L + "pointwise_conv1.weight"], p[L + "pointwise_conv1.bias"])
+    x = F.glu(x, dim=1)
+    x = x.masked_fill(pad_mask.unsqueeze(1), 0.0)
+    d = x.shape[1]
+    x = F.conv1d(x, p[L + "depthwise_conv.weight"], p[L + "depthwise_conv.bias"],
+                 padding=(cfg.conv_kernel - 1) // 2, groups=d)
+    rm, rv = bn_state[L + "batch_norm.running_mean"], bn_state[L + "batch_norm.running_var"]
+    x = F.batch_norm(x, rm, rv, p[L + "batch_norm.weight"], p[L + "batch_norm.bias"], training=training,
+                     momentum=cfg.bn_momentum, eps=cfg.bn_eps)
+    x = F.silu(x)
+    x = F.conv1d(x, p[L + "pointwise_conv2.weight"], p[L + "pointwise_conv2.bias"])
+    return x.transpose(1, 2)
+
+
+def conformer_layer(x, pos_emb, att_mask, pad_mask, p, L, h, training, bn_state, cfg: StepConfig):
+    def ln(t, n):
+        return F.layer_norm(t, (t.shape[-1],), p[L + n + ".weight"], p[L + n + ".bias"], cfg.ln_eps)
+
+    r = x + 0.5 * ffn(ln(x, "norm_feed_forward1"), p, L + "feed_forward1.")
+    r = r + rel_mha(ln(r, "norm_self_att"), pos_emb, att_mask, p, L + "self_attn.", h)
+    r = r + conv_module(ln(r, "norm_conv"), pad_mask, p, L + "conv.", training, bn_state, cfg)
+    r = r + 0.5 * ffn(ln(r, "norm_feed_forward2"), p, L + "feed_forward2.")
+    return ln(r, "norm_out")
+
+
+def encoder(mel, lengths, p, prefix, d, h, cfg: StepConfig, training, bn_state):
+    """ConformerEncoder.forward -> (B,d,T') , lengths, [per-layer outputs (B,T',d)]"""
+    x = mel.transpose(1, 2)
+    x, length = subsampling(x, lengths, p, prefix + "pre_encode.", cfg)
+    B, T, _ = x.shape
+    x = x * math.sqrt(d)
+    pos_emb = rel_pos_emb(T, d)
+    valid = torch.arange(T).expand(B, T) < length.unsqueeze(1)
+    att_ok = valid.unsqueeze(1).repeat(1, T, 1)
+    att_ok = att_ok & att_ok.transpose(1, 2)
+    att_mask = ~att_ok
+    pad_mask = ~valid
+    feats = []
+    for i in range(cfg.n_layers):
+        x = conformer_layer(x, pos_emb, att_mask, pad_mask, p, prefix + f"layers.{i}.", h, training, bn_state, cfg)
+        feats.append(x)
+    return x.transpose(1, 2), length, feats
+
+
+def decoder(enc_bdt, p, prefix):
+    logits = F.conv1d(enc_bdt, p[prefix + "decoder_layers.0.weight"], p[prefix + "decoder_layers.0.bias"])
+    return F.log_softmax(logits.transpose(1, 2), dim=-1)
+
+
+def ctc_loss_mean_batch(log_probs, targets, input_lengths, target_lengths, blank):
+    loss = F.ctc_loss(log_probs.transpose(0, 1), targets.long(), input_lengths.long(), target_lengths.long(),
+                      blank=blank, reduction="none", zero_infinity=True)
+    return loss.mean()
+
+
+# ------------------------------------------------------------------------------------------
+# KD heads (asr_train_diffm.py:400-497, 852-856, 1270-1427) — layout (B,C,T) as the reference
+# ------------------------------------------------------------------------------------------
+
+def _c1(x, p, name, padding=0):
+    return F.conv1d(x, p[name + ".weight"], p[name + ".bias"], padding=padding)
+
+
+def tae(t_bct, p):
+    z = _c1(t_bct, p, "tae.enc")
+    return z, _c1(z, p, "tae.dec")
+
+
+def sproj(s_bct, p):
+    return _c1(s_bct, p, "sproj.proj")
+
+
+def noise_adapter(z, p, eps):
+    g = torch.sigmoid(_c1(F.relu(_c1(z, p, "adapter.gamma_head.0")), p, "adapter.gamma_head.2"))
+    return g * z + (1.0 - g) * eps, g
+
+
+def denoiser(z, p, steps):
+    x = z
+    for _ in range(steps):
+        pred = _c1(F.relu(_c1(x, p, "denoiser.net.0", 1)), p, "denoiser.net.2", 1)
+        x = x - pred / steps
+    return x
+
+
+def fm_latent(s_bct, t_bct, p, steps, prefix="fm_latent.fm."):
+    """FMLatent.forward -> FlowMatchingModule.forward (training, rectified, mlp, linear)."""
+    s_f = s_bct.transpose(1, 2)
+    t_f = t_bct.transpose(1, 2)
+    x = s_f
+    velocity = None
+    t = None
+    for i in range(steps, 0, -1):
+        t = torch.full((s_f.size(0), s_f.size(1), 1), i / steps)
+        e = F.linear(t, p[prefix + "time_embed.weight"], p[prefix + "time_embed.bias"])
+        h = F.relu(F.linear(torch.cat([x, e], dim=-1), p[prefix + "meta_encoder.0.weight"],
+                            p[prefix + "meta_encoder.0.bias"]))
+        velocity = F.linear(h, p[prefix + "meta_encoder.2.weight"], p[prefix + "meta_encoder.2.bias"])
+        x = x - velocity / steps
+    dalpha, dsigma = torch.ones_like(t), -torch.ones_like(t)        # rectified_flow_schedule_deriv
+    nsx = (dalpha * s_f - velocity) / (-dsigma)
+    tr = F.linear(nsx, p[prefix + "shape_transformation_function.weight"],
+                  p[prefix + "shape_transformation_function.bias"])
+    return F.mse_loss(tr, t_f), x.transpose(1, 2)
+
+
+def ver5_layer_losses(s_btd, t_btd, p, eps, cfg: StepConfig):
+    """_compute_v_losses_one_layer, version 5 (asr_train_diffm.py:645-702)."""
+    s = s_btd.transpose(1, 2)
+    t = t_btd.transpose(1, 2)
+    z_t, rec = tae(t, p)
+    z_t = z_t.detach()
+    recon = F.mse_loss(rec, t)
+    z_s = sproj(s, p)
+    z_noisy, _ = noise_adapter(z_s, p, eps)
+    z_deno = denoiser(z_noisy, p, cfg.denoiser_steps)
+    fm, _ = fm_latent(z_deno, z_t, p, cfg.fm_steps)
+    return recon, fm
+
+
+# ------------------------------------------------------------------------------------------
+# The whole step
+# ------------------------------------------------------------------------------------------
+
+def ver5_step(p, wav, wav_len, targets, target_len, cfg: StepConfig, eps, spec_mask=None,
+              student_train=True, bn_state=None):
+    """Forward of one ver5 training step; returns dict of losses and intermediates.
+
+    eps: (n_layers, B, latent, T') NoiseAdapter noise (injected; the reference draws randn_like).
+    spec_mask: optional (B, nfilt, T_mel) bool SpecAugment mask (True = masked to 0).
+    bn_state: dict of running stats (cloned, updated in place for the student).
+    """
+    if bn_state is None:
+        bn_state = {k: v.clone() for k, v in p.items() if "running_" in k}
+    mel, mel_len = preprocess(wav, wav_len, p["preprocessor.featurizer.window"],
+                              p["preprocessor.featurizer.fb"][0], cfg)
+    mel_s = mel.masked_fill(spec_mask, 0.0) if spec_mask is not None else mel
+    enc, enc_len, s_feats = encoder(mel_s, mel_len, p, "encoder.", cfg.d_student, cfg.heads_student, cfg,
+                                    student_train, bn_state)
+    with torch.no_grad():
+        mel_t, mel_t_len = preprocess(wav, wav_len, p["teacher.preprocessor.featurizer.window"],
+                                      p["teacher.preprocessor.featurizer.fb"][0], cfg)
+        _, _, t_feats = encoder(mel_t, mel_t_len, p, "teacher.encoder.", cfg.d_teacher, cfg.heads_teacher, cfg,
+                                False, bn_state)
+    log_probs = decoder(enc, p, "decoder.")
+    ctc = ctc_loss_mean_batch(log_probs, targets, enc_len, target_len, cfg.vocab)
+    with torch.no_grad():
+        tch_logp = decoder(t_feats[-1].permute(0, 2, 1), p, "teacher.decoder.")
+        tch_p = F.softmax(tch_logp / cfg.kd_temperature, dim=-1)
+    stu_logp = F.log_softmax(log_probs / cfg.kd_temperature, dim=-1)
+    kl = F.kl_div(stu_logp, tch_p, reduction="batchmean") * cfg.kd_temperature ** 2
+    recon_sum = torch.zeros(())
+    fm_sum = torch.zeros(())
+    for i, (s, t) in enumerate(zip(s_feats, t_feats)):
+        r, f = ver5_layer_losses(s, t, p, eps[i], cfg)
+        recon_sum = recon_sum + r
+        fm_sum = fm_sum + f
+    total = ctc + cfg.kd_alpha * kl + recon_sum + fm_sum
+    return {"loss": total, "ctc": ctc, "kl": kl, "recon": recon_sum, "fm": fm_sum, "log_probs": log_probs,
+            "enc_len": enc_len, "mel": mel, "mel_len": mel_len, "s_feats": s_feats, "t_feats": t_feats,
+            "bn_state": bn_state}
+
+
+def trainable_names(p: dict) -> list:
+    """Names of the parameters the step trains (teacher frozen; buffers/running stats excluded;
+    fm_latent_2 is unused by ver5 and so receives no gradient)."""
+    out = []
+    for k, v in p.items():
+        if k.startswith("teacher.") or k.startswith("preprocessor.") or "running_" in k or "num_batches" in k:
+            continue
+        if k.startswith("fm_latent_2."):
+            continue
+        out.append(k)
+    return out
+
+
+def greedy_ctc(log_probs, lengths, blank):
+    """CTC greedy decode ids (A.9): argmax, collapse repeats, drop blank."""
+    out = []
+    am = log_probs.argmax(-1)
+    for b in range(am.shape[0]):
+        prev = -1
+        seq = []
+        for t in range(int(lengths[b])):
+            c = int(am[b, t])
+            if c != prev and c != blank:
+                seq.append(c)
+            prev = c
+        out.append(seq)
+    return out
