@@ -70,7 +70,9 @@ enum {
   KDFM_EPI_DSILU = 1 << 6,     /* *= silu'(aux)                                         */
   KDFM_EPI_RESID = 1 << 7,     /* value = R + rscale*value   (R laid out like C)        */
   KDFM_EPI_BETA = 1 << 8,      /* value += beta*C_old                                   */
-  KDFM_EPI_ATOMIC = 1 << 9     /* atomicAdd into C (split-K reductions; no other epi)   */
+  KDFM_EPI_ATOMIC = 1 << 9,    /* atomicAdd into C (split-K reductions; no other epi)   */
+  KDFM_EPI_ROWMASK = 1 << 10,  /* value = 0 on padded frames (see mask_len below)       */
+  KDFM_EPI_MSE = 1 << 11       /* diff = value - R; C = rscale*diff; *loss_acc += loss_scale*diff^2 */
 };
 
 typedef struct kdfm_gemm_desc {
@@ -92,14 +94,135 @@ typedef struct kdfm_gemm_desc {
   int32_t splitk;
   int32_t conv_taps, conv_pad;
   int64_t conv_c, conv_t;
+  /* EPI_ROWMASK: row m is frame t = (m / mask_div) % mask_T of utterance u = m / (mask_div*mask_T);
+   * the value is zeroed when t >= mask_len[u] (NeMo pad_mask semantics). */
+  const int64_t* mask_len;
+  int64_t mask_T, mask_div;
+  /* EPI_MSE accumulator (device scalar) */
+  float* loss_acc;
+  float loss_scale;
 } kdfm_gemm_desc;
 
 int kdfm_gemm(const kdfm_gemm_desc* d, void* stream);
 
-/* column sums: out[n] (+)= sum_m X[m*ld + n], m < M; accumulate != 0 adds into out.
+/* column sums: out[n] (+)= scale * sum_m X[m*ld + n], m < M; accumulate != 0 adds into out.
  * (bias gradients of every Linear / Conv1d on the path) */
-int kdfm_colsum(const float* X, float* out, int64_t M, int64_t N, int64_t ld, int32_t accumulate,
+int kdfm_colsum(const float* X, float* out, int64_t M, int64_t N, int64_t ld, float scale, int32_t accumulate,
                 void* stream);
+
+/* ---------------- frontend: AudioToMelSpectrogramPreprocessor (audio_preprocessing.py:214-300,
+ * FilterbankFeatures semantics SURVEY Appendix A.1) --------------------------------------- */
+/* xp (B, N + 2*pad): zero-centre-padded preemphasised signal, masked beyond lengths[b];
+ * optional dither (training) from the counter RNG. */
+int kdfm_preemph_pad(const float* wav, const int64_t* lengths, float* xp, int64_t B, int64_t N, int64_t pad,
+                     float preemph, float dither, const uint64_t* seed, uint64_t rng_stream, void* stream);
+/* power[r, f] = spec[r, f]^2 + spec[r, nbins + f]^2 (spec rows = [re | im] from the DFT GEMM) */
+int kdfm_power_spectrum(const float* spec, float* power, int64_t rows, int64_t nbins, void* stream);
+/* log(mel + guard), per-feature mean / unbiased std over valid frames, zero beyond seq_len;
+ * mel/out laid out (B, T, nfilt). */
+int kdfm_logmel_normalize(const float* mel, const int64_t* seq_len, float* out, int64_t B, int64_t T, int64_t nfilt,
+                          float log_guard, void* stream);
+/* SpectrogramAugmentation (audio_preprocessing.py:443-553, called asr_train_diffm.py:622-623),
+ * in place on (B, T, nfilt); mask_out (optional, uint8) records the masked cells. */
+int kdfm_specaugment(float* x, const int64_t* seq_len, uint8_t* mask_out, int64_t B, int64_t T, int64_t nfilt,
+                     int32_t freq_masks, int32_t freq_width, int32_t time_masks, float time_width,
+                     const uint64_t* seed, uint64_t rng_stream, void* stream);
+
+/* ---------------- ConvSubsampling 'striding' (conformer_encoder.py:381-390, 635; A.3) ------- */
+/* cols[(b,t2,f2), c*9 + ky*3 + kx] = X[b, 2t2-1+ky, 2f2-1+kx, c] ; X channels-last (B,T1,F1,C),
+ * frames >= len_in[b] read as zero (padding mask). */
+int kdfm_im2col_3x3s2(const float* X, const int64_t* len_in, float* cols, int64_t B, int64_t T1, int64_t F1,
+                      int64_t C, void* stream);
+/* adjoint of the above (gather form); optionally multiplied by relu'(relu_out). */
+int kdfm_col2im_3x3s2(const float* dcols, const int64_t* len_in, const float* relu_out, float* dX, int64_t B,
+                      int64_t T1, int64_t F1, int64_t C, void* stream);
+
+/* ---------------- ConformerLayer (Appendix A.5-A.8; layers built conformer_encoder.py:450-472) */
+int kdfm_layernorm_fwd(const float* x, const float* gamma, const float* beta, float* y, float* mean, float* rstd,
+                       int64_t rows, int64_t d, float eps, void* stream);
+/* dx = LN'(dy) (+ dres if non-null); dgamma/dbeta accumulate (+=). */
+int kdfm_layernorm_bwd(const float* dy, const float* x, const float* gamma, const float* mean, const float* rstd,
+                       const float* dres, float* dx, float* dgamma, float* dbeta, int64_t rows, int64_t d,
+                       void* stream);
+/* Qu = Q + pos_bias_u, Qv = Q + pos_bias_v from the fused (rows, 3d) q|k|v projection */
+int kdfm_qkv_prep(const float* qkv, const float* pos_bias_u, const float* pos_bias_v, float* qu, float* qv,
+                  int64_t rows, int64_t d, void* stream);
+/* softmax((AC + rel_shift(BD)) * scale) with NeMo masking, optional dropout_att -> Pdrop */
+int kdfm_relpos_softmax_fwd(const float* ac, const float* bd, const int64_t* lengths, float* P, float* Pdrop,
+                            int64_t B, int64_t H, int64_t T, float scale, float dropout_p, const uint64_t* seed,
+                            uint64_t rng_stream, void* stream);
+int kdfm_relpos_softmax_bwd(const float* P, const float* dPdrop, float* dAC, float* dBD, int64_t B, int64_t H,
+                            int64_t T, float scale, float dropout_p, const uint64_t* seed, uint64_t rng_stream,
+                            void* stream);
+/* sinusoidal table for relative positions T-1 ... -(T-1), (2T-1, d) */
+int kdfm_relpos_table(float* pe, int64_t T, int64_t d, void* stream);
+/* conv module: GLU over channels + pad mask; depthwise conv (k odd) with optional f64 BN stats */
+int kdfm_glu_mask_fwd(const float* a, const int64_t* lengths, float* g, int64_t B, int64_t T, int64_t d,
+                      void* stream);
+int kdfm_glu_mask_bwd(const float* dg, const float* a, const int64_t* lengths, float* da, int64_t B, int64_t T,
+                      int64_t d, void* stream);
+int kdfm_dwconv_fwd(const float* g, const float* w, const float* bias, float* y, double* stats, int64_t B, int64_t T,
+                    int64_t d, int64_t K, void* stream);
+/* dg = conv^T(dy); dw, db accumulate (+=) */
+int kdfm_dwconv_bwd(const float* dy, const float* g, const float* w, float* dg, float* dw, float* db, int64_t B,
+                    int64_t T, int64_t d, int64_t K, void* stream);
+int kdfm_bn_finalize(const double* stats, const float* running_mean, const float* running_var, float* mean,
+                     float* rstd, int64_t d, int64_t count, float eps, void* stream);
+int kdfm_bn_running_update(float* running_mean, float* running_var, const double* stats, int64_t d, int64_t count,
+                           float momentum, void* stream);
+int kdfm_bn_silu_fwd(const float* y, const float* mean, const float* rstd, const float* gamma, const float* beta,
+                     float* z, int64_t rows, int64_t d, void* stream);
+int kdfm_bn_silu_bwd(const float* dz, const float* y, const float* mean, const float* rstd, const float* gamma,
+                     const float* beta, double* red_ws, float* dy, float* dgamma, float* dbeta, int64_t rows,
+                     int64_t d, int32_t batch_stats, void* stream);
+
+/* ---------------- decoder / losses (conv_asr.py:456-468; losses/ctc.py:68-82; asr_train_diffm.py:740-811) */
+int kdfm_log_softmax(const float* x, float* y, int64_t rows, int64_t C, int64_t ldx, int64_t ldy, void* stream);
+/* per-utterance CTC NLL and d(grad_scale * nll)/dlogits = grad_scale*(exp(lp) - posterior) */
+int kdfm_ctc_loss(const float* log_probs, const int64_t* targets, const int64_t* input_lengths,
+                  const int64_t* target_lengths, float* alpha_ws, float* beta_ws, float* nll, float* grad, int64_t B,
+                  int64_t T, int64_t C, int64_t Umax, int64_t blank, float grad_scale, int32_t zero_infinity,
+                  void* stream);
+/* KL(softmax(t/T) || log_softmax(s/T)); grad += grad_coef*(softmax(s/T) - p_t); *loss_acc += loss_scale*KL */
+int kdfm_kl_div_logits(const float* student_logp, const float* teacher_logits, float* grad, float* loss_acc,
+                       int64_t rows, int64_t C, float temperature, float grad_coef, float loss_scale, void* stream);
+/* out5 = [total, ctc(mean_batch), kl, recon, fm] */
+int kdfm_loss_combine(const float* nll, int64_t B, const float* kl, const float* recon, const float* fm,
+                      float kd_alpha, float* out5, void* stream);
+
+/* ---------------- ver5 KD heads (asr_train_diffm.py:400-497, 1270-1427) -------------------- */
+int kdfm_adapter_fwd(const float* zs, const float* h, const float* w2, const float* b2, const float* eps_in, float* zn,
+                     float* gamma, int64_t rows, int64_t L, const uint64_t* seed, uint64_t rng_stream, void* stream);
+int kdfm_adapter_bwd(const float* dzn, const float* zs, const float* h, const float* gamma, const float* w2,
+                     const float* eps_in, float* dzs, float* dh, float* dw2, float* db2, int64_t rows, int64_t L,
+                     const uint64_t* seed, uint64_t rng_stream, void* stream);
+int kdfm_fm_step_bias(const float* w_te, const float* b_te, const float* W1, const float* b1, float* cvec, float* evec,
+                      int64_t L, int64_t E, int64_t steps, void* stream);
+int kdfm_fm_time_bwd(const float* dc, const float* evec, const float* W1, float* dW1, float* db1, float* dw_te,
+                     float* db_te, int64_t L, int64_t E, int64_t steps, void* stream);
+
+/* ---------------- glue ------------------------------------------------------------------ */
+int kdfm_fill(float* x, float value, int64_t n, void* stream);
+int kdfm_axpby(const float* a, int64_t lda, const float* b, int64_t ldb, float* out, int64_t ldo, int64_t rows,
+               int64_t cols, float alpha, float beta, void* stream);
+int kdfm_dropout(const float* x, float* out, int64_t n, float p, float scale, const uint64_t* seed,
+                 uint64_t rng_stream, void* stream);
+/* NeMo Conv1d weight (O,I,K) -> fwd (O,K,I) and transposed+flipped bwd (I,K,O) GEMM layouts */
+int kdfm_convw_prep(const float* W, float* fwd, float* bwd, int64_t O, int64_t I, int64_t K, void* stream);
+/* dW(O,I,K) += alpha * G(O,K,I) */
+int kdfm_convw_grad(const float* G, float* dW, int64_t O, int64_t I, int64_t K, float alpha, void* stream);
+/* mel_len = wav_len // hop (FilterbankFeatures.get_seq_len); len1/len2 after each striding conv
+ * (ConvSubsampling calc_length: floor((l + 2*1 - 3)/2 + 1)) */
+int kdfm_subsample_lengths(const int64_t* wav_len, int64_t* mel_len, int64_t* len1, int64_t* len2, int64_t B,
+                           int64_t hop, void* stream);
+/* step counter += 1 and per-step RNG seed advance, on device */
+int kdfm_step_advance(int64_t* step, uint64_t* seed, void* stream);
+
+/* ---------------- optimizer (modelPT.py:650-897, lr_scheduler.py:473-530) ------------------ */
+int kdfm_adamw_noam(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, int64_t n,
+                    const int64_t* step, float base_lr, float d_model, float warmup_steps, float min_lr,
+                    float beta1, float beta2, float eps, float weight_decay, float grad_scale, float* lr_out,
+                    void* stream);
 
 #ifdef __cplusplus
 }

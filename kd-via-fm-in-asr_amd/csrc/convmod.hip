@@ -1,0 +1,370 @@
+// Conformer convolution module pieces (NeMo ConformerConvolution, Appendix A.8; built at
+// conformer_encoder.py:450-472 with conv_kernel_size 31, conv_norm_type batch_norm):
+//   GLU(dim=channels) + pad-mask  ->  depthwise Conv1d(k=31, pad 15/15)  ->  BatchNorm1d
+//   (batch statistics in training, running statistics in eval)  ->  SiLU.
+// Layout: channels-last rows (B*T, C).  The depthwise conv stages a (64+k-1) x 64 frame x channel
+// tile in LDS (coalesced along channels) so each input element is read from HBM once per tile.
+// BatchNorm statistics accumulate in f64.
+#include "common.h"
+
+namespace kdfm {
+namespace {
+
+constexpr int TT = 64;    // frames per tile
+constexpr int CT = 64;    // channels per tile
+constexpr int KMAX = 63;  // max kernel size
+
+__global__ __launch_bounds__(256) void glu_mask_fwd_kernel(const float* __restrict__ a, const int64_t* __restrict__ lens,
+                                                           float* __restrict__ g, int64_t rows, int64_t T, int64_t d) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= rows * d) return;
+  const int64_t r = idx / d, c = idx - r * d;
+  const int64_t t = r % T, b = r / T;
+  float v = 0.f;
+  if (!lens || t < lens[b]) {
+    const float x = a[r * 2 * d + c], y = a[r * 2 * d + d + c];
+    v = x * sigmoidf_(y);
+  }
+  g[idx] = v;
+}
+
+__global__ __launch_bounds__(256) void glu_mask_bwd_kernel(const float* __restrict__ dg, const float* __restrict__ a,
+                                                           const int64_t* __restrict__ lens, float* __restrict__ da,
+                                                           int64_t rows, int64_t T, int64_t d) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= rows * d) return;
+  const int64_t r = idx / d, c = idx - r * d;
+  const int64_t t = r % T, b = r / T;
+  float dx = 0.f, dyv = 0.f;
+  if (!lens || t < lens[b]) {
+    const float x = a[r * 2 * d + c], y = a[r * 2 * d + d + c];
+    const float s = sigmoidf_(y);
+    const float gg = dg[idx];
+    dx = gg * s;
+    dyv = gg * x * s * (1.f - s);
+  }
+  da[r * 2 * d + c] = dx;
+  da[r * 2 * d + d + c] = dyv;
+}
+
+// y[b,t,c] = bias[c] + sum_k w[c,k] * g[b,t+k-pad,c]; stats[c] += (sum y, sum y^2)
+__global__ __launch_bounds__(256) void dwconv_fwd_kernel(const float* __restrict__ g, const float* __restrict__ w,
+                                                         const float* __restrict__ bias, float* __restrict__ y,
+                                                         double* __restrict__ stats, int64_t T, int64_t d, int K) {
+  __shared__ float tile[(TT + KMAX - 1) * CT];
+  __shared__ float wt[CT * KMAX];
+  __shared__ double red[2][4][CT];
+  const int pad = (K - 1) / 2;
+  const int64_t b = blockIdx.z;
+  const int64_t t0 = (int64_t)blockIdx.x * TT;
+  const int64_t c0 = (int64_t)blockIdx.y * CT;
+  const int rowsIn = TT + K - 1;
+  for (int e = threadIdx.x; e < rowsIn * CT; e += 256) {
+    const int rr = e / CT, cc = e % CT;
+    const int64_t t = t0 + rr - pad, c = c0 + cc;
+    tile[e] = (t >= 0 && t < T && c < d) ? g[(b * T + t) * d + c] : 0.f;
+  }
+  for (int e = threadIdx.x; e < CT * K; e += 256) {
+    const int cc = e / K, k = e % K;
+    wt[cc * KMAX + k] = (c0 + cc < d) ? w[(c0 + cc) * K + k] : 0.f;
+  }
+  __syncthreads();
+  const int cc = threadIdx.x & 63;
+  const int tq = threadIdx.x >> 6;  // 4 frame groups of 16
+  const int64_t c = c0 + cc;
+  double s1 = 0.0, s2 = 0.0;
+  if (c < d) {
+    const float bc = bias ? bias[c] : 0.f;
+    for (int tt = tq; tt < TT; tt += 4) {
+      const int64_t t = t0 + tt;
+      if (t >= T) break;
+      float acc = bc;
+      for (int k = 0; k < K; ++k) acc += wt[cc * KMAX + k] * tile[(tt + k) * CT + cc];
+      y[(b * T + t) * d + c] = acc;
+      s1 += acc;
+      s2 += (double)acc * acc;
+    }
+  }
+  red[0][tq][cc] = s1;
+  red[1][tq][cc] = s2;
+  __syncthreads();
+  if (stats && threadIdx.x < CT && c0 + threadIdx.x < d) {
+    const int q = threadIdx.x;
+    atomicAdd(stats + c0 + q, red[0][0][q] + red[0][1][q] + red[0][2][q] + red[0][3][q]);
+    atomicAdd(stats + d + c0 + q, red[1][0][q] + red[1][1][q] + red[1][2][q] + red[1][3][q]);
+  }
+}
+
+// mean/rstd per channel: batch statistics (biased var) or running statistics (eval)
+__global__ __launch_bounds__(256) void bn_finalize_kernel(const double* __restrict__ stats, const float* __restrict__ rm,
+                                                          const float* __restrict__ rv, float* __restrict__ mean,
+                                                          float* __restrict__ rstd, int64_t d, double count, float eps) {
+  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (c >= d) return;
+  if (stats) {
+    const double m = stats[c] / count;
+    double var = stats[d + c] / count - m * m;
+    if (var < 0.0) var = 0.0;
+    mean[c] = (float)m;
+    rstd[c] = (float)(1.0 / sqrt(var + (double)eps));
+  } else {
+    mean[c] = rm[c];
+    rstd[c] = rsqrtf(rv[c] + eps);
+  }
+}
+
+__global__ __launch_bounds__(256) void bn_running_kernel(float* __restrict__ rm, float* __restrict__ rv,
+                                                         const double* __restrict__ stats, int64_t d, double count,
+                                                         float momentum) {
+  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (c >= d) return;
+  const double m = stats[c] / count;
+  double var = stats[d + c] / count - m * m;
+  if (var < 0.0) var = 0.0;
+  const double unb = count > 1.0 ? var * count / (count - 1.0) : var;
+  rm[c] = (float)((1.0 - momentum) * rm[c] + momentum * m);
+  rv[c] = (float)((1.0 - momentum) * rv[c] + momentum * unb);
+}
+
+// z = silu(gamma * (y - mean) * rstd + beta)
+__global__ __launch_bounds__(256) void bn_silu_fwd_kernel(const float* __restrict__ y, const float* __restrict__ mean,
+                                                          const float* __restrict__ rstd, const float* __restrict__ gm,
+                                                          const float* __restrict__ bt, float* __restrict__ z,
+                                                          int64_t n, int64_t d) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= n) return;
+  const int64_t c = idx % d;
+  const float pre = gm[c] * (y[idx] - mean[c]) * rstd[c] + bt[c];
+  z[idx] = siluf_(pre);
+}
+
+// red[c] += sum dyb ; red[d+c] += sum dyb * xhat, with dyb = dz * silu'(pre)
+__global__ __launch_bounds__(256) void bn_silu_bwd_reduce_kernel(const float* __restrict__ dz, const float* __restrict__ y,
+                                                                 const float* __restrict__ mean,
+                                                                 const float* __restrict__ rstd,
+                                                                 const float* __restrict__ gm, const float* __restrict__ bt,
+                                                                 double* __restrict__ red, int64_t rows, int64_t d,
+                                                                 int64_t rows_per) {
+  __shared__ double sh[2][4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t c = (int64_t)blockIdx.x * 64 + lane;
+  const int64_t r0 = (int64_t)blockIdx.y * rows_per;
+  const int64_t r1 = (r0 + rows_per < rows) ? r0 + rows_per : rows;
+  double s1 = 0.0, s2 = 0.0;
+  if (c < d) {
+    const float mu = mean[c], rs = rstd[c], g = gm[c], b = bt[c];
+    for (int64_t r = r0 + w; r < r1; r += 4) {
+      const float xh = (y[r * d + c] - mu) * rs;
+      const float dyb = dz[r * d + c] * dsiluf_(g * xh + b);
+      s1 += dyb;
+      s2 += (double)dyb * xh;
+    }
+  }
+  sh[0][w][lane] = s1;
+  sh[1][w][lane] = s2;
+  __syncthreads();
+  if (w == 0 && c < d) {
+    atomicAdd(red + c, sh[0][0][lane] + sh[0][1][lane] + sh[0][2][lane] + sh[0][3][lane]);
+    atomicAdd(red + d + c, sh[1][0][lane] + sh[1][1][lane] + sh[1][2][lane] + sh[1][3][lane]);
+  }
+}
+
+// dy = gamma*rstd*(dyb - mean(dyb) - xhat*mean(dyb*xhat))  (batch stats)   or gamma*rstd*dyb (eval)
+__global__ __launch_bounds__(256) void bn_silu_bwd_apply_kernel(const float* __restrict__ dz, const float* __restrict__ y,
+                                                                const float* __restrict__ mean,
+                                                                const float* __restrict__ rstd,
+                                                                const float* __restrict__ gm,
+                                                                const float* __restrict__ bt,
+                                                                const double* __restrict__ red, float* __restrict__ dy,
+                                                                int64_t n, int64_t d, double count, int batch_stats) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= n) return;
+  const int64_t c = idx % d;
+  const float xh = (y[idx] - mean[c]) * rstd[c];
+  const float dyb = dz[idx] * dsiluf_(gm[c] * xh + bt[c]);
+  float v;
+  if (batch_stats) {
+    const float m1 = (float)(red[c] / count), m2 = (float)(red[d + c] / count);
+    v = gm[c] * rstd[c] * (dyb - m1 - xh * m2);
+  } else {
+    v = gm[c] * rstd[c] * dyb;
+  }
+  dy[idx] = v;
+}
+
+__global__ void bn_param_grad_kernel(const double* __restrict__ red, float* __restrict__ dgamma,
+                                     float* __restrict__ dbeta, int64_t d) {
+  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (c >= d) return;
+  dgamma[c] += (float)red[d + c];
+  dbeta[c] += (float)red[c];
+}
+
+// dg[b,t,c] = sum_k w[c,k] * dy[b,t-k+pad,c];  dw[c,k] += sum dy[b,t,c]*g[b,t+k-pad,c]; db += sum dy
+__global__ __launch_bounds__(256) void dwconv_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ g,
+                                                         const float* __restrict__ w, float* __restrict__ dg,
+                                                         float* __restrict__ dw, float* __restrict__ db, int64_t T,
+                                                         int64_t d, int K) {
+  __shared__ float tdy[(TT + KMAX - 1) * CT];  // dy rows t0-pad' .. (for dg: needs t - k + pad)
+  __shared__ float tg[(TT + KMAX - 1) * CT];   // g rows t0-pad .. t0+TT-1+pad
+  __shared__ float wt[CT * KMAX];
+  const int pad = (K - 1) / 2;
+  const int64_t b = blockIdx.z;
+  const int64_t t0 = (int64_t)blockIdx.x * TT;
+  const int64_t c0 = (int64_t)blockIdx.y * CT;
+  const int rowsIn = TT + K - 1;
+  // dy tile holds frames t0 - (K-1-pad) ... t0 + TT - 1 + pad  (index rr -> t = t0 + rr - (K-1-pad))
+  const int lo = K - 1 - pad;
+  for (int e = threadIdx.x; e < rowsIn * CT; e += 256) {
+    const int rr = e / CT, cc = e % CT;
+    const int64_t c = c0 + cc;
+    const int64_t td = t0 + rr - lo;
+    tdy[e] = (td >= 0 && td < T && c < d) ? dy[(b * T + td) * d + c] : 0.f;
+    const int64_t tg_ = t0 + rr - pad;
+    tg[e] = (tg_ >= 0 && tg_ < T && c < d) ? g[(b * T + tg_) * d + c] : 0.f;
+  }
+  for (int e = threadIdx.x; e < CT * K; e += 256) {
+    const int cc = e / K, k = e % K;
+    wt[cc * KMAX + k] = (c0 + cc < d) ? w[(c0 + cc) * K + k] : 0.f;
+  }
+  __syncthreads();
+  const int cc = threadIdx.x & 63;
+  const int tq = threadIdx.x >> 6;
+  const int64_t c = c0 + cc;
+  if (c < d) {
+    for (int tt = tq; tt < TT; tt += 4) {
+      const int64_t t = t0 + tt;
+      if (t >= T) break;
+      // dy[t - k + pad] -> tdy index (t - k + pad) - t0 + lo = tt - k + pad + lo = tt + (K-1) - k
+      float acc = 0.f;
+      for (int k = 0; k < K; ++k) acc += wt[cc * KMAX + k] * tdy[(tt + K - 1 - k) * CT + cc];
+      dg[(b * T + t) * d + c] = acc;
+    }
+  }
+  // weight / bias gradient partials over this tile's frames
+  for (int e = threadIdx.x; e < CT * (K + 1); e += 256) {
+    const int q = e % CT, k = e / CT;  // k == K -> bias
+    const int64_t cq = c0 + q;
+    if (cq >= d) continue;
+    float acc = 0.f;
+    for (int tt = 0; tt < TT; ++tt) {
+      const int64_t t = t0 + tt;
+      if (t >= T) break;
+      const float dyv = tdy[(tt + lo) * CT + q];
+      acc += (k < K) ? dyv * tg[(tt + k) * CT + q] : dyv;
+    }
+    if (k < K)
+      atomicAdd(dw + cq * K + k, acc);
+    else
+      atomicAdd(db + cq, acc);
+  }
+}
+
+}  // namespace
+}  // namespace kdfm
+
+extern "C" {
+
+int kdfm_glu_mask_fwd(const float* a, const int64_t* lengths, float* g, int64_t B, int64_t T, int64_t d,
+                      void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(a && g, "null pointer");
+  const int64_t n = B * T * d;
+  if (n == 0) return KDFM_OK;
+  hipLaunchKernelGGL(glu_mask_fwd_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, as_stream(stream), a,
+                     lengths, g, B * T, T, d);
+  return check_launch("kdfm_glu_mask_fwd");
+}
+
+int kdfm_glu_mask_bwd(const float* dg, const float* a, const int64_t* lengths, float* da, int64_t B, int64_t T,
+                      int64_t d, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(dg && a && da, "null pointer");
+  const int64_t n = B * T * d;
+  if (n == 0) return KDFM_OK;
+  hipLaunchKernelGGL(glu_mask_bwd_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, as_stream(stream), dg, a,
+                     lengths, da, B * T, T, d);
+  return check_launch("kdfm_glu_mask_bwd");
+}
+
+int kdfm_dwconv_fwd(const float* g, const float* w, const float* bias, float* y, double* stats, int64_t B, int64_t T,
+                    int64_t d, int64_t K, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(g && w && y, "null pointer");
+  KDFM_REQUIRE(K >= 1 && K <= KMAX && (K % 2) == 1, "kernel size must be odd and <= 63");
+  if (B * T * d == 0) return KDFM_OK;
+  dim3 grid((unsigned)ceil_div(T, TT), (unsigned)ceil_div(d, CT), (unsigned)B);
+  hipLaunchKernelGGL(dwconv_fwd_kernel, grid, dim3(256), 0, as_stream(stream), g, w, bias, y, stats, T, d, (int)K);
+  return check_launch("kdfm_dwconv_fwd");
+}
+
+int kdfm_dwconv_bwd(const float* dy, const float* g, const float* w, float* dg, float* dw, float* db, int64_t B,
+                    int64_t T, int64_t d, int64_t K, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(dy && g && w && dg && dw && db, "null pointer");
+  KDFM_REQUIRE(K >= 1 && K <= KMAX && (K % 2) == 1, "kernel size must be odd and <= 63");
+  if (B * T * d == 0) return KDFM_OK;
+  dim3 grid((unsigned)ceil_div(T, TT), (unsigned)ceil_div(d, CT), (unsigned)B);
+  hipLaunchKernelGGL(dwconv_bwd_kernel, grid, dim3(256), 0, as_stream(stream), dy, g, w, dg, dw, db, T, d, (int)K);
+  return check_launch("kdfm_dwconv_bwd");
+}
+
+int kdfm_bn_finalize(const double* stats, const float* running_mean, const float* running_var, float* mean,
+                     float* rstd, int64_t d, int64_t count, float eps, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(mean && rstd, "null pointer");
+  KDFM_REQUIRE(stats || (running_mean && running_var), "need batch stats or running stats");
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((unsigned)ceil_div(d, 256)), dim3(256), 0, as_stream(stream), stats,
+                     running_mean, running_var, mean, rstd, d, (double)count, eps);
+  return check_launch("kdfm_bn_finalize");
+}
+
+int kdfm_bn_running_update(float* running_mean, float* running_var, const double* stats, int64_t d, int64_t count,
+                           float momentum, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(running_mean && running_var && stats, "null pointer");
+  hipLaunchKernelGGL(bn_running_kernel, dim3((unsigned)ceil_div(d, 256)), dim3(256), 0, as_stream(stream),
+                     running_mean, running_var, stats, d, (double)count, momentum);
+  return check_launch("kdfm_bn_running_update");
+}
+
+int kdfm_bn_silu_fwd(const float* y, const float* mean, const float* rstd, const float* gamma, const float* beta,
+                     float* z, int64_t rows, int64_t d, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(y && mean && rstd && gamma && beta && z, "null pointer");
+  const int64_t n = rows * d;
+  if (n == 0) return KDFM_OK;
+  hipLaunchKernelGGL(bn_silu_fwd_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, as_stream(stream), y, mean,
+                     rstd, gamma, beta, z, n, d);
+  return check_launch("kdfm_bn_silu_fwd");
+}
+
+int kdfm_bn_silu_bwd(const float* dz, const float* y, const float* mean, const float* rstd, const float* gamma,
+                     const float* beta, double* red_ws, float* dy, float* dgamma, float* dbeta, int64_t rows,
+                     int64_t d, int32_t batch_stats, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(dz && y && mean && rstd && gamma && beta && red_ws && dy && dgamma && dbeta, "null pointer");
+  if (rows * d == 0) return KDFM_OK;
+  hipStream_t st = as_stream(stream);
+  if (hipMemsetAsync(red_ws, 0, sizeof(double) * 2 * d, st) != hipSuccess) {
+    set_error("kdfm_bn_silu_bwd: memset failed");
+    return KDFM_ELAUNCH;
+  }
+  int64_t gy = ceil_div(rows, 256);
+  if (gy > 512) gy = 512;
+  const int64_t rp = ceil_div(rows, gy);
+  gy = ceil_div(rows, rp);
+  hipLaunchKernelGGL(bn_silu_bwd_reduce_kernel, dim3((unsigned)ceil_div(d, 64), (unsigned)gy), dim3(256), 0, st, dz,
+                     y, mean, rstd, gamma, beta, red_ws, rows, d, rp);
+  int rc = check_launch("kdfm_bn_silu_bwd(reduce)");
+  if (rc) return rc;
+  hipLaunchKernelGGL(bn_silu_bwd_apply_kernel, dim3((unsigned)ceil_div(rows * d, 256)), dim3(256), 0, st, dz, y, mean,
+                     rstd, gamma, beta, red_ws, dy, rows * d, d, (double)rows, batch_stats);
+  rc = check_launch("kdfm_bn_silu_bwd(apply)");
+  if (rc) return rc;
+  hipLaunchKernelGGL(bn_param_grad_kernel, dim3((unsigned)ceil_div(d, 256)), dim3(256), 0, st, red_ws, dgamma, dbeta,
+                     d);
+  return check_launch("kdfm_bn_silu_bwd(params)");
+}
+
+}  // extern "C"

@@ -1,0 +1,243 @@
+// Log-mel frontend (NeMo AudioToMelSpectrogramPreprocessor -> FilterbankFeatures, called at
+// audio_preprocessing.py:299-300; semantics SURVEY.md Appendix A.1) and SpecAugment (A.2),
+// plus the im2col/col2im of the striding ConvSubsampling (A.3, built conformer_encoder.py:381-390).
+//
+// STFT-as-GEMM: the frames of the zero-centre-padded, pre-emphasised signal are read as a strided
+// view (frame t = samples [160t+56, 160t+456) of the padded row) and multiplied by a 400 x 514
+// basis (Hann(400) folded into cos / -sin) in the MFMA GEMM; this file holds the surrounding
+// memory-bound passes.
+#include "common.h"
+
+namespace kdfm {
+namespace {
+
+// xp[b, pad + n] = preemph(x + dither*noise)[n] masked to n < len;  zero halo of `pad` each side
+__global__ __launch_bounds__(256) void preemph_pad_kernel(const float* __restrict__ x, const int64_t* __restrict__ lens,
+                                                          float* __restrict__ xp, int64_t N, int64_t pad, float coef,
+                                                          float dither, const uint64_t* seed_ptr, uint64_t rng_stream) {
+  const int64_t b = blockIdx.y;
+  const int64_t W = N + 2 * pad;
+  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j >= W) return;
+  const int64_t n = j - pad;
+  float v = 0.f;
+  const int64_t len = lens ? lens[b] : N;
+  if (n >= 0 && n < N && n < len) {
+    const float* xr = x + b * N;
+    float cur = xr[n];
+    if (dither > 0.f) cur += dither * rng_normal(load_seed(seed_ptr), rng_stream, (uint64_t)(b * N + n));
+    if (n == 0) {
+      v = cur;
+    } else {
+      float prev = xr[n - 1];
+      if (dither > 0.f) prev += dither * rng_normal(load_seed(seed_ptr), rng_stream, (uint64_t)(b * N + n - 1));
+      v = cur - coef * prev;
+    }
+  }
+  xp[b * W + j] = v;
+}
+
+// pw[r, f] = spec[r, f]^2 + spec[r, F + f]^2   (spec rows = [re(0..F-1) | im(0..F-1)])
+__global__ __launch_bounds__(256) void power_kernel(const float* __restrict__ spec, float* __restrict__ pw, int64_t rows,
+                                                    int64_t F) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= rows * F) return;
+  const int64_t r = idx / F, f = idx - r * F;
+  const float re = spec[r * 2 * F + f], im = spec[r * 2 * F + F + f];
+  pw[idx] = re * re + im * im;
+}
+
+// out[b,t,j] = (log(mel+guard) - mean_j) / (std_j + 1e-5) for t < seq_len, 0 beyond
+// mean/std over valid frames, unbiased (n-1) std; block = (b, 64 mel columns), 4 frame lanes.
+__global__ __launch_bounds__(256) void logmel_norm_kernel(const float* __restrict__ mel, const int64_t* __restrict__ sl,
+                                                          float* __restrict__ out, int64_t T, int64_t nf, float guard) {
+  __shared__ float red[4][64];
+  const int64_t b = blockIdx.y;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t j = (int64_t)blockIdx.x * 64 + lane;
+  const int64_t n = sl[b] < T ? sl[b] : T;
+  const float* mr = mel + b * T * nf;
+  float* orow = out + b * T * nf;
+  float s = 0.f;
+  if (j < nf)
+    for (int64_t t = w; t < n; t += 4) s += __logf(mr[t * nf + j] + guard);
+  red[w][lane] = s;
+  __syncthreads();
+  const float mean = (red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane]) / (float)n;
+  __syncthreads();
+  float q = 0.f;
+  if (j < nf)
+    for (int64_t t = w; t < n; t += 4) {
+      const float dv = __logf(mr[t * nf + j] + guard) - mean;
+      q += dv * dv;
+    }
+  red[w][lane] = q;
+  __syncthreads();
+  float var = (red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane]) / ((float)n - 1.f);
+  float sd = sqrtf(var);
+  if (!(sd == sd)) sd = 0.f;  // n == 1 -> nan -> 0 (normalize_batch edge case)
+  const float inv = 1.f / (sd + 1e-5f);
+  if (j < nf)
+    for (int64_t t = w; t < T; t += 4) orow[t * nf + j] = (t < n) ? (__logf(mr[t * nf + j] + guard) - mean) * inv : 0.f;
+}
+
+// SpecAugment: per utterance `fmasks` frequency bands of width floor(U*(fwidth+1)) and `tmasks`
+// time bands of width floor(U*(max(1,int(len*twidth))+1)); masked cells set to 0.
+__device__ __forceinline__ bool spec_masked(int64_t b, int64_t t, int64_t f, int64_t len, int64_t nf, int fmasks,
+                                            int fwidth, int tmasks, float twidth, uint64_t seed, uint64_t st) {
+  for (int q = 0; q < fmasks; ++q) {
+    const uint64_t base = (uint64_t)b * 64 + (uint64_t)q * 2;
+    int w = (int)(rng_uniform(seed, st, base) * (fwidth + 1));
+    if (w > fwidth) w = fwidth;
+    if (w > nf) w = (int)nf;
+    const int64_t s0 = (int64_t)(rng_uniform(seed, st, base + 1) * (float)(nf - w + 1));
+    if (f >= s0 && f < s0 + w) return true;
+  }
+  int64_t maxw = (int64_t)((float)len * twidth);
+  if (maxw < 1) maxw = 1;
+  for (int q = 0; q < tmasks; ++q) {
+    const uint64_t base = (uint64_t)b * 64 + 32 + (uint64_t)q * 2;
+    int64_t w = (int64_t)(rng_uniform(seed, st, base) * (float)(maxw + 1));
+    if (w > maxw) w = maxw;
+    int64_t room = len - w + 1;
+    if (room < 1) room = 1;
+    const int64_t s0 = (int64_t)(rng_uniform(seed, st, base + 1) * (float)room);
+    if (t >= s0 && t < s0 + w) return true;
+  }
+  return false;
+}
+
+__global__ __launch_bounds__(256) void specaug_kernel(float* __restrict__ x, const int64_t* __restrict__ sl,
+                                                      uint8_t* __restrict__ mask_out, int64_t B, int64_t T, int64_t nf,
+                                                      int fmasks, int fwidth, int tmasks, float twidth,
+                                                      const uint64_t* seed_ptr, uint64_t st) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= B * T * nf) return;
+  const int64_t f = idx % nf, t = (idx / nf) % T, b = idx / (nf * T);
+  const bool m = spec_masked(b, t, f, sl[b], nf, fmasks, fwidth, tmasks, twidth, load_seed(seed_ptr), st);
+  if (m) x[idx] = 0.f;
+  if (mask_out) mask_out[idx] = m ? 1 : 0;
+}
+
+// cols[(b,t2,f2), c*9 + ky*3 + kx] = X[b, 2*t2-1+ky, 2*f2-1+kx, c]  (0 outside / beyond len_in)
+__global__ __launch_bounds__(256) void im2col_kernel(const float* __restrict__ X, const int64_t* __restrict__ lin,
+                                                     float* __restrict__ cols, int64_t B, int64_t T1, int64_t F1,
+                                                     int64_t C, int64_t T2, int64_t F2) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t KC = 9 * C;
+  if (idx >= B * T2 * F2 * KC) return;
+  const int64_t q = idx % KC, row = idx / KC;
+  const int64_t c = q / 9, tap = q % 9, ky = tap / 3, kx = tap % 3;
+  const int64_t f2 = row % F2, t2 = (row / F2) % T2, b = row / (F2 * T2);
+  const int64_t t1 = 2 * t2 - 1 + ky, f1 = 2 * f2 - 1 + kx;
+  float v = 0.f;
+  const int64_t len = lin ? lin[b] : T1;
+  if (t1 >= 0 && t1 < T1 && t1 < len && f1 >= 0 && f1 < F1) v = X[((b * T1 + t1) * F1 + f1) * C + c];
+  cols[idx] = v;
+}
+
+// dX[b,t1,f1,c] = sum over taps hitting (t1,f1) of dcols; zero beyond len_in; *= (aux > 0) if aux
+__global__ __launch_bounds__(256) void col2im_kernel(const float* __restrict__ dcols, const int64_t* __restrict__ lin,
+                                                     const float* __restrict__ aux, float* __restrict__ dX, int64_t B,
+                                                     int64_t T1, int64_t F1, int64_t C, int64_t T2, int64_t F2) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= B * T1 * F1 * C) return;
+  const int64_t c = idx % C, f1 = (idx / C) % F1, t1 = (idx / (C * F1)) % T1, b = idx / (C * F1 * T1);
+  const int64_t len = lin ? lin[b] : T1;
+  float acc = 0.f;
+  if (t1 < len) {
+    for (int ky = 0; ky < 3; ++ky) {
+      const int64_t tn = t1 + 1 - ky;
+      if (tn < 0 || (tn & 1)) continue;
+      const int64_t t2 = tn >> 1;
+      if (t2 >= T2) continue;
+      for (int kx = 0; kx < 3; ++kx) {
+        const int64_t fn = f1 + 1 - kx;
+        if (fn < 0 || (fn & 1)) continue;
+        const int64_t f2 = fn >> 1;
+        if (f2 >= F2) continue;
+        acc += dcols[((b * T2 + t2) * F2 + f2) * 9 * C + c * 9 + ky * 3 + kx];
+      }
+    }
+    if (aux && !(aux[idx] > 0.f)) acc = 0.f;
+  }
+  dX[idx] = acc;
+}
+
+}  // namespace
+}  // namespace kdfm
+
+extern "C" {
+
+int kdfm_preemph_pad(const float* wav, const int64_t* lengths, float* xp, int64_t B, int64_t N, int64_t pad,
+                     float preemph, float dither, const uint64_t* seed, uint64_t rng_stream, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(wav && xp, "null pointer");
+  KDFM_REQUIRE(B >= 0 && N >= 0 && pad >= 0, "bad shape");
+  KDFM_REQUIRE(dither == 0.f || seed, "dither needs a seed");
+  if (B == 0) return KDFM_OK;
+  dim3 grid((unsigned)ceil_div(N + 2 * pad, 256), (unsigned)B);
+  hipLaunchKernelGGL(preemph_pad_kernel, grid, dim3(256), 0, as_stream(stream), wav, lengths, xp, N, pad, preemph,
+                     dither, seed, rng_stream);
+  return check_launch("kdfm_preemph_pad");
+}
+
+int kdfm_power_spectrum(const float* spec, float* power, int64_t rows, int64_t nbins, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(spec && power, "null pointer");
+  const int64_t n = rows * nbins;
+  if (n == 0) return KDFM_OK;
+  hipLaunchKernelGGL(power_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, as_stream(stream), spec, power,
+                     rows, nbins);
+  return check_launch("kdfm_power_spectrum");
+}
+
+int kdfm_logmel_normalize(const float* mel, const int64_t* seq_len, float* out, int64_t B, int64_t T, int64_t nfilt,
+                          float log_guard, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(mel && seq_len && out, "null pointer");
+  if (B * T * nfilt == 0) return KDFM_OK;
+  dim3 grid((unsigned)ceil_div(nfilt, 64), (unsigned)B);
+  hipLaunchKernelGGL(logmel_norm_kernel, grid, dim3(256), 0, as_stream(stream), mel, seq_len, out, T, nfilt,
+                     log_guard);
+  return check_launch("kdfm_logmel_normalize");
+}
+
+int kdfm_specaugment(float* x, const int64_t* seq_len, uint8_t* mask_out, int64_t B, int64_t T, int64_t nfilt,
+                     int32_t freq_masks, int32_t freq_width, int32_t time_masks, float time_width,
+                     const uint64_t* seed, uint64_t rng_stream, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(x && seq_len && seed, "null pointer");
+  KDFM_REQUIRE(freq_masks >= 0 && freq_masks <= 16 && time_masks >= 0 && time_masks <= 16, "mask counts in [0,16]");
+  const int64_t n = B * T * nfilt;
+  if (n == 0) return KDFM_OK;
+  hipLaunchKernelGGL(specaug_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, as_stream(stream), x, seq_len,
+                     mask_out, B, T, nfilt, freq_masks, freq_width, time_masks, time_width, seed, rng_stream);
+  return check_launch("kdfm_specaugment");
+}
+
+int kdfm_im2col_3x3s2(const float* X, const int64_t* len_in, float* cols, int64_t B, int64_t T1, int64_t F1, int64_t C,
+                      void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(X && cols, "null pointer");
+  const int64_t T2 = (T1 - 1) / 2 + 1, F2 = (F1 - 1) / 2 + 1;
+  const int64_t n = B * T2 * F2 * 9 * C;
+  if (n == 0) return KDFM_OK;
+  hipLaunchKernelGGL(im2col_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, as_stream(stream), X, len_in,
+                     cols, B, T1, F1, C, T2, F2);
+  return check_launch("kdfm_im2col_3x3s2");
+}
+
+int kdfm_col2im_3x3s2(const float* dcols, const int64_t* len_in, const float* relu_out, float* dX, int64_t B,
+                      int64_t T1, int64_t F1, int64_t C, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(dcols && dX, "null pointer");
+  const int64_t T2 = (T1 - 1) / 2 + 1, F2 = (F1 - 1) / 2 + 1;
+  const int64_t n = B * T1 * F1 * C;
+  if (n == 0) return KDFM_OK;
+  hipLaunchKernelGGL(col2im_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, as_stream(stream), dcols, len_in,
+                     relu_out, dX, B, T1, F1, C, T2, F2);
+  return check_launch("kdfm_col2im_3x3s2");
+}
+
+}  // extern "C"

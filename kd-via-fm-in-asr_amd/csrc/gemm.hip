@@ -29,6 +29,8 @@ struct P {
   const uint64_t* seed; uint64_t rng_stream;
   int epi, splitk, taps, pad;
   int64_t conv_c, conv_t;
+  const int64_t* mask_len; int64_t mask_T, mask_div;
+  float* loss_acc; float loss_scale;
 };
 
 // Operand element fetch for the "row operand" view: X(r, q) where r is the row-like index
@@ -223,6 +225,7 @@ __global__ __launch_bounds__(NT) void gemm_kernel(P p) {
   uint64_t seed = 0;
   if (epi & KDFM_EPI_DROPOUT) seed = load_seed(p.seed);
   const float keep_scale = (epi & KDFM_EPI_DROPOUT) ? 1.f / (1.f - p.dropout_p) : 1.f;
+  float mse_part = 0.f;
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -239,6 +242,12 @@ __global__ __launch_bounds__(NT) void gemm_kernel(P p) {
           continue;
         }
         if (epi & KDFM_EPI_BIAS) v += p.bias[n];
+        if (epi & KDFM_EPI_MSE) {
+          const float diff = v - p.R[off];
+          mse_part += diff * diff;
+          p.C[off] = p.rscale * diff;
+          continue;
+        }
         if (epi & KDFM_EPI_STORE_PRE) p.Cpre[off] = v;
         if (epi & KDFM_EPI_RELU) v = fmaxf(v, 0.f);
         if (epi & KDFM_EPI_SILU) v = siluf_(v);
@@ -250,8 +259,17 @@ __global__ __launch_bounds__(NT) void gemm_kernel(P p) {
         if (epi & KDFM_EPI_DSILU) v *= dsiluf_(p.aux[off]);
         if (epi & KDFM_EPI_RESID) v = p.R[off] + p.rscale * v;
         if (epi & KDFM_EPI_BETA) v += p.beta * p.C[off];
+        if (epi & KDFM_EPI_ROWMASK) {
+          const int64_t fr = m / p.mask_div;
+          const int64_t t = fr % p.mask_T, u = fr / p.mask_T;
+          if (t >= p.mask_len[u]) v = 0.f;
+        }
         p.C[off] = v;
       }
+  if (epi & KDFM_EPI_MSE) {
+    mse_part = wave_sum(mse_part);
+    if (lane == 0) atomicAdd(p.loss_acc, mse_part * p.loss_scale);
+  }
 }
 
 template <bool BF16>
@@ -306,6 +324,12 @@ extern "C" int kdfm_gemm(const kdfm_gemm_desc* d, void* stream) {
   p.seed = d->seed; p.rng_stream = d->rng_stream;
   p.epi = d->epi; p.splitk = d->splitk; p.taps = d->conv_taps; p.pad = d->conv_pad;
   p.conv_c = d->conv_c; p.conv_t = d->conv_t;
+  p.mask_len = d->mask_len; p.mask_T = d->mask_T; p.mask_div = d->mask_div;
+  p.loss_acc = d->loss_acc; p.loss_scale = d->loss_scale;
+  if (d->epi & KDFM_EPI_ROWMASK)
+    KDFM_REQUIRE(d->mask_len && d->mask_T > 0 && d->mask_div > 0 && d->batch1 == 1 && d->batch2 == 1,
+                 "ROWMASK needs mask_len/mask_T/mask_div and an unbatched GEMM");
+  if (d->epi & KDFM_EPI_MSE) KDFM_REQUIRE(d->loss_acc && d->R, "MSE needs loss_acc and target R");
   if (d->K == 0) p.splitk = 1;
   const int64_t gx = ceil_div(d->M, BM), gy = ceil_div(d->N, BN), gz = d->batch1 * d->batch2 * p.splitk;
   KDFM_REQUIRE(gx < (1ll << 31) && gy < 65536 && gz < 65536, "grid too large");

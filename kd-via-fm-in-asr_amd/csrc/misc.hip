@@ -1,0 +1,338 @@
+// Memory-bound glue of the step: fills, strided axpby, dropout application, the attention
+// q+u / q+v prep, conv-weight re-layouts, and the ver5 KD-head pieces that are not GEMMs:
+// NoiseAdapter gating (asr_train_diffm.py:425-442) and the FlowMatchingModule time embedding
+// (asr_train_diffm.py:1368-1378: Linear(1->32) of t = i/steps, concatenated to the 96-d state;
+// folded here into a per-step bias of the first meta-encoder Linear).
+#include "common.h"
+
+namespace kdfm {
+namespace {
+
+__global__ __launch_bounds__(256) void fill_kernel(float* x, float v, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) x[i] = v;
+}
+
+// out[r,c] = alpha*a[r,c] + beta*b[r,c]
+__global__ __launch_bounds__(256) void axpby_kernel(const float* a, int64_t lda, const float* b, int64_t ldb, float* out,
+                                                    int64_t ldo, int64_t rows, int64_t cols, float alpha, float beta) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= rows * cols) return;
+  const int64_t r = i / cols, c = i - r * cols;
+  float v = alpha * a[r * lda + c];
+  if (b) v += beta * b[r * ldb + c];
+  out[r * ldo + c] = v;
+}
+
+// out = scale * dropout(x) with the flat-index mask of the GEMM epilogue (idx = r*cols + c)
+__global__ __launch_bounds__(256) void dropout_kernel(const float* x, float* out, int64_t n, float p, float scale,
+                                                      const uint64_t* seed_ptr, uint64_t st) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  float v = x[i] * scale;
+  if (p > 0.f) v = dropout_keep(load_seed(seed_ptr), st, (uint64_t)i, p) ? v / (1.f - p) : 0.f;
+  out[i] = v;
+}
+
+// qu[r, j] = qkv[r, j] + u[j]; qv[r, j] = qkv[r, j] + v[j]   (j = h*dk + c over d columns)
+__global__ __launch_bounds__(256) void qkv_prep_kernel(const float* __restrict__ qkv, const float* __restrict__ u,
+                                                       const float* __restrict__ v, float* __restrict__ qu,
+                                                       float* __restrict__ qv, int64_t rows, int64_t d) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= rows * d) return;
+  const int64_t r = i / d, j = i - r * d;
+  const float q = qkv[r * 3 * d + j];
+  qu[i] = q + u[j];
+  qv[i] = q + v[j];
+}
+
+// NeMo Conv1d weight (O, I, K) -> GEMM layouts: fwd[o][k][i] = W[o][i][k];
+// bwd (transposed + flipped taps) [i][k][o] = W[o][i][K-1-k]
+__global__ __launch_bounds__(256) void convw_prep_kernel(const float* __restrict__ W, float* __restrict__ fwd,
+                                                         float* __restrict__ bwd, int64_t O, int64_t I, int64_t K) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= O * I * K) return;
+  const int64_t k = idx % K, i = (idx / K) % I, o = idx / (K * I);
+  const float w = W[idx];
+  if (fwd) fwd[(o * K + k) * I + i] = w;
+  if (bwd) bwd[(i * K + (K - 1 - k)) * O + o] = w;
+}
+
+// dW[o][i][k] += alpha * G[o][k][i]
+__global__ __launch_bounds__(256) void convw_grad_kernel(const float* __restrict__ G, float* __restrict__ dW, int64_t O,
+                                                         int64_t I, int64_t K, float alpha) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= O * I * K) return;
+  const int64_t k = idx % K, i = (idx / K) % I, o = idx / (K * I);
+  dW[idx] += alpha * G[(o * K + k) * I + i];
+}
+
+// NoiseAdapter: gamma = sigmoid(h . w2 + b2); zn = gamma*zs + (1-gamma)*eps   (one wave per row)
+__global__ __launch_bounds__(256) void adapter_fwd_kernel(const float* __restrict__ zs, const float* __restrict__ h,
+                                                          const float* __restrict__ w2, const float* __restrict__ b2,
+                                                          const float* __restrict__ eps_in, float* __restrict__ zn,
+                                                          float* __restrict__ gamma, int64_t rows, int L,
+                                                          const uint64_t* seed_ptr, uint64_t st) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= rows) return;
+  float s = 0.f;
+  for (int c = lane; c < L; c += 64) s += h[r * L + c] * w2[c];
+  s = wave_sum(s) + b2[0];
+  const float g = sigmoidf_(s);
+  const uint64_t seed = eps_in ? 0 : load_seed(seed_ptr);
+  for (int c = lane; c < L; c += 64) {
+    const float e = eps_in ? eps_in[r * L + c] : rng_normal(seed, st, (uint64_t)(r * L + c));
+    zn[r * L + c] = g * zs[r * L + c] + (1.f - g) * e;
+  }
+  if (lane == 0) gamma[r] = g;
+}
+
+// backward: dzs = g*dzn ; dgl = g(1-g) * sum_c dzn*(zs-eps) ; dh = dgl*w2*(h>0) ; dw2 += dgl*h ; db2 += dgl
+__global__ __launch_bounds__(256) void adapter_bwd_kernel(const float* __restrict__ dzn, const float* __restrict__ zs,
+                                                          const float* __restrict__ h, const float* __restrict__ gamma,
+                                                          const float* __restrict__ w2, const float* __restrict__ eps_in,
+                                                          float* __restrict__ dzs, float* __restrict__ dh,
+                                                          float* __restrict__ dw2, float* __restrict__ db2, int64_t rows,
+                                                          int L, const uint64_t* seed_ptr, uint64_t st,
+                                                          int64_t rows_per) {
+  __shared__ float sw[4][128];
+  __shared__ float sb[4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float pw0 = 0.f, pw1 = 0.f, pb = 0.f;  // L <= 128: lane holds columns lane, lane+64
+  const uint64_t seed = eps_in ? 0 : load_seed(seed_ptr);
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per;
+  const int64_t r1 = (r0 + rows_per < rows) ? r0 + rows_per : rows;
+  for (int64_t r = r0 + w; r < r1; r += 4) {
+    const float g = gamma[r];
+    float s = 0.f;
+    for (int c = lane; c < L; c += 64) {
+      const float e = eps_in ? eps_in[r * L + c] : rng_normal(seed, st, (uint64_t)(r * L + c));
+      const float d = dzn[r * L + c];
+      s += d * (zs[r * L + c] - e);
+      dzs[r * L + c] = g * d;
+    }
+    const float dgl = wave_sum(s) * g * (1.f - g);
+    for (int c = lane, q = 0; c < L; c += 64, ++q) {
+      const float hv = h[r * L + c];
+      dh[r * L + c] = (hv > 0.f) ? dgl * w2[c] : 0.f;
+      if (q == 0) pw0 += dgl * hv; else pw1 += dgl * hv;
+    }
+    pb += dgl;
+  }
+  sw[w][lane] = pw0;
+  sw[w][lane + 64] = pw1;
+  if (lane == 0) sb[w] = pb;
+  __syncthreads();
+  for (int c = threadIdx.x; c < L; c += 256) atomicAdd(dw2 + c, sw[0][c] + sw[1][c] + sw[2][c] + sw[3][c]);
+  if (threadIdx.x == 0) atomicAdd(db2, sb[0] + sb[1] + sb[2] + sb[3]);
+}
+
+// per FM step j (t = (S-j)/S): e_j = w_te*t + b_te ; c_j = W1[:, L:] e_j + b1   (W1 is L x (L+E))
+__global__ __launch_bounds__(256) void fm_step_bias_kernel(const float* __restrict__ w_te, const float* __restrict__ b_te,
+                                                           const float* __restrict__ W1, const float* __restrict__ b1,
+                                                           float* __restrict__ cvec, float* __restrict__ evec, int L,
+                                                           int E, int S) {
+  const int j = blockIdx.x;
+  const float t = (float)(S - j) / (float)S;
+  for (int o = threadIdx.x; o < L; o += 256) {
+    float acc = b1[o];
+    for (int q = 0; q < E; ++q) acc += W1[o * (L + E) + L + q] * (w_te[q] * t + b_te[q]);
+    cvec[j * L + o] = acc;
+  }
+  for (int q = threadIdx.x; q < E; q += 256) evec[j * E + q] = w_te[q] * t + b_te[q];
+}
+
+// given dc_j (S x L): dW1[:, L:] += dc_j e_j^T ; db1 += dc_j ; de_j = W1[:, L:]^T dc_j ;
+// dw_te += de_j * t_j ; db_te += de_j        (single block)
+__global__ __launch_bounds__(256) void fm_time_bwd_kernel(const float* __restrict__ dc, const float* __restrict__ evec,
+                                                          const float* __restrict__ W1, float* __restrict__ dW1,
+                                                          float* __restrict__ db1, float* __restrict__ dw_te,
+                                                          float* __restrict__ db_te, int L, int E, int S) {
+  for (int idx = threadIdx.x; idx < L * E; idx += 256) {
+    const int o = idx / E, q = idx % E;
+    float acc = 0.f;
+    for (int j = 0; j < S; ++j) acc += dc[j * L + o] * evec[j * E + q];
+    dW1[o * (L + E) + L + q] += acc;
+  }
+  for (int o = threadIdx.x; o < L; o += 256) {
+    float acc = 0.f;
+    for (int j = 0; j < S; ++j) acc += dc[j * L + o];
+    db1[o] += acc;
+  }
+  for (int q = threadIdx.x; q < E; q += 256) {
+    float gw = 0.f, gb = 0.f;
+    for (int j = 0; j < S; ++j) {
+      const float t = (float)(S - j) / (float)S;
+      float de = 0.f;
+      for (int o = 0; o < L; ++o) de += W1[o * (L + E) + L + q] * dc[j * L + o];
+      gw += de * t;
+      gb += de;
+    }
+    dw_te[q] += gw;
+    db_te[q] += gb;
+  }
+}
+
+// sinusoidal relative position table, positions T-1 ... -(T-1) (RelPositionalEncoding, A.4)
+__global__ __launch_bounds__(256) void relpos_table_kernel(float* __restrict__ pe, int64_t T, int64_t d) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (2 * T - 1) * d) return;
+  const int64_t p = idx / d, c = idx % d;
+  const double pos = (double)(T - 1 - p);
+  const int64_t i2 = c & ~1ll;
+  const double div = exp((double)i2 * -(log(10000.0) / (double)d));
+  pe[idx] = (float)((c & 1) ? cos(pos * div) : sin(pos * div));
+}
+
+// mel_len = L // hop (pinned: frames - 1); two striding convs: floor((l - 1)/2 + 1)
+__global__ void lengths_kernel(const int64_t* __restrict__ wl, int64_t* __restrict__ ml, int64_t* __restrict__ l1,
+                               int64_t* __restrict__ l2, int64_t B, int64_t hop) {
+  const int64_t b = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  if (b >= B) return;
+  const int64_t m = wl[b] / hop;
+  const int64_t a = (int64_t)floor(((double)m - 1.0) / 2.0 + 1.0);
+  const int64_t c = (int64_t)floor(((double)a - 1.0) / 2.0 + 1.0);
+  ml[b] = m;
+  if (l1) l1[b] = a;
+  if (l2) l2[b] = c;
+}
+
+// step counter / per-step RNG seed advance (graph-replay safe: runs on device)
+__global__ void step_advance_kernel(int64_t* step, uint64_t* seed) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    if (step) step[0] += 1;
+    if (seed) seed[0] = mix64(seed[0] + 0x632BE59BD9B4E019ull);
+  }
+}
+
+}  // namespace
+}  // namespace kdfm
+
+extern "C" {
+
+#define KDFM_1D(kernel, n, ...)                                                                              \
+  do {                                                                                                       \
+    if ((n) == 0) return KDFM_OK;                                                                            \
+    hipLaunchKernelGGL(kernel, dim3((unsigned)kdfm::ceil_div((n), 256)), dim3(256), 0,                        \
+                       kdfm::as_stream(stream), __VA_ARGS__);                                                \
+  } while (0)
+
+int kdfm_fill(float* x, float value, int64_t n, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(x || n == 0, "null pointer");
+  KDFM_1D(fill_kernel, n, x, value, n);
+  return check_launch("kdfm_fill");
+}
+
+int kdfm_axpby(const float* a, int64_t lda, const float* b, int64_t ldb, float* out, int64_t ldo, int64_t rows,
+               int64_t cols, float alpha, float beta, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(a && out, "null pointer");
+  KDFM_1D(axpby_kernel, rows * cols, a, lda, b, ldb, out, ldo, rows, cols, alpha, beta);
+  return check_launch("kdfm_axpby");
+}
+
+int kdfm_dropout(const float* x, float* out, int64_t n, float p, float scale, const uint64_t* seed,
+                 uint64_t rng_stream, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(x && out, "null pointer");
+  KDFM_REQUIRE(p >= 0.f && p < 1.f && (p == 0.f || seed), "dropout p / seed");
+  KDFM_1D(dropout_kernel, n, x, out, n, p, scale, seed, rng_stream);
+  return check_launch("kdfm_dropout");
+}
+
+int kdfm_qkv_prep(const float* qkv, const float* pos_bias_u, const float* pos_bias_v, float* qu, float* qv,
+                  int64_t rows, int64_t d, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(qkv && pos_bias_u && pos_bias_v && qu && qv, "null pointer");
+  KDFM_1D(qkv_prep_kernel, rows * d, qkv, pos_bias_u, pos_bias_v, qu, qv, rows, d);
+  return check_launch("kdfm_qkv_prep");
+}
+
+int kdfm_convw_prep(const float* W, float* fwd, float* bwd, int64_t O, int64_t I, int64_t K, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(W && (fwd || bwd), "null pointer");
+  KDFM_1D(convw_prep_kernel, O * I * K, W, fwd, bwd, O, I, K);
+  return check_launch("kdfm_convw_prep");
+}
+
+int kdfm_convw_grad(const float* G, float* dW, int64_t O, int64_t I, int64_t K, float alpha, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(G && dW, "null pointer");
+  KDFM_1D(convw_grad_kernel, O * I * K, G, dW, O, I, K, alpha);
+  return check_launch("kdfm_convw_grad");
+}
+
+int kdfm_adapter_fwd(const float* zs, const float* h, const float* w2, const float* b2, const float* eps_in, float* zn,
+                     float* gamma, int64_t rows, int64_t L, const uint64_t* seed, uint64_t rng_stream, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(zs && h && w2 && b2 && zn && gamma, "null pointer");
+  KDFM_REQUIRE(eps_in || seed, "need injected eps or a seed");
+  KDFM_REQUIRE(L > 0 && L <= 128, "latent dim in (0,128]");
+  if (rows == 0) return KDFM_OK;
+  hipLaunchKernelGGL(adapter_fwd_kernel, dim3((unsigned)ceil_div(rows, 4)), dim3(256), 0, as_stream(stream), zs, h, w2,
+                     b2, eps_in, zn, gamma, rows, (int)L, seed, rng_stream);
+  return check_launch("kdfm_adapter_fwd");
+}
+
+int kdfm_adapter_bwd(const float* dzn, const float* zs, const float* h, const float* gamma, const float* w2,
+                     const float* eps_in, float* dzs, float* dh, float* dw2, float* db2, int64_t rows, int64_t L,
+                     const uint64_t* seed, uint64_t rng_stream, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(dzn && zs && h && gamma && w2 && dzs && dh && dw2 && db2, "null pointer");
+  KDFM_REQUIRE(eps_in || seed, "need injected eps or a seed");
+  KDFM_REQUIRE(L > 0 && L <= 128, "latent dim in (0,128]");
+  if (rows == 0) return KDFM_OK;
+  int64_t blocks = ceil_div(rows, 64);
+  if (blocks > 2048) blocks = 2048;
+  const int64_t rp = ceil_div(rows, blocks);
+  blocks = ceil_div(rows, rp);
+  hipLaunchKernelGGL(adapter_bwd_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), dzn, zs, h, gamma, w2,
+                     eps_in, dzs, dh, dw2, db2, rows, (int)L, seed, rng_stream, rp);
+  return check_launch("kdfm_adapter_bwd");
+}
+
+int kdfm_fm_step_bias(const float* w_te, const float* b_te, const float* W1, const float* b1, float* cvec, float* evec,
+                      int64_t L, int64_t E, int64_t steps, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(w_te && b_te && W1 && b1 && cvec && evec, "null pointer");
+  KDFM_REQUIRE(steps >= 1 && steps <= 4096, "steps");
+  hipLaunchKernelGGL(fm_step_bias_kernel, dim3((unsigned)steps), dim3(256), 0, as_stream(stream), w_te, b_te, W1, b1,
+                     cvec, evec, (int)L, (int)E, (int)steps);
+  return check_launch("kdfm_fm_step_bias");
+}
+
+int kdfm_fm_time_bwd(const float* dc, const float* evec, const float* W1, float* dW1, float* db1, float* dw_te,
+                     float* db_te, int64_t L, int64_t E, int64_t steps, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(dc && evec && W1 && dW1 && db1 && dw_te && db_te, "null pointer");
+  hipLaunchKernelGGL(fm_time_bwd_kernel, dim3(1), dim3(256), 0, as_stream(stream), dc, evec, W1, dW1, db1, dw_te, db_te,
+                     (int)L, (int)E, (int)steps);
+  return check_launch("kdfm_fm_time_bwd");
+}
+
+int kdfm_relpos_table(float* pe, int64_t T, int64_t d, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(pe && T > 0 && d > 0 && (d % 2) == 0, "bad args");
+  KDFM_1D(relpos_table_kernel, (2 * T - 1) * d, pe, T, d);
+  return check_launch("kdfm_relpos_table");
+}
+
+int kdfm_subsample_lengths(const int64_t* wav_len, int64_t* mel_len, int64_t* len1, int64_t* len2, int64_t B,
+                           int64_t hop, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(wav_len && mel_len && hop > 0, "bad args");
+  if (B == 0) return KDFM_OK;
+  hipLaunchKernelGGL(lengths_kernel, dim3((unsigned)ceil_div(B, 64)), dim3(64), 0, as_stream(stream), wav_len, mel_len,
+                     len1, len2, B, hop);
+  return check_launch("kdfm_subsample_lengths");
+}
+
+int kdfm_step_advance(int64_t* step, uint64_t* seed, void* stream) {
+  using namespace kdfm;
+  hipLaunchKernelGGL(step_advance_kernel, dim3(1), dim3(64), 0, as_stream(stream), step, seed);
+  return check_launch("kdfm_step_advance");
+}
+
+}  // extern "C"

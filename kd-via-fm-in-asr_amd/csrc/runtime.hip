@@ -23,7 +23,7 @@ namespace {
 // out[n] (+)= sum_{m<M} X[m*ld + n]; grid.x over column blocks of 64, grid.y splits M; atomics
 // combine the row slabs (bias gradients: N <= 1024, M up to ~2e5 rows).
 __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ X, float* __restrict__ out,
-                                                     int64_t M, int64_t N, int64_t ld, int64_t rows_per) {
+                                                     int64_t M, int64_t N, int64_t ld, int64_t rows_per, float scale) {
   __shared__ float red[4][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t n = (int64_t)blockIdx.x * 64 + lane;
@@ -34,7 +34,7 @@ __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ X
     for (int64_t m = mb + w; m < me; m += 4) s += X[m * ld + n];
   red[w][lane] = s;
   __syncthreads();
-  if (w == 0 && n < N) atomicAdd(out + n, red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane]);
+  if (w == 0 && n < N) atomicAdd(out + n, scale * (red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane]));
 }
 
 __global__ void zero_kernel(float* out, int64_t n) {
@@ -64,7 +64,8 @@ int kdfm_device_arch(char* buf, int64_t len) {
   return KDFM_OK;
 }
 
-int kdfm_colsum(const float* X, float* out, int64_t M, int64_t N, int64_t ld, int32_t accumulate, void* stream) {
+int kdfm_colsum(const float* X, float* out, int64_t M, int64_t N, int64_t ld, float scale, int32_t accumulate,
+                void* stream) {
   using namespace kdfm;
   KDFM_REQUIRE(X && out, "null pointer");
   KDFM_REQUIRE(M >= 0 && N >= 0 && ld >= N, "bad shape");
@@ -79,7 +80,7 @@ int kdfm_colsum(const float* X, float* out, int64_t M, int64_t N, int64_t ld, in
   int64_t gy = ceil_div(M, 512);
   if (gy > 1024) gy = 1024;
   const int64_t rows_per = ceil_div(M, gy);
-  hipLaunchKernelGGL(colsum_kernel, dim3((unsigned)gx, (unsigned)gy), dim3(256), 0, st, X, out, M, N, ld, rows_per);
+  hipLaunchKernelGGL(colsum_kernel, dim3((unsigned)gx, (unsigned)gy), dim3(256), 0, st, X, out, M, N, ld, rows_per, scale);
   return check_launch("kdfm_colsum");
 }
 

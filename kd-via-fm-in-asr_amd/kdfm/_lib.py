@@ -28,6 +28,8 @@ EPI_DSILU = 1 << 6
 EPI_RESID = 1 << 7
 EPI_BETA = 1 << 8
 EPI_ATOMIC = 1 << 9
+EPI_ROWMASK = 1 << 10
+EPI_MSE = 1 << 11
 
 _i64 = C.c_int64
 _i32 = C.c_int32
@@ -48,6 +50,8 @@ class GemmDesc(C.Structure):
         ("splitk", _i32),
         ("conv_taps", _i32), ("conv_pad", _i32),
         ("conv_c", _i64), ("conv_t", _i64),
+        ("mask_len", _vp), ("mask_T", _i64), ("mask_div", _i64),
+        ("loss_acc", _vp), ("loss_scale", _f32),
     ]
 
 
@@ -59,7 +63,43 @@ SIGNATURES: dict[str, tuple] = {
     "kdfm_last_error": (C.c_char_p, []),
     "kdfm_device_arch": (_i32, [C.c_char_p, _i64]),
     "kdfm_gemm": (_i32, [C.POINTER(GemmDesc), P]),
-    "kdfm_colsum": (_i32, [P, P, _i64, _i64, _i64, _i32, P]),
+    "kdfm_colsum": (_i32, [P, P, _i64, _i64, _i64, _f32, _i32, P]),
+    "kdfm_preemph_pad": (_i32, [P, P, P, _i64, _i64, _i64, _f32, _f32, P, C.c_uint64, P]),
+    "kdfm_power_spectrum": (_i32, [P, P, _i64, _i64, P]),
+    "kdfm_logmel_normalize": (_i32, [P, P, P, _i64, _i64, _i64, _f32, P]),
+    "kdfm_specaugment": (_i32, [P, P, P, _i64, _i64, _i64, _i32, _i32, _i32, _f32, P, C.c_uint64, P]),
+    "kdfm_im2col_3x3s2": (_i32, [P, P, P, _i64, _i64, _i64, _i64, P]),
+    "kdfm_col2im_3x3s2": (_i32, [P, P, P, P, _i64, _i64, _i64, _i64, P]),
+    "kdfm_layernorm_fwd": (_i32, [P, P, P, P, P, P, _i64, _i64, _f32, P]),
+    "kdfm_layernorm_bwd": (_i32, [P, P, P, P, P, P, P, P, P, _i64, _i64, P]),
+    "kdfm_qkv_prep": (_i32, [P, P, P, P, P, _i64, _i64, P]),
+    "kdfm_relpos_softmax_fwd": (_i32, [P, P, P, P, P, _i64, _i64, _i64, _f32, _f32, P, C.c_uint64, P]),
+    "kdfm_relpos_softmax_bwd": (_i32, [P, P, P, P, _i64, _i64, _i64, _f32, _f32, P, C.c_uint64, P]),
+    "kdfm_relpos_table": (_i32, [P, _i64, _i64, P]),
+    "kdfm_glu_mask_fwd": (_i32, [P, P, P, _i64, _i64, _i64, P]),
+    "kdfm_glu_mask_bwd": (_i32, [P, P, P, P, _i64, _i64, _i64, P]),
+    "kdfm_dwconv_fwd": (_i32, [P, P, P, P, P, _i64, _i64, _i64, _i64, P]),
+    "kdfm_dwconv_bwd": (_i32, [P, P, P, P, P, P, _i64, _i64, _i64, _i64, P]),
+    "kdfm_bn_finalize": (_i32, [P, P, P, P, P, _i64, _i64, _f32, P]),
+    "kdfm_bn_running_update": (_i32, [P, P, P, _i64, _i64, _f32, P]),
+    "kdfm_bn_silu_fwd": (_i32, [P, P, P, P, P, P, _i64, _i64, P]),
+    "kdfm_bn_silu_bwd": (_i32, [P, P, P, P, P, P, P, P, P, P, _i64, _i64, _i32, P]),
+    "kdfm_log_softmax": (_i32, [P, P, _i64, _i64, _i64, _i64, P]),
+    "kdfm_ctc_loss": (_i32, [P, P, P, P, P, P, P, P, _i64, _i64, _i64, _i64, _i64, _f32, _i32, P]),
+    "kdfm_kl_div_logits": (_i32, [P, P, P, P, _i64, _i64, _f32, _f32, _f32, P]),
+    "kdfm_loss_combine": (_i32, [P, _i64, P, P, P, _f32, P, P]),
+    "kdfm_adapter_fwd": (_i32, [P, P, P, P, P, P, P, _i64, _i64, P, C.c_uint64, P]),
+    "kdfm_adapter_bwd": (_i32, [P, P, P, P, P, P, P, P, P, P, _i64, _i64, P, C.c_uint64, P]),
+    "kdfm_fm_step_bias": (_i32, [P, P, P, P, P, P, _i64, _i64, _i64, P]),
+    "kdfm_fm_time_bwd": (_i32, [P, P, P, P, P, P, P, _i64, _i64, _i64, P]),
+    "kdfm_fill": (_i32, [P, _f32, _i64, P]),
+    "kdfm_axpby": (_i32, [P, _i64, P, _i64, P, _i64, _i64, _i64, _f32, _f32, P]),
+    "kdfm_dropout": (_i32, [P, P, _i64, _f32, _f32, P, C.c_uint64, P]),
+    "kdfm_convw_prep": (_i32, [P, P, P, _i64, _i64, _i64, P]),
+    "kdfm_convw_grad": (_i32, [P, P, _i64, _i64, _i64, _f32, P]),
+    "kdfm_subsample_lengths": (_i32, [P, P, P, P, _i64, _i64, P]),
+    "kdfm_step_advance": (_i32, [P, P, P]),
+    "kdfm_adamw_noam": (_i32, [P, P, P, P, _i64, P, _f32, _f32, _f32, _f32, _f32, _f32, _f32, _f32, _f32, P, P]),
 }
 
 _LIB = None

@@ -1,0 +1,175 @@
+"""Configuration and NeMo state-dict naming of the ver5 FM-distillation step.
+
+Defaults follow the reference's canonical run (scripts/train/diffm_libri100_ver5.sh:10-26 ->
+asr_train_diffm.py argparse :1430-1648, ver5 construction :1892-1900) on the Conformer-CTC-small
+teacher recipe (NeMo/examples/asr/conf/conformer/conformer_ctc_bpe.yaml:10, 93-157, 180-196) with
+the student halved (asr_train_diffm.py:128-130).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field, replace
+
+
+@dataclass
+class Ver5Config:
+    # model
+    n_layers: int = 16
+    d_student: int = 88
+    heads_student: int = 2
+    d_teacher: int = 176
+    heads_teacher: int = 4
+    latent: int = 96
+    vocab: int = 128                 # decoder emits vocab + 1 classes, blank = vocab
+    conv_kernel: int = 31
+    ff_expansion: int = 4
+    # frontend (FilterbankFeatures defaults, audio_preprocessing.py:216-243)
+    sample_rate: int = 16000
+    n_fft: int = 512
+    win: int = 400
+    hop: int = 160
+    nfilt: int = 80
+    preemph: float = 0.97
+    dither: float = 1e-5
+    log_guard: float = 2.0 ** -24
+    # SpecAugment (conformer_ctc_bpe.yaml:108-114, Small row of the table at :10 -> 5 time masks)
+    specaug: bool = True
+    freq_masks: int = 2
+    freq_width: int = 27
+    time_masks: int = 5
+    time_width: float = 0.05
+    # heads (asr_train_diffm.py:539, 1804-1837)
+    fm_steps: int = 8
+    denoiser_steps: int = 9
+    time_embed_dim: int = 32
+    kd_alpha: float = 0.1
+    kd_temperature: float = 1.0
+    # regularisation (conformer_ctc_bpe.yaml:150-153)
+    dropout: float = 0.1
+    dropout_pre: float = 0.1
+    dropout_att: float = 0.1
+    subsampling_mask: bool = True
+    bn_momentum: float = 0.1
+    ln_eps: float = 1e-5
+    bn_eps: float = 1e-5
+    # optimizer (teacher .nemo optim: adamw + NoamAnnealing; Small lr 5.0)
+    lr: float = 5.0
+    betas: tuple = (0.9, 0.98)
+    weight_decay: float = 1e-3
+    adam_eps: float = 1e-8
+    warmup_steps: int = 10000
+    min_lr: float = 1e-6
+    sched_d_model: int = 88
+    # execution
+    math: str = "bf16"               # MFMA arithmetic: "bf16" (throughput) or "f32" (parity)
+    share_frontend: bool = True      # one mel frontend for student+teacher when dither == 0
+
+    @property
+    def classes(self) -> int:
+        return self.vocab + 1
+
+    def parity(self) -> "Ver5Config":
+        """Deterministic fp32 configuration used against the oracle."""
+        return replace(self, dither=0.0, specaug=False, dropout=0.0, dropout_pre=0.0, dropout_att=0.0, math="f32")
+
+
+# ------------------------------------------------------------------------------------------------
+# NeMo state-dict names.  The order below is also the layout of the flat
+# parameter buffer: q/k/v weights (and biases) are adjacent so one (3d, d) GEMM projects all three.
+# ------------------------------------------------------------------------------------------------
+
+def encoder_specs(cfg: Ver5Config, d: int, h: int, prefix: str) -> list:
+    C = d
+    F2 = cfg.nfilt // 4
+    ff = cfg.ff_expansion * d
+    dk = d // h
+    s = [
+        (prefix + "pre_encode.conv.0.weight", (C, 1, 3, 3)), (prefix + "pre_encode.conv.0.bias", (C,)),
+        (prefix + "pre_encode.conv.2.weight", (C, C, 3, 3)), (prefix + "pre_encode.conv.2.bias", (C,)),
+        (prefix + "pre_encode.out.weight", (d, C * F2)), (prefix + "pre_encode.out.bias", (d,)),
+    ]
+    for i in range(cfg.n_layers):
+        L = f"{prefix}layers.{i}."
+        s += [(L + "norm_feed_forward1.weight", (d,)), (L + "norm_feed_forward1.bias", (d,)),
+              (L + "feed_forward1.linear1.weight", (ff, d)), (L + "feed_forward1.linear1.bias", (ff,)),
+              (L + "feed_forward1.linear2.weight", (d, ff)), (L + "feed_forward1.linear2.bias", (d,)),
+              (L + "norm_self_att.weight", (d,)), (L + "norm_self_att.bias", (d,)),
+              (L + "self_attn.linear_q.weight", (d, d)), (L + "self_attn.linear_k.weight", (d, d)),
+              (L + "self_attn.linear_v.weight", (d, d)),
+              (L + "self_attn.linear_q.bias", (d,)), (L + "self_attn.linear_k.bias", (d,)),
+              (L + "self_attn.linear_v.bias", (d,)),
+              (L + "self_attn.linear_out.weight", (d, d)), (L + "self_attn.linear_out.bias", (d,)),
+              (L + "self_attn.linear_pos.weight", (d, d)),
+              (L + "self_attn.pos_bias_u", (h, dk)), (L + "self_attn.pos_bias_v", (h, dk)),
+              (L + "norm_conv.weight", (d,)), (L + "norm_conv.bias", (d,)),
+              (L + "conv.pointwise_conv1.weight", (2 * d, d, 1)), (L + "conv.pointwise_conv1.bias", (2 * d,)),
+              (L + "conv.depthwise_conv.weight", (d, 1, cfg.conv_kernel)), (L + "conv.depthwise_conv.bias", (d,)),
+              (L + "conv.batch_norm.weight", (d,)), (L + "conv.batch_norm.bias", (d,)),
+              (L + "conv.pointwise_conv2.weight", (d, d, 1)), (L + "conv.pointwise_conv2.bias", (d,)),
+              (L + "norm_feed_forward2.weight", (d,)), (L + "norm_feed_forward2.bias", (d,)),
+              (L + "feed_forward2.linear1.weight", (ff, d)), (L + "feed_forward2.linear1.bias", (ff,)),
+              (L + "feed_forward2.linear2.weight", (d, ff)), (L + "feed_forward2.linear2.bias", (d,)),
+              (L + "norm_out.weight", (d,)), (L + "norm_out.bias", (d,))]
+    return s
+
+
+def bn_buffer_specs(cfg: Ver5Config, d: int, prefix: str) -> list:
+    s = []
+    for i in range(cfg.n_layers):
+        L = f"{prefix}layers.{i}.conv.batch_norm."
+        s += [(L + "running_mean", (d,)), (L + "running_var", (d,))]
+    return s
+
+
+def decoder_specs(cfg: Ver5Config, d: int, prefix: str) -> list:
+    return [(prefix + "decoder_layers.0.weight", (cfg.classes, d, 1)), (prefix + "decoder_layers.0.bias", (cfg.classes,))]
+
+
+def head_specs(cfg: Ver5Config, fm_prefixes=("fm_latent.fm.",)) -> list:
+    L, Ct, Cs, E = cfg.latent, cfg.d_teacher, cfg.d_student, cfg.time_embed_dim
+    s = [("tae.enc.weight", (L, Ct, 1)), ("tae.enc.bias", (L,)),
+         ("tae.dec.weight", (Ct, L, 1)), ("tae.dec.bias", (Ct,)),
+         ("sproj.proj.weight", (L, Cs, 1)), ("sproj.proj.bias", (L,)),
+         ("adapter.gamma_head.0.weight", (L, L, 1)), ("adapter.gamma_head.0.bias", (L,)),
+         ("adapter.gamma_head.2.weight", (1, L, 1)), ("adapter.gamma_head.2.bias", (1,)),
+         ("denoiser.net.0.weight", (L, L, 3)), ("denoiser.net.0.bias", (L,)),
+         ("denoiser.net.2.weight", (L, L, 3)), ("denoiser.net.2.bias", (L,))]
+    for fm in fm_prefixes:
+        s += [(fm + "time_embed.weight", (E, 1)), (fm + "time_embed.bias", (E,)),
+              (fm + "meta_encoder.0.weight", (L, L + E)), (fm + "meta_encoder.0.bias", (L,)),
+              (fm + "meta_encoder.2.weight", (L, L)), (fm + "meta_encoder.2.bias", (L,)),
+              (fm + "shape_transformation_function.weight", (L, L)),
+              (fm + "shape_transformation_function.bias", (L,))]
+    return s
+
+
+def student_specs(cfg: Ver5Config) -> list:
+    """Trainable parameters of the ver5 step (fm_latent_2 exists in the reference but is unused by
+    ver5 and never receives a gradient, asr_train_diffm.py:564)."""
+    return (encoder_specs(cfg, cfg.d_student, cfg.heads_student, "encoder.")
+            + decoder_specs(cfg, cfg.d_student, "decoder.") + head_specs(cfg))
+
+
+def teacher_specs(cfg: Ver5Config) -> list:
+    return (encoder_specs(cfg, cfg.d_teacher, cfg.heads_teacher, "teacher.encoder.")
+            + decoder_specs(cfg, cfg.d_teacher, "teacher.decoder."))
+
+
+def fused_groups(specs: list) -> dict:
+    """name of fused view -> (first member, count, fused shape): q|k|v weights and biases."""
+    out = {}
+    names = [n for n, _ in specs]
+    shapes = dict(specs)
+    for n in names:
+        if n.endswith("self_attn.linear_q.weight"):
+            base = n[: -len("linear_q.weight")]
+            d = shapes[n][0]
+            out[base + "qkv.weight"] = (n, 3, (3 * d, d))
+            out[base + "qkv.bias"] = (base + "linear_q.bias", 3, (3 * d,))
+    return out
+
+
+DEFAULT = Ver5Config()
+PARITY = DEFAULT.parity()
+
+__all__ = ["Ver5Config", "DEFAULT", "PARITY", "encoder_specs", "decoder_specs", "head_specs", "student_specs",
+           "teacher_specs", "bn_buffer_specs", "fused_groups", "field"]

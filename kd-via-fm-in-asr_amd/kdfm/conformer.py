@@ -1,0 +1,408 @@
+"""Conformer encoder forward/backward on libkdfm kernels.
+
+Reference path: NeMo ConformerEncoder.forward_internal (conformer_encoder.py:595-761) with
+ConvSubsampling 'striding' (built :381-390, called :635), RelPositionalEncoding (:422-429, :658),
+_create_masks (:796-850) and 16 ConformerLayers (:450-472, :677-692) whose sources are absent from
+the snapshot (SURVEY.md Appendix A.3-A.8 restates them):
+  r = x + 0.5*drop(FF1(LN1 x)); r += drop(MHSA(LN2 r)); r += drop(Conv(LN3 r)); r += 0.5*drop(FF2(LN4 r));
+  out = LN5(r)
+Layout: channels-last rows = (utterance, frame); every per-layer output is written straight into
+slot i of a (n_layers, B*T', d) buffer — the tensors the reference's forward hooks capture
+(asr_train_diffm.py:584-596) — so the KD heads consume all layers as one row batch.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from . import _lib
+from . import kernels as K
+from .config import Ver5Config
+
+# dropout site ids (rng stream = model_salt * 4096 + layer * 16 + site)
+SITE_FF1_ACT, SITE_FF1_OUT, SITE_ATT_P, SITE_ATT_OUT, SITE_CONV_OUT, SITE_FF2_ACT, SITE_FF2_OUT = range(7)
+SITE_PRE = 15
+
+
+def _stream(salt, layer, site):
+    return salt * 4096 + (layer + 1) * 16 + site
+
+
+class EncoderShapes:
+    def __init__(self, cfg: Ver5Config, B: int, T_mel: int, d: int, h: int):
+        self.B, self.Tm, self.d, self.h = B, T_mel, d, h
+        self.dk = d // h
+        self.F1 = (cfg.nfilt - 1) // 2 + 1
+        self.T1 = (T_mel - 1) // 2 + 1
+        self.F2 = (self.F1 - 1) // 2 + 1
+        self.T = (self.T1 - 1) // 2 + 1
+        self.rows = B * self.T
+        self.ff = cfg.ff_expansion * d
+
+
+def _empty(*shape, dev):
+    return torch.empty(*shape, device=dev, dtype=torch.float32)
+
+
+# ------------------------------------------------------------------------------------------------
+# Subsampling (A.3): im2col + MFMA GEMM, ReLU and frame masks fused into the epilogues.
+# ------------------------------------------------------------------------------------------------
+
+def subsampling_forward(cfg, S: EncoderShapes, P, pre, mel, mel_len, len1, len2, *, train, seed, salt, save, ws):
+    dev = mel.device
+    B, C, d = S.B, S.d, S.d
+    cols0 = _empty(B * S.T1 * S.F1, 9, dev=dev)
+    K.im2col_3x3s2(mel, mel_len if cfg.subsampling_mask else None, cols0, B, S.Tm, cfg.nfilt, 1)
+    y1 = _empty(B * S.T1 * S.F1, C, dev=dev)
+    w0 = P[pre + "pre_encode.conv.0.weight"].view(C, 9)
+    K.linear(cols0, w0, P[pre + "pre_encode.conv.0.bias"], y1, epi=_lib.EPI_RELU,
+             rowmask=(len1, S.T1, S.F1) if cfg.subsampling_mask else None, math="f32")
+    cols1 = _empty(B * S.T * S.F2, 9 * C, dev=dev)
+    K.im2col_3x3s2(y1, len1 if cfg.subsampling_mask else None, cols1, B, S.T1, S.F1, C)
+    y2 = _empty(B * S.T * S.F2, C, dev=dev)
+    w2 = P[pre + "pre_encode.conv.2.weight"].view(C, 9 * C)
+    K.linear(cols1, w2, P[pre + "pre_encode.conv.2.bias"], y2, epi=_lib.EPI_RELU,
+             rowmask=(len2, S.T, S.F2) if cfg.subsampling_mask else None)
+    if not save:
+        del cols1
+    # Linear(C*F2 -> d) on channels-last (f, c) flattening: weight re-laid out (d, F2, C) on device
+    wout = ws["wout_perm"]
+    K.convw_prep(P[pre + "pre_encode.out.weight"].view(d, C, S.F2), fwd=wout)
+    xscale = math.sqrt(d)
+    bscaled = ws["bout_scaled"]
+    K.axpby(P[pre + "pre_encode.out.bias"].view(1, d), None, bscaled.view(1, d), alpha=xscale)
+    x = _empty(S.rows, d, dev=dev)
+    p_pre = cfg.dropout_pre if train else 0.0
+    K.linear(y2.view(S.rows, S.F2 * C), wout.view(d, S.F2 * C), bscaled, x, alpha=xscale, dropout_p=p_pre,
+             seed=seed, rng_stream=_stream(salt, -1, SITE_PRE))
+    ctx = None
+    if save:
+        ctx = dict(cols0=cols0, y1=y1, cols1=cols1, y2=y2, p_pre=p_pre, xscale=xscale)
+    return x, ctx
+
+
+def subsampling_backward(cfg, S: EncoderShapes, P, G, pre, ctx, dx, len1, *, seed, salt, ws):
+    dev = dx.device
+    B, C, d = S.B, S.d, S.d
+    dlin = _empty(S.rows, d, dev=dev)
+    K.dropout(dx, dlin, ctx["p_pre"], ctx["xscale"], seed, _stream(salt, -1, SITE_PRE))
+    y2 = ctx["y2"]
+    Gout = ws["wout_perm_grad"]
+    K.fill(Gout, 0.0)
+    K.linear_dw(dlin, y2.view(S.rows, S.F2 * C), Gout.view(d, S.F2 * C))
+    K.convw_grad(Gout, G[pre + "pre_encode.out.weight"].view(d, C, S.F2))
+    K.colsum(dlin, G[pre + "pre_encode.out.bias"])
+    dy2 = _empty(B * S.T * S.F2, C, dev=dev)
+    K.linear_dx(dlin, ws["wout_perm"].view(d, S.F2 * C), dy2.view(S.rows, S.F2 * C), epi=_lib.EPI_DRELU,
+                aux=y2.view(S.rows, S.F2 * C))
+    K.linear_dw(dy2, ctx["cols1"], G[pre + "pre_encode.conv.2.weight"].view(C, 9 * C))
+    K.colsum(dy2, G[pre + "pre_encode.conv.2.bias"])
+    dcols1 = _empty(B * S.T * S.F2, 9 * C, dev=dev)
+    K.linear_dx(dy2, P[pre + "pre_encode.conv.2.weight"].view(C, 9 * C), dcols1)
+    del dy2
+    dy1 = _empty(B * S.T1 * S.F1, C, dev=dev)
+    K.col2im_3x3s2(dcols1, len1 if cfg.subsampling_mask else None, ctx["y1"], dy1, B, S.T1, S.F1, C)
+    del dcols1
+    K.linear_dw(dy1, ctx["cols0"], G[pre + "pre_encode.conv.0.weight"].view(C, 9), math="f32")
+    K.colsum(dy1, G[pre + "pre_encode.conv.0.bias"])
+
+
+# ------------------------------------------------------------------------------------------------
+# One ConformerLayer
+# ------------------------------------------------------------------------------------------------
+
+def _ln(x, P, name, eps, dev, save_stats=True):
+    rows, d = x.shape
+    y = _empty(rows, d, dev=dev)
+    m = _empty(rows, dev=dev)
+    r = _empty(rows, dev=dev)
+    K.layernorm_fwd(x, P[name + ".weight"], P[name + ".bias"], y, m, r, eps)
+    return y, m, r
+
+
+def layer_forward(cfg, S: EncoderShapes, P, L, li, x, out, pos_emb, lengths, *, train, seed, salt, save,
+                  bn_update=None, rm_batch=True):
+    """x (rows, d) -> out (rows, d) (written in place).  Returns ctx for backward when save."""
+    dev = x.device
+    rows, d, H, dk, T, B, ff = S.rows, S.d, S.h, S.dk, S.T, S.B, S.ff
+    pd = cfg.dropout if train else 0.0
+    pa = cfg.dropout_att if train else 0.0
+    ctx = {} if save else None
+
+    def keep(**kw):
+        if save:
+            ctx.update(kw)
+
+    # ---- FFN1 (macaron half-step) ----
+    ln1, m1, r1 = _ln(x, P, L + "norm_feed_forward1", cfg.ln_eps, dev)
+    h1 = _empty(rows, ff, dev=dev) if save else None
+    a1 = _empty(rows, ff, dev=dev)
+    K.linear(ln1, P[L + "feed_forward1.linear1.weight"], P[L + "feed_forward1.linear1.bias"], a1,
+             epi=_lib.EPI_SILU | (_lib.EPI_STORE_PRE if save else 0), Cpre=h1, dropout_p=pd, seed=seed,
+             rng_stream=_stream(salt, li, SITE_FF1_ACT), tag="ffn_up")
+    x1 = _empty(rows, d, dev=dev)
+    K.linear(a1, P[L + "feed_forward1.linear2.weight"], P[L + "feed_forward1.linear2.bias"], x1,
+             epi=_lib.EPI_RESID, R=x, rscale=0.5, dropout_p=pd, seed=seed, rng_stream=_stream(salt, li, SITE_FF1_OUT))
+    keep(x=x, ln1=ln1, m1=m1, r1=r1, h1=h1, a1=a1)
+    del ln1, h1, a1
+
+    # ---- relative-position MHSA ----
+    ln2, m2, r2 = _ln(x1, P, L + "norm_self_att", cfg.ln_eps, dev)
+    qkv = _empty(rows, 3 * d, dev=dev)
+    K.linear(ln2, P[L + "self_attn.qkv.weight"], P[L + "self_attn.qkv.bias"], qkv)
+    qu = _empty(rows, d, dev=dev)
+    qv = _empty(rows, d, dev=dev)
+    K.qkv_prep(qkv, P[L + "self_attn.pos_bias_u"], P[L + "self_attn.pos_bias_v"], qu, qv)
+    npos = 2 * T - 1
+    ppos = _empty(npos, d, dev=dev)
+    K.linear(pos_emb, P[L + "self_attn.linear_pos.weight"], None, ppos)
+    ac = _empty(B, H, T, T, dev=dev)
+    # AC = (q+u) K^T  per (b,h): A(i,c)=qu[b,i,h*dk+c]  B(c,j)=K[b,j,h*dk+c]
+    K.gemm(qu, qkv[:, d:], ac, T, T, dk, d, 1, 1, 3 * d, T, 1, amode=_lib.LD_KC, bmode=_lib.LD_KC,
+           batch=(B, H), bA=(T * d, dk), bB=(T * 3 * d, dk), bC=(H * T * T, T * T))
+    bd = _empty(B, H, T, npos, dev=dev)
+    K.gemm(qv, ppos, bd, T, npos, dk, d, 1, 1, d, npos, 1, amode=_lib.LD_KC, bmode=_lib.LD_KC,
+           batch=(B, H), bA=(T * d, dk), bB=(0, dk), bC=(H * T * npos, T * npos))
+    Pm = _empty(B, H, T, T, dev=dev)
+    Pd = _empty(B, H, T, T, dev=dev) if pa > 0 else Pm
+    K.relpos_softmax_fwd(ac, bd, lengths, Pm, Pd if pa > 0 else None, B, H, T, 1.0 / math.sqrt(dk), pa, seed,
+                         _stream(salt, li, SITE_ATT_P))
+    del ac, bd
+    o = _empty(rows, d, dev=dev)
+    # O = Pd V : A = Pd (T x T), B(j,c) = V[b,j,h*dk+c]  -> o[b,i,h*dk+c]
+    K.gemm(Pd, qkv[:, 2 * d:], o, T, dk, T, T, 1, 3 * d, 1, d, 1, amode=_lib.LD_KC, bmode=_lib.LD_XC,
+           batch=(B, H), bA=(H * T * T, T * T), bB=(T * 3 * d, dk), bC=(T * d, dk))
+    x2 = _empty(rows, d, dev=dev)
+    K.linear(o, P[L + "self_attn.linear_out.weight"], P[L + "self_attn.linear_out.bias"], x2, epi=_lib.EPI_RESID,
+             R=x1, rscale=1.0, dropout_p=pd, seed=seed, rng_stream=_stream(salt, li, SITE_ATT_OUT))
+    keep(x1=x1, ln2=ln2, m2=m2, r2=r2, qkv=qkv, qu=qu, qv=qv, ppos=ppos, P=Pm, Pd=Pd, o=o, pa=pa)
+    del ln2, qkv, qu, qv, ppos, Pm, Pd, o
+
+    # ---- convolution module ----
+    ln3, m3, r3 = _ln(x2, P, L + "norm_conv", cfg.ln_eps, dev)
+    a = _empty(rows, 2 * d, dev=dev)
+    K.linear(ln3, P[L + "conv.pointwise_conv1.weight"].view(2 * d, d), P[L + "conv.pointwise_conv1.bias"], a)
+    g = _empty(rows, d, dev=dev)
+    K.glu_mask_fwd(a, lengths, g, B, T, d)
+    y = _empty(rows, d, dev=dev)
+    stats = torch.zeros(2 * d, device=dev, dtype=torch.float64) if rm_batch else None
+    K.dwconv_fwd(g, P[L + "conv.depthwise_conv.weight"].view(d, -1), P[L + "conv.depthwise_conv.bias"], y, stats,
+                 B, T, d, cfg.conv_kernel)
+    bmean = _empty(d, dev=dev)
+    brstd = _empty(d, dev=dev)
+    rmn, rvr = bn_update if bn_update is not None else (None, None)
+    K.bn_finalize(stats, rmn, rvr, bmean, brstd, d, rows, cfg.bn_eps)
+    if rm_batch and bn_update is not None and train:
+        K.bn_running_update(rmn, rvr, stats, d, rows, cfg.bn_momentum)
+    z = _empty(rows, d, dev=dev)
+    K.bn_silu_fwd(y, bmean, brstd, P[L + "conv.batch_norm.weight"], P[L + "conv.batch_norm.bias"], z)
+    x3 = _empty(rows, d, dev=dev)
+    K.linear(z, P[L + "conv.pointwise_conv2.weight"].view(d, d), P[L + "conv.pointwise_conv2.bias"], x3,
+             epi=_lib.EPI_RESID, R=x2, rscale=1.0, dropout_p=pd, seed=seed, rng_stream=_stream(salt, li, SITE_CONV_OUT))
+    keep(x2=x2, ln3=ln3, m3=m3, r3=r3, a=a, g=g, y=y, bmean=bmean, brstd=brstd, z=z, rm_batch=rm_batch)
+    del ln3, a, g, y, z
+
+    # ---- FFN2 ----
+    ln4, m4, r4 = _ln(x3, P, L + "norm_feed_forward2", cfg.ln_eps, dev)
+    h2 = _empty(rows, ff, dev=dev) if save else None
+    a2 = _empty(rows, ff, dev=dev)
+    K.linear(ln4, P[L + "feed_forward2.linear1.weight"], P[L + "feed_forward2.linear1.bias"], a2,
+             epi=_lib.EPI_SILU | (_lib.EPI_STORE_PRE if save else 0), Cpre=h2, dropout_p=pd, seed=seed,
+             rng_stream=_stream(salt, li, SITE_FF2_ACT), tag="ffn_up")
+    x4 = _empty(rows, d, dev=dev)
+    K.linear(a2, P[L + "feed_forward2.linear2.weight"], P[L + "feed_forward2.linear2.bias"], x4,
+             epi=_lib.EPI_RESID, R=x3, rscale=0.5, dropout_p=pd, seed=seed, rng_stream=_stream(salt, li, SITE_FF2_OUT))
+    # ---- norm_out -> hooked layer output ----
+    m5 = _empty(rows, dev=dev)
+    r5 = _empty(rows, dev=dev)
+    K.layernorm_fwd(x4, P[L + "norm_out.weight"], P[L + "norm_out.bias"], out, m5, r5, cfg.ln_eps)
+    keep(x3=x3, ln4=ln4, m4=m4, r4=r4, h2=h2, a2=a2, x4=x4, m5=m5, r5=r5, pd=pd)
+    return ctx
+
+
+def _ffn_backward(P, G, L, which, dres_out, ln, h, a, x_in_ln, m, r, norm, pd, seed, salt, li, site_act, site_out,
+                  dres_in, dev):
+    """Backward of r_out = r_in + 0.5*drop(W2 drop(silu(W1 LN(r_in)))) ; returns d r_in."""
+    rows, d = dres_out.shape
+    ff = h.shape[1]
+    dlin2 = _empty(rows, d, dev=dev)
+    K.dropout(dres_out, dlin2, pd, 0.5, seed, _stream(salt, li, site_out))
+    K.linear_dw(dlin2, a, G[L + which + ".linear2.weight"])
+    K.colsum(dlin2, G[L + which + ".linear2.bias"])
+    dh = _empty(rows, ff, dev=dev)
+    K.linear_dx(dlin2, P[L + which + ".linear2.weight"], dh, epi=_lib.EPI_DSILU, aux=h, dropout_p=pd, seed=seed,
+                rng_stream=_stream(salt, li, site_act))
+    del dlin2
+    K.linear_dw(dh, ln, G[L + which + ".linear1.weight"])
+    K.colsum(dh, G[L + which + ".linear1.bias"])
+    dln = _empty(rows, d, dev=dev)
+    K.linear_dx(dh, P[L + which + ".linear1.weight"], dln)
+    del dh
+    dx = _empty(rows, d, dev=dev)
+    K.layernorm_bwd(dln, x_in_ln, P[norm + ".weight"], m, r, dx, G[norm + ".weight"], G[norm + ".bias"],
+                    dres=dres_in)
+    return dx
+
+
+def layer_backward(cfg, S: EncoderShapes, P, G, L, li, ctx, dout, pos_emb, lengths, *, seed, salt):
+    """dout: grad wrt the layer output (rows, d). Returns grad wrt the layer input."""
+    dev = dout.device
+    rows, d, H, dk, T, B = S.rows, S.d, S.h, S.dk, S.T, S.B
+    pd = ctx["pd"]
+    # norm_out
+    dx4 = _empty(rows, d, dev=dev)
+    K.layernorm_bwd(dout, ctx["x4"], P[L + "norm_out.weight"], ctx["m5"], ctx["r5"], dx4, G[L + "norm_out.weight"],
+                    G[L + "norm_out.bias"])
+    # FFN2: x4 = x3 + 0.5 drop(ffn(LN4 x3))
+    dx3 = _ffn_backward(P, G, L, "feed_forward2", dx4, ctx["ln4"], ctx["h2"], ctx["a2"], ctx["x3"], ctx["m4"],
+                        ctx["r4"], L + "norm_feed_forward2", pd, seed, salt, li, SITE_FF2_ACT, SITE_FF2_OUT, dx4, dev)
+    del dx4
+    # conv module: x3 = x2 + drop(pw2(z))
+    dpw2 = _empty(rows, d, dev=dev)
+    K.dropout(dx3, dpw2, pd, 1.0, seed, _stream(salt, li, SITE_CONV_OUT))
+    K.linear_dw(dpw2, ctx["z"], G[L + "conv.pointwise_conv2.weight"].view(d, d))
+    K.colsum(dpw2, G[L + "conv.pointwise_conv2.bias"])
+    dz = _empty(rows, d, dev=dev)
+    K.linear_dx(dpw2, P[L + "conv.pointwise_conv2.weight"].view(d, d), dz)
+    del dpw2
+    dy = _empty(rows, d, dev=dev)
+    red = torch.empty(2 * d, device=dev, dtype=torch.float64)
+    K.bn_silu_bwd(dz, ctx["y"], ctx["bmean"], ctx["brstd"], P[L + "conv.batch_norm.weight"],
+                  P[L + "conv.batch_norm.bias"], red, dy, G[L + "conv.batch_norm.weight"],
+                  G[L + "conv.batch_norm.bias"], batch_stats=ctx["rm_batch"])
+    del dz
+    dg = _empty(rows, d, dev=dev)
+    K.dwconv_bwd(dy, ctx["g"], P[L + "conv.depthwise_conv.weight"].view(d, -1), dg,
+                 G[L + "conv.depthwise_conv.weight"].view(d, -1), G[L + "conv.depthwise_conv.bias"], B, T, d,
+                 cfg.conv_kernel)
+    del dy
+    da = _empty(rows, 2 * d, dev=dev)
+    K.glu_mask_bwd(dg, ctx["a"], lengths, da, B, T, d)
+    del dg
+    K.linear_dw(da, ctx["ln3"], G[L + "conv.pointwise_conv1.weight"].view(2 * d, d))
+    K.colsum(da, G[L + "conv.pointwise_conv1.bias"])
+    dln3 = _empty(rows, d, dev=dev)
+    K.linear_dx(da, P[L + "conv.pointwise_conv1.weight"].view(2 * d, d), dln3)
+    del da
+    dx2 = _empty(rows, d, dev=dev)
+    K.layernorm_bwd(dln3, ctx["x2"], P[L + "norm_conv.weight"], ctx["m3"], ctx["r3"], dx2, G[L + "norm_conv.weight"],
+                    G[L + "norm_conv.bias"], dres=dx3)
+    del dln3, dx3
+    # MHSA: x2 = x1 + drop(out(O))
+    dlo = _empty(rows, d, dev=dev)
+    K.dropout(dx2, dlo, pd, 1.0, seed, _stream(salt, li, SITE_ATT_OUT))
+    K.linear_dw(dlo, ctx["o"], G[L + "self_attn.linear_out.weight"])
+    K.colsum(dlo, G[L + "self_attn.linear_out.bias"])
+    do = _empty(rows, d, dev=dev)
+    K.linear_dx(dlo, P[L + "self_attn.linear_out.weight"], do)
+    del dlo
+    qkv, Pm, Pd, qu, qv, ppos = ctx["qkv"], ctx["P"], ctx["Pd"], ctx["qu"], ctx["qv"], ctx["ppos"]
+    npos = 2 * T - 1
+    dPd = _empty(B, H, T, T, dev=dev)
+    # dPd = dO V^T : A(i,c)=do[b,i,h*dk+c], B(c,j)=V[b,j,h*dk+c]
+    K.gemm(do, qkv[:, 2 * d:], dPd, T, T, dk, d, 1, 1, 3 * d, T, 1, amode=_lib.LD_KC, bmode=_lib.LD_KC,
+           batch=(B, H), bA=(T * d, dk), bB=(T * 3 * d, dk), bC=(H * T * T, T * T))
+    dac = _empty(B, H, T, T, dev=dev)
+    dbd = _empty(B, H, T, npos, dev=dev)
+    K.relpos_softmax_bwd(Pm, dPd, dac, dbd, B, H, T, 1.0 / math.sqrt(dk), ctx["pa"], seed,
+                         _stream(salt, li, SITE_ATT_P))
+    del dPd
+    dqkv = _empty(rows, 3 * d, dev=dev)
+    # dV = Pd^T dO : A(j,i) = Pd[i,j] (XC), B(i,c) = do[b,i,h*dk+c] (XC) -> dqkv[b,j,2d+h*dk+c]
+    K.gemm(Pd, do, dqkv[:, 2 * d:], T, dk, T, 1, T, d, 1, 3 * d, 1, amode=_lib.LD_XC, bmode=_lib.LD_XC,
+           batch=(B, H), bA=(H * T * T, T * T), bB=(T * d, dk), bC=(T * 3 * d, dk))
+    del do
+    dqu = _empty(rows, d, dev=dev)
+    # dQu = dAC K : A = dac (KC), B(j,c) = K[b,j,h*dk+c] (XC)
+    K.gemm(dac, qkv[:, d:], dqu, T, dk, T, T, 1, 3 * d, 1, d, 1, amode=_lib.LD_KC, bmode=_lib.LD_XC,
+           batch=(B, H), bA=(H * T * T, T * T), bB=(T * 3 * d, dk), bC=(T * d, dk))
+    # dK = dAC^T Qu : A(j,i) = dac[i,j] (XC), B(i,c) = qu (XC) -> dqkv[b,j,d+h*dk+c]
+    K.gemm(dac, qu, dqkv[:, d:], T, dk, T, 1, T, d, 1, 3 * d, 1, amode=_lib.LD_XC, bmode=_lib.LD_XC,
+           batch=(B, H), bA=(H * T * T, T * T), bB=(T * d, dk), bC=(T * 3 * d, dk))
+    del dac
+    dqv = _empty(rows, d, dev=dev)
+    # dQv = dBD Ppos : A = dbd (KC, T x npos), B(p,c) = ppos[p, h*dk+c] (XC)
+    K.gemm(dbd, ppos, dqv, T, dk, npos, npos, 1, d, 1, d, 1, amode=_lib.LD_KC, bmode=_lib.LD_XC,
+           batch=(B, H), bA=(H * T * npos, T * npos), bB=(0, dk), bC=(T * d, dk))
+    dppos = torch.zeros(npos, d, device=dev)
+    # dPpos[p, h*dk+c] += sum_b sum_i dbd[b,h,i,p] qv[b,i,h*dk+c]
+    K.gemm(dbd, qv, dppos, npos, dk, T, 1, npos, d, 1, d, 1, amode=_lib.LD_XC, bmode=_lib.LD_XC,
+           batch=(B, H), bA=(H * T * npos, T * npos), bB=(T * d, dk), bC=(0, dk), epi=_lib.EPI_ATOMIC)
+    del dbd
+    K.colsum(dqu, G[L + "self_attn.pos_bias_u"].view(-1))
+    K.colsum(dqv, G[L + "self_attn.pos_bias_v"].view(-1))
+    K.axpby(dqu, dqv, dqkv[:, :d], 1.0, 1.0)
+    del dqu, dqv
+    K.linear_dw(dppos, pos_emb, G[L + "self_attn.linear_pos.weight"])
+    del dppos
+    K.linear_dw(dqkv, ctx["ln2"], G[L + "self_attn.qkv.weight"])
+    K.colsum(dqkv, G[L + "self_attn.qkv.bias"])
+    dln2 = _empty(rows, d, dev=dev)
+    K.linear_dx(dqkv, P[L + "self_attn.qkv.weight"], dln2)
+    del dqkv
+    dx1 = _empty(rows, d, dev=dev)
+    K.layernorm_bwd(dln2, ctx["x1"], P[L + "norm_self_att.weight"], ctx["m2"], ctx["r2"], dx1,
+                    G[L + "norm_self_att.weight"], G[L + "norm_self_att.bias"], dres=dx2)
+    del dln2, dx2
+    # FFN1
+    dx = _ffn_backward(P, G, L, "feed_forward1", dx1, ctx["ln1"], ctx["h1"], ctx["a1"], ctx["x"], ctx["m1"],
+                       ctx["r1"], L + "norm_feed_forward1", pd, seed, salt, li, SITE_FF1_ACT, SITE_FF1_OUT, dx1, dev)
+    return dx
+
+
+# ------------------------------------------------------------------------------------------------
+# Whole encoder
+# ------------------------------------------------------------------------------------------------
+
+class EncoderRun:
+    """Forward state of one encoder pass (what backward needs)."""
+
+    def __init__(self):
+        self.sub = None
+        self.layers = []
+
+
+def encoder_forward(cfg, S: EncoderShapes, P, prefix, mel, mel_len, len1, len2, feats, pos_emb, *, train, seed,
+                    salt, save, bn_running=None, use_batch_stats=True, ws):
+    """mel (B, Tm, nfilt) -> feats (n_layers, rows, d) filled; returns EncoderRun when save."""
+    run = EncoderRun() if save else None
+    x, sctx = subsampling_forward(cfg, S, P, prefix, mel, mel_len, len1, len2, train=train, seed=seed, salt=salt,
+                                  save=save, ws=ws)
+    if save:
+        run.sub = sctx
+    for i in range(cfg.n_layers):
+        L = f"{prefix}layers.{i}."
+        bn = None
+        if bn_running is not None:
+            bn = (bn_running[L + "conv.batch_norm.running_mean"], bn_running[L + "conv.batch_norm.running_var"])
+        ctx = layer_forward(cfg, S, P, L, i, x, feats[i], pos_emb, len2, train=train, seed=seed, salt=salt,
+                            save=save, bn_update=bn, rm_batch=use_batch_stats)
+        if save:
+            run.layers.append(ctx)
+        x = feats[i]
+    return run
+
+
+def encoder_backward(cfg, S: EncoderShapes, P, G, prefix, run: EncoderRun, dfeats, pos_emb, len1, len2, *, seed,
+                     salt, ws):
+    """dfeats (n_layers, rows, d): grads wrt every hooked layer output (heads + decoder), summed into
+    the residual chain as the backward walks down the stack."""
+    dout = dfeats[cfg.n_layers - 1]
+    for i in range(cfg.n_layers - 1, -1, -1):
+        L = f"{prefix}layers.{i}."
+        dx = layer_backward(cfg, S, P, G, L, i, run.layers[i], dout, pos_emb, len2, seed=seed, salt=salt)
+        run.layers[i] = None
+        if i > 0:
+            K.axpby(dfeats[i - 1], dx, dfeats[i - 1], 1.0, 1.0)
+            dout = dfeats[i - 1]
+    subsampling_backward(cfg, S, P, G, prefix, run.sub, dx, len1, seed=seed, salt=salt, ws=ws)
+    run.sub = None
+
+
+def make_workspace(S: EncoderShapes, dev):
+    return {
+        "wout_perm": torch.empty(S.d, S.F2, S.d, device=dev),
+        "wout_perm_grad": torch.empty(S.d, S.F2, S.d, device=dev),
+        "bout_scaled": torch.empty(S.d, device=dev),
+    }

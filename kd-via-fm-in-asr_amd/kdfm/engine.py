@@ -1,0 +1,206 @@
+"""The ver5 FM-distillation training step as an explicit forward/backward schedule of libkdfm
+kernels (no autograd graph, no per-op Python autograd overhead, capturable as one HIP graph).
+
+Reference call stack: DistilFlowMatchingCTCModelBPE.training_step
+(asr_train_diffm.py:731-828) -> forward (:606-643) [student preprocessor + SpecAugment + encoder,
+teacher preprocessor + encoder under no_grad, decoder] -> CTC (:740-746) -> logit KD (:751-756)
+-> per-layer ver5 heads (:773-792) -> total (:803-811) -> Lightning backward -> AdamW + Noam.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from . import _lib
+from . import kernels as K
+from .config import Ver5Config, bn_buffer_specs, student_specs, teacher_specs
+from .conformer import EncoderShapes, encoder_backward, encoder_forward, make_workspace
+from .frontend import FrontendConsts, frontend_forward, mel_frames, specaugment_
+from .heads import HeadsWorkspace, heads_backward, heads_forward
+from .store import FlatStore, init_uniform
+
+SALT_STUDENT, SALT_TEACHER, SALT_FRONT = 1, 2, 3
+
+
+class Ver5Engine:
+    """Owns the student (trainable, flat buffer + AdamW state), the frozen teacher and all step
+    buffers on one device."""
+
+    def __init__(self, cfg: Ver5Config, device="cuda", *, teacher_seed=0, student_seed=1, heads_seed=2,
+                 init=True):
+        self.cfg = cfg
+        self.device = torch.device(device)
+        dev = self.device
+        self.student = FlatStore(student_specs(cfg), dev, with_grad=True, with_adam=True)
+        self.teacher = FlatStore(teacher_specs(cfg), dev, with_grad=False)
+        self.bn = FlatStore(bn_buffer_specs(cfg, cfg.d_student, "encoder.")
+                            + bn_buffer_specs(cfg, cfg.d_teacher, "teacher.encoder."), dev, with_grad=False)
+        self.fe = FrontendConsts(cfg, dev)
+        self.seed = torch.zeros(1, dtype=torch.int64, device=dev)     # uint64 bits, advanced on device
+        self.step = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.lr = torch.zeros(1, device=dev)
+        self.losses = torch.zeros(5, device=dev)                     # total, ctc, kl, recon, fm
+        self.hws = HeadsWorkspace(cfg, dev)
+        self._pos = {}
+        self._ws = {}
+        if init:
+            st = init_uniform(student_specs(cfg), student_seed)
+            hd = init_uniform([s for s in student_specs(cfg) if not s[0].startswith(("encoder.", "decoder."))],
+                              heads_seed)
+            st.update(hd)
+            self.student.load(st)
+            self.teacher.load(init_uniform(teacher_specs(cfg), teacher_seed))
+            self.reset_bn()
+
+    # ---------------------------------------------------------------------------------------------
+    def reset_bn(self):
+        for name, _ in self.bn.specs:
+            K.fill(self.bn.P[name], 1.0 if name.endswith("running_var") else 0.0)
+
+    def set_seed(self, seed: int):
+        self.seed.fill_(int(seed) & 0x7FFFFFFFFFFFFFFF)
+
+    @property
+    def seed_u64(self):
+        return self.seed  # passed as const uint64_t* (bit pattern)
+
+    def _pos_emb(self, T, d):
+        key = (T, d)
+        if key not in self._pos:
+            pe = torch.empty(2 * T - 1, d, device=self.device)
+            K.relpos_table(T, d, pe)
+            self._pos[key] = pe
+        return self._pos[key]
+
+    def _enc_ws(self, S):
+        key = (S.d, S.F2)
+        if key not in self._ws:
+            self._ws[key] = make_workspace(S, self.device)
+        return self._ws[key]
+
+    # ---------------------------------------------------------------------------------------------
+    def forward(self, wav, wav_len, targets, tgt_len, *, train=True, eps=None, save=True):
+        """One forward pass; returns the context backward() consumes.  eps: optional injected
+        NoiseAdapter noise (n_layers*B*T', latent) for parity runs."""
+        cfg = self.cfg
+        dev = self.device
+        B, N = wav.shape
+        Tm = mel_frames(cfg, N)
+        Ss = EncoderShapes(cfg, B, Tm, cfg.d_student, cfg.heads_student)
+        St = EncoderShapes(cfg, B, Tm, cfg.d_teacher, cfg.heads_teacher)
+        T = Ss.T
+        mel_len = torch.empty(B, dtype=torch.int64, device=dev)
+        len1 = torch.empty_like(mel_len)
+        len2 = torch.empty_like(mel_len)
+        K.subsample_lengths(wav_len, mel_len, len1, len2, cfg.hop)
+        seed = self.seed
+        # ---- frontends (teacher preprocessor is in eval mode: no dither) ----
+        dither = cfg.dither if train else 0.0
+        mel_t = frontend_forward(cfg, self.fe, wav, wav_len, mel_len, dither=0.0)
+        if train and (dither > 0.0 or not cfg.share_frontend):
+            mel_s = frontend_forward(cfg, self.fe, wav, wav_len, mel_len, dither=dither, seed=seed,
+                                     rng_stream=SALT_FRONT)
+        elif train and cfg.specaug:
+            mel_s = torch.empty_like(mel_t)
+            K.axpby(mel_t.view(B * Tm, -1), None, mel_s.view(B * Tm, -1), 1.0, 0.0)
+        else:
+            mel_s = mel_t
+        if train and cfg.specaug:
+            specaugment_(cfg, mel_s, mel_len, seed, SALT_FRONT + 1)
+        # ---- student encoder (saved for backward) ----
+        sfeats = torch.empty(cfg.n_layers, Ss.rows, Ss.d, device=dev)
+        pos_s = self._pos_emb(T, Ss.d)
+        srun = encoder_forward(cfg, Ss, self.student.P, "encoder.", mel_s, mel_len, len1, len2, sfeats, pos_s,
+                               train=train, seed=seed, salt=SALT_STUDENT, save=save, bn_running=self.bn.P,
+                               use_batch_stats=train, ws=self._enc_ws(Ss))
+        # ---- frozen teacher encoder (eval mode, nothing saved) ----
+        tfeats = torch.empty(cfg.n_layers, St.rows, St.d, device=dev)
+        encoder_forward(cfg, St, self.teacher.P, "teacher.encoder.", mel_t, mel_len, len1, len2, tfeats,
+                        self._pos_emb(T, St.d), train=False, seed=seed, salt=SALT_TEACHER, save=False,
+                        bn_running=self.bn.P, use_batch_stats=False, ws=self._enc_ws(St))
+        # ---- decoders, CTC, logit KD ----
+        Cn = cfg.classes
+        rows = Ss.rows
+        logits = torch.empty(rows, Cn, device=dev)
+        K.linear(sfeats[-1], self.student.P["decoder.decoder_layers.0.weight"].view(Cn, Ss.d),
+                 self.student.P["decoder.decoder_layers.0.bias"], logits)
+        lp = torch.empty(rows, Cn, device=dev)
+        K.log_softmax(logits, lp)
+        tlogits = torch.empty(rows, Cn, device=dev)
+        K.linear(tfeats[-1], self.teacher.P["teacher.decoder.decoder_layers.0.weight"].view(Cn, St.d),
+                 self.teacher.P["teacher.decoder.decoder_layers.0.bias"], tlogits)
+        Umax = targets.shape[1]
+        alpha_ws = torch.empty(B * T * (2 * Umax + 1), device=dev)
+        beta_ws = torch.empty_like(alpha_ws)
+        nll = torch.empty(B, device=dev)
+        glogits = torch.empty(rows, Cn, device=dev)
+        K.ctc_loss(lp, targets, len2, tgt_len, alpha_ws, beta_ws, nll, glogits, B, T, Cn, cfg.vocab, 1.0 / B)
+        del alpha_ws, beta_ws
+        acc = torch.zeros(3, device=dev)   # kl, recon, fm
+        Tk = cfg.kd_temperature
+        K.kl_div_logits(lp, tlogits, glogits, acc[0:1], Tk, cfg.kd_alpha * Tk / B, Tk * Tk / B)
+        # ---- ver5 heads over all layers at once ----
+        n = cfg.n_layers * rows
+        hctx = heads_forward(cfg, self.student.P, sfeats.view(n, Ss.d), tfeats.view(n, St.d), T, self.hws, acc[1:3],
+                             seed=seed, eps=eps, save=save)
+        K.loss_combine(nll, acc[0:1], acc[1:2], acc[2:3], cfg.kd_alpha, self.losses)
+        ctx = dict(B=B, T=T, Ss=Ss, St=St, mel_len=mel_len, len1=len1, len2=len2, srun=srun, sfeats=sfeats,
+                   glogits=glogits, hctx=hctx, lp=lp, nll=nll, pos_s=pos_s)
+        return ctx
+
+    def backward(self, ctx):
+        cfg = self.cfg
+        P, G = self.student.P, self.student.G
+        Ss = ctx["Ss"]
+        n = cfg.n_layers * Ss.rows
+        self.student.zero_grad()
+        dfeats = torch.empty(cfg.n_layers, Ss.rows, Ss.d, device=self.device)
+        heads_backward(cfg, P, G, ctx.pop("hctx"), self.hws, dfeats.view(n, Ss.d), seed=self.seed)
+        # decoder: logits = W enc + b ; grad wrt logits from CTC + KL
+        g = ctx.pop("glogits")
+        Cn = cfg.classes
+        Wd = P["decoder.decoder_layers.0.weight"].view(Cn, Ss.d)
+        K.linear_dw(g, ctx["sfeats"][-1], G["decoder.decoder_layers.0.weight"].view(Cn, Ss.d))
+        K.colsum(g, G["decoder.decoder_layers.0.bias"])
+        K.linear_dx(g, Wd, dfeats[-1], R=dfeats[-1], rscale=1.0)
+        del g
+        encoder_backward(cfg, Ss, P, G, "encoder.", ctx.pop("srun"), dfeats, ctx["pos_s"], ctx["len1"],
+                         ctx["len2"], seed=self.seed, salt=SALT_STUDENT, ws=self._enc_ws(Ss))
+
+    def optimizer_step(self, grad_scale: float = 1.0):
+        cfg = self.cfg
+        st = self.student
+        K.step_advance(self.step, None)
+        K.adamw_noam(st.data, st.grad, st.exp_avg, st.exp_avg_sq, self.step, cfg.lr, cfg.sched_d_model,
+                     cfg.warmup_steps, cfg.min_lr, cfg.betas[0], cfg.betas[1], cfg.adam_eps, cfg.weight_decay,
+                     grad_scale, self.lr)
+
+    def advance_rng(self):
+        K.step_advance(None, self.seed)
+
+    def train_step(self, wav, wav_len, targets, tgt_len, allreduce=None):
+        """forward + backward + (all-reduce) + AdamW.  Returns the device loss vector."""
+        self.advance_rng()
+        ctx = self.forward(wav, wav_len, targets, tgt_len, train=True)
+        self.backward(ctx)
+        del ctx
+        scale = 1.0
+        if allreduce is not None:
+            scale = allreduce(self.student.grad)
+        self.optimizer_step(scale)
+        return self.losses
+
+
+def synthetic_batch(cfg: Ver5Config, B: int, n_samples: int, U: int, device, seed: int = 1234, tgt_seed: int = 4321):
+    """wav = 0.1*N(0,1), all lengths N; U tokens uniform in [0, vocab)."""
+    g = torch.Generator().manual_seed(seed)
+    wav = (0.1 * torch.randn(B, n_samples, generator=g)).to(device)
+    wav_len = torch.full((B,), n_samples, dtype=torch.int64, device=device)
+    gt = torch.Generator().manual_seed(tgt_seed)
+    targets = torch.randint(0, cfg.vocab, (B, U), generator=gt, dtype=torch.int64).to(device)
+    tgt_len = torch.full((B,), U, dtype=torch.int64, device=device)
+    return wav, wav_len, targets, tgt_len
+
+
+__all__ = ["Ver5Engine", "synthetic_batch", "math", "_lib"]

@@ -1,7 +1,9 @@
 """Thin, typed Python wrappers over the libkdfm.so C-ABI (no autograd here).
 
-Tensors are torch CUDA tensors used purely as device allocations; every arithmetic operation
-runs in a libkdfm kernel on torch's current HIP stream.
+Tensors are torch CUDA tensors used purely as device allocations (the caching allocator owns the
+memory, torch's current HIP stream orders the work); every arithmetic operation runs in a libkdfm
+kernel.  Each wrapper validates shapes on the host before the launch, so a bad call raises here
+instead of faulting on the device.
 """
 from __future__ import annotations
 
@@ -19,6 +21,34 @@ class _State:
     math = "f32"
 
 
+class Trace:
+    """Brackets every GEMM launch carrying one of `tags` with HIP events on the launch stream
+    (bench.py's live per-kernel timing of the dominant kernel)."""
+    active = None
+
+    def __init__(self, tags):
+        self.tags = set(tags)
+        self.events = []   # (tag, flops, start, end)
+
+    def __enter__(self):
+        Trace.active = self
+        return self
+
+    def __exit__(self, *a):
+        Trace.active = None
+
+    def summary(self):
+        torch.cuda.synchronize()
+        out = {}
+        for tag, flops, s, e in self.events:
+            ms = s.elapsed_time(e)
+            t = out.setdefault(tag, [0, 0.0, 0.0])
+            t[0] += 1
+            t[1] += ms
+            t[2] += flops
+        return {k: {"launches": v[0], "ms_total": v[1], "flops_total": v[2]} for k, v in out.items()}
+
+
 def set_math(mode: str) -> None:
     if mode not in _MATH:
         raise ValueError(f"math mode must be one of {list(_MATH)}")
@@ -33,24 +63,42 @@ def stream_ptr() -> int:
     return torch.cuda.current_stream().cuda_stream
 
 
-def ptr(t: torch.Tensor | None) -> int | None:
+def ptr(t):
     if t is None:
         return None
     if not t.is_cuda:
         raise _lib.KdfmError("kdfm kernels need device tensors (HIP); got a CPU tensor")
-    if t.dtype not in (torch.float32, torch.int64, torch.int32, torch.uint64, torch.uint8, torch.bool):
-        raise _lib.KdfmError(f"unsupported dtype {t.dtype}")
     return t.data_ptr()
 
+
+def _f32(t, name="tensor"):
+    if t is not None and t.dtype != torch.float32:
+        raise _lib.KdfmError(f"{name} must be float32, got {t.dtype}")
+    return t
+
+
+def _i64(t, name="lengths"):
+    if t is not None and t.dtype != torch.int64:
+        raise _lib.KdfmError(f"{name} must be int64, got {t.dtype}")
+    return t
+
+
+def _s():
+    return stream_ptr()
+
+
+# ------------------------------------------------------------------------------------------------
+# GEMM
+# ------------------------------------------------------------------------------------------------
 
 def gemm(A, B, Cout, M, N, K, sAm, sAk, sBk, sBn, sCm, sCn, *, amode, bmode,
          batch=(1, 1), bA=(0, 0), bB=(0, 0), bC=(0, 0), alpha=1.0, epi=0, bias=None, R=None, rscale=1.0,
          aux=None, Cpre=None, beta=0.0, dropout_p=0.0, seed=None, rng_stream=0, splitk=1,
-         conv=None, math=None):
+         conv=None, math=None, rowmask=None, mse=None, tag=None):
     d = GemmDesc()
     d.A, d.B, d.C = ptr(A), ptr(B), ptr(Cout)
     d.bias, d.R, d.aux, d.Cpre = ptr(bias), ptr(R), ptr(aux), ptr(Cpre)
-    d.M, d.N, d.K = M, N, K
+    d.M, d.N, d.K = int(M), int(N), int(K)
     d.sAm, d.sAk, d.sBk, d.sBn, d.sCm, d.sCn = sAm, sAk, sBk, sBn, sCm, sCn
     d.batch1, d.batch2 = batch
     d.bA1, d.bA2 = bA
@@ -59,58 +107,317 @@ def gemm(A, B, Cout, M, N, K, sAm, sAk, sBk, sBn, sCm, sCn, *, amode, bmode,
     d.alpha, d.beta, d.rscale, d.dropout_p = alpha, beta, rscale, dropout_p
     d.seed = ptr(seed)
     d.rng_stream = rng_stream
+    if dropout_p > 0.0:
+        epi |= _lib.EPI_DROPOUT
     d.amode, d.bmode, d.epi = amode, bmode, epi
     d.math = _MATH[math or _State.math]
     d.splitk = splitk
     if conv is not None:
         d.conv_taps, d.conv_pad, d.conv_c, d.conv_t = conv
-    call("kdfm_gemm", C.byref(d), stream_ptr())
+    if rowmask is not None:
+        lens, T, div = rowmask
+        d.mask_len, d.mask_T, d.mask_div = ptr(_i64(lens)), int(T), int(div)
+        d.epi |= _lib.EPI_ROWMASK
+    if mse is not None:
+        acc, lscale = mse
+        d.loss_acc, d.loss_scale = ptr(acc), float(lscale)
+        d.epi |= _lib.EPI_MSE
+    tr = Trace.active
+    if tr is not None and tag in tr.tags:
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev0.record()
+        call("kdfm_gemm", C.byref(d), _s())
+        ev1.record()
+        tr.events.append((tag, 2.0 * M * N * K * batch[0] * batch[1], ev0, ev1))
+        return
+    call("kdfm_gemm", C.byref(d), _s())
 
 
 def _splitk_for(M, N, K):
     tiles = -(-M // 64) * -(-N // 64)
-    if K <= 256 or tiles >= 512:
+    if K <= 512 or tiles >= 256:
         return 1
-    want = max(1, 1024 // tiles)
-    return int(min(want, max(1, K // 256), 256))
+    want = max(1, 512 // tiles)
+    return int(min(want, max(1, K // 512), 1024))
 
 
-# ---------------- Linear-layer products on row-major 2-D views ---------------------------------
-
-def linear_fwd(x, W, bias, out, *, epi=0, R=None, rscale=1.0, Cpre=None, dropout_p=0.0, seed=None,
-               rng_stream=0, math=None):
-    """out[M,N] = epi(x[M,K] @ W[N,K]^T + bias)"""
+def linear(x, W, bias, out, *, epi=0, R=None, rscale=1.0, Cpre=None, dropout_p=0.0, seed=None, rng_stream=0,
+           alpha=1.0, math=None, rowmask=None, mse=None, tag=None):
+    """out[M,N] = epi(alpha * x[M,K] @ W[N,K]^T + bias)   (W may be a strided view)"""
     M, K = x.shape
     N = W.shape[0]
+    assert W.shape[1] == K and out.shape[0] == M and out.shape[1] == N, (x.shape, W.shape, out.shape)
     if bias is not None:
         epi |= _lib.EPI_BIAS
     gemm(x, W, out, M, N, K, x.stride(0), x.stride(1), W.stride(1), W.stride(0), out.stride(0), out.stride(1),
          amode=_lib.LD_KC, bmode=_lib.LD_KC, epi=epi, bias=bias, R=R, rscale=rscale, Cpre=Cpre,
-         dropout_p=dropout_p, seed=seed, rng_stream=rng_stream, math=math)
+         dropout_p=dropout_p, seed=seed, rng_stream=rng_stream, alpha=alpha, math=math, rowmask=rowmask, mse=mse,
+         tag=tag)
 
 
-def linear_dx(dy, W, dx, *, epi=0, aux=None, dropout_p=0.0, seed=None, rng_stream=0, beta=0.0, R=None,
-              rscale=1.0, math=None):
-    """dx[M,K] = epi(dy[M,N] @ W[N,K])"""
+def linear_dx(dy, W, dx, *, epi=0, aux=None, dropout_p=0.0, seed=None, rng_stream=0, R=None, rscale=1.0,
+              alpha=1.0, math=None):
+    """dx[M,K] = epi(alpha * dy[M,N] @ W[N,K])"""
     M, N = dy.shape
     K = W.shape[1]
+    assert W.shape[0] == N and dx.shape[0] == M and dx.shape[1] == K, (dy.shape, W.shape, dx.shape)
+    if R is not None:
+        epi |= _lib.EPI_RESID
     gemm(dy, W, dx, M, K, N, dy.stride(0), dy.stride(1), W.stride(0), W.stride(1), dx.stride(0), dx.stride(1),
          amode=_lib.LD_KC, bmode=_lib.LD_XC, epi=epi, aux=aux, dropout_p=dropout_p, seed=seed,
-         rng_stream=rng_stream, beta=beta, R=R, rscale=rscale, math=math)
+         rng_stream=rng_stream, R=R, rscale=rscale, alpha=alpha, math=math)
 
 
-def linear_dw(dy, x, dW, *, accumulate=False, math=None):
-    """dW[N,K] (+)= dy[M,N]^T @ x[M,K]   (split-K with f32 atomics)"""
+def linear_dw(dy, x, dW, *, alpha=1.0, math=None):
+    """dW[N,K] += alpha * dy[M,N]^T @ x[M,K]   (split-K, f32 atomics into the grad buffer)"""
     M, N = dy.shape
     K = x.shape[1]
-    if not accumulate:
-        dW.zero_()  # noqa: kernel-side memset via torch allocator (hipMemsetAsync)
+    assert x.shape[0] == M and dW.shape[0] == N and dW.shape[1] == K, (dy.shape, x.shape, dW.shape)
     sk = _splitk_for(N, K, M)
     gemm(dy, x, dW, N, K, M, dy.stride(1), dy.stride(0), x.stride(0), x.stride(1), dW.stride(0), dW.stride(1),
-         amode=_lib.LD_XC, bmode=_lib.LD_XC, epi=_lib.EPI_ATOMIC, splitk=sk, math=math)
+         amode=_lib.LD_XC, bmode=_lib.LD_XC, epi=_lib.EPI_ATOMIC, splitk=sk, alpha=alpha, math=math)
 
 
-def colsum(x2d, out, accumulate=False):
+def conv3(x, Wf, bias, out, T, *, epi=0, R=None, rscale=1.0, alpha=1.0, aux=None, math=None):
+    """Conv1d(k=3, pad=1) along frames on channels-last rows: out[r,o] = sum_{tap,c} Wf[o, tap*C+c] x[r+tap-1, c]
+    Wf: (O, 3*C) GEMM layout from kdfm_convw_prep; rows grouped in utterances of T frames."""
+    M, Cc = x.shape
+    O = Wf.shape[0]
+    assert Wf.shape[1] == 3 * Cc and x.stride(1) == 1
+    if bias is not None:
+        epi |= _lib.EPI_BIAS
+    if R is not None:
+        epi |= _lib.EPI_RESID
+    gemm(x, Wf, out, M, O, 3 * Cc, x.stride(0), 1, 1, Wf.stride(0), out.stride(0), out.stride(1),
+         amode=_lib.LD_CONV, bmode=_lib.LD_KC, epi=epi, bias=bias, R=R, rscale=rscale, alpha=alpha, aux=aux,
+         conv=(3, 1, Cc, T), math=math)
+
+
+def conv3_dw(dy, x, G, T, *, alpha=1.0, math=None):
+    """G[o, tap*C + c] += alpha * sum_r dy[r,o] x[r+tap-1, c]   (weight grad in GEMM layout)"""
+    M, O = dy.shape
+    Cc = x.shape[1]
+    assert G.shape == (O, 3 * Cc)
+    sk = _splitk_for(O, 3 * Cc, M)
+    gemm(dy, x, G, O, 3 * Cc, M, dy.stride(1), dy.stride(0), x.stride(0), 1, G.stride(0), 1,
+         amode=_lib.LD_XC, bmode=_lib.LD_CONV, epi=_lib.EPI_ATOMIC, splitk=sk, alpha=alpha,
+         conv=(3, 1, Cc, T), math=math)
+
+
+def colsum(x2d, out, *, scale=1.0, accumulate=True):
     M, N = x2d.shape
-    assert x2d.stride(1) == 1
-    call("kdfm_colsum", ptr(x2d), ptr(out), M, N, x2d.stride(0), int(accumulate), stream_ptr())
+    assert x2d.stride(1) == 1 and out.numel() == N
+    call("kdfm_colsum", ptr(x2d), ptr(out), M, N, x2d.stride(0), float(scale), int(accumulate), _s())
+
+
+# ------------------------------------------------------------------------------------------------
+# elementwise / glue
+# ------------------------------------------------------------------------------------------------
+
+def fill(x, value=0.0):
+    assert x.is_contiguous()
+    call("kdfm_fill", ptr(_f32(x)), float(value), x.numel(), _s())
+
+
+def axpby(a, b, out, alpha=1.0, beta=1.0):
+    """out = alpha*a + beta*b on 2-D (possibly row-strided) views; b may be None."""
+    rows, cols = out.shape
+    assert a.shape == out.shape and (b is None or b.shape == out.shape)
+    assert a.stride(1) == 1 and out.stride(1) == 1 and (b is None or b.stride(1) == 1)
+    call("kdfm_axpby", ptr(a), a.stride(0), ptr(b), b.stride(0) if b is not None else 0, ptr(out), out.stride(0),
+         rows, cols, float(alpha), float(beta), _s())
+
+
+def dropout(x, out, p, scale, seed, rng_stream):
+    assert x.is_contiguous() and out.is_contiguous() and x.numel() == out.numel()
+    call("kdfm_dropout", ptr(x), ptr(out), x.numel(), float(p), float(scale), ptr(seed), int(rng_stream), _s())
+
+
+def convw_prep(W, fwd=None, bwd=None):
+    O, I, K = W.shape
+    call("kdfm_convw_prep", ptr(W.contiguous()), ptr(fwd), ptr(bwd), O, I, K, _s())
+
+
+def convw_grad(G, dW, alpha=1.0):
+    O, I, K = dW.shape
+    assert G.numel() == dW.numel() and dW.is_contiguous()
+    call("kdfm_convw_grad", ptr(G), ptr(dW), O, I, K, float(alpha), _s())
+
+
+def subsample_lengths(wav_len, mel_len, len1, len2, hop):
+    call("kdfm_subsample_lengths", ptr(_i64(wav_len)), ptr(mel_len), ptr(len1), ptr(len2), wav_len.numel(), hop, _s())
+
+
+def step_advance(step, seed):
+    call("kdfm_step_advance", ptr(step), ptr(seed), _s())
+
+
+def relpos_table(T, d, out):
+    assert out.shape == (2 * T - 1, d)
+    call("kdfm_relpos_table", ptr(out), T, d, _s())
+
+
+# ------------------------------------------------------------------------------------------------
+# frontend / subsampling
+# ------------------------------------------------------------------------------------------------
+
+def preemph_pad(wav, lengths, xp, pad, preemph, dither, seed, rng_stream):
+    B, N = wav.shape
+    assert xp.shape == (B, N + 2 * pad) and wav.is_contiguous()
+    call("kdfm_preemph_pad", ptr(_f32(wav)), ptr(_i64(lengths)), ptr(xp), B, N, pad, float(preemph),
+         float(dither), ptr(seed), int(rng_stream), _s())
+
+
+def power_spectrum(spec, power):
+    rows, F = power.shape
+    assert spec.shape == (rows, 2 * F)
+    call("kdfm_power_spectrum", ptr(spec), ptr(power), rows, F, _s())
+
+
+def logmel_normalize(mel, seq_len, out, B, T, nf, guard):
+    call("kdfm_logmel_normalize", ptr(mel), ptr(_i64(seq_len)), ptr(out), B, T, nf, float(guard), _s())
+
+
+def specaugment(x, seq_len, B, T, nf, freq_masks, freq_width, time_masks, time_width, seed, rng_stream,
+                mask_out=None):
+    call("kdfm_specaugment", ptr(x), ptr(_i64(seq_len)), ptr(mask_out), B, T, nf, int(freq_masks),
+         int(freq_width), int(time_masks), float(time_width), ptr(seed), int(rng_stream), _s())
+
+
+def im2col_3x3s2(X, len_in, cols, B, T1, F1, Cc):
+    T2, F2 = (T1 - 1) // 2 + 1, (F1 - 1) // 2 + 1
+    assert cols.shape == (B * T2 * F2, 9 * Cc) and X.numel() == B * T1 * F1 * Cc
+    call("kdfm_im2col_3x3s2", ptr(X), ptr(_i64(len_in)), ptr(cols), B, T1, F1, Cc, _s())
+
+
+def col2im_3x3s2(dcols, len_in, relu_out, dX, B, T1, F1, Cc):
+    T2, F2 = (T1 - 1) // 2 + 1, (F1 - 1) // 2 + 1
+    assert dcols.shape == (B * T2 * F2, 9 * Cc) and dX.numel() == B * T1 * F1 * Cc
+    call("kdfm_col2im_3x3s2", ptr(dcols), ptr(_i64(len_in)), ptr(relu_out), ptr(dX), B, T1, F1, Cc, _s())
+
+
+# ------------------------------------------------------------------------------------------------
+# conformer layer pieces
+# ------------------------------------------------------------------------------------------------
+
+def layernorm_fwd(x, g, b, y, mean, rstd, eps):
+    rows, d = x.shape
+    assert x.is_contiguous() and y.is_contiguous() and mean.numel() == rows
+    call("kdfm_layernorm_fwd", ptr(x), ptr(g), ptr(b), ptr(y), ptr(mean), ptr(rstd), rows, d, float(eps), _s())
+
+
+def layernorm_bwd(dy, x, g, mean, rstd, dx, dg, db, dres=None):
+    rows, d = x.shape
+    assert dy.is_contiguous() and dx.is_contiguous() and (dres is None or dres.is_contiguous())
+    call("kdfm_layernorm_bwd", ptr(dy), ptr(x), ptr(g), ptr(mean), ptr(rstd), ptr(dres), ptr(dx), ptr(dg), ptr(db),
+         rows, d, _s())
+
+
+def qkv_prep(qkv, u, v, qu, qv):
+    rows, d = qu.shape
+    assert qkv.shape == (rows, 3 * d) and u.numel() == d and v.numel() == d
+    call("kdfm_qkv_prep", ptr(qkv), ptr(u), ptr(v), ptr(qu), ptr(qv), rows, d, _s())
+
+
+def relpos_softmax_fwd(ac, bd, lengths, P, Pd, B, H, T, scale, p, seed, rng_stream):
+    assert ac.numel() == B * H * T * T and bd.numel() == B * H * T * (2 * T - 1)
+    call("kdfm_relpos_softmax_fwd", ptr(ac), ptr(bd), ptr(_i64(lengths)), ptr(P), ptr(Pd), B, H, T, float(scale),
+         float(p), ptr(seed), int(rng_stream), _s())
+
+
+def relpos_softmax_bwd(P, dPd, dAC, dBD, B, H, T, scale, p, seed, rng_stream):
+    assert dBD.numel() == B * H * T * (2 * T - 1)
+    call("kdfm_relpos_softmax_bwd", ptr(P), ptr(dPd), ptr(dAC), ptr(dBD), B, H, T, float(scale), float(p), ptr(seed),
+         int(rng_stream), _s())
+
+
+def glu_mask_fwd(a, lengths, g, B, T, d):
+    call("kdfm_glu_mask_fwd", ptr(a), ptr(_i64(lengths)), ptr(g), B, T, d, _s())
+
+
+def glu_mask_bwd(dg, a, lengths, da, B, T, d):
+    call("kdfm_glu_mask_bwd", ptr(dg), ptr(a), ptr(_i64(lengths)), ptr(da), B, T, d, _s())
+
+
+def dwconv_fwd(g, w, bias, y, stats, B, T, d, K):
+    call("kdfm_dwconv_fwd", ptr(g), ptr(w), ptr(bias), ptr(y), ptr(stats), B, T, d, K, _s())
+
+
+def dwconv_bwd(dy, g, w, dg, dw, db, B, T, d, K):
+    call("kdfm_dwconv_bwd", ptr(dy), ptr(g), ptr(w), ptr(dg), ptr(dw), ptr(db), B, T, d, K, _s())
+
+
+def bn_finalize(stats, rm, rv, mean, rstd, d, count, eps):
+    call("kdfm_bn_finalize", ptr(stats), ptr(rm), ptr(rv), ptr(mean), ptr(rstd), d, int(count), float(eps), _s())
+
+
+def bn_running_update(rm, rv, stats, d, count, momentum):
+    call("kdfm_bn_running_update", ptr(rm), ptr(rv), ptr(stats), d, int(count), float(momentum), _s())
+
+
+def bn_silu_fwd(y, mean, rstd, g, b, z):
+    rows, d = y.shape
+    call("kdfm_bn_silu_fwd", ptr(y), ptr(mean), ptr(rstd), ptr(g), ptr(b), ptr(z), rows, d, _s())
+
+
+def bn_silu_bwd(dz, y, mean, rstd, g, b, red_ws, dy, dg, db, batch_stats=True):
+    rows, d = y.shape
+    call("kdfm_bn_silu_bwd", ptr(dz), ptr(y), ptr(mean), ptr(rstd), ptr(g), ptr(b), ptr(red_ws), ptr(dy), ptr(dg),
+         ptr(db), rows, d, int(batch_stats), _s())
+
+
+# ------------------------------------------------------------------------------------------------
+# losses / heads / optimizer
+# ------------------------------------------------------------------------------------------------
+
+def log_softmax(x, y):
+    rows, Cc = x.shape
+    call("kdfm_log_softmax", ptr(x), ptr(y), rows, Cc, x.stride(0), y.stride(0), _s())
+
+
+def ctc_loss(lp, targets, in_len, tgt_len, alpha_ws, beta_ws, nll, grad, B, T, Cc, blank, grad_scale,
+             zero_infinity=True):
+    Umax = targets.shape[1]
+    assert targets.dtype == torch.int64 and targets.is_contiguous()
+    assert alpha_ws.numel() >= B * T * (2 * Umax + 1) and beta_ws.numel() >= B * T * (2 * Umax + 1)
+    call("kdfm_ctc_loss", ptr(lp), ptr(targets), ptr(_i64(in_len)), ptr(_i64(tgt_len)), ptr(alpha_ws), ptr(beta_ws),
+         ptr(nll), ptr(grad), B, T, Cc, Umax, blank, float(grad_scale), int(zero_infinity), _s())
+
+
+def kl_div_logits(lp, tlogits, grad, loss_acc, temperature, grad_coef, loss_scale):
+    rows, Cc = lp.shape
+    call("kdfm_kl_div_logits", ptr(lp), ptr(tlogits), ptr(grad), ptr(loss_acc), rows, Cc, float(temperature),
+         float(grad_coef), float(loss_scale), _s())
+
+
+def loss_combine(nll, kl, recon, fm, kd_alpha, out5):
+    call("kdfm_loss_combine", ptr(nll), nll.numel(), ptr(kl), ptr(recon), ptr(fm), float(kd_alpha), ptr(out5), _s())
+
+
+def adapter_fwd(zs, h, w2, b2, eps_in, zn, gamma, seed, rng_stream):
+    rows, L = zs.shape
+    call("kdfm_adapter_fwd", ptr(zs), ptr(h), ptr(w2), ptr(b2), ptr(eps_in), ptr(zn), ptr(gamma), rows, L, ptr(seed),
+         int(rng_stream), _s())
+
+
+def adapter_bwd(dzn, zs, h, gamma, w2, eps_in, dzs, dh, dw2, db2, seed, rng_stream):
+    rows, L = zs.shape
+    call("kdfm_adapter_bwd", ptr(dzn), ptr(zs), ptr(h), ptr(gamma), ptr(w2), ptr(eps_in), ptr(dzs), ptr(dh),
+         ptr(dw2), ptr(db2), rows, L, ptr(seed), int(rng_stream), _s())
+
+
+def fm_step_bias(w_te, b_te, W1, b1, cvec, evec, L, E, steps):
+    call("kdfm_fm_step_bias", ptr(w_te), ptr(b_te), ptr(W1), ptr(b1), ptr(cvec), ptr(evec), L, E, steps, _s())
+
+
+def fm_time_bwd(dc, evec, W1, dW1, db1, dw_te, db_te, L, E, steps):
+    call("kdfm_fm_time_bwd", ptr(dc), ptr(evec), ptr(W1), ptr(dW1), ptr(db1), ptr(dw_te), ptr(db_te), L, E, steps,
+         _s())
+
+
+def adamw_noam(p, g, m, v, step, base_lr, d_model, warmup, min_lr, beta1, beta2, eps, wd, grad_scale, lr_out=None):
+    assert p.numel() == g.numel() == m.numel() == v.numel()
+    call("kdfm_adamw_noam", ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), ptr(step), float(base_lr), float(d_model),
+         float(warmup), float(min_lr), float(beta1), float(beta2), float(eps), float(wd), float(grad_scale),
+         ptr(lr_out), _s())

@@ -1,0 +1,106 @@
+"""Flat device buffers for parameters, gradients and optimizer state.
+
+Every trainable tensor of the step is a view into ONE contiguous fp32 buffer (and its gradient a
+view into one gradient buffer).  This is the MI355X layout choice that makes the data-parallel
+exchange a single large RCCL all-reduce and the optimizer a single fused AdamW launch, and it lets
+the fused q|k|v projection read three NeMo parameters as one (3d, d) matrix.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from . import kernels as K
+from .config import fused_groups
+
+ALIGN = 4  # floats (16 bytes): every tensor starts 16-B aligned for dwordx4 loads
+
+
+def _numel(shape):
+    return int(math.prod(shape)) if shape else 1
+
+
+class FlatStore:
+    def __init__(self, specs: list, device, with_grad: bool = True, with_adam: bool = False):
+        self.specs = list(specs)
+        self.device = torch.device(device)
+        self.offsets = {}
+        off = 0
+        for name, shape in self.specs:
+            self.offsets[name] = off
+            n = _numel(shape)
+            off += -(-n // ALIGN) * ALIGN
+        self.numel = off
+        self.data = torch.zeros(self.numel, device=self.device, dtype=torch.float32)
+        self.grad = torch.zeros(self.numel, device=self.device, dtype=torch.float32) if with_grad else None
+        self.exp_avg = torch.zeros_like(self.data) if with_adam else None
+        self.exp_avg_sq = torch.zeros_like(self.data) if with_adam else None
+        self.P = {}
+        self.G = {}
+        shapes = dict(self.specs)
+        for name, shape in self.specs:
+            o, n = self.offsets[name], _numel(shape)
+            self.P[name] = self.data[o:o + n].view(shape)
+            if self.grad is not None:
+                self.G[name] = self.grad[o:o + n].view(shape)
+        for fname, (first, count, fshape) in fused_groups(self.specs).items():
+            o = self.offsets[first]
+            n = _numel(fshape)
+            # members must be adjacent and unpadded for the fused view to be exact
+            assert _numel(shapes[first]) % ALIGN == 0, fname
+            self.P[fname] = self.data[o:o + n].view(fshape)
+            if self.grad is not None:
+                self.G[fname] = self.grad[o:o + n].view(fshape)
+
+    @property
+    def trainable_count(self) -> int:
+        return sum(_numel(s) for _, s in self.specs)
+
+    def load(self, state: dict, strict: bool = True) -> None:
+        """Copy a {name: tensor} dict (NeMo names) into the buffer (host->device upload)."""
+        missing = []
+        for name, shape in self.specs:
+            if name not in state:
+                missing.append(name)
+                continue
+            t = state[name]
+            if tuple(t.shape) != tuple(shape):
+                raise ValueError(f"{name}: shape {tuple(t.shape)} != {tuple(shape)}")
+            self.P[name].copy_(t.detach().to(torch.float32))
+        if strict and missing:
+            raise KeyError(f"missing parameters: {missing[:5]}{'...' if len(missing) > 5 else ''}")
+
+    def state_dict(self) -> dict:
+        return {name: self.P[name].detach().clone().cpu() for name, _ in self.specs}
+
+    def grads(self) -> dict:
+        return {name: self.G[name].detach().clone().cpu() for name, _ in self.specs}
+
+    def zero_grad(self) -> None:
+        if self.grad is not None:
+            K.fill(self.grad, 0.0)
+
+
+def init_uniform(specs: list, seed: int) -> dict:
+    """Seeded host-side init: U(-1/sqrt(fan_in), 1/sqrt(fan_in)) for weights/biases, ~1 for norm
+    scales, small normal for the relative-position biases (random-init weights for the benchmark;
+    the real teacher checkpoint needs a remote fetch)."""
+    g = torch.Generator().manual_seed(seed)
+    out = {}
+    shapes = dict(specs)
+    for name, shape in specs:
+        if (".norm_" in name or "batch_norm" in name) and name.endswith(".weight"):
+            t = 1.0 + 0.1 * (torch.rand(shape, generator=g) * 2 - 1)
+        elif (".norm_" in name or "batch_norm" in name) and name.endswith(".bias"):
+            t = 0.1 * (torch.rand(shape, generator=g) * 2 - 1)
+        elif "pos_bias" in name:
+            t = 0.1 * torch.randn(shape, generator=g)
+        else:
+            wname = name[: -len("bias")] + "weight" if name.endswith(".bias") else name
+            ws = shapes.get(wname, shape)
+            fan_in = _numel(ws[1:]) if len(ws) > 1 else ws[0]
+            s = 1.0 / math.sqrt(max(1, fan_in))
+            t = (torch.rand(shape, generator=g) * 2 - 1) * s
+        out[name] = t.float()
+    return out

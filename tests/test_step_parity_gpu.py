@@ -1,0 +1,107 @@
+"""Parity of the whole ver5 step (HIP path, f32 MFMA parity mode) against the CPU oracle.
+
+The oracle (oracle/ver5.py) is pinned to the reference's own KD-head classes by golden vectors and
+to NeMo's invariants; here the product (kdfm.engine.Ver5Engine, all libkdfm kernels) runs the same
+seeded weights and inputs and must match losses, the mel frontend, every hooked layer output and
+every trainable gradient.  Tolerances (fp32): losses rtol 2e-4; activations and gradients
+max|diff| <= 2e-3 * max|ref| per tensor (summation order differs: MFMA vs MKL, split-K atomics).
+"""
+import pytest
+import torch
+
+from oracle import ver5 as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _build(n_layers, B, N, lens, U, tl, seed=0):
+    from kdfm.config import PARITY
+    from dataclasses import replace
+    from kdfm.engine import Ver5Engine
+    cfg = replace(PARITY, n_layers=n_layers)
+    eng = Ver5Engine(cfg, "cuda", teacher_seed=seed, student_seed=seed + 1, heads_seed=seed + 2)
+    g = torch.Generator().manual_seed(seed + 10)
+    for name, _ in eng.bn.specs:   # non-trivial running stats for the eval-mode teacher
+        if name.startswith("teacher."):
+            v = (1.0 + 0.3 * torch.rand(eng.bn.P[name].shape, generator=g)) if name.endswith("running_var") else \
+                0.2 * torch.randn(eng.bn.P[name].shape, generator=g)
+            eng.bn.P[name].copy_(v)
+    wav = 0.1 * torch.randn(B, N, generator=g)
+    wl = torch.tensor(lens, dtype=torch.int64)
+    tg = torch.randint(0, cfg.vocab, (B, U), generator=g)
+    tgl = torch.tensor(tl, dtype=torch.int64)
+    return cfg, eng, wav, wl, tg, tgl, g
+
+
+def _oracle_params(cfg, eng):
+    ocfg = O.StepConfig(n_layers=cfg.n_layers)
+    p = {}
+    p.update(O.frontend_buffers(ocfg))
+    p.update(O.frontend_buffers(ocfg, "teacher.preprocessor.featurizer."))
+    p.update(eng.student.state_dict())
+    p.update(eng.teacher.state_dict())
+    for name, _ in eng.bn.specs:
+        p[name] = eng.bn.P[name].detach().cpu().clone()
+    return ocfg, p
+
+
+def _close(a, b, tol, what):
+    a = a.detach().float().cpu()
+    b = b.detach().float().cpu()
+    assert a.shape == b.shape, (what, a.shape, b.shape)
+    scale = b.abs().max().item()
+    err = (a - b).abs().max().item()
+    assert err <= tol * max(scale, 1e-6), f"{what}: max|diff| {err:.3e} vs max|ref| {scale:.3e}"
+
+
+@pytest.mark.parametrize("n_layers,B,N,lens,U,tl", [
+    (2, 2, 19200, [19200, 16123], 12, [12, 7]),
+    (16, 2, 16000, [16000, 12800], 10, [10, 6]),
+])
+def test_ver5_step_matches_oracle(n_layers, B, N, lens, U, tl):
+    cfg, eng, wav, wl, tg, tgl, g = _build(n_layers, B, N, lens, U, tl)
+    T = ((N // cfg.hop) + 1 - 1) // 2 + 1
+    T = (T - 1) // 2 + 1
+    eps_rows = torch.randn(n_layers * B * T, cfg.latent, generator=g)
+    ctx = eng.forward(wav.cuda(), wl.cuda(), tg.cuda(), tgl.cuda(), train=True, eps=eps_rows.cuda())
+    losses = eng.losses.detach().cpu().clone()
+    sfeats = ctx["sfeats"].detach().cpu().clone()
+    eng.backward(ctx)
+    torch.cuda.synchronize()
+    grads = eng.student.grads()
+
+    ocfg, p = _oracle_params(cfg, eng)
+    names = O.trainable_names(p)
+    for k in names:
+        p[k] = p[k].clone().requires_grad_(True)
+    eps_o = eps_rows.view(n_layers, B, T, cfg.latent).permute(0, 1, 3, 2)
+    out = O.ver5_step(p, wav, wl, tg, tgl, ocfg, eps_o)
+    ref = torch.stack([out["loss"], out["ctc"], out["kl"], out["recon"], out["fm"]]).detach()
+    torch.testing.assert_close(losses, ref, rtol=2e-4, atol=2e-4)
+    for i in range(n_layers):
+        _close(sfeats[i].view(B, T, -1), out["s_feats"][i], 2e-3, f"student layer {i} output")
+    og = torch.autograd.grad(out["loss"], [p[k] for k in names], allow_unused=True)
+    for k, gr in zip(names, og):
+        if gr is None:
+            gr = torch.zeros_like(p[k])
+        _close(grads[k], gr, 2e-3, f"grad {k}")
+
+
+def test_frontend_matches_oracle():
+    from kdfm.config import PARITY
+    from kdfm.frontend import FrontendConsts, frontend_forward
+    from kdfm import kernels as K
+    cfg = PARITY
+    g = torch.Generator().manual_seed(3)
+    B, N = 3, 48000
+    wav = 0.2 * torch.randn(B, N, generator=g)
+    wl = torch.tensor([N, 40001, 16000], dtype=torch.int64)
+    fe = FrontendConsts(cfg, "cuda")
+    ml = torch.empty(B, dtype=torch.int64, device="cuda")
+    K.subsample_lengths(wl.cuda(), ml, None, None, cfg.hop)
+    mel = frontend_forward(cfg, fe, wav.cuda(), wl.cuda(), ml, dither=0.0)
+    ocfg = O.StepConfig()
+    b = O.frontend_buffers(ocfg)
+    ref, rl = O.preprocess(wav, wl, b["preprocessor.featurizer.window"], b["preprocessor.featurizer.fb"][0], ocfg)
+    assert torch.equal(ml.cpu(), rl)
+    _close(mel.cpu().transpose(1, 2), ref, 2e-4, "log-mel")
