@@ -23,7 +23,7 @@ def test_linear_fwd_dx_dw(K, math, M, N, Kd):
     W = torch.randn(N, Kd, device="cuda", generator=g) * 0.1
     b = torch.randn(N, device="cuda", generator=g)
     y = torch.empty(M, N, device="cuda")
-    K.linear_fwd(x, W, b, y, math=math)
+    K.linear(x, W, b, y, math=math)
     ref = x @ W.T + b
     rt, at = _tol(math)
     torch.testing.assert_close(y, ref, rtol=rt, atol=at * ref.abs().max().item())
@@ -32,7 +32,7 @@ def test_linear_fwd_dx_dw(K, math, M, N, Kd):
     K.linear_dx(dy, W, dx, math=math)
     ref = dy @ W
     torch.testing.assert_close(dx, ref, rtol=rt, atol=at * ref.abs().max().item())
-    dW = torch.empty(N, Kd, device="cuda")
+    dW = torch.zeros(N, Kd, device="cuda")
     K.linear_dw(dy, x, dW, math=math)
     ref = dy.T @ x
     torch.testing.assert_close(dW, ref, rtol=rt, atol=at * ref.abs().max().item() + 1e-5)
@@ -49,7 +49,7 @@ def test_epilogues(K, math):
     R = torch.randn(M, N, device="cuda", generator=g)
     pre = torch.empty(M, N, device="cuda")
     out = torch.empty(M, N, device="cuda")
-    K.linear_fwd(x, W, b, out, epi=_lib.EPI_SILU | _lib.EPI_STORE_PRE | _lib.EPI_RESID, R=R, rscale=0.5,
+    K.linear(x, W, b, out, epi=_lib.EPI_SILU | _lib.EPI_STORE_PRE | _lib.EPI_RESID, R=R, rscale=0.5,
                  Cpre=pre, math=math)
     h = x @ W.T + b
     rt, at = _tol(math)

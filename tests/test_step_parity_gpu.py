@@ -4,7 +4,8 @@ The oracle (oracle/ver5.py) is pinned to the reference's own KD-head classes by 
 to NeMo's invariants; here the product (kdfm.engine.Ver5Engine, all libkdfm kernels) runs the same
 seeded weights and inputs and must match losses, the mel frontend, every hooked layer output and
 every trainable gradient.  Tolerances (fp32): losses rtol 2e-4; activations and gradients
-max|diff| <= 2e-3 * max|ref| per tensor (summation order differs: MFMA vs MKL, split-K atomics).
+max|diff| <= 2e-3 * max|ref| + 1e-6 per tensor (summation order differs: MFMA vs MKL, split-K
+atomics).
 """
 import pytest
 import torch
@@ -12,6 +13,10 @@ import torch
 from oracle import ver5 as O
 
 pytestmark = pytest.mark.gpu
+
+# gradients that vanish analytically: a key bias shifts every score of a query row by the same
+# constant (softmax-invariant); the depthwise-conv bias is removed by batch-statistics BatchNorm.
+ANALYTIC_ZERO = ("self_attn.linear_k.bias", "conv.depthwise_conv.bias")
 
 
 def _build(n_layers, B, N, lens, U, tl, seed=0):
@@ -45,13 +50,15 @@ def _oracle_params(cfg, eng):
     return ocfg, p
 
 
-def _close(a, b, tol, what):
+def _close(a, b, tol, what, atol=1e-6):
+    """max|a-b| <= tol*max|b| + atol.  The absolute floor covers gradients that are analytically
+    zero (e.g. linear_k.bias: a per-row constant shift of the scores cancels in the softmax)."""
     a = a.detach().float().cpu()
     b = b.detach().float().cpu()
     assert a.shape == b.shape, (what, a.shape, b.shape)
     scale = b.abs().max().item()
     err = (a - b).abs().max().item()
-    assert err <= tol * max(scale, 1e-6), f"{what}: max|diff| {err:.3e} vs max|ref| {scale:.3e}"
+    assert err <= tol * scale + atol, f"{what}: max|diff| {err:.3e} vs max|ref| {scale:.3e}"
 
 
 @pytest.mark.parametrize("n_layers,B,N,lens,U,tl", [
@@ -84,6 +91,12 @@ def test_ver5_step_matches_oracle(n_layers, B, N, lens, U, tl):
     for k, gr in zip(names, og):
         if gr is None:
             gr = torch.zeros_like(p[k])
+        if k.endswith(ANALYTIC_ZERO):
+            # both sides must be rounding noise; compare against the layer's weight-grad scale
+            ref_scale = grads[k.rsplit(".", 1)[0] + ".weight"].abs().max().item()
+            assert grads[k].abs().max().item() <= 1e-4 * ref_scale + 1e-6, k
+            assert gr.abs().max().item() <= 1e-4 * ref_scale + 1e-6, k
+            continue
         _close(grads[k], gr, 2e-3, f"grad {k}")
 
 
