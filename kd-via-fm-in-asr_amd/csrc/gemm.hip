@@ -81,6 +81,25 @@ __device__ __forceinline__ void load_tile_A(float (&v)[8], const float* base, in
     }
   } else {
     const int64_t r = r0 + (t >> 2), k = k0 + (t & 3) * 8;
+    if constexpr (MODE == KDFM_LD_CONV) {
+      // 8 consecutive k stay inside one tap when conv_c % 8 == 0: one validity test, 2x dwordx4
+      if (sq == 1 && (p.conv_c & 7) == 0 && r < R && k + 7 < Q) {
+        const int64_t tap = k / p.conv_c, c = k - tap * p.conv_c;
+        const int64_t tt = (r % p.conv_t) + tap - p.pad;
+        if (tt < 0 || tt >= p.conv_t) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) v[i] = 0.f;
+          return;
+        }
+        const float* src = base + (r + tap - p.pad) * sr + c;
+        if ((((uintptr_t)src) & 15) == 0) {
+          const float4* q4 = reinterpret_cast<const float4*>(src);
+          float4 a = q4[0], b = q4[1];
+          v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+          return;
+        }
+      }
+    }
     if (MODE == KDFM_LD_KC && sq == 1 && r < R && k + 7 < Q &&
         ((((uintptr_t)(base + r * sr + k)) & 15) == 0)) {
       const float4* q4 = reinterpret_cast<const float4*>(base + r * sr + k);
@@ -105,6 +124,22 @@ __device__ __forceinline__ void load_tile_B(float (&v)[8], const float* base, in
     load_tile_A<KDFM_LD_XC>(v, base, n0, k0, N, K, sBn, sBk, p);
   } else {
     const int64_t k = k0 + (t >> 3), n = n0 + (t & 7) * 8;
+    if (sBn == 1 && (p.conv_c & 7) == 0 && k < K && n + 7 < N) {
+      const int64_t tap = n / p.conv_c, c = n - tap * p.conv_c;
+      const int64_t tt = (k % p.conv_t) + tap - p.pad;
+      if (tt < 0 || tt >= p.conv_t) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = 0.f;
+        return;
+      }
+      const float* src = base + (k + tap - p.pad) * sBk + c;
+      if ((((uintptr_t)src) & 15) == 0) {
+        const float4* q4 = reinterpret_cast<const float4*>(src);
+        float4 a = q4[0], b = q4[1];
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+        return;
+      }
+    }
 #pragma unroll
     for (int i = 0; i < 8; ++i) v[i] = fetch_bconv(base, k, n + i, K, N, sBk, sBn, p);
   }

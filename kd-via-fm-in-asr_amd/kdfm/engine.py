@@ -73,6 +73,11 @@ class Ver5Engine:
             self._pos[key] = pe
         return self._pos[key]
 
+    def _side_stream(self):
+        if getattr(self, "_side", None) is None:
+            self._side = torch.cuda.Stream(self.device)
+        return self._side
+
     def _enc_ws(self, S):
         key = (S.d, S.F2)
         if key not in self._ws:
@@ -108,28 +113,37 @@ class Ver5Engine:
             mel_s = mel_t
         if train and cfg.specaug:
             specaugment_(cfg, mel_s, mel_len, seed, SALT_FRONT + 1)
+        Cn = cfg.classes
+        rows = Ss.rows
+        # ---- frozen teacher encoder + decoder (eval mode, nothing saved) on a second HIP stream:
+        # independent of the student until the KD losses, so the two encoders overlap on the CUs ----
+        tfeats = torch.empty(cfg.n_layers, St.rows, St.d, device=dev)
+        tlogits = torch.empty(rows, Cn, device=dev)
+        pos_t = self._pos_emb(T, St.d)
+        main = torch.cuda.current_stream(dev)
+        side = self._side_stream()
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            encoder_forward(cfg, St, self.teacher.P, "teacher.encoder.", mel_t, mel_len, len1, len2, tfeats,
+                            pos_t, train=False, seed=seed, salt=SALT_TEACHER, save=False,
+                            bn_running=self.bn.P, use_batch_stats=False, ws=self._enc_ws(St))
+            K.linear(tfeats[-1], self.teacher.P["teacher.decoder.decoder_layers.0.weight"].view(Cn, St.d),
+                     self.teacher.P["teacher.decoder.decoder_layers.0.bias"], tlogits)
+        for t in (tfeats, tlogits, mel_t, mel_len, len1, len2):
+            t.record_stream(side)
         # ---- student encoder (saved for backward) ----
         sfeats = torch.empty(cfg.n_layers, Ss.rows, Ss.d, device=dev)
         pos_s = self._pos_emb(T, Ss.d)
         srun = encoder_forward(cfg, Ss, self.student.P, "encoder.", mel_s, mel_len, len1, len2, sfeats, pos_s,
                                train=train, seed=seed, salt=SALT_STUDENT, save=save, bn_running=self.bn.P,
                                use_batch_stats=train, ws=self._enc_ws(Ss))
-        # ---- frozen teacher encoder (eval mode, nothing saved) ----
-        tfeats = torch.empty(cfg.n_layers, St.rows, St.d, device=dev)
-        encoder_forward(cfg, St, self.teacher.P, "teacher.encoder.", mel_t, mel_len, len1, len2, tfeats,
-                        self._pos_emb(T, St.d), train=False, seed=seed, salt=SALT_TEACHER, save=False,
-                        bn_running=self.bn.P, use_batch_stats=False, ws=self._enc_ws(St))
         # ---- decoders, CTC, logit KD ----
-        Cn = cfg.classes
-        rows = Ss.rows
         logits = torch.empty(rows, Cn, device=dev)
         K.linear(sfeats[-1], self.student.P["decoder.decoder_layers.0.weight"].view(Cn, Ss.d),
                  self.student.P["decoder.decoder_layers.0.bias"], logits)
         lp = torch.empty(rows, Cn, device=dev)
         K.log_softmax(logits, lp)
-        tlogits = torch.empty(rows, Cn, device=dev)
-        K.linear(tfeats[-1], self.teacher.P["teacher.decoder.decoder_layers.0.weight"].view(Cn, St.d),
-                 self.teacher.P["teacher.decoder.decoder_layers.0.bias"], tlogits)
+        main.wait_stream(side)
         Umax = targets.shape[1]
         alpha_ws = torch.empty(B * T * (2 * Umax + 1), device=dev)
         beta_ws = torch.empty_like(alpha_ws)
@@ -190,6 +204,37 @@ class Ver5Engine:
             scale = allreduce(self.student.grad)
         self.optimizer_step(scale)
         return self.losses
+
+
+class GraphedTrainStep:
+    """The whole training step captured as HIP graphs (fixed shapes, static input buffers):
+    graph A = RNG advance + forward + backward (both streams), then the optional eager RCCL
+    all-reduce of the flat gradient buffer, then graph B = fused AdamW.  Replays launch the ~3k
+    kernels of a step with no Python or per-launch host cost."""
+
+    def __init__(self, eng: Ver5Engine, wav, wav_len, targets, tgt_len, allreduce=None, world: int = 1):
+        self.eng = eng
+        self.inputs = (wav, wav_len, targets, tgt_len)
+        self.allreduce = allreduce
+        scale = 1.0 / world
+        self.g_step = torch.cuda.CUDAGraph()
+        self.g_opt = torch.cuda.CUDAGraph()
+        torch.cuda.synchronize()
+        with torch.cuda.graph(self.g_step):
+            eng.advance_rng()
+            ctx = eng.forward(*self.inputs, train=True)
+            eng.backward(ctx)
+            del ctx
+        with torch.cuda.graph(self.g_opt, pool=self.g_step.pool()):
+            eng.optimizer_step(scale)
+        torch.cuda.synchronize()
+
+    def step(self):
+        self.g_step.replay()
+        if self.allreduce is not None:
+            self.allreduce(self.eng.student.grad)
+        self.g_opt.replay()
+        return self.eng.losses
 
 
 def synthetic_batch(cfg: Ver5Config, B: int, n_samples: int, U: int, device, seed: int = 1234, tgt_seed: int = 4321):
