@@ -101,6 +101,11 @@ typedef struct kdfm_gemm_desc {
   /* EPI_MSE accumulator (device scalar) */
   float* loss_acc;
   float loss_scale;
+  /* implicit ones column (bias gradients fused into weight-gradient GEMMs): when ones_col >= 0,
+   * B(k, ones_col) = 1 for every k (B memory holds only ones_col columns) and output column
+   * ones_col is atomically added into ones_out[m] instead of C.  Requires EPI_ATOMIC. */
+  float* ones_out;
+  int64_t ones_col;
 } kdfm_gemm_desc;
 
 int kdfm_gemm(const kdfm_gemm_desc* d, void* stream);

@@ -31,6 +31,7 @@ struct P {
   int64_t conv_c, conv_t;
   const int64_t* mask_len; int64_t mask_T, mask_div;
   float* loss_acc; float loss_scale;
+  float* ones_out; int64_t ones_col;
 };
 
 // Operand element fetch for the "row operand" view: X(r, q) where r is the row-like index
@@ -115,8 +116,8 @@ __device__ __forceinline__ void load_tile_A(float (&v)[8], const float* base, in
 // B operand tile (n rows x k) staging.  KC: B(k,n) contiguous along k (W[n][k]);
 // XC: contiguous along n; CONV: k is a frame row, n = tap*C + c.
 template <int MODE>
-__device__ __forceinline__ void load_tile_B(float (&v)[8], const float* base, int64_t n0, int64_t k0,
-                                            int64_t N, int64_t K, int64_t sBk, int64_t sBn, const P& p) {
+__device__ __forceinline__ void load_tile_B_mem(float (&v)[8], const float* base, int64_t n0, int64_t k0,
+                                                int64_t N, int64_t K, int64_t sBk, int64_t sBn, const P& p) {
   const int t = threadIdx.x;
   if constexpr (MODE == KDFM_LD_KC) {
     load_tile_A<KDFM_LD_KC>(v, base, n0, k0, N, K, sBn, sBk, p);
@@ -142,6 +143,29 @@ __device__ __forceinline__ void load_tile_B(float (&v)[8], const float* base, in
     }
 #pragma unroll
     for (int i = 0; i < 8; ++i) v[i] = fetch_bconv(base, k, n + i, K, N, sBk, sBn, p);
+  }
+}
+
+// B staging with the optional implicit ones column at n == ones_col (memory holds ones_col columns)
+template <int MODE>
+__device__ __forceinline__ void load_tile_B(float (&v)[8], const float* base, int64_t n0, int64_t k0,
+                                            int64_t N, int64_t K, int64_t sBk, int64_t sBn, const P& p) {
+  if (p.ones_col < 0) {
+    load_tile_B_mem<MODE>(v, base, n0, k0, N, K, sBk, sBn, p);
+    return;
+  }
+  load_tile_B_mem<MODE>(v, base, n0, k0, p.ones_col, K, sBk, sBn, p);
+  const int t = threadIdx.x;
+  if constexpr (MODE == KDFM_LD_KC) {
+    const int64_t n = n0 + (t >> 2), k = k0 + (t & 3) * 8;
+    if (n == p.ones_col)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = (k + i < K) ? 1.f : 0.f;
+  } else {
+    const int64_t k = k0 + (t >> 3), n = n0 + (t & 7) * 8;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      if (n + i == p.ones_col) v[i] = (k < K) ? 1.f : 0.f;
   }
 }
 
@@ -273,7 +297,10 @@ __global__ __launch_bounds__(NT) void gemm_kernel(P p) {
         const int64_t off = cOff + m * p.sCm + n * p.sCn;
         float v = p.alpha * acc[i][j][r];
         if (epi & KDFM_EPI_ATOMIC) {
-          atomicAdd(p.C + off, v);
+          if (n == p.ones_col)
+            atomicAdd(p.ones_out + m, v);
+          else
+            atomicAdd(p.C + off, v);
           continue;
         }
         if (epi & KDFM_EPI_BIAS) v += p.bias[n];
@@ -361,6 +388,11 @@ extern "C" int kdfm_gemm(const kdfm_gemm_desc* d, void* stream) {
   p.conv_c = d->conv_c; p.conv_t = d->conv_t;
   p.mask_len = d->mask_len; p.mask_T = d->mask_T; p.mask_div = d->mask_div;
   p.loss_acc = d->loss_acc; p.loss_scale = d->loss_scale;
+  p.ones_out = d->ones_out; p.ones_col = d->ones_col;
+  if (d->ones_col >= 0)
+    KDFM_REQUIRE(d->ones_out && (d->epi & KDFM_EPI_ATOMIC) && d->ones_col == d->N - 1 && d->batch1 == 1 &&
+                     d->batch2 == 1,
+                 "ones column needs ATOMIC, ones_out, ones_col == N-1 and an unbatched GEMM");
   if (d->epi & KDFM_EPI_ROWMASK)
     KDFM_REQUIRE(d->mask_len && d->mask_T > 0 && d->mask_div > 0 && d->batch1 == 1 && d->batch2 == 1,
                  "ROWMASK needs mask_len/mask_T/mask_div and an unbatched GEMM");

@@ -20,40 +20,30 @@ int check_launch(const char* what) {
 }
 
 namespace {
-// out[n] (+)= scale * sum_{m<M} X[m*ld + n]  (bias gradients: N <= 2048, M up to ~2e5 rows).
-// Each block streams a slab of rows in flat (coalesced) order, accumulates per column in LDS with
-// LDS float atomics, then issues one global atomic per column.
+// out[n] (+)= scale * sum_{m<M} X[m*ld + n].  grid = (column groups of 64, row slabs); lane owns a
+// column, the 4 waves stride the slab's rows with 4 independent accumulators each (latency hiding),
+// LDS combine, one global atomic per column per block.
 __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ X, float* __restrict__ out,
                                                      int64_t M, int64_t N, int64_t ld, int64_t rows_per, float scale) {
-  __shared__ float acc[2048];
-  for (int64_t c = threadIdx.x; c < N; c += 256) acc[c] = 0.f;
-  __syncthreads();
-  const int64_t mb = (int64_t)blockIdx.x * rows_per;
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t n = (int64_t)blockIdx.x * 64 + lane;
+  const int64_t mb = (int64_t)blockIdx.y * rows_per;
   const int64_t me = (mb + rows_per < M) ? mb + rows_per : M;
-  if (me > mb) {
-    const int64_t cnt = (me - mb) * N;
-    if (ld == N) {
-      const float* base = X + mb * N;
-      int64_t c = threadIdx.x % N;
-      const int64_t step_c = 256 % N;
-      float part = 0.f;
-      for (int64_t i = threadIdx.x; i < cnt; i += 256) {
-        // column of element i advances by 256 % N each iteration; flush when it wraps
-        const float v = base[i];
-        atomicAdd(&acc[c], v);
-        c += step_c;
-        if (c >= N) c -= N;
-      }
-      (void)part;
-    } else {
-      for (int64_t i = threadIdx.x; i < cnt; i += 256) {
-        const int64_t r = i / N, c = i - r * N;
-        atomicAdd(&acc[c], X[(mb + r) * ld + c]);
-      }
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (n < N) {
+    int64_t m = mb + w;
+    for (; m + 12 < me; m += 16) {
+      s0 += X[m * ld + n];
+      s1 += X[(m + 4) * ld + n];
+      s2 += X[(m + 8) * ld + n];
+      s3 += X[(m + 12) * ld + n];
     }
+    for (; m < me; m += 4) s0 += X[m * ld + n];
   }
+  red[w][lane] = (s0 + s1) + (s2 + s3);
   __syncthreads();
-  for (int64_t c = threadIdx.x; c < N; c += 256) atomicAdd(out + c, scale * acc[c]);
+  if (w == 0 && n < N) atomicAdd(out + n, scale * (red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane]));
 }
 
 __global__ void zero_kernel(float* out, int64_t n) {
@@ -87,7 +77,7 @@ int kdfm_colsum(const float* X, float* out, int64_t M, int64_t N, int64_t ld, fl
                 void* stream) {
   using namespace kdfm;
   KDFM_REQUIRE(X && out, "null pointer");
-  KDFM_REQUIRE(M >= 0 && N >= 0 && ld >= N && N <= 2048, "bad shape (N <= 2048)");
+  KDFM_REQUIRE(M >= 0 && N >= 0 && ld >= N, "bad shape");
   hipStream_t st = as_stream(stream);
   if (!accumulate) {
     hipLaunchKernelGGL(zero_kernel, dim3((unsigned)ceil_div(N, 256)), dim3(256), 0, st, out, N);
@@ -95,11 +85,13 @@ int kdfm_colsum(const float* X, float* out, int64_t M, int64_t N, int64_t ld, fl
     if (rc) return rc;
   }
   if (M == 0 || N == 0) return KDFM_OK;
-  // ~16K elements per block, at most 1024 blocks
-  int64_t rows_per = ceil_div(16384, N);
-  if (ceil_div(M, rows_per) > 1024) rows_per = ceil_div(M, 1024);
-  const int64_t gx = ceil_div(M, rows_per);
-  hipLaunchKernelGGL(colsum_kernel, dim3((unsigned)gx), dim3(256), 0, st, X, out, M, N, ld, rows_per, scale);
+  const int64_t gx = ceil_div(N, 64);
+  int64_t gy = ceil_div(M, 128);
+  if (gy * gx > 2048) gy = (2048 + gx - 1) / gx;
+  const int64_t rows_per = ceil_div(M, gy);
+  gy = ceil_div(M, rows_per);
+  hipLaunchKernelGGL(colsum_kernel, dim3((unsigned)gx, (unsigned)gy), dim3(256), 0, st, X, out, M, N, ld, rows_per,
+                     scale);
   return check_launch("kdfm_colsum");
 }
 

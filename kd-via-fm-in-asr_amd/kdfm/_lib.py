@@ -52,6 +52,7 @@ class GemmDesc(C.Structure):
         ("conv_c", _i64), ("conv_t", _i64),
         ("mask_len", _vp), ("mask_T", _i64), ("mask_div", _i64),
         ("loss_acc", _vp), ("loss_scale", _f32),
+        ("ones_out", _vp), ("ones_col", _i64),
     ]
 
 

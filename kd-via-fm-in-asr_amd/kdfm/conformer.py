@@ -96,17 +96,15 @@ def subsampling_backward(cfg, S: EncoderShapes, P, G, pre, ctx, dx, len1, *, see
     dy2 = _empty(B * S.T * S.F2, C, dev=dev)
     K.linear_dx(dlin, ws["wout_perm"].view(d, S.F2 * C), dy2.view(S.rows, S.F2 * C), epi=_lib.EPI_DRELU,
                 aux=y2.view(S.rows, S.F2 * C))
-    K.linear_dw(dy2, ctx["cols1"], G[pre + "pre_encode.conv.2.weight"].view(C, 9 * C))
-    K.colsum(dy2, G[pre + "pre_encode.conv.2.bias"])
+    K.linear_dw(dy2, ctx["cols1"], G[pre + "pre_encode.conv.2.weight"].view(C, 9 * C), db=G[pre + "pre_encode.conv.2.bias"])
     dcols1 = _empty(B * S.T * S.F2, 9 * C, dev=dev)
     K.linear_dx(dy2, P[pre + "pre_encode.conv.2.weight"].view(C, 9 * C), dcols1)
     del dy2
     dy1 = _empty(B * S.T1 * S.F1, C, dev=dev)
     K.col2im_3x3s2(dcols1, len1 if cfg.subsampling_mask else None, ctx["y1"], dy1, B, S.T1, S.F1, C)
     del dcols1
-    K.linear_dw(dy1, ctx["cols0"], G[pre + "pre_encode.conv.0.weight"].view(C, 9), math="f32")
-    K.colsum(dy1, G[pre + "pre_encode.conv.0.bias"])
-
+    K.linear_dw(dy1, ctx["cols0"], G[pre + "pre_encode.conv.0.weight"].view(C, 9), math="f32", db=G[pre + "pre_encode.conv.0.bias"])
+    
 
 # ------------------------------------------------------------------------------------------------
 # One ConformerLayer
@@ -228,14 +226,12 @@ def _ffn_backward(P, G, L, which, dres_out, ln, h, a, x_in_ln, m, r, norm, pd, s
     ff = h.shape[1]
     dlin2 = _empty(rows, d, dev=dev)
     K.dropout(dres_out, dlin2, pd, 0.5, seed, _stream(salt, li, site_out))
-    K.linear_dw(dlin2, a, G[L + which + ".linear2.weight"])
-    K.colsum(dlin2, G[L + which + ".linear2.bias"])
+    K.linear_dw(dlin2, a, G[L + which + ".linear2.weight"], db=G[L + which + ".linear2.bias"])
     dh = _empty(rows, ff, dev=dev)
     K.linear_dx(dlin2, P[L + which + ".linear2.weight"], dh, epi=_lib.EPI_DSILU, aux=h, dropout_p=pd, seed=seed,
                 rng_stream=_stream(salt, li, site_act))
     del dlin2
-    K.linear_dw(dh, ln, G[L + which + ".linear1.weight"])
-    K.colsum(dh, G[L + which + ".linear1.bias"])
+    K.linear_dw(dh, ln, G[L + which + ".linear1.weight"], db=G[L + which + ".linear1.bias"])
     dln = _empty(rows, d, dev=dev)
     K.linear_dx(dh, P[L + which + ".linear1.weight"], dln)
     del dh
@@ -261,8 +257,7 @@ def layer_backward(cfg, S: EncoderShapes, P, G, L, li, ctx, dout, pos_emb, lengt
     # conv module: x3 = x2 + drop(pw2(z))
     dpw2 = _empty(rows, d, dev=dev)
     K.dropout(dx3, dpw2, pd, 1.0, seed, _stream(salt, li, SITE_CONV_OUT))
-    K.linear_dw(dpw2, ctx["z"], G[L + "conv.pointwise_conv2.weight"].view(d, d))
-    K.colsum(dpw2, G[L + "conv.pointwise_conv2.bias"])
+    K.linear_dw(dpw2, ctx["z"], G[L + "conv.pointwise_conv2.weight"].view(d, d), db=G[L + "conv.pointwise_conv2.bias"])
     dz = _empty(rows, d, dev=dev)
     K.linear_dx(dpw2, P[L + "conv.pointwise_conv2.weight"].view(d, d), dz)
     del dpw2
@@ -280,8 +275,7 @@ def layer_backward(cfg, S: EncoderShapes, P, G, L, li, ctx, dout, pos_emb, lengt
     da = _empty(rows, 2 * d, dev=dev)
     K.glu_mask_bwd(dg, ctx["a"], lengths, da, B, T, d)
     del dg
-    K.linear_dw(da, ctx["ln3"], G[L + "conv.pointwise_conv1.weight"].view(2 * d, d))
-    K.colsum(da, G[L + "conv.pointwise_conv1.bias"])
+    K.linear_dw(da, ctx["ln3"], G[L + "conv.pointwise_conv1.weight"].view(2 * d, d), db=G[L + "conv.pointwise_conv1.bias"])
     dln3 = _empty(rows, d, dev=dev)
     K.linear_dx(da, P[L + "conv.pointwise_conv1.weight"].view(2 * d, d), dln3)
     del da
@@ -292,8 +286,7 @@ def layer_backward(cfg, S: EncoderShapes, P, G, L, li, ctx, dout, pos_emb, lengt
     # MHSA: x2 = x1 + drop(out(O))
     dlo = _empty(rows, d, dev=dev)
     K.dropout(dx2, dlo, pd, 1.0, seed, _stream(salt, li, SITE_ATT_OUT))
-    K.linear_dw(dlo, ctx["o"], G[L + "self_attn.linear_out.weight"])
-    K.colsum(dlo, G[L + "self_attn.linear_out.bias"])
+    K.linear_dw(dlo, ctx["o"], G[L + "self_attn.linear_out.weight"], db=G[L + "self_attn.linear_out.bias"])
     do = _empty(rows, d, dev=dev)
     K.linear_dx(dlo, P[L + "self_attn.linear_out.weight"], do)
     del dlo
@@ -336,8 +329,7 @@ def layer_backward(cfg, S: EncoderShapes, P, G, L, li, ctx, dout, pos_emb, lengt
     del dqu, dqv
     K.linear_dw(dppos, pos_emb, G[L + "self_attn.linear_pos.weight"])
     del dppos
-    K.linear_dw(dqkv, ctx["ln2"], G[L + "self_attn.qkv.weight"])
-    K.colsum(dqkv, G[L + "self_attn.qkv.bias"])
+    K.linear_dw(dqkv, ctx["ln2"], G[L + "self_attn.qkv.weight"], db=G[L + "self_attn.qkv.bias"])
     dln2 = _empty(rows, d, dev=dev)
     K.linear_dx(dqkv, P[L + "self_attn.qkv.weight"], dln2)
     del dqkv

@@ -175,8 +175,7 @@ class Ver5Engine:
         g = ctx.pop("glogits")
         Cn = cfg.classes
         Wd = P["decoder.decoder_layers.0.weight"].view(Cn, Ss.d)
-        K.linear_dw(g, ctx["sfeats"][-1], G["decoder.decoder_layers.0.weight"].view(Cn, Ss.d))
-        K.colsum(g, G["decoder.decoder_layers.0.bias"])
+        K.linear_dw(g, ctx["sfeats"][-1], G["decoder.decoder_layers.0.weight"].view(Cn, Ss.d), db=G["decoder.decoder_layers.0.bias"])
         K.linear_dx(g, Wd, dfeats[-1], R=dfeats[-1], rscale=1.0)
         del g
         encoder_backward(cfg, Ss, P, G, "encoder.", ctx.pop("srun"), dfeats, ctx["pos_s"], ctx["len1"],

@@ -139,24 +139,22 @@ def heads_backward(cfg: Ver5Config, P, G, ctx, ws: HeadsWorkspace, ds_feats, *, 
     W2 = P[fm + "meta_encoder.2.weight"]
     # ---- FM loss: tr = Wst nsx + b ; d_tr given ----
     dtr = ctx["dtr"]
-    K.linear_dw(dtr, ctx["nsx"], G[fm + "shape_transformation_function.weight"])
-    K.colsum(dtr, G[fm + "shape_transformation_function.bias"])
+    K.linear_dw(dtr, ctx["nsx"], G[fm + "shape_transformation_function.weight"], db=G[fm + "shape_transformation_function.bias"])
     dnsx = _empty(n, Lt, dev=dev)
     K.linear_dx(dtr, P[fm + "shape_transformation_function.weight"], dnsx)
     # nsx = zd - v  ->  d zd += dnsx ; dv = -dnsx
     fx, fa = ctx["fx"], ctx["fa"]
     gx_next = None     # grad wrt fx[j+1]
+    K.fill(ws.dc, 0.0)
     for j in range(S_ - 1, -1, -1):
         if j == S_ - 1:
             gsrc, alpha = dnsx, -1.0          # dv_{S-1} = -dnsx
         else:
             gsrc, alpha = gx_next, -1.0 / S_  # dv_j = -(1/S) g_{x_{j+1}}
-        K.linear_dw(gsrc, fa[j], G[fm + "meta_encoder.2.weight"], alpha=alpha)
-        K.colsum(gsrc, G[fm + "meta_encoder.2.bias"], scale=alpha)
+        K.linear_dw(gsrc, fa[j], G[fm + "meta_encoder.2.weight"], alpha=alpha, db=G[fm + "meta_encoder.2.bias"])
         da = _empty(n, Lt, dev=dev)
         K.linear_dx(gsrc, W2, da, epi=_lib.EPI_DRELU, aux=fa[j], alpha=alpha)
-        K.linear_dw(da, fx[j], dW1x)
-        K.colsum(da, ws.dc[j], accumulate=False)
+        K.linear_dw(da, fx[j], dW1x, db=ws.dc[j])
         gx = _empty(n, Lt, dev=dev)
         if gx_next is None:
             K.linear_dx(da, W1x, gx)
@@ -177,12 +175,10 @@ def heads_backward(cfg: Ver5Config, P, G, ctx, ws: HeadsWorkspace, ds_feats, *, 
     K.fill(ws.g2, 0.0)
     for i in range(ds - 1, -1, -1):
         # x_{i+1} = x_i - (1/ds)(conv(a_i, W2) + b2)
-        K.conv3_dw(g, acts[i], ws.g2, T, alpha=-1.0 / ds)
-        K.colsum(g, G["denoiser.net.2.bias"], scale=-1.0 / ds)
+        K.conv3_dw(g, acts[i], ws.g2, T, alpha=-1.0 / ds, db=G["denoiser.net.2.bias"])
         da = _empty(n, Lt, dev=dev)
         K.conv3(g, ws.w2b, None, da, T, epi=_lib.EPI_DRELU, aux=acts[i], alpha=-1.0 / ds)
-        K.conv3_dw(da, xs[i], ws.g1, T)
-        K.colsum(da, G["denoiser.net.0.bias"])
+        K.conv3_dw(da, xs[i], ws.g1, T, db=G["denoiser.net.0.bias"])
         gi = _empty(n, Lt, dev=dev)
         K.conv3(da, ws.w1b, None, gi, T, R=g, rscale=1.0)
         g = gi
@@ -196,21 +192,18 @@ def heads_backward(cfg: Ver5Config, P, G, ctx, ws: HeadsWorkspace, ds_feats, *, 
     K.adapter_bwd(g, zs, hA, ctx["gamma"], P["adapter.gamma_head.2.weight"].view(-1), ctx["eps"], dzs_direct, dh,
                   G["adapter.gamma_head.2.weight"].view(-1), G["adapter.gamma_head.2.bias"], seed, SALT_HEADS)
     del g
-    K.linear_dw(dh, zs, G["adapter.gamma_head.0.weight"].view(Lt, Lt))
-    K.colsum(dh, G["adapter.gamma_head.0.bias"])
+    K.linear_dw(dh, zs, G["adapter.gamma_head.0.weight"].view(Lt, Lt), db=G["adapter.gamma_head.0.bias"])
     dzs = _empty(n, Lt, dev=dev)
     K.linear_dx(dh, P["adapter.gamma_head.0.weight"].view(Lt, Lt), dzs, R=dzs_direct, rscale=1.0)
     del dh, dzs_direct
     # ---- StudentProjector backward -> grads wrt the student layer outputs ----
-    K.linear_dw(dzs, ctx["s_feats"], G["sproj.proj.weight"].view(Lt, cfg.d_student))
-    K.colsum(dzs, G["sproj.proj.bias"])
+    K.linear_dw(dzs, ctx["s_feats"], G["sproj.proj.weight"].view(Lt, cfg.d_student), db=G["sproj.proj.bias"])
     K.linear_dx(dzs, P["sproj.proj.weight"].view(Lt, cfg.d_student), ds_feats)
     del dzs
     # ---- TeacherAutoEncoder backward (recon only; z_t is detached for the FM target) ----
     drec, zt = ctx["drec"], ctx["zt"]
-    K.linear_dw(drec, zt, G["tae.dec.weight"].view(Ct, Lt))
-    K.colsum(drec, G["tae.dec.bias"])
+    K.linear_dw(drec, zt, G["tae.dec.weight"].view(Ct, Lt), db=G["tae.dec.bias"])
     dzt = _empty(n, Lt, dev=dev)
     K.linear_dx(drec, P["tae.dec.weight"].view(Ct, Lt), dzt)
-    K.linear_dw(dzt, ctx["t_feats"], G["tae.enc.weight"].view(Lt, Ct))
-    K.colsum(dzt, G["tae.enc.bias"])
+    K.linear_dw(dzt, ctx["t_feats"], G["tae.enc.weight"].view(Lt, Ct), db=G["tae.enc.bias"])
+    

@@ -94,8 +94,11 @@ def _s():
 def gemm(A, B, Cout, M, N, K, sAm, sAk, sBk, sBn, sCm, sCn, *, amode, bmode,
          batch=(1, 1), bA=(0, 0), bB=(0, 0), bC=(0, 0), alpha=1.0, epi=0, bias=None, R=None, rscale=1.0,
          aux=None, Cpre=None, beta=0.0, dropout_p=0.0, seed=None, rng_stream=0, splitk=1,
-         conv=None, math=None, rowmask=None, mse=None, tag=None):
+         conv=None, math=None, rowmask=None, mse=None, tag=None, ones_out=None):
     d = GemmDesc()
+    d.ones_col = -1
+    if ones_out is not None:
+        d.ones_out, d.ones_col = ptr(ones_out), int(N) - 1
     d.A, d.B, d.C = ptr(A), ptr(B), ptr(Cout)
     d.bias, d.R, d.aux, d.Cpre = ptr(bias), ptr(R), ptr(aux), ptr(Cpre)
     d.M, d.N, d.K = int(M), int(N), int(K)
@@ -169,14 +172,16 @@ def linear_dx(dy, W, dx, *, epi=0, aux=None, dropout_p=0.0, seed=None, rng_strea
          rng_stream=rng_stream, R=R, rscale=rscale, alpha=alpha, math=math)
 
 
-def linear_dw(dy, x, dW, *, alpha=1.0, math=None):
-    """dW[N,K] += alpha * dy[M,N]^T @ x[M,K]   (split-K, f32 atomics into the grad buffer)"""
+def linear_dw(dy, x, dW, *, alpha=1.0, math=None, db=None):
+    """dW[N,K] += alpha * dy[M,N]^T @ x[M,K]; with db: db[N] += alpha * colsum(dy) fused as an
+    implicit ones column of x (split-K, f32 atomics into the grad buffer)"""
     M, N = dy.shape
     K = x.shape[1]
     assert x.shape[0] == M and dW.shape[0] == N and dW.shape[1] == K, (dy.shape, x.shape, dW.shape)
-    sk = _splitk_for(N, K, M)
-    gemm(dy, x, dW, N, K, M, dy.stride(1), dy.stride(0), x.stride(0), x.stride(1), dW.stride(0), dW.stride(1),
-         amode=_lib.LD_XC, bmode=_lib.LD_XC, epi=_lib.EPI_ATOMIC, splitk=sk, alpha=alpha, math=math)
+    Kx = K + (1 if db is not None else 0)
+    sk = _splitk_for(N, Kx, M)
+    gemm(dy, x, dW, N, Kx, M, dy.stride(1), dy.stride(0), x.stride(0), x.stride(1), dW.stride(0), dW.stride(1),
+         amode=_lib.LD_XC, bmode=_lib.LD_XC, epi=_lib.EPI_ATOMIC, splitk=sk, alpha=alpha, math=math, ones_out=db)
 
 
 def conv3(x, Wf, bias, out, T, *, epi=0, R=None, rscale=1.0, alpha=1.0, aux=None, math=None):
@@ -194,15 +199,17 @@ def conv3(x, Wf, bias, out, T, *, epi=0, R=None, rscale=1.0, alpha=1.0, aux=None
          conv=(3, 1, Cc, T), math=math)
 
 
-def conv3_dw(dy, x, G, T, *, alpha=1.0, math=None):
-    """G[o, tap*C + c] += alpha * sum_r dy[r,o] x[r+tap-1, c]   (weight grad in GEMM layout)"""
+def conv3_dw(dy, x, G, T, *, alpha=1.0, math=None, db=None):
+    """G[o, tap*C + c] += alpha * sum_r dy[r,o] x[r+tap-1, c]   (weight grad in GEMM layout);
+    with db: db[o] += alpha * sum_r dy[r,o] (implicit ones column)"""
     M, O = dy.shape
     Cc = x.shape[1]
     assert G.shape == (O, 3 * Cc)
-    sk = _splitk_for(O, 3 * Cc, M)
-    gemm(dy, x, G, O, 3 * Cc, M, dy.stride(1), dy.stride(0), x.stride(0), 1, G.stride(0), 1,
+    Nx = 3 * Cc + (1 if db is not None else 0)
+    sk = _splitk_for(O, Nx, M)
+    gemm(dy, x, G, O, Nx, M, dy.stride(1), dy.stride(0), x.stride(0), 1, G.stride(0), 1,
          amode=_lib.LD_XC, bmode=_lib.LD_CONV, epi=_lib.EPI_ATOMIC, splitk=sk, alpha=alpha,
-         conv=(3, 1, Cc, T), math=math)
+         conv=(3, 1, Cc, T), math=math, ones_out=db)
 
 
 def colsum(x2d, out, *, scale=1.0, accumulate=True):
