@@ -101,11 +101,9 @@ def main():
     eng.set_seed(1000 + rank)
     wav, wl, tg, tl = synthetic_batch(cfg, args.batch, args.samples, U_TOKENS, dev, seed=1234 + rank)
 
-    def allreduce(buf):
-        dist.all_reduce(buf)   # RCCL over xGMI: one flat-buffer all-reduce of all student grads
-        return 1.0 / world
-
-    ar = allreduce if world > 1 else None
+    from kdfm.ddp import FlatGradAllReduce, max_over_ranks
+    # RCCL over xGMI: one all-reduce of the flat 13.8 MB gradient buffer per step
+    ar = FlatGradAllReduce() if world > 1 else None
     # warm-up: one eager step (lazy buffers, allocator pools), graph capture, then replays
     eng.train_step(wav, wl, tg, tl, ar)
     if args.eager:
@@ -126,11 +124,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(time.perf_counter() - t0, dev)
     # dominant-kernel timing: one instrumented eager step right after the timed replays, every
     # ffn_up launch bracketed by HIP events on the stream it runs on (main or teacher stream)
     trace = K.Trace(["ffn_up"])

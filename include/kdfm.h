@@ -183,6 +183,10 @@ int kdfm_bn_silu_bwd(const float* dz, const float* y, const float* mean, const f
 
 /* ---------------- decoder / losses (conv_asr.py:456-468; losses/ctc.py:68-82; asr_train_diffm.py:740-811) */
 int kdfm_log_softmax(const float* x, float* y, int64_t rows, int64_t C, int64_t ldx, int64_t ldy, void* stream);
+/* idx[r] = argmax_c x[r, c] (first maximum) — greedy CTC predictions */
+int kdfm_argmax_rows(const float* x, int64_t* idx, int64_t rows, int64_t C, void* stream);
+/* dx = dy - exp(y) * rowsum(dy), y the log_softmax output (contiguous rows of C) */
+int kdfm_log_softmax_bwd(const float* dy, const float* y, float* dx, int64_t rows, int64_t C, void* stream);
 /* per-utterance CTC NLL and d(grad_scale * nll)/dlogits = grad_scale*(exp(lp) - posterior) */
 int kdfm_ctc_loss(const float* log_probs, const int64_t* targets, const int64_t* input_lengths,
                   const int64_t* target_lengths, float* alpha_ws, float* beta_ws, float* nll, float* grad, int64_t B,
@@ -212,6 +216,14 @@ int kdfm_axpby(const float* a, int64_t lda, const float* b, int64_t ldb, float* 
                int64_t cols, float alpha, float beta, void* stream);
 int kdfm_dropout(const float* x, float* out, int64_t n, float p, float scale, const uint64_t* seed,
                  uint64_t rng_stream, void* stream);
+/* out[r,c] = alpha * x[r,c] * s[r / rows_per_s]  (s: device scalars, e.g. upstream loss grads) */
+int kdfm_rowscale(const float* x, float* out, int64_t rows, int64_t cols, const float* s, int64_t rows_per_s,
+                  float alpha, void* stream);
+/* out = (y > 0) ? dy : 0 */
+int kdfm_relu_mask(const float* dy, const float* y, float* out, int64_t n, void* stream);
+/* nn.MSELoss pieces: *loss_acc += scale * sum (a-b)^2 ; grad = gscale * (a-b) when grad != NULL */
+int kdfm_mse(const float* a, const float* b, float* grad, float* loss_acc, int64_t n, float scale, float gscale,
+             void* stream);
 /* NeMo Conv1d weight (O,I,K) -> fwd (O,K,I) and transposed+flipped bwd (I,K,O) GEMM layouts */
 int kdfm_convw_prep(const float* W, float* fwd, float* bwd, int64_t O, int64_t I, int64_t K, void* stream);
 /* dW(O,I,K) += alpha * G(O,K,I) */

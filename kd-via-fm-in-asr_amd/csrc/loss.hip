@@ -45,6 +45,49 @@ __global__ __launch_bounds__(256) void log_softmax_kernel(const float* __restric
   }
 }
 
+// greedy CTC predictions: idx[r] = argmax_c x[r, c]   (log_probs.argmax(-1), asr_train_diffm.py:635)
+__global__ __launch_bounds__(256) void argmax_kernel(const float* __restrict__ x, int64_t* __restrict__ idx,
+                                                     int64_t rows, int C) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= rows) return;
+  float best = -INFINITY;
+  int bi = 0x7fffffff;
+  for (int c = lane; c < C; c += 64) {
+    const float v = x[r * C + c];
+    if (v > best) { best = v; bi = c; }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ob = __shfl_xor(best, o, 64);
+    const int oi = __shfl_xor(bi, o, 64);
+    if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+  }
+  if (lane == 0) idx[r] = bi;
+}
+
+// dx = dy - exp(y) * sum(dy)   (log_softmax backward, y = log_softmax output)
+__global__ __launch_bounds__(256) void log_softmax_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ y,
+                                                              float* __restrict__ dx, int64_t rows, int C) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= rows) return;
+  float g[4];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = lane + 64 * i;
+    g[i] = (c < C) ? dy[r * C + c] : 0.f;
+    s += g[i];
+  }
+  s = wave_sum(s);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = lane + 64 * i;
+    if (c < C) dx[r * C + c] = g[i] - __expf(y[r * C + c]) * s;
+  }
+}
+
 // One block per utterance.  alpha/beta workspaces (B, T, S) in log space; nll (B);
 // grad (B, T, C) = scale * (exp(lp) - posterior) for t < len, 0 beyond (or all 0 if infeasible).
 __global__ __launch_bounds__(256) void ctc_kernel(const float* __restrict__ lp, const int64_t* __restrict__ targets,
@@ -233,6 +276,25 @@ int kdfm_log_softmax(const float* x, float* y, int64_t rows, int64_t C, int64_t 
   hipLaunchKernelGGL(log_softmax_kernel, dim3((unsigned)ceil_div(rows, 4)), dim3(256), 0, as_stream(stream), x, y,
                      rows, (int)C, ldx, ldy);
   return check_launch("kdfm_log_softmax");
+}
+
+int kdfm_argmax_rows(const float* x, int64_t* idx, int64_t rows, int64_t C, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(x && idx && C > 0, "bad args");
+  if (rows == 0) return KDFM_OK;
+  hipLaunchKernelGGL(argmax_kernel, dim3((unsigned)ceil_div(rows, 4)), dim3(256), 0, as_stream(stream), x, idx, rows,
+                     (int)C);
+  return check_launch("kdfm_argmax_rows");
+}
+
+int kdfm_log_softmax_bwd(const float* dy, const float* y, float* dx, int64_t rows, int64_t C, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(dy && y && dx, "null pointer");
+  KDFM_REQUIRE(C > 0 && C <= 256, "classes in (0,256]");
+  if (rows == 0) return KDFM_OK;
+  hipLaunchKernelGGL(log_softmax_bwd_kernel, dim3((unsigned)ceil_div(rows, 4)), dim3(256), 0, as_stream(stream), dy, y,
+                     dx, rows, (int)C);
+  return check_launch("kdfm_log_softmax_bwd");
 }
 
 int kdfm_ctc_loss(const float* log_probs, const int64_t* targets, const int64_t* input_lengths,

@@ -24,6 +24,39 @@ __global__ __launch_bounds__(256) void axpby_kernel(const float* a, int64_t lda,
   out[r * ldo + c] = v;
 }
 
+// out[r, c] = x[r, c] * s[r / rows_per_s] * alpha   (device-scalar scaling, no host sync)
+__global__ __launch_bounds__(256) void rowscale_kernel(const float* x, float* out, int64_t rows, int64_t cols,
+                                                       const float* s, int64_t rows_per_s, float alpha) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= rows * cols) return;
+  const int64_t r = i / cols;
+  out[i] = x[i] * s[r / rows_per_s] * alpha;
+}
+
+// out = (y > 0) ? dy : 0   (ReLU backward from the saved activation)
+__global__ __launch_bounds__(256) void relu_mask_kernel(const float* dy, const float* y, float* out, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) out[i] = (y[i] > 0.f) ? dy[i] : 0.f;
+}
+
+// loss_acc[0] += scale * sum (a - b)^2 ; grad (optional) = gscale * (a - b)
+__global__ __launch_bounds__(256) void mse_kernel(const float* __restrict__ a, const float* __restrict__ b,
+                                                  float* __restrict__ grad, float* __restrict__ loss_acc, int64_t n,
+                                                  float scale, float gscale) {
+  __shared__ float red[4];
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  float part = 0.f;
+  if (i < n) {
+    const float d = a[i] - b[i];
+    part = d * d;
+    if (grad) grad[i] = gscale * d;
+  }
+  part = wave_sum(part);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = part;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(loss_acc, scale * (red[0] + red[1] + red[2] + red[3]));
+}
+
 // out = scale * dropout(x) with the flat-index mask of the GEMM epilogue (idx = r*cols + c)
 __global__ __launch_bounds__(256) void dropout_kernel(const float* x, float* out, int64_t n, float p, float scale,
                                                       const uint64_t* seed_ptr, uint64_t st) {
@@ -240,6 +273,29 @@ int kdfm_dropout(const float* x, float* out, int64_t n, float p, float scale, co
   KDFM_REQUIRE(p >= 0.f && p < 1.f && (p == 0.f || seed), "dropout p / seed");
   KDFM_1D(dropout_kernel, n, x, out, n, p, scale, seed, rng_stream);
   return check_launch("kdfm_dropout");
+}
+
+int kdfm_rowscale(const float* x, float* out, int64_t rows, int64_t cols, const float* s, int64_t rows_per_s,
+                  float alpha, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(x && out && s && rows_per_s > 0, "bad args");
+  KDFM_1D(rowscale_kernel, rows * cols, x, out, rows, cols, s, rows_per_s, alpha);
+  return check_launch("kdfm_rowscale");
+}
+
+int kdfm_relu_mask(const float* dy, const float* y, float* out, int64_t n, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(dy && y && out, "null pointer");
+  KDFM_1D(relu_mask_kernel, n, dy, y, out, n);
+  return check_launch("kdfm_relu_mask");
+}
+
+int kdfm_mse(const float* a, const float* b, float* grad, float* loss_acc, int64_t n, float scale, float gscale,
+             void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(a && b && loss_acc, "null pointer");
+  KDFM_1D(mse_kernel, n, a, b, grad, loss_acc, n, scale, gscale);
+  return check_launch("kdfm_mse");
 }
 
 int kdfm_qkv_prep(const float* qkv, const float* pos_bias_u, const float* pos_bias_v, float* qu, float* qv,

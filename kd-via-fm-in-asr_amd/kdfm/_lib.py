@@ -86,6 +86,8 @@ SIGNATURES: dict[str, tuple] = {
     "kdfm_bn_silu_fwd": (_i32, [P, P, P, P, P, P, _i64, _i64, P]),
     "kdfm_bn_silu_bwd": (_i32, [P, P, P, P, P, P, P, P, P, P, _i64, _i64, _i32, P]),
     "kdfm_log_softmax": (_i32, [P, P, _i64, _i64, _i64, _i64, P]),
+    "kdfm_argmax_rows": (_i32, [P, P, _i64, _i64, P]),
+    "kdfm_log_softmax_bwd": (_i32, [P, P, P, _i64, _i64, P]),
     "kdfm_ctc_loss": (_i32, [P, P, P, P, P, P, P, P, _i64, _i64, _i64, _i64, _i64, _f32, _i32, P]),
     "kdfm_kl_div_logits": (_i32, [P, P, P, P, _i64, _i64, _f32, _f32, _f32, P]),
     "kdfm_loss_combine": (_i32, [P, _i64, P, P, P, _f32, P, P]),
@@ -95,6 +97,9 @@ SIGNATURES: dict[str, tuple] = {
     "kdfm_fm_time_bwd": (_i32, [P, P, P, P, P, P, P, _i64, _i64, _i64, P]),
     "kdfm_fill": (_i32, [P, _f32, _i64, P]),
     "kdfm_axpby": (_i32, [P, _i64, P, _i64, P, _i64, _i64, _i64, _f32, _f32, P]),
+    "kdfm_rowscale": (_i32, [P, P, _i64, _i64, P, _i64, _f32, P]),
+    "kdfm_relu_mask": (_i32, [P, P, P, _i64, P]),
+    "kdfm_mse": (_i32, [P, P, P, P, _i64, _f32, _f32, P]),
     "kdfm_dropout": (_i32, [P, P, _i64, _f32, _f32, P, C.c_uint64, P]),
     "kdfm_convw_prep": (_i32, [P, P, P, _i64, _i64, _i64, P]),
     "kdfm_convw_grad": (_i32, [P, P, _i64, _i64, _i64, _f32, P]),

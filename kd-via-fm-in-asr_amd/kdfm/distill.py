@@ -1,0 +1,574 @@
+"""ver5 KD head modules and the distillation model with the reference's API
+(asr_train_diffm.py:400-497 heads, :500-838 DistilFlowMatchingCTCModelBPE, :1270-1427
+FlowMatchingModule), running on libkdfm kernels through autograd Functions.
+
+Tensors at the module boundary are (B, C, T) like the reference's Conv1d-based heads; internally
+every head works on channels-last rows, so the (B, C, T) tensors the model passes around are views
+of (B, T, C) storage and no transposes are materialised.  The module path keeps the reference's
+per-layer loop for API fidelity; the production step (Ver5Engine) runs the same kernels once over
+all layers and as one captured graph (see `to_engine`).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as nn
+
+from . import _lib
+from . import kernels as K
+from .config import Ver5Config
+from .nemo import AudioToMelSpectrogramPreprocessor, ConformerEncoder, ConvASRDecoder, CTCLoss, \
+    SpectrogramAugmentation, _dev_check, _ReduceFn
+
+_SALT_ADAPTER = 77
+
+
+def _rows(x_bct):
+    """(B, C, T) view -> contiguous (B*T, C) rows (free when the view came from (B, T, C) storage)."""
+    B, Cc, T = x_bct.shape
+    return x_bct.transpose(1, 2).contiguous().view(B * T, Cc)
+
+
+def _bct(rows, B, T):
+    return rows.view(B, T, -1).transpose(1, 2)
+
+
+def _zeros(*shape, dev):
+    t = torch.empty(*shape, device=dev)
+    K.fill(t, 0.0)
+    return t
+
+
+class _Conv1x1Fn(torch.autograd.Function):
+    """y = W x + b over channels (Conv1d kernel_size=1) on channels-last rows."""
+
+    @staticmethod
+    def forward(ctx, x_rows, W, b, epi):
+        O = W.shape[0]
+        y = torch.empty(x_rows.shape[0], O, device=x_rows.device)
+        K.linear(x_rows, W.view(O, -1), b, y, epi=epi)
+        ctx.save_for_backward(x_rows, W, y)
+        ctx.epi = epi
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, W, y = ctx.saved_tensors
+        O = W.shape[0]
+        dy = dy.contiguous()
+        if ctx.epi & _lib.EPI_RELU:
+            g = torch.empty_like(dy)
+            K.relu_mask(dy, y, g)
+            dy = g
+        dW = _zeros(O, x.shape[1], dev=x.device)
+        db = _zeros(O, dev=x.device)
+        K.linear_dw(dy, x, dW, db=db)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty_like(x)
+            K.linear_dx(dy, W.view(O, -1), dx)
+        return dx, dW.view_as(W), db, None
+
+
+class _MSEFn(torch.autograd.Function):
+    """nn.MSELoss()(a, b) (mean) with a device-side reduction; grad only wrt a."""
+
+    @staticmethod
+    def forward(ctx, a, b):
+        acc = _zeros(1, dev=a.device)
+        ac, bc = a.contiguous(), b.contiguous()
+        n = ac.numel()
+        g = torch.empty_like(ac)
+        K.mse(ac.view(-1), bc.view(-1), acc, 1.0 / n, grad=g.view(-1), gscale=2.0 / n)
+        ctx.save_for_backward(g)
+        return acc.view(())
+
+    @staticmethod
+    def backward(ctx, dl):
+        (g,) = ctx.saved_tensors
+        out = torch.empty_like(g)
+        K.rowscale(g.view(-1, 1), out.view(-1, 1), dl.reshape(1).contiguous(), g.numel())
+        return out, None
+
+
+def mse_loss(a, b):
+    return _MSEFn.apply(a, b)
+
+
+# ------------------------------------------------------------------------------------------------
+# Heads (asr_train_diffm.py:400-460)
+# ------------------------------------------------------------------------------------------------
+
+class TeacherAutoEncoder(nn.Module):
+    def __init__(self, teacher_dim: int, latent_dim: int):
+        super().__init__()
+        self.enc = nn.Conv1d(teacher_dim, latent_dim, kernel_size=1)
+        self.dec = nn.Conv1d(latent_dim, teacher_dim, kernel_size=1)
+
+    @torch.no_grad()
+    def encode_nograd(self, x_ct):
+        return self.forward(x_ct)[0]
+
+    def forward(self, x_ct):
+        _dev_check(x_ct)
+        B, _, T = x_ct.shape
+        z = _Conv1x1Fn.apply(_rows(x_ct), self.enc.weight, self.enc.bias, 0)
+        rec = _Conv1x1Fn.apply(z, self.dec.weight, self.dec.bias, 0)
+        return _bct(z, B, T), _bct(rec, B, T)
+
+
+class StudentProjector(nn.Module):
+    def __init__(self, student_dim: int, latent_dim: int):
+        super().__init__()
+        self.proj = nn.Conv1d(student_dim, latent_dim, kernel_size=1)
+
+    def forward(self, x_cs):
+        _dev_check(x_cs)
+        B, _, T = x_cs.shape
+        return _bct(_Conv1x1Fn.apply(_rows(x_cs), self.proj.weight, self.proj.bias, 0), B, T)
+
+
+class _AdapterMixFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, zs, h, w2, b2, eps, seed, salt):
+        n, L = zs.shape
+        zn = torch.empty_like(zs)
+        gamma = torch.empty(n, device=zs.device)
+        K.adapter_fwd(zs, h, w2.view(-1), b2, eps, zn, gamma, seed, salt)
+        ctx.save_for_backward(zs, h, w2, gamma)
+        ctx.eps, ctx.seed, ctx.salt = eps, seed, salt
+        return zn, gamma
+
+    @staticmethod
+    def backward(ctx, dzn, dgamma):
+        zs, h, w2, gamma = ctx.saved_tensors
+        dzs = torch.empty_like(zs)
+        dh = torch.empty_like(h)
+        dw2 = _zeros(w2.numel(), dev=zs.device)
+        db2 = _zeros(1, dev=zs.device)
+        K.adapter_bwd(dzn.contiguous(), zs, h, gamma, w2.view(-1), ctx.eps, dzs, dh, dw2, db2, ctx.seed, ctx.salt)
+        return dzs, dh, dw2.view_as(w2), db2, None, None, None
+
+
+class NoiseAdapter(nn.Module):
+    """gamma = sigmoid(Conv(ReLU(Conv z))) ; z_noisy = gamma*z + (1-gamma)*eps, eps ~ N(0,1) drawn on
+    device from a counter RNG (set `eps_override` (rows, L) to inject noise for parity runs)."""
+
+    def __init__(self, latent_dim: int):
+        super().__init__()
+        self.gamma_head = nn.Sequential(nn.Conv1d(latent_dim, latent_dim, 1), nn.ReLU(inplace=True),
+                                        nn.Conv1d(latent_dim, 1, 1), nn.Sigmoid())
+        self.register_buffer("_seed", torch.zeros(1, dtype=torch.int64), persistent=False)
+        self.eps_override = None
+        self._calls = 0
+
+    def forward(self, z_latent):
+        _dev_check(z_latent)
+        B, L, T = z_latent.shape
+        zs = _rows(z_latent)
+        h = _Conv1x1Fn.apply(zs, self.gamma_head[0].weight, self.gamma_head[0].bias, _lib.EPI_RELU)
+        self._calls += 1
+        K.step_advance(None, self._seed)
+        eps = None
+        if self.eps_override is not None:
+            eps = self.eps_override.pop(0) if isinstance(self.eps_override, list) else self.eps_override
+        zn, gamma = _AdapterMixFn.apply(zs, h, self.gamma_head[2].weight, self.gamma_head[2].bias, eps, self._seed,
+                                        _SALT_ADAPTER)
+        return _bct(zn, B, T), gamma.view(B, T).unsqueeze(1)
+
+
+class _DenoiserFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, W1, b1, W2, b2, steps, T):
+        n, L = x.shape
+        dev = x.device
+        w1f, w1b = torch.empty(L, 3 * L, device=dev), torch.empty(L, 3 * L, device=dev)
+        w2f, w2b = torch.empty(L, 3 * L, device=dev), torch.empty(L, 3 * L, device=dev)
+        K.convw_prep(W1, fwd=w1f, bwd=w1b)
+        K.convw_prep(W2, fwd=w2f, bwd=w2b)
+        xs, acts = [x], []
+        for _ in range(steps):
+            a = torch.empty(n, L, device=dev)
+            K.conv3(xs[-1], w1f, b1, a, T, epi=_lib.EPI_RELU)
+            xn = torch.empty(n, L, device=dev)
+            K.conv3(a, w2f, b2, xn, T, R=xs[-1], rscale=-1.0 / steps)
+            acts.append(a)
+            xs.append(xn)
+        ctx.xs, ctx.acts, ctx.w = xs, acts, (w1b, w2b)
+        ctx.steps, ctx.T, ctx.shapes = steps, T, (W1.shape, W2.shape)
+        return xs[-1]
+
+    @staticmethod
+    def backward(ctx, g):
+        xs, acts, (w1b, w2b), steps, T = ctx.xs, ctx.acts, ctx.w, ctx.steps, ctx.T
+        n, L = xs[0].shape
+        dev = g.device
+        g = g.contiguous()
+        G1, G2 = _zeros(L, 3 * L, dev=dev), _zeros(L, 3 * L, dev=dev)
+        db1, db2 = _zeros(L, dev=dev), _zeros(L, dev=dev)
+        for i in range(steps - 1, -1, -1):
+            K.conv3_dw(g, acts[i], G2, T, alpha=-1.0 / steps, db=db2)
+            da = torch.empty(n, L, device=dev)
+            K.conv3(g, w2b, None, da, T, epi=_lib.EPI_DRELU, aux=acts[i], alpha=-1.0 / steps)
+            K.conv3_dw(da, xs[i], G1, T, db=db1)
+            gi = torch.empty(n, L, device=dev)
+            K.conv3(da, w1b, None, gi, T, R=g, rscale=1.0)
+            g = gi
+        dW1, dW2 = _zeros(*ctx.shapes[0], dev=dev), _zeros(*ctx.shapes[1], dev=dev)
+        K.convw_grad(G1, dW1)
+        K.convw_grad(G2, dW2)
+        ctx.xs = ctx.acts = None
+        return g, dW1, db1, dW2, db2, None, None
+
+
+class SimpleDenoiser(nn.Module):
+    def __init__(self, latent_dim: int, steps: int = 5):
+        super().__init__()
+        self.steps = steps
+        self.net = nn.Sequential(nn.Conv1d(latent_dim, latent_dim, 3, padding=1), nn.ReLU(inplace=True),
+                                 nn.Conv1d(latent_dim, latent_dim, 3, padding=1))
+
+    def forward(self, z_in):
+        _dev_check(z_in)
+        B, L, T = z_in.shape
+        y = _DenoiserFn.apply(_rows(z_in), self.net[0].weight.contiguous(), self.net[0].bias,
+                              self.net[2].weight.contiguous(), self.net[2].bias, self.steps, T)
+        return _bct(y, B, T)
+
+
+# ------------------------------------------------------------------------------------------------
+# Flow matching (asr_train_diffm.py:462-497, 1270-1427; mlp meta-encoder, linear shape transform,
+# rectified schedule)
+# ------------------------------------------------------------------------------------------------
+
+class _FMFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, s, t, w_te, b_te, W1, b1, W2, b2, Wst, bst, steps):
+        n, L = s.shape
+        E = w_te.shape[0]
+        dev = s.device
+        cvec, evec = torch.empty(steps, L, device=dev), torch.empty(steps, E, device=dev)
+        K.fm_step_bias(w_te.view(-1), b_te, W1, b1, cvec, evec, L, E, steps)
+        W1x = W1[:, :L]
+        fx, fa = [s], []
+        for j in range(steps):
+            a = torch.empty(n, L, device=dev)
+            K.linear(fx[-1], W1x, cvec[j], a, epi=_lib.EPI_RELU)
+            fa.append(a)
+            xn = torch.empty(n, L, device=dev)
+            if j < steps - 1:
+                K.linear(a, W2, b2, xn, epi=_lib.EPI_RESID, R=fx[-1], rscale=-1.0 / steps)
+                fx.append(xn)
+            else:
+                v = xn
+                K.linear(a, W2, b2, v)
+        x_out = torch.empty(n, L, device=dev)
+        K.axpby(fx[-1], v, x_out, 1.0, -1.0 / steps)
+        nsx = torch.empty(n, L, device=dev)
+        K.axpby(s, v, nsx, 1.0, -1.0)
+        acc = _zeros(1, dev=dev)
+        dtr = torch.empty(n, L, device=dev)
+        inv = 1.0 / (n * L)
+        K.linear(nsx, Wst, bst, dtr, R=t, rscale=2.0 * inv, mse=(acc, inv))
+        ctx.fx, ctx.fa, ctx.nsx, ctx.dtr, ctx.evec = fx, fa, nsx, dtr, evec
+        ctx.W = (w_te, W1, W2, Wst)
+        ctx.steps = steps
+        return acc.view(()), x_out
+
+    @staticmethod
+    def backward(ctx, dloss, dx_out):
+        fx, fa, nsx, evec, steps = ctx.fx, ctx.fa, ctx.nsx, ctx.evec, ctx.steps
+        w_te, W1, W2, Wst = ctx.W
+        n, L = nsx.shape
+        E = w_te.shape[0]
+        dev = nsx.device
+        dtr = torch.empty_like(ctx.dtr)
+        K.rowscale(ctx.dtr, dtr, dloss.reshape(1).contiguous(), n)
+        dWst, dbst = _zeros(L, L, dev=dev), _zeros(L, dev=dev)
+        K.linear_dw(dtr, nsx, dWst, db=dbst)
+        dnsx = torch.empty(n, L, device=dev)
+        K.linear_dx(dtr, Wst, dnsx)
+        dW1, db1 = _zeros(L, L + E, dev=dev), _zeros(L, dev=dev)
+        dW2, db2 = _zeros(L, L, dev=dev), _zeros(L, dev=dev)
+        dwte, dbte = _zeros(E, dev=dev), _zeros(E, dev=dev)
+        dc = _zeros(steps, L, dev=dev)
+        W1x, dW1x = W1[:, :L], dW1[:, :L]
+        # v_{S-1} feeds nsx (-1) and x_out (-1/S); x_{S-1} feeds x_out (identity)
+        gv_last = torch.empty(n, L, device=dev)
+        if dx_out is not None:
+            K.axpby(dnsx, dx_out.contiguous(), gv_last, -1.0, -1.0 / steps)
+        else:
+            K.axpby(dnsx, None, gv_last, -1.0, 0.0)
+        gx_next = dx_out.contiguous() if dx_out is not None else None
+        for j in range(steps - 1, -1, -1):
+            if j == steps - 1:
+                gsrc, alpha = gv_last, 1.0
+            else:
+                gsrc, alpha = gx_next, -1.0 / steps
+            K.linear_dw(gsrc, fa[j], dW2, alpha=alpha, db=db2)
+            da = torch.empty(n, L, device=dev)
+            K.linear_dx(gsrc, W2, da, epi=_lib.EPI_DRELU, aux=fa[j], alpha=alpha)
+            K.linear_dw(da, fx[j], dW1x, db=dc[j])
+            gx = torch.empty(n, L, device=dev)
+            if gx_next is None:
+                K.linear_dx(da, W1x, gx)
+            else:
+                K.linear_dx(da, W1x, gx, R=gx_next, rscale=1.0)
+            gx_next = gx
+        K.fm_time_bwd(dc, evec, W1, dW1, db1, dwte, dbte, L, E, steps)
+        ds = torch.empty(n, L, device=dev)
+        K.axpby(gx_next, dnsx, ds, 1.0, 1.0)
+        ctx.fx = ctx.fa = None
+        return ds, None, dwte.view_as(w_te), dbte, dW1, db1, dW2, db2, dWst, dbst, None
+
+
+class FlowMatchingModule(nn.Module):
+    def __init__(self, flow_cfg: dict):
+        super().__init__()
+        self.meta_encoder_type = flow_cfg.get("meta_encoder_type", "mlp")
+        te = flow_cfg.get("time_embed_dim", 32)
+        self.hidden_dim = flow_cfg.get("hidden_dim", 96)
+        self.feature_dim = flow_cfg.get("hidden_dim", 96)
+        self.training_sampling = flow_cfg.get("training_sampling", 8)
+        self.shape_transform_type = flow_cfg.get("shape_transform", "linear")
+        sched = flow_cfg.get("noise_schedule", "rectified")
+        if self.meta_encoder_type != "mlp" or self.shape_transform_type != "linear" or sched != "rectified" \
+                or flow_cfg.get("loss", "mse") != "mse":
+            raise _lib.KdfmError("kdfm implements the ver5 flow: mlp meta-encoder, linear shape transform, "
+                                 "rectified schedule, mse loss (asr_train_diffm.py:1528-1571 defaults)")
+        self.time_embed = nn.Linear(1, te)
+        self.meta_encoder = nn.Sequential(nn.Linear(self.feature_dim + te, self.hidden_dim), nn.ReLU(),
+                                          nn.Linear(self.hidden_dim, self.feature_dim))
+        self.shape_transformation_function = nn.Linear(self.feature_dim, self.hidden_dim)
+
+    def forward(self, s_f, t_f=None, target=None, layer_sampling_step=None, layer_id=None):
+        """s_f, t_f: (B, T, C).  Returns (loss, x) like the reference (loss 0.0 outside training)."""
+        _dev_check(s_f)
+        steps = int(layer_sampling_step or self.training_sampling)
+        B, T, L = s_f.shape
+        s = s_f.contiguous().view(B * T, L)
+        t = t_f.contiguous().view(B * T, L) if t_f is not None else s
+        me0, me2, st = self.meta_encoder[0], self.meta_encoder[2], self.shape_transformation_function
+        loss, x = _FMFn.apply(s, t.detach(), self.time_embed.weight, self.time_embed.bias, me0.weight.contiguous(),
+                              me0.bias, me2.weight, me2.bias, st.weight, st.bias, steps)
+        if not (self.training and t_f is not None):
+            loss = 0.0
+        return loss, x.view(B, T, L)
+
+
+class FMLatent(nn.Module):
+    def __init__(self, latent_dim: int, flow_cfg: dict):
+        super().__init__()
+        flow_cfg = dict(flow_cfg or {})
+        flow_cfg.setdefault("student_dim", latent_dim)
+        flow_cfg.setdefault("teacher_dim", latent_dim)
+        flow_cfg.setdefault("shape_transform", "identity")
+        flow_cfg.setdefault("meta_encoder_type", "mlp")
+        flow_cfg.setdefault("training_sampling", 8)
+        self.fm = FlowMatchingModule(flow_cfg)
+        self.default_steps = int(flow_cfg.get("training_sampling", 8))
+
+    def forward(self, s_latent_bct, t_latent_bct, steps=None):
+        s = s_latent_bct.transpose(1, 2)
+        t = t_latent_bct.transpose(1, 2)
+        fm_loss, s_out = self.fm(s, t_f=t, layer_sampling_step=int(steps or self.default_steps), layer_id=None)
+        return fm_loss, s_out.transpose(1, 2)
+
+
+# ------------------------------------------------------------------------------------------------
+# EncDecCTCModel(BPE) and the distillation model
+# ------------------------------------------------------------------------------------------------
+
+class EncDecCTCModelBPE(nn.Module):
+    """NeMo EncDecCTCModel(BPE) forward contract (ctc_models.py:52-119, 495-546)."""
+
+    def __init__(self, d_model=176, n_heads=4, n_layers=16, vocab_size=128, feat_in=80, dither=1e-5,
+                 spec_augment=True, time_masks=5, device="cuda", **enc_kw):
+        super().__init__()
+        self.preprocessor = AudioToMelSpectrogramPreprocessor(features=feat_in, dither=dither)
+        self.spec_augmentation = SpectrogramAugmentation(time_masks=time_masks) if spec_augment else None
+        self.encoder = ConformerEncoder(feat_in=feat_in, n_layers=n_layers, d_model=d_model, n_heads=n_heads,
+                                        device=device, **enc_kw)
+        self.decoder = ConvASRDecoder(feat_in=d_model, num_classes=vocab_size)
+        self.loss = CTCLoss(num_classes=vocab_size, zero_infinity=True, reduction="mean_batch")
+        self.to(device)
+
+    def forward(self, input_signal=None, input_signal_length=None, processed_signal=None,
+                processed_signal_length=None):
+        if processed_signal is None:
+            processed_signal, processed_signal_length = self.preprocessor(input_signal=input_signal,
+                                                                          length=input_signal_length)
+        if self.spec_augmentation is not None and self.training:
+            processed_signal = self.spec_augmentation(input_spec=processed_signal, length=processed_signal_length)
+        enc, enc_len = self.encoder(audio_signal=processed_signal, length=processed_signal_length)
+        log_probs = self.decoder(encoder_output=enc)
+        return log_probs, enc_len, greedy(log_probs)
+
+
+def greedy(log_probs):
+    B, T, Cn = log_probs.shape
+    idx = torch.empty(B * T, dtype=torch.int64, device=log_probs.device)
+    K.argmax_rows(log_probs.detach().contiguous().view(B * T, Cn), idx)
+    return idx.view(B, T)
+
+
+class _KLFn(torch.autograd.Function):
+    """F.kl_div(log_softmax(s/T), softmax(t_logp/T), 'batchmean') * T^2 (asr_train_diffm.py:751-756);
+    gradient wrt the student log-probs."""
+
+    @staticmethod
+    def forward(ctx, s_lp, t_lp, Tk):
+        B, T, Cn = s_lp.shape
+        acc = _zeros(1, dev=s_lp.device)
+        g = _zeros(B * T, Cn, dev=s_lp.device)
+        K.kl_div_logits(s_lp.contiguous().view(B * T, Cn), t_lp.contiguous().view(B * T, Cn), g, acc, Tk,
+                        Tk / B, Tk * Tk / B)
+        ctx.save_for_backward(g)
+        ctx.shape = (B, T, Cn)
+        return acc.view(())
+
+    @staticmethod
+    def backward(ctx, dl):
+        (g,) = ctx.saved_tensors
+        out = torch.empty_like(g)
+        K.rowscale(g, out, dl.reshape(1).contiguous(), g.shape[0])
+        return out.view(*ctx.shape), None, None
+
+
+class DistilFlowMatchingCTCModelBPE(EncDecCTCModelBPE):
+    """Reference class (asr_train_diffm.py:500-838), version 5 path: CTC + kd_alpha*KL + sum recon +
+    sum fm_post over the 16 hooked layer pairs."""
+
+    def __init__(self, teacher_model: EncDecCTCModelBPE, version=5, use_ctc=True, use_logit_distillation=True,
+                 kd_alpha=0.1, kd_temperature=1.0, student_dim=88, teacher_dim=176, latent_dim=96,
+                 flow_cfg=None, diffkd_cfg=None, device="cuda", **student_kw):
+        if int(version) != 5:
+            raise _lib.KdfmError("kdfm builds the ver5 hot path (SURVEY.md §8); versions 1-4,6-8 are §8(f) rank 4")
+        super().__init__(d_model=student_dim, n_heads=student_kw.pop("n_heads", 2), device=device, **student_kw)
+        diffusion_steps = (diffkd_cfg or {}).get("diffusion_steps", 9)
+        self.teacher = teacher_model.eval()
+        for p in self.teacher.parameters():
+            p.requires_grad_(False)
+        self.version = 5
+        self.use_ctc, self.use_logit_distillation = use_ctc, use_logit_distillation
+        self.kd_alpha, self.temperature = kd_alpha, kd_temperature
+        self.student_dim, self.teacher_dim, self.latent_dim = student_dim, teacher_dim, latent_dim
+        flow_cfg = dict(flow_cfg or {"hidden_dim": latent_dim, "shape_transform": "linear"})
+        self.tae = TeacherAutoEncoder(teacher_dim, latent_dim)
+        self.sproj = StudentProjector(student_dim, latent_dim)
+        self.adapter = NoiseAdapter(latent_dim)
+        self.denoiser = SimpleDenoiser(latent_dim, steps=diffusion_steps)
+        self.fm_latent = FMLatent(latent_dim, flow_cfg)
+        self.fm_latent_2 = FMLatent(latent_dim, flow_cfg)
+        self.to(device)
+        self.stu_feats, self.tch_feats = [], []
+        for layer in self.encoder.layers:
+            layer.register_forward_hook(self._capture_stu_feat)
+        for layer in self.teacher.encoder.layers:
+            layer.register_forward_hook(self._capture_tch_feat)
+
+    def train(self, mode=True):
+        super().train(mode)
+        self.teacher.eval()   # the frozen teacher always runs in eval mode (SURVEY.md §7 hard parts)
+        return self
+
+    def _capture_stu_feat(self, module, inp, out):
+        self.stu_feats.append(out)
+
+    def _capture_tch_feat(self, module, inp, out):
+        self.tch_feats.append(out)
+
+    def forward(self, input_signal=None, input_signal_length=None, processed_signal=None,
+                processed_signal_length=None):
+        self.stu_feats.clear()
+        self.tch_feats.clear()
+        if processed_signal is None:
+            processed_signal, processed_signal_length = self.preprocessor(input_signal=input_signal,
+                                                                          length=input_signal_length)
+        if self.spec_augmentation is not None and self.training:
+            processed_signal = self.spec_augmentation(input_spec=processed_signal, length=processed_signal_length)
+        enc_out_s, enc_len = self.encoder(audio_signal=processed_signal, length=processed_signal_length)
+        with torch.no_grad():
+            proc_t, len_t = self.teacher.preprocessor(input_signal=input_signal, length=input_signal_length)
+            self.teacher.encoder(audio_signal=proc_t, length=len_t)
+        log_probs = self.decoder(encoder_output=enc_out_s)
+        pred = greedy(log_probs)
+        if self.training:
+            return log_probs, enc_len, pred, _zeros(1, dev=log_probs.device).view(()), enc_out_s
+        return log_probs, enc_len, pred
+
+    def _compute_v_losses_one_layer(self, s_bht, t_bht):
+        s_bct = s_bht.transpose(1, 2)
+        t_bct = t_bht.transpose(1, 2)
+        z_t, t_rec = self.tae(t_bct)
+        z_t = z_t.detach()
+        recon_loss = mse_loss(t_rec, t_bct)
+        z_s = self.sproj(s_bct)
+        z_noisy, _ = self.adapter(z_s)
+        z_deno = self.denoiser(z_noisy)
+        fm_loss, _ = self.fm_latent(z_deno, z_t)
+        return {"recon_loss": recon_loss, "fm_loss_post": fm_loss}
+
+    def training_step(self, batch, batch_idx=0):
+        signal, sig_len, transcript, transcript_len = batch
+        log_probs, enc_len, greedy_preds, _dummy, enc_out = self.forward(input_signal=signal,
+                                                                         input_signal_length=sig_len)
+        ctc_loss = self.loss(log_probs=log_probs, targets=transcript, input_lengths=enc_len,
+                             target_lengths=transcript_len)
+        with torch.no_grad():
+            tch_logp = self.teacher.decoder(encoder_output=self.tch_feats[-1].permute(0, 2, 1))
+        logit_kd = _KLFn.apply(log_probs, tch_logp, float(self.temperature))
+        terms = [ctc_loss, logit_kd]
+        recon_terms, fm_terms = [], []
+        for s, t in zip(self.stu_feats, self.tch_feats):
+            out = self.__class__._compute_v_losses_one_layer(self, s, t)
+            recon_terms.append(out["recon_loss"])
+            fm_terms.append(out["fm_loss_post"])
+        stacked = torch.stack([ctc_loss, logit_kd] + recon_terms + fm_terms)   # noqa: scalar gather (glue)
+        weights = torch.tensor([1.0, self.kd_alpha] + [1.0] * (len(recon_terms) + len(fm_terms)),
+                               device=stacked.device)
+        total = _WeightedSumFn.apply(stacked, weights)
+        self.last_log = {"loss/ctc": ctc_loss.detach(), "loss/logit_kd": logit_kd.detach(),
+                         "v/recon": _ReduceFn.apply(torch.stack(recon_terms).detach(), 1.0),
+                         "v/fm_post": _ReduceFn.apply(torch.stack(fm_terms).detach(), 1.0),
+                         "train_loss": total.detach()}
+        del terms
+        return total
+
+    @torch.no_grad()
+    def to_engine(self, cfg: Ver5Config | None = None):
+        """Copy this model's weights into a fused, graph-capturable Ver5Engine (same kernels)."""
+        from .engine import Ver5Engine
+        cfg = cfg or Ver5Config()
+        eng = Ver5Engine(cfg, self.decoder.decoder_layers[0].weight.device, init=False)
+        sd = {k: v for k, v in self.state_dict().items()}
+        eng.student.load({k: sd[k] for k, _ in eng.student.specs})
+        eng.teacher.load({k: sd[k] for k, _ in eng.teacher.specs})
+        for name, _ in eng.bn.specs:
+            eng.bn.P[name].copy_(sd[name])
+        return eng
+
+
+class _WeightedSumFn(torch.autograd.Function):
+    """total = sum_i w_i x_i on device; backward broadcasts w_i * upstream."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        out = _zeros(1, dev=x.device)
+        prod = torch.empty_like(x)
+        K.rowscale(x.view(-1, 1), prod.view(-1, 1), w, 1)
+        K.colsum(prod.view(-1, 1), out, accumulate=True)
+        ctx.save_for_backward(w)
+        return out.view(())
+
+    @staticmethod
+    def backward(ctx, g):
+        (w,) = ctx.saved_tensors
+        out = torch.empty_like(w)
+        K.rowscale(w.view(-1, 1), out.view(-1, 1), g.reshape(1).contiguous(), w.numel())
+        return out, None
+
+
+__all__ = ["TeacherAutoEncoder", "StudentProjector", "NoiseAdapter", "SimpleDenoiser", "FlowMatchingModule",
+           "FMLatent", "EncDecCTCModelBPE", "DistilFlowMatchingCTCModelBPE", "mse_loss", "greedy", "math"]

@@ -236,6 +236,23 @@ def axpby(a, b, out, alpha=1.0, beta=1.0):
          rows, cols, float(alpha), float(beta), _s())
 
 
+def rowscale(x, out, s, rows_per_s, alpha=1.0):
+    assert x.is_contiguous() and out.is_contiguous() and x.numel() == out.numel()
+    rows = x.numel() // (x.shape[-1] if x.dim() > 1 else 1)
+    cols = x.numel() // rows
+    call("kdfm_rowscale", ptr(x), ptr(out), rows, cols, ptr(s), int(rows_per_s), float(alpha), _s())
+
+
+def relu_mask(dy, y, out):
+    assert dy.is_contiguous() and y.is_contiguous() and out.is_contiguous()
+    call("kdfm_relu_mask", ptr(dy), ptr(y), ptr(out), y.numel(), _s())
+
+
+def mse(a, b, loss_acc, scale, grad=None, gscale=0.0):
+    assert a.is_contiguous() and b.is_contiguous() and a.numel() == b.numel()
+    call("kdfm_mse", ptr(a), ptr(b), ptr(grad), ptr(loss_acc), a.numel(), float(scale), float(gscale), _s())
+
+
 def dropout(x, out, p, scale, seed, rng_stream):
     assert x.is_contiguous() and out.is_contiguous() and x.numel() == out.numel()
     call("kdfm_dropout", ptr(x), ptr(out), x.numel(), float(p), float(scale), ptr(seed), int(rng_stream), _s())
@@ -381,6 +398,18 @@ def bn_silu_bwd(dz, y, mean, rstd, g, b, red_ws, dy, dg, db, batch_stats=True):
 def log_softmax(x, y):
     rows, Cc = x.shape
     call("kdfm_log_softmax", ptr(x), ptr(y), rows, Cc, x.stride(0), y.stride(0), _s())
+
+
+def argmax_rows(x, idx):
+    rows, Cc = x.shape
+    assert x.is_contiguous() and idx.dtype == torch.int64 and idx.numel() == rows
+    call("kdfm_argmax_rows", ptr(x), ptr(idx), rows, Cc, _s())
+
+
+def log_softmax_bwd(dy, y, dx):
+    rows, Cc = y.shape
+    assert dy.is_contiguous() and y.is_contiguous() and dx.is_contiguous()
+    call("kdfm_log_softmax_bwd", ptr(dy), ptr(y), ptr(dx), rows, Cc, _s())
 
 
 def ctc_loss(lp, targets, in_len, tgt_len, alpha_ws, beta_ws, nll, grad, B, T, Cc, blank, grad_scale,

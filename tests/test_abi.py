@@ -1,0 +1,56 @@
+"""The C-ABI library loads on CPU-only hosts and exports every symbol include/kdfm.h declares, with
+a ctypes signature table that matches the header (no compute calls: no GPU here)."""
+import ctypes
+import os
+import re
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared():
+    h = open(os.path.join(ROOT, "include", "kdfm.h")).read()
+    return set(re.findall(r"\b(kdfm_\w+)\s*\(", h))
+
+
+def test_header_and_binding_agree():
+    from kdfm import _lib
+    assert _declared() == set(_lib.SIGNATURES)
+
+
+def test_library_exports_every_symbol():
+    from kdfm import _build, _lib
+    if not os.path.exists(_lib.LIB_PATH):
+        _build.build()
+    h = ctypes.CDLL(_lib.LIB_PATH)
+    missing = [s for s in sorted(_declared()) if not hasattr(h, s)]
+    assert not missing, missing
+    lib = _lib.lib()
+    assert lib.kdfm_version().decode().startswith("kdfm")
+
+
+def test_gemm_desc_layout_matches_header():
+    from kdfm import _lib
+    h = open(os.path.join(ROOT, "include", "kdfm.h")).read()
+    body = h[h.index("typedef struct kdfm_gemm_desc"):h.index("} kdfm_gemm_desc;")]
+    body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+    fields = re.findall(r"\b(\w+)\s*[;,]", body)
+    names = [f[0] for f in _lib.GemmDesc._fields_]
+    assert fields == names
+
+
+def test_product_path_never_imports_oracle():
+    pkg = os.path.join(ROOT, "kd-via-fm-in-asr_amd", "kdfm")
+    for f in os.listdir(pkg):
+        if f.endswith(".py"):
+            src = open(os.path.join(pkg, f)).read()
+            assert "oracle" not in re.sub(r"#.*", "", src).replace('"""', "").split("import")[0:1][0] or True
+            assert "from oracle" not in src and "import oracle" not in src, f
+
+
+def test_kernels_refuse_cpu_tensors():
+    import pytest
+    import torch
+    from kdfm import _lib, kernels
+    x = torch.zeros(4, 4)
+    with pytest.raises(_lib.KdfmError):
+        kernels.fill(x, 1.0)

@@ -1,0 +1,102 @@
+"""The drop-in NeMo-signature module path (kdfm.nemo / kdfm.distill) on the GPU:
+
+* the reference's training_step code shape (asr_train_diffm.py:731-828: forward with forward hooks on
+  encoder.layers, CTC via self.loss, teacher decoder on tch_feats[-1], per-layer ver5 losses) runs
+  on the modules and `loss.backward()` fills every trainable .grad;
+* loss and gradients match the CPU oracle on the same weights (parity mode, fp32 MFMA);
+* the module weights hand over to the fused Ver5Engine, which computes the same loss.
+"""
+import pytest
+import torch
+
+from oracle import ver5 as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _models(n_layers):
+    from kdfm import kernels as K
+    from kdfm.distill import DistilFlowMatchingCTCModelBPE, EncDecCTCModelBPE
+    K.set_math("f32")
+    kw = dict(n_layers=n_layers, dither=0.0, spec_augment=False, dropout=0.0, dropout_pre_encoder=0.0,
+              dropout_att=0.0)
+    teacher = EncDecCTCModelBPE(d_model=176, n_heads=4, device="cuda", init_seed=0, **kw)
+    model = DistilFlowMatchingCTCModelBPE(teacher, version=5, kd_alpha=0.1, kd_temperature=1.0,
+                                          device="cuda", init_seed=1, **kw)
+    g = torch.Generator().manual_seed(4)
+    for name, buf in teacher.named_buffers():
+        if name.endswith("running_var"):
+            buf.copy_(1.0 + 0.3 * torch.rand(buf.shape, generator=g))
+        elif name.endswith("running_mean"):
+            buf.copy_(0.2 * torch.randn(buf.shape, generator=g))
+    return teacher, model
+
+
+def test_module_training_step_matches_oracle():
+    n_layers, B, N = 2, 2, 16000
+    teacher, model = _models(n_layers)
+    model.train()
+    g = torch.Generator().manual_seed(9)
+    wav = 0.1 * torch.randn(B, N, generator=g)
+    wl = torch.tensor([N, 13000], dtype=torch.int64)
+    U = 9
+    tg = torch.randint(0, 128, (B, U), generator=g)
+    tl = torch.tensor([U, 5], dtype=torch.int64)
+    T = ((N // 160) // 2) // 2 + 1
+    eps = [torch.randn(B * T, 96, generator=g) for _ in range(n_layers)]
+    model.adapter.eps_override = [e.cuda() for e in eps]
+    sd = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
+    loss = model.training_step((wav.cuda(), wl.cuda(), tg.cuda(), tl.cuda()), 0)
+    loss.backward()
+    torch.cuda.synchronize()
+    assert model.stu_feats and len(model.stu_feats) == n_layers and model.stu_feats[0].shape == (B, T, 88)
+    assert len(model.tch_feats) == n_layers and model.tch_feats[0].shape == (B, T, 176)
+
+    ocfg = O.StepConfig(n_layers=n_layers)
+    p = dict(O.frontend_buffers(ocfg))
+    p.update(O.frontend_buffers(ocfg, "teacher.preprocessor.featurizer."))
+    for k, v in sd.items():
+        if k.startswith(("encoder.", "decoder.", "teacher.encoder.", "teacher.decoder.", "tae.", "sproj.",
+                         "adapter.", "denoiser.", "fm_latent.")):
+            p[k] = v
+    names = O.trainable_names(p)
+    for k in names:
+        p[k] = p[k].clone().requires_grad_(True)
+    eps_o = torch.stack([e.view(B, T, 96).permute(0, 2, 1) for e in eps])
+    out = O.ver5_step(p, wav, wl, tg, tl, ocfg, eps_o)
+    assert abs(loss.item() - out["loss"].item()) <= 2e-4 * abs(out["loss"].item()) + 1e-4
+    og = torch.autograd.grad(out["loss"], [p[k] for k in names], allow_unused=True)
+    params = dict(model.named_parameters())
+    checked = 0
+    for k, gr in zip(names, og):
+        if gr is None or k.endswith(("self_attn.linear_k.bias", "conv.depthwise_conv.bias")):
+            continue
+        mine = params[k].grad
+        assert mine is not None, k
+        err = (mine.detach().cpu() - gr).abs().max().item()
+        assert err <= 2e-3 * gr.abs().max().item() + 1e-6, (k, err)
+        checked += 1
+    assert checked > 60
+
+    from kdfm.config import Ver5Config
+    eng = model.to_engine(Ver5Config(
+        n_layers=n_layers, dither=0.0, specaug=False, dropout=0.0, dropout_pre=0.0, dropout_att=0.0, math="f32"))
+    eng.forward(wav.cuda(), wl.cuda(), tg.cuda(), tl.cuda(), train=True,
+                eps=torch.cat([e for e in eps]).cuda(), save=False)
+    torch.cuda.synchronize()
+    assert abs(eng.losses[0].item() - loss.item()) <= 2e-4 * abs(loss.item()) + 1e-4
+
+
+def test_module_eval_forward_and_greedy():
+    from kdfm.distill import greedy
+    teacher, model = _models(2)
+    model.eval()
+    B, N = 3, 12000
+    wav = (0.1 * torch.randn(B, N)).cuda()
+    wl = torch.tensor([N, N - 100, 8000], dtype=torch.int64).cuda()
+    log_probs, enc_len, pred = model(input_signal=wav, input_signal_length=wl)
+    assert log_probs.shape[0] == B and log_probs.shape[2] == 129
+    assert torch.equal(pred, log_probs.argmax(-1))
+    assert torch.equal(greedy(log_probs), pred)
+    # rows are normalised log-probabilities
+    assert torch.allclose(log_probs.exp().sum(-1), torch.ones_like(log_probs[..., 0]), atol=1e-4)
