@@ -233,6 +233,7 @@ class _SubsampleFn(torch.autograd.Function):
     def forward(ctx, mel_btf, mel_len, len1, len2, mod, *params):
         P = mod._P(params)
         S = EncoderShapes(mod.cfg, mel_btf.shape[0], mel_btf.shape[1], mod.d, 1)
+        P = {"pre_encode." + k: v for k, v in P.items()}
         x, sctx = subsampling_forward(mod.cfg, S, P, "", mel_btf.contiguous(), mel_len, len1, len2,
                                       train=mod.training, seed=mod._seed, salt=_SALT + 3, save=True, ws=mod._ws(S))
         ctx.sctx, ctx.S, ctx.mod, ctx.len1, ctx.params = sctx, S, mod, len1, params
@@ -242,7 +243,9 @@ class _SubsampleFn(torch.autograd.Function):
     def backward(ctx, dx):
         mod, S = ctx.mod, ctx.S
         G = _Flat._G(mod._specs, dx.device)
-        subsampling_backward(mod.cfg, S, mod._P(ctx.params), G, "", ctx.sctx, dx.contiguous().view(S.rows, S.d),
+        Gp = {"pre_encode." + k: v for k, v in G.items()}
+        Pp = {"pre_encode." + k: v for k, v in mod._P(ctx.params).items()}
+        subsampling_backward(mod.cfg, S, Pp, Gp, "", ctx.sctx, dx.contiguous().view(S.rows, S.d),
                              ctx.len1, seed=mod._seed, salt=_SALT + 3, ws=mod._ws(S))
         return (None, None, None, None, None, *[G[n] for n, _ in mod._specs])
 
