@@ -201,180 +201,6 @@ __device__ __forceinline__ void store_lds(void* lds, const float (&v)[8]) {
   }
 }
 
-// Fused epilogue shared by both main loops.  Wave (wr, wc) owns rows wr*32 + [0,32) and columns
-// wc*16*WN + [0, 16*WN) of the block tile; 16x16 MFMA accumulator layout: col = lane&15,
-// row = (lane>>4)*4 + r.
-template <int WN>
-__device__ __forceinline__ void epilogue(const P& p, const f32x4 (&acc)[2][WN], int64_t m0, int64_t n0,
-                                         int64_t cOff, int64_t bz, int wr, int wc, int lane) {
-  const int epi = p.epi;
-  uint64_t seed = 0;
-  if (epi & KDFM_EPI_DROPOUT) seed = load_seed(p.seed);
-  const float keep_scale = (epi & KDFM_EPI_DROPOUT) ? 1.f / (1.f - p.dropout_p) : 1.f;
-  float mse_part = 0.f;
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < WN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int64_t m = m0 + wr * 32 + i * 16 + (lane >> 4) * 4 + r;
-        const int64_t n = n0 + wc * 16 * WN + j * 16 + (lane & 15);
-        if (m >= p.M || n >= p.N) continue;
-        const int64_t off = cOff + m * p.sCm + n * p.sCn;
-        float v = p.alpha * acc[i][j][r];
-        if (epi & KDFM_EPI_ATOMIC) {
-          if (n == p.ones_col)
-            atomicAdd(p.ones_out + m, v);
-          else
-            atomicAdd(p.C + off, v);
-          continue;
-        }
-        if (epi & KDFM_EPI_BIAS) v += p.bias[n];
-        if (epi & KDFM_EPI_MSE) {
-          const float diff = v - p.R[off];
-          mse_part += diff * diff;
-          p.C[off] = p.rscale * diff;
-          continue;
-        }
-        if (epi & KDFM_EPI_STORE_PRE) p.Cpre[off] = v;
-        if (epi & KDFM_EPI_RELU) v = fmaxf(v, 0.f);
-        if (epi & KDFM_EPI_SILU) v = siluf_(v);
-        if (epi & KDFM_EPI_DROPOUT) {
-          const uint64_t idx = ((uint64_t)bz * (uint64_t)p.M + (uint64_t)m) * (uint64_t)p.N + (uint64_t)n;
-          v = dropout_keep(seed, p.rng_stream, idx, p.dropout_p) ? v * keep_scale : 0.f;
-        }
-        if (epi & KDFM_EPI_DRELU) v = (p.aux[off] > 0.f) ? v : 0.f;
-        if (epi & KDFM_EPI_DSILU) v *= dsiluf_(p.aux[off]);
-        if (epi & KDFM_EPI_RESID) v = p.R[off] + p.rscale * v;
-        if (epi & KDFM_EPI_BETA) v += p.beta * p.C[off];
-        if (epi & KDFM_EPI_ROWMASK) {
-          const int64_t fr = m / p.mask_div;
-          const int64_t t = fr % p.mask_T, u = fr / p.mask_T;
-          if (t >= p.mask_len[u]) v = 0.f;
-        }
-        p.C[off] = v;
-      }
-  if (epi & KDFM_EPI_MSE) {
-    mse_part = wave_sum(mse_part);
-    if (lane == 0) atomicAdd(p.loss_acc, mse_part * p.loss_scale);
-  }
-}
-
-__device__ __forceinline__ bf16x8 to_bf16x8(const float (&v)[8]) {
-  bf16x8 pk;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) pk[i] = (short)f2bf(v[i]);
-  return pk;
-}
-
-// store one thread's packed 8 bf16 into a [64 rows][LDK_BF] sub-tile image
-template <bool KRUN>
-__device__ __forceinline__ void pack_store(uint16_t* s, const bf16x8& pk) {
-  const int t = threadIdx.x;
-  if constexpr (KRUN) {
-    const int r = t >> 2, k = (t & 3) * 8;
-    *reinterpret_cast<bf16x8*>(s + r * LDK_BF + k) = pk;
-  } else {
-    const int k = t >> 3, r = (t & 7) * 8;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) s[(r + i) * LDK_BF + k] = (uint16_t)pk[i];
-  }
-}
-
-// bf16 main loop: stages of BK2 = 64 (two 32-deep sub-tiles), LDS double-buffered with ONE barrier
-// per stage; the next stage's global loads are in flight (packed to bf16 in registers) while the
-// current stage's MFMAs run.  Block tile 64 x (32*WN); 4 waves as 2 (M) x 2 (N).
-template <int AM, int BMODE, int WN>
-__global__ __launch_bounds__(NT) void gemm_bf16_kernel(P p) {
-  constexpr int BNv = 32 * WN;
-  constexpr int NH = BNv / 64;            // 64-row halves of the B tile
-  constexpr int SUB = 64 * LDK_BF;        // u16 per 64 x 32 sub-tile image
-  constexpr int A_ST = 2 * SUB, B_ST = NH * 2 * SUB, ST = A_ST + B_ST;
-  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * ST];
-
-  const int64_t z = blockIdx.z;
-  const int64_t split = z % p.splitk;
-  const int64_t bz = z / p.splitk;
-  const int64_t b1 = bz / p.batch2, b2 = bz % p.batch2;
-  const float* A = p.A + b1 * p.bA1 + b2 * p.bA2;
-  const float* B = p.B + b1 * p.bB1 + b2 * p.bB2;
-  const int64_t cOff = b1 * p.bC1 + b2 * p.bC2;
-  const int64_t m0 = (int64_t)blockIdx.x * BM;
-  const int64_t n0 = (int64_t)blockIdx.y * BNv;
-  constexpr int BK2 = 64;
-  const int64_t kchunk = ceil_div(ceil_div(p.K, p.splitk), BK2) * BK2;
-  const int64_t kbeg = split * kchunk;
-  const int64_t kend = (kbeg + kchunk < p.K) ? (kbeg + kchunk) : p.K;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int wr = wave >> 1, wc = wave & 1;
-  constexpr bool A_KRUN = (AM != KDFM_LD_XC);
-  constexpr bool B_KRUN = (BMODE == KDFM_LD_KC);
-
-  f32x4 acc[2][WN];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < WN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  bf16x8 ra[2], rb[NH][2];
-  auto gload = [&](int64_t k0) {
-#pragma unroll
-    for (int kh = 0; kh < 2; ++kh) {
-      float v[8];
-      load_tile_A<AM>(v, A, m0, k0 + 32 * kh, p.M, kend, p.sAm, p.sAk, p);
-      ra[kh] = to_bf16x8(v);
-#pragma unroll
-      for (int nh = 0; nh < NH; ++nh) {
-        load_tile_B<BMODE>(v, B, n0 + 64 * nh, k0 + 32 * kh, p.N, kend, p.sBk, p.sBn, p);
-        rb[nh][kh] = to_bf16x8(v);
-      }
-    }
-  };
-  auto sstore = [&](int buf) {
-    uint16_t* base = smem + buf * ST;
-#pragma unroll
-    for (int kh = 0; kh < 2; ++kh) {
-      pack_store<A_KRUN>(base + kh * SUB, ra[kh]);
-#pragma unroll
-      for (int nh = 0; nh < NH; ++nh) pack_store<B_KRUN>(base + A_ST + (nh * 2 + kh) * SUB, rb[nh][kh]);
-    }
-  };
-  const int64_t nst = (kend > kbeg) ? ceil_div(kend - kbeg, BK2) : 0;
-  if (nst > 0) {
-    gload(kbeg);
-    sstore(0);
-    __syncthreads();
-  }
-  for (int64_t s = 0; s < nst; ++s) {
-    const int cur = (int)(s & 1);
-    if (s + 1 < nst) gload(kbeg + (s + 1) * BK2);
-    const uint16_t* base = smem + cur * ST;
-#pragma unroll
-    for (int kh = 0; kh < 2; ++kh) {
-      bf16x8 af[2], bfr[WN];
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-        af[i] = *reinterpret_cast<const bf16x8*>(base + kh * SUB + (wr * 32 + i * 16 + (lane & 15)) * LDK_BF +
-                                                 8 * (lane >> 4));
-#pragma unroll
-      for (int j = 0; j < WN; ++j) {
-        const int nrow = wc * 16 * WN + j * 16 + (lane & 15);
-        bfr[j] = *reinterpret_cast<const bf16x8*>(base + A_ST + ((nrow >> 6) * 2 + kh) * SUB +
-                                                  (nrow & 63) * LDK_BF + 8 * (lane >> 4));
-      }
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < WN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    }
-    if (s + 1 < nst) sstore(cur ^ 1);
-    __syncthreads();
-  }
-  epilogue<WN>(p, acc, m0, n0, cOff, bz, wr, wc, lane);
-}
-
 template <bool BF16, int AM, int BMODE>
 __global__ __launch_bounds__(NT) void gemm_kernel(P p) {
   constexpr int LDS_ELEMS = BF16 ? (64 * LDK_BF / 2) : (BK * LDX_F32);  // in floats
@@ -453,25 +279,67 @@ __global__ __launch_bounds__(NT) void gemm_kernel(P p) {
     }
   }
 
-  epilogue<2>(p, acc, m0, n0, cOff, bz, wr, wc, lane);
+  // ---- epilogue ----
+  const int epi = p.epi;
+  uint64_t seed = 0;
+  if (epi & KDFM_EPI_DROPOUT) seed = load_seed(p.seed);
+  const float keep_scale = (epi & KDFM_EPI_DROPOUT) ? 1.f / (1.f - p.dropout_p) : 1.f;
+  float mse_part = 0.f;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t m = m0 + wr * 32 + i * 16 + (lane >> 4) * 4 + r;
+        const int64_t n = n0 + wc * 32 + j * 16 + (lane & 15);
+        if (m >= p.M || n >= p.N) continue;
+        const int64_t off = cOff + m * p.sCm + n * p.sCn;
+        float v = p.alpha * acc[i][j][r];
+        if (epi & KDFM_EPI_ATOMIC) {
+          if (n == p.ones_col)
+            atomicAdd(p.ones_out + m, v);
+          else
+            atomicAdd(p.C + off, v);
+          continue;
+        }
+        if (epi & KDFM_EPI_BIAS) v += p.bias[n];
+        if (epi & KDFM_EPI_MSE) {
+          const float diff = v - p.R[off];
+          mse_part += diff * diff;
+          p.C[off] = p.rscale * diff;
+          continue;
+        }
+        if (epi & KDFM_EPI_STORE_PRE) p.Cpre[off] = v;
+        if (epi & KDFM_EPI_RELU) v = fmaxf(v, 0.f);
+        if (epi & KDFM_EPI_SILU) v = siluf_(v);
+        if (epi & KDFM_EPI_DROPOUT) {
+          const uint64_t idx = ((uint64_t)bz * (uint64_t)p.M + (uint64_t)m) * (uint64_t)p.N + (uint64_t)n;
+          v = dropout_keep(seed, p.rng_stream, idx, p.dropout_p) ? v * keep_scale : 0.f;
+        }
+        if (epi & KDFM_EPI_DRELU) v = (p.aux[off] > 0.f) ? v : 0.f;
+        if (epi & KDFM_EPI_DSILU) v *= dsiluf_(p.aux[off]);
+        if (epi & KDFM_EPI_RESID) v = p.R[off] + p.rscale * v;
+        if (epi & KDFM_EPI_BETA) v += p.beta * p.C[off];
+        if (epi & KDFM_EPI_ROWMASK) {
+          const int64_t fr = m / p.mask_div;
+          const int64_t t = fr % p.mask_T, u = fr / p.mask_T;
+          if (t >= p.mask_len[u]) v = 0.f;
+        }
+        p.C[off] = v;
+      }
+  if (epi & KDFM_EPI_MSE) {
+    mse_part = wave_sum(mse_part);
+    if (lane == 0) atomicAdd(p.loss_acc, mse_part * p.loss_scale);
+  }
 }
-
-// wave N-tiles: 4 (block N = 128) when it pads N no more than the 64-wide tile does
-inline int pick_wn(int64_t N) { return (ceil_div(N, 128) * 128 <= ceil_div(N, 64) * 64) ? 4 : 2; }
 
 template <bool BF16>
 int launch(const P& p, int amode, int bmode, dim3 grid, hipStream_t st) {
-  const int wn = BF16 ? pick_wn(p.N) : 2;
-  if (BF16) grid.y = (unsigned)ceil_div(p.N, 32 * wn);
-#define KDFM_GEMM_CASE(AMv, BMv)                                                            \
-  if (amode == AMv && bmode == BMv) {                                                       \
-    if (!BF16)                                                                              \
-      hipLaunchKernelGGL((gemm_kernel<false, AMv, BMv>), grid, dim3(NT), 0, st, p);          \
-    else if (wn == 4)                                                                       \
-      hipLaunchKernelGGL((gemm_bf16_kernel<AMv, BMv, 4>), grid, dim3(NT), 0, st, p);        \
-    else                                                                                    \
-      hipLaunchKernelGGL((gemm_bf16_kernel<AMv, BMv, 2>), grid, dim3(NT), 0, st, p);        \
-    return check_launch("kdfm_gemm");                                                       \
+#define KDFM_GEMM_CASE(AMv, BMv)                                                    \
+  if (amode == AMv && bmode == BMv) {                                               \
+    hipLaunchKernelGGL((gemm_kernel<BF16, AMv, BMv>), grid, dim3(NT), 0, st, p);    \
+    return check_launch("kdfm_gemm");                                               \
   }
   KDFM_GEMM_CASE(KDFM_LD_KC, KDFM_LD_KC)
   KDFM_GEMM_CASE(KDFM_LD_KC, KDFM_LD_XC)

@@ -138,13 +138,11 @@ def gemm(A, B, Cout, M, N, K, sAm, sAk, sBk, sBn, sCm, sCn, *, amode, bmode,
 
 
 def _splitk_for(M, N, K):
-    """K-splits for weight-gradient GEMMs (M, N <= ~700, K = rows up to ~2.6e5): aim for ~1024
-    blocks with >= 512 rows each, so every block's serial K loop stays short (latency-bound)."""
     tiles = -(-M // 64) * -(-N // 64)
-    if K <= 1024 or tiles >= 512:
+    if K <= 512 or tiles >= 256:
         return 1
-    want = max(1, 1024 // tiles)
-    return int(min(want, max(1, K // 512), 4096))
+    want = max(1, 512 // tiles)
+    return int(min(want, max(1, K // 512), 1024))
 
 
 def linear(x, W, bias, out, *, epi=0, R=None, rscale=1.0, Cpre=None, dropout_p=0.0, seed=None, rng_stream=0,

@@ -72,24 +72,3 @@ def test_conv3_mode(K):
            epi=_lib.EPI_BIAS, bias=b, conv=(3, 1, Cc, T), math="f32")
     ref = torch.nn.functional.conv1d(x.transpose(1, 2), W, b, padding=1).transpose(1, 2).reshape(Bn * T, Cc)
     torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-4)
-
-
-@pytest.mark.parametrize("M,N,Kd", [(205312, 96, 96), (12832, 352, 88), (12832, 97, 44), (777, 129, 300)])
-def test_bf16_wide_tiles_and_splitk(K, M, N, Kd):
-    """bf16 main loop (BK=64 double-buffered; N=96/97/352 take the 128-wide tile) incl. split-K dW with
-    the fused ones column (bias gradient)."""
-    g = torch.Generator(device="cuda").manual_seed(3)
-    x = torch.randn(M, Kd, device="cuda", generator=g)
-    W = torch.randn(N, Kd, device="cuda", generator=g) * 0.1
-    b = torch.randn(N, device="cuda", generator=g)
-    y = torch.empty(M, N, device="cuda")
-    K.linear(x, W, b, y, math="bf16")
-    ref = x @ W.T + b
-    torch.testing.assert_close(y, ref, rtol=3e-2, atol=3e-2 * ref.abs().max().item())
-    dy = torch.randn(M, N, device="cuda", generator=g)
-    dW = torch.zeros(N, Kd, device="cuda")
-    db = torch.zeros(N, device="cuda")
-    K.linear_dw(dy, x, dW, db=db, math="bf16")
-    rW, rb = dy.T @ x, dy.sum(0)
-    torch.testing.assert_close(dW, rW, rtol=3e-2, atol=2e-2 * rW.abs().max().item())
-    torch.testing.assert_close(db, rb, rtol=3e-2, atol=2e-2 * rb.abs().max().item())
