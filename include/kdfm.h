@@ -146,9 +146,12 @@ int kdfm_col2im_3x3s2(const float* dcols, const int64_t* len_in, const float* re
 int kdfm_layernorm_fwd(const float* x, const float* gamma, const float* beta, float* y, float* mean, float* rstd,
                        int64_t rows, int64_t d, float eps, void* stream);
 /* dx = LN'(dy) (+ dres if non-null); dgamma/dbeta accumulate (+=). */
+/* dgamma/dbeta are accumulated (+=) through per-block partials in ws, which must hold at least
+ * kdfm_layernorm_bwd_ws(rows, d) floats (no zeroing needed) */
 int kdfm_layernorm_bwd(const float* dy, const float* x, const float* gamma, const float* mean, const float* rstd,
-                       const float* dres, float* dx, float* dgamma, float* dbeta, int64_t rows, int64_t d,
+                       const float* dres, float* dx, float* dgamma, float* dbeta, float* ws, int64_t rows, int64_t d,
                        void* stream);
+int64_t kdfm_layernorm_bwd_ws(int64_t rows, int64_t d);
 /* Qu = Q + pos_bias_u, Qv = Q + pos_bias_v from the fused (rows, 3d) q|k|v projection */
 int kdfm_qkv_prep(const float* qkv, const float* pos_bias_u, const float* pos_bias_v, float* qu, float* qv,
                   int64_t rows, int64_t d, void* stream);
@@ -169,8 +172,10 @@ int kdfm_glu_mask_bwd(const float* dg, const float* a, const int64_t* lengths, f
 int kdfm_dwconv_fwd(const float* g, const float* w, const float* bias, float* y, double* stats, int64_t B, int64_t T,
                     int64_t d, int64_t K, void* stream);
 /* dg = conv^T(dy); dw, db accumulate (+=) */
-int kdfm_dwconv_bwd(const float* dy, const float* g, const float* w, float* dg, float* dw, float* db, int64_t B,
-                    int64_t T, int64_t d, int64_t K, void* stream);
+/* dw/db accumulated (+=) through per-block partials in ws (>= kdfm_dwconv_bwd_ws(B, T, d, K) floats) */
+int kdfm_dwconv_bwd(const float* dy, const float* g, const float* w, float* dg, float* dw, float* db, float* ws,
+                    int64_t B, int64_t T, int64_t d, int64_t K, void* stream);
+int64_t kdfm_dwconv_bwd_ws(int64_t B, int64_t T, int64_t d, int64_t K);
 int kdfm_bn_finalize(const double* stats, const float* running_mean, const float* running_var, float* mean,
                      float* rstd, int64_t d, int64_t count, float eps, void* stream);
 int kdfm_bn_running_update(float* running_mean, float* running_var, const double* stats, int64_t d, int64_t count,

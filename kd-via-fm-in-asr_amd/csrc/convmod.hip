@@ -200,63 +200,117 @@ __global__ void bn_param_grad_kernel(const double* __restrict__ red, float* __re
   dbeta[c] += (float)red[c];
 }
 
-// dg[b,t,c] = sum_k w[c,k] * dy[b,t-k+pad,c];  dw[c,k] += sum dy[b,t,c]*g[b,t+k-pad,c]; db += sum dy
+// Backward of the depthwise conv over one (TT frames x CT channels) tile of one utterance:
+//   dg[b,t,c] = sum_k w[c,k] * dy[b,t-k+pad,c]
+//   dw[c,k]  += sum_t dy[b,t,c] * g[b,t+k-pad,c],   db[c] += sum_t dy[b,t,c]
+// Lane = channel, wave = a 16-frame group.  With the kernel size known at compile time (KC > 0)
+// both sums run from register sliding windows (one LDS read per 16..K FMAs); KC == 0 is the
+// runtime-K path.  Weight/bias sums land in part[(b*ntt + tile)][c*K + k | d*K + c] and are folded
+// by launch_colsum on the host side (no hot atomics).
+template <int KC>
 __global__ __launch_bounds__(256) void dwconv_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ g,
                                                          const float* __restrict__ w, float* __restrict__ dg,
-                                                         float* __restrict__ dw, float* __restrict__ db, int64_t T,
-                                                         int64_t d, int K) {
-  __shared__ float tdy[(TT + KMAX - 1) * CT];  // dy rows t0-pad' .. (for dg: needs t - k + pad)
-  __shared__ float tg[(TT + KMAX - 1) * CT];   // g rows t0-pad .. t0+TT-1+pad
-  __shared__ float wt[CT * KMAX];
+                                                         float* __restrict__ part, int64_t T, int64_t d, int Krt) {
+  constexpr int KM = KC > 0 ? KC : KMAX;
+  __shared__ float tdy[(TT + KM - 1) * CT];  // frames t0-pad .. t0+TT-1+pad
+  __shared__ float tg[(TT + KM - 1) * CT];
+  __shared__ float red[(KM + 1) * CT];
+  const int K = KC > 0 ? KC : Krt;
   const int pad = (K - 1) / 2;
   const int64_t b = blockIdx.z;
   const int64_t t0 = (int64_t)blockIdx.x * TT;
   const int64_t c0 = (int64_t)blockIdx.y * CT;
   const int rowsIn = TT + K - 1;
-  // dy tile holds frames t0 - (K-1-pad) ... t0 + TT - 1 + pad  (index rr -> t = t0 + rr - (K-1-pad))
-  const int lo = K - 1 - pad;
   for (int e = threadIdx.x; e < rowsIn * CT; e += 256) {
     const int rr = e / CT, cc = e % CT;
     const int64_t c = c0 + cc;
-    const int64_t td = t0 + rr - lo;
-    tdy[e] = (td >= 0 && td < T && c < d) ? dy[(b * T + td) * d + c] : 0.f;
-    const int64_t tg_ = t0 + rr - pad;
-    tg[e] = (tg_ >= 0 && tg_ < T && c < d) ? g[(b * T + tg_) * d + c] : 0.f;
+    const int64_t t = t0 + rr - pad;
+    const bool ok = t >= 0 && t < T && c < d;
+    tdy[e] = ok ? dy[(b * T + t) * d + c] : 0.f;
+    tg[e] = ok ? g[(b * T + t) * d + c] : 0.f;
   }
-  for (int e = threadIdx.x; e < CT * K; e += 256) {
-    const int cc = e / K, k = e % K;
-    wt[cc * KMAX + k] = (c0 + cc < d) ? w[(c0 + cc) * K + k] : 0.f;
-  }
+  for (int e = threadIdx.x; e < (K + 1) * CT; e += 256) red[e] = 0.f;
   __syncthreads();
   const int cc = threadIdx.x & 63;
-  const int tq = threadIdx.x >> 6;
+  const int f0 = (threadIdx.x >> 6) * 16;  // this wave's first frame in the tile
   const int64_t c = c0 + cc;
-  if (c < d) {
-    for (int tt = tq; tt < TT; tt += 4) {
-      const int64_t t = t0 + tt;
-      if (t >= T) break;
-      // dy[t - k + pad] -> tdy index (t - k + pad) - t0 + lo = tt - k + pad + lo = tt + (K-1) - k
+  const bool cok = c < d;
+  float bsum = 0.f;
+  if constexpr (KC > 0) {
+    // Sliding 16-frame register windows with the tap loop outermost: every register index is a
+    // compile-time constant (a data-dependent tap index would make the compiler fall back to
+    // VGPR-indexed moves).  Tile row r <-> frame t0 + r - pad.
+    // dg[f0+tt] = sum_k w[K-1-kk] * tdy[f0 + tt + kk]   (kk = K-1-k)
+    float win[16], acc[16];
+#pragma unroll
+    for (int tt = 0; tt < 16; ++tt) {
+      win[tt] = tdy[(f0 + tt) * CT + cc];
+      acc[tt] = 0.f;
+    }
+#pragma unroll
+    for (int kk = 0; kk < KC; ++kk) {
+      const float wk = cok ? w[c * KC + (KC - 1 - kk)] : 0.f;
+#pragma unroll
+      for (int tt = 0; tt < 16; ++tt) acc[tt] += wk * win[tt];
+      if (kk + 1 < KC) {
+#pragma unroll
+        for (int tt = 0; tt < 15; ++tt) win[tt] = win[tt + 1];
+        win[15] = tdy[(f0 + kk + 16) * CT + cc];
+      }
+    }
+    if (cok) {
+#pragma unroll
+      for (int tt = 0; tt < 16; ++tt) {
+        const int64_t t = t0 + f0 + tt;
+        if (t < T) dg[(b * T + t) * d + c] = acc[tt];
+      }
+    }
+    // dw[k] = sum_tt dy[f0+tt] * tg[f0 + tt + k]
+    float dyr[16];
+#pragma unroll
+    for (int tt = 0; tt < 16; ++tt) {
+      dyr[tt] = tdy[(f0 + tt + pad) * CT + cc];
+      bsum += dyr[tt];
+      win[tt] = tg[(f0 + tt) * CT + cc];
+    }
+#pragma unroll
+    for (int k = 0; k < KC; ++k) {
+      float s = 0.f;
+#pragma unroll
+      for (int tt = 0; tt < 16; ++tt) s += dyr[tt] * win[tt];
+      atomicAdd(&red[k * CT + cc], s);
+      if (k + 1 < KC) {
+#pragma unroll
+        for (int tt = 0; tt < 15; ++tt) win[tt] = win[tt + 1];
+        win[15] = tg[(f0 + k + 16) * CT + cc];
+      }
+    }
+  } else {
+    for (int tt = 0; tt < 16; ++tt) {
+      const int64_t t = t0 + f0 + tt;
       float acc = 0.f;
-      for (int k = 0; k < K; ++k) acc += wt[cc * KMAX + k] * tdy[(tt + K - 1 - k) * CT + cc];
-      dg[(b * T + t) * d + c] = acc;
+      for (int k = 0; k < K; ++k) acc += (cok ? w[c * K + k] : 0.f) * tdy[(f0 + tt + K - 1 - k) * CT + cc];
+      if (cok && t < T) dg[(b * T + t) * d + c] = acc;
+      bsum += tdy[(f0 + tt + pad) * CT + cc];
+    }
+    for (int k = 0; k < K; ++k) {
+      float acc = 0.f;
+      for (int tt = 0; tt < 16; ++tt) acc += tdy[(f0 + tt + pad) * CT + cc] * tg[(f0 + tt + k) * CT + cc];
+      atomicAdd(&red[k * CT + cc], acc);
     }
   }
-  // weight / bias gradient partials over this tile's frames
-  for (int e = threadIdx.x; e < CT * (K + 1); e += 256) {
-    const int q = e % CT, k = e / CT;  // k == K -> bias
+  atomicAdd(&red[K * CT + cc], bsum);
+  __syncthreads();
+  const int64_t ld = d * (K + 1);
+  float* pr = part + (b * gridDim.x + blockIdx.x) * ld;
+  for (int e = threadIdx.x; e < (K + 1) * CT; e += 256) {
+    const int q = e / (K + 1), k = e % (K + 1);
     const int64_t cq = c0 + q;
     if (cq >= d) continue;
-    float acc = 0.f;
-    for (int tt = 0; tt < TT; ++tt) {
-      const int64_t t = t0 + tt;
-      if (t >= T) break;
-      const float dyv = tdy[(tt + lo) * CT + q];
-      acc += (k < K) ? dyv * tg[(tt + k) * CT + q] : dyv;
-    }
     if (k < K)
-      atomicAdd(dw + cq * K + k, acc);
+      pr[cq * K + k] = red[k * CT + q];
     else
-      atomicAdd(db + cq, acc);
+      pr[d * K + cq] = red[K * CT + q];
   }
 }
 
@@ -298,15 +352,32 @@ int kdfm_dwconv_fwd(const float* g, const float* w, const float* bias, float* y,
   return check_launch("kdfm_dwconv_fwd");
 }
 
-int kdfm_dwconv_bwd(const float* dy, const float* g, const float* w, float* dg, float* dw, float* db, int64_t B,
-                    int64_t T, int64_t d, int64_t K, void* stream) {
+int64_t kdfm_dwconv_bwd_ws(int64_t B, int64_t T, int64_t d, int64_t K) {
+  return B * kdfm::ceil_div(T, kdfm::TT) * d * (K + 1);
+}
+
+int kdfm_dwconv_bwd(const float* dy, const float* g, const float* w, float* dg, float* dw, float* db, float* ws,
+                    int64_t B, int64_t T, int64_t d, int64_t K, void* stream) {
   using namespace kdfm;
-  KDFM_REQUIRE(dy && g && w && dg && dw && db, "null pointer");
+  KDFM_REQUIRE(dy && g && w && dg && dw && db && ws, "null pointer");
   KDFM_REQUIRE(K >= 1 && K <= KMAX && (K % 2) == 1, "kernel size must be odd and <= 63");
   if (B * T * d == 0) return KDFM_OK;
-  dim3 grid((unsigned)ceil_div(T, TT), (unsigned)ceil_div(d, CT), (unsigned)B);
-  hipLaunchKernelGGL(dwconv_bwd_kernel, grid, dim3(256), 0, as_stream(stream), dy, g, w, dg, dw, db, T, d, (int)K);
-  return check_launch("kdfm_dwconv_bwd");
+  static_assert(TT == 64, "dwconv_bwd assumes 4 waves x 16 frames per tile");
+  hipStream_t st = as_stream(stream);
+  const int64_t ntt = ceil_div(T, TT);
+  dim3 grid((unsigned)ntt, (unsigned)ceil_div(d, CT), (unsigned)B);
+  if (K == 31)
+    hipLaunchKernelGGL(dwconv_bwd_kernel<31>, grid, dim3(256), 0, st, dy, g, w, dg, ws, T, d, (int)K);
+  else if (K == 15)
+    hipLaunchKernelGGL(dwconv_bwd_kernel<15>, grid, dim3(256), 0, st, dy, g, w, dg, ws, T, d, (int)K);
+  else
+    hipLaunchKernelGGL(dwconv_bwd_kernel<0>, grid, dim3(256), 0, st, dy, g, w, dg, ws, T, d, (int)K);
+  int rc = check_launch("kdfm_dwconv_bwd");
+  if (rc) return rc;
+  const int64_t ld = d * (K + 1);
+  rc = launch_colsum(ws, dw, B * ntt, d * K, ld, 1.f, st);
+  if (rc) return rc;
+  return launch_colsum(ws + d * K, db, B * ntt, d, ld, 1.f, st);
 }
 
 int kdfm_bn_finalize(const double* stats, const float* running_mean, const float* running_var, float* mean,

@@ -52,6 +52,19 @@ __global__ void zero_kernel(float* out, int64_t n) {
 }
 }  // namespace
 
+int launch_colsum(const float* X, float* out, int64_t M, int64_t N, int64_t ld, float scale, hipStream_t st) {
+  if (M == 0 || N == 0) return KDFM_OK;
+  const int64_t gx = ceil_div(N, 64);
+  int64_t gy = ceil_div(M, 128);
+  if (gy * gx > 2048) gy = (2048 + gx - 1) / gx;
+  if (gy < 1) gy = 1;
+  const int64_t rows_per = ceil_div(M, gy);
+  gy = ceil_div(M, rows_per);
+  hipLaunchKernelGGL(colsum_kernel, dim3((unsigned)gx, (unsigned)gy), dim3(256), 0, st, X, out, M, N, ld, rows_per,
+                     scale);
+  return check_launch("colsum");
+}
+
 }  // namespace kdfm
 
 extern "C" {
@@ -84,15 +97,7 @@ int kdfm_colsum(const float* X, float* out, int64_t M, int64_t N, int64_t ld, fl
     int rc = check_launch("kdfm_colsum(zero)");
     if (rc) return rc;
   }
-  if (M == 0 || N == 0) return KDFM_OK;
-  const int64_t gx = ceil_div(N, 64);
-  int64_t gy = ceil_div(M, 128);
-  if (gy * gx > 2048) gy = (2048 + gx - 1) / gx;
-  const int64_t rows_per = ceil_div(M, gy);
-  gy = ceil_div(M, rows_per);
-  hipLaunchKernelGGL(colsum_kernel, dim3((unsigned)gx, (unsigned)gy), dim3(256), 0, st, X, out, M, N, ld, rows_per,
-                     scale);
-  return check_launch("kdfm_colsum");
+  return launch_colsum(X, out, M, N, ld, scale, st);
 }
 
 }  // extern "C"

@@ -72,7 +72,8 @@ SIGNATURES: dict[str, tuple] = {
     "kdfm_im2col_3x3s2": (_i32, [P, P, P, _i64, _i64, _i64, _i64, P]),
     "kdfm_col2im_3x3s2": (_i32, [P, P, P, P, _i64, _i64, _i64, _i64, P]),
     "kdfm_layernorm_fwd": (_i32, [P, P, P, P, P, P, _i64, _i64, _f32, P]),
-    "kdfm_layernorm_bwd": (_i32, [P, P, P, P, P, P, P, P, P, _i64, _i64, P]),
+    "kdfm_layernorm_bwd": (_i32, [P, P, P, P, P, P, P, P, P, P, _i64, _i64, P]),
+    "kdfm_layernorm_bwd_ws": (_i64, [_i64, _i64]),
     "kdfm_qkv_prep": (_i32, [P, P, P, P, P, _i64, _i64, P]),
     "kdfm_relpos_softmax_fwd": (_i32, [P, P, P, P, P, _i64, _i64, _i64, _f32, _f32, P, C.c_uint64, P]),
     "kdfm_relpos_softmax_bwd": (_i32, [P, P, P, P, _i64, _i64, _i64, _f32, _f32, P, C.c_uint64, P]),
@@ -80,7 +81,8 @@ SIGNATURES: dict[str, tuple] = {
     "kdfm_glu_mask_fwd": (_i32, [P, P, P, _i64, _i64, _i64, P]),
     "kdfm_glu_mask_bwd": (_i32, [P, P, P, P, _i64, _i64, _i64, P]),
     "kdfm_dwconv_fwd": (_i32, [P, P, P, P, P, _i64, _i64, _i64, _i64, P]),
-    "kdfm_dwconv_bwd": (_i32, [P, P, P, P, P, P, _i64, _i64, _i64, _i64, P]),
+    "kdfm_dwconv_bwd": (_i32, [P, P, P, P, P, P, P, _i64, _i64, _i64, _i64, P]),
+    "kdfm_dwconv_bwd_ws": (_i64, [_i64, _i64, _i64, _i64]),
     "kdfm_bn_finalize": (_i32, [P, P, P, P, P, _i64, _i64, _f32, P]),
     "kdfm_bn_running_update": (_i32, [P, P, P, _i64, _i64, _f32, P]),
     "kdfm_bn_silu_fwd": (_i32, [P, P, P, P, P, P, _i64, _i64, P]),

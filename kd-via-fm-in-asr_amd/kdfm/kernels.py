@@ -87,6 +87,21 @@ def _s():
     return stream_ptr()
 
 
+_SCRATCH: dict = {}
+
+
+def scratch(dev, nfloats: int):
+    """Per-device f32 scratch for per-block reduction partials.  Consumers use it strictly in
+    stream order (kernel then fold), so one buffer serves every call site; it only grows, and the
+    eager warm-up step sizes it before any graph capture."""
+    key = torch.device(dev).index if torch.device(dev).index is not None else torch.cuda.current_device()
+    buf = _SCRATCH.get(key)
+    if buf is None or buf.numel() < nfloats:
+        buf = torch.empty(max(int(nfloats), 1 << 16), device=dev, dtype=torch.float32)
+        _SCRATCH[key] = buf
+    return buf
+
+
 # ------------------------------------------------------------------------------------------------
 # GEMM
 # ------------------------------------------------------------------------------------------------
@@ -334,8 +349,9 @@ def layernorm_fwd(x, g, b, y, mean, rstd, eps):
 def layernorm_bwd(dy, x, g, mean, rstd, dx, dg, db, dres=None):
     rows, d = x.shape
     assert dy.is_contiguous() and dx.is_contiguous() and (dres is None or dres.is_contiguous())
+    ws = scratch(x.device, _lib.lib().kdfm_layernorm_bwd_ws(rows, d))
     call("kdfm_layernorm_bwd", ptr(dy), ptr(x), ptr(g), ptr(mean), ptr(rstd), ptr(dres), ptr(dx), ptr(dg), ptr(db),
-         rows, d, _s())
+         ptr(ws), rows, d, _s())
 
 
 def qkv_prep(qkv, u, v, qu, qv):
@@ -369,7 +385,8 @@ def dwconv_fwd(g, w, bias, y, stats, B, T, d, K):
 
 
 def dwconv_bwd(dy, g, w, dg, dw, db, B, T, d, K):
-    call("kdfm_dwconv_bwd", ptr(dy), ptr(g), ptr(w), ptr(dg), ptr(dw), ptr(db), B, T, d, K, _s())
+    ws = scratch(dy.device, _lib.lib().kdfm_dwconv_bwd_ws(B, T, d, K))
+    call("kdfm_dwconv_bwd", ptr(dy), ptr(g), ptr(w), ptr(dg), ptr(dw), ptr(db), ptr(ws), B, T, d, K, _s())
 
 
 def bn_finalize(stats, rm, rv, mean, rstd, d, count, eps):

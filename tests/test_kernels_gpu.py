@@ -1,0 +1,67 @@
+"""Unit parity of the reduction-heavy backward kernels against torch fp32 autograd (the numerics
+reference for a single floating-point op).  Tolerance: 1e-4 relative to the max |ref| (f32
+accumulation-order differences only)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _K():
+    from kdfm import kernels as K
+    return K
+
+
+def _close(a, b, rel=1e-4):
+    tol = rel * b.abs().max().item() + 1e-6
+    err = (a - b).abs().max().item()
+    assert err <= tol, f"max err {err} > {tol}"
+
+
+@pytest.mark.parametrize("rows,d", [(1, 88), (63, 88), (12832, 88), (1000, 176), (77, 256), (130, 40)])
+def test_layernorm_bwd(rows, d):
+    K = _K()
+    g = torch.Generator().manual_seed(rows + d)
+    x = torch.randn(rows, d, generator=g).cuda()
+    gam = torch.randn(d, generator=g).cuda()
+    bet = torch.randn(d, generator=g).cuda()
+    dy = torch.randn(rows, d, generator=g).cuda()
+    dres = torch.randn(rows, d, generator=g).cuda()
+    y = torch.empty_like(x)
+    mean = torch.empty(rows, device="cuda")
+    rstd = torch.empty(rows, device="cuda")
+    K.layernorm_fwd(x, gam, bet, y, mean, rstd, 1e-5)
+    xr, gr, br = (t.clone().requires_grad_() for t in (x, gam, bet))
+    yr = torch.nn.functional.layer_norm(xr, (d,), gr, br, 1e-5)
+    yr.backward(dy)
+    dx = torch.empty_like(x)
+    dg = torch.full((d,), 0.5, device="cuda")   # accumulates into existing grads
+    db = torch.full((d,), -0.25, device="cuda")
+    K.layernorm_bwd(dy, x, gam, mean, rstd, dx, dg, db, dres=dres)
+    torch.cuda.synchronize()
+    _close(y, yr.detach())
+    _close(dx, xr.grad + dres)
+    _close(dg - 0.5, gr.grad)
+    _close(db + 0.25, br.grad)
+
+
+@pytest.mark.parametrize("B,T,d,k", [(2, 26, 88, 31), (3, 401, 88, 31), (2, 130, 176, 31), (2, 70, 40, 15),
+                                     (2, 50, 24, 7)])
+def test_dwconv_bwd(B, T, d, k):
+    K = _K()
+    g = torch.Generator().manual_seed(B * T + d + k)
+    x = torch.randn(B, T, d, generator=g).cuda()
+    w = torch.randn(d, k, generator=g).cuda()
+    bias = torch.randn(d, generator=g).cuda()
+    dy = torch.randn(B, T, d, generator=g).cuda()
+    xr, wr, br = (t.clone().requires_grad_() for t in (x, w, bias))
+    yr = torch.nn.functional.conv1d(xr.transpose(1, 2), wr.unsqueeze(1), br, padding=(k - 1) // 2, groups=d)
+    yr.transpose(1, 2).backward(dy)
+    dx = torch.empty_like(x)
+    dw = torch.zeros(d, k, device="cuda")
+    db = torch.zeros(d, device="cuda")
+    K.dwconv_bwd(dy, x, w, dx, dw, db, B, T, d, k)
+    torch.cuda.synchronize()
+    _close(dx, xr.grad)
+    _close(dw, wr.grad)
+    _close(db, br.grad)
