@@ -106,9 +106,15 @@ typedef struct kdfm_gemm_desc {
    * ones_col is atomically added into ones_out[m] instead of C.  Requires EPI_ATOMIC. */
   float* ones_out;
   int64_t ones_col;
+  /* optional device workspace (f32 elements): lets bf16 weight-gradient GEMMs (amode XC, EPI_ATOMIC,
+   * K >> M*N) run as one wide-tile pass per row chunk with deterministic partial folding instead
+   * of split-K atomics.  NULL / too small -> generic path.  kdfm_gemm_ws() gives the size used. */
+  float* ws;
+  int64_t ws_len;
 } kdfm_gemm_desc;
 
 int kdfm_gemm(const kdfm_gemm_desc* d, void* stream);
+int64_t kdfm_gemm_ws(const kdfm_gemm_desc* d); /* workspace elements kdfm_gemm would use (0: none) */
 
 /* column sums: out[n] (+)= scale * sum_m X[m*ld + n], m < M; accumulate != 0 adds into out.
  * (bias gradients of every Linear / Conv1d on the path) */

@@ -6,7 +6,7 @@
 //   BF16: v_mfma_f32_16x16x32_bf16, LDS image [m][k] (k contiguous, 16-B fragment reads)
 //   F32 : v_mfma_f32_16x16x4_f32 (exact f32), LDS image [k][m] (conflict-free b32 reads)
 // Global->register prefetch of tile t+1 overlaps the MFMAs of tile t (T14 split).
-#include "common.h"
+#include "gemm_common.h"
 
 namespace kdfm {
 namespace {
@@ -15,24 +15,7 @@ constexpr int BM = 64, BN = 64, BK = 32, NT = 256;
 constexpr int LDK_BF = BK + 8;   // bf16 image row stride (elements)
 constexpr int LDX_F32 = BM + 16; // f32 image row stride (elements) -> lanes 16..31 on banks +16
 
-typedef __attribute__((ext_vector_type(8))) short bf16x8;
-typedef __attribute__((ext_vector_type(4))) float f32x4;
-
-struct P {
-  const float* A; const float* B; float* C; const float* bias; const float* R; const float* aux;
-  float* Cpre;
-  int64_t M, N, K;
-  int64_t sAm, sAk, sBk, sBn, sCm, sCn;
-  int64_t batch2;
-  int64_t bA1, bA2, bB1, bB2, bC1, bC2;
-  float alpha, beta, rscale, dropout_p;
-  const uint64_t* seed; uint64_t rng_stream;
-  int epi, splitk, taps, pad;
-  int64_t conv_c, conv_t;
-  const int64_t* mask_len; int64_t mask_T, mask_div;
-  float* loss_acc; float loss_scale;
-  float* ones_out; int64_t ones_col;
-};
+using P = GemmP;
 
 // Operand element fetch for the "row operand" view: X(r, q) where r is the row-like index
 // (m for A, n for B) and q the contraction index k.  Returns 0 outside bounds.
@@ -303,30 +286,7 @@ __global__ __launch_bounds__(NT) void gemm_kernel(P p) {
             atomicAdd(p.C + off, v);
           continue;
         }
-        if (epi & KDFM_EPI_BIAS) v += p.bias[n];
-        if (epi & KDFM_EPI_MSE) {
-          const float diff = v - p.R[off];
-          mse_part += diff * diff;
-          p.C[off] = p.rscale * diff;
-          continue;
-        }
-        if (epi & KDFM_EPI_STORE_PRE) p.Cpre[off] = v;
-        if (epi & KDFM_EPI_RELU) v = fmaxf(v, 0.f);
-        if (epi & KDFM_EPI_SILU) v = siluf_(v);
-        if (epi & KDFM_EPI_DROPOUT) {
-          const uint64_t idx = ((uint64_t)bz * (uint64_t)p.M + (uint64_t)m) * (uint64_t)p.N + (uint64_t)n;
-          v = dropout_keep(seed, p.rng_stream, idx, p.dropout_p) ? v * keep_scale : 0.f;
-        }
-        if (epi & KDFM_EPI_DRELU) v = (p.aux[off] > 0.f) ? v : 0.f;
-        if (epi & KDFM_EPI_DSILU) v *= dsiluf_(p.aux[off]);
-        if (epi & KDFM_EPI_RESID) v = p.R[off] + p.rscale * v;
-        if (epi & KDFM_EPI_BETA) v += p.beta * p.C[off];
-        if (epi & KDFM_EPI_ROWMASK) {
-          const int64_t fr = m / p.mask_div;
-          const int64_t t = fr % p.mask_T, u = fr / p.mask_T;
-          if (t >= p.mask_len[u]) v = 0.f;
-        }
-        p.C[off] = v;
+        epilogue_store(p, bz, m, n, off, v, seed, keep_scale, mse_part);
       }
   if (epi & KDFM_EPI_MSE) {
     mse_part = wave_sum(mse_part);
@@ -389,6 +349,7 @@ extern "C" int kdfm_gemm(const kdfm_gemm_desc* d, void* stream) {
   p.mask_len = d->mask_len; p.mask_T = d->mask_T; p.mask_div = d->mask_div;
   p.loss_acc = d->loss_acc; p.loss_scale = d->loss_scale;
   p.ones_out = d->ones_out; p.ones_col = d->ones_col;
+  p.ws = d->ws; p.ws_len = d->ws_len;
   if (d->ones_col >= 0)
     KDFM_REQUIRE(d->ones_out && (d->epi & KDFM_EPI_ATOMIC) && d->ones_col == d->N - 1 && d->batch1 == 1 &&
                      d->batch2 == 1,
@@ -398,10 +359,28 @@ extern "C" int kdfm_gemm(const kdfm_gemm_desc* d, void* stream) {
                  "ROWMASK needs mask_len/mask_T/mask_div and an unbatched GEMM");
   if (d->epi & KDFM_EPI_MSE) KDFM_REQUIRE(d->loss_acc && d->R, "MSE needs loss_acc and target R");
   if (d->K == 0) p.splitk = 1;
+  hipStream_t st = as_stream(stream);
+  if (d->math == KDFM_MATH_BF16 && d->K > 0) {
+    const int64_t batch = d->batch1 * d->batch2;
+    int rc = try_rowstream_wgrad(p, d->amode, d->bmode, batch, st);
+    if (rc >= 0) return rc;
+    rc = try_rowstream_fwd(p, d->amode, d->bmode, batch, st);
+    if (rc >= 0) return rc;
+  }
   const int64_t gx = ceil_div(d->M, BM), gy = ceil_div(d->N, BN), gz = d->batch1 * d->batch2 * p.splitk;
   KDFM_REQUIRE(gx < (1ll << 31) && gy < 65536 && gz < 65536, "grid too large");
   dim3 grid((unsigned)gx, (unsigned)gy, (unsigned)gz);
-  hipStream_t st = as_stream(stream);
   return d->math == KDFM_MATH_BF16 ? launch<true>(p, d->amode, d->bmode, grid, st)
                                    : launch<false>(p, d->amode, d->bmode, grid, st);
+}
+
+extern "C" int64_t kdfm_gemm_ws(const kdfm_gemm_desc* d) {
+  using namespace kdfm;
+  if (!d || d->math != KDFM_MATH_BF16 || d->K <= 0 || d->M <= 0 || d->N <= 0) return 0;
+  GemmP p{};
+  p.M = d->M; p.N = d->N; p.K = d->K;
+  p.sAm = d->sAm; p.sAk = d->sAk; p.sBk = d->sBk; p.sBn = d->sBn; p.sCm = d->sCm; p.sCn = d->sCn;
+  p.epi = d->epi; p.splitk = d->splitk; p.taps = d->conv_taps; p.pad = d->conv_pad;
+  p.conv_c = d->conv_c; p.conv_t = d->conv_t; p.ones_col = d->ones_col; p.ones_out = d->ones_out;
+  return rowstream_wgrad_ws(p, d->amode, d->bmode, d->batch1 * d->batch2);
 }

@@ -1,0 +1,67 @@
+// Shared pieces of the GEMM family (gemm.hip: generic 64x64-tile kernel; rowstream.hip: full-N
+// row-streaming forward kernel and wide-tile weight-gradient kernel): the launch parameter block
+// and the fused epilogue, so every kernel applies exactly the same per-element semantics
+// (include/kdfm.h, KDFM_EPI_*).
+#pragma once
+#include "common.h"
+
+namespace kdfm {
+
+typedef __attribute__((ext_vector_type(8))) short bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+struct GemmP {
+  const float* A; const float* B; float* C; const float* bias; const float* R; const float* aux;
+  float* Cpre;
+  int64_t M, N, K;
+  int64_t sAm, sAk, sBk, sBn, sCm, sCn;
+  int64_t batch2;
+  int64_t bA1, bA2, bB1, bB2, bC1, bC2;
+  float alpha, beta, rscale, dropout_p;
+  const uint64_t* seed; uint64_t rng_stream;
+  int epi, splitk, taps, pad;
+  int64_t conv_c, conv_t;
+  const int64_t* mask_len; int64_t mask_T, mask_div;
+  float* loss_acc; float loss_scale;
+  float* ones_out; int64_t ones_col;
+  float* ws; int64_t ws_len;
+};
+
+// Non-atomic epilogue for one output element.  v = alpha * acc (already scaled).  bz = batch
+// index (dropout RNG stream position).  Accumulates the MSE partial into mse_part.
+__device__ __forceinline__ void epilogue_store(const GemmP& p, int64_t bz, int64_t m, int64_t n, int64_t off,
+                                               float v, uint64_t seed, float keep_scale, float& mse_part) {
+  const int epi = p.epi;
+  if (epi & KDFM_EPI_BIAS) v += p.bias[n];
+  if (epi & KDFM_EPI_MSE) {
+    const float diff = v - p.R[off];
+    mse_part += diff * diff;
+    p.C[off] = p.rscale * diff;
+    return;
+  }
+  if (epi & KDFM_EPI_STORE_PRE) p.Cpre[off] = v;
+  if (epi & KDFM_EPI_RELU) v = fmaxf(v, 0.f);
+  if (epi & KDFM_EPI_SILU) v = siluf_(v);
+  if (epi & KDFM_EPI_DROPOUT) {
+    const uint64_t idx = ((uint64_t)bz * (uint64_t)p.M + (uint64_t)m) * (uint64_t)p.N + (uint64_t)n;
+    v = dropout_keep(seed, p.rng_stream, idx, p.dropout_p) ? v * keep_scale : 0.f;
+  }
+  if (epi & KDFM_EPI_DRELU) v = (p.aux[off] > 0.f) ? v : 0.f;
+  if (epi & KDFM_EPI_DSILU) v *= dsiluf_(p.aux[off]);
+  if (epi & KDFM_EPI_RESID) v = p.R[off] + p.rscale * v;
+  if (epi & KDFM_EPI_BETA) v += p.beta * p.C[off];
+  if (epi & KDFM_EPI_ROWMASK) {
+    const int64_t fr = m / p.mask_div;
+    const int64_t t = fr % p.mask_T, u = fr / p.mask_T;
+    if (t >= p.mask_len[u]) v = 0.f;
+  }
+  p.C[off] = v;
+}
+
+// Row-stream / wide-tile entry points (rowstream.hip).  try_* return -1 when the descriptor is
+// not eligible (caller falls back to the generic kernel), else a kdfm_status.
+int try_rowstream_fwd(const GemmP& p, int amode, int bmode, int64_t batch, hipStream_t st);
+int try_rowstream_wgrad(const GemmP& p, int amode, int bmode, int64_t batch, hipStream_t st);
+int64_t rowstream_wgrad_ws(const GemmP& p, int amode, int bmode, int64_t batch);
+
+}  // namespace kdfm

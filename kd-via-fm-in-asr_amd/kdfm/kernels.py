@@ -140,6 +140,11 @@ def gemm(A, B, Cout, M, N, K, sAm, sAk, sBk, sBn, sCm, sCn, *, amode, bmode,
         acc, lscale = mse
         d.loss_acc, d.loss_scale = ptr(acc), float(lscale)
         d.epi |= _lib.EPI_MSE
+    if d.epi == _lib.EPI_ATOMIC and d.math == _lib.KDFM_MATH_BF16:
+        nws = _lib.lib().kdfm_gemm_ws(C.byref(d))
+        if nws > 0:
+            ws = scratch(Cout.device, nws)
+            d.ws, d.ws_len = ws.data_ptr(), ws.numel()
     tr = Trace.active
     if tr is not None and tag in tr.tags:
         ev0 = torch.cuda.Event(enable_timing=True)

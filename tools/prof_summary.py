@@ -1,26 +1,49 @@
-"""Summarise a rocprofv3 --kernel-trace CSV: kernel time per step grouped by kernel (+GEMM template
-and grid).  usage: python tools/prof_summary.py <run_kernel_trace.csv> <steps_in_trace> [top]"""
+"""Summarise a rocprofv3 kernel trace (rocpd .db or --output-format csv kernel_trace.csv): kernel
+time per step grouped by kernel (+GEMM template and grid).
+usage: python tools/prof_summary.py <run_results.db | run_kernel_trace.csv> [steps] [top]
+steps defaults to the number of ctc_kernel launches (one per training step)."""
 import collections
 import csv
+import sqlite3
 import sys
 
-path, nsteps = sys.argv[1], float(sys.argv[2])
-top = int(sys.argv[3]) if len(sys.argv) > 3 else 40
-rows = list(csv.DictReader(open(path)))
-agg = collections.defaultdict(lambda: [0, 0.0])
-tot = 0.0
-for r in rows:
-    n = r["Kernel_Name"].replace("kdfm::(anonymous namespace)::", "")
-    d = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
-    tot += d
-    if "gemm" in n:
-        key = n.split("(")[0] + f" grid=({int(r['Grid_Size_X']) // 256},{r['Grid_Size_Y']},{r['Grid_Size_Z']})"
+
+def rows(path):
+    if path.endswith(".db"):
+        c = sqlite3.connect(path)
+        for name, dur, gx, gy, gz, wx in c.execute(
+                "select name, duration, grid_x, grid_y, grid_z, workgroup_x from kernels"):
+            yield name, int(dur), int(gx) // max(int(wx), 1), int(gy), int(gz)
     else:
-        key = n.split("(")[0]
-    agg[key][0] += 1
-    agg[key][1] += d
-print(f"total kernel time per step: {tot / nsteps / 1e6:.3f} ms  ({len(rows) / nsteps:.0f} launches/step)")
-gemm = sum(v[1] for k, v in agg.items() if "gemm" in k)
-print(f"  gemm share: {gemm / tot * 100:.1f}%")
-for k, v in sorted(agg.items(), key=lambda kv: -kv[1][1])[:top]:
-    print(f"{v[1] / nsteps / 1e6:8.3f} ms/step  {v[0] / nsteps:6.1f}/step  avg {v[1] / v[0] / 1e3:8.1f} us  {k}")
+        for r in csv.DictReader(open(path)):
+            wx = int(r.get("Workgroup_Size_X", 256) or 256)
+            yield (r["Kernel_Name"], int(r["End_Timestamp"]) - int(r["Start_Timestamp"]),
+                   int(r["Grid_Size_X"]) // wx, int(r["Grid_Size_Y"]), int(r["Grid_Size_Z"]))
+
+
+def main():
+    path = sys.argv[1]
+    nsteps = float(sys.argv[2]) if len(sys.argv) > 2 and float(sys.argv[2]) > 0 else None
+    top = int(sys.argv[3]) if len(sys.argv) > 3 else 45
+    agg = collections.defaultdict(lambda: [0, 0.0])
+    tot, nl, nctc = 0.0, 0, 0
+    for name, d, gx, gy, gz in rows(path):
+        n = name.replace("kdfm::(anonymous namespace)::", "").replace("kdfm::", "")
+        if n.startswith("ctc_kernel") or "::ctc_kernel" in name:
+            nctc += 1
+        tot += d
+        nl += 1
+        base = n.split("(")[0]
+        key = base + (f" grid=({gx},{gy},{gz})" if "gemm" in n else "")
+        agg[key][0] += 1
+        agg[key][1] += d
+    nsteps = nsteps or max(nctc, 1)
+    print(f"steps={nsteps:g}  total kernel time per step: {tot / nsteps / 1e6:.3f} ms  ({nl / nsteps:.0f} launches/step)")
+    gemm = sum(v[1] for k, v in agg.items() if "gemm" in k)
+    print(f"  gemm share: {gemm / tot * 100:.1f}%")
+    for k, v in sorted(agg.items(), key=lambda kv: -kv[1][1])[:top]:
+        print(f"{v[1] / nsteps / 1e6:8.3f} ms/step  {v[0] / nsteps:6.1f}/step  avg {v[1] / v[0] / 1e3:8.1f} us  {k}")
+
+
+if __name__ == "__main__":
+    main()
