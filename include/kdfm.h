@@ -170,6 +170,15 @@ int kdfm_relpos_softmax_bwd(const float* P, const float* dPdrop, float* dAC, flo
                             void* stream);
 /* sinusoidal table for relative positions T-1 ... -(T-1), (2T-1, d) */
 int kdfm_relpos_table(float* pe, int64_t T, int64_t d, void* stream);
+/* Fused relative-position MHA forward (bf16 MFMA): o[b,t,h*dk+c] = sum_j Pdrop[b,h,t,j] V[b,j,h*dk+c] with
+ * scores ((q+u)K^T + rel_shift((q+v)Ppos^T)) * scale, key-padding mask from lengths, softmax,
+ * inverted dropout (same counter-RNG mask as kdfm_relpos_softmax_fwd).  qu/qv/o: (B*T, d);
+ * qkv: (B*T, 3d) (K at +d, V at +2d); pos: (2T-1, d) projected positions.  P / Pdrop (B,H,T,T) are
+ * written when non-null (backward operands).  dk = d/H <= 48. */
+int kdfm_relpos_attn_fwd(const float* qu, const float* qv, const float* qkv, const float* pos,
+                         const int64_t* lengths, float* o, float* P, float* Pdrop, int64_t B, int64_t H,
+                         int64_t T, int64_t d, float scale, float dropout_p, const uint64_t* seed,
+                         uint64_t rng_stream, void* stream);
 /* conv module: GLU over channels + pad mask; depthwise conv (k odd) with optional f64 BN stats */
 int kdfm_glu_mask_fwd(const float* a, const int64_t* lengths, float* g, int64_t B, int64_t T, int64_t d,
                       void* stream);

@@ -1,0 +1,307 @@
+// Fused relative-position multi-head attention forward (bf16 MFMA, f32 softmax/accumulate).
+//
+// NeMo RelPositionMultiHeadAttention.forward (Appendix A.7; called per ConformerLayer,
+// conformer_encoder.py:685-692): scores = ((q+u)K^T + rel_shift((q+v)P^T)) / sqrt(dk), key padding
+// mask, softmax, dropout_att, P V.  The unfused path materialises AC (B,H,T,T) and BD (B,H,T,2T-1)
+// in HBM; here one workgroup owns (b, h, 64 query rows) and streams 64-key blocks:
+//   * S_ac = Qu K_blk^T (per wave 16 x 64), Qu/Qv fragments live in registers;
+//   * the BD term only needs the 127-row band of P that the block's (i, j) pairs address
+//     (r = T-1-i+j); each wave computes G = Qv P_band^T (16 x 80) and reads it back skewed from
+//     LDS: S_bd[ii][jj] = G[ii][jj - ii + 15]  (rel_shift as an index map, no copy);
+//   * two passes over the key blocks: (1) row max and sum, (2) exact probabilities, optional
+//     P / P_drop output (the student's backward consumes them), the counter-RNG dropout mask of
+//     the unfused kernel (same index -> same mask) and O += P_drop V via MFMA (P staged through
+//     LDS into A-fragment order, V staged transposed).
+// Output O is written straight into the (rows, d) head-interleaved layout.
+#include "gemm_common.h"
+
+namespace kdfm {
+namespace {
+
+constexpr int AQ = 64;            // query rows per workgroup (4 waves x 16)
+constexpr int AKB = 64;           // keys per block
+constexpr int DKP = 64;           // head dim padded to 2 MFMA k-steps
+constexpr int LDR = DKP + 8;      // bf16 row stride of the [row][c] tiles (K, P band)
+constexpr int LDVT = AKB + 8;     // bf16 row stride of V^T [c][key]
+constexpr int LDPS = AKB + 8;     // bf16 row stride of the per-wave P tile [row][key]
+constexpr int BAND = 128;         // P rows staged per key block (127 used)
+constexpr int GW = 80;            // band columns per wave (79 used)
+constexpr int LDG = GW + 1;       // f32 stride of the per-wave G tile
+
+struct AttnP {
+  const float* qu; const float* qv; const float* k; const float* v; const float* pos;
+  const int64_t* lens;
+  float* o; float* P; float* Pd;
+  int64_t B, H, T, d, dk, ldq, ldkv;
+  float scale, p_drop;
+  const uint64_t* seed; uint64_t rng_stream;
+};
+
+__device__ __forceinline__ bf16x8 load_frag8(const float* src, int valid) {
+  // 8 consecutive floats -> bf16x8, elements >= valid are zero (valid is a multiple of 4 or >= 8)
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+  if (valid >= 4) a = *reinterpret_cast<const float4*>(src);
+  if (valid >= 8) b = *reinterpret_cast<const float4*>(src + 4);
+  bf16x8 r;
+  r[0] = (short)f2bf(a.x); r[1] = (short)f2bf(a.y); r[2] = (short)f2bf(a.z); r[3] = (short)f2bf(a.w);
+  r[4] = (short)f2bf(b.x); r[5] = (short)f2bf(b.y); r[6] = (short)f2bf(b.z); r[7] = (short)f2bf(b.w);
+  return r;
+}
+
+__device__ __forceinline__ void store4_bf16(uint16_t* dst, float4 v) {
+  const uint32_t lo = (uint32_t)f2bf(v.x) | ((uint32_t)f2bf(v.y) << 16);
+  const uint32_t hi = (uint32_t)f2bf(v.z) | ((uint32_t)f2bf(v.w) << 16);
+  *reinterpret_cast<uint2*>(dst) = make_uint2(lo, hi);
+}
+
+// wave-local LDS hand-off: this wave's ds_writes complete before its following ds_reads, and the
+// compiler may not move LDS accesses across the point
+__device__ __forceinline__ void wave_lds_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ float group16_max(float v) {
+#pragma unroll
+  for (int o = 8; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ float group16_sum(float v) {
+#pragma unroll
+  for (int o = 8; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__global__ __launch_bounds__(256, 2) void relpos_attn_fwd_kernel(AttnP p) {
+  __shared__ __attribute__((aligned(16))) uint16_t Ks[AKB * LDR];
+  __shared__ __attribute__((aligned(16))) uint16_t Vt[DKP * LDVT];
+  __shared__ __attribute__((aligned(16))) uint16_t Pr[BAND * LDR];
+  __shared__ __attribute__((aligned(16))) float Gs[4][16 * LDG];
+  __shared__ __attribute__((aligned(16))) uint16_t Ps[4][16 * LDPS];
+
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int T = (int)p.T, dk = (int)p.dk;
+  const int64_t bh = blockIdx.y;
+  const int64_t b = bh / p.H, h = bh - b * p.H;
+  const int i0 = blockIdx.x * AQ;
+  const int len = p.lens ? (int)p.lens[b] : T;
+  const int nkb = (min(len, T) + AKB - 1) / AKB;  // key blocks with at least one valid key
+  const int npos = 2 * T - 1;
+  const int64_t hoff = h * p.dk;
+
+  // zero the padded head-dim columns once (never overwritten afterwards)
+  for (int e = threadIdx.x; e < AKB * (DKP - dk); e += 256) {
+    const int r = e / (DKP - dk), c = dk + e % (DKP - dk);
+    Ks[r * LDR + c] = 0;
+  }
+  for (int e = threadIdx.x; e < BAND * (DKP - dk); e += 256) {
+    const int r = e / (DKP - dk), c = dk + e % (DKP - dk);
+    Pr[r * LDR + c] = 0;
+  }
+  for (int e = threadIdx.x; e < (DKP - dk) * LDVT; e += 256) Vt[dk * LDVT + e] = 0;
+
+  // this lane's query row (A-fragment row) and its Qu / Qv fragments
+  const int iq = i0 + w * 16 + (lane & 15);
+  bf16x8 fu[2], fv[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    const int c0 = ks * 32 + 8 * (lane >> 4);
+    const int valid = (iq < T) ? dk - c0 : 0;
+    const int64_t off = (b * p.T + iq) * p.ldq + hoff + c0;
+    fu[ks] = load_frag8(p.qu + off, valid);
+    fv[ks] = load_frag8(p.qv + off, valid);
+  }
+
+  // rows owned by this lane in the C layout: ii = 4*(lane>>4) + r
+  const int ib = i0 + w * 16 + 4 * (lane >> 4);
+  float mrow[4], lrow[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) { mrow[r] = -3.0e38f; lrow[r] = 0.f; }
+
+  auto stage_kp = [&](int j0, bool with_v) {
+    // K block [key][c]
+    const int cq = dk >> 2;
+    for (int e = threadIdx.x; e < AKB * cq; e += 256) {
+      const int jj = e / cq, c4 = (e - jj * cq) * 4;
+      const int j = j0 + jj;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (j < T) v = *reinterpret_cast<const float4*>(p.k + (b * p.T + j) * p.ldkv + hoff + c4);
+      store4_bf16(Ks + jj * LDR + c4, v);
+      if (with_v) {
+        float4 u = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (j < T) u = *reinterpret_cast<const float4*>(p.v + (b * p.T + j) * p.ldkv + hoff + c4);
+        Vt[(c4 + 0) * LDVT + jj] = f2bf(u.x);
+        Vt[(c4 + 1) * LDVT + jj] = f2bf(u.y);
+        Vt[(c4 + 2) * LDVT + jj] = f2bf(u.z);
+        Vt[(c4 + 3) * LDVT + jj] = f2bf(u.w);
+      }
+    }
+    // P band: rows r = rbase + rr, rbase = T-1-(i0+63)+j0
+    const int rbase = T - 1 - (i0 + AQ - 1) + j0;
+    for (int e = threadIdx.x; e < BAND * cq; e += 256) {
+      const int rr = e / cq, c4 = (e - rr * cq) * 4;
+      const int r = rbase + rr;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (r >= 0 && r < npos) v = *reinterpret_cast<const float4*>(p.pos + (int64_t)r * p.d + hoff + c4);
+      store4_bf16(Pr + rr * LDR + c4, v);
+    }
+  };
+
+  // scores of this wave's 16 rows x 64 keys of block j0, C layout: s[t][r] = S[ii][16t + (lane&15)]
+  auto scores = [&](int j0, float (&s)[4][4]) {
+    f32x4 ac[4], g[5];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) ac[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 5; ++t) g[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int wb = 48 - 16 * w;  // this wave's band offset inside Pr
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int kof = ks * 32 + 8 * (lane >> 4);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const bf16x8 kb = *reinterpret_cast<const bf16x8*>(Ks + (16 * t + (lane & 15)) * LDR + kof);
+        ac[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fu[ks], kb, ac[t], 0, 0, 0);
+      }
+#pragma unroll
+      for (int t = 0; t < 5; ++t) {
+        const bf16x8 pb = *reinterpret_cast<const bf16x8*>(Pr + (wb + 16 * t + (lane & 15)) * LDR + kof);
+        g[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fv[ks], pb, g[t], 0, 0, 0);
+      }
+    }
+    float* G = Gs[w];
+#pragma unroll
+    for (int t = 0; t < 5; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) G[(4 * (lane >> 4) + r) * LDG + 16 * t + (lane & 15)] = g[t][r];
+    wave_lds_sync();
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ii = 4 * (lane >> 4) + r, jj = 16 * t + (lane & 15);
+        const int j = j0 + jj;
+        const float bd = G[ii * LDG + jj - ii + 15];
+        s[t][r] = (j < len && j < T) ? (ac[t][r] + bd) * p.scale : -3.0e38f;
+      }
+    wave_lds_sync();  // G is rewritten by the next call
+  };
+
+  // ---- pass 1: row max / sum ----
+  for (int kb = 0; kb < nkb; ++kb) {
+    const int j0 = kb * AKB;
+    __syncthreads();
+    stage_kp(j0, false);
+    __syncthreads();
+    float s[4][4];
+    scores(j0, s);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float mx = fmaxf(fmaxf(s[0][r], s[1][r]), fmaxf(s[2][r], s[3][r]));
+      mx = group16_max(mx);
+      const float mn = fmaxf(mrow[r], mx);
+      float sum = 0.f;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) sum += (s[t][r] > -1.0e38f) ? __expf(s[t][r] - mn) : 0.f;
+      sum = group16_sum(sum);
+      lrow[r] = lrow[r] * ((mrow[r] > -1.0e38f) ? __expf(mrow[r] - mn) : 0.f) + sum;
+      mrow[r] = mn;
+    }
+  }
+  float inv[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) inv[r] = (ib + r < len && lrow[r] > 0.f) ? 1.f / lrow[r] : 0.f;
+
+  // ---- pass 2: probabilities, dropout, O += Pd V ----
+  const uint64_t seed = (p.p_drop > 0.f) ? load_seed(p.seed) : 0ull;
+  const float keep_scale = (p.p_drop > 0.f) ? 1.f / (1.f - p.p_drop) : 1.f;
+  f32x4 oacc[3];
+#pragma unroll
+  for (int u = 0; u < 3; ++u) oacc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int64_t prow0 = (bh * p.T + ib) * p.T;  // P row of (ib, j = 0)
+  for (int kb = 0; kb < (T + AKB - 1) / AKB; ++kb) {
+    const int j0 = kb * AKB;
+    const bool live = kb < nkb;
+    if (live) {
+      __syncthreads();
+      stage_kp(j0, true);
+      __syncthreads();
+    }
+    float s[4][4];
+    if (live) {
+      scores(j0, s);
+    } else {
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s[t][r] = -3.0e38f;
+    }
+    uint16_t* Pw = Ps[w];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ii = 4 * (lane >> 4) + r, jj = 16 * t + (lane & 15);
+        const int i = ib + r, j = j0 + jj;
+        float pv = (s[t][r] > -1.0e38f) ? __expf(s[t][r] - mrow[r]) * inv[r] : 0.f;
+        float pdv = pv;
+        if (p.p_drop > 0.f && pv != 0.f) {
+          const uint64_t idx = (uint64_t)(prow0 + (int64_t)r * p.T) + (uint64_t)j;
+          pdv = dropout_keep(seed, p.rng_stream, idx, p.p_drop) ? pv * keep_scale : 0.f;
+        }
+        if (i < T && j < T) {
+          const int64_t off = prow0 + (int64_t)r * p.T + j;
+          if (p.P) p.P[off] = pv;
+          if (p.Pd) p.Pd[off] = pdv;
+        }
+        Pw[ii * LDPS + jj] = f2bf(pdv);
+      }
+    if (!live) continue;  // P row tail beyond len is written as zeros; no O contribution
+    wave_lds_sync();
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const bf16x8 pa = *reinterpret_cast<const bf16x8*>(Pw + (lane & 15) * LDPS + ks * 32 + 8 * (lane >> 4));
+#pragma unroll
+      for (int u = 0; u < 3; ++u) {
+        const bf16x8 vb = *reinterpret_cast<const bf16x8*>(Vt + (16 * u + (lane & 15)) * LDVT + ks * 32 + 8 * (lane >> 4));
+        oacc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, vb, oacc[u], 0, 0, 0);
+      }
+    }
+    wave_lds_sync();  // Ps is rewritten by the next block
+  }
+
+  // ---- O -> (rows, d) ----
+#pragma unroll
+  for (int u = 0; u < 3; ++u)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = ib + r, c = 16 * u + (lane & 15);
+      if (i < T && c < dk) p.o[(b * p.T + i) * p.ldq + hoff + c] = oacc[u][r];
+    }
+}
+
+}  // namespace
+}  // namespace kdfm
+
+extern "C" int kdfm_relpos_attn_fwd(const float* qu, const float* qv, const float* qkv, const float* pos,
+                                    const int64_t* lengths, float* o, float* P, float* Pdrop, int64_t B, int64_t H,
+                                    int64_t T, int64_t d, float scale, float dropout_p, const uint64_t* seed,
+                                    uint64_t rng_stream, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(qu && qv && qkv && pos && o, "null pointer");
+  KDFM_REQUIRE(H > 0 && d % H == 0, "d must be a multiple of H");
+  const int64_t dk = d / H;
+  KDFM_REQUIRE(dk <= 48 && dk % 4 == 0, "head dim must be a multiple of 4 and <= 48");
+  KDFM_REQUIRE(T > 0 && T <= 4096, "T out of range");
+  KDFM_REQUIRE(d % 4 == 0, "d must be a multiple of 4");
+  KDFM_REQUIRE(dropout_p == 0.f || seed, "dropout needs a seed");
+  if (B == 0) return KDFM_OK;
+  AttnP p;
+  p.qu = qu; p.qv = qv; p.k = qkv + d; p.v = qkv + 2 * d; p.pos = pos; p.lens = lengths;
+  p.o = o; p.P = P; p.Pd = Pdrop;
+  p.B = B; p.H = H; p.T = T; p.d = d; p.dk = dk; p.ldq = d; p.ldkv = 3 * d;
+  p.scale = scale; p.p_drop = dropout_p; p.seed = seed; p.rng_stream = rng_stream;
+  dim3 grid((unsigned)ceil_div(T, AQ), (unsigned)(B * H));
+  hipLaunchKernelGGL(relpos_attn_fwd_kernel, grid, dim3(256), 0, as_stream(stream), p);
+  return check_launch("kdfm_relpos_attn_fwd");
+}

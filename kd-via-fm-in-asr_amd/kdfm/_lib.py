@@ -79,6 +79,7 @@ SIGNATURES: dict[str, tuple] = {
     "kdfm_qkv_prep": (_i32, [P, P, P, P, P, _i64, _i64, P]),
     "kdfm_relpos_softmax_fwd": (_i32, [P, P, P, P, P, _i64, _i64, _i64, _f32, _f32, P, C.c_uint64, P]),
     "kdfm_relpos_softmax_bwd": (_i32, [P, P, P, P, _i64, _i64, _i64, _f32, _f32, P, C.c_uint64, P]),
+    "kdfm_relpos_attn_fwd": (_i32, [P, P, P, P, P, P, P, P, _i64, _i64, _i64, _i64, _f32, _f32, P, C.c_uint64, P]),
     "kdfm_relpos_table": (_i32, [P, _i64, _i64, P]),
     "kdfm_glu_mask_fwd": (_i32, [P, P, P, _i64, _i64, _i64, P]),
     "kdfm_glu_mask_bwd": (_i32, [P, P, P, P, _i64, _i64, _i64, P]),

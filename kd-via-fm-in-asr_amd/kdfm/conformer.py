@@ -155,22 +155,30 @@ def layer_forward(cfg, S: EncoderShapes, P, L, li, x, out, pos_emb, lengths, *, 
     npos = 2 * T - 1
     ppos = _empty(npos, d, dev=dev)
     K.linear(pos_emb, P[L + "self_attn.linear_pos.weight"], None, ppos)
-    ac = _empty(B, H, T, T, dev=dev)
-    # AC = (q+u) K^T  per (b,h): A(i,c)=qu[b,i,h*dk+c]  B(c,j)=K[b,j,h*dk+c]
-    K.gemm(qu, qkv[:, d:], ac, T, T, dk, d, 1, 1, 3 * d, T, 1, amode=_lib.LD_KC, bmode=_lib.LD_KC,
-           batch=(B, H), bA=(T * d, dk), bB=(T * 3 * d, dk), bC=(H * T * T, T * T))
-    bd = _empty(B, H, T, npos, dev=dev)
-    K.gemm(qv, ppos, bd, T, npos, dk, d, 1, 1, d, npos, 1, amode=_lib.LD_KC, bmode=_lib.LD_KC,
-           batch=(B, H), bA=(T * d, dk), bB=(0, dk), bC=(H * T * npos, T * npos))
-    Pm = _empty(B, H, T, T, dev=dev)
-    Pd = _empty(B, H, T, T, dev=dev) if pa > 0 else Pm
-    K.relpos_softmax_fwd(ac, bd, lengths, Pm, Pd if pa > 0 else None, B, H, T, 1.0 / math.sqrt(dk), pa, seed,
-                         _stream(salt, li, SITE_ATT_P))
-    del ac, bd
     o = _empty(rows, d, dev=dev)
-    # O = Pd V : A = Pd (T x T), B(j,c) = V[b,j,h*dk+c]  -> o[b,i,h*dk+c]
-    K.gemm(Pd, qkv[:, 2 * d:], o, T, dk, T, T, 1, 3 * d, 1, d, 1, amode=_lib.LD_KC, bmode=_lib.LD_XC,
-           batch=(B, H), bA=(H * T * T, T * T), bB=(T * 3 * d, dk), bC=(T * d, dk))
+    if K.get_math() == "bf16" and dk <= 48:
+        # fused flash-style kernel: no AC / BD materialisation; P (and P_drop) only when the
+        # backward needs them
+        Pm = _empty(B, H, T, T, dev=dev) if save else None
+        Pd = (_empty(B, H, T, T, dev=dev) if pa > 0 else Pm) if save else None
+        K.relpos_attn_fwd(qu, qv, qkv, ppos, lengths, o, Pm, Pd if pa > 0 else None, B, H, T,
+                          1.0 / math.sqrt(dk), pa, seed, _stream(salt, li, SITE_ATT_P))
+    else:
+        ac = _empty(B, H, T, T, dev=dev)
+        # AC = (q+u) K^T  per (b,h): A(i,c)=qu[b,i,h*dk+c]  B(c,j)=K[b,j,h*dk+c]
+        K.gemm(qu, qkv[:, d:], ac, T, T, dk, d, 1, 1, 3 * d, T, 1, amode=_lib.LD_KC, bmode=_lib.LD_KC,
+               batch=(B, H), bA=(T * d, dk), bB=(T * 3 * d, dk), bC=(H * T * T, T * T))
+        bd = _empty(B, H, T, npos, dev=dev)
+        K.gemm(qv, ppos, bd, T, npos, dk, d, 1, 1, d, npos, 1, amode=_lib.LD_KC, bmode=_lib.LD_KC,
+               batch=(B, H), bA=(T * d, dk), bB=(0, dk), bC=(H * T * npos, T * npos))
+        Pm = _empty(B, H, T, T, dev=dev)
+        Pd = _empty(B, H, T, T, dev=dev) if pa > 0 else Pm
+        K.relpos_softmax_fwd(ac, bd, lengths, Pm, Pd if pa > 0 else None, B, H, T, 1.0 / math.sqrt(dk), pa, seed,
+                             _stream(salt, li, SITE_ATT_P))
+        del ac, bd
+        # O = Pd V : A = Pd (T x T), B(j,c) = V[b,j,h*dk+c]  -> o[b,i,h*dk+c]
+        K.gemm(Pd, qkv[:, 2 * d:], o, T, dk, T, T, 1, 3 * d, 1, d, 1, amode=_lib.LD_KC, bmode=_lib.LD_XC,
+               batch=(B, H), bA=(H * T * T, T * T), bB=(T * 3 * d, dk), bC=(T * d, dk))
     x2 = _empty(rows, d, dev=dev)
     K.linear(o, P[L + "self_attn.linear_out.weight"], P[L + "self_attn.linear_out.bias"], x2, epi=_lib.EPI_RESID,
              R=x1, rscale=1.0, dropout_p=pd, seed=seed, rng_stream=_stream(salt, li, SITE_ATT_OUT))

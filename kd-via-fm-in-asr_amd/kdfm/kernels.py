@@ -365,6 +365,15 @@ def qkv_prep(qkv, u, v, qu, qv):
     call("kdfm_qkv_prep", ptr(qkv), ptr(u), ptr(v), ptr(qu), ptr(qv), rows, d, _s())
 
 
+def relpos_attn_fwd(qu, qv, qkv, ppos, lengths, o, P, Pd, B, H, T, scale, p, seed, rng_stream):
+    """Fused rel-pos MHA forward (bf16); P / Pd (B,H,T,T) written when given."""
+    rows, d = qu.shape
+    assert rows == B * T and qkv.shape == (rows, 3 * d) and ppos.shape == (2 * T - 1, d) and o.shape == (rows, d)
+    assert qu.is_contiguous() and qv.is_contiguous() and qkv.is_contiguous() and ppos.is_contiguous()
+    call("kdfm_relpos_attn_fwd", ptr(qu), ptr(qv), ptr(qkv), ptr(ppos), ptr(_i64(lengths)), ptr(o), ptr(P), ptr(Pd),
+         B, H, T, d, float(scale), float(p), ptr(seed), rng_stream, _s())
+
+
 def relpos_softmax_fwd(ac, bd, lengths, P, Pd, B, H, T, scale, p, seed, rng_stream):
     assert ac.numel() == B * H * T * T and bd.numel() == B * H * T * (2 * T - 1)
     call("kdfm_relpos_softmax_fwd", ptr(ac), ptr(bd), ptr(_i64(lengths)), ptr(P), ptr(Pd), B, H, T, float(scale),
