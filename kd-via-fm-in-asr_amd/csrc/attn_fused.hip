@@ -72,6 +72,7 @@ __device__ __forceinline__ float group16_sum(float v) {
   return v;
 }
 
+template <bool TWO_PASS>
 __global__ __launch_bounds__(256, 2) void relpos_attn_fwd_kernel(AttnP p) {
   __shared__ __attribute__((aligned(16))) uint16_t Ks[AKB * LDR];
   __shared__ __attribute__((aligned(16))) uint16_t Vt[DKP * LDVT];
@@ -118,32 +119,56 @@ __global__ __launch_bounds__(256, 2) void relpos_attn_fwd_kernel(AttnP p) {
 #pragma unroll
   for (int r = 0; r < 4; ++r) { mrow[r] = -3.0e38f; lrow[r] = 0.f; }
 
-  auto stage_kp = [&](int j0, bool with_v) {
-    // K block [key][c]
-    const int cq = dk >> 2;
-    for (int e = threadIdx.x; e < AKB * cq; e += 256) {
+  // ---- staging of one key block: all global loads of a stage are issued before any LDS store
+  // (register staging; the next block's loads are in flight while this block computes) ----
+  constexpr int KU = (AKB * (DKP / 4 * 3 / 4) + 255) / 256;  // K / V float4 per thread (dk <= 48)
+  constexpr int PU = (BAND * (DKP / 4 * 3 / 4) + 255) / 256; // P-band float4 per thread
+  const int cq = dk >> 2;
+  float4 rk[KU], rv[KU], rp[PU];
+  auto load_stage = [&](int j0, bool with_v) {
+#pragma unroll
+    for (int i = 0; i < KU; ++i) {
+      const int e = threadIdx.x + i * 256;
       const int jj = e / cq, c4 = (e - jj * cq) * 4;
       const int j = j0 + jj;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (j < T) v = *reinterpret_cast<const float4*>(p.k + (b * p.T + j) * p.ldkv + hoff + c4);
-      store4_bf16(Ks + jj * LDR + c4, v);
-      if (with_v) {
-        float4 u = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (j < T) u = *reinterpret_cast<const float4*>(p.v + (b * p.T + j) * p.ldkv + hoff + c4);
-        Vt[(c4 + 0) * LDVT + jj] = f2bf(u.x);
-        Vt[(c4 + 1) * LDVT + jj] = f2bf(u.y);
-        Vt[(c4 + 2) * LDVT + jj] = f2bf(u.z);
-        Vt[(c4 + 3) * LDVT + jj] = f2bf(u.w);
-      }
+      const bool ok = e < AKB * cq && j < T;
+      const int64_t off = (b * p.T + j) * p.ldkv + hoff + c4;
+      rk[i] = ok ? *reinterpret_cast<const float4*>(p.k + off) : make_float4(0.f, 0.f, 0.f, 0.f);
+      rv[i] = (ok && with_v) ? *reinterpret_cast<const float4*>(p.v + off) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    // P band: rows r = rbase + rr, rbase = T-1-(i0+63)+j0
-    const int rbase = T - 1 - (i0 + AQ - 1) + j0;
-    for (int e = threadIdx.x; e < BAND * cq; e += 256) {
+    const int rbase = T - 1 - (i0 + AQ - 1) + j0;  // P band rows r = rbase + rr
+#pragma unroll
+    for (int i = 0; i < PU; ++i) {
+      const int e = threadIdx.x + i * 256;
       const int rr = e / cq, c4 = (e - rr * cq) * 4;
       const int r = rbase + rr;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (r >= 0 && r < npos) v = *reinterpret_cast<const float4*>(p.pos + (int64_t)r * p.d + hoff + c4);
-      store4_bf16(Pr + rr * LDR + c4, v);
+      const bool ok = e < BAND * cq && r >= 0 && r < npos;
+      rp[i] = ok ? *reinterpret_cast<const float4*>(p.pos + (int64_t)r * p.d + hoff + c4)
+                 : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  auto store_stage = [&](bool with_v) {
+#pragma unroll
+    for (int i = 0; i < KU; ++i) {
+      const int e = threadIdx.x + i * 256;
+      if (e < AKB * cq) {
+        const int jj = e / cq, c4 = (e - jj * cq) * 4;
+        store4_bf16(Ks + jj * LDR + c4, rk[i]);
+        if (with_v) {
+          Vt[(c4 + 0) * LDVT + jj] = f2bf(rv[i].x);
+          Vt[(c4 + 1) * LDVT + jj] = f2bf(rv[i].y);
+          Vt[(c4 + 2) * LDVT + jj] = f2bf(rv[i].z);
+          Vt[(c4 + 3) * LDVT + jj] = f2bf(rv[i].w);
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < PU; ++i) {
+      const int e = threadIdx.x + i * 256;
+      if (e < BAND * cq) {
+        const int rr = e / cq, c4 = (e - rr * cq) * 4;
+        store4_bf16(Pr + rr * LDR + c4, rp[i]);
+      }
     }
   };
 
@@ -187,12 +212,16 @@ __global__ __launch_bounds__(256, 2) void relpos_attn_fwd_kernel(AttnP p) {
     wave_lds_sync();  // G is rewritten by the next call
   };
 
-  // ---- pass 1: row max / sum ----
-  for (int kb = 0; kb < nkb; ++kb) {
+  // ---- pass 1 (two-pass mode): row max / sum ----
+  if (TWO_PASS && nkb > 0) load_stage(0, false);
+  if (!TWO_PASS && nkb > 0) load_stage(0, true);
+  for (int kb = 0; kb < (TWO_PASS ? nkb : 0); ++kb) {
     const int j0 = kb * AKB;
     __syncthreads();
-    stage_kp(j0, false);
+    store_stage(false);
     __syncthreads();
+    if (kb + 1 < nkb) load_stage(j0 + AKB, false);
+    else if (nkb > 0) load_stage(0, true);  // first block of pass 2
     float s[4][4];
     scores(j0, s);
 #pragma unroll
@@ -210,7 +239,7 @@ __global__ __launch_bounds__(256, 2) void relpos_attn_fwd_kernel(AttnP p) {
   }
   float inv[4];
 #pragma unroll
-  for (int r = 0; r < 4; ++r) inv[r] = (ib + r < len && lrow[r] > 0.f) ? 1.f / lrow[r] : 0.f;
+  for (int r = 0; r < 4; ++r) inv[r] = TWO_PASS ? ((ib + r < len && lrow[r] > 0.f) ? 1.f / lrow[r] : 0.f) : 1.f;
 
   // ---- pass 2: probabilities, dropout, O += Pd V ----
   const uint64_t seed = (p.p_drop > 0.f) ? load_seed(p.seed) : 0ull;
@@ -224,8 +253,9 @@ __global__ __launch_bounds__(256, 2) void relpos_attn_fwd_kernel(AttnP p) {
     const bool live = kb < nkb;
     if (live) {
       __syncthreads();
-      stage_kp(j0, true);
+      store_stage(true);
       __syncthreads();
+      if (kb + 1 < nkb) load_stage(j0 + AKB, true);
     }
     float s[4][4];
     if (live) {
@@ -235,6 +265,22 @@ __global__ __launch_bounds__(256, 2) void relpos_attn_fwd_kernel(AttnP p) {
       for (int t = 0; t < 4; ++t)
 #pragma unroll
         for (int r = 0; r < 4; ++r) s[t][r] = -3.0e38f;
+    }
+    if (!TWO_PASS && live) {  // online softmax: rescale the running sum and O to the new row max
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float mx = fmaxf(fmaxf(s[0][r], s[1][r]), fmaxf(s[2][r], s[3][r]));
+        mx = group16_max(mx);
+        const float mn = fmaxf(mrow[r], mx);
+        const float corr = (mrow[r] > -1.0e38f) ? __expf(mrow[r] - mn) : 0.f;
+        float sum = 0.f;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) sum += (s[t][r] > -1.0e38f) ? __expf(s[t][r] - mn) : 0.f;
+        lrow[r] = lrow[r] * corr + group16_sum(sum);
+        mrow[r] = mn;
+#pragma unroll
+        for (int u = 0; u < 3; ++u) oacc[u][r] *= corr;
+      }
     }
     uint16_t* Pw = Ps[w];
 #pragma unroll
@@ -249,14 +295,17 @@ __global__ __launch_bounds__(256, 2) void relpos_attn_fwd_kernel(AttnP p) {
           const uint64_t idx = (uint64_t)(prow0 + (int64_t)r * p.T) + (uint64_t)j;
           pdv = dropout_keep(seed, p.rng_stream, idx, p.p_drop) ? pv * keep_scale : 0.f;
         }
-        if (i < T && j < T) {
+        if (TWO_PASS && i < T && j < T) {
           const int64_t off = prow0 + (int64_t)r * p.T + j;
           if (p.P) p.P[off] = pv;
           if (p.Pd) p.Pd[off] = pdv;
         }
         Pw[ii * LDPS + jj] = f2bf(pdv);
       }
-    if (!live) continue;  // P row tail beyond len is written as zeros; no O contribution
+    if (!live) {
+      if (!TWO_PASS) break;  // nothing to write: no P outputs in single-pass mode
+      continue;              // P row tail beyond len is written as zeros; no O contribution
+    }
     wave_lds_sync();
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
@@ -271,12 +320,15 @@ __global__ __launch_bounds__(256, 2) void relpos_attn_fwd_kernel(AttnP p) {
   }
 
   // ---- O -> (rows, d) ----
+  float fin[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) fin[r] = TWO_PASS ? 1.f : ((ib + r < len && lrow[r] > 0.f) ? 1.f / lrow[r] : 0.f);
 #pragma unroll
   for (int u = 0; u < 3; ++u)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int i = ib + r, c = 16 * u + (lane & 15);
-      if (i < T && c < dk) p.o[(b * p.T + i) * p.ldq + hoff + c] = oacc[u][r];
+      if (i < T && c < dk) p.o[(b * p.T + i) * p.ldq + hoff + c] = oacc[u][r] * fin[r];
     }
 }
 
@@ -302,6 +354,9 @@ extern "C" int kdfm_relpos_attn_fwd(const float* qu, const float* qv, const floa
   p.B = B; p.H = H; p.T = T; p.d = d; p.dk = dk; p.ldq = d; p.ldkv = 3 * d;
   p.scale = scale; p.p_drop = dropout_p; p.seed = seed; p.rng_stream = rng_stream;
   dim3 grid((unsigned)ceil_div(T, AQ), (unsigned)(B * H));
-  hipLaunchKernelGGL(relpos_attn_fwd_kernel, grid, dim3(256), 0, as_stream(stream), p);
+  if (P || Pdrop)
+    hipLaunchKernelGGL(relpos_attn_fwd_kernel<true>, grid, dim3(256), 0, as_stream(stream), p);
+  else
+    hipLaunchKernelGGL(relpos_attn_fwd_kernel<false>, grid, dim3(256), 0, as_stream(stream), p);
   return check_launch("kdfm_relpos_attn_fwd");
 }

@@ -87,7 +87,8 @@ def test_fused_attention_matches(B, H, T, d, p):
 
 
 def test_fused_attention_no_P(K=None):
-    """teacher mode: no P / P_drop outputs, same O"""
+    """teacher mode (no P / P_drop outputs): single-pass online softmax, same O as the two-pass
+    mode up to bf16 rounding of the unnormalised probabilities (1e-2 of max |O|)"""
     from kdfm import kernels as K
     g = torch.Generator(device="cuda").manual_seed(3)
     B, H, T, d = 2, 4, 401, 176
@@ -103,4 +104,5 @@ def test_fused_attention_no_P(K=None):
     K.relpos_attn_fwd(qu, qv, qkv, ppos, lens, o1, None, None, B, H, T, 0.15, 0.0, None, 0)
     K.relpos_attn_fwd(qu, qv, qkv, ppos, lens, o2, P, None, B, H, T, 0.15, 0.0, None, 0)
     torch.cuda.synchronize()
-    assert torch.equal(o1, o2)
+    assert (o1 - o2).abs().max().item() <= 1e-2 * o2.abs().max().item()
+    assert o1.view(B, T, d)[1, 300:].abs().max().item() == 0
