@@ -47,46 +47,97 @@ __global__ __launch_bounds__(256) void glu_mask_bwd_kernel(const float* __restri
   da[r * 2 * d + d + c] = dyv;
 }
 
+// Frame x channel tile staging shared by the depthwise-conv kernels: rows [t0 - pad, t0 + rows - pad)
+// of one utterance, CT channels from c0, as float4 chunks (d % 4 == 0).  Every load of the tile is
+// issued before the first LDS store, so the tile costs one memory round trip, not one per chunk.
+constexpr int TQ = 8;  // float4 chunks per thread (rows <= TT + KMAX - 1 = 126)
+
+__device__ __forceinline__ void tile_load(float4 (&v)[TQ], const float* __restrict__ src, int64_t b, int64_t t0,
+                                          int pad, int rows, int64_t T, int64_t d, int64_t c0) {
+#pragma unroll
+  for (int i = 0; i < TQ; ++i) {
+    const int q = threadIdx.x + i * 256;
+    const int rr = q >> 4, c4 = (q & 15) * 4;
+    const int64_t t = t0 + rr - pad, c = c0 + c4;
+    const bool ok = rr < rows && t >= 0 && t < T && c < d;
+    v[i] = ok ? *reinterpret_cast<const float4*>(src + (b * T + t) * d + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
+__device__ __forceinline__ void tile_store(const float4 (&v)[TQ], float* tile, int rows) {
+#pragma unroll
+  for (int i = 0; i < TQ; ++i) {
+    const int q = threadIdx.x + i * 256;
+    const int rr = q >> 4, c4 = (q & 15) * 4;
+    if (rr < rows) *reinterpret_cast<float4*>(tile + rr * CT + c4) = v[i];
+  }
+}
+
 // y[b,t,c] = bias[c] + sum_k w[c,k] * g[b,t+k-pad,c]; stats[c] += (sum y, sum y^2)
+// Lane = channel, wave = 16-frame group; with KC > 0 a 16-frame register window slides over the
+// tile (one LDS read per 16 FMAs) with the taps in registers.
+template <int KC>
 __global__ __launch_bounds__(256) void dwconv_fwd_kernel(const float* __restrict__ g, const float* __restrict__ w,
                                                          const float* __restrict__ bias, float* __restrict__ y,
-                                                         double* __restrict__ stats, int64_t T, int64_t d, int K) {
-  __shared__ float tile[(TT + KMAX - 1) * CT];
-  __shared__ float wt[CT * KMAX];
+                                                         double* __restrict__ stats, int64_t T, int64_t d, int Krt) {
+  constexpr int KM = KC > 0 ? KC : KMAX;
+  __shared__ __attribute__((aligned(16))) float tile[(TT + KM - 1) * CT];
   __shared__ double red[2][4][CT];
+  const int K = KC > 0 ? KC : Krt;
   const int pad = (K - 1) / 2;
   const int64_t b = blockIdx.z;
   const int64_t t0 = (int64_t)blockIdx.x * TT;
   const int64_t c0 = (int64_t)blockIdx.y * CT;
-  const int rowsIn = TT + K - 1;
-  for (int e = threadIdx.x; e < rowsIn * CT; e += 256) {
-    const int rr = e / CT, cc = e % CT;
-    const int64_t t = t0 + rr - pad, c = c0 + cc;
-    tile[e] = (t >= 0 && t < T && c < d) ? g[(b * T + t) * d + c] : 0.f;
+  {
+    float4 v[TQ];
+    tile_load(v, g, b, t0, pad, TT + K - 1, T, d, c0);
+    tile_store(v, tile, TT + K - 1);
   }
-  for (int e = threadIdx.x; e < CT * K; e += 256) {
-    const int cc = e / K, k = e % K;
-    wt[cc * KMAX + k] = (c0 + cc < d) ? w[(c0 + cc) * K + k] : 0.f;
-  }
-  __syncthreads();
   const int cc = threadIdx.x & 63;
-  const int tq = threadIdx.x >> 6;  // 4 frame groups of 16
+  const int f0 = (threadIdx.x >> 6) * 16;
   const int64_t c = c0 + cc;
-  double s1 = 0.0, s2 = 0.0;
-  if (c < d) {
-    const float bc = bias ? bias[c] : 0.f;
-    for (int tt = tq; tt < TT; tt += 4) {
-      const int64_t t = t0 + tt;
-      if (t >= T) break;
-      float acc = bc;
-      for (int k = 0; k < K; ++k) acc += wt[cc * KMAX + k] * tile[(tt + k) * CT + cc];
-      y[(b * T + t) * d + c] = acc;
-      s1 += acc;
-      s2 += (double)acc * acc;
+  const bool cok = c < d;
+  const float bc = (bias && cok) ? bias[c] : 0.f;
+  __syncthreads();
+  float acc[16];
+#pragma unroll
+  for (int tt = 0; tt < 16; ++tt) acc[tt] = bc;
+  if constexpr (KC > 0) {
+    float win[16];
+#pragma unroll
+    for (int tt = 0; tt < 16; ++tt) win[tt] = tile[(f0 + tt) * CT + cc];
+#pragma unroll
+    for (int k = 0; k < KC; ++k) {
+      const float wk = cok ? w[c * KC + k] : 0.f;
+#pragma unroll
+      for (int tt = 0; tt < 16; ++tt) acc[tt] += wk * win[tt];
+      if (k + 1 < KC) {
+#pragma unroll
+        for (int tt = 0; tt < 15; ++tt) win[tt] = win[tt + 1];
+        win[15] = tile[(f0 + k + 16) * CT + cc];
+      }
+    }
+  } else {
+    for (int k = 0; k < K; ++k) {
+      const float wk = cok ? w[c * K + k] : 0.f;
+#pragma unroll
+      for (int tt = 0; tt < 16; ++tt) acc[tt] += wk * tile[(f0 + tt + k) * CT + cc];
     }
   }
-  red[0][tq][cc] = s1;
-  red[1][tq][cc] = s2;
+  double s1 = 0.0, s2 = 0.0;
+  if (cok) {
+#pragma unroll
+    for (int tt = 0; tt < 16; ++tt) {
+      const int64_t t = t0 + f0 + tt;
+      if (t < T) {
+        y[(b * T + t) * d + c] = acc[tt];
+        s1 += acc[tt];
+        s2 += (double)acc[tt] * acc[tt];
+      }
+    }
+  }
+  red[0][threadIdx.x >> 6][cc] = s1;
+  red[1][threadIdx.x >> 6][cc] = s2;
   __syncthreads();
   if (stats && threadIdx.x < CT && c0 + threadIdx.x < d) {
     const int q = threadIdx.x;
@@ -212,8 +263,8 @@ __global__ __launch_bounds__(256) void dwconv_bwd_kernel(const float* __restrict
                                                          const float* __restrict__ w, float* __restrict__ dg,
                                                          float* __restrict__ part, int64_t T, int64_t d, int Krt) {
   constexpr int KM = KC > 0 ? KC : KMAX;
-  __shared__ float tdy[(TT + KM - 1) * CT];  // frames t0-pad .. t0+TT-1+pad
-  __shared__ float tg[(TT + KM - 1) * CT];
+  __shared__ __attribute__((aligned(16))) float tdy[(TT + KM - 1) * CT];  // frames t0-pad .. t0+TT-1+pad
+  __shared__ __attribute__((aligned(16))) float tg[(TT + KM - 1) * CT];
   __shared__ float red[(KM + 1) * CT];
   const int K = KC > 0 ? KC : Krt;
   const int pad = (K - 1) / 2;
@@ -221,13 +272,12 @@ __global__ __launch_bounds__(256) void dwconv_bwd_kernel(const float* __restrict
   const int64_t t0 = (int64_t)blockIdx.x * TT;
   const int64_t c0 = (int64_t)blockIdx.y * CT;
   const int rowsIn = TT + K - 1;
-  for (int e = threadIdx.x; e < rowsIn * CT; e += 256) {
-    const int rr = e / CT, cc = e % CT;
-    const int64_t c = c0 + cc;
-    const int64_t t = t0 + rr - pad;
-    const bool ok = t >= 0 && t < T && c < d;
-    tdy[e] = ok ? dy[(b * T + t) * d + c] : 0.f;
-    tg[e] = ok ? g[(b * T + t) * d + c] : 0.f;
+  {
+    float4 v1[TQ], v2[TQ];
+    tile_load(v1, dy, b, t0, pad, rowsIn, T, d, c0);
+    tile_load(v2, g, b, t0, pad, rowsIn, T, d, c0);
+    tile_store(v1, tdy, rowsIn);
+    tile_store(v2, tg, rowsIn);
   }
   for (int e = threadIdx.x; e < (K + 1) * CT; e += 256) red[e] = 0.f;
   __syncthreads();
@@ -346,9 +396,15 @@ int kdfm_dwconv_fwd(const float* g, const float* w, const float* bias, float* y,
   using namespace kdfm;
   KDFM_REQUIRE(g && w && y, "null pointer");
   KDFM_REQUIRE(K >= 1 && K <= KMAX && (K % 2) == 1, "kernel size must be odd and <= 63");
+  KDFM_REQUIRE(d % 4 == 0 && (((uintptr_t)g) & 15) == 0, "channels must be a multiple of 4, input 16-B aligned");
   if (B * T * d == 0) return KDFM_OK;
   dim3 grid((unsigned)ceil_div(T, TT), (unsigned)ceil_div(d, CT), (unsigned)B);
-  hipLaunchKernelGGL(dwconv_fwd_kernel, grid, dim3(256), 0, as_stream(stream), g, w, bias, y, stats, T, d, (int)K);
+  if (K == 31)
+    hipLaunchKernelGGL(dwconv_fwd_kernel<31>, grid, dim3(256), 0, as_stream(stream), g, w, bias, y, stats, T, d, (int)K);
+  else if (K == 15)
+    hipLaunchKernelGGL(dwconv_fwd_kernel<15>, grid, dim3(256), 0, as_stream(stream), g, w, bias, y, stats, T, d, (int)K);
+  else
+    hipLaunchKernelGGL(dwconv_fwd_kernel<0>, grid, dim3(256), 0, as_stream(stream), g, w, bias, y, stats, T, d, (int)K);
   return check_launch("kdfm_dwconv_fwd");
 }
 
@@ -361,6 +417,8 @@ int kdfm_dwconv_bwd(const float* dy, const float* g, const float* w, float* dg, 
   using namespace kdfm;
   KDFM_REQUIRE(dy && g && w && dg && dw && db && ws, "null pointer");
   KDFM_REQUIRE(K >= 1 && K <= KMAX && (K % 2) == 1, "kernel size must be odd and <= 63");
+  KDFM_REQUIRE(d % 4 == 0 && ((((uintptr_t)g) | ((uintptr_t)dy)) & 15) == 0,
+               "channels must be a multiple of 4, inputs 16-B aligned");
   if (B * T * d == 0) return KDFM_OK;
   static_assert(TT == 64, "dwconv_bwd assumes 4 waves x 16 frames per tile");
   hipStream_t st = as_stream(stream);

@@ -493,7 +493,11 @@ bool wg_pick(int64_t M, int64_t N, WgCfg& c) {
 bool wg_eligible(const GemmP& p, int amode, int bmode, int64_t batch) {
   if (batch != 1 || p.epi != KDFM_EPI_ATOMIC || amode != KDFM_LD_XC) return false;
   if (p.sAm != 1 || (p.sAk & 1) || (p.M & 1) || (((uintptr_t)p.A) & 7)) return false;
-  if (p.K < 4096) return false;
+  static const int64_t min_k = [] {
+    const char* e = getenv("KDFM_RS_WGRAD_MINK");
+    return e ? atoll(e) : 65536ll;
+  }();
+  if (p.K < min_k) return false;
   if (bmode == KDFM_LD_XC) {
     if (p.sBn != 1 || (p.sBk & 1) || (((uintptr_t)p.B) & 7)) return false;
   } else if (bmode == KDFM_LD_CONV) {
@@ -514,9 +518,17 @@ void wg_plan(const GemmP& p, int64_t& tiles, int64_t& tilesN, int64_t& S, int64_
   tilesN = ceil_div(p.N, 32 * c.nt);
   tiles = tilesM * tilesN;
   const int64_t steps = ceil_div(p.K, 32);
-  S = 256 / tiles;
+  static const int64_t target = [] {
+    const char* e = getenv("KDFM_RS_WGRAD_WGS");
+    return e ? atoll(e) : 256ll;
+  }();
+  S = target / tiles;
   if (S < 1) S = 1;
-  const int64_t smax = steps / 4 > 0 ? steps / 4 : 1;
+  static const int64_t min_steps = [] {
+    const char* e = getenv("KDFM_RS_WGRAD_STEPS");
+    return e ? atoll(e) : 4ll;
+  }();
+  const int64_t smax = steps / min_steps > 0 ? steps / min_steps : 1;
   if (S > smax) S = smax;
   kchunk = ceil_div(steps, S) * 32;
   S = ceil_div(p.K, kchunk);

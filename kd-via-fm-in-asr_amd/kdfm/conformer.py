@@ -18,6 +18,7 @@ import torch
 
 from . import _lib
 from . import kernels as K
+from .overlap import WGRAD
 from .config import Ver5Config
 
 # dropout site ids (rng stream = model_salt * 4096 + layer * 16 + site)
@@ -96,14 +97,14 @@ def subsampling_backward(cfg, S: EncoderShapes, P, G, pre, ctx, dx, len1, *, see
     dy2 = _empty(B * S.T * S.F2, C, dev=dev)
     K.linear_dx(dlin, ws["wout_perm"].view(d, S.F2 * C), dy2.view(S.rows, S.F2 * C), epi=_lib.EPI_DRELU,
                 aux=y2.view(S.rows, S.F2 * C))
-    K.linear_dw(dy2, ctx["cols1"], G[pre + "pre_encode.conv.2.weight"].view(C, 9 * C), db=G[pre + "pre_encode.conv.2.bias"])
+    WGRAD.run(lambda: K.linear_dw(dy2, ctx["cols1"], G[pre + "pre_encode.conv.2.weight"].view(C, 9 * C), db=G[pre + "pre_encode.conv.2.bias"]), dy2, ctx["cols1"])
     dcols1 = _empty(B * S.T * S.F2, 9 * C, dev=dev)
     K.linear_dx(dy2, P[pre + "pre_encode.conv.2.weight"].view(C, 9 * C), dcols1)
     del dy2
     dy1 = _empty(B * S.T1 * S.F1, C, dev=dev)
     K.col2im_3x3s2(dcols1, len1 if cfg.subsampling_mask else None, ctx["y1"], dy1, B, S.T1, S.F1, C)
     del dcols1
-    K.linear_dw(dy1, ctx["cols0"], G[pre + "pre_encode.conv.0.weight"].view(C, 9), math="f32", db=G[pre + "pre_encode.conv.0.bias"])
+    WGRAD.run(lambda: K.linear_dw(dy1, ctx["cols0"], G[pre + "pre_encode.conv.0.weight"].view(C, 9), math="f32", db=G[pre + "pre_encode.conv.0.bias"]), dy1, ctx["cols0"])
     
 
 # ------------------------------------------------------------------------------------------------
@@ -234,12 +235,12 @@ def _ffn_backward(P, G, L, which, dres_out, ln, h, a, x_in_ln, m, r, norm, pd, s
     ff = h.shape[1]
     dlin2 = _empty(rows, d, dev=dev)
     K.dropout(dres_out, dlin2, pd, 0.5, seed, _stream(salt, li, site_out))
-    K.linear_dw(dlin2, a, G[L + which + ".linear2.weight"], db=G[L + which + ".linear2.bias"])
+    WGRAD.run(lambda: K.linear_dw(dlin2, a, G[L + which + ".linear2.weight"], db=G[L + which + ".linear2.bias"]), dlin2, a)
     dh = _empty(rows, ff, dev=dev)
     K.linear_dx(dlin2, P[L + which + ".linear2.weight"], dh, epi=_lib.EPI_DSILU, aux=h, dropout_p=pd, seed=seed,
                 rng_stream=_stream(salt, li, site_act))
     del dlin2
-    K.linear_dw(dh, ln, G[L + which + ".linear1.weight"], db=G[L + which + ".linear1.bias"])
+    WGRAD.run(lambda: K.linear_dw(dh, ln, G[L + which + ".linear1.weight"], db=G[L + which + ".linear1.bias"]), dh, ln)
     dln = _empty(rows, d, dev=dev)
     K.linear_dx(dh, P[L + which + ".linear1.weight"], dln)
     del dh
@@ -265,7 +266,7 @@ def layer_backward(cfg, S: EncoderShapes, P, G, L, li, ctx, dout, pos_emb, lengt
     # conv module: x3 = x2 + drop(pw2(z))
     dpw2 = _empty(rows, d, dev=dev)
     K.dropout(dx3, dpw2, pd, 1.0, seed, _stream(salt, li, SITE_CONV_OUT))
-    K.linear_dw(dpw2, ctx["z"], G[L + "conv.pointwise_conv2.weight"].view(d, d), db=G[L + "conv.pointwise_conv2.bias"])
+    WGRAD.run(lambda: K.linear_dw(dpw2, ctx["z"], G[L + "conv.pointwise_conv2.weight"].view(d, d), db=G[L + "conv.pointwise_conv2.bias"]), dpw2, ctx["z"])
     dz = _empty(rows, d, dev=dev)
     K.linear_dx(dpw2, P[L + "conv.pointwise_conv2.weight"].view(d, d), dz)
     del dpw2
@@ -283,7 +284,7 @@ def layer_backward(cfg, S: EncoderShapes, P, G, L, li, ctx, dout, pos_emb, lengt
     da = _empty(rows, 2 * d, dev=dev)
     K.glu_mask_bwd(dg, ctx["a"], lengths, da, B, T, d)
     del dg
-    K.linear_dw(da, ctx["ln3"], G[L + "conv.pointwise_conv1.weight"].view(2 * d, d), db=G[L + "conv.pointwise_conv1.bias"])
+    WGRAD.run(lambda: K.linear_dw(da, ctx["ln3"], G[L + "conv.pointwise_conv1.weight"].view(2 * d, d), db=G[L + "conv.pointwise_conv1.bias"]), da, ctx["ln3"])
     dln3 = _empty(rows, d, dev=dev)
     K.linear_dx(da, P[L + "conv.pointwise_conv1.weight"].view(2 * d, d), dln3)
     del da
@@ -294,7 +295,7 @@ def layer_backward(cfg, S: EncoderShapes, P, G, L, li, ctx, dout, pos_emb, lengt
     # MHSA: x2 = x1 + drop(out(O))
     dlo = _empty(rows, d, dev=dev)
     K.dropout(dx2, dlo, pd, 1.0, seed, _stream(salt, li, SITE_ATT_OUT))
-    K.linear_dw(dlo, ctx["o"], G[L + "self_attn.linear_out.weight"], db=G[L + "self_attn.linear_out.bias"])
+    WGRAD.run(lambda: K.linear_dw(dlo, ctx["o"], G[L + "self_attn.linear_out.weight"], db=G[L + "self_attn.linear_out.bias"]), dlo, ctx["o"])
     do = _empty(rows, d, dev=dev)
     K.linear_dx(dlo, P[L + "self_attn.linear_out.weight"], do)
     del dlo
@@ -335,9 +336,9 @@ def layer_backward(cfg, S: EncoderShapes, P, G, L, li, ctx, dout, pos_emb, lengt
     K.colsum(dqv, G[L + "self_attn.pos_bias_v"].view(-1))
     K.axpby(dqu, dqv, dqkv[:, :d], 1.0, 1.0)
     del dqu, dqv
-    K.linear_dw(dppos, pos_emb, G[L + "self_attn.linear_pos.weight"])
+    WGRAD.run(lambda: K.linear_dw(dppos, pos_emb, G[L + "self_attn.linear_pos.weight"]), dppos, pos_emb)
     del dppos
-    K.linear_dw(dqkv, ctx["ln2"], G[L + "self_attn.qkv.weight"], db=G[L + "self_attn.qkv.bias"])
+    WGRAD.run(lambda: K.linear_dw(dqkv, ctx["ln2"], G[L + "self_attn.qkv.weight"], db=G[L + "self_attn.qkv.bias"]), dqkv, ctx["ln2"])
     dln2 = _empty(rows, d, dev=dev)
     K.linear_dx(dqkv, P[L + "self_attn.qkv.weight"], dln2)
     del dqkv
@@ -398,6 +399,7 @@ def encoder_backward(cfg, S: EncoderShapes, P, G, prefix, run: EncoderRun, dfeat
             dout = dfeats[i - 1]
     subsampling_backward(cfg, S, P, G, prefix, run.sub, dx, len1, seed=seed, salt=salt, ws=ws)
     run.sub = None
+    WGRAD.join()  # weight gradients computed on the side stream are complete before anyone reads G
 
 
 def make_workspace(S: EncoderShapes, dev):

@@ -21,6 +21,7 @@ import torch
 
 from . import _lib
 from . import kernels as K
+from .overlap import WGRAD
 from .config import Ver5Config
 
 SALT_HEADS = 7
@@ -139,7 +140,7 @@ def heads_backward(cfg: Ver5Config, P, G, ctx, ws: HeadsWorkspace, ds_feats, *, 
     W2 = P[fm + "meta_encoder.2.weight"]
     # ---- FM loss: tr = Wst nsx + b ; d_tr given ----
     dtr = ctx["dtr"]
-    K.linear_dw(dtr, ctx["nsx"], G[fm + "shape_transformation_function.weight"], db=G[fm + "shape_transformation_function.bias"])
+    WGRAD.run(lambda: K.linear_dw(dtr, ctx["nsx"], G[fm + "shape_transformation_function.weight"], db=G[fm + "shape_transformation_function.bias"]), dtr, ctx["nsx"])
     dnsx = _empty(n, Lt, dev=dev)
     K.linear_dx(dtr, P[fm + "shape_transformation_function.weight"], dnsx)
     # nsx = zd - v  ->  d zd += dnsx ; dv = -dnsx
@@ -151,10 +152,10 @@ def heads_backward(cfg: Ver5Config, P, G, ctx, ws: HeadsWorkspace, ds_feats, *, 
             gsrc, alpha = dnsx, -1.0          # dv_{S-1} = -dnsx
         else:
             gsrc, alpha = gx_next, -1.0 / S_  # dv_j = -(1/S) g_{x_{j+1}}
-        K.linear_dw(gsrc, fa[j], G[fm + "meta_encoder.2.weight"], alpha=alpha, db=G[fm + "meta_encoder.2.bias"])
+        WGRAD.run(lambda: K.linear_dw(gsrc, fa[j], G[fm + "meta_encoder.2.weight"], alpha=alpha, db=G[fm + "meta_encoder.2.bias"]), gsrc, fa[j])
         da = _empty(n, Lt, dev=dev)
         K.linear_dx(gsrc, W2, da, epi=_lib.EPI_DRELU, aux=fa[j], alpha=alpha)
-        K.linear_dw(da, fx[j], dW1x, db=ws.dc[j])
+        WGRAD.run(lambda: K.linear_dw(da, fx[j], dW1x, db=ws.dc[j]), da, fx[j])
         gx = _empty(n, Lt, dev=dev)
         if gx_next is None:
             K.linear_dx(da, W1x, gx)
@@ -162,6 +163,7 @@ def heads_backward(cfg: Ver5Config, P, G, ctx, ws: HeadsWorkspace, ds_feats, *, 
             K.linear_dx(da, W1x, gx, R=gx_next, rscale=1.0)
         gx_next = gx
         del da
+    WGRAD.join()  # ws.dc (per-step bias grads) is produced on the side stream
     K.fm_time_bwd(ws.dc, ws.evec, W1, dW1, G[fm + "meta_encoder.0.bias"], G[fm + "time_embed.weight"].view(-1),
                   G[fm + "time_embed.bias"], Lt, E, S_)
     # d zd = gx_0 + dnsx
@@ -175,14 +177,15 @@ def heads_backward(cfg: Ver5Config, P, G, ctx, ws: HeadsWorkspace, ds_feats, *, 
     K.fill(ws.g2, 0.0)
     for i in range(ds - 1, -1, -1):
         # x_{i+1} = x_i - (1/ds)(conv(a_i, W2) + b2)
-        K.conv3_dw(g, acts[i], ws.g2, T, alpha=-1.0 / ds, db=G["denoiser.net.2.bias"])
+        WGRAD.run(lambda: K.conv3_dw(g, acts[i], ws.g2, T, alpha=-1.0 / ds, db=G["denoiser.net.2.bias"]), g, acts[i])
         da = _empty(n, Lt, dev=dev)
         K.conv3(g, ws.w2b, None, da, T, epi=_lib.EPI_DRELU, aux=acts[i], alpha=-1.0 / ds)
-        K.conv3_dw(da, xs[i], ws.g1, T, db=G["denoiser.net.0.bias"])
+        WGRAD.run(lambda: K.conv3_dw(da, xs[i], ws.g1, T, db=G["denoiser.net.0.bias"]), da, xs[i])
         gi = _empty(n, Lt, dev=dev)
         K.conv3(da, ws.w1b, None, gi, T, R=g, rscale=1.0)
         g = gi
         del da
+    WGRAD.join()  # ws.g1 / ws.g2 are produced on the side stream
     K.convw_grad(ws.g1, G["denoiser.net.0.weight"])
     K.convw_grad(ws.g2, G["denoiser.net.2.weight"])
     # ---- NoiseAdapter backward ----
@@ -192,18 +195,18 @@ def heads_backward(cfg: Ver5Config, P, G, ctx, ws: HeadsWorkspace, ds_feats, *, 
     K.adapter_bwd(g, zs, hA, ctx["gamma"], P["adapter.gamma_head.2.weight"].view(-1), ctx["eps"], dzs_direct, dh,
                   G["adapter.gamma_head.2.weight"].view(-1), G["adapter.gamma_head.2.bias"], seed, SALT_HEADS)
     del g
-    K.linear_dw(dh, zs, G["adapter.gamma_head.0.weight"].view(Lt, Lt), db=G["adapter.gamma_head.0.bias"])
+    WGRAD.run(lambda: K.linear_dw(dh, zs, G["adapter.gamma_head.0.weight"].view(Lt, Lt), db=G["adapter.gamma_head.0.bias"]), dh, zs)
     dzs = _empty(n, Lt, dev=dev)
     K.linear_dx(dh, P["adapter.gamma_head.0.weight"].view(Lt, Lt), dzs, R=dzs_direct, rscale=1.0)
     del dh, dzs_direct
     # ---- StudentProjector backward -> grads wrt the student layer outputs ----
-    K.linear_dw(dzs, ctx["s_feats"], G["sproj.proj.weight"].view(Lt, cfg.d_student), db=G["sproj.proj.bias"])
+    WGRAD.run(lambda: K.linear_dw(dzs, ctx["s_feats"], G["sproj.proj.weight"].view(Lt, cfg.d_student), db=G["sproj.proj.bias"]), dzs, ctx["s_feats"])
     K.linear_dx(dzs, P["sproj.proj.weight"].view(Lt, cfg.d_student), ds_feats)
     del dzs
     # ---- TeacherAutoEncoder backward (recon only; z_t is detached for the FM target) ----
     drec, zt = ctx["drec"], ctx["zt"]
-    K.linear_dw(drec, zt, G["tae.dec.weight"].view(Ct, Lt), db=G["tae.dec.bias"])
+    WGRAD.run(lambda: K.linear_dw(drec, zt, G["tae.dec.weight"].view(Ct, Lt), db=G["tae.dec.bias"]), drec, zt)
     dzt = _empty(n, Lt, dev=dev)
     K.linear_dx(drec, P["tae.dec.weight"].view(Ct, Lt), dzt)
-    K.linear_dw(dzt, ctx["t_feats"], G["tae.enc.weight"].view(Lt, Ct), db=G["tae.enc.bias"])
+    WGRAD.run(lambda: K.linear_dw(dzt, ctx["t_feats"], G["tae.enc.weight"].view(Lt, Ct), db=G["tae.enc.bias"]), dzt, ctx["t_feats"])
     

@@ -91,10 +91,11 @@ _SCRATCH: dict = {}
 
 
 def scratch(dev, nfloats: int):
-    """Per-device f32 scratch for per-block reduction partials.  Consumers use it strictly in
-    stream order (kernel then fold), so one buffer serves every call site; it only grows, and the
-    eager warm-up step sizes it before any graph capture."""
-    key = torch.device(dev).index if torch.device(dev).index is not None else torch.cuda.current_device()
+    """f32 scratch for per-block reduction partials, one buffer per (device, stream).  Consumers
+    use it strictly in stream order (kernel then fold), so one buffer serves every call site of a
+    stream (the weight-gradient side stream gets its own); it only grows."""
+    idx = torch.device(dev).index if torch.device(dev).index is not None else torch.cuda.current_device()
+    key = (idx, torch.cuda.current_stream(idx).cuda_stream)
     buf = _SCRATCH.get(key)
     if buf is None or buf.numel() < nfloats:
         buf = torch.empty(max(int(nfloats), 1 << 16), device=dev, dtype=torch.float32)

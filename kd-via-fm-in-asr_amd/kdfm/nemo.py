@@ -20,6 +20,7 @@ import torch.nn as nn
 
 from . import _lib
 from . import kernels as K
+from .overlap import WGRAD
 from .config import Ver5Config, encoder_specs
 from .conformer import EncoderShapes, layer_backward, layer_forward, make_workspace, subsampling_backward, \
     subsampling_forward
@@ -187,6 +188,7 @@ class _LayerFn(torch.autograd.Function):
         G = _Flat._G(mod._specs, dout.device)
         dx = layer_backward(mod.cfg, S, P, G, "", mod.idx, ctx.lctx, dout.contiguous().view(S.rows, S.d), ctx.pos,
                             ctx.lengths, seed=mod._seed, salt=_SALT + 2)
+        WGRAD.join()  # the returned grads are read by autograd as soon as this returns
         ctx.lctx = None
         grads = [G[name] for name, _ in mod._specs]
         return (dx.view_as(dout), None, None, None, None, None, *grads)
@@ -247,6 +249,7 @@ class _SubsampleFn(torch.autograd.Function):
         Pp = {"pre_encode." + k: v for k, v in mod._P(ctx.params).items()}
         subsampling_backward(mod.cfg, S, Pp, Gp, "", ctx.sctx, dx.contiguous().view(S.rows, S.d),
                              ctx.len1, seed=mod._seed, salt=_SALT + 3, ws=mod._ws(S))
+        WGRAD.join()
         return (None, None, None, None, None, *[G[n] for n, _ in mod._specs])
 
 

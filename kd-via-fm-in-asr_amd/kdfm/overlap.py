@@ -1,0 +1,61 @@
+"""Weight-gradient overlap: run the backward's weight-gradient GEMMs on a second HIP stream.
+
+In the backward every Linear contributes a dX product (on the critical path: the next layer needs
+it) and a dW product (needed only by the optimizer).  The dW GEMMs of the Conformer layers are
+small (K = B*T' rows, a few hundred outputs) and latency bound, so running them concurrently
+with the dX chain fills CUs the chain leaves idle.  Ordering:
+
+  * fork: the side stream waits for everything issued on the main stream so far (one event), so
+    the dY / X operands are complete;
+  * the operand tensors are kept referenced until the join, so the caching allocator cannot hand
+    their memory to main-stream work while the side stream still reads them (capture-safe,
+    unlike record_stream);
+  * join: the main stream waits for the side stream before anything reads the accumulated
+    gradients (optimizer, all-reduce, or a consumer of a side-produced partial).
+
+Both streams are captured into the same HIP graph by GraphedTrainStep (fork/join are graph
+edges)."""
+from __future__ import annotations
+
+import torch
+
+
+class WgradOverlap:
+    def __init__(self, enabled: bool = True):
+        self.enabled = enabled
+        self._side = {}
+        self._keep = []
+        self._pending = False
+
+    def _stream(self, dev):
+        key = torch.device(dev).index
+        s = self._side.get(key)
+        if s is None:
+            s = torch.cuda.Stream(device=dev)
+            self._side[key] = s
+        return s
+
+    def run(self, fn, *keep):
+        """Issue fn() (kernel launches only) on the side stream after all current main-stream work."""
+        if not self.enabled:
+            fn()
+            return
+        main = torch.cuda.current_stream()
+        side = self._stream(main.device)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            fn()
+        self._keep.extend(keep)
+        self._pending = True
+
+    def join(self):
+        """Main stream waits for all side-stream work; releases the kept operands."""
+        if not self._pending:
+            return
+        main = torch.cuda.current_stream()
+        main.wait_stream(self._stream(main.device))
+        self._keep.clear()
+        self._pending = False
+
+
+WGRAD = WgradOverlap()

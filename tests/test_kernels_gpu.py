@@ -65,3 +65,22 @@ def test_dwconv_bwd(B, T, d, k):
     _close(dx, xr.grad)
     _close(dw, wr.grad)
     _close(db, br.grad)
+
+
+@pytest.mark.parametrize("B,T,d,k", [(2, 26, 88, 31), (3, 401, 176, 31), (2, 70, 40, 15), (2, 50, 24, 7)])
+def test_dwconv_fwd_stats(B, T, d, k):
+    K = _K()
+    g = torch.Generator().manual_seed(B * T + d + k + 1)
+    x = torch.randn(B, T, d, generator=g).cuda()
+    w = torch.randn(d, k, generator=g).cuda()
+    bias = torch.randn(d, generator=g).cuda()
+    y = torch.empty_like(x)
+    stats = torch.zeros(2 * d, dtype=torch.float64, device="cuda")
+    K.dwconv_fwd(x, w, bias, y, stats, B, T, d, k)
+    torch.cuda.synchronize()
+    ref = torch.nn.functional.conv1d(x.transpose(1, 2), w.unsqueeze(1), bias, padding=(k - 1) // 2,
+                                     groups=d).transpose(1, 2)
+    _close(y, ref)
+    r64 = ref.double().reshape(-1, d)
+    torch.testing.assert_close(stats[:d], r64.sum(0), rtol=1e-5, atol=1e-3)
+    torch.testing.assert_close(stats[d:], (r64 * r64).sum(0), rtol=1e-5, atol=1e-3)
