@@ -148,6 +148,23 @@ int kdfm_im2col_3x3s2(const float* X, const int64_t* len_in, float* cols, int64_
 int kdfm_col2im_3x3s2(const float* dcols, const int64_t* len_in, const float* relu_out, float* dX, int64_t B,
                       int64_t T1, int64_t F1, int64_t C, void* stream);
 
+/* Fused striding subsampling forward (bf16 MFMA mode; replaces im2col + GEMM for the same A.3
+ * arithmetic, conformer_encoder.py:381-390, 635):
+ *   kdfm_subsample_conv1: y1[(b,t1,f1), c] = mask(t1 < len1[b]) * relu(b0[c] + sum_tap w0[c,tap] *
+ *     mel[b, 2t1-1+ky, 2f1-1+kx]) with mel frames >= mel_len[b] read as zero; mel channels-last
+ *     (B,Tm,F); y1b bf16 (B,T1,F1,C) and optionally y1f f32 (same layout).  C % 8 == 0.
+ *   kdfm_subsample_wprep: conv2 weight (C,C,3,3) f32 -> bf16 image [Np][9][Cp] (Np = C rounded up
+ *     to 32, Cp = C rounded up to 16, zero padded); kdfm_subsample_wprep_elems gives its size.
+ *   kdfm_subsample_conv2: implicit GEMM y2[(b,t2,f2), c] = mask(t2 < len2[b]) * relu(b2[c] +
+ *     sum_{tap,ci} W2[c,ci,tap] y1[b, 2t2-1+ky, 2f2-1+kx, ci]); y2 f32 channels-last.  C <= 192. */
+int64_t kdfm_subsample_wprep_elems(int64_t C);
+int kdfm_subsample_wprep(const float* w2, uint16_t* wb, int64_t C, void* stream);
+int kdfm_subsample_conv1(const float* mel, const int64_t* mel_len, const int64_t* len1, const float* w0,
+                         const float* b0, uint16_t* y1b, float* y1f, int64_t B, int64_t Tm, int64_t F, int64_t C,
+                         void* stream);
+int kdfm_subsample_conv2(const uint16_t* y1b, const int64_t* len2, const uint16_t* wb, const float* b2, float* y2,
+                         int64_t B, int64_t T1, int64_t F1, int64_t C, void* stream);
+
 /* ---------------- ConformerLayer (Appendix A.5-A.8; layers built conformer_encoder.py:450-472) */
 int kdfm_layernorm_fwd(const float* x, const float* gamma, const float* beta, float* y, float* mean, float* rstd,
                        int64_t rows, int64_t d, float eps, void* stream);

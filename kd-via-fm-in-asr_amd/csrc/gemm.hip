@@ -268,6 +268,54 @@ __global__ __launch_bounds__(NT) void gemm_kernel(P p) {
   if (epi & KDFM_EPI_DROPOUT) seed = load_seed(p.seed);
   const float keep_scale = (epi & KDFM_EPI_DROPOUT) ? 1.f / (1.f - p.dropout_p) : 1.f;
   float mse_part = 0.f;
+  bool single;
+  const float* side = epi_side_src(p, single);
+  if (!(epi & KDFM_EPI_ATOMIC) && single) {
+    // two-phase: every side operand / bias / row-mask load first, then compute and store
+    float sv[2][2][4], bnv[2][2];
+    bool rok[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t m = m0 + wr * 32 + i * 16 + (lane >> 4) * 4 + r;
+        rok[i][r] = m < p.M && epi_row_ok(p, m < p.M ? m : 0);
+      }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int64_t n = n0 + wc * 32 + j * 16 + (lane & 15);
+      bnv[j][0] = ((epi & KDFM_EPI_BIAS) && n < p.N) ? p.bias[n] : 0.f;
+    }
+    if (side) {
+      const float* sb = side + cOff;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int64_t m = m0 + wr * 32 + i * 16 + (lane >> 4) * 4 + r;
+            const int64_t n = n0 + wc * 32 + j * 16 + (lane & 15);
+            sv[i][j][r] = (m < p.M && n < p.N) ? sb[m * p.sCm + n * p.sCn] : 0.f;
+          }
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int64_t m = m0 + wr * 32 + i * 16 + (lane >> 4) * 4 + r;
+          const int64_t n = n0 + wc * 32 + j * 16 + (lane & 15);
+          if (m >= p.M || n >= p.N) continue;
+          const int64_t off = cOff + m * p.sCm + n * p.sCn;
+          float pre = 0.f;
+          const float v = epi_apply(p, bz, m, n, p.alpha * acc[i][j][r], bnv[j][0], side ? sv[i][j][r] : 0.f,
+                                    rok[i][r], seed, keep_scale, mse_part, pre);
+          if (epi & KDFM_EPI_STORE_PRE) p.Cpre[off] = pre;
+          p.C[off] = v;
+        }
+  } else {
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -288,6 +336,7 @@ __global__ __launch_bounds__(NT) void gemm_kernel(P p) {
         }
         epilogue_store(p, bz, m, n, off, v, seed, keep_scale, mse_part);
       }
+  }
   if (epi & KDFM_EPI_MSE) {
     mse_part = wave_sum(mse_part);
     if (lane == 0) atomicAdd(p.loss_acc, mse_part * p.loss_scale);
@@ -363,6 +412,8 @@ extern "C" int kdfm_gemm(const kdfm_gemm_desc* d, void* stream) {
   if (d->math == KDFM_MATH_BF16 && d->K > 0) {
     const int64_t batch = d->batch1 * d->batch2;
     int rc = try_rowstream_wgrad(p, d->amode, d->bmode, batch, st);
+    if (rc >= 0) return rc;
+    rc = try_skinny_fwd(p, d->amode, d->bmode, batch, st);
     if (rc >= 0) return rc;
     rc = try_rowstream_fwd(p, d->amode, d->bmode, batch, st);
     if (rc >= 0) return rc;

@@ -58,10 +58,63 @@ __device__ __forceinline__ void epilogue_store(const GemmP& p, int64_t bz, int64
   p.C[off] = v;
 }
 
+// Two-phase epilogue (load every side operand of a tile, THEN compute and store).  On CDNA the
+// vector-memory counter covers loads and stores alike, so a per-element load issued after earlier
+// stores waits for all of them: an interleaved load/store epilogue serialises on store latency.
+// The side operand an epilogue reads per element is at most one of R (RESID/MSE), aux
+// (DRELU/DSILU) or C_old (BETA); epi_side_src() returns it and clears `single` when a descriptor
+// needs more than one (callers then use epilogue_store).
+__host__ __device__ inline const float* epi_side_src(const GemmP& p, bool& single) {
+  const int e = p.epi;
+  int cnt = 0;
+  const float* s = nullptr;
+  if (e & (KDFM_EPI_RESID | KDFM_EPI_MSE)) { ++cnt; s = p.R; }
+  if (e & (KDFM_EPI_DRELU | KDFM_EPI_DSILU)) { ++cnt; s = p.aux; }
+  if (e & KDFM_EPI_BETA) { ++cnt; s = p.C; }
+  single = cnt <= 1;
+  return s;
+}
+
+__device__ __forceinline__ bool epi_row_ok(const GemmP& p, int64_t m) {
+  if (!(p.epi & KDFM_EPI_ROWMASK)) return true;
+  const int64_t fr = m / p.mask_div;
+  const int64_t t = fr % p.mask_T, u = fr / p.mask_T;
+  return t < p.mask_len[u];
+}
+
+// Same per-element semantics as epilogue_store with the side value `sv` and bias `bn` already in
+// registers.  Returns the value for C; *pre receives the pre-activation (STORE_PRE).
+__device__ __forceinline__ float epi_apply(const GemmP& p, int64_t bz, int64_t m, int64_t n, float v, float bn, float sv,
+                                           bool rowok, uint64_t seed, float keep_scale, float& mse_part,
+                                           float& pre) {
+  const int epi = p.epi;
+  if (epi & KDFM_EPI_BIAS) v += bn;
+  if (epi & KDFM_EPI_MSE) {
+    const float diff = v - sv;
+    mse_part += diff * diff;
+    return p.rscale * diff;
+  }
+  pre = v;
+  if (epi & KDFM_EPI_RELU) v = fmaxf(v, 0.f);
+  if (epi & KDFM_EPI_SILU) v = siluf_(v);
+  if (epi & KDFM_EPI_DROPOUT) {
+    const uint64_t idx = ((uint64_t)bz * (uint64_t)p.M + (uint64_t)m) * (uint64_t)p.N + (uint64_t)n;
+    v = dropout_keep(seed, p.rng_stream, idx, p.dropout_p) ? v * keep_scale : 0.f;
+  }
+  if (epi & KDFM_EPI_DRELU) v = (sv > 0.f) ? v : 0.f;
+  if (epi & KDFM_EPI_DSILU) v *= dsiluf_(sv);
+  if (epi & KDFM_EPI_RESID) v = sv + p.rscale * v;
+  if (epi & KDFM_EPI_BETA) v += p.beta * sv;
+  if (!rowok) v = 0.f;
+  return v;
+}
+
 // Row-stream / wide-tile entry points (rowstream.hip).  try_* return -1 when the descriptor is
 // not eligible (caller falls back to the generic kernel), else a kdfm_status.
 int try_rowstream_fwd(const GemmP& p, int amode, int bmode, int64_t batch, hipStream_t st);
 int try_rowstream_wgrad(const GemmP& p, int amode, int bmode, int64_t batch, hipStream_t st);
 int64_t rowstream_wgrad_ws(const GemmP& p, int amode, int bmode, int64_t batch);
+// Weight-stationary skinny forward (skinny.hip); -1 when not eligible.
+int try_skinny_fwd(const GemmP& p, int amode, int bmode, int64_t batch, hipStream_t st);
 
 }  // namespace kdfm

@@ -1,0 +1,388 @@
+// Weight-stationary skinny GEMM for the Conformer / KD-head products (bf16 MFMA 32x32x16, f32
+// accumulate):  C[M x N] = epi(alpha * A[M x K] * B[K x N]),  M >> N, K (N, K <= a few hundred).
+//
+// Every Linear / 1x1 conv / k=3 time conv of the ver5 step and its data-gradient has this shape:
+// 12,832 rows (B*T' frames) for the encoders (conformer_encoder.py:685-692, App. A.5-A.8) and
+// 205,312 rows (16 layers x B*T') for the stacked KD heads (asr_train_diffm.py:400-497), against
+// 88..704 output channels.  Such a product is HBM/latency bound, so the kernel is shaped around
+// streaming the activation exactly once with many bytes in flight:
+//
+//  * a workgroup owns a column range of B (weights) and stages it ONCE, as bf16, into LDS
+//    ([n][k] image, k padded to 16); it then walks row tiles persistently (grid-stride), so the
+//    weight staging is amortised over all the rows it processes;
+//  * each wave computes a 32-row x (32*NCT)-column tile with v_mfma_f32_32x32x16_bf16; its A
+//    fragments are loaded straight from HBM into registers (8 consecutive k per lane, f32 ->
+//    bf16 in registers; no LDS, no barrier in the row loop) in chunks of 96 k, and the next
+//    chunk/tile is prefetched while the MFMAs of the current one run;
+//  * CONV mode (Conv1d k=3 along frames, per-utterance zero padding): chunk c = tap c reads the
+//    shifted rows m + c - pad, so the conv never materialises an im2col matrix;
+//  * the fused epilogue is the shared per-element epilogue_store (bias, ReLU/SiLU, STORE_PRE,
+//    counter-RNG dropout, dReLU/dSiLU, residual, beta, row mask, MSE) — identical semantics to
+//    the generic kernel; the 32x32 accumulator layout stores 128 contiguous bytes per half-wave.
+//
+// Selected inside kdfm_gemm for bf16 math (the f32 parity mode keeps the generic kernel), so the
+// C-ABI and every call site are unchanged.
+#include "gemm_common.h"
+
+#include <cstdlib>
+
+namespace kdfm {
+namespace {
+
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+
+constexpr int SK_CKS = 6;             // k-steps (16 k each) per A chunk in KC mode
+constexpr int SK_CHUNK = 16 * SK_CKS; // 96
+
+struct SkGeo {
+  int Kp;       // B image k extent (K rounded up to 16)
+  int ldb;      // B image row stride in bf16 elements (Kp + 8)
+  int chunk;    // k per A chunk (96 in KC mode, conv_c in CONV mode); multiple of 16
+  int nchunks;  // chunks per row tile
+  int cw;       // columns per column range (= 32 * NCT * gcols)
+  int gcols;    // waves sharing one row tile (column groups)
+  int64_t tiles;  // 32-row tiles
+};
+
+__device__ __forceinline__ void pk4(uint16_t* dst, float4 v) {
+  const uint32_t lo = (uint32_t)f2bf(v.x) | ((uint32_t)f2bf(v.y) << 16);
+  const uint32_t hi = (uint32_t)f2bf(v.z) | ((uint32_t)f2bf(v.w) << 16);
+  *reinterpret_cast<uint2*>(dst) = make_uint2(lo, hi);
+}
+
+__device__ __forceinline__ bf16x8 cvt8(float4 a, float4 b) {
+  bf16x8 r;
+  r[0] = (short)f2bf(a.x); r[1] = (short)f2bf(a.y); r[2] = (short)f2bf(a.z); r[3] = (short)f2bf(a.w);
+  r[4] = (short)f2bf(b.x); r[5] = (short)f2bf(b.y); r[6] = (short)f2bf(b.z); r[7] = (short)f2bf(b.w);
+  return r;
+}
+
+// Stage B columns [n0, n0 + cw) x k [0, Kp) into the bf16 [n][k] image (zero outside N / K).
+__device__ void sk_stage_B(const GemmP& p, const SkGeo& g, uint16_t* Bs, int64_t n0) {
+  const int nth = blockDim.x, tid = threadIdx.x;
+  const int cw = g.cw, Kp = g.Kp, ldb = g.ldb;
+  if (p.sBk == 1 && (p.K & 3) == 0 && (p.sBn & 3) == 0 && ((((uintptr_t)p.B) & 15) == 0)) {
+    // W[n][k]: float4 along k
+    const int kq = Kp >> 2;
+    const int total = cw * kq;
+    for (int base = 0; base < total; base += nth * 4) {
+      float4 v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int e = base + tid + i * nth;
+        const int nl = e / kq, k = (e - nl * kq) * 4;
+        const int64_t n = n0 + nl;
+        v[i] = (e < total && n < p.N && k < p.K) ? *reinterpret_cast<const float4*>(p.B + n * p.sBn + k)
+                                                 : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int e = base + tid + i * nth;
+        if (e < total) {
+          const int nl = e / kq, k = (e - nl * kq) * 4;
+          pk4(Bs + nl * ldb + k, v[i]);
+        }
+      }
+    }
+  } else if (p.sBn == 1 && (p.N & 3) == 0 && (p.sBk & 3) == 0 && ((((uintptr_t)p.B) & 15) == 0) &&
+             (n0 & 3) == 0) {
+    // B(k, n) contiguous along n: float4 along n, transposed into the image
+    const int nq = cw >> 2;
+    const int total = Kp * nq;
+    for (int base = 0; base < total; base += nth * 4) {
+      float4 v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int e = base + tid + i * nth;
+        const int k = e / nq, nl = (e - k * nq) * 4;
+        const int64_t n = n0 + nl;
+        v[i] = (e < total && n < p.N && k < p.K) ? *reinterpret_cast<const float4*>(p.B + (int64_t)k * p.sBk + n)
+                                                 : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int e = base + tid + i * nth;
+        if (e < total) {
+          const int k = e / nq, nl = (e - k * nq) * 4;
+          Bs[(nl + 0) * ldb + k] = f2bf(v[i].x);
+          Bs[(nl + 1) * ldb + k] = f2bf(v[i].y);
+          Bs[(nl + 2) * ldb + k] = f2bf(v[i].z);
+          Bs[(nl + 3) * ldb + k] = f2bf(v[i].w);
+        }
+      }
+    }
+  } else {
+    for (int e = tid; e < cw * Kp; e += nth) {
+      const int nl = e / Kp, k = e - nl * Kp;
+      const int64_t n = n0 + nl;
+      const float x = (n < p.N && k < p.K) ? p.B[(int64_t)k * p.sBk + n * p.sBn] : 0.f;
+      Bs[nl * ldb + k] = f2bf(x);
+    }
+  }
+}
+
+// A chunk for one wave: lane (r = lane&31, h = lane>>5) holds, for k-step s, the 8 values
+// A(m0 + r, kc + 16 s + 8 h + j), j = 0..7 (two float4 loads); zero outside M / K / utterance.
+template <int AMODE>
+__device__ __forceinline__ void sk_load_A(float4 (&v)[SK_CKS][2], const GemmP& p, const SkGeo& g, int64_t m0,
+                                          int c, int lane) {
+  const int r = lane & 31, h = lane >> 5;
+  const int64_t m = m0 + r;
+  int64_t row = m;
+  bool ok = m < p.M;
+  int kbase;
+  if constexpr (AMODE == KDFM_LD_CONV) {
+    // chunk c is tap c: rows shifted by c - pad, zero outside the utterance
+    const int64_t t = m % p.conv_t;
+    const int64_t tt = t + c - p.pad;
+    ok = ok && tt >= 0 && tt < p.conv_t;
+    row = m + c - p.pad;
+    kbase = 0;
+  } else {
+    kbase = c * SK_CHUNK;
+  }
+  const float* src = p.A + row * p.sAm;
+  const int klim = (AMODE == KDFM_LD_CONV) ? (int)p.conv_c : (int)p.K;
+#pragma unroll
+  for (int s = 0; s < SK_CKS; ++s) {
+    const int k = kbase + 16 * s + 8 * h;
+    if (ok && 16 * s < g.chunk && k < klim) {
+      const float4* q = reinterpret_cast<const float4*>(src + k);
+      v[s][0] = q[0];
+      v[s][1] = q[1];
+    } else {
+      v[s][0] = make_float4(0.f, 0.f, 0.f, 0.f);
+      v[s][1] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+}
+
+template <int NCT, int AMODE, int WV>
+__global__ __launch_bounds__(64 * WV, 2) void sk_fwd_kernel(GemmP p, SkGeo g) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t sk_lds[];
+  uint16_t* Bs = sk_lds;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t ncr0 = (int64_t)blockIdx.y * g.cw;
+  sk_stage_B(p, g, Bs, ncr0);
+  __syncthreads();
+
+  const int cg = wave % g.gcols;
+  const int rpi = WV / g.gcols;                 // row tiles per workgroup iteration
+  const int rsub = wave / g.gcols;
+  if (rsub >= rpi) return;                      // (WV not a multiple of gcols)
+  const int nl0 = cg * 32 * NCT;                // first image column of this wave
+  const int64_t n0 = ncr0 + nl0;
+  if (n0 >= p.N) return;                        // no columns for this wave (no barrier follows)
+  const int r = lane & 31, h = lane >> 5;
+  const int64_t tstride = (int64_t)gridDim.x * rpi;
+  const int64_t tfirst = (int64_t)blockIdx.x * rpi + rsub;
+  if (tfirst >= g.tiles) return;
+  const int64_t ntile = (g.tiles - tfirst + tstride - 1) / tstride;
+  const int64_t nsteps = ntile * g.nchunks;
+
+  const int epi = p.epi;
+  const uint64_t seed = (epi & KDFM_EPI_DROPOUT) ? load_seed(p.seed) : 0ull;
+  const float keep_scale = (epi & KDFM_EPI_DROPOUT) ? 1.f / (1.f - p.dropout_p) : 1.f;
+  bool single;
+  const float* side = epi_side_src(p, single);  // the dispatcher guarantees `single`
+  float mse_part = 0.f;
+  // per-lane column constants: this lane's output column in tile j is n0 + 32 j + r
+  float bn[NCT];
+#pragma unroll
+  for (int j = 0; j < NCT; ++j) {
+    const int64_t n = n0 + 32 * j + r;
+    bn[j] = ((epi & KDFM_EPI_BIAS) && n < p.N) ? p.bias[n] : 0.f;
+  }
+
+  const uint16_t* bp = Bs + (nl0 + r) * g.ldb + 8 * h;
+  f32x16 acc[NCT];
+  float4 av[SK_CKS][2];
+  sk_load_A<AMODE>(av, p, g, tfirst * 32, 0, lane);
+  int c = 0;
+  int64_t tile = tfirst;
+  for (int64_t q = 0; q < nsteps; ++q) {
+    const bool last = (c == g.nchunks - 1);
+    const int64_t m0 = tile * 32;
+    // side operands of this tile's epilogue: issued before the prefetch and the MFMAs
+    float sv[NCT][16];
+    bool rowok[16];
+    if (last) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int64_t m = m0 + (i & 3) + 8 * (i >> 2) + 4 * h;
+        rowok[i] = m < p.M && epi_row_ok(p, m < p.M ? m : 0);
+      }
+      if (side) {
+#pragma unroll
+        for (int j = 0; j < NCT; ++j) {
+          const int64_t n = n0 + 32 * j + r;
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int64_t m = m0 + (i & 3) + 8 * (i >> 2) + 4 * h;
+            sv[j][i] = (m < p.M && n < p.N) ? side[m * p.sCm + n * p.sCn] : 0.f;
+          }
+        }
+      }
+    }
+    bf16x8 af[SK_CKS];
+#pragma unroll
+    for (int s = 0; s < SK_CKS; ++s) af[s] = cvt8(av[s][0], av[s][1]);
+    // prefetch the next (tile, chunk)
+    {
+      int c2 = c + 1;
+      int64_t t2 = tile;
+      if (c2 == g.nchunks) { c2 = 0; t2 += tstride; }
+      if (q + 1 < nsteps) sk_load_A<AMODE>(av, p, g, t2 * 32, c2, lane);
+    }
+    if (c == 0) {
+#pragma unroll
+      for (int j = 0; j < NCT; ++j)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[j][i] = 0.f;
+    }
+    const int kimg = c * g.chunk;
+#pragma unroll
+    for (int s = 0; s < SK_CKS; ++s) {
+      if (16 * s < g.chunk) {
+#pragma unroll
+        for (int j = 0; j < NCT; ++j) {
+          const bf16x8 bfr = *reinterpret_cast<const bf16x8*>(bp + j * 32 * g.ldb + kimg + 16 * s);
+          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[s], bfr, acc[j], 0, 0, 0);
+        }
+      }
+    }
+    if (last) {
+#pragma unroll
+      for (int j = 0; j < NCT; ++j) {
+        const int64_t n = n0 + 32 * j + r;
+        const bool nok = n < p.N;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int64_t m = m0 + (i & 3) + 8 * (i >> 2) + 4 * h;
+          if (!nok || m >= p.M) continue;
+          float pre = 0.f;
+          const float v = epi_apply(p, 0, m, n, p.alpha * acc[j][i], bn[j], side ? sv[j][i] : 0.f, rowok[i], seed,
+                                    keep_scale, mse_part, pre);
+          const int64_t off = m * p.sCm + n * p.sCn;
+          if (epi & KDFM_EPI_STORE_PRE) p.Cpre[off] = pre;
+          p.C[off] = v;
+        }
+      }
+      c = 0;
+      tile += tstride;
+    } else {
+      ++c;
+    }
+  }
+  if (epi & KDFM_EPI_MSE) {
+    mse_part = wave_sum(mse_part);
+    if (lane == 0) atomicAdd(p.loss_acc, mse_part * p.loss_scale);
+  }
+}
+
+template <int NCT, int AMODE, int WV>
+int sk_launch(const GemmP& p, const SkGeo& g, int64_t gx, int64_t ncr, size_t lds, hipStream_t st) {
+  if (lds > 64 * 1024) {
+    static bool once = [] {
+      hipFuncSetAttribute((const void*)sk_fwd_kernel<NCT, AMODE, WV>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          160 * 1024);
+      return true;
+    }();
+    (void)once;
+  }
+  hipLaunchKernelGGL((sk_fwd_kernel<NCT, AMODE, WV>), dim3((unsigned)gx, (unsigned)ncr), dim3(64 * WV), lds, st, p,
+                     g);
+  return check_launch("kdfm_gemm(skinny fwd)");
+}
+
+template <int AMODE, int WV>
+int sk_dispatch_nct(int nct, const GemmP& p, const SkGeo& g, int64_t gx, int64_t ncr, size_t lds, hipStream_t st) {
+  switch (nct) {
+    case 1: return sk_launch<1, AMODE, WV>(p, g, gx, ncr, lds, st);
+    case 2: return sk_launch<2, AMODE, WV>(p, g, gx, ncr, lds, st);
+    default: return sk_launch<3, AMODE, WV>(p, g, gx, ncr, lds, st);
+  }
+}
+
+int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+
+}  // namespace
+
+int try_skinny_fwd(const GemmP& p, int amode, int bmode, int64_t batch, hipStream_t st) {
+  static const int enabled = env_int("KDFM_SKINNY", 1);
+  static const int min_m = env_int("KDFM_SKINNY_MIN_M", 65536);
+  static const int target_wgs = env_int("KDFM_SKINNY_WGS", 512);
+  if (!enabled) return -1;
+  if (batch != 1 || p.splitk != 1 || (p.epi & KDFM_EPI_ATOMIC) || p.ones_col >= 0) return -1;
+  if (p.M < min_m || p.N <= 0 || p.K <= 0) return -1;
+  if (bmode != KDFM_LD_KC && bmode != KDFM_LD_XC) return -1;
+  if (p.sAk != 1 || (p.sAm & 3) || (((uintptr_t)p.A) & 15)) return -1;
+  bool single;
+  epi_side_src(p, single);
+  if (!single) return -1;
+  SkGeo g;
+  if (amode == KDFM_LD_CONV) {
+    if (p.conv_c % 16 != 0 || p.conv_c > SK_CHUNK || p.K != p.taps * p.conv_c || p.pad < 0 || p.pad >= p.taps)
+      return -1;
+    g.chunk = (int)p.conv_c;
+    g.nchunks = p.taps;
+  } else if (amode == KDFM_LD_KC) {
+    if (p.K & 7) return -1;
+    g.chunk = SK_CHUNK;
+    g.nchunks = (int)ceil_div(p.K, SK_CHUNK);
+  } else {
+    return -1;
+  }
+  g.Kp = (int)(ceil_div(p.K, 16) * 16);
+  if (amode == KDFM_LD_KC) {
+    // the last chunk may read image columns up to nchunks*96 - 1: pad the image to that
+    g.Kp = g.nchunks * SK_CHUNK;
+  }
+  g.ldb = g.Kp + 8;
+  // column decomposition: NCT 32-col tiles per wave, gcols waves per row tile
+  const int64_t nt32 = ceil_div(p.N, 32);
+  int gcols, nct;
+  if (nt32 <= 4) { gcols = 1; nct = (int)nt32; }
+  else if (nt32 <= 8) { gcols = 2; nct = (int)ceil_div(nt32, 2); }
+  else { gcols = 4; nct = (int)(nt32 <= 12 ? ceil_div(nt32, 4) : 3); }
+  auto lds_of = [&](int gc, int nc) { return (size_t)32 * nc * gc * g.ldb * sizeof(uint16_t); };
+  const size_t lds_soft = 80 * 1024, lds_hard = 160 * 1024;
+  while (lds_of(gcols, nct) > lds_soft && (nct > 1 || gcols > 1)) {
+    if (nct > 1) --nct; else gcols >>= 1;
+  }
+  const size_t lds = lds_of(gcols, nct);
+  if (lds > lds_hard) return -1;
+  g.gcols = gcols;
+  g.cw = 32 * nct * gcols;
+  const int64_t ncr = ceil_div(p.N, g.cw);
+  static const int max_ncr = env_int("KDFM_SKINNY_MAX_NCR", 2);
+  if (ncr > max_ncr) return -1;  // A would be re-read more than max_ncr times: generic kernel
+  g.tiles = ceil_div(p.M, 32);
+  // waves per workgroup: enough workgroups to cover the CUs for small M, 4 waves otherwise
+  int wv = 4;
+  while (wv > gcols && (g.tiles * gcols) / wv * ncr < 256) wv >>= 1;
+  if (wv < gcols) wv = gcols;
+  const int rpi = wv / gcols;
+  int64_t gx = ceil_div(g.tiles, rpi);
+  const int64_t cap = ceil_div(target_wgs, ncr);
+  if (gx > cap) gx = cap;
+  if (gx < 1) gx = 1;
+  if (ncr > 65535) return -1;
+  if (amode == KDFM_LD_CONV) {
+    switch (wv) {
+      case 1: return sk_dispatch_nct<KDFM_LD_CONV, 1>(nct, p, g, gx, ncr, lds, st);
+      case 2: return sk_dispatch_nct<KDFM_LD_CONV, 2>(nct, p, g, gx, ncr, lds, st);
+      default: return sk_dispatch_nct<KDFM_LD_CONV, 4>(nct, p, g, gx, ncr, lds, st);
+    }
+  }
+  switch (wv) {
+    case 1: return sk_dispatch_nct<KDFM_LD_KC, 1>(nct, p, g, gx, ncr, lds, st);
+    case 2: return sk_dispatch_nct<KDFM_LD_KC, 2>(nct, p, g, gx, ncr, lds, st);
+    default: return sk_dispatch_nct<KDFM_LD_KC, 4>(nct, p, g, gx, ncr, lds, st);
+  }
+}
+
+}  // namespace kdfm

@@ -1,0 +1,306 @@
+// Striding ConvSubsampling forward as two fused kernels (bf16 MFMA mode).
+//
+// Reference: ConvSubsampling(subsampling='striding', factor 4, conv_channels = d), built
+// conformer_encoder.py:381-390 and called :635 (source absent):
+//   x (B,T,80) -> Conv2d(1->C, 3x3, s2, p1) -> ReLU -> Conv2d(C->C, 3x3, s2, p1) -> ReLU
+// with padded frames masked to zero before each conv (A.3 flag, default on).
+//
+// The im2col formulation materialises 9x the conv1 output (1.6 GB for the teacher at B=32, 16 s)
+// and streams it through a GEMM.  Here:
+//   ss_conv1  y1 = mask1(ReLU(conv1(mask0(mel)))) computed directly (9 FMAs per output, K = 9 is
+//             far too small for MFMA), stored channels-last as bf16 — the next kernel's MFMA
+//             operand — and optionally as f32 for the backward;
+//   ss_conv2  implicit GEMM: M = output positions (b,t2,f2), N = C_out, K = 9 taps x C_in.
+//             A fragments are 16-byte loads of 8 consecutive channels of y1 at the tap's shifted
+//             position (no im2col matrix); the tap's weight slab [C_out][C_in] (bf16, prepared
+//             by ss_wprep) is double-buffered through LDS with one barrier per tap; 8 waves x 32
+//             positions per workgroup, v_mfma_f32_32x32x16_bf16; bias + ReLU + len2 frame mask
+//             fused in the epilogue, output channels-last f32 rows (b,t2,f2) x C — the layout the
+//             following Linear(C*F2 -> d) consumes.
+#include "common.h"
+
+namespace kdfm {
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) short bf16x8_t;
+typedef __attribute__((ext_vector_type(16))) float f32x16_t;
+
+// ---- weight prep: W (C, C, 3, 3) f32 -> wb[n][tap][ci] bf16, n < Np (zero rows >= C), ci < Cp
+__global__ __launch_bounds__(256) void ss_wprep_kernel(const float* __restrict__ W, uint16_t* __restrict__ wb, int C,
+                                                       int Np, int Cp) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t total = (int64_t)Np * 9 * Cp;
+  if (idx >= total) return;
+  const int ci = (int)(idx % Cp), tap = (int)((idx / Cp) % 9), n = (int)(idx / (9 * Cp));
+  float v = 0.f;
+  if (n < C && ci < C) v = W[((int64_t)n * C + ci) * 9 + tap];
+  wb[idx] = f2bf(v);
+}
+
+// ---- conv1 + ReLU + masks: one thread = one output position x 8 channels
+__global__ __launch_bounds__(256) void ss_conv1_kernel(const float* __restrict__ mel, const int64_t* __restrict__ mel_len,
+                                                       const int64_t* __restrict__ len1, const float* __restrict__ w0,
+                                                       const float* __restrict__ b0, uint16_t* __restrict__ y1b,
+                                                       float* __restrict__ y1f, int B, int Tm, int F, int C, int T1,
+                                                       int F1) {
+  const int CG = C >> 3;
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t total = (int64_t)B * T1 * F1 * CG;
+  if (idx >= total) return;
+  const int cg = (int)(idx % CG);
+  const int64_t pos = idx / CG;
+  const int f1 = (int)(pos % F1);
+  const int t1 = (int)((pos / F1) % T1);
+  const int b = (int)(pos / ((int64_t)F1 * T1));
+  const int64_t ml = mel_len ? mel_len[b] : Tm;
+  const bool rowok = !len1 || t1 < len1[b];
+  float x[9];
+#pragma unroll
+  for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) {
+      const int t = 2 * t1 - 1 + ky, f = 2 * f1 - 1 + kx;
+      x[ky * 3 + kx] = (t >= 0 && t < Tm && t < ml && f >= 0 && f < F) ? mel[((int64_t)b * Tm + t) * F + f] : 0.f;
+    }
+  float out[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = cg * 8 + j;
+    float v = b0[c];
+#pragma unroll
+    for (int q = 0; q < 9; ++q) v = fmaf(w0[c * 9 + q], x[q], v);
+    v = fmaxf(v, 0.f);
+    out[j] = rowok ? v : 0.f;
+  }
+  bf16x8_t pk;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) pk[j] = (short)f2bf(out[j]);
+  *reinterpret_cast<bf16x8_t*>(y1b + pos * C + cg * 8) = pk;
+  if (y1f) {
+    float4* d = reinterpret_cast<float4*>(y1f + pos * C + cg * 8);
+    d[0] = make_float4(out[0], out[1], out[2], out[3]);
+    d[1] = make_float4(out[4], out[5], out[6], out[7]);
+  }
+}
+
+// ---- conv2 implicit GEMM
+constexpr int SS_WAVES = 8;
+constexpr int SS_NT = 64 * SS_WAVES;
+
+struct SsGeo {
+  int B, T1, F1, C, T2, F2;
+  int64_t P;     // output positions B*T2*F2
+  int Cp;        // C_in padded to 16 (k per tap)
+  int ldb;       // LDS image row stride (Cp + 8)
+};
+
+// NCT 32-col tiles of C_out per wave, NWN waves across C_out, KS = Cp/16 k-steps per tap
+template <int NCT, int NWN, int KS>
+__global__ __launch_bounds__(SS_NT, 1) void ss_conv2_kernel(const uint16_t* __restrict__ y1, const int64_t* __restrict__ len2,
+                                                             const uint16_t* __restrict__ wb, const float* __restrict__ b2,
+                                                             float* __restrict__ y2, SsGeo g) {
+  constexpr int NP = 32 * NCT * NWN;                    // padded C_out rows of the image
+  constexpr int BMW = 32 * SS_WAVES / NWN;             // positions per workgroup tile
+  extern __shared__ __attribute__((aligned(16))) uint16_t ss_lds[];
+  const int ldb = g.ldb;
+  uint16_t* buf0 = ss_lds;
+  uint16_t* buf1 = ss_lds + NP * ldb;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int wm = wave / NWN, wn = wave % NWN;
+  const int64_t pos0 = (int64_t)blockIdx.x * BMW + wm * 32;
+  const int nb0 = wn * 32 * NCT;                       // first C_out column of this wave
+
+  // this lane's A position (row r of the wave tile)
+  const int64_t pa = pos0 + r;
+  const bool pok = pa < g.P;
+  const int f2 = pok ? (int)(pa % g.F2) : 0;
+  const int t2 = pok ? (int)((pa / g.F2) % g.T2) : 0;
+  const int bb = pok ? (int)(pa / ((int64_t)g.F2 * g.T2)) : 0;
+  const uint16_t* ybase = y1 + (int64_t)bb * g.T1 * g.F1 * g.C;
+
+  // B slab staging: NP rows x Cp bf16 per tap, 16-byte chunks
+  constexpr int CPR = KS * 2;                           // 16-B chunks per row (Cp / 8)
+  constexpr int CHUNKS = NP * CPR;
+  constexpr int BPT = (CHUNKS + SS_NT - 1) / SS_NT;     // chunks per thread
+  bf16x8_t breg[BPT];
+  auto load_B = [&](int tap) {
+#pragma unroll
+    for (int i = 0; i < BPT; ++i) {
+      const int e = threadIdx.x + i * SS_NT;
+      if (e < CHUNKS) {
+        const int n = e / CPR, q = e - n * CPR;
+        breg[i] = *reinterpret_cast<const bf16x8_t*>(wb + ((int64_t)n * 9 + tap) * g.Cp + q * 8);
+      }
+    }
+  };
+  auto store_B = [&](uint16_t* dst) {
+#pragma unroll
+    for (int i = 0; i < BPT; ++i) {
+      const int e = threadIdx.x + i * SS_NT;
+      if (e < CHUNKS) {
+        const int n = e / CPR, q = e - n * CPR;
+        *reinterpret_cast<bf16x8_t*>(dst + n * ldb + q * 8) = breg[i];
+      }
+    }
+  };
+  auto load_A = [&](bf16x8_t (&a)[KS], int tap) {
+    const int ky = tap / 3, kx = tap - ky * 3;
+    const int t1 = 2 * t2 - 1 + ky, f1 = 2 * f2 - 1 + kx;
+    const bool ok = pok && t1 >= 0 && t1 < g.T1 && f1 >= 0 && f1 < g.F1;
+    const uint16_t* src = ybase + ((int64_t)t1 * g.F1 + f1) * g.C;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int ci = 16 * s + 8 * h;
+      if (ok && ci < g.C)
+        a[s] = *reinterpret_cast<const bf16x8_t*>(src + ci);
+      else
+        a[s] = bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+  };
+
+  f32x16_t acc[NCT];
+#pragma unroll
+  for (int j = 0; j < NCT; ++j)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[j][i] = 0.f;
+
+  bf16x8_t acur[KS], anxt[KS];
+  load_B(0);
+  load_A(acur, 0);
+  store_B(buf0);
+  __syncthreads();
+  for (int tap = 0; tap < 9; ++tap) {
+    const bool more = tap + 1 < 9;
+    if (more) {
+      load_B(tap + 1);
+      load_A(anxt, tap + 1);
+    }
+    const uint16_t* bs = (tap & 1) ? buf1 : buf0;
+    const uint16_t* bp = bs + (nb0 + r) * ldb + 8 * h;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+#pragma unroll
+      for (int j = 0; j < NCT; ++j) {
+        const bf16x8_t bfr = *reinterpret_cast<const bf16x8_t*>(bp + j * 32 * ldb + 16 * s);
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(acur[s], bfr, acc[j], 0, 0, 0);
+      }
+    }
+    if (more) {
+      store_B((tap & 1) ? buf0 : buf1);
+#pragma unroll
+      for (int s = 0; s < KS; ++s) acur[s] = anxt[s];
+    }
+    __syncthreads();
+  }
+
+  // ---- epilogue: bias + ReLU + frame mask (t2 >= len2[b] -> 0); all loads before stores
+  float bn[NCT];
+#pragma unroll
+  for (int j = 0; j < NCT; ++j) {
+    const int n = nb0 + 32 * j + r;
+    bn[j] = n < g.C ? b2[n] : 0.f;
+  }
+  bool rowok[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int64_t pm = pos0 + (i & 3) + 8 * (i >> 2) + 4 * h;
+    bool ok = pm < g.P;
+    if (ok && len2) {
+      const int tt = (int)((pm / g.F2) % g.T2);
+      const int b = (int)(pm / ((int64_t)g.F2 * g.T2));
+      ok = tt < len2[b];
+      rowok[i] = ok;
+    } else {
+      rowok[i] = ok;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NCT; ++j) {
+    const int n = nb0 + 32 * j + r;
+    if (n >= g.C) continue;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int64_t pm = pos0 + (i & 3) + 8 * (i >> 2) + 4 * h;
+      if (pm >= g.P) continue;
+      const float v = fmaxf(acc[j][i] + bn[j], 0.f);
+      y2[pm * g.C + n] = rowok[i] ? v : 0.f;
+    }
+  }
+}
+
+template <int NCT, int NWN, int KS>
+int ss_launch(const uint16_t* y1, const int64_t* len2, const uint16_t* wb, const float* b2, float* y2,
+              const SsGeo& g, hipStream_t st) {
+  const size_t lds = (size_t)2 * 32 * NCT * NWN * g.ldb * sizeof(uint16_t);
+  if (lds > 64 * 1024) {
+    static bool once = [] {
+      hipFuncSetAttribute((const void*)ss_conv2_kernel<NCT, NWN, KS>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          160 * 1024);
+      return true;
+    }();
+    (void)once;
+  }
+  const int64_t grid = ceil_div(g.P, 32 * SS_WAVES / NWN);
+  hipLaunchKernelGGL((ss_conv2_kernel<NCT, NWN, KS>), dim3((unsigned)grid), dim3(SS_NT), lds, st, y1, len2, wb, b2, y2, g);
+  return check_launch("kdfm_subsample_conv2");
+}
+
+}  // namespace
+}  // namespace kdfm
+
+extern "C" {
+
+int64_t kdfm_subsample_wprep_elems(int64_t C) {
+  const int64_t Np = kdfm::ceil_div(C, 32) * 32, Cp = kdfm::ceil_div(C, 16) * 16;
+  return Np * 9 * Cp;
+}
+
+int kdfm_subsample_wprep(const float* w2, uint16_t* wb, int64_t C, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(w2 && wb && C > 0, "bad arguments");
+  const int64_t Np = ceil_div(C, 32) * 32, Cp = ceil_div(C, 16) * 16;
+  const int64_t n = Np * 9 * Cp;
+  hipLaunchKernelGGL(ss_wprep_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, as_stream(stream), w2, wb,
+                     (int)C, (int)Np, (int)Cp);
+  return check_launch("kdfm_subsample_wprep");
+}
+
+int kdfm_subsample_conv1(const float* mel, const int64_t* mel_len, const int64_t* len1, const float* w0,
+                         const float* b0, uint16_t* y1b, float* y1f, int64_t B, int64_t Tm, int64_t F, int64_t C,
+                         void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(mel && w0 && b0 && y1b, "null pointer");
+  KDFM_REQUIRE(C % 8 == 0 && B > 0 && Tm > 0 && F > 0, "C must be a multiple of 8");
+  const int64_t T1 = (Tm - 1) / 2 + 1, F1 = (F - 1) / 2 + 1;
+  const int64_t n = B * T1 * F1 * (C / 8);
+  KDFM_REQUIRE(n < (1ll << 40), "too large");
+  hipLaunchKernelGGL(ss_conv1_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, as_stream(stream), mel, mel_len,
+                     len1, w0, b0, y1b, y1f, (int)B, (int)Tm, (int)F, (int)C, (int)T1, (int)F1);
+  return check_launch("kdfm_subsample_conv1");
+}
+
+int kdfm_subsample_conv2(const uint16_t* y1b, const int64_t* len2, const uint16_t* wb, const float* b2, float* y2,
+                         int64_t B, int64_t T1, int64_t F1, int64_t C, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(y1b && wb && b2 && y2, "null pointer");
+  KDFM_REQUIRE(C % 8 == 0 && C <= 192 && B > 0 && T1 > 0 && F1 > 0, "C must be a multiple of 8, <= 192");
+  KDFM_REQUIRE((((uintptr_t)y1b) & 15) == 0 && (((uintptr_t)wb) & 15) == 0, "y1b / wb must be 16-byte aligned");
+  SsGeo g;
+  g.B = (int)B; g.T1 = (int)T1; g.F1 = (int)F1; g.C = (int)C;
+  g.T2 = (int)((T1 - 1) / 2 + 1); g.F2 = (int)((F1 - 1) / 2 + 1);
+  g.P = B * g.T2 * g.F2;
+  g.Cp = (int)(ceil_div(C, 16) * 16);
+  g.ldb = g.Cp + 8;
+  const int nct = (int)ceil_div(C, 32), ks = g.Cp / 16;
+  hipStream_t st = as_stream(stream);
+  if (nct == 3 && ks == 6) return ss_launch<3, 1, 6>(y1b, len2, wb, b2, y2, g, st);    // d = 88 / 96
+  if (nct == 6 && ks == 11) return ss_launch<3, 2, 11>(y1b, len2, wb, b2, y2, g, st);  // d = 176
+  if (nct == 6 && ks == 12) return ss_launch<3, 2, 12>(y1b, len2, wb, b2, y2, g, st);  // d = 192
+  if (nct == 1 && ks == 2) return ss_launch<1, 1, 2>(y1b, len2, wb, b2, y2, g, st);    // tiny test sizes
+  if (nct == 2 && ks == 4) return ss_launch<1, 2, 4>(y1b, len2, wb, b2, y2, g, st);
+  set_error("kdfm_subsample_conv2: unsupported channel count");
+  return KDFM_EUNSUPPORTED;
+}
+
+}  // extern "C"

@@ -53,20 +53,37 @@ def _empty(*shape, dev):
 def subsampling_forward(cfg, S: EncoderShapes, P, pre, mel, mel_len, len1, len2, *, train, seed, salt, save, ws):
     dev = mel.device
     B, C, d = S.B, S.d, S.d
-    cols0 = _empty(B * S.T1 * S.F1, 9, dev=dev)
-    K.im2col_3x3s2(mel, mel_len if cfg.subsampling_mask else None, cols0, B, S.Tm, cfg.nfilt, 1)
-    y1 = _empty(B * S.T1 * S.F1, C, dev=dev)
-    w0 = P[pre + "pre_encode.conv.0.weight"].view(C, 9)
-    K.linear(cols0, w0, P[pre + "pre_encode.conv.0.bias"], y1, epi=_lib.EPI_RELU,
-             rowmask=(len1, S.T1, S.F1) if cfg.subsampling_mask else None, math="f32")
-    cols1 = _empty(B * S.T * S.F2, 9 * C, dev=dev)
-    K.im2col_3x3s2(y1, len1 if cfg.subsampling_mask else None, cols1, B, S.T1, S.F1, C)
+    cols0 = cols1 = y1 = None
     y2 = _empty(B * S.T * S.F2, C, dev=dev)
-    w2 = P[pre + "pre_encode.conv.2.weight"].view(C, 9 * C)
-    K.linear(cols1, w2, P[pre + "pre_encode.conv.2.bias"], y2, epi=_lib.EPI_RELU,
-             rowmask=(len2, S.T, S.F2) if cfg.subsampling_mask else None)
-    if not save:
-        del cols1
+    m0 = mel_len if cfg.subsampling_mask else None
+    m1 = len1 if cfg.subsampling_mask else None
+    m2 = len2 if cfg.subsampling_mask else None
+    if K.get_math() == "bf16" and C % 8 == 0 and C <= 192:
+        # fused: direct conv1 (+ReLU+masks) -> bf16 y1, implicit-GEMM conv2 (+bias+ReLU+mask); no
+        # im2col matrix.  The f32 y1 is kept only for the backward (which rebuilds its im2col).
+        y1b = torch.empty(B * S.T1 * S.F1, C, device=dev, dtype=torch.bfloat16)
+        y1 = _empty(B * S.T1 * S.F1, C, dev=dev) if save else None
+        K.subsample_conv1(mel, m0, m1, P[pre + "pre_encode.conv.0.weight"], P[pre + "pre_encode.conv.0.bias"], y1b, y1,
+                          B, S.Tm, cfg.nfilt, C)
+        wb = ws["w2_bf16"]
+        K.subsample_wprep(P[pre + "pre_encode.conv.2.weight"], wb)
+        K.subsample_conv2(y1b, m2, wb, P[pre + "pre_encode.conv.2.bias"], y2, B, S.T1, S.F1, C)
+        del y1b
+    else:
+        cols0 = _empty(B * S.T1 * S.F1, 9, dev=dev)
+        K.im2col_3x3s2(mel, m0, cols0, B, S.Tm, cfg.nfilt, 1)
+        y1 = _empty(B * S.T1 * S.F1, C, dev=dev)
+        w0 = P[pre + "pre_encode.conv.0.weight"].view(C, 9)
+        K.linear(cols0, w0, P[pre + "pre_encode.conv.0.bias"], y1, epi=_lib.EPI_RELU,
+                 rowmask=(len1, S.T1, S.F1) if cfg.subsampling_mask else None, math="f32")
+        cols1 = _empty(B * S.T * S.F2, 9 * C, dev=dev)
+        K.im2col_3x3s2(y1, m1, cols1, B, S.T1, S.F1, C)
+        w2 = P[pre + "pre_encode.conv.2.weight"].view(C, 9 * C)
+        K.linear(cols1, w2, P[pre + "pre_encode.conv.2.bias"], y2, epi=_lib.EPI_RELU,
+                 rowmask=(len2, S.T, S.F2) if cfg.subsampling_mask else None)
+        if not save:
+            del cols1, cols0
+            cols0 = cols1 = None
     # Linear(C*F2 -> d) on channels-last (f, c) flattening: weight re-laid out (d, F2, C) on device
     wout = ws["wout_perm"]
     K.convw_prep(P[pre + "pre_encode.out.weight"].view(d, C, S.F2), fwd=wout)
@@ -79,7 +96,7 @@ def subsampling_forward(cfg, S: EncoderShapes, P, pre, mel, mel_len, len1, len2,
              seed=seed, rng_stream=_stream(salt, -1, SITE_PRE))
     ctx = None
     if save:
-        ctx = dict(cols0=cols0, y1=y1, cols1=cols1, y2=y2, p_pre=p_pre, xscale=xscale)
+        ctx = dict(cols0=cols0, y1=y1, cols1=cols1, y2=y2, p_pre=p_pre, xscale=xscale, mel=mel, mel_len=mel_len)
     return x, ctx
 
 
@@ -97,6 +114,12 @@ def subsampling_backward(cfg, S: EncoderShapes, P, G, pre, ctx, dx, len1, *, see
     dy2 = _empty(B * S.T * S.F2, C, dev=dev)
     K.linear_dx(dlin, ws["wout_perm"].view(d, S.F2 * C), dy2.view(S.rows, S.F2 * C), epi=_lib.EPI_DRELU,
                 aux=y2.view(S.rows, S.F2 * C))
+    if ctx["cols1"] is None:   # fused forward: rebuild the im2col operands of the weight gradients
+        ctx["cols0"] = _empty(B * S.T1 * S.F1, 9, dev=dev)
+        K.im2col_3x3s2(ctx["mel"], ctx["mel_len"] if cfg.subsampling_mask else None, ctx["cols0"], B, S.Tm,
+                       cfg.nfilt, 1)
+        ctx["cols1"] = _empty(B * S.T * S.F2, 9 * C, dev=dev)
+        K.im2col_3x3s2(ctx["y1"], len1 if cfg.subsampling_mask else None, ctx["cols1"], B, S.T1, S.F1, C)
     WGRAD.run(lambda: K.linear_dw(dy2, ctx["cols1"], G[pre + "pre_encode.conv.2.weight"].view(C, 9 * C), db=G[pre + "pre_encode.conv.2.bias"]), dy2, ctx["cols1"])
     dcols1 = _empty(B * S.T * S.F2, 9 * C, dev=dev)
     K.linear_dx(dy2, P[pre + "pre_encode.conv.2.weight"].view(C, 9 * C), dcols1)
@@ -405,6 +428,7 @@ def encoder_backward(cfg, S: EncoderShapes, P, G, prefix, run: EncoderRun, dfeat
 def make_workspace(S: EncoderShapes, dev):
     return {
         "wout_perm": torch.empty(S.d, S.F2, S.d, device=dev),
+        "w2_bf16": torch.empty(K.subsample_wprep_elems(S.d), device=dev, dtype=torch.bfloat16),
         "wout_perm_grad": torch.empty(S.d, S.F2, S.d, device=dev),
         "bout_scaled": torch.empty(S.d, device=dev),
     }

@@ -144,24 +144,42 @@ class Ver5Engine:
         lp = torch.empty(rows, Cn, device=dev)
         K.log_softmax(logits, lp)
         main.wait_stream(side)
+        # ---- CTC + logit KD on a third stream: they only need the two logit tensors, and their
+        # result is first needed after the KD heads' forward, so the serial CTC recursion overlaps it ----
+        acc = torch.zeros(3, device=dev)   # kl, recon, fm
+        aux = self._aux_stream()
+        aux.wait_stream(main)
         Umax = targets.shape[1]
-        alpha_ws = torch.empty(B * T * (2 * Umax + 1), device=dev)
-        beta_ws = torch.empty_like(alpha_ws)
         nll = torch.empty(B, device=dev)
         glogits = torch.empty(rows, Cn, device=dev)
-        K.ctc_loss(lp, targets, len2, tgt_len, alpha_ws, beta_ws, nll, glogits, B, T, Cn, cfg.vocab, 1.0 / B)
-        del alpha_ws, beta_ws
-        acc = torch.zeros(3, device=dev)   # kl, recon, fm
-        Tk = cfg.kd_temperature
-        K.kl_div_logits(lp, tlogits, glogits, acc[0:1], Tk, cfg.kd_alpha * Tk / B, Tk * Tk / B)
+        with torch.cuda.stream(aux):
+            alpha_ws = torch.empty(B * T * (2 * Umax + 1), device=dev)
+            beta_ws = torch.empty_like(alpha_ws)
+            K.ctc_loss(lp, targets, len2, tgt_len, alpha_ws, beta_ws, nll, glogits, B, T, Cn, cfg.vocab, 1.0 / B)
+            del alpha_ws, beta_ws
+            Tk = cfg.kd_temperature
+            K.kl_div_logits(lp, tlogits, glogits, acc[0:1], Tk, cfg.kd_alpha * Tk / B, Tk * Tk / B)
+        for t in (lp, tlogits, targets, len2, tgt_len, nll, glogits, acc):
+            t.record_stream(aux)
         # ---- ver5 heads over all layers at once ----
         n = cfg.n_layers * rows
         hctx = heads_forward(cfg, self.student.P, sfeats.view(n, Ss.d), tfeats.view(n, St.d), T, self.hws, acc[1:3],
                              seed=seed, eps=eps, save=save)
-        K.loss_combine(nll, acc[0:1], acc[1:2], acc[2:3], cfg.kd_alpha, self.losses)
         ctx = dict(B=B, T=T, Ss=Ss, St=St, mel_len=mel_len, len1=len1, len2=len2, srun=srun, sfeats=sfeats,
-                   glogits=glogits, hctx=hctx, lp=lp, nll=nll, pos_s=pos_s)
+                   glogits=glogits, hctx=hctx, lp=lp, nll=nll, pos_s=pos_s, acc=acc)
+        self._join_losses(ctx)   # CTC/KL overlapped the heads forward; losses valid after forward()
         return ctx
+
+    def _aux_stream(self):
+        if getattr(self, "_aux", None) is None:
+            self._aux = torch.cuda.Stream(self.device)
+        return self._aux
+
+    def _join_losses(self, ctx):
+        """Join the CTC/KL stream and assemble the loss vector (total, ctc, kl, recon, fm)."""
+        torch.cuda.current_stream(self.device).wait_stream(self._aux_stream())
+        acc = ctx["acc"]
+        K.loss_combine(ctx["nll"], acc[0:1], acc[1:2], acc[2:3], self.cfg.kd_alpha, self.losses)
 
     def backward(self, ctx):
         cfg = self.cfg

@@ -342,6 +342,35 @@ def col2im_3x3s2(dcols, len_in, relu_out, dX, B, T1, F1, Cc):
     call("kdfm_col2im_3x3s2", ptr(dcols), ptr(_i64(len_in)), ptr(relu_out), ptr(dX), B, T1, F1, Cc, _s())
 
 
+def subsample_wprep(w2, wb):
+    """conv2 weight (C, C, 3, 3) f32 -> the bf16 [Np][9][Cp] image kdfm_subsample_conv2 reads"""
+    Cc = w2.shape[0]
+    assert w2.numel() == Cc * Cc * 9 and wb.dtype == torch.bfloat16
+    assert wb.numel() >= _lib.lib().kdfm_subsample_wprep_elems(Cc)
+    call("kdfm_subsample_wprep", ptr(_f32(w2)), ptr(wb), Cc, _s())
+
+
+def subsample_wprep_elems(Cc):
+    return int(_lib.lib().kdfm_subsample_wprep_elems(Cc))
+
+
+def subsample_conv1(mel, mel_len, len1, w0, b0, y1b, y1f, B, Tm, F, Cc):
+    T1, F1 = (Tm - 1) // 2 + 1, (F - 1) // 2 + 1
+    assert mel.numel() == B * Tm * F and mel.is_contiguous()
+    assert y1b.dtype == torch.bfloat16 and y1b.numel() == B * T1 * F1 * Cc
+    assert y1f is None or y1f.numel() == B * T1 * F1 * Cc
+    assert w0.numel() == Cc * 9 and b0.numel() == Cc
+    call("kdfm_subsample_conv1", ptr(_f32(mel)), ptr(_i64(mel_len)), ptr(_i64(len1)), ptr(_f32(w0)), ptr(_f32(b0)),
+         ptr(y1b), ptr(y1f), B, Tm, F, Cc, _s())
+
+
+def subsample_conv2(y1b, len2, wb, b2, y2, B, T1, F1, Cc):
+    T2, F2 = (T1 - 1) // 2 + 1, (F1 - 1) // 2 + 1
+    assert y1b.dtype == torch.bfloat16 and y1b.numel() == B * T1 * F1 * Cc
+    assert y2.numel() == B * T2 * F2 * Cc and wb.dtype == torch.bfloat16
+    call("kdfm_subsample_conv2", ptr(y1b), ptr(_i64(len2)), ptr(wb), ptr(_f32(b2)), ptr(_f32(y2)), B, T1, F1, Cc, _s())
+
+
 # ------------------------------------------------------------------------------------------------
 # conformer layer pieces
 # ------------------------------------------------------------------------------------------------

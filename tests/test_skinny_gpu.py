@@ -1,0 +1,124 @@
+"""GPU numerics of the weight-stationary skinny GEMM (csrc/skinny.hip) that kdfm_gemm selects for
+bf16 products with M >= 2048 rows: every encoder Linear / 1x1 conv (M = B*T' = 12,832 at the bench
+config), the KD heads (M = 16*B*T') and their data-gradients.  Reference: torch fp32 matmul of
+the SAME bf16-rounded operands (only the f32 accumulation order differs: tolerance 2e-3 of
+max |ref|).  Dropout masks are checked against the exact-f32 generic kernel (same counter RNG)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def K():
+    from kdfm import kernels
+    return kernels
+
+
+def _bf(t):
+    return t.to(torch.bfloat16).float()
+
+
+def _close(out, ref, rel=2e-3):
+    tol = rel * ref.abs().max().item() + 1e-6
+    err = (out - ref).abs().max().item()
+    assert err <= tol, f"max err {err:.3e} > tol {tol:.3e}"
+
+
+# (M, N, K): student / teacher encoder products (d = 88 / 176, FFN 4d, qkv 3d, pw1 2d), decoder,
+# ragged M, and K spanning several 96-wide chunks.
+SHAPES = [(12832, 88, 88), (12832, 352, 88), (12832, 88, 352), (12832, 264, 88), (12832, 176, 88),
+          (12832, 176, 176), (12832, 704, 176), (12832, 176, 704), (12832, 528, 176), (12832, 129, 88),
+          (2053, 40, 24), (4099, 96, 200)]
+
+
+@pytest.mark.parametrize("M,N,Kd", SHAPES)
+def test_skinny_linear(K, M, N, Kd):
+    from kdfm import _lib
+    g = torch.Generator(device="cuda").manual_seed(M + 3 * N + Kd)
+    x = torch.randn(M, Kd, device="cuda", generator=g)
+    W = torch.randn(N, Kd, device="cuda", generator=g) * 0.1
+    b = torch.randn(N, device="cuda", generator=g)
+    y = torch.empty(M, N, device="cuda")
+    K.linear(x, W, b, y, epi=_lib.EPI_SILU, math="bf16")
+    h = _bf(x) @ _bf(W).T + b
+    _close(y, torch.nn.functional.silu(h))
+    # residual epilogue (out = R + rscale * (xW^T + b))
+    R = torch.randn(M, N, device="cuda", generator=g)
+    K.linear(x, W, b, y, R=R, rscale=0.5, epi=_lib.EPI_RESID, math="bf16")
+    _close(y, R + 0.5 * h)
+
+
+@pytest.mark.parametrize("M,N,Kd", SHAPES[:9])
+def test_skinny_linear_dx(K, M, N, Kd):
+    """dx = dy @ W with B contiguous along n (XC), dSiLU epilogue"""
+    from kdfm import _lib
+    g = torch.Generator(device="cuda").manual_seed(7 * M + N + Kd)
+    W = torch.randn(N, Kd, device="cuda", generator=g) * 0.1
+    dy = torch.randn(M, N, device="cuda", generator=g)
+    aux = torch.randn(M, Kd, device="cuda", generator=g)
+    dx = torch.empty(M, Kd, device="cuda")
+    K.linear_dx(dy, W, dx, epi=_lib.EPI_DSILU, aux=aux, math="bf16")
+    s = torch.sigmoid(aux)
+    _close(dx, (_bf(dy) @ _bf(W)) * s * (1 + aux * (1 - s)))
+
+
+def test_skinny_strided_views(K):
+    """A as a column slice of a wider row-major buffer (qkv[:, d:]-style views) and C strided."""
+    g = torch.Generator(device="cuda").manual_seed(11)
+    M, d = 12832, 88
+    big = torch.randn(M, 3 * d, device="cuda", generator=g)
+    x = big[:, d:2 * d]
+    W = torch.randn(d, d, device="cuda", generator=g) * 0.1
+    outbig = torch.zeros(M, 2 * d, device="cuda")
+    y = outbig[:, d:]
+    K.linear(x, W, None, y, math="bf16")
+    _close(y, _bf(x) @ _bf(W).T)
+    assert outbig[:, :d].abs().max().item() == 0.0
+
+
+def test_skinny_dropout_matches_generic(K):
+    """The counter-RNG dropout mask depends only on (seed, stream, row, col): the skinny bf16 path
+    and the generic exact-f32 path must drop exactly the same elements."""
+    from kdfm import _lib
+    g = torch.Generator(device="cuda").manual_seed(3)
+    M, N, Kd = 12832, 352, 88
+    x = torch.randn(M, Kd, device="cuda", generator=g)
+    W = torch.randn(N, Kd, device="cuda", generator=g) * 0.1
+    b = torch.randn(N, device="cuda", generator=g) + 3.0     # keep SiLU outputs away from 0
+    seed = torch.tensor([12345], dtype=torch.int64, device="cuda")
+    pre_bf = torch.empty(M, N, device="cuda")
+    y_bf = torch.empty(M, N, device="cuda")
+    K.linear(x, W, b, y_bf, epi=_lib.EPI_SILU | _lib.EPI_STORE_PRE, Cpre=pre_bf, dropout_p=0.1, seed=seed,
+             rng_stream=77, math="bf16")
+    pre_f = torch.empty(M, N, device="cuda")
+    y_f = torch.empty(M, N, device="cuda")
+    K.linear(x, W, b, y_f, epi=_lib.EPI_SILU | _lib.EPI_STORE_PRE, Cpre=pre_f, dropout_p=0.1, seed=seed,
+             rng_stream=77, math="f32")
+    assert torch.equal(y_bf == 0, y_f == 0)
+    frac = (y_bf == 0).float().mean().item()
+    assert 0.08 < frac < 0.12
+    _close(pre_bf, _bf(x) @ _bf(W).T + b)
+    _close(y_bf, y_f, rel=1e-2)
+
+
+def test_skinny_rowmask_and_mse(K):
+    g = torch.Generator(device="cuda").manual_seed(4)
+    U, T, N, Kd = 32, 401, 96, 96
+    M = U * T
+    x = torch.randn(M, Kd, device="cuda", generator=g)
+    W = torch.randn(N, Kd, device="cuda", generator=g) * 0.1
+    b = torch.randn(N, device="cuda", generator=g)
+    lens = torch.randint(100, T + 1, (U,), generator=torch.Generator().manual_seed(0)).to("cuda")
+    y = torch.empty(M, N, device="cuda")
+    K.linear(x, W, b, y, rowmask=(lens, T, 1), math="bf16")
+    ref = (_bf(x) @ _bf(W).T + b).view(U, T, N)
+    keep = (torch.arange(T, device="cuda")[None, :] < lens[:, None]).float()[..., None]
+    _close(y, (ref * keep).view(M, N))
+    tgt = torch.randn(M, N, device="cuda", generator=g)
+    acc = torch.zeros(1, device="cuda")
+    d = torch.empty(M, N, device="cuda")
+    K.linear(x, W, b, d, R=tgt, rscale=2.0 / (M * N), mse=(acc, 1.0 / (M * N)), math="bf16")
+    diff = _bf(x) @ _bf(W).T + b - tgt
+    _close(d, diff * 2.0 / (M * N))
+    assert abs(acc.item() - (diff ** 2).mean().item()) <= 1e-4 * (diff ** 2).mean().item()

@@ -1,0 +1,101 @@
+"""GPU numerics of the fused striding-subsampling forward (csrc/subsample.hip): direct conv1 with
+the frame masks of SURVEY.md A.3, and the implicit-GEMM conv2 (bf16 MFMA).  Reference: torch CPU
+f32 conv2d of the same (masked) inputs; conv2 is compared on the bf16-rounded operands it consumes
+(tolerance 2e-3 of max |ref|: f32 accumulation order only)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def K():
+    from kdfm import kernels
+    return kernels
+
+
+def _bf(t):
+    return t.to(torch.bfloat16).float()
+
+
+def _lens(L):
+    return (L - 1) // 2 + 1
+
+
+@pytest.mark.parametrize("C", [88, 176, 32, 64])
+def test_subsample_fused_forward(K, C):
+    g = torch.Generator().manual_seed(C)
+    B, Tm, Fq = 3, 57, 80
+    mel = torch.randn(B, Tm, Fq, generator=g)
+    mel_len = torch.tensor([Tm, 40, 23], dtype=torch.int64)
+    len1 = _lens(mel_len)
+    len2 = _lens(len1)
+    w0 = torch.randn(C, 1, 3, 3, generator=g) * 0.3
+    b0 = torch.randn(C, generator=g) * 0.1
+    w2 = torch.randn(C, C, 3, 3, generator=g) * (1.0 / (3 * C ** 0.5))
+    b2 = torch.randn(C, generator=g) * 0.1
+    T1, F1 = _lens(Tm), _lens(Fq)
+    T2, F2 = _lens(T1), _lens(F1)
+
+    # reference (CPU f32)
+    x = mel.clone()
+    for b in range(B):
+        x[b, mel_len[b]:] = 0
+    y1 = F.relu(F.conv2d(x[:, None], w0, b0, stride=2, padding=1))          # (B, C, T1, F1)
+    for b in range(B):
+        y1[b, :, len1[b]:] = 0
+    y2 = F.relu(F.conv2d(_bf(y1), _bf(w2), b2, stride=2, padding=1))       # (B, C, T2, F2)
+    for b in range(B):
+        y2[b, :, len2[b]:] = 0
+
+    dev = "cuda"
+    y1b = torch.empty(B * T1 * F1, C, device=dev, dtype=torch.bfloat16)
+    y1f = torch.empty(B * T1 * F1, C, device=dev)
+    K.subsample_conv1(mel.to(dev), mel_len.to(dev), len1.to(dev), w0.to(dev), b0.to(dev), y1b, y1f, B, Tm, Fq, C)
+    y1_ref = y1.permute(0, 2, 3, 1).reshape(B * T1 * F1, C)
+    torch.testing.assert_close(y1f.cpu(), y1_ref, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(y1b.float().cpu(), _bf(y1_ref), rtol=1e-2, atol=1e-2)
+
+    wb = torch.empty(K.subsample_wprep_elems(C), device=dev, dtype=torch.bfloat16)
+    K.subsample_wprep(w2.to(dev), wb)
+    out = torch.full((B * T2 * F2, C), float("nan"), device=dev)
+    # feed the exact bf16 y1 of the reference so only accumulation order differs
+    K.subsample_conv2(_bf(y1_ref).to(torch.bfloat16).to(dev), len2.to(dev), wb, b2.to(dev), out, B, T1, F1, C)
+    ref = y2.permute(0, 2, 3, 1).reshape(B * T2 * F2, C)
+    err = (out.cpu() - ref).abs().max().item()
+    assert err <= 2e-3 * ref.abs().max().item() + 1e-6, err
+
+
+def test_subsample_bench_shape_matches_im2col_path(K):
+    """The fused path and the im2col+GEMM path (kept for f32 parity mode) agree at the bench shape
+    of one utterance (T_mel = 1601, d = 176)."""
+    from kdfm import _lib
+    g = torch.Generator(device="cuda").manual_seed(0)
+    B, Tm, Fq, C = 2, 1601, 80, 176
+    dev = "cuda"
+    mel = torch.randn(B, Tm, Fq, device=dev, generator=g)
+    mel_len = torch.tensor([Tm, 1000], dtype=torch.int64, device=dev)
+    len1 = (mel_len - 1) // 2 + 1
+    len2 = (len1 - 1) // 2 + 1
+    w0 = torch.randn(C, 9, device=dev, generator=g) * 0.3
+    b0 = torch.randn(C, device=dev, generator=g) * 0.1
+    w2 = torch.randn(C, C, 9, device=dev, generator=g) * 0.02
+    b2 = torch.randn(C, device=dev, generator=g) * 0.1
+    T1, F1 = _lens(Tm), _lens(Fq)
+    T2, F2 = _lens(T1), _lens(F1)
+    y1b = torch.empty(B * T1 * F1, C, device=dev, dtype=torch.bfloat16)
+    y1f = torch.empty(B * T1 * F1, C, device=dev)
+    K.subsample_conv1(mel, mel_len, len1, w0, b0, y1b, y1f, B, Tm, Fq, C)
+    wb = torch.empty(K.subsample_wprep_elems(C), device=dev, dtype=torch.bfloat16)
+    K.subsample_wprep(w2, wb)
+    y2 = torch.empty(B * T2 * F2, C, device=dev)
+    K.subsample_conv2(y1b, len2, wb, b2, y2, B, T1, F1, C)
+    # im2col path on the same bf16 y1
+    cols1 = torch.empty(B * T2 * F2, 9 * C, device=dev)
+    K.im2col_3x3s2(y1b.float().contiguous(), len1, cols1, B, T1, F1, C)
+    ref = torch.empty_like(y2)
+    K.linear(cols1, w2.view(C, 9 * C), b2, ref, epi=_lib.EPI_RELU, rowmask=(len2, T2, F2), math="f32")
+    # the f32 path sees f32 weights; the fused path bf16 weights -> bf16-level tolerance
+    err = (y2 - ref).abs().max().item()
+    assert err <= 1e-2 * ref.abs().max().item(), err
