@@ -111,9 +111,24 @@ typedef struct kdfm_gemm_desc {
    * of split-K atomics.  NULL / too small -> generic path.  kdfm_gemm_ws() gives the size used. */
   float* ws;
   int64_t ws_len;
+  /* optional bf16 twin of the B operand (bf16 math only): B(k, n) ~= Bh[n*sBh + k], one row per
+   * output column, contiguous along k — a weight's [out][in] layout for forward products or its
+   * transpose for data gradients (kdfm_cast_bf16 / kdfm_cast_bf16_t build them once per step).
+   * When set, skinny products stream B fragments straight from it instead of staging f32 weights
+   * through LDS in every workgroup.  NULL: not used. */
+  const uint16_t* Bh;
+  int64_t sBh;
 } kdfm_gemm_desc;
 
 int kdfm_gemm(const kdfm_gemm_desc* d, void* stream);
+/* bf16 weight twins (once per step, before the GEMMs that read them):
+ *   kdfm_cast_bf16:   dst[i] = bf16(src[i]), i < n  (same layout as the f32 flat parameter buffer)
+ *   kdfm_cast_bf16_t: per table entry e = (offset, rows, cols, first_block) (device int64 [ntab][4]):
+ *     dst[offset + c*rows + r] = bf16(src[offset + r*cols + c]) — each 2-D weight transposed in
+ *     place of itself; first_block = prefix sum of ceil(rows*cols/256); nblocks = total. */
+int kdfm_cast_bf16(const float* src, uint16_t* dst, int64_t n, void* stream);
+int kdfm_cast_bf16_t(const float* src, uint16_t* dst, const int64_t* table, int64_t ntab, int64_t nblocks,
+                     void* stream);
 int64_t kdfm_gemm_ws(const kdfm_gemm_desc* d); /* workspace elements kdfm_gemm would use (0: none) */
 
 /* column sums: out[n] (+)= scale * sum_m X[m*ld + n], m < M; accumulate != 0 adds into out.

@@ -399,6 +399,7 @@ extern "C" int kdfm_gemm(const kdfm_gemm_desc* d, void* stream) {
   p.loss_acc = d->loss_acc; p.loss_scale = d->loss_scale;
   p.ones_out = d->ones_out; p.ones_col = d->ones_col;
   p.ws = d->ws; p.ws_len = d->ws_len;
+  p.Bh = d->Bh; p.sBh = d->sBh;
   if (d->ones_col >= 0)
     KDFM_REQUIRE(d->ones_out && (d->epi & KDFM_EPI_ATOMIC) && d->ones_col == d->N - 1 && d->batch1 == 1 &&
                      d->batch2 == 1,
@@ -433,5 +434,6 @@ extern "C" int64_t kdfm_gemm_ws(const kdfm_gemm_desc* d) {
   p.sAm = d->sAm; p.sAk = d->sAk; p.sBk = d->sBk; p.sBn = d->sBn; p.sCm = d->sCm; p.sCn = d->sCn;
   p.epi = d->epi; p.splitk = d->splitk; p.taps = d->conv_taps; p.pad = d->conv_pad;
   p.conv_c = d->conv_c; p.conv_t = d->conv_t; p.ones_col = d->ones_col; p.ones_out = d->ones_out;
+  p.Bh = nullptr; p.sBh = 0;
   return rowstream_wgrad_ws(p, d->amode, d->bmode, d->batch1 * d->batch2);
 }

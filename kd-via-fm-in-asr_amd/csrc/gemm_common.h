@@ -25,6 +25,7 @@ struct GemmP {
   float* loss_acc; float loss_scale;
   float* ones_out; int64_t ones_col;
   float* ws; int64_t ws_len;
+  const uint16_t* Bh; int64_t sBh;
 };
 
 // Non-atomic epilogue for one output element.  v = alpha * acc (already scaled).  bz = batch

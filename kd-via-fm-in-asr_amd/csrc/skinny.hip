@@ -280,6 +280,130 @@ __global__ __launch_bounds__(64 * WV, 2) void sk_fwd_kernel(GemmP p, SkGeo g) {
   }
 }
 
+// Direct-B variant (p.Bh set): no LDS at all.  Work items are (32-row tile, column group) pairs
+// spread over every wave of the grid; B fragments are 16-byte loads from the bf16 weight twin
+// (L2-resident), issued together with the A loads, so a K <= 96 product is one memory round trip
+// per wave plus the epilogue.  Waves of one workgroup take the column groups of the same row tile,
+// so the repeated A rows hit L1/L2.
+template <int NCT, int AMODE>
+__global__ __launch_bounds__(256, 2) void skd_fwd_kernel(GemmP p, SkGeo g, int G) {
+  const int lane = threadIdx.x & 63;
+  const int r = lane & 31, h = lane >> 5;
+  const int64_t wglob = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t wstride = (int64_t)gridDim.x * 4;
+  const int64_t ntasks = g.tiles * G;
+  if (wglob >= ntasks) return;
+  const int64_t nmine = (ntasks - wglob + wstride - 1) / wstride;
+  const int64_t nsteps = nmine * g.nchunks;
+
+  const int epi = p.epi;
+  const uint64_t seed = (epi & KDFM_EPI_DROPOUT) ? load_seed(p.seed) : 0ull;
+  const float keep_scale = (epi & KDFM_EPI_DROPOUT) ? 1.f / (1.f - p.dropout_p) : 1.f;
+  bool single;
+  const float* side = epi_side_src(p, single);
+  float mse_part = 0.f;
+
+  f32x16 acc[NCT];
+  float4 av[SK_CKS][2];
+  int64_t task = wglob;
+  sk_load_A<AMODE>(av, p, g, (task / G) * 32, 0, lane);
+  int c = 0;
+  for (int64_t q = 0; q < nsteps; ++q) {
+    const bool last = (c == g.nchunks - 1);
+    const int64_t m0 = (task / G) * 32;
+    const int64_t n0 = (int64_t)(task % G) * 32 * NCT;
+    const int kimg = c * g.chunk;
+    // B fragments of this chunk (bf16 twin, row n contiguous along k)
+    bf16x8 bfr[SK_CKS][NCT];
+#pragma unroll
+    for (int s = 0; s < SK_CKS; ++s)
+#pragma unroll
+      for (int j = 0; j < NCT; ++j) {
+        const int64_t n = n0 + 32 * j + r;
+        const int k = kimg + 16 * s + 8 * h;
+        if (16 * s < g.chunk && n < p.N && k < p.K)
+          bfr[s][j] = *reinterpret_cast<const bf16x8*>(p.Bh + n * p.sBh + k);
+        else
+          bfr[s][j] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      }
+    bf16x8 af[SK_CKS];
+#pragma unroll
+    for (int s = 0; s < SK_CKS; ++s) af[s] = cvt8(av[s][0], av[s][1]);
+    {
+      int c2 = c + 1;
+      int64_t t2 = task;
+      if (c2 == g.nchunks) { c2 = 0; t2 += wstride; }
+      if (q + 1 < nsteps) sk_load_A<AMODE>(av, p, g, (t2 / G) * 32, c2, lane);
+    }
+    if (c == 0) {
+#pragma unroll
+      for (int j = 0; j < NCT; ++j)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[j][i] = 0.f;
+    }
+#pragma unroll
+    for (int s = 0; s < SK_CKS; ++s)
+#pragma unroll
+      for (int j = 0; j < NCT; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[s], bfr[s][j], acc[j], 0, 0, 0);
+    if (last) {
+      // side operands after the MFMAs: their latency overlaps the A prefetch already in flight
+      float sv[NCT][16], bn[NCT];
+      bool rowok[16];
+#pragma unroll
+      for (int j = 0; j < NCT; ++j) {
+        const int64_t n = n0 + 32 * j + r;
+        bn[j] = ((epi & KDFM_EPI_BIAS) && n < p.N) ? p.bias[n] : 0.f;
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int64_t m = m0 + (i & 3) + 8 * (i >> 2) + 4 * h;
+        rowok[i] = m < p.M && epi_row_ok(p, m < p.M ? m : 0);
+      }
+      if (side) {
+#pragma unroll
+        for (int j = 0; j < NCT; ++j) {
+          const int64_t n = n0 + 32 * j + r;
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int64_t m = m0 + (i & 3) + 8 * (i >> 2) + 4 * h;
+            sv[j][i] = (m < p.M && n < p.N) ? side[m * p.sCm + n * p.sCn] : 0.f;
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < NCT; ++j) {
+        const int64_t n = n0 + 32 * j + r;
+        const bool nok = n < p.N;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int64_t m = m0 + (i & 3) + 8 * (i >> 2) + 4 * h;
+          if (!nok || m >= p.M) continue;
+          float pre = 0.f;
+          const float v = epi_apply(p, 0, m, n, p.alpha * acc[j][i], bn[j], side ? sv[j][i] : 0.f, rowok[i], seed,
+                                    keep_scale, mse_part, pre);
+          const int64_t off = m * p.sCm + n * p.sCn;
+          if (epi & KDFM_EPI_STORE_PRE) p.Cpre[off] = pre;
+          p.C[off] = v;
+        }
+      }
+      c = 0;
+      task += wstride;
+    } else {
+      ++c;
+    }
+  }
+  if (epi & KDFM_EPI_MSE) {
+    mse_part = wave_sum(mse_part);
+    if (lane == 0) atomicAdd(p.loss_acc, mse_part * p.loss_scale);
+  }
+}
+
+template <int NCT, int AMODE>
+int skd_launch(const GemmP& p, const SkGeo& g, int G, int64_t gx, hipStream_t st) {
+  hipLaunchKernelGGL((skd_fwd_kernel<NCT, AMODE>), dim3((unsigned)gx), dim3(256), 0, st, p, g, G);
+  return check_launch("kdfm_gemm(skinny direct)");
+}
+
 template <int NCT, int AMODE, int WV>
 int sk_launch(const GemmP& p, const SkGeo& g, int64_t gx, int64_t ncr, size_t lds, hipStream_t st) {
   if (lds > 64 * 1024) {
@@ -317,7 +441,7 @@ int try_skinny_fwd(const GemmP& p, int amode, int bmode, int64_t batch, hipStrea
   static const int target_wgs = env_int("KDFM_SKINNY_WGS", 512);
   if (!enabled) return -1;
   if (batch != 1 || p.splitk != 1 || (p.epi & KDFM_EPI_ATOMIC) || p.ones_col >= 0) return -1;
-  if (p.M < min_m || p.N <= 0 || p.K <= 0) return -1;
+  if (p.N <= 0 || p.K <= 0) return -1;
   if (bmode != KDFM_LD_KC && bmode != KDFM_LD_XC) return -1;
   if (p.sAk != 1 || (p.sAm & 3) || (((uintptr_t)p.A) & 15)) return -1;
   bool single;
@@ -336,6 +460,33 @@ int try_skinny_fwd(const GemmP& p, int amode, int bmode, int64_t batch, hipStrea
   } else {
     return -1;
   }
+  if (p.Bh && (p.K & 7) == 0 && (p.sBh & 7) == 0 && ((((uintptr_t)p.Bh) & 15) == 0)) {
+    // measured slower than the generic 64x64 kernel on the 12,832-row encoder products
+    // (fragment-shaped global loads, tools/shape_micro.py): opt-in only
+    static const int direct_min_m = env_int("KDFM_SKINNY_DIRECT_MIN_M", 1 << 30);
+    static const int direct_wgs = env_int("KDFM_SKINNY_DIRECT_WGS", 1024);
+    if (p.M >= direct_min_m) {
+      g.tiles = ceil_div(p.M, 32);
+      const int64_t nt32 = ceil_div(p.N, 32);
+      const int nct = nt32 <= 3 ? (int)nt32 : (nt32 % 3 == 0 || nt32 % 2 == 1) ? 3 : 2;
+      const int G = (int)ceil_div(nt32, nct);
+      int64_t gx = ceil_div(g.tiles * G, 4);
+      if (gx > direct_wgs) gx = direct_wgs;
+      if (amode == KDFM_LD_CONV) {
+        switch (nct) {
+          case 1: return skd_launch<1, KDFM_LD_CONV>(p, g, G, gx, st);
+          case 2: return skd_launch<2, KDFM_LD_CONV>(p, g, G, gx, st);
+          default: return skd_launch<3, KDFM_LD_CONV>(p, g, G, gx, st);
+        }
+      }
+      switch (nct) {
+        case 1: return skd_launch<1, KDFM_LD_KC>(p, g, G, gx, st);
+        case 2: return skd_launch<2, KDFM_LD_KC>(p, g, G, gx, st);
+        default: return skd_launch<3, KDFM_LD_KC>(p, g, G, gx, st);
+      }
+    }
+  }
+  if (p.M < min_m) return -1;
   g.Kp = (int)(ceil_div(p.K, 16) * 16);
   if (amode == KDFM_LD_KC) {
     // the last chunk may read image columns up to nchunks*96 - 1: pad the image to that

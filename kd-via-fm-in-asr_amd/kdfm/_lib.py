@@ -54,6 +54,7 @@ class GemmDesc(C.Structure):
         ("loss_acc", _vp), ("loss_scale", _f32),
         ("ones_out", _vp), ("ones_col", _i64),
         ("ws", _vp), ("ws_len", _i64),
+        ("Bh", _vp), ("sBh", _i64),
     ]
 
 
@@ -66,6 +67,8 @@ SIGNATURES: dict[str, tuple] = {
     "kdfm_device_arch": (_i32, [C.c_char_p, _i64]),
     "kdfm_gemm": (_i32, [C.POINTER(GemmDesc), P]),
     "kdfm_gemm_ws": (_i64, [C.POINTER(GemmDesc)]),
+    "kdfm_cast_bf16": (_i32, [P, P, _i64, P]),
+    "kdfm_cast_bf16_t": (_i32, [P, P, P, _i64, _i64, P]),
     "kdfm_colsum": (_i32, [P, P, _i64, _i64, _i64, _f32, _i32, P]),
     "kdfm_preemph_pad": (_i32, [P, P, P, _i64, _i64, _i64, _f32, _f32, P, C.c_uint64, P]),
     "kdfm_power_spectrum": (_i32, [P, P, _i64, _i64, P]),

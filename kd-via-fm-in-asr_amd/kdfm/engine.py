@@ -42,6 +42,9 @@ class Ver5Engine:
         self.lr = torch.zeros(1, device=dev)
         self.losses = torch.zeros(5, device=dev)                     # total, ctc, kl, recon, fm
         self.hws = HeadsWorkspace(cfg, dev)
+        if K.twins_enabled():   # opt-in direct-B skinny path (KDFM_SKINNY_DIRECT_MIN_M)
+            self.student.enable_bf16_twins()
+            self.teacher.enable_bf16_twins()
         self._pos = {}
         self._ws = {}
         if init:
@@ -100,6 +103,9 @@ class Ver5Engine:
         len2 = torch.empty_like(mel_len)
         K.subsample_lengths(wav_len, mel_len, len1, len2, cfg.hop)
         seed = self.seed
+        if K.get_math() == "bf16":   # bf16 twins of the weights the skinny products stream
+            self.student.refresh_bf16()
+            self.teacher.refresh_bf16()
         # ---- frontends (teacher preprocessor is in eval mode: no dither) ----
         dither = cfg.dither if train else 0.0
         mel_t = frontend_forward(cfg, self.fe, wav, wav_len, mel_len, dither=0.0)

@@ -36,10 +36,12 @@ class HeadsWorkspace:
 
     def __init__(self, cfg: Ver5Config, dev):
         L, E, S = cfg.latent, cfg.time_embed_dim, cfg.fm_steps
-        self.w1f = _empty(L, 3 * L, dev=dev)
-        self.w1b = _empty(L, 3 * L, dev=dev)
-        self.w2f = _empty(L, 3 * L, dev=dev)
-        self.w2b = _empty(L, 3 * L, dev=dev)
+        self.wconv = _empty(4, L, 3 * L, dev=dev)      # denoiser conv weights in GEMM layouts
+        self.w1f, self.w1b, self.w2f, self.w2b = self.wconv.unbind(0)
+        self.wconv_h = None
+        if K.twins_enabled():
+            self.wconv_h = torch.empty(4, L, 3 * L, device=dev, dtype=torch.bfloat16)
+            K.register_bf16_twin(self.wconv, self.wconv_h)
         self.g1 = _empty(L, 3 * L, dev=dev)
         self.g2 = _empty(L, 3 * L, dev=dev)
         self.cvec = _empty(S, L, dev=dev)
@@ -77,6 +79,8 @@ def heads_forward(cfg: Ver5Config, P, s_feats, t_feats, T, ws: HeadsWorkspace, a
     # ---- SimpleDenoiser: x <- x - net(x)/steps ----
     K.convw_prep(P["denoiser.net.0.weight"], fwd=ws.w1f, bwd=ws.w1b)
     K.convw_prep(P["denoiser.net.2.weight"], fwd=ws.w2f, bwd=ws.w2b)
+    if K.get_math() == "bf16" and ws.wconv_h is not None:
+        K.cast_bf16(ws.wconv, ws.wconv_h)
     ds = cfg.denoiser_steps
     xs = [zn]
     acts = []

@@ -107,11 +107,83 @@ def scratch(dev, nfloats: int):
 # GEMM
 # ------------------------------------------------------------------------------------------------
 
+# ------------------------------------------------------------------------------------------------
+# bf16 weight twins (kdfm_gemm_desc.Bh): an f32 parameter buffer registered here has a bf16 copy
+# in the same layout (forward products read W[n][k] rows) and, for every 2-D weight, a transposed
+# copy at the same offset (data-gradient products read W^T rows).  The owner refreshes them with
+# cast_bf16 / cast_bf16_t whenever the f32 values change (the engine: at the top of every step).
+# ------------------------------------------------------------------------------------------------
+
+class _Twin:
+    def __init__(self, src, h, ht, entries):
+        import weakref
+        self.src = weakref.ref(src)
+        self.base = src.data_ptr()
+        self.end = self.base + 4 * src.numel()
+        self.h, self.ht = h, ht
+        self.entries = sorted(entries)              # (offset, rows, cols) of the transposed images
+        self.starts = [e[0] for e in self.entries]
+
+
+_TWINS: list = []
+
+
+def twins_enabled() -> bool:
+    """The direct-B skinny path that reads the twins is opt-in (KDFM_SKINNY_DIRECT_MIN_M)."""
+    import os
+    return bool(os.environ.get("KDFM_SKINNY_DIRECT_MIN_M"))
+
+
+def register_bf16_twin(src, h, ht=None, entries=()):
+    """src: f32 flat buffer; h: bf16 copy (same numel); ht: bf16 per-entry transposes or None."""
+    assert src.dtype == torch.float32 and h.dtype == torch.bfloat16 and h.numel() == src.numel()
+    _TWINS[:] = [t for t in _TWINS if t.src() is not None]
+    _TWINS.append(_Twin(src, h, ht, entries))
+
+
+def bf16_twin(W, transposed=False):
+    """(device pointer, row stride) of the bf16 twin of weight view W — rows = W's rows (forward,
+    B(k,n) = W[n][k]) or W's columns (transposed: B(k,n) = W[k][n]) — or None."""
+    import bisect
+    if W.dim() != 2 or W.stride(1) != 1:
+        return None
+    p = W.data_ptr()
+    for t in _TWINS:
+        if not (t.base <= p < t.end) or t.src() is None:
+            continue
+        off = (p - t.base) // 4
+        if not transposed:
+            return t.h.data_ptr() + 2 * off, W.stride(0)
+        if t.ht is None:
+            return None
+        i = bisect.bisect_right(t.starts, off) - 1
+        if i < 0:
+            return None
+        eoff, rows, cols = t.entries[i]
+        rel = off - eoff
+        r0, c0 = divmod(rel, cols)
+        if rel >= rows * cols or W.stride(0) != cols or r0 + W.shape[0] > rows or c0 + W.shape[1] > cols:
+            return None
+        return t.ht.data_ptr() + 2 * (eoff + c0 * rows + r0), rows
+    return None
+
+
+def cast_bf16(src, dst):
+    assert src.is_contiguous() and dst.is_contiguous() and src.numel() == dst.numel()
+    call("kdfm_cast_bf16", ptr(_f32(src)), ptr(dst), src.numel(), _s())
+
+
+def cast_bf16_t(src, dst, table, ntab, nblocks):
+    call("kdfm_cast_bf16_t", ptr(_f32(src)), ptr(dst), ptr(table), int(ntab), int(nblocks), _s())
+
+
 def gemm(A, B, Cout, M, N, K, sAm, sAk, sBk, sBn, sCm, sCn, *, amode, bmode,
          batch=(1, 1), bA=(0, 0), bB=(0, 0), bC=(0, 0), alpha=1.0, epi=0, bias=None, R=None, rscale=1.0,
          aux=None, Cpre=None, beta=0.0, dropout_p=0.0, seed=None, rng_stream=0, splitk=1,
-         conv=None, math=None, rowmask=None, mse=None, tag=None, ones_out=None):
+         conv=None, math=None, rowmask=None, mse=None, tag=None, ones_out=None, Bh=None):
     d = GemmDesc()
+    if Bh is not None and (math or _State.math) == "bf16":
+        d.Bh, d.sBh = Bh
     d.ones_col = -1
     if ones_out is not None:
         d.ones_out, d.ones_col = ptr(ones_out), int(N) - 1
@@ -177,7 +249,7 @@ def linear(x, W, bias, out, *, epi=0, R=None, rscale=1.0, Cpre=None, dropout_p=0
     gemm(x, W, out, M, N, K, x.stride(0), x.stride(1), W.stride(1), W.stride(0), out.stride(0), out.stride(1),
          amode=_lib.LD_KC, bmode=_lib.LD_KC, epi=epi, bias=bias, R=R, rscale=rscale, Cpre=Cpre,
          dropout_p=dropout_p, seed=seed, rng_stream=rng_stream, alpha=alpha, math=math, rowmask=rowmask, mse=mse,
-         tag=tag)
+         tag=tag, Bh=bf16_twin(W) if _TWINS else None)
 
 
 def linear_dx(dy, W, dx, *, epi=0, aux=None, dropout_p=0.0, seed=None, rng_stream=0, R=None, rscale=1.0,
@@ -190,7 +262,8 @@ def linear_dx(dy, W, dx, *, epi=0, aux=None, dropout_p=0.0, seed=None, rng_strea
         epi |= _lib.EPI_RESID
     gemm(dy, W, dx, M, K, N, dy.stride(0), dy.stride(1), W.stride(0), W.stride(1), dx.stride(0), dx.stride(1),
          amode=_lib.LD_KC, bmode=_lib.LD_XC, epi=epi, aux=aux, dropout_p=dropout_p, seed=seed,
-         rng_stream=rng_stream, R=R, rscale=rscale, alpha=alpha, math=math)
+         rng_stream=rng_stream, R=R, rscale=rscale, alpha=alpha, math=math,
+         Bh=bf16_twin(W, transposed=True) if _TWINS else None)
 
 
 def linear_dw(dy, x, dW, *, alpha=1.0, math=None, db=None):
@@ -217,7 +290,7 @@ def conv3(x, Wf, bias, out, T, *, epi=0, R=None, rscale=1.0, alpha=1.0, aux=None
         epi |= _lib.EPI_RESID
     gemm(x, Wf, out, M, O, 3 * Cc, x.stride(0), 1, 1, Wf.stride(0), out.stride(0), out.stride(1),
          amode=_lib.LD_CONV, bmode=_lib.LD_KC, epi=epi, bias=bias, R=R, rscale=rscale, alpha=alpha, aux=aux,
-         conv=(3, 1, Cc, T), math=math)
+         conv=(3, 1, Cc, T), math=math, Bh=bf16_twin(Wf) if _TWINS else None)
 
 
 def conv3_dw(dy, x, G, T, *, alpha=1.0, math=None, db=None):

@@ -53,6 +53,47 @@ class FlatStore:
             if self.grad is not None:
                 self.G[fname] = self.grad[o:o + n].view(fshape)
 
+    # ---- bf16 twins for the bf16 GEMM path (kernels.bf16_twin) ----
+    def enable_bf16_twins(self) -> None:
+        """Allocate and register the bf16 copy of the buffer and the per-weight transposed copy
+        (2-D weights and fused groups as units); refresh_bf16() fills them."""
+        if getattr(self, "h", None) is not None:
+            return
+        shapes = dict(self.specs)
+        fused = fused_groups(self.specs)
+        members = set()
+        entries = []
+        for fname, (first, count, fshape) in fused.items():
+            names = [n for n, _ in self.specs]
+            i0 = names.index(first)
+            members.update(names[i0:i0 + count])
+            if len(fshape) == 2:
+                entries.append((self.offsets[first], fshape[0], fshape[1]))
+        for name, shape in self.specs:
+            if name in members or not name.endswith(".weight") or len(shape) < 2:
+                continue
+            if _numel(shape[2:]) != 1 or shape[0] * shape[1] < 64:
+                continue
+            entries.append((self.offsets[name], int(shape[0]), int(shape[1])))
+        entries.sort()
+        tab = []
+        blk = 0
+        for off, r, c in entries:
+            tab.append((off, r, c, blk))
+            blk += -(-(r * c) // 256)
+        self.h = torch.zeros(self.numel, device=self.device, dtype=torch.bfloat16)
+        self.ht = torch.zeros(self.numel, device=self.device, dtype=torch.bfloat16)
+        self._ttab = torch.tensor(tab, dtype=torch.int64, device=self.device)
+        self._tblocks = blk
+        K.register_bf16_twin(self.data, self.h, self.ht, entries)
+
+    def refresh_bf16(self) -> None:
+        if getattr(self, "h", None) is None:
+            return
+        K.cast_bf16(self.data, self.h)
+        if self._tblocks:
+            K.cast_bf16_t(self.data, self.ht, self._ttab, self._ttab.shape[0], self._tblocks)
+
     @property
     def trainable_count(self) -> int:
         return sum(_numel(s) for _, s in self.specs)

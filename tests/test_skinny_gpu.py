@@ -122,3 +122,72 @@ def test_skinny_rowmask_and_mse(K):
     diff = _bf(x) @ _bf(W).T + b - tgt
     _close(d, diff * 2.0 / (M * N))
     assert abs(acc.item() - (diff ** 2).mean().item()) <= 1e-4 * (diff ** 2).mean().item()
+
+
+def _twin_buffer(shapes, seed):
+    """A flat f32 buffer holding weights of the given 2-D shapes, with registered bf16 twins
+    (same layout + per-weight transposes), like FlatStore.enable_bf16_twins."""
+    from kdfm import kernels as Kk
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    offs, off = [], 0
+    for r, c in shapes:
+        offs.append(off)
+        off += -(-(r * c) // 4) * 4
+    src = torch.randn(off, device="cuda", generator=g) * 0.1
+    h = torch.empty(off, device="cuda", dtype=torch.bfloat16)
+    ht = torch.empty(off, device="cuda", dtype=torch.bfloat16)
+    entries = [(o, r, c) for o, (r, c) in zip(offs, shapes)]
+    tab, blk = [], 0
+    for o, r, c in entries:
+        tab.append((o, r, c, blk))
+        blk += -(-(r * c) // 256)
+    Kk.register_bf16_twin(src, h, ht, entries)
+    Kk.cast_bf16(src, h)
+    Kk.cast_bf16_t(src, ht, torch.tensor(tab, dtype=torch.int64, device="cuda"), len(tab), blk)
+    Ws = [src[o:o + r * c].view(r, c) for o, (r, c) in zip(offs, shapes)]
+    return src, h, ht, Ws
+
+
+@pytest.mark.parametrize("M", [12832, 205312 // 4, 3001])
+def test_skinny_direct_twins(K, M):
+    """Forward (B = W rows) and data-gradient (B = W^T rows) products reading the bf16 twins, incl.
+    a column-slice view (W1[:, :96] of a (96, 128) weight, the FM meta-encoder's x part)."""
+    from kdfm import _lib
+    d = 88
+    shapes = [(4 * d, d), (d, 4 * d), (3 * d, d), (129, d), (96, 128), (96, 176)]
+    src, h, ht, Ws = _twin_buffer(shapes, M)
+    assert torch.equal(h.float(), _bf(src))
+    g = torch.Generator(device="cuda").manual_seed(1)
+    for W in Ws[:4] + [Ws[4][:, :96], Ws[5]]:
+        N, Kd = W.shape
+        x = torch.randn(M, Kd, device="cuda", generator=g)
+        b = torch.randn(N, device="cuda", generator=g)
+        R = torch.randn(M, N, device="cuda", generator=g)
+        y = torch.empty(M, N, device="cuda")
+        K.linear(x, W, b, y, R=R, rscale=-0.25, epi=_lib.EPI_RESID, math="bf16")
+        _close(y, R - 0.25 * (_bf(x) @ _bf(W).T + b))
+        dy = torch.randn(M, N, device="cuda", generator=g)
+        aux = torch.randn(M, Kd, device="cuda", generator=g)
+        dx = torch.empty(M, Kd, device="cuda")
+        K.linear_dx(dy, W, dx, epi=_lib.EPI_DRELU, aux=aux, alpha=0.5, math="bf16")
+        _close(dx, torch.where(aux > 0, 0.5 * (_bf(dy) @ _bf(W)), torch.zeros_like(aux)))
+    del src
+
+
+def test_skinny_direct_conv3_twin(K):
+    from kdfm import kernels as Kk
+    T, U, C = 401, 40, 96
+    M = T * U
+    g = torch.Generator(device="cuda").manual_seed(9)
+    wconv = torch.randn(2, C, 3 * C, device="cuda", generator=g) * 0.05
+    wh = torch.empty(2, C, 3 * C, device="cuda", dtype=torch.bfloat16)
+    Kk.register_bf16_twin(wconv, wh)
+    Kk.cast_bf16(wconv, wh)
+    x = torch.randn(M, C, device="cuda", generator=g)
+    b = torch.randn(C, device="cuda", generator=g)
+    out = torch.empty(M, C, device="cuda")
+    from kdfm import _lib
+    K.conv3(x, wconv[1], b, out, T, epi=_lib.EPI_RELU, math="bf16")
+    xs = torch.nn.functional.pad(_bf(x).view(U, T, C), (0, 0, 1, 1))
+    taps = torch.cat([xs[:, t:t + T] for t in range(3)], dim=2).reshape(M, 3 * C)
+    _close(out, torch.relu(taps @ _bf(wconv[1]).T + b))
