@@ -33,6 +33,13 @@ typedef __attribute__((ext_vector_type(16))) float f32x16;
 
 constexpr int SK_CKS = 6;             // k-steps (16 k each) per A chunk in KC mode
 constexpr int SK_CHUNK = 16 * SK_CKS; // 96
+constexpr int SK_EPS = 36;            // f32 row stride of the per-wave epilogue tile (16-B rows)
+
+// wave-local LDS hand-off: this wave's ds_writes complete before its following ds_reads
+__device__ __forceinline__ void sk_wave_lds_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
 
 struct SkGeo {
   int Kp;       // B image k extent (K rounded up to 16)
@@ -186,12 +193,22 @@ __global__ __launch_bounds__(64 * WV, 2) void sk_fwd_kernel(GemmP p, SkGeo g) {
   bool single;
   const float* side = epi_side_src(p, single);  // the dispatcher guarantees `single`
   float mse_part = 0.f;
-  // per-lane column constants: this lane's output column in tile j is n0 + 32 j + r
-  float bn[NCT];
+  // Epilogue lane map (row-major, 16-byte global accesses): the 32x32 accumulator tile is turned
+  // around through a per-wave LDS tile, then lane -> rows er + 8 i (i < 4), columns ec..ec+3 of each
+  // 32-column tile j.  Scalar 4-byte stores issue-limit the write stream (MI355X_MICROARCH.md,
+  // 'epilogue store tail'); dwordx4 stores and loads move 4x the bytes per instruction.
+  const int er = lane >> 3, ec = (lane & 7) * 4;
+  float* Ep = reinterpret_cast<float*>(sk_lds + (size_t)g.cw * g.ldb) + wave * 32 * SK_EPS;
+  float4 bn4[NCT];
 #pragma unroll
   for (int j = 0; j < NCT; ++j) {
-    const int64_t n = n0 + 32 * j + r;
-    bn[j] = ((epi & KDFM_EPI_BIAS) && n < p.N) ? p.bias[n] : 0.f;
+    float t[4];
+#pragma unroll
+    for (int c4 = 0; c4 < 4; ++c4) {
+      const int64_t n = n0 + 32 * j + ec + c4;
+      t[c4] = ((epi & KDFM_EPI_BIAS) && n < p.N) ? p.bias[n] : 0.f;
+    }
+    bn4[j] = make_float4(t[0], t[1], t[2], t[3]);
   }
 
   const uint16_t* bp = Bs + (nl0 + r) * g.ldb + 8 * h;
@@ -203,23 +220,31 @@ __global__ __launch_bounds__(64 * WV, 2) void sk_fwd_kernel(GemmP p, SkGeo g) {
   for (int64_t q = 0; q < nsteps; ++q) {
     const bool last = (c == g.nchunks - 1);
     const int64_t m0 = tile * 32;
-    // side operands of this tile's epilogue: issued before the prefetch and the MFMAs
-    float sv[NCT][16];
-    bool rowok[16];
+    // side operands of this tile's epilogue (row-major float4): issued before the prefetch and MFMAs
+    float4 sv4[NCT][4];
+    bool rowok[4];
     if (last) {
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int64_t m = m0 + (i & 3) + 8 * (i >> 2) + 4 * h;
+      for (int i = 0; i < 4; ++i) {
+        const int64_t m = m0 + er + 8 * i;
         rowok[i] = m < p.M && epi_row_ok(p, m < p.M ? m : 0);
       }
       if (side) {
 #pragma unroll
         for (int j = 0; j < NCT; ++j) {
-          const int64_t n = n0 + 32 * j + r;
+          const int64_t n = n0 + 32 * j + ec;
 #pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const int64_t m = m0 + (i & 3) + 8 * (i >> 2) + 4 * h;
-            sv[j][i] = (m < p.M && n < p.N) ? side[m * p.sCm + n * p.sCn] : 0.f;
+          for (int i = 0; i < 4; ++i) {
+            const int64_t m = m0 + er + 8 * i;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (m < p.M && n + 3 < p.N) {
+              v = *reinterpret_cast<const float4*>(side + m * p.sCm + n);
+            } else if (m < p.M && n < p.N) {
+              v.x = side[m * p.sCm + n];
+              if (n + 1 < p.N) v.y = side[m * p.sCm + n + 1];
+              if (n + 2 < p.N) v.z = side[m * p.sCm + n + 2];
+            }
+            sv4[j][i] = v;
           }
         }
       }
@@ -254,19 +279,43 @@ __global__ __launch_bounds__(64 * WV, 2) void sk_fwd_kernel(GemmP p, SkGeo g) {
     if (last) {
 #pragma unroll
       for (int j = 0; j < NCT; ++j) {
-        const int64_t n = n0 + 32 * j + r;
-        const bool nok = n < p.N;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int64_t m = m0 + (i & 3) + 8 * (i >> 2) + 4 * h;
-          if (!nok || m >= p.M) continue;
-          float pre = 0.f;
-          const float v = epi_apply(p, 0, m, n, p.alpha * acc[j][i], bn[j], side ? sv[j][i] : 0.f, rowok[i], seed,
-                                    keep_scale, mse_part, pre);
-          const int64_t off = m * p.sCm + n * p.sCn;
-          if (epi & KDFM_EPI_STORE_PRE) p.Cpre[off] = pre;
-          p.C[off] = v;
+        for (int i = 0; i < 16; ++i) Ep[((i & 3) + 8 * (i >> 2) + 4 * h) * SK_EPS + r] = acc[j][i];
+        sk_wave_lds_sync();
+        const int64_t n = n0 + 32 * j + ec;
+        const float bv[4] = {bn4[j].x, bn4[j].y, bn4[j].z, bn4[j].w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = er + 8 * i;
+          const int64_t m = m0 + row;
+          const float4 a = *reinterpret_cast<const float4*>(Ep + row * SK_EPS + ec);
+          if (m >= p.M || n >= p.N) continue;
+          const float av4[4] = {a.x, a.y, a.z, a.w};
+          const float s4[4] = {sv4[j][i].x, sv4[j][i].y, sv4[j][i].z, sv4[j][i].w};
+          float o[4], pr[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            o[e] = 0.f;
+            pr[e] = 0.f;
+            if (n + e < p.N)
+              o[e] = epi_apply(p, 0, m, n + e, p.alpha * av4[e], bv[e], side ? s4[e] : 0.f, rowok[i], seed,
+                               keep_scale, mse_part, pr[e]);
+          }
+          const int64_t off = m * p.sCm + n;
+          if (n + 3 < p.N) {
+            *reinterpret_cast<float4*>(p.C + off) = make_float4(o[0], o[1], o[2], o[3]);
+            if (epi & KDFM_EPI_STORE_PRE)
+              *reinterpret_cast<float4*>(p.Cpre + off) = make_float4(pr[0], pr[1], pr[2], pr[3]);
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              if (n + e < p.N) {
+                p.C[off + e] = o[e];
+                if (epi & KDFM_EPI_STORE_PRE) p.Cpre[off + e] = pr[e];
+              }
+          }
         }
+        sk_wave_lds_sync();  // Ep is rewritten for the next column tile
       }
       c = 0;
       tile += tstride;
@@ -447,6 +496,10 @@ int try_skinny_fwd(const GemmP& p, int amode, int bmode, int64_t batch, hipStrea
   bool single;
   epi_side_src(p, single);
   if (!single) return -1;
+  // row-major float4 epilogue: C (and R / aux / Cpre, laid out like C) 16-byte aligned rows
+  if (p.sCn != 1 || (p.sCm & 3)) return -1;
+  for (const void* q : {(const void*)p.C, (const void*)p.R, (const void*)p.aux, (const void*)p.Cpre})
+    if (q && (((uintptr_t)q) & 15)) return -1;
   SkGeo g;
   if (amode == KDFM_LD_CONV) {
     if (p.conv_c % 16 != 0 || p.conv_c > SK_CHUNK || p.K != p.taps * p.conv_c || p.pad < 0 || p.pad >= p.taps)
@@ -499,7 +552,9 @@ int try_skinny_fwd(const GemmP& p, int amode, int bmode, int64_t batch, hipStrea
   if (nt32 <= 4) { gcols = 1; nct = (int)nt32; }
   else if (nt32 <= 8) { gcols = 2; nct = (int)ceil_div(nt32, 2); }
   else { gcols = 4; nct = (int)(nt32 <= 12 ? ceil_div(nt32, 4) : 3); }
-  auto lds_of = [&](int gc, int nc) { return (size_t)32 * nc * gc * g.ldb * sizeof(uint16_t); };
+  auto lds_of = [&](int gc, int nc) {
+    return (size_t)32 * nc * gc * g.ldb * sizeof(uint16_t) + (size_t)4 * 32 * SK_EPS * sizeof(float);
+  };
   const size_t lds_soft = 80 * 1024, lds_hard = 160 * 1024;
   while (lds_of(gcols, nct) > lds_soft && (nct > 1 || gcols > 1)) {
     if (nct > 1) --nct; else gcols >>= 1;
