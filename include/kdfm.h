@@ -180,6 +180,17 @@ int kdfm_subsample_conv1(const float* mel, const int64_t* mel_len, const int64_t
 int kdfm_subsample_conv2(const uint16_t* y1b, const int64_t* len2, const uint16_t* wb, const float* b2, float* y2,
                          int64_t B, int64_t T1, int64_t F1, int64_t C, void* stream);
 
+/* ---------------- Evaluation path (ctc_models.py:625-692, wer.py) ---------
+ * kdfm_ctc_greedy: CTC greedy decoding (Appendix A.9; WER.update wer.py:329-333): per utterance b,
+ *   argmax over C classes of frames t < lengths[b] (first index on ties), collapse repeats when
+ *   fold != 0, drop `blank`; tokens[b*T + i], i < ntok[b] (int32); optional labels[b*T + t] = the
+ *   per-frame argmax (blank beyond the length).  log_probs rows (b*T + t) with row stride ld.
+ * kdfm_edit_distance: host-side Levenshtein distance between two int32 sequences (editdistance.eval,
+ *   wer.py:66-69); -1 on bad arguments.  No device work. */
+int kdfm_ctc_greedy(const float* log_probs, int64_t ld, const int64_t* lengths, int32_t* tokens, int32_t* ntok,
+                    int32_t* labels, int64_t B, int64_t T, int64_t C, int64_t blank, int32_t fold, void* stream);
+int64_t kdfm_edit_distance(const int32_t* a, int64_t na, const int32_t* b, int64_t nb);
+
 /* ---------------- ConformerLayer (Appendix A.5-A.8; layers built conformer_encoder.py:450-472) */
 int kdfm_layernorm_fwd(const float* x, const float* gamma, const float* beta, float* y, float* mean, float* rstd,
                        int64_t rows, int64_t d, float eps, void* stream);

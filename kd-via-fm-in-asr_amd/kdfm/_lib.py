@@ -80,6 +80,8 @@ SIGNATURES: dict[str, tuple] = {
     "kdfm_subsample_wprep": (_i32, [P, P, _i64, P]),
     "kdfm_subsample_conv1": (_i32, [P, P, P, P, P, P, P, _i64, _i64, _i64, _i64, P]),
     "kdfm_subsample_conv2": (_i32, [P, P, P, P, P, _i64, _i64, _i64, _i64, P]),
+    "kdfm_ctc_greedy": (_i32, [P, _i64, P, P, P, P, _i64, _i64, _i64, _i64, _i32, P]),
+    "kdfm_edit_distance": (_i64, [P, _i64, P, _i64]),
     "kdfm_layernorm_fwd": (_i32, [P, P, P, P, P, P, _i64, _i64, _f32, P]),
     "kdfm_layernorm_bwd": (_i32, [P, P, P, P, P, P, P, P, P, P, _i64, _i64, P]),
     "kdfm_layernorm_bwd_ws": (_i64, [_i64, _i64]),

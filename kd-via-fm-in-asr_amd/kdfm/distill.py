@@ -405,6 +405,21 @@ class EncDecCTCModelBPE(nn.Module):
         log_probs = self.decoder(encoder_output=enc)
         return log_probs, enc_len, greedy(log_probs)
 
+    # ---- evaluation (ctc_models.py:625-692); self.wer: a kdfm.eval.WER over the model's tokenizer ----
+    wer = None
+
+    def validation_pass(self, batch, batch_idx=0, dataloader_idx=0):
+        from .eval import validation_pass
+        if self.wer is None:
+            raise RuntimeError("set model.wer = kdfm.eval.WER(kdfm.eval.CTCGreedyDecoding(tokenizer)) first")
+        return validation_pass(self, batch, self.wer)
+
+    def validation_step(self, batch, batch_idx=0, dataloader_idx=0):
+        return self.validation_pass(batch, batch_idx, dataloader_idx)
+
+    def test_step(self, batch, batch_idx=0, dataloader_idx=0):
+        return {k.replace("val_", "test_"): v for k, v in self.validation_pass(batch, batch_idx).items()}
+
 
 def greedy(log_probs):
     B, T, Cn = log_probs.shape

@@ -176,6 +176,50 @@ class Ver5Engine:
         self._join_losses(ctx)   # CTC/KL overlapped the heads forward; losses valid after forward()
         return ctx
 
+    # ---------------------------------------------------------------------------------------------
+    def infer(self, wav, wav_len):
+        """Eval-mode student forward (asr_train_diffm.py:606-643 with self.training False; the
+        validation pass of ctc_models.py:625-665): frontend without dither or SpecAugment, encoder
+        with BatchNorm running statistics and no dropout, decoder + log_softmax.  The reference's eval
+        forward also runs the teacher encoder (:629-631) and discards it (only training_step reads
+        the hooks), so it is skipped.  Returns log_probs (B, T', V+1) and enc_len (B,)."""
+        cfg = self.cfg
+        dev = self.device
+        B, N = wav.shape
+        Tm = mel_frames(cfg, N)
+        Ss = EncoderShapes(cfg, B, Tm, cfg.d_student, cfg.heads_student)
+        mel_len = torch.empty(B, dtype=torch.int64, device=dev)
+        len1 = torch.empty_like(mel_len)
+        len2 = torch.empty_like(mel_len)
+        K.subsample_lengths(wav_len.to(device=dev, dtype=torch.int64), mel_len, len1, len2, cfg.hop)
+        mel = frontend_forward(cfg, self.fe, wav.to(dev), wav_len.to(dev), mel_len, dither=0.0)
+        feats = torch.empty(cfg.n_layers, Ss.rows, Ss.d, device=dev)
+        encoder_forward(cfg, Ss, self.student.P, "encoder.", mel, mel_len, len1, len2, feats,
+                        self._pos_emb(Ss.T, Ss.d), train=False, seed=self.seed, salt=SALT_STUDENT, save=False,
+                        bn_running=self.bn.P, use_batch_stats=False, ws=self._enc_ws(Ss))
+        Cn = cfg.classes
+        logits = torch.empty(Ss.rows, Cn, device=dev)
+        K.linear(feats[-1], self.student.P["decoder.decoder_layers.0.weight"].view(Cn, Ss.d),
+                 self.student.P["decoder.decoder_layers.0.bias"], logits)
+        lp = torch.empty(Ss.rows, Cn, device=dev)
+        K.log_softmax(logits, lp)
+        return lp.view(B, Ss.T, Cn), len2
+
+    def ctc_mean(self, log_probs, enc_len, targets, tgt_len):
+        """CTCLoss(reduction='mean_batch', zero_infinity=True) of eval log-probs (ctc_models.py:637)."""
+        B, T, Cn = log_probs.shape
+        dev = log_probs.device
+        targets = targets.to(device=dev, dtype=torch.int64).contiguous()
+        tgt_len = tgt_len.to(device=dev, dtype=torch.int64)
+        Umax = max(1, targets.shape[1])
+        a = torch.empty(B * T * (2 * Umax + 1), device=dev)
+        bta = torch.empty_like(a)
+        nll = torch.empty(B, device=dev)
+        g = torch.empty(B * T, Cn, device=dev)
+        K.ctc_loss(log_probs.reshape(B * T, Cn), targets, enc_len, tgt_len, a, bta, nll, g, B, T, Cn, self.cfg.vocab,
+                   1.0 / B)
+        return nll.mean()
+
     def _aux_stream(self):
         if getattr(self, "_aux", None) is None:
             self._aux = torch.cuda.Stream(self.device)
