@@ -31,6 +31,23 @@ U_TOKENS = 100
 FFN_FLOPS_NOTE = "ffn_up GEMMs: 2*M*N*K per launch (M=B*T' rows, N=4d, K=d)"
 MI355X_BF16_DENSE_TFLOPS = 2500.0   # /opt/skills/guides/MI355X_MICROARCH.md chip table (dense)
 MI355X_F32_MFMA_TFLOPS = 157.3
+MI355X_HBM_GBPS = 8000.0            # MI355X_MICROARCH.md §HBM (8 TB/s spec peak)
+# PMC traffic of the roofline kernel (tools/pmc_traffic.sh -> tools/pmc_summary.py, 2 separate --pmc
+# passes, FETCH_SIZE doubled per the gfx950 correction); committed under profiles/
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+ROOF_KERNEL = "kdfm::sk_fwd_kernel<3, 2, 4>"
+
+
+def pmc_traffic(kernel: str):
+    try:
+        with open(PMC_TRAFFIC) as fh:
+            rows = json.load(fh)
+    except (OSError, ValueError):
+        return None
+    for r in rows:
+        if r["kernel"] == kernel:
+            return r["bytes_per_launch"]
+    return None
 
 
 def parse():
@@ -131,12 +148,15 @@ def main():
     elapsed = max_over_ranks(time.perf_counter() - t0, dev)
     # dominant-kernel timing: one instrumented eager step right after the timed replays, every
     # ffn_up launch bracketed by HIP events on the stream it runs on (main or teacher stream)
-    trace = K.Trace(["ffn_up"])
+    trace = K.Trace(["ffn_up", "deno_conv"])
     with trace:
         eng.train_step(wav, wl, tg, tl, ar)
     torch.cuda.synchronize()
     losses = eng.losses.detach().cpu().tolist()
-    summ = trace.summary().get("ffn_up", {"launches": 0, "ms_total": 0.0, "flops_total": 0.0})
+    tsum = trace.summary()
+    empty = {"launches": 0, "ms_total": 0.0, "flops_total": 0.0, "bytes_total": 0.0}
+    summ = tsum.get("ffn_up", empty)
+    deno = tsum.get("deno_conv", empty)
     if rank == 0:
         utt = world * args.batch * args.steps / elapsed
         n_l = max(1, summ["launches"])
@@ -144,6 +164,13 @@ def main():
         flops_per_launch = summ["flops_total"] / n_l
         achieved = flops_per_launch / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
         peak = MI355X_BF16_DENSE_TFLOPS if cfg.math == "bf16" else MI355X_F32_MFMA_TFLOPS
+        # roofline subject: the dominant kernel of the step (rocprof: the denoiser k=3 conv products,
+        # kdfm_gemm skinny CONV mode) - HBM-bound (72 flop/B at f32 storage << the bf16 ridge)
+        d_l = max(1, deno["launches"])
+        d_ms = deno["ms_total"] / d_l
+        d_bytes = deno["bytes_total"] / d_l
+        d_gbps = d_bytes / (d_ms * 1e-3) / 1e9 if d_ms > 0 else 0.0
+        d_traffic = pmc_traffic(ROOF_KERNEL)
         cpu = None
         if not args.no_cpu_baseline:
             cpu = cpu_baseline(args.cpu_threads, args.samples)
@@ -164,11 +191,17 @@ def main():
                                    "(d88 h2 L16), BASELINE.json configs[1] shape",
                        "global_batch": world * args.batch, "seq_len": args.samples,
                        "frames_subsampled": (args.samples // 160) // 4 + 1, "parallelism": f"dp{world}"},
-            "roofline": {"bound": "mfma", "kernel": "kdfm_gemm ffn_up (Conformer FFN d->4d, SiLU+dropout epilogue)",
-                         "achieved": round(achieved, 3), "peak": peak, "unit": "TFLOP/s",
-                         "frac": round(achieved / peak, 5), "traffic": None,
-                         "launches": summ["launches"], "avg_ms": round(avg_ms, 5),
-                         "flops_per_launch": flops_per_launch},
+            "roofline": {"bound": "hbm",
+                         "kernel": "kdfm_gemm CONV (denoiser Conv1d k=3 over 16 stacked layers, 205312 x 96 x 288, "
+                                   "sk_fwd_kernel<3,2,4>)",
+                         "achieved": round(d_gbps, 1), "peak": MI355X_HBM_GBPS, "unit": "GB/s",
+                         "frac": round(d_gbps / MI355X_HBM_GBPS, 4), "traffic": d_traffic,
+                         "traffic_source": "profiles/r01_pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE)",
+                         "launches": deno["launches"], "avg_ms": round(d_ms, 5), "bytes_per_launch": d_bytes},
+            "roofline_mfma_ffn": {"bound": "mfma", "kernel": "kdfm_gemm ffn_up (Conformer FFN d->4d, SiLU+dropout)",
+                                  "achieved": round(achieved, 3), "peak": peak, "unit": "TFLOP/s",
+                                  "frac": round(achieved / peak, 5), "launches": summ["launches"],
+                                  "avg_ms": round(avg_ms, 5), "flops_per_launch": flops_per_launch},
             "cpu_baseline": cpu,
             "losses_last_step": [round(x, 5) for x in losses],
         }

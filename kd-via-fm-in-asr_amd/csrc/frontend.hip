@@ -81,6 +81,59 @@ __global__ __launch_bounds__(256) void logmel_norm_kernel(const float* __restric
     for (int64_t t = w; t < T; t += 4) orow[t * nf + j] = (t < n) ? (__logf(mr[t * nf + j] + guard) - mean) * inv : 0.f;
 }
 
+// Register-resident form for T <= 32 * LM_PER frames: block = (b, 8 mel columns), 256 threads =
+// 8 columns x 32 frame lanes; every log value of the block's slice is loaded once (all loads in
+// flight together) and kept in registers across the mean, the variance and the write pass.
+constexpr int LM_PER = 64;
+__global__ __launch_bounds__(256) void logmel_norm_reg_kernel(const float* __restrict__ mel, const int64_t* __restrict__ sl,
+                                                              float* __restrict__ out, int T, int nf, float guard) {
+  __shared__ float red[32][9];
+  const int b = blockIdx.y;
+  const int fl = threadIdx.x & 7, tg = threadIdx.x >> 3;
+  const int j = blockIdx.x * 8 + fl;
+  const int n = (int)(sl[b] < T ? sl[b] : T);
+  const float* mr = mel + (int64_t)b * T * nf;
+  float* orow = out + (int64_t)b * T * nf;
+  float l[LM_PER];
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < LM_PER; ++k) {
+    const int t = tg + 32 * k;
+    l[k] = (j < nf && t < n) ? __logf(mr[(int64_t)t * nf + j] + guard) : 0.f;
+    s += l[k];
+  }
+  red[tg][fl] = s;
+  __syncthreads();
+  float tot = 0.f;
+#pragma unroll 8
+  for (int q = 0; q < 32; ++q) tot += red[q][fl];
+  const float mean = tot / (float)n;
+  __syncthreads();
+  float qv = 0.f;
+#pragma unroll
+  for (int k = 0; k < LM_PER; ++k) {
+    const int t = tg + 32 * k;
+    const float dv = (t < n) ? l[k] - mean : 0.f;
+    qv += dv * dv;
+  }
+  red[tg][fl] = qv;
+  __syncthreads();
+  float var = 0.f;
+#pragma unroll 8
+  for (int q = 0; q < 32; ++q) var += red[q][fl];
+  var /= ((float)n - 1.f);
+  float sd = sqrtf(var);
+  if (!(sd == sd)) sd = 0.f;
+  const float inv = 1.f / (sd + 1e-5f);
+  if (j < nf) {
+#pragma unroll
+    for (int k = 0; k < LM_PER; ++k) {
+      const int t = tg + 32 * k;
+      if (t < T) orow[(int64_t)t * nf + j] = (t < n) ? (l[k] - mean) * inv : 0.f;
+    }
+  }
+}
+
 // SpecAugment: per utterance `fmasks` frequency bands of width floor(U*(fwidth+1)) and `tmasks`
 // time bands of width floor(U*(max(1,int(len*twidth))+1)); masked cells set to 0.
 __device__ __forceinline__ bool spec_masked(int64_t b, int64_t t, int64_t f, int64_t len, int64_t nf, int fmasks,
@@ -197,6 +250,12 @@ int kdfm_logmel_normalize(const float* mel, const int64_t* seq_len, float* out, 
   using namespace kdfm;
   KDFM_REQUIRE(mel && seq_len && out, "null pointer");
   if (B * T * nfilt == 0) return KDFM_OK;
+  if (T <= 32 * LM_PER) {
+    dim3 grid((unsigned)ceil_div(nfilt, 8), (unsigned)B);
+    hipLaunchKernelGGL(logmel_norm_reg_kernel, grid, dim3(256), 0, as_stream(stream), mel, seq_len, out, (int)T,
+                       (int)nfilt, log_guard);
+    return check_launch("kdfm_logmel_normalize");
+  }
   dim3 grid((unsigned)ceil_div(nfilt, 64), (unsigned)B);
   hipLaunchKernelGGL(logmel_norm_kernel, grid, dim3(256), 0, as_stream(stream), mel, seq_len, out, T, nfilt,
                      log_guard);

@@ -86,9 +86,9 @@ def heads_forward(cfg: Ver5Config, P, s_feats, t_feats, T, ws: HeadsWorkspace, a
     acts = []
     for _ in range(ds):
         a = _empty(n, Lt, dev=dev)
-        K.conv3(xs[-1], ws.w1f, P["denoiser.net.0.bias"], a, T, epi=_lib.EPI_RELU)
+        K.conv3(xs[-1], ws.w1f, P["denoiser.net.0.bias"], a, T, epi=_lib.EPI_RELU, tag="deno_conv")
         xn = _empty(n, Lt, dev=dev)
-        K.conv3(a, ws.w2f, P["denoiser.net.2.bias"], xn, T, R=xs[-1], rscale=-1.0 / ds)
+        K.conv3(a, ws.w2f, P["denoiser.net.2.bias"], xn, T, R=xs[-1], rscale=-1.0 / ds, tag="deno_conv")
         acts.append(a)
         xs.append(xn)
     zd = xs[-1]
@@ -183,10 +183,10 @@ def heads_backward(cfg: Ver5Config, P, G, ctx, ws: HeadsWorkspace, ds_feats, *, 
         # x_{i+1} = x_i - (1/ds)(conv(a_i, W2) + b2)
         WGRAD.run(lambda: K.conv3_dw(g, acts[i], ws.g2, T, alpha=-1.0 / ds, db=G["denoiser.net.2.bias"]), g, acts[i])
         da = _empty(n, Lt, dev=dev)
-        K.conv3(g, ws.w2b, None, da, T, epi=_lib.EPI_DRELU, aux=acts[i], alpha=-1.0 / ds)
+        K.conv3(g, ws.w2b, None, da, T, epi=_lib.EPI_DRELU, aux=acts[i], alpha=-1.0 / ds, tag="deno_conv")
         WGRAD.run(lambda: K.conv3_dw(da, xs[i], ws.g1, T, db=G["denoiser.net.0.bias"]), da, xs[i])
         gi = _empty(n, Lt, dev=dev)
-        K.conv3(da, ws.w1b, None, gi, T, R=g, rscale=1.0)
+        K.conv3(da, ws.w1b, None, gi, T, R=g, rscale=1.0, tag="deno_conv")
         g = gi
         del da
     WGRAD.join()  # ws.g1 / ws.g2 are produced on the side stream

@@ -28,7 +28,7 @@ class Trace:
 
     def __init__(self, tags):
         self.tags = set(tags)
-        self.events = []   # (tag, flops, start, end)
+        self.events = []   # (tag, flops, algorithmic bytes, start, end)
 
     def __enter__(self):
         Trace.active = self
@@ -40,13 +40,15 @@ class Trace:
     def summary(self):
         torch.cuda.synchronize()
         out = {}
-        for tag, flops, s, e in self.events:
+        for tag, flops, nbytes, s, e in self.events:
             ms = s.elapsed_time(e)
-            t = out.setdefault(tag, [0, 0.0, 0.0])
+            t = out.setdefault(tag, [0, 0.0, 0.0, 0.0])
             t[0] += 1
             t[1] += ms
             t[2] += flops
-        return {k: {"launches": v[0], "ms_total": v[1], "flops_total": v[2]} for k, v in out.items()}
+            t[3] += nbytes
+        return {k: {"launches": v[0], "ms_total": v[1], "flops_total": v[2], "bytes_total": v[3]}
+                for k, v in out.items()}
 
 
 def set_math(mode: str) -> None:
@@ -180,7 +182,7 @@ def cast_bf16_t(src, dst, table, ntab, nblocks):
 def gemm(A, B, Cout, M, N, K, sAm, sAk, sBk, sBn, sCm, sCn, *, amode, bmode,
          batch=(1, 1), bA=(0, 0), bB=(0, 0), bC=(0, 0), alpha=1.0, epi=0, bias=None, R=None, rscale=1.0,
          aux=None, Cpre=None, beta=0.0, dropout_p=0.0, seed=None, rng_stream=0, splitk=1,
-         conv=None, math=None, rowmask=None, mse=None, tag=None, ones_out=None, Bh=None):
+         conv=None, math=None, rowmask=None, mse=None, tag=None, ones_out=None, Bh=None, nbytes=None):
     d = GemmDesc()
     if Bh is not None and (math or _State.math) == "bf16":
         d.Bh, d.sBh = Bh
@@ -225,7 +227,8 @@ def gemm(A, B, Cout, M, N, K, sAm, sAk, sBk, sBn, sCm, sCn, *, amode, bmode,
         ev0.record()
         call("kdfm_gemm", C.byref(d), _s())
         ev1.record()
-        tr.events.append((tag, 2.0 * M * N * K * batch[0] * batch[1], ev0, ev1))
+        nb = nbytes if nbytes is not None else 4.0 * (M * K + K * N + M * N) * batch[0] * batch[1]
+        tr.events.append((tag, 2.0 * M * N * K * batch[0] * batch[1], nb, ev0, ev1))
         return
     call("kdfm_gemm", C.byref(d), _s())
 
@@ -278,9 +281,11 @@ def linear_dw(dy, x, dW, *, alpha=1.0, math=None, db=None):
          amode=_lib.LD_XC, bmode=_lib.LD_XC, epi=_lib.EPI_ATOMIC, splitk=sk, alpha=alpha, math=math, ones_out=db)
 
 
-def conv3(x, Wf, bias, out, T, *, epi=0, R=None, rscale=1.0, alpha=1.0, aux=None, math=None):
+def conv3(x, Wf, bias, out, T, *, epi=0, R=None, rscale=1.0, alpha=1.0, aux=None, math=None, tag=None):
     """Conv1d(k=3, pad=1) along frames on channels-last rows: out[r,o] = sum_{tap,c} Wf[o, tap*C+c] x[r+tap-1, c]
-    Wf: (O, 3*C) GEMM layout from kdfm_convw_prep; rows grouped in utterances of T frames."""
+    Wf: (O, 3*C) GEMM layout from kdfm_convw_prep; rows grouped in utterances of T frames.
+    Algorithmic bytes (bench roofline): x read once (the taps are re-reads of the same rows), the
+    output and each side operand (R / aux) once, the weights once; all f32."""
     M, Cc = x.shape
     O = Wf.shape[0]
     assert Wf.shape[1] == 3 * Cc and x.stride(1) == 1
@@ -290,7 +295,8 @@ def conv3(x, Wf, bias, out, T, *, epi=0, R=None, rscale=1.0, alpha=1.0, aux=None
         epi |= _lib.EPI_RESID
     gemm(x, Wf, out, M, O, 3 * Cc, x.stride(0), 1, 1, Wf.stride(0), out.stride(0), out.stride(1),
          amode=_lib.LD_CONV, bmode=_lib.LD_KC, epi=epi, bias=bias, R=R, rscale=rscale, alpha=alpha, aux=aux,
-         conv=(3, 1, Cc, T), math=math, Bh=bf16_twin(Wf) if _TWINS else None)
+         conv=(3, 1, Cc, T), math=math, Bh=bf16_twin(Wf) if _TWINS else None, tag=tag,
+         nbytes=4.0 * (M * Cc + M * O * (1 + (R is not None) + (aux is not None)) + O * 3 * Cc))
 
 
 def conv3_dw(dy, x, G, T, *, alpha=1.0, math=None, db=None):
