@@ -447,6 +447,195 @@ __global__ __launch_bounds__(256, 2) void skd_fwd_kernel(GemmP p, SkGeo g, int G
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// CONV mode with an LDS slab (the denoiser k=3 convolutions, asr_train_diffm.py:444-460, stacked
+// over 16 layers: 205,312 rows x 96 channels).  The register-fragment loader above reads each row
+// three times (once per tap, 32 B per lane across 32 rows: 32 cache lines per instruction) and
+// PMC shows ~1.25x the algorithmic bytes.  Here a wave loads its tile's rows m0-pad .. m0+31+taps-1-pad
+// ONCE, as contiguous float4 (1 KiB per instruction, every line fully used), converts them to bf16
+// into a per-wave LDS slab, and the three taps read their A fragments from that slab at row
+// offsets r + tap (per-lane zero select where the tap crosses an utterance boundary).  The next
+// tile's slab is prefetched into registers while the MFMAs and the epilogue of the current one run.
+// 8 waves share one staged weight image (96 x 288 bf16); the epilogue's transposition tile aliases
+// the wave's slab (free once the MFMAs have read it).
+constexpr int SKC_WV = 8;
+constexpr int SKC_SLAB_V = 13;            // float4 per lane: (32 + 2) rows x 96 ch / 4 / 64 lanes
+constexpr int SKC_LDA = SK_CHUNK + 8;     // bf16 slab row stride (208 B, 16-B aligned)
+constexpr int SKC_SLAB_BYTES = 34 * SKC_LDA * 2;
+
+__device__ __forceinline__ void skc_load_slab(float4 (&v)[SKC_SLAB_V], const GemmP& p, int64_t m0, int rows, int cq,
+                                              int lane) {
+  const int total = rows * cq;
+#pragma unroll
+  for (int i = 0; i < SKC_SLAB_V; ++i) {
+    const int e = lane + 64 * i;
+    const int j = e / cq, q = e - j * cq;
+    const int64_t gr = m0 - p.pad + j;
+    v[i] = (e < total && gr >= 0 && gr < p.M) ? *reinterpret_cast<const float4*>(p.A + gr * p.sAm + 4 * q)
+                                             : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
+template <int NCT>
+__global__ __launch_bounds__(64 * SKC_WV, 1) void skc_fwd_kernel(GemmP p, SkGeo g) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t sk_lds[];
+  uint16_t* Bs = sk_lds;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  sk_stage_B(p, g, Bs, 0);
+  __syncthreads();
+
+  const int r = lane & 31, h = lane >> 5;
+  const int64_t tstride = (int64_t)gridDim.x * SKC_WV;
+  int64_t tile = (int64_t)blockIdx.x * SKC_WV + wave;
+  if (tile >= g.tiles) return;
+  const int C = (int)p.conv_c, cq = C >> 2, taps = p.taps;
+  const int rows = 32 + taps - 1;
+  const int64_t T = p.conv_t;
+
+  uint16_t* As = reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(sk_lds) + (size_t)g.cw * g.ldb * 2 +
+                                             (size_t)wave * SKC_SLAB_BYTES);
+  float* Ep = reinterpret_cast<float*>(As);  // epilogue tile (32 x SK_EPS f32) aliases the slab
+
+  const int epi = p.epi;
+  const uint64_t seed = (epi & KDFM_EPI_DROPOUT) ? load_seed(p.seed) : 0ull;
+  const float keep_scale = (epi & KDFM_EPI_DROPOUT) ? 1.f / (1.f - p.dropout_p) : 1.f;
+  bool single;
+  const float* side = epi_side_src(p, single);
+  float mse_part = 0.f;
+  const int er = lane >> 3, ec = (lane & 7) * 4;
+  float4 bn4[NCT];
+#pragma unroll
+  for (int j = 0; j < NCT; ++j) {
+    float t4[4];
+#pragma unroll
+    for (int c4 = 0; c4 < 4; ++c4) {
+      const int64_t n = 32 * j + ec + c4;
+      t4[c4] = ((epi & KDFM_EPI_BIAS) && n < p.N) ? p.bias[n] : 0.f;
+    }
+    bn4[j] = make_float4(t4[0], t4[1], t4[2], t4[3]);
+  }
+  const uint16_t* bp = Bs + r * g.ldb + 8 * h;
+
+  float4 sv[SKC_SLAB_V];
+  skc_load_slab(sv, p, tile * 32, rows, cq, lane);
+  for (; tile < g.tiles; tile += tstride) {
+    const int64_t m0 = tile * 32;
+    // slab registers -> bf16 LDS slab
+#pragma unroll
+    for (int i = 0; i < SKC_SLAB_V; ++i) {
+      const int e = lane + 64 * i;
+      if (e < rows * cq) {
+        const int j = e / cq, q = e - j * cq;
+        pk4(As + j * SKC_LDA + 4 * q, sv[i]);
+      }
+    }
+    sk_wave_lds_sync();
+    // next slab prefetch: its latency overlaps the MFMAs and the epilogue of this tile
+    if (tile + tstride < g.tiles) skc_load_slab(sv, p, (tile + tstride) * 32, rows, cq, lane);
+
+    f32x16 acc[NCT];
+#pragma unroll
+    for (int j = 0; j < NCT; ++j)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[j][i] = 0.f;
+    const int64_t m = m0 + r;
+    const int64_t t = m % T;
+    for (int c = 0; c < taps; ++c) {
+      const int64_t tt = t + c - p.pad;
+      const bool ok = m < p.M && tt >= 0 && tt < T;
+      const uint16_t* ap = As + (r + c) * SKC_LDA + 8 * h;
+#pragma unroll
+      for (int s = 0; s < SK_CKS; ++s) {
+        if (16 * s < C) {
+          bf16x8 af = *reinterpret_cast<const bf16x8*>(ap + 16 * s);
+          if (!ok) af = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+          for (int j = 0; j < NCT; ++j) {
+            const bf16x8 bfr = *reinterpret_cast<const bf16x8*>(bp + j * 32 * g.ldb + c * C + 16 * s);
+            acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfr, acc[j], 0, 0, 0);
+          }
+        }
+      }
+    }
+    bool rowok[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t mm = m0 + er + 8 * i;
+      rowok[i] = mm < p.M && epi_row_ok(p, mm < p.M ? mm : 0);
+    }
+    sk_wave_lds_sync();  // every slab read issued above has returned before Ep overwrites it
+#pragma unroll
+    for (int j = 0; j < NCT; ++j) {
+      const int64_t n = 32 * j + ec;
+      float4 sd4[4];  // side operand rows of this column tile (register budget: one tile at a time)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int64_t mm = m0 + er + 8 * i;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (side && mm < p.M && n + 3 < p.N) {
+          v = *reinterpret_cast<const float4*>(side + mm * p.sCm + n);
+        } else if (side && mm < p.M && n < p.N) {
+          v.x = side[mm * p.sCm + n];
+          if (n + 1 < p.N) v.y = side[mm * p.sCm + n + 1];
+          if (n + 2 < p.N) v.z = side[mm * p.sCm + n + 2];
+        }
+        sd4[i] = v;
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) Ep[((i & 3) + 8 * (i >> 2) + 4 * h) * SK_EPS + r] = acc[j][i];
+      sk_wave_lds_sync();
+      const float bv[4] = {bn4[j].x, bn4[j].y, bn4[j].z, bn4[j].w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = er + 8 * i;
+        const int64_t mm = m0 + row;
+        const float4 a = *reinterpret_cast<const float4*>(Ep + row * SK_EPS + ec);
+        if (mm >= p.M || n >= p.N) continue;
+        const float av4[4] = {a.x, a.y, a.z, a.w};
+        const float s4[4] = {sd4[i].x, sd4[i].y, sd4[i].z, sd4[i].w};
+        float o[4], pr[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          o[e] = 0.f;
+          pr[e] = 0.f;
+          if (n + e < p.N)
+            o[e] = epi_apply(p, 0, mm, n + e, p.alpha * av4[e], bv[e], side ? s4[e] : 0.f, rowok[i], seed, keep_scale,
+                             mse_part, pr[e]);
+        }
+        const int64_t off = mm * p.sCm + n;
+        if (n + 3 < p.N) {
+          *reinterpret_cast<float4*>(p.C + off) = make_float4(o[0], o[1], o[2], o[3]);
+          if (epi & KDFM_EPI_STORE_PRE)
+            *reinterpret_cast<float4*>(p.Cpre + off) = make_float4(pr[0], pr[1], pr[2], pr[3]);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (n + e < p.N) {
+              p.C[off + e] = o[e];
+              if (epi & KDFM_EPI_STORE_PRE) p.Cpre[off + e] = pr[e];
+            }
+        }
+      }
+      sk_wave_lds_sync();  // Ep / the slab are rewritten next
+    }
+  }
+  if (epi & KDFM_EPI_MSE) {
+    mse_part = wave_sum(mse_part);
+    if (lane == 0) atomicAdd(p.loss_acc, mse_part * p.loss_scale);
+  }
+}
+
+template <int NCT>
+int skc_launch(const GemmP& p, const SkGeo& g, int64_t gx, size_t lds, hipStream_t st) {
+  static bool once = [] {
+    hipFuncSetAttribute((const void*)skc_fwd_kernel<NCT>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    return true;
+  }();
+  (void)once;
+  hipLaunchKernelGGL((skc_fwd_kernel<NCT>), dim3((unsigned)gx), dim3(64 * SKC_WV), lds, st, p, g);
+  return check_launch("kdfm_gemm(skinny conv slab)");
+}
+
 template <int NCT, int AMODE>
 int skd_launch(const GemmP& p, const SkGeo& g, int G, int64_t gx, hipStream_t st) {
   hipLaunchKernelGGL((skd_fwd_kernel<NCT, AMODE>), dim3((unsigned)gx), dim3(256), 0, st, p, g, G);
@@ -541,6 +730,24 @@ int try_skinny_fwd(const GemmP& p, int amode, int bmode, int64_t batch, hipStrea
   }
   if (p.M < min_m) return -1;
   g.Kp = (int)(ceil_div(p.K, 16) * 16);
+  static const int slab = env_int("KDFM_SKINNY_CONV_SLAB", 1);
+  static const int slab_wgs = env_int("KDFM_SKINNY_CONV_SLAB_WGS", 256);
+  if (slab && amode == KDFM_LD_CONV && p.N <= 96 && p.conv_c <= SK_CHUNK && p.taps <= 3 && p.sAm >= p.conv_c) {
+    // slab rows (32 + taps - 1) x conv_c must fit the SKC_SLAB_V registers / SKC_SLAB_BYTES of a wave
+    g.ldb = g.Kp + 8;
+    const int nct = (int)ceil_div(p.N, 32);
+    g.gcols = 1;
+    g.cw = 32 * nct;
+    g.tiles = ceil_div(p.M, 32);
+    const size_t lds = (size_t)g.cw * g.ldb * 2 + (size_t)SKC_WV * SKC_SLAB_BYTES;
+    int64_t gx = ceil_div(g.tiles, SKC_WV);
+    if (gx > slab_wgs) gx = slab_wgs;
+    switch (nct) {
+      case 1: return skc_launch<1>(p, g, gx, lds, st);
+      case 2: return skc_launch<2>(p, g, gx, lds, st);
+      default: return skc_launch<3>(p, g, gx, lds, st);
+    }
+  }
   if (amode == KDFM_LD_KC) {
     // the last chunk may read image columns up to nchunks*96 - 1: pad the image to that
     g.Kp = g.nchunks * SK_CHUNK;

@@ -191,3 +191,34 @@ def test_skinny_direct_conv3_twin(K):
     xs = torch.nn.functional.pad(_bf(x).view(U, T, C), (0, 0, 1, 1))
     taps = torch.cat([xs[:, t:t + T] for t in range(3)], dim=2).reshape(M, 3 * C)
     _close(out, torch.relu(taps @ _bf(wconv[1]).T + b))
+
+
+@pytest.mark.parametrize("T,U", [(401, 164), (7, 9363), (33, 2000)])
+def test_skinny_conv3_slab(K, T, U):
+    """LDS-slab CONV kernel (skc_fwd_kernel: M >= 65536 rows, N <= 96, the denoiser convs of
+    asr_train_diffm.py:444-460 stacked over layers): each epilogue the heads use, utterance
+    boundaries inside a 32-row tile (T = 7, 33) and a ragged last tile (M % 32 != 0)."""
+    from kdfm import _lib
+    C = 96
+    M = T * U
+    g = torch.Generator(device="cuda").manual_seed(11)
+    Wf = torch.randn(C, 3 * C, device="cuda", generator=g) * 0.05
+    x = torch.randn(M, C, device="cuda", generator=g)
+    b = torch.randn(C, device="cuda", generator=g)
+    R = torch.randn(M, C, device="cuda", generator=g)
+    xs = torch.nn.functional.pad(_bf(x).view(U, T, C), (0, 0, 1, 1))
+    taps = torch.cat([xs[:, t:t + T] for t in range(3)], dim=2).reshape(M, 3 * C)
+    ref = taps @ _bf(Wf).T
+    del xs, taps
+    out = torch.empty(M, C, device="cuda")
+    K.conv3(x, Wf, b, out, T, epi=_lib.EPI_RELU, math="bf16")
+    _close(out, torch.relu(ref + b))
+    K.conv3(x, Wf, b, out, T, R=R, rscale=-1.0 / 9, math="bf16")
+    _close(out, R - (ref + b) / 9)
+    K.conv3(x, Wf, None, out, T, epi=_lib.EPI_DRELU, aux=R, alpha=-1.0 / 9, math="bf16")
+    _close(out, torch.where(R > 0, -ref / 9, torch.zeros_like(R)))
+    # N < 96 (one and two 32-column tiles) through the same kernel
+    for n_out in (32, 70):
+        o2 = torch.empty(M, n_out, device="cuda")
+        K.conv3(x, Wf[:n_out].contiguous(), b[:n_out].contiguous(), o2, T, math="bf16")
+        _close(o2, ref[:, :n_out] + b[:n_out])
