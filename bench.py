@@ -102,9 +102,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = os.environ.get("KDFM_DIST_BACKEND", "nccl")   # gloo only for 1-GPU rehearsals
+    if backend != "nccl":
+        local = local % max(1, torch.cuda.device_count())
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -120,9 +126,10 @@ def main():
     eng.set_seed(1000 + rank)
     wav, wl, tg, tl = synthetic_batch(cfg, args.batch, args.samples, U_TOKENS, dev, seed=1234 + rank)
 
-    from kdfm.ddp import FlatGradAllReduce, max_over_ranks
-    # RCCL over xGMI: one all-reduce of the flat 13.8 MB gradient buffer per step
-    ar = FlatGradAllReduce() if world > 1 else None
+    from kdfm.ddp import BucketedGradAllReduce, max_over_ranks
+    # RCCL over xGMI: the flat 13.8 MB gradient buffer in 4 buckets, each all-reduced on a comm
+    # stream as soon as the backward has finalised it (heads, decoder, layers 15..0)
+    ar = BucketedGradAllReduce(eng.student.numel, buckets=4) if world > 1 else None
     # warm-up: one eager step (lazy buffers, allocator pools), graph capture, then replays
     eng.train_step(wav, wl, tg, tl, ar)
     if not args.graph:

@@ -409,14 +409,17 @@ def encoder_forward(cfg, S: EncoderShapes, P, prefix, mel, mel_len, len1, len2, 
 
 
 def encoder_backward(cfg, S: EncoderShapes, P, G, prefix, run: EncoderRun, dfeats, pos_emb, len1, len2, *, seed,
-                     salt, ws):
+                     salt, ws, on_layer_done=None):
     """dfeats (n_layers, rows, d): grads wrt every hooked layer output (heads + decoder), summed into
-    the residual chain as the backward walks down the stack."""
+    the residual chain as the backward walks down the stack.  on_layer_done(i) is called once layer
+    i's parameter gradients are all issued (bucketed all-reduce overlap, kdfm/ddp.py)."""
     dout = dfeats[cfg.n_layers - 1]
     for i in range(cfg.n_layers - 1, -1, -1):
         L = f"{prefix}layers.{i}."
         dx = layer_backward(cfg, S, P, G, L, i, run.layers[i], dout, pos_emb, len2, seed=seed, salt=salt)
         run.layers[i] = None
+        if on_layer_done is not None:
+            on_layer_done(i)
         if i > 0:
             K.axpby(dfeats[i - 1], dx, dfeats[i - 1], 1.0, 1.0)
             dout = dfeats[i - 1]

@@ -34,6 +34,75 @@ class FlatGradAllReduce:
         return 1.0 / self.world
 
 
+class BucketedGradAllReduce:
+    """Bucketed all-reduce overlapped with the backward (2-4 buckets in reverse
+    layer order, each launched as soon as its gradients are final).
+
+    The flat gradient buffer is laid out encoder (subsampling, layers 0..15), decoder, heads, and the
+    backward finalises it from the END: heads, then the decoder, then layers 15..0, then the
+    subsampling.  Ver5Engine.backward calls `ready(flat, offset)` whenever every gradient at index
+    >= offset is final (after the heads, the decoder, every encoder layer); each bucket
+    [lo, hi) with lo >= offset that has not been launched yet is all-reduced asynchronously on a
+    communication stream that first waits for the main stream AND the weight-gradient side stream
+    (kdfm.overlap.WGRAD), so RCCL over xGMI runs while the dX chain of the lower layers continues.
+    `__call__(flat)` (after the backward) launches what is left, makes the current stream wait for
+    every collective and returns the 1/world mean scale for the fused AdamW.  With no ready() calls
+    it is exactly FlatGradAllReduce with `buckets` chunks.  Bucket edges are aligned to 64 floats."""
+
+    def __init__(self, numel: int, group=None, buckets: int = 4):
+        self.group = group
+        self.world = dist.get_world_size(group)
+        nb = max(1, int(buckets))
+        step = -(-numel // nb)
+        step = -(-step // 64) * 64
+        self.edges = [min(numel, i * step) for i in range(nb)] + [numel]
+        self.edges = sorted(set(self.edges))
+        self._works = []
+        self._launched = set()
+        self._comm = None
+
+    def _stream(self, flat):
+        if not flat.is_cuda:
+            return None
+        if self._comm is None:
+            self._comm = torch.cuda.Stream(device=flat.device)
+        return self._comm
+
+    def _launch(self, flat, k: int):
+        lo, hi = self.edges[k], self.edges[k + 1]
+        comm = self._stream(flat)
+        if comm is None:
+            self._works.append(dist.all_reduce(flat[lo:hi], group=self.group, async_op=True))
+        else:
+            from .overlap import WGRAD
+            comm.wait_stream(torch.cuda.current_stream(flat.device))
+            WGRAD.fence(comm)
+            with torch.cuda.stream(comm):
+                self._works.append(dist.all_reduce(flat[lo:hi], group=self.group, async_op=True))
+        self._launched.add(k)
+
+    def ready(self, flat: torch.Tensor, offset: int) -> None:
+        if self.world == 1:
+            return
+        for k in range(len(self.edges) - 2, -1, -1):
+            if k not in self._launched and self.edges[k] >= offset:
+                self._launch(flat, k)
+
+    def __call__(self, flat: torch.Tensor) -> float:
+        if self.world == 1:
+            return 1.0
+        for k in range(len(self.edges) - 2, -1, -1):
+            if k not in self._launched:
+                self._launch(flat, k)
+        for w in self._works:
+            w.wait()   # device-side: the current stream waits for the collective
+        if self._comm is not None:
+            torch.cuda.current_stream(flat.device).wait_stream(self._comm)
+        self._works.clear()
+        self._launched.clear()
+        return 1.0 / self.world
+
+
 def max_over_ranks(value: float, device) -> float:
     """Max of a host float over all ranks (bench timing: the slowest rank defines the step)."""
     if not dist.is_initialized() or dist.get_world_size() == 1:

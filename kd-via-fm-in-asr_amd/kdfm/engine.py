@@ -231,14 +231,20 @@ class Ver5Engine:
         acc = ctx["acc"]
         K.loss_combine(ctx["nll"], acc[0:1], acc[1:2], acc[2:3], self.cfg.kd_alpha, self.losses)
 
-    def backward(self, ctx):
+    def backward(self, ctx, grad_ready=None):
+        """grad_ready(offset): optional callback, called whenever every student gradient at flat
+        index >= offset is final (BucketedGradAllReduce.ready overlap)."""
         cfg = self.cfg
         P, G = self.student.P, self.student.G
+        off = self.student.offsets
         Ss = ctx["Ss"]
         n = cfg.n_layers * Ss.rows
         self.student.zero_grad()
         dfeats = torch.empty(cfg.n_layers, Ss.rows, Ss.d, device=self.device)
         heads_backward(cfg, P, G, ctx.pop("hctx"), self.hws, dfeats.view(n, Ss.d), seed=self.seed)
+        dec0 = off["decoder.decoder_layers.0.weight"]
+        if grad_ready is not None:
+            grad_ready(min(o for k, o in off.items() if not k.startswith(("encoder.", "decoder."))))
         # decoder: logits = W enc + b ; grad wrt logits from CTC + KL
         g = ctx.pop("glogits")
         Cn = cfg.classes
@@ -246,8 +252,15 @@ class Ver5Engine:
         K.linear_dw(g, ctx["sfeats"][-1], G["decoder.decoder_layers.0.weight"].view(Cn, Ss.d), db=G["decoder.decoder_layers.0.bias"])
         K.linear_dx(g, Wd, dfeats[-1], R=dfeats[-1], rscale=1.0)
         del g
+        layer_done = None
+        if grad_ready is not None:
+            grad_ready(min(dec0, off["decoder.decoder_layers.0.bias"]))
+            firsts = {i: min(o for k, o in off.items() if k.startswith(f"encoder.layers.{i}."))
+                      for i in range(cfg.n_layers)}
+            layer_done = lambda i: grad_ready(firsts[i])  # noqa: E731
         encoder_backward(cfg, Ss, P, G, "encoder.", ctx.pop("srun"), dfeats, ctx["pos_s"], ctx["len1"],
-                         ctx["len2"], seed=self.seed, salt=SALT_STUDENT, ws=self._enc_ws(Ss))
+                         ctx["len2"], seed=self.seed, salt=SALT_STUDENT, ws=self._enc_ws(Ss),
+                         on_layer_done=layer_done)
 
     def optimizer_step(self, grad_scale: float = 1.0):
         cfg = self.cfg
@@ -264,7 +277,9 @@ class Ver5Engine:
         """forward + backward + (all-reduce) + AdamW.  Returns the device loss vector."""
         self.advance_rng()
         ctx = self.forward(wav, wav_len, targets, tgt_len, train=True)
-        self.backward(ctx)
+        ready = getattr(allreduce, "ready", None)
+        grad = self.student.grad
+        self.backward(ctx, grad_ready=(lambda o: ready(grad, o)) if ready is not None else None)
         del ctx
         scale = 1.0
         if allreduce is not None:

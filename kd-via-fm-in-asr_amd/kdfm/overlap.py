@@ -48,6 +48,11 @@ class WgradOverlap:
         self._keep.extend(keep)
         self._pending = True
 
+    def fence(self, stream) -> None:
+        """`stream` waits for every side-stream launch issued so far (no effect when none pending)."""
+        if self._pending:
+            stream.wait_stream(self._stream(stream.device))
+
     def join(self):
         """Main stream waits for all side-stream work; releases the kept operands."""
         if not self._pending:
