@@ -1,0 +1,116 @@
+"""Checkpoint interop (kdfm/checkpoint.py) on CPU stores: reference key
+names, Lightning .ckpt round trip with the flat AdamW moments (resume), .nemo archive round trip,
+teacher initialisation from a stand-alone Conformer-CTC .nemo (encoder./decoder. -> teacher.*),
+and the inference script's strict=False contract (asr_inference_diffm.py:486-492)."""
+import io
+import os
+import tarfile
+from dataclasses import replace
+
+import pytest
+import torch
+
+from kdfm import checkpoint as C
+from kdfm.config import DEFAULT
+from kdfm.engine import Ver5Engine
+
+
+@pytest.fixture()
+def eng():
+    cfg = replace(DEFAULT, n_layers=2)
+    e = Ver5Engine(cfg, "cpu", init=False)
+    g = torch.Generator().manual_seed(3)
+    for st in (e.student, e.teacher, e.bn):
+        st.data.copy_(torch.randn(st.data.shape, generator=g))
+    e.student.exp_avg.copy_(torch.randn(e.student.numel, generator=g))
+    e.student.exp_avg_sq.copy_(torch.rand(e.student.numel, generator=g))
+    e.step.fill_(123)
+    return e
+
+
+def _same(a, b):
+    """per-parameter equality of two FlatStores (the alignment padding is not state)"""
+    return all(torch.equal(a.P[n], b.P[n]) for n, _ in a.specs)
+
+
+def _fresh():
+    return Ver5Engine(replace(DEFAULT, n_layers=2), "cpu", init=False)
+
+
+def test_state_dict_reference_names(eng):
+    sd = C.engine_state_dict(eng)
+    for k in ("encoder.pre_encode.conv.0.weight", "encoder.layers.1.self_attn.pos_bias_u",
+              "encoder.layers.0.conv.batch_norm.running_var", "encoder.layers.0.conv.batch_norm.num_batches_tracked",
+              "decoder.decoder_layers.0.weight", "denoiser.net.0.weight", "fm_latent.fm.meta_encoder.0.weight",
+              "teacher.encoder.layers.1.feed_forward2.linear2.weight", "teacher.decoder.decoder_layers.0.bias",
+              "preprocessor.featurizer.fb", "teacher.preprocessor.featurizer.window"):
+        assert k in sd, k
+    assert sd["preprocessor.featurizer.fb"].shape[0] == 1
+    assert sd["decoder.decoder_layers.0.weight"].shape == (DEFAULT.classes, DEFAULT.d_student, 1)
+
+
+def test_lightning_roundtrip_and_resume(eng, tmp_path):
+    p = str(tmp_path / "last.ckpt")
+    C.save_lightning_ckpt(eng, p, epoch=4)
+    e2 = _fresh()
+    info = C.restore_lightning_ckpt(e2, p, strict=True)
+    assert info["resumed_optimizer"] and info["epoch"] == 4 and info["global_step"] == 123
+    assert info["frontend_mismatch"] == [] and info["unexpected"] == []
+    assert _same(eng.student, e2.student) and _same(eng.teacher, e2.teacher) and _same(eng.bn, e2.bn)
+    assert torch.equal(eng.student.exp_avg, e2.student.exp_avg)
+    assert torch.equal(eng.student.exp_avg_sq, e2.student.exp_avg_sq)
+    assert int(e2.step) == 123
+    # the inference script's load: ckpt["state_dict"], strict=False, on a model without the teacher
+    ck = C.read_lightning_ckpt(p)
+    sd = {k: v for k, v in ck["state_dict"].items() if not k.startswith("teacher.")}
+    e3 = _fresh()
+    info = C.load_engine_state(e3, sd, strict=False)
+    assert all(k.startswith("teacher.") for k in info["missing"])
+    assert _same(e3.student, eng.student)
+
+
+def test_shape_mismatch_raises(eng):
+    sd = C.engine_state_dict(eng)
+    sd["decoder.decoder_layers.0.bias"] = torch.zeros(7)
+    with pytest.raises(ValueError):
+        C.load_engine_state(_fresh(), sd)
+
+
+def test_unexpected_keys_strict(eng):
+    sd = C.engine_state_dict(eng)
+    sd["fm_latent_2.fm.time_embed.weight"] = torch.zeros(1)   # unused by ver5: ignored
+    sd["layer_proj.0.weight"] = torch.zeros(1)
+    assert C.load_engine_state(_fresh(), sd)["unexpected"] == ["layer_proj.0.weight"]
+    with pytest.raises(KeyError):
+        C.load_engine_state(_fresh(), sd, strict=True)
+
+
+def test_nemo_roundtrip(eng, tmp_path):
+    p = str(tmp_path / "student.nemo")
+    C.save_nemo(eng, p, {"encoder": {"d_model": 88, "n_layers": 2}, "target": "kdfm"})
+    cfg, sd = C.read_nemo(p)
+    assert cfg["encoder"]["d_model"] == 88
+    assert not any(k.startswith("teacher.") for k in sd)
+    e2 = _fresh()
+    C.load_engine_state(e2, sd)
+    assert _same(e2.student, eng.student)
+
+
+def test_teacher_from_nemo_gz(eng, tmp_path):
+    """A stand-alone EncDecCTCModelBPE .nemo (gzip'd tar, './'-prefixed names, tokenizer files)."""
+    sd = {k[len("teacher."):]: v for k, v in C.engine_state_dict(eng).items() if k.startswith("teacher.")}
+    wbuf = io.BytesIO()
+    torch.save(sd, wbuf)
+    p = str(tmp_path / "stt_en_conformer_ctc_small.nemo")
+    with tarfile.open(p, "w:gz") as tf:
+        for name, data in (("./model_config.yaml", b"encoder:\n  d_model: 176\n"),
+                           ("./model_weights.ckpt", wbuf.getvalue()), ("./tokenizer.model", b"\x00")):
+            ti = tarfile.TarInfo(name)
+            ti.size = len(data)
+            tf.addfile(ti, io.BytesIO(data))
+    e2 = _fresh()
+    info = C.load_teacher_nemo(e2, p)
+    assert info["config"]["encoder"]["d_model"] == 176
+    assert _same(e2.teacher, eng.teacher)
+    tb = [n for n, _ in e2.bn.specs if n.startswith("teacher.")]
+    assert all(torch.equal(e2.bn.P[n], eng.bn.P[n]) for n in tb)
