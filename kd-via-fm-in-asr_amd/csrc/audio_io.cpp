@@ -1,0 +1,634 @@
+// audio_io.cpp — native audio decode + batch collate for the ver5 data path (include/kdfm_io.h).
+//
+// Replaces the soundfile decode inside NeMo's AudioToBPEDataset workers (the dataset the reference
+// builds in ctc_bpe_models.py:96-165 from the manifests of asr_train_diffm.py:31-88) and the
+// zero-padding collate that follows.  Host code only: decoding is branchy integer work on a few
+// hundred KB per utterance, it belongs on the host cores next to the pinned staging buffer that the
+// step's H2D copy reads (kdfm/data.py), never on the GPU.
+//
+// FLAC: a straight decoder of the published format (metadata, frame header + CRC-8, subframes
+// CONSTANT / VERBATIM / FIXED(0..4) / LPC(1..32), partitioned Rice / Rice2 residuals with escape
+// partitions, wasted bits, the four channel assignments, byte-aligned CRC-16 footer).
+// WAV: RIFF chunks, PCM u8/s16/s24/s32, IEEE float32/64, WAVE_FORMAT_EXTENSIBLE.
+// Float conversion follows libsndfile/soundfile (integer / 2^(bits-1)); the mono mix follows
+// NeMo AudioSegment (float32 mean over channels).
+#include "kdfm_io.h"
+
+#include <algorithm>
+#include <atomic>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+bool read_file(const char* path, std::vector<uint8_t>& buf) {
+  FILE* f = std::fopen(path, "rb");
+  if (!f) return false;
+  std::fseek(f, 0, SEEK_END);
+  long sz = std::ftell(f);
+  std::fseek(f, 0, SEEK_SET);
+  if (sz < 0) {
+    std::fclose(f);
+    return false;
+  }
+  buf.resize((size_t)sz);
+  size_t got = sz ? std::fread(buf.data(), 1, (size_t)sz, f) : 0;
+  std::fclose(f);
+  return got == (size_t)sz;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Output sink: mono float32, frames [offset, offset + limit) of the stream.
+struct Sink {
+  float* out = nullptr;
+  int64_t capacity = 0;
+  int64_t offset = 0;
+  int64_t limit = -1;  // < 0: unbounded
+  int64_t pos = 0;     // stream frame index of the next frame
+  int64_t written = 0;
+  bool overflow = false;
+  bool done() const { return limit >= 0 && pos >= offset + limit; }
+  // one frame given per-channel values already scaled to float
+  inline void put(float v) {
+    if (pos >= offset && (limit < 0 || pos < offset + limit)) {
+      if (written < capacity)
+        out[written++] = v;
+      else
+        overflow = true;
+    }
+    ++pos;
+  }
+};
+
+// ---------------------------------------------------------------------------------------------
+// MSB-first bit reader over a byte buffer.
+struct BitReader {
+  const uint8_t* d;
+  size_t size;
+  size_t bit = 0;
+  bool bad = false;
+
+  BitReader(const uint8_t* d_, size_t n) : d(d_), size(n) {}
+
+  inline uint64_t load8(size_t byte) const {
+    uint64_t v = 0;
+    if (byte + 8 <= size) {
+      std::memcpy(&v, d + byte, 8);
+      v = __builtin_bswap64(v);
+    } else {
+      for (int i = 0; i < 8; ++i) v = (v << 8) | (byte + i < size ? d[byte + i] : 0u);
+    }
+    return v;
+  }
+  // the next >= 57 bits, left aligned
+  inline uint64_t peek() const { return load8(bit >> 3) << (bit & 7); }
+  inline uint32_t get(int k) {  // 0 <= k <= 32
+    if (k == 0) return 0;
+    uint32_t v = (uint32_t)(peek() >> (64 - k));
+    bit += (size_t)k;
+    if (bit > size * 8) bad = true;
+    return v;
+  }
+  inline int64_t sget(int k) {  // two's-complement, 0 <= k <= 33
+    if (k == 0) return 0;
+    uint64_t v;
+    if (k <= 32) {
+      v = get(k);
+    } else {
+      v = (uint64_t)get(k - 32) << 32;
+      v |= get(32);
+    }
+    uint64_t sign = 1ull << (k - 1);
+    return (int64_t)((v ^ sign) - sign);
+  }
+  inline uint32_t unary() {  // count of 0 bits before the next 1
+    uint32_t cnt = 0;
+    for (;;) {
+      uint64_t w = peek();
+      if (w) {
+        int z = __builtin_clzll(w);
+        if (z < 57) {
+          cnt += (uint32_t)z;
+          bit += (size_t)z + 1;
+          if (bit > size * 8) bad = true;
+          return cnt;
+        }
+      }
+      cnt += 56;
+      bit += 56;
+      if (bit > size * 8) {
+        bad = true;
+        return cnt;
+      }
+    }
+  }
+  void align() { bit = (bit + 7) & ~(size_t)7; }
+  size_t byte() const { return bit >> 3; }
+};
+
+uint8_t crc8(const uint8_t* p, size_t n) {
+  uint8_t c = 0;
+  for (size_t i = 0; i < n; ++i) {
+    c ^= p[i];
+    for (int b = 0; b < 8; ++b) c = (uint8_t)((c & 0x80) ? (c << 1) ^ 0x07 : (c << 1));
+  }
+  return c;
+}
+
+uint16_t crc16(const uint8_t* p, size_t n) {
+  static uint16_t table[256];
+  static std::once_flag once;
+  std::call_once(once, [] {
+    for (int i = 0; i < 256; ++i) {
+      uint16_t c = (uint16_t)(i << 8);
+      for (int b = 0; b < 8; ++b) c = (uint16_t)((c & 0x8000) ? (c << 1) ^ 0x8005 : (c << 1));
+      table[i] = c;
+    }
+  });
+  uint16_t c = 0;
+  for (size_t i = 0; i < n; ++i) c = (uint16_t)((c << 8) ^ table[((c >> 8) ^ p[i]) & 0xff]);
+  return c;
+}
+
+// ---------------------------------------------------------------------------------------------
+// FLAC
+struct FlacInfo {
+  int32_t rate = 0, channels = 0, bps = 0;
+  int64_t total = 0;
+  size_t first_frame = 0;
+};
+
+int flac_header(const std::vector<uint8_t>& b, FlacInfo& fi) {
+  size_t p = 0;
+  // tolerate a leading ID3v2 tag
+  if (b.size() >= 10 && std::memcmp(b.data(), "ID3", 3) == 0) {
+    size_t tag = ((size_t)(b[6] & 0x7f) << 21) | ((size_t)(b[7] & 0x7f) << 14) |
+                 ((size_t)(b[8] & 0x7f) << 7) | (size_t)(b[9] & 0x7f);
+    p = 10 + tag;
+  }
+  if (b.size() < p + 4 || std::memcmp(b.data() + p, "fLaC", 4) != 0)
+    return fail(KDFM_IO_ERR_FORMAT, "not a FLAC stream");
+  p += 4;
+  bool have_info = false;
+  for (;;) {
+    if (p + 4 > b.size()) return fail(KDFM_IO_ERR_CORRUPT, "truncated FLAC metadata");
+    bool last = b[p] & 0x80;
+    int type = b[p] & 0x7f;
+    size_t len = ((size_t)b[p + 1] << 16) | ((size_t)b[p + 2] << 8) | b[p + 3];
+    p += 4;
+    if (p + len > b.size()) return fail(KDFM_IO_ERR_CORRUPT, "truncated FLAC metadata block");
+    if (type == 0) {
+      if (len < 34) return fail(KDFM_IO_ERR_CORRUPT, "short STREAMINFO");
+      BitReader br(b.data() + p, len);
+      br.get(16);
+      br.get(16);
+      br.get(24);
+      br.get(24);
+      fi.rate = (int32_t)br.get(20);
+      fi.channels = (int32_t)br.get(3) + 1;
+      fi.bps = (int32_t)br.get(5) + 1;
+      fi.total = ((int64_t)br.get(4) << 32) | br.get(32);
+      have_info = true;
+    }
+    p += len;
+    if (last) break;
+  }
+  if (!have_info) return fail(KDFM_IO_ERR_FORMAT, "FLAC stream without STREAMINFO");
+  fi.first_frame = p;
+  return KDFM_IO_OK;
+}
+
+int flac_residual(BitReader& br, int bs, int order, int64_t* res) {
+  uint32_t method = br.get(2);
+  if (method > 1) return fail(KDFM_IO_ERR_CORRUPT, "reserved residual coding method");
+  int pbits = method == 0 ? 4 : 5;
+  uint32_t esc = method == 0 ? 15u : 31u;
+  int porder = (int)br.get(4);
+  int parts = 1 << porder;
+  int psize = bs >> porder;
+  if ((psize << porder) != bs || psize < order)
+    return fail(KDFM_IO_ERR_CORRUPT, "bad residual partition order");
+  int64_t* r = res;
+  for (int p = 0; p < parts; ++p) {
+    int n = p == 0 ? psize - order : psize;
+    uint32_t k = br.get(pbits);
+    if (k == esc) {
+      int nb = (int)br.get(5);
+      for (int i = 0; i < n; ++i) r[i] = br.sget(nb);
+    } else {
+      for (int i = 0; i < n; ++i) {
+        uint64_t q = br.unary();
+        uint64_t u = (q << k) | br.get((int)k);
+        r[i] = (int64_t)(u >> 1) ^ -(int64_t)(u & 1);
+      }
+    }
+    r += n;
+    if (br.bad) return fail(KDFM_IO_ERR_CORRUPT, "truncated residual");
+  }
+  return KDFM_IO_OK;
+}
+
+int flac_subframe(BitReader& br, int bs, int bps, int64_t* x, std::vector<int64_t>& res) {
+  if (br.get(1) != 0) return fail(KDFM_IO_ERR_CORRUPT, "subframe padding bit set");
+  uint32_t type = br.get(6);
+  int wasted = 0;
+  if (br.get(1)) wasted = (int)br.unary() + 1;
+  int sb = bps - wasted;
+  if (sb <= 0) return fail(KDFM_IO_ERR_CORRUPT, "wasted bits exceed sample size");
+  if (type == 0) {
+    int64_t v = br.sget(sb);
+    for (int i = 0; i < bs; ++i) x[i] = v;
+  } else if (type == 1) {
+    for (int i = 0; i < bs; ++i) x[i] = br.sget(sb);
+  } else if (type >= 8 && type <= 12) {
+    int order = (int)type - 8;
+    if (order > bs) return fail(KDFM_IO_ERR_CORRUPT, "FIXED order exceeds block size");
+    for (int i = 0; i < order; ++i) x[i] = br.sget(sb);
+    int rc = flac_residual(br, bs, order, res.data());
+    if (rc) return rc;
+    const int64_t* r = res.data();
+    switch (order) {
+      case 0: for (int i = 0; i < bs; ++i) x[i] = r[i]; break;
+      case 1: for (int i = 1; i < bs; ++i) x[i] = r[i - 1] + x[i - 1]; break;
+      case 2: for (int i = 2; i < bs; ++i) x[i] = r[i - 2] + 2 * x[i - 1] - x[i - 2]; break;
+      case 3:
+        for (int i = 3; i < bs; ++i) x[i] = r[i - 3] + 3 * x[i - 1] - 3 * x[i - 2] + x[i - 3];
+        break;
+      case 4:
+        for (int i = 4; i < bs; ++i)
+          x[i] = r[i - 4] + 4 * x[i - 1] - 6 * x[i - 2] + 4 * x[i - 3] - x[i - 4];
+        break;
+    }
+  } else if (type >= 32) {
+    int order = (int)(type & 31) + 1;
+    if (order > bs) return fail(KDFM_IO_ERR_CORRUPT, "LPC order exceeds block size");
+    for (int i = 0; i < order; ++i) x[i] = br.sget(sb);
+    int prec = (int)br.get(4) + 1;
+    if (prec == 16) return fail(KDFM_IO_ERR_CORRUPT, "invalid LPC precision");
+    int shift = (int)br.sget(5);
+    if (shift < 0) return fail(KDFM_IO_ERR_CORRUPT, "negative LPC shift");
+    int64_t coef[32];
+    for (int j = 0; j < order; ++j) coef[j] = br.sget(prec);
+    int rc = flac_residual(br, bs, order, res.data());
+    if (rc) return rc;
+    const int64_t* r = res.data();
+    for (int i = order; i < bs; ++i) {
+      int64_t acc = 0;
+      for (int j = 0; j < order; ++j) acc += coef[j] * x[i - 1 - j];
+      x[i] = r[i - order] + (acc >> shift);
+    }
+  } else {
+    return fail(KDFM_IO_ERR_CORRUPT, "reserved subframe type");
+  }
+  if (wasted)
+    for (int i = 0; i < bs; ++i) x[i] = (int64_t)((uint64_t)x[i] << wasted);
+  if (br.bad) return fail(KDFM_IO_ERR_CORRUPT, "truncated subframe");
+  return KDFM_IO_OK;
+}
+
+int flac_decode(const std::vector<uint8_t>& b, Sink& sink, int32_t* rate_out) {
+  FlacInfo fi;
+  int rc = flac_header(b, fi);
+  if (rc) return rc;
+  if (rate_out) *rate_out = fi.rate;
+  // per-thread scratch, grown once and reused across files: fresh multi-MB allocations per file
+  // page-fault under the address-space lock and serialise the batch threads
+  thread_local std::vector<int64_t> chan, res;
+  if (chan.size() < (size_t)8 * 65536) {
+    chan.resize((size_t)8 * 65536);
+    res.resize(65536);
+  }
+  size_t p = fi.first_frame;
+  const uint8_t* d = b.data();
+  while (p + 2 <= b.size() && !sink.done()) {
+    // frame sync (frames are byte aligned and contiguous; skip stray bytes defensively)
+    if (!(d[p] == 0xff && (d[p + 1] & 0xfe) == 0xf8)) {
+      ++p;
+      continue;
+    }
+    size_t frame_start = p;
+    BitReader br(d + p, b.size() - p);
+    br.get(14);
+    if (br.get(1)) return fail(KDFM_IO_ERR_CORRUPT, "reserved frame header bit");
+    br.get(1);  // blocking strategy
+    uint32_t bs_code = br.get(4), sr_code = br.get(4), ch_code = br.get(4), ss_code = br.get(3);
+    if (br.get(1)) return fail(KDFM_IO_ERR_CORRUPT, "reserved frame header bit");
+    // UTF-8-style coded frame/sample number
+    uint32_t c0 = br.get(8);
+    int extra = 0;
+    if (c0 & 0x80) {
+      if ((c0 & 0xe0) == 0xc0) extra = 1;
+      else if ((c0 & 0xf0) == 0xe0) extra = 2;
+      else if ((c0 & 0xf8) == 0xf0) extra = 3;
+      else if ((c0 & 0xfc) == 0xf8) extra = 4;
+      else if ((c0 & 0xfe) == 0xfc) extra = 5;
+      else if (c0 == 0xfe) extra = 6;
+      else return fail(KDFM_IO_ERR_CORRUPT, "bad coded frame number");
+    }
+    for (int i = 0; i < extra; ++i)
+      if ((br.get(8) & 0xc0) != 0x80) return fail(KDFM_IO_ERR_CORRUPT, "bad coded frame number");
+    int bs;
+    if (bs_code == 0) return fail(KDFM_IO_ERR_CORRUPT, "reserved block size");
+    else if (bs_code == 1) bs = 192;
+    else if (bs_code <= 5) bs = 576 << (bs_code - 2);
+    else if (bs_code == 6) bs = (int)br.get(8) + 1;
+    else if (bs_code == 7) bs = (int)br.get(16) + 1;
+    else bs = 256 << (bs_code - 8);
+    if (sr_code == 12) br.get(8);
+    else if (sr_code == 13 || sr_code == 14) br.get(16);
+    else if (sr_code == 15) return fail(KDFM_IO_ERR_CORRUPT, "invalid sample rate code");
+    int bps;
+    switch (ss_code) {
+      case 0: bps = fi.bps; break;
+      case 1: bps = 8; break;
+      case 2: bps = 12; break;
+      case 4: bps = 16; break;
+      case 5: bps = 20; break;
+      case 6: bps = 24; break;
+      case 7: bps = 32; break;
+      default: return fail(KDFM_IO_ERR_CORRUPT, "reserved sample size");
+    }
+    size_t hdr_len = br.byte();
+    uint32_t crc_h = br.get(8);
+    if (br.bad || crc8(d + frame_start, hdr_len) != crc_h)
+      return fail(KDFM_IO_ERR_CORRUPT, "FLAC frame header CRC-8 mismatch");
+    int nch;
+    if (ch_code <= 7) nch = (int)ch_code + 1;
+    else if (ch_code <= 10) nch = 2;
+    else return fail(KDFM_IO_ERR_CORRUPT, "reserved channel assignment");
+    if (nch != fi.channels) return fail(KDFM_IO_ERR_CORRUPT, "frame channel count differs from STREAMINFO");
+    for (int c = 0; c < nch; ++c) {
+      int cb = bps;
+      if ((ch_code == 8 && c == 1) || (ch_code == 9 && c == 0) || (ch_code == 10 && c == 1)) cb += 1;
+      rc = flac_subframe(br, bs, cb, chan.data() + (size_t)c * 65536, res);
+      if (rc) return rc;
+    }
+    br.align();
+    size_t body = br.byte();
+    uint32_t crc_f = br.get(16);
+    if (br.bad || crc16(d + frame_start, body) != crc_f)
+      return fail(KDFM_IO_ERR_CORRUPT, "FLAC frame CRC-16 mismatch");
+    int64_t* c0p = chan.data();
+    int64_t* c1p = chan.data() + 65536;
+    if (ch_code == 8) {
+      for (int i = 0; i < bs; ++i) c1p[i] = c0p[i] - c1p[i];
+    } else if (ch_code == 9) {
+      for (int i = 0; i < bs; ++i) c0p[i] = c0p[i] + c1p[i];
+    } else if (ch_code == 10) {
+      for (int i = 0; i < bs; ++i) {
+        int64_t side = c1p[i];
+        int64_t mid = (int64_t)((uint64_t)c0p[i] << 1) | (side & 1);
+        c0p[i] = (mid + side) >> 1;
+        c1p[i] = (mid - side) >> 1;
+      }
+    }
+    const float scale = 1.0f / (float)(1ull << (bps - 1));
+    if (nch == 1) {
+      for (int i = 0; i < bs; ++i) sink.put((float)c0p[i] * scale);
+    } else {
+      const float fn = (float)nch;
+      for (int i = 0; i < bs; ++i) {
+        float s = 0.f;
+        for (int c = 0; c < nch; ++c) s += (float)chan[(size_t)c * 65536 + i] * scale;
+        sink.put(s / fn);
+      }
+    }
+    p = frame_start + br.byte();
+  }
+  return KDFM_IO_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// RIFF WAV
+struct WavInfo {
+  int32_t rate = 0, channels = 0, bits = 0, fmt = 0;  // fmt: 1 PCM, 3 IEEE float
+  size_t data = 0, data_len = 0;
+};
+
+inline uint32_t le32(const uint8_t* p) { return p[0] | (p[1] << 8) | (p[2] << 16) | ((uint32_t)p[3] << 24); }
+inline uint16_t le16(const uint8_t* p) { return (uint16_t)(p[0] | (p[1] << 8)); }
+
+int wav_header(const std::vector<uint8_t>& b, WavInfo& wi) {
+  if (b.size() < 12 || std::memcmp(b.data(), "RIFF", 4) != 0 || std::memcmp(b.data() + 8, "WAVE", 4) != 0)
+    return fail(KDFM_IO_ERR_FORMAT, "not a RIFF/WAVE stream");
+  size_t p = 12;
+  bool have_fmt = false, have_data = false;
+  while (p + 8 <= b.size()) {
+    const uint8_t* c = b.data() + p;
+    size_t len = le32(c + 4);
+    size_t body = p + 8;
+    if (std::memcmp(c, "fmt ", 4) == 0) {
+      if (len < 16 || body + len > b.size()) return fail(KDFM_IO_ERR_CORRUPT, "bad fmt chunk");
+      wi.fmt = le16(b.data() + body);
+      wi.channels = le16(b.data() + body + 2);
+      wi.rate = (int32_t)le32(b.data() + body + 4);
+      wi.bits = le16(b.data() + body + 14);
+      if (wi.fmt == 0xFFFE) {
+        if (len < 40) return fail(KDFM_IO_ERR_CORRUPT, "short WAVE_FORMAT_EXTENSIBLE");
+        wi.fmt = le16(b.data() + body + 24);  // SubFormat GUID's leading format code
+      }
+      have_fmt = true;
+    } else if (std::memcmp(c, "data", 4) == 0) {
+      wi.data = body;
+      wi.data_len = (len == 0xFFFFFFFFu || body + len > b.size()) ? b.size() - body : len;
+      have_data = true;
+      break;
+    }
+    p = body + len + (len & 1);
+  }
+  if (!have_fmt || !have_data) return fail(KDFM_IO_ERR_FORMAT, "WAV without fmt/data chunk");
+  if (wi.channels <= 0) return fail(KDFM_IO_ERR_FORMAT, "WAV with zero channels");
+  bool ok = (wi.fmt == 1 && (wi.bits == 8 || wi.bits == 16 || wi.bits == 24 || wi.bits == 32)) ||
+            (wi.fmt == 3 && (wi.bits == 32 || wi.bits == 64));
+  if (!ok) return fail(KDFM_IO_ERR_FORMAT, "unsupported WAV encoding (format " +
+                                               std::to_string(wi.fmt) + ", " + std::to_string(wi.bits) + " bits)");
+  return KDFM_IO_OK;
+}
+
+inline float wav_sample(const uint8_t* s, const WavInfo& wi) {
+  if (wi.fmt == 3) {
+    if (wi.bits == 32) {
+      float f;
+      std::memcpy(&f, s, 4);
+      return f;
+    }
+    double g;
+    std::memcpy(&g, s, 8);
+    return (float)g;
+  }
+  switch (wi.bits) {
+    case 8: return (float)((int)s[0] - 128) * (1.0f / 128.0f);
+    case 16: return (float)(int16_t)le16(s) * (1.0f / 32768.0f);
+    case 24: {
+      int32_t v = (int32_t)((uint32_t)s[0] << 8 | (uint32_t)s[1] << 16 | (uint32_t)s[2] << 24) >> 8;
+      return (float)v * (1.0f / 8388608.0f);
+    }
+    default: return (float)(int32_t)le32(s) * (1.0f / 2147483648.0f);
+  }
+}
+
+int wav_decode(const std::vector<uint8_t>& b, Sink& sink, int32_t* rate_out) {
+  WavInfo wi;
+  int rc = wav_header(b, wi);
+  if (rc) return rc;
+  if (rate_out) *rate_out = wi.rate;
+  size_t bpsamp = (size_t)wi.bits / 8, frame = bpsamp * (size_t)wi.channels;
+  int64_t frames = (int64_t)(wi.data_len / frame);
+  int64_t start = sink.offset < frames ? sink.offset : frames;
+  int64_t end = sink.limit < 0 ? frames : std::min<int64_t>(frames, sink.offset + sink.limit);
+  sink.pos = start;
+  const float fn = (float)wi.channels;
+  for (int64_t i = start; i < end; ++i) {
+    const uint8_t* f = b.data() + wi.data + (size_t)i * frame;
+    if (wi.channels == 1) {
+      sink.put(wav_sample(f, wi));
+    } else {
+      float s = 0.f;
+      for (int c = 0; c < wi.channels; ++c) s += wav_sample(f + c * bpsamp, wi);
+      sink.put(s / fn);
+    }
+  }
+  return KDFM_IO_OK;
+}
+
+bool is_flac(const std::vector<uint8_t>& b) {
+  if (b.size() >= 4 && std::memcmp(b.data(), "fLaC", 4) == 0) return true;
+  return b.size() >= 10 && std::memcmp(b.data(), "ID3", 3) == 0;
+}
+
+int decode_buffer(const std::vector<uint8_t>& b, Sink& sink, int32_t* rate) {
+  return is_flac(b) ? flac_decode(b, sink, rate) : wav_decode(b, sink, rate);
+}
+
+int probe_buffer(const std::vector<uint8_t>& b, int32_t* sr, int32_t* ch, int32_t* bits, int64_t* frames) {
+  if (is_flac(b)) {
+    FlacInfo fi;
+    int rc = flac_header(b, fi);
+    if (rc) return rc;
+    if (sr) *sr = fi.rate;
+    if (ch) *ch = fi.channels;
+    if (bits) *bits = fi.bps;
+    if (frames) *frames = fi.total;
+    if (fi.total == 0 && frames) {  // unknown length in STREAMINFO: count by decoding
+      Sink s;
+      s.capacity = 0;
+      rc = flac_decode(b, s, nullptr);
+      if (rc) return rc;
+      *frames = s.pos;
+    }
+    return KDFM_IO_OK;
+  }
+  WavInfo wi;
+  int rc = wav_header(b, wi);
+  if (rc) return rc;
+  if (sr) *sr = wi.rate;
+  if (ch) *ch = wi.channels;
+  if (bits) *bits = wi.bits;
+  if (frames) *frames = (int64_t)(wi.data_len / ((size_t)wi.bits / 8 * (size_t)wi.channels));
+  return KDFM_IO_OK;
+}
+
+int decode_path(const char* path, int64_t offset, int64_t max_frames, float* out, int64_t capacity,
+                int64_t* n_out, int32_t* rate) {
+  if (!path || (!out && capacity > 0) || capacity < 0 || offset < 0)
+    return fail(KDFM_IO_ERR_ARG, "kdfm_audio_decode: bad argument");
+  thread_local std::vector<uint8_t> buf;  // reused: see flac_decode's scratch
+  if (!read_file(path, buf)) return fail(KDFM_IO_ERR_OPEN, std::string("cannot read ") + path);
+  Sink s;
+  s.out = out;
+  s.capacity = capacity;
+  s.offset = offset;
+  s.limit = max_frames;
+  int rc = decode_buffer(buf, s, rate);
+  if (rc) {
+    g_err = std::string(path) + ": " + g_err;
+    return rc;
+  }
+  if (s.overflow)
+    return fail(KDFM_IO_ERR_ARG, std::string(path) + ": decoded audio exceeds the output capacity (" +
+                                     std::to_string(capacity) + " samples)");
+  if (n_out) *n_out = s.written;
+  return KDFM_IO_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int kdfm_audio_probe(const char* path, int32_t* sample_rate, int32_t* channels, int32_t* bits_per_sample,
+                     int64_t* frames) {
+  if (!path) return fail(KDFM_IO_ERR_ARG, "kdfm_audio_probe: null path");
+  std::vector<uint8_t> buf;
+  if (!read_file(path, buf)) return fail(KDFM_IO_ERR_OPEN, std::string("cannot read ") + path);
+  int rc = probe_buffer(buf, sample_rate, channels, bits_per_sample, frames);
+  if (rc) g_err = std::string(path) + ": " + g_err;
+  return rc;
+}
+
+int kdfm_audio_decode(const char* path, int64_t offset, int64_t max_frames, float* out, int64_t capacity,
+                      int64_t* n_out, int32_t* sample_rate) {
+  return decode_path(path, offset, max_frames, out, capacity, n_out, sample_rate);
+}
+
+int kdfm_audio_load_batch(const char* const* paths, int32_t n, const int64_t* offsets, const int64_t* max_frames,
+                          float* out, int64_t row_stride, int64_t* lens, int32_t expected_rate, int32_t threads) {
+  if (n < 0 || row_stride < 0 || (n > 0 && (!paths || !out || !lens)))
+    return fail(KDFM_IO_ERR_ARG, "kdfm_audio_load_batch: bad argument");
+  if (n == 0) return KDFM_IO_OK;
+  int nt = threads < 1 ? 1 : threads;
+  if (nt > n) nt = n;
+  std::atomic<int32_t> next{0};
+  std::mutex mu;
+  int first_rc = 0;
+  int32_t first_idx = n;
+  std::string first_msg;
+  auto work = [&]() {
+    for (;;) {
+      int32_t i = next.fetch_add(1);
+      if (i >= n) return;
+      float* row = out + (size_t)i * (size_t)row_stride;
+      int64_t got = 0;
+      int32_t rate = 0;
+      int rc = decode_path(paths[i], offsets ? offsets[i] : 0, max_frames ? max_frames[i] : -1, row, row_stride,
+                           &got, &rate);
+      if (rc == 0 && expected_rate > 0 && rate != expected_rate)
+        rc = fail(KDFM_IO_ERR_FORMAT, std::string(paths[i]) + ": sample rate " + std::to_string(rate) +
+                                          " != expected " + std::to_string(expected_rate) +
+                                          " (resampling is not part of the native path)");
+      if (rc) {
+        std::lock_guard<std::mutex> g(mu);
+        if (i < first_idx) {
+          first_idx = i;
+          first_rc = rc;
+          first_msg = g_err;
+        }
+        got = 0;
+      }
+      std::memset(row + got, 0, sizeof(float) * (size_t)(row_stride - got));
+      lens[i] = got;
+    }
+  };
+  std::vector<std::thread> pool;
+  for (int t = 1; t < nt; ++t) pool.emplace_back(work);
+  work();
+  for (auto& th : pool) th.join();
+  if (first_rc) return fail(first_rc, first_msg);
+  return KDFM_IO_OK;
+}
+
+const char* kdfm_io_last_error(void) { return g_err.c_str(); }
+
+const char* kdfm_io_version(void) { return "kdfm_io 0.1.0"; }
+
+}  // extern "C"

@@ -15,6 +15,9 @@ ROOT = os.path.dirname(PKG_DIR)  # kd-via-fm-in-asr_amd/
 CSRC = os.path.join(ROOT, "csrc")
 INCLUDE = os.path.join(os.path.dirname(ROOT), "include")
 LIB_PATH = os.path.join(PKG_DIR, "libkdfm.so")
+IO_LIB_PATH = os.path.join(PKG_DIR, "libkdfm_io.so")
+IO_SRC = os.path.join(CSRC, "audio_io.cpp")
+CXX = os.environ.get("CXX", "g++")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
@@ -23,7 +26,8 @@ CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-ffp-contract
 
 
 def _headers():
-    return glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(INCLUDE, "*.h"))
+    return glob.glob(os.path.join(CSRC, "*.h")) + [h for h in glob.glob(os.path.join(INCLUDE, "*.h"))
+                                                   if not h.endswith("kdfm_io.h")]
 
 
 def _compile(src: str, obj: str) -> str:
@@ -34,7 +38,24 @@ def _compile(src: str, obj: str) -> str:
     return obj
 
 
+def build_io(verbose: bool = False) -> str:
+    """libkdfm_io.so: the host-only audio decode / collate library (include/kdfm_io.h), g++."""
+    hdr = os.path.join(INCLUDE, "kdfm_io.h")
+    src_mtime = max(os.path.getmtime(IO_SRC), os.path.getmtime(hdr))
+    if os.path.exists(IO_LIB_PATH) and os.path.getmtime(IO_LIB_PATH) >= src_mtime:
+        return IO_LIB_PATH
+    cmd = [CXX, "-O3", "-std=c++17", "-fPIC", "-shared", "-pthread", "-Wall", f"-I{INCLUDE}",
+           IO_SRC, "-o", IO_LIB_PATH]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"g++ failed for audio_io.cpp:\n{r.stderr[-6000:]}")
+    if verbose:
+        print("linked", IO_LIB_PATH)
+    return IO_LIB_PATH
+
+
 def build(verbose: bool = False, jobs: int | None = None) -> str:
+    build_io(verbose)
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
     if not srcs:
         raise RuntimeError(f"no HIP sources under {CSRC}")
