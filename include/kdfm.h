@@ -287,6 +287,10 @@ int kdfm_relu_mask(const float* dy, const float* y, float* out, int64_t n, void*
 /* nn.MSELoss pieces: *loss_acc += scale * sum (a-b)^2 ; grad = gscale * (a-b) when grad != NULL */
 int kdfm_mse(const float* a, const float* b, float* grad, float* loss_acc, int64_t n, float scale, float gscale,
              void* stream);
+/* nn.L1Loss pieces (kd_crit, kd_loss_type "l1": asr_train_diffm.py:557, used by versions 1/3/4/8 at
+ * :675-727): *loss_acc += scale * sum |a-b| ; grad = gscale * sign(a-b) when grad != NULL */
+int kdfm_l1(const float* a, const float* b, float* grad, float* loss_acc, int64_t n, float scale, float gscale,
+            void* stream);
 /* NeMo Conv1d weight (O,I,K) -> fwd (O,K,I) and transposed+flipped bwd (I,K,O) GEMM layouts */
 int kdfm_convw_prep(const float* W, float* fwd, float* bwd, int64_t O, int64_t I, int64_t K, void* stream);
 /* dW(O,I,K) += alpha * G(O,K,I) */

@@ -57,6 +57,25 @@ __global__ __launch_bounds__(256) void mse_kernel(const float* __restrict__ a, c
   if (threadIdx.x == 0) atomicAdd(loss_acc, scale * (red[0] + red[1] + red[2] + red[3]));
 }
 
+// nn.L1Loss pieces (kd_crit with kd_loss_type="l1", asr_train_diffm.py:557): |a-b| summed, torch's
+// sign(a-b) subgradient (0 at a == b)
+__global__ __launch_bounds__(256) void l1_kernel(const float* __restrict__ a, const float* __restrict__ b,
+                                                 float* __restrict__ grad, float* __restrict__ loss_acc, int64_t n,
+                                                 float scale, float gscale) {
+  __shared__ float red[4];
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  float part = 0.f;
+  if (i < n) {
+    const float d = a[i] - b[i];
+    part = fabsf(d);
+    if (grad) grad[i] = d > 0.f ? gscale : (d < 0.f ? -gscale : 0.f);
+  }
+  part = wave_sum(part);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = part;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(loss_acc, scale * (red[0] + red[1] + red[2] + red[3]));
+}
+
 // out = scale * dropout(x) with the flat-index mask of the GEMM epilogue (idx = r*cols + c)
 __global__ __launch_bounds__(256) void dropout_kernel(const float* x, float* out, int64_t n, float p, float scale,
                                                       const uint64_t* seed_ptr, uint64_t st) {
@@ -296,6 +315,14 @@ int kdfm_mse(const float* a, const float* b, float* grad, float* loss_acc, int64
   KDFM_REQUIRE(a && b && loss_acc, "null pointer");
   KDFM_1D(mse_kernel, n, a, b, grad, loss_acc, n, scale, gscale);
   return check_launch("kdfm_mse");
+}
+
+int kdfm_l1(const float* a, const float* b, float* grad, float* loss_acc, int64_t n, float scale, float gscale,
+            void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(a && b && loss_acc, "null pointer");
+  KDFM_1D(l1_kernel, n, a, b, grad, loss_acc, n, scale, gscale);
+  return check_launch("kdfm_l1");
 }
 
 int kdfm_qkv_prep(const float* qkv, const float* pos_bias_u, const float* pos_bias_v, float* qu, float* qv,

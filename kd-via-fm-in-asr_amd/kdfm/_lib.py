@@ -114,6 +114,7 @@ SIGNATURES: dict[str, tuple] = {
     "kdfm_rowscale": (_i32, [P, P, _i64, _i64, P, _i64, _f32, P]),
     "kdfm_relu_mask": (_i32, [P, P, P, _i64, P]),
     "kdfm_mse": (_i32, [P, P, P, P, _i64, _f32, _f32, P]),
+    "kdfm_l1": (_i32, [P, P, P, P, _i64, _f32, _f32, P]),
     "kdfm_dropout": (_i32, [P, P, _i64, _f32, _f32, P, C.c_uint64, P]),
     "kdfm_convw_prep": (_i32, [P, P, P, _i64, _i64, _i64, P]),
     "kdfm_convw_grad": (_i32, [P, P, _i64, _i64, _i64, _f32, P]),

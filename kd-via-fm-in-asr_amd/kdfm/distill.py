@@ -96,6 +96,31 @@ def mse_loss(a, b):
     return _MSEFn.apply(a, b)
 
 
+class _L1Fn(torch.autograd.Function):
+    """nn.L1Loss()(a, b) (mean) on device; grad only wrt a (b is the detached teacher latent)."""
+
+    @staticmethod
+    def forward(ctx, a, b):
+        acc = _zeros(1, dev=a.device)
+        ac, bc = a.contiguous(), b.contiguous()
+        n = ac.numel()
+        g = torch.empty_like(ac)
+        K.l1(ac.view(-1), bc.view(-1), acc, 1.0 / n, grad=g.view(-1), gscale=1.0 / n)
+        ctx.save_for_backward(g)
+        return acc.view(())
+
+    @staticmethod
+    def backward(ctx, dl):
+        (g,) = ctx.saved_tensors
+        out = torch.empty_like(g)
+        K.rowscale(g.view(-1, 1), out.view(-1, 1), dl.reshape(1).contiguous(), g.numel())
+        return out, None
+
+
+def l1_loss(a, b):
+    return _L1Fn.apply(a, b)
+
+
 # ------------------------------------------------------------------------------------------------
 # Heads (asr_train_diffm.py:400-460)
 # ------------------------------------------------------------------------------------------------
@@ -457,15 +482,24 @@ class DistilFlowMatchingCTCModelBPE(EncDecCTCModelBPE):
 
     def __init__(self, teacher_model: EncDecCTCModelBPE, version=5, use_ctc=True, use_logit_distillation=True,
                  kd_alpha=0.1, kd_temperature=1.0, student_dim=88, teacher_dim=176, latent_dim=96,
-                 flow_cfg=None, diffkd_cfg=None, device="cuda", **student_kw):
-        if int(version) != 5:
-            raise _lib.KdfmError("kdfm builds the ver5 hot path (SURVEY.md §8); versions 1-4,6-8 are §8(f) rank 4")
+                 flow_cfg=None, diffkd_cfg=None, device="cuda", kd_loss_type="mse", use_diffkd=False,
+                 use_layerwise_distillation=False, **student_kw):
+        if int(version) not in range(1, 9):
+            raise _lib.KdfmError("version must be 1..8 (asr_train_diffm.py:543)")
+        if kd_loss_type not in ("mse", "l1"):
+            raise _lib.KdfmError("kd_loss_type must be 'mse' or 'l1' (asr_train_diffm.py:557)")
+        if use_diffkd or use_layerwise_distillation:
+            # use_diffkd: the DiffKD module (asr_train_diffm.py:326-394) is not on the FM path;
+            # use_layerwise_distillation builds a fresh random nn.Linear inside every training_step
+            # (asr_train_diffm.py:763-769), i.e. an untrained projection: neither is built here.
+            raise _lib.KdfmError("use_diffkd / use_layerwise_distillation are outside kdfm's scope (DESIGN.md §7)")
         super().__init__(d_model=student_dim, n_heads=student_kw.pop("n_heads", 2), device=device, **student_kw)
         diffusion_steps = (diffkd_cfg or {}).get("diffusion_steps", 9)
         self.teacher = teacher_model.eval()
         for p in self.teacher.parameters():
             p.requires_grad_(False)
-        self.version = 5
+        self.version = int(version)
+        self.kd_crit = l1_loss if kd_loss_type == "l1" else mse_loss
         self.use_ctc, self.use_logit_distillation = use_ctc, use_logit_distillation
         self.kd_alpha, self.temperature = kd_alpha, kd_temperature
         self.student_dim, self.teacher_dim, self.latent_dim = student_dim, teacher_dim, latent_dim
@@ -514,16 +548,47 @@ class DistilFlowMatchingCTCModelBPE(EncDecCTCModelBPE):
         return log_probs, enc_len, pred
 
     def _compute_v_losses_one_layer(self, s_bht, t_bht):
+        """asr_train_diffm.py:645-729, every version: teacher AE recon always; then
+        1 KD(z_s) | 2 FM(z_s) | 3 KD(deno(adapt(z_s))) | 4 FM(z_s) + KD(deno(adapt(z_s))) |
+        5 FM(deno(adapt(z_s))) | 6 FM(z_s)->x, FM2(deno(adapt(x))) | 7 FM(z_s) + FM2(deno(adapt(z_s))) |
+        8 FM(z_s)->x, KD(deno(adapt(x))).  All against the detached teacher latent z_t."""
         s_bct = s_bht.transpose(1, 2)
         t_bct = t_bht.transpose(1, 2)
         z_t, t_rec = self.tae(t_bct)
         z_t = z_t.detach()
-        recon_loss = mse_loss(t_rec, t_bct)
+        zero = _zeros(1, dev=s_bct.device).view(())
+        out = {"recon_loss": mse_loss(t_rec, t_bct), "kd_loss_pre": zero, "fm_loss_pre": zero,
+               "kd_loss_post": zero, "fm_loss_post": zero}
         z_s = self.sproj(s_bct)
-        z_noisy, _ = self.adapter(z_s)
-        z_deno = self.denoiser(z_noisy)
-        fm_loss, _ = self.fm_latent(z_deno, z_t)
-        return {"recon_loss": recon_loss, "fm_loss_post": fm_loss}
+        v = self.version
+        if v == 1:
+            out["kd_loss_pre"] = self.kd_crit(z_s, z_t)
+        elif v == 2:
+            out["fm_loss_pre"], _ = self.fm_latent(z_s, z_t)
+        elif v == 3:
+            out["kd_loss_post"] = self.kd_crit(self.denoiser(self.adapter(z_s)[0]), z_t)
+        elif v == 4:
+            out["fm_loss_pre"], _ = self.fm_latent(z_s, z_t)
+            out["kd_loss_post"] = self.kd_crit(self.denoiser(self.adapter(z_s)[0]), z_t)
+        elif v == 5:
+            out["fm_loss_post"], _ = self.fm_latent(self.denoiser(self.adapter(z_s)[0]), z_t)
+        elif v == 6:
+            out["fm_loss_pre"], z_al = self.fm_latent(z_s, z_t)
+            out["fm_loss_post"], _ = self.fm_latent_2(self.denoiser(self.adapter(z_al)[0]), z_t)
+        elif v == 7:
+            out["fm_loss_pre"], _ = self.fm_latent(z_s, z_t)
+            out["fm_loss_post"], _ = self.fm_latent_2(self.denoiser(self.adapter(z_s)[0]), z_t)
+        else:
+            out["fm_loss_pre"], z_al = self.fm_latent(z_s, z_t)
+            out["kd_loss_post"] = self.kd_crit(self.denoiser(self.adapter(z_al)[0]), z_t)
+        return out
+
+    _USES = {1: ("kd_loss_pre",), 2: ("fm_loss_pre",), 3: ("kd_loss_post",), 4: ("fm_loss_pre", "kd_loss_post"),
+             5: ("fm_loss_post",), 6: ("fm_loss_pre", "fm_loss_post"), 7: ("fm_loss_pre", "fm_loss_post"),
+             8: ("fm_loss_pre", "kd_loss_post")}
+
+    def _uses(self, key):
+        return key in self._USES[self.version]
 
     def training_step(self, batch, batch_idx=0):
         signal, sig_len, transcript, transcript_len = batch
@@ -535,19 +600,25 @@ class DistilFlowMatchingCTCModelBPE(EncDecCTCModelBPE):
             tch_logp = self.teacher.decoder(encoder_output=self.tch_feats[-1].permute(0, 2, 1))
         logit_kd = _KLFn.apply(log_probs, tch_logp, float(self.temperature))
         terms = [ctc_loss, logit_kd]
-        recon_terms, fm_terms = [], []
+        # per-layer terms are SUMMED over the hooked layers (asr_train_diffm.py:773-792); the version
+        # decides which of the four KD/FM sums are non-zero (:796-811)
+        keys = ("recon_loss", "kd_loss_pre", "fm_loss_pre", "kd_loss_post", "fm_loss_post")
+        per = {k: [] for k in keys}
         for s, t in zip(self.stu_feats, self.tch_feats):
             out = self.__class__._compute_v_losses_one_layer(self, s, t)
-            recon_terms.append(out["recon_loss"])
-            fm_terms.append(out["fm_loss_post"])
-        stacked = torch.stack([ctc_loss, logit_kd] + recon_terms + fm_terms)   # noqa: scalar gather (glue)
-        weights = torch.tensor([1.0, self.kd_alpha] + [1.0] * (len(recon_terms) + len(fm_terms)),
-                               device=stacked.device)
+            for k in keys:
+                per[k].append(out[k])
+        used = ["recon_loss"] + [k for k in keys[1:] if self._uses(k)]
+        terms = [ctc_loss, logit_kd] + [x for k in used for x in per[k]]
+        stacked = torch.stack(terms)   # noqa: scalar gather (glue)
+        weights = torch.tensor([1.0, self.kd_alpha] + [1.0] * (len(terms) - 2), device=stacked.device)
         total = _WeightedSumFn.apply(stacked, weights)
-        self.last_log = {"loss/ctc": ctc_loss.detach(), "loss/logit_kd": logit_kd.detach(),
-                         "v/recon": _ReduceFn.apply(torch.stack(recon_terms).detach(), 1.0),
-                         "v/fm_post": _ReduceFn.apply(torch.stack(fm_terms).detach(), 1.0),
-                         "train_loss": total.detach()}
+        log_names = {"recon_loss": "v/recon", "kd_loss_pre": "v/kd_pre", "fm_loss_pre": "v/fm_pre",
+                     "kd_loss_post": "v/kd_post", "fm_loss_post": "v/fm_post"}
+        self.last_log = {"loss/ctc": ctc_loss.detach(), "loss/logit_kd": logit_kd.detach(), "train_loss": total.detach()}
+        for k in keys:
+            self.last_log[log_names[k]] = (_ReduceFn.apply(torch.stack(per[k]).detach(), 1.0) if k in used
+                                           else _zeros(1, dev=ctc_loss.device).view(()))
         del terms
         return total
 
@@ -555,6 +626,8 @@ class DistilFlowMatchingCTCModelBPE(EncDecCTCModelBPE):
     def to_engine(self, cfg: Ver5Config | None = None):
         """Copy this model's weights into a fused, graph-capturable Ver5Engine (same kernels)."""
         from .engine import Ver5Engine
+        if self.version != 5:
+            raise _lib.KdfmError("the fused engine runs the ver5 step; other versions train through the module API")
         cfg = cfg or Ver5Config()
         eng = Ver5Engine(cfg, self.decoder.decoder_layers[0].weight.device, init=False)
         sd = {k: v for k, v in self.state_dict().items()}
@@ -586,4 +659,4 @@ class _WeightedSumFn(torch.autograd.Function):
 
 
 __all__ = ["TeacherAutoEncoder", "StudentProjector", "NoiseAdapter", "SimpleDenoiser", "FlowMatchingModule",
-           "FMLatent", "EncDecCTCModelBPE", "DistilFlowMatchingCTCModelBPE", "mse_loss", "greedy", "math"]
+           "FMLatent", "EncDecCTCModelBPE", "DistilFlowMatchingCTCModelBPE", "mse_loss", "l1_loss", "greedy", "math"]

@@ -353,6 +353,11 @@ def mse(a, b, loss_acc, scale, grad=None, gscale=0.0):
     call("kdfm_mse", ptr(a), ptr(b), ptr(grad), ptr(loss_acc), a.numel(), float(scale), float(gscale), _s())
 
 
+def l1(a, b, loss_acc, scale, grad=None, gscale=0.0):
+    assert a.is_contiguous() and b.is_contiguous() and a.numel() == b.numel()
+    call("kdfm_l1", ptr(a), ptr(b), ptr(grad), ptr(loss_acc), a.numel(), float(scale), float(gscale), _s())
+
+
 def dropout(x, out, p, scale, seed, rng_stream):
     assert x.is_contiguous() and out.is_contiguous() and x.numel() == out.numel()
     call("kdfm_dropout", ptr(x), ptr(out), x.numel(), float(p), float(scale), ptr(seed), int(rng_stream), _s())

@@ -428,6 +428,51 @@ def ver5_layer_losses(s_btd, t_btd, p, eps, cfg: StepConfig):
     return recon, fm
 
 
+def v_layer_losses(version, s_btd, t_btd, p, eps, denoiser_steps=9, fm_steps=8, kd="mse"):
+    """_compute_v_losses_one_layer for every version 1-8 (asr_train_diffm.py:645-729); kd_crit is
+    nn.MSELoss or nn.L1Loss (:557).  eps: the NoiseAdapter draw (B, L, T) (one adapter call per
+    version).  Returns the dict of the five per-layer terms (zeros where the version has none)."""
+    s = s_btd.transpose(1, 2)
+    t = t_btd.transpose(1, 2)
+    z_t, rec = tae(t, p)
+    z_t = z_t.detach()
+    kd_crit = F.l1_loss if kd == "l1" else F.mse_loss
+    zero = torch.zeros(())
+    out = {"recon_loss": F.mse_loss(rec, t), "kd_loss_pre": zero, "fm_loss_pre": zero, "kd_loss_post": zero,
+           "fm_loss_post": zero}
+    z_s = sproj(s, p)
+
+    def deno(z):
+        return denoiser(noise_adapter(z, p, eps)[0], p, denoiser_steps)
+
+    def fm(a, prefix="fm_latent.fm."):
+        return fm_latent(a, z_t, p, fm_steps, prefix)
+
+    if version == 1:
+        out["kd_loss_pre"] = kd_crit(z_s, z_t)
+    elif version == 2:
+        out["fm_loss_pre"] = fm(z_s)[0]
+    elif version == 3:
+        out["kd_loss_post"] = kd_crit(deno(z_s), z_t)
+    elif version == 4:
+        out["fm_loss_pre"] = fm(z_s)[0]
+        out["kd_loss_post"] = kd_crit(deno(z_s), z_t)
+    elif version == 5:
+        out["fm_loss_post"] = fm(deno(z_s))[0]
+    elif version == 6:
+        out["fm_loss_pre"], x = fm(z_s)
+        out["fm_loss_post"] = fm(deno(x), "fm_latent_2.fm.")[0]
+    elif version == 7:
+        out["fm_loss_pre"] = fm(z_s)[0]
+        out["fm_loss_post"] = fm(deno(z_s), "fm_latent_2.fm.")[0]
+    elif version == 8:
+        out["fm_loss_pre"], x = fm(z_s)
+        out["kd_loss_post"] = kd_crit(deno(x), z_t)
+    else:
+        raise ValueError(version)
+    return out
+
+
 # ------------------------------------------------------------------------------------------
 # The whole step
 # ------------------------------------------------------------------------------------------
