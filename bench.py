@@ -34,8 +34,8 @@ MI355X_F32_MFMA_TFLOPS = 157.3
 MI355X_HBM_GBPS = 8000.0            # MI355X_MICROARCH.md §HBM (8 TB/s spec peak)
 # PMC traffic of the roofline kernel (tools/pmc_traffic.sh -> tools/pmc_summary.py, 2 separate --pmc
 # passes, FETCH_SIZE doubled per the gfx950 correction); committed under profiles/
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
-ROOF_KERNEL = "kdfm::sk_fwd_kernel<3, 2, 4>"
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r01_s8_pmc_traffic.json")
+ROOF_KERNEL = "kdfm::skc_fwd_kernel<3>"
 
 
 def pmc_traffic(kernel: str):
@@ -200,10 +200,10 @@ def main():
                        "frames_subsampled": (args.samples // 160) // 4 + 1, "parallelism": f"dp{world}"},
             "roofline": {"bound": "hbm",
                          "kernel": "kdfm_gemm CONV (denoiser Conv1d k=3 over 16 stacked layers, 205312 x 96 x 288, "
-                                   "sk_fwd_kernel<3,2,4>)",
+                                   "LDS-slab skc_fwd_kernel<3>)",
                          "achieved": round(d_gbps, 1), "peak": MI355X_HBM_GBPS, "unit": "GB/s",
                          "frac": round(d_gbps / MI355X_HBM_GBPS, 4), "traffic": d_traffic,
-                         "traffic_source": "profiles/r01_pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE)",
+                         "traffic_source": "profiles/r01_s8_pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE)",
                          "launches": deno["launches"], "avg_ms": round(d_ms, 5), "bytes_per_launch": d_bytes},
             "roofline_mfma_ffn": {"bound": "mfma", "kernel": "kdfm_gemm ffn_up (Conformer FFN d->4d, SiLU+dropout)",
                                   "achieved": round(achieved, 3), "peak": peak, "unit": "TFLOP/s",

@@ -162,6 +162,10 @@ int kdfm_im2col_3x3s2(const float* X, const int64_t* len_in, float* cols, int64_
 /* adjoint of the above (gather form); optionally multiplied by relu'(relu_out). */
 int kdfm_col2im_3x3s2(const float* dcols, const int64_t* len_in, const float* relu_out, float* dX, int64_t B,
                       int64_t T1, int64_t F1, int64_t C, void* stream);
+/* the same adjoint for a tap-major dcols (column tap*C + c, tap = ky*3 + kx): produced by the
+ * data-gradient GEMM against the (C, 9, C) re-laid weight, read with contiguous lanes */
+int kdfm_col2im_3x3s2_tapmajor(const float* dcols, const int64_t* len_in, const float* relu_out, float* dX, int64_t B,
+                      int64_t T1, int64_t F1, int64_t C, void* stream);
 
 /* Fused striding subsampling forward (bf16 MFMA mode; replaces im2col + GEMM for the same A.3
  * arithmetic, conformer_encoder.py:381-390, 635):

@@ -68,6 +68,18 @@ __device__ __forceinline__ bool dropout_keep(uint64_t seed, uint64_t stream, uin
 __device__ __forceinline__ uint64_t load_seed(const uint64_t* seed_ptr) { return seed_ptr ? *seed_ptr : 0ull; }
 
 // ---- wave64 reductions --------------------------------------------------------------------------
+// XCD-aware block order for 1-D grids.  The dispatcher deals consecutive workgroups round-robin
+// to the 8 XCDs, each with its own L2: neighbouring blocks that share input lines (gathers such as
+// col2im / im2col, whose taps overlap) would fetch the same lines once per XCD.  This bijection
+// gives XCD x a CONTIGUOUS range of logical blocks instead, so the overlap is served by one L2.
+constexpr int kNumXcd = 8;
+__device__ __forceinline__ int64_t xcd_block() {
+  const int64_t b = blockIdx.x, n = gridDim.x;
+  const int64_t x = b % kNumXcd, local = b / kNumXcd;
+  const int64_t per = n / kNumXcd, rem = n % kNumXcd;
+  return x < rem ? x * (per + 1) + local : rem * (per + 1) + (x - rem) * per + local;
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

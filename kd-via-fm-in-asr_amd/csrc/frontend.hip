@@ -176,7 +176,7 @@ __global__ __launch_bounds__(256) void specaug_kernel(float* __restrict__ x, con
 __global__ __launch_bounds__(256) void im2col_kernel(const float* __restrict__ X, const int64_t* __restrict__ lin,
                                                      float* __restrict__ cols, int64_t B, int64_t T1, int64_t F1,
                                                      int64_t C, int64_t T2, int64_t F2) {
-  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t idx = xcd_block() * 256 + threadIdx.x;
   const int64_t KC = 9 * C;
   if (idx >= B * T2 * F2 * KC) return;
   const int64_t q = idx % KC, row = idx / KC;
@@ -189,11 +189,14 @@ __global__ __launch_bounds__(256) void im2col_kernel(const float* __restrict__ X
   cols[idx] = v;
 }
 
-// dX[b,t1,f1,c] = sum over taps hitting (t1,f1) of dcols; zero beyond len_in; *= (aux > 0) if aux
+// dX[b,t1,f1,c] = sum over taps hitting (t1,f1) of dcols; zero beyond len_in; *= (aux > 0) if aux.
+// TAPMAJOR: dcols columns are tap*C + c (the lanes of a wave, consecutive c, read one contiguous run
+// per tap) instead of c*9 + tap (stride-9 lanes: 36 partially used lines per load).
+template <bool TAPMAJOR>
 __global__ __launch_bounds__(256) void col2im_kernel(const float* __restrict__ dcols, const int64_t* __restrict__ lin,
                                                      const float* __restrict__ aux, float* __restrict__ dX, int64_t B,
                                                      int64_t T1, int64_t F1, int64_t C, int64_t T2, int64_t F2) {
-  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t idx = xcd_block() * 256 + threadIdx.x;
   if (idx >= B * T1 * F1 * C) return;
   const int64_t c = idx % C, f1 = (idx / C) % F1, t1 = (idx / (C * F1)) % T1, b = idx / (C * F1 * T1);
   const int64_t len = lin ? lin[b] : T1;
@@ -209,7 +212,8 @@ __global__ __launch_bounds__(256) void col2im_kernel(const float* __restrict__ d
         if (fn < 0 || (fn & 1)) continue;
         const int64_t f2 = fn >> 1;
         if (f2 >= F2) continue;
-        acc += dcols[((b * T2 + t2) * F2 + f2) * 9 * C + c * 9 + ky * 3 + kx];
+        const int64_t cell = ((b * T2 + t2) * F2 + f2) * 9 * C;
+        acc += TAPMAJOR ? dcols[cell + (ky * 3 + kx) * C + c] : dcols[cell + c * 9 + ky * 3 + kx];
       }
     }
     if (aux && !(aux[idx] > 0.f)) acc = 0.f;
@@ -294,9 +298,21 @@ int kdfm_col2im_3x3s2(const float* dcols, const int64_t* len_in, const float* re
   const int64_t T2 = (T1 - 1) / 2 + 1, F2 = (F1 - 1) / 2 + 1;
   const int64_t n = B * T1 * F1 * C;
   if (n == 0) return KDFM_OK;
-  hipLaunchKernelGGL(col2im_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, as_stream(stream), dcols, len_in,
+  hipLaunchKernelGGL(col2im_kernel<false>, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, as_stream(stream), dcols, len_in,
                      relu_out, dX, B, T1, F1, C, T2, F2);
   return check_launch("kdfm_col2im_3x3s2");
+}
+
+int kdfm_col2im_3x3s2_tapmajor(const float* dcols, const int64_t* len_in, const float* relu_out, float* dX, int64_t B,
+                      int64_t T1, int64_t F1, int64_t C, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(dcols && dX, "null pointer");
+  const int64_t T2 = (T1 - 1) / 2 + 1, F2 = (F1 - 1) / 2 + 1;
+  const int64_t n = B * T1 * F1 * C;
+  if (n == 0) return KDFM_OK;
+  hipLaunchKernelGGL(col2im_kernel<true>, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, as_stream(stream), dcols, len_in,
+                     relu_out, dX, B, T1, F1, C, T2, F2);
+  return check_launch("kdfm_col2im_3x3s2_tapmajor");
 }
 
 }  // extern "C"

@@ -65,6 +65,19 @@ __device__ __forceinline__ bf16x8 cvt8(float4 a, float4 b) {
 }
 
 // Stage B columns [n0, n0 + cw) x k [0, Kp) into the bf16 [n][k] image (zero outside N / K).
+// Predicated loads as UNCONDITIONAL loads from a clamped address + a select.  Written as
+// `ok ? *ptr : 0` the compiler branches around each load and waits vmcnt(0) inside the branch,
+// serialising a batch of loads into one memory latency each (the weight staging took ~13 us per
+// launch that way).  `base` must be a valid address (the operand's first element).
+__device__ __forceinline__ float4 ld4_or0(const float* base, int64_t off, bool ok) {
+  const float4 t = *reinterpret_cast<const float4*>(base + (ok ? off : 0));
+  return ok ? t : make_float4(0.f, 0.f, 0.f, 0.f);
+}
+__device__ __forceinline__ float ld_or0(const float* base, int64_t off, bool ok) {
+  const float t = base[ok ? off : 0];
+  return ok ? t : 0.f;
+}
+
 __device__ void sk_stage_B(const GemmP& p, const SkGeo& g, uint16_t* Bs, int64_t n0) {
   const int nth = blockDim.x, tid = threadIdx.x;
   const int cw = g.cw, Kp = g.Kp, ldb = g.ldb;
@@ -79,8 +92,7 @@ __device__ void sk_stage_B(const GemmP& p, const SkGeo& g, uint16_t* Bs, int64_t
         const int e = base + tid + i * nth;
         const int nl = e / kq, k = (e - nl * kq) * 4;
         const int64_t n = n0 + nl;
-        v[i] = (e < total && n < p.N && k < p.K) ? *reinterpret_cast<const float4*>(p.B + n * p.sBn + k)
-                                                 : make_float4(0.f, 0.f, 0.f, 0.f);
+        v[i] = ld4_or0(p.B, n * p.sBn + k, e < total && n < p.N && k < p.K);
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -103,8 +115,7 @@ __device__ void sk_stage_B(const GemmP& p, const SkGeo& g, uint16_t* Bs, int64_t
         const int e = base + tid + i * nth;
         const int k = e / nq, nl = (e - k * nq) * 4;
         const int64_t n = n0 + nl;
-        v[i] = (e < total && n < p.N && k < p.K) ? *reinterpret_cast<const float4*>(p.B + (int64_t)k * p.sBk + n)
-                                                 : make_float4(0.f, 0.f, 0.f, 0.f);
+        v[i] = ld4_or0(p.B, (int64_t)k * p.sBk + n, e < total && n < p.N && k < p.K);
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -122,7 +133,7 @@ __device__ void sk_stage_B(const GemmP& p, const SkGeo& g, uint16_t* Bs, int64_t
     for (int e = tid; e < cw * Kp; e += nth) {
       const int nl = e / Kp, k = e - nl * Kp;
       const int64_t n = n0 + nl;
-      const float x = (n < p.N && k < p.K) ? p.B[(int64_t)k * p.sBk + n * p.sBn] : 0.f;
+      const float x = ld_or0(p.B, (int64_t)k * p.sBk + n * p.sBn, n < p.N && k < p.K);
       Bs[nl * ldb + k] = f2bf(x);
     }
   }
@@ -148,15 +159,15 @@ __device__ __forceinline__ void sk_load_A(float4 (&v)[SK_CKS][2], const GemmP& p
   } else {
     kbase = c * SK_CHUNK;
   }
-  const float* src = p.A + row * p.sAm;
   const int klim = (AMODE == KDFM_LD_CONV) ? (int)p.conv_c : (int)p.K;
 #pragma unroll
   for (int s = 0; s < SK_CKS; ++s) {
     const int k = kbase + 16 * s + 8 * h;
-    if (ok && 16 * s < g.chunk && k < klim) {
-      const float4* q = reinterpret_cast<const float4*>(src + k);
-      v[s][0] = q[0];
-      v[s][1] = q[1];
+    if (16 * s < g.chunk) {  // compile-time after unrolling for the common chunk sizes
+      const bool okk = ok && k < klim;
+      const int64_t off = (row * p.sAm + k) * (okk ? 1 : 0);
+      v[s][0] = ld4_or0(p.A, off, okk);
+      v[s][1] = ld4_or0(p.A, off + 4, okk);
     } else {
       v[s][0] = make_float4(0.f, 0.f, 0.f, 0.f);
       v[s][1] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -415,7 +426,7 @@ __global__ __launch_bounds__(256, 2) void skd_fwd_kernel(GemmP p, SkGeo g, int G
 #pragma unroll
           for (int i = 0; i < 16; ++i) {
             const int64_t m = m0 + (i & 3) + 8 * (i >> 2) + 4 * h;
-            sv[j][i] = (m < p.M && n < p.N) ? side[m * p.sCm + n * p.sCn] : 0.f;
+            sv[j][i] = ld_or0(side, m * p.sCm + n * p.sCn, m < p.M && n < p.N);
           }
         }
       }
@@ -471,8 +482,7 @@ __device__ __forceinline__ void skc_load_slab(float4 (&v)[SKC_SLAB_V], const Gem
     const int e = lane + 64 * i;
     const int j = e / cq, q = e - j * cq;
     const int64_t gr = m0 - p.pad + j;
-    v[i] = (e < total && gr >= 0 && gr < p.M) ? *reinterpret_cast<const float4*>(p.A + gr * p.sAm + 4 * q)
-                                             : make_float4(0.f, 0.f, 0.f, 0.f);
+    v[i] = ld4_or0(p.A, gr * p.sAm + 4 * q, e < total && gr >= 0 && gr < p.M);
   }
 }
 
@@ -572,8 +582,8 @@ __global__ __launch_bounds__(64 * SKC_WV, 1) void skc_fwd_kernel(GemmP p, SkGeo 
       for (int i = 0; i < 4; ++i) {
         const int64_t mm = m0 + er + 8 * i;
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (side && mm < p.M && n + 3 < p.N) {
-          v = *reinterpret_cast<const float4*>(side + mm * p.sCm + n);
+        if (side && n + 3 < p.N) {
+          v = ld4_or0(side, mm * p.sCm + n, mm < p.M);
         } else if (side && mm < p.M && n < p.N) {
           v.x = side[mm * p.sCm + n];
           if (n + 1 < p.N) v.y = side[mm * p.sCm + n + 1];

@@ -76,6 +76,7 @@ SIGNATURES: dict[str, tuple] = {
     "kdfm_specaugment": (_i32, [P, P, P, _i64, _i64, _i64, _i32, _i32, _i32, _f32, P, C.c_uint64, P]),
     "kdfm_im2col_3x3s2": (_i32, [P, P, P, _i64, _i64, _i64, _i64, P]),
     "kdfm_col2im_3x3s2": (_i32, [P, P, P, P, _i64, _i64, _i64, _i64, P]),
+    "kdfm_col2im_3x3s2_tapmajor": (_i32, [P, P, P, P, _i64, _i64, _i64, _i64, P]),
     "kdfm_subsample_wprep_elems": (_i64, [_i64]),
     "kdfm_subsample_wprep": (_i32, [P, P, _i64, P]),
     "kdfm_subsample_conv1": (_i32, [P, P, P, P, P, P, P, _i64, _i64, _i64, _i64, P]),

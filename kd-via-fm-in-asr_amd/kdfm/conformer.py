@@ -121,11 +121,15 @@ def subsampling_backward(cfg, S: EncoderShapes, P, G, pre, ctx, dx, len1, *, see
         ctx["cols1"] = _empty(B * S.T * S.F2, 9 * C, dev=dev)
         K.im2col_3x3s2(ctx["y1"], len1 if cfg.subsampling_mask else None, ctx["cols1"], B, S.T1, S.F1, C)
     WGRAD.run(lambda: K.linear_dw(dy2, ctx["cols1"], G[pre + "pre_encode.conv.2.weight"].view(C, 9 * C), db=G[pre + "pre_encode.conv.2.bias"]), dy2, ctx["cols1"])
+    # data gradient in TAP-MAJOR columns (tap*C + c): GEMM against the (C, 9, C) re-laid weight, so the
+    # col2im gather reads contiguous channel runs per tap
+    w2tm = ws["w2_tapmajor"]
+    K.convw_prep(P[pre + "pre_encode.conv.2.weight"].view(C, C, 9), fwd=w2tm)
     dcols1 = _empty(B * S.T * S.F2, 9 * C, dev=dev)
-    K.linear_dx(dy2, P[pre + "pre_encode.conv.2.weight"].view(C, 9 * C), dcols1)
+    K.linear_dx(dy2, w2tm.view(C, 9 * C), dcols1)
     del dy2
     dy1 = _empty(B * S.T1 * S.F1, C, dev=dev)
-    K.col2im_3x3s2(dcols1, len1 if cfg.subsampling_mask else None, ctx["y1"], dy1, B, S.T1, S.F1, C)
+    K.col2im_3x3s2(dcols1, len1 if cfg.subsampling_mask else None, ctx["y1"], dy1, B, S.T1, S.F1, C, tapmajor=True)
     del dcols1
     WGRAD.run(lambda: K.linear_dw(dy1, ctx["cols0"], G[pre + "pre_encode.conv.0.weight"].view(C, 9), math="f32", db=G[pre + "pre_encode.conv.0.bias"]), dy1, ctx["cols0"])
     
@@ -433,5 +437,6 @@ def make_workspace(S: EncoderShapes, dev):
         "wout_perm": torch.empty(S.d, S.F2, S.d, device=dev),
         "w2_bf16": torch.empty(K.subsample_wprep_elems(S.d), device=dev, dtype=torch.bfloat16),
         "wout_perm_grad": torch.empty(S.d, S.F2, S.d, device=dev),
+        "w2_tapmajor": torch.empty(S.d, 9, S.d, device=dev),
         "bout_scaled": torch.empty(S.d, device=dev),
     }

@@ -420,10 +420,10 @@ def im2col_3x3s2(X, len_in, cols, B, T1, F1, Cc):
     call("kdfm_im2col_3x3s2", ptr(X), ptr(_i64(len_in)), ptr(cols), B, T1, F1, Cc, _s())
 
 
-def col2im_3x3s2(dcols, len_in, relu_out, dX, B, T1, F1, Cc):
+def col2im_3x3s2(dcols, len_in, relu_out, dX, B, T1, F1, Cc, tapmajor=False):
     T2, F2 = (T1 - 1) // 2 + 1, (F1 - 1) // 2 + 1
     assert dcols.shape == (B * T2 * F2, 9 * Cc) and dX.numel() == B * T1 * F1 * Cc
-    call("kdfm_col2im_3x3s2", ptr(dcols), ptr(_i64(len_in)), ptr(relu_out), ptr(dX), B, T1, F1, Cc, _s())
+    call("kdfm_col2im_3x3s2_tapmajor" if tapmajor else "kdfm_col2im_3x3s2", ptr(dcols), ptr(_i64(len_in)), ptr(relu_out), ptr(dX), B, T1, F1, Cc, _s())
 
 
 def subsample_wprep(w2, wb):
