@@ -469,7 +469,10 @@ __global__ __launch_bounds__(256, 2) void skd_fwd_kernel(GemmP p, SkGeo g, int G
 // tile's slab is prefetched into registers while the MFMAs and the epilogue of the current one run.
 // 8 waves share one staged weight image (96 x 288 bf16); the epilogue's transposition tile aliases
 // the wave's slab (free once the MFMAs have read it).
-constexpr int SKC_WV = 8;
+#ifndef KDFM_SKC_WV
+#define KDFM_SKC_WV 8  // waves per workgroup (one workgroup per CU: the staged weight image is shared)
+#endif
+constexpr int SKC_WV = KDFM_SKC_WV;
 constexpr int SKC_SLAB_V = 13;            // float4 per lane: (32 + 2) rows x 96 ch / 4 / 64 lanes
 constexpr int SKC_LDA = SK_CHUNK + 8;     // bf16 slab row stride (208 B, 16-B aligned)
 constexpr int SKC_SLAB_BYTES = 34 * SKC_LDA * 2;
@@ -486,7 +489,35 @@ __device__ __forceinline__ void skc_load_slab(float4 (&v)[SKC_SLAB_V], const Gem
   }
 }
 
-template <int NCT>
+// Compile-time epilogues for the four denoiser products (heads.py deno_conv: conv+bias+ReLU,
+// conv+bias+residual forward; conv*alpha with dReLU, conv+residual backward).  The generic
+// epi_apply tests every flag per element; at 48 elements per lane per tile that flag walk, not
+// HBM, bounds this HBM-shaped kernel.  EMODE 0 = generic.
+enum { SKC_EPI_GENERIC = 0, SKC_EPI_RELU = 1, SKC_EPI_RESID = 2, SKC_EPI_DRELU = 3 };
+
+template <int EMODE>
+__device__ __forceinline__ float skc_epi(const GemmP& p, int64_t m, int64_t n, float v, float bn, float sv, bool rowok,
+                                         uint64_t seed, float keep_scale, float& mse_part, float& pre) {
+  if constexpr (EMODE == SKC_EPI_GENERIC) {
+    return epi_apply(p, 0, m, n, v, bn, sv, rowok, seed, keep_scale, mse_part, pre);
+  } else {
+    v += bn;  // bn is 0 without KDFM_EPI_BIAS
+    if constexpr (EMODE == SKC_EPI_RELU) return fmaxf(v, 0.f);
+    if constexpr (EMODE == SKC_EPI_RESID) return sv + p.rscale * v;
+    return sv > 0.f ? v : 0.f;  // SKC_EPI_DRELU
+  }
+}
+
+__host__ inline int skc_epi_mode(int epi) {
+  switch (epi & ~KDFM_EPI_BIAS) {
+    case KDFM_EPI_RELU: return SKC_EPI_RELU;
+    case KDFM_EPI_RESID: return SKC_EPI_RESID;
+    case KDFM_EPI_DRELU: return SKC_EPI_DRELU;
+    default: return SKC_EPI_GENERIC;
+  }
+}
+
+template <int NCT, int EMODE>
 __global__ __launch_bounds__(64 * SKC_WV, 1) void skc_fwd_kernel(GemmP p, SkGeo g) {
   extern __shared__ __attribute__((aligned(16))) uint16_t sk_lds[];
   uint16_t* Bs = sk_lds;
@@ -567,6 +598,21 @@ __global__ __launch_bounds__(64 * SKC_WV, 1) void skc_fwd_kernel(GemmP p, SkGeo 
         }
       }
     }
+    // side operand (residual / dReLU aux) of the specialised epilogues: all column tiles issued
+    // together here, one memory latency per tile instead of one per column tile
+    constexpr bool kSideAll = (EMODE == SKC_EPI_RESID || EMODE == SKC_EPI_DRELU);
+    float4 sdall[kSideAll ? NCT : 1][4];
+    if constexpr (kSideAll) {
+#pragma unroll
+      for (int j = 0; j < NCT; ++j) {
+        const int64_t n = 32 * j + ec;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int64_t mm = m0 + er + 8 * i;
+          sdall[j][i] = ld4_or0(side, mm * p.sCm + n, mm < p.M && n + 3 < p.N);
+        }
+      }
+    }
     bool rowok[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -580,6 +626,10 @@ __global__ __launch_bounds__(64 * SKC_WV, 1) void skc_fwd_kernel(GemmP p, SkGeo 
       float4 sd4[4];  // side operand rows of this column tile (register budget: one tile at a time)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
+        if constexpr (kSideAll) {
+          sd4[i] = sdall[j][i];
+          continue;
+        }
         const int64_t mm = m0 + er + 8 * i;
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
         if (side && n + 3 < p.N) {
@@ -609,7 +659,7 @@ __global__ __launch_bounds__(64 * SKC_WV, 1) void skc_fwd_kernel(GemmP p, SkGeo 
           o[e] = 0.f;
           pr[e] = 0.f;
           if (n + e < p.N)
-            o[e] = epi_apply(p, 0, mm, n + e, p.alpha * av4[e], bv[e], side ? s4[e] : 0.f, rowok[i], seed, keep_scale,
+            o[e] = skc_epi<EMODE>(p, mm, n + e, p.alpha * av4[e], bv[e], side ? s4[e] : 0.f, rowok[i], seed, keep_scale,
                              mse_part, pr[e]);
         }
         const int64_t off = mm * p.sCm + n;
@@ -635,14 +685,15 @@ __global__ __launch_bounds__(64 * SKC_WV, 1) void skc_fwd_kernel(GemmP p, SkGeo 
   }
 }
 
-template <int NCT>
+template <int NCT, int EMODE = SKC_EPI_GENERIC>
 int skc_launch(const GemmP& p, const SkGeo& g, int64_t gx, size_t lds, hipStream_t st) {
   static bool once = [] {
-    hipFuncSetAttribute((const void*)skc_fwd_kernel<NCT>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    hipFuncSetAttribute((const void*)skc_fwd_kernel<NCT, EMODE>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        160 * 1024);
     return true;
   }();
   (void)once;
-  hipLaunchKernelGGL((skc_fwd_kernel<NCT>), dim3((unsigned)gx), dim3(64 * SKC_WV), lds, st, p, g);
+  hipLaunchKernelGGL((skc_fwd_kernel<NCT, EMODE>), dim3((unsigned)gx), dim3(64 * SKC_WV), lds, st, p, g);
   return check_launch("kdfm_gemm(skinny conv slab)");
 }
 
@@ -755,7 +806,15 @@ int try_skinny_fwd(const GemmP& p, int amode, int bmode, int64_t batch, hipStrea
     switch (nct) {
       case 1: return skc_launch<1>(p, g, gx, lds, st);
       case 2: return skc_launch<2>(p, g, gx, lds, st);
-      default: return skc_launch<3>(p, g, gx, lds, st);
+      default: {
+        static const int fast = env_int("KDFM_SKC_FAST_EPI", 1);
+        switch ((fast && (p.N & 3) == 0 && (p.sCm & 3) == 0) ? skc_epi_mode(p.epi) : SKC_EPI_GENERIC) {
+          case SKC_EPI_RELU: return skc_launch<3, SKC_EPI_RELU>(p, g, gx, lds, st);
+          case SKC_EPI_RESID: return skc_launch<3, SKC_EPI_RESID>(p, g, gx, lds, st);
+          case SKC_EPI_DRELU: return skc_launch<3, SKC_EPI_DRELU>(p, g, gx, lds, st);
+          default: return skc_launch<3>(p, g, gx, lds, st);
+        }
+      }
     }
   }
   if (amode == KDFM_LD_KC) {

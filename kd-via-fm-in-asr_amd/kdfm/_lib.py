@@ -12,6 +12,8 @@ import os
 import torch  # noqa: F401  (must be imported first, see module docstring)
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libkdfm.so")
+# experiment builds (tools/): an alternative in-tree library, e.g. a kernel-variant sweep
+LIB_PATH = os.environ.get("KDFM_LIB") or LIB_PATH
 
 KDFM_MATH_F32 = 0
 KDFM_MATH_BF16 = 1
