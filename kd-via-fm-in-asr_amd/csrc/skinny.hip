@@ -175,7 +175,38 @@ __device__ __forceinline__ void sk_load_A(float4 (&v)[SK_CKS][2], const GemmP& p
   }
 }
 
-template <int NCT, int AMODE, int WV>
+// Compile-time epilogues for the common flag sets (the denoiser products, heads.py deno_conv:
+// conv+bias+ReLU, conv+bias+residual forward, conv*alpha with dReLU, conv+residual backward; and
+// plain / bias-only products).  The generic epi_apply tests every flag per element; at 48
+// elements per lane per tile that flag walk, not HBM, bounded these HBM-shaped kernels.
+// Row masks, STORE_PRE, dropout, MSE, SiLU keep the generic path.  EMODE 0 = generic.
+enum { SKC_EPI_GENERIC = 0, SKC_EPI_RELU = 1, SKC_EPI_RESID = 2, SKC_EPI_DRELU = 3, SKC_EPI_NONE = 4 };
+
+template <int EMODE>
+__device__ __forceinline__ float skc_epi(const GemmP& p, int64_t m, int64_t n, float v, float bn, float sv, bool rowok,
+                                         uint64_t seed, float keep_scale, float& mse_part, float& pre) {
+  if constexpr (EMODE == SKC_EPI_GENERIC) {
+    return epi_apply(p, 0, m, n, v, bn, sv, rowok, seed, keep_scale, mse_part, pre);
+  } else {
+    v += bn;  // bn is 0 without KDFM_EPI_BIAS
+    if constexpr (EMODE == SKC_EPI_RELU) return fmaxf(v, 0.f);
+    if constexpr (EMODE == SKC_EPI_RESID) return sv + p.rscale * v;
+    if constexpr (EMODE == SKC_EPI_DRELU) return sv > 0.f ? v : 0.f;
+    return v;  // SKC_EPI_NONE
+  }
+}
+
+__host__ inline int skc_epi_mode(int epi) {
+  switch (epi & ~KDFM_EPI_BIAS) {
+    case 0: return SKC_EPI_NONE;
+    case KDFM_EPI_RELU: return SKC_EPI_RELU;
+    case KDFM_EPI_RESID: return SKC_EPI_RESID;
+    case KDFM_EPI_DRELU: return SKC_EPI_DRELU;
+    default: return SKC_EPI_GENERIC;
+  }
+}
+
+template <int NCT, int AMODE, int WV, int EMODE = SKC_EPI_GENERIC>
 __global__ __launch_bounds__(64 * WV, 2) void sk_fwd_kernel(GemmP p, SkGeo g) {
   extern __shared__ __attribute__((aligned(16))) uint16_t sk_lds[];
   uint16_t* Bs = sk_lds;
@@ -248,8 +279,8 @@ __global__ __launch_bounds__(64 * WV, 2) void sk_fwd_kernel(GemmP p, SkGeo g) {
           for (int i = 0; i < 4; ++i) {
             const int64_t m = m0 + er + 8 * i;
             float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (m < p.M && n + 3 < p.N) {
-              v = *reinterpret_cast<const float4*>(side + m * p.sCm + n);
+            if (n + 3 < p.N) {
+              v = ld4_or0(side, m * p.sCm + n, m < p.M);
             } else if (m < p.M && n < p.N) {
               v.x = side[m * p.sCm + n];
               if (n + 1 < p.N) v.y = side[m * p.sCm + n + 1];
@@ -309,8 +340,8 @@ __global__ __launch_bounds__(64 * WV, 2) void sk_fwd_kernel(GemmP p, SkGeo g) {
             o[e] = 0.f;
             pr[e] = 0.f;
             if (n + e < p.N)
-              o[e] = epi_apply(p, 0, m, n + e, p.alpha * av4[e], bv[e], side ? s4[e] : 0.f, rowok[i], seed,
-                               keep_scale, mse_part, pr[e]);
+              o[e] = skc_epi<EMODE>(p, m, n + e, p.alpha * av4[e], bv[e], side ? s4[e] : 0.f, rowok[i], seed,
+                                    keep_scale, mse_part, pr[e]);
           }
           const int64_t off = m * p.sCm + n;
           if (n + 3 < p.N) {
@@ -486,34 +517,6 @@ __device__ __forceinline__ void skc_load_slab(float4 (&v)[SKC_SLAB_V], const Gem
     const int j = e / cq, q = e - j * cq;
     const int64_t gr = m0 - p.pad + j;
     v[i] = ld4_or0(p.A, gr * p.sAm + 4 * q, e < total && gr >= 0 && gr < p.M);
-  }
-}
-
-// Compile-time epilogues for the four denoiser products (heads.py deno_conv: conv+bias+ReLU,
-// conv+bias+residual forward; conv*alpha with dReLU, conv+residual backward).  The generic
-// epi_apply tests every flag per element; at 48 elements per lane per tile that flag walk, not
-// HBM, bounds this HBM-shaped kernel.  EMODE 0 = generic.
-enum { SKC_EPI_GENERIC = 0, SKC_EPI_RELU = 1, SKC_EPI_RESID = 2, SKC_EPI_DRELU = 3 };
-
-template <int EMODE>
-__device__ __forceinline__ float skc_epi(const GemmP& p, int64_t m, int64_t n, float v, float bn, float sv, bool rowok,
-                                         uint64_t seed, float keep_scale, float& mse_part, float& pre) {
-  if constexpr (EMODE == SKC_EPI_GENERIC) {
-    return epi_apply(p, 0, m, n, v, bn, sv, rowok, seed, keep_scale, mse_part, pre);
-  } else {
-    v += bn;  // bn is 0 without KDFM_EPI_BIAS
-    if constexpr (EMODE == SKC_EPI_RELU) return fmaxf(v, 0.f);
-    if constexpr (EMODE == SKC_EPI_RESID) return sv + p.rscale * v;
-    return sv > 0.f ? v : 0.f;  // SKC_EPI_DRELU
-  }
-}
-
-__host__ inline int skc_epi_mode(int epi) {
-  switch (epi & ~KDFM_EPI_BIAS) {
-    case KDFM_EPI_RELU: return SKC_EPI_RELU;
-    case KDFM_EPI_RESID: return SKC_EPI_RESID;
-    case KDFM_EPI_DRELU: return SKC_EPI_DRELU;
-    default: return SKC_EPI_GENERIC;
   }
 }
 
@@ -703,27 +706,41 @@ int skd_launch(const GemmP& p, const SkGeo& g, int G, int64_t gx, hipStream_t st
   return check_launch("kdfm_gemm(skinny direct)");
 }
 
-template <int NCT, int AMODE, int WV>
+template <int NCT, int AMODE, int WV, int EMODE = SKC_EPI_GENERIC>
 int sk_launch(const GemmP& p, const SkGeo& g, int64_t gx, int64_t ncr, size_t lds, hipStream_t st) {
   if (lds > 64 * 1024) {
     static bool once = [] {
-      hipFuncSetAttribute((const void*)sk_fwd_kernel<NCT, AMODE, WV>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          160 * 1024);
+      hipFuncSetAttribute((const void*)sk_fwd_kernel<NCT, AMODE, WV, EMODE>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       return true;
     }();
     (void)once;
   }
-  hipLaunchKernelGGL((sk_fwd_kernel<NCT, AMODE, WV>), dim3((unsigned)gx, (unsigned)ncr), dim3(64 * WV), lds, st, p,
-                     g);
+  hipLaunchKernelGGL((sk_fwd_kernel<NCT, AMODE, WV, EMODE>), dim3((unsigned)gx, (unsigned)ncr), dim3(64 * WV), lds,
+                     st, p, g);
   return check_launch("kdfm_gemm(skinny fwd)");
 }
+
+int env_int(const char* name, int dflt);
 
 template <int AMODE, int WV>
 int sk_dispatch_nct(int nct, const GemmP& p, const SkGeo& g, int64_t gx, int64_t ncr, size_t lds, hipStream_t st) {
   switch (nct) {
     case 1: return sk_launch<1, AMODE, WV>(p, g, gx, ncr, lds, st);
     case 2: return sk_launch<2, AMODE, WV>(p, g, gx, ncr, lds, st);
-    default: return sk_launch<3, AMODE, WV>(p, g, gx, ncr, lds, st);
+    default:
+      if constexpr (AMODE == KDFM_LD_KC && WV == 4) {
+        // the hot instantiation (stacked-head 1x1 convs / FM linears): compile-time epilogues
+        static const int fast = env_int("KDFM_SKC_FAST_EPI", 1);
+        switch ((fast && (p.N & 3) == 0 && (p.sCm & 3) == 0) ? skc_epi_mode(p.epi) : SKC_EPI_GENERIC) {
+          case SKC_EPI_NONE: return sk_launch<3, AMODE, WV, SKC_EPI_NONE>(p, g, gx, ncr, lds, st);
+          case SKC_EPI_RELU: return sk_launch<3, AMODE, WV, SKC_EPI_RELU>(p, g, gx, ncr, lds, st);
+          case SKC_EPI_RESID: return sk_launch<3, AMODE, WV, SKC_EPI_RESID>(p, g, gx, ncr, lds, st);
+          case SKC_EPI_DRELU: return sk_launch<3, AMODE, WV, SKC_EPI_DRELU>(p, g, gx, ncr, lds, st);
+          default: break;
+        }
+      }
+      return sk_launch<3, AMODE, WV>(p, g, gx, ncr, lds, st);
   }
 }
 
