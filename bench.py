@@ -34,20 +34,23 @@ MI355X_F32_MFMA_TFLOPS = 157.3
 MI355X_HBM_GBPS = 8000.0            # MI355X_MICROARCH.md §HBM (8 TB/s spec peak)
 # PMC traffic of the roofline kernel (tools/pmc_traffic.sh -> tools/pmc_summary.py, 2 separate --pmc
 # passes, FETCH_SIZE doubled per the gfx950 correction); committed under profiles/
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r01_s8_pmc_traffic.json")
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r01_s10_pmc_traffic.json")
 ROOF_KERNEL = "kdfm::skc_fwd_kernel<3>"
 
 
 def pmc_traffic(kernel: str):
+    """HBM bytes per launch of `kernel` from the committed PMC summary; template instantiations of
+    the same kernel (e.g. the compile-time epilogue variants skc_fwd_kernel<3, E>) are pooled,
+    launch-weighted, since the bench's timing tag covers all of them."""
     try:
         with open(PMC_TRAFFIC) as fh:
             rows = json.load(fh)
     except (OSError, ValueError):
         return None
-    for r in rows:
-        if r["kernel"] == kernel:
-            return r["bytes_per_launch"]
-    return None
+    stem = kernel[:-1] if kernel.endswith(">") else kernel
+    hit = [r for r in rows if r["kernel"] == kernel or r["kernel"].startswith(stem + ",")]
+    n = sum(r["launches"] for r in hit)
+    return sum(r["bytes_total"] for r in hit) / n if n else None
 
 
 def parse():
@@ -203,7 +206,7 @@ def main():
                                    "LDS-slab skc_fwd_kernel<3>)",
                          "achieved": round(d_gbps, 1), "peak": MI355X_HBM_GBPS, "unit": "GB/s",
                          "frac": round(d_gbps / MI355X_HBM_GBPS, 4), "traffic": d_traffic,
-                         "traffic_source": "profiles/r01_s8_pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE)",
+                         "traffic_source": "profiles/r01_s10_pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE)",
                          "launches": deno["launches"], "avg_ms": round(d_ms, 5), "bytes_per_launch": d_bytes},
             "roofline_mfma_ffn": {"bound": "mfma", "kernel": "kdfm_gemm ffn_up (Conformer FFN d->4d, SiLU+dropout)",
                                   "achieved": round(achieved, 3), "peak": peak, "unit": "TFLOP/s",
