@@ -184,7 +184,7 @@ __device__ __forceinline__ void store_lds(void* lds, const float (&v)[8]) {
   }
 }
 
-template <bool BF16, int AM, int BMODE>
+template <bool BF16, int AM, int BMODE, int EMODE = SKC_EPI_GENERIC>
 __global__ __launch_bounds__(NT) void gemm_kernel(P p) {
   constexpr int LDS_ELEMS = BF16 ? (64 * LDK_BF / 2) : (BK * LDX_F32);  // in floats
   __shared__ __attribute__((aligned(16))) float smem[2 * LDS_ELEMS];
@@ -310,8 +310,8 @@ __global__ __launch_bounds__(NT) void gemm_kernel(P p) {
           if (m >= p.M || n >= p.N) continue;
           const int64_t off = cOff + m * p.sCm + n * p.sCn;
           float pre = 0.f;
-          const float v = epi_apply(p, bz, m, n, p.alpha * acc[i][j][r], bnv[j][0], side ? sv[i][j][r] : 0.f,
-                                    rok[i][r], seed, keep_scale, mse_part, pre);
+          const float v = skc_epi<EMODE>(p, m, n, p.alpha * acc[i][j][r], bnv[j][0], side ? sv[i][j][r] : 0.f,
+                                         rok[i][r], seed, keep_scale, mse_part, pre, bz);
           if (epi & KDFM_EPI_STORE_PRE) p.Cpre[off] = pre;
           p.C[off] = v;
         }
@@ -345,6 +345,30 @@ __global__ __launch_bounds__(NT) void gemm_kernel(P p) {
 
 template <bool BF16>
 int launch(const P& p, int amode, int bmode, dim3 grid, hipStream_t st) {
+  if constexpr (BF16) {
+    // compile-time epilogues (gemm_common.h) for the bf16 row-operand products of the layers
+    static const int fast = [] {
+      const char* e = getenv("KDFM_SKC_FAST_EPI");
+      return e ? atoi(e) : 1;
+    }();
+    const int em = fast ? skc_epi_mode(p.epi) : SKC_EPI_GENERIC;
+    if (em != SKC_EPI_GENERIC && amode == KDFM_LD_KC && (bmode == KDFM_LD_KC || bmode == KDFM_LD_XC)) {
+#define KDFM_GEMM_FAST(BMv, EMv)                                                           \
+  if (bmode == BMv && em == EMv) {                                                         \
+    hipLaunchKernelGGL((gemm_kernel<true, KDFM_LD_KC, BMv, EMv>), grid, dim3(NT), 0, st, p); \
+    return check_launch("kdfm_gemm");                                                      \
+  }
+      KDFM_GEMM_FAST(KDFM_LD_KC, SKC_EPI_NONE)
+      KDFM_GEMM_FAST(KDFM_LD_KC, SKC_EPI_RELU)
+      KDFM_GEMM_FAST(KDFM_LD_KC, SKC_EPI_RESID)
+      KDFM_GEMM_FAST(KDFM_LD_KC, SKC_EPI_DRELU)
+      KDFM_GEMM_FAST(KDFM_LD_XC, SKC_EPI_NONE)
+      KDFM_GEMM_FAST(KDFM_LD_XC, SKC_EPI_RELU)
+      KDFM_GEMM_FAST(KDFM_LD_XC, SKC_EPI_RESID)
+      KDFM_GEMM_FAST(KDFM_LD_XC, SKC_EPI_DRELU)
+#undef KDFM_GEMM_FAST
+    }
+  }
 #define KDFM_GEMM_CASE(AMv, BMv)                                                    \
   if (amode == AMv && bmode == BMv) {                                               \
     hipLaunchKernelGGL((gemm_kernel<BF16, AMv, BMv>), grid, dim3(NT), 0, st, p);    \

@@ -110,6 +110,38 @@ __device__ __forceinline__ float epi_apply(const GemmP& p, int64_t bz, int64_t m
   return v;
 }
 
+// Compile-time epilogues for the common flag sets (the denoiser products, heads.py deno_conv:
+// conv+bias+ReLU, conv+bias+residual forward, conv*alpha with dReLU, conv+residual backward; and
+// plain / bias-only products).  The generic epi_apply tests every flag per element; at 48
+// elements per lane per tile that flag walk, not HBM, bounded the skinny HBM-shaped kernels.
+// Row masks, STORE_PRE, dropout, MSE, SiLU, BETA keep the generic path.  EMODE 0 = generic.
+enum { SKC_EPI_GENERIC = 0, SKC_EPI_RELU = 1, SKC_EPI_RESID = 2, SKC_EPI_DRELU = 3, SKC_EPI_NONE = 4 };
+
+template <int EMODE>
+__device__ __forceinline__ float skc_epi(const GemmP& p, int64_t m, int64_t n, float v, float bn, float sv, bool rowok,
+                                         uint64_t seed, float keep_scale, float& mse_part, float& pre,
+                                         int64_t bz = 0) {
+  if constexpr (EMODE == SKC_EPI_GENERIC) {
+    return epi_apply(p, bz, m, n, v, bn, sv, rowok, seed, keep_scale, mse_part, pre);
+  } else {
+    v += bn;  // bn is 0 without KDFM_EPI_BIAS
+    if constexpr (EMODE == SKC_EPI_RELU) return fmaxf(v, 0.f);
+    if constexpr (EMODE == SKC_EPI_RESID) return sv + p.rscale * v;
+    if constexpr (EMODE == SKC_EPI_DRELU) return sv > 0.f ? v : 0.f;
+    return v;  // SKC_EPI_NONE
+  }
+}
+
+__host__ inline int skc_epi_mode(int epi) {
+  switch (epi & ~KDFM_EPI_BIAS) {
+    case 0: return SKC_EPI_NONE;
+    case KDFM_EPI_RELU: return SKC_EPI_RELU;
+    case KDFM_EPI_RESID: return SKC_EPI_RESID;
+    case KDFM_EPI_DRELU: return SKC_EPI_DRELU;
+    default: return SKC_EPI_GENERIC;
+  }
+}
+
 // Row-stream / wide-tile entry points (rowstream.hip).  try_* return -1 when the descriptor is
 // not eligible (caller falls back to the generic kernel), else a kdfm_status.
 int try_rowstream_fwd(const GemmP& p, int amode, int bmode, int64_t batch, hipStream_t st);

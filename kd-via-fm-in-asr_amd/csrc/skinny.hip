@@ -175,37 +175,7 @@ __device__ __forceinline__ void sk_load_A(float4 (&v)[SK_CKS][2], const GemmP& p
   }
 }
 
-// Compile-time epilogues for the common flag sets (the denoiser products, heads.py deno_conv:
-// conv+bias+ReLU, conv+bias+residual forward, conv*alpha with dReLU, conv+residual backward; and
-// plain / bias-only products).  The generic epi_apply tests every flag per element; at 48
-// elements per lane per tile that flag walk, not HBM, bounded these HBM-shaped kernels.
-// Row masks, STORE_PRE, dropout, MSE, SiLU keep the generic path.  EMODE 0 = generic.
-enum { SKC_EPI_GENERIC = 0, SKC_EPI_RELU = 1, SKC_EPI_RESID = 2, SKC_EPI_DRELU = 3, SKC_EPI_NONE = 4 };
-
-template <int EMODE>
-__device__ __forceinline__ float skc_epi(const GemmP& p, int64_t m, int64_t n, float v, float bn, float sv, bool rowok,
-                                         uint64_t seed, float keep_scale, float& mse_part, float& pre) {
-  if constexpr (EMODE == SKC_EPI_GENERIC) {
-    return epi_apply(p, 0, m, n, v, bn, sv, rowok, seed, keep_scale, mse_part, pre);
-  } else {
-    v += bn;  // bn is 0 without KDFM_EPI_BIAS
-    if constexpr (EMODE == SKC_EPI_RELU) return fmaxf(v, 0.f);
-    if constexpr (EMODE == SKC_EPI_RESID) return sv + p.rscale * v;
-    if constexpr (EMODE == SKC_EPI_DRELU) return sv > 0.f ? v : 0.f;
-    return v;  // SKC_EPI_NONE
-  }
-}
-
-__host__ inline int skc_epi_mode(int epi) {
-  switch (epi & ~KDFM_EPI_BIAS) {
-    case 0: return SKC_EPI_NONE;
-    case KDFM_EPI_RELU: return SKC_EPI_RELU;
-    case KDFM_EPI_RESID: return SKC_EPI_RESID;
-    case KDFM_EPI_DRELU: return SKC_EPI_DRELU;
-    default: return SKC_EPI_GENERIC;
-  }
-}
-
+// (compile-time epilogues SKC_EPI_*: gemm_common.h)
 template <int NCT, int AMODE, int WV, int EMODE = SKC_EPI_GENERIC>
 __global__ __launch_bounds__(64 * WV, 2) void sk_fwd_kernel(GemmP p, SkGeo g) {
   extern __shared__ __attribute__((aligned(16))) uint16_t sk_lds[];

@@ -4,7 +4,7 @@
 set -o pipefail
 OUT=gpurun_out/ab_epi
 mkdir -p $OUT
-timeout -k 10 300 python -u -m pytest tests/test_skinny_gpu.py tests/test_kernels_gpu.py tests/test_ddp_overlap_gpu.py -x -q --timeout 120 --timeout-method thread > $OUT/t.log 2>&1 || { tail -20 $OUT/t.log; exit 1; }
+timeout -k 10 300 python -u -m pytest tests/test_gemm_gpu.py tests/test_skinny_gpu.py tests/test_kernels_gpu.py tests/test_ddp_overlap_gpu.py tests/test_rowstream_gpu.py -x -q --timeout 120 --timeout-method thread > $OUT/t.log 2>&1 || { tail -20 $OUT/t.log; exit 1; }
 tail -1 $OUT/t.log
 for f in 0 1; do
   KDFM_SKC_FAST_EPI=$f timeout -k 10 120 python -u tools/skc_scan.py > $OUT/scan_$f.log 2>&1 || exit 1
