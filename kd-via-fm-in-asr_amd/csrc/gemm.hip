@@ -366,6 +366,10 @@ int launch(const P& p, int amode, int bmode, dim3 grid, hipStream_t st) {
       KDFM_GEMM_FAST(KDFM_LD_XC, SKC_EPI_RELU)
       KDFM_GEMM_FAST(KDFM_LD_XC, SKC_EPI_RESID)
       KDFM_GEMM_FAST(KDFM_LD_XC, SKC_EPI_DRELU)
+      KDFM_GEMM_FAST(KDFM_LD_KC, SKC_EPI_SILU_DROP)
+      KDFM_GEMM_FAST(KDFM_LD_KC, SKC_EPI_DROP_RESID)
+      KDFM_GEMM_FAST(KDFM_LD_XC, SKC_EPI_SILU_DROP)
+      KDFM_GEMM_FAST(KDFM_LD_XC, SKC_EPI_DROP_RESID)
 #undef KDFM_GEMM_FAST
     }
   }

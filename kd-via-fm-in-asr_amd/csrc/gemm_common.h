@@ -115,7 +115,11 @@ __device__ __forceinline__ float epi_apply(const GemmP& p, int64_t bz, int64_t m
 // plain / bias-only products).  The generic epi_apply tests every flag per element; at 48
 // elements per lane per tile that flag walk, not HBM, bounded the skinny HBM-shaped kernels.
 // Row masks, STORE_PRE, dropout, MSE, SiLU, BETA keep the generic path.  EMODE 0 = generic.
-enum { SKC_EPI_GENERIC = 0, SKC_EPI_RELU = 1, SKC_EPI_RESID = 2, SKC_EPI_DRELU = 3, SKC_EPI_NONE = 4 };
+// SILU_DROP: Conformer FFN up-projection (bias, SiLU, optional dropout, optional STORE_PRE);
+// DROP_RESID: FFN down / attention out / conv pw2 (bias, dropout, scaled residual).  Same
+// arithmetic and dropout index as epi_apply.
+enum { SKC_EPI_GENERIC = 0, SKC_EPI_RELU = 1, SKC_EPI_RESID = 2, SKC_EPI_DRELU = 3, SKC_EPI_NONE = 4,
+       SKC_EPI_SILU_DROP = 5, SKC_EPI_DROP_RESID = 6 };
 
 template <int EMODE>
 __device__ __forceinline__ float skc_epi(const GemmP& p, int64_t m, int64_t n, float v, float bn, float sv, bool rowok,
@@ -128,6 +132,16 @@ __device__ __forceinline__ float skc_epi(const GemmP& p, int64_t m, int64_t n, f
     if constexpr (EMODE == SKC_EPI_RELU) return fmaxf(v, 0.f);
     if constexpr (EMODE == SKC_EPI_RESID) return sv + p.rscale * v;
     if constexpr (EMODE == SKC_EPI_DRELU) return sv > 0.f ? v : 0.f;
+    if constexpr (EMODE == SKC_EPI_SILU_DROP || EMODE == SKC_EPI_DROP_RESID) {
+      pre = v;
+      if constexpr (EMODE == SKC_EPI_SILU_DROP) v = siluf_(v);
+      if (p.epi & KDFM_EPI_DROPOUT) {
+        const uint64_t idx = ((uint64_t)bz * (uint64_t)p.M + (uint64_t)m) * (uint64_t)p.N + (uint64_t)n;
+        v = dropout_keep(seed, p.rng_stream, idx, p.dropout_p) ? v * keep_scale : 0.f;
+      }
+      if constexpr (EMODE == SKC_EPI_DROP_RESID) v = sv + p.rscale * v;
+      return v;
+    }
     return v;  // SKC_EPI_NONE
   }
 }
@@ -138,8 +152,11 @@ __host__ inline int skc_epi_mode(int epi) {
     case KDFM_EPI_RELU: return SKC_EPI_RELU;
     case KDFM_EPI_RESID: return SKC_EPI_RESID;
     case KDFM_EPI_DRELU: return SKC_EPI_DRELU;
-    default: return SKC_EPI_GENERIC;
+    case KDFM_EPI_RESID | KDFM_EPI_DROPOUT: return SKC_EPI_DROP_RESID;
+    default: break;
   }
+  if ((epi & ~(KDFM_EPI_BIAS | KDFM_EPI_DROPOUT | KDFM_EPI_STORE_PRE)) == KDFM_EPI_SILU) return SKC_EPI_SILU_DROP;
+  return SKC_EPI_GENERIC;
 }
 
 // Row-stream / wide-tile entry points (rowstream.hip).  try_* return -1 when the descriptor is

@@ -72,3 +72,45 @@ def test_conv3_mode(K):
            epi=_lib.EPI_BIAS, bias=b, conv=(3, 1, Cc, T), math="f32")
     ref = torch.nn.functional.conv1d(x.transpose(1, 2), W, b, padding=1).transpose(1, 2).reshape(Bn * T, Cc)
     torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("kind", ["silu", "resid"])
+def test_bf16_dropout_epilogues_match_f32_path(kind):
+    """The compile-time FFN epilogues of the bf16 GEMM (SiLU+dropout+STORE_PRE, dropout+residual)
+    against the generic f32 GEMM followed by the standalone dropout kernel with the same counter
+    RNG: identical drop pattern, values within bf16 tolerance."""
+    from kdfm import _lib
+    from kdfm import kernels as K
+    g = torch.Generator(device="cuda").manual_seed(7)
+    M, Kd, N = 12832, 88, 352 if kind == "silu" else 88
+    x = torch.randn(M, Kd, device="cuda", generator=g)
+    W = torch.randn(N, Kd, device="cuda", generator=g) * 0.1
+    b = torch.randn(N, device="cuda", generator=g)
+    R = torch.randn(M, N, device="cuda", generator=g)
+    seed = torch.tensor([12345], dtype=torch.int64, device="cuda")
+    p = 0.1
+    y = torch.empty(M, N, device="cuda")
+    pre = torch.empty(M, N, device="cuda")
+    ref_pre = torch.empty(M, N, device="cuda")
+    if kind == "silu":
+        K.linear(x, W, b, y, epi=_lib.EPI_SILU | _lib.EPI_STORE_PRE, Cpre=pre, dropout_p=p, seed=seed,
+                 rng_stream=5, math="bf16")
+        K.linear(x, W, b, ref_pre, math="f32")
+        act = torch.nn.functional.silu(ref_pre)
+    else:
+        K.linear(x, W, b, y, epi=_lib.EPI_RESID, R=R, rscale=0.5, dropout_p=p, seed=seed, rng_stream=5,
+                 math="bf16")
+        K.linear(x, W, b, ref_pre, math="f32")
+        act = ref_pre.clone()
+    ref = torch.empty_like(act)
+    K.dropout(act.contiguous(), ref, p, 1.0, seed, 5)
+    if kind == "resid":
+        ref = R + 0.5 * ref
+        kept = (y - R).abs() > 0
+        want_kept = (ref - R).abs() > 0
+    else:
+        kept = y != 0
+        want_kept = ref != 0
+        torch.testing.assert_close(pre, ref_pre, rtol=2e-2, atol=2e-2)
+    assert torch.equal(kept, want_kept)
+    torch.testing.assert_close(y, ref, rtol=2e-2, atol=3e-2)
