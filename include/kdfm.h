@@ -39,6 +39,16 @@ typedef enum kdfm_math {
 const char* kdfm_version(void);
 const char* kdfm_last_error(void);
 int kdfm_device_arch(char* buf, int64_t len); /* writes the gcnArchName of the current device */
+/* Deterministic-reduction mode ("a deterministic reduction flag is used for parity
+ * runs").  When on, every reduction that feeds an activation or a gradient runs in a fixed order:
+ * GEMM split-K and batch-axis reductions become ordered launches, per-block partial folds
+ * (column sums, BatchNorm statistics and their backward, NoiseAdapter gate gradients) run in one
+ * workgroup per output group, wide-tile weight-gradient partials fold in slab order — so two runs
+ * on the same inputs give bitwise-identical activations and gradients.  Scalar loss accumulators
+ * (MSE / KL sums) keep float atomics and may differ in the last bits.  Process-global; read on the
+ * host when a launch is configured (set it before capturing a graph).  Default off. */
+void kdfm_set_deterministic(int32_t on);
+int32_t kdfm_get_deterministic(void);
 
 /* --------------------------------------------------------------------------------------------
  * Generic batched GEMM with fused epilogue:

@@ -15,6 +15,10 @@ namespace kdfm {
 // ---- error handling -------------------------------------------------------------------------
 void set_error(const std::string& msg);
 int check_launch(const char* what);
+// Deterministic-reduction mode (kdfm_set_deterministic): every reduction that feeds an activation
+// or a gradient runs in a fixed order (no split-K / cross-block float atomics), so two runs on the
+// same inputs give bitwise-identical results.  Read on the host when a launch is configured.
+bool deterministic();
 
 #define KDFM_REQUIRE(cond, msg)                                  \
   do {                                                           \

@@ -146,6 +146,30 @@ __global__ __launch_bounds__(256) void dwconv_fwd_kernel(const float* __restrict
   }
 }
 
+// Deterministic-mode BatchNorm statistics: stats[c] += sum_r y[r,c], stats[d+c] += sum_r y[r,c]^2 with
+// one workgroup per 64 channels (lane = channel, the 4 waves stride the rows, fixed-order combine),
+// replacing the per-tile f64 atomics of dwconv_fwd_kernel.
+__global__ __launch_bounds__(256) void bn_stats_det_kernel(const float* __restrict__ y, double* __restrict__ stats,
+                                                           int64_t rows, int64_t d) {
+  __shared__ double sh[2][4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t c = (int64_t)blockIdx.x * 64 + lane;
+  double s1 = 0.0, s2 = 0.0;
+  if (c < d)
+    for (int64_t r = w; r < rows; r += 4) {
+      const double v = y[r * d + c];
+      s1 += v;
+      s2 += v * v;
+    }
+  sh[0][w][lane] = s1;
+  sh[1][w][lane] = s2;
+  __syncthreads();
+  if (w == 0 && c < d) {
+    stats[c] += (sh[0][0][lane] + sh[0][1][lane]) + (sh[0][2][lane] + sh[0][3][lane]);
+    stats[d + c] += (sh[1][0][lane] + sh[1][1][lane]) + (sh[1][2][lane] + sh[1][3][lane]);
+  }
+}
+
 // mean/rstd per channel: batch statistics (biased var) or running statistics (eval)
 __global__ __launch_bounds__(256) void bn_finalize_kernel(const double* __restrict__ stats, const float* __restrict__ rm,
                                                           const float* __restrict__ rv, float* __restrict__ mean,
@@ -265,7 +289,10 @@ __global__ __launch_bounds__(256) void dwconv_bwd_kernel(const float* __restrict
   constexpr int KM = KC > 0 ? KC : KMAX;
   __shared__ __attribute__((aligned(16))) float tdy[(TT + KM - 1) * CT];  // frames t0-pad .. t0+TT-1+pad
   __shared__ __attribute__((aligned(16))) float tg[(TT + KM - 1) * CT];
-  __shared__ float red[(KM + 1) * CT];
+  // KC > 0: one partial slot per wave, folded in wave order below (deterministic); the runtime-K
+  // path keeps LDS atomics (not used by the k = 15 / 31 configurations)
+  constexpr int NSLOT = KC > 0 ? 4 : 1;
+  __shared__ float red[NSLOT][(KM + 1) * CT];
   const int K = KC > 0 ? KC : Krt;
   const int pad = (K - 1) / 2;
   const int64_t b = blockIdx.z;
@@ -279,8 +306,9 @@ __global__ __launch_bounds__(256) void dwconv_bwd_kernel(const float* __restrict
     tile_store(v1, tdy, rowsIn);
     tile_store(v2, tg, rowsIn);
   }
-  for (int e = threadIdx.x; e < (K + 1) * CT; e += 256) red[e] = 0.f;
+  for (int e = threadIdx.x; e < NSLOT * (K + 1) * CT; e += 256) (&red[0][0])[e] = 0.f;
   __syncthreads();
+  const int slot = KC > 0 ? (threadIdx.x >> 6) : 0;
   const int cc = threadIdx.x & 63;
   const int f0 = (threadIdx.x >> 6) * 16;  // this wave's first frame in the tile
   const int64_t c = c0 + cc;
@@ -328,7 +356,7 @@ __global__ __launch_bounds__(256) void dwconv_bwd_kernel(const float* __restrict
       float s = 0.f;
 #pragma unroll
       for (int tt = 0; tt < 16; ++tt) s += dyr[tt] * win[tt];
-      atomicAdd(&red[k * CT + cc], s);
+      red[slot][k * CT + cc] = s;
       if (k + 1 < KC) {
 #pragma unroll
         for (int tt = 0; tt < 15; ++tt) win[tt] = win[tt + 1];
@@ -346,10 +374,13 @@ __global__ __launch_bounds__(256) void dwconv_bwd_kernel(const float* __restrict
     for (int k = 0; k < K; ++k) {
       float acc = 0.f;
       for (int tt = 0; tt < 16; ++tt) acc += tdy[(f0 + tt + pad) * CT + cc] * tg[(f0 + tt + k) * CT + cc];
-      atomicAdd(&red[k * CT + cc], acc);
+      atomicAdd(&red[0][k * CT + cc], acc);
     }
   }
-  atomicAdd(&red[K * CT + cc], bsum);
+  if constexpr (KC > 0)
+    red[slot][K * CT + cc] = bsum;
+  else
+    atomicAdd(&red[0][K * CT + cc], bsum);
   __syncthreads();
   const int64_t ld = d * (K + 1);
   float* pr = part + (b * gridDim.x + blockIdx.x) * ld;
@@ -357,10 +388,12 @@ __global__ __launch_bounds__(256) void dwconv_bwd_kernel(const float* __restrict
     const int q = e / (K + 1), k = e % (K + 1);
     const int64_t cq = c0 + q;
     if (cq >= d) continue;
+    float v = red[0][k * CT + q];
+    if constexpr (KC > 0) v = (v + red[1][k * CT + q]) + (red[2][k * CT + q] + red[3][k * CT + q]);
     if (k < K)
-      pr[cq * K + k] = red[k * CT + q];
+      pr[cq * K + k] = v;
     else
-      pr[d * K + cq] = red[K * CT + q];
+      pr[d * K + cq] = v;
   }
 }
 
@@ -399,13 +432,18 @@ int kdfm_dwconv_fwd(const float* g, const float* w, const float* bias, float* y,
   KDFM_REQUIRE(d % 4 == 0 && (((uintptr_t)g) & 15) == 0, "channels must be a multiple of 4, input 16-B aligned");
   if (B * T * d == 0) return KDFM_OK;
   dim3 grid((unsigned)ceil_div(T, TT), (unsigned)ceil_div(d, CT), (unsigned)B);
+  double* st_fused = deterministic() ? nullptr : stats;
   if (K == 31)
-    hipLaunchKernelGGL(dwconv_fwd_kernel<31>, grid, dim3(256), 0, as_stream(stream), g, w, bias, y, stats, T, d, (int)K);
+    hipLaunchKernelGGL(dwconv_fwd_kernel<31>, grid, dim3(256), 0, as_stream(stream), g, w, bias, y, st_fused, T, d, (int)K);
   else if (K == 15)
-    hipLaunchKernelGGL(dwconv_fwd_kernel<15>, grid, dim3(256), 0, as_stream(stream), g, w, bias, y, stats, T, d, (int)K);
+    hipLaunchKernelGGL(dwconv_fwd_kernel<15>, grid, dim3(256), 0, as_stream(stream), g, w, bias, y, st_fused, T, d, (int)K);
   else
-    hipLaunchKernelGGL(dwconv_fwd_kernel<0>, grid, dim3(256), 0, as_stream(stream), g, w, bias, y, stats, T, d, (int)K);
-  return check_launch("kdfm_dwconv_fwd");
+    hipLaunchKernelGGL(dwconv_fwd_kernel<0>, grid, dim3(256), 0, as_stream(stream), g, w, bias, y, st_fused, T, d, (int)K);
+  int rc = check_launch("kdfm_dwconv_fwd");
+  if (rc || !stats || st_fused) return rc;
+  hipLaunchKernelGGL(bn_stats_det_kernel, dim3((unsigned)ceil_div(d, 64)), dim3(256), 0, as_stream(stream), y, stats,
+                     B * T, d);
+  return check_launch("kdfm_dwconv_fwd(det stats)");
 }
 
 int64_t kdfm_dwconv_bwd_ws(int64_t B, int64_t T, int64_t d, int64_t K) {
@@ -481,6 +519,7 @@ int kdfm_bn_silu_bwd(const float* dz, const float* y, const float* mean, const f
   }
   int64_t gy = ceil_div(rows, 256);
   if (gy > 512) gy = 512;
+  if (deterministic()) gy = 1;  // one workgroup per channel group: fixed summation order
   const int64_t rp = ceil_div(rows, gy);
   gy = ceil_div(rows, rp);
   hipLaunchKernelGGL(bn_silu_bwd_reduce_kernel, dim3((unsigned)ceil_div(d, 64), (unsigned)gy), dim3(256), 0, st, dz,

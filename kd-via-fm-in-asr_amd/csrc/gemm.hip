@@ -328,6 +328,10 @@ __global__ __launch_bounds__(NT) void gemm_kernel(P p) {
         const int64_t off = cOff + m * p.sCm + n * p.sCn;
         float v = p.alpha * acc[i][j][r];
         if (epi & KDFM_EPI_ATOMIC) {
+          if (p.partial) {  // deterministic split-K: raw partial, folded in split order afterwards
+            p.ws[(split * p.M + m) * p.N + n] = acc[i][j][r];
+            continue;
+          }
           if (n == p.ones_col)
             atomicAdd(p.ones_out + m, v);
           else
@@ -438,6 +442,40 @@ extern "C" int kdfm_gemm(const kdfm_gemm_desc* d, void* stream) {
   if (d->epi & KDFM_EPI_MSE) KDFM_REQUIRE(d->loss_acc && d->R, "MSE needs loss_acc and target R");
   if (d->K == 0) p.splitk = 1;
   hipStream_t st = as_stream(stream);
+  p.partial = 0;
+  if (deterministic() && (d->epi & KDFM_EPI_ATOMIC)) {
+    // fixed-order reductions: split-K partials go to the caller's workspace and are folded in split
+    // order (or, without a workspace, no split: one add per output element per launch); a batch
+    // axis that reduces into one C (a zero C batch stride) is walked by successive launches on the
+    // stream instead of concurrent atomics
+    const bool red1 = d->batch1 > 1 && d->bC1 == 0, red2 = d->batch2 > 1 && d->bC2 == 0;
+    if (red1 || red2) {
+      kdfm_gemm_desc e = *d;
+      e.splitk = 1;
+      const int64_t n1 = red1 ? d->batch1 : 1, n2 = red2 ? d->batch2 : 1;
+      for (int64_t i1 = 0; i1 < n1; ++i1)
+        for (int64_t i2 = 0; i2 < n2; ++i2) {
+          e.A = d->A + i1 * (red1 ? d->bA1 : 0) + i2 * (red2 ? d->bA2 : 0);
+          e.B = d->B + i1 * (red1 ? d->bB1 : 0) + i2 * (red2 ? d->bB2 : 0);
+          e.batch1 = red1 ? 1 : d->batch1;
+          e.batch2 = red2 ? 1 : d->batch2;
+          const int rc = kdfm_gemm(&e, stream);
+          if (rc) return rc;
+        }
+      return KDFM_OK;
+    }
+    const int64_t need = (int64_t)p.splitk * d->M * d->N;
+    if (p.splitk > 1 && d->batch1 * d->batch2 == 1 && d->ws && d->ws_len >= need &&
+        !(d->math == KDFM_MATH_BF16 && rowstream_wgrad_ws(p, d->amode, d->bmode, 1) > 0)) {
+      p.partial = 1;
+      dim3 grid((unsigned)ceil_div(d->M, BM), (unsigned)ceil_div(d->N, BN), (unsigned)p.splitk);
+      const int rc = d->math == KDFM_MATH_BF16 ? launch<true>(p, d->amode, d->bmode, grid, st)
+                                               : launch<false>(p, d->amode, d->bmode, grid, st);
+      if (rc) return rc;
+      return launch_split_fold(p, p.splitk, true, st);
+    }
+    if (!(d->math == KDFM_MATH_BF16 && d->ws && rowstream_wgrad_ws(p, d->amode, d->bmode, 1) > 0)) p.splitk = 1;
+  }
   if (d->math == KDFM_MATH_BF16 && d->K > 0) {
     const int64_t batch = d->batch1 * d->batch2;
     int rc = try_rowstream_wgrad(p, d->amode, d->bmode, batch, st);
@@ -456,12 +494,18 @@ extern "C" int kdfm_gemm(const kdfm_gemm_desc* d, void* stream) {
 
 extern "C" int64_t kdfm_gemm_ws(const kdfm_gemm_desc* d) {
   using namespace kdfm;
-  if (!d || d->math != KDFM_MATH_BF16 || d->K <= 0 || d->M <= 0 || d->N <= 0) return 0;
+  if (!d || d->K <= 0 || d->M <= 0 || d->N <= 0) return 0;
+  if (d->math != KDFM_MATH_BF16 && !(deterministic() && (d->epi & KDFM_EPI_ATOMIC) && d->splitk > 1)) return 0;
   GemmP p{};
   p.M = d->M; p.N = d->N; p.K = d->K;
   p.sAm = d->sAm; p.sAk = d->sAk; p.sBk = d->sBk; p.sBn = d->sBn; p.sCm = d->sCm; p.sCn = d->sCn;
   p.epi = d->epi; p.splitk = d->splitk; p.taps = d->conv_taps; p.pad = d->conv_pad;
   p.conv_c = d->conv_c; p.conv_t = d->conv_t; p.ones_col = d->ones_col; p.ones_out = d->ones_out;
   p.Bh = nullptr; p.sBh = 0;
-  return rowstream_wgrad_ws(p, d->amode, d->bmode, d->batch1 * d->batch2);
+  int64_t n = rowstream_wgrad_ws(p, d->amode, d->bmode, d->batch1 * d->batch2);
+  if (deterministic() && (d->epi & KDFM_EPI_ATOMIC) && d->splitk > 1 && d->batch1 * d->batch2 == 1) {
+    const int64_t sk = (int64_t)d->splitk * d->M * d->N;  // ordered split-K partials
+    if (sk > n) n = sk;
+  }
+  return n;
 }

@@ -26,6 +26,7 @@ struct GemmP {
   float* ones_out; int64_t ones_col;
   float* ws; int64_t ws_len;
   const uint16_t* Bh; int64_t sBh;
+  int partial;  // deterministic split-K: ATOMIC tiles store raw partials to ws[split][m][n] (folded in order)
 };
 
 // Non-atomic epilogue for one output element.  v = alpha * acc (already scaled).  bz = batch
@@ -164,6 +165,9 @@ __host__ inline int skc_epi_mode(int epi) {
 int try_rowstream_fwd(const GemmP& p, int amode, int bmode, int64_t batch, hipStream_t st);
 int try_rowstream_wgrad(const GemmP& p, int amode, int bmode, int64_t batch, hipStream_t st);
 int64_t rowstream_wgrad_ws(const GemmP& p, int amode, int bmode, int64_t batch);
+// C(m,n) += alpha * sum_{s<S} ws[s][m][n] in slab order (n == ones_col -> ones_out[m]); one thread
+// per element sums all S partials when `ordered` (deterministic mode), else slabs of 16.
+int launch_split_fold(const GemmP& p, int64_t S, bool ordered, hipStream_t st);
 // Weight-stationary skinny forward (skinny.hip); -1 when not eligible.
 int try_skinny_fwd(const GemmP& p, int amode, int bmode, int64_t batch, hipStream_t st);
 

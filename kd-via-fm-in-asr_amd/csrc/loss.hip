@@ -104,13 +104,29 @@ __global__ __launch_bounds__(256) void ctc_kernel(const float* __restrict__ lp, 
   float* prev = sh;                      // S_max
   float* cur = sh + S_max;               // S_max
   int* lab = reinterpret_cast<int*>(sh + 2 * S_max);  // S_max
-  float* bins = sh + 3 * S_max;          // C
-  __shared__ float nll_sh;
+  float* contrib = sh + 3 * S_max;       // S_max: per-position posterior term of the current frame
+  int* nxt = reinterpret_cast<int*>(sh + 4 * S_max);  // S_max: next odd position with the same label
+  int* head = reinterpret_cast<int*>(sh + 5 * S_max);  // C: first odd position of each label (-1: none)
+  __shared__ float nll_sh, blank_sh;
   const float* lpb = lp + b * T * C;
   float* al = alpha + b * T * S_max;
   float* be = beta + b * T * S_max;
   for (int64_t s = threadIdx.x; s < S; s += blockDim.x)
     lab[s] = (s & 1) ? (int)targets[b * Umax + (s >> 1)] : blank;
+  __syncthreads();
+  // per-label position lists (built once per utterance by one lane): the posterior of class c at a
+  // frame is summed over its positions in ascending order, a fixed order (no LDS atomics), so the
+  // logits gradient is bitwise reproducible
+  if (threadIdx.x == 0) {
+    for (int c = 0; c < C; ++c) head[c] = -1;
+    for (int64_t s = S - 2; s >= 1; s -= 2) {  // S = 2U+1: the odd (label) positions
+      const int l = lab[s];
+      if (l >= 0 && l < C) {
+        nxt[s] = head[l];
+        head[l] = (int)s;
+      }
+    }
+  }
   __syncthreads();
   if (Tb <= 0) {
     if (threadIdx.x == 0) nll_out[b] = (U == 0 || !zero_inf) ? (U == 0 ? 0.f : INFINITY) : 0.f;
@@ -175,15 +191,23 @@ __global__ __launch_bounds__(256) void ctc_kernel(const float* __restrict__ lp, 
       __syncthreads();
       float* tmp = prev; prev = cur; cur = tmp;
     }
-    for (int c = threadIdx.x; c < C; c += blockDim.x) bins[c] = 0.f;
-    __syncthreads();
     for (int64_t s = threadIdx.x; s < S; s += blockDim.x) {
       const float ab = al[t * S_max + s] + prev[s];
-      if (ab > NEG_INF) atomicAdd(&bins[lab[s]], __expf(ab - lpb[t * C + lab[s]] + nll));
+      contrib[s] = (ab > NEG_INF) ? __expf(ab - lpb[t * C + lab[s]] + nll) : 0.f;
     }
     __syncthreads();
-    for (int c = threadIdx.x; c < C; c += blockDim.x)
-      grad[(b * T + t) * C + c] = scale * (__expf(lpb[t * C + c]) - bins[c]);
+    if (threadIdx.x < 64) {  // blank posterior: the even positions, lane-strided + butterfly
+      float v = 0.f;
+      for (int64_t s = 2 * threadIdx.x; s < S; s += 128) v += contrib[s];
+      v = wave_sum(v);
+      if (threadIdx.x == 0) blank_sh = v;
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+      float post = (c == blank) ? blank_sh : 0.f;
+      for (int s = head[c]; s >= 0; s = nxt[s]) post += contrib[s];
+      grad[(b * T + t) * C + c] = scale * (__expf(lpb[t * C + c]) - post);
+    }
     __syncthreads();
   }
   for (int64_t i = Tb * C + threadIdx.x; i < T * C; i += blockDim.x) grad[b * T * C + i] = 0.f;
@@ -306,7 +330,7 @@ int kdfm_ctc_loss(const float* log_probs, const int64_t* targets, const int64_t*
                "null pointer");
   KDFM_REQUIRE(blank >= 0 && blank < C && C <= 4096 && Umax >= 1 && Umax <= 4096, "bad sizes");
   if (B == 0) return KDFM_OK;
-  const size_t shmem = sizeof(float) * (3 * (2 * Umax + 1) + C);
+  const size_t shmem = sizeof(float) * (5 * (2 * Umax + 1) + C);
   KDFM_REQUIRE(shmem <= 60 * 1024, "CTC workspace exceeds LDS");
   hipLaunchKernelGGL(ctc_kernel, dim3((unsigned)B), dim3(256), shmem, as_stream(stream), log_probs, targets,
                      input_lengths, target_lengths, alpha_ws, beta_ws, nll, grad, T, (int)C, Umax, (int)blank,

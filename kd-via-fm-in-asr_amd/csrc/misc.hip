@@ -369,6 +369,7 @@ int kdfm_adapter_bwd(const float* dzn, const float* zs, const float* h, const fl
   if (rows == 0) return KDFM_OK;
   int64_t blocks = ceil_div(rows, 64);
   if (blocks > 2048) blocks = 2048;
+  if (deterministic()) blocks = 1;  // dw2 / db2 summed by one workgroup in a fixed order
   const int64_t rp = ceil_div(rows, blocks);
   blocks = ceil_div(rows, rp);
   hipLaunchKernelGGL(adapter_bwd_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), dzn, zs, h, gamma, w2,

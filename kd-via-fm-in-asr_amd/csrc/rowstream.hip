@@ -580,11 +580,15 @@ int try_rowstream_wgrad(const GemmP& p, int amode, int bmode, int64_t batch, hip
     }
   }
   if (rc) return rc;
+  return launch_split_fold(p, S, deterministic(), st);
+}
+
+int launch_split_fold(const GemmP& p, int64_t S, bool ordered, hipStream_t st) {
   const int64_t MN = p.M * p.N;
-  const int64_t per = 16;
+  const int64_t per = ordered ? S : 16;  // ordered: one fold thread sums every slab in order
   const int64_t slabs = ceil_div(S, per);
   hipLaunchKernelGGL(rs_fold_kernel, dim3((unsigned)ceil_div(MN, 256), (unsigned)slabs), dim3(256), 0, st, p, S, per);
-  return check_launch("kdfm_gemm(rowstream fold)");
+  return check_launch("kdfm_gemm(split fold)");
 }
 
 namespace {

@@ -7,8 +7,10 @@
 namespace kdfm {
 
 static thread_local std::string g_last_error;
+static int g_deterministic = 0;
 
 void set_error(const std::string& msg) { g_last_error = msg; }
+bool deterministic() { return g_deterministic != 0; }
 
 int check_launch(const char* what) {
   hipError_t e = hipGetLastError();
@@ -57,7 +59,7 @@ int launch_colsum(const float* X, float* out, int64_t M, int64_t N, int64_t ld, 
   const int64_t gx = ceil_div(N, 64);
   int64_t gy = ceil_div(M, 128);
   if (gy * gx > 2048) gy = (2048 + gx - 1) / gx;
-  if (gy < 1) gy = 1;
+  if (gy < 1 || deterministic()) gy = 1;  // one block per column group: a fixed summation order
   const int64_t rows_per = ceil_div(M, gy);
   gy = ceil_div(M, rows_per);
   hipLaunchKernelGGL(colsum_kernel, dim3((unsigned)gx, (unsigned)gy), dim3(256), 0, st, X, out, M, N, ld, rows_per,
@@ -72,6 +74,10 @@ extern "C" {
 const char* kdfm_version(void) { return "kdfm 0.1.0 (gfx950)"; }
 
 const char* kdfm_last_error(void) { return kdfm::g_last_error.c_str(); }
+
+void kdfm_set_deterministic(int32_t on) { kdfm::g_deterministic = on ? 1 : 0; }
+
+int32_t kdfm_get_deterministic(void) { return kdfm::g_deterministic; }
 
 int kdfm_device_arch(char* buf, int64_t len) {
   KDFM_REQUIRE(buf && len > 0, "null buffer");

@@ -67,6 +67,8 @@ SIGNATURES: dict[str, tuple] = {
     "kdfm_version": (C.c_char_p, []),
     "kdfm_last_error": (C.c_char_p, []),
     "kdfm_device_arch": (_i32, [C.c_char_p, _i64]),
+    "kdfm_set_deterministic": (None, [_i32]),
+    "kdfm_get_deterministic": (_i32, []),
     "kdfm_gemm": (_i32, [C.POINTER(GemmDesc), P]),
     "kdfm_gemm_ws": (_i64, [C.POINTER(GemmDesc)]),
     "kdfm_cast_bf16": (_i32, [P, P, _i64, P]),

@@ -61,6 +61,7 @@ class Ver5Config:
     sched_d_model: int = 88
     # execution
     math: str = "bf16"               # MFMA arithmetic: "bf16" (throughput) or "f32" (parity)
+    deterministic: bool = False      # ordered reductions (kdfm_set_deterministic): bitwise-reproducible runs
     share_frontend: bool = True      # one mel frontend for student+teacher when dither == 0
 
     @property
@@ -69,7 +70,8 @@ class Ver5Config:
 
     def parity(self) -> "Ver5Config":
         """Deterministic fp32 configuration used against the oracle."""
-        return replace(self, dither=0.0, specaug=False, dropout=0.0, dropout_pre=0.0, dropout_att=0.0, math="f32")
+        return replace(self, dither=0.0, specaug=False, dropout=0.0, dropout_pre=0.0, dropout_att=0.0, math="f32",
+                       deterministic=True)
 
 
 # ------------------------------------------------------------------------------------------------

@@ -18,6 +18,7 @@ from .config import Ver5Config, bn_buffer_specs, student_specs, teacher_specs
 from .conformer import EncoderShapes, encoder_backward, encoder_forward, make_workspace
 from .frontend import FrontendConsts, frontend_forward, mel_frames, specaugment_
 from .heads import HeadsWorkspace, heads_backward, heads_forward
+from .overlap import WGRAD
 from .store import FlatStore, init_uniform
 
 SALT_STUDENT, SALT_TEACHER, SALT_FRONT = 1, 2, 3
@@ -88,9 +89,18 @@ class Ver5Engine:
         return self._ws[key]
 
     # ---------------------------------------------------------------------------------------------
+    def _mode(self):
+        """The config's MFMA arithmetic and reduction mode for the duration of a call (restored
+        afterwards: the kernels' modes are process-global)."""
+        return K.mode(self.cfg.math, self.cfg.deterministic)
+
     def forward(self, wav, wav_len, targets, tgt_len, *, train=True, eps=None, save=True):
         """One forward pass; returns the context backward() consumes.  eps: optional injected
         NoiseAdapter noise (n_layers*B*T', latent) for parity runs."""
+        with self._mode():
+            return self._forward(wav, wav_len, targets, tgt_len, train=train, eps=eps, save=save)
+
+    def _forward(self, wav, wav_len, targets, tgt_len, *, train, eps, save):
         cfg = self.cfg
         dev = self.device
         B, N = wav.shape
@@ -183,6 +193,10 @@ class Ver5Engine:
         with BatchNorm running statistics and no dropout, decoder + log_softmax.  The reference's eval
         forward also runs the teacher encoder (:629-631) and discards it (only training_step reads
         the hooks), so it is skipped.  Returns log_probs (B, T', V+1) and enc_len (B,)."""
+        with self._mode():
+            return self._infer(wav, wav_len)
+
+    def _infer(self, wav, wav_len):
         cfg = self.cfg
         dev = self.device
         B, N = wav.shape
@@ -234,6 +248,12 @@ class Ver5Engine:
     def backward(self, ctx, grad_ready=None):
         """grad_ready(offset): optional callback, called whenever every student gradient at flat
         index >= offset is final (BucketedGradAllReduce.ready overlap)."""
+        # deterministic mode also keeps the weight-gradient products on the issuing stream: with the
+        # side stream overlapping, repeated runs differed in ~1e-3 of some gradients (DESIGN.md §4)
+        with self._mode(), WGRAD.serialized(self.cfg.deterministic):
+            self._backward(ctx, grad_ready)
+
+    def _backward(self, ctx, grad_ready):
         cfg = self.cfg
         P, G = self.student.P, self.student.G
         off = self.student.offsets
@@ -263,6 +283,10 @@ class Ver5Engine:
                          on_layer_done=layer_done)
 
     def optimizer_step(self, grad_scale: float = 1.0):
+        with self._mode():
+            self._optimizer_step(grad_scale)
+
+    def _optimizer_step(self, grad_scale):
         cfg = self.cfg
         st = self.student
         K.step_advance(self.step, None)

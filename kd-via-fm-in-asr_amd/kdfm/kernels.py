@@ -19,6 +19,7 @@ _MATH = {"f32": _lib.KDFM_MATH_F32, "bf16": _lib.KDFM_MATH_BF16}
 
 class _State:
     math = "f32"
+    deterministic = False
 
 
 class Trace:
@@ -61,6 +62,39 @@ def get_math() -> str:
     return _State.math
 
 
+def set_deterministic(on: bool) -> None:
+    """Deterministic-reduction mode of the library (include/kdfm.h kdfm_set_deterministic): ordered
+    reductions everywhere an activation or gradient is summed, bitwise reproducible runs."""
+    _lib.lib().kdfm_set_deterministic(1 if on else 0)
+    _State.deterministic = bool(on)
+
+
+def get_deterministic() -> bool:
+    return _State.deterministic
+
+
+class mode:
+    """Context manager: run a block in the given MFMA arithmetic / reduction mode and restore the
+    previous process-global modes afterwards (the engine applies its config this way)."""
+
+    def __init__(self, math: str | None = None, deterministic: bool | None = None):
+        self.math, self.det = math, deterministic
+
+    def __enter__(self):
+        self._saved = (_State.math, _State.deterministic)
+        if self.math is not None:
+            set_math(self.math)
+        if self.det is not None and self.det != _State.deterministic:
+            set_deterministic(self.det)
+        return self
+
+    def __exit__(self, *a):
+        m, d = self._saved
+        set_math(m)
+        if d != _State.deterministic:
+            set_deterministic(d)
+
+
 def stream_ptr() -> int:
     return torch.cuda.current_stream().cuda_stream
 
@@ -90,16 +124,20 @@ def _s():
 
 
 _SCRATCH: dict = {}
+_RETIRED: list = []
 
 
 def scratch(dev, nfloats: int):
     """f32 scratch for per-block reduction partials, one buffer per (device, stream).  Consumers
     use it strictly in stream order (kernel then fold), so one buffer serves every call site of a
     stream (the weight-gradient side stream gets its own); it only grows."""
+    import os
     idx = torch.device(dev).index if torch.device(dev).index is not None else torch.cuda.current_device()
     key = (idx, torch.cuda.current_stream(idx).cuda_stream)
     buf = _SCRATCH.get(key)
     if buf is None or buf.numel() < nfloats:
+        if buf is not None and os.environ.get("KDFM_SCRATCH_RETIRE", "1") == "1":
+            _RETIRED.append(buf)
         buf = torch.empty(max(int(nfloats), 1 << 16), device=dev, dtype=torch.float32)
         _SCRATCH[key] = buf
     return buf
@@ -215,7 +253,7 @@ def gemm(A, B, Cout, M, N, K, sAm, sAk, sBk, sBn, sCm, sCn, *, amode, bmode,
         acc, lscale = mse
         d.loss_acc, d.loss_scale = ptr(acc), float(lscale)
         d.epi |= _lib.EPI_MSE
-    if d.epi == _lib.EPI_ATOMIC and d.math == _lib.KDFM_MATH_BF16:
+    if d.epi == _lib.EPI_ATOMIC and (d.math == _lib.KDFM_MATH_BF16 or (_State.deterministic and splitk > 1)):
         nws = _lib.lib().kdfm_gemm_ws(C.byref(d))
         if nws > 0:
             ws = scratch(Cout.device, nws)

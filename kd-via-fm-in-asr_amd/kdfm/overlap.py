@@ -53,6 +53,24 @@ class WgradOverlap:
         if self._pending:
             stream.wait_stream(self._stream(stream.device))
 
+    def serialized(self, on: bool = True):
+        """Context manager: with on=True every weight-gradient product runs in line on the issuing
+        stream (deterministic mode: bitwise-reproducible backward, see engine.Ver5Engine._mode)."""
+        ov = self
+
+        class _Ctx:
+            def __enter__(self):
+                self.prev = ov.enabled
+                if on:
+                    ov.join()
+                    ov.enabled = False
+                return self
+
+            def __exit__(self, *a):
+                ov.enabled = self.prev
+
+        return _Ctx()
+
     def join(self):
         """Main stream waits for all side-stream work; releases the kept operands."""
         if not self._pending:

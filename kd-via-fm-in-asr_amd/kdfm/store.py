@@ -15,6 +15,8 @@ from . import kernels as K
 from .config import fused_groups
 
 ALIGN = 4  # floats (16 bytes): every tensor starts 16-B aligned for dwordx4 loads
+# start of every parameter (fused q|k|v group: of the group) in floats; experiment knob
+GROUP_ALIGN = int(__import__("os").environ.get("KDFM_STORE_ALIGN", str(ALIGN)))
 
 
 def _numel(shape):
@@ -26,11 +28,19 @@ class FlatStore:
         self.specs = list(specs)
         self.device = torch.device(device)
         self.offsets = {}
+        inner = set()
+        names = [n for n, _ in self.specs]
+        for fname, (first, count, fshape) in fused_groups(self.specs).items():
+            i = names.index(first)
+            inner.update(names[i + 1:i + count])
         off = 0
         for name, shape in self.specs:
+            if name not in inner:
+                off = -(-off // GROUP_ALIGN) * GROUP_ALIGN
             self.offsets[name] = off
             n = _numel(shape)
             off += -(-n // ALIGN) * ALIGN
+        off = -(-off // GROUP_ALIGN) * GROUP_ALIGN
         self.numel = off
         self.data = torch.zeros(self.numel, device=self.device, dtype=torch.float32)
         self.grad = torch.zeros(self.numel, device=self.device, dtype=torch.float32) if with_grad else None

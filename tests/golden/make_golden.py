@@ -10,6 +10,8 @@ tensor so the fixture is reproducible.  Nothing from the reference is written to
 the resulting numbers (inputs, parameters, outputs, gradients) in kd_heads_ver5.npz.
 
 Usage:  python tests/golden/make_golden.py
+  -> kd_heads_ver5.npz (B=2, T'=29) and kd_heads_ver5_b1t401.npz (one benchmark-shape layer: B=1,
+     T'=401 = 16.0 s of audio after 4x subsampling)
 """
 from __future__ import annotations
 
@@ -68,7 +70,7 @@ def load_reference():
     return ns, proxy
 
 
-def main(B=2, T=29, seed=7):
+def main(B=2, T=29, seed=7, out_path=OUT, extras=True):
     ns, proxy = load_reference()
     torch.manual_seed(seed)
     Cs, Ct, L = 88, 176, 96
@@ -111,6 +113,11 @@ def main(B=2, T=29, seed=7):
     for n, g in zip(names, grads[:-1]):
         arrays["grad." + n] = g.numpy()
     # a second, independent check of the 9-step denoiser output and FM-returned x
+    if not extras:
+        arrays.update({"meta.B": np.array(B), "meta.T": np.array(T)})
+        np.savez_compressed(out_path, **arrays)
+        print("wrote", out_path, out_vals(arrays))
+        return
     with torch.no_grad():
         z = heads.sproj(s.transpose(1, 2))
         proxy.queue.append(eps)
@@ -119,9 +126,15 @@ def main(B=2, T=29, seed=7):
         fm, xo = heads.fm_latent(zd, heads.tae.enc(t.transpose(1, 2)))
     arrays.update({"out.gamma": gamma.numpy(), "out.z_deno": zd.numpy(), "out.fm_x": xo.numpy(),
                    "meta.B": np.array(B), "meta.T": np.array(T)})
-    np.savez_compressed(OUT, **arrays)
-    print("wrote", OUT, "recon", out["recon_loss"].item(), "fm", out["fm_loss_post"].item())
+    np.savez_compressed(out_path, **arrays)
+    print("wrote", out_path, out_vals(arrays))
+
+
+def out_vals(arrays):
+    return f"recon {float(arrays['out.recon']):.6f} fm {float(arrays['out.fm_post']):.6f}"
 
 
 if __name__ == "__main__":
-    sys.exit(main())
+    main()
+    main(B=1, T=401, seed=11, out_path=OUT.replace(".npz", "_b1t401.npz"), extras=False)
+    sys.exit(0)

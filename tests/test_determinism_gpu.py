@@ -1,0 +1,57 @@
+"""Deterministic-reduction mode (include/kdfm.h kdfm_set_deterministic): two runs
+of the whole ver5 step on the same inputs and seeds give BITWISE-identical hooked layer outputs and
+trainable gradients.
+
+* f32 parity configuration (PARITY: deterministic=True), 2 layers, padded batch;
+* bf16 throughput kernels with training randomness ON (dropout, SpecAugment, dither, on-device
+  NoiseAdapter eps: all counter-RNG draws, reproducible by construction), 16 layers, B=4 x 16 s so
+  the stacked heads rows (25 664) take the row-streaming / LDS-slab / wide-tile weight-gradient
+  kernels of the benchmark.
+Scalar loss accumulators (MSE / KL sums) keep float atomics and are compared to 1e-5 relative.
+"""
+from dataclasses import replace
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(cfg, wav, wl, tg, tl, eps):
+    from kdfm.engine import Ver5Engine
+    eng = Ver5Engine(cfg, "cuda", teacher_seed=0, student_seed=1, heads_seed=2)
+    eng.set_seed(77)
+    eng.advance_rng()
+    ctx = eng.forward(wav, wl, tg, tl, train=True, eps=eps)
+    feats = ctx["sfeats"].clone()
+    eng.backward(ctx)
+    torch.cuda.synchronize()
+    return eng.losses.clone(), feats, eng.student.grads()
+
+
+@pytest.mark.parametrize("which", ["f32-parity", "bf16-train"])
+def test_step_is_bitwise_reproducible(which):
+    from kdfm.config import DEFAULT, PARITY
+    g = torch.Generator().manual_seed(21)
+    if which == "f32-parity":
+        cfg = replace(PARITY, n_layers=2)
+        B, N, lens = 2, 24000, [24000, 17001]
+        U = 11
+    else:
+        cfg = replace(DEFAULT, n_layers=16, deterministic=True)
+        B, N, lens = 4, 256000, [256000, 256000, 230000, 256000]
+        U = 60
+    wav = (0.1 * torch.randn(B, N, generator=g)).cuda()
+    wl = torch.tensor(lens, dtype=torch.int64).cuda()
+    tg = torch.randint(0, cfg.vocab, (B, U), generator=g).cuda()
+    tl = torch.full((B,), U, dtype=torch.int64).cuda()
+    T = ((N // cfg.hop) // 2) // 2 + 1
+    eps = torch.randn(cfg.n_layers * B * T, cfg.latent, generator=g).cuda() if which == "f32-parity" else None
+    l1, f1, g1 = _run(cfg, wav, wl, tg, tl, eps)
+    l2, f2, g2 = _run(cfg, wav, wl, tg, tl, eps)
+    assert all(torch.isfinite(v).all() for v in g1.values())
+    assert torch.equal(f1, f2), "hooked layer outputs differ between runs"
+    bad = [k for k in g1 if not torch.equal(g1[k], g2[k])]
+    detail = [(k, f"{(g1[k] - g2[k]).abs().max().item():.3e}/{g1[k].abs().max().item():.3e}") for k in bad]
+    assert not bad, f"{len(bad)} of {len(g1)} gradient tensors differ between runs: {detail}"
+    torch.testing.assert_close(l1, l2, rtol=1e-5, atol=0.0)

@@ -18,6 +18,7 @@ def _models(n_layers):
     from kdfm import kernels as K
     from kdfm.distill import DistilFlowMatchingCTCModelBPE, EncDecCTCModelBPE
     K.set_math("f32")
+    K.set_deterministic(True)   # ordered reductions (restored by the conftest fixture)
     kw = dict(n_layers=n_layers, dither=0.0, spec_augment=False, dropout=0.0, dropout_pre_encoder=0.0,
               dropout_att=0.0)
     teacher = EncDecCTCModelBPE(d_model=176, n_heads=4, device="cuda", init_seed=0, **kw)

@@ -1,0 +1,77 @@
+"""kdfm_adamw_noam (csrc/optim.hip) against torch.optim.AdamW driven by the NoamAnnealing schedule
+the reference gets from the teacher's .nemo optim config (NeMo/nemo/core/optim/lr_scheduler.py:
+473-530, restated below line for line; ModelPT.setup_optimization modelPT.py:650-897), stepped as
+Lightning steps an interval='step' scheduler: scheduler.step() after every optimizer.step(), so
+optimizer step k runs at schedule step max(1, k-1).
+
+Crosses warmup (warmup_steps=3, 7 steps), hits the min_lr clamp after warmup, uses weight decay and
+grad_scale = 1/world (DDP mean of summed gradients).  Tolerance: fp32 elementwise, params and both
+moments rtol 1e-5 / atol 1e-6 (torch updates exp_avg with lerp, the kernel with b1*m + (1-b1)*g: one
+ulp apart near zero); the reported lr rtol 1e-6.
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+class NoamAnnealing(torch.optim.lr_scheduler.LRScheduler):
+    """lr_scheduler.py:473-530 (warmup_steps given; max_steps unused by this policy)."""
+
+    def __init__(self, optimizer, *, d_model, warmup_steps, min_lr=0.0, last_epoch=-1):
+        self._normalize = d_model ** (-0.5)
+        self.warmup_steps = warmup_steps
+        self.min_lr = min_lr
+        super().__init__(optimizer, last_epoch)
+
+    def get_lr(self):
+        step = max(1, self.last_epoch)
+        return [self._noam_annealing(lr, step) for lr in self.base_lrs]
+
+    def _noam_annealing(self, initial_lr, step):
+        if self.warmup_steps > 0:
+            mult = self._normalize * min(step ** (-0.5), step * (self.warmup_steps ** (-1.5)))
+        else:
+            mult = self._normalize * step ** (-0.5)
+        out_lr = initial_lr * mult
+        if step > self.warmup_steps:
+            out_lr = max(out_lr, self.min_lr)
+        return out_lr
+
+
+@pytest.mark.parametrize("grad_scale,min_lr", [(1.0, 1e-6), (0.5, 0.25)])
+def test_adamw_noam_matches_torch(grad_scale, min_lr):
+    from kdfm import kernels as K
+    n = 50_000
+    g = torch.Generator().manual_seed(0)
+    p0 = torch.randn(n, generator=g)
+    base_lr, d_model, warmup = 5.0, 88.0, 3
+    betas, eps, wd = (0.9, 0.98), 1e-8, 1e-3
+    ref = p0.clone().requires_grad_(True)
+    opt = torch.optim.AdamW([ref], lr=base_lr, betas=betas, eps=eps, weight_decay=wd)
+    sched = NoamAnnealing(opt, d_model=d_model, warmup_steps=warmup, min_lr=min_lr)
+
+    dev = torch.device("cuda")
+    p = p0.clone().to(dev)
+    m = torch.zeros(n, device=dev)
+    v = torch.zeros(n, device=dev)
+    step = torch.zeros(1, dtype=torch.int64, device=dev)
+    lr_out = torch.zeros(1, device=dev)
+    for k in range(1, 8):
+        grad = torch.randn(n, generator=g)
+        # reference: DDP hands AdamW the mean gradient = grad_scale * summed gradient
+        ref.grad = grad * grad_scale
+        lr_ref = opt.param_groups[0]["lr"]
+        opt.step()
+        sched.step()
+        K.step_advance(step, None)
+        K.adamw_noam(p, grad.to(dev), m, v, step, base_lr, d_model, warmup, min_lr, betas[0], betas[1], eps, wd,
+                     grad_scale, lr_out)
+        torch.cuda.synchronize()
+        assert abs(lr_out.item() - lr_ref) <= 1e-6 * lr_ref, (k, lr_out.item(), lr_ref)
+        st = opt.state[ref]
+        torch.testing.assert_close(m.cpu(), st["exp_avg"], rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(v.cpu(), st["exp_avg_sq"], rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(p.cpu(), ref.detach(), rtol=1e-5, atol=1e-6)
+    if min_lr > 0.1:   # the clamp engaged after warmup
+        assert lr_out.item() == pytest.approx(min_lr, rel=1e-6)
