@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -32,25 +33,31 @@ FFN_FLOPS_NOTE = "ffn_up GEMMs: 2*M*N*K per launch (M=B*T' rows, N=4d, K=d)"
 MI355X_BF16_DENSE_TFLOPS = 2500.0   # /opt/skills/guides/MI355X_MICROARCH.md chip table (dense)
 MI355X_F32_MFMA_TFLOPS = 157.3
 MI355X_HBM_GBPS = 8000.0            # MI355X_MICROARCH.md §HBM (8 TB/s spec peak)
-# PMC traffic of the roofline kernel (tools/pmc_traffic.sh -> tools/pmc_summary.py, 2 separate --pmc
-# passes, FETCH_SIZE doubled per the gfx950 correction); committed under profiles/
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r01_s10_pmc_traffic.json")
-ROOF_KERNEL = "kdfm::skc_fwd_kernel<3>"
+# PMC traffic per kernel (tools/pmc_traffic.sh -> tools/pmc_summary.py: separate --pmc FETCH_SIZE and
+# WRITE_SIZE passes, FETCH_SIZE doubled per the gfx950 correction), committed under profiles/
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r02_pmc_traffic.json")
+# kdfm_gemm kernel family (kernels.ROUTES) -> kernel-name stems in the rocprofv3 / PMC summaries
+ROUTE_KERNELS = {"generic": ("gemm_kernel",), "skinny": ("sk_fwd_kernel", "skd_fwd_kernel"),
+                 "rowstream_fwd": ("rs_fwd_kernel",), "wide_wgrad": ("rs_wgrad_kernel", "rs_fold_kernel"),
+                 "split_fold": ("gemm_kernel", "rs_fold_kernel"), "slab_conv": ("skc_fwd_kernel",),
+                 "wgrad_rows": ("wgr_kernel", "wgr_fold_kernel")}
+# FLOPs per utterance of one training step (B=32, 16.0 s) and of its attention +
+# FFN dense contractions (student fwd+bwd + teacher fwd), the north-star MFMA roofline subject
+STEP_GFLOP_PER_UTT = 62.6
+ATTN_FFN_GFLOP_PER_UTT = 23.0
 
 
-def pmc_traffic(kernel: str):
-    """HBM bytes per launch of `kernel` from the committed PMC summary; template instantiations of
-    the same kernel (e.g. the compile-time epilogue variants skc_fwd_kernel<3, E>) are pooled,
-    launch-weighted, since the bench's timing tag covers all of them."""
+def pmc_traffic(stems):
+    """HBM bytes per launch pooled over the kernels whose names start with one of `stems` (the
+    launches of one kdfm_gemm kernel family) from the committed PMC summary; None if absent."""
     try:
         with open(PMC_TRAFFIC) as fh:
             rows = json.load(fh)
     except (OSError, ValueError):
         return None
-    stem = kernel[:-1] if kernel.endswith(">") else kernel
-    hit = [r for r in rows if r["kernel"] == kernel or r["kernel"].startswith(stem + ",")]
+    hit = [r for r in rows if any(r["kernel"].split(" ")[0].split("<")[0].endswith(st) for st in stems)]
     n = sum(r["launches"] for r in hit)
-    return sum(r["bytes_total"] for r in hit) / n if n else None
+    return round(sum(r["bytes_total"] for r in hit) / n, 1) if n else None
 
 
 def parse():
@@ -62,16 +69,21 @@ def parse():
     ap.add_argument("--samples", type=int, default=N_SAMPLES)
     ap.add_argument("--math", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=16,
+                    help="host threads for the CPU baseline (the GPU box gives one GPU 16 host CPUs)")
     ap.add_argument("--graph", action="store_true",
                     help="replay the step as one captured HIP graph (measured slower: hipGraph replay ran the "
                          "teacher / weight-gradient / CTC streams serially, 43.9 vs 40.1 ms/step eager)")
     return ap.parse_args()
 
 
-def cpu_baseline(threads: int, samples: int):
-    """Oracle (pure-PyTorch CPU restatement of the same step, fp32) on a bounded sample:
-    B=2 utterances of the same 16 s shape, 1 warm-up + 2 timed steps (forward + backward)."""
+def cpu_baseline(threads: int, samples: int, batches=(2, 32), steps: int = 5):
+    """Oracle (pure-PyTorch CPU restatement of the same step, fp32: frontend x2, teacher + student
+    encoders, decoders, CTC, logit KD, ver5 heads, autograd backward) on the host cores, per
+    BASELINE.md: B=2 (config 1) and B=32 (the bench batch) utterances of the same 16 s shape,
+    1 warm-up + `steps` timed forward+backward steps each, median.  `value` is the B=32 rate."""
+    import platform
+    import statistics
     from oracle import ver5 as O
     torch.set_num_threads(threads)
     ocfg = O.StepConfig()
@@ -79,25 +91,37 @@ def cpu_baseline(threads: int, samples: int):
     names = O.trainable_names(p)
     for k in names:
         p[k].requires_grad_(True)
-    Bc = 2
-    g = torch.Generator().manual_seed(1234)
-    wav = 0.1 * torch.randn(Bc, samples, generator=g)
-    wl = torch.full((Bc,), samples, dtype=torch.int64)
-    tg = torch.randint(0, ocfg.vocab, (Bc, U_TOKENS), generator=g)
-    tl = torch.full((Bc,), U_TOKENS, dtype=torch.int64)
     T = ((samples // ocfg.hop) // 2) // 2 + 1
-    eps = torch.randn(ocfg.n_layers, Bc, ocfg.latent, T, generator=g)
-    times = []
-    for i in range(3):
-        t0 = time.perf_counter()
-        out = O.ver5_step(p, wav, wl, tg, tl, ocfg, eps)
-        torch.autograd.grad(out["loss"], [p[k] for k in names], allow_unused=True)
-        times.append(time.perf_counter() - t0)
-    per_step = sum(times[1:]) / len(times[1:])
-    return {"value": round(Bc / per_step, 4), "unit": "utterances/sec", "cores": threads, "kind": "port",
-            "sample": f"oracle/ver5.py fp32 forward+backward, B={Bc} x {samples / 16000:.1f} s utterances, "
-                      f"mean of {len(times) - 1} steps after 1 warm-up ({per_step:.2f} s/step), "
-                      f"torch.set_num_threads({threads})"}
+    res = {}
+    for Bc in batches:
+        g = torch.Generator().manual_seed(1234)
+        wav = 0.1 * torch.randn(Bc, samples, generator=g)
+        wl = torch.full((Bc,), samples, dtype=torch.int64)
+        tg = torch.randint(0, ocfg.vocab, (Bc, U_TOKENS), generator=g)
+        tl = torch.full((Bc,), U_TOKENS, dtype=torch.int64)
+        eps = torch.randn(ocfg.n_layers, Bc, ocfg.latent, T, generator=g)
+        times = []
+        for i in range(steps + 1):
+            t0 = time.perf_counter()
+            out = O.ver5_step(p, wav, wl, tg, tl, ocfg, eps)
+            torch.autograd.grad(out["loss"], [p[k] for k in names], allow_unused=True)
+            times.append(time.perf_counter() - t0)
+            del out
+        med = statistics.median(times[1:])
+        res[Bc] = {"utt_per_s": round(Bc / med, 4), "s_per_step_median": round(med, 3),
+                   "s_per_step": [round(t, 3) for t in times[1:]]}
+    cpu = "unknown"
+    try:
+        with open("/proc/cpuinfo") as fh:
+            cpu = next((ln.split(":", 1)[1].strip() for ln in fh if ln.startswith("model name")), cpu)
+    except OSError:
+        cpu = platform.processor() or cpu
+    big = max(batches)
+    return {"value": res[big]["utt_per_s"], "unit": "utterances/sec", "cores": threads, "kind": "port",
+            "cpu_model": cpu, "host_cpus": os.cpu_count(), "by_batch": {str(b): v for b, v in res.items()},
+            "sample": f"oracle/ver5.py fp32 forward+backward of the same step, B={list(batches)} x "
+                      f"{samples / 16000:.1f} s utterances, median of {steps} steps after 1 warm-up, "
+                      f"torch.set_num_threads({threads}); value = B={big}"}
 
 
 def main():
@@ -156,31 +180,61 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = max_over_ranks(time.perf_counter() - t0, dev)
-    # dominant-kernel timing: one instrumented eager step right after the timed replays, every
-    # ffn_up launch bracketed by HIP events on the stream it runs on (main or teacher stream)
-    trace = K.Trace(["ffn_up", "deno_conv"])
+    # live per-kernel timing: one instrumented eager step right after the timed steps; every
+    # kdfm_gemm launch (keyed by the kernel family libkdfm routed it to), the frontend and the
+    # depthwise convs bracketed by HIP events on the stream they run on
+    trace = K.Trace(["*", "ffn_up", "frontend", "dwconv"])
     with trace:
         eng.train_step(wav, wl, tg, tl, ar)
     torch.cuda.synchronize()
     losses = eng.losses.detach().cpu().tolist()
+    if not all(math.isfinite(x) for x in losses):
+        raise RuntimeError(f"non-finite losses after the timed steps: {losses}")
     tsum = trace.summary()
     empty = {"launches": 0, "ms_total": 0.0, "flops_total": 0.0, "bytes_total": 0.0}
-    summ = tsum.get("ffn_up", empty)
-    deno = tsum.get("deno_conv", empty)
     if rank == 0:
         utt = world * args.batch * args.steps / elapsed
-        n_l = max(1, summ["launches"])
-        avg_ms = summ["ms_total"] / n_l
-        flops_per_launch = summ["flops_total"] / n_l
-        achieved = flops_per_launch / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
-        peak = MI355X_BF16_DENSE_TFLOPS if cfg.math == "bf16" else MI355X_F32_MFMA_TFLOPS
-        # roofline subject: the dominant kernel of the step (rocprof: the denoiser k=3 conv products,
-        # kdfm_gemm skinny CONV mode) - HBM-bound (72 flop/B at f32 storage << the bf16 ridge)
-        d_l = max(1, deno["launches"])
-        d_ms = deno["ms_total"] / d_l
-        d_bytes = deno["bytes_total"] / d_l
-        d_gbps = d_bytes / (d_ms * 1e-3) / 1e9 if d_ms > 0 else 0.0
-        d_traffic = pmc_traffic(ROOF_KERNEL)
+        utt_gpu = utt / world
+        bf16_peak = MI355X_BF16_DENSE_TFLOPS if cfg.math == "bf16" else MI355X_F32_MFMA_TFLOPS
+
+        def rate(t):
+            n = max(1, t["launches"])
+            ms = t["ms_total"] / n
+            gbps = (t["bytes_total"] / n) / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+            tfl = (t["flops_total"] / n) / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
+            return n, ms, gbps, tfl
+
+        routes = {k[5:]: v for k, v in tsum.items() if k.startswith("gemm:")}
+        by_route = {}
+        for r, t in sorted(routes.items(), key=lambda kv: -kv[1]["ms_total"]):
+            n, ms, gbps, tfl = rate(t)
+            by_route[r] = {"launches": n, "ms_per_step": round(t["ms_total"], 3), "avg_ms": round(ms, 5),
+                           "GB_per_s": round(gbps, 1), "TFLOP_per_s": round(tfl, 2),
+                           "bytes_per_launch": round(t["bytes_total"] / n, 1),
+                           "flops_per_launch": round(t["flops_total"] / n, 1)}
+        dom = next(iter(by_route)) if by_route else "generic"
+        dt = routes.get(dom, empty)
+        n, ms, gbps, tfl = rate(dt)
+        intensity = dt["flops_total"] / max(1.0, dt["bytes_total"])
+        ridge = bf16_peak * 1e12 / (MI355X_HBM_GBPS * 1e9)
+        if intensity < ridge:
+            roof = {"bound": "hbm", "achieved": round(gbps, 1), "peak": MI355X_HBM_GBPS, "unit": "GB/s",
+                    "frac": round(gbps / MI355X_HBM_GBPS, 4)}
+        else:
+            roof = {"bound": "mfma", "achieved": round(tfl, 2), "peak": bf16_peak, "unit": "TFLOP/s",
+                    "frac": round(tfl / bf16_peak, 4)}
+        roof.update({"traffic": pmc_traffic(ROUTE_KERNELS.get(dom, (dom,))),
+                     "traffic_source": os.path.relpath(PMC_TRAFFIC, ROOT) + " (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, "
+                                       "pooled over the family's kernels, bytes per launch)",
+                     "kernel": f"kdfm_gemm {dom} family ({', '.join(ROUTE_KERNELS.get(dom, (dom,)))}): the kernel "
+                               f"family with the largest aggregated time of the step",
+                     "launches": n, "avg_ms": round(ms, 5), "bytes_per_launch": round(dt["bytes_total"] / n, 1),
+                     "flops_per_launch": round(dt["flops_total"] / n, 1),
+                     "arith_intensity_flop_per_byte": round(intensity, 2)})
+        f_n, f_ms, f_gbps, _ = rate(tsum.get("ffn_up", empty))
+        f_tfl = rate(tsum.get("ffn_up", empty))[3]
+        fe = rate(tsum.get("frontend", empty))
+        dw = rate(tsum.get("dwconv", empty))
         cpu = None
         if not args.no_cpu_baseline:
             cpu = cpu_baseline(args.cpu_threads, args.samples)
@@ -201,17 +255,22 @@ def main():
                                    "(d88 h2 L16), BASELINE.json configs[1] shape",
                        "global_batch": world * args.batch, "seq_len": args.samples,
                        "frames_subsampled": (args.samples // 160) // 4 + 1, "parallelism": f"dp{world}"},
-            "roofline": {"bound": "hbm",
-                         "kernel": "kdfm_gemm CONV (denoiser Conv1d k=3 over 16 stacked layers, 205312 x 96 x 288, "
-                                   "LDS-slab skc_fwd_kernel<3>)",
-                         "achieved": round(d_gbps, 1), "peak": MI355X_HBM_GBPS, "unit": "GB/s",
-                         "frac": round(d_gbps / MI355X_HBM_GBPS, 4), "traffic": d_traffic,
-                         "traffic_source": "profiles/r01_s10_pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE)",
-                         "launches": deno["launches"], "avg_ms": round(d_ms, 5), "bytes_per_launch": d_bytes},
+            "roofline": roof,
+            "roofline_by_gemm_family": by_route,
             "roofline_mfma_ffn": {"bound": "mfma", "kernel": "kdfm_gemm ffn_up (Conformer FFN d->4d, SiLU+dropout)",
-                                  "achieved": round(achieved, 3), "peak": peak, "unit": "TFLOP/s",
-                                  "frac": round(achieved / peak, 5), "launches": summ["launches"],
-                                  "avg_ms": round(avg_ms, 5), "flops_per_launch": flops_per_launch},
+                                  "achieved": round(f_tfl, 3), "peak": bf16_peak, "unit": "TFLOP/s",
+                                  "frac": round(f_tfl / bf16_peak, 5), "launches": f_n, "avg_ms": round(f_ms, 5)},
+            "attn_ffn_mfma_frac": {"value": round(ATTN_FFN_GFLOP_PER_UTT * 1e9 * utt_gpu / (bf16_peak * 1e12), 5),
+                                   "formula": "23.0 GFLOP/utt (SURVEY §8(d)) x utt/s per GPU / dense bf16 peak"},
+            "whole_step": {"tflops": round(STEP_GFLOP_PER_UTT * 1e9 * utt_gpu / 1e12, 2),
+                           "frac_bf16_peak": round(STEP_GFLOP_PER_UTT * 1e9 * utt_gpu / (bf16_peak * 1e12), 5),
+                           "formula": "62.6 GFLOP/utt (SURVEY §8(d)) x utt/s per GPU"},
+            "mel_frontend_hbm": {"achieved": round(fe[2], 1), "unit": "GB/s", "peak": MI355X_HBM_GBPS,
+                                 "frac": round(fe[2] / MI355X_HBM_GBPS, 4), "launches": fe[0], "avg_ms": round(fe[1], 5),
+                                 "bytes": "4 B x (N samples + T x 80 mel) per utterance (1.54 MB at 16 s)"},
+            "dwconv_hbm": {"achieved": round(dw[2], 1), "unit": "GB/s", "peak": MI355X_HBM_GBPS,
+                           "frac": round(dw[2] / MI355X_HBM_GBPS, 4), "launches": dw[0], "avg_ms": round(dw[1], 5),
+                           "bytes": "read g + write y, 4 B x rows x d per launch"},
             "cpu_baseline": cpu,
             "losses_last_step": [round(x, 5) for x in losses],
         }

@@ -140,6 +140,10 @@ int kdfm_cast_bf16(const float* src, uint16_t* dst, int64_t n, void* stream);
 int kdfm_cast_bf16_t(const float* src, uint16_t* dst, const int64_t* table, int64_t ntab, int64_t nblocks,
                      void* stream);
 int64_t kdfm_gemm_ws(const kdfm_gemm_desc* d); /* workspace elements kdfm_gemm would use (0: none) */
+/* kernel family the calling thread's most recent kdfm_gemm launched (profiling attribution):
+ * 0 generic 64x64 MFMA tile, 1 weight-stationary skinny, 2 row-streaming forward, 3 wide-tile
+ * weight gradient + fold, 4 generic tile with ordered split-K fold, 5 LDS-slab k=3 conv; -1 none */
+int32_t kdfm_gemm_last_route(void);
 
 /* column sums: out[n] (+)= scale * sum_m X[m*ld + n], m < M; accumulate != 0 adds into out.
  * (bias gradients of every Linear / Conv1d on the path) */

@@ -19,6 +19,12 @@ int check_launch(const char* what);
 // or a gradient runs in a fixed order (no split-K / cross-block float atomics), so two runs on the
 // same inputs give bitwise-identical results.  Read on the host when a launch is configured.
 bool deterministic();
+// Kernel family the most recent kdfm_gemm call on this thread launched (kdfm_gemm_last_route):
+// 0 generic 64x64 tile, 1 weight-stationary skinny, 2 row-streaming forward, 3 wide-tile weight
+// gradient (+ fold), 4 generic with ordered split-K fold, 5 LDS-slab k=3 conv.
+enum { ROUTE_GENERIC = 0, ROUTE_SKINNY = 1, ROUTE_RS_FWD = 2, ROUTE_RS_WGRAD = 3, ROUTE_SPLIT_FOLD = 4,
+       ROUTE_SLAB_CONV = 5 };
+void set_route(int r);
 
 #define KDFM_REQUIRE(cond, msg)                                  \
   do {                                                           \

@@ -468,6 +468,7 @@ extern "C" int kdfm_gemm(const kdfm_gemm_desc* d, void* stream) {
     if (p.splitk > 1 && d->batch1 * d->batch2 == 1 && d->ws && d->ws_len >= need &&
         !(d->math == KDFM_MATH_BF16 && rowstream_wgrad_ws(p, d->amode, d->bmode, 1) > 0)) {
       p.partial = 1;
+      set_route(ROUTE_SPLIT_FOLD);
       dim3 grid((unsigned)ceil_div(d->M, BM), (unsigned)ceil_div(d->N, BN), (unsigned)p.splitk);
       const int rc = d->math == KDFM_MATH_BF16 ? launch<true>(p, d->amode, d->bmode, grid, st)
                                                : launch<false>(p, d->amode, d->bmode, grid, st);
@@ -479,12 +480,14 @@ extern "C" int kdfm_gemm(const kdfm_gemm_desc* d, void* stream) {
   if (d->math == KDFM_MATH_BF16 && d->K > 0) {
     const int64_t batch = d->batch1 * d->batch2;
     int rc = try_rowstream_wgrad(p, d->amode, d->bmode, batch, st);
-    if (rc >= 0) return rc;
+    if (rc >= 0) return set_route(ROUTE_RS_WGRAD), rc;
+    set_route(ROUTE_SKINNY);  // try_skinny_fwd marks its LDS-slab conv instance itself
     rc = try_skinny_fwd(p, d->amode, d->bmode, batch, st);
     if (rc >= 0) return rc;
     rc = try_rowstream_fwd(p, d->amode, d->bmode, batch, st);
-    if (rc >= 0) return rc;
+    if (rc >= 0) return set_route(ROUTE_RS_FWD), rc;
   }
+  set_route(ROUTE_GENERIC);
   const int64_t gx = ceil_div(d->M, BM), gy = ceil_div(d->N, BN), gz = d->batch1 * d->batch2 * p.splitk;
   KDFM_REQUIRE(gx < (1ll << 31) && gy < 65536 && gz < 65536, "grid too large");
   dim3 grid((unsigned)gx, (unsigned)gy, (unsigned)gz);

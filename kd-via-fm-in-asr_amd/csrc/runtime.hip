@@ -8,9 +8,11 @@ namespace kdfm {
 
 static thread_local std::string g_last_error;
 static int g_deterministic = 0;
+static thread_local int g_route = -1;
 
 void set_error(const std::string& msg) { g_last_error = msg; }
 bool deterministic() { return g_deterministic != 0; }
+void set_route(int r) { g_route = r; }
 
 int check_launch(const char* what) {
   hipError_t e = hipGetLastError();
@@ -78,6 +80,8 @@ const char* kdfm_last_error(void) { return kdfm::g_last_error.c_str(); }
 void kdfm_set_deterministic(int32_t on) { kdfm::g_deterministic = on ? 1 : 0; }
 
 int32_t kdfm_get_deterministic(void) { return kdfm::g_deterministic; }
+
+int32_t kdfm_gemm_last_route(void) { return kdfm::g_route; }
 
 int kdfm_device_arch(char* buf, int64_t len) {
   KDFM_REQUIRE(buf && len > 0, "null buffer");

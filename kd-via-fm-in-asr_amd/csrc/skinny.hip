@@ -666,6 +666,7 @@ int skc_launch(const GemmP& p, const SkGeo& g, int64_t gx, size_t lds, hipStream
     return true;
   }();
   (void)once;
+  set_route(ROUTE_SLAB_CONV);
   hipLaunchKernelGGL((skc_fwd_kernel<NCT, EMODE>), dim3((unsigned)gx), dim3(64 * SKC_WV), lds, st, p, g);
   return check_launch("kdfm_gemm(skinny conv slab)");
 }

@@ -10,8 +10,9 @@
   teacher `stt_en_conformer_ctc_small` arrives this way (asr_train_diffm.py:91-102); its
   `encoder.*` / `decoder.*` / `preprocessor.*` keys map to the engine's `teacher.*` store.
 
-Every file is read with loaders that execute nothing: torch.load(weights_only=True) and
-yaml.safe_load.  Optimizer moments are kept in the engine's own flat layout under
+Every file is read with loaders that execute nothing: torch.load(weights_only=True) (classes the
+weights-only allowlist rejects, e.g. the OmegaConf DictConfig NeMo stores as hyper_parameters, are
+replaced by inert stand-ins for that load) and yaml.safe_load.  Optimizer moments are kept in the engine's own flat layout under
 `optimizer_states[0]["kdfm_flat"]` (Lightning's per-parameter index depends on NeMo's module
 registration order, which does not exist here); resume restores them bit-exactly.
 """
@@ -41,14 +42,21 @@ def engine_state_dict(eng, *, teacher: bool = True, frontend: bool = True) -> "O
     if frontend:
         sd["preprocessor.featurizer.window"] = eng.fe.window.detach().cpu().clone()
         sd["preprocessor.featurizer.fb"] = _fb_nemo(eng.fe.fb)
+    # the student's BatchNorm layers saw one batch-statistics update per optimizer step; the frozen
+    # teacher's counters are whatever was loaded (its BN runs on running statistics and never counts)
     nbt = torch.tensor(int(eng.step.item()), dtype=torch.int64)
+    loaded_nbt = getattr(eng, "bn_batches_tracked", {})
     for name, _ in eng.student.specs:
         sd[name] = eng.student.P[name].detach().cpu().clone()
     for name, _ in eng.bn.specs:
         if teacher or not name.startswith("teacher."):
             sd[name] = eng.bn.P[name].detach().cpu().clone()
             if name.endswith("running_var"):
-                sd[name[:-len("running_var")] + "num_batches_tracked"] = nbt.clone()
+                key = name[:-len("running_var")] + "num_batches_tracked"
+                if name.startswith("teacher."):
+                    sd[key] = loaded_nbt.get(key, torch.tensor(0, dtype=torch.int64)).clone()
+                else:
+                    sd[key] = nbt.clone()
     if teacher:
         if frontend:
             sd["teacher.preprocessor.featurizer.window"] = eng.fe.window.detach().cpu().clone()
@@ -84,6 +92,10 @@ def load_engine_state(eng, sd: dict, *, strict: bool = False, fb_atol: float = 1
                 if ref.shape != mine.shape or (ref - mine.detach().cpu()).abs().max().item() > fb_atol:
                     fe_bad.append(k)
             elif k.endswith(_IGNORED_SUFFIXES) or k.startswith("fm_latent_2."):
+                if k.startswith("teacher.") and k.endswith("num_batches_tracked"):
+                    if not hasattr(eng, "bn_batches_tracked"):
+                        eng.bn_batches_tracked = {}
+                    eng.bn_batches_tracked[k] = v.detach().to("cpu", torch.int64).reshape(())
                 continue
             else:
                 unexpected.append(k)
@@ -98,8 +110,50 @@ def load_engine_state(eng, sd: dict, *, strict: bool = False, fb_atol: float = 1
 
 # ---- Lightning .ckpt ------------------------------------------------------------------------------
 
+class InertGlobal:
+    """Stand-in for a class the checkpoint names but torch's weights-only unpickler does not allow
+    (NeMo's ModelPT.save_hyperparameters stores an OmegaConf DictConfig under 'hyper_parameters').
+    It records its construction arguments and pickled state and runs nothing."""
+
+    def __init__(self, *args, **kwargs):
+        self._args, self._kwargs = args, kwargs
+
+    def __setstate__(self, state):
+        self.__dict__["_state"] = state
+
+    def __repr__(self):
+        return f"<inert {type(self).__module__}.{type(self).__qualname__}>"
+
+
+def _inert(module: str, name: str):
+    cls = type(name, (InertGlobal,), {"__module__": module})
+    cls.__qualname__ = name
+    return cls
+
+
+def _load_weights_only(src, *, max_globals: int = 64):
+    """torch.load(weights_only=True) that tolerates classes outside the allowlist: each global the
+    weights-only unpickler rejects is re-declared as an InertGlobal subclass of the same qualified
+    name and allowlisted for this load only, so the file still executes nothing."""
+    import pickle
+    import re
+    extra = []
+    data = src if isinstance(src, (bytes, bytearray)) else None
+    for _ in range(max_globals):
+        try:
+            with torch.serialization.safe_globals(extra):
+                return torch.load(io.BytesIO(data) if data is not None else src, map_location="cpu",
+                                  weights_only=True)
+        except pickle.UnpicklingError as e:
+            m = re.search(r"GLOBAL ([\w.]+)\.(\w+) was not an allowed global", str(e))
+            if m is None:
+                raise
+            extra.append(_inert(m.group(1), m.group(2)))
+    raise ValueError(f"checkpoint names more than {max_globals} classes outside the weights-only allowlist")
+
+
 def read_lightning_ckpt(path: str) -> dict:
-    ck = torch.load(path, map_location="cpu", weights_only=True)
+    ck = _load_weights_only(path)
     if not isinstance(ck, dict) or "state_dict" not in ck:
         raise ValueError(f"{path}: not a Lightning checkpoint (no 'state_dict')")
     return ck
@@ -143,6 +197,14 @@ def restore_lightning_ckpt(eng, path: str, *, optimizer: bool = True, strict: bo
             eng.student.exp_avg_sq.copy_(opt["exp_avg_sq"].to(eng.student.exp_avg_sq.device))
             eng.step.fill_(int(opt["step"]))
         info["resumed_optimizer"] = True
+    elif optimizer and "global_step" in ck:
+        # a reference (Lightning/NeMo) checkpoint: its AdamW moments are keyed by NeMo's module
+        # registration order and are not restored, but the Noam schedule resumes at its step
+        import warnings
+        warnings.warn(f"{path}: no kdfm flat optimizer state; AdamW moments restart from zero, "
+                      f"the schedule resumes at global_step {int(ck['global_step'])}")
+        with torch.no_grad():
+            eng.step.fill_(int(ck["global_step"]))
     info["epoch"] = int(ck.get("epoch", 0))
     info["global_step"] = int(ck.get("global_step", 0))
     return info
@@ -165,7 +227,7 @@ def read_nemo(path: str):
     if raw_w is None:
         raise ValueError(f"{path}: no model_weights.ckpt in the archive")
     cfg = yaml.safe_load(raw_cfg.decode()) if raw_cfg is not None else {}
-    sd = torch.load(io.BytesIO(raw_w), map_location="cpu", weights_only=True)
+    sd = _load_weights_only(raw_w)
     if isinstance(sd, dict) and "state_dict" in sd and not any(k.startswith("encoder.") for k in sd):
         sd = sd["state_dict"]
     return cfg, sd

@@ -221,8 +221,9 @@ def layer_forward(cfg, S: EncoderShapes, P, L, li, x, out, pos_emb, lengths, *, 
     K.glu_mask_fwd(a, lengths, g, B, T, d)
     y = _empty(rows, d, dev=dev)
     stats = torch.zeros(2 * d, device=dev, dtype=torch.float64) if rm_batch else None
-    K.dwconv_fwd(g, P[L + "conv.depthwise_conv.weight"].view(d, -1), P[L + "conv.depthwise_conv.bias"], y, stats,
-                 B, T, d, cfg.conv_kernel)
+    with K.span("dwconv", nbytes=4.0 * 2 * rows * d):   # read g + write y (f32), SURVEY.md §8(d)
+        K.dwconv_fwd(g, P[L + "conv.depthwise_conv.weight"].view(d, -1), P[L + "conv.depthwise_conv.bias"], y, stats,
+                     B, T, d, cfg.conv_kernel)
     bmean = _empty(d, dev=dev)
     brstd = _empty(d, dev=dev)
     rmn, rvr = bn_update if bn_update is not None else (None, None)

@@ -89,6 +89,14 @@ def frontend_forward(cfg: Ver5Config, consts: FrontendConsts, wav: torch.Tensor,
     if not wav.is_cuda:
         raise _lib.KdfmError("frontend_forward needs a device tensor")
     B, N = wav.shape
+    T = mel_frames(cfg, N)
+    # algorithmic HBM bytes: read the f32 waveform, write the f32 log-mel
+    with K.span("frontend", nbytes=4.0 * B * (N + T * cfg.nfilt)):
+        return _frontend(cfg, consts, wav, wav_len, mel_len, dither, seed, rng_stream, out)
+
+
+def _frontend(cfg, consts, wav, wav_len, mel_len, dither, seed, rng_stream, out):
+    B, N = wav.shape
     pad = cfg.n_fft // 2
     T = mel_frames(cfg, N)
     F = cfg.n_fft // 2 + 1

@@ -22,9 +22,15 @@ class _State:
     deterministic = False
 
 
+ROUTES = {0: "generic", 1: "skinny", 2: "rowstream_fwd", 3: "wide_wgrad", 4: "split_fold", 5: "slab_conv",
+          6: "wgrad_rows"}
+
+
 class Trace:
-    """Brackets every GEMM launch carrying one of `tags` with HIP events on the launch stream
-    (bench.py's live per-kernel timing of the dominant kernel)."""
+    """Brackets launches with HIP events on the launch stream (bench.py's live per-kernel timing):
+    every GEMM launch carrying one of `tags` (tag "*" = every kdfm_gemm call; those are also keyed
+    by the kernel family libkdfm routed them to, kdfm_gemm_last_route), and every `span(tag)` block.
+    Each record carries the algorithmic FLOPs and HBM bytes of the launch."""
     active = None
 
     def __init__(self, tags):
@@ -38,6 +44,9 @@ class Trace:
     def __exit__(self, *a):
         Trace.active = None
 
+    def wants(self, tag):
+        return tag in self.tags or ("*" in self.tags and tag is None)
+
     def summary(self):
         torch.cuda.synchronize()
         out = {}
@@ -50,6 +59,27 @@ class Trace:
             t[3] += nbytes
         return {k: {"launches": v[0], "ms_total": v[1], "flops_total": v[2], "bytes_total": v[3]}
                 for k, v in out.items()}
+
+
+class span:
+    """Context manager: time the enclosed launches (one stream) as one record of `tag` when the
+    active Trace asks for it."""
+
+    def __init__(self, tag, nbytes=0.0, flops=0.0):
+        self.tag, self.nbytes, self.flops = tag, nbytes, flops
+        self.ev = None
+
+    def __enter__(self):
+        tr = Trace.active
+        if tr is not None and self.tag in tr.tags:
+            self.ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            self.ev[0].record()
+        return self
+
+    def __exit__(self, *a):
+        if self.ev is not None:
+            self.ev[1].record()
+            Trace.active.events.append((self.tag, self.flops, self.nbytes, self.ev[0], self.ev[1]))
 
 
 def set_math(mode: str) -> None:
@@ -259,14 +289,20 @@ def gemm(A, B, Cout, M, N, K, sAm, sAk, sBk, sBn, sCm, sCn, *, amode, bmode,
             ws = scratch(Cout.device, nws)
             d.ws, d.ws_len = ws.data_ptr(), ws.numel()
     tr = Trace.active
-    if tr is not None and tag in tr.tags:
+    if tr is not None and (tag in tr.tags or "*" in tr.tags):
         ev0 = torch.cuda.Event(enable_timing=True)
         ev1 = torch.cuda.Event(enable_timing=True)
         ev0.record()
         call("kdfm_gemm", C.byref(d), _s())
         ev1.record()
-        nb = nbytes if nbytes is not None else 4.0 * (M * K + K * N + M * N) * batch[0] * batch[1]
-        tr.events.append((tag, 2.0 * M * N * K * batch[0] * batch[1], nb, ev0, ev1))
+        if nbytes is None:   # fp32 storage: both operands and the output once, plus each side operand
+            side = sum(1 for t in (R, aux, Cpre) if t is not None)
+            nbytes = 4.0 * (M * K + K * N + M * N * (1 + side)) * batch[0] * batch[1]
+        fl = 2.0 * M * N * K * batch[0] * batch[1]
+        if tag in tr.tags:
+            tr.events.append((tag, fl, nbytes, ev0, ev1))
+        if "*" in tr.tags:
+            tr.events.append(("gemm:" + ROUTES.get(int(_lib.lib().kdfm_gemm_last_route()), "?"), fl, nbytes, ev0, ev1))
         return
     call("kdfm_gemm", C.byref(d), _s())
 

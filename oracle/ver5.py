@@ -199,7 +199,7 @@ def init_all(cfg: StepConfig, teacher_seed=0, student_seed=1, heads_seed=2) -> d
 
 def preprocess(wav, lengths, window, fb, cfg: StepConfig, dither_noise=None):
     seq_len = torch.div(lengths, cfg.hop, rounding_mode="floor")      # pinned: frames - 1
-    x = wav.float()
+    x = wav.to(window.dtype)   # float32 (parity) or float64 (accuracy reference)
     if dither_noise is not None:
         x = x + cfg.dither * dither_noise
     timemask = torch.arange(x.shape[1]).unsqueeze(0) < lengths.unsqueeze(1)
@@ -262,11 +262,11 @@ def subsampling(x_btf, lengths, p, pre, cfg: StepConfig):
     return x, l2
 
 
-def rel_pos_emb(T, d):
+def rel_pos_emb(T, d, dtype=torch.float32):
     """RelPositionalEncoding (A.4): sinusoids for relative positions T-1 ... -(T-1)."""
-    pos = torch.arange(T - 1, -T, -1, dtype=torch.float32).unsqueeze(1)
-    div = torch.exp(torch.arange(0, d, 2, dtype=torch.float32) * -(math.log(10000.0) / d))
-    pe = torch.zeros(pos.shape[0], d)
+    pos = torch.arange(T - 1, -T, -1, dtype=dtype).unsqueeze(1)
+    div = torch.exp(torch.arange(0, d, 2, dtype=dtype) * -(math.log(10000.0) / d))
+    pe = torch.zeros(pos.shape[0], d, dtype=dtype)
     pe[:, 0::2] = torch.sin(pos * div)
     pe[:, 1::2] = torch.cos(pos * div)
     return pe.unsqueeze(0)
@@ -339,7 +339,7 @@ def encoder(mel, lengths, p, prefix, d, h, cfg: StepConfig, training, bn_state):
     x, length = subsampling(x, lengths, p, prefix + "pre_encode.", cfg)
     B, T, _ = x.shape
     x = x * math.sqrt(d)
-    pos_emb = rel_pos_emb(T, d)
+    pos_emb = rel_pos_emb(T, d, x.dtype)
     valid = torch.arange(T).expand(B, T) < length.unsqueeze(1)
     att_ok = valid.unsqueeze(1).repeat(1, T, 1)
     att_ok = att_ok & att_ok.transpose(1, 2)
@@ -401,7 +401,7 @@ def fm_latent(s_bct, t_bct, p, steps, prefix="fm_latent.fm."):
     velocity = None
     t = None
     for i in range(steps, 0, -1):
-        t = torch.full((s_f.size(0), s_f.size(1), 1), i / steps)
+        t = torch.full((s_f.size(0), s_f.size(1), 1), i / steps, dtype=s_f.dtype)
         e = F.linear(t, p[prefix + "time_embed.weight"], p[prefix + "time_embed.bias"])
         h = F.relu(F.linear(torch.cat([x, e], dim=-1), p[prefix + "meta_encoder.0.weight"],
                             p[prefix + "meta_encoder.0.bias"]))
@@ -504,8 +504,8 @@ def ver5_step(p, wav, wav_len, targets, target_len, cfg: StepConfig, eps, spec_m
         tch_p = F.softmax(tch_logp / cfg.kd_temperature, dim=-1)
     stu_logp = F.log_softmax(log_probs / cfg.kd_temperature, dim=-1)
     kl = F.kl_div(stu_logp, tch_p, reduction="batchmean") * cfg.kd_temperature ** 2
-    recon_sum = torch.zeros(())
-    fm_sum = torch.zeros(())
+    recon_sum = torch.zeros((), dtype=log_probs.dtype)
+    fm_sum = torch.zeros((), dtype=log_probs.dtype)
     for i, (s, t) in enumerate(zip(s_feats, t_feats)):
         r, f = ver5_layer_losses(s, t, p, eps[i], cfg)
         recon_sum = recon_sum + r

@@ -114,3 +114,41 @@ def test_teacher_from_nemo_gz(eng, tmp_path):
     assert _same(e2.teacher, eng.teacher)
     tb = [n for n, _ in e2.bn.specs if n.startswith("teacher.")]
     assert all(torch.equal(e2.bn.P[n], eng.bn.P[n]) for n in tb)
+
+
+class DictConfigStandIn:
+    """Stands for omegaconf.DictConfig (not importable here), which NeMo's ModelPT stores as
+    ckpt["hyper_parameters"] through save_hyperparameters(cfg): a class outside torch's
+    weights-only allowlist.  Instantiating it would record the side effect below."""
+    constructed = 0
+
+    def __init__(self, content):
+        type(self).constructed += 1
+        self._content = content
+
+
+def test_reference_style_ckpt_with_foreign_hyperparameters(eng, tmp_path):
+    """A Lightning checkpoint as the reference writes it: hyper_parameters hold a non-allowlisted
+    class and there is no kdfm flat optimizer entry.  The state dict loads, the foreign
+    object comes back as an inert stand-in (its code never runs), and the Noam schedule resumes at
+    global_step."""
+    sd = C.engine_state_dict(eng)
+    sd["teacher.encoder.layers.0.conv.batch_norm.num_batches_tracked"] = torch.tensor(777)
+    p = str(tmp_path / "reference.ckpt")
+    torch.save({"epoch": 2, "global_step": 4567, "state_dict": sd,
+                "optimizer_states": [{"state": {}, "param_groups": []}],
+                "hyper_parameters": {"cfg": DictConfigStandIn({"encoder": {"d_model": 88}})}}, p)
+    DictConfigStandIn.constructed = 0
+    e2 = _fresh()
+    with pytest.warns(UserWarning, match="schedule resumes"):
+        info = C.restore_lightning_ckpt(e2, p)
+    assert DictConfigStandIn.constructed == 0
+    assert not info["resumed_optimizer"] and info["global_step"] == 4567 and int(e2.step) == 4567
+    assert _same(e2.student, eng.student) and _same(e2.teacher, eng.teacher)
+    hp = C.read_lightning_ckpt(p)["hyper_parameters"]["cfg"]
+    assert isinstance(hp, C.InertGlobal) and not isinstance(hp, DictConfigStandIn)
+    assert hp._state == {"_content": {"encoder": {"d_model": 88}}}
+    # teacher BatchNorm counters pass through; the student's count its optimizer steps
+    out = C.engine_state_dict(e2)
+    assert int(out["teacher.encoder.layers.0.conv.batch_norm.num_batches_tracked"]) == 777
+    assert int(out["encoder.layers.0.conv.batch_norm.num_batches_tracked"]) == 4567

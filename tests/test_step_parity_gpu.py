@@ -3,14 +3,19 @@
 The oracle (oracle/ver5.py) is pinned to the reference's own KD-head classes by golden vectors and
 to NeMo's invariants; here the product (kdfm.engine.Ver5Engine, all libkdfm kernels) runs the same
 seeded weights and inputs and must match losses, the mel frontend, every hooked layer output and
-every trainable gradient.  Tolerances (fp32): losses rtol 2e-4; activations and gradients
-max|diff| <= 2e-3 * max|ref| + 1e-6 per tensor (summation order differs: MFMA vs MKL).  The engine
+every trainable gradient.  Tolerances (fp32 kernels vs the oracle evaluated in float64): losses rtol 2e-4; activations
+max|diff| <= 2e-3 * max|ref| + 1e-6 per tensor; gradients the same, or within 4x the float32
+oracle's own distance to float64 (the step's f32 rounding noise) where that noise is larger.  The engine
 runs with deterministic reductions (PARITY.deterministic: no split-K / cross-block atomics).
 """
+import os
+
 import pytest
 import torch
 
 from oracle import ver5 as O
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 pytestmark = pytest.mark.gpu
 
@@ -50,15 +55,21 @@ def _oracle_params(cfg, eng):
     return ocfg, p
 
 
-def _close(a, b, tol, what, atol=1e-6):
+def _close(a, b, tol, what, atol=1e-6, failures=None):
     """max|a-b| <= tol*max|b| + atol.  The absolute floor covers gradients that are analytically
-    zero (e.g. linear_k.bias: a per-row constant shift of the scores cancels in the softmax)."""
+    zero (e.g. linear_k.bias: a per-row constant shift of the scores cancels in the softmax).
+    With `failures` (a list) mismatches are collected instead of raised."""
     a = a.detach().float().cpu()
     b = b.detach().float().cpu()
     assert a.shape == b.shape, (what, a.shape, b.shape)
     scale = b.abs().max().item()
     err = (a - b).abs().max().item()
-    assert err <= tol * scale + atol, f"{what}: max|diff| {err:.3e} vs max|ref| {scale:.3e}"
+    msg = f"{what}: max|diff| {err:.3e} vs max|ref| {scale:.3e}"
+    if failures is not None:
+        if not err <= tol * scale + atol:
+            failures.append(msg)
+        return
+    assert err <= tol * scale + atol, msg
 
 
 @pytest.mark.parametrize("n_layers,B,N,lens,U,tl", [
@@ -79,17 +90,27 @@ def test_ver5_step_matches_oracle(n_layers, B, N, lens, U, tl):
     torch.cuda.synchronize()
     grads = eng.student.grads()
 
-    ocfg, p = _oracle_params(cfg, eng)
+    ocfg, p32 = _oracle_params(cfg, eng)
+    # The reference values come from the oracle evaluated in float64 (same restatement, higher
+    # precision), so the comparison measures the kernels' f32 rounding.  The oracle is also run in
+    # float32: its own distance to float64 is the f32 rounding noise of the step on a CPU, the
+    # yardstick for tensors whose gradient is ill-conditioned in f32 (at 16 s the subsampling conv
+    # weight gradient sums 64k cancelling terms after the 16-layer backward).
+    eps_o = eps_rows.view(n_layers, B, T, cfg.latent).permute(0, 1, 3, 2)
+    p = {k: (v.double() if v.is_floating_point() else v) for k, v in p32.items()}
     names = O.trainable_names(p)
     for k in names:
         p[k] = p[k].clone().requires_grad_(True)
-    eps_o = eps_rows.view(n_layers, B, T, cfg.latent).permute(0, 1, 3, 2)
-    out = O.ver5_step(p, wav, wl, tg, tgl, ocfg, eps_o)
-    ref = torch.stack([out["loss"], out["ctc"], out["kl"], out["recon"], out["fm"]]).detach()
+        p32[k] = p32[k].clone().requires_grad_(True)
+    out = O.ver5_step(p, wav.double(), wl, tg, tgl, ocfg, eps_o.double())
+    out32 = O.ver5_step(p32, wav, wl, tg, tgl, ocfg, eps_o)
+    g32 = dict(zip(names, torch.autograd.grad(out32["loss"], [p32[k] for k in names], allow_unused=True)))
+    ref = torch.stack([out["loss"], out["ctc"], out["kl"], out["recon"], out["fm"]]).detach().float()
     torch.testing.assert_close(losses, ref, rtol=2e-4, atol=2e-4)
     for i in range(n_layers):
         _close(sfeats[i].view(B, T, -1), out["s_feats"][i], 2e-3, f"student layer {i} output")
     og = torch.autograd.grad(out["loss"], [p[k] for k in names], allow_unused=True)
+    failures, report = [], []
     for k, gr in zip(names, og):
         if gr is None:
             gr = torch.zeros_like(p[k])
@@ -99,7 +120,20 @@ def test_ver5_step_matches_oracle(n_layers, B, N, lens, U, tl):
             assert grads[k].abs().max().item() <= 1e-4 * ref_scale + 1e-6, k
             assert gr.abs().max().item() <= 1e-4 * ref_scale + 1e-6, k
             continue
-        _close(grads[k], gr, 2e-3, f"grad {k}")
+        mine = grads[k].detach().double().cpu()
+        err = (mine - gr).abs().max().item()
+        noise = ((g32[k].double() - gr).abs().max().item()) if g32.get(k) is not None else 0.0
+        scale = gr.abs().max().item()
+        report.append((err / max(scale, 1e-30), k, err, noise, scale))
+        if not (err <= 2e-3 * scale + 1e-6 or err <= 4.0 * noise):
+            failures.append(f"grad {k}: max|diff| {err:.3e} vs max|ref| {scale:.3e} (f32 CPU noise {noise:.3e})")
+    report.sort(reverse=True)
+    out_dir = os.path.join(ROOT, "gpurun_out")
+    if os.path.isdir(out_dir):
+        with open(os.path.join(out_dir, f"step_parity_{n_layers}L_{N}.txt"), "w") as fh:
+            for r in report[:25]:
+                fh.write(f"{r[0]:.3e} {r[1]} err {r[2]:.3e} f32cpu-noise {r[3]:.3e} max {r[4]:.3e}\n")
+    assert not failures, f"{len(failures)} gradients out of tolerance: {failures}"
 
 
 def test_frontend_matches_oracle():

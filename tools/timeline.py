@@ -1,0 +1,59 @@
+"""Per-stream busy time and critical-path view of one training step from a rocprofv3 kernel trace
+(--kernel-trace --output-format csv).  usage: python tools/timeline.py <kernel_trace.csv> [steps]
+Steps are delimited by the CTC kernel (one launch per step); the last full step is analysed."""
+import csv
+import sys
+from collections import defaultdict
+
+
+def main():
+    path = sys.argv[1]
+    rows = []
+    with open(path) as fh:
+        for r in csv.DictReader(fh):
+            sid = r.get("Stream_Id") or r.get("Queue_Id") or "0"
+            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), sid,
+                         r["Kernel_Name"].replace("kdfm::(anonymous namespace)::", "").split("(")[0]))
+    rows.sort()
+    # step boundaries: the adamw kernel ends every step
+    ends = [e for s, e, q, n in rows if n.startswith("adamw_kernel") or "adamw_kernel" in n]
+    if len(ends) < 3:
+        print("need >= 3 steps in the trace")
+        return
+    t0, t1 = ends[-3], ends[-2]
+    step = [(s, e, q, n) for s, e, q, n in rows if s >= t0 and e <= t1]
+    span = (t1 - t0) / 1e6
+    print(f"step window {span:.3f} ms, {len(step)} kernels")
+    busy = defaultdict(float)
+    cnt = defaultdict(int)
+    for s, e, q, n in step:
+        busy[q] += (e - s) / 1e6
+        cnt[q] += 1
+    for q in sorted(busy, key=lambda k: -busy[k]):
+        print(f"  stream {q}: busy {busy[q]:8.3f} ms  ({busy[q] / span * 100:5.1f}% of step)  {cnt[q]} kernels")
+    # union of busy intervals (any stream running)
+    ivs = sorted((s, e) for s, e, q, n in step)
+    tot, cs, ce = 0, None, None
+    for s, e in ivs:
+        if cs is None:
+            cs, ce = s, e
+        elif s <= ce:
+            ce = max(ce, e)
+        else:
+            tot += ce - cs
+            cs, ce = s, e
+    if cs is not None:
+        tot += ce - cs
+    print(f"  GPU busy (any stream): {tot / 1e6:.3f} ms = {tot / 1e6 / span * 100:.1f}% of the step; idle {span - tot / 1e6:.3f} ms")
+    # top kernels per stream
+    for q in sorted(busy, key=lambda k: -busy[k]):
+        agg = defaultdict(float)
+        for s, e, qq, n in step:
+            if qq == q:
+                agg[n] += (e - s) / 1e6
+        top = sorted(agg.items(), key=lambda kv: -kv[1])[:8]
+        print(f"  stream {q} top: " + "; ".join(f"{n[:40]} {t:.2f}" for n, t in top))
+
+
+if __name__ == "__main__":
+    main()
