@@ -219,6 +219,16 @@ int kdfm_layernorm_bwd(const float* dy, const float* x, const float* gamma, cons
                        const float* dres, float* dx, float* dgamma, float* dbeta, float* ws, int64_t rows, int64_t d,
                        void* stream);
 int64_t kdfm_layernorm_bwd_ws(int64_t rows, int64_t d);
+/* the same backward with the fold deferred: dgamma|dbeta block partials are written to `part`
+ * (kdfm_layernorm_bwd_ws(rows, d) floats) and folded later, for up to KDFM_LN_FOLD_MAX LayerNorms of
+ * the same (rows, d) in one launch, by kdfm_ln_fold (dgamma[i] / dbeta[i] accumulate, block order:
+ * deterministic).  parts / dgamma / dbeta are HOST arrays of n device pointers. */
+#define KDFM_LN_FOLD_MAX 8
+int kdfm_layernorm_bwd_part(const float* dy, const float* x, const float* gamma, const float* mean,
+                            const float* rstd, const float* dres, float* dx, float* part, int64_t rows, int64_t d,
+                            void* stream);
+int kdfm_ln_fold(const float* const* parts, float* const* dgamma, float* const* dbeta, int32_t n, int64_t rows,
+                 int64_t d, void* stream);
 /* Qu = Q + pos_bias_u, Qv = Q + pos_bias_v from the fused (rows, 3d) q|k|v projection */
 int kdfm_qkv_prep(const float* qkv, const float* pos_bias_u, const float* pos_bias_v, float* qu, float* qv,
                   int64_t rows, int64_t d, void* stream);

@@ -21,9 +21,10 @@ int check_launch(const char* what);
 bool deterministic();
 // Kernel family the most recent kdfm_gemm call on this thread launched (kdfm_gemm_last_route):
 // 0 generic 64x64 tile, 1 weight-stationary skinny, 2 row-streaming forward, 3 wide-tile weight
-// gradient (+ fold), 4 generic with ordered split-K fold, 5 LDS-slab k=3 conv.
+// gradient (+ fold), 4 generic with ordered split-K fold, 5 LDS-slab k=3 conv, 6 row-parallel
+// weight gradient (+ ordered fold).
 enum { ROUTE_GENERIC = 0, ROUTE_SKINNY = 1, ROUTE_RS_FWD = 2, ROUTE_RS_WGRAD = 3, ROUTE_SPLIT_FOLD = 4,
-       ROUTE_SLAB_CONV = 5 };
+       ROUTE_SLAB_CONV = 5, ROUTE_WGRAD_ROWS = 6 };
 void set_route(int r);
 
 #define KDFM_REQUIRE(cond, msg)                                  \

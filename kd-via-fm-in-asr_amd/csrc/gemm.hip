@@ -465,8 +465,10 @@ extern "C" int kdfm_gemm(const kdfm_gemm_desc* d, void* stream) {
       return KDFM_OK;
     }
     const int64_t need = (int64_t)p.splitk * d->M * d->N;
-    if (p.splitk > 1 && d->batch1 * d->batch2 == 1 && d->ws && d->ws_len >= need &&
-        !(d->math == KDFM_MATH_BF16 && rowstream_wgrad_ws(p, d->amode, d->bmode, 1) > 0)) {
+    // the bf16 wide-tile / row-parallel weight-gradient kernels fold their partials in order themselves
+    const bool wide = d->math == KDFM_MATH_BF16 && d->ws &&
+                      (rowstream_wgrad_ws(p, d->amode, d->bmode, 1) > 0 || wgrad_rows_ws(p, d->amode, d->bmode, 1) > 0);
+    if (p.splitk > 1 && d->batch1 * d->batch2 == 1 && d->ws && d->ws_len >= need && !wide) {
       p.partial = 1;
       set_route(ROUTE_SPLIT_FOLD);
       dim3 grid((unsigned)ceil_div(d->M, BM), (unsigned)ceil_div(d->N, BN), (unsigned)p.splitk);
@@ -475,11 +477,13 @@ extern "C" int kdfm_gemm(const kdfm_gemm_desc* d, void* stream) {
       if (rc) return rc;
       return launch_split_fold(p, p.splitk, true, st);
     }
-    if (!(d->math == KDFM_MATH_BF16 && d->ws && rowstream_wgrad_ws(p, d->amode, d->bmode, 1) > 0)) p.splitk = 1;
+    if (!wide) p.splitk = 1;
   }
   if (d->math == KDFM_MATH_BF16 && d->K > 0) {
     const int64_t batch = d->batch1 * d->batch2;
-    int rc = try_rowstream_wgrad(p, d->amode, d->bmode, batch, st);
+    int rc = try_wgrad_rows(p, d->amode, d->bmode, batch, st);
+    if (rc >= 0) return set_route(ROUTE_WGRAD_ROWS), rc;
+    rc = try_rowstream_wgrad(p, d->amode, d->bmode, batch, st);
     if (rc >= 0) return set_route(ROUTE_RS_WGRAD), rc;
     set_route(ROUTE_SKINNY);  // try_skinny_fwd marks its LDS-slab conv instance itself
     rc = try_skinny_fwd(p, d->amode, d->bmode, batch, st);
@@ -506,6 +510,10 @@ extern "C" int64_t kdfm_gemm_ws(const kdfm_gemm_desc* d) {
   p.conv_c = d->conv_c; p.conv_t = d->conv_t; p.ones_col = d->ones_col; p.ones_out = d->ones_out;
   p.Bh = nullptr; p.sBh = 0;
   int64_t n = rowstream_wgrad_ws(p, d->amode, d->bmode, d->batch1 * d->batch2);
+  if (d->math == KDFM_MATH_BF16) {
+    const int64_t w = wgrad_rows_ws(p, d->amode, d->bmode, d->batch1 * d->batch2);
+    if (w > n) n = w;
+  }
   if (deterministic() && (d->epi & KDFM_EPI_ATOMIC) && d->splitk > 1 && d->batch1 * d->batch2 == 1) {
     const int64_t sk = (int64_t)d->splitk * d->M * d->N;  // ordered split-K partials
     if (sk > n) n = sk;

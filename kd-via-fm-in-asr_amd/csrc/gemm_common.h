@@ -168,6 +168,9 @@ int64_t rowstream_wgrad_ws(const GemmP& p, int amode, int bmode, int64_t batch);
 // C(m,n) += alpha * sum_{s<S} ws[s][m][n] in slab order (n == ones_col -> ones_out[m]); one thread
 // per element sums all S partials when `ordered` (deterministic mode), else slabs of 16.
 int launch_split_fold(const GemmP& p, int64_t S, bool ordered, hipStream_t st);
+// Row-parallel weight gradient with ordered fold (wgrad.hip); -1 when not eligible.
+int try_wgrad_rows(const GemmP& p, int amode, int bmode, int64_t batch, hipStream_t st);
+int64_t wgrad_rows_ws(const GemmP& p, int amode, int bmode, int64_t batch);
 // Weight-stationary skinny forward (skinny.hip); -1 when not eligible.
 int try_skinny_fwd(const GemmP& p, int amode, int bmode, int64_t batch, hipStream_t st);
 

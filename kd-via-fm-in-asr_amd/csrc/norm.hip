@@ -1,7 +1,7 @@
 // LayerNorm forward/backward (Conformer pre-norms, NeMo ConformerLayer norm_* with eps 1e-5;
 // called per layer from conformer_encoder.py:685-692).  One wave per row (d <= 256), fp32
 // statistics; the backward fuses the residual-stream gradient add and reduces dgamma/dbeta with
-// per-block partials + one atomic per column per block.
+// per-block partials folded in block order (one fold launch can serve several LayerNorms).
 #include "common.h"
 
 namespace kdfm {
@@ -46,9 +46,13 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
   }
 }
 
-// dx = rstd * (dy*g - mean(dy*g) - xhat * mean(dy*g*xhat)) (+ dres).  Each block owns 64 rows
-// (16 per wave, processed 4 at a time so their loads are in flight together) and writes its
-// dgamma|dbeta column partials to part[block][2d]; the host folds them with launch_colsum.
+// dx = rstd * (dy*g - mean(dy*g) - xhat * mean(dy*g*xhat)) (+ dres).  A block is 4 waves x LN_RPW
+// rows (one row per wave per step, every load of the wave's rows issued before the first use), so a
+// 12,832-row LayerNorm runs as ~800 workgroups: enough loads in flight to stream at HBM rate, where
+// 64-row blocks (~200 workgroups) left most CUs idle.  The block's dgamma|dbeta column partials go
+// to part[block][2d]; kdfm_ln_fold (one launch for several LayerNorms) sums them in block order.
+constexpr int LN_RPW = 4;
+
 template <int V>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ x,
                                                      const float* __restrict__ g, const float* __restrict__ mean,
@@ -64,51 +68,45 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ d
     pg[i] = 0.f;
     pb[i] = 0.f;
   }
-  const int64_t base = (int64_t)blockIdx.x * 64 + w * 16;
-#pragma unroll 1
-  for (int rb = 0; rb < 16; rb += 4) {
-    float dyv[4][V], xv[4][V], mu[4], rs[4];
+  const int64_t base = ((int64_t)blockIdx.x * 4 + w) * LN_RPW;
+  float dyv[LN_RPW][V], xv[LN_RPW][V], rv[LN_RPW][V], mu[LN_RPW], rs[LN_RPW];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int64_t row = base + rb + j;
-      const bool ok = row < rows;
-      mu[j] = ok ? mean[row] : 0.f;
-      rs[j] = ok ? rstd[row] : 0.f;
+  for (int j = 0; j < LN_RPW; ++j) {
+    const int64_t row = base + j;
+    const bool ok = row < rows;
+    mu[j] = ok ? mean[row] : 0.f;
+    rs[j] = ok ? rstd[row] : 0.f;
 #pragma unroll
-      for (int i = 0; i < V; ++i) {
-        const int c = lane + 64 * i;
-        const bool in = ok && c < d;
-        dyv[j][i] = in ? dy[row * d + c] : 0.f;
-        xv[j][i] = in ? x[row * d + c] : 0.f;
-      }
+    for (int i = 0; i < V; ++i) {
+      const int c = lane + 64 * i;
+      const bool in = ok && c < d;
+      dyv[j][i] = in ? dy[row * d + c] : 0.f;
+      xv[j][i] = in ? x[row * d + c] : 0.f;
+      rv[j][i] = (in && dres) ? dres[row * d + c] : 0.f;
     }
+  }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int64_t row = base + rb + j;
-      float s1 = 0.f, s2 = 0.f;
+  for (int j = 0; j < LN_RPW; ++j) {
+    const int64_t row = base + j;
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+      const int c = lane + 64 * i;
+      const float xh = (c < d) ? (xv[j][i] - mu[j]) * rs[j] : 0.f;
+      xv[j][i] = xh;
+      const float gy = dyv[j][i] * gl[i];
+      pg[i] += dyv[j][i] * xh;
+      pb[i] += dyv[j][i];
+      s1 += gy;
+      s2 += gy * xh;
+    }
+    s1 = wave_sum(s1) / d;
+    s2 = wave_sum(s2) / d;
+    if (row < rows) {
 #pragma unroll
       for (int i = 0; i < V; ++i) {
         const int c = lane + 64 * i;
-        const float xh = (c < d) ? (xv[j][i] - mu[j]) * rs[j] : 0.f;
-        xv[j][i] = xh;
-        const float gy = dyv[j][i] * gl[i];
-        pg[i] += dyv[j][i] * xh;
-        pb[i] += dyv[j][i];
-        s1 += gy;
-        s2 += gy * xh;
-      }
-      s1 = wave_sum(s1) / d;
-      s2 = wave_sum(s2) / d;
-      if (row < rows) {
-#pragma unroll
-        for (int i = 0; i < V; ++i) {
-          const int c = lane + 64 * i;
-          if (c < d) {
-            float v = rs[j] * (dyv[j][i] * gl[i] - s1 - xv[j][i] * s2);
-            if (dres) v += dres[row * d + c];
-            dx[row * d + c] = v;
-          }
-        }
+        if (c < d) dx[row * d + c] = rs[j] * (dyv[j][i] * gl[i] - s1 - xv[j][i] * s2) + rv[j][i];
       }
     }
   }
@@ -123,6 +121,68 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ d
     pr[c] = (red[0][0][c] + red[0][1][c]) + (red[0][2][c] + red[0][3][c]);
     pr[d + c] = (red[1][0][c] + red[1][1][c]) + (red[1][2][c] + red[1][3][c]);
   }
+}
+
+// Ordered fold of LayerNorm partials for up to KDFM_LN_FOLD_MAX LayerNorms in one launch:
+// dgamma_e[c] += sum_b part_e[b][c], dbeta_e[c] += sum_b part_e[b][d + c].  grid = (column groups of
+// 64 over 2d, entries); lane = column, the 4 waves stride the partial rows, fixed-order combine
+// (deterministic: one workgroup owns each output column).
+struct LnFold {
+  const float* part[KDFM_LN_FOLD_MAX];
+  float* dg[KDFM_LN_FOLD_MAX];
+  float* db[KDFM_LN_FOLD_MAX];
+};
+
+__global__ __launch_bounds__(256) void ln_fold_kernel(LnFold f, int64_t nparts, int d) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int e = blockIdx.y;
+  const int c = blockIdx.x * 64 + lane;
+  const float* part = f.part[e];
+  float s0 = 0.f, s1 = 0.f;
+  if (c < 2 * d) {
+    int64_t b = w;
+    for (; b + 4 < nparts; b += 8) {
+      s0 += part[b * 2 * d + c];
+      s1 += part[(b + 4) * 2 * d + c];
+    }
+    for (; b < nparts; b += 4) s0 += part[b * 2 * d + c];
+  }
+  red[w][lane] = s0 + s1;
+  __syncthreads();
+  if (w == 0 && c < 2 * d) {
+    const float v = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+    if (c < d)
+      f.dg[e][c] += v;
+    else
+      f.db[e][c - d] += v;
+  }
+}
+
+int ln_fold(const float* const* parts, float* const* dgs, float* const* dbs, int n, int64_t nparts, int64_t d,
+            hipStream_t st) {
+  LnFold f{};
+  for (int i = 0; i < n; ++i) {
+    f.part[i] = parts[i];
+    f.dg[i] = dgs[i];
+    f.db[i] = dbs[i];
+  }
+  hipLaunchKernelGGL(ln_fold_kernel, dim3((unsigned)ceil_div(2 * d, 64), (unsigned)n), dim3(256), 0, st, f, nparts,
+                     (int)d);
+  return check_launch("kdfm_ln_fold");
+}
+
+int ln_bwd_launch(const float* dy, const float* x, const float* gamma, const float* mean, const float* rstd,
+                  const float* dres, float* dx, float* part, int64_t rows, int64_t d, hipStream_t st) {
+  const int64_t blocks = ceil_div(rows, 4 * LN_RPW);
+  const dim3 grid((unsigned)blocks), blk(256);
+  switch ((d + 63) / 64) {
+    case 1: hipLaunchKernelGGL(ln_bwd_kernel<1>, grid, blk, 0, st, dy, x, gamma, mean, rstd, dres, dx, part, rows, (int)d); break;
+    case 2: hipLaunchKernelGGL(ln_bwd_kernel<2>, grid, blk, 0, st, dy, x, gamma, mean, rstd, dres, dx, part, rows, (int)d); break;
+    case 3: hipLaunchKernelGGL(ln_bwd_kernel<3>, grid, blk, 0, st, dy, x, gamma, mean, rstd, dres, dx, part, rows, (int)d); break;
+    default: hipLaunchKernelGGL(ln_bwd_kernel<4>, grid, blk, 0, st, dy, x, gamma, mean, rstd, dres, dx, part, rows, (int)d); break;
+  }
+  return check_launch("kdfm_layernorm_bwd");
 }
 
 }  // namespace
@@ -141,7 +201,7 @@ int kdfm_layernorm_fwd(const float* x, const float* gamma, const float* beta, fl
   return check_launch("kdfm_layernorm_fwd");
 }
 
-int64_t kdfm_layernorm_bwd_ws(int64_t rows, int64_t d) { return kdfm::ceil_div(rows, 64) * 2 * d; }
+int64_t kdfm_layernorm_bwd_ws(int64_t rows, int64_t d) { return kdfm::ceil_div(rows, 4 * kdfm::LN_RPW) * 2 * d; }
 
 int kdfm_layernorm_bwd(const float* dy, const float* x, const float* gamma, const float* mean, const float* rstd,
                        const float* dres, float* dx, float* dgamma, float* dbeta, float* ws, int64_t rows, int64_t d,
@@ -151,19 +211,31 @@ int kdfm_layernorm_bwd(const float* dy, const float* x, const float* gamma, cons
   KDFM_REQUIRE(d > 0 && d <= 64 * MAXV, "d must be in (0, 256]");
   if (rows == 0) return KDFM_OK;
   hipStream_t st = as_stream(stream);
-  const int64_t blocks = ceil_div(rows, 64);
-  const dim3 grid((unsigned)blocks), blk(256);
-  switch ((d + 63) / 64) {
-    case 1: hipLaunchKernelGGL(ln_bwd_kernel<1>, grid, blk, 0, st, dy, x, gamma, mean, rstd, dres, dx, ws, rows, (int)d); break;
-    case 2: hipLaunchKernelGGL(ln_bwd_kernel<2>, grid, blk, 0, st, dy, x, gamma, mean, rstd, dres, dx, ws, rows, (int)d); break;
-    case 3: hipLaunchKernelGGL(ln_bwd_kernel<3>, grid, blk, 0, st, dy, x, gamma, mean, rstd, dres, dx, ws, rows, (int)d); break;
-    default: hipLaunchKernelGGL(ln_bwd_kernel<4>, grid, blk, 0, st, dy, x, gamma, mean, rstd, dres, dx, ws, rows, (int)d); break;
-  }
-  int rc = check_launch("kdfm_layernorm_bwd");
+  int rc = ln_bwd_launch(dy, x, gamma, mean, rstd, dres, dx, ws, rows, d, st);
   if (rc) return rc;
-  rc = launch_colsum(ws, dgamma, blocks, d, 2 * d, 1.f, st);
-  if (rc) return rc;
-  return launch_colsum(ws + d, dbeta, blocks, d, 2 * d, 1.f, st);
+  const float* parts[1] = {ws};
+  float* dgs[1] = {dgamma};
+  float* dbs[1] = {dbeta};
+  return ln_fold(parts, dgs, dbs, 1, ceil_div(rows, 4 * LN_RPW), d, st);
+}
+
+int kdfm_layernorm_bwd_part(const float* dy, const float* x, const float* gamma, const float* mean,
+                            const float* rstd, const float* dres, float* dx, float* part, int64_t rows, int64_t d,
+                            void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(dy && x && gamma && mean && rstd && dx && part, "null pointer");
+  KDFM_REQUIRE(d > 0 && d <= 64 * MAXV, "d must be in (0, 256]");
+  if (rows == 0) return KDFM_OK;
+  return ln_bwd_launch(dy, x, gamma, mean, rstd, dres, dx, part, rows, d, as_stream(stream));
+}
+
+int kdfm_ln_fold(const float* const* parts, float* const* dgamma, float* const* dbeta, int32_t n, int64_t rows,
+                 int64_t d, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(parts && dgamma && dbeta && n >= 1 && n <= KDFM_LN_FOLD_MAX, "1..KDFM_LN_FOLD_MAX LayerNorms");
+  for (int i = 0; i < n; ++i) KDFM_REQUIRE(parts[i] && dgamma[i] && dbeta[i], "null pointer");
+  if (rows == 0) return KDFM_OK;
+  return ln_fold(parts, dgamma, dbeta, n, ceil_div(rows, 4 * LN_RPW), d, as_stream(stream));
 }
 
 }  // extern "C"

@@ -1,0 +1,439 @@
+// Row-parallel weight gradients for the tall-skinny products of the ver5 step (bf16 MFMA, f32
+// accumulate, deterministic ordered fold).
+//
+//   dW[m][n] (+)= alpha * sum_r dY[r][m] * X[r][n]      (+ the implicit ones column n = N-1 -> bias)
+//
+// Every Linear / 1x1 Conv1d weight gradient of the Conformer layers (12,832 rows at the bench
+// shape, outputs up to 352 x 89) and of the layer-batched KD heads (205,312 rows, SimpleDenoiser's
+// Conv1d(k=3) in CONV mode: X[r][n = tap*C + c] = x[r + tap - 1][c] inside each utterance;
+// asr_train_diffm.py:400-460, 1295-1338) contracts over ALL rows into an output that fits one
+// workgroup.  So each workgroup takes a contiguous run of rows and accumulates the WHOLE output (or a
+// column slice of a very wide one) in MFMA accumulators: dY and X are each read from HBM exactly once,
+// in 16-byte loads, and every workgroup writes one f32 partial; a fold kernel sums the partials in
+// split order (one thread per output element: deterministic, no float atomics on the weight
+// gradient).  The split-K generic kernel this replaces re-read the operands once per 64x64 output
+// tile and added 25 partial sums per element with atomics.
+//
+// Pipeline: rows advance in 32-row steps (the MFMA K); step s+PD is loaded into registers while step
+// s is multiplied out of LDS, so PD slabs of loads are in flight per workgroup.  Staging converts to
+// bf16 and transposes into a [column][32 rows] LDS image (8-byte stores of 4 rows per column), from
+// which A / B fragments are single 16-byte reads.
+#include "gemm_common.h"
+
+#include <cstdlib>
+
+namespace kdfm {
+namespace {
+
+// explicit LDS (address space 3) views: generic pointers into the dynamic LDS array compiled to FLAT
+// loads/stores, which also wait on the global-load counter and serialised the software pipeline
+typedef __attribute__((address_space(3))) uint16_t lds_u16;
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+template <typename T>
+__device__ __forceinline__ __attribute__((address_space(3))) T* lds_at(uint16_t* base, int off) {
+  return reinterpret_cast<__attribute__((address_space(3))) T*>((lds_u16*)base + off);
+}
+
+constexpr int WR_NT = 512;      // threads: 8 waves, 2 per SIMD
+constexpr int WR_LDK = 40;      // bf16 row stride of the [col][32 rows] image (80 B: conflict-light b128 reads)
+constexpr int WR_MAXU = 2;      // staging units (4 rows x 4 cols) per thread per slab (template UPT <= this)
+
+struct WrGeo {
+  int wm, wn;        // wave grid over the block grid (wm * wn == 8)
+  int Ma;            // A image columns: M padded to 16 * MBW * wm
+  int Nb;            // B image columns of one slice (16 * NBW * wn)
+  int64_t steps_per; // 32-row steps per split
+  int64_t nmem;      // X columns in memory = ones_col if >= 0 else N
+};
+
+template <int MBW, int NBW, bool CONV, int PD, int UPT>
+__global__ __launch_bounds__(WR_NT, 2) void wgr_kernel(GemmP p, WrGeo g) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t wr_lds[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // LDS images as element offsets into wr_lds (an array of pointers would decay to generic pointers
+  // and turn every LDS access into a FLAT access that also waits on the global-load counter)
+  const int ia = g.Ma * WR_LDK, ib = g.Nb * WR_LDK;   // image sizes (elements) of one buffer
+  const int bufsz = ia + ib;                           // buffer b: A at b*bufsz, B at b*bufsz + ia
+  const int64_t split = blockIdx.x;
+  const int64_t n0 = (int64_t)blockIdx.y * g.Nb;       // first output column of this slice
+  const int64_t kb = split * g.steps_per * 32;
+  int64_t ke = kb + g.steps_per * 32;
+  if (ke > p.K) ke = p.K;
+  // B memory columns of this slice and the slab's staging units (4 rows x 4 columns each)
+  const int ncols_mem = (int)((g.nmem - n0 < g.Nb) ? g.nmem - n0 : g.Nb);
+  const int units = 8 * (int)((p.M >> 2) + (ncols_mem >> 2));
+
+  // static image columns: A columns >= M and B columns beyond the memory columns are zero, the
+  // ones column (bias gradient) is 1 in every row (rows past K contribute 0 through A)
+  for (int e = threadIdx.x; e < 2 * (g.Ma + g.Nb) * 4; e += WR_NT) {
+    const int buf = e / ((g.Ma + g.Nb) * 4);
+    const int q = e - buf * (g.Ma + g.Nb) * 4;
+    const int col = q >> 2, kq = (q & 3) * 8;
+    int img;
+    int c;
+    bool zero = false, one = false;
+    if (col < g.Ma) {
+      img = buf * bufsz;
+      c = col;
+      zero = c >= p.M;
+    } else {
+      img = buf * bufsz + ia;
+      c = col - g.Ma;
+      const int64_t n = n0 + c;
+      one = (p.ones_col >= 0 && n == p.ones_col);
+      zero = !one && (c >= ncols_mem);
+    }
+    if (zero || one) {
+      const uint16_t v = one ? (uint16_t)0x3F80 : (uint16_t)0;  // bf16(1.0) = 0x3F80
+      bf16x8 pk;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) pk[i] = (short)v;
+      *lds_at<bf16x8>(wr_lds, img + c * WR_LDK + kq) = pk;
+    }
+  }
+
+  // staging unit u: row group rg = u % 8 (rows 4rg..4rg+3 of a slab), column group cg = u / 8 (4
+  // consecutive columns of A (cg < ma4) or of B).  Per-unit source pointers and (CONV) frame
+  // counters are set up once and advanced by one slab per step: no 64-bit multiplies in the loop.
+  // Rows past the split's end or outside the utterance (CONV taps) load from a clamped valid address
+  // and are zeroed by a select (branch-free).
+  const int ma4 = (int)(p.M >> 2);
+  const float* src[UPT];
+  int64_t ld[UPT];
+  int tfr[UPT], toff[UPT];   // CONV: frame of the unit's first row in its utterance; tap - pad
+  bool act[UPT];
+#pragma unroll
+  for (int i = 0; i < UPT; ++i) {
+    const int u = threadIdx.x + i * WR_NT;
+    act[i] = u < units;
+    const int rg = u & 7, cg = act[i] ? (u >> 3) : 0;
+    const int64_t r0 = kb + rg * 4;
+    tfr[i] = 0;
+    toff[i] = 0;
+    if (cg < ma4) {
+      src[i] = p.A + r0 * p.sAk + cg * 4;
+      ld[i] = p.sAk;
+    } else {
+      const int64_t n = n0 + (int64_t)(cg - ma4) * 4;
+      ld[i] = p.sBk;
+      if constexpr (CONV) {
+        const int64_t tap = n / p.conv_c, c = n - tap * p.conv_c;
+        toff[i] = (int)(tap - p.pad);
+        tfr[i] = (int)(r0 % p.conv_t);
+        src[i] = p.B + (r0 + toff[i]) * p.sBk + c;
+      } else {
+        src[i] = p.B + r0 * p.sBk + n;
+      }
+    }
+  }
+  const int T = CONV ? (int)p.conv_t : 0;
+  float4 reg[PD][UPT][4];
+  uint32_t msk[PD];   // bit i*4+j: row j of unit i is real data (else staged as 0)
+  // k0: first row of the slab (uniform); the unit pointers already point at it.  The loads go
+  // straight into the slab registers and the validity select is applied at staging time: a select
+  // right after a load would make every load wait for its own data (no loads in flight across steps).
+  auto load = [&](float4 (&r)[UPT][4], uint32_t& m, int64_t k0) {
+    const bool full = k0 + 32 <= ke;
+    m = 0u;
+#pragma unroll
+    for (int i = 0; i < UPT; ++i) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        bool ok = act[i];
+        if (!full) ok = ok && (k0 + (threadIdx.x & 7) * 4 + j < ke);
+        if constexpr (CONV) {
+          if (ok) {   // frame of row j within the utterance, shifted by the tap
+            int t = tfr[i] + j;
+            t = (t >= T) ? t - T : t;
+            const int tt = t + toff[i];
+            ok = tt >= 0 && tt < T;
+          }
+        }
+        const float* q = ok ? src[i] + j * ld[i] : p.B;   // p.B: any valid, aligned address
+        r[i][j] = *reinterpret_cast<const float4*>(q);
+        m |= (ok ? 1u : 0u) << (i * 4 + j);
+      }
+      src[i] += 32 * ld[i];
+      if constexpr (CONV) {
+        tfr[i] += 32;
+        while (tfr[i] >= T) tfr[i] -= T;
+      }
+    }
+  };
+  auto stage = [&](const float4 (&r)[UPT][4], uint32_t m, int buf) {
+#pragma unroll
+    for (int i = 0; i < UPT; ++i) {
+      const int u = threadIdx.x + i * WR_NT;
+      if (u >= units) continue;
+      const int rg = u & 7, cg = u >> 3;
+      int img, c0;
+      if (cg < ma4) {
+        img = buf * bufsz;
+        c0 = cg * 4;
+      } else {
+        img = buf * bufsz + ia;
+        c0 = (cg - ma4) * 4;
+      }
+      const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+      const float4 v0 = ((m >> (i * 4 + 0)) & 1u) ? r[i][0] : z;
+      const float4 v1 = ((m >> (i * 4 + 1)) & 1u) ? r[i][1] : z;
+      const float4 v2 = ((m >> (i * 4 + 2)) & 1u) ? r[i][2] : z;
+      const float4 v3 = ((m >> (i * 4 + 3)) & 1u) ? r[i][3] : z;
+      const float* f0 = reinterpret_cast<const float*>(&v0);
+      const float* f1 = reinterpret_cast<const float*>(&v1);
+      const float* f2 = reinterpret_cast<const float*>(&v2);
+      const float* f3 = reinterpret_cast<const float*>(&v3);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t lo = (uint32_t)f2bf(f0[q]) | ((uint32_t)f2bf(f1[q]) << 16);
+        const uint32_t hi = (uint32_t)f2bf(f2[q]) | ((uint32_t)f2bf(f3[q]) << 16);
+        *lds_at<u32x2>(wr_lds, img + (c0 + q) * WR_LDK + rg * 4) = u32x2{lo, hi};
+      }
+    }
+  };
+
+  const int wr_ = wave / g.wn, wc_ = wave - (wave / g.wn) * g.wn;
+  const int mb0 = wr_ * MBW, nb0 = wc_ * NBW;
+  f32x4 acc[MBW][NBW];
+#pragma unroll
+  for (int i = 0; i < MBW; ++i)
+#pragma unroll
+    for (int j = 0; j < NBW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int64_t nsteps = (ke > kb) ? (ke - kb + 31) / 32 : 0;
+  auto mfma_step = [&](int buf) {
+    const int oA = buf * bufsz, oB = buf * bufsz + ia;
+    bf16x8 af[MBW];
+#pragma unroll
+    for (int i = 0; i < MBW; ++i)
+      af[i] = *lds_at<bf16x8>(wr_lds, oA + ((mb0 + i) * 16 + (lane & 15)) * WR_LDK + 8 * (lane >> 4));
+#pragma unroll
+    for (int j = 0; j < NBW; ++j) {
+      const bf16x8 bfr = *lds_at<bf16x8>(wr_lds, oB + ((nb0 + j) * 16 + (lane & 15)) * WR_LDK + 8 * (lane >> 4));
+#pragma unroll
+      for (int i = 0; i < MBW; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr, acc[i][j], 0, 0, 0);
+    }
+  };
+  if constexpr (PD == 1) {
+    if (nsteps > 0) {
+      load(reg[0], msk[0], kb);
+      stage(reg[0], msk[0], 0);
+    }
+    __syncthreads();
+    int buf = 0;
+    for (int64_t s = 0; s < nsteps; ++s) {
+      if (s + 1 < nsteps) load(reg[0], msk[0], kb + 32 * (s + 1));
+      mfma_step(buf);
+      if (s + 1 < nsteps) stage(reg[0], msk[0], buf ^ 1);
+      __syncthreads();
+      buf ^= 1;
+    }
+  } else {
+    // two slabs in flight: slot 0 carries even steps, slot 1 odd steps (compile-time slots, so the
+    // compiler waits only for the older slot's loads before staging it)
+    if (nsteps > 0) load(reg[0], msk[0], kb);
+    if (nsteps > 1) load(reg[1], msk[1], kb + 32);
+    if (nsteps > 0) stage(reg[0], msk[0], 0);
+    __syncthreads();
+    for (int64_t s = 0; s < nsteps; s += 2) {
+      // even step s in buffer 0
+      if (s + 2 < nsteps) load(reg[0], msk[0], kb + 32 * (s + 2));
+      mfma_step(0);
+      if (s + 1 < nsteps) stage(reg[1], msk[1], 1);
+      __syncthreads();
+      if (s + 1 >= nsteps) break;
+      // odd step s+1 in buffer 1
+      if (s + 3 < nsteps) load(reg[1], msk[1], kb + 32 * (s + 3));
+      mfma_step(1);
+      if (s + 2 < nsteps) stage(reg[0], msk[0], 0);
+      __syncthreads();
+    }
+  }
+
+  // raw partial of this (split, slice) -> ws[split][m][n]
+  float* wsp = p.ws + split * p.M * p.N;
+#pragma unroll
+  for (int i = 0; i < MBW; ++i)
+#pragma unroll
+    for (int j = 0; j < NBW; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t m = (mb0 + i) * 16 + (lane >> 4) * 4 + r;
+        const int64_t n = n0 + (nb0 + j) * 16 + (lane & 15);
+        if (m < p.M && n < p.N && n < n0 + g.Nb) wsp[m * p.N + n] = acc[i][j][r];
+      }
+}
+
+// C(m, n) += alpha * sum_{s<S} ws[s][m][n]   (n == ones_col -> ones_out[m]), deterministic: the block
+// owns 64 consecutive output elements (lane = element: coalesced partial rows), its 8 waves take the
+// splits s = w, w+8, ... with 4 independent accumulators each (many loads in flight: the fold is
+// latency-bound otherwise), then a fixed-order combine in LDS and one plain add per element.
+constexpr int WF_WAVES = 8;
+
+__global__ __launch_bounds__(64 * WF_WAVES) void wgr_fold_kernel(GemmP p, int64_t S) {
+  __shared__ float red[WF_WAVES][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t MN = p.M * p.N;
+  const int64_t e = (int64_t)blockIdx.x * 64 + lane;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  if (e < MN) {
+    int64_t s = w;
+    for (; s + 3 * WF_WAVES < S; s += 4 * WF_WAVES) {
+      a0 += p.ws[s * MN + e];
+      a1 += p.ws[(s + WF_WAVES) * MN + e];
+      a2 += p.ws[(s + 2 * WF_WAVES) * MN + e];
+      a3 += p.ws[(s + 3 * WF_WAVES) * MN + e];
+    }
+    for (; s < S; s += WF_WAVES) a0 += p.ws[s * MN + e];
+  }
+  red[w][lane] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  if (w == 0 && e < MN) {
+    float v = 0.f;
+#pragma unroll
+    for (int i = 0; i < WF_WAVES; ++i) v += red[i][lane];
+    v *= p.alpha;
+    const int64_t m = e / p.N, n = e - m * p.N;
+    if (n == p.ones_col)
+      p.ones_out[m] += v;
+    else
+      p.C[m * p.sCm + n * p.sCn] += v;
+  }
+}
+
+struct WrPick { int mbw, nbw, wm, wn; };
+
+// per-wave block counts among the compiled instances (3,2) (3,3) (3,4) (3,6) (6,3), 8 waves
+bool wr_pick(int64_t M, int64_t Ncols, WrPick& w) {
+  const int64_t Mb = ceil_div(M, 16), Nb = ceil_div(Ncols, 16);
+  static const int shapes[5][2] = {{3, 2}, {3, 3}, {3, 4}, {3, 6}, {6, 3}};
+  static const int grids[4][2] = {{1, 8}, {2, 4}, {4, 2}, {8, 1}};
+  int best = 1 << 30;
+  for (auto& gr : grids)
+    for (auto& sh : shapes) {
+      if ((int64_t)sh[0] * gr[0] < Mb || (int64_t)sh[1] * gr[1] < Nb) continue;
+      const int cost = sh[0] * sh[1] * 4 + (sh[0] + sh[1]);   // MFMA slots (incl. padding) + fragment reads
+      if (cost < best) {
+        best = cost;
+        w = {sh[0], sh[1], gr[0], gr[1]};
+      }
+    }
+  return best < (1 << 30);
+}
+
+int env_i(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+
+struct WrPlan {
+  WrPick w;
+  WrGeo g;
+  int64_t S, slices;
+  size_t lds;
+  int upt;
+};
+
+bool wr_plan(const GemmP& p, int amode, int bmode, int64_t batch, WrPlan& pl) {
+  static const int enabled = env_i("KDFM_WGR", 1);
+  if (!enabled) return false;
+  if (batch != 1 || p.epi != KDFM_EPI_ATOMIC || amode != KDFM_LD_XC) return false;
+  if (bmode != KDFM_LD_XC && bmode != KDFM_LD_CONV) return false;
+  if (p.sAm != 1 || (p.sAk & 3) || (p.M & 3) || (((uintptr_t)p.A) & 15)) return false;
+  if (p.sBn != 1 || (p.sBk & 3) || (((uintptr_t)p.B) & 15)) return false;
+  if (p.ones_col >= 0 && p.ones_col != p.N - 1) return false;
+  const int64_t nmem = p.ones_col >= 0 ? p.ones_col : p.N;
+  if (nmem & 3) return false;
+  if (bmode == KDFM_LD_CONV && ((p.conv_c & 3) || p.taps < 1 || p.pad < 0 || nmem != p.taps * p.conv_c)) return false;
+  static const int min_k = env_i("KDFM_WGR_MINK", 2048);
+  if (p.K < min_k) return false;
+  // column slices of at most 24 16-wide blocks (a (6,3) wave tile on a 1x8 wave grid)
+  const int64_t Nb_all = ceil_div(p.N, 16);
+  pl.slices = ceil_div(Nb_all, 24);
+  const int64_t ncols_slice = ceil_div(Nb_all, pl.slices) * 16;
+  if (!wr_pick(p.M, ncols_slice, pl.w)) return false;
+  pl.g.wm = pl.w.wm;
+  pl.g.wn = pl.w.wn;
+  pl.g.Ma = 16 * pl.w.mbw * pl.w.wm;
+  pl.g.Nb = 16 * pl.w.nbw * pl.w.wn;
+  pl.slices = ceil_div(p.N, pl.g.Nb);
+  pl.g.nmem = nmem;
+  // staging units per thread: the widest slice's slab
+  const int64_t units = 8 * (p.M / 4 + (nmem < pl.g.Nb ? nmem : pl.g.Nb) / 4);
+  pl.upt = (int)ceil_div(units, WR_NT);
+  if (pl.upt > WR_MAXU) return false;
+  pl.lds = (size_t)2 * (pl.g.Ma + pl.g.Nb) * WR_LDK * sizeof(uint16_t);
+  if (pl.lds > 160 * 1024) return false;
+  const int64_t steps = ceil_div(p.K, 32);
+  static const int target = env_i("KDFM_WGR_WGS", 256);
+  static const int min_steps = env_i("KDFM_WGR_STEPS", 4);
+  int64_t S = target / pl.slices;
+  if (S < 1) S = 1;
+  const int64_t smax = steps / min_steps > 0 ? steps / min_steps : 1;
+  if (S > smax) S = smax;
+  pl.g.steps_per = ceil_div(steps, S);
+  pl.S = ceil_div(steps, pl.g.steps_per);
+  return true;
+}
+
+template <int MBW, int NBW, bool CONV>
+int wr_launch(const GemmP& p, const WrPlan& pl, hipStream_t st) {
+  static const int pd = env_i("KDFM_WGR_PD", 2);
+  auto go = [&](auto kern) {
+    static bool once = [&] {
+      return hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) ==
+             hipSuccess;
+    }();
+    (void)once;
+    hipLaunchKernelGGL(kern, dim3((unsigned)pl.S, (unsigned)pl.slices), dim3(WR_NT), pl.lds, st, p, pl.g);
+  };
+  if (pl.upt <= 1) {
+    if (pd >= 2) go(wgr_kernel<MBW, NBW, CONV, 2, 1>); else go(wgr_kernel<MBW, NBW, CONV, 1, 1>);
+  } else {
+    // two slabs of two units each next to an 18-block accumulator tile exceed the 256 registers of
+    // a 2-waves-per-SIMD wave (spills): one slab in flight there
+    if (pd >= 2 && MBW * NBW < 18) go(wgr_kernel<MBW, NBW, CONV, 2, 2>); else go(wgr_kernel<MBW, NBW, CONV, 1, 2>);
+  }
+  return check_launch("kdfm_gemm(wgrad rows)");
+}
+
+}  // namespace
+
+int64_t wgrad_rows_ws(const GemmP& p, int amode, int bmode, int64_t batch) {
+  GemmP q = p;
+  q.A = reinterpret_cast<const float*>(16);  // alignment checks only
+  q.B = reinterpret_cast<const float*>(16);
+  WrPlan pl;
+  if (!wr_plan(q, amode, bmode, batch, pl)) return 0;
+  return pl.S * p.M * p.N;
+}
+
+int try_wgrad_rows(const GemmP& p, int amode, int bmode, int64_t batch, hipStream_t st) {
+  WrPlan pl;
+  if (!p.ws || !wr_plan(p, amode, bmode, batch, pl)) return -1;
+  if (p.ws_len < pl.S * p.M * p.N) return -1;
+  int rc;
+  const int key = pl.w.mbw * 10 + pl.w.nbw;
+  if (bmode == KDFM_LD_CONV) {
+    switch (key) {
+      case 32: rc = wr_launch<3, 2, true>(p, pl, st); break;
+      case 33: rc = wr_launch<3, 3, true>(p, pl, st); break;
+      case 34: rc = wr_launch<3, 4, true>(p, pl, st); break;
+      case 36: rc = wr_launch<3, 6, true>(p, pl, st); break;
+      default: rc = wr_launch<6, 3, true>(p, pl, st); break;
+    }
+  } else {
+    switch (key) {
+      case 32: rc = wr_launch<3, 2, false>(p, pl, st); break;
+      case 33: rc = wr_launch<3, 3, false>(p, pl, st); break;
+      case 34: rc = wr_launch<3, 4, false>(p, pl, st); break;
+      case 36: rc = wr_launch<3, 6, false>(p, pl, st); break;
+      default: rc = wr_launch<6, 3, false>(p, pl, st); break;
+    }
+  }
+  if (rc) return rc;
+  hipLaunchKernelGGL(wgr_fold_kernel, dim3((unsigned)ceil_div(p.M * p.N, 64)), dim3(64 * WF_WAVES), 0, st, p, pl.S);
+  return check_launch("kdfm_gemm(wgrad rows fold)");
+}
+
+}  // namespace kdfm

@@ -256,8 +256,28 @@ def layer_forward(cfg, S: EncoderShapes, P, L, li, x, out, pos_emb, lengths, *, 
     return ctx
 
 
+class LnGrads:
+    """The five LayerNorm backwards of one ConformerLayer write dgamma|dbeta block partials into
+    slots of one buffer and fold them with ONE launch at the end of the layer (kdfm_ln_fold)."""
+
+    def __init__(self, buf, rows, d):
+        self.buf, self.rows, self.d = buf, rows, d
+        self.n = K.layernorm_bwd_ws(rows, d)
+        self.pending = []
+
+    def bwd(self, dy, x, g, mean, rstd, dx, dg, db, dres=None):
+        part = self.buf[len(self.pending)][: self.n]
+        K.layernorm_bwd_part(dy, x, g, mean, rstd, dx, part, dres=dres)
+        self.pending.append((part, dg, db))
+
+    def fold(self):
+        if self.pending:
+            K.ln_fold(self.pending, self.rows, self.d)
+            self.pending = []
+
+
 def _ffn_backward(P, G, L, which, dres_out, ln, h, a, x_in_ln, m, r, norm, pd, seed, salt, li, site_act, site_out,
-                  dres_in, dev):
+                  dres_in, dev, lng=None):
     """Backward of r_out = r_in + 0.5*drop(W2 drop(silu(W1 LN(r_in)))) ; returns d r_in."""
     rows, d = dres_out.shape
     ff = h.shape[1]
@@ -273,23 +293,26 @@ def _ffn_backward(P, G, L, which, dres_out, ln, h, a, x_in_ln, m, r, norm, pd, s
     K.linear_dx(dh, P[L + which + ".linear1.weight"], dln)
     del dh
     dx = _empty(rows, d, dev=dev)
-    K.layernorm_bwd(dln, x_in_ln, P[norm + ".weight"], m, r, dx, G[norm + ".weight"], G[norm + ".bias"],
-                    dres=dres_in)
+    lng.bwd(dln, x_in_ln, P[norm + ".weight"], m, r, dx, G[norm + ".weight"], G[norm + ".bias"], dres=dres_in)
     return dx
 
 
-def layer_backward(cfg, S: EncoderShapes, P, G, L, li, ctx, dout, pos_emb, lengths, *, seed, salt):
+def layer_backward(cfg, S: EncoderShapes, P, G, L, li, ctx, dout, pos_emb, lengths, *, seed, salt, ln_buf=None):
     """dout: grad wrt the layer output (rows, d). Returns grad wrt the layer input."""
     dev = dout.device
     rows, d, H, dk, T, B = S.rows, S.d, S.h, S.dk, S.T, S.B
     pd = ctx["pd"]
+    if ln_buf is None:
+        ln_buf = torch.empty(5, K.layernorm_bwd_ws(rows, d), device=dev)
+    lng = LnGrads(ln_buf, rows, d)
     # norm_out
     dx4 = _empty(rows, d, dev=dev)
-    K.layernorm_bwd(dout, ctx["x4"], P[L + "norm_out.weight"], ctx["m5"], ctx["r5"], dx4, G[L + "norm_out.weight"],
-                    G[L + "norm_out.bias"])
+    lng.bwd(dout, ctx["x4"], P[L + "norm_out.weight"], ctx["m5"], ctx["r5"], dx4, G[L + "norm_out.weight"],
+            G[L + "norm_out.bias"])
     # FFN2: x4 = x3 + 0.5 drop(ffn(LN4 x3))
     dx3 = _ffn_backward(P, G, L, "feed_forward2", dx4, ctx["ln4"], ctx["h2"], ctx["a2"], ctx["x3"], ctx["m4"],
-                        ctx["r4"], L + "norm_feed_forward2", pd, seed, salt, li, SITE_FF2_ACT, SITE_FF2_OUT, dx4, dev)
+                        ctx["r4"], L + "norm_feed_forward2", pd, seed, salt, li, SITE_FF2_ACT, SITE_FF2_OUT, dx4, dev,
+                        lng)
     del dx4
     # conv module: x3 = x2 + drop(pw2(z))
     dpw2 = _empty(rows, d, dev=dev)
@@ -317,8 +340,8 @@ def layer_backward(cfg, S: EncoderShapes, P, G, L, li, ctx, dout, pos_emb, lengt
     K.linear_dx(da, P[L + "conv.pointwise_conv1.weight"].view(2 * d, d), dln3)
     del da
     dx2 = _empty(rows, d, dev=dev)
-    K.layernorm_bwd(dln3, ctx["x2"], P[L + "norm_conv.weight"], ctx["m3"], ctx["r3"], dx2, G[L + "norm_conv.weight"],
-                    G[L + "norm_conv.bias"], dres=dx3)
+    lng.bwd(dln3, ctx["x2"], P[L + "norm_conv.weight"], ctx["m3"], ctx["r3"], dx2, G[L + "norm_conv.weight"],
+            G[L + "norm_conv.bias"], dres=dx3)
     del dln3, dx3
     # MHSA: x2 = x1 + drop(out(O))
     dlo = _empty(rows, d, dev=dev)
@@ -371,12 +394,14 @@ def layer_backward(cfg, S: EncoderShapes, P, G, L, li, ctx, dout, pos_emb, lengt
     K.linear_dx(dqkv, P[L + "self_attn.qkv.weight"], dln2)
     del dqkv
     dx1 = _empty(rows, d, dev=dev)
-    K.layernorm_bwd(dln2, ctx["x1"], P[L + "norm_self_att.weight"], ctx["m2"], ctx["r2"], dx1,
-                    G[L + "norm_self_att.weight"], G[L + "norm_self_att.bias"], dres=dx2)
+    lng.bwd(dln2, ctx["x1"], P[L + "norm_self_att.weight"], ctx["m2"], ctx["r2"], dx1,
+            G[L + "norm_self_att.weight"], G[L + "norm_self_att.bias"], dres=dx2)
     del dln2, dx2
     # FFN1
     dx = _ffn_backward(P, G, L, "feed_forward1", dx1, ctx["ln1"], ctx["h1"], ctx["a1"], ctx["x"], ctx["m1"],
-                       ctx["r1"], L + "norm_feed_forward1", pd, seed, salt, li, SITE_FF1_ACT, SITE_FF1_OUT, dx1, dev)
+                       ctx["r1"], L + "norm_feed_forward1", pd, seed, salt, li, SITE_FF1_ACT, SITE_FF1_OUT, dx1, dev,
+                       lng)
+    lng.fold()   # the layer's five dgamma/dbeta folds in one launch
     return dx
 
 
@@ -419,9 +444,12 @@ def encoder_backward(cfg, S: EncoderShapes, P, G, prefix, run: EncoderRun, dfeat
     the residual chain as the backward walks down the stack.  on_layer_done(i) is called once layer
     i's parameter gradients are all issued (bucketed all-reduce overlap, kdfm/ddp.py)."""
     dout = dfeats[cfg.n_layers - 1]
+    if "ln_parts" not in ws:
+        ws["ln_parts"] = torch.empty(5, K.layernorm_bwd_ws(S.rows, S.d), device=dfeats.device)
     for i in range(cfg.n_layers - 1, -1, -1):
         L = f"{prefix}layers.{i}."
-        dx = layer_backward(cfg, S, P, G, L, i, run.layers[i], dout, pos_emb, len2, seed=seed, salt=salt)
+        dx = layer_backward(cfg, S, P, G, L, i, run.layers[i], dout, pos_emb, len2, seed=seed, salt=salt,
+                            ln_buf=ws["ln_parts"])
         run.layers[i] = None
         if on_layer_done is not None:
             on_layer_done(i)

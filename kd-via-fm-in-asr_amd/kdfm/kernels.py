@@ -547,6 +547,31 @@ def layernorm_bwd(dy, x, g, mean, rstd, dx, dg, db, dres=None):
          ptr(ws), rows, d, _s())
 
 
+def layernorm_bwd_ws(rows, d):
+    return int(_lib.lib().kdfm_layernorm_bwd_ws(rows, d))
+
+
+def layernorm_bwd_part(dy, x, g, mean, rstd, dx, part, dres=None):
+    """LayerNorm backward with the dgamma/dbeta fold deferred to ln_fold (part: >= layernorm_bwd_ws
+    floats, kept until the fold)."""
+    rows, d = x.shape
+    assert dy.is_contiguous() and dx.is_contiguous() and (dres is None or dres.is_contiguous())
+    assert part.numel() >= layernorm_bwd_ws(rows, d)
+    call("kdfm_layernorm_bwd_part", ptr(dy), ptr(x), ptr(g), ptr(mean), ptr(rstd), ptr(dres), ptr(dx), ptr(part),
+         rows, d, _s())
+
+
+def ln_fold(entries, rows, d):
+    """entries: [(part, dgamma, dbeta)] (<= 8) of LayerNorms over the same (rows, d): one launch."""
+    n = len(entries)
+    arr = C.c_void_p * n
+    parts = arr(*[ptr(e[0]) for e in entries])
+    dgs = arr(*[ptr(e[1]) for e in entries])
+    dbs = arr(*[ptr(e[2]) for e in entries])
+    call("kdfm_ln_fold", C.cast(parts, C.POINTER(C.c_void_p)), C.cast(dgs, C.POINTER(C.c_void_p)),
+         C.cast(dbs, C.POINTER(C.c_void_p)), n, rows, d, _s())
+
+
 def qkv_prep(qkv, u, v, qu, qv):
     rows, d = qu.shape
     assert qkv.shape == (rows, 3 * d) and u.numel() == d and v.numel() == d

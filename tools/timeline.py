@@ -1,7 +1,9 @@
 """Per-stream busy time and critical-path view of one training step from a rocprofv3 kernel trace
-(--kernel-trace --output-format csv).  usage: python tools/timeline.py <kernel_trace.csv> [steps]
+(--kernel-trace, rocpd .db or --output-format csv).
+usage: python tools/timeline.py <run_results.db | kernel_trace.csv>
 Steps are delimited by the CTC kernel (one launch per step); the last full step is analysed."""
 import csv
+import sqlite3
 import sys
 from collections import defaultdict
 
@@ -9,11 +11,16 @@ from collections import defaultdict
 def main():
     path = sys.argv[1]
     rows = []
-    with open(path) as fh:
-        for r in csv.DictReader(fh):
-            sid = r.get("Stream_Id") or r.get("Queue_Id") or "0"
-            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), sid,
-                         r["Kernel_Name"].replace("kdfm::(anonymous namespace)::", "").split("(")[0]))
+    clean = lambda n: n.replace("kdfm::(anonymous namespace)::", "").split("(")[0]
+    if path.endswith(".db"):
+        c = sqlite3.connect(path)
+        for name, st, en, sid, qid in c.execute("select name, start, end, stream_id, queue_id from kernels"):
+            rows.append((int(st), int(en), str(sid if sid is not None else qid), clean(name)))
+    else:
+        with open(path) as fh:
+            for r in csv.DictReader(fh):
+                sid = r.get("Stream_Id") or r.get("Queue_Id") or "0"
+                rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), sid, clean(r["Kernel_Name"])))
     rows.sort()
     # step boundaries: the adamw kernel ends every step
     ends = [e for s, e, q, n in rows if n.startswith("adamw_kernel") or "adamw_kernel" in n]
