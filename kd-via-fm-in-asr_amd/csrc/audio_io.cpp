@@ -257,17 +257,21 @@ int flac_subframe(BitReader& br, int bs, int bps, int64_t* x, std::vector<int64_
     for (int i = 0; i < order; ++i) x[i] = br.sget(sb);
     int rc = flac_residual(br, bs, order, res.data());
     if (rc) return rc;
+    // predictions in wrapping 64-bit arithmetic: a corrupt frame (rejected by its CRC-16 only
+    // after the subframes are decoded) must not overflow a signed integer
     const int64_t* r = res.data();
+    auto u = [](int64_t v) { return (uint64_t)v; };
     switch (order) {
       case 0: for (int i = 0; i < bs; ++i) x[i] = r[i]; break;
-      case 1: for (int i = 1; i < bs; ++i) x[i] = r[i - 1] + x[i - 1]; break;
-      case 2: for (int i = 2; i < bs; ++i) x[i] = r[i - 2] + 2 * x[i - 1] - x[i - 2]; break;
+      case 1: for (int i = 1; i < bs; ++i) x[i] = (int64_t)(u(r[i - 1]) + u(x[i - 1])); break;
+      case 2: for (int i = 2; i < bs; ++i) x[i] = (int64_t)(u(r[i - 2]) + 2 * u(x[i - 1]) - u(x[i - 2])); break;
       case 3:
-        for (int i = 3; i < bs; ++i) x[i] = r[i - 3] + 3 * x[i - 1] - 3 * x[i - 2] + x[i - 3];
+        for (int i = 3; i < bs; ++i)
+          x[i] = (int64_t)(u(r[i - 3]) + 3 * u(x[i - 1]) - 3 * u(x[i - 2]) + u(x[i - 3]));
         break;
       case 4:
         for (int i = 4; i < bs; ++i)
-          x[i] = r[i - 4] + 4 * x[i - 1] - 6 * x[i - 2] + 4 * x[i - 3] - x[i - 4];
+          x[i] = (int64_t)(u(r[i - 4]) + 4 * u(x[i - 1]) - 6 * u(x[i - 2]) + 4 * u(x[i - 3]) - u(x[i - 4]));
         break;
     }
   } else if (type >= 32) {
@@ -284,9 +288,9 @@ int flac_subframe(BitReader& br, int bs, int bps, int64_t* x, std::vector<int64_
     if (rc) return rc;
     const int64_t* r = res.data();
     for (int i = order; i < bs; ++i) {
-      int64_t acc = 0;
-      for (int j = 0; j < order; ++j) acc += coef[j] * x[i - 1 - j];
-      x[i] = r[i - order] + (acc >> shift);
+      uint64_t acc = 0;  // wrapping, as above; exact for any valid stream
+      for (int j = 0; j < order; ++j) acc += (uint64_t)coef[j] * (uint64_t)x[i - 1 - j];
+      x[i] = (int64_t)((uint64_t)r[i - order] + (uint64_t)((int64_t)acc >> shift));
     }
   } else {
     return fail(KDFM_IO_ERR_CORRUPT, "reserved subframe type");
@@ -382,15 +386,15 @@ int flac_decode(const std::vector<uint8_t>& b, Sink& sink, int32_t* rate_out) {
     int64_t* c0p = chan.data();
     int64_t* c1p = chan.data() + 65536;
     if (ch_code == 8) {
-      for (int i = 0; i < bs; ++i) c1p[i] = c0p[i] - c1p[i];
+      for (int i = 0; i < bs; ++i) c1p[i] = (int64_t)((uint64_t)c0p[i] - (uint64_t)c1p[i]);
     } else if (ch_code == 9) {
-      for (int i = 0; i < bs; ++i) c0p[i] = c0p[i] + c1p[i];
+      for (int i = 0; i < bs; ++i) c0p[i] = (int64_t)((uint64_t)c0p[i] + (uint64_t)c1p[i]);
     } else if (ch_code == 10) {
       for (int i = 0; i < bs; ++i) {
         int64_t side = c1p[i];
         int64_t mid = (int64_t)((uint64_t)c0p[i] << 1) | (side & 1);
-        c0p[i] = (mid + side) >> 1;
-        c1p[i] = (mid - side) >> 1;
+        c0p[i] = (int64_t)((uint64_t)mid + (uint64_t)side) >> 1;
+        c1p[i] = (int64_t)((uint64_t)mid - (uint64_t)side) >> 1;
       }
     }
     const float scale = 1.0f / (float)(1ull << (bps - 1));
