@@ -50,6 +50,13 @@ int kdfm_device_arch(char* buf, int64_t len); /* writes the gcnArchName of the c
 void kdfm_set_deterministic(int32_t on);
 int32_t kdfm_get_deterministic(void);
 
+/* Tracing (the reference's Lightning profiler / NVTX ranges): a ROCTx range on the
+ * calling host thread, seen by `rocprofv3 --marker-trace` next to the kernels it enqueued.
+ * push returns the 0-based nesting level of the range it opened; pop returns the level of the range
+ * it closed (negative if none was open). */
+int32_t kdfm_range_push(const char* name);
+int32_t kdfm_range_pop(void);
+
 /* --------------------------------------------------------------------------------------------
  * Generic batched GEMM with fused epilogue:
  *   C[b](m,n) = epi( alpha * sum_k A[b](m,k) * B[b](k,n) )
@@ -142,7 +149,8 @@ int kdfm_cast_bf16_t(const float* src, uint16_t* dst, const int64_t* table, int6
 int64_t kdfm_gemm_ws(const kdfm_gemm_desc* d); /* workspace elements kdfm_gemm would use (0: none) */
 /* kernel family the calling thread's most recent kdfm_gemm launched (profiling attribution):
  * 0 generic 64x64 MFMA tile, 1 weight-stationary skinny, 2 row-streaming forward, 3 wide-tile
- * weight gradient + fold, 4 generic tile with ordered split-K fold, 5 LDS-slab k=3 conv; -1 none */
+ * weight gradient + fold, 4 generic tile with ordered split-K fold, 5 LDS-slab k=3 conv,
+ * 6 row-parallel weight gradient + ordered fold; -1 none */
 int32_t kdfm_gemm_last_route(void);
 
 /* column sums: out[n] (+)= scale * sum_m X[m*ld + n], m < M; accumulate != 0 adds into out.

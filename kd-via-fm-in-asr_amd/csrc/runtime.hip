@@ -2,6 +2,8 @@
 #include <cstring>
 #include <string>
 
+#include <rocprofiler-sdk-roctx/roctx.h>
+
 #include "common.h"
 
 namespace kdfm {
@@ -82,6 +84,10 @@ void kdfm_set_deterministic(int32_t on) { kdfm::g_deterministic = on ? 1 : 0; }
 int32_t kdfm_get_deterministic(void) { return kdfm::g_deterministic; }
 
 int32_t kdfm_gemm_last_route(void) { return kdfm::g_route; }
+
+int32_t kdfm_range_push(const char* name) { return roctxRangePushA(name ? name : "kdfm"); }
+
+int32_t kdfm_range_pop(void) { return roctxRangePop(); }
 
 int kdfm_device_arch(char* buf, int64_t len) {
   KDFM_REQUIRE(buf && len > 0, "null buffer");

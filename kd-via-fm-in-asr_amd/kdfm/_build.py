@@ -79,7 +79,8 @@ def build(verbose: bool = False, jobs: int | None = None) -> str:
                     print("compiled", os.path.basename(o))
     lib_mtime = os.path.getmtime(LIB_PATH) if os.path.exists(LIB_PATH) else -1.0
     if todo or lib_mtime < max(os.path.getmtime(o) for o in objs):
-        cmd = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", LIB_PATH, *objs]
+        cmd = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", LIB_PATH, *objs, "-L/opt/rocm/lib",
+               "-Wl,-rpath,/opt/rocm/lib", "-lrocprofiler-sdk-roctx"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr[-6000:]}")

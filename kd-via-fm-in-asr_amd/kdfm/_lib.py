@@ -72,6 +72,8 @@ SIGNATURES: dict[str, tuple] = {
     "kdfm_gemm": (_i32, [C.POINTER(GemmDesc), P]),
     "kdfm_gemm_ws": (_i64, [C.POINTER(GemmDesc)]),
     "kdfm_gemm_last_route": (_i32, []),
+    "kdfm_range_push": (_i32, [C.c_char_p]),
+    "kdfm_range_pop": (_i32, []),
     "kdfm_cast_bf16": (_i32, [P, P, _i64, P]),
     "kdfm_cast_bf16_t": (_i32, [P, P, P, _i64, _i64, P]),
     "kdfm_colsum": (_i32, [P, P, _i64, _i64, _i64, _f32, _i32, P]),

@@ -97,7 +97,7 @@ class Ver5Engine:
     def forward(self, wav, wav_len, targets, tgt_len, *, train=True, eps=None, save=True):
         """One forward pass; returns the context backward() consumes.  eps: optional injected
         NoiseAdapter noise (n_layers*B*T', latent) for parity runs."""
-        with self._mode():
+        with self._mode(), K.region("forward"):
             return self._forward(wav, wav_len, targets, tgt_len, train=train, eps=eps, save=save)
 
     def _forward(self, wav, wav_len, targets, tgt_len, *, train, eps, save):
@@ -139,7 +139,7 @@ class Ver5Engine:
         main = torch.cuda.current_stream(dev)
         side = self._side_stream()
         side.wait_stream(main)
-        with torch.cuda.stream(side):
+        with torch.cuda.stream(side), K.region("teacher_encoder"):
             encoder_forward(cfg, St, self.teacher.P, "teacher.encoder.", mel_t, mel_len, len1, len2, tfeats,
                             pos_t, train=False, seed=seed, salt=SALT_TEACHER, save=False,
                             bn_running=self.bn.P, use_batch_stats=False, ws=self._enc_ws(St))
@@ -150,9 +150,10 @@ class Ver5Engine:
         # ---- student encoder (saved for backward) ----
         sfeats = torch.empty(cfg.n_layers, Ss.rows, Ss.d, device=dev)
         pos_s = self._pos_emb(T, Ss.d)
-        srun = encoder_forward(cfg, Ss, self.student.P, "encoder.", mel_s, mel_len, len1, len2, sfeats, pos_s,
-                               train=train, seed=seed, salt=SALT_STUDENT, save=save, bn_running=self.bn.P,
-                               use_batch_stats=train, ws=self._enc_ws(Ss))
+        with K.region("student_encoder"):
+            srun = encoder_forward(cfg, Ss, self.student.P, "encoder.", mel_s, mel_len, len1, len2, sfeats, pos_s,
+                                   train=train, seed=seed, salt=SALT_STUDENT, save=save, bn_running=self.bn.P,
+                                   use_batch_stats=train, ws=self._enc_ws(Ss))
         # ---- decoders, CTC, logit KD ----
         logits = torch.empty(rows, Cn, device=dev)
         K.linear(sfeats[-1], self.student.P["decoder.decoder_layers.0.weight"].view(Cn, Ss.d),
@@ -168,7 +169,7 @@ class Ver5Engine:
         Umax = targets.shape[1]
         nll = torch.empty(B, device=dev)
         glogits = torch.empty(rows, Cn, device=dev)
-        with torch.cuda.stream(aux):
+        with torch.cuda.stream(aux), K.region("ctc_kl"):
             alpha_ws = torch.empty(B * T * (2 * Umax + 1), device=dev)
             beta_ws = torch.empty_like(alpha_ws)
             K.ctc_loss(lp, targets, len2, tgt_len, alpha_ws, beta_ws, nll, glogits, B, T, Cn, cfg.vocab, 1.0 / B)
@@ -179,8 +180,9 @@ class Ver5Engine:
             t.record_stream(aux)
         # ---- ver5 heads over all layers at once ----
         n = cfg.n_layers * rows
-        hctx = heads_forward(cfg, self.student.P, sfeats.view(n, Ss.d), tfeats.view(n, St.d), T, self.hws, acc[1:3],
-                             seed=seed, eps=eps, save=save)
+        with K.region("heads_forward"):
+            hctx = heads_forward(cfg, self.student.P, sfeats.view(n, Ss.d), tfeats.view(n, St.d), T, self.hws,
+                                 acc[1:3], seed=seed, eps=eps, save=save)
         ctx = dict(B=B, T=T, Ss=Ss, St=St, mel_len=mel_len, len1=len1, len2=len2, srun=srun, sfeats=sfeats,
                    glogits=glogits, hctx=hctx, lp=lp, nll=nll, pos_s=pos_s, acc=acc)
         self._join_losses(ctx)   # CTC/KL overlapped the heads forward; losses valid after forward()
@@ -250,7 +252,7 @@ class Ver5Engine:
         index >= offset is final (BucketedGradAllReduce.ready overlap)."""
         # deterministic mode also keeps the weight-gradient products on the issuing stream: with the
         # side stream overlapping, repeated runs differed in ~1e-3 of some gradients (DESIGN.md §4)
-        with self._mode(), WGRAD.serialized(self.cfg.deterministic):
+        with self._mode(), WGRAD.serialized(self.cfg.deterministic), K.region("backward"):
             self._backward(ctx, grad_ready)
 
     def _backward(self, ctx, grad_ready):
@@ -261,7 +263,8 @@ class Ver5Engine:
         n = cfg.n_layers * Ss.rows
         self.student.zero_grad()
         dfeats = torch.empty(cfg.n_layers, Ss.rows, Ss.d, device=self.device)
-        heads_backward(cfg, P, G, ctx.pop("hctx"), self.hws, dfeats.view(n, Ss.d), seed=self.seed)
+        with K.region("heads_backward"):
+            heads_backward(cfg, P, G, ctx.pop("hctx"), self.hws, dfeats.view(n, Ss.d), seed=self.seed)
         dec0 = off["decoder.decoder_layers.0.weight"]
         if grad_ready is not None:
             grad_ready(min(o for k, o in off.items() if not k.startswith(("encoder.", "decoder."))))
@@ -278,12 +281,13 @@ class Ver5Engine:
             firsts = {i: min(o for k, o in off.items() if k.startswith(f"encoder.layers.{i}."))
                       for i in range(cfg.n_layers)}
             layer_done = lambda i: grad_ready(firsts[i])  # noqa: E731
-        encoder_backward(cfg, Ss, P, G, "encoder.", ctx.pop("srun"), dfeats, ctx["pos_s"], ctx["len1"],
-                         ctx["len2"], seed=self.seed, salt=SALT_STUDENT, ws=self._enc_ws(Ss),
-                         on_layer_done=layer_done)
+        with K.region("encoder_backward"):
+            encoder_backward(cfg, Ss, P, G, "encoder.", ctx.pop("srun"), dfeats, ctx["pos_s"], ctx["len1"],
+                             ctx["len2"], seed=self.seed, salt=SALT_STUDENT, ws=self._enc_ws(Ss),
+                             on_layer_done=layer_done)
 
     def optimizer_step(self, grad_scale: float = 1.0):
-        with self._mode():
+        with self._mode(), K.region("optimizer"):
             self._optimizer_step(grad_scale)
 
     def _optimizer_step(self, grad_scale):
@@ -307,7 +311,8 @@ class Ver5Engine:
         del ctx
         scale = 1.0
         if allreduce is not None:
-            scale = allreduce(self.student.grad)
+            with K.region("allreduce"):
+                scale = allreduce(self.student.grad)
         self.optimizer_step(scale)
         return self.losses
 

@@ -8,6 +8,7 @@ instead of faulting on the device.
 from __future__ import annotations
 
 import ctypes as C
+import os
 
 import torch
 
@@ -20,6 +21,7 @@ _MATH = {"f32": _lib.KDFM_MATH_F32, "bf16": _lib.KDFM_MATH_BF16}
 class _State:
     math = "f32"
     deterministic = False
+    ranges = os.environ.get("KDFM_ROCTX", "0") == "1"   # ROCTx ranges around engine phases
 
 
 ROUTES = {0: "generic", 1: "skinny", 2: "rowstream_fwd", 3: "wide_wgrad", 4: "split_fold", 5: "slab_conv",
@@ -61,15 +63,43 @@ class Trace:
                 for k, v in out.items()}
 
 
-class span:
+def set_ranges(on: bool) -> None:
+    """Emit ROCTx ranges (kdfm_range_push/pop) around the engine's phases and every span(); env
+    KDFM_ROCTX=1 sets it at import.  rocprofv3 --marker-trace records them with the kernels."""
+    _State.ranges = bool(on)
+
+
+class region:
+    """Context manager: one ROCTx range named `name` on this host thread when ranges are on."""
+    __slots__ = ("name", "on")
+
+    def __init__(self, name):
+        self.name = name
+        self.on = False
+
+    def __enter__(self):
+        if _State.ranges:
+            _lib.lib().kdfm_range_push(("kdfm:" + self.name).encode())
+            self.on = True
+        return self
+
+    def __exit__(self, *a):
+        if self.on:
+            _lib.lib().kdfm_range_pop()
+
+
+class span(region):
     """Context manager: time the enclosed launches (one stream) as one record of `tag` when the
-    active Trace asks for it."""
+    active Trace asks for it (and a ROCTx range of the same name when ranges are on)."""
+    __slots__ = ("tag", "nbytes", "flops", "ev")
 
     def __init__(self, tag, nbytes=0.0, flops=0.0):
+        super().__init__(tag)
         self.tag, self.nbytes, self.flops = tag, nbytes, flops
         self.ev = None
 
     def __enter__(self):
+        super().__enter__()
         tr = Trace.active
         if tr is not None and self.tag in tr.tags:
             self.ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -80,6 +110,7 @@ class span:
         if self.ev is not None:
             self.ev[1].record()
             Trace.active.events.append((self.tag, self.flops, self.nbytes, self.ev[0], self.ev[1]))
+        super().__exit__(*a)
 
 
 def set_math(mode: str) -> None:

@@ -54,3 +54,23 @@ def test_kernels_refuse_cpu_tensors():
     x = torch.zeros(4, 4)
     with pytest.raises(_lib.KdfmError):
         kernels.fill(x, 1.0)
+
+
+def test_roctx_ranges_nest_without_a_gpu():
+    """kdfm_range_push/pop (SURVEY.md §5 tracing) are host-only ROCTx calls: usable with no device,
+    nesting levels as documented in include/kdfm.h, and the engine's region() wrapper balanced."""
+    from kdfm import _lib
+    from kdfm import kernels as K
+    L = _lib.lib()
+    assert L.kdfm_range_push(b"kdfm:test-outer") == 0
+    assert L.kdfm_range_push(b"kdfm:test-inner") == 1
+    assert L.kdfm_range_pop() == 1
+    assert L.kdfm_range_pop() == 0
+    assert L.kdfm_range_pop() < 0
+    K.set_ranges(True)
+    try:
+        with K.region("a"), K.region("b"):
+            pass
+    finally:
+        K.set_ranges(False)
+    assert L.kdfm_range_pop() < 0   # region() closed everything it opened
