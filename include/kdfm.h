@@ -189,6 +189,35 @@ int kdfm_col2im_3x3s2(const float* dcols, const int64_t* len_in, const float* re
 int kdfm_col2im_3x3s2_tapmajor(const float* dcols, const int64_t* len_in, const float* relu_out, float* dX, int64_t B,
                       int64_t T1, int64_t F1, int64_t C, void* stream);
 
+/* ---------------- ConvSubsampling 'dw_striding' (conformer_encoder.py:381-390; recipe
+ * fast-conformer_ctc_bpe.yaml:122-125): Conv2d(1->C,3,s2)+ReLU, then per further stage a depthwise
+ * Conv2d(C,3,s2,groups=C) + pointwise 1x1 (kdfm_gemm, EPI_BIAS|RELU|ROWMASK) + ReLU; NeMo's masked
+ * conv sequence zeroes frames >= each layer's length before and after it.  Activations
+ * channels-last (B, T, F, C), C % 4 == 0, 16-byte aligned; weights (C, 1, 3, 3), bias (C).
+ * Padding (pad_t, pad_f) = left padding of both axes (1 symmetric, 2 for CausalConv2D). */
+/* out[i] = floor((in[i] + pad_total - kernel) / stride) + 1 (NeMo calc_length, one stage) */
+int kdfm_conv_lengths(const int64_t* in, int64_t* out, int64_t n, int32_t pad_total, int32_t kernel, int32_t stride,
+                      void* stream);
+/* y[b,to,fo,c] = mask(to < out_len[b]) * act(bias[c] + sum_{i,j} w[c,i,j] * x[b, 2to-pad_t+i, 2fo-pad_f+j, Cin==1 ? 0 : c])
+ * with x frames >= in_len[b] (and outside the input) read as zero; act = relu when relu != 0.
+ * in_len / out_len may be NULL (no mask). */
+int kdfm_dwsub_conv(const float* x, const int64_t* in_len, const float* w, const float* bias, float* y,
+                    const int64_t* out_len, int64_t B, int64_t Ti, int64_t Fi, int64_t Cin, int64_t C, int64_t To,
+                    int64_t Fo, int32_t pad_t, int32_t pad_f, int32_t relu, void* stream);
+/* data gradient of the depthwise layer (Cin == C): dx = adjoint(dy masked at out_len), times
+ * relu'(x_saved) when x_saved != NULL (the layer's input was a ReLU output), zero at ti >= in_len. */
+int kdfm_dwsub_conv_dgrad(const float* dy, const int64_t* out_len, const float* w, const float* x_saved,
+                          const int64_t* in_len, float* dx, int64_t B, int64_t Ti, int64_t Fi, int64_t C, int64_t To,
+                          int64_t Fo, int32_t pad_t, int32_t pad_f, void* stream);
+/* weight and bias gradients dw (C,1,3,3), db (C) of kdfm_dwsub_conv (Cin 1 or C): per-slab partials
+ * in ws then an ordered fold (deterministic in every mode); accumulate != 0 adds into dw/db.
+ * kdfm_dwsub_conv_wgrad_ws gives the workspace size in floats. */
+int64_t kdfm_dwsub_conv_wgrad_ws(int64_t B, int64_t To, int64_t Fo, int64_t C);
+int kdfm_dwsub_conv_wgrad(const float* dy, const int64_t* out_len, const float* x, const int64_t* in_len, float* dw,
+                          float* db, float* ws, int64_t ws_len, int64_t B, int64_t Ti, int64_t Fi, int64_t Cin,
+                          int64_t C, int64_t To, int64_t Fo, int32_t pad_t, int32_t pad_f, int32_t accumulate,
+                          void* stream);
+
 /* Fused striding subsampling forward (bf16 MFMA mode; replaces im2col + GEMM for the same A.3
  * arithmetic, conformer_encoder.py:381-390, 635):
  *   kdfm_subsample_conv1: y1[(b,t1,f1), c] = mask(t1 < len1[b]) * relu(b0[c] + sum_tap w0[c,tap] *

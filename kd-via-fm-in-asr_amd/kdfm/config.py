@@ -48,6 +48,13 @@ class Ver5Config:
     dropout_pre: float = 0.1
     dropout_att: float = 0.1
     subsampling_mask: bool = True
+    # ConvSubsampling (conformer_encoder.py:371-390): "striding" (Conformer-CTC recipe, x4) or
+    # "dw_striding" (FastConformer recipe fast-conformer_ctc_bpe.yaml:122-125: x8, 256 channels)
+    subsampling: str = "striding"
+    subsampling_factor: int = 4
+    subsampling_conv_channels: int = -1   # -1: d_model
+    causal_downsampling: bool = False
+    xscaling: bool = True                 # x * sqrt(d_model) after subsampling (RelPositionalEncoding)
     bn_momentum: float = 0.1
     ln_eps: float = 1e-5
     bn_eps: float = 1e-5
@@ -79,16 +86,64 @@ class Ver5Config:
 # parameter buffer: q/k/v weights (and biases) are adjacent so one (3d, d) GEMM projects all three.
 # ------------------------------------------------------------------------------------------------
 
+def sub_stages(cfg: Ver5Config) -> int:
+    """Number of stride-2 stages of the subsampling module (log2 of the factor)."""
+    f = cfg.subsampling_factor
+    if f < 2 or f & (f - 1):
+        raise ValueError("subsampling_factor must be a power of 2")
+    if cfg.subsampling == "striding":
+        if f != 4 or cfg.causal_downsampling:
+            raise ValueError("'striding' subsampling is implemented for the Conformer-CTC recipe (x4, non-causal)")
+    elif cfg.subsampling != "dw_striding":
+        raise ValueError(f"subsampling {cfg.subsampling!r} is not on this path (striding | dw_striding)")
+    return f.bit_length() - 1
+
+
+def sub_pad(cfg: Ver5Config) -> tuple:
+    """(left, right) padding of every 3x3 stride-2 subsampling conv: 1/1, or CausalConv2D's 2/1."""
+    return (2, 1) if cfg.causal_downsampling else (1, 1)
+
+
+def sub_channels(cfg: Ver5Config, d: int) -> int:
+    return d if cfg.subsampling_conv_channels == -1 else cfg.subsampling_conv_channels
+
+
+def sub_len(cfg: Ver5Config, n: int) -> int:
+    """NeMo calc_length for one stage (host ints): floor((n + pl + pr - 3) / 2) + 1."""
+    pl, pr = sub_pad(cfg)
+    return (n + pl + pr - 3) // 2 + 1
+
+
+def sub_dims(cfg: Ver5Config, T_mel: int) -> list:
+    """[(T, F)] of the input and of every stage output."""
+    out = [(T_mel, cfg.nfilt)]
+    for _ in range(sub_stages(cfg)):
+        t, f = out[-1]
+        out.append((sub_len(cfg, t), sub_len(cfg, f)))
+    return out
+
+
+def subsampling_specs(cfg: Ver5Config, d: int, prefix: str) -> list:
+    C = sub_channels(cfg, d)
+    n = sub_stages(cfg)
+    Fo = sub_dims(cfg, 1)[-1][1]
+    p = prefix + "pre_encode."
+    if cfg.subsampling == "striding":
+        return [(p + "conv.0.weight", (C, 1, 3, 3)), (p + "conv.0.bias", (C,)),
+                (p + "conv.2.weight", (C, C, 3, 3)), (p + "conv.2.bias", (C,)),
+                (p + "out.weight", (d, C * Fo)), (p + "out.bias", (d,))]
+    s = [(p + "conv.0.weight", (C, 1, 3, 3)), (p + "conv.0.bias", (C,))]
+    for st in range(1, n):
+        i = 2 + 3 * (st - 1)     # nn.Sequential: conv, ReLU, [dw, pw, ReLU] x (stages - 1)
+        s += [(p + f"conv.{i}.weight", (C, 1, 3, 3)), (p + f"conv.{i}.bias", (C,)),
+              (p + f"conv.{i + 1}.weight", (C, C, 1, 1)), (p + f"conv.{i + 1}.bias", (C,))]
+    return s + [(p + "out.weight", (d, C * Fo)), (p + "out.bias", (d,))]
+
+
 def encoder_specs(cfg: Ver5Config, d: int, h: int, prefix: str) -> list:
-    C = d
-    F2 = cfg.nfilt // 4
     ff = cfg.ff_expansion * d
     dk = d // h
-    s = [
-        (prefix + "pre_encode.conv.0.weight", (C, 1, 3, 3)), (prefix + "pre_encode.conv.0.bias", (C,)),
-        (prefix + "pre_encode.conv.2.weight", (C, C, 3, 3)), (prefix + "pre_encode.conv.2.bias", (C,)),
-        (prefix + "pre_encode.out.weight", (d, C * F2)), (prefix + "pre_encode.out.bias", (d,)),
-    ]
+    s = subsampling_specs(cfg, d, prefix)
     for i in range(cfg.n_layers):
         L = f"{prefix}layers.{i}."
         s += [(L + "norm_feed_forward1.weight", (d,)), (L + "norm_feed_forward1.bias", (d,)),
@@ -173,5 +228,6 @@ def fused_groups(specs: list) -> dict:
 DEFAULT = Ver5Config()
 PARITY = DEFAULT.parity()
 
-__all__ = ["Ver5Config", "DEFAULT", "PARITY", "encoder_specs", "decoder_specs", "head_specs", "student_specs",
+__all__ = ["Ver5Config", "DEFAULT", "PARITY", "encoder_specs", "subsampling_specs", "sub_stages", "sub_pad",
+           "sub_channels", "sub_len", "sub_dims", "decoder_specs", "head_specs", "student_specs",
            "teacher_specs", "bn_buffer_specs", "fused_groups", "field"]

@@ -19,7 +19,7 @@ import torch
 from . import _lib
 from . import kernels as K
 from .overlap import WGRAD
-from .config import Ver5Config
+from .config import Ver5Config, sub_channels, sub_dims, sub_pad, sub_stages
 
 # dropout site ids (rng stream = model_salt * 4096 + layer * 16 + site)
 SITE_FF1_ACT, SITE_FF1_OUT, SITE_ATT_P, SITE_ATT_OUT, SITE_CONV_OUT, SITE_FF2_ACT, SITE_FF2_OUT = range(7)
@@ -34,12 +34,31 @@ class EncoderShapes:
     def __init__(self, cfg: Ver5Config, B: int, T_mel: int, d: int, h: int):
         self.B, self.Tm, self.d, self.h = B, T_mel, d, h
         self.dk = d // h
-        self.F1 = (cfg.nfilt - 1) // 2 + 1
-        self.T1 = (T_mel - 1) // 2 + 1
-        self.F2 = (self.F1 - 1) // 2 + 1
-        self.T = (self.T1 - 1) // 2 + 1
+        self.C = sub_channels(cfg, d)
+        self.stages = sub_dims(cfg, T_mel)      # [(T, F)] of the subsampling input and stage outputs
+        self.pad = sub_pad(cfg)[0]
+        self.T1, self.F1 = self.stages[1]
+        self.T, self.F2 = self.stages[-1]       # F2: features per frame at the subsampling output
         self.rows = B * self.T
         self.ff = cfg.ff_expansion * d
+
+
+def compute_lengths(cfg: Ver5Config, wav_len, mel_len, len1, len2, hop):
+    """Frame lengths of one batch: mel_len = L // hop, then the subsampling stages.  'striding':
+    len1 / len2 = after stage 1 / 2 (one kernel).  'dw_striding': len1 = (stages, B) lengths of every
+    stage output and len2 = its last row (a view), both returned."""
+    if cfg.subsampling == "striding":
+        K.subsample_lengths(wav_len, mel_len, len1, len2, hop)
+        return len1, len2
+    K.subsample_lengths(wav_len, mel_len, None, None, hop)
+    n = sub_stages(cfg)
+    lens = torch.empty(n, mel_len.numel(), dtype=torch.int64, device=mel_len.device)
+    pl, pr = sub_pad(cfg)
+    prev = mel_len
+    for s in range(n):
+        K.conv_lengths(prev, lens[s], pl + pr, 3, 2)
+        prev = lens[s]
+    return lens, lens[n - 1]
 
 
 def _empty(*shape, dev):
@@ -50,7 +69,102 @@ def _empty(*shape, dev):
 # Subsampling (A.3): im2col + MFMA GEMM, ReLU and frame masks fused into the epilogues.
 # ------------------------------------------------------------------------------------------------
 
+def _out_linear(cfg, S, P, pre, y, *, train, seed, salt, ws):
+    """Linear(C*F -> d) on the channels-last (f, c) flattening of the last stage (weight re-laid
+    out (d, F, C) on device), x*sqrt(d) and pre-encoder dropout fused."""
+    d, C = S.d, S.C
+    wout = ws["wout_perm"]
+    K.convw_prep(P[pre + "pre_encode.out.weight"].view(d, C, S.F2), fwd=wout)
+    xscale = math.sqrt(d) if cfg.xscaling else 1.0
+    bscaled = ws["bout_scaled"]
+    K.axpby(P[pre + "pre_encode.out.bias"].view(1, d), None, bscaled.view(1, d), alpha=xscale)
+    x = _empty(S.rows, d, dev=y.device)
+    p_pre = cfg.dropout_pre if train else 0.0
+    K.linear(y.view(S.rows, S.F2 * C), wout.view(d, S.F2 * C), bscaled, x, alpha=xscale, dropout_p=p_pre,
+             seed=seed, rng_stream=_stream(salt, -1, SITE_PRE))
+    return x, p_pre, xscale
+
+
+def _out_linear_backward(S, P, G, pre, ctx, dx, y, *, seed, salt, ws):
+    """-> gradient wrt the last stage's pre-activation (relu'(y) applied: y is a ReLU output)."""
+    d, C = S.d, S.C
+    dlin = _empty(S.rows, d, dev=dx.device)
+    K.dropout(dx, dlin, ctx["p_pre"], ctx["xscale"], seed, _stream(salt, -1, SITE_PRE))
+    Gout = ws["wout_perm_grad"]
+    K.fill(Gout, 0.0)
+    K.linear_dw(dlin, y.view(S.rows, S.F2 * C), Gout.view(d, S.F2 * C))
+    K.convw_grad(Gout, G[pre + "pre_encode.out.weight"].view(d, C, S.F2))
+    K.colsum(dlin, G[pre + "pre_encode.out.bias"])
+    g = _empty(y.shape[0], C, dev=dx.device)
+    K.linear_dx(dlin, ws["wout_perm"].view(d, S.F2 * C), g.view(S.rows, S.F2 * C), epi=_lib.EPI_DRELU,
+                aux=y.view(S.rows, S.F2 * C))
+    return g
+
+
+def dw_subsampling_forward(cfg, S: EncoderShapes, P, pre, mel, mel_len, lens, *, train, seed, salt, save, ws):
+    """ConvSubsampling 'dw_striding' (oracle/ver5.py subsampling_dw_striding): direct 3x3 stride-2
+    kernels (csrc/dwsub.hip) for the first conv and the depthwise convs, kdfm_gemm for the pointwise
+    1x1 convs (bias + ReLU + frame mask in the epilogue) and the output Linear."""
+    dev = mel.device
+    B, C = S.B, S.C
+    m = cfg.subsampling_mask
+    L = lambda s: (mel_len if s == 0 else lens[s - 1]) if m else None   # noqa: E731  (stage-s frame lengths)
+    T1, F1 = S.stages[1]
+    a = _empty(B * T1 * F1, C, dev=dev)
+    K.dwsub_conv(mel, L(0), P[pre + "pre_encode.conv.0.weight"], P[pre + "pre_encode.conv.0.bias"], a, L(1),
+                 B, S.Tm, cfg.nfilt, 1, C, T1, F1, S.pad, relu=True)
+    acts, dws = [a], []
+    for st in range(1, len(S.stages) - 1):
+        i = 2 + 3 * (st - 1)
+        (Ti, Fi), (To, Fo) = S.stages[st], S.stages[st + 1]
+        q = _empty(B * To * Fo, C, dev=dev)
+        K.dwsub_conv(a, L(st), P[pre + f"pre_encode.conv.{i}.weight"], P[pre + f"pre_encode.conv.{i}.bias"], q,
+                     L(st + 1), B, Ti, Fi, C, C, To, Fo, S.pad, relu=False)
+        a = _empty(B * To * Fo, C, dev=dev)
+        K.linear(q, P[pre + f"pre_encode.conv.{i + 1}.weight"].view(C, C), P[pre + f"pre_encode.conv.{i + 1}.bias"],
+                 a, epi=_lib.EPI_RELU, rowmask=(lens[st], To, Fo) if m else None)
+        dws.append(q)
+        acts.append(a)
+    x, p_pre, xscale = _out_linear(cfg, S, P, pre, a, train=train, seed=seed, salt=salt, ws=ws)
+    ctx = None
+    if save:
+        ctx = dict(acts=acts, dws=dws, p_pre=p_pre, xscale=xscale, mel=mel, mel_len=mel_len, lens=lens)
+    return x, ctx
+
+
+def dw_subsampling_backward(cfg, S: EncoderShapes, P, G, pre, ctx, dx, *, seed, salt, ws):
+    B, C = S.B, S.C
+    m = cfg.subsampling_mask
+    lens, mel_len = ctx["lens"], ctx["mel_len"]
+    L = lambda s: (mel_len if s == 0 else lens[s - 1]) if m else None   # noqa: E731
+    acts, dws = ctx["acts"], ctx["dws"]
+    g = _out_linear_backward(S, P, G, pre, ctx, dx, acts[-1], seed=seed, salt=salt, ws=ws)
+    for st in range(len(S.stages) - 2, 0, -1):
+        # g: gradient wrt the pre-activation of pointwise conv `st` (stage st+1 frames)
+        i = 2 + 3 * (st - 1)
+        (Ti, Fi), (To, Fo) = S.stages[st], S.stages[st + 1]
+        q = dws[st - 1]
+        Wpw = P[pre + f"pre_encode.conv.{i + 1}.weight"].view(C, C)
+        WGRAD.run(lambda g=g, q=q, i=i: K.linear_dw(g, q, G[pre + f"pre_encode.conv.{i + 1}.weight"].view(C, C),
+                                                    db=G[pre + f"pre_encode.conv.{i + 1}.bias"]), g, q)
+        gq = _empty(B * To * Fo, C, dev=dx.device)
+        K.linear_dx(g, Wpw, gq, rowmask=(lens[st], To, Fo) if m else None)
+        a_in = acts[st - 1]
+        K.dwsub_conv_wgrad(gq, L(st + 1), a_in, L(st), G[pre + f"pre_encode.conv.{i}.weight"],
+                           G[pre + f"pre_encode.conv.{i}.bias"], B, Ti, Fi, C, C, To, Fo, S.pad)
+        ga = _empty(B * Ti * Fi, C, dev=dx.device)
+        K.dwsub_conv_dgrad(gq, L(st + 1), P[pre + f"pre_encode.conv.{i}.weight"], a_in, L(st), ga, B, Ti, Fi, C, To,
+                           Fo, S.pad)
+        g = ga
+    T1, F1 = S.stages[1]
+    K.dwsub_conv_wgrad(g, L(1), ctx["mel"], L(0), G[pre + "pre_encode.conv.0.weight"], G[pre + "pre_encode.conv.0.bias"],
+                       B, S.Tm, cfg.nfilt, 1, C, T1, F1, S.pad)
+
+
 def subsampling_forward(cfg, S: EncoderShapes, P, pre, mel, mel_len, len1, len2, *, train, seed, salt, save, ws):
+    if cfg.subsampling == "dw_striding":
+        return dw_subsampling_forward(cfg, S, P, pre, mel, mel_len, len1, train=train, seed=seed, salt=salt,
+                                      save=save, ws=ws)
     dev = mel.device
     B, C, d = S.B, S.d, S.d
     cols0 = cols1 = y1 = None
@@ -84,16 +198,7 @@ def subsampling_forward(cfg, S: EncoderShapes, P, pre, mel, mel_len, len1, len2,
         if not save:
             del cols1, cols0
             cols0 = cols1 = None
-    # Linear(C*F2 -> d) on channels-last (f, c) flattening: weight re-laid out (d, F2, C) on device
-    wout = ws["wout_perm"]
-    K.convw_prep(P[pre + "pre_encode.out.weight"].view(d, C, S.F2), fwd=wout)
-    xscale = math.sqrt(d)
-    bscaled = ws["bout_scaled"]
-    K.axpby(P[pre + "pre_encode.out.bias"].view(1, d), None, bscaled.view(1, d), alpha=xscale)
-    x = _empty(S.rows, d, dev=dev)
-    p_pre = cfg.dropout_pre if train else 0.0
-    K.linear(y2.view(S.rows, S.F2 * C), wout.view(d, S.F2 * C), bscaled, x, alpha=xscale, dropout_p=p_pre,
-             seed=seed, rng_stream=_stream(salt, -1, SITE_PRE))
+    x, p_pre, xscale = _out_linear(cfg, S, P, pre, y2, train=train, seed=seed, salt=salt, ws=ws)
     ctx = None
     if save:
         ctx = dict(cols0=cols0, y1=y1, cols1=cols1, y2=y2, p_pre=p_pre, xscale=xscale, mel=mel, mel_len=mel_len)
@@ -101,19 +206,11 @@ def subsampling_forward(cfg, S: EncoderShapes, P, pre, mel, mel_len, len1, len2,
 
 
 def subsampling_backward(cfg, S: EncoderShapes, P, G, pre, ctx, dx, len1, *, seed, salt, ws):
+    if cfg.subsampling == "dw_striding":
+        return dw_subsampling_backward(cfg, S, P, G, pre, ctx, dx, seed=seed, salt=salt, ws=ws)
     dev = dx.device
-    B, C, d = S.B, S.d, S.d
-    dlin = _empty(S.rows, d, dev=dev)
-    K.dropout(dx, dlin, ctx["p_pre"], ctx["xscale"], seed, _stream(salt, -1, SITE_PRE))
-    y2 = ctx["y2"]
-    Gout = ws["wout_perm_grad"]
-    K.fill(Gout, 0.0)
-    K.linear_dw(dlin, y2.view(S.rows, S.F2 * C), Gout.view(d, S.F2 * C))
-    K.convw_grad(Gout, G[pre + "pre_encode.out.weight"].view(d, C, S.F2))
-    K.colsum(dlin, G[pre + "pre_encode.out.bias"])
-    dy2 = _empty(B * S.T * S.F2, C, dev=dev)
-    K.linear_dx(dlin, ws["wout_perm"].view(d, S.F2 * C), dy2.view(S.rows, S.F2 * C), epi=_lib.EPI_DRELU,
-                aux=y2.view(S.rows, S.F2 * C))
+    B, C = S.B, S.C
+    dy2 = _out_linear_backward(S, P, G, pre, ctx, dx, ctx["y2"], seed=seed, salt=salt, ws=ws)
     if ctx["cols1"] is None:   # fused forward: rebuild the im2col operands of the weight gradients
         ctx["cols0"] = _empty(B * S.T1 * S.F1, 9, dev=dev)
         K.im2col_3x3s2(ctx["mel"], ctx["mel_len"] if cfg.subsampling_mask else None, ctx["cols0"], B, S.Tm,
@@ -462,10 +559,12 @@ def encoder_backward(cfg, S: EncoderShapes, P, G, prefix, run: EncoderRun, dfeat
 
 
 def make_workspace(S: EncoderShapes, dev):
-    return {
-        "wout_perm": torch.empty(S.d, S.F2, S.d, device=dev),
-        "w2_bf16": torch.empty(K.subsample_wprep_elems(S.d), device=dev, dtype=torch.bfloat16),
-        "wout_perm_grad": torch.empty(S.d, S.F2, S.d, device=dev),
-        "w2_tapmajor": torch.empty(S.d, 9, S.d, device=dev),
+    ws = {
+        "wout_perm": torch.empty(S.d, S.F2, S.C, device=dev),
+        "wout_perm_grad": torch.empty(S.d, S.F2, S.C, device=dev),
         "bout_scaled": torch.empty(S.d, device=dev),
     }
+    if len(S.stages) == 3 and S.C == S.d:     # 'striding' x4 kernels
+        ws["w2_bf16"] = torch.empty(K.subsample_wprep_elems(S.d), device=dev, dtype=torch.bfloat16)
+        ws["w2_tapmajor"] = torch.empty(S.d, 9, S.d, device=dev)
+    return ws

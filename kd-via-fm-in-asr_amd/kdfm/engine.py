@@ -15,7 +15,7 @@ import torch
 from . import _lib
 from . import kernels as K
 from .config import Ver5Config, bn_buffer_specs, student_specs, teacher_specs
-from .conformer import EncoderShapes, encoder_backward, encoder_forward, make_workspace
+from .conformer import EncoderShapes, compute_lengths, encoder_backward, encoder_forward, make_workspace
 from .frontend import FrontendConsts, frontend_forward, mel_frames, specaugment_
 from .heads import HeadsWorkspace, heads_backward, heads_forward
 from .overlap import WGRAD
@@ -111,7 +111,7 @@ class Ver5Engine:
         mel_len = torch.empty(B, dtype=torch.int64, device=dev)
         len1 = torch.empty_like(mel_len)
         len2 = torch.empty_like(mel_len)
-        K.subsample_lengths(wav_len, mel_len, len1, len2, cfg.hop)
+        len1, len2 = compute_lengths(cfg, wav_len, mel_len, len1, len2, cfg.hop)
         seed = self.seed
         if K.get_math() == "bf16":   # bf16 twins of the weights the skinny products stream
             self.student.refresh_bf16()
@@ -207,7 +207,7 @@ class Ver5Engine:
         mel_len = torch.empty(B, dtype=torch.int64, device=dev)
         len1 = torch.empty_like(mel_len)
         len2 = torch.empty_like(mel_len)
-        K.subsample_lengths(wav_len.to(device=dev, dtype=torch.int64), mel_len, len1, len2, cfg.hop)
+        len1, len2 = compute_lengths(cfg, wav_len.to(device=dev, dtype=torch.int64), mel_len, len1, len2, cfg.hop)
         mel = frontend_forward(cfg, self.fe, wav.to(dev), wav_len.to(dev), mel_len, dither=0.0)
         feats = torch.empty(cfg.n_layers, Ss.rows, Ss.d, device=dev)
         encoder_forward(cfg, Ss, self.student.P, "encoder.", mel, mel_len, len1, len2, feats,

@@ -361,7 +361,7 @@ def linear(x, W, bias, out, *, epi=0, R=None, rscale=1.0, Cpre=None, dropout_p=0
 
 
 def linear_dx(dy, W, dx, *, epi=0, aux=None, dropout_p=0.0, seed=None, rng_stream=0, R=None, rscale=1.0,
-              alpha=1.0, math=None):
+              alpha=1.0, math=None, rowmask=None):
     """dx[M,K] = epi(alpha * dy[M,N] @ W[N,K])"""
     M, N = dy.shape
     K = W.shape[1]
@@ -370,7 +370,7 @@ def linear_dx(dy, W, dx, *, epi=0, aux=None, dropout_p=0.0, seed=None, rng_strea
         epi |= _lib.EPI_RESID
     gemm(dy, W, dx, M, K, N, dy.stride(0), dy.stride(1), W.stride(0), W.stride(1), dx.stride(0), dx.stride(1),
          amode=_lib.LD_KC, bmode=_lib.LD_XC, epi=epi, aux=aux, dropout_p=dropout_p, seed=seed,
-         rng_stream=rng_stream, R=R, rscale=rscale, alpha=alpha, math=math,
+         rng_stream=rng_stream, R=R, rscale=rscale, alpha=alpha, math=math, rowmask=rowmask,
          Bh=bf16_twin(W, transposed=True) if _TWINS else None)
 
 
@@ -529,6 +529,42 @@ def col2im_3x3s2(dcols, len_in, relu_out, dX, B, T1, F1, Cc, tapmajor=False):
     T2, F2 = (T1 - 1) // 2 + 1, (F1 - 1) // 2 + 1
     assert dcols.shape == (B * T2 * F2, 9 * Cc) and dX.numel() == B * T1 * F1 * Cc
     call("kdfm_col2im_3x3s2_tapmajor" if tapmajor else "kdfm_col2im_3x3s2", ptr(dcols), ptr(_i64(len_in)), ptr(relu_out), ptr(dX), B, T1, F1, Cc, _s())
+
+
+def conv_lengths(inp, out, pad_total, kernel=3, stride=2):
+    """NeMo calc_length for one conv stage: out = floor((in + pad_total - kernel) / stride) + 1."""
+    assert out.numel() == inp.numel() and out.dtype == torch.int64
+    call("kdfm_conv_lengths", ptr(_i64(inp)), ptr(out), inp.numel(), int(pad_total), int(kernel), int(stride), _s())
+
+
+def _dws_sizes(B, Ti, Fi, C, To, Fo):
+    assert C % 4 == 0, "dw_striding channels must be a multiple of 4"
+    return B * Ti * Fi * C, B * To * Fo * C
+
+
+def dwsub_conv(x, in_len, w, b, y, out_len, B, Ti, Fi, Cin, C, To, Fo, pad, relu):
+    """3x3 stride-2 conv of dw_striding subsampling (Cin 1: first stage; Cin C: depthwise)."""
+    nin, nout = _dws_sizes(B, Ti, Fi, C, To, Fo)
+    assert x.numel() == nin // C * Cin and y.numel() == nout and w.numel() == 9 * C and b.numel() == C
+    assert x.is_contiguous() and y.is_contiguous()
+    call("kdfm_dwsub_conv", ptr(_f32(x)), ptr(_i64(in_len)), ptr(_f32(w)), ptr(_f32(b)), ptr(y), ptr(_i64(out_len)),
+         B, Ti, Fi, Cin, C, To, Fo, int(pad), int(pad), int(bool(relu)), _s())
+
+
+def dwsub_conv_dgrad(dy, out_len, w, x_saved, in_len, dx, B, Ti, Fi, C, To, Fo, pad):
+    nin, nout = _dws_sizes(B, Ti, Fi, C, To, Fo)
+    assert dy.numel() == nout and dx.numel() == nin and (x_saved is None or x_saved.numel() == nin)
+    call("kdfm_dwsub_conv_dgrad", ptr(_f32(dy)), ptr(_i64(out_len)), ptr(_f32(w)), ptr(x_saved), ptr(_i64(in_len)),
+         ptr(dx), B, Ti, Fi, C, To, Fo, int(pad), int(pad), _s())
+
+
+def dwsub_conv_wgrad(dy, out_len, x, in_len, dw, db, B, Ti, Fi, Cin, C, To, Fo, pad, accumulate=True):
+    nin, nout = _dws_sizes(B, Ti, Fi, C, To, Fo)
+    assert dy.numel() == nout and x.numel() == nin // C * Cin and dw.numel() == 9 * C and db.numel() == C
+    n = int(_lib.lib().kdfm_dwsub_conv_wgrad_ws(B, To, Fo, C))
+    ws = scratch(dy.device, n)
+    call("kdfm_dwsub_conv_wgrad", ptr(_f32(dy)), ptr(_i64(out_len)), ptr(_f32(x)), ptr(_i64(in_len)), ptr(dw), ptr(db),
+         ptr(ws), ws.numel(), B, Ti, Fi, Cin, C, To, Fo, int(pad), int(pad), int(bool(accumulate)), _s())
 
 
 def subsample_wprep(w2, wb):

@@ -21,9 +21,9 @@ import torch.nn as nn
 from . import _lib
 from . import kernels as K
 from .overlap import WGRAD
-from .config import Ver5Config, encoder_specs
-from .conformer import EncoderShapes, layer_backward, layer_forward, make_workspace, subsampling_backward, \
-    subsampling_forward
+from .config import Ver5Config, encoder_specs, sub_stages
+from .conformer import EncoderShapes, compute_lengths, layer_backward, layer_forward, make_workspace, \
+    subsampling_backward, subsampling_forward
 from .frontend import FrontendConsts, frontend_forward, mel_frames, specaugment_
 
 _SALT = 11
@@ -254,7 +254,9 @@ class _SubsampleFn(torch.autograd.Function):
 
 
 class ConvSubsampling(_Flat):
-    """'striding' x4 subsampling (conformer_encoder.py:381-390; Appendix A.3)."""
+    """ConvSubsampling (conformer_encoder.py:381-390): 'striding' x4 (Appendix A.3) or 'dw_striding'
+    (x2^n, depthwise-separable, optional causal padding; oracle/ver5.py subsampling_dw_striding).
+    forward(x (B, T, feat_in), lengths) -> ((B, T', d), lengths')."""
 
     def __init__(self, cfg: Ver5Config, d: int, device=None):
         super().__init__()
@@ -272,11 +274,12 @@ class ConvSubsampling(_Flat):
     def forward(self, x, lengths):
         _dev_check(x)
         B = x.shape[0]
+        lengths = lengths.to(torch.int64).contiguous()
         len1 = torch.empty(B, dtype=torch.int64, device=x.device)
         len2 = torch.empty_like(len1)
-        # lengths are mel frames here: len1/len2 = calc_length applied once / twice
-        K.subsample_lengths(lengths.to(torch.int64).contiguous(), torch.empty_like(len1), len1, len2, 1)
-        y = _SubsampleFn.apply(x, lengths.to(torch.int64).contiguous(), len1, len2, self, *self.flat_params())
+        # lengths are mel frames here (hop 1): calc_length per stage
+        len1, len2 = compute_lengths(self.cfg, lengths, torch.empty_like(len1), len1, len2, 1)
+        y = _SubsampleFn.apply(x, lengths, len1, len2, self, *self.flat_params())
         return y, len2
 
 
@@ -298,26 +301,28 @@ class RelPositionalEncoding(nn.Module):
 
 class ConformerEncoder(nn.Module):
     """NeMo ConformerEncoder API: forward(audio_signal (B, feat_in, T), length) -> ((B, d, T'), lengths).
-    The x*sqrt(d) scaling and pre-encoder dropout are fused into pre_encode's output GEMM."""
+    The x*sqrt(d) scaling (xscaling) and pre-encoder dropout are fused into pre_encode's output GEMM."""
 
     def __init__(self, feat_in=80, n_layers=16, d_model=176, n_heads=4, subsampling="striding",
-                 subsampling_factor=4, subsampling_conv_channels=-1, ff_expansion_factor=4,
+                 subsampling_factor=4, subsampling_conv_channels=-1, causal_downsampling=False, ff_expansion_factor=4,
                  self_attention_model="rel_pos", conv_kernel_size=31, dropout=0.1, dropout_pre_encoder=0.1,
                  dropout_emb=0.0, dropout_att=0.1, xscaling=True, untie_biases=True, pos_emb_max_len=5000,
                  conv_norm_type="batch_norm", device=None, init_seed=0, **_):
         super().__init__()
-        if subsampling != "striding" or subsampling_factor != 4 or self_attention_model != "rel_pos" \
-                or conv_norm_type != "batch_norm" or not xscaling or not untie_biases \
-                or subsampling_conv_channels not in (-1, d_model):
-            raise _lib.KdfmError("kdfm ConformerEncoder implements the Conformer-CTC recipe (striding x4, rel_pos, "
-                                 "batch_norm conv, xscaling, untied biases)")
+        if self_attention_model != "rel_pos" or conv_norm_type != "batch_norm" or not untie_biases \
+                or (subsampling == "striding" and subsampling_conv_channels not in (-1, d_model)):
+            raise _lib.KdfmError("kdfm ConformerEncoder implements the Conformer-CTC / FastConformer recipes "
+                                 "(rel_pos, batch_norm conv, untied biases)")
         self.cfg = Ver5Config(nfilt=feat_in, n_layers=n_layers, ff_expansion=ff_expansion_factor,
                               conv_kernel=conv_kernel_size, dropout=dropout, dropout_pre=dropout_pre_encoder,
-                              dropout_att=dropout_att)
+                              dropout_att=dropout_att, subsampling=subsampling, subsampling_factor=subsampling_factor,
+                              subsampling_conv_channels=subsampling_conv_channels,
+                              causal_downsampling=causal_downsampling, xscaling=xscaling)
+        sub_stages(self.cfg)   # validates the subsampling choice
         self.d_model, self.n_heads = d_model, n_heads
         self._feat_out = d_model
         self.pre_encode = ConvSubsampling(self.cfg, d_model, device)
-        self.pos_enc = RelPositionalEncoding(d_model, math.sqrt(d_model))
+        self.pos_enc = RelPositionalEncoding(d_model, math.sqrt(d_model) if xscaling else None)
         self.layers = nn.ModuleList([ConformerLayer(self.cfg, d_model, n_heads, i, device) for i in range(n_layers)])
         self.register_buffer("_seed", torch.zeros(1, dtype=torch.int64, device=device), persistent=False)
         self.init_weights(init_seed)

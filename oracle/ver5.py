@@ -59,6 +59,11 @@ class StepConfig:
     kd_alpha: float = 0.1
     kd_temperature: float = 1.0
     subsampling_mask: bool = True
+    subsampling: str = "striding"       # or "dw_striding" (conformer_encoder.py:371-390)
+    subsampling_factor: int = 4
+    subsampling_conv_channels: int = -1  # -1: d_model
+    causal_downsampling: bool = False
+    xscaling: bool = True
     bn_momentum: float = 0.1
     ln_eps: float = 1e-5
     bn_eps: float = 1e-5
@@ -75,14 +80,47 @@ def _lin(g, n_out, n_in, bias=True, scale=None):
     return w, b
 
 
+def sub_pads(cfg) -> tuple:
+    """(left, right) zero padding of every stride-2 3x3 subsampling conv: symmetric 1/1, or
+    CausalConv2D's kernel-1 / stride-1 = 2/1 with causal_downsampling."""
+    return (2, 1) if cfg.causal_downsampling else (1, 1)
+
+
+def sub_stage_len(l, cfg):
+    """calc_length for one stride-2 k=3 stage: floor((l + pl + pr - 3) / 2 + 1) in floating point."""
+    pl, pr = sub_pads(cfg)
+    return torch.floor((torch.as_tensor(l).double() + pl + pr - 3) / 2.0 + 1.0).long()
+
+
+def sub_out_features(cfg) -> int:
+    f = torch.tensor(cfg.nfilt)
+    for _ in range(int(math.log2(cfg.subsampling_factor))):
+        f = sub_stage_len(f, cfg)
+    return int(f)
+
+
+def subsampling_param_shapes(cfg: StepConfig, d: int) -> dict:
+    C = d if cfg.subsampling_conv_channels == -1 else cfg.subsampling_conv_channels
+    if cfg.subsampling == "striding":
+        return {"pre_encode.conv.0.weight": (C, 1, 3, 3), "pre_encode.conv.0.bias": (C,),
+                "pre_encode.conv.2.weight": (C, C, 3, 3), "pre_encode.conv.2.bias": (C,),
+                "pre_encode.out.weight": (d, C * (cfg.nfilt // 4)), "pre_encode.out.bias": (d,)}
+    assert cfg.subsampling == "dw_striding", cfg.subsampling
+    shapes = {"pre_encode.conv.0.weight": (C, 1, 3, 3), "pre_encode.conv.0.bias": (C,)}
+    for s in range(1, int(math.log2(cfg.subsampling_factor))):
+        i = 2 + 3 * (s - 1)            # Sequential: conv, ReLU, [dw, pw, ReLU] x (stages - 1)
+        shapes[f"pre_encode.conv.{i}.weight"] = (C, 1, 3, 3)
+        shapes[f"pre_encode.conv.{i}.bias"] = (C,)
+        shapes[f"pre_encode.conv.{i + 1}.weight"] = (C, C, 1, 1)
+        shapes[f"pre_encode.conv.{i + 1}.bias"] = (C,)
+    shapes["pre_encode.out.weight"] = (d, C * sub_out_features(cfg))
+    shapes["pre_encode.out.bias"] = (d,)
+    return shapes
+
+
 def encoder_param_shapes(cfg: StepConfig, d: int, h: int) -> dict:
     dk = d // h
-    C = d
-    shapes = {
-        "pre_encode.conv.0.weight": (C, 1, 3, 3), "pre_encode.conv.0.bias": (C,),
-        "pre_encode.conv.2.weight": (C, C, 3, 3), "pre_encode.conv.2.bias": (C,),
-        "pre_encode.out.weight": (d, C * (cfg.nfilt // 4)), "pre_encode.out.bias": (d,),
-    }
+    shapes = subsampling_param_shapes(cfg, d)
     ff = cfg.ff_expansion * d
     for i in range(cfg.n_layers):
         L = f"layers.{i}."
@@ -243,8 +281,46 @@ def _time_mask(x, lengths, tdim):
     return x * m.view(shape).to(x.dtype)
 
 
+def subsampling_dw_striding(x_btf, lengths, p, pre, cfg: StepConfig):
+    """ConvSubsampling 'dw_striding' (built at conformer_encoder.py:381-390 with subsampling
+    'dw_striding', recipe fast-conformer_ctc_bpe.yaml:122-125; module source absent, restated):
+    Conv2d(1->C, 3, s2) -> ReLU, then (log2(factor) - 1) x [depthwise Conv2d(C, 3, s2, groups=C) ->
+    pointwise Conv2d(C->C, 1) -> ReLU], then Linear(C*F' -> d) on (B, T', C*F') (c-major flattening).
+    Padding 1/1, or 2/1 (CausalConv2D) with causal_downsampling.  Frames at or past each layer's
+    valid length are zeroed before every layer and at the end (the masked conv sequence pinned by
+    NeMo/tests/collections/asr/test_padding_and_batch_size_invariance.py:49-130)."""
+    pl, pr = sub_pads(cfg)
+    mask = cfg.subsampling_mask
+
+    def m(x, L):
+        return _time_mask(x, L, 2) if mask else x
+
+    def conv3(x, w, b, groups):
+        return F.conv2d(F.pad(x, (pl, pr, pl, pr)), w, b, stride=2, groups=groups)
+
+    x = x_btf.unsqueeze(1)                         # (B,1,T,F)
+    L = lengths
+    x = conv3(m(x, L), p[pre + "conv.0.weight"], p[pre + "conv.0.bias"], 1)
+    L = sub_stage_len(L, cfg)
+    x = F.relu(m(x, L))
+    C = x.shape[1]
+    for s in range(1, int(math.log2(cfg.subsampling_factor))):
+        i = 2 + 3 * (s - 1)
+        x = conv3(m(x, L), p[pre + f"conv.{i}.weight"], p[pre + f"conv.{i}.bias"], C)
+        L = sub_stage_len(L, cfg)
+        x = F.conv2d(m(x, L), p[pre + f"conv.{i + 1}.weight"], p[pre + f"conv.{i + 1}.bias"])
+        x = F.relu(m(x, L))
+    x = m(x, L)
+    b, c, t, f = x.shape
+    x = x.transpose(1, 2).reshape(b, t, c * f)
+    x = F.linear(x, p[pre + "out.weight"], p[pre + "out.bias"])
+    return x, L
+
+
 def subsampling(x_btf, lengths, p, pre, cfg: StepConfig):
-    """ConvSubsampling 'striding' factor 4 (A.3)."""
+    """ConvSubsampling 'striding' factor 4 (A.3); 'dw_striding' dispatches to the function above."""
+    if cfg.subsampling == "dw_striding":
+        return subsampling_dw_striding(x_btf, lengths, p, pre, cfg)
     x = x_btf.unsqueeze(1)                         # (B,1,T,F)
     l1 = _conv_len(lengths)
     l2 = _conv_len(l1)
@@ -338,7 +414,8 @@ def encoder(mel, lengths, p, prefix, d, h, cfg: StepConfig, training, bn_state):
     x = mel.transpose(1, 2)
     x, length = subsampling(x, lengths, p, prefix + "pre_encode.", cfg)
     B, T, _ = x.shape
-    x = x * math.sqrt(d)
+    if cfg.xscaling:
+        x = x * math.sqrt(d)
     pos_emb = rel_pos_emb(T, d, x.dtype)
     valid = torch.arange(T).expand(B, T) < length.unsqueeze(1)
     att_ok = valid.unsqueeze(1).repeat(1, T, 1)

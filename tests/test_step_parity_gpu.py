@@ -24,11 +24,11 @@ pytestmark = pytest.mark.gpu
 ANALYTIC_ZERO = ("self_attn.linear_k.bias", "conv.depthwise_conv.bias")
 
 
-def _build(n_layers, B, N, lens, U, tl, seed=0):
+def _build(n_layers, B, N, lens, U, tl, seed=0, sub=None):
     from kdfm.config import PARITY
     from dataclasses import replace
     from kdfm.engine import Ver5Engine
-    cfg = replace(PARITY, n_layers=n_layers)
+    cfg = replace(PARITY, n_layers=n_layers, **(sub or {}))
     eng = Ver5Engine(cfg, "cuda", teacher_seed=seed, student_seed=seed + 1, heads_seed=seed + 2)
     g = torch.Generator().manual_seed(seed + 10)
     for name, _ in eng.bn.specs:   # non-trivial running stats for the eval-mode teacher
@@ -44,7 +44,9 @@ def _build(n_layers, B, N, lens, U, tl, seed=0):
 
 
 def _oracle_params(cfg, eng):
-    ocfg = O.StepConfig(n_layers=cfg.n_layers)
+    ocfg = O.StepConfig(n_layers=cfg.n_layers, subsampling=cfg.subsampling, subsampling_factor=cfg.subsampling_factor,
+                        subsampling_conv_channels=cfg.subsampling_conv_channels,
+                        causal_downsampling=cfg.causal_downsampling)
     p = {}
     p.update(O.frontend_buffers(ocfg))
     p.update(O.frontend_buffers(ocfg, "teacher.preprocessor.featurizer."))
@@ -72,16 +74,23 @@ def _close(a, b, tol, what, atol=1e-6, failures=None):
     assert err <= tol * scale + atol, msg
 
 
-@pytest.mark.parametrize("n_layers,B,N,lens,U,tl", [
-    (2, 2, 19200, [19200, 16123], 12, [12, 7]),
-    (16, 2, 16000, [16000, 12800], 10, [10, 6]),
+DW4 = dict(subsampling="dw_striding", subsampling_factor=4)
+DW8C = dict(subsampling="dw_striding", subsampling_factor=8, subsampling_conv_channels=32, causal_downsampling=True)
+
+
+@pytest.mark.parametrize("n_layers,B,N,lens,U,tl,sub", [
+    (2, 2, 19200, [19200, 16123], 12, [12, 7], None),
+    (16, 2, 16000, [16000, 12800], 10, [10, 6], None),
     # the benchmark's utterance shape: 16.0 s (T'=401), U=100 targets, one padded utterance
-    (16, 2, 256000, [256000, 200000], 100, [100, 61]),
-], ids=["2L-1.2s", "16L-1s", "16L-16s"])
-def test_ver5_step_matches_oracle(n_layers, B, N, lens, U, tl):
-    cfg, eng, wav, wl, tg, tgl, g = _build(n_layers, B, N, lens, U, tl)
-    T = ((N // cfg.hop) + 1 - 1) // 2 + 1
-    T = (T - 1) // 2 + 1
+    (16, 2, 256000, [256000, 200000], 100, [100, 61], None),
+    # depthwise-separable subsampling (teacher and student): x4 symmetric, x8 causal 32 channels
+    (2, 2, 19200, [19200, 16123], 12, [12, 7], DW4),
+    (2, 2, 19200, [19200, 16123], 8, [8, 5], DW8C),
+], ids=["2L-1.2s", "16L-1s", "16L-16s", "2L-1.2s-dw4", "2L-1.2s-dw8-causal"])
+def test_ver5_step_matches_oracle(n_layers, B, N, lens, U, tl, sub):
+    from kdfm.config import sub_dims
+    cfg, eng, wav, wl, tg, tgl, g = _build(n_layers, B, N, lens, U, tl, sub=sub)
+    T = sub_dims(cfg, N // cfg.hop + 1)[-1][0]
     eps_rows = torch.randn(n_layers * B * T, cfg.latent, generator=g)
     ctx = eng.forward(wav.cuda(), wl.cuda(), tg.cuda(), tgl.cuda(), train=True, eps=eps_rows.cuda())
     losses = eng.losses.detach().cpu().clone()
@@ -130,7 +139,8 @@ def test_ver5_step_matches_oracle(n_layers, B, N, lens, U, tl):
     report.sort(reverse=True)
     out_dir = os.path.join(ROOT, "gpurun_out")
     if os.path.isdir(out_dir):
-        with open(os.path.join(out_dir, f"step_parity_{n_layers}L_{N}.txt"), "w") as fh:
+        tag = "" if sub is None else f"_{cfg.subsampling}{cfg.subsampling_factor}"
+        with open(os.path.join(out_dir, f"step_parity_{n_layers}L_{N}{tag}.txt"), "w") as fh:
             for r in report[:25]:
                 fh.write(f"{r[0]:.3e} {r[1]} err {r[2]:.3e} f32cpu-noise {r[3]:.3e} max {r[4]:.3e}\n")
     assert not failures, f"{len(failures)} gradients out of tolerance: {failures}"
