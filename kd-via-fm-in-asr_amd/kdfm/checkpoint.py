@@ -29,6 +29,7 @@ import yaml
 TEACHER_MAP = (("encoder.", "teacher.encoder."), ("decoder.", "teacher.decoder."),
                ("preprocessor.", "teacher.preprocessor."))
 _IGNORED_SUFFIXES = ("num_batches_tracked",)
+_HEAD_PREFIXES = ("tae.", "sproj.", "adapter.", "denoiser.", "fm_latent.", "fm_latent_2.")
 
 
 def _fb_nemo(fb: torch.Tensor) -> torch.Tensor:
@@ -69,7 +70,8 @@ def engine_state_dict(eng, *, teacher: bool = True, frontend: bool = True) -> "O
 def load_engine_state(eng, sd: dict, *, strict: bool = False, fb_atol: float = 1e-5) -> dict:
     """Copy every known key of `sd` into the engine's device stores (shapes must match exactly).
     Returns {"missing": [...], "unexpected": [...], "frontend_mismatch": [...]}; strict=True raises
-    on missing or unexpected keys (num_batches_tracked and unused `fm_latent_2.*` excepted)."""
+    on missing or unexpected keys (num_batches_tracked and the KD heads the version does not use
+    excepted: the reference builds every head for every version)."""
     stores = [eng.student, eng.teacher, eng.bn]
     known = {}
     for st in stores:
@@ -91,7 +93,8 @@ def load_engine_state(eng, sd: dict, *, strict: bool = False, fb_atol: float = 1
                 ref = v.reshape(mine.shape).to(torch.float32).cpu()
                 if ref.shape != mine.shape or (ref - mine.detach().cpu()).abs().max().item() > fb_atol:
                     fe_bad.append(k)
-            elif k.endswith(_IGNORED_SUFFIXES) or k.startswith("fm_latent_2."):
+            elif k.endswith(_IGNORED_SUFFIXES) or k.startswith(_HEAD_PREFIXES):
+                # heads the configured model version does not train (kdfm.config.head_modules)
                 if k.startswith("teacher.") and k.endswith("num_batches_tracked"):
                     if not hasattr(eng, "bn_batches_tracked"):
                         eng.bn_batches_tracked = {}

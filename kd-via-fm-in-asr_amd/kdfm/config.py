@@ -37,7 +37,10 @@ class Ver5Config:
     freq_width: int = 27
     time_masks: int = 5
     time_width: float = 0.05
-    # heads (asr_train_diffm.py:539, 1804-1837)
+    # heads (asr_train_diffm.py:539, 1804-1837); version = --model_version verN (:1636-1641, 645-729),
+    # kd_loss_type = the kd_crit of versions 1/3/4/8 (:527, 556)
+    version: int = 5
+    kd_loss_type: str = "mse"
     fm_steps: int = 8
     denoiser_steps: int = 9
     time_embed_dim: int = 32
@@ -181,15 +184,38 @@ def decoder_specs(cfg: Ver5Config, d: int, prefix: str) -> list:
     return [(prefix + "decoder_layers.0.weight", (cfg.classes, d, 1)), (prefix + "decoder_layers.0.bias", (cfg.classes,))]
 
 
-def head_specs(cfg: Ver5Config, fm_prefixes=("fm_latent.fm.",)) -> list:
+def head_modules(cfg: Ver5Config) -> tuple:
+    """The KD head modules a model version trains (asr_train_diffm.py:645-729): the rest of the
+    reference's heads exist in its state dict but never receive a gradient, so AdamW (which skips
+    params whose .grad is None) never touches them — they are kept out of the trained buffer."""
+    v = cfg.version
+    if v not in range(1, 9):
+        raise ValueError(f"model version must be 1..8, got {v}")
+    if cfg.kd_loss_type not in ("mse", "l1"):
+        raise ValueError("kd_loss_type must be 'mse' or 'l1'")
+    mods = ["tae", "sproj"]
+    if v >= 3:
+        mods += ["adapter", "denoiser"]
+    if v in (2, 4, 5, 6, 7, 8):
+        mods.append("fm_latent")
+    if v in (6, 7):
+        mods.append("fm_latent_2")
+    return tuple(mods)
+
+
+def head_specs(cfg: Ver5Config, fm_prefixes=None) -> list:
     L, Ct, Cs, E = cfg.latent, cfg.d_teacher, cfg.d_student, cfg.time_embed_dim
+    mods = head_modules(cfg)
     s = [("tae.enc.weight", (L, Ct, 1)), ("tae.enc.bias", (L,)),
          ("tae.dec.weight", (Ct, L, 1)), ("tae.dec.bias", (Ct,)),
-         ("sproj.proj.weight", (L, Cs, 1)), ("sproj.proj.bias", (L,)),
-         ("adapter.gamma_head.0.weight", (L, L, 1)), ("adapter.gamma_head.0.bias", (L,)),
-         ("adapter.gamma_head.2.weight", (1, L, 1)), ("adapter.gamma_head.2.bias", (1,)),
-         ("denoiser.net.0.weight", (L, L, 3)), ("denoiser.net.0.bias", (L,)),
-         ("denoiser.net.2.weight", (L, L, 3)), ("denoiser.net.2.bias", (L,))]
+         ("sproj.proj.weight", (L, Cs, 1)), ("sproj.proj.bias", (L,))]
+    if "adapter" in mods:
+        s += [("adapter.gamma_head.0.weight", (L, L, 1)), ("adapter.gamma_head.0.bias", (L,)),
+              ("adapter.gamma_head.2.weight", (1, L, 1)), ("adapter.gamma_head.2.bias", (1,)),
+              ("denoiser.net.0.weight", (L, L, 3)), ("denoiser.net.0.bias", (L,)),
+              ("denoiser.net.2.weight", (L, L, 3)), ("denoiser.net.2.bias", (L,))]
+    if fm_prefixes is None:
+        fm_prefixes = [m + ".fm." for m in mods if m.startswith("fm_latent")]
     for fm in fm_prefixes:
         s += [(fm + "time_embed.weight", (E, 1)), (fm + "time_embed.bias", (E,)),
               (fm + "meta_encoder.0.weight", (L, L + E)), (fm + "meta_encoder.0.bias", (L,)),
@@ -200,8 +226,8 @@ def head_specs(cfg: Ver5Config, fm_prefixes=("fm_latent.fm.",)) -> list:
 
 
 def student_specs(cfg: Ver5Config) -> list:
-    """Trainable parameters of the ver5 step (fm_latent_2 exists in the reference but is unused by
-    ver5 and never receives a gradient, asr_train_diffm.py:564)."""
+    """Trainable parameters of the step: student encoder + decoder + the heads the version uses
+    (head_modules; for ver5 fm_latent_2 exists in the reference but never receives a gradient)."""
     return (encoder_specs(cfg, cfg.d_student, cfg.heads_student, "encoder.")
             + decoder_specs(cfg, cfg.d_student, "decoder.") + head_specs(cfg))
 
@@ -229,5 +255,5 @@ DEFAULT = Ver5Config()
 PARITY = DEFAULT.parity()
 
 __all__ = ["Ver5Config", "DEFAULT", "PARITY", "encoder_specs", "subsampling_specs", "sub_stages", "sub_pad",
-           "sub_channels", "sub_len", "sub_dims", "decoder_specs", "head_specs", "student_specs",
+           "sub_channels", "sub_len", "sub_dims", "decoder_specs", "head_specs", "head_modules", "student_specs",
            "teacher_specs", "bn_buffer_specs", "fused_groups", "field"]

@@ -625,10 +625,10 @@ class DistilFlowMatchingCTCModelBPE(EncDecCTCModelBPE):
     @torch.no_grad()
     def to_engine(self, cfg: Ver5Config | None = None):
         """Copy this model's weights into a fused, graph-capturable Ver5Engine (same kernels)."""
+        from dataclasses import replace
         from .engine import Ver5Engine
-        if self.version != 5:
-            raise _lib.KdfmError("the fused engine runs the ver5 step; other versions train through the module API")
-        cfg = cfg or Ver5Config()
+        cfg = replace(cfg or Ver5Config(), version=int(self.version),
+                      kd_loss_type="l1" if self.kd_crit is l1_loss else "mse")
         eng = Ver5Engine(cfg, self.decoder.decoder_layers[0].weight.device, init=False)
         sd = {k: v for k, v in self.state_dict().items()}
         eng.student.load({k: sd[k] for k, _ in eng.student.specs})

@@ -41,7 +41,7 @@ class Ver5Engine:
         self.seed = torch.zeros(1, dtype=torch.int64, device=dev)     # uint64 bits, advanced on device
         self.step = torch.zeros(1, dtype=torch.int64, device=dev)
         self.lr = torch.zeros(1, device=dev)
-        self.losses = torch.zeros(5, device=dev)                     # total, ctc, kl, recon, fm
+        self.losses = torch.zeros(5, device=dev)   # total, ctc, kl, recon, layer KD (kd/fm pre+post; ver5: fm_post)
         self.hws = HeadsWorkspace(cfg, dev)
         if K.twins_enabled():   # opt-in direct-B skinny path (KDFM_SKINNY_DIRECT_MIN_M)
             self.student.enable_bf16_twins()
@@ -163,7 +163,8 @@ class Ver5Engine:
         main.wait_stream(side)
         # ---- CTC + logit KD on a third stream: they only need the two logit tensors, and their
         # result is first needed after the KD heads' forward, so the serial CTC recursion overlaps it ----
-        acc = torch.zeros(3, device=dev)   # kl, recon, fm
+        # kl | recon, kd_pre, fm_pre, kd_post, fm_post (heads.RECON..FM_POST) | sum of the four layer-KD terms
+        acc = torch.zeros(7, device=dev)
         aux = self._aux_stream()
         aux.wait_stream(main)
         Umax = targets.shape[1]
@@ -182,7 +183,9 @@ class Ver5Engine:
         n = cfg.n_layers * rows
         with K.region("heads_forward"):
             hctx = heads_forward(cfg, self.student.P, sfeats.view(n, Ss.d), tfeats.view(n, St.d), T, self.hws,
-                                 acc[1:3], seed=seed, eps=eps, save=save)
+                                 acc[1:6], seed=seed, eps=eps, save=save)
+            K.colsum(acc[2:6].view(4, 1), acc[6:7], accumulate=False)
+        self.kd_terms = acc[1:6]   # device (recon, kd_pre, fm_pre, kd_post, fm_post): the v/* log keys
         ctx = dict(B=B, T=T, Ss=Ss, St=St, mel_len=mel_len, len1=len1, len2=len2, srun=srun, sfeats=sfeats,
                    glogits=glogits, hctx=hctx, lp=lp, nll=nll, pos_s=pos_s, acc=acc)
         self._join_losses(ctx)   # CTC/KL overlapped the heads forward; losses valid after forward()
@@ -245,7 +248,7 @@ class Ver5Engine:
         """Join the CTC/KL stream and assemble the loss vector (total, ctc, kl, recon, fm)."""
         torch.cuda.current_stream(self.device).wait_stream(self._aux_stream())
         acc = ctx["acc"]
-        K.loss_combine(ctx["nll"], acc[0:1], acc[1:2], acc[2:3], self.cfg.kd_alpha, self.losses)
+        K.loss_combine(ctx["nll"], acc[0:1], acc[1:2], acc[6:7], self.cfg.kd_alpha, self.losses)
 
     def backward(self, ctx, grad_ready=None):
         """grad_ready(offset): optional callback, called whenever every student gradient at flat

@@ -64,6 +64,8 @@ class StepConfig:
     subsampling_conv_channels: int = -1  # -1: d_model
     causal_downsampling: bool = False
     xscaling: bool = True
+    version: int = 5                    # --model_version verN (asr_train_diffm.py:1636-1641)
+    kd_loss_type: str = "mse"
     bn_momentum: float = 0.1
     ln_eps: float = 1e-5
     bn_eps: float = 1e-5
@@ -582,25 +584,37 @@ def ver5_step(p, wav, wav_len, targets, target_len, cfg: StepConfig, eps, spec_m
     stu_logp = F.log_softmax(log_probs / cfg.kd_temperature, dim=-1)
     kl = F.kl_div(stu_logp, tch_p, reduction="batchmean") * cfg.kd_temperature ** 2
     recon_sum = torch.zeros((), dtype=log_probs.dtype)
-    fm_sum = torch.zeros((), dtype=log_probs.dtype)
+    fm_sum = torch.zeros((), dtype=log_probs.dtype)     # ver5: fm_post; other versions: all four KD terms
+    terms = {k: torch.zeros((), dtype=log_probs.dtype) for k in ("kd_loss_pre", "fm_loss_pre", "kd_loss_post",
+                                                                 "fm_loss_post")}
     for i, (s, t) in enumerate(zip(s_feats, t_feats)):
-        r, f = ver5_layer_losses(s, t, p, eps[i], cfg)
+        if cfg.version == 5:
+            r, f = ver5_layer_losses(s, t, p, eps[i], cfg)
+            terms["fm_loss_post"] = terms["fm_loss_post"] + f
+        else:
+            o = v_layer_losses(cfg.version, s, t, p, eps[i], cfg.denoiser_steps, cfg.fm_steps, cfg.kd_loss_type)
+            r = o["recon_loss"]
+            f = o["kd_loss_pre"] + o["fm_loss_pre"] + o["kd_loss_post"] + o["fm_loss_post"]
+            for k in terms:
+                terms[k] = terms[k] + o[k]
         recon_sum = recon_sum + r
         fm_sum = fm_sum + f
+    # training_step (asr_train_diffm.py:813-821): ctc + kd_alpha * logit_kd + recon + kd/fm pre/post
     total = ctc + cfg.kd_alpha * kl + recon_sum + fm_sum
-    return {"loss": total, "ctc": ctc, "kl": kl, "recon": recon_sum, "fm": fm_sum, "log_probs": log_probs,
+    return {"loss": total, "ctc": ctc, "kl": kl, "recon": recon_sum, "fm": fm_sum, "terms": terms,
+            "log_probs": log_probs,
             "enc_len": enc_len, "mel": mel, "mel_len": mel_len, "s_feats": s_feats, "t_feats": t_feats,
             "bn_state": bn_state}
 
 
-def trainable_names(p: dict) -> list:
+def trainable_names(p: dict, version: int = 5) -> list:
     """Names of the parameters the step trains (teacher frozen; buffers/running stats excluded;
-    fm_latent_2 is unused by ver5 and so receives no gradient)."""
+    fm_latent_2 is used by versions 6 and 7 only, and otherwise receives no gradient)."""
     out = []
     for k, v in p.items():
         if k.startswith("teacher.") or k.startswith("preprocessor.") or "running_" in k or "num_batches" in k:
             continue
-        if k.startswith("fm_latent_2."):
+        if k.startswith("fm_latent_2.") and version not in (6, 7):
             continue
         out.append(k)
     return out

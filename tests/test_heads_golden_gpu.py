@@ -61,13 +61,14 @@ def test_heads_match_reference_layer(math, copies, ltol, gtol, rn):
             G[name] = torch.zeros_like(P[name])
     with K.mode(math, True):
         ws = HeadsWorkspace(cfg, dev)
-        acc = torch.zeros(2, device=dev)
+        acc = torch.zeros(5, device=dev)   # recon, kd_pre, fm_pre, kd_post, fm_post
         seed = torch.zeros(1, dtype=torch.int64, device=dev)
         ctx = heads_forward(cfg, P, s_rows, t_rows, T, ws, acc, seed=seed, eps=eps_rows, save=True)
         ds = torch.empty(n, cfg.d_student, device=dev)
         heads_backward(cfg, P, G, ctx, ws, ds, seed=seed)
         torch.cuda.synchronize()
-    recon, fm = acc.cpu().tolist()
+    recon, kd_pre, fm_pre, kd_post, fm = acc.cpu().tolist()
+    assert kd_pre == fm_pre == kd_post == 0.0   # ver5 adds only recon and fm_post
     assert abs(recon - float(gold["out.recon"])) <= ltol * abs(float(gold["out.recon"])), (recon, gold["out.recon"])
     assert abs(fm - float(gold["out.fm_post"])) <= ltol * abs(float(gold["out.fm_post"])), (fm, gold["out.fm_post"])
     checked = 0

@@ -46,7 +46,8 @@ def _build(n_layers, B, N, lens, U, tl, seed=0, sub=None):
 def _oracle_params(cfg, eng):
     ocfg = O.StepConfig(n_layers=cfg.n_layers, subsampling=cfg.subsampling, subsampling_factor=cfg.subsampling_factor,
                         subsampling_conv_channels=cfg.subsampling_conv_channels,
-                        causal_downsampling=cfg.causal_downsampling)
+                        causal_downsampling=cfg.causal_downsampling, version=cfg.version,
+                        kd_loss_type=cfg.kd_loss_type)
     p = {}
     p.update(O.frontend_buffers(ocfg))
     p.update(O.frontend_buffers(ocfg, "teacher.preprocessor.featurizer."))
@@ -86,7 +87,12 @@ DW8C = dict(subsampling="dw_striding", subsampling_factor=8, subsampling_conv_ch
     # depthwise-separable subsampling (teacher and student): x4 symmetric, x8 causal 32 channels
     (2, 2, 19200, [19200, 16123], 12, [12, 7], DW4),
     (2, 2, 19200, [19200, 16123], 8, [8, 5], DW8C),
-], ids=["2L-1.2s", "16L-1s", "16L-16s", "2L-1.2s-dw4", "2L-1.2s-dw8-causal"])
+    # other model versions through the fused engine (fm_latent_2: 6, 7; kd_crit L1: 8)
+    (2, 2, 19200, [19200, 16123], 12, [12, 7], dict(version=6)),
+    (2, 2, 19200, [19200, 16123], 12, [12, 7], dict(version=7)),
+    (2, 2, 19200, [19200, 16123], 12, [12, 7], dict(version=8, kd_loss_type="l1")),
+], ids=["2L-1.2s", "16L-1s", "16L-16s", "2L-1.2s-dw4", "2L-1.2s-dw8-causal", "2L-1.2s-ver6", "2L-1.2s-ver7",
+        "2L-1.2s-ver8-l1"])
 def test_ver5_step_matches_oracle(n_layers, B, N, lens, U, tl, sub):
     from kdfm.config import sub_dims
     cfg, eng, wav, wl, tg, tgl, g = _build(n_layers, B, N, lens, U, tl, sub=sub)
@@ -107,7 +113,7 @@ def test_ver5_step_matches_oracle(n_layers, B, N, lens, U, tl, sub):
     # weight gradient sums 64k cancelling terms after the 16-layer backward).
     eps_o = eps_rows.view(n_layers, B, T, cfg.latent).permute(0, 1, 3, 2)
     p = {k: (v.double() if v.is_floating_point() else v) for k, v in p32.items()}
-    names = O.trainable_names(p)
+    names = O.trainable_names(p, cfg.version)
     for k in names:
         p[k] = p[k].clone().requires_grad_(True)
         p32[k] = p32[k].clone().requires_grad_(True)
@@ -139,7 +145,7 @@ def test_ver5_step_matches_oracle(n_layers, B, N, lens, U, tl, sub):
     report.sort(reverse=True)
     out_dir = os.path.join(ROOT, "gpurun_out")
     if os.path.isdir(out_dir):
-        tag = "" if sub is None else f"_{cfg.subsampling}{cfg.subsampling_factor}"
+        tag = "" if sub is None else "_" + "_".join(f"{k}{v}" for k, v in sub.items())
         with open(os.path.join(out_dir, f"step_parity_{n_layers}L_{N}{tag}.txt"), "w") as fh:
             for r in report[:25]:
                 fh.write(f"{r[0]:.3e} {r[1]} err {r[2]:.3e} f32cpu-noise {r[3]:.3e} max {r[4]:.3e}\n")
