@@ -138,6 +138,31 @@ typedef struct kdfm_gemm_desc {
 } kdfm_gemm_desc;
 
 int kdfm_gemm(const kdfm_gemm_desc* d, void* stream);
+
+/* Row-parallel weight gradient with bf16 operands (the fused KD-head chains' saved operands):
+ *   dW[m][n] += alpha * sum_r dY[r][m] * X[r][n]  (dW row stride ldc),  db[m] += alpha * sum_r dY[r][m]
+ * dY (rows, M), X (rows, N) bf16 row-major, M % 4 == N % 4 == 0, 16-byte aligned; db may be NULL.
+ * Per-workgroup partials in ws (kdfm_wgrad_bf16_ws floats, -1: shape unsupported) folded in a
+ * fixed order (deterministic). */
+int64_t kdfm_wgrad_bf16_ws(int64_t rows, int64_t M, int64_t N, int32_t bias);
+int kdfm_wgrad_bf16(const uint16_t* dY, const uint16_t* X, float* dW, int64_t ldc, float* db, int64_t rows,
+                    int64_t M, int64_t N, float alpha, float* ws, int64_t ws_len, void* stream);
+
+/* Fused FlowMatchingModule chain (asr_train_diffm.py:1368-1427, rectified, meta_encoder 'mlp',
+ * shape_transform 'linear'; bf16 MFMA, f32 state; latent width L == 96).  Rows n:
+ *   forward: x_0 = x0; a_j = relu(W1[:, :L] x_j + cvec[j]); x_{j+1} = x_j - (W2 a_j + b2)/S;
+ *     v = W2 a_{S-1} + b2; nsx = x0 - v; d = Wst nsx + bst - zt; *loss += inv * sum d^2; dtr = 2 inv d;
+ *     xS (optional) = x_{S-1} - v/S; X[j] = x_j and A[j] = a_j saved as bf16 (S, n, L) when non-NULL.
+ *   backward: from dtr, the saved A and the optional gradient gxS of xS: DV[j] = dL/dv_j and
+ *     DA[j] = dL/d(pre-activation of a_j) as bf16 (S, n, L), gx0 = dL/dx0 (f32).
+ * W1 row stride ld_w1 (the time-embedding columns of meta_encoder.0 follow the first L). */
+int kdfm_fm_chain_fwd(const float* x0, const float* zt, const float* W1, int64_t ld_w1, const float* cvec,
+                      const float* W2, const float* b2, const float* Wst, const float* bst, uint16_t* X, uint16_t* A,
+                      float* nsx, float* dtr, float* xS, float* loss, float inv, int64_t n, int32_t L, int32_t S,
+                      void* stream);
+int kdfm_fm_chain_bwd(const float* dtr, const uint16_t* A, const float* gxS, const float* W1, int64_t ld_w1,
+                      const float* W2, const float* Wst, uint16_t* DV, uint16_t* DA, float* gx0, int64_t n, int32_t L,
+                      int32_t S, void* stream);
 /* bf16 weight twins (once per step, before the GEMMs that read them):
  *   kdfm_cast_bf16:   dst[i] = bf16(src[i]), i < n  (same layout as the f32 flat parameter buffer)
  *   kdfm_cast_bf16_t: per table entry e = (offset, rows, cols, first_block) (device int64 [ntab][4]):

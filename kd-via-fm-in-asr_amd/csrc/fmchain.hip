@@ -1,0 +1,387 @@
+// Fused FlowMatchingModule chain of the KD heads (bf16 MFMA, f32 state): the whole rectified
+// flow-matching recurrence of one FMLatent, forward and data-gradient backward, in one launch each.
+//
+// Reference: FlowMatchingModule.forward (asr_train_diffm.py:1368-1427; meta_encoder 'mlp',
+// shape_transform 'linear', rectified schedule :852-856) wrapped by FMLatent (:462-497), applied
+// to the stacked (16 layers x B x T') latent rows by kdfm/heads.py.  Per row (L = 96 features):
+//   x_0 = input;  for j < S:  a_j = relu(W1x x_j + c_j)       (c_j = b1 + W1e e(t_j): time embedding folded)
+//                             x_{j+1} = x_j - (W2 a_j + b2) / S   (j < S-1);  v = W2 a_{S-1} + b2
+//   nsx = x_0 - v;  tr = Wst nsx + bst;  loss += inv * sum (tr - z_t)^2;  dtr = 2 inv (tr - z_t)
+//   module output x_S = x_{S-1} - v / S (versions 6 / 8 feed it on)
+// The unfused path ran 2 GEMM launches per step, each reading and writing a 205k x 96 f32 tensor;
+// here a wave keeps its 32-row tile in registers across all S steps and only the operands the
+// weight gradients need leave the chip, as bf16 (X[j] = x_j, A[j] = a_j — exactly the values the
+// bf16 GEMM path rounds at staging).  The backward kernel runs the data-gradient recurrence
+//   dv_{S-1} = -W^T_st dtr - g_xS / S,  dv_j = -g_{x_{j+1}} / S,  da_j = (W2^T dv_j) . [a_j > 0],
+//   g_{x_j} = W1x^T da_j + g_{x_{j+1}},  d x_0 = g_{x_0} + W^T_st dtr
+// and stores dv_j, da_j (bf16) for the row-parallel weight-gradient kernel (kdfm_wgrad_bf16).
+//
+// Layout: every GEMM is computed transposed, C^T (96 features x 32 rows) = W (96 x 96) x X^T, with
+// v_mfma_f32_32x32x16_bf16: the A operand is a row of the weight image in LDS ([out][in] bf16,
+// shared by the 8 waves), the B operand a row of the wave's staged activations ([row][feature]
+// bf16); the accumulator gives each lane one row (lane & 31) and 48 of its 96 features
+// (32 mt + 8 q + 4 (lane >> 5) + 0..3), so global I/O is 16-byte per lane and re-staging an
+// activation for the next GEMM is one 8-byte LDS store per 4 features.
+#include "gemm_common.h"
+
+namespace kdfm {
+namespace {
+
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((address_space(3))) uint16_t lds_u16;
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+template <typename T>
+__device__ __forceinline__ __attribute__((address_space(3))) T* lds_at(uint16_t* base, int off) {
+  return reinterpret_cast<__attribute__((address_space(3))) T*>((lds_u16*)base + off);
+}
+
+constexpr int FC_L = 96;
+constexpr int FC_LDW = 104;           // bf16 row stride of weight images and row staging (208 B)
+constexpr int FC_NT = 512;            // 8 waves
+constexpr int FC_W = FC_NT / 64;
+constexpr int FC_IMG = FC_L * FC_LDW; // elements of one weight image
+constexpr int FC_STG = 32 * FC_LDW;   // elements of one wave's row staging
+constexpr int FC_MAXS = 32;
+
+__device__ __forceinline__ void fc_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ uint32_t pk2(float a, float b) { return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16); }
+__device__ __forceinline__ float bf2f(uint32_t b16) { return __builtin_bit_cast(float, b16 << 16); }
+
+// image[r][c] = bf16(trans ? W[c][r] : W[r][c]), W row stride ld
+__device__ void fc_stage_w(uint16_t* lds, int img, const float* __restrict__ W, int64_t ld, bool trans) {
+  for (int e = threadIdx.x; e < FC_L * FC_L; e += FC_NT) {
+    const int r = e / FC_L, c = e - r * FC_L;
+    const float v = trans ? W[(int64_t)c * ld + r] : W[(int64_t)r * ld + c];
+    *lds_at<uint16_t>(lds, img + r * FC_LDW + c) = f2bf(v);
+  }
+}
+
+// acc[mt][i] = sum_k W(img)[32 mt + f(i)][k] * stage[lane & 31][k]
+__device__ __forceinline__ void fc_gemm(f32x16 (&acc)[3], uint16_t* lds, int img, int stg, int lane) {
+  const int r = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int mt = 0; mt < 3; ++mt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[mt][i] = 0.f;
+#pragma unroll
+  for (int ks = 0; ks < 6; ++ks) {
+    const bf16x8 b = *lds_at<bf16x8>(lds, stg + r * FC_LDW + ks * 16 + 8 * h);
+#pragma unroll
+    for (int mt = 0; mt < 3; ++mt) {
+      const bf16x8 a = *lds_at<bf16x8>(lds, img + (mt * 32 + r) * FC_LDW + ks * 16 + 8 * h);
+      acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc[mt], 0, 0, 0);
+    }
+  }
+}
+
+template <typename V>
+__device__ __forceinline__ void fc_stage_rows(uint16_t* lds, int stg, const V& v, int lane) {
+  const int r = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int mt = 0; mt < 3; ++mt)
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      *lds_at<u32x2>(lds, stg + r * FC_LDW + mt * 32 + 8 * q + 4 * h) =
+          u32x2{pk2(v[mt][4 * q], v[mt][4 * q + 1]), pk2(v[mt][4 * q + 2], v[mt][4 * q + 3])};
+}
+
+template <typename V>
+__device__ __forceinline__ void fc_load_rows(V& v, const float* __restrict__ src, int64_t row, bool ok, int h) {
+  const float* base = src + (ok ? row : 0) * FC_L;
+#pragma unroll
+  for (int mt = 0; mt < 3; ++mt)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 t = *reinterpret_cast<const float4*>(base + mt * 32 + 8 * q + 4 * h);
+      v[mt][4 * q] = ok ? t.x : 0.f;
+      v[mt][4 * q + 1] = ok ? t.y : 0.f;
+      v[mt][4 * q + 2] = ok ? t.z : 0.f;
+      v[mt][4 * q + 3] = ok ? t.w : 0.f;
+    }
+}
+
+template <typename V>
+__device__ __forceinline__ void fc_store_rows(float* __restrict__ dst, const V& v, int64_t row, bool ok, int h) {
+  if (!ok) return;
+  float* base = dst + row * FC_L;
+#pragma unroll
+  for (int mt = 0; mt < 3; ++mt)
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      *reinterpret_cast<float4*>(base + mt * 32 + 8 * q + 4 * h) =
+          make_float4(v[mt][4 * q], v[mt][4 * q + 1], v[mt][4 * q + 2], v[mt][4 * q + 3]);
+}
+
+template <typename V>
+__device__ __forceinline__ void fc_store_bf16(uint16_t* __restrict__ dst, const V& v, int64_t row, bool ok, int h) {
+  if (!ok) return;
+  uint16_t* base = dst + row * FC_L;
+#pragma unroll
+  for (int mt = 0; mt < 3; ++mt)
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      *reinterpret_cast<uint2*>(base + mt * 32 + 8 * q + 4 * h) =
+          make_uint2(pk2(v[mt][4 * q], v[mt][4 * q + 1]), pk2(v[mt][4 * q + 2], v[mt][4 * q + 3]));
+}
+
+struct FcFwd {
+  const float* x0; const float* zt;
+  const float* W1; int64_t ld1; const float* cvec; const float* W2; const float* b2; const float* Wst;
+  const float* bst;
+  uint16_t* X; uint16_t* A;      // (S, n, 96) bf16 saves (either may be null)
+  float* nsx; float* dtr; float* xS; float* loss; float inv;
+  int64_t n; int S;
+};
+
+__global__ __launch_bounds__(FC_NT, 1) void fm_chain_fwd_kernel(FcFwd a) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t fc_lds[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  constexpr int IW1 = 0, IW2 = FC_IMG, IWS = 2 * FC_IMG;
+  const int stg = 3 * FC_IMG + wave * FC_STG;
+  // f32 biases after the images and staging (uint16 offsets): cvec[S][96], b2[96], bst[96]
+  constexpr int FB = 3 * FC_IMG + FC_W * FC_STG;
+  fc_stage_w(fc_lds, IW1, a.W1, a.ld1, false);
+  fc_stage_w(fc_lds, IW2, a.W2, FC_L, false);
+  fc_stage_w(fc_lds, IWS, a.Wst, FC_L, false);
+  for (int e = threadIdx.x; e < (a.S + 2) * FC_L; e += FC_NT)
+    *lds_at<float>(fc_lds, FB + 2 * e) =
+        e < a.S * FC_L ? a.cvec[e] : (e < (a.S + 1) * FC_L ? a.b2[e - a.S * FC_L] : a.bst[e - (a.S + 1) * FC_L]);
+  __syncthreads();
+  // the 4 biases of features 32 mt + 8 q + 4 h + 0..3 (one 16-byte LDS read)
+  auto bias4 = [&](int vec, int mt, int q) {
+    return *lds_at<f32x4>(fc_lds, FB + 2 * (vec * FC_L + mt * 32 + 8 * q + 4 * h));
+  };
+  const int VB2 = a.S, VBST = a.S + 1;
+  const float invS = 1.f / (float)a.S;
+  const int64_t nL = a.n * FC_L;
+  const int64_t ntiles = ceil_div(a.n, 32);
+  float lossp = 0.f;
+  for (int64_t t = (int64_t)blockIdx.x * FC_W + wave; t < ntiles; t += (int64_t)gridDim.x * FC_W) {
+    const int64_t row = t * 32 + r;
+    const bool ok = row < a.n;
+    float x[3][16];
+    f32x16 acc[3];
+    fc_load_rows(x, a.x0, row, ok, h);
+    if (a.X) fc_store_bf16(a.X, x, row, ok, h);
+    fc_stage_rows(fc_lds, stg, x, lane);
+    fc_sync();
+    for (int j = 0; j < a.S; ++j) {
+      fc_gemm(acc, fc_lds, IW1, stg, lane);
+      // a_j = relu(. + c_j), in place
+#pragma unroll
+      for (int mt = 0; mt < 3; ++mt)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const f32x4 b = bias4(j, mt, q);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) acc[mt][4 * q + k] = fmaxf(acc[mt][4 * q + k] + b[k], 0.f);
+        }
+      if (a.A) fc_store_bf16(a.A + j * nL, acc, row, ok, h);
+      fc_stage_rows(fc_lds, stg, acc, lane);
+      fc_sync();
+      fc_gemm(acc, fc_lds, IW2, stg, lane);
+      // u = W2 a_j + b2, in place; x_{j+1} = x_j - u / S (the last step keeps u = v)
+#pragma unroll
+      for (int mt = 0; mt < 3; ++mt)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const f32x4 b = bias4(VB2, mt, q);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) acc[mt][4 * q + k] += b[k];
+        }
+      if (j < a.S - 1) {
+#pragma unroll
+        for (int mt = 0; mt < 3; ++mt)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) x[mt][i] -= acc[mt][i] * invS;
+        if (a.X) fc_store_bf16(a.X + (j + 1) * nL, x, row, ok, h);
+        fc_stage_rows(fc_lds, stg, x, lane);
+        fc_sync();
+      }
+    }
+    // acc = v.  Module output x_S = x_{S-1} - v / S; then nsx = x_0 - v (rectified noise_scheduled_x)
+    if (a.xS) {
+#pragma unroll
+      for (int mt = 0; mt < 3; ++mt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) x[mt][i] -= acc[mt][i] * invS;
+      fc_store_rows(a.xS, x, row, ok, h);
+    }
+    fc_load_rows(x, a.x0, row, ok, h);
+#pragma unroll
+    for (int mt = 0; mt < 3; ++mt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) x[mt][i] -= acc[mt][i];
+    if (a.nsx) fc_store_rows(a.nsx, x, row, ok, h);
+    fc_stage_rows(fc_lds, stg, x, lane);
+    fc_sync();
+    fc_gemm(acc, fc_lds, IWS, stg, lane);
+    fc_load_rows(x, a.zt, row, ok, h);
+#pragma unroll
+    for (int mt = 0; mt < 3; ++mt)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f32x4 b = bias4(VBST, mt, q);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float d = acc[mt][4 * q + k] + b[k] - x[mt][4 * q + k];
+          lossp += ok ? d * d : 0.f;
+          x[mt][4 * q + k] = 2.f * a.inv * d;
+        }
+      }
+    fc_store_rows(a.dtr, x, row, ok, h);
+  }
+  // one float atomic per wave for the loss scalar (as the GEMM MSE epilogue)
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) lossp += __shfl_xor(lossp, o);
+  if (lane == 0 && lossp != 0.f) atomicAdd(a.loss, lossp * a.inv);
+}
+
+struct FcBwd {
+  const float* dtr; const uint16_t* A; const float* gxs;
+  const float* W1; int64_t ld1; const float* W2; const float* Wst;
+  uint16_t* DV; uint16_t* DA; float* gx0;
+  int64_t n; int S;
+};
+
+__global__ __launch_bounds__(FC_NT, 1) void fm_chain_bwd_kernel(FcBwd a) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t fc_lds[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  constexpr int IW1 = 0, IW2 = FC_IMG, IWS = 2 * FC_IMG;   // transposed images: [in][out]
+  const int stg = 3 * FC_IMG + wave * FC_STG;
+  fc_stage_w(fc_lds, IW1, a.W1, a.ld1, true);
+  fc_stage_w(fc_lds, IW2, a.W2, FC_L, true);
+  fc_stage_w(fc_lds, IWS, a.Wst, FC_L, true);
+  __syncthreads();
+  const float invS = 1.f / (float)a.S;
+  const int64_t nL = a.n * FC_L;
+  const int64_t ntiles = ceil_div(a.n, 32);
+  for (int64_t t = (int64_t)blockIdx.x * FC_W + wave; t < ntiles; t += (int64_t)gridDim.x * FC_W) {
+    const int64_t row = t * 32 + r;
+    const bool ok = row < a.n;
+    float dn[3][16], g[3][16], d[3][16];
+    f32x16 acc[3];
+    fc_load_rows(d, a.dtr, row, ok, h);
+    fc_stage_rows(fc_lds, stg, d, lane);
+    fc_sync();
+    fc_gemm(acc, fc_lds, IWS, stg, lane);
+#pragma unroll
+    for (int mt = 0; mt < 3; ++mt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) dn[mt][i] = acc[mt][i];
+    const bool have_g = a.gxs != nullptr;
+    if (have_g) fc_load_rows(g, a.gxs, row, ok, h);
+    for (int j = a.S - 1; j >= 0; --j) {
+      // dv_j
+      if (j == a.S - 1) {
+#pragma unroll
+        for (int mt = 0; mt < 3; ++mt)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) d[mt][i] = -dn[mt][i] - (have_g ? g[mt][i] * invS : 0.f);
+      } else {
+#pragma unroll
+        for (int mt = 0; mt < 3; ++mt)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) d[mt][i] = -g[mt][i] * invS;
+      }
+      if (a.DV) fc_store_bf16(a.DV + j * nL, d, row, ok, h);
+      fc_stage_rows(fc_lds, stg, d, lane);
+      fc_sync();
+      fc_gemm(acc, fc_lds, IW2, stg, lane);
+      // da_j = (W2^T dv_j) . [a_j > 0]
+      const uint16_t* aj = a.A + j * nL + (ok ? row : 0) * FC_L;
+#pragma unroll
+      for (int mt = 0; mt < 3; ++mt)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint2 w = *reinterpret_cast<const uint2*>(aj + mt * 32 + 8 * q + 4 * h);
+          const uint32_t e[4] = {w.x & 0xFFFFu, w.x >> 16, w.y & 0xFFFFu, w.y >> 16};
+#pragma unroll
+          for (int k = 0; k < 4; ++k) d[mt][4 * q + k] = bf2f(e[k]) > 0.f ? acc[mt][4 * q + k] : 0.f;
+        }
+      if (a.DA) fc_store_bf16(a.DA + j * nL, d, row, ok, h);
+      fc_stage_rows(fc_lds, stg, d, lane);
+      fc_sync();
+      fc_gemm(acc, fc_lds, IW1, stg, lane);
+      const bool first = (j == a.S - 1) && !have_g;
+#pragma unroll
+      for (int mt = 0; mt < 3; ++mt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) g[mt][i] = first ? acc[mt][i] : acc[mt][i] + g[mt][i];
+    }
+#pragma unroll
+    for (int mt = 0; mt < 3; ++mt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) g[mt][i] += dn[mt][i];
+    fc_store_rows(a.gx0, g, row, ok, h);
+  }
+}
+
+size_t fc_lds_bytes(int S, bool fwd) {
+  return (size_t)(3 * FC_IMG + FC_W * FC_STG) * sizeof(uint16_t) + (fwd ? (size_t)(S + 2) * FC_L * sizeof(float) : 0);
+}
+
+unsigned fc_grid(int64_t n) {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    hipDeviceProp_t prop;
+    cus = (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess) ? prop.multiProcessorCount
+                                                                                                  : 256;
+  }
+  const int64_t groups = ceil_div(ceil_div(n, 32), FC_W);
+  return (unsigned)(groups < cus ? groups : cus);
+}
+
+template <typename K>
+void fc_allow_lds(K kern) {
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+}
+
+}  // namespace
+}  // namespace kdfm
+
+extern "C" {
+
+int kdfm_fm_chain_fwd(const float* x0, const float* zt, const float* W1, int64_t ld_w1, const float* cvec,
+                      const float* W2, const float* b2, const float* Wst, const float* bst, uint16_t* X, uint16_t* A,
+                      float* nsx, float* dtr, float* xS, float* loss, float inv, int64_t n, int32_t L, int32_t S,
+                      void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(x0 && zt && W1 && cvec && W2 && b2 && Wst && bst && dtr && loss, "null pointer");
+  KDFM_REQUIRE(L == FC_L, "the fused chain is compiled for latent width 96");
+  KDFM_REQUIRE(S >= 1 && S <= FC_MAXS && ld_w1 >= L, "bad steps / W1 stride");
+  KDFM_REQUIRE(((((uintptr_t)x0) | ((uintptr_t)zt) | ((uintptr_t)dtr) | ((uintptr_t)nsx) | ((uintptr_t)xS) |
+                 ((uintptr_t)X) | ((uintptr_t)A)) & 15) == 0, "row operands must be 16-byte aligned");
+  if (n <= 0) return KDFM_OK;
+  FcFwd a{x0, zt, W1, ld_w1, cvec, W2, b2, Wst, bst, X, A, nsx, dtr, xS, loss, inv, n, S};
+  static bool once = (fc_allow_lds(fm_chain_fwd_kernel), true);
+  (void)once;
+  hipLaunchKernelGGL(fm_chain_fwd_kernel, dim3(fc_grid(n)), dim3(FC_NT), fc_lds_bytes(S, true), as_stream(stream), a);
+  return check_launch("kdfm_fm_chain_fwd");
+}
+
+int kdfm_fm_chain_bwd(const float* dtr, const uint16_t* A, const float* gxS, const float* W1, int64_t ld_w1,
+                      const float* W2, const float* Wst, uint16_t* DV, uint16_t* DA, float* gx0, int64_t n, int32_t L,
+                      int32_t S, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(dtr && A && W1 && W2 && Wst && gx0, "null pointer");
+  KDFM_REQUIRE(L == FC_L, "the fused chain is compiled for latent width 96");
+  KDFM_REQUIRE(S >= 1 && S <= FC_MAXS && ld_w1 >= L, "bad steps / W1 stride");
+  KDFM_REQUIRE(((((uintptr_t)dtr) | ((uintptr_t)A) | ((uintptr_t)gxS) | ((uintptr_t)DV) | ((uintptr_t)DA) |
+                 ((uintptr_t)gx0)) & 15) == 0, "row operands must be 16-byte aligned");
+  if (n <= 0) return KDFM_OK;
+  FcBwd a{dtr, A, gxS, W1, ld_w1, W2, Wst, DV, DA, gx0, n, S};
+  static bool once = (fc_allow_lds(fm_chain_bwd_kernel), true);
+  (void)once;
+  hipLaunchKernelGGL(fm_chain_bwd_kernel, dim3(fc_grid(n)), dim3(FC_NT), fc_lds_bytes(S, false), as_stream(stream), a);
+  return check_launch("kdfm_fm_chain_bwd");
+}
+
+}  // extern "C"

@@ -46,8 +46,11 @@ struct WrGeo {
   int64_t nmem;      // X columns in memory = ones_col if >= 0 else N
 };
 
-template <int MBW, int NBW, bool CONV, int PD, int UPT>
+// BIN: dY and X are bf16 in memory (the fused KD-head chains store their saved operands as bf16,
+// exactly the values the f32 path would round at staging): 8-byte loads, no conversion.
+template <int MBW, int NBW, bool CONV, int PD, int UPT, bool BIN = false>
 __global__ __launch_bounds__(WR_NT, 2) void wgr_kernel(GemmP p, WrGeo g) {
+  constexpr int ES = BIN ? 2 : 4;   // element size in memory
   extern __shared__ __attribute__((aligned(16))) uint16_t wr_lds[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   // LDS images as element offsets into wr_lds (an array of pointers would decay to generic pointers
@@ -98,8 +101,8 @@ __global__ __launch_bounds__(WR_NT, 2) void wgr_kernel(GemmP p, WrGeo g) {
   // Rows past the split's end or outside the utterance (CONV taps) load from a clamped valid address
   // and are zeroed by a select (branch-free).
   const int ma4 = (int)(p.M >> 2);
-  const float* src[UPT];
-  int64_t ld[UPT];
+  const char* src[UPT];   // byte pointers (ES-byte elements)
+  int64_t ld[UPT];        // row stride in bytes
   int tfr[UPT], toff[UPT];   // CONV: frame of the unit's first row in its utterance; tap - pad
   bool act[UPT];
 #pragma unroll
@@ -111,18 +114,18 @@ __global__ __launch_bounds__(WR_NT, 2) void wgr_kernel(GemmP p, WrGeo g) {
     tfr[i] = 0;
     toff[i] = 0;
     if (cg < ma4) {
-      src[i] = p.A + r0 * p.sAk + cg * 4;
-      ld[i] = p.sAk;
+      src[i] = reinterpret_cast<const char*>(p.A) + ES * (r0 * p.sAk + cg * 4);
+      ld[i] = ES * p.sAk;
     } else {
       const int64_t n = n0 + (int64_t)(cg - ma4) * 4;
-      ld[i] = p.sBk;
+      ld[i] = ES * p.sBk;
       if constexpr (CONV) {
         const int64_t tap = n / p.conv_c, c = n - tap * p.conv_c;
         toff[i] = (int)(tap - p.pad);
         tfr[i] = (int)(r0 % p.conv_t);
-        src[i] = p.B + (r0 + toff[i]) * p.sBk + c;
+        src[i] = reinterpret_cast<const char*>(p.B) + ES * ((r0 + toff[i]) * p.sBk + c);
       } else {
-        src[i] = p.B + r0 * p.sBk + n;
+        src[i] = reinterpret_cast<const char*>(p.B) + ES * (r0 * p.sBk + n);
       }
     }
   }
@@ -149,8 +152,13 @@ __global__ __launch_bounds__(WR_NT, 2) void wgr_kernel(GemmP p, WrGeo g) {
             ok = tt >= 0 && tt < T;
           }
         }
-        const float* q = ok ? src[i] + j * ld[i] : p.B;   // p.B: any valid, aligned address
-        r[i][j] = *reinterpret_cast<const float4*>(q);
+        const char* q = ok ? src[i] + j * ld[i] : reinterpret_cast<const char*>(p.B);   // any valid, aligned address
+        if constexpr (BIN) {
+          const uint2 t = *reinterpret_cast<const uint2*>(q);
+          r[i][j] = make_float4(__builtin_bit_cast(float, t.x), __builtin_bit_cast(float, t.y), 0.f, 0.f);
+        } else {
+          r[i][j] = *reinterpret_cast<const float4*>(q);
+        }
         m |= (ok ? 1u : 0u) << (i * 4 + j);
       }
       src[i] += 32 * ld[i];
@@ -179,15 +187,30 @@ __global__ __launch_bounds__(WR_NT, 2) void wgr_kernel(GemmP p, WrGeo g) {
       const float4 v1 = ((m >> (i * 4 + 1)) & 1u) ? r[i][1] : z;
       const float4 v2 = ((m >> (i * 4 + 2)) & 1u) ? r[i][2] : z;
       const float4 v3 = ((m >> (i * 4 + 3)) & 1u) ? r[i][3] : z;
-      const float* f0 = reinterpret_cast<const float*>(&v0);
-      const float* f1 = reinterpret_cast<const float*>(&v1);
-      const float* f2 = reinterpret_cast<const float*>(&v2);
-      const float* f3 = reinterpret_cast<const float*>(&v3);
+      if constexpr (BIN) {
+        // row j's 4 bf16 columns: (q0 | q1 << 16) in .x, (q2 | q3 << 16) in .y
+        const uint32_t w[4][2] = {{__builtin_bit_cast(uint32_t, v0.x), __builtin_bit_cast(uint32_t, v0.y)},
+                                  {__builtin_bit_cast(uint32_t, v1.x), __builtin_bit_cast(uint32_t, v1.y)},
+                                  {__builtin_bit_cast(uint32_t, v2.x), __builtin_bit_cast(uint32_t, v2.y)},
+                                  {__builtin_bit_cast(uint32_t, v3.x), __builtin_bit_cast(uint32_t, v3.y)}};
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const uint32_t lo = (uint32_t)f2bf(f0[q]) | ((uint32_t)f2bf(f1[q]) << 16);
-        const uint32_t hi = (uint32_t)f2bf(f2[q]) | ((uint32_t)f2bf(f3[q]) << 16);
-        *lds_at<u32x2>(wr_lds, img + (c0 + q) * WR_LDK + rg * 4) = u32x2{lo, hi};
+        for (int q = 0; q < 4; ++q) {
+          const int sh = 16 * (q & 1);
+          const uint32_t b0 = (w[0][q >> 1] >> sh) & 0xFFFFu, b1 = (w[1][q >> 1] >> sh) & 0xFFFFu;
+          const uint32_t b2 = (w[2][q >> 1] >> sh) & 0xFFFFu, b3 = (w[3][q >> 1] >> sh) & 0xFFFFu;
+          *lds_at<u32x2>(wr_lds, img + (c0 + q) * WR_LDK + rg * 4) = u32x2{b0 | (b1 << 16), b2 | (b3 << 16)};
+        }
+      } else {
+        const float* f0 = reinterpret_cast<const float*>(&v0);
+        const float* f1 = reinterpret_cast<const float*>(&v1);
+        const float* f2 = reinterpret_cast<const float*>(&v2);
+        const float* f3 = reinterpret_cast<const float*>(&v3);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint32_t lo = (uint32_t)f2bf(f0[q]) | ((uint32_t)f2bf(f1[q]) << 16);
+          const uint32_t hi = (uint32_t)f2bf(f2[q]) | ((uint32_t)f2bf(f3[q]) << 16);
+          *lds_at<u32x2>(wr_lds, img + (c0 + q) * WR_LDK + rg * 4) = u32x2{lo, hi};
+        }
       }
     }
   };
@@ -334,9 +357,9 @@ struct WrPlan {
   int upt;
 };
 
-bool wr_plan(const GemmP& p, int amode, int bmode, int64_t batch, WrPlan& pl) {
+bool wr_plan(const GemmP& p, int amode, int bmode, int64_t batch, WrPlan& pl, bool force = false) {
   static const int enabled = env_i("KDFM_WGR", 1);
-  if (!enabled) return false;
+  if (!enabled && !force) return false;
   if (batch != 1 || p.epi != KDFM_EPI_ATOMIC || amode != KDFM_LD_XC) return false;
   if (bmode != KDFM_LD_XC && bmode != KDFM_LD_CONV) return false;
   if (p.sAm != 1 || (p.sAk & 3) || (p.M & 3) || (((uintptr_t)p.A) & 15)) return false;
@@ -346,7 +369,7 @@ bool wr_plan(const GemmP& p, int amode, int bmode, int64_t batch, WrPlan& pl) {
   if (nmem & 3) return false;
   if (bmode == KDFM_LD_CONV && ((p.conv_c & 3) || p.taps < 1 || p.pad < 0 || nmem != p.taps * p.conv_c)) return false;
   static const int min_k = env_i("KDFM_WGR_MINK", 2048);
-  if (p.K < min_k) return false;
+  if (p.K < min_k && !force) return false;
   // column slices of at most 24 16-wide blocks (a (6,3) wave tile on a 1x8 wave grid)
   const int64_t Nb_all = ceil_div(p.N, 16);
   pl.slices = ceil_div(Nb_all, 24);
@@ -376,7 +399,7 @@ bool wr_plan(const GemmP& p, int amode, int bmode, int64_t batch, WrPlan& pl) {
   return true;
 }
 
-template <int MBW, int NBW, bool CONV>
+template <int MBW, int NBW, bool CONV, bool BIN = false>
 int wr_launch(const GemmP& p, const WrPlan& pl, hipStream_t st) {
   static const int pd = env_i("KDFM_WGR_PD", 2);
   auto go = [&](auto kern) {
@@ -388,11 +411,12 @@ int wr_launch(const GemmP& p, const WrPlan& pl, hipStream_t st) {
     hipLaunchKernelGGL(kern, dim3((unsigned)pl.S, (unsigned)pl.slices), dim3(WR_NT), pl.lds, st, p, pl.g);
   };
   if (pl.upt <= 1) {
-    if (pd >= 2) go(wgr_kernel<MBW, NBW, CONV, 2, 1>); else go(wgr_kernel<MBW, NBW, CONV, 1, 1>);
+    if (pd >= 2) go(wgr_kernel<MBW, NBW, CONV, 2, 1, BIN>); else go(wgr_kernel<MBW, NBW, CONV, 1, 1, BIN>);
   } else {
     // two slabs of two units each next to an 18-block accumulator tile exceed the 256 registers of
     // a 2-waves-per-SIMD wave (spills): one slab in flight there
-    if (pd >= 2 && MBW * NBW < 18) go(wgr_kernel<MBW, NBW, CONV, 2, 2>); else go(wgr_kernel<MBW, NBW, CONV, 1, 2>);
+    if (pd >= 2 && MBW * NBW < 18) go(wgr_kernel<MBW, NBW, CONV, 2, 2, BIN>);
+    else go(wgr_kernel<MBW, NBW, CONV, 1, 2, BIN>);
   }
   return check_launch("kdfm_gemm(wgrad rows)");
 }
@@ -437,3 +461,72 @@ int try_wgrad_rows(const GemmP& p, int amode, int bmode, int64_t batch, hipStrea
 }
 
 }  // namespace kdfm
+
+// ---- bf16-operand weight gradient (the fused KD-head chains' saved operands) ---------------------
+namespace kdfm {
+namespace {
+GemmP wgrad_bf16_params(const uint16_t* dY, const uint16_t* X, float* dW, int64_t ldc, float* db, int64_t rows,
+                        int64_t M, int64_t N, float alpha, float* ws, int64_t ws_len) {
+  GemmP p{};
+  p.A = reinterpret_cast<const float*>(dY);
+  p.B = reinterpret_cast<const float*>(X);
+  p.C = dW;
+  p.M = M;
+  p.N = db ? N + 1 : N;
+  p.K = rows;
+  p.sAm = 1;
+  p.sAk = M;
+  p.sBk = N;
+  p.sBn = 1;
+  p.sCm = ldc;
+  p.sCn = 1;
+  p.alpha = alpha;
+  p.epi = KDFM_EPI_ATOMIC;
+  p.ones_out = db;
+  p.ones_col = db ? N : -1;
+  p.ws = ws;
+  p.ws_len = ws_len;
+  p.splitk = 1;
+  return p;
+}
+}  // namespace
+}  // namespace kdfm
+
+extern "C" {
+
+int64_t kdfm_wgrad_bf16_ws(int64_t rows, int64_t M, int64_t N, int32_t bias) {
+  using namespace kdfm;
+  GemmP p = wgrad_bf16_params(reinterpret_cast<const uint16_t*>(16), reinterpret_cast<const uint16_t*>(16), nullptr, N,
+                              bias ? reinterpret_cast<float*>(16) : nullptr, rows, M, N, 1.f, nullptr, 0);
+  WrPlan pl;
+  if (!wr_plan(p, KDFM_LD_XC, KDFM_LD_XC, 1, pl, true)) return -1;
+  return pl.S * p.M * p.N;
+}
+
+int kdfm_wgrad_bf16(const uint16_t* dY, const uint16_t* X, float* dW, int64_t ldc, float* db, int64_t rows,
+                    int64_t M, int64_t N, float alpha, float* ws, int64_t ws_len, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(dY && X && dW && ws, "null pointer");
+  KDFM_REQUIRE(rows > 0 && M > 0 && N > 0 && M % 4 == 0 && N % 4 == 0, "M, N must be positive multiples of 4");
+  KDFM_REQUIRE(((((uintptr_t)dY) | ((uintptr_t)X)) & 15) == 0, "operands must be 16-byte aligned");
+  KDFM_REQUIRE(ldc >= N, "ldc < N");
+  GemmP p = wgrad_bf16_params(dY, X, dW, ldc, db, rows, M, N, alpha, ws, ws_len);
+  WrPlan pl;
+  KDFM_REQUIRE(wr_plan(p, KDFM_LD_XC, KDFM_LD_XC, 1, pl, true), "shape not supported by the row-parallel kernel");
+  KDFM_REQUIRE(ws_len >= pl.S * p.M * p.N, "workspace too small (kdfm_wgrad_bf16_ws)");
+  hipStream_t st = as_stream(stream);
+  set_route(ROUTE_WGRAD_ROWS);
+  int rc;
+  switch (pl.w.mbw * 10 + pl.w.nbw) {
+    case 32: rc = wr_launch<3, 2, false, true>(p, pl, st); break;
+    case 33: rc = wr_launch<3, 3, false, true>(p, pl, st); break;
+    case 34: rc = wr_launch<3, 4, false, true>(p, pl, st); break;
+    case 36: rc = wr_launch<3, 6, false, true>(p, pl, st); break;
+    default: rc = wr_launch<6, 3, false, true>(p, pl, st); break;
+  }
+  if (rc) return rc;
+  hipLaunchKernelGGL(wgr_fold_kernel, dim3((unsigned)ceil_div(p.M * p.N, 64)), dim3(64 * WF_WAVES), 0, st, p, pl.S);
+  return check_launch("kdfm_wgrad_bf16(fold)");
+}
+
+}  // extern "C"

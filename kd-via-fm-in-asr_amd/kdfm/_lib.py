@@ -73,6 +73,10 @@ SIGNATURES: dict[str, tuple] = {
     "kdfm_gemm_ws": (_i64, [C.POINTER(GemmDesc)]),
     "kdfm_gemm_last_route": (_i32, []),
     "kdfm_range_push": (_i32, [C.c_char_p]),
+    "kdfm_wgrad_bf16_ws": (_i64, [_i64, _i64, _i64, _i32]),
+    "kdfm_wgrad_bf16": (_i32, [P, P, P, _i64, P, _i64, _i64, _i64, _f32, P, _i64, P]),
+    "kdfm_fm_chain_fwd": (_i32, [P, P, P, _i64, P, P, P, P, P, P, P, P, P, P, P, _f32, _i64, _i32, _i32, P]),
+    "kdfm_fm_chain_bwd": (_i32, [P, P, P, P, _i64, P, P, P, P, P, _i64, _i32, _i32, P]),
     "kdfm_range_pop": (_i32, []),
     "kdfm_cast_bf16": (_i32, [P, P, _i64, P]),
     "kdfm_cast_bf16_t": (_i32, [P, P, P, _i64, _i64, P]),

@@ -167,7 +167,7 @@ def subsampling_forward(cfg, S: EncoderShapes, P, pre, mel, mel_len, len1, len2,
                                       save=save, ws=ws)
     dev = mel.device
     B, C, d = S.B, S.d, S.d
-    cols0 = cols1 = y1 = None
+    cols1 = y1 = None
     y2 = _empty(B * S.T * S.F2, C, dev=dev)
     m0 = mel_len if cfg.subsampling_mask else None
     m1 = len1 if cfg.subsampling_mask else None
@@ -190,18 +190,19 @@ def subsampling_forward(cfg, S: EncoderShapes, P, pre, mel, mel_len, len1, len2,
         w0 = P[pre + "pre_encode.conv.0.weight"].view(C, 9)
         K.linear(cols0, w0, P[pre + "pre_encode.conv.0.bias"], y1, epi=_lib.EPI_RELU,
                  rowmask=(len1, S.T1, S.F1) if cfg.subsampling_mask else None, math="f32")
+        del cols0   # the conv0 weight gradient reads the mel frames directly
         cols1 = _empty(B * S.T * S.F2, 9 * C, dev=dev)
         K.im2col_3x3s2(y1, m1, cols1, B, S.T1, S.F1, C)
         w2 = P[pre + "pre_encode.conv.2.weight"].view(C, 9 * C)
         K.linear(cols1, w2, P[pre + "pre_encode.conv.2.bias"], y2, epi=_lib.EPI_RELU,
                  rowmask=(len2, S.T, S.F2) if cfg.subsampling_mask else None)
         if not save:
-            del cols1, cols0
-            cols0 = cols1 = None
+            del cols1
+            cols1 = None
     x, p_pre, xscale = _out_linear(cfg, S, P, pre, y2, train=train, seed=seed, salt=salt, ws=ws)
     ctx = None
     if save:
-        ctx = dict(cols0=cols0, y1=y1, cols1=cols1, y2=y2, p_pre=p_pre, xscale=xscale, mel=mel, mel_len=mel_len)
+        ctx = dict(y1=y1, cols1=cols1, y2=y2, p_pre=p_pre, xscale=xscale, mel=mel, mel_len=mel_len)
     return x, ctx
 
 
@@ -211,10 +212,7 @@ def subsampling_backward(cfg, S: EncoderShapes, P, G, pre, ctx, dx, len1, *, see
     dev = dx.device
     B, C = S.B, S.C
     dy2 = _out_linear_backward(S, P, G, pre, ctx, dx, ctx["y2"], seed=seed, salt=salt, ws=ws)
-    if ctx["cols1"] is None:   # fused forward: rebuild the im2col operands of the weight gradients
-        ctx["cols0"] = _empty(B * S.T1 * S.F1, 9, dev=dev)
-        K.im2col_3x3s2(ctx["mel"], ctx["mel_len"] if cfg.subsampling_mask else None, ctx["cols0"], B, S.Tm,
-                       cfg.nfilt, 1)
+    if ctx["cols1"] is None:   # fused forward: rebuild the im2col operand of the conv2 weight gradient
         ctx["cols1"] = _empty(B * S.T * S.F2, 9 * C, dev=dev)
         K.im2col_3x3s2(ctx["y1"], len1 if cfg.subsampling_mask else None, ctx["cols1"], B, S.T1, S.F1, C)
     WGRAD.run(lambda: K.linear_dw(dy2, ctx["cols1"], G[pre + "pre_encode.conv.2.weight"].view(C, 9 * C), db=G[pre + "pre_encode.conv.2.bias"]), dy2, ctx["cols1"])
@@ -228,7 +226,12 @@ def subsampling_backward(cfg, S: EncoderShapes, P, G, pre, ctx, dx, len1, *, see
     dy1 = _empty(B * S.T1 * S.F1, C, dev=dev)
     K.col2im_3x3s2(dcols1, len1 if cfg.subsampling_mask else None, ctx["y1"], dy1, B, S.T1, S.F1, C, tapmajor=True)
     del dcols1
-    WGRAD.run(lambda: K.linear_dw(dy1, ctx["cols0"], G[pre + "pre_encode.conv.0.weight"].view(C, 9), math="f32", db=G[pre + "pre_encode.conv.0.bias"]), dy1, ctx["cols0"])
+    # conv0 (1 -> C, 3x3, s2) weight gradient straight from the mel frames: the direct stride-2 kernel
+    # of dw_striding's first stage (same layer), no im2col of the input, deterministic fold
+    m = cfg.subsampling_mask
+    WGRAD.run(lambda: K.dwsub_conv_wgrad(dy1, len1 if m else None, ctx["mel"], ctx["mel_len"] if m else None,
+                                         G[pre + "pre_encode.conv.0.weight"], G[pre + "pre_encode.conv.0.bias"],
+                                         B, S.Tm, cfg.nfilt, 1, C, S.T1, S.F1, S.pad), dy1, ctx["mel"])
     
 
 # ------------------------------------------------------------------------------------------------
@@ -514,14 +517,17 @@ class EncoderRun:
         self.layers = []
 
 
-def encoder_forward(cfg, S: EncoderShapes, P, prefix, mel, mel_len, len1, len2, feats, pos_emb, *, train, seed,
-                    salt, save, bn_running=None, use_batch_stats=True, ws):
-    """mel (B, Tm, nfilt) -> feats (n_layers, rows, d) filled; returns EncoderRun when save."""
-    run = EncoderRun() if save else None
+def encoder_forward_steps(cfg, S: EncoderShapes, P, prefix, mel, mel_len, len1, len2, feats, pos_emb, *, train,
+                          seed, salt, save, bn_running=None, use_batch_stats=True, ws, run=None):
+    """Generator form of encoder_forward: issues the subsampling, then one layer per next() (the
+    engine interleaves the teacher's and the student's launches this way, so both HIP streams get
+    work from the first microsecond instead of one encoder waiting for the host to issue the other).
+    `run` (an EncoderRun, when save) is filled as it goes."""
     x, sctx = subsampling_forward(cfg, S, P, prefix, mel, mel_len, len1, len2, train=train, seed=seed, salt=salt,
                                   save=save, ws=ws)
     if save:
         run.sub = sctx
+    yield
     for i in range(cfg.n_layers):
         L = f"{prefix}layers.{i}."
         bn = None
@@ -532,6 +538,17 @@ def encoder_forward(cfg, S: EncoderShapes, P, prefix, mel, mel_len, len1, len2, 
         if save:
             run.layers.append(ctx)
         x = feats[i]
+        yield
+
+
+def encoder_forward(cfg, S: EncoderShapes, P, prefix, mel, mel_len, len1, len2, feats, pos_emb, *, train, seed,
+                    salt, save, bn_running=None, use_batch_stats=True, ws):
+    """mel (B, Tm, nfilt) -> feats (n_layers, rows, d) filled; returns EncoderRun when save."""
+    run = EncoderRun() if save else None
+    for _ in encoder_forward_steps(cfg, S, P, prefix, mel, mel_len, len1, len2, feats, pos_emb, train=train, seed=seed,
+                                   salt=salt, save=save, bn_running=bn_running, use_batch_stats=use_batch_stats,
+                                   ws=ws, run=run):
+        pass
     return run
 
 

@@ -15,13 +15,41 @@ import torch
 from . import _lib
 from . import kernels as K
 from .config import Ver5Config, bn_buffer_specs, student_specs, teacher_specs
-from .conformer import EncoderShapes, compute_lengths, encoder_backward, encoder_forward, make_workspace
+from .conformer import EncoderRun, EncoderShapes, compute_lengths, encoder_backward, encoder_forward, \
+    encoder_forward_steps, make_workspace
 from .frontend import FrontendConsts, frontend_forward, mel_frames, specaugment_
 from .heads import HeadsWorkspace, heads_backward, heads_forward
 from .overlap import WGRAD
 from .store import FlatStore, init_uniform
 
 SALT_STUDENT, SALT_TEACHER, SALT_FRONT = 1, 2, 3
+
+
+class _OnStream:
+    """Run a block on the engine's compute stream: it first waits for the caller's current stream,
+    and the caller's stream waits for it afterwards (no-op when already on it, e.g. while capturing)."""
+
+    def __init__(self, eng):
+        self.eng = eng
+        self.ctx = None
+
+    def __enter__(self):
+        cs = self.eng.compute_stream
+        if cs is None:
+            return self
+        self.caller = torch.cuda.current_stream(self.eng.device)
+        if self.caller == cs:
+            return self
+        cs.wait_stream(self.caller)
+        self.ctx = torch.cuda.stream(cs)
+        self.ctx.__enter__()
+        return self
+
+    def __exit__(self, *a):
+        if self.ctx is not None:
+            self.ctx.__exit__(*a)
+            self.caller.wait_stream(self.eng.compute_stream)
+            self.ctx = None
 
 
 class Ver5Engine:
@@ -48,6 +76,13 @@ class Ver5Engine:
             self.teacher.enable_bf16_twins()
         self._pos = {}
         self._ws = {}
+        self._tgraphs = {}
+        # the step runs on a created (non-null) stream: ROCm makes the legacy null stream wait for a
+        # HIP graph replayed on any other stream (tools/graph_probe.py), which serialised the teacher
+        # graph and the whole-step graph's branches behind the main stream
+        self.compute_stream = torch.cuda.Stream(dev) if dev.type == "cuda" else None
+        # capture the frozen teacher as a HIP graph in training steps (KDFM_TEACHER_GRAPH=0: eager)
+        self.teacher_graph = __import__("os").environ.get("KDFM_TEACHER_GRAPH", "0") == "1"
         if init:
             st = init_uniform(student_specs(cfg), student_seed)
             hd = init_uniform([s for s in student_specs(cfg) if not s[0].startswith(("encoder.", "decoder."))],
@@ -82,6 +117,58 @@ class Ver5Engine:
             self._side = torch.cuda.Stream(self.device)
         return self._side
 
+    def _teacher_forward(self, mel_t, mel_len, len1, len2, tfeats, tlogits, St, T):
+        cfg = self.cfg
+        Cn = cfg.classes
+        encoder_forward(cfg, St, self.teacher.P, "teacher.encoder.", mel_t, mel_len, len1, len2, tfeats,
+                        self._pos_emb(T, St.d), train=False, seed=self.seed, salt=SALT_TEACHER, save=False,
+                        bn_running=self.bn.P, use_batch_stats=False, ws=self._enc_ws(St))
+        K.linear(tfeats[-1], self.teacher.P["teacher.decoder.decoder_layers.0.weight"].view(Cn, St.d),
+                 self.teacher.P["teacher.decoder.decoder_layers.0.bias"], tlogits)
+
+    def _teacher_graph(self, wav, wav_len, mel_len, len1, len2, St, T):
+        """Static-input HIP graph of the teacher's frontend + encoder + decoder for this batch shape
+        (captured on first use; the teacher is frozen, so nothing but its inputs changes between
+        steps).  The step's inputs and frame lengths are copied into the graph's input buffers on
+        the issuing stream; its outputs (tfeats, tlogits) are rewritten by every replay."""
+        B, N = wav.shape
+        key = (B, N, K.get_math(), K.get_deterministic(), tuple(len1.shape))
+        tg = self._tgraphs.get(key)
+        if tg is None:
+            import types
+            dev = self.device
+            cfg = self.cfg
+            tg = types.SimpleNamespace()
+            tg.wav = torch.empty_like(wav)
+            tg.wav_len = torch.empty_like(wav_len)
+            tg.mel_len = torch.empty_like(mel_len)
+            tg.len1 = torch.empty_like(len1)
+            tg.len2 = torch.empty_like(len2)
+            tg.tfeats = torch.empty(cfg.n_layers, St.rows, St.d, device=dev)
+            tg.tlogits = torch.empty(St.rows, cfg.classes, device=dev)
+            for dst, src in ((tg.wav, wav), (tg.wav_len, wav_len), (tg.mel_len, mel_len), (tg.len1, len1),
+                             (tg.len2, len2)):
+                dst.copy_(src)
+            side = self._side_stream()
+            side.wait_stream(torch.cuda.current_stream(dev))
+
+            def body():
+                mel = frontend_forward(cfg, self.fe, tg.wav, tg.wav_len, tg.mel_len, dither=0.0)
+                self._teacher_forward(mel, tg.mel_len, tg.len1, tg.len2, tg.tfeats, tg.tlogits, St, T)
+
+            with torch.cuda.stream(side):
+                body()        # eager warm-up: lazy workspaces exist before capture
+            torch.cuda.synchronize()
+            tg.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(tg.graph, stream=side):
+                body()
+            torch.cuda.synchronize()
+            self._tgraphs[key] = tg
+        for dst, src in ((tg.wav, wav), (tg.wav_len, wav_len), (tg.mel_len, mel_len), (tg.len1, len1),
+                         (tg.len2, len2)):
+            dst.copy_(src)
+        return tg
+
     def _enc_ws(self, S):
         key = (S.d, S.F2)
         if key not in self._ws:
@@ -89,6 +176,9 @@ class Ver5Engine:
         return self._ws[key]
 
     # ---------------------------------------------------------------------------------------------
+    def _on_stream(self):
+        return _OnStream(self)
+
     def _mode(self):
         """The config's MFMA arithmetic and reduction mode for the duration of a call (restored
         afterwards: the kernels' modes are process-global)."""
@@ -97,7 +187,7 @@ class Ver5Engine:
     def forward(self, wav, wav_len, targets, tgt_len, *, train=True, eps=None, save=True):
         """One forward pass; returns the context backward() consumes.  eps: optional injected
         NoiseAdapter noise (n_layers*B*T', latent) for parity runs."""
-        with self._mode(), K.region("forward"):
+        with self._on_stream(), self._mode(), K.region("forward"):
             return self._forward(wav, wav_len, targets, tgt_len, train=train, eps=eps, save=save)
 
     def _forward(self, wav, wav_len, targets, tgt_len, *, train, eps, save):
@@ -118,8 +208,37 @@ class Ver5Engine:
             self.teacher.refresh_bf16()
         # ---- frontends (teacher preprocessor is in eval mode: no dither) ----
         dither = cfg.dither if train else 0.0
-        mel_t = frontend_forward(cfg, self.fe, wav, wav_len, mel_len, dither=0.0)
-        if train and (dither > 0.0 or not cfg.share_frontend):
+        own_mel = train and (dither > 0.0 or not cfg.share_frontend)   # the student computes its own mel
+        Cn = cfg.classes
+        rows = Ss.rows
+        main = torch.cuda.current_stream(dev)
+        side = self._side_stream()
+        tg = None
+        tgen = None
+        if own_mel and self.teacher_graph and not torch.cuda.is_current_stream_capturing():
+            # experiment (KDFM_TEACHER_GRAPH=1): the frozen teacher as one captured HIP graph.  Off by
+            # default: on ROCm work issued to other streams after the replay waited for the whole
+            # graph (tools/teacher_graph_probe.py), which cost the teacher/student overlap
+            tg = self._teacher_graph(wav, wav_len, mel_len, len1, len2, St, T)
+            side.wait_stream(main)
+            with torch.cuda.stream(side), K.region("teacher_graph"):
+                tg.graph.replay()
+            mel_t, tfeats, tlogits = None, tg.tfeats, tg.tlogits
+        else:
+            tfeats = torch.empty(cfg.n_layers, St.rows, St.d, device=dev)
+            tlogits = torch.empty(rows, Cn, device=dev)
+            if own_mel:
+                # the teacher's own (undithered) frontend goes to the teacher stream with its encoder
+                side.wait_stream(main)
+                with torch.cuda.stream(side), K.region("teacher_frontend"):
+                    mel_t = frontend_forward(cfg, self.fe, wav, wav_len, mel_len, dither=0.0)
+            else:
+                mel_t = frontend_forward(cfg, self.fe, wav, wav_len, mel_len, dither=0.0)
+                side.wait_stream(main)
+            tgen = encoder_forward_steps(cfg, St, self.teacher.P, "teacher.encoder.", mel_t, mel_len, len1, len2,
+                                         tfeats, self._pos_emb(T, St.d), train=False, seed=seed, salt=SALT_TEACHER,
+                                         save=False, bn_running=self.bn.P, use_batch_stats=False, ws=self._enc_ws(St))
+        if own_mel:
             mel_s = frontend_forward(cfg, self.fe, wav, wav_len, mel_len, dither=dither, seed=seed,
                                      rng_stream=SALT_FRONT)
         elif train and cfg.specaug:
@@ -129,31 +248,27 @@ class Ver5Engine:
             mel_s = mel_t
         if train and cfg.specaug:
             specaugment_(cfg, mel_s, mel_len, seed, SALT_FRONT + 1)
-        Cn = cfg.classes
-        rows = Ss.rows
-        # ---- frozen teacher encoder + decoder (eval mode, nothing saved) on a second HIP stream:
-        # independent of the student until the KD losses, so the two encoders overlap on the CUs ----
-        tfeats = torch.empty(cfg.n_layers, St.rows, St.d, device=dev)
-        tlogits = torch.empty(rows, Cn, device=dev)
-        pos_t = self._pos_emb(T, St.d)
-        main = torch.cuda.current_stream(dev)
-        side = self._side_stream()
-        side.wait_stream(main)
-        with torch.cuda.stream(side), K.region("teacher_encoder"):
-            encoder_forward(cfg, St, self.teacher.P, "teacher.encoder.", mel_t, mel_len, len1, len2, tfeats,
-                            pos_t, train=False, seed=seed, salt=SALT_TEACHER, save=False,
-                            bn_running=self.bn.P, use_batch_stats=False, ws=self._enc_ws(St))
-            K.linear(tfeats[-1], self.teacher.P["teacher.decoder.decoder_layers.0.weight"].view(Cn, St.d),
-                     self.teacher.P["teacher.decoder.decoder_layers.0.bias"], tlogits)
-        for t in (tfeats, tlogits, mel_t, mel_len, len1, len2):
-            t.record_stream(side)
-        # ---- student encoder (saved for backward) ----
+        # ---- the frozen teacher encoder (eval mode, nothing saved) on the teacher stream and the
+        # student encoder (saved for backward) on this one, issued layer by layer in alternation so
+        # the two encoders overlap on the CUs while the host is still issuing ----
         sfeats = torch.empty(cfg.n_layers, Ss.rows, Ss.d, device=dev)
         pos_s = self._pos_emb(T, Ss.d)
-        with K.region("student_encoder"):
-            srun = encoder_forward(cfg, Ss, self.student.P, "encoder.", mel_s, mel_len, len1, len2, sfeats, pos_s,
-                                   train=train, seed=seed, salt=SALT_STUDENT, save=save, bn_running=self.bn.P,
-                                   use_batch_stats=train, ws=self._enc_ws(Ss))
+        srun = EncoderRun() if save else None
+        sgen = encoder_forward_steps(cfg, Ss, self.student.P, "encoder.", mel_s, mel_len, len1, len2, sfeats, pos_s,
+                                     train=train, seed=seed, salt=SALT_STUDENT, save=save, bn_running=self.bn.P,
+                                     use_batch_stats=train, ws=self._enc_ws(Ss), run=srun)
+        with K.region("encoders"):
+            for _ in range(cfg.n_layers + 1):
+                if tgen is not None:
+                    with torch.cuda.stream(side):
+                        next(tgen)
+                next(sgen)
+        if tgen is not None:
+            with torch.cuda.stream(side):
+                K.linear(tfeats[-1], self.teacher.P["teacher.decoder.decoder_layers.0.weight"].view(Cn, St.d),
+                         self.teacher.P["teacher.decoder.decoder_layers.0.bias"], tlogits)
+            for t in (tfeats, tlogits, mel_t, mel_len, len1, len2):
+                t.record_stream(side)
         # ---- decoders, CTC, logit KD ----
         logits = torch.empty(rows, Cn, device=dev)
         K.linear(sfeats[-1], self.student.P["decoder.decoder_layers.0.weight"].view(Cn, Ss.d),
@@ -198,7 +313,7 @@ class Ver5Engine:
         with BatchNorm running statistics and no dropout, decoder + log_softmax.  The reference's eval
         forward also runs the teacher encoder (:629-631) and discards it (only training_step reads
         the hooks), so it is skipped.  Returns log_probs (B, T', V+1) and enc_len (B,)."""
-        with self._mode():
+        with self._on_stream(), self._mode():
             return self._infer(wav, wav_len)
 
     def _infer(self, wav, wav_len):
@@ -255,7 +370,7 @@ class Ver5Engine:
         index >= offset is final (BucketedGradAllReduce.ready overlap)."""
         # deterministic mode also keeps the weight-gradient products on the issuing stream: with the
         # side stream overlapping, repeated runs differed in ~1e-3 of some gradients (DESIGN.md §4)
-        with self._mode(), WGRAD.serialized(self.cfg.deterministic), K.region("backward"):
+        with self._on_stream(), self._mode(), WGRAD.serialized(self.cfg.deterministic), K.region("backward"):
             self._backward(ctx, grad_ready)
 
     def _backward(self, ctx, grad_ready):
@@ -290,7 +405,7 @@ class Ver5Engine:
                              on_layer_done=layer_done)
 
     def optimizer_step(self, grad_scale: float = 1.0):
-        with self._mode(), K.region("optimizer"):
+        with self._on_stream(), self._mode(), K.region("optimizer"):
             self._optimizer_step(grad_scale)
 
     def _optimizer_step(self, grad_scale):
@@ -302,7 +417,8 @@ class Ver5Engine:
                      grad_scale, self.lr)
 
     def advance_rng(self):
-        K.step_advance(None, self.seed)
+        with self._on_stream():
+            K.step_advance(None, self.seed)
 
     def train_step(self, wav, wav_len, targets, tgt_len, allreduce=None):
         """forward + backward + (all-reduce) + AdamW.  Returns the device loss vector."""
@@ -334,20 +450,22 @@ class GraphedTrainStep:
         self.g_step = torch.cuda.CUDAGraph()
         self.g_opt = torch.cuda.CUDAGraph()
         torch.cuda.synchronize()
-        with torch.cuda.graph(self.g_step):
+        cs = eng.compute_stream
+        with torch.cuda.graph(self.g_step, stream=cs):
             eng.advance_rng()
             ctx = eng.forward(*self.inputs, train=True)
             eng.backward(ctx)
             del ctx
-        with torch.cuda.graph(self.g_opt, pool=self.g_step.pool()):
+        with torch.cuda.graph(self.g_opt, pool=self.g_step.pool(), stream=cs):
             eng.optimizer_step(scale)
         torch.cuda.synchronize()
 
     def step(self):
-        self.g_step.replay()
-        if self.allreduce is not None:
-            self.allreduce(self.eng.student.grad)
-        self.g_opt.replay()
+        with self.eng._on_stream():
+            self.g_step.replay()
+            if self.allreduce is not None:
+                self.allreduce(self.eng.student.grad)
+            self.g_opt.replay()
         return self.eng.losses
 
 

@@ -74,6 +74,15 @@ def _kd(cfg, a, b, slot, inv, dev):
     return g
 
 
+def _fm_fused(Lt):
+    """bf16 math runs the fused chain kernels (csrc/fmchain.hip); the f32 parity mode keeps the
+    per-step GEMMs (KDFM_FM_FUSED=0 forces them in bf16 too)."""
+    return K.get_math() == "bf16" and Lt == 96 and _FM_FUSED
+
+
+_FM_FUSED = __import__("os").environ.get("KDFM_FM_FUSED", "1") == "1"
+
+
 def _fm_forward(cfg, P, pre, ws, x0, zt, slot, inv, need_out, dev):
     """FlowMatchingModule over rows x0 (n, L) against z_t: loss into slot; ctx for backward.  With
     need_out the module's second output x_s is materialised (versions 6 and 8 feed it onward)."""
@@ -86,6 +95,17 @@ def _fm_forward(cfg, P, pre, ws, x0, zt, slot, inv, need_out, dev):
     cvec, evec, _ = ws.fm[pre]
     K.fm_step_bias(P[pre + "time_embed.weight"].view(-1), P[pre + "time_embed.bias"], W1, P[pre + "meta_encoder.0.bias"],
                    cvec, evec, Lt, E, S_)
+    if _fm_fused(Lt):
+        X = torch.empty(S_, n, Lt, device=dev, dtype=torch.bfloat16)
+        A = torch.empty(S_, n, Lt, device=dev, dtype=torch.bfloat16)
+        nsx = _empty(n, Lt, dev=dev)
+        dtr = _empty(n, Lt, dev=dev)
+        xs = _empty(n, Lt, dev=dev) if need_out else None
+        with K.span("fm_chain_fwd"):
+            K.fm_chain_fwd(x0, zt, W1, cvec, W2, P[pre + "meta_encoder.2.bias"],
+                           P[pre + "shape_transformation_function.weight"],
+                           P[pre + "shape_transformation_function.bias"], X, A, nsx, dtr, xs, slot, inv, S_)
+        return dict(pre=pre, fused=True, X=X, A=A, nsx=nsx, dtr=dtr), xs
     fx = [x0]
     fa = []
     v = None
@@ -118,8 +138,7 @@ def _fm_backward(cfg, P, G, ws, c, gxs, dev):
     """Backward of _fm_forward: parameter grads into G; returns d/d x0.  gxs: optional gradient
     wrt the module's x_s output."""
     pre = c["pre"]
-    fx, fa = c["fx"], c["fa"]
-    n, Lt = fx[0].shape
+    n, Lt = c["dtr"].shape
     S_ = cfg.fm_steps
     E = cfg.time_embed_dim
     W1 = P[pre + "meta_encoder.0.weight"]
@@ -131,6 +150,25 @@ def _fm_backward(cfg, P, G, ws, c, gxs, dev):
     dtr, nsx = c["dtr"], c["nsx"]
     WGRAD.run(lambda: K.linear_dw(dtr, nsx, G[pre + "shape_transformation_function.weight"],
                                   db=G[pre + "shape_transformation_function.bias"]), dtr, nsx)
+    if c.get("fused"):
+        X, A = c["X"], c["A"]
+        DV = torch.empty_like(A)
+        DA = torch.empty_like(A)
+        g = _empty(n, Lt, dev=dev)
+        with K.span("fm_chain_bwd"):
+            K.fm_chain_bwd(dtr, A, gxs, W1, W2, P[pre + "shape_transformation_function.weight"], DV, DA, g, S_)
+        # weight gradients from the saved bf16 operands: dW2 over all steps' rows at once, dW1x (and
+        # the per-step first-layer bias grads dc_j) per step
+        K.fill(dc, 0.0)
+        WGRAD.run(lambda: K.wgrad_bf16(DV.view(S_ * n, Lt), A.view(S_ * n, Lt), G[pre + "meta_encoder.2.weight"],
+                                       db=G[pre + "meta_encoder.2.bias"]), DV, A)
+        for j in range(S_):
+            WGRAD.run(lambda j=j: K.wgrad_bf16(DA[j], X[j], dW1x, db=dc[j]), DA, X)
+        # dc is produced on the side stream: fold it there too (no main-stream join)
+        WGRAD.run(lambda: K.fm_time_bwd(dc, evec, W1, dW1, G[pre + "meta_encoder.0.bias"],
+                                        G[pre + "time_embed.weight"].view(-1), G[pre + "time_embed.bias"], Lt, E, S_))
+        return g
+    fx, fa = c["fx"], c["fa"]
     dnsx = _empty(n, Lt, dev=dev)
     K.linear_dx(dtr, P[pre + "shape_transformation_function.weight"], dnsx)
     # nsx = x0 - v_{S-1}  ->  d x0 += dnsx ; dv_{S-1} = -dnsx (- gxs / S when x_S is used)
@@ -159,9 +197,9 @@ def _fm_backward(cfg, P, G, ws, c, gxs, dev):
             K.linear_dx(da, W1x, gx, R=gx_next, rscale=1.0)
         gx_next = gx
         del da
-    WGRAD.join()  # dc (per-step bias grads) is produced on the side stream
-    K.fm_time_bwd(dc, evec, W1, dW1, G[pre + "meta_encoder.0.bias"], G[pre + "time_embed.weight"].view(-1),
-                  G[pre + "time_embed.bias"], Lt, E, S_)
+    # dc (per-step bias grads) is produced on the side stream: fold it there too
+    WGRAD.run(lambda: K.fm_time_bwd(dc, evec, W1, dW1, G[pre + "meta_encoder.0.bias"],
+                                    G[pre + "time_embed.weight"].view(-1), G[pre + "time_embed.bias"], Lt, E, S_))
     g = _empty(n, Lt, dev=dev)
     K.axpby(gx_next, dnsx, g, 1.0, 1.0)
     return g
@@ -212,9 +250,8 @@ def _adapt_denoise_backward(cfg, P, G, ws, c, g, T, seed, dev):
         K.conv3(da, ws.w1b, None, gi, T, R=g, rscale=1.0, tag="deno_conv")
         g = gi
         del da
-    WGRAD.join()  # ws.g1 / ws.g2 are produced on the side stream
-    K.convw_grad(ws.g1, G["denoiser.net.0.weight"])
-    K.convw_grad(ws.g2, G["denoiser.net.2.weight"])
+    # ws.g1 / ws.g2 are produced on the side stream: re-lay them out there too
+    WGRAD.run(lambda: (K.convw_grad(ws.g1, G["denoiser.net.0.weight"]), K.convw_grad(ws.g2, G["denoiser.net.2.weight"])))
     x, hA = c["x"], c["hA"]
     dx_direct = _empty(n, Lt, dev=dev)
     dh = _empty(n, Lt, dev=dev)

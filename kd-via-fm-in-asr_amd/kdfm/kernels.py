@@ -531,6 +531,47 @@ def col2im_3x3s2(dcols, len_in, relu_out, dX, B, T1, F1, Cc, tapmajor=False):
     call("kdfm_col2im_3x3s2_tapmajor" if tapmajor else "kdfm_col2im_3x3s2", ptr(dcols), ptr(_i64(len_in)), ptr(relu_out), ptr(dX), B, T1, F1, Cc, _s())
 
 
+def _bf16(t, name="tensor"):
+    if t is not None and t.dtype != torch.bfloat16:
+        raise _lib.KdfmError(f"{name} must be bfloat16, got {t.dtype}")
+    return t
+
+
+def wgrad_bf16(dY, X, dW, *, db=None, alpha=1.0):
+    """dW[m, n] += alpha * dY[:, m]^T X[:, n] (+ db[m] += alpha * colsum(dY)), bf16 row operands,
+    row-parallel MFMA kernel with an ordered fold.  dW may be a row-strided view (stride(1) == 1)."""
+    rows, M = dY.shape
+    N = X.shape[1]
+    assert X.shape[0] == rows and dW.shape == (M, N) and dW.stride(1) == 1, (dY.shape, X.shape, dW.shape)
+    assert dY.is_contiguous() and X.is_contiguous()
+    n = int(_lib.lib().kdfm_wgrad_bf16_ws(rows, M, N, 1 if db is not None else 0))
+    if n < 0:
+        raise _lib.KdfmError(f"kdfm_wgrad_bf16: unsupported shape rows={rows} M={M} N={N}")
+    ws = scratch(dY.device, n)
+    call("kdfm_wgrad_bf16", ptr(_bf16(dY)), ptr(_bf16(X)), ptr(_f32(dW)), dW.stride(0), ptr(db), rows, M, N,
+         float(alpha), ptr(ws), ws.numel(), _s())
+
+
+def fm_chain_fwd(x0, zt, W1, cvec, W2, b2, Wst, bst, X, A, nsx, dtr, xS, loss, inv, S):
+    n, L = x0.shape
+    assert zt.shape == (n, L) and dtr.shape == (n, L) and W1.stride(1) == 1 and cvec.shape[0] >= S
+    for t in (X, A):
+        assert t is None or (t.shape == (S, n, L) and t.is_contiguous())
+    call("kdfm_fm_chain_fwd", ptr(_f32(x0)), ptr(_f32(zt)), ptr(_f32(W1)), W1.stride(0), ptr(_f32(cvec)),
+         ptr(_f32(W2)), ptr(_f32(b2)), ptr(_f32(Wst)), ptr(_f32(bst)), ptr(_bf16(X)), ptr(_bf16(A)), ptr(nsx),
+         ptr(dtr), ptr(xS), ptr(loss), float(inv), n, L, S, _s())
+
+
+def fm_chain_bwd(dtr, A, gxS, W1, W2, Wst, DV, DA, gx0, S):
+    n, L = dtr.shape
+    assert A.shape == (S, n, L) and gx0.shape == (n, L) and W1.stride(1) == 1
+    for t in (DV, DA):
+        assert t is None or (t.shape == (S, n, L) and t.is_contiguous())
+    assert gxS is None or (gxS.shape == (n, L) and gxS.is_contiguous())
+    call("kdfm_fm_chain_bwd", ptr(_f32(dtr)), ptr(_bf16(A)), ptr(_f32(gxS)), ptr(_f32(W1)), W1.stride(0),
+         ptr(_f32(W2)), ptr(_f32(Wst)), ptr(_bf16(DV)), ptr(_bf16(DA)), ptr(gx0), n, L, S, _s())
+
+
 def conv_lengths(inp, out, pad_total, kernel=3, stride=2):
     """NeMo calc_length for one conv stage: out = floor((in + pad_total - kernel) / stride) + 1."""
     assert out.numel() == inp.numel() and out.dtype == torch.int64

@@ -17,9 +17,10 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _run(cfg, wav, wl, tg, tl, eps):
+def _run(cfg, wav, wl, tg, tl, eps, teacher_graph=True):
     from kdfm.engine import Ver5Engine
     eng = Ver5Engine(cfg, "cuda", teacher_seed=0, student_seed=1, heads_seed=2)
+    eng.teacher_graph = teacher_graph
     eng.set_seed(77)
     eng.advance_rng()
     ctx = eng.forward(wav, wl, tg, tl, train=True, eps=eps)
@@ -29,8 +30,10 @@ def _run(cfg, wav, wl, tg, tl, eps):
     return eng.losses.clone(), feats, eng.student.grads()
 
 
-@pytest.mark.parametrize("which", ["f32-parity", "bf16-train"])
+@pytest.mark.parametrize("which", ["f32-parity", "bf16-train", "bf16-train-teacher-graph-vs-eager"])
 def test_step_is_bitwise_reproducible(which):
+    """The third case replays the frozen teacher as a captured HIP graph in run 1 and issues it
+    eagerly in run 2: the graph must not change a single bit."""
     from kdfm.config import DEFAULT, PARITY
     g = torch.Generator().manual_seed(21)
     if which == "f32-parity":
@@ -48,7 +51,7 @@ def test_step_is_bitwise_reproducible(which):
     T = ((N // cfg.hop) // 2) // 2 + 1
     eps = torch.randn(cfg.n_layers * B * T, cfg.latent, generator=g).cuda() if which == "f32-parity" else None
     l1, f1, g1 = _run(cfg, wav, wl, tg, tl, eps)
-    l2, f2, g2 = _run(cfg, wav, wl, tg, tl, eps)
+    l2, f2, g2 = _run(cfg, wav, wl, tg, tl, eps, teacher_graph=not which.endswith("vs-eager"))
     assert all(torch.isfinite(v).all() for v in g1.values())
     assert torch.equal(f1, f2), "hooked layer outputs differ between runs"
     bad = [k for k in g1 if not torch.equal(g1[k], g2[k])]

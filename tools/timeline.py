@@ -64,3 +64,45 @@ def main():
 
 if __name__ == "__main__":
     main()
+
+
+def gaps(path, main_sid=None, min_us=30.0):
+    """Main-stream idle gaps inside the last full step, with the kernels other streams run during them."""
+    rows = []
+    clean = lambda n: n.replace("kdfm::(anonymous namespace)::", "").split("(")[0]  # noqa: E731
+    c = sqlite3.connect(path)
+    for name, st, en, sid, qid in c.execute("select name, start, end, stream_id, queue_id from kernels"):
+        rows.append((int(st), int(en), str(sid if sid is not None else qid), clean(name)))
+    rows.sort()
+    ends = [e for s, e, q, n in rows if "adamw_kernel" in n]
+    t0, t1 = ends[-3], ends[-2]
+    step = [r for r in rows if r[0] >= t0 and r[1] <= t1]
+    busy = defaultdict(float)
+    for s, e, q, n in step:
+        busy[q] += e - s
+    main = main_sid or max(busy, key=busy.get)
+    mk = [(s, e, n) for s, e, q, n in step if q == main]
+    total = 0.0
+    agg = defaultdict(float)
+    prev_end, prev_name = t0, "step start"
+    out = []
+    for s, e, n in mk:
+        g = (s - prev_end) / 1e3
+        if g > min_us:
+            others = defaultdict(float)
+            for s2, e2, q2, n2 in step:
+                if q2 != main and e2 > prev_end and s2 < s:
+                    others[f"{q2}:{n2[:28]}"] += (min(e2, s) - max(s2, prev_end)) / 1e3
+            top = sorted(others.items(), key=lambda kv: -kv[1])[:3]
+            out.append((g, prev_name[:30], n[:30], top))
+            total += g
+            for k, v in others.items():
+                agg[k.split(":")[0]] += v
+        prev_end, prev_name = max(prev_end, e), n
+    print(f"main stream {main}: {len(out)} gaps > {min_us} us, {total / 1e3:.3f} ms total")
+    for g, a, b, top in sorted(out, key=lambda x: -x[0])[:15]:
+        print(f"  {g:8.1f} us after {a:30s} before {b:30s} | " + "; ".join(f"{k} {v:.0f}" for k, v in top))
+
+
+if __name__ == "__main__" and len(sys.argv) > 2 and sys.argv[2] == "gaps":
+    gaps(sys.argv[1])
