@@ -156,6 +156,22 @@ int kdfm_wgrad_bf16(const uint16_t* dY, const uint16_t* X, float* dW, int64_t ld
  *   backward: from dtr, the saved A and the optional gradient gxS of xS: DV[j] = dL/dv_j and
  *     DA[j] = dL/d(pre-activation of a_j) as bf16 (S, n, L), gx0 = dL/dx0 (f32).
  * W1 row stride ld_w1 (the time-embedding columns of meta_encoder.0 follow the first L). */
+/* Fused relative-position attention backward (bf16 MFMA; NeMo RelPositionMultiHeadAttention,
+ * Appendix A.7): from dO (rows, d), the forward's q+u / q+v rows, the fused q|k|v rows (ld 3d), the
+ * projected positions pos (2T-1, d), the forward output O (rows, d) and the saved probabilities
+ * P (B, H, T, T) it writes
+ *   dqu = dS K, dqv_i = sum_j dS[i][j] pos[T-1-i+j]  (rows, d),  dK, dV into dqkv[:, d:] and [:, 2d:],
+ *   dpos[r] = sum_{b,i} dS[i][r-T+1+i] qv_i  (2T-1, d, overwritten)
+ * with dS = P (dP - r) scale, r_i = dO_i . O_i (= rowsum(dP P)) and dP the dropout-masked dO V^T (counter-RNG mask of the
+ * forward).  No T x T intermediate in HBM; deterministic (ordered chunk fold, no atomics).  Head
+ * dim d/H <= 48.  ws: kdfm_relpos_attn_bwd_ws floats. */
+int64_t kdfm_relpos_attn_bwd_ws(int64_t B, int64_t H, int64_t T, int64_t d);
+int kdfm_relpos_attn_bwd(const float* dO, const float* O, const float* qu, const float* qv, const float* qkv,
+                         const float* pos, const float* P, const int64_t* lengths, float* dqu, float* dqv, float* dqkv,
+                         float* dpos,
+                         float* ws, int64_t ws_len, int64_t B, int64_t H, int64_t T, int64_t d, float scale,
+                         float dropout_p, const uint64_t* seed, uint64_t rng_stream, void* stream);
+
 int kdfm_fm_chain_fwd(const float* x0, const float* zt, const float* W1, int64_t ld_w1, const float* cvec,
                       const float* W2, const float* b2, const float* Wst, const float* bst, uint16_t* X, uint16_t* A,
                       float* nsx, float* dtr, float* xS, float* loss, float inv, int64_t n, int32_t L, int32_t S,

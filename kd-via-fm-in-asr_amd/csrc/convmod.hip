@@ -517,8 +517,9 @@ int kdfm_bn_silu_bwd(const float* dz, const float* y, const float* mean, const f
     set_error("kdfm_bn_silu_bwd: memset failed");
     return KDFM_ELAUNCH;
   }
-  int64_t gy = ceil_div(rows, 256);
-  if (gy > 512) gy = 512;
+  // ~64 rows per workgroup: the per-channel f64 sums are latency-bound, so spread them wide
+  int64_t gy = ceil_div(rows, 64);
+  if (gy > 1024) gy = 1024;
   if (deterministic()) gy = 1;  // one workgroup per channel group: fixed summation order
   const int64_t rp = ceil_div(rows, gy);
   gy = ceil_div(rows, rp);

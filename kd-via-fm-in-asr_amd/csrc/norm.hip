@@ -133,25 +133,35 @@ struct LnFold {
   float* db[KDFM_LN_FOLD_MAX];
 };
 
-__global__ __launch_bounds__(256) void ln_fold_kernel(LnFold f, int64_t nparts, int d) {
-  __shared__ float red[4][64];
+// 16 waves per block, lane = output column: wave w sums the parts b = w, w + 16, ... with four
+// independent accumulators (many loads in flight; the 4-wave version was latency-bound at ~50 us per
+// layer), then a fixed-order combine in LDS — the same order every run (deterministic).
+constexpr int LNF_WAVES = 16;
+
+__global__ __launch_bounds__(64 * LNF_WAVES) void ln_fold_kernel(LnFold f, int64_t nparts, int d) {
+  __shared__ float red[LNF_WAVES][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int e = blockIdx.y;
   const int c = blockIdx.x * 64 + lane;
   const float* part = f.part[e];
-  float s0 = 0.f, s1 = 0.f;
+  const int64_t ld = 2 * (int64_t)d;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
   if (c < 2 * d) {
     int64_t b = w;
-    for (; b + 4 < nparts; b += 8) {
-      s0 += part[b * 2 * d + c];
-      s1 += part[(b + 4) * 2 * d + c];
+    for (; b + 3 * LNF_WAVES < nparts; b += 4 * LNF_WAVES) {
+      s0 += part[b * ld + c];
+      s1 += part[(b + LNF_WAVES) * ld + c];
+      s2 += part[(b + 2 * LNF_WAVES) * ld + c];
+      s3 += part[(b + 3 * LNF_WAVES) * ld + c];
     }
-    for (; b < nparts; b += 4) s0 += part[b * 2 * d + c];
+    for (; b < nparts; b += LNF_WAVES) s0 += part[b * ld + c];
   }
-  red[w][lane] = s0 + s1;
+  red[w][lane] = (s0 + s1) + (s2 + s3);
   __syncthreads();
   if (w == 0 && c < 2 * d) {
-    const float v = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+    float v = 0.f;
+#pragma unroll
+    for (int i = 0; i < LNF_WAVES; ++i) v += red[i][lane];
     if (c < d)
       f.dg[e][c] += v;
     else
@@ -167,8 +177,8 @@ int ln_fold(const float* const* parts, float* const* dgs, float* const* dbs, int
     f.dg[i] = dgs[i];
     f.db[i] = dbs[i];
   }
-  hipLaunchKernelGGL(ln_fold_kernel, dim3((unsigned)ceil_div(2 * d, 64), (unsigned)n), dim3(256), 0, st, f, nparts,
-                     (int)d);
+  hipLaunchKernelGGL(ln_fold_kernel, dim3((unsigned)ceil_div(2 * d, 64), (unsigned)n), dim3(64 * LNF_WAVES), 0, st, f,
+                     nparts, (int)d);
   return check_launch("kdfm_ln_fold");
 }
 

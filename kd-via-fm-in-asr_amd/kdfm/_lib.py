@@ -74,6 +74,9 @@ SIGNATURES: dict[str, tuple] = {
     "kdfm_gemm_last_route": (_i32, []),
     "kdfm_range_push": (_i32, [C.c_char_p]),
     "kdfm_wgrad_bf16_ws": (_i64, [_i64, _i64, _i64, _i32]),
+    "kdfm_relpos_attn_bwd_ws": (_i64, [_i64, _i64, _i64, _i64]),
+    "kdfm_relpos_attn_bwd": (_i32, [P, P, P, P, P, P, P, P, P, P, P, P, P, _i64, _i64, _i64, _i64, _i64, _f32, _f32, P,
+                                    C.c_uint64, P]),
     "kdfm_wgrad_bf16": (_i32, [P, P, P, _i64, P, _i64, _i64, _i64, _f32, P, _i64, P]),
     "kdfm_fm_chain_fwd": (_i32, [P, P, P, _i64, P, P, P, P, P, P, P, P, P, P, P, _f32, _i64, _i32, _i32, P]),
     "kdfm_fm_chain_bwd": (_i32, [P, P, P, P, _i64, P, P, P, P, P, _i64, _i32, _i32, P]),

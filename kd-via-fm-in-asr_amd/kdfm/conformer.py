@@ -26,6 +26,11 @@ SITE_FF1_ACT, SITE_FF1_OUT, SITE_ATT_P, SITE_ATT_OUT, SITE_CONV_OUT, SITE_FF2_AC
 SITE_PRE = 15
 
 
+# bf16 math: attention backward through the fused kernels of csrc/attn_bwd.hip (KDFM_ATTN_BWD_FUSED=0:
+# the unfused dPd / dAC / dBD path; the f32 parity mode always takes it)
+_ATTN_BWD_FUSED = __import__("os").environ.get("KDFM_ATTN_BWD_FUSED", "1") == "1"
+
+
 def _stream(salt, layer, site):
     return salt * 4096 + (layer + 1) * 16 + site
 
@@ -288,7 +293,10 @@ def layer_forward(cfg, S: EncoderShapes, P, L, li, x, out, pos_emb, lengths, *, 
         # fused flash-style kernel: no AC / BD materialisation; P (and P_drop) only when the
         # backward needs them
         Pm = _empty(B, H, T, T, dev=dev) if save else None
-        Pd = (_empty(B, H, T, T, dev=dev) if pa > 0 else Pm) if save else None
+        if _ATTN_BWD_FUSED:
+            Pd = None   # the fused backward regenerates the dropout mask from the counter RNG
+        else:
+            Pd = (_empty(B, H, T, T, dev=dev) if pa > 0 else Pm) if save else None
         K.relpos_attn_fwd(qu, qv, qkv, ppos, lengths, o, Pm, Pd if pa > 0 else None, B, H, T,
                           1.0 / math.sqrt(dk), pa, seed, _stream(salt, li, SITE_ATT_P))
     else:
@@ -310,7 +318,8 @@ def layer_forward(cfg, S: EncoderShapes, P, L, li, x, out, pos_emb, lengths, *, 
     x2 = _empty(rows, d, dev=dev)
     K.linear(o, P[L + "self_attn.linear_out.weight"], P[L + "self_attn.linear_out.bias"], x2, epi=_lib.EPI_RESID,
              R=x1, rscale=1.0, dropout_p=pd, seed=seed, rng_stream=_stream(salt, li, SITE_ATT_OUT))
-    keep(x1=x1, ln2=ln2, m2=m2, r2=r2, qkv=qkv, qu=qu, qv=qv, ppos=ppos, P=Pm, Pd=Pd, o=o, pa=pa)
+    keep(x1=x1, ln2=ln2, m2=m2, r2=r2, qkv=qkv, qu=qu, qv=qv, ppos=ppos, P=Pm, Pd=Pd, o=o, pa=pa,
+         attn_fused=K.get_math() == "bf16" and dk <= 48 and _ATTN_BWD_FUSED)
     del ln2, qkv, qu, qv, ppos, Pm, Pd, o
 
     # ---- convolution module ----
@@ -452,6 +461,16 @@ def layer_backward(cfg, S: EncoderShapes, P, G, L, li, ctx, dout, pos_emb, lengt
     del dlo
     qkv, Pm, Pd, qu, qv, ppos = ctx["qkv"], ctx["P"], ctx["Pd"], ctx["qu"], ctx["qv"], ctx["ppos"]
     npos = 2 * T - 1
+    if ctx.get("attn_fused"):
+        dqkv = _empty(rows, 3 * d, dev=dev)
+        dqu = _empty(rows, d, dev=dev)
+        dqv = _empty(rows, d, dev=dev)
+        dppos = _empty(npos, d, dev=dev)
+        K.relpos_attn_bwd(do, ctx["o"], qu, qv, qkv, ppos, Pm, lengths, dqu, dqv, dqkv, dppos, B, H, T, 1.0 / math.sqrt(dk),
+                          ctx["pa"], seed, _stream(salt, li, SITE_ATT_P))
+        del do
+        return _attn_bwd_tail(P, G, L, ctx, dqkv, dqu, dqv, dppos, pos_emb, dx2, lng, cfg, pd, seed, salt, li, rows, d,
+                              dev)
     dPd = _empty(B, H, T, T, dev=dev)
     # dPd = dO V^T : A(i,c)=do[b,i,h*dk+c], B(c,j)=V[b,j,h*dk+c]
     K.gemm(do, qkv[:, 2 * d:], dPd, T, T, dk, d, 1, 1, 3 * d, T, 1, amode=_lib.LD_KC, bmode=_lib.LD_KC,
@@ -483,6 +502,11 @@ def layer_backward(cfg, S: EncoderShapes, P, G, L, li, ctx, dout, pos_emb, lengt
     K.gemm(dbd, qv, dppos, npos, dk, T, 1, npos, d, 1, d, 1, amode=_lib.LD_XC, bmode=_lib.LD_XC,
            batch=(B, H), bA=(H * T * npos, T * npos), bB=(T * d, dk), bC=(0, dk), epi=_lib.EPI_ATOMIC)
     del dbd
+    return _attn_bwd_tail(P, G, L, ctx, dqkv, dqu, dqv, dppos, pos_emb, dx2, lng, cfg, pd, seed, salt, li, rows, d, dev)
+
+
+def _attn_bwd_tail(P, G, L, ctx, dqkv, dqu, dqv, dppos, pos_emb, dx2, lng, cfg, pd, seed, salt, li, rows, d, dev):
+    """Pos-bias / linear_pos / q|k|v projection grads, norm_self_att and FFN1 backward."""
     K.colsum(dqu, G[L + "self_attn.pos_bias_u"].view(-1))
     K.colsum(dqv, G[L + "self_attn.pos_bias_v"].view(-1))
     K.axpby(dqu, dqv, dqkv[:, :d], 1.0, 1.0)

@@ -686,6 +686,19 @@ def qkv_prep(qkv, u, v, qu, qv):
     call("kdfm_qkv_prep", ptr(qkv), ptr(u), ptr(v), ptr(qu), ptr(qv), rows, d, _s())
 
 
+def relpos_attn_bwd(do, o, qu, qv, qkv, ppos, P, lengths, dqu, dqv, dqkv, dppos, B, H, T, scale, p, seed, rng_stream):
+    """Fused attention backward (csrc/attn_bwd.hip): dqu, dqv, dK/dV into dqkv[:, d:], dppos."""
+    rows, d = do.shape
+    assert rows == B * T and qkv.shape == (rows, 3 * d) and P.shape == (B, H, T, T) and dppos.shape == (2 * T - 1, d)
+    for t in (do, o, qu, qv, qkv, ppos, P, dqu, dqv, dqkv, dppos):
+        assert t.is_contiguous()
+    assert o.shape == do.shape
+    ws = scratch(do.device, int(_lib.lib().kdfm_relpos_attn_bwd_ws(B, H, T, d)))
+    call("kdfm_relpos_attn_bwd", ptr(do), ptr(o), ptr(qu), ptr(qv), ptr(qkv), ptr(ppos), ptr(P), ptr(_i64(lengths)), ptr(dqu),
+         ptr(dqv), ptr(dqkv), ptr(dppos), ptr(ws), ws.numel(), B, H, T, d, float(scale), float(p), ptr(seed),
+         int(rng_stream), _s())
+
+
 def relpos_attn_fwd(qu, qv, qkv, ppos, lengths, o, P, Pd, B, H, T, scale, p, seed, rng_stream):
     """Fused rel-pos MHA forward (bf16); P / Pd (B,H,T,T) written when given."""
     rows, d = qu.shape

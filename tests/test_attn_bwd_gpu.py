@@ -1,0 +1,130 @@
+"""Fused relative-position attention backward (kdfm_relpos_attn_bwd, csrc/attn_bwd.hip, bf16 MFMA)
+against (a) float64 torch autograd of NeMo's rel-pos attention (Appendix A.7: scores = ((q+u)K^T +
+rel_shift((q+v)Ppos^T)) / sqrt(dk), key mask, softmax, rows of padded queries zeroed, O = P V) with
+no dropout, and (b) the unfused f32 path (dPd GEMM + relpos_softmax_bwd + five batched GEMMs) on
+the same saved P with attention dropout 0.1 (same counter-RNG mask).
+
+Tolerances: relative Frobenius error per gradient (dQu, dQv, dK, dV, dPpos) <= 2e-2 against float64
+(bf16 operands, f32 accumulation) and <= 2e-2 against the unfused f32 kernels; padded keys get
+exactly zero dK / dV; two runs are bitwise identical (no atomics).
+"""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+def _inputs(B, H, T, d, seed):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    rows = B * T
+    qkv = torch.randn(rows, 3 * d, device="cuda", generator=g)
+    qu = torch.randn(rows, d, device="cuda", generator=g)
+    qv = torch.randn(rows, d, device="cuda", generator=g)
+    ppos = torch.randn(2 * T - 1, d, device="cuda", generator=g)
+    do = torch.randn(rows, d, device="cuda", generator=g)
+    lens = torch.tensor([T] + [max(1, T - 23 * (i + 1)) for i in range(B - 1)], dtype=torch.int64, device="cuda")
+    return qkv, qu, qv, ppos, do, lens
+
+
+def _fused(K, qkv, qu, qv, ppos, do, lens, B, H, T, d, p, seed):
+    dk = d // H
+    P = torch.empty(B, H, T, T, device="cuda")
+    o = torch.empty(B * T, d, device="cuda")
+    K.relpos_attn_fwd(qu, qv, qkv, ppos, lens, o, P, None, B, H, T, 1.0 / math.sqrt(dk), p, seed, 11)
+    dqu = torch.empty(B * T, d, device="cuda")
+    dqv = torch.empty_like(dqu)
+    dqkv = torch.zeros(B * T, 3 * d, device="cuda")
+    dpos = torch.empty(2 * T - 1, d, device="cuda")
+    K.relpos_attn_bwd(do, o, qu, qv, qkv, ppos, P, lens, dqu, dqv, dqkv, dpos, B, H, T, 1.0 / math.sqrt(dk), p, seed, 11)
+    torch.cuda.synchronize()
+    return P, dqu, dqv, dqkv[:, d:2 * d], dqkv[:, 2 * d:], dpos
+
+
+def _torch_grads(qkv, qu, qv, ppos, do, lens, B, H, T, d):
+    dk = d // H
+    f = lambda t: t.double().detach().clone().requires_grad_(True)  # noqa: E731
+    q_u, q_v, k, v, pp = f(qu), f(qv), f(qkv[:, d:2 * d]), f(qkv[:, 2 * d:]), f(ppos)
+    sh = lambda t: t.view(B, T, H, dk).permute(0, 2, 1, 3)  # noqa: E731
+    ac = sh(q_u) @ sh(k).transpose(-1, -2)
+    bdf = torch.einsum("bhic,hrc->bhir", sh(q_v), pp.view(2 * T - 1, H, dk).permute(1, 0, 2))
+    idx = (T - 1 - torch.arange(T, device="cuda")[:, None] + torch.arange(T, device="cuda")[None, :])
+    bd = torch.gather(bdf, 3, idx.expand(B, H, T, T))
+    s = (ac + bd) / math.sqrt(dk)
+    keym = torch.arange(T, device="cuda")[None, :] < lens[:, None]
+    s = s.masked_fill(~keym[:, None, None, :], float("-inf"))
+    P = torch.softmax(s, -1)
+    P = torch.where(keym[:, None, :, None], P, torch.zeros_like(P))
+    O = (P @ sh(v)).permute(0, 2, 1, 3).reshape(B * T, d)
+    loss = (O * do.double()).sum()
+    return torch.autograd.grad(loss, [q_u, q_v, k, v, pp])
+
+
+@pytest.mark.parametrize("B,H,T,d", [(3, 2, 401, 88), (2, 4, 130, 176), (2, 2, 77, 88)])
+def test_attn_bwd_matches_float64(B, H, T, d):
+    from kdfm import kernels as K
+    qkv, qu, qv, ppos, do, lens = _inputs(B, H, T, d, T + d)
+    seed = torch.tensor([99], dtype=torch.int64, device="cuda")
+    _, dqu, dqv, dk_, dv_, dpos = _fused(K, qkv, qu, qv, ppos, do, lens, B, H, T, d, 0.0, seed)
+    ref = _torch_grads(qkv, qu, qv, ppos, do, lens, B, H, T, d)
+    for name, got, want in zip(("dQu", "dQv", "dK", "dV", "dPpos"), (dqu, dqv, dk_, dv_, dpos), ref):
+        assert _rel(got, want) <= 2e-2, (name, _rel(got, want))
+    # keys past an utterance's length receive no gradient
+    for bi in range(B):
+        L = int(lens[bi])
+        if L < T:
+            assert dk_.view(B, T, d)[bi, L:].abs().max().item() == 0.0
+            assert dv_.view(B, T, d)[bi, L:].abs().max().item() == 0.0
+
+
+def test_attn_bwd_matches_unfused_with_dropout():
+    from kdfm import _lib
+    from kdfm import kernels as K
+    B, H, T, d, p = 2, 2, 401, 88, 0.1
+    dk = d // H
+    npos = 2 * T - 1
+    qkv, qu, qv, ppos, do, lens = _inputs(B, H, T, d, 5)
+    seed = torch.tensor([4242], dtype=torch.int64, device="cuda")
+    P, dqu, dqv, dk_, dv_, dpos = _fused(K, qkv, qu, qv, ppos, do, lens, B, H, T, d, p, seed)
+    again = _fused(K, qkv, qu, qv, ppos, do, lens, B, H, T, d, p, seed)
+    for a, b in zip((dqu, dqv, dk_, dv_, dpos), again[1:]):
+        assert torch.equal(a, b), "fused attention backward is not bitwise reproducible"
+    # unfused f32 chain on the same P (Pd rebuilt from the same RNG by relpos_softmax_fwd's twin:
+    # take it from the forward kernel run with a P_drop output)
+    Pd = torch.empty_like(P)
+    o = torch.empty(B * T, d, device="cuda")
+    K.relpos_attn_fwd(qu, qv, qkv, ppos, lens, o, torch.empty_like(P), Pd, B, H, T, 1.0 / math.sqrt(dk), p, seed, 11)
+    f32 = dict(math="f32")
+    dPd = torch.empty(B, H, T, T, device="cuda")
+    K.gemm(do, qkv[:, 2 * d:], dPd, T, T, dk, d, 1, 1, 3 * d, T, 1, amode=_lib.LD_KC, bmode=_lib.LD_KC,
+           batch=(B, H), bA=(T * d, dk), bB=(T * 3 * d, dk), bC=(H * T * T, T * T), **f32)
+    dac = torch.empty(B, H, T, T, device="cuda")
+    dbd = torch.empty(B, H, T, npos, device="cuda")
+    K.relpos_softmax_bwd(P, dPd, dac, dbd, B, H, T, 1.0 / math.sqrt(dk), p, seed, 11)
+    rows = B * T
+    r_dv = torch.zeros(rows, d, device="cuda")
+    K.gemm(Pd, do, r_dv, T, dk, T, 1, T, d, 1, d, 1, amode=_lib.LD_XC, bmode=_lib.LD_XC,
+           batch=(B, H), bA=(H * T * T, T * T), bB=(T * d, dk), bC=(T * d, dk), **f32)
+    r_dqu = torch.zeros(rows, d, device="cuda")
+    K.gemm(dac, qkv[:, d:], r_dqu, T, dk, T, T, 1, 3 * d, 1, d, 1, amode=_lib.LD_KC, bmode=_lib.LD_XC,
+           batch=(B, H), bA=(H * T * T, T * T), bB=(T * 3 * d, dk), bC=(T * d, dk), **f32)
+    r_dk = torch.zeros(rows, d, device="cuda")
+    K.gemm(dac, qu, r_dk, T, dk, T, 1, T, d, 1, d, 1, amode=_lib.LD_XC, bmode=_lib.LD_XC,
+           batch=(B, H), bA=(H * T * T, T * T), bB=(T * d, dk), bC=(T * d, dk), **f32)
+    r_dqv = torch.zeros(rows, d, device="cuda")
+    K.gemm(dbd, ppos, r_dqv, T, dk, npos, npos, 1, d, 1, d, 1, amode=_lib.LD_KC, bmode=_lib.LD_XC,
+           batch=(B, H), bA=(H * T * npos, T * npos), bB=(0, dk), bC=(T * d, dk), **f32)
+    r_dpos = torch.zeros(npos, d, device="cuda")
+    K.gemm(dbd, qv, r_dpos, npos, dk, T, 1, npos, d, 1, d, 1, amode=_lib.LD_XC, bmode=_lib.LD_XC,
+           batch=(B, H), bA=(H * T * npos, T * npos), bB=(T * d, dk), bC=(0, dk), epi=_lib.EPI_ATOMIC, **f32)
+    torch.cuda.synchronize()
+    for name, got, want in zip(("dQu", "dQv", "dK", "dV", "dPpos"), (dqu, dqv, dk_, dv_, dpos),
+                               (r_dqu, r_dqv, r_dk, r_dv, r_dpos)):
+        assert _rel(got, want) <= 2e-2, (name, _rel(got, want))

@@ -3,7 +3,11 @@
 * the reference's training_step code shape (asr_train_diffm.py:731-828: forward with forward hooks on
   encoder.layers, CTC via self.loss, teacher decoder on tch_feats[-1], per-layer ver5 losses) runs
   on the modules and `loss.backward()` fills every trainable .grad;
-* loss and gradients match the CPU oracle on the same weights (parity mode, fp32 MFMA);
+* loss and gradients match the CPU oracle on the same weights (parity mode, fp32 MFMA).  As in
+  tests/test_step_parity_gpu.py the reference is the oracle evaluated in float64 and a gradient
+  passes at 2e-3 of its max or within 4x the float32 oracle's own distance to float64 (the f32
+  rounding noise of the step: the denoiser's first conv weight gradient sums cancelling terms and
+  moves by ~1e-5 under any change of f32 summation order);
 * the module weights hand over to the fused Ver5Engine, which computes the same loss.
 """
 import pytest
@@ -61,21 +65,26 @@ def test_module_training_step_matches_oracle():
                          "adapter.", "denoiser.", "fm_latent.")):
             p[k] = v
     names = O.trainable_names(p)
+    p64 = {k: (v.double() if v.is_floating_point() else v) for k, v in p.items()}
     for k in names:
         p[k] = p[k].clone().requires_grad_(True)
+        p64[k] = p64[k].clone().requires_grad_(True)
     eps_o = torch.stack([e.view(B, T, 96).permute(0, 2, 1) for e in eps])
-    out = O.ver5_step(p, wav, wl, tg, tl, ocfg, eps_o)
+    out = O.ver5_step(p64, wav.double(), wl, tg, tl, ocfg, eps_o.double())
+    out32 = O.ver5_step(p, wav, wl, tg, tl, ocfg, eps_o)
     assert abs(loss.item() - out["loss"].item()) <= 2e-4 * abs(out["loss"].item()) + 1e-4
-    og = torch.autograd.grad(out["loss"], [p[k] for k in names], allow_unused=True)
+    og = torch.autograd.grad(out["loss"], [p64[k] for k in names], allow_unused=True)
+    og32 = torch.autograd.grad(out32["loss"], [p[k] for k in names], allow_unused=True)
     params = dict(model.named_parameters())
     checked = 0
-    for k, gr in zip(names, og):
+    for k, gr, g32 in zip(names, og, og32):
         if gr is None or k.endswith(("self_attn.linear_k.bias", "conv.depthwise_conv.bias")):
             continue
         mine = params[k].grad
         assert mine is not None, k
-        err = (mine.detach().cpu() - gr).abs().max().item()
-        assert err <= 2e-3 * gr.abs().max().item() + 1e-6, (k, err)
+        err = (mine.detach().cpu().double() - gr).abs().max().item()
+        noise = (g32.double() - gr).abs().max().item() if g32 is not None else 0.0
+        assert err <= 2e-3 * gr.abs().max().item() + 1e-6 or err <= 4.0 * noise, (k, err, noise)
         checked += 1
     assert checked > 60
 
