@@ -126,9 +126,10 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AbP p) {
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int T = (int)p.T, dk = (int)p.dkh;
-  const int64_t bh = blockIdx.y;
+  const Blk3 blk = xcd_block3();
+  const int64_t bh = blk.y;
   const int64_t b = bh / p.H, h = bh - b * p.H;
-  const int i0 = blockIdx.x * BQ;
+  const int i0 = (int)blk.x * BQ;
   const int len = p.lens ? (int)min<int64_t>(p.lens[b], p.T) : T;
   const int nkb = (len + BK - 1) / BK;
   const int npos = 2 * T - 1;
@@ -258,9 +259,10 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkv_kernel(AbP p) {
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int T = (int)p.T, dk = (int)p.dkh;
-  const int64_t bh = blockIdx.y;
+  const Blk3 blk = xcd_block3();
+  const int64_t bh = blk.y;
   const int64_t b = bh / p.H, h = bh - b * p.H;
-  const int j0 = blockIdx.x * BK;
+  const int j0 = (int)blk.x * BK;
   const int len = p.lens ? (int)min<int64_t>(p.lens[b], p.T) : T;
   const int64_t hoff = h * p.dkh;
   for (int e = threadIdx.x; e < BQ * (BDK - dk); e += 256) Os[(e / (BDK - dk)) * LR + dk + e % (BDK - dk)] = 0;
@@ -369,9 +371,10 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dpos_kernel(AbP p) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int T = (int)p.T, dk = (int)p.dkh;
   const int npos = 2 * T - 1;
-  const int r0 = blockIdx.x * 64;
-  const int64_t h = blockIdx.y;
-  const int64_t bchunk = blockIdx.z;
+  const Blk3 blk = xcd_block3();
+  const int r0 = (int)blk.x * 64;
+  const int64_t h = blk.y;
+  const int64_t bchunk = blk.z;
   const int64_t hoff = h * p.dkh;
   const uint64_t seed = (p.p_drop > 0.f) ? load_seed(p.seed) : 0ull;
   const float keep = (p.p_drop > 0.f) ? 1.f / (1.f - p.p_drop) : 1.f;

@@ -82,9 +82,10 @@ __global__ __launch_bounds__(256, 2) void relpos_attn_fwd_kernel(AttnP p) {
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int T = (int)p.T, dk = (int)p.dk;
-  const int64_t bh = blockIdx.y;
+  const Blk3 blk = xcd_block3();
+  const int64_t bh = blk.y;
   const int64_t b = bh / p.H, h = bh - b * p.H;
-  const int i0 = blockIdx.x * AQ;
+  const int i0 = (int)blk.x * AQ;
   const int len = p.lens ? (int)p.lens[b] : T;
   const int nkb = (min(len, T) + AKB - 1) / AKB;  // key blocks with at least one valid key
   const int npos = 2 * T - 1;

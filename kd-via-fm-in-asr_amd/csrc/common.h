@@ -90,6 +90,29 @@ __device__ __forceinline__ int64_t xcd_block() {
   const int64_t per = n / kNumXcd, rem = n % kNumXcd;
   return x < rem ? x * (per + 1) + local : rem * (per + 1) + (x - rem) * per + local;
 }
+// The same bijection over a 3-D grid (dispatched x fastest, then y, then z): returns the logical
+// block (bx, by, bz).  Attention grids put the blocks of one (utterance, head) along x, so they
+// land on one XCD and share its L2 for K / V / positions instead of fetching them once per XCD.
+struct Blk3 { int64_t x, y, z; };
+__device__ __forceinline__ int64_t xcd_linear() {
+  const int64_t nx = gridDim.x, ny = gridDim.y;
+  const int64_t b = blockIdx.x + nx * (blockIdx.y + ny * (int64_t)blockIdx.z);
+  const int64_t n = nx * ny * (int64_t)gridDim.z;
+  const int64_t x = b % kNumXcd, local = b / kNumXcd;
+  const int64_t per = n / kNumXcd, rem = n % kNumXcd;
+  return x < rem ? x * (per + 1) + local : rem * (per + 1) + (x - rem) * per + local;
+}
+__device__ __forceinline__ Blk3 xcd_block3() {
+  const int64_t nx = gridDim.x, ny = gridDim.y, l = xcd_linear();
+  return Blk3{l % nx, (l / nx) % ny, l / (nx * ny)};
+}
+// y-fastest variant for GEMM grids (x = row tiles, y = column tiles): the column tiles of one row
+// block share its A rows, so they go to the same XCD.
+__device__ __forceinline__ Blk3 xcd_block3_yfast() {
+  const int64_t nx = gridDim.x, ny = gridDim.y, l = xcd_linear();
+  const int64_t r = l % (nx * ny);
+  return Blk3{r / ny, r % ny, l / (nx * ny)};
+}
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

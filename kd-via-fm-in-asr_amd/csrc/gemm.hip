@@ -191,7 +191,8 @@ __global__ __launch_bounds__(NT) void gemm_kernel(P p) {
   float* As = smem;
   float* Bs = smem + LDS_ELEMS;
 
-  const int64_t z = blockIdx.z;
+  const Blk3 blk = xcd_block3_yfast();
+  const int64_t z = blk.z;
   const int64_t split = z % p.splitk;
   const int64_t bz = z / p.splitk;
   const int64_t b1 = bz / p.batch2, b2 = bz % p.batch2;
@@ -199,8 +200,8 @@ __global__ __launch_bounds__(NT) void gemm_kernel(P p) {
   const float* B = p.B + b1 * p.bB1 + b2 * p.bB2;
   const int64_t cOff = b1 * p.bC1 + b2 * p.bC2;
 
-  const int64_t m0 = (int64_t)blockIdx.x * BM;
-  const int64_t n0 = (int64_t)blockIdx.y * BN;
+  const int64_t m0 = blk.x * BM;
+  const int64_t n0 = blk.y * BN;
   const int64_t kchunk = ceil_div(ceil_div(p.K, p.splitk), BK) * BK;
   const int64_t kbeg = split * kchunk;
   const int64_t kend = (kbeg + kchunk < p.K) ? (kbeg + kchunk) : p.K;
