@@ -88,38 +88,178 @@ __global__ __launch_bounds__(256) void log_softmax_bwd_kernel(const float* __res
   }
 }
 
-// One block per utterance.  alpha/beta workspaces (B, T, S) in log space; nll (B);
-// grad (B, T, C) = scale * (exp(lp) - posterior) for t < len, 0 beyond (or all 0 if infeasible).
-__global__ __launch_bounds__(256) void ctc_kernel(const float* __restrict__ lp, const int64_t* __restrict__ targets,
-                                                  const int64_t* __restrict__ in_len, const int64_t* __restrict__ tgt_len,
-                                                  float* __restrict__ alpha, float* __restrict__ beta,
-                                                  float* __restrict__ nll_out, float* __restrict__ grad, int64_t T,
-                                                  int C, int64_t Umax, int blank, float scale, int zero_inf) {
+// CTC in two launches (the alpha / beta recursions are latency-bound chains over the frames):
+//  ctc_ab_kernel, grid (B, 2): y = 0 runs the alpha recursion forwards and y = 1 the beta recursion
+//    backwards, concurrently.  SPT states per thread; the emissions of CH frames are gathered into
+//    registers per chunk (one memory latency per CH frames instead of one per frame), the chunk's
+//    alpha / beta values stay in registers and are stored at the chunk's end, and one barrier per
+//    frame orders the ping-pong LDS rows.  The alpha block also writes the utterance's nll.
+//  ctc_grad_kernel, grid (B, ceil(T / CTC_FPB)): posteriors and the logits gradient, independent
+//    across frames.  Workspaces alpha / beta (B, T, 2 Umax + 1) in log space; nll (B);
+//    grad (B, T, C) = scale * (exp(lp) - posterior) for t < len, 0 beyond (all 0 / NaN if infeasible).
+// Same recursions, the same lse2 order and the same fixed-order posterior sums as a single-block
+// formulation: the result is bitwise reproducible.
+constexpr int CTC_FPB = 4;
+
+__device__ __forceinline__ int ctc_label(const int64_t* tg, int64_t s, int blank) {
+  return (s & 1) ? (int)tg[s >> 1] : blank;
+}
+
+template <int SPT, int CH>
+__global__ __launch_bounds__(1024) void ctc_ab_kernel(const float* __restrict__ lp, const int64_t* __restrict__ targets,
+                                                      const int64_t* __restrict__ in_len,
+                                                      const int64_t* __restrict__ tgt_len, float* __restrict__ alpha,
+                                                      float* __restrict__ beta, float* __restrict__ nll_out, int64_t T,
+                                                      int C, int64_t Umax, int blank, int zero_inf) {
   extern __shared__ float sh[];
   const int64_t b = blockIdx.x;
+  const bool bwd = blockIdx.y == 1;
+  const int64_t S_max = 2 * Umax + 1;
+  const int64_t U = tgt_len[b] < Umax ? tgt_len[b] : Umax;
+  const int S = (int)(2 * U + 1);
+  const int64_t Tb = in_len[b] < T ? in_len[b] : T;
+  if (Tb <= 0) {
+    if (!bwd && threadIdx.x == 0) nll_out[b] = (U == 0 || !zero_inf) ? (U == 0 ? 0.f : INFINITY) : 0.f;
+    return;
+  }
+  const float* lpb = lp + b * T * C;
+  const int64_t* tg = targets + b * Umax;
+  float* out = (bwd ? beta : alpha) + b * T * S_max;
+  float* cur = sh;
+  float* nxt = sh + S_max;
+  int lab[SPT];
+  bool skip[SPT];
+#pragma unroll
+  for (int k = 0; k < SPT; ++k) {
+    const int s = threadIdx.x + k * blockDim.x;
+    lab[k] = blank;
+    skip[k] = false;
+    if (s < S) {
+      lab[k] = ctc_label(tg, s, blank);
+      if (!bwd) skip[k] = s >= 2 && lab[k] != blank && lab[k] != ctc_label(tg, s - 2, blank);
+      else skip[k] = s + 2 < S && lab[k] != blank && lab[k] != ctc_label(tg, s + 2, blank);
+    }
+  }
+  const int64_t tfirst = bwd ? Tb - 1 : 0;
+#pragma unroll
+  for (int k = 0; k < SPT; ++k) {
+    const int s = threadIdx.x + k * blockDim.x;
+    if (s < S) {
+      float v = NEG_INF;
+      if (!bwd) {
+        if (s == 0) v = lpb[blank];
+        if (s == 1) v = lpb[lab[k]];
+      } else {
+        if (s == S - 1) v = lpb[tfirst * C + blank];
+        if (S >= 2 && s == S - 2) v = lpb[tfirst * C + lab[k]];
+      }
+      cur[s] = v;
+      out[tfirst * S_max + s] = v;
+    }
+  }
+  __syncthreads();
+  for (int64_t n0 = 1; n0 < Tb; n0 += CH) {
+    float em[SPT][CH];
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+      const int64_t n = n0 + j;
+      const int64_t t = bwd ? Tb - 1 - n : n;
+#pragma unroll
+      for (int k = 0; k < SPT; ++k) {
+        const int s = threadIdx.x + k * blockDim.x;
+        em[k][j] = (n < Tb && s < S) ? lpb[t * C + lab[k]] : 0.f;
+      }
+    }
+    float av[SPT][CH];
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+      if (n0 + j < Tb) {   // uniform over the block
+#pragma unroll
+        for (int k = 0; k < SPT; ++k) {
+          const int s = threadIdx.x + k * blockDim.x;
+          av[k][j] = NEG_INF;
+          if (s < S) {
+            float a = cur[s];
+            if (!bwd) {
+              if (s >= 1) a = lse2(a, cur[s - 1]);
+              if (skip[k]) a = lse2(a, cur[s - 2]);
+            } else {
+              if (s + 1 < S) a = lse2(a, cur[s + 1]);
+              if (skip[k]) a = lse2(a, cur[s + 2]);
+            }
+            const float v = (a == NEG_INF) ? NEG_INF : a + em[k][j];
+            nxt[s] = v;
+            av[k][j] = v;
+          }
+        }
+        __syncthreads();
+        float* tmp = cur; cur = nxt; nxt = tmp;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+      const int64_t n = n0 + j;
+      const int64_t t = bwd ? Tb - 1 - n : n;
+#pragma unroll
+      for (int k = 0; k < SPT; ++k) {
+        const int s = threadIdx.x + k * blockDim.x;
+        if (n < Tb && s < S) out[t * S_max + s] = av[k][j];
+      }
+    }
+  }
+  if (!bwd && threadIdx.x == 0) {
+    float ll = cur[S - 1];
+    if (S >= 2) ll = lse2(ll, cur[S - 2]);
+    const float nll = -ll;
+    nll_out[b] = (!(nll < INFINITY) && zero_inf) ? 0.f : nll;
+  }
+}
+
+__global__ __launch_bounds__(256) void ctc_grad_kernel(const float* __restrict__ lp, const int64_t* __restrict__ targets,
+                                                       const int64_t* __restrict__ in_len,
+                                                       const int64_t* __restrict__ tgt_len,
+                                                       const float* __restrict__ alpha, const float* __restrict__ beta,
+                                                       float* __restrict__ grad, int64_t T, int C, int64_t Umax,
+                                                       int blank, float scale, int zero_inf) {
+  extern __shared__ float sh[];
+  const int64_t b = blockIdx.x;
+  const int64_t t0 = (int64_t)blockIdx.y * CTC_FPB;
+  const int64_t t1 = t0 + CTC_FPB < T ? t0 + CTC_FPB : T;
   const int64_t S_max = 2 * Umax + 1;
   const int64_t U = tgt_len[b] < Umax ? tgt_len[b] : Umax;
   const int64_t S = 2 * U + 1;
-  int64_t Tb = in_len[b] < T ? in_len[b] : T;
-  float* prev = sh;                      // S_max
-  float* cur = sh + S_max;               // S_max
-  int* lab = reinterpret_cast<int*>(sh + 2 * S_max);  // S_max
-  float* contrib = sh + 3 * S_max;       // S_max: per-position posterior term of the current frame
-  int* nxt = reinterpret_cast<int*>(sh + 4 * S_max);  // S_max: next odd position with the same label
-  int* head = reinterpret_cast<int*>(sh + 5 * S_max);  // C: first odd position of each label (-1: none)
-  __shared__ float nll_sh, blank_sh;
+  const int64_t Tb = in_len[b] < T ? in_len[b] : T;
+  float* gb = grad + b * T * C;
+  if (Tb <= 0) {
+    for (int64_t i = t0 * C + threadIdx.x; i < t1 * C; i += blockDim.x) gb[i] = 0.f;
+    return;
+  }
+  const float* al = alpha + b * T * S_max;
+  const float* be = beta + b * T * S_max;
+  float ll = al[(Tb - 1) * S_max + S - 1];
+  if (S >= 2) ll = lse2(ll, al[(Tb - 1) * S_max + S - 2]);
+  const float nll = -ll;
+  if (!(nll < INFINITY)) {
+    const float fill = zero_inf ? 0.f : NAN;
+    for (int64_t i = t0 * C + threadIdx.x; i < t1 * C; i += blockDim.x) gb[i] = fill;
+    return;
+  }
+  const int64_t tv = t1 < Tb ? t1 : Tb;    // frames of this block inside the utterance: [t0, tv)
+  for (int64_t i = (t0 > tv ? t0 : tv) * C + threadIdx.x; i < t1 * C; i += blockDim.x) gb[i] = 0.f;
+  if (t0 >= tv) return;
+  float* contrib = sh;                                  // S_max
+  int* lab = reinterpret_cast<int*>(sh + S_max);        // S_max
+  int* nxt = reinterpret_cast<int*>(sh + 2 * S_max);    // S_max: next odd position with the same label
+  int* head = reinterpret_cast<int*>(sh + 3 * S_max);   // C: first odd position of each label (-1: none)
+  __shared__ float blank_sh;
   const float* lpb = lp + b * T * C;
-  float* al = alpha + b * T * S_max;
-  float* be = beta + b * T * S_max;
-  for (int64_t s = threadIdx.x; s < S; s += blockDim.x)
-    lab[s] = (s & 1) ? (int)targets[b * Umax + (s >> 1)] : blank;
+  for (int64_t s = threadIdx.x; s < S; s += blockDim.x) lab[s] = ctc_label(targets + b * Umax, s, blank);
   __syncthreads();
-  // per-label position lists (built once per utterance by one lane): the posterior of class c at a
-  // frame is summed over its positions in ascending order, a fixed order (no LDS atomics), so the
-  // logits gradient is bitwise reproducible
+  // per-label position lists: the posterior of class c is summed over its positions in ascending
+  // order, a fixed order (no LDS atomics), so the logits gradient is bitwise reproducible
   if (threadIdx.x == 0) {
     for (int c = 0; c < C; ++c) head[c] = -1;
-    for (int64_t s = S - 2; s >= 1; s -= 2) {  // S = 2U+1: the odd (label) positions
+    for (int64_t s = S - 2; s >= 1; s -= 2) {
       const int l = lab[s];
       if (l >= 0 && l < C) {
         nxt[s] = head[l];
@@ -128,71 +268,9 @@ __global__ __launch_bounds__(256) void ctc_kernel(const float* __restrict__ lp, 
     }
   }
   __syncthreads();
-  if (Tb <= 0) {
-    if (threadIdx.x == 0) nll_out[b] = (U == 0 || !zero_inf) ? (U == 0 ? 0.f : INFINITY) : 0.f;
-    for (int64_t i = threadIdx.x; i < T * C; i += blockDim.x) grad[b * T * C + i] = 0.f;
-    return;
-  }
-  // ---- alpha ----
-  for (int64_t s = threadIdx.x; s < S; s += blockDim.x) {
-    float v = NEG_INF;
-    if (s == 0) v = lpb[blank];
-    if (s == 1) v = lpb[lab[1]];
-    prev[s] = v;
-    al[s] = v;
-  }
-  __syncthreads();
-  for (int64_t t = 1; t < Tb; ++t) {
+  for (int64_t t = t0; t < tv; ++t) {
     for (int64_t s = threadIdx.x; s < S; s += blockDim.x) {
-      float a = prev[s];
-      if (s >= 1) a = lse2(a, prev[s - 1]);
-      if (s >= 2 && lab[s] != blank && lab[s] != lab[s - 2]) a = lse2(a, prev[s - 2]);
-      const float v = (a == NEG_INF) ? NEG_INF : a + lpb[t * C + lab[s]];
-      cur[s] = v;
-      al[t * S_max + s] = v;
-    }
-    __syncthreads();
-    float* tmp = prev; prev = cur; cur = tmp;
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    float ll = prev[S - 1];
-    if (S >= 2) ll = lse2(ll, prev[S - 2]);
-    nll_sh = -ll;
-  }
-  __syncthreads();
-  const float nll = nll_sh;
-  const bool infeasible = !(nll < INFINITY);
-  if (threadIdx.x == 0) nll_out[b] = (infeasible && zero_inf) ? 0.f : nll;
-  if (infeasible) {
-    const float fill = zero_inf ? 0.f : NAN;
-    for (int64_t i = threadIdx.x; i < T * C; i += blockDim.x) grad[b * T * C + i] = fill;
-    return;
-  }
-  // ---- beta + gradient, walking t backwards ----
-  for (int64_t s = threadIdx.x; s < S; s += blockDim.x) {
-    float v = NEG_INF;
-    if (s == S - 1) v = lpb[(Tb - 1) * C + blank];
-    if (S >= 2 && s == S - 2) v = lpb[(Tb - 1) * C + lab[S - 2]];
-    prev[s] = v;
-    be[(Tb - 1) * S_max + s] = v;
-  }
-  __syncthreads();
-  for (int64_t t = Tb - 1; t >= 0; --t) {
-    if (t < Tb - 1) {
-      for (int64_t s = threadIdx.x; s < S; s += blockDim.x) {
-        float a = prev[s];
-        if (s + 1 < S) a = lse2(a, prev[s + 1]);
-        if (s + 2 < S && lab[s] != blank && lab[s] != lab[s + 2]) a = lse2(a, prev[s + 2]);
-        const float v = (a == NEG_INF) ? NEG_INF : a + lpb[t * C + lab[s]];
-        cur[s] = v;
-        be[t * S_max + s] = v;
-      }
-      __syncthreads();
-      float* tmp = prev; prev = cur; cur = tmp;
-    }
-    for (int64_t s = threadIdx.x; s < S; s += blockDim.x) {
-      const float ab = al[t * S_max + s] + prev[s];
+      const float ab = al[t * S_max + s] + be[t * S_max + s];
       contrib[s] = (ab > NEG_INF) ? __expf(ab - lpb[t * C + lab[s]] + nll) : 0.f;
     }
     __syncthreads();
@@ -206,11 +284,10 @@ __global__ __launch_bounds__(256) void ctc_kernel(const float* __restrict__ lp, 
     for (int c = threadIdx.x; c < C; c += blockDim.x) {
       float post = (c == blank) ? blank_sh : 0.f;
       for (int s = head[c]; s >= 0; s = nxt[s]) post += contrib[s];
-      grad[(b * T + t) * C + c] = scale * (__expf(lpb[t * C + c]) - post);
+      gb[t * C + c] = scale * (__expf(lpb[t * C + c]) - post);
     }
     __syncthreads();
   }
-  for (int64_t i = Tb * C + threadIdx.x; i < T * C; i += blockDim.x) grad[b * T * C + i] = 0.f;
 }
 
 // grad += coef*(softmax(lp/T) - p_t) ; loss_acc += loss_scale * sum_c p_t (log p_t - log_softmax(lp/T))
@@ -330,11 +407,27 @@ int kdfm_ctc_loss(const float* log_probs, const int64_t* targets, const int64_t*
                "null pointer");
   KDFM_REQUIRE(blank >= 0 && blank < C && C <= 4096 && Umax >= 1 && Umax <= 4096, "bad sizes");
   if (B == 0) return KDFM_OK;
-  const size_t shmem = sizeof(float) * (5 * (2 * Umax + 1) + C);
-  KDFM_REQUIRE(shmem <= 60 * 1024, "CTC workspace exceeds LDS");
-  hipLaunchKernelGGL(ctc_kernel, dim3((unsigned)B), dim3(256), shmem, as_stream(stream), log_probs, targets,
-                     input_lengths, target_lengths, alpha_ws, beta_ws, nll, grad, T, (int)C, Umax, (int)blank,
-                     grad_scale, zero_infinity);
+  const int64_t S_max = 2 * Umax + 1;
+  const size_t sh_ab = sizeof(float) * 2 * S_max;
+  const size_t sh_gr = sizeof(float) * (3 * S_max + C);
+  KDFM_REQUIRE(sh_gr <= 60 * 1024, "CTC workspace exceeds LDS");
+  hipStream_t st = as_stream(stream);
+  const unsigned nt = S_max <= 256 ? 256 : 1024;
+  const int64_t spt = ceil_div(S_max, nt);
+  const dim3 gab((unsigned)B, 2);
+#define KDFM_CTC_AB(SPT_, CH_)                                                                                   \
+  hipLaunchKernelGGL((ctc_ab_kernel<SPT_, CH_>), gab, dim3(nt), sh_ab, st, log_probs, targets, input_lengths,  \
+                     target_lengths, alpha_ws, beta_ws, nll, T, (int)C, Umax, (int)blank, zero_infinity)
+  if (spt <= 1) KDFM_CTC_AB(1, 16);
+  else if (spt <= 2) KDFM_CTC_AB(2, 8);
+  else if (spt <= 4) KDFM_CTC_AB(4, 4);
+  else KDFM_CTC_AB(9, 2);
+#undef KDFM_CTC_AB
+  if (int rc = check_launch("kdfm_ctc_loss (alpha/beta)")) return rc;
+  if (T <= 0) return KDFM_OK;
+  hipLaunchKernelGGL(ctc_grad_kernel, dim3((unsigned)B, (unsigned)ceil_div(T, CTC_FPB)), dim3(256), sh_gr, st,
+                     log_probs, targets, input_lengths, target_lengths, alpha_ws, beta_ws, grad, T, (int)C, Umax,
+                     (int)blank, grad_scale, zero_infinity);
   return check_launch("kdfm_ctc_loss");
 }
 
