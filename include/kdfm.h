@@ -147,6 +147,14 @@ int kdfm_gemm(const kdfm_gemm_desc* d, void* stream);
 int64_t kdfm_wgrad_bf16_ws(int64_t rows, int64_t M, int64_t N, int32_t bias);
 int kdfm_wgrad_bf16(const uint16_t* dY, const uint16_t* X, float* dW, int64_t ldc, float* db, int64_t rows,
                     int64_t M, int64_t N, float alpha, float* ws, int64_t ws_len, void* stream);
+/* The same for a Conv1d(C -> M, taps, padding pad) over utterances of T frames (rows % T == 0):
+ *   dW[m][tap*C + c] += alpha * sum_r dY[r][m] * X[r + tap - pad][c]   (0 outside the utterance)
+ * in the GEMM weight layout of kdfm_convw_prep (re-laid out by kdfm_convw_grad); the weight gradient
+ * of SimpleDenoiser's convs (asr_train_diffm.py:449-453) over the fused chain's stacked saves. */
+int64_t kdfm_wgrad_bf16_conv_ws(int64_t rows, int64_t M, int64_t C, int32_t taps, int32_t pad, int64_t T, int32_t bias);
+int kdfm_wgrad_bf16_conv(const uint16_t* dY, const uint16_t* X, float* dW, int64_t ldc, float* db, int64_t rows,
+                         int64_t M, int64_t C, int32_t taps, int32_t pad, int64_t T, float alpha, float* ws,
+                         int64_t ws_len, void* stream);
 
 /* Fused FlowMatchingModule chain (asr_train_diffm.py:1368-1427, rectified, meta_encoder 'mlp',
  * shape_transform 'linear'; bf16 MFMA, f32 state; latent width L == 96).  Rows n:
@@ -179,6 +187,20 @@ int kdfm_fm_chain_fwd(const float* x0, const float* zt, const float* W1, int64_t
 int kdfm_fm_chain_bwd(const float* dtr, const uint16_t* A, const float* gxS, const float* W1, int64_t ld_w1,
                       const float* W2, const float* Wst, uint16_t* DV, uint16_t* DA, float* gx0, int64_t n, int32_t L,
                       int32_t S, void* stream);
+/* Fused SimpleDenoiser chain (asr_train_diffm.py:444-460: S steps of x <- x - net(x)/S, net =
+ * Conv1d(L,L,3,p=1) -> ReLU -> Conv1d(L,L,3,p=1); bf16 MFMA, f32 state; L == 96) over n rows =
+ * (n / T) utterances of T frames, channels-last.  W1 / W2: PyTorch Conv1d weights (L, L, 3) fp32.
+ *   forward:  out = x_S;  saves X[i] = x_i and A[i] = relu(conv1(x_i) + b1) as bf16 (S, n, L)
+ *   backward: gout = dL/dx_S -> gin = dL/dx_0;  saves GV[i] = dL/dx_{i+1} and
+ *             DA[i] = -(1/S) conv2^T(GV[i]) . [A[i] > 0] as bf16 (S, n, L)
+ * Weight gradients: kdfm_wgrad_bf16_conv(DA, X) and (GV, A) with alpha -1/S over S n rows. */
+int64_t kdfm_denoise_wimg_elems(void);   /* bf16 elements of the wimg workspace (prepared weight images) */
+int kdfm_denoise_chain_fwd(const float* z, const float* W1, const float* b1, const float* W2, const float* b2,
+                           uint16_t* wimg, uint16_t* X, uint16_t* A, float* out, int64_t n, int64_t T, int32_t L,
+                           int32_t S, void* stream);
+int kdfm_denoise_chain_bwd(const float* gout, const uint16_t* A, const float* W1, const float* W2, uint16_t* wimg,
+                           uint16_t* GV, uint16_t* DA, float* gin, int64_t n, int64_t T, int32_t L, int32_t S,
+                           void* stream);
 /* bf16 weight twins (once per step, before the GEMMs that read them):
  *   kdfm_cast_bf16:   dst[i] = bf16(src[i]), i < n  (same layout as the f32 flat parameter buffer)
  *   kdfm_cast_bf16_t: per table entry e = (offset, rows, cols, first_block) (device int64 [ntab][4]):

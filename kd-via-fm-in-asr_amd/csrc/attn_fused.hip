@@ -42,15 +42,13 @@ __device__ __forceinline__ bf16x8 load_frag8(const float* src, int valid) {
   float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
   if (valid >= 4) a = *reinterpret_cast<const float4*>(src);
   if (valid >= 8) b = *reinterpret_cast<const float4*>(src + 4);
-  bf16x8 r;
-  r[0] = (short)f2bf(a.x); r[1] = (short)f2bf(a.y); r[2] = (short)f2bf(a.z); r[3] = (short)f2bf(a.w);
-  r[4] = (short)f2bf(b.x); r[5] = (short)f2bf(b.y); r[6] = (short)f2bf(b.z); r[7] = (short)f2bf(b.w);
-  return r;
+  const float t[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  return pack_bf16x8<bf16x8>(t);
 }
 
 __device__ __forceinline__ void store4_bf16(uint16_t* dst, float4 v) {
-  const uint32_t lo = (uint32_t)f2bf(v.x) | ((uint32_t)f2bf(v.y) << 16);
-  const uint32_t hi = (uint32_t)f2bf(v.z) | ((uint32_t)f2bf(v.w) << 16);
+  const uint32_t lo = pack_bf16x2(v.x, v.y);
+  const uint32_t hi = pack_bf16x2(v.z, v.w);
   *reinterpret_cast<uint2*>(dst) = make_uint2(lo, hi);
 }
 

@@ -44,6 +44,23 @@ __device__ __forceinline__ uint16_t f2bf(float f) {
   return __builtin_bit_cast(uint16_t, h);
 }
 
+// two floats -> packed bf16 pair (lo = a, hi = b), round-to-nearest-even: ONE v_cvt_pk_bf16_f32 (two
+// scalar f2bf calls cost a convert each plus a shift and an or)
+typedef __bf16 kdfm_bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float kdfm_f32x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
+  const kdfm_f32x2_t v = {a, b};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, kdfm_bf16x2_t));
+}
+
+// 8 floats -> 8 packed bf16 (4 converts), as the 16-byte MFMA operand vector type V
+template <typename V>
+__device__ __forceinline__ V pack_bf16x8(const float* v) {
+  typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+  const u32x4_t w = {pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]), pack_bf16x2(v[6], v[7])};
+  return __builtin_bit_cast(V, w);
+}
+
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
 __device__ __forceinline__ float siluf_(float x) { return x * sigmoidf_(x); }
 __device__ __forceinline__ float dsiluf_(float x) {

@@ -48,15 +48,25 @@ __device__ __forceinline__ void fc_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
-__device__ __forceinline__ uint32_t pk2(float a, float b) { return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16); }
+__device__ __forceinline__ uint32_t pk2(float a, float b) { return pack_bf16x2(a, b); }
 __device__ __forceinline__ float bf2f(uint32_t b16) { return __builtin_bit_cast(float, b16 << 16); }
 
 // image[r][c] = bf16(trans ? W[c][r] : W[r][c]), W row stride ld
 __device__ void fc_stage_w(uint16_t* lds, int img, const float* __restrict__ W, int64_t ld, bool trans) {
-  for (int e = threadIdx.x; e < FC_L * FC_L; e += FC_NT) {
+  constexpr int PER = FC_L * FC_L / FC_NT;   // 18 elements per thread, all loads in flight at once
+  static_assert(FC_L * FC_L % FC_NT == 0, "staging split");
+  float v[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int e = j * FC_NT + threadIdx.x;
     const int r = e / FC_L, c = e - r * FC_L;
-    const float v = trans ? W[(int64_t)c * ld + r] : W[(int64_t)r * ld + c];
-    *lds_at<uint16_t>(lds, img + r * FC_LDW + c) = f2bf(v);
+    v[j] = trans ? W[(int64_t)c * ld + r] : W[(int64_t)r * ld + c];
+  }
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int e = j * FC_NT + threadIdx.x;
+    const int r = e / FC_L, c = e - r * FC_L;
+    *lds_at<uint16_t>(lds, img + r * FC_LDW + c) = f2bf(v[j]);
   }
 }
 

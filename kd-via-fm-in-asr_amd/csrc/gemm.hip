@@ -160,10 +160,7 @@ __device__ __forceinline__ void store_lds(void* lds, const float (&v)[8]) {
     uint16_t* s = reinterpret_cast<uint16_t*>(lds);  // [64][LDK_BF]
     if constexpr (KRUN) {
       const int r = t >> 2, k = (t & 3) * 8;
-      bf16x8 pk;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) pk[i] = (short)f2bf(v[i]);
-      *reinterpret_cast<bf16x8*>(s + r * LDK_BF + k) = pk;
+      *reinterpret_cast<bf16x8*>(s + r * LDK_BF + k) = pack_bf16x8<bf16x8>(v);
     } else {
       const int k = t >> 3, r = (t & 7) * 8;
 #pragma unroll

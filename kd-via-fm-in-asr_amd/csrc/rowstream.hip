@@ -32,8 +32,8 @@ constexpr int RS_BM = 64;    // rows per forward tile
 constexpr int PRE_MAX = 12;  // float4 prefetch registers per thread (forward)
 
 __device__ __forceinline__ void pack4_bf16(uint16_t* dst, float4 v) {
-  const uint32_t lo = (uint32_t)f2bf(v.x) | ((uint32_t)f2bf(v.y) << 16);
-  const uint32_t hi = (uint32_t)f2bf(v.z) | ((uint32_t)f2bf(v.w) << 16);
+  const uint32_t lo = pack_bf16x2(v.x, v.y);
+  const uint32_t hi = pack_bf16x2(v.z, v.w);
   *reinterpret_cast<uint2*>(dst) = make_uint2(lo, hi);
 }
 
@@ -352,12 +352,13 @@ template <int COLS>
 __device__ __forceinline__ void wg_store_unit(uint16_t* img, int u, const float2 (&v)[8]) {
   constexpr int CG = COLS / 2;
   const int kg = u / CG, cg = u - kg * CG;
-  bf16x8 c0, c1;
+  float t0[8], t1[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    c0[i] = (short)f2bf(v[i].x);
-    c1[i] = (short)f2bf(v[i].y);
+    t0[i] = v[i].x;
+    t1[i] = v[i].y;
   }
+  const bf16x8 c0 = pack_bf16x8<bf16x8>(t0), c1 = pack_bf16x8<bf16x8>(t1);
   *reinterpret_cast<bf16x8*>(img + (cg * 2 + 0) * WG_LDK + kg * 8) = c0;
   *reinterpret_cast<bf16x8*>(img + (cg * 2 + 1) * WG_LDK + kg * 8) = c1;
 }

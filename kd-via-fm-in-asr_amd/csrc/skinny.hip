@@ -52,16 +52,14 @@ struct SkGeo {
 };
 
 __device__ __forceinline__ void pk4(uint16_t* dst, float4 v) {
-  const uint32_t lo = (uint32_t)f2bf(v.x) | ((uint32_t)f2bf(v.y) << 16);
-  const uint32_t hi = (uint32_t)f2bf(v.z) | ((uint32_t)f2bf(v.w) << 16);
+  const uint32_t lo = pack_bf16x2(v.x, v.y);
+  const uint32_t hi = pack_bf16x2(v.z, v.w);
   *reinterpret_cast<uint2*>(dst) = make_uint2(lo, hi);
 }
 
 __device__ __forceinline__ bf16x8 cvt8(float4 a, float4 b) {
-  bf16x8 r;
-  r[0] = (short)f2bf(a.x); r[1] = (short)f2bf(a.y); r[2] = (short)f2bf(a.z); r[3] = (short)f2bf(a.w);
-  r[4] = (short)f2bf(b.x); r[5] = (short)f2bf(b.y); r[6] = (short)f2bf(b.z); r[7] = (short)f2bf(b.w);
-  return r;
+  const float t[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  return pack_bf16x8<bf16x8>(t);
 }
 
 // Stage B columns [n0, n0 + cw) x k [0, Kp) into the bf16 [n][k] image (zero outside N / K).

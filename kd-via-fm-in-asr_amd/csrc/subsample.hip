@@ -72,10 +72,7 @@ __global__ __launch_bounds__(256) void ss_conv1_kernel(const float* __restrict__
     v = fmaxf(v, 0.f);
     out[j] = rowok ? v : 0.f;
   }
-  bf16x8_t pk;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) pk[j] = (short)f2bf(out[j]);
-  *reinterpret_cast<bf16x8_t*>(y1b + pos * C + cg * 8) = pk;
+  *reinterpret_cast<bf16x8_t*>(y1b + pos * C + cg * 8) = pack_bf16x8<bf16x8_t>(out);
   if (y1f) {
     float4* d = reinterpret_cast<float4*>(y1f + pos * C + cg * 8);
     d[0] = make_float4(out[0], out[1], out[2], out[3]);

@@ -12,8 +12,8 @@ __global__ __launch_bounds__(256) void cast_bf16_kernel(const float* __restrict_
   const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
   if (i + 3 < n) {
     const float4 v = *reinterpret_cast<const float4*>(src + i);
-    const uint32_t lo = (uint32_t)f2bf(v.x) | ((uint32_t)f2bf(v.y) << 16);
-    const uint32_t hi = (uint32_t)f2bf(v.z) | ((uint32_t)f2bf(v.w) << 16);
+    const uint32_t lo = pack_bf16x2(v.x, v.y);
+    const uint32_t hi = pack_bf16x2(v.z, v.w);
     *reinterpret_cast<uint2*>(dst + i) = make_uint2(lo, hi);
   } else {
     for (int64_t j = i; j < n; ++j) dst[j] = f2bf(src[j]);

@@ -207,8 +207,8 @@ __global__ __launch_bounds__(WR_NT, 2) void wgr_kernel(GemmP p, WrGeo g) {
         const float* f3 = reinterpret_cast<const float*>(&v3);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const uint32_t lo = (uint32_t)f2bf(f0[q]) | ((uint32_t)f2bf(f1[q]) << 16);
-          const uint32_t hi = (uint32_t)f2bf(f2[q]) | ((uint32_t)f2bf(f3[q]) << 16);
+          const uint32_t lo = pack_bf16x2(f0[q], f1[q]);
+          const uint32_t hi = pack_bf16x2(f2[q], f3[q]);
           *lds_at<u32x2>(wr_lds, img + (c0 + q) * WR_LDK + rg * 4) = u32x2{lo, hi};
         }
       }
@@ -489,6 +489,45 @@ GemmP wgrad_bf16_params(const uint16_t* dY, const uint16_t* X, float* dW, int64_
   p.splitk = 1;
   return p;
 }
+
+// CONV mode: X is (rows, C) frames; column n = tap * C + c reads frame r + tap - pad of the same
+// utterance of T frames (zero outside)
+void conv_geometry(GemmP& p, int64_t C, int taps, int pad, int64_t T) {
+  p.sBk = C;
+  p.conv_c = C;
+  p.taps = taps;
+  p.pad = pad;
+  p.conv_t = T;
+}
+
+int wgrad_bf16_run(const GemmP& p, int bmode, hipStream_t st) {
+  WrPlan pl;
+  KDFM_REQUIRE(wr_plan(p, KDFM_LD_XC, bmode, 1, pl, true), "shape not supported by the row-parallel kernel");
+  KDFM_REQUIRE(p.ws_len >= pl.S * p.M * p.N, "workspace too small (kdfm_wgrad_bf16*_ws)");
+  set_route(ROUTE_WGRAD_ROWS);
+  int rc;
+  const int key = pl.w.mbw * 10 + pl.w.nbw;
+  if (bmode == KDFM_LD_CONV) {
+    switch (key) {
+      case 32: rc = wr_launch<3, 2, true, true>(p, pl, st); break;
+      case 33: rc = wr_launch<3, 3, true, true>(p, pl, st); break;
+      case 34: rc = wr_launch<3, 4, true, true>(p, pl, st); break;
+      case 36: rc = wr_launch<3, 6, true, true>(p, pl, st); break;
+      default: rc = wr_launch<6, 3, true, true>(p, pl, st); break;
+    }
+  } else {
+    switch (key) {
+      case 32: rc = wr_launch<3, 2, false, true>(p, pl, st); break;
+      case 33: rc = wr_launch<3, 3, false, true>(p, pl, st); break;
+      case 34: rc = wr_launch<3, 4, false, true>(p, pl, st); break;
+      case 36: rc = wr_launch<3, 6, false, true>(p, pl, st); break;
+      default: rc = wr_launch<6, 3, false, true>(p, pl, st); break;
+    }
+  }
+  if (rc) return rc;
+  hipLaunchKernelGGL(wgr_fold_kernel, dim3((unsigned)ceil_div(p.M * p.N, 64)), dim3(64 * WF_WAVES), 0, st, p, pl.S);
+  return check_launch("kdfm_wgrad_bf16(fold)");
+}
 }  // namespace
 }  // namespace kdfm
 
@@ -511,22 +550,31 @@ int kdfm_wgrad_bf16(const uint16_t* dY, const uint16_t* X, float* dW, int64_t ld
   KDFM_REQUIRE(((((uintptr_t)dY) | ((uintptr_t)X)) & 15) == 0, "operands must be 16-byte aligned");
   KDFM_REQUIRE(ldc >= N, "ldc < N");
   GemmP p = wgrad_bf16_params(dY, X, dW, ldc, db, rows, M, N, alpha, ws, ws_len);
+  return wgrad_bf16_run(p, KDFM_LD_XC, as_stream(stream));
+}
+
+int64_t kdfm_wgrad_bf16_conv_ws(int64_t rows, int64_t M, int64_t C, int32_t taps, int32_t pad, int64_t T, int32_t bias) {
+  using namespace kdfm;
+  GemmP p = wgrad_bf16_params(reinterpret_cast<const uint16_t*>(16), reinterpret_cast<const uint16_t*>(16), nullptr,
+                              taps * C, bias ? reinterpret_cast<float*>(16) : nullptr, rows, M, taps * C, 1.f, nullptr, 0);
+  conv_geometry(p, C, taps, pad, T);
   WrPlan pl;
-  KDFM_REQUIRE(wr_plan(p, KDFM_LD_XC, KDFM_LD_XC, 1, pl, true), "shape not supported by the row-parallel kernel");
-  KDFM_REQUIRE(ws_len >= pl.S * p.M * p.N, "workspace too small (kdfm_wgrad_bf16_ws)");
-  hipStream_t st = as_stream(stream);
-  set_route(ROUTE_WGRAD_ROWS);
-  int rc;
-  switch (pl.w.mbw * 10 + pl.w.nbw) {
-    case 32: rc = wr_launch<3, 2, false, true>(p, pl, st); break;
-    case 33: rc = wr_launch<3, 3, false, true>(p, pl, st); break;
-    case 34: rc = wr_launch<3, 4, false, true>(p, pl, st); break;
-    case 36: rc = wr_launch<3, 6, false, true>(p, pl, st); break;
-    default: rc = wr_launch<6, 3, false, true>(p, pl, st); break;
-  }
-  if (rc) return rc;
-  hipLaunchKernelGGL(wgr_fold_kernel, dim3((unsigned)ceil_div(p.M * p.N, 64)), dim3(64 * WF_WAVES), 0, st, p, pl.S);
-  return check_launch("kdfm_wgrad_bf16(fold)");
+  if (!wr_plan(p, KDFM_LD_XC, KDFM_LD_CONV, 1, pl, true)) return -1;
+  return pl.S * p.M * p.N;
+}
+
+int kdfm_wgrad_bf16_conv(const uint16_t* dY, const uint16_t* X, float* dW, int64_t ldc, float* db, int64_t rows,
+                         int64_t M, int64_t C, int32_t taps, int32_t pad, int64_t T, float alpha, float* ws,
+                         int64_t ws_len, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(dY && X && dW && ws, "null pointer");
+  KDFM_REQUIRE(rows > 0 && M > 0 && C > 0 && M % 4 == 0 && C % 4 == 0, "M, C must be positive multiples of 4");
+  KDFM_REQUIRE(taps >= 1 && pad >= 0 && pad < taps && T >= 1 && rows % T == 0, "bad conv geometry");
+  KDFM_REQUIRE(((((uintptr_t)dY) | ((uintptr_t)X)) & 15) == 0, "operands must be 16-byte aligned");
+  KDFM_REQUIRE(ldc >= taps * C, "ldc < taps * C");
+  GemmP p = wgrad_bf16_params(dY, X, dW, ldc, db, rows, M, taps * C, alpha, ws, ws_len);
+  conv_geometry(p, C, taps, pad, T);
+  return wgrad_bf16_run(p, KDFM_LD_CONV, as_stream(stream));
 }
 
 }  // extern "C"

@@ -217,10 +217,16 @@ def subsampling_backward(cfg, S: EncoderShapes, P, G, pre, ctx, dx, len1, *, see
     dev = dx.device
     B, C = S.B, S.C
     dy2 = _out_linear_backward(S, P, G, pre, ctx, dx, ctx["y2"], seed=seed, salt=salt, ws=ws)
-    if ctx["cols1"] is None:   # fused forward: rebuild the im2col operand of the conv2 weight gradient
-        ctx["cols1"] = _empty(B * S.T * S.F2, 9 * C, dev=dev)
-        K.im2col_3x3s2(ctx["y1"], len1 if cfg.subsampling_mask else None, ctx["cols1"], B, S.T1, S.F1, C)
-    WGRAD.run(lambda: K.linear_dw(dy2, ctx["cols1"], G[pre + "pre_encode.conv.2.weight"].view(C, 9 * C), db=G[pre + "pre_encode.conv.2.bias"]), dy2, ctx["cols1"])
+    cols1 = ctx["cols1"]
+    rebuild = cols1 is None
+    if rebuild:   # fused forward: the im2col operand of the conv2 weight gradient is rebuilt on the
+        cols1 = _empty(B * S.T * S.F2, 9 * C, dev=dev)   # weight-gradient stream, beside the data gradient
+
+    def conv2_wgrad():
+        if rebuild:
+            K.im2col_3x3s2(ctx["y1"], len1 if cfg.subsampling_mask else None, cols1, B, S.T1, S.F1, C)
+        K.linear_dw(dy2, cols1, G[pre + "pre_encode.conv.2.weight"].view(C, 9 * C), db=G[pre + "pre_encode.conv.2.bias"])
+    WGRAD.run(conv2_wgrad, dy2, cols1, ctx["y1"])
     # data gradient in TAP-MAJOR columns (tap*C + c): GEMM against the (C, 9, C) re-laid weight, so the
     # col2im gather reads contiguous channel runs per tap
     w2tm = ws["w2_tapmajor"]

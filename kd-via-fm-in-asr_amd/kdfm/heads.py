@@ -205,6 +205,15 @@ def _fm_backward(cfg, P, G, ws, c, gxs, dev):
     return g
 
 
+_DENO_FUSED = __import__("os").environ.get("KDFM_DENOISE_FUSED", "1") == "1"
+
+
+def _deno_fused(Lt):
+    """bf16 math runs the fused SimpleDenoiser chain kernels (csrc/denoise.hip); the f32 parity mode
+    keeps the per-step conv GEMMs (KDFM_DENOISE_FUSED=0 forces them in bf16 too)."""
+    return K.get_math() == "bf16" and Lt == 96 and _DENO_FUSED
+
+
 def _adapt_denoise_forward(cfg, P, ws, x, T, seed, eps, dev):
     """NoiseAdapter then the 9-step SimpleDenoiser over rows x; returns (ctx, z_deno)."""
     n, Lt = x.shape
@@ -214,12 +223,20 @@ def _adapt_denoise_forward(cfg, P, ws, x, T, seed, eps, dev):
     gamma = _empty(n, dev=dev)
     K.adapter_fwd(x, hA, P["adapter.gamma_head.2.weight"].view(-1), P["adapter.gamma_head.2.bias"], eps, zn, gamma,
                   seed, SALT_HEADS)
+    ds = cfg.denoiser_steps
+    if _deno_fused(Lt):
+        X = torch.empty(ds, n, Lt, device=dev, dtype=torch.bfloat16)
+        A = torch.empty(ds, n, Lt, device=dev, dtype=torch.bfloat16)
+        out = _empty(n, Lt, dev=dev)
+        with K.span("denoise_chain_fwd"):
+            K.denoise_chain_fwd(zn, P["denoiser.net.0.weight"], P["denoiser.net.0.bias"], P["denoiser.net.2.weight"],
+                                P["denoiser.net.2.bias"], X, A, out, T, ds)
+        return dict(x=x, hA=hA, gamma=gamma, eps=eps, fused=True, X=X, A=A), out
     # SimpleDenoiser: x <- x - net(x)/steps
     K.convw_prep(P["denoiser.net.0.weight"], fwd=ws.w1f, bwd=ws.w1b)
     K.convw_prep(P["denoiser.net.2.weight"], fwd=ws.w2f, bwd=ws.w2b)
     if K.get_math() == "bf16" and ws.wconv_h is not None:
         K.cast_bf16(ws.wconv, ws.wconv_h)
-    ds = cfg.denoiser_steps
     xs = [zn]
     acts = []
     for _ in range(ds):
@@ -234,6 +251,45 @@ def _adapt_denoise_forward(cfg, P, ws, x, T, seed, eps, dev):
 
 def _adapt_denoise_backward(cfg, P, G, ws, c, g, T, seed, dev):
     """g = d/d z_deno -> returns d/d (adapter input)."""
+    n, Lt = g.shape
+    ds = cfg.denoiser_steps
+    if c.get("fused"):
+        W1, W2 = P["denoiser.net.0.weight"], P["denoiser.net.2.weight"]
+        X, A = c["X"], c["A"]
+        GV = torch.empty(ds, n, Lt, device=dev, dtype=torch.bfloat16)
+        DA = torch.empty(ds, n, Lt, device=dev, dtype=torch.bfloat16)
+        gin = _empty(n, Lt, dev=dev)
+        with K.span("denoise_chain_bwd"):
+            K.denoise_chain_bwd(g, A, W1, W2, GV, DA, gin, T, ds)
+
+        def wgrads():
+            # one row-parallel launch per conv over all ds steps (the stacked saves keep whole utterances)
+            K.fill(ws.g1, 0.0)
+            K.fill(ws.g2, 0.0)
+            K.wgrad_bf16_conv(DA.view(ds * n, Lt), X.view(ds * n, Lt), ws.g1, T, db=G["denoiser.net.0.bias"])
+            K.wgrad_bf16_conv(GV.view(ds * n, Lt), A.view(ds * n, Lt), ws.g2, T, alpha=-1.0 / ds,
+                              db=G["denoiser.net.2.bias"])
+            K.convw_grad(ws.g1, G["denoiser.net.0.weight"])
+            K.convw_grad(ws.g2, G["denoiser.net.2.weight"])
+        WGRAD.run(wgrads, X, A, GV, DA)
+        g = gin
+    else:
+        g = _denoise_backward_unfused(cfg, P, G, ws, c, g, T, dev)
+    x, hA = c["x"], c["hA"]
+    dx_direct = _empty(n, Lt, dev=dev)
+    dh = _empty(n, Lt, dev=dev)
+    K.adapter_bwd(g, x, hA, c["gamma"], P["adapter.gamma_head.2.weight"].view(-1), c["eps"], dx_direct, dh,
+                  G["adapter.gamma_head.2.weight"].view(-1), G["adapter.gamma_head.2.bias"], seed, SALT_HEADS)
+    del g
+    WGRAD.run(lambda: K.linear_dw(dh, x, G["adapter.gamma_head.0.weight"].view(Lt, Lt),
+                                  db=G["adapter.gamma_head.0.bias"]), dh, x)
+    dx = _empty(n, Lt, dev=dev)
+    K.linear_dx(dh, P["adapter.gamma_head.0.weight"].view(Lt, Lt), dx, R=dx_direct, rscale=1.0)
+    return dx
+
+
+def _denoise_backward_unfused(cfg, P, G, ws, c, g, T, dev):
+    """Per-step conv GEMMs of the denoiser backward (f32 parity mode); returns d/d(denoiser input)."""
     n, Lt = g.shape
     ds = cfg.denoiser_steps
     xs, acts = c["xs"], c["acts"]
@@ -252,17 +308,7 @@ def _adapt_denoise_backward(cfg, P, G, ws, c, g, T, seed, dev):
         del da
     # ws.g1 / ws.g2 are produced on the side stream: re-lay them out there too
     WGRAD.run(lambda: (K.convw_grad(ws.g1, G["denoiser.net.0.weight"]), K.convw_grad(ws.g2, G["denoiser.net.2.weight"])))
-    x, hA = c["x"], c["hA"]
-    dx_direct = _empty(n, Lt, dev=dev)
-    dh = _empty(n, Lt, dev=dev)
-    K.adapter_bwd(g, x, hA, c["gamma"], P["adapter.gamma_head.2.weight"].view(-1), c["eps"], dx_direct, dh,
-                  G["adapter.gamma_head.2.weight"].view(-1), G["adapter.gamma_head.2.bias"], seed, SALT_HEADS)
-    del g
-    WGRAD.run(lambda: K.linear_dw(dh, x, G["adapter.gamma_head.0.weight"].view(Lt, Lt),
-                                  db=G["adapter.gamma_head.0.bias"]), dh, x)
-    dx = _empty(n, Lt, dev=dev)
-    K.linear_dx(dh, P["adapter.gamma_head.0.weight"].view(Lt, Lt), dx, R=dx_direct, rscale=1.0)
-    return dx
+    return g
 
 
 # ------------------------------------------------------------------------------------------------

@@ -572,6 +572,43 @@ def fm_chain_bwd(dtr, A, gxS, W1, W2, Wst, DV, DA, gx0, S):
          ptr(_f32(W2)), ptr(_f32(Wst)), ptr(_bf16(DV)), ptr(_bf16(DA)), ptr(gx0), n, L, S, _s())
 
 
+def wgrad_bf16_conv(dY, X, dW, T, *, taps=3, pad=1, db=None, alpha=1.0):
+    """Conv1d weight gradient over utterances of T frames, bf16 row operands:
+    dW[m, tap*C + c] += alpha * sum_r dY[r, m] X[r + tap - pad, c] (GEMM layout of convw_prep)."""
+    rows, M = dY.shape
+    C = X.shape[1]
+    assert X.shape[0] == rows and dW.shape == (M, taps * C) and dW.stride(1) == 1 and rows % T == 0
+    assert dY.is_contiguous() and X.is_contiguous()
+    n = int(_lib.lib().kdfm_wgrad_bf16_conv_ws(rows, M, C, taps, pad, T, 1 if db is not None else 0))
+    if n < 0:
+        raise _lib.KdfmError(f"kdfm_wgrad_bf16_conv: unsupported shape rows={rows} M={M} C={C}")
+    ws = scratch(dY.device, n)
+    call("kdfm_wgrad_bf16_conv", ptr(_bf16(dY)), ptr(_bf16(X)), ptr(_f32(dW)), dW.stride(0), ptr(db), rows, M, C,
+         taps, pad, T, float(alpha), ptr(ws), ws.numel(), _s())
+
+
+def denoise_chain_fwd(z, W1, b1, W2, b2, X, A, out, T, S):
+    """Fused SimpleDenoiser forward (S steps) over utterances of T frames; W1/W2 Conv1d (L, L, 3)."""
+    n, L = z.shape
+    assert out.shape == (n, L) and n % T == 0 and W1.shape == (L, L, 3) and W2.shape == (L, L, 3)
+    for t in (X, A):
+        assert t is None or (t.shape == (S, n, L) and t.is_contiguous())
+    wimg = torch.empty(int(_lib.lib().kdfm_denoise_wimg_elems()), device=z.device, dtype=torch.bfloat16)
+    call("kdfm_denoise_chain_fwd", ptr(_f32(z)), ptr(_f32(W1.contiguous())), ptr(_f32(b1)), ptr(_f32(W2.contiguous())),
+         ptr(_f32(b2)), ptr(wimg), ptr(_bf16(X)), ptr(_bf16(A)), ptr(_f32(out)), n, T, L, S, _s())
+
+
+def denoise_chain_bwd(gout, A, W1, W2, GV, DA, gin, T, S):
+    """Fused SimpleDenoiser data-gradient backward: gin = dL/dx_0 from gout = dL/dx_S; saves GV, DA."""
+    n, L = gout.shape
+    assert A.shape == (S, n, L) and gin.shape == (n, L) and n % T == 0
+    for t in (GV, DA):
+        assert t is None or (t.shape == (S, n, L) and t.is_contiguous())
+    wimg = torch.empty(int(_lib.lib().kdfm_denoise_wimg_elems()), device=gout.device, dtype=torch.bfloat16)
+    call("kdfm_denoise_chain_bwd", ptr(_f32(gout)), ptr(_bf16(A)), ptr(_f32(W1.contiguous())),
+         ptr(_f32(W2.contiguous())), ptr(wimg), ptr(_bf16(GV)), ptr(_bf16(DA)), ptr(_f32(gin)), n, T, L, S, _s())
+
+
 def conv_lengths(inp, out, pad_total, kernel=3, stride=2):
     """NeMo calc_length for one conv stage: out = floor((in + pad_total - kernel) / stride) + 1."""
     assert out.numel() == inp.numel() and out.dtype == torch.int64

@@ -1,7 +1,7 @@
 """Summarise a rocprofv3 kernel trace (rocpd .db or --output-format csv kernel_trace.csv): kernel
 time per step grouped by kernel (+GEMM template and grid).
 usage: python tools/prof_summary.py <run_results.db | run_kernel_trace.csv> [steps] [top]
-steps defaults to the number of ctc_kernel launches (one per training step)."""
+steps defaults to the number of CTC alpha/beta launches (one per training step)."""
 import collections
 import csv
 import sqlite3
@@ -29,7 +29,7 @@ def main():
     tot, nl, nctc = 0.0, 0, 0
     for name, d, gx, gy, gz in rows(path):
         n = name.replace("kdfm::(anonymous namespace)::", "").replace("kdfm::", "")
-        if n.startswith("ctc_kernel") or "::ctc_kernel" in name:
+        if n.startswith(("ctc_kernel", "ctc_ab_kernel")) or "::ctc_kernel" in name or "ctc_ab_kernel" in name:
             nctc += 1
         tot += d
         nl += 1
