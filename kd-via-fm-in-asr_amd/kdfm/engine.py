@@ -37,18 +37,17 @@ class _OnStream:
         cs = self.eng.compute_stream
         if cs is None:
             return self
-        self.caller = torch.cuda.current_stream(self.eng.device)
-        if self.caller == cs:
+        if K.stream_ptr() == cs.cuda_stream:
             return self
-        cs.wait_stream(self.caller)
-        self.ctx = torch.cuda.stream(cs)
+        self.eng._link_in.after_current(cs)
+        self.ctx = K.on_stream(cs)
         self.ctx.__enter__()
         return self
 
     def __exit__(self, *a):
         if self.ctx is not None:
             self.ctx.__exit__(*a)
-            self.caller.wait_stream(self.eng.compute_stream)
+            self.eng._link_out.current_after(self.eng.compute_stream)
             self.ctx = None
 
 
@@ -81,6 +80,7 @@ class Ver5Engine:
         # HIP graph replayed on any other stream (tools/graph_probe.py), which serialised the teacher
         # graph and the whole-step graph's branches behind the main stream
         self.compute_stream = torch.cuda.Stream(dev) if dev.type == "cuda" else None
+        self._link_in, self._link_out = K.StreamLink(), K.StreamLink()   # caller <-> compute stream
         # capture the frozen teacher as a HIP graph in training steps (KDFM_TEACHER_GRAPH=0: eager)
         self.teacher_graph = __import__("os").environ.get("KDFM_TEACHER_GRAPH", "0") == "1"
         if init:
@@ -260,7 +260,7 @@ class Ver5Engine:
         with K.region("encoders"):
             for _ in range(cfg.n_layers + 1):
                 if tgen is not None:
-                    with torch.cuda.stream(side):
+                    with K.on_stream(side):
                         next(tgen)
                 next(sgen)
         if tgen is not None:

@@ -156,8 +156,63 @@ class mode:
             set_deterministic(d)
 
 
+# host-issue fast paths: torch.cuda.current_stream() costs several µs per call in Python (device
+# index resolution, availability checks, a Stream object); the enqueue of one step makes ~1.3k of
+# these queries, so the raw C entry points are used directly
+_cur_dev = torch._C._cuda_getDevice
+_raw_stream = torch._C._cuda_getCurrentRawStream
+
+
 def stream_ptr() -> int:
-    return torch.cuda.current_stream().cuda_stream
+    return _raw_stream(_cur_dev())
+
+
+def current_device() -> int:
+    return _cur_dev()
+
+
+class on_stream:
+    """torch.cuda.stream(s) without the Python overhead: makes `s` (a torch.cuda.Stream on the current
+    device) torch's current stream for the block and restores the previous one afterwards."""
+    __slots__ = ("s", "prev")
+
+    def __init__(self, s):
+        self.s = s
+
+    def __enter__(self):
+        s = self.s
+        self.prev = torch._C._cuda_getCurrentStream(s.device_index)
+        torch._C._cuda_setStream(stream_id=s.stream_id, device_index=s.device_index, device_type=s.device_type)
+        return s
+
+    def __exit__(self, *a):
+        p = self.prev
+        torch._C._cuda_setStream(stream_id=p[0], device_index=p[1], device_type=p[2])
+
+
+class StreamLink:
+    """Cross-stream ordering with one reusable event (a stream wait binds to the record made before
+    it, so re-recording later is safe): `after_current(dst)` makes dst wait for the current stream,
+    `current_after(src)` makes the current stream wait for src."""
+    __slots__ = ("ev",)
+
+    def __init__(self):
+        self.ev = None
+
+    def _event(self):
+        if self.ev is None:
+            self.ev = torch.cuda.Event()
+        return self.ev
+
+    def after_current(self, dst):
+        ev = self._event()
+        ev.record()
+        dst.wait_event(ev)
+
+    def current_after(self, src):
+        ev = self._event()
+        ev.record(src)
+        ev.wait()
 
 
 def ptr(t):
@@ -194,7 +249,7 @@ def scratch(dev, nfloats: int):
     stream (the weight-gradient side stream gets its own); it only grows."""
     import os
     idx = torch.device(dev).index if torch.device(dev).index is not None else torch.cuda.current_device()
-    key = (idx, torch.cuda.current_stream(idx).cuda_stream)
+    key = (idx, _raw_stream(idx))
     buf = _SCRATCH.get(key)
     if buf is None or buf.numel() < nfloats:
         if buf is not None and os.environ.get("KDFM_SCRATCH_RETIRE", "1") == "1":

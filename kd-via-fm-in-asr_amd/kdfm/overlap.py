@@ -19,20 +19,24 @@ from __future__ import annotations
 
 import torch
 
+from . import kernels as K
+
 
 class WgradOverlap:
     def __init__(self, enabled: bool = True):
         self.enabled = enabled
         self._side = {}
+        self._links = {}
         self._keep = []
         self._pending = False
 
     def _stream(self, dev):
-        key = torch.device(dev).index
+        key = torch.device(dev).index if not isinstance(dev, int) else dev
         s = self._side.get(key)
         if s is None:
-            s = torch.cuda.Stream(device=dev)
+            s = torch.cuda.Stream(device=key)
             self._side[key] = s
+            self._links[key] = (K.StreamLink(), K.StreamLink())
         return s
 
     def run(self, fn, *keep):
@@ -40,10 +44,10 @@ class WgradOverlap:
         if not self.enabled:
             fn()
             return
-        main = torch.cuda.current_stream()
-        side = self._stream(main.device)
-        side.wait_stream(main)
-        with torch.cuda.stream(side):
+        dev = K.current_device()
+        side = self._stream(dev)
+        self._links[dev][0].after_current(side)
+        with K.on_stream(side):
             fn()
         self._keep.extend(keep)
         self._pending = True
@@ -75,8 +79,8 @@ class WgradOverlap:
         """Main stream waits for all side-stream work; releases the kept operands."""
         if not self._pending:
             return
-        main = torch.cuda.current_stream()
-        main.wait_stream(self._stream(main.device))
+        dev = K.current_device()
+        self._links[dev][1].current_after(self._stream(dev))
         self._keep.clear()
         self._pending = False
 

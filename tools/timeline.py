@@ -8,10 +8,10 @@ import sys
 from collections import defaultdict
 
 
-def main():
-    path = sys.argv[1]
+def load(path):
+    """(start, end, stream, kernel) rows of a rocpd .db or a kernel_trace.csv, sorted by start."""
     rows = []
-    clean = lambda n: n.replace("kdfm::(anonymous namespace)::", "").split("(")[0]
+    clean = lambda n: n.replace("kdfm::(anonymous namespace)::", "").split("(")[0]  # noqa: E731
     if path.endswith(".db"):
         c = sqlite3.connect(path)
         for name, st, en, sid, qid in c.execute("select name, start, end, stream_id, queue_id from kernels"):
@@ -22,6 +22,11 @@ def main():
                 sid = r.get("Stream_Id") or r.get("Queue_Id") or "0"
                 rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), sid, clean(r["Kernel_Name"])))
     rows.sort()
+    return rows
+
+
+def main():
+    rows = load(sys.argv[1])
     # step boundaries: the adamw kernel ends every step
     ends = [e for s, e, q, n in rows if n.startswith("adamw_kernel") or "adamw_kernel" in n]
     if len(ends) < 3:
@@ -62,18 +67,9 @@ def main():
         print(f"  stream {q} top: " + "; ".join(f"{n[:40]} {t:.2f}" for n, t in top))
 
 
-if __name__ == "__main__":
-    main()
-
-
 def gaps(path, main_sid=None, min_us=30.0):
     """Main-stream idle gaps inside the last full step, with the kernels other streams run during them."""
-    rows = []
-    clean = lambda n: n.replace("kdfm::(anonymous namespace)::", "").split("(")[0]  # noqa: E731
-    c = sqlite3.connect(path)
-    for name, st, en, sid, qid in c.execute("select name, start, end, stream_id, queue_id from kernels"):
-        rows.append((int(st), int(en), str(sid if sid is not None else qid), clean(name)))
-    rows.sort()
+    rows = load(path)
     ends = [e for s, e, q, n in rows if "adamw_kernel" in n]
     t0, t1 = ends[-3], ends[-2]
     step = [r for r in rows if r[0] >= t0 and r[1] <= t1]
@@ -104,5 +100,7 @@ def gaps(path, main_sid=None, min_us=30.0):
         print(f"  {g:8.1f} us after {a:30s} before {b:30s} | " + "; ".join(f"{k} {v:.0f}" for k, v in top))
 
 
-if __name__ == "__main__" and len(sys.argv) > 2 and sys.argv[2] == "gaps":
-    gaps(sys.argv[1])
+if __name__ == "__main__":
+    main()
+    if len(sys.argv) > 2 and sys.argv[2] == "gaps":
+        gaps(sys.argv[1])
