@@ -297,6 +297,15 @@ int kdfm_subsample_conv1(const float* mel, const int64_t* mel_len, const int64_t
                          void* stream);
 int kdfm_subsample_conv2(const uint16_t* y1b, const int64_t* len2, const uint16_t* wb, const float* b2, float* y2,
                          int64_t B, int64_t T1, int64_t F1, int64_t C, void* stream);
+/* conv2's data gradient without an im2col matrix (bf16 MFMA, f32 accumulate):
+ *   dy1[b,t1,f1,ci] = [y1 > 0] * sum_{ky,kx,co: 2 t2 - 1 + ky = t1, 2 f2 - 1 + kx = f1} W[co,ci,ky,kx] dy2[b,t2,f2,co]
+ * over the parity classes of (t1, f1) (1, 2, 2 or 4 taps each); wt = kdfm_subsample_dgrad_wprep(W)
+ * (kdfm_subsample_dgrad_wprep_elems(C) bf16).  Replaces the ConvSubsampling backward's linear_dx into
+ * (B T2 F2, 9C) columns + col2im (conformer_encoder.py:381-390). */
+int64_t kdfm_subsample_dgrad_wprep_elems(int64_t C);
+int kdfm_subsample_dgrad_wprep(const float* w2, uint16_t* wt, int64_t C, void* stream);
+int kdfm_subsample_conv2_dgrad(const float* dy2, const uint16_t* wt, const float* y1, float* dy1, int64_t B, int64_t T1,
+                               int64_t F1, int64_t C, void* stream);
 
 /* ---------------- Evaluation path (ctc_models.py:625-692, wer.py) ---------
  * kdfm_ctc_greedy: CTC greedy decoding (Appendix A.9; WER.update wer.py:329-333): per utterance b,

@@ -243,6 +243,152 @@ int ss_launch(const uint16_t* y1, const int64_t* len2, const uint16_t* wb, const
   return check_launch("kdfm_subsample_conv2");
 }
 
+
+// ---- conv2 data gradient (transposed conv) without the im2col matrix --------------------------
+// dy1[b,t1,f1,ci] = [y1 > 0] * sum_{ky,kx,co: 2 t2 - 1 + ky = t1, 2 f2 - 1 + kx = f1} W[co,ci,ky,kx] dy2[b,t2,f2,co]
+// The input positions split into 4 parity classes (t1 % 2, f1 % 2) with a FIXED tap set each:
+// t1 even takes ky = 1 (t2 = t1/2); t1 odd takes ky = 0 (t2 = (t1+1)/2) and ky = 2 (t2 = (t1-1)/2);
+// the same for f1 / kx -> 1, 2, 2 or 4 taps.  Each workgroup computes 256 positions of one class as an
+// implicit GEMM (M = positions, N = C_in, K = taps x C_out, v_mfma_f32_32x32x16_bf16): the class's
+// tap weight slabs [ci][co] (bf16, prepared by ss_dgrad_wprep) are staged in LDS once, A fragments
+// are 8 consecutive C_out of dy2 at the tap's source position (two float4 loads, converted), and the
+// ReLU' of the conv1 output is applied in the epilogue.  Replaces linear_dx into a 9C-wide column
+// matrix (813 MB at the bench shape) plus its col2im gather.
+struct SdGeo {
+  int B, T1, F1, C, T2, F2, Cp, ldb;
+  int64_t npos[4];   // positions per class (class = 2 * (t1 % 2) + f1 % 2)
+  int64_t wg0[5];    // first workgroup of each class; wg0[4] = grid size
+};
+
+__global__ __launch_bounds__(256) void ss_dgrad_wprep_kernel(const float* __restrict__ W, uint16_t* __restrict__ wt,
+                                                             int C, int Np, int Cp) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t total = (int64_t)9 * Np * Cp;
+  if (idx >= total) return;
+  const int co = (int)(idx % Cp), ci = (int)((idx / Cp) % Np), tap = (int)(idx / ((int64_t)Np * Cp));
+  float v = 0.f;
+  if (ci < C && co < C) v = W[((int64_t)co * C + ci) * 9 + tap];
+  wt[idx] = f2bf(v);
+}
+
+template <int NCT, int KS>
+__global__ __launch_bounds__(SS_NT, 2) void ss_dgrad_kernel(const float* __restrict__ dy2,
+                                                            const uint16_t* __restrict__ wt,
+                                                            const float* __restrict__ y1, float* __restrict__ dy1,
+                                                            SdGeo g) {
+  constexpr int NP = 32 * NCT;
+  constexpr int CP = 16 * KS;
+  extern __shared__ __attribute__((aligned(16))) uint16_t sd_lds[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  int cls = 0;
+  while (cls < 3 && (int64_t)blockIdx.x >= g.wg0[cls + 1]) ++cls;
+  const int pt = cls >> 1, pf = cls & 1;
+  const int nT = (g.T1 - pt + 1) / 2, nF = (g.F1 - pf + 1) / 2;
+  // the class's taps: (ky, kx) and the source offsets t2 - i, f2 - j
+  int ntap = 0;
+  int tap_id[4], tdt[4], tdf[4];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int ky = pt ? 2 * a : 1, kx = pf ? 2 * c : 1;
+      const bool use = (a == 0 || pt) && (c == 0 || pf);
+      if (use) {
+        tap_id[ntap] = 3 * ky + kx;
+        tdt[ntap] = ky == 0 ? 1 : 0;
+        tdf[ntap] = kx == 0 ? 1 : 0;
+        ++ntap;
+      }
+    }
+  // stage the tap slabs: LDS [t][ci][co] with row stride ldb
+  const int cpr = CP / 8;   // 16-byte chunks per slab row
+  for (int t = 0; t < ntap; ++t) {
+    const uint16_t* src = wt + (int64_t)tap_id[t] * NP * CP;
+    for (int e = threadIdx.x; e < NP * cpr; e += SS_NT) {
+      const int row = e / cpr, c8 = (e - row * cpr) * 8;
+      *reinterpret_cast<bf16x8_t*>(sd_lds + (t * NP + row) * g.ldb + c8) =
+          *reinterpret_cast<const bf16x8_t*>(src + (int64_t)row * CP + c8);
+    }
+  }
+  // this lane's A position
+  const int64_t pos0 = (blockIdx.x - g.wg0[cls]) * (int64_t)(32 * SS_WAVES) + wave * 32;
+  const int64_t pa = pos0 + r;
+  const bool pok = pa < g.npos[cls];
+  const int64_t per_b = (int64_t)nT * nF;
+  const int ba = pok ? (int)(pa / per_b) : 0;
+  const int ia = pok ? (int)((pa % per_b) / nF) : 0;
+  const int ja = pok ? (int)(pa % nF) : 0;
+  __syncthreads();
+  f32x16_t acc[NCT];
+#pragma unroll
+  for (int n = 0; n < NCT; ++n)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[n][e] = 0.f;
+  for (int t = 0; t < ntap; ++t) {
+    const int t2 = ia + tdt[t], f2 = ja + tdf[t];
+    const bool ok = pok && t2 < g.T2 && f2 < g.F2;
+    const float* src = dy2 + (((int64_t)ba * g.T2 + t2) * g.F2 + f2) * g.C;
+    bf16x8_t a[KS];
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int co = 16 * s + 8 * h;
+      if (ok && co < g.C) {
+        const float4 u = *reinterpret_cast<const float4*>(src + co);
+        const float4 v = *reinterpret_cast<const float4*>(src + co + 4);
+        const float q[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+        a[s] = pack_bf16x8<bf16x8_t>(q);
+      } else {
+        a[s] = bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+      }
+    }
+    const uint16_t* bp = sd_lds + (t * NP + r) * g.ldb + 8 * h;
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+#pragma unroll
+      for (int n = 0; n < NCT; ++n) {
+        const bf16x8_t b = *reinterpret_cast<const bf16x8_t*>(bp + n * 32 * g.ldb + 16 * s);
+        acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[s], b, acc[n], 0, 0, 0);
+      }
+  }
+  // epilogue: rows = positions 8 (e/4) + 4 h + e % 4 of the wave tile, column ci = 32 n + r
+  int64_t m1[16];
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const int64_t pm = pos0 + 8 * (e >> 2) + 4 * h + (e & 3);
+    if (pm < g.npos[cls]) {
+      const int b = (int)(pm / per_b), i = (int)((pm % per_b) / nF), j = (int)(pm % nF);
+      m1[e] = ((int64_t)b * g.T1 + 2 * i + pt) * g.F1 + 2 * j + pf;
+    } else {
+      m1[e] = -1;
+    }
+  }
+#pragma unroll
+  for (int n = 0; n < NCT; ++n) {
+    const int ci = 32 * n + r;
+    if (ci >= g.C) continue;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      if (m1[e] < 0) continue;
+      const int64_t off = m1[e] * g.C + ci;
+      dy1[off] = y1[off] > 0.f ? acc[n][e] : 0.f;
+    }
+  }
+}
+
+template <int NCT, int KS>
+int sd_launch(const float* dy2, const uint16_t* wt, const float* y1, float* dy1, const SdGeo& g, hipStream_t st) {
+  const size_t lds = (size_t)4 * 32 * NCT * g.ldb * sizeof(uint16_t);
+  static bool once = [] {
+    (void)hipFuncSetAttribute((const void*)ss_dgrad_kernel<NCT, KS>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    return true;
+  }();
+  (void)once;
+  hipLaunchKernelGGL((ss_dgrad_kernel<NCT, KS>), dim3((unsigned)g.wg0[4]), dim3(SS_NT), lds, st, dy2, wt, y1, dy1, g);
+  return check_launch("kdfm_subsample_conv2_dgrad");
+}
+
 }  // namespace
 }  // namespace kdfm
 
@@ -297,6 +443,48 @@ int kdfm_subsample_conv2(const uint16_t* y1b, const int64_t* len2, const uint16_
   if (nct == 1 && ks == 2) return ss_launch<1, 1, 2>(y1b, len2, wb, b2, y2, g, st);    // tiny test sizes
   if (nct == 2 && ks == 4) return ss_launch<1, 2, 4>(y1b, len2, wb, b2, y2, g, st);
   set_error("kdfm_subsample_conv2: unsupported channel count");
+  return KDFM_EUNSUPPORTED;
+}
+
+int64_t kdfm_subsample_dgrad_wprep_elems(int64_t C) {
+  return 9 * kdfm::ceil_div(C, 32) * 32 * kdfm::ceil_div(C, 16) * 16;
+}
+
+int kdfm_subsample_dgrad_wprep(const float* w2, uint16_t* wt, int64_t C, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(w2 && wt && C > 0, "bad arguments");
+  const int64_t Np = ceil_div(C, 32) * 32, Cp = ceil_div(C, 16) * 16;
+  const int64_t n = 9 * Np * Cp;
+  hipLaunchKernelGGL(ss_dgrad_wprep_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, as_stream(stream), w2, wt,
+                     (int)C, (int)Np, (int)Cp);
+  return check_launch("kdfm_subsample_dgrad_wprep");
+}
+
+int kdfm_subsample_conv2_dgrad(const float* dy2, const uint16_t* wt, const float* y1, float* dy1, int64_t B, int64_t T1,
+                               int64_t F1, int64_t C, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(dy2 && wt && y1 && dy1, "null pointer");
+  KDFM_REQUIRE(C % 8 == 0 && B > 0 && T1 > 0 && F1 > 0, "C must be a multiple of 8");
+  KDFM_REQUIRE(((((uintptr_t)dy2) | ((uintptr_t)wt)) & 15) == 0, "dy2 / wt must be 16-byte aligned");
+  SdGeo g;
+  g.B = (int)B; g.T1 = (int)T1; g.F1 = (int)F1; g.C = (int)C;
+  g.T2 = (int)((T1 - 1) / 2 + 1); g.F2 = (int)((F1 - 1) / 2 + 1);
+  g.Cp = (int)(ceil_div(C, 16) * 16);
+  g.ldb = g.Cp + 8;
+  g.wg0[0] = 0;
+  for (int c = 0; c < 4; ++c) {
+    const int pt = c >> 1, pf = c & 1;
+    g.npos[c] = B * ((T1 - pt + 1) / 2) * ((F1 - pf + 1) / 2);
+    g.wg0[c + 1] = g.wg0[c] + ceil_div(g.npos[c], 32 * SS_WAVES);
+  }
+  KDFM_REQUIRE(g.wg0[4] < (1ll << 31), "too large");
+  const int nct = (int)ceil_div(C, 32), ks = g.Cp / 16;
+  hipStream_t st = as_stream(stream);
+  if (nct == 3 && ks == 6) return sd_launch<3, 6>(dy2, wt, y1, dy1, g, st);    // d = 88 / 96
+  if (nct == 1 && ks == 1) return sd_launch<1, 1>(dy2, wt, y1, dy1, g, st);    // test sizes
+  if (nct == 1 && ks == 2) return sd_launch<1, 2>(dy2, wt, y1, dy1, g, st);
+  if (nct == 2 && ks == 4) return sd_launch<2, 4>(dy2, wt, y1, dy1, g, st);
+  set_error("kdfm_subsample_conv2_dgrad: unsupported channel count");
   return KDFM_EUNSUPPORTED;
 }
 

@@ -227,16 +227,23 @@ def subsampling_backward(cfg, S: EncoderShapes, P, G, pre, ctx, dx, len1, *, see
             K.im2col_3x3s2(ctx["y1"], len1 if cfg.subsampling_mask else None, cols1, B, S.T1, S.F1, C)
         K.linear_dw(dy2, cols1, G[pre + "pre_encode.conv.2.weight"].view(C, 9 * C), db=G[pre + "pre_encode.conv.2.bias"])
     WGRAD.run(conv2_wgrad, dy2, cols1, ctx["y1"])
-    # data gradient in TAP-MAJOR columns (tap*C + c): GEMM against the (C, 9, C) re-laid weight, so the
-    # col2im gather reads contiguous channel runs per tap
-    w2tm = ws["w2_tapmajor"]
-    K.convw_prep(P[pre + "pre_encode.conv.2.weight"].view(C, C, 9), fwd=w2tm)
-    dcols1 = _empty(B * S.T * S.F2, 9 * C, dev=dev)
-    K.linear_dx(dy2, w2tm.view(C, 9 * C), dcols1)
-    del dy2
     dy1 = _empty(B * S.T1 * S.F1, C, dev=dev)
-    K.col2im_3x3s2(dcols1, len1 if cfg.subsampling_mask else None, ctx["y1"], dy1, B, S.T1, S.F1, C, tapmajor=True)
-    del dcols1
+    if K.get_math() == "bf16" and K.subsample_dgrad_supported(C):
+        # direct transposed conv over the input positions' parity classes (no column matrix); the
+        # ReLU' of y1 (zero at masked frames) is applied in its epilogue
+        wt = ws["w2_dgrad"]
+        K.subsample_dgrad_wprep(P[pre + "pre_encode.conv.2.weight"].view(C, C, 3, 3), wt)
+        K.subsample_conv2_dgrad(dy2, wt, ctx["y1"], dy1, B, S.T1, S.F1, C)
+    else:
+        # data gradient in TAP-MAJOR columns (tap*C + c): GEMM against the (C, 9, C) re-laid weight, so
+        # the col2im gather reads contiguous channel runs per tap
+        w2tm = ws["w2_tapmajor"]
+        K.convw_prep(P[pre + "pre_encode.conv.2.weight"].view(C, C, 9), fwd=w2tm)
+        dcols1 = _empty(B * S.T * S.F2, 9 * C, dev=dev)
+        K.linear_dx(dy2, w2tm.view(C, 9 * C), dcols1)
+        K.col2im_3x3s2(dcols1, len1 if cfg.subsampling_mask else None, ctx["y1"], dy1, B, S.T1, S.F1, C, tapmajor=True)
+        del dcols1
+    del dy2
     # conv0 (1 -> C, 3x3, s2) weight gradient straight from the mel frames: the direct stride-2 kernel
     # of dw_striding's first stage (same layer), no im2col of the input, deterministic fold
     m = cfg.subsampling_mask
@@ -614,4 +621,5 @@ def make_workspace(S: EncoderShapes, dev):
     if len(S.stages) == 3 and S.C == S.d:     # 'striding' x4 kernels
         ws["w2_bf16"] = torch.empty(K.subsample_wprep_elems(S.d), device=dev, dtype=torch.bfloat16)
         ws["w2_tapmajor"] = torch.empty(S.d, 9, S.d, device=dev)
+        ws["w2_dgrad"] = torch.empty(K.subsample_dgrad_wprep_elems(S.d), device=dev, dtype=torch.bfloat16)
     return ws

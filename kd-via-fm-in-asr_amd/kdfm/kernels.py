@@ -729,6 +729,29 @@ def subsample_conv2(y1b, len2, wb, b2, y2, B, T1, F1, Cc):
     call("kdfm_subsample_conv2", ptr(y1b), ptr(_i64(len2)), ptr(wb), ptr(_f32(b2)), ptr(_f32(y2)), B, T1, F1, Cc, _s())
 
 
+def subsample_dgrad_wprep_elems(Cc):
+    return int(_lib.lib().kdfm_subsample_dgrad_wprep_elems(Cc))
+
+
+def subsample_dgrad_supported(Cc):
+    """Channel counts the direct conv2 data-gradient kernel is instantiated for."""
+    return Cc % 8 == 0 and ((-(-Cc // 32), -(-Cc // 16)) in ((3, 6), (1, 1), (1, 2), (2, 4)))
+
+
+def subsample_dgrad_wprep(w2, wt):
+    Cc = w2.shape[0]
+    assert wt.dtype == torch.bfloat16 and wt.numel() >= subsample_dgrad_wprep_elems(Cc)
+    call("kdfm_subsample_dgrad_wprep", ptr(_f32(w2.contiguous())), ptr(wt), Cc, _s())
+
+
+def subsample_conv2_dgrad(dy2, wt, y1, dy1, B, T1, F1, Cc):
+    """dy1 = [y1 > 0] * conv2^T(dy2) (stride-2 3x3 transposed conv, no im2col); dy2 (B T2 F2, C),
+    y1 / dy1 (B T1 F1, C) channels-last f32."""
+    T2, F2 = (T1 - 1) // 2 + 1, (F1 - 1) // 2 + 1
+    assert dy2.numel() == B * T2 * F2 * Cc and y1.numel() == B * T1 * F1 * Cc and dy1.numel() == y1.numel()
+    call("kdfm_subsample_conv2_dgrad", ptr(_f32(dy2)), ptr(wt), ptr(_f32(y1)), ptr(_f32(dy1)), B, T1, F1, Cc, _s())
+
+
 # ------------------------------------------------------------------------------------------------
 # conformer layer pieces
 # ------------------------------------------------------------------------------------------------

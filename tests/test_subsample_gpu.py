@@ -99,3 +99,32 @@ def test_subsample_bench_shape_matches_im2col_path(K):
     # the f32 path sees f32 weights; the fused path bf16 weights -> bf16-level tolerance
     err = (y2 - ref).abs().max().item()
     assert err <= 1e-2 * ref.abs().max().item(), err
+
+
+@pytest.mark.parametrize("C,T1,F1", [(88, 401, 40), (88, 37, 13), (16, 29, 11), (32, 30, 40), (64, 7, 5)])
+def test_subsample_conv2_dgrad_direct(K, C, T1, F1):
+    """kdfm_subsample_conv2_dgrad (parity-class transposed conv, bf16 MFMA) against the float64
+    gradient of conv2d(stride 2, pad 1) wrt its input times ReLU'(y1), on bf16-rounded dy2 / W (the
+    operands the kernel consumes): rel. Frobenius <= 1e-5 (f32 accumulation only); frames where
+    y1 == 0 (ReLU'd or masked) get exactly 0."""
+    g = torch.Generator().manual_seed(C + T1)
+    B = 2
+    T2, F2 = _lens(T1), _lens(F1)
+    y1 = torch.relu(torch.randn(B, T1, F1, C, generator=g))
+    y1[1, T1 // 2:] = 0.0                                   # masked frames of a shorter utterance
+    dy2 = torch.randn(B, T2, F2, C, generator=g)
+    w2 = torch.randn(C, C, 3, 3, generator=g) * (1.0 / (3 * C ** 0.5))
+    x = torch.zeros(B, C, T1, F1, dtype=torch.float64, requires_grad=True)
+    out = F.conv2d(x, _bf(w2).double(), stride=2, padding=1)
+    (gx,) = torch.autograd.grad(out, x, _bf(dy2).double().permute(0, 3, 1, 2))
+    ref = gx.permute(0, 2, 3, 1) * (y1 > 0).double()
+    wt = torch.empty(K.subsample_dgrad_wprep_elems(C), device="cuda", dtype=torch.bfloat16)
+    K.subsample_dgrad_wprep(w2.cuda(), wt)
+    dy1 = torch.full((B * T1 * F1, C), float("nan"), device="cuda")
+    K.subsample_conv2_dgrad(dy2.cuda().reshape(-1, C), wt, y1.cuda().reshape(-1, C), dy1, B, T1, F1, C)
+    torch.cuda.synchronize()
+    got = dy1.cpu().double().view(B, T1, F1, C)
+    assert torch.isfinite(got).all()
+    err = ((got - ref).norm() / ref.norm()).item()
+    assert err <= 1e-5, err
+    assert got[y1 == 0].abs().max().item() == 0.0
