@@ -244,6 +244,10 @@ int kdfm_specaugment(float* x, const int64_t* seq_len, uint8_t* mask_out, int64_
  * frames >= len_in[b] read as zero (padding mask). */
 int kdfm_im2col_3x3s2(const float* X, const int64_t* len_in, float* cols, int64_t B, int64_t T1, int64_t F1,
                       int64_t C, void* stream);
+/* Tap-major bf16 columns: cols[(b,t2,f2), tap*C + c] = bf16(X[b, 2 t2 - 1 + ky, 2 f2 - 1 + kx, c]) (0 outside /
+ * beyond len_in), C % 8 == 0; the bf16 step's conv2 weight-gradient operand. */
+int kdfm_im2col_3x3s2_tm_bf16(const float* X, const int64_t* len_in, uint16_t* cols, int64_t B, int64_t T1, int64_t F1,
+                              int64_t C, void* stream);
 /* adjoint of the above (gather form); optionally multiplied by relu'(relu_out). */
 int kdfm_col2im_3x3s2(const float* dcols, const int64_t* len_in, const float* relu_out, float* dX, int64_t B,
                       int64_t T1, int64_t F1, int64_t C, void* stream);

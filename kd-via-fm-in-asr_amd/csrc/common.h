@@ -77,8 +77,16 @@ __host__ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
   z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
   return z ^ (z >> 31);
 }
+// (seed, stream) -> per-stream key (uniform per launch: the compiler keeps it scalar), then ONE
+// splitmix64 finaliser per element at counter position idx of that key's sequence
+__host__ __device__ __forceinline__ uint64_t rng_key(uint64_t seed, uint64_t stream) {
+  return mix64(seed ^ mix64(stream * 0x2545F4914F6CDD1Dull));
+}
+__device__ __forceinline__ uint64_t rng_bits_k(uint64_t key, uint64_t idx) {
+  return mix64(key + idx * 0x9E3779B97F4A7C15ull);
+}
 __device__ __forceinline__ uint64_t rng_bits(uint64_t seed, uint64_t stream, uint64_t idx) {
-  return mix64(seed ^ mix64(stream * 0x2545F4914F6CDD1Dull + idx));
+  return rng_bits_k(rng_key(seed, stream), idx);
 }
 __device__ __forceinline__ float rng_uniform(uint64_t seed, uint64_t stream, uint64_t idx) {
   return (float)(rng_bits(seed, stream, idx) >> 40) * (1.0f / 16777216.0f);  // [0,1)

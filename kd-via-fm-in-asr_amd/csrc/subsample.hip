@@ -254,6 +254,8 @@ int ss_launch(const uint16_t* y1, const int64_t* len2, const uint16_t* wb, const
 // are 8 consecutive C_out of dy2 at the tap's source position (two float4 loads, converted), and the
 // ReLU' of the conv1 output is applied in the epilogue.  Replaces linear_dx into a 9C-wide column
 // matrix (813 MB at the bench shape) plus its col2im gather.
+constexpr int SD_TPW = 4;   // position tiles per workgroup (amortises the tap-slab staging)
+
 struct SdGeo {
   int B, T1, F1, C, T2, F2, Cp, ldb;
   int64_t npos[4];   // positions per class (class = 2 * (t1 % 2) + f1 % 2)
@@ -311,67 +313,97 @@ __global__ __launch_bounds__(SS_NT, 2) void ss_dgrad_kernel(const float* __restr
           *reinterpret_cast<const bf16x8_t*>(src + (int64_t)row * CP + c8);
     }
   }
-  // this lane's A position
-  const int64_t pos0 = (blockIdx.x - g.wg0[cls]) * (int64_t)(32 * SS_WAVES) + wave * 32;
-  const int64_t pa = pos0 + r;
-  const bool pok = pa < g.npos[cls];
-  const int64_t per_b = (int64_t)nT * nF;
-  const int ba = pok ? (int)(pa / per_b) : 0;
-  const int ia = pok ? (int)((pa % per_b) / nF) : 0;
-  const int ja = pok ? (int)(pa % nF) : 0;
   __syncthreads();
-  f32x16_t acc[NCT];
-#pragma unroll
-  for (int n = 0; n < NCT; ++n)
-#pragma unroll
-    for (int e = 0; e < 16; ++e) acc[n][e] = 0.f;
-  for (int t = 0; t < ntap; ++t) {
-    const int t2 = ia + tdt[t], f2 = ja + tdf[t];
-    const bool ok = pok && t2 < g.T2 && f2 < g.F2;
-    const float* src = dy2 + (((int64_t)ba * g.T2 + t2) * g.F2 + f2) * g.C;
-    bf16x8_t a[KS];
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      const int co = 16 * s + 8 * h;
-      if (ok && co < g.C) {
-        const float4 u = *reinterpret_cast<const float4*>(src + co);
-        const float4 v = *reinterpret_cast<const float4*>(src + co + 4);
-        const float q[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
-        a[s] = pack_bf16x8<bf16x8_t>(q);
-      } else {
-        a[s] = bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+  const int per_b = nT * nF;                      // positions < 2^31 (checked on the host)
+  const int npos = (int)g.npos[cls];
+  const int ntile = (npos + 32 * SS_WAVES - 1) / (32 * SS_WAVES);
+  // position q of the class -> (b, i, j); 32-bit decode of a base plus small normalising steps
+  // (64-bit div / mod per epilogue element cost more than the MFMAs of the tile)
+  auto decode = [&](int q, int& b, int& i, int& j) {
+    b = q / per_b;
+    const int rem = q - b * per_b;
+    i = rem / nF;
+    j = rem - i * nF;
+  };
+  auto advance = [&](int& b, int& i, int& j, int by) {
+    j += by;
+    while (j >= nF) {
+      j -= nF;
+      if (++i == nT) {
+        i = 0;
+        ++b;
       }
     }
-    const uint16_t* bp = sd_lds + (t * NP + r) * g.ldb + 8 * h;
+  };
+  // each workgroup walks SD_TPW position tiles of its class with the staged tap slabs
+  const int tile0 = (int)(blockIdx.x - g.wg0[cls]) * SD_TPW;
+  for (int tile = tile0, tend = min(tile0 + SD_TPW, ntile); tile < tend; ++tile) {
+    const int pos0 = tile * (32 * SS_WAVES) + wave * 32;
+    // epilogue rows first (positions 8 (e/4) + 4 h + e % 4 of the wave tile): their ReLU' operands are
+    // loaded before the MFMAs so the latency hides behind them
+    int64_t m1[16];
+    {
+      int b, i, j;
+      decode(pos0 + 4 * h, b, i, j);
 #pragma unroll
-    for (int s = 0; s < KS; ++s)
-#pragma unroll
-      for (int n = 0; n < NCT; ++n) {
-        const bf16x8_t b = *reinterpret_cast<const bf16x8_t*>(bp + n * 32 * g.ldb + 16 * s);
-        acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[s], b, acc[n], 0, 0, 0);
+      for (int e = 0; e < 16; ++e) {
+        const int pm = pos0 + 8 * (e >> 2) + 4 * h + (e & 3);
+        m1[e] = pm < npos ? ((int64_t)b * g.T1 + 2 * i + pt) * g.F1 + 2 * j + pf : -1;
+        advance(b, i, j, (e & 3) == 3 ? 5 : 1);   // next row of the C layout: +1, or +5 to the next group of 8
       }
-  }
-  // epilogue: rows = positions 8 (e/4) + 4 h + e % 4 of the wave tile, column ci = 32 n + r
-  int64_t m1[16];
-#pragma unroll
-  for (int e = 0; e < 16; ++e) {
-    const int64_t pm = pos0 + 8 * (e >> 2) + 4 * h + (e & 3);
-    if (pm < g.npos[cls]) {
-      const int b = (int)(pm / per_b), i = (int)((pm % per_b) / nF), j = (int)(pm % nF);
-      m1[e] = ((int64_t)b * g.T1 + 2 * i + pt) * g.F1 + 2 * j + pf;
-    } else {
-      m1[e] = -1;
     }
-  }
+    bool pos_y[NCT][16];
 #pragma unroll
-  for (int n = 0; n < NCT; ++n) {
-    const int ci = 32 * n + r;
-    if (ci >= g.C) continue;
+    for (int n = 0; n < NCT; ++n) {
+      const int ci = 32 * n + r;
 #pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      if (m1[e] < 0) continue;
-      const int64_t off = m1[e] * g.C + ci;
-      dy1[off] = y1[off] > 0.f ? acc[n][e] : 0.f;
+      for (int e = 0; e < 16; ++e) pos_y[n][e] = (m1[e] >= 0 && ci < g.C) ? y1[m1[e] * g.C + ci] > 0.f : false;
+    }
+    // this lane's A position
+    const int pa = pos0 + r;
+    const bool pok = pa < npos;
+    int ba = 0, ia = 0, ja = 0;
+    if (pok) decode(pa, ba, ia, ja);
+    f32x16_t acc[NCT];
+#pragma unroll
+    for (int n = 0; n < NCT; ++n)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[n][e] = 0.f;
+    for (int t = 0; t < ntap; ++t) {
+      const int t2 = ia + tdt[t], f2 = ja + tdf[t];
+      const bool ok = pok && t2 < g.T2 && f2 < g.F2;
+      const float* src = dy2 + (((int64_t)ba * g.T2 + t2) * g.F2 + f2) * g.C;
+      bf16x8_t a[KS];
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const int co = 16 * s + 8 * h;
+        if (ok && co < g.C) {
+          const float4 u = *reinterpret_cast<const float4*>(src + co);
+          const float4 v = *reinterpret_cast<const float4*>(src + co + 4);
+          const float q[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+          a[s] = pack_bf16x8<bf16x8_t>(q);
+        } else {
+          a[s] = bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+        }
+      }
+      const uint16_t* bp = sd_lds + (t * NP + r) * g.ldb + 8 * h;
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+#pragma unroll
+        for (int n = 0; n < NCT; ++n) {
+          const bf16x8_t b = *reinterpret_cast<const bf16x8_t*>(bp + n * 32 * g.ldb + 16 * s);
+          acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[s], b, acc[n], 0, 0, 0);
+        }
+    }
+#pragma unroll
+    for (int n = 0; n < NCT; ++n) {
+      const int ci = 32 * n + r;
+      if (ci >= g.C) continue;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        if (m1[e] < 0) continue;
+        dy1[m1[e] * g.C + ci] = pos_y[n][e] ? acc[n][e] : 0.f;
+      }
     }
   }
 }
@@ -475,9 +507,9 @@ int kdfm_subsample_conv2_dgrad(const float* dy2, const uint16_t* wt, const float
   for (int c = 0; c < 4; ++c) {
     const int pt = c >> 1, pf = c & 1;
     g.npos[c] = B * ((T1 - pt + 1) / 2) * ((F1 - pf + 1) / 2);
-    g.wg0[c + 1] = g.wg0[c] + ceil_div(g.npos[c], 32 * SS_WAVES);
+    g.wg0[c + 1] = g.wg0[c] + ceil_div(ceil_div(g.npos[c], 32 * SS_WAVES), SD_TPW);
   }
-  KDFM_REQUIRE(g.wg0[4] < (1ll << 31), "too large");
+  KDFM_REQUIRE(g.wg0[4] < (1ll << 31) && g.npos[0] < (1ll << 30), "too large");
   const int nct = (int)ceil_div(C, 32), ks = g.Cp / 16;
   hipStream_t st = as_stream(stream);
   if (nct == 3 && ks == 6) return sd_launch<3, 6>(dy2, wt, y1, dy1, g, st);    // d = 88 / 96

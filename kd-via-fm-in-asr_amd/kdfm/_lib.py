@@ -97,6 +97,7 @@ SIGNATURES: dict[str, tuple] = {
     "kdfm_logmel_normalize": (_i32, [P, P, P, _i64, _i64, _i64, _f32, P]),
     "kdfm_specaugment": (_i32, [P, P, P, _i64, _i64, _i64, _i32, _i32, _i32, _f32, P, C.c_uint64, P]),
     "kdfm_im2col_3x3s2": (_i32, [P, P, P, _i64, _i64, _i64, _i64, P]),
+    "kdfm_im2col_3x3s2_tm_bf16": (_i32, [P, P, P, _i64, _i64, _i64, _i64, P]),
     "kdfm_conv_lengths": (_i32, [P, P, _i64, _i32, _i32, _i32, P]),
     "kdfm_dwsub_conv": (_i32, [P, P, P, P, P, P, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _i32, P]),
     "kdfm_dwsub_conv_dgrad": (_i32, [P, P, P, P, P, P, _i64, _i64, _i64, _i64, _i64, _i64, _i32, _i32, P]),

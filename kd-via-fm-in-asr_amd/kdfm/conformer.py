@@ -217,18 +217,36 @@ def subsampling_backward(cfg, S: EncoderShapes, P, G, pre, ctx, dx, len1, *, see
     dev = dx.device
     B, C = S.B, S.C
     dy2 = _out_linear_backward(S, P, G, pre, ctx, dx, ctx["y2"], seed=seed, salt=salt, ws=ws)
-    cols1 = ctx["cols1"]
-    rebuild = cols1 is None
-    if rebuild:   # fused forward: the im2col operand of the conv2 weight gradient is rebuilt on the
-        cols1 = _empty(B * S.T * S.F2, 9 * C, dev=dev)   # weight-gradient stream, beside the data gradient
+    direct = K.get_math() == "bf16" and K.subsample_dgrad_supported(C) and ctx["cols1"] is None
+    if direct:
+        # conv2 weight gradient on the weight-gradient stream from bf16 operands: tap-major bf16
+        # columns of y1 (half the bytes of the f32 im2col) and a bf16 copy of dy2, one row-parallel
+        # launch into (C, 9, C) then re-laid out into (C, C, 3, 3)
+        cols1 = torch.empty(B * S.T * S.F2, 9 * C, device=dev, dtype=torch.bfloat16)
+        dy2h = torch.empty(B * S.T * S.F2, C, device=dev, dtype=torch.bfloat16)
+        gtm = ws["w2_tapmajor_grad"]
 
-    def conv2_wgrad():
-        if rebuild:
-            K.im2col_3x3s2(ctx["y1"], len1 if cfg.subsampling_mask else None, cols1, B, S.T1, S.F1, C)
-        K.linear_dw(dy2, cols1, G[pre + "pre_encode.conv.2.weight"].view(C, 9 * C), db=G[pre + "pre_encode.conv.2.bias"])
-    WGRAD.run(conv2_wgrad, dy2, cols1, ctx["y1"])
+        def conv2_wgrad():
+            K.im2col_3x3s2_tm_bf16(ctx["y1"], len1 if cfg.subsampling_mask else None, cols1, B, S.T1, S.F1, C)
+            K.cast_bf16(dy2, dy2h)
+            K.fill(gtm, 0.0)
+            K.wgrad_bf16(dy2h, cols1, gtm.view(C, 9 * C), db=G[pre + "pre_encode.conv.2.bias"])
+            K.convw_grad(gtm.view(C, 9 * C), G[pre + "pre_encode.conv.2.weight"].view(C, C, 9))
+        WGRAD.run(conv2_wgrad, dy2, cols1, dy2h, ctx["y1"])
+    else:
+        cols1 = ctx["cols1"]
+        rebuild = cols1 is None
+        if rebuild:   # fused forward: the im2col operand of the conv2 weight gradient is rebuilt on the
+            cols1 = _empty(B * S.T * S.F2, 9 * C, dev=dev)   # weight-gradient stream, beside the data gradient
+
+        def conv2_wgrad():
+            if rebuild:
+                K.im2col_3x3s2(ctx["y1"], len1 if cfg.subsampling_mask else None, cols1, B, S.T1, S.F1, C)
+            K.linear_dw(dy2, cols1, G[pre + "pre_encode.conv.2.weight"].view(C, 9 * C),
+                        db=G[pre + "pre_encode.conv.2.bias"])
+        WGRAD.run(conv2_wgrad, dy2, cols1, ctx["y1"])
     dy1 = _empty(B * S.T1 * S.F1, C, dev=dev)
-    if K.get_math() == "bf16" and K.subsample_dgrad_supported(C):
+    if direct:
         # direct transposed conv over the input positions' parity classes (no column matrix); the
         # ReLU' of y1 (zero at masked frames) is applied in its epilogue
         wt = ws["w2_dgrad"]
@@ -247,7 +265,8 @@ def subsampling_backward(cfg, S: EncoderShapes, P, G, pre, ctx, dx, len1, *, see
     # conv0 (1 -> C, 3x3, s2) weight gradient straight from the mel frames: the direct stride-2 kernel
     # of dw_striding's first stage (same layer), no im2col of the input, deterministic fold
     m = cfg.subsampling_mask
-    WGRAD.run(lambda: K.dwsub_conv_wgrad(dy1, len1 if m else None, ctx["mel"], ctx["mel_len"] if m else None,
+    run = (lambda fn, *keep: fn()) if direct else WGRAD.run   # direct: the main stream is free here
+    run(lambda: K.dwsub_conv_wgrad(dy1, len1 if m else None, ctx["mel"], ctx["mel_len"] if m else None,
                                          G[pre + "pre_encode.conv.0.weight"], G[pre + "pre_encode.conv.0.bias"],
                                          B, S.Tm, cfg.nfilt, 1, C, S.T1, S.F1, S.pad), dy1, ctx["mel"])
     
@@ -622,4 +641,5 @@ def make_workspace(S: EncoderShapes, dev):
         ws["w2_bf16"] = torch.empty(K.subsample_wprep_elems(S.d), device=dev, dtype=torch.bfloat16)
         ws["w2_tapmajor"] = torch.empty(S.d, 9, S.d, device=dev)
         ws["w2_dgrad"] = torch.empty(K.subsample_dgrad_wprep_elems(S.d), device=dev, dtype=torch.bfloat16)
+        ws["w2_tapmajor_grad"] = torch.empty(S.d, 9, S.d, device=dev)
     return ws

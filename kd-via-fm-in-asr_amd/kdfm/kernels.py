@@ -580,6 +580,12 @@ def im2col_3x3s2(X, len_in, cols, B, T1, F1, Cc):
     call("kdfm_im2col_3x3s2", ptr(X), ptr(_i64(len_in)), ptr(cols), B, T1, F1, Cc, _s())
 
 
+def im2col_3x3s2_tm_bf16(X, len_in, cols, B, T1, F1, Cc):
+    T2, F2 = (T1 - 1) // 2 + 1, (F1 - 1) // 2 + 1
+    assert cols.shape == (B * T2 * F2, 9 * Cc) and cols.dtype == torch.bfloat16 and X.numel() == B * T1 * F1 * Cc
+    call("kdfm_im2col_3x3s2_tm_bf16", ptr(_f32(X)), ptr(_i64(len_in)), ptr(cols), B, T1, F1, Cc, _s())
+
+
 def col2im_3x3s2(dcols, len_in, relu_out, dX, B, T1, F1, Cc, tapmajor=False):
     T2, F2 = (T1 - 1) // 2 + 1, (F1 - 1) // 2 + 1
     assert dcols.shape == (B * T2 * F2, 9 * Cc) and dX.numel() == B * T1 * F1 * Cc

@@ -128,3 +128,20 @@ def test_subsample_conv2_dgrad_direct(K, C, T1, F1):
     err = ((got - ref).norm() / ref.norm()).item()
     assert err <= 1e-5, err
     assert got[y1 == 0].abs().max().item() == 0.0
+
+
+def test_im2col_tapmajor_bf16_matches_f32_im2col(K):
+    """kdfm_im2col_3x3s2_tm_bf16 = the f32 im2col (columns c*9 + tap) re-ordered to tap*C + c and
+    rounded to bf16, including the len_in frame mask: bit-exact."""
+    g = torch.Generator().manual_seed(7)
+    B, T1, F1, C = 3, 41, 40, 88
+    X = torch.randn(B * T1 * F1, C, generator=g).cuda()
+    lin = torch.tensor([41, 30, 9], dtype=torch.int64).cuda()
+    T2, F2 = _lens(T1), _lens(F1)
+    ref = torch.empty(B * T2 * F2, 9 * C, device="cuda")
+    K.im2col_3x3s2(X, lin, ref, B, T1, F1, C)
+    got = torch.empty(B * T2 * F2, 9 * C, device="cuda", dtype=torch.bfloat16)
+    K.im2col_3x3s2_tm_bf16(X, lin, got, B, T1, F1, C)
+    torch.cuda.synchronize()
+    want = ref.view(-1, C, 9).transpose(1, 2).reshape(-1, 9 * C).bfloat16()
+    assert torch.equal(got, want)
