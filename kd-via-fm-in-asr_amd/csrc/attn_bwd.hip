@@ -97,6 +97,40 @@ __device__ void stage_rows(uint16_t* rc, uint16_t* cr, int ldt, const float* src
   }
 }
 
+// Software-pipelined staging: fetch_rows issues the global loads of rows [r0, r0 + n) into registers
+// (MAXI float4 per thread) one block ahead, put_rows writes them to the LDS tiles after the barrier
+// that retires the current block, so the loads' latency hides behind the current block's MFMAs.
+template <int MAXI>
+__device__ __forceinline__ void fetch_rows(float4 (&v)[MAXI], const float* src, int64_t ld, int64_t base_row, int r0,
+                                           int n, int lo, int hi, int64_t c0, int dk) {
+  const int cq = dk >> 2;
+#pragma unroll
+  for (int it = 0; it < MAXI; ++it) {
+    const int e = threadIdx.x + it * 256;
+    const int rr = e / cq, c4 = (e - rr * cq) * 4;
+    const int r = r0 + rr;
+    const bool ok = e < n * cq && r >= lo && r < hi;
+    v[it] = ok ? *reinterpret_cast<const float4*>(src + (base_row + r) * ld + c0 + c4) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+template <int MAXI>
+__device__ __forceinline__ void put_rows(uint16_t* rc, uint16_t* cr, int ldt, const float4 (&v)[MAXI], int n, int dk) {
+  const int cq = dk >> 2;
+#pragma unroll
+  for (int it = 0; it < MAXI; ++it) {
+    const int e = threadIdx.x + it * 256;
+    if (e >= n * cq) continue;
+    const int rr = e / cq, c4 = (e - rr * cq) * 4;
+    if (rc) st4(rc + rr * LR + c4, v[it]);
+    if (cr) {
+      cr[(c4 + 0) * ldt + rr] = f2bf(v[it].x);
+      cr[(c4 + 1) * ldt + rr] = f2bf(v[it].y);
+      cr[(c4 + 2) * ldt + rr] = f2bf(v[it].z);
+      cr[(c4 + 3) * ldt + rr] = f2bf(v[it].w);
+    }
+  }
+}
+
 // r[(b*H + h)*T + i] = sum_c dO[b*T + i][h*dk + c] * O[b*T + i][h*dk + c]; one wave per (row, head)
 __global__ __launch_bounds__(256) void attn_rowdot_kernel(const float* __restrict__ dO, const float* __restrict__ O,
                                                           float* __restrict__ r, int64_t B, int64_t H, int64_t T,
@@ -160,38 +194,44 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AbP p) {
         a[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fdo[ks], vb, a[t], 0, 0, 0);
       }
   };
-  // dP (dropout-masked dPd) and P of element (t, r) of key block j0
-  auto elem = [&](const f32x4 (&a)[4], int t, int r, int j0, float& pv, float& g) {
-    const int i = ib + r, j = j0 + 16 * t + (lane & 15);
-    pv = 0.f;
-    g = 0.f;
-    if (i < T && j < len) {
-      const int64_t idx = prow0 + (int64_t)r * p.T + j;
-      pv = p.P[idx];
-      g = a[t][r];
-      if (p.p_drop > 0.f) g = dropout_keep(seed, p.rng_stream, (uint64_t)idx, p.p_drop) ? g * keep : 0.f;
-    }
-  };
 
   // r_i = sum_j dP P = dO_i . O_i (attn_rowdot_kernel, before this kernel)
   float rs[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) rs[r] = (ib + r < T) ? p.rsum[bh * p.T + ib + r] : 0.f;
 
-  // ---- pass B: dQu += dS K, dQv += skew(dS) Pband ----
+  // next key block's operands in registers: V, K rows, the Ppos band, this lane's 16 P elements
+  float4 nv[3], nk[3], nb[6];
+  float np[4][4];
+  auto fetch = [&](int kb) {
+    const int j0 = kb * BK;
+    const int rbase = T - 1 - (i0 + BQ - 1) + j0;
+    fetch_rows<3>(nv, p.v, p.ldkv, b * p.T, j0, BK, 0, len, hoff, dk);
+    fetch_rows<3>(nk, p.k, p.ldkv, b * p.T, j0, BK, 0, len, hoff, dk);
+    fetch_rows<6>(nb, p.pos, p.d, 0, rbase, 127, 0, npos, hoff, dk);
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = ib + r, j = j0 + 16 * t + (lane & 15);
+        np[t][r] = (i < T && j < len) ? p.P[prow0 + (int64_t)r * p.T + j] : 0.f;
+      }
+  };
+
+  // ---- dQu += dS K, dQv += skew(dS) Pband ----
   f32x4 aq[3], av[3];
 #pragma unroll
   for (int u = 0; u < 3; ++u) { aq[u] = f32x4{0.f, 0.f, 0.f, 0.f}; av[u] = aq[u]; }
   const int wb = 48 - 16 * w;   // this wave's band offset
   uint16_t* D = Ds[w];
   uint16_t* G = Gs[w];
+  if (nkb > 0) fetch(0);
   for (int kb = 0; kb < nkb; ++kb) {
     const int j0 = kb * BK;
-    const int rbase = T - 1 - (i0 + BQ - 1) + j0;
     __syncthreads();
-    stage_rows(Vs, nullptr, 0, p.v, p.ldkv, b * p.T, j0, BK, 0, len, hoff, dk);
-    stage_rows(nullptr, Kt, LT, p.k, p.ldkv, b * p.T, j0, BK, 0, len, hoff, dk);
-    stage_rows(nullptr, Pbt, LB, p.pos, p.d, 0, rbase, 127, 0, npos, hoff, dk);
+    put_rows<3>(Vs, nullptr, 0, nv, BK, dk);
+    put_rows<3>(nullptr, Kt, LT, nk, BK, dk);
+    put_rows<6>(nullptr, Pbt, LB, nb, 127, dk);
     for (int e = lane; e < 16 * LG / 2; e += 64) reinterpret_cast<uint32_t*>(G)[e] = 0u;
     __syncthreads();
     f32x4 a[4];
@@ -200,14 +240,20 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AbP p) {
     for (int t = 0; t < 4; ++t)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        float pv, g;
-        elem(a, t, r, j0, pv, g);
-        const float ds = pv * (g - rs[r]) * p.scale;
+        const int i = ib + r, j = j0 + 16 * t + (lane & 15);
+        float g = 0.f;
+        if (i < T && j < len) {
+          g = a[t][r];
+          if (p.p_drop > 0.f)
+            g = dropout_keep(seed, p.rng_stream, (uint64_t)(prow0 + (int64_t)r * p.T + j), p.p_drop) ? g * keep : 0.f;
+        }
+        const float ds = np[t][r] * (g - rs[r]) * p.scale;
         const int ii = 4 * (lane >> 4) + r, jj = 16 * t + (lane & 15);
         const uint16_t bv = f2bf(ds);
         D[ii * LW + jj] = bv;
         G[ii * LG + jj - ii + 15] = bv;
       }
+    if (kb + 1 < nkb) fetch(kb + 1);   // the P elements are consumed: the next block's loads overlap the MFMAs
     wsync();
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
@@ -283,19 +329,39 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkv_kernel(AbP p) {
   uint16_t* PW = Pw[w];
   uint16_t* DW = Dw[w];
   const int nqb = (j0 < len) ? (len + BQ - 1) / BQ : 0;   // query rows >= len have P == 0
+  // next query block's operands in registers: dO and Qu rows, the P block (row-major, coalesced along
+  // keys), the row sums
+  float4 ndo[3], nqu[3];
+  float npb[BQ * BK / 256];
+  float nrs = 0.f;
+  auto fetch = [&](int qb) {
+    const int i0 = qb * BQ;
+    fetch_rows<3>(ndo, p.dO, p.ldq, b * p.T, i0, BQ, 0, T, hoff, dk);
+    fetch_rows<3>(nqu, p.qu, p.ldq, b * p.T, i0, BQ, 0, T, hoff, dk);
+#pragma unroll
+    for (int it = 0; it < BQ * BK / 256; ++it) {
+      const int e = threadIdx.x + it * 256;
+      const int ii = e / BK, kk = e - ii * BK;
+      const int i = i0 + ii, j = j0 + kk;
+      npb[it] = (i < T && j < T) ? p.P[(bh * p.T + i) * p.T + j] : 0.f;
+    }
+    if (threadIdx.x < BQ) nrs = (i0 + threadIdx.x < T) ? p.rsum[bh * p.T + i0 + threadIdx.x] : 0.f;
+  };
+  if (nqb > 0) fetch(0);
   for (int qb = 0; qb < nqb; ++qb) {
     const int i0 = qb * BQ;
     __syncthreads();
-    stage_rows(Os, Ot, LT, p.dO, p.ldq, b * p.T, i0, BQ, 0, T, hoff, dk);
-    stage_rows(nullptr, Qt, LT, p.qu, p.ldq, b * p.T, i0, BQ, 0, T, hoff, dk);
-    // P rows i0.. (coalesced along keys; rows of odd length T are not 16-byte aligned) -> P^T in LDS
-    for (int e = threadIdx.x; e < BQ * BK; e += 256) {
+    put_rows<3>(Os, Ot, LT, ndo, BQ, dk);
+    put_rows<3>(nullptr, Qt, LT, nqu, BQ, dk);
+#pragma unroll
+    for (int it = 0; it < BQ * BK / 256; ++it) {
+      const int e = threadIdx.x + it * 256;
       const int ii = e / BK, kk = e - ii * BK;
-      const int i = i0 + ii, j = j0 + kk;
-      Pt[kk * (BQ + 1) + ii] = (i < T && j < T) ? p.P[(bh * p.T + i) * p.T + j] : 0.f;
+      Pt[kk * (BQ + 1) + ii] = npb[it];
     }
-    for (int e = threadIdx.x; e < BQ; e += 256) Rs[e] = (i0 + e < T) ? p.rsum[bh * p.T + i0 + e] : 0.f;
+    if (threadIdx.x < BQ) Rs[threadIdx.x] = nrs;
     __syncthreads();
+    if (qb + 1 < nqb) fetch(qb + 1);
     // dPd^T = V dO^T (16 keys x 64 queries per wave)
     f32x4 a[4];
 #pragma unroll
