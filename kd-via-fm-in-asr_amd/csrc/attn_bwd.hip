@@ -450,64 +450,108 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dpos_kernel(AbP p) {
   const int qh = w & 1, kh = w >> 1;   // dS computation: query half, key half (48 keys)
   const int64_t b0 = bchunk * p.bpc;
   const int64_t b1 = min<int64_t>(p.B, b0 + p.bpc);
-  for (int64_t b = b0; b < b1; ++b) {
-    const int len = p.lens ? (int)min<int64_t>(p.lens[b], p.T) : T;
+  // iterations (utterance b, query block ib0) that address a valid key for these positions
+  auto ulen = [&](int64_t bb) { return p.lens ? (int)min<int64_t>(p.lens[bb], p.T) : T; };
+  auto advance = [&](int64_t& bb, int& ib, int& ln) -> bool {
+    ib += NPQ;
+    while (bb < b1) {
+      for (; ib < ln; ib += NPQ) {
+        const int jb = r0 - (T - 1) + ib;
+        if (!(jb + NPJ <= 0 || jb >= ln)) return true;
+      }
+      if (++bb >= b1) break;
+      ib = 0;
+      ln = ulen(bb);
+      if (ib < ln) {
+        const int jb = r0 - (T - 1) + ib;
+        if (!(jb + NPJ <= 0 || jb >= ln)) return true;
+      }
+    }
+    return false;
+  };
+  // next iteration's operands in registers (software pipeline): V rows, Qv rows, row sums, this
+  // lane's dO fragments and 12 P elements
+  float4 nvr[(NPJ * 12 + 255) / 256], nqr[(NPQ * 12 + 255) / 256];
+  float nrs = 0.f;
+  bf16x8 nfdo[2];
+  float np[3][4];
+  auto fetch = [&](int64_t bb, int ib, int ln) {
+    const int jb = r0 - (T - 1) + ib;
+    const int64_t bhh = bb * p.H + h;
+    fetch_rows<(NPJ * 12 + 255) / 256>(nvr, p.v, p.ldkv, bb * p.T, jb, NPJ, 0, ln, hoff, dk);
+    fetch_rows<(NPQ * 12 + 255) / 256>(nqr, p.qv, p.ldq, bb * p.T, ib, NPQ, 0, ln, hoff, dk);
+    if (threadIdx.x < NPQ) nrs = (ib + (int)threadIdx.x < ln) ? p.rsum[bhh * p.T + ib + threadIdx.x] : 0.f;
+    const int iq = ib + 16 * qh + (lane & 15);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int c0 = ks * 32 + 8 * (lane >> 4);
+      const bool ok = iq < ln;
+      nfdo[ks] = frag8(p.dO + (bb * p.T + (ok ? iq : 0)) * p.ldq + hoff + c0, ok ? dk - c0 : 0);
+    }
+#pragma unroll
+    for (int t = 0; t < 3; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int il = 16 * qh + 4 * (lane >> 4) + r, jl = 48 * kh + 16 * t + (lane & 15);
+        const int i = ib + il, j = jb + jl;
+        np[t][r] = (i < ln && j >= 0 && j < ln) ? p.P[(bhh * p.T + i) * p.T + j] : 0.f;
+      }
+  };
+  int64_t b = b0;
+  int ib0 = -NPQ, len = b0 < b1 ? ulen(b0) : 0;
+  bool more = b0 < b1 && advance(b, ib0, len);
+  if (more) fetch(b, ib0, len);
+  while (more) {
     const int64_t bh = b * p.H + h;
-    for (int ib0 = 0; ib0 < len; ib0 += NPQ) {
-      const int jbase = r0 - (T - 1) + ib0;
-      if (jbase + NPJ <= 0 || jbase >= len) continue;   // no valid key for these positions
-      __syncthreads();
-      stage_rows(Vs, nullptr, 0, p.v, p.ldkv, b * p.T, jbase, NPJ, 0, len, hoff, dk);
-      stage_rows(nullptr, Qt, LQ3, p.qv, p.ldq, b * p.T, ib0, NPQ, 0, len, hoff, dk);
-      for (int e = threadIdx.x; e < NPQ; e += 256) Rs[e] = (ib0 + e < len) ? p.rsum[bh * p.T + ib0 + e] : 0.f;
-      __syncthreads();
-      // dPd for queries ib0 + 16 qh + .., keys jbase + 48 kh + ..
-      const int iq = ib0 + 16 * qh + (lane & 15);
-      bf16x8 fdo[2];
+    const int jbase = r0 - (T - 1) + ib0;
+    const int cur_len = len;
+    const int cur_ib0 = ib0;
+    __syncthreads();
+    put_rows<(NPJ * 12 + 255) / 256>(Vs, nullptr, 0, nvr, NPJ, dk);
+    put_rows<(NPQ * 12 + 255) / 256>(nullptr, Qt, LQ3, nqr, NPQ, dk);
+    if (threadIdx.x < NPQ) Rs[threadIdx.x] = nrs;
+    const bf16x8 fdo[2] = {nfdo[0], nfdo[1]};
+    __syncthreads();
+    // dPd for queries ib0 + 16 qh + .., keys jbase + 48 kh + ..
+    f32x4 a[3];
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const int c0 = ks * 32 + 8 * (lane >> 4);
-        const bool ok = iq < len;
-        fdo[ks] = frag8(p.dO + (b * p.T + (ok ? iq : 0)) * p.ldq + hoff + c0, ok ? dk - c0 : 0);
+    for (int t = 0; t < 3; ++t) a[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int t = 0; t < 3; ++t) {
+        const bf16x8 vb = *reinterpret_cast<const bf16x8*>(Vs + (48 * kh + 16 * t + (lane & 15)) * LR + ks * 32 +
+                                                             8 * (lane >> 4));
+        a[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fdo[ks], vb, a[t], 0, 0, 0);
       }
-      f32x4 a[3];
 #pragma unroll
-      for (int t = 0; t < 3; ++t) a[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < 3; ++t)
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int t = 0; t < 3; ++t) {
-          const bf16x8 vb = *reinterpret_cast<const bf16x8*>(Vs + (48 * kh + 16 * t + (lane & 15)) * LR + ks * 32 +
-                                                               8 * (lane >> 4));
-          a[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fdo[ks], vb, a[t], 0, 0, 0);
+      for (int r = 0; r < 4; ++r) {
+        const int il = 16 * qh + 4 * (lane >> 4) + r, jl = 48 * kh + 16 * t + (lane & 15);
+        const int i = cur_ib0 + il, j = jbase + jl;
+        float ds = 0.f;
+        if (i < cur_len && j >= 0 && j < cur_len) {
+          const int64_t idx = (bh * p.T + i) * p.T + j;
+          float g = a[t][r];
+          if (p.p_drop > 0.f) g = dropout_keep(seed, p.rng_stream, (uint64_t)idx, p.p_drop) ? g * keep : 0.f;
+          ds = np[t][r] * (g - Rs[il]) * p.scale;
         }
-#pragma unroll
-      for (int t = 0; t < 3; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int il = 16 * qh + 4 * (lane >> 4) + r, jl = 48 * kh + 16 * t + (lane & 15);
-          const int i = ib0 + il, j = jbase + jl;
-          float ds = 0.f;
-          if (i < len && j >= 0 && j < len) {
-            const int64_t idx = (bh * p.T + i) * p.T + j;
-            const float pv = p.P[idx];
-            float g = a[t][r];
-            if (p.p_drop > 0.f) g = dropout_keep(seed, p.rng_stream, (uint64_t)idx, p.p_drop) ? g * keep : 0.f;
-            ds = pv * (g - Rs[il]) * p.scale;
-          }
-          Dl[il * LDL + jl] = f2bf(ds);
-        }
-      __syncthreads();
-      // dPpos[r0 + 16 w + m] += sum_i dS[i][(16 w + m) + i] Qv_i: A[m][k = i] = Dl[i][16 w + m + i]
-      const int m = lane & 15, kq = 8 * (lane >> 4);
-      bf16x8 fa;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) fa[e] = (short)Dl[(kq + e) * LDL + 16 * w + m + kq + e];
-#pragma unroll
-      for (int u = 0; u < 3; ++u) {
-        const bf16x8 qb = *reinterpret_cast<const bf16x8*>(Qt + (16 * u + (lane & 15)) * LQ3 + kq);
-        acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, qb, acc[u], 0, 0, 0);
+        Dl[il * LDL + jl] = f2bf(ds);
       }
+    // the P elements are consumed: the next iteration's loads overlap the dPpos MFMAs
+    more = advance(b, ib0, len);
+    if (more) fetch(b, ib0, len);
+    __syncthreads();
+    // dPpos[r0 + 16 w + m] += sum_i dS[i][(16 w + m) + i] Qv_i: A[m][k = i] = Dl[i][16 w + m + i]
+    const int m = lane & 15, kq = 8 * (lane >> 4);
+    bf16x8 fa;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) fa[e] = (short)Dl[(kq + e) * LDL + 16 * w + m + kq + e];
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      const bf16x8 qb = *reinterpret_cast<const bf16x8*>(Qt + (16 * u + (lane & 15)) * LQ3 + kq);
+      acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, qb, acc[u], 0, 0, 0);
     }
   }
 #pragma unroll
