@@ -182,5 +182,13 @@ def check(rc: int, what: str) -> None:
         raise KdfmError(f"{what} failed (status {rc}): {msg}")
 
 
+_FN: dict = {}
+
+
 def call(name: str, *args) -> None:
-    check(getattr(lib(), name)(*args), name)
+    fn = _FN.get(name)
+    if fn is None:
+        fn = _FN[name] = getattr(lib(), name)
+    rc = fn(*args)
+    if rc:
+        check(rc, name)

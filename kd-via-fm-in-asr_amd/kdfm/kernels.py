@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import struct
 
 import torch
 
@@ -333,53 +334,60 @@ def cast_bf16_t(src, dst, table, ntab, nblocks):
     call("kdfm_cast_bf16_t", ptr(_f32(src)), ptr(dst), ptr(table), int(ntab), int(nblocks), _s())
 
 
+# kdfm_gemm_desc packed with one struct call into a reusable buffer (filling a ctypes Structure
+# field by field cost ~6 µs of host time per GEMM launch).  Field order / native alignment match
+# include/kdfm.h kdfm_gemm_desc (tests/test_abi.py checks the layout against GemmDesc).  Launches are
+# issued from one host thread (the engine's), so one buffer suffices.
+_GEMM_FMT = struct.Struct("@7P17q4fPQ7i2qPqqPfPqPqPq")
+_GEMM_BUF = C.create_string_buffer(_GEMM_FMT.size)
+_GEMM_DESC = C.cast(_GEMM_BUF, C.POINTER(GemmDesc))
+_GEMM_WS_OFF = _GEMM_FMT.size - 4 * 8   # (ws, ws_len, Bh, sBh) are the last four 8-byte fields
+
+
+def _p(t):
+    return 0 if t is None else ptr(t)
+
+
 def gemm(A, B, Cout, M, N, K, sAm, sAk, sBk, sBn, sCm, sCn, *, amode, bmode,
          batch=(1, 1), bA=(0, 0), bB=(0, 0), bC=(0, 0), alpha=1.0, epi=0, bias=None, R=None, rscale=1.0,
          aux=None, Cpre=None, beta=0.0, dropout_p=0.0, seed=None, rng_stream=0, splitk=1,
          conv=None, math=None, rowmask=None, mse=None, tag=None, ones_out=None, Bh=None, nbytes=None):
-    d = GemmDesc()
-    if Bh is not None and (math or _State.math) == "bf16":
-        d.Bh, d.sBh = Bh
-    d.ones_col = -1
-    if ones_out is not None:
-        d.ones_out, d.ones_col = ptr(ones_out), int(N) - 1
-    d.A, d.B, d.C = ptr(A), ptr(B), ptr(Cout)
-    d.bias, d.R, d.aux, d.Cpre = ptr(bias), ptr(R), ptr(aux), ptr(Cpre)
-    d.M, d.N, d.K = int(M), int(N), int(K)
-    d.sAm, d.sAk, d.sBk, d.sBn, d.sCm, d.sCn = sAm, sAk, sBk, sBn, sCm, sCn
-    d.batch1, d.batch2 = batch
-    d.bA1, d.bA2 = bA
-    d.bB1, d.bB2 = bB
-    d.bC1, d.bC2 = bC
-    d.alpha, d.beta, d.rscale, d.dropout_p = alpha, beta, rscale, dropout_p
-    d.seed = ptr(seed)
-    d.rng_stream = rng_stream
+    mth = math or _State.math
+    bh, sbh = Bh if (Bh is not None and mth == "bf16") else (None, 0)
+    ones_col = int(N) - 1 if ones_out is not None else -1
     if dropout_p > 0.0:
         epi |= _lib.EPI_DROPOUT
-    d.amode, d.bmode, d.epi = amode, bmode, epi
-    d.math = _MATH[math or _State.math]
-    d.splitk = splitk
-    if conv is not None:
-        d.conv_taps, d.conv_pad, d.conv_c, d.conv_t = conv
+    taps, pad, cc, ct = conv if conv is not None else (0, 0, 0, 0)
+    mlen, mT, mdiv = 0, 0, 0
     if rowmask is not None:
-        lens, T, div = rowmask
-        d.mask_len, d.mask_T, d.mask_div = ptr(_i64(lens)), int(T), int(div)
-        d.epi |= _lib.EPI_ROWMASK
+        lens, mT, mdiv = rowmask
+        mlen = ptr(_i64(lens))
+        epi |= _lib.EPI_ROWMASK
+    lacc, lscale = 0, 0.0
     if mse is not None:
         acc, lscale = mse
-        d.loss_acc, d.loss_scale = ptr(acc), float(lscale)
-        d.epi |= _lib.EPI_MSE
-    if d.epi == _lib.EPI_ATOMIC and (d.math == _lib.KDFM_MATH_BF16 or (_State.deterministic and splitk > 1)):
-        nws = _lib.lib().kdfm_gemm_ws(C.byref(d))
+        lacc = ptr(acc)
+        epi |= _lib.EPI_MSE
+    math_id = _MATH[mth]
+    vals = [ptr(A), ptr(B), ptr(Cout), _p(bias), _p(R), _p(aux), _p(Cpre),
+            int(M), int(N), int(K), sAm, sAk, sBk, sBn, sCm, sCn, batch[0], batch[1],
+            bA[0], bA[1], bB[0], bB[1], bC[0], bC[1],
+            alpha, beta, rscale, dropout_p, _p(seed), rng_stream,
+            amode, bmode, epi, math_id, splitk, taps, pad, cc, ct,
+            mlen, int(mT), int(mdiv), lacc, float(lscale), _p(ones_out), ones_col,
+            0, 0, bh or 0, sbh]   # Bh: (device address, row stride) of the bf16 twin
+    _GEMM_FMT.pack_into(_GEMM_BUF, 0, *vals)
+    if epi == _lib.EPI_ATOMIC and (math_id == _lib.KDFM_MATH_BF16 or (_State.deterministic and splitk > 1)):
+        nws = _lib.lib().kdfm_gemm_ws(_GEMM_DESC)
         if nws > 0:
             ws = scratch(Cout.device, nws)
-            d.ws, d.ws_len = ws.data_ptr(), ws.numel()
+            struct.pack_into("@Pq", _GEMM_BUF, _GEMM_WS_OFF, ws.data_ptr(), ws.numel())
     tr = Trace.active
     if tr is not None and (tag in tr.tags or "*" in tr.tags):
         ev0 = torch.cuda.Event(enable_timing=True)
         ev1 = torch.cuda.Event(enable_timing=True)
         ev0.record()
-        call("kdfm_gemm", C.byref(d), _s())
+        call("kdfm_gemm", _GEMM_DESC, _s())
         ev1.record()
         if nbytes is None:   # fp32 storage: both operands and the output once, plus each side operand
             side = sum(1 for t in (R, aux, Cpre) if t is not None)
@@ -390,7 +398,7 @@ def gemm(A, B, Cout, M, N, K, sAm, sAk, sBk, sBn, sCm, sCn, *, amode, bmode,
         if "*" in tr.tags:
             tr.events.append(("gemm:" + ROUTES.get(int(_lib.lib().kdfm_gemm_last_route()), "?"), fl, nbytes, ev0, ev1))
         return
-    call("kdfm_gemm", C.byref(d), _s())
+    call("kdfm_gemm", _GEMM_DESC, _s())
 
 
 def _splitk_for(M, N, K):

@@ -74,3 +74,24 @@ def test_roctx_ranges_nest_without_a_gpu():
     finally:
         K.set_ranges(False)
     assert L.kdfm_range_pop() < 0   # region() closed everything it opened
+
+
+def test_gemm_desc_packing_matches_ctypes_layout():
+    """kernels.gemm packs kdfm_gemm_desc with struct (host fast path): the packed bytes must equal a
+    GemmDesc filled field by field with the same values."""
+    import ctypes as C
+    from kdfm import kernels as K
+    from kdfm._lib import GemmDesc
+    vals = list(range(1, 8)) + list(range(100, 117)) + [1.5, 2.5, 3.5, 0.25] + [7777, 2 ** 63 + 5] + \
+        list(range(10, 17)) + [21, 22] + [31, 32, 33] + [41, 0.5] + [51, 52] + [61, 62] + [71, 72]
+    names = [f[0] for f in GemmDesc._fields_]
+    assert len(vals) == len(names) == 50
+    d = GemmDesc()
+    for n, v in zip(names, vals):
+        setattr(d, n, v)
+    buf = C.create_string_buffer(K._GEMM_FMT.size)
+    K._GEMM_FMT.pack_into(buf, 0, *vals)
+    assert K._GEMM_FMT.size == C.sizeof(GemmDesc)
+    assert bytes(buf) == C.string_at(C.addressof(d), C.sizeof(d))
+    off = GemmDesc.ws.offset
+    assert off == K._GEMM_WS_OFF
