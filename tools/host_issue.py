@@ -37,3 +37,19 @@ for _ in range(steps):
     eng.train_step(wav, wl, tg, tl, None)
 torch.cuda.synchronize()
 print(f"back-to-back {1e3 * (time.perf_counter() - t0) / steps:.2f} ms/step", flush=True)
+# forward phase alone: host enqueue vs enqueue + drain
+fe, ff = [], []
+for _ in range(steps):
+    eng.advance_rng()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ctx = eng.forward(wav, wl, tg, tl, train=True)
+    t1 = time.perf_counter()
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    fe.append(t1 - t0)
+    ff.append(t2 - t0)
+    eng.backward(ctx)
+    del ctx
+    torch.cuda.synchronize()
+print(f"forward: enqueue {1e3 * min(fe):.2f} ms, enqueue+drain {1e3 * min(ff):.2f} ms", flush=True)
