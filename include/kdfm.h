@@ -229,6 +229,14 @@ int kdfm_preemph_pad(const float* wav, const int64_t* lengths, float* xp, int64_
                      float preemph, float dither, const uint64_t* seed, uint64_t rng_stream, void* stream);
 /* power[r, f] = spec[r, f]^2 + spec[r, nbins + f]^2 (spec rows = [re | im] from the DFT GEMM) */
 int kdfm_power_spectrum(const float* spec, float* power, int64_t rows, int64_t nbins, void* stream);
+/* Mel power spectrum via a 512-point real FFT per frame (FilterbankFeatures, audio_preprocessing.py:
+ * 93-103, 214-300): mel[f][m] = sum_{k in [fb_lo[m], fb_hi[m])} fb[m][k] |X_f[k]|^2 with
+ * X_f = FFT_512(window (win taps, centred) * xp[b][t hop + n]), f = b T + t; twiddle = e^{-2 pi i j/512}
+ * as (re, im) float pairs, j < 512; fb (nfilt, 257) row-major.  Replaces the DFT-as-GEMM + power +
+ * filterbank GEMM chain (same arithmetic in f32, ~35x fewer flops). */
+int kdfm_logmel_fft(const float* xp, int64_t ldx, const float* window, const float* twiddle, const float* fb,
+                    const int32_t* fb_lo, const int32_t* fb_hi, float* mel, int64_t B, int64_t T, int64_t hop,
+                    int64_t n_fft, int64_t win, int64_t nfilt, void* stream);
 /* log(mel + guard), per-feature mean / unbiased std over valid frames, zero beyond seq_len;
  * mel/out laid out (B, T, nfilt). */
 int kdfm_logmel_normalize(const float* mel, const int64_t* seq_len, float* out, int64_t B, int64_t T, int64_t nfilt,

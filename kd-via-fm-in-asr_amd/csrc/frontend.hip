@@ -189,6 +189,93 @@ __global__ __launch_bounds__(256) void im2col_kernel(const float* __restrict__ X
   cols[idx] = v;
 }
 
+
+// ---- STFT power + mel filterbank via a 512-point real FFT per frame ------------------------------
+// FilterbankFeatures (audio_preprocessing.py:93-103, 214-300): |STFT|^2 of the Hann(400)-windowed
+// frame centred in n_fft = 512, then the Slaney mel filterbank.  The DFT-as-GEMM formulation costs
+// 2 x 512 x 514 flops per frame on f32 MFMA; here one wave owns a frame and runs the real FFT as a
+// 256-point complex radix-2 FFT of z[m] = s[2m] + i s[2m+1] in LDS (8 in-place stages, twiddles
+// e^{-2 pi i j / 512} from a host-computed table), the real-FFT split
+//   X[k] = (Z[k] + conj Z[256-k]) / 2 - i W^k (Z[k] - conj Z[256-k]) / 2,   W = e^{-2 pi i / 512},
+// |X[k]|^2 for k = 0..256, and each mel filter's dot product over its nonzero bin range
+// [fb_lo, fb_hi).  Output mel (B*T, nfilt) f32 (log + per-feature normalisation follow).
+constexpr int FFT_N = 512, FFT_H = 256, FFT_WAVES = 4;
+
+// wave-local LDS hand-off (each wave owns its buffers): drain this wave's LDS ops; the asm's memory
+// clobber keeps the compiler from moving LDS accesses across it
+__device__ __forceinline__ void fft_wsync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ int bitrev8(int v) { return (int)(__builtin_bitreverse32((uint32_t)v) >> 24); }
+
+__global__ __launch_bounds__(64 * FFT_WAVES) void logmel_fft_kernel(
+    const float* __restrict__ xp, int64_t ldx, const float* __restrict__ win, const float2* __restrict__ tw,
+    const float* __restrict__ fb, const int* __restrict__ fb_lo, const int* __restrict__ fb_hi, float* __restrict__ mel,
+    int64_t B, int64_t T, int hop, int off, int nwin, int nfilt, int nbins) {
+  __shared__ float2 Zs[FFT_WAVES][FFT_H];
+  __shared__ float Pw[FFT_WAVES][FFT_H + 8];
+  __shared__ float2 W[FFT_N];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int e = threadIdx.x; e < FFT_N; e += 64 * FFT_WAVES) W[e] = tw[e];
+  __syncthreads();
+  float2* Z = Zs[w];
+  float* P = Pw[w];
+  const int64_t nframes = B * T;
+  for (int64_t f = (int64_t)blockIdx.x * FFT_WAVES + w; f < nframes; f += (int64_t)gridDim.x * FFT_WAVES) {
+    const int64_t b = f / T, t = f - b * T;
+    const float* src = xp + b * ldx + t * hop;
+    // z[m] = s[2m] + i s[2m+1], s[n] = win[n - off] x[t hop + n] on [off, off + nwin), stored bit-reversed
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int m = lane + 64 * q;
+      const int n0 = 2 * m, n1 = 2 * m + 1;
+      const float a = (n0 >= off && n0 < off + nwin) ? win[n0 - off] * src[n0] : 0.f;
+      const float c = (n1 >= off && n1 < off + nwin) ? win[n1 - off] * src[n1] : 0.f;
+      Z[bitrev8(m)] = make_float2(a, c);
+    }
+    fft_wsync();   // this wave's LDS writes complete before its reads
+    // radix-2 DIT stages: butterflies j = lane, lane + 64 of 128; twiddle W256^pos = W512^(2 pos * 256/len)
+#pragma unroll
+    for (int ls = 1; ls <= 8; ++ls) {
+      const int half = 1 << (ls - 1);
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int j = lane + 64 * q;
+        const int g = j >> (ls - 1), pos = j & (half - 1);
+        const int i0 = g * (2 * half) + pos, i1 = i0 + half;
+        const float2 wv = W[(pos << (9 - ls)) & (FFT_N - 1)];
+        const float2 u = Z[i0], v = Z[i1];
+        const float2 bv = make_float2(v.x * wv.x - v.y * wv.y, v.x * wv.y + v.y * wv.x);
+        Z[i0] = make_float2(u.x + bv.x, u.y + bv.y);
+        Z[i1] = make_float2(u.x - bv.x, u.y - bv.y);
+      }
+      fft_wsync();
+    }
+    // real-FFT split and power
+    for (int k = lane; k < nbins; k += 64) {
+      const float2 zk = Z[k & (FFT_H - 1)], zr = Z[(FFT_H - k) & (FFT_H - 1)];
+      const float er = 0.5f * (zk.x + zr.x), ei = 0.5f * (zk.y - zr.y);          // (Zk + conj Zr) / 2
+      const float dr = 0.5f * (zk.x - zr.x), di = 0.5f * (zk.y + zr.y);          // (Zk - conj Zr) / 2
+      const float2 wk = W[k & (FFT_N - 1)];
+      // -i W^k (dr + i di) = (wk.y dr + wk.x di) + i (wk.y di - wk.x dr)
+      const float xr = er + (wk.x * di + wk.y * dr);
+      const float xi = ei + (wk.y * di - wk.x * dr);
+      P[k] = xr * xr + xi * xi;
+    }
+    fft_wsync();
+    float* out = mel + f * nfilt;
+    for (int m = lane; m < nfilt; m += 64) {
+      const float* row = fb + (int64_t)m * nbins;
+      float acc = 0.f;
+      for (int k = fb_lo[m]; k < fb_hi[m]; ++k) acc = fmaf(row[k], P[k], acc);
+      out[m] = acc;
+    }
+    fft_wsync();   // Z / P are rewritten by the next frame
+  }
+}
+
 // TAP-MAJOR bf16 variant: cols[(b,t2,f2), tap*C + c] = bf16(X[b, 2*t2-1+ky, 2*f2-1+kx, c]); one thread
 // per 8 consecutive channels of one (row, tap): two coalesced float4 reads, one 16-byte store.  The
 // bf16 column matrix is the weight-gradient operand of the bf16 step (half the bytes of the f32 one).
@@ -264,6 +351,21 @@ int kdfm_preemph_pad(const float* wav, const int64_t* lengths, float* xp, int64_
   hipLaunchKernelGGL(preemph_pad_kernel, grid, dim3(256), 0, as_stream(stream), wav, lengths, xp, N, pad, preemph,
                      dither, seed, rng_stream);
   return check_launch("kdfm_preemph_pad");
+}
+
+int kdfm_logmel_fft(const float* xp, int64_t ldx, const float* window, const float* twiddle, const float* fb,
+                    const int32_t* fb_lo, const int32_t* fb_hi, float* mel, int64_t B, int64_t T, int64_t hop,
+                    int64_t n_fft, int64_t win, int64_t nfilt, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(xp && window && twiddle && fb && fb_lo && fb_hi && mel, "null pointer");
+  KDFM_REQUIRE(n_fft == FFT_N && win > 0 && win <= n_fft && nfilt > 0 && hop > 0, "n_fft must be 512");
+  if (B * T == 0) return KDFM_OK;
+  const int64_t groups = ceil_div(B * T, FFT_WAVES);
+  const unsigned grid = (unsigned)(groups < 2048 ? groups : 2048);
+  hipLaunchKernelGGL(logmel_fft_kernel, dim3(grid), dim3(64 * FFT_WAVES), 0, as_stream(stream), xp, ldx, window,
+                     reinterpret_cast<const float2*>(twiddle), fb, fb_lo, fb_hi, mel, B, T, (int)hop,
+                     (int)((n_fft - win) / 2), (int)win, (int)nfilt, (int)(n_fft / 2 + 1));
+  return check_launch("kdfm_logmel_fft");
 }
 
 int kdfm_power_spectrum(const float* spec, float* power, int64_t rows, int64_t nbins, void* stream) {

@@ -12,7 +12,8 @@ namespace kdfm {
 namespace {
 
 constexpr int BM = 64, BN = 64, BK = 32, NT = 256;
-constexpr int LDK_BF = BK + 8;   // bf16 image row stride (elements)
+constexpr int KSUB_BF = 2;                 // bf16: two 32-wide k halves per iteration (BK 64)
+constexpr int LDK_BF = BK * KSUB_BF + 8;   // bf16 image row stride (elements)
 constexpr int LDX_F32 = BM + 16; // f32 image row stride (elements) -> lanes 16..31 on banks +16
 
 using P = GemmP;
@@ -154,10 +155,10 @@ __device__ __forceinline__ void load_tile_B(float (&v)[8], const float* base, in
 
 // Write a staged 8-vector into the LDS image.  `kmajor_thread` = thread held 8 consecutive k.
 template <bool BF16, bool KRUN>
-__device__ __forceinline__ void store_lds(void* lds, const float (&v)[8]) {
+__device__ __forceinline__ void store_lds(void* lds, const float (&v)[8], int khalf = 0) {
   const int t = threadIdx.x;
   if constexpr (BF16) {
-    uint16_t* s = reinterpret_cast<uint16_t*>(lds);  // [64][LDK_BF]
+    uint16_t* s = reinterpret_cast<uint16_t*>(lds) + khalf * BK;  // [64][LDK_BF], k half khalf
     if constexpr (KRUN) {
       const int r = t >> 2, k = (t & 3) * 8;
       *reinterpret_cast<bf16x8*>(s + r * LDK_BF + k) = pack_bf16x8<bf16x8>(v);
@@ -184,6 +185,8 @@ __device__ __forceinline__ void store_lds(void* lds, const float (&v)[8]) {
 template <bool BF16, int AM, int BMODE, int EMODE = SKC_EPI_GENERIC>
 __global__ __launch_bounds__(NT) void gemm_kernel(P p) {
   constexpr int LDS_ELEMS = BF16 ? (64 * LDK_BF / 2) : (BK * LDX_F32);  // in floats
+  constexpr int KSUB = BF16 ? KSUB_BF : 1;   // 32-wide k halves per iteration
+  constexpr int BKI = BK * KSUB;             // k per iteration (one barrier pair)
   __shared__ __attribute__((aligned(16))) float smem[2 * LDS_ELEMS];
   float* As = smem;
   float* Bs = smem + LDS_ELEMS;
@@ -199,7 +202,7 @@ __global__ __launch_bounds__(NT) void gemm_kernel(P p) {
 
   const int64_t m0 = blk.x * BM;
   const int64_t n0 = blk.y * BN;
-  const int64_t kchunk = ceil_div(ceil_div(p.K, p.splitk), BK) * BK;
+  const int64_t kchunk = ceil_div(ceil_div(p.K, p.splitk), BKI) * BKI;
   const int64_t kbeg = split * kchunk;
   const int64_t kend = (kbeg + kchunk < p.K) ? (kbeg + kchunk) : p.K;
 
@@ -215,35 +218,44 @@ __global__ __launch_bounds__(NT) void gemm_kernel(P p) {
   constexpr bool A_KRUN = (AM != KDFM_LD_XC);
   constexpr bool B_KRUN = (BMODE == KDFM_LD_KC);
 
-  float va[8], vb[8];
-  if (kbeg < kend) {
-    load_tile_A<AM>(va, A, m0, kbeg, p.M, kend, p.sAm, p.sAk, p);
-    load_tile_B<BMODE>(vb, B, n0, kbeg, p.N, kend, p.sBk, p.sBn, p);
-  }
-  for (int64_t k0 = kbeg; k0 < kend; k0 += BK) {
-    __syncthreads();
-    store_lds<BF16, A_KRUN>(As, va);
-    store_lds<BF16, B_KRUN>(Bs, vb);
-    __syncthreads();
-    if (k0 + BK < kend) {  // prefetch next tile into registers while the MFMAs run
-      load_tile_A<AM>(va, A, m0, k0 + BK, p.M, kend, p.sAm, p.sAk, p);
-      load_tile_B<BMODE>(vb, B, n0, k0 + BK, p.N, kend, p.sBk, p.sBn, p);
+  float va[KSUB][8], vb[KSUB][8];
+  auto load_it = [&](int64_t k0) {
+#pragma unroll
+    for (int hh = 0; hh < KSUB; ++hh) {
+      load_tile_A<AM>(va[hh], A, m0, k0 + hh * BK, p.M, kend, p.sAm, p.sAk, p);
+      load_tile_B<BMODE>(vb[hh], B, n0, k0 + hh * BK, p.N, kend, p.sBk, p.sBn, p);
     }
+  };
+  if (kbeg < kend) load_it(kbeg);
+  for (int64_t k0 = kbeg; k0 < kend; k0 += BKI) {
+    __syncthreads();
+#pragma unroll
+    for (int hh = 0; hh < KSUB; ++hh) {
+      store_lds<BF16, A_KRUN>(As, va[hh], hh);
+      store_lds<BF16, B_KRUN>(Bs, vb[hh], hh);
+    }
+    __syncthreads();
+    if (k0 + BKI < kend) load_it(k0 + BKI);  // prefetch next tile into registers while the MFMAs run
     if constexpr (BF16) {
       const uint16_t* as = reinterpret_cast<const uint16_t*>(As);
       const uint16_t* bs = reinterpret_cast<const uint16_t*>(Bs);
-      bf16x8 af[2], bfr[2];
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
-        af[i] = *reinterpret_cast<const bf16x8*>(as + (wr * 32 + i * 16 + (lane & 15)) * LDK_BF + 8 * (lane >> 4));
+      for (int hh = 0; hh < KSUB; ++hh) {
+        bf16x8 af[2], bfr[2];
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
-        bfr[j] = *reinterpret_cast<const bf16x8*>(bs + (wc * 32 + j * 16 + (lane & 15)) * LDK_BF + 8 * (lane >> 4));
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < 2; ++i)
+          af[i] = *reinterpret_cast<const bf16x8*>(as + (wr * 32 + i * 16 + (lane & 15)) * LDK_BF + hh * BK +
+                                                   8 * (lane >> 4));
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          bfr[j] = *reinterpret_cast<const bf16x8*>(bs + (wc * 32 + j * 16 + (lane & 15)) * LDK_BF + hh * BK +
+                                                    8 * (lane >> 4));
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
     } else {
 #pragma unroll
       for (int kk = 0; kk < BK; kk += 4) {

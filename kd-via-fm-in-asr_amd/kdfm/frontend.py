@@ -3,10 +3,12 @@
 
 Device pipeline (all libkdfm kernels):
   preemph_pad (dither, preemphasis, length mask, centre zero-pad 256)
-  -> f32 MFMA GEMM: strided frames (hop 160, 400 taps at window offset 56) x DFT basis (400 x 514,
-     Hann(400, periodic=False) folded in, columns = [cos | -sin] of bins 0..256)
-  -> power = re^2 + im^2 -> f32 MFMA GEMM with the Slaney mel filterbank (80 x 257)
+  -> kdfm_logmel_fft: per frame (hop 160, Hann(400, periodic=False) centred in n_fft 512) a 512-point
+     real FFT in f32 (one wave, LDS radix-2), |X|^2 of bins 0..256 and the Slaney mel filterbank
+     (80 x 257, each filter over its nonzero bin range)
   -> log(x + 2^-24), per-feature normalisation over valid frames, zero beyond seq_len.
+(KDFM_FRONTEND_FFT=0 selects the earlier DFT-as-GEMM chain: f32 MFMA GEMM against a (400 x 514)
+[w cos | -w sin] basis, power, f32 filterbank GEMM.)
 Output layout (B, T, 80) channels-last; the NeMo-facing module returns the (B, 80, T) view.
 """
 from __future__ import annotations
@@ -75,10 +77,21 @@ class FrontendConsts:
         self.window = torch.tensor(hann_symmetric(cfg.win).astype(np.float32), device=device)
         self.fb = torch.tensor(slaney_filterbank(cfg.sample_rate, cfg.n_fft, cfg.nfilt), device=device)
         self.basis = torch.tensor(dft_basis(cfg.n_fft, cfg.win), device=device)
+        j = np.arange(cfg.n_fft, dtype=np.float64)
+        tw = np.stack([np.cos(2 * np.pi * j / cfg.n_fft), -np.sin(2 * np.pi * j / cfg.n_fft)], axis=1)
+        self.twiddle = torch.tensor(tw.astype(np.float32), device=device)
+        fbn = slaney_filterbank(cfg.sample_rate, cfg.n_fft, cfg.nfilt)
+        lo = np.array([np.flatnonzero(r)[0] if r.any() else 0 for r in fbn], dtype=np.int32)
+        hi = np.array([np.flatnonzero(r)[-1] + 1 if r.any() else 0 for r in fbn], dtype=np.int32)
+        self.fb_lo = torch.tensor(lo, device=device)
+        self.fb_hi = torch.tensor(hi, device=device)
 
 
 def mel_frames(cfg: Ver5Config, n_samples: int) -> int:
     return n_samples // cfg.hop + 1
+
+
+_FFT = __import__("os").environ.get("KDFM_FRONTEND_FFT", "1") == "1"
 
 
 def frontend_forward(cfg: Ver5Config, consts: FrontendConsts, wav: torch.Tensor, wav_len: torch.Tensor,
@@ -103,16 +116,20 @@ def _frontend(cfg, consts, wav, wav_len, mel_len, dither, seed, rng_stream, out)
     dev = wav.device
     xp = torch.empty(B, N + 2 * pad, device=dev)
     K.preemph_pad(wav.contiguous(), wav_len, xp, pad, cfg.preemph, dither, seed, rng_stream)
-    spec = torch.empty(B * T, 2 * F, device=dev)
-    off = (cfg.n_fft - cfg.win) // 2
-    xv = xp[:, off:]
-    K.gemm(xv, consts.basis, spec, T, 2 * F, cfg.win, cfg.hop, 1, 2 * F, 1, 2 * F, 1,
-           amode=_lib.LD_KC, bmode=_lib.LD_XC, batch=(B, 1), bA=(N + 2 * pad, 0), bC=(T * 2 * F, 0), math="f32")
-    power = torch.empty(B * T, F, device=dev)
-    K.power_spectrum(spec, power)
-    del spec
     mel = torch.empty(B * T, cfg.nfilt, device=dev)
-    K.linear(power, consts.fb, None, mel, math="f32")
+    if _FFT and cfg.n_fft == 512:
+        K.logmel_fft(xp, consts.window, consts.twiddle, consts.fb, consts.fb_lo, consts.fb_hi, mel, B, T, cfg.hop,
+                     cfg.n_fft, cfg.win)
+    else:
+        spec = torch.empty(B * T, 2 * F, device=dev)
+        off = (cfg.n_fft - cfg.win) // 2
+        xv = xp[:, off:]
+        K.gemm(xv, consts.basis, spec, T, 2 * F, cfg.win, cfg.hop, 1, 2 * F, 1, 2 * F, 1,
+               amode=_lib.LD_KC, bmode=_lib.LD_XC, batch=(B, 1), bA=(N + 2 * pad, 0), bC=(T * 2 * F, 0), math="f32")
+        power = torch.empty(B * T, F, device=dev)
+        K.power_spectrum(spec, power)
+        del spec
+        K.linear(power, consts.fb, None, mel, math="f32")
     if out is None:
         out = torch.empty(B, T, cfg.nfilt, device=dev)
     K.logmel_normalize(mel, mel_len, out, B, T, cfg.nfilt, cfg.log_guard)

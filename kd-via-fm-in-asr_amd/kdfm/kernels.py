@@ -566,6 +566,15 @@ def preemph_pad(wav, lengths, xp, pad, preemph, dither, seed, rng_stream):
          float(dither), ptr(seed), int(rng_stream), _s())
 
 
+def logmel_fft(xp, window, twiddle, fb, fb_lo, fb_hi, mel, B, T, hop, n_fft, win):
+    """mel (B*T, nfilt) = filterbank(|FFT_512(window * frame)|^2) per frame of the padded waveform xp."""
+    nfilt = fb.shape[0]
+    assert xp.shape[0] == B and xp.stride(1) == 1 and mel.shape == (B * T, nfilt) and fb.shape[1] == n_fft // 2 + 1
+    assert twiddle.shape == (n_fft, 2) and fb_lo.dtype == torch.int32 and fb_hi.dtype == torch.int32
+    call("kdfm_logmel_fft", ptr(_f32(xp)), xp.stride(0), ptr(_f32(window)), ptr(_f32(twiddle)), ptr(_f32(fb)),
+         ptr(fb_lo), ptr(fb_hi), ptr(_f32(mel)), B, T, hop, n_fft, win, nfilt, _s())
+
+
 def power_spectrum(spec, power):
     rows, F = power.shape
     assert spec.shape == (rows, 2 * F)

@@ -126,13 +126,20 @@ class AudioToMelSpectrogramPreprocessor(nn.Module):
         self.featurizer.register_buffer("window", c.window)
         self.featurizer.register_buffer("fb", c.fb.unsqueeze(0))
         self.featurizer.register_buffer("dft_basis", c.basis, persistent=False)
+        self.featurizer.register_buffer("fft_twiddle", c.twiddle, persistent=False)
+        # the filterbank may be replaced by a checkpoint's: every filter over all bins (dense)
+        self.featurizer.register_buffer("fb_lo", torch.zeros(features, dtype=torch.int32), persistent=False)
+        self.featurizer.register_buffer("fb_hi", torch.full((features,), n_fft // 2 + 1, dtype=torch.int32),
+                                        persistent=False)
         self.register_buffer("_seed", torch.zeros(1, dtype=torch.int64), persistent=False)
 
     @torch.no_grad()
     def forward(self, input_signal, length):
         _dev_check(input_signal)
         c = type("C", (), {})()
-        c.window, c.fb, c.basis = self.featurizer.window, self.featurizer.fb[0], self.featurizer.dft_basis
+        f = self.featurizer
+        c.window, c.fb, c.basis, c.twiddle, c.fb_lo, c.fb_hi = (f.window, f.fb[0].contiguous(), f.dft_basis,
+                                                                f.fft_twiddle, f.fb_lo, f.fb_hi)
         B = input_signal.shape[0]
         mel_len = torch.empty(B, dtype=torch.int64, device=input_signal.device)
         K.subsample_lengths(length.to(torch.int64).contiguous(), mel_len, None, None, self.cfg.hop)

@@ -2,7 +2,10 @@
 the real engine backward on the GPU: two ranks share cuda:0 over gloo (RCCL needs one GPU per rank;
 the 1-GPU box cannot host an nccl world of 2), so this checks the stream ordering of the overlap -
 the comm stream waits for the main stream and the weight-gradient side stream before each bucket -
-against a plain all-reduce of the finished local gradients."""
+against a plain all-reduce of the finished local gradients.  The engine runs in its default
+(non-deterministic, overlapped weight-gradient stream) mode, whose repeated runs differ by float
+summation order; the tolerance is the larger of 1e-4 x max|grad| and 8x the run-to-run difference
+measured here — a mis-ordered bucket would be off by O(|grad|) over whole buckets."""
 import os
 import socket
 
@@ -47,6 +50,11 @@ def _worker(rank, world, port, out):
     del ctx
     torch.cuda.synchronize()
     ref = eng.student.grad.clone()
+    ctx = eng.forward(wav, wl, tg, tl, train=True)   # same RNG state: run-to-run float noise only
+    eng.backward(ctx)
+    del ctx
+    torch.cuda.synchronize()
+    noise = float((eng.student.grad - ref).abs().max())
     dist.all_reduce(ref)
     ar = BucketedGradAllReduce(eng.student.numel, buckets=4)
     grad = eng.student.grad
@@ -56,7 +64,7 @@ def _worker(rank, world, port, out):
     del ctx
     scale = ar(grad)
     torch.cuda.synchronize()
-    tol = 1e-4 * ref.abs().max().item()
+    tol = max(1e-4 * ref.abs().max().item(), 8.0 * noise)
     out[rank] = (float((grad - ref).abs().max()), tol, scale, early)
     dist.destroy_process_group()
 
