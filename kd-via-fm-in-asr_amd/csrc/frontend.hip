@@ -136,40 +136,56 @@ __global__ __launch_bounds__(256) void logmel_norm_reg_kernel(const float* __res
 
 // SpecAugment: per utterance `fmasks` frequency bands of width floor(U*(fwidth+1)) and `tmasks`
 // time bands of width floor(U*(max(1,int(len*twidth))+1)); masked cells set to 0.
-__device__ __forceinline__ bool spec_masked(int64_t b, int64_t t, int64_t f, int64_t len, int64_t nf, int fmasks,
-                                            int fwidth, int tmasks, float twidth, uint64_t seed, uint64_t st) {
-  for (int q = 0; q < fmasks; ++q) {
-    const uint64_t base = (uint64_t)b * 64 + (uint64_t)q * 2;
-    int w = (int)(rng_uniform(seed, st, base) * (fwidth + 1));
-    if (w > fwidth) w = fwidth;
-    if (w > nf) w = (int)nf;
-    const int64_t s0 = (int64_t)(rng_uniform(seed, st, base + 1) * (float)(nf - w + 1));
-    if (f >= s0 && f < s0 + w) return true;
-  }
-  int64_t maxw = (int64_t)((float)len * twidth);
-  if (maxw < 1) maxw = 1;
-  for (int q = 0; q < tmasks; ++q) {
-    const uint64_t base = (uint64_t)b * 64 + 32 + (uint64_t)q * 2;
-    int64_t w = (int64_t)(rng_uniform(seed, st, base) * (float)(maxw + 1));
-    if (w > maxw) w = maxw;
-    int64_t room = len - w + 1;
-    if (room < 1) room = 1;
-    const int64_t s0 = (int64_t)(rng_uniform(seed, st, base + 1) * (float)room);
-    if (t >= s0 && t < s0 + w) return true;
-  }
-  return false;
-}
-
+// One block per (utterance, chunk of SA_EPB cells): the utterance's mask intervals (counter-RNG draws:
+// frequency mask q from indices b*64 + 2q, + 1; time mask q from b*64 + 32 + 2q, + 1) are computed once
+// into LDS by the first fmasks + tmasks threads, then every cell tests against them (the per-cell
+// formulation re-drew all the masks for each of the B x T x 80 cells).
+constexpr int SA_EPB = 256 * 8;
 __global__ __launch_bounds__(256) void specaug_kernel(float* __restrict__ x, const int64_t* __restrict__ sl,
                                                       uint8_t* __restrict__ mask_out, int64_t B, int64_t T, int64_t nf,
                                                       int fmasks, int fwidth, int tmasks, float twidth,
                                                       const uint64_t* seed_ptr, uint64_t st) {
-  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (idx >= B * T * nf) return;
-  const int64_t f = idx % nf, t = (idx / nf) % T, b = idx / (nf * T);
-  const bool m = spec_masked(b, t, f, sl[b], nf, fmasks, fwidth, tmasks, twidth, load_seed(seed_ptr), st);
-  if (m) x[idx] = 0.f;
-  if (mask_out) mask_out[idx] = m ? 1 : 0;
+  __shared__ int lo[32], hi[32];   // [0, fmasks): frequency bands; [fmasks, fmasks + tmasks): time bands
+  const int64_t b = blockIdx.y;
+  const int64_t cells = T * nf;
+  const int64_t len = sl[b];
+  if (threadIdx.x < fmasks + tmasks) {
+    const uint64_t seed = load_seed(seed_ptr);
+    const int q = threadIdx.x;
+    if (q < fmasks) {
+      const uint64_t base = (uint64_t)b * 64 + (uint64_t)q * 2;
+      int w = (int)(rng_uniform(seed, st, base) * (fwidth + 1));
+      if (w > fwidth) w = fwidth;
+      if (w > nf) w = (int)nf;
+      const int64_t s0 = (int64_t)(rng_uniform(seed, st, base + 1) * (float)(nf - w + 1));
+      lo[q] = (int)s0;
+      hi[q] = (int)(s0 + w);
+    } else {
+      const int qt = q - fmasks;
+      int64_t maxw = (int64_t)((float)len * twidth);
+      if (maxw < 1) maxw = 1;
+      const uint64_t base = (uint64_t)b * 64 + 32 + (uint64_t)qt * 2;
+      int64_t w = (int64_t)(rng_uniform(seed, st, base) * (float)(maxw + 1));
+      if (w > maxw) w = maxw;
+      int64_t room = len - w + 1;
+      if (room < 1) room = 1;
+      const int64_t s0 = (int64_t)(rng_uniform(seed, st, base + 1) * (float)room);
+      lo[q] = (int)s0;
+      hi[q] = (int)(s0 + w);
+    }
+  }
+  __syncthreads();
+  const int n = (int)nf;
+  for (int64_t c = (int64_t)blockIdx.x * SA_EPB + threadIdx.x; c < min<int64_t>(cells, (int64_t)(blockIdx.x + 1) * SA_EPB);
+       c += 256) {
+    const int t = (int)(c / n), f = (int)(c - (int64_t)t * n);
+    bool m = false;
+    for (int q = 0; q < fmasks; ++q) m |= f >= lo[q] && f < hi[q];
+    for (int q = fmasks; q < fmasks + tmasks; ++q) m |= t >= lo[q] && t < hi[q];
+    const int64_t idx = b * cells + c;
+    if (m) x[idx] = 0.f;
+    if (mask_out) mask_out[idx] = m ? 1 : 0;
+  }
 }
 
 // cols[(b,t2,f2), c*9 + ky*3 + kx] = X[b, 2*t2-1+ky, 2*f2-1+kx, c]  (0 outside / beyond len_in)
@@ -403,8 +419,10 @@ int kdfm_specaugment(float* x, const int64_t* seq_len, uint8_t* mask_out, int64_
   KDFM_REQUIRE(freq_masks >= 0 && freq_masks <= 16 && time_masks >= 0 && time_masks <= 16, "mask counts in [0,16]");
   const int64_t n = B * T * nfilt;
   if (n == 0) return KDFM_OK;
-  hipLaunchKernelGGL(specaug_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, as_stream(stream), x, seq_len,
-                     mask_out, B, T, nfilt, freq_masks, freq_width, time_masks, time_width, seed, rng_stream);
+  KDFM_REQUIRE(freq_masks + time_masks <= 32, "at most 32 masks");
+  hipLaunchKernelGGL(specaug_kernel, dim3((unsigned)ceil_div(T * nfilt, SA_EPB), (unsigned)B), dim3(256), 0,
+                     as_stream(stream), x, seq_len, mask_out, B, T, nfilt, freq_masks, freq_width, time_masks,
+                     time_width, seed, rng_stream);
   return check_launch("kdfm_specaugment");
 }
 

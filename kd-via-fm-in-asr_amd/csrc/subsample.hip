@@ -43,15 +43,21 @@ __global__ __launch_bounds__(256) void ss_conv1_kernel(const float* __restrict__
                                                        const float* __restrict__ b0, uint16_t* __restrict__ y1b,
                                                        float* __restrict__ y1f, int B, int Tm, int F, int C, int T1,
                                                        int F1) {
+  // weights and biases staged in LDS (C <= 256); 32-bit index math (B T1 F1 C/8 < 2^31, host-checked)
+  __shared__ float ws[256 * 9], bs[256];
+  for (int e = threadIdx.x; e < C * 9; e += 256) ws[e] = w0[e];
+  for (int e = threadIdx.x; e < C; e += 256) bs[e] = b0[e];
+  __syncthreads();
   const int CG = C >> 3;
-  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int64_t total = (int64_t)B * T1 * F1 * CG;
+  const uint32_t idx = blockIdx.x * 256u + threadIdx.x;
+  const uint32_t total = (uint32_t)B * T1 * F1 * CG;
   if (idx >= total) return;
   const int cg = (int)(idx % CG);
-  const int64_t pos = idx / CG;
-  const int f1 = (int)(pos % F1);
-  const int t1 = (int)((pos / F1) % T1);
-  const int b = (int)(pos / ((int64_t)F1 * T1));
+  const uint32_t pos32 = idx / CG;
+  const int64_t pos = pos32;
+  const int f1 = (int)(pos32 % F1);
+  const int t1 = (int)((pos32 / F1) % T1);
+  const int b = (int)(pos32 / ((uint32_t)F1 * T1));
   const int64_t ml = mel_len ? mel_len[b] : Tm;
   const bool rowok = !len1 || t1 < len1[b];
   float x[9];
@@ -66,9 +72,9 @@ __global__ __launch_bounds__(256) void ss_conv1_kernel(const float* __restrict__
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int c = cg * 8 + j;
-    float v = b0[c];
+    float v = bs[c];
 #pragma unroll
-    for (int q = 0; q < 9; ++q) v = fmaf(w0[c * 9 + q], x[q], v);
+    for (int q = 0; q < 9; ++q) v = fmaf(ws[c * 9 + q], x[q], v);
     v = fmaxf(v, 0.f);
     out[j] = rowok ? v : 0.f;
   }
@@ -449,7 +455,7 @@ int kdfm_subsample_conv1(const float* mel, const int64_t* mel_len, const int64_t
   KDFM_REQUIRE(C % 8 == 0 && B > 0 && Tm > 0 && F > 0, "C must be a multiple of 8");
   const int64_t T1 = (Tm - 1) / 2 + 1, F1 = (F - 1) / 2 + 1;
   const int64_t n = B * T1 * F1 * (C / 8);
-  KDFM_REQUIRE(n < (1ll << 40), "too large");
+  KDFM_REQUIRE(n < (1ll << 31) && C <= 256, "too large (32-bit indexing, C <= 256)");
   hipLaunchKernelGGL(ss_conv1_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, as_stream(stream), mel, mel_len,
                      len1, w0, b0, y1b, y1f, (int)B, (int)Tm, (int)F, (int)C, (int)T1, (int)F1);
   return check_launch("kdfm_subsample_conv1");
