@@ -180,6 +180,65 @@ int kdfm_relpos_attn_bwd(const float* dO, const float* O, const float* qu, const
                          float* ws, int64_t ws_len, int64_t B, int64_t H, int64_t T, int64_t d, float scale,
                          float dropout_p, const uint64_t* seed, uint64_t rng_stream, void* stream);
 
+/* Fused Conformer macaron feed-forward block (replaces the LayerNorm + Linear(d,ff)+SiLU+dropout +
+ * Linear(ff,d)+dropout+residual of ConformerLayer.forward's feed_forward1 / feed_forward2 half steps,
+ * NeMo conformer_modules.py, called conformer_encoder.py:685-692):
+ *   out = x + rscale * drop_out(W2 drop_act(silu(W1 LN(x) + b1)) + b2)      (rows, d) fp32
+ * bf16 MFMA, f32 state; the ff-wide hidden activation never reaches HBM.  Dropout masks use the
+ * GEMM-epilogue flat indices (act: row*ff + n on stream_act, out: row*d + n on stream_out).
+ * img: kdfm_ffn_img_elems(d, ff) bf16 prepared by kdfm_ffn_wprep from W1 (ff, d) / W2 (d, ff) fp32
+ * (fwd_only: only the forward half of every chunk image is written).  mean / rstd (rows) fp32, or
+ * both null (no backward).  Supported: d % 8 == 0 with d in (80, 96] or (160, 192], ff % 32 == 0
+ * (kdfm_ffn_supported); all row operands 16-byte aligned.
+ * Backward (dout = dL/dout): dx = dout + LN'(dln) with dln = W1^T dh, dh = (W2^T dl2) . drop_act' .
+ * silu'(h), dl2 = rscale drop_out(dout); the hidden h is recomputed from LN(x).  Writes the bf16
+ * weight-gradient operands ln_h (rows, d), a_h (rows, ff), dl2_h (rows, d), dh_h (rows, ff) for
+ * kdfm_wgrad_bf16 (dW2 = dl2^T a, dW1 = dh^T ln) and the LayerNorm dgamma|dbeta partials `part` in
+ * the kdfm_layernorm_bwd_part layout (kdfm_layernorm_bwd_ws(rows, d) floats) for kdfm_ln_fold. */
+int32_t kdfm_ffn_supported(int64_t d, int64_t ff);
+
+/* LayerNorm-fused input projections of the attention and convolution modules (ConformerLayer.forward,
+ * SURVEY.md Appendix A.6/A.7; NeMo RelPositionMultiHeadAttention linear_q/k/v + pos_bias_u/v, and
+ * ConformerConvolution pointwise_conv1 + GLU + pad mask; called conformer_encoder.py:685-692):
+ *   kind 0 (QKV): ln = LN(x); [q|k|v] = ln W^T + bias (W (3d, d)); qu = q + pos_u, qv = q + pos_v (rows, d);
+ *                 k, v into qkv[:, d:2d], qkv[:, 2d:3d] (rows, 3d; columns [0, d) are not written)
+ *   kind 1 (GLU): ln = LN(x); [a|gate] = ln W^T + bias (W (2d, d)); g = a sigmoid(gate), 0 on frames
+ *                 t >= lengths[b] (rows = B T, utterance-major)
+ * bf16 MFMA, f32 state.  mean / rstd (rows) and ln_h (rows, d bf16, the weight-gradient operand) are
+ * optional (null: not written).  img: kdfm_lnproj_img_elems(kind, d, bwd) bf16 from
+ * kdfm_lnproj_wprep(kind, W, ...) (bwd = 0: forward image, 1: backward image).
+ * Backward (d in (80, 96]): dx = dres + LN'(W^T dproj) with dproj = [dqu + dqv | dqkv[:, d:2d] |
+ * dqkv[:, 2d:]] (QKV) or GLU'(dg) from the recomputed projection (GLU); writes ln_h, the bf16 dproj
+ * (dqkv_h (rows, 3d) / da_h (rows, 2d): dW = dproj^T ln via kdfm_wgrad_bf16) and the LayerNorm
+ * dgamma|dbeta partials `part` (kdfm_layernorm_bwd_part layout, folded by kdfm_ln_fold). */
+int64_t kdfm_lnproj_img_elems(int32_t kind, int64_t d, int32_t bwd);
+int kdfm_lnproj_wprep(int32_t kind, const float* W, uint16_t* img, int64_t d, int32_t bwd, void* stream);
+int kdfm_ln_qkv_fwd(const float* x, const float* ln_g, const float* ln_b, float ln_eps, const uint16_t* img,
+                    const float* bias, const float* pos_u, const float* pos_v, float* qu, float* qv, float* qkv,
+                    float* mean, float* rstd, uint16_t* ln_h, int64_t rows, int64_t d, void* stream);
+int kdfm_ln_glu_fwd(const float* x, const float* ln_g, const float* ln_b, float ln_eps, const uint16_t* img,
+                    const float* bias, const int64_t* lengths, int64_t T, float* g, float* mean, float* rstd,
+                    uint16_t* ln_h, int64_t rows, int64_t d, void* stream);
+int kdfm_ln_qkv_bwd(const float* dqu, const float* dqv, const float* dqkv, const float* x, const float* mean,
+                    const float* rstd, const float* ln_g, const float* ln_b, const uint16_t* img, const float* dres,
+                    float* dx, uint16_t* ln_h, uint16_t* dqkv_h, float* part, int64_t rows, int64_t d, void* stream);
+int kdfm_ln_glu_bwd(const float* dg, const float* x, const float* mean, const float* rstd, const float* ln_g,
+                    const float* ln_b, const uint16_t* img, const float* bias, const int64_t* lengths, int64_t T,
+                    const float* dres, float* dx, uint16_t* ln_h, uint16_t* da_h, float* part, int64_t rows,
+                    int64_t d, void* stream);
+int64_t kdfm_ffn_img_elems(int64_t d, int64_t ff);
+int kdfm_ffn_wprep(const float* W1, const float* W2, uint16_t* img, int64_t d, int64_t ff, int32_t fwd_only,
+                   void* stream);
+int kdfm_ffn_fwd(const float* x, const float* ln_g, const float* ln_b, float ln_eps, const uint16_t* img,
+                 const float* b1, const float* b2, float* out, float* mean, float* rstd, int64_t rows, int64_t d,
+                 int64_t ff, float rscale, float p_act, float p_out, const uint64_t* seed, uint64_t stream_act,
+                 uint64_t stream_out, void* stream);
+int kdfm_ffn_bwd(const float* dout, const float* x, const float* mean, const float* rstd, const float* ln_g,
+                 const float* ln_b, const uint16_t* img, const float* b1, float* dx, uint16_t* ln_h, uint16_t* a_h,
+                 uint16_t* dl2_h, uint16_t* dh_h, float* part, int64_t rows, int64_t d, int64_t ff, float rscale,
+                 float p_act, float p_out, const uint64_t* seed, uint64_t stream_act, uint64_t stream_out,
+                 void* stream);
+
 int kdfm_fm_chain_fwd(const float* x0, const float* zt, const float* W1, int64_t ld_w1, const float* cvec,
                       const float* W2, const float* b2, const float* Wst, const float* bst, uint16_t* X, uint16_t* A,
                       float* nsx, float* dtr, float* xS, float* loss, float inv, int64_t n, int32_t L, int32_t S,

@@ -97,9 +97,28 @@ __device__ __forceinline__ float rng_normal(uint64_t seed, uint64_t stream, uint
   float u2 = (float)((b >> 16) & 0xFFFFFF) * (1.0f / 16777216.0f);
   return sqrtf(-2.f * __logf(u1)) * __cosf(6.283185307179586f * u2);
 }
-// dropout keep test: keep iff u >= p
+// Dropout decisions are the hottest RNG use (every FFN / attention / residual element of a training
+// step): a 32-bit keyed hash (two lowbias32 rounds, 4 v_mul_lo_u32) instead of the 64-bit splitmix
+// finaliser (12 32-bit multiplies per element).  Round 1 mixes the low index word with the low key
+// word, round 2 the high words, so different (seed, stream) keys give unrelated sequences.
+__host__ __device__ __forceinline__ uint32_t hash32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x21f0aaadu;
+  x ^= x >> 15;
+  x *= 0x735a2d97u;
+  x ^= x >> 15;
+  return x;
+}
+__host__ __device__ __forceinline__ uint32_t drop_bits_k(uint64_t key, uint64_t idx) {
+  const uint32_t h = hash32((uint32_t)idx ^ (uint32_t)key);
+  return hash32(h ^ (uint32_t)(idx >> 32) ^ (uint32_t)(key >> 32));
+}
+// dropout keep test on a precomputed key: keep iff u >= p, u = top 24 hash bits / 2^24 in [0,1)
+__device__ __forceinline__ bool dropout_keep_k(uint64_t key, uint64_t idx, float p) {
+  return (float)(drop_bits_k(key, idx) >> 8) * (1.0f / 16777216.0f) >= p;
+}
 __device__ __forceinline__ bool dropout_keep(uint64_t seed, uint64_t stream, uint64_t idx, float p) {
-  return rng_uniform(seed, stream, idx) >= p;
+  return dropout_keep_k(rng_key(seed, stream), idx, p);
 }
 __device__ __forceinline__ uint64_t load_seed(const uint64_t* seed_ptr) { return seed_ptr ? *seed_ptr : 0ull; }
 

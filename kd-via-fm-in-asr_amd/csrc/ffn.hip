@@ -1,0 +1,437 @@
+// Fused Conformer macaron FFN block (LayerNorm -> Linear(d,4d) -> SiLU -> dropout -> Linear(4d,d) ->
+// dropout -> scaled residual), forward and data-gradient backward, one launch each (bf16 MFMA, f32
+// state).
+//
+// Reference: ConformerLayer.forward, the two half-step feed-forward modules (SURVEY.md Appendix A.5,
+// NeMo conformer_modules.py ConformerFeedForward; built conformer_encoder.py:450-472, called :685-692):
+//   r_out = r_in + rscale * drop(W2 drop(silu(W1 LN(r_in) + b1)) + b2),   rscale = 0.5
+// The unfused path ran LN, the up-projection (writing the 4d-wide pre-activation AND activation in
+// f32) and the down-projection as three launches; here one wave keeps 32 rows of LN(r_in) as bf16
+// MFMA operands in registers and streams the 4d hidden width through in 32-feature chunks, so the
+// hidden activation never leaves the chip.  Training saves only the row statistics (mean, rstd); the
+// backward recomputes the hidden chunk from LN(r_in) (same operands, same MFMA order: bit-identical
+// to the forward's) and emits the bf16 weight-gradient operands ln, a, dl2, dh for kdfm_wgrad_bf16.
+//
+// Layout: every product is computed transposed, C^T (32 features x 32 rows) = W (32 x K) x X^T, with
+// v_mfma_f32_32x32x16_bf16.  A operand: a fragment of a prepared weight image (kdfm_ffn_wprep:
+// fragment-major, one 1 KB lane-contiguous block per (tile, k-step) -> conflict-free ds_read_b128),
+// staged chunk by chunk through LDS and shared by the 4 waves of a workgroup.  B operand: the wave's
+// rows, lane (r, h) holding 8 features k = 16 ks + 8 h .. +7 of row r.  The accumulator gives lane
+// (r, h) the features 8 q + 4 h + 0..3 of row r; one v_permlane32_swap per packed bf16 dword turns a
+// chunk's activation into the B operand of the next product (cdna_hip_programming.md T21).
+//
+// Work split: a workgroup owns 64 rows = 2 row tiles of 32; the two waves of a tile take the even and
+// the odd hidden chunks and their partial down-projections are added (in that fixed order) through
+// LDS at the end, so 12,832 rows give 804 waves instead of 402.
+#include "lnblock.h"
+
+namespace kdfm {
+namespace {
+
+using namespace lnb;
+
+constexpr int FF_NT = 256;        // 4 waves: 2 row tiles x 2 chunk parities
+constexpr int FF_ROWS = 64;       // rows per workgroup
+
+// Chunk image (one 32-feature slice of the hidden width), fragment order:
+//   W2c(mt, ks2) = 2 mt + ks2            A of the down-projection (d rows x 32 hidden)     [fwd]
+//   W1c(ks)      = 2 DT + ks             A of the up-projection (32 hidden x d)            [fwd, bwd]
+//   W2Tc(ks)     = 2 DT + KS1 + ks       A of dA^T = W2^T dl2^T (32 hidden x d)             [bwd]
+//   W1Tc(mt,ks2) = 2 DT + 2 KS1 + 2 mt + ks2   A of dln^T = W1^T dh^T (d rows x 32 hidden)  [bwd]
+// so the forward stages fragments [0, 2DT + KS1) and the backward [2DT, CS) of each chunk.
+template <int KS1, int DT>
+struct FfnGeo {
+  static constexpr int FWD = 2 * DT + KS1;
+  static constexpr int BWD = 2 * KS1 + 2 * DT;
+  static constexpr int CS = 4 * DT + 2 * KS1;
+};
+
+// ---- weight images ------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void ffn_wprep_kernel(const float* __restrict__ W1, const float* __restrict__ W2,
+                                                        uint16_t* __restrict__ img, int d, int ff, int KS1, int DT,
+                                                        int nfr, int64_t total) {
+  const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (g >= total) return;
+  const int lane = (int)(g & 63);
+  const int64_t rest = g >> 6;
+  const int f = (int)(rest % nfr);
+  const int64_t c = rest / nfr;
+  const int r = lane & 31, h = lane >> 5;
+  const int CS = 4 * DT + 2 * KS1;
+  float v[8];
+  if (f < 2 * DT) {                       // W2c(mt, ks2): W2[mt*32 + r][c*32 + ks2*16 + 8h + j]
+    const int row = (f >> 1) * 32 + r;
+    const int64_t col = c * 32 + (f & 1) * 16 + 8 * h;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = row < d ? W2[(int64_t)row * ff + col + j] : 0.f;
+  } else if (f < 2 * DT + KS1) {          // W1c(ks): W1[c*32 + r][ks*16 + 8h + j]
+    const int k0 = (f - 2 * DT) * 16 + 8 * h;
+    const int64_t row = c * 32 + r;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = k0 + j < d ? W1[row * d + k0 + j] : 0.f;
+  } else if (f < 2 * DT + 2 * KS1) {      // W2Tc(ks): W2[ks*16 + 8h + j][c*32 + r]
+    const int k0 = (f - 2 * DT - KS1) * 16 + 8 * h;
+    const int64_t col = c * 32 + r;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = k0 + j < d ? W2[(int64_t)(k0 + j) * ff + col] : 0.f;
+  } else {                                // W1Tc(mt, ks2): W1[c*32 + ks2*16 + 8h + j][mt*32 + r]
+    const int t = f - 2 * DT - 2 * KS1;
+    const int row = (t >> 1) * 32 + r;
+    const int64_t k0 = c * 32 + (t & 1) * 16 + 8 * h;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = row < d ? W1[(k0 + j) * d + row] : 0.f;
+  }
+  *reinterpret_cast<bf16x8*>(img + ((c * CS + f) * 64 + lane) * 8) = pack_bf16x8<bf16x8>(v);
+}
+
+struct FfnFwd {
+  const float* x; const float* g; const float* b; float eps;
+  const uint16_t* img; const float* b1; const float* b2;
+  float* out; float* mean; float* rstd;
+  int64_t rows; int d, ff;
+  float rscale, p_act, p_out;
+  const uint64_t* seed; uint64_t st_act, st_out;
+};
+
+template <int KS1, int DT>
+__global__ __launch_bounds__(FF_NT) void ffn_fwd_kernel(FfnFwd a) {
+  using G = FfnGeo<KS1, DT>;
+  extern __shared__ __attribute__((aligned(16))) uint4 ff_lds[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int h = lane >> 5, par = wave & 1, tile = wave >> 1;
+  const int64_t row = (int64_t)blockIdx.x * FF_ROWS + tile * 32 + (lane & 31);
+  const bool ok = row < a.rows;
+  const int d = a.d, ff = a.ff, FC = ff / 32;
+  const uint64_t seed = (a.p_act > 0.f || a.p_out > 0.f) ? load_seed(a.seed) : 0ull;
+  const uint64_t kact = rng_key(seed, a.st_act), kout = rng_key(seed, a.st_out);
+  const float ks_act = 1.f / (1.f - a.p_act), ks_out = 1.f / (1.f - a.p_out);
+
+  Stager<G::FWD, 0, G::CS, 2, FF_NT> stg;
+  const uint4* img = reinterpret_cast<const uint4*>(a.img);
+  stg.load(img, 0, FC);
+
+  float mean = 0.f, rstd = 0.f;
+  bf16x8 bx[KS1];
+  ln_operands<KS1>(a.x, a.g, a.b, row, ok, d, h, a.eps, false, mean, rstd, bx, nullptr);
+  if (a.mean && par == 0 && h == 0 && ok) {
+    a.mean[row] = mean;
+    a.rstd[row] = rstd;
+  }
+  f32x16 acc[DT];
+#pragma unroll
+  for (int mt = 0; mt < DT; ++mt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[mt][i] = 0.f;
+
+  stg.store(ff_lds, 0);
+  __syncthreads();
+  const int nit = (FC + 1) / 2;
+  for (int it = 0; it < nit; ++it) {
+    if (it + 1 < nit) stg.load(img, it + 1, FC);
+    const int c = 2 * it + par;
+    if (c < FC) {
+      const uint4* W = ff_lds + ((it & 1) * 2 + par) * G::FWD * FRAG_U4;
+      f32x16 hacc;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) hacc[i] = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < KS1; ++ks)
+        hacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(W[(2 * DT + ks) * FRAG_U4 + lane]), bx[ks], hacc, 0, 0, 0);
+      uint32_t pk[4][2];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int n0 = c * 32 + 8 * q + 4 * h;
+        const float4 bb = *reinterpret_cast<const float4*>(a.b1 + n0);
+        const float bv[4] = {bb.x, bb.y, bb.z, bb.w};
+        float v[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float t = siluf_(hacc[4 * q + i] + bv[i]);
+          if (a.p_act > 0.f) t = dropout_keep_k(kact, (uint64_t)row * ff + n0 + i, a.p_act) ? t * ks_act : 0.f;
+          v[i] = t;
+        }
+        pk[q][0] = pack_bf16x2(v[0], v[1]);
+        pk[q][1] = pack_bf16x2(v[2], v[3]);
+      }
+      bf16x8 ba[2];
+      tile_operands(pk, ba);
+#pragma unroll
+      for (int mt = 0; mt < DT; ++mt)
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+          acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(W[(2 * mt + s) * FRAG_U4 + lane]), ba[s], acc[mt], 0, 0, 0);
+    }
+    if (it + 1 < nit) stg.store(ff_lds, (it + 1) & 1);
+    __syncthreads();
+  }
+  // odd-chunk partial -> even wave (fixed order: even + odd)
+  float* red = reinterpret_cast<float*>(ff_lds) + tile * (DT * 16 * 64);
+  if (par == 1) {
+#pragma unroll
+    for (int mt = 0; mt < DT; ++mt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) red[(mt * 16 + i) * 64 + lane] = acc[mt][i];
+  }
+  __syncthreads();
+  if (par == 1 || !ok) return;
+#pragma unroll
+  for (int mt = 0; mt < DT; ++mt)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int n0 = mt * 32 + 8 * q + 4 * h;
+      if (n0 >= d) continue;
+      const float4 bb = *reinterpret_cast<const float4*>(a.b2 + n0);
+      const float4 xr = *reinterpret_cast<const float4*>(a.x + row * d + n0);
+      const float bv[4] = {bb.x, bb.y, bb.z, bb.w}, xv[4] = {xr.x, xr.y, xr.z, xr.w};
+      float o[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float v = acc[mt][4 * q + i] + red[(mt * 16 + 4 * q + i) * 64 + lane] + bv[i];
+        if (a.p_out > 0.f) v = dropout_keep_k(kout, (uint64_t)row * d + n0 + i, a.p_out) ? v * ks_out : 0.f;
+        o[i] = xv[i] + a.rscale * v;
+      }
+      *reinterpret_cast<float4*>(a.out + row * d + n0) = make_float4(o[0], o[1], o[2], o[3]);
+    }
+}
+
+struct FfnBwd {
+  const float* dout; const float* x; const float* mean; const float* rstd; const float* g; const float* b;
+  const uint16_t* img; const float* b1;
+  float* dx; uint16_t* ln_h; uint16_t* a_h; uint16_t* dl2_h; uint16_t* dh_h; float* part;
+  int64_t rows, nparts; int d, ff;
+  float rscale, p_act, p_out;
+  const uint64_t* seed; uint64_t st_act, st_out;
+};
+
+template <int KS1, int DT>
+__global__ __launch_bounds__(FF_NT) void ffn_bwd_kernel(FfnBwd a) {
+  using G = FfnGeo<KS1, DT>;
+  extern __shared__ __attribute__((aligned(16))) uint4 ff_lds[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int h = lane >> 5, par = wave & 1, tile = wave >> 1;
+  const int64_t row = (int64_t)blockIdx.x * FF_ROWS + tile * 32 + (lane & 31);
+  const bool ok = row < a.rows;
+  const int d = a.d, ff = a.ff, FC = ff / 32;
+  const uint64_t seed = (a.p_act > 0.f || a.p_out > 0.f) ? load_seed(a.seed) : 0ull;
+  const uint64_t kact = rng_key(seed, a.st_act), kout = rng_key(seed, a.st_out);
+  const float ks_act = 1.f / (1.f - a.p_act), ks_out = 1.f / (1.f - a.p_out);
+
+  Stager<G::BWD, 2 * DT, G::CS, 2, FF_NT> stg;
+  const uint4* img = reinterpret_cast<const uint4*>(a.img);
+  stg.load(img, 0, FC);
+
+  // dl2 = rscale * drop_out(dout): B operands of dA^T; the even wave writes the bf16 copy (dW2 operand)
+  bf16x8 bd[KS1];
+#pragma unroll
+  for (int ks = 0; ks < KS1; ++ks) {
+    const int k0 = ks * 16 + 8 * h;
+    const bool in = ok && k0 < d;
+    const float4* p = reinterpret_cast<const float4*>(a.dout + (in ? row * d + k0 : 0));
+    const float4 u = p[0], w = p[1];
+    float v[8] = {u.x, u.y, u.z, u.w, w.x, w.y, w.z, w.w};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float t = in ? v[j] * a.rscale : 0.f;
+      if (a.p_out > 0.f) t = dropout_keep_k(kout, (uint64_t)row * d + k0 + j, a.p_out) ? t * ks_out : 0.f;
+      v[j] = t;
+    }
+    bd[ks] = pack_bf16x8<bf16x8>(v);
+    if (par == 0 && in) *reinterpret_cast<bf16x8*>(a.dl2_h + row * d + k0) = bd[ks];
+  }
+  float mean = ok ? a.mean[row] : 0.f, rstd = ok ? a.rstd[row] : 0.f;
+  bf16x8 bx[KS1];
+  ln_operands<KS1>(a.x, a.g, a.b, row, ok, d, h, 0.f, true, mean, rstd, bx, par == 0 ? a.ln_h : nullptr);
+
+  f32x16 acc[DT];
+#pragma unroll
+  for (int mt = 0; mt < DT; ++mt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[mt][i] = 0.f;
+
+  stg.store(ff_lds, 0);
+  __syncthreads();
+  const int nit = (FC + 1) / 2;
+  for (int it = 0; it < nit; ++it) {
+    if (it + 1 < nit) stg.load(img, it + 1, FC);
+    const int c = 2 * it + par;
+    if (c < FC) {
+      const uint4* W = ff_lds + ((it & 1) * 2 + par) * G::BWD * FRAG_U4;   // W1c | W2Tc | W1Tc
+      f32x16 hacc, gacc;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) hacc[i] = gacc[i] = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < KS1; ++ks) {
+        hacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(W[ks * FRAG_U4 + lane]), bx[ks], hacc, 0, 0, 0);
+        gacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(W[(KS1 + ks) * FRAG_U4 + lane]), bd[ks], gacc, 0, 0, 0);
+      }
+      uint32_t pa[4][2], pd[4][2];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int n0 = c * 32 + 8 * q + 4 * h;
+        const float4 bb = *reinterpret_cast<const float4*>(a.b1 + n0);
+        const float bv[4] = {bb.x, bb.y, bb.z, bb.w};
+        float av[4], dv[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float hv = hacc[4 * q + i] + bv[i];
+          const float sg = sigmoidf_(hv);
+          float s = hv * sg, gv = gacc[4 * q + i];
+          if (a.p_act > 0.f) {
+            const bool kp = dropout_keep_k(kact, (uint64_t)row * ff + n0 + i, a.p_act);
+            s = kp ? s * ks_act : 0.f;
+            gv = kp ? gv * ks_act : 0.f;
+          }
+          av[i] = s;
+          dv[i] = gv * (sg * (1.f + hv * (1.f - sg)));
+        }
+        pa[q][0] = pack_bf16x2(av[0], av[1]);
+        pa[q][1] = pack_bf16x2(av[2], av[3]);
+        pd[q][0] = pack_bf16x2(dv[0], dv[1]);
+        pd[q][1] = pack_bf16x2(dv[2], dv[3]);
+      }
+      bf16x8 ba[2], bdh[2];
+      tile_operands(pa, ba);
+      tile_operands(pd, bdh);
+      if (ok) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const int64_t off = row * ff + c * 32 + s * 16 + 8 * h;
+          *reinterpret_cast<bf16x8*>(a.a_h + off) = ba[s];
+          *reinterpret_cast<bf16x8*>(a.dh_h + off) = bdh[s];
+        }
+      }
+#pragma unroll
+      for (int mt = 0; mt < DT; ++mt)
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+          acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(W[(2 * KS1 + 2 * mt + s) * FRAG_U4 + lane]), bdh[s],
+                                                            acc[mt], 0, 0, 0);
+    }
+    if (it + 1 < nit) stg.store(ff_lds, (it + 1) & 1);
+    __syncthreads();
+  }
+  float* red = reinterpret_cast<float*>(ff_lds) + tile * (DT * 16 * 64);
+  if (par == 1) {
+#pragma unroll
+    for (int mt = 0; mt < DT; ++mt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) red[(mt * 16 + i) * 64 + lane] = acc[mt][i];
+  }
+  __syncthreads();
+  if (par == 1) return;
+  float dl[DT * 16];
+#pragma unroll
+  for (int mt = 0; mt < DT; ++mt)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) dl[mt * 16 + e] = acc[mt][e] + red[(mt * 16 + e) * 64 + lane];
+  ln_backward_rows<DT>(dl, a.x, a.g, a.dout, a.dx, a.part, a.nparts, (int64_t)blockIdx.x * FF_ROWS + tile * 32, row, ok,
+                       d, mean, rstd, lane);
+}
+
+int ffn_dims(int64_t d, int& KS1, int& DT) { return ln_dims(d, KS1, DT); }
+
+template <typename K>
+void ffn_allow_lds(K kern) {
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+}
+
+template <int KS1, int DT>
+int launch_fwd(const FfnFwd& a, hipStream_t st) {
+  using G = FfnGeo<KS1, DT>;
+  static bool once = (ffn_allow_lds(ffn_fwd_kernel<KS1, DT>), true);
+  (void)once;
+  const size_t lds = (size_t)4 * G::FWD * 1024 > (size_t)2 * DT * 16 * 64 * 4 ? (size_t)4 * G::FWD * 1024
+                                                                                : (size_t)2 * DT * 16 * 64 * 4;
+  hipLaunchKernelGGL((ffn_fwd_kernel<KS1, DT>), dim3((unsigned)ceil_div(a.rows, FF_ROWS)), dim3(FF_NT), lds, st, a);
+  return check_launch("kdfm_ffn_fwd");
+}
+
+template <int KS1, int DT>
+int launch_bwd(const FfnBwd& a, hipStream_t st) {
+  using G = FfnGeo<KS1, DT>;
+  static bool once = (ffn_allow_lds(ffn_bwd_kernel<KS1, DT>), true);
+  (void)once;
+  const size_t lds = (size_t)4 * G::BWD * 1024 > (size_t)2 * DT * 16 * 64 * 4 ? (size_t)4 * G::BWD * 1024
+                                                                                : (size_t)2 * DT * 16 * 64 * 4;
+  hipLaunchKernelGGL((ffn_bwd_kernel<KS1, DT>), dim3((unsigned)ceil_div(a.rows, FF_ROWS)), dim3(FF_NT), lds, st, a);
+  return check_launch("kdfm_ffn_bwd");
+}
+
+}  // namespace
+}  // namespace kdfm
+
+extern "C" {
+
+int32_t kdfm_ffn_supported(int64_t d, int64_t ff) {
+  int KS1, DT;
+  return kdfm::ffn_dims(d, KS1, DT) == 0 && ff > 0 && ff % 32 == 0 ? 1 : 0;
+}
+
+int64_t kdfm_ffn_img_elems(int64_t d, int64_t ff) {
+  int KS1, DT;
+  if (kdfm::ffn_dims(d, KS1, DT) != 0 || ff <= 0 || ff % 32 != 0) return 0;
+  return (ff / 32) * (int64_t)(4 * DT + 2 * KS1) * 512;
+}
+
+int kdfm_ffn_wprep(const float* W1, const float* W2, uint16_t* img, int64_t d, int64_t ff, int32_t fwd_only,
+                   void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(W1 && W2 && img, "null pointer");
+  int KS1, DT;
+  KDFM_REQUIRE(ffn_dims(d, KS1, DT) == 0 && ff > 0 && ff % 32 == 0, "unsupported FFN shape (d, ff)");
+  KDFM_REQUIRE(al16(img), "img must be 16-byte aligned");
+  const int CS = 4 * DT + 2 * KS1;
+  const int nfr = fwd_only ? 2 * DT + KS1 : CS;
+  const int64_t total = (ff / 32) * (int64_t)nfr * 64;
+  hipLaunchKernelGGL(ffn_wprep_kernel, dim3((unsigned)ceil_div(total, 256)), dim3(256), 0, as_stream(stream), W1, W2,
+                     img, (int)d, (int)ff, KS1, DT, nfr, total);
+  return check_launch("kdfm_ffn_wprep");
+}
+
+int kdfm_ffn_fwd(const float* x, const float* ln_g, const float* ln_b, float ln_eps, const uint16_t* img,
+                 const float* b1, const float* b2, float* out, float* mean, float* rstd, int64_t rows, int64_t d,
+                 int64_t ff, float rscale, float p_act, float p_out, const uint64_t* seed, uint64_t stream_act,
+                 uint64_t stream_out, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(x && ln_g && ln_b && img && b1 && b2 && out, "null pointer");
+  KDFM_REQUIRE((mean == nullptr) == (rstd == nullptr), "mean and rstd go together");
+  int KS1, DT;
+  KDFM_REQUIRE(ffn_dims(d, KS1, DT) == 0 && ff > 0 && ff % 32 == 0, "unsupported FFN shape (d, ff)");
+  KDFM_REQUIRE(al16(x) && al16(out) && al16(ln_g) && al16(ln_b) && al16(b1) && al16(b2) && al16(img),
+               "operands must be 16-byte aligned");
+  KDFM_REQUIRE(p_act >= 0.f && p_act < 1.f && p_out >= 0.f && p_out < 1.f, "dropout p");
+  KDFM_REQUIRE((p_act == 0.f && p_out == 0.f) || seed, "dropout needs a seed");
+  if (rows <= 0) return KDFM_OK;
+  FfnFwd a{x, ln_g, ln_b, ln_eps, img, b1, b2, out, mean, rstd, rows, (int)d, (int)ff, rscale, p_act, p_out,
+           seed, stream_act, stream_out};
+  hipStream_t st = as_stream(stream);
+  if (KS1 == 6) return launch_fwd<6, 3>(a, st);
+  if (KS1 == 11) return launch_fwd<11, 6>(a, st);
+  return launch_fwd<12, 6>(a, st);
+}
+
+int kdfm_ffn_bwd(const float* dout, const float* x, const float* mean, const float* rstd, const float* ln_g,
+                 const float* ln_b, const uint16_t* img, const float* b1, float* dx, uint16_t* ln_h, uint16_t* a_h,
+                 uint16_t* dl2_h, uint16_t* dh_h, float* part, int64_t rows, int64_t d, int64_t ff, float rscale,
+                 float p_act, float p_out, const uint64_t* seed, uint64_t stream_act, uint64_t stream_out,
+                 void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(dout && x && mean && rstd && ln_g && ln_b && img && b1 && dx && ln_h && a_h && dl2_h && dh_h && part,
+               "null pointer");
+  int KS1, DT;
+  KDFM_REQUIRE(ffn_dims(d, KS1, DT) == 0 && ff > 0 && ff % 32 == 0, "unsupported FFN shape (d, ff)");
+  KDFM_REQUIRE(al16(dout) && al16(x) && al16(dx) && al16(ln_g) && al16(ln_b) && al16(b1) && al16(img) &&
+                   al16(ln_h) && al16(a_h) && al16(dl2_h) && al16(dh_h),
+               "operands must be 16-byte aligned");
+  KDFM_REQUIRE(p_act >= 0.f && p_act < 1.f && p_out >= 0.f && p_out < 1.f, "dropout p");
+  KDFM_REQUIRE((p_act == 0.f && p_out == 0.f) || seed, "dropout needs a seed");
+  if (rows <= 0) return KDFM_OK;
+  FfnBwd a{dout, x, mean, rstd, ln_g, ln_b, img, b1, dx, ln_h, a_h, dl2_h, dh_h, part, rows, ceil_div(rows, 16),
+           (int)d, (int)ff, rscale, p_act, p_out, seed, stream_act, stream_out};
+  hipStream_t st = as_stream(stream);
+  if (KS1 == 6) return launch_bwd<6, 3>(a, st);
+  if (KS1 == 11) return launch_bwd<11, 6>(a, st);
+  return launch_bwd<12, 6>(a, st);
+}
+
+}  // extern "C"

@@ -1,0 +1,255 @@
+// Building blocks of the LayerNorm-fused Conformer sub-block kernels (ffn.hip: macaron FFN;
+// lnproj.hip: attention q|k|v projection and conv-module pointwise conv + GLU).
+//
+// All of them compute transposed products C^T (32 features x 32 rows) = W (32 x K) x X^T with
+// v_mfma_f32_32x32x16_bf16: the A operand is a fragment of a prepared, fragment-major weight image
+// (one lane-contiguous 1 KB block per (32-row tile, 16-wide k-step): conflict-free ds_read_b128),
+// staged through LDS and shared by the waves of a workgroup; the B operand is the wave's rows, lane
+// (r, h) holding the 8 features 16 ks + 8 h .. +7 of row r.  The accumulator gives lane (r, h) the
+// features 8 q + 4 h + 0..3 of row r; one v_permlane32_swap per packed bf16 dword turns such a tile
+// into the B operand of a following product (cdna_hip_programming.md T21).
+#pragma once
+#include "gemm_common.h"
+
+namespace kdfm {
+namespace lnb {
+
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+
+constexpr int FRAG_U4 = 64;       // uint4 (8 bf16) units per fragment: one per lane
+
+__device__ __forceinline__ bf16x8 as_bf(const uint4& u) { return __builtin_bit_cast(bf16x8, u); }
+
+__device__ __forceinline__ f32x16 zero16() {
+  f32x16 z;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) z[i] = 0.f;
+  return z;
+}
+
+__device__ __forceinline__ f32x16 mfma32(const uint4& a, const bf16x8& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(a), b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ void swap_halves(uint32_t& a, uint32_t& b) {
+  // lanes 32-63 of a <-> lanes 0-31 of b
+  const auto r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
+  a = r[0];
+  b = r[1];
+}
+
+// pk[q] = packed bf16 of the accumulator features 8 q + 4 h + 0..3 -> B operands of the two 16-wide
+// k-steps of the tile (lanes 0-31: k 0..7, lanes 32-63: k 8..15)
+__device__ __forceinline__ void tile_operands(uint32_t (&pk)[4][2], bf16x8 (&b)[2]) {
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    swap_halves(pk[2 * s][0], pk[2 * s + 1][0]);
+    swap_halves(pk[2 * s][1], pk[2 * s + 1][1]);
+    b[s] = __builtin_bit_cast(bf16x8, u32x4v{pk[2 * s][0], pk[2 * s][1], pk[2 * s + 1][0], pk[2 * s + 1][1]});
+  }
+}
+
+__device__ __forceinline__ void pack4(uint32_t (&pk)[2], const float (&v)[4]) {
+  pk[0] = pack_bf16x2(v[0], v[1]);
+  pk[1] = pack_bf16x2(v[2], v[3]);
+}
+
+// Double-buffered staging of weight-image blocks into LDS.  Iteration `it` stages SLOTS blocks of SF
+// fragments: block (SLOTS it + slot) starts at fragment ((SLOTS it + slot) * STRIDE + OFF) of the
+// image (blocks >= nblk are zero-filled).  All of a stage's global loads are issued before its LDS
+// stores (registers carry the next stage while the current one computes).
+template <int SF, int OFF, int STRIDE, int SLOTS, int NT>
+struct Stager {
+  static constexpr int UNITS = SLOTS * SF * FRAG_U4;
+  static constexpr int PER = (UNITS + NT - 1) / NT;
+  uint4 pre[PER];
+  __device__ __forceinline__ void load(const uint4* __restrict__ img, int it, int nblk) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int u = threadIdx.x + NT * i;
+      const int slot = u / (SF * FRAG_U4), w = u - slot * SF * FRAG_U4;
+      const int c = SLOTS * it + slot;
+      pre[i] = (u < UNITS && c < nblk) ? img[((int64_t)c * STRIDE + OFF) * FRAG_U4 + w] : make_uint4(0, 0, 0, 0);
+    }
+  }
+  __device__ __forceinline__ void store(uint4* lds, int buf) const {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int u = threadIdx.x + NT * i;
+      if (u < UNITS) lds[buf * UNITS + u] = pre[i];
+    }
+  }
+  // this slot's block of the stage in buffer `buf`
+  __device__ __forceinline__ static const uint4* block(const uint4* lds, int buf, int slot) {
+    return lds + buf * UNITS + slot * SF * FRAG_U4;
+  }
+};
+
+// Row r = `row` of x (d features, 16-B aligned rows) normalised into the B operands bx[ks]
+// (features 16 ks + 8 h .. +7; zero beyond d).  have_stats: mean / rstd given (backward recompute);
+// else computed (two-pass, biased variance, as kdfm_layernorm_fwd).  ln_out: bf16 copy of the row.
+template <int KS1>
+__device__ __forceinline__ void ln_operands(const float* __restrict__ x, const float* __restrict__ g,
+                                            const float* __restrict__ b, int64_t row, bool ok, int d, int h,
+                                            float eps, bool have_stats, float& mean, float& rstd,
+                                            bf16x8 (&bx)[KS1], uint16_t* ln_out) {
+  float xv[KS1][8];
+#pragma unroll
+  for (int ks = 0; ks < KS1; ++ks) {
+    const int k0 = ks * 16 + 8 * h;
+    const bool in = ok && k0 < d;
+    const float4* p = reinterpret_cast<const float4*>(x + (in ? row * d + k0 : 0));
+    const float4 u = p[0], w = p[1];
+    xv[ks][0] = in ? u.x : 0.f; xv[ks][1] = in ? u.y : 0.f; xv[ks][2] = in ? u.z : 0.f; xv[ks][3] = in ? u.w : 0.f;
+    xv[ks][4] = in ? w.x : 0.f; xv[ks][5] = in ? w.y : 0.f; xv[ks][6] = in ? w.z : 0.f; xv[ks][7] = in ? w.w : 0.f;
+  }
+  if (!have_stats) {
+    float s = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < KS1; ++ks)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += xv[ks][j];
+    s += __shfl_xor(s, 32, 64);
+    mean = s / d;
+    float q = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < KS1; ++ks) {
+      const bool in = ks * 16 + 8 * h < d;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float t = in ? xv[ks][j] - mean : 0.f;
+        q += t * t;
+      }
+    }
+    q += __shfl_xor(q, 32, 64);
+    rstd = rsqrtf(q / d + eps);
+  }
+#pragma unroll
+  for (int ks = 0; ks < KS1; ++ks) {
+    const int k0 = ks * 16 + 8 * h;
+    const bool in = k0 < d;
+    float y[8];
+    if (in) {
+      const float4 g0 = *reinterpret_cast<const float4*>(g + k0), g1 = *reinterpret_cast<const float4*>(g + k0 + 4);
+      const float4 b0 = *reinterpret_cast<const float4*>(b + k0), b1 = *reinterpret_cast<const float4*>(b + k0 + 4);
+      const float gg[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+      const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) y[j] = (xv[ks][j] - mean) * rstd * gg[j] + bb[j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) y[j] = 0.f;
+    }
+    bx[ks] = pack_bf16x8<bf16x8>(y);
+    if (ln_out && ok && in) *reinterpret_cast<bf16x8*>(ln_out + row * d + k0) = bx[ks];
+  }
+}
+
+// in-register reduce-scatter of N values over the 16 lanes of a DPP row (lane bits 8,4,2,1): afterwards
+// lane (b8 b4 b2 b1) holds the 16-lane sums of the original entries b8 N/2 + b4 N/4 + b2 N/8 + b1 N/16 + j
+template <int N, int M>
+__device__ __forceinline__ void rs_step(const float (&in)[N], float (&out)[N / 2], int lane) {
+  const bool up = (lane & M) != 0;
+#pragma unroll
+  for (int j = 0; j < N / 2; ++j) {
+    const float send = up ? in[j] : in[j + N / 2];
+    const float keep = up ? in[j + N / 2] : in[j];
+    out[j] = keep + __shfl_xor(send, M, 64);
+  }
+}
+
+// LayerNorm backward of the lane's row from dln in the accumulator layout (dl[mt*16 + 4q + i] =
+// feature mt*32 + 8q + 4h + i): dx = rstd (g dln - mean(g dln) - xhat mean(g dln xhat)) + dres, and
+// the dgamma (sum dln xhat) / dbeta (sum dln) partials of the lane's 16-row group written to
+// part[grp][2d] (the kdfm_layernorm_bwd_part layout, folded by kdfm_ln_fold).  Every lane of the
+// wave must call it (cross-lane reductions); row_base = first row of the wave's 32-row tile.
+template <int DT>
+__device__ __forceinline__ void ln_backward_rows(const float (&dl)[DT * 16], const float* __restrict__ x,
+                                                 const float* __restrict__ g, const float* __restrict__ dres,
+                                                 float* __restrict__ dx, float* __restrict__ part, int64_t nparts,
+                                                 int64_t row_base, int64_t row, bool ok, int d, float mean,
+                                                 float rstd, int lane) {
+  constexpr int NV = DT * 16;
+  const int h = lane >> 5;
+  float xh[NV];
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int mt = 0; mt < DT; ++mt)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int n0 = mt * 32 + 8 * q + 4 * h;
+      const bool in = ok && n0 < d;
+      const float4 xr = *reinterpret_cast<const float4*>(x + (in ? row * d + n0 : 0));
+      const float4 gg = *reinterpret_cast<const float4*>(g + (n0 < d ? n0 : 0));
+      const float xv[4] = {xr.x, xr.y, xr.z, xr.w}, gv[4] = {gg.x, gg.y, gg.z, gg.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int e = mt * 16 + 4 * q + i;
+        const float xhat = in ? (xv[i] - mean) * rstd : 0.f;
+        xh[e] = xhat;
+        const float gyv = in ? dl[e] * gv[i] : 0.f;
+        s1 += gyv;
+        s2 += gyv * xhat;
+      }
+    }
+  s1 += __shfl_xor(s1, 32, 64);
+  s2 += __shfl_xor(s2, 32, 64);
+  s1 /= d;
+  s2 /= d;
+  if (ok) {
+#pragma unroll
+    for (int mt = 0; mt < DT; ++mt)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int n0 = mt * 32 + 8 * q + 4 * h;
+        if (n0 >= d) continue;
+        const float4 dr = *reinterpret_cast<const float4*>(dres + row * d + n0);
+        const float4 gg = *reinterpret_cast<const float4*>(g + n0);
+        const float rv[4] = {dr.x, dr.y, dr.z, dr.w}, gv[4] = {gg.x, gg.y, gg.z, gg.w};
+        float o[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int e = mt * 16 + 4 * q + i;
+          o[i] = rstd * (dl[e] * gv[i] - s1 - xh[e] * s2) + rv[i];
+        }
+        *reinterpret_cast<float4*>(dx + row * d + n0) = make_float4(o[0], o[1], o[2], o[3]);
+      }
+  }
+  const int64_t grp = row_base / 16 + ((lane >> 4) & 1);
+  const int base = ((lane & 8) ? NV / 2 : 0) + ((lane & 4) ? NV / 4 : 0) + ((lane & 2) ? NV / 8 : 0) +
+                   ((lane & 1) ? NV / 16 : 0);
+  float* pr = part + grp * 2 * d;
+#pragma unroll
+  for (int qty = 0; qty < 2; ++qty) {
+    float v0[NV], r1[NV / 2], r2[NV / 4], r3[NV / 8], r4[NV / 16];
+#pragma unroll
+    for (int e = 0; e < NV; ++e) v0[e] = ok ? (qty == 0 ? dl[e] * xh[e] : dl[e]) : 0.f;
+    rs_step<NV, 8>(v0, r1, lane);
+    rs_step<NV / 2, 4>(r1, r2, lane);
+    rs_step<NV / 4, 2>(r2, r3, lane);
+    rs_step<NV / 8, 1>(r3, r4, lane);
+    if (grp < nparts) {
+#pragma unroll
+      for (int j = 0; j < NV / 16; ++j) {
+        const int e = base + j;
+        const int n = (e / 16) * 32 + 8 * ((e % 16) / 4) + 4 * h + (e % 4);
+        if (n < d) pr[qty * d + n] = r4[j];
+      }
+    }
+  }
+}
+
+// d -> (KS1 = 16-wide k-steps over d, DT = 32-wide feature tiles over d) of the compiled variants
+inline int ln_dims(int64_t d, int& KS1, int& DT) {
+  if (d % 8 != 0) return -1;
+  if (d > 80 && d <= 96) { KS1 = 6; DT = 3; return 0; }
+  if (d > 160 && d <= 176) { KS1 = 11; DT = 6; return 0; }
+  if (d > 176 && d <= 192) { KS1 = 12; DT = 6; return 0; }
+  return -1;
+}
+
+inline bool al16(const void* p) { return (((uintptr_t)p) & 15) == 0; }
+
+}  // namespace lnb
+}  // namespace kdfm

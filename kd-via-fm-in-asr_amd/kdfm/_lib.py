@@ -79,6 +79,19 @@ SIGNATURES: dict[str, tuple] = {
                                     C.c_uint64, P]),
     "kdfm_wgrad_bf16": (_i32, [P, P, P, _i64, P, _i64, _i64, _i64, _f32, P, _i64, P]),
     "kdfm_fm_chain_fwd": (_i32, [P, P, P, _i64, P, P, P, P, P, P, P, P, P, P, P, _f32, _i64, _i32, _i32, P]),
+    "kdfm_lnproj_img_elems": (_i64, [_i32, _i64, _i32]),
+    "kdfm_lnproj_wprep": (_i32, [_i32, P, P, _i64, _i32, P]),
+    "kdfm_ln_qkv_fwd": (_i32, [P, P, P, _f32, P, P, P, P, P, P, P, P, P, P, _i64, _i64, P]),
+    "kdfm_ln_glu_fwd": (_i32, [P, P, P, _f32, P, P, P, _i64, P, P, P, P, _i64, _i64, P]),
+    "kdfm_ln_qkv_bwd": (_i32, [P, P, P, P, P, P, P, P, P, P, P, P, P, P, _i64, _i64, P]),
+    "kdfm_ln_glu_bwd": (_i32, [P, P, P, P, P, P, P, P, P, _i64, P, P, P, P, P, _i64, _i64, P]),
+    "kdfm_ffn_supported": (_i32, [_i64, _i64]),
+    "kdfm_ffn_img_elems": (_i64, [_i64, _i64]),
+    "kdfm_ffn_wprep": (_i32, [P, P, P, _i64, _i64, _i32, P]),
+    "kdfm_ffn_fwd": (_i32, [P, P, P, _f32, P, P, P, P, P, P, _i64, _i64, _i64, _f32, _f32, _f32, P, C.c_uint64,
+                            C.c_uint64, P]),
+    "kdfm_ffn_bwd": (_i32, [P, P, P, P, P, P, P, P, P, P, P, P, P, P, _i64, _i64, _i64, _f32, _f32, _f32, P,
+                            C.c_uint64, C.c_uint64, P]),
     "kdfm_fm_chain_bwd": (_i32, [P, P, P, P, _i64, P, P, P, P, P, _i64, _i32, _i32, P]),
     "kdfm_wgrad_bf16_conv_ws": (_i64, [_i64, _i64, _i64, _i32, _i32, _i64, _i32]),
     "kdfm_wgrad_bf16_conv": (_i32, [P, P, P, _i64, P, _i64, _i64, _i64, _i32, _i32, _i64, _f32, P, _i64, P]),

@@ -284,6 +284,53 @@ def _ln(x, P, name, eps, dev, save_stats=True):
     return y, m, r
 
 
+# bf16 math: the fused macaron FFN block (csrc/ffn.hip) where the shape is supported (KDFM_FFN_FUSED=0: the
+# LayerNorm + two-GEMM path; the f32 parity mode always takes it)
+_FFN_FUSED = __import__("os").environ.get("KDFM_FFN_FUSED", "1") == "1"
+
+
+def _lnproj_fused(kind, rows, d, save):
+    """bf16 math: LN-fused q|k|v / pointwise-conv1+GLU kernels where compiled (KDFM_LNPROJ_FUSED=0: the
+    LN + GEMM + prep path; training also needs the fused backward and the bf16 weight-gradient shape)."""
+    if not (_LNPROJ_FUSED and K.get_math() == "bf16" and K.lnproj_supported(kind, d)):
+        return False
+    if not save:
+        return True
+    n = (3 if kind == K.LNPROJ_QKV else 2) * d
+    return K.lnproj_supported(kind, d, bwd=True) and K.wgrad_bf16_supported(rows, n, d)
+
+
+_LNPROJ_FUSED = __import__("os").environ.get("KDFM_LNPROJ_FUSED", "1") == "1"
+
+
+def _ffn_forward(cfg, P, L, which, norm, x, pd, seed, salt, li, site_act, site_out, save, keep, tag):
+    """r_out = r_in + 0.5*drop(W2 drop(silu(W1 LN(r_in) + b1)) + b2) (NeMo ConformerFeedForward half step)."""
+    rows, d = x.shape
+    dev = x.device
+    W1, W2 = P[L + which + ".linear1.weight"], P[L + which + ".linear2.weight"]
+    ff = W1.shape[0]
+    out = _empty(rows, d, dev=dev)
+    if _FFN_FUSED and K.get_math() == "bf16" and K.ffn_supported(d, ff) and (
+            not save or (K.wgrad_bf16_supported(rows, d, ff) and K.wgrad_bf16_supported(rows, ff, d))):
+        m = _empty(rows, dev=dev) if save else None
+        r = _empty(rows, dev=dev) if save else None
+        img = K.ffn_img(W1, W2, fwd_only=not save)
+        K.ffn_fwd(x, P[norm + ".weight"], P[norm + ".bias"], cfg.ln_eps, img, P[L + which + ".linear1.bias"],
+                  P[L + which + ".linear2.bias"], out, m, r, ff, rscale=0.5, p_act=pd, p_out=pd, seed=seed,
+                  st_act=_stream(salt, li, site_act), st_out=_stream(salt, li, site_out))
+        keep(**{"m" + tag: m, "r" + tag: r, "ffn_img" + tag: img})
+        return out
+    ln, m, r = _ln(x, P, norm, cfg.ln_eps, dev)
+    h = _empty(rows, ff, dev=dev) if save else None
+    a = _empty(rows, ff, dev=dev)
+    K.linear(ln, W1, P[L + which + ".linear1.bias"], a, epi=_lib.EPI_SILU | (_lib.EPI_STORE_PRE if save else 0), Cpre=h,
+             dropout_p=pd, seed=seed, rng_stream=_stream(salt, li, site_act), tag="ffn_up")
+    K.linear(a, W2, P[L + which + ".linear2.bias"], out, epi=_lib.EPI_RESID, R=x, rscale=0.5, dropout_p=pd, seed=seed,
+             rng_stream=_stream(salt, li, site_out))
+    keep(**{"ln" + tag: ln, "m" + tag: m, "r" + tag: r, "h" + tag: h, "a" + tag: a})
+    return out
+
+
 def layer_forward(cfg, S: EncoderShapes, P, L, li, x, out, pos_emb, lengths, *, train, seed, salt, save,
                   bn_update=None, rm_batch=True):
     """x (rows, d) -> out (rows, d) (written in place).  Returns ctx for backward when save."""
@@ -298,25 +345,27 @@ def layer_forward(cfg, S: EncoderShapes, P, L, li, x, out, pos_emb, lengths, *, 
             ctx.update(kw)
 
     # ---- FFN1 (macaron half-step) ----
-    ln1, m1, r1 = _ln(x, P, L + "norm_feed_forward1", cfg.ln_eps, dev)
-    h1 = _empty(rows, ff, dev=dev) if save else None
-    a1 = _empty(rows, ff, dev=dev)
-    K.linear(ln1, P[L + "feed_forward1.linear1.weight"], P[L + "feed_forward1.linear1.bias"], a1,
-             epi=_lib.EPI_SILU | (_lib.EPI_STORE_PRE if save else 0), Cpre=h1, dropout_p=pd, seed=seed,
-             rng_stream=_stream(salt, li, SITE_FF1_ACT), tag="ffn_up")
-    x1 = _empty(rows, d, dev=dev)
-    K.linear(a1, P[L + "feed_forward1.linear2.weight"], P[L + "feed_forward1.linear2.bias"], x1,
-             epi=_lib.EPI_RESID, R=x, rscale=0.5, dropout_p=pd, seed=seed, rng_stream=_stream(salt, li, SITE_FF1_OUT))
-    keep(x=x, ln1=ln1, m1=m1, r1=r1, h1=h1, a1=a1)
-    del ln1, h1, a1
+    x1 = _ffn_forward(cfg, P, L, "feed_forward1", "norm_feed_forward1", x, pd, seed, salt, li, SITE_FF1_ACT,
+                      SITE_FF1_OUT, save, keep, "1")
+    keep(x=x)
 
     # ---- relative-position MHSA ----
-    ln2, m2, r2 = _ln(x1, P, L + "norm_self_att", cfg.ln_eps, dev)
     qkv = _empty(rows, 3 * d, dev=dev)
-    K.linear(ln2, P[L + "self_attn.qkv.weight"], P[L + "self_attn.qkv.bias"], qkv)
     qu = _empty(rows, d, dev=dev)
     qv = _empty(rows, d, dev=dev)
-    K.qkv_prep(qkv, P[L + "self_attn.pos_bias_u"], P[L + "self_attn.pos_bias_v"], qu, qv)
+    if _lnproj_fused(K.LNPROJ_QKV, rows, d, save):
+        # LN + q|k|v projection + positional biases in one kernel (csrc/lnproj.hip); the backward
+        # recomputes the bf16 LN output it needs for the weight gradient
+        ln2 = None
+        m2 = _empty(rows, dev=dev) if save else None
+        r2 = _empty(rows, dev=dev) if save else None
+        K.ln_qkv_fwd(x1, P[L + "norm_self_att.weight"], P[L + "norm_self_att.bias"], cfg.ln_eps,
+                     K.lnproj_img(K.LNPROJ_QKV, P[L + "self_attn.qkv.weight"]), P[L + "self_attn.qkv.bias"],
+                     P[L + "self_attn.pos_bias_u"], P[L + "self_attn.pos_bias_v"], qu, qv, qkv, m2, r2)
+    else:
+        ln2, m2, r2 = _ln(x1, P, L + "norm_self_att", cfg.ln_eps, dev)
+        K.linear(ln2, P[L + "self_attn.qkv.weight"], P[L + "self_attn.qkv.bias"], qkv)
+        K.qkv_prep(qkv, P[L + "self_attn.pos_bias_u"], P[L + "self_attn.pos_bias_v"], qu, qv)
     npos = 2 * T - 1
     ppos = _empty(npos, d, dev=dev)
     K.linear(pos_emb, P[L + "self_attn.linear_pos.weight"], None, ppos)
@@ -355,11 +404,21 @@ def layer_forward(cfg, S: EncoderShapes, P, L, li, x, out, pos_emb, lengths, *, 
     del ln2, qkv, qu, qv, ppos, Pm, Pd, o
 
     # ---- convolution module ----
-    ln3, m3, r3 = _ln(x2, P, L + "norm_conv", cfg.ln_eps, dev)
-    a = _empty(rows, 2 * d, dev=dev)
-    K.linear(ln3, P[L + "conv.pointwise_conv1.weight"].view(2 * d, d), P[L + "conv.pointwise_conv1.bias"], a)
     g = _empty(rows, d, dev=dev)
-    K.glu_mask_fwd(a, lengths, g, B, T, d)
+    if _lnproj_fused(K.LNPROJ_GLU, rows, d, save):
+        # LN + pointwise_conv1 + GLU + pad mask in one kernel (csrc/lnproj.hip); the backward recomputes
+        # the projection for GLU'
+        ln3 = a = None
+        m3 = _empty(rows, dev=dev) if save else None
+        r3 = _empty(rows, dev=dev) if save else None
+        K.ln_glu_fwd(x2, P[L + "norm_conv.weight"], P[L + "norm_conv.bias"], cfg.ln_eps,
+                     K.lnproj_img(K.LNPROJ_GLU, P[L + "conv.pointwise_conv1.weight"].view(2 * d, d)),
+                     P[L + "conv.pointwise_conv1.bias"], lengths, T, g, m3, r3)
+    else:
+        ln3, m3, r3 = _ln(x2, P, L + "norm_conv", cfg.ln_eps, dev)
+        a = _empty(rows, 2 * d, dev=dev)
+        K.linear(ln3, P[L + "conv.pointwise_conv1.weight"].view(2 * d, d), P[L + "conv.pointwise_conv1.bias"], a)
+        K.glu_mask_fwd(a, lengths, g, B, T, d)
     y = _empty(rows, d, dev=dev)
     stats = torch.zeros(2 * d, device=dev, dtype=torch.float64) if rm_batch else None
     with K.span("dwconv", nbytes=4.0 * 2 * rows * d):   # read g + write y (f32), SURVEY.md §8(d)
@@ -380,20 +439,13 @@ def layer_forward(cfg, S: EncoderShapes, P, L, li, x, out, pos_emb, lengths, *, 
     del ln3, a, g, y, z
 
     # ---- FFN2 ----
-    ln4, m4, r4 = _ln(x3, P, L + "norm_feed_forward2", cfg.ln_eps, dev)
-    h2 = _empty(rows, ff, dev=dev) if save else None
-    a2 = _empty(rows, ff, dev=dev)
-    K.linear(ln4, P[L + "feed_forward2.linear1.weight"], P[L + "feed_forward2.linear1.bias"], a2,
-             epi=_lib.EPI_SILU | (_lib.EPI_STORE_PRE if save else 0), Cpre=h2, dropout_p=pd, seed=seed,
-             rng_stream=_stream(salt, li, SITE_FF2_ACT), tag="ffn_up")
-    x4 = _empty(rows, d, dev=dev)
-    K.linear(a2, P[L + "feed_forward2.linear2.weight"], P[L + "feed_forward2.linear2.bias"], x4,
-             epi=_lib.EPI_RESID, R=x3, rscale=0.5, dropout_p=pd, seed=seed, rng_stream=_stream(salt, li, SITE_FF2_OUT))
+    x4 = _ffn_forward(cfg, P, L, "feed_forward2", "norm_feed_forward2", x3, pd, seed, salt, li, SITE_FF2_ACT,
+                      SITE_FF2_OUT, save, keep, "4")
     # ---- norm_out -> hooked layer output ----
     m5 = _empty(rows, dev=dev)
     r5 = _empty(rows, dev=dev)
     K.layernorm_fwd(x4, P[L + "norm_out.weight"], P[L + "norm_out.bias"], out, m5, r5, cfg.ln_eps)
-    keep(x3=x3, ln4=ln4, m4=m4, r4=r4, h2=h2, a2=a2, x4=x4, m5=m5, r5=r5, pd=pd)
+    keep(x3=x3, x4=x4, m5=m5, r5=r5, pd=pd)
     return ctx
 
 
@@ -411,16 +463,44 @@ class LnGrads:
         K.layernorm_bwd_part(dy, x, g, mean, rstd, dx, part, dres=dres)
         self.pending.append((part, dg, db))
 
+    def reserve(self, dg, db):
+        """A partial slot for a LayerNorm backward computed elsewhere (the fused FFN kernel)."""
+        part = self.buf[len(self.pending)][: self.n]
+        self.pending.append((part, dg, db))
+        return part
+
     def fold(self):
         if self.pending:
             K.ln_fold(self.pending, self.rows, self.d)
             self.pending = []
 
 
-def _ffn_backward(P, G, L, which, dres_out, ln, h, a, x_in_ln, m, r, norm, pd, seed, salt, li, site_act, site_out,
-                  dres_in, dev, lng=None):
+def _ffn_backward(P, G, L, which, dres_out, ctx, tag, x_in_ln, norm, pd, seed, salt, li, site_act, site_out, dev,
+                  lng):
     """Backward of r_out = r_in + 0.5*drop(W2 drop(silu(W1 LN(r_in)))) ; returns d r_in."""
     rows, d = dres_out.shape
+    m, r = ctx["m" + tag], ctx["r" + tag]
+    img = ctx.get("ffn_img" + tag)
+    if img is not None:
+        # fused kernel: hidden chunk recomputed from LN(r_in), data gradient + LN backward in one launch;
+        # the bf16 operands it writes feed the row-parallel weight gradients on the wgrad stream
+        ff = P[L + which + ".linear1.weight"].shape[0]
+        bf = torch.bfloat16
+        ln_h = torch.empty(rows, d, device=dev, dtype=bf)
+        dl2_h = torch.empty(rows, d, device=dev, dtype=bf)
+        a_h = torch.empty(rows, ff, device=dev, dtype=bf)
+        dh_h = torch.empty(rows, ff, device=dev, dtype=bf)
+        dx = _empty(rows, d, dev=dev)
+        part = lng.reserve(G[norm + ".weight"], G[norm + ".bias"])
+        K.ffn_bwd(dres_out, x_in_ln, m, r, P[norm + ".weight"], P[norm + ".bias"], img,
+                  P[L + which + ".linear1.bias"], dx, ln_h, a_h, dl2_h, dh_h, part, ff, rscale=0.5, p_act=pd, p_out=pd,
+                  seed=seed, st_act=_stream(salt, li, site_act), st_out=_stream(salt, li, site_out))
+        WGRAD.run(lambda: K.wgrad_bf16(dl2_h, a_h, G[L + which + ".linear2.weight"], db=G[L + which + ".linear2.bias"]),
+                  dl2_h, a_h)
+        WGRAD.run(lambda: K.wgrad_bf16(dh_h, ln_h, G[L + which + ".linear1.weight"], db=G[L + which + ".linear1.bias"]),
+                  dh_h, ln_h)
+        return dx
+    ln, h, a = ctx["ln" + tag], ctx["h" + tag], ctx["a" + tag]
     ff = h.shape[1]
     dlin2 = _empty(rows, d, dev=dev)
     K.dropout(dres_out, dlin2, pd, 0.5, seed, _stream(salt, li, site_out))
@@ -434,7 +514,7 @@ def _ffn_backward(P, G, L, which, dres_out, ln, h, a, x_in_ln, m, r, norm, pd, s
     K.linear_dx(dh, P[L + which + ".linear1.weight"], dln)
     del dh
     dx = _empty(rows, d, dev=dev)
-    lng.bwd(dln, x_in_ln, P[norm + ".weight"], m, r, dx, G[norm + ".weight"], G[norm + ".bias"], dres=dres_in)
+    lng.bwd(dln, x_in_ln, P[norm + ".weight"], m, r, dx, G[norm + ".weight"], G[norm + ".bias"], dres=dres_out)
     return dx
 
 
@@ -451,9 +531,8 @@ def layer_backward(cfg, S: EncoderShapes, P, G, L, li, ctx, dout, pos_emb, lengt
     lng.bwd(dout, ctx["x4"], P[L + "norm_out.weight"], ctx["m5"], ctx["r5"], dx4, G[L + "norm_out.weight"],
             G[L + "norm_out.bias"])
     # FFN2: x4 = x3 + 0.5 drop(ffn(LN4 x3))
-    dx3 = _ffn_backward(P, G, L, "feed_forward2", dx4, ctx["ln4"], ctx["h2"], ctx["a2"], ctx["x3"], ctx["m4"],
-                        ctx["r4"], L + "norm_feed_forward2", pd, seed, salt, li, SITE_FF2_ACT, SITE_FF2_OUT, dx4, dev,
-                        lng)
+    dx3 = _ffn_backward(P, G, L, "feed_forward2", dx4, ctx, "4", ctx["x3"], L + "norm_feed_forward2", pd, seed, salt,
+                        li, SITE_FF2_ACT, SITE_FF2_OUT, dev, lng)
     del dx4
     # conv module: x3 = x2 + drop(pw2(z))
     dpw2 = _empty(rows, d, dev=dev)
@@ -473,17 +552,29 @@ def layer_backward(cfg, S: EncoderShapes, P, G, L, li, ctx, dout, pos_emb, lengt
                  G[L + "conv.depthwise_conv.weight"].view(d, -1), G[L + "conv.depthwise_conv.bias"], B, T, d,
                  cfg.conv_kernel)
     del dy
-    da = _empty(rows, 2 * d, dev=dev)
-    K.glu_mask_bwd(dg, ctx["a"], lengths, da, B, T, d)
-    del dg
-    WGRAD.run(lambda: K.linear_dw(da, ctx["ln3"], G[L + "conv.pointwise_conv1.weight"].view(2 * d, d), db=G[L + "conv.pointwise_conv1.bias"]), da, ctx["ln3"])
-    dln3 = _empty(rows, d, dev=dev)
-    K.linear_dx(da, P[L + "conv.pointwise_conv1.weight"].view(2 * d, d), dln3)
-    del da
     dx2 = _empty(rows, d, dev=dev)
-    lng.bwd(dln3, ctx["x2"], P[L + "norm_conv.weight"], ctx["m3"], ctx["r3"], dx2, G[L + "norm_conv.weight"],
-            G[L + "norm_conv.bias"], dres=dx3)
-    del dln3, dx3
+    if ctx["ln3"] is None:   # fused LN + pointwise_conv1 + GLU forward: fused backward
+        W1 = P[L + "conv.pointwise_conv1.weight"].view(2 * d, d)
+        ln3_h = torch.empty(rows, d, device=dev, dtype=torch.bfloat16)
+        da_h = torch.empty(rows, 2 * d, device=dev, dtype=torch.bfloat16)
+        part = lng.reserve(G[L + "norm_conv.weight"], G[L + "norm_conv.bias"])
+        K.ln_glu_bwd(dg, ctx["x2"], ctx["m3"], ctx["r3"], P[L + "norm_conv.weight"], P[L + "norm_conv.bias"],
+                     K.lnproj_img(K.LNPROJ_GLU, W1, bwd=True), P[L + "conv.pointwise_conv1.bias"], lengths, T, dx3,
+                     dx2, ln3_h, da_h, part)
+        del dg, dx3
+        WGRAD.run(lambda: K.wgrad_bf16(da_h, ln3_h, G[L + "conv.pointwise_conv1.weight"].view(2 * d, d),
+                                       db=G[L + "conv.pointwise_conv1.bias"]), da_h, ln3_h)
+    else:
+        da = _empty(rows, 2 * d, dev=dev)
+        K.glu_mask_bwd(dg, ctx["a"], lengths, da, B, T, d)
+        del dg
+        WGRAD.run(lambda: K.linear_dw(da, ctx["ln3"], G[L + "conv.pointwise_conv1.weight"].view(2 * d, d), db=G[L + "conv.pointwise_conv1.bias"]), da, ctx["ln3"])
+        dln3 = _empty(rows, d, dev=dev)
+        K.linear_dx(da, P[L + "conv.pointwise_conv1.weight"].view(2 * d, d), dln3)
+        del da
+        lng.bwd(dln3, ctx["x2"], P[L + "norm_conv.weight"], ctx["m3"], ctx["r3"], dx2, G[L + "norm_conv.weight"],
+                G[L + "norm_conv.bias"], dres=dx3)
+        del dln3, dx3
     # MHSA: x2 = x1 + drop(out(O))
     dlo = _empty(rows, d, dev=dev)
     K.dropout(dx2, dlo, pd, 1.0, seed, _stream(salt, li, SITE_ATT_OUT))
@@ -541,22 +632,32 @@ def _attn_bwd_tail(P, G, L, ctx, dqkv, dqu, dqv, dppos, pos_emb, dx2, lng, cfg, 
     """Pos-bias / linear_pos / q|k|v projection grads, norm_self_att and FFN1 backward."""
     K.colsum(dqu, G[L + "self_attn.pos_bias_u"].view(-1))
     K.colsum(dqv, G[L + "self_attn.pos_bias_v"].view(-1))
-    K.axpby(dqu, dqv, dqkv[:, :d], 1.0, 1.0)
-    del dqu, dqv
     WGRAD.run(lambda: K.linear_dw(dppos, pos_emb, G[L + "self_attn.linear_pos.weight"]), dppos, pos_emb)
     del dppos
-    WGRAD.run(lambda: K.linear_dw(dqkv, ctx["ln2"], G[L + "self_attn.qkv.weight"], db=G[L + "self_attn.qkv.bias"]), dqkv, ctx["ln2"])
-    dln2 = _empty(rows, d, dev=dev)
-    K.linear_dx(dqkv, P[L + "self_attn.qkv.weight"], dln2)
-    del dqkv
     dx1 = _empty(rows, d, dev=dev)
-    lng.bwd(dln2, ctx["x1"], P[L + "norm_self_att.weight"], ctx["m2"], ctx["r2"], dx1,
-            G[L + "norm_self_att.weight"], G[L + "norm_self_att.bias"], dres=dx2)
-    del dln2, dx2
+    if ctx["ln2"] is None:   # fused LN + q|k|v forward: fused backward (dq = dqu + dqv formed in-kernel)
+        ln2_h = torch.empty(rows, d, device=dev, dtype=torch.bfloat16)
+        dqkv_h = torch.empty(rows, 3 * d, device=dev, dtype=torch.bfloat16)
+        part = lng.reserve(G[L + "norm_self_att.weight"], G[L + "norm_self_att.bias"])
+        K.ln_qkv_bwd(dqu, dqv, dqkv, ctx["x1"], ctx["m2"], ctx["r2"], P[L + "norm_self_att.weight"],
+                     P[L + "norm_self_att.bias"], K.lnproj_img(K.LNPROJ_QKV, P[L + "self_attn.qkv.weight"], bwd=True),
+                     dx2, dx1, ln2_h, dqkv_h, part)
+        del dqu, dqv, dqkv, dx2
+        WGRAD.run(lambda: K.wgrad_bf16(dqkv_h, ln2_h, G[L + "self_attn.qkv.weight"], db=G[L + "self_attn.qkv.bias"]),
+                  dqkv_h, ln2_h)
+    else:
+        K.axpby(dqu, dqv, dqkv[:, :d], 1.0, 1.0)
+        del dqu, dqv
+        WGRAD.run(lambda: K.linear_dw(dqkv, ctx["ln2"], G[L + "self_attn.qkv.weight"], db=G[L + "self_attn.qkv.bias"]), dqkv, ctx["ln2"])
+        dln2 = _empty(rows, d, dev=dev)
+        K.linear_dx(dqkv, P[L + "self_attn.qkv.weight"], dln2)
+        del dqkv
+        lng.bwd(dln2, ctx["x1"], P[L + "norm_self_att.weight"], ctx["m2"], ctx["r2"], dx1,
+                G[L + "norm_self_att.weight"], G[L + "norm_self_att.bias"], dres=dx2)
+        del dln2, dx2
     # FFN1
-    dx = _ffn_backward(P, G, L, "feed_forward1", dx1, ctx["ln1"], ctx["h1"], ctx["a1"], ctx["x"], ctx["m1"],
-                       ctx["r1"], L + "norm_feed_forward1", pd, seed, salt, li, SITE_FF1_ACT, SITE_FF1_OUT, dx1, dev,
-                       lng)
+    dx = _ffn_backward(P, G, L, "feed_forward1", dx1, ctx, "1", ctx["x"], L + "norm_feed_forward1", pd, seed, salt, li,
+                       SITE_FF1_ACT, SITE_FF1_OUT, dev, lng)
     lng.fold()   # the layer's five dgamma/dbeta folds in one launch
     return dx
 

@@ -615,6 +615,10 @@ def _bf16(t, name="tensor"):
     return t
 
 
+def wgrad_bf16_supported(rows, M, N, bias=True) -> bool:
+    return int(_lib.lib().kdfm_wgrad_bf16_ws(int(rows), int(M), int(N), 1 if bias else 0)) >= 0
+
+
 def wgrad_bf16(dY, X, dW, *, db=None, alpha=1.0):
     """dW[m, n] += alpha * dY[:, m]^T X[:, n] (+ db[m] += alpha * colsum(dY)), bf16 row operands,
     row-parallel MFMA kernel with an ordered fold.  dW may be a row-strided view (stride(1) == 1)."""
@@ -648,6 +652,97 @@ def fm_chain_bwd(dtr, A, gxS, W1, W2, Wst, DV, DA, gx0, S):
     assert gxS is None or (gxS.shape == (n, L) and gxS.is_contiguous())
     call("kdfm_fm_chain_bwd", ptr(_f32(dtr)), ptr(_bf16(A)), ptr(_f32(gxS)), ptr(_f32(W1)), W1.stride(0),
          ptr(_f32(W2)), ptr(_f32(Wst)), ptr(_bf16(DV)), ptr(_bf16(DA)), ptr(gx0), n, L, S, _s())
+
+
+def ffn_supported(d, ff) -> bool:
+    return bool(_lib.lib().kdfm_ffn_supported(int(d), int(ff)))
+
+
+def ffn_img(W1, W2, *, fwd_only=False, out=None):
+    """bf16 chunk images of one feed-forward module's W1 (ff, d) / W2 (d, ff) for kdfm_ffn_fwd/bwd."""
+    ff, d = W1.shape
+    assert W2.shape == (d, ff) and W1.is_contiguous() and W2.is_contiguous()
+    n = int(_lib.lib().kdfm_ffn_img_elems(d, ff))
+    if n <= 0:
+        raise _lib.KdfmError(f"kdfm_ffn: unsupported shape d={d} ff={ff}")
+    img = out if out is not None else torch.empty(n, device=W1.device, dtype=torch.bfloat16)
+    assert img.numel() >= n and img.dtype == torch.bfloat16
+    call("kdfm_ffn_wprep", ptr(_f32(W1)), ptr(_f32(W2)), ptr(img), d, ff, int(bool(fwd_only)), _s())
+    return img
+
+
+def ffn_fwd(x, g, b, eps, img, b1, b2, out, mean, rstd, ff, *, rscale, p_act, p_out, seed, st_act, st_out):
+    """out = x + rscale * drop(W2 drop(silu(W1 LN(x) + b1)) + b2) (the fused macaron FFN block)."""
+    rows, d = x.shape
+    assert out.shape == (rows, d) and x.is_contiguous() and out.is_contiguous()
+    assert (mean is None) == (rstd is None)
+    call("kdfm_ffn_fwd", ptr(_f32(x)), ptr(_f32(g)), ptr(_f32(b)), float(eps), ptr(_bf16(img)), ptr(_f32(b1)),
+         ptr(_f32(b2)), ptr(out), ptr(mean), ptr(rstd), rows, d, int(ff), float(rscale), float(p_act), float(p_out),
+         ptr(seed), int(st_act), int(st_out), _s())
+
+
+def ffn_bwd(dout, x, mean, rstd, g, b, img, b1, dx, ln_h, a_h, dl2_h, dh_h, part, ff, *, rscale, p_act, p_out, seed,
+            st_act, st_out):
+    rows, d = x.shape
+    assert dout.shape == (rows, d) and dx.shape == (rows, d) and dout.is_contiguous() and dx.is_contiguous()
+    assert ln_h.shape == (rows, d) and dl2_h.shape == (rows, d) and a_h.shape == (rows, ff) and dh_h.shape == (rows, ff)
+    assert part.numel() >= layernorm_bwd_ws(rows, d)
+    call("kdfm_ffn_bwd", ptr(_f32(dout)), ptr(_f32(x)), ptr(_f32(mean)), ptr(_f32(rstd)), ptr(_f32(g)), ptr(_f32(b)),
+         ptr(_bf16(img)), ptr(_f32(b1)), ptr(dx), ptr(_bf16(ln_h)), ptr(_bf16(a_h)), ptr(_bf16(dl2_h)),
+         ptr(_bf16(dh_h)), ptr(part), rows, d, int(ff), float(rscale), float(p_act), float(p_out), ptr(seed),
+         int(st_act), int(st_out), _s())
+
+
+LNPROJ_QKV, LNPROJ_GLU = 0, 1
+
+
+def lnproj_supported(kind, d, bwd=False) -> bool:
+    return int(_lib.lib().kdfm_lnproj_img_elems(int(kind), int(d), int(bool(bwd)))) > 0
+
+
+def lnproj_img(kind, W, *, bwd=False):
+    """bf16 fragment image of a LayerNorm-fused projection weight W ((3d | 2d), d) fp32."""
+    d = W.shape[1]
+    assert W.is_contiguous() and W.shape[0] == (3 if kind == LNPROJ_QKV else 2) * d
+    n = int(_lib.lib().kdfm_lnproj_img_elems(int(kind), d, int(bool(bwd))))
+    if n <= 0:
+        raise _lib.KdfmError(f"kdfm_lnproj: unsupported kind={kind} d={d} bwd={bwd}")
+    img = torch.empty(n, device=W.device, dtype=torch.bfloat16)
+    call("kdfm_lnproj_wprep", int(kind), ptr(_f32(W)), ptr(img), d, int(bool(bwd)), _s())
+    return img
+
+
+def ln_qkv_fwd(x, g, b, eps, img, bias, pos_u, pos_v, qu, qv, qkv, mean=None, rstd=None, ln_h=None):
+    rows, d = x.shape
+    assert qu.shape == (rows, d) and qv.shape == (rows, d) and qkv.shape == (rows, 3 * d) and x.is_contiguous()
+    call("kdfm_ln_qkv_fwd", ptr(_f32(x)), ptr(_f32(g)), ptr(_f32(b)), float(eps), ptr(_bf16(img)), ptr(_f32(bias)),
+         ptr(_f32(pos_u)), ptr(_f32(pos_v)), ptr(qu), ptr(qv), ptr(qkv), ptr(mean), ptr(rstd), ptr(_bf16(ln_h)), rows, d,
+         _s())
+
+
+def ln_glu_fwd(x, g, b, eps, img, bias, lengths, T, gout, mean=None, rstd=None, ln_h=None):
+    rows, d = x.shape
+    assert gout.shape == (rows, d) and x.is_contiguous() and rows % T == 0
+    call("kdfm_ln_glu_fwd", ptr(_f32(x)), ptr(_f32(g)), ptr(_f32(b)), float(eps), ptr(_bf16(img)), ptr(_f32(bias)),
+         ptr(_i64(lengths)), int(T), ptr(gout), ptr(mean), ptr(rstd), ptr(_bf16(ln_h)), rows, d, _s())
+
+
+def ln_qkv_bwd(dqu, dqv, dqkv, x, mean, rstd, g, b, img, dres, dx, ln_h, dqkv_h, part):
+    rows, d = x.shape
+    assert dqkv.shape == (rows, 3 * d) and dqkv_h.shape == (rows, 3 * d) and ln_h.shape == (rows, d)
+    assert part.numel() >= layernorm_bwd_ws(rows, d)
+    call("kdfm_ln_qkv_bwd", ptr(_f32(dqu)), ptr(_f32(dqv)), ptr(_f32(dqkv)), ptr(_f32(x)), ptr(_f32(mean)),
+         ptr(_f32(rstd)), ptr(_f32(g)), ptr(_f32(b)), ptr(_bf16(img)), ptr(_f32(dres)), ptr(dx), ptr(_bf16(ln_h)),
+         ptr(_bf16(dqkv_h)), ptr(part), rows, d, _s())
+
+
+def ln_glu_bwd(dg, x, mean, rstd, g, b, img, bias, lengths, T, dres, dx, ln_h, da_h, part):
+    rows, d = x.shape
+    assert dg.shape == (rows, d) and da_h.shape == (rows, 2 * d) and ln_h.shape == (rows, d)
+    assert part.numel() >= layernorm_bwd_ws(rows, d)
+    call("kdfm_ln_glu_bwd", ptr(_f32(dg)), ptr(_f32(x)), ptr(_f32(mean)), ptr(_f32(rstd)), ptr(_f32(g)), ptr(_f32(b)),
+         ptr(_bf16(img)), ptr(_f32(bias)), ptr(_i64(lengths)), int(T), ptr(_f32(dres)), ptr(dx), ptr(_bf16(ln_h)),
+         ptr(_bf16(da_h)), ptr(part), rows, d, _s())
 
 
 def wgrad_bf16_conv(dY, X, dW, T, *, taps=3, pad=1, db=None, alpha=1.0):
