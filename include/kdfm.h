@@ -212,6 +212,41 @@ int32_t kdfm_ffn_supported(int64_t d, int64_t ff);
  * (dqkv_h (rows, 3d) / da_h (rows, 2d): dW = dproj^T ln via kdfm_wgrad_bf16) and the LayerNorm
  * dgamma|dbeta partials `part` (kdfm_layernorm_bwd_part layout, folded by kdfm_ln_fold). */
 int64_t kdfm_lnproj_img_elems(int32_t kind, int64_t d, int32_t bwd);
+
+/* Row-streaming d x d products of a Conformer layer (attention linear_out, conv pointwise_conv2 and
+ * their data gradients; ConformerLayer.forward, SURVEY.md Appendix A.6/A.7, called
+ * conformer_encoder.py:685-692): out = epi(pro(x) Wop^T) over (rows, d) fp32 rows, bf16 MFMA.
+ *   prologue 0: x;  1 (dropout): x * s_in * keep(row*d + k, stream_in) / (1 - p_in);
+ *            2 (BN-SiLU): silu((x - bn_mean) bn_rstd bn_g + bn_b) per channel
+ *   x_h (optional, rows x d bf16): the prologue output as the weight-gradient operand
+ *   epilogue 0: acc;  1 (residual): R + rscale * drop(acc + bias) (mask row*d + n on stream_out)
+ * img: kdfm_rowgemm_img_elems(d) bf16 from kdfm_rowgemm_wprep(W (d, d) [out][in]; trans = 1 for the
+ * data gradient dx = dy W).  d as kdfm_ffn_supported; rows 16-byte aligned. */
+int64_t kdfm_rowgemm_img_elems(int64_t d);
+
+/* Every weight image of a model in ONE launch per step: a device array of jobs (the host builds it
+ * once; pointers stay valid while the parameter buffer lives), each job one image of the fused
+ * Conformer kernels above.  start = first global thread of the job (jobs in increasing start, each
+ * kdfm_wimg_job_threads(job) threads); total_threads = sum over jobs. */
+typedef struct kdfm_wimg_job {
+  int64_t type;   /* 0: FFN chunk image (W1, W2; kdfm_ffn_wprep), 1: LN projection (W1 = W;
+                     kdfm_lnproj_wprep), 2: row-streaming (W1 = W; kdfm_rowgemm_wprep) */
+  int64_t kind;   /* LN projection: 0 QKV, 1 GLU */
+  int64_t flag;   /* FFN: forward-only image; LN projection: backward image; row-streaming: transposed */
+  int64_t d, ff;
+  const float* W1;
+  const float* W2;
+  uint16_t* img;
+  int64_t start;
+} kdfm_wimg_job;
+int64_t kdfm_wimg_job_threads(const kdfm_wimg_job* job);
+int kdfm_wimg_prep_batch(const kdfm_wimg_job* jobs, int32_t njobs, int64_t total_threads, void* stream);
+int kdfm_rowgemm_wprep(const float* W, uint16_t* img, int64_t d, int32_t trans, void* stream);
+int kdfm_rowgemm(const float* x, const uint16_t* img, float* out, int64_t rows, int64_t d, int32_t prologue,
+                 float p_in, float s_in, uint64_t stream_in, const float* bn_mean, const float* bn_rstd,
+                 const float* bn_g, const float* bn_b, uint16_t* x_h, int32_t epilogue, const float* bias,
+                 const float* R, float rscale, float p_out, uint64_t stream_out, const uint64_t* seed,
+                 void* stream);
 int kdfm_lnproj_wprep(int32_t kind, const float* W, uint16_t* img, int64_t d, int32_t bwd, void* stream);
 int kdfm_ln_qkv_fwd(const float* x, const float* ln_g, const float* ln_b, float ln_eps, const uint16_t* img,
                     const float* bias, const float* pos_u, const float* pos_v, float* qu, float* qv, float* qkv,

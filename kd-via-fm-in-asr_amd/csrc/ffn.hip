@@ -24,6 +24,7 @@
 // the odd hidden chunks and their partial down-projections are added (in that fixed order) through
 // LDS at the end, so 12,832 rows give 804 waves instead of 402.
 #include "lnblock.h"
+#include "wimg.h"
 
 namespace kdfm {
 namespace {
@@ -56,32 +57,9 @@ __global__ __launch_bounds__(256) void ffn_wprep_kernel(const float* __restrict_
   const int64_t rest = g >> 6;
   const int f = (int)(rest % nfr);
   const int64_t c = rest / nfr;
-  const int r = lane & 31, h = lane >> 5;
-  const int CS = 4 * DT + 2 * KS1;
   float v[8];
-  if (f < 2 * DT) {                       // W2c(mt, ks2): W2[mt*32 + r][c*32 + ks2*16 + 8h + j]
-    const int row = (f >> 1) * 32 + r;
-    const int64_t col = c * 32 + (f & 1) * 16 + 8 * h;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = row < d ? W2[(int64_t)row * ff + col + j] : 0.f;
-  } else if (f < 2 * DT + KS1) {          // W1c(ks): W1[c*32 + r][ks*16 + 8h + j]
-    const int k0 = (f - 2 * DT) * 16 + 8 * h;
-    const int64_t row = c * 32 + r;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = k0 + j < d ? W1[row * d + k0 + j] : 0.f;
-  } else if (f < 2 * DT + 2 * KS1) {      // W2Tc(ks): W2[ks*16 + 8h + j][c*32 + r]
-    const int k0 = (f - 2 * DT - KS1) * 16 + 8 * h;
-    const int64_t col = c * 32 + r;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = k0 + j < d ? W2[(int64_t)(k0 + j) * ff + col] : 0.f;
-  } else {                                // W1Tc(mt, ks2): W1[c*32 + ks2*16 + 8h + j][mt*32 + r]
-    const int t = f - 2 * DT - 2 * KS1;
-    const int row = (t >> 1) * 32 + r;
-    const int64_t k0 = c * 32 + (t & 1) * 16 + 8 * h;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = row < d ? W1[(k0 + j) * d + row] : 0.f;
-  }
-  *reinterpret_cast<bf16x8*>(img + ((c * CS + f) * 64 + lane) * 8) = pack_bf16x8<bf16x8>(v);
+  wimg::ffn_frag(W1, W2, d, ff, KS1, DT, c, f, lane, v);
+  *reinterpret_cast<bf16x8*>(img + ((c * (4 * DT + 2 * KS1) + f) * 64 + lane) * 8) = pack_bf16x8<bf16x8>(v);
 }
 
 struct FfnFwd {
@@ -92,6 +70,14 @@ struct FfnFwd {
   float rscale, p_act, p_out;
   const uint64_t* seed; uint64_t st_act, st_out;
 };
+
+// bytes of the weight-stage region (double-buffered 2-chunk stages, reused for the final reduction);
+// the per-feature vectors (biases) follow it in LDS: a global bias load inside the chunk loop would
+// wait (in-order vmcnt) for the next stage's prefetch and expose its latency every iteration
+template <int SF, int DT>
+constexpr int ffn_stage_bytes() {
+  return 4 * SF * 1024 > 2 * DT * 16 * 64 * 4 ? 4 * SF * 1024 : 2 * DT * 16 * 64 * 4;
+}
 
 template <int KS1, int DT>
 __global__ __launch_bounds__(FF_NT) void ffn_fwd_kernel(FfnFwd a) {
@@ -123,6 +109,8 @@ __global__ __launch_bounds__(FF_NT) void ffn_fwd_kernel(FfnFwd a) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[mt][i] = 0.f;
 
+  float* bias_s = reinterpret_cast<float*>(reinterpret_cast<char*>(ff_lds) + ffn_stage_bytes<G::FWD, DT>());
+  for (int e = threadIdx.x; e < ff + d; e += FF_NT) bias_s[e] = e < ff ? a.b1[e] : a.b2[e - ff];
   stg.store(ff_lds, 0);
   __syncthreads();
   const int nit = (FC + 1) / 2;
@@ -141,7 +129,7 @@ __global__ __launch_bounds__(FF_NT) void ffn_fwd_kernel(FfnFwd a) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int n0 = c * 32 + 8 * q + 4 * h;
-        const float4 bb = *reinterpret_cast<const float4*>(a.b1 + n0);
+        const float4 bb = *reinterpret_cast<const float4*>(bias_s + n0);
         const float bv[4] = {bb.x, bb.y, bb.z, bb.w};
         float v[4];
 #pragma unroll
@@ -180,7 +168,7 @@ __global__ __launch_bounds__(FF_NT) void ffn_fwd_kernel(FfnFwd a) {
     for (int q = 0; q < 4; ++q) {
       const int n0 = mt * 32 + 8 * q + 4 * h;
       if (n0 >= d) continue;
-      const float4 bb = *reinterpret_cast<const float4*>(a.b2 + n0);
+      const float4 bb = *reinterpret_cast<const float4*>(bias_s + ff + n0);
       const float4 xr = *reinterpret_cast<const float4*>(a.x + row * d + n0);
       const float bv[4] = {bb.x, bb.y, bb.z, bb.w}, xv[4] = {xr.x, xr.y, xr.z, xr.w};
       float o[4];
@@ -248,6 +236,8 @@ __global__ __launch_bounds__(FF_NT) void ffn_bwd_kernel(FfnBwd a) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[mt][i] = 0.f;
 
+  float* bias_s = reinterpret_cast<float*>(reinterpret_cast<char*>(ff_lds) + ffn_stage_bytes<G::BWD, DT>());
+  for (int e = threadIdx.x; e < ff; e += FF_NT) bias_s[e] = a.b1[e];
   stg.store(ff_lds, 0);
   __syncthreads();
   const int nit = (FC + 1) / 2;
@@ -268,7 +258,7 @@ __global__ __launch_bounds__(FF_NT) void ffn_bwd_kernel(FfnBwd a) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int n0 = c * 32 + 8 * q + 4 * h;
-        const float4 bb = *reinterpret_cast<const float4*>(a.b1 + n0);
+        const float4 bb = *reinterpret_cast<const float4*>(bias_s + n0);
         const float bv[4] = {bb.x, bb.y, bb.z, bb.w};
         float av[4], dv[4];
 #pragma unroll
@@ -340,8 +330,7 @@ int launch_fwd(const FfnFwd& a, hipStream_t st) {
   using G = FfnGeo<KS1, DT>;
   static bool once = (ffn_allow_lds(ffn_fwd_kernel<KS1, DT>), true);
   (void)once;
-  const size_t lds = (size_t)4 * G::FWD * 1024 > (size_t)2 * DT * 16 * 64 * 4 ? (size_t)4 * G::FWD * 1024
-                                                                                : (size_t)2 * DT * 16 * 64 * 4;
+  const size_t lds = (size_t)ffn_stage_bytes<G::FWD, DT>() + (size_t)(a.ff + a.d) * 4;
   hipLaunchKernelGGL((ffn_fwd_kernel<KS1, DT>), dim3((unsigned)ceil_div(a.rows, FF_ROWS)), dim3(FF_NT), lds, st, a);
   return check_launch("kdfm_ffn_fwd");
 }
@@ -351,8 +340,7 @@ int launch_bwd(const FfnBwd& a, hipStream_t st) {
   using G = FfnGeo<KS1, DT>;
   static bool once = (ffn_allow_lds(ffn_bwd_kernel<KS1, DT>), true);
   (void)once;
-  const size_t lds = (size_t)4 * G::BWD * 1024 > (size_t)2 * DT * 16 * 64 * 4 ? (size_t)4 * G::BWD * 1024
-                                                                                : (size_t)2 * DT * 16 * 64 * 4;
+  const size_t lds = (size_t)ffn_stage_bytes<G::BWD, DT>() + (size_t)a.ff * 4;
   hipLaunchKernelGGL((ffn_bwd_kernel<KS1, DT>), dim3((unsigned)ceil_div(a.rows, FF_ROWS)), dim3(FF_NT), lds, st, a);
   return check_launch("kdfm_ffn_bwd");
 }

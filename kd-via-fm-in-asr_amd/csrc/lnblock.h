@@ -241,7 +241,7 @@ __device__ __forceinline__ void ln_backward_rows(const float (&dl)[DT * 16], con
 }
 
 // d -> (KS1 = 16-wide k-steps over d, DT = 32-wide feature tiles over d) of the compiled variants
-inline int ln_dims(int64_t d, int& KS1, int& DT) {
+__host__ __device__ inline int ln_dims(int64_t d, int& KS1, int& DT) {
   if (d % 8 != 0) return -1;
   if (d > 80 && d <= 96) { KS1 = 6; DT = 3; return 0; }
   if (d > 160 && d <= 176) { KS1 = 11; DT = 6; return 0; }

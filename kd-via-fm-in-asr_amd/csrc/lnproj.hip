@@ -18,6 +18,7 @@
 // Work split: 3 waves per 32-row tile (one per q / k / v kind, or one per 32-feature GLU group),
 // 2 tiles per workgroup (384 threads); backward partial dln sums are added in wave order through LDS.
 #include "lnblock.h"
+#include "wimg.h"
 
 namespace kdfm {
 namespace {
@@ -52,49 +53,8 @@ __global__ __launch_bounds__(256) void lnproj_wprep_kernel(const float* __restri
   if (gidx >= total) return;
   const int lane = (int)(gidx & 63);
   const int f = (int)(gidx >> 6);
-  const int r = lane & 31, h = lane >> 5;
-  const int G = mode == LP_QKV ? 3 : 2;
-  int wrow = -1, k0 = 0;  // W row (valid < G d), first column (8 consecutive)
-  bool trans = false;
-  auto fwd_frag = [&](int g, int t, int ks) {
-    const int feat = 32 * t + r;
-    wrow = feat < d ? g * d + feat : -1;
-    k0 = 16 * ks + 8 * h;
-  };
-  if (!bwd) {
-    if (mode == LP_QKV) {
-      const int u = f / KS1, ks = f % KS1;
-      fwd_frag(u % 3, u / 3, ks);
-    } else {
-      const int u = f / (2 * KS1), rem = f % (2 * KS1);
-      fwd_frag(rem / KS1, u, rem % KS1);
-    }
-  } else {
-    const int BB = (mode == LP_GLU ? 2 * KS1 : 0) + 2 * G * DT;
-    const int t = f / BB;
-    int rem = f % BB;
-    if (mode == LP_GLU && rem < 2 * KS1) {
-      fwd_frag(rem / KS1, t, rem % KS1);
-    } else {
-      if (mode == LP_GLU) rem -= 2 * KS1;
-      const int g = rem / (2 * DT), s2 = (rem / DT) % 2, mt = rem % DT;
-      trans = true;
-      const int feat0 = 32 * t + 16 * s2 + 8 * h;   // proj feature (8 consecutive, all valid or none)
-      wrow = feat0 < d ? g * d + feat0 : -1;
-      k0 = 32 * mt + r;                               // column of W
-    }
-  }
   float v[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    if (wrow < 0) {
-      v[j] = 0.f;
-    } else if (!trans) {
-      v[j] = k0 + j < d ? W[(int64_t)wrow * d + k0 + j] : 0.f;
-    } else {
-      v[j] = k0 < d ? W[(int64_t)(wrow + j) * d + k0] : 0.f;
-    }
-  }
+  wimg::lnproj_frag(W, d, KS1, DT, mode, bwd, f, lane, v);
   *reinterpret_cast<bf16x8*>(img + ((int64_t)f * 64 + lane) * 8) = pack_bf16x8<bf16x8>(v);
 }
 
@@ -129,9 +89,15 @@ __global__ __launch_bounds__(LP_NT) void lnproj_fwd_kernel(LpFwd a) {
   }
   bool live = ok;
   if (MODE == LP_GLU && ok && a.lens) live = (row % a.T) < a.lens[row / a.T];
+  constexpr int S = (Gm::NU + LP_NP - 1) / LP_NP;
+  // projection bias (and the positional biases) in LDS: a global load inside the loop would wait
+  // (in-order vmcnt) for the next stage's prefetch
+  float* vec_s = reinterpret_cast<float*>(lp_lds + (S > 1 ? 2 : 1) * St::UNITS);
+  const int nvec = (MODE == LP_QKV ? 5 : 2) * d;
+  for (int e = threadIdx.x; e < nvec; e += LP_NT)
+    vec_s[e] = e < Gm::G * d ? a.bias[e] : (e < 4 * d ? a.pu[e - 3 * d] : a.pv[e - 4 * d]);
   stg.store(lp_lds, 0);
   __syncthreads();
-  constexpr int S = (Gm::NU + LP_NP - 1) / LP_NP;
   for (int s = 0; s < S; ++s) {
     if (s + 1 < S) stg.load(img, s + 1, Gm::NU);
     const int u = s * LP_NP + p;
@@ -146,12 +112,12 @@ __global__ __launch_bounds__(LP_NT) void lnproj_fwd_kernel(LpFwd a) {
         for (int q = 0; q < 4; ++q) {
           const int n0 = 32 * t + 8 * q + 4 * h;
           if (!ok || n0 >= d) continue;
-          const float4 bb = *reinterpret_cast<const float4*>(a.bias + g * d + n0);
+          const float4 bb = *reinterpret_cast<const float4*>(vec_s + g * d + n0);
           const float v0 = acc[4 * q] + bb.x, v1 = acc[4 * q + 1] + bb.y, v2 = acc[4 * q + 2] + bb.z,
                       v3 = acc[4 * q + 3] + bb.w;
           if (g == 0) {
-            const float4 uu = *reinterpret_cast<const float4*>(a.pu + n0);
-            const float4 vv = *reinterpret_cast<const float4*>(a.pv + n0);
+            const float4 uu = *reinterpret_cast<const float4*>(vec_s + 3 * d + n0);
+            const float4 vv = *reinterpret_cast<const float4*>(vec_s + 4 * d + n0);
             *reinterpret_cast<float4*>(a.qu + row * d + n0) = make_float4(v0 + uu.x, v1 + uu.y, v2 + uu.z, v3 + uu.w);
             *reinterpret_cast<float4*>(a.qv + row * d + n0) = make_float4(v0 + vv.x, v1 + vv.y, v2 + vv.z, v3 + vv.w);
           } else {
@@ -170,8 +136,8 @@ __global__ __launch_bounds__(LP_NT) void lnproj_fwd_kernel(LpFwd a) {
         for (int q = 0; q < 4; ++q) {
           const int n0 = 32 * t + 8 * q + 4 * h;
           if (!ok || n0 >= d) continue;
-          const float4 ba = *reinterpret_cast<const float4*>(a.bias + n0);
-          const float4 bg = *reinterpret_cast<const float4*>(a.bias + d + n0);
+          const float4 ba = *reinterpret_cast<const float4*>(vec_s + n0);
+          const float4 bg = *reinterpret_cast<const float4*>(vec_s + d + n0);
           const float va[4] = {aa[4 * q] + ba.x, aa[4 * q + 1] + ba.y, aa[4 * q + 2] + ba.z, aa[4 * q + 3] + ba.w};
           const float vg[4] = {ag[4 * q] + bg.x, ag[4 * q + 1] + bg.y, ag[4 * q + 2] + bg.z, ag[4 * q + 3] + bg.w};
           float o[4];
@@ -366,7 +332,7 @@ int launch_lp_fwd(const LpFwd& a, hipStream_t st) {
   static bool once = (lp_allow_lds(lnproj_fwd_kernel<KS1, DT, MODE>), true);
   (void)once;
   constexpr int S = (Gm::NU + LP_NP - 1) / LP_NP;
-  const size_t lds = (size_t)(S > 1 ? 2 : 1) * LP_NP * Gm::UF * 1024;
+  const size_t lds = (size_t)(S > 1 ? 2 : 1) * LP_NP * Gm::UF * 1024 + (size_t)(MODE == LP_QKV ? 5 : 2) * a.d * 4;
   hipLaunchKernelGGL((lnproj_fwd_kernel<KS1, DT, MODE>), dim3((unsigned)ceil_div(a.rows, LP_ROWS)), dim3(LP_NT), lds, st,
                      a);
   return check_launch(MODE == LP_QKV ? "kdfm_ln_qkv_fwd" : "kdfm_ln_glu_fwd");

@@ -301,6 +301,15 @@ def _lnproj_fused(kind, rows, d, save):
 
 
 _LNPROJ_FUSED = __import__("os").environ.get("KDFM_LNPROJ_FUSED", "1") == "1"
+_ROWGEMM_FUSED = __import__("os").environ.get("KDFM_ROWGEMM_FUSED", "1") == "1"
+
+
+def _rowgemm_fused(rows, d, save):
+    """bf16 math: the d x d products (linear_out, BN-SiLU + pointwise_conv2) on kdfm_rowgemm
+    (KDFM_ROWGEMM_FUSED=0: kdfm_gemm + separate BN-SiLU / dropout kernels)."""
+    if not (_ROWGEMM_FUSED and K.get_math() == "bf16" and K.rowgemm_supported(d)):
+        return False
+    return not save or K.wgrad_bf16_supported(rows, d, d)
 
 
 def _ffn_forward(cfg, P, L, which, norm, x, pd, seed, salt, li, site_act, site_out, save, keep, tag):
@@ -345,7 +354,7 @@ def layer_forward(cfg, S: EncoderShapes, P, L, li, x, out, pos_emb, lengths, *, 
             ctx.update(kw)
 
     # ---- FFN1 (macaron half-step) ----
-    x1 = _ffn_forward(cfg, P, L, "feed_forward1", "norm_feed_forward1", x, pd, seed, salt, li, SITE_FF1_ACT,
+    x1 = _ffn_forward(cfg, P, L, "feed_forward1", L + "norm_feed_forward1", x, pd, seed, salt, li, SITE_FF1_ACT,
                       SITE_FF1_OUT, save, keep, "1")
     keep(x=x)
 
@@ -397,9 +406,18 @@ def layer_forward(cfg, S: EncoderShapes, P, L, li, x, out, pos_emb, lengths, *, 
         K.gemm(Pd, qkv[:, 2 * d:], o, T, dk, T, T, 1, 3 * d, 1, d, 1, amode=_lib.LD_KC, bmode=_lib.LD_XC,
                batch=(B, H), bA=(H * T * T, T * T), bB=(T * 3 * d, dk), bC=(T * d, dk))
     x2 = _empty(rows, d, dev=dev)
-    K.linear(o, P[L + "self_attn.linear_out.weight"], P[L + "self_attn.linear_out.bias"], x2, epi=_lib.EPI_RESID,
-             R=x1, rscale=1.0, dropout_p=pd, seed=seed, rng_stream=_stream(salt, li, SITE_ATT_OUT))
-    keep(x1=x1, ln2=ln2, m2=m2, r2=r2, qkv=qkv, qu=qu, qv=qv, ppos=ppos, P=Pm, Pd=Pd, o=o, pa=pa,
+    o_h = None
+    if _rowgemm_fused(rows, d, save):
+        # linear_out + dropout + residual on the row-streaming kernel; training keeps o as the bf16
+        # weight-gradient operand it rounds anyway
+        o_h = torch.empty(rows, d, device=dev, dtype=torch.bfloat16) if save else None
+        K.rowgemm(o, K.rowgemm_img(P[L + "self_attn.linear_out.weight"]), x2, x_h=o_h, epi=K.RG_EPI_RESID,
+                  bias=P[L + "self_attn.linear_out.bias"], R=x1, rscale=1.0, p_out=pd,
+                  st_out=_stream(salt, li, SITE_ATT_OUT), seed=seed)
+    else:
+        K.linear(o, P[L + "self_attn.linear_out.weight"], P[L + "self_attn.linear_out.bias"], x2, epi=_lib.EPI_RESID,
+                 R=x1, rscale=1.0, dropout_p=pd, seed=seed, rng_stream=_stream(salt, li, SITE_ATT_OUT))
+    keep(x1=x1, ln2=ln2, m2=m2, r2=r2, qkv=qkv, qu=qu, qv=qv, ppos=ppos, P=Pm, Pd=Pd, o=o, o_h=o_h, pa=pa,
          attn_fused=K.get_math() == "bf16" and dk <= 48 and _ATTN_BWD_FUSED)
     del ln2, qkv, qu, qv, ppos, Pm, Pd, o
 
@@ -430,16 +448,27 @@ def layer_forward(cfg, S: EncoderShapes, P, L, li, x, out, pos_emb, lengths, *, 
     K.bn_finalize(stats, rmn, rvr, bmean, brstd, d, rows, cfg.bn_eps)
     if rm_batch and bn_update is not None and train:
         K.bn_running_update(rmn, rvr, stats, d, rows, cfg.bn_momentum)
-    z = _empty(rows, d, dev=dev)
-    K.bn_silu_fwd(y, bmean, brstd, P[L + "conv.batch_norm.weight"], P[L + "conv.batch_norm.bias"], z)
     x3 = _empty(rows, d, dev=dev)
-    K.linear(z, P[L + "conv.pointwise_conv2.weight"].view(d, d), P[L + "conv.pointwise_conv2.bias"], x3,
-             epi=_lib.EPI_RESID, R=x2, rscale=1.0, dropout_p=pd, seed=seed, rng_stream=_stream(salt, li, SITE_CONV_OUT))
-    keep(x2=x2, ln3=ln3, m3=m3, r3=r3, a=a, g=g, y=y, bmean=bmean, brstd=brstd, z=z, rm_batch=rm_batch)
+    z = z_h = None
+    if _rowgemm_fused(rows, d, save):
+        # BatchNorm + SiLU as the prologue of pointwise_conv2 (+ dropout + residual): z never reaches HBM
+        # in f32; training keeps its bf16 copy for the weight gradient
+        z_h = torch.empty(rows, d, device=dev, dtype=torch.bfloat16) if save else None
+        K.rowgemm(y, K.rowgemm_img(P[L + "conv.pointwise_conv2.weight"].view(d, d)), x3, pro=K.RG_PRO_BNSILU,
+                  bn=(bmean, brstd, P[L + "conv.batch_norm.weight"], P[L + "conv.batch_norm.bias"]), x_h=z_h,
+                  epi=K.RG_EPI_RESID, bias=P[L + "conv.pointwise_conv2.bias"], R=x2, rscale=1.0, p_out=pd,
+                  st_out=_stream(salt, li, SITE_CONV_OUT), seed=seed)
+    else:
+        z = _empty(rows, d, dev=dev)
+        K.bn_silu_fwd(y, bmean, brstd, P[L + "conv.batch_norm.weight"], P[L + "conv.batch_norm.bias"], z)
+        K.linear(z, P[L + "conv.pointwise_conv2.weight"].view(d, d), P[L + "conv.pointwise_conv2.bias"], x3,
+                 epi=_lib.EPI_RESID, R=x2, rscale=1.0, dropout_p=pd, seed=seed,
+                 rng_stream=_stream(salt, li, SITE_CONV_OUT))
+    keep(x2=x2, ln3=ln3, m3=m3, r3=r3, a=a, g=g, y=y, bmean=bmean, brstd=brstd, z=z, z_h=z_h, rm_batch=rm_batch)
     del ln3, a, g, y, z
 
     # ---- FFN2 ----
-    x4 = _ffn_forward(cfg, P, L, "feed_forward2", "norm_feed_forward2", x3, pd, seed, salt, li, SITE_FF2_ACT,
+    x4 = _ffn_forward(cfg, P, L, "feed_forward2", L + "norm_feed_forward2", x3, pd, seed, salt, li, SITE_FF2_ACT,
                       SITE_FF2_OUT, save, keep, "4")
     # ---- norm_out -> hooked layer output ----
     m5 = _empty(rows, dev=dev)
@@ -535,12 +564,19 @@ def layer_backward(cfg, S: EncoderShapes, P, G, L, li, ctx, dout, pos_emb, lengt
                         li, SITE_FF2_ACT, SITE_FF2_OUT, dev, lng)
     del dx4
     # conv module: x3 = x2 + drop(pw2(z))
-    dpw2 = _empty(rows, d, dev=dev)
-    K.dropout(dx3, dpw2, pd, 1.0, seed, _stream(salt, li, SITE_CONV_OUT))
-    WGRAD.run(lambda: K.linear_dw(dpw2, ctx["z"], G[L + "conv.pointwise_conv2.weight"].view(d, d), db=G[L + "conv.pointwise_conv2.bias"]), dpw2, ctx["z"])
     dz = _empty(rows, d, dev=dev)
-    K.linear_dx(dpw2, P[L + "conv.pointwise_conv2.weight"].view(d, d), dz)
-    del dpw2
+    if ctx.get("z_h") is not None:   # dropout prologue + data gradient on the row-streaming kernel
+        dpw2_h = torch.empty(rows, d, device=dev, dtype=torch.bfloat16)
+        K.rowgemm(dx3, K.rowgemm_img(P[L + "conv.pointwise_conv2.weight"].view(d, d), trans=True), dz,
+                  pro=K.RG_PRO_DROP, p_in=pd, s_in=1.0, st_in=_stream(salt, li, SITE_CONV_OUT), x_h=dpw2_h, seed=seed)
+        WGRAD.run(lambda: K.wgrad_bf16(dpw2_h, ctx["z_h"], G[L + "conv.pointwise_conv2.weight"].view(d, d),
+                                       db=G[L + "conv.pointwise_conv2.bias"]), dpw2_h, ctx["z_h"])
+    else:
+        dpw2 = _empty(rows, d, dev=dev)
+        K.dropout(dx3, dpw2, pd, 1.0, seed, _stream(salt, li, SITE_CONV_OUT))
+        WGRAD.run(lambda: K.linear_dw(dpw2, ctx["z"], G[L + "conv.pointwise_conv2.weight"].view(d, d), db=G[L + "conv.pointwise_conv2.bias"]), dpw2, ctx["z"])
+        K.linear_dx(dpw2, P[L + "conv.pointwise_conv2.weight"].view(d, d), dz)
+        del dpw2
     dy = _empty(rows, d, dev=dev)
     red = torch.empty(2 * d, device=dev, dtype=torch.float64)
     K.bn_silu_bwd(dz, ctx["y"], ctx["bmean"], ctx["brstd"], P[L + "conv.batch_norm.weight"],
@@ -576,12 +612,19 @@ def layer_backward(cfg, S: EncoderShapes, P, G, L, li, ctx, dout, pos_emb, lengt
                 G[L + "norm_conv.bias"], dres=dx3)
         del dln3, dx3
     # MHSA: x2 = x1 + drop(out(O))
-    dlo = _empty(rows, d, dev=dev)
-    K.dropout(dx2, dlo, pd, 1.0, seed, _stream(salt, li, SITE_ATT_OUT))
-    WGRAD.run(lambda: K.linear_dw(dlo, ctx["o"], G[L + "self_attn.linear_out.weight"], db=G[L + "self_attn.linear_out.bias"]), dlo, ctx["o"])
     do = _empty(rows, d, dev=dev)
-    K.linear_dx(dlo, P[L + "self_attn.linear_out.weight"], do)
-    del dlo
+    if ctx.get("o_h") is not None:
+        dlo_h = torch.empty(rows, d, device=dev, dtype=torch.bfloat16)
+        K.rowgemm(dx2, K.rowgemm_img(P[L + "self_attn.linear_out.weight"], trans=True), do, pro=K.RG_PRO_DROP,
+                  p_in=pd, s_in=1.0, st_in=_stream(salt, li, SITE_ATT_OUT), x_h=dlo_h, seed=seed)
+        WGRAD.run(lambda: K.wgrad_bf16(dlo_h, ctx["o_h"], G[L + "self_attn.linear_out.weight"],
+                                       db=G[L + "self_attn.linear_out.bias"]), dlo_h, ctx["o_h"])
+    else:
+        dlo = _empty(rows, d, dev=dev)
+        K.dropout(dx2, dlo, pd, 1.0, seed, _stream(salt, li, SITE_ATT_OUT))
+        WGRAD.run(lambda: K.linear_dw(dlo, ctx["o"], G[L + "self_attn.linear_out.weight"], db=G[L + "self_attn.linear_out.bias"]), dlo, ctx["o"])
+        K.linear_dx(dlo, P[L + "self_attn.linear_out.weight"], do)
+        del dlo
     qkv, Pm, Pd, qu, qv, ppos = ctx["qkv"], ctx["P"], ctx["Pd"], ctx["qu"], ctx["qv"], ctx["ppos"]
     npos = 2 * T - 1
     if ctx.get("attn_fused"):
@@ -730,6 +773,32 @@ def encoder_backward(cfg, S: EncoderShapes, P, G, prefix, run: EncoderRun, dfeat
     subsampling_backward(cfg, S, P, G, prefix, run.sub, dx, len1, seed=seed, salt=salt, ws=ws)
     run.sub = None
     WGRAD.join()  # weight gradients computed on the side stream are complete before anyone reads G
+
+
+def layer_images(cfg: Ver5Config, P, prefix, d, *, train, dev):
+    """The weight images of every fused-kernel product of an encoder's layers (kernels.WeightImages:
+    one buffer, one prep launch per step, looked up by ffn_img / lnproj_img / rowgemm_img)."""
+    imgs = K.WeightImages(dev)
+    ff = cfg.ff_expansion * d
+    for i in range(cfg.n_layers):
+        L = f"{prefix}layers.{i}."
+        if K.ffn_supported(d, ff):
+            for which in ("feed_forward1", "feed_forward2"):
+                imgs.add(L + which, K.IMG_FFN, P[L + which + ".linear1.weight"], P[L + which + ".linear2.weight"],
+                         flag=0 if train else 1, d=d, ff=ff)
+        for kind, W in ((K.LNPROJ_QKV, P[L + "self_attn.qkv.weight"]),
+                        (K.LNPROJ_GLU, P[L + "conv.pointwise_conv1.weight"].view(2 * d, d))):
+            if K.lnproj_supported(kind, d):
+                imgs.add(L + f"lnproj{kind}", K.IMG_LNPROJ, W, kind=kind, flag=0, d=d)
+            if train and K.lnproj_supported(kind, d, bwd=True):
+                imgs.add(L + f"lnproj{kind}_b", K.IMG_LNPROJ, W, kind=kind, flag=1, d=d)
+        if K.rowgemm_supported(d):
+            for name, W in (("out", P[L + "self_attn.linear_out.weight"]),
+                            ("pw2", P[L + "conv.pointwise_conv2.weight"].view(d, d))):
+                imgs.add(L + name, K.IMG_ROWGEMM, W, flag=0, d=d)
+                if train:
+                    imgs.add(L + name + "_t", K.IMG_ROWGEMM, W, flag=1, d=d)
+    return imgs.finalize().register()
 
 
 def make_workspace(S: EncoderShapes, dev):

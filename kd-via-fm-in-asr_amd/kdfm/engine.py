@@ -16,7 +16,7 @@ from . import _lib
 from . import kernels as K
 from .config import Ver5Config, bn_buffer_specs, student_specs, teacher_specs
 from .conformer import EncoderRun, EncoderShapes, compute_lengths, encoder_backward, encoder_forward, \
-    encoder_forward_steps, make_workspace
+    encoder_forward_steps, layer_images, make_workspace
 from .frontend import FrontendConsts, frontend_forward, mel_frames, specaugment_
 from .heads import HeadsWorkspace, heads_backward, heads_forward
 from .overlap import WGRAD
@@ -74,6 +74,7 @@ class Ver5Engine:
             self.student.enable_bf16_twins()
             self.teacher.enable_bf16_twins()
         self._pos = {}
+        self._imgs = None   # kernels.WeightImages of the student and the teacher encoders (bf16 math)
         self._ws = {}
         self._tgraphs = {}
         # the step runs on a created (non-null) stream: ROCm makes the legacy null stream wait for a
@@ -206,6 +207,14 @@ class Ver5Engine:
         if K.get_math() == "bf16":   # bf16 twins of the weights the skinny products stream
             self.student.refresh_bf16()
             self.teacher.refresh_bf16()
+            # fragment images of the fused Conformer kernels (ffn / lnproj / rowgemm): one launch each
+            if self._imgs is None:
+                self._imgs = (layer_images(cfg, self.student.P, "encoder.", cfg.d_student, train=True, dev=dev),
+                              layer_images(cfg, self.teacher.P, "teacher.encoder.", cfg.d_teacher, train=False,
+                                           dev=dev))
+            for im in self._imgs:
+                im.register()
+                im.refresh()
         # ---- frontends (teacher preprocessor is in eval mode: no dither) ----
         dither = cfg.dither if train else 0.0
         own_mel = train and (dither > 0.0 or not cfg.share_frontend)   # the student computes its own mel

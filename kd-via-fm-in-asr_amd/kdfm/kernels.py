@@ -662,6 +662,10 @@ def ffn_img(W1, W2, *, fwd_only=False, out=None):
     """bf16 chunk images of one feed-forward module's W1 (ff, d) / W2 (d, ff) for kdfm_ffn_fwd/bwd."""
     ff, d = W1.shape
     assert W2.shape == (d, ff) and W1.is_contiguous() and W2.is_contiguous()
+    if _IMGSETS and out is None:
+        img = _registered_img(IMG_FFN, 0, 0, W1) or (_registered_img(IMG_FFN, 0, 1, W1) if fwd_only else None)
+        if img is not None:
+            return img
     n = int(_lib.lib().kdfm_ffn_img_elems(d, ff))
     if n <= 0:
         raise _lib.KdfmError(f"kdfm_ffn: unsupported shape d={d} ff={ff}")
@@ -693,7 +697,122 @@ def ffn_bwd(dout, x, mean, rstd, g, b, img, b1, dx, ln_h, a_h, dl2_h, dh_h, part
          int(st_act), int(st_out), _s())
 
 
+RG_PRO_NONE, RG_PRO_DROP, RG_PRO_BNSILU = 0, 1, 2
+RG_EPI_NONE, RG_EPI_RESID = 0, 1
+
+
+def rowgemm_supported(d) -> bool:
+    return int(_lib.lib().kdfm_rowgemm_img_elems(int(d))) > 0
+
+
+def rowgemm_img(W, *, trans=False):
+    """bf16 fragment image of a (d, d) weight for kdfm_rowgemm (trans: the data-gradient product)."""
+    d = W.shape[0]
+    assert W.shape == (d, d) and W.is_contiguous()
+    if _IMGSETS:
+        img = _registered_img(IMG_ROWGEMM, 0, int(bool(trans)), W)
+        if img is not None:
+            return img
+    n = int(_lib.lib().kdfm_rowgemm_img_elems(d))
+    if n <= 0:
+        raise _lib.KdfmError(f"kdfm_rowgemm: unsupported d={d}")
+    img = torch.empty(n, device=W.device, dtype=torch.bfloat16)
+    call("kdfm_rowgemm_wprep", ptr(_f32(W)), ptr(img), d, int(bool(trans)), _s())
+    return img
+
+
+def rowgemm(x, img, out, *, pro=0, p_in=0.0, s_in=1.0, st_in=0, bn=None, x_h=None, epi=0, bias=None, R=None,
+            rscale=1.0, p_out=0.0, st_out=0, seed=None):
+    """out = epi(pro(x) Wop^T) over d-wide rows (kdfm_rowgemm); bn = (mean, rstd, gamma, beta)."""
+    rows, d = x.shape
+    assert out.shape == (rows, d) and x.is_contiguous() and out.is_contiguous()
+    bm, br, bg, bb = bn if bn is not None else (None, None, None, None)
+    call("kdfm_rowgemm", ptr(_f32(x)), ptr(_bf16(img)), ptr(out), rows, d, int(pro), float(p_in), float(s_in),
+         int(st_in), ptr(bm), ptr(br), ptr(bg), ptr(bb), ptr(_bf16(x_h)), int(epi), ptr(_f32(bias)), ptr(_f32(R)),
+         float(rscale), float(p_out), int(st_out), ptr(seed), _s())
+
+
 LNPROJ_QKV, LNPROJ_GLU = 0, 1
+IMG_FFN, IMG_LNPROJ, IMG_ROWGEMM = 0, 1, 2
+
+
+_IMGSETS: list = []
+
+
+def _registered_img(typ, kind, flag, W):
+    p = W.data_ptr()
+    for r in _IMGSETS:
+        ws = r()
+        if ws is not None:
+            img = ws.by_weight.get((typ, kind, flag, p))
+            if img is not None:
+                return img
+    return None
+
+
+class WeightImages:
+    """Every fused-kernel weight image of one model in ONE bf16 buffer, rebuilt by ONE launch
+    (kdfm_wimg_prep_batch) whenever the f32 weights change (the engine: at the top of each step).
+    Jobs are registered with add(); finalize() sizes the buffer and uploads the job table."""
+    _FMT = struct.Struct("@5q3Pq")   # kdfm_wimg_job: type, kind, flag, d, ff, W1, W2, img, start
+
+    def __init__(self, device):
+        self.device = device
+        self.specs = []    # (key, type, kind, flag, d, ff, W1, W2)
+        self.imgs = {}
+        self.table = None
+
+    def add(self, key, typ, W1, W2=None, *, kind=0, flag=0, d=0, ff=0):
+        assert self.table is None and W1.is_contiguous() and (W2 is None or W2.is_contiguous())
+        self.specs.append((key, typ, kind, int(flag), int(d), int(ff), W1, W2))
+
+    def _elems(self, typ, kind, flag, d, ff):
+        lib = _lib.lib()
+        if typ == IMG_FFN:
+            return int(lib.kdfm_ffn_img_elems(d, ff))
+        if typ == IMG_LNPROJ:
+            return int(lib.kdfm_lnproj_img_elems(kind, d, flag))
+        return int(lib.kdfm_rowgemm_img_elems(d))
+
+    def finalize(self):
+        sizes = [self._elems(t, k, f, d, ff) for _, t, k, f, d, ff, _, _ in self.specs]
+        total = sum(sizes)
+        if total == 0:
+            return self
+        self.buf = torch.empty(total, device=self.device, dtype=torch.bfloat16)
+        raw = bytearray()
+        off = start = 0
+        one = C.create_string_buffer(self._FMT.size)
+        for (key, t, k, f, d, ff, W1, W2), n in zip(self.specs, sizes):
+            img = self.buf[off:off + n]
+            self._FMT.pack_into(one, 0, t, k, f, d, ff, W1.data_ptr(), W2.data_ptr() if W2 is not None else 0,
+                                img.data_ptr(), start)
+            nthr = int(_lib.lib().kdfm_wimg_job_threads(one))
+            if nthr <= 0:
+                raise _lib.KdfmError(f"kdfm_wimg_job_threads: unsupported image {key}")
+            raw += one.raw
+            self.imgs[key] = img
+            off += n
+            start += nthr
+        self.total_threads = start
+        self.table = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(self.device)
+        self.keep = [s[6:] for s in self.specs]   # the weight views stay alive with the table
+        return self
+
+    def register(self):
+        """Make ffn_img / lnproj_img / rowgemm_img return these images for their weights."""
+        import weakref
+        _IMGSETS[:] = [r for r in _IMGSETS if r() is not None and r() is not self]
+        _IMGSETS.append(weakref.ref(self))
+        self.by_weight = {(t, k, f, W1.data_ptr()): self.imgs[key] for key, t, k, f, d, ff, W1, W2 in self.specs}
+        return self
+
+    def refresh(self):
+        if self.table is not None:
+            call("kdfm_wimg_prep_batch", ptr(self.table), len(self.imgs), self.total_threads, _s())
+
+    def get(self, key):
+        return self.imgs.get(key)
 
 
 def lnproj_supported(kind, d, bwd=False) -> bool:
@@ -704,6 +823,10 @@ def lnproj_img(kind, W, *, bwd=False):
     """bf16 fragment image of a LayerNorm-fused projection weight W ((3d | 2d), d) fp32."""
     d = W.shape[1]
     assert W.is_contiguous() and W.shape[0] == (3 if kind == LNPROJ_QKV else 2) * d
+    if _IMGSETS:
+        img = _registered_img(IMG_LNPROJ, int(kind), int(bool(bwd)), W)
+        if img is not None:
+            return img
     n = int(_lib.lib().kdfm_lnproj_img_elems(int(kind), d, int(bool(bwd))))
     if n <= 0:
         raise _lib.KdfmError(f"kdfm_lnproj: unsupported kind={kind} d={d} bwd={bwd}")

@@ -138,3 +138,42 @@ def test_lnproj_backward(kind, B, T):
     assert _rel(Gb, ref["b"]) <= 2e-2
     assert _rel(Gg, ref["ln_g"]) <= 2e-2
     assert _rel(Gbeta, ref["ln_b"]) <= 2e-2
+
+
+def test_batched_weight_images_match_single_preps():
+    """kdfm_wimg_prep_batch (one launch for every image of an encoder) writes the same bytes as the
+    per-image prep entry points, for the student (training images) and the teacher (forward-only)."""
+    from kdfm import kernels as K
+    from kdfm.config import DEFAULT
+    from kdfm.conformer import layer_images
+    from kdfm.store import FlatStore
+    from kdfm.config import student_specs, teacher_specs
+    from dataclasses import replace
+    cfg = replace(DEFAULT, n_layers=2)
+    for specs, prefix, d, train in ((student_specs(cfg), "encoder.", cfg.d_student, True),
+                                    (teacher_specs(cfg), "teacher.encoder.", cfg.d_teacher, False)):
+        st = FlatStore(specs, "cuda", with_grad=False)
+        st.data.copy_(torch.randn(st.numel, generator=torch.Generator().manual_seed(d)))
+        imgs = layer_images(cfg, st.P, prefix, d, train=train, dev=torch.device("cuda"))
+        imgs.refresh()
+        torch.cuda.synchronize()
+        saved, K._IMGSETS[:] = list(K._IMGSETS), []   # per-image preps, not the registered batch
+        try:
+            for key, typ, kind, flag, dd, ff, W1, W2 in imgs.specs:
+                if typ == K.IMG_FFN:
+                    ref = K.ffn_img(W1, W2, fwd_only=bool(flag))
+                    if flag:   # forward-only: compare the forward halves of every chunk
+                        KS1, DT = (6, 3) if d <= 96 else (11, 6)
+                        cs, fw = 4 * DT + 2 * KS1, 2 * DT + KS1
+                        a = imgs.get(key).view(-1, cs, 512)[:, :fw]
+                        b = ref.view(-1, cs, 512)[:, :fw]
+                        assert torch.equal(a, b), key
+                        continue
+                elif typ == K.IMG_LNPROJ:
+                    ref = K.lnproj_img(kind, W1, bwd=bool(flag))
+                else:
+                    ref = K.rowgemm_img(W1, trans=bool(flag))
+                torch.cuda.synchronize()
+                assert torch.equal(imgs.get(key), ref), key
+        finally:
+            K._IMGSETS[:] = saved
