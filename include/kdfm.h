@@ -254,9 +254,12 @@ int kdfm_ln_qkv_fwd(const float* x, const float* ln_g, const float* ln_b, float 
 int kdfm_ln_glu_fwd(const float* x, const float* ln_g, const float* ln_b, float ln_eps, const uint16_t* img,
                     const float* bias, const int64_t* lengths, int64_t T, float* g, float* mean, float* rstd,
                     uint16_t* ln_h, int64_t rows, int64_t d, void* stream);
+/* part_uv (optional, kdfm_layernorm_bwd_ws(rows, d) floats): the pos_bias_u | pos_bias_v gradients
+ * (column sums of dqu | dqv) as 16-row-group partials in the same layout, folded by kdfm_ln_fold. */
 int kdfm_ln_qkv_bwd(const float* dqu, const float* dqv, const float* dqkv, const float* x, const float* mean,
                     const float* rstd, const float* ln_g, const float* ln_b, const uint16_t* img, const float* dres,
-                    float* dx, uint16_t* ln_h, uint16_t* dqkv_h, float* part, int64_t rows, int64_t d, void* stream);
+                    float* dx, uint16_t* ln_h, uint16_t* dqkv_h, float* part, float* part_uv, int64_t rows, int64_t d,
+                    void* stream);
 int kdfm_ln_glu_bwd(const float* dg, const float* x, const float* mean, const float* rstd, const float* ln_g,
                     const float* ln_b, const uint16_t* img, const float* bias, const int64_t* lengths, int64_t T,
                     const float* dres, float* dx, uint16_t* ln_h, uint16_t* da_h, float* part, int64_t rows,
@@ -264,10 +267,13 @@ int kdfm_ln_glu_bwd(const float* dg, const float* x, const float* mean, const fl
 int64_t kdfm_ffn_img_elems(int64_t d, int64_t ff);
 int kdfm_ffn_wprep(const float* W1, const float* W2, uint16_t* img, int64_t d, int64_t ff, int32_t fwd_only,
                    void* stream);
+/* out_ln (optional): the layer's norm_out fused into the epilogue, out_ln = LN(out; out_ln_g, out_ln_b,
+ * out_ln_eps) with its row statistics in out_ln_mean / out_ln_rstd (all null: not computed). */
 int kdfm_ffn_fwd(const float* x, const float* ln_g, const float* ln_b, float ln_eps, const uint16_t* img,
                  const float* b1, const float* b2, float* out, float* mean, float* rstd, int64_t rows, int64_t d,
                  int64_t ff, float rscale, float p_act, float p_out, const uint64_t* seed, uint64_t stream_act,
-                 uint64_t stream_out, void* stream);
+                 uint64_t stream_out, const float* out_ln_g, const float* out_ln_b, float out_ln_eps, float* out_ln,
+                 float* out_ln_mean, float* out_ln_rstd, void* stream);
 int kdfm_ffn_bwd(const float* dout, const float* x, const float* mean, const float* rstd, const float* ln_g,
                  const float* ln_b, const uint16_t* img, const float* b1, float* dx, uint16_t* ln_h, uint16_t* a_h,
                  uint16_t* dl2_h, uint16_t* dh_h, float* part, int64_t rows, int64_t d, int64_t ff, float rscale,
@@ -348,6 +354,9 @@ int kdfm_im2col_3x3s2(const float* X, const int64_t* len_in, float* cols, int64_
                       int64_t C, void* stream);
 /* Tap-major bf16 columns: cols[(b,t2,f2), tap*C + c] = bf16(X[b, 2 t2 - 1 + ky, 2 f2 - 1 + kx, c]) (0 outside /
  * beyond len_in), C % 8 == 0; the bf16 step's conv2 weight-gradient operand. */
+/* the same tap-major bf16 columns from a bf16 source (the saved bf16 conv1 output y1) */
+int kdfm_im2col_3x3s2_tm_from_bf16(const uint16_t* X, const int64_t* len_in, uint16_t* cols, int64_t B, int64_t T1,
+                                   int64_t F1, int64_t C, void* stream);
 int kdfm_im2col_3x3s2_tm_bf16(const float* X, const int64_t* len_in, uint16_t* cols, int64_t B, int64_t T1, int64_t F1,
                               int64_t C, void* stream);
 /* adjoint of the above (gather form); optionally multiplied by relu'(relu_out). */
@@ -406,11 +415,12 @@ int kdfm_subsample_conv2(const uint16_t* y1b, const int64_t* len2, const uint16_
 /* conv2's data gradient without an im2col matrix (bf16 MFMA, f32 accumulate):
  *   dy1[b,t1,f1,ci] = [y1 > 0] * sum_{ky,kx,co: 2 t2 - 1 + ky = t1, 2 f2 - 1 + kx = f1} W[co,ci,ky,kx] dy2[b,t2,f2,co]
  * over the parity classes of (t1, f1) (1, 2, 2 or 4 taps each); wt = kdfm_subsample_dgrad_wprep(W)
- * (kdfm_subsample_dgrad_wprep_elems(C) bf16).  Replaces the ConvSubsampling backward's linear_dx into
+ * (kdfm_subsample_dgrad_wprep_elems(C) bf16); y1 = the bf16 conv1 output (only its sign is read).
+ * Replaces the ConvSubsampling backward's linear_dx into
  * (B T2 F2, 9C) columns + col2im (conformer_encoder.py:381-390). */
 int64_t kdfm_subsample_dgrad_wprep_elems(int64_t C);
 int kdfm_subsample_dgrad_wprep(const float* w2, uint16_t* wt, int64_t C, void* stream);
-int kdfm_subsample_conv2_dgrad(const float* dy2, const uint16_t* wt, const float* y1, float* dy1, int64_t B, int64_t T1,
+int kdfm_subsample_conv2_dgrad(const float* dy2, const uint16_t* wt, const uint16_t* y1, float* dy1, int64_t B, int64_t T1,
                                int64_t F1, int64_t C, void* stream);
 
 /* ---------------- Evaluation path (ctc_models.py:625-692, wer.py) ---------

@@ -69,6 +69,9 @@ struct FfnFwd {
   int64_t rows; int d, ff;
   float rscale, p_act, p_out;
   const uint64_t* seed; uint64_t st_act, st_out;
+  // optional LayerNorm of the block output (the layer's norm_out after feed_forward2):
+  // ln_out = LN(out) with (ln_g, ln_b, ln_eps); its row statistics to ln_mean / ln_rstd
+  const float* ln_g; const float* ln_b; float ln_eps; float* ln_out; float* ln_mean; float* ln_rstd;
 };
 
 // bytes of the weight-stage region (double-buffered 2-chunk stages, reused for the final reduction);
@@ -161,24 +164,65 @@ __global__ __launch_bounds__(FF_NT) void ffn_fwd_kernel(FfnFwd a) {
       for (int i = 0; i < 16; ++i) red[(mt * 16 + i) * 64 + lane] = acc[mt][i];
   }
   __syncthreads();
-  if (par == 1 || !ok) return;
+  if (par == 1) return;   // (every lane of the even wave stays: the optional LN reduces across lanes)
+  float o[DT][16];
+#pragma unroll
+  for (int mt = 0; mt < DT; ++mt)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int n0 = mt * 32 + 8 * q + 4 * h;
+      const bool in = ok && n0 < d;
+      const float4 bb = *reinterpret_cast<const float4*>(bias_s + ff + (n0 < d ? n0 : 0));
+      const float4 xr = *reinterpret_cast<const float4*>(a.x + (in ? row * d + n0 : 0));
+      const float bv[4] = {bb.x, bb.y, bb.z, bb.w}, xv[4] = {xr.x, xr.y, xr.z, xr.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float v = acc[mt][4 * q + i] + red[(mt * 16 + 4 * q + i) * 64 + lane] + bv[i];
+        if (a.p_out > 0.f) v = dropout_keep_k(kout, (uint64_t)row * d + n0 + i, a.p_out) ? v * ks_out : 0.f;
+        o[mt][4 * q + i] = in ? xv[i] + a.rscale * v : 0.f;
+      }
+      if (in)
+        *reinterpret_cast<float4*>(a.out + row * d + n0) =
+            make_float4(o[mt][4 * q], o[mt][4 * q + 1], o[mt][4 * q + 2], o[mt][4 * q + 3]);
+    }
+  if (!a.ln_out) return;
+  // norm_out: two-pass row statistics (this lane's half of the row + its partner lane's)
+  float s = 0.f;
+#pragma unroll
+  for (int mt = 0; mt < DT; ++mt)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) s += o[mt][e];
+  s += __shfl_xor(s, 32, 64);
+  const float mu = s / d;
+  float qv = 0.f;
+#pragma unroll
+  for (int mt = 0; mt < DT; ++mt)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const bool in = mt * 32 + 8 * (e / 4) + 4 * h + (e % 4) < d;
+      const float t = in ? o[mt][e] - mu : 0.f;
+      qv += t * t;
+    }
+  qv += __shfl_xor(qv, 32, 64);
+  const float rs = rsqrtf(qv / d + a.ln_eps);
+  if (!ok) return;
+  if (h == 0) {
+    a.ln_mean[row] = mu;
+    a.ln_rstd[row] = rs;
+  }
 #pragma unroll
   for (int mt = 0; mt < DT; ++mt)
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int n0 = mt * 32 + 8 * q + 4 * h;
       if (n0 >= d) continue;
-      const float4 bb = *reinterpret_cast<const float4*>(bias_s + ff + n0);
-      const float4 xr = *reinterpret_cast<const float4*>(a.x + row * d + n0);
-      const float bv[4] = {bb.x, bb.y, bb.z, bb.w}, xv[4] = {xr.x, xr.y, xr.z, xr.w};
-      float o[4];
+      const float4 gg = *reinterpret_cast<const float4*>(a.ln_g + n0);
+      const float4 bb = *reinterpret_cast<const float4*>(a.ln_b + n0);
+      const float gv[4] = {gg.x, gg.y, gg.z, gg.w}, bv[4] = {bb.x, bb.y, bb.z, bb.w};
+      float y[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        float v = acc[mt][4 * q + i] + red[(mt * 16 + 4 * q + i) * 64 + lane] + bv[i];
-        if (a.p_out > 0.f) v = dropout_keep_k(kout, (uint64_t)row * d + n0 + i, a.p_out) ? v * ks_out : 0.f;
-        o[i] = xv[i] + a.rscale * v;
-      }
-      *reinterpret_cast<float4*>(a.out + row * d + n0) = make_float4(o[0], o[1], o[2], o[3]);
+      for (int i = 0; i < 4; ++i) y[i] = (o[mt][4 * q + i] - mu) * rs * gv[i] + bv[i];
+      *reinterpret_cast<float4*>(a.ln_out + row * d + n0) = make_float4(y[0], y[1], y[2], y[3]);
     }
 }
 
@@ -379,7 +423,8 @@ int kdfm_ffn_wprep(const float* W1, const float* W2, uint16_t* img, int64_t d, i
 int kdfm_ffn_fwd(const float* x, const float* ln_g, const float* ln_b, float ln_eps, const uint16_t* img,
                  const float* b1, const float* b2, float* out, float* mean, float* rstd, int64_t rows, int64_t d,
                  int64_t ff, float rscale, float p_act, float p_out, const uint64_t* seed, uint64_t stream_act,
-                 uint64_t stream_out, void* stream) {
+                 uint64_t stream_out, const float* out_ln_g, const float* out_ln_b, float out_ln_eps, float* out_ln,
+                 float* out_ln_mean, float* out_ln_rstd, void* stream) {
   using namespace kdfm;
   KDFM_REQUIRE(x && ln_g && ln_b && img && b1 && b2 && out, "null pointer");
   KDFM_REQUIRE((mean == nullptr) == (rstd == nullptr), "mean and rstd go together");
@@ -390,8 +435,11 @@ int kdfm_ffn_fwd(const float* x, const float* ln_g, const float* ln_b, float ln_
   KDFM_REQUIRE(p_act >= 0.f && p_act < 1.f && p_out >= 0.f && p_out < 1.f, "dropout p");
   KDFM_REQUIRE((p_act == 0.f && p_out == 0.f) || seed, "dropout needs a seed");
   if (rows <= 0) return KDFM_OK;
+  KDFM_REQUIRE(!out_ln || (out_ln_g && out_ln_b && out_ln_mean && out_ln_rstd && al16(out_ln) && al16(out_ln_g) &&
+                             al16(out_ln_b)),
+               "output LayerNorm needs gamma / beta / mean / rstd (16-byte aligned)");
   FfnFwd a{x, ln_g, ln_b, ln_eps, img, b1, b2, out, mean, rstd, rows, (int)d, (int)ff, rscale, p_act, p_out,
-           seed, stream_act, stream_out};
+           seed, stream_act, stream_out, out_ln_g, out_ln_b, out_ln_eps, out_ln, out_ln_mean, out_ln_rstd};
   hipStream_t st = as_stream(stream);
   if (KS1 == 6) return launch_fwd<6, 3>(a, st);
   if (KS1 == 11) return launch_fwd<11, 6>(a, st);

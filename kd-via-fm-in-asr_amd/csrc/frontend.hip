@@ -295,7 +295,8 @@ __global__ __launch_bounds__(64 * FFT_WAVES) void logmel_fft_kernel(
 // TAP-MAJOR bf16 variant: cols[(b,t2,f2), tap*C + c] = bf16(X[b, 2*t2-1+ky, 2*f2-1+kx, c]); one thread
 // per 8 consecutive channels of one (row, tap): two coalesced float4 reads, one 16-byte store.  The
 // bf16 column matrix is the weight-gradient operand of the bf16 step (half the bytes of the f32 one).
-__global__ __launch_bounds__(256) void im2col_tm_bf16_kernel(const float* __restrict__ X, const int64_t* __restrict__ lin,
+template <typename TX>
+__global__ __launch_bounds__(256) void im2col_tm_bf16_kernel(const TX* __restrict__ X, const int64_t* __restrict__ lin,
                                                              uint16_t* __restrict__ cols, int64_t B, int64_t T1,
                                                              int64_t F1, int C, int64_t T2, int64_t F2) {
   const int64_t idx = xcd_block() * 256 + threadIdx.x;
@@ -309,14 +310,20 @@ __global__ __launch_bounds__(256) void im2col_tm_bf16_kernel(const float* __rest
   const int64_t f2 = row % F2, t2 = (row / F2) % T2, b = row / (F2 * T2);
   const int64_t t1 = 2 * t2 - 1 + ky, f1 = 2 * f2 - 1 + kx;
   const int64_t len = lin ? lin[b] : T1;
-  float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  if (t1 >= 0 && t1 < T1 && t1 < len && f1 >= 0 && f1 < F1) {
-    const float* src = X + ((b * T1 + t1) * F1 + f1) * C + 8 * cg;
-    const float4 a = *reinterpret_cast<const float4*>(src), c = *reinterpret_cast<const float4*>(src + 4);
-    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = c.x; v[5] = c.y; v[6] = c.z; v[7] = c.w;
-  }
   typedef __attribute__((ext_vector_type(8))) short bf8;
-  *reinterpret_cast<bf8*>(cols + row * 9 * C + tap * C + 8 * cg) = pack_bf16x8<bf8>(v);
+  const bool in = t1 >= 0 && t1 < T1 && t1 < len && f1 >= 0 && f1 < F1;
+  bf8* dst = reinterpret_cast<bf8*>(cols + row * 9 * C + tap * C + 8 * cg);
+  if constexpr (sizeof(TX) == 2) {   // bf16 source: a 16-byte copy
+    *dst = in ? *reinterpret_cast<const bf8*>(X + ((b * T1 + t1) * F1 + f1) * C + 8 * cg) : bf8{0, 0, 0, 0, 0, 0, 0, 0};
+  } else {
+    float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (in) {
+      const float* src = X + ((b * T1 + t1) * F1 + f1) * C + 8 * cg;
+      const float4 a = *reinterpret_cast<const float4*>(src), c = *reinterpret_cast<const float4*>(src + 4);
+      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = c.x; v[5] = c.y; v[6] = c.z; v[7] = c.w;
+    }
+    *dst = pack_bf16x8<bf8>(v);
+  }
 }
 
 // dX[b,t1,f1,c] = sum over taps hitting (t1,f1) of dcols; zero beyond len_in; *= (aux > 0) if aux.
@@ -446,9 +453,22 @@ int kdfm_im2col_3x3s2_tm_bf16(const float* X, const int64_t* len_in, uint16_t* c
   const int64_t T2 = (T1 - 1) / 2 + 1, F2 = (F1 - 1) / 2 + 1;
   const int64_t n = B * T2 * F2 * 9 * (C / 8);
   if (n == 0) return KDFM_OK;
-  hipLaunchKernelGGL(im2col_tm_bf16_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, as_stream(stream), X, len_in,
-                     cols, B, T1, F1, (int)C, T2, F2);
+  hipLaunchKernelGGL(im2col_tm_bf16_kernel<float>, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, as_stream(stream), X,
+                     len_in, cols, B, T1, F1, (int)C, T2, F2);
   return check_launch("kdfm_im2col_3x3s2_tm_bf16");
+}
+
+int kdfm_im2col_3x3s2_tm_from_bf16(const uint16_t* X, const int64_t* len_in, uint16_t* cols, int64_t B, int64_t T1,
+                                   int64_t F1, int64_t C, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(X && cols, "null pointer");
+  KDFM_REQUIRE(C % 8 == 0 && ((((uintptr_t)X) | ((uintptr_t)cols)) & 15) == 0, "C % 8 and 16-byte alignment");
+  const int64_t T2 = (T1 - 1) / 2 + 1, F2 = (F1 - 1) / 2 + 1;
+  const int64_t n = B * T2 * F2 * 9 * (C / 8);
+  if (n == 0) return KDFM_OK;
+  hipLaunchKernelGGL(im2col_tm_bf16_kernel<uint16_t>, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0,
+                     as_stream(stream), X, len_in, cols, B, T1, F1, (int)C, T2, F2);
+  return check_launch("kdfm_im2col_3x3s2_tm_from_bf16");
 }
 
 int kdfm_col2im_3x3s2(const float* dcols, const int64_t* len_in, const float* relu_out, float* dX, int64_t B,

@@ -158,6 +158,7 @@ struct LpBwd {
   const float* x; const float* mean; const float* rstd; const float* g; const float* b;
   const uint16_t* img; const float* dres; float* dx; uint16_t* ln_h; float* part;
   int64_t rows, nparts; int d;
+  float* part_uv;   // QKV: optional pos_bias_u / pos_bias_v column-sum partials
 };
 
 // dln partials of the 3 waves of a tile -> wave 0 (fixed order 0 + 1 + 2), then the LN backward
@@ -243,6 +244,39 @@ __global__ __launch_bounds__(LP_NT) void ln_qkv_bwd_kernel(LpBwd a) {
         acc[mt] = mfma32(W[((2 * p + s2) * DT + mt) * FRAG_U4 + lane], bop[2 * t + s2], acc[mt]);
     if (t + 1 < DT) stg.store(lp_lds, (t + 1) & 1);
     __syncthreads();
+  }
+  if (a.part_uv && p > 0) {
+    // pos_bias_u / pos_bias_v gradients (column sums of dqu / dqv) as 16-row-group partials in the
+    // LayerNorm partial layout (part_uv[grp][2d]), folded by the layer's kdfm_ln_fold with its LNs
+    constexpr int NV = 2 * DT * 8;
+    const float* src = p == 1 ? a.dqu : a.dqv;
+    float v0[NV];
+#pragma unroll
+    for (int k = 0; k < 2 * DT; ++k) {
+      const int f0 = 16 * k + 8 * h;
+      const bool in = ok && f0 < d;
+      const float4* q = reinterpret_cast<const float4*>(src + (in ? row * d + f0 : 0));
+      const float4 u0 = q[0], u1 = q[1];
+      const float u[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v0[8 * k + j] = in ? u[j] : 0.f;
+    }
+    float r1[NV / 2], r2[NV / 4], r3[NV / 8], r4[NV / 16];
+    rs_step<NV, 8>(v0, r1, lane);
+    rs_step<NV / 2, 4>(r1, r2, lane);
+    rs_step<NV / 4, 2>(r2, r3, lane);
+    rs_step<NV / 8, 1>(r3, r4, lane);
+    const int64_t grp = (row - (lane & 31)) / 16 + ((lane >> 4) & 1);
+    const int base = ((lane & 8) ? NV / 2 : 0) + ((lane & 4) ? NV / 4 : 0) + ((lane & 2) ? NV / 8 : 0) +
+                     ((lane & 1) ? NV / 16 : 0);
+    if (grp < a.nparts) {
+#pragma unroll
+      for (int j = 0; j < NV / 16; ++j) {
+        const int e = base + j;
+        const int f = 16 * (e / 8) + 8 * h + (e % 8);
+        if (f < d) a.part_uv[grp * 2 * d + (p - 1) * d + f] = r4[j];
+      }
+    }
   }
   lp_finish<DT>(acc, reinterpret_cast<float*>(lp_lds), a, p, tile, lane, row, ok, mean, rstd);
 }
@@ -440,7 +474,8 @@ int kdfm_ln_glu_fwd(const float* x, const float* ln_g, const float* ln_b, float 
 
 int kdfm_ln_qkv_bwd(const float* dqu, const float* dqv, const float* dqkv, const float* x, const float* mean,
                     const float* rstd, const float* ln_g, const float* ln_b, const uint16_t* img, const float* dres,
-                    float* dx, uint16_t* ln_h, uint16_t* dqkv_h, float* part, int64_t rows, int64_t d, void* stream) {
+                    float* dx, uint16_t* ln_h, uint16_t* dqkv_h, float* part, float* part_uv, int64_t rows, int64_t d,
+                    void* stream) {
   using namespace kdfm;
   using namespace kdfm::lnb;
   KDFM_REQUIRE(dqu && dqv && dqkv && x && mean && rstd && ln_g && ln_b && img && dres && dx && ln_h && dqkv_h && part,
@@ -451,7 +486,7 @@ int kdfm_ln_qkv_bwd(const float* dqu, const float* dqv, const float* dqkv, const
                "operands must be 16-byte aligned");
   if (rows <= 0) return KDFM_OK;
   LpBwd a{dqu, dqv, dqkv, dqkv_h, nullptr, nullptr, 1, nullptr, x, mean, rstd, ln_g, ln_b, img, dres, dx, ln_h, part,
-          rows, ceil_div(rows, 16), (int)d};
+          rows, ceil_div(rows, 16), (int)d, part_uv};
   return launch_qkv_bwd<6, 3>(a, as_stream(stream));
 }
 
@@ -470,7 +505,7 @@ int kdfm_ln_glu_bwd(const float* dg, const float* x, const float* mean, const fl
                "operands must be 16-byte aligned");
   if (rows <= 0) return KDFM_OK;
   LpBwd a{nullptr, nullptr, nullptr, da_h, dg, lengths, T, bias, x, mean, rstd, ln_g, ln_b, img, dres, dx, ln_h, part,
-          rows, ceil_div(rows, 16), (int)d};
+          rows, ceil_div(rows, 16), (int)d, nullptr};
   return launch_glu_bwd<6, 3>(a, as_stream(stream));
 }
 

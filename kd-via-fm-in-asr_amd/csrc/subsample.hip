@@ -282,7 +282,7 @@ __global__ __launch_bounds__(256) void ss_dgrad_wprep_kernel(const float* __rest
 template <int NCT, int KS>
 __global__ __launch_bounds__(SS_NT, 2) void ss_dgrad_kernel(const float* __restrict__ dy2,
                                                             const uint16_t* __restrict__ wt,
-                                                            const float* __restrict__ y1, float* __restrict__ dy1,
+                                                            const uint16_t* __restrict__ y1, float* __restrict__ dy1,
                                                             SdGeo g) {
   constexpr int NP = 32 * NCT;
   constexpr int CP = 16 * KS;
@@ -363,7 +363,10 @@ __global__ __launch_bounds__(SS_NT, 2) void ss_dgrad_kernel(const float* __restr
     for (int n = 0; n < NCT; ++n) {
       const int ci = 32 * n + r;
 #pragma unroll
-      for (int e = 0; e < 16; ++e) pos_y[n][e] = (m1[e] >= 0 && ci < g.C) ? y1[m1[e] * g.C + ci] > 0.f : false;
+      for (int e = 0; e < 16; ++e) {   // ReLU' from the sign of the bf16 y1 (bf16 RNE keeps the sign and zero)
+        const uint16_t yb = (m1[e] >= 0 && ci < g.C) ? y1[m1[e] * g.C + ci] : (uint16_t)0;
+        pos_y[n][e] = (yb & 0x7fff) != 0 && !(yb & 0x8000);
+      }
     }
     // this lane's A position
     const int pa = pos0 + r;
@@ -415,7 +418,7 @@ __global__ __launch_bounds__(SS_NT, 2) void ss_dgrad_kernel(const float* __restr
 }
 
 template <int NCT, int KS>
-int sd_launch(const float* dy2, const uint16_t* wt, const float* y1, float* dy1, const SdGeo& g, hipStream_t st) {
+int sd_launch(const float* dy2, const uint16_t* wt, const uint16_t* y1, float* dy1, const SdGeo& g, hipStream_t st) {
   const size_t lds = (size_t)4 * 32 * NCT * g.ldb * sizeof(uint16_t);
   static bool once = [] {
     (void)hipFuncSetAttribute((const void*)ss_dgrad_kernel<NCT, KS>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -498,7 +501,7 @@ int kdfm_subsample_dgrad_wprep(const float* w2, uint16_t* wt, int64_t C, void* s
   return check_launch("kdfm_subsample_dgrad_wprep");
 }
 
-int kdfm_subsample_conv2_dgrad(const float* dy2, const uint16_t* wt, const float* y1, float* dy1, int64_t B, int64_t T1,
+int kdfm_subsample_conv2_dgrad(const float* dy2, const uint16_t* wt, const uint16_t* y1, float* dy1, int64_t B, int64_t T1,
                                int64_t F1, int64_t C, void* stream) {
   using namespace kdfm;
   KDFM_REQUIRE(dy2 && wt && y1 && dy1, "null pointer");

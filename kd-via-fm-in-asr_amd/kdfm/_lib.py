@@ -89,13 +89,13 @@ SIGNATURES: dict[str, tuple] = {
     "kdfm_lnproj_wprep": (_i32, [_i32, P, P, _i64, _i32, P]),
     "kdfm_ln_qkv_fwd": (_i32, [P, P, P, _f32, P, P, P, P, P, P, P, P, P, P, _i64, _i64, P]),
     "kdfm_ln_glu_fwd": (_i32, [P, P, P, _f32, P, P, P, _i64, P, P, P, P, _i64, _i64, P]),
-    "kdfm_ln_qkv_bwd": (_i32, [P, P, P, P, P, P, P, P, P, P, P, P, P, P, _i64, _i64, P]),
+    "kdfm_ln_qkv_bwd": (_i32, [P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, _i64, _i64, P]),
     "kdfm_ln_glu_bwd": (_i32, [P, P, P, P, P, P, P, P, P, _i64, P, P, P, P, P, _i64, _i64, P]),
     "kdfm_ffn_supported": (_i32, [_i64, _i64]),
     "kdfm_ffn_img_elems": (_i64, [_i64, _i64]),
     "kdfm_ffn_wprep": (_i32, [P, P, P, _i64, _i64, _i32, P]),
     "kdfm_ffn_fwd": (_i32, [P, P, P, _f32, P, P, P, P, P, P, _i64, _i64, _i64, _f32, _f32, _f32, P, C.c_uint64,
-                            C.c_uint64, P]),
+                            C.c_uint64, P, P, _f32, P, P, P, P]),
     "kdfm_ffn_bwd": (_i32, [P, P, P, P, P, P, P, P, P, P, P, P, P, P, _i64, _i64, _i64, _f32, _f32, _f32, P,
                             C.c_uint64, C.c_uint64, P]),
     "kdfm_fm_chain_bwd": (_i32, [P, P, P, P, _i64, P, P, P, P, P, _i64, _i32, _i32, P]),
@@ -118,6 +118,7 @@ SIGNATURES: dict[str, tuple] = {
     "kdfm_specaugment": (_i32, [P, P, P, _i64, _i64, _i64, _i32, _i32, _i32, _f32, P, C.c_uint64, P]),
     "kdfm_im2col_3x3s2": (_i32, [P, P, P, _i64, _i64, _i64, _i64, P]),
     "kdfm_im2col_3x3s2_tm_bf16": (_i32, [P, P, P, _i64, _i64, _i64, _i64, P]),
+    "kdfm_im2col_3x3s2_tm_from_bf16": (_i32, [P, P, P, _i64, _i64, _i64, _i64, P]),
     "kdfm_conv_lengths": (_i32, [P, P, _i64, _i32, _i32, _i32, P]),
     "kdfm_dwsub_conv": (_i32, [P, P, P, P, P, P, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _i32, P]),
     "kdfm_dwsub_conv_dgrad": (_i32, [P, P, P, P, P, P, _i64, _i64, _i64, _i64, _i64, _i64, _i32, _i32, P]),

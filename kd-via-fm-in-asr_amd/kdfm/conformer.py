@@ -179,14 +179,15 @@ def subsampling_forward(cfg, S: EncoderShapes, P, pre, mel, mel_len, len1, len2,
     m2 = len2 if cfg.subsampling_mask else None
     if K.get_math() == "bf16" and C % 8 == 0 and C <= 192:
         # fused: direct conv1 (+ReLU+masks) -> bf16 y1, implicit-GEMM conv2 (+bias+ReLU+mask); no
-        # im2col matrix.  The f32 y1 is kept only for the backward (which rebuilds its im2col).
+        # im2col matrix.  The backward keeps the same bf16 y1: its ReLU' needs only the sign and the conv2
+        # weight gradient's columns are bf16 anyway (an f32 copy would be 2x the bytes, written and re-read).
         y1b = torch.empty(B * S.T1 * S.F1, C, device=dev, dtype=torch.bfloat16)
-        y1 = _empty(B * S.T1 * S.F1, C, dev=dev) if save else None
-        K.subsample_conv1(mel, m0, m1, P[pre + "pre_encode.conv.0.weight"], P[pre + "pre_encode.conv.0.bias"], y1b, y1,
+        K.subsample_conv1(mel, m0, m1, P[pre + "pre_encode.conv.0.weight"], P[pre + "pre_encode.conv.0.bias"], y1b, None,
                           B, S.Tm, cfg.nfilt, C)
         wb = ws["w2_bf16"]
         K.subsample_wprep(P[pre + "pre_encode.conv.2.weight"], wb)
         K.subsample_conv2(y1b, m2, wb, P[pre + "pre_encode.conv.2.bias"], y2, B, S.T1, S.F1, C)
+        y1 = y1b if save else None
         del y1b
     else:
         cols0 = _empty(B * S.T1 * S.F1, 9, dev=dev)
@@ -234,6 +235,8 @@ def subsampling_backward(cfg, S: EncoderShapes, P, G, pre, ctx, dx, len1, *, see
             K.convw_grad(gtm.view(C, 9 * C), G[pre + "pre_encode.conv.2.weight"].view(C, C, 9))
         WGRAD.run(conv2_wgrad, dy2, cols1, dy2h, ctx["y1"])
     else:
+        if ctx["y1"] is not None and ctx["y1"].dtype == torch.bfloat16:   # fused forward kept only the bf16 y1
+            ctx["y1"] = ctx["y1"].float()
         cols1 = ctx["cols1"]
         rebuild = cols1 is None
         if rebuild:   # fused forward: the im2col operand of the conv2 weight gradient is rebuilt on the
@@ -312,8 +315,10 @@ def _rowgemm_fused(rows, d, save):
     return not save or K.wgrad_bf16_supported(rows, d, d)
 
 
-def _ffn_forward(cfg, P, L, which, norm, x, pd, seed, salt, li, site_act, site_out, save, keep, tag):
-    """r_out = r_in + 0.5*drop(W2 drop(silu(W1 LN(r_in) + b1)) + b2) (NeMo ConformerFeedForward half step)."""
+def _ffn_forward(cfg, P, L, which, norm, x, pd, seed, salt, li, site_act, site_out, save, keep, tag, out_ln=None):
+    """r_out = r_in + 0.5*drop(W2 drop(silu(W1 LN(r_in) + b1)) + b2) (NeMo ConformerFeedForward half step).
+    out_ln = (norm name, y): the fused kernel also writes y = LN(r_out) (the layer's norm_out) and keeps
+    its row statistics as m5 / r5; returns (r_out, True) then, else (r_out, False)."""
     rows, d = x.shape
     dev = x.device
     W1, W2 = P[L + which + ".linear1.weight"], P[L + which + ".linear2.weight"]
@@ -324,11 +329,16 @@ def _ffn_forward(cfg, P, L, which, norm, x, pd, seed, salt, li, site_act, site_o
         m = _empty(rows, dev=dev) if save else None
         r = _empty(rows, dev=dev) if save else None
         img = K.ffn_img(W1, W2, fwd_only=not save)
+        oln = None
+        if out_ln is not None:
+            m5, r5 = _empty(rows, dev=dev), _empty(rows, dev=dev)
+            oln = (P[out_ln[0] + ".weight"], P[out_ln[0] + ".bias"], cfg.ln_eps, out_ln[1], m5, r5)
+            keep(m5=m5, r5=r5)
         K.ffn_fwd(x, P[norm + ".weight"], P[norm + ".bias"], cfg.ln_eps, img, P[L + which + ".linear1.bias"],
                   P[L + which + ".linear2.bias"], out, m, r, ff, rscale=0.5, p_act=pd, p_out=pd, seed=seed,
-                  st_act=_stream(salt, li, site_act), st_out=_stream(salt, li, site_out))
+                  st_act=_stream(salt, li, site_act), st_out=_stream(salt, li, site_out), out_ln=oln)
         keep(**{"m" + tag: m, "r" + tag: r, "ffn_img" + tag: img})
-        return out
+        return out, out_ln is not None
     ln, m, r = _ln(x, P, norm, cfg.ln_eps, dev)
     h = _empty(rows, ff, dev=dev) if save else None
     a = _empty(rows, ff, dev=dev)
@@ -337,7 +347,7 @@ def _ffn_forward(cfg, P, L, which, norm, x, pd, seed, salt, li, site_act, site_o
     K.linear(a, W2, P[L + which + ".linear2.bias"], out, epi=_lib.EPI_RESID, R=x, rscale=0.5, dropout_p=pd, seed=seed,
              rng_stream=_stream(salt, li, site_out))
     keep(**{"ln" + tag: ln, "m" + tag: m, "r" + tag: r, "h" + tag: h, "a" + tag: a})
-    return out
+    return out, False
 
 
 def layer_forward(cfg, S: EncoderShapes, P, L, li, x, out, pos_emb, lengths, *, train, seed, salt, save,
@@ -354,8 +364,8 @@ def layer_forward(cfg, S: EncoderShapes, P, L, li, x, out, pos_emb, lengths, *, 
             ctx.update(kw)
 
     # ---- FFN1 (macaron half-step) ----
-    x1 = _ffn_forward(cfg, P, L, "feed_forward1", L + "norm_feed_forward1", x, pd, seed, salt, li, SITE_FF1_ACT,
-                      SITE_FF1_OUT, save, keep, "1")
+    x1, _ = _ffn_forward(cfg, P, L, "feed_forward1", L + "norm_feed_forward1", x, pd, seed, salt, li, SITE_FF1_ACT,
+                         SITE_FF1_OUT, save, keep, "1")
     keep(x=x)
 
     # ---- relative-position MHSA ----
@@ -468,13 +478,15 @@ def layer_forward(cfg, S: EncoderShapes, P, L, li, x, out, pos_emb, lengths, *, 
     del ln3, a, g, y, z
 
     # ---- FFN2 ----
-    x4 = _ffn_forward(cfg, P, L, "feed_forward2", L + "norm_feed_forward2", x3, pd, seed, salt, li, SITE_FF2_ACT,
-                      SITE_FF2_OUT, save, keep, "4")
-    # ---- norm_out -> hooked layer output ----
-    m5 = _empty(rows, dev=dev)
-    r5 = _empty(rows, dev=dev)
-    K.layernorm_fwd(x4, P[L + "norm_out.weight"], P[L + "norm_out.bias"], out, m5, r5, cfg.ln_eps)
-    keep(x3=x3, x4=x4, m5=m5, r5=r5, pd=pd)
+    x4, ln_done = _ffn_forward(cfg, P, L, "feed_forward2", L + "norm_feed_forward2", x3, pd, seed, salt, li,
+                               SITE_FF2_ACT, SITE_FF2_OUT, save, keep, "4", out_ln=(L + "norm_out", out))
+    # ---- norm_out -> hooked layer output (fused into the FFN2 kernel's epilogue when it ran) ----
+    if not ln_done:
+        m5 = _empty(rows, dev=dev)
+        r5 = _empty(rows, dev=dev)
+        K.layernorm_fwd(x4, P[L + "norm_out.weight"], P[L + "norm_out.bias"], out, m5, r5, cfg.ln_eps)
+        keep(m5=m5, r5=r5)
+    keep(x3=x3, x4=x4, pd=pd)
     return ctx
 
 
@@ -553,7 +565,7 @@ def layer_backward(cfg, S: EncoderShapes, P, G, L, li, ctx, dout, pos_emb, lengt
     rows, d, H, dk, T, B = S.rows, S.d, S.h, S.dk, S.T, S.B
     pd = ctx["pd"]
     if ln_buf is None:
-        ln_buf = torch.empty(5, K.layernorm_bwd_ws(rows, d), device=dev)
+        ln_buf = torch.empty(6, K.layernorm_bwd_ws(rows, d), device=dev)
     lng = LnGrads(ln_buf, rows, d)
     # norm_out
     dx4 = _empty(rows, d, dev=dev)
@@ -673,8 +685,6 @@ def layer_backward(cfg, S: EncoderShapes, P, G, L, li, ctx, dout, pos_emb, lengt
 
 def _attn_bwd_tail(P, G, L, ctx, dqkv, dqu, dqv, dppos, pos_emb, dx2, lng, cfg, pd, seed, salt, li, rows, d, dev):
     """Pos-bias / linear_pos / q|k|v projection grads, norm_self_att and FFN1 backward."""
-    K.colsum(dqu, G[L + "self_attn.pos_bias_u"].view(-1))
-    K.colsum(dqv, G[L + "self_attn.pos_bias_v"].view(-1))
     WGRAD.run(lambda: K.linear_dw(dppos, pos_emb, G[L + "self_attn.linear_pos.weight"]), dppos, pos_emb)
     del dppos
     dx1 = _empty(rows, d, dev=dev)
@@ -682,13 +692,17 @@ def _attn_bwd_tail(P, G, L, ctx, dqkv, dqu, dqv, dppos, pos_emb, dx2, lng, cfg, 
         ln2_h = torch.empty(rows, d, device=dev, dtype=torch.bfloat16)
         dqkv_h = torch.empty(rows, 3 * d, device=dev, dtype=torch.bfloat16)
         part = lng.reserve(G[L + "norm_self_att.weight"], G[L + "norm_self_att.bias"])
+        # the positional-bias gradients ride along as one more partial entry of the layer's LN fold
+        part_uv = lng.reserve(G[L + "self_attn.pos_bias_u"].view(-1), G[L + "self_attn.pos_bias_v"].view(-1))
         K.ln_qkv_bwd(dqu, dqv, dqkv, ctx["x1"], ctx["m2"], ctx["r2"], P[L + "norm_self_att.weight"],
                      P[L + "norm_self_att.bias"], K.lnproj_img(K.LNPROJ_QKV, P[L + "self_attn.qkv.weight"], bwd=True),
-                     dx2, dx1, ln2_h, dqkv_h, part)
+                     dx2, dx1, ln2_h, dqkv_h, part, part_uv)
         del dqu, dqv, dqkv, dx2
         WGRAD.run(lambda: K.wgrad_bf16(dqkv_h, ln2_h, G[L + "self_attn.qkv.weight"], db=G[L + "self_attn.qkv.bias"]),
                   dqkv_h, ln2_h)
     else:
+        K.colsum(dqu, G[L + "self_attn.pos_bias_u"].view(-1))
+        K.colsum(dqv, G[L + "self_attn.pos_bias_v"].view(-1))
         K.axpby(dqu, dqv, dqkv[:, :d], 1.0, 1.0)
         del dqu, dqv
         WGRAD.run(lambda: K.linear_dw(dqkv, ctx["ln2"], G[L + "self_attn.qkv.weight"], db=G[L + "self_attn.qkv.bias"]), dqkv, ctx["ln2"])
@@ -759,7 +773,7 @@ def encoder_backward(cfg, S: EncoderShapes, P, G, prefix, run: EncoderRun, dfeat
     i's parameter gradients are all issued (bucketed all-reduce overlap, kdfm/ddp.py)."""
     dout = dfeats[cfg.n_layers - 1]
     if "ln_parts" not in ws:
-        ws["ln_parts"] = torch.empty(5, K.layernorm_bwd_ws(S.rows, S.d), device=dfeats.device)
+        ws["ln_parts"] = torch.empty(6, K.layernorm_bwd_ws(S.rows, S.d), device=dfeats.device)
     for i in range(cfg.n_layers - 1, -1, -1):
         L = f"{prefix}layers.{i}."
         dx = layer_backward(cfg, S, P, G, L, i, run.layers[i], dout, pos_emb, len2, seed=seed, salt=salt,

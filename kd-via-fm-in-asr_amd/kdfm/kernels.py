@@ -600,6 +600,9 @@ def im2col_3x3s2(X, len_in, cols, B, T1, F1, Cc):
 def im2col_3x3s2_tm_bf16(X, len_in, cols, B, T1, F1, Cc):
     T2, F2 = (T1 - 1) // 2 + 1, (F1 - 1) // 2 + 1
     assert cols.shape == (B * T2 * F2, 9 * Cc) and cols.dtype == torch.bfloat16 and X.numel() == B * T1 * F1 * Cc
+    if X.dtype == torch.bfloat16:
+        call("kdfm_im2col_3x3s2_tm_from_bf16", ptr(X), ptr(_i64(len_in)), ptr(cols), B, T1, F1, Cc, _s())
+        return
     call("kdfm_im2col_3x3s2_tm_bf16", ptr(_f32(X)), ptr(_i64(len_in)), ptr(cols), B, T1, F1, Cc, _s())
 
 
@@ -663,7 +666,9 @@ def ffn_img(W1, W2, *, fwd_only=False, out=None):
     ff, d = W1.shape
     assert W2.shape == (d, ff) and W1.is_contiguous() and W2.is_contiguous()
     if _IMGSETS and out is None:
-        img = _registered_img(IMG_FFN, 0, 0, W1) or (_registered_img(IMG_FFN, 0, 1, W1) if fwd_only else None)
+        img = _registered_img(IMG_FFN, 0, 0, W1)
+        if img is None and fwd_only:
+            img = _registered_img(IMG_FFN, 0, 1, W1)
         if img is not None:
             return img
     n = int(_lib.lib().kdfm_ffn_img_elems(d, ff))
@@ -675,14 +680,18 @@ def ffn_img(W1, W2, *, fwd_only=False, out=None):
     return img
 
 
-def ffn_fwd(x, g, b, eps, img, b1, b2, out, mean, rstd, ff, *, rscale, p_act, p_out, seed, st_act, st_out):
-    """out = x + rscale * drop(W2 drop(silu(W1 LN(x) + b1)) + b2) (the fused macaron FFN block)."""
+def ffn_fwd(x, g, b, eps, img, b1, b2, out, mean, rstd, ff, *, rscale, p_act, p_out, seed, st_act, st_out,
+            out_ln=None):
+    """out = x + rscale * drop(W2 drop(silu(W1 LN(x) + b1)) + b2) (the fused macaron FFN block);
+    out_ln = (gamma, beta, eps, y, mean, rstd): also y = LN(out) (the layer's norm_out) in the epilogue."""
     rows, d = x.shape
     assert out.shape == (rows, d) and x.is_contiguous() and out.is_contiguous()
     assert (mean is None) == (rstd is None)
+    og, ob, oeps, oy, om, orr = out_ln if out_ln is not None else (None, None, 0.0, None, None, None)
+    assert oy is None or (oy.shape == (rows, d) and oy.is_contiguous())
     call("kdfm_ffn_fwd", ptr(_f32(x)), ptr(_f32(g)), ptr(_f32(b)), float(eps), ptr(_bf16(img)), ptr(_f32(b1)),
          ptr(_f32(b2)), ptr(out), ptr(mean), ptr(rstd), rows, d, int(ff), float(rscale), float(p_act), float(p_out),
-         ptr(seed), int(st_act), int(st_out), _s())
+         ptr(seed), int(st_act), int(st_out), ptr(og), ptr(ob), float(oeps), ptr(oy), ptr(om), ptr(orr), _s())
 
 
 def ffn_bwd(dout, x, mean, rstd, g, b, img, b1, dx, ln_h, a_h, dl2_h, dh_h, part, ff, *, rscale, p_act, p_out, seed,
@@ -850,13 +859,14 @@ def ln_glu_fwd(x, g, b, eps, img, bias, lengths, T, gout, mean=None, rstd=None, 
          ptr(_i64(lengths)), int(T), ptr(gout), ptr(mean), ptr(rstd), ptr(_bf16(ln_h)), rows, d, _s())
 
 
-def ln_qkv_bwd(dqu, dqv, dqkv, x, mean, rstd, g, b, img, dres, dx, ln_h, dqkv_h, part):
+def ln_qkv_bwd(dqu, dqv, dqkv, x, mean, rstd, g, b, img, dres, dx, ln_h, dqkv_h, part, part_uv=None):
     rows, d = x.shape
     assert dqkv.shape == (rows, 3 * d) and dqkv_h.shape == (rows, 3 * d) and ln_h.shape == (rows, d)
     assert part.numel() >= layernorm_bwd_ws(rows, d)
+    assert part_uv is None or part_uv.numel() >= layernorm_bwd_ws(rows, d)
     call("kdfm_ln_qkv_bwd", ptr(_f32(dqu)), ptr(_f32(dqv)), ptr(_f32(dqkv)), ptr(_f32(x)), ptr(_f32(mean)),
          ptr(_f32(rstd)), ptr(_f32(g)), ptr(_f32(b)), ptr(_bf16(img)), ptr(_f32(dres)), ptr(dx), ptr(_bf16(ln_h)),
-         ptr(_bf16(dqkv_h)), ptr(part), rows, d, _s())
+         ptr(_bf16(dqkv_h)), ptr(part), ptr(part_uv), rows, d, _s())
 
 
 def ln_glu_bwd(dg, x, mean, rstd, g, b, img, bias, lengths, T, dres, dx, ln_h, da_h, part):
@@ -990,7 +1000,8 @@ def subsample_conv2_dgrad(dy2, wt, y1, dy1, B, T1, F1, Cc):
     y1 / dy1 (B T1 F1, C) channels-last f32."""
     T2, F2 = (T1 - 1) // 2 + 1, (F1 - 1) // 2 + 1
     assert dy2.numel() == B * T2 * F2 * Cc and y1.numel() == B * T1 * F1 * Cc and dy1.numel() == y1.numel()
-    call("kdfm_subsample_conv2_dgrad", ptr(_f32(dy2)), ptr(wt), ptr(_f32(y1)), ptr(_f32(dy1)), B, T1, F1, Cc, _s())
+    call("kdfm_subsample_conv2_dgrad", ptr(_f32(dy2)), ptr(wt), ptr(_bf16(y1, "y1 (bf16 conv1 output)")), ptr(_f32(dy1)),
+         B, T1, F1, Cc, _s())
 
 
 # ------------------------------------------------------------------------------------------------

@@ -165,3 +165,33 @@ def test_ffn_unsupported_shape_raises():
     W2 = torch.zeros(64, 256, device="cuda")
     with pytest.raises(_lib.KdfmError):
         K.ffn_img(W1, W2)
+
+
+@pytest.mark.parametrize("rows,d", [(12832, 88), (37, 88), (2049, 176)])
+def test_ffn_block_fused_norm_out(rows, d):
+    """The layer's norm_out LayerNorm computed in the FFN2 epilogue (kdfm_ffn_fwd out_ln): the block
+    output, LN(output) and its row statistics against float64."""
+    from kdfm import kernels as K
+    ff = 4 * d
+    g = torch.Generator().manual_seed(5 * rows + d)
+    P = _params(d, ff, g)
+    x = torch.randn(rows, d, generator=g)
+    g5 = 1.0 + 0.1 * torch.randn(d, generator=g)
+    b5 = 0.1 * torch.randn(d, generator=g)
+    ref_out, _ = _ref(P, x, torch.zeros(rows, d))
+    ref_y = torch.nn.functional.layer_norm(ref_out, (d,), g5.double(), b5.double(), 1e-5)
+    Pc = {k: v.cuda() for k, v in P.items()}
+    out = torch.empty(rows, d, device="cuda")
+    y = torch.empty(rows, d, device="cuda")
+    m5, r5 = torch.empty(rows, device="cuda"), torch.empty(rows, device="cuda")
+    K.ffn_fwd(x.cuda(), Pc["ln_g"], Pc["ln_b"], 1e-5, K.ffn_img(Pc["W1"], Pc["W2"], fwd_only=True), Pc["b1"], Pc["b2"],
+              out, None, None, ff, rscale=0.5, p_act=0.0, p_out=0.0, seed=None, st_act=0, st_out=0,
+              out_ln=(g5.cuda(), b5.cuda(), 1e-5, y, m5, r5))
+    torch.cuda.synchronize()
+    assert _rel(out - x.cuda(), ref_out - x.double()) <= 2e-2
+    # LN of the kernel's own output in float64 (the statistics must match what it normalised)
+    own = torch.nn.functional.layer_norm(out.double().cpu(), (d,), g5.double(), b5.double(), 1e-5)
+    assert _rel(y, own) <= 1e-6
+    assert _rel(y, ref_y) <= 2e-2
+    assert _rel(m5, out.double().mean(1)) <= 1e-6
+    assert _rel(r5, 1.0 / (out.double().var(1, unbiased=False) + 1e-5).sqrt()) <= 1e-5

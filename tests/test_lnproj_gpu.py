@@ -121,8 +121,9 @@ def test_lnproj_backward(kind, B, T):
         dqkv = torch.zeros(rows, 3 * d)
         dqkv[:, d:2 * d] = grads_out["k"].float()
         dqkv[:, 2 * d:] = grads_out["vv"].float()
+        part_uv = torch.empty(K.layernorm_bwd_ws(rows, d), device="cuda")
         K.ln_qkv_bwd(grads_out["qu"].float().cuda(), grads_out["qv"].float().cuda(), dqkv.cuda(), xc, mean, rstd,
-                     Pc["ln_g"], Pc["ln_b"], img, dres.cuda(), dx, lnh, dph, part)
+                     Pc["ln_g"], Pc["ln_b"], img, dres.cuda(), dx, lnh, dph, part, part_uv)
     else:
         K.ln_glu_bwd(grads_out["g"].float().cuda(), xc, mean, rstd, Pc["ln_g"], Pc["ln_b"], img, Pc["b"], lens_c, T,
                      dres.cuda(), dx, lnh, dph, part)
@@ -131,8 +132,15 @@ def test_lnproj_backward(kind, B, T):
     K.wgrad_bf16(dph, lnh, GW, db=Gb)
     Gg = torch.zeros(d, device="cuda")
     Gbeta = torch.zeros(d, device="cuda")
-    K.ln_fold([(part, Gg, Gbeta)], rows, d)
+    entries = [(part, Gg, Gbeta)]
+    if kind == 0:   # positional-bias gradients folded with the LN partials
+        Gu = torch.full((d,), 0.25, device="cuda")
+        Gv = torch.zeros(d, device="cuda")
+        entries.append((part_uv, Gu, Gv))
+    K.ln_fold(entries, rows, d)
     torch.cuda.synchronize()
+    if kind == 0:
+        assert _rel(Gu - 0.25, ref["u"]) <= 1e-5 and _rel(Gv, ref["v"]) <= 1e-5
     assert _rel(dx - dres.cuda(), ref["x"]) <= 2e-2
     assert _rel(GW, ref["W"]) <= 2e-2
     assert _rel(Gb, ref["b"]) <= 2e-2

@@ -105,7 +105,7 @@ def test_subsample_bench_shape_matches_im2col_path(K):
 def test_subsample_conv2_dgrad_direct(K, C, T1, F1):
     """kdfm_subsample_conv2_dgrad (parity-class transposed conv, bf16 MFMA) against the float64
     gradient of conv2d(stride 2, pad 1) wrt its input times ReLU'(y1), on bf16-rounded dy2 / W (the
-    operands the kernel consumes): rel. Frobenius <= 1e-5 (f32 accumulation only); frames where
+    operands the kernel consumes; y1 is passed as the bf16 copy the engine saves, only its sign is read): rel. Frobenius <= 1e-5 (f32 accumulation only); frames where
     y1 == 0 (ReLU'd or masked) get exactly 0."""
     g = torch.Generator().manual_seed(C + T1)
     B = 2
@@ -121,7 +121,7 @@ def test_subsample_conv2_dgrad_direct(K, C, T1, F1):
     wt = torch.empty(K.subsample_dgrad_wprep_elems(C), device="cuda", dtype=torch.bfloat16)
     K.subsample_dgrad_wprep(w2.cuda(), wt)
     dy1 = torch.full((B * T1 * F1, C), float("nan"), device="cuda")
-    K.subsample_conv2_dgrad(dy2.cuda().reshape(-1, C), wt, y1.cuda().reshape(-1, C), dy1, B, T1, F1, C)
+    K.subsample_conv2_dgrad(dy2.cuda().reshape(-1, C), wt, y1.cuda().reshape(-1, C).bfloat16(), dy1, B, T1, F1, C)
     torch.cuda.synchronize()
     got = dy1.cpu().double().view(B, T1, F1, C)
     assert torch.isfinite(got).all()
