@@ -98,10 +98,13 @@ __device__ __forceinline__ float rng_normal(uint64_t seed, uint64_t stream, uint
   return sqrtf(-2.f * __logf(u1)) * __cosf(6.283185307179586f * u2);
 }
 // Dropout decisions are the hottest RNG use (every FFN / attention / residual element of a training
-// step): a 32-bit keyed hash (two lowbias32 rounds, 4 v_mul_lo_u32) instead of the 64-bit splitmix
-// finaliser (12 32-bit multiplies per element).  Round 1 mixes the low index word with the low key
-// word, round 2 the high words, so different (seed, stream) keys give unrelated sequences.
-__host__ __device__ __forceinline__ uint32_t hash32(uint32_t x) {
+// step).  One 32-bit keyed hash per PAIR of elements (2 * pair, 2 * pair + 1): the pair index times an
+// odd per-stream multiplier plus a per-stream offset, then one lowbias32 round (3 v_mul_lo_u32 per pair
+// in all, vs 12 per element for a 64-bit splitmix finaliser); each element of the pair tests 16 of the
+// 32 bits.  keep iff u16 >= ceil(p * 65536): P(drop) = ceil(p * 2^16) / 2^16 (p = 0.1 -> 0.1000061).
+__host__ __device__ __forceinline__ uint32_t drop_pair_bits(uint64_t key, uint64_t pair) {
+  uint32_t x = (uint32_t)pair * ((uint32_t)(key >> 32) | 1u) + (uint32_t)key;
+  x ^= (uint32_t)(pair >> 32);
   x ^= x >> 16;
   x *= 0x21f0aaadu;
   x ^= x >> 15;
@@ -109,13 +112,18 @@ __host__ __device__ __forceinline__ uint32_t hash32(uint32_t x) {
   x ^= x >> 15;
   return x;
 }
-__host__ __device__ __forceinline__ uint32_t drop_bits_k(uint64_t key, uint64_t idx) {
-  const uint32_t h = hash32((uint32_t)idx ^ (uint32_t)key);
-  return hash32(h ^ (uint32_t)(idx >> 32) ^ (uint32_t)(key >> 32));
-}
-// dropout keep test on a precomputed key: keep iff u >= p, u = top 24 hash bits / 2^24 in [0,1)
+__device__ __forceinline__ uint32_t drop_threshold(float p) { return (uint32_t)ceilf(p * 65536.f); }
+// dropout keep test on a precomputed key (rng_key(seed, stream)) for flat element index idx
 __device__ __forceinline__ bool dropout_keep_k(uint64_t key, uint64_t idx, float p) {
-  return (float)(drop_bits_k(key, idx) >> 8) * (1.0f / 16777216.0f) >= p;
+  const uint32_t h = drop_pair_bits(key, idx >> 1);
+  return ((idx & 1) ? (h >> 16) : (h & 0xffffu)) >= drop_threshold(p);
+}
+// the two decisions of elements idx_even and idx_even + 1 (idx_even even) from one hash
+__device__ __forceinline__ void dropout_keep2_k(uint64_t key, uint64_t idx_even, float p, bool& k0, bool& k1) {
+  const uint32_t h = drop_pair_bits(key, idx_even >> 1);
+  const uint32_t t = drop_threshold(p);
+  k0 = (h & 0xffffu) >= t;
+  k1 = (h >> 16) >= t;
 }
 __device__ __forceinline__ bool dropout_keep(uint64_t seed, uint64_t stream, uint64_t idx, float p) {
   return dropout_keep_k(rng_key(seed, stream), idx, p);

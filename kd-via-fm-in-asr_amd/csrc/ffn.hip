@@ -114,6 +114,20 @@ __global__ __launch_bounds__(FF_NT) void ffn_fwd_kernel(FfnFwd a) {
 
   float* bias_s = reinterpret_cast<float*>(reinterpret_cast<char*>(ff_lds) + ffn_stage_bytes<G::FWD, DT>());
   for (int e = threadIdx.x; e < ff + d; e += FF_NT) bias_s[e] = e < ff ? a.b1[e] : a.b2[e - ff];
+  // the residual rows in the accumulator layout for the epilogue, fetched now so their latency hides
+  // behind the chunk loop (narrow d only: 4 DT float4 registers)
+  constexpr bool XPRE = DT <= 3;
+  float4 xres[XPRE ? DT : 1][4];
+  if constexpr (XPRE) {
+#pragma unroll
+    for (int mt = 0; mt < DT; ++mt)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int n0 = mt * 32 + 8 * q + 4 * h;
+        const bool in = par == 0 && ok && n0 < d;
+        xres[mt][q] = *reinterpret_cast<const float4*>(a.x + (in ? row * d + n0 : 0));
+      }
+  }
   stg.store(ff_lds, 0);
   __syncthreads();
   const int nit = (FC + 1) / 2;
@@ -136,10 +150,13 @@ __global__ __launch_bounds__(FF_NT) void ffn_fwd_kernel(FfnFwd a) {
         const float bv[4] = {bb.x, bb.y, bb.z, bb.w};
         float v[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          float t = siluf_(hacc[4 * q + i] + bv[i]);
-          if (a.p_act > 0.f) t = dropout_keep_k(kact, (uint64_t)row * ff + n0 + i, a.p_act) ? t * ks_act : 0.f;
-          v[i] = t;
+        for (int i = 0; i < 4; ++i) v[i] = siluf_(hacc[4 * q + i] + bv[i]);
+        if (a.p_act > 0.f) {
+          bool kp[4];
+          dropout_keep2_k(kact, (uint64_t)row * ff + n0, a.p_act, kp[0], kp[1]);
+          dropout_keep2_k(kact, (uint64_t)row * ff + n0 + 2, a.p_act, kp[2], kp[3]);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v[i] = kp[i] ? v[i] * ks_act : 0.f;
         }
         pk[q][0] = pack_bf16x2(v[0], v[1]);
         pk[q][1] = pack_bf16x2(v[2], v[3]);
@@ -173,12 +190,19 @@ __global__ __launch_bounds__(FF_NT) void ffn_fwd_kernel(FfnFwd a) {
       const int n0 = mt * 32 + 8 * q + 4 * h;
       const bool in = ok && n0 < d;
       const float4 bb = *reinterpret_cast<const float4*>(bias_s + ff + (n0 < d ? n0 : 0));
-      const float4 xr = *reinterpret_cast<const float4*>(a.x + (in ? row * d + n0 : 0));
+      float4 xr;
+      if constexpr (XPRE) xr = xres[mt][q];
+      else xr = *reinterpret_cast<const float4*>(a.x + (in ? row * d + n0 : 0));
       const float bv[4] = {bb.x, bb.y, bb.z, bb.w}, xv[4] = {xr.x, xr.y, xr.z, xr.w};
+      bool kp[4] = {true, true, true, true};
+      if (a.p_out > 0.f) {
+        dropout_keep2_k(kout, (uint64_t)row * d + n0, a.p_out, kp[0], kp[1]);
+        dropout_keep2_k(kout, (uint64_t)row * d + n0 + 2, a.p_out, kp[2], kp[3]);
+      }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         float v = acc[mt][4 * q + i] + red[(mt * 16 + 4 * q + i) * 64 + lane] + bv[i];
-        if (a.p_out > 0.f) v = dropout_keep_k(kout, (uint64_t)row * d + n0 + i, a.p_out) ? v * ks_out : 0.f;
+        if (a.p_out > 0.f) v = kp[i] ? v * ks_out : 0.f;
         o[mt][4 * q + i] = in ? xv[i] + a.rscale * v : 0.f;
       }
       if (in)
@@ -261,10 +285,14 @@ __global__ __launch_bounds__(FF_NT) void ffn_bwd_kernel(FfnBwd a) {
     const float4* p = reinterpret_cast<const float4*>(a.dout + (in ? row * d + k0 : 0));
     const float4 u = p[0], w = p[1];
     float v[8] = {u.x, u.y, u.z, u.w, w.x, w.y, w.z, w.w};
+    bool kp[8] = {true, true, true, true, true, true, true, true};
+    if (a.p_out > 0.f)
+#pragma unroll
+      for (int j = 0; j < 8; j += 2) dropout_keep2_k(kout, (uint64_t)row * d + k0 + j, a.p_out, kp[j], kp[j + 1]);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float t = in ? v[j] * a.rscale : 0.f;
-      if (a.p_out > 0.f) t = dropout_keep_k(kout, (uint64_t)row * d + k0 + j, a.p_out) ? t * ks_out : 0.f;
+      if (a.p_out > 0.f) t = kp[j] ? t * ks_out : 0.f;
       v[j] = t;
     }
     bd[ks] = pack_bf16x8<bf16x8>(v);
@@ -305,15 +333,19 @@ __global__ __launch_bounds__(FF_NT) void ffn_bwd_kernel(FfnBwd a) {
         const float4 bb = *reinterpret_cast<const float4*>(bias_s + n0);
         const float bv[4] = {bb.x, bb.y, bb.z, bb.w};
         float av[4], dv[4];
+        bool kq[4] = {true, true, true, true};
+        if (a.p_act > 0.f) {
+          dropout_keep2_k(kact, (uint64_t)row * ff + n0, a.p_act, kq[0], kq[1]);
+          dropout_keep2_k(kact, (uint64_t)row * ff + n0 + 2, a.p_act, kq[2], kq[3]);
+        }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const float hv = hacc[4 * q + i] + bv[i];
           const float sg = sigmoidf_(hv);
           float s = hv * sg, gv = gacc[4 * q + i];
           if (a.p_act > 0.f) {
-            const bool kp = dropout_keep_k(kact, (uint64_t)row * ff + n0 + i, a.p_act);
-            s = kp ? s * ks_act : 0.f;
-            gv = kp ? gv * ks_act : 0.f;
+            s = kq[i] ? s * ks_act : 0.f;
+            gv = kq[i] ? gv * ks_act : 0.f;
           }
           av[i] = s;
           dv[i] = gv * (sg * (1.f + hv * (1.f - sg)));

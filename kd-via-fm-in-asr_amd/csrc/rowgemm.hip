@@ -77,10 +77,14 @@ __global__ __launch_bounds__(RG_NT) void rowgemm_kernel(RgArgs a) {
     float v[8] = {u.x, u.y, u.z, u.w, w.x, w.y, w.z, w.w};
     if constexpr (PRO == PRO_DROP) {
       const float ks_in = a.s_in / (1.f - a.p_in);
+      bool kp[8] = {true, true, true, true, true, true, true, true};
+      if (a.p_in > 0.f)
+#pragma unroll
+        for (int j = 0; j < 8; j += 2) dropout_keep2_k(kin, (uint64_t)row * d + k0 + j, a.p_in, kp[j], kp[j + 1]);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         float t = v[j] * (a.p_in > 0.f ? ks_in : a.s_in);
-        if (a.p_in > 0.f) t = dropout_keep_k(kin, (uint64_t)row * d + k0 + j, a.p_in) ? t : 0.f;
+        if (a.p_in > 0.f) t = kp[j] ? t : 0.f;
         v[j] = t;
       }
     } else if constexpr (PRO == PRO_BNSILU) {
@@ -118,10 +122,15 @@ __global__ __launch_bounds__(RG_NT) void rowgemm_kernel(RgArgs a) {
         const float4 rr = *reinterpret_cast<const float4*>(a.R + row * d + n0);
         const float bv[4] = {bb.x, bb.y, bb.z, bb.w}, rv[4] = {rr.x, rr.y, rr.z, rr.w};
         const float ks_out = 1.f / (1.f - a.p_out);
+        bool kp[4] = {true, true, true, true};
+        if (a.p_out > 0.f) {
+          dropout_keep2_k(kout, (uint64_t)row * d + n0, a.p_out, kp[0], kp[1]);
+          dropout_keep2_k(kout, (uint64_t)row * d + n0 + 2, a.p_out, kp[2], kp[3]);
+        }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           float v = o[i] + bv[i];
-          if (a.p_out > 0.f) v = dropout_keep_k(kout, (uint64_t)row * d + n0 + i, a.p_out) ? v * ks_out : 0.f;
+          if (a.p_out > 0.f) v = kp[i] ? v * ks_out : 0.f;
           o[i] = rv[i] + a.rscale * v;
         }
       }
