@@ -41,6 +41,11 @@ ROUTE_KERNELS = {"generic": ("gemm_kernel",), "skinny": ("sk_fwd_kernel", "skd_f
                  "rowstream_fwd": ("rs_fwd_kernel",), "wide_wgrad": ("rs_wgrad_kernel", "rs_fold_kernel"),
                  "split_fold": ("gemm_kernel", "rs_fold_kernel"), "slab_conv": ("skc_fwd_kernel",),
                  "wgrad_rows": ("wgr_kernel", "wgr_fold_kernel")}
+# the fused kernels traced outside kdfm_gemm (kernels._traced tags) -> kernel-name stems
+FAMILY_KERNELS = {"ffn_fwd": ("ffn_fwd_kernel",), "ffn_bwd": ("ffn_bwd_kernel",),
+                  "wgrad_bf16": ("wgr_kernel", "wgr_fold_kernel"), "attn_fwd": ("relpos_attn_fwd_kernel",),
+                  "attn_bwd": ("attn_bwd_dq_kernel", "attn_bwd_dkv_kernel", "attn_bwd_dpos_kernel",
+                               "attn_rowdot_kernel", "attn_dpos_fold_kernel")}
 # FLOPs per utterance of one training step (B=32, 16.0 s) and of its attention +
 # FFN dense contractions (student fwd+bwd + teacher fwd), the north-star MFMA roofline subject
 STEP_GFLOP_PER_UTT = 62.6
@@ -183,7 +188,8 @@ def main():
     # live per-kernel timing: one instrumented eager step right after the timed steps; every
     # kdfm_gemm launch (keyed by the kernel family libkdfm routed it to), the frontend and the
     # depthwise convs bracketed by HIP events on the stream they run on
-    trace = K.Trace(["*", "ffn_up", "frontend", "dwconv"])
+    trace = K.Trace(["*", "ffn_up", "frontend", "dwconv", "ffn_fwd", "ffn_bwd", "wgrad_bf16", "attn_fwd",
+                     "attn_bwd"])
     with trace:
         eng.train_step(wav, wl, tg, tl, ar)
     torch.cuda.synchronize()
@@ -205,6 +211,16 @@ def main():
             return n, ms, gbps, tfl
 
         routes = {k[5:]: v for k, v in tsum.items() if k.startswith("gemm:")}
+        # the row-parallel weight gradients run both inside kdfm_gemm (f32 operands) and as kdfm_wgrad_bf16
+        # (bf16 operands): one kernel family
+        if "wgrad_bf16" in tsum:
+            w = dict(routes.get("wgrad_rows", empty))
+            for k in ("launches", "ms_total", "flops_total", "bytes_total"):
+                w[k] = w.get(k, 0) + tsum["wgrad_bf16"][k]
+            routes["wgrad_rows"] = w
+        for fam in ("ffn_fwd", "ffn_bwd", "attn_fwd", "attn_bwd"):
+            if fam in tsum:
+                routes[fam] = tsum[fam]
         by_route = {}
         for r, t in sorted(routes.items(), key=lambda kv: -kv[1]["ms_total"]):
             n, ms, gbps, tfl = rate(t)
@@ -223,11 +239,12 @@ def main():
         else:
             roof = {"bound": "mfma", "achieved": round(tfl, 2), "peak": bf16_peak, "unit": "TFLOP/s",
                     "frac": round(tfl / bf16_peak, 4)}
-        roof.update({"traffic": pmc_traffic(ROUTE_KERNELS.get(dom, (dom,))),
+        stems = FAMILY_KERNELS.get(dom) or ROUTE_KERNELS.get(dom, (dom,))
+        roof.update({"traffic": pmc_traffic(stems),
                      "traffic_source": os.path.relpath(PMC_TRAFFIC, ROOT) + " (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, "
                                        "pooled over the family's kernels, bytes per launch)",
-                     "kernel": f"kdfm_gemm {dom} family ({', '.join(ROUTE_KERNELS.get(dom, (dom,)))}): the kernel "
-                               f"family with the largest aggregated time of the step",
+                     "kernel": f"{dom} family ({', '.join(stems)}): the kernel family with the largest aggregated "
+                               f"time of the step (kdfm_gemm routes + the fused kernels, HIP events on their streams)",
                      "launches": n, "avg_ms": round(ms, 5), "bytes_per_launch": round(dt["bytes_total"] / n, 1),
                      "flops_per_launch": round(dt["flops_total"] / n, 1),
                      "arith_intensity_flop_per_byte": round(intensity, 2)})
@@ -256,7 +273,7 @@ def main():
                        "global_batch": world * args.batch, "seq_len": args.samples,
                        "frames_subsampled": (args.samples // 160) // 4 + 1, "parallelism": f"dp{world}"},
             "roofline": roof,
-            "roofline_by_gemm_family": by_route,
+            "roofline_by_family": by_route,
             "roofline_mfma_ffn": {"bound": "mfma", "kernel": "kdfm_gemm ffn_up (Conformer FFN d->4d, SiLU+dropout)",
                                   "achieved": round(f_tfl, 3), "peak": bf16_peak, "unit": "TFLOP/s",
                                   "frac": round(f_tfl / bf16_peak, 5), "launches": f_n, "avg_ms": round(f_ms, 5)},

@@ -174,6 +174,16 @@ int kdfm_wgrad_bf16_conv(const uint16_t* dY, const uint16_t* X, float* dW, int64
  * forward).  No T x T intermediate in HBM; deterministic (ordered chunk fold, no atomics).  Head
  * dim d/H <= 48.  ws: kdfm_relpos_attn_bwd_ws floats. */
 int64_t kdfm_relpos_attn_bwd_ws(int64_t B, int64_t H, int64_t T, int64_t d);
+/* The same backward issued in parts (a caller may put them on different streams): ROWDOT writes
+ * D_i into ws; DQ, DKV and DPOS (+ its ordered fold) read it, so they must be ordered after ROWDOT
+ * (same ws); DQ writes dqu / dqv, DKV dqkv[:, d:], DPOS dpos (the ws tail, which DQ / DKV do not touch). */
+enum { KDFM_ATTN_BWD_ROWDOT = 1, KDFM_ATTN_BWD_DQ = 2, KDFM_ATTN_BWD_DKV = 4, KDFM_ATTN_BWD_DPOS = 8,
+       KDFM_ATTN_BWD_ALL = 15 };
+int kdfm_relpos_attn_bwd_parts(const float* dO, const float* O, const float* qu, const float* qv, const float* qkv,
+                               const float* pos, const float* P, const int64_t* lengths, float* dqu, float* dqv,
+                               float* dqkv, float* dpos, float* ws, int64_t ws_len, int64_t B, int64_t H, int64_t T,
+                               int64_t d, float scale, float dropout_p, const uint64_t* seed, uint64_t rng_stream,
+                               int32_t parts, void* stream);
 int kdfm_relpos_attn_bwd(const float* dO, const float* O, const float* qu, const float* qv, const float* qkv,
                          const float* pos, const float* P, const int64_t* lengths, float* dqu, float* dqv, float* dqkv,
                          float* dpos,
@@ -420,6 +430,16 @@ int kdfm_subsample_conv2(const uint16_t* y1b, const int64_t* len2, const uint16_
  * (B T2 F2, 9C) columns + col2im (conformer_encoder.py:381-390). */
 int64_t kdfm_subsample_dgrad_wprep_elems(int64_t C);
 int kdfm_subsample_dgrad_wprep(const float* w2, uint16_t* wt, int64_t C, void* stream);
+/* The same data gradient with ConvSubsampling conv0's weight gradient fused into its epilogue (the
+ * striding path: conv0 = Conv2d(1 -> C, 3x3, stride 2, pad) over the (B, Tm, Fm) mel frames, frames
+ * t >= mel_len[b] read as zero; mel_len may be null): dw0 (C, 9) += sum dy1 x_patch, db0 (C) += sum dy1,
+ * from per-workgroup partials in ws (kdfm_subsample_conv2_dgrad_w0_ws floats) folded in workgroup order.
+ * dy1 may be null (not written).  Requires B T1 F1 < 2^24. */
+int64_t kdfm_subsample_conv2_dgrad_w0_ws(int64_t B, int64_t T1, int64_t F1, int64_t C);
+int kdfm_subsample_conv2_dgrad_w0(const float* dy2, const uint16_t* wt, const uint16_t* y1, float* dy1, int64_t B,
+                                  int64_t T1, int64_t F1, int64_t C, const float* mel, const int64_t* mel_len,
+                                  int64_t Tm, int64_t Fm, int64_t pad, float* dw0, float* db0, float* ws,
+                                  int64_t ws_len, void* stream);
 int kdfm_subsample_conv2_dgrad(const float* dy2, const uint16_t* wt, const uint16_t* y1, float* dy1, int64_t B, int64_t T1,
                                int64_t F1, int64_t C, void* stream);
 

@@ -589,8 +589,20 @@ int kdfm_relpos_attn_bwd(const float* dO, const float* O, const float* qu, const
                          float* dpos,
                          float* ws, int64_t ws_len, int64_t B, int64_t H, int64_t T, int64_t d, float scale,
                          float dropout_p, const uint64_t* seed, uint64_t rng_stream, void* stream) {
+  return kdfm_relpos_attn_bwd_parts(dO, O, qu, qv, qkv, pos, P, lengths, dqu, dqv, dqkv, dpos, ws, ws_len, B, H, T, d,
+                                    scale, dropout_p, seed, rng_stream, KDFM_ATTN_BWD_ALL, stream);
+}
+
+int kdfm_relpos_attn_bwd_parts(const float* dO, const float* O, const float* qu, const float* qv, const float* qkv,
+                               const float* pos, const float* P, const int64_t* lengths, float* dqu, float* dqv,
+                               float* dqkv, float* dpos, float* ws, int64_t ws_len, int64_t B, int64_t H, int64_t T,
+                               int64_t d, float scale, float dropout_p, const uint64_t* seed, uint64_t rng_stream,
+                               int32_t parts, void* stream) {
   using namespace kdfm;
-  KDFM_REQUIRE(dO && O && qu && qv && qkv && pos && P && dqu && dqv && dqkv && dpos && ws, "null pointer");
+  KDFM_REQUIRE(dO && O && qu && qv && qkv && pos && P && ws, "null pointer");
+  KDFM_REQUIRE(!(parts & KDFM_ATTN_BWD_DQ) || (dqu && dqv), "dq part needs dqu / dqv");
+  KDFM_REQUIRE(!(parts & KDFM_ATTN_BWD_DKV) || dqkv, "dkv part needs dqkv");
+  KDFM_REQUIRE(!(parts & KDFM_ATTN_BWD_DPOS) || dpos, "dpos part needs dpos");
   KDFM_REQUIRE(H > 0 && d % H == 0, "d must be a multiple of H");
   const int64_t dk = d / H;
   KDFM_REQUIRE(dk <= 48 && dk % 4 == 0, "head dim must be a multiple of 4 and <= 48");
@@ -602,22 +614,32 @@ int kdfm_relpos_attn_bwd(const float* dO, const float* O, const float* qu, const
   if (B == 0) return KDFM_OK;
   AbP p{};
   p.dO = dO; p.qu = qu; p.qv = qv; p.k = qkv + d; p.v = qkv + 2 * d; p.pos = pos; p.P = P; p.lens = lengths;
-  p.dqu = dqu; p.dqv = dqv; p.rsum = ws; p.dk = dqkv + d; p.dv = dqkv + 2 * d; p.dpos_part = ws + B * H * T;
+  p.dqu = dqu; p.dqv = dqv; p.rsum = ws; p.dpos_part = ws + B * H * T;
+  p.dk = dqkv ? dqkv + d : nullptr;
+  p.dv = dqkv ? dqkv + 2 * d : nullptr;
   p.B = B; p.H = H; p.T = T; p.d = d; p.dkh = dk; p.ldq = d; p.ldkv = 3 * d;
   p.scale = scale; p.p_drop = dropout_p; p.seed = seed; p.rng_stream = rng_stream;
   const int chunks = (int)(B < DPOS_MAX_CHUNKS ? B : DPOS_MAX_CHUNKS);
   p.bpc = (int)ceil_div(B, chunks);
   hipStream_t st = as_stream(stream);
-  hipLaunchKernelGGL(attn_rowdot_kernel, dim3((unsigned)ceil_div(B * T * H, 4)), dim3(256), 0, st, dO, O, p.rsum, B, H,
-                     T, d, (int)dk);
-  int rc0 = check_launch("kdfm_relpos_attn_bwd(rowdot)");
-  if (rc0) return rc0;
-  hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3((unsigned)ceil_div(T, BQ), (unsigned)(B * H)), dim3(256), 0, st, p);
-  int rc = check_launch("kdfm_relpos_attn_bwd(dq)");
-  if (rc) return rc;
-  hipLaunchKernelGGL(attn_bwd_dkv_kernel, dim3((unsigned)ceil_div(T, BK), (unsigned)(B * H)), dim3(256), 0, st, p);
-  rc = check_launch("kdfm_relpos_attn_bwd(dkv)");
-  if (rc) return rc;
+  int rc = KDFM_OK;
+  if (parts & KDFM_ATTN_BWD_ROWDOT) {
+    hipLaunchKernelGGL(attn_rowdot_kernel, dim3((unsigned)ceil_div(B * T * H, 4)), dim3(256), 0, st, dO, O, p.rsum, B,
+                       H, T, d, (int)dk);
+    rc = check_launch("kdfm_relpos_attn_bwd(rowdot)");
+    if (rc) return rc;
+  }
+  if (parts & KDFM_ATTN_BWD_DQ) {
+    hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3((unsigned)ceil_div(T, BQ), (unsigned)(B * H)), dim3(256), 0, st, p);
+    rc = check_launch("kdfm_relpos_attn_bwd(dq)");
+    if (rc) return rc;
+  }
+  if (parts & KDFM_ATTN_BWD_DKV) {
+    hipLaunchKernelGGL(attn_bwd_dkv_kernel, dim3((unsigned)ceil_div(T, BK), (unsigned)(B * H)), dim3(256), 0, st, p);
+    rc = check_launch("kdfm_relpos_attn_bwd(dkv)");
+    if (rc) return rc;
+  }
+  if (!(parts & KDFM_ATTN_BWD_DPOS)) return KDFM_OK;
   const int64_t npos = 2 * T - 1;
   hipLaunchKernelGGL(attn_bwd_dpos_kernel, dim3((unsigned)ceil_div(npos, 64), (unsigned)H, (unsigned)chunks),
                      dim3(256), 0, st, p);

@@ -266,6 +266,10 @@ struct SdGeo {
   int B, T1, F1, C, T2, F2, Cp, ldb;
   int64_t npos[4];   // positions per class (class = 2 * (t1 % 2) + f1 % 2)
   int64_t wg0[5];    // first workgroup of each class; wg0[4] = grid size
+  // fused conv0 weight gradient (wpart != null): conv0 = Conv2d(1 -> C, 3x3, stride 2, pad) over the
+  // (B, Tm, Fm) mel frames (rows t >= mel_len[b] read as 0); per-workgroup partials
+  // wpart[wg][C * 9 + C] = (sum dy1 x_patch | sum dy1), folded in workgroup order on the host side
+  const float* mel; const int64_t* mel_len; int Tm, Fm, pad; float* wpart;
 };
 
 __global__ __launch_bounds__(256) void ss_dgrad_wprep_kernel(const float* __restrict__ W, uint16_t* __restrict__ wt,
@@ -341,20 +345,25 @@ __global__ __launch_bounds__(SS_NT, 2) void ss_dgrad_kernel(const float* __restr
       }
     }
   };
+  float wacc[NCT][10];
+#pragma unroll
+  for (int n = 0; n < NCT; ++n)
+#pragma unroll
+    for (int k = 0; k < 10; ++k) wacc[n][k] = 0.f;
   // each workgroup walks SD_TPW position tiles of its class with the staged tap slabs
   const int tile0 = (int)(blockIdx.x - g.wg0[cls]) * SD_TPW;
   for (int tile = tile0, tend = min(tile0 + SD_TPW, ntile); tile < tend; ++tile) {
     const int pos0 = tile * (32 * SS_WAVES) + wave * 32;
     // epilogue rows first (positions 8 (e/4) + 4 h + e % 4 of the wave tile): their ReLU' operands are
     // loaded before the MFMAs so the latency hides behind them
-    int64_t m1[16];
+    int m1[16];           // y1 position (< 2^31, checked on the host) or -1
     {
       int b, i, j;
       decode(pos0 + 4 * h, b, i, j);
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
         const int pm = pos0 + 8 * (e >> 2) + 4 * h + (e & 3);
-        m1[e] = pm < npos ? ((int64_t)b * g.T1 + 2 * i + pt) * g.F1 + 2 * j + pf : -1;
+        m1[e] = pm < npos ? (b * g.T1 + 2 * i + pt) * g.F1 + 2 * j + pf : -1;
         advance(b, i, j, (e & 3) == 3 ? 5 : 1);   // next row of the C layout: +1, or +5 to the next group of 8
       }
     }
@@ -364,7 +373,7 @@ __global__ __launch_bounds__(SS_NT, 2) void ss_dgrad_kernel(const float* __restr
       const int ci = 32 * n + r;
 #pragma unroll
       for (int e = 0; e < 16; ++e) {   // ReLU' from the sign of the bf16 y1 (bf16 RNE keeps the sign and zero)
-        const uint16_t yb = (m1[e] >= 0 && ci < g.C) ? y1[m1[e] * g.C + ci] : (uint16_t)0;
+        const uint16_t yb = (m1[e] >= 0 && ci < g.C) ? y1[(int64_t)m1[e] * g.C + ci] : (uint16_t)0;
         pos_y[n][e] = (yb & 0x7fff) != 0 && !(yb & 0x8000);
       }
     }
@@ -404,22 +413,85 @@ __global__ __launch_bounds__(SS_NT, 2) void ss_dgrad_kernel(const float* __restr
           acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[s], b, acc[n], 0, 0, 0);
         }
     }
+    if (dy1) {
 #pragma unroll
-    for (int n = 0; n < NCT; ++n) {
-      const int ci = 32 * n + r;
-      if (ci >= g.C) continue;
+      for (int n = 0; n < NCT; ++n) {
+        const int ci = 32 * n + r;
+        if (ci >= g.C) continue;
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        if (m1[e] < 0) continue;
-        dy1[m1[e] * g.C + ci] = pos_y[n][e] ? acc[n][e] : 0.f;
+        for (int e = 0; e < 16; ++e) {
+          if (m1[e] < 0) continue;
+          dy1[(int64_t)m1[e] * g.C + ci] = pos_y[n][e] ? acc[n][e] : 0.f;
+        }
       }
     }
+    if (g.wpart) {
+      // conv0 weight gradient of this tile: wacc[n][tap] += dy1 x_patch[tap], wacc[n][9] += dy1 (the
+      // patch values are the same for the 32 lanes of a half-wave: broadcast loads)
+      const float invF1 = 1.f / (float)g.F1, invT1 = 1.f / (float)g.T1;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        // (b, t1, f1) of the y1 position (exact float-reciprocal division: positions < 2^24, host-checked)
+        const int mp = m1[e] < 0 ? 0 : m1[e];
+        int q = (int)((float)mp * invF1);
+        q -= q * g.F1 > mp;
+        q += (q + 1) * g.F1 <= mp;
+        const int f1 = mp - q * g.F1;
+        int b = (int)((float)q * invT1);
+        b -= b * g.T1 > q;
+        b += (b + 1) * g.T1 <= q;
+        const int t1 = q - b * g.T1;
+        const int t0 = 2 * t1 - g.pad, f0 = 2 * f1 - g.pad;
+        const int tl = m1[e] < 0 ? 0 : (g.mel_len ? (int)min((int64_t)g.Tm, g.mel_len[b]) : g.Tm);
+        const float* mrow = g.mel + ((int64_t)b * g.Tm + t0) * g.Fm + f0;
+        float xp[9];
+#pragma unroll
+        for (int tp = 0; tp < 9; ++tp) {
+          const int tt = t0 + tp / 3, ff = f0 + tp % 3;
+          xp[tp] = (tt >= 0 && tt < tl && ff >= 0 && ff < g.Fm) ? mrow[(tp / 3) * g.Fm + tp % 3] : 0.f;
+        }
+#pragma unroll
+        for (int n = 0; n < NCT; ++n) {
+          const float v = pos_y[n][e] ? acc[n][e] : 0.f;
+#pragma unroll
+          for (int tp = 0; tp < 9; ++tp) wacc[n][tp] += v * xp[tp];
+          wacc[n][9] += v;
+        }
+      }
+    }
+  }
+  if (!g.wpart) return;
+  // per-workgroup partial: lanes r / r + 32 hold the same channels, then the 8 waves in order
+#pragma unroll
+  for (int n = 0; n < NCT; ++n)
+#pragma unroll
+    for (int k = 0; k < 10; ++k) wacc[n][k] += __shfl_xor(wacc[n][k], 32, 64);
+  __syncthreads();   // the tap slabs are no longer read: reuse the LDS
+  float* red = reinterpret_cast<float*>(sd_lds);
+  if (h == 0) {
+#pragma unroll
+    for (int n = 0; n < NCT; ++n)
+#pragma unroll
+      for (int k = 0; k < 10; ++k) red[(wave * NCT * 10 + n * 10 + k) * 32 + r] = wacc[n][k];
+  }
+  __syncthreads();
+  float* wp = g.wpart + (int64_t)blockIdx.x * g.C * 10;
+  for (int o = threadIdx.x; o < NCT * 32 * 10; o += SS_NT) {
+    const int n = o / 320, rem = o % 320, k = rem / 32, rr = rem % 32;
+    const int ci = 32 * n + rr;
+    if (ci >= g.C) continue;
+    float v = 0.f;
+    for (int w = 0; w < SS_WAVES; ++w) v += red[(w * NCT * 10 + n * 10 + k) * 32 + rr];
+    if (k < 9) wp[ci * 9 + k] = v;
+    else wp[g.C * 9 + ci] = v;
   }
 }
 
 template <int NCT, int KS>
 int sd_launch(const float* dy2, const uint16_t* wt, const uint16_t* y1, float* dy1, const SdGeo& g, hipStream_t st) {
-  const size_t lds = (size_t)4 * 32 * NCT * g.ldb * sizeof(uint16_t);
+  size_t lds = (size_t)4 * 32 * NCT * g.ldb * sizeof(uint16_t);
+  const size_t red = (size_t)SS_WAVES * NCT * 10 * 32 * sizeof(float);   // fused conv0 wgrad reduction
+  if (g.wpart && red > lds) lds = red;
   static bool once = [] {
     (void)hipFuncSetAttribute((const void*)ss_dgrad_kernel<NCT, KS>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
@@ -501,13 +573,9 @@ int kdfm_subsample_dgrad_wprep(const float* w2, uint16_t* wt, int64_t C, void* s
   return check_launch("kdfm_subsample_dgrad_wprep");
 }
 
-int kdfm_subsample_conv2_dgrad(const float* dy2, const uint16_t* wt, const uint16_t* y1, float* dy1, int64_t B, int64_t T1,
-                               int64_t F1, int64_t C, void* stream) {
-  using namespace kdfm;
-  KDFM_REQUIRE(dy2 && wt && y1 && dy1, "null pointer");
-  KDFM_REQUIRE(C % 8 == 0 && B > 0 && T1 > 0 && F1 > 0, "C must be a multiple of 8");
-  KDFM_REQUIRE(((((uintptr_t)dy2) | ((uintptr_t)wt)) & 15) == 0, "dy2 / wt must be 16-byte aligned");
-  SdGeo g;
+namespace kdfm {
+namespace {
+int sd_geo(SdGeo& g, int64_t B, int64_t T1, int64_t F1, int64_t C) {
   g.B = (int)B; g.T1 = (int)T1; g.F1 = (int)F1; g.C = (int)C;
   g.T2 = (int)((T1 - 1) / 2 + 1); g.F2 = (int)((F1 - 1) / 2 + 1);
   g.Cp = (int)(ceil_div(C, 16) * 16);
@@ -518,15 +586,61 @@ int kdfm_subsample_conv2_dgrad(const float* dy2, const uint16_t* wt, const uint1
     g.npos[c] = B * ((T1 - pt + 1) / 2) * ((F1 - pf + 1) / 2);
     g.wg0[c + 1] = g.wg0[c] + ceil_div(ceil_div(g.npos[c], 32 * SS_WAVES), SD_TPW);
   }
-  KDFM_REQUIRE(g.wg0[4] < (1ll << 31) && g.npos[0] < (1ll << 30), "too large");
-  const int nct = (int)ceil_div(C, 32), ks = g.Cp / 16;
-  hipStream_t st = as_stream(stream);
+  g.mel = nullptr; g.mel_len = nullptr; g.Tm = g.Fm = g.pad = 0; g.wpart = nullptr;
+  return 0;
+}
+int sd_dispatch(const float* dy2, const uint16_t* wt, const uint16_t* y1, float* dy1, const SdGeo& g, hipStream_t st) {
+  const int nct = (int)ceil_div(g.C, 32), ks = g.Cp / 16;
   if (nct == 3 && ks == 6) return sd_launch<3, 6>(dy2, wt, y1, dy1, g, st);    // d = 88 / 96
   if (nct == 1 && ks == 1) return sd_launch<1, 1>(dy2, wt, y1, dy1, g, st);    // test sizes
   if (nct == 1 && ks == 2) return sd_launch<1, 2>(dy2, wt, y1, dy1, g, st);
   if (nct == 2 && ks == 4) return sd_launch<2, 4>(dy2, wt, y1, dy1, g, st);
   set_error("kdfm_subsample_conv2_dgrad: unsupported channel count");
   return KDFM_EUNSUPPORTED;
+}
+}  // namespace
+}  // namespace kdfm
+
+int64_t kdfm_subsample_conv2_dgrad_w0_ws(int64_t B, int64_t T1, int64_t F1, int64_t C) {
+  kdfm::SdGeo g;
+  kdfm::sd_geo(g, B, T1, F1, C);
+  return g.wg0[4] * C * 10;
+}
+
+int kdfm_subsample_conv2_dgrad_w0(const float* dy2, const uint16_t* wt, const uint16_t* y1, float* dy1, int64_t B,
+                                  int64_t T1, int64_t F1, int64_t C, const float* mel, const int64_t* mel_len,
+                                  int64_t Tm, int64_t Fm, int64_t pad, float* dw0, float* db0, float* ws,
+                                  int64_t ws_len, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(dy2 && wt && y1 && mel && dw0 && db0 && ws, "null pointer");
+  KDFM_REQUIRE(C % 8 == 0 && B > 0 && T1 > 0 && F1 > 0, "C must be a multiple of 8");
+  KDFM_REQUIRE(((((uintptr_t)dy2) | ((uintptr_t)wt)) & 15) == 0, "dy2 / wt must be 16-byte aligned");
+  KDFM_REQUIRE(T1 == (Tm + 2 * pad - 3) / 2 + 1 && F1 == (Fm + 2 * pad - 3) / 2 + 1, "conv0 geometry");
+  SdGeo g;
+  sd_geo(g, B, T1, F1, C);
+  KDFM_REQUIRE(g.wg0[4] < (1ll << 31) && B * T1 * F1 < (1ll << 24) && B * Tm * Fm < (1ll << 31),
+               "too large for the fused conv0 weight gradient (y1 positions < 2^24)");
+  KDFM_REQUIRE(ws_len >= g.wg0[4] * C * 10, "workspace too small (kdfm_subsample_conv2_dgrad_w0_ws)");
+  g.mel = mel; g.mel_len = mel_len; g.Tm = (int)Tm; g.Fm = (int)Fm; g.pad = (int)pad; g.wpart = ws;
+  hipStream_t st = as_stream(stream);
+  int rc = sd_dispatch(dy2, wt, y1, dy1, g, st);
+  if (rc) return rc;
+  // fixed-order fold of the per-workgroup partials: dW0 (C, 9) += sum_wg, db0 (C) += sum_wg
+  rc = launch_colsum(ws, dw0, g.wg0[4], C * 9, C * 10, 1.f, st);
+  if (rc) return rc;
+  return launch_colsum(ws + C * 9, db0, g.wg0[4], C, C * 10, 1.f, st);
+}
+
+int kdfm_subsample_conv2_dgrad(const float* dy2, const uint16_t* wt, const uint16_t* y1, float* dy1, int64_t B, int64_t T1,
+                               int64_t F1, int64_t C, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(dy2 && wt && y1 && dy1, "null pointer");
+  KDFM_REQUIRE(C % 8 == 0 && B > 0 && T1 > 0 && F1 > 0, "C must be a multiple of 8");
+  KDFM_REQUIRE(((((uintptr_t)dy2) | ((uintptr_t)wt)) & 15) == 0, "dy2 / wt must be 16-byte aligned");
+  SdGeo g;
+  sd_geo(g, B, T1, F1, C);
+  KDFM_REQUIRE(g.wg0[4] < (1ll << 31) && B * T1 * F1 < (1ll << 31), "too large");
+  return sd_dispatch(dy2, wt, y1, dy1, g, as_stream(stream));
 }
 
 }  // extern "C"

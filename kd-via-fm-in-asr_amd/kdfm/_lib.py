@@ -77,6 +77,8 @@ SIGNATURES: dict[str, tuple] = {
     "kdfm_relpos_attn_bwd_ws": (_i64, [_i64, _i64, _i64, _i64]),
     "kdfm_relpos_attn_bwd": (_i32, [P, P, P, P, P, P, P, P, P, P, P, P, P, _i64, _i64, _i64, _i64, _i64, _f32, _f32, P,
                                     C.c_uint64, P]),
+    "kdfm_relpos_attn_bwd_parts": (_i32, [P, P, P, P, P, P, P, P, P, P, P, P, P, _i64, _i64, _i64, _i64, _i64, _f32,
+                                          _f32, P, C.c_uint64, _i32, P]),
     "kdfm_wgrad_bf16": (_i32, [P, P, P, _i64, P, _i64, _i64, _i64, _f32, P, _i64, P]),
     "kdfm_fm_chain_fwd": (_i32, [P, P, P, _i64, P, P, P, P, P, P, P, P, P, P, P, _f32, _i64, _i32, _i32, P]),
     "kdfm_rowgemm_img_elems": (_i64, [_i64]),
@@ -105,6 +107,9 @@ SIGNATURES: dict[str, tuple] = {
     "kdfm_subsample_dgrad_wprep_elems": (_i64, [_i64]),
     "kdfm_subsample_dgrad_wprep": (_i32, [P, P, _i64, P]),
     "kdfm_subsample_conv2_dgrad": (_i32, [P, P, P, P, _i64, _i64, _i64, _i64, P]),
+    "kdfm_subsample_conv2_dgrad_w0_ws": (_i64, [_i64, _i64, _i64, _i64]),
+    "kdfm_subsample_conv2_dgrad_w0": (_i32, [P, P, P, P, _i64, _i64, _i64, _i64, P, P, _i64, _i64, _i64, P, P, P, _i64,
+                                              P]),
     "kdfm_denoise_chain_fwd": (_i32, [P, P, P, P, P, P, P, P, P, _i64, _i64, _i32, _i32, P]),
     "kdfm_denoise_chain_bwd": (_i32, [P, P, P, P, P, P, P, P, _i64, _i64, _i32, _i32, P]),
     "kdfm_range_pop": (_i32, []),

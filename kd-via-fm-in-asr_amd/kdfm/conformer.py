@@ -248,6 +248,17 @@ def subsampling_backward(cfg, S: EncoderShapes, P, G, pre, ctx, dx, len1, *, see
             K.linear_dw(dy2, cols1, G[pre + "pre_encode.conv.2.weight"].view(C, 9 * C),
                         db=G[pre + "pre_encode.conv.2.bias"])
         WGRAD.run(conv2_wgrad, dy2, cols1, ctx["y1"])
+    m = cfg.subsampling_mask
+    if direct and B * S.T1 * S.F1 < (1 << 24):
+        # direct transposed conv over the input positions' parity classes (no column matrix), the ReLU'
+        # of y1 in its epilogue, and conv0's weight gradient accumulated from the mel patches in the same
+        # epilogue: dy1 never reaches HBM
+        wt = ws["w2_dgrad"]
+        K.subsample_dgrad_wprep(P[pre + "pre_encode.conv.2.weight"].view(C, C, 3, 3), wt)
+        K.subsample_conv2_dgrad_w0(dy2, wt, ctx["y1"], B, S.T1, S.F1, C, ctx["mel"], ctx["mel_len"] if m else None,
+                                   S.Tm, cfg.nfilt, S.pad, G[pre + "pre_encode.conv.0.weight"].view(C, 9),
+                                   G[pre + "pre_encode.conv.0.bias"])
+        return
     dy1 = _empty(B * S.T1 * S.F1, C, dev=dev)
     if direct:
         # direct transposed conv over the input positions' parity classes (no column matrix); the
@@ -267,7 +278,6 @@ def subsampling_backward(cfg, S: EncoderShapes, P, G, pre, ctx, dx, len1, *, see
     del dy2
     # conv0 (1 -> C, 3x3, s2) weight gradient straight from the mel frames: the direct stride-2 kernel
     # of dw_striding's first stage (same layer), no im2col of the input, deterministic fold
-    m = cfg.subsampling_mask
     run = (lambda fn, *keep: fn()) if direct else WGRAD.run   # direct: the main stream is free here
     run(lambda: K.dwsub_conv_wgrad(dy1, len1 if m else None, ctx["mel"], ctx["mel_len"] if m else None,
                                          G[pre + "pre_encode.conv.0.weight"], G[pre + "pre_encode.conv.0.bias"],
@@ -644,10 +654,22 @@ def layer_backward(cfg, S: EncoderShapes, P, G, L, li, ctx, dout, pos_emb, lengt
         dqu = _empty(rows, d, dev=dev)
         dqv = _empty(rows, d, dev=dev)
         dppos = _empty(npos, d, dev=dev)
-        K.relpos_attn_bwd(do, ctx["o"], qu, qv, qkv, ppos, Pm, lengths, dqu, dqv, dqkv, dppos, B, H, T, 1.0 / math.sqrt(dk),
-                          ctx["pa"], seed, _stream(salt, li, SITE_ATT_P))
+        sc = 1.0 / math.sqrt(dk)
+        st_att = _stream(salt, li, SITE_ATT_P)
+        # the positional-term gradient dPpos feeds only the linear_pos weight gradient: it runs on the
+        # weight-gradient stream beside the dQ / dK,dV kernels the main stream needs next
+        abws = torch.empty(K.relpos_attn_bwd_ws(B, H, T, d), device=dev)
+        K.relpos_attn_bwd(do, ctx["o"], qu, qv, qkv, ppos, Pm, lengths, dqu, dqv, dqkv, None, B, H, T, sc, ctx["pa"], seed,
+                          st_att, parts=K.ATTN_BWD_ROWDOT | K.ATTN_BWD_DQ | K.ATTN_BWD_DKV, ws=abws)
+        o_ = ctx["o"]
+
+        def dpos_and_wgrad():
+            K.relpos_attn_bwd(do, o_, qu, qv, qkv, ppos, Pm, lengths, None, None, None, dppos, B, H, T, sc, ctx["pa"],
+                              seed, st_att, parts=K.ATTN_BWD_DPOS, ws=abws)
+            K.linear_dw(dppos, pos_emb, G[L + "self_attn.linear_pos.weight"])
+        WGRAD.run(dpos_and_wgrad, do, o_, qu, qv, qkv, ppos, Pm, dppos, abws, pos_emb)
         del do
-        return _attn_bwd_tail(P, G, L, ctx, dqkv, dqu, dqv, dppos, pos_emb, dx2, lng, cfg, pd, seed, salt, li, rows, d,
+        return _attn_bwd_tail(P, G, L, ctx, dqkv, dqu, dqv, None, pos_emb, dx2, lng, cfg, pd, seed, salt, li, rows, d,
                               dev)
     dPd = _empty(B, H, T, T, dev=dev)
     # dPd = dO V^T : A(i,c)=do[b,i,h*dk+c], B(c,j)=V[b,j,h*dk+c]
@@ -685,7 +707,8 @@ def layer_backward(cfg, S: EncoderShapes, P, G, L, li, ctx, dout, pos_emb, lengt
 
 def _attn_bwd_tail(P, G, L, ctx, dqkv, dqu, dqv, dppos, pos_emb, dx2, lng, cfg, pd, seed, salt, li, rows, d, dev):
     """Pos-bias / linear_pos / q|k|v projection grads, norm_self_att and FFN1 backward."""
-    WGRAD.run(lambda: K.linear_dw(dppos, pos_emb, G[L + "self_attn.linear_pos.weight"]), dppos, pos_emb)
+    if dppos is not None:   # (the fused path ran dPpos and this weight gradient on the wgrad stream)
+        WGRAD.run(lambda: K.linear_dw(dppos, pos_emb, G[L + "self_attn.linear_pos.weight"]), dppos, pos_emb)
     del dppos
     dx1 = _empty(rows, d, dev=dev)
     if ctx["ln2"] is None:   # fused LN + q|k|v forward: fused backward (dq = dqu + dqv formed in-kernel)

@@ -64,6 +64,21 @@ class Trace:
                 for k, v in out.items()}
 
 
+def _traced(tag, flops, nbytes, name, *args):
+    """call(name, *args); when the active Trace wants `tag` (or "*"), bracket the launch with HIP events
+    on the current stream and record its algorithmic FLOPs / HBM bytes (bench.py roofline families)."""
+    tr = Trace.active
+    if tr is None or not (tag in tr.tags or "*" in tr.tags):
+        call(name, *args)
+        return
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    call(name, *args)
+    ev1.record()
+    tr.events.append((tag, float(flops), float(nbytes), ev0, ev1))
+
+
 def set_ranges(on: bool) -> None:
     """Emit ROCTx ranges (kdfm_range_push/pop) around the engine's phases and every span(); env
     KDFM_ROCTX=1 sets it at import.  rocprofv3 --marker-trace records them with the kernels."""
@@ -633,8 +648,9 @@ def wgrad_bf16(dY, X, dW, *, db=None, alpha=1.0):
     if n < 0:
         raise _lib.KdfmError(f"kdfm_wgrad_bf16: unsupported shape rows={rows} M={M} N={N}")
     ws = scratch(dY.device, n)
-    call("kdfm_wgrad_bf16", ptr(_bf16(dY)), ptr(_bf16(X)), ptr(_f32(dW)), dW.stride(0), ptr(db), rows, M, N,
-         float(alpha), ptr(ws), ws.numel(), _s())
+    # algorithmic bytes: both bf16 row operands once, the f32 gradient read + written
+    _traced("wgrad_bf16", 2.0 * rows * M * N, 2.0 * rows * (M + N) + 8.0 * M * N, "kdfm_wgrad_bf16", ptr(_bf16(dY)),
+            ptr(_bf16(X)), ptr(_f32(dW)), dW.stride(0), ptr(db), rows, M, N, float(alpha), ptr(ws), ws.numel(), _s())
 
 
 def fm_chain_fwd(x0, zt, W1, cvec, W2, b2, Wst, bst, X, A, nsx, dtr, xS, loss, inv, S):
@@ -689,9 +705,13 @@ def ffn_fwd(x, g, b, eps, img, b1, b2, out, mean, rstd, ff, *, rscale, p_act, p_
     assert (mean is None) == (rstd is None)
     og, ob, oeps, oy, om, orr = out_ln if out_ln is not None else (None, None, 0.0, None, None, None)
     assert oy is None or (oy.shape == (rows, d) and oy.is_contiguous())
-    call("kdfm_ffn_fwd", ptr(_f32(x)), ptr(_f32(g)), ptr(_f32(b)), float(eps), ptr(_bf16(img)), ptr(_f32(b1)),
-         ptr(_f32(b2)), ptr(out), ptr(mean), ptr(rstd), rows, d, int(ff), float(rscale), float(p_act), float(p_out),
-         ptr(seed), int(st_act), int(st_out), ptr(og), ptr(ob), float(oeps), ptr(oy), ptr(om), ptr(orr), _s())
+    # algorithmic bytes: x read, out written (+ the row statistics, + the LN output), weights once (bf16)
+    nb = 8.0 * rows * d + 4.0 * d * ff + (8.0 * rows if mean is not None else 0.0) + \
+        (4.0 * rows * d + 8.0 * rows if oy is not None else 0.0)
+    _traced("ffn_fwd", 4.0 * rows * d * ff, nb, "kdfm_ffn_fwd", ptr(_f32(x)), ptr(_f32(g)), ptr(_f32(b)), float(eps),
+            ptr(_bf16(img)), ptr(_f32(b1)), ptr(_f32(b2)), ptr(out), ptr(mean), ptr(rstd), rows, d, int(ff),
+            float(rscale), float(p_act), float(p_out), ptr(seed), int(st_act), int(st_out), ptr(og), ptr(ob),
+            float(oeps), ptr(oy), ptr(om), ptr(orr), _s())
 
 
 def ffn_bwd(dout, x, mean, rstd, g, b, img, b1, dx, ln_h, a_h, dl2_h, dh_h, part, ff, *, rscale, p_act, p_out, seed,
@@ -700,10 +720,13 @@ def ffn_bwd(dout, x, mean, rstd, g, b, img, b1, dx, ln_h, a_h, dl2_h, dh_h, part
     assert dout.shape == (rows, d) and dx.shape == (rows, d) and dout.is_contiguous() and dx.is_contiguous()
     assert ln_h.shape == (rows, d) and dl2_h.shape == (rows, d) and a_h.shape == (rows, ff) and dh_h.shape == (rows, ff)
     assert part.numel() >= layernorm_bwd_ws(rows, d)
-    call("kdfm_ffn_bwd", ptr(_f32(dout)), ptr(_f32(x)), ptr(_f32(mean)), ptr(_f32(rstd)), ptr(_f32(g)), ptr(_f32(b)),
-         ptr(_bf16(img)), ptr(_f32(b1)), ptr(dx), ptr(_bf16(ln_h)), ptr(_bf16(a_h)), ptr(_bf16(dl2_h)),
-         ptr(_bf16(dh_h)), ptr(part), rows, d, int(ff), float(rscale), float(p_act), float(p_out), ptr(seed),
-         int(st_act), int(st_out), _s())
+    # algorithmic bytes: dout, x read; dx written (f32); ln, dl2 (bf16, d wide), a, dh (bf16, ff wide)
+    # written; row statistics read; weights once
+    nb = 12.0 * rows * d + 8.0 * rows + 4.0 * rows * d + 4.0 * rows * ff + 4.0 * d * ff
+    _traced("ffn_bwd", 6.0 * rows * d * ff, nb, "kdfm_ffn_bwd", ptr(_f32(dout)), ptr(_f32(x)), ptr(_f32(mean)),
+            ptr(_f32(rstd)), ptr(_f32(g)), ptr(_f32(b)), ptr(_bf16(img)), ptr(_f32(b1)), ptr(dx), ptr(_bf16(ln_h)),
+            ptr(_bf16(a_h)), ptr(_bf16(dl2_h)), ptr(_bf16(dh_h)), ptr(part), rows, d, int(ff), float(rscale),
+            float(p_act), float(p_out), ptr(seed), int(st_act), int(st_out), _s())
 
 
 RG_PRO_NONE, RG_PRO_DROP, RG_PRO_BNSILU = 0, 1, 2
@@ -984,6 +1007,17 @@ def subsample_dgrad_wprep_elems(Cc):
     return int(_lib.lib().kdfm_subsample_dgrad_wprep_elems(Cc))
 
 
+def subsample_conv2_dgrad_w0(dy2, wt, y1, B, T1, F1, Cc, mel, mel_len, Tm, Fm, pad, dw0, db0, dy1=None):
+    """conv2 data gradient (as subsample_conv2_dgrad) with conv0's weight gradient fused into the epilogue:
+    dw0 (C, 9) += sum dy1 x_patch(mel), db0 (C) += sum dy1; dy1 optional."""
+    assert dw0.numel() == Cc * 9 and dw0.is_contiguous() and db0.numel() == Cc
+    n = int(_lib.lib().kdfm_subsample_conv2_dgrad_w0_ws(B, T1, F1, Cc))
+    ws = scratch(dy2.device, n)
+    call("kdfm_subsample_conv2_dgrad_w0", ptr(_f32(dy2)), ptr(wt), ptr(_bf16(y1, "y1 (bf16 conv1 output)")), ptr(dy1),
+         B, T1, F1, Cc, ptr(_f32(mel)), ptr(_i64(mel_len)), Tm, Fm, pad, ptr(_f32(dw0)), ptr(_f32(db0)), ptr(ws),
+         ws.numel(), _s())
+
+
 def subsample_dgrad_supported(Cc):
     """Channel counts the direct conv2 data-gradient kernel is instantiated for."""
     return Cc % 8 == 0 and ((-(-Cc // 32), -(-Cc // 16)) in ((3, 6), (1, 1), (1, 2), (2, 4)))
@@ -1053,17 +1087,39 @@ def qkv_prep(qkv, u, v, qu, qv):
     call("kdfm_qkv_prep", ptr(qkv), ptr(u), ptr(v), ptr(qu), ptr(qv), rows, d, _s())
 
 
-def relpos_attn_bwd(do, o, qu, qv, qkv, ppos, P, lengths, dqu, dqv, dqkv, dppos, B, H, T, scale, p, seed, rng_stream):
-    """Fused attention backward (csrc/attn_bwd.hip): dqu, dqv, dK/dV into dqkv[:, d:], dppos."""
+ATTN_BWD_ROWDOT, ATTN_BWD_DQ, ATTN_BWD_DKV, ATTN_BWD_DPOS, ATTN_BWD_ALL = 1, 2, 4, 8, 15
+
+
+def relpos_attn_bwd_ws(B, H, T, d):
+    return int(_lib.lib().kdfm_relpos_attn_bwd_ws(B, H, T, d))
+
+
+def relpos_attn_bwd(do, o, qu, qv, qkv, ppos, P, lengths, dqu, dqv, dqkv, dppos, B, H, T, scale, p, seed, rng_stream,
+                    parts=ATTN_BWD_ALL, ws=None):
+    """Fused attention backward (csrc/attn_bwd.hip): dqu, dqv, dK/dV into dqkv[:, d:], dppos.  `parts`
+    (ATTN_BWD_*) issues a subset; parts issued on different streams must share a dedicated `ws`
+    (relpos_attn_bwd_ws floats) and be ordered after ROWDOT."""
     rows, d = do.shape
-    assert rows == B * T and qkv.shape == (rows, 3 * d) and P.shape == (B, H, T, T) and dppos.shape == (2 * T - 1, d)
+    assert rows == B * T and qkv.shape == (rows, 3 * d) and P.shape == (B, H, T, T)
+    assert dppos is None or dppos.shape == (2 * T - 1, d)
     for t in (do, o, qu, qv, qkv, ppos, P, dqu, dqv, dqkv, dppos):
-        assert t.is_contiguous()
+        assert t is None or t.is_contiguous()
     assert o.shape == do.shape
-    ws = scratch(do.device, int(_lib.lib().kdfm_relpos_attn_bwd_ws(B, H, T, d)))
-    call("kdfm_relpos_attn_bwd", ptr(do), ptr(o), ptr(qu), ptr(qv), ptr(qkv), ptr(ppos), ptr(P), ptr(_i64(lengths)), ptr(dqu),
-         ptr(dqv), ptr(dqkv), ptr(dppos), ptr(ws), ws.numel(), B, H, T, d, float(scale), float(p), ptr(seed),
-         int(rng_stream), _s())
+    if parts != ATTN_BWD_ALL:
+        assert ws is not None and ws.numel() >= relpos_attn_bwd_ws(B, H, T, d)
+        call("kdfm_relpos_attn_bwd_parts", ptr(do), ptr(o), ptr(qu), ptr(qv), ptr(qkv), ptr(ppos), ptr(P),
+             ptr(_i64(lengths)), ptr(dqu), ptr(dqv), ptr(dqkv), ptr(dppos), ptr(ws), ws.numel(), B, H, T, d,
+             float(scale), float(p), ptr(seed), int(rng_stream), int(parts), _s())
+        return
+    ws = scratch(do.device, relpos_attn_bwd_ws(B, H, T, d))
+    # algorithmic: the 4 products per (b, h) of dQu, dQv, dK, dV, dPpos + dP (2 T^2 dk each, band ~2 T^2 dk)
+    # and bytes: dO, O, qu, qv, K, V read, P (f32) read, dqu, dqv, dK, dV written
+    dk = d // H
+    fl = 2.0 * B * H * T * T * dk * 6
+    nb = 4.0 * rows * d * 10 + 4.0 * B * H * T * T
+    _traced("attn_bwd", fl, nb, "kdfm_relpos_attn_bwd", ptr(do), ptr(o), ptr(qu), ptr(qv), ptr(qkv), ptr(ppos), ptr(P),
+            ptr(_i64(lengths)), ptr(dqu), ptr(dqv), ptr(dqkv), ptr(dppos), ptr(ws), ws.numel(), B, H, T, d,
+            float(scale), float(p), ptr(seed), int(rng_stream), _s())
 
 
 def relpos_attn_fwd(qu, qv, qkv, ppos, lengths, o, P, Pd, B, H, T, scale, p, seed, rng_stream):
@@ -1071,8 +1127,12 @@ def relpos_attn_fwd(qu, qv, qkv, ppos, lengths, o, P, Pd, B, H, T, scale, p, see
     rows, d = qu.shape
     assert rows == B * T and qkv.shape == (rows, 3 * d) and ppos.shape == (2 * T - 1, d) and o.shape == (rows, d)
     assert qu.is_contiguous() and qv.is_contiguous() and qkv.is_contiguous() and ppos.is_contiguous()
-    call("kdfm_relpos_attn_fwd", ptr(qu), ptr(qv), ptr(qkv), ptr(ppos), ptr(_i64(lengths)), ptr(o), ptr(P), ptr(Pd),
-         B, H, T, d, float(scale), float(p), ptr(seed), rng_stream, _s())
+    # algorithmic: QK^T, the positional band (one T x T-equivalent) and PV, 2 T^2 dk FLOP each per (b, h);
+    # bytes: qu, qv, K, V, o once (+ P written when saved)
+    fl = 2.0 * B * H * T * T * (d // H) * 3
+    nb = 4.0 * rows * d * 5 + (4.0 * B * H * T * T if P is not None else 0.0)
+    _traced("attn_fwd", fl, nb, "kdfm_relpos_attn_fwd", ptr(qu), ptr(qv), ptr(qkv), ptr(ppos), ptr(_i64(lengths)),
+            ptr(o), ptr(P), ptr(Pd), B, H, T, d, float(scale), float(p), ptr(seed), rng_stream, _s())
 
 
 def relpos_softmax_fwd(ac, bd, lengths, P, Pd, B, H, T, scale, p, seed, rng_stream):

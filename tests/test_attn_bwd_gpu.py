@@ -128,3 +128,35 @@ def test_attn_bwd_matches_unfused_with_dropout():
     for name, got, want in zip(("dQu", "dQv", "dK", "dV", "dPpos"), (dqu, dqv, dk_, dv_, dpos),
                                (r_dqu, r_dqv, r_dk, r_dv, r_dpos)):
         assert _rel(got, want) <= 2e-2, (name, _rel(got, want))
+
+
+def test_attn_bwd_parts_on_two_streams_match_one_launch():
+    """kdfm_relpos_attn_bwd_parts: ROWDOT | DQ | DKV on one stream and DPOS (+ fold) on a second stream
+    ordered after it (the engine puts DPOS on the weight-gradient stream) give bitwise the outputs of
+    the single-stream call."""
+    from kdfm import kernels as K
+    B, H, T, d, p = 4, 2, 101, 88, 0.1
+    dk = d // H
+    seed = torch.tensor([77], dtype=torch.int64, device="cuda")
+    qkv, qu, qv, ppos, do, lens = _inputs(B, H, T, d, 3)
+    ref = _fused(K, qkv, qu, qv, ppos, do, lens, B, H, T, d, p, seed)
+    P = ref[0]
+    o = torch.empty(B * T, d, device="cuda")
+    K.relpos_attn_fwd(qu, qv, qkv, ppos, lens, o, torch.empty_like(P), None, B, H, T, 1.0 / math.sqrt(dk), p, seed, 11)
+    dqu = torch.empty(B * T, d, device="cuda")
+    dqv = torch.empty_like(dqu)
+    dqkv = torch.zeros(B * T, 3 * d, device="cuda")
+    dpos = torch.empty(2 * T - 1, d, device="cuda")
+    ws = torch.empty(K.relpos_attn_bwd_ws(B, H, T, d), device="cuda")
+    sc = 1.0 / math.sqrt(dk)
+    K.relpos_attn_bwd(do, o, qu, qv, qkv, ppos, P, lens, dqu, dqv, dqkv, None, B, H, T, sc, p, seed, 11,
+                      parts=K.ATTN_BWD_ROWDOT | K.ATTN_BWD_DQ | K.ATTN_BWD_DKV, ws=ws)
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        K.relpos_attn_bwd(do, o, qu, qv, qkv, ppos, P, lens, None, None, None, dpos, B, H, T, sc, p, seed, 11,
+                          parts=K.ATTN_BWD_DPOS, ws=ws)
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    for got, want in zip((dqu, dqv, dqkv[:, d:2 * d], dqkv[:, 2 * d:], dpos), ref[1:]):
+        assert torch.equal(got, want)

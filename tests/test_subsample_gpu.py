@@ -19,6 +19,12 @@ def _bf(t):
     return t.to(torch.bfloat16).float()
 
 
+def _rel(a, b):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
 def _lens(L):
     return (L - 1) // 2 + 1
 
@@ -145,3 +151,41 @@ def test_im2col_tapmajor_bf16_matches_f32_im2col(K):
     torch.cuda.synchronize()
     want = ref.view(-1, C, 9).transpose(1, 2).reshape(-1, 9 * C).bfloat16()
     assert torch.equal(got, want)
+
+
+@pytest.mark.parametrize("C,Tm,Fm", [(88, 801, 80), (88, 75, 27), (32, 61, 80), (64, 13, 9)])
+def test_subsample_dgrad_fused_conv0_wgrad(K, C, Tm, Fm):
+    """kdfm_subsample_conv2_dgrad_w0: conv0's weight / bias gradient accumulated in the conv2 data
+    gradient's epilogue equals the float64 conv0 weight gradient of the same dy1 (the kernel's own
+    dy1, also written) over the mel frames with frames t >= mel_len zeroed: rel. Frobenius <= 1e-5
+    (f32 sums over ~1e6 positions, ordered per-workgroup fold)."""
+    g = torch.Generator().manual_seed(C + Tm)
+    B = 3
+    T1, F1 = _lens(Tm), _lens(Fm)
+    T2, F2 = _lens(T1), _lens(F1)
+    mel = torch.randn(B, Tm, Fm, generator=g)
+    mel_len = torch.tensor([Tm, Tm - Tm // 3, Tm // 2], dtype=torch.int64)
+    y1 = torch.relu(torch.randn(B, T1, F1, C, generator=g))
+    for b in range(B):   # conv1 output rows past the subsampled length are masked (zero)
+        y1[b, (int(mel_len[b]) - 1) // 2 + 1:] = 0.0
+    dy2 = torch.randn(B, T2, F2, C, generator=g)
+    w2 = torch.randn(C, C, 3, 3, generator=g) * (1.0 / (3 * C ** 0.5))
+    wt = torch.empty(K.subsample_dgrad_wprep_elems(C), device="cuda", dtype=torch.bfloat16)
+    K.subsample_dgrad_wprep(w2.cuda(), wt)
+    dy1 = torch.empty(B * T1 * F1, C, device="cuda")
+    dw0 = torch.full((C, 9), 0.5, device="cuda")
+    db0 = torch.zeros(C, device="cuda")
+    K.subsample_conv2_dgrad_w0(dy2.cuda().reshape(-1, C), wt, y1.cuda().reshape(-1, C).bfloat16(), B, T1, F1, C,
+                               mel.cuda(), mel_len.cuda(), Tm, Fm, 1, dw0, db0, dy1=dy1)
+    torch.cuda.synchronize()
+    d1 = dy1.cpu().double().view(B, T1, F1, C).permute(0, 3, 1, 2)
+    xm = mel.double().clone()
+    for b in range(B):
+        xm[b, int(mel_len[b]):] = 0.0
+    x = xm[:, None]
+    w = torch.zeros(C, 1, 3, 3, dtype=torch.float64, requires_grad=True)
+    bias = torch.zeros(C, dtype=torch.float64, requires_grad=True)
+    out = F.conv2d(x, w, bias, stride=2, padding=1)
+    gw, gb = torch.autograd.grad(out, [w, bias], d1)
+    assert _rel(dw0.cpu() - 0.5, gw.view(C, 9)) <= 1e-5
+    assert _rel(db0.cpu(), gb) <= 1e-5
