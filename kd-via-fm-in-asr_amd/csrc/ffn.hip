@@ -20,9 +20,13 @@
 // (r, h) the features 8 q + 4 h + 0..3 of row r; one v_permlane32_swap per packed bf16 dword turns a
 // chunk's activation into the B operand of the next product (cdna_hip_programming.md T21).
 //
-// Work split: a workgroup owns 64 rows = 2 row tiles of 32; the two waves of a tile take the even and
-// the odd hidden chunks and their partial down-projections are added (in that fixed order) through
-// LDS at the end, so 12,832 rows give 804 waves instead of 402.
+// Work split: a workgroup owns 64 rows = 2 row tiles of 32.  Backward: the two waves of a tile take
+// the even and the odd hidden chunks.  Forward (d <= 96): NP = 4 waves per tile take the chunks
+// c = NP it + par, so 12,832 rows give 1,604 waves (the kernel is latency bound: a wave's serial
+// chain of chunks sets the launch time and 201 workgroups fill at most 201 CUs); their partial
+// down-projections are added in the fixed order ((p0 + p1) + p2) + p3 through LDS at the end, and
+// registers are held to 256 per lane (launch bound 512) so the 8 waves run 2 per SIMD.  d = 176
+// keeps NP = 2 (even / odd chunks, 256 threads).
 #include "lnblock.h"
 #include "wimg.h"
 
@@ -31,8 +35,12 @@ namespace {
 
 using namespace lnb;
 
-constexpr int FF_NT = 256;        // 4 waves: 2 row tiles x 2 chunk parities
+constexpr int FF_NT = 256;        // backward: 4 waves = 2 row tiles x 2 chunk parities
 constexpr int FF_ROWS = 64;       // rows per workgroup
+// forward: chunk parities per row tile (4 for d <= 96; d = 176 keeps 2: four 23 KB chunks per stage and
+// its 96 accumulators do not fit the 256-register budget of 2 waves per SIMD)
+template <int DT> constexpr int fwd_np() { return DT <= 3 ? 4 : 2; }
+template <int DT> constexpr int fwd_nt() { return 2 * fwd_np<DT>() * 64; }
 
 // Chunk image (one 32-feature slice of the hidden width), fragment order:
 //   W2c(mt, ks2) = 2 mt + ks2            A of the down-projection (d rows x 32 hidden)     [fwd]
@@ -81,13 +89,20 @@ template <int SF, int DT>
 constexpr int ffn_stage_bytes() {
   return 4 * SF * 1024 > 2 * DT * 16 * 64 * 4 ? 4 * SF * 1024 : 2 * DT * 16 * 64 * 4;
 }
+// forward: two stages of NP chunks, or the NP - 1 partials per tile of the final reduction
+template <int SF, int DT>
+constexpr int ffn_fwd_stage_bytes() {
+  constexpr int NP = fwd_np<DT>();
+  return 2 * NP * SF * 1024 > 2 * (NP - 1) * DT * 16 * 64 * 4 ? 2 * NP * SF * 1024 : 2 * (NP - 1) * DT * 16 * 64 * 4;
+}
 
 template <int KS1, int DT>
-__global__ __launch_bounds__(FF_NT) void ffn_fwd_kernel(FfnFwd a) {
+__global__ __launch_bounds__(fwd_nt<DT>()) void ffn_fwd_kernel(FfnFwd a) {
   using G = FfnGeo<KS1, DT>;
+  constexpr int FWD_NP = fwd_np<DT>(), FWD_NT = fwd_nt<DT>();
   extern __shared__ __attribute__((aligned(16))) uint4 ff_lds[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int h = lane >> 5, par = wave & 1, tile = wave >> 1;
+  const int h = lane >> 5, par = wave % FWD_NP, tile = wave / FWD_NP;
   const int64_t row = (int64_t)blockIdx.x * FF_ROWS + tile * 32 + (lane & 31);
   const bool ok = row < a.rows;
   const int d = a.d, ff = a.ff, FC = ff / 32;
@@ -95,7 +110,7 @@ __global__ __launch_bounds__(FF_NT) void ffn_fwd_kernel(FfnFwd a) {
   const uint64_t kact = rng_key(seed, a.st_act), kout = rng_key(seed, a.st_out);
   const float ks_act = 1.f / (1.f - a.p_act), ks_out = 1.f / (1.f - a.p_out);
 
-  Stager<G::FWD, 0, G::CS, 2, FF_NT> stg;
+  Stager<G::FWD, 0, G::CS, FWD_NP, FWD_NT> stg;
   const uint4* img = reinterpret_cast<const uint4*>(a.img);
   stg.load(img, 0, FC);
 
@@ -112,11 +127,11 @@ __global__ __launch_bounds__(FF_NT) void ffn_fwd_kernel(FfnFwd a) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[mt][i] = 0.f;
 
-  float* bias_s = reinterpret_cast<float*>(reinterpret_cast<char*>(ff_lds) + ffn_stage_bytes<G::FWD, DT>());
-  for (int e = threadIdx.x; e < ff + d; e += FF_NT) bias_s[e] = e < ff ? a.b1[e] : a.b2[e - ff];
+  float* bias_s = reinterpret_cast<float*>(reinterpret_cast<char*>(ff_lds) + ffn_fwd_stage_bytes<G::FWD, DT>());
+  for (int e = threadIdx.x; e < ff + d; e += FWD_NT) bias_s[e] = e < ff ? a.b1[e] : a.b2[e - ff];
   // the residual rows in the accumulator layout for the epilogue, fetched now so their latency hides
   // behind the chunk loop (narrow d only: 4 DT float4 registers)
-  constexpr bool XPRE = DT <= 3;
+  constexpr bool XPRE = DT <= 3 && FWD_NP == 2;
   float4 xres[XPRE ? DT : 1][4];
   if constexpr (XPRE) {
 #pragma unroll
@@ -130,12 +145,12 @@ __global__ __launch_bounds__(FF_NT) void ffn_fwd_kernel(FfnFwd a) {
   }
   stg.store(ff_lds, 0);
   __syncthreads();
-  const int nit = (FC + 1) / 2;
+  const int nit = (FC + FWD_NP - 1) / FWD_NP;
   for (int it = 0; it < nit; ++it) {
     if (it + 1 < nit) stg.load(img, it + 1, FC);
-    const int c = 2 * it + par;
+    const int c = FWD_NP * it + par;
     if (c < FC) {
-      const uint4* W = ff_lds + ((it & 1) * 2 + par) * G::FWD * FRAG_U4;
+      const uint4* W = stg.block(ff_lds, it & 1, par);
       f32x16 hacc;
 #pragma unroll
       for (int i = 0; i < 16; ++i) hacc[i] = 0.f;
@@ -172,16 +187,23 @@ __global__ __launch_bounds__(FF_NT) void ffn_fwd_kernel(FfnFwd a) {
     if (it + 1 < nit) stg.store(ff_lds, (it + 1) & 1);
     __syncthreads();
   }
-  // odd-chunk partial -> even wave (fixed order: even + odd)
-  float* red = reinterpret_cast<float*>(ff_lds) + tile * (DT * 16 * 64);
-  if (par == 1) {
+  // partials of parities 1..NP-1 -> parity 0, added in the fixed order ((p0 + p1) + p2) + p3
+  float* red = reinterpret_cast<float*>(ff_lds) + tile * ((FWD_NP - 1) * DT * 16 * 64);
+  if (par != 0) {
+    float* mine = red + (par - 1) * (DT * 16 * 64);
 #pragma unroll
     for (int mt = 0; mt < DT; ++mt)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) red[(mt * 16 + i) * 64 + lane] = acc[mt][i];
+      for (int i = 0; i < 16; ++i) mine[(mt * 16 + i) * 64 + lane] = acc[mt][i];
   }
   __syncthreads();
-  if (par == 1) return;   // (every lane of the even wave stays: the optional LN reduces across lanes)
+  if (par != 0) return;   // (every lane of the parity-0 wave stays: the optional LN reduces across lanes)
+#pragma unroll
+  for (int q = 1; q < FWD_NP; ++q)
+#pragma unroll
+    for (int mt = 0; mt < DT; ++mt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[mt][i] += red[((q - 1) * DT * 16 + mt * 16 + i) * 64 + lane];
   float o[DT][16];
 #pragma unroll
   for (int mt = 0; mt < DT; ++mt)
@@ -201,7 +223,7 @@ __global__ __launch_bounds__(FF_NT) void ffn_fwd_kernel(FfnFwd a) {
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        float v = acc[mt][4 * q + i] + red[(mt * 16 + 4 * q + i) * 64 + lane] + bv[i];
+        float v = acc[mt][4 * q + i] + bv[i];
         if (a.p_out > 0.f) v = kp[i] ? v * ks_out : 0.f;
         o[mt][4 * q + i] = in ? xv[i] + a.rscale * v : 0.f;
       }
@@ -406,8 +428,9 @@ int launch_fwd(const FfnFwd& a, hipStream_t st) {
   using G = FfnGeo<KS1, DT>;
   static bool once = (ffn_allow_lds(ffn_fwd_kernel<KS1, DT>), true);
   (void)once;
-  const size_t lds = (size_t)ffn_stage_bytes<G::FWD, DT>() + (size_t)(a.ff + a.d) * 4;
-  hipLaunchKernelGGL((ffn_fwd_kernel<KS1, DT>), dim3((unsigned)ceil_div(a.rows, FF_ROWS)), dim3(FF_NT), lds, st, a);
+  const size_t lds = (size_t)ffn_fwd_stage_bytes<G::FWD, DT>() + (size_t)(a.ff + a.d) * 4;
+  if (lds > 160 * 1024) { set_error("kdfm_ffn_fwd: hidden width too large for the LDS bias table"); return KDFM_EINVAL; }
+  hipLaunchKernelGGL((ffn_fwd_kernel<KS1, DT>), dim3((unsigned)ceil_div(a.rows, FF_ROWS)), dim3(fwd_nt<DT>()), lds, st, a);
   return check_launch("kdfm_ffn_fwd");
 }
 

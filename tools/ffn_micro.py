@@ -2,7 +2,7 @@
 forward / backward (student d=88 with dropout, teacher d=176 without), LN-fused projections and the
 row-streaming products, against the unfused kdfm_gemm path they replace.  HIP events around N
 back-to-back launches on one stream; prints one line per case (us per launch).
-usage: python tools/ffn_micro.py [iters]"""
+usage: python tools/ffn_micro.py [iters] [rows]"""
 import os
 import sys
 
@@ -30,7 +30,7 @@ def timeit(fn, iters):
 
 def main():
     iters = int(sys.argv[1]) if len(sys.argv) > 1 else 50
-    rows = 12832
+    rows = int(sys.argv[2]) if len(sys.argv) > 2 else 12832
     dev = "cuda"
     seed = torch.tensor([12345], dtype=torch.int64, device=dev)
     K.set_math("bf16")
@@ -69,7 +69,7 @@ def main():
             K.linear(a, W2, b2, out, epi=_lib.EPI_RESID, R=x, rscale=0.5, dropout_p=p, seed=seed, rng_stream=2)
         t_u = timeit(unf, iters)
         flop = 4.0 * rows * d * ff
-        print(f"ffn d={d} p={p}: fused fwd {t_f:7.1f} us ({flop / t_f / 1e6:6.1f} TFLOP/s)  bwd {t_b:7.1f} us  "
+        print(f"ffn rows={rows} d={d} p={p}: fused fwd {t_f:7.1f} us ({flop / t_f / 1e6:6.1f} TFLOP/s)  bwd {t_b:7.1f} us  "
               f"| unfused fwd {t_u:7.1f} us", flush=True)
     # LN projections and row-streaming products at d=88
     d = 88
