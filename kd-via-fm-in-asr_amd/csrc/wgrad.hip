@@ -44,13 +44,19 @@ struct WrGeo {
   int Nb;            // B image columns of one slice (16 * NBW * wn)
   int64_t steps_per; // 32-row steps per split
   int64_t nmem;      // X columns in memory = ones_col if >= 0 else N
+  int Msl;           // A columns (output rows) of one M slice (blockIdx.z), a multiple of 16
 };
 
 // BIN: dY and X are bf16 in memory (the fused KD-head chains store their saved operands as bf16,
-// exactly the values the f32 path would round at staging): 8-byte loads, no conversion.
-template <int MBW, int NBW, bool CONV, int PD, int UPT, bool BIN = false>
+// exactly the values the f32 path would round at staging), no conversion.  BIN = 1: staging units of
+// 4 rows x 4 columns (8-byte loads); BIN = 2 (every column count a multiple of 8): 4 rows x 8 columns,
+// 16-byte loads as in the f32 mode -- half the load instructions and half the units per slab, so
+// the slab fits one unit per thread and two slabs stay in flight.
+template <int MBW, int NBW, bool CONV, int PD, int UPT, int BIN = 0>
 __global__ __launch_bounds__(WR_NT, 2) void wgr_kernel(GemmP p, WrGeo g) {
   constexpr int ES = BIN ? 2 : 4;   // element size in memory
+  constexpr int CW = BIN == 2 ? 8 : 4;   // columns per staging unit
+  constexpr int CWS = BIN == 2 ? 3 : 2;  // log2(CW)
   extern __shared__ __attribute__((aligned(16))) uint16_t wr_lds[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   // LDS images as element offsets into wr_lds (an array of pointers would decay to generic pointers
@@ -59,12 +65,16 @@ __global__ __launch_bounds__(WR_NT, 2) void wgr_kernel(GemmP p, WrGeo g) {
   const int bufsz = ia + ib;                           // buffer b: A at b*bufsz, B at b*bufsz + ia
   const int64_t split = blockIdx.x;
   const int64_t n0 = (int64_t)blockIdx.y * g.Nb;       // first output column of this slice
+  // M slice: output rows m0 .. m0 + mcols - 1 (dY columns); more workgroups for short reductions
+  // without growing any workgroup's partial
+  const int m0 = (int)blockIdx.z * g.Msl;
+  const int mcols = (p.M - m0 < g.Msl) ? (int)(p.M - m0) : g.Msl;
   const int64_t kb = split * g.steps_per * 32;
   int64_t ke = kb + g.steps_per * 32;
   if (ke > p.K) ke = p.K;
   // B memory columns of this slice and the slab's staging units (4 rows x 4 columns each)
   const int ncols_mem = (int)((g.nmem - n0 < g.Nb) ? g.nmem - n0 : g.Nb);
-  const int units = 8 * (int)((p.M >> 2) + (ncols_mem >> 2));
+  const int units = 8 * ((mcols >> CWS) + (ncols_mem >> CWS));
 
   // static image columns: A columns >= M and B columns beyond the memory columns are zero, the
   // ones column (bias gradient) is 1 in every row (rows past K contribute 0 through A)
@@ -78,7 +88,7 @@ __global__ __launch_bounds__(WR_NT, 2) void wgr_kernel(GemmP p, WrGeo g) {
     if (col < g.Ma) {
       img = buf * bufsz;
       c = col;
-      zero = c >= p.M;
+      zero = c >= mcols;
     } else {
       img = buf * bufsz + ia;
       c = col - g.Ma;
@@ -100,7 +110,7 @@ __global__ __launch_bounds__(WR_NT, 2) void wgr_kernel(GemmP p, WrGeo g) {
   // counters are set up once and advanced by one slab per step: no 64-bit multiplies in the loop.
   // Rows past the split's end or outside the utterance (CONV taps) load from a clamped valid address
   // and are zeroed by a select (branch-free).
-  const int ma4 = (int)(p.M >> 2);
+  const int ma4 = mcols >> CWS;   // A column groups
   const char* src[UPT];   // byte pointers (ES-byte elements)
   int64_t ld[UPT];        // row stride in bytes
   int tfr[UPT], toff[UPT];   // CONV: frame of the unit's first row in its utterance; tap - pad
@@ -114,10 +124,10 @@ __global__ __launch_bounds__(WR_NT, 2) void wgr_kernel(GemmP p, WrGeo g) {
     tfr[i] = 0;
     toff[i] = 0;
     if (cg < ma4) {
-      src[i] = reinterpret_cast<const char*>(p.A) + ES * (r0 * p.sAk + cg * 4);
+      src[i] = reinterpret_cast<const char*>(p.A) + ES * (r0 * p.sAk + m0 + cg * CW);
       ld[i] = ES * p.sAk;
     } else {
-      const int64_t n = n0 + (int64_t)(cg - ma4) * 4;
+      const int64_t n = n0 + (int64_t)(cg - ma4) * CW;
       ld[i] = ES * p.sBk;
       if constexpr (CONV) {
         const int64_t tap = n / p.conv_c, c = n - tap * p.conv_c;
@@ -153,7 +163,7 @@ __global__ __launch_bounds__(WR_NT, 2) void wgr_kernel(GemmP p, WrGeo g) {
           }
         }
         const char* q = ok ? src[i] + j * ld[i] : reinterpret_cast<const char*>(p.B);   // any valid, aligned address
-        if constexpr (BIN) {
+        if constexpr (BIN == 1) {
           const uint2 t = *reinterpret_cast<const uint2*>(q);
           r[i][j] = make_float4(__builtin_bit_cast(float, t.x), __builtin_bit_cast(float, t.y), 0.f, 0.f);
         } else {
@@ -177,17 +187,35 @@ __global__ __launch_bounds__(WR_NT, 2) void wgr_kernel(GemmP p, WrGeo g) {
       int img, c0;
       if (cg < ma4) {
         img = buf * bufsz;
-        c0 = cg * 4;
+        c0 = cg * CW;
       } else {
         img = buf * bufsz + ia;
-        c0 = (cg - ma4) * 4;
+        c0 = (cg - ma4) * CW;
       }
       const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
       const float4 v0 = ((m >> (i * 4 + 0)) & 1u) ? r[i][0] : z;
       const float4 v1 = ((m >> (i * 4 + 1)) & 1u) ? r[i][1] : z;
       const float4 v2 = ((m >> (i * 4 + 2)) & 1u) ? r[i][2] : z;
       const float4 v3 = ((m >> (i * 4 + 3)) & 1u) ? r[i][3] : z;
-      if constexpr (BIN) {
+      if constexpr (BIN == 2) {
+        // row j's 8 bf16 columns: column q is half (q & 1) of dword q >> 1; the 4 rows of a column
+        // pair up by byte permutes (low halves: selector 0x05040100, high halves: 0x07060302)
+        const uint32_t w[4][4] = {{__builtin_bit_cast(uint32_t, v0.x), __builtin_bit_cast(uint32_t, v0.y),
+                                   __builtin_bit_cast(uint32_t, v0.z), __builtin_bit_cast(uint32_t, v0.w)},
+                                  {__builtin_bit_cast(uint32_t, v1.x), __builtin_bit_cast(uint32_t, v1.y),
+                                   __builtin_bit_cast(uint32_t, v1.z), __builtin_bit_cast(uint32_t, v1.w)},
+                                  {__builtin_bit_cast(uint32_t, v2.x), __builtin_bit_cast(uint32_t, v2.y),
+                                   __builtin_bit_cast(uint32_t, v2.z), __builtin_bit_cast(uint32_t, v2.w)},
+                                  {__builtin_bit_cast(uint32_t, v3.x), __builtin_bit_cast(uint32_t, v3.y),
+                                   __builtin_bit_cast(uint32_t, v3.z), __builtin_bit_cast(uint32_t, v3.w)}};
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const uint32_t sel = (q & 1) ? 0x07060302u : 0x05040100u;
+          const uint32_t lo = __builtin_amdgcn_perm(w[1][q >> 1], w[0][q >> 1], sel);
+          const uint32_t hi = __builtin_amdgcn_perm(w[3][q >> 1], w[2][q >> 1], sel);
+          *lds_at<u32x2>(wr_lds, img + (c0 + q) * WR_LDK + rg * 4) = u32x2{lo, hi};
+        }
+      } else if constexpr (BIN == 1) {
         // row j's 4 bf16 columns: (q0 | q1 << 16) in .x, (q2 | q3 << 16) in .y
         const uint32_t w[4][2] = {{__builtin_bit_cast(uint32_t, v0.x), __builtin_bit_cast(uint32_t, v0.y)},
                                   {__builtin_bit_cast(uint32_t, v1.x), __builtin_bit_cast(uint32_t, v1.y)},
@@ -281,9 +309,9 @@ __global__ __launch_bounds__(WR_NT, 2) void wgr_kernel(GemmP p, WrGeo g) {
     for (int j = 0; j < NBW; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int64_t m = (mb0 + i) * 16 + (lane >> 4) * 4 + r;
+        const int ml = (mb0 + i) * 16 + (lane >> 4) * 4 + r;
         const int64_t n = n0 + (nb0 + j) * 16 + (lane & 15);
-        if (m < p.M && n < p.N && n < n0 + g.Nb) wsp[m * p.N + n] = acc[i][j][r];
+        if (ml < mcols && n < p.N && n < n0 + g.Nb) wsp[(m0 + ml) * p.N + n] = acc[i][j][r];
       }
 }
 
@@ -352,12 +380,14 @@ int env_i(const char* name, int dflt) {
 struct WrPlan {
   WrPick w;
   WrGeo g;
-  int64_t S, slices;
+  int64_t S, slices, mslices;
   size_t lds;
   int upt;
+  int bin;   // wgr_kernel BIN: 0 f32 operands, 1 / 2 bf16 operands in 4- / 8-column staging units
 };
 
-bool wr_plan(const GemmP& p, int amode, int bmode, int64_t batch, WrPlan& pl, bool force = false) {
+bool wr_plan(const GemmP& p, int amode, int bmode, int64_t batch, WrPlan& pl, bool force = false,
+             bool bf16in = false) {
   static const int enabled = env_i("KDFM_WGR", 1);
   if (!enabled && !force) return false;
   if (batch != 1 || p.epi != KDFM_EPI_ATOMIC || amode != KDFM_LD_XC) return false;
@@ -374,7 +404,30 @@ bool wr_plan(const GemmP& p, int amode, int bmode, int64_t batch, WrPlan& pl, bo
   const int64_t Nb_all = ceil_div(p.N, 16);
   pl.slices = ceil_div(Nb_all, 24);
   const int64_t ncols_slice = ceil_div(Nb_all, pl.slices) * 16;
-  if (!wr_pick(p.M, ncols_slice, pl.w)) return false;
+  // short reductions (the 12,832-row Conformer products: S is capped by min_steps, ~100 splits)
+  // leave most of the 256 CUs idle; slice the output rows too, so every CU gets a workgroup while
+  // each workgroup's partial (and the fold's input) shrinks with its slice
+  const int64_t steps = ceil_div(p.K, 32);
+  static const int target = env_i("KDFM_WGR_WGS", 256);
+  static const int min_steps = env_i("KDFM_WGR_STEPS", 4);
+  const int msl_on = env_i("KDFM_WGR_MSL", 1);   // read per call: tests compare sliced / unsliced
+  const int64_t smax = steps / min_steps > 0 ? steps / min_steps : 1;
+  {
+    const int64_t s0 = target / pl.slices < 1 ? 1 : target / pl.slices;
+    const int64_t s_est = s0 < smax ? s0 : smax;
+    int64_t ms = msl_on ? target / (s_est * pl.slices) : 1;
+    const int64_t ms_cap = p.M / 32;   // slices of at least 32 output rows
+    if (ms > ms_cap) ms = ms_cap;
+    if (ms < 1) ms = 1;
+    pl.g.Msl = (int)(ceil_div(ceil_div(p.M, ms), 16) * 16);
+    pl.mslices = ceil_div(p.M, pl.g.Msl);
+  }
+  if (!wr_pick(pl.g.Msl, ncols_slice, pl.w)) return false;
+  const int bin8 = env_i("KDFM_WGR_BIN8", 1);   // per call, like KDFM_WGR_MSL
+  pl.bin = !bf16in ? 0
+           : (bin8 && p.M % 8 == 0 && nmem % 8 == 0 && p.sAk % 8 == 0 && p.sBk % 8 == 0 &&
+              (bmode != KDFM_LD_CONV || p.conv_c % 8 == 0)) ? 2 : 1;
+  const int cw = pl.bin == 2 ? 8 : 4;
   pl.g.wm = pl.w.wm;
   pl.g.wn = pl.w.wn;
   pl.g.Ma = 16 * pl.w.mbw * pl.w.wm;
@@ -382,24 +435,20 @@ bool wr_plan(const GemmP& p, int amode, int bmode, int64_t batch, WrPlan& pl, bo
   pl.slices = ceil_div(p.N, pl.g.Nb);
   pl.g.nmem = nmem;
   // staging units per thread: the widest slice's slab
-  const int64_t units = 8 * (p.M / 4 + (nmem < pl.g.Nb ? nmem : pl.g.Nb) / 4);
+  const int64_t units = 8 * (pl.g.Msl / cw + (nmem < pl.g.Nb ? nmem : pl.g.Nb) / cw);
   pl.upt = (int)ceil_div(units, WR_NT);
   if (pl.upt > WR_MAXU) return false;
   pl.lds = (size_t)2 * (pl.g.Ma + pl.g.Nb) * WR_LDK * sizeof(uint16_t);
   if (pl.lds > 160 * 1024) return false;
-  const int64_t steps = ceil_div(p.K, 32);
-  static const int target = env_i("KDFM_WGR_WGS", 256);
-  static const int min_steps = env_i("KDFM_WGR_STEPS", 4);
   int64_t S = target / pl.slices;
   if (S < 1) S = 1;
-  const int64_t smax = steps / min_steps > 0 ? steps / min_steps : 1;
   if (S > smax) S = smax;
   pl.g.steps_per = ceil_div(steps, S);
   pl.S = ceil_div(steps, pl.g.steps_per);
   return true;
 }
 
-template <int MBW, int NBW, bool CONV, bool BIN = false>
+template <int MBW, int NBW, bool CONV, int BIN = 0>
 int wr_launch(const GemmP& p, const WrPlan& pl, hipStream_t st) {
   static const int pd = env_i("KDFM_WGR_PD", 2);
   auto go = [&](auto kern) {
@@ -408,7 +457,7 @@ int wr_launch(const GemmP& p, const WrPlan& pl, hipStream_t st) {
              hipSuccess;
     }();
     (void)once;
-    hipLaunchKernelGGL(kern, dim3((unsigned)pl.S, (unsigned)pl.slices), dim3(WR_NT), pl.lds, st, p, pl.g);
+    hipLaunchKernelGGL(kern, dim3((unsigned)pl.S, (unsigned)pl.slices, (unsigned)pl.mslices), dim3(WR_NT), pl.lds, st, p, pl.g);
   };
   if (pl.upt <= 1) {
     if (pd >= 2) go(wgr_kernel<MBW, NBW, CONV, 2, 1, BIN>); else go(wgr_kernel<MBW, NBW, CONV, 1, 1, BIN>);
@@ -465,6 +514,27 @@ int try_wgrad_rows(const GemmP& p, int amode, int bmode, int64_t batch, hipStrea
 // ---- bf16-operand weight gradient (the fused KD-head chains' saved operands) ---------------------
 namespace kdfm {
 namespace {
+template <int BIN>
+int wr_dispatch(const GemmP& p, const WrPlan& pl, int bmode, hipStream_t st) {
+  const int key = pl.w.mbw * 10 + pl.w.nbw;
+  if (bmode == KDFM_LD_CONV) {
+    switch (key) {
+      case 32: return wr_launch<3, 2, true, BIN>(p, pl, st);
+      case 33: return wr_launch<3, 3, true, BIN>(p, pl, st);
+      case 34: return wr_launch<3, 4, true, BIN>(p, pl, st);
+      case 36: return wr_launch<3, 6, true, BIN>(p, pl, st);
+      default: return wr_launch<6, 3, true, BIN>(p, pl, st);
+    }
+  }
+  switch (key) {
+    case 32: return wr_launch<3, 2, false, BIN>(p, pl, st);
+    case 33: return wr_launch<3, 3, false, BIN>(p, pl, st);
+    case 34: return wr_launch<3, 4, false, BIN>(p, pl, st);
+    case 36: return wr_launch<3, 6, false, BIN>(p, pl, st);
+    default: return wr_launch<6, 3, false, BIN>(p, pl, st);
+  }
+}
+
 GemmP wgrad_bf16_params(const uint16_t* dY, const uint16_t* X, float* dW, int64_t ldc, float* db, int64_t rows,
                         int64_t M, int64_t N, float alpha, float* ws, int64_t ws_len) {
   GemmP p{};
@@ -502,28 +572,10 @@ void conv_geometry(GemmP& p, int64_t C, int taps, int pad, int64_t T) {
 
 int wgrad_bf16_run(const GemmP& p, int bmode, hipStream_t st) {
   WrPlan pl;
-  KDFM_REQUIRE(wr_plan(p, KDFM_LD_XC, bmode, 1, pl, true), "shape not supported by the row-parallel kernel");
+  KDFM_REQUIRE(wr_plan(p, KDFM_LD_XC, bmode, 1, pl, true, true), "shape not supported by the row-parallel kernel");
   KDFM_REQUIRE(p.ws_len >= pl.S * p.M * p.N, "workspace too small (kdfm_wgrad_bf16*_ws)");
   set_route(ROUTE_WGRAD_ROWS);
-  int rc;
-  const int key = pl.w.mbw * 10 + pl.w.nbw;
-  if (bmode == KDFM_LD_CONV) {
-    switch (key) {
-      case 32: rc = wr_launch<3, 2, true, true>(p, pl, st); break;
-      case 33: rc = wr_launch<3, 3, true, true>(p, pl, st); break;
-      case 34: rc = wr_launch<3, 4, true, true>(p, pl, st); break;
-      case 36: rc = wr_launch<3, 6, true, true>(p, pl, st); break;
-      default: rc = wr_launch<6, 3, true, true>(p, pl, st); break;
-    }
-  } else {
-    switch (key) {
-      case 32: rc = wr_launch<3, 2, false, true>(p, pl, st); break;
-      case 33: rc = wr_launch<3, 3, false, true>(p, pl, st); break;
-      case 34: rc = wr_launch<3, 4, false, true>(p, pl, st); break;
-      case 36: rc = wr_launch<3, 6, false, true>(p, pl, st); break;
-      default: rc = wr_launch<6, 3, false, true>(p, pl, st); break;
-    }
-  }
+  const int rc = pl.bin == 2 ? wr_dispatch<2>(p, pl, bmode, st) : wr_dispatch<1>(p, pl, bmode, st);
   if (rc) return rc;
   hipLaunchKernelGGL(wgr_fold_kernel, dim3((unsigned)ceil_div(p.M * p.N, 64)), dim3(64 * WF_WAVES), 0, st, p, pl.S);
   return check_launch("kdfm_wgrad_bf16(fold)");
@@ -538,7 +590,7 @@ int64_t kdfm_wgrad_bf16_ws(int64_t rows, int64_t M, int64_t N, int32_t bias) {
   GemmP p = wgrad_bf16_params(reinterpret_cast<const uint16_t*>(16), reinterpret_cast<const uint16_t*>(16), nullptr, N,
                               bias ? reinterpret_cast<float*>(16) : nullptr, rows, M, N, 1.f, nullptr, 0);
   WrPlan pl;
-  if (!wr_plan(p, KDFM_LD_XC, KDFM_LD_XC, 1, pl, true)) return -1;
+  if (!wr_plan(p, KDFM_LD_XC, KDFM_LD_XC, 1, pl, true, true)) return -1;
   return pl.S * p.M * p.N;
 }
 
@@ -559,7 +611,7 @@ int64_t kdfm_wgrad_bf16_conv_ws(int64_t rows, int64_t M, int64_t C, int32_t taps
                               taps * C, bias ? reinterpret_cast<float*>(16) : nullptr, rows, M, taps * C, 1.f, nullptr, 0);
   conv_geometry(p, C, taps, pad, T);
   WrPlan pl;
-  if (!wr_plan(p, KDFM_LD_XC, KDFM_LD_CONV, 1, pl, true)) return -1;
+  if (!wr_plan(p, KDFM_LD_XC, KDFM_LD_CONV, 1, pl, true, true)) return -1;
   return pl.S * p.M * p.N;
 }
 

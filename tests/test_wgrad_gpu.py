@@ -71,3 +71,86 @@ def test_conv3_dw_rows(B, T):
     ref = 0.5 * gW.permute(0, 2, 1).reshape(C, 3 * C)   # GEMM layout G[o, tap*C + c]
     assert (G.double() - ref).abs().max().item() <= 2e-2 * ref.abs().max().item()
     assert (db.double() - 0.5 * gb).abs().max().item() <= 2e-2 * (0.5 * gb).abs().max().item()
+
+
+@pytest.mark.parametrize("R,M,N", [(12832, 352, 88), (12832, 88, 352), (12832, 176, 88), (4097, 96, 88)])
+def test_m_slices_bitwise(R, M, N, monkeypatch):
+    """Output-row slicing (blockIdx.z, for short reductions) changes which workgroup owns an output
+    row, not the row order of any sum: the sliced result equals the unsliced one bit for bit."""
+    from kdfm import kernels as K
+    g = torch.Generator(device="cuda").manual_seed(7 * R + M)
+    dy = torch.randn(R, M, device="cuda", generator=g)
+    x = torch.randn(R, N, device="cuda", generator=g)
+    out = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("KDFM_WGR_MSL", flag)
+        dW, db = torch.zeros(M, N, device="cuda"), torch.zeros(M, device="cuda")
+        with K.mode("bf16"):
+            K.linear_dw(dy, x, dW, alpha=1.0, db=db)
+        assert _route() == "wgrad_rows"
+        out.append((dW, db))
+    torch.cuda.synchronize()
+    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
+
+
+BF16_SHAPES = [  # rows, M, N, bias: multiples of 8 (8-column staging units) and of 4 only (4-column units)
+    (12832, 352, 88, True), (12832, 88, 352, True), (12832, 88, 88, True), (205312 // 4, 96, 96, True),
+    (4097, 264, 88, False), (12832, 84, 92, True), (3001, 20, 36, True),
+]
+
+
+def _bf16_ref(dy, x, alpha):
+    return alpha * (dy.double().T @ x.double()), alpha * dy.double().sum(0)
+
+
+@pytest.mark.parametrize("R,M,N,bias", BF16_SHAPES)
+def test_wgrad_bf16_units(R, M, N, bias, monkeypatch):
+    """kdfm_wgrad_bf16 (bf16 row operands): against float64 on the same bf16 values (exact products,
+    f32 accumulation: 1e-5 relative), and the 8-column staging units bitwise equal to the 4-column
+    ones (same LDS image, same MFMA order)."""
+    from kdfm import kernels as K
+    g = torch.Generator(device="cuda").manual_seed(R * 3 + M + N)
+    dy = torch.randn(R, M, device="cuda", generator=g).to(torch.bfloat16)
+    x = torch.randn(R, N, device="cuda", generator=g).to(torch.bfloat16)
+    rw, rb = _bf16_ref(dy, x, 0.75)
+    out = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("KDFM_WGR_BIN8", flag)
+        dW = torch.zeros(M, N, device="cuda")
+        db = torch.zeros(M, device="cuda") if bias else None
+        K.wgrad_bf16(dy, x, dW, db=db, alpha=0.75)
+        torch.cuda.synchronize()
+        assert (dW.double() - rw).abs().max().item() <= 1e-5 * rw.abs().max().item() + 1e-6
+        if bias:
+            assert (db.double() - rb).abs().max().item() <= 1e-5 * rb.abs().max().item() + 1e-6
+        out.append((dW, db))
+    assert torch.equal(out[0][0], out[1][0])
+    if bias:
+        assert torch.equal(out[0][1], out[1][1])
+
+
+@pytest.mark.parametrize("B,T,C", [(64, 401, 96), (9, 123, 44)])
+def test_wgrad_bf16_conv_units(B, T, C, monkeypatch):
+    """kdfm_wgrad_bf16_conv (SimpleDenoiser Conv1d(k=3) over utterances of T frames), 8- and
+    4-column staging units, against float64 conv1d autograd on the same bf16 values."""
+    from kdfm import kernels as K
+    g = torch.Generator(device="cuda").manual_seed(B * T + C)
+    x = torch.randn(B, T, C, device="cuda", generator=g).to(torch.bfloat16)
+    dy = torch.randn(B, T, C, device="cuda", generator=g).to(torch.bfloat16)
+    xr = x.double().transpose(1, 2).requires_grad_(True)
+    W = torch.zeros(C, C, 3, dtype=torch.float64, device="cuda", requires_grad=True)
+    bb = torch.zeros(C, dtype=torch.float64, device="cuda", requires_grad=True)
+    out = torch.nn.functional.conv1d(xr, W, bb, padding=1)
+    gW, gb = torch.autograd.grad(out, [W, bb], dy.double().transpose(1, 2))
+    ref = gW.permute(0, 2, 1).reshape(C, 3 * C)
+    res = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("KDFM_WGR_BIN8", flag)
+        G = torch.zeros(C, 3 * C, device="cuda")
+        db = torch.zeros(C, device="cuda")
+        K.wgrad_bf16_conv(dy.view(B * T, C), x.view(B * T, C), G, T, db=db)
+        torch.cuda.synchronize()
+        assert (G.double() - ref).abs().max().item() <= 1e-5 * ref.abs().max().item() + 1e-6
+        assert (db.double() - gb).abs().max().item() <= 1e-5 * gb.abs().max().item() + 1e-6
+        res.append(G)
+    assert torch.equal(res[0], res[1])

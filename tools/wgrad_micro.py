@@ -46,3 +46,37 @@ for name, R, M, Kd, conv in cases:
     us = e0.elapsed_time(e1) / n * 1e3
     nbytes = 4.0 * (R * M + R * Kd + M * (G.shape[1] + 1))
     print(f"{name:12s} R={R:6d} M={M:3d} N={G.shape[1]:4d}  {us:8.1f} us  {nbytes / us / 1e3:7.1f} GB/s  route={K.ROUTES.get(int(K._lib.lib().kdfm_gemm_last_route()))}")
+
+# bf16 row operands (kdfm_wgrad_bf16 / _conv: the fused kernels' saved operands), bytes at 2 B/element
+bcases = [("ffn W2", 12832, 88, 352), ("ffn W1", 12832, 352, 88), ("qkv", 12832, 264, 88), ("out", 12832, 88, 88),
+          ("fm dW1x", 205312, 96, 96), ("fm dW2", 8 * 205312, 96, 96), ("deno conv3", 9 * 205312, 96, 96)]
+for name, R, M, N in bcases:
+    conv = name.startswith("deno")
+    dy = torch.randn(R, M, device=dev).to(torch.bfloat16)
+    x = torch.randn(R, N, device=dev).to(torch.bfloat16)
+    G = torch.zeros(M, 3 * N if conv else N, device=dev)
+    db = torch.zeros(M, device=dev)
+    def run():
+        if conv:
+            K.wgrad_bf16_conv(dy, x, G, 401, db=db)
+        else:
+            K.wgrad_bf16(dy, x, G, db=db)
+    for _ in range(3):
+        run()
+    torch.cuda.synchronize()
+    n = 10
+    gr = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(gr):
+        for _ in range(n):
+            run()
+    gr.replay()
+    torch.cuda.synchronize()
+    e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
+    e0.record()
+    gr.replay()
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) / n * 1e3
+    nbytes = 2.0 * R * (M + N) + 8.0 * M * (G.shape[1] + 1)
+    print(f"bf16 {name:10s} R={R:7d} M={M:3d} N={G.shape[1]:4d}  {us:8.1f} us  {nbytes / us / 1e3:7.1f} GB/s", flush=True)
+    del dy, x
