@@ -408,7 +408,11 @@ bool wr_plan(const GemmP& p, int amode, int bmode, int64_t batch, WrPlan& pl, bo
   // leave most of the 256 CUs idle; slice the output rows too, so every CU gets a workgroup while
   // each workgroup's partial (and the fold's input) shrinks with its slice
   const int64_t steps = ceil_div(p.K, 32);
-  static const int target = env_i("KDFM_WGR_WGS", 256);
+  // workgroup target: two per CU where the LDS images allow it (more slabs in flight: the FM-chain
+  // products went 247 -> 164 us at 1.64M rows); the 3-tap CONV images are wide, one per CU
+  // (tools/gpu_wgr_wgs.sh, profiles/r02/wgs_*.log)
+  static const int target_env = env_i("KDFM_WGR_WGS", 0);
+  const int target = target_env > 0 ? target_env : (bmode == KDFM_LD_CONV ? 256 : 512);
   static const int min_steps = env_i("KDFM_WGR_STEPS", 4);
   const int msl_on = env_i("KDFM_WGR_MSL", 1);   // read per call: tests compare sliced / unsliced
   const int64_t smax = steps / min_steps > 0 ? steps / min_steps : 1;

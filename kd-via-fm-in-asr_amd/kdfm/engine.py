@@ -20,6 +20,18 @@ from .conformer import EncoderRun, EncoderShapes, compute_lengths, encoder_backw
 from .frontend import FrontendConsts, frontend_forward, mel_frames, specaugment_
 from .heads import HeadsWorkspace, heads_backward, heads_forward
 from .overlap import WGRAD
+
+# Stream priorities (KDFM_STREAM_PRIO=1): the critical-path streams (the compute stream that carries
+# the student chain and the backward, the teacher stream that bounds the forward, the CTC/KL stream the
+# heads join on) are created high-priority, the weight-gradient stream keeps the default low one, so
+# the dispatcher hands freed CUs to the critical path first when both have workgroups waiting.
+# Off by default: measured 19.2 -> 25.8 ms per step on ROCm 7 (profiles/r02/prio_bench_*.log) --
+# the high-priority streams lose their overlap with each other.
+_PRIO = __import__("os").environ.get("KDFM_STREAM_PRIO", "0") == "1"
+
+
+def _crit_stream(dev):
+    return torch.cuda.Stream(dev, priority=-1) if _PRIO else torch.cuda.Stream(dev)
 from .store import FlatStore, init_uniform
 
 SALT_STUDENT, SALT_TEACHER, SALT_FRONT = 1, 2, 3
@@ -80,7 +92,7 @@ class Ver5Engine:
         # the step runs on a created (non-null) stream: ROCm makes the legacy null stream wait for a
         # HIP graph replayed on any other stream (tools/graph_probe.py), which serialised the teacher
         # graph and the whole-step graph's branches behind the main stream
-        self.compute_stream = torch.cuda.Stream(dev) if dev.type == "cuda" else None
+        self.compute_stream = _crit_stream(dev) if dev.type == "cuda" else None
         self._link_in, self._link_out = K.StreamLink(), K.StreamLink()   # caller <-> compute stream
         # capture the frozen teacher as a HIP graph in training steps (KDFM_TEACHER_GRAPH=0: eager)
         self.teacher_graph = __import__("os").environ.get("KDFM_TEACHER_GRAPH", "0") == "1"
@@ -115,7 +127,7 @@ class Ver5Engine:
 
     def _side_stream(self):
         if getattr(self, "_side", None) is None:
-            self._side = torch.cuda.Stream(self.device)
+            self._side = _crit_stream(self.device)
         return self._side
 
     def _teacher_forward(self, mel_t, mel_len, len1, len2, tfeats, tlogits, St, T):
@@ -365,7 +377,7 @@ class Ver5Engine:
 
     def _aux_stream(self):
         if getattr(self, "_aux", None) is None:
-            self._aux = torch.cuda.Stream(self.device)
+            self._aux = _crit_stream(self.device)
         return self._aux
 
     def _join_losses(self, ctx):
