@@ -147,6 +147,13 @@ int kdfm_gemm(const kdfm_gemm_desc* d, void* stream);
 int64_t kdfm_wgrad_bf16_ws(int64_t rows, int64_t M, int64_t N, int32_t bias);
 int kdfm_wgrad_bf16(const uint16_t* dY, const uint16_t* X, float* dW, int64_t ldc, float* db, int64_t rows,
                     int64_t M, int64_t N, float alpha, float* ws, int64_t ws_len, void* stream);
+/* The same over nseg = rows / seg_rows stacked segments (seg_rows % 32 == 0, nseg <= 16) with one bias
+ * gradient per segment: db[j][m] += alpha * sum_{r in segment j} dY[r][m] (db is (nseg, M), required),
+ * dW summed over all rows -- the FM chain's first-layer weight over its S steps in one launch
+ * (asr_train_diffm.py:1368-1427: W1 is shared by the steps, the time-conditioned bias is per step). */
+int64_t kdfm_wgrad_bf16_seg_ws(int64_t rows, int64_t M, int64_t N, int64_t seg_rows);
+int kdfm_wgrad_bf16_seg(const uint16_t* dY, const uint16_t* X, float* dW, int64_t ldc, float* db, int64_t seg_rows,
+                        int64_t rows, int64_t M, int64_t N, float alpha, float* ws, int64_t ws_len, void* stream);
 /* The same for a Conv1d(C -> M, taps, padding pad) over utterances of T frames (rows % T == 0):
  *   dW[m][tap*C + c] += alpha * sum_r dY[r][m] * X[r + tap - pad][c]   (0 outside the utterance)
  * in the GEMM weight layout of kdfm_convw_prep (re-laid out by kdfm_convw_grad); the weight gradient

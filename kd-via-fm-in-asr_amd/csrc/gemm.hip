@@ -427,7 +427,7 @@ extern "C" int kdfm_gemm(const kdfm_gemm_desc* d, void* stream) {
   if (d->amode == KDFM_LD_CONV || d->bmode == KDFM_LD_CONV)
     KDFM_REQUIRE(d->conv_c > 0 && d->conv_t > 0 && d->conv_taps > 0, "conv mode needs conv_c/conv_t/taps");
   KDFM_REQUIRE(!(d->amode == KDFM_LD_CONV && d->bmode == KDFM_LD_CONV), "only one CONV operand");
-  P p;
+  P p{};   // value-initialised: fields a descriptor does not carry (partial, nseg, ...) start at 0
   p.A = d->A; p.B = d->B; p.C = d->C; p.bias = d->bias; p.R = d->R; p.aux = d->aux; p.Cpre = d->Cpre;
   p.M = d->M; p.N = d->N; p.K = d->K;
   p.sAm = d->sAm; p.sAk = d->sAk; p.sBk = d->sBk; p.sBn = d->sBn; p.sCm = d->sCm; p.sCn = d->sCn;

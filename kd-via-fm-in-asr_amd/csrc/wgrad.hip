@@ -93,8 +93,9 @@ __global__ __launch_bounds__(WR_NT, 2) void wgr_kernel(GemmP p, WrGeo g) {
       img = buf * bufsz + ia;
       c = col - g.Ma;
       const int64_t n = n0 + c;
-      one = (p.ones_col >= 0 && n == p.ones_col);
-      zero = !one && (c >= ncols_mem);
+      one = p.nseg <= 1 && p.ones_col >= 0 && n == p.ones_col;   // segment columns: per slab (stage)
+      const bool segc = p.nseg > 1 && n >= p.ones_col && n < p.ones_col + p.nseg;   // written by stage()
+      zero = !one && !segc && (c >= ncols_mem);
     }
     if (zero || one) {
       const uint16_t v = one ? (uint16_t)0x3F80 : (uint16_t)0;  // bf16(1.0) = 0x3F80
@@ -178,7 +179,20 @@ __global__ __launch_bounds__(WR_NT, 2) void wgr_kernel(GemmP p, WrGeo g) {
       }
     }
   };
-  auto stage = [&](const float4 (&r)[UPT][4], uint32_t m, int buf) {
+  auto stage = [&](const float4 (&r)[UPT][4], uint32_t m, int buf, int64_t k0) {
+    if (p.nseg > 1) {
+      // per-segment ones columns (a slab never straddles segments: seg_rows % 32 == 0): column
+      // ones_col + j is 1 in the slab's rows iff the slab lies in segment j
+      const int t = threadIdx.x;
+      if (t < 4 * p.nseg) {
+        const int sc = t >> 2;
+        const uint16_t v = (sc == (int)(k0 / p.seg_rows)) ? (uint16_t)0x3F80 : (uint16_t)0;
+        bf16x8 pk;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) pk[i] = (short)v;
+        *lds_at<bf16x8>(wr_lds, buf * bufsz + ia + (int)(p.ones_col - n0 + sc) * WR_LDK + (t & 3) * 8) = pk;
+      }
+    }
 #pragma unroll
     for (int i = 0; i < UPT; ++i) {
       const int u = threadIdx.x + i * WR_NT;
@@ -268,14 +282,14 @@ __global__ __launch_bounds__(WR_NT, 2) void wgr_kernel(GemmP p, WrGeo g) {
   if constexpr (PD == 1) {
     if (nsteps > 0) {
       load(reg[0], msk[0], kb);
-      stage(reg[0], msk[0], 0);
+      stage(reg[0], msk[0], 0, kb);
     }
     __syncthreads();
     int buf = 0;
     for (int64_t s = 0; s < nsteps; ++s) {
       if (s + 1 < nsteps) load(reg[0], msk[0], kb + 32 * (s + 1));
       mfma_step(buf);
-      if (s + 1 < nsteps) stage(reg[0], msk[0], buf ^ 1);
+      if (s + 1 < nsteps) stage(reg[0], msk[0], buf ^ 1, kb + 32 * (s + 1));
       __syncthreads();
       buf ^= 1;
     }
@@ -284,19 +298,19 @@ __global__ __launch_bounds__(WR_NT, 2) void wgr_kernel(GemmP p, WrGeo g) {
     // compiler waits only for the older slot's loads before staging it)
     if (nsteps > 0) load(reg[0], msk[0], kb);
     if (nsteps > 1) load(reg[1], msk[1], kb + 32);
-    if (nsteps > 0) stage(reg[0], msk[0], 0);
+    if (nsteps > 0) stage(reg[0], msk[0], 0, kb);
     __syncthreads();
     for (int64_t s = 0; s < nsteps; s += 2) {
       // even step s in buffer 0
       if (s + 2 < nsteps) load(reg[0], msk[0], kb + 32 * (s + 2));
       mfma_step(0);
-      if (s + 1 < nsteps) stage(reg[1], msk[1], 1);
+      if (s + 1 < nsteps) stage(reg[1], msk[1], 1, kb + 32 * (s + 1));
       __syncthreads();
       if (s + 1 >= nsteps) break;
       // odd step s+1 in buffer 1
       if (s + 3 < nsteps) load(reg[1], msk[1], kb + 32 * (s + 3));
       mfma_step(1);
-      if (s + 2 < nsteps) stage(reg[0], msk[0], 0);
+      if (s + 2 < nsteps) stage(reg[0], msk[0], 0, kb + 32 * (s + 2));
       __syncthreads();
     }
   }
@@ -345,8 +359,8 @@ __global__ __launch_bounds__(64 * WF_WAVES) void wgr_fold_kernel(GemmP p, int64_
     for (int i = 0; i < WF_WAVES; ++i) v += red[i][lane];
     v *= p.alpha;
     const int64_t m = e / p.N, n = e - m * p.N;
-    if (n == p.ones_col)
-      p.ones_out[m] += v;
+    if (p.ones_col >= 0 && n >= p.ones_col)   // bias column(s): segment j -> ones_out[j][m]
+      p.ones_out[(n - p.ones_col) * p.M + m] += v;
     else
       p.C[m * p.sCm + n * p.sCn] += v;
   }
@@ -394,7 +408,10 @@ bool wr_plan(const GemmP& p, int amode, int bmode, int64_t batch, WrPlan& pl, bo
   if (bmode != KDFM_LD_XC && bmode != KDFM_LD_CONV) return false;
   if (p.sAm != 1 || (p.sAk & 3) || (p.M & 3) || (((uintptr_t)p.A) & 15)) return false;
   if (p.sBn != 1 || (p.sBk & 3) || (((uintptr_t)p.B) & 15)) return false;
-  if (p.ones_col >= 0 && p.ones_col != p.N - 1) return false;
+  const int nseg = p.nseg > 1 ? p.nseg : 1;
+  if (p.ones_col >= 0 && p.ones_col != p.N - nseg) return false;
+  if (nseg > 1 && (p.ones_col < 0 || nseg > 16 || p.seg_rows <= 0 || p.seg_rows % 32 || p.K != nseg * p.seg_rows))
+    return false;
   const int64_t nmem = p.ones_col >= 0 ? p.ones_col : p.N;
   if (nmem & 3) return false;
   if (bmode == KDFM_LD_CONV && ((p.conv_c & 3) || p.taps < 1 || p.pad < 0 || nmem != p.taps * p.conv_c)) return false;
@@ -403,18 +420,22 @@ bool wr_plan(const GemmP& p, int amode, int bmode, int64_t batch, WrPlan& pl, bo
   // column slices of at most 24 16-wide blocks (a (6,3) wave tile on a 1x8 wave grid)
   const int64_t Nb_all = ceil_div(p.N, 16);
   pl.slices = ceil_div(Nb_all, 24);
+  if (nseg > 1 && pl.slices != 1) return false;   // the segment columns live in the one slice
   const int64_t ncols_slice = ceil_div(Nb_all, pl.slices) * 16;
   // short reductions (the 12,832-row Conformer products: S is capped by min_steps, ~100 splits)
   // leave most of the 256 CUs idle; slice the output rows too, so every CU gets a workgroup while
   // each workgroup's partial (and the fold's input) shrinks with its slice
   const int64_t steps = ceil_div(p.K, 32);
-  // workgroup target: two per CU where the LDS images allow it (more slabs in flight: the FM-chain
-  // products went 247 -> 164 us at 1.64M rows); the 3-tap CONV images are wide, one per CU
-  // (tools/gpu_wgr_wgs.sh, profiles/r02/wgs_*.log)
-  static const int target_env = env_i("KDFM_WGR_WGS", 0);
-  const int target = target_env > 0 ? target_env : (bmode == KDFM_LD_CONV ? 256 : 512);
+  // workgroup target.  Isolated, two per CU is faster for the non-CONV products (FM dW2 at 1.64M
+  // rows 247 -> 164 us, tools/gpu_wgr_wgs.sh, profiles/r02/wgs_*.log); inside the step, where these
+  // run on the weight-gradient stream beside the critical-path kernels, one per CU wins (bench
+  // 1655 -> 1686 utt/s, tools/gpu_wgr_env_ab.sh, profiles/r02/envab_*.log)
+  static const int target = env_i("KDFM_WGR_WGS", 256);
   static const int min_steps = env_i("KDFM_WGR_STEPS", 4);
-  const int msl_on = env_i("KDFM_WGR_MSL", 1);   // read per call: tests compare sliced / unsliced
+  // off by default: isolated the slices help (FFN W1 25 -> 19 us) but in the step the extra
+  // workgroups queue behind the critical-path kernels (bench 1687 unsliced vs 1635 sliced at
+  // target 256, profiles/r02/envab_*.log).  Read per call: tests compare sliced / unsliced.
+  const int msl_on = env_i("KDFM_WGR_MSL", 0);
   const int64_t smax = steps / min_steps > 0 ? steps / min_steps : 1;
   {
     const int64_t s0 = target / pl.slices < 1 ? 1 : target / pl.slices;
@@ -606,6 +627,39 @@ int kdfm_wgrad_bf16(const uint16_t* dY, const uint16_t* X, float* dW, int64_t ld
   KDFM_REQUIRE(((((uintptr_t)dY) | ((uintptr_t)X)) & 15) == 0, "operands must be 16-byte aligned");
   KDFM_REQUIRE(ldc >= N, "ldc < N");
   GemmP p = wgrad_bf16_params(dY, X, dW, ldc, db, rows, M, N, alpha, ws, ws_len);
+  return wgrad_bf16_run(p, KDFM_LD_XC, as_stream(stream));
+}
+
+int64_t kdfm_wgrad_bf16_seg_ws(int64_t rows, int64_t M, int64_t N, int64_t seg_rows) {
+  using namespace kdfm;
+  if (seg_rows <= 0 || rows % seg_rows) return -1;
+  GemmP p = wgrad_bf16_params(reinterpret_cast<const uint16_t*>(16), reinterpret_cast<const uint16_t*>(16), nullptr, N,
+                              nullptr, rows, M, N, 1.f, nullptr, 0);
+  p.nseg = (int)(rows / seg_rows);
+  p.seg_rows = seg_rows;
+  p.N = N + p.nseg;
+  p.ones_col = N;
+  p.ones_out = reinterpret_cast<float*>(16);
+  WrPlan pl;
+  if (!wr_plan(p, KDFM_LD_XC, KDFM_LD_XC, 1, pl, true, true)) return -1;
+  return pl.S * p.M * p.N;
+}
+
+int kdfm_wgrad_bf16_seg(const uint16_t* dY, const uint16_t* X, float* dW, int64_t ldc, float* db, int64_t seg_rows,
+                        int64_t rows, int64_t M, int64_t N, float alpha, float* ws, int64_t ws_len, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(dY && X && dW && db && ws, "null pointer");
+  KDFM_REQUIRE(rows > 0 && M > 0 && N > 0 && M % 4 == 0 && N % 4 == 0, "M, N must be positive multiples of 4");
+  KDFM_REQUIRE(seg_rows > 0 && seg_rows % 32 == 0 && rows % seg_rows == 0 && rows / seg_rows <= 16,
+               "seg_rows must be a multiple of 32 dividing rows into at most 16 segments");
+  KDFM_REQUIRE(((((uintptr_t)dY) | ((uintptr_t)X)) & 15) == 0, "operands must be 16-byte aligned");
+  KDFM_REQUIRE(ldc >= N, "ldc < N");
+  GemmP p = wgrad_bf16_params(dY, X, dW, ldc, nullptr, rows, M, N, alpha, ws, ws_len);
+  p.nseg = (int)(rows / seg_rows);
+  p.seg_rows = seg_rows;
+  p.N = N + p.nseg;
+  p.ones_col = N;
+  p.ones_out = db;
   return wgrad_bf16_run(p, KDFM_LD_XC, as_stream(stream));
 }
 

@@ -101,6 +101,8 @@ SIGNATURES: dict[str, tuple] = {
     "kdfm_ffn_bwd": (_i32, [P, P, P, P, P, P, P, P, P, P, P, P, P, P, _i64, _i64, _i64, _f32, _f32, _f32, P,
                             C.c_uint64, C.c_uint64, P]),
     "kdfm_fm_chain_bwd": (_i32, [P, P, P, P, _i64, P, P, P, P, P, _i64, _i32, _i32, P]),
+    "kdfm_wgrad_bf16_seg_ws": (_i64, [_i64, _i64, _i64, _i64]),
+    "kdfm_wgrad_bf16_seg": (_i32, [P, P, P, _i64, P, _i64, _i64, _i64, _i64, _f32, P, _i64, P]),
     "kdfm_wgrad_bf16_conv_ws": (_i64, [_i64, _i64, _i64, _i32, _i32, _i64, _i32]),
     "kdfm_wgrad_bf16_conv": (_i32, [P, P, P, _i64, P, _i64, _i64, _i64, _i32, _i32, _i64, _f32, P, _i64, P]),
     "kdfm_denoise_wimg_elems": (_i64, []),

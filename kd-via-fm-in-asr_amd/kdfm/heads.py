@@ -162,8 +162,13 @@ def _fm_backward(cfg, P, G, ws, c, gxs, dev):
         K.fill(dc, 0.0)
         WGRAD.run(lambda: K.wgrad_bf16(DV.view(S_ * n, Lt), A.view(S_ * n, Lt), G[pre + "meta_encoder.2.weight"],
                                        db=G[pre + "meta_encoder.2.bias"]), DV, A)
-        for j in range(S_):
-            WGRAD.run(lambda j=j: K.wgrad_bf16(DA[j], X[j], dW1x, db=dc[j]), DA, X)
+        # dW1x over all S_ steps' rows in one launch, with the per-step bias grads dc_j as segment
+        # columns (kdfm_wgrad_bf16_seg; was S_ launches + S_ folds)
+        if K.wgrad_bf16_seg_ok(S_ * n, Lt, Lt, n):
+            WGRAD.run(lambda: K.wgrad_bf16_seg(DA.view(S_ * n, Lt), X.view(S_ * n, Lt), dW1x, dc, n), DA, X)
+        else:
+            for j in range(S_):
+                WGRAD.run(lambda j=j: K.wgrad_bf16(DA[j], X[j], dW1x, db=dc[j]), DA, X)
         # dc is produced on the side stream: fold it there too (no main-stream join)
         WGRAD.run(lambda: K.fm_time_bwd(dc, evec, W1, dW1, G[pre + "meta_encoder.0.bias"],
                                         G[pre + "time_embed.weight"].view(-1), G[pre + "time_embed.bias"], Lt, E, S_))

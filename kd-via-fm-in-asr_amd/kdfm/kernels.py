@@ -653,6 +653,27 @@ def wgrad_bf16(dY, X, dW, *, db=None, alpha=1.0):
             ptr(_bf16(X)), ptr(_f32(dW)), dW.stride(0), ptr(db), rows, M, N, float(alpha), ptr(ws), ws.numel(), _s())
 
 
+def wgrad_bf16_seg_ok(rows, M, N, seg_rows) -> bool:
+    return int(_lib.lib().kdfm_wgrad_bf16_seg_ws(int(rows), int(M), int(N), int(seg_rows))) >= 0
+
+
+def wgrad_bf16_seg(dY, X, dW, db, seg_rows, *, alpha=1.0):
+    """dW[m, n] += alpha * dY[:, m]^T X[:, n] over all rows, and one bias gradient per stacked segment
+    of seg_rows rows: db[j, m] += alpha * sum_{r in segment j} dY[r, m] (one launch + one fold)."""
+    rows, M = dY.shape
+    N = X.shape[1]
+    nseg = rows // seg_rows
+    assert X.shape[0] == rows and dW.shape == (M, N) and dW.stride(1) == 1, (dY.shape, X.shape, dW.shape)
+    assert dY.is_contiguous() and X.is_contiguous() and db.shape == (nseg, M) and db.is_contiguous()
+    n = int(_lib.lib().kdfm_wgrad_bf16_seg_ws(rows, M, N, seg_rows))
+    if n < 0:
+        raise _lib.KdfmError(f"kdfm_wgrad_bf16_seg: unsupported shape rows={rows} M={M} N={N} seg_rows={seg_rows}")
+    ws = scratch(dY.device, n)
+    _traced("wgrad_bf16", 2.0 * rows * M * N, 2.0 * rows * (M + N) + 8.0 * M * N, "kdfm_wgrad_bf16_seg",
+            ptr(_bf16(dY)), ptr(_bf16(X)), ptr(_f32(dW)), dW.stride(0), ptr(_f32(db)), seg_rows, rows, M, N,
+            float(alpha), ptr(ws), ws.numel(), _s())
+
+
 def fm_chain_fwd(x0, zt, W1, cvec, W2, b2, Wst, bst, X, A, nsx, dtr, xS, loss, inv, S):
     n, L = x0.shape
     assert zt.shape == (n, L) and dtr.shape == (n, L) and W1.stride(1) == 1 and cvec.shape[0] >= S

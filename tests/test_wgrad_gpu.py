@@ -154,3 +154,27 @@ def test_wgrad_bf16_conv_units(B, T, C, monkeypatch):
         assert (db.double() - gb).abs().max().item() <= 1e-5 * gb.abs().max().item() + 1e-6
         res.append(G)
     assert torch.equal(res[0], res[1])
+
+
+@pytest.mark.parametrize("nseg,seg,M,N", [(8, 205312 // 16, 96, 96), (3, 4096, 88, 352), (1, 2048, 96, 96),
+                                          (16, 64, 20, 36)])
+def test_wgrad_bf16_segments(nseg, seg, M, N):
+    """kdfm_wgrad_bf16_seg (one launch over stacked segments, per-segment bias columns) against float64
+    on the same bf16 values: dW over all rows, db[j] over segment j only."""
+    from kdfm import kernels as K
+    R = nseg * seg
+    g = torch.Generator(device="cuda").manual_seed(nseg * 1000 + seg + M)
+    dy = torch.randn(R, M, device="cuda", generator=g).to(torch.bfloat16)
+    x = torch.randn(R, N, device="cuda", generator=g).to(torch.bfloat16)
+    W0 = torch.randn(M, N + 5, device="cuda", generator=g)
+    dW = W0.clone()
+    db = torch.ones(nseg, M, device="cuda")
+    assert K.wgrad_bf16_seg_ok(R, M, N, seg)
+    K.wgrad_bf16_seg(dy, x, dW[:, :N], db, seg, alpha=-0.5)
+    torch.cuda.synchronize()
+    rw = -0.5 * (dy.double().T @ x.double())
+    rb = 1.0 - 0.5 * dy.double().view(nseg, seg, M).sum(1)
+    assert (dW[:, :N].double() - W0[:, :N].double() - rw).abs().max().item() <= 1e-5 * rw.abs().max().item() + 1e-5
+    assert torch.equal(dW[:, N:], W0[:, N:])   # ldc > N: columns past N untouched
+    assert (db.double() - rb).abs().max().item() <= 1e-5 * rb.abs().max().item() + 1e-5
+    assert not K.wgrad_bf16_seg_ok(R + 32, M, N, seg)   # rows must be whole segments

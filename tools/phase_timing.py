@@ -12,6 +12,7 @@ from kdfm import kernels as K  # noqa: E402
 from kdfm.config import DEFAULT  # noqa: E402
 from kdfm.conformer import EncoderShapes, encoder_backward, encoder_forward  # noqa: E402
 from kdfm.engine import Ver5Engine, synthetic_batch  # noqa: E402
+from kdfm.overlap import WGRAD  # noqa: E402
 from kdfm.frontend import frontend_forward, mel_frames  # noqa: E402
 from kdfm.heads import heads_backward, heads_forward  # noqa: E402
 
@@ -28,6 +29,7 @@ ev = {}
 
 
 def mark(name):
+    WGRAD.join()   # side-stream weight gradients of the phase count in the phase
     e = torch.cuda.Event(enable_timing=True)
     e.record()
     ev[name] = e
@@ -60,8 +62,8 @@ for rep in range(2):
                     use_batch_stats=False, ws=eng._enc_ws(St))
     mark("teacher_fwd")
     n = cfg.n_layers * Ss.rows
-    acc = torch.zeros(3, device=dev)
-    hctx = heads_forward(cfg, eng.student.P, sfeats.view(n, Ss.d), tfeats.view(n, St.d), T, eng.hws, acc[1:3],
+    acc = torch.zeros(7, device=dev)
+    hctx = heads_forward(cfg, eng.student.P, sfeats.view(n, Ss.d), tfeats.view(n, St.d), T, eng.hws, acc[1:6],
                          seed=eng.seed)
     mark("heads_fwd")
     eng.student.zero_grad()

@@ -80,3 +80,24 @@ for name, R, M, N in bcases:
     nbytes = 2.0 * R * (M + N) + 8.0 * M * (G.shape[1] + 1)
     print(f"bf16 {name:10s} R={R:7d} M={M:3d} N={G.shape[1]:4d}  {us:8.1f} us  {nbytes / us / 1e3:7.1f} GB/s", flush=True)
     del dy, x
+
+# the FM chain's dW1x over its 8 steps: 8 per-step launches vs one segmented launch
+R, M, S8 = 205312, 96, 8
+dy = torch.randn(S8 * R, M, device=dev).to(torch.bfloat16)
+x = torch.randn(S8 * R, M, device=dev).to(torch.bfloat16)
+G = torch.zeros(M, M, device=dev)
+dc = torch.zeros(S8, M, device=dev)
+for name, run in (("8 launches", lambda: [K.wgrad_bf16(dy[j * R:(j + 1) * R], x[j * R:(j + 1) * R], G, db=dc[j])
+                                          for j in range(S8)]),
+                  ("segmented", lambda: K.wgrad_bf16_seg(dy, x, G, dc, R))):
+    for _ in range(3):
+        run()
+    torch.cuda.synchronize()
+    e0 = torch.cuda.Event(enable_timing=True); e1 = torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(10):
+        run()
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) / 10 * 1e3
+    print(f"fm dW1x x8 {name:10s} {us:8.1f} us  {2.0 * S8 * R * 2 * M / us / 1e3:7.1f} GB/s", flush=True)
