@@ -582,11 +582,14 @@ int kdfm_subsample_lengths(const int64_t* wav_len, int64_t* mel_len, int64_t* le
 /* step counter += 1 and per-step RNG seed advance, on device */
 int kdfm_step_advance(int64_t* step, uint64_t* seed, void* stream);
 
-/* ---------------- optimizer (modelPT.py:650-897, lr_scheduler.py:473-530) ------------------ */
+/* ---------------- optimizer (modelPT.py:650-897, lr_scheduler.py:473-530) ------------------
+ * step[0] = k, the 1-based optimizer step (Noam schedule); AdamW's bias correction counts
+ * k - adam_base[0] (adam_base may be NULL = 0): the moments restarted adam_base steps into the run
+ * (a resume whose optimizer state could not be restored), like a fresh torch AdamW state. */
 int kdfm_adamw_noam(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, int64_t n,
-                    const int64_t* step, float base_lr, float d_model, float warmup_steps, float min_lr,
-                    float beta1, float beta2, float eps, float weight_decay, float grad_scale, float* lr_out,
-                    void* stream);
+                    const int64_t* step, const int64_t* adam_base, float base_lr, float d_model,
+                    float warmup_steps, float min_lr, float beta1, float beta2, float eps, float weight_decay,
+                    float grad_scale, float* lr_out, void* stream);
 
 #ifdef __cplusplus
 }

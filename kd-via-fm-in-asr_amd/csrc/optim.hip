@@ -5,7 +5,9 @@
 //   lr(s) = base * d^-0.5 * min(s^-0.5, s * warmup^-1.5), floored at min_lr after warmup,
 //   s = max(1, last_epoch) where Lightning steps the scheduler after each optimizer step, so
 //   optimizer step k (1-based) runs with s = max(1, k-1).
-// torch.optim.AdamW semantics (decoupled decay, bias correction).  Gradients arrive summed over
+// torch.optim.AdamW semantics (decoupled decay, bias correction).  The bias correction counts the
+// steps since the moments (re)started, k - adam_base: torch keeps AdamW's `step` in the optimizer
+// state, so a resume that cannot restore the moments restarts it while the schedule continues.  Gradients arrive summed over
 // data-parallel ranks; grad_scale = 1/world turns the sum into DDP's mean.
 #include "common.h"
 
@@ -26,13 +28,15 @@ __device__ __forceinline__ float noam_lr(int64_t k, float base, float d_model, f
 
 __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                     float* __restrict__ m, float* __restrict__ v, int64_t n,
-                                                    const int64_t* __restrict__ step, float base, float d_model,
+                                                    const int64_t* __restrict__ step,
+                                                    const int64_t* __restrict__ adam_base, float base, float d_model,
                                                     float warmup, float min_lr, float b1, float b2, float eps, float wd,
                                                     float gscale, float* __restrict__ lr_out) {
   const int64_t k = step[0];
   const float lr = noam_lr(k, base, d_model, warmup, min_lr);
-  const float bc1 = 1.f - powf(b1, (float)k);
-  const float bc2 = 1.f - powf(b2, (float)k);
+  const int64_t ka = adam_base ? k - adam_base[0] : k;   // AdamW's own step count
+  const float bc1 = 1.f - powf(b1, (float)ka);
+  const float bc2 = 1.f - powf(b2, (float)ka);
   const float step_size = lr / bc1;
   const float bc2s = sqrtf(bc2);
   if (lr_out && blockIdx.x == 0 && threadIdx.x == 0) lr_out[0] = lr;
@@ -53,7 +57,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const
 }  // namespace kdfm
 
 extern "C" int kdfm_adamw_noam(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, int64_t n,
-                               const int64_t* step, float base_lr, float d_model, float warmup_steps, float min_lr,
+                               const int64_t* step, const int64_t* adam_base, float base_lr, float d_model, float warmup_steps, float min_lr,
                                float beta1, float beta2, float eps, float weight_decay, float grad_scale,
                                float* lr_out, void* stream) {
   using namespace kdfm;
@@ -62,7 +66,7 @@ extern "C" int kdfm_adamw_noam(float* params, const float* grads, float* exp_avg
   int64_t blocks = ceil_div(n, 256);
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(adamw_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), params, grads, exp_avg,
-                     exp_avg_sq, n, step, base_lr, d_model, warmup_steps, min_lr, beta1, beta2, eps, weight_decay,
+                     exp_avg_sq, n, step, adam_base, base_lr, d_model, warmup_steps, min_lr, beta1, beta2, eps, weight_decay,
                      grad_scale, lr_out);
   return check_launch("kdfm_adamw_noam");
 }

@@ -632,7 +632,9 @@ int kdfm_wgrad_bf16(const uint16_t* dY, const uint16_t* X, float* dW, int64_t ld
 
 int64_t kdfm_wgrad_bf16_seg_ws(int64_t rows, int64_t M, int64_t N, int64_t seg_rows) {
   using namespace kdfm;
-  if (seg_rows <= 0 || rows % seg_rows) return -1;
+  // the launch's own preconditions (kdfm_wgrad_bf16_seg): a query must never accept a shape the
+  // launch rejects (with one segment wr_plan would not check seg_rows % 32 itself)
+  if (seg_rows <= 0 || seg_rows % 32 || rows % seg_rows || rows / seg_rows > 16 || M % 4 || N % 4) return -1;
   GemmP p = wgrad_bf16_params(reinterpret_cast<const uint16_t*>(16), reinterpret_cast<const uint16_t*>(16), nullptr, N,
                               nullptr, rows, M, N, 1.f, nullptr, 0);
   p.nseg = (int)(rows / seg_rows);

@@ -180,7 +180,7 @@ SIGNATURES: dict[str, tuple] = {
     "kdfm_convw_grad": (_i32, [P, P, _i64, _i64, _i64, _f32, P]),
     "kdfm_subsample_lengths": (_i32, [P, P, P, P, _i64, _i64, P]),
     "kdfm_step_advance": (_i32, [P, P, P]),
-    "kdfm_adamw_noam": (_i32, [P, P, P, P, _i64, P, _f32, _f32, _f32, _f32, _f32, _f32, _f32, _f32, _f32, P, P]),
+    "kdfm_adamw_noam": (_i32, [P, P, P, P, _i64, P, P, _f32, _f32, _f32, _f32, _f32, _f32, _f32, _f32, _f32, P, P]),
 }
 
 _LIB = None

@@ -49,6 +49,9 @@ def engine_state_dict(eng, *, teacher: bool = True, frontend: bool = True) -> "O
     loaded_nbt = getattr(eng, "bn_batches_tracked", {})
     for name, _ in eng.student.specs:
         sd[name] = eng.student.P[name].detach().cpu().clone()
+    # heads this version never trains (kept so the reference module can load the dict strictly)
+    for name, t in getattr(eng, "frozen_heads", {}).items():
+        sd[name] = t.detach().cpu().clone()
     for name, _ in eng.bn.specs:
         if teacher or not name.startswith("teacher."):
             sd[name] = eng.bn.P[name].detach().cpu().clone()
@@ -93,8 +96,14 @@ def load_engine_state(eng, sd: dict, *, strict: bool = False, fb_atol: float = 1
                 ref = v.reshape(mine.shape).to(torch.float32).cpu()
                 if ref.shape != mine.shape or (ref - mine.detach().cpu()).abs().max().item() > fb_atol:
                     fe_bad.append(k)
+            elif k in getattr(eng, "frozen_heads", {}):
+                # a head the configured version does not train (kdfm.config.head_modules): kept
+                # host-side and written back by engine_state_dict
+                dst = eng.frozen_heads[k]
+                if tuple(v.shape) != tuple(dst.shape):
+                    raise ValueError(f"{k}: checkpoint shape {tuple(v.shape)} != reference head shape {tuple(dst.shape)}")
+                eng.frozen_heads[k] = v.detach().to("cpu", torch.float32).clone()
             elif k.endswith(_IGNORED_SUFFIXES) or k.startswith(_HEAD_PREFIXES):
-                # heads the configured model version does not train (kdfm.config.head_modules)
                 if k.startswith("teacher.") and k.endswith("num_batches_tracked"):
                     if not hasattr(eng, "bn_batches_tracked"):
                         eng.bn_batches_tracked = {}
@@ -174,6 +183,8 @@ def save_lightning_ckpt(eng, path: str, *, epoch: int = 0, global_step: int | No
             "exp_avg": eng.student.exp_avg.detach().cpu().clone(),
             "exp_avg_sq": eng.student.exp_avg_sq.detach().cpu().clone(),
             "step": torch.tensor(step, dtype=torch.int64),
+            # optimizer steps taken before the moments started (AdamW bias correction counts from here)
+            "adam_base": torch.tensor(int(eng.adam_base.item()), dtype=torch.int64),
             "names": [n for n, _ in eng.student.specs],
             "offsets": torch.tensor([eng.student.offsets[n] for n, _ in eng.student.specs], dtype=torch.int64),
         }}],
@@ -199,6 +210,7 @@ def restore_lightning_ckpt(eng, path: str, *, optimizer: bool = True, strict: bo
             eng.student.exp_avg.copy_(opt["exp_avg"].to(eng.student.exp_avg.device))
             eng.student.exp_avg_sq.copy_(opt["exp_avg_sq"].to(eng.student.exp_avg_sq.device))
             eng.step.fill_(int(opt["step"]))
+            eng.adam_base.fill_(int(opt.get("adam_base", 0)))
         info["resumed_optimizer"] = True
     elif optimizer and "global_step" in ck:
         # a reference (Lightning/NeMo) checkpoint: its AdamW moments are keyed by NeMo's module
@@ -208,6 +220,9 @@ def restore_lightning_ckpt(eng, path: str, *, optimizer: bool = True, strict: bo
                       f"the schedule resumes at global_step {int(ck['global_step'])}")
         with torch.no_grad():
             eng.step.fill_(int(ck["global_step"]))
+            # fresh moments: AdamW's bias correction restarts (torch's per-parameter state 'step'
+            # would be 0), only the Noam schedule continues at global_step
+            eng.adam_base.fill_(int(ck["global_step"]))
     info["epoch"] = int(ck.get("epoch", 0))
     info["global_step"] = int(ck.get("global_step", 0))
     return info

@@ -225,6 +225,13 @@ def head_specs(cfg: Ver5Config, fm_prefixes=None) -> list:
     return s
 
 
+def all_head_specs(cfg: Ver5Config) -> list:
+    """Every KD head the reference module builds, whatever the version (asr_train_diffm.py:559-564):
+    version 6 uses all of them."""
+    from dataclasses import replace
+    return head_specs(replace(cfg, version=6))
+
+
 def student_specs(cfg: Ver5Config) -> list:
     """Trainable parameters of the step: student encoder + decoder + the heads the version uses
     (head_modules; for ver5 fm_latent_2 exists in the reference but never receives a gradient)."""
@@ -255,5 +262,5 @@ DEFAULT = Ver5Config()
 PARITY = DEFAULT.parity()
 
 __all__ = ["Ver5Config", "DEFAULT", "PARITY", "encoder_specs", "subsampling_specs", "sub_stages", "sub_pad",
-           "sub_channels", "sub_len", "sub_dims", "decoder_specs", "head_specs", "head_modules", "student_specs",
+           "sub_channels", "sub_len", "sub_dims", "decoder_specs", "head_specs", "all_head_specs", "head_modules", "student_specs",
            "teacher_specs", "bn_buffer_specs", "fused_groups", "field"]

@@ -14,7 +14,7 @@ import torch
 
 from . import _lib
 from . import kernels as K
-from .config import Ver5Config, bn_buffer_specs, student_specs, teacher_specs
+from .config import Ver5Config, all_head_specs, bn_buffer_specs, student_specs, teacher_specs
 from .conformer import EncoderRun, EncoderShapes, compute_lengths, encoder_backward, encoder_forward, \
     encoder_forward_steps, layer_images, make_workspace
 from .frontend import FrontendConsts, frontend_forward, mel_frames, specaugment_
@@ -79,6 +79,10 @@ class Ver5Engine:
         self.fe = FrontendConsts(cfg, dev)
         self.seed = torch.zeros(1, dtype=torch.int64, device=dev)     # uint64 bits, advanced on device
         self.step = torch.zeros(1, dtype=torch.int64, device=dev)
+        # optimizer steps taken before the AdamW moments were (re)started: AdamW's bias correction
+        # counts from here while the Noam schedule counts from 0 (a resume whose moments could not
+        # be restored, checkpoint.restore_lightning_ckpt)
+        self.adam_base = torch.zeros(1, dtype=torch.int64, device=dev)
         self.lr = torch.zeros(1, device=dev)
         self.losses = torch.zeros(5, device=dev)   # total, ctc, kl, recon, layer KD (kd/fm pre+post; ver5: fm_post)
         self.hws = HeadsWorkspace(cfg, dev)
@@ -104,6 +108,12 @@ class Ver5Engine:
             self.student.load(st)
             self.teacher.load(init_uniform(teacher_specs(cfg), teacher_seed))
             self.reset_bn()
+        # heads the reference module builds but this version never trains (asr_train_diffm.py:559-564):
+        # kept host-side (seeded init, or whatever a checkpoint held) so saved state dicts carry the
+        # reference's full key set
+        trained = {n for n, _ in student_specs(cfg)}
+        frozen = [s for s in all_head_specs(cfg) if s[0] not in trained]
+        self.frozen_heads = init_uniform(frozen, heads_seed + 1000) if frozen else {}
 
     # ---------------------------------------------------------------------------------------------
     def reset_bn(self):
@@ -135,7 +145,7 @@ class Ver5Engine:
         Cn = cfg.classes
         encoder_forward(cfg, St, self.teacher.P, "teacher.encoder.", mel_t, mel_len, len1, len2, tfeats,
                         self._pos_emb(T, St.d), train=False, seed=self.seed, salt=SALT_TEACHER, save=False,
-                        bn_running=self.bn.P, use_batch_stats=False, ws=self._enc_ws(St))
+                        bn_running=self.bn.P, use_batch_stats=False, ws=self._enc_ws(St, "teacher.encoder."))
         K.linear(tfeats[-1], self.teacher.P["teacher.decoder.decoder_layers.0.weight"].view(Cn, St.d),
                  self.teacher.P["teacher.decoder.decoder_layers.0.bias"], tlogits)
 
@@ -182,8 +192,10 @@ class Ver5Engine:
             dst.copy_(src)
         return tg
 
-    def _enc_ws(self, S):
-        key = (S.d, S.F2)
+    def _enc_ws(self, S, prefix):
+        # one workspace per encoder: the teacher and the student run concurrently on two streams and
+        # each writes its own re-laid-out weights here (equal widths shared one)
+        key = (prefix, S.d, S.F2)
         if key not in self._ws:
             self._ws[key] = make_workspace(S, self.device)
         return self._ws[key]
@@ -258,7 +270,7 @@ class Ver5Engine:
                 side.wait_stream(main)
             tgen = encoder_forward_steps(cfg, St, self.teacher.P, "teacher.encoder.", mel_t, mel_len, len1, len2,
                                          tfeats, self._pos_emb(T, St.d), train=False, seed=seed, salt=SALT_TEACHER,
-                                         save=False, bn_running=self.bn.P, use_batch_stats=False, ws=self._enc_ws(St))
+                                         save=False, bn_running=self.bn.P, use_batch_stats=False, ws=self._enc_ws(St, "teacher.encoder."))
         if own_mel:
             mel_s = frontend_forward(cfg, self.fe, wav, wav_len, mel_len, dither=dither, seed=seed,
                                      rng_stream=SALT_FRONT)
@@ -277,7 +289,7 @@ class Ver5Engine:
         srun = EncoderRun() if save else None
         sgen = encoder_forward_steps(cfg, Ss, self.student.P, "encoder.", mel_s, mel_len, len1, len2, sfeats, pos_s,
                                      train=train, seed=seed, salt=SALT_STUDENT, save=save, bn_running=self.bn.P,
-                                     use_batch_stats=train, ws=self._enc_ws(Ss), run=srun)
+                                     use_batch_stats=train, ws=self._enc_ws(Ss, "encoder."), run=srun)
         with K.region("encoders"):
             for _ in range(cfg.n_layers + 1):
                 if tgen is not None:
@@ -351,7 +363,7 @@ class Ver5Engine:
         feats = torch.empty(cfg.n_layers, Ss.rows, Ss.d, device=dev)
         encoder_forward(cfg, Ss, self.student.P, "encoder.", mel, mel_len, len1, len2, feats,
                         self._pos_emb(Ss.T, Ss.d), train=False, seed=self.seed, salt=SALT_STUDENT, save=False,
-                        bn_running=self.bn.P, use_batch_stats=False, ws=self._enc_ws(Ss))
+                        bn_running=self.bn.P, use_batch_stats=False, ws=self._enc_ws(Ss, "encoder."))
         Cn = cfg.classes
         logits = torch.empty(Ss.rows, Cn, device=dev)
         K.linear(feats[-1], self.student.P["decoder.decoder_layers.0.weight"].view(Cn, Ss.d),
@@ -422,7 +434,7 @@ class Ver5Engine:
             layer_done = lambda i: grad_ready(firsts[i])  # noqa: E731
         with K.region("encoder_backward"):
             encoder_backward(cfg, Ss, P, G, "encoder.", ctx.pop("srun"), dfeats, ctx["pos_s"], ctx["len1"],
-                             ctx["len2"], seed=self.seed, salt=SALT_STUDENT, ws=self._enc_ws(Ss),
+                             ctx["len2"], seed=self.seed, salt=SALT_STUDENT, ws=self._enc_ws(Ss, "encoder."),
                              on_layer_done=layer_done)
 
     def optimizer_step(self, grad_scale: float = 1.0):
@@ -435,7 +447,7 @@ class Ver5Engine:
         K.step_advance(self.step, None)
         K.adamw_noam(st.data, st.grad, st.exp_avg, st.exp_avg_sq, self.step, cfg.lr, cfg.sched_d_model,
                      cfg.warmup_steps, cfg.min_lr, cfg.betas[0], cfg.betas[1], cfg.adam_eps, cfg.weight_decay,
-                     grad_scale, self.lr)
+                     grad_scale, self.lr, adam_base=self.adam_base)
 
     def advance_rng(self):
         with self._on_stream():

@@ -1265,8 +1265,10 @@ def fm_time_bwd(dc, evec, W1, dW1, db1, dw_te, db_te, L, E, steps):
          _s())
 
 
-def adamw_noam(p, g, m, v, step, base_lr, d_model, warmup, min_lr, beta1, beta2, eps, wd, grad_scale, lr_out=None):
+def adamw_noam(p, g, m, v, step, base_lr, d_model, warmup, min_lr, beta1, beta2, eps, wd, grad_scale, lr_out=None,
+               adam_base=None):
     assert p.numel() == g.numel() == m.numel() == v.numel()
-    call("kdfm_adamw_noam", ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), ptr(step), float(base_lr), float(d_model),
+    call("kdfm_adamw_noam", ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), ptr(step), ptr(adam_base), float(base_lr),
+         float(d_model),
          float(warmup), float(min_lr), float(beta1), float(beta2), float(eps), float(wd), float(grad_scale),
          ptr(lr_out), _s())

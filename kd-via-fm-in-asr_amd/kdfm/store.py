@@ -15,8 +15,9 @@ from . import kernels as K
 from .config import fused_groups
 
 ALIGN = 4  # floats (16 bytes): every tensor starts 16-B aligned for dwordx4 loads
-# start of every parameter (fused q|k|v group: of the group) in floats; experiment knob
-GROUP_ALIGN = int(__import__("os").environ.get("KDFM_STORE_ALIGN", str(ALIGN)))
+# start of every parameter (fused q|k|v group: of the group) in floats.  Fixed: the flat layout (and
+# with it the saved AdamW moments, checkpoint.py) must not depend on the environment
+GROUP_ALIGN = ALIGN
 
 
 def _numel(shape):

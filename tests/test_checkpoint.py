@@ -59,7 +59,7 @@ def test_lightning_roundtrip_and_resume(eng, tmp_path):
     assert _same(eng.student, e2.student) and _same(eng.teacher, e2.teacher) and _same(eng.bn, e2.bn)
     assert torch.equal(eng.student.exp_avg, e2.student.exp_avg)
     assert torch.equal(eng.student.exp_avg_sq, e2.student.exp_avg_sq)
-    assert int(e2.step) == 123
+    assert int(e2.step) == 123 and int(e2.adam_base) == 0
     # the inference script's load: ckpt["state_dict"], strict=False, on a model without the teacher
     ck = C.read_lightning_ckpt(p)
     sd = {k: v for k, v in ck["state_dict"].items() if not k.startswith("teacher.")}
@@ -78,11 +78,29 @@ def test_shape_mismatch_raises(eng):
 
 def test_unexpected_keys_strict(eng):
     sd = C.engine_state_dict(eng)
-    sd["fm_latent_2.fm.time_embed.weight"] = torch.zeros(1)   # unused by ver5: ignored
     sd["layer_proj.0.weight"] = torch.zeros(1)
     assert C.load_engine_state(_fresh(), sd)["unexpected"] == ["layer_proj.0.weight"]
     with pytest.raises(KeyError):
         C.load_engine_state(_fresh(), sd, strict=True)
+
+
+def test_untrained_heads_round_trip(eng):
+    """the heads a version never trains (fm_latent_2 for ver5) are kept as loaded and
+    written back, so a kdfm state dict carries the reference module's full key set
+    (asr_train_diffm.py:559-564 builds every head for every version)."""
+    from kdfm.config import all_head_specs
+    sd = C.engine_state_dict(eng)
+    for name, shape in all_head_specs(eng.cfg):
+        assert name in sd and tuple(sd[name].shape) == tuple(shape), name
+    w = torch.arange(32, dtype=torch.float32).view(32, 1)
+    sd["fm_latent_2.fm.time_embed.weight"] = w
+    e2 = _fresh()
+    info = C.load_engine_state(e2, sd, strict=True)
+    assert info["unexpected"] == []
+    assert torch.equal(C.engine_state_dict(e2)["fm_latent_2.fm.time_embed.weight"], w)
+    sd["fm_latent_2.fm.time_embed.weight"] = torch.zeros(1)
+    with pytest.raises(ValueError):
+        C.load_engine_state(_fresh(), sd)
 
 
 def test_nemo_roundtrip(eng, tmp_path):
@@ -144,6 +162,8 @@ def test_reference_style_ckpt_with_foreign_hyperparameters(eng, tmp_path):
         info = C.restore_lightning_ckpt(e2, p)
     assert DictConfigStandIn.constructed == 0
     assert not info["resumed_optimizer"] and info["global_step"] == 4567 and int(e2.step) == 4567
+    # fresh moments: AdamW's bias correction restarts while the schedule continues
+    assert int(e2.adam_base) == 4567
     assert _same(e2.student, eng.student) and _same(e2.teacher, eng.teacher)
     hp = C.read_lightning_ckpt(p)["hyper_parameters"]["cfg"]
     assert isinstance(hp, C.InertGlobal) and not isinstance(hp, DictConfigStandIn)

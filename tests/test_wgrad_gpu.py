@@ -178,3 +178,7 @@ def test_wgrad_bf16_segments(nseg, seg, M, N):
     assert torch.equal(dW[:, N:], W0[:, N:])   # ldc > N: columns past N untouched
     assert (db.double() - rb).abs().max().item() <= 1e-5 * rb.abs().max().item() + 1e-5
     assert not K.wgrad_bf16_seg_ok(R + 32, M, N, seg)   # rows must be whole segments
+    # the shape query agrees with the launch's preconditions even with one segment:
+    # seg_rows % 32 != 0 is refused by both
+    assert not K.wgrad_bf16_seg_ok(seg + 8, M, N, seg + 8)
+    assert not K.wgrad_bf16_seg_ok(17 * 64, M, N, 64)    # at most 16 segments
