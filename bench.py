@@ -29,7 +29,6 @@ B_PER_GPU = 32
 N_SAMPLES = 256000
 U_TOKENS = 100
 # attention + FFN dense contractions per utterance (student fwd+bwd + teacher fwd)
-FFN_FLOPS_NOTE = "ffn_up GEMMs: 2*M*N*K per launch (M=B*T' rows, N=4d, K=d)"
 MI355X_BF16_DENSE_TFLOPS = 2500.0   # /opt/skills/guides/MI355X_MICROARCH.md chip table (dense)
 MI355X_F32_MFMA_TFLOPS = 157.3
 MI355X_HBM_GBPS = 8000.0            # MI355X_MICROARCH.md §HBM (8 TB/s spec peak)
@@ -74,12 +73,39 @@ def parse():
     ap.add_argument("--samples", type=int, default=N_SAMPLES)
     ap.add_argument("--math", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=16,
-                    help="host threads for the CPU baseline (the GPU box gives one GPU 16 host CPUs)")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="host threads for the CPU baseline (default: os.cpu_count(), BASELINE.md)")
+    ap.add_argument("--no-f32-sensitivity", action="store_true",
+                    help="skip the --math f32 sensitivity measurement (the reference trains fp32)")
     ap.add_argument("--graph", action="store_true",
                     help="replay the step as one captured HIP graph (measured slower: hipGraph replay ran the "
                          "teacher / weight-gradient / CTC streams serially, 43.9 vs 40.1 ms/step eager)")
     return ap.parse_args()
+
+
+def f32_sensitivity(dev, samples, steps=3):
+    """utt/s of the same step with exact-f32 MFMA arithmetic (the reference trains in fp32,
+    asr_train_diffm.py:1762-1769): a separate engine, 1 warm-up + `steps` timed steps."""
+    from dataclasses import replace
+
+    from kdfm import kernels as K
+    from kdfm.config import DEFAULT
+    from kdfm.engine import Ver5Engine, synthetic_batch
+    cfg = replace(DEFAULT, math="f32")
+    eng = Ver5Engine(cfg, dev)
+    eng.set_seed(1000)
+    wav, wl, tg, tl = synthetic_batch(cfg, B_PER_GPU, samples, U_TOKENS, dev, seed=1234)
+    with K.mode("f32"):
+        eng.train_step(wav, wl, tg, tl)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            eng.train_step(wav, wl, tg, tl)
+        torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    return {"value": round(B_PER_GPU * steps / el, 3), "unit": "utterances/sec", "ms_per_step": round(1e3 * el / steps, 3),
+            "dtype": "f32", "steps": steps, "note": "same workload, exact f32 MFMA (v_mfma_f32_16x16x4_f32) instead of "
+                                                  "bf16 operands: sensitivity only, not the headline value"}
 
 
 def cpu_baseline(threads: int, samples: int, batches=(2, 32), steps: int = 5):
@@ -188,8 +214,7 @@ def main():
     # live per-kernel timing: one instrumented eager step right after the timed steps; every
     # kdfm_gemm launch (keyed by the kernel family libkdfm routed it to), the frontend and the
     # depthwise convs bracketed by HIP events on the stream they run on
-    trace = K.Trace(["*", "ffn_up", "frontend", "dwconv", "ffn_fwd", "ffn_bwd", "wgrad_bf16", "attn_fwd",
-                     "attn_bwd"])
+    trace = K.Trace(["*", "frontend", "dwconv", "ffn_fwd", "ffn_bwd", "wgrad_bf16", "attn_fwd", "attn_bwd"])
     with trace:
         eng.train_step(wav, wl, tg, tl, ar)
     torch.cuda.synchronize()
@@ -248,13 +273,47 @@ def main():
                      "launches": n, "avg_ms": round(ms, 5), "bytes_per_launch": round(dt["bytes_total"] / n, 1),
                      "flops_per_launch": round(dt["flops_total"] / n, 1),
                      "arith_intensity_flop_per_byte": round(intensity, 2)})
-        f_n, f_ms, f_gbps, _ = rate(tsum.get("ffn_up", empty))
-        f_tfl = rate(tsum.get("ffn_up", empty))[3]
+        # the critical path: the compute stream carries the student chain and the whole backward's data
+        # gradients (the teacher, weight gradients and CTC/KL overlap it on their own streams)
+        csum = trace.summary(stream=eng.compute_stream.cuda_stream)
+        croutes = {k[5:]: v for k, v in csum.items() if k.startswith("gemm:")}
+        for fam in ("ffn_fwd", "ffn_bwd", "attn_fwd", "attn_bwd", "wgrad_bf16"):
+            if fam in csum:
+                croutes[fam] = csum[fam]
+        crit = None
+        if croutes:
+            cdom, ct = max(croutes.items(), key=lambda kv: kv[1]["ms_total"])
+            cn, cms, cgbps, ctfl = rate(ct)
+            cint = ct["flops_total"] / max(1.0, ct["bytes_total"])
+            cb = "hbm" if cint < ridge else "mfma"
+            crit = {"bound": cb, "achieved": round(cgbps if cb == "hbm" else ctfl, 2),
+                    "peak": MI355X_HBM_GBPS if cb == "hbm" else bf16_peak, "unit": "GB/s" if cb == "hbm" else "TFLOP/s",
+                    "frac": round((cgbps / MI355X_HBM_GBPS) if cb == "hbm" else (ctfl / bf16_peak), 4),
+                    "kernel": f"{cdom} family: the most time on the compute (critical-path) stream",
+                    "ms_per_step_on_stream": round(ct["ms_total"], 3), "launches": cn, "avg_ms": round(cms, 5),
+                    "traffic": pmc_traffic(FAMILY_KERNELS.get(cdom) or ROUTE_KERNELS.get(cdom, (cdom,))),
+                    "by_family_ms": {k: round(v["ms_total"], 3) for k, v in
+                                     sorted(croutes.items(), key=lambda kv: -kv[1]["ms_total"])}}
+        # MFMA rate of the attention / FFN kernels (the north-star MFMA subject) per family
+        mfma_fams = {}
+        for fam in ("ffn_fwd", "ffn_bwd", "attn_fwd", "attn_bwd"):
+            if fam in tsum:
+                n_, ms_, _, tfl_ = rate(tsum[fam])
+                mfma_fams[fam] = {"TFLOP_per_s": round(tfl_, 2), "frac_bf16_peak": round(tfl_ / bf16_peak, 5),
+                                  "launches": n_, "avg_ms": round(ms_, 5),
+                                  "flops_per_launch": round(tsum[fam]["flops_total"] / n_, 1)}
         fe = rate(tsum.get("frontend", empty))
         dw = rate(tsum.get("dwconv", empty))
         cpu = None
         if not args.no_cpu_baseline:
-            cpu = cpu_baseline(args.cpu_threads, args.samples)
+            threads = args.cpu_threads or os.cpu_count()
+            cpu = cpu_baseline(threads, args.samples)
+            if threads != 16:   # the box's per-GPU CPU share, kept beside the all-cores figure
+                c16 = cpu_baseline(16, args.samples, batches=(32,), steps=3)
+                cpu["at_16_threads"] = {"value": c16["value"], "cores": 16, "sample": c16["sample"]}
+        f32 = None
+        if not args.no_f32_sensitivity and cfg.math == "bf16" and world == 1:
+            f32 = f32_sensitivity(dev, args.samples)
         line = {
             "metric": "utterances/sec (FM-distill train step, Conformer-CTC-small) at 1/2/4/8 MI355X",
             "value": round(utt, 3),
@@ -274,9 +333,8 @@ def main():
                        "frames_subsampled": (args.samples // 160) // 4 + 1, "parallelism": f"dp{world}"},
             "roofline": roof,
             "roofline_by_family": by_route,
-            "roofline_mfma_ffn": {"bound": "mfma", "kernel": "kdfm_gemm ffn_up (Conformer FFN d->4d, SiLU+dropout)",
-                                  "achieved": round(f_tfl, 3), "peak": bf16_peak, "unit": "TFLOP/s",
-                                  "frac": round(f_tfl / bf16_peak, 5), "launches": f_n, "avg_ms": round(f_ms, 5)},
+            "roofline_critical_path": crit,
+            "mfma_attn_ffn_by_family": mfma_fams,
             "attn_ffn_mfma_frac": {"value": round(ATTN_FFN_GFLOP_PER_UTT * 1e9 * utt_gpu / (bf16_peak * 1e12), 5),
                                    "formula": "23.0 GFLOP/utt (SURVEY §8(d)) x utt/s per GPU / dense bf16 peak"},
             "whole_step": {"tflops": round(STEP_GFLOP_PER_UTT * 1e9 * utt_gpu / 1e12, 2),
@@ -289,6 +347,7 @@ def main():
                            "frac": round(dw[2] / MI355X_HBM_GBPS, 4), "launches": dw[0], "avg_ms": round(dw[1], 5),
                            "bytes": "read g + write y, 4 B x rows x d per launch"},
             "cpu_baseline": cpu,
+            "f32_sensitivity": f32,
             "losses_last_step": [round(x, 5) for x in losses],
         }
         print(json.dumps(line))

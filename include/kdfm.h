@@ -57,6 +57,14 @@ int32_t kdfm_get_deterministic(void);
 int32_t kdfm_range_push(const char* name);
 int32_t kdfm_range_pop(void);
 
+/* Step-plan replay primitives (kdfm/plan.py records one training step's launches and re-issues them
+ * without the Python wrappers): hipEventRecord(event, stream), hipStreamWaitEvent(stream, event, 0)
+ * and hipMemsetAsync on the caller's handles; they exist so a replay uses the same HIP runtime as the
+ * kernels.  `event` is a hipEvent_t, `stream` a hipStream_t, both owned by the caller. */
+int kdfm_event_record(void* event, void* stream);
+int kdfm_stream_wait_event(void* stream, void* event);
+int kdfm_memset_async(void* ptr, int32_t value, int64_t bytes, void* stream);
+
 /* --------------------------------------------------------------------------------------------
  * Generic batched GEMM with fused epilogue:
  *   C[b](m,n) = epi( alpha * sum_k A[b](m,k) * B[b](k,n) )
@@ -173,12 +181,12 @@ int kdfm_wgrad_bf16_conv(const uint16_t* dY, const uint16_t* X, float* dW, int64
  * W1 row stride ld_w1 (the time-embedding columns of meta_encoder.0 follow the first L). */
 /* Fused relative-position attention backward (bf16 MFMA; NeMo RelPositionMultiHeadAttention,
  * Appendix A.7): from dO (rows, d), the forward's q+u / q+v rows, the fused q|k|v rows (ld 3d), the
- * projected positions pos (2T-1, d), the forward output O (rows, d) and the saved probabilities
- * P (B, H, T, T) it writes
+ * projected positions pos (2T-1, d), the forward output O (rows, d) and the forward's per-row
+ * log-sum-exp lse (B, H, T) (kdfm_relpos_attn_fwd) it recomputes P = exp(S - lse) tile by tile and writes
  *   dqu = dS K, dqv_i = sum_j dS[i][j] pos[T-1-i+j]  (rows, d),  dK, dV into dqkv[:, d:] and [:, 2d:],
  *   dpos[r] = sum_{b,i} dS[i][r-T+1+i] qv_i  (2T-1, d, overwritten)
  * with dS = P (dP - r) scale, r_i = dO_i . O_i (= rowsum(dP P)) and dP the dropout-masked dO V^T (counter-RNG mask of the
- * forward).  No T x T intermediate in HBM; deterministic (ordered chunk fold, no atomics).  Head
+ * forward).  No T x T tensor in HBM at all; deterministic (ordered chunk fold, no atomics).  Head
  * dim d/H <= 48.  ws: kdfm_relpos_attn_bwd_ws floats. */
 int64_t kdfm_relpos_attn_bwd_ws(int64_t B, int64_t H, int64_t T, int64_t d);
 /* The same backward issued in parts (a caller may put them on different streams): ROWDOT writes
@@ -187,13 +195,13 @@ int64_t kdfm_relpos_attn_bwd_ws(int64_t B, int64_t H, int64_t T, int64_t d);
 enum { KDFM_ATTN_BWD_ROWDOT = 1, KDFM_ATTN_BWD_DQ = 2, KDFM_ATTN_BWD_DKV = 4, KDFM_ATTN_BWD_DPOS = 8,
        KDFM_ATTN_BWD_ALL = 15 };
 int kdfm_relpos_attn_bwd_parts(const float* dO, const float* O, const float* qu, const float* qv, const float* qkv,
-                               const float* pos, const float* P, const int64_t* lengths, float* dqu, float* dqv,
+                               const float* pos, const float* lse, const int64_t* lengths, float* dqu, float* dqv,
                                float* dqkv, float* dpos, float* ws, int64_t ws_len, int64_t B, int64_t H, int64_t T,
                                int64_t d, float scale, float dropout_p, const uint64_t* seed, uint64_t rng_stream,
                                int32_t parts, void* stream);
 int kdfm_relpos_attn_bwd(const float* dO, const float* O, const float* qu, const float* qv, const float* qkv,
-                         const float* pos, const float* P, const int64_t* lengths, float* dqu, float* dqv, float* dqkv,
-                         float* dpos,
+                         const float* pos, const float* lse, const int64_t* lengths, float* dqu, float* dqv,
+                         float* dqkv, float* dpos,
                          float* ws, int64_t ws_len, int64_t B, int64_t H, int64_t T, int64_t d, float scale,
                          float dropout_p, const uint64_t* seed, uint64_t rng_stream, void* stream);
 
@@ -497,9 +505,11 @@ int kdfm_relpos_table(float* pe, int64_t T, int64_t d, void* stream);
  * scores ((q+u)K^T + rel_shift((q+v)Ppos^T)) * scale, key-padding mask from lengths, softmax,
  * inverted dropout (same counter-RNG mask as kdfm_relpos_softmax_fwd).  qu/qv/o: (B*T, d);
  * qkv: (B*T, 3d) (K at +d, V at +2d); pos: (2T-1, d) projected positions.  P / Pdrop (B,H,T,T) are
- * written when non-null (backward operands).  dk = d/H <= 48. */
+ * written when non-null (the per-op backward's operands; two passes over the keys); otherwise one
+ * online-softmax pass, and lse (B,H,T) = per-row log-sum-exp of the scaled scores when non-null
+ * (kdfm_relpos_attn_bwd's operand; 3e38 for rows without a valid key).  dk = d/H <= 48. */
 int kdfm_relpos_attn_fwd(const float* qu, const float* qv, const float* qkv, const float* pos,
-                         const int64_t* lengths, float* o, float* P, float* Pdrop, int64_t B, int64_t H,
+                         const int64_t* lengths, float* o, float* P, float* Pdrop, float* lse, int64_t B, int64_t H,
                          int64_t T, int64_t d, float scale, float dropout_p, const uint64_t* seed,
                          uint64_t rng_stream, void* stream);
 /* conv module: GLU over channels + pad mask; depthwise conv (k odd) with optional f64 BN stats */

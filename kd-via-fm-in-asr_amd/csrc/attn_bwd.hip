@@ -2,21 +2,22 @@
 //
 // NeMo RelPositionMultiHeadAttention (Appendix A.7; per ConformerLayer, conformer_encoder.py:685-692):
 //   S = (Qu K^T + rel_shift(Qv Ppos^T)) * scale, P = masked softmax(S), Pd = dropout(P), O = Pd V
-// with rel_shift as the index map bd[i][j] = Qv_i . Ppos[T-1-i+j].  Given dO and the forward's
-// saved P, the gradients are
+// with rel_shift as the index map bd[i][j] = Qv_i . Ppos[T-1-i+j].  The gradients are
 //   dP = dropout'(dO V^T),  r_i = sum_j dP P,  dS = P (dP - r_i) scale
 //   dQu = dS K,  dQv_i = sum_j dS[i][j] Ppos[T-1-i+j],  dK = dS^T Qu,  dV = Pd^T dO,
 //   dPpos[r] = sum_{b, i} dS[i][r-(T-1)+i] Qv_i.
-// The unfused path materialised dPd, dAC (B,H,T,T) and dBD (B,H,T,2T-1) in HBM (f32) and ran five
-// batched GEMMs over them.  Here nothing of size T x T besides the saved P is read or written:
-//   * the row sums r_i = sum_j dP P equal dO_i . O_i (O = Pd V: FlashAttention's D_i), one row dot
-//     product over the saved forward output;
-//   * kernel 1 (one workgroup per (b, h, 64 query rows)): dPd = dO V^T on the fly,
-//     then dQu += dS K and dQv += skew(dS) Pband — the skew is the forward's band trick in reverse:
-//     dS is written into a per-wave LDS tile at column j - i + 15 and multiplied by the 128-row
-//     band of Ppos the block addresses;
-//   * kernel 2 (one workgroup per (b, h, 64 keys)): dPd^T = V dO^T on the fly, P^T staged through
-//     LDS from coalesced row loads, dV += Pd^T dO and dK += dS^T Qu over all query blocks;
+// Nothing of size T x T is read or written: every kernel recomputes its tile of S with the
+// forward's own score code (same MFMAs in the same order) and P = exp(S - lse_i) from the forward's
+// per-row log-sum-exp (kdfm_relpos_attn_fwd), and r_i = sum_j dP P = dO_i . O_i (FlashAttention's
+// D_i) is one row dot product over the saved forward output:
+//   * kernel 1 (one workgroup per (b, h, 64 query rows), 4 waves x 16 rows): S as in the forward
+//     (Qu K^T from a [key][c] K image, the positional term as G = Qv Pband^T read back skewed),
+//     dPd = dO V^T, then dQu += dS K and dQv += skew(dS) Pband, the K and band operands read
+//     TRANSPOSED out of the same [row][c] images with ds_read_b64_tr_b16 (one LDS image per tile);
+//   * kernel 2 (one workgroup per (b, h, 64 keys), 4 waves x 16 keys): S^T = K Qu^T and the band
+//     term per 16-query slice as H = Pband Qv^T (32 band rows x 16 queries) read back skewed;
+//     dPd^T = V dO^T; dV += Pd^T dO and dK += dS^T Qu over all query blocks (dO / Qu read
+//     transposed out of their row images);
 //   * kernel 3 (one workgroup per (h, 64 relative positions, batch chunk)): dS recomputed for the
 //     (i, j) diagonal band of its positions, dPpos += skew(dS)^T Qv; per-chunk partials are folded
 //     in chunk order.
@@ -30,19 +31,26 @@ namespace {
 constexpr int BQ = 64;             // query rows per workgroup (kernel 1), 4 waves x 16
 constexpr int BK = 64;             // keys per block
 constexpr int BDK = 64;            // head dim padded to 2 MFMA k-steps
-constexpr int LR = BDK + 8;        // bf16 row stride of [row][c] tiles
-constexpr int LT = 64 + 8;         // bf16 row stride of [c][64 rows] transposed tiles
+constexpr int LR = BDK + 8;        // bf16 row stride of [row][c] tiles (144 B: 8-B aligned transposed reads)
 constexpr int LW = 64 + 8;         // bf16 row stride of per-wave [16][64] tiles
-constexpr int BANDR = 144;         // Ppos band rows staged (127 addressed, the rest zero)
-constexpr int LB = BANDR + 8;      // bf16 row stride of the transposed band [c][band row]
+constexpr int PB1 = 144;           // kernel 1 band rows (127 staged; dQv's transposed reads reach row 143)
+constexpr int PB = 128;            // kernel 2 / 3 band rows (127 staged)
+constexpr int LG32 = 81;           // f32 stride of kernel 1's per-wave score band tile [16][80]
 constexpr int LG = 96 + 8;         // bf16 row stride of the per-wave skewed dS tile [16][96]
+constexpr int LH = 17;             // f32 stride of kernel 2's per-wave band tile [32][16]
 constexpr int NPQ = 32;            // query rows per step of kernel 3
 constexpr int NPJ = 96;            // keys per step of kernel 3 (64 positions + 31 rows of skew)
 constexpr int LDL = NPJ + 8;       // bf16 row stride of kernel 3's dS tile
 constexpr int LQ3 = NPQ + 8;       // bf16 row stride of kernel 3's Qv^T tile
+constexpr int LG3 = 65;            // f32 stride of kernel 3's per-wave score band tile [16][64]
+// per-wave scratch (bytes): kernel 1 aliases the f32 score band with the bf16 dS + skewed dS tiles,
+// kernel 2 the f32 band tile with the bf16 Pd^T + dS^T tiles
+constexpr int WS1 = (16 * LG32 * 4 > 16 * (LW + LG) * 2) ? 16 * LG32 * 4 : 16 * (LW + LG) * 2;
+constexpr int WS2 = (32 * LH * 4 > 2 * 16 * LW * 2) ? 32 * LH * 4 : 2 * 16 * LW * 2;
 
 struct AbP {
-  const float* dO; const float* qu; const float* qv; const float* k; const float* v; const float* pos; const float* P;
+  const float* dO; const float* qu; const float* qv; const float* k; const float* v; const float* pos;
+  const float* lse;
   const int64_t* lens;
   float* dqu; float* dqv; float* rsum; float* dk; float* dv; float* dpos_part;
   int64_t B, H, T, d, dkh, ldq, ldkv;
@@ -51,12 +59,27 @@ struct AbP {
   int bpc;   // batches per chunk (kernel 3)
 };
 
+typedef short v4s __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4s lds_v4s;
+
 __device__ __forceinline__ bf16x8 frag8(const float* src, int valid) {
   float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
   if (valid >= 4) a = *reinterpret_cast<const float4*>(src);
   if (valid >= 8) b = *reinterpret_cast<const float4*>(src + 4);
   const float t[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
   return pack_bf16x8<bf16x8>(t);
+}
+
+// MFMA 16x16x32 operand read TRANSPOSED out of a [k][n] bf16 LDS image (row stride ld elements):
+// lane l receives X[k0 + 8*(l>>4) + e][n0 + (l & 15)], e = 0..7 -- the B operand X[k][n], or the A
+// operand of X^T.  Two ds_read_b64_tr_b16: lane 4q+p of each 16-lane group addresses row q, columns
+// 4p..4p+3 of a 4-row block and receives column (l & 15) of the block's 4 rows.  EXEC must be full.
+__device__ __forceinline__ bf16x8 tr_frag(const uint16_t* img, int ld, int k0, int n0, int lane) {
+  const int li = lane & 15;
+  const uint16_t* a = img + (k0 + 8 * (lane >> 4) + (li >> 2)) * ld + n0 + 4 * (li & 3);
+  const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)a);
+  const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(a + 4 * ld));
+  return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
 __device__ __forceinline__ void st4(uint16_t* dst, float4 v) {
@@ -68,33 +91,6 @@ __device__ __forceinline__ void st4(uint16_t* dst, float4 v) {
 __device__ __forceinline__ void wsync() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_wave_barrier();
-}
-
-__device__ __forceinline__ float g16_sum(float v) {
-#pragma unroll
-  for (int o = 8; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
-
-// rows [r0, r0 + n) of a (rows, ld) f32 matrix, columns [c0, c0 + dk) -> bf16 [row][c] (stride LR) and/or
-// [c][row] (stride ldt); rows outside [lo, hi) are zero.  256 threads.
-__device__ void stage_rows(uint16_t* rc, uint16_t* cr, int ldt, const float* src, int64_t ld, int64_t base_row,
-                           int r0, int n, int lo, int hi, int64_t c0, int dk) {
-  const int cq = dk >> 2;
-  for (int e = threadIdx.x; e < n * cq; e += 256) {
-    const int rr = e / cq, c4 = (e - rr * cq) * 4;
-    const int r = r0 + rr;
-    const bool ok = r >= lo && r < hi;
-    const float4 v = ok ? *reinterpret_cast<const float4*>(src + (base_row + r) * ld + c0 + c4)
-                        : make_float4(0.f, 0.f, 0.f, 0.f);
-    if (rc) st4(rc + rr * LR + c4, v);
-    if (cr) {
-      cr[(c4 + 0) * ldt + rr] = f2bf(v.x);
-      cr[(c4 + 1) * ldt + rr] = f2bf(v.y);
-      cr[(c4 + 2) * ldt + rr] = f2bf(v.z);
-      cr[(c4 + 3) * ldt + rr] = f2bf(v.w);
-    }
-  }
 }
 
 // Software-pipelined staging: fetch_rows issues the global loads of rows [r0, r0 + n) into registers
@@ -131,6 +127,12 @@ __device__ __forceinline__ void put_rows(uint16_t* rc, uint16_t* cr, int ldt, co
   }
 }
 
+// zero columns [dk, 64) of rows [0, rows) of a [row][c] image, and every column of rows [z0, rows)
+__device__ __forceinline__ void zero_pad(uint16_t* img, int rows, int dk, int z0) {
+  for (int e = threadIdx.x; e < rows * (BDK - dk); e += 256) img[(e / (BDK - dk)) * LR + dk + e % (BDK - dk)] = 0;
+  for (int e = threadIdx.x; e < (rows - z0) * dk; e += 256) img[(z0 + e / dk) * LR + e % dk] = 0;
+}
+
 // r[(b*H + h)*T + i] = sum_c dO[b*T + i][h*dk + c] * O[b*T + i][h*dk + c]; one wave per (row, head)
 __global__ __launch_bounds__(256) void attn_rowdot_kernel(const float* __restrict__ dO, const float* __restrict__ O,
                                                           float* __restrict__ r, int64_t B, int64_t H, int64_t T,
@@ -150,11 +152,10 @@ __global__ __launch_bounds__(256) void attn_rowdot_kernel(const float* __restric
 // kernel 1: dQu, dQv
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AbP p) {
+  __shared__ __attribute__((aligned(16))) uint16_t Ks[BK * LR];     // K block [key][c]
   __shared__ __attribute__((aligned(16))) uint16_t Vs[BK * LR];     // V block [key][c]
-  __shared__ __attribute__((aligned(16))) uint16_t Kt[BDK * LT];    // K block^T [c][key]
-  __shared__ __attribute__((aligned(16))) uint16_t Pbt[BDK * LB];   // Ppos band^T [c][band row]
-  __shared__ __attribute__((aligned(16))) uint16_t Ds[4][16 * LW];  // per wave dS [ii][jj]
-  __shared__ __attribute__((aligned(16))) uint16_t Gs[4][16 * LG];  // per wave skewed dS [ii][jj - ii + 15]
+  __shared__ __attribute__((aligned(16))) uint16_t Pr[PB1 * LR];    // Ppos band [band row][c]
+  __shared__ __attribute__((aligned(16))) float Wsc[4][WS1 / 4];    // per-wave scratch
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int T = (int)p.T, dk = (int)p.dkh;
@@ -166,24 +167,100 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AbP p) {
   const int nkb = (len + BK - 1) / BK;
   const int npos = 2 * T - 1;
   const int64_t hoff = h * p.dkh;
-  // zero padding columns / rows that staging never writes
-  for (int e = threadIdx.x; e < BK * (BDK - dk); e += 256) Vs[(e / (BDK - dk)) * LR + dk + e % (BDK - dk)] = 0;
-  for (int e = threadIdx.x; e < (BDK - dk) * LT; e += 256) Kt[dk * LT + e] = 0;
-  for (int e = threadIdx.x; e < BDK * LB; e += 256) Pbt[e] = 0;
+  zero_pad(Ks, BK, dk, BK);
+  zero_pad(Vs, BK, dk, BK);
+  zero_pad(Pr, PB1, dk, 127);
 
-  const int iq = i0 + w * 16 + (lane & 15);   // A-fragment row
-  bf16x8 fdo[2];
+  // this lane's query row (A-fragment row): Qu, Qv and dO fragments
+  const int iq = i0 + w * 16 + (lane & 15);
+  bf16x8 fu[2], fv[2], fdo[2];
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks) {
     const int c0 = ks * 32 + 8 * (lane >> 4);
-    fdo[ks] = frag8(p.dO + (b * p.T + (iq < T ? iq : 0)) * p.ldq + hoff + c0, iq < T ? dk - c0 : 0);
+    const int valid = iq < T ? dk - c0 : 0;
+    const int64_t off = (b * p.T + (iq < T ? iq : 0)) * p.ldq + hoff + c0;
+    fu[ks] = frag8(p.qu + off, valid);
+    fv[ks] = frag8(p.qv + off, valid);
+    fdo[ks] = frag8(p.dO + off, valid);
   }
   const int ib = i0 + w * 16 + 4 * (lane >> 4);   // C-layout rows ib + r
   const int64_t prow0 = (bh * p.T + ib) * p.T;
   const uint64_t seed = (p.p_drop > 0.f) ? load_seed(p.seed) : 0ull;
   const float keep = (p.p_drop > 0.f) ? 1.f / (1.f - p.p_drop) : 1.f;
+  // r_i = sum_j dP P = dO_i . O_i (attn_rowdot_kernel, before this kernel) and the forward's lse_i
+  float rs[4], ls[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const bool ok = ib + r < len;
+    rs[r] = ok ? p.rsum[bh * p.T + ib + r] : 0.f;
+    ls[r] = ok ? p.lse[bh * p.T + ib + r] : 3.0e38f;
+  }
 
-  auto dpd = [&](f32x4 (&a)[4]) {
+  // next key block's operands in registers: V and K rows, the Ppos band
+  float4 nv[3], nk[3], nb[6];
+  auto fetch = [&](int kb) {
+    const int j0 = kb * BK;
+    const int rbase = T - 1 - (i0 + BQ - 1) + j0;
+    fetch_rows<3>(nv, p.v, p.ldkv, b * p.T, j0, BK, 0, len, hoff, dk);
+    fetch_rows<3>(nk, p.k, p.ldkv, b * p.T, j0, BK, 0, len, hoff, dk);
+    fetch_rows<6>(nb, p.pos, p.d, 0, rbase, 127, 0, npos, hoff, dk);
+  };
+
+  f32x4 aq[3], av[3];
+#pragma unroll
+  for (int u = 0; u < 3; ++u) { aq[u] = f32x4{0.f, 0.f, 0.f, 0.f}; av[u] = aq[u]; }
+  const int wb = 48 - 16 * w;   // this wave's band offset
+  float* G = Wsc[w];                                    // f32 score band [16][LG32]
+  uint16_t* D = reinterpret_cast<uint16_t*>(Wsc[w]);    // bf16 dS [16][LW]   (after the scores)
+  uint16_t* Gk = D + 16 * LW;                           // bf16 skewed dS [16][LG]
+  if (nkb > 0) fetch(0);
+  for (int kb = 0; kb < nkb; ++kb) {
+    const int j0 = kb * BK;
+    __syncthreads();
+    put_rows<3>(Vs, nullptr, 0, nv, BK, dk);
+    put_rows<3>(Ks, nullptr, 0, nk, BK, dk);
+    put_rows<6>(Pr, nullptr, 0, nb, 127, dk);
+    __syncthreads();
+    if (kb + 1 < nkb) fetch(kb + 1);
+    // ---- S of this wave's 16 rows x 64 keys: the forward's scores (relpos_attn_fwd_kernel) ----
+    float s[4][4];
+    {
+      f32x4 ac[4], g[5];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) ac[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int t = 0; t < 5; ++t) g[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int kof = ks * 32 + 8 * (lane >> 4);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const bf16x8 kbf = *reinterpret_cast<const bf16x8*>(Ks + (16 * t + (lane & 15)) * LR + kof);
+          ac[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fu[ks], kbf, ac[t], 0, 0, 0);
+        }
+#pragma unroll
+        for (int t = 0; t < 5; ++t) {
+          const bf16x8 pb = *reinterpret_cast<const bf16x8*>(Pr + (wb + 16 * t + (lane & 15)) * LR + kof);
+          g[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fv[ks], pb, g[t], 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < 5; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) G[(4 * (lane >> 4) + r) * LG32 + 16 * t + (lane & 15)] = g[t][r];
+      wsync();
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int ii = 4 * (lane >> 4) + r, jj = 16 * t + (lane & 15);
+          const float bd = G[ii * LG32 + jj - ii + 15];
+          s[t][r] = (j0 + jj < len) ? (ac[t][r] + bd) * p.scale : -3.0e38f;
+        }
+      wsync();   // the scratch is rewritten below
+    }
+    // ---- dPd = dO V^T ----
+    f32x4 a[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) a[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -193,86 +270,39 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AbP p) {
         const bf16x8 vb = *reinterpret_cast<const bf16x8*>(Vs + (16 * t + (lane & 15)) * LR + ks * 32 + 8 * (lane >> 4));
         a[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fdo[ks], vb, a[t], 0, 0, 0);
       }
-  };
-
-  // r_i = sum_j dP P = dO_i . O_i (attn_rowdot_kernel, before this kernel)
-  float rs[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) rs[r] = (ib + r < T) ? p.rsum[bh * p.T + ib + r] : 0.f;
-
-  // next key block's operands in registers: V, K rows, the Ppos band, this lane's 16 P elements
-  float4 nv[3], nk[3], nb[6];
-  float np[4][4];
-  auto fetch = [&](int kb) {
-    const int j0 = kb * BK;
-    const int rbase = T - 1 - (i0 + BQ - 1) + j0;
-    fetch_rows<3>(nv, p.v, p.ldkv, b * p.T, j0, BK, 0, len, hoff, dk);
-    fetch_rows<3>(nk, p.k, p.ldkv, b * p.T, j0, BK, 0, len, hoff, dk);
-    fetch_rows<6>(nb, p.pos, p.d, 0, rbase, 127, 0, npos, hoff, dk);
+    for (int e = lane; e < 16 * LG / 2; e += 64) reinterpret_cast<uint32_t*>(Gk)[e] = 0u;
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int i = ib + r, j = j0 + 16 * t + (lane & 15);
-        np[t][r] = (i < T && j < len) ? p.P[prow0 + (int64_t)r * p.T + j] : 0.f;
-      }
-  };
-
-  // ---- dQu += dS K, dQv += skew(dS) Pband ----
-  f32x4 aq[3], av[3];
-#pragma unroll
-  for (int u = 0; u < 3; ++u) { aq[u] = f32x4{0.f, 0.f, 0.f, 0.f}; av[u] = aq[u]; }
-  const int wb = 48 - 16 * w;   // this wave's band offset
-  uint16_t* D = Ds[w];
-  uint16_t* G = Gs[w];
-  if (nkb > 0) fetch(0);
-  for (int kb = 0; kb < nkb; ++kb) {
-    const int j0 = kb * BK;
-    __syncthreads();
-    put_rows<3>(Vs, nullptr, 0, nv, BK, dk);
-    put_rows<3>(nullptr, Kt, LT, nk, BK, dk);
-    put_rows<6>(nullptr, Pbt, LB, nb, 127, dk);
-    for (int e = lane; e < 16 * LG / 2; e += 64) reinterpret_cast<uint32_t*>(G)[e] = 0u;
-    __syncthreads();
-    f32x4 a[4];
-    dpd(a);
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int i = ib + r, j = j0 + 16 * t + (lane & 15);
-        float g = 0.f;
-        if (i < T && j < len) {
-          g = a[t][r];
+        float ds = 0.f;
+        if (i < len && j < len) {
+          float g = a[t][r];
           if (p.p_drop > 0.f)
             g = dropout_keep(seed, p.rng_stream, (uint64_t)(prow0 + (int64_t)r * p.T + j), p.p_drop) ? g * keep : 0.f;
+          ds = __expf(s[t][r] - ls[r]) * (g - rs[r]) * p.scale;
         }
-        const float ds = np[t][r] * (g - rs[r]) * p.scale;
         const int ii = 4 * (lane >> 4) + r, jj = 16 * t + (lane & 15);
         const uint16_t bv = f2bf(ds);
         D[ii * LW + jj] = bv;
-        G[ii * LG + jj - ii + 15] = bv;
+        Gk[ii * LG + jj - ii + 15] = bv;
       }
-    if (kb + 1 < nkb) fetch(kb + 1);   // the P elements are consumed: the next block's loads overlap the MFMAs
     wsync();
+    // ---- dQu += dS K (K read transposed), dQv += skew(dS) Pband (band read transposed) ----
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const bf16x8 da = *reinterpret_cast<const bf16x8*>(D + (lane & 15) * LW + ks * 32 + 8 * (lane >> 4));
 #pragma unroll
-      for (int u = 0; u < 3; ++u) {
-        const bf16x8 kbf = *reinterpret_cast<const bf16x8*>(Kt + (16 * u + (lane & 15)) * LT + ks * 32 + 8 * (lane >> 4));
-        aq[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, kbf, aq[u], 0, 0, 0);
-      }
+      for (int u = 0; u < 3; ++u) aq[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, tr_frag(Ks, LR, ks * 32, 16 * u, lane),
+                                                                                aq[u], 0, 0, 0);
     }
 #pragma unroll
     for (int ks = 0; ks < 3; ++ks) {
-      const bf16x8 ga = *reinterpret_cast<const bf16x8*>(G + (lane & 15) * LG + ks * 32 + 8 * (lane >> 4));
+      const bf16x8 ga = *reinterpret_cast<const bf16x8*>(Gk + (lane & 15) * LG + ks * 32 + 8 * (lane >> 4));
 #pragma unroll
-      for (int u = 0; u < 3; ++u) {
-        const bf16x8 pb =
-            *reinterpret_cast<const bf16x8*>(Pbt + (16 * u + (lane & 15)) * LB + wb + ks * 32 + 8 * (lane >> 4));
-        av[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ga, pb, av[u], 0, 0, 0);
-      }
+      for (int u = 0; u < 3; ++u)
+        av[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ga, tr_frag(Pr, LR, wb + ks * 32, 16 * u, lane), av[u], 0, 0, 0);
     }
     wsync();
   }
@@ -294,12 +324,11 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AbP p) {
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256, 2) void attn_bwd_dkv_kernel(AbP p) {
   __shared__ __attribute__((aligned(16))) uint16_t Os[BQ * LR];     // dO block [query][c]
-  __shared__ __attribute__((aligned(16))) uint16_t Ot[BDK * LT];    // dO block^T [c][query]
-  __shared__ __attribute__((aligned(16))) uint16_t Qt[BDK * LT];    // Qu block^T [c][query]
-  __shared__ __attribute__((aligned(16))) float Pt[BK * (BQ + 1)];  // P block^T [key][query]
-  __shared__ __attribute__((aligned(16))) uint16_t Pw[4][16 * LW];  // per wave Pd^T [key][query]
-  __shared__ __attribute__((aligned(16))) uint16_t Dw[4][16 * LW];  // per wave dS^T [key][query]
-  __shared__ float Rs[BQ];
+  __shared__ __attribute__((aligned(16))) uint16_t Qs[BQ * LR];     // Qu block [query][c]
+  __shared__ __attribute__((aligned(16))) uint16_t Qvs[BQ * LR];    // Qv block [query][c]
+  __shared__ __attribute__((aligned(16))) uint16_t Pr[PB * LR];     // Ppos band [band row][c]
+  __shared__ __attribute__((aligned(16))) float Wsc[4][WS2 / 4];    // per-wave scratch
+  __shared__ float Rs[BQ], Ls[BQ];
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int T = (int)p.T, dk = (int)p.dkh;
@@ -308,17 +337,22 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkv_kernel(AbP p) {
   const int64_t b = bh / p.H, h = bh - b * p.H;
   const int j0 = (int)blk.x * BK;
   const int len = p.lens ? (int)min<int64_t>(p.lens[b], p.T) : T;
+  const int npos = 2 * T - 1;
   const int64_t hoff = h * p.dkh;
-  for (int e = threadIdx.x; e < BQ * (BDK - dk); e += 256) Os[(e / (BDK - dk)) * LR + dk + e % (BDK - dk)] = 0;
-  for (int e = threadIdx.x; e < (BDK - dk) * LT; e += 256) { Ot[dk * LT + e] = 0; Qt[dk * LT + e] = 0; }
+  zero_pad(Os, BQ, dk, BQ);
+  zero_pad(Qs, BQ, dk, BQ);
+  zero_pad(Qvs, BQ, dk, BQ);
+  zero_pad(Pr, PB, dk, 127);
 
-  const int jk = j0 + w * 16 + (lane & 15);   // A-fragment row (key)
-  bf16x8 fv[2];
+  const int jk = j0 + w * 16 + (lane & 15);   // A-fragment row (key): K and V fragments
+  bf16x8 fk[2], fv[2];
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks) {
     const int c0 = ks * 32 + 8 * (lane >> 4);
     const bool ok = jk < len;
-    fv[ks] = frag8(p.v + (b * p.T + (ok ? jk : 0)) * p.ldkv + hoff + c0, ok ? dk - c0 : 0);
+    const int64_t off = (b * p.T + (ok ? jk : 0)) * p.ldkv + hoff + c0;
+    fk[ks] = frag8(p.k + off, ok ? dk - c0 : 0);
+    fv[ks] = frag8(p.v + off, ok ? dk - c0 : 0);
   }
   const int jb = j0 + w * 16 + 4 * (lane >> 4);   // C-layout key rows jb + r
   const uint64_t seed = (p.p_drop > 0.f) ? load_seed(p.seed) : 0ull;
@@ -326,63 +360,95 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkv_kernel(AbP p) {
   f32x4 adv[3], adk[3];
 #pragma unroll
   for (int u = 0; u < 3; ++u) { adv[u] = f32x4{0.f, 0.f, 0.f, 0.f}; adk[u] = adv[u]; }
-  uint16_t* PW = Pw[w];
-  uint16_t* DW = Dw[w];
-  const int nqb = (j0 < len) ? (len + BQ - 1) / BQ : 0;   // query rows >= len have P == 0
-  // next query block's operands in registers: dO and Qu rows, the P block (row-major, coalesced along
-  // keys), the row sums
-  float4 ndo[3], nqu[3];
-  float npb[BQ * BK / 256];
-  float nrs = 0.f;
+  float* H = Wsc[w];                                         // f32 band tile [32][LH]
+  uint16_t* PW = reinterpret_cast<uint16_t*>(Wsc[w]);        // bf16 Pd^T [key][query]  (after the band)
+  uint16_t* DW = PW + 16 * LW;                               // bf16 dS^T [key][query]
+  const int nqb = (j0 < len) ? (len + BQ - 1) / BQ : 0;      // query rows >= len have P == 0
+  // next query block's operands in registers: dO, Qu and Qv rows, the band, row sums and lse
+  float4 ndo[3], nqu[3], nqv[3], nb[6];
+  float nrs = 0.f, nls = 3.0e38f;
   auto fetch = [&](int qb) {
     const int i0 = qb * BQ;
     fetch_rows<3>(ndo, p.dO, p.ldq, b * p.T, i0, BQ, 0, T, hoff, dk);
     fetch_rows<3>(nqu, p.qu, p.ldq, b * p.T, i0, BQ, 0, T, hoff, dk);
-#pragma unroll
-    for (int it = 0; it < BQ * BK / 256; ++it) {
-      const int e = threadIdx.x + it * 256;
-      const int ii = e / BK, kk = e - ii * BK;
-      const int i = i0 + ii, j = j0 + kk;
-      npb[it] = (i < T && j < T) ? p.P[(bh * p.T + i) * p.T + j] : 0.f;
+    fetch_rows<3>(nqv, p.qv, p.ldq, b * p.T, i0, BQ, 0, T, hoff, dk);
+    fetch_rows<6>(nb, p.pos, p.d, 0, T - 1 - i0 - 63 + j0, 127, 0, npos, hoff, dk);
+    if (threadIdx.x < BQ) {
+      const bool ok = i0 + (int)threadIdx.x < len;
+      nrs = ok ? p.rsum[bh * p.T + i0 + threadIdx.x] : 0.f;
+      nls = ok ? p.lse[bh * p.T + i0 + threadIdx.x] : 3.0e38f;
     }
-    if (threadIdx.x < BQ) nrs = (i0 + threadIdx.x < T) ? p.rsum[bh * p.T + i0 + threadIdx.x] : 0.f;
   };
   if (nqb > 0) fetch(0);
   for (int qb = 0; qb < nqb; ++qb) {
     const int i0 = qb * BQ;
     __syncthreads();
-    put_rows<3>(Os, Ot, LT, ndo, BQ, dk);
-    put_rows<3>(nullptr, Qt, LT, nqu, BQ, dk);
-#pragma unroll
-    for (int it = 0; it < BQ * BK / 256; ++it) {
-      const int e = threadIdx.x + it * 256;
-      const int ii = e / BK, kk = e - ii * BK;
-      Pt[kk * (BQ + 1) + ii] = npb[it];
-    }
-    if (threadIdx.x < BQ) Rs[threadIdx.x] = nrs;
+    put_rows<3>(Os, nullptr, 0, ndo, BQ, dk);
+    put_rows<3>(Qs, nullptr, 0, nqu, BQ, dk);
+    put_rows<3>(Qvs, nullptr, 0, nqv, BQ, dk);
+    put_rows<6>(Pr, nullptr, 0, nb, 127, dk);
+    if (threadIdx.x < BQ) { Rs[threadIdx.x] = nrs; Ls[threadIdx.x] = nls; }
     __syncthreads();
-    if (qb + 1 < nqb) fetch(qb + 1);
-    // dPd^T = V dO^T (16 keys x 64 queries per wave)
-    f32x4 a[4];
+    // ---- S^T (16 keys x 64 queries) = K Qu^T + the band term ----
+    f32x4 ac[4];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) a[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < 4; ++t) ac[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
-        const bf16x8 ob = *reinterpret_cast<const bf16x8*>(Os + (16 * t + (lane & 15)) * LR + ks * 32 + 8 * (lane >> 4));
-        a[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fv[ks], ob, a[t], 0, 0, 0);
+        const int ro = (16 * t + (lane & 15)) * LR + ks * 32 + 8 * (lane >> 4);
+        ac[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fk[ks], *reinterpret_cast<const bf16x8*>(Qs + ro), ac[t], 0, 0, 0);
+      }
+    // band term of query slice t: bd^T[jj][ii'] = Qv_{i0+16t+ii'} . Ppos[T-1-i+j] = H[jj - ii' + 15][ii'] with
+    // H = Pband[base .. base+31] Qv_slice^T, base = 48 - 16 t + 16 w
+    float s[4][4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      f32x4 hh[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+      const int base = 48 - 16 * t + 16 * w;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const bf16x8 qvb = *reinterpret_cast<const bf16x8*>(Qvs + (16 * t + (lane & 15)) * LR + ks * 32 + 8 * (lane >> 4));
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+          const bf16x8 pa = *reinterpret_cast<const bf16x8*>(Pr + (base + 16 * mt + (lane & 15)) * LR + ks * 32 +
+                                                             8 * (lane >> 4));
+          hh[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, qvb, hh[mt], 0, 0, 0);
+        }
       }
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) H[(16 * mt + 4 * (lane >> 4) + r) * LH + (lane & 15)] = hh[mt][r];
+      wsync();
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int jj = 4 * (lane >> 4) + r, ii = lane & 15;
+        s[t][r] = (ac[t][r] + H[(jj - ii + 15) * LH + ii]) * p.scale;
+      }
+      wsync();
+    }
+    // the next block's loads are issued here (not before the band term: register pressure) and overlap
+    // the dPd / dV / dK MFMAs
+    if (qb + 1 < nqb) fetch(qb + 1);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      // ---- dPd^T = V dO^T, one 16-query slice at a time (register pressure) ----
+      f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int ro = (16 * t + (lane & 15)) * LR + ks * 32 + 8 * (lane >> 4);
+        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fv[ks], *reinterpret_cast<const bf16x8*>(Os + ro), a, 0, 0, 0);
+      }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int kk = 4 * (lane >> 4) + r, qq = 16 * t + (lane & 15);
         const int j = jb + r, i = i0 + qq;
         float pd = 0.f, ds = 0.f;
-        if (j < len && i < T) {
-          const float pv = Pt[(j - j0) * (BQ + 1) + qq];
-          float g = a[t][r];
+        if (j < len && i < len) {
+          const float pv = __expf(s[t][r] - Ls[qq]);
+          float g = a[r];
           pd = pv;
           if (p.p_drop > 0.f) {
             const uint64_t idx = (uint64_t)((bh * p.T + i) * p.T + j);
@@ -395,17 +461,17 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkv_kernel(AbP p) {
         PW[kk * LW + qq] = f2bf(pd);
         DW[kk * LW + qq] = f2bf(ds);
       }
+    }
     wsync();
+    // ---- dV += Pd^T dO, dK += dS^T Qu (dO / Qu read transposed out of their row images) ----
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const bf16x8 pa = *reinterpret_cast<const bf16x8*>(PW + (lane & 15) * LW + ks * 32 + 8 * (lane >> 4));
       const bf16x8 da = *reinterpret_cast<const bf16x8*>(DW + (lane & 15) * LW + ks * 32 + 8 * (lane >> 4));
 #pragma unroll
       for (int u = 0; u < 3; ++u) {
-        const bf16x8 ob = *reinterpret_cast<const bf16x8*>(Ot + (16 * u + (lane & 15)) * LT + ks * 32 + 8 * (lane >> 4));
-        const bf16x8 qb = *reinterpret_cast<const bf16x8*>(Qt + (16 * u + (lane & 15)) * LT + ks * 32 + 8 * (lane >> 4));
-        adv[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, ob, adv[u], 0, 0, 0);
-        adk[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, qb, adk[u], 0, 0, 0);
+        adv[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, tr_frag(Os, LR, ks * 32, 16 * u, lane), adv[u], 0, 0, 0);
+        adk[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, tr_frag(Qs, LR, ks * 32, 16 * u, lane), adk[u], 0, 0, 0);
       }
     }
     wsync();
@@ -428,9 +494,12 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkv_kernel(AbP p) {
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256, 2) void attn_bwd_dpos_kernel(AbP p) {
   __shared__ __attribute__((aligned(16))) uint16_t Vs[NPJ * LR];     // V rows jbase.. [key][c]
+  __shared__ __attribute__((aligned(16))) uint16_t Ks[NPJ * LR];     // K rows jbase.. [key][c]
+  __shared__ __attribute__((aligned(16))) uint16_t Pr[PB * LR];      // Ppos rows r0-31 .. r0+95 [row][c]
   __shared__ __attribute__((aligned(16))) uint16_t Dl[NPQ * LDL];    // dS [i - ib0][j - jbase]
   __shared__ __attribute__((aligned(16))) uint16_t Qt[BDK * LQ3];    // Qv^T [c][i - ib0]
-  __shared__ float Rs[NPQ];
+  __shared__ __attribute__((aligned(16))) float Gw[4][16 * LG3];     // per-wave f32 score band
+  __shared__ float Rs[NPQ], Ls[NPQ];
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int T = (int)p.T, dk = (int)p.dkh;
@@ -442,12 +511,26 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dpos_kernel(AbP p) {
   const int64_t hoff = h * p.dkh;
   const uint64_t seed = (p.p_drop > 0.f) ? load_seed(p.seed) : 0ull;
   const float keep = (p.p_drop > 0.f) ? 1.f / (1.f - p.p_drop) : 1.f;
-  for (int e = threadIdx.x; e < NPJ * (BDK - dk); e += 256) Vs[(e / (BDK - dk)) * LR + dk + e % (BDK - dk)] = 0;
+  zero_pad(Vs, NPJ, dk, NPJ);
+  zero_pad(Ks, NPJ, dk, NPJ);
   for (int e = threadIdx.x; e < (BDK - dk) * LQ3; e += 256) Qt[dk * LQ3 + e] = 0;
+  // the positional band is the same for every iteration of this workgroup: staged once
+  zero_pad(Pr, PB, dk, 127);
+  {
+    const int cq = dk >> 2;
+    for (int e = threadIdx.x; e < 127 * cq; e += 256) {
+      const int rr = e / cq, c4 = (e - rr * cq) * 4;
+      const int r = r0 - 31 + rr;
+      const float4 v = (r >= 0 && r < npos) ? *reinterpret_cast<const float4*>(p.pos + (int64_t)r * p.d + hoff + c4)
+                                            : make_float4(0.f, 0.f, 0.f, 0.f);
+      st4(Pr + rr * LR + c4, v);
+    }
+  }
   f32x4 acc[3];
 #pragma unroll
   for (int u = 0; u < 3; ++u) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int qh = w & 1, kh = w >> 1;   // dS computation: query half, key half (48 keys)
+  const int qh = w & 1, kh = w >> 1;   // S / dS computation: query half, key half (48 keys)
+  const int wb = 16 - 16 * qh + 48 * kh;   // this wave's band offset inside Pr
   const int64_t b0 = bchunk * p.bpc;
   const int64_t b1 = min<int64_t>(p.B, b0 + p.bpc);
   // iterations (utterance b, query block ib0) that address a valid key for these positions
@@ -469,34 +552,33 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dpos_kernel(AbP p) {
     }
     return false;
   };
-  // next iteration's operands in registers (software pipeline): V rows, Qv rows, row sums, this
-  // lane's dO fragments and 12 P elements
-  float4 nvr[(NPJ * 12 + 255) / 256], nqr[(NPQ * 12 + 255) / 256];
-  float nrs = 0.f;
-  bf16x8 nfdo[2];
-  float np[3][4];
+  // next iteration's operands in registers (software pipeline): V and K rows, Qv rows, row sums and
+  // lse, this lane's dO and Qu fragments
+  float4 nvr[(NPJ * 12 + 255) / 256], nkr[(NPJ * 12 + 255) / 256], nqr[(NPQ * 12 + 255) / 256];
+  float nrs = 0.f, nls = 3.0e38f;
+  bf16x8 nfdo[2], nfqu[2];
   auto fetch = [&](int64_t bb, int ib, int ln) {
     const int jb = r0 - (T - 1) + ib;
     const int64_t bhh = bb * p.H + h;
     fetch_rows<(NPJ * 12 + 255) / 256>(nvr, p.v, p.ldkv, bb * p.T, jb, NPJ, 0, ln, hoff, dk);
+    fetch_rows<(NPJ * 12 + 255) / 256>(nkr, p.k, p.ldkv, bb * p.T, jb, NPJ, 0, ln, hoff, dk);
     fetch_rows<(NPQ * 12 + 255) / 256>(nqr, p.qv, p.ldq, bb * p.T, ib, NPQ, 0, ln, hoff, dk);
-    if (threadIdx.x < NPQ) nrs = (ib + (int)threadIdx.x < ln) ? p.rsum[bhh * p.T + ib + threadIdx.x] : 0.f;
+    if (threadIdx.x < NPQ) {
+      const bool ok = ib + (int)threadIdx.x < ln;
+      nrs = ok ? p.rsum[bhh * p.T + ib + threadIdx.x] : 0.f;
+      nls = ok ? p.lse[bhh * p.T + ib + threadIdx.x] : 3.0e38f;
+    }
     const int iq = ib + 16 * qh + (lane & 15);
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int c0 = ks * 32 + 8 * (lane >> 4);
       const bool ok = iq < ln;
-      nfdo[ks] = frag8(p.dO + (bb * p.T + (ok ? iq : 0)) * p.ldq + hoff + c0, ok ? dk - c0 : 0);
+      const int64_t off = (bb * p.T + (ok ? iq : 0)) * p.ldq + hoff + c0;
+      nfdo[ks] = frag8(p.dO + off, ok ? dk - c0 : 0);
+      nfqu[ks] = frag8(p.qu + off, ok ? dk - c0 : 0);
     }
-#pragma unroll
-    for (int t = 0; t < 3; ++t)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int il = 16 * qh + 4 * (lane >> 4) + r, jl = 48 * kh + 16 * t + (lane & 15);
-        const int i = ib + il, j = jb + jl;
-        np[t][r] = (i < ln && j >= 0 && j < ln) ? p.P[(bhh * p.T + i) * p.T + j] : 0.f;
-      }
   };
+  float* G = Gw[w];
   int64_t b = b0;
   int ib0 = -NPQ, len = b0 < b1 ? ulen(b0) : 0;
   bool more = b0 < b1 && advance(b, ib0, len);
@@ -508,38 +590,57 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dpos_kernel(AbP p) {
     const int cur_ib0 = ib0;
     __syncthreads();
     put_rows<(NPJ * 12 + 255) / 256>(Vs, nullptr, 0, nvr, NPJ, dk);
+    put_rows<(NPJ * 12 + 255) / 256>(Ks, nullptr, 0, nkr, NPJ, dk);
     put_rows<(NPQ * 12 + 255) / 256>(nullptr, Qt, LQ3, nqr, NPQ, dk);
-    if (threadIdx.x < NPQ) Rs[threadIdx.x] = nrs;
+    if (threadIdx.x < NPQ) { Rs[threadIdx.x] = nrs; Ls[threadIdx.x] = nls; }
     const bf16x8 fdo[2] = {nfdo[0], nfdo[1]};
+    const bf16x8 fqu[2] = {nfqu[0], nfqu[1]};
     __syncthreads();
-    // dPd for queries ib0 + 16 qh + .., keys jbase + 48 kh + ..
-    f32x4 a[3];
+    // queries ib0 + 16 qh + .., keys jbase + 48 kh + ..: S (AC + skewed band) and dPd
+    f32x4 ac[3], a[3], g[4];
 #pragma unroll
-    for (int t = 0; t < 3; ++t) a[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < 3; ++t) { ac[t] = f32x4{0.f, 0.f, 0.f, 0.f}; a[t] = ac[t]; }
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
+    for (int t = 0; t < 4; ++t) g[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const bf16x8 fqv = tr_frag(Qt, LQ3, ks * 32, 16 * qh, lane);   // Qv rows as the A operand
 #pragma unroll
       for (int t = 0; t < 3; ++t) {
-        const bf16x8 vb = *reinterpret_cast<const bf16x8*>(Vs + (48 * kh + 16 * t + (lane & 15)) * LR + ks * 32 +
-                                                             8 * (lane >> 4));
-        a[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fdo[ks], vb, a[t], 0, 0, 0);
+        const int ro = (48 * kh + 16 * t + (lane & 15)) * LR + ks * 32 + 8 * (lane >> 4);
+        ac[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fqu[ks], *reinterpret_cast<const bf16x8*>(Ks + ro), ac[t], 0, 0, 0);
+        a[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fdo[ks], *reinterpret_cast<const bf16x8*>(Vs + ro), a[t], 0, 0, 0);
       }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const bf16x8 pb = *reinterpret_cast<const bf16x8*>(Pr + (wb + 16 * t + (lane & 15)) * LR + ks * 32 +
+                                                           8 * (lane >> 4));
+        g[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fqv, pb, g[t], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) G[(4 * (lane >> 4) + r) * LG3 + 16 * t + (lane & 15)] = g[t][r];
+    wsync();
 #pragma unroll
     for (int t = 0; t < 3; ++t)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int il = 16 * qh + 4 * (lane >> 4) + r, jl = 48 * kh + 16 * t + (lane & 15);
+        const int ii = 4 * (lane >> 4) + r, jj = 16 * t + (lane & 15);
+        const int il = 16 * qh + ii, jl = 48 * kh + jj;
         const int i = cur_ib0 + il, j = jbase + jl;
         float ds = 0.f;
         if (i < cur_len && j >= 0 && j < cur_len) {
+          const float sv = (ac[t][r] + G[ii * LG3 + jj - ii + 15]) * p.scale;
           const int64_t idx = (bh * p.T + i) * p.T + j;
-          float g = a[t][r];
-          if (p.p_drop > 0.f) g = dropout_keep(seed, p.rng_stream, (uint64_t)idx, p.p_drop) ? g * keep : 0.f;
-          ds = np[t][r] * (g - Rs[il]) * p.scale;
+          float gg = a[t][r];
+          if (p.p_drop > 0.f) gg = dropout_keep(seed, p.rng_stream, (uint64_t)idx, p.p_drop) ? gg * keep : 0.f;
+          ds = __expf(sv - Ls[il]) * (gg - Rs[il]) * p.scale;
         }
         Dl[il * LDL + jl] = f2bf(ds);
       }
-    // the P elements are consumed: the next iteration's loads overlap the dPpos MFMAs
+    // the operands are consumed: the next iteration's loads overlap the dPpos MFMAs
     more = advance(b, ib0, len);
     if (more) fetch(b, ib0, len);
     __syncthreads();
@@ -585,21 +686,21 @@ int64_t kdfm_relpos_attn_bwd_ws(int64_t B, int64_t H, int64_t T, int64_t d) {
 }
 
 int kdfm_relpos_attn_bwd(const float* dO, const float* O, const float* qu, const float* qv, const float* qkv,
-                         const float* pos, const float* P, const int64_t* lengths, float* dqu, float* dqv, float* dqkv,
-                         float* dpos,
+                         const float* pos, const float* lse, const int64_t* lengths, float* dqu, float* dqv,
+                         float* dqkv, float* dpos,
                          float* ws, int64_t ws_len, int64_t B, int64_t H, int64_t T, int64_t d, float scale,
                          float dropout_p, const uint64_t* seed, uint64_t rng_stream, void* stream) {
-  return kdfm_relpos_attn_bwd_parts(dO, O, qu, qv, qkv, pos, P, lengths, dqu, dqv, dqkv, dpos, ws, ws_len, B, H, T, d,
+  return kdfm_relpos_attn_bwd_parts(dO, O, qu, qv, qkv, pos, lse, lengths, dqu, dqv, dqkv, dpos, ws, ws_len, B, H, T, d,
                                     scale, dropout_p, seed, rng_stream, KDFM_ATTN_BWD_ALL, stream);
 }
 
 int kdfm_relpos_attn_bwd_parts(const float* dO, const float* O, const float* qu, const float* qv, const float* qkv,
-                               const float* pos, const float* P, const int64_t* lengths, float* dqu, float* dqv,
+                               const float* pos, const float* lse, const int64_t* lengths, float* dqu, float* dqv,
                                float* dqkv, float* dpos, float* ws, int64_t ws_len, int64_t B, int64_t H, int64_t T,
                                int64_t d, float scale, float dropout_p, const uint64_t* seed, uint64_t rng_stream,
                                int32_t parts, void* stream) {
   using namespace kdfm;
-  KDFM_REQUIRE(dO && O && qu && qv && qkv && pos && P && ws, "null pointer");
+  KDFM_REQUIRE(dO && O && qu && qv && qkv && pos && lse && ws, "null pointer");
   KDFM_REQUIRE(!(parts & KDFM_ATTN_BWD_DQ) || (dqu && dqv), "dq part needs dqu / dqv");
   KDFM_REQUIRE(!(parts & KDFM_ATTN_BWD_DKV) || dqkv, "dkv part needs dqkv");
   KDFM_REQUIRE(!(parts & KDFM_ATTN_BWD_DPOS) || dpos, "dpos part needs dpos");
@@ -609,11 +710,11 @@ int kdfm_relpos_attn_bwd_parts(const float* dO, const float* O, const float* qu,
   KDFM_REQUIRE(T > 0 && T <= 4096 && d % 4 == 0, "bad T / d");
   KDFM_REQUIRE(dropout_p == 0.f || seed, "dropout needs a seed");
   KDFM_REQUIRE(ws_len >= kdfm_relpos_attn_bwd_ws(B, H, T, d), "workspace too small (kdfm_relpos_attn_bwd_ws)");
-  KDFM_REQUIRE((((uintptr_t)dO | (uintptr_t)qu | (uintptr_t)qv | (uintptr_t)qkv | (uintptr_t)pos | (uintptr_t)P) & 15) == 0,
+  KDFM_REQUIRE((((uintptr_t)dO | (uintptr_t)qu | (uintptr_t)qv | (uintptr_t)qkv | (uintptr_t)pos) & 15) == 0,
                "operands must be 16-byte aligned");
   if (B == 0) return KDFM_OK;
   AbP p{};
-  p.dO = dO; p.qu = qu; p.qv = qv; p.k = qkv + d; p.v = qkv + 2 * d; p.pos = pos; p.P = P; p.lens = lengths;
+  p.dO = dO; p.qu = qu; p.qv = qv; p.k = qkv + d; p.v = qkv + 2 * d; p.pos = pos; p.lse = lse; p.lens = lengths;
   p.dqu = dqu; p.dqv = dqv; p.rsum = ws; p.dpos_part = ws + B * H * T;
   p.dk = dqkv ? dqkv + d : nullptr;
   p.dv = dqkv ? dqkv + 2 * d : nullptr;

@@ -8,10 +8,13 @@
 //   * the BD term only needs the 127-row band of P that the block's (i, j) pairs address
 //     (r = T-1-i+j); each wave computes G = Qv P_band^T (16 x 80) and reads it back skewed from
 //     LDS: S_bd[ii][jj] = G[ii][jj - ii + 15]  (rel_shift as an index map, no copy);
-//   * two passes over the key blocks: (1) row max and sum, (2) exact probabilities, optional
-//     P / P_drop output (the student's backward consumes them), the counter-RNG dropout mask of
-//     the unfused kernel (same index -> same mask) and O += P_drop V via MFMA (P staged through
-//     LDS into A-fragment order, V staged transposed).
+//   * one pass over the key blocks with an online softmax (running row max / sum, O rescaled), the
+//     counter-RNG dropout mask of the unfused kernel (same index -> same mask) applied to the
+//     unnormalised probabilities and O += P_drop V via MFMA (P staged through LDS into A-fragment
+//     order, V staged transposed); training writes only the per-row log-sum-exp
+//     lse_i = m_i + ln l_i (B*H*T floats), from which the backward recomputes P = exp(S - lse);
+//   * (the unfused backward's path) two passes: (1) row max and sum, (2) exact probabilities with
+//     the P / P_drop outputs the per-op backward reads.
 // Output O is written straight into the (rows, d) head-interleaved layout.
 #include "gemm_common.h"
 
@@ -31,7 +34,7 @@ constexpr int LDG = GW + 1;       // f32 stride of the per-wave G tile
 struct AttnP {
   const float* qu; const float* qv; const float* k; const float* v; const float* pos;
   const int64_t* lens;
-  float* o; float* P; float* Pd;
+  float* o; float* P; float* Pd; float* lse;
   int64_t B, H, T, d, dk, ldq, ldkv;
   float scale, p_drop;
   const uint64_t* seed; uint64_t rng_stream;
@@ -318,6 +321,15 @@ __global__ __launch_bounds__(256, 2) void relpos_attn_fwd_kernel(AttnP p) {
     wave_lds_sync();  // Ps is rewritten by the next block
   }
 
+  // ---- per-row log-sum-exp for the backward's recompute (single pass; +inf-like sentinel for rows
+  // with no valid key: their P row is zero) ----
+  if (!TWO_PASS && p.lse && (lane & 15) == 0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = ib + r;
+      if (i < T) p.lse[bh * p.T + i] = (i < len && lrow[r] > 0.f) ? mrow[r] + logf(lrow[r]) : 3.0e38f;
+    }
+  }
   // ---- O -> (rows, d) ----
   float fin[4];
 #pragma unroll
@@ -335,7 +347,8 @@ __global__ __launch_bounds__(256, 2) void relpos_attn_fwd_kernel(AttnP p) {
 }  // namespace kdfm
 
 extern "C" int kdfm_relpos_attn_fwd(const float* qu, const float* qv, const float* qkv, const float* pos,
-                                    const int64_t* lengths, float* o, float* P, float* Pdrop, int64_t B, int64_t H,
+                                    const int64_t* lengths, float* o, float* P, float* Pdrop, float* lse,
+                                    int64_t B, int64_t H,
                                     int64_t T, int64_t d, float scale, float dropout_p, const uint64_t* seed,
                                     uint64_t rng_stream, void* stream) {
   using namespace kdfm;
@@ -346,10 +359,11 @@ extern "C" int kdfm_relpos_attn_fwd(const float* qu, const float* qv, const floa
   KDFM_REQUIRE(T > 0 && T <= 4096, "T out of range");
   KDFM_REQUIRE(d % 4 == 0, "d must be a multiple of 4");
   KDFM_REQUIRE(dropout_p == 0.f || seed, "dropout needs a seed");
+  KDFM_REQUIRE(!(lse && (P || Pdrop)), "lse is the single-pass output (no P / Pdrop with it)");
   if (B == 0) return KDFM_OK;
   AttnP p;
   p.qu = qu; p.qv = qv; p.k = qkv + d; p.v = qkv + 2 * d; p.pos = pos; p.lens = lengths;
-  p.o = o; p.P = P; p.Pd = Pdrop;
+  p.o = o; p.P = P; p.Pd = Pdrop; p.lse = lse;
   p.B = B; p.H = H; p.T = T; p.d = d; p.dk = dk; p.ldq = d; p.ldkv = 3 * d;
   p.scale = scale; p.p_drop = dropout_p; p.seed = seed; p.rng_stream = rng_stream;
   dim3 grid((unsigned)ceil_div(T, AQ), (unsigned)(B * H));

@@ -6,6 +6,8 @@
 //   and the final loss assembly (asr_train_diffm.py:803-811).
 #include <math.h>
 
+#include <type_traits>
+
 #include "common.h"
 
 namespace kdfm {
@@ -20,15 +22,18 @@ __device__ __forceinline__ float lse2(float a, float b) {
   return m + log1pf(__expf(-fabsf(a - b)));
 }
 
+// one wave per row, NV = ceil(C / 64) values per lane in registers (vocabularies up to 4096 classes:
+// the decoder width V+1 comes from the teacher's tokenizer, conformer_ctc_bpe.yaml:87)
+template <int NV>
 __global__ __launch_bounds__(256) void log_softmax_kernel(const float* __restrict__ x, float* __restrict__ y, int64_t rows,
                                                           int C, int64_t ldx, int64_t ldy) {
   const int lane = threadIdx.x & 63;
   const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= rows) return;
-  float v[4];
+  float v[NV];
   float mx = NEG_INF;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < NV; ++i) {
     const int c = lane + 64 * i;
     v[i] = (c < C) ? x[r * ldx + c] : NEG_INF;
     mx = fmaxf(mx, v[i]);
@@ -36,10 +41,10 @@ __global__ __launch_bounds__(256) void log_softmax_kernel(const float* __restric
   mx = wave_max(mx);
   float s = 0.f;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) s += (lane + 64 * i < C) ? __expf(v[i] - mx) : 0.f;
+  for (int i = 0; i < NV; ++i) s += (lane + 64 * i < C) ? __expf(v[i] - mx) : 0.f;
   const float lz = mx + __logf(wave_sum(s));
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < NV; ++i) {
     const int c = lane + 64 * i;
     if (c < C) y[r * ldy + c] = v[i] - lz;
   }
@@ -67,22 +72,23 @@ __global__ __launch_bounds__(256) void argmax_kernel(const float* __restrict__ x
 }
 
 // dx = dy - exp(y) * sum(dy)   (log_softmax backward, y = log_softmax output)
+template <int NV>
 __global__ __launch_bounds__(256) void log_softmax_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ y,
                                                               float* __restrict__ dx, int64_t rows, int C) {
   const int lane = threadIdx.x & 63;
   const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= rows) return;
-  float g[4];
+  float g[NV];
   float s = 0.f;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < NV; ++i) {
     const int c = lane + 64 * i;
     g[i] = (c < C) ? dy[r * C + c] : 0.f;
     s += g[i];
   }
   s = wave_sum(s);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < NV; ++i) {
     const int c = lane + 64 * i;
     if (c < C) dx[r * C + c] = g[i] - __expf(y[r * C + c]) * s;
   }
@@ -292,6 +298,7 @@ __global__ __launch_bounds__(256) void ctc_grad_kernel(const float* __restrict__
 
 // grad += coef*(softmax(lp/T) - p_t) ; loss_acc += loss_scale * sum_c p_t (log p_t - log_softmax(lp/T))
 // teacher p_t = softmax(log_softmax(tl)/T)   (tl: teacher decoder logits)
+template <int NV>
 __global__ __launch_bounds__(256) void kl_kernel(const float* __restrict__ lp, const float* __restrict__ tl,
                                                  float* __restrict__ grad, float* __restrict__ loss_acc, int64_t rows,
                                                  int C, float invT, float coef, float loss_scale) {
@@ -299,10 +306,10 @@ __global__ __launch_bounds__(256) void kl_kernel(const float* __restrict__ lp, c
   const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   float contrib = 0.f;
   if (r < rows) {
-    float sv[4], tv[4];
+    float sv[NV], tv[NV];
     float ms = NEG_INF, mt = NEG_INF;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < NV; ++i) {
       const int c = lane + 64 * i;
       sv[i] = (c < C) ? lp[r * C + c] * invT : NEG_INF;
       tv[i] = (c < C) ? tl[r * C + c] : NEG_INF;
@@ -313,27 +320,27 @@ __global__ __launch_bounds__(256) void kl_kernel(const float* __restrict__ lp, c
     mt = wave_max(mt);
     float ss = 0.f, st = 0.f;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < NV; ++i) {
       ss += (lane + 64 * i < C) ? __expf(sv[i] - ms) : 0.f;
       st += (lane + 64 * i < C) ? __expf(tv[i] - mt) : 0.f;
     }
     const float lzs = ms + __logf(wave_sum(ss));
     const float lzt = mt + __logf(wave_sum(st));
     // teacher: logp = tl - lzt ; then q = softmax(logp / T)
-    float q[4];
+    float q[NV];
     float mq = NEG_INF;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < NV; ++i) {
       q[i] = (lane + 64 * i < C) ? (tv[i] - lzt) * invT : NEG_INF;
       mq = fmaxf(mq, q[i]);
     }
     mq = wave_max(mq);
     float sq = 0.f;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) sq += (lane + 64 * i < C) ? __expf(q[i] - mq) : 0.f;
+    for (int i = 0; i < NV; ++i) sq += (lane + 64 * i < C) ? __expf(q[i] - mq) : 0.f;
     const float lzq = mq + __logf(wave_sum(sq));
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < NV; ++i) {
       const int c = lane + 64 * i;
       if (c < C) {
         const float logpt = q[i] - lzq;
@@ -364,6 +371,16 @@ __global__ void loss_combine_kernel(const float* __restrict__ nll, int64_t B, co
   out[4] = f;
 }
 
+// values per lane of the row kernels: the smallest compiled NV with 64 * NV >= C (C <= 4096)
+template <typename F>
+int row_dispatch(int64_t C, F&& go) {
+  if (C <= 256) return go(std::integral_constant<int, 4>{});
+  if (C <= 512) return go(std::integral_constant<int, 8>{});
+  if (C <= 1088) return go(std::integral_constant<int, 17>{});   // V = 1024 BPE: 1025 classes
+  if (C <= 2048) return go(std::integral_constant<int, 32>{});
+  return go(std::integral_constant<int, 64>{});
+}
+
 }  // namespace
 }  // namespace kdfm
 
@@ -372,11 +389,13 @@ extern "C" {
 int kdfm_log_softmax(const float* x, float* y, int64_t rows, int64_t C, int64_t ldx, int64_t ldy, void* stream) {
   using namespace kdfm;
   KDFM_REQUIRE(x && y, "null pointer");
-  KDFM_REQUIRE(C > 0 && C <= 256, "classes in (0,256]");
+  KDFM_REQUIRE(C > 0 && C <= 4096, "classes in (0,4096]");
   if (rows == 0) return KDFM_OK;
-  hipLaunchKernelGGL(log_softmax_kernel, dim3((unsigned)ceil_div(rows, 4)), dim3(256), 0, as_stream(stream), x, y,
-                     rows, (int)C, ldx, ldy);
-  return check_launch("kdfm_log_softmax");
+  return row_dispatch(C, [&](auto nv) {
+    hipLaunchKernelGGL(log_softmax_kernel<decltype(nv)::value>, dim3((unsigned)ceil_div(rows, 4)), dim3(256), 0,
+                       as_stream(stream), x, y, rows, (int)C, ldx, ldy);
+    return check_launch("kdfm_log_softmax");
+  });
 }
 
 int kdfm_argmax_rows(const float* x, int64_t* idx, int64_t rows, int64_t C, void* stream) {
@@ -391,11 +410,13 @@ int kdfm_argmax_rows(const float* x, int64_t* idx, int64_t rows, int64_t C, void
 int kdfm_log_softmax_bwd(const float* dy, const float* y, float* dx, int64_t rows, int64_t C, void* stream) {
   using namespace kdfm;
   KDFM_REQUIRE(dy && y && dx, "null pointer");
-  KDFM_REQUIRE(C > 0 && C <= 256, "classes in (0,256]");
+  KDFM_REQUIRE(C > 0 && C <= 4096, "classes in (0,4096]");
   if (rows == 0) return KDFM_OK;
-  hipLaunchKernelGGL(log_softmax_bwd_kernel, dim3((unsigned)ceil_div(rows, 4)), dim3(256), 0, as_stream(stream), dy, y,
-                     dx, rows, (int)C);
-  return check_launch("kdfm_log_softmax_bwd");
+  return row_dispatch(C, [&](auto nv) {
+    hipLaunchKernelGGL(log_softmax_bwd_kernel<decltype(nv)::value>, dim3((unsigned)ceil_div(rows, 4)), dim3(256), 0,
+                       as_stream(stream), dy, y, dx, rows, (int)C);
+    return check_launch("kdfm_log_softmax_bwd");
+  });
 }
 
 int kdfm_ctc_loss(const float* log_probs, const int64_t* targets, const int64_t* input_lengths,
@@ -435,11 +456,14 @@ int kdfm_kl_div_logits(const float* student_logp, const float* teacher_logits, f
                        int64_t rows, int64_t C, float temperature, float grad_coef, float loss_scale, void* stream) {
   using namespace kdfm;
   KDFM_REQUIRE(student_logp && teacher_logits && grad && loss_acc, "null pointer");
-  KDFM_REQUIRE(C > 0 && C <= 256 && temperature > 0.f, "bad args");
+  KDFM_REQUIRE(C > 0 && C <= 4096 && temperature > 0.f, "bad args");
   if (rows == 0) return KDFM_OK;
-  hipLaunchKernelGGL(kl_kernel, dim3((unsigned)ceil_div(rows, 4)), dim3(256), 0, as_stream(stream), student_logp,
-                     teacher_logits, grad, loss_acc, rows, (int)C, 1.f / temperature, grad_coef, loss_scale);
-  return check_launch("kdfm_kl_div_logits");
+  return row_dispatch(C, [&](auto nv) {
+    hipLaunchKernelGGL(kl_kernel<decltype(nv)::value>, dim3((unsigned)ceil_div(rows, 4)), dim3(256), 0,
+                       as_stream(stream), student_logp, teacher_logits, grad, loss_acc, rows, (int)C, 1.f / temperature,
+                       grad_coef, loss_scale);
+    return check_launch("kdfm_kl_div_logits");
+  });
 }
 
 int kdfm_loss_combine(const float* nll, int64_t B, const float* kl, const float* recon, const float* fm,

@@ -102,6 +102,34 @@ int kdfm_device_arch(char* buf, int64_t len) {
   return KDFM_OK;
 }
 
+// stream-ordering and memset primitives of the step-plan replay (kdfm/plan.py): the recorded step's
+// cross-stream edges and zero fills re-issued without going through torch
+int kdfm_event_record(void* event, void* stream) {
+  if (hipEventRecord(static_cast<hipEvent_t>(event), kdfm::as_stream(stream)) != hipSuccess) {
+    kdfm::set_error("kdfm_event_record: hipEventRecord failed");
+    return KDFM_ELAUNCH;
+  }
+  return KDFM_OK;
+}
+
+int kdfm_stream_wait_event(void* stream, void* event) {
+  if (hipStreamWaitEvent(kdfm::as_stream(stream), static_cast<hipEvent_t>(event), 0) != hipSuccess) {
+    kdfm::set_error("kdfm_stream_wait_event: hipStreamWaitEvent failed");
+    return KDFM_ELAUNCH;
+  }
+  return KDFM_OK;
+}
+
+int kdfm_memset_async(void* ptr, int32_t value, int64_t bytes, void* stream) {
+  KDFM_REQUIRE(ptr || bytes == 0, "null pointer");
+  if (bytes == 0) return KDFM_OK;
+  if (hipMemsetAsync(ptr, value, (size_t)bytes, kdfm::as_stream(stream)) != hipSuccess) {
+    kdfm::set_error("kdfm_memset_async: hipMemsetAsync failed");
+    return KDFM_ELAUNCH;
+  }
+  return KDFM_OK;
+}
+
 int kdfm_colsum(const float* X, float* out, int64_t M, int64_t N, int64_t ld, float scale, int32_t accumulate,
                 void* stream) {
   using namespace kdfm;

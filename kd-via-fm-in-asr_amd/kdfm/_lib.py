@@ -115,6 +115,9 @@ SIGNATURES: dict[str, tuple] = {
     "kdfm_denoise_chain_fwd": (_i32, [P, P, P, P, P, P, P, P, P, _i64, _i64, _i32, _i32, P]),
     "kdfm_denoise_chain_bwd": (_i32, [P, P, P, P, P, P, P, P, _i64, _i64, _i32, _i32, P]),
     "kdfm_range_pop": (_i32, []),
+    "kdfm_event_record": (_i32, [P, P]),
+    "kdfm_stream_wait_event": (_i32, [P, P]),
+    "kdfm_memset_async": (_i32, [P, _i32, _i64, P]),
     "kdfm_cast_bf16": (_i32, [P, P, _i64, P]),
     "kdfm_cast_bf16_t": (_i32, [P, P, P, _i64, _i64, P]),
     "kdfm_colsum": (_i32, [P, P, _i64, _i64, _i64, _f32, _i32, P]),
@@ -148,7 +151,7 @@ SIGNATURES: dict[str, tuple] = {
     "kdfm_qkv_prep": (_i32, [P, P, P, P, P, _i64, _i64, P]),
     "kdfm_relpos_softmax_fwd": (_i32, [P, P, P, P, P, _i64, _i64, _i64, _f32, _f32, P, C.c_uint64, P]),
     "kdfm_relpos_softmax_bwd": (_i32, [P, P, P, P, _i64, _i64, _i64, _f32, _f32, P, C.c_uint64, P]),
-    "kdfm_relpos_attn_fwd": (_i32, [P, P, P, P, P, P, P, P, _i64, _i64, _i64, _i64, _f32, _f32, P, C.c_uint64, P]),
+    "kdfm_relpos_attn_fwd": (_i32, [P, P, P, P, P, P, P, P, P, _i64, _i64, _i64, _i64, _f32, _f32, P, C.c_uint64, P]),
     "kdfm_relpos_table": (_i32, [P, _i64, _i64, P]),
     "kdfm_glu_mask_fwd": (_i32, [P, P, P, _i64, _i64, _i64, P]),
     "kdfm_glu_mask_bwd": (_i32, [P, P, P, P, _i64, _i64, _i64, P]),

@@ -98,6 +98,10 @@ class Ver5Engine:
         # graph and the whole-step graph's branches behind the main stream
         self.compute_stream = _crit_stream(dev) if dev.type == "cuda" else None
         self._link_in, self._link_out = K.StreamLink(), K.StreamLink()   # caller <-> compute stream
+        # weight gradients on the side stream (the benchmark's schedule) or in line: None follows the
+        # config (in line exactly when deterministic); the overlapped-vs-serialised determinism test
+        # forces both with ordered reductions
+        self.overlap_wgrad = None
         # capture the frozen teacher as a HIP graph in training steps (KDFM_TEACHER_GRAPH=0: eager)
         self.teacher_graph = __import__("os").environ.get("KDFM_TEACHER_GRAPH", "0") == "1"
         if init:
@@ -401,9 +405,10 @@ class Ver5Engine:
     def backward(self, ctx, grad_ready=None):
         """grad_ready(offset): optional callback, called whenever every student gradient at flat
         index >= offset is final (BucketedGradAllReduce.ready overlap)."""
-        # deterministic mode also keeps the weight-gradient products on the issuing stream: with the
-        # side stream overlapping, repeated runs differed in ~1e-3 of some gradients (DESIGN.md §4)
-        with self._on_stream(), self._mode(), WGRAD.serialized(self.cfg.deterministic), K.region("backward"):
+        # deterministic mode keeps the weight-gradient products on the issuing stream unless
+        # overlap_wgrad says otherwise
+        serial = self.cfg.deterministic if self.overlap_wgrad is None else not self.overlap_wgrad
+        with self._on_stream(), self._mode(), WGRAD.serialized(serial), K.region("backward"):
             self._backward(ctx, grad_ready)
 
     def _backward(self, ctx, grad_ready):
@@ -467,6 +472,36 @@ class Ver5Engine:
                 scale = allreduce(self.student.grad)
         self.optimizer_step(scale)
         return self.losses
+
+
+    def make_plan(self, wav, wav_len, targets, tgt_len, allreduce=None):
+        """Record one training step (RNG advance, forward, backward, all-reduce, AdamW) as a StepPlan
+        (kdfm/plan.py) whose replay() is the same step issued without the Python wrappers, on the same
+        four streams.  The inputs are the plan's static buffers (copy each new batch into them).  Run
+        one eager train_step first so every lazily created workspace exists.  The all-reduce's ready()
+        callbacks and its final wait run as host callbacks in their recorded places."""
+        from .plan import StepPlan
+        plan = StepPlan()
+        ready = getattr(allreduce, "ready", None)
+        grad = self.student.grad
+        box = {}
+
+        def finish():
+            box["scale"] = allreduce(self.student.grad) if allreduce is not None else 1.0
+
+        def step():
+            self.advance_rng()
+            ctx = self.forward(wav, wav_len, targets, tgt_len, train=True)
+            self.backward(ctx, grad_ready=(lambda o: plan.host(ready, grad, o)) if ready is not None else None)
+            del ctx
+            if allreduce is not None:
+                with K.region("allreduce"):
+                    plan.host(finish)
+            self.optimizer_step(box.get("scale", 1.0))
+
+        plan.record(step)
+        plan.inputs = (wav, wav_len, targets, tgt_len)
+        return plan
 
 
 class GraphedTrainStep:

@@ -38,7 +38,7 @@ class Trace:
 
     def __init__(self, tags):
         self.tags = set(tags)
-        self.events = []   # (tag, flops, algorithmic bytes, start, end)
+        self.events = []   # (tag, flops, algorithmic bytes, start, end, raw stream)
 
     def __enter__(self):
         Trace.active = self
@@ -50,10 +50,14 @@ class Trace:
     def wants(self, tag):
         return tag in self.tags or ("*" in self.tags and tag is None)
 
-    def summary(self):
+    def summary(self, stream=None):
+        """{tag: launches, ms_total, flops_total, bytes_total}; with `stream` (a raw stream pointer)
+        only the launches issued on that stream (e.g. the engine's critical-path compute stream)."""
         torch.cuda.synchronize()
         out = {}
-        for tag, flops, nbytes, s, e in self.events:
+        for tag, flops, nbytes, s, e, st in self.events:
+            if stream is not None and st != stream:
+                continue
             ms = s.elapsed_time(e)
             t = out.setdefault(tag, [0, 0.0, 0.0, 0.0])
             t[0] += 1
@@ -76,7 +80,7 @@ def _traced(tag, flops, nbytes, name, *args):
     ev0.record()
     call(name, *args)
     ev1.record()
-    tr.events.append((tag, float(flops), float(nbytes), ev0, ev1))
+    tr.events.append((tag, float(flops), float(nbytes), ev0, ev1, stream_ptr()))
 
 
 def set_ranges(on: bool) -> None:
@@ -125,7 +129,7 @@ class span(region):
     def __exit__(self, *a):
         if self.ev is not None:
             self.ev[1].record()
-            Trace.active.events.append((self.tag, self.flops, self.nbytes, self.ev[0], self.ev[1]))
+            Trace.active.events.append((self.tag, self.flops, self.nbytes, self.ev[0], self.ev[1], stream_ptr()))
         super().__exit__(*a)
 
 
@@ -408,10 +412,12 @@ def gemm(A, B, Cout, M, N, K, sAm, sAk, sBk, sBn, sCm, sCn, *, amode, bmode,
             side = sum(1 for t in (R, aux, Cpre) if t is not None)
             nbytes = 4.0 * (M * K + K * N + M * N * (1 + side)) * batch[0] * batch[1]
         fl = 2.0 * M * N * K * batch[0] * batch[1]
+        sp = stream_ptr()
         if tag in tr.tags:
-            tr.events.append((tag, fl, nbytes, ev0, ev1))
+            tr.events.append((tag, fl, nbytes, ev0, ev1, sp))
         if "*" in tr.tags:
-            tr.events.append(("gemm:" + ROUTES.get(int(_lib.lib().kdfm_gemm_last_route()), "?"), fl, nbytes, ev0, ev1))
+            tr.events.append(("gemm:" + ROUTES.get(int(_lib.lib().kdfm_gemm_last_route()), "?"), fl, nbytes, ev0, ev1,
+                              sp))
         return
     call("kdfm_gemm", _GEMM_DESC, _s())
 
@@ -1115,45 +1121,50 @@ def relpos_attn_bwd_ws(B, H, T, d):
     return int(_lib.lib().kdfm_relpos_attn_bwd_ws(B, H, T, d))
 
 
-def relpos_attn_bwd(do, o, qu, qv, qkv, ppos, P, lengths, dqu, dqv, dqkv, dppos, B, H, T, scale, p, seed, rng_stream,
+def relpos_attn_bwd(do, o, qu, qv, qkv, ppos, lse, lengths, dqu, dqv, dqkv, dppos, B, H, T, scale, p, seed, rng_stream,
                     parts=ATTN_BWD_ALL, ws=None):
-    """Fused attention backward (csrc/attn_bwd.hip): dqu, dqv, dK/dV into dqkv[:, d:], dppos.  `parts`
+    """Fused attention backward (csrc/attn_bwd.hip): dqu, dqv, dK/dV into dqkv[:, d:], dppos, with the
+    probabilities recomputed from the forward's per-row log-sum-exp `lse` (B, H, T).  `parts`
     (ATTN_BWD_*) issues a subset; parts issued on different streams must share a dedicated `ws`
     (relpos_attn_bwd_ws floats) and be ordered after ROWDOT."""
     rows, d = do.shape
-    assert rows == B * T and qkv.shape == (rows, 3 * d) and P.shape == (B, H, T, T)
+    assert rows == B * T and qkv.shape == (rows, 3 * d) and lse.shape == (B, H, T)
     assert dppos is None or dppos.shape == (2 * T - 1, d)
-    for t in (do, o, qu, qv, qkv, ppos, P, dqu, dqv, dqkv, dppos):
+    for t in (do, o, qu, qv, qkv, ppos, lse, dqu, dqv, dqkv, dppos):
         assert t is None or t.is_contiguous()
     assert o.shape == do.shape
     if parts != ATTN_BWD_ALL:
         assert ws is not None and ws.numel() >= relpos_attn_bwd_ws(B, H, T, d)
-        call("kdfm_relpos_attn_bwd_parts", ptr(do), ptr(o), ptr(qu), ptr(qv), ptr(qkv), ptr(ppos), ptr(P),
+        call("kdfm_relpos_attn_bwd_parts", ptr(do), ptr(o), ptr(qu), ptr(qv), ptr(qkv), ptr(ppos), ptr(lse),
              ptr(_i64(lengths)), ptr(dqu), ptr(dqv), ptr(dqkv), ptr(dppos), ptr(ws), ws.numel(), B, H, T, d,
              float(scale), float(p), ptr(seed), int(rng_stream), int(parts), _s())
         return
     ws = scratch(do.device, relpos_attn_bwd_ws(B, H, T, d))
-    # algorithmic: the 4 products per (b, h) of dQu, dQv, dK, dV, dPpos + dP (2 T^2 dk each, band ~2 T^2 dk)
-    # and bytes: dO, O, qu, qv, K, V read, P (f32) read, dqu, dqv, dK, dV written
+    # algorithmic: per (b, h) the products dP, dQu, dQv, dK, dV, dPpos (2 T^2 dk each, the positional band
+    # counted as one T x T) plus the score recompute (QK^T + band), bytes: dO, O, qu, qv, K, V read once,
+    # dqu, dqv, dK, dV written, lse read
     dk = d // H
-    fl = 2.0 * B * H * T * T * dk * 6
-    nb = 4.0 * rows * d * 10 + 4.0 * B * H * T * T
-    _traced("attn_bwd", fl, nb, "kdfm_relpos_attn_bwd", ptr(do), ptr(o), ptr(qu), ptr(qv), ptr(qkv), ptr(ppos), ptr(P),
-            ptr(_i64(lengths)), ptr(dqu), ptr(dqv), ptr(dqkv), ptr(dppos), ptr(ws), ws.numel(), B, H, T, d,
+    fl = 2.0 * B * H * T * T * dk * 8
+    nb = 4.0 * rows * d * 10 + 4.0 * B * H * T
+    _traced("attn_bwd", fl, nb, "kdfm_relpos_attn_bwd", ptr(do), ptr(o), ptr(qu), ptr(qv), ptr(qkv), ptr(ppos),
+            ptr(lse), ptr(_i64(lengths)), ptr(dqu), ptr(dqv), ptr(dqkv), ptr(dppos), ptr(ws), ws.numel(), B, H, T, d,
             float(scale), float(p), ptr(seed), int(rng_stream), _s())
 
 
-def relpos_attn_fwd(qu, qv, qkv, ppos, lengths, o, P, Pd, B, H, T, scale, p, seed, rng_stream):
-    """Fused rel-pos MHA forward (bf16); P / Pd (B,H,T,T) written when given."""
+def relpos_attn_fwd(qu, qv, qkv, ppos, lengths, o, P, Pd, B, H, T, scale, p, seed, rng_stream, lse=None):
+    """Fused rel-pos MHA forward (bf16): P / Pd (B,H,T,T) written when given (two passes), else one
+    online-softmax pass that writes the per-row log-sum-exp `lse` (B,H,T) when given."""
     rows, d = qu.shape
     assert rows == B * T and qkv.shape == (rows, 3 * d) and ppos.shape == (2 * T - 1, d) and o.shape == (rows, d)
     assert qu.is_contiguous() and qv.is_contiguous() and qkv.is_contiguous() and ppos.is_contiguous()
+    assert lse is None or (lse.shape == (B, H, T) and P is None and Pd is None)
     # algorithmic: QK^T, the positional band (one T x T-equivalent) and PV, 2 T^2 dk FLOP each per (b, h);
-    # bytes: qu, qv, K, V, o once (+ P written when saved)
+    # bytes: qu, qv, K, V, o once (+ P written when saved, + lse)
     fl = 2.0 * B * H * T * T * (d // H) * 3
-    nb = 4.0 * rows * d * 5 + (4.0 * B * H * T * T if P is not None else 0.0)
+    nb = 4.0 * rows * d * 5 + (4.0 * B * H * T * T if P is not None else 0.0) + (4.0 * B * H * T if lse is not None
+                                                                                 else 0.0)
     _traced("attn_fwd", fl, nb, "kdfm_relpos_attn_fwd", ptr(qu), ptr(qv), ptr(qkv), ptr(ppos), ptr(_i64(lengths)),
-            ptr(o), ptr(P), ptr(Pd), B, H, T, d, float(scale), float(p), ptr(seed), rng_stream, _s())
+            ptr(o), ptr(P), ptr(Pd), ptr(lse), B, H, T, d, float(scale), float(p), ptr(seed), rng_stream, _s())
 
 
 def relpos_softmax_fwd(ac, bd, lengths, P, Pd, B, H, T, scale, p, seed, rng_stream):

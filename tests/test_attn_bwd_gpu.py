@@ -2,7 +2,9 @@
 against (a) float64 torch autograd of NeMo's rel-pos attention (Appendix A.7: scores = ((q+u)K^T +
 rel_shift((q+v)Ppos^T)) / sqrt(dk), key mask, softmax, rows of padded queries zeroed, O = P V) with
 no dropout, and (b) the unfused f32 path (dPd GEMM + relpos_softmax_bwd + five batched GEMMs) on
-the same saved P with attention dropout 0.1 (same counter-RNG mask).
+the saved P of the two-pass forward with attention dropout 0.1 (same counter-RNG mask).  The fused
+backward itself reads no probabilities: it recomputes them from the single-pass forward's per-row
+log-sum-exp, which is checked against float64 too.
 
 Tolerances: relative Frobenius error per gradient (dQu, dQv, dK, dV, dPpos) <= 2e-2 against float64
 (bf16 operands, f32 accumulation) and <= 2e-2 against the unfused f32 kernels; padded keys get
@@ -35,17 +37,19 @@ def _inputs(B, H, T, d, seed):
 
 
 def _fused(K, qkv, qu, qv, ppos, do, lens, B, H, T, d, p, seed):
+    """single-pass forward (O + lse), then the fused backward; returns (lse, O, grads...)"""
     dk = d // H
-    P = torch.empty(B, H, T, T, device="cuda")
+    lse = torch.empty(B, H, T, device="cuda")
     o = torch.empty(B * T, d, device="cuda")
-    K.relpos_attn_fwd(qu, qv, qkv, ppos, lens, o, P, None, B, H, T, 1.0 / math.sqrt(dk), p, seed, 11)
+    K.relpos_attn_fwd(qu, qv, qkv, ppos, lens, o, None, None, B, H, T, 1.0 / math.sqrt(dk), p, seed, 11, lse=lse)
     dqu = torch.empty(B * T, d, device="cuda")
     dqv = torch.empty_like(dqu)
     dqkv = torch.zeros(B * T, 3 * d, device="cuda")
     dpos = torch.empty(2 * T - 1, d, device="cuda")
-    K.relpos_attn_bwd(do, o, qu, qv, qkv, ppos, P, lens, dqu, dqv, dqkv, dpos, B, H, T, 1.0 / math.sqrt(dk), p, seed, 11)
+    K.relpos_attn_bwd(do, o, qu, qv, qkv, ppos, lse, lens, dqu, dqv, dqkv, dpos, B, H, T, 1.0 / math.sqrt(dk), p,
+                      seed, 11)
     torch.cuda.synchronize()
-    return P, dqu, dqv, dqkv[:, d:2 * d], dqkv[:, 2 * d:], dpos
+    return lse, o, dqu, dqv, dqkv[:, d:2 * d], dqkv[:, 2 * d:], dpos
 
 
 def _torch_grads(qkv, qu, qv, ppos, do, lens, B, H, T, d):
@@ -60,6 +64,7 @@ def _torch_grads(qkv, qu, qv, ppos, do, lens, B, H, T, d):
     s = (ac + bd) / math.sqrt(dk)
     keym = torch.arange(T, device="cuda")[None, :] < lens[:, None]
     s = s.masked_fill(~keym[:, None, None, :], float("-inf"))
+    _torch_grads.lse = torch.logsumexp(s, -1).detach()
     P = torch.softmax(s, -1)
     P = torch.where(keym[:, None, :, None], P, torch.zeros_like(P))
     O = (P @ sh(v)).permute(0, 2, 1, 3).reshape(B * T, d)
@@ -72,10 +77,18 @@ def test_attn_bwd_matches_float64(B, H, T, d):
     from kdfm import kernels as K
     qkv, qu, qv, ppos, do, lens = _inputs(B, H, T, d, T + d)
     seed = torch.tensor([99], dtype=torch.int64, device="cuda")
-    _, dqu, dqv, dk_, dv_, dpos = _fused(K, qkv, qu, qv, ppos, do, lens, B, H, T, d, 0.0, seed)
+    lse, _, dqu, dqv, dk_, dv_, dpos = _fused(K, qkv, qu, qv, ppos, do, lens, B, H, T, d, 0.0, seed)
     ref = _torch_grads(qkv, qu, qv, ppos, do, lens, B, H, T, d)
     for name, got, want in zip(("dQu", "dQv", "dK", "dV", "dPpos"), (dqu, dqv, dk_, dv_, dpos), ref):
         assert _rel(got, want) <= 2e-2, (name, _rel(got, want))
+    # the forward's per-row log-sum-exp (valid rows) against float64; rows past the length are 3e38
+    want = _torch_grads.lse
+    for bi in range(B):
+        L = int(lens[bi])
+        err = (lse[bi, :, :L].double().cpu() - want[bi, :, :L].cpu()).abs().max().item()
+        assert err <= 2e-2 * max(1.0, want[bi, :, :L].abs().max().item()), (bi, err)
+        if L < T:
+            assert (lse[bi, :, L:] == 3.0e38).all()
     # keys past an utterance's length receive no gradient
     for bi in range(B):
         L = int(lens[bi])
@@ -92,15 +105,17 @@ def test_attn_bwd_matches_unfused_with_dropout():
     npos = 2 * T - 1
     qkv, qu, qv, ppos, do, lens = _inputs(B, H, T, d, 5)
     seed = torch.tensor([4242], dtype=torch.int64, device="cuda")
-    P, dqu, dqv, dk_, dv_, dpos = _fused(K, qkv, qu, qv, ppos, do, lens, B, H, T, d, p, seed)
+    _, o1, dqu, dqv, dk_, dv_, dpos = _fused(K, qkv, qu, qv, ppos, do, lens, B, H, T, d, p, seed)
     again = _fused(K, qkv, qu, qv, ppos, do, lens, B, H, T, d, p, seed)
-    for a, b in zip((dqu, dqv, dk_, dv_, dpos), again[1:]):
+    for a, b in zip((dqu, dqv, dk_, dv_, dpos), again[2:]):
         assert torch.equal(a, b), "fused attention backward is not bitwise reproducible"
-    # unfused f32 chain on the same P (Pd rebuilt from the same RNG by relpos_softmax_fwd's twin:
-    # take it from the forward kernel run with a P_drop output)
+    # unfused f32 chain on the two-pass forward's saved P and P_drop (same counter-RNG dropout mask)
+    P = torch.empty(B, H, T, T, device="cuda")
     Pd = torch.empty_like(P)
     o = torch.empty(B * T, d, device="cuda")
-    K.relpos_attn_fwd(qu, qv, qkv, ppos, lens, o, torch.empty_like(P), Pd, B, H, T, 1.0 / math.sqrt(dk), p, seed, 11)
+    K.relpos_attn_fwd(qu, qv, qkv, ppos, lens, o, P, Pd, B, H, T, 1.0 / math.sqrt(dk), p, seed, 11)
+    # the single-pass output (online softmax, dropout on the unnormalised probabilities) = the two-pass one
+    assert _rel(o1, o) <= 1e-2, _rel(o1, o)
     f32 = dict(math="f32")
     dPd = torch.empty(B, H, T, T, device="cuda")
     K.gemm(do, qkv[:, 2 * d:], dPd, T, T, dk, d, 1, 1, 3 * d, T, 1, amode=_lib.LD_KC, bmode=_lib.LD_KC,
@@ -140,23 +155,21 @@ def test_attn_bwd_parts_on_two_streams_match_one_launch():
     seed = torch.tensor([77], dtype=torch.int64, device="cuda")
     qkv, qu, qv, ppos, do, lens = _inputs(B, H, T, d, 3)
     ref = _fused(K, qkv, qu, qv, ppos, do, lens, B, H, T, d, p, seed)
-    P = ref[0]
-    o = torch.empty(B * T, d, device="cuda")
-    K.relpos_attn_fwd(qu, qv, qkv, ppos, lens, o, torch.empty_like(P), None, B, H, T, 1.0 / math.sqrt(dk), p, seed, 11)
+    lse, o = ref[0], ref[1]
     dqu = torch.empty(B * T, d, device="cuda")
     dqv = torch.empty_like(dqu)
     dqkv = torch.zeros(B * T, 3 * d, device="cuda")
     dpos = torch.empty(2 * T - 1, d, device="cuda")
     ws = torch.empty(K.relpos_attn_bwd_ws(B, H, T, d), device="cuda")
     sc = 1.0 / math.sqrt(dk)
-    K.relpos_attn_bwd(do, o, qu, qv, qkv, ppos, P, lens, dqu, dqv, dqkv, None, B, H, T, sc, p, seed, 11,
+    K.relpos_attn_bwd(do, o, qu, qv, qkv, ppos, lse, lens, dqu, dqv, dqkv, None, B, H, T, sc, p, seed, 11,
                       parts=K.ATTN_BWD_ROWDOT | K.ATTN_BWD_DQ | K.ATTN_BWD_DKV, ws=ws)
     side = torch.cuda.Stream()
     side.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(side):
-        K.relpos_attn_bwd(do, o, qu, qv, qkv, ppos, P, lens, None, None, None, dpos, B, H, T, sc, p, seed, 11,
+        K.relpos_attn_bwd(do, o, qu, qv, qkv, ppos, lse, lens, None, None, None, dpos, B, H, T, sc, p, seed, 11,
                           parts=K.ATTN_BWD_DPOS, ws=ws)
     torch.cuda.current_stream().wait_stream(side)
     torch.cuda.synchronize()
-    for got, want in zip((dqu, dqv, dqkv[:, d:2 * d], dqkv[:, 2 * d:], dpos), ref[1:]):
+    for got, want in zip((dqu, dqv, dqkv[:, d:2 * d], dqkv[:, 2 * d:], dpos), ref[2:]):
         assert torch.equal(got, want)

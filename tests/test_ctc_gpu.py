@@ -49,7 +49,7 @@ def _run(K, lp, tg, in_len, tgt_len, scale):
 
 
 @pytest.mark.parametrize("B,T,C,Umax", [(6, 401, 129, 100), (3, 700, 129, 300), (2, 1300, 33, 600),
-                                        (4, 7, 5, 3)])
+                                        (4, 7, 5, 3), (4, 401, 1025, 100)])
 def test_ctc_matches_torch_float64(B, T, C, Umax):
     from kdfm import kernels as K
     lp, tg, in_len, tgt_len = _case(B, T, C, Umax, T + Umax)
@@ -74,3 +74,34 @@ def test_ctc_matches_torch_float64(B, T, C, Umax):
         assert nll[2].item() == 0.0 and grad[2].abs().max().item() == 0.0
     nll2, grad2 = _run(K, lp, tg, in_len, tgt_len, scale)
     assert torch.equal(nll, nll2) and torch.equal(grad, grad2)
+
+
+@pytest.mark.parametrize("C", [129, 300, 1025, 3001])
+def test_log_softmax_and_logit_kd_wide_vocab(C):
+    """kdfm_log_softmax / kdfm_kl_div_logits beyond 256 classes (V = 1024 BPE: 1025 decoder outputs,
+    conformer_ctc_bpe.yaml:87; SURVEY §8 V sensitivity) against float64 torch: log_softmax, and the
+    logit KD of asr_train_diffm.py:751-756 (kl_div(log_softmax(s/T), softmax(t/T), 'batchmean') * T^2)
+    with its gradient wrt the student log-probs' logits."""
+    from kdfm import kernels as K
+    g = torch.Generator().manual_seed(C)
+    rows, Tk = 37, 2.0
+    x = torch.randn(rows, C, generator=g, dtype=torch.float64) * 3
+    t = torch.randn(rows, C, generator=g, dtype=torch.float64) * 3
+    lp = torch.empty(rows, C, device="cuda")
+    K.log_softmax(x.float().cuda(), lp)
+    ref = torch.log_softmax(x.float().double(), -1)
+    assert (lp.double().cpu() - ref).abs().max().item() <= 2e-5 * ref.abs().max().item()
+    grad = torch.zeros(rows, C, device="cuda")
+    acc = torch.zeros(1, device="cuda")
+    B = 3
+    K.kl_div_logits(lp, t.float().cuda(), grad, acc, Tk, 0.1 * Tk / B, Tk * Tk / B)
+    torch.cuda.synchronize()
+    s_ = lp.double().cpu().clone().requires_grad_(True)
+    kl = torch.nn.functional.kl_div(torch.log_softmax(s_ / Tk, -1), torch.softmax(torch.log_softmax(t.float().double(), -1)
+                                                                                   / Tk, -1), reduction="sum") * Tk * Tk / B
+    (gs,) = torch.autograd.grad(kl, s_)
+    assert abs(acc.item() - kl.item()) <= 1e-4 * abs(kl.item()) + 1e-6, (acc.item(), kl.item())
+    # the kernel returns d(0.1 * kl)/d(logits): the student log-probs' own log_softmax backward folded in
+    # (sum of the per-row gradient is zero), so compare against dkl/ds projected onto the zero-sum space
+    want = 0.1 * (gs - torch.exp(s_.detach()) * gs.sum(-1, keepdim=True))
+    assert (grad.double().cpu() - want).abs().max().item() <= 1e-4 * want.abs().max().item() + 1e-7

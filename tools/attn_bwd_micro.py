@@ -1,4 +1,4 @@
-"""Micro-benchmark of the fused rel-pos attention forward (with the saved P) and backward kernels at
+"""Micro-benchmark of the fused rel-pos attention forward (training: O + per-row lse) and backward kernels at
 the student bench shape (B=32 utterances, H=2 heads, T'=401 frames, d=88, attention dropout 0.1).
 usage: python tools/attn_bwd_micro.py [reps] [p_drop]   (run under rocprofv3 --kernel-trace --stats for
 the per-kernel split)"""
@@ -30,6 +30,7 @@ def main():
     lens[1::3] = T - 57
     seed = torch.tensor([7], dtype=torch.int64, device=dev)
     P = torch.empty(B, H, T, T, device=dev)
+    lse = torch.empty(B, H, T, device=dev)
     o = torch.empty(rows, d, device=dev)
     dqu = torch.empty(rows, d, device=dev)
     dqv = torch.empty_like(dqu)
@@ -37,13 +38,17 @@ def main():
     dpos = torch.empty(2 * T - 1, d, device=dev)
     sc = 1.0 / math.sqrt(dk)
 
-    def fwd():
+    def fwd_p():
         K.relpos_attn_fwd(qu, qv, qkv, ppos, lens, o, P, None, B, H, T, sc, p, seed, 11)
 
-    def bwd():
-        K.relpos_attn_bwd(do, o, qu, qv, qkv, ppos, P, lens, dqu, dqv, dqkv, dpos, B, H, T, sc, p, seed, 11)
+    def fwd():
+        K.relpos_attn_fwd(qu, qv, qkv, ppos, lens, o, None, None, B, H, T, sc, p, seed, 11, lse=lse)
 
-    for name, fn in (("relpos_attn_fwd (P saved)", fwd), ("relpos_attn_bwd (all kernels)", bwd)):
+    def bwd():
+        K.relpos_attn_bwd(do, o, qu, qv, qkv, ppos, lse, lens, dqu, dqv, dqkv, dpos, B, H, T, sc, p, seed, 11)
+
+    for name, fn in (("relpos_attn_fwd (two-pass, P)", fwd_p), ("relpos_attn_fwd (one pass, lse)", fwd),
+                     ("relpos_attn_bwd (all kernels)", bwd)):
         for _ in range(3):
             fn()
         torch.cuda.synchronize()
