@@ -77,6 +77,11 @@ def parse():
                     help="host threads for the CPU baseline (default: os.cpu_count(), BASELINE.md)")
     ap.add_argument("--no-f32-sensitivity", action="store_true",
                     help="skip the --math f32 sensitivity measurement (the reference trains fp32)")
+    ap.add_argument("--deterministic", action="store_true",
+                    help="ordered reductions everywhere (bitwise-reproducible steps; kdfm_set_deterministic)")
+    ap.add_argument("--eager", action="store_true",
+                    help="issue every timed step through the Python wrappers instead of replaying the recorded "
+                         "step plan (kdfm/plan.py)")
     ap.add_argument("--graph", action="store_true",
                     help="replay the step as one captured HIP graph (measured slower: hipGraph replay ran the "
                          "teacher / weight-gradient / CTC streams serially, 43.9 vs 40.1 ms/step eager)")
@@ -178,7 +183,7 @@ def main():
     from kdfm.config import DEFAULT
     from kdfm.engine import GraphedTrainStep, Ver5Engine, synthetic_batch
 
-    cfg = replace(DEFAULT, math=args.math)
+    cfg = replace(DEFAULT, math=args.math, deterministic=args.deterministic)
     K.set_math(cfg.math)
     eng = Ver5Engine(cfg, dev)
     eng.set_seed(1000 + rank)
@@ -190,11 +195,21 @@ def main():
     ar = BucketedGradAllReduce(eng.student.numel, buckets=4) if world > 1 else None
     # warm-up: one eager step (lazy buffers, allocator pools), graph capture, then replays
     eng.train_step(wav, wl, tg, tl, ar)
-    if not args.graph:
+    issue = "eager"
+    if args.graph:
+        issue = "hip_graph"
+    elif args.eager:
         # eager multi-stream issue: teacher encoder, weight-gradient GEMMs and CTC/KL overlap the
         # student / head chain on their own HIP streams
         run = lambda: eng.train_step(wav, wl, tg, tl, ar)  # noqa: E731
     else:
+        # the same four-stream schedule replayed from a recorded step plan: the launches, cross-stream
+        # edges and all-reduce callbacks of one step, re-issued without the Python wrappers (the
+        # recording is itself a full training step)
+        plan = eng.make_plan(wav, wl, tg, tl, ar)
+        run = plan.replay
+        issue = f"step plan ({len(plan)} recorded ops)"
+    if args.graph:
         graphed = GraphedTrainStep(eng, wav, wl, tg, tl, ar, world)
         run = graphed.step
     for _ in range(max(0, args.warmup - 1)):
@@ -329,7 +344,8 @@ def main():
             "data": "synthetic (0.1*N(0,1) 16 kHz audio, random-init weights; no network for corpora/checkpoints)",
             "config": {"workload": "ver5 FM-distill step, Conformer-CTC-small teacher (d176 h4 L16) -> student "
                                    "(d88 h2 L16), BASELINE.json configs[1] shape",
-                       "global_batch": world * args.batch, "seq_len": args.samples,
+                       "global_batch": world * args.batch, "seq_len": args.samples, "issue": issue,
+                       "deterministic": cfg.deterministic,
                        "frames_subsampled": (args.samples // 160) // 4 + 1, "parallelism": f"dp{world}"},
             "roofline": roof,
             "roofline_by_family": by_route,

@@ -29,7 +29,7 @@ import yaml
 TEACHER_MAP = (("encoder.", "teacher.encoder."), ("decoder.", "teacher.decoder."),
                ("preprocessor.", "teacher.preprocessor."))
 _IGNORED_SUFFIXES = ("num_batches_tracked",)
-_HEAD_PREFIXES = ("tae.", "sproj.", "adapter.", "denoiser.", "fm_latent.", "fm_latent_2.")
+_HEAD_PREFIXES = ("tae.", "sproj.", "adapter.", "denoiser.", "fm_latent.", "fm_latent_2.", "diffkd.")
 
 
 def _fb_nemo(fb: torch.Tensor) -> torch.Tensor:
@@ -52,6 +52,9 @@ def engine_state_dict(eng, *, teacher: bool = True, frontend: bool = True) -> "O
     # heads this version never trains (kept so the reference module can load the dict strictly)
     for name, t in getattr(eng, "frozen_heads", {}).items():
         sd[name] = t.detach().cpu().clone()
+    fixed = getattr(eng, "fixed", None)
+    for name, _ in (fixed.specs if fixed is not None else []):   # used, never trained (DiffKD's encoder)
+        sd[name] = fixed.P[name].detach().cpu().clone()
     for name, _ in eng.bn.specs:
         if teacher or not name.startswith("teacher."):
             sd[name] = eng.bn.P[name].detach().cpu().clone()
@@ -75,7 +78,7 @@ def load_engine_state(eng, sd: dict, *, strict: bool = False, fb_atol: float = 1
     Returns {"missing": [...], "unexpected": [...], "frontend_mismatch": [...]}; strict=True raises
     on missing or unexpected keys (num_batches_tracked and the KD heads the version does not use
     excepted: the reference builds every head for every version)."""
-    stores = [eng.student, eng.teacher, eng.bn]
+    stores = [eng.student, eng.teacher, eng.bn] + ([eng.fixed] if getattr(eng, "fixed", None) is not None else [])
     known = {}
     for st in stores:
         for name, _ in st.specs:

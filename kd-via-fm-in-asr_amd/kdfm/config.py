@@ -43,6 +43,10 @@ class Ver5Config:
     kd_loss_type: str = "mse"
     fm_steps: int = 8
     denoiser_steps: int = 9
+    # --use_diffkd / --diffkd_steps: the DiffKD module on every layer pair, mean over the layers
+    # (asr_train_diffm.py:326-394, :795-800), on top of the version's heads
+    use_diffkd: bool = False
+    diffkd_steps: int = 9
     time_embed_dim: int = 32
     kd_alpha: float = 0.1
     kd_temperature: float = 1.0
@@ -225,6 +229,18 @@ def head_specs(cfg: Ver5Config, fm_prefixes=None) -> list:
     return s
 
 
+def diffkd_specs(cfg: Ver5Config, trained: bool) -> list:
+    """DiffKDModule parameters (asr_train_diffm.py:341-358): trained = decoder, proj, denoiser; the
+    encoder never receives a gradient (its output is detached before every use, :382-383)."""
+    L, Ct, Cs = cfg.latent, cfg.d_teacher, cfg.d_student
+    if not trained:
+        return [("diffkd.encoder.weight", (L, Ct, 1)), ("diffkd.encoder.bias", (L,))]
+    return [("diffkd.decoder.weight", (Ct, L, 1)), ("diffkd.decoder.bias", (Ct,)),
+            ("diffkd.proj.weight", (L, Cs, 1)), ("diffkd.proj.bias", (L,)),
+            ("diffkd.denoiser.0.weight", (L, L, 3)), ("diffkd.denoiser.0.bias", (L,)),
+            ("diffkd.denoiser.2.weight", (L, L, 3)), ("diffkd.denoiser.2.bias", (L,))]
+
+
 def all_head_specs(cfg: Ver5Config) -> list:
     """Every KD head the reference module builds, whatever the version (asr_train_diffm.py:559-564):
     version 6 uses all of them."""
@@ -236,7 +252,8 @@ def student_specs(cfg: Ver5Config) -> list:
     """Trainable parameters of the step: student encoder + decoder + the heads the version uses
     (head_modules; for ver5 fm_latent_2 exists in the reference but never receives a gradient)."""
     return (encoder_specs(cfg, cfg.d_student, cfg.heads_student, "encoder.")
-            + decoder_specs(cfg, cfg.d_student, "decoder.") + head_specs(cfg))
+            + decoder_specs(cfg, cfg.d_student, "decoder.") + head_specs(cfg)
+            + (diffkd_specs(cfg, True) if cfg.use_diffkd else []))
 
 
 def teacher_specs(cfg: Ver5Config) -> list:
@@ -262,5 +279,5 @@ DEFAULT = Ver5Config()
 PARITY = DEFAULT.parity()
 
 __all__ = ["Ver5Config", "DEFAULT", "PARITY", "encoder_specs", "subsampling_specs", "sub_stages", "sub_pad",
-           "sub_channels", "sub_len", "sub_dims", "decoder_specs", "head_specs", "all_head_specs", "head_modules", "student_specs",
+           "sub_channels", "sub_len", "sub_dims", "decoder_specs", "head_specs", "all_head_specs", "diffkd_specs", "head_modules", "student_specs",
            "teacher_specs", "bn_buffer_specs", "fused_groups", "field"]

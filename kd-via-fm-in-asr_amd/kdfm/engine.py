@@ -14,7 +14,7 @@ import torch
 
 from . import _lib
 from . import kernels as K
-from .config import Ver5Config, all_head_specs, bn_buffer_specs, student_specs, teacher_specs
+from .config import Ver5Config, all_head_specs, bn_buffer_specs, diffkd_specs, student_specs, teacher_specs
 from .conformer import EncoderRun, EncoderShapes, compute_lengths, encoder_backward, encoder_forward, \
     encoder_forward_steps, layer_images, make_workspace
 from .frontend import FrontendConsts, frontend_forward, mel_frames, specaugment_
@@ -74,6 +74,9 @@ class Ver5Engine:
         dev = self.device
         self.student = FlatStore(student_specs(cfg), dev, with_grad=True, with_adam=True)
         self.teacher = FlatStore(teacher_specs(cfg), dev, with_grad=False)
+        # used but never-trained student-side parameters: DiffKD's encoder (its output is detached
+        # before every use, asr_train_diffm.py:382-383, so AdamW never touches it)
+        self.fixed = FlatStore(diffkd_specs(cfg, False) if cfg.use_diffkd else [], dev, with_grad=False)
         self.bn = FlatStore(bn_buffer_specs(cfg, cfg.d_student, "encoder.")
                             + bn_buffer_specs(cfg, cfg.d_teacher, "teacher.encoder."), dev, with_grad=False)
         self.fe = FrontendConsts(cfg, dev)
@@ -84,7 +87,8 @@ class Ver5Engine:
         # be restored, checkpoint.restore_lightning_ckpt)
         self.adam_base = torch.zeros(1, dtype=torch.int64, device=dev)
         self.lr = torch.zeros(1, device=dev)
-        self.losses = torch.zeros(5, device=dev)   # total, ctc, kl, recon, layer KD (kd/fm pre+post; ver5: fm_post)
+        # total, ctc, kl, recon, layer KD (kd/fm pre+post, ver5: fm_post; + the DiffKD term with use_diffkd)
+        self.losses = torch.zeros(5, device=dev)
         self.hws = HeadsWorkspace(cfg, dev)
         if K.twins_enabled():   # opt-in direct-B skinny path (KDFM_SKINNY_DIRECT_MIN_M)
             self.student.enable_bf16_twins()
@@ -111,6 +115,8 @@ class Ver5Engine:
             st.update(hd)
             self.student.load(st)
             self.teacher.load(init_uniform(teacher_specs(cfg), teacher_seed))
+            if self.fixed.specs:
+                self.fixed.load(init_uniform(self.fixed.specs, heads_seed + 2000))
             self.reset_bn()
         # heads the reference module builds but this version never trains (asr_train_diffm.py:559-564):
         # kept host-side (seeded init, or whatever a checkpoint held) so saved state dicts carry the
@@ -315,8 +321,9 @@ class Ver5Engine:
         main.wait_stream(side)
         # ---- CTC + logit KD on a third stream: they only need the two logit tensors, and their
         # result is first needed after the KD heads' forward, so the serial CTC recursion overlaps it ----
-        # kl | recon, kd_pre, fm_pre, kd_post, fm_post (heads.RECON..FM_POST) | sum of the four layer-KD terms
-        acc = torch.zeros(7, device=dev)
+        # kl | recon, kd_pre, fm_pre, kd_post, fm_post (heads.RECON..FM_POST) | diffkd | sum of the layer-KD
+        # terms and diffkd
+        acc = torch.zeros(8, device=dev)
         aux = self._aux_stream()
         aux.wait_stream(main)
         Umax = targets.shape[1]
@@ -335,9 +342,10 @@ class Ver5Engine:
         n = cfg.n_layers * rows
         with K.region("heads_forward"):
             hctx = heads_forward(cfg, self.student.P, sfeats.view(n, Ss.d), tfeats.view(n, St.d), T, self.hws,
-                                 acc[1:6], seed=seed, eps=eps, save=save)
-            K.colsum(acc[2:6].view(4, 1), acc[6:7], accumulate=False)
-        self.kd_terms = acc[1:6]   # device (recon, kd_pre, fm_pre, kd_post, fm_post): the v/* log keys
+                                 acc[1:6], seed=seed, eps=eps, save=save, Pfix=self.fixed.P, acc_diffkd=acc[6:7])
+            K.colsum(acc[2:7].view(5, 1), acc[7:8], accumulate=False)
+        # device (recon, kd_pre, fm_pre, kd_post, fm_post, diffkd): the v/* log keys
+        self.kd_terms = acc[1:7]
         ctx = dict(B=B, T=T, Ss=Ss, St=St, mel_len=mel_len, len1=len1, len2=len2, srun=srun, sfeats=sfeats,
                    glogits=glogits, hctx=hctx, lp=lp, nll=nll, pos_s=pos_s, acc=acc)
         self._join_losses(ctx)   # CTC/KL overlapped the heads forward; losses valid after forward()
@@ -400,7 +408,7 @@ class Ver5Engine:
         """Join the CTC/KL stream and assemble the loss vector (total, ctc, kl, recon, fm)."""
         torch.cuda.current_stream(self.device).wait_stream(self._aux_stream())
         acc = ctx["acc"]
-        K.loss_combine(ctx["nll"], acc[0:1], acc[1:2], acc[6:7], self.cfg.kd_alpha, self.losses)
+        K.loss_combine(ctx["nll"], acc[0:1], acc[1:2], acc[7:8], self.cfg.kd_alpha, self.losses)
 
     def backward(self, ctx, grad_ready=None):
         """grad_ready(offset): optional callback, called whenever every student gradient at flat

@@ -52,6 +52,11 @@ class HeadsWorkspace:
             K.register_bf16_twin(self.wconv, self.wconv_h)
         self.g1 = _empty(L, 3 * L, dev=dev)
         self.g2 = _empty(L, 3 * L, dev=dev)
+        # the DiffKD denoiser's own GEMM-layout weights and weight-gradient accumulators (its backward
+        # can overlap the version denoiser's on the weight-gradient stream)
+        self.dk_wconv = _empty(4, L, 3 * L, dev=dev)
+        self.dk_g1 = _empty(L, 3 * L, dev=dev)
+        self.dk_g2 = _empty(L, 3 * L, dev=dev)
         # per FM module: per-step first-layer bias (time embedding folded in), time features, bias grads
         self.fm = {}
         for pre in ("fm_latent.fm.", "fm_latent_2.fm."):
@@ -219,6 +224,73 @@ def _deno_fused(Lt):
     return K.get_math() == "bf16" and Lt == 96 and _DENO_FUSED
 
 
+class _Deno:
+    """Weight names and workspace slots of one SimpleDenoiser-shaped chain: the version's denoiser
+    (asr_train_diffm.py:444-460, `denoiser.net.{0,2}`) or DiffKD's (:350-354, `diffkd.denoiser.{0,2}`)."""
+
+    def __init__(self, ws, pre, steps, diffkd=False):
+        self.w1, self.w2 = pre + "0.weight", pre + "2.weight"
+        self.b1, self.b2 = pre + "0.bias", pre + "2.bias"
+        self.steps = steps
+        if diffkd:
+            self.wconv, self.wconv_h, self.g1, self.g2 = ws.dk_wconv, None, ws.dk_g1, ws.dk_g2
+        else:
+            self.wconv, self.wconv_h, self.g1, self.g2 = ws.wconv, ws.wconv_h, ws.g1, ws.g2
+        self.w1f, self.w1b, self.w2f, self.w2b = self.wconv.unbind(0)
+
+
+def _denoise_forward(P, dn: _Deno, zn, T, dev):
+    """x <- x - net(x)/steps, `steps` times over rows zn; returns (ctx, x_steps)."""
+    n, Lt = zn.shape
+    ds = dn.steps
+    if _deno_fused(Lt):
+        X = torch.empty(ds, n, Lt, device=dev, dtype=torch.bfloat16)
+        A = torch.empty(ds, n, Lt, device=dev, dtype=torch.bfloat16)
+        out = _empty(n, Lt, dev=dev)
+        with K.span("denoise_chain_fwd"):
+            K.denoise_chain_fwd(zn, P[dn.w1], P[dn.b1], P[dn.w2], P[dn.b2], X, A, out, T, ds)
+        return dict(fused=True, X=X, A=A), out
+    K.convw_prep(P[dn.w1], fwd=dn.w1f, bwd=dn.w1b)
+    K.convw_prep(P[dn.w2], fwd=dn.w2f, bwd=dn.w2b)
+    if K.get_math() == "bf16" and dn.wconv_h is not None:
+        K.cast_bf16(dn.wconv, dn.wconv_h)
+    xs = [zn]
+    acts = []
+    for _ in range(ds):
+        a = _empty(n, Lt, dev=dev)
+        K.conv3(xs[-1], dn.w1f, P[dn.b1], a, T, epi=_lib.EPI_RELU, tag="deno_conv")
+        xn = _empty(n, Lt, dev=dev)
+        K.conv3(a, dn.w2f, P[dn.b2], xn, T, R=xs[-1], rscale=-1.0 / ds, tag="deno_conv")
+        acts.append(a)
+        xs.append(xn)
+    return dict(xs=xs, acts=acts), xs[-1]
+
+
+def _denoise_backward(P, G, dn: _Deno, c, g, T, dev):
+    """g = d/d x_steps -> returns d/d x_0; parameter gradients into G (weight-gradient stream)."""
+    n, Lt = g.shape
+    ds = dn.steps
+    if not c.get("fused"):
+        return _denoise_backward_unfused(P, G, dn, c, g, T, dev)
+    X, A = c["X"], c["A"]
+    GV = torch.empty(ds, n, Lt, device=dev, dtype=torch.bfloat16)
+    DA = torch.empty(ds, n, Lt, device=dev, dtype=torch.bfloat16)
+    gin = _empty(n, Lt, dev=dev)
+    with K.span("denoise_chain_bwd"):
+        K.denoise_chain_bwd(g, A, P[dn.w1], P[dn.w2], GV, DA, gin, T, ds)
+
+    def wgrads():
+        # one row-parallel launch per conv over all ds steps (the stacked saves keep whole utterances)
+        K.fill(dn.g1, 0.0)
+        K.fill(dn.g2, 0.0)
+        K.wgrad_bf16_conv(DA.view(ds * n, Lt), X.view(ds * n, Lt), dn.g1, T, db=G[dn.b1])
+        K.wgrad_bf16_conv(GV.view(ds * n, Lt), A.view(ds * n, Lt), dn.g2, T, alpha=-1.0 / ds, db=G[dn.b2])
+        K.convw_grad(dn.g1, G[dn.w1])
+        K.convw_grad(dn.g2, G[dn.w2])
+    WGRAD.run(wgrads, X, A, GV, DA)
+    return gin
+
+
 def _adapt_denoise_forward(cfg, P, ws, x, T, seed, eps, dev):
     """NoiseAdapter then the 9-step SimpleDenoiser over rows x; returns (ctx, z_deno)."""
     n, Lt = x.shape
@@ -228,58 +300,15 @@ def _adapt_denoise_forward(cfg, P, ws, x, T, seed, eps, dev):
     gamma = _empty(n, dev=dev)
     K.adapter_fwd(x, hA, P["adapter.gamma_head.2.weight"].view(-1), P["adapter.gamma_head.2.bias"], eps, zn, gamma,
                   seed, SALT_HEADS)
-    ds = cfg.denoiser_steps
-    if _deno_fused(Lt):
-        X = torch.empty(ds, n, Lt, device=dev, dtype=torch.bfloat16)
-        A = torch.empty(ds, n, Lt, device=dev, dtype=torch.bfloat16)
-        out = _empty(n, Lt, dev=dev)
-        with K.span("denoise_chain_fwd"):
-            K.denoise_chain_fwd(zn, P["denoiser.net.0.weight"], P["denoiser.net.0.bias"], P["denoiser.net.2.weight"],
-                                P["denoiser.net.2.bias"], X, A, out, T, ds)
-        return dict(x=x, hA=hA, gamma=gamma, eps=eps, fused=True, X=X, A=A), out
-    # SimpleDenoiser: x <- x - net(x)/steps
-    K.convw_prep(P["denoiser.net.0.weight"], fwd=ws.w1f, bwd=ws.w1b)
-    K.convw_prep(P["denoiser.net.2.weight"], fwd=ws.w2f, bwd=ws.w2b)
-    if K.get_math() == "bf16" and ws.wconv_h is not None:
-        K.cast_bf16(ws.wconv, ws.wconv_h)
-    xs = [zn]
-    acts = []
-    for _ in range(ds):
-        a = _empty(n, Lt, dev=dev)
-        K.conv3(xs[-1], ws.w1f, P["denoiser.net.0.bias"], a, T, epi=_lib.EPI_RELU, tag="deno_conv")
-        xn = _empty(n, Lt, dev=dev)
-        K.conv3(a, ws.w2f, P["denoiser.net.2.bias"], xn, T, R=xs[-1], rscale=-1.0 / ds, tag="deno_conv")
-        acts.append(a)
-        xs.append(xn)
-    return dict(x=x, hA=hA, gamma=gamma, eps=eps, xs=xs, acts=acts), xs[-1]
+    dctx, out = _denoise_forward(P, _Deno(ws, "denoiser.net.", cfg.denoiser_steps), zn, T, dev)
+    dctx.update(x=x, hA=hA, gamma=gamma, eps=eps)
+    return dctx, out
 
 
 def _adapt_denoise_backward(cfg, P, G, ws, c, g, T, seed, dev):
     """g = d/d z_deno -> returns d/d (adapter input)."""
     n, Lt = g.shape
-    ds = cfg.denoiser_steps
-    if c.get("fused"):
-        W1, W2 = P["denoiser.net.0.weight"], P["denoiser.net.2.weight"]
-        X, A = c["X"], c["A"]
-        GV = torch.empty(ds, n, Lt, device=dev, dtype=torch.bfloat16)
-        DA = torch.empty(ds, n, Lt, device=dev, dtype=torch.bfloat16)
-        gin = _empty(n, Lt, dev=dev)
-        with K.span("denoise_chain_bwd"):
-            K.denoise_chain_bwd(g, A, W1, W2, GV, DA, gin, T, ds)
-
-        def wgrads():
-            # one row-parallel launch per conv over all ds steps (the stacked saves keep whole utterances)
-            K.fill(ws.g1, 0.0)
-            K.fill(ws.g2, 0.0)
-            K.wgrad_bf16_conv(DA.view(ds * n, Lt), X.view(ds * n, Lt), ws.g1, T, db=G["denoiser.net.0.bias"])
-            K.wgrad_bf16_conv(GV.view(ds * n, Lt), A.view(ds * n, Lt), ws.g2, T, alpha=-1.0 / ds,
-                              db=G["denoiser.net.2.bias"])
-            K.convw_grad(ws.g1, G["denoiser.net.0.weight"])
-            K.convw_grad(ws.g2, G["denoiser.net.2.weight"])
-        WGRAD.run(wgrads, X, A, GV, DA)
-        g = gin
-    else:
-        g = _denoise_backward_unfused(cfg, P, G, ws, c, g, T, dev)
+    g = _denoise_backward(P, G, _Deno(ws, "denoiser.net.", cfg.denoiser_steps), c, g, T, dev)
     x, hA = c["x"], c["hA"]
     dx_direct = _empty(n, Lt, dev=dev)
     dh = _empty(n, Lt, dev=dev)
@@ -293,26 +322,25 @@ def _adapt_denoise_backward(cfg, P, G, ws, c, g, T, seed, dev):
     return dx
 
 
-def _denoise_backward_unfused(cfg, P, G, ws, c, g, T, dev):
+def _denoise_backward_unfused(P, G, dn: _Deno, c, g, T, dev):
     """Per-step conv GEMMs of the denoiser backward (f32 parity mode); returns d/d(denoiser input)."""
     n, Lt = g.shape
-    ds = cfg.denoiser_steps
+    ds = dn.steps
     xs, acts = c["xs"], c["acts"]
-    K.fill(ws.g1, 0.0)
-    K.fill(ws.g2, 0.0)
+    # the accumulators are zeroed on the weight-gradient stream, where they are accumulated and read
+    WGRAD.run(lambda: (K.fill(dn.g1, 0.0), K.fill(dn.g2, 0.0)))
     for i in range(ds - 1, -1, -1):
         # x_{i+1} = x_i - (1/ds)(conv(a_i, W2) + b2)
-        WGRAD.run(lambda g=g, i=i: K.conv3_dw(g, acts[i], ws.g2, T, alpha=-1.0 / ds, db=G["denoiser.net.2.bias"]),
-                  g, acts[i])
+        WGRAD.run(lambda g=g, i=i: K.conv3_dw(g, acts[i], dn.g2, T, alpha=-1.0 / ds, db=G[dn.b2]), g, acts[i])
         da = _empty(n, Lt, dev=dev)
-        K.conv3(g, ws.w2b, None, da, T, epi=_lib.EPI_DRELU, aux=acts[i], alpha=-1.0 / ds, tag="deno_conv")
-        WGRAD.run(lambda da=da, i=i: K.conv3_dw(da, xs[i], ws.g1, T, db=G["denoiser.net.0.bias"]), da, xs[i])
+        K.conv3(g, dn.w2b, None, da, T, epi=_lib.EPI_DRELU, aux=acts[i], alpha=-1.0 / ds, tag="deno_conv")
+        WGRAD.run(lambda da=da, i=i: K.conv3_dw(da, xs[i], dn.g1, T, db=G[dn.b1]), da, xs[i])
         gi = _empty(n, Lt, dev=dev)
-        K.conv3(da, ws.w1b, None, gi, T, R=g, rscale=1.0, tag="deno_conv")
+        K.conv3(da, dn.w1b, None, gi, T, R=g, rscale=1.0, tag="deno_conv")
         g = gi
         del da
-    # ws.g1 / ws.g2 are produced on the side stream: re-lay them out there too
-    WGRAD.run(lambda: (K.convw_grad(ws.g1, G["denoiser.net.0.weight"]), K.convw_grad(ws.g2, G["denoiser.net.2.weight"])))
+    # the accumulators are produced on the side stream: re-lay them out there too
+    WGRAD.run(lambda: (K.convw_grad(dn.g1, G[dn.w1]), K.convw_grad(dn.g2, G[dn.w2])))
     return g
 
 
@@ -320,7 +348,46 @@ def _denoise_backward_unfused(cfg, P, G, ws, c, g, T, dev):
 # the version graph
 # ------------------------------------------------------------------------------------------------
 
-def heads_forward(cfg: Ver5Config, P, s_feats, t_feats, T, ws: HeadsWorkspace, acc, *, seed, eps=None, save=True):
+def _diffkd_forward(cfg, P, Pfix, s_feats, t_feats, T, ws, acc, dev):
+    """DiffKDModule over every layer pair at once (asr_train_diffm.py:364-394), the layer mean of
+    :795-800 folded into the MSE scales: z_t = encoder(t) (no gradient reaches the encoder, :382),
+    ae = MSE(decoder(z_t), t), x = denoise^S(proj(s)), distill = MSE(x, z_t); acc += (ae + distill) / L."""
+    n = s_feats.shape[0]
+    Lt, Ct, Cs = cfg.latent, cfg.d_teacher, cfg.d_student
+    rows = n // cfg.n_layers
+    zt = _empty(n, Lt, dev=dev)
+    K.linear(t_feats, Pfix["diffkd.encoder.weight"].view(Lt, Ct), Pfix["diffkd.encoder.bias"], zt)
+    drec = _empty(n, Ct, dev=dev)
+    inv_rec = 1.0 / (rows * Ct * cfg.n_layers)
+    K.linear(zt, P["diffkd.decoder.weight"].view(Ct, Lt), P["diffkd.decoder.bias"], drec, R=t_feats,
+             rscale=2.0 * inv_rec, mse=(acc, inv_rec))
+    zs = _empty(n, Lt, dev=dev)
+    K.linear(s_feats, P["diffkd.proj.weight"].view(Lt, Cs), P["diffkd.proj.bias"], zs)
+    dn = _Deno(ws, "diffkd.denoiser.", cfg.diffkd_steps, diffkd=True)
+    dctx, zd = _denoise_forward(P, dn, zs, T, dev)
+    inv = 1.0 / (rows * Lt * cfg.n_layers)
+    gzd = _empty(n, Lt, dev=dev)
+    K.mse(zd, zt, acc, inv, grad=gzd, gscale=2.0 * inv)
+    return dict(zt=zt, drec=drec, dctx=dctx, gzd=gzd)
+
+
+def _diffkd_backward(cfg, P, G, c, s_feats, T, ws, ds_feats, dev):
+    """Backward of _diffkd_forward: decoder / proj / denoiser gradients into G, d/d(student layer
+    outputs) ADDED into ds_feats."""
+    Lt, Cs = cfg.latent, cfg.d_student
+    Ct = cfg.d_teacher
+    drec, zt = c["drec"], c["zt"]
+    WGRAD.run(lambda: K.linear_dw(drec, zt, G["diffkd.decoder.weight"].view(Ct, Lt), db=G["diffkd.decoder.bias"]),
+              drec, zt)
+    dn = _Deno(ws, "diffkd.denoiser.", cfg.diffkd_steps, diffkd=True)
+    dzs = _denoise_backward(P, G, dn, c["dctx"], c["gzd"], T, dev)
+    WGRAD.run(lambda: K.linear_dw(dzs, s_feats, G["diffkd.proj.weight"].view(Lt, Cs), db=G["diffkd.proj.bias"]),
+              dzs, s_feats)
+    K.linear_dx(dzs, P["diffkd.proj.weight"].view(Lt, Cs), ds_feats, R=ds_feats, rscale=1.0)
+
+
+def heads_forward(cfg: Ver5Config, P, s_feats, t_feats, T, ws: HeadsWorkspace, acc, *, seed, eps=None, save=True,
+                  Pfix=None, acc_diffkd=None):
     """s_feats (n, d_student) and t_feats (n, d_teacher) stacked student/teacher layer outputs
     (n = layers*B*T').  acc: device (5,) f32 accumulators [recon, kd_pre, fm_pre, kd_post, fm_post]
     (added to; the slots a version does not use stay untouched).  Returns ctx for backward."""
@@ -356,6 +423,8 @@ def heads_forward(cfg: Ver5Config, P, s_feats, t_feats, T, ws: HeadsWorkspace, a
         else:
             pre = "fm_latent.fm." if v == 5 else "fm_latent_2.fm."
             ctx["fm_post"], _ = _fm_forward(cfg, P, pre, ws, zd, zt, acc[FM_POST:FM_POST + 1], inv_lat, False, dev)
+    if cfg.use_diffkd:
+        ctx["diffkd"] = _diffkd_forward(cfg, P, Pfix, s_feats, t_feats, T, ws, acc_diffkd, dev)
     return ctx if save else None
 
 
@@ -399,3 +468,5 @@ def heads_backward(cfg: Ver5Config, P, G, ctx, ws: HeadsWorkspace, ds_feats, *, 
     K.linear_dx(drec, P["tae.dec.weight"].view(Ct, Lt), dzt)
     WGRAD.run(lambda: K.linear_dw(dzt, ctx["t_feats"], G["tae.enc.weight"].view(Lt, Ct), db=G["tae.enc.bias"]), dzt,
               ctx["t_feats"])
+    if "diffkd" in ctx:
+        _diffkd_backward(cfg, P, G, ctx.pop("diffkd"), ctx["s_feats"], T, ws, ds_feats, dev)

@@ -66,6 +66,8 @@ class StepConfig:
     xscaling: bool = True
     version: int = 5                    # --model_version verN (asr_train_diffm.py:1636-1641)
     kd_loss_type: str = "mse"
+    use_diffkd: bool = False            # --use_diffkd: DiffKDModule on every layer pair (:795-800)
+    diffkd_steps: int = 9               # --diffkd_steps (diffkd_cfg["diffusion_steps"], :1830-1836)
     bn_momentum: float = 0.1
     ln_eps: float = 1e-5
     bn_eps: float = 1e-5
@@ -210,6 +212,12 @@ def init_heads(cfg: StepConfig, seed: int) -> dict:
         w, b = _lin(g, L, L)
         p[fm + "shape_transformation_function.weight"] = w
         p[fm + "shape_transformation_function.bias"] = b
+    # DiffKDModule (asr_train_diffm.py:326-394): its own linear autoencoder, projector and denoiser
+    conv("diffkd.encoder", L, Ct, 1)
+    conv("diffkd.decoder", Ct, L, 1)
+    conv("diffkd.proj", L, Cs, 1)
+    conv("diffkd.denoiser.0", L, L, 3)
+    conv("diffkd.denoiser.2", L, L, 3)
     return p
 
 
@@ -472,6 +480,20 @@ def denoiser(z, p, steps):
     return x
 
 
+def diffkd(s_btd, t_btd, p, steps):
+    """DiffKDModule.forward (asr_train_diffm.py:364-394): teacher latent z = encoder(t) DETACHED (the
+    encoder never receives a gradient), recon MSE(decoder(z), t), student latent proj(s) denoised by
+    `steps` Euler steps x -= denoiser(x) / steps, distill MSE(denoised, z); returns their sum."""
+    s = s_btd.permute(0, 2, 1)
+    t = t_btd.permute(0, 2, 1)
+    z_t = _c1(t, p, "diffkd.encoder").detach()
+    ae = F.mse_loss(_c1(z_t, p, "diffkd.decoder"), t)
+    x = _c1(s, p, "diffkd.proj")
+    for _ in range(steps):
+        x = x - _c1(F.relu(_c1(x, p, "diffkd.denoiser.0", 1)), p, "diffkd.denoiser.2", 1) / steps
+    return ae + F.mse_loss(x, z_t)
+
+
 def fm_latent(s_bct, t_bct, p, steps, prefix="fm_latent.fm."):
     """FMLatent.forward -> FlowMatchingModule.forward (training, rectified, mlp, linear)."""
     s_f = s_bct.transpose(1, 2)
@@ -599,22 +621,32 @@ def ver5_step(p, wav, wav_len, targets, target_len, cfg: StepConfig, eps, spec_m
                 terms[k] = terms[k] + o[k]
         recon_sum = recon_sum + r
         fm_sum = fm_sum + f
-    # training_step (asr_train_diffm.py:813-821): ctc + kd_alpha * logit_kd + recon + kd/fm pre/post
-    total = ctc + cfg.kd_alpha * kl + recon_sum + fm_sum
-    return {"loss": total, "ctc": ctc, "kl": kl, "recon": recon_sum, "fm": fm_sum, "terms": terms,
+    # (optional) DiffKD: mean over the layer pairs (asr_train_diffm.py:795-800)
+    dkd = torch.zeros((), dtype=log_probs.dtype)
+    if cfg.use_diffkd:
+        for s, t in zip(s_feats, t_feats):
+            dkd = dkd + diffkd(s, t, p, cfg.diffkd_steps)
+        dkd = dkd / max(1, len(s_feats))
+    # training_step (asr_train_diffm.py:803-811): ctc + kd_alpha * logit_kd + recon + kd/fm pre/post + diffkd
+    total = ctc + cfg.kd_alpha * kl + recon_sum + fm_sum + dkd
+    return {"loss": total, "ctc": ctc, "kl": kl, "recon": recon_sum, "fm": fm_sum + dkd, "diffkd": dkd,
+            "terms": terms,
             "log_probs": log_probs,
             "enc_len": enc_len, "mel": mel, "mel_len": mel_len, "s_feats": s_feats, "t_feats": t_feats,
             "bn_state": bn_state}
 
 
-def trainable_names(p: dict, version: int = 5) -> list:
+def trainable_names(p: dict, version: int = 5, use_diffkd: bool = False) -> list:
     """Names of the parameters the step trains (teacher frozen; buffers/running stats excluded;
-    fm_latent_2 is used by versions 6 and 7 only, and otherwise receives no gradient)."""
+    fm_latent_2 is used by versions 6 and 7 only, and otherwise receives no gradient; the DiffKD
+    module only with use_diffkd, and its encoder never: its output is detached before every use)."""
     out = []
     for k, v in p.items():
         if k.startswith("teacher.") or k.startswith("preprocessor.") or "running_" in k or "num_batches" in k:
             continue
         if k.startswith("fm_latent_2.") and version not in (6, 7):
+            continue
+        if k.startswith("diffkd.") and (not use_diffkd or k.startswith("diffkd.encoder.")):
             continue
         out.append(k)
     return out

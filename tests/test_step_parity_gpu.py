@@ -49,12 +49,14 @@ def _oracle_params(cfg, eng):
     ocfg = O.StepConfig(n_layers=cfg.n_layers, subsampling=cfg.subsampling, subsampling_factor=cfg.subsampling_factor,
                         subsampling_conv_channels=cfg.subsampling_conv_channels,
                         causal_downsampling=cfg.causal_downsampling, version=cfg.version,
-                        kd_loss_type=cfg.kd_loss_type)
+                        kd_loss_type=cfg.kd_loss_type, use_diffkd=cfg.use_diffkd, diffkd_steps=cfg.diffkd_steps,
+                        vocab=cfg.vocab)
     p = {}
     p.update(O.frontend_buffers(ocfg))
     p.update(O.frontend_buffers(ocfg, "teacher.preprocessor.featurizer."))
     p.update(eng.student.state_dict())
     p.update(eng.teacher.state_dict())
+    p.update(eng.fixed.state_dict())
     for name, _ in eng.bn.specs:
         p[name] = eng.bn.P[name].detach().cpu().clone()
     return ocfg, p
@@ -97,8 +99,12 @@ DW8C = dict(subsampling="dw_striding", subsampling_factor=8, subsampling_conv_ch
     (2, 2, 19200, [19200, 16123], 12, [12, 7], dict(version=6)),
     (2, 2, 19200, [19200, 16123], 12, [12, 7], dict(version=7)),
     (2, 2, 19200, [19200, 16123], 12, [12, 7], dict(version=8, kd_loss_type="l1")),
+    # --use_diffkd on top of ver5 (asr_train_diffm.py:326-394, 795-800)
+    (2, 2, 19200, [19200, 16123], 12, [12, 7], dict(use_diffkd=True)),
+    # a V = 1024 BPE vocabulary (1025 decoder classes; conformer_ctc_bpe.yaml:87, SURVEY §8 V sensitivity)
+    (2, 2, 19200, [19200, 16123], 12, [12, 7], dict(vocab=1024)),
 ], ids=["2L-1.2s", "16L-1s", "16L-16s", "16L-16s-overlapped", "2L-1.2s-dw4", "2L-1.2s-dw8-causal", "2L-1.2s-ver6", "2L-1.2s-ver7",
-        "2L-1.2s-ver8-l1"])
+        "2L-1.2s-ver8-l1", "2L-1.2s-diffkd", "2L-1.2s-V1024"])
 def test_ver5_step_matches_oracle(n_layers, B, N, lens, U, tl, sub):
     from kdfm.config import sub_dims
     cfg, eng, wav, wl, tg, tgl, g = _build(n_layers, B, N, lens, U, tl, sub=sub)
@@ -119,7 +125,7 @@ def test_ver5_step_matches_oracle(n_layers, B, N, lens, U, tl, sub):
     # weight gradient sums 64k cancelling terms after the 16-layer backward).
     eps_o = eps_rows.view(n_layers, B, T, cfg.latent).permute(0, 1, 3, 2)
     p = {k: (v.double() if v.is_floating_point() else v) for k, v in p32.items()}
-    names = O.trainable_names(p, cfg.version)
+    names = O.trainable_names(p, cfg.version, cfg.use_diffkd)
     for k in names:
         p[k] = p[k].clone().requires_grad_(True)
         p32[k] = p32[k].clone().requires_grad_(True)

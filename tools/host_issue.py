@@ -53,3 +53,22 @@ for _ in range(steps):
     del ctx
     torch.cuda.synchronize()
 print(f"forward: enqueue {1e3 * min(fe):.2f} ms, enqueue+drain {1e3 * min(ff):.2f} ms", flush=True)
+# the same step replayed from a recorded step plan (kdfm/plan.py): host enqueue vs enqueue + drain
+plan = eng.make_plan(wav, wl, tg, tl)
+torch.cuda.synchronize()
+pe, pf = [], []
+for _ in range(steps):
+    t0 = time.perf_counter()
+    plan.replay()
+    t1 = time.perf_counter()
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    pe.append(t1 - t0)
+    pf.append(t2 - t0)
+print(f"step plan ({len(plan)} ops): enqueue {1e3 * min(pe):.2f} ms (median {1e3 * sorted(pe)[len(pe) // 2]:.2f}), "
+      f"enqueue+drain {1e3 * min(pf):.2f} ms", flush=True)
+t0 = time.perf_counter()
+for _ in range(steps):
+    plan.replay()
+torch.cuda.synchronize()
+print(f"step plan back-to-back {1e3 * (time.perf_counter() - t0) / steps:.2f} ms/step", flush=True)
