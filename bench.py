@@ -74,7 +74,8 @@ def parse():
     ap.add_argument("--math", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0,
-                    help="host threads for the CPU baseline (default: os.cpu_count(), BASELINE.md)")
+                    help="host threads for the CPU baseline (default: every core this process may run on, "
+                         "len(os.sched_getaffinity(0)); os.cpu_count() is reported beside it)")
     ap.add_argument("--no-f32-sensitivity", action="store_true",
                     help="skip the --math f32 sensitivity measurement (the reference trains fp32)")
     ap.add_argument("--deterministic", action="store_true",
@@ -88,19 +89,21 @@ def parse():
     return ap.parse_args()
 
 
-def f32_sensitivity(dev, samples, steps=3):
-    """utt/s of the same step with exact-f32 MFMA arithmetic (the reference trains in fp32,
-    asr_train_diffm.py:1762-1769): a separate engine, 1 warm-up + `steps` timed steps."""
+def sensitivity(dev, samples, steps=3, **overrides):
+    """utt/s of the same step with one configuration change (1 warm-up + `steps` timed eager steps on a
+    separate engine): math="f32" -- exact-f32 MFMA arithmetic, the reference trains fp32
+    (asr_train_diffm.py:1762-1769); vocab=1024 -- a 1024-token BPE tokenizer, 1025 decoder classes
+    (conformer_ctc_bpe.yaml:87, SURVEY.md §8 V sensitivity)."""
     from dataclasses import replace
 
     from kdfm import kernels as K
     from kdfm.config import DEFAULT
     from kdfm.engine import Ver5Engine, synthetic_batch
-    cfg = replace(DEFAULT, math="f32")
+    cfg = replace(DEFAULT, **overrides)
     eng = Ver5Engine(cfg, dev)
     eng.set_seed(1000)
     wav, wl, tg, tl = synthetic_batch(cfg, B_PER_GPU, samples, U_TOKENS, dev, seed=1234)
-    with K.mode("f32"):
+    with K.mode(cfg.math):
         eng.train_step(wav, wl, tg, tl)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -108,16 +111,32 @@ def f32_sensitivity(dev, samples, steps=3):
             eng.train_step(wav, wl, tg, tl)
         torch.cuda.synchronize()
     el = time.perf_counter() - t0
+    del eng
+    torch.cuda.empty_cache()
     return {"value": round(B_PER_GPU * steps / el, 3), "unit": "utterances/sec", "ms_per_step": round(1e3 * el / steps, 3),
-            "dtype": "f32", "steps": steps, "note": "same workload, exact f32 MFMA (v_mfma_f32_16x16x4_f32) instead of "
-                                                  "bf16 operands: sensitivity only, not the headline value"}
+            "steps": steps, "issue": "eager", "config_change": overrides,
+            "note": "same workload with this one change; sensitivity only, not the headline value"}
 
 
-def cpu_baseline(threads: int, samples: int, batches=(2, 32), steps: int = 5):
+def _cgroup_cpu_max():
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            return fh.read().strip()
+    except OSError:
+        return None
+
+
+def _progress(msg):
+    # the GPU pool's watchdog kills a command that prints nothing for 3 minutes: long CPU phases report
+    print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
+def cpu_baseline(threads: int, samples: int, batches=(2, 32), steps: int = 5, budget_s: float = 25.0):
     """Oracle (pure-PyTorch CPU restatement of the same step, fp32: frontend x2, teacher + student
     encoders, decoders, CTC, logit KD, ver5 heads, autograd backward) on the host cores, per
     BASELINE.md: B=2 (config 1) and B=32 (the bench batch) utterances of the same 16 s shape,
-    1 warm-up + `steps` timed forward+backward steps each, median.  `value` is the B=32 rate."""
+    1 warm-up + up to `steps` timed forward+backward steps each (fewer once a batch size has used
+    `budget_s` seconds, at least 2), median.  `value` is the B=32 rate."""
     import platform
     import statistics
     from oracle import ver5 as O
@@ -137,12 +156,17 @@ def cpu_baseline(threads: int, samples: int, batches=(2, 32), steps: int = 5):
         tl = torch.full((Bc,), U_TOKENS, dtype=torch.int64)
         eps = torch.randn(ocfg.n_layers, Bc, ocfg.latent, T, generator=g)
         times = []
+        t_start = time.perf_counter()
         for i in range(steps + 1):
             t0 = time.perf_counter()
             out = O.ver5_step(p, wav, wl, tg, tl, ocfg, eps)
             torch.autograd.grad(out["loss"], [p[k] for k in names], allow_unused=True)
             times.append(time.perf_counter() - t0)
             del out
+            _progress(f"cpu_baseline threads={threads} B={Bc} step {i} ({'warm-up' if i == 0 else 'timed'}): "
+                      f"{times[-1]:.2f} s")
+            if i >= 2 and time.perf_counter() - t_start > budget_s:
+                break
         med = statistics.median(times[1:])
         res[Bc] = {"utt_per_s": round(Bc / med, 4), "s_per_step_median": round(med, 3),
                    "s_per_step": [round(t, 3) for t in times[1:]]}
@@ -153,10 +177,12 @@ def cpu_baseline(threads: int, samples: int, batches=(2, 32), steps: int = 5):
     except OSError:
         cpu = platform.processor() or cpu
     big = max(batches)
+    nt = len(res[big]["s_per_step"])
     return {"value": res[big]["utt_per_s"], "unit": "utterances/sec", "cores": threads, "kind": "port",
-            "cpu_model": cpu, "host_cpus": os.cpu_count(), "by_batch": {str(b): v for b, v in res.items()},
+            "cpu_model": cpu, "host_cpus": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)),
+            "by_batch": {str(b): v for b, v in res.items()},
             "sample": f"oracle/ver5.py fp32 forward+backward of the same step, B={list(batches)} x "
-                      f"{samples / 16000:.1f} s utterances, median of {steps} steps after 1 warm-up, "
+                      f"{samples / 16000:.1f} s utterances, median of {nt} timed steps (B={big}) after 1 warm-up, "
                       f"torch.set_num_threads({threads}); value = B={big}"}
 
 
@@ -320,15 +346,23 @@ def main():
         fe = rate(tsum.get("frontend", empty))
         dw = rate(tsum.get("dwconv", empty))
         cpu = None
-        if not args.no_cpu_baseline:
-            threads = args.cpu_threads or os.cpu_count()
+        _progress(f"timed {args.steps} steps: {1e3 * elapsed / args.steps:.3f} ms/step ({utt:.1f} utt/s)")
+        if not args.no_cpu_baseline and world == 1:
+            # every core this process may run on (the GPU box's share of the host; os.cpu_count() is the
+            # whole machine and is reported beside it)
+            threads = args.cpu_threads or len(os.sched_getaffinity(0))
             cpu = cpu_baseline(threads, args.samples)
+            cpu["cgroup_cpu_max"] = _cgroup_cpu_max()
             if threads != 16:   # the box's per-GPU CPU share, kept beside the all-cores figure
                 c16 = cpu_baseline(16, args.samples, batches=(32,), steps=3)
                 cpu["at_16_threads"] = {"value": c16["value"], "cores": 16, "sample": c16["sample"]}
-        f32 = None
+        f32 = v1024 = None
         if not args.no_f32_sensitivity and cfg.math == "bf16" and world == 1:
-            f32 = f32_sensitivity(dev, args.samples)
+            _progress("f32 sensitivity")
+            f32 = sensitivity(dev, args.samples, math="f32")
+            f32["dtype"] = "f32"
+            _progress("V=1024 sensitivity")
+            v1024 = sensitivity(dev, args.samples, vocab=1024)
         line = {
             "metric": "utterances/sec (FM-distill train step, Conformer-CTC-small) at 1/2/4/8 MI355X",
             "value": round(utt, 3),
@@ -364,6 +398,7 @@ def main():
                            "bytes": "read g + write y, 4 B x rows x d per launch"},
             "cpu_baseline": cpu,
             "f32_sensitivity": f32,
+            "vocab_1024_sensitivity": v1024,
             "losses_last_step": [round(x, 5) for x in losses],
         }
         print(json.dumps(line))

@@ -182,11 +182,13 @@ int kdfm_wgrad_bf16_conv(const uint16_t* dY, const uint16_t* X, float* dW, int64
 /* Fused relative-position attention backward (bf16 MFMA; NeMo RelPositionMultiHeadAttention,
  * Appendix A.7): from dO (rows, d), the forward's q+u / q+v rows, the fused q|k|v rows (ld 3d), the
  * projected positions pos (2T-1, d), the forward output O (rows, d) and the forward's per-row
- * log-sum-exp lse (B, H, T) (kdfm_relpos_attn_fwd) it recomputes P = exp(S - lse) tile by tile and writes
+ * log-sum-exp lse (B, H, T) with its bf16 unnormalised probabilities p_tilde (B, H, T, T) and per-64-key-block
+ * running maxima m_blk (B, H, T, ceil(T/64)) (kdfm_relpos_attn_fwd), it forms P = p_tilde exp(m_blk - lse)
+ * for dK / dV / dpos (DQ recomputes P = exp(S - lse) tile by tile and reads neither) and writes
  *   dqu = dS K, dqv_i = sum_j dS[i][j] pos[T-1-i+j]  (rows, d),  dK, dV into dqkv[:, d:] and [:, 2d:],
  *   dpos[r] = sum_{b,i} dS[i][r-T+1+i] qv_i  (2T-1, d, overwritten)
  * with dS = P (dP - r) scale, r_i = dO_i . O_i (= rowsum(dP P)) and dP the dropout-masked dO V^T (counter-RNG mask of the
- * forward).  No T x T tensor in HBM at all; deterministic (ordered chunk fold, no atomics).  Head
+ * forward).  The one T x T operand is the forward's bf16 p_tilde; deterministic (ordered chunk fold, no atomics).  Head
  * dim d/H <= 48.  ws: kdfm_relpos_attn_bwd_ws floats. */
 int64_t kdfm_relpos_attn_bwd_ws(int64_t B, int64_t H, int64_t T, int64_t d);
 /* The same backward issued in parts (a caller may put them on different streams): ROWDOT writes
@@ -195,13 +197,13 @@ int64_t kdfm_relpos_attn_bwd_ws(int64_t B, int64_t H, int64_t T, int64_t d);
 enum { KDFM_ATTN_BWD_ROWDOT = 1, KDFM_ATTN_BWD_DQ = 2, KDFM_ATTN_BWD_DKV = 4, KDFM_ATTN_BWD_DPOS = 8,
        KDFM_ATTN_BWD_ALL = 15 };
 int kdfm_relpos_attn_bwd_parts(const float* dO, const float* O, const float* qu, const float* qv, const float* qkv,
-                               const float* pos, const float* lse, const int64_t* lengths, float* dqu, float* dqv,
-                               float* dqkv, float* dpos, float* ws, int64_t ws_len, int64_t B, int64_t H, int64_t T,
+                               const float* pos, const float* lse, const uint16_t* p_tilde, const float* m_blk,
+                               const int64_t* lengths, float* dqu, float* dqv, float* dqkv, float* dpos, float* ws, int64_t ws_len, int64_t B, int64_t H, int64_t T,
                                int64_t d, float scale, float dropout_p, const uint64_t* seed, uint64_t rng_stream,
                                int32_t parts, void* stream);
 int kdfm_relpos_attn_bwd(const float* dO, const float* O, const float* qu, const float* qv, const float* qkv,
-                         const float* pos, const float* lse, const int64_t* lengths, float* dqu, float* dqv,
-                         float* dqkv, float* dpos,
+                         const float* pos, const float* lse, const uint16_t* p_tilde, const float* m_blk,
+                         const int64_t* lengths, float* dqu, float* dqv, float* dqkv, float* dpos,
                          float* ws, int64_t ws_len, int64_t B, int64_t H, int64_t T, int64_t d, float scale,
                          float dropout_p, const uint64_t* seed, uint64_t rng_stream, void* stream);
 
@@ -507,9 +509,13 @@ int kdfm_relpos_table(float* pe, int64_t T, int64_t d, void* stream);
  * qkv: (B*T, 3d) (K at +d, V at +2d); pos: (2T-1, d) projected positions.  P / Pdrop (B,H,T,T) are
  * written when non-null (the per-op backward's operands; two passes over the keys); otherwise one
  * online-softmax pass, and lse (B,H,T) = per-row log-sum-exp of the scaled scores when non-null
- * (kdfm_relpos_attn_bwd's operand; 3e38 for rows without a valid key).  dk = d/H <= 48. */
+ * (kdfm_relpos_attn_bwd's operand; 3e38 for rows without a valid key).  In the one-pass mode p_tilde
+ * (B,H,T,T) bf16 = exp(s_ij - m_i,kb) before dropout and m_blk (B,H,T,ceil(T/64)) = the running row max
+ * m_i,kb after key block kb are written when non-null (pairs with lse; entries at i or j >= length are not
+ * written and not read).  dk = d/H <= 48. */
 int kdfm_relpos_attn_fwd(const float* qu, const float* qv, const float* qkv, const float* pos,
-                         const int64_t* lengths, float* o, float* P, float* Pdrop, float* lse, int64_t B, int64_t H,
+                         const int64_t* lengths, float* o, float* P, float* Pdrop, float* lse, uint16_t* p_tilde,
+                         float* m_blk, int64_t B, int64_t H,
                          int64_t T, int64_t d, float scale, float dropout_p, const uint64_t* seed,
                          uint64_t rng_stream, void* stream);
 /* conv module: GLU over channels + pad mask; depthwise conv (k odd) with optional f64 BN stats */
@@ -595,11 +601,22 @@ int kdfm_step_advance(int64_t* step, uint64_t* seed, void* stream);
 /* ---------------- optimizer (modelPT.py:650-897, lr_scheduler.py:473-530) ------------------
  * step[0] = k, the 1-based optimizer step (Noam schedule); AdamW's bias correction counts
  * k - adam_base[0] (adam_base may be NULL = 0): the moments restarted adam_base steps into the run
- * (a resume whose optimizer state could not be restored), like a fresh torch AdamW state. */
+ * (a resume whose optimizer state could not be restored), like a fresh torch AdamW state.
+ * gstats (optional, kdfm_grad_stats' output): when gstats[1] != 0 the gradient holds a non-finite
+ * value and the update is skipped (parameters and moments unchanged; the schedule step still counts,
+ * lr_out still written).  The reference has no such check (Lightning's default); it is opt-in
+ * (Ver5Config.grad_check). */
 int kdfm_adamw_noam(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, int64_t n,
                     const int64_t* step, const int64_t* adam_base, float base_lr, float d_model,
                     float warmup_steps, float min_lr, float beta1, float beta2, float eps, float weight_decay,
-                    float grad_scale, float* lr_out, void* stream);
+                    float grad_scale, float* lr_out, const float* gstats, void* stream);
+/* out2 = [sum_i (scale g_i)^2 over the finite entries, number of non-finite entries] of the flat gradient
+ * buffer (the all-reduced sum with scale = 1/world: the global gradient norm^2 and the
+ * skip flag of kdfm_adamw_noam); fixed-order two-stage reduction (deterministic).  ws: kdfm_grad_stats_ws
+ * floats. */
+int64_t kdfm_grad_stats_ws(void);
+int kdfm_grad_stats(const float* grads, int64_t n, float scale, float* ws, int64_t ws_len, float* out2,
+                    void* stream);
 
 #ifdef __cplusplus
 }

@@ -50,7 +50,7 @@ constexpr int WS2 = (32 * LH * 4 > 2 * 16 * LW * 2) ? 32 * LH * 4 : 2 * 16 * LW 
 
 struct AbP {
   const float* dO; const float* qu; const float* qv; const float* k; const float* v; const float* pos;
-  const float* lse;
+  const float* lse; const uint16_t* pt; const float* mblk;   // lse (B,H,T); p~ (B,H,T,T) bf16; m (B,H,T,nkb)
   const int64_t* lens;
   float* dqu; float* dqv; float* rsum; float* dk; float* dv; float* dpos_part;
   int64_t B, H, T, d, dkh, ldq, ldkv;
@@ -320,39 +320,36 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AbP p) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// kernel 2: dK, dV
+// kernel 2: dK, dV  (P = p~ exp(m_ikb - lse_i) read from the forward's bf16 p~ and block maxima)
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256, 2) void attn_bwd_dkv_kernel(AbP p) {
   __shared__ __attribute__((aligned(16))) uint16_t Os[BQ * LR];     // dO block [query][c]
   __shared__ __attribute__((aligned(16))) uint16_t Qs[BQ * LR];     // Qu block [query][c]
-  __shared__ __attribute__((aligned(16))) uint16_t Qvs[BQ * LR];    // Qv block [query][c]
-  __shared__ __attribute__((aligned(16))) uint16_t Pr[PB * LR];     // Ppos band [band row][c]
-  __shared__ __attribute__((aligned(16))) float Wsc[4][WS2 / 4];    // per-wave scratch
-  __shared__ float Rs[BQ], Ls[BQ];
+  __shared__ __attribute__((aligned(16))) float Pt[BK * (BQ + 1)];  // P block^T [key][query]
+  __shared__ __attribute__((aligned(16))) uint16_t Pw[4][16 * LW];  // per wave Pd^T [key][query]
+  __shared__ __attribute__((aligned(16))) uint16_t Dw[4][16 * LW];  // per wave dS^T [key][query]
+  __shared__ float Rs[BQ], Cs[BQ];
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int T = (int)p.T, dk = (int)p.dkh;
   const Blk3 blk = xcd_block3();
   const int64_t bh = blk.y;
   const int64_t b = bh / p.H, h = bh - b * p.H;
-  const int j0 = (int)blk.x * BK;
+  const int j0 = (int)blk.x * BK;   // = kb * 64: this workgroup's keys lie in one block of the forward
+  const int kb = (int)blk.x;
+  const int nkb_all = (T + BK - 1) / BK;
   const int len = p.lens ? (int)min<int64_t>(p.lens[b], p.T) : T;
-  const int npos = 2 * T - 1;
   const int64_t hoff = h * p.dkh;
   zero_pad(Os, BQ, dk, BQ);
   zero_pad(Qs, BQ, dk, BQ);
-  zero_pad(Qvs, BQ, dk, BQ);
-  zero_pad(Pr, PB, dk, 127);
 
-  const int jk = j0 + w * 16 + (lane & 15);   // A-fragment row (key): K and V fragments
-  bf16x8 fk[2], fv[2];
+  const int jk = j0 + w * 16 + (lane & 15);   // A-fragment row (key)
+  bf16x8 fv[2];
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks) {
     const int c0 = ks * 32 + 8 * (lane >> 4);
     const bool ok = jk < len;
-    const int64_t off = (b * p.T + (ok ? jk : 0)) * p.ldkv + hoff + c0;
-    fk[ks] = frag8(p.k + off, ok ? dk - c0 : 0);
-    fv[ks] = frag8(p.v + off, ok ? dk - c0 : 0);
+    fv[ks] = frag8(p.v + (b * p.T + (ok ? jk : 0)) * p.ldkv + hoff + c0, ok ? dk - c0 : 0);
   }
   const int jb = j0 + w * 16 + 4 * (lane >> 4);   // C-layout key rows jb + r
   const uint64_t seed = (p.p_drop > 0.f) ? load_seed(p.seed) : 0ull;
@@ -360,23 +357,31 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkv_kernel(AbP p) {
   f32x4 adv[3], adk[3];
 #pragma unroll
   for (int u = 0; u < 3; ++u) { adv[u] = f32x4{0.f, 0.f, 0.f, 0.f}; adk[u] = adv[u]; }
-  float* H = Wsc[w];                                         // f32 band tile [32][LH]
-  uint16_t* PW = reinterpret_cast<uint16_t*>(Wsc[w]);        // bf16 Pd^T [key][query]  (after the band)
-  uint16_t* DW = PW + 16 * LW;                               // bf16 dS^T [key][query]
-  const int nqb = (j0 < len) ? (len + BQ - 1) / BQ : 0;      // query rows >= len have P == 0
-  // next query block's operands in registers: dO, Qu and Qv rows, the band, row sums and lse
-  float4 ndo[3], nqu[3], nqv[3], nb[6];
-  float nrs = 0.f, nls = 3.0e38f;
+  uint16_t* PW = Pw[w];
+  uint16_t* DW = Dw[w];
+  const int nqb = (j0 < len) ? (len + BQ - 1) / BQ : 0;   // query rows >= len have P == 0
+  // next query block's operands in registers: dO and Qu rows, the p~ block (row-major, coalesced along
+  // keys), the row sums and the rows' scales exp(m_ikb - lse_i)
+  float4 ndo[3], nqu[3];
+  uint16_t npb[BQ * BK / 256];
+  float nrs = 0.f, nm = 0.f, nl = 3.0e38f;
   auto fetch = [&](int qb) {
     const int i0 = qb * BQ;
     fetch_rows<3>(ndo, p.dO, p.ldq, b * p.T, i0, BQ, 0, T, hoff, dk);
     fetch_rows<3>(nqu, p.qu, p.ldq, b * p.T, i0, BQ, 0, T, hoff, dk);
-    fetch_rows<3>(nqv, p.qv, p.ldq, b * p.T, i0, BQ, 0, T, hoff, dk);
-    fetch_rows<6>(nb, p.pos, p.d, 0, T - 1 - i0 - 63 + j0, 127, 0, npos, hoff, dk);
+#pragma unroll
+    for (int it = 0; it < BQ * BK / 256; ++it) {
+      const int e = threadIdx.x + it * 256;
+      const int ii = e / BK, kk = e - ii * BK;
+      const int i = i0 + ii, j = j0 + kk;
+      npb[it] = (i < len && j < len) ? p.pt[(bh * p.T + i) * p.T + j] : (uint16_t)0;
+    }
     if (threadIdx.x < BQ) {
-      const bool ok = i0 + (int)threadIdx.x < len;
-      nrs = ok ? p.rsum[bh * p.T + i0 + threadIdx.x] : 0.f;
-      nls = ok ? p.lse[bh * p.T + i0 + threadIdx.x] : 3.0e38f;
+      const int i = i0 + (int)threadIdx.x;
+      const bool ok = i < len;
+      nrs = ok ? p.rsum[bh * p.T + i] : 0.f;
+      nm = ok ? p.mblk[(bh * p.T + i) * nkb_all + kb] : 0.f;
+      nl = ok ? p.lse[bh * p.T + i] : 3.0e38f;
     }
   };
   if (nqb > 0) fetch(0);
@@ -385,70 +390,39 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkv_kernel(AbP p) {
     __syncthreads();
     put_rows<3>(Os, nullptr, 0, ndo, BQ, dk);
     put_rows<3>(Qs, nullptr, 0, nqu, BQ, dk);
-    put_rows<3>(Qvs, nullptr, 0, nqv, BQ, dk);
-    put_rows<6>(Pr, nullptr, 0, nb, 127, dk);
-    if (threadIdx.x < BQ) { Rs[threadIdx.x] = nrs; Ls[threadIdx.x] = nls; }
-    __syncthreads();
-    // ---- S^T (16 keys x 64 queries) = K Qu^T + the band term ----
-    f32x4 ac[4];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) ac[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int it = 0; it < BQ * BK / 256; ++it) {
+      const int e = threadIdx.x + it * 256;
+      const int ii = e / BK, kk = e - ii * BK;
+      Pt[kk * (BQ + 1) + ii] = __uint_as_float((uint32_t)npb[it] << 16);
+    }
+    if (threadIdx.x < BQ) {
+      Rs[threadIdx.x] = nrs;
+      Cs[threadIdx.x] = __expf(nm - nl);
+    }
+    __syncthreads();
+    if (qb + 1 < nqb) fetch(qb + 1);
+    // dPd^T = V dO^T (16 keys x 64 queries per wave)
+    f32x4 a[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) a[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
-        const int ro = (16 * t + (lane & 15)) * LR + ks * 32 + 8 * (lane >> 4);
-        ac[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fk[ks], *reinterpret_cast<const bf16x8*>(Qs + ro), ac[t], 0, 0, 0);
-      }
-    // band term of query slice t: bd^T[jj][ii'] = Qv_{i0+16t+ii'} . Ppos[T-1-i+j] = H[jj - ii' + 15][ii'] with
-    // H = Pband[base .. base+31] Qv_slice^T, base = 48 - 16 t + 16 w
-    float s[4][4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      f32x4 hh[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-      const int base = 48 - 16 * t + 16 * w;
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const bf16x8 qvb = *reinterpret_cast<const bf16x8*>(Qvs + (16 * t + (lane & 15)) * LR + ks * 32 + 8 * (lane >> 4));
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt) {
-          const bf16x8 pa = *reinterpret_cast<const bf16x8*>(Pr + (base + 16 * mt + (lane & 15)) * LR + ks * 32 +
-                                                             8 * (lane >> 4));
-          hh[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, qvb, hh[mt], 0, 0, 0);
-        }
+        const bf16x8 ob = *reinterpret_cast<const bf16x8*>(Os + (16 * t + (lane & 15)) * LR + ks * 32 + 8 * (lane >> 4));
+        a[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fv[ks], ob, a[t], 0, 0, 0);
       }
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) H[(16 * mt + 4 * (lane >> 4) + r) * LH + (lane & 15)] = hh[mt][r];
-      wsync();
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int jj = 4 * (lane >> 4) + r, ii = lane & 15;
-        s[t][r] = (ac[t][r] + H[(jj - ii + 15) * LH + ii]) * p.scale;
-      }
-      wsync();
-    }
-    // the next block's loads are issued here (not before the band term: register pressure) and overlap
-    // the dPd / dV / dK MFMAs
-    if (qb + 1 < nqb) fetch(qb + 1);
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      // ---- dPd^T = V dO^T, one 16-query slice at a time (register pressure) ----
-      f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const int ro = (16 * t + (lane & 15)) * LR + ks * 32 + 8 * (lane >> 4);
-        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fv[ks], *reinterpret_cast<const bf16x8*>(Os + ro), a, 0, 0, 0);
-      }
+    for (int t = 0; t < 4; ++t)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int kk = 4 * (lane >> 4) + r, qq = 16 * t + (lane & 15);
         const int j = jb + r, i = i0 + qq;
         float pd = 0.f, ds = 0.f;
         if (j < len && i < len) {
-          const float pv = __expf(s[t][r] - Ls[qq]);
-          float g = a[r];
+          const float pv = Pt[(j - j0) * (BQ + 1) + qq] * Cs[qq];
+          float g = a[t][r];
           pd = pv;
           if (p.p_drop > 0.f) {
             const uint64_t idx = (uint64_t)((bh * p.T + i) * p.T + j);
@@ -461,9 +435,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkv_kernel(AbP p) {
         PW[kk * LW + qq] = f2bf(pd);
         DW[kk * LW + qq] = f2bf(ds);
       }
-    }
     wsync();
-    // ---- dV += Pd^T dO, dK += dS^T Qu (dO / Qu read transposed out of their row images) ----
+    // dV += Pd^T dO, dK += dS^T Qu (dO / Qu read transposed out of their row images)
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const bf16x8 pa = *reinterpret_cast<const bf16x8*>(PW + (lane & 15) * LW + ks * 32 + 8 * (lane >> 4));
@@ -490,20 +463,19 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkv_kernel(AbP p) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// kernel 3: per-chunk partials of dPpos
+// kernel 3: per-chunk partials of dPpos  (P from p~ and the block maxima, as kernel 2)
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256, 2) void attn_bwd_dpos_kernel(AbP p) {
   __shared__ __attribute__((aligned(16))) uint16_t Vs[NPJ * LR];     // V rows jbase.. [key][c]
-  __shared__ __attribute__((aligned(16))) uint16_t Ks[NPJ * LR];     // K rows jbase.. [key][c]
-  __shared__ __attribute__((aligned(16))) uint16_t Pr[PB * LR];      // Ppos rows r0-31 .. r0+95 [row][c]
   __shared__ __attribute__((aligned(16))) uint16_t Dl[NPQ * LDL];    // dS [i - ib0][j - jbase]
   __shared__ __attribute__((aligned(16))) uint16_t Qt[BDK * LQ3];    // Qv^T [c][i - ib0]
-  __shared__ __attribute__((aligned(16))) float Gw[4][16 * LG3];     // per-wave f32 score band
-  __shared__ float Rs[NPQ], Ls[NPQ];
+  __shared__ float Rs[NPQ];
+  __shared__ float Cs[NPQ * 3];   // exp(m_{i,kb} - lse_i) of the (up to) 3 key blocks the 96 keys touch
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int T = (int)p.T, dk = (int)p.dkh;
   const int npos = 2 * T - 1;
+  const int nkb_all = (T + BK - 1) / BK;
   const Blk3 blk = xcd_block3();
   const int r0 = (int)blk.x * 64;
   const int64_t h = blk.y;
@@ -512,25 +484,11 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dpos_kernel(AbP p) {
   const uint64_t seed = (p.p_drop > 0.f) ? load_seed(p.seed) : 0ull;
   const float keep = (p.p_drop > 0.f) ? 1.f / (1.f - p.p_drop) : 1.f;
   zero_pad(Vs, NPJ, dk, NPJ);
-  zero_pad(Ks, NPJ, dk, NPJ);
   for (int e = threadIdx.x; e < (BDK - dk) * LQ3; e += 256) Qt[dk * LQ3 + e] = 0;
-  // the positional band is the same for every iteration of this workgroup: staged once
-  zero_pad(Pr, PB, dk, 127);
-  {
-    const int cq = dk >> 2;
-    for (int e = threadIdx.x; e < 127 * cq; e += 256) {
-      const int rr = e / cq, c4 = (e - rr * cq) * 4;
-      const int r = r0 - 31 + rr;
-      const float4 v = (r >= 0 && r < npos) ? *reinterpret_cast<const float4*>(p.pos + (int64_t)r * p.d + hoff + c4)
-                                            : make_float4(0.f, 0.f, 0.f, 0.f);
-      st4(Pr + rr * LR + c4, v);
-    }
-  }
   f32x4 acc[3];
 #pragma unroll
   for (int u = 0; u < 3; ++u) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int qh = w & 1, kh = w >> 1;   // S / dS computation: query half, key half (48 keys)
-  const int wb = 16 - 16 * qh + 48 * kh;   // this wave's band offset inside Pr
+  const int qh = w & 1, kh = w >> 1;   // dS computation: query half, key half (48 keys)
   const int64_t b0 = bchunk * p.bpc;
   const int64_t b1 = min<int64_t>(p.B, b0 + p.bpc);
   // iterations (utterance b, query block ib0) that address a valid key for these positions
@@ -552,33 +510,42 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dpos_kernel(AbP p) {
     }
     return false;
   };
-  // next iteration's operands in registers (software pipeline): V and K rows, Qv rows, row sums and
-  // lse, this lane's dO and Qu fragments
-  float4 nvr[(NPJ * 12 + 255) / 256], nkr[(NPJ * 12 + 255) / 256], nqr[(NPQ * 12 + 255) / 256];
-  float nrs = 0.f, nls = 3.0e38f;
-  bf16x8 nfdo[2], nfqu[2];
+  // next iteration's operands in registers (software pipeline): V rows, Qv rows, row sums, the rows'
+  // block scales, this lane's dO fragments and 12 p~ elements
+  float4 nvr[(NPJ * 12 + 255) / 256], nqr[(NPQ * 12 + 255) / 256];
+  float nrs = 0.f, nm = 0.f, nl = 3.0e38f;
+  bf16x8 nfdo[2];
+  uint16_t np[3][4];
+  auto kbase = [&](int jb) { return (jb > 0 ? jb : 0) >> 6; };
   auto fetch = [&](int64_t bb, int ib, int ln) {
     const int jb = r0 - (T - 1) + ib;
     const int64_t bhh = bb * p.H + h;
     fetch_rows<(NPJ * 12 + 255) / 256>(nvr, p.v, p.ldkv, bb * p.T, jb, NPJ, 0, ln, hoff, dk);
-    fetch_rows<(NPJ * 12 + 255) / 256>(nkr, p.k, p.ldkv, bb * p.T, jb, NPJ, 0, ln, hoff, dk);
     fetch_rows<(NPQ * 12 + 255) / 256>(nqr, p.qv, p.ldq, bb * p.T, ib, NPQ, 0, ln, hoff, dk);
-    if (threadIdx.x < NPQ) {
-      const bool ok = ib + (int)threadIdx.x < ln;
-      nrs = ok ? p.rsum[bhh * p.T + ib + threadIdx.x] : 0.f;
-      nls = ok ? p.lse[bhh * p.T + ib + threadIdx.x] : 3.0e38f;
+    if (threadIdx.x < NPQ) nrs = (ib + (int)threadIdx.x < ln) ? p.rsum[bhh * p.T + ib + threadIdx.x] : 0.f;
+    if (threadIdx.x < 3 * NPQ) {
+      const int il = threadIdx.x / 3, q = threadIdx.x - 3 * il;
+      const int i = ib + il, kb = kbase(jb) + q;
+      const bool ok = i < ln && kb < nkb_all;
+      nm = ok ? p.mblk[(bhh * p.T + i) * nkb_all + kb] : 0.f;
+      nl = ok ? p.lse[bhh * p.T + i] : 3.0e38f;
     }
     const int iq = ib + 16 * qh + (lane & 15);
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int c0 = ks * 32 + 8 * (lane >> 4);
       const bool ok = iq < ln;
-      const int64_t off = (bb * p.T + (ok ? iq : 0)) * p.ldq + hoff + c0;
-      nfdo[ks] = frag8(p.dO + off, ok ? dk - c0 : 0);
-      nfqu[ks] = frag8(p.qu + off, ok ? dk - c0 : 0);
+      nfdo[ks] = frag8(p.dO + (bb * p.T + (ok ? iq : 0)) * p.ldq + hoff + c0, ok ? dk - c0 : 0);
     }
+#pragma unroll
+    for (int t = 0; t < 3; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int il = 16 * qh + 4 * (lane >> 4) + r, jl = 48 * kh + 16 * t + (lane & 15);
+        const int i = ib + il, j = jb + jl;
+        np[t][r] = (i < ln && j >= 0 && j < ln) ? p.pt[(bhh * p.T + i) * p.T + j] : (uint16_t)0;
+      }
   };
-  float* G = Gw[w];
   int64_t b = b0;
   int ib0 = -NPQ, len = b0 < b1 ? ulen(b0) : 0;
   bool more = b0 < b1 && advance(b, ib0, len);
@@ -586,61 +553,49 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dpos_kernel(AbP p) {
   while (more) {
     const int64_t bh = b * p.H + h;
     const int jbase = r0 - (T - 1) + ib0;
+    const int kb0 = kbase(jbase);
     const int cur_len = len;
     const int cur_ib0 = ib0;
     __syncthreads();
     put_rows<(NPJ * 12 + 255) / 256>(Vs, nullptr, 0, nvr, NPJ, dk);
-    put_rows<(NPJ * 12 + 255) / 256>(Ks, nullptr, 0, nkr, NPJ, dk);
     put_rows<(NPQ * 12 + 255) / 256>(nullptr, Qt, LQ3, nqr, NPQ, dk);
-    if (threadIdx.x < NPQ) { Rs[threadIdx.x] = nrs; Ls[threadIdx.x] = nls; }
+    if (threadIdx.x < NPQ) Rs[threadIdx.x] = nrs;
+    if (threadIdx.x < 3 * NPQ) Cs[threadIdx.x] = __expf(nm - nl);
     const bf16x8 fdo[2] = {nfdo[0], nfdo[1]};
-    const bf16x8 fqu[2] = {nfqu[0], nfqu[1]};
+    float pcur[3][4];
+#pragma unroll
+    for (int t = 0; t < 3; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) pcur[t][r] = __uint_as_float((uint32_t)np[t][r] << 16);
     __syncthreads();
-    // queries ib0 + 16 qh + .., keys jbase + 48 kh + ..: S (AC + skewed band) and dPd
-    f32x4 ac[3], a[3], g[4];
+    // dPd for queries ib0 + 16 qh + .., keys jbase + 48 kh + ..
+    f32x4 a[3];
 #pragma unroll
-    for (int t = 0; t < 3; ++t) { ac[t] = f32x4{0.f, 0.f, 0.f, 0.f}; a[t] = ac[t]; }
+    for (int t = 0; t < 3; ++t) a[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int t = 0; t < 4; ++t) g[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const bf16x8 fqv = tr_frag(Qt, LQ3, ks * 32, 16 * qh, lane);   // Qv rows as the A operand
+    for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
       for (int t = 0; t < 3; ++t) {
-        const int ro = (48 * kh + 16 * t + (lane & 15)) * LR + ks * 32 + 8 * (lane >> 4);
-        ac[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fqu[ks], *reinterpret_cast<const bf16x8*>(Ks + ro), ac[t], 0, 0, 0);
-        a[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fdo[ks], *reinterpret_cast<const bf16x8*>(Vs + ro), a[t], 0, 0, 0);
+        const bf16x8 vb = *reinterpret_cast<const bf16x8*>(Vs + (48 * kh + 16 * t + (lane & 15)) * LR + ks * 32 +
+                                                             8 * (lane >> 4));
+        a[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fdo[ks], vb, a[t], 0, 0, 0);
       }
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const bf16x8 pb = *reinterpret_cast<const bf16x8*>(Pr + (wb + 16 * t + (lane & 15)) * LR + ks * 32 +
-                                                           8 * (lane >> 4));
-        g[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fqv, pb, g[t], 0, 0, 0);
-      }
-    }
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) G[(4 * (lane >> 4) + r) * LG3 + 16 * t + (lane & 15)] = g[t][r];
-    wsync();
 #pragma unroll
     for (int t = 0; t < 3; ++t)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int ii = 4 * (lane >> 4) + r, jj = 16 * t + (lane & 15);
-        const int il = 16 * qh + ii, jl = 48 * kh + jj;
+        const int il = 16 * qh + 4 * (lane >> 4) + r, jl = 48 * kh + 16 * t + (lane & 15);
         const int i = cur_ib0 + il, j = jbase + jl;
         float ds = 0.f;
         if (i < cur_len && j >= 0 && j < cur_len) {
-          const float sv = (ac[t][r] + G[ii * LG3 + jj - ii + 15]) * p.scale;
           const int64_t idx = (bh * p.T + i) * p.T + j;
-          float gg = a[t][r];
-          if (p.p_drop > 0.f) gg = dropout_keep(seed, p.rng_stream, (uint64_t)idx, p.p_drop) ? gg * keep : 0.f;
-          ds = __expf(sv - Ls[il]) * (gg - Rs[il]) * p.scale;
+          float g = a[t][r];
+          if (p.p_drop > 0.f) g = dropout_keep(seed, p.rng_stream, (uint64_t)idx, p.p_drop) ? g * keep : 0.f;
+          ds = pcur[t][r] * Cs[il * 3 + ((j >> 6) - kb0)] * (g - Rs[il]) * p.scale;
         }
         Dl[il * LDL + jl] = f2bf(ds);
       }
-    // the operands are consumed: the next iteration's loads overlap the dPpos MFMAs
+    // the p~ elements are consumed: the next iteration's loads overlap the dPpos MFMAs
     more = advance(b, ib0, len);
     if (more) fetch(b, ib0, len);
     __syncthreads();
@@ -686,17 +641,17 @@ int64_t kdfm_relpos_attn_bwd_ws(int64_t B, int64_t H, int64_t T, int64_t d) {
 }
 
 int kdfm_relpos_attn_bwd(const float* dO, const float* O, const float* qu, const float* qv, const float* qkv,
-                         const float* pos, const float* lse, const int64_t* lengths, float* dqu, float* dqv,
-                         float* dqkv, float* dpos,
+                         const float* pos, const float* lse, const uint16_t* p_tilde, const float* m_blk,
+                         const int64_t* lengths, float* dqu, float* dqv, float* dqkv, float* dpos,
                          float* ws, int64_t ws_len, int64_t B, int64_t H, int64_t T, int64_t d, float scale,
                          float dropout_p, const uint64_t* seed, uint64_t rng_stream, void* stream) {
-  return kdfm_relpos_attn_bwd_parts(dO, O, qu, qv, qkv, pos, lse, lengths, dqu, dqv, dqkv, dpos, ws, ws_len, B, H, T, d,
+  return kdfm_relpos_attn_bwd_parts(dO, O, qu, qv, qkv, pos, lse, p_tilde, m_blk, lengths, dqu, dqv, dqkv, dpos, ws, ws_len, B, H, T, d,
                                     scale, dropout_p, seed, rng_stream, KDFM_ATTN_BWD_ALL, stream);
 }
 
 int kdfm_relpos_attn_bwd_parts(const float* dO, const float* O, const float* qu, const float* qv, const float* qkv,
-                               const float* pos, const float* lse, const int64_t* lengths, float* dqu, float* dqv,
-                               float* dqkv, float* dpos, float* ws, int64_t ws_len, int64_t B, int64_t H, int64_t T,
+                               const float* pos, const float* lse, const uint16_t* p_tilde, const float* m_blk,
+                               const int64_t* lengths, float* dqu, float* dqv, float* dqkv, float* dpos, float* ws, int64_t ws_len, int64_t B, int64_t H, int64_t T,
                                int64_t d, float scale, float dropout_p, const uint64_t* seed, uint64_t rng_stream,
                                int32_t parts, void* stream) {
   using namespace kdfm;
@@ -704,6 +659,8 @@ int kdfm_relpos_attn_bwd_parts(const float* dO, const float* O, const float* qu,
   KDFM_REQUIRE(!(parts & KDFM_ATTN_BWD_DQ) || (dqu && dqv), "dq part needs dqu / dqv");
   KDFM_REQUIRE(!(parts & KDFM_ATTN_BWD_DKV) || dqkv, "dkv part needs dqkv");
   KDFM_REQUIRE(!(parts & KDFM_ATTN_BWD_DPOS) || dpos, "dpos part needs dpos");
+  KDFM_REQUIRE(!(parts & (KDFM_ATTN_BWD_DKV | KDFM_ATTN_BWD_DPOS)) || (p_tilde && m_blk),
+               "dkv / dpos parts need the forward's p_tilde and m_blk");
   KDFM_REQUIRE(H > 0 && d % H == 0, "d must be a multiple of H");
   const int64_t dk = d / H;
   KDFM_REQUIRE(dk <= 48 && dk % 4 == 0, "head dim must be a multiple of 4 and <= 48");
@@ -714,7 +671,8 @@ int kdfm_relpos_attn_bwd_parts(const float* dO, const float* O, const float* qu,
                "operands must be 16-byte aligned");
   if (B == 0) return KDFM_OK;
   AbP p{};
-  p.dO = dO; p.qu = qu; p.qv = qv; p.k = qkv + d; p.v = qkv + 2 * d; p.pos = pos; p.lse = lse; p.lens = lengths;
+  p.dO = dO; p.qu = qu; p.qv = qv; p.k = qkv + d; p.v = qkv + 2 * d; p.pos = pos; p.lse = lse; p.pt = p_tilde; p.mblk = m_blk;
+  p.lens = lengths;
   p.dqu = dqu; p.dqv = dqv; p.rsum = ws; p.dpos_part = ws + B * H * T;
   p.dk = dqkv ? dqkv + d : nullptr;
   p.dv = dqkv ? dqkv + 2 * d : nullptr;

@@ -11,8 +11,10 @@
 //   * one pass over the key blocks with an online softmax (running row max / sum, O rescaled), the
 //     counter-RNG dropout mask of the unfused kernel (same index -> same mask) applied to the
 //     unnormalised probabilities and O += P_drop V via MFMA (P staged through LDS into A-fragment
-//     order, V staged transposed); training writes only the per-row log-sum-exp
-//     lse_i = m_i + ln l_i (B*H*T floats), from which the backward recomputes P = exp(S - lse);
+//     order, V staged transposed); training writes the per-row log-sum-exp lse_i = m_i + ln l_i,
+//     the UNNORMALISED probabilities p~ = exp(s - m_ikb) as bf16 (B,H,T,T) and the running row max
+//     m_ikb after each 64-key block (B,H,T,ceil(T/64)): P = p~ exp(m_ikb - lse_i) (the backward's
+//     dK/dV and dPpos kernels read P this way: half the bytes of an f32 P, and no second pass);
 //   * (the unfused backward's path) two passes: (1) row max and sum, (2) exact probabilities with
 //     the P / P_drop outputs the per-op backward reads.
 // Output O is written straight into the (rows, d) head-interleaved layout.
@@ -34,7 +36,7 @@ constexpr int LDG = GW + 1;       // f32 stride of the per-wave G tile
 struct AttnP {
   const float* qu; const float* qv; const float* k; const float* v; const float* pos;
   const int64_t* lens;
-  float* o; float* P; float* Pd; float* lse;
+  float* o; float* P; float* Pd; float* lse; uint16_t* pt; float* mblk;
   int64_t B, H, T, d, dk, ldq, ldkv;
   float scale, p_drop;
   const uint64_t* seed; uint64_t rng_stream;
@@ -284,6 +286,12 @@ __global__ __launch_bounds__(256, 2) void relpos_attn_fwd_kernel(AttnP p) {
         for (int u = 0; u < 3; ++u) oacc[u][r] *= corr;
       }
     }
+    if (!TWO_PASS && live && p.mblk && (lane & 15) == 0) {   // the running max this block's p~ is relative to
+      const int nkb_all = (T + AKB - 1) / AKB;
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (ib + r < T) p.mblk[(bh * p.T + ib + r) * nkb_all + kb] = mrow[r];
+    }
     uint16_t* Pw = Ps[w];
 #pragma unroll
     for (int t = 0; t < 4; ++t)
@@ -292,6 +300,7 @@ __global__ __launch_bounds__(256, 2) void relpos_attn_fwd_kernel(AttnP p) {
         const int ii = 4 * (lane >> 4) + r, jj = 16 * t + (lane & 15);
         const int i = ib + r, j = j0 + jj;
         float pv = (s[t][r] > -1.0e38f) ? __expf(s[t][r] - mrow[r]) * inv[r] : 0.f;
+        if (!TWO_PASS && p.pt && i < T && j < T) p.pt[prow0 + (int64_t)r * p.T + j] = f2bf(pv);
         float pdv = pv;
         if (p.p_drop > 0.f && pv != 0.f) {
           const uint64_t idx = (uint64_t)(prow0 + (int64_t)r * p.T) + (uint64_t)j;
@@ -348,7 +357,7 @@ __global__ __launch_bounds__(256, 2) void relpos_attn_fwd_kernel(AttnP p) {
 
 extern "C" int kdfm_relpos_attn_fwd(const float* qu, const float* qv, const float* qkv, const float* pos,
                                     const int64_t* lengths, float* o, float* P, float* Pdrop, float* lse,
-                                    int64_t B, int64_t H,
+                                    uint16_t* p_tilde, float* m_blk, int64_t B, int64_t H,
                                     int64_t T, int64_t d, float scale, float dropout_p, const uint64_t* seed,
                                     uint64_t rng_stream, void* stream) {
   using namespace kdfm;
@@ -359,11 +368,12 @@ extern "C" int kdfm_relpos_attn_fwd(const float* qu, const float* qv, const floa
   KDFM_REQUIRE(T > 0 && T <= 4096, "T out of range");
   KDFM_REQUIRE(d % 4 == 0, "d must be a multiple of 4");
   KDFM_REQUIRE(dropout_p == 0.f || seed, "dropout needs a seed");
-  KDFM_REQUIRE(!(lse && (P || Pdrop)), "lse is the single-pass output (no P / Pdrop with it)");
+  KDFM_REQUIRE(!((lse || p_tilde || m_blk) && (P || Pdrop)), "lse / p~ / m_blk are single-pass outputs (no P / Pdrop)");
+  KDFM_REQUIRE((p_tilde == nullptr) == (m_blk == nullptr), "p~ and m_blk go together");
   if (B == 0) return KDFM_OK;
   AttnP p;
   p.qu = qu; p.qv = qv; p.k = qkv + d; p.v = qkv + 2 * d; p.pos = pos; p.lens = lengths;
-  p.o = o; p.P = P; p.Pd = Pdrop; p.lse = lse;
+  p.o = o; p.P = P; p.Pd = Pdrop; p.lse = lse; p.pt = p_tilde; p.mblk = m_blk;
   p.B = B; p.H = H; p.T = T; p.d = d; p.dk = dk; p.ldq = d; p.ldkv = 3 * d;
   p.scale = scale; p.p_drop = dropout_p; p.seed = seed; p.rng_stream = rng_stream;
   dim3 grid((unsigned)ceil_div(T, AQ), (unsigned)(B * H));

@@ -31,15 +31,17 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const
                                                     const int64_t* __restrict__ step,
                                                     const int64_t* __restrict__ adam_base, float base, float d_model,
                                                     float warmup, float min_lr, float b1, float b2, float eps, float wd,
-                                                    float gscale, float* __restrict__ lr_out) {
+                                                    float gscale, float* __restrict__ lr_out,
+                                                    const float* __restrict__ gstats) {
   const int64_t k = step[0];
   const float lr = noam_lr(k, base, d_model, warmup, min_lr);
+  if (lr_out && blockIdx.x == 0 && threadIdx.x == 0) lr_out[0] = lr;
+  if (gstats && gstats[1] != 0.f) return;   // a non-finite gradient: parameters and moments unchanged
   const int64_t ka = adam_base ? k - adam_base[0] : k;   // AdamW's own step count
   const float bc1 = 1.f - powf(b1, (float)ka);
   const float bc2 = 1.f - powf(b2, (float)ka);
   const float step_size = lr / bc1;
   const float bc2s = sqrtf(bc2);
-  if (lr_out && blockIdx.x == 0 && threadIdx.x == 0) lr_out[0] = lr;
   const int64_t stride = (int64_t)gridDim.x * 256;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
     const float gi = g[i] * gscale;
@@ -53,13 +55,94 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const
   }
 }
 
+// gradient statistics: per-workgroup partials of sum g^2 and of the non-finite count over a fixed
+// grid (grid-stride, fixed lane order), then one workgroup folds them in a fixed tree: deterministic
+constexpr int GS_BLOCKS = 512;
+
+__device__ __forceinline__ void block_sum2(float& a, float& b, float* red) {
+  for (int o = 32; o > 0; o >>= 1) {
+    a += __shfl_xor(a, o);
+    b += __shfl_xor(b, o);
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) {
+    red[2 * w] = a;
+    red[2 * w + 1] = b;
+  }
+  __syncthreads();
+  a = red[0] + red[2] + (red[4] + red[6]);
+  b = red[1] + red[3] + (red[5] + red[7]);
+}
+
+__global__ __launch_bounds__(256) void grad_stats_kernel(const float* __restrict__ g, int64_t n, float scale,
+                                                         float* __restrict__ part) {
+  __shared__ float red[8];
+  float ss = 0.f, bad = 0.f;
+  const int64_t stride = (int64_t)gridDim.x * 256 * 4;
+  const bool vec = (((uintptr_t)g) & 15) == 0;
+  for (int64_t i0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4; i0 < n; i0 += stride) {
+    float v[4];
+    if (vec && i0 + 4 <= n) {
+      const float4 q = *reinterpret_cast<const float4*>(g + i0);
+      v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = i0 + e < n ? g[i0 + e] : 0.f;
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float x = v[e] * scale;
+      if (isfinite(x)) ss += x * x; else bad += 1.f;
+    }
+  }
+  block_sum2(ss, bad, red);
+  if (threadIdx.x == 0) {
+    part[2 * blockIdx.x] = ss;
+    part[2 * blockIdx.x + 1] = bad;
+  }
+}
+
+__global__ __launch_bounds__(256) void grad_stats_fold_kernel(const float* __restrict__ part, int nb,
+                                                              float* __restrict__ out) {
+  __shared__ float red[8];
+  float ss = 0.f, bad = 0.f;
+  for (int i = threadIdx.x; i < nb; i += 256) {
+    ss += part[2 * i];
+    bad += part[2 * i + 1];
+  }
+  block_sum2(ss, bad, red);
+  if (threadIdx.x == 0) {
+    out[0] = ss;
+    out[1] = bad;
+  }
+}
+
 }  // namespace
 }  // namespace kdfm
+
+extern "C" int64_t kdfm_grad_stats_ws(void) { return 2 * kdfm::GS_BLOCKS; }
+
+extern "C" int kdfm_grad_stats(const float* grads, int64_t n, float scale, float* ws, int64_t ws_len, float* out2,
+                               void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(grads && ws && out2 && n >= 0, "bad args");
+  KDFM_REQUIRE(ws_len >= 2 * GS_BLOCKS, "workspace too small (kdfm_grad_stats_ws)");
+  int64_t nb = ceil_div(n, 1024);
+  if (nb > GS_BLOCKS) nb = GS_BLOCKS;
+  if (nb < 1) nb = 1;
+  hipStream_t st = as_stream(stream);
+  hipLaunchKernelGGL(grad_stats_kernel, dim3((unsigned)nb), dim3(256), 0, st, grads, n, scale, ws);
+  int rc = check_launch("kdfm_grad_stats");
+  if (rc) return rc;
+  hipLaunchKernelGGL(grad_stats_fold_kernel, dim3(1), dim3(256), 0, st, ws, (int)nb, out2);
+  return check_launch("kdfm_grad_stats(fold)");
+}
 
 extern "C" int kdfm_adamw_noam(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, int64_t n,
                                const int64_t* step, const int64_t* adam_base, float base_lr, float d_model, float warmup_steps, float min_lr,
                                float beta1, float beta2, float eps, float weight_decay, float grad_scale,
-                               float* lr_out, void* stream) {
+                               float* lr_out, const float* gstats, void* stream) {
   using namespace kdfm;
   KDFM_REQUIRE(params && grads && exp_avg && exp_avg_sq && step, "null pointer");
   if (n == 0) return KDFM_OK;
@@ -67,6 +150,6 @@ extern "C" int kdfm_adamw_noam(float* params, const float* grads, float* exp_avg
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(adamw_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), params, grads, exp_avg,
                      exp_avg_sq, n, step, adam_base, base_lr, d_model, warmup_steps, min_lr, beta1, beta2, eps, weight_decay,
-                     grad_scale, lr_out);
+                     grad_scale, lr_out, gstats);
   return check_launch("kdfm_adamw_noam");
 }

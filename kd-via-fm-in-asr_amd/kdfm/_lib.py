@@ -75,9 +75,9 @@ SIGNATURES: dict[str, tuple] = {
     "kdfm_range_push": (_i32, [C.c_char_p]),
     "kdfm_wgrad_bf16_ws": (_i64, [_i64, _i64, _i64, _i32]),
     "kdfm_relpos_attn_bwd_ws": (_i64, [_i64, _i64, _i64, _i64]),
-    "kdfm_relpos_attn_bwd": (_i32, [P, P, P, P, P, P, P, P, P, P, P, P, P, _i64, _i64, _i64, _i64, _i64, _f32, _f32, P,
+    "kdfm_relpos_attn_bwd": (_i32, [P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, _i64, _i64, _i64, _i64, _i64, _f32, _f32, P,
                                     C.c_uint64, P]),
-    "kdfm_relpos_attn_bwd_parts": (_i32, [P, P, P, P, P, P, P, P, P, P, P, P, P, _i64, _i64, _i64, _i64, _i64, _f32,
+    "kdfm_relpos_attn_bwd_parts": (_i32, [P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, _i64, _i64, _i64, _i64, _i64, _f32,
                                           _f32, P, C.c_uint64, _i32, P]),
     "kdfm_wgrad_bf16": (_i32, [P, P, P, _i64, P, _i64, _i64, _i64, _f32, P, _i64, P]),
     "kdfm_fm_chain_fwd": (_i32, [P, P, P, _i64, P, P, P, P, P, P, P, P, P, P, P, _f32, _i64, _i32, _i32, P]),
@@ -151,7 +151,7 @@ SIGNATURES: dict[str, tuple] = {
     "kdfm_qkv_prep": (_i32, [P, P, P, P, P, _i64, _i64, P]),
     "kdfm_relpos_softmax_fwd": (_i32, [P, P, P, P, P, _i64, _i64, _i64, _f32, _f32, P, C.c_uint64, P]),
     "kdfm_relpos_softmax_bwd": (_i32, [P, P, P, P, _i64, _i64, _i64, _f32, _f32, P, C.c_uint64, P]),
-    "kdfm_relpos_attn_fwd": (_i32, [P, P, P, P, P, P, P, P, P, _i64, _i64, _i64, _i64, _f32, _f32, P, C.c_uint64, P]),
+    "kdfm_relpos_attn_fwd": (_i32, [P, P, P, P, P, P, P, P, P, P, P, _i64, _i64, _i64, _i64, _f32, _f32, P, C.c_uint64, P]),
     "kdfm_relpos_table": (_i32, [P, _i64, _i64, P]),
     "kdfm_glu_mask_fwd": (_i32, [P, P, P, _i64, _i64, _i64, P]),
     "kdfm_glu_mask_bwd": (_i32, [P, P, P, P, _i64, _i64, _i64, P]),
@@ -183,7 +183,9 @@ SIGNATURES: dict[str, tuple] = {
     "kdfm_convw_grad": (_i32, [P, P, _i64, _i64, _i64, _f32, P]),
     "kdfm_subsample_lengths": (_i32, [P, P, P, P, _i64, _i64, P]),
     "kdfm_step_advance": (_i32, [P, P, P]),
-    "kdfm_adamw_noam": (_i32, [P, P, P, P, _i64, P, P, _f32, _f32, _f32, _f32, _f32, _f32, _f32, _f32, _f32, P, P]),
+    "kdfm_adamw_noam": (_i32, [P, P, P, P, _i64, P, P, _f32, _f32, _f32, _f32, _f32, _f32, _f32, _f32, _f32, P, P, P]),
+    "kdfm_grad_stats_ws": (_i64, []),
+    "kdfm_grad_stats": (_i32, [P, _i64, _f32, P, _i64, P, P]),
 }
 
 _LIB = None

@@ -76,6 +76,9 @@ class Ver5Config:
     # execution
     math: str = "bf16"               # MFMA arithmetic: "bf16" (throughput) or "f32" (parity)
     deterministic: bool = False      # ordered reductions (kdfm_set_deterministic): bitwise-reproducible runs
+    # opt-in gradient check (not in the reference): global gradient norm + non-finite count each step
+    # (kdfm_grad_stats, logged as grad_norm / grad_nonfinite); a non-finite gradient skips the AdamW update
+    grad_check: bool = False
     share_frontend: bool = True      # one mel frontend for student+teacher when dither == 0
 
     @property

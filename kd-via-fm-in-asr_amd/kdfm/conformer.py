@@ -403,16 +403,17 @@ def layer_forward(cfg, S: EncoderShapes, P, L, li, x, out, pos_emb, lengths, *, 
         # fused flash-style kernel: no AC / BD materialisation; P (and P_drop) only when the
         # backward needs them
         if _ATTN_BWD_FUSED:
-            # one online-softmax pass; training keeps only the per-row log-sum-exp: the fused backward
-            # recomputes P tile by tile and regenerates the dropout mask from the counter RNG
+            # one online-softmax pass; training keeps the per-row log-sum-exp (the backward's dQ kernel
+            # recomputes P tile by tile from it) and the bf16 unnormalised p~ with its per-block maxima
+            # (dK / dV and dPpos read P from them); dropout masks are regenerated from the counter RNG
             Pm = Pd = None
-            lse = _empty(B, H, T, dev=dev) if save else None
+            lse, pt, mblk = K.attn_saved(B, H, T, dev) if save else (None, None, None)
         else:
             Pm = _empty(B, H, T, T, dev=dev) if save else None
             Pd = (_empty(B, H, T, T, dev=dev) if pa > 0 else Pm) if save else None
-            lse = None
+            lse = pt = mblk = None
         K.relpos_attn_fwd(qu, qv, qkv, ppos, lengths, o, Pm, Pd if pa > 0 else None, B, H, T,
-                          1.0 / math.sqrt(dk), pa, seed, _stream(salt, li, SITE_ATT_P), lse=lse)
+                          1.0 / math.sqrt(dk), pa, seed, _stream(salt, li, SITE_ATT_P), lse=lse, p_tilde=pt, m_blk=mblk)
     else:
         ac = _empty(B, H, T, T, dev=dev)
         # AC = (q+u) K^T  per (b,h): A(i,c)=qu[b,i,h*dk+c]  B(c,j)=K[b,j,h*dk+c]
@@ -443,7 +444,8 @@ def layer_forward(cfg, S: EncoderShapes, P, L, li, x, out, pos_emb, lengths, *, 
                  R=x1, rscale=1.0, dropout_p=pd, seed=seed, rng_stream=_stream(salt, li, SITE_ATT_OUT))
     fused_attn = K.get_math() == "bf16" and dk <= 48 and _ATTN_BWD_FUSED
     keep(x1=x1, ln2=ln2, m2=m2, r2=r2, qkv=qkv, qu=qu, qv=qv, ppos=ppos, P=Pm, Pd=Pd, o=o, o_h=o_h, pa=pa,
-         attn_fused=fused_attn, lse=lse if fused_attn else None)
+         attn_fused=fused_attn, lse=lse if fused_attn else None, pt=pt if fused_attn else None,
+         mblk=mblk if fused_attn else None)
     del ln2, qkv, qu, qv, ppos, Pm, Pd, o
 
     # ---- convolution module ----
@@ -664,16 +666,16 @@ def layer_backward(cfg, S: EncoderShapes, P, G, L, li, ctx, dout, pos_emb, lengt
         # the positional-term gradient dPpos feeds only the linear_pos weight gradient: it runs on the
         # weight-gradient stream beside the dQ / dK,dV kernels the main stream needs next
         abws = torch.empty(K.relpos_attn_bwd_ws(B, H, T, d), device=dev)
-        lse = ctx["lse"]
-        K.relpos_attn_bwd(do, ctx["o"], qu, qv, qkv, ppos, lse, lengths, dqu, dqv, dqkv, None, B, H, T, sc, ctx["pa"],
-                          seed, st_att, parts=K.ATTN_BWD_ROWDOT | K.ATTN_BWD_DQ | K.ATTN_BWD_DKV, ws=abws)
+        lse, pt, mblk = ctx["lse"], ctx["pt"], ctx["mblk"]
+        K.relpos_attn_bwd(do, ctx["o"], qu, qv, qkv, ppos, lse, pt, mblk, lengths, dqu, dqv, dqkv, None, B, H, T, sc,
+                          ctx["pa"], seed, st_att, parts=K.ATTN_BWD_ROWDOT | K.ATTN_BWD_DQ | K.ATTN_BWD_DKV, ws=abws)
         o_ = ctx["o"]
 
         def dpos_and_wgrad():
-            K.relpos_attn_bwd(do, o_, qu, qv, qkv, ppos, lse, lengths, None, None, None, dppos, B, H, T, sc, ctx["pa"],
-                              seed, st_att, parts=K.ATTN_BWD_DPOS, ws=abws)
+            K.relpos_attn_bwd(do, o_, qu, qv, qkv, ppos, lse, pt, mblk, lengths, None, None, None, dppos, B, H, T, sc,
+                              ctx["pa"], seed, st_att, parts=K.ATTN_BWD_DPOS, ws=abws)
             K.linear_dw(dppos, pos_emb, G[L + "self_attn.linear_pos.weight"])
-        WGRAD.run(dpos_and_wgrad, do, o_, qu, qv, qkv, ppos, lse, dppos, abws, pos_emb, lengths, seed)
+        WGRAD.run(dpos_and_wgrad, do, o_, qu, qv, qkv, ppos, lse, pt, mblk, dppos, abws, pos_emb, lengths, seed)
         del do
         return _attn_bwd_tail(P, G, L, ctx, dqkv, dqu, dqv, None, pos_emb, dx2, lng, cfg, pd, seed, salt, li, rows, d,
                               dev)

@@ -42,9 +42,13 @@ class BucketedGradAllReduce:
     backward finalises it from the END: heads, then the decoder, then layers 15..0, then the
     subsampling.  Ver5Engine.backward calls `ready(flat, offset)` whenever every gradient at index
     >= offset is final (after the heads, the decoder, every encoder layer); each bucket
-    [lo, hi) with lo >= offset that has not been launched yet is all-reduced asynchronously on a
-    communication stream that first waits for the main stream AND the weight-gradient side stream
-    (kdfm.overlap.WGRAD), so RCCL over xGMI runs while the dX chain of the lower layers continues.
+    [lo, hi) with lo >= offset that has not been launched yet is all-reduced asynchronously, issued
+    from the weight-gradient side stream (kdfm.overlap.WGRAD) after it has joined the main stream, so
+    the collective -- on RCCL's own stream, which waits for the issuing one -- starts once both
+    streams' gradients for the bucket are final, and RCCL over xGMI runs while the dX chain of the
+    lower layers continues.  No extra stream of ours: compute, teacher (+ CTC/KL), weight gradients
+    and RCCL's stream are four, one per hardware queue (GPU_MAX_HW_QUEUES=4).  With weight gradients
+    in line (deterministic mode) the collective is issued from the main stream.
     `__call__(flat)` (after the backward) launches what is left, makes the current stream wait for
     every collective and returns the 1/world mean scale for the fused AdamW.  With no ready() calls
     it is exactly FlatGradAllReduce with `buckets` chunks.  Bucket edges are aligned to 64 floats."""
@@ -59,25 +63,17 @@ class BucketedGradAllReduce:
         self.edges = sorted(set(self.edges))
         self._works = []
         self._launched = set()
-        self._comm = None
-
-    def _stream(self, flat):
-        if not flat.is_cuda:
-            return None
-        if self._comm is None:
-            self._comm = torch.cuda.Stream(device=flat.device)
-        return self._comm
 
     def _launch(self, flat, k: int):
         lo, hi = self.edges[k], self.edges[k + 1]
-        comm = self._stream(flat)
-        if comm is None:
+        side = None
+        if flat.is_cuda:
+            from .overlap import WGRAD
+            side = WGRAD.stream_after_current()
+        if side is None:
             self._works.append(dist.all_reduce(flat[lo:hi], group=self.group, async_op=True))
         else:
-            from .overlap import WGRAD
-            comm.wait_stream(torch.cuda.current_stream(flat.device))
-            WGRAD.fence(comm)
-            with torch.cuda.stream(comm):
+            with torch.cuda.stream(side):
                 self._works.append(dist.all_reduce(flat[lo:hi], group=self.group, async_op=True))
         self._launched.add(k)
 
@@ -96,8 +92,6 @@ class BucketedGradAllReduce:
                 self._launch(flat, k)
         for w in self._works:
             w.wait()   # device-side: the current stream waits for the collective
-        if self._comm is not None:
-            torch.cuda.current_stream(flat.device).wait_stream(self._comm)
         self._works.clear()
         self._launched.clear()
         return 1.0 / self.world

@@ -89,6 +89,8 @@ class Ver5Engine:
         self.lr = torch.zeros(1, device=dev)
         # total, ctc, kl, recon, layer KD (kd/fm pre+post, ver5: fm_post; + the DiffKD term with use_diffkd)
         self.losses = torch.zeros(5, device=dev)
+        # [sum g^2 of the (all-reduced, mean) gradient, #non-finite entries] when cfg.grad_check
+        self.grad_stats = torch.zeros(2, device=dev) if cfg.grad_check else None
         self.hws = HeadsWorkspace(cfg, dev)
         if K.twins_enabled():   # opt-in direct-B skinny path (KDFM_SKINNY_DIRECT_MIN_M)
             self.student.enable_bf16_twins()
@@ -400,8 +402,14 @@ class Ver5Engine:
         return nll.mean()
 
     def _aux_stream(self):
+        """The CTC/KL stream.  By default it IS the teacher stream: the main stream has just joined the
+        teacher there (the heads need its features), so the teacher stream is idle for exactly the span
+        CTC/KL run beside the heads forward, and the step keeps to three compute streams -- with RCCL's
+        own stream under DDP, four, within the GPU_MAX_HW_QUEUES=4 hardware queues, so no two streams
+        share a queue (a shared queue serialises its streams).  KDFM_AUX_STREAM=1: a stream of its own."""
         if getattr(self, "_aux", None) is None:
-            self._aux = _crit_stream(self.device)
+            own = __import__("os").environ.get("KDFM_AUX_STREAM", "0") == "1"
+            self._aux = _crit_stream(self.device) if own else self._side_stream()
         return self._aux
 
     def _join_losses(self, ctx):
@@ -458,9 +466,11 @@ class Ver5Engine:
         cfg = self.cfg
         st = self.student
         K.step_advance(self.step, None)
+        if self.grad_stats is not None:
+            K.grad_stats(st.grad, grad_scale, self.grad_stats)
         K.adamw_noam(st.data, st.grad, st.exp_avg, st.exp_avg_sq, self.step, cfg.lr, cfg.sched_d_model,
                      cfg.warmup_steps, cfg.min_lr, cfg.betas[0], cfg.betas[1], cfg.adam_eps, cfg.weight_decay,
-                     grad_scale, self.lr, adam_base=self.adam_base)
+                     grad_scale, self.lr, adam_base=self.adam_base, gstats=self.grad_stats)
 
     def advance_rng(self):
         with self._on_stream():

@@ -1121,50 +1121,69 @@ def relpos_attn_bwd_ws(B, H, T, d):
     return int(_lib.lib().kdfm_relpos_attn_bwd_ws(B, H, T, d))
 
 
-def relpos_attn_bwd(do, o, qu, qv, qkv, ppos, lse, lengths, dqu, dqv, dqkv, dppos, B, H, T, scale, p, seed, rng_stream,
-                    parts=ATTN_BWD_ALL, ws=None):
-    """Fused attention backward (csrc/attn_bwd.hip): dqu, dqv, dK/dV into dqkv[:, d:], dppos, with the
-    probabilities recomputed from the forward's per-row log-sum-exp `lse` (B, H, T).  `parts`
-    (ATTN_BWD_*) issues a subset; parts issued on different streams must share a dedicated `ws`
+def attn_saved(B, H, T, device):
+    """The single-pass forward's saved operands for the backward: lse (B,H,T) f32, p~ (B,H,T,T) bf16 and
+    the per-64-key-block running maxima m_blk (B,H,T,ceil(T/64)) f32."""
+    return (torch.empty(B, H, T, device=device), torch.empty(B, H, T, T, dtype=torch.bfloat16, device=device),
+            torch.empty(B, H, T, (T + 63) // 64, device=device))
+
+
+def relpos_attn_bwd(do, o, qu, qv, qkv, ppos, lse, p_tilde, m_blk, lengths, dqu, dqv, dqkv, dppos, B, H, T, scale, p,
+                    seed, rng_stream, parts=ATTN_BWD_ALL, ws=None):
+    """Fused attention backward (csrc/attn_bwd.hip): dqu, dqv, dK/dV into dqkv[:, d:], dppos.  DQ
+    recomputes the probabilities from the forward's per-row log-sum-exp `lse` (B, H, T); DKV / DPOS form
+    them from the forward's bf16 `p_tilde` and block maxima `m_blk` (attn_saved).  `parts` (ATTN_BWD_*)
+    issues a subset; parts issued on different streams must share a dedicated `ws`
     (relpos_attn_bwd_ws floats) and be ordered after ROWDOT."""
     rows, d = do.shape
     assert rows == B * T and qkv.shape == (rows, 3 * d) and lse.shape == (B, H, T)
+    if parts & (ATTN_BWD_DKV | ATTN_BWD_DPOS):
+        assert p_tilde is not None and p_tilde.dtype == torch.bfloat16 and p_tilde.shape == (B, H, T, T)
+        assert m_blk is not None and m_blk.shape == (B, H, T, (T + 63) // 64)
     assert dppos is None or dppos.shape == (2 * T - 1, d)
-    for t in (do, o, qu, qv, qkv, ppos, lse, dqu, dqv, dqkv, dppos):
+    for t in (do, o, qu, qv, qkv, ppos, lse, p_tilde, m_blk, dqu, dqv, dqkv, dppos):
         assert t is None or t.is_contiguous()
     assert o.shape == do.shape
     if parts != ATTN_BWD_ALL:
         assert ws is not None and ws.numel() >= relpos_attn_bwd_ws(B, H, T, d)
         call("kdfm_relpos_attn_bwd_parts", ptr(do), ptr(o), ptr(qu), ptr(qv), ptr(qkv), ptr(ppos), ptr(lse),
-             ptr(_i64(lengths)), ptr(dqu), ptr(dqv), ptr(dqkv), ptr(dppos), ptr(ws), ws.numel(), B, H, T, d,
-             float(scale), float(p), ptr(seed), int(rng_stream), int(parts), _s())
+             ptr(p_tilde), ptr(m_blk), ptr(_i64(lengths)), ptr(dqu), ptr(dqv), ptr(dqkv), ptr(dppos), ptr(ws),
+             ws.numel(), B, H, T, d, float(scale), float(p), ptr(seed), int(rng_stream), int(parts), _s())
         return
     ws = scratch(do.device, relpos_attn_bwd_ws(B, H, T, d))
-    # algorithmic: per (b, h) the products dP, dQu, dQv, dK, dV, dPpos (2 T^2 dk each, the positional band
-    # counted as one T x T) plus the score recompute (QK^T + band), bytes: dO, O, qu, qv, K, V read once,
-    # dqu, dqv, dK, dV written, lse read
+    # algorithmic: per (b, h) the products dP (twice: DQ and DKV / DPOS), dQu, dQv, dK, dV, dPpos (2 T^2 dk
+    # each, the positional band counted as one T x T) plus DQ's score recompute (QK^T + band); bytes: dO, O,
+    # qu, qv, K, V read once, dqu, dqv, dK, dV written, lse read, p~ read twice (DKV, DPOS)
     dk = d // H
-    fl = 2.0 * B * H * T * T * dk * 8
-    nb = 4.0 * rows * d * 10 + 4.0 * B * H * T
+    fl = 2.0 * B * H * T * T * dk * 9
+    nb = 4.0 * rows * d * 10 + 4.0 * B * H * T + 2.0 * 2.0 * B * H * T * T
     _traced("attn_bwd", fl, nb, "kdfm_relpos_attn_bwd", ptr(do), ptr(o), ptr(qu), ptr(qv), ptr(qkv), ptr(ppos),
-            ptr(lse), ptr(_i64(lengths)), ptr(dqu), ptr(dqv), ptr(dqkv), ptr(dppos), ptr(ws), ws.numel(), B, H, T, d,
-            float(scale), float(p), ptr(seed), int(rng_stream), _s())
+            ptr(lse), ptr(p_tilde), ptr(m_blk), ptr(_i64(lengths)), ptr(dqu), ptr(dqv), ptr(dqkv), ptr(dppos),
+            ptr(ws), ws.numel(), B, H, T, d, float(scale), float(p), ptr(seed), int(rng_stream), _s())
 
 
-def relpos_attn_fwd(qu, qv, qkv, ppos, lengths, o, P, Pd, B, H, T, scale, p, seed, rng_stream, lse=None):
+def relpos_attn_fwd(qu, qv, qkv, ppos, lengths, o, P, Pd, B, H, T, scale, p, seed, rng_stream, lse=None, p_tilde=None,
+                    m_blk=None):
     """Fused rel-pos MHA forward (bf16): P / Pd (B,H,T,T) written when given (two passes), else one
-    online-softmax pass that writes the per-row log-sum-exp `lse` (B,H,T) when given."""
+    online-softmax pass that writes the per-row log-sum-exp `lse` (B,H,T) and the backward's bf16
+    p~ / block maxima (attn_saved) when given."""
     rows, d = qu.shape
     assert rows == B * T and qkv.shape == (rows, 3 * d) and ppos.shape == (2 * T - 1, d) and o.shape == (rows, d)
     assert qu.is_contiguous() and qv.is_contiguous() and qkv.is_contiguous() and ppos.is_contiguous()
     assert lse is None or (lse.shape == (B, H, T) and P is None and Pd is None)
+    assert (p_tilde is None) == (m_blk is None)
+    if p_tilde is not None:
+        assert lse is not None and p_tilde.dtype == torch.bfloat16 and p_tilde.shape == (B, H, T, T)
+        assert m_blk.shape == (B, H, T, (T + 63) // 64) and p_tilde.is_contiguous() and m_blk.is_contiguous()
     # algorithmic: QK^T, the positional band (one T x T-equivalent) and PV, 2 T^2 dk FLOP each per (b, h);
-    # bytes: qu, qv, K, V, o once (+ P written when saved, + lse)
+    # bytes: qu, qv, K, V, o once (+ P written when saved, + lse, + p~ bf16)
     fl = 2.0 * B * H * T * T * (d // H) * 3
     nb = 4.0 * rows * d * 5 + (4.0 * B * H * T * T if P is not None else 0.0) + (4.0 * B * H * T if lse is not None
                                                                                  else 0.0)
+    nb += 2.0 * B * H * T * T if p_tilde is not None else 0.0
     _traced("attn_fwd", fl, nb, "kdfm_relpos_attn_fwd", ptr(qu), ptr(qv), ptr(qkv), ptr(ppos), ptr(_i64(lengths)),
-            ptr(o), ptr(P), ptr(Pd), ptr(lse), B, H, T, d, float(scale), float(p), ptr(seed), rng_stream, _s())
+            ptr(o), ptr(P), ptr(Pd), ptr(lse), ptr(p_tilde), ptr(m_blk), B, H, T, d, float(scale), float(p), ptr(seed),
+            rng_stream, _s())
 
 
 def relpos_softmax_fwd(ac, bd, lengths, P, Pd, B, H, T, scale, p, seed, rng_stream):
@@ -1277,9 +1296,20 @@ def fm_time_bwd(dc, evec, W1, dW1, db1, dw_te, db_te, L, E, steps):
 
 
 def adamw_noam(p, g, m, v, step, base_lr, d_model, warmup, min_lr, beta1, beta2, eps, wd, grad_scale, lr_out=None,
-               adam_base=None):
+               adam_base=None, gstats=None):
+    """Fused AdamW + Noam (csrc/optim.hip); with `gstats` (grad_stats' output) the update is skipped
+    when the gradient holds a non-finite value."""
     assert p.numel() == g.numel() == m.numel() == v.numel()
+    assert gstats is None or (gstats.numel() >= 2 and gstats.dtype == torch.float32)
     call("kdfm_adamw_noam", ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), ptr(step), ptr(adam_base), float(base_lr),
          float(d_model),
          float(warmup), float(min_lr), float(beta1), float(beta2), float(eps), float(wd), float(grad_scale),
-         ptr(lr_out), _s())
+         ptr(lr_out), ptr(gstats), _s())
+
+
+def grad_stats(g, scale, out2):
+    """out2 = [sum (scale g)^2 over finite entries, number of non-finite entries] (deterministic)."""
+    assert g.is_contiguous() and g.dtype == torch.float32 and out2.numel() >= 2
+    n = int(_lib.lib().kdfm_grad_stats_ws())
+    ws = scratch(g.device, n)
+    call("kdfm_grad_stats", ptr(g), g.numel(), float(scale), ptr(ws), ws.numel(), ptr(out2), _s())

@@ -52,6 +52,17 @@ class WgradOverlap:
         self._keep.extend(keep)
         self._pending = True
 
+    def stream_after_current(self):
+        """The side stream, ordered after all current main-stream work (None when weight gradients run
+        in line): the bucketed all-reduce issues its collectives from it, so they start after both the
+        main stream's and the side stream's gradient work without a stream of their own."""
+        if not self.enabled:
+            return None
+        dev = K.current_device()
+        side = self._stream(dev)
+        self._links[dev][0].after_current(side)
+        return side
+
     def fence(self, stream) -> None:
         """`stream` waits for every side-stream launch issued so far (no effect when none pending)."""
         if self._pending:

@@ -3,8 +3,10 @@ against (a) float64 torch autograd of NeMo's rel-pos attention (Appendix A.7: sc
 rel_shift((q+v)Ppos^T)) / sqrt(dk), key mask, softmax, rows of padded queries zeroed, O = P V) with
 no dropout, and (b) the unfused f32 path (dPd GEMM + relpos_softmax_bwd + five batched GEMMs) on
 the saved P of the two-pass forward with attention dropout 0.1 (same counter-RNG mask).  The fused
-backward itself reads no probabilities: it recomputes them from the single-pass forward's per-row
-log-sum-exp, which is checked against float64 too.
+backward reads no f32 probabilities: its dQ kernel recomputes them from the single-pass forward's
+per-row log-sum-exp, its dK/dV and dPpos kernels form P = p~ exp(m_blk - lse) from the forward's bf16
+unnormalised p~ and per-64-key-block running maxima; lse and that reconstruction are checked against
+float64 too (P: max |diff| <= 1e-2 * max P + 1e-3, bf16 p~).
 
 Tolerances: relative Frobenius error per gradient (dQu, dQv, dK, dV, dPpos) <= 2e-2 against float64
 (bf16 operands, f32 accumulation) and <= 2e-2 against the unfused f32 kernels; padded keys get
@@ -37,19 +39,20 @@ def _inputs(B, H, T, d, seed):
 
 
 def _fused(K, qkv, qu, qv, ppos, do, lens, B, H, T, d, p, seed):
-    """single-pass forward (O + lse), then the fused backward; returns (lse, O, grads...)"""
+    """single-pass forward (O + lse, p~, m_blk), then the fused backward; returns ((lse, p~, m_blk), O, grads...)"""
     dk = d // H
-    lse = torch.empty(B, H, T, device="cuda")
+    lse, pt, mblk = K.attn_saved(B, H, T, "cuda")
     o = torch.empty(B * T, d, device="cuda")
-    K.relpos_attn_fwd(qu, qv, qkv, ppos, lens, o, None, None, B, H, T, 1.0 / math.sqrt(dk), p, seed, 11, lse=lse)
+    K.relpos_attn_fwd(qu, qv, qkv, ppos, lens, o, None, None, B, H, T, 1.0 / math.sqrt(dk), p, seed, 11, lse=lse,
+                      p_tilde=pt, m_blk=mblk)
     dqu = torch.empty(B * T, d, device="cuda")
     dqv = torch.empty_like(dqu)
     dqkv = torch.zeros(B * T, 3 * d, device="cuda")
     dpos = torch.empty(2 * T - 1, d, device="cuda")
-    K.relpos_attn_bwd(do, o, qu, qv, qkv, ppos, lse, lens, dqu, dqv, dqkv, dpos, B, H, T, 1.0 / math.sqrt(dk), p,
-                      seed, 11)
+    K.relpos_attn_bwd(do, o, qu, qv, qkv, ppos, lse, pt, mblk, lens, dqu, dqv, dqkv, dpos, B, H, T,
+                      1.0 / math.sqrt(dk), p, seed, 11)
     torch.cuda.synchronize()
-    return lse, o, dqu, dqv, dqkv[:, d:2 * d], dqkv[:, 2 * d:], dpos
+    return (lse, pt, mblk), o, dqu, dqv, dqkv[:, d:2 * d], dqkv[:, 2 * d:], dpos
 
 
 def _torch_grads(qkv, qu, qv, ppos, do, lens, B, H, T, d):
@@ -67,6 +70,7 @@ def _torch_grads(qkv, qu, qv, ppos, do, lens, B, H, T, d):
     _torch_grads.lse = torch.logsumexp(s, -1).detach()
     P = torch.softmax(s, -1)
     P = torch.where(keym[:, None, :, None], P, torch.zeros_like(P))
+    _torch_grads.P = P.detach()
     O = (P @ sh(v)).permute(0, 2, 1, 3).reshape(B * T, d)
     loss = (O * do.double()).sum()
     return torch.autograd.grad(loss, [q_u, q_v, k, v, pp])
@@ -77,7 +81,7 @@ def test_attn_bwd_matches_float64(B, H, T, d):
     from kdfm import kernels as K
     qkv, qu, qv, ppos, do, lens = _inputs(B, H, T, d, T + d)
     seed = torch.tensor([99], dtype=torch.int64, device="cuda")
-    lse, _, dqu, dqv, dk_, dv_, dpos = _fused(K, qkv, qu, qv, ppos, do, lens, B, H, T, d, 0.0, seed)
+    (lse, pt, mblk), _, dqu, dqv, dk_, dv_, dpos = _fused(K, qkv, qu, qv, ppos, do, lens, B, H, T, d, 0.0, seed)
     ref = _torch_grads(qkv, qu, qv, ppos, do, lens, B, H, T, d)
     for name, got, want in zip(("dQu", "dQv", "dK", "dV", "dPpos"), (dqu, dqv, dk_, dv_, dpos), ref):
         assert _rel(got, want) <= 2e-2, (name, _rel(got, want))
@@ -89,6 +93,12 @@ def test_attn_bwd_matches_float64(B, H, T, d):
         assert err <= 2e-2 * max(1.0, want[bi, :, :L].abs().max().item()), (bi, err)
         if L < T:
             assert (lse[bi, :, L:] == 3.0e38).all()
+        # P = p~ exp(m_blk[key block] - lse) on the valid square
+        kb = torch.arange(L, device="cuda") // 64
+        prec = pt[bi, :, :L, :L].float() * torch.exp(mblk[bi, :, :L][:, :, kb] - lse[bi, :, :L, None])
+        pw = _torch_grads.P[bi, :, :L, :L]
+        perr = (prec.double() - pw).abs().max().item()
+        assert perr <= 1e-2 * pw.abs().max().item() + 1e-3, (bi, perr)
     # keys past an utterance's length receive no gradient
     for bi in range(B):
         L = int(lens[bi])
@@ -155,19 +165,19 @@ def test_attn_bwd_parts_on_two_streams_match_one_launch():
     seed = torch.tensor([77], dtype=torch.int64, device="cuda")
     qkv, qu, qv, ppos, do, lens = _inputs(B, H, T, d, 3)
     ref = _fused(K, qkv, qu, qv, ppos, do, lens, B, H, T, d, p, seed)
-    lse, o = ref[0], ref[1]
+    (lse, pt, mblk), o = ref[0], ref[1]
     dqu = torch.empty(B * T, d, device="cuda")
     dqv = torch.empty_like(dqu)
     dqkv = torch.zeros(B * T, 3 * d, device="cuda")
     dpos = torch.empty(2 * T - 1, d, device="cuda")
     ws = torch.empty(K.relpos_attn_bwd_ws(B, H, T, d), device="cuda")
     sc = 1.0 / math.sqrt(dk)
-    K.relpos_attn_bwd(do, o, qu, qv, qkv, ppos, lse, lens, dqu, dqv, dqkv, None, B, H, T, sc, p, seed, 11,
+    K.relpos_attn_bwd(do, o, qu, qv, qkv, ppos, lse, pt, mblk, lens, dqu, dqv, dqkv, None, B, H, T, sc, p, seed, 11,
                       parts=K.ATTN_BWD_ROWDOT | K.ATTN_BWD_DQ | K.ATTN_BWD_DKV, ws=ws)
     side = torch.cuda.Stream()
     side.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(side):
-        K.relpos_attn_bwd(do, o, qu, qv, qkv, ppos, lse, lens, None, None, None, dpos, B, H, T, sc, p, seed, 11,
+        K.relpos_attn_bwd(do, o, qu, qv, qkv, ppos, lse, pt, mblk, lens, None, None, None, dpos, B, H, T, sc, p, seed, 11,
                           parts=K.ATTN_BWD_DPOS, ws=ws)
     torch.cuda.current_stream().wait_stream(side)
     torch.cuda.synchronize()

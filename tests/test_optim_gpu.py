@@ -75,3 +75,44 @@ def test_adamw_noam_matches_torch(grad_scale, min_lr):
         torch.testing.assert_close(p.cpu(), ref.detach(), rtol=1e-5, atol=1e-6)
     if min_lr > 0.1:   # the clamp engaged after warmup
         assert lr_out.item() == pytest.approx(min_lr, rel=1e-6)
+
+
+def test_grad_stats_and_nonfinite_skip():
+    """kdfm_grad_stats: sum (scale g)^2 over finite entries and the non-finite count (float64 torch
+    reference, rtol 1e-5; bitwise-reproducible); kdfm_adamw_noam with gstats skips the update exactly
+    when a gradient entry is non-finite and still writes the step's learning rate."""
+    from kdfm import kernels as K
+    dev = torch.device("cuda")
+    g = torch.Generator().manual_seed(3)
+    n = 3_438_090   # the ver5 flat buffer (odd tail: the vector loop's scalar edge)
+    grad = torch.randn(n, generator=g).to(dev)
+    out = torch.zeros(2, device=dev)
+    K.grad_stats(grad, 0.5, out)
+    again = torch.zeros(2, device=dev)
+    K.grad_stats(grad, 0.5, again)
+    torch.cuda.synchronize()
+    want = (0.5 * grad.double()).pow(2).sum().item()
+    assert abs(out[0].item() - want) <= 1e-5 * want and out[1].item() == 0.0
+    assert torch.equal(out, again)
+    bad = grad.clone()
+    bad[17] = float("nan")
+    bad[n - 1] = float("inf")
+    K.grad_stats(bad, 1.0, out)
+    torch.cuda.synchronize()
+    assert out[1].item() == 2.0
+    want = bad.double()[torch.isfinite(bad)].pow(2).sum().item()
+    assert abs(out[0].item() - want) <= 1e-5 * want
+    # the skip: parameters / moments untouched, lr still written
+    p = torch.randn(n, generator=g).to(dev)
+    m = torch.zeros(n, device=dev)
+    v = torch.zeros(n, device=dev)
+    p0 = p.clone()
+    step = torch.tensor([5], dtype=torch.int64, device=dev)
+    lr = torch.zeros(1, device=dev)
+    K.adamw_noam(p, bad, m, v, step, 2.0, 176, 10, 1e-6, 0.9, 0.98, 1e-9, 1e-3, 1.0, lr_out=lr, gstats=out)
+    torch.cuda.synchronize()
+    assert torch.equal(p, p0) and m.abs().max().item() == 0.0 and lr.item() > 0.0
+    K.grad_stats(grad, 1.0, out)
+    K.adamw_noam(p, grad, m, v, step, 2.0, 176, 10, 1e-6, 0.9, 0.98, 1e-9, 1e-3, 1.0, lr_out=lr, gstats=out)
+    torch.cuda.synchronize()
+    assert not torch.equal(p, p0)

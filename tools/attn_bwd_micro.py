@@ -30,7 +30,7 @@ def main():
     lens[1::3] = T - 57
     seed = torch.tensor([7], dtype=torch.int64, device=dev)
     P = torch.empty(B, H, T, T, device=dev)
-    lse = torch.empty(B, H, T, device=dev)
+    lse, pt, mblk = K.attn_saved(B, H, T, dev)
     o = torch.empty(rows, d, device=dev)
     dqu = torch.empty(rows, d, device=dev)
     dqv = torch.empty_like(dqu)
@@ -41,14 +41,19 @@ def main():
     def fwd_p():
         K.relpos_attn_fwd(qu, qv, qkv, ppos, lens, o, P, None, B, H, T, sc, p, seed, 11)
 
-    def fwd():
+    def fwd_lse():
         K.relpos_attn_fwd(qu, qv, qkv, ppos, lens, o, None, None, B, H, T, sc, p, seed, 11, lse=lse)
 
-    def bwd():
-        K.relpos_attn_bwd(do, o, qu, qv, qkv, ppos, lse, lens, dqu, dqv, dqkv, dpos, B, H, T, sc, p, seed, 11)
+    def fwd():
+        K.relpos_attn_fwd(qu, qv, qkv, ppos, lens, o, None, None, B, H, T, sc, p, seed, 11, lse=lse, p_tilde=pt,
+                          m_blk=mblk)
 
-    for name, fn in (("relpos_attn_fwd (two-pass, P)", fwd_p), ("relpos_attn_fwd (one pass, lse)", fwd),
-                     ("relpos_attn_bwd (all kernels)", bwd)):
+    def bwd():
+        K.relpos_attn_bwd(do, o, qu, qv, qkv, ppos, lse, pt, mblk, lens, dqu, dqv, dqkv, dpos, B, H, T, sc, p, seed,
+                          11)
+
+    for name, fn in (("relpos_attn_fwd (two-pass, P)", fwd_p), ("relpos_attn_fwd (one pass, lse)", fwd_lse),
+                     ("relpos_attn_fwd (one pass, lse + p~)", fwd), ("relpos_attn_bwd (all kernels)", bwd)):
         for _ in range(3):
             fn()
         torch.cuda.synchronize()

@@ -503,8 +503,6 @@ def run(layers=3, batch=8, seconds=16.0, steps=2, ddp=True, deterministic=False,
                  eng._aux_stream().cuda_stream: "ctc_kl", 0: "null"}
         for k, st in WGRAD._side.items():
             roles[st.cuda_stream] = "wgrad"
-        if ar is not None and ar._comm is not None:
-            roles[ar._comm.cuda_stream] = "comm"
         roles[torch.cuda.current_stream().cuda_stream] = roles.get(torch.cuda.current_stream().cuda_stream, "caller")
         tr.roles.update(roles)
         tr.active = True
