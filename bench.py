@@ -74,8 +74,8 @@ def parse():
     ap.add_argument("--math", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0,
-                    help="host threads for the CPU baseline (default: every core this process may run on, "
-                         "len(os.sched_getaffinity(0)); os.cpu_count() is reported beside it)")
+                    help="host threads for the CPU baseline (default: every core this process may use, its "
+                         "affinity set capped by the cgroup CPU quota; os.cpu_count() is reported beside it)")
     ap.add_argument("--no-f32-sensitivity", action="store_true",
                     help="skip the --math f32 sensitivity measurement (the reference trains fp32)")
     ap.add_argument("--deterministic", action="store_true",
@@ -124,6 +124,15 @@ def _cgroup_cpu_max():
             return fh.read().strip()
     except OSError:
         return None
+
+
+def _usable_cpus():
+    n = len(os.sched_getaffinity(0))
+    q = _cgroup_cpu_max()
+    if q and not q.startswith("max"):
+        quota, period = (int(v) for v in q.split()[:2])
+        n = min(n, max(1, quota // period))
+    return n
 
 
 def _progress(msg):
@@ -348,14 +357,12 @@ def main():
         cpu = None
         _progress(f"timed {args.steps} steps: {1e3 * elapsed / args.steps:.3f} ms/step ({utt:.1f} utt/s)")
         if not args.no_cpu_baseline and world == 1:
-            # every core this process may run on (the GPU box's share of the host; os.cpu_count() is the
-            # whole machine and is reported beside it)
-            threads = args.cpu_threads or len(os.sched_getaffinity(0))
+            # every core this process may use: its affinity set capped by the cgroup CPU quota (the GPU
+            # box: 256 CPUs visible, cpu.max = 16 CPUs; 256 threads under that quota stall for minutes).
+            # os.cpu_count() (the whole machine) is reported beside it
+            threads = args.cpu_threads or _usable_cpus()
             cpu = cpu_baseline(threads, args.samples)
             cpu["cgroup_cpu_max"] = _cgroup_cpu_max()
-            if threads != 16:   # the box's per-GPU CPU share, kept beside the all-cores figure
-                c16 = cpu_baseline(16, args.samples, batches=(32,), steps=3)
-                cpu["at_16_threads"] = {"value": c16["value"], "cores": 16, "sample": c16["sample"]}
         f32 = v1024 = None
         if not args.no_f32_sensitivity and cfg.math == "bf16" and world == 1:
             _progress("f32 sensitivity")

@@ -159,6 +159,12 @@ int kdfm_wgrad_bf16(const uint16_t* dY, const uint16_t* X, float* dW, int64_t ld
  * gradient per segment: db[j][m] += alpha * sum_{r in segment j} dY[r][m] (db is (nseg, M), required),
  * dW summed over all rows -- the FM chain's first-layer weight over its S steps in one launch
  * (asr_train_diffm.py:1368-1427: W1 is shared by the steps, the time-conditioned bias is per step). */
+/* The same with the row count decided on the device: rows_dev[0] (<= rows, the capacity the launch and
+ * the workspace are planned for, kdfm_wgrad_bf16_ws(rows, ...)) rows take part; read at run time, so a
+ * producer kernel earlier on the stream may set it (kdfm_encfm_strategy's compact step saves). */
+int kdfm_wgrad_bf16_dev(const uint16_t* dY, const uint16_t* X, float* dW, int64_t ldc, float* db, int64_t rows,
+                        const int64_t* rows_dev, int64_t M, int64_t N, float alpha, float* ws, int64_t ws_len,
+                        void* stream);
 int64_t kdfm_wgrad_bf16_seg_ws(int64_t rows, int64_t M, int64_t N, int64_t seg_rows);
 int kdfm_wgrad_bf16_seg(const uint16_t* dY, const uint16_t* X, float* dW, int64_t ldc, float* db, int64_t seg_rows,
                         int64_t rows, int64_t M, int64_t N, float alpha, float* ws, int64_t ws_len, void* stream);
@@ -314,6 +320,67 @@ int kdfm_fm_chain_fwd(const float* x0, const float* zt, const float* W1, int64_t
 int kdfm_fm_chain_bwd(const float* dtr, const uint16_t* A, const float* gxS, const float* W1, int64_t ld_w1,
                       const float* W2, const float* Wst, uint16_t* DV, uint16_t* DA, float* gx0, int64_t n, int32_t L,
                       int32_t S, void* stream);
+/* Encoder-level flow matching with the dynamic step router (asr_train.py DistilFlowMatchingCTCModelBPE,
+ * use_flow_matching + use_dynamic_steps; DynamicStepRouter :1021-1218, FlowMatchingModule :1220-1377 with
+ * meta_encoder 'mlp' [Cs+32 -> 128 -> Cs], time_embed Linear(1, 32), shape_transform Linear(Cs, Ct), MSE; the
+ * per-layer loop of forward() :595-666).  All L hooked layers at once: rows are (layer, utterance, frame)
+ * = segment u = l*B + b of T frames, features (L*B*T, Cs) student / (L*B*T, Ct) teacher.
+ *   kdfm_encfm_time_prep:  c01 = [c0 | c1] (2 x 128): c0 = b1 + W1e b_te, c1 = W1e w_te (time bias c0 + t c1)
+ *   kdfm_encfm_router_fwd: per segment: time means sv, tv; hcat = [relu(Wsp sv + bsp) | relu(Wtp tv + btp) |
+ *     emb[l]] (288); h0 = relu(W0 hcat + b0) (128); logits = W2 h0 + b2 (K); probs = softmax (min_steps mask);
+ *     ent = -sum p log max(p, 1e-8); steps = argmax(logits + g) + 1 with g Gumbel(0,1) (the `gumbel` (U, K)
+ *     array, else counter RNG (seed, rng_stream)) when train, argmax(logits) + 1 otherwise
+ *   kdfm_encfm_strategy: per layer the flow step counts S[u] (0 batch_mode: smallest most frequent;
+ *     1 batch_avg: round-half-even of the mean, clamped to [1, K]; 2 batch_median: lower median; 3 group:
+ *     S[u] = steps[u]), the MSE weights inv[u] = 1 / (elements of the FM call the segment belongs to), the
+ *     compact save offsets off[u] = T * sum_{v<u} S[v] and rows_total = T * sum S; the router loss
+ *     rloss[l] = budget_weight (mean steps - budget_target)^2 - entropy_weight mean ent (train) and mean_steps[l]
+ *   kdfm_encfm_chain_fwd: per row (S = S[u]): x_0 = x0; for j < S, t = (S - j) / S:
+ *     a_j = relu(W1x x_j + c0 + t c1); v_j = W2 a_j + b2; x_{j+1} = x_j - v_j / S;
+ *     nsx = ca[S] x0 + cv[S] v_{S-1} (noise_scheduled_x at t = 1/S: (dalpha s - v) / (-dsigma));
+ *     d = Wst nsx + bst - tf; loss[l] += inv[u] sum d^2; dtr = 2 inv[u] d; rows >= xs_row0: xS = x_S;
+ *     saves (bf16, compact rows off[u] + j T + frame): X = [x_j | 1 | t | 0] (96 wide), A = a_j (128)
+ *   kdfm_encfm_chain_bwd: the data gradients: dnsx = Wst^T dtr; g = gxS (rows >= xs_row0) or 0;
+ *     j = S-1..0: dv_j = (j == S-1 ? cv dnsx : 0) - g / S; da_j = (W2^T dv_j) . [a_j > 0]; g += W1x^T da_j;
+ *     gx0 = g + ca dnsx + dsv[u] / T (the router's time-mean gradient, optional); saves DV (Cs), DA (128)
+ *     Weight gradients: kdfm_wgrad_bf16_dev(DA, X -> W1[:, :96] (dW1x | dc0 | dc1), rows_total) and
+ *     (DV, A -> W2, b2), the f32 row-parallel gradient of (dtr, nsx -> Wst, bst), then kdfm_encfm_time_bwd.
+ *   kdfm_encfm_router_bwd: dlogits = coef dH/dlogits (coef = -router_weight entropy_weight / B; the budget
+ *     term has no gradient), dh0 = W2^T dlogits . [h0 > 0], dhcat = W0^T dh0 (ReLU masks on the projections),
+ *     dsv = Wsp^T dhcat[:128]; weight gradients by the caller ((dlogits, h0), (dh0, hcat), (dhcat[:128], sv),
+ *     (dhcat[128:256], tv))
+ *   kdfm_encfm_time_bwd: from dW1's columns Cs (dc0) and Cs+1 (dc1): gb1 += dc0; gW1[:, Cs:] = dc0 b_te^T +
+ *     dc1 w_te^T (overwritten); gw_te += W1e^T dc1; gb_te += W1e^T dc0; gemb[l] += sum_b dhcat[u][256:288].
+ * Hidden widths fixed at 128 (FM and router), time / layer embeddings 32; Cs + 2 <= 96, Ct <= 192, steps <= 16.
+ * ca / cv: host arrays of the schedule coefficients for S = 1..max_steps. */
+int kdfm_encfm_time_prep(const float* W1, int64_t ld_w1, const float* b1, const float* w_te, const float* b_te,
+                         int32_t Cs, int32_t H, int32_t E, float* c01, void* stream);
+int kdfm_encfm_router_fwd(const float* s, const float* t, const float* Wsp, const float* bsp, const float* Wtp,
+                          const float* btp, const float* emb, const float* W0, const float* b0, const float* W2,
+                          const float* b2, const float* gumbel, const uint64_t* seed, uint64_t rng_stream,
+                          int32_t train, float* sv, float* tv, float* hcat, float* h0, float* probs, float* ent,
+                          int32_t* steps, int64_t L, int64_t B, int64_t T, int32_t Cs, int32_t Ct, int32_t K,
+                          int32_t P, int32_t E, int32_t min_steps, void* stream);
+int kdfm_encfm_strategy(const int32_t* steps, const float* ent, int32_t* S, float* inv, int64_t* off,
+                        int64_t* rows_total, float* rloss, float* mean_steps, int64_t L, int64_t B, int64_t T,
+                        int32_t K, int32_t Ct, int32_t strategy, float budget_target, float budget_weight,
+                        float entropy_weight, int32_t train, void* stream);
+int kdfm_encfm_chain_fwd(const float* x0, const float* tf, const int32_t* S, const float* inv, const int64_t* off,
+                         const float* W1, int64_t ld_w1, const float* c01, const float* W2, const float* b2,
+                         const float* Wst, const float* bst, const float* ca, const float* cv, int32_t max_steps,
+                         uint16_t* X, uint16_t* A, float* nsx, float* dtr, float* xS, int64_t xs_row0, float* loss,
+                         int64_t L, int64_t B, int64_t T, int32_t Cs, int32_t Ct, void* stream);
+int kdfm_encfm_chain_bwd(const float* dtr, const uint16_t* A, const float* gxS, int64_t xs_row0, const int32_t* S,
+                         const int64_t* off, const float* W1, int64_t ld_w1, const float* W2, const float* Wst,
+                         const float* ca, const float* cv, int32_t max_steps, const float* dsv, uint16_t* DV,
+                         uint16_t* DA, float* gx0, int64_t L, int64_t B, int64_t T, int32_t Cs, int32_t Ct,
+                         void* stream);
+int kdfm_encfm_router_bwd(const float* probs, const float* hcat, const float* h0, const float* W2, const float* W0,
+                          const float* Wsp, float coef, float* dlogits, float* dh0, float* dhcat, float* dsv,
+                          int64_t L, int64_t B, int32_t Cs, int32_t K, void* stream);
+int kdfm_encfm_time_bwd(float* gW1, int64_t ld_w1, float* gb1, const float* W1, const float* w_te, const float* b_te,
+                        float* gw_te, float* gb_te, const float* dhcat, float* gemb, int64_t L, int64_t B, int32_t Cs,
+                        void* stream);
 /* Fused SimpleDenoiser chain (asr_train_diffm.py:444-460: S steps of x <- x - net(x)/S, net =
  * Conv1d(L,L,3,p=1) -> ReLU -> Conv1d(L,L,3,p=1); bf16 MFMA, f32 state; L == 96) over n rows =
  * (n / T) utterances of T frames, channels-last.  W1 / W2: PyTorch Conv1d weights (L, L, 3) fp32.

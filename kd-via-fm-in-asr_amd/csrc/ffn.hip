@@ -20,8 +20,9 @@
 // (r, h) the features 8 q + 4 h + 0..3 of row r; one v_permlane32_swap per packed bf16 dword turns a
 // chunk's activation into the B operand of the next product (cdna_hip_programming.md T21).
 //
-// Work split: a workgroup owns 64 rows = 2 row tiles of 32.  Backward: the two waves of a tile take
-// the even and the odd hidden chunks.  Forward (d <= 96): NP = 4 waves per tile take the chunks
+// Work split: a workgroup owns 64 rows = 2 row tiles of 32.  Backward (d <= 96): NP = 4 waves per tile
+// take the chunks c = NP it + par (d = 176: NP = 2), their dLN partials added in a fixed order through
+// LDS like the forward's.  Forward (d <= 96): NP = 4 waves per tile take the chunks
 // c = NP it + par, so 12,832 rows give 1,604 waves (the kernel is latency bound: a wave's serial
 // chain of chunks sets the launch time and 201 workgroups fill at most 201 CUs); their partial
 // down-projections are added in the fixed order ((p0 + p1) + p2) + p3 through LDS at the end, and
@@ -41,6 +42,10 @@ constexpr int FF_ROWS = 64;       // rows per workgroup
 // its 96 accumulators do not fit the 256-register budget of 2 waves per SIMD)
 template <int DT> constexpr int fwd_np() { return DT <= 3 ? 4 : 2; }
 template <int DT> constexpr int fwd_nt() { return 2 * fwd_np<DT>() * 64; }
+// backward: the same split (d <= 96: 4 chunk parities per row tile, 8 waves; a wave's serial chain of
+// chunks is what bounds the launch at ~1 wave per SIMD); d = 176 keeps 2 (its 18 + 12 KB chunk stages)
+template <int DT> constexpr int bwd_np() { return DT <= 3 ? 4 : 2; }
+template <int DT> constexpr int bwd_nt() { return 2 * bwd_np<DT>() * 64; }
 
 // Chunk image (one 32-feature slice of the hidden width), fragment order:
 //   W2c(mt, ks2) = 2 mt + ks2            A of the down-projection (d rows x 32 hidden)     [fwd]
@@ -82,12 +87,14 @@ struct FfnFwd {
   const float* ln_g; const float* ln_b; float ln_eps; float* ln_out; float* ln_mean; float* ln_rstd;
 };
 
-// bytes of the weight-stage region (double-buffered 2-chunk stages, reused for the final reduction);
-// the per-feature vectors (biases) follow it in LDS: a global bias load inside the chunk loop would
-// wait (in-order vmcnt) for the next stage's prefetch and expose its latency every iteration
+// bytes of the backward's weight-stage region (double-buffered NP-chunk stages, reused for the final
+// reduction of the NP - 1 partials per tile); the per-feature vectors (biases) follow it in LDS: a global
+// bias load inside the chunk loop would wait (in-order vmcnt) for the next stage's prefetch and expose
+// its latency every iteration
 template <int SF, int DT>
 constexpr int ffn_stage_bytes() {
-  return 4 * SF * 1024 > 2 * DT * 16 * 64 * 4 ? 4 * SF * 1024 : 2 * DT * 16 * 64 * 4;
+  constexpr int NP = bwd_np<DT>();
+  return 2 * NP * SF * 1024 > 2 * (NP - 1) * DT * 16 * 64 * 4 ? 2 * NP * SF * 1024 : 2 * (NP - 1) * DT * 16 * 64 * 4;
 }
 // forward: two stages of NP chunks, or the NP - 1 partials per tile of the final reduction
 template <int SF, int DT>
@@ -282,11 +289,12 @@ struct FfnBwd {
 };
 
 template <int KS1, int DT>
-__global__ __launch_bounds__(FF_NT) void ffn_bwd_kernel(FfnBwd a) {
+__global__ __launch_bounds__(bwd_nt<DT>()) void ffn_bwd_kernel(FfnBwd a) {
   using G = FfnGeo<KS1, DT>;
+  constexpr int NP = bwd_np<DT>(), NT = bwd_nt<DT>();
   extern __shared__ __attribute__((aligned(16))) uint4 ff_lds[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int h = lane >> 5, par = wave & 1, tile = wave >> 1;
+  const int h = lane >> 5, par = wave % NP, tile = wave / NP;
   const int64_t row = (int64_t)blockIdx.x * FF_ROWS + tile * 32 + (lane & 31);
   const bool ok = row < a.rows;
   const int d = a.d, ff = a.ff, FC = ff / 32;
@@ -294,7 +302,7 @@ __global__ __launch_bounds__(FF_NT) void ffn_bwd_kernel(FfnBwd a) {
   const uint64_t kact = rng_key(seed, a.st_act), kout = rng_key(seed, a.st_out);
   const float ks_act = 1.f / (1.f - a.p_act), ks_out = 1.f / (1.f - a.p_out);
 
-  Stager<G::BWD, 2 * DT, G::CS, 2, FF_NT> stg;
+  Stager<G::BWD, 2 * DT, G::CS, NP, NT> stg;
   const uint4* img = reinterpret_cast<const uint4*>(a.img);
   stg.load(img, 0, FC);
 
@@ -331,15 +339,15 @@ __global__ __launch_bounds__(FF_NT) void ffn_bwd_kernel(FfnBwd a) {
     for (int i = 0; i < 16; ++i) acc[mt][i] = 0.f;
 
   float* bias_s = reinterpret_cast<float*>(reinterpret_cast<char*>(ff_lds) + ffn_stage_bytes<G::BWD, DT>());
-  for (int e = threadIdx.x; e < ff; e += FF_NT) bias_s[e] = a.b1[e];
+  for (int e = threadIdx.x; e < ff; e += NT) bias_s[e] = a.b1[e];
   stg.store(ff_lds, 0);
   __syncthreads();
-  const int nit = (FC + 1) / 2;
+  const int nit = (FC + NP - 1) / NP;
   for (int it = 0; it < nit; ++it) {
     if (it + 1 < nit) stg.load(img, it + 1, FC);
-    const int c = 2 * it + par;
+    const int c = NP * it + par;
     if (c < FC) {
-      const uint4* W = ff_lds + ((it & 1) * 2 + par) * G::BWD * FRAG_U4;   // W1c | W2Tc | W1Tc
+      const uint4* W = ff_lds + ((it & 1) * NP + par) * G::BWD * FRAG_U4;   // W1c | W2Tc | W1Tc
       f32x16 hacc, gacc;
 #pragma unroll
       for (int i = 0; i < 16; ++i) hacc[i] = gacc[i] = 0.f;
@@ -398,20 +406,28 @@ __global__ __launch_bounds__(FF_NT) void ffn_bwd_kernel(FfnBwd a) {
     if (it + 1 < nit) stg.store(ff_lds, (it + 1) & 1);
     __syncthreads();
   }
-  float* red = reinterpret_cast<float*>(ff_lds) + tile * (DT * 16 * 64);
-  if (par == 1) {
+  // partials of parities 1..NP-1 -> parity 0, added in the fixed order ((p0 + p1) + p2) + p3
+  float* red = reinterpret_cast<float*>(ff_lds) + tile * ((NP - 1) * DT * 16 * 64);
+  if (par != 0) {
+    float* mine = red + (par - 1) * (DT * 16 * 64);
 #pragma unroll
     for (int mt = 0; mt < DT; ++mt)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) red[(mt * 16 + i) * 64 + lane] = acc[mt][i];
+      for (int i = 0; i < 16; ++i) mine[(mt * 16 + i) * 64 + lane] = acc[mt][i];
   }
   __syncthreads();
-  if (par == 1) return;
+  if (par != 0) return;
   float dl[DT * 16];
 #pragma unroll
   for (int mt = 0; mt < DT; ++mt)
 #pragma unroll
-    for (int e = 0; e < 16; ++e) dl[mt * 16 + e] = acc[mt][e] + red[(mt * 16 + e) * 64 + lane];
+    for (int e = 0; e < 16; ++e) dl[mt * 16 + e] = acc[mt][e];
+#pragma unroll
+  for (int q = 1; q < NP; ++q)
+#pragma unroll
+    for (int mt = 0; mt < DT; ++mt)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) dl[mt * 16 + e] += red[((q - 1) * DT * 16 + mt * 16 + e) * 64 + lane];
   ln_backward_rows<DT>(dl, a.x, a.g, a.dout, a.dx, a.part, a.nparts, (int64_t)blockIdx.x * FF_ROWS + tile * 32, row, ok,
                        d, mean, rstd, lane);
 }
@@ -440,7 +456,8 @@ int launch_bwd(const FfnBwd& a, hipStream_t st) {
   static bool once = (ffn_allow_lds(ffn_bwd_kernel<KS1, DT>), true);
   (void)once;
   const size_t lds = (size_t)ffn_stage_bytes<G::BWD, DT>() + (size_t)a.ff * 4;
-  hipLaunchKernelGGL((ffn_bwd_kernel<KS1, DT>), dim3((unsigned)ceil_div(a.rows, FF_ROWS)), dim3(FF_NT), lds, st, a);
+  hipLaunchKernelGGL((ffn_bwd_kernel<KS1, DT>), dim3((unsigned)ceil_div(a.rows, FF_ROWS)), dim3(bwd_nt<DT>()), lds, st,
+                     a);
   return check_launch("kdfm_ffn_bwd");
 }
 

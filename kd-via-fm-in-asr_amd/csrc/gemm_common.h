@@ -27,7 +27,8 @@ struct GemmP {
   float* ws; int64_t ws_len;
   const uint16_t* Bh; int64_t sBh;
   int partial;  // deterministic split-K: ATOMIC tiles store raw partials to ws[split][m][n] (folded in order)
-  int nseg; int64_t seg_rows;  // row-parallel wgrad: per-segment bias columns ones_col .. ones_col + nseg - 1
+  int nseg; int64_t seg_rows;  // row-parallel wgrad: per-segment bias columns ones_col .. one_col + nseg - 1
+  const int64_t* k_dev;        // row-parallel wgrad: device-side row count (<= K) read at run time (NULL: K)
 };
 
 // Non-atomic epilogue for one output element.  v = alpha * acc (already scaled).  bz = batch

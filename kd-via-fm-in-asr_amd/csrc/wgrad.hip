@@ -72,6 +72,10 @@ __global__ __launch_bounds__(WR_NT, 2) void wgr_kernel(GemmP p, WrGeo g) {
   const int64_t kb = split * g.steps_per * 32;
   int64_t ke = kb + g.steps_per * 32;
   if (ke > p.K) ke = p.K;
+  if (p.k_dev) {   // rows decided on the device (compact step saves): the plan covers the capacity K
+    const int64_t kd = *p.k_dev;
+    if (ke > kd) ke = kd;
+  }
   // B memory columns of this slice and the slab's staging units (4 rows x 4 columns each)
   const int ncols_mem = (int)((g.nmem - n0 < g.Nb) ? g.nmem - n0 : g.Nb);
   const int units = 8 * ((mcols >> CWS) + (ncols_mem >> CWS));
@@ -627,6 +631,20 @@ int kdfm_wgrad_bf16(const uint16_t* dY, const uint16_t* X, float* dW, int64_t ld
   KDFM_REQUIRE(((((uintptr_t)dY) | ((uintptr_t)X)) & 15) == 0, "operands must be 16-byte aligned");
   KDFM_REQUIRE(ldc >= N, "ldc < N");
   GemmP p = wgrad_bf16_params(dY, X, dW, ldc, db, rows, M, N, alpha, ws, ws_len);
+  return wgrad_bf16_run(p, KDFM_LD_XC, as_stream(stream));
+}
+
+int kdfm_wgrad_bf16_dev(const uint16_t* dY, const uint16_t* X, float* dW, int64_t ldc, float* db, int64_t rows,
+                        const int64_t* rows_dev, int64_t M, int64_t N, float alpha, float* ws, int64_t ws_len,
+                        void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(rows_dev, "rows_dev is required (kdfm_wgrad_bf16 for a host row count)");
+  KDFM_REQUIRE(dY && X && dW && ws, "null pointer");
+  KDFM_REQUIRE(rows > 0 && M > 0 && N > 0 && M % 4 == 0 && N % 4 == 0, "M, N must be positive multiples of 4");
+  KDFM_REQUIRE(ldc >= N, "ldc < N");
+  KDFM_REQUIRE(ws_len >= kdfm_wgrad_bf16_ws(rows, M, N, db ? 1 : 0), "workspace too small (kdfm_wgrad_bf16_ws)");
+  GemmP p = wgrad_bf16_params(dY, X, dW, ldc, db, rows, M, N, alpha, ws, ws_len);
+  p.k_dev = rows_dev;
   return wgrad_bf16_run(p, KDFM_LD_XC, as_stream(stream));
 }
 

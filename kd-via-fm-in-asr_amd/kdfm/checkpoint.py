@@ -29,7 +29,7 @@ import yaml
 TEACHER_MAP = (("encoder.", "teacher.encoder."), ("decoder.", "teacher.decoder."),
                ("preprocessor.", "teacher.preprocessor."))
 _IGNORED_SUFFIXES = ("num_batches_tracked",)
-_HEAD_PREFIXES = ("tae.", "sproj.", "adapter.", "denoiser.", "fm_latent.", "fm_latent_2.", "diffkd.")
+_HEAD_PREFIXES = ("tae.", "sproj.", "adapter.", "denoiser.", "fm_latent.", "fm_latent_2.", "diffkd.", "flow_matching.", "router.")
 
 
 def _fb_nemo(fb: torch.Tensor) -> torch.Tensor:

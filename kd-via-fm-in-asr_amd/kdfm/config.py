@@ -48,6 +48,20 @@ class Ver5Config:
     use_diffkd: bool = False
     diffkd_steps: int = 9
     time_embed_dim: int = 32
+    # model family: "diffm" = asr_train_diffm.py's latent KD heads (model versions 1-8 above);
+    # "encfm" = asr_train.py's encoder-level flow matching on every hooked layer pair with the
+    # DynamicStepRouter (use_flow_matching, :469-666, 1021-1377): per-layer step counts from the router
+    # (encfm_dynamic, the --use_dynamic_steps path) turned into FM calls by encfm_strategy
+    # (--router_strategy), or fixed per layer (encfm_steps_per_layer = --sampling_steps_per_layer);
+    # router_max_steps = --router_max_sampling_steps, router_weight = --router_weight,
+    # flow_schedule = --flow_schedule (rectified | vp_ode)
+    kd_model: str = "diffm"
+    encfm_strategy: str = "batch_mode"
+    encfm_dynamic: bool = True
+    encfm_steps_per_layer: tuple = None
+    router_max_steps: int = 8
+    router_weight: float = 1.0
+    flow_schedule: str = "rectified"
     kd_alpha: float = 0.1
     kd_temperature: float = 1.0
     # regularisation (conformer_ctc_bpe.yaml:150-153)
@@ -210,7 +224,39 @@ def head_modules(cfg: Ver5Config) -> tuple:
     return tuple(mods)
 
 
+ENCFM_HIDDEN = 128     # FlowMatchingModule hidden_dim (asr_train.py:1753); the router's proj / hidden widths
+ENCFM_ROUTER_EMB = 32  # DynamicStepRouter layer_emb_dim (:514)
+
+
+def encfm_specs(cfg: Ver5Config, trained: bool = True) -> list:
+    """Parameters of the encoder-level FM family, named as the reference module tree.  trained:
+    flow_matching.* and (dynamic steps) router.*; else the ones the reference builds but never trains:
+    layer_proj (built whenever flow matching is on, asr_train.py:525-529, used only by layerwise KD) and
+    the router when the step counts are fixed."""
+    Cs, Ct, E, H = cfg.d_student, cfg.d_teacher, cfg.time_embed_dim, ENCFM_HIDDEN
+    fm = "flow_matching."
+    fm_specs = [(fm + "time_embed.weight", (E, 1)), (fm + "time_embed.bias", (E,)),
+                (fm + "meta_encoder.0.weight", (H, Cs + E)), (fm + "meta_encoder.0.bias", (H,)),
+                (fm + "meta_encoder.2.weight", (Cs, H)), (fm + "meta_encoder.2.bias", (Cs,)),
+                (fm + "shape_transformation_function.weight", (Ct, Cs)),
+                (fm + "shape_transformation_function.bias", (Ct,))]
+    r = "router."
+    router_specs = [(r + "stu_proj.0.weight", (H, Cs)), (r + "stu_proj.0.bias", (H,)),
+                    (r + "tch_proj.0.weight", (H, Ct)), (r + "tch_proj.0.bias", (H,)),
+                    (r + "layer_emb.weight", (cfg.n_layers, ENCFM_ROUTER_EMB)),
+                    (r + "router.0.weight", (H, 2 * H + ENCFM_ROUTER_EMB)), (r + "router.0.bias", (H,)),
+                    (r + "router.2.weight", (cfg.router_max_steps, H)), (r + "router.2.bias", (cfg.router_max_steps,))]
+    if trained:
+        return fm_specs + (router_specs if cfg.encfm_dynamic else [])
+    return (router_specs if not cfg.encfm_dynamic else []) + [("layer_proj.weight", (Ct, Cs)),
+                                                              ("layer_proj.bias", (Ct,))]
+
+
 def head_specs(cfg: Ver5Config, fm_prefixes=None) -> list:
+    if cfg.kd_model == "encfm":
+        return encfm_specs(cfg, True)
+    if cfg.kd_model != "diffm":
+        raise ValueError(f"kd_model must be 'diffm' or 'encfm', got {cfg.kd_model!r}")
     L, Ct, Cs, E = cfg.latent, cfg.d_teacher, cfg.d_student, cfg.time_embed_dim
     mods = head_modules(cfg)
     s = [("tae.enc.weight", (L, Ct, 1)), ("tae.enc.bias", (L,)),
@@ -248,6 +294,8 @@ def all_head_specs(cfg: Ver5Config) -> list:
     """Every KD head the reference module builds, whatever the version (asr_train_diffm.py:559-564):
     version 6 uses all of them."""
     from dataclasses import replace
+    if cfg.kd_model == "encfm":
+        return encfm_specs(cfg, True) + encfm_specs(cfg, False)
     return head_specs(replace(cfg, version=6))
 
 
@@ -282,5 +330,5 @@ DEFAULT = Ver5Config()
 PARITY = DEFAULT.parity()
 
 __all__ = ["Ver5Config", "DEFAULT", "PARITY", "encoder_specs", "subsampling_specs", "sub_stages", "sub_pad",
-           "sub_channels", "sub_len", "sub_dims", "decoder_specs", "head_specs", "all_head_specs", "diffkd_specs", "head_modules", "student_specs",
+           "sub_channels", "sub_len", "sub_dims", "decoder_specs", "head_specs", "all_head_specs", "diffkd_specs", "encfm_specs", "head_modules", "student_specs",
            "teacher_specs", "bn_buffer_specs", "fused_groups", "field"]

@@ -18,6 +18,7 @@ from .config import Ver5Config, all_head_specs, bn_buffer_specs, diffkd_specs, s
 from .conformer import EncoderRun, EncoderShapes, compute_lengths, encoder_backward, encoder_forward, \
     encoder_forward_steps, layer_images, make_workspace
 from .frontend import FrontendConsts, frontend_forward, mel_frames, specaugment_
+from .encfm import EncFMWorkspace, encfm_backward, encfm_forward
 from .heads import HeadsWorkspace, heads_backward, heads_forward
 from .overlap import WGRAD
 
@@ -108,6 +109,11 @@ class Ver5Engine:
         # config (in line exactly when deterministic); the overlapped-vs-serialised determinism test
         # forces both with ordered reductions
         self.overlap_wgrad = None
+        # encoder-level FM (kd_model "encfm"): optional injected router Gumbel noise (L*B, K) for parity
+        # runs, the per-(B, T) workspaces, and the last step's [flow, router, total, mean steps] stats
+        self.encfm_gumbel = None
+        self._encfm = {}
+        self.encfm_stats = None
         # capture the frozen teacher as a HIP graph in training steps (KDFM_TEACHER_GRAPH=0: eager)
         self.teacher_graph = __import__("os").environ.get("KDFM_TEACHER_GRAPH", "0") == "1"
         if init:
@@ -146,6 +152,12 @@ class Ver5Engine:
             K.relpos_table(T, d, pe)
             self._pos[key] = pe
         return self._pos[key]
+
+    def _encfm_ws(self, B, T):
+        ws = self._encfm.get((B, T))
+        if ws is None:
+            ws = self._encfm[(B, T)] = EncFMWorkspace(self.cfg, B, T, self.device)
+        return ws
 
     def _side_stream(self):
         if getattr(self, "_side", None) is None:
@@ -315,12 +327,24 @@ class Ver5Engine:
             for t in (tfeats, tlogits, mel_t, mel_len, len1, len2):
                 t.record_stream(side)
         # ---- decoders, CTC, logit KD ----
+        encfm = cfg.kd_model == "encfm"
+        dec_in = sfeats[-1]
+        if encfm:
+            # asr_train.py: the router + flow matching over every hooked layer pair (it needs the teacher's
+            # features), and the decoder reads the last layer's FM output (:595-666)
+            main.wait_stream(side)
+            ews = self._encfm_ws(B, T)
+            with K.region("encfm_forward"):
+                dec_in = encfm_forward(cfg, self.student.P, sfeats, tfeats, ews, seed=seed, train=train,
+                                       gumbel=self.encfm_gumbel)
+            self.encfm_stats = ews.stats
         logits = torch.empty(rows, Cn, device=dev)
-        K.linear(sfeats[-1], self.student.P["decoder.decoder_layers.0.weight"].view(Cn, Ss.d),
+        K.linear(dec_in, self.student.P["decoder.decoder_layers.0.weight"].view(Cn, Ss.d),
                  self.student.P["decoder.decoder_layers.0.bias"], logits)
         lp = torch.empty(rows, Cn, device=dev)
         K.log_softmax(logits, lp)
-        main.wait_stream(side)
+        if not encfm:
+            main.wait_stream(side)
         # ---- CTC + logit KD on a third stream: they only need the two logit tensors, and their
         # result is first needed after the KD heads' forward, so the serial CTC recursion overlaps it ----
         # kl | recon, kd_pre, fm_pre, kd_post, fm_post (heads.RECON..FM_POST) | diffkd | sum of the layer-KD
@@ -342,14 +366,20 @@ class Ver5Engine:
             t.record_stream(aux)
         # ---- ver5 heads over all layers at once ----
         n = cfg.n_layers * rows
-        with K.region("heads_forward"):
-            hctx = heads_forward(cfg, self.student.P, sfeats.view(n, Ss.d), tfeats.view(n, St.d), T, self.hws,
-                                 acc[1:6], seed=seed, eps=eps, save=save, Pfix=self.fixed.P, acc_diffkd=acc[6:7])
-            K.colsum(acc[2:7].view(5, 1), acc[7:8], accumulate=False)
+        if encfm:
+            hctx = None
+            K.axpby(ews.stats[2:3].view(1, 1), None, acc[7:8].view(1, 1), 1.0, 0.0)   # forward's total_loss
+        else:
+            with K.region("heads_forward"):
+                hctx = heads_forward(cfg, self.student.P, sfeats.view(n, Ss.d), tfeats.view(n, St.d), T, self.hws,
+                                     acc[1:6], seed=seed, eps=eps, save=save, Pfix=self.fixed.P,
+                                     acc_diffkd=acc[6:7])
+                K.colsum(acc[2:7].view(5, 1), acc[7:8], accumulate=False)
         # device (recon, kd_pre, fm_pre, kd_post, fm_post, diffkd): the v/* log keys
         self.kd_terms = acc[1:7]
         ctx = dict(B=B, T=T, Ss=Ss, St=St, mel_len=mel_len, len1=len1, len2=len2, srun=srun, sfeats=sfeats,
-                   glogits=glogits, hctx=hctx, lp=lp, nll=nll, pos_s=pos_s, acc=acc)
+                   glogits=glogits, hctx=hctx, lp=lp, nll=nll, pos_s=pos_s, acc=acc, dec_in=dec_in,
+                   ews=ews if encfm else None)
         self._join_losses(ctx)   # CTC/KL overlapped the heads forward; losses valid after forward()
         return ctx
 
@@ -435,18 +465,31 @@ class Ver5Engine:
         n = cfg.n_layers * Ss.rows
         self.student.zero_grad()
         dfeats = torch.empty(cfg.n_layers, Ss.rows, Ss.d, device=self.device)
-        with K.region("heads_backward"):
-            heads_backward(cfg, P, G, ctx.pop("hctx"), self.hws, dfeats.view(n, Ss.d), seed=self.seed)
         dec0 = off["decoder.decoder_layers.0.weight"]
-        if grad_ready is not None:
-            grad_ready(min(o for k, o in off.items() if not k.startswith(("encoder.", "decoder."))))
-        # decoder: logits = W enc + b ; grad wrt logits from CTC + KL
         g = ctx.pop("glogits")
         Cn = cfg.classes
         Wd = P["decoder.decoder_layers.0.weight"].view(Cn, Ss.d)
-        K.linear_dw(g, ctx["sfeats"][-1], G["decoder.decoder_layers.0.weight"].view(Cn, Ss.d), db=G["decoder.decoder_layers.0.bias"])
-        K.linear_dx(g, Wd, dfeats[-1], R=dfeats[-1], rscale=1.0)
-        del g
+        if cfg.kd_model == "encfm":
+            # decoder first: its input is the last layer's FM output, whose gradient the FM backward needs
+            ews = ctx.pop("ews")
+            K.linear_dw(g, ctx["dec_in"], G["decoder.decoder_layers.0.weight"].view(Cn, Ss.d),
+                        db=G["decoder.decoder_layers.0.bias"])
+            K.linear_dx(g, Wd, ews.gxS)
+            del g
+            with K.region("encfm_backward"):
+                encfm_backward(cfg, P, G, ews, dfeats.view(n, Ss.d), ews.gxS, WGRAD.run)
+            if grad_ready is not None:
+                grad_ready(min(o for k, o in off.items() if not k.startswith(("encoder.", "decoder."))))
+        else:
+            with K.region("heads_backward"):
+                heads_backward(cfg, P, G, ctx.pop("hctx"), self.hws, dfeats.view(n, Ss.d), seed=self.seed)
+            if grad_ready is not None:
+                grad_ready(min(o for k, o in off.items() if not k.startswith(("encoder.", "decoder."))))
+            # decoder: logits = W enc + b ; grad wrt logits from CTC + KL
+            K.linear_dw(g, ctx["sfeats"][-1], G["decoder.decoder_layers.0.weight"].view(Cn, Ss.d),
+                        db=G["decoder.decoder_layers.0.bias"])
+            K.linear_dx(g, Wd, dfeats[-1], R=dfeats[-1], rscale=1.0)
+            del g
         layer_done = None
         if grad_ready is not None:
             grad_ready(min(dec0, off["decoder.decoder_layers.0.bias"]))

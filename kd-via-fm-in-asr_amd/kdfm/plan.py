@@ -15,7 +15,11 @@ captured HIP graph removes the host cost but on this ROCm loses the cross-stream
     events re-recorded / waited through libkdfm's thin hipEventRecord / hipStreamWaitEvent wrappers.
 
 Everything the step computes from changing state reads it on the device (RNG seed, step counter,
-Noam learning rate, the inputs' static buffers), so a replay is the step.  Torch ops that touch
+Noam learning rate, the inputs' static buffers), so a replay is the step.  The library's one
+process-global launch setting, the deterministic-reduction mode (kdfm_set_deterministic: it picks
+ordered or atomic reduction routes at launch time), is recorded with every launch and re-applied
+around it on replay, so a plan recorded in deterministic mode replays the ordered kernels whatever
+mode the caller is in.  Torch ops that touch
 memory inside the recorded step are restricted to fills (replayed as kdfm_fill); anything else raises
 at record time, so a plan is never silently incomplete.
 """
@@ -71,10 +75,11 @@ class _Recorder(TorchDispatchMode):
                 self.plan._bad.append(f"{func} on a non-contiguous tensor")
             elif val == 0.0:   # zero fill of any dtype: a memset of its bytes
                 self.plan.ops.append(("k", self.plan._fn("kdfm_memset_async"),
-                                      (tgt.data_ptr(), 0, tgt.numel() * tgt.element_size(), K.stream_ptr())))
+                                      (tgt.data_ptr(), 0, tgt.numel() * tgt.element_size(), K.stream_ptr()),
+                                      K.get_deterministic()))
             elif tgt.dtype == torch.float32:
                 self.plan.ops.append(("k", self.plan._fn("kdfm_fill"), (tgt.data_ptr(), val, tgt.numel(),
-                                                                        K.stream_ptr())))
+                                                                        K.stream_ptr()), K.get_deterministic()))
             else:
                 self.plan._bad.append(f"{func} = {val} on {tgt.dtype}")
             return out
@@ -86,7 +91,7 @@ class StepPlan:
     """Record `fn()` (one training step, device work only) once; `replay()` re-issues it."""
 
     def __init__(self):
-        self.ops = []      # ("k", ctypes fn, args) | ("er", event, stream) | ("ew", event, stream) | ("py", callable)
+        self.ops = []      # ("k", ctypes fn, args, det) | ("er", event, stream) | ("ew", event, stream) | ("py", fn, args)
         self.keep = []     # every tensor / event / descriptor the recorded launches address
         self._bad = []
         self._paused = False
@@ -127,7 +132,7 @@ class StepPlan:
                 plan.keep.append(buf)
                 args = (C.cast(buf, C.POINTER(_lib.GemmDesc)),) + tuple(args[1:])
             plan.keep.append(args)
-            plan.ops.append(("k", plan._fn(name), args))
+            plan.ops.append(("k", plan._fn(name), args, K.get_deterministic()))
 
         def record_ev(self_ev, stream=None):
             e_record(self_ev, stream)
@@ -164,22 +169,31 @@ class StepPlan:
     # ---- replay ---------------------------------------------------------------------------------
     def replay(self):
         rec, wt = self._ev_record, self._ev_wait
-        for op in self.ops:
-            kind = op[0]
-            if kind == "k":
-                rc = op[1](*op[2])
-                if rc:
-                    _lib.check(rc, "plan replay")
-            elif kind == "er":
-                rc = rec(op[1], op[2])
-                if rc:
-                    _lib.check(rc, "plan replay (event record)")
-            elif kind == "ew":
-                rc = wt(op[2], op[1])
-                if rc:
-                    _lib.check(rc, "plan replay (stream wait)")
-            else:
-                op[1](*op[2])
+        saved = K.get_deterministic()
+        det = saved
+        try:
+            for op in self.ops:
+                kind = op[0]
+                if kind == "k":
+                    if op[3] != det:
+                        det = op[3]
+                        K.set_deterministic(det)
+                    rc = op[1](*op[2])
+                    if rc:
+                        _lib.check(rc, "plan replay")
+                elif kind == "er":
+                    rc = rec(op[1], op[2])
+                    if rc:
+                        _lib.check(rc, "plan replay (event record)")
+                elif kind == "ew":
+                    rc = wt(op[2], op[1])
+                    if rc:
+                        _lib.check(rc, "plan replay (stream wait)")
+                else:
+                    op[1](*op[2])
+        finally:
+            if det != saved:
+                K.set_deterministic(saved)
 
     def __len__(self):
         return len(self.ops)

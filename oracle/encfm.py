@@ -1,0 +1,164 @@
+"""CPU oracle (TEST INFRASTRUCTURE ONLY -- never imported by the product path) for the ENCODER-LEVEL
+flow matching of asr_train.py's DistilFlowMatchingCTCModelBPE (use_flow_matching=True,
+use_dynamic_steps=True): the DynamicStepRouter, the step-count strategies and the FlowMatchingModule
+applied to every hooked Conformer layer, plus the decoder reading the last layer's FM output.
+
+A plain-PyTorch restatement (autograd supplies the gradients), pinned by tests/golden/kd_encfm.npz,
+which make_golden_encfm.py produced from the reference's own DynamicStepRouter / FlowMatchingModule
+classes (tests/test_oracle_encfm.py).  Citations are /root/reference/asr_train.py line numbers.
+
+Parameter names follow the reference module tree: flow_matching.{time_embed, meta_encoder.0,
+meta_encoder.2, shape_transformation_function}.*, router.{stu_proj.0, tch_proj.0, layer_emb, router.0,
+router.2}.*.  Features are in the hook layout (B, T, C).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+STRATEGIES = ("batch_mode", "batch_avg", "batch_median", "group")
+
+
+def _lin(x, P, name):
+    return x @ P[name + ".weight"].t() + P[name + ".bias"]
+
+
+def router_forward(P, s, t, layer_id, gumbel, tau=1.0, budget_target=8.0, budget_weight=0.05,
+                   entropy_weight=0.001, min_steps=1):
+    """DynamicStepRouter.forward in training mode (:1131-1218).  The time axis is reduced by a plain
+    mean over all T frames (feature_reduce 'gap', :1121-1129; padding included, as the hooks hand the
+    padded features over).  steps = argmax(softmax((logits + g) / tau)) + 1 = argmax(logits + g) + 1
+    (the straight-through y is unused by the caller, :603); loss = budget_weight (mean(steps) -
+    budget_target)^2 (no gradient: steps are integers) - entropy_weight * mean_b H(softmax(logits))."""
+    B = s.shape[0]
+    sv = s.mean(dim=1)
+    tv = t.mean(dim=1)
+    sh = torch.relu(_lin(sv, P, "router.stu_proj.0"))
+    th = torch.relu(_lin(tv, P, "router.tch_proj.0"))
+    emb = P["router.layer_emb.weight"][layer_id].expand(B, -1)
+    h = torch.cat([sh, th, emb], dim=-1)
+    logits = _lin(torch.relu(_lin(h, P, "router.router.0")), P, "router.router.2")
+    K = logits.shape[-1]
+    if min_steps > 1:
+        mask = torch.zeros(K, dtype=logits.dtype)
+        mask[:min_steps - 1] = float("-inf")
+        logits = logits + mask
+    probs = torch.softmax(logits, dim=-1)
+    steps = torch.argmax(logits + gumbel, dim=-1) + 1
+    loss = logits.new_zeros(())
+    if budget_target is not None and budget_weight > 0:
+        loss = loss + budget_weight * (steps.to(logits.dtype).mean() - budget_target) ** 2
+    if entropy_weight > 0:
+        ent = -(probs * probs.clamp_min(1e-8).log()).sum(-1).mean()
+        loss = loss - entropy_weight * ent
+    return steps, loss, probs
+
+
+def choose_steps(steps, strategy, max_steps):
+    """The layer's flow step count from the per-utterance router steps (:609-625): batch_mode = the most
+    frequent value (smallest on ties, torch.mode on the CPU); batch_avg = round-half-even of the mean,
+    clamped; batch_median = the lower median, clamped."""
+    if strategy == "batch_mode":
+        vals, counts = torch.unique(steps, return_counts=True)
+        return int(vals[torch.argmax(counts)])   # unique is sorted: the first maximum is the smallest value
+    if strategy == "batch_avg":
+        return int(min(max(round(float(steps.double().mean())), 1), max_steps))
+    if strategy == "batch_median":
+        srt = torch.sort(steps).values
+        return int(min(max(int(srt[(len(srt) - 1) // 2]), 1), max_steps))
+    raise ValueError(strategy)
+
+
+def schedule_coeffs(S, schedule="rectified", vp=(19.9, 0.1)):
+    """noise_scheduled_x = (dalpha * s_f - v) / (-dsigma) at the last loop time t = 1/S (:1366-1367;
+    schedules :790-823).  Returns (ca, cv) with nsx = ca * s_f + cv * v."""
+    tt = 1.0 / S
+    if schedule == "rectified":
+        da, ds = 1.0, -1.0
+    elif schedule == "vp_ode":
+        a, b = vp
+        al = math.exp(-0.25 * a * (1 - tt) ** 2 - 0.5 * b * (1 - tt))
+        da = al * (0.5 * a * (1 - tt) + 0.5 * b)
+        ds = -al * da / math.sqrt(1 - al * al)
+    else:
+        raise ValueError(f"schedule {schedule!r}: ve_ode has dsigma/dt = 0 (:816-823), a division by zero")
+    return da / (-ds), -1.0 / (-ds)
+
+
+def fm_forward(P, x0, tf, S, schedule="rectified"):
+    """FlowMatchingModule.forward, meta_encoder 'mlp', shape_transform 'linear', loss 'mse'
+    (:1318-1377): for i = S..1, t = i/S: v = W2 relu(W1 [x; te(t)] + b1) + b2, x <- x - v/S; then
+    loss = mean((Wst nsx + bst - t_f)^2) with nsx from the LAST velocity and the ORIGINAL input.
+    x0: (..., Cs), tf: (..., Ct).  Returns (loss, x_S)."""
+    x = x0
+    v = None
+    for i in range(S, 0, -1):
+        tt = torch.full(x0.shape[:-1] + (1,), i / S, dtype=x0.dtype)
+        te = _lin(tt, P, "flow_matching.time_embed")
+        h = torch.relu(_lin(torch.cat([x, te], dim=-1), P, "flow_matching.meta_encoder.0"))
+        v = _lin(h, P, "flow_matching.meta_encoder.2")
+        x = x - v / S
+    ca, cv = schedule_coeffs(S, schedule)
+    nsx = ca * x0 + cv * v
+    tr = _lin(nsx, P, "flow_matching.shape_transformation_function")
+    return ((tr - tf) ** 2).mean(), x
+
+
+def encfm_forward(P, sfeats, tfeats, gumbels, strategy="batch_mode", max_steps=8, router_weight=1.0,
+                  tau=1.0, schedule="rectified"):
+    """The flow-matching block of DistilFlowMatchingCTCModelBPE.forward (:595-666) over the hooked layer
+    pairs (lists of (B, T, C)): returns dict(total = router_weight * sum router losses + sum flow losses,
+    flow (per layer), router_loss (per layer), steps (L, B), S (per layer; 0 for 'group'), fm_out = the
+    last layer's FM output, which replaces the encoder output as the decoder input, :666)."""
+    total_flow = sfeats[0].new_zeros(())
+    total_router = sfeats[0].new_zeros(())
+    flows, rls, steps_all, S_all = [], [], [], []
+    fm_out = None
+    for i, (s, t) in enumerate(zip(sfeats, tfeats)):
+        steps, rl, _ = router_forward(P, s, t, i, gumbels[i], tau=tau)
+        total_router = total_router + rl
+        if strategy == "group":
+            fm_out = torch.zeros_like(s)
+            fl = s.new_zeros(())
+            for sv in torch.unique(steps).tolist():
+                idx = steps == sv
+                f, o = fm_forward(P, s[idx], t[idx], int(sv), schedule)
+                fm_out = fm_out.index_put((idx.nonzero()[:, 0],), o)
+                fl = fl + f
+            S = 0
+        else:
+            S = choose_steps(steps, strategy, max_steps)
+            fl, fm_out = fm_forward(P, s, t, S, schedule)
+        total_flow = total_flow + fl
+        flows.append(fl)
+        rls.append(rl)
+        steps_all.append(steps)
+        S_all.append(S)
+    return {"total": router_weight * total_router + total_flow, "flow": flows, "router_loss": rls,
+            "steps": torch.stack(steps_all), "S": S_all, "fm_out": fm_out}
+
+
+def init_encfm(Cs=88, Ct=176, L=16, hidden=128, time_dim=32, proj=128, rhidden=128, K=8, layer_emb=32, seed=0):
+    """nn.Linear / nn.Embedding default initialisation shapes for the two modules (:1240-1292, :1076-1098)."""
+    g = torch.Generator().manual_seed(seed)
+
+    def lin(name, o, i):
+        bound = 1.0 / math.sqrt(i)
+        return {name + ".weight": (torch.rand(o, i, generator=g) * 2 - 1) * bound,
+                name + ".bias": (torch.rand(o, generator=g) * 2 - 1) * bound}
+    P = {}
+    P.update(lin("flow_matching.time_embed", time_dim, 1))
+    P.update(lin("flow_matching.meta_encoder.0", hidden, Cs + time_dim))
+    P.update(lin("flow_matching.meta_encoder.2", Cs, hidden))
+    P.update(lin("flow_matching.shape_transformation_function", Ct, Cs))
+    P.update(lin("router.stu_proj.0", proj, Cs))
+    P.update(lin("router.tch_proj.0", proj, Ct))
+    P["router.layer_emb.weight"] = torch.randn(L, layer_emb, generator=g)
+    P.update(lin("router.router.0", rhidden, 2 * proj + layer_emb))
+    P.update(lin("router.router.2", K, rhidden))
+    return P
+
+
+__all__ = ["router_forward", "choose_steps", "schedule_coeffs", "fm_forward", "encfm_forward", "init_encfm",
+           "STRATEGIES"]

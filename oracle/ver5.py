@@ -67,6 +67,12 @@ class StepConfig:
     version: int = 5                    # --model_version verN (asr_train_diffm.py:1636-1641)
     kd_loss_type: str = "mse"
     use_diffkd: bool = False            # --use_diffkd: DiffKDModule on every layer pair (:795-800)
+    # asr_train.py's encoder-level FM family instead of the latent heads (oracle/encfm.py)
+    kd_model: str = "diffm"
+    encfm_strategy: str = "batch_mode"
+    router_max_steps: int = 8
+    router_weight: float = 1.0
+    flow_schedule: str = "rectified"
     diffkd_steps: int = 9               # --diffkd_steps (diffkd_cfg["diffusion_steps"], :1830-1836)
     bn_momentum: float = 0.1
     ln_eps: float = 1e-5
@@ -579,12 +585,13 @@ def v_layer_losses(version, s_btd, t_btd, p, eps, denoiser_steps=9, fm_steps=8, 
 # ------------------------------------------------------------------------------------------
 
 def ver5_step(p, wav, wav_len, targets, target_len, cfg: StepConfig, eps, spec_mask=None,
-              student_train=True, bn_state=None):
+              student_train=True, bn_state=None, gumbel=None):
     """Forward of one ver5 training step; returns dict of losses and intermediates.
 
     eps: (n_layers, B, latent, T') NoiseAdapter noise (injected; the reference draws randn_like).
     spec_mask: optional (B, nfilt, T_mel) bool SpecAugment mask (True = masked to 0).
     bn_state: dict of running stats (cloned, updated in place for the student).
+    gumbel: kd_model "encfm": per-layer (B, router_max_steps) router Gumbel noise (injected).
     """
     if bn_state is None:
         bn_state = {k: v.clone() for k, v in p.items() if "running_" in k}
@@ -598,6 +605,15 @@ def ver5_step(p, wav, wav_len, targets, target_len, cfg: StepConfig, eps, spec_m
                                       p["teacher.preprocessor.featurizer.fb"][0], cfg)
         _, _, t_feats = encoder(mel_t, mel_t_len, p, "teacher.encoder.", cfg.d_teacher, cfg.heads_teacher, cfg,
                                 False, bn_state)
+    encfm_out = None
+    if cfg.kd_model == "encfm":
+        # asr_train.py:595-666: router + FM over the hooked layer pairs; the decoder reads the last
+        # layer's FM output (hook layout (B, T, C) -> the decoder's (B, C, T))
+        from oracle import encfm as E
+        encfm_out = E.encfm_forward(p, s_feats, t_feats, gumbel, strategy=cfg.encfm_strategy,
+                                    max_steps=cfg.router_max_steps, router_weight=cfg.router_weight,
+                                    schedule=cfg.flow_schedule)
+        enc = encfm_out["fm_out"].transpose(1, 2)
     log_probs = decoder(enc, p, "decoder.")
     ctc = ctc_loss_mean_batch(log_probs, targets, enc_len, target_len, cfg.vocab)
     with torch.no_grad():
@@ -605,6 +621,13 @@ def ver5_step(p, wav, wav_len, targets, target_len, cfg: StepConfig, eps, spec_m
         tch_p = F.softmax(tch_logp / cfg.kd_temperature, dim=-1)
     stu_logp = F.log_softmax(log_probs / cfg.kd_temperature, dim=-1)
     kl = F.kl_div(stu_logp, tch_p, reduction="batchmean") * cfg.kd_temperature ** 2
+    if encfm_out is not None:
+        # training_step (asr_train.py:762-768): ctc + kd_alpha * logit_kd + forward's total_loss
+        zero = torch.zeros((), dtype=log_probs.dtype)
+        total = ctc + cfg.kd_alpha * kl + encfm_out["total"]
+        return {"loss": total, "ctc": ctc, "kl": kl, "recon": zero, "fm": encfm_out["total"], "diffkd": zero,
+                "encfm": encfm_out, "log_probs": log_probs, "enc_len": enc_len, "mel": mel, "mel_len": mel_len,
+                "s_feats": s_feats, "t_feats": t_feats, "bn_state": bn_state}
     recon_sum = torch.zeros((), dtype=log_probs.dtype)
     fm_sum = torch.zeros((), dtype=log_probs.dtype)     # ver5: fm_post; other versions: all four KD terms
     terms = {k: torch.zeros((), dtype=log_probs.dtype) for k in ("kd_loss_pre", "fm_loss_pre", "kd_loss_post",
@@ -647,6 +670,8 @@ def trainable_names(p: dict, version: int = 5, use_diffkd: bool = False) -> list
         if k.startswith("fm_latent_2.") and version not in (6, 7):
             continue
         if k.startswith("diffkd.") and (not use_diffkd or k.startswith("diffkd.encoder.")):
+            continue
+        if k.startswith("layer_proj."):   # built with flow matching, used only by layerwise KD (asr_train.py:525-529)
             continue
         out.append(k)
     return out
