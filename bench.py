@@ -363,13 +363,17 @@ def main():
             threads = args.cpu_threads or _usable_cpus()
             cpu = cpu_baseline(threads, args.samples)
             cpu["cgroup_cpu_max"] = _cgroup_cpu_max()
-        f32 = v1024 = None
+        f32 = v1024 = encfm = None
         if not args.no_f32_sensitivity and cfg.math == "bf16" and world == 1:
             _progress("f32 sensitivity")
             f32 = sensitivity(dev, args.samples, math="f32")
             f32["dtype"] = "f32"
             _progress("V=1024 sensitivity")
             v1024 = sensitivity(dev, args.samples, vocab=1024)
+            _progress("encoder-level FM + router sensitivity")
+            encfm = sensitivity(dev, args.samples, kd_model="encfm")
+            encfm["note"] = ("the asr_train.py model family on the same workload: router + flow matching on every "
+                             "hooked layer pair instead of the ver5 latent heads; not the headline value")
         line = {
             "metric": "utterances/sec (FM-distill train step, Conformer-CTC-small) at 1/2/4/8 MI355X",
             "value": round(utt, 3),
@@ -406,6 +410,7 @@ def main():
             "cpu_baseline": cpu,
             "f32_sensitivity": f32,
             "vocab_1024_sensitivity": v1024,
+            "encoder_fm_router_sensitivity": encfm,
             "losses_last_step": [round(x, 5) for x in losses],
         }
         print(json.dumps(line))

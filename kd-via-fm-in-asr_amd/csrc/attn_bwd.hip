@@ -151,7 +151,8 @@ __global__ __launch_bounds__(256) void attn_rowdot_kernel(const float* __restric
 // ---------------------------------------------------------------------------------------------
 // kernel 1: dQu, dQv
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AbP p) {
+template <int NU>
+__global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dq_kernel(AbP p) {
   __shared__ __attribute__((aligned(16))) uint16_t Ks[BK * LR];     // K block [key][c]
   __shared__ __attribute__((aligned(16))) uint16_t Vs[BK * LR];     // V block [key][c]
   __shared__ __attribute__((aligned(16))) uint16_t Pr[PB1 * LR];    // Ppos band [band row][c]
@@ -197,18 +198,18 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AbP p) {
   }
 
   // next key block's operands in registers: V and K rows, the Ppos band
-  float4 nv[3], nk[3], nb[6];
+  float4 nv[NU], nk[NU], nb[2 * NU];
   auto fetch = [&](int kb) {
     const int j0 = kb * BK;
     const int rbase = T - 1 - (i0 + BQ - 1) + j0;
-    fetch_rows<3>(nv, p.v, p.ldkv, b * p.T, j0, BK, 0, len, hoff, dk);
-    fetch_rows<3>(nk, p.k, p.ldkv, b * p.T, j0, BK, 0, len, hoff, dk);
-    fetch_rows<6>(nb, p.pos, p.d, 0, rbase, 127, 0, npos, hoff, dk);
+    fetch_rows<NU>(nv, p.v, p.ldkv, b * p.T, j0, BK, 0, len, hoff, dk);
+    fetch_rows<NU>(nk, p.k, p.ldkv, b * p.T, j0, BK, 0, len, hoff, dk);
+    fetch_rows<2 * NU>(nb, p.pos, p.d, 0, rbase, 127, 0, npos, hoff, dk);
   };
 
-  f32x4 aq[3], av[3];
+  f32x4 aq[NU], av[NU];
 #pragma unroll
-  for (int u = 0; u < 3; ++u) { aq[u] = f32x4{0.f, 0.f, 0.f, 0.f}; av[u] = aq[u]; }
+  for (int u = 0; u < NU; ++u) { aq[u] = f32x4{0.f, 0.f, 0.f, 0.f}; av[u] = aq[u]; }
   const int wb = 48 - 16 * w;   // this wave's band offset
   float* G = Wsc[w];                                    // f32 score band [16][LG32]
   uint16_t* D = reinterpret_cast<uint16_t*>(Wsc[w]);    // bf16 dS [16][LW]   (after the scores)
@@ -217,9 +218,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AbP p) {
   for (int kb = 0; kb < nkb; ++kb) {
     const int j0 = kb * BK;
     __syncthreads();
-    put_rows<3>(Vs, nullptr, 0, nv, BK, dk);
-    put_rows<3>(Ks, nullptr, 0, nk, BK, dk);
-    put_rows<6>(Pr, nullptr, 0, nb, 127, dk);
+    put_rows<NU>(Vs, nullptr, 0, nv, BK, dk);
+    put_rows<NU>(Ks, nullptr, 0, nk, BK, dk);
+    put_rows<2 * NU>(Pr, nullptr, 0, nb, 127, dk);
     __syncthreads();
     if (kb + 1 < nkb) fetch(kb + 1);
     // ---- S of this wave's 16 rows x 64 keys: the forward's scores (relpos_attn_fwd_kernel) ----
@@ -294,20 +295,20 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AbP p) {
     for (int ks = 0; ks < 2; ++ks) {
       const bf16x8 da = *reinterpret_cast<const bf16x8*>(D + (lane & 15) * LW + ks * 32 + 8 * (lane >> 4));
 #pragma unroll
-      for (int u = 0; u < 3; ++u) aq[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, tr_frag(Ks, LR, ks * 32, 16 * u, lane),
+      for (int u = 0; u < NU; ++u) aq[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, tr_frag(Ks, LR, ks * 32, 16 * u, lane),
                                                                                 aq[u], 0, 0, 0);
     }
 #pragma unroll
     for (int ks = 0; ks < 3; ++ks) {
       const bf16x8 ga = *reinterpret_cast<const bf16x8*>(Gk + (lane & 15) * LG + ks * 32 + 8 * (lane >> 4));
 #pragma unroll
-      for (int u = 0; u < 3; ++u)
+      for (int u = 0; u < NU; ++u)
         av[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ga, tr_frag(Pr, LR, wb + ks * 32, 16 * u, lane), av[u], 0, 0, 0);
     }
     wsync();
   }
 #pragma unroll
-  for (int u = 0; u < 3; ++u)
+  for (int u = 0; u < NU; ++u)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int i = ib + r, c = 16 * u + (lane & 15);
@@ -322,7 +323,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AbP p) {
 // ---------------------------------------------------------------------------------------------
 // kernel 2: dK, dV  (P = p~ exp(m_ikb - lse_i) read from the forward's bf16 p~ and block maxima)
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256, 2) void attn_bwd_dkv_kernel(AbP p) {
+template <int NU>
+__global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dkv_kernel(AbP p) {
   __shared__ __attribute__((aligned(16))) uint16_t Os[BQ * LR];     // dO block [query][c]
   __shared__ __attribute__((aligned(16))) uint16_t Qs[BQ * LR];     // Qu block [query][c]
   __shared__ __attribute__((aligned(16))) float Pt[BK * (BQ + 1)];  // P block^T [key][query]
@@ -354,21 +356,21 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkv_kernel(AbP p) {
   const int jb = j0 + w * 16 + 4 * (lane >> 4);   // C-layout key rows jb + r
   const uint64_t seed = (p.p_drop > 0.f) ? load_seed(p.seed) : 0ull;
   const float keep = (p.p_drop > 0.f) ? 1.f / (1.f - p.p_drop) : 1.f;
-  f32x4 adv[3], adk[3];
+  f32x4 adv[NU], adk[NU];
 #pragma unroll
-  for (int u = 0; u < 3; ++u) { adv[u] = f32x4{0.f, 0.f, 0.f, 0.f}; adk[u] = adv[u]; }
+  for (int u = 0; u < NU; ++u) { adv[u] = f32x4{0.f, 0.f, 0.f, 0.f}; adk[u] = adv[u]; }
   uint16_t* PW = Pw[w];
   uint16_t* DW = Dw[w];
   const int nqb = (j0 < len) ? (len + BQ - 1) / BQ : 0;   // query rows >= len have P == 0
   // next query block's operands in registers: dO and Qu rows, the p~ block (row-major, coalesced along
   // keys), the row sums and the rows' scales exp(m_ikb - lse_i)
-  float4 ndo[3], nqu[3];
+  float4 ndo[NU], nqu[NU];
   uint16_t npb[BQ * BK / 256];
   float nrs = 0.f, nm = 0.f, nl = 3.0e38f;
   auto fetch = [&](int qb) {
     const int i0 = qb * BQ;
-    fetch_rows<3>(ndo, p.dO, p.ldq, b * p.T, i0, BQ, 0, T, hoff, dk);
-    fetch_rows<3>(nqu, p.qu, p.ldq, b * p.T, i0, BQ, 0, T, hoff, dk);
+    fetch_rows<NU>(ndo, p.dO, p.ldq, b * p.T, i0, BQ, 0, T, hoff, dk);
+    fetch_rows<NU>(nqu, p.qu, p.ldq, b * p.T, i0, BQ, 0, T, hoff, dk);
 #pragma unroll
     for (int it = 0; it < BQ * BK / 256; ++it) {
       const int e = threadIdx.x + it * 256;
@@ -388,8 +390,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkv_kernel(AbP p) {
   for (int qb = 0; qb < nqb; ++qb) {
     const int i0 = qb * BQ;
     __syncthreads();
-    put_rows<3>(Os, nullptr, 0, ndo, BQ, dk);
-    put_rows<3>(Qs, nullptr, 0, nqu, BQ, dk);
+    put_rows<NU>(Os, nullptr, 0, ndo, BQ, dk);
+    put_rows<NU>(Qs, nullptr, 0, nqu, BQ, dk);
 #pragma unroll
     for (int it = 0; it < BQ * BK / 256; ++it) {
       const int e = threadIdx.x + it * 256;
@@ -442,7 +444,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkv_kernel(AbP p) {
       const bf16x8 pa = *reinterpret_cast<const bf16x8*>(PW + (lane & 15) * LW + ks * 32 + 8 * (lane >> 4));
       const bf16x8 da = *reinterpret_cast<const bf16x8*>(DW + (lane & 15) * LW + ks * 32 + 8 * (lane >> 4));
 #pragma unroll
-      for (int u = 0; u < 3; ++u) {
+      for (int u = 0; u < NU; ++u) {
         adv[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, tr_frag(Os, LR, ks * 32, 16 * u, lane), adv[u], 0, 0, 0);
         adk[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, tr_frag(Qs, LR, ks * 32, 16 * u, lane), adk[u], 0, 0, 0);
       }
@@ -450,7 +452,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkv_kernel(AbP p) {
     wsync();
   }
 #pragma unroll
-  for (int u = 0; u < 3; ++u)
+  for (int u = 0; u < NU; ++u)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int j = jb + r, c = 16 * u + (lane & 15);
@@ -465,7 +467,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkv_kernel(AbP p) {
 // ---------------------------------------------------------------------------------------------
 // kernel 3: per-chunk partials of dPpos  (P from p~ and the block maxima, as kernel 2)
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256, 2) void attn_bwd_dpos_kernel(AbP p) {
+template <int NU>
+__global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dpos_kernel(AbP p) {
   __shared__ __attribute__((aligned(16))) uint16_t Vs[NPJ * LR];     // V rows jbase.. [key][c]
   __shared__ __attribute__((aligned(16))) uint16_t Dl[NPQ * LDL];    // dS [i - ib0][j - jbase]
   __shared__ __attribute__((aligned(16))) uint16_t Qt[BDK * LQ3];    // Qv^T [c][i - ib0]
@@ -485,9 +488,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dpos_kernel(AbP p) {
   const float keep = (p.p_drop > 0.f) ? 1.f / (1.f - p.p_drop) : 1.f;
   zero_pad(Vs, NPJ, dk, NPJ);
   for (int e = threadIdx.x; e < (BDK - dk) * LQ3; e += 256) Qt[dk * LQ3 + e] = 0;
-  f32x4 acc[3];
+  f32x4 acc[NU];
 #pragma unroll
-  for (int u = 0; u < 3; ++u) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int u = 0; u < NU; ++u) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int qh = w & 1, kh = w >> 1;   // dS computation: query half, key half (48 keys)
   const int64_t b0 = bchunk * p.bpc;
   const int64_t b1 = min<int64_t>(p.B, b0 + p.bpc);
@@ -512,7 +515,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dpos_kernel(AbP p) {
   };
   // next iteration's operands in registers (software pipeline): V rows, Qv rows, row sums, the rows'
   // block scales, this lane's dO fragments and 12 p~ elements
-  float4 nvr[(NPJ * 12 + 255) / 256], nqr[(NPQ * 12 + 255) / 256];
+  float4 nvr[(NPJ * 4 * NU + 255) / 256], nqr[(NPQ * 4 * NU + 255) / 256];
   float nrs = 0.f, nm = 0.f, nl = 3.0e38f;
   bf16x8 nfdo[2];
   uint16_t np[3][4];
@@ -520,8 +523,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dpos_kernel(AbP p) {
   auto fetch = [&](int64_t bb, int ib, int ln) {
     const int jb = r0 - (T - 1) + ib;
     const int64_t bhh = bb * p.H + h;
-    fetch_rows<(NPJ * 12 + 255) / 256>(nvr, p.v, p.ldkv, bb * p.T, jb, NPJ, 0, ln, hoff, dk);
-    fetch_rows<(NPQ * 12 + 255) / 256>(nqr, p.qv, p.ldq, bb * p.T, ib, NPQ, 0, ln, hoff, dk);
+    fetch_rows<(NPJ * 4 * NU + 255) / 256>(nvr, p.v, p.ldkv, bb * p.T, jb, NPJ, 0, ln, hoff, dk);
+    fetch_rows<(NPQ * 4 * NU + 255) / 256>(nqr, p.qv, p.ldq, bb * p.T, ib, NPQ, 0, ln, hoff, dk);
     if (threadIdx.x < NPQ) nrs = (ib + (int)threadIdx.x < ln) ? p.rsum[bhh * p.T + ib + threadIdx.x] : 0.f;
     if (threadIdx.x < 3 * NPQ) {
       const int il = threadIdx.x / 3, q = threadIdx.x - 3 * il;
@@ -557,8 +560,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dpos_kernel(AbP p) {
     const int cur_len = len;
     const int cur_ib0 = ib0;
     __syncthreads();
-    put_rows<(NPJ * 12 + 255) / 256>(Vs, nullptr, 0, nvr, NPJ, dk);
-    put_rows<(NPQ * 12 + 255) / 256>(nullptr, Qt, LQ3, nqr, NPQ, dk);
+    put_rows<(NPJ * 4 * NU + 255) / 256>(Vs, nullptr, 0, nvr, NPJ, dk);
+    put_rows<(NPQ * 4 * NU + 255) / 256>(nullptr, Qt, LQ3, nqr, NPQ, dk);
     if (threadIdx.x < NPQ) Rs[threadIdx.x] = nrs;
     if (threadIdx.x < 3 * NPQ) Cs[threadIdx.x] = __expf(nm - nl);
     const bf16x8 fdo[2] = {nfdo[0], nfdo[1]};
@@ -605,13 +608,13 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dpos_kernel(AbP p) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) fa[e] = (short)Dl[(kq + e) * LDL + 16 * w + m + kq + e];
 #pragma unroll
-    for (int u = 0; u < 3; ++u) {
+    for (int u = 0; u < NU; ++u) {
       const bf16x8 qb = *reinterpret_cast<const bf16x8*>(Qt + (16 * u + (lane & 15)) * LQ3 + kq);
       acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, qb, acc[u], 0, 0, 0);
     }
   }
 #pragma unroll
-  for (int u = 0; u < 3; ++u)
+  for (int u = 0; u < NU; ++u)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int rr = r0 + 16 * w + 4 * (lane >> 4) + r, c = 16 * u + (lane & 15);
@@ -663,7 +666,8 @@ int kdfm_relpos_attn_bwd_parts(const float* dO, const float* O, const float* qu,
                "dkv / dpos parts need the forward's p_tilde and m_blk");
   KDFM_REQUIRE(H > 0 && d % H == 0, "d must be a multiple of H");
   const int64_t dk = d / H;
-  KDFM_REQUIRE(dk <= 48 && dk % 4 == 0, "head dim must be a multiple of 4 and <= 48");
+  KDFM_REQUIRE(dk <= 64 && dk % 4 == 0, "head dim must be a multiple of 4 and <= 64");
+  const bool wide = dk > 48;   // 4 output column tiles of 16 (FastConformer's 64) instead of 3
   KDFM_REQUIRE(T > 0 && T <= 4096 && d % 4 == 0, "bad T / d");
   KDFM_REQUIRE(dropout_p == 0.f || seed, "dropout needs a seed");
   KDFM_REQUIRE(ws_len >= kdfm_relpos_attn_bwd_ws(B, H, T, d), "workspace too small (kdfm_relpos_attn_bwd_ws)");
@@ -689,19 +693,29 @@ int kdfm_relpos_attn_bwd_parts(const float* dO, const float* O, const float* qu,
     if (rc) return rc;
   }
   if (parts & KDFM_ATTN_BWD_DQ) {
-    hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3((unsigned)ceil_div(T, BQ), (unsigned)(B * H)), dim3(256), 0, st, p);
+    if (wide)
+      hipLaunchKernelGGL(attn_bwd_dq_kernel<4>, dim3((unsigned)ceil_div(T, BQ), (unsigned)(B * H)), dim3(256), 0, st, p);
+    else
+      hipLaunchKernelGGL(attn_bwd_dq_kernel<3>, dim3((unsigned)ceil_div(T, BQ), (unsigned)(B * H)), dim3(256), 0, st, p);
     rc = check_launch("kdfm_relpos_attn_bwd(dq)");
     if (rc) return rc;
   }
   if (parts & KDFM_ATTN_BWD_DKV) {
-    hipLaunchKernelGGL(attn_bwd_dkv_kernel, dim3((unsigned)ceil_div(T, BK), (unsigned)(B * H)), dim3(256), 0, st, p);
+    if (wide)
+      hipLaunchKernelGGL(attn_bwd_dkv_kernel<4>, dim3((unsigned)ceil_div(T, BK), (unsigned)(B * H)), dim3(256), 0, st, p);
+    else
+      hipLaunchKernelGGL(attn_bwd_dkv_kernel<3>, dim3((unsigned)ceil_div(T, BK), (unsigned)(B * H)), dim3(256), 0, st, p);
     rc = check_launch("kdfm_relpos_attn_bwd(dkv)");
     if (rc) return rc;
   }
   if (!(parts & KDFM_ATTN_BWD_DPOS)) return KDFM_OK;
   const int64_t npos = 2 * T - 1;
-  hipLaunchKernelGGL(attn_bwd_dpos_kernel, dim3((unsigned)ceil_div(npos, 64), (unsigned)H, (unsigned)chunks),
-                     dim3(256), 0, st, p);
+  if (wide)
+    hipLaunchKernelGGL(attn_bwd_dpos_kernel<4>, dim3((unsigned)ceil_div(npos, 64), (unsigned)H, (unsigned)chunks),
+                       dim3(256), 0, st, p);
+  else
+    hipLaunchKernelGGL(attn_bwd_dpos_kernel<3>, dim3((unsigned)ceil_div(npos, 64), (unsigned)H, (unsigned)chunks),
+                       dim3(256), 0, st, p);
   rc = check_launch("kdfm_relpos_attn_bwd(dpos)");
   if (rc) return rc;
   hipLaunchKernelGGL(attn_dpos_fold_kernel, dim3((unsigned)ceil_div(npos * d, 256)), dim3(256), 0, st, p.dpos_part,

@@ -75,8 +75,8 @@ __device__ __forceinline__ float group16_sum(float v) {
   return v;
 }
 
-template <bool TWO_PASS>
-__global__ __launch_bounds__(256, 2) void relpos_attn_fwd_kernel(AttnP p) {
+template <bool TWO_PASS, int NU>   // NU: 16-column output tiles of the head dim (3: dk <= 48, 4: dk <= 64)
+__global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void relpos_attn_fwd_kernel(AttnP p) {
   __shared__ __attribute__((aligned(16))) uint16_t Ks[AKB * LDR];
   __shared__ __attribute__((aligned(16))) uint16_t Vt[DKP * LDVT];
   __shared__ __attribute__((aligned(16))) uint16_t Pr[BAND * LDR];
@@ -125,8 +125,8 @@ __global__ __launch_bounds__(256, 2) void relpos_attn_fwd_kernel(AttnP p) {
 
   // ---- staging of one key block: all global loads of a stage are issued before any LDS store
   // (register staging; the next block's loads are in flight while this block computes) ----
-  constexpr int KU = (AKB * (DKP / 4 * 3 / 4) + 255) / 256;  // K / V float4 per thread (dk <= 48)
-  constexpr int PU = (BAND * (DKP / 4 * 3 / 4) + 255) / 256; // P-band float4 per thread
+  constexpr int KU = (AKB * 4 * NU + 255) / 256;    // K / V float4 per thread (dk <= 16 NU)
+  constexpr int PU = (BAND * 4 * NU + 255) / 256;   // P-band float4 per thread
   const int cq = dk >> 2;
   float4 rk[KU], rv[KU], rp[PU];
   auto load_stage = [&](int j0, bool with_v) {
@@ -248,9 +248,9 @@ __global__ __launch_bounds__(256, 2) void relpos_attn_fwd_kernel(AttnP p) {
   // ---- pass 2: probabilities, dropout, O += Pd V ----
   const uint64_t seed = (p.p_drop > 0.f) ? load_seed(p.seed) : 0ull;
   const float keep_scale = (p.p_drop > 0.f) ? 1.f / (1.f - p.p_drop) : 1.f;
-  f32x4 oacc[3];
+  f32x4 oacc[NU];
 #pragma unroll
-  for (int u = 0; u < 3; ++u) oacc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int u = 0; u < NU; ++u) oacc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int64_t prow0 = (bh * p.T + ib) * p.T;  // P row of (ib, j = 0)
   for (int kb = 0; kb < (T + AKB - 1) / AKB; ++kb) {
     const int j0 = kb * AKB;
@@ -283,7 +283,7 @@ __global__ __launch_bounds__(256, 2) void relpos_attn_fwd_kernel(AttnP p) {
         lrow[r] = lrow[r] * corr + group16_sum(sum);
         mrow[r] = mn;
 #pragma unroll
-        for (int u = 0; u < 3; ++u) oacc[u][r] *= corr;
+        for (int u = 0; u < NU; ++u) oacc[u][r] *= corr;
       }
     }
     if (!TWO_PASS && live && p.mblk && (lane & 15) == 0) {   // the running max this block's p~ is relative to
@@ -322,7 +322,7 @@ __global__ __launch_bounds__(256, 2) void relpos_attn_fwd_kernel(AttnP p) {
     for (int ks = 0; ks < 2; ++ks) {
       const bf16x8 pa = *reinterpret_cast<const bf16x8*>(Pw + (lane & 15) * LDPS + ks * 32 + 8 * (lane >> 4));
 #pragma unroll
-      for (int u = 0; u < 3; ++u) {
+      for (int u = 0; u < NU; ++u) {
         const bf16x8 vb = *reinterpret_cast<const bf16x8*>(Vt + (16 * u + (lane & 15)) * LDVT + ks * 32 + 8 * (lane >> 4));
         oacc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, vb, oacc[u], 0, 0, 0);
       }
@@ -344,7 +344,7 @@ __global__ __launch_bounds__(256, 2) void relpos_attn_fwd_kernel(AttnP p) {
 #pragma unroll
   for (int r = 0; r < 4; ++r) fin[r] = TWO_PASS ? 1.f : ((ib + r < len && lrow[r] > 0.f) ? 1.f / lrow[r] : 0.f);
 #pragma unroll
-  for (int u = 0; u < 3; ++u)
+  for (int u = 0; u < NU; ++u)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int i = ib + r, c = 16 * u + (lane & 15);
@@ -364,7 +364,7 @@ extern "C" int kdfm_relpos_attn_fwd(const float* qu, const float* qv, const floa
   KDFM_REQUIRE(qu && qv && qkv && pos && o, "null pointer");
   KDFM_REQUIRE(H > 0 && d % H == 0, "d must be a multiple of H");
   const int64_t dk = d / H;
-  KDFM_REQUIRE(dk <= 48 && dk % 4 == 0, "head dim must be a multiple of 4 and <= 48");
+  KDFM_REQUIRE(dk <= 64 && dk % 4 == 0, "head dim must be a multiple of 4 and <= 64");
   KDFM_REQUIRE(T > 0 && T <= 4096, "T out of range");
   KDFM_REQUIRE(d % 4 == 0, "d must be a multiple of 4");
   KDFM_REQUIRE(dropout_p == 0.f || seed, "dropout needs a seed");
@@ -377,9 +377,14 @@ extern "C" int kdfm_relpos_attn_fwd(const float* qu, const float* qv, const floa
   p.B = B; p.H = H; p.T = T; p.d = d; p.dk = dk; p.ldq = d; p.ldkv = 3 * d;
   p.scale = scale; p.p_drop = dropout_p; p.seed = seed; p.rng_stream = rng_stream;
   dim3 grid((unsigned)ceil_div(T, AQ), (unsigned)(B * H));
-  if (P || Pdrop)
-    hipLaunchKernelGGL(relpos_attn_fwd_kernel<true>, grid, dim3(256), 0, as_stream(stream), p);
+  const bool two = P || Pdrop, wide = dk > 48;
+  if (two && !wide)
+    hipLaunchKernelGGL((relpos_attn_fwd_kernel<true, 3>), grid, dim3(256), 0, as_stream(stream), p);
+  else if (two)
+    hipLaunchKernelGGL((relpos_attn_fwd_kernel<true, 4>), grid, dim3(256), 0, as_stream(stream), p);
+  else if (!wide)
+    hipLaunchKernelGGL((relpos_attn_fwd_kernel<false, 3>), grid, dim3(256), 0, as_stream(stream), p);
   else
-    hipLaunchKernelGGL(relpos_attn_fwd_kernel<false>, grid, dim3(256), 0, as_stream(stream), p);
+    hipLaunchKernelGGL((relpos_attn_fwd_kernel<false, 4>), grid, dim3(256), 0, as_stream(stream), p);
   return check_launch("kdfm_relpos_attn_fwd");
 }

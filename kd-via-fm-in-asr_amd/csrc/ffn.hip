@@ -20,9 +20,9 @@
 // (r, h) the features 8 q + 4 h + 0..3 of row r; one v_permlane32_swap per packed bf16 dword turns a
 // chunk's activation into the B operand of the next product (cdna_hip_programming.md T21).
 //
-// Work split: a workgroup owns 64 rows = 2 row tiles of 32.  Backward (d <= 96): NP = 4 waves per tile
-// take the chunks c = NP it + par (d = 176: NP = 2), their dLN partials added in a fixed order through
-// LDS like the forward's.  Forward (d <= 96): NP = 4 waves per tile take the chunks
+// Work split: a workgroup owns 64 rows = 2 row tiles of 32.  Backward: NP = 2 waves per tile take the
+// chunks c = NP it + par, their dLN partials added in a fixed order through LDS like the forward's.
+// Forward (d <= 96): NP = 4 waves per tile take the chunks
 // c = NP it + par, so 12,832 rows give 1,604 waves (the kernel is latency bound: a wave's serial
 // chain of chunks sets the launch time and 201 workgroups fill at most 201 CUs); their partial
 // down-projections are added in the fixed order ((p0 + p1) + p2) + p3 through LDS at the end, and
@@ -42,9 +42,10 @@ constexpr int FF_ROWS = 64;       // rows per workgroup
 // its 96 accumulators do not fit the 256-register budget of 2 waves per SIMD)
 template <int DT> constexpr int fwd_np() { return DT <= 3 ? 4 : 2; }
 template <int DT> constexpr int fwd_nt() { return 2 * fwd_np<DT>() * 64; }
-// backward: the same split (d <= 96: 4 chunk parities per row tile, 8 waves; a wave's serial chain of
-// chunks is what bounds the launch at ~1 wave per SIMD); d = 176 keeps 2 (its 18 + 12 KB chunk stages)
-template <int DT> constexpr int bwd_np() { return DT <= 3 ? 4 : 2; }
+// backward: 2 chunk parities per row tile (4 waves).  Measured: 4 parities (8 waves, 144 KB of stages,
+// the 256-register cap of 2 waves per SIMD) ran 67.6 us against 64.8 us per in-step launch
+// (profiles/r03/r3f_kernel_summary.txt vs r3b): the shorter chain did not pay for the larger stages
+template <int DT> constexpr int bwd_np() { return 2; }
 template <int DT> constexpr int bwd_nt() { return 2 * bwd_np<DT>() * 64; }
 
 // Chunk image (one 32-feature slice of the hidden width), fragment order:

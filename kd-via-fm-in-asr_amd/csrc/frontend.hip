@@ -226,6 +226,8 @@ __device__ __forceinline__ void fft_wsync() {
 
 __device__ __forceinline__ int bitrev8(int v) { return (int)(__builtin_bitreverse32((uint32_t)v) >> 24); }
 
+constexpr int FB_LDS = 4096;   // compact filterbank (nonzero ranges of every filter) staged per workgroup
+
 __global__ __launch_bounds__(64 * FFT_WAVES) void logmel_fft_kernel(
     const float* __restrict__ xp, int64_t ldx, const float* __restrict__ win, const float2* __restrict__ tw,
     const float* __restrict__ fb, const int* __restrict__ fb_lo, const int* __restrict__ fb_hi, float* __restrict__ mel,
@@ -233,8 +235,51 @@ __global__ __launch_bounds__(64 * FFT_WAVES) void logmel_fft_kernel(
   __shared__ float2 Zs[FFT_WAVES][FFT_H];
   __shared__ float Pw[FFT_WAVES][FFT_H + 8];
   __shared__ float2 W[FFT_N];
+  __shared__ float Fc[FB_LDS];          // filter m's weights for bins [lo_m, hi_m) at Fc[Fo[m] ...]
+  __shared__ int Fo[256 + 1], Flo[256], Fn[256];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   for (int e = threadIdx.x; e < FFT_N; e += 64 * FFT_WAVES) W[e] = tw[e];
+  // the mel filterbank is ~2 nonzero weights per bin (triangular filters): its nonzero ranges go to LDS
+  // once per workgroup, so the per-frame dot products read LDS instead of waiting on global loads
+  for (int m = threadIdx.x; m < nfilt; m += 64 * FFT_WAVES) {
+    const int lo = fb_lo[m], hi = fb_hi[m];
+    Flo[m] = lo;
+    Fn[m] = hi > lo ? hi - lo : 0;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int o = 0;
+    for (int m = 0; m < nfilt; ++m) {
+      Fo[m] = o;
+      o += Fn[m];
+    }
+    Fo[nfilt] = o;
+  }
+  __syncthreads();
+  const int total = Fo[nfilt];
+  const bool staged = total <= FB_LDS;
+  if (staged) {   // flat over the nonzero weights: every thread's loads are independent and in flight together
+    constexpr int PER = FB_LDS / (64 * FFT_WAVES);
+    float v[PER];
+#pragma unroll
+    for (int it = 0; it < PER; ++it) {
+      const int e = threadIdx.x + it * 64 * FFT_WAVES;
+      v[it] = 0.f;
+      if (e < total) {
+        int lo = 0, hi = nfilt - 1;   // the filter m with Fo[m] <= e < Fo[m + 1]
+        while (lo < hi) {
+          const int mid = (lo + hi + 1) >> 1;
+          if (Fo[mid] <= e) lo = mid; else hi = mid - 1;
+        }
+        v[it] = fb[(int64_t)lo * nbins + Flo[lo] + (e - Fo[lo])];
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < PER; ++it) {
+      const int e = threadIdx.x + it * 64 * FFT_WAVES;
+      if (e < total) Fc[e] = v[it];
+    }
+  }
   __syncthreads();
   float2* Z = Zs[w];
   float* P = Pw[w];
@@ -283,9 +328,15 @@ __global__ __launch_bounds__(64 * FFT_WAVES) void logmel_fft_kernel(
     fft_wsync();
     float* out = mel + f * nfilt;
     for (int m = lane; m < nfilt; m += 64) {
-      const float* row = fb + (int64_t)m * nbins;
+      const int lo = Flo[m], nk = Fn[m];
       float acc = 0.f;
-      for (int k = fb_lo[m]; k < fb_hi[m]; ++k) acc = fmaf(row[k], P[k], acc);
+      if (staged) {
+        const float* fr = Fc + Fo[m];
+        for (int k = 0; k < nk; ++k) acc = fmaf(fr[k], P[lo + k], acc);
+      } else {
+        const float* row = fb + (int64_t)m * nbins + lo;
+        for (int k = 0; k < nk; ++k) acc = fmaf(row[k], P[lo + k], acc);
+      }
       out[m] = acc;
     }
     fft_wsync();   // Z / P are rewritten by the next frame
@@ -381,10 +432,15 @@ int kdfm_logmel_fft(const float* xp, int64_t ldx, const float* window, const flo
                     int64_t n_fft, int64_t win, int64_t nfilt, void* stream) {
   using namespace kdfm;
   KDFM_REQUIRE(xp && window && twiddle && fb && fb_lo && fb_hi && mel, "null pointer");
-  KDFM_REQUIRE(n_fft == FFT_N && win > 0 && win <= n_fft && nfilt > 0 && hop > 0, "n_fft must be 512");
+  KDFM_REQUIRE(n_fft == FFT_N && win > 0 && win <= n_fft && nfilt > 0 && nfilt <= 256 && hop > 0,
+               "n_fft must be 512, at most 256 filters");
   if (B * T == 0) return KDFM_OK;
   const int64_t groups = ceil_div(B * T, FFT_WAVES);
-  const unsigned grid = (unsigned)(groups < 2048 ? groups : 2048);
+  static const int64_t cap = [] {   // workgroups (frames are grid-strided); KDFM_FFT_GRID overrides
+    const char* v = getenv("KDFM_FFT_GRID");
+    return v && atoi(v) > 0 ? (int64_t)atoi(v) : (int64_t)2048;
+  }();
+  const unsigned grid = (unsigned)(groups < cap ? groups : cap);
   hipLaunchKernelGGL(logmel_fft_kernel, dim3(grid), dim3(64 * FFT_WAVES), 0, as_stream(stream), xp, ldx, window,
                      reinterpret_cast<const float2*>(twiddle), fb, fb_lo, fb_hi, mel, B, T, (int)hop,
                      (int)((n_fft - win) / 2), (int)win, (int)nfilt, (int)(n_fft / 2 + 1));

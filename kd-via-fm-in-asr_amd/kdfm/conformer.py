@@ -399,7 +399,7 @@ def layer_forward(cfg, S: EncoderShapes, P, L, li, x, out, pos_emb, lengths, *, 
     ppos = _empty(npos, d, dev=dev)
     K.linear(pos_emb, P[L + "self_attn.linear_pos.weight"], None, ppos)
     o = _empty(rows, d, dev=dev)
-    if K.get_math() == "bf16" and dk <= 48:
+    if K.get_math() == "bf16" and dk <= 64:
         # fused flash-style kernel: no AC / BD materialisation; P (and P_drop) only when the
         # backward needs them
         if _ATTN_BWD_FUSED:
@@ -442,7 +442,7 @@ def layer_forward(cfg, S: EncoderShapes, P, L, li, x, out, pos_emb, lengths, *, 
     else:
         K.linear(o, P[L + "self_attn.linear_out.weight"], P[L + "self_attn.linear_out.bias"], x2, epi=_lib.EPI_RESID,
                  R=x1, rscale=1.0, dropout_p=pd, seed=seed, rng_stream=_stream(salt, li, SITE_ATT_OUT))
-    fused_attn = K.get_math() == "bf16" and dk <= 48 and _ATTN_BWD_FUSED
+    fused_attn = K.get_math() == "bf16" and dk <= 64 and _ATTN_BWD_FUSED
     keep(x1=x1, ln2=ln2, m2=m2, r2=r2, qkv=qkv, qu=qu, qv=qv, ppos=ppos, P=Pm, Pd=Pd, o=o, o_h=o_h, pa=pa,
          attn_fused=fused_attn, lse=lse if fused_attn else None, pt=pt if fused_attn else None,
          mblk=mblk if fused_attn else None)

@@ -176,11 +176,12 @@ def encfm_backward(cfg, P, G, ws: EncFMWorkspace, dfeats, gxS, wgrad_run):
                K.ptr(G[fm + "meta_encoder.2.bias"]), cap, K.ptr(ws.rows), Cs, H, 1.0, K.ptr(wsb), wsb.numel(), K._s())
         K.linear_dw(ws.dtr, ws.nsx, G[fm + "shape_transformation_function.weight"],
                     db=G[fm + "shape_transformation_function.bias"])
-        if cfg.encfm_dynamic:
-            K.linear_dw(ws.dlogits, ws.h0, G[r + "router.2.weight"], db=G[r + "router.2.bias"])
-            K.linear_dw(ws.dh0, ws.hcat, G[r + "router.0.weight"], db=G[r + "router.0.bias"])
-            K.linear_dw(ws.dhcat[:, :H], ws.sv, G[r + "stu_proj.0.weight"], db=G[r + "stu_proj.0.bias"])
-            K.linear_dw(ws.dhcat[:, H:2 * H], ws.tv, G[r + "tch_proj.0.weight"], db=G[r + "tch_proj.0.bias"])
+        if cfg.encfm_dynamic:   # L*B-row products: exact f32 (the router's forward is f32 too)
+            K.linear_dw(ws.dlogits, ws.h0, G[r + "router.2.weight"], db=G[r + "router.2.bias"], math="f32")
+            K.linear_dw(ws.dh0, ws.hcat, G[r + "router.0.weight"], db=G[r + "router.0.bias"], math="f32")
+            K.linear_dw(ws.dhcat[:, :H], ws.sv, G[r + "stu_proj.0.weight"], db=G[r + "stu_proj.0.bias"], math="f32")
+            K.linear_dw(ws.dhcat[:, H:2 * H], ws.tv, G[r + "tch_proj.0.weight"], db=G[r + "tch_proj.0.bias"],
+                        math="f32")
         gemb = G[r + "layer_emb.weight"] if cfg.encfm_dynamic else ws.dsv   # ws.dsv: an unused sink when fixed
         K.call("kdfm_encfm_time_bwd", K.ptr(gW1), gW1.stride(0), K.ptr(G[fm + "meta_encoder.0.bias"]), K.ptr(W1),
                K.ptr(P[fm + "time_embed.weight"]), K.ptr(P[fm + "time_embed.bias"]), K.ptr(G[fm + "time_embed.weight"]),

@@ -1146,9 +1146,21 @@ def relpos_attn_bwd(do, o, qu, qv, qkv, ppos, lse, p_tilde, m_blk, lengths, dqu,
     assert o.shape == do.shape
     if parts != ATTN_BWD_ALL:
         assert ws is not None and ws.numel() >= relpos_attn_bwd_ws(B, H, T, d)
-        call("kdfm_relpos_attn_bwd_parts", ptr(do), ptr(o), ptr(qu), ptr(qv), ptr(qkv), ptr(ppos), ptr(lse),
-             ptr(p_tilde), ptr(m_blk), ptr(_i64(lengths)), ptr(dqu), ptr(dqv), ptr(dqkv), ptr(dppos), ptr(ws),
-             ws.numel(), B, H, T, d, float(scale), float(p), ptr(seed), int(rng_stream), int(parts), _s())
+        # algorithmic work of the issued parts (per (b, h), 2 T^2 dk FLOP per product): DQ recomputes the
+        # scores (QK^T + band) and forms dP, dQu, dQv; DKV dP, dK, dV; DPOS dP and dPpos.  Bytes: the row
+        # operands each part reads / writes once at f32, p~ (bf16) once per part that reads it
+        dk = d // H
+        tt = 2.0 * B * H * T * T * dk
+        fl = tt * ((5 if parts & ATTN_BWD_DQ else 0) + (3 if parts & ATTN_BWD_DKV else 0)
+                   + (2 if parts & ATTN_BWD_DPOS else 0))
+        nrow = (2 if parts & ATTN_BWD_ROWDOT else 0) + (6 if parts & ATTN_BWD_DQ else 0) + \
+            (6 if parts & ATTN_BWD_DKV else 0) + (3 if parts & ATTN_BWD_DPOS else 0)
+        nb = 4.0 * rows * d * nrow + 2.0 * B * H * T * T * ((1 if parts & ATTN_BWD_DKV else 0)
+                                                            + (1 if parts & ATTN_BWD_DPOS else 0))
+        _traced("attn_bwd", fl, nb, "kdfm_relpos_attn_bwd_parts", ptr(do), ptr(o), ptr(qu), ptr(qv), ptr(qkv),
+                ptr(ppos), ptr(lse), ptr(p_tilde), ptr(m_blk), ptr(_i64(lengths)), ptr(dqu), ptr(dqv), ptr(dqkv),
+                ptr(dppos), ptr(ws), ws.numel(), B, H, T, d, float(scale), float(p), ptr(seed), int(rng_stream),
+                int(parts), _s())
         return
     ws = scratch(do.device, relpos_attn_bwd_ws(B, H, T, d))
     # algorithmic: per (b, h) the products dP (twice: DQ and DKV / DPOS), dQu, dQv, dK, dV, dPpos (2 T^2 dk

@@ -76,7 +76,9 @@ def _torch_grads(qkv, qu, qv, ppos, do, lens, B, H, T, d):
     return torch.autograd.grad(loss, [q_u, q_v, k, v, pp])
 
 
-@pytest.mark.parametrize("B,H,T,d", [(3, 2, 401, 88), (2, 4, 130, 176), (2, 2, 77, 88)])
+@pytest.mark.parametrize("B,H,T,d", [(3, 2, 401, 88), (2, 4, 130, 176), (2, 2, 77, 88),
+                                     # head dim 64 (FastConformer d=512, 8 heads; fast-conformer_ctc_bpe.yaml:94-143)
+                                     (2, 8, 201, 512), (2, 2, 77, 128)])
 def test_attn_bwd_matches_float64(B, H, T, d):
     from kdfm import kernels as K
     qkv, qu, qv, ppos, do, lens = _inputs(B, H, T, d, T + d)

@@ -54,7 +54,9 @@ def _torch_ref_P(qu, qv, qkv, ppos, lens, B, H, T, d):
 
 
 @pytest.mark.parametrize("B,H,T,d,p", [(3, 2, 401, 88, 0.0), (2, 4, 401, 176, 0.1), (2, 2, 77, 88, 0.1),
-                                       (2, 4, 130, 176, 0.0), (1, 2, 64, 88, 0.0)])
+                                       (2, 4, 130, 176, 0.0), (1, 2, 64, 88, 0.0),
+                                       # head dim 64 (FastConformer d=512, 8 heads)
+                                       (2, 8, 201, 512, 0.1), (2, 2, 77, 128, 0.0)])
 def test_fused_attention_matches(B, H, T, d, p):
     from kdfm import _lib
     from kdfm import kernels as K

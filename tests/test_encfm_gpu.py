@@ -28,8 +28,9 @@ def _rel(a, b):
 
 def _cfg(L, strategy, **kw):
     from kdfm.config import DEFAULT
-    return replace(DEFAULT, n_layers=L, kd_model="encfm", encfm_strategy=strategy, encfm_dynamic=True,
-                   router_max_steps=8, **kw)
+    args = dict(n_layers=L, kd_model="encfm", encfm_strategy=strategy, encfm_dynamic=True, router_max_steps=8)
+    args.update(kw)
+    return replace(DEFAULT, **args)
 
 
 def _run(cfg, P, s, t, gumbel, B, T, R):

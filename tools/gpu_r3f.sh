@@ -4,7 +4,7 @@
 set -o pipefail
 OUT=gpurun_out/r3f
 mkdir -p "$OUT"
-timeout -k 10 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_ffn_gpu.py \
+timeout -k 10 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_ffn_gpu.py "tests/test_step_parity_gpu.py::test_frontend_matches_oracle" \
   tests/test_plan_gpu.py tests/test_determinism_gpu.py > "$OUT/tests.log" 2>&1 || exit $?
 timeout -k 10 300 python -u tools/ffn_micro.py 20 > "$OUT/ffn_micro.log" 2>&1 || exit $?
 timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-f32-sensitivity \
