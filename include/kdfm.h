@@ -628,9 +628,12 @@ int kdfm_loss_combine(const float* nll, int64_t B, const float* kl, const float*
 /* ---------------- ver5 KD heads (asr_train_diffm.py:400-497, 1270-1427) -------------------- */
 int kdfm_adapter_fwd(const float* zs, const float* h, const float* w2, const float* b2, const float* eps_in, float* zn,
                      float* gamma, int64_t rows, int64_t L, const uint64_t* seed, uint64_t rng_stream, void* stream);
+/* NoiseAdapter backward: dzs, dh per row; dw2 += sum dgl h, db2 += sum dgl through per-workgroup partials in
+ * ws (kdfm_adapter_bwd_ws floats) folded in a fixed order (deterministic).  L a multiple of 16, <= 128. */
+int64_t kdfm_adapter_bwd_ws(int64_t rows, int64_t L);
 int kdfm_adapter_bwd(const float* dzn, const float* zs, const float* h, const float* gamma, const float* w2,
-                     const float* eps_in, float* dzs, float* dh, float* dw2, float* db2, int64_t rows, int64_t L,
-                     const uint64_t* seed, uint64_t rng_stream, void* stream);
+                     const float* eps_in, float* dzs, float* dh, float* dw2, float* db2, float* ws, int64_t ws_len,
+                     int64_t rows, int64_t L, const uint64_t* seed, uint64_t rng_stream, void* stream);
 int kdfm_fm_step_bias(const float* w_te, const float* b_te, const float* W1, const float* b1, float* cvec, float* evec,
                       int64_t L, int64_t E, int64_t steps, void* stream);
 int kdfm_fm_time_bwd(const float* dc, const float* evec, const float* W1, float* dW1, float* db1, float* dw_te,

@@ -210,12 +210,17 @@ __global__ __launch_bounds__(256) void im2col_kernel(const float* __restrict__ X
 // FilterbankFeatures (audio_preprocessing.py:93-103, 214-300): |STFT|^2 of the Hann(400)-windowed
 // frame centred in n_fft = 512, then the Slaney mel filterbank.  The DFT-as-GEMM formulation costs
 // 2 x 512 x 514 flops per frame on f32 MFMA; here one wave owns a frame and runs the real FFT as a
-// 256-point complex radix-2 FFT of z[m] = s[2m] + i s[2m+1] in LDS (8 in-place stages, twiddles
-// e^{-2 pi i j / 512} from a host-computed table), the real-FFT split
+// 256-point complex radix-2 decimation-in-frequency FFT of z[m] = s[2m] + i s[2m+1] IN REGISTERS:
+// lane l holds z[l + 64 q], q = 0..3, so the spans 128 and 64 pair a lane's own registers and the
+// spans 32..1 pair lane l with lane l ^ span, exchanged by DPP row permutations (1, 2, 4, 8) and
+// v_permlane16/32_swap (16, 32) -- no LDS traffic until the bit-reversed result is stored once
+// (the radix-2 stages in LDS cost 8 read+write passes per frame and bound the kernel on the LDS
+// pipe); twiddles e^{-2 pi i j / 512} from a host-computed table, held per lane in registers.
+// Then the real-FFT split
 //   X[k] = (Z[k] + conj Z[256-k]) / 2 - i W^k (Z[k] - conj Z[256-k]) / 2,   W = e^{-2 pi i / 512},
 // |X[k]|^2 for k = 0..256, and each mel filter's dot product over its nonzero bin range
 // [fb_lo, fb_hi).  Output mel (B*T, nfilt) f32 (log + per-feature normalisation follow).
-constexpr int FFT_N = 512, FFT_H = 256, FFT_WAVES = 4;
+constexpr int FFT_N = 512, FFT_H = 256, FFT_WAVES = 16;
 
 // wave-local LDS hand-off (each wave owns its buffers): drain this wave's LDS ops; the asm's memory
 // clobber keeps the compiler from moving LDS accesses across it
@@ -225,6 +230,49 @@ __device__ __forceinline__ void fft_wsync() {
 }
 
 __device__ __forceinline__ int bitrev8(int v) { return (int)(__builtin_bitreverse32((uint32_t)v) >> 24); }
+
+// v from lane (lane ^ D) of the wave: DPP quad / row permutations for D <= 8 (xor 4 = xor 3 then xor 7,
+// xor 8 = xor 7 then xor 15), the gfx950 half-row / half-wave swaps for 16 and 32 (swap(x, x) returns
+// [own lower part in both | own upper part in both]: the partner's value is the other one)
+template <int D>
+__device__ __forceinline__ float lane_xor(float v, int lane) {
+  const int i = __builtin_bit_cast(int, v);
+  int r;
+  if constexpr (D == 1) {
+    r = __builtin_amdgcn_mov_dpp(i, 0xB1, 0xF, 0xF, false);                 // quad_perm [1,0,3,2]
+  } else if constexpr (D == 2) {
+    r = __builtin_amdgcn_mov_dpp(i, 0x4E, 0xF, 0xF, false);                 // quad_perm [2,3,0,1]
+  } else if constexpr (D == 4) {
+    r = __builtin_amdgcn_mov_dpp(__builtin_amdgcn_mov_dpp(i, 0x1B, 0xF, 0xF, false), 0x141, 0xF, 0xF, false);
+  } else if constexpr (D == 8) {
+    r = __builtin_amdgcn_mov_dpp(__builtin_amdgcn_mov_dpp(i, 0x141, 0xF, 0xF, false), 0x140, 0xF, 0xF, false);
+  } else if constexpr (D == 16) {
+    const auto p = __builtin_amdgcn_permlane16_swap(i, i, false, false);
+    r = (lane & 16) ? (int)p[0] : (int)p[1];
+  } else {
+    static_assert(D == 32, "span");
+    const auto p = __builtin_amdgcn_permlane32_swap(i, i, false, false);
+    r = (lane & 32) ? (int)p[0] : (int)p[1];
+  }
+  return __builtin_bit_cast(float, r);
+}
+
+__device__ __forceinline__ float2 cmul(float2 a, float2 w) {
+  return make_float2(a.x * w.x - a.y * w.y, a.x * w.y + a.y * w.x);
+}
+
+// DIF stage of span D < 64 across lanes: the lane without bit D keeps a + b, the lane with it takes
+// (a - b) w (w = 1 on the lower lanes, so the twiddle multiply is branch-free)
+template <int D>
+__device__ __forceinline__ void dif_lanes(float2 (&z)[4], int lane, float2 w) {
+  const float sg = (lane & D) ? -1.f : 1.f;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float yx = lane_xor<D>(z[q].x, lane), yy = lane_xor<D>(z[q].y, lane);
+    const float2 u = make_float2(fmaf(sg, z[q].x, yx), fmaf(sg, z[q].y, yy));
+    z[q] = D == 1 ? u : cmul(u, w);
+  }
+}
 
 constexpr int FB_LDS = 4096;   // compact filterbank (nonzero ranges of every filter) staged per workgroup
 
@@ -284,36 +332,65 @@ __global__ __launch_bounds__(64 * FFT_WAVES) void logmel_fft_kernel(
   float2* Z = Zs[w];
   float* P = Pw[w];
   const int64_t nframes = B * T;
-  for (int64_t f = (int64_t)blockIdx.x * FFT_WAVES + w; f < nframes; f += (int64_t)gridDim.x * FFT_WAVES) {
-    const int64_t b = f / T, t = f - b * T;
+  // the window taps of this lane's 8 samples are the same for every frame: registers, loaded once
+  float wv[8];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int n0 = 2 * (lane + 64 * q), n1 = n0 + 1;
+    wv[2 * q] = (n0 >= off && n0 < off + nwin) ? win[n0 - off] : 0.f;
+    wv[2 * q + 1] = (n1 >= off && n1 < off + nwin) ? win[n1 - off] : 0.f;
+  }
+  // per-lane DIF twiddles W_{2D}^{e mod D} = W512^{(e mod D) 256 / D} of every span D (the lower lanes
+  // of a cross-lane span multiply by 1)
+  float2 t128[2], t64, tl[5];
+  t128[0] = W[2 * lane];
+  t128[1] = W[2 * lane + 128];
+  t64 = W[4 * lane];
+#pragma unroll
+  for (int s = 0; s < 5; ++s) {
+    const int D = 32 >> s;
+    tl[s] = (lane & D) ? W[(lane & (D - 1)) * (256 / D)] : make_float2(1.f, 0.f);
+  }
+  // software pipeline: the next frame's samples are loaded while this frame is transformed
+  const int64_t fstep = (int64_t)gridDim.x * FFT_WAVES;
+  float2 nx[4];
+  auto fetch = [&](int64_t fr) {
+    const int64_t b = fr / T, t = fr - b * T;
     const float* src = xp + b * ldx + t * hop;
-    // z[m] = s[2m] + i s[2m+1], s[n] = win[n - off] x[t hop + n] on [off, off + nwin), stored bit-reversed
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int m = lane + 64 * q;
-      const int n0 = 2 * m, n1 = 2 * m + 1;
-      const float a = (n0 >= off && n0 < off + nwin) ? win[n0 - off] * src[n0] : 0.f;
-      const float c = (n1 >= off && n1 < off + nwin) ? win[n1 - off] * src[n1] : 0.f;
-      Z[bitrev8(m)] = make_float2(a, c);
+    for (int q = 0; q < 4; ++q) nx[q] = *reinterpret_cast<const float2*>(src + 2 * (lane + 64 * q));
+  };
+  int64_t f = (int64_t)blockIdx.x * FFT_WAVES + w;
+  if (f < nframes) fetch(f);
+  for (; f < nframes; f += fstep) {
+    // z[m] = s[2m] + i s[2m+1], s[n] = win[n - off] x[t hop + n] on [off, off + nwin); lane holds m = lane + 64 q
+    float2 z[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) z[q] = make_float2(wv[2 * q] * nx[q].x, wv[2 * q + 1] * nx[q].y);
+    if (f + fstep < nframes) fetch(f + fstep);
+    // spans 128 and 64: within the lane's registers
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const float2 a = z[q], b = z[q + 2];
+      z[q] = make_float2(a.x + b.x, a.y + b.y);
+      z[q + 2] = cmul(make_float2(a.x - b.x, a.y - b.y), t128[q]);
     }
+#pragma unroll
+    for (int q = 0; q < 4; q += 2) {
+      const float2 a = z[q], b = z[q + 1];
+      z[q] = make_float2(a.x + b.x, a.y + b.y);
+      z[q + 1] = cmul(make_float2(a.x - b.x, a.y - b.y), t64);
+    }
+    dif_lanes<32>(z, lane, tl[0]);
+    dif_lanes<16>(z, lane, tl[1]);
+    dif_lanes<8>(z, lane, tl[2]);
+    dif_lanes<4>(z, lane, tl[3]);
+    dif_lanes<2>(z, lane, tl[4]);
+    dif_lanes<1>(z, lane, make_float2(1.f, 0.f));
+    // element e = lane + 64 q now holds Z[bitrev8(e)]
+#pragma unroll
+    for (int q = 0; q < 4; ++q) Z[bitrev8(lane + 64 * q)] = z[q];
     fft_wsync();   // this wave's LDS writes complete before its reads
-    // radix-2 DIT stages: butterflies j = lane, lane + 64 of 128; twiddle W256^pos = W512^(2 pos * 256/len)
-#pragma unroll
-    for (int ls = 1; ls <= 8; ++ls) {
-      const int half = 1 << (ls - 1);
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const int j = lane + 64 * q;
-        const int g = j >> (ls - 1), pos = j & (half - 1);
-        const int i0 = g * (2 * half) + pos, i1 = i0 + half;
-        const float2 wv = W[(pos << (9 - ls)) & (FFT_N - 1)];
-        const float2 u = Z[i0], v = Z[i1];
-        const float2 bv = make_float2(v.x * wv.x - v.y * wv.y, v.x * wv.y + v.y * wv.x);
-        Z[i0] = make_float2(u.x + bv.x, u.y + bv.y);
-        Z[i1] = make_float2(u.x - bv.x, u.y - bv.y);
-      }
-      fft_wsync();
-    }
     // real-FFT split and power
     for (int k = lane; k < nbins; k += 64) {
       const float2 zk = Z[k & (FFT_H - 1)], zr = Z[(FFT_H - k) & (FFT_H - 1)];
@@ -330,9 +407,19 @@ __global__ __launch_bounds__(64 * FFT_WAVES) void logmel_fft_kernel(
     for (int m = lane; m < nfilt; m += 64) {
       const int lo = Flo[m], nk = Fn[m];
       float acc = 0.f;
-      if (staged) {
+      if (staged) {   // four independent partial sums: the LDS reads of a filter's bins overlap
         const float* fr = Fc + Fo[m];
-        for (int k = 0; k < nk; ++k) acc = fmaf(fr[k], P[lo + k], acc);
+        const float* pp = P + lo;
+        float a1 = 0.f, a2 = 0.f, a3 = 0.f;
+        int k = 0;
+        for (; k + 4 <= nk; k += 4) {
+          acc = fmaf(fr[k], pp[k], acc);
+          a1 = fmaf(fr[k + 1], pp[k + 1], a1);
+          a2 = fmaf(fr[k + 2], pp[k + 2], a2);
+          a3 = fmaf(fr[k + 3], pp[k + 3], a3);
+        }
+        for (; k < nk; ++k) acc = fmaf(fr[k], pp[k], acc);
+        acc = (acc + a1) + (a2 + a3);
       } else {
         const float* row = fb + (int64_t)m * nbins + lo;
         for (int k = 0; k < nk; ++k) acc = fmaf(row[k], P[lo + k], acc);
@@ -438,7 +525,7 @@ int kdfm_logmel_fft(const float* xp, int64_t ldx, const float* window, const flo
   const int64_t groups = ceil_div(B * T, FFT_WAVES);
   static const int64_t cap = [] {   // workgroups (frames are grid-strided); KDFM_FFT_GRID overrides
     const char* v = getenv("KDFM_FFT_GRID");
-    return v && atoi(v) > 0 ? (int64_t)atoi(v) : (int64_t)2048;
+    return v && atoi(v) > 0 ? (int64_t)atoi(v) : (int64_t)512;
   }();
   const unsigned grid = (unsigned)(groups < cap ? groups : cap);
   hipLaunchKernelGGL(logmel_fft_kernel, dim3(grid), dim3(64 * FFT_WAVES), 0, as_stream(stream), xp, ldx, window,

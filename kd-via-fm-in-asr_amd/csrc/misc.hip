@@ -140,45 +140,127 @@ __global__ __launch_bounds__(256) void adapter_fwd_kernel(const float* __restric
   if (lane == 0) gamma[r] = g;
 }
 
-// backward: dzs = g*dzn ; dgl = g(1-g) * sum_c dzn*(zs-eps) ; dh = dgl*w2*(h>0) ; dw2 += dgl*h ; db2 += dgl
+// the same with 16 lanes per row (L a multiple of 16): a wave has 4 rows' loads in flight instead of
+// one row's dependent reduce-then-mix chain (205k rows of 96 at the bench shape)
+template <int PL>
+__global__ __launch_bounds__(256) void adapter_fwd16_kernel(const float* __restrict__ zs, const float* __restrict__ h,
+                                                            const float* __restrict__ w2, const float* __restrict__ b2,
+                                                            const float* __restrict__ eps_in, float* __restrict__ zn,
+                                                            float* __restrict__ gamma, int64_t rows, int L,
+                                                            const uint64_t* seed_ptr, uint64_t st) {
+  const int sub = threadIdx.x & 15;
+  const uint64_t seed = eps_in ? 0 : load_seed(seed_ptr);
+  float w2v[PL];
+#pragma unroll
+  for (int k = 0; k < PL; ++k) w2v[k] = w2[sub + 16 * k];
+  const float bias = b2[0];
+  for (int64_t r = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4); r < rows; r += (int64_t)gridDim.x * 16) {
+    float hv[PL], z[PL], e[PL];
+#pragma unroll
+    for (int k = 0; k < PL; ++k) {
+      const int64_t off = r * L + sub + 16 * k;
+      hv[k] = h[off];
+      z[k] = zs[off];
+      e[k] = eps_in ? eps_in[off] : rng_normal(seed, st, (uint64_t)off);
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < PL; ++k) s += hv[k] * w2v[k];
+#pragma unroll
+    for (int o = 8; o >= 1; o >>= 1) s += __shfl_xor(s, o, 16);
+    const float g = sigmoidf_(s + bias);
+#pragma unroll
+    for (int k = 0; k < PL; ++k) zn[r * L + sub + 16 * k] = g * z[k] + (1.f - g) * e[k];
+    if (sub == 0) gamma[r] = g;
+  }
+}
+
+// backward: dzs = g*dzn ; dgl = g(1-g) * sum_c dzn*(zs-eps) ; dh = dgl*w2*(h>0) ; dw2 += dgl*h ; db2 += dgl.
+// 16 lanes per row (lane k of the group owns columns k, k+16, ..: 64-byte coalesced segments), 4 rows per
+// wave and 16 per workgroup in flight, so a row's loads overlap the others' instead of one dependent
+// chain per row; each workgroup writes its (dw2 | db2) partial to ws, folded in workgroup order by
+// adapter_bwd_fold_kernel (deterministic in either reduction mode, no atomics)
+constexpr int AB_MAXPL = 8;   // L <= 128
+template <int PL>
 __global__ __launch_bounds__(256) void adapter_bwd_kernel(const float* __restrict__ dzn, const float* __restrict__ zs,
                                                           const float* __restrict__ h, const float* __restrict__ gamma,
                                                           const float* __restrict__ w2, const float* __restrict__ eps_in,
                                                           float* __restrict__ dzs, float* __restrict__ dh,
-                                                          float* __restrict__ dw2, float* __restrict__ db2, int64_t rows,
-                                                          int L, const uint64_t* seed_ptr, uint64_t st,
-                                                          int64_t rows_per) {
-  __shared__ float sw[4][128];
-  __shared__ float sb[4];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  float pw0 = 0.f, pw1 = 0.f, pb = 0.f;  // L <= 128: lane holds columns lane, lane+64
+                                                          float* __restrict__ part, int64_t rows, int L,
+                                                          const uint64_t* seed_ptr, uint64_t st, int64_t rows_per) {
+  __shared__ float red[16][AB_MAXPL * 16 + 1];
+  const int sub = threadIdx.x & 15, grp = threadIdx.x >> 4;   // 16 row groups of 16 lanes
   const uint64_t seed = eps_in ? 0 : load_seed(seed_ptr);
+  float pw[PL], pb = 0.f, w2v[PL];
+#pragma unroll
+  for (int k = 0; k < PL; ++k) {
+    pw[k] = 0.f;
+    w2v[k] = w2[sub + 16 * k];
+  }
   const int64_t r0 = (int64_t)blockIdx.x * rows_per;
   const int64_t r1 = (r0 + rows_per < rows) ? r0 + rows_per : rows;
-  for (int64_t r = r0 + w; r < r1; r += 4) {
+  for (int64_t r = r0 + grp; r < r1; r += 16) {
     const float g = gamma[r];
-    float s = 0.f;
-    for (int c = lane; c < L; c += 64) {
-      const float e = eps_in ? eps_in[r * L + c] : rng_normal(seed, st, (uint64_t)(r * L + c));
-      const float d = dzn[r * L + c];
-      s += d * (zs[r * L + c] - e);
-      dzs[r * L + c] = g * d;
+    float d[PL], z[PL], hv[PL], e[PL];
+#pragma unroll
+    for (int k = 0; k < PL; ++k) {
+      const int64_t off = r * L + sub + 16 * k;
+      d[k] = dzn[off];
+      z[k] = zs[off];
+      hv[k] = h[off];
+      e[k] = eps_in ? eps_in[off] : 0.f;
     }
-    const float dgl = wave_sum(s) * g * (1.f - g);
-    for (int c = lane, q = 0; c < L; c += 64, ++q) {
-      const float hv = h[r * L + c];
-      dh[r * L + c] = (hv > 0.f) ? dgl * w2[c] : 0.f;
-      if (q == 0) pw0 += dgl * hv; else pw1 += dgl * hv;
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < PL; ++k) {
+      const int64_t off = r * L + sub + 16 * k;
+      const float ev = eps_in ? e[k] : rng_normal(seed, st, (uint64_t)off);
+      s += d[k] * (z[k] - ev);
+      dzs[off] = g * d[k];
+    }
+#pragma unroll
+    for (int o = 8; o >= 1; o >>= 1) s += __shfl_xor(s, o, 16);
+    const float dgl = s * g * (1.f - g);
+#pragma unroll
+    for (int k = 0; k < PL; ++k) {
+      dh[r * L + sub + 16 * k] = (hv[k] > 0.f) ? dgl * w2v[k] : 0.f;
+      pw[k] += dgl * hv[k];
     }
     pb += dgl;
   }
-  sw[w][lane] = pw0;
-  sw[w][lane + 64] = pw1;
-  if (lane == 0) sb[w] = pb;
+#pragma unroll
+  for (int k = 0; k < PL; ++k) red[grp][sub + 16 * k] = pw[k];
+  if (sub == 0) red[grp][AB_MAXPL * 16] = pb;
   __syncthreads();
-  for (int c = threadIdx.x; c < L; c += 256) atomicAdd(dw2 + c, sw[0][c] + sw[1][c] + sw[2][c] + sw[3][c]);
-  if (threadIdx.x == 0) atomicAdd(db2, sb[0] + sb[1] + sb[2] + sb[3]);
+  // this workgroup's partial: column c summed over the 16 row groups in order
+  for (int c = threadIdx.x; c <= L; c += 256) {
+    const int cc = c < L ? c : AB_MAXPL * 16;
+    float a = 0.f;
+    for (int q = 0; q < 16; ++q) a += red[q][cc];
+    part[(int64_t)blockIdx.x * (L + 1) + c] = a;
+  }
 }
+
+// dw2[c] += sum_b part[b][c] (c < L), db2 += sum_b part[b][L]: one workgroup per column, fixed order
+__global__ __launch_bounds__(256) void adapter_bwd_fold_kernel(const float* __restrict__ part, int64_t nb, int L,
+                                                               float* __restrict__ dw2, float* __restrict__ db2) {
+  __shared__ float red[256];
+  const int c = blockIdx.x;
+  float a = 0.f;
+  for (int64_t b = threadIdx.x; b < nb; b += 256) a += part[b * (L + 1) + c];
+  red[threadIdx.x] = a;
+  __syncthreads();
+  for (int o = 128; o >= 1; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    if (c < L) dw2[c] += red[0];
+    else db2[0] += red[0];
+  }
+}
+
+constexpr int64_t AB_BLOCKS = 2048;
 
 // per FM step j (t = (S-j)/S): e_j = w_te*t + b_te ; c_j = W1[:, L:] e_j + b1   (W1 is L x (L+E))
 __global__ __launch_bounds__(256) void fm_step_bias_kernel(const float* __restrict__ w_te, const float* __restrict__ b_te,
@@ -196,33 +278,51 @@ __global__ __launch_bounds__(256) void fm_step_bias_kernel(const float* __restri
 }
 
 // given dc_j (S x L): dW1[:, L:] += dc_j e_j^T ; db1 += dc_j ; de_j = W1[:, L:]^T dc_j ;
-// dw_te += de_j * t_j ; db_te += de_j        (single block)
+// dw_te += de_j * t_j ; db_te += de_j.  Workgroup q < E owns time-embedding feature q (thread o = output
+// row o: its dW1 entry, and w_o * sum_j t_j dc_j[o] / w_o * sum_j dc_j[o] tree-reduced over o in a fixed
+// order); workgroup E sums db1.  (One workgroup looping 8 x L serial loads per feature took 280 us.)
 __global__ __launch_bounds__(256) void fm_time_bwd_kernel(const float* __restrict__ dc, const float* __restrict__ evec,
                                                           const float* __restrict__ W1, float* __restrict__ dW1,
                                                           float* __restrict__ db1, float* __restrict__ dw_te,
                                                           float* __restrict__ db_te, int L, int E, int S) {
-  for (int idx = threadIdx.x; idx < L * E; idx += 256) {
-    const int o = idx / E, q = idx % E;
-    float acc = 0.f;
-    for (int j = 0; j < S; ++j) acc += dc[j * L + o] * evec[j * E + q];
-    dW1[o * (L + E) + L + q] += acc;
-  }
-  for (int o = threadIdx.x; o < L; o += 256) {
-    float acc = 0.f;
-    for (int j = 0; j < S; ++j) acc += dc[j * L + o];
-    db1[o] += acc;
-  }
-  for (int q = threadIdx.x; q < E; q += 256) {
-    float gw = 0.f, gb = 0.f;
-    for (int j = 0; j < S; ++j) {
-      const float t = (float)(S - j) / (float)S;
-      float de = 0.f;
-      for (int o = 0; o < L; ++o) de += W1[o * (L + E) + L + q] * dc[j * L + o];
-      gw += de * t;
-      gb += de;
+  __shared__ float rw[256], rb[256];
+  const int q = blockIdx.x, o = threadIdx.x;
+  if (q == E) {
+    if (o < L) {
+      float acc = 0.f;
+      for (int j = 0; j < S; ++j) acc += dc[j * L + o];
+      db1[o] += acc;
     }
-    dw_te[q] += gw;
-    db_te[q] += gb;
+    return;
+  }
+  float gw = 0.f, gb = 0.f;
+  if (o < L) {
+    float dw = 0.f, st = 0.f, s1 = 0.f;
+    for (int j = 0; j < S; ++j) {
+      const float d = dc[j * L + o];
+      dw += d * evec[j * E + q];
+      st += d * ((float)(S - j) / (float)S);
+      s1 += d;
+    }
+    const int64_t wi = (int64_t)o * (L + E) + L + q;
+    dW1[wi] += dw;
+    const float w = W1[wi];
+    gw = w * st;
+    gb = w * s1;
+  }
+  rw[o] = gw;
+  rb[o] = gb;
+  __syncthreads();
+  for (int h = 128; h >= 1; h >>= 1) {
+    if (o < h) {
+      rw[o] += rw[o + h];
+      rb[o] += rb[o + h];
+    }
+    __syncthreads();
+  }
+  if (o == 0) {
+    dw_te[q] += rw[0];
+    db_te[q] += rb[0];
   }
 }
 
@@ -354,27 +454,56 @@ int kdfm_adapter_fwd(const float* zs, const float* h, const float* w2, const flo
   KDFM_REQUIRE(eps_in || seed, "need injected eps or a seed");
   KDFM_REQUIRE(L > 0 && L <= 128, "latent dim in (0,128]");
   if (rows == 0) return KDFM_OK;
-  hipLaunchKernelGGL(adapter_fwd_kernel, dim3((unsigned)ceil_div(rows, 4)), dim3(256), 0, as_stream(stream), zs, h, w2,
+  hipStream_t st = as_stream(stream);
+  if (L % 16 == 0) {
+    const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(rows, 16), 4096);
+    switch (L / 16) {
+#define AF_CASE(n)                                                                                                  \
+  case n:                                                                                                           \
+    hipLaunchKernelGGL(adapter_fwd16_kernel<n>, dim3(grid), dim3(256), 0, st, zs, h, w2, b2, eps_in, zn, gamma, rows, \
+                       (int)L, seed, rng_stream);                                                                   \
+    break;
+      AF_CASE(1) AF_CASE(2) AF_CASE(3) AF_CASE(4) AF_CASE(5) AF_CASE(6) AF_CASE(7) AF_CASE(8)
+#undef AF_CASE
+    }
+    return check_launch("kdfm_adapter_fwd");
+  }
+  hipLaunchKernelGGL(adapter_fwd_kernel, dim3((unsigned)ceil_div(rows, 4)), dim3(256), 0, st, zs, h, w2,
                      b2, eps_in, zn, gamma, rows, (int)L, seed, rng_stream);
   return check_launch("kdfm_adapter_fwd");
 }
 
+int64_t kdfm_adapter_bwd_ws(int64_t rows, int64_t L) {
+  const int64_t nb = rows < 16 ? 1 : (kdfm::ceil_div(rows, 16) < kdfm::AB_BLOCKS ? kdfm::ceil_div(rows, 16) : kdfm::AB_BLOCKS);
+  return nb * (L + 1);
+}
+
 int kdfm_adapter_bwd(const float* dzn, const float* zs, const float* h, const float* gamma, const float* w2,
-                     const float* eps_in, float* dzs, float* dh, float* dw2, float* db2, int64_t rows, int64_t L,
-                     const uint64_t* seed, uint64_t rng_stream, void* stream) {
+                     const float* eps_in, float* dzs, float* dh, float* dw2, float* db2, float* ws, int64_t ws_len,
+                     int64_t rows, int64_t L, const uint64_t* seed, uint64_t rng_stream, void* stream) {
   using namespace kdfm;
-  KDFM_REQUIRE(dzn && zs && h && gamma && w2 && dzs && dh && dw2 && db2, "null pointer");
+  KDFM_REQUIRE(dzn && zs && h && gamma && w2 && dzs && dh && dw2 && db2 && ws, "null pointer");
   KDFM_REQUIRE(eps_in || seed, "need injected eps or a seed");
-  KDFM_REQUIRE(L > 0 && L <= 128, "latent dim in (0,128]");
+  KDFM_REQUIRE(L > 0 && L <= 128 && L % 16 == 0, "latent dim a multiple of 16 in (0,128]");
   if (rows == 0) return KDFM_OK;
-  int64_t blocks = ceil_div(rows, 64);
-  if (blocks > 2048) blocks = 2048;
-  if (deterministic()) blocks = 1;  // dw2 / db2 summed by one workgroup in a fixed order
-  const int64_t rp = ceil_div(rows, blocks);
-  blocks = ceil_div(rows, rp);
-  hipLaunchKernelGGL(adapter_bwd_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), dzn, zs, h, gamma, w2,
-                     eps_in, dzs, dh, dw2, db2, rows, (int)L, seed, rng_stream, rp);
-  return check_launch("kdfm_adapter_bwd");
+  int64_t nb = kdfm_adapter_bwd_ws(rows, L) / (L + 1);
+  KDFM_REQUIRE(ws_len >= nb * (L + 1), "workspace too small (kdfm_adapter_bwd_ws)");
+  const int64_t rp = ceil_div(rows, nb);
+  nb = ceil_div(rows, rp);
+  hipStream_t st = as_stream(stream);
+  switch (L / 16) {
+#define AB_CASE(n)                                                                                                  \
+  case n:                                                                                                           \
+    hipLaunchKernelGGL(adapter_bwd_kernel<n>, dim3((unsigned)nb), dim3(256), 0, st, dzn, zs, h, gamma, w2, eps_in,    \
+                       dzs, dh, ws, rows, (int)L, seed, rng_stream, rp);                                             \
+    break;
+    AB_CASE(1) AB_CASE(2) AB_CASE(3) AB_CASE(4) AB_CASE(5) AB_CASE(6) AB_CASE(7) AB_CASE(8)
+#undef AB_CASE
+  }
+  int rc = check_launch("kdfm_adapter_bwd");
+  if (rc) return rc;
+  hipLaunchKernelGGL(adapter_bwd_fold_kernel, dim3((unsigned)(L + 1)), dim3(256), 0, st, ws, nb, (int)L, dw2, db2);
+  return check_launch("kdfm_adapter_bwd(fold)");
 }
 
 int kdfm_fm_step_bias(const float* w_te, const float* b_te, const float* W1, const float* b1, float* cvec, float* evec,
@@ -391,7 +520,8 @@ int kdfm_fm_time_bwd(const float* dc, const float* evec, const float* W1, float*
                      float* db_te, int64_t L, int64_t E, int64_t steps, void* stream) {
   using namespace kdfm;
   KDFM_REQUIRE(dc && evec && W1 && dW1 && db1 && dw_te && db_te, "null pointer");
-  hipLaunchKernelGGL(fm_time_bwd_kernel, dim3(1), dim3(256), 0, as_stream(stream), dc, evec, W1, dW1, db1, dw_te, db_te,
+  KDFM_REQUIRE(L >= 1 && L <= 256 && E >= 1 && steps >= 1, "fm_time_bwd: 1 <= L <= 256");
+  hipLaunchKernelGGL(fm_time_bwd_kernel, dim3((unsigned)(E + 1)), dim3(256), 0, as_stream(stream), dc, evec, W1, dW1, db1, dw_te, db_te,
                      (int)L, (int)E, (int)steps);
   return check_launch("kdfm_fm_time_bwd");
 }

@@ -169,7 +169,8 @@ SIGNATURES: dict[str, tuple] = {
     "kdfm_kl_div_logits": (_i32, [P, P, P, P, _i64, _i64, _f32, _f32, _f32, P]),
     "kdfm_loss_combine": (_i32, [P, _i64, P, P, P, _f32, P, P]),
     "kdfm_adapter_fwd": (_i32, [P, P, P, P, P, P, P, _i64, _i64, P, C.c_uint64, P]),
-    "kdfm_adapter_bwd": (_i32, [P, P, P, P, P, P, P, P, P, P, _i64, _i64, P, C.c_uint64, P]),
+    "kdfm_adapter_bwd_ws": (_i64, [_i64, _i64]),
+    "kdfm_adapter_bwd": (_i32, [P, P, P, P, P, P, P, P, P, P, P, _i64, _i64, _i64, P, C.c_uint64, P]),
     "kdfm_fm_step_bias": (_i32, [P, P, P, P, P, P, _i64, _i64, _i64, P]),
     "kdfm_fm_time_bwd": (_i32, [P, P, P, P, P, P, P, _i64, _i64, _i64, P]),
     "kdfm_fill": (_i32, [P, _f32, _i64, P]),

@@ -19,7 +19,7 @@ from .conformer import EncoderRun, EncoderShapes, compute_lengths, encoder_backw
     encoder_forward_steps, layer_images, make_workspace
 from .frontend import FrontendConsts, frontend_forward, mel_frames, specaugment_
 from .encfm import EncFMWorkspace, encfm_backward, encfm_forward
-from .heads import HeadsWorkspace, heads_backward, heads_forward
+from .heads import HeadsWorkspace, heads_backward, heads_forward, tae_forward
 from .overlap import WGRAD
 
 # Stream priorities (KDFM_STREAM_PRIO=1): the critical-path streams (the compute stream that carries
@@ -252,6 +252,10 @@ class Ver5Engine:
         len2 = torch.empty_like(mel_len)
         len1, len2 = compute_lengths(cfg, wav_len, mel_len, len1, len2, cfg.hop)
         seed = self.seed
+        encfm = cfg.kd_model == "encfm"
+        # kl | recon, kd_pre, fm_pre, kd_post, fm_post (heads.RECON..FM_POST) | diffkd | sum of the layer-KD
+        # terms and diffkd (zeroed before the teacher stream forks: its auto-encoder adds the recon term)
+        acc = torch.zeros(8, device=dev)
         if K.get_math() == "bf16":   # bf16 twins of the weights the skinny products stream
             self.student.refresh_bf16()
             self.teacher.refresh_bf16()
@@ -326,8 +330,17 @@ class Ver5Engine:
                          self.teacher.P["teacher.decoder.decoder_layers.0.bias"], tlogits)
             for t in (tfeats, tlogits, mel_t, mel_len, len1, len2):
                 t.record_stream(side)
+        # ---- the ver5 heads' TeacherAutoEncoder reads only the teacher: on the teacher stream, right after
+        # the teacher encoder, off the student's chain (the main stream joins the teacher stream below) ----
+        tae = None
+        if not encfm:
+            n_st = cfg.n_layers * Ss.rows
+            tae = (torch.empty(n_st, cfg.latent, device=dev), torch.empty(n_st, St.d, device=dev))
+            with torch.cuda.stream(side):
+                tae_forward(cfg, self.student.P, tfeats.view(n_st, St.d), tae[0], tae[1], acc[1:2])
+            for t in (*tae, acc, tfeats):
+                t.record_stream(side)
         # ---- decoders, CTC, logit KD ----
-        encfm = cfg.kd_model == "encfm"
         dec_in = sfeats[-1]
         if encfm:
             # asr_train.py: the router + flow matching over every hooked layer pair (it needs the teacher's
@@ -347,9 +360,6 @@ class Ver5Engine:
             main.wait_stream(side)
         # ---- CTC + logit KD on a third stream: they only need the two logit tensors, and their
         # result is first needed after the KD heads' forward, so the serial CTC recursion overlaps it ----
-        # kl | recon, kd_pre, fm_pre, kd_post, fm_post (heads.RECON..FM_POST) | diffkd | sum of the layer-KD
-        # terms and diffkd
-        acc = torch.zeros(8, device=dev)
         aux = self._aux_stream()
         aux.wait_stream(main)
         Umax = targets.shape[1]
@@ -373,7 +383,7 @@ class Ver5Engine:
             with K.region("heads_forward"):
                 hctx = heads_forward(cfg, self.student.P, sfeats.view(n, Ss.d), tfeats.view(n, St.d), T, self.hws,
                                      acc[1:6], seed=seed, eps=eps, save=save, Pfix=self.fixed.P,
-                                     acc_diffkd=acc[6:7])
+                                     acc_diffkd=acc[6:7], tae=tae)
                 K.colsum(acc[2:7].view(5, 1), acc[7:8], accumulate=False)
         # device (recon, kd_pre, fm_pre, kd_post, fm_post, diffkd): the v/* log keys
         self.kd_terms = acc[1:7]

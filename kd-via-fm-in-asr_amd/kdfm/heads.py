@@ -386,11 +386,38 @@ def _diffkd_backward(cfg, P, G, c, s_feats, T, ws, ds_feats, dev):
     K.linear_dx(dzs, P["diffkd.proj.weight"].view(Lt, Cs), ds_feats, R=ds_feats, rscale=1.0)
 
 
+def tae_forward(cfg: Ver5Config, P, t_feats, zt, drec, acc_recon):
+    """TeacherAutoEncoder over the stacked teacher layer outputs t_feats (n, d_teacher): z_t = enc(t) into
+    zt (n, latent), the recon MSE (mean over B*C*T per layer, summed over layers) added into acc_recon and
+    its gradient d/d t_rec into drec (n, d_teacher).  It reads nothing of the student, so the engine issues
+    it on the teacher stream right after the teacher encoder (off the student's critical path)."""
+    n = t_feats.shape[0]
+    Lt, Ct = cfg.latent, cfg.d_teacher
+    inv_rec = 1.0 / ((n // cfg.n_layers) * Ct)
+    K.linear(t_feats, P["tae.enc.weight"].view(Lt, Ct), P["tae.enc.bias"], zt)
+    K.linear(zt, P["tae.dec.weight"].view(Ct, Lt), P["tae.dec.bias"], drec, R=t_feats, rscale=2.0 * inv_rec,
+             mse=(acc_recon, inv_rec))
+
+
+def tae_backward(cfg: Ver5Config, P, G, zt, drec, t_feats, dzt):
+    """TeacherAutoEncoder backward (recon only; z_t is detached for every KD target): weight gradients
+    only, nothing flows to the student, so all of it (the dz_t product included, into the caller's dzt)
+    runs on the weight-gradient stream."""
+    Lt, Ct = cfg.latent, cfg.d_teacher
+
+    def work():
+        K.linear_dw(drec, zt, G["tae.dec.weight"].view(Ct, Lt), db=G["tae.dec.bias"])
+        K.linear_dx(drec, P["tae.dec.weight"].view(Ct, Lt), dzt)
+        K.linear_dw(dzt, t_feats, G["tae.enc.weight"].view(Lt, Ct), db=G["tae.enc.bias"])
+    WGRAD.run(work, drec, zt, t_feats, dzt)
+
+
 def heads_forward(cfg: Ver5Config, P, s_feats, t_feats, T, ws: HeadsWorkspace, acc, *, seed, eps=None, save=True,
-                  Pfix=None, acc_diffkd=None):
+                  Pfix=None, acc_diffkd=None, tae=None):
     """s_feats (n, d_student) and t_feats (n, d_teacher) stacked student/teacher layer outputs
     (n = layers*B*T').  acc: device (5,) f32 accumulators [recon, kd_pre, fm_pre, kd_post, fm_post]
-    (added to; the slots a version does not use stay untouched).  Returns ctx for backward."""
+    (added to; the slots a version does not use stay untouched).  tae: (zt, drec) when the caller has
+    already run tae_forward (recon added into acc[0] there).  Returns ctx for backward."""
     dev = s_feats.device
     n = s_feats.shape[0]
     Lt, Ct = cfg.latent, cfg.d_teacher
@@ -398,12 +425,11 @@ def heads_forward(cfg: Ver5Config, P, s_feats, t_feats, T, ws: HeadsWorkspace, a
     per_layer_rows = n // cfg.n_layers
     inv_lat = 1.0 / (per_layer_rows * Lt)
     # ---- TeacherAutoEncoder + recon MSE (mean over B*C*T per layer, summed over layers) ----
-    zt = _empty(n, Lt, dev=dev)
-    K.linear(t_feats, P["tae.enc.weight"].view(Lt, Ct), P["tae.enc.bias"], zt)
-    drec = _empty(n, Ct, dev=dev)
-    inv_rec = 1.0 / (per_layer_rows * Ct)
-    K.linear(zt, P["tae.dec.weight"].view(Ct, Lt), P["tae.dec.bias"], drec, R=t_feats, rscale=2.0 * inv_rec,
-             mse=(acc[RECON:RECON + 1], inv_rec))
+    if tae is None:
+        zt, drec = _empty(n, Lt, dev=dev), _empty(n, Ct, dev=dev)
+        tae_forward(cfg, P, t_feats, zt, drec, acc[RECON:RECON + 1])
+    else:
+        zt, drec = tae
     # ---- StudentProjector ----
     zs = _empty(n, Lt, dev=dev)
     K.linear(s_feats, P["sproj.proj.weight"].view(Lt, cfg.d_student), P["sproj.proj.bias"], zs)
@@ -461,12 +487,7 @@ def heads_backward(cfg: Ver5Config, P, G, ctx, ws: HeadsWorkspace, ds_feats, *, 
                                   db=G["sproj.proj.bias"]), dzs, ctx["s_feats"])
     K.linear_dx(dzs, P["sproj.proj.weight"].view(Lt, cfg.d_student), ds_feats)
     del dzs
-    # ---- TeacherAutoEncoder backward (recon only; z_t is detached for every KD target) ----
-    drec, zt = ctx["drec"], ctx["zt"]
-    WGRAD.run(lambda: K.linear_dw(drec, zt, G["tae.dec.weight"].view(Ct, Lt), db=G["tae.dec.bias"]), drec, zt)
-    dzt = _empty(n, Lt, dev=dev)
-    K.linear_dx(drec, P["tae.dec.weight"].view(Ct, Lt), dzt)
-    WGRAD.run(lambda: K.linear_dw(dzt, ctx["t_feats"], G["tae.enc.weight"].view(Lt, Ct), db=G["tae.enc.bias"]), dzt,
-              ctx["t_feats"])
+    # ---- TeacherAutoEncoder backward ----
+    tae_backward(cfg, P, G, ctx["zt"], ctx["drec"], ctx["t_feats"], _empty(n, Lt, dev=dev))
     if "diffkd" in ctx:
         _diffkd_backward(cfg, P, G, ctx.pop("diffkd"), ctx["s_feats"], T, ws, ds_feats, dev)

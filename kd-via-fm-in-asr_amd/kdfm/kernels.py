@@ -1294,8 +1294,9 @@ def adapter_fwd(zs, h, w2, b2, eps_in, zn, gamma, seed, rng_stream):
 
 def adapter_bwd(dzn, zs, h, gamma, w2, eps_in, dzs, dh, dw2, db2, seed, rng_stream):
     rows, L = zs.shape
+    ws = scratch(zs.device, int(_lib.lib().kdfm_adapter_bwd_ws(rows, L)))
     call("kdfm_adapter_bwd", ptr(dzn), ptr(zs), ptr(h), ptr(gamma), ptr(w2), ptr(eps_in), ptr(dzs), ptr(dh),
-         ptr(dw2), ptr(db2), rows, L, ptr(seed), int(rng_stream), _s())
+         ptr(dw2), ptr(db2), ptr(ws), ws.numel(), rows, L, ptr(seed), int(rng_stream), _s())
 
 
 def fm_step_bias(w_te, b_te, W1, b1, cvec, evec, L, E, steps):

@@ -116,3 +116,36 @@ def test_grad_stats_and_nonfinite_skip():
     K.adamw_noam(p, grad, m, v, step, 2.0, 176, 10, 1e-6, 0.9, 0.98, 1e-9, 1e-3, 1.0, lr_out=lr, gstats=out)
     torch.cuda.synchronize()
     assert not torch.equal(p, p0)
+
+
+def test_resumed_moments_restart_bias_correction():
+    """A resume whose AdamW moments could not be restored (a reference checkpoint without optimizer
+    state: checkpoint.restore_lightning_ckpt sets adam_base = global_step) must take the first update
+    with the size of a FRESH AdamW step 1 at the resumed Noam learning rate -- torch restarts its own
+    step counter with fresh moments -- not with bias corrections of ~1 on zeroed moments (ADVICE r2:
+    3-6.5x too large).  Reference: torch.optim.AdamW step 1 at lr = noam(k)."""
+    from kdfm import kernels as K
+    n, k = 20_000, 4568
+    g = torch.Generator().manual_seed(4)
+    p0 = torch.randn(n, generator=g)
+    grad = torch.randn(n, generator=g)
+    base, d_model, warm, min_lr, wd = 2.0, 176, 10000, 1e-6, 1e-3
+    dev = torch.device("cuda")
+    p = p0.to(dev)
+    m = torch.zeros(n, device=dev)
+    v = torch.zeros(n, device=dev)
+    step = torch.tensor([k], dtype=torch.int64, device=dev)
+    adam_base = torch.tensor([k - 1], dtype=torch.int64, device=dev)
+    lr = torch.zeros(1, device=dev)
+    K.adamw_noam(p, grad.to(dev), m, v, step, base, d_model, warm, min_lr, 0.9, 0.98, 1e-9, wd, 1.0, lr_out=lr,
+                 adam_base=adam_base)
+    torch.cuda.synchronize()
+    s = max(1, k - 1)
+    want_lr = max(base * d_model ** -0.5 * min(s ** -0.5, s * warm ** -1.5), min_lr) if s > warm else \
+        base * d_model ** -0.5 * min(s ** -0.5, s * warm ** -1.5)
+    assert abs(lr.item() - want_lr) <= 1e-6 * want_lr
+    ref = p0.clone().requires_grad_(True)
+    opt = torch.optim.AdamW([ref], lr=want_lr, betas=(0.9, 0.98), eps=1e-9, weight_decay=wd)
+    ref.grad = grad.clone()
+    opt.step()
+    torch.testing.assert_close(p.cpu(), ref.detach(), rtol=1e-5, atol=1e-6)

@@ -50,7 +50,7 @@ def _oracle_params(cfg, eng):
                         subsampling_conv_channels=cfg.subsampling_conv_channels,
                         causal_downsampling=cfg.causal_downsampling, version=cfg.version,
                         kd_loss_type=cfg.kd_loss_type, use_diffkd=cfg.use_diffkd, diffkd_steps=cfg.diffkd_steps,
-                        vocab=cfg.vocab)
+                        vocab=cfg.vocab, d_teacher=cfg.d_teacher, heads_teacher=cfg.heads_teacher)
     p = {}
     p.update(O.frontend_buffers(ocfg))
     p.update(O.frontend_buffers(ocfg, "teacher.preprocessor.featurizer."))
@@ -103,8 +103,11 @@ DW8C = dict(subsampling="dw_striding", subsampling_factor=8, subsampling_conv_ch
     (2, 2, 19200, [19200, 16123], 12, [12, 7], dict(use_diffkd=True)),
     # a V = 1024 BPE vocabulary (1025 decoder classes; conformer_ctc_bpe.yaml:87, SURVEY §8 V sensitivity)
     (2, 2, 19200, [19200, 16123], 12, [12, 7], dict(vocab=1024)),
+    # teacher as wide as the student: the two encoders (issued interleaved on two streams) must keep
+    # separate workspaces (the workspace key now includes the parameter prefix)
+    (2, 2, 19200, [19200, 16123], 12, [12, 7], dict(d_teacher=88, heads_teacher=2)),
 ], ids=["2L-1.2s", "16L-1s", "16L-16s", "16L-16s-overlapped", "2L-1.2s-dw4", "2L-1.2s-dw8-causal", "2L-1.2s-ver6", "2L-1.2s-ver7",
-        "2L-1.2s-ver8-l1", "2L-1.2s-diffkd", "2L-1.2s-V1024"])
+        "2L-1.2s-ver8-l1", "2L-1.2s-diffkd", "2L-1.2s-V1024", "2L-1.2s-equal-widths"])
 def test_ver5_step_matches_oracle(n_layers, B, N, lens, U, tl, sub):
     from kdfm.config import sub_dims
     cfg, eng, wav, wl, tg, tgl, g = _build(n_layers, B, N, lens, U, tl, sub=sub)

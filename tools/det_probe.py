@@ -1,0 +1,73 @@
+"""Which stage makes the teacher-graph forward differ from the eager one?  Runs the
+test_determinism bf16 'teacher-graph-vs-eager' forward twice and compares every frontend output
+(teacher and student, in call order) and the hooked layer outputs bitwise.
+usage: python tools/det_probe.py"""
+import os
+import sys
+from dataclasses import replace
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "kd-via-fm-in-asr_amd"))
+import torch  # noqa: E402
+
+from kdfm import engine as E  # noqa: E402
+from kdfm.config import DEFAULT  # noqa: E402
+
+rec = []
+orig = E.frontend_forward
+
+
+def patched(*a, **k):
+    out = orig(*a, **k)
+    rec.append(("frontend", out, out.clone(), k.get("dither")))   # clone: stream-ordered right after the call
+    return out
+
+
+E.frontend_forward = patched
+g = torch.Generator().manual_seed(21)
+cfg = replace(DEFAULT, n_layers=16, deterministic=True)
+B, N, lens = 4, 256000, [256000, 256000, 230000, 256000]
+U = 60
+wav = (0.1 * torch.randn(B, N, generator=g)).cuda()
+wl = torch.tensor(lens, dtype=torch.int64).cuda()
+tg = torch.randint(0, cfg.vocab, (B, U), generator=g).cuda()
+tl = torch.full((B,), U, dtype=torch.int64).cuda()
+
+
+def run(graph):
+    rec.clear()
+    eng = E.Ver5Engine(cfg, "cuda", teacher_seed=0, student_seed=1, heads_seed=2)
+    eng.teacher_graph = graph
+    eng.set_seed(77)
+    eng.advance_rng()
+    ctx = eng.forward(wav, wl, tg, tl, train=True)
+    torch.cuda.synchronize()
+    outs = [(n, t.clone(), c, dz) for n, t, c, dz in rec]
+    return outs, ctx["sfeats"].clone()
+
+
+def where(a, b):
+    d = (a - b).abs()
+    nz = (d > 0).nonzero()
+    if nz.numel() == 0:
+        return "identical"
+    bad = ~torch.isfinite(a) | ~torch.isfinite(b)
+    return (f"{nz.shape[0]} differing elements, first {nz[0].tolist()} last {nz[-1].tolist()}, "
+            f"utterances {sorted(set(nz[:, 0].tolist()))}, frames {nz[:, 1].min().item()}..{nz[:, 1].max().item()}, "
+            f"non-finite {bad.sum().item()}")
+
+
+for trial in range(4):
+    o1, f1 = run(True)
+    o2, f2 = run(False)
+    s1 = [o for o in o1 if o[3] and o[3] > 0]   # the student's (dithered) frontend
+    s2 = [o for o in o2 if o[3] and o[3] > 0]
+    t1 = [o for o in o1 if not o[3]]
+    t2 = [o for o in o2 if not o[3]]
+    print(f"trial {trial}: sfeats equal={torch.equal(f1, f2)}", flush=True)
+    print(f"  student mel right after the call: {where(s1[0][2], s2[0][2])}", flush=True)
+    print(f"  student mel at the end of forward: {where(s1[0][1], s2[0][1])}", flush=True)
+    print(f"  graph-run student mel: after call vs end: {where(s1[0][2], s1[0][1])}", flush=True)
+    print(f"  eager-run student mel: after call vs end: {where(s2[0][2], s2[0][1])}", flush=True)
+    for i, o in enumerate(t1):
+        print(f"  teacher mel graph-run call {i} (end) vs eager: {where(o[1], t2[0][1])}", flush=True)
