@@ -601,6 +601,9 @@ int kdfm_bn_finalize(const double* stats, const float* running_mean, const float
                      float* rstd, int64_t d, int64_t count, float eps, void* stream);
 int kdfm_bn_running_update(float* running_mean, float* running_var, const double* stats, int64_t d, int64_t count,
                            float momentum, void* stream);
+/* training step: kdfm_bn_finalize from the batch sums plus kdfm_bn_running_update in one launch */
+int kdfm_bn_finalize_running(const double* stats, float* running_mean, float* running_var, float* mean, float* rstd,
+                             int64_t d, int64_t count, float eps, float momentum, void* stream);
 int kdfm_bn_silu_fwd(const float* y, const float* mean, const float* rstd, const float* gamma, const float* beta,
                      float* z, int64_t rows, int64_t d, void* stream);
 int kdfm_bn_silu_bwd(const float* dz, const float* y, const float* mean, const float* rstd, const float* gamma,

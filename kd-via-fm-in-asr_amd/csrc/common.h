@@ -199,5 +199,7 @@ inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s);
 // out[n] += scale * sum_m X[m*ld + n]  (n < N); defined in runtime.hip.  Used to fold per-block
 // column partials written by reduction-heavy backward kernels (deterministic, no hot atomics).
 int launch_colsum(const float* X, float* out, int64_t M, int64_t N, int64_t ld, float scale, hipStream_t st);
+int launch_colsum2(const float* X, float* out, int64_t n1, float* out2, int64_t M, int64_t N, int64_t ld, float scale,
+                   hipStream_t st);
 
 }  // namespace kdfm

@@ -188,6 +188,23 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const double* __restri
   }
 }
 
+// training step: batch mean/rstd AND the running-statistics update in one launch
+__global__ __launch_bounds__(256) void bn_finalize_running_kernel(const double* __restrict__ stats,
+                                                                  float* __restrict__ rm, float* __restrict__ rv,
+                                                                  float* __restrict__ mean, float* __restrict__ rstd,
+                                                                  int64_t d, double count, float eps, float momentum) {
+  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (c >= d) return;
+  const double m = stats[c] / count;
+  double var = stats[d + c] / count - m * m;
+  if (var < 0.0) var = 0.0;
+  mean[c] = (float)m;
+  rstd[c] = (float)(1.0 / sqrt(var + (double)eps));
+  const double unb = count > 1.0 ? var * count / (count - 1.0) : var;
+  rm[c] = (float)((1.0 - momentum) * rm[c] + momentum * m);
+  rv[c] = (float)((1.0 - momentum) * rv[c] + momentum * unb);
+}
+
 __global__ __launch_bounds__(256) void bn_running_kernel(float* __restrict__ rm, float* __restrict__ rv,
                                                          const double* __restrict__ stats, int64_t d, double count,
                                                          float momentum) {
@@ -251,7 +268,13 @@ __global__ __launch_bounds__(256) void bn_silu_bwd_apply_kernel(const float* __r
                                                                 const float* __restrict__ gm,
                                                                 const float* __restrict__ bt,
                                                                 const double* __restrict__ red, float* __restrict__ dy,
+                                                                float* __restrict__ dgamma, float* __restrict__ dbeta,
                                                                 int64_t n, int64_t d, double count, int batch_stats) {
+  if (blockIdx.x == 0)   // the affine parameters' gradients (the reduction's totals): one launch fewer
+    for (int64_t c = threadIdx.x; c < d; c += 256) {
+      dgamma[c] += (float)red[d + c];
+      dbeta[c] += (float)red[c];
+    }
   const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (idx >= n) return;
   const int64_t c = idx % d;
@@ -265,14 +288,6 @@ __global__ __launch_bounds__(256) void bn_silu_bwd_apply_kernel(const float* __r
     v = gm[c] * rstd[c] * dyb;
   }
   dy[idx] = v;
-}
-
-__global__ void bn_param_grad_kernel(const double* __restrict__ red, float* __restrict__ dgamma,
-                                     float* __restrict__ dbeta, int64_t d) {
-  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (c >= d) return;
-  dgamma[c] += (float)red[d + c];
-  dbeta[c] += (float)red[c];
 }
 
 // Backward of the depthwise conv over one (TT frames x CT channels) tile of one utterance:
@@ -471,9 +486,7 @@ int kdfm_dwconv_bwd(const float* dy, const float* g, const float* w, float* dg, 
   int rc = check_launch("kdfm_dwconv_bwd");
   if (rc) return rc;
   const int64_t ld = d * (K + 1);
-  rc = launch_colsum(ws, dw, B * ntt, d * K, ld, 1.f, st);
-  if (rc) return rc;
-  return launch_colsum(ws + d * K, db, B * ntt, d, ld, 1.f, st);
+  return launch_colsum2(ws, dw, d * K, db, B * ntt, ld, ld, 1.f, st);   // [dw | db] partial columns, one fold
 }
 
 int kdfm_bn_finalize(const double* stats, const float* running_mean, const float* running_var, float* mean,
@@ -484,6 +497,15 @@ int kdfm_bn_finalize(const double* stats, const float* running_mean, const float
   hipLaunchKernelGGL(bn_finalize_kernel, dim3((unsigned)ceil_div(d, 256)), dim3(256), 0, as_stream(stream), stats,
                      running_mean, running_var, mean, rstd, d, (double)count, eps);
   return check_launch("kdfm_bn_finalize");
+}
+
+int kdfm_bn_finalize_running(const double* stats, float* running_mean, float* running_var, float* mean, float* rstd,
+                             int64_t d, int64_t count, float eps, float momentum, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(stats && running_mean && running_var && mean && rstd, "null pointer");
+  hipLaunchKernelGGL(bn_finalize_running_kernel, dim3((unsigned)ceil_div(d, 256)), dim3(256), 0, as_stream(stream),
+                     stats, running_mean, running_var, mean, rstd, d, (double)count, eps, momentum);
+  return check_launch("kdfm_bn_finalize_running");
 }
 
 int kdfm_bn_running_update(float* running_mean, float* running_var, const double* stats, int64_t d, int64_t count,
@@ -528,12 +550,8 @@ int kdfm_bn_silu_bwd(const float* dz, const float* y, const float* mean, const f
   int rc = check_launch("kdfm_bn_silu_bwd(reduce)");
   if (rc) return rc;
   hipLaunchKernelGGL(bn_silu_bwd_apply_kernel, dim3((unsigned)ceil_div(rows * d, 256)), dim3(256), 0, st, dz, y, mean,
-                     rstd, gamma, beta, red_ws, dy, rows * d, d, (double)rows, batch_stats);
-  rc = check_launch("kdfm_bn_silu_bwd(apply)");
-  if (rc) return rc;
-  hipLaunchKernelGGL(bn_param_grad_kernel, dim3((unsigned)ceil_div(d, 256)), dim3(256), 0, st, red_ws, dgamma, dbeta,
-                     d);
-  return check_launch("kdfm_bn_silu_bwd(params)");
+                     rstd, gamma, beta, red_ws, dy, dgamma, dbeta, rows * d, d, (double)rows, batch_stats);
+  return check_launch("kdfm_bn_silu_bwd(apply)");
 }
 
 }  // extern "C"

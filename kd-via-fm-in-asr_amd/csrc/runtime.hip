@@ -29,8 +29,11 @@ namespace {
 // out[n] (+)= scale * sum_{m<M} X[m*ld + n].  grid = (column groups of 64, row slabs); lane owns a
 // column, the 4 waves stride the slab's rows with 4 independent accumulators each (latency hiding),
 // LDS combine, one global atomic per column per block.
+// out[n] += scale * sum_m X[m, n]; with out2, the columns n >= n1 go to out2[n - n1] instead (two
+// adjacent partial blocks, e.g. a weight and a bias gradient, folded by one launch)
 __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ X, float* __restrict__ out,
-                                                     int64_t M, int64_t N, int64_t ld, int64_t rows_per, float scale) {
+                                                     float* __restrict__ out2, int64_t n1, int64_t M, int64_t N,
+                                                     int64_t ld, int64_t rows_per, float scale) {
   __shared__ float red[4][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t n = (int64_t)blockIdx.x * 64 + lane;
@@ -49,7 +52,9 @@ __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ X
   }
   red[w][lane] = (s0 + s1) + (s2 + s3);
   __syncthreads();
-  if (w == 0 && n < N) atomicAdd(out + n, scale * (red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane]));
+  if (w == 0 && n < N)
+    atomicAdd((out2 && n >= n1) ? out2 + (n - n1) : out + n,
+              scale * (red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane]));
 }
 
 __global__ void zero_kernel(float* out, int64_t n) {
@@ -59,6 +64,11 @@ __global__ void zero_kernel(float* out, int64_t n) {
 }  // namespace
 
 int launch_colsum(const float* X, float* out, int64_t M, int64_t N, int64_t ld, float scale, hipStream_t st) {
+  return launch_colsum2(X, out, N, nullptr, M, N, ld, scale, st);
+}
+
+int launch_colsum2(const float* X, float* out, int64_t n1, float* out2, int64_t M, int64_t N, int64_t ld, float scale,
+                   hipStream_t st) {
   if (M == 0 || N == 0) return KDFM_OK;
   const int64_t gx = ceil_div(N, 64);
   int64_t gy = ceil_div(M, 128);
@@ -66,8 +76,8 @@ int launch_colsum(const float* X, float* out, int64_t M, int64_t N, int64_t ld, 
   if (gy < 1 || deterministic()) gy = 1;  // one block per column group: a fixed summation order
   const int64_t rows_per = ceil_div(M, gy);
   gy = ceil_div(M, rows_per);
-  hipLaunchKernelGGL(colsum_kernel, dim3((unsigned)gx, (unsigned)gy), dim3(256), 0, st, X, out, M, N, ld, rows_per,
-                     scale);
+  hipLaunchKernelGGL(colsum_kernel, dim3((unsigned)gx, (unsigned)gy), dim3(256), 0, st, X, out, out2, n1, M, N, ld,
+                     rows_per, scale);
   return check_launch("colsum");
 }
 

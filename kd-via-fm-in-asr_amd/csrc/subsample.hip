@@ -270,6 +270,7 @@ struct SdGeo {
   // (B, Tm, Fm) mel frames (rows t >= mel_len[b] read as 0); per-workgroup partials
   // wpart[wg][C * 9 + C] = (sum dy1 x_patch | sum dy1), folded in workgroup order on the host side
   const float* mel; const int64_t* mel_len; int Tm, Fm, pad; float* wpart;
+  const uint16_t* wt;   // tap slabs [tap][ci (Np)][co (Cp)] bf16 (ss_dgrad_wprep)
 };
 
 __global__ __launch_bounds__(256) void ss_dgrad_wprep_kernel(const float* __restrict__ W, uint16_t* __restrict__ wt,
@@ -283,182 +284,223 @@ __global__ __launch_bounds__(256) void ss_dgrad_wprep_kernel(const float* __rest
   wt[idx] = f2bf(v);
 }
 
+// Per parity class (PT, PF) the taps are compile-time constants.  A wave owns 32 positions per tile:
+// lane r (both halves) decodes position r ONCE per tile into per-wave LDS (its y1 row index and, with
+// the fused conv0 weight gradient, its 9 mel patch values + the ones column), so the epilogue reads
+// them as LDS broadcasts instead of re-deriving them per accumulator row.  dy2 / y1 / dy1 go through
+// buffer descriptors (32-bit offsets; an out-of-range offset reads 0 / drops the store, which is how
+// masked positions, padded channels and positions past the end are handled without branches), and
+// tap 0's dy2 fragments are in flight while the ReLU' masks load.  (A next-tap prefetch spilled at 256
+// VGPRs; with 227 and 8 waves per CU, the other wave of a SIMD covers the tap loads.)  (The previous form kept
+// the taps in a runtime-indexed private array and re-decoded every accumulator row's position and
+// mel patch per lane: ~3.4k VALU instructions per 32-position tile, ~600 us at the bench shape.)
+constexpr int SD_PTS = 12;          // patch row stride (floats): 9 taps, the ones column, 2 pad
+constexpr uint32_t SD_OOB = 0x7fffffffu;
+
 template <int NCT, int KS>
-__global__ __launch_bounds__(SS_NT, 2) void ss_dgrad_kernel(const float* __restrict__ dy2,
-                                                            const uint16_t* __restrict__ wt,
-                                                            const uint16_t* __restrict__ y1, float* __restrict__ dy1,
-                                                            SdGeo g) {
+struct SdFrag {
+  float4 v[KS][2];
+};
+
+template <int NCT, int KS, int PT, int PF>
+__device__ __forceinline__ void sd_class(const SdGeo& g, __amdgpu_buffer_rsrc_t rdy2, __amdgpu_buffer_rsrc_t ry1,
+                                         __amdgpu_buffer_rsrc_t rdy1, bool has_dy1, uint16_t* lds, int cls,
+                                         float (&wacc)[NCT][10]) {
   constexpr int NP = 32 * NCT;
   constexpr int CP = 16 * KS;
-  extern __shared__ __attribute__((aligned(16))) uint16_t sd_lds[];
+  constexpr int DT = PT ? 2 : 1, DF = PF ? 2 : 1, NTAP = DT * DF;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 31, h = lane >> 5;
-  int cls = 0;
-  while (cls < 3 && (int64_t)blockIdx.x >= g.wg0[cls + 1]) ++cls;
-  const int pt = cls >> 1, pf = cls & 1;
-  const int nT = (g.T1 - pt + 1) / 2, nF = (g.F1 - pf + 1) / 2;
-  // the class's taps: (ky, kx) and the source offsets t2 - i, f2 - j
-  int ntap = 0;
-  int tap_id[4], tdt[4], tdf[4];
+  const int nT = (g.T1 - PT + 1) / 2, nF = (g.F1 - PF + 1) / 2;
+  // stage the class's tap slabs [t][ci][co] (row stride ldb)
+  constexpr int cpr = CP / 8;
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const int ky = pt ? 2 * a : 1, kx = pf ? 2 * c : 1;
-      const bool use = (a == 0 || pt) && (c == 0 || pf);
-      if (use) {
-        tap_id[ntap] = 3 * ky + kx;
-        tdt[ntap] = ky == 0 ? 1 : 0;
-        tdf[ntap] = kx == 0 ? 1 : 0;
-        ++ntap;
-      }
-    }
-  // stage the tap slabs: LDS [t][ci][co] with row stride ldb
-  const int cpr = CP / 8;   // 16-byte chunks per slab row
-  for (int t = 0; t < ntap; ++t) {
-    const uint16_t* src = wt + (int64_t)tap_id[t] * NP * CP;
+  for (int t = 0; t < NTAP; ++t) {
+    const int ky = PT ? 2 * (t / DF) : 1, kx = PF ? 2 * (t % DF) : 1;
+    const uint16_t* src = g.wt + (int64_t)(3 * ky + kx) * NP * CP;
     for (int e = threadIdx.x; e < NP * cpr; e += SS_NT) {
       const int row = e / cpr, c8 = (e - row * cpr) * 8;
-      *reinterpret_cast<bf16x8_t*>(sd_lds + (t * NP + row) * g.ldb + c8) =
+      *reinterpret_cast<bf16x8_t*>(lds + (t * NP + row) * g.ldb + c8) =
           *reinterpret_cast<const bf16x8_t*>(src + (int64_t)row * CP + c8);
     }
   }
   __syncthreads();
-  const int per_b = nT * nF;                      // positions < 2^31 (checked on the host)
+  // per-wave LDS: patches [32][SD_PTS] f32, then y1 row indices [32] int
+  float* pt = reinterpret_cast<float*>(lds + NTAP * NP * g.ldb) + wave * (32 * SD_PTS + 32);
+  int* mp = reinterpret_cast<int*>(pt + 32 * SD_PTS);
+  const int per_b = nT * nF;
   const int npos = (int)g.npos[cls];
   const int ntile = (npos + 32 * SS_WAVES - 1) / (32 * SS_WAVES);
-  // position q of the class -> (b, i, j); 32-bit decode of a base plus small normalising steps
-  // (64-bit div / mod per epilogue element cost more than the MFMAs of the tile)
-  auto decode = [&](int q, int& b, int& i, int& j) {
-    b = q / per_b;
-    const int rem = q - b * per_b;
-    i = rem / nF;
-    j = rem - i * nF;
-  };
-  auto advance = [&](int& b, int& i, int& j, int by) {
-    j += by;
-    while (j >= nF) {
-      j -= nF;
-      if (++i == nT) {
-        i = 0;
-        ++b;
-      }
-    }
-  };
-  float wacc[NCT][10];
-#pragma unroll
-  for (int n = 0; n < NCT; ++n)
-#pragma unroll
-    for (int k = 0; k < 10; ++k) wacc[n][k] = 0.f;
-  // each workgroup walks SD_TPW position tiles of its class with the staged tap slabs
   const int tile0 = (int)(blockIdx.x - g.wg0[cls]) * SD_TPW;
-  for (int tile = tile0, tend = min(tile0 + SD_TPW, ntile); tile < tend; ++tile) {
+  const int tend = min(tile0 + SD_TPW, ntile);
+  // lane's channel offsets (bytes) into dy2 rows per k-step s; padded channels (>= C) read out of range
+  uint32_t coff[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const int co = 16 * s + 8 * h;
+    coff[s] = co < g.C ? (uint32_t)co * 4u : SD_OOB;
+  }
+  auto load_tap = [&](SdFrag<NCT, KS>& f, int t, bool ok, int b, int i, int j) {
+    const int t2 = i + ((PT && (t / DF) == 0) ? 1 : 0), f2 = j + ((PF && (t % DF) == 0) ? 1 : 0);
+    const bool in = ok && t2 < g.T2 && f2 < g.F2;
+    const uint32_t base = in ? (uint32_t)(((b * g.T2 + t2) * g.F2 + f2) * g.C) * 4u : SD_OOB;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const uint32_t o = (base == SD_OOB || coff[s] == SD_OOB) ? SD_OOB : base + coff[s];
+      f.v[s][0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rdy2, o, 0, 0));
+      f.v[s][1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rdy2, o == SD_OOB ? SD_OOB : o + 16, 0, 0));
+    }
+  };
+  SdFrag<NCT, KS> fa;   // a tap's dy2 fragments (f32); tap 0's are loaded before the ReLU' masks
+  for (int tile = tile0; tile < tend; ++tile) {
     const int pos0 = tile * (32 * SS_WAVES) + wave * 32;
-    // epilogue rows first (positions 8 (e/4) + 4 h + e % 4 of the wave tile): their ReLU' operands are
-    // loaded before the MFMAs so the latency hides behind them
-    int m1[16];           // y1 position (< 2^31, checked on the host) or -1
-    {
-      int b, i, j;
-      decode(pos0 + 4 * h, b, i, j);
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int pm = pos0 + 8 * (e >> 2) + 4 * h + (e & 3);
-        m1[e] = pm < npos ? (b * g.T1 + 2 * i + pt) * g.F1 + 2 * j + pf : -1;
-        advance(b, i, j, (e & 3) == 3 ? 5 : 1);   // next row of the C layout: +1, or +5 to the next group of 8
-      }
-    }
-    bool pos_y[NCT][16];
-#pragma unroll
-    for (int n = 0; n < NCT; ++n) {
-      const int ci = 32 * n + r;
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {   // ReLU' from the sign of the bf16 y1 (bf16 RNE keeps the sign and zero)
-        const uint16_t yb = (m1[e] >= 0 && ci < g.C) ? y1[(int64_t)m1[e] * g.C + ci] : (uint16_t)0;
-        pos_y[n][e] = (yb & 0x7fff) != 0 && !(yb & 0x8000);
-      }
-    }
-    // this lane's A position
+    // this lane's position (lanes r and r + 32 hold the same one)
     const int pa = pos0 + r;
-    const bool pok = pa < npos;
-    int ba = 0, ia = 0, ja = 0;
-    if (pok) decode(pa, ba, ia, ja);
-    f32x16_t acc[NCT];
-#pragma unroll
-    for (int n = 0; n < NCT; ++n)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[n][e] = 0.f;
-    for (int t = 0; t < ntap; ++t) {
-      const int t2 = ia + tdt[t], f2 = ja + tdf[t];
-      const bool ok = pok && t2 < g.T2 && f2 < g.F2;
-      const float* src = dy2 + (((int64_t)ba * g.T2 + t2) * g.F2 + f2) * g.C;
-      bf16x8_t a[KS];
-#pragma unroll
-      for (int s = 0; s < KS; ++s) {
-        const int co = 16 * s + 8 * h;
-        if (ok && co < g.C) {
-          const float4 u = *reinterpret_cast<const float4*>(src + co);
-          const float4 v = *reinterpret_cast<const float4*>(src + co + 4);
-          const float q[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
-          a[s] = pack_bf16x8<bf16x8_t>(q);
-        } else {
-          a[s] = bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
-        }
-      }
-      const uint16_t* bp = sd_lds + (t * NP + r) * g.ldb + 8 * h;
-#pragma unroll
-      for (int s = 0; s < KS; ++s)
-#pragma unroll
-        for (int n = 0; n < NCT; ++n) {
-          const bf16x8_t b = *reinterpret_cast<const bf16x8_t*>(bp + n * 32 * g.ldb + 16 * s);
-          acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[s], b, acc[n], 0, 0, 0);
-        }
+    const bool ok = pa < npos;
+    int b = 0, i = 0, j = 0;
+    if (ok) {
+      b = pa / per_b;
+      const int rem = pa - b * per_b;
+      i = rem / nF;
+      j = rem - i * nF;
     }
-    if (dy1) {
-#pragma unroll
-      for (int n = 0; n < NCT; ++n) {
-        const int ci = 32 * n + r;
-        if (ci >= g.C) continue;
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          if (m1[e] < 0) continue;
-          dy1[(int64_t)m1[e] * g.C + ci] = pos_y[n][e] ? acc[n][e] : 0.f;
-        }
-      }
-    }
-    if (g.wpart) {
-      // conv0 weight gradient of this tile: wacc[n][tap] += dy1 x_patch[tap], wacc[n][9] += dy1 (the
-      // patch values are the same for the 32 lanes of a half-wave: broadcast loads)
-      const float invF1 = 1.f / (float)g.F1, invT1 = 1.f / (float)g.T1;
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        // (b, t1, f1) of the y1 position (exact float-reciprocal division: positions < 2^24, host-checked)
-        const int mp = m1[e] < 0 ? 0 : m1[e];
-        int q = (int)((float)mp * invF1);
-        q -= q * g.F1 > mp;
-        q += (q + 1) * g.F1 <= mp;
-        const int f1 = mp - q * g.F1;
-        int b = (int)((float)q * invT1);
-        b -= b * g.T1 > q;
-        b += (b + 1) * g.T1 <= q;
-        const int t1 = q - b * g.T1;
+    load_tap(fa, 0, ok, b, i, j);
+    const int t1 = 2 * i + PT, f1 = 2 * j + PF;
+    if (h == 0) {
+      mp[r] = ok ? (b * g.T1 + t1) * g.F1 + f1 : -1;
+      if (g.wpart) {
         const int t0 = 2 * t1 - g.pad, f0 = 2 * f1 - g.pad;
-        const int tl = m1[e] < 0 ? 0 : (g.mel_len ? (int)min((int64_t)g.Tm, g.mel_len[b]) : g.Tm);
+        const int tl = !ok ? 0 : (g.mel_len ? (int)min((int64_t)g.Tm, g.mel_len[b]) : g.Tm);
         const float* mrow = g.mel + ((int64_t)b * g.Tm + t0) * g.Fm + f0;
-        float xp[9];
+        float xp[SD_PTS];
 #pragma unroll
         for (int tp = 0; tp < 9; ++tp) {
           const int tt = t0 + tp / 3, ff = f0 + tp % 3;
           xp[tp] = (tt >= 0 && tt < tl && ff >= 0 && ff < g.Fm) ? mrow[(tp / 3) * g.Fm + tp % 3] : 0.f;
         }
+        xp[9] = ok ? 1.f : 0.f;
+        xp[10] = xp[11] = 0.f;
 #pragma unroll
-        for (int n = 0; n < NCT; ++n) {
-          const float v = pos_y[n][e] ? acc[n][e] : 0.f;
+        for (int q = 0; q < SD_PTS / 4; ++q)
+          *reinterpret_cast<float4*>(pt + r * SD_PTS + 4 * q) = make_float4(xp[4 * q], xp[4 * q + 1], xp[4 * q + 2], xp[4 * q + 3]);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's LDS writes land before its reads
+    __builtin_amdgcn_wave_barrier();
+    // y1 row indices of the accumulator rows (positions 8 (e / 4) + 4 h + e % 4) and their ReLU' masks
+    auto rows4 = [&](int q) { return *reinterpret_cast<const int4*>(mp + 8 * q + 4 * h); };
+    uint32_t mask[NCT];
 #pragma unroll
-          for (int tp = 0; tp < 9; ++tp) wacc[n][tp] += v * xp[tp];
-          wacc[n][9] += v;
+    for (int n = 0; n < NCT; ++n) mask[n] = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int4 v = rows4(q);
+      const int mq[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int n = 0; n < NCT; ++n) {
+        const int ci = 32 * n + r;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const uint32_t o = (mq[u] >= 0 && ci < g.C) ? (uint32_t)(mq[u] * g.C + ci) * 2u : SD_OOB;
+          const uint16_t yb = __builtin_amdgcn_raw_buffer_load_b16(ry1, o, 0, 0);
+          mask[n] |= ((yb & 0x7fff) != 0 && !(yb & 0x8000)) ? (1u << (4 * q + u)) : 0u;   // ReLU' from the bf16 sign
         }
       }
     }
+    f32x16_t acc[NCT];
+#pragma unroll
+    for (int n = 0; n < NCT; ++n)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[n][e] = 0.f;
+#pragma unroll
+    for (int t = 0; t < NTAP; ++t) {
+      if (t > 0) load_tap(fa, t, ok, b, i, j);
+      bf16x8_t a[KS];
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const float q[8] = {fa.v[s][0].x, fa.v[s][0].y, fa.v[s][0].z, fa.v[s][0].w,
+                            fa.v[s][1].x, fa.v[s][1].y, fa.v[s][1].z, fa.v[s][1].w};
+        a[s] = pack_bf16x8<bf16x8_t>(q);
+      }
+      const uint16_t* bp = lds + (t * NP + r) * g.ldb + 8 * h;
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+#pragma unroll
+        for (int n = 0; n < NCT; ++n) {
+          const bf16x8_t bv = *reinterpret_cast<const bf16x8_t*>(bp + n * 32 * g.ldb + 16 * s);
+          acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[s], bv, acc[n], 0, 0, 0);
+        }
+    }
+    // epilogue: dy1 = ReLU'(y1) * acc; stores dropped for masked rows / padded channels
+#pragma unroll
+    for (int n = 0; n < NCT; ++n)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[n][e] = ((mask[n] >> e) & 1u) ? acc[n][e] : 0.f;
+    if (has_dy1) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int4 v = rows4(q);
+        const int mq[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int n = 0; n < NCT; ++n) {
+          const int ci = 32 * n + r;
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const uint32_t o = (mq[u] >= 0 && ci < g.C) ? (uint32_t)(mq[u] * g.C + ci) * 4u : SD_OOB;
+            // through a scalar temporary: hipcc (ROCm 7.2) lowers __builtin_bit_cast of an ext-vector
+            // ELEMENT lvalue to element 0 whatever the index (tools/ss_dgrad_debug.py found it)
+            const float val = acc[n][4 * q + u];
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, val), rdy1, o, 0, 0);
+          }
+        }
+      }
+    }
+    if (g.wpart) {
+      // conv0 weight gradient: wacc[n][tap] += dy1 x_patch[tap] over the tile's rows (patch rows are
+      // LDS broadcasts within each half-wave)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const float* pr = pt + (8 * (e >> 2) + 4 * h + (e & 3)) * SD_PTS;
+        const float4 x0 = *reinterpret_cast<const float4*>(pr);
+        const float4 x1 = *reinterpret_cast<const float4*>(pr + 4);
+        const float2 x2 = *reinterpret_cast<const float2*>(pr + 8);
+        const float xv[10] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w, x2.x, x2.y};
+#pragma unroll
+        for (int n = 0; n < NCT; ++n)
+#pragma unroll
+          for (int k = 0; k < 10; ++k) wacc[n][k] = fmaf(acc[n][e], xv[k], wacc[n][k]);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // patch / index reads done before the next tile's writes
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+template <int NCT, int KS>
+__global__ __launch_bounds__(SS_NT, 1) void ss_dgrad_kernel(const float* __restrict__ dy2,
+                                                            const uint16_t* __restrict__ y1, float* __restrict__ dy1,
+                                                            SdGeo g) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t sd_lds[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  int cls = 0;
+  while (cls < 3 && (int64_t)blockIdx.x >= g.wg0[cls + 1]) ++cls;
+  const __amdgpu_buffer_rsrc_t rdy2 =
+      __builtin_amdgcn_make_buffer_rsrc((void*)dy2, (short)0, (int)((int64_t)g.B * g.T2 * g.F2 * g.C * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t ry1 =
+      __builtin_amdgcn_make_buffer_rsrc((void*)y1, (short)0, (int)((int64_t)g.B * g.T1 * g.F1 * g.C * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rdy1 = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)dy1, (short)0, dy1 ? (int)((int64_t)g.B * g.T1 * g.F1 * g.C * 4) : 0, 0x00020000);
+  float wacc[NCT][10];
+#pragma unroll
+  for (int n = 0; n < NCT; ++n)
+#pragma unroll
+    for (int k = 0; k < 10; ++k) wacc[n][k] = 0.f;
+  switch (cls) {
+    case 0: sd_class<NCT, KS, 0, 0>(g, rdy2, ry1, rdy1, dy1 != nullptr, sd_lds, 0, wacc); break;
+    case 1: sd_class<NCT, KS, 0, 1>(g, rdy2, ry1, rdy1, dy1 != nullptr, sd_lds, 1, wacc); break;
+    case 2: sd_class<NCT, KS, 1, 0>(g, rdy2, ry1, rdy1, dy1 != nullptr, sd_lds, 2, wacc); break;
+    default: sd_class<NCT, KS, 1, 1>(g, rdy2, ry1, rdy1, dy1 != nullptr, sd_lds, 3, wacc); break;
   }
   if (!g.wpart) return;
   // per-workgroup partial: lanes r / r + 32 hold the same channels, then the 8 waves in order
@@ -466,7 +508,7 @@ __global__ __launch_bounds__(SS_NT, 2) void ss_dgrad_kernel(const float* __restr
   for (int n = 0; n < NCT; ++n)
 #pragma unroll
     for (int k = 0; k < 10; ++k) wacc[n][k] += __shfl_xor(wacc[n][k], 32, 64);
-  __syncthreads();   // the tap slabs are no longer read: reuse the LDS
+  __syncthreads();   // the tap slabs and per-wave buffers are no longer read: reuse the LDS
   float* red = reinterpret_cast<float*>(sd_lds);
   if (h == 0) {
 #pragma unroll
@@ -488,8 +530,10 @@ __global__ __launch_bounds__(SS_NT, 2) void ss_dgrad_kernel(const float* __restr
 }
 
 template <int NCT, int KS>
-int sd_launch(const float* dy2, const uint16_t* wt, const uint16_t* y1, float* dy1, const SdGeo& g, hipStream_t st) {
-  size_t lds = (size_t)4 * 32 * NCT * g.ldb * sizeof(uint16_t);
+int sd_launch(const float* dy2, const uint16_t* wt, const uint16_t* y1, float* dy1, SdGeo g, hipStream_t st) {
+  g.wt = wt;
+  // 4 tap slabs (the largest class) + per-wave patch / index buffers; the fold reuses the space
+  size_t lds = (size_t)4 * 32 * NCT * g.ldb * sizeof(uint16_t) + (size_t)SS_WAVES * (32 * SD_PTS + 32) * 4;
   const size_t red = (size_t)SS_WAVES * NCT * 10 * 32 * sizeof(float);   // fused conv0 wgrad reduction
   if (g.wpart && red > lds) lds = red;
   static bool once = [] {
@@ -498,7 +542,7 @@ int sd_launch(const float* dy2, const uint16_t* wt, const uint16_t* y1, float* d
     return true;
   }();
   (void)once;
-  hipLaunchKernelGGL((ss_dgrad_kernel<NCT, KS>), dim3((unsigned)g.wg0[4]), dim3(SS_NT), lds, st, dy2, wt, y1, dy1, g);
+  hipLaunchKernelGGL((ss_dgrad_kernel<NCT, KS>), dim3((unsigned)g.wg0[4]), dim3(SS_NT), lds, st, dy2, y1, dy1, g);
   return check_launch("kdfm_subsample_conv2_dgrad");
 }
 
@@ -586,7 +630,7 @@ int sd_geo(SdGeo& g, int64_t B, int64_t T1, int64_t F1, int64_t C) {
     g.npos[c] = B * ((T1 - pt + 1) / 2) * ((F1 - pf + 1) / 2);
     g.wg0[c + 1] = g.wg0[c] + ceil_div(ceil_div(g.npos[c], 32 * SS_WAVES), SD_TPW);
   }
-  g.mel = nullptr; g.mel_len = nullptr; g.Tm = g.Fm = g.pad = 0; g.wpart = nullptr;
+  g.mel = nullptr; g.mel_len = nullptr; g.Tm = g.Fm = g.pad = 0; g.wpart = nullptr; g.wt = nullptr;
   return 0;
 }
 int sd_dispatch(const float* dy2, const uint16_t* wt, const uint16_t* y1, float* dy1, const SdGeo& g, hipStream_t st) {
@@ -618,17 +662,15 @@ int kdfm_subsample_conv2_dgrad_w0(const float* dy2, const uint16_t* wt, const ui
   KDFM_REQUIRE(T1 == (Tm + 2 * pad - 3) / 2 + 1 && F1 == (Fm + 2 * pad - 3) / 2 + 1, "conv0 geometry");
   SdGeo g;
   sd_geo(g, B, T1, F1, C);
-  KDFM_REQUIRE(g.wg0[4] < (1ll << 31) && B * T1 * F1 < (1ll << 24) && B * Tm * Fm < (1ll << 31),
-               "too large for the fused conv0 weight gradient (y1 positions < 2^24)");
+  KDFM_REQUIRE(g.wg0[4] < (1ll << 31) && B * T1 * F1 * C * 4 < (1ll << 31) && B * Tm * Fm < (1ll << 31),
+               "too large (32-bit buffer offsets: dy1 / y1 / dy2 < 2 GiB)");
   KDFM_REQUIRE(ws_len >= g.wg0[4] * C * 10, "workspace too small (kdfm_subsample_conv2_dgrad_w0_ws)");
   g.mel = mel; g.mel_len = mel_len; g.Tm = (int)Tm; g.Fm = (int)Fm; g.pad = (int)pad; g.wpart = ws;
   hipStream_t st = as_stream(stream);
   int rc = sd_dispatch(dy2, wt, y1, dy1, g, st);
   if (rc) return rc;
   // fixed-order fold of the per-workgroup partials: dW0 (C, 9) += sum_wg, db0 (C) += sum_wg
-  rc = launch_colsum(ws, dw0, g.wg0[4], C * 9, C * 10, 1.f, st);
-  if (rc) return rc;
-  return launch_colsum(ws + C * 9, db0, g.wg0[4], C, C * 10, 1.f, st);
+  return launch_colsum2(ws, dw0, C * 9, db0, g.wg0[4], C * 10, C * 10, 1.f, st);
 }
 
 int kdfm_subsample_conv2_dgrad(const float* dy2, const uint16_t* wt, const uint16_t* y1, float* dy1, int64_t B, int64_t T1,
@@ -639,7 +681,8 @@ int kdfm_subsample_conv2_dgrad(const float* dy2, const uint16_t* wt, const uint1
   KDFM_REQUIRE(((((uintptr_t)dy2) | ((uintptr_t)wt)) & 15) == 0, "dy2 / wt must be 16-byte aligned");
   SdGeo g;
   sd_geo(g, B, T1, F1, C);
-  KDFM_REQUIRE(g.wg0[4] < (1ll << 31) && B * T1 * F1 < (1ll << 31), "too large");
+  KDFM_REQUIRE(g.wg0[4] < (1ll << 31) && B * T1 * F1 * C * 4 < (1ll << 31),
+               "too large (32-bit buffer offsets: dy1 / y1 / dy2 < 2 GiB)");
   return sd_dispatch(dy2, wt, y1, dy1, g, as_stream(stream));
 }
 

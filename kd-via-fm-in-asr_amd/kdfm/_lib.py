@@ -160,6 +160,7 @@ SIGNATURES: dict[str, tuple] = {
     "kdfm_dwconv_bwd_ws": (_i64, [_i64, _i64, _i64, _i64]),
     "kdfm_bn_finalize": (_i32, [P, P, P, P, P, _i64, _i64, _f32, P]),
     "kdfm_bn_running_update": (_i32, [P, P, P, _i64, _i64, _f32, P]),
+    "kdfm_bn_finalize_running": (_i32, [P, P, P, P, P, _i64, _i64, _f32, _f32, P]),
     "kdfm_bn_silu_fwd": (_i32, [P, P, P, P, P, P, _i64, _i64, P]),
     "kdfm_bn_silu_bwd": (_i32, [P, P, P, P, P, P, P, P, P, P, _i64, _i64, _i32, P]),
     "kdfm_log_softmax": (_i32, [P, P, _i64, _i64, _i64, _i64, P]),

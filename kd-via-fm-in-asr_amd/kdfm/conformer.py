@@ -472,9 +472,13 @@ def layer_forward(cfg, S: EncoderShapes, P, L, li, x, out, pos_emb, lengths, *, 
     bmean = _empty(d, dev=dev)
     brstd = _empty(d, dev=dev)
     rmn, rvr = bn_update if bn_update is not None else (None, None)
-    K.bn_finalize(stats, rmn, rvr, bmean, brstd, d, rows, cfg.bn_eps)
-    if rm_batch and bn_update is not None and train:
-        K.bn_running_update(rmn, rvr, stats, d, rows, cfg.bn_momentum)
+    if stats is not None and rm_batch and bn_update is not None and train:
+        # batch statistics and the running-statistics update in one launch
+        K.bn_finalize_running(stats, rmn, rvr, bmean, brstd, d, rows, cfg.bn_eps, cfg.bn_momentum)
+    else:
+        K.bn_finalize(stats, rmn, rvr, bmean, brstd, d, rows, cfg.bn_eps)
+        if rm_batch and bn_update is not None and train:
+            K.bn_running_update(rmn, rvr, stats, d, rows, cfg.bn_momentum)
     x3 = _empty(rows, d, dev=dev)
     z = z_h = None
     if _rowgemm_fused(rows, d, save):
@@ -798,10 +802,12 @@ def encoder_forward(cfg, S: EncoderShapes, P, prefix, mel, mel_len, len1, len2, 
 
 
 def encoder_backward(cfg, S: EncoderShapes, P, G, prefix, run: EncoderRun, dfeats, pos_emb, len1, len2, *, seed,
-                     salt, ws, on_layer_done=None):
+                     salt, ws, on_layer_done=None, before_read=None):
     """dfeats (n_layers, rows, d): grads wrt every hooked layer output (heads + decoder), summed into
     the residual chain as the backward walks down the stack.  on_layer_done(i) is called once layer
-    i's parameter gradients are all issued (bucketed all-reduce overlap, kdfm/ddp.py)."""
+    i's parameter gradients are all issued (bucketed all-reduce overlap, kdfm/ddp.py);
+    before_read {j: fn}: fn() runs right before dfeats[j] is first read (a stream join for heads
+    gradients produced on another stream)."""
     dout = dfeats[cfg.n_layers - 1]
     if "ln_parts" not in ws:
         ws["ln_parts"] = torch.empty(6, K.layernorm_bwd_ws(S.rows, S.d), device=dfeats.device)
@@ -813,6 +819,8 @@ def encoder_backward(cfg, S: EncoderShapes, P, G, prefix, run: EncoderRun, dfeat
         if on_layer_done is not None:
             on_layer_done(i)
         if i > 0:
+            if before_read is not None and (i - 1) in before_read:
+                before_read[i - 1]()
             K.axpby(dfeats[i - 1], dx, dfeats[i - 1], 1.0, 1.0)
             dout = dfeats[i - 1]
     subsampling_backward(cfg, S, P, G, prefix, run.sub, dx, len1, seed=seed, salt=salt, ws=ws)

@@ -19,7 +19,7 @@ from .conformer import EncoderRun, EncoderShapes, compute_lengths, encoder_backw
     encoder_forward_steps, layer_images, make_workspace
 from .frontend import FrontendConsts, frontend_forward, mel_frames, specaugment_
 from .encfm import EncFMWorkspace, encfm_backward, encfm_forward
-from .heads import HeadsWorkspace, heads_backward, heads_forward, tae_forward
+from .heads import SALT_HEADS, HeadsWorkspace, heads_backward, heads_forward, tae_forward
 from .overlap import WGRAD
 
 # Stream priorities (KDFM_STREAM_PRIO=1): the critical-path streams (the compute stream that carries
@@ -93,16 +93,20 @@ class Ver5Engine:
         # [sum g^2 of the (all-reduced, mean) gradient, #non-finite entries] when cfg.grad_check
         self.grad_stats = torch.zeros(2, device=dev) if cfg.grad_check else None
         self.hws = HeadsWorkspace(cfg, dev)
+        # the ver5 heads run in two layer halves: layers [0, L/2) as soon as both encoders have issued layer
+        # L/2 - 1 (beside the encoders' second half), backward beside the encoder backward's first half;
+        # the halves have their own workspaces (per-step weight layouts, bias-gradient accumulators)
+        self.heads_split = __import__("os").environ.get("KDFM_HEADS_SPLIT", "1") == "1"
+        self.hws_b = HeadsWorkspace(cfg, dev)
         if K.twins_enabled():   # opt-in direct-B skinny path (KDFM_SKINNY_DIRECT_MIN_M)
             self.student.enable_bf16_twins()
             self.teacher.enable_bf16_twins()
         self._pos = {}
         self._imgs = None   # kernels.WeightImages of the student and the teacher encoders (bf16 math)
         self._ws = {}
-        self._tgraphs = {}
         # the step runs on a created (non-null) stream: ROCm makes the legacy null stream wait for a
-        # HIP graph replayed on any other stream (tools/graph_probe.py), which serialised the teacher
-        # graph and the whole-step graph's branches behind the main stream
+        # HIP graph replayed on any other stream (tools/graph_probe.py), which serialised the whole-step
+        # graph's branches behind the main stream
         self.compute_stream = _crit_stream(dev) if dev.type == "cuda" else None
         self._link_in, self._link_out = K.StreamLink(), K.StreamLink()   # caller <-> compute stream
         # weight gradients on the side stream (the benchmark's schedule) or in line: None follows the
@@ -114,8 +118,6 @@ class Ver5Engine:
         self.encfm_gumbel = None
         self._encfm = {}
         self.encfm_stats = None
-        # capture the frozen teacher as a HIP graph in training steps (KDFM_TEACHER_GRAPH=0: eager)
-        self.teacher_graph = __import__("os").environ.get("KDFM_TEACHER_GRAPH", "0") == "1"
         if init:
             st = init_uniform(student_specs(cfg), student_seed)
             hd = init_uniform([s for s in student_specs(cfg) if not s[0].startswith(("encoder.", "decoder."))],
@@ -172,49 +174,6 @@ class Ver5Engine:
                         bn_running=self.bn.P, use_batch_stats=False, ws=self._enc_ws(St, "teacher.encoder."))
         K.linear(tfeats[-1], self.teacher.P["teacher.decoder.decoder_layers.0.weight"].view(Cn, St.d),
                  self.teacher.P["teacher.decoder.decoder_layers.0.bias"], tlogits)
-
-    def _teacher_graph(self, wav, wav_len, mel_len, len1, len2, St, T):
-        """Static-input HIP graph of the teacher's frontend + encoder + decoder for this batch shape
-        (captured on first use; the teacher is frozen, so nothing but its inputs changes between
-        steps).  The step's inputs and frame lengths are copied into the graph's input buffers on
-        the issuing stream; its outputs (tfeats, tlogits) are rewritten by every replay."""
-        B, N = wav.shape
-        key = (B, N, K.get_math(), K.get_deterministic(), tuple(len1.shape))
-        tg = self._tgraphs.get(key)
-        if tg is None:
-            import types
-            dev = self.device
-            cfg = self.cfg
-            tg = types.SimpleNamespace()
-            tg.wav = torch.empty_like(wav)
-            tg.wav_len = torch.empty_like(wav_len)
-            tg.mel_len = torch.empty_like(mel_len)
-            tg.len1 = torch.empty_like(len1)
-            tg.len2 = torch.empty_like(len2)
-            tg.tfeats = torch.empty(cfg.n_layers, St.rows, St.d, device=dev)
-            tg.tlogits = torch.empty(St.rows, cfg.classes, device=dev)
-            for dst, src in ((tg.wav, wav), (tg.wav_len, wav_len), (tg.mel_len, mel_len), (tg.len1, len1),
-                             (tg.len2, len2)):
-                dst.copy_(src)
-            side = self._side_stream()
-            side.wait_stream(torch.cuda.current_stream(dev))
-
-            def body():
-                mel = frontend_forward(cfg, self.fe, tg.wav, tg.wav_len, tg.mel_len, dither=0.0)
-                self._teacher_forward(mel, tg.mel_len, tg.len1, tg.len2, tg.tfeats, tg.tlogits, St, T)
-
-            with torch.cuda.stream(side):
-                body()        # eager warm-up: lazy workspaces exist before capture
-            torch.cuda.synchronize()
-            tg.graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(tg.graph, stream=side):
-                body()
-            torch.cuda.synchronize()
-            self._tgraphs[key] = tg
-        for dst, src in ((tg.wav, wav), (tg.wav_len, wav_len), (tg.mel_len, mel_len), (tg.len1, len1),
-                         (tg.len2, len2)):
-            dst.copy_(src)
-        return tg
 
     def _enc_ws(self, S, prefix):
         # one workspace per encoder: the teacher and the student run concurrently on two streams and
@@ -274,31 +233,19 @@ class Ver5Engine:
         rows = Ss.rows
         main = torch.cuda.current_stream(dev)
         side = self._side_stream()
-        tg = None
-        tgen = None
-        if own_mel and self.teacher_graph and not torch.cuda.is_current_stream_capturing():
-            # experiment (KDFM_TEACHER_GRAPH=1): the frozen teacher as one captured HIP graph.  Off by
-            # default: on ROCm work issued to other streams after the replay waited for the whole
-            # graph (tools/teacher_graph_probe.py), which cost the teacher/student overlap
-            tg = self._teacher_graph(wav, wav_len, mel_len, len1, len2, St, T)
+        tfeats = torch.empty(cfg.n_layers, St.rows, St.d, device=dev)
+        tlogits = torch.empty(rows, Cn, device=dev)
+        if own_mel:
+            # the teacher's own (undithered) frontend goes to the teacher stream with its encoder
             side.wait_stream(main)
-            with torch.cuda.stream(side), K.region("teacher_graph"):
-                tg.graph.replay()
-            mel_t, tfeats, tlogits = None, tg.tfeats, tg.tlogits
-        else:
-            tfeats = torch.empty(cfg.n_layers, St.rows, St.d, device=dev)
-            tlogits = torch.empty(rows, Cn, device=dev)
-            if own_mel:
-                # the teacher's own (undithered) frontend goes to the teacher stream with its encoder
-                side.wait_stream(main)
-                with torch.cuda.stream(side), K.region("teacher_frontend"):
-                    mel_t = frontend_forward(cfg, self.fe, wav, wav_len, mel_len, dither=0.0)
-            else:
+            with torch.cuda.stream(side), K.region("teacher_frontend"):
                 mel_t = frontend_forward(cfg, self.fe, wav, wav_len, mel_len, dither=0.0)
-                side.wait_stream(main)
-            tgen = encoder_forward_steps(cfg, St, self.teacher.P, "teacher.encoder.", mel_t, mel_len, len1, len2,
-                                         tfeats, self._pos_emb(T, St.d), train=False, seed=seed, salt=SALT_TEACHER,
-                                         save=False, bn_running=self.bn.P, use_batch_stats=False, ws=self._enc_ws(St, "teacher.encoder."))
+        else:
+            mel_t = frontend_forward(cfg, self.fe, wav, wav_len, mel_len, dither=0.0)
+            side.wait_stream(main)
+        tgen = encoder_forward_steps(cfg, St, self.teacher.P, "teacher.encoder.", mel_t, mel_len, len1, len2,
+                                     tfeats, self._pos_emb(T, St.d), train=False, seed=seed, salt=SALT_TEACHER,
+                                     save=False, bn_running=self.bn.P, use_batch_stats=False, ws=self._enc_ws(St, "teacher.encoder."))
         if own_mel:
             mel_s = frontend_forward(cfg, self.fe, wav, wav_len, mel_len, dither=dither, seed=seed,
                                      rng_stream=SALT_FRONT)
@@ -318,26 +265,38 @@ class Ver5Engine:
         sgen = encoder_forward_steps(cfg, Ss, self.student.P, "encoder.", mel_s, mel_len, len1, len2, sfeats, pos_s,
                                      train=train, seed=seed, salt=SALT_STUDENT, save=save, bn_running=self.bn.P,
                                      use_batch_stats=train, ws=self._enc_ws(Ss, "encoder."), run=srun)
-        with K.region("encoders"):
-            for _ in range(cfg.n_layers + 1):
-                if tgen is not None:
-                    with K.on_stream(side):
-                        next(tgen)
-                next(sgen)
-        if tgen is not None:
-            with torch.cuda.stream(side):
-                K.linear(tfeats[-1], self.teacher.P["teacher.decoder.decoder_layers.0.weight"].view(Cn, St.d),
-                         self.teacher.P["teacher.decoder.decoder_layers.0.bias"], tlogits)
-            for t in (tfeats, tlogits, mel_t, mel_len, len1, len2):
-                t.record_stream(side)
-        # ---- the ver5 heads' TeacherAutoEncoder reads only the teacher: on the teacher stream, right after
-        # the teacher encoder, off the student's chain (the main stream joins the teacher stream below) ----
+        n_st = cfg.n_layers * Ss.rows
         tae = None
         if not encfm:
-            n_st = cfg.n_layers * Ss.rows
             tae = (torch.empty(n_st, cfg.latent, device=dev), torch.empty(n_st, St.d, device=dev))
+        h = self._heads_half(train, save) if not encfm else 0
+        nb = h * Ss.rows
+        hctx_b = None
+        with K.region("encoders"):
+            for k in range(cfg.n_layers + 1):
+                with K.on_stream(side):
+                    next(tgen)
+                next(sgen)
+                if h and k == h:
+                    # both encoders have issued layers [0, h): the auto-encoder of those teacher layers on the
+                    # teacher stream, then the heads of those layers on the heads stream, beside layers [h, L)
+                    with torch.cuda.stream(side):
+                        tae_forward(cfg, self.student.P, tfeats[:h].view(nb, St.d), tae[0][:nb], tae[1][:nb], acc[1:2],
+                                    layers=h)
+                    hctx_b = self._heads_first_half(cfg, Ss, St, T, h, sfeats, tfeats, tae, acc, eps, seed, save, main,
+                                                    side)
+        with torch.cuda.stream(side):
+            K.linear(tfeats[-1], self.teacher.P["teacher.decoder.decoder_layers.0.weight"].view(Cn, St.d),
+                     self.teacher.P["teacher.decoder.decoder_layers.0.bias"], tlogits)
+        for t in (tfeats, tlogits, mel_t, mel_len, len1, len2):
+            t.record_stream(side)
+        # ---- the ver5 heads' TeacherAutoEncoder reads only the teacher: on the teacher stream, right after
+        # the teacher encoder (the second layer half; the first went out after teacher layer h - 1), off the
+        # student's chain (the main stream joins the teacher stream below) ----
+        if tae is not None:
             with torch.cuda.stream(side):
-                tae_forward(cfg, self.student.P, tfeats.view(n_st, St.d), tae[0], tae[1], acc[1:2])
+                tae_forward(cfg, self.student.P, tfeats[h:].view(n_st - nb, St.d), tae[0][nb:], tae[1][nb:], acc[1:2],
+                            layers=cfg.n_layers - h)
             for t in (*tae, acc, tfeats):
                 t.record_stream(side)
         # ---- decoders, CTC, logit KD ----
@@ -381,9 +340,14 @@ class Ver5Engine:
             K.axpby(ews.stats[2:3].view(1, 1), None, acc[7:8].view(1, 1), 1.0, 0.0)   # forward's total_loss
         else:
             with K.region("heads_forward"):
-                hctx = heads_forward(cfg, self.student.P, sfeats.view(n, Ss.d), tfeats.view(n, St.d), T, self.hws,
-                                     acc[1:6], seed=seed, eps=eps, save=save, Pfix=self.fixed.P,
-                                     acc_diffkd=acc[6:7], tae=tae)
+                na = n - nb
+                hctx_a = heads_forward(cfg, self.student.P, sfeats[h:].view(na, Ss.d), tfeats[h:].view(na, St.d), T,
+                                       self.hws, acc[1:6], seed=seed, eps=None if eps is None else eps[nb:],
+                                       save=save, Pfix=self.fixed.P, acc_diffkd=acc[6:7], tae=(tae[0][nb:], tae[1][nb:]),
+                                       layers=cfg.n_layers - h)
+                if h:
+                    main.wait_stream(self._heads_stream(main))   # the first half's loss terms
+                hctx = (hctx_b, hctx_a, h) if save else None
                 K.colsum(acc[2:7].view(5, 1), acc[7:8], accumulate=False)
         # device (recon, kd_pre, fm_pre, kd_post, fm_post, diffkd): the v/* log keys
         self.kd_terms = acc[1:7]
@@ -452,6 +416,34 @@ class Ver5Engine:
             self._aux = _crit_stream(self.device) if own else self._side_stream()
         return self._aux
 
+    def _serial(self):
+        """Weight gradients (and the heads' second stream) in line: deterministic mode unless overlap_wgrad
+        says otherwise."""
+        return self.cfg.deterministic if self.overlap_wgrad is None else not self.overlap_wgrad
+
+    def _heads_half(self, train, save):
+        """h > 0: the heads run as layers [0, h) and [h, L) (KDFM_HEADS_SPLIT=0: one call over all)."""
+        return self.cfg.n_layers // 2 if self.heads_split and self.cfg.n_layers >= 2 else 0
+
+    def _heads_stream(self, main):
+        """Where the first heads half runs in the forward: the weight-gradient stream (idle until the
+        backward), or in line when the schedule is serialised."""
+        return main if self._serial() else WGRAD.stream()
+
+    def _heads_first_half(self, cfg, Ss, St, T, h, sfeats, tfeats, tae, acc, eps, seed, save, main, side):
+        nb = h * Ss.rows
+        hs = self._heads_stream(main)
+        if hs is not main:
+            hs.wait_stream(main)
+            hs.wait_stream(side)
+            for t in (sfeats, tfeats, *tae, acc) + (() if eps is None else (eps,)):
+                t.record_stream(hs)
+        with K.on_stream(hs), K.region("heads_forward_first_half"):
+            return heads_forward(cfg, self.student.P, sfeats[:h].view(nb, Ss.d), tfeats[:h].view(nb, St.d), T,
+                                 self.hws_b, acc[1:6], seed=seed, eps=None if eps is None else eps[:nb], save=save,
+                                 Pfix=self.fixed.P, acc_diffkd=acc[6:7], tae=(tae[0][:nb], tae[1][:nb]), layers=h,
+                                 salt=SALT_HEADS + 100)
+
     def _join_losses(self, ctx):
         """Join the CTC/KL stream and assemble the loss vector (total, ctc, kl, recon, fm)."""
         torch.cuda.current_stream(self.device).wait_stream(self._aux_stream())
@@ -491,8 +483,25 @@ class Ver5Engine:
             if grad_ready is not None:
                 grad_ready(min(o for k, o in off.items() if not k.startswith(("encoder.", "decoder."))))
         else:
+            hctx_b, hctx_a, h = ctx.pop("hctx")
+            nb = h * Ss.rows
+            dfv = dfeats.view(n, Ss.d)
+            if h:
+                # the first layer half's heads backward: in line, or on the teacher stream (idle since CTC/KL)
+                # beside this half and the encoder backward of layers [h, L); the encoder backward joins it
+                # before it reads dfeats[h - 1].  Its weight gradients are issued first either way, so the
+                # weight-gradient stream sees the same launch order as the serialised schedule.
+                side = main = torch.cuda.current_stream(self.device)
+                if not self._serial():
+                    side = self._side_stream()
+                    side.wait_stream(main)
+                    dfeats.record_stream(side)
+                with K.on_stream(side), K.region("heads_backward_first_half"):
+                    heads_backward(cfg, P, G, hctx_b, self.hws_b, dfv[:nb], seed=self.seed)
+                if side is not main:
+                    ctx["heads_join"] = (h - 1, side)
             with K.region("heads_backward"):
-                heads_backward(cfg, P, G, ctx.pop("hctx"), self.hws, dfeats.view(n, Ss.d), seed=self.seed)
+                heads_backward(cfg, P, G, hctx_a, self.hws, dfv[nb:], seed=self.seed)
             if grad_ready is not None:
                 grad_ready(min(o for k, o in off.items() if not k.startswith(("encoder.", "decoder."))))
             # decoder: logits = W enc + b ; grad wrt logits from CTC + KL
@@ -506,10 +515,13 @@ class Ver5Engine:
             firsts = {i: min(o for k, o in off.items() if k.startswith(f"encoder.layers.{i}."))
                       for i in range(cfg.n_layers)}
             layer_done = lambda i: grad_ready(firsts[i])  # noqa: E731
+        join = ctx.pop("heads_join", None)
         with K.region("encoder_backward"):
             encoder_backward(cfg, Ss, P, G, "encoder.", ctx.pop("srun"), dfeats, ctx["pos_s"], ctx["len1"],
                              ctx["len2"], seed=self.seed, salt=SALT_STUDENT, ws=self._enc_ws(Ss, "encoder."),
-                             on_layer_done=layer_done)
+                             on_layer_done=layer_done,
+                             before_read=None if join is None else {join[0]: lambda: torch.cuda.current_stream(
+                                 self.device).wait_stream(join[1])})
 
     def optimizer_step(self, grad_scale: float = 1.0):
         with self._on_stream(), self._mode(), K.region("optimizer"):

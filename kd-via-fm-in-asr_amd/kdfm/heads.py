@@ -291,17 +291,18 @@ def _denoise_backward(P, G, dn: _Deno, c, g, T, dev):
     return gin
 
 
-def _adapt_denoise_forward(cfg, P, ws, x, T, seed, eps, dev):
-    """NoiseAdapter then the 9-step SimpleDenoiser over rows x; returns (ctx, z_deno)."""
+def _adapt_denoise_forward(cfg, P, ws, x, T, seed, eps, dev, salt=SALT_HEADS):
+    """NoiseAdapter then the 9-step SimpleDenoiser over rows x; returns (ctx, z_deno).  salt: the counter-RNG
+    stream of the adapter noise (one per layer-half call, so the halves draw independent noise)."""
     n, Lt = x.shape
     hA = _empty(n, Lt, dev=dev)
     K.linear(x, P["adapter.gamma_head.0.weight"].view(Lt, Lt), P["adapter.gamma_head.0.bias"], hA, epi=_lib.EPI_RELU)
     zn = _empty(n, Lt, dev=dev)
     gamma = _empty(n, dev=dev)
     K.adapter_fwd(x, hA, P["adapter.gamma_head.2.weight"].view(-1), P["adapter.gamma_head.2.bias"], eps, zn, gamma,
-                  seed, SALT_HEADS)
+                  seed, salt)
     dctx, out = _denoise_forward(P, _Deno(ws, "denoiser.net.", cfg.denoiser_steps), zn, T, dev)
-    dctx.update(x=x, hA=hA, gamma=gamma, eps=eps)
+    dctx.update(x=x, hA=hA, gamma=gamma, eps=eps, salt=salt)
     return dctx, out
 
 
@@ -313,7 +314,7 @@ def _adapt_denoise_backward(cfg, P, G, ws, c, g, T, seed, dev):
     dx_direct = _empty(n, Lt, dev=dev)
     dh = _empty(n, Lt, dev=dev)
     K.adapter_bwd(g, x, hA, c["gamma"], P["adapter.gamma_head.2.weight"].view(-1), c["eps"], dx_direct, dh,
-                  G["adapter.gamma_head.2.weight"].view(-1), G["adapter.gamma_head.2.bias"], seed, SALT_HEADS)
+                  G["adapter.gamma_head.2.weight"].view(-1), G["adapter.gamma_head.2.bias"], seed, c["salt"])
     del g
     WGRAD.run(lambda: K.linear_dw(dh, x, G["adapter.gamma_head.0.weight"].view(Lt, Lt),
                                   db=G["adapter.gamma_head.0.bias"]), dh, x)
@@ -348,13 +349,13 @@ def _denoise_backward_unfused(P, G, dn: _Deno, c, g, T, dev):
 # the version graph
 # ------------------------------------------------------------------------------------------------
 
-def _diffkd_forward(cfg, P, Pfix, s_feats, t_feats, T, ws, acc, dev):
+def _diffkd_forward(cfg, P, Pfix, s_feats, t_feats, T, ws, acc, dev, layers=None):
     """DiffKDModule over every layer pair at once (asr_train_diffm.py:364-394), the layer mean of
     :795-800 folded into the MSE scales: z_t = encoder(t) (no gradient reaches the encoder, :382),
     ae = MSE(decoder(z_t), t), x = denoise^S(proj(s)), distill = MSE(x, z_t); acc += (ae + distill) / L."""
     n = s_feats.shape[0]
     Lt, Ct, Cs = cfg.latent, cfg.d_teacher, cfg.d_student
-    rows = n // cfg.n_layers
+    rows = n // (layers or cfg.n_layers)
     zt = _empty(n, Lt, dev=dev)
     K.linear(t_feats, Pfix["diffkd.encoder.weight"].view(Lt, Ct), Pfix["diffkd.encoder.bias"], zt)
     drec = _empty(n, Ct, dev=dev)
@@ -386,14 +387,14 @@ def _diffkd_backward(cfg, P, G, c, s_feats, T, ws, ds_feats, dev):
     K.linear_dx(dzs, P["diffkd.proj.weight"].view(Lt, Cs), ds_feats, R=ds_feats, rscale=1.0)
 
 
-def tae_forward(cfg: Ver5Config, P, t_feats, zt, drec, acc_recon):
+def tae_forward(cfg: Ver5Config, P, t_feats, zt, drec, acc_recon, layers=None):
     """TeacherAutoEncoder over the stacked teacher layer outputs t_feats (n, d_teacher): z_t = enc(t) into
     zt (n, latent), the recon MSE (mean over B*C*T per layer, summed over layers) added into acc_recon and
     its gradient d/d t_rec into drec (n, d_teacher).  It reads nothing of the student, so the engine issues
     it on the teacher stream right after the teacher encoder (off the student's critical path)."""
     n = t_feats.shape[0]
     Lt, Ct = cfg.latent, cfg.d_teacher
-    inv_rec = 1.0 / ((n // cfg.n_layers) * Ct)
+    inv_rec = 1.0 / ((n // (layers or cfg.n_layers)) * Ct)
     K.linear(t_feats, P["tae.enc.weight"].view(Lt, Ct), P["tae.enc.bias"], zt)
     K.linear(zt, P["tae.dec.weight"].view(Ct, Lt), P["tae.dec.bias"], drec, R=t_feats, rscale=2.0 * inv_rec,
              mse=(acc_recon, inv_rec))
@@ -413,21 +414,23 @@ def tae_backward(cfg: Ver5Config, P, G, zt, drec, t_feats, dzt):
 
 
 def heads_forward(cfg: Ver5Config, P, s_feats, t_feats, T, ws: HeadsWorkspace, acc, *, seed, eps=None, save=True,
-                  Pfix=None, acc_diffkd=None, tae=None):
+                  Pfix=None, acc_diffkd=None, tae=None, layers=None, salt=SALT_HEADS):
     """s_feats (n, d_student) and t_feats (n, d_teacher) stacked student/teacher layer outputs
     (n = layers*B*T').  acc: device (5,) f32 accumulators [recon, kd_pre, fm_pre, kd_post, fm_post]
     (added to; the slots a version does not use stay untouched).  tae: (zt, drec) when the caller has
-    already run tae_forward (recon added into acc[0] there).  Returns ctx for backward."""
+    already run tae_forward (recon added into acc[0] there).  layers: how many hooked layers the rows
+    stack (default all: the per-layer means; the engine runs the heads in two layer halves), salt: the
+    adapter noise stream.  Returns ctx for backward."""
     dev = s_feats.device
     n = s_feats.shape[0]
     Lt, Ct = cfg.latent, cfg.d_teacher
     v = cfg.version
-    per_layer_rows = n // cfg.n_layers
+    per_layer_rows = n // (layers or cfg.n_layers)
     inv_lat = 1.0 / (per_layer_rows * Lt)
     # ---- TeacherAutoEncoder + recon MSE (mean over B*C*T per layer, summed over layers) ----
     if tae is None:
         zt, drec = _empty(n, Lt, dev=dev), _empty(n, Ct, dev=dev)
-        tae_forward(cfg, P, t_feats, zt, drec, acc[RECON:RECON + 1])
+        tae_forward(cfg, P, t_feats, zt, drec, acc[RECON:RECON + 1], layers)
     else:
         zt, drec = tae
     # ---- StudentProjector ----
@@ -443,14 +446,14 @@ def heads_forward(cfg: Ver5Config, P, s_feats, t_feats, T, ws: HeadsWorkspace, a
     if v == 1:
         ctx["dkd_pre"] = _kd(cfg, zs, zt, acc[KD_PRE:KD_PRE + 1], inv_lat, dev)
     if v >= 3:
-        ctx["ad"], zd = _adapt_denoise_forward(cfg, P, ws, x_adapt, T, seed, eps, dev)
+        ctx["ad"], zd = _adapt_denoise_forward(cfg, P, ws, x_adapt, T, seed, eps, dev, salt)
         if v in (3, 4, 8):
             ctx["dkd_post"] = _kd(cfg, zd, zt, acc[KD_POST:KD_POST + 1], inv_lat, dev)
         else:
             pre = "fm_latent.fm." if v == 5 else "fm_latent_2.fm."
             ctx["fm_post"], _ = _fm_forward(cfg, P, pre, ws, zd, zt, acc[FM_POST:FM_POST + 1], inv_lat, False, dev)
     if cfg.use_diffkd:
-        ctx["diffkd"] = _diffkd_forward(cfg, P, Pfix, s_feats, t_feats, T, ws, acc_diffkd, dev)
+        ctx["diffkd"] = _diffkd_forward(cfg, P, Pfix, s_feats, t_feats, T, ws, acc_diffkd, dev, layers)
     return ctx if save else None
 
 

@@ -1235,6 +1235,12 @@ def bn_running_update(rm, rv, stats, d, count, momentum):
     call("kdfm_bn_running_update", ptr(rm), ptr(rv), ptr(stats), d, int(count), float(momentum), _s())
 
 
+def bn_finalize_running(stats, rm, rv, mean, rstd, d, count, eps, momentum):
+    """Batch mean/rstd from the f64 sums AND the running-statistics update (training), one launch."""
+    call("kdfm_bn_finalize_running", ptr(stats), ptr(rm), ptr(rv), ptr(mean), ptr(rstd), d, int(count), float(eps),
+         float(momentum), _s())
+
+
 def bn_silu_fwd(y, mean, rstd, g, b, z):
     rows, d = y.shape
     call("kdfm_bn_silu_fwd", ptr(y), ptr(mean), ptr(rstd), ptr(g), ptr(b), ptr(z), rows, d, _s())

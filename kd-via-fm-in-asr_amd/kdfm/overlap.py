@@ -52,6 +52,11 @@ class WgradOverlap:
         self._keep.extend(keep)
         self._pending = True
 
+    def stream(self):
+        """The side stream of the current device (created on first use).  The engine also borrows it in
+        the forward, where no weight gradient runs, for the first layer-half of the KD heads."""
+        return self._stream(K.current_device())
+
     def stream_after_current(self):
         """The side stream, ordered after all current main-stream work (None when weight gradients run
         in line): the bucketed all-reduce issues its collectives from it, so they start after both the

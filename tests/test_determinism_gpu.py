@@ -17,12 +17,11 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _run(cfg, wav, wl, tg, tl, eps, teacher_graph=True, overlap=None):
+def _run(cfg, wav, wl, tg, tl, eps, overlap=None):
     from kdfm.engine import Ver5Engine
     eng = Ver5Engine(cfg, "cuda", teacher_seed=0, student_seed=1, heads_seed=2)
     if overlap is not None:
         eng.overlap_wgrad = overlap
-    eng.teacher_graph = teacher_graph
     eng.set_seed(77)
     eng.advance_rng()
     ctx = eng.forward(wav, wl, tg, tl, train=True, eps=eps)
@@ -32,11 +31,9 @@ def _run(cfg, wav, wl, tg, tl, eps, teacher_graph=True, overlap=None):
     return eng.losses.clone(), feats, eng.student.grads()
 
 
-@pytest.mark.parametrize("which", ["f32-parity", "bf16-train", "bf16-train-teacher-graph-vs-eager",
-                                   "bf16-train-overlapped-vs-serialised"])
+@pytest.mark.parametrize("which", ["f32-parity", "bf16-train", "bf16-train-overlapped-vs-serialised"])
 def test_step_is_bitwise_reproducible(which):
-    """The third case replays the frozen teacher as a captured HIP graph in run 1 and issues it
-    eagerly in run 2: the graph must not change a single bit.  The fourth runs the benchmark's
+    """The third case runs the benchmark's
     schedule (weight gradients on the side stream, overlapping the data-gradient chain) in run 1 and
     every weight gradient in line in run 2, both with ordered reductions: the overlap changes when
     kernels run, never what they compute, so any difference is a cross-stream race."""
@@ -58,8 +55,7 @@ def test_step_is_bitwise_reproducible(which):
     eps = torch.randn(cfg.n_layers * B * T, cfg.latent, generator=g).cuda() if which == "f32-parity" else None
     ov = which.endswith("overlapped-vs-serialised")
     l1, f1, g1 = _run(cfg, wav, wl, tg, tl, eps, overlap=True if ov else None)
-    l2, f2, g2 = _run(cfg, wav, wl, tg, tl, eps, teacher_graph=not which.endswith("vs-eager"),
-                      overlap=False if ov else None)
+    l2, f2, g2 = _run(cfg, wav, wl, tg, tl, eps, overlap=False if ov else None)
     assert all(torch.isfinite(v).all() for v in g1.values())
     assert torch.equal(f1, f2), "hooked layer outputs differ between runs"
     bad = [k for k in g1 if not torch.equal(g1[k], g2[k])]

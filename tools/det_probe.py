@@ -1,4 +1,4 @@
-"""Which stage makes the teacher-graph forward differ from the eager one?  Runs the
+"""(Historical, round 3: the captured-teacher path it probed is removed.)  Which stage made the teacher-graph forward differ from the eager one?  Ran the
 test_determinism bf16 'teacher-graph-vs-eager' forward twice and compares every frontend output
 (teacher and student, in call order) and the hooked layer outputs bitwise.
 usage: python tools/det_probe.py"""

@@ -15,6 +15,6 @@ if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "test process rc=$rc: stopping"; ex
 timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 > "$OUT/bench.log" 2>&1 || { echo "bench failed"; tail -20 "$OUT/bench.log"; exit 3; }
 tail -1 "$OUT/bench.log" | cut -c1-400
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv \
-  -- python3 -u bench.py --steps 5 --warmup 2 --no-cpu-baseline > "$OUT/prof_bench.log" 2>&1 || { echo "prof failed"; exit 4; }
+  -- python3 -u bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-f32-sensitivity > "$OUT/prof_bench.log" 2>&1 || { echo "prof failed"; exit 4; }
 echo "prof ok"
 exit $rc
