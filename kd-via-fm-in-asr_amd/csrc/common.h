@@ -61,7 +61,9 @@ __device__ __forceinline__ V pack_bf16x8(const float* v) {
   return __builtin_bit_cast(V, w);
 }
 
-__device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
+// v_rcp_f32 (1 ulp) instead of the IEEE division sequence (div_scale / div_fmas / div_fixup, ~10 VALU
+// ops per element): the SiLU / GLU epilogues of the fused LN-block kernels were VALU-bound on it
+__device__ __forceinline__ float sigmoidf_(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
 __device__ __forceinline__ float siluf_(float x) { return x * sigmoidf_(x); }
 __device__ __forceinline__ float dsiluf_(float x) {
   float s = sigmoidf_(x);

@@ -31,6 +31,11 @@
 #include "lnblock.h"
 #include "wimg.h"
 
+// timing probe points (tools/ffn_probe.hip defines FFN_PROBE; empty in the library)
+#ifndef FFN_PROBE
+#define FFN_PROBE(i)
+#endif
+
 namespace kdfm {
 namespace {
 
@@ -118,9 +123,10 @@ __global__ __launch_bounds__(fwd_nt<DT>()) void ffn_fwd_kernel(FfnFwd a) {
   const uint64_t kact = rng_key(seed, a.st_act), kout = rng_key(seed, a.st_out);
   const float ks_act = 1.f / (1.f - a.p_act), ks_out = 1.f / (1.f - a.p_out);
 
-  Stager<G::FWD, 0, G::CS, FWD_NP, FWD_NT> stg;
+  FFN_PROBE(0);
+  using DS = DmaStager<G::FWD, 0, G::CS, FWD_NP, FWD_NT>;
   const uint4* img = reinterpret_cast<const uint4*>(a.img);
-  stg.load(img, 0, FC);
+  DS::issue(img, 0, FC, ff_lds, 0);
 
   float mean = 0.f, rstd = 0.f;
   bf16x8 bx[KS1];
@@ -151,14 +157,24 @@ __global__ __launch_bounds__(fwd_nt<DT>()) void ffn_fwd_kernel(FfnFwd a) {
         xres[mt][q] = *reinterpret_cast<const float4*>(a.x + (in ? row * d + n0 : 0));
       }
   }
-  stg.store(ff_lds, 0);
+  FFN_PROBE(1);
   __syncthreads();
+  FFN_PROBE(2);
   const int nit = (FC + FWD_NP - 1) / FWD_NP;
   for (int it = 0; it < nit; ++it) {
-    if (it + 1 < nit) stg.load(img, it + 1, FC);
+    // no branch around the chunk (a conditional MFMA block makes the compiler carry acc through the
+    // loop in VGPRs and copy it to and from AGPRs every iteration): a parity past the last chunk
+    // computes on the clamped, loaded last block and adds an all-zero activation operand (+0 exactly)
     const int c = FWD_NP * it + par;
-    if (c < FC) {
-      const uint4* W = stg.block(ff_lds, it & 1, par);
+    const bool live = c < FC;
+    // the chunk's biases are read from LDS BEFORE the next stage's DMA is issued: an LDS read while an
+    // LDS-DMA is in flight makes the compiler drain it (vmcnt(0)) first
+    float4 bq[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) bq[q] = *reinterpret_cast<const float4*>(bias_s + c * 32 + 8 * q + 4 * h);
+    if (it + 1 < nit) DS::issue(img, it + 1, FC, ff_lds, (it + 1) & 1);
+    {
+      const uint4* W = DS::block(ff_lds, it & 1, par);
       f32x16 hacc;
 #pragma unroll
       for (int i = 0; i < 16; ++i) hacc[i] = 0.f;
@@ -169,8 +185,7 @@ __global__ __launch_bounds__(fwd_nt<DT>()) void ffn_fwd_kernel(FfnFwd a) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int n0 = c * 32 + 8 * q + 4 * h;
-        const float4 bb = *reinterpret_cast<const float4*>(bias_s + n0);
-        const float bv[4] = {bb.x, bb.y, bb.z, bb.w};
+        const float bv[4] = {bq[q].x, bq[q].y, bq[q].z, bq[q].w};
         float v[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) v[i] = siluf_(hacc[4 * q + i] + bv[i]);
@@ -181,8 +196,8 @@ __global__ __launch_bounds__(fwd_nt<DT>()) void ffn_fwd_kernel(FfnFwd a) {
 #pragma unroll
           for (int i = 0; i < 4; ++i) v[i] = kp[i] ? v[i] * ks_act : 0.f;
         }
-        pk[q][0] = pack_bf16x2(v[0], v[1]);
-        pk[q][1] = pack_bf16x2(v[2], v[3]);
+        pk[q][0] = live ? pack_bf16x2(v[0], v[1]) : 0u;
+        pk[q][1] = live ? pack_bf16x2(v[2], v[3]) : 0u;
       }
       bf16x8 ba[2];
       tile_operands(pk, ba);
@@ -192,8 +207,9 @@ __global__ __launch_bounds__(fwd_nt<DT>()) void ffn_fwd_kernel(FfnFwd a) {
         for (int s = 0; s < 2; ++s)
           acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(W[(2 * mt + s) * FRAG_U4 + lane]), ba[s], acc[mt], 0, 0, 0);
     }
-    if (it + 1 < nit) stg.store(ff_lds, (it + 1) & 1);
+    FFN_PROBE(4 + 2 * it);
     __syncthreads();
+    FFN_PROBE(5 + 2 * it);
   }
   // partials of parities 1..NP-1 -> parity 0, added in the fixed order ((p0 + p1) + p2) + p3
   float* red = reinterpret_cast<float*>(ff_lds) + tile * ((FWD_NP - 1) * DT * 16 * 64);
@@ -205,6 +221,7 @@ __global__ __launch_bounds__(fwd_nt<DT>()) void ffn_fwd_kernel(FfnFwd a) {
       for (int i = 0; i < 16; ++i) mine[(mt * 16 + i) * 64 + lane] = acc[mt][i];
   }
   __syncthreads();
+  FFN_PROBE(30);
   if (par != 0) return;   // (every lane of the parity-0 wave stays: the optional LN reduces across lanes)
 #pragma unroll
   for (int q = 1; q < FWD_NP; ++q)
@@ -239,6 +256,7 @@ __global__ __launch_bounds__(fwd_nt<DT>()) void ffn_fwd_kernel(FfnFwd a) {
         *reinterpret_cast<float4*>(a.out + row * d + n0) =
             make_float4(o[mt][4 * q], o[mt][4 * q + 1], o[mt][4 * q + 2], o[mt][4 * q + 3]);
     }
+  FFN_PROBE(31);
   if (!a.ln_out) return;
   // norm_out: two-pass row statistics (this lane's half of the row + its partner lane's)
   float s = 0.f;
@@ -303,9 +321,9 @@ __global__ __launch_bounds__(bwd_nt<DT>()) void ffn_bwd_kernel(FfnBwd a) {
   const uint64_t kact = rng_key(seed, a.st_act), kout = rng_key(seed, a.st_out);
   const float ks_act = 1.f / (1.f - a.p_act), ks_out = 1.f / (1.f - a.p_out);
 
-  Stager<G::BWD, 2 * DT, G::CS, NP, NT> stg;
+  using DS = DmaStager<G::BWD, 2 * DT, G::CS, NP, NT>;
   const uint4* img = reinterpret_cast<const uint4*>(a.img);
-  stg.load(img, 0, FC);
+  DS::issue(img, 0, FC, ff_lds, 0);
 
   // dl2 = rscale * drop_out(dout): B operands of dA^T; the even wave writes the bf16 copy (dW2 operand)
   bf16x8 bd[KS1];
@@ -341,14 +359,19 @@ __global__ __launch_bounds__(bwd_nt<DT>()) void ffn_bwd_kernel(FfnBwd a) {
 
   float* bias_s = reinterpret_cast<float*>(reinterpret_cast<char*>(ff_lds) + ffn_stage_bytes<G::BWD, DT>());
   for (int e = threadIdx.x; e < ff; e += NT) bias_s[e] = a.b1[e];
-  stg.store(ff_lds, 0);
   __syncthreads();
   const int nit = (FC + NP - 1) / NP;
   for (int it = 0; it < nit; ++it) {
-    if (it + 1 < nit) stg.load(img, it + 1, FC);
+    // branch-free chunk (as the forward): a parity past the last chunk adds an all-zero dh operand
+    // and stores nothing; its biases are read before the next stage's DMA is issued
     const int c = NP * it + par;
-    if (c < FC) {
-      const uint4* W = ff_lds + ((it & 1) * NP + par) * G::BWD * FRAG_U4;   // W1c | W2Tc | W1Tc
+    const bool live = c < FC;
+    float4 bq[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) bq[q] = *reinterpret_cast<const float4*>(bias_s + (live ? c * 32 : 0) + 8 * q + 4 * h);
+    if (it + 1 < nit) DS::issue(img, it + 1, FC, ff_lds, (it + 1) & 1);
+    {
+      const uint4* W = DS::block(ff_lds, it & 1, par);   // W1c | W2Tc | W1Tc
       f32x16 hacc, gacc;
 #pragma unroll
       for (int i = 0; i < 16; ++i) hacc[i] = gacc[i] = 0.f;
@@ -361,8 +384,7 @@ __global__ __launch_bounds__(bwd_nt<DT>()) void ffn_bwd_kernel(FfnBwd a) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int n0 = c * 32 + 8 * q + 4 * h;
-        const float4 bb = *reinterpret_cast<const float4*>(bias_s + n0);
-        const float bv[4] = {bb.x, bb.y, bb.z, bb.w};
+        const float bv[4] = {bq[q].x, bq[q].y, bq[q].z, bq[q].w};
         float av[4], dv[4];
         bool kq[4] = {true, true, true, true};
         if (a.p_act > 0.f) {
@@ -383,13 +405,13 @@ __global__ __launch_bounds__(bwd_nt<DT>()) void ffn_bwd_kernel(FfnBwd a) {
         }
         pa[q][0] = pack_bf16x2(av[0], av[1]);
         pa[q][1] = pack_bf16x2(av[2], av[3]);
-        pd[q][0] = pack_bf16x2(dv[0], dv[1]);
-        pd[q][1] = pack_bf16x2(dv[2], dv[3]);
+        pd[q][0] = live ? pack_bf16x2(dv[0], dv[1]) : 0u;
+        pd[q][1] = live ? pack_bf16x2(dv[2], dv[3]) : 0u;
       }
       bf16x8 ba[2], bdh[2];
       tile_operands(pa, ba);
       tile_operands(pd, bdh);
-      if (ok) {
+      if (ok && live) {
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
           const int64_t off = row * ff + c * 32 + s * 16 + 8 * h;
@@ -404,7 +426,6 @@ __global__ __launch_bounds__(bwd_nt<DT>()) void ffn_bwd_kernel(FfnBwd a) {
           acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(W[(2 * KS1 + 2 * mt + s) * FRAG_U4 + lane]), bdh[s],
                                                             acc[mt], 0, 0, 0);
     }
-    if (it + 1 < nit) stg.store(ff_lds, (it + 1) & 1);
     __syncthreads();
   }
   // partials of parities 1..NP-1 -> parity 0, added in the fixed order ((p0 + p1) + p2) + p3

@@ -86,6 +86,37 @@ struct Stager {
   }
 };
 
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void gl_void_t;
+
+// The same double-buffered staging by LDS-DMA (global_load_lds_dwordx4): one wave-instruction moves
+// one 1 KB fragment of the image (lane l: bytes 16 l .. 16 l + 15) straight into its LDS block, so no
+// staging registers and no ds_write pass.  A slot past the last block gets the last block again
+// (finite data for callers that compute on it branch-free and discard the result).  The DMA of a stage is retired by the vmcnt(0) that the next __syncthreads()
+// emits while an LDS-DMA is in flight (cdna_hip_programming.md §5 'Async global->LDS copy').
+template <int SF, int OFF, int STRIDE, int SLOTS, int NT>
+struct DmaStager {
+  static constexpr int UNITS = SLOTS * SF * FRAG_U4;
+  static constexpr int NFR = SLOTS * SF;
+  static constexpr int NW = NT / 64;
+  __device__ __forceinline__ static void issue(const uint4* __restrict__ img, int it, int nblk, uint4* lds, int buf) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int i = 0; i < (NFR + NW - 1) / NW; ++i) {
+      const int f = wave + NW * i;   // wave-uniform
+      if (f < NFR) {
+        const int slot = f / SF, w = f - slot * SF;
+        const int c = SLOTS * it + slot < nblk ? SLOTS * it + slot : nblk - 1;
+        __builtin_amdgcn_global_load_lds((gl_void_t*)(img + ((int64_t)c * STRIDE + OFF + w) * FRAG_U4 + lane),
+                                         (lds_void_t*)(lds + buf * UNITS + f * FRAG_U4), 16, 0, 0);
+      }
+    }
+  }
+  __device__ __forceinline__ static const uint4* block(const uint4* lds, int buf, int slot) {
+    return lds + buf * UNITS + slot * SF * FRAG_U4;
+  }
+};
+
 // Row r = `row` of x (d features, 16-B aligned rows) normalised into the B operands bx[ks]
 // (features 16 ks + 8 h .. +7; zero beyond d).  have_stats: mean / rstd given (backward recompute);
 // else computed (two-pass, biased variance, as kdfm_layernorm_fwd).  ln_out: bf16 copy of the row.
@@ -130,16 +161,16 @@ __device__ __forceinline__ void ln_operands(const float* __restrict__ x, const f
     const int k0 = ks * 16 + 8 * h;
     const bool in = k0 < d;
     float y[8];
-    if (in) {
-      const float4 g0 = *reinterpret_cast<const float4*>(g + k0), g1 = *reinterpret_cast<const float4*>(g + k0 + 4);
-      const float4 b0 = *reinterpret_cast<const float4*>(b + k0), b1 = *reinterpret_cast<const float4*>(b + k0 + 4);
+    {
+      // unconditional loads at a clamped index (speculatable: the compiler may issue them beside the
+      // row loads instead of one dependent L2 round trip after the statistics)
+      const int kc = in ? k0 : 0;
+      const float4 g0 = *reinterpret_cast<const float4*>(g + kc), g1 = *reinterpret_cast<const float4*>(g + kc + 4);
+      const float4 b0 = *reinterpret_cast<const float4*>(b + kc), b1 = *reinterpret_cast<const float4*>(b + kc + 4);
       const float gg[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
       const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
 #pragma unroll
-      for (int j = 0; j < 8; ++j) y[j] = (xv[ks][j] - mean) * rstd * gg[j] + bb[j];
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) y[j] = 0.f;
+      for (int j = 0; j < 8; ++j) y[j] = in ? (xv[ks][j] - mean) * rstd * gg[j] + bb[j] : 0.f;
     }
     bx[ks] = pack_bf16x8<bf16x8>(y);
     if (ln_out && ok && in) *reinterpret_cast<bf16x8*>(ln_out + row * d + k0) = bx[ks];

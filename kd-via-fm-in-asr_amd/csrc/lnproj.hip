@@ -70,16 +70,15 @@ struct LpFwd {
 template <int KS1, int DT, int MODE>
 __global__ __launch_bounds__(LP_NT) void lnproj_fwd_kernel(LpFwd a) {
   using Gm = LpGeo<KS1, DT, MODE>;
-  using St = Stager<Gm::UF, 0, Gm::UF, LP_NP, LP_NT>;
+  using St = DmaStager<Gm::UF, 0, Gm::UF, LP_NP, LP_NT>;
   extern __shared__ __attribute__((aligned(16))) uint4 lp_lds[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int h = lane >> 5, p = wave % LP_NP, tile = wave / LP_NP;
   const int64_t row = (int64_t)blockIdx.x * LP_ROWS + tile * 32 + (lane & 31);
   const bool ok = row < a.rows;
   const int d = a.d;
-  St stg;
   const uint4* img = reinterpret_cast<const uint4*>(a.img);
-  stg.load(img, 0, Gm::NU);
+  St::issue(img, 0, Gm::NU, lp_lds, 0);
   float mean = 0.f, rstd = 0.f;
   bf16x8 bx[KS1];
   ln_operands<KS1>(a.x, a.g, a.b, row, ok, d, h, a.eps, false, mean, rstd, bx, p == 0 ? a.ln_h : nullptr);
@@ -96,11 +95,25 @@ __global__ __launch_bounds__(LP_NT) void lnproj_fwd_kernel(LpFwd a) {
   const int nvec = (MODE == LP_QKV ? 5 : 2) * d;
   for (int e = threadIdx.x; e < nvec; e += LP_NT)
     vec_s[e] = e < Gm::G * d ? a.bias[e] : (e < 4 * d ? a.pu[e - 3 * d] : a.pv[e - 4 * d]);
-  stg.store(lp_lds, 0);
   __syncthreads();
   for (int s = 0; s < S; ++s) {
-    if (s + 1 < S) stg.load(img, s + 1, Gm::NU);
     const int u = s * LP_NP + p;
+    // this unit's bias vectors are read from LDS before the next stage's DMA is issued (an LDS read
+    // while an LDS-DMA is in flight makes the compiler drain it first)
+    float4 vb[2][4], vq[2][4];
+    {
+      const int uu = u < Gm::NU ? u : 0;
+      const int t = MODE == LP_QKV ? uu / 3 : uu, g = MODE == LP_QKV ? uu % 3 : 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int n0 = 32 * t + 8 * q + 4 * h < d ? 32 * t + 8 * q + 4 * h : 0;
+        vb[0][q] = *reinterpret_cast<const float4*>(vec_s + g * d + n0);
+        vb[1][q] = *reinterpret_cast<const float4*>(vec_s + d + n0);   // GLU: gate bias
+        vq[0][q] = *reinterpret_cast<const float4*>(vec_s + 3 * (MODE == LP_QKV) * d + n0);
+        vq[1][q] = *reinterpret_cast<const float4*>(vec_s + 4 * (MODE == LP_QKV) * d + n0);
+      }
+    }
+    if (s + 1 < S) St::issue(img, s + 1, Gm::NU, lp_lds, (s + 1) & 1);
     if (u < Gm::NU) {
       const uint4* W = St::block(lp_lds, s & 1, p);
       if constexpr (MODE == LP_QKV) {
@@ -112,12 +125,12 @@ __global__ __launch_bounds__(LP_NT) void lnproj_fwd_kernel(LpFwd a) {
         for (int q = 0; q < 4; ++q) {
           const int n0 = 32 * t + 8 * q + 4 * h;
           if (!ok || n0 >= d) continue;
-          const float4 bb = *reinterpret_cast<const float4*>(vec_s + g * d + n0);
+          const float4 bb = vb[0][q];
           const float v0 = acc[4 * q] + bb.x, v1 = acc[4 * q + 1] + bb.y, v2 = acc[4 * q + 2] + bb.z,
                       v3 = acc[4 * q + 3] + bb.w;
           if (g == 0) {
-            const float4 uu = *reinterpret_cast<const float4*>(vec_s + 3 * d + n0);
-            const float4 vv = *reinterpret_cast<const float4*>(vec_s + 4 * d + n0);
+            const float4 uu = vq[0][q];
+            const float4 vv = vq[1][q];
             *reinterpret_cast<float4*>(a.qu + row * d + n0) = make_float4(v0 + uu.x, v1 + uu.y, v2 + uu.z, v3 + uu.w);
             *reinterpret_cast<float4*>(a.qv + row * d + n0) = make_float4(v0 + vv.x, v1 + vv.y, v2 + vv.z, v3 + vv.w);
           } else {
@@ -136,8 +149,8 @@ __global__ __launch_bounds__(LP_NT) void lnproj_fwd_kernel(LpFwd a) {
         for (int q = 0; q < 4; ++q) {
           const int n0 = 32 * t + 8 * q + 4 * h;
           if (!ok || n0 >= d) continue;
-          const float4 ba = *reinterpret_cast<const float4*>(vec_s + n0);
-          const float4 bg = *reinterpret_cast<const float4*>(vec_s + d + n0);
+          const float4 ba = vb[0][q];
+          const float4 bg = vb[1][q];
           const float va[4] = {aa[4 * q] + ba.x, aa[4 * q + 1] + ba.y, aa[4 * q + 2] + ba.z, aa[4 * q + 3] + ba.w};
           const float vg[4] = {ag[4 * q] + bg.x, ag[4 * q + 1] + bg.y, ag[4 * q + 2] + bg.z, ag[4 * q + 3] + bg.w};
           float o[4];
@@ -147,7 +160,6 @@ __global__ __launch_bounds__(LP_NT) void lnproj_fwd_kernel(LpFwd a) {
         }
       }
     }
-    if (s + 1 < S) stg.store(lp_lds, (s + 1) & 1);
     __syncthreads();
   }
 }
@@ -191,16 +203,15 @@ __device__ __forceinline__ void lp_finish(f32x16 (&acc)[DT], float* red, const L
 template <int KS1, int DT>
 __global__ __launch_bounds__(LP_NT) void ln_qkv_bwd_kernel(LpBwd a) {
   using Gm = LpGeo<KS1, DT, LP_QKV>;
-  using St = Stager<Gm::TB, 0, Gm::TB, 1, LP_NT>;
+  using St = DmaStager<Gm::TB, 0, Gm::TB, 1, LP_NT>;
   extern __shared__ __attribute__((aligned(16))) uint4 lp_lds[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int h = lane >> 5, p = wave % LP_NP, tile = wave / LP_NP;   // p = kind (q, k, v)
   const int64_t row = (int64_t)blockIdx.x * LP_ROWS + tile * 32 + (lane & 31);
   const bool ok = row < a.rows;
   const int d = a.d;
-  St stg;
   const uint4* img = reinterpret_cast<const uint4*>(a.img);
-  stg.load(img, 0, DT);
+  St::issue(img, 0, DT, lp_lds, 0);
   // B operands of this kind: dproj features 32 t + 16 s2 + 8 h .. +7
   bf16x8 bop[2 * DT];
 #pragma unroll
@@ -232,17 +243,15 @@ __global__ __launch_bounds__(LP_NT) void ln_qkv_bwd_kernel(LpBwd a) {
   f32x16 acc[DT];
 #pragma unroll
   for (int mt = 0; mt < DT; ++mt) acc[mt] = zero16();
-  stg.store(lp_lds, 0);
   __syncthreads();
   for (int t = 0; t < DT; ++t) {
-    if (t + 1 < DT) stg.load(img, t + 1, DT);
+    if (t + 1 < DT) St::issue(img, t + 1, DT, lp_lds, (t + 1) & 1);
     const uint4* W = St::block(lp_lds, t & 1, 0);
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
       for (int mt = 0; mt < DT; ++mt)
         acc[mt] = mfma32(W[((2 * p + s2) * DT + mt) * FRAG_U4 + lane], bop[2 * t + s2], acc[mt]);
-    if (t + 1 < DT) stg.store(lp_lds, (t + 1) & 1);
     __syncthreads();
   }
   if (a.part_uv && p > 0) {
@@ -284,7 +293,7 @@ __global__ __launch_bounds__(LP_NT) void ln_qkv_bwd_kernel(LpBwd a) {
 template <int KS1, int DT>
 __global__ __launch_bounds__(LP_NT) void ln_glu_bwd_kernel(LpBwd a) {
   using Gm = LpGeo<KS1, DT, LP_GLU>;
-  using St = Stager<Gm::BB, 0, Gm::BB, LP_NP, LP_NT>;
+  using St = DmaStager<Gm::BB, 0, Gm::BB, LP_NP, LP_NT>;
   static_assert(DT <= LP_NP, "one GLU group per wave");
   extern __shared__ __attribute__((aligned(16))) uint4 lp_lds[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -292,8 +301,7 @@ __global__ __launch_bounds__(LP_NT) void ln_glu_bwd_kernel(LpBwd a) {
   const int64_t row = (int64_t)blockIdx.x * LP_ROWS + tile * 32 + (lane & 31);
   const bool ok = row < a.rows;
   const int d = a.d;
-  St stg;
-  stg.load(reinterpret_cast<const uint4*>(a.img), 0, DT);
+  St::issue(reinterpret_cast<const uint4*>(a.img), 0, DT, lp_lds, 0);
   float mean = ok ? a.mean[row] : 0.f, rstd = ok ? a.rstd[row] : 0.f;
   bf16x8 bx[KS1];
   ln_operands<KS1>(a.x, a.g, a.b, row, ok, d, h, 0.f, true, mean, rstd, bx, p == 0 ? a.ln_h : nullptr);
@@ -302,7 +310,6 @@ __global__ __launch_bounds__(LP_NT) void ln_glu_bwd_kernel(LpBwd a) {
   f32x16 acc[DT];
 #pragma unroll
   for (int mt = 0; mt < DT; ++mt) acc[mt] = zero16();
-  stg.store(lp_lds, 0);
   __syncthreads();
   const int t = p;
   if (t < DT) {
