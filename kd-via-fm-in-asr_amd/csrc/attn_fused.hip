@@ -20,6 +20,11 @@
 // Output O is written straight into the (rows, d) head-interleaved layout.
 #include "gemm_common.h"
 
+// timing probe points (tools/attn_probe.hip defines KPROBE; empty in the library)
+#ifndef KPROBE
+#define KPROBE(i)
+#endif
+
 namespace kdfm {
 namespace {
 
@@ -64,18 +69,31 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
+// reductions over the 16 lanes of a DPP row (one query row's 16 key columns of a C tile) by DPP moves
+// (VALU, no LDS round trip as ds_bpermute): quad_perm [1,0,3,2], quad_perm [2,3,0,1], row_half_mirror,
+// row_mirror -- every lane ends with the same value (commutative pairings of the same tree)
+template <int CTRL>
+__device__ __forceinline__ float dppmov(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
 __device__ __forceinline__ float group16_max(float v) {
-#pragma unroll
-  for (int o = 8; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
+  v = fmaxf(v, dppmov<0xB1>(v));
+  v = fmaxf(v, dppmov<0x4E>(v));
+  v = fmaxf(v, dppmov<0x141>(v));
+  return fmaxf(v, dppmov<0x140>(v));
 }
 __device__ __forceinline__ float group16_sum(float v) {
-#pragma unroll
-  for (int o = 8; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  v += dppmov<0xB1>(v);
+  v += dppmov<0x4E>(v);
+  v += dppmov<0x141>(v);
+  return v + dppmov<0x140>(v);
 }
 
-template <bool TWO_PASS, int NU>   // NU: 16-column output tiles of the head dim (3: dk <= 48, 4: dk <= 64)
+// NU: 16-column output tiles of the head dim (3: dk <= 48, 4: dk <= 64); WPT (single pass): p~ and m_blk
+// are written -- through buffer stores whose out-of-range lanes carry an offset past the buffer (dropped
+// by the range check) instead of a branch, so each key block issues a fixed number of stores and the
+// wait for the next block's staged loads counts past them instead of draining them (vmcnt(0))
+template <bool TWO_PASS, int NU, bool WPT = false>
 __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void relpos_attn_fwd_kernel(AttnP p) {
   __shared__ __attribute__((aligned(16))) uint16_t Ks[AKB * LDR];
   __shared__ __attribute__((aligned(16))) uint16_t Vt[DKP * LDVT];
@@ -83,6 +101,7 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void relpos_attn_fwd_kernel(A
   __shared__ __attribute__((aligned(16))) float Gs[4][16 * LDG];
   __shared__ __attribute__((aligned(16))) uint16_t Ps[4][16 * LDPS];
 
+  KPROBE(0);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int T = (int)p.T, dk = (int)p.dk;
   const Blk3 blk = xcd_block3();
@@ -92,6 +111,12 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void relpos_attn_fwd_kernel(A
   const int len = p.lens ? (int)p.lens[b] : T;
   const int nkb = (min(len, T) + AKB - 1) / AKB;  // key blocks with at least one valid key
   const int npos = 2 * T - 1;
+  constexpr uint32_t OOB = 0x80000000u;
+  const int nkb_all = (T + AKB - 1) / AKB;
+  const __amdgpu_buffer_rsrc_t rpt =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.pt, (short)0, WPT ? (int)(p.B * p.H * p.T * p.T * 2) : 0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rmb =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.mblk, (short)0, WPT ? (int)(p.B * p.H * p.T * nkb_all * 4) : 0, 0x00020000);
   const int64_t hoff = h * p.dk;
 
   // zero the padded head-dim columns once (never overwritten afterwards)
@@ -124,56 +149,78 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void relpos_attn_fwd_kernel(A
   for (int r = 0; r < 4; ++r) { mrow[r] = -3.0e38f; lrow[r] = 0.f; }
 
   // ---- staging of one key block: all global loads of a stage are issued before any LDS store
-  // (register staging; the next block's loads are in flight while this block computes) ----
+  // (register staging; the next block's loads are in flight while this block computes).  The per-thread
+  // staging geometry is loop invariant and computed once; every load is issued unconditionally from a
+  // clamped valid address and out-of-range elements are zeroed by a select at store time (a load under
+  // a runtime condition is branched around and waited for one by one) ----
   constexpr int KU = (AKB * 4 * NU + 255) / 256;    // K / V float4 per thread (dk <= 16 NU)
   constexpr int PU = (BAND * 4 * NU + 255) / 256;   // P-band float4 per thread
   const int cq = dk >> 2;
+  int kj[KU], kc[KU], pj[PU], pc[PU];
+  uint32_t kin = 0u, pin = 0u;   // bit i: slot i maps to a real (row, column) of the tile
+#pragma unroll
+  for (int i = 0; i < KU; ++i) {
+    const int e = threadIdx.x + i * 256;
+    const bool in = e < AKB * cq;
+    const int ee = in ? e : 0;
+    kj[i] = ee / cq;
+    kc[i] = (ee - kj[i] * cq) * 4;
+    kin |= (in ? 1u : 0u) << i;
+  }
+#pragma unroll
+  for (int i = 0; i < PU; ++i) {
+    const int e = threadIdx.x + i * 256;
+    const bool in = e < BAND * cq;
+    const int ee = in ? e : 0;
+    pj[i] = ee / cq;
+    pc[i] = (ee - pj[i] * cq) * 4;
+    pin |= (in ? 1u : 0u) << i;
+  }
+  const float* kbase = p.k + b * p.T * p.ldkv + hoff;
+  const float* vbase = p.v + b * p.T * p.ldkv + hoff;
+  const float* pbase = p.pos + hoff;
   float4 rk[KU], rv[KU], rp[PU];
+  uint32_t kok = 0u, pok = 0u;   // validity of the staged slots of the stage in flight
   auto load_stage = [&](int j0, bool with_v) {
+    kok = 0u;
 #pragma unroll
     for (int i = 0; i < KU; ++i) {
-      const int e = threadIdx.x + i * 256;
-      const int jj = e / cq, c4 = (e - jj * cq) * 4;
-      const int j = j0 + jj;
-      const bool ok = e < AKB * cq && j < T;
-      const int64_t off = (b * p.T + j) * p.ldkv + hoff + c4;
-      rk[i] = ok ? *reinterpret_cast<const float4*>(p.k + off) : make_float4(0.f, 0.f, 0.f, 0.f);
-      rv[i] = (ok && with_v) ? *reinterpret_cast<const float4*>(p.v + off) : make_float4(0.f, 0.f, 0.f, 0.f);
+      const int j = j0 + kj[i];
+      const bool ok = ((kin >> i) & 1u) && j < T;
+      const int64_t off = (int64_t)(ok ? j : 0) * p.ldkv + kc[i];
+      rk[i] = *reinterpret_cast<const float4*>(kbase + off);
+      if (with_v) rv[i] = *reinterpret_cast<const float4*>(vbase + off);
+      kok |= (ok ? 1u : 0u) << i;
     }
     const int rbase = T - 1 - (i0 + AQ - 1) + j0;  // P band rows r = rbase + rr
+    pok = 0u;
 #pragma unroll
     for (int i = 0; i < PU; ++i) {
-      const int e = threadIdx.x + i * 256;
-      const int rr = e / cq, c4 = (e - rr * cq) * 4;
-      const int r = rbase + rr;
-      const bool ok = e < BAND * cq && r >= 0 && r < npos;
-      rp[i] = ok ? *reinterpret_cast<const float4*>(p.pos + (int64_t)r * p.d + hoff + c4)
-                 : make_float4(0.f, 0.f, 0.f, 0.f);
+      const int r = rbase + pj[i];
+      const bool ok = ((pin >> i) & 1u) && r >= 0 && r < npos;
+      rp[i] = *reinterpret_cast<const float4*>(pbase + (int64_t)(ok ? r : 0) * p.d + pc[i]);
+      pok |= (ok ? 1u : 0u) << i;
     }
   };
   auto store_stage = [&](bool with_v) {
+    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
     for (int i = 0; i < KU; ++i) {
-      const int e = threadIdx.x + i * 256;
-      if (e < AKB * cq) {
-        const int jj = e / cq, c4 = (e - jj * cq) * 4;
-        store4_bf16(Ks + jj * LDR + c4, rk[i]);
+      if ((kin >> i) & 1u) {
+        const bool ok = (kok >> i) & 1u;
+        store4_bf16(Ks + kj[i] * LDR + kc[i], ok ? rk[i] : z);
         if (with_v) {
-          Vt[(c4 + 0) * LDVT + jj] = f2bf(rv[i].x);
-          Vt[(c4 + 1) * LDVT + jj] = f2bf(rv[i].y);
-          Vt[(c4 + 2) * LDVT + jj] = f2bf(rv[i].z);
-          Vt[(c4 + 3) * LDVT + jj] = f2bf(rv[i].w);
+          const float4 vv = ok ? rv[i] : z;
+          Vt[(kc[i] + 0) * LDVT + kj[i]] = f2bf(vv.x);
+          Vt[(kc[i] + 1) * LDVT + kj[i]] = f2bf(vv.y);
+          Vt[(kc[i] + 2) * LDVT + kj[i]] = f2bf(vv.z);
+          Vt[(kc[i] + 3) * LDVT + kj[i]] = f2bf(vv.w);
         }
       }
     }
 #pragma unroll
-    for (int i = 0; i < PU; ++i) {
-      const int e = threadIdx.x + i * 256;
-      if (e < BAND * cq) {
-        const int rr = e / cq, c4 = (e - rr * cq) * 4;
-        store4_bf16(Pr + rr * LDR + c4, rp[i]);
-      }
-    }
+    for (int i = 0; i < PU; ++i)
+      if ((pin >> i) & 1u) store4_bf16(Pr + pj[i] * LDR + pc[i], ((pok >> i) & 1u) ? rp[i] : z);
   };
 
   // scores of this wave's 16 rows x 64 keys of block j0, C layout: s[t][r] = S[ii][16t + (lane&15)]
@@ -219,6 +266,13 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void relpos_attn_fwd_kernel(A
   // ---- pass 1 (two-pass mode): row max / sum ----
   if (TWO_PASS && nkb > 0) load_stage(0, false);
   if (!TWO_PASS && nkb > 0) load_stage(0, true);
+  if constexpr (WPT) {
+    // the loop body leaves its 4 m_blk + 16 p~ stores behind the next block's loads; the same number of
+    // (range-dropped) stores behind the first block's loads lets the compiler's wait for a staged load
+    // count past them on every path into the loop instead of draining the stores (vmcnt(0))
+#pragma unroll
+    for (int i = 0; i < 20; ++i) __builtin_amdgcn_raw_buffer_store_b16((uint16_t)0, rpt, OOB + 2u * i, 0, 0);
+  }
   for (int kb = 0; kb < (TWO_PASS ? nkb : 0); ++kb) {
     const int j0 = kb * AKB;
     __syncthreads();
@@ -247,20 +301,39 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void relpos_attn_fwd_kernel(A
 
   // ---- pass 2: probabilities, dropout, O += Pd V ----
   const uint64_t seed = (p.p_drop > 0.f) ? load_seed(p.seed) : 0ull;
+  const uint64_t dkey = rng_key(seed, p.rng_stream);
   const float keep_scale = (p.p_drop > 0.f) ? 1.f / (1.f - p.p_drop) : 1.f;
   f32x4 oacc[NU];
 #pragma unroll
   for (int u = 0; u < NU; ++u) oacc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int64_t prow0 = (bh * p.T + ib) * p.T;  // P row of (ib, j = 0)
-  for (int kb = 0; kb < (T + AKB - 1) / AKB; ++kb) {
+  // per owned row: flat index of its (i, j = 0) element (dropout counter, p~ offset) and whether i < T
+  int64_t prow[4];
+  bool rowin[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    prow[r] = prow0 + (int64_t)r * p.T;
+    rowin[r] = ib + r < T;
+  }
+  const bool drop = p.p_drop > 0.f;
+  KPROBE(1);
+  // single pass: only the key blocks with a valid key (the p~ zeros of the first block past them are
+  // written after the loop), and the next stage is always loaded (the last block reloads itself), so
+  // every iteration issues the same loads and stores
+  for (int kb = 0; kb < (TWO_PASS ? nkb_all : nkb); ++kb) {
     const int j0 = kb * AKB;
-    const bool live = kb < nkb;
+    const bool live = TWO_PASS ? kb < nkb : true;
     if (live) {
       __syncthreads();
       store_stage(true);
       __syncthreads();
-      if (kb + 1 < nkb) load_stage(j0 + AKB, true);
+      if (TWO_PASS) {
+        if (kb + 1 < nkb) load_stage(j0 + AKB, true);
+      } else {
+        load_stage(kb + 1 < nkb ? j0 + AKB : j0, true);
+      }
     }
+    KPROBE(2 + 4 * kb);
     float s[4][4];
     if (live) {
       scores(j0, s);
@@ -286,12 +359,14 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void relpos_attn_fwd_kernel(A
         for (int u = 0; u < NU; ++u) oacc[u][r] *= corr;
       }
     }
-    if (!TWO_PASS && live && p.mblk && (lane & 15) == 0) {   // the running max this block's p~ is relative to
-      const int nkb_all = (T + AKB - 1) / AKB;
+    if (WPT && live) {   // the running max this block's p~ is relative to (the 16 lanes of a row hold the same)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        if (ib + r < T) p.mblk[(bh * p.T + ib + r) * nkb_all + kb] = mrow[r];
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, mrow[r]), rmb,
+                                              rowin[r] ? (uint32_t)(((bh * p.T + ib + r) * nkb_all + kb) * 4) : OOB,
+                                              0, 0);
     }
+    KPROBE(3 + 4 * kb);
     uint16_t* Pw = Ps[w];
 #pragma unroll
     for (int t = 0; t < 4; ++t)
@@ -300,12 +375,12 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void relpos_attn_fwd_kernel(A
         const int ii = 4 * (lane >> 4) + r, jj = 16 * t + (lane & 15);
         const int i = ib + r, j = j0 + jj;
         float pv = (s[t][r] > -1.0e38f) ? __expf(s[t][r] - mrow[r]) * inv[r] : 0.f;
-        if (!TWO_PASS && p.pt && i < T && j < T) p.pt[prow0 + (int64_t)r * p.T + j] = f2bf(pv);
+        if (WPT)
+          __builtin_amdgcn_raw_buffer_store_b16(f2bf(pv), rpt, (rowin[r] && j < T) ? (uint32_t)((prow[r] + j) * 2) : OOB,
+                                                0, 0);
         float pdv = pv;
-        if (p.p_drop > 0.f && pv != 0.f) {
-          const uint64_t idx = (uint64_t)(prow0 + (int64_t)r * p.T) + (uint64_t)j;
-          pdv = dropout_keep(seed, p.rng_stream, idx, p.p_drop) ? pv * keep_scale : 0.f;
-        }
+        if (drop)   // (a zero probability stays zero either way: no per-element branch on it)
+          pdv = dropout_keep_k(dkey, (uint64_t)(prow[r] + j), p.p_drop) ? pv * keep_scale : 0.f;
         if (TWO_PASS && i < T && j < T) {
           const int64_t off = prow0 + (int64_t)r * p.T + j;
           if (p.P) p.P[off] = pv;
@@ -317,6 +392,7 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void relpos_attn_fwd_kernel(A
       if (!TWO_PASS) break;  // nothing to write: no P outputs in single-pass mode
       continue;              // P row tail beyond len is written as zeros; no O contribution
     }
+    KPROBE(4 + 4 * kb);
     wave_lds_sync();
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
@@ -328,7 +404,19 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void relpos_attn_fwd_kernel(A
       }
     }
     wave_lds_sync();  // Ps is rewritten by the next block
+    KPROBE(5 + 4 * kb);
   }
+  if (WPT && nkb < nkb_all) {   // p~ of the first key block past the valid keys: zeros
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int j = nkb * AKB + 16 * t + (lane & 15);
+        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)0, rpt,
+                                              (rowin[r] && j < T) ? (uint32_t)((prow[r] + j) * 2) : OOB, 0, 0);
+      }
+  }
+  KPROBE(30);
 
   // ---- per-row log-sum-exp for the backward's recompute (single pass; +inf-like sentinel for rows
   // with no valid key: their P row is zero) ----
@@ -350,6 +438,7 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void relpos_attn_fwd_kernel(A
       const int i = ib + r, c = 16 * u + (lane & 15);
       if (i < T && c < dk) p.o[(b * p.T + i) * p.ldq + hoff + c] = oacc[u][r] * fin[r];
     }
+  KPROBE(31);
 }
 
 }  // namespace
@@ -378,7 +467,12 @@ extern "C" int kdfm_relpos_attn_fwd(const float* qu, const float* qv, const floa
   p.scale = scale; p.p_drop = dropout_p; p.seed = seed; p.rng_stream = rng_stream;
   dim3 grid((unsigned)ceil_div(T, AQ), (unsigned)(B * H));
   const bool two = P || Pdrop, wide = dk > 48;
-  if (two && !wide)
+  KDFM_REQUIRE(!p_tilde || B * H * T * T * 2 <= (int64_t)INT32_MAX, "p~ exceeds the 2 GB buffer-offset range");
+  if (!two && p_tilde && !wide)
+    hipLaunchKernelGGL((relpos_attn_fwd_kernel<false, 3, true>), grid, dim3(256), 0, as_stream(stream), p);
+  else if (!two && p_tilde)
+    hipLaunchKernelGGL((relpos_attn_fwd_kernel<false, 4, true>), grid, dim3(256), 0, as_stream(stream), p);
+  else if (two && !wide)
     hipLaunchKernelGGL((relpos_attn_fwd_kernel<true, 3>), grid, dim3(256), 0, as_stream(stream), p);
   else if (two)
     hipLaunchKernelGGL((relpos_attn_fwd_kernel<true, 4>), grid, dim3(256), 0, as_stream(stream), p);

@@ -324,6 +324,9 @@ __global__ __launch_bounds__(bwd_nt<DT>()) void ffn_bwd_kernel(FfnBwd a) {
   using DS = DmaStager<G::BWD, 2 * DT, G::CS, NP, NT>;
   const uint4* img = reinterpret_cast<const uint4*>(a.img);
   DS::issue(img, 0, FC, ff_lds, 0);
+  const int side_bytes = (int)(a.rows * ff * 2);
+  const __amdgpu_buffer_rsrc_t r_a = __builtin_amdgcn_make_buffer_rsrc((void*)a.a_h, (short)0, side_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t r_dh = __builtin_amdgcn_make_buffer_rsrc((void*)a.dh_h, (short)0, side_bytes, 0x00020000);
 
   // dl2 = rscale * drop_out(dout): B operands of dA^T; the even wave writes the bf16 copy (dW2 operand)
   bf16x8 bd[KS1];
@@ -411,13 +414,14 @@ __global__ __launch_bounds__(bwd_nt<DT>()) void ffn_bwd_kernel(FfnBwd a) {
       bf16x8 ba[2], bdh[2];
       tile_operands(pa, ba);
       tile_operands(pd, bdh);
-      if (ok && live) {
+      // the four bf16 side-output stores are issued by every lane (rows past the end / a parity past the
+      // last chunk carry an out-of-range offset the buffer range check drops): a fixed count behind the
+      // stage's DMA for the counted barrier below
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          const int64_t off = row * ff + c * 32 + s * 16 + 8 * h;
-          *reinterpret_cast<bf16x8*>(a.a_h + off) = ba[s];
-          *reinterpret_cast<bf16x8*>(a.dh_h + off) = bdh[s];
-        }
+      for (int s = 0; s < 2; ++s) {
+        const uint32_t off = (ok && live) ? (uint32_t)((row * ff + c * 32 + s * 16 + 8 * h) * 2) : 0x80000000u;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, ba[s]), r_a, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, bdh[s]), r_dh, off, 0, 0);
       }
 #pragma unroll
       for (int mt = 0; mt < DT; ++mt)
@@ -426,7 +430,7 @@ __global__ __launch_bounds__(bwd_nt<DT>()) void ffn_bwd_kernel(FfnBwd a) {
           acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf(W[(2 * KS1 + 2 * mt + s) * FRAG_U4 + lane]), bdh[s],
                                                             acc[mt], 0, 0, 0);
     }
-    __syncthreads();
+    dma_barrier<4>();   // stage it + 1 landed; this iteration's 4 side-output stores stay in flight
   }
   // partials of parities 1..NP-1 -> parity 0, added in the fixed order ((p0 + p1) + p2) + p3
   float* red = reinterpret_cast<float*>(ff_lds) + tile * ((NP - 1) * DT * 16 * 64);
@@ -555,6 +559,7 @@ int kdfm_ffn_bwd(const float* dout, const float* x, const float* mean, const flo
                "operands must be 16-byte aligned");
   KDFM_REQUIRE(p_act >= 0.f && p_act < 1.f && p_out >= 0.f && p_out < 1.f, "dropout p");
   KDFM_REQUIRE((p_act == 0.f && p_out == 0.f) || seed, "dropout needs a seed");
+  KDFM_REQUIRE(rows * ff * 2 <= (int64_t)INT32_MAX - 64, "rows x ff exceeds the 2 GB side-output buffer range");
   if (rows <= 0) return KDFM_OK;
   FfnBwd a{dout, x, mean, rstd, ln_g, ln_b, img, b1, dx, ln_h, a_h, dl2_h, dh_h, part, rows, ceil_div(rows, 16),
            (int)d, (int)ff, rscale, p_act, p_out, seed, stream_act, stream_out};

@@ -117,6 +117,19 @@ struct DmaStager {
   }
 };
 
+// Workgroup barrier that retires this wave's LDS-DMA stage and its LDS reads but leaves its N youngest
+// vector-memory operations -- the side-output stores issued after the stage's DMA -- in flight.  Loads,
+// stores and LDS-DMA retire in issue order on one counter (MI355X_MICROARCH.md 'vmcnt'), so vmcnt(N)
+// with the N stores issued after the DMA guarantees the DMA has landed; a __syncthreads() there waits
+// vmcnt(0) and drains the stores too.  Encoding (gfx9 s_waitcnt): vmcnt bits [3:0] + [15:14],
+// expcnt [6:4] (7 = no wait), lgkmcnt [11:8] (0).
+template <int N>
+__device__ __forceinline__ void dma_barrier() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4));
+  __builtin_amdgcn_s_barrier();
+}
+
 // Row r = `row` of x (d features, 16-B aligned rows) normalised into the B operands bx[ks]
 // (features 16 ks + 8 h .. +7; zero beyond d).  have_stats: mean / rstd given (backward recompute);
 // else computed (two-pass, biased variance, as kdfm_layernorm_fwd).  ln_out: bf16 copy of the row.
