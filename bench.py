@@ -22,6 +22,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "kd-via-fm-in-asr_amd"))
 sys.path.insert(0, ROOT)
 
+import kdfm  # noqa: E402,F401  (sets HIP_FORCE_DEV_KERNARG before the HIP runtime initialises)
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 

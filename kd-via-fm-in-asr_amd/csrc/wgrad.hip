@@ -22,6 +22,11 @@
 
 #include <cstdlib>
 
+// timing probe points (tools/wgrad_probe.hip defines KPROBE; empty in the library)
+#ifndef KPROBE
+#define KPROBE(i)
+#endif
+
 namespace kdfm {
 namespace {
 
@@ -58,6 +63,7 @@ __global__ __launch_bounds__(WR_NT, 2) void wgr_kernel(GemmP p, WrGeo g) {
   constexpr int CW = BIN == 2 ? 8 : 4;   // columns per staging unit
   constexpr int CWS = BIN == 2 ? 3 : 2;  // log2(CW)
   extern __shared__ __attribute__((aligned(16))) uint16_t wr_lds[];
+  KPROBE(0);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   // LDS images as element offsets into wr_lds (an array of pointers would decay to generic pointers
   // and turn every LDS access into a FLAT access that also waits on the global-load counter)
@@ -300,10 +306,12 @@ __global__ __launch_bounds__(WR_NT, 2) void wgr_kernel(GemmP p, WrGeo g) {
   } else {
     // two slabs in flight: slot 0 carries even steps, slot 1 odd steps (compile-time slots, so the
     // compiler waits only for the older slot's loads before staging it)
+    KPROBE(1);
     if (nsteps > 0) load(reg[0], msk[0], kb);
     if (nsteps > 1) load(reg[1], msk[1], kb + 32);
     if (nsteps > 0) stage(reg[0], msk[0], 0, kb);
     __syncthreads();
+    KPROBE(2);
     for (int64_t s = 0; s < nsteps; s += 2) {
       // even step s in buffer 0
       if (s + 2 < nsteps) load(reg[0], msk[0], kb + 32 * (s + 2));
@@ -316,8 +324,10 @@ __global__ __launch_bounds__(WR_NT, 2) void wgr_kernel(GemmP p, WrGeo g) {
       mfma_step(1);
       if (s + 2 < nsteps) stage(reg[0], msk[0], 0, kb + 32 * (s + 2));
       __syncthreads();
+      if (s < 40) KPROBE(3 + (int)(s >> 1));
     }
   }
+  KPROBE(29);
 
   // raw partial of this (split, slice) -> ws[split][m][n]
   float* wsp = p.ws + split * p.M * p.N;
@@ -331,6 +341,7 @@ __global__ __launch_bounds__(WR_NT, 2) void wgr_kernel(GemmP p, WrGeo g) {
         const int64_t n = n0 + (nb0 + j) * 16 + (lane & 15);
         if (ml < mcols && n < p.N && n < n0 + g.Nb) wsp[(m0 + ml) * p.N + n] = acc[i][j][r];
       }
+  KPROBE(31);
 }
 
 // C(m, n) += alpha * sum_{s<S} ws[s][m][n]   (n == ones_col -> ones_out[m]), deterministic: the block
@@ -339,6 +350,7 @@ __global__ __launch_bounds__(WR_NT, 2) void wgr_kernel(GemmP p, WrGeo g) {
 // latency-bound otherwise), then a fixed-order combine in LDS and one plain add per element.
 constexpr int WF_WAVES = 8;
 
+template <bool TRANS = false>   // TRANS: partials stored ws[s][n][m] (wgd_kernel)
 __global__ __launch_bounds__(64 * WF_WAVES) void wgr_fold_kernel(GemmP p, int64_t S) {
   __shared__ float red[WF_WAVES][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -362,7 +374,14 @@ __global__ __launch_bounds__(64 * WF_WAVES) void wgr_fold_kernel(GemmP p, int64_
 #pragma unroll
     for (int i = 0; i < WF_WAVES; ++i) v += red[i][lane];
     v *= p.alpha;
-    const int64_t m = e / p.N, n = e - m * p.N;
+    int64_t m, n;
+    if (TRANS) {
+      n = e / p.M;
+      m = e - n * p.M;
+    } else {
+      m = e / p.N;
+      n = e - m * p.N;
+    }
     if (p.ones_col >= 0 && n >= p.ones_col)   // bias column(s): segment j -> ones_out[j][m]
       p.ones_out[(n - p.ones_col) * p.M + m] += v;
     else
@@ -395,6 +414,15 @@ int env_i(const char* name, int dflt) {
   return e ? atoi(e) : dflt;
 }
 
+// geometry of wgd_kernel (bf16 operands streamed by LDS-DMA, below)
+struct WdGeo {
+  int wm, wn;            // wave grid
+  int Mt, Nt;            // 16-wide tiles of M and of X's memory columns
+  int64_t steps_per;     // 32-row slabs per split
+  int pa, pb, pw;        // 1 KB DMA pieces of a slab's dY / X image, DMA instructions per wave per slab
+  int aimg, slab;        // bf16 elements of the (1 KB padded) dY image and of one slab buffer
+};
+
 struct WrPlan {
   WrPick w;
   WrGeo g;
@@ -402,10 +430,16 @@ struct WrPlan {
   size_t lds;
   int upt;
   int bin;   // wgr_kernel BIN: 0 f32 operands, 1 / 2 bf16 operands in 4- / 8-column staging units
+  bool dma = false;   // wgd_kernel route
+  int ns = 0;         // wgd_kernel slab buffers
+  WdGeo wd{};
 };
+
+bool wd_plan(const GemmP& p, int bmode, WrPlan& pl);
 
 bool wr_plan(const GemmP& p, int amode, int bmode, int64_t batch, WrPlan& pl, bool force = false,
              bool bf16in = false) {
+  if (bf16in && force && batch == 1 && amode == KDFM_LD_XC && wd_plan(p, bmode, pl)) return true;
   static const int enabled = env_i("KDFM_WGR", 1);
   if (!enabled && !force) return false;
   if (batch != 1 || p.epi != KDFM_EPI_ATOMIC || amode != KDFM_LD_XC) return false;
@@ -534,10 +568,311 @@ int try_wgrad_rows(const GemmP& p, int amode, int bmode, int64_t batch, hipStrea
     }
   }
   if (rc) return rc;
-  hipLaunchKernelGGL(wgr_fold_kernel, dim3((unsigned)ceil_div(p.M * p.N, 64)), dim3(64 * WF_WAVES), 0, st, p, pl.S);
+  hipLaunchKernelGGL(wgr_fold_kernel<false>, dim3((unsigned)ceil_div(p.M * p.N, 64)), dim3(64 * WF_WAVES), 0, st, p, pl.S);
   return check_launch("kdfm_gemm(wgrad rows fold)");
 }
 
+}  // namespace kdfm
+
+namespace kdfm {
+namespace {
+
+// ---- bf16 weight gradient streamed by LDS-DMA -----------------------------------------------------
+// Dense bf16 operands dY (rows, M) and X (rows, N) (M, N multiples of 8; no conv taps, no segments):
+// every 32-row slab of dY and of X is one contiguous run of HBM, copied into LDS unchanged by
+// global_load_lds_dwordx4 (a wave-instruction moves 1 KB; no staging registers, no transpose pass),
+// and the MFMA fragments are read TRANSPOSED out of the row-major images with ds_read_b64_tr_b16
+// (dW = dY^T X: A = dY^T, B = X, both summing over the slab's rows).  A ring of NS slab buffers keeps
+// NS - 2 slabs in flight behind the one being multiplied: every wave issues exactly pw DMA
+// instructions per slab (pieces past the image repeat its last piece, slabs past the split's end
+// repeat its last slab), so the wait for slab s is the fixed count vmcnt(pw (NS - 2)).  Rows past
+// the split's end are loaded from a clamped address and zeroed in LDS before use.  The bias gradient
+// (column sums of dY) is one extra MFMA per output-row tile against an all-ones B operand.  Partials
+// go out transposed, ws[split][n][m] -- one 16-byte store per accumulator tile -- and
+// wgr_fold_kernel<true> adds them in split order (deterministic).
+constexpr int WD_NT = 512;
+
+__device__ __forceinline__ void vm_wait(int n) {   // s_waitcnt vmcnt(n) for a wave-uniform n < 64
+  switch (n) {
+    case 0: __builtin_amdgcn_s_waitcnt(3952); break;
+    case 1: __builtin_amdgcn_s_waitcnt(3953); break;
+    case 2: __builtin_amdgcn_s_waitcnt(3954); break;
+    case 3: __builtin_amdgcn_s_waitcnt(3955); break;
+    case 4: __builtin_amdgcn_s_waitcnt(3956); break;
+    case 5: __builtin_amdgcn_s_waitcnt(3957); break;
+    case 6: __builtin_amdgcn_s_waitcnt(3958); break;
+    case 7: __builtin_amdgcn_s_waitcnt(3959); break;
+    case 8: __builtin_amdgcn_s_waitcnt(3960); break;
+    case 9: __builtin_amdgcn_s_waitcnt(3961); break;
+    case 10: __builtin_amdgcn_s_waitcnt(3962); break;
+    case 11: __builtin_amdgcn_s_waitcnt(3963); break;
+    case 12: __builtin_amdgcn_s_waitcnt(3964); break;
+    case 13: __builtin_amdgcn_s_waitcnt(3965); break;
+    case 14: __builtin_amdgcn_s_waitcnt(3966); break;
+    case 15: __builtin_amdgcn_s_waitcnt(3967); break;
+    case 16: __builtin_amdgcn_s_waitcnt(20336); break;
+    case 17: __builtin_amdgcn_s_waitcnt(20337); break;
+    case 18: __builtin_amdgcn_s_waitcnt(20338); break;
+    case 19: __builtin_amdgcn_s_waitcnt(20339); break;
+    case 20: __builtin_amdgcn_s_waitcnt(20340); break;
+    case 21: __builtin_amdgcn_s_waitcnt(20341); break;
+    case 22: __builtin_amdgcn_s_waitcnt(20342); break;
+    case 23: __builtin_amdgcn_s_waitcnt(20343); break;
+    case 24: __builtin_amdgcn_s_waitcnt(20344); break;
+    case 25: __builtin_amdgcn_s_waitcnt(20345); break;
+    case 26: __builtin_amdgcn_s_waitcnt(20346); break;
+    case 27: __builtin_amdgcn_s_waitcnt(20347); break;
+    case 28: __builtin_amdgcn_s_waitcnt(20348); break;
+    case 29: __builtin_amdgcn_s_waitcnt(20349); break;
+    case 30: __builtin_amdgcn_s_waitcnt(20350); break;
+    case 31: __builtin_amdgcn_s_waitcnt(20351); break;
+    case 32: __builtin_amdgcn_s_waitcnt(36720); break;
+    case 33: __builtin_amdgcn_s_waitcnt(36721); break;
+    case 34: __builtin_amdgcn_s_waitcnt(36722); break;
+    case 35: __builtin_amdgcn_s_waitcnt(36723); break;
+    case 36: __builtin_amdgcn_s_waitcnt(36724); break;
+    case 37: __builtin_amdgcn_s_waitcnt(36725); break;
+    case 38: __builtin_amdgcn_s_waitcnt(36726); break;
+    case 39: __builtin_amdgcn_s_waitcnt(36727); break;
+    case 40: __builtin_amdgcn_s_waitcnt(36728); break;
+    case 41: __builtin_amdgcn_s_waitcnt(36729); break;
+    case 42: __builtin_amdgcn_s_waitcnt(36730); break;
+    case 43: __builtin_amdgcn_s_waitcnt(36731); break;
+    case 44: __builtin_amdgcn_s_waitcnt(36732); break;
+    case 45: __builtin_amdgcn_s_waitcnt(36733); break;
+    case 46: __builtin_amdgcn_s_waitcnt(36734); break;
+    case 47: __builtin_amdgcn_s_waitcnt(36735); break;
+    case 48: __builtin_amdgcn_s_waitcnt(53104); break;
+    case 49: __builtin_amdgcn_s_waitcnt(53105); break;
+    case 50: __builtin_amdgcn_s_waitcnt(53106); break;
+    case 51: __builtin_amdgcn_s_waitcnt(53107); break;
+    case 52: __builtin_amdgcn_s_waitcnt(53108); break;
+    case 53: __builtin_amdgcn_s_waitcnt(53109); break;
+    case 54: __builtin_amdgcn_s_waitcnt(53110); break;
+    case 55: __builtin_amdgcn_s_waitcnt(53111); break;
+    case 56: __builtin_amdgcn_s_waitcnt(53112); break;
+    case 57: __builtin_amdgcn_s_waitcnt(53113); break;
+    case 58: __builtin_amdgcn_s_waitcnt(53114); break;
+    case 59: __builtin_amdgcn_s_waitcnt(53115); break;
+    case 60: __builtin_amdgcn_s_waitcnt(53116); break;
+    case 61: __builtin_amdgcn_s_waitcnt(53117); break;
+    case 62: __builtin_amdgcn_s_waitcnt(53118); break;
+    case 63: __builtin_amdgcn_s_waitcnt(53119); break;
+    default: __builtin_amdgcn_s_waitcnt((7 << 4) | (15 << 8)); break;
+  }
+}
+
+typedef short wd_v4s __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) wd_v4s wd_lds_v4s;
+typedef __attribute__((address_space(3))) void wd_lds_void;
+typedef __attribute__((address_space(1))) void wd_gl_void;
+
+// lane l: X[8 (l >> 4) + e][n0 + (l & 15)], e = 0..7, of a row-major [32][ld] bf16 image (EXEC full).
+// The two ds_read_b64_tr_b16 are issued as inline asm: with LDS-DMA in flight the compiler drains it
+// (vmcnt(0)) before any LDS read it can see, which would empty the slab ring every iteration.  The
+// caller must retire them (wd_lds_wait) before using the fragment.
+__device__ __forceinline__ bf16x8 wd_tr_frag(const uint16_t* img, int ld, int n0, int lane) {
+  const int li = lane & 15;
+  const uint16_t* a = img + (8 * (lane >> 4) + (li >> 2)) * ld + n0 + 4 * (li & 3);
+  const uint32_t a0 = (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) uint16_t*)a);
+  wd_v4s lo, hi;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(a0));
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(hi) : "v"(a0 + 8u * (uint32_t)ld));
+  return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+// lgkmcnt(0) for the asm reads, tied to the fragments so no use of them is scheduled above it
+template <int MBW, int NBW>
+__device__ __forceinline__ void wd_lds_wait(bf16x8 (&af)[MBW], bf16x8 (&bf)[NBW]) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int i = 0; i < MBW; ++i) asm volatile("" : "+v"(af[i]));
+#pragma unroll
+  for (int j = 0; j < NBW; ++j) asm volatile("" : "+v"(bf[j]));
+}
+
+template <int MBW, int NBW, int NS>
+__global__ __launch_bounds__(WD_NT) void wgd_kernel(GemmP p, WdGeo g) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t wd_lds[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t kb = (int64_t)blockIdx.x * g.steps_per * 32;
+  int64_t ke = kb + g.steps_per * 32;
+  if (ke > p.K) ke = p.K;
+  if (p.k_dev) {
+    const int64_t kd = *p.k_dev;
+    if (ke > kd) ke = kd;
+  }
+  const int nsteps = ke > kb ? (int)((ke - kb + 31) / 32) : 0;
+  const int M = (int)p.M;
+  const int N = (int)(p.ones_col >= 0 ? p.ones_col : p.N);   // X's memory columns
+  const bool bias = p.ones_col >= 0;
+  const uint16_t* A = reinterpret_cast<const uint16_t*>(p.A);
+  const uint16_t* X = reinterpret_cast<const uint16_t*>(p.B);
+  const int npc = g.pa + g.pb;
+
+  // DMA of slab s (clamped to the last) into buffer s % NS: exactly g.pw instructions per wave
+  auto issue = [&](int s) {
+    const int sc = s < nsteps ? s : nsteps - 1;
+    const int64_t r0 = kb + 32 * (int64_t)sc;
+    const int64_t vr = ke - r0 < 32 ? ke - r0 : 32;   // valid rows of the slab
+    const int va = (int)(vr * M * 2), vb = (int)(vr * N * 2);
+    uint16_t* buf = wd_lds + (s % NS) * g.slab;
+    for (int i = 0; i < g.pw; ++i) {
+      int f = wave + 8 * i;
+      f = f < npc ? f : npc - 1;
+      const bool isa = f < g.pa;
+      const int fl = isa ? f : f - g.pa;
+      const int byte = 1024 * fl + 16 * lane;
+      const int valid = isa ? va : vb;
+      const int src_b = byte < valid ? byte : 0;   // clamped: the lane writes its (padded) slot anyway
+      const uint16_t* src = isa ? A + r0 * M + src_b / 2 : X + r0 * N + src_b / 2;
+      uint16_t* dst = buf + (isa ? 0 : g.aimg) + fl * 512;
+      __builtin_amdgcn_global_load_lds((wd_gl_void*)src, (wd_lds_void*)dst, 16, 0, 0);
+    }
+  };
+
+  const int wr_ = wave / g.wn, wc_ = wave - (wave / g.wn) * g.wn;
+  const int mb0 = wr_ * MBW, nb0 = wc_ * NBW;
+  f32x4 acc[MBW][NBW], accb[MBW];
+#pragma unroll
+  for (int i = 0; i < MBW; ++i) {
+    accb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < NBW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  bf16x8 ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = (short)0x3F80;   // bf16(1.0)
+  const bool do_bias = bias && wc_ == 0;
+
+  if (nsteps > 0) {
+    for (int s = 0; s < NS - 1; ++s) issue(s);
+    for (int s = 0; s < nsteps; ++s) {
+      vm_wait(g.pw * (NS - 2));                         // slab s has landed (this wave's part)
+      __builtin_amdgcn_s_waitcnt((0xF) | (3 << 14) | (7 << 4));   // lgkmcnt(0): reads of slab s - 1 done
+      __builtin_amdgcn_s_barrier();
+      const uint16_t* buf = wd_lds + (s % NS) * g.slab;
+      const int64_t r0 = kb + 32 * (int64_t)s;
+      if (ke - r0 < 32) {   // tail slab: zero its rows past the end (both images), then re-sync
+        const int vr = (int)(ke - r0);
+        uint16_t* wb = wd_lds + (s % NS) * g.slab;
+        for (int e = threadIdx.x; e < (32 - vr) * (M + N); e += WD_NT) {
+          const int ea = (32 - vr) * M;
+          if (e < ea) wb[vr * M + e] = 0;
+          else wb[g.aimg + vr * N + (e - ea)] = 0;
+        }
+        __syncthreads();
+      }
+      bf16x8 af[MBW], bfr[NBW];
+#pragma unroll
+      for (int i = 0; i < MBW; ++i) {
+        const int mt = mb0 + i < g.Mt ? mb0 + i : g.Mt - 1;
+        af[i] = wd_tr_frag(buf, M, 16 * mt, lane);
+      }
+#pragma unroll
+      for (int j = 0; j < NBW; ++j) {
+        const int nt = nb0 + j < g.Nt ? nb0 + j : g.Nt - 1;
+        bfr[j] = wd_tr_frag(buf + g.aimg, N, 16 * nt, lane);
+      }
+      issue(s + NS - 1);   // into the buffer of slab s - 1, which every wave has finished reading
+      wd_lds_wait<MBW, NBW>(af, bfr);
+#pragma unroll
+      for (int i = 0; i < MBW; ++i) {
+#pragma unroll
+        for (int j = 0; j < NBW; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        if (do_bias) accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], ones, accb[i], 0, 0, 0);
+      }
+    }
+    vm_wait(0);   // no LDS-DMA may outlive the workgroup's LDS allocation
+  }
+
+  // raw partial of this split, transposed: ws[split][n][m] (n = N: the bias column)
+  const int64_t MN = p.M * p.N;
+  float* wsp = p.ws + (int64_t)blockIdx.x * MN;
+#pragma unroll
+  for (int i = 0; i < MBW; ++i) {
+    const int m = 16 * (mb0 + i) + 4 * (lane >> 4);
+    const bool mok = mb0 + i < g.Mt && m < M;
+#pragma unroll
+    for (int j = 0; j < NBW; ++j) {
+      const int n = 16 * (nb0 + j) + (lane & 15);
+      if (mok && nb0 + j < g.Nt && n < N)
+        *reinterpret_cast<f32x4*>(wsp + (int64_t)n * M + m) = acc[i][j];
+    }
+    if (do_bias && mok && (lane & 15) == 0) *reinterpret_cast<f32x4*>(wsp + (int64_t)N * M + m) = accb[i];
+  }
+}
+
+template <int MBW, int NBW>
+int wd_launch(const GemmP& p, const WrPlan& pl, hipStream_t st) {
+  auto go = [&](auto kern) {
+    static bool once = [&] {
+      return hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) ==
+             hipSuccess;
+    }();
+    (void)once;
+    hipLaunchKernelGGL(kern, dim3((unsigned)pl.S), dim3(WD_NT), pl.lds, st, p, pl.wd);
+  };
+  if (pl.ns == 8) go(wgd_kernel<MBW, NBW, 8>);
+  else go(wgd_kernel<MBW, NBW, 4>);
+  return check_launch("kdfm_wgrad_bf16(dma)");
+}
+
+int wd_dispatch(const GemmP& p, const WrPlan& pl, hipStream_t st) {
+  switch (pl.w.mbw * 10 + pl.w.nbw) {
+    case 32: return wd_launch<3, 2>(p, pl, st);
+    case 33: return wd_launch<3, 3>(p, pl, st);
+    case 34: return wd_launch<3, 4>(p, pl, st);
+    case 36: return wd_launch<3, 6>(p, pl, st);
+    default: return wd_launch<6, 3>(p, pl, st);
+  }
+}
+
+// the wgd route: dense bf16 operands, no conv taps / segments, one column slice, slabs that fit 4 or 8
+// buffers in LDS, and long reductions (>= KDFM_WGD_MIN_ROWS rows, default 65,536: the KD heads' stacked
+// rows).  LDS-DMA moves ~25-90 GB/s per CU, so a short product (the 12,832-row Conformer layers) spread
+// over 31 workgroups took longer than the register-staged kernel over 81 (FFN W1 29 vs 23 us,
+// profiles/r03/r3t_wgrad_probe_*.log) while the 1.64M-row FM dW2 over 256 went 228 -> 201 us.
+// S: splits of >= KDFM_WGD_STEPS (12) slabs each, at most 256 (one per CU)
+bool wd_plan(const GemmP& p, int bmode, WrPlan& pl) {
+  static const int on = env_i("KDFM_WGD", 1);
+  static const int min_steps = env_i("KDFM_WGD_STEPS", 12);
+  static const int64_t min_rows = env_i("KDFM_WGD_MIN_ROWS", 65536);
+  if (!on || bmode != KDFM_LD_XC || p.nseg > 1 || p.epi != KDFM_EPI_ATOMIC || p.K < min_rows) return false;
+  const int64_t nmem = p.ones_col >= 0 ? p.ones_col : p.N;
+  if (p.ones_col >= 0 && p.ones_col != p.N - 1) return false;
+  if (p.M % 8 || nmem % 8 || p.sAm != 1 || p.sBn != 1 || p.sAk != p.M || p.sBk != nmem) return false;
+  if ((((uintptr_t)p.A) | ((uintptr_t)p.B)) & 15) return false;
+  if (p.K * (p.M > nmem ? p.M : nmem) * 2 > (int64_t)INT32_MAX * 64) return false;
+  const int64_t Mt = ceil_div(p.M, 16), Nt = ceil_div(nmem, 16);
+  if (Nt > 24 || !wr_pick(p.M, nmem, pl.w)) return false;
+  WdGeo& g = pl.wd;
+  g.wm = pl.w.wm;
+  g.wn = pl.w.wn;
+  g.Mt = (int)Mt;
+  g.Nt = (int)Nt;
+  g.pa = (int)ceil_div(64 * p.M, 1024);
+  g.pb = (int)ceil_div(64 * nmem, 1024);
+  g.pw = (int)ceil_div(g.pa + g.pb, WD_NT / 64);
+  g.aimg = g.pa * 512;
+  g.slab = (g.pa + g.pb) * 512;
+  const size_t slab_bytes = (size_t)g.slab * 2;
+  pl.ns = slab_bytes * 8 + 64 <= 150 * 1024 ? 8 : (slab_bytes * 4 + 64 <= 150 * 1024 ? 4 : 0);
+  if (!pl.ns || g.pw * (pl.ns - 2) > 63) return false;
+  pl.lds = slab_bytes * pl.ns + 64;   // + the last buffer's transposed-read overreach
+  const int64_t steps = ceil_div(p.K, 32);
+  int64_t S = steps / min_steps;
+  if (S > 256) S = 256;
+  if (S < 1) S = 1;
+  g.steps_per = ceil_div(steps, S);
+  pl.S = ceil_div(steps, g.steps_per);
+  pl.slices = pl.mslices = 1;
+  pl.upt = 1;
+  pl.bin = 2;
+  pl.dma = true;
+  return true;
+}
+
+}  // namespace
 }  // namespace kdfm
 
 // ---- bf16-operand weight gradient (the fused KD-head chains' saved operands) ---------------------
@@ -604,9 +939,16 @@ int wgrad_bf16_run(const GemmP& p, int bmode, hipStream_t st) {
   KDFM_REQUIRE(wr_plan(p, KDFM_LD_XC, bmode, 1, pl, true, true), "shape not supported by the row-parallel kernel");
   KDFM_REQUIRE(p.ws_len >= pl.S * p.M * p.N, "workspace too small (kdfm_wgrad_bf16*_ws)");
   set_route(ROUTE_WGRAD_ROWS);
+  if (pl.dma) {
+    const int rc = wd_dispatch(p, pl, st);
+    if (rc) return rc;
+    hipLaunchKernelGGL(wgr_fold_kernel<true>, dim3((unsigned)ceil_div(p.M * p.N, 64)), dim3(64 * WF_WAVES), 0, st, p,
+                       pl.S);
+    return check_launch("kdfm_wgrad_bf16(fold)");
+  }
   const int rc = pl.bin == 2 ? wr_dispatch<2>(p, pl, bmode, st) : wr_dispatch<1>(p, pl, bmode, st);
   if (rc) return rc;
-  hipLaunchKernelGGL(wgr_fold_kernel, dim3((unsigned)ceil_div(p.M * p.N, 64)), dim3(64 * WF_WAVES), 0, st, p, pl.S);
+  hipLaunchKernelGGL(wgr_fold_kernel<false>, dim3((unsigned)ceil_div(p.M * p.N, 64)), dim3(64 * WF_WAVES), 0, st, p, pl.S);
   return check_launch("kdfm_wgrad_bf16(fold)");
 }
 }  // namespace
