@@ -35,15 +35,16 @@ MI355X_F32_MFMA_TFLOPS = 157.3
 MI355X_HBM_GBPS = 8000.0            # MI355X_MICROARCH.md §HBM (8 TB/s spec peak)
 # PMC traffic per kernel (tools/pmc_traffic.sh -> tools/pmc_summary.py: separate --pmc FETCH_SIZE and
 # WRITE_SIZE passes, FETCH_SIZE doubled per the gfx950 correction), committed under profiles/
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r02_pmc_traffic.json")
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r03_pmc_traffic.json")
 # kdfm_gemm kernel family (kernels.ROUTES) -> kernel-name stems in the rocprofv3 / PMC summaries
 ROUTE_KERNELS = {"generic": ("gemm_kernel",), "skinny": ("sk_fwd_kernel", "skd_fwd_kernel"),
                  "rowstream_fwd": ("rs_fwd_kernel",), "wide_wgrad": ("rs_wgrad_kernel", "rs_fold_kernel"),
                  "split_fold": ("gemm_kernel", "rs_fold_kernel"), "slab_conv": ("skc_fwd_kernel",),
-                 "wgrad_rows": ("wgr_kernel", "wgr_fold_kernel")}
+                 "wgrad_rows": ("wgr_kernel", "wgd_kernel", "wgr_fold_kernel")}
 # the fused kernels traced outside kdfm_gemm (kernels._traced tags) -> kernel-name stems
 FAMILY_KERNELS = {"ffn_fwd": ("ffn_fwd_kernel",), "ffn_bwd": ("ffn_bwd_kernel",),
-                  "wgrad_bf16": ("wgr_kernel", "wgr_fold_kernel"), "attn_fwd": ("relpos_attn_fwd_kernel",),
+                  "wgrad_bf16": ("wgr_kernel", "wgd_kernel", "wgr_fold_kernel"),
+                  "attn_fwd": ("relpos_attn_fwd_kernel",),
                   "attn_bwd": ("attn_bwd_dq_kernel", "attn_bwd_dkv_kernel", "attn_bwd_dpos_kernel",
                                "attn_rowdot_kernel", "attn_dpos_fold_kernel")}
 # FLOPs per utterance of one training step (B=32, 16.0 s) and of its attention +
