@@ -128,21 +128,17 @@ __global__ __launch_bounds__(fwd_nt<DT>()) void ffn_fwd_kernel(FfnFwd a) {
   const uint4* img = reinterpret_cast<const uint4*>(a.img);
   DS::issue(img, 0, FC, ff_lds, 0);
 
-  float mean = 0.f, rstd = 0.f;
-  bf16x8 bx[KS1];
-  ln_operands<KS1>(a.x, a.g, a.b, row, ok, d, h, a.eps, false, mean, rstd, bx, nullptr);
-  if (a.mean && par == 0 && h == 0 && ok) {
-    a.mean[row] = mean;
-    a.rstd[row] = rstd;
-  }
+  // prologue: the row loads, the bias / gamma / beta table fill and the stage-0 DMA are all in flight
+  // together; one barrier; then the LayerNorm from registers and the LDS table
+  float xv[KS1][8];
+  ln_load<KS1>(a.x, row, ok, d, h, xv);
+  float* bias_s = reinterpret_cast<float*>(reinterpret_cast<char*>(ff_lds) + ffn_fwd_stage_bytes<G::FWD, DT>());
+  fill_vec5<7 * 32 * DT, FWD_NT>(bias_s, a.b1, ff, a.b2, d, a.g, d, a.b, d, a.b, 0);   // ff = 4 d <= 4 * 32 DT
   f32x16 acc[DT];
 #pragma unroll
   for (int mt = 0; mt < DT; ++mt)
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[mt][i] = 0.f;
-
-  float* bias_s = reinterpret_cast<float*>(reinterpret_cast<char*>(ff_lds) + ffn_fwd_stage_bytes<G::FWD, DT>());
-  for (int e = threadIdx.x; e < ff + d; e += FWD_NT) bias_s[e] = e < ff ? a.b1[e] : a.b2[e - ff];
   // the residual rows in the accumulator layout for the epilogue, fetched now so their latency hides
   // behind the chunk loop (narrow d only: 4 DT float4 registers)
   constexpr bool XPRE = DT <= 3 && FWD_NP == 2;
@@ -158,8 +154,22 @@ __global__ __launch_bounds__(fwd_nt<DT>()) void ffn_fwd_kernel(FfnFwd a) {
       }
   }
   FFN_PROBE(1);
-  __syncthreads();
+  __syncthreads();   // stage 0 landed, the tables written
   FFN_PROBE(2);
+  float mean = 0.f, rstd = 0.f;
+  bf16x8 bx[KS1];
+  ln_finish<KS1>(xv, bias_s + ff + d, bias_s + ff + 2 * d, row, ok, d, h, a.eps, false, mean, rstd, bx, nullptr);
+  // the row statistics as 2 buffer stores every lane issues (the lanes that own no statistic write past
+  // the buffer, dropped)
+  {
+    const bool own = a.mean != nullptr && par == 0 && h == 0 && ok;
+    const int nb = a.mean ? (int)(a.rows * 4) : 0;
+    const __amdgpu_buffer_rsrc_t rm = __builtin_amdgcn_make_buffer_rsrc((void*)a.mean, (short)0, nb, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc((void*)a.rstd, (short)0, nb, 0x00020000);
+    const uint32_t off = own ? (uint32_t)(row * 4) : 0x80000000u;
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, mean), rm, off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, rstd), rr, off, 0, 0);
+  }
   const int nit = (FC + FWD_NP - 1) / FWD_NP;
   for (int it = 0; it < nit; ++it) {
     // no branch around the chunk (a conditional MFMA block makes the compiler carry acc through the
@@ -328,6 +338,13 @@ __global__ __launch_bounds__(bwd_nt<DT>()) void ffn_bwd_kernel(FfnBwd a) {
   const __amdgpu_buffer_rsrc_t r_a = __builtin_amdgcn_make_buffer_rsrc((void*)a.a_h, (short)0, side_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t r_dh = __builtin_amdgcn_make_buffer_rsrc((void*)a.dh_h, (short)0, side_bytes, 0x00020000);
 
+  // prologue loads first (row statistics, x rows, the bias / gamma / beta table, dout below): every load
+  // is issued before the prologue's stores, so waiting for a load never waits for a store
+  float mean = ok ? a.mean[row] : 0.f, rstd = ok ? a.rstd[row] : 0.f;
+  float xv[KS1][8];
+  ln_load<KS1>(a.x, row, ok, d, h, xv);
+  float* bias_s = reinterpret_cast<float*>(reinterpret_cast<char*>(ff_lds) + ffn_stage_bytes<G::BWD, DT>());
+  fill_vec5<6 * 32 * DT, NT>(bias_s, a.b1, ff, a.g, d, a.b, d, a.b, 0, a.b, 0);
   // dl2 = rscale * drop_out(dout): B operands of dA^T; the even wave writes the bf16 copy (dW2 operand)
   bf16x8 bd[KS1];
 #pragma unroll
@@ -348,11 +365,25 @@ __global__ __launch_bounds__(bwd_nt<DT>()) void ffn_bwd_kernel(FfnBwd a) {
       v[j] = t;
     }
     bd[ks] = pack_bf16x8<bf16x8>(v);
-    if (par == 0 && in) *reinterpret_cast<bf16x8*>(a.dl2_h + row * d + k0) = bd[ks];
   }
-  float mean = ok ? a.mean[row] : 0.f, rstd = ok ? a.rstd[row] : 0.f;
+  __syncthreads();   // stage 0 landed, the tables written
   bf16x8 bx[KS1];
-  ln_operands<KS1>(a.x, a.g, a.b, row, ok, d, h, 0.f, true, mean, rstd, bx, par == 0 ? a.ln_h : nullptr);
+  ln_finish<KS1>(xv, bias_s + ff, bias_s + ff + d, row, ok, d, h, 0.f, true, mean, rstd, bx, nullptr);
+  // the bf16 copies of dl2 and LN(x) (weight-gradient operands): 2 KS1 buffer stores every lane issues
+  // (other parities / rows past the end / features past d write past the buffer, dropped) -- a fixed
+  // count for the counted barrier
+  {
+    const int rb = (int)(a.rows * d * 2);
+    const __amdgpu_buffer_rsrc_t r_l2 = __builtin_amdgcn_make_buffer_rsrc((void*)a.dl2_h, (short)0, rb, 0x00020000);
+    const __amdgpu_buffer_rsrc_t r_ln = __builtin_amdgcn_make_buffer_rsrc((void*)a.ln_h, (short)0, rb, 0x00020000);
+#pragma unroll
+    for (int ks = 0; ks < KS1; ++ks) {
+      const int k0 = ks * 16 + 8 * h;
+      const uint32_t off = (par == 0 && ok && k0 < d) ? (uint32_t)((row * d + k0) * 2) : 0x80000000u;
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, bd[ks]), r_l2, off, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, bx[ks]), r_ln, off, 0, 0);
+    }
+  }
 
   f32x16 acc[DT];
 #pragma unroll
@@ -360,9 +391,7 @@ __global__ __launch_bounds__(bwd_nt<DT>()) void ffn_bwd_kernel(FfnBwd a) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[mt][i] = 0.f;
 
-  float* bias_s = reinterpret_cast<float*>(reinterpret_cast<char*>(ff_lds) + ffn_stage_bytes<G::BWD, DT>());
-  for (int e = threadIdx.x; e < ff; e += NT) bias_s[e] = a.b1[e];
-  __syncthreads();
+
   const int nit = (FC + NP - 1) / NP;
   for (int it = 0; it < nit; ++it) {
     // branch-free chunk (as the forward): a parity past the last chunk adds an all-zero dh operand
@@ -470,7 +499,7 @@ int launch_fwd(const FfnFwd& a, hipStream_t st) {
   using G = FfnGeo<KS1, DT>;
   static bool once = (ffn_allow_lds(ffn_fwd_kernel<KS1, DT>), true);
   (void)once;
-  const size_t lds = (size_t)ffn_fwd_stage_bytes<G::FWD, DT>() + (size_t)(a.ff + a.d) * 4;
+  const size_t lds = (size_t)ffn_fwd_stage_bytes<G::FWD, DT>() + (size_t)(a.ff + 3 * a.d) * 4;
   if (lds > 160 * 1024) { set_error("kdfm_ffn_fwd: hidden width too large for the LDS bias table"); return KDFM_EINVAL; }
   hipLaunchKernelGGL((ffn_fwd_kernel<KS1, DT>), dim3((unsigned)ceil_div(a.rows, FF_ROWS)), dim3(fwd_nt<DT>()), lds, st, a);
   return check_launch("kdfm_ffn_fwd");
@@ -481,7 +510,7 @@ int launch_bwd(const FfnBwd& a, hipStream_t st) {
   using G = FfnGeo<KS1, DT>;
   static bool once = (ffn_allow_lds(ffn_bwd_kernel<KS1, DT>), true);
   (void)once;
-  const size_t lds = (size_t)ffn_stage_bytes<G::BWD, DT>() + (size_t)a.ff * 4;
+  const size_t lds = (size_t)ffn_stage_bytes<G::BWD, DT>() + (size_t)(a.ff + 2 * a.d) * 4;
   hipLaunchKernelGGL((ffn_bwd_kernel<KS1, DT>), dim3((unsigned)ceil_div(a.rows, FF_ROWS)), dim3(bwd_nt<DT>()), lds, st,
                      a);
   return check_launch("kdfm_ffn_bwd");
@@ -494,7 +523,7 @@ extern "C" {
 
 int32_t kdfm_ffn_supported(int64_t d, int64_t ff) {
   int KS1, DT;
-  return kdfm::ffn_dims(d, KS1, DT) == 0 && ff > 0 && ff % 32 == 0 ? 1 : 0;
+  return kdfm::ffn_dims(d, KS1, DT) == 0 && ff > 0 && ff % 32 == 0 && ff <= 128 * DT ? 1 : 0;
 }
 
 int64_t kdfm_ffn_img_elems(int64_t d, int64_t ff) {
@@ -508,7 +537,7 @@ int kdfm_ffn_wprep(const float* W1, const float* W2, uint16_t* img, int64_t d, i
   using namespace kdfm;
   KDFM_REQUIRE(W1 && W2 && img, "null pointer");
   int KS1, DT;
-  KDFM_REQUIRE(ffn_dims(d, KS1, DT) == 0 && ff > 0 && ff % 32 == 0, "unsupported FFN shape (d, ff)");
+  KDFM_REQUIRE(ffn_dims(d, KS1, DT) == 0 && ff > 0 && ff % 32 == 0 && ff <= 128 * DT, "unsupported FFN shape (d, ff)");
   KDFM_REQUIRE(al16(img), "img must be 16-byte aligned");
   const int CS = 4 * DT + 2 * KS1;
   const int nfr = fwd_only ? 2 * DT + KS1 : CS;
@@ -527,7 +556,7 @@ int kdfm_ffn_fwd(const float* x, const float* ln_g, const float* ln_b, float ln_
   KDFM_REQUIRE(x && ln_g && ln_b && img && b1 && b2 && out, "null pointer");
   KDFM_REQUIRE((mean == nullptr) == (rstd == nullptr), "mean and rstd go together");
   int KS1, DT;
-  KDFM_REQUIRE(ffn_dims(d, KS1, DT) == 0 && ff > 0 && ff % 32 == 0, "unsupported FFN shape (d, ff)");
+  KDFM_REQUIRE(ffn_dims(d, KS1, DT) == 0 && ff > 0 && ff % 32 == 0 && ff <= 128 * DT, "unsupported FFN shape (d, ff)");
   KDFM_REQUIRE(al16(x) && al16(out) && al16(ln_g) && al16(ln_b) && al16(b1) && al16(b2) && al16(img),
                "operands must be 16-byte aligned");
   KDFM_REQUIRE(p_act >= 0.f && p_act < 1.f && p_out >= 0.f && p_out < 1.f, "dropout p");
@@ -553,7 +582,7 @@ int kdfm_ffn_bwd(const float* dout, const float* x, const float* mean, const flo
   KDFM_REQUIRE(dout && x && mean && rstd && ln_g && ln_b && img && b1 && dx && ln_h && a_h && dl2_h && dh_h && part,
                "null pointer");
   int KS1, DT;
-  KDFM_REQUIRE(ffn_dims(d, KS1, DT) == 0 && ff > 0 && ff % 32 == 0, "unsupported FFN shape (d, ff)");
+  KDFM_REQUIRE(ffn_dims(d, KS1, DT) == 0 && ff > 0 && ff % 32 == 0 && ff <= 128 * DT, "unsupported FFN shape (d, ff)");
   KDFM_REQUIRE(al16(dout) && al16(x) && al16(dx) && al16(ln_g) && al16(ln_b) && al16(b1) && al16(img) &&
                    al16(ln_h) && al16(a_h) && al16(dl2_h) && al16(dh_h),
                "operands must be 16-byte aligned");

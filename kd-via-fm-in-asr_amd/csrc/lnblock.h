@@ -130,24 +130,81 @@ __device__ __forceinline__ void dma_barrier() {
   __builtin_amdgcn_s_barrier();
 }
 
-// Row r = `row` of x (d features, 16-B aligned rows) normalised into the B operands bx[ks]
-// (features 16 ks + 8 h .. +7; zero beyond d).  have_stats: mean / rstd given (backward recompute);
-// else computed (two-pass, biased variance, as kdfm_layernorm_fwd).  ln_out: bf16 copy of the row.
+// dst[0, na) = a[0, na), dst[na, na + nb) = b[0, nb) in LDS (bias tables): every thread issues all of
+// its (at most MAXE) loads at clamped addresses first and writes LDS afterwards -- a fill loop with a
+// load per iteration waits for each load in turn (vmcnt(0) per element)
+template <int MAXE, int NT>
+__device__ __forceinline__ void fill_vec3(float* dst, const float* __restrict__ a, int na, const float* __restrict__ b,
+                                          int nb, const float* __restrict__ c, int nc) {
+  constexpr int PER = (MAXE + NT - 1) / NT;
+  float v[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int e = (int)threadIdx.x + i * NT;
+    const float* src = e < na ? a + e : (e < na + nb ? b + (e - na) : (e < na + nb + nc ? c + (e - na - nb) : a));
+    v[i] = *src;
+  }
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int e = (int)threadIdx.x + i * NT;
+    if (e < na + nb + nc) dst[e] = v[i];
+  }
+}
+template <int MAXE, int NT>
+__device__ __forceinline__ void fill_vec2(float* dst, const float* __restrict__ a, int na, const float* __restrict__ b,
+                                          int nb) {
+  fill_vec3<MAXE, NT>(dst, a, na, b, nb, a, 0);
+}
+// five sources (bias tables followed by the LayerNorm gamma / beta)
+template <int MAXE, int NT>
+__device__ __forceinline__ void fill_vec5(float* dst, const float* a, int na, const float* b, int nb, const float* c,
+                                          int nc, const float* e4, int n4, const float* e5, int n5) {
+  constexpr int PER = (MAXE + NT - 1) / NT;
+  const int o1 = na, o2 = na + nb, o3 = o2 + nc, o4 = o3 + n4, o5 = o4 + n5;
+  float v[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int e = (int)threadIdx.x + i * NT;
+    const float* src = e < o1 ? a + e
+                     : e < o2 ? b + (e - o1)
+                     : e < o3 ? c + (e - o2)
+                     : e < o4 ? e4 + (e - o3)
+                     : e < o5 ? e5 + (e - o4) : a;
+    v[i] = *src;
+  }
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int e = (int)threadIdx.x + i * NT;
+    if (e < o5) dst[e] = v[i];
+  }
+}
+
+// LayerNorm operands in two parts so the row loads can be issued before a barrier and the statistics /
+// normalisation computed after it (gamma / beta then read from an LDS table).  Out-of-range elements are
+// loaded from a clamped valid address and zeroed by a 0 / 1 multiply, not a select: with
+// `in ? f(load) : 0` the compiler sinks each load into a branch and waits for it there (vmcnt(0) per
+// 16-feature step: a serial chain of L2 round trips in every kernel's prologue).
 template <int KS1>
-__device__ __forceinline__ void ln_operands(const float* __restrict__ x, const float* __restrict__ g,
-                                            const float* __restrict__ b, int64_t row, bool ok, int d, int h,
-                                            float eps, bool have_stats, float& mean, float& rstd,
-                                            bf16x8 (&bx)[KS1], uint16_t* ln_out) {
-  float xv[KS1][8];
+__device__ __forceinline__ void ln_load(const float* __restrict__ x, int64_t row, bool ok, int d, int h,
+                                        float (&xv)[KS1][8]) {
 #pragma unroll
   for (int ks = 0; ks < KS1; ++ks) {
     const int k0 = ks * 16 + 8 * h;
     const bool in = ok && k0 < d;
     const float4* p = reinterpret_cast<const float4*>(x + (in ? row * d + k0 : 0));
     const float4 u = p[0], w = p[1];
-    xv[ks][0] = in ? u.x : 0.f; xv[ks][1] = in ? u.y : 0.f; xv[ks][2] = in ? u.z : 0.f; xv[ks][3] = in ? u.w : 0.f;
-    xv[ks][4] = in ? w.x : 0.f; xv[ks][5] = in ? w.y : 0.f; xv[ks][6] = in ? w.z : 0.f; xv[ks][7] = in ? w.w : 0.f;
+    const float m = in ? 1.f : 0.f;
+    xv[ks][0] = u.x * m; xv[ks][1] = u.y * m; xv[ks][2] = u.z * m; xv[ks][3] = u.w * m;
+    xv[ks][4] = w.x * m; xv[ks][5] = w.y * m; xv[ks][6] = w.z * m; xv[ks][7] = w.w * m;
   }
+}
+
+// statistics (unless have_stats) and the bf16 B operands bx[ks] of LN(x); g / b: gamma / beta (global or
+// LDS); ln_out: optional bf16 copy of the row
+template <int KS1>
+__device__ __forceinline__ void ln_finish(const float (&xv)[KS1][8], const float* g, const float* b, int64_t row,
+                                          bool ok, int d, int h, float eps, bool have_stats, float& mean, float& rstd,
+                                          bf16x8 (&bx)[KS1], uint16_t* ln_out) {
   if (!have_stats) {
     float s = 0.f;
 #pragma unroll
@@ -173,21 +230,31 @@ __device__ __forceinline__ void ln_operands(const float* __restrict__ x, const f
   for (int ks = 0; ks < KS1; ++ks) {
     const int k0 = ks * 16 + 8 * h;
     const bool in = k0 < d;
+    const int kc = in ? k0 : 0;
+    const float m = in ? 1.f : 0.f;
+    const float4 g0 = *reinterpret_cast<const float4*>(g + kc), g1 = *reinterpret_cast<const float4*>(g + kc + 4);
+    const float4 b0 = *reinterpret_cast<const float4*>(b + kc), b1 = *reinterpret_cast<const float4*>(b + kc + 4);
+    const float gg[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+    const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
     float y[8];
-    {
-      // unconditional loads at a clamped index (speculatable: the compiler may issue them beside the
-      // row loads instead of one dependent L2 round trip after the statistics)
-      const int kc = in ? k0 : 0;
-      const float4 g0 = *reinterpret_cast<const float4*>(g + kc), g1 = *reinterpret_cast<const float4*>(g + kc + 4);
-      const float4 b0 = *reinterpret_cast<const float4*>(b + kc), b1 = *reinterpret_cast<const float4*>(b + kc + 4);
-      const float gg[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
-      const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
 #pragma unroll
-      for (int j = 0; j < 8; ++j) y[j] = in ? (xv[ks][j] - mean) * rstd * gg[j] + bb[j] : 0.f;
-    }
+    for (int j = 0; j < 8; ++j) y[j] = ((xv[ks][j] - mean) * rstd * gg[j] + bb[j]) * m;
     bx[ks] = pack_bf16x8<bf16x8>(y);
     if (ln_out && ok && in) *reinterpret_cast<bf16x8*>(ln_out + row * d + k0) = bx[ks];
   }
+}
+
+// Row r = `row` of x (d features, 16-B aligned rows) normalised into the B operands bx[ks]
+// (features 16 ks + 8 h .. +7; zero beyond d).  have_stats: mean / rstd given (backward recompute);
+// else computed (two-pass, biased variance, as kdfm_layernorm_fwd).  ln_out: bf16 copy of the row.
+template <int KS1>
+__device__ __forceinline__ void ln_operands(const float* __restrict__ x, const float* __restrict__ g,
+                                            const float* __restrict__ b, int64_t row, bool ok, int d, int h,
+                                            float eps, bool have_stats, float& mean, float& rstd,
+                                            bf16x8 (&bx)[KS1], uint16_t* ln_out) {
+  float xv[KS1][8];
+  ln_load<KS1>(x, row, ok, d, h, xv);
+  ln_finish<KS1>(xv, g, b, row, ok, d, h, eps, have_stats, mean, rstd, bx, ln_out);
 }
 
 // in-register reduce-scatter of N values over the 16 lanes of a DPP row (lane bits 8,4,2,1): afterwards

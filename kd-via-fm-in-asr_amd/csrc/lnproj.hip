@@ -79,23 +79,30 @@ __global__ __launch_bounds__(LP_NT) void lnproj_fwd_kernel(LpFwd a) {
   const int d = a.d;
   const uint4* img = reinterpret_cast<const uint4*>(a.img);
   St::issue(img, 0, Gm::NU, lp_lds, 0);
-  float mean = 0.f, rstd = 0.f;
-  bf16x8 bx[KS1];
-  ln_operands<KS1>(a.x, a.g, a.b, row, ok, d, h, a.eps, false, mean, rstd, bx, p == 0 ? a.ln_h : nullptr);
-  if (a.mean && p == 0 && h == 0 && ok) {
-    a.mean[row] = mean;
-    a.rstd[row] = rstd;
-  }
+  float xv[KS1][8];
+  ln_load<KS1>(a.x, row, ok, d, h, xv);
   bool live = ok;
   if (MODE == LP_GLU && ok && a.lens) live = (row % a.T) < a.lens[row / a.T];
   constexpr int S = (Gm::NU + LP_NP - 1) / LP_NP;
   // projection bias (and the positional biases) in LDS: a global load inside the loop would wait
   // (in-order vmcnt) for the next stage's prefetch
   float* vec_s = reinterpret_cast<float*>(lp_lds + (S > 1 ? 2 : 1) * St::UNITS);
-  const int nvec = (MODE == LP_QKV ? 5 : 2) * d;
-  for (int e = threadIdx.x; e < nvec; e += LP_NT)
-    vec_s[e] = e < Gm::G * d ? a.bias[e] : (e < 4 * d ? a.pu[e - 3 * d] : a.pv[e - 4 * d]);
+  // [bias | pos_bias_u | pos_bias_v | gamma | beta] (QKV) or [bias | gamma | beta] (GLU), filled while the
+  // row loads and the stage-0 DMA are in flight; the LayerNorm runs after the barrier
+  const int ng = (MODE == LP_QKV ? 5 : 2) * d;
+  if (MODE == LP_QKV)
+    fill_vec5<7 * 32 * DT, LP_NT>(vec_s, a.bias, 3 * d, a.pu, d, a.pv, d, a.g, d, a.b, d);
+  else
+    fill_vec5<4 * 32 * DT, LP_NT>(vec_s, a.bias, 2 * d, a.g, d, a.b, d, a.b, 0, a.b, 0);
   __syncthreads();
+  float mean = 0.f, rstd = 0.f;
+  bf16x8 bx[KS1];
+  ln_finish<KS1>(xv, vec_s + ng, vec_s + ng + d, row, ok, d, h, a.eps, false, mean, rstd, bx,
+                 p == 0 ? a.ln_h : nullptr);
+  if (a.mean && p == 0 && h == 0 && ok) {
+    a.mean[row] = mean;
+    a.rstd[row] = rstd;
+  }
   for (int s = 0; s < S; ++s) {
     const int u = s * LP_NP + p;
     // this unit's bias vectors are read from LDS before the next stage's DMA is issued (an LDS read
@@ -373,7 +380,7 @@ int launch_lp_fwd(const LpFwd& a, hipStream_t st) {
   static bool once = (lp_allow_lds(lnproj_fwd_kernel<KS1, DT, MODE>), true);
   (void)once;
   constexpr int S = (Gm::NU + LP_NP - 1) / LP_NP;
-  const size_t lds = (size_t)(S > 1 ? 2 : 1) * LP_NP * Gm::UF * 1024 + (size_t)(MODE == LP_QKV ? 5 : 2) * a.d * 4;
+  const size_t lds = (size_t)(S > 1 ? 2 : 1) * LP_NP * Gm::UF * 1024 + (size_t)(MODE == LP_QKV ? 7 : 4) * a.d * 4;
   hipLaunchKernelGGL((lnproj_fwd_kernel<KS1, DT, MODE>), dim3((unsigned)ceil_div(a.rows, LP_ROWS)), dim3(LP_NT), lds, st,
                      a);
   return check_launch(MODE == LP_QKV ? "kdfm_ln_qkv_fwd" : "kdfm_ln_glu_fwd");
