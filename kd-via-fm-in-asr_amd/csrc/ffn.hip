@@ -133,7 +133,10 @@ __global__ __launch_bounds__(fwd_nt<DT>()) void ffn_fwd_kernel(FfnFwd a) {
   float xv[KS1][8];
   ln_load<KS1>(a.x, row, ok, d, h, xv);
   float* bias_s = reinterpret_cast<float*>(reinterpret_cast<char*>(ff_lds) + ffn_fwd_stage_bytes<G::FWD, DT>());
-  fill_vec5<7 * 32 * DT, FWD_NT>(bias_s, a.b1, ff, a.b2, d, a.g, d, a.b, d, a.b, 0);   // ff = 4 d <= 4 * 32 DT
+  // [b1 | b2 | gamma | beta | (norm_out) gamma | beta]: ff = 4 d <= 4 * 32 DT
+  const int nlo = a.ln_out ? d : 0;
+  fill_vec6<9 * 32 * DT, FWD_NT>(bias_s, a.b1, ff, a.b2, d, a.g, d, a.b, d, a.ln_out ? a.ln_g : a.b, nlo,
+                                 a.ln_out ? a.ln_b : a.b, nlo);
   f32x16 acc[DT];
 #pragma unroll
   for (int mt = 0; mt < DT; ++mt)
@@ -142,7 +145,7 @@ __global__ __launch_bounds__(fwd_nt<DT>()) void ffn_fwd_kernel(FfnFwd a) {
   // the residual rows in the accumulator layout for the epilogue, fetched now so their latency hides
   // behind the chunk loop (narrow d only: 4 DT float4 registers)
   constexpr bool XPRE = DT <= 3 && FWD_NP == 2;
-  float4 xres[XPRE ? DT : 1][4];
+  float4 xres[DT][4];   // (wide d: loaded after the chunk loop, below)
   if constexpr (XPRE) {
 #pragma unroll
     for (int mt = 0; mt < DT; ++mt)
@@ -221,6 +224,19 @@ __global__ __launch_bounds__(fwd_nt<DT>()) void ffn_fwd_kernel(FfnFwd a) {
     __syncthreads();
     FFN_PROBE(5 + 2 * it);
   }
+  // wide d (4 waves, 512 registers): the epilogue's residual rows, all issued before any of its stores
+  // (one wait, not one per row piece behind the previous store) and before the partials' reduction so
+  // their latency overlaps it
+  if constexpr (!XPRE && DT > 3) {
+#pragma unroll
+    for (int mt = 0; mt < DT; ++mt)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int n0 = mt * 32 + 8 * q + 4 * h;
+        const bool in = par == 0 && ok && n0 < d;
+        xres[mt][q] = *reinterpret_cast<const float4*>(a.x + (in ? row * d + n0 : 0));
+      }
+  }
   // partials of parities 1..NP-1 -> parity 0, added in the fixed order ((p0 + p1) + p2) + p3
   float* red = reinterpret_cast<float*>(ff_lds) + tile * ((FWD_NP - 1) * DT * 16 * 64);
   if (par != 0) {
@@ -233,6 +249,7 @@ __global__ __launch_bounds__(fwd_nt<DT>()) void ffn_fwd_kernel(FfnFwd a) {
   __syncthreads();
   FFN_PROBE(30);
   if (par != 0) return;   // (every lane of the parity-0 wave stays: the optional LN reduces across lanes)
+
 #pragma unroll
   for (int q = 1; q < FWD_NP; ++q)
 #pragma unroll
@@ -247,9 +264,8 @@ __global__ __launch_bounds__(fwd_nt<DT>()) void ffn_fwd_kernel(FfnFwd a) {
       const int n0 = mt * 32 + 8 * q + 4 * h;
       const bool in = ok && n0 < d;
       const float4 bb = *reinterpret_cast<const float4*>(bias_s + ff + (n0 < d ? n0 : 0));
-      float4 xr;
-      if constexpr (XPRE) xr = xres[mt][q];
-      else xr = *reinterpret_cast<const float4*>(a.x + (in ? row * d + n0 : 0));
+      // (narrow d: loaded here, one piece at a time -- batching them spills at 2 waves per SIMD)
+      const float4 xr = (XPRE || DT > 3) ? xres[mt][q] : *reinterpret_cast<const float4*>(a.x + (in ? row * d + n0 : 0));
       const float bv[4] = {bb.x, bb.y, bb.z, bb.w}, xv[4] = {xr.x, xr.y, xr.z, xr.w};
       bool kp[4] = {true, true, true, true};
       if (a.p_out > 0.f) {
@@ -268,6 +284,7 @@ __global__ __launch_bounds__(fwd_nt<DT>()) void ffn_fwd_kernel(FfnFwd a) {
     }
   FFN_PROBE(31);
   if (!a.ln_out) return;
+  asm volatile("" ::: "memory");   // keep the gamma / beta table reads below here (register pressure)
   // norm_out: two-pass row statistics (this lane's half of the row + its partner lane's)
   float s = 0.f;
 #pragma unroll
@@ -298,8 +315,8 @@ __global__ __launch_bounds__(fwd_nt<DT>()) void ffn_fwd_kernel(FfnFwd a) {
     for (int q = 0; q < 4; ++q) {
       const int n0 = mt * 32 + 8 * q + 4 * h;
       if (n0 >= d) continue;
-      const float4 gg = *reinterpret_cast<const float4*>(a.ln_g + n0);
-      const float4 bb = *reinterpret_cast<const float4*>(a.ln_b + n0);
+      const float4 gg = *reinterpret_cast<const float4*>(bias_s + ff + 3 * d + n0);   // LDS table
+      const float4 bb = *reinterpret_cast<const float4*>(bias_s + ff + 4 * d + n0);
       const float gv[4] = {gg.x, gg.y, gg.z, gg.w}, bv[4] = {bb.x, bb.y, bb.z, bb.w};
       float y[4];
 #pragma unroll
@@ -483,7 +500,7 @@ __global__ __launch_bounds__(bwd_nt<DT>()) void ffn_bwd_kernel(FfnBwd a) {
     for (int mt = 0; mt < DT; ++mt)
 #pragma unroll
       for (int e = 0; e < 16; ++e) dl[mt * 16 + e] += red[((q - 1) * DT * 16 + mt * 16 + e) * 64 + lane];
-  ln_backward_rows<DT>(dl, a.x, a.g, a.dout, a.dx, a.part, a.nparts, (int64_t)blockIdx.x * FF_ROWS + tile * 32, row, ok,
+  ln_backward_rows<DT>(dl, a.x, bias_s + ff, a.dout, a.dx, a.part, a.nparts, (int64_t)blockIdx.x * FF_ROWS + tile * 32, row, ok,
                        d, mean, rstd, lane);
 }
 
@@ -499,7 +516,7 @@ int launch_fwd(const FfnFwd& a, hipStream_t st) {
   using G = FfnGeo<KS1, DT>;
   static bool once = (ffn_allow_lds(ffn_fwd_kernel<KS1, DT>), true);
   (void)once;
-  const size_t lds = (size_t)ffn_fwd_stage_bytes<G::FWD, DT>() + (size_t)(a.ff + 3 * a.d) * 4;
+  const size_t lds = (size_t)ffn_fwd_stage_bytes<G::FWD, DT>() + (size_t)(a.ff + 5 * a.d) * 4;
   if (lds > 160 * 1024) { set_error("kdfm_ffn_fwd: hidden width too large for the LDS bias table"); return KDFM_EINVAL; }
   hipLaunchKernelGGL((ffn_fwd_kernel<KS1, DT>), dim3((unsigned)ceil_div(a.rows, FF_ROWS)), dim3(fwd_nt<DT>()), lds, st, a);
   return check_launch("kdfm_ffn_fwd");

@@ -155,12 +155,13 @@ __device__ __forceinline__ void fill_vec2(float* dst, const float* __restrict__ 
                                           int nb) {
   fill_vec3<MAXE, NT>(dst, a, na, b, nb, a, 0);
 }
-// five sources (bias tables followed by the LayerNorm gamma / beta)
+// up to six sources (bias tables followed by LayerNorm gamma / beta)
 template <int MAXE, int NT>
-__device__ __forceinline__ void fill_vec5(float* dst, const float* a, int na, const float* b, int nb, const float* c,
-                                          int nc, const float* e4, int n4, const float* e5, int n5) {
+__device__ __forceinline__ void fill_vec6(float* dst, const float* a, int na, const float* b, int nb, const float* c,
+                                          int nc, const float* e4, int n4, const float* e5, int n5, const float* e6,
+                                          int n6) {
   constexpr int PER = (MAXE + NT - 1) / NT;
-  const int o1 = na, o2 = na + nb, o3 = o2 + nc, o4 = o3 + n4, o5 = o4 + n5;
+  const int o1 = na, o2 = na + nb, o3 = o2 + nc, o4 = o3 + n4, o5 = o4 + n5, o6 = o5 + n6;
   float v[PER];
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
@@ -169,14 +170,20 @@ __device__ __forceinline__ void fill_vec5(float* dst, const float* a, int na, co
                      : e < o2 ? b + (e - o1)
                      : e < o3 ? c + (e - o2)
                      : e < o4 ? e4 + (e - o3)
-                     : e < o5 ? e5 + (e - o4) : a;
+                     : e < o5 ? e5 + (e - o4)
+                     : e < o6 ? e6 + (e - o5) : a;
     v[i] = *src;
   }
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
     const int e = (int)threadIdx.x + i * NT;
-    if (e < o5) dst[e] = v[i];
+    if (e < o6) dst[e] = v[i];
   }
+}
+template <int MAXE, int NT>
+__device__ __forceinline__ void fill_vec5(float* dst, const float* a, int na, const float* b, int nb, const float* c,
+                                          int nc, const float* e4, int n4, const float* e5, int n5) {
+  fill_vec6<MAXE, NT>(dst, a, na, b, nb, c, nc, e4, n4, e5, n5, a, 0);
 }
 
 // LayerNorm operands in two parts so the row loads can be issued before a barrier and the statistics /
@@ -283,26 +290,49 @@ __device__ __forceinline__ void ln_backward_rows(const float (&dl)[DT * 16], con
                                                  float rstd, int lane) {
   constexpr int NV = DT * 16;
   const int h = lane >> 5;
-  float xh[NV];
+  // loads are issued in two batches, each before any store and consumed as a batch (x and gamma, then
+  // the residual-gradient rows): a load under a condition, or issued after this function's own stores,
+  // is waited for one at a time; two batches keep the live registers of 2-wave-per-SIMD kernels in bounds
+  float xh[NV], gy[NV];
   float s1 = 0.f, s2 = 0.f;
+  {
+    float4 xr[DT][4], gq[DT][4];
+#pragma unroll
+    for (int mt = 0; mt < DT; ++mt)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int n0 = mt * 32 + 8 * q + 4 * h;
+        const bool in = ok && n0 < d;
+        xr[mt][q] = *reinterpret_cast<const float4*>(x + (in ? row * d + n0 : 0));
+        gq[mt][q] = *reinterpret_cast<const float4*>(g + (n0 < d ? n0 : 0));
+      }
+#pragma unroll
+    for (int mt = 0; mt < DT; ++mt)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int n0 = mt * 32 + 8 * q + 4 * h;
+        const float m = (ok && n0 < d) ? 1.f : 0.f;
+        const float xv[4] = {xr[mt][q].x, xr[mt][q].y, xr[mt][q].z, xr[mt][q].w};
+        const float gv[4] = {gq[mt][q].x, gq[mt][q].y, gq[mt][q].z, gq[mt][q].w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int e = mt * 16 + 4 * q + i;
+          const float xhat = (xv[i] - mean) * rstd * m;
+          xh[e] = xhat;
+          gy[e] = dl[e] * gv[i] * m;
+          s1 += gy[e];
+          s2 += gy[e] * xhat;
+        }
+      }
+  }
+  float4 dr[DT][4];
 #pragma unroll
   for (int mt = 0; mt < DT; ++mt)
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int n0 = mt * 32 + 8 * q + 4 * h;
       const bool in = ok && n0 < d;
-      const float4 xr = *reinterpret_cast<const float4*>(x + (in ? row * d + n0 : 0));
-      const float4 gg = *reinterpret_cast<const float4*>(g + (n0 < d ? n0 : 0));
-      const float xv[4] = {xr.x, xr.y, xr.z, xr.w}, gv[4] = {gg.x, gg.y, gg.z, gg.w};
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int e = mt * 16 + 4 * q + i;
-        const float xhat = in ? (xv[i] - mean) * rstd : 0.f;
-        xh[e] = xhat;
-        const float gyv = in ? dl[e] * gv[i] : 0.f;
-        s1 += gyv;
-        s2 += gyv * xhat;
-      }
+      dr[mt][q] = *reinterpret_cast<const float4*>(dres + (in ? row * d + n0 : 0));
     }
   s1 += __shfl_xor(s1, 32, 64);
   s2 += __shfl_xor(s2, 32, 64);
@@ -315,14 +345,12 @@ __device__ __forceinline__ void ln_backward_rows(const float (&dl)[DT * 16], con
       for (int q = 0; q < 4; ++q) {
         const int n0 = mt * 32 + 8 * q + 4 * h;
         if (n0 >= d) continue;
-        const float4 dr = *reinterpret_cast<const float4*>(dres + row * d + n0);
-        const float4 gg = *reinterpret_cast<const float4*>(g + n0);
-        const float rv[4] = {dr.x, dr.y, dr.z, dr.w}, gv[4] = {gg.x, gg.y, gg.z, gg.w};
+        const float rv[4] = {dr[mt][q].x, dr[mt][q].y, dr[mt][q].z, dr[mt][q].w};
         float o[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int e = mt * 16 + 4 * q + i;
-          o[i] = rstd * (dl[e] * gv[i] - s1 - xh[e] * s2) + rv[i];
+          o[i] = rstd * (gy[e] - s1 - xh[e] * s2) + rv[i];
         }
         *reinterpret_cast<float4*>(dx + row * d + n0) = make_float4(o[0], o[1], o[2], o[3]);
       }
