@@ -103,6 +103,18 @@ __global__ __launch_bounds__(LP_NT) void lnproj_fwd_kernel(LpFwd a) {
     a.mean[row] = mean;
     a.rstd[row] = rstd;
   }
+  // the outputs leave as buffer stores every lane issues, a fixed count per unit (QKV: 8 -- the k / v
+  // waves add 4 range-dropped ones; GLU: 4), so the stage barrier counts past them (dma_barrier)
+  static_assert(Gm::NU % LP_NP == 0, "every wave has a unit in every stage");
+  constexpr uint32_t OOB = 0x80000000u;
+  constexpr int NST = MODE == LP_QKV ? 8 : 4;
+  const int rd4 = (int)(a.rows * d * 4);
+  const __amdgpu_buffer_rsrc_t r_a = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(MODE == LP_QKV ? a.qu : a.gout), (short)0, rd4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t r_b = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(MODE == LP_QKV ? a.qv : a.gout), (short)0, rd4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t r_k = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(MODE == LP_QKV ? a.qkv : a.gout), (short)0, MODE == LP_QKV ? 3 * rd4 : rd4, 0x00020000);
   for (int s = 0; s < S; ++s) {
     const int u = s * LP_NP + p;
     // this unit's bias vectors are read from LDS before the next stage's DMA is issued (an LDS read
@@ -128,21 +140,22 @@ __global__ __launch_bounds__(LP_NT) void lnproj_fwd_kernel(LpFwd a) {
         f32x16 acc = zero16();
 #pragma unroll
         for (int ks = 0; ks < KS1; ++ks) acc = mfma32(W[ks * FRAG_U4 + lane], bx[ks], acc);
+        const __amdgpu_buffer_rsrc_t r1 = g == 0 ? r_a : r_k;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int n0 = 32 * t + 8 * q + 4 * h;
-          if (!ok || n0 >= d) continue;
+          const bool in = ok && n0 < d;
           const float4 bb = vb[0][q];
           const float v0 = acc[4 * q] + bb.x, v1 = acc[4 * q + 1] + bb.y, v2 = acc[4 * q + 2] + bb.z,
                       v3 = acc[4 * q + 3] + bb.w;
-          if (g == 0) {
-            const float4 uu = vq[0][q];
-            const float4 vv = vq[1][q];
-            *reinterpret_cast<float4*>(a.qu + row * d + n0) = make_float4(v0 + uu.x, v1 + uu.y, v2 + uu.z, v3 + uu.w);
-            *reinterpret_cast<float4*>(a.qv + row * d + n0) = make_float4(v0 + vv.x, v1 + vv.y, v2 + vv.z, v3 + vv.w);
-          } else {
-            *reinterpret_cast<float4*>(a.qkv + row * 3 * d + g * d + n0) = make_float4(v0, v1, v2, v3);
-          }
+          const float4 uu = vq[0][q], vv = vq[1][q];
+          // qu (g == 0) or the k / v slice of qkv; then qv (g == 0) or a dropped store
+          const f32x4 o1 = g == 0 ? f32x4{v0 + uu.x, v1 + uu.y, v2 + uu.z, v3 + uu.w} : f32x4{v0, v1, v2, v3};
+          const f32x4 o2 = f32x4{v0 + vv.x, v1 + vv.y, v2 + vv.z, v3 + vv.w};
+          const uint32_t off1 = !in ? OOB : (uint32_t)((g == 0 ? row * d + n0 : row * 3 * d + g * d + n0) * 4);
+          const uint32_t off2 = (!in || g != 0) ? OOB : (uint32_t)((row * d + n0) * 4);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, o1), r1, off1, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, o2), r_b, off2, 0, 0);
         }
       } else {
         const int t = u;
@@ -155,7 +168,7 @@ __global__ __launch_bounds__(LP_NT) void lnproj_fwd_kernel(LpFwd a) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int n0 = 32 * t + 8 * q + 4 * h;
-          if (!ok || n0 >= d) continue;
+          const bool in = ok && n0 < d;
           const float4 ba = vb[0][q];
           const float4 bg = vb[1][q];
           const float va[4] = {aa[4 * q] + ba.x, aa[4 * q + 1] + ba.y, aa[4 * q + 2] + ba.z, aa[4 * q + 3] + ba.w};
@@ -163,11 +176,12 @@ __global__ __launch_bounds__(LP_NT) void lnproj_fwd_kernel(LpFwd a) {
           float o[4];
 #pragma unroll
           for (int i = 0; i < 4; ++i) o[i] = live ? va[i] * sigmoidf_(vg[i]) : 0.f;
-          *reinterpret_cast<float4*>(a.gout + row * d + n0) = make_float4(o[0], o[1], o[2], o[3]);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, f32x4{o[0], o[1], o[2], o[3]}), r_a,
+                                                 in ? (uint32_t)((row * d + n0) * 4) : OOB, 0, 0);
         }
       }
     }
-    __syncthreads();
+    dma_barrier<NST>();   // stage s + 1 landed; this unit's NST output stores stay in flight
   }
 }
 
@@ -453,6 +467,7 @@ int kdfm_ln_qkv_fwd(const float* x, const float* ln_g, const float* ln_b, float 
   KDFM_REQUIRE((mean == nullptr) == (rstd == nullptr), "mean and rstd go together");
   int KS1, DT;
   KDFM_REQUIRE(ln_dims(d, KS1, DT) == 0, "unsupported d");
+  KDFM_REQUIRE(rows * 3 * d * 4 <= (int64_t)INT32_MAX - 64, "rows x 3d exceeds the 2 GB buffer-store range");
   KDFM_REQUIRE(al16(x) && al16(ln_g) && al16(ln_b) && al16(img) && al16(bias) && al16(pos_u) && al16(pos_v) &&
                    al16(qu) && al16(qv) && al16(qkv) && al16(ln_h),
                "operands must be 16-byte aligned");
@@ -475,6 +490,7 @@ int kdfm_ln_glu_fwd(const float* x, const float* ln_g, const float* ln_b, float 
   KDFM_REQUIRE(T > 0 && rows % T == 0, "rows must be whole utterances of T frames");
   int KS1, DT;
   KDFM_REQUIRE(ln_dims(d, KS1, DT) == 0, "unsupported d");
+  KDFM_REQUIRE(rows * d * 4 <= (int64_t)INT32_MAX - 64, "rows x d exceeds the 2 GB buffer-store range");
   KDFM_REQUIRE(al16(x) && al16(ln_g) && al16(ln_b) && al16(img) && al16(bias) && al16(g) && al16(ln_h),
                "operands must be 16-byte aligned");
   if (rows <= 0) return KDFM_OK;
