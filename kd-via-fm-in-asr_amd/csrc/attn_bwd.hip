@@ -62,11 +62,14 @@ struct AbP {
 typedef short v4s __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4s lds_v4s;
 
-__device__ __forceinline__ bf16x8 frag8(const float* src, int valid) {
-  float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
-  if (valid >= 4) a = *reinterpret_cast<const float4*>(src);
-  if (valid >= 8) b = *reinterpret_cast<const float4*>(src + 4);
-  const float t[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+// columns c0 .. c0 + 7 of a row (head = the row's first column of this head) as bf16, zero past `valid`;
+// both loads unconditional (column clamped) and masked by a multiply: a conditional load, or a select
+// on a loaded value, is branched around and waited for one at a time
+__device__ __forceinline__ bf16x8 frag8(const float* head, int c0, int valid) {
+  const float m0 = valid >= 4 ? 1.f : 0.f, m1 = valid >= 8 ? 1.f : 0.f;
+  const float4 a = *reinterpret_cast<const float4*>(head + (valid >= 4 ? c0 : 0));
+  const float4 b = *reinterpret_cast<const float4*>(head + (valid >= 8 ? c0 + 4 : 0));
+  const float t[8] = {a.x * m0, a.y * m0, a.z * m0, a.w * m0, b.x * m1, b.y * m1, b.z * m1, b.w * m1};
   return pack_bf16x8<bf16x8>(t);
 }
 
@@ -179,10 +182,10 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dq_kernel(AbP p
   for (int ks = 0; ks < 2; ++ks) {
     const int c0 = ks * 32 + 8 * (lane >> 4);
     const int valid = iq < T ? dk - c0 : 0;
-    const int64_t off = (b * p.T + (iq < T ? iq : 0)) * p.ldq + hoff + c0;
-    fu[ks] = frag8(p.qu + off, valid);
-    fv[ks] = frag8(p.qv + off, valid);
-    fdo[ks] = frag8(p.dO + off, valid);
+    const int64_t off = (b * p.T + (iq < T ? iq : 0)) * p.ldq + hoff;
+    fu[ks] = frag8(p.qu + off, c0, valid);
+    fv[ks] = frag8(p.qv + off, c0, valid);
+    fdo[ks] = frag8(p.dO + off, c0, valid);
   }
   const int ib = i0 + w * 16 + 4 * (lane >> 4);   // C-layout rows ib + r
   const int64_t prow0 = (bh * p.T + ib) * p.T;
@@ -351,7 +354,7 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dkv_kernel(AbP 
   for (int ks = 0; ks < 2; ++ks) {
     const int c0 = ks * 32 + 8 * (lane >> 4);
     const bool ok = jk < len;
-    fv[ks] = frag8(p.v + (b * p.T + (ok ? jk : 0)) * p.ldkv + hoff + c0, ok ? dk - c0 : 0);
+    fv[ks] = frag8(p.v + (b * p.T + (ok ? jk : 0)) * p.ldkv + hoff, c0, ok ? dk - c0 : 0);
   }
   const int jb = j0 + w * 16 + 4 * (lane >> 4);   // C-layout key rows jb + r
   const uint64_t seed = (p.p_drop > 0.f) ? load_seed(p.seed) : 0ull;
@@ -538,7 +541,7 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dpos_kernel(AbP
     for (int ks = 0; ks < 2; ++ks) {
       const int c0 = ks * 32 + 8 * (lane >> 4);
       const bool ok = iq < ln;
-      nfdo[ks] = frag8(p.dO + (bb * p.T + (ok ? iq : 0)) * p.ldq + hoff + c0, ok ? dk - c0 : 0);
+      nfdo[ks] = frag8(p.dO + (bb * p.T + (ok ? iq : 0)) * p.ldq + hoff, c0, ok ? dk - c0 : 0);
     }
 #pragma unroll
     for (int t = 0; t < 3; ++t)

@@ -47,12 +47,14 @@ struct AttnP {
   const uint64_t* seed; uint64_t rng_stream;
 };
 
-__device__ __forceinline__ bf16x8 load_frag8(const float* src, int valid) {
-  // 8 consecutive floats -> bf16x8, elements >= valid are zero (valid is a multiple of 4 or >= 8)
-  float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
-  if (valid >= 4) a = *reinterpret_cast<const float4*>(src);
-  if (valid >= 8) b = *reinterpret_cast<const float4*>(src + 4);
-  const float t[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+__device__ __forceinline__ bf16x8 load_frag8(const float* head, int c0, int valid) {
+  // columns c0 .. c0 + 7 of a row (head: its first column of this head) -> bf16x8, elements >= valid
+  // zero (valid a multiple of 4 or >= 8); unconditional loads at a clamped column, masked by a
+  // multiply (a conditional load, or a select on a loaded value, is branched around and waited for)
+  const float m0 = valid >= 4 ? 1.f : 0.f, m1 = valid >= 8 ? 1.f : 0.f;
+  const float4 a = *reinterpret_cast<const float4*>(head + (valid >= 4 ? c0 : 0));
+  const float4 b = *reinterpret_cast<const float4*>(head + (valid >= 8 ? c0 + 4 : 0));
+  const float t[8] = {a.x * m0, a.y * m0, a.z * m0, a.w * m0, b.x * m1, b.y * m1, b.z * m1, b.w * m1};
   return pack_bf16x8<bf16x8>(t);
 }
 
@@ -137,9 +139,9 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void relpos_attn_fwd_kernel(A
   for (int ks = 0; ks < 2; ++ks) {
     const int c0 = ks * 32 + 8 * (lane >> 4);
     const int valid = (iq < T) ? dk - c0 : 0;
-    const int64_t off = (b * p.T + iq) * p.ldq + hoff + c0;
-    fu[ks] = load_frag8(p.qu + off, valid);
-    fv[ks] = load_frag8(p.qv + off, valid);
+    const int64_t off = (b * p.T + (iq < T ? iq : 0)) * p.ldq + hoff;
+    fu[ks] = load_frag8(p.qu + off, c0, valid);
+    fv[ks] = load_frag8(p.qv + off, c0, valid);
   }
 
   // rows owned by this lane in the C layout: ii = 4*(lane>>4) + r
