@@ -233,33 +233,56 @@ __global__ __launch_bounds__(LP_NT) void ln_qkv_bwd_kernel(LpBwd a) {
   const int d = a.d;
   const uint4* img = reinterpret_cast<const uint4*>(a.img);
   St::issue(img, 0, DT, lp_lds, 0);
+  // every prologue load first (the dproj rows, row statistics, x rows of the q wave), masks by multiply,
+  // then the bf16 stores: a load issued after a store, or a select on a loaded value, is waited for
+  // one at a time
   // B operands of this kind: dproj features 32 t + 16 s2 + 8 h .. +7
-  bf16x8 bop[2 * DT];
+  float4 r0[2 * DT], r1[2 * DT];
 #pragma unroll
   for (int k = 0; k < 2 * DT; ++k) {
     const int f0 = 16 * k + 8 * h;
     const bool in = ok && f0 < d;
-    float v[8];
+    const float* src = p == 0 ? a.dqu + (in ? row * d + f0 : 0) : a.dqkv + (in ? row * 3 * d + p * d + f0 : 0);
+    r0[k] = reinterpret_cast<const float4*>(src)[0];
+    r1[k] = reinterpret_cast<const float4*>(src)[1];
+  }
+  float4 w0[2 * DT], w1[2 * DT];
+  if (p == 0) {
+#pragma unroll
+    for (int k = 0; k < 2 * DT; ++k) {
+      const int f0 = 16 * k + 8 * h;
+      const bool in = ok && f0 < d;
+      w0[k] = reinterpret_cast<const float4*>(a.dqv + (in ? row * d + f0 : 0))[0];
+      w1[k] = reinterpret_cast<const float4*>(a.dqv + (in ? row * d + f0 : 0))[1];
+    }
+  }
+  const int64_t rc = ok ? row : 0;
+  const float rm = ok ? 1.f : 0.f;
+  float mean = a.mean[rc] * rm, rstd = a.rstd[rc] * rm;
+  float xv[KS1][8];
+  if (p == 0) ln_load<KS1>(a.x, row, ok, d, h, xv);
+  bf16x8 bop[2 * DT];
+#pragma unroll
+  for (int k = 0; k < 2 * DT; ++k) {
+    const int f0 = 16 * k + 8 * h;
+    const float m = (ok && f0 < d) ? 1.f : 0.f;
+    float v[8] = {r0[k].x, r0[k].y, r0[k].z, r0[k].w, r1[k].x, r1[k].y, r1[k].z, r1[k].w};
     if (p == 0) {
-      const float4* pu = reinterpret_cast<const float4*>(a.dqu + (in ? row * d + f0 : 0));
-      const float4* pv = reinterpret_cast<const float4*>(a.dqv + (in ? row * d + f0 : 0));
-      const float4 u0 = pu[0], u1 = pu[1], w0 = pv[0], w1 = pv[1];
-      v[0] = u0.x + w0.x; v[1] = u0.y + w0.y; v[2] = u0.z + w0.z; v[3] = u0.w + w0.w;
-      v[4] = u1.x + w1.x; v[5] = u1.y + w1.y; v[6] = u1.z + w1.z; v[7] = u1.w + w1.w;
-    } else {
-      const float4* pk = reinterpret_cast<const float4*>(a.dqkv + (in ? row * 3 * d + p * d + f0 : 0));
-      const float4 u0 = pk[0], u1 = pk[1];
-      v[0] = u0.x; v[1] = u0.y; v[2] = u0.z; v[3] = u0.w; v[4] = u1.x; v[5] = u1.y; v[6] = u1.z; v[7] = u1.w;
+      v[0] += w0[k].x; v[1] += w0[k].y; v[2] += w0[k].z; v[3] += w0[k].w;
+      v[4] += w1[k].x; v[5] += w1[k].y; v[6] += w1[k].z; v[7] += w1[k].w;
     }
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = in ? v[j] : 0.f;
+    for (int j = 0; j < 8; ++j) v[j] *= m;
     bop[k] = pack_bf16x8<bf16x8>(v);
-    if (in) *reinterpret_cast<bf16x8*>(a.dproj_h + row * 3 * d + p * d + f0) = bop[k];
   }
-  float mean = ok ? a.mean[row] : 0.f, rstd = ok ? a.rstd[row] : 0.f;
+#pragma unroll
+  for (int k = 0; k < 2 * DT; ++k) {
+    const int f0 = 16 * k + 8 * h;
+    if (ok && f0 < d) *reinterpret_cast<bf16x8*>(a.dproj_h + row * 3 * d + p * d + f0) = bop[k];
+  }
   if (p == 0) {   // bf16 LN output: the weight-gradient operand
     bf16x8 bx[KS1];
-    ln_operands<KS1>(a.x, a.g, a.b, row, ok, d, h, 0.f, true, mean, rstd, bx, a.ln_h);
+    ln_finish<KS1>(xv, a.g, a.b, row, ok, d, h, 0.f, true, mean, rstd, bx, a.ln_h);
   }
   f32x16 acc[DT];
 #pragma unroll
@@ -323,16 +346,31 @@ __global__ __launch_bounds__(LP_NT) void ln_glu_bwd_kernel(LpBwd a) {
   const bool ok = row < a.rows;
   const int d = a.d;
   St::issue(reinterpret_cast<const uint4*>(a.img), 0, DT, lp_lds, 0);
-  float mean = ok ? a.mean[row] : 0.f, rstd = ok ? a.rstd[row] : 0.f;
+  // every prologue load first (row statistics, x rows, this group's biases and dg rows, the length),
+  // then the LayerNorm and its bf16 store: a load issued after a store is waited for one at a time
+  const int64_t rc = ok ? row : 0;
+  const float rm = ok ? 1.f : 0.f;
+  float mean = a.mean[rc] * rm, rstd = a.rstd[rc] * rm;
+  float xv[KS1][8];
+  ln_load<KS1>(a.x, row, ok, d, h, xv);
+  const int t = p;
+  float4 bav[4], bgv[4], dgr[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int n0 = 32 * t + 8 * q + 4 * h;
+    const bool in = ok && n0 < d;
+    bav[q] = *reinterpret_cast<const float4*>(a.bias + (n0 < d ? n0 : 0));
+    bgv[q] = *reinterpret_cast<const float4*>(a.bias + d + (n0 < d ? n0 : 0));
+    dgr[q] = *reinterpret_cast<const float4*>(a.dg + (in ? row * d + n0 : 0));
+  }
+  const int64_t ln = a.lens ? a.lens[rc / a.T] : a.T;
+  const bool live = ok && (row % a.T) < ln;
   bf16x8 bx[KS1];
-  ln_operands<KS1>(a.x, a.g, a.b, row, ok, d, h, 0.f, true, mean, rstd, bx, p == 0 ? a.ln_h : nullptr);
-  bool live = ok;
-  if (ok && a.lens) live = (row % a.T) < a.lens[row / a.T];
+  ln_finish<KS1>(xv, a.g, a.b, row, ok, d, h, 0.f, true, mean, rstd, bx, p == 0 ? a.ln_h : nullptr);
   f32x16 acc[DT];
 #pragma unroll
   for (int mt = 0; mt < DT; ++mt) acc[mt] = zero16();
   __syncthreads();
-  const int t = p;
   if (t < DT) {
     const uint4* W = St::block(lp_lds, 0, p);
     f32x16 aa = zero16(), ag = zero16();
@@ -346,9 +384,7 @@ __global__ __launch_bounds__(LP_NT) void ln_glu_bwd_kernel(LpBwd a) {
     for (int q = 0; q < 4; ++q) {
       const int n0 = 32 * t + 8 * q + 4 * h;
       const bool in = live && n0 < d;
-      const float4 ba = *reinterpret_cast<const float4*>(a.bias + (n0 < d ? n0 : 0));
-      const float4 bg = *reinterpret_cast<const float4*>(a.bias + d + (n0 < d ? n0 : 0));
-      const float4 dgv = *reinterpret_cast<const float4*>(a.dg + (in ? row * d + n0 : 0));
+      const float4 ba = bav[q], bg = bgv[q], dgv = dgr[q];
       const float va[4] = {aa[4 * q] + ba.x, aa[4 * q + 1] + ba.y, aa[4 * q + 2] + ba.z, aa[4 * q + 3] + ba.w};
       const float vg[4] = {ag[4 * q] + bg.x, ag[4 * q + 1] + bg.y, ag[4 * q + 2] + bg.z, ag[4 * q + 3] + bg.w};
       const float gv[4] = {dgv.x, dgv.y, dgv.z, dgv.w};
