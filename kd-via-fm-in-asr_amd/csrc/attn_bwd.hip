@@ -25,6 +25,11 @@
 // element is owned by one workgroup and the fold is ordered: deterministic, no atomics.
 #include "gemm_common.h"
 
+// timing probe points (tools/attn_bwd_probe.hip defines KPROBE; empty in the library)
+#ifndef KPROBE
+#define KPROBE(i)
+#endif
+
 namespace kdfm {
 namespace {
 
@@ -161,6 +166,7 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dq_kernel(AbP p
   __shared__ __attribute__((aligned(16))) uint16_t Pr[PB1 * LR];    // Ppos band [band row][c]
   __shared__ __attribute__((aligned(16))) float Wsc[4][WS1 / 4];    // per-wave scratch
 
+  KPROBE(0);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int T = (int)p.T, dk = (int)p.dkh;
   const Blk3 blk = xcd_block3();
@@ -218,6 +224,7 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dq_kernel(AbP p
   uint16_t* D = reinterpret_cast<uint16_t*>(Wsc[w]);    // bf16 dS [16][LW]   (after the scores)
   uint16_t* Gk = D + 16 * LW;                           // bf16 skewed dS [16][LG]
   if (nkb > 0) fetch(0);
+  KPROBE(1);
   for (int kb = 0; kb < nkb; ++kb) {
     const int j0 = kb * BK;
     __syncthreads();
@@ -226,6 +233,7 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dq_kernel(AbP p
     put_rows<2 * NU>(Pr, nullptr, 0, nb, 127, dk);
     __syncthreads();
     if (kb + 1 < nkb) fetch(kb + 1);
+    KPROBE(2 + 4 * kb);
     // ---- S of this wave's 16 rows x 64 keys: the forward's scores (relpos_attn_fwd_kernel) ----
     float s[4][4];
     {
@@ -263,6 +271,7 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dq_kernel(AbP p
         }
       wsync();   // the scratch is rewritten below
     }
+    KPROBE(3 + 4 * kb);
     // ---- dPd = dO V^T ----
     f32x4 a[4];
 #pragma unroll
@@ -293,6 +302,7 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dq_kernel(AbP p
         Gk[ii * LG + jj - ii + 15] = bv;
       }
     wsync();
+    KPROBE(4 + 4 * kb);
     // ---- dQu += dS K (K read transposed), dQv += skew(dS) Pband (band read transposed) ----
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
@@ -309,7 +319,9 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dq_kernel(AbP p
         av[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ga, tr_frag(Pr, LR, wb + ks * 32, 16 * u, lane), av[u], 0, 0, 0);
     }
     wsync();
+    KPROBE(5 + 4 * kb);
   }
+  KPROBE(30);
 #pragma unroll
   for (int u = 0; u < NU; ++u)
 #pragma unroll
@@ -321,6 +333,7 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dq_kernel(AbP p
         p.dqv[off] = av[u][r];
       }
     }
+  KPROBE(31);
 }
 
 // ---------------------------------------------------------------------------------------------
