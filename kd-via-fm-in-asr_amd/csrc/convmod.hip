@@ -49,7 +49,9 @@ __global__ __launch_bounds__(256) void glu_mask_bwd_kernel(const float* __restri
 
 // Frame x channel tile staging shared by the depthwise-conv kernels: rows [t0 - pad, t0 + rows - pad)
 // of one utterance, CT channels from c0, as float4 chunks (d % 4 == 0).  Every load of the tile is
-// issued before the first LDS store, so the tile costs one memory round trip, not one per chunk.
+// issued before the first LDS store, so the tile costs one memory round trip, not one per chunk: the
+// loads are unconditional (frame and channel clamped into range) and masked by a multiply, since a
+// conditional load is branched around and waited for one at a time.
 constexpr int TQ = 8;  // float4 chunks per thread (rows <= TT + KMAX - 1 = 126)
 
 __device__ __forceinline__ void tile_load(float4 (&v)[TQ], const float* __restrict__ src, int64_t b, int64_t t0,
@@ -60,8 +62,22 @@ __device__ __forceinline__ void tile_load(float4 (&v)[TQ], const float* __restri
     const int rr = q >> 4, c4 = (q & 15) * 4;
     const int64_t t = t0 + rr - pad, c = c0 + c4;
     const bool ok = rr < rows && t >= 0 && t < T && c < d;
-    v[i] = ok ? *reinterpret_cast<const float4*>(src + (b * T + t) * d + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float m = ok ? 1.f : 0.f;
+    const float4 x = *reinterpret_cast<const float4*>(src + (b * T + (ok ? t : 0)) * d + (ok ? c : 0));
+    v[i] = make_float4(x.x * m, x.y * m, x.z * m, x.w * m);
   }
+}
+
+// the KC taps of channel c (zero past d), every load issued at once (channel clamped, masked by a
+// multiply) before the tile's barrier: per-tap conditional loads inside the FMA loop were each
+// waited for on their own
+template <int KC>
+__device__ __forceinline__ void taps_load(float (&wv)[KC], const float* __restrict__ w, int64_t c, int64_t d) {
+  const bool ok = c < d;
+  const float m = ok ? 1.f : 0.f;
+  const float* wc = w + (ok ? c : 0) * KC;
+#pragma unroll
+  for (int k = 0; k < KC; ++k) wv[k] = wc[k] * m;
 }
 
 __device__ __forceinline__ void tile_store(const float4 (&v)[TQ], float* tile, int rows) {
@@ -88,16 +104,19 @@ __global__ __launch_bounds__(256) void dwconv_fwd_kernel(const float* __restrict
   const int64_t b = blockIdx.z;
   const int64_t t0 = (int64_t)blockIdx.x * TT;
   const int64_t c0 = (int64_t)blockIdx.y * CT;
-  {
-    float4 v[TQ];
-    tile_load(v, g, b, t0, pad, TT + K - 1, T, d, c0);
-    tile_store(v, tile, TT + K - 1);
-  }
   const int cc = threadIdx.x & 63;
   const int f0 = (threadIdx.x >> 6) * 16;
   const int64_t c = c0 + cc;
   const bool cok = c < d;
-  const float bc = (bias && cok) ? bias[c] : 0.f;
+  float wv[KC > 0 ? KC : 1];
+  float bc = 0.f;
+  {
+    float4 v[TQ];
+    tile_load(v, g, b, t0, pad, TT + K - 1, T, d, c0);
+    if constexpr (KC > 0) taps_load<KC>(wv, w, c, d);
+    if (bias) bc = bias[cok ? c : 0] * (cok ? 1.f : 0.f);
+    tile_store(v, tile, TT + K - 1);
+  }
   __syncthreads();
   float acc[16];
 #pragma unroll
@@ -108,7 +127,7 @@ __global__ __launch_bounds__(256) void dwconv_fwd_kernel(const float* __restrict
     for (int tt = 0; tt < 16; ++tt) win[tt] = tile[(f0 + tt) * CT + cc];
 #pragma unroll
     for (int k = 0; k < KC; ++k) {
-      const float wk = cok ? w[c * KC + k] : 0.f;
+      const float wk = wv[k];
 #pragma unroll
       for (int tt = 0; tt < 16; ++tt) acc[tt] += wk * win[tt];
       if (k + 1 < KC) {
@@ -314,20 +333,22 @@ __global__ __launch_bounds__(256) void dwconv_bwd_kernel(const float* __restrict
   const int64_t t0 = (int64_t)blockIdx.x * TT;
   const int64_t c0 = (int64_t)blockIdx.y * CT;
   const int rowsIn = TT + K - 1;
-  {
-    float4 v1[TQ], v2[TQ];
-    tile_load(v1, dy, b, t0, pad, rowsIn, T, d, c0);
-    tile_load(v2, g, b, t0, pad, rowsIn, T, d, c0);
-    tile_store(v1, tdy, rowsIn);
-    tile_store(v2, tg, rowsIn);
-  }
-  for (int e = threadIdx.x; e < NSLOT * (K + 1) * CT; e += 256) (&red[0][0])[e] = 0.f;
-  __syncthreads();
   const int slot = KC > 0 ? (threadIdx.x >> 6) : 0;
   const int cc = threadIdx.x & 63;
   const int f0 = (threadIdx.x >> 6) * 16;  // this wave's first frame in the tile
   const int64_t c = c0 + cc;
   const bool cok = c < d;
+  float wv[KC > 0 ? KC : 1];
+  {
+    float4 v1[TQ], v2[TQ];
+    tile_load(v1, dy, b, t0, pad, rowsIn, T, d, c0);
+    tile_load(v2, g, b, t0, pad, rowsIn, T, d, c0);
+    if constexpr (KC > 0) taps_load<KC>(wv, w, c, d);
+    tile_store(v1, tdy, rowsIn);
+    tile_store(v2, tg, rowsIn);
+  }
+  for (int e = threadIdx.x; e < NSLOT * (K + 1) * CT; e += 256) (&red[0][0])[e] = 0.f;
+  __syncthreads();
   float bsum = 0.f;
   if constexpr (KC > 0) {
     // Sliding 16-frame register windows with the tap loop outermost: every register index is a
@@ -342,7 +363,7 @@ __global__ __launch_bounds__(256) void dwconv_bwd_kernel(const float* __restrict
     }
 #pragma unroll
     for (int kk = 0; kk < KC; ++kk) {
-      const float wk = cok ? w[c * KC + (KC - 1 - kk)] : 0.f;
+      const float wk = wv[KC - 1 - kk];
 #pragma unroll
       for (int tt = 0; tt < 16; ++tt) acc[tt] += wk * win[tt];
       if (kk + 1 < KC) {
