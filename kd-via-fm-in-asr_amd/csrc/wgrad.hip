@@ -453,7 +453,7 @@ bool wr_plan(const GemmP& p, int amode, int bmode, int64_t batch, WrPlan& pl, bo
   const int64_t nmem = p.ones_col >= 0 ? p.ones_col : p.N;
   if (nmem & 3) return false;
   if (bmode == KDFM_LD_CONV && ((p.conv_c & 3) || p.taps < 1 || p.pad < 0 || nmem != p.taps * p.conv_c)) return false;
-  static const int min_k = env_i("KDFM_WGR_MINK", 2048);
+  static const int min_k = env_i("KDFM_WGR_MINK", 512);
   if (p.K < min_k && !force) return false;
   // column slices of at most 24 16-wide blocks (a (6,3) wave tile on a 1x8 wave grid)
   const int64_t Nb_all = ceil_div(p.N, 16);
