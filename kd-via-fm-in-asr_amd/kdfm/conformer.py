@@ -13,6 +13,7 @@ slot i of a (n_layers, B*T', d) buffer — the tensors the reference's forward h
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
@@ -361,8 +362,10 @@ def _ffn_forward(cfg, P, L, which, norm, x, pd, seed, salt, li, site_act, site_o
 
 
 def layer_forward(cfg, S: EncoderShapes, P, L, li, x, out, pos_emb, lengths, *, train, seed, salt, save,
-                  bn_update=None, rm_batch=True):
-    """x (rows, d) -> out (rows, d) (written in place).  Returns ctx for backward when save."""
+                  bn_update=None, rm_batch=True, ppos=None):
+    """x (rows, d) -> out (rows, d) (written in place).  Returns ctx for backward when save.
+    ppos: this layer's projected positions linear_pos(pos_emb) (npos, d) when the caller computed
+    every layer's at once (pos_proj_all); otherwise projected here."""
     dev = x.device
     rows, d, H, dk, T, B, ff = S.rows, S.d, S.h, S.dk, S.T, S.B, S.ff
     pd = cfg.dropout if train else 0.0
@@ -396,8 +399,9 @@ def layer_forward(cfg, S: EncoderShapes, P, L, li, x, out, pos_emb, lengths, *, 
         K.linear(ln2, P[L + "self_attn.qkv.weight"], P[L + "self_attn.qkv.bias"], qkv)
         K.qkv_prep(qkv, P[L + "self_attn.pos_bias_u"], P[L + "self_attn.pos_bias_v"], qu, qv)
     npos = 2 * T - 1
-    ppos = _empty(npos, d, dev=dev)
-    K.linear(pos_emb, P[L + "self_attn.linear_pos.weight"], None, ppos)
+    if ppos is None:
+        ppos = _empty(npos, d, dev=dev)
+        K.linear(pos_emb, P[L + "self_attn.linear_pos.weight"], None, ppos)
     o = _empty(rows, d, dev=dev)
     if K.get_math() == "bf16" and dk <= 64:
         # fused flash-style kernel: no AC / BD materialisation; P (and P_drop) only when the
@@ -766,6 +770,42 @@ class EncoderRun:
         self.layers = []
 
 
+_PP_BUF = {}
+
+
+def pos_proj_all(cfg, P, prefix, pos_emb):
+    """Every layer's linear_pos(pos_emb) in ONE batched GEMM -> (n_layers, npos, d), or None.
+
+    The projection depends only on the (fixed) relative positions and each layer's weight, so the
+    encoder computes all of them before its first layer instead of one small (npos x d x d) launch per
+    layer on the critical stream (the reference applies NeMo's RelPositionMultiHeadAttention.linear_pos
+    inside every layer).  Needs the layers' weights at one element stride (the flat parameter buffer);
+    anything else, or KDFM_POS_BATCH=0, keeps the per-layer projection."""
+    nl = cfg.n_layers
+    if nl < 2 or os.environ.get("KDFM_POS_BATCH", "1") == "0":
+        return None
+    Ws = [P[f"{prefix}layers.{i}.self_attn.linear_pos.weight"] for i in range(nl)]
+    d = Ws[0].shape[0]
+    es = Ws[0].element_size()
+    st = (Ws[1].data_ptr() - Ws[0].data_ptr()) // es
+    if st <= 0 or any(W.shape != (d, d) or W.stride() != (d, 1) or W.dtype != torch.float32 or
+                      W.data_ptr() - Ws[0].data_ptr() != i * st * es for i, W in enumerate(Ws)):
+        return None
+    npos = pos_emb.shape[0]
+    # one persistent buffer per weight set: a per-step allocation freed while another stream's layers
+    # still read it breaks the stream-ordered reuse of torch's pools (the eager step then differed from
+    # its recorded plan); the next step's projection is ordered after every reader of this one (the
+    # step's streams join before the optimizer, and the teacher stream waits for the main stream)
+    key = (Ws[0].data_ptr(), st, nl, npos, d, pos_emb.device)
+    out = _PP_BUF.get(key)
+    if out is None:
+        out = _PP_BUF[key] = _empty(nl, npos, d, dev=pos_emb.device)
+    # out[l] = pos_emb @ W_l^T : A = pos_emb (KC), B(k, n) = W_l[n][k] (KC), batch l over W and out
+    K.gemm(pos_emb, Ws[0], out, npos, d, d, pos_emb.stride(0), pos_emb.stride(1), 1, d, d, 1,
+           amode=_lib.LD_KC, bmode=_lib.LD_KC, batch=(nl, 1), bA=(0, 0), bB=(st, 0), bC=(npos * d, 0))
+    return out
+
+
 def encoder_forward_steps(cfg, S: EncoderShapes, P, prefix, mel, mel_len, len1, len2, feats, pos_emb, *, train,
                           seed, salt, save, bn_running=None, use_batch_stats=True, ws, run=None):
     """Generator form of encoder_forward: issues the subsampling, then one layer per next() (the
@@ -777,13 +817,16 @@ def encoder_forward_steps(cfg, S: EncoderShapes, P, prefix, mel, mel_len, len1, 
     if save:
         run.sub = sctx
     yield
+    # after the yield: the caller issues the layers under their own stream, and the projections must be
+    # allocated (torch's per-stream pools) and written on the stream whose layers read them
+    pp = pos_proj_all(cfg, P, prefix, pos_emb)
     for i in range(cfg.n_layers):
         L = f"{prefix}layers.{i}."
         bn = None
         if bn_running is not None:
             bn = (bn_running[L + "conv.batch_norm.running_mean"], bn_running[L + "conv.batch_norm.running_var"])
         ctx = layer_forward(cfg, S, P, L, i, x, feats[i], pos_emb, len2, train=train, seed=seed, salt=salt,
-                            save=save, bn_update=bn, rm_batch=use_batch_stats)
+                            save=save, bn_update=bn, rm_batch=use_batch_stats, ppos=None if pp is None else pp[i])
         if save:
             run.layers.append(ctx)
         x = feats[i]

@@ -1,0 +1,9 @@
+#!/bin/bash
+# round 3 closing measurement pass: full GPU suite, bench, kernel-trace profile, PMC HBM traffic
+set -o pipefail
+T=r3f3
+bash tools/gpu_full.sh $T || exit $?
+f=$(find gpurun_out/$T/prof -name '*kernel_trace.csv' -print -quit)
+python3 tools/prof_summary.py "$f" 5 > gpurun_out/$T/kernel_summary.txt 2>&1
+python3 tools/timeline.py "$f" > gpurun_out/$T/timeline.txt 2>&1
+bash tools/pmc_traffic.sh ${T}_pmc || exit $?
