@@ -197,8 +197,52 @@ def cpu_baseline(threads: int, samples: int, batches=(2, 32), steps: int = 5, bu
                       f"torch.set_num_threads({threads}); value = B={big}"}
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def rank_launch_cmd(argv, gpus: int, port: int) -> list:
+    """The command that runs this benchmark as `gpus` ranks on one node (one process per GPU,
+    torch.distributed.run over 127.0.0.1), forwarding this process's own arguments."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+
+
+def launch_ranks(args, argv, run=None) -> int | None:
+    """`bench.py --gpus N` outside a launcher (no WORLD_SIZE in the environment) with N > 1: start the N
+    ranks as child processes and return their exit code (the reference trains with Lightning's
+    `devices=args.gpus`, asr_train_diffm.py:1762-1769).  This process never touches the GPU (nothing here
+    initialises HIP; the children are fresh processes, not an exec).  Inside a launcher (WORLD_SIZE set)
+    each rank checks that the launcher's world size is the one asked for.  Returns None when this process
+    is itself the (only) rank to run."""
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is not None:
+        if int(env_world) != args.gpus:
+            raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={env_world} ranks")
+        return None
+    if args.gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    if args.gpus == 1:
+        return None
+    backend = os.environ.get("KDFM_DIST_BACKEND", "nccl")
+    n_dev = torch.cuda.device_count()   # does not initialise the HIP runtime on this image
+    if backend == "nccl" and n_dev and n_dev < args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} needs {args.gpus} visible GPUs, found {n_dev} "
+                         f"(KDFM_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs)")
+    cmd = rank_launch_cmd(argv, args.gpus, _free_port())
+    _progress("launching " + " ".join(cmd))
+    import subprocess
+    return (run or subprocess.call)(cmd)
+
+
 def main():
     args = parse()
+    rc = launch_ranks(args, sys.argv[1:])
+    if rc is not None:
+        sys.exit(rc)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

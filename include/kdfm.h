@@ -435,11 +435,16 @@ int kdfm_logmel_fft(const float* xp, int64_t ldx, const float* window, const flo
  * mel/out laid out (B, T, nfilt). */
 int kdfm_logmel_normalize(const float* mel, const int64_t* seq_len, float* out, int64_t B, int64_t T, int64_t nfilt,
                           float log_guard, void* stream);
-/* SpectrogramAugmentation (audio_preprocessing.py:443-553, called asr_train_diffm.py:622-623),
- * in place on (B, T, nfilt); mask_out (optional, uint8) records the masked cells. */
+/* SpectrogramAugmentation (audio_preprocessing.py:443-553, called asr_train_diffm.py:622-623; NeMo's
+ * vectorized SpecAugment, the use_vectorized_spec_augment=True default), in place on
+ * (B, T, nfilt): per utterance, time mask q has width (int)(U * min(time_width * len, T)) and start
+ * (int)(U' * (len - width)); frequency mask q width (int)(U * freq_width), start (int)(U' * (nfilt - width));
+ * f32 arithmetic.  uniforms (optional, B x 2 (time_masks + freq_masks) floats in [0, 1), per utterance
+ * [time widths | time starts | freq widths | freq starts]): the draws as an input (parity mode); NULL =
+ * drawn from the counter RNG (seed, rng_stream).  mask_out (optional, uint8) records the masked cells. */
 int kdfm_specaugment(float* x, const int64_t* seq_len, uint8_t* mask_out, int64_t B, int64_t T, int64_t nfilt,
                      int32_t freq_masks, int32_t freq_width, int32_t time_masks, float time_width,
-                     const uint64_t* seed, uint64_t rng_stream, void* stream);
+                     const uint64_t* seed, uint64_t rng_stream, const float* uniforms, void* stream);
 
 /* ---------------- ConvSubsampling 'striding' (conformer_encoder.py:381-390, 635; A.3) ------- */
 /* cols[(b,t2,f2), c*9 + ky*3 + kx] = X[b, 2t2-1+ky, 2f2-1+kx, c] ; X channels-last (B,T1,F1,C),
@@ -677,10 +682,11 @@ int kdfm_step_advance(int64_t* step, uint64_t* seed, void* stream);
  * (a resume whose optimizer state could not be restored), like a fresh torch AdamW state.
  * gstats (optional, kdfm_grad_stats' output): when gstats[1] != 0 the gradient holds a non-finite
  * value and the update is skipped (parameters and moments unchanged; the schedule step still counts,
- * lr_out still written).  The reference has no such check (Lightning's default); it is opt-in
- * (Ver5Config.grad_check). */
+ * lr_out still written) and adam_base[0] += 1, so AdamW's bias correction counts only the steps that
+ * updated the moments (torch's AdamW `step` semantics).  The reference has no such check (Lightning's
+ * default); it is opt-in (Ver5Config.grad_check). */
 int kdfm_adamw_noam(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, int64_t n,
-                    const int64_t* step, const int64_t* adam_base, float base_lr, float d_model,
+                    const int64_t* step, int64_t* adam_base, float base_lr, float d_model,
                     float warmup_steps, float min_lr, float beta1, float beta2, float eps, float weight_decay,
                     float grad_scale, float* lr_out, const float* gstats, void* stream);
 /* out2 = [sum_i (scale g_i)^2 over the finite entries, number of non-finite entries] of the flat gradient

@@ -134,42 +134,59 @@ __global__ __launch_bounds__(256) void logmel_norm_reg_kernel(const float* __res
   }
 }
 
-// SpecAugment: per utterance `fmasks` frequency bands of width floor(U*(fwidth+1)) and `tmasks`
-// time bands of width floor(U*(max(1,int(len*twidth))+1)); masked cells set to 0.
-// One block per (utterance, chunk of SA_EPB cells): the utterance's mask intervals (counter-RNG draws:
-// frequency mask q from indices b*64 + 2q, + 1; time mask q from b*64 + 32 + 2q, + 1) are computed once
-// into LDS by the first fmasks + tmasks threads, then every cell tests against them (the per-cell
-// formulation re-drew all the masks for each of the B x T x 80 cells).
+// SpecAugment, NeMo's vectorized form (SpectrogramAugmentation(use_vectorized_spec_augment=True), the
+// default at audio_preprocessing.py:490-520), per utterance b and mask q with
+// uniforms U in [0, 1) (f32 arithmetic, truncation toward zero as torch's .long()):
+//   time:  w = (int)(U_w * min(time_width * len, T)),  start = (int)(U_s * (float)(len - w))
+//   freq:  w = (int)(U_w * freq_width),                start = (int)(U_s * (float)(nf - w))
+// cells with start <= index < start + w are set to 0.  The uniforms come from `uni` when given (parity
+// mode, SURVEY.md §8(b): RNG as an input) laid out uni[b][4 q'] for [time widths (tmasks) | time starts
+// (tmasks) | freq widths (fmasks) | freq starts (fmasks)], else from the counter RNG (time mask q: indices
+// b*64 + 32 + 2q, + 1; frequency mask q: b*64 + 2q, + 1).
+// One block per (utterance, chunk of SA_EPB cells): the utterance's mask intervals are computed once into
+// LDS by the first fmasks + tmasks threads, then every cell tests against them.
 constexpr int SA_EPB = 256 * 8;
 __global__ __launch_bounds__(256) void specaug_kernel(float* __restrict__ x, const int64_t* __restrict__ sl,
                                                       uint8_t* __restrict__ mask_out, int64_t B, int64_t T, int64_t nf,
                                                       int fmasks, int fwidth, int tmasks, float twidth,
-                                                      const uint64_t* seed_ptr, uint64_t st) {
+                                                      const uint64_t* seed_ptr, uint64_t st,
+                                                      const float* __restrict__ uni) {
   __shared__ int lo[32], hi[32];   // [0, fmasks): frequency bands; [fmasks, fmasks + tmasks): time bands
   const int64_t b = blockIdx.y;
   const int64_t cells = T * nf;
   const int64_t len = sl[b];
   if (threadIdx.x < fmasks + tmasks) {
-    const uint64_t seed = load_seed(seed_ptr);
     const int q = threadIdx.x;
+    const float* ub = uni ? uni + b * 2 * (fmasks + tmasks) : nullptr;
+    float uw, us;
     if (q < fmasks) {
-      const uint64_t base = (uint64_t)b * 64 + (uint64_t)q * 2;
-      int w = (int)(rng_uniform(seed, st, base) * (fwidth + 1));
-      if (w > fwidth) w = fwidth;
-      if (w > nf) w = (int)nf;
-      const int64_t s0 = (int64_t)(rng_uniform(seed, st, base + 1) * (float)(nf - w + 1));
+      if (ub) {
+        uw = ub[2 * tmasks + q];
+        us = ub[2 * tmasks + fmasks + q];
+      } else {
+        const uint64_t seed = load_seed(seed_ptr);
+        const uint64_t base = (uint64_t)b * 64 + (uint64_t)q * 2;
+        uw = rng_uniform(seed, st, base);
+        us = rng_uniform(seed, st, base + 1);
+      }
+      const int64_t w = (int64_t)(uw * (float)fwidth);
+      const int64_t s0 = (int64_t)(us * (float)(nf - w));
       lo[q] = (int)s0;
       hi[q] = (int)(s0 + w);
     } else {
       const int qt = q - fmasks;
-      int64_t maxw = (int64_t)((float)len * twidth);
-      if (maxw < 1) maxw = 1;
-      const uint64_t base = (uint64_t)b * 64 + 32 + (uint64_t)qt * 2;
-      int64_t w = (int64_t)(rng_uniform(seed, st, base) * (float)(maxw + 1));
-      if (w > maxw) w = maxw;
-      int64_t room = len - w + 1;
-      if (room < 1) room = 1;
-      const int64_t s0 = (int64_t)(rng_uniform(seed, st, base + 1) * (float)room);
+      if (ub) {
+        uw = ub[qt];
+        us = ub[tmasks + qt];
+      } else {
+        const uint64_t seed = load_seed(seed_ptr);
+        const uint64_t base = (uint64_t)b * 64 + 32 + (uint64_t)qt * 2;
+        uw = rng_uniform(seed, st, base);
+        us = rng_uniform(seed, st, base + 1);
+      }
+      const float wmax = fminf(twidth * (float)len, (float)T);
+      const int64_t w = (int64_t)(uw * wmax);
+      const int64_t s0 = (int64_t)(us * (float)(len - w));
       lo[q] = (int)s0;
       hi[q] = (int)(s0 + w);
     }
@@ -563,16 +580,16 @@ int kdfm_logmel_normalize(const float* mel, const int64_t* seq_len, float* out, 
 
 int kdfm_specaugment(float* x, const int64_t* seq_len, uint8_t* mask_out, int64_t B, int64_t T, int64_t nfilt,
                      int32_t freq_masks, int32_t freq_width, int32_t time_masks, float time_width,
-                     const uint64_t* seed, uint64_t rng_stream, void* stream) {
+                     const uint64_t* seed, uint64_t rng_stream, const float* uniforms, void* stream) {
   using namespace kdfm;
-  KDFM_REQUIRE(x && seq_len && seed, "null pointer");
+  KDFM_REQUIRE(x && seq_len && (seed || uniforms), "null pointer");
   KDFM_REQUIRE(freq_masks >= 0 && freq_masks <= 16 && time_masks >= 0 && time_masks <= 16, "mask counts in [0,16]");
   const int64_t n = B * T * nfilt;
   if (n == 0) return KDFM_OK;
   KDFM_REQUIRE(freq_masks + time_masks <= 32, "at most 32 masks");
   hipLaunchKernelGGL(specaug_kernel, dim3((unsigned)ceil_div(T * nfilt, SA_EPB), (unsigned)B), dim3(256), 0,
                      as_stream(stream), x, seq_len, mask_out, B, T, nfilt, freq_masks, freq_width, time_masks,
-                     time_width, seed, rng_stream);
+                     time_width, seed, rng_stream, uniforms);
   return check_launch("kdfm_specaugment");
 }
 

@@ -29,14 +29,20 @@ __device__ __forceinline__ float noam_lr(int64_t k, float base, float d_model, f
 __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                     float* __restrict__ m, float* __restrict__ v, int64_t n,
                                                     const int64_t* __restrict__ step,
-                                                    const int64_t* __restrict__ adam_base, float base, float d_model,
+                                                    int64_t* __restrict__ adam_base, float base, float d_model,
                                                     float warmup, float min_lr, float b1, float b2, float eps, float wd,
                                                     float gscale, float* __restrict__ lr_out,
                                                     const float* __restrict__ gstats) {
   const int64_t k = step[0];
   const float lr = noam_lr(k, base, d_model, warmup, min_lr);
   if (lr_out && blockIdx.x == 0 && threadIdx.x == 0) lr_out[0] = lr;
-  if (gstats && gstats[1] != 0.f) return;   // a non-finite gradient: parameters and moments unchanged
+  if (gstats && gstats[1] != 0.f) {
+    // a non-finite gradient: parameters and moments unchanged.  The schedule still advances (Lightning
+    // steps the scheduler after a skipped optimizer step) but AdamW's own step count does not (torch only
+    // counts steps that update the moments): the moments' origin moves one step later
+    if (adam_base && blockIdx.x == 0 && threadIdx.x == 0) adam_base[0] += 1;
+    return;
+  }
   const int64_t ka = adam_base ? k - adam_base[0] : k;   // AdamW's own step count
   const float bc1 = 1.f - powf(b1, (float)ka);
   const float bc2 = 1.f - powf(b2, (float)ka);
@@ -140,7 +146,7 @@ extern "C" int kdfm_grad_stats(const float* grads, int64_t n, float scale, float
 }
 
 extern "C" int kdfm_adamw_noam(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, int64_t n,
-                               const int64_t* step, const int64_t* adam_base, float base_lr, float d_model, float warmup_steps, float min_lr,
+                               const int64_t* step, int64_t* adam_base, float base_lr, float d_model, float warmup_steps, float min_lr,
                                float beta1, float beta2, float eps, float weight_decay, float grad_scale,
                                float* lr_out, const float* gstats, void* stream) {
   using namespace kdfm;

@@ -125,7 +125,7 @@ SIGNATURES: dict[str, tuple] = {
     "kdfm_power_spectrum": (_i32, [P, P, _i64, _i64, P]),
     "kdfm_logmel_fft": (_i32, [P, _i64, P, P, P, P, P, P, _i64, _i64, _i64, _i64, _i64, _i64, P]),
     "kdfm_logmel_normalize": (_i32, [P, P, P, _i64, _i64, _i64, _f32, P]),
-    "kdfm_specaugment": (_i32, [P, P, P, _i64, _i64, _i64, _i32, _i32, _i32, _f32, P, C.c_uint64, P]),
+    "kdfm_specaugment": (_i32, [P, P, P, _i64, _i64, _i64, _i32, _i32, _i32, _f32, P, C.c_uint64, P, P]),
     "kdfm_im2col_3x3s2": (_i32, [P, P, P, _i64, _i64, _i64, _i64, P]),
     "kdfm_im2col_3x3s2_tm_bf16": (_i32, [P, P, P, _i64, _i64, _i64, _i64, P]),
     "kdfm_im2col_3x3s2_tm_from_bf16": (_i32, [P, P, P, _i64, _i64, _i64, _i64, P]),

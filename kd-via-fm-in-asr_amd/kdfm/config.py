@@ -254,6 +254,11 @@ def encfm_specs(cfg: Ver5Config, trained: bool = True) -> list:
 
 def head_specs(cfg: Ver5Config, fm_prefixes=None) -> list:
     if cfg.kd_model == "encfm":
+        if cfg.use_diffkd:
+            # asr_train.py runs DiffKD beside the encoder-level FM (latent = the student width, loss summed
+            # over the layers, :754-767, 1776-1782); the engine does not: refuse rather than train its
+            # parameters on zero gradients
+            raise ValueError("kd_model='encfm' with use_diffkd is not supported by the engine")
         return encfm_specs(cfg, True)
     if cfg.kd_model != "diffm":
         raise ValueError(f"kd_model must be 'diffm' or 'encfm', got {cfg.kd_model!r}")

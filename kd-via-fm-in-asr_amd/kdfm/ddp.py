@@ -71,11 +71,15 @@ class BucketedGradAllReduce:
             from .overlap import WGRAD
             side = WGRAD.stream_after_current()
         if side is None:
-            self._works.append(dist.all_reduce(flat[lo:hi], group=self.group, async_op=True))
+            self._works.append(self._issue(flat[lo:hi], k))
         else:
             with torch.cuda.stream(side):
-                self._works.append(dist.all_reduce(flat[lo:hi], group=self.group, async_op=True))
+                self._works.append(self._issue(flat[lo:hi], k))
         self._launched.add(k)
+
+    def _issue(self, chunk: torch.Tensor, k: int):
+        """The collective of bucket k, issued on the current (issuing) stream; returns its work handle."""
+        return dist.all_reduce(chunk, group=self.group, async_op=True)
 
     def ready(self, flat: torch.Tensor, offset: int) -> None:
         if self.world == 1:
@@ -91,7 +95,8 @@ class BucketedGradAllReduce:
             if k not in self._launched:
                 self._launch(flat, k)
         for w in self._works:
-            w.wait()   # device-side: the current stream waits for the collective
+            if w is not None:
+                w.wait()   # device-side: the current stream waits for the collective
         self._works.clear()
         self._launched.clear()
         return 1.0 / self.world

@@ -272,6 +272,9 @@ class Ver5Engine:
         h = self._heads_half(train, save) if not encfm else 0
         nb = h * Ss.rows
         hctx_b = None
+        # the first heads half accumulates its loss terms into slots of its own (it runs on another stream
+        # beside the second half: no two streams add into one scalar), folded into acc after the join
+        acc_h = torch.zeros(8, device=dev) if h else None
         with K.region("encoders"):
             for k in range(cfg.n_layers + 1):
                 with K.on_stream(side):
@@ -283,8 +286,8 @@ class Ver5Engine:
                     with torch.cuda.stream(side):
                         tae_forward(cfg, self.student.P, tfeats[:h].view(nb, St.d), tae[0][:nb], tae[1][:nb], acc[1:2],
                                     layers=h)
-                    hctx_b = self._heads_first_half(cfg, Ss, St, T, h, sfeats, tfeats, tae, acc, eps, seed, save, main,
-                                                    side)
+                    hctx_b = self._heads_first_half(cfg, Ss, St, T, h, sfeats, tfeats, tae, acc_h, eps, seed, save,
+                                                    main, side)
         with torch.cuda.stream(side):
             K.linear(tfeats[-1], self.teacher.P["teacher.decoder.decoder_layers.0.weight"].view(Cn, St.d),
                      self.teacher.P["teacher.decoder.decoder_layers.0.bias"], tlogits)
@@ -347,6 +350,7 @@ class Ver5Engine:
                                        layers=cfg.n_layers - h)
                 if h:
                     main.wait_stream(self._heads_stream(main))   # the first half's loss terms
+                    K.axpby(acc_h[2:7].view(1, 5), acc[2:7].view(1, 5), acc[2:7].view(1, 5), 1.0, 1.0)
                 hctx = (hctx_b, hctx_a, h) if save else None
                 K.colsum(acc[2:7].view(5, 1), acc[7:8], accumulate=False)
         # device (recon, kd_pre, fm_pre, kd_post, fm_post, diffkd): the v/* log keys
@@ -431,6 +435,8 @@ class Ver5Engine:
         return main if self._serial() else WGRAD.stream()
 
     def _heads_first_half(self, cfg, Ss, St, T, h, sfeats, tfeats, tae, acc, eps, seed, save, main, side):
+        """acc: the half's own loss slots (same layout as the step's accumulator; recon stays with the teacher
+        auto-encoder on the teacher stream)."""
         nb = h * Ss.rows
         hs = self._heads_stream(main)
         if hs is not main:

@@ -136,10 +136,13 @@ def _frontend(cfg, consts, wav, wav_len, mel_len, dither, seed, rng_stream, out)
     return out
 
 
-def specaugment_(cfg: Ver5Config, mel: torch.Tensor, mel_len: torch.Tensor, seed, rng_stream: int, mask_out=None):
+def specaugment_(cfg: Ver5Config, mel: torch.Tensor, mel_len: torch.Tensor, seed, rng_stream: int, mask_out=None,
+                 uniforms=None):
+    """NeMo's vectorized SpecAugment in place on mel (B, T, nfilt); uniforms: optional injected
+    draws (parity mode, kernels.specaugment)."""
     B, T, nf = mel.shape
     K.specaugment(mel, mel_len, B, T, nf, cfg.freq_masks, cfg.freq_width, cfg.time_masks, cfg.time_width, seed,
-                  rng_stream, mask_out)
+                  rng_stream, mask_out, uniforms)
     return mel
 
 

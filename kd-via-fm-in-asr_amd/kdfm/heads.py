@@ -62,6 +62,10 @@ class HeadsWorkspace:
         for pre in ("fm_latent.fm.", "fm_latent_2.fm."):
             self.fm[pre] = (_empty(S, L, dev=dev), _empty(S, E, dev=dev), _empty(S, L, dev=dev))
         self.cvec, self.evec, self.dc = self.fm["fm_latent.fm."]
+        # NoiseAdapter gamma-head output-layer gradient [dw2 (L) | db2] of one heads call, folded into G on
+        # the weight-gradient stream (two layer halves run their backward concurrently: a direct
+        # read-modify-write of G from both issuing streams could lose one half's sum)
+        self.adw = _empty(1, L + 1, dev=dev)
 
 
 # ------------------------------------------------------------------------------------------------
@@ -313,9 +317,14 @@ def _adapt_denoise_backward(cfg, P, G, ws, c, g, T, seed, dev):
     x, hA = c["x"], c["hA"]
     dx_direct = _empty(n, Lt, dev=dev)
     dh = _empty(n, Lt, dev=dev)
+    adw = ws.adw
+    K.fill(adw, 0.0)
     K.adapter_bwd(g, x, hA, c["gamma"], P["adapter.gamma_head.2.weight"].view(-1), c["eps"], dx_direct, dh,
-                  G["adapter.gamma_head.2.weight"].view(-1), G["adapter.gamma_head.2.bias"], seed, c["salt"])
+                  adw[0, :Lt], adw[0, Lt:], seed, c["salt"])
     del g
+    gw2 = G["adapter.gamma_head.2.weight"].view(1, Lt)
+    gb2 = G["adapter.gamma_head.2.bias"].view(1, 1)
+    WGRAD.run(lambda: (K.axpby(adw[:, :Lt], gw2, gw2, 1.0, 1.0), K.axpby(adw[:, Lt:], gb2, gb2, 1.0, 1.0)), adw)
     WGRAD.run(lambda: K.linear_dw(dh, x, G["adapter.gamma_head.0.weight"].view(Lt, Lt),
                                   db=G["adapter.gamma_head.0.bias"]), dh, x)
     dx = _empty(n, Lt, dev=dev)

@@ -607,9 +607,14 @@ def logmel_normalize(mel, seq_len, out, B, T, nf, guard):
 
 
 def specaugment(x, seq_len, B, T, nf, freq_masks, freq_width, time_masks, time_width, seed, rng_stream,
-                mask_out=None):
+                mask_out=None, uniforms=None):
+    """uniforms: optional (B, 2 (time_masks + freq_masks)) f32 draws in [0, 1) (parity mode: the RNG as an
+    input), per utterance [time widths | time starts | freq widths | freq starts]; else the counter RNG."""
+    if uniforms is not None:
+        assert uniforms.dtype == torch.float32 and uniforms.is_contiguous()
+        assert uniforms.numel() == B * 2 * (int(freq_masks) + int(time_masks))
     call("kdfm_specaugment", ptr(x), ptr(_i64(seq_len)), ptr(mask_out), B, T, nf, int(freq_masks),
-         int(freq_width), int(time_masks), float(time_width), ptr(seed), int(rng_stream), _s())
+         int(freq_width), int(time_masks), float(time_width), ptr(seed), int(rng_stream), ptr(uniforms), _s())
 
 
 def im2col_3x3s2(X, len_in, cols, B, T1, F1, Cc):

@@ -23,26 +23,39 @@ def step_metrics(eng) -> dict:
 
     Layout read: eng.losses = [total, ctc, logit_kd (already T^2-scaled, before kd_alpha), recon,
     layer KD sum], eng.kd_terms = [recon, kd_pre, fm_pre, kd_post, fm_post, diffkd] (per-layer
-    sums, asr_train_diffm.py:773-800), eng.lr, eng.step, eng.grad_stats = [sum g^2, #non-finite]."""
-    parts = [eng.losses, eng.kd_terms, eng.lr, eng.step.to(torch.float32)]
+    sums, asr_train_diffm.py:773-800), eng.lr, eng.step, eng.grad_stats = [sum g^2, #non-finite].
+    kd_model "encfm": asr_train.py's keys (train_ctc_loss, train_logit_kd_loss, train_flow_matching_loss,
+    train_router_loss, router/batch_mean_sampling_steps_mean, train_loss) from eng.encfm_stats."""
+    encfm = eng.cfg.kd_model == "encfm"
+    # the encoder-level FM family (asr_train.py) logs its own key set from eng.encfm_stats = [flow total,
+    # router_weight * router total, their sum, mean sampled steps] (:657-663, 770-777)
+    terms = eng.encfm_stats if encfm else eng.kd_terms
+    parts = [eng.losses, terms, eng.lr, eng.step.to(torch.float32)]
     gs = getattr(eng, "grad_stats", None)
     if gs is not None:
         parts.append(gs)
     with torch.cuda.stream(eng.compute_stream) if eng.losses.is_cuda else _null():
         v = torch.cat([p.reshape(-1).to(torch.float32) for p in parts]).cpu().tolist()
     total, ctc, kl = v[0], v[1], v[2]
-    t = v[5:11]
-    out = {"loss/ctc": ctc, "loss/logit_kd": kl, "loss/layer_kd": 0.0}
-    for k, x in zip(_V_KEYS, t[:5]):
-        out[k] = x
-    if eng.cfg.use_diffkd:
-        out["v/diffkd"] = t[5]
+    nt = terms.numel()
+    t = v[5:5 + nt]
+    if encfm:
+        out = {"train_ctc_loss": ctc, "train_logit_kd_loss": kl, "train_flow_matching_loss": t[0]}
+        if eng.cfg.encfm_dynamic:
+            out["train_router_loss"] = t[1]
+            out["router/batch_mean_sampling_steps_mean"] = t[3]
+    else:
+        out = {"loss/ctc": ctc, "loss/logit_kd": kl, "loss/layer_kd": 0.0}
+        for k, x in zip(_V_KEYS, t[:5]):
+            out[k] = x
+        if eng.cfg.use_diffkd:
+            out["v/diffkd"] = t[5]
     out["train_loss"] = total
-    out["lr"] = v[11]
-    out["step"] = int(v[12])
+    out["lr"] = v[5 + nt]
+    out["step"] = int(v[6 + nt])
     if gs is not None:
-        out["grad_norm"] = v[13] ** 0.5
-        out["grad_nonfinite"] = int(v[14])
+        out["grad_norm"] = v[7 + nt] ** 0.5
+        out["grad_nonfinite"] = int(v[8 + nt])
     return out
 
 

@@ -281,6 +281,34 @@ def preprocess(wav, lengths, window, fb, cfg: StepConfig, dither_noise=None):
     return x, seq_len
 
 
+def specaugment_mask(length, T, nfilt, uniforms, freq_masks=2, freq_width=27, time_masks=5, time_width=0.05):
+    """SpecAugment mask, NeMo's vectorized form (SpectrogramAugmentation(use_vectorized_spec_augment=True),
+    the default at audio_preprocessing.py:490-520 -> SpecAugment._forward_vectorized / _apply_masks;
+    SURVEY.md Appendix A.2), with the torch.rand draws given as `uniforms` (B, 2 (time_masks +
+    freq_masks)) = per utterance [time widths | time starts | freq widths | freq starts].  Restated with
+    the same torch ops, dtypes and order as NeMo's _apply_masks: time axis first (width = time_width *
+    length clamped to T, per-utterance float), then frequency (int width).  Returns (B, T, nfilt) bool,
+    True = masked.  Parity unpinned against NeMo itself (its source is absent here); the formula is
+    SURVEY A.2's."""
+    length = torch.as_tensor(length, dtype=torch.int64)
+    u = torch.as_tensor(uniforms, dtype=torch.float32).reshape(length.shape[0], -1)
+    B = length.shape[0]
+    ut_w, ut_s = u[:, :time_masks], u[:, time_masks:2 * time_masks]
+    uf_w, uf_s = u[:, 2 * time_masks:2 * time_masks + freq_masks], u[:, 2 * time_masks + freq_masks:]
+    # axis 2 (time): width = clamp(width * length, max=axis_length).unsqueeze(1)
+    w_t = torch.clamp(time_width * length, max=T).unsqueeze(1)
+    mw = (ut_w * w_t).long()
+    ms = (ut_s * (length.unsqueeze(1) - mw)).long()
+    idx = torch.arange(T)
+    tmask = ((idx >= ms.unsqueeze(-1)) & (idx < (ms + mw).unsqueeze(-1))).any(dim=1)      # (B, T)
+    # axis 1 (freq): int width
+    fw = (uf_w * freq_width).long()
+    fs = (uf_s * (nfilt - fw)).long()
+    idf = torch.arange(nfilt)
+    fmask = ((idf >= fs.unsqueeze(-1)) & (idf < (fs + fw).unsqueeze(-1))).any(dim=1)      # (B, nfilt)
+    return tmask[:, :, None] | fmask[:, None, :]
+
+
 # ------------------------------------------------------------------------------------------
 # Encoder (conformer_encoder.py:549-850 + Appendix A.3-A.8)
 # ------------------------------------------------------------------------------------------

@@ -14,7 +14,7 @@ def _fake_engine(diffkd=False, grad=False):
     # the engine's device buffers, on the CPU here: losses [total, ctc, kl, recon, layer KD],
     # kd_terms [recon, kd_pre, fm_pre, kd_post, fm_post, diffkd]
     return types.SimpleNamespace(
-        cfg=types.SimpleNamespace(use_diffkd=diffkd),
+        cfg=types.SimpleNamespace(use_diffkd=diffkd, kd_model="diffm"),
         losses=torch.tensor([10.0, 6.0, 1.5, 0.25, 2.0]),
         kd_terms=torch.tensor([0.25, 0.0, 0.0, 0.0, 1.75, 0.5]),
         lr=torch.tensor([1e-3]), step=torch.tensor([7], dtype=torch.int64),
@@ -29,6 +29,24 @@ def test_step_metrics_keys_and_values():
     assert "v/diffkd" not in m and m["step"] == 7 and abs(m["lr"] - 1e-3) < 1e-9
     m = step_metrics(_fake_engine(diffkd=True, grad=True))
     assert m["v/diffkd"] == 0.5 and m["grad_norm"] == 4.0 and m["grad_nonfinite"] == 0
+
+
+def test_step_metrics_encfm_keys():
+    """kd_model 'encfm' (asr_train.py): train_ctc_loss, train_logit_kd_loss, train_flow_matching_loss,
+    train_router_loss (router_weight-scaled), router/batch_mean_sampling_steps_mean, train_loss
+    (:657-663, 770-777) from eng.encfm_stats = [flow, weighted router, sum, mean steps]; no v/* keys."""
+    eng = _fake_engine()
+    eng.cfg = types.SimpleNamespace(use_diffkd=False, kd_model="encfm", encfm_dynamic=True)
+    eng.encfm_stats = torch.tensor([3.0, 0.5, 3.5, 4.25])
+    m = step_metrics(eng)
+    assert list(m)[:6] == ["train_ctc_loss", "train_logit_kd_loss", "train_flow_matching_loss", "train_router_loss",
+                           "router/batch_mean_sampling_steps_mean", "train_loss"]
+    assert m["train_flow_matching_loss"] == 3.0 and m["train_router_loss"] == 0.5
+    assert m["router/batch_mean_sampling_steps_mean"] == 4.25 and m["train_loss"] == 10.0
+    assert not any(k.startswith("v/") for k in m) and m["step"] == 7 and abs(m["lr"] - 1e-3) < 1e-9
+    eng.cfg.encfm_dynamic = False
+    m = step_metrics(eng)
+    assert "train_router_loss" not in m and m["train_flow_matching_loss"] == 3.0
 
 
 def test_jsonl_logger_every_n(tmp_path):

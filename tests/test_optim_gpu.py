@@ -108,14 +108,26 @@ def test_grad_stats_and_nonfinite_skip():
     v = torch.zeros(n, device=dev)
     p0 = p.clone()
     step = torch.tensor([5], dtype=torch.int64, device=dev)
+    adam_base = torch.tensor([4], dtype=torch.int64, device=dev)
     lr = torch.zeros(1, device=dev)
-    K.adamw_noam(p, bad, m, v, step, 2.0, 176, 10, 1e-6, 0.9, 0.98, 1e-9, 1e-3, 1.0, lr_out=lr, gstats=out)
+    K.adamw_noam(p, bad, m, v, step, 2.0, 176, 10, 1e-6, 0.9, 0.98, 1e-9, 1e-3, 1.0, lr_out=lr, adam_base=adam_base,
+                 gstats=out)
     torch.cuda.synchronize()
     assert torch.equal(p, p0) and m.abs().max().item() == 0.0 and lr.item() > 0.0
+    # the skipped step does not count toward AdamW's bias correction: the next update at
+    # schedule step 6 is a fresh AdamW step 1 (torch.optim.AdamW counts only the steps it took)
+    assert adam_base.item() == 5
+    step.fill_(6)
     K.grad_stats(grad, 1.0, out)
-    K.adamw_noam(p, grad, m, v, step, 2.0, 176, 10, 1e-6, 0.9, 0.98, 1e-9, 1e-3, 1.0, lr_out=lr, gstats=out)
+    K.adamw_noam(p, grad, m, v, step, 2.0, 176, 10, 1e-6, 0.9, 0.98, 1e-9, 1e-3, 1.0, lr_out=lr, adam_base=adam_base,
+                 gstats=out)
     torch.cuda.synchronize()
-    assert not torch.equal(p, p0)
+    assert not torch.equal(p, p0) and adam_base.item() == 5
+    ref = p0.cpu().clone().requires_grad_(True)
+    opt = torch.optim.AdamW([ref], lr=lr.item(), betas=(0.9, 0.98), eps=1e-9, weight_decay=1e-3)
+    ref.grad = grad.cpu().clone()
+    opt.step()
+    torch.testing.assert_close(p.cpu(), ref.detach(), rtol=1e-5, atol=1e-6)
 
 
 def test_resumed_moments_restart_bias_correction():

@@ -4,7 +4,8 @@ reference's draws have:
 
 * SpecAugment (NeMo SpectrogramAugmentation, audio_preprocessing.py:443-553, called
   asr_train_diffm.py:622-623; recipe conformer_ctc_bpe.yaml:108-114:
-  2 frequency masks of width <= 27, 5 time masks of width <= 0.05*len): masked cells exactly 0,
+  2 frequency masks of width <= 27, 5 time masks of width <= 0.05*len): with injected uniforms the
+  masks equal the oracle's restatement of NeMo's vectorized form bit for bit; drawn on device, masked cells exactly 0,
   others untouched; the mask of an utterance is (frequency band set) x all frames  U  all bins x
   (time band set); at most 2 frequency runs (union width <= 54) and 5 time runs, time runs inside the
   valid length; mean widths match the uniform width draw; seeded (same seed -> same masks).
@@ -80,6 +81,40 @@ def test_specaugment_mask_structure():
     m3 = torch.empty_like(mask)
     K.specaugment(x0.clone(), lens.cuda(), B, T, nf, 2, 27, 5, 0.05, _seed(100), 5, mask_out=m3)
     assert torch.equal(m2, mask) and not torch.equal(m3, mask)
+
+
+def test_specaugment_injected_uniforms_match_oracle():
+    """Parity mode (RNG as an input): the kernel fed the same uniforms as the oracle's
+    restatement of NeMo's vectorized SpecAugment (oracle.ver5.specaugment_mask, A.2: time width
+    (int)(U min(0.05 len, T)), start (int)(U' (len - w)); freq width (int)(27 U), start (int)(U' (80 - w)))
+    gives the IDENTICAL mask, at ragged lengths (incl. lengths where 0.05 len crosses an integer, len < 20,
+    len = T) and edge uniforms (0, the largest float below 1, values landing on integer widths)."""
+    from kdfm import kernels as K
+    from oracle.ver5 import specaugment_mask
+    B, T, nf, fm, tm = 40, 1601, 80, 2, 5
+    g = torch.Generator().manual_seed(8)
+    lens = torch.randint(1, T + 1, (B,), generator=g)
+    lens[:8] = torch.tensor([T, 1, 19, 20, 21, 39, 40, 1580])
+    u = torch.rand(B, 2 * (fm + tm), generator=g)
+    below1 = torch.nextafter(torch.tensor(1.0), torch.tensor(0.0))
+    u[0] = below1
+    u[1] = 0.0
+    u[2, :tm] = 1.0 / (0.05 * 19)          # lands on width 1 before truncation
+    u[3, 2 * tm:2 * tm + fm] = 1.0 / 27     # freq width exactly 1 in f32 or just below
+    u[4, :] = below1
+    u[5, tm:2 * tm] = below1                # starts at the last admissible frame
+    x0 = torch.randn(B, T, nf, generator=g)
+    x = x0.cuda()
+    mask = torch.empty(B, T, nf, dtype=torch.uint8, device="cuda")
+    K.specaugment(x, lens.cuda(), B, T, nf, fm, 27, tm, 0.05, None, 0, mask_out=mask, uniforms=u.cuda())
+    torch.cuda.synchronize()
+    want = specaugment_mask(lens, T, nf, u, fm, 27, tm, 0.05)
+    got = mask.bool().cpu()
+    bad = (got != want).nonzero()
+    assert bad.numel() == 0, f"{bad.shape[0]} cells differ, first at (b, t, f) = {bad[0].tolist()}"
+    assert want.any()
+    xc = x.cpu()
+    assert torch.equal(xc[want], torch.zeros(int(want.sum()))) and torch.equal(xc[~want], x0[~want])
 
 
 def test_dropout_keep_rate_and_gemm_mask_agree():

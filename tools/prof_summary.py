@@ -1,7 +1,10 @@
 """Summarise a rocprofv3 kernel trace (rocpd .db or --output-format csv kernel_trace.csv): kernel
 time per step grouped by kernel (+GEMM template and grid).
 usage: python tools/prof_summary.py <run_results.db | run_kernel_trace.csv> [steps] [top]
-steps defaults to the number of CTC alpha/beta launches (one per training step)."""
+The step count is the number of fused AdamW launches the trace holds (one per optimizer step: the
+bench's eager warm-up, the recorded plan step, the warm-up and timed replays and the instrumented
+step all count); an explicit `steps` that disagrees with it is reported and ignored (a
+fixed "5" over a 9-step trace overstated every per-step figure 1.8x)."""
 import collections
 import csv
 import sqlite3
@@ -26,18 +29,20 @@ def main():
     nsteps = float(sys.argv[2]) if len(sys.argv) > 2 and float(sys.argv[2]) > 0 else None
     top = int(sys.argv[3]) if len(sys.argv) > 3 else 45
     agg = collections.defaultdict(lambda: [0, 0.0])
-    tot, nl, nctc = 0.0, 0, 0
+    tot, nl, nopt = 0.0, 0, 0
     for name, d, gx, gy, gz in rows(path):
         n = name.replace("kdfm::(anonymous namespace)::", "").replace("kdfm::", "")
-        if n.startswith(("ctc_kernel", "ctc_ab_kernel")) or "::ctc_kernel" in name or "ctc_ab_kernel" in name:
-            nctc += 1
+        if "adamw_kernel" in n:
+            nopt += 1
         tot += d
         nl += 1
         base = n.split("(")[0]
         key = base + (f" grid=({gx},{gy},{gz})" if "gemm" in n else "")
         agg[key][0] += 1
         agg[key][1] += d
-    nsteps = nsteps or max(nctc, 1)
+    if nopt and nsteps and nsteps != nopt:
+        print(f"note: {nsteps:g} steps given but the trace holds {nopt} optimizer steps; using {nopt}")
+    nsteps = nopt or nsteps or 1
     print(f"steps={nsteps:g}  total kernel time per step: {tot / nsteps / 1e6:.3f} ms  ({nl / nsteps:.0f} launches/step)")
     gemm = sum(v[1] for k, v in agg.items() if "gemm" in k)
     print(f"  gemm share: {gemm / tot * 100:.1f}%")

@@ -21,8 +21,10 @@ the caching allocator has meanwhile handed to a new tensor (a different generati
 only if the old owner's stream never recorded itself on it (Tensor.record_stream makes the allocator
 wait for that stream in real time before reuse, which no stream edge shows).
 
-Usage (on the GPU box):  python tools/race_check.py [--layers N] [--batch B] [--seconds S] [--steps K]
+Usage (on the GPU box):  python tools/race_check.py [--layers N] [--batch B] [--seconds S] [--steps K] [--diffkd]
 prints one line per distinct conflicting pair (issue site of both accesses) and exits 1 if any.
+tests/test_race_gpu.py runs it on the default overlapped schedule (KD heads in two layer halves, the
+bucketed all-reduce of a world of 2) with use_diffkd off and on.
 """
 from __future__ import annotations
 
@@ -475,7 +477,8 @@ def _on_aten(func, args, kwargs, out):
 # the scenario: the bench's overlapped bf16 step (+ the bucketed all-reduce of a world of 2)
 # ------------------------------------------------------------------------------------------------
 
-def run(layers=3, batch=8, seconds=16.0, steps=2, ddp=True, deterministic=False, math="bf16", verbose=True):
+def run(layers=3, batch=8, seconds=16.0, steps=2, ddp=True, deterministic=False, math="bf16", verbose=True,
+        diffkd=False):
     from dataclasses import replace
 
     from kdfm import kernels as K
@@ -484,7 +487,7 @@ def run(layers=3, batch=8, seconds=16.0, steps=2, ddp=True, deterministic=False,
     from kdfm.engine import Ver5Engine, synthetic_batch
     from kdfm.overlap import WGRAD
 
-    cfg = replace(DEFAULT, n_layers=layers, deterministic=deterministic, math=math)
+    cfg = replace(DEFAULT, n_layers=layers, deterministic=deterministic, math=math, use_diffkd=diffkd)
     dev = torch.device("cuda", 0)
     tr = Tracer()
     install(tr)
@@ -512,7 +515,8 @@ def run(layers=3, batch=8, seconds=16.0, steps=2, ddp=True, deterministic=False,
         torch.cuda.synchronize()
     if verbose:
         print(f"race_check: layers={layers} B={batch} {seconds}s steps={steps} ddp={ddp} math={math} "
-              f"deterministic={deterministic}: {tr.naccess} accesses, {len(tr.vc)} streams, "
+              f"deterministic={deterministic} diffkd={diffkd} heads_split={eng.heads_split}: {tr.naccess} accesses, "
+              f"{len(tr.vc)} streams, "
               f"{len(tr.conflicts)} conflicting site pairs")
     return tr
 
@@ -526,8 +530,9 @@ def main():
     ap.add_argument("--no-ddp", action="store_true")
     ap.add_argument("--math", default="bf16")
     ap.add_argument("--deterministic", action="store_true")
+    ap.add_argument("--diffkd", action="store_true")
     a = ap.parse_args()
-    tr = run(a.layers, a.batch, a.seconds, a.steps, not a.no_ddp, a.deterministic, a.math)
+    tr = run(a.layers, a.batch, a.seconds, a.steps, not a.no_ddp, a.deterministic, a.math, diffkd=a.diffkd)
     n = tr.report()
     sys.exit(1 if n else 0)
 

@@ -67,8 +67,22 @@ def main():
         print(f"  stream {q} top: " + "; ".join(f"{n[:40]} {t:.2f}" for n, t in top))
 
 
+def producer(step, main, t_prev_end, t_next, slack_us=8.0):
+    """The kernel a main-stream gap most likely waited for: the latest-ending kernel on another stream
+    that finished inside the gap and at most `slack_us` before the main stream resumed (a cross-stream
+    event wait resumes within a few microseconds of its producer's end).  None: nothing on another
+    stream ended right before the resume -- the gap is host issue (or a launch the trace cannot see)."""
+    best = None
+    for s, e, q, n in step:
+        if q != main and t_prev_end <= e <= t_next and (t_next - e) / 1e3 <= slack_us:
+            if best is None or e > best[0]:
+                best = (e, q, n)
+    return best
+
+
 def gaps(path, main_sid=None, min_us=30.0):
-    """Main-stream idle gaps inside the last full step, with the kernels other streams run during them."""
+    """Main-stream idle gaps inside the last full step, each attributed to the producer it waited on
+    (producer()): cross-stream waits summed per producer stream / kernel, the rest as host issue."""
     rows = load(path)
     ends = [e for s, e, q, n in rows if "adamw_kernel" in n]
     t0, t1 = ends[-3], ends[-2]
@@ -82,22 +96,34 @@ def gaps(path, main_sid=None, min_us=30.0):
     agg = defaultdict(float)
     prev_end, prev_name = t0, "step start"
     out = []
+    by_prod = defaultdict(float)
+    allgap = 0.0
     for s, e, n in mk:
         g = (s - prev_end) / 1e3
+        if g > 0:
+            allgap += g
         if g > min_us:
             others = defaultdict(float)
             for s2, e2, q2, n2 in step:
                 if q2 != main and e2 > prev_end and s2 < s:
                     others[f"{q2}:{n2[:28]}"] += (min(e2, s) - max(s2, prev_end)) / 1e3
             top = sorted(others.items(), key=lambda kv: -kv[1])[:3]
-            out.append((g, prev_name[:30], n[:30], top))
+            pr = producer(step, main, prev_end, s)
+            who = f"waits {pr[1]}:{pr[2][:34]}" if pr else "host issue"
+            by_prod[who] += g
+            out.append((g, prev_name[:30], n[:30], top, who))
             total += g
             for k, v in others.items():
                 agg[k.split(":")[0]] += v
         prev_end, prev_name = max(prev_end, e), n
-    print(f"main stream {main}: {len(out)} gaps > {min_us} us, {total / 1e3:.3f} ms total")
-    for g, a, b, top in sorted(out, key=lambda x: -x[0])[:15]:
-        print(f"  {g:8.1f} us after {a:30s} before {b:30s} | " + "; ".join(f"{k} {v:.0f}" for k, v in top))
+    span = (t1 - t0) / 1e6
+    print(f"main stream {main}: idle {allgap / 1e3:.3f} ms of the {span:.3f} ms step; {len(out)} gaps > {min_us} us, "
+          f"{total / 1e3:.3f} ms total")
+    print("  attributed (gaps > min_us), by producer:")
+    for who, g in sorted(by_prod.items(), key=lambda kv: -kv[1])[:20]:
+        print(f"    {g / 1e3:7.3f} ms  {who}")
+    for g, a, b, top, who in sorted(out, key=lambda x: -x[0])[:25]:
+        print(f"  {g:8.1f} us after {a:30s} before {b:30s} [{who}] | " + "; ".join(f"{k} {v:.0f}" for k, v in top))
 
 
 if __name__ == "__main__":
