@@ -212,6 +212,27 @@ int kdfm_relpos_attn_bwd(const float* dO, const float* O, const float* qu, const
                          const int64_t* lengths, float* dqu, float* dqv, float* dqkv, float* dpos,
                          float* ws, int64_t ws_len, int64_t B, int64_t H, int64_t T, int64_t d, float scale,
                          float dropout_p, const uint64_t* seed, uint64_t rng_stream, void* stream);
+/* The backward in three kernels over SAVED probabilities (bwd2; the forward then writes only lse):
+ *   _dq: r_i = dO_i . O_i into rsum (B*H*T floats), then dqu / dqv exactly as above, and the bf16 score
+ *        gradient dS and dropout-masked probabilities Pd = dropout(P) of every (i, j < len) written into
+ *        ds / pd, each (B, H, T, ldt) with ldt = kdfm_relpos_attn_bwd2_ldt(T) (T rounded up to 8; keys
+ *        >= len in the last written 64-key block are 0, key blocks past len and rows >= T unwritten);
+ *   _dkv: dV[key] = sum_q Pd[q][key] dO_q, dK[key] = sum_q dS[q][key] qu_q into dqkv[:, 2d:] / [:, d:] --
+ *        two plain products, no recompute of P, dP or the dropout mask;
+ *   _dpos: dpos[r] = sum_{b,i} dS[i][r-T+1+i] qv_i (2T-1, d, overwritten) over per-utterance-chunk
+ *        partials in ws (kdfm_relpos_attn_bwd2_dpos_ws floats) folded in chunk order.
+ * _dkv and _dpos only read ds / pd: they may run concurrently on two streams after _dq. */
+int64_t kdfm_relpos_attn_bwd2_ldt(int64_t T);
+int64_t kdfm_relpos_attn_bwd2_dpos_ws(int64_t B, int64_t T, int64_t d);
+int kdfm_relpos_attn_bwd2_dq(const float* dO, const float* O, const float* qu, const float* qv, const float* qkv,
+                             const float* pos, const float* lse, const int64_t* lengths, float* rsum, uint16_t* ds,
+                             uint16_t* pd, float* dqu, float* dqv, int64_t B, int64_t H, int64_t T, int64_t d,
+                             float scale, float dropout_p, const uint64_t* seed, uint64_t rng_stream, void* stream);
+int kdfm_relpos_attn_bwd2_dkv(const float* dO, const float* qu, const uint16_t* ds, const uint16_t* pd,
+                              const int64_t* lengths, float* dqkv, int64_t B, int64_t H, int64_t T, int64_t d,
+                              void* stream);
+int kdfm_relpos_attn_bwd2_dpos(const float* qv, const uint16_t* ds, const int64_t* lengths, float* dpos, float* ws,
+                               int64_t ws_len, int64_t B, int64_t H, int64_t T, int64_t d, void* stream);
 
 /* Fused Conformer macaron feed-forward block (replaces the LayerNorm + Linear(d,ff)+SiLU+dropout +
  * Linear(ff,d)+dropout+residual of ConformerLayer.forward's feed_forward1 / feed_forward2 half steps,
@@ -451,6 +472,20 @@ int kdfm_specaugment(float* x, const int64_t* seq_len, uint8_t* mask_out, int64_
  * frames >= len_in[b] read as zero (padding mask). */
 int kdfm_im2col_3x3s2(const float* X, const int64_t* len_in, float* cols, int64_t B, int64_t T1, int64_t F1,
                       int64_t C, void* stream);
+/* Striding subsampling forward in one kernel (bf16 MFMA; conformer_encoder.py:381-390, 635; A.3):
+ * y2 = mask2(ReLU(conv2(mask1(ReLU(conv1(mask0(mel))))))) with conv1 / conv2 = Conv2d(3x3, stride 2,
+ * pad 1), mel (B, Tm, F = 80) f32, y2 (B * T2 * 20, C) f32 channels-last rows; conv1 is computed on the
+ * fly per workgroup (MFMA over hi/lo bf16 splits of the mel taps and weights, f32 accumulation) and never
+ * leaves LDS, except that y1 (optional, (B * T1 * 40, C) bf16) receives the conv1 output for a trained
+ * student's backward.  mel_len / len1 / len2 (optional): the frame masks.  wp: kdfm_subsample_fused_wprep's
+ * operand image of (w0 (C,1,3,3), w2 (C,C,3,3)), kdfm_subsample_fused_wprep_elems(C) bf16.
+ * C in {88, 96, 176, 192} (kdfm_subsample_fused_supported). */
+int kdfm_subsample_fused_supported(int64_t C, int64_t F);
+int64_t kdfm_subsample_fused_wprep_elems(int64_t C);
+int kdfm_subsample_fused_wprep(const float* w0, const float* w2, uint16_t* wp, int64_t C, void* stream);
+int kdfm_subsample_fused(const float* mel, const int64_t* mel_len, const int64_t* len1, const int64_t* len2,
+                         const uint16_t* wp, const float* b0, const float* b2, float* y2, uint16_t* y1, int64_t B,
+                         int64_t Tm, int64_t F, int64_t C, void* stream);
 /* Tap-major bf16 columns: cols[(b,t2,f2), tap*C + c] = bf16(X[b, 2 t2 - 1 + ky, 2 f2 - 1 + kx, c]) (0 outside /
  * beyond len_in), C % 8 == 0; the bf16 step's conv2 weight-gradient operand. */
 /* the same tap-major bf16 columns from a bf16 source (the saved bf16 conv1 output y1) */

@@ -62,7 +62,11 @@ struct AbP {
   float scale, p_drop;
   const uint64_t* seed; uint64_t rng_stream;
   int bpc;   // batches per chunk (kernel 3)
+  // bwd2: dS and Pd (dropout-applied P) as bf16 (B, H, T, ldt), written by kernel 1, read by kernels 2b / 3b
+  uint16_t* ds; uint16_t* pdo; int64_t ldt;
 };
+
+constexpr uint32_t AB_OOB = 0x80000000u;   // buffer offset past every buffer: the access is dropped / reads 0
 
 typedef short v4s __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4s lds_v4s;
@@ -159,12 +163,15 @@ __global__ __launch_bounds__(256) void attn_rowdot_kernel(const float* __restric
 // ---------------------------------------------------------------------------------------------
 // kernel 1: dQu, dQv
 // ---------------------------------------------------------------------------------------------
-template <int NU>
+template <int NU, bool SAVE = false>
 __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dq_kernel(AbP p) {
   __shared__ __attribute__((aligned(16))) uint16_t Ks[BK * LR];     // K block [key][c]
   __shared__ __attribute__((aligned(16))) uint16_t Vs[BK * LR];     // V block [key][c]
   __shared__ __attribute__((aligned(16))) uint16_t Pr[PB1 * LR];    // Ppos band [band row][c]
   __shared__ __attribute__((aligned(16))) float Wsc[4][WS1 / 4];    // per-wave scratch
+  // SAVE (bwd2): per wave Pd tile [16][LW] bf16; dS and Pd leave as 16-byte buffer stores (fixed count per
+  // lane and key block, out-of-range chunks dropped by the range check)
+  __shared__ __attribute__((aligned(16))) uint16_t Pdw[SAVE ? 4 : 1][SAVE ? 16 * LW : 8];
 
   KPROBE(0);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -223,6 +230,9 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dq_kernel(AbP p
   float* G = Wsc[w];                                    // f32 score band [16][LG32]
   uint16_t* D = reinterpret_cast<uint16_t*>(Wsc[w]);    // bf16 dS [16][LW]   (after the scores)
   uint16_t* Gk = D + 16 * LW;                           // bf16 skewed dS [16][LG]
+  const int sbytes = SAVE ? (int)(p.B * p.H * p.T * p.ldt * 2) : 0;
+  const __amdgpu_buffer_rsrc_t rds = __builtin_amdgcn_make_buffer_rsrc((void*)p.ds, (short)0, sbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rpd = __builtin_amdgcn_make_buffer_rsrc((void*)p.pdo, (short)0, sbytes, 0x00020000);
   if (nkb > 0) fetch(0);
   KPROBE(1);
   for (int kb = 0; kb < nkb; ++kb) {
@@ -289,19 +299,40 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dq_kernel(AbP p
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int i = ib + r, j = j0 + 16 * t + (lane & 15);
-        float ds = 0.f;
+        float ds = 0.f, pdv = 0.f;
         if (i < len && j < len) {
           float g = a[t][r];
-          if (p.p_drop > 0.f)
-            g = dropout_keep(seed, p.rng_stream, (uint64_t)(prow0 + (int64_t)r * p.T + j), p.p_drop) ? g * keep : 0.f;
-          ds = __expf(s[t][r] - ls[r]) * (g - rs[r]) * p.scale;
+          bool kp = true;
+          if (p.p_drop > 0.f) {
+            kp = dropout_keep(seed, p.rng_stream, (uint64_t)(prow0 + (int64_t)r * p.T + j), p.p_drop);
+            g = kp ? g * keep : 0.f;
+          }
+          const float pe = __expf(s[t][r] - ls[r]);
+          ds = pe * (g - rs[r]) * p.scale;
+          pdv = kp ? pe * keep : 0.f;
         }
         const int ii = 4 * (lane >> 4) + r, jj = 16 * t + (lane & 15);
         const uint16_t bv = f2bf(ds);
         D[ii * LW + jj] = bv;
         Gk[ii * LG + jj - ii + 15] = bv;
+        if (SAVE) Pdw[w][ii * LW + jj] = f2bf(pdv);
       }
     wsync();
+    if (SAVE) {
+      // this wave's 16 rows x 64 keys of dS and Pd: 128 16-byte chunks each, two per lane
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int c = lane + 64 * q, row = c >> 3, c8 = c & 7;
+        const int i = i0 + w * 16 + row, jc = j0 + 8 * c8;
+        const uint32_t off = (i < T && jc < p.ldt) ? (uint32_t)(((bh * p.T + i) * p.ldt + jc) * 2) : AB_OOB;
+        const uint4 vd = *reinterpret_cast<const uint4*>(D + row * LW + 8 * c8);
+        const uint4 vp = *reinterpret_cast<const uint4*>(&Pdw[w][row * LW + 8 * c8]);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, vd), rds,
+                                               off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, vp), rpd,
+                                               off, 0, 0);
+      }
+    }
     KPROBE(4 + 4 * kb);
     // ---- dQu += dS K (K read transposed), dQv += skew(dS) Pband (band read transposed) ----
 #pragma unroll
@@ -648,6 +679,186 @@ __global__ __launch_bounds__(256) void attn_dpos_fold_kernel(const float* __rest
   dpos[e] = s;
 }
 
+// ---------------------------------------------------------------------------------------------
+// bwd2 kernel 2b: dK, dV as plain products over the saved bf16 dS and Pd (kernel 1 with SAVE):
+//   dV[key] += sum_q Pd[q][key] dO[q],  dK[key] += sum_q dS[q][key] Qu[q]
+// one workgroup per (b, h, 64 keys), 4 waves x 16 keys; per 64-query block the dO / Qu rows are staged
+// [query][c] and the Pd / dS tiles [query][key] as copied (16-byte loads of 128-byte row runs), all four
+// read TRANSPOSED into MFMA fragments (ds_read_b64_tr_b16).  No recompute of P, dP or the dropout mask.
+// ---------------------------------------------------------------------------------------------
+template <int NU>
+__global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dkv2_kernel(AbP p) {
+  __shared__ __attribute__((aligned(16))) uint16_t Os[BQ * LR];     // dO block [query][c]
+  __shared__ __attribute__((aligned(16))) uint16_t Qs[BQ * LR];     // Qu block [query][c]
+  __shared__ __attribute__((aligned(16))) uint16_t Pq[BQ * LW];     // Pd block [query][key]
+  __shared__ __attribute__((aligned(16))) uint16_t Dq[BQ * LW];     // dS block [query][key]
+
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int T = (int)p.T, dk = (int)p.dkh;
+  const Blk3 blk = xcd_block3();
+  const int64_t bh = blk.y;
+  const int64_t b = bh / p.H, h = bh - b * p.H;
+  const int j0 = (int)blk.x * BK;
+  const int len = p.lens ? (int)min<int64_t>(p.lens[b], p.T) : T;
+  const int64_t hoff = h * p.dkh;
+  zero_pad(Os, BQ, dk, BQ);
+  zero_pad(Qs, BQ, dk, BQ);
+  const int sbytes = (int)(p.B * p.H * p.T * p.ldt * 2);
+  const __amdgpu_buffer_rsrc_t rds = __builtin_amdgcn_make_buffer_rsrc((void*)p.ds, (short)0, sbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rpd = __builtin_amdgcn_make_buffer_rsrc((void*)p.pdo, (short)0, sbytes, 0x00020000);
+  f32x4 adv[NU], adk[NU];
+#pragma unroll
+  for (int u = 0; u < NU; ++u) { adv[u] = f32x4{0.f, 0.f, 0.f, 0.f}; adk[u] = adv[u]; }
+  const int nqb = (j0 < len) ? (len + BQ - 1) / BQ : 0;
+  typedef __attribute__((ext_vector_type(4))) uint32_t u32x4v;
+  float4 ndo[NU], nqu[NU];
+  u32x4v npd[2], nds[2];
+  // query rows >= len and keys >= len read as 0 (key columns past len inside a written block are 0
+  // already; whole rows >= len are dropped here)
+  auto fetch = [&](int qb) {
+    const int i0 = qb * BQ;
+    fetch_rows<NU>(ndo, p.dO, p.ldq, b * p.T, i0, BQ, 0, len, hoff, dk);
+    fetch_rows<NU>(nqu, p.qu, p.ldq, b * p.T, i0, BQ, 0, len, hoff, dk);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int c = threadIdx.x + 256 * q, row = c >> 3, c8 = c & 7;
+      const int i = i0 + row, jc = j0 + 8 * c8;
+      const uint32_t off = (i < len && jc < p.ldt) ? (uint32_t)(((bh * p.T + i) * p.ldt + jc) * 2) : AB_OOB;
+      npd[q] = __builtin_amdgcn_raw_buffer_load_b128(rpd, off, 0, 0);
+      nds[q] = __builtin_amdgcn_raw_buffer_load_b128(rds, off, 0, 0);
+    }
+  };
+  if (nqb > 0) fetch(0);
+  for (int qb = 0; qb < nqb; ++qb) {
+    __syncthreads();
+    put_rows<NU>(Os, nullptr, 0, ndo, BQ, dk);
+    put_rows<NU>(Qs, nullptr, 0, nqu, BQ, dk);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int c = threadIdx.x + 256 * q, row = c >> 3, c8 = c & 7;
+      *reinterpret_cast<u32x4v*>(Pq + row * LW + 8 * c8) = npd[q];
+      *reinterpret_cast<u32x4v*>(Dq + row * LW + 8 * c8) = nds[q];
+    }
+    __syncthreads();
+    if (qb + 1 < nqb) fetch(qb + 1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const bf16x8 pa = tr_frag(Pq, LW, ks * 32, 16 * w, lane);   // A[key][q] = Pd[q][key]
+      const bf16x8 da = tr_frag(Dq, LW, ks * 32, 16 * w, lane);
+#pragma unroll
+      for (int u = 0; u < NU; ++u) {
+        adv[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, tr_frag(Os, LR, ks * 32, 16 * u, lane), adv[u], 0, 0, 0);
+        adk[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, tr_frag(Qs, LR, ks * 32, 16 * u, lane), adk[u], 0, 0, 0);
+      }
+    }
+  }
+  const int jb = j0 + w * 16 + 4 * (lane >> 4);
+#pragma unroll
+  for (int u = 0; u < NU; ++u)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int j = jb + r, c = 16 * u + (lane & 15);
+      if (j < T && c < dk) {
+        const int64_t off = (b * p.T + j) * p.ldkv + hoff + c;
+        p.dv[off] = adv[u][r];
+        p.dk[off] = adk[u][r];
+      }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// bwd2 kernel 3b: per-chunk partials of dPpos[r] = sum_{b, i} dS[i][r - (T-1) + i] Qv_i over the saved bf16
+// dS: per (h, 64 positions, batch chunk), query steps of 32 rows; the dS band [32][96] of the step is
+// staged from HBM, the skewed A fragments and Qv^T read as kernel 3 does.
+// ---------------------------------------------------------------------------------------------
+template <int NU>
+__global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dpos2_kernel(AbP p) {
+  __shared__ __attribute__((aligned(16))) uint16_t Dl[NPQ * LDL];    // dS [i - ib0][j - jbase]
+  __shared__ __attribute__((aligned(16))) uint16_t Qt[BDK * LQ3];    // Qv^T [c][i - ib0]
+
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int T = (int)p.T, dk = (int)p.dkh;
+  const int npos = 2 * T - 1;
+  const Blk3 blk = xcd_block3();
+  const int r0 = (int)blk.x * 64;
+  const int64_t h = blk.y;
+  const int64_t bchunk = blk.z;
+  const int64_t hoff = h * p.dkh;
+  for (int e = threadIdx.x; e < (BDK - dk) * LQ3; e += 256) Qt[dk * LQ3 + e] = 0;
+  f32x4 acc[NU];
+#pragma unroll
+  for (int u = 0; u < NU; ++u) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int64_t b0 = bchunk * p.bpc;
+  const int64_t b1 = min<int64_t>(p.B, b0 + p.bpc);
+  auto ulen = [&](int64_t bb) { return p.lens ? (int)min<int64_t>(p.lens[bb], p.T) : T; };
+  auto advance = [&](int64_t& bb, int& ib, int& ln) -> bool {
+    ib += NPQ;
+    while (bb < b1) {
+      for (; ib < ln; ib += NPQ) {
+        const int jb = r0 - (T - 1) + ib;
+        if (!(jb + NPJ <= 0 || jb >= ln)) return true;
+      }
+      if (++bb >= b1) break;
+      ib = 0;
+      ln = ulen(bb);
+      if (ib < ln) {
+        const int jb = r0 - (T - 1) + ib;
+        if (!(jb + NPJ <= 0 || jb >= ln)) return true;
+      }
+    }
+    return false;
+  };
+  constexpr int NE = NPQ * NPJ / 256;   // dS elements per thread per step
+  float4 nqr[(NPQ * 4 * NU + 255) / 256];
+  uint16_t nd[NE];
+  auto fetch = [&](int64_t bb, int ib, int ln) {
+    const int jb = r0 - (T - 1) + ib;
+    const int64_t bhh = bb * p.H + h;
+    fetch_rows<(NPQ * 4 * NU + 255) / 256>(nqr, p.qv, p.ldq, bb * p.T, ib, NPQ, 0, ln, hoff, dk);
+#pragma unroll
+    for (int it = 0; it < NE; ++it) {
+      const int e = threadIdx.x + 256 * it;
+      const int il = e / NPJ, jl = e - il * NPJ;
+      const int i = ib + il, j = jb + jl;
+      nd[it] = (i < ln && j >= 0 && j < ln) ? p.ds[(bhh * p.T + i) * p.ldt + j] : (uint16_t)0;
+    }
+  };
+  int64_t b = b0;
+  int ib0 = -NPQ, len = b0 < b1 ? ulen(b0) : 0;
+  bool more = b0 < b1 && advance(b, ib0, len);
+  if (more) fetch(b, ib0, len);
+  while (more) {
+    __syncthreads();
+    put_rows<(NPQ * 4 * NU + 255) / 256>(nullptr, Qt, LQ3, nqr, NPQ, dk);
+#pragma unroll
+    for (int it = 0; it < NE; ++it) {
+      const int e = threadIdx.x + 256 * it;
+      const int il = e / NPJ, jl = e - il * NPJ;
+      Dl[il * LDL + jl] = nd[it];
+    }
+    __syncthreads();
+    more = advance(b, ib0, len);
+    if (more) fetch(b, ib0, len);
+    // dPpos[r0 + 16 w + m] += sum_i dS[i][(16 w + m) + i] Qv_i: A[m][k = i] = Dl[i][16 w + m + i]
+    const int m = lane & 15, kq = 8 * (lane >> 4);
+    bf16x8 fa;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) fa[e] = (short)Dl[(kq + e) * LDL + 16 * w + m + kq + e];
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      const bf16x8 qb = *reinterpret_cast<const bf16x8*>(Qt + (16 * u + (lane & 15)) * LQ3 + kq);
+      acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, qb, acc[u], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < NU; ++u)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int rr = r0 + 16 * w + 4 * (lane >> 4) + r, c = 16 * u + (lane & 15);
+      if (rr < npos && c < dk) p.dpos_part[(bchunk * npos + rr) * p.d + hoff + c] = acc[u][r];
+    }
+}
+
 constexpr int DPOS_MAX_CHUNKS = 64;   // dPpos partials: one chunk per utterance (up to 64)
 
 }  // namespace
@@ -737,6 +948,105 @@ int kdfm_relpos_attn_bwd_parts(const float* dO, const float* O, const float* qu,
   hipLaunchKernelGGL(attn_dpos_fold_kernel, dim3((unsigned)ceil_div(npos * d, 256)), dim3(256), 0, st, p.dpos_part,
                      dpos, npos * d, chunks);
   return check_launch("kdfm_relpos_attn_bwd(fold)");
+}
+
+int64_t kdfm_relpos_attn_bwd2_ldt(int64_t T) { return kdfm::ceil_div(T, 8) * 8; }
+
+int64_t kdfm_relpos_attn_bwd2_dpos_ws(int64_t B, int64_t T, int64_t d) {
+  return (B < kdfm::DPOS_MAX_CHUNKS ? B : (int64_t)kdfm::DPOS_MAX_CHUNKS) * (2 * T - 1) * d;
+}
+
+namespace kdfm {
+namespace {
+int ab2_setup(AbP& p, const float* qu, const float* qv, const float* qkv, const float* lse, const int64_t* lengths,
+              int64_t B, int64_t H, int64_t T, int64_t d, float scale, float dropout_p, const uint64_t* seed,
+              uint64_t rng_stream) {
+  KDFM_REQUIRE(H > 0 && d % H == 0, "d must be a multiple of H");
+  const int64_t dk = d / H;
+  KDFM_REQUIRE(dk <= 64 && dk % 4 == 0, "head dim must be a multiple of 4 and <= 64");
+  KDFM_REQUIRE(T > 0 && T <= 4096 && d % 4 == 0, "bad T / d");
+  KDFM_REQUIRE(dropout_p == 0.f || seed, "dropout needs a seed");
+  KDFM_REQUIRE(B * H * T * kdfm_relpos_attn_bwd2_ldt(T) * 2 < (1ll << 31), "dS / Pd larger than 2 GiB (buffer offsets)");
+  p = AbP{};
+  p.qu = qu; p.qv = qv; p.k = qkv ? qkv + d : nullptr; p.v = qkv ? qkv + 2 * d : nullptr; p.lse = lse;
+  p.lens = lengths;
+  p.B = B; p.H = H; p.T = T; p.d = d; p.dkh = dk; p.ldq = d; p.ldkv = 3 * d;
+  p.scale = scale; p.p_drop = dropout_p; p.seed = seed; p.rng_stream = rng_stream;
+  p.ldt = kdfm_relpos_attn_bwd2_ldt(T);
+  const int chunks = (int)(B < DPOS_MAX_CHUNKS ? B : DPOS_MAX_CHUNKS);
+  p.bpc = B > 0 ? (int)ceil_div(B, chunks) : 1;
+  return KDFM_OK;
+}
+}  // namespace
+}  // namespace kdfm
+
+int kdfm_relpos_attn_bwd2_dq(const float* dO, const float* O, const float* qu, const float* qv, const float* qkv,
+                             const float* pos, const float* lse, const int64_t* lengths, float* rsum, uint16_t* ds,
+                             uint16_t* pd, float* dqu, float* dqv, int64_t B, int64_t H, int64_t T, int64_t d,
+                             float scale, float dropout_p, const uint64_t* seed, uint64_t rng_stream, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(dO && O && qu && qv && qkv && pos && lse && rsum && ds && pd && dqu && dqv, "null pointer");
+  KDFM_REQUIRE((((uintptr_t)dO | (uintptr_t)qu | (uintptr_t)qv | (uintptr_t)qkv | (uintptr_t)pos | (uintptr_t)ds |
+                 (uintptr_t)pd) & 15) == 0, "operands must be 16-byte aligned");
+  AbP p;
+  int rc = ab2_setup(p, qu, qv, qkv, lse, lengths, B, H, T, d, scale, dropout_p, seed, rng_stream);
+  if (rc || B == 0) return rc;
+  p.dO = dO; p.pos = pos; p.rsum = rsum; p.dqu = dqu; p.dqv = dqv; p.ds = ds; p.pdo = pd;
+  hipStream_t st = as_stream(stream);
+  hipLaunchKernelGGL(attn_rowdot_kernel, dim3((unsigned)ceil_div(B * T * H, 4)), dim3(256), 0, st, dO, O, rsum, B, H, T,
+                     d, (int)p.dkh);
+  rc = check_launch("kdfm_relpos_attn_bwd2_dq(rowdot)");
+  if (rc) return rc;
+  if (p.dkh > 48)
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<4, true>), dim3((unsigned)ceil_div(T, BQ), (unsigned)(B * H)), dim3(256), 0, st, p);
+  else
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<3, true>), dim3((unsigned)ceil_div(T, BQ), (unsigned)(B * H)), dim3(256), 0, st, p);
+  return check_launch("kdfm_relpos_attn_bwd2_dq");
+}
+
+int kdfm_relpos_attn_bwd2_dkv(const float* dO, const float* qu, const uint16_t* ds, const uint16_t* pd,
+                              const int64_t* lengths, float* dqkv, int64_t B, int64_t H, int64_t T, int64_t d,
+                              void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(dO && qu && ds && pd && dqkv, "null pointer");
+  KDFM_REQUIRE((((uintptr_t)dO | (uintptr_t)qu | (uintptr_t)ds | (uintptr_t)pd) & 15) == 0,
+               "operands must be 16-byte aligned");
+  AbP p;
+  int rc = ab2_setup(p, qu, nullptr, nullptr, nullptr, lengths, B, H, T, d, 1.f, 0.f, nullptr, 0);
+  if (rc || B == 0) return rc;
+  p.dO = dO; p.ds = const_cast<uint16_t*>(ds); p.pdo = const_cast<uint16_t*>(pd);
+  p.dk = dqkv + d; p.dv = dqkv + 2 * d;
+  hipStream_t st = as_stream(stream);
+  if (p.dkh > 48)
+    hipLaunchKernelGGL(attn_bwd_dkv2_kernel<4>, dim3((unsigned)ceil_div(T, BK), (unsigned)(B * H)), dim3(256), 0, st, p);
+  else
+    hipLaunchKernelGGL(attn_bwd_dkv2_kernel<3>, dim3((unsigned)ceil_div(T, BK), (unsigned)(B * H)), dim3(256), 0, st, p);
+  return check_launch("kdfm_relpos_attn_bwd2_dkv");
+}
+
+int kdfm_relpos_attn_bwd2_dpos(const float* qv, const uint16_t* ds, const int64_t* lengths, float* dpos, float* ws,
+                               int64_t ws_len, int64_t B, int64_t H, int64_t T, int64_t d, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(qv && ds && dpos && ws, "null pointer");
+  KDFM_REQUIRE(ws_len >= kdfm_relpos_attn_bwd2_dpos_ws(B, T, d), "workspace too small (kdfm_relpos_attn_bwd2_dpos_ws)");
+  AbP p;
+  int rc = ab2_setup(p, nullptr, qv, nullptr, nullptr, lengths, B, H, T, d, 1.f, 0.f, nullptr, 0);
+  if (rc || B == 0) return rc;
+  p.ds = const_cast<uint16_t*>(ds); p.dpos_part = ws;
+  const int chunks = (int)(B < DPOS_MAX_CHUNKS ? B : DPOS_MAX_CHUNKS);
+  const int64_t npos = 2 * T - 1;
+  hipStream_t st = as_stream(stream);
+  if (p.dkh > 48)
+    hipLaunchKernelGGL(attn_bwd_dpos2_kernel<4>, dim3((unsigned)ceil_div(npos, 64), (unsigned)H, (unsigned)chunks),
+                       dim3(256), 0, st, p);
+  else
+    hipLaunchKernelGGL(attn_bwd_dpos2_kernel<3>, dim3((unsigned)ceil_div(npos, 64), (unsigned)H, (unsigned)chunks),
+                       dim3(256), 0, st, p);
+  rc = check_launch("kdfm_relpos_attn_bwd2_dpos");
+  if (rc) return rc;
+  hipLaunchKernelGGL(attn_dpos_fold_kernel, dim3((unsigned)ceil_div(npos * d, 256)), dim3(256), 0, st, p.dpos_part,
+                     dpos, npos * d, chunks);
+  return check_launch("kdfm_relpos_attn_bwd2_dpos(fold)");
 }
 
 }  // extern "C"

@@ -77,6 +77,12 @@ SIGNATURES: dict[str, tuple] = {
     "kdfm_relpos_attn_bwd_ws": (_i64, [_i64, _i64, _i64, _i64]),
     "kdfm_relpos_attn_bwd": (_i32, [P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, _i64, _i64, _i64, _i64, _i64, _f32, _f32, P,
                                     C.c_uint64, P]),
+    "kdfm_relpos_attn_bwd2_ldt": (_i64, [_i64]),
+    "kdfm_relpos_attn_bwd2_dpos_ws": (_i64, [_i64, _i64, _i64]),
+    "kdfm_relpos_attn_bwd2_dq": (_i32, [P, P, P, P, P, P, P, P, P, P, P, P, P, _i64, _i64, _i64, _i64, _f32, _f32, P,
+                                        C.c_uint64, P]),
+    "kdfm_relpos_attn_bwd2_dkv": (_i32, [P, P, P, P, P, P, _i64, _i64, _i64, _i64, P]),
+    "kdfm_relpos_attn_bwd2_dpos": (_i32, [P, P, P, P, P, _i64, _i64, _i64, _i64, _i64, P]),
     "kdfm_relpos_attn_bwd_parts": (_i32, [P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, _i64, _i64, _i64, _i64, _i64, _f32,
                                           _f32, P, C.c_uint64, _i32, P]),
     "kdfm_wgrad_bf16": (_i32, [P, P, P, _i64, P, _i64, _i64, _i64, _f32, P, _i64, P]),
@@ -141,6 +147,10 @@ SIGNATURES: dict[str, tuple] = {
     "kdfm_subsample_wprep": (_i32, [P, P, _i64, P]),
     "kdfm_subsample_conv1": (_i32, [P, P, P, P, P, P, P, _i64, _i64, _i64, _i64, P]),
     "kdfm_subsample_conv2": (_i32, [P, P, P, P, P, _i64, _i64, _i64, _i64, P]),
+    "kdfm_subsample_fused_supported": (_i32, [_i64, _i64]),
+    "kdfm_subsample_fused_wprep_elems": (_i64, [_i64]),
+    "kdfm_subsample_fused_wprep": (_i32, [P, P, P, _i64, P]),
+    "kdfm_subsample_fused": (_i32, [P, P, P, P, P, P, P, P, P, _i64, _i64, _i64, _i64, P]),
     "kdfm_ctc_greedy": (_i32, [P, _i64, P, P, P, P, _i64, _i64, _i64, _i64, _i32, P]),
     "kdfm_edit_distance": (_i64, [P, _i64, P, _i64]),
     "kdfm_layernorm_fwd": (_i32, [P, P, P, P, P, P, _i64, _i64, _f32, P]),

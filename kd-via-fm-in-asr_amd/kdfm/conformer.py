@@ -30,6 +30,10 @@ SITE_PRE = 15
 # bf16 math: attention backward through the fused kernels of csrc/attn_bwd.hip (KDFM_ATTN_BWD_FUSED=0:
 # the unfused dPd / dAC / dBD path; the f32 parity mode always takes it)
 _ATTN_BWD_FUSED = __import__("os").environ.get("KDFM_ATTN_BWD_FUSED", "1") == "1"
+# ...in the bwd2 form (default): the forward saves only the per-row log-sum-exp, the dQ kernel writes the bf16
+# score gradient dS and dropped-out probabilities Pd, and dK / dV / dPpos are plain products over them
+# (KDFM_ATTN_BWD2=0: the forward saves bf16 p~ and block maxima, dK / dV / dPpos recompute dS from them)
+_ATTN_BWD2 = __import__("os").environ.get("KDFM_ATTN_BWD2", "1") == "1"
 
 
 def _stream(salt, layer, site):
@@ -167,6 +171,11 @@ def dw_subsampling_backward(cfg, S: EncoderShapes, P, G, pre, ctx, dx, *, seed, 
                        B, S.Tm, cfg.nfilt, 1, C, T1, F1, S.pad)
 
 
+# KDFM_SS_ONE_KERNEL=0: the two-kernel striding forward (conv1 to HBM, implicit-GEMM conv2) instead of the
+# one-kernel form
+_SS_ONE_KERNEL = __import__("os").environ.get("KDFM_SS_ONE_KERNEL", "1") == "1"
+
+
 def subsampling_forward(cfg, S: EncoderShapes, P, pre, mel, mel_len, len1, len2, *, train, seed, salt, save, ws):
     if cfg.subsampling == "dw_striding":
         return dw_subsampling_forward(cfg, S, P, pre, mel, mel_len, len1, train=train, seed=seed, salt=salt,
@@ -178,7 +187,18 @@ def subsampling_forward(cfg, S: EncoderShapes, P, pre, mel, mel_len, len1, len2,
     m0 = mel_len if cfg.subsampling_mask else None
     m1 = len1 if cfg.subsampling_mask else None
     m2 = len2 if cfg.subsampling_mask else None
-    if K.get_math() == "bf16" and C % 8 == 0 and C <= 192:
+    if K.get_math() == "bf16" and _SS_ONE_KERNEL and "ss_fused_w" in ws and S.F2 * 4 == cfg.nfilt:
+        # one kernel (csrc/ssfused.hip): conv1 computed per workgroup into LDS (MFMA over hi/lo bf16 splits),
+        # conv2 as an implicit GEMM over it; y1 reaches HBM only as the trained student's bf16 side output
+        # (the backward's ReLU' sign and conv2 weight-gradient columns)
+        y1b = torch.empty(B * S.T1 * S.F1, C, device=dev, dtype=torch.bfloat16) if save else None
+        wp = ws["ss_fused_w"]
+        K.subsample_fused_wprep(P[pre + "pre_encode.conv.0.weight"], P[pre + "pre_encode.conv.2.weight"], wp)
+        K.subsample_fused(mel, m0, m1, m2, wp, P[pre + "pre_encode.conv.0.bias"], P[pre + "pre_encode.conv.2.bias"],
+                          y2, y1b, B, S.Tm, cfg.nfilt, C)
+        y1 = y1b
+        del y1b
+    elif K.get_math() == "bf16" and C % 8 == 0 and C <= 192:
         # fused: direct conv1 (+ReLU+masks) -> bf16 y1, implicit-GEMM conv2 (+bias+ReLU+mask); no
         # im2col matrix.  The backward keeps the same bf16 y1: its ReLU' needs only the sign and the conv2
         # weight gradient's columns are bf16 anyway (an f32 copy would be 2x the bytes, written and re-read).
@@ -411,7 +431,10 @@ def layer_forward(cfg, S: EncoderShapes, P, L, li, x, out, pos_emb, lengths, *, 
             # recomputes P tile by tile from it) and the bf16 unnormalised p~ with its per-block maxima
             # (dK / dV and dPpos read P from them); dropout masks are regenerated from the counter RNG
             Pm = Pd = None
-            lse, pt, mblk = K.attn_saved(B, H, T, dev) if save else (None, None, None)
+            if _ATTN_BWD2:
+                lse, pt, mblk = (torch.empty(B, H, T, device=dev) if save else None), None, None
+            else:
+                lse, pt, mblk = K.attn_saved(B, H, T, dev) if save else (None, None, None)
         else:
             Pm = _empty(B, H, T, T, dev=dev) if save else None
             Pd = (_empty(B, H, T, T, dev=dev) if pa > 0 else Pm) if save else None
@@ -673,8 +696,24 @@ def layer_backward(cfg, S: EncoderShapes, P, G, L, li, ctx, dout, pos_emb, lengt
         st_att = _stream(salt, li, SITE_ATT_P)
         # the positional-term gradient dPpos feeds only the linear_pos weight gradient: it runs on the
         # weight-gradient stream beside the dQ / dK,dV kernels the main stream needs next
-        abws = torch.empty(K.relpos_attn_bwd_ws(B, H, T, d), device=dev)
         lse, pt, mblk = ctx["lse"], ctx["pt"], ctx["mblk"]
+        if pt is None:   # bwd2
+            rsum = torch.empty(B * H * T, device=dev)
+            dS, Pdr = K.attn_bwd2_saved(B, H, T, dev)
+            K.relpos_attn_bwd2_dq(do, ctx["o"], qu, qv, qkv, ppos, lse, lengths, rsum, dS, Pdr, dqu, dqv, B, H, T, sc,
+                                  ctx["pa"], seed, st_att)
+            del rsum
+            dpws = torch.empty(K.relpos_attn_bwd2_dpos_ws(B, T, d), device=dev)
+
+            def dpos_and_wgrad2():
+                K.relpos_attn_bwd2_dpos(qv, dS, lengths, dppos, B, H, T, ws=dpws)
+                K.linear_dw(dppos, pos_emb, G[L + "self_attn.linear_pos.weight"])
+            WGRAD.run(dpos_and_wgrad2, qv, dS, dppos, dpws, pos_emb, lengths)
+            K.relpos_attn_bwd2_dkv(do, qu, dS, Pdr, lengths, dqkv, B, H, T)
+            del do, Pdr, dS
+            return _attn_bwd_tail(P, G, L, ctx, dqkv, dqu, dqv, None, pos_emb, dx2, lng, cfg, pd, seed, salt, li, rows,
+                                  d, dev)
+        abws = torch.empty(K.relpos_attn_bwd_ws(B, H, T, d), device=dev)
         K.relpos_attn_bwd(do, ctx["o"], qu, qv, qkv, ppos, lse, pt, mblk, lengths, dqu, dqv, dqkv, None, B, H, T, sc,
                           ctx["pa"], seed, st_att, parts=K.ATTN_BWD_ROWDOT | K.ATTN_BWD_DQ | K.ATTN_BWD_DKV, ws=abws)
         o_ = ctx["o"]
@@ -908,4 +947,6 @@ def make_workspace(S: EncoderShapes, dev):
         ws["w2_tapmajor"] = torch.empty(S.d, 9, S.d, device=dev)
         ws["w2_dgrad"] = torch.empty(K.subsample_dgrad_wprep_elems(S.d), device=dev, dtype=torch.bfloat16)
         ws["w2_tapmajor_grad"] = torch.empty(S.d, 9, S.d, device=dev)
+        if K.subsample_fused_supported(S.d):
+            ws["ss_fused_w"] = torch.empty(K.subsample_fused_wprep_elems(S.d), device=dev, dtype=torch.bfloat16)
     return ws

@@ -1035,6 +1035,36 @@ def subsample_conv2(y1b, len2, wb, b2, y2, B, T1, F1, Cc):
     call("kdfm_subsample_conv2", ptr(y1b), ptr(_i64(len2)), ptr(wb), ptr(_f32(b2)), ptr(_f32(y2)), B, T1, F1, Cc, _s())
 
 
+def subsample_fused_supported(Cc, F=80):
+    return bool(_lib.lib().kdfm_subsample_fused_supported(int(Cc), int(F)))
+
+
+def subsample_fused_wprep_elems(Cc):
+    return int(_lib.lib().kdfm_subsample_fused_wprep_elems(Cc))
+
+
+def subsample_fused_wprep(w0, w2, wp):
+    """conv1 (C, 1, 3, 3) and conv2 (C, C, 3, 3) f32 weights -> the bf16 operand image of
+    kdfm_subsample_fused (conv1 as hi/lo bf16 splits, conv2 as [tap][chunk][co][32 ci] slabs)."""
+    Cc = w2.shape[0]
+    assert w0.numel() == Cc * 9 and w2.numel() == Cc * Cc * 9 and wp.dtype == torch.bfloat16
+    assert wp.numel() >= subsample_fused_wprep_elems(Cc)
+    call("kdfm_subsample_fused_wprep", ptr(_f32(w0)), ptr(_f32(w2)), ptr(wp), Cc, _s())
+
+
+def subsample_fused(mel, mel_len, len1, len2, wp, b0, b2, y2, y1, B, Tm, F, Cc):
+    """Striding subsampling forward in one kernel: y2 (B*T2*F2, C) f32; y1 (optional, (B*T1*F1, C) bf16)
+    receives the conv1 output (kdfm_subsample_fused)."""
+    T1, F1 = (Tm - 1) // 2 + 1, (F - 1) // 2 + 1
+    T2, F2 = (T1 - 1) // 2 + 1, (F1 - 1) // 2 + 1
+    assert mel.numel() == B * Tm * F and mel.is_contiguous() and wp.dtype == torch.bfloat16
+    assert y2.numel() == B * T2 * F2 * Cc and y2.is_contiguous()
+    assert y1 is None or (y1.dtype == torch.bfloat16 and y1.numel() == B * T1 * F1 * Cc)
+    assert b0.numel() == Cc and b2.numel() == Cc
+    call("kdfm_subsample_fused", ptr(_f32(mel)), ptr(_i64(mel_len)), ptr(_i64(len1)), ptr(_i64(len2)), ptr(wp),
+         ptr(_f32(b0)), ptr(_f32(b2)), ptr(_f32(y2)), ptr(y1), B, Tm, F, Cc, _s())
+
+
 def subsample_dgrad_wprep_elems(Cc):
     return int(_lib.lib().kdfm_subsample_dgrad_wprep_elems(Cc))
 
@@ -1177,6 +1207,59 @@ def relpos_attn_bwd(do, o, qu, qv, qkv, ppos, lse, p_tilde, m_blk, lengths, dqu,
     _traced("attn_bwd", fl, nb, "kdfm_relpos_attn_bwd", ptr(do), ptr(o), ptr(qu), ptr(qv), ptr(qkv), ptr(ppos),
             ptr(lse), ptr(p_tilde), ptr(m_blk), ptr(_i64(lengths)), ptr(dqu), ptr(dqv), ptr(dqkv), ptr(dppos),
             ptr(ws), ws.numel(), B, H, T, d, float(scale), float(p), ptr(seed), int(rng_stream), _s())
+
+
+def attn_bwd2_saved(B, H, T, device):
+    """bwd2's saved T x T operands, written by relpos_attn_bwd2_dq: dS and Pd, each (B, H, T, ldt) bf16."""
+    ldt = int(_lib.lib().kdfm_relpos_attn_bwd2_ldt(T))
+    return (torch.empty(B, H, T, ldt, dtype=torch.bfloat16, device=device),
+            torch.empty(B, H, T, ldt, dtype=torch.bfloat16, device=device))
+
+
+def relpos_attn_bwd2_dq(do, o, qu, qv, qkv, ppos, lse, lengths, rsum, ds, pd, dqu, dqv, B, H, T, scale, p, seed,
+                        rng_stream):
+    """bwd2 part 1 (csrc/attn_bwd.hip): row sums r_i = dO_i . O_i into rsum (B*H*T), dqu / dqv, and the bf16
+    dS / Pd (attn_bwd2_saved) the _dkv / _dpos parts read."""
+    rows, d = do.shape
+    assert rows == B * T and qkv.shape == (rows, 3 * d) and lse.shape == (B, H, T) and o.shape == do.shape
+    assert rsum.numel() >= B * H * T and ds.dtype == torch.bfloat16 and pd.dtype == torch.bfloat16
+    assert ds.shape == pd.shape and ds.shape[:3] == (B, H, T) and ds.is_contiguous() and pd.is_contiguous()
+    for t in (do, o, qu, qv, qkv, ppos, lse, dqu, dqv):
+        assert t.is_contiguous()
+    dk = d // H
+    tt = 2.0 * B * H * T * T * dk
+    # scores (QK^T + band), dP, dQu, dQv: 5 T x T products; bytes: dO, O, qu, qv, K, V read, dqu, dqv written,
+    # dS and Pd written (bf16)
+    _traced("attn_bwd", 5 * tt, 4.0 * rows * d * 8 + 2.0 * 2.0 * B * H * T * T, "kdfm_relpos_attn_bwd2_dq", ptr(do),
+            ptr(o), ptr(qu), ptr(qv), ptr(qkv), ptr(ppos), ptr(lse), ptr(_i64(lengths)), ptr(rsum), ptr(ds), ptr(pd),
+            ptr(dqu), ptr(dqv), B, H, T, d, float(scale), float(p), ptr(seed), int(rng_stream), _s())
+
+
+def relpos_attn_bwd2_dkv(do, qu, ds, pd, lengths, dqkv, B, H, T):
+    """bwd2 part 2: dK / dV into dqkv[:, d:] / [:, 2d:] from the saved dS / Pd (no recompute)."""
+    rows, d = do.shape
+    assert dqkv.shape == (rows, 3 * d) and dqkv.is_contiguous() and do.is_contiguous() and qu.is_contiguous()
+    tt = 2.0 * B * H * T * T * (d // H)
+    _traced("attn_bwd", 2 * tt, 4.0 * rows * d * 4 + 2.0 * 2.0 * B * H * T * T, "kdfm_relpos_attn_bwd2_dkv", ptr(do),
+            ptr(qu), ptr(ds), ptr(pd), ptr(_i64(lengths)), ptr(dqkv), B, H, T, d, _s())
+
+
+def relpos_attn_bwd2_dpos_ws(B, T, d):
+    return int(_lib.lib().kdfm_relpos_attn_bwd2_dpos_ws(B, T, d))
+
+
+def relpos_attn_bwd2_dpos(qv, ds, lengths, dppos, B, H, T, ws=None):
+    """bwd2 part 3: dppos (2T-1, d) from the saved dS and qv (ordered per-utterance-chunk fold)."""
+    rows, d = qv.shape
+    assert dppos.shape == (2 * T - 1, d) and dppos.is_contiguous() and qv.is_contiguous()
+    n = relpos_attn_bwd2_dpos_ws(B, T, d)
+    if ws is None:
+        ws = scratch(qv.device, n)
+    assert ws.numel() >= n
+    tt = 2.0 * B * H * T * T * (d // H)
+    _traced("attn_bwd", tt, 4.0 * rows * d + 2.0 * B * H * T * T + 4.0 * (2 * T - 1) * d,
+            "kdfm_relpos_attn_bwd2_dpos", ptr(qv), ptr(ds), ptr(_i64(lengths)), ptr(dppos), ptr(ws), ws.numel(), B, H,
+            T, d, _s())
 
 
 def relpos_attn_fwd(qu, qv, qkv, ppos, lengths, o, P, Pd, B, H, T, scale, p, seed, rng_stream, lse=None, p_tilde=None,

@@ -185,3 +185,87 @@ def test_attn_bwd_parts_on_two_streams_match_one_launch():
     torch.cuda.synchronize()
     for got, want in zip((dqu, dqv, dqkv[:, d:2 * d], dqkv[:, 2 * d:], dpos), ref[2:]):
         assert torch.equal(got, want)
+
+
+def _bwd2(K, qkv, qu, qv, ppos, do, lens, B, H, T, d, p, seed, two_streams=False):
+    """bwd2: lse-only single-pass forward, then _dq (writes the bf16 dS / Pd), _dkv and _dpos (optionally
+    on a second stream, as the engine runs it); returns (O, lse, dS, Pd, grads...)."""
+    dk = d // H
+    lse = torch.empty(B, H, T, device="cuda")
+    o = torch.empty(B * T, d, device="cuda")
+    K.relpos_attn_fwd(qu, qv, qkv, ppos, lens, o, None, None, B, H, T, 1.0 / math.sqrt(dk), p, seed, 11, lse=lse)
+    dqu = torch.empty(B * T, d, device="cuda")
+    dqv = torch.empty_like(dqu)
+    dqkv = torch.zeros(B * T, 3 * d, device="cuda")
+    dpos = torch.empty(2 * T - 1, d, device="cuda")
+    rsum = torch.empty(B * H * T, device="cuda")
+    dS, Pd = K.attn_bwd2_saved(B, H, T, "cuda")
+    K.relpos_attn_bwd2_dq(do, o, qu, qv, qkv, ppos, lse, lens, rsum, dS, Pd, dqu, dqv, B, H, T, 1.0 / math.sqrt(dk), p,
+                          seed, 11)
+    if two_streams:
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            K.relpos_attn_bwd2_dpos(qv, dS, lens, dpos, B, H, T)
+    else:
+        K.relpos_attn_bwd2_dpos(qv, dS, lens, dpos, B, H, T)
+    K.relpos_attn_bwd2_dkv(do, qu, dS, Pd, lens, dqkv, B, H, T)
+    if two_streams:
+        torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    return o, lse, dS, Pd, dqu, dqv, dqkv[:, d:2 * d], dqkv[:, 2 * d:], dpos
+
+
+@pytest.mark.parametrize("B,H,T,d", [(3, 2, 401, 88), (2, 4, 130, 176), (2, 2, 77, 88), (2, 8, 201, 512),
+                                     (2, 2, 77, 128)])
+def test_attn_bwd2_matches_float64(B, H, T, d):
+    """bwd2 (the dQ kernel saves bf16 dS and Pd; dK / dV / dPpos are plain products over them) against
+    float64 autograd: rel. Frobenius <= 2e-2 per gradient; the saved Pd equals the float64 P on every
+    valid (query, key) (no dropout: max |diff| <= 1e-2 max P + 1e-3); keys past a length get exactly zero
+    dK / dV."""
+    from kdfm import kernels as K
+    qkv, qu, qv, ppos, do, lens = _inputs(B, H, T, d, T + d + 1)
+    seed = torch.tensor([98], dtype=torch.int64, device="cuda")
+    _, _, dS, Pd, dqu, dqv, dk_, dv_, dpos = _bwd2(K, qkv, qu, qv, ppos, do, lens, B, H, T, d, 0.0, seed)
+    ref = _torch_grads(qkv, qu, qv, ppos, do, lens, B, H, T, d)
+    for name, got, want in zip(("dQu", "dQv", "dK", "dV", "dPpos"), (dqu, dqv, dk_, dv_, dpos), ref):
+        assert _rel(got, want) <= 2e-2, (name, _rel(got, want))
+    for bi in range(B):
+        L = int(lens[bi])
+        pw = _torch_grads.P[bi, :, :L, :L]
+        perr = (Pd[bi, :, :L, :L].double() - pw).abs().max().item()
+        assert perr <= 1e-2 * pw.abs().max().item() + 1e-3, (bi, perr)
+        if L < T:
+            assert dk_.view(B, T, d)[bi, L:].abs().max().item() == 0.0
+            assert dv_.view(B, T, d)[bi, L:].abs().max().item() == 0.0
+
+
+def test_attn_bwd2_matches_bwd1_with_dropout():
+    """With attention dropout 0.1 the bwd2 gradients equal the recompute backward's (same counter-RNG mask)
+    to bf16 level (rel. Frobenius <= 1e-2), the saved Pd is exactly 0 where the mask drops a valid
+    probability and P / (1 - p) elsewhere (the recompute path's P to bf16 precision), dPpos on a second
+    stream is bitwise the one-stream result, and two runs are bitwise identical."""
+    from kdfm import kernels as K
+    B, H, T, d, p = 3, 2, 401, 88, 0.1
+    qkv, qu, qv, ppos, do, lens = _inputs(B, H, T, d, 6)
+    seed = torch.tensor([4243], dtype=torch.int64, device="cuda")
+    one = _bwd2(K, qkv, qu, qv, ppos, do, lens, B, H, T, d, p, seed)
+    two = _bwd2(K, qkv, qu, qv, ppos, do, lens, B, H, T, d, p, seed, two_streams=True)
+    for a, b in zip(one[4:], two[4:]):
+        assert torch.equal(a, b), "bwd2 is not bitwise reproducible / stream-order independent"
+    (lse1, pt, mblk), o1, *g1 = _fused(K, qkv, qu, qv, ppos, do, lens, B, H, T, d, p, seed)
+    for name, got, want in zip(("dQu", "dQv", "dK", "dV", "dPpos"), one[4:], g1):
+        assert _rel(got, want) <= 1e-2, (name, _rel(got, want))
+    assert torch.equal(one[0], o1) and torch.equal(one[1], lse1)
+    Pd = one[3]
+    for bi in range(B):
+        L = int(lens[bi])
+        kb = torch.arange(L, device="cuda") // 64
+        prec = pt[bi, :, :L, :L].float() * torch.exp(mblk[bi, :, :L][:, :, kb] - lse1[bi, :, :L, None])
+        got = Pd[bi, :, :L, :L].float()
+        dropped = got == 0
+        frac = (dropped & (prec > 1e-20)).double().sum().item() / max(1.0, (prec > 1e-20).double().sum().item())
+        assert 0.07 < frac < 0.13, frac
+        kept = ~dropped
+        err = (got[kept] - prec[kept] / (1 - p)).abs().max().item()
+        assert err <= 2e-2 * (prec.max().item() / (1 - p)) + 1e-3, (bi, err)

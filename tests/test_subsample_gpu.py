@@ -73,6 +73,69 @@ def test_subsample_fused_forward(K, C):
     assert err <= 2e-3 * ref.abs().max().item() + 1e-6, err
 
 
+@pytest.mark.parametrize("C,Tm,lens", [(88, 57, (57, 40, 23)), (176, 57, (57, 40, 23)), (96, 200, (200, 199, 17)),
+                                        (192, 73, (73, 8, 3)), (176, 1601, (1601, 1000, 333)),
+                                        (88, 1601, (1601, 1600, 5))])
+def test_subsample_one_kernel_forward(K, C, Tm, lens):
+    """kdfm_subsample_fused (conv1 on the fly in LDS by hi/lo-split bf16 MFMA, conv2 implicit GEMM):
+    * y1 (the student's side output) against the f32 conv1 of the masked mel rounded to bf16: the f32
+      values agree to ~2^-16 relative, so every bf16 y1 is the reference's or its bf16 neighbour (ties
+      at a rounding boundary), >= 99 % exactly equal, masked rows / padding exactly 0;
+    * y2 against float64 conv2d(stride 2, pad 1) of the kernel's own bf16 y1 with the bf16 weights,
+      + bias, ReLU, len2 mask: max error <= 1e-4 of max |ref| (f32 accumulation order only);
+    * the teacher form (no y1 output) gives the identical y2 bit for bit.
+    Shapes: output rows not a multiple of the 8-row workgroup strip, the bench utterance (T_mel 1601),
+    ragged lengths down to a 3-frame utterance."""
+    g = torch.Generator().manual_seed(C + Tm)
+    B, Fq = 3, 80
+    mel = torch.randn(B, Tm, Fq, generator=g)
+    mel_len = torch.tensor(lens, dtype=torch.int64)
+    len1 = _lens(mel_len)
+    len2 = _lens(len1)
+    w0 = torch.randn(C, 1, 3, 3, generator=g) * 0.3
+    b0 = torch.randn(C, generator=g) * 0.1
+    w2 = torch.randn(C, C, 3, 3, generator=g) * (1.0 / (3 * C ** 0.5))
+    b2 = torch.randn(C, generator=g) * 0.1
+    T1, F1 = _lens(Tm), _lens(Fq)
+    T2, F2 = _lens(T1), _lens(F1)
+    dev = "cuda"
+    wp = torch.empty(K.subsample_fused_wprep_elems(C), device=dev, dtype=torch.bfloat16)
+    K.subsample_fused_wprep(w0.cuda(), w2.cuda(), wp)
+    y1 = torch.full((B * T1 * F1, C), float("nan"), device=dev).bfloat16()
+    y2 = torch.full((B * T2 * F2, C), float("nan"), device=dev)
+    args = (mel.cuda(), mel_len.cuda(), len1.cuda(), len2.cuda(), wp, b0.cuda(), b2.cuda())
+    K.subsample_fused(*args, y2, y1, B, Tm, Fq, C)
+    y2t = torch.full_like(y2, float("nan"))
+    K.subsample_fused(*args, y2t, None, B, Tm, Fq, C)
+    torch.cuda.synchronize()
+    assert torch.equal(y2, y2t)
+    # conv1 reference (f32, masked)
+    x = mel.clone()
+    for b in range(B):
+        x[b, mel_len[b]:] = 0
+    r1 = F.relu(F.conv2d(x.double()[:, None], w0.double(), b0.double(), stride=2, padding=1))
+    for b in range(B):
+        r1[b, :, len1[b]:] = 0
+    r1 = r1.permute(0, 2, 3, 1).reshape(B * T1 * F1, C)
+    got1 = y1.float().cpu()
+    assert torch.isfinite(got1).all()
+    d = (got1.double() - r1).abs()
+    assert (d <= 2.0 ** -7 * r1.abs() + 1e-6).all(), d.max().item()
+    exact = (got1 == r1.float().bfloat16().float()).double().mean().item()
+    assert exact >= 0.99, exact
+    assert got1[r1 == 0].abs().max().item() == 0.0
+    # conv2 reference on the kernel's own bf16 y1 and the bf16 weights
+    y1d = got1.double().view(B, T1, F1, C).permute(0, 3, 1, 2)
+    r2 = F.relu(F.conv2d(y1d, _bf(w2).double(), b2.double(), stride=2, padding=1))
+    for b in range(B):
+        r2[b, :, len2[b]:] = 0
+    r2 = r2.permute(0, 2, 3, 1).reshape(B * T2 * F2, C)
+    got2 = y2.cpu().double()
+    assert torch.isfinite(got2).all()
+    err = (got2 - r2).abs().max().item()
+    assert err <= 1e-4 * r2.abs().max().item() + 1e-6, err
+
+
 def test_subsample_bench_shape_matches_im2col_path(K):
     """The fused path and the im2col+GEMM path (kept for f32 parity mode) agree at the bench shape
     of one utterance (T_mel = 1601, d = 176)."""

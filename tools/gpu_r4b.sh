@@ -1,8 +1,11 @@
 set -o pipefail
 mkdir -p gpurun_out/r4b
 export TMPDIR=/tmp
-timeout -k 10 400 python -u -m pytest -v --timeout 120 --timeout-method thread tests/test_race_gpu.py tests/test_training_rng_gpu.py tests/test_ddp_overlap_nondet_gpu.py tests/test_optim_gpu.py tests/test_determinism_gpu.py tests/test_step_parity_gpu.py > gpurun_out/r4b/tests.log 2>&1; rc=$?
+timeout -k 10 500 python -u -m pytest -v --timeout 120 --timeout-method thread tests/test_subsample_gpu.py tests/test_attn_bwd_gpu.py tests/test_race_gpu.py tests/test_training_rng_gpu.py tests/test_ddp_overlap_nondet_gpu.py tests/test_optim_gpu.py tests/test_determinism_gpu.py tests/test_step_parity_gpu.py tests/test_bench_shape_gpu.py > gpurun_out/r4b/tests.log 2>&1; rc=$?
 tail -5 gpurun_out/r4b/tests.log
+grep -E "FAILED|ERROR" gpurun_out/r4b/tests.log | head
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+timeout -k 10 200 python -u bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-f32-sensitivity > gpurun_out/r4b/bench_new.log 2>&1 && tail -1 gpurun_out/r4b/bench_new.log | cut -c1-300 &&
+KDFM_SS_ONE_KERNEL=0 KDFM_ATTN_BWD2=0 timeout -k 10 200 python -u bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-f32-sensitivity > gpurun_out/r4b/bench_old.log 2>&1 && tail -1 gpurun_out/r4b/bench_old.log | cut -c1-300 &&
 timeout -k 10 200 python -u tools/plan_issue_probe.py 6 40 > gpurun_out/r4b/plan_issue.log 2>&1
-cat gpurun_out/r4b/plan_issue.log | tail -45
+tail -45 gpurun_out/r4b/plan_issue.log
