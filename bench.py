@@ -437,6 +437,7 @@ def main():
                                    "(d88 h2 L16), BASELINE.json configs[1] shape",
                        "global_batch": world * args.batch, "seq_len": args.samples, "issue": issue,
                        "deterministic": cfg.deterministic,
+                       "kernarg_device_memory": bool(getattr(__import__("kdfm"), "KERNARG_IN_DEVICE_MEMORY", False)),
                        "frames_subsampled": (args.samples // 160) // 4 + 1, "parallelism": f"dp{world}"},
             "roofline": roof,
             "roofline_by_family": by_route,

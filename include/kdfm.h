@@ -63,6 +63,9 @@ int32_t kdfm_range_pop(void);
  * kernels.  `event` is a hipEvent_t, `stream` a hipStream_t, both owned by the caller. */
 int kdfm_event_record(void* event, void* stream);
 int kdfm_stream_wait_event(void* stream, void* event);
+/* A HIP stream restricted to n_cus CUs spread uniformly over the device (hipExtStreamCreateWithCUMask);
+ * *out receives the hipStream_t (the caller destroys it with hipStreamDestroy). */
+int kdfm_stream_create_cu_mask(int32_t n_cus, void** out);
 int kdfm_memset_async(void* ptr, int32_t value, int64_t bytes, void* stream);
 
 /* --------------------------------------------------------------------------------------------

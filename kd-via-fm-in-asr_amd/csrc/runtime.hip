@@ -6,6 +6,8 @@
 
 #include "common.h"
 
+#include <vector>
+
 namespace kdfm {
 
 static thread_local std::string g_last_error;
@@ -127,6 +129,34 @@ int kdfm_stream_wait_event(void* stream, void* event) {
     kdfm::set_error("kdfm_stream_wait_event: hipStreamWaitEvent failed");
     return KDFM_ELAUNCH;
   }
+  return KDFM_OK;
+}
+
+// A stream restricted to n_cus of the device's CUs (hipExtStreamCreateWithCUMask), spread uniformly over the
+// CU index space (every (total / n_cus)-th CU, so whatever the index -> XCD mapping every XCD keeps its
+// share): the weight-gradient stream runs its products beside the critical-path kernels without taking
+// every CU's LDS and wave slots when its workgroups arrive first.  *out receives the hipStream_t.
+int kdfm_stream_create_cu_mask(int32_t n_cus, void** out) {
+  KDFM_REQUIRE(out && n_cus > 0, "bad arguments");
+  int dev = 0;
+  hipDeviceProp_t prop;
+  if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) {
+    kdfm::set_error("kdfm_stream_create_cu_mask: no device");
+    return KDFM_ELAUNCH;
+  }
+  const int total = prop.multiProcessorCount;
+  KDFM_REQUIRE(n_cus <= total, "more CUs than the device has");
+  std::vector<uint32_t> mask((size_t)(total + 31) / 32, 0u);
+  for (int i = 0; i < n_cus; ++i) {
+    const int cu = (int)(((int64_t)i * total) / n_cus);
+    mask[(size_t)cu / 32] |= 1u << (cu % 32);
+  }
+  hipStream_t st = nullptr;
+  if (hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()) != hipSuccess) {
+    kdfm::set_error("kdfm_stream_create_cu_mask: hipExtStreamCreateWithCUMask failed");
+    return KDFM_ELAUNCH;
+  }
+  *out = st;
   return KDFM_OK;
 }
 

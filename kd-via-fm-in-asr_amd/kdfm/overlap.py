@@ -17,9 +17,29 @@ Both streams are captured into the same HIP graph by GraphedTrainStep (fork/join
 edges)."""
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import kernels as K
+
+# KDFM_WGRAD_CUS=n: the weight-gradient stream is created restricted to n CUs (spread over every XCD;
+# kdfm_stream_create_cu_mask), so its products never hold every CU's LDS / wave slots when the
+# critical-path kernels arrive; the row-parallel weight gradients then target n workgroups (fewer
+# K-splits, smaller partials) unless KDFM_WGR_WGS says otherwise.  0 (default): an ordinary stream.
+WGRAD_CUS = int(os.environ.get("KDFM_WGRAD_CUS", "0"))
+if WGRAD_CUS > 0:
+    os.environ.setdefault("KDFM_WGR_WGS", str(WGRAD_CUS))
+
+
+def _masked_stream(dev, n_cus):
+    import ctypes as C
+
+    from . import _lib
+    with torch.cuda.device(dev):
+        out = C.c_void_p()
+        _lib.check(_lib.lib().kdfm_stream_create_cu_mask(int(n_cus), C.byref(out)), "kdfm_stream_create_cu_mask")
+        return torch.cuda.ExternalStream(out.value, device=dev)
 
 
 class WgradOverlap:
@@ -34,7 +54,7 @@ class WgradOverlap:
         key = torch.device(dev).index if not isinstance(dev, int) else dev
         s = self._side.get(key)
         if s is None:
-            s = torch.cuda.Stream(device=key)
+            s = _masked_stream(key, WGRAD_CUS) if WGRAD_CUS > 0 else torch.cuda.Stream(device=key)
             self._side[key] = s
             self._links[key] = (K.StreamLink(), K.StreamLink())
         return s

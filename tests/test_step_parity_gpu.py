@@ -50,7 +50,8 @@ def _oracle_params(cfg, eng):
                         subsampling_conv_channels=cfg.subsampling_conv_channels,
                         causal_downsampling=cfg.causal_downsampling, version=cfg.version,
                         kd_loss_type=cfg.kd_loss_type, use_diffkd=cfg.use_diffkd, diffkd_steps=cfg.diffkd_steps,
-                        vocab=cfg.vocab, d_teacher=cfg.d_teacher, heads_teacher=cfg.heads_teacher)
+                        vocab=cfg.vocab, d_teacher=cfg.d_teacher, heads_teacher=cfg.heads_teacher,
+                        d_student=cfg.d_student, heads_student=cfg.heads_student, conv_kernel=cfg.conv_kernel)
     p = {}
     p.update(O.frontend_buffers(ocfg))
     p.update(O.frontend_buffers(ocfg, "teacher.preprocessor.featurizer."))
@@ -81,6 +82,10 @@ def _close(a, b, tol, what, atol=1e-6, failures=None):
 
 DW4 = dict(subsampling="dw_striding", subsampling_factor=4)
 DW8C = dict(subsampling="dw_striding", subsampling_factor=8, subsampling_conv_channels=32, causal_downsampling=True)
+# FastConformer layer shapes (configs[4]; fast-conformer_ctc_bpe.yaml:113-145): d_model 512, 8 heads (head dim 64),
+# dw_striding x8 with 256 channels, depthwise conv kernel 9 -- student and teacher at that width
+FC = dict(d_student=512, heads_student=8, d_teacher=512, heads_teacher=8, subsampling="dw_striding",
+          subsampling_factor=8, subsampling_conv_channels=256, conv_kernel=9, sched_d_model=512)
 
 
 @pytest.mark.parametrize("n_layers,B,N,lens,U,tl,sub", [
@@ -106,8 +111,10 @@ DW8C = dict(subsampling="dw_striding", subsampling_factor=8, subsampling_conv_ch
     # teacher as wide as the student: the two encoders (issued interleaved on two streams) must keep
     # separate workspaces (the workspace key now includes the parameter prefix)
     (2, 2, 19200, [19200, 16123], 12, [12, 7], dict(d_teacher=88, heads_teacher=2)),
+    # FastConformer shapes (f32 parity arithmetic)
+    (2, 2, 32000, [32000, 24321], 12, [12, 7], FC),
 ], ids=["2L-1.2s", "16L-1s", "16L-16s", "16L-16s-overlapped", "2L-1.2s-dw4", "2L-1.2s-dw8-causal", "2L-1.2s-ver6", "2L-1.2s-ver7",
-        "2L-1.2s-ver8-l1", "2L-1.2s-diffkd", "2L-1.2s-V1024", "2L-1.2s-equal-widths"])
+        "2L-1.2s-ver8-l1", "2L-1.2s-diffkd", "2L-1.2s-V1024", "2L-1.2s-equal-widths", "2L-2s-fastconformer-d512"])
 def test_ver5_step_matches_oracle(n_layers, B, N, lens, U, tl, sub):
     from kdfm.config import sub_dims
     cfg, eng, wav, wl, tg, tgl, g = _build(n_layers, B, N, lens, U, tl, sub=sub)
@@ -185,3 +192,51 @@ def test_frontend_matches_oracle():
     ref, rl = O.preprocess(wav, wl, b["preprocessor.featurizer.window"], b["preprocessor.featurizer.fb"][0], ocfg)
     assert torch.equal(ml.cpu(), rl)
     _close(mel.cpu().transpose(1, 2), ref, 2e-4, "log-mel")
+
+
+@pytest.mark.parametrize("sub", [FC, dict()], ids=["fastconformer-d512-h8", "conformer-small"])
+def test_bf16_step_matches_float64_oracle(sub):
+    """The bf16 benchmark kernels (fused LN-block FFN / projections where the width has them, the fused
+    rel-pos attention forward and the bwd2 backward -- at head dim 64 for the FastConformer shapes --,
+    bf16 weight gradients, the one-kernel striding subsampling for Conformer-small) through a whole
+    2-layer step against the float64 oracle, dropout / SpecAugment / dither off, deterministic reductions.
+    Tolerances are the bf16 step's (tests/test_bench_shape_gpu.py): losses rel 3e-3, layer outputs rel.
+    Frobenius 1.5e-2, every gradient rel. Frobenius 5e-2."""
+    from dataclasses import replace
+    n_layers, B, N, U = 2, 2, 32000, 12
+    cfg, eng, wav, wl, tg, tgl, g = _build(n_layers, B, N, [32000, 24321], U, [12, 7], sub=dict(sub, math="bf16"))
+    from kdfm.config import sub_dims
+    T = sub_dims(cfg, N // cfg.hop + 1)[-1][0]
+    eps_rows = torch.randn(n_layers * B * T, cfg.latent, generator=g)
+    ctx = eng.forward(wav.cuda(), wl.cuda(), tg.cuda(), tgl.cuda(), train=True, eps=eps_rows.cuda())
+    losses = eng.losses.detach().cpu().clone()
+    sfeats = ctx["sfeats"].detach().cpu().clone()
+    eng.backward(ctx)
+    torch.cuda.synchronize()
+    grads = eng.student.grads()
+    ocfg, p32 = _oracle_params(cfg, eng)
+    p = {k: (v.double() if v.is_floating_point() else v) for k, v in p32.items()}
+    names = O.trainable_names(p, cfg.version, cfg.use_diffkd)
+    for k in names:
+        p[k] = p[k].clone().requires_grad_(True)
+    eps_o = eps_rows.view(n_layers, B, T, cfg.latent).permute(0, 1, 3, 2)
+    out = O.ver5_step(p, wav.double(), wl, tg, tgl, ocfg, eps_o.double())
+    ref = torch.stack([out["loss"], out["ctc"], out["kl"], out["recon"], out["fm"]]).detach().double()
+    rel = ((losses.double() - ref).abs() / ref.abs().clamp_min(1e-6)).max().item()
+    assert rel <= 3e-3, (rel, losses.tolist(), ref.tolist())
+
+    def frob(a, b):
+        a, b = a.detach().double().cpu(), b.detach().double().cpu()
+        return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+    for i in range(n_layers):
+        e = frob(sfeats[i].view(B, T, -1), out["s_feats"][i])
+        assert e <= 1.5e-2, (i, e)
+    og = torch.autograd.grad(out["loss"], [p[k] for k in names], allow_unused=True)
+    bad = []
+    for k, gr in zip(names, og):
+        if gr is None or k.endswith(ANALYTIC_ZERO) or gr.abs().max().item() == 0.0:
+            continue
+        e = frob(grads[k], gr)
+        if e > 5e-2:
+            bad.append((k, e))
+    assert not bad, bad
