@@ -54,7 +54,8 @@ class Ver5Config:
     # (encfm_dynamic, the --use_dynamic_steps path) turned into FM calls by encfm_strategy
     # (--router_strategy), or fixed per layer (encfm_steps_per_layer = --sampling_steps_per_layer);
     # router_max_steps = --router_max_sampling_steps, router_weight = --router_weight,
-    # flow_schedule = --flow_schedule (rectified | vp_ode)
+    # flow_schedule = --flow_schedule (rectified | vp_ode); "logitkd" = the baseline DistilEncDecCTCModelBPE
+    # (CTC + kd_alpha * logit KD only, asr_train_diffm.py:170-324)
     kd_model: str = "diffm"
     encfm_strategy: str = "batch_mode"
     encfm_dynamic: bool = True
@@ -260,8 +261,15 @@ def head_specs(cfg: Ver5Config, fm_prefixes=None) -> list:
             # parameters on zero gradients
             raise ValueError("kd_model='encfm' with use_diffkd is not supported by the engine")
         return encfm_specs(cfg, True)
+    if cfg.kd_model == "logitkd":
+        # DistilEncDecCTCModelBPE (asr_train_diffm.py:170-324, asr_train.py:314-466; the logitkd_* launchers):
+        # CTC + kd_alpha * logit KD, no latent heads.  Its use_layerwise_distillation branch builds a fresh
+        # projection lazily after the optimizer exists (never trained) and stays out of scope
+        if cfg.use_diffkd:
+            raise ValueError("kd_model='logitkd' has no DiffKD module")
+        return []
     if cfg.kd_model != "diffm":
-        raise ValueError(f"kd_model must be 'diffm' or 'encfm', got {cfg.kd_model!r}")
+        raise ValueError(f"kd_model must be 'diffm', 'encfm' or 'logitkd', got {cfg.kd_model!r}")
     L, Ct, Cs, E = cfg.latent, cfg.d_teacher, cfg.d_student, cfg.time_embed_dim
     mods = head_modules(cfg)
     s = [("tae.enc.weight", (L, Ct, 1)), ("tae.enc.bias", (L,)),
@@ -301,6 +309,8 @@ def all_head_specs(cfg: Ver5Config) -> list:
     from dataclasses import replace
     if cfg.kd_model == "encfm":
         return encfm_specs(cfg, True) + encfm_specs(cfg, False)
+    if cfg.kd_model == "logitkd":
+        return []
     return head_specs(replace(cfg, version=6))
 
 

@@ -638,6 +638,71 @@ class DistilFlowMatchingCTCModelBPE(EncDecCTCModelBPE):
         return eng
 
 
+class DistilEncDecCTCModelBPE(EncDecCTCModelBPE):
+    """Reference class (asr_train_diffm.py:170-324; asr_train.py:314-466 is the same model): the baseline
+    logit distillation that the logitkd_* launchers train -- CTC + kd_alpha * KL(log_softmax(s/T) ||
+    softmax(teacher log-probs / T)) * T^2 ('batchmean').  The teacher's log-probs come from its own
+    forward (preprocessor, encoder, decoder) under no_grad; like the FM models' teacher it runs in eval mode
+    (SURVEY.md Appendix B).  use_layerwise_distillation (a projection built lazily inside training_step,
+    after the optimizer exists, so never trained, plus a second student forward) stays out of scope."""
+
+    def __init__(self, teacher_model: EncDecCTCModelBPE, use_logit_distillation=True, kd_alpha=0.1,
+                 kd_temperature=1.0, use_layerwise_distillation=False, layer_kd_alpha=1.0, student_dim=88,
+                 device="cuda", **student_kw):
+        if use_layerwise_distillation:
+            raise _lib.KdfmError("use_layerwise_distillation is outside kdfm's scope (DESIGN.md §8)")
+        super().__init__(d_model=student_dim, n_heads=student_kw.pop("n_heads", 2), device=device, **student_kw)
+        self.teacher = teacher_model.eval()
+        for p in self.teacher.parameters():
+            p.requires_grad_(False)
+        self.use_logit_distillation = use_logit_distillation
+        self.kd_alpha, self.temperature = kd_alpha, kd_temperature
+        self.use_layerwise_distillation, self.layer_kd_alpha = False, layer_kd_alpha
+        self.to(device)
+
+    def train(self, mode=True):
+        super().train(mode)
+        self.teacher.eval()
+        return self
+
+    def training_step(self, batch, batch_idx=0):
+        signal, signal_length, transcript, transcript_length = batch
+        log_probs, encoded_len, _ = EncDecCTCModelBPE.forward(self, input_signal=signal,
+                                                               input_signal_length=signal_length)
+        ctc_loss = self.loss(log_probs=log_probs, targets=transcript, input_lengths=encoded_len,
+                             target_lengths=transcript_length)
+        terms, weights = [ctc_loss], [1.0]
+        self.last_log = {"train_ctc_loss": ctc_loss.detach()}
+        if self.use_logit_distillation:
+            with torch.no_grad():
+                tch_log_probs, _, _ = self.teacher.forward(input_signal=signal, input_signal_length=signal_length)
+            logit_kd = _KLFn.apply(log_probs, tch_log_probs, float(self.temperature))
+            terms.append(logit_kd)
+            weights.append(self.kd_alpha)
+            self.last_log["train_kd_loss"] = logit_kd.detach()
+        stacked = torch.stack(terms)   # noqa: scalar gather (glue)
+        total = _WeightedSumFn.apply(stacked, torch.tensor(weights, device=stacked.device))
+        self.last_log["train_loss"] = total.detach()
+        return total
+
+    @torch.no_grad()
+    def to_engine(self, cfg: Ver5Config | None = None):
+        """This model's weights in the fused engine (kd_model "logitkd": no latent heads)."""
+        from dataclasses import replace
+        from .engine import Ver5Engine
+        if not self.use_logit_distillation:
+            raise _lib.KdfmError("the engine's logitkd step always includes the logit KD term")
+        cfg = replace(cfg or Ver5Config(), kd_model="logitkd", kd_alpha=float(self.kd_alpha),
+                      kd_temperature=float(self.temperature))
+        eng = Ver5Engine(cfg, self.decoder.decoder_layers[0].weight.device, init=False)
+        sd = {k: v for k, v in self.state_dict().items()}
+        eng.student.load({k: sd[k] for k, _ in eng.student.specs})
+        eng.teacher.load({k: sd[k] for k, _ in eng.teacher.specs})
+        for name, _ in eng.bn.specs:
+            eng.bn.P[name].copy_(sd[name])
+        return eng
+
+
 class _WeightedSumFn(torch.autograd.Function):
     """total = sum_i w_i x_i on device; backward broadcasts w_i * upstream."""
 
@@ -659,4 +724,4 @@ class _WeightedSumFn(torch.autograd.Function):
 
 
 __all__ = ["TeacherAutoEncoder", "StudentProjector", "NoiseAdapter", "SimpleDenoiser", "FlowMatchingModule",
-           "FMLatent", "EncDecCTCModelBPE", "DistilFlowMatchingCTCModelBPE", "mse_loss", "l1_loss", "greedy", "math"]
+           "FMLatent", "EncDecCTCModelBPE", "DistilFlowMatchingCTCModelBPE", "DistilEncDecCTCModelBPE", "mse_loss", "l1_loss", "greedy", "math"]

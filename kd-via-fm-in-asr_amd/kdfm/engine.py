@@ -212,6 +212,7 @@ class Ver5Engine:
         len1, len2 = compute_lengths(cfg, wav_len, mel_len, len1, len2, cfg.hop)
         seed = self.seed
         encfm = cfg.kd_model == "encfm"
+        heads = cfg.kd_model == "diffm"     # "logitkd": CTC + logit KD only, no latent heads
         # kl | recon, kd_pre, fm_pre, kd_post, fm_post (heads.RECON..FM_POST) | diffkd | sum of the layer-KD
         # terms and diffkd (zeroed before the teacher stream forks: its auto-encoder adds the recon term)
         acc = torch.zeros(8, device=dev)
@@ -267,9 +268,9 @@ class Ver5Engine:
                                      use_batch_stats=train, ws=self._enc_ws(Ss, "encoder."), run=srun)
         n_st = cfg.n_layers * Ss.rows
         tae = None
-        if not encfm:
+        if heads:
             tae = (torch.empty(n_st, cfg.latent, device=dev), torch.empty(n_st, St.d, device=dev))
-        h = self._heads_half(train, save) if not encfm else 0
+        h = self._heads_half(train, save) if heads else 0
         nb = h * Ss.rows
         hctx_b = None
         # the first heads half accumulates its loss terms into slots of its own (it runs on another stream
@@ -341,6 +342,8 @@ class Ver5Engine:
         if encfm:
             hctx = None
             K.axpby(ews.stats[2:3].view(1, 1), None, acc[7:8].view(1, 1), 1.0, 0.0)   # forward's total_loss
+        elif not heads:
+            hctx = None   # logit KD only: acc[1:8] stay 0, the total is CTC + kd_alpha * KL
         else:
             with K.region("heads_forward"):
                 na = n - nb
@@ -488,6 +491,14 @@ class Ver5Engine:
                 encfm_backward(cfg, P, G, ews, dfeats.view(n, Ss.d), ews.gxS, WGRAD.run)
             if grad_ready is not None:
                 grad_ready(min(o for k, o in off.items() if not k.startswith(("encoder.", "decoder."))))
+        elif ctx.get("hctx") is None:
+            # logit KD only (kd_model "logitkd"): the decoder's gradient is the encoder's only input gradient
+            ctx.pop("hctx", None)
+            K.linear_dw(g, ctx["sfeats"][-1], G["decoder.decoder_layers.0.weight"].view(Cn, Ss.d),
+                        db=G["decoder.decoder_layers.0.bias"])
+            K.fill(dfeats, 0.0)
+            K.linear_dx(g, Wd, dfeats[-1])
+            del g
         else:
             hctx_b, hctx_a, h = ctx.pop("hctx")
             nb = h * Ss.rows

@@ -39,7 +39,10 @@ def step_metrics(eng) -> dict:
     total, ctc, kl = v[0], v[1], v[2]
     nt = terms.numel()
     t = v[5:5 + nt]
-    if encfm:
+    if eng.cfg.kd_model == "logitkd":
+        # DistilEncDecCTCModelBPE.training_step (asr_train_diffm.py:282, 318-320)
+        out = {"train_kd_loss": kl, "train_ctc_loss": ctc}
+    elif encfm:
         out = {"train_ctc_loss": ctc, "train_logit_kd_loss": kl, "train_flow_matching_loss": t[0]}
         if eng.cfg.encfm_dynamic:
             out["train_router_loss"] = t[1]

@@ -68,7 +68,7 @@ class StepConfig:
     kd_loss_type: str = "mse"
     use_diffkd: bool = False            # --use_diffkd: DiffKDModule on every layer pair (:795-800)
     # asr_train.py's encoder-level FM family instead of the latent heads (oracle/encfm.py)
-    kd_model: str = "diffm"
+    kd_model: str = "diffm"             # "encfm" (asr_train.py) or "logitkd" (DistilEncDecCTCModelBPE)
     encfm_strategy: str = "batch_mode"
     router_max_steps: int = 8
     router_weight: float = 1.0
@@ -649,6 +649,13 @@ def ver5_step(p, wav, wav_len, targets, target_len, cfg: StepConfig, eps, spec_m
         tch_p = F.softmax(tch_logp / cfg.kd_temperature, dim=-1)
     stu_logp = F.log_softmax(log_probs / cfg.kd_temperature, dim=-1)
     kl = F.kl_div(stu_logp, tch_p, reduction="batchmean") * cfg.kd_temperature ** 2
+    if cfg.kd_model == "logitkd":
+        # DistilEncDecCTCModelBPE.training_step (asr_train_diffm.py:243-321): ctc + kd_alpha * logit KD; the
+        # KL is the same as ver5's (log_softmax(s/T) vs softmax(teacher log-probs / T), batchmean, * T^2)
+        zero = torch.zeros((), dtype=log_probs.dtype)
+        return {"loss": ctc + cfg.kd_alpha * kl, "ctc": ctc, "kl": kl, "recon": zero, "fm": zero, "diffkd": zero,
+                "log_probs": log_probs, "enc_len": enc_len, "mel": mel, "mel_len": mel_len, "s_feats": s_feats,
+                "t_feats": t_feats, "bn_state": bn_state}
     if encfm_out is not None:
         # training_step (asr_train.py:762-768): ctc + kd_alpha * logit_kd + forward's total_loss
         zero = torch.zeros((), dtype=log_probs.dtype)
@@ -687,7 +694,7 @@ def ver5_step(p, wav, wav_len, targets, target_len, cfg: StepConfig, eps, spec_m
             "bn_state": bn_state}
 
 
-def trainable_names(p: dict, version: int = 5, use_diffkd: bool = False) -> list:
+def trainable_names(p: dict, version: int = 5, use_diffkd: bool = False, kd_model: str = "diffm") -> list:
     """Names of the parameters the step trains (teacher frozen; buffers/running stats excluded;
     fm_latent_2 is used by versions 6 and 7 only, and otherwise receives no gradient; the DiffKD
     module only with use_diffkd, and its encoder never: its output is detached before every use)."""
@@ -700,6 +707,8 @@ def trainable_names(p: dict, version: int = 5, use_diffkd: bool = False) -> list
         if k.startswith("diffkd.") and (not use_diffkd or k.startswith("diffkd.encoder.")):
             continue
         if k.startswith("layer_proj."):   # built with flow matching, used only by layerwise KD (asr_train.py:525-529)
+            continue
+        if kd_model == "logitkd" and not k.startswith(("encoder.", "decoder.")):
             continue
         out.append(k)
     return out

@@ -110,3 +110,72 @@ def test_module_eval_forward_and_greedy():
     assert torch.equal(greedy(log_probs), pred)
     # rows are normalised log-probabilities
     assert torch.allclose(log_probs.exp().sum(-1), torch.ones_like(log_probs[..., 0]), atol=1e-4)
+
+
+def test_logit_kd_module_training_step_matches_oracle():
+    """DistilEncDecCTCModelBPE (asr_train_diffm.py:170-324, the logitkd_* launchers' model): its
+    training_step -- student forward, CTC, the teacher's own forward under no_grad, KL * T^2 -- on the module
+    path matches the oracle's kd_model="logitkd" step (loss rtol 2e-4, every encoder / decoder gradient at
+    2e-3 of its max or 4x the f32 CPU noise), and the engine (to_engine: kd_model "logitkd", no latent heads)
+    computes the same loss."""
+    from kdfm import kernels as K
+    from kdfm.distill import DistilEncDecCTCModelBPE, EncDecCTCModelBPE
+    K.set_math("f32")
+    K.set_deterministic(True)
+    n_layers, B, N = 2, 2, 16000
+    kw = dict(n_layers=n_layers, dither=0.0, spec_augment=False, dropout=0.0, dropout_pre_encoder=0.0,
+              dropout_att=0.0)
+    teacher = EncDecCTCModelBPE(d_model=176, n_heads=4, device="cuda", init_seed=0, **kw)
+    model = DistilEncDecCTCModelBPE(teacher, kd_alpha=0.1, kd_temperature=1.0, device="cuda", init_seed=1, **kw)
+    g = torch.Generator().manual_seed(14)
+    for name, buf in teacher.named_buffers():
+        if name.endswith("running_var"):
+            buf.copy_(1.0 + 0.3 * torch.rand(buf.shape, generator=g))
+        elif name.endswith("running_mean"):
+            buf.copy_(0.2 * torch.randn(buf.shape, generator=g))
+    model.train()
+    wav = 0.1 * torch.randn(B, N, generator=g)
+    wl = torch.tensor([N, 12345], dtype=torch.int64)
+    U = 9
+    tg = torch.randint(0, 128, (B, U), generator=g)
+    tl = torch.tensor([U, 4], dtype=torch.int64)
+    sd = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
+    loss = model.training_step((wav.cuda(), wl.cuda(), tg.cuda(), tl.cuda()), 0)
+    loss.backward()
+    torch.cuda.synchronize()
+    assert set(model.last_log) == {"train_ctc_loss", "train_kd_loss", "train_loss"}
+
+    ocfg = O.StepConfig(n_layers=n_layers, kd_model="logitkd")
+    p = dict(O.frontend_buffers(ocfg))
+    p.update(O.frontend_buffers(ocfg, "teacher.preprocessor.featurizer."))
+    for k, v in sd.items():
+        if k.startswith(("encoder.", "decoder.", "teacher.encoder.", "teacher.decoder.")):
+            p[k] = v
+    names = O.trainable_names(p, kd_model="logitkd")
+    p64 = {k: (v.double() if v.is_floating_point() else v) for k, v in p.items()}
+    for k in names:
+        p[k] = p[k].clone().requires_grad_(True)
+        p64[k] = p64[k].clone().requires_grad_(True)
+    out = O.ver5_step(p64, wav.double(), wl, tg, tl, ocfg, None)
+    out32 = O.ver5_step(p, wav, wl, tg, tl, ocfg, None)
+    assert abs(loss.item() - out["loss"].item()) <= 2e-4 * abs(out["loss"].item()) + 1e-4
+    og = torch.autograd.grad(out["loss"], [p64[k] for k in names], allow_unused=True)
+    og32 = torch.autograd.grad(out32["loss"], [p[k] for k in names], allow_unused=True)
+    params = dict(model.named_parameters())
+    checked = 0
+    for k, gr, g32 in zip(names, og, og32):
+        if gr is None or k.endswith(("self_attn.linear_k.bias", "conv.depthwise_conv.bias")):
+            continue
+        mine = params[k].grad
+        assert mine is not None, k
+        err = (mine.detach().cpu().double() - gr).abs().max().item()
+        noise = (g32.double() - gr).abs().max().item() if g32 is not None else 0.0
+        assert err <= 2e-3 * gr.abs().max().item() + 1e-6 or err <= 4.0 * noise, (k, err, noise)
+        checked += 1
+    assert checked > 40
+    from kdfm.config import Ver5Config
+    eng = model.to_engine(Ver5Config(
+        n_layers=n_layers, dither=0.0, specaug=False, dropout=0.0, dropout_pre=0.0, dropout_att=0.0, math="f32"))
+    eng.forward(wav.cuda(), wl.cuda(), tg.cuda(), tl.cuda(), train=True, save=False)
+    torch.cuda.synchronize()
+    assert abs(eng.losses[0].item() - loss.item()) <= 2e-4 * abs(loss.item()) + 1e-4

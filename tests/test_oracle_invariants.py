@@ -68,3 +68,27 @@ def test_encoder_batch_size_invariance():
     y2, _, _ = ver5.encoder(mel.repeat(2, 1, 1), l.repeat(2), p, "enc.", 88, 2, cfg, False, bn)
     torch.testing.assert_close(y1, y2[:1], rtol=1e-5, atol=1e-5)
     torch.testing.assert_close(y1, y2[1:], rtol=1e-5, atol=1e-5)
+
+
+def test_logitkd_oracle_is_ctc_plus_alpha_kl():
+    """kd_model "logitkd" (DistilEncDecCTCModelBPE, asr_train_diffm.py:243-321): the same student / teacher
+    forward as the FM step, total = CTC + kd_alpha * KL, no latent heads; only encoder / decoder train."""
+    import torch
+    from oracle import ver5 as O
+    cfg = O.StepConfig(n_layers=1)
+    p = O.init_all(cfg)
+    g = torch.Generator().manual_seed(2)
+    B, N = 2, 8000
+    wav = 0.1 * torch.randn(B, N, generator=g)
+    wl = torch.tensor([N, 6000])
+    tg = torch.randint(0, cfg.vocab, (B, 5), generator=g)
+    tl = torch.tensor([5, 3])
+    T = ((N // cfg.hop) // 2) // 2 + 1
+    eps = torch.randn(1, B, cfg.latent, T, generator=g)
+    full = O.ver5_step(p, wav, wl, tg, tl, cfg, eps)
+    lk = O.ver5_step(p, wav, wl, tg, tl, O.StepConfig(n_layers=1, kd_model="logitkd"), None)
+    torch.testing.assert_close(lk["ctc"], full["ctc"])
+    torch.testing.assert_close(lk["kl"], full["kl"])
+    torch.testing.assert_close(lk["loss"], full["ctc"] + cfg.kd_alpha * full["kl"])
+    names = O.trainable_names(p, kd_model="logitkd")
+    assert names and all(k.startswith(("encoder.", "decoder.")) for k in names)

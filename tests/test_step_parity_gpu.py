@@ -51,7 +51,8 @@ def _oracle_params(cfg, eng):
                         causal_downsampling=cfg.causal_downsampling, version=cfg.version,
                         kd_loss_type=cfg.kd_loss_type, use_diffkd=cfg.use_diffkd, diffkd_steps=cfg.diffkd_steps,
                         vocab=cfg.vocab, d_teacher=cfg.d_teacher, heads_teacher=cfg.heads_teacher,
-                        d_student=cfg.d_student, heads_student=cfg.heads_student, conv_kernel=cfg.conv_kernel)
+                        d_student=cfg.d_student, heads_student=cfg.heads_student, conv_kernel=cfg.conv_kernel,
+                        kd_model=cfg.kd_model)
     p = {}
     p.update(O.frontend_buffers(ocfg))
     p.update(O.frontend_buffers(ocfg, "teacher.preprocessor.featurizer."))
@@ -113,8 +114,11 @@ FC = dict(d_student=512, heads_student=8, d_teacher=512, heads_teacher=8, subsam
     (2, 2, 19200, [19200, 16123], 12, [12, 7], dict(d_teacher=88, heads_teacher=2)),
     # FastConformer shapes (f32 parity arithmetic)
     (2, 2, 32000, [32000, 24321], 12, [12, 7], FC),
+    # the baseline logit-KD model family (DistilEncDecCTCModelBPE, asr_train_diffm.py:170-324): CTC + 0.1 KL
+    (2, 2, 19200, [19200, 16123], 12, [12, 7], dict(kd_model="logitkd")),
 ], ids=["2L-1.2s", "16L-1s", "16L-16s", "16L-16s-overlapped", "2L-1.2s-dw4", "2L-1.2s-dw8-causal", "2L-1.2s-ver6", "2L-1.2s-ver7",
-        "2L-1.2s-ver8-l1", "2L-1.2s-diffkd", "2L-1.2s-V1024", "2L-1.2s-equal-widths", "2L-2s-fastconformer-d512"])
+        "2L-1.2s-ver8-l1", "2L-1.2s-diffkd", "2L-1.2s-V1024", "2L-1.2s-equal-widths", "2L-2s-fastconformer-d512",
+        "2L-1.2s-logitkd"])
 def test_ver5_step_matches_oracle(n_layers, B, N, lens, U, tl, sub):
     from kdfm.config import sub_dims
     cfg, eng, wav, wl, tg, tgl, g = _build(n_layers, B, N, lens, U, tl, sub=sub)
@@ -135,7 +139,7 @@ def test_ver5_step_matches_oracle(n_layers, B, N, lens, U, tl, sub):
     # weight gradient sums 64k cancelling terms after the 16-layer backward).
     eps_o = eps_rows.view(n_layers, B, T, cfg.latent).permute(0, 1, 3, 2)
     p = {k: (v.double() if v.is_floating_point() else v) for k, v in p32.items()}
-    names = O.trainable_names(p, cfg.version, cfg.use_diffkd)
+    names = O.trainable_names(p, cfg.version, cfg.use_diffkd, cfg.kd_model)
     for k in names:
         p[k] = p[k].clone().requires_grad_(True)
         p32[k] = p32[k].clone().requires_grad_(True)
@@ -216,7 +220,7 @@ def test_bf16_step_matches_float64_oracle(sub):
     grads = eng.student.grads()
     ocfg, p32 = _oracle_params(cfg, eng)
     p = {k: (v.double() if v.is_floating_point() else v) for k, v in p32.items()}
-    names = O.trainable_names(p, cfg.version, cfg.use_diffkd)
+    names = O.trainable_names(p, cfg.version, cfg.use_diffkd, cfg.kd_model)
     for k in names:
         p[k] = p[k].clone().requires_grad_(True)
     eps_o = eps_rows.view(n_layers, B, T, cfg.latent).permute(0, 1, 3, 2)

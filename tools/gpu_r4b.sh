@@ -1,7 +1,7 @@
 set -o pipefail
 mkdir -p gpurun_out/r4b
 export TMPDIR=/tmp
-timeout -k 10 500 python -u -m pytest -v --timeout 120 --timeout-method thread tests/test_subsample_gpu.py tests/test_attn_bwd_gpu.py tests/test_race_gpu.py tests/test_training_rng_gpu.py tests/test_ddp_overlap_nondet_gpu.py tests/test_optim_gpu.py tests/test_determinism_gpu.py tests/test_step_parity_gpu.py tests/test_bench_shape_gpu.py > gpurun_out/r4b/tests.log 2>&1; rc=$?
+timeout -k 10 500 python -u -m pytest -v --timeout 120 --timeout-method thread tests/test_subsample_gpu.py tests/test_attn_bwd_gpu.py tests/test_nemo_api_gpu.py tests/test_race_gpu.py tests/test_training_rng_gpu.py tests/test_ddp_overlap_nondet_gpu.py tests/test_optim_gpu.py tests/test_determinism_gpu.py tests/test_step_parity_gpu.py tests/test_bench_shape_gpu.py > gpurun_out/r4b/tests.log 2>&1; rc=$?
 tail -5 gpurun_out/r4b/tests.log
 grep -E "FAILED|ERROR" gpurun_out/r4b/tests.log | head -20
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
