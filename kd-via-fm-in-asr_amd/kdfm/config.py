@@ -60,6 +60,9 @@ class Ver5Config:
     encfm_strategy: str = "batch_mode"
     encfm_dynamic: bool = True
     encfm_steps_per_layer: tuple = None
+    # FlowMatchingModule meta_encoder_type (--meta_encoder_type, asr_train.py:1241-1279): "mlp" (router or
+    # fixed steps, kdfm/encfm.py) or "cnn" / "swin" (fixed steps, kdfm/fmmeta.py)
+    encfm_meta: str = "mlp"
     router_max_steps: int = 8
     router_weight: float = 1.0
     flow_schedule: str = "rectified"
@@ -229,6 +232,26 @@ ENCFM_HIDDEN = 128     # FlowMatchingModule hidden_dim (asr_train.py:1753); the 
 ENCFM_ROUTER_EMB = 32  # DynamicStepRouter layer_emb_dim (:514)
 
 
+def meta_specs(cfg: Ver5Config) -> list:
+    """FlowMatchingModule.meta_encoder parameters for cfg.encfm_meta (asr_train.py:1244-1259, 844-851)."""
+    Cs, E, H = cfg.d_student, cfg.time_embed_dim, ENCFM_HIDDEN
+    Ci = Cs + E
+    me = "flow_matching.meta_encoder."
+    if cfg.encfm_meta == "mlp":
+        return [(me + "0.weight", (H, Ci)), (me + "0.bias", (H,)), (me + "2.weight", (Cs, H)), (me + "2.bias", (Cs,))]
+    if cfg.encfm_meta == "cnn":
+        return [(me + "0.weight", (Cs, Ci, 3)), (me + "0.bias", (Cs,)), (me + "2.weight", (Cs, Cs, 1)),
+                (me + "2.bias", (Cs,))]
+    if cfg.encfm_meta == "swin":
+        return [(me + "attn.in_proj_weight", (3 * Ci, Ci)), (me + "attn.in_proj_bias", (3 * Ci,)),
+                (me + "attn.out_proj.weight", (Ci, Ci)), (me + "attn.out_proj.bias", (Ci,)),
+                (me + "linear1.weight", (Cs, Ci)), (me + "linear1.bias", (Cs,)),
+                (me + "linear2.weight", (Cs, Cs)), (me + "linear2.bias", (Cs,))]
+    # "conformer" (ConformerEncoder, :918-1020) and "unet" (UNet1D, :880-917; odd frame counts crash the
+    # reference's update x - v / S) are not on the engine
+    raise ValueError(f"encfm_meta must be 'mlp', 'cnn' or 'swin', got {cfg.encfm_meta!r}")
+
+
 def encfm_specs(cfg: Ver5Config, trained: bool = True) -> list:
     """Parameters of the encoder-level FM family, named as the reference module tree.  trained:
     flow_matching.* and (dynamic steps) router.*; else the ones the reference builds but never trains:
@@ -236,9 +259,7 @@ def encfm_specs(cfg: Ver5Config, trained: bool = True) -> list:
     the router when the step counts are fixed."""
     Cs, Ct, E, H = cfg.d_student, cfg.d_teacher, cfg.time_embed_dim, ENCFM_HIDDEN
     fm = "flow_matching."
-    fm_specs = [(fm + "time_embed.weight", (E, 1)), (fm + "time_embed.bias", (E,)),
-                (fm + "meta_encoder.0.weight", (H, Cs + E)), (fm + "meta_encoder.0.bias", (H,)),
-                (fm + "meta_encoder.2.weight", (Cs, H)), (fm + "meta_encoder.2.bias", (Cs,)),
+    fm_specs = [(fm + "time_embed.weight", (E, 1)), (fm + "time_embed.bias", (E,))] + meta_specs(cfg) + [
                 (fm + "shape_transformation_function.weight", (Ct, Cs)),
                 (fm + "shape_transformation_function.bias", (Ct,))]
     r = "router."
@@ -260,6 +281,9 @@ def head_specs(cfg: Ver5Config, fm_prefixes=None) -> list:
             # over the layers, :754-767, 1776-1782); the engine does not: refuse rather than train its
             # parameters on zero gradients
             raise ValueError("kd_model='encfm' with use_diffkd is not supported by the engine")
+        if cfg.encfm_meta != "mlp" and cfg.encfm_dynamic:
+            raise ValueError(f"encfm_meta={cfg.encfm_meta!r} runs with fixed step counts (encfm_dynamic=False, "
+                             "encfm_steps_per_layer); the dynamic router drives the 'mlp' meta-encoder only")
         return encfm_specs(cfg, True)
     if cfg.kd_model == "logitkd":
         # DistilEncDecCTCModelBPE (asr_train_diffm.py:170-324, asr_train.py:314-466; the logitkd_* launchers):
@@ -345,5 +369,5 @@ DEFAULT = Ver5Config()
 PARITY = DEFAULT.parity()
 
 __all__ = ["Ver5Config", "DEFAULT", "PARITY", "encoder_specs", "subsampling_specs", "sub_stages", "sub_pad",
-           "sub_channels", "sub_len", "sub_dims", "decoder_specs", "head_specs", "all_head_specs", "diffkd_specs", "encfm_specs", "head_modules", "student_specs",
+           "sub_channels", "sub_len", "sub_dims", "decoder_specs", "head_specs", "all_head_specs", "diffkd_specs", "encfm_specs", "meta_specs", "head_modules", "student_specs",
            "teacher_specs", "bn_buffer_specs", "fused_groups", "field"]

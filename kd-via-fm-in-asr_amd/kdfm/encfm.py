@@ -108,6 +108,9 @@ def encfm_forward(cfg, P, sfeats, tfeats, ws: EncFMWorkspace, *, seed=None, trai
     outputs.  Returns ws.xS (B*T, Cs): the last layer's FM output, the decoder's input.  ws.stats holds
     [sum flow losses, router_weight * sum router losses, their sum (forward's total_loss), mean steps];
     ws.flow / ws.rloss / ws.mean_steps the per-layer values (the reference's log keys)."""
+    if cfg.encfm_meta != "mlp":
+        from .fmmeta import meta_forward
+        return meta_forward(cfg, P, sfeats, tfeats, ws)
     L, B, T = cfg.n_layers, ws.B, ws.T
     Cs, Ct, H, Kmax = cfg.d_student, cfg.d_teacher, HIDDEN, cfg.router_max_steps
     fm, r = "flow_matching.", "router."
@@ -145,6 +148,10 @@ def encfm_backward(cfg, P, G, ws: EncFMWorkspace, dfeats, gxS, wgrad_run):
     """Data gradients into dfeats (L*B*T, Cs) (overwritten) from the flow losses, the router's entropy
     term and gxS (B*T, Cs) = d loss / d (last layer's FM output) through the decoder; the parameter
     gradients of flow_matching.* and router.* via `wgrad_run(fn, *keep)` (the weight-gradient stream)."""
+    if cfg.encfm_meta != "mlp":
+        from .fmmeta import meta_backward
+        meta_backward(cfg, P, G, ws, dfeats, gxS)
+        return
     L, B, T = cfg.n_layers, ws.B, ws.T
     Cs, Ct, H, Kmax = cfg.d_student, cfg.d_teacher, HIDDEN, cfg.router_max_steps
     fm, r = "flow_matching.", "router."

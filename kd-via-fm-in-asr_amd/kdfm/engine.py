@@ -158,7 +158,11 @@ class Ver5Engine:
     def _encfm_ws(self, B, T):
         ws = self._encfm.get((B, T))
         if ws is None:
-            ws = self._encfm[(B, T)] = EncFMWorkspace(self.cfg, B, T, self.device)
+            if self.cfg.encfm_meta != "mlp":
+                from .fmmeta import MetaFMWorkspace
+                ws = self._encfm[(B, T)] = MetaFMWorkspace(self.cfg, B, T, self.device)
+            else:
+                ws = self._encfm[(B, T)] = EncFMWorkspace(self.cfg, B, T, self.device)
         return ws
 
     def _side_stream(self):

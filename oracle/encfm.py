@@ -86,23 +86,59 @@ def schedule_coeffs(S, schedule="rectified", vp=(19.9, 0.1)):
     return da / (-ds), -1.0 / (-ds)
 
 
-def fm_forward(P, x0, tf, S, schedule="rectified"):
-    """FlowMatchingModule.forward, meta_encoder 'mlp', shape_transform 'linear', loss 'mse'
-    (:1318-1377): for i = S..1, t = i/S: v = W2 relu(W1 [x; te(t)] + b1) + b2, x <- x - v/S; then
+def meta_velocity(P, e, meta="mlp", heads=2):
+    """FlowMatchingModule.meta_encoder on e = [x; te(t)] (B, T, Cs+E) -> v (B, T, Cs) (:1244-1259, 1328-1345).
+    mlp: W2 relu(W1 e + b1) + b2.  cnn: Conv1d(k=3, pad 1 per utterance) -> ReLU -> Conv1d(k=1) over the
+    frames.  swin (SwinTransformerEncoder :844-866): nn.MultiheadAttention(e, e, e) over the T frames of
+    each utterance (no mask, `heads` heads, q scaled by 1/sqrt(dk)), out_proj, then linear2 relu(linear1)."""
+    me = "flow_matching.meta_encoder."
+    if meta == "mlp":
+        return _lin(torch.relu(_lin(e, P, me + "0")), P, me + "2")
+    if meta == "cnn":
+        a = torch.relu(torch.nn.functional.conv1d(e.transpose(1, 2), P[me + "0.weight"], P[me + "0.bias"], padding=1))
+        return torch.nn.functional.conv1d(a, P[me + "2.weight"], P[me + "2.bias"]).transpose(1, 2)
+    if meta == "swin":
+        B, T, C = e.shape
+        dk = C // heads
+        qkv = e @ P[me + "attn.in_proj_weight"].t() + P[me + "attn.in_proj_bias"]
+        q, k, v = (qkv[..., j * C:(j + 1) * C].reshape(B, T, heads, dk).transpose(1, 2) for j in range(3))
+        att = torch.softmax((q / math.sqrt(dk)) @ k.transpose(-1, -2), dim=-1)
+        o = (att @ v).transpose(1, 2).reshape(B, T, C)
+        ao = _lin(o, P, me + "attn.out_proj")
+        return _lin(torch.relu(_lin(ao, P, me + "linear1")), P, me + "linear2")
+    raise ValueError(f"meta-encoder {meta!r} not in the oracle (mlp, cnn, swin)")
+
+
+def fm_forward(P, x0, tf, S, schedule="rectified", meta="mlp", heads=2):
+    """FlowMatchingModule.forward, shape_transform 'linear', loss 'mse' (:1318-1377): for i = S..1,
+    t = i/S: v = meta_encoder([x; te(t)]) (meta_velocity), x <- x - v/S; then
     loss = mean((Wst nsx + bst - t_f)^2) with nsx from the LAST velocity and the ORIGINAL input.
-    x0: (..., Cs), tf: (..., Ct).  Returns (loss, x_S)."""
+    x0: (B, T, Cs), tf: (B, T, Ct).  Returns (loss, x_S)."""
     x = x0
     v = None
     for i in range(S, 0, -1):
         tt = torch.full(x0.shape[:-1] + (1,), i / S, dtype=x0.dtype)
         te = _lin(tt, P, "flow_matching.time_embed")
-        h = torch.relu(_lin(torch.cat([x, te], dim=-1), P, "flow_matching.meta_encoder.0"))
-        v = _lin(h, P, "flow_matching.meta_encoder.2")
+        v = meta_velocity(P, torch.cat([x, te], dim=-1), meta, heads)
         x = x - v / S
     ca, cv = schedule_coeffs(S, schedule)
     nsx = ca * x0 + cv * v
     tr = _lin(nsx, P, "flow_matching.shape_transformation_function")
     return ((tr - tf) ** 2).mean(), x
+
+
+def encfm_fixed_forward(P, sfeats, tfeats, steps, schedule="rectified", meta="mlp", heads=2):
+    """use_dynamic_steps=False with sampling_steps_per_layer (:639-641): no router, layer i runs steps[i]
+    FM steps; same result dict as encfm_forward (router losses 0)."""
+    flows = []
+    fm_out = None
+    for i, (s, t) in enumerate(zip(sfeats, tfeats)):
+        fl, fm_out = fm_forward(P, s, t, int(steps[i]), schedule, meta, heads)
+        flows.append(fl)
+    total = sum(flows[1:], flows[0])
+    B = sfeats[0].shape[0]
+    return {"total": total, "flow": flows, "router_loss": [total.new_zeros(()) for _ in flows],
+            "steps": torch.tensor([[int(S)] * B for S in steps]), "S": [int(S) for S in steps], "fm_out": fm_out}
 
 
 def encfm_forward(P, sfeats, tfeats, gumbels, strategy="batch_mode", max_steps=8, router_weight=1.0,

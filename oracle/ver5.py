@@ -70,6 +70,8 @@ class StepConfig:
     # asr_train.py's encoder-level FM family instead of the latent heads (oracle/encfm.py)
     kd_model: str = "diffm"             # "encfm" (asr_train.py) or "logitkd" (DistilEncDecCTCModelBPE)
     encfm_strategy: str = "batch_mode"
+    encfm_fixed: tuple = None           # sampling_steps_per_layer (fixed steps, no router) when given
+    encfm_meta: str = "mlp"             # FlowMatchingModule meta_encoder_type (mlp | cnn | swin)
     router_max_steps: int = 8
     router_weight: float = 1.0
     flow_schedule: str = "rectified"
@@ -638,9 +640,13 @@ def ver5_step(p, wav, wav_len, targets, target_len, cfg: StepConfig, eps, spec_m
         # asr_train.py:595-666: router + FM over the hooked layer pairs; the decoder reads the last
         # layer's FM output (hook layout (B, T, C) -> the decoder's (B, C, T))
         from oracle import encfm as E
-        encfm_out = E.encfm_forward(p, s_feats, t_feats, gumbel, strategy=cfg.encfm_strategy,
-                                    max_steps=cfg.router_max_steps, router_weight=cfg.router_weight,
-                                    schedule=cfg.flow_schedule)
+        if cfg.encfm_fixed is not None:
+            encfm_out = E.encfm_fixed_forward(p, s_feats, t_feats, cfg.encfm_fixed, schedule=cfg.flow_schedule,
+                                              meta=cfg.encfm_meta, heads=cfg.heads_student)
+        else:
+            encfm_out = E.encfm_forward(p, s_feats, t_feats, gumbel, strategy=cfg.encfm_strategy,
+                                        max_steps=cfg.router_max_steps, router_weight=cfg.router_weight,
+                                        schedule=cfg.flow_schedule)
         enc = encfm_out["fm_out"].transpose(1, 2)
     log_probs = decoder(enc, p, "decoder.")
     ctc = ctc_loss_mean_batch(log_probs, targets, enc_len, target_len, cfg.vocab)
