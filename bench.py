@@ -53,16 +53,23 @@ STEP_GFLOP_PER_UTT = 62.6
 ATTN_FFN_GFLOP_PER_UTT = 23.0
 
 
+def _is_call_kernel(stem):
+    """Kernels that start a traced call; folds / row-dot prologues run inside a call and add bytes, not calls."""
+    return "fold" not in stem and "rowdot" not in stem
+
+
 def pmc_traffic(stems):
-    """HBM bytes per launch pooled over the kernels whose names start with one of `stems` (the
-    launches of one kdfm_gemm kernel family) from the committed PMC summary; None if absent."""
+    """HBM bytes per CALL of a kernel family from the committed PMC summary: every family kernel's
+    bytes (main kernels, their folds) divided by the launches of the main kernels only, i.e. the same
+    unit as `bytes_per_launch` (one traced call = one main launch + its fold); None if absent."""
     try:
         with open(PMC_TRAFFIC) as fh:
             rows = json.load(fh)
     except (OSError, ValueError):
         return None
-    hit = [r for r in rows if any(r["kernel"].split(" ")[0].split("<")[0].endswith(st) for st in stems)]
-    n = sum(r["launches"] for r in hit)
+    name = lambda r: r["kernel"].split(" ")[0].split("<")[0]  # noqa: E731
+    hit = [r for r in rows if any(name(r).endswith(st) for st in stems)]
+    n = sum(r["launches"] for r in hit if _is_call_kernel(name(r)))
     return round(sum(r["bytes_total"] for r in hit) / n, 1) if n else None
 
 
@@ -363,7 +370,7 @@ def main():
         stems = FAMILY_KERNELS.get(dom) or ROUTE_KERNELS.get(dom, (dom,))
         roof.update({"traffic": pmc_traffic(stems),
                      "traffic_source": os.path.relpath(PMC_TRAFFIC, ROOT) + " (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, "
-                                       "pooled over the family's kernels, bytes per launch)",
+                                       "all of the family's kernels incl. folds, per call = per main-kernel launch)",
                      "kernel": f"{dom} family ({', '.join(stems)}): the kernel family with the largest aggregated "
                                f"time of the step (kdfm_gemm routes + the fused kernels, HIP events on their streams)",
                      "launches": n, "avg_ms": round(ms, 5), "bytes_per_launch": round(dt["bytes_total"] / n, 1),

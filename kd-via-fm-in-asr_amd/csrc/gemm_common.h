@@ -29,6 +29,7 @@ struct GemmP {
   int partial;  // deterministic split-K: ATOMIC tiles store raw partials to ws[split][m][n] (folded in order)
   int nseg; int64_t seg_rows;  // row-parallel wgrad: per-segment bias columns ones_col .. one_col + nseg - 1
   const int64_t* k_dev;        // row-parallel wgrad: device-side row count (<= K) read at run time (NULL: K)
+  int xslots;                  // row-parallel wgrad: 0 = one raw partial per split; 8 = per-XCD slots (atomics)
 };
 
 // Non-atomic epilogue for one output element.  v = alpha * acc (already scaled).  bz = batch

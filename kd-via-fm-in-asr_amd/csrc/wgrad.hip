@@ -329,6 +329,25 @@ __global__ __launch_bounds__(WR_NT, 2) void wgr_kernel(GemmP p, WrGeo g) {
   }
   KPROBE(29);
 
+  if (p.xslots) {
+    // non-deterministic mode: add into the slot of the XCD this workgroup runs on (HW_REG_XCC_ID; the
+    // slot choice is locality only -- the adds are device-coherent atomics wherever they land), so the
+    // partial traffic is 8 slots in L2 instead of one f32 tile per split through HBM
+    const int xcd = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 7;
+    float* wsx = p.ws + (int64_t)xcd * p.M * p.N;
+#pragma unroll
+    for (int i = 0; i < MBW; ++i)
+#pragma unroll
+      for (int j = 0; j < NBW; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int ml = (mb0 + i) * 16 + (lane >> 4) * 4 + r;
+          const int64_t n = n0 + (nb0 + j) * 16 + (lane & 15);
+          if (ml < mcols && n < p.N && n < n0 + g.Nb)
+            __hip_atomic_fetch_add(wsx + (m0 + ml) * p.N + n, acc[i][j][r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    return;
+  }
   // raw partial of this (split, slice) -> ws[split][m][n]
   float* wsp = p.ws + split * p.M * p.N;
 #pragma unroll
@@ -535,6 +554,30 @@ int wr_launch(const GemmP& p, const WrPlan& pl, hipStream_t st) {
 
 }  // namespace
 
+// per-XCD slot accumulation (GemmP::xslots) for the register-staged kernel: non-deterministic mode
+// only (float atomics), and only where it saves traffic (>= 16 splits: 8 slots + a memset instead of
+// S raw partials written and read back).  KDFM_WGR_XCD=0 keeps the per-split partials.
+constexpr int WR_XSLOTS = 8;
+bool wr_use_xslots(const WrPlan& pl) {
+  const int on = env_i("KDFM_WGR_XCD", 1);   // read per call, like KDFM_WGR_MSL (tests compare both)
+  return on && !deterministic() && !pl.dma && pl.S >= 2 * WR_XSLOTS;
+}
+
+// zero the slots (stream-ordered) and mark the launch parameters
+int wr_prep_xslots(GemmP& q, const WrPlan& pl, hipStream_t st) {
+  if (!wr_use_xslots(pl)) return 0;
+  q.xslots = WR_XSLOTS;
+  if (hipMemsetAsync(q.ws, 0, sizeof(float) * WR_XSLOTS * q.M * q.N, st) != hipSuccess)
+    return check_launch("kdfm wgrad rows (slot memset)");
+  return 0;
+}
+
+int wr_fold(const GemmP& p, int64_t S, hipStream_t st) {
+  hipLaunchKernelGGL(wgr_fold_kernel<false>, dim3((unsigned)ceil_div(p.M * p.N, 64)), dim3(64 * WF_WAVES), 0, st, p,
+                     p.xslots ? (int64_t)p.xslots : S);
+  return check_launch("kdfm wgrad rows (fold)");
+}
+
 int64_t wgrad_rows_ws(const GemmP& p, int amode, int bmode, int64_t batch) {
   GemmP q = p;
   q.A = reinterpret_cast<const float*>(16);  // alignment checks only
@@ -548,28 +591,29 @@ int try_wgrad_rows(const GemmP& p, int amode, int bmode, int64_t batch, hipStrea
   WrPlan pl;
   if (!p.ws || !wr_plan(p, amode, bmode, batch, pl)) return -1;
   if (p.ws_len < pl.S * p.M * p.N) return -1;
-  int rc;
+  GemmP q = p;
+  int rc = wr_prep_xslots(q, pl, st);
+  if (rc) return rc;
   const int key = pl.w.mbw * 10 + pl.w.nbw;
   if (bmode == KDFM_LD_CONV) {
     switch (key) {
-      case 32: rc = wr_launch<3, 2, true>(p, pl, st); break;
-      case 33: rc = wr_launch<3, 3, true>(p, pl, st); break;
-      case 34: rc = wr_launch<3, 4, true>(p, pl, st); break;
-      case 36: rc = wr_launch<3, 6, true>(p, pl, st); break;
-      default: rc = wr_launch<6, 3, true>(p, pl, st); break;
+      case 32: rc = wr_launch<3, 2, true>(q, pl, st); break;
+      case 33: rc = wr_launch<3, 3, true>(q, pl, st); break;
+      case 34: rc = wr_launch<3, 4, true>(q, pl, st); break;
+      case 36: rc = wr_launch<3, 6, true>(q, pl, st); break;
+      default: rc = wr_launch<6, 3, true>(q, pl, st); break;
     }
   } else {
     switch (key) {
-      case 32: rc = wr_launch<3, 2, false>(p, pl, st); break;
-      case 33: rc = wr_launch<3, 3, false>(p, pl, st); break;
-      case 34: rc = wr_launch<3, 4, false>(p, pl, st); break;
-      case 36: rc = wr_launch<3, 6, false>(p, pl, st); break;
-      default: rc = wr_launch<6, 3, false>(p, pl, st); break;
+      case 32: rc = wr_launch<3, 2, false>(q, pl, st); break;
+      case 33: rc = wr_launch<3, 3, false>(q, pl, st); break;
+      case 34: rc = wr_launch<3, 4, false>(q, pl, st); break;
+      case 36: rc = wr_launch<3, 6, false>(q, pl, st); break;
+      default: rc = wr_launch<6, 3, false>(q, pl, st); break;
     }
   }
   if (rc) return rc;
-  hipLaunchKernelGGL(wgr_fold_kernel<false>, dim3((unsigned)ceil_div(p.M * p.N, 64)), dim3(64 * WF_WAVES), 0, st, p, pl.S);
-  return check_launch("kdfm_gemm(wgrad rows fold)");
+  return wr_fold(q, pl.S, st);
 }
 
 }  // namespace kdfm
@@ -946,10 +990,12 @@ int wgrad_bf16_run(const GemmP& p, int bmode, hipStream_t st) {
                        pl.S);
     return check_launch("kdfm_wgrad_bf16(fold)");
   }
-  const int rc = pl.bin == 2 ? wr_dispatch<2>(p, pl, bmode, st) : wr_dispatch<1>(p, pl, bmode, st);
+  GemmP q = p;
+  int rc = wr_prep_xslots(q, pl, st);
   if (rc) return rc;
-  hipLaunchKernelGGL(wgr_fold_kernel<false>, dim3((unsigned)ceil_div(p.M * p.N, 64)), dim3(64 * WF_WAVES), 0, st, p, pl.S);
-  return check_launch("kdfm_wgrad_bf16(fold)");
+  rc = pl.bin == 2 ? wr_dispatch<2>(q, pl, bmode, st) : wr_dispatch<1>(q, pl, bmode, st);
+  if (rc) return rc;
+  return wr_fold(q, pl.S, st);
 }
 }  // namespace
 }  // namespace kdfm

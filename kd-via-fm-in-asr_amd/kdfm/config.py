@@ -60,6 +60,11 @@ class Ver5Config:
     encfm_strategy: str = "batch_mode"
     encfm_dynamic: bool = True
     encfm_steps_per_layer: tuple = None
+    # --flow_steps (flow_cfg training_sampling): the per-layer count of the fixed-step path when
+    # encfm_steps_per_layer is None.  The reference reads it from self.flow_cfg, which its __init__
+    # never sets (asr_train.py:644 vs :498-529: AttributeError -- every flowkd_* launcher without
+    # --sampling_steps_per_layer stops there); the engine runs the value that line names.
+    encfm_flow_steps: int = 8
     # FlowMatchingModule meta_encoder_type (--meta_encoder_type, asr_train.py:1241-1279): "mlp" (router or
     # fixed steps, kdfm/encfm.py) or "cnn" / "swin" (fixed steps, kdfm/fmmeta.py)
     encfm_meta: str = "mlp"
@@ -232,6 +237,19 @@ ENCFM_HIDDEN = 128     # FlowMatchingModule hidden_dim (asr_train.py:1753); the 
 ENCFM_ROUTER_EMB = 32  # DynamicStepRouter layer_emb_dim (:514)
 
 
+def encfm_fixed_steps(cfg: Ver5Config) -> tuple:
+    """Per-layer FM step counts of the fixed-step path (use_dynamic_steps False, asr_train.py:639-645):
+    sampling_steps_per_layer when given, else training_sampling (= --flow_steps) for every layer."""
+    if cfg.encfm_steps_per_layer is not None:
+        steps = tuple(int(s) for s in cfg.encfm_steps_per_layer)
+    else:
+        steps = (int(cfg.encfm_flow_steps),) * cfg.n_layers
+    if len(steps) != cfg.n_layers or not all(1 <= s <= cfg.router_max_steps for s in steps):
+        raise ValueError(f"fixed FM step counts {steps}: need one count in [1, router_max_steps="
+                         f"{cfg.router_max_steps}] per layer ({cfg.n_layers})")
+    return steps
+
+
 def meta_specs(cfg: Ver5Config) -> list:
     """FlowMatchingModule.meta_encoder parameters for cfg.encfm_meta (asr_train.py:1244-1259, 844-851)."""
     Cs, E, H = cfg.d_student, cfg.time_embed_dim, ENCFM_HIDDEN
@@ -369,5 +387,5 @@ DEFAULT = Ver5Config()
 PARITY = DEFAULT.parity()
 
 __all__ = ["Ver5Config", "DEFAULT", "PARITY", "encoder_specs", "subsampling_specs", "sub_stages", "sub_pad",
-           "sub_channels", "sub_len", "sub_dims", "decoder_specs", "head_specs", "all_head_specs", "diffkd_specs", "encfm_specs", "meta_specs", "head_modules", "student_specs",
+           "sub_channels", "sub_len", "sub_dims", "decoder_specs", "head_specs", "all_head_specs", "diffkd_specs", "encfm_specs", "meta_specs", "encfm_fixed_steps", "head_modules", "student_specs",
            "teacher_specs", "bn_buffer_specs", "fused_groups", "field"]

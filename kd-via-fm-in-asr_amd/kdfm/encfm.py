@@ -23,7 +23,7 @@ from . import _lib
 from . import kernels as K
 from .config import ENCFM_HIDDEN as HIDDEN
 from .config import ENCFM_ROUTER_EMB as ROUTER_EMB
-from .config import encfm_specs
+from .config import encfm_fixed_steps, encfm_specs
 
 STRATEGIES = {"batch_mode": 0, "batch_avg": 1, "batch_median": 2, "group": 3}
 SALT_ROUTER = 41      # counter-RNG stream of the router's Gumbel noise
@@ -82,14 +82,11 @@ class EncFMWorkspace:
             self._fixed(cfg, dev)
 
     def _fixed(self, cfg, dev):
-        """use_dynamic_steps=False: the per-layer step counts of sampling_steps_per_layer (:639-641),
-        constant, so the strategy's outputs are computed once here."""
+        """use_dynamic_steps=False: the per-layer step counts of sampling_steps_per_layer, else
+        training_sampling (:639-645, config.encfm_fixed_steps), constant, so the strategy's outputs are
+        computed once here."""
         L, B, T = cfg.n_layers, self.B, self.T
-        steps = list(cfg.encfm_steps_per_layer or [])
-        if len(steps) != L or not all(1 <= int(s) <= cfg.router_max_steps for s in steps):
-            raise ValueError("encfm_steps_per_layer needs one step count in [1, router_max_steps] per layer "
-                             "(the reference's fixed-step path reads self.flow_cfg, which it never sets, so it "
-                             "only runs with sampling_steps_per_layer)")
+        steps = list(encfm_fixed_steps(cfg))
         S = [int(steps[u // B]) for u in range(L * B)]
         off, o = [], 0
         for s in S:

@@ -18,7 +18,8 @@ the fused attention kernel pair (attn_fused.hip forward, attn_bwd.hip bwd2) with
 table, i.e. plain softmax(q k^T / sqrt(dk)) v -- nn.MultiheadAttention without masks (every frame,
 padded ones included, as the reference).  Only fixed step counts (sampling_steps_per_layer): the
 router's per-utterance counts would put a device->host sync on the step to drive the per-step
-launches; with meta "mlp" the dynamic router path is kdfm/encfm.py.  Parity: tests/golden/
+launches; with meta "mlp" the dynamic router path is kdfm/encfm.py.  Step counts: config.encfm_fixed_steps
+(sampling_steps_per_layer, else --flow_steps for every layer).  Parity: tests/golden/
 kd_encfm_meta.npz (the reference's own classes).
 """
 from __future__ import annotations
@@ -29,6 +30,7 @@ import torch
 
 from . import _lib
 from . import kernels as K
+from .config import encfm_fixed_steps
 from .encfm import schedule_coeffs
 
 META_TYPES = ("mlp", "cnn", "swin")
@@ -41,10 +43,9 @@ class MetaFMWorkspace:
         if cfg.encfm_meta not in ("cnn", "swin"):
             raise ValueError(f"MetaFMWorkspace is for the cnn / swin meta-encoders, got {cfg.encfm_meta!r}")
         L, Cs, Ct, E = cfg.n_layers, cfg.d_student, cfg.d_teacher, cfg.time_embed_dim
-        steps = [int(s) for s in (cfg.encfm_steps_per_layer or [])]
-        if cfg.encfm_dynamic or len(steps) != L or not all(1 <= s <= cfg.router_max_steps for s in steps):
-            raise ValueError("meta_encoder 'cnn' / 'swin' run with fixed step counts: encfm_dynamic=False and "
-                             "encfm_steps_per_layer with one count in [1, router_max_steps] per layer")
+        if cfg.encfm_dynamic:
+            raise ValueError("meta_encoder 'cnn' / 'swin' run with fixed step counts (encfm_dynamic=False)")
+        steps = list(encfm_fixed_steps(cfg))
         Ci = Cs + E
         n = B * T
         self.meta, self.B, self.T, self.n, self.Ci = cfg.encfm_meta, B, T, n, Ci

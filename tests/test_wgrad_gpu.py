@@ -2,7 +2,8 @@
 torch fp32 on the same device: every wave-tile instance, the implicit ones column (bias gradient),
 alpha, accumulation into a non-zero gradient, rows that are not a multiple of the 32-row step,
 multi-slice wide outputs, and the Conv1d(k=3) CONV mode with utterance boundaries.  bf16 operands,
-f32 accumulation: max|diff| <= 2e-2 * max|ref|.  Also: bitwise reproducible (ordered fold)."""
+f32 accumulation: max|diff| <= 2e-2 * max|ref|.  Also: bitwise reproducible in deterministic mode (ordered
+fold), and the non-deterministic per-XCD slot accumulation equal to it up to f32 summation order."""
 import pytest
 import torch
 
@@ -41,9 +42,9 @@ def test_linear_dw_rows(R, M, N, bias):
         assert (db - rb).abs().max().item() <= 2e-2 * dy.double().sum(0).abs().max().item() * abs(alpha) + 1e-4
     else:
         assert torch.equal(db, db0)
-    # ordered fold: a second identical call adds bitwise the same increment
+    # deterministic mode (ordered fold): a second identical call adds bitwise the same increment
     dW2 = dW0.clone()
-    with K.mode("bf16"):
+    with K.mode("bf16", True):
         K.linear_dw(dy, x, dW2, alpha=alpha, db=None)
         dW3 = dW0.clone()
         K.linear_dw(dy, x, dW3, alpha=alpha, db=None)
@@ -182,3 +183,33 @@ def test_wgrad_bf16_segments(nseg, seg, M, N):
     # seg_rows % 32 != 0 is refused by both
     assert not K.wgrad_bf16_seg_ok(seg + 8, M, N, seg + 8)
     assert not K.wgrad_bf16_seg_ok(17 * 64, M, N, 64)    # at most 16 segments
+
+
+@pytest.mark.parametrize("R,M,N,bias", [(12832, 352, 88, True), (12832, 88, 352, True), (12832, 88, 88, True),
+                                        (12832, 88, 1760, False), (4097, 264, 88, False)])
+def test_xcd_slots_match_ordered_fold(R, M, N, bias, monkeypatch):
+    """Non-deterministic mode adds each split's tile into one of 8 per-XCD slots with float atomics
+    (csrc/wgrad.hip GemmP::xslots) instead of one raw partial per split: same products, only the f32
+    summation order differs -- against the deterministic ordered fold <= 1e-5 relative, for the f32
+    (kdfm_gemm) and the bf16-operand (kdfm_wgrad_bf16) entry points; KDFM_WGR_XCD=0 restores the per-split
+    partials bitwise."""
+    from kdfm import kernels as K
+    g = torch.Generator(device="cuda").manual_seed(R + 5 * M + N)
+    dy = torch.randn(R, M, device="cuda", generator=g)
+    x = torch.randn(R, N, device="cuda", generator=g)
+    res = {}
+    for det, xcd in ((True, "1"), (False, "1"), (False, "0")):
+        monkeypatch.setenv("KDFM_WGR_XCD", xcd)
+        dW, db = torch.zeros(M, N, device="cuda"), torch.zeros(M, device="cuda")
+        dWh, dbh = torch.zeros(M, N, device="cuda"), torch.zeros(M, device="cuda")
+        with K.mode("bf16", det):
+            K.linear_dw(dy, x, dW, alpha=0.5, db=db if bias else None)
+            assert _route() == "wgrad_rows"
+            K.wgrad_bf16(dy.to(torch.bfloat16), x.to(torch.bfloat16), dWh, db=dbh if bias else None, alpha=0.5)
+        torch.cuda.synchronize()
+        res[(det, xcd)] = (dW, db, dWh, dbh)
+    ref = res[(True, "1")]
+    for a, b in zip(res[(False, "1")], ref):
+        assert (a - b).abs().max().item() <= 1e-5 * b.abs().max().item() + 1e-6
+    for a, b in zip(res[(False, "0")], ref):
+        assert torch.equal(a, b)
