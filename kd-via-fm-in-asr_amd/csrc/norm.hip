@@ -1,5 +1,5 @@
 // LayerNorm forward/backward (Conformer pre-norms, NeMo ConformerLayer norm_* with eps 1e-5;
-// called per layer from conformer_encoder.py:685-692).  One wave per row (d <= 256), fp32
+// called per layer from conformer_encoder.py:685-692).  One wave per row (d <= 1024), fp32
 // statistics; the backward fuses the residual-stream gradient add and reduces dgamma/dbeta with
 // per-block partials folded in block order (one fold launch can serve several LayerNorms).
 #include "common.h"
@@ -7,8 +7,9 @@
 namespace kdfm {
 namespace {
 
-constexpr int MAXV = 4;  // d <= 256
+constexpr int MAXV = 16;  // d <= 1024 (FastConformer d_model 512 / 1024); V = 64-column groups per lane
 
+template <int MAXV>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x, const float* __restrict__ g,
                                                      const float* __restrict__ b, float* __restrict__ y,
                                                      float* __restrict__ mean_out, float* __restrict__ rstd_out,
@@ -186,13 +187,31 @@ int ln_bwd_launch(const float* dy, const float* x, const float* gamma, const flo
                   const float* dres, float* dx, float* part, int64_t rows, int64_t d, hipStream_t st) {
   const int64_t blocks = ceil_div(rows, 4 * LN_RPW);
   const dim3 grid((unsigned)blocks), blk(256);
-  switch ((d + 63) / 64) {
-    case 1: hipLaunchKernelGGL(ln_bwd_kernel<1>, grid, blk, 0, st, dy, x, gamma, mean, rstd, dres, dx, part, rows, (int)d); break;
-    case 2: hipLaunchKernelGGL(ln_bwd_kernel<2>, grid, blk, 0, st, dy, x, gamma, mean, rstd, dres, dx, part, rows, (int)d); break;
-    case 3: hipLaunchKernelGGL(ln_bwd_kernel<3>, grid, blk, 0, st, dy, x, gamma, mean, rstd, dres, dx, part, rows, (int)d); break;
-    default: hipLaunchKernelGGL(ln_bwd_kernel<4>, grid, blk, 0, st, dy, x, gamma, mean, rstd, dres, dx, part, rows, (int)d); break;
-  }
+  const int64_t v = (d + 63) / 64;
+#define LNB(V) hipLaunchKernelGGL(ln_bwd_kernel<V>, grid, blk, 0, st, dy, x, gamma, mean, rstd, dres, dx, part, rows, (int)d)
+  if (v == 1) LNB(1);
+  else if (v == 2) LNB(2);
+  else if (v == 3) LNB(3);
+  else if (v == 4) LNB(4);
+  else if (v <= 8) LNB(8);
+  else LNB(16);
+#undef LNB
   return check_launch("kdfm_layernorm_bwd");
+}
+
+int ln_fwd_launch(const float* x, const float* gamma, const float* beta, float* y, float* mean, float* rstd,
+                  int64_t rows, int64_t d, float eps, hipStream_t st) {
+  const dim3 grid((unsigned)ceil_div(rows, 4)), blk(256);
+  const int64_t v = (d + 63) / 64;
+#define LNF(V) hipLaunchKernelGGL(ln_fwd_kernel<V>, grid, blk, 0, st, x, gamma, beta, y, mean, rstd, rows, (int)d, eps)
+  if (v == 1) LNF(1);
+  else if (v == 2) LNF(2);
+  else if (v == 3) LNF(3);
+  else if (v == 4) LNF(4);
+  else if (v <= 8) LNF(8);
+  else LNF(16);
+#undef LNF
+  return check_launch("kdfm_layernorm_fwd");
 }
 
 }  // namespace
@@ -204,11 +223,9 @@ int kdfm_layernorm_fwd(const float* x, const float* gamma, const float* beta, fl
                        int64_t rows, int64_t d, float eps, void* stream) {
   using namespace kdfm;
   KDFM_REQUIRE(x && gamma && beta && y && mean && rstd, "null pointer");
-  KDFM_REQUIRE(d > 0 && d <= 64 * MAXV, "d must be in (0, 256]");
+  KDFM_REQUIRE(d > 0 && d <= 64 * MAXV, "d must be in (0, 1024]");
   if (rows == 0) return KDFM_OK;
-  hipLaunchKernelGGL(ln_fwd_kernel, dim3((unsigned)ceil_div(rows, 4)), dim3(256), 0, as_stream(stream), x, gamma,
-                     beta, y, mean, rstd, rows, (int)d, eps);
-  return check_launch("kdfm_layernorm_fwd");
+  return ln_fwd_launch(x, gamma, beta, y, mean, rstd, rows, d, eps, as_stream(stream));
 }
 
 int64_t kdfm_layernorm_bwd_ws(int64_t rows, int64_t d) { return kdfm::ceil_div(rows, 4 * kdfm::LN_RPW) * 2 * d; }
@@ -218,7 +235,7 @@ int kdfm_layernorm_bwd(const float* dy, const float* x, const float* gamma, cons
                        void* stream) {
   using namespace kdfm;
   KDFM_REQUIRE(dy && x && gamma && mean && rstd && dx && dgamma && dbeta && ws, "null pointer");
-  KDFM_REQUIRE(d > 0 && d <= 64 * MAXV, "d must be in (0, 256]");
+  KDFM_REQUIRE(d > 0 && d <= 64 * MAXV, "d must be in (0, 1024]");
   if (rows == 0) return KDFM_OK;
   hipStream_t st = as_stream(stream);
   int rc = ln_bwd_launch(dy, x, gamma, mean, rstd, dres, dx, ws, rows, d, st);
@@ -234,7 +251,7 @@ int kdfm_layernorm_bwd_part(const float* dy, const float* x, const float* gamma,
                             void* stream) {
   using namespace kdfm;
   KDFM_REQUIRE(dy && x && gamma && mean && rstd && dx && part, "null pointer");
-  KDFM_REQUIRE(d > 0 && d <= 64 * MAXV, "d must be in (0, 256]");
+  KDFM_REQUIRE(d > 0 && d <= 64 * MAXV, "d must be in (0, 1024]");
   if (rows == 0) return KDFM_OK;
   return ln_bwd_launch(dy, x, gamma, mean, rstd, dres, dx, part, rows, d, as_stream(stream));
 }

@@ -556,10 +556,12 @@ int wr_launch(const GemmP& p, const WrPlan& pl, hipStream_t st) {
 
 // per-XCD slot accumulation (GemmP::xslots) for the register-staged kernel: non-deterministic mode
 // only (float atomics), and only where it saves traffic (>= 16 splits: 8 slots + a memset instead of
-// S raw partials written and read back).  KDFM_WGR_XCD=0 keeps the per-split partials.
+// S raw partials written and read back).  OFF by default (KDFM_WGR_XCD=1 enables it): in the step the
+// slot atomics + memset made the weight-gradient stream slower, not faster -- 2051 utt/s with the
+// per-split partials vs 1826 with the slots, same box, interleaved (profiles/r04/r4c_bench_*.log).
 constexpr int WR_XSLOTS = 8;
 bool wr_use_xslots(const WrPlan& pl) {
-  const int on = env_i("KDFM_WGR_XCD", 1);   // read per call, like KDFM_WGR_MSL (tests compare both)
+  const int on = env_i("KDFM_WGR_XCD", 0);   // read per call, like KDFM_WGR_MSL (tests compare both)
   return on && !deterministic() && !pl.dma && pl.S >= 2 * WR_XSLOTS;
 }
 

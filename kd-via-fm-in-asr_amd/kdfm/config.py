@@ -265,9 +265,20 @@ def meta_specs(cfg: Ver5Config) -> list:
                 (me + "attn.out_proj.weight", (Ci, Ci)), (me + "attn.out_proj.bias", (Ci,)),
                 (me + "linear1.weight", (Cs, Ci)), (me + "linear1.bias", (Cs,)),
                 (me + "linear2.weight", (Cs, Cs)), (me + "linear2.bias", (Cs,))]
-    # "conformer" (ConformerEncoder, :918-1020) and "unet" (UNet1D, :880-917; odd frame counts crash the
-    # reference's update x - v / S) are not on the engine
-    raise ValueError(f"encfm_meta must be 'mlp', 'cnn' or 'swin', got {cfg.encfm_meta!r}")
+    if cfg.encfm_meta == "conformer":   # ConformerEncoder (:1000-1020), kdfm/fmconf.py
+        from .fmconf import conformer_specs
+        return conformer_specs(Cs, E)
+    # "unet" (UNet1D, :880-917: odd frame counts crash the reference's update x - v / S) is not on the engine
+    raise ValueError(f"encfm_meta must be 'mlp', 'cnn', 'swin' or 'conformer', got {cfg.encfm_meta!r}")
+
+
+def meta_bn_specs(cfg: Ver5Config) -> list:
+    """BatchNorm running statistics of the FM meta-encoder (the conformer's 4 ConvModules), kept beside the
+    encoders' in the engine's buffer store."""
+    if cfg.kd_model != "encfm" or cfg.encfm_meta != "conformer":
+        return []
+    from .fmconf import bn_buffer_specs as conf_bn
+    return conf_bn(cfg.d_student)
 
 
 def encfm_specs(cfg: Ver5Config, trained: bool = True) -> list:
@@ -387,5 +398,5 @@ DEFAULT = Ver5Config()
 PARITY = DEFAULT.parity()
 
 __all__ = ["Ver5Config", "DEFAULT", "PARITY", "encoder_specs", "subsampling_specs", "sub_stages", "sub_pad",
-           "sub_channels", "sub_len", "sub_dims", "decoder_specs", "head_specs", "all_head_specs", "diffkd_specs", "encfm_specs", "meta_specs", "encfm_fixed_steps", "head_modules", "student_specs",
+           "sub_channels", "sub_len", "sub_dims", "decoder_specs", "head_specs", "all_head_specs", "diffkd_specs", "encfm_specs", "meta_specs", "meta_bn_specs", "encfm_fixed_steps", "head_modules", "student_specs",
            "teacher_specs", "bn_buffer_specs", "fused_groups", "field"]

@@ -254,7 +254,7 @@ def subsampling_backward(cfg, S: EncoderShapes, P, G, pre, ctx, dx, len1, *, see
             K.fill(gtm, 0.0)
             K.wgrad_bf16(dy2h, cols1, gtm.view(C, 9 * C), db=G[pre + "pre_encode.conv.2.bias"])
             K.convw_grad(gtm.view(C, 9 * C), G[pre + "pre_encode.conv.2.weight"].view(C, C, 9))
-        WGRAD.run(conv2_wgrad, dy2, cols1, dy2h, ctx["y1"])
+        WGRAD.run(conv2_wgrad, dy2, cols1, dy2h, ctx["y1"], len1)
     else:
         if ctx["y1"] is not None and ctx["y1"].dtype == torch.bfloat16:   # fused forward kept only the bf16 y1
             ctx["y1"] = ctx["y1"].float()
@@ -268,7 +268,7 @@ def subsampling_backward(cfg, S: EncoderShapes, P, G, pre, ctx, dx, len1, *, see
                 K.im2col_3x3s2(ctx["y1"], len1 if cfg.subsampling_mask else None, cols1, B, S.T1, S.F1, C)
             K.linear_dw(dy2, cols1, G[pre + "pre_encode.conv.2.weight"].view(C, 9 * C),
                         db=G[pre + "pre_encode.conv.2.bias"])
-        WGRAD.run(conv2_wgrad, dy2, cols1, ctx["y1"])
+        WGRAD.run(conv2_wgrad, dy2, cols1, ctx["y1"], len1)
     m = cfg.subsampling_mask
     if direct and B * S.T1 * S.F1 < (1 << 24):
         # direct transposed conv over the input positions' parity classes (no column matrix), the ReLU'
@@ -300,9 +300,13 @@ def subsampling_backward(cfg, S: EncoderShapes, P, G, pre, ctx, dx, len1, *, see
     # conv0 (1 -> C, 3x3, s2) weight gradient straight from the mel frames: the direct stride-2 kernel
     # of dw_striding's first stage (same layer), no im2col of the input, deterministic fold
     run = (lambda fn, *keep: fn()) if direct else WGRAD.run   # direct: the main stream is free here
+    # every tensor the side-stream launch reads stays referenced until the join (the frame lengths too: the
+    # module API frees its autograd ctx right after this backward, and a 16-byte length block is the first
+    # one the allocator hands out again)
     run(lambda: K.dwsub_conv_wgrad(dy1, len1 if m else None, ctx["mel"], ctx["mel_len"] if m else None,
                                          G[pre + "pre_encode.conv.0.weight"], G[pre + "pre_encode.conv.0.bias"],
-                                         B, S.Tm, cfg.nfilt, 1, C, S.T1, S.F1, S.pad), dy1, ctx["mel"])
+                                         B, S.Tm, cfg.nfilt, 1, C, S.T1, S.F1, S.pad), dy1, ctx["mel"], len1,
+        ctx["mel_len"])
     
 
 # ------------------------------------------------------------------------------------------------

@@ -100,14 +100,15 @@ class EncFMWorkspace:
         self.mean_steps.copy_(torch.tensor([float(s) for s in steps]))
 
 
-def encfm_forward(cfg, P, sfeats, tfeats, ws: EncFMWorkspace, *, seed=None, train=True, gumbel=None):
+def encfm_forward(cfg, P, sfeats, tfeats, ws: EncFMWorkspace, *, seed=None, train=True, gumbel=None,
+                  bn_running=None):
     """All layers' router + strategy + FM chain.  sfeats (L, B*T, Cs), tfeats (L, B*T, Ct) stacked hook
     outputs.  Returns ws.xS (B*T, Cs): the last layer's FM output, the decoder's input.  ws.stats holds
     [sum flow losses, router_weight * sum router losses, their sum (forward's total_loss), mean steps];
     ws.flow / ws.rloss / ws.mean_steps the per-layer values (the reference's log keys)."""
     if cfg.encfm_meta != "mlp":
         from .fmmeta import meta_forward
-        return meta_forward(cfg, P, sfeats, tfeats, ws)
+        return meta_forward(cfg, P, sfeats, tfeats, ws, seed=seed, bn_running=bn_running, train=train)
     L, B, T = cfg.n_layers, ws.B, ws.T
     Cs, Ct, H, Kmax = cfg.d_student, cfg.d_teacher, HIDDEN, cfg.router_max_steps
     fm, r = "flow_matching.", "router."
@@ -141,13 +142,13 @@ def encfm_forward(cfg, P, sfeats, tfeats, ws: EncFMWorkspace, *, seed=None, trai
     return ws.xS
 
 
-def encfm_backward(cfg, P, G, ws: EncFMWorkspace, dfeats, gxS, wgrad_run):
+def encfm_backward(cfg, P, G, ws: EncFMWorkspace, dfeats, gxS, wgrad_run, *, seed=None):
     """Data gradients into dfeats (L*B*T, Cs) (overwritten) from the flow losses, the router's entropy
     term and gxS (B*T, Cs) = d loss / d (last layer's FM output) through the decoder; the parameter
     gradients of flow_matching.* and router.* via `wgrad_run(fn, *keep)` (the weight-gradient stream)."""
     if cfg.encfm_meta != "mlp":
         from .fmmeta import meta_backward
-        meta_backward(cfg, P, G, ws, dfeats, gxS)
+        meta_backward(cfg, P, G, ws, dfeats, gxS, seed=seed)
         return
     L, B, T = cfg.n_layers, ws.B, ws.T
     Cs, Ct, H, Kmax = cfg.d_student, cfg.d_teacher, HIDDEN, cfg.router_max_steps

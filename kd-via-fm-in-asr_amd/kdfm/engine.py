@@ -14,7 +14,8 @@ import torch
 
 from . import _lib
 from . import kernels as K
-from .config import Ver5Config, all_head_specs, bn_buffer_specs, diffkd_specs, student_specs, teacher_specs
+from .config import (Ver5Config, all_head_specs, bn_buffer_specs, diffkd_specs, meta_bn_specs, student_specs,
+                     teacher_specs)
 from .conformer import EncoderRun, EncoderShapes, compute_lengths, encoder_backward, encoder_forward, \
     encoder_forward_steps, layer_images, make_workspace
 from .frontend import FrontendConsts, frontend_forward, mel_frames, specaugment_
@@ -79,7 +80,8 @@ class Ver5Engine:
         # before every use, asr_train_diffm.py:382-383, so AdamW never touches it)
         self.fixed = FlatStore(diffkd_specs(cfg, False) if cfg.use_diffkd else [], dev, with_grad=False)
         self.bn = FlatStore(bn_buffer_specs(cfg, cfg.d_student, "encoder.")
-                            + bn_buffer_specs(cfg, cfg.d_teacher, "teacher.encoder."), dev, with_grad=False)
+                            + bn_buffer_specs(cfg, cfg.d_teacher, "teacher.encoder.") + meta_bn_specs(cfg), dev,
+                            with_grad=False)
         self.fe = FrontendConsts(cfg, dev)
         self.seed = torch.zeros(1, dtype=torch.int64, device=dev)     # uint64 bits, advanced on device
         self.step = torch.zeros(1, dtype=torch.int64, device=dev)
@@ -240,6 +242,14 @@ class Ver5Engine:
         side = self._side_stream()
         tfeats = torch.empty(cfg.n_layers, St.rows, St.d, device=dev)
         tlogits = torch.empty(rows, Cn, device=dev)
+        n_st = cfg.n_layers * Ss.rows
+        # the teacher auto-encoder's outputs are written on the teacher stream: allocated BEFORE the teacher
+        # stream's join below, so a block the caching allocator hands over here cannot be one this stream
+        # frees later in the step (the student frontend's temporaries) and the teacher stream then overwrites
+        # while this stream still reads it (tools/race_check.py: preemph_pad.xp vs tae_forward's zt)
+        tae = None
+        if heads:
+            tae = (torch.empty(n_st, cfg.latent, device=dev), torch.empty(n_st, St.d, device=dev))
         if own_mel:
             # the teacher's own (undithered) frontend goes to the teacher stream with its encoder
             side.wait_stream(main)
@@ -270,10 +280,6 @@ class Ver5Engine:
         sgen = encoder_forward_steps(cfg, Ss, self.student.P, "encoder.", mel_s, mel_len, len1, len2, sfeats, pos_s,
                                      train=train, seed=seed, salt=SALT_STUDENT, save=save, bn_running=self.bn.P,
                                      use_batch_stats=train, ws=self._enc_ws(Ss, "encoder."), run=srun)
-        n_st = cfg.n_layers * Ss.rows
-        tae = None
-        if heads:
-            tae = (torch.empty(n_st, cfg.latent, device=dev), torch.empty(n_st, St.d, device=dev))
         h = self._heads_half(train, save) if heads else 0
         nb = h * Ss.rows
         hctx_b = None
@@ -316,7 +322,7 @@ class Ver5Engine:
             ews = self._encfm_ws(B, T)
             with K.region("encfm_forward"):
                 dec_in = encfm_forward(cfg, self.student.P, sfeats, tfeats, ews, seed=seed, train=train,
-                                       gumbel=self.encfm_gumbel)
+                                       gumbel=self.encfm_gumbel, bn_running=self.bn.P)
             self.encfm_stats = ews.stats
         logits = torch.empty(rows, Cn, device=dev)
         K.linear(dec_in, self.student.P["decoder.decoder_layers.0.weight"].view(Cn, Ss.d),
@@ -492,7 +498,7 @@ class Ver5Engine:
             K.linear_dx(g, Wd, ews.gxS)
             del g
             with K.region("encfm_backward"):
-                encfm_backward(cfg, P, G, ews, dfeats.view(n, Ss.d), ews.gxS, WGRAD.run)
+                encfm_backward(cfg, P, G, ews, dfeats.view(n, Ss.d), ews.gxS, WGRAD.run, seed=self.seed)
             if grad_ready is not None:
                 grad_ready(min(o for k, o in off.items() if not k.startswith(("encoder.", "decoder."))))
         elif ctx.get("hctx") is None:

@@ -14,9 +14,9 @@ one (rows, Cs+E) slab of a resident (sum S_i, rows, Cs+E) buffer, so x_{j+1} is 
 GEMM's residual epilogue straight into the next slab's first Cs columns (no separate x tensors), and
 the backward re-reads the slabs as its saved activations.  The cnn's k=3 conv is the implicit-GEMM
 conv3 (LD_CONV taps across utterance borders zero-padded, as Conv1d's pad=1); the swin's attention is
-the fused attention kernel pair (attn_fused.hip forward, attn_bwd.hip bwd2) with a zero positional
-table, i.e. plain softmax(q k^T / sqrt(dk)) v -- nn.MultiheadAttention without masks (every frame,
-padded ones included, as the reference).  Only fixed step counts (sampling_steps_per_layer): the
+kdfm/mha.py (the fused attention pair in bf16 math, the exact-f32 unfused form in parity math): plain
+softmax(q k^T / sqrt(dk)) v -- nn.MultiheadAttention without masks (every frame, padded ones included,
+as the reference).  Only fixed step counts (sampling_steps_per_layer): the
 router's per-utterance counts would put a device->host sync on the step to drive the per-step
 launches; with meta "mlp" the dynamic router path is kdfm/encfm.py.  Step counts: config.encfm_fixed_steps
 (sampling_steps_per_layer, else --flow_steps for every layer).  Parity: tests/golden/
@@ -24,24 +24,23 @@ kd_encfm_meta.npz (the reference's own classes).
 """
 from __future__ import annotations
 
-import math
-
 import torch
 
 from . import _lib
 from . import kernels as K
 from .config import encfm_fixed_steps
 from .encfm import schedule_coeffs
+from .mha import mha_bwd, mha_fwd
 
-META_TYPES = ("mlp", "cnn", "swin")
+META_TYPES = ("mlp", "cnn", "swin", "conformer")
 
 
 class MetaFMWorkspace:
     """Per-(B, T) resident buffers for the meta-encoder chain (fixed steps, so every size is static)."""
 
     def __init__(self, cfg, B, T, dev):
-        if cfg.encfm_meta not in ("cnn", "swin"):
-            raise ValueError(f"MetaFMWorkspace is for the cnn / swin meta-encoders, got {cfg.encfm_meta!r}")
+        if cfg.encfm_meta not in ("cnn", "swin", "conformer"):
+            raise ValueError(f"MetaFMWorkspace is for the cnn / swin / conformer meta-encoders, got {cfg.encfm_meta!r}")
         L, Cs, Ct, E = cfg.n_layers, cfg.d_student, cfg.d_teacher, cfg.time_embed_dim
         if cfg.encfm_dynamic:
             raise ValueError("meta_encoder 'cnn' / 'swin' run with fixed step counts (encfm_dynamic=False)")
@@ -71,6 +70,9 @@ class MetaFMWorkspace:
             self.act = f(N, n, Cs)
             self.w0f, self.w0b, self.g0 = f(Cs, 3 * Ci), f(Ci, 3 * Cs), f(Cs, 3 * Ci)
             self.da = f(n, Cs)
+        elif self.meta == "conformer":
+            from .fmconf import ConformerMeta
+            self.conf = ConformerMeta(cfg, n, B, T, N, dev)
         else:
             H = cfg.heads_student
             if Ci % H or (Ci // H) % 4 or Ci // H > 64:
@@ -78,18 +80,26 @@ class MetaFMWorkspace:
                                  "multiple of 4 and <= 64 (the fused attention kernels)")
             self.H = H
             self.qkv, self.q, self.o = f(N, n, 3 * Ci), f(N, n, Ci), f(N, n, Ci)
-            self.lse = f(N, B, H, T)
             self.ao, self.h = f(N, n, Ci), f(N, n, Cs)
-            self.ppos = torch.zeros(2 * T - 1, Ci, device=dev)
-            self.lens = torch.full((B,), T, dtype=torch.int64, device=dev)
             self.dpre, self.dao, self.do = f(n, Cs), f(n, Ci), f(n, Ci)
-            self.dqkv, self.dqu, self.dqv = f(n, 3 * Ci), f(n, Ci), f(n, Ci)
-            self.rsum = f(B * H * T)
-            self.ds, self.pd = K.attn_bwd2_saved(B, H, T, dev)
+            self.dqkv = f(n, 3 * Ci)
+            self.mha, self.att = None, None   # per-math attention buffers (kdfm/mha.py), made at first use
+        self.dev = dev
+
+    def attention(self):
+        """The attention buffers for the current math mode (fused bf16 pair or exact-f32 unfused form)."""
+        from .mha import MhaShape
+        fused = K.get_math() == "bf16"
+        if self.mha is None or self.mha.fused != fused:
+            self.mha = MhaShape(self.B, self.H, self.T, self.Ci, self.dev)
+            self.att = [self.mha.saves(self.dev) for _ in range(self.embed.shape[0])]
+        return self.mha
 
 
 def _names(meta):
     me = "flow_matching.meta_encoder."
+    if meta == "conformer":
+        return {}
     if meta == "cnn":
         return dict(w0=me + "0.weight", b0=me + "0.bias", w2=me + "2.weight", b2=me + "2.bias")
     return dict(win=me + "attn.in_proj_weight", bin=me + "attn.in_proj_bias", wo=me + "attn.out_proj.weight",
@@ -97,51 +107,56 @@ def _names(meta):
                 w2=me + "linear2.weight", b2=me + "linear2.bias")
 
 
-def _meta_fwd(ws, P, nm, k, out, R, rscale):
+def _meta_fwd(ws, P, nm, k, out, R, rscale, seed=None, bn_running=None, train=True):
     """One meta-encoder evaluation on slab k: out = v (R None) or R + rscale * v."""
     Cs = out.shape[1]
     x = ws.embed[k]
     epi = _lib.EPI_RESID if R is not None else 0
+    if ws.meta == "conformer":
+        from .fmconf import conformer_fwd
+        v = conformer_fwd(ws.conf, P, k, x, seed, bn_running, train)
+        if R is None:
+            K.axpby(v, None, out, 1.0, 0.0)
+        else:
+            K.axpby(R, v, out, 1.0, rscale)
+        return
     if ws.meta == "cnn":
         K.conv3(x, ws.w0f, P[nm["b0"]], ws.act[k], ws.T, epi=_lib.EPI_RELU)
         K.linear(ws.act[k], P[nm["w2"]].view(Cs, Cs), P[nm["b2"]], out, epi=epi, R=R, rscale=rscale)
         return
-    B, T, H, Ci = ws.B, ws.T, ws.H, ws.Ci
     K.linear(x, P[nm["win"]], P[nm["bin"]], ws.qkv[k])
-    K.axpby(ws.qkv[k][:, :Ci], None, ws.q[k], 1.0, 0.0)
-    K.relpos_attn_fwd(ws.q[k], ws.q[k], ws.qkv[k], ws.ppos, ws.lens, ws.o[k], None, None, B, H, T,
-                      1.0 / math.sqrt(Ci // H), 0.0, None, 0, lse=ws.lse[k])
+    mha_fwd(ws.attention(), ws.att[k], ws.qkv[k], ws.q[k], ws.o[k], 0.0, None, 0)   # MHA dropout 0 (:847)
     K.linear(ws.o[k], P[nm["wo"]], P[nm["bo"]], ws.ao[k])
     K.linear(ws.ao[k], P[nm["w1"]], P[nm["b1"]], ws.h[k], epi=_lib.EPI_RELU)
     K.linear(ws.h[k], P[nm["w2"]], P[nm["b2"]], out, epi=epi, R=R, rscale=rscale)
 
 
-def _meta_bwd(ws, P, G, nm, k, dv, dembed):
+def _meta_bwd(ws, P, G, nm, k, dv, dembed, seed=None):
     """dembed = d/d[x | e] of slab k's meta-encoder given dv; parameter gradients accumulated into G."""
     Cs = dv.shape[1]
     x = ws.embed[k]
+    if ws.meta == "conformer":
+        from .fmconf import conformer_bwd
+        conformer_bwd(ws.conf, P, G, k, x, dv, dembed, seed)
+        return
     if ws.meta == "cnn":
         K.linear_dw(dv, ws.act[k], G[nm["w2"]].view(Cs, Cs), db=G[nm["b2"]])
         K.linear_dx(dv, P[nm["w2"]].view(Cs, Cs), ws.da, epi=_lib.EPI_DRELU, aux=ws.act[k])
         K.conv3_dw(ws.da, x, ws.g0, ws.T, db=G[nm["b0"]])
         K.conv3(ws.da, ws.w0b, None, dembed, ws.T)
         return
-    B, T, H, Ci = ws.B, ws.T, ws.H, ws.Ci
     K.linear_dw(dv, ws.h[k], G[nm["w2"]], db=G[nm["b2"]])
     K.linear_dx(dv, P[nm["w2"]], ws.dpre, epi=_lib.EPI_DRELU, aux=ws.h[k])
     K.linear_dw(ws.dpre, ws.ao[k], G[nm["w1"]], db=G[nm["b1"]])
     K.linear_dx(ws.dpre, P[nm["w1"]], ws.dao)
     K.linear_dw(ws.dao, ws.o[k], G[nm["wo"]], db=G[nm["bo"]])
     K.linear_dx(ws.dao, P[nm["wo"]], ws.do)
-    K.relpos_attn_bwd2_dq(ws.do, ws.o[k], ws.q[k], ws.q[k], ws.qkv[k], ws.ppos, ws.lse[k], ws.lens, ws.rsum, ws.ds,
-                          ws.pd, ws.dqu, ws.dqv, B, H, T, 1.0 / math.sqrt(Ci // H), 0.0, None, 0)
-    K.relpos_attn_bwd2_dkv(ws.do, ws.q[k], ws.ds, ws.pd, ws.lens, ws.dqkv, B, H, T)
-    K.axpby(ws.dqu, None, ws.dqkv[:, :Ci], 1.0, 0.0)
+    mha_bwd(ws.attention(), ws.att[k], ws.qkv[k], ws.q[k], ws.o[k], ws.do, ws.dqkv, 0.0, None, 0)
     K.linear_dw(ws.dqkv, x, G[nm["win"]], db=G[nm["bin"]])
     K.linear_dx(ws.dqkv, P[nm["win"]], dembed)
 
 
-def meta_forward(cfg, P, sfeats, tfeats, ws: MetaFMWorkspace):
+def meta_forward(cfg, P, sfeats, tfeats, ws: MetaFMWorkspace, *, seed=None, bn_running=None, train=True):
     """All layers' FM chains.  sfeats (L, B*T, Cs) / tfeats (L, B*T, Ct) hook outputs; returns ws.xS, the
     last layer's FM output.  ws.stats = [sum of flow losses, 0, total, mean steps] as encfm_forward."""
     L, Cs, E, n = cfg.n_layers, cfg.d_student, cfg.time_embed_dim, ws.n
@@ -162,9 +177,9 @@ def meta_forward(cfg, P, sfeats, tfeats, ws: MetaFMWorkspace):
             K.axpby(wte, bte, ws.erow[k:k + 1], (S - j) / S, 1.0)          # time_embed(t), t = (S - j) / S
             K.axpby(ws.erow[k:k + 1].expand(n, E), None, slab[:, Cs:], 1.0, 0.0)
             if j < S - 1:   # x_{j+1} = x_j - v_j / S straight into the next slab
-                _meta_fwd(ws, P, nm, k, ws.embed[k + 1][:, :Cs], slab[:, :Cs], -1.0 / S)
+                _meta_fwd(ws, P, nm, k, ws.embed[k + 1][:, :Cs], slab[:, :Cs], -1.0 / S, seed, bn_running, train)
             else:
-                _meta_fwd(ws, P, nm, k, ws.vl, None, 0.0)
+                _meta_fwd(ws, P, nm, k, ws.vl, None, 0.0, seed, bn_running, train)
         last = ws.embed[b0 + S - 1][:, :Cs]
         if i == L - 1:
             K.axpby(last, ws.vl, ws.xS, 1.0, -1.0 / S)
@@ -178,7 +193,7 @@ def meta_forward(cfg, P, sfeats, tfeats, ws: MetaFMWorkspace):
     return ws.xS
 
 
-def meta_backward(cfg, P, G, ws: MetaFMWorkspace, dfeats, gxS):
+def meta_backward(cfg, P, G, ws: MetaFMWorkspace, dfeats, gxS, *, seed=None):
     """dfeats (L*B*T, Cs) (overwritten) = d loss / d s_i from the flow losses and gxS (d loss / d x_S of the
     last layer through the decoder); flow_matching.* parameter gradients accumulated into G."""
     L, Cs, E, n = cfg.n_layers, cfg.d_student, cfg.time_embed_dim, ws.n
@@ -204,7 +219,7 @@ def meta_backward(cfg, P, G, ws: MetaFMWorkspace, dfeats, gxS):
                 K.axpby(ws.dnsx, ws.gx if have_gx else None, ws.dv, ws.cv[i], -1.0 / S if have_gx else 0.0)
             else:
                 K.axpby(ws.gx, None, ws.dv, -1.0 / S, 0.0)
-            _meta_bwd(ws, P, G, nm, k, ws.dv, ws.dembed)
+            _meta_bwd(ws, P, G, nm, k, ws.dv, ws.dembed, seed)
             if have_gx:
                 K.axpby(ws.gx, ws.dembed[:, :Cs], ws.gx, 1.0, 1.0)
             else:

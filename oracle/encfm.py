@@ -86,7 +86,60 @@ def schedule_coeffs(S, schedule="rectified", vp=(19.9, 0.1)):
     return da / (-ds), -1.0 / (-ds)
 
 
-def meta_velocity(P, e, meta="mlp", heads=2):
+def _layer_norm(x, P, name, eps=1e-5):
+    return torch.nn.functional.layer_norm(x, (x.shape[-1],), P[name + ".weight"], P[name + ".bias"], eps)
+
+
+def _mha(x, P, name, heads):
+    """nn.MultiheadAttention(x, x, x) core, batch-first (B, T, C), no masks, dropout off (:847, :968)."""
+    B, T, C = x.shape
+    dk = C // heads
+    qkv = x @ P[name + ".in_proj_weight"].t() + P[name + ".in_proj_bias"]
+    q, k, v = (qkv[..., j * C:(j + 1) * C].reshape(B, T, heads, dk).transpose(1, 2) for j in range(3))
+    att = torch.softmax((q / math.sqrt(dk)) @ k.transpose(-1, -2), dim=-1)
+    return _lin((att @ v).transpose(1, 2).reshape(B, T, C), P, name + ".out_proj")
+
+
+def _conformer_meta(P, e, heads, bn_state=None, momentum=0.1, eps=1e-5):
+    """ConformerEncoder (:1000-1020) with dropouts off: input_proj, then 4 ConformerBlocks (:962-999),
+    each FF1 half step (norm_ff1 then the module's own LN, Linear -> SiLU -> Linear), MHA on mha_layer(x),
+    ConvModule (:932-961: LN -> pointwise_conv1 -> depthwise k=31 pad 15 -> BatchNorm1d with batch
+    statistics -> SiLU -> pointwise_conv2), FF2 half step, norm_final.  bn_state: {buffer name: tensor}
+    running statistics updated in place per call (training mode, unbiased variance, momentum 0.1)."""
+    me = "flow_matching.meta_encoder."
+    F_ = torch.nn.functional
+    x = _lin(e, P, me + "input_proj")
+    for l in range(4):
+        p = f"{me}layers.{l}."
+
+        def ff(y, name):
+            y = _layer_norm(y, P, p + name + ".net.0")
+            return _lin(F_.silu(_lin(y, P, p + name + ".net.1")), P, p + name + ".net.4")
+
+        x = x + 0.5 * ff(_layer_norm(x, P, p + "norm_ff1"), "ff1")
+        x = x + _mha(_layer_norm(x, P, p + "mha_layer"), P, p + "mha", heads)
+        c = p + "conv_module."
+        y = _layer_norm(x, P, c + "layer_norm").transpose(1, 2)
+        y = F_.conv1d(y, P[c + "pointwise_conv1.weight"], P[c + "pointwise_conv1.bias"])
+        C2 = y.shape[1]
+        y = F_.conv1d(y, P[c + "depthwise_conv.weight"], P[c + "depthwise_conv.bias"], padding=15, groups=C2)
+        mean = y.mean(dim=(0, 2))
+        var = y.var(dim=(0, 2), unbiased=False)
+        if bn_state is not None:
+            n = y.shape[0] * y.shape[2]
+            rm, rv = bn_state[c + "batch_norm.running_mean"], bn_state[c + "batch_norm.running_var"]
+            rm.mul_(1 - momentum).add_(momentum * mean.detach())
+            rv.mul_(1 - momentum).add_(momentum * var.detach() * n / (n - 1))
+        y = (y - mean[None, :, None]) / torch.sqrt(var[None, :, None] + eps)
+        y = y * P[c + "batch_norm.weight"][None, :, None] + P[c + "batch_norm.bias"][None, :, None]
+        y = F_.conv1d(F_.silu(y), P[c + "pointwise_conv2.weight"], P[c + "pointwise_conv2.bias"])
+        x = x + y.transpose(1, 2)
+        x = x + 0.5 * ff(_layer_norm(x, P, p + "norm_ff2"), "ff2")
+        x = _layer_norm(x, P, p + "norm_final")
+    return x
+
+
+def meta_velocity(P, e, meta="mlp", heads=2, bn_state=None):
     """FlowMatchingModule.meta_encoder on e = [x; te(t)] (B, T, Cs+E) -> v (B, T, Cs) (:1244-1259, 1328-1345).
     mlp: W2 relu(W1 e + b1) + b2.  cnn: Conv1d(k=3, pad 1 per utterance) -> ReLU -> Conv1d(k=1) over the
     frames.  swin (SwinTransformerEncoder :844-866): nn.MultiheadAttention(e, e, e) over the T frames of
@@ -106,10 +159,12 @@ def meta_velocity(P, e, meta="mlp", heads=2):
         o = (att @ v).transpose(1, 2).reshape(B, T, C)
         ao = _lin(o, P, me + "attn.out_proj")
         return _lin(torch.relu(_lin(ao, P, me + "linear1")), P, me + "linear2")
-    raise ValueError(f"meta-encoder {meta!r} not in the oracle (mlp, cnn, swin)")
+    if meta == "conformer":
+        return _conformer_meta(P, e, heads, bn_state)
+    raise ValueError(f"meta-encoder {meta!r} not in the oracle (mlp, cnn, swin, conformer)")
 
 
-def fm_forward(P, x0, tf, S, schedule="rectified", meta="mlp", heads=2):
+def fm_forward(P, x0, tf, S, schedule="rectified", meta="mlp", heads=2, bn_state=None):
     """FlowMatchingModule.forward, shape_transform 'linear', loss 'mse' (:1318-1377): for i = S..1,
     t = i/S: v = meta_encoder([x; te(t)]) (meta_velocity), x <- x - v/S; then
     loss = mean((Wst nsx + bst - t_f)^2) with nsx from the LAST velocity and the ORIGINAL input.
@@ -119,7 +174,7 @@ def fm_forward(P, x0, tf, S, schedule="rectified", meta="mlp", heads=2):
     for i in range(S, 0, -1):
         tt = torch.full(x0.shape[:-1] + (1,), i / S, dtype=x0.dtype)
         te = _lin(tt, P, "flow_matching.time_embed")
-        v = meta_velocity(P, torch.cat([x, te], dim=-1), meta, heads)
+        v = meta_velocity(P, torch.cat([x, te], dim=-1), meta, heads, bn_state)
         x = x - v / S
     ca, cv = schedule_coeffs(S, schedule)
     nsx = ca * x0 + cv * v
@@ -127,13 +182,13 @@ def fm_forward(P, x0, tf, S, schedule="rectified", meta="mlp", heads=2):
     return ((tr - tf) ** 2).mean(), x
 
 
-def encfm_fixed_forward(P, sfeats, tfeats, steps, schedule="rectified", meta="mlp", heads=2):
+def encfm_fixed_forward(P, sfeats, tfeats, steps, schedule="rectified", meta="mlp", heads=2, bn_state=None):
     """use_dynamic_steps=False with sampling_steps_per_layer (:639-641): no router, layer i runs steps[i]
     FM steps; same result dict as encfm_forward (router losses 0)."""
     flows = []
     fm_out = None
     for i, (s, t) in enumerate(zip(sfeats, tfeats)):
-        fl, fm_out = fm_forward(P, s, t, int(steps[i]), schedule, meta, heads)
+        fl, fm_out = fm_forward(P, s, t, int(steps[i]), schedule, meta, heads, bn_state)
         flows.append(fl)
     total = sum(flows[1:], flows[0])
     B = sfeats[0].shape[0]

@@ -40,3 +40,17 @@ def inputs(z, seed=SEED, Cs=88, Ct=176):
     t = [torch.randn(B, T, Ct, generator=gi) for _ in range(L)]
     R = torch.randn(B, T, Cs, generator=gi)
     return s, t, R
+
+
+def bn_init(z, meta):
+    """BatchNorm running statistics at construction (mean 0, var 1), float64, named as the fixture's
+    buffers (empty for meta-encoders without BatchNorm)."""
+    out = {}
+    pre = meta + ".buffer."
+    for k in z:
+        if k.startswith(pre) and k.endswith(("running_mean", "running_var")):
+            name = k[len(pre):]
+            shape = z[k].shape
+            out[name] = torch.zeros(shape, dtype=torch.float64) if name.endswith("mean") else \
+                torch.ones(shape, dtype=torch.float64)
+    return out

@@ -59,6 +59,7 @@ def _close(a, b, tol, what, rn=None):
     (8, False, 64, "f32", 1e-4, None),
     (8, True, 32, "f32", 1e-4, None),
     (16, True, 16, "f32", 1e-4, None),
+    (8, False, 256, "f32", 1e-4, None),    # FastConformer's 256 channels (fast-conformer_ctc_bpe.yaml:122-125)
     (8, False, 64, "bf16", 1e-1, 3e-2),
 ])
 def test_module_matches_oracle(factor, causal, C, math, tol, rn):

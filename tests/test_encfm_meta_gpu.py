@@ -1,12 +1,9 @@
 """The cnn / swin FM meta-encoders on the engine (kdfm/fmmeta.py) against (a) tests/golden/
 kd_encfm_meta.npz, made from the reference's own FlowMatchingModule / SwinTransformerEncoder
-(make_golden_encfm_meta.py; asr_train.py:844-866, 1220-1377), and (b) the whole training step of the
-asr_train.py family with that meta-encoder vs oracle/ver5.py (fixed steps) in float64.
-
-The meta-encoder GEMMs run bf16 MFMA with f32 state (the swin attention is the fused bf16 attention
-pair): flow losses rtol 2e-2, FM output and every FM / feature gradient relative Frobenius <= 3e-2 (the
-tolerance of the other bf16 FM chains); whole step as test_encfm_gpu.py (losses rtol 2e-2, gradients
-relative Frobenius <= 5e-2)."""
+(make_golden_encfm_meta.py; asr_train.py:844-1020, 1220-1377) -- in f32 math exactly, in bf16 math at the bf16 tolerances below --
+and (b) the whole training step of the asr_train.py family with that meta-encoder (PARITY: f32 math,
+deterministic, dropout off, fixed steps) vs oracle/ver5.py in float64: losses rtol 1e-4, every trainable
+gradient relative Frobenius <= 1e-3."""
 from dataclasses import replace
 
 import numpy as np
@@ -24,17 +21,30 @@ def _rel(a, b):
     return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
 
 
-@pytest.mark.parametrize("meta", ["cnn", "swin"])
-def test_meta_matches_reference(meta):
+# bf16-math tolerance on the parameter gradients (relative Frobenius).  cnn: the GEMMs' bf16 operands
+# only (measured <= 1.6e-2).  swin: + the fused attention pair's bf16 P / dS, whose error the time
+# embedding and the in / out projections collect through both chained steps (measured 3.0-5.8e-2 against
+# the reference, 2-2.7e-2 with exact-f32 GEMMs around the same bf16 attention: profiles/r04/swin_diag.log).
+BF16_GRAD_TOL = {"cnn": 3e-2, "swin": 8e-2, "conformer": 8e-2}
+
+
+@pytest.mark.parametrize("math", ["f32", "bf16"])
+@pytest.mark.parametrize("meta", ["cnn", "swin", "conformer"])
+def test_meta_matches_reference(meta, math):
+    """f32 math: every kernel on the path exact f32 (the attention in its unfused f32 form) -- losses rtol
+    1e-5, FM output / feature gradients / parameter gradients relative Frobenius <= 1e-4 (BatchNorm's
+    analytically-zero depthwise bias gradient: |g| < 1e-4, as the reference's own f32 residue), BatchNorm
+    running statistics rtol 1e-4.  bf16 math: flow losses rtol 2e-2, FM output and feature gradients
+    <= 3e-2, parameter gradients <= BF16_GRAD_TOL[meta]."""
     from kdfm import kernels as K
-    from kdfm.config import DEFAULT, encfm_specs
+    from kdfm.config import DEFAULT, encfm_specs, meta_bn_specs
     from kdfm.encfm import encfm_backward, encfm_forward
     from kdfm.fmmeta import MetaFMWorkspace
     z = FX.load()
     L, B, T = int(z["meta.L"]), int(z["meta.B"]), int(z["meta.T"])
     steps = tuple(int(x) for x in z["meta.steps"])
     cfg = replace(DEFAULT, n_layers=L, kd_model="encfm", encfm_meta=meta, encfm_dynamic=False,
-                  encfm_steps_per_layer=steps, heads_student=2)
+                  encfm_steps_per_layer=steps, heads_student=2, dropout=0.0)
     dev = torch.device("cuda")
     P = {k: v.to(dev).contiguous() for k, v in FX.params(z, meta).items()}
     s, t, R = FX.inputs(z)
@@ -42,29 +52,45 @@ def test_meta_matches_reference(meta):
     td = torch.stack([x.reshape(B * T, -1) for x in t]).to(dev).contiguous()
     Rd = R.reshape(B * T, -1).to(dev).contiguous()
     G = {n: torch.zeros(shape, device=dev) for n, shape in encfm_specs(cfg)}
+    bn = {n: (torch.ones if n.endswith("running_var") else torch.zeros)(shape, device=dev)
+          for n, shape in meta_bn_specs(cfg)}
     ws = MetaFMWorkspace(cfg, B, T, dev)
-    with K.mode("bf16", True):
-        encfm_forward(cfg, P, sd, td, ws, train=True)
+    with K.mode(math, True):
+        encfm_forward(cfg, P, sd, td, ws, train=True, bn_running=bn)
         dfeats = torch.empty(L * B * T, cfg.d_student, device=dev)
         encfm_backward(cfg, P, G, ws, dfeats, Rd, lambda fn, *keep: fn())
     torch.cuda.synchronize()
     pre = meta + "."
-    np.testing.assert_allclose(ws.flow.cpu().numpy(), z[pre + "flow"], rtol=2e-2)
-    np.testing.assert_allclose(ws.stats[2].item(), float(z[pre + "total"]), rtol=2e-2)
-    assert _rel(ws.xS.view(B, T, -1), z[pre + "fm_out"]) <= 3e-2
+    exact = math == "f32"
+    np.testing.assert_allclose(ws.flow.cpu().numpy(), z[pre + "flow"], rtol=1e-5 if exact else 2e-2)
+    np.testing.assert_allclose(ws.stats[2].item(), float(z[pre + "total"]), rtol=1e-5 if exact else 2e-2)
+    tol = 1e-4 if exact else 3e-2
+    assert _rel(ws.xS.view(B, T, -1), z[pre + "fm_out"]) <= tol
     d = dfeats.view(L, B, T, -1)
     for i in range(L):
         r = _rel(d[i], z[pre + f"grad.s{i}"])
-        assert r <= 3e-2, f"d/ds layer {i}: {r:.3e}"
-    bad = []
+        assert r <= tol, f"d/ds layer {i}: {r:.3e}"
+    gtol = 1e-4 if exact else BF16_GRAD_TOL[meta]
+    bad, worst = [], 0.0
     for n, gr in G.items():
-        r = _rel(gr, z[pre + "grad." + n])
-        if r > 3e-2:
+        ref = z[pre + "grad." + n]
+        if n.endswith("depthwise_conv.bias"):   # analytically zero (batch-statistics BatchNorm)
+            assert gr.abs().max().item() < 1e-4 and np.abs(ref).max() < 1e-4, n
+            continue
+        r = _rel(gr, ref)
+        worst = max(worst, r)
+        if r > gtol:
             bad.append(f"{n}: {r:.3e}")
+    print(f"{meta} {math}: worst parameter-gradient error {worst:.3e}")
     assert not bad, bad
+    for n, v in bn.items():   # running statistics after sum(steps) module calls
+        if exact:
+            np.testing.assert_allclose(v.cpu().numpy(), z[pre + "buffer." + n], rtol=1e-4, atol=1e-6)
+        else:
+            assert _rel(v, z[pre + "buffer." + n]) <= 3e-2, n
 
 
-@pytest.mark.parametrize("meta", ["cnn", "swin"])
+@pytest.mark.parametrize("meta", ["cnn", "swin", "conformer"])
 def test_meta_engine_step_matches_oracle(meta):
     import test_step_parity_gpu as SP
     from oracle import ver5 as O
@@ -87,14 +113,16 @@ def test_meta_engine_step_matches_oracle(meta):
         p[k] = p[k].clone().requires_grad_(True)
     out = O.ver5_step(p, wav.double(), wl, tg, tgl, ocfg, None)
     ref = torch.stack([out["loss"], out["ctc"], out["kl"], out["recon"], out["fm"]]).detach().float()
-    torch.testing.assert_close(losses, ref, rtol=2e-2, atol=1e-3)
+    torch.testing.assert_close(losses, ref, rtol=1e-4, atol=1e-5)
     og = torch.autograd.grad(out["loss"], [p[k] for k in names], allow_unused=True)
     bad = []
     for k, gr in zip(names, og):
         gr = torch.zeros_like(p[k]) if gr is None else gr
         if k.endswith(SP.ANALYTIC_ZERO) or gr.norm() == 0:
             continue
+        if k.endswith("depthwise_conv.bias"):
+            continue
         r = _rel(grads[k], gr)
-        if r > 5e-2:
+        if r > 1e-3:
             bad.append(f"{k}: {r:.3e}")
     assert not bad, bad

