@@ -158,6 +158,14 @@ int kdfm_gemm(const kdfm_gemm_desc* d, void* stream);
 int64_t kdfm_wgrad_bf16_ws(int64_t rows, int64_t M, int64_t N, int32_t bias);
 int kdfm_wgrad_bf16(const uint16_t* dY, const uint16_t* X, float* dW, int64_t ldc, float* db, int64_t rows,
                     int64_t M, int64_t N, float alpha, float* ws, int64_t ws_len, void* stream);
+/* Two weight gradients of the SAME shape in one launch (paired): dW (+)= alpha dY^T X and dW2 (+)= alpha
+ * dY2^T X2 (+ db / db2 column sums, both or neither), one grid of 2x the single launch's workgroups and one
+ * fold launch -- each product bitwise equal to its own kdfm_wgrad_bf16.  Used for the Conformer layer's
+ * same-shape products (feed_forward1/2 linear1 and linear2, linear_out with pointwise_conv2): half the
+ * launches on the weight-gradient stream.  ws >= 2 * kdfm_wgrad_bf16_ws(rows, M, N, bias) floats. */
+int kdfm_wgrad_bf16_pair(const uint16_t* dY, const uint16_t* X, float* dW, float* db, const uint16_t* dY2,
+                         const uint16_t* X2, float* dW2, float* db2, int64_t ldc, int64_t rows, int64_t M, int64_t N,
+                         float alpha, float* ws, int64_t ws_len, void* stream);
 /* The same over nseg = rows / seg_rows stacked segments (seg_rows % 32 == 0, nseg <= 16) with one bias
  * gradient per segment: db[j][m] += alpha * sum_{r in segment j} dY[r][m] (db is (nseg, M), required),
  * dW summed over all rows -- the FM chain's first-layer weight over its S steps in one launch
@@ -216,7 +224,8 @@ int kdfm_relpos_attn_bwd(const float* dO, const float* O, const float* qu, const
                          float* ws, int64_t ws_len, int64_t B, int64_t H, int64_t T, int64_t d, float scale,
                          float dropout_p, const uint64_t* seed, uint64_t rng_stream, void* stream);
 /* The backward in three kernels over SAVED probabilities (bwd2; the forward then writes only lse):
- *   _dq: r_i = dO_i . O_i into rsum (B*H*T floats), then dqu / dqv exactly as above, and the bf16 score
+ *   _dq: r_i = dO_i . O_i into rsum (B*H*T floats), then dqu / dqv exactly as above (with the forward's key /
+ *        value centring: dPd_ij = dO_i . (V_j - vc) + dO_i . vc, the second term in f32), and the bf16 score
  *        gradient dS and dropout-masked probabilities Pd = dropout(P) of every (i, j < len) written into
  *        ds / pd, each (B, H, T, ldt) with ldt = kdfm_relpos_attn_bwd2_ldt(T) (T rounded up to 8; keys
  *        >= len in the last written 64-key block are 0, key blocks past len and rows >= T unwritten);
@@ -622,7 +631,10 @@ int kdfm_relpos_table(float* pe, int64_t T, int64_t d, void* stream);
  * (kdfm_relpos_attn_bwd's operand; 3e38 for rows without a valid key).  In the one-pass mode p_tilde
  * (B,H,T,T) bf16 = exp(s_ij - m_i,kb) before dropout and m_blk (B,H,T,ceil(T/64)) = the running row max
  * m_i,kb after key block kb are written when non-null (pairs with lse; entries at i or j >= length are not
- * written and not read).  dk = d/H <= 48. */
+ * written and not read).  dk = d/H <= 64.  K and V are centred before their bf16 rounding on kc / vc, the
+ * mean of the utterance's first min(length, 16) (rounded down to a power of two) key / value rows: scores,
+ * lse, p_tilde and m_blk are those of the centred keys (softmax is invariant; the backward kernels centre
+ * identically) and O_i = sum_j Pdrop_ij (V_j - vc) + (sum_j Pdrop_ij) vc. */
 int kdfm_relpos_attn_fwd(const float* qu, const float* qv, const float* qkv, const float* pos,
                          const int64_t* lengths, float* o, float* P, float* Pdrop, float* lse, uint16_t* p_tilde,
                          float* m_blk, int64_t B, int64_t H,

@@ -24,6 +24,7 @@
 // The dropout mask is the forward's counter-RNG draw (same index -> same mask).  Every output
 // element is owned by one workgroup and the fold is ordered: deterministic, no atomics.
 #include "gemm_common.h"
+#include "attn_centre.h"
 
 // timing probe points (tools/attn_bwd_probe.hip defines KPROBE; empty in the library)
 #ifndef KPROBE
@@ -172,6 +173,7 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dq_kernel(AbP p
   // SAVE (bwd2): per wave Pd tile [16][LW] bf16; dS and Pd leave as 16-byte buffer stores (fixed count per
   // lane and key block, out-of-range chunks dropped by the range check)
   __shared__ __attribute__((aligned(16))) uint16_t Pdw[SAVE ? 4 : 1][SAVE ? 16 * LW : 8];
+  __shared__ __attribute__((aligned(16))) float Cn[2][64];   // the forward's key / value centre (attn_centre.h)
 
   KPROBE(0);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -223,6 +225,48 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dq_kernel(AbP p
     fetch_rows<2 * NU>(nb, p.pos, p.d, 0, rbase, 127, 0, npos, hoff, dk);
   };
 
+  // the forward's centring (attn_centre.h): K rows staged as K_j - kc (the scores, hence P = exp(s - lse),
+  // are the forward's), V rows as V_j - vc with cs_i = dO_i . vc added back to dPd in f32
+  kv_centre(p.k + b * p.T * p.ldkv + hoff, p.v + b * p.T * p.ldkv + hoff, p.ldkv, len, dk, Cn);
+  float4 ck[NU], cv[NU];
+  {
+    const int cq = dk >> 2;
+#pragma unroll
+    for (int it = 0; it < NU; ++it) {
+      const int e = threadIdx.x + it * 256;
+      const int c4 = (e - (e / cq) * cq) * 4;
+      ck[it] = *reinterpret_cast<const float4*>(&Cn[0][c4]);
+      cv[it] = *reinterpret_cast<const float4*>(&Cn[1][c4]);
+    }
+  }
+  // cs_i for this lane's C-layout rows: row (lane & 15) of the wave's 16 dotted in f32 by its 4 lane groups
+  // (16 columns each), summed across them, then picked up by the lanes owning each row
+  float cs[4];
+  {
+    const int q = lane >> 4;
+    float part = 0.f;
+    if (iq < T) {
+      const float* dor = p.dO + (b * p.T + iq) * p.ldq + hoff;
+#pragma unroll
+      for (int c = 16 * q; c < 16 * q + 16; ++c)
+        if (c < dk) part += dor[c] * Cn[1][c];
+    }
+    part += __shfl_xor(part, 16, 64);
+    part += __shfl_xor(part, 32, 64);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) cs[r] = __shfl(part, 4 * q + r, 64);
+  }
+  // subtract the centre from the staged rows of keys [j0, j0 + BK) that are valid (rows past len stay 0)
+  auto centre = [&](float4 (&v)[NU], const float4 (&c)[NU], int j0) {
+    const int cq = dk >> 2;
+#pragma unroll
+    for (int it = 0; it < NU; ++it) {
+      const int e = threadIdx.x + it * 256;
+      const bool ok = e < BK * cq && j0 + e / cq < len;
+      if (ok) v[it] = make_float4(v[it].x - c[it].x, v[it].y - c[it].y, v[it].z - c[it].z, v[it].w - c[it].w);
+    }
+  };
+
   f32x4 aq[NU], av[NU];
 #pragma unroll
   for (int u = 0; u < NU; ++u) { aq[u] = f32x4{0.f, 0.f, 0.f, 0.f}; av[u] = aq[u]; }
@@ -238,6 +282,8 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dq_kernel(AbP p
   for (int kb = 0; kb < nkb; ++kb) {
     const int j0 = kb * BK;
     __syncthreads();
+    centre(nk, ck, j0);
+    centre(nv, cv, j0);
     put_rows<NU>(Vs, nullptr, 0, nv, BK, dk);
     put_rows<NU>(Ks, nullptr, 0, nk, BK, dk);
     put_rows<2 * NU>(Pr, nullptr, 0, nb, 127, dk);
@@ -301,7 +347,7 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dq_kernel(AbP p
         const int i = ib + r, j = j0 + 16 * t + (lane & 15);
         float ds = 0.f, pdv = 0.f;
         if (i < len && j < len) {
-          float g = a[t][r];
+          float g = a[t][r] + cs[r];
           bool kp = true;
           if (p.p_drop > 0.f) {
             kp = dropout_keep(seed, p.rng_stream, (uint64_t)(prow0 + (int64_t)r * p.T + j), p.p_drop);

@@ -1,0 +1,39 @@
+// Key / value centring of the fused relative-position attention (attn_fused.hip forward, attn_bwd.hip dQ
+// kernel).  K and V enter the bf16 MFMAs as K_j - kc and V_j - vc, kc / vc = the mean of the utterance's
+// first n key / value rows (this head's columns), n = min(length, 16) rounded down to a power of two.
+// Scores move by q_i . kc, the same along a row, so softmax is unchanged; O_i = sum_j Pd_ij (V_j - vc) +
+// (sum_j Pd_ij) vc and dPd_ij = dO_i . (V_j - vc) + dO_i . vc with the second terms in f32.  A component
+// the keys / values share (a per-channel offset common to all frames) then never goes through the bf16
+// rounding, whose error it would scale (7 % on the FastConformer layer-0 q/k gradients before,
+// tools/attn_small_diag.py); a mean rather than one row keeps zero-mean keys' rounding error unchanged.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace kdfm {
+
+// c[0][0..dk) = kc, c[1][0..dk) = vc (zeros for an empty utterance).  Every thread of the block must call
+// it (ends with a barrier); rows are summed in order by one thread per float4 column group, so the forward
+// and the backward compute the same bits.
+__device__ __forceinline__ void kv_centre(const float* kbase, const float* vbase, int64_t ld, int len, int dk,
+                                          float (*c)[64]) {
+  const int cq = dk >> 2;
+  const int t = threadIdx.x;
+  if (t < 2 * cq) {
+    const bool isv = t >= cq;
+    const int c4 = (isv ? t - cq : t) * 4;
+    const float* src = (isv ? vbase : kbase) + c4;
+    const int n = len >= 16 ? 16 : len >= 8 ? 8 : len >= 4 ? 4 : len >= 2 ? 2 : (len > 0 ? 1 : 0);
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int r = 0; r < n; ++r) {
+      const float4 v = *reinterpret_cast<const float4*>(src + (int64_t)r * ld);
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    const float inv = n > 0 ? 1.f / (float)n : 0.f;   // a power of two: exact
+    float* o = c[isv ? 1 : 0] + c4;
+    o[0] = s.x * inv; o[1] = s.y * inv; o[2] = s.z * inv; o[3] = s.w * inv;
+  }
+  __syncthreads();
+}
+
+}  // namespace kdfm

@@ -19,6 +19,7 @@
 //     the P / P_drop outputs the per-op backward reads.
 // Output O is written straight into the (rows, d) head-interleaved layout.
 #include "gemm_common.h"
+#include "attn_centre.h"
 
 // timing probe points (tools/attn_probe.hip defines KPROBE; empty in the library)
 #ifndef KPROBE
@@ -102,6 +103,7 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void relpos_attn_fwd_kernel(A
   __shared__ __attribute__((aligned(16))) uint16_t Pr[BAND * LDR];
   __shared__ __attribute__((aligned(16))) float Gs[4][16 * LDG];
   __shared__ __attribute__((aligned(16))) uint16_t Ps[4][16 * LDPS];
+  __shared__ __attribute__((aligned(16))) float Cn[2][64];   // key / value centre (attn_centre.h)
 
   KPROBE(0);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -181,6 +183,15 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void relpos_attn_fwd_kernel(A
   const float* kbase = p.k + b * p.T * p.ldkv + hoff;
   const float* vbase = p.v + b * p.T * p.ldkv + hoff;
   const float* pbase = p.pos + hoff;
+  // key / value centring (attn_centre.h): K and V are staged as bf16(K_j - kc) and bf16(V_j - vc); the
+  // scores (hence lse, p~, m_blk) are those of the centred keys, O gets (sum_j Pd_ij) vc back in f32
+  kv_centre(kbase, vbase, p.ldkv, min(len, T), dk, Cn);
+  float4 ck4[KU], cv4[KU];
+#pragma unroll
+  for (int i = 0; i < KU; ++i) {
+    ck4[i] = *reinterpret_cast<const float4*>(&Cn[0][kc[i]]);
+    cv4[i] = *reinterpret_cast<const float4*>(&Cn[1][kc[i]]);
+  }
   float4 rk[KU], rv[KU], rp[PU];
   uint32_t kok = 0u, pok = 0u;   // validity of the staged slots of the stage in flight
   auto load_stage = [&](int j0, bool with_v) {
@@ -210,9 +221,11 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void relpos_attn_fwd_kernel(A
     for (int i = 0; i < KU; ++i) {
       if ((kin >> i) & 1u) {
         const bool ok = (kok >> i) & 1u;
-        store4_bf16(Ks + kj[i] * LDR + kc[i], ok ? rk[i] : z);
+        const float4 kk = make_float4(rk[i].x - ck4[i].x, rk[i].y - ck4[i].y, rk[i].z - ck4[i].z, rk[i].w - ck4[i].w);
+        store4_bf16(Ks + kj[i] * LDR + kc[i], ok ? kk : z);
         if (with_v) {
-          const float4 vv = ok ? rv[i] : z;
+          const float4 vc = make_float4(rv[i].x - cv4[i].x, rv[i].y - cv4[i].y, rv[i].z - cv4[i].z, rv[i].w - cv4[i].w);
+          const float4 vv = ok ? vc : z;
           Vt[(kc[i] + 0) * LDVT + kj[i]] = f2bf(vv.x);
           Vt[(kc[i] + 1) * LDVT + kj[i]] = f2bf(vv.y);
           Vt[(kc[i] + 2) * LDVT + kj[i]] = f2bf(vv.z);
@@ -318,6 +331,7 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void relpos_attn_fwd_kernel(A
     rowin[r] = ib + r < T;
   }
   const bool drop = p.p_drop > 0.f;
+  float ps[4] = {0.f, 0.f, 0.f, 0.f};   // sum_j Pd_ij (dropout only; rescaled with O in the online softmax)
   KPROBE(1);
   // single pass: only the key blocks with a valid key (the p~ zeros of the first block past them are
   // written after the loop), and the next stage is always loaded (the last block reloads itself), so
@@ -357,6 +371,7 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void relpos_attn_fwd_kernel(A
         for (int t = 0; t < 4; ++t) sum += (s[t][r] > -1.0e38f) ? __expf(s[t][r] - mn) : 0.f;
         lrow[r] = lrow[r] * corr + group16_sum(sum);
         mrow[r] = mn;
+        ps[r] *= corr;
 #pragma unroll
         for (int u = 0; u < NU; ++u) oacc[u][r] *= corr;
       }
@@ -370,6 +385,7 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void relpos_attn_fwd_kernel(A
     }
     KPROBE(3 + 4 * kb);
     uint16_t* Pw = Ps[w];
+    float pds[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
@@ -381,8 +397,10 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void relpos_attn_fwd_kernel(A
           __builtin_amdgcn_raw_buffer_store_b16(f2bf(pv), rpt, (rowin[r] && j < T) ? (uint32_t)((prow[r] + j) * 2) : OOB,
                                                 0, 0);
         float pdv = pv;
-        if (drop)   // (a zero probability stays zero either way: no per-element branch on it)
+        if (drop) {   // (a zero probability stays zero either way: no per-element branch on it)
           pdv = dropout_keep_k(dkey, (uint64_t)(prow[r] + j), p.p_drop) ? pv * keep_scale : 0.f;
+          pds[r] += pdv;
+        }
         if (TWO_PASS && i < T && j < T) {
           const int64_t off = prow0 + (int64_t)r * p.T + j;
           if (p.P) p.P[off] = pv;
@@ -390,6 +408,10 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void relpos_attn_fwd_kernel(A
         }
         Pw[ii * LDPS + jj] = f2bf(pdv);
       }
+    if (drop) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) ps[r] += group16_sum(pds[r]);
+    }
     if (!live) {
       if (!TWO_PASS) break;  // nothing to write: no P outputs in single-pass mode
       continue;              // P row tail beyond len is written as zeros; no O contribution
@@ -429,17 +451,24 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void relpos_attn_fwd_kernel(A
       if (i < T) p.lse[bh * p.T + i] = (i < len && lrow[r] > 0.f) ? mrow[r] + logf(lrow[r]) : 3.0e38f;
     }
   }
-  // ---- O -> (rows, d) ----
-  float fin[4];
+  // ---- O -> (rows, d): the centred sum plus S_i vc ----
+  float fin[4], sv[4];
 #pragma unroll
-  for (int r = 0; r < 4; ++r) fin[r] = TWO_PASS ? 1.f : ((ib + r < len && lrow[r] > 0.f) ? 1.f / lrow[r] : 0.f);
+  for (int r = 0; r < 4; ++r) {
+    const bool rv_ok = ib + r < len && lrow[r] > 0.f;
+    fin[r] = TWO_PASS ? 1.f : (rv_ok ? 1.f / lrow[r] : 0.f);
+    sv[r] = drop ? ps[r] * fin[r] : (rv_ok ? 1.f : 0.f);
+  }
 #pragma unroll
-  for (int u = 0; u < NU; ++u)
+  for (int u = 0; u < NU; ++u) {
+    const int c = 16 * u + (lane & 15);
+    const float v0 = Cn[1][c < dk ? c : 0];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int i = ib + r, c = 16 * u + (lane & 15);
-      if (i < T && c < dk) p.o[(b * p.T + i) * p.ldq + hoff + c] = oacc[u][r] * fin[r];
+      const int i = ib + r;
+      if (i < T && c < dk) p.o[(b * p.T + i) * p.ldq + hoff + c] = oacc[u][r] * fin[r] + sv[r] * v0;
     }
+  }
   KPROBE(31);
 }
 

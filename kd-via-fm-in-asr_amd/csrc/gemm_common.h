@@ -30,6 +30,9 @@ struct GemmP {
   int nseg; int64_t seg_rows;  // row-parallel wgrad: per-segment bias columns ones_col .. one_col + nseg - 1
   const int64_t* k_dev;        // row-parallel wgrad: device-side row count (<= K) read at run time (NULL: K)
   int xslots;                  // row-parallel wgrad: 0 = one raw partial per split; 8 = per-XCD slots (atomics)
+  // row-parallel wgrad, paired launch: a second product of the same shape (dY2, X2 -> C2 / ones_out2,
+  // partials in ws2) in the same grid (blocks [S, 2S) and the fold's blockIdx.y == 1); A2 == NULL: none
+  const float* A2; const float* B2; float* C2; float* ones_out2; float* ws2;
 };
 
 // Non-atomic epilogue for one output element.  v = alpha * acc (already scaled).  bz = batch

@@ -69,7 +69,13 @@ __global__ __launch_bounds__(WR_NT, 2) void wgr_kernel(GemmP p, WrGeo g) {
   // and turn every LDS access into a FLAT access that also waits on the global-load counter)
   const int ia = g.Ma * WR_LDK, ib = g.Nb * WR_LDK;   // image sizes (elements) of one buffer
   const int bufsz = ia + ib;                           // buffer b: A at b*bufsz, B at b*bufsz + ia
-  const int64_t split = blockIdx.x;
+  // paired launch: blocks [S, 2S) compute the second product (same shape, its own operands / partials)
+  const int64_t S_ = p.A2 ? (int64_t)gridDim.x / 2 : (int64_t)gridDim.x;
+  const bool second = (int64_t)blockIdx.x >= S_;
+  const int64_t split = second ? (int64_t)blockIdx.x - S_ : (int64_t)blockIdx.x;
+  const float* pA = second ? p.A2 : p.A;
+  const float* pB = second ? p.B2 : p.B;
+  float* pws = second ? p.ws2 : p.ws;
   const int64_t n0 = (int64_t)blockIdx.y * g.Nb;       // first output column of this slice
   // M slice: output rows m0 .. m0 + mcols - 1 (dY columns); more workgroups for short reductions
   // without growing any workgroup's partial
@@ -135,7 +141,7 @@ __global__ __launch_bounds__(WR_NT, 2) void wgr_kernel(GemmP p, WrGeo g) {
     tfr[i] = 0;
     toff[i] = 0;
     if (cg < ma4) {
-      src[i] = reinterpret_cast<const char*>(p.A) + ES * (r0 * p.sAk + m0 + cg * CW);
+      src[i] = reinterpret_cast<const char*>(pA) + ES * (r0 * p.sAk + m0 + cg * CW);
       ld[i] = ES * p.sAk;
     } else {
       const int64_t n = n0 + (int64_t)(cg - ma4) * CW;
@@ -144,9 +150,9 @@ __global__ __launch_bounds__(WR_NT, 2) void wgr_kernel(GemmP p, WrGeo g) {
         const int64_t tap = n / p.conv_c, c = n - tap * p.conv_c;
         toff[i] = (int)(tap - p.pad);
         tfr[i] = (int)(r0 % p.conv_t);
-        src[i] = reinterpret_cast<const char*>(p.B) + ES * ((r0 + toff[i]) * p.sBk + c);
+        src[i] = reinterpret_cast<const char*>(pB) + ES * ((r0 + toff[i]) * p.sBk + c);
       } else {
-        src[i] = reinterpret_cast<const char*>(p.B) + ES * (r0 * p.sBk + n);
+        src[i] = reinterpret_cast<const char*>(pB) + ES * (r0 * p.sBk + n);
       }
     }
   }
@@ -173,7 +179,7 @@ __global__ __launch_bounds__(WR_NT, 2) void wgr_kernel(GemmP p, WrGeo g) {
             ok = tt >= 0 && tt < T;
           }
         }
-        const char* q = ok ? src[i] + j * ld[i] : reinterpret_cast<const char*>(p.B);   // any valid, aligned address
+        const char* q = ok ? src[i] + j * ld[i] : reinterpret_cast<const char*>(pB);   // any valid, aligned address
         if constexpr (BIN == 1) {
           const uint2 t = *reinterpret_cast<const uint2*>(q);
           r[i][j] = make_float4(__builtin_bit_cast(float, t.x), __builtin_bit_cast(float, t.y), 0.f, 0.f);
@@ -334,7 +340,7 @@ __global__ __launch_bounds__(WR_NT, 2) void wgr_kernel(GemmP p, WrGeo g) {
     // slot choice is locality only -- the adds are device-coherent atomics wherever they land), so the
     // partial traffic is 8 slots in L2 instead of one f32 tile per split through HBM
     const int xcd = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 7;
-    float* wsx = p.ws + (int64_t)xcd * p.M * p.N;
+    float* wsx = pws + (int64_t)xcd * p.M * p.N;
 #pragma unroll
     for (int i = 0; i < MBW; ++i)
 #pragma unroll
@@ -349,7 +355,7 @@ __global__ __launch_bounds__(WR_NT, 2) void wgr_kernel(GemmP p, WrGeo g) {
     return;
   }
   // raw partial of this (split, slice) -> ws[split][m][n]
-  float* wsp = p.ws + split * p.M * p.N;
+  float* wsp = pws + split * p.M * p.N;
 #pragma unroll
   for (int i = 0; i < MBW; ++i)
 #pragma unroll
@@ -375,16 +381,20 @@ __global__ __launch_bounds__(64 * WF_WAVES) void wgr_fold_kernel(GemmP p, int64_
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t MN = p.M * p.N;
   const int64_t e = (int64_t)blockIdx.x * 64 + lane;
+  const bool second = blockIdx.y == 1;   // paired launch: the second product
+  const float* ws = second ? p.ws2 : p.ws;
+  float* Cout = second ? p.C2 : p.C;
+  float* ones = second ? p.ones_out2 : p.ones_out;
   float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
   if (e < MN) {
     int64_t s = w;
     for (; s + 3 * WF_WAVES < S; s += 4 * WF_WAVES) {
-      a0 += p.ws[s * MN + e];
-      a1 += p.ws[(s + WF_WAVES) * MN + e];
-      a2 += p.ws[(s + 2 * WF_WAVES) * MN + e];
-      a3 += p.ws[(s + 3 * WF_WAVES) * MN + e];
+      a0 += ws[s * MN + e];
+      a1 += ws[(s + WF_WAVES) * MN + e];
+      a2 += ws[(s + 2 * WF_WAVES) * MN + e];
+      a3 += ws[(s + 3 * WF_WAVES) * MN + e];
     }
-    for (; s < S; s += WF_WAVES) a0 += p.ws[s * MN + e];
+    for (; s < S; s += WF_WAVES) a0 += ws[s * MN + e];
   }
   red[w][lane] = (a0 + a1) + (a2 + a3);
   __syncthreads();
@@ -402,10 +412,77 @@ __global__ __launch_bounds__(64 * WF_WAVES) void wgr_fold_kernel(GemmP p, int64_
       n = e - m * p.N;
     }
     if (p.ones_col >= 0 && n >= p.ones_col)   // bias column(s): segment j -> ones_out[j][m]
-      p.ones_out[(n - p.ones_col) * p.M + m] += v;
+      ones[(n - p.ones_col) * p.M + m] += v;
     else
-      p.C[m * p.sCm + n * p.sCn] += v;
+      Cout[m * p.sCm + n * p.sCn] += v;
   }
+}
+
+// The same fold with 4 consecutive output elements per lane (16-byte partial loads; M*N % 4 == 0): a block
+// owns 256 elements, so the launch has a quarter of the blocks and every load instruction moves 4x the
+// bytes -- the fold is load-issue bound (r4k: 162 launches per step at 7.3 us each).
+template <bool TRANS = false>
+__global__ __launch_bounds__(64 * WF_WAVES) void wgr_fold4_kernel(GemmP p, int64_t S) {
+  __shared__ float4 red4[WF_WAVES][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t MN = p.M * p.N;
+  const int64_t e0 = ((int64_t)blockIdx.x * 64 + lane) * 4;
+  const bool second = blockIdx.y == 1;   // paired launch: the second product
+  float* Cout = second ? p.C2 : p.C;
+  float* ones = second ? p.ones_out2 : p.ones_out;
+  float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f), a1 = a0, a2 = a0, a3 = a0;
+  auto add = [](float4& a, const float4 b) { a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w; };
+  if (e0 < MN) {
+    const float4* base = reinterpret_cast<const float4*>((second ? p.ws2 : p.ws) + e0);
+    const int64_t st = MN / 4;   // float4 stride between splits
+    int64_t s = w;
+    for (; s + 3 * WF_WAVES < S; s += 4 * WF_WAVES) {
+      add(a0, base[s * st]);
+      add(a1, base[(s + WF_WAVES) * st]);
+      add(a2, base[(s + 2 * WF_WAVES) * st]);
+      add(a3, base[(s + 3 * WF_WAVES) * st]);
+    }
+    for (; s < S; s += WF_WAVES) add(a0, base[s * st]);
+  }
+  add(a0, a1);
+  add(a2, a3);
+  add(a0, a2);
+  red4[w][lane] = a0;
+  __syncthreads();
+  if (w == 0 && e0 < MN) {
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int i = 0; i < WF_WAVES; ++i) add(v, red4[i][lane]);
+    const float vv[4] = {v.x * p.alpha, v.y * p.alpha, v.z * p.alpha, v.w * p.alpha};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int64_t e = e0 + q;
+      int64_t m, n;
+      if (TRANS) {
+        n = e / p.M;
+        m = e - n * p.M;
+      } else {
+        m = e / p.N;
+        n = e - m * p.N;
+      }
+      if (p.ones_col >= 0 && n >= p.ones_col)
+        ones[(n - p.ones_col) * p.M + m] += vv[q];
+      else
+        Cout[m * p.sCm + n * p.sCn] += vv[q];
+    }
+  }
+}
+
+// fold launch: the 4-wide kernel when the partial layout allows it (KDFM_WGR_FOLD4=0: the scalar one)
+template <bool TRANS>
+void fold_launch(const GemmP& p, int64_t S, hipStream_t st) {
+  static const int f4 = [] { const char* e = getenv("KDFM_WGR_FOLD4"); return e ? atoi(e) : 1; }();
+  const int64_t MN = p.M * p.N;
+  const unsigned np = p.A2 ? 2u : 1u;
+  if (f4 && MN % 4 == 0 && (((uintptr_t)p.ws | (uintptr_t)p.ws2) & 15) == 0)
+    hipLaunchKernelGGL(wgr_fold4_kernel<TRANS>, dim3((unsigned)ceil_div(MN, 256), np), dim3(64 * WF_WAVES), 0, st, p, S);
+  else
+    hipLaunchKernelGGL(wgr_fold_kernel<TRANS>, dim3((unsigned)ceil_div(MN, 64), np), dim3(64 * WF_WAVES), 0, st, p, S);
 }
 
 struct WrPick { int mbw, nbw, wm, wn; };
@@ -539,7 +616,8 @@ int wr_launch(const GemmP& p, const WrPlan& pl, hipStream_t st) {
              hipSuccess;
     }();
     (void)once;
-    hipLaunchKernelGGL(kern, dim3((unsigned)pl.S, (unsigned)pl.slices, (unsigned)pl.mslices), dim3(WR_NT), pl.lds, st, p, pl.g);
+    hipLaunchKernelGGL(kern, dim3((unsigned)(pl.S * (p.A2 ? 2 : 1)), (unsigned)pl.slices, (unsigned)pl.mslices),
+                       dim3(WR_NT), pl.lds, st, p, pl.g);
   };
   if (pl.upt <= 1) {
     if (pd >= 2) go(wgr_kernel<MBW, NBW, CONV, 2, 1, BIN>); else go(wgr_kernel<MBW, NBW, CONV, 1, 1, BIN>);
@@ -567,7 +645,7 @@ bool wr_use_xslots(const WrPlan& pl) {
 
 // zero the slots (stream-ordered) and mark the launch parameters
 int wr_prep_xslots(GemmP& q, const WrPlan& pl, hipStream_t st) {
-  if (!wr_use_xslots(pl)) return 0;
+  if (q.A2 || !wr_use_xslots(pl)) return 0;   // paired launches keep the per-split partials
   q.xslots = WR_XSLOTS;
   if (hipMemsetAsync(q.ws, 0, sizeof(float) * WR_XSLOTS * q.M * q.N, st) != hipSuccess)
     return check_launch("kdfm wgrad rows (slot memset)");
@@ -575,8 +653,7 @@ int wr_prep_xslots(GemmP& q, const WrPlan& pl, hipStream_t st) {
 }
 
 int wr_fold(const GemmP& p, int64_t S, hipStream_t st) {
-  hipLaunchKernelGGL(wgr_fold_kernel<false>, dim3((unsigned)ceil_div(p.M * p.N, 64)), dim3(64 * WF_WAVES), 0, st, p,
-                     p.xslots ? (int64_t)p.xslots : S);
+  fold_launch<false>(p, p.xslots ? (int64_t)p.xslots : S, st);
   return check_launch("kdfm wgrad rows (fold)");
 }
 
@@ -988,8 +1065,7 @@ int wgrad_bf16_run(const GemmP& p, int bmode, hipStream_t st) {
   if (pl.dma) {
     const int rc = wd_dispatch(p, pl, st);
     if (rc) return rc;
-    hipLaunchKernelGGL(wgr_fold_kernel<true>, dim3((unsigned)ceil_div(p.M * p.N, 64)), dim3(64 * WF_WAVES), 0, st, p,
-                       pl.S);
+    fold_launch<true>(p, pl.S, st);
     return check_launch("kdfm_wgrad_bf16(fold)");
   }
   GemmP q = p;
@@ -1022,6 +1098,41 @@ int kdfm_wgrad_bf16(const uint16_t* dY, const uint16_t* X, float* dW, int64_t ld
   KDFM_REQUIRE(ldc >= N, "ldc < N");
   GemmP p = wgrad_bf16_params(dY, X, dW, ldc, db, rows, M, N, alpha, ws, ws_len);
   return wgrad_bf16_run(p, KDFM_LD_XC, as_stream(stream));
+}
+
+int kdfm_wgrad_bf16_pair(const uint16_t* dY, const uint16_t* X, float* dW, float* db, const uint16_t* dY2,
+                         const uint16_t* X2, float* dW2, float* db2, int64_t ldc, int64_t rows, int64_t M, int64_t N,
+                         float alpha, float* ws, int64_t ws_len, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(dY && X && dW && dY2 && X2 && dW2 && ws, "null pointer");
+  KDFM_REQUIRE((db == nullptr) == (db2 == nullptr), "both products have a bias gradient or neither");
+  KDFM_REQUIRE(rows > 0 && M > 0 && N > 0 && M % 4 == 0 && N % 4 == 0, "M, N must be positive multiples of 4");
+  KDFM_REQUIRE(((((uintptr_t)dY) | ((uintptr_t)X) | ((uintptr_t)dY2) | ((uintptr_t)X2)) & 15) == 0,
+               "operands must be 16-byte aligned");
+  KDFM_REQUIRE(ldc >= N, "ldc < N");
+  const int64_t one = kdfm_wgrad_bf16_ws(rows, M, N, db ? 1 : 0);
+  KDFM_REQUIRE(one > 0 && ws_len >= 2 * one, "workspace too small (2 x kdfm_wgrad_bf16_ws)");
+  hipStream_t st = as_stream(stream);
+  GemmP p = wgrad_bf16_params(dY, X, dW, ldc, db, rows, M, N, alpha, ws, one);
+  WrPlan pl;
+  KDFM_REQUIRE(wr_plan(p, KDFM_LD_XC, KDFM_LD_XC, 1, pl, true, true), "shape not supported by the row-parallel kernel");
+  if (pl.dma) {   // long reductions take the LDS-DMA kernel: two ordinary launches
+    int rc = wgrad_bf16_run(p, KDFM_LD_XC, st);
+    if (rc) return rc;
+    GemmP q = wgrad_bf16_params(dY2, X2, dW2, ldc, db2, rows, M, N, alpha, ws + one, one);
+    return wgrad_bf16_run(q, KDFM_LD_XC, st);
+  }
+  // one grid of 2 S workgroups (blocks [S, 2 S) run the second product), one fold launch over both:
+  // each product's splits, partial layout and fold order are those of a single launch (bitwise equal)
+  p.A2 = reinterpret_cast<const float*>(dY2);
+  p.B2 = reinterpret_cast<const float*>(X2);
+  p.C2 = dW2;
+  p.ones_out2 = db2;
+  p.ws2 = ws + one;
+  set_route(ROUTE_WGRAD_ROWS);
+  const int rc = pl.bin == 2 ? wr_dispatch<2>(p, pl, KDFM_LD_XC, st) : wr_dispatch<1>(p, pl, KDFM_LD_XC, st);
+  if (rc) return rc;
+  return wr_fold(p, pl.S, st);
 }
 
 int kdfm_wgrad_bf16_dev(const uint16_t* dY, const uint16_t* X, float* dW, int64_t ldc, float* db, int64_t rows,

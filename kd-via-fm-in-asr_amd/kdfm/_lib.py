@@ -86,6 +86,7 @@ SIGNATURES: dict[str, tuple] = {
     "kdfm_relpos_attn_bwd_parts": (_i32, [P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, _i64, _i64, _i64, _i64, _i64, _f32,
                                           _f32, P, C.c_uint64, _i32, P]),
     "kdfm_wgrad_bf16": (_i32, [P, P, P, _i64, P, _i64, _i64, _i64, _f32, P, _i64, P]),
+    "kdfm_wgrad_bf16_pair": (_i32, [P, P, P, P, P, P, P, P, _i64, _i64, _i64, _i64, _f32, P, _i64, P]),
     "kdfm_fm_chain_fwd": (_i32, [P, P, P, _i64, P, P, P, P, P, P, P, P, P, P, P, _f32, _i64, _i32, _i32, P]),
     "kdfm_rowgemm_img_elems": (_i64, [_i64]),
     "kdfm_wimg_job_threads": (_i64, [P]),

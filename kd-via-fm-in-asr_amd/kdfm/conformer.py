@@ -34,6 +34,10 @@ _ATTN_BWD_FUSED = __import__("os").environ.get("KDFM_ATTN_BWD_FUSED", "1") == "1
 # score gradient dS and dropped-out probabilities Pd, and dK / dV / dPpos are plain products over them
 # (KDFM_ATTN_BWD2=0: the forward saves bf16 p~ and block maxima, dK / dV / dPpos recompute dS from them)
 _ATTN_BWD2 = __import__("os").environ.get("KDFM_ATTN_BWD2", "1") == "1"
+# bf16 math: the layer backward's same-shape weight gradients (feed_forward2 / feed_forward1 linear2 and
+# linear1, pointwise_conv2 with linear_out) leave as paired launches (kdfm_wgrad_bf16_pair, each product
+# bitwise its single launch's); KDFM_WGRAD_PAIRS=0: one launch per product
+_WGRAD_PAIRS = __import__("os").environ.get("KDFM_WGRAD_PAIRS", "1") == "1"
 
 
 def _stream(salt, layer, site):
@@ -568,8 +572,29 @@ class LnGrads:
             self.pending = []
 
 
+def _wgrad_paired(pend, key, L, dY, X, wname, bname, G):
+    """Issue a bf16 weight gradient on the weight-gradient stream, paired with a waiting same-shape one:
+    the first of a pair is parked in `pend[key]`, the second launches both (kdfm_wgrad_bf16_pair)."""
+    if pend is None or not _WGRAD_PAIRS:
+        WGRAD.run(lambda: K.wgrad_bf16(dY, X, G[wname], db=G[bname]), dY, X)
+        return
+    if key not in pend:
+        pend[key] = (dY, X, wname, bname)
+        return
+    dY0, X0, w0, b0 = pend.pop(key)
+    WGRAD.run(lambda: K.wgrad_bf16_pair(dY0, X0, G[w0], G[b0], dY, X, G[wname], G[bname]), dY0, X0, dY, X)
+
+
+def _wgrad_flush(pend, G):
+    """Launch what is still parked (a pair whose partner took another path) as single products."""
+    if pend:
+        for dY, X, w, b in list(pend.values()):
+            WGRAD.run(lambda dY=dY, X=X, w=w, b=b: K.wgrad_bf16(dY, X, G[w], db=G[b]), dY, X)
+        pend.clear()
+
+
 def _ffn_backward(P, G, L, which, dres_out, ctx, tag, x_in_ln, norm, pd, seed, salt, li, site_act, site_out, dev,
-                  lng):
+                  lng, pend=None):
     """Backward of r_out = r_in + 0.5*drop(W2 drop(silu(W1 LN(r_in)))) ; returns d r_in."""
     rows, d = dres_out.shape
     m, r = ctx["m" + tag], ctx["r" + tag]
@@ -588,10 +613,8 @@ def _ffn_backward(P, G, L, which, dres_out, ctx, tag, x_in_ln, norm, pd, seed, s
         K.ffn_bwd(dres_out, x_in_ln, m, r, P[norm + ".weight"], P[norm + ".bias"], img,
                   P[L + which + ".linear1.bias"], dx, ln_h, a_h, dl2_h, dh_h, part, ff, rscale=0.5, p_act=pd, p_out=pd,
                   seed=seed, st_act=_stream(salt, li, site_act), st_out=_stream(salt, li, site_out))
-        WGRAD.run(lambda: K.wgrad_bf16(dl2_h, a_h, G[L + which + ".linear2.weight"], db=G[L + which + ".linear2.bias"]),
-                  dl2_h, a_h)
-        WGRAD.run(lambda: K.wgrad_bf16(dh_h, ln_h, G[L + which + ".linear1.weight"], db=G[L + which + ".linear1.bias"]),
-                  dh_h, ln_h)
+        _wgrad_paired(pend, "ffn_l2", L, dl2_h, a_h, L + which + ".linear2.weight", L + which + ".linear2.bias", G)
+        _wgrad_paired(pend, "ffn_l1", L, dh_h, ln_h, L + which + ".linear1.weight", L + which + ".linear1.bias", G)
         return dx
     ln, h, a = ctx["ln" + tag], ctx["h" + tag], ctx["a" + tag]
     ff = h.shape[1]
@@ -619,13 +642,14 @@ def layer_backward(cfg, S: EncoderShapes, P, G, L, li, ctx, dout, pos_emb, lengt
     if ln_buf is None:
         ln_buf = torch.empty(6, K.layernorm_bwd_ws(rows, d), device=dev)
     lng = LnGrads(ln_buf, rows, d)
+    pend = ctx["_pend"] = {}   # same-shape bf16 weight gradients waiting for their pair (_wgrad_paired)
     # norm_out
     dx4 = _empty(rows, d, dev=dev)
     lng.bwd(dout, ctx["x4"], P[L + "norm_out.weight"], ctx["m5"], ctx["r5"], dx4, G[L + "norm_out.weight"],
             G[L + "norm_out.bias"])
     # FFN2: x4 = x3 + 0.5 drop(ffn(LN4 x3))
     dx3 = _ffn_backward(P, G, L, "feed_forward2", dx4, ctx, "4", ctx["x3"], L + "norm_feed_forward2", pd, seed, salt,
-                        li, SITE_FF2_ACT, SITE_FF2_OUT, dev, lng)
+                        li, SITE_FF2_ACT, SITE_FF2_OUT, dev, lng, pend)
     del dx4
     # conv module: x3 = x2 + drop(pw2(z))
     dz = _empty(rows, d, dev=dev)
@@ -633,8 +657,12 @@ def layer_backward(cfg, S: EncoderShapes, P, G, L, li, ctx, dout, pos_emb, lengt
         dpw2_h = torch.empty(rows, d, device=dev, dtype=torch.bfloat16)
         K.rowgemm(dx3, K.rowgemm_img(P[L + "conv.pointwise_conv2.weight"].view(d, d), trans=True), dz,
                   pro=K.RG_PRO_DROP, p_in=pd, s_in=1.0, st_in=_stream(salt, li, SITE_CONV_OUT), x_h=dpw2_h, seed=seed)
-        WGRAD.run(lambda: K.wgrad_bf16(dpw2_h, ctx["z_h"], G[L + "conv.pointwise_conv2.weight"].view(d, d),
-                                       db=G[L + "conv.pointwise_conv2.bias"]), dpw2_h, ctx["z_h"])
+        if _WGRAD_PAIRS:   # paired with linear_out's (same (d, d) shape) in the attention backward below
+            pend["dd"] = (dpw2_h, ctx["z_h"], G[L + "conv.pointwise_conv2.weight"].view(d, d),
+                          G[L + "conv.pointwise_conv2.bias"])
+        else:
+            WGRAD.run(lambda: K.wgrad_bf16(dpw2_h, ctx["z_h"], G[L + "conv.pointwise_conv2.weight"].view(d, d),
+                                           db=G[L + "conv.pointwise_conv2.bias"]), dpw2_h, ctx["z_h"])
     else:
         dpw2 = _empty(rows, d, dev=dev)
         K.dropout(dx3, dpw2, pd, 1.0, seed, _stream(salt, li, SITE_CONV_OUT))
@@ -681,8 +709,14 @@ def layer_backward(cfg, S: EncoderShapes, P, G, L, li, ctx, dout, pos_emb, lengt
         dlo_h = torch.empty(rows, d, device=dev, dtype=torch.bfloat16)
         K.rowgemm(dx2, K.rowgemm_img(P[L + "self_attn.linear_out.weight"], trans=True), do, pro=K.RG_PRO_DROP,
                   p_in=pd, s_in=1.0, st_in=_stream(salt, li, SITE_ATT_OUT), x_h=dlo_h, seed=seed)
-        WGRAD.run(lambda: K.wgrad_bf16(dlo_h, ctx["o_h"], G[L + "self_attn.linear_out.weight"],
-                                       db=G[L + "self_attn.linear_out.bias"]), dlo_h, ctx["o_h"])
+        if "dd" in pend:
+            dpw2_h, z_h, gw2, gb2 = pend.pop("dd")
+            WGRAD.run(lambda: K.wgrad_bf16_pair(dpw2_h, z_h, gw2, gb2, dlo_h, ctx["o_h"],
+                                                G[L + "self_attn.linear_out.weight"], G[L + "self_attn.linear_out.bias"]),
+                      dpw2_h, z_h, dlo_h, ctx["o_h"])
+        else:
+            WGRAD.run(lambda: K.wgrad_bf16(dlo_h, ctx["o_h"], G[L + "self_attn.linear_out.weight"],
+                                           db=G[L + "self_attn.linear_out.bias"]), dlo_h, ctx["o_h"])
     else:
         dlo = _empty(rows, d, dev=dev)
         K.dropout(dx2, dlo, pd, 1.0, seed, _stream(salt, li, SITE_ATT_OUT))
@@ -795,8 +829,14 @@ def _attn_bwd_tail(P, G, L, ctx, dqkv, dqu, dqv, dppos, pos_emb, dx2, lng, cfg, 
                 G[L + "norm_self_att.weight"], G[L + "norm_self_att.bias"], dres=dx2)
         del dln2, dx2
     # FFN1
+    pend = ctx.pop("_pend", None)
+    if pend and "dd" in pend:   # linear_out took the unfused path: pointwise_conv2's gradient alone
+        dpw2_h, z_h, gw2, gb2 = pend.pop("dd")
+        WGRAD.run(lambda: K.wgrad_bf16(dpw2_h, z_h, gw2, db=gb2), dpw2_h, z_h)
     dx = _ffn_backward(P, G, L, "feed_forward1", dx1, ctx, "1", ctx["x"], L + "norm_feed_forward1", pd, seed, salt, li,
-                       SITE_FF1_ACT, SITE_FF1_OUT, dev, lng)
+                       SITE_FF1_ACT, SITE_FF1_OUT, dev, lng, pend)
+    if pend:
+        _wgrad_flush(pend, G)
     lng.fold()   # the layer's five dgamma/dbeta folds in one launch
     return dx
 

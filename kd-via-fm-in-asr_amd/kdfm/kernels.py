@@ -664,6 +664,25 @@ def wgrad_bf16(dY, X, dW, *, db=None, alpha=1.0):
             ptr(_bf16(X)), ptr(_f32(dW)), dW.stride(0), ptr(db), rows, M, N, float(alpha), ptr(ws), ws.numel(), _s())
 
 
+def wgrad_bf16_pair(dY, X, dW, db, dY2, X2, dW2, db2, *, alpha=1.0):
+    """Two same-shape weight gradients in one launch (kdfm_wgrad_bf16_pair): each equal bit for bit to its
+    own wgrad_bf16; db / db2 both given or both None; dW and dW2 share the row stride."""
+    rows, M = dY.shape
+    N = X.shape[1]
+    assert dY2.shape == dY.shape and X2.shape == X.shape and dW.shape == (M, N) and dW2.shape == (M, N)
+    assert dW.stride(1) == 1 and dW2.stride(1) == 1 and dW.stride(0) == dW2.stride(0)
+    assert (db is None) == (db2 is None)
+    for t in (dY, X, dY2, X2):
+        assert t.is_contiguous()
+    n = int(_lib.lib().kdfm_wgrad_bf16_ws(rows, M, N, 1 if db is not None else 0))
+    if n < 0:
+        raise _lib.KdfmError(f"kdfm_wgrad_bf16_pair: unsupported shape rows={rows} M={M} N={N}")
+    ws = scratch(dY.device, 2 * n)
+    _traced("wgrad_bf16", 4.0 * rows * M * N, 2.0 * (2.0 * rows * (M + N) + 8.0 * M * N), "kdfm_wgrad_bf16_pair",
+            ptr(_bf16(dY)), ptr(_bf16(X)), ptr(_f32(dW)), ptr(db), ptr(_bf16(dY2)), ptr(_bf16(X2)), ptr(_f32(dW2)),
+            ptr(db2), dW.stride(0), rows, M, N, float(alpha), ptr(ws), ws.numel(), _s())
+
+
 def wgrad_bf16_seg_ok(rows, M, N, seg_rows) -> bool:
     return int(_lib.lib().kdfm_wgrad_bf16_seg_ws(int(rows), int(M), int(N), int(seg_rows))) >= 0
 

@@ -87,8 +87,12 @@ def test_attn_bwd_matches_float64(B, H, T, d):
     ref = _torch_grads(qkv, qu, qv, ppos, do, lens, B, H, T, d)
     for name, got, want in zip(("dQu", "dQv", "dK", "dV", "dPpos"), (dqu, dqv, dk_, dv_, dpos), ref):
         assert _rel(got, want) <= 2e-2, (name, _rel(got, want))
-    # the forward's per-row log-sum-exp (valid rows) against float64; rows past the length are 3e38
-    want = _torch_grads.lse
+    # the forward's per-row log-sum-exp (valid rows) against float64 -- of the centred keys' scores
+    # (csrc/attn_centre.h: lse - scale qu_i . kc); rows past the length are 3e38
+    from test_attn_fused_gpu import kv_centred
+    kc = (qkv - kv_centred(qkv, lens, B, T, d))[:, d:2 * d].double().view(B, T, H, d // H)
+    shift = (qu.double().view(B, T, H, d // H) * kc).sum(-1).permute(0, 2, 1) / math.sqrt(d // H)
+    want = _torch_grads.lse - shift
     for bi in range(B):
         L = int(lens[bi])
         err = (lse[bi, :, :L].double().cpu() - want[bi, :, :L].cpu()).abs().max().item()
@@ -109,25 +113,16 @@ def test_attn_bwd_matches_float64(B, H, T, d):
             assert dv_.view(B, T, d)[bi, L:].abs().max().item() == 0.0
 
 
-def test_attn_bwd_matches_unfused_with_dropout():
+def _unfused(K, qkv, qu, qv, ppos, do, lens, B, H, T, d, p, seed):
+    """The unfused f32 chain on the two-pass forward's saved P and P_drop (same counter-RNG dropout mask):
+    returns (O, (dQu, dQv, dK, dV, dPpos))."""
     from kdfm import _lib
-    from kdfm import kernels as K
-    B, H, T, d, p = 2, 2, 401, 88, 0.1
     dk = d // H
     npos = 2 * T - 1
-    qkv, qu, qv, ppos, do, lens = _inputs(B, H, T, d, 5)
-    seed = torch.tensor([4242], dtype=torch.int64, device="cuda")
-    _, o1, dqu, dqv, dk_, dv_, dpos = _fused(K, qkv, qu, qv, ppos, do, lens, B, H, T, d, p, seed)
-    again = _fused(K, qkv, qu, qv, ppos, do, lens, B, H, T, d, p, seed)
-    for a, b in zip((dqu, dqv, dk_, dv_, dpos), again[2:]):
-        assert torch.equal(a, b), "fused attention backward is not bitwise reproducible"
-    # unfused f32 chain on the two-pass forward's saved P and P_drop (same counter-RNG dropout mask)
     P = torch.empty(B, H, T, T, device="cuda")
     Pd = torch.empty_like(P)
     o = torch.empty(B * T, d, device="cuda")
     K.relpos_attn_fwd(qu, qv, qkv, ppos, lens, o, P, Pd, B, H, T, 1.0 / math.sqrt(dk), p, seed, 11)
-    # the single-pass output (online softmax, dropout on the unnormalised probabilities) = the two-pass one
-    assert _rel(o1, o) <= 1e-2, _rel(o1, o)
     f32 = dict(math="f32")
     dPd = torch.empty(B, H, T, T, device="cuda")
     K.gemm(do, qkv[:, 2 * d:], dPd, T, T, dk, d, 1, 1, 3 * d, T, 1, amode=_lib.LD_KC, bmode=_lib.LD_KC,
@@ -152,8 +147,22 @@ def test_attn_bwd_matches_unfused_with_dropout():
     K.gemm(dbd, qv, r_dpos, npos, dk, T, 1, npos, d, 1, d, 1, amode=_lib.LD_XC, bmode=_lib.LD_XC,
            batch=(B, H), bA=(H * T * npos, T * npos), bB=(T * d, dk), bC=(0, dk), epi=_lib.EPI_ATOMIC, **f32)
     torch.cuda.synchronize()
-    for name, got, want in zip(("dQu", "dQv", "dK", "dV", "dPpos"), (dqu, dqv, dk_, dv_, dpos),
-                               (r_dqu, r_dqv, r_dk, r_dv, r_dpos)):
+    return o, (r_dqu, r_dqv, r_dk, r_dv, r_dpos)
+
+
+def test_attn_bwd_matches_unfused_with_dropout():
+    from kdfm import kernels as K
+    B, H, T, d, p = 2, 2, 401, 88, 0.1
+    qkv, qu, qv, ppos, do, lens = _inputs(B, H, T, d, 5)
+    seed = torch.tensor([4242], dtype=torch.int64, device="cuda")
+    _, o1, dqu, dqv, dk_, dv_, dpos = _fused(K, qkv, qu, qv, ppos, do, lens, B, H, T, d, p, seed)
+    again = _fused(K, qkv, qu, qv, ppos, do, lens, B, H, T, d, p, seed)
+    for a, b in zip((dqu, dqv, dk_, dv_, dpos), again[2:]):
+        assert torch.equal(a, b), "fused attention backward is not bitwise reproducible"
+    o, ref = _unfused(K, qkv, qu, qv, ppos, do, lens, B, H, T, d, p, seed)
+    # the single-pass output (online softmax, dropout on the unnormalised probabilities) = the two-pass one
+    assert _rel(o1, o) <= 1e-2, _rel(o1, o)
+    for name, got, want in zip(("dQu", "dQv", "dK", "dV", "dPpos"), (dqu, dqv, dk_, dv_, dpos), ref):
         assert _rel(got, want) <= 2e-2, (name, _rel(got, want))
 
 
@@ -269,3 +278,26 @@ def test_attn_bwd2_matches_bwd1_with_dropout():
         kept = ~dropped
         err = (got[kept] - prec[kept] / (1 - p)).abs().max().item()
         assert err <= 2e-2 * (prec.max().item() / (1 - p)) + 1e-3, (bi, err)
+
+
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_attn_bwd2_common_mode_keys_values(p):
+    """Keys and values sharing a per-channel offset (3x their spread: the FastConformer layer-0 keys carry
+    one, tools/attn_small_diag.py) -- the forward centres K and V on the utterance's first row before their
+    bf16 rounding and the backward adds c_i = dO_i . v0 back in f32, so the offset costs no accuracy: the
+    output and every bwd2 gradient within rel. Frobenius 2e-2 of float64 autograd (no dropout) or of the
+    unfused f32 chain (dropout 0.1, same mask).  Uncentred, dQu was 6-10 % off here."""
+    from kdfm import kernels as K
+    B, H, T, d = 2, 8, 201, 512
+    qkv, qu, qv, ppos, do, lens = _inputs(B, H, T, d, 31)
+    g = torch.Generator(device="cuda").manual_seed(1)
+    qkv[:, d:] += 3.0 * torch.randn(1, 2 * d, device="cuda", generator=g)
+    seed = torch.tensor([77], dtype=torch.int64, device="cuda")
+    o, _, _, _, *got = _bwd2(K, qkv, qu, qv, ppos, do, lens, B, H, T, d, p, seed)
+    if p == 0.0:
+        ref = _torch_grads(qkv, qu, qv, ppos, do, lens, B, H, T, d)
+    else:
+        o_ref, ref = _unfused(K, qkv, qu, qv, ppos, do, lens, B, H, T, d, p, seed)
+        assert _rel(o, o_ref) <= 1e-2, _rel(o, o_ref)
+    for name, a, w in zip(("dQu", "dQv", "dK", "dV", "dPpos"), got, ref):
+        assert _rel(a, w) <= 2e-2, (name, _rel(a, w))

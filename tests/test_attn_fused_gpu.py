@@ -2,6 +2,10 @@
 bf16 path the encoder uses in parity mode's structure (AC / BD GEMMs + relpos_softmax_fwd + PV GEMM)
 and (b) torch fp32 on the same bf16-rounded operands.
 
+The fused kernel rounds the CENTRED keys / values to bf16 (K_j - kc, V_j - vc; kc / vc = the mean of the
+utterance's first min(length, 16) rows, csrc/attn_centre.h), so the P references are formed from the same
+centred keys (softmax is invariant to the shift; the bf16 rounding is then the kernel's).
+
 Tolerances: P within 2e-3 absolute of the fp32 reference (scores from identical bf16 operands,
 different f32 accumulation order; P <= 1); the dropout mask identical to the unfused kernel's
 (same counter-RNG index); O within 1e-2 of max |O| (both round P_drop to bf16 for the PV MFMA)."""
@@ -15,6 +19,18 @@ pytestmark = pytest.mark.gpu
 
 def _bf(t):
     return t.to(torch.bfloat16).float()
+
+
+def kv_centred(qkv, lens, B, T, d):
+    """qkv with each utterance's keys and values shifted by the fused attention's centre (attn_centre.h):
+    the mean of its first n rows, n = min(length, 16) rounded down to a power of two."""
+    out = qkv.clone().view(B, T, 3 * d)
+    for bi in range(B):
+        L = min(int(lens[bi]), T)
+        n = 1 << (min(L, 16).bit_length() - 1) if L > 0 else 0
+        if n:
+            out[bi, :, d:] -= out[bi, :n, d:].sum(0) / n
+    return out.view(B * T, 3 * d)
 
 
 def _unfused(K, _lib, qu, qv, qkv, ppos, lens, B, H, T, d, p, seed):
@@ -68,13 +84,15 @@ def test_fused_attention_matches(B, H, T, d, p):
     ppos = torch.randn(2 * T - 1, d, device="cuda", generator=g)
     lens = torch.tensor([T] + [max(1, T - 17 * (i + 1)) for i in range(B - 1)], dtype=torch.int64, device="cuda")
     seed = torch.tensor([1234567], dtype=torch.int64, device="cuda")
-    P_u, Pd_u, o_u = _unfused(K, _lib, qu, qv, qkv, ppos, lens, B, H, T, d, p, seed)
+    qkv_c = kv_centred(qkv, lens, B, T, d)
+    P_u, Pd_u, _ = _unfused(K, _lib, qu, qv, qkv_c, ppos, lens, B, H, T, d, p, seed)
+    _, _, o_u = _unfused(K, _lib, qu, qv, qkv, ppos, lens, B, H, T, d, p, seed)
     P_f = torch.empty(B, H, T, T, device="cuda")
     Pd_f = torch.empty(B, H, T, T, device="cuda") if p > 0 else None
     o_f = torch.empty(rows, d, device="cuda")
     K.relpos_attn_fwd(qu, qv, qkv, ppos, lens, o_f, P_f, Pd_f, B, H, T, 1.0 / math.sqrt(d // H), p, seed, 11)
     torch.cuda.synchronize()
-    P_ref = _torch_ref_P(qu, qv, qkv, ppos, lens, B, H, T, d)
+    P_ref = _torch_ref_P(qu, qv, qkv_c, ppos, lens, B, H, T, d)
     assert (P_f - P_ref).abs().max().item() < 2e-3
     assert (P_f - P_u).abs().max().item() < 2e-3
     if p > 0:

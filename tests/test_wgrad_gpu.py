@@ -213,3 +213,28 @@ def test_xcd_slots_match_ordered_fold(R, M, N, bias, monkeypatch):
         assert (a - b).abs().max().item() <= 1e-5 * b.abs().max().item() + 1e-6
     for a, b in zip(res[(False, "0")], ref):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("R,M,N,bias", [(12832, 352, 88, True), (12832, 88, 352, True), (12832, 88, 88, True),
+                                        (4097, 264, 88, False), (205312 // 2, 96, 96, True)])
+def test_wgrad_bf16_pair_bitwise(R, M, N, bias):
+    """kdfm_wgrad_bf16_pair: two same-shape products in one launch (2S workgroups, one fold over both)
+    equal their single launches bit for bit, into row-strided outputs sharing ldc; the long-reduction
+    shape (>= 64 Ki rows) takes the LDS-DMA kernel as two launches -- also bitwise."""
+    from kdfm import kernels as K
+    g = torch.Generator(device="cuda").manual_seed(R + M * 3 + N)
+    mk = lambda *s: torch.randn(*s, device="cuda", generator=g).to(torch.bfloat16)  # noqa: E731
+    dy1, x1, dy2, x2 = mk(R, M), mk(R, N), mk(R, M), mk(R, N)
+    base = torch.randn(2, M, N + 3, device="cuda", generator=g)
+    bb = torch.randn(2, M, device="cuda", generator=g)
+    single = base.clone()
+    sb = bb.clone()
+    K.wgrad_bf16(dy1, x1, single[0, :, :N], db=sb[0] if bias else None, alpha=0.5)
+    K.wgrad_bf16(dy2, x2, single[1, :, :N], db=sb[1] if bias else None, alpha=0.5)
+    pair = base.clone()
+    pb = bb.clone()
+    K.wgrad_bf16_pair(dy1, x1, pair[0, :, :N], pb[0] if bias else None, dy2, x2, pair[1, :, :N],
+                      pb[1] if bias else None, alpha=0.5)
+    torch.cuda.synchronize()
+    assert torch.equal(single, pair)
+    assert torch.equal(sb, pb)
