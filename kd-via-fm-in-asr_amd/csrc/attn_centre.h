@@ -24,10 +24,16 @@ __device__ __forceinline__ void kv_centre(const float* kbase, const float* vbase
     const int c4 = (isv ? t - cq : t) * 4;
     const float* src = (isv ? vbase : kbase) + c4;
     const int n = len >= 16 ? 16 : len >= 8 ? 8 : len >= 4 ? 4 : len >= 2 ? 2 : (len > 0 ? 1 : 0);
+    // all 16 loads in flight at once (clamped rows, masked by a multiply; adding the zeros of rows >= n
+    // leaves the in-order sum unchanged)
+    float4 v[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = *reinterpret_cast<const float4*>(src + (int64_t)(r < n ? r : 0) * ld);
     float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int r = 0; r < n; ++r) {
-      const float4 v = *reinterpret_cast<const float4*>(src + (int64_t)r * ld);
-      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float m = r < n ? 1.f : 0.f;
+      s.x += m * v[r].x; s.y += m * v[r].y; s.z += m * v[r].z; s.w += m * v[r].w;
     }
     const float inv = n > 0 ? 1.f / (float)n : 0.f;   // a power of two: exact
     float* o = c[isv ? 1 : 0] + c4;

@@ -102,6 +102,10 @@ DW8C = dict(subsampling="dw_striding", subsampling_factor=8, subsampling_conv_ch
 # dw_striding x8 with 256 channels, depthwise conv kernel 9 -- student and teacher at that width
 FC = dict(d_student=512, heads_student=8, d_teacher=512, heads_teacher=8, subsampling="dw_striding",
           subsampling_factor=8, subsampling_conv_channels=256, conv_kernel=9, sched_d_model=512)
+# Conformer-CTC-large layer shapes (configs[3]'s student; NeMo conformer_ctc_bpe.yaml large: d_model 512,
+# 8 heads, 'striding' x4 with d_model conv channels, depthwise kernel 31) -- the 512-channel striding
+# subsampling runs the im2col + GEMM path (the one-kernel / implicit-GEMM kernels cover C <= 192)
+CL = dict(d_student=512, heads_student=8, d_teacher=512, heads_teacher=8, sched_d_model=512)
 
 
 @pytest.mark.parametrize("n_layers,B,N,lens,U,tl,sub", [
@@ -129,11 +133,13 @@ FC = dict(d_student=512, heads_student=8, d_teacher=512, heads_teacher=8, subsam
     (2, 2, 19200, [19200, 16123], 12, [12, 7], dict(d_teacher=88, heads_teacher=2)),
     # FastConformer shapes (f32 parity arithmetic)
     (2, 2, 32000, [32000, 24321], 12, [12, 7], FC),
+    # Conformer-CTC-large shapes (f32 parity arithmetic)
+    (2, 2, 19200, [19200, 16123], 12, [12, 7], CL),
     # the baseline logit-KD model family (DistilEncDecCTCModelBPE, asr_train_diffm.py:170-324): CTC + 0.1 KL
     (2, 2, 19200, [19200, 16123], 12, [12, 7], dict(kd_model="logitkd")),
 ], ids=["2L-1.2s", "16L-1s", "16L-16s", "16L-16s-overlapped", "2L-1.2s-dw4", "2L-1.2s-dw8-causal", "2L-1.2s-ver6", "2L-1.2s-ver7",
         "2L-1.2s-ver8-l1", "2L-1.2s-diffkd", "2L-1.2s-V1024", "2L-1.2s-equal-widths", "2L-2s-fastconformer-d512",
-        "2L-1.2s-logitkd"])
+        "2L-1.2s-conformer-large-d512", "2L-1.2s-logitkd"])
 def test_ver5_step_matches_oracle(n_layers, B, N, lens, U, tl, sub):
     from kdfm.config import sub_dims
     cfg, eng, wav, wl, tg, tgl, g = _build(n_layers, B, N, lens, U, tl, sub=sub)
@@ -213,7 +219,8 @@ def test_frontend_matches_oracle():
     _close(mel.cpu().transpose(1, 2), ref, 2e-4, "log-mel")
 
 
-@pytest.mark.parametrize("sub", [FC, dict()], ids=["fastconformer-d512-h8", "conformer-small"])
+@pytest.mark.parametrize("sub", [FC, CL, dict()], ids=["fastconformer-d512-h8", "conformer-large-d512-h8",
+                                                       "conformer-small"])
 def test_bf16_step_matches_float64_oracle(sub):
     """The bf16 benchmark kernels (fused LN-block FFN / projections where the width has them, the fused
     rel-pos attention forward and the bwd2 backward -- at head dim 64 for the FastConformer shapes --,

@@ -19,7 +19,7 @@ static float* dev_rand(size_t n, float scale, unsigned seed) {
   return d;
 }
 
-static void run(int64_t B, int64_t T, int64_t d, int64_t H, float p, KProbe& kp) {
+static void run(int64_t B, int64_t T, int64_t d, int64_t H, float p, KProbe& kp, bool wpt = true) {
   const int64_t rows = B * T;
   float* qu = dev_rand(rows * d, 1.f, 1);
   float* qv = dev_rand(rows * d, 1.f, 2);
@@ -40,8 +40,8 @@ static void run(int64_t B, int64_t T, int64_t d, int64_t H, float p, KProbe& kp)
   (void)hipMemset(seed, 7, 8);
   const float scale = 1.f / sqrtf((float)(d / H));
   auto launch = [&]() {
-    if (kdfm_relpos_attn_fwd(qu, qv, qkv, pos, lens, o, nullptr, nullptr, lse, pt, mblk, B, H, T, d, scale, p, seed, 5,
-                             nullptr))
+    if (kdfm_relpos_attn_fwd(qu, qv, qkv, pos, lens, o, nullptr, nullptr, lse, wpt ? pt : nullptr, wpt ? mblk : nullptr,
+                             B, H, T, d, scale, p, seed, 5, nullptr))
       exit(3);
   };
   for (int i = 0; i < 3; ++i) launch();
@@ -59,8 +59,8 @@ static void run(int64_t B, int64_t T, int64_t d, int64_t H, float p, KProbe& kp)
   launch();
   (void)hipDeviceSynchronize();
   char title[128];
-  snprintf(title, sizeof title, "relpos_attn_fwd B=%lld T=%lld d=%lld H=%lld p=%.1f", (long long)B, (long long)T,
-           (long long)d, (long long)H, p);
+  snprintf(title, sizeof title, "relpos_attn_fwd B=%lld T=%lld d=%lld H=%lld p=%.1f%s", (long long)B, (long long)T,
+           (long long)d, (long long)H, p, wpt ? " (p~ / m_blk)" : " (lse only: the bench's bwd2 mode)");
   kp.report(title, 1e3f * ms / 10);
   (void)hipFree(qu); (void)hipFree(qv); (void)hipFree(qkv); (void)hipFree(pos); (void)hipFree(lens);
   (void)hipFree(o); (void)hipFree(lse); (void)hipFree(pt); (void)hipFree(mblk); (void)hipFree(seed);
@@ -68,9 +68,9 @@ static void run(int64_t B, int64_t T, int64_t d, int64_t H, float p, KProbe& kp)
 
 int main() {
   KProbe kp;
-  kp.alloc((size_t)7 * 32 * 4 * 4);
-  run(32, 401, 88, 2, 0.1f, kp);
-  run(32, 401, 176, 4, 0.0f, kp);
-  run(1, 401, 88, 2, 0.1f, kp);
+  kp.alloc((size_t)7 * 32 * 8 * 4);
+  run(32, 401, 176, 4, 0.1f, kp, false);
+  run(32, 401, 176, 4, 0.0f, kp, false);
+  run(32, 401, 512, 8, 0.1f, kp, false);
   return 0;
 }
