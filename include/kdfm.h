@@ -224,8 +224,9 @@ int kdfm_relpos_attn_bwd(const float* dO, const float* O, const float* qu, const
                          float* ws, int64_t ws_len, int64_t B, int64_t H, int64_t T, int64_t d, float scale,
                          float dropout_p, const uint64_t* seed, uint64_t rng_stream, void* stream);
 /* The backward in three kernels over SAVED probabilities (bwd2; the forward then writes only lse):
- *   _dq: r_i = dO_i . O_i into rsum (B*H*T floats), then dqu / dqv exactly as above (with the forward's key /
- *        value centring: dPd_ij = dO_i . (V_j - vc) + dO_i . vc, the second term in f32), and the bf16 score
+ *   _dq: r_i = dO_i . O_i formed in the dQ kernel's prologue (rsum: unused, may be NULL -- kept for the
+ *        ABI), then dqu / dqv exactly as above (with the forward's key / value centring: dPd_ij =
+ *        dO_i . (V_j - vc) + dO_i . vc, the second term in f32), and the bf16 score
  *        gradient dS and dropout-masked probabilities Pd = dropout(P) of every (i, j < len) written into
  *        ds / pd, each (B, H, T, ldt) with ldt = kdfm_relpos_attn_bwd2_ldt(T) (T rounded up to 8; keys
  *        >= len in the last written 64-key block are 0, key blocks past len and rows >= T unwritten);
@@ -608,6 +609,11 @@ int64_t kdfm_layernorm_bwd_ws(int64_t rows, int64_t d);
 int kdfm_layernorm_bwd_part(const float* dy, const float* x, const float* gamma, const float* mean,
                             const float* rstd, const float* dres, float* dx, float* part, int64_t rows, int64_t d,
                             void* stream);
+/* the same with dy + dy2 as the output gradient (summed on load: the encoder backward's layer-input
+ * gradient plus the next hooked output's, without an add launch) */
+int kdfm_layernorm_bwd_part2(const float* dy, const float* dy2, const float* x, const float* gamma, const float* mean,
+                             const float* rstd, const float* dres, float* dx, float* part, int64_t rows, int64_t d,
+                             void* stream);
 int kdfm_ln_fold(const float* const* parts, float* const* dgamma, float* const* dbeta, int32_t n, int64_t rows,
                  int64_t d, void* stream);
 /* Qu = Q + pos_bias_u, Qv = Q + pos_bias_v from the fused (rows, 3d) q|k|v projection */
@@ -648,16 +654,22 @@ int kdfm_glu_mask_bwd(const float* dg, const float* a, const int64_t* lengths, f
 int kdfm_dwconv_fwd(const float* g, const float* w, const float* bias, float* y, double* stats, int64_t B, int64_t T,
                     int64_t d, int64_t K, void* stream);
 /* dg = conv^T(dy); dw, db accumulate (+=) */
-/* dw/db accumulated (+=) through per-block partials in ws (>= kdfm_dwconv_bwd_ws(B, T, d, K) floats) */
+/* dw/db accumulated (+=) through per-block partials in ws (>= kdfm_dwconv_bwd_ws(B, T, d, K) floats);
+ * dw == db == NULL: only dg, the partials are left in ws for kdfm_dwconv_bwd_fold (which may run on
+ * another stream once this launch is complete -- the engine folds on the weight-gradient stream) */
 int kdfm_dwconv_bwd(const float* dy, const float* g, const float* w, float* dg, float* dw, float* db, float* ws,
                     int64_t B, int64_t T, int64_t d, int64_t K, void* stream);
+int kdfm_dwconv_bwd_fold(const float* ws, float* dw, float* db, int64_t B, int64_t T, int64_t d, int64_t K,
+                         void* stream);
 int64_t kdfm_dwconv_bwd_ws(int64_t B, int64_t T, int64_t d, int64_t K);
 int kdfm_bn_finalize(const double* stats, const float* running_mean, const float* running_var, float* mean,
                      float* rstd, int64_t d, int64_t count, float eps, void* stream);
 int kdfm_bn_running_update(float* running_mean, float* running_var, const double* stats, int64_t d, int64_t count,
                            float momentum, void* stream);
-/* training step: kdfm_bn_finalize from the batch sums plus kdfm_bn_running_update in one launch */
-int kdfm_bn_finalize_running(const double* stats, float* running_mean, float* running_var, float* mean, float* rstd,
+/* training step: kdfm_bn_finalize from the batch sums plus kdfm_bn_running_update in one launch; the
+ * sums are reset to zero after they are read (a persistent stats buffer then serves the next layer's
+ * kdfm_dwconv_fwd without a memset) */
+int kdfm_bn_finalize_running(double* stats, float* running_mean, float* running_var, float* mean, float* rstd,
                              int64_t d, int64_t count, float eps, float momentum, void* stream);
 int kdfm_bn_silu_fwd(const float* y, const float* mean, const float* rstd, const float* gamma, const float* beta,
                      float* z, int64_t rows, int64_t d, void* stream);

@@ -65,6 +65,7 @@ struct AbP {
   int bpc;   // batches per chunk (kernel 3)
   // bwd2: dS and Pd (dropout-applied P) as bf16 (B, H, T, ldt), written by kernel 1, read by kernels 2b / 3b
   uint16_t* ds; uint16_t* pdo; int64_t ldt;
+  const float* O;   // bwd2: the forward output (row sums formed in the dQ kernel)
 };
 
 constexpr uint32_t AB_OOB = 0x80000000u;   // buffer offset past every buffer: the access is dropped / reads 0
@@ -164,7 +165,8 @@ __global__ __launch_bounds__(256) void attn_rowdot_kernel(const float* __restric
 // ---------------------------------------------------------------------------------------------
 // kernel 1: dQu, dQv
 // ---------------------------------------------------------------------------------------------
-template <int NU, bool SAVE = false>
+// RIN: the row sums r_i are formed in the prologue from dO and O (p.O) instead of read from p.rsum
+template <int NU, bool SAVE = false, bool RIN = false>
 __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dq_kernel(AbP p) {
   __shared__ __attribute__((aligned(16))) uint16_t Ks[BK * LR];     // K block [key][c]
   __shared__ __attribute__((aligned(16))) uint16_t Vs[BK * LR];     // V block [key][c]
@@ -211,7 +213,7 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dq_kernel(AbP p
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const bool ok = ib + r < len;
-    rs[r] = ok ? p.rsum[bh * p.T + ib + r] : 0.f;
+    rs[r] = (ok && !RIN) ? p.rsum[bh * p.T + ib + r] : 0.f;
     ls[r] = ok ? p.lse[bh * p.T + ib + r] : 3.0e38f;
   }
 
@@ -240,21 +242,43 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dq_kernel(AbP p
     }
   }
   // cs_i for this lane's C-layout rows: row (lane & 15) of the wave's 16 dotted in f32 by its 4 lane groups
-  // (16 columns each), summed across them, then picked up by the lanes owning each row
-  float cs[4];
+  // (16 columns each), summed across them, then picked up by the lanes owning each row.  With RIN (bwd2)
+  // the row sums r_i = dO_i . O_i are formed the same way here instead of by attn_rowdot_kernel
+  float cs[4], rin[4];
   {
     const int q = lane >> 4;
-    float part = 0.f;
+    float part = 0.f, pr = 0.f;
     if (iq < T) {
       const float* dor = p.dO + (b * p.T + iq) * p.ldq + hoff;
+      const float* orow = p.O + (b * p.T + iq) * p.ldq + hoff;
 #pragma unroll
-      for (int c = 16 * q; c < 16 * q + 16; ++c)
-        if (c < dk) part += dor[c] * Cn[1][c];
+      for (int c4 = 0; c4 < 4; ++c4) {
+        const int c = 16 * q + 4 * c4;
+        if (c < dk) {
+          const float4 g = *reinterpret_cast<const float4*>(dor + c);
+          part += g.x * Cn[1][c] + g.y * Cn[1][c + 1] + g.z * Cn[1][c + 2] + g.w * Cn[1][c + 3];
+          if (RIN) {
+            const float4 o = *reinterpret_cast<const float4*>(orow + c);
+            pr += g.x * o.x + g.y * o.y + g.z * o.z + g.w * o.w;
+          }
+        }
+      }
     }
     part += __shfl_xor(part, 16, 64);
     part += __shfl_xor(part, 32, 64);
+    if (RIN) {
+      pr += __shfl_xor(pr, 16, 64);
+      pr += __shfl_xor(pr, 32, 64);
+    }
 #pragma unroll
-    for (int r = 0; r < 4; ++r) cs[r] = __shfl(part, 4 * q + r, 64);
+    for (int r = 0; r < 4; ++r) {
+      cs[r] = __shfl(part, 4 * q + r, 64);
+      rin[r] = RIN ? __shfl(pr, 4 * q + r, 64) : 0.f;
+    }
+  }
+  if (RIN) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) rs[r] = ib + r < len ? rin[r] : 0.f;
   }
   // subtract the centre from the staged rows of keys [j0, j0 + BK) that are valid (rows past len stay 0)
   auto centre = [&](float4 (&v)[NU], const float4 (&c)[NU], int j0) {
@@ -1031,22 +1055,18 @@ int kdfm_relpos_attn_bwd2_dq(const float* dO, const float* O, const float* qu, c
                              uint16_t* pd, float* dqu, float* dqv, int64_t B, int64_t H, int64_t T, int64_t d,
                              float scale, float dropout_p, const uint64_t* seed, uint64_t rng_stream, void* stream) {
   using namespace kdfm;
-  KDFM_REQUIRE(dO && O && qu && qv && qkv && pos && lse && rsum && ds && pd && dqu && dqv, "null pointer");
-  KDFM_REQUIRE((((uintptr_t)dO | (uintptr_t)qu | (uintptr_t)qv | (uintptr_t)qkv | (uintptr_t)pos | (uintptr_t)ds |
-                 (uintptr_t)pd) & 15) == 0, "operands must be 16-byte aligned");
+  KDFM_REQUIRE(dO && O && qu && qv && qkv && pos && lse && ds && pd && dqu && dqv, "null pointer");
+  KDFM_REQUIRE((((uintptr_t)dO | (uintptr_t)O | (uintptr_t)qu | (uintptr_t)qv | (uintptr_t)qkv | (uintptr_t)pos |
+                 (uintptr_t)ds | (uintptr_t)pd) & 15) == 0, "operands must be 16-byte aligned");
   AbP p;
   int rc = ab2_setup(p, qu, qv, qkv, lse, lengths, B, H, T, d, scale, dropout_p, seed, rng_stream);
   if (rc || B == 0) return rc;
-  p.dO = dO; p.pos = pos; p.rsum = rsum; p.dqu = dqu; p.dqv = dqv; p.ds = ds; p.pdo = pd;
+  p.dO = dO; p.pos = pos; p.rsum = rsum; p.dqu = dqu; p.dqv = dqv; p.ds = ds; p.pdo = pd; p.O = O;
   hipStream_t st = as_stream(stream);
-  hipLaunchKernelGGL(attn_rowdot_kernel, dim3((unsigned)ceil_div(B * T * H, 4)), dim3(256), 0, st, dO, O, rsum, B, H, T,
-                     d, (int)p.dkh);
-  rc = check_launch("kdfm_relpos_attn_bwd2_dq(rowdot)");
-  if (rc) return rc;
   if (p.dkh > 48)
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<4, true>), dim3((unsigned)ceil_div(T, BQ), (unsigned)(B * H)), dim3(256), 0, st, p);
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<4, true, true>), dim3((unsigned)ceil_div(T, BQ), (unsigned)(B * H)), dim3(256), 0, st, p);
   else
-    hipLaunchKernelGGL((attn_bwd_dq_kernel<3, true>), dim3((unsigned)ceil_div(T, BQ), (unsigned)(B * H)), dim3(256), 0, st, p);
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<3, true, true>), dim3((unsigned)ceil_div(T, BQ), (unsigned)(B * H)), dim3(256), 0, st, p);
   return check_launch("kdfm_relpos_attn_bwd2_dq");
 }
 

@@ -208,14 +208,17 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const double* __restri
 }
 
 // training step: batch mean/rstd AND the running-statistics update in one launch
-__global__ __launch_bounds__(256) void bn_finalize_running_kernel(const double* __restrict__ stats,
+__global__ __launch_bounds__(256) void bn_finalize_running_kernel(double* __restrict__ stats,
                                                                   float* __restrict__ rm, float* __restrict__ rv,
                                                                   float* __restrict__ mean, float* __restrict__ rstd,
                                                                   int64_t d, double count, float eps, float momentum) {
   const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (c >= d) return;
-  const double m = stats[c] / count;
-  double var = stats[d + c] / count - m * m;
+  const double s1 = stats[c], s2 = stats[d + c];
+  stats[c] = 0.0;   // reset for the next kdfm_dwconv_fwd accumulation (no memset launch per layer)
+  stats[d + c] = 0.0;
+  const double m = s1 / count;
+  double var = s2 / count - m * m;
   if (var < 0.0) var = 0.0;
   mean[c] = (float)m;
   rstd[c] = (float)(1.0 / sqrt(var + (double)eps));
@@ -489,7 +492,8 @@ int64_t kdfm_dwconv_bwd_ws(int64_t B, int64_t T, int64_t d, int64_t K) {
 int kdfm_dwconv_bwd(const float* dy, const float* g, const float* w, float* dg, float* dw, float* db, float* ws,
                     int64_t B, int64_t T, int64_t d, int64_t K, void* stream) {
   using namespace kdfm;
-  KDFM_REQUIRE(dy && g && w && dg && dw && db && ws, "null pointer");
+  KDFM_REQUIRE(dy && g && w && dg && ws, "null pointer");
+  KDFM_REQUIRE((dw == nullptr) == (db == nullptr), "dw and db: both or neither");
   KDFM_REQUIRE(K >= 1 && K <= KMAX && (K % 2) == 1, "kernel size must be odd and <= 63");
   KDFM_REQUIRE(d % 4 == 0 && ((((uintptr_t)g) | ((uintptr_t)dy)) & 15) == 0,
                "channels must be a multiple of 4, inputs 16-B aligned");
@@ -505,9 +509,17 @@ int kdfm_dwconv_bwd(const float* dy, const float* g, const float* w, float* dg, 
   else
     hipLaunchKernelGGL(dwconv_bwd_kernel<0>, grid, dim3(256), 0, st, dy, g, w, dg, ws, T, d, (int)K);
   int rc = check_launch("kdfm_dwconv_bwd");
-  if (rc) return rc;
+  if (rc || !dw) return rc;   // dw == db == NULL: the partials stay in ws for kdfm_dwconv_bwd_fold
+  return kdfm_dwconv_bwd_fold(ws, dw, db, B, T, d, K, stream);
+}
+
+int kdfm_dwconv_bwd_fold(const float* ws, float* dw, float* db, int64_t B, int64_t T, int64_t d, int64_t K,
+                         void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(ws && dw && db, "null pointer");
   const int64_t ld = d * (K + 1);
-  return launch_colsum2(ws, dw, d * K, db, B * ntt, ld, ld, 1.f, st);   // [dw | db] partial columns, one fold
+  // [dw | db] partial columns, one fold
+  return launch_colsum2(ws, dw, d * K, db, B * ceil_div(T, TT), ld, ld, 1.f, as_stream(stream));
 }
 
 int kdfm_bn_finalize(const double* stats, const float* running_mean, const float* running_var, float* mean,
@@ -520,7 +532,7 @@ int kdfm_bn_finalize(const double* stats, const float* running_mean, const float
   return check_launch("kdfm_bn_finalize");
 }
 
-int kdfm_bn_finalize_running(const double* stats, float* running_mean, float* running_var, float* mean, float* rstd,
+int kdfm_bn_finalize_running(double* stats, float* running_mean, float* running_var, float* mean, float* rstd,
                              int64_t d, int64_t count, float eps, float momentum, void* stream) {
   using namespace kdfm;
   KDFM_REQUIRE(stats && running_mean && running_var && mean && rstd, "null pointer");

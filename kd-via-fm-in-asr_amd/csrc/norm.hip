@@ -55,10 +55,13 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
 constexpr int LN_RPW = 4;
 
 template <int V>
+// dy2 (nullable): a second gradient summed into dy on load (the encoder backward's layer-input gradient
+// plus the hooked output's gradient, without an add launch in between)
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ x,
                                                      const float* __restrict__ g, const float* __restrict__ mean,
                                                      const float* __restrict__ rstd, const float* dres, float* dx,
-                                                     float* __restrict__ part, int64_t rows, int d) {
+                                                     float* __restrict__ part, int64_t rows, int d,
+                                                     const float* __restrict__ dy2) {
   __shared__ float red[2][4][64 * V];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   float gl[V], pg[V], pb[V];
@@ -81,7 +84,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ d
     for (int i = 0; i < V; ++i) {
       const int c = lane + 64 * i;
       const bool in = ok && c < d;
-      dyv[j][i] = in ? dy[row * d + c] : 0.f;
+      dyv[j][i] = in ? dy[row * d + c] + (dy2 ? dy2[row * d + c] : 0.f) : 0.f;
       xv[j][i] = in ? x[row * d + c] : 0.f;
       rv[j][i] = (in && dres) ? dres[row * d + c] : 0.f;
     }
@@ -184,11 +187,12 @@ int ln_fold(const float* const* parts, float* const* dgs, float* const* dbs, int
 }
 
 int ln_bwd_launch(const float* dy, const float* x, const float* gamma, const float* mean, const float* rstd,
-                  const float* dres, float* dx, float* part, int64_t rows, int64_t d, hipStream_t st) {
+                  const float* dres, float* dx, float* part, int64_t rows, int64_t d, hipStream_t st,
+                  const float* dy2 = nullptr) {
   const int64_t blocks = ceil_div(rows, 4 * LN_RPW);
   const dim3 grid((unsigned)blocks), blk(256);
   const int64_t v = (d + 63) / 64;
-#define LNB(V) hipLaunchKernelGGL(ln_bwd_kernel<V>, grid, blk, 0, st, dy, x, gamma, mean, rstd, dres, dx, part, rows, (int)d)
+#define LNB(V) hipLaunchKernelGGL(ln_bwd_kernel<V>, grid, blk, 0, st, dy, x, gamma, mean, rstd, dres, dx, part, rows, (int)d, dy2)
   if (v == 1) LNB(1);
   else if (v == 2) LNB(2);
   else if (v == 3) LNB(3);
@@ -254,6 +258,16 @@ int kdfm_layernorm_bwd_part(const float* dy, const float* x, const float* gamma,
   KDFM_REQUIRE(d > 0 && d <= 64 * MAXV, "d must be in (0, 1024]");
   if (rows == 0) return KDFM_OK;
   return ln_bwd_launch(dy, x, gamma, mean, rstd, dres, dx, part, rows, d, as_stream(stream));
+}
+
+int kdfm_layernorm_bwd_part2(const float* dy, const float* dy2, const float* x, const float* gamma, const float* mean,
+                             const float* rstd, const float* dres, float* dx, float* part, int64_t rows, int64_t d,
+                             void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(dy && dy2 && x && gamma && mean && rstd && dx && part, "null pointer");
+  KDFM_REQUIRE(d > 0 && d <= 64 * MAXV, "d must be in (0, 1024]");
+  if (rows == 0) return KDFM_OK;
+  return ln_bwd_launch(dy, x, gamma, mean, rstd, dres, dx, part, rows, d, as_stream(stream), dy2);
 }
 
 int kdfm_ln_fold(const float* const* parts, float* const* dgamma, float* const* dbeta, int32_t n, int64_t rows,

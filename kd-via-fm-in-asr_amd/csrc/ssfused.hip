@@ -30,6 +30,11 @@
 // columns) the workgroup also writes the y1 rows it owns (t1 in [2 t2a, 2 t2a + 2R)) as bf16.
 #include "gemm_common.h"
 
+// timing probe points (tools/ss_probe.hip defines KPROBE; empty in the library)
+#ifndef KPROBE
+#define KPROBE(i)
+#endif
+
 namespace kdfm {
 namespace {
 
@@ -70,11 +75,19 @@ __global__ __launch_bounds__(FS_NT, 1) void ss_fused_kernel(FsArgs a) {
   constexpr int MR = 4 * R + 3;                   // mel patch rows
   constexpr int Y1_BYTES = ((NPT * 16 * FS_CKP * 2 + 1023) / 1024) * 1024;
   static_assert(MR * FS_MC * 4 <= Y1_BYTES, "mel patch aliases the y1 buffer");
+  // the chunk's conv2 weight slab ([9 taps][NPAD co][32 ci] bf16) staged in LDS when it fits beside y1 and P:
+  // the B fragments are then LDS reads instead of L2 loads one tap ahead (an L2 round trip per tap)
+  constexpr int WS_BYTES = 9 * NPAD * FS_CK * 2;
+  constexpr bool STAGEB = Y1_BYTES + NPT * 1024 + WS_BYTES <= 160 * 1024;
+  constexpr int WSU = WS_BYTES / 16;                       // 16-byte units of one slab
+  constexpr int WSPT = STAGEB ? (WSU + FS_NT - 1) / FS_NT : 1;   // units per thread
   extern __shared__ __attribute__((aligned(16))) unsigned char fs_lds[];
   uint16_t* y1s = reinterpret_cast<uint16_t*>(fs_lds);
   float* mels = reinterpret_cast<float*>(fs_lds);
   unsigned char* Ps = fs_lds + Y1_BYTES;
+  uint16_t* Wsl = reinterpret_cast<uint16_t*>(fs_lds + Y1_BYTES + NPT * 1024);
 
+  KPROBE(0);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r16 = lane & 15, kq = lane >> 4;
   const int nstrip = (a.T2 + R - 1) / R;
@@ -88,12 +101,28 @@ __global__ __launch_bounds__(FS_NT, 1) void ss_fused_kernel(FsArgs a) {
 
   // ---- prologue: mel patch, then the conv1 A operand P (fragment-major [tile][kq][r][8])
   const float* melb = a.mel + (int64_t)b * a.Tm * a.F;
-  for (int e = threadIdx.x; e < MR * FS_MC; e += FS_NT) {
-    const int i = e / FS_MC, j = e - i * FS_MC;
-    const int t = tm0 + i, f = j - 1;
-    mels[e] = (t >= 0 && t < ml && f >= 0 && f < a.F) ? melb[(int64_t)t * a.F + f] : 0.f;
+  {
+    // every load of the patch in flight at once: clamped (always valid) addresses, masked by a multiply
+    // (a conditional load is branched around and waited for one by one)
+    constexpr int MPT = (MR * FS_MC + FS_NT - 1) / FS_NT;
+    float mv[MPT], mm[MPT];
+#pragma unroll
+    for (int u = 0; u < MPT; ++u) {
+      const int e = threadIdx.x + u * FS_NT;
+      const int i = e / FS_MC, j = e - i * FS_MC;
+      const int t = tm0 + i, f = j - 1;
+      const bool ok = e < MR * FS_MC && t >= 0 && t < ml && f >= 0 && f < a.F;
+      mv[u] = melb[ok ? (int64_t)t * a.F + f : 0];
+      mm[u] = ok ? 1.f : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < MPT; ++u) {
+      const int e = threadIdx.x + u * FS_NT;
+      if (e < MR * FS_MC) mels[e] = mv[u] * mm[u];
+    }
   }
   __syncthreads();
+  KPROBE(1);
   for (int q = threadIdx.x; q < NPT * 16; q += FS_NT) {
     const int i = q / FS_F1C, j = q - (q / FS_F1C) * FS_F1C;
     const bool in = q < NQ;
@@ -116,6 +145,7 @@ __global__ __launch_bounds__(FS_NT, 1) void ss_fused_kernel(FsArgs a) {
       *reinterpret_cast<bf16x8*>(Ps + ((pt * 4 + g) * 16 + r) * 16) = pack_bf16x8<bf16x8>(e + 8 * g);
   }
   __syncthreads();   // P complete; the mel patch (aliasing y1s) is dead from here
+  KPROBE(2);
 
   // ---- conv2 geometry of this lane: the y1 element offset of its A row in every M tile
   const int wm = wave / WN, wn = wave - (wave / WN) * WN;
@@ -139,28 +169,63 @@ __global__ __launch_bounds__(FS_NT, 1) void ss_fused_kernel(FsArgs a) {
 
 #pragma unroll 1
   for (int c = 0; c < NCH; ++c) {
-    // ---- conv1 of channels [32c, 32c + 32) for every y1 position of the patch -> bf16 y1 chunk in LDS
+    // conv1 operands of the chunk: weight fragments (channels as the A rows) and this lane's 4 channels'
+    // biases per 16-channel tile -- loaded before the slab so waiting for them does not wait for it
     const bf16x8 w1f0 = *reinterpret_cast<const bf16x8*>(a.w1p + (int64_t)(c * FS_CK + r16) * FS_CK + 8 * kq);
     const bf16x8 w1f1 = *reinterpret_cast<const bf16x8*>(a.w1p + (int64_t)(c * FS_CK + 16 + r16) * FS_CK + 8 * kq);
-    const int ch0 = c * FS_CK + r16, ch1 = ch0 + 16;
-    const float bias0 = ch0 < C ? a.b0[ch0] : 0.f, bias1 = ch1 < C ? a.b0[ch1] : 0.f;
-    for (int it = wave; it < NPT * 2; it += 8) {
-      const int pt = it >> 1, nt = it & 1;
-      const bf16x8 af = *reinterpret_cast<const bf16x8*>(Ps + ((pt * 4 + kq) * 16 + r16) * 16);
-      f32x4 v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, nt ? w1f1 : w1f0, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-      const float bias = nt ? bias1 : bias0;
-      const bool chok = (nt ? ch1 : ch0) < C;
+    float bias[2][4], chm[2][4];
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int q = pt * 16 + 4 * kq + e;
-        const int i = q / FS_F1C, j = q - (q / FS_F1C) * FS_F1C;
-        const int t1 = t1a + i;
-        const bool ok = chok && q < NQ && t1 >= 0 && t1 < l1 && j >= 1;
-        const float y = ok ? fmaxf(v[e] + bias, 0.f) : 0.f;
-        y1s[q * FS_CKP + nt * 16 + r16] = f2bf(y);
+        const int ch = c * FS_CK + nt * 16 + 4 * kq + e;
+        bias[nt][e] = a.b0[ch < C ? ch : 0];
+        chm[nt][e] = ch < C ? 1.f : 0.f;
+      }
+    // the chunk's conv2 weight slab into registers first: its loads fly while conv1 runs
+    uint4 wreg[WSPT];
+    if constexpr (STAGEB) {
+#pragma unroll
+      for (int i = 0; i < WSPT; ++i) {
+        const int u = threadIdx.x + i * FS_NT;
+        const int uu = u < WSU ? u : 0;
+        const int tap = uu / (NPAD * 4), rest = uu - tap * (NPAD * 4);
+        wreg[i] = *reinterpret_cast<const uint4*>(a.w2p + ((int64_t)(tap * NCH + c) * NPAD * FS_CK + rest * 8));
+      }
+    }
+    // ---- conv1 of channels [32c, 32c + 32) for every y1 position of the patch -> bf16 y1 chunk in LDS.
+    // Computed transposed (channels x positions: A = the weights, B = the patch operand), so a lane holds
+    // 4 consecutive channels of ONE position: one validity test and one 8-byte LDS store per tile
+    for (int pt = wave; pt < NPT; pt += 8) {
+      const bf16x8 pf = *reinterpret_cast<const bf16x8*>(Ps + ((pt * 4 + kq) * 16 + r16) * 16);
+      const f32x4 v0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1f0, pf, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      const f32x4 v1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1f1, pf, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      const int q = pt * 16 + r16;
+      const int i = q / FS_F1C, j = q - i * FS_F1C;
+      const int t1 = t1a + i;
+      const float pm = (q < NQ && t1 >= 0 && t1 < l1 && j >= 1) ? 1.f : 0.f;
+      float y[2][4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        y[0][e] = fmaxf(v0[e] + bias[0][e], 0.f) * (pm * chm[0][e]);
+        y[1][e] = fmaxf(v1[e] + bias[1][e], 0.f) * (pm * chm[1][e]);
+      }
+      if (q < NPT * 16) {
+        uint16_t* dst = y1s + q * FS_CKP + 4 * kq;
+        *reinterpret_cast<uint2*>(dst) = make_uint2(pack_bf16x2(y[0][0], y[0][1]), pack_bf16x2(y[0][2], y[0][3]));
+        *reinterpret_cast<uint2*>(dst + 16) = make_uint2(pack_bf16x2(y[1][0], y[1][1]), pack_bf16x2(y[1][2], y[1][3]));
+      }
+    }
+    if (c < 8) KPROBE(3 + 3 * c);
+    if constexpr (STAGEB) {
+#pragma unroll
+      for (int i = 0; i < WSPT; ++i) {
+        const int u = threadIdx.x + i * FS_NT;
+        if (u < WSU) *reinterpret_cast<uint4*>(Wsl + u * 8) = wreg[i];
       }
     }
     __syncthreads();
+    if (c < 8) KPROBE(4 + 3 * c);
     if (a.y1) {
       // the y1 rows this workgroup owns (patch rows 1 .. 2R), 8 channels per 16-byte store
       constexpr int UN = 2 * R * 40 * 4;
@@ -173,7 +238,27 @@ __global__ __launch_bounds__(FS_NT, 1) void ss_fused_kernel(FsArgs a) {
               *reinterpret_cast<const bf16x8*>(y1s + (i * FS_F1C + f1 + 1) * FS_CKP + 8 * g);
       }
     }
-    // ---- conv2 over the chunk: 9 taps, B slabs from L2 one tap ahead
+    // ---- conv2 over the chunk: 9 taps, B slabs from the LDS image (STAGEB) or from L2 one tap ahead
+    if constexpr (STAGEB) {
+      const uint16_t* wl = Wsl + ((wn * NT) * 16 + r16) * FS_CK + 8 * kq;
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        bf16x8 bl[NT];
+#pragma unroll
+        for (int j = 0; j < NT; ++j) bl[j] = *reinterpret_cast<const bf16x8*>(wl + (tap * NPAD + j * 16) * FS_CK);
+        const int toff = ((tap / 3) * FS_F1C + (tap % 3)) * FS_CKP;
+#pragma unroll
+        for (int i = 0; i < MT; ++i) {
+          if (!mvalid[i]) continue;
+          const bf16x8 af = *reinterpret_cast<const bf16x8*>(y1s + yoff[i] + toff);
+#pragma unroll
+          for (int j = 0; j < NT; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bl[j], acc[i][j], 0, 0, 0);
+        }
+      }
+      if (c < 8) KPROBE(5 + 3 * c);
+      __syncthreads();   // the next chunk's conv1 overwrites y1s (and its slab Wsl)
+      continue;
+    }
     bf16x8 bq[2][NT];
     const uint16_t* wc = w2l + (int64_t)c * NPAD * FS_CK;
 #pragma unroll
@@ -194,8 +279,10 @@ __global__ __launch_bounds__(FS_NT, 1) void ss_fused_kernel(FsArgs a) {
         for (int j = 0; j < NT; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bq[tap & 1][j], acc[i][j], 0, 0, 0);
       }
     }
+    if (c < 8) KPROBE(5 + 3 * c);
     __syncthreads();   // the next chunk's conv1 overwrites y1s
   }
+  KPROBE(30);
 
   // ---- epilogue: bias + ReLU + len2 mask, f32 rows (b, t2, f2) x C
 #pragma unroll
@@ -215,13 +302,16 @@ __global__ __launch_bounds__(FS_NT, 1) void ss_fused_kernel(FsArgs a) {
       }
     }
   }
+  KPROBE(31);
 }
 
 template <int C, int R, int WM, int WN, int MT, int NT>
 int fs_launch(const FsArgs& a, hipStream_t st) {
   constexpr int NR1 = 2 * R + 1, NQ = NR1 * FS_F1C, NPT = (NQ + 15) / 16;
   constexpr int Y1_BYTES = ((NPT * 16 * FS_CKP * 2 + 1023) / 1024) * 1024;
-  constexpr size_t lds = (size_t)Y1_BYTES + (size_t)NPT * 1024;
+  constexpr int NPAD = NT * 16 * WN, WS_BYTES = 9 * NPAD * FS_CK * 2;
+  constexpr size_t base = (size_t)Y1_BYTES + (size_t)NPT * 1024;
+  constexpr size_t lds = base + (base + WS_BYTES <= 160 * 1024 ? (size_t)WS_BYTES : 0);   // STAGEB (kernel)
   static_assert(lds <= 160 * 1024, "LDS");
   static bool once = [] {
     (void)hipFuncSetAttribute((const void*)ss_fused_kernel<C, R, WM, WN, MT, NT>,

@@ -159,6 +159,7 @@ SIGNATURES: dict[str, tuple] = {
     "kdfm_layernorm_bwd": (_i32, [P, P, P, P, P, P, P, P, P, P, _i64, _i64, P]),
     "kdfm_layernorm_bwd_ws": (_i64, [_i64, _i64]),
     "kdfm_layernorm_bwd_part": (_i32, [P, P, P, P, P, P, P, P, _i64, _i64, P]),
+    "kdfm_layernorm_bwd_part2": (_i32, [P, P, P, P, P, P, P, P, P, _i64, _i64, P]),
     "kdfm_ln_fold": (_i32, [C.POINTER(P), C.POINTER(P), C.POINTER(P), _i32, _i64, _i64, P]),
     "kdfm_qkv_prep": (_i32, [P, P, P, P, P, _i64, _i64, P]),
     "kdfm_relpos_softmax_fwd": (_i32, [P, P, P, P, P, _i64, _i64, _i64, _f32, _f32, P, C.c_uint64, P]),
@@ -169,6 +170,7 @@ SIGNATURES: dict[str, tuple] = {
     "kdfm_glu_mask_bwd": (_i32, [P, P, P, P, _i64, _i64, _i64, P]),
     "kdfm_dwconv_fwd": (_i32, [P, P, P, P, P, _i64, _i64, _i64, _i64, P]),
     "kdfm_dwconv_bwd": (_i32, [P, P, P, P, P, P, P, _i64, _i64, _i64, _i64, P]),
+    "kdfm_dwconv_bwd_fold": (_i32, [P, P, P, _i64, _i64, _i64, _i64, P]),
     "kdfm_dwconv_bwd_ws": (_i64, [_i64, _i64, _i64, _i64]),
     "kdfm_bn_finalize": (_i32, [P, P, P, P, P, _i64, _i64, _f32, P]),
     "kdfm_bn_running_update": (_i32, [P, P, P, _i64, _i64, _f32, P]),

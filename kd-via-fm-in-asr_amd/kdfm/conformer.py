@@ -105,10 +105,14 @@ def _out_linear_backward(S, P, G, pre, ctx, dx, y, *, seed, salt, ws):
     dlin = _empty(S.rows, d, dev=dx.device)
     K.dropout(dx, dlin, ctx["p_pre"], ctx["xscale"], seed, _stream(salt, -1, SITE_PRE))
     Gout = ws["wout_perm_grad"]
-    K.fill(Gout, 0.0)
-    K.linear_dw(dlin, y.view(S.rows, S.F2 * C), Gout.view(d, S.F2 * C))
-    K.convw_grad(Gout, G[pre + "pre_encode.out.weight"].view(d, C, S.F2))
-    K.colsum(dlin, G[pre + "pre_encode.out.bias"])
+    yv = y.view(S.rows, S.F2 * C)
+
+    def out_wgrad():   # parameter gradients only: on the weight-gradient stream
+        K.fill(Gout, 0.0)
+        K.linear_dw(dlin, yv, Gout.view(d, S.F2 * C))
+        K.convw_grad(Gout, G[pre + "pre_encode.out.weight"].view(d, C, S.F2))
+        K.colsum(dlin, G[pre + "pre_encode.out.bias"])
+    WGRAD.run(out_wgrad, dlin, yv)
     g = _empty(y.shape[0], C, dev=dx.device)
     K.linear_dx(dlin, ws["wout_perm"].view(d, S.F2 * C), g.view(S.rows, S.F2 * C), epi=_lib.EPI_DRELU,
                 aux=y.view(S.rows, S.F2 * C))
@@ -390,10 +394,12 @@ def _ffn_forward(cfg, P, L, which, norm, x, pd, seed, salt, li, site_act, site_o
 
 
 def layer_forward(cfg, S: EncoderShapes, P, L, li, x, out, pos_emb, lengths, *, train, seed, salt, save,
-                  bn_update=None, rm_batch=True, ppos=None):
+                  bn_update=None, rm_batch=True, ppos=None, bn_stats=None):
     """x (rows, d) -> out (rows, d) (written in place).  Returns ctx for backward when save.
     ppos: this layer's projected positions linear_pos(pos_emb) (npos, d) when the caller computed
-    every layer's at once (pos_proj_all); otherwise projected here."""
+    every layer's at once (pos_proj_all); otherwise projected here.  bn_stats: a zeroed (2d,) f64 buffer
+    the BatchNorm batch sums may accumulate into when the training finalize runs (it leaves the buffer
+    zeroed again, so the encoder's layers reuse one buffer without a memset per layer)."""
     dev = x.device
     rows, d, H, dk, T, B, ff = S.rows, S.d, S.h, S.dk, S.T, S.B, S.ff
     pd = cfg.dropout if train else 0.0
@@ -500,7 +506,11 @@ def layer_forward(cfg, S: EncoderShapes, P, L, li, x, out, pos_emb, lengths, *, 
         K.linear(ln3, P[L + "conv.pointwise_conv1.weight"].view(2 * d, d), P[L + "conv.pointwise_conv1.bias"], a)
         K.glu_mask_fwd(a, lengths, g, B, T, d)
     y = _empty(rows, d, dev=dev)
-    stats = torch.zeros(2 * d, device=dev, dtype=torch.float64) if rm_batch else None
+    fin_running = rm_batch and bn_update is not None and train
+    if fin_running and bn_stats is not None:
+        stats = bn_stats   # zero on entry; kdfm_bn_finalize_running re-zeroes it after reading
+    else:
+        stats = torch.zeros(2 * d, device=dev, dtype=torch.float64) if rm_batch else None
     with K.span("dwconv", nbytes=4.0 * 2 * rows * d):   # read g + write y (f32), SURVEY.md §8(d)
         K.dwconv_fwd(g, P[L + "conv.depthwise_conv.weight"].view(d, -1), P[L + "conv.depthwise_conv.bias"], y, stats,
                      B, T, d, cfg.conv_kernel)
@@ -555,9 +565,9 @@ class LnGrads:
         self.n = K.layernorm_bwd_ws(rows, d)
         self.pending = []
 
-    def bwd(self, dy, x, g, mean, rstd, dx, dg, db, dres=None):
+    def bwd(self, dy, x, g, mean, rstd, dx, dg, db, dres=None, dy2=None):
         part = self.buf[len(self.pending)][: self.n]
-        K.layernorm_bwd_part(dy, x, g, mean, rstd, dx, part, dres=dres)
+        K.layernorm_bwd_part(dy, x, g, mean, rstd, dx, part, dres=dres, dy2=dy2)
         self.pending.append((part, dg, db))
 
     def reserve(self, dg, db):
@@ -567,8 +577,11 @@ class LnGrads:
         return part
 
     def fold(self):
+        """On the weight-gradient stream (the partials are complete when it forks): the buffer must not be
+        reused by the next layer before the join -- encoder_backward gives every layer its own."""
         if self.pending:
-            K.ln_fold(self.pending, self.rows, self.d)
+            pend, rows, d = self.pending, self.rows, self.d
+            WGRAD.run(lambda: K.ln_fold(pend, rows, d), self.buf)
             self.pending = []
 
 
@@ -634,8 +647,9 @@ def _ffn_backward(P, G, L, which, dres_out, ctx, tag, x_in_ln, norm, pd, seed, s
     return dx
 
 
-def layer_backward(cfg, S: EncoderShapes, P, G, L, li, ctx, dout, pos_emb, lengths, *, seed, salt, ln_buf=None):
-    """dout: grad wrt the layer output (rows, d). Returns grad wrt the layer input."""
+def layer_backward(cfg, S: EncoderShapes, P, G, L, li, ctx, dout, pos_emb, lengths, *, seed, salt, ln_buf=None,
+                   dout2=None):
+    """dout (+ dout2 when given): grad wrt the layer output (rows, d). Returns grad wrt the layer input."""
     dev = dout.device
     rows, d, H, dk, T, B = S.rows, S.d, S.h, S.dk, S.T, S.B
     pd = ctx["pd"]
@@ -646,7 +660,7 @@ def layer_backward(cfg, S: EncoderShapes, P, G, L, li, ctx, dout, pos_emb, lengt
     # norm_out
     dx4 = _empty(rows, d, dev=dev)
     lng.bwd(dout, ctx["x4"], P[L + "norm_out.weight"], ctx["m5"], ctx["r5"], dx4, G[L + "norm_out.weight"],
-            G[L + "norm_out.bias"])
+            G[L + "norm_out.bias"], dy2=dout2)
     # FFN2: x4 = x3 + 0.5 drop(ffn(LN4 x3))
     dx3 = _ffn_backward(P, G, L, "feed_forward2", dx4, ctx, "4", ctx["x3"], L + "norm_feed_forward2", pd, seed, salt,
                         li, SITE_FF2_ACT, SITE_FF2_OUT, dev, lng, pend)
@@ -676,9 +690,12 @@ def layer_backward(cfg, S: EncoderShapes, P, G, L, li, ctx, dout, pos_emb, lengt
                   G[L + "conv.batch_norm.bias"], batch_stats=ctx["rm_batch"])
     del dz
     dg = _empty(rows, d, dev=dev)
-    K.dwconv_bwd(dy, ctx["g"], P[L + "conv.depthwise_conv.weight"].view(d, -1), dg,
-                 G[L + "conv.depthwise_conv.weight"].view(d, -1), G[L + "conv.depthwise_conv.bias"], B, T, d,
-                 cfg.conv_kernel)
+    # the depthwise weight / bias gradient's fold of per-block partials runs on the weight-gradient stream
+    dws = torch.empty(K.dwconv_bwd_ws(B, T, d, cfg.conv_kernel), device=dev)
+    K.dwconv_bwd(dy, ctx["g"], P[L + "conv.depthwise_conv.weight"].view(d, -1), dg, None, None, B, T, d,
+                 cfg.conv_kernel, ws=dws)
+    WGRAD.run(lambda: K.dwconv_bwd_fold(dws, G[L + "conv.depthwise_conv.weight"].view(d, -1),
+                                        G[L + "conv.depthwise_conv.bias"], B, T, d, cfg.conv_kernel), dws)
     del dy
     dx2 = _empty(rows, d, dev=dev)
     if ctx["ln3"] is None:   # fused LN + pointwise_conv1 + GLU forward: fused backward
@@ -736,11 +753,9 @@ def layer_backward(cfg, S: EncoderShapes, P, G, L, li, ctx, dout, pos_emb, lengt
         # weight-gradient stream beside the dQ / dK,dV kernels the main stream needs next
         lse, pt, mblk = ctx["lse"], ctx["pt"], ctx["mblk"]
         if pt is None:   # bwd2
-            rsum = torch.empty(B * H * T, device=dev)
             dS, Pdr = K.attn_bwd2_saved(B, H, T, dev)
-            K.relpos_attn_bwd2_dq(do, ctx["o"], qu, qv, qkv, ppos, lse, lengths, rsum, dS, Pdr, dqu, dqv, B, H, T, sc,
+            K.relpos_attn_bwd2_dq(do, ctx["o"], qu, qv, qkv, ppos, lse, lengths, None, dS, Pdr, dqu, dqv, B, H, T, sc,
                                   ctx["pa"], seed, st_att)
-            del rsum
             dpws = torch.empty(K.relpos_attn_bwd2_dpos_ws(B, T, d), device=dev)
 
             def dpos_and_wgrad2():
@@ -903,13 +918,19 @@ def encoder_forward_steps(cfg, S: EncoderShapes, P, prefix, mel, mel_len, len1, 
     # after the yield: the caller issues the layers under their own stream, and the projections must be
     # allocated (torch's per-stream pools) and written on the stream whose layers read them
     pp = pos_proj_all(cfg, P, prefix, pos_emb)
+    bn_stats = None
+    if train and bn_running is not None and use_batch_stats:
+        bn_stats = ws.get("bn_stats")
+        if bn_stats is None:
+            bn_stats = ws["bn_stats"] = torch.zeros(2 * S.d, device=mel.device, dtype=torch.float64)
     for i in range(cfg.n_layers):
         L = f"{prefix}layers.{i}."
         bn = None
         if bn_running is not None:
             bn = (bn_running[L + "conv.batch_norm.running_mean"], bn_running[L + "conv.batch_norm.running_var"])
         ctx = layer_forward(cfg, S, P, L, i, x, feats[i], pos_emb, len2, train=train, seed=seed, salt=salt,
-                            save=save, bn_update=bn, rm_batch=use_batch_stats, ppos=None if pp is None else pp[i])
+                            save=save, bn_update=bn, rm_batch=use_batch_stats, ppos=None if pp is None else pp[i],
+                            bn_stats=bn_stats)
         if save:
             run.layers.append(ctx)
         x = feats[i]
@@ -934,21 +955,22 @@ def encoder_backward(cfg, S: EncoderShapes, P, G, prefix, run: EncoderRun, dfeat
     i's parameter gradients are all issued (bucketed all-reduce overlap, kdfm/ddp.py);
     before_read {j: fn}: fn() runs right before dfeats[j] is first read (a stream join for heads
     gradients produced on another stream)."""
-    dout = dfeats[cfg.n_layers - 1]
-    if "ln_parts" not in ws:
-        ws["ln_parts"] = torch.empty(6, K.layernorm_bwd_ws(S.rows, S.d), device=dfeats.device)
+    dout, dout2 = dfeats[cfg.n_layers - 1], None
     for i in range(cfg.n_layers - 1, -1, -1):
         L = f"{prefix}layers.{i}."
+        # a partial buffer per layer: its LayerNorm fold runs on the weight-gradient stream (LnGrads.fold);
+        # layer i's output gradient is dfeats[i] + the gradient layer i + 1 passed down (summed on load by
+        # norm_out's LayerNorm backward)
         dx = layer_backward(cfg, S, P, G, L, i, run.layers[i], dout, pos_emb, len2, seed=seed, salt=salt,
-                            ln_buf=ws["ln_parts"])
+                            ln_buf=torch.empty(6, K.layernorm_bwd_ws(S.rows, S.d), device=dfeats.device),
+                            dout2=dout2)
         run.layers[i] = None
         if on_layer_done is not None:
             on_layer_done(i)
         if i > 0:
             if before_read is not None and (i - 1) in before_read:
                 before_read[i - 1]()
-            K.axpby(dfeats[i - 1], dx, dfeats[i - 1], 1.0, 1.0)
-            dout = dfeats[i - 1]
+            dout, dout2 = dfeats[i - 1], dx
     subsampling_backward(cfg, S, P, G, prefix, run.sub, dx, len1, seed=seed, salt=salt, ws=ws)
     run.sub = None
     WGRAD.join()  # weight gradients computed on the side stream are complete before anyone reads G

@@ -493,8 +493,7 @@ class Ver5Engine:
         if cfg.kd_model == "encfm":
             # decoder first: its input is the last layer's FM output, whose gradient the FM backward needs
             ews = ctx.pop("ews")
-            K.linear_dw(g, ctx["dec_in"], G["decoder.decoder_layers.0.weight"].view(Cn, Ss.d),
-                        db=G["decoder.decoder_layers.0.bias"])
+            self._decoder_dw(g, ctx["dec_in"])
             K.linear_dx(g, Wd, ews.gxS)
             del g
             with K.region("encfm_backward"):
@@ -504,8 +503,7 @@ class Ver5Engine:
         elif ctx.get("hctx") is None:
             # logit KD only (kd_model "logitkd"): the decoder's gradient is the encoder's only input gradient
             ctx.pop("hctx", None)
-            K.linear_dw(g, ctx["sfeats"][-1], G["decoder.decoder_layers.0.weight"].view(Cn, Ss.d),
-                        db=G["decoder.decoder_layers.0.bias"])
+            self._decoder_dw(g, ctx["sfeats"][-1])
             K.fill(dfeats, 0.0)
             K.linear_dx(g, Wd, dfeats[-1])
             del g
@@ -532,8 +530,7 @@ class Ver5Engine:
             if grad_ready is not None:
                 grad_ready(min(o for k, o in off.items() if not k.startswith(("encoder.", "decoder."))))
             # decoder: logits = W enc + b ; grad wrt logits from CTC + KL
-            K.linear_dw(g, ctx["sfeats"][-1], G["decoder.decoder_layers.0.weight"].view(Cn, Ss.d),
-                        db=G["decoder.decoder_layers.0.bias"])
+            self._decoder_dw(g, ctx["sfeats"][-1])
             K.linear_dx(g, Wd, dfeats[-1], R=dfeats[-1], rscale=1.0)
             del g
         layer_done = None
@@ -549,6 +546,14 @@ class Ver5Engine:
                              on_layer_done=layer_done,
                              before_read=None if join is None else {join[0]: lambda: torch.cuda.current_stream(
                                  self.device).wait_stream(join[1])})
+
+    def _decoder_dw(self, g, x):
+        """The decoder's weight / bias gradient from the logits gradient g and its input x, on the
+        weight-gradient stream (a parameter gradient only: off the compute stream's path)."""
+        G = self.student.G
+        Cn, d = g.shape[1], x.shape[1]
+        WGRAD.run(lambda: K.linear_dw(g, x, G["decoder.decoder_layers.0.weight"].view(Cn, d),
+                                      db=G["decoder.decoder_layers.0.bias"]), g, x)
 
     def optimizer_step(self, grad_scale: float = 1.0):
         with self._on_stream(), self._mode(), K.region("optimizer"):

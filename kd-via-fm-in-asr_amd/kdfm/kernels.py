@@ -1141,12 +1141,17 @@ def layernorm_bwd_ws(rows, d):
     return int(_lib.lib().kdfm_layernorm_bwd_ws(rows, d))
 
 
-def layernorm_bwd_part(dy, x, g, mean, rstd, dx, part, dres=None):
+def layernorm_bwd_part(dy, x, g, mean, rstd, dx, part, dres=None, dy2=None):
     """LayerNorm backward with the dgamma/dbeta fold deferred to ln_fold (part: >= layernorm_bwd_ws
-    floats, kept until the fold)."""
+    floats, kept until the fold); dy2: a second output gradient summed into dy on load."""
     rows, d = x.shape
     assert dy.is_contiguous() and dx.is_contiguous() and (dres is None or dres.is_contiguous())
     assert part.numel() >= layernorm_bwd_ws(rows, d)
+    if dy2 is not None:
+        assert dy2.is_contiguous() and dy2.shape == dy.shape
+        call("kdfm_layernorm_bwd_part2", ptr(dy), ptr(dy2), ptr(x), ptr(g), ptr(mean), ptr(rstd), ptr(dres), ptr(dx),
+             ptr(part), rows, d, _s())
+        return
     call("kdfm_layernorm_bwd_part", ptr(dy), ptr(x), ptr(g), ptr(mean), ptr(rstd), ptr(dres), ptr(dx), ptr(part),
          rows, d, _s())
 
@@ -1237,11 +1242,12 @@ def attn_bwd2_saved(B, H, T, device):
 
 def relpos_attn_bwd2_dq(do, o, qu, qv, qkv, ppos, lse, lengths, rsum, ds, pd, dqu, dqv, B, H, T, scale, p, seed,
                         rng_stream):
-    """bwd2 part 1 (csrc/attn_bwd.hip): row sums r_i = dO_i . O_i into rsum (B*H*T), dqu / dqv, and the bf16
+    """bwd2 part 1 (csrc/attn_bwd.hip): dqu / dqv (the row sums r_i = dO_i . O_i formed in-kernel; rsum is
+    unused and may be None), and the bf16
     dS / Pd (attn_bwd2_saved) the _dkv / _dpos parts read."""
     rows, d = do.shape
     assert rows == B * T and qkv.shape == (rows, 3 * d) and lse.shape == (B, H, T) and o.shape == do.shape
-    assert rsum.numel() >= B * H * T and ds.dtype == torch.bfloat16 and pd.dtype == torch.bfloat16
+    assert ds.dtype == torch.bfloat16 and pd.dtype == torch.bfloat16
     assert ds.shape == pd.shape and ds.shape[:3] == (B, H, T) and ds.is_contiguous() and pd.is_contiguous()
     for t in (do, o, qu, qv, qkv, ppos, lse, dqu, dqv):
         assert t.is_contiguous()
@@ -1329,9 +1335,21 @@ def dwconv_fwd(g, w, bias, y, stats, B, T, d, K):
     call("kdfm_dwconv_fwd", ptr(g), ptr(w), ptr(bias), ptr(y), ptr(stats), B, T, d, K, _s())
 
 
-def dwconv_bwd(dy, g, w, dg, dw, db, B, T, d, K):
-    ws = scratch(dy.device, _lib.lib().kdfm_dwconv_bwd_ws(B, T, d, K))
+def dwconv_bwd(dy, g, w, dg, dw, db, B, T, d, K, *, ws=None):
+    """dg = conv^T(dy) and dw / db (+=).  dw = db = None with `ws` given: only dg, the weight-gradient
+    partials left in ws for dwconv_bwd_fold (e.g. on another stream)."""
+    if ws is None:
+        assert dw is not None
+        ws = scratch(dy.device, _lib.lib().kdfm_dwconv_bwd_ws(B, T, d, K))
     call("kdfm_dwconv_bwd", ptr(dy), ptr(g), ptr(w), ptr(dg), ptr(dw), ptr(db), ptr(ws), B, T, d, K, _s())
+
+
+def dwconv_bwd_ws(B, T, d, K):
+    return int(_lib.lib().kdfm_dwconv_bwd_ws(B, T, d, K))
+
+
+def dwconv_bwd_fold(ws, dw, db, B, T, d, K):
+    call("kdfm_dwconv_bwd_fold", ptr(ws), ptr(dw), ptr(db), B, T, d, K, _s())
 
 
 def bn_finalize(stats, rm, rv, mean, rstd, d, count, eps):

@@ -34,7 +34,6 @@ class MhaShape:
         self.dqu, self.dqv = f(n, d), f(n, d)
         if self.fused:
             self.ppos = torch.zeros(2 * T - 1, d, device=dev)
-            self.rsum = f(B * H * T)
             self.ds, self.pd = K.attn_bwd2_saved(B, H, T, dev)
         else:
             self.bd = torch.zeros(B, H, T, 2 * T - 1, device=dev)
@@ -69,7 +68,7 @@ def mha_bwd(sh: MhaShape, sv, qkv, q, o, do, dqkv, p, seed, rng_stream):
     """dqkv (rows, 3d) = d loss / d [q | k | v] given do = d loss / d o (overwritten)."""
     B, H, T, d, dk = sh.B, sh.H, sh.T, sh.d, sh.dk
     if sh.fused:
-        K.relpos_attn_bwd2_dq(do, o, q, q, qkv, sh.ppos, sv["lse"], sh.lens, sh.rsum, sh.ds, sh.pd, sh.dqu, sh.dqv,
+        K.relpos_attn_bwd2_dq(do, o, q, q, qkv, sh.ppos, sv["lse"], sh.lens, None, sh.ds, sh.pd, sh.dqu, sh.dqv,
                               B, H, T, sh.scale, p, seed, rng_stream)
         K.relpos_attn_bwd2_dkv(do, q, sh.ds, sh.pd, sh.lens, dqkv, B, H, T)
         K.axpby(sh.dqu, None, dqkv[:, :d], 1.0, 0.0)
