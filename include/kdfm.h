@@ -653,6 +653,14 @@ int kdfm_glu_mask_bwd(const float* dg, const float* a, const int64_t* lengths, f
                       int64_t d, void* stream);
 int kdfm_dwconv_fwd(const float* g, const float* w, const float* bias, float* y, double* stats, int64_t B, int64_t T,
                     int64_t d, int64_t K, void* stream);
+/* kdfm_dwconv_fwd with the training BatchNorm finalize in the same launch: the last workgroup to add its
+ * batch sums into stats (zero on entry; 2d doubles) forms mean / rstd (d floats each), updates the running
+ * statistics with `momentum` (unbiased variance), and resets stats and *counter (a device uint32, zero on
+ * entry) to zero for the next call -- kdfm_bn_finalize_running without its launch.  Deterministic mode:
+ * the ordered statistics kernel and the finalize as separate launches, same results contract. */
+int kdfm_dwconv_fwd_bn(const float* g, const float* w, const float* bias, float* y, double* stats, uint32_t* counter,
+                       float* running_mean, float* running_var, float* mean, float* rstd, int64_t B, int64_t T,
+                       int64_t d, int64_t K, float eps, float momentum, void* stream);
 /* dg = conv^T(dy); dw, db accumulate (+=) */
 /* dw/db accumulated (+=) through per-block partials in ws (>= kdfm_dwconv_bwd_ws(B, T, d, K) floats);
  * dw == db == NULL: only dg, the partials are left in ws for kdfm_dwconv_bwd_fold (which may run on
@@ -676,6 +684,11 @@ int kdfm_bn_silu_fwd(const float* y, const float* mean, const float* rstd, const
 int kdfm_bn_silu_bwd(const float* dz, const float* y, const float* mean, const float* rstd, const float* gamma,
                      const float* beta, double* red_ws, float* dy, float* dgamma, float* dbeta, int64_t rows,
                      int64_t d, int32_t batch_stats, void* stream);
+/* the same without the memset: red_ws (2d doubles) must be zero on entry; red_next (another 2d buffer or
+ * NULL) is zeroed by the launch for the next call -- a ring of buffers serves a stack of layers */
+int kdfm_bn_silu_bwd2(const float* dz, const float* y, const float* mean, const float* rstd, const float* gamma,
+                      const float* beta, double* red_ws, double* red_next, float* dy, float* dgamma, float* dbeta,
+                      int64_t rows, int64_t d, int32_t batch_stats, void* stream);
 
 /* ---------------- decoder / losses (conv_asr.py:456-468; losses/ctc.py:68-82; asr_train_diffm.py:740-811) */
 int kdfm_log_softmax(const float* x, float* y, int64_t rows, int64_t C, int64_t ldx, int64_t ldy, void* stream);

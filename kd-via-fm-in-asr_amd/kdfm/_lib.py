@@ -169,6 +169,7 @@ SIGNATURES: dict[str, tuple] = {
     "kdfm_glu_mask_fwd": (_i32, [P, P, P, _i64, _i64, _i64, P]),
     "kdfm_glu_mask_bwd": (_i32, [P, P, P, P, _i64, _i64, _i64, P]),
     "kdfm_dwconv_fwd": (_i32, [P, P, P, P, P, _i64, _i64, _i64, _i64, P]),
+    "kdfm_dwconv_fwd_bn": (_i32, [P, P, P, P, P, P, P, P, P, P, _i64, _i64, _i64, _i64, _f32, _f32, P]),
     "kdfm_dwconv_bwd": (_i32, [P, P, P, P, P, P, P, _i64, _i64, _i64, _i64, P]),
     "kdfm_dwconv_bwd_fold": (_i32, [P, P, P, _i64, _i64, _i64, _i64, P]),
     "kdfm_dwconv_bwd_ws": (_i64, [_i64, _i64, _i64, _i64]),
@@ -177,6 +178,7 @@ SIGNATURES: dict[str, tuple] = {
     "kdfm_bn_finalize_running": (_i32, [P, P, P, P, P, _i64, _i64, _f32, _f32, P]),
     "kdfm_bn_silu_fwd": (_i32, [P, P, P, P, P, P, _i64, _i64, P]),
     "kdfm_bn_silu_bwd": (_i32, [P, P, P, P, P, P, P, P, P, P, _i64, _i64, _i32, P]),
+    "kdfm_bn_silu_bwd2": (_i32, [P, P, P, P, P, P, P, P, P, P, P, _i64, _i64, _i32, P]),
     "kdfm_log_softmax": (_i32, [P, P, _i64, _i64, _i64, _i64, P]),
     "kdfm_argmax_rows": (_i32, [P, P, _i64, _i64, P]),
     "kdfm_log_softmax_bwd": (_i32, [P, P, P, _i64, _i64, P]),

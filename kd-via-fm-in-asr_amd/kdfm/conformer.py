@@ -397,9 +397,10 @@ def layer_forward(cfg, S: EncoderShapes, P, L, li, x, out, pos_emb, lengths, *, 
                   bn_update=None, rm_batch=True, ppos=None, bn_stats=None):
     """x (rows, d) -> out (rows, d) (written in place).  Returns ctx for backward when save.
     ppos: this layer's projected positions linear_pos(pos_emb) (npos, d) when the caller computed
-    every layer's at once (pos_proj_all); otherwise projected here.  bn_stats: a zeroed (2d,) f64 buffer
-    the BatchNorm batch sums may accumulate into when the training finalize runs (it leaves the buffer
-    zeroed again, so the encoder's layers reuse one buffer without a memset per layer)."""
+    every layer's at once (pos_proj_all); otherwise projected here.  bn_stats: (sums (2d,) f64, counter (1,)
+    int32), both zero: the training BatchNorm finalize then rides on the depthwise-conv launch
+    (kdfm_dwconv_fwd_bn), which leaves them zero again -- the encoder's layers share one pair, no memset
+    or finalize launch per layer."""
     dev = x.device
     rows, d, H, dk, T, B, ff = S.rows, S.d, S.h, S.dk, S.T, S.B, S.ff
     pd = cfg.dropout if train else 0.0
@@ -507,17 +508,23 @@ def layer_forward(cfg, S: EncoderShapes, P, L, li, x, out, pos_emb, lengths, *, 
         K.glu_mask_fwd(a, lengths, g, B, T, d)
     y = _empty(rows, d, dev=dev)
     fin_running = rm_batch and bn_update is not None and train
-    if fin_running and bn_stats is not None:
-        stats = bn_stats   # zero on entry; kdfm_bn_finalize_running re-zeroes it after reading
-    else:
-        stats = torch.zeros(2 * d, device=dev, dtype=torch.float64) if rm_batch else None
-    with K.span("dwconv", nbytes=4.0 * 2 * rows * d):   # read g + write y (f32), SURVEY.md §8(d)
-        K.dwconv_fwd(g, P[L + "conv.depthwise_conv.weight"].view(d, -1), P[L + "conv.depthwise_conv.bias"], y, stats,
-                     B, T, d, cfg.conv_kernel)
     bmean = _empty(d, dev=dev)
     brstd = _empty(d, dev=dev)
     rmn, rvr = bn_update if bn_update is not None else (None, None)
-    if stats is not None and rm_batch and bn_update is not None and train:
+    stats = None
+    if fin_running and bn_stats is not None:
+        with K.span("dwconv", nbytes=4.0 * 2 * rows * d):   # read g + write y (f32), SURVEY.md §8(d)
+            K.dwconv_fwd_bn(g, P[L + "conv.depthwise_conv.weight"].view(d, -1), P[L + "conv.depthwise_conv.bias"], y,
+                            bn_stats[0], bn_stats[1], rmn, rvr, bmean, brstd, B, T, d, cfg.conv_kernel, cfg.bn_eps,
+                            cfg.bn_momentum)
+    else:
+        stats = torch.zeros(2 * d, device=dev, dtype=torch.float64) if rm_batch else None
+        with K.span("dwconv", nbytes=4.0 * 2 * rows * d):
+            K.dwconv_fwd(g, P[L + "conv.depthwise_conv.weight"].view(d, -1), P[L + "conv.depthwise_conv.bias"], y,
+                         stats, B, T, d, cfg.conv_kernel)
+    if stats is None and fin_running and bn_stats is not None:
+        pass   # finalized in the depthwise-conv launch
+    elif stats is not None and rm_batch and bn_update is not None and train:
         # batch statistics and the running-statistics update in one launch
         K.bn_finalize_running(stats, rmn, rvr, bmean, brstd, d, rows, cfg.bn_eps, cfg.bn_momentum)
     else:
@@ -648,8 +655,10 @@ def _ffn_backward(P, G, L, which, dres_out, ctx, tag, x_in_ln, norm, pd, seed, s
 
 
 def layer_backward(cfg, S: EncoderShapes, P, G, L, li, ctx, dout, pos_emb, lengths, *, seed, salt, ln_buf=None,
-                   dout2=None):
-    """dout (+ dout2 when given): grad wrt the layer output (rows, d). Returns grad wrt the layer input."""
+                   dout2=None, bn_red=None):
+    """dout (+ dout2 when given): grad wrt the layer output (rows, d). Returns grad wrt the layer input.
+    bn_red: (red, red_next) f64 (2d,) buffers of a ring: red zero on entry, red_next zeroed for the next
+    layer (no memset launch per layer); None: a fresh buffer zeroed by the launch."""
     dev = dout.device
     rows, d, H, dk, T, B = S.rows, S.d, S.h, S.dk, S.T, S.B
     pd = ctx["pd"]
@@ -684,10 +693,15 @@ def layer_backward(cfg, S: EncoderShapes, P, G, L, li, ctx, dout, pos_emb, lengt
         K.linear_dx(dpw2, P[L + "conv.pointwise_conv2.weight"].view(d, d), dz)
         del dpw2
     dy = _empty(rows, d, dev=dev)
-    red = torch.empty(2 * d, device=dev, dtype=torch.float64)
-    K.bn_silu_bwd(dz, ctx["y"], ctx["bmean"], ctx["brstd"], P[L + "conv.batch_norm.weight"],
-                  P[L + "conv.batch_norm.bias"], red, dy, G[L + "conv.batch_norm.weight"],
-                  G[L + "conv.batch_norm.bias"], batch_stats=ctx["rm_batch"])
+    if bn_red is not None:
+        K.bn_silu_bwd(dz, ctx["y"], ctx["bmean"], ctx["brstd"], P[L + "conv.batch_norm.weight"],
+                      P[L + "conv.batch_norm.bias"], bn_red[0], dy, G[L + "conv.batch_norm.weight"],
+                      G[L + "conv.batch_norm.bias"], batch_stats=ctx["rm_batch"], red_next=bn_red[1], zeroed=True)
+    else:
+        red = torch.empty(2 * d, device=dev, dtype=torch.float64)
+        K.bn_silu_bwd(dz, ctx["y"], ctx["bmean"], ctx["brstd"], P[L + "conv.batch_norm.weight"],
+                      P[L + "conv.batch_norm.bias"], red, dy, G[L + "conv.batch_norm.weight"],
+                      G[L + "conv.batch_norm.bias"], batch_stats=ctx["rm_batch"])
     del dz
     dg = _empty(rows, d, dev=dev)
     # the depthwise weight / bias gradient's fold of per-block partials runs on the weight-gradient stream
@@ -922,7 +936,8 @@ def encoder_forward_steps(cfg, S: EncoderShapes, P, prefix, mel, mel_len, len1, 
     if train and bn_running is not None and use_batch_stats:
         bn_stats = ws.get("bn_stats")
         if bn_stats is None:
-            bn_stats = ws["bn_stats"] = torch.zeros(2 * S.d, device=mel.device, dtype=torch.float64)
+            bn_stats = ws["bn_stats"] = (torch.zeros(2 * S.d, device=mel.device, dtype=torch.float64),
+                                         torch.zeros(1, device=mel.device, dtype=torch.int32))
     for i in range(cfg.n_layers):
         L = f"{prefix}layers.{i}."
         bn = None
@@ -956,14 +971,22 @@ def encoder_backward(cfg, S: EncoderShapes, P, G, prefix, run: EncoderRun, dfeat
     before_read {j: fn}: fn() runs right before dfeats[j] is first read (a stream join for heads
     gradients produced on another stream)."""
     dout, dout2 = dfeats[cfg.n_layers - 1], None
+    n = cfg.n_layers
+    ring = None
+    if n >= 2:   # BatchNorm-backward sums: call k uses ring[k] and zeroes ring[(k + 1) % n] for the next call
+        ring = ws.get("bn_red_ring")
+        if ring is None:
+            ring = ws["bn_red_ring"] = torch.zeros(n, 2 * S.d, device=dfeats.device, dtype=torch.float64)
     for i in range(cfg.n_layers - 1, -1, -1):
         L = f"{prefix}layers.{i}."
+        k = n - 1 - i
+        bn_red = None if ring is None else (ring[k], ring[(k + 1) % n])
         # a partial buffer per layer: its LayerNorm fold runs on the weight-gradient stream (LnGrads.fold);
         # layer i's output gradient is dfeats[i] + the gradient layer i + 1 passed down (summed on load by
         # norm_out's LayerNorm backward)
         dx = layer_backward(cfg, S, P, G, L, i, run.layers[i], dout, pos_emb, len2, seed=seed, salt=salt,
                             ln_buf=torch.empty(6, K.layernorm_bwd_ws(S.rows, S.d), device=dfeats.device),
-                            dout2=dout2)
+                            dout2=dout2, bn_red=bn_red)
         run.layers[i] = None
         if on_layer_done is not None:
             on_layer_done(i)

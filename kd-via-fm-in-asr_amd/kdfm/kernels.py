@@ -1335,6 +1335,14 @@ def dwconv_fwd(g, w, bias, y, stats, B, T, d, K):
     call("kdfm_dwconv_fwd", ptr(g), ptr(w), ptr(bias), ptr(y), ptr(stats), B, T, d, K, _s())
 
 
+def dwconv_fwd_bn(g, w, bias, y, stats, counter, rm, rv, mean, rstd, B, T, d, K, eps, momentum):
+    """dwconv_fwd + the training BatchNorm finalize (batch mean / rstd, running statistics) in one launch;
+    stats (2d f64) and counter (1 int32) must be zero on entry and are zero again on exit."""
+    assert stats.dtype == torch.float64 and counter.dtype == torch.int32
+    call("kdfm_dwconv_fwd_bn", ptr(g), ptr(w), ptr(bias), ptr(y), ptr(stats), ptr(counter), ptr(rm), ptr(rv),
+         ptr(mean), ptr(rstd), B, T, d, K, float(eps), float(momentum), _s())
+
+
 def dwconv_bwd(dy, g, w, dg, dw, db, B, T, d, K, *, ws=None):
     """dg = conv^T(dy) and dw / db (+=).  dw = db = None with `ws` given: only dg, the weight-gradient
     partials left in ws for dwconv_bwd_fold (e.g. on another stream)."""
@@ -1371,8 +1379,14 @@ def bn_silu_fwd(y, mean, rstd, g, b, z):
     call("kdfm_bn_silu_fwd", ptr(y), ptr(mean), ptr(rstd), ptr(g), ptr(b), ptr(z), rows, d, _s())
 
 
-def bn_silu_bwd(dz, y, mean, rstd, g, b, red_ws, dy, dg, db, batch_stats=True):
+def bn_silu_bwd(dz, y, mean, rstd, g, b, red_ws, dy, dg, db, batch_stats=True, red_next=None, zeroed=False):
+    """zeroed: red_ws is already zero (no memset; kdfm_bn_silu_bwd2), and red_next (when given) is zeroed by the
+    launch for the next call."""
     rows, d = y.shape
+    if zeroed:
+        call("kdfm_bn_silu_bwd2", ptr(dz), ptr(y), ptr(mean), ptr(rstd), ptr(g), ptr(b), ptr(red_ws), ptr(red_next),
+             ptr(dy), ptr(dg), ptr(db), rows, d, int(batch_stats), _s())
+        return
     call("kdfm_bn_silu_bwd", ptr(dz), ptr(y), ptr(mean), ptr(rstd), ptr(g), ptr(b), ptr(red_ws), ptr(dy), ptr(dg),
          ptr(db), rows, d, int(batch_stats), _s())
 
