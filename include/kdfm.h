@@ -669,6 +669,19 @@ int kdfm_dwconv_bwd(const float* dy, const float* g, const float* w, float* dg, 
                     int64_t B, int64_t T, int64_t d, int64_t K, void* stream);
 int kdfm_dwconv_bwd_fold(const float* ws, float* dw, float* db, int64_t B, int64_t T, int64_t d, int64_t K,
                          void* stream);
+/* The BatchNorm(+SiLU) backward's elementwise half applied on load by the depthwise backward: dz is the
+ * gradient wrt silu(BN(y)); red (2d doubles, zero before kdfm_bn_silu_bwd_reduce) holds the reduction's
+ * sums (batch_stats: sum dyb | sum dyb xhat); the launch forms dy = d loss / d y tile by tile (never stored),
+ * then dg and the weight partials as kdfm_dwconv_bwd (fold with kdfm_dwconv_bwd_fold); its first workgroup
+ * adds the affine gradients dgamma += sum dyb xhat, dbeta += sum dyb and zeroes red_next (another 2d buffer
+ * or NULL).  K = 15 or 31.  Replaces kdfm_bn_silu_bwd2's apply launch. */
+int kdfm_dwconv_bwd_bn(const float* dz, const float* y, const float* mean, const float* rstd, const float* gamma,
+                       const float* beta, const double* red, double* red_next, float* dgamma, float* dbeta,
+                       int32_t batch_stats, const float* g, const float* w, float* dg, float* ws, int64_t B,
+                       int64_t T, int64_t d, int64_t K, void* stream);
+/* the BN-SiLU backward's reduction alone: red (2d doubles, zero on entry) += (sum dyb, sum dyb xhat) */
+int kdfm_bn_silu_bwd_reduce(const float* dz, const float* y, const float* mean, const float* rstd, const float* gamma,
+                            const float* beta, double* red, int64_t rows, int64_t d, void* stream);
 int64_t kdfm_dwconv_bwd_ws(int64_t B, int64_t T, int64_t d, int64_t K);
 int kdfm_bn_finalize(const double* stats, const float* running_mean, const float* running_var, float* mean,
                      float* rstd, int64_t d, int64_t count, float eps, void* stream);

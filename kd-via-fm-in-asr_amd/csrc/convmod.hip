@@ -353,6 +353,60 @@ __global__ __launch_bounds__(256) void bn_silu_bwd_apply_kernel(const float* __r
   dy[idx] = v;
 }
 
+// BatchNorm + SiLU backward applied on load (kdfm_dwconv_bwd_bn): the depthwise backward's input gradient
+//   dy = gamma rstd (dz silu'(gamma xh + beta) - m1 - xh m2),  xh = (y - mean) rstd,  m1|m2 = red / count
+// (batch statistics; gamma rstd dz silu'(.) with the running ones) is formed from dz and y as the tile is
+// staged, so it never reaches HBM and its elementwise launch disappears.
+struct BnApply {
+  const float* y; const float* mean; const float* rstd; const float* gm; const float* bt; const double* red;
+  double count; int batch_stats;
+  float* dgamma; float* dbeta; double* red_next;   // block (0,0,0): affine grads from red, zero red_next
+};
+
+__device__ __forceinline__ void tile_load_bn(float4 (&v)[TQ], const float* __restrict__ dz, const BnApply& a,
+                                             int64_t b, int64_t t0, int pad, int rows, int64_t T, int64_t d,
+                                             int64_t c0) {
+  // this thread's 4 channels are the same for every unit (256 threads, 16 float4 per tile row)
+  const int c4 = (threadIdx.x & 15) * 4;
+  const int64_t cb = c0 + c4 < d ? c0 + c4 : 0;
+  float mu[4], rs[4], gm[4], bt[4], m1[4], m2[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    mu[j] = a.mean[cb + j];
+    rs[j] = a.rstd[cb + j];
+    gm[j] = a.gm[cb + j];
+    bt[j] = a.bt[cb + j];
+    m1[j] = a.batch_stats ? (float)(a.red[cb + j] / a.count) : 0.f;
+    m2[j] = a.batch_stats ? (float)(a.red[d + cb + j] / a.count) : 0.f;
+  }
+  float4 z[TQ], yv[TQ];
+  float mk[TQ];
+#pragma unroll
+  for (int i = 0; i < TQ; ++i) {
+    const int q = threadIdx.x + i * 256;
+    const int rr = q >> 4;
+    const int64_t t = t0 + rr - pad, c = c0 + c4;
+    const bool ok = rr < rows && t >= 0 && t < T && c < d;
+    mk[i] = ok ? 1.f : 0.f;
+    const int64_t off = (b * T + (ok ? t : 0)) * d + (ok ? c : 0);
+    z[i] = *reinterpret_cast<const float4*>(dz + off);
+    yv[i] = *reinterpret_cast<const float4*>(a.y + off);
+  }
+#pragma unroll
+  for (int i = 0; i < TQ; ++i) {
+    const float zz[4] = {z[i].x, z[i].y, z[i].z, z[i].w};
+    const float yy[4] = {yv[i].x, yv[i].y, yv[i].z, yv[i].w};
+    float o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float xh = (yy[j] - mu[j]) * rs[j];
+      const float dyb = zz[j] * dsiluf_(gm[j] * xh + bt[j]);
+      o[j] = gm[j] * rs[j] * (dyb - m1[j] - xh * m2[j]) * mk[i];
+    }
+    v[i] = make_float4(o[0], o[1], o[2], o[3]);
+  }
+}
+
 // Backward of the depthwise conv over one (TT frames x CT channels) tile of one utterance:
 //   dg[b,t,c] = sum_k w[c,k] * dy[b,t-k+pad,c]
 //   dw[c,k]  += sum_t dy[b,t,c] * g[b,t+k-pad,c],   db[c] += sum_t dy[b,t,c]
@@ -360,10 +414,11 @@ __global__ __launch_bounds__(256) void bn_silu_bwd_apply_kernel(const float* __r
 // both sums run from register sliding windows (one LDS read per 16..K FMAs); KC == 0 is the
 // runtime-K path.  Weight/bias sums land in part[(b*ntt + tile)][c*K + k | d*K + c] and are folded
 // by launch_colsum on the host side (no hot atomics).
-template <int KC>
+template <int KC, bool BN = false>
 __global__ __launch_bounds__(256) void dwconv_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ g,
                                                          const float* __restrict__ w, float* __restrict__ dg,
-                                                         float* __restrict__ part, int64_t T, int64_t d, int Krt) {
+                                                         float* __restrict__ part, int64_t T, int64_t d, int Krt,
+                                                         BnApply bn) {
   constexpr int KM = KC > 0 ? KC : KMAX;
   __shared__ __attribute__((aligned(16))) float tdy[(TT + KM - 1) * CT];  // frames t0-pad .. t0+TT-1+pad
   __shared__ __attribute__((aligned(16))) float tg[(TT + KM - 1) * CT];
@@ -385,8 +440,22 @@ __global__ __launch_bounds__(256) void dwconv_bwd_kernel(const float* __restrict
   float wv[KC > 0 ? KC : 1];
   {
     float4 v1[TQ], v2[TQ];
-    tile_load(v1, dy, b, t0, pad, rowsIn, T, d, c0);
+    if constexpr (BN) {
+      tile_load_bn(v1, dy, bn, b, t0, pad, rowsIn, T, d, c0);   // dy here is dz: the BN-SiLU input gradient
+    } else {
+      tile_load(v1, dy, b, t0, pad, rowsIn, T, d, c0);
+    }
     tile_load(v2, g, b, t0, pad, rowsIn, T, d, c0);
+    if (BN && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0) {
+      for (int64_t ch = threadIdx.x; ch < d; ch += 256) {   // the BatchNorm affine gradients (the reduction's totals)
+        bn.dgamma[ch] += (float)bn.red[d + ch];
+        bn.dbeta[ch] += (float)bn.red[ch];
+        if (bn.red_next) {
+          bn.red_next[ch] = 0.0;
+          bn.red_next[d + ch] = 0.0;
+        }
+      }
+    }
     if constexpr (KC > 0) taps_load<KC>(wv, w, c, d);
     tile_store(v1, tdy, rowsIn);
     tile_store(v2, tg, rowsIn);
@@ -570,15 +639,54 @@ int kdfm_dwconv_bwd(const float* dy, const float* g, const float* w, float* dg, 
   hipStream_t st = as_stream(stream);
   const int64_t ntt = ceil_div(T, TT);
   dim3 grid((unsigned)ntt, (unsigned)ceil_div(d, CT), (unsigned)B);
+  const BnApply none{};
   if (K == 31)
-    hipLaunchKernelGGL(dwconv_bwd_kernel<31>, grid, dim3(256), 0, st, dy, g, w, dg, ws, T, d, (int)K);
+    hipLaunchKernelGGL(dwconv_bwd_kernel<31>, grid, dim3(256), 0, st, dy, g, w, dg, ws, T, d, (int)K, none);
   else if (K == 15)
-    hipLaunchKernelGGL(dwconv_bwd_kernel<15>, grid, dim3(256), 0, st, dy, g, w, dg, ws, T, d, (int)K);
+    hipLaunchKernelGGL(dwconv_bwd_kernel<15>, grid, dim3(256), 0, st, dy, g, w, dg, ws, T, d, (int)K, none);
   else
-    hipLaunchKernelGGL(dwconv_bwd_kernel<0>, grid, dim3(256), 0, st, dy, g, w, dg, ws, T, d, (int)K);
+    hipLaunchKernelGGL(dwconv_bwd_kernel<0>, grid, dim3(256), 0, st, dy, g, w, dg, ws, T, d, (int)K, none);
   int rc = check_launch("kdfm_dwconv_bwd");
   if (rc || !dw) return rc;   // dw == db == NULL: the partials stay in ws for kdfm_dwconv_bwd_fold
   return kdfm_dwconv_bwd_fold(ws, dw, db, B, T, d, K, stream);
+}
+
+int kdfm_dwconv_bwd_bn(const float* dz, const float* y, const float* mean, const float* rstd, const float* gamma,
+                       const float* beta, const double* red, double* red_next, float* dgamma, float* dbeta,
+                       int32_t batch_stats, const float* g, const float* w, float* dg, float* ws, int64_t B,
+                       int64_t T, int64_t d, int64_t K, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(dz && y && mean && rstd && gamma && beta && red && dgamma && dbeta && g && w && dg && ws,
+               "null pointer");
+  KDFM_REQUIRE(K == 31 || K == 15, "BN-applied depthwise backward: kernel size 15 or 31");
+  KDFM_REQUIRE(d % 4 == 0 && ((((uintptr_t)g) | ((uintptr_t)dz) | ((uintptr_t)y)) & 15) == 0,
+               "channels must be a multiple of 4, inputs 16-B aligned");
+  KDFM_REQUIRE(red_next != red, "red_next must be another buffer");
+  if (B * T * d == 0) return KDFM_OK;
+  hipStream_t st = as_stream(stream);
+  const int64_t ntt = ceil_div(T, TT);
+  dim3 grid((unsigned)ntt, (unsigned)ceil_div(d, CT), (unsigned)B);
+  const BnApply bn{y, mean, rstd, gamma, beta, red, (double)(B * T), batch_stats, dgamma, dbeta, red_next};
+  if (K == 31)
+    hipLaunchKernelGGL((dwconv_bwd_kernel<31, true>), grid, dim3(256), 0, st, dz, g, w, dg, ws, T, d, (int)K, bn);
+  else
+    hipLaunchKernelGGL((dwconv_bwd_kernel<15, true>), grid, dim3(256), 0, st, dz, g, w, dg, ws, T, d, (int)K, bn);
+  return check_launch("kdfm_dwconv_bwd_bn");
+}
+
+int kdfm_bn_silu_bwd_reduce(const float* dz, const float* y, const float* mean, const float* rstd, const float* gamma,
+                            const float* beta, double* red, int64_t rows, int64_t d, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(dz && y && mean && rstd && gamma && beta && red, "null pointer");
+  if (rows * d == 0) return KDFM_OK;
+  int64_t gy = ceil_div(rows, 64);
+  if (gy > 1024) gy = 1024;
+  if (deterministic()) gy = 1;  // one workgroup per channel group: fixed summation order
+  const int64_t rp = ceil_div(rows, gy);
+  gy = ceil_div(rows, rp);
+  hipLaunchKernelGGL(bn_silu_bwd_reduce_kernel, dim3((unsigned)ceil_div(d, 64), (unsigned)gy), dim3(256), 0,
+                     as_stream(stream), dz, y, mean, rstd, gamma, beta, red, rows, d, rp);
+  return check_launch("kdfm_bn_silu_bwd_reduce");
 }
 
 int kdfm_dwconv_bwd_fold(const float* ws, float* dw, float* db, int64_t B, int64_t T, int64_t d, int64_t K,

@@ -172,6 +172,8 @@ SIGNATURES: dict[str, tuple] = {
     "kdfm_dwconv_fwd_bn": (_i32, [P, P, P, P, P, P, P, P, P, P, _i64, _i64, _i64, _i64, _f32, _f32, P]),
     "kdfm_dwconv_bwd": (_i32, [P, P, P, P, P, P, P, _i64, _i64, _i64, _i64, P]),
     "kdfm_dwconv_bwd_fold": (_i32, [P, P, P, _i64, _i64, _i64, _i64, P]),
+    "kdfm_dwconv_bwd_bn": (_i32, [P, P, P, P, P, P, P, P, P, P, _i32, P, P, P, P, _i64, _i64, _i64, _i64, P]),
+    "kdfm_bn_silu_bwd_reduce": (_i32, [P, P, P, P, P, P, P, _i64, _i64, P]),
     "kdfm_dwconv_bwd_ws": (_i64, [_i64, _i64, _i64, _i64]),
     "kdfm_bn_finalize": (_i32, [P, P, P, P, P, _i64, _i64, _f32, P]),
     "kdfm_bn_running_update": (_i32, [P, P, P, _i64, _i64, _f32, P]),

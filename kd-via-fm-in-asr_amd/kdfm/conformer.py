@@ -692,25 +692,36 @@ def layer_backward(cfg, S: EncoderShapes, P, G, L, li, ctx, dout, pos_emb, lengt
         WGRAD.run(lambda: K.linear_dw(dpw2, ctx["z"], G[L + "conv.pointwise_conv2.weight"].view(d, d), db=G[L + "conv.pointwise_conv2.bias"]), dpw2, ctx["z"])
         K.linear_dx(dpw2, P[L + "conv.pointwise_conv2.weight"].view(d, d), dz)
         del dpw2
-    dy = _empty(rows, d, dev=dev)
-    if bn_red is not None:
-        K.bn_silu_bwd(dz, ctx["y"], ctx["bmean"], ctx["brstd"], P[L + "conv.batch_norm.weight"],
-                      P[L + "conv.batch_norm.bias"], bn_red[0], dy, G[L + "conv.batch_norm.weight"],
-                      G[L + "conv.batch_norm.bias"], batch_stats=ctx["rm_batch"], red_next=bn_red[1], zeroed=True)
-    else:
-        red = torch.empty(2 * d, device=dev, dtype=torch.float64)
-        K.bn_silu_bwd(dz, ctx["y"], ctx["bmean"], ctx["brstd"], P[L + "conv.batch_norm.weight"],
-                      P[L + "conv.batch_norm.bias"], red, dy, G[L + "conv.batch_norm.weight"],
-                      G[L + "conv.batch_norm.bias"], batch_stats=ctx["rm_batch"])
-    del dz
     dg = _empty(rows, d, dev=dev)
     # the depthwise weight / bias gradient's fold of per-block partials runs on the weight-gradient stream
     dws = torch.empty(K.dwconv_bwd_ws(B, T, d, cfg.conv_kernel), device=dev)
-    K.dwconv_bwd(dy, ctx["g"], P[L + "conv.depthwise_conv.weight"].view(d, -1), dg, None, None, B, T, d,
-                 cfg.conv_kernel, ws=dws)
+    if bn_red is not None and cfg.conv_kernel in (15, 31):
+        # BN + SiLU backward: the sums, then their elementwise half applied on load by the depthwise backward
+        # (dy never stored); the sums' buffer comes from the ring, the launch zeroes the next one
+        Pbw, Pbb = P[L + "conv.batch_norm.weight"], P[L + "conv.batch_norm.bias"]
+        K.bn_silu_bwd_reduce(dz, ctx["y"], ctx["bmean"], ctx["brstd"], Pbw, Pbb, bn_red[0])
+        K.dwconv_bwd_bn(dz, ctx["y"], ctx["bmean"], ctx["brstd"], Pbw, Pbb, bn_red[0], bn_red[1],
+                        G[L + "conv.batch_norm.weight"], G[L + "conv.batch_norm.bias"], ctx["rm_batch"], ctx["g"],
+                        P[L + "conv.depthwise_conv.weight"].view(d, -1), dg, dws, B, T, d, cfg.conv_kernel)
+        del dz
+    else:
+        dy = _empty(rows, d, dev=dev)
+        if bn_red is not None:
+            K.bn_silu_bwd(dz, ctx["y"], ctx["bmean"], ctx["brstd"], P[L + "conv.batch_norm.weight"],
+                          P[L + "conv.batch_norm.bias"], bn_red[0], dy, G[L + "conv.batch_norm.weight"],
+                          G[L + "conv.batch_norm.bias"], batch_stats=ctx["rm_batch"], red_next=bn_red[1],
+                          zeroed=True)
+        else:
+            red = torch.empty(2 * d, device=dev, dtype=torch.float64)
+            K.bn_silu_bwd(dz, ctx["y"], ctx["bmean"], ctx["brstd"], P[L + "conv.batch_norm.weight"],
+                          P[L + "conv.batch_norm.bias"], red, dy, G[L + "conv.batch_norm.weight"],
+                          G[L + "conv.batch_norm.bias"], batch_stats=ctx["rm_batch"])
+        del dz
+        K.dwconv_bwd(dy, ctx["g"], P[L + "conv.depthwise_conv.weight"].view(d, -1), dg, None, None, B, T, d,
+                     cfg.conv_kernel, ws=dws)
+        del dy
     WGRAD.run(lambda: K.dwconv_bwd_fold(dws, G[L + "conv.depthwise_conv.weight"].view(d, -1),
                                         G[L + "conv.depthwise_conv.bias"], B, T, d, cfg.conv_kernel), dws)
-    del dy
     dx2 = _empty(rows, d, dev=dev)
     if ctx["ln3"] is None:   # fused LN + pointwise_conv1 + GLU forward: fused backward
         W1 = P[L + "conv.pointwise_conv1.weight"].view(2 * d, d)

@@ -1352,6 +1352,21 @@ def dwconv_bwd(dy, g, w, dg, dw, db, B, T, d, K, *, ws=None):
     call("kdfm_dwconv_bwd", ptr(dy), ptr(g), ptr(w), ptr(dg), ptr(dw), ptr(db), ptr(ws), B, T, d, K, _s())
 
 
+def dwconv_bwd_bn(dz, y, mean, rstd, gamma, beta, red, red_next, dgamma, dbeta, batch_stats, g, w, dg, ws, B, T, d,
+                  K):
+    """Depthwise backward with the BatchNorm(+SiLU) backward's elementwise half applied on load
+    (kdfm_dwconv_bwd_bn): dz = d loss / d silu(BN(y)), red = the bn_silu_bwd_reduce sums; leaves the weight
+    partials in ws (dwconv_bwd_fold) and adds the BN affine gradients."""
+    call("kdfm_dwconv_bwd_bn", ptr(dz), ptr(y), ptr(mean), ptr(rstd), ptr(gamma), ptr(beta), ptr(red), ptr(red_next),
+         ptr(dgamma), ptr(dbeta), int(batch_stats), ptr(g), ptr(w), ptr(dg), ptr(ws), B, T, d, K, _s())
+
+
+def bn_silu_bwd_reduce(dz, y, mean, rstd, gamma, beta, red):
+    rows, d = y.shape
+    call("kdfm_bn_silu_bwd_reduce", ptr(dz), ptr(y), ptr(mean), ptr(rstd), ptr(gamma), ptr(beta), ptr(red), rows, d,
+         _s())
+
+
 def dwconv_bwd_ws(B, T, d, K):
     return int(_lib.lib().kdfm_dwconv_bwd_ws(B, T, d, K))
 

@@ -126,3 +126,51 @@ def test_dwconv_fwd_bn_finalize(B, T, d, k, det):
             assert int(cnt.item()) == 0 and bool((stats == 0).all()), (call, cnt.item())
     finally:
         _lib.lib().kdfm_set_deterministic(0)
+
+
+@pytest.mark.parametrize("batch_stats", [True, False])
+@pytest.mark.parametrize("B,T,d,k", [(3, 401, 88, 31), (2, 70, 40, 15)])
+def test_dwconv_bwd_bn_equals_separate(B, T, d, k, batch_stats):
+    """kdfm_bn_silu_bwd_reduce + kdfm_dwconv_bwd_bn (the BN-SiLU backward's elementwise half applied on load)
+    equal kdfm_bn_silu_bwd + kdfm_dwconv_bwd bit for bit (same formula, same operation order): dg, the folded
+    depthwise weight / bias gradients and the BN affine gradients; red_next comes back zeroed."""
+    K = _K()
+    g = torch.Generator().manual_seed(B * T + d + k + 11)
+    dz = torch.randn(B * T, d, generator=g).cuda()
+    y = torch.randn(B * T, d, generator=g).cuda()
+    gin = torch.randn(B * T, d, generator=g).cuda()
+    w = torch.randn(d, k, generator=g).cuda()
+    mean = torch.randn(d, generator=g).cuda() * 0.1
+    rstd = torch.rand(d, generator=g).cuda() + 0.5
+    gm = torch.randn(d, generator=g).cuda()
+    bt = torch.randn(d, generator=g).cuda()
+    # reference: separate BN-SiLU backward (memset + reduce + apply) then the depthwise backward
+    red = torch.empty(2 * d, dtype=torch.float64, device="cuda")
+    dy = torch.empty(B * T, d, device="cuda")
+    dgm0, dbt0 = torch.zeros(d, device="cuda"), torch.zeros(d, device="cuda")
+    K.bn_silu_bwd(dz, y, mean, rstd, gm, bt, red, dy, dgm0, dbt0, batch_stats=batch_stats)
+    dg0 = torch.empty(B * T, d, device="cuda")
+    dw0, db0 = torch.zeros(d, k, device="cuda"), torch.zeros(d, device="cuda")
+    K.dwconv_bwd(dy, gin, w, dg0, dw0, db0, B, T, d, k)
+    # fused
+    red1 = torch.zeros(2 * d, dtype=torch.float64, device="cuda")
+    red_next = torch.full((2 * d,), 7.0, dtype=torch.float64, device="cuda")
+    dgm1, dbt1 = torch.zeros(d, device="cuda"), torch.zeros(d, device="cuda")
+    K.bn_silu_bwd_reduce(dz, y, mean, rstd, gm, bt, red1)
+    dg1 = torch.empty(B * T, d, device="cuda")
+    ws = torch.empty(K.dwconv_bwd_ws(B, T, d, k), device="cuda")
+    K.dwconv_bwd_bn(dz, y, mean, rstd, gm, bt, red1, red_next, dgm1, dbt1, batch_stats, gin, w, dg1, ws, B, T, d, k)
+    dw1, db1 = torch.zeros(d, k, device="cuda"), torch.zeros(d, device="cuda")
+    K.dwconv_bwd_fold(ws, dw1, db1, B, T, d, k)
+    torch.cuda.synchronize()
+    # the f64 sums are atomics (their order varies run to run): compare the affine grads to f32 rounding,
+    # and the rest exactly when the sums agree bit for bit
+    _close(dgm1, dgm0, rel=1e-6)
+    _close(dbt1, dbt0, rel=1e-6)
+    assert bool((red_next == 0).all())
+    if torch.equal(red, red1):
+        assert torch.equal(dg1, dg0) and torch.equal(dw1, dw0) and torch.equal(db1, db0)
+    else:
+        _close(dg1, dg0, rel=1e-5)
+        _close(dw1, dw0, rel=1e-5)
+        _close(db1, db0, rel=1e-5)
