@@ -94,6 +94,7 @@ SIGNATURES: dict[str, tuple] = {
     "kdfm_rowgemm_wprep": (_i32, [P, P, _i64, _i32, P]),
     "kdfm_rowgemm": (_i32, [P, P, P, _i64, _i64, _i32, _f32, _f32, C.c_uint64, P, P, P, P, P, _i32, P, P, _f32, _f32,
                             C.c_uint64, P, P]),
+    "kdfm_rowgemm_bnred": (_i32, [P, P, P, _i64, _i64, _f32, _f32, C.c_uint64, P, P, P, P, P, P, P, P, P]),
     "kdfm_lnproj_img_elems": (_i64, [_i32, _i64, _i32]),
     "kdfm_lnproj_wprep": (_i32, [_i32, P, P, _i64, _i32, P]),
     "kdfm_ln_qkv_fwd": (_i32, [P, P, P, _f32, P, P, P, P, P, P, P, P, P, P, _i64, _i64, P]),

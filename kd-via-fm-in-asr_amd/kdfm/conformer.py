@@ -675,11 +675,20 @@ def layer_backward(cfg, S: EncoderShapes, P, G, L, li, ctx, dout, pos_emb, lengt
                         li, SITE_FF2_ACT, SITE_FF2_OUT, dev, lng, pend)
     del dx4
     # conv module: x3 = x2 + drop(pw2(z))
+    bn_fused = bn_red is not None and cfg.conv_kernel in (15, 31) and not K.get_deterministic()
+    bn_summed = False
     dz = _empty(rows, d, dev=dev)
     if ctx.get("z_h") is not None:   # dropout prologue + data gradient on the row-streaming kernel
         dpw2_h = torch.empty(rows, d, device=dev, dtype=torch.bfloat16)
-        K.rowgemm(dx3, K.rowgemm_img(P[L + "conv.pointwise_conv2.weight"].view(d, d), trans=True), dz,
-                  pro=K.RG_PRO_DROP, p_in=pd, s_in=1.0, st_in=_stream(salt, li, SITE_CONV_OUT), x_h=dpw2_h, seed=seed)
+        img2 = K.rowgemm_img(P[L + "conv.pointwise_conv2.weight"].view(d, d), trans=True)
+        if bn_fused:   # + the BN-SiLU backward's sums in the epilogue (no reduce launch)
+            K.rowgemm_bnred(dx3, img2, dz, p_in=pd, s_in=1.0, st_in=_stream(salt, li, SITE_CONV_OUT), x_h=dpw2_h,
+                            seed=seed, bn=(ctx["y"], ctx["bmean"], ctx["brstd"], P[L + "conv.batch_norm.weight"],
+                                           P[L + "conv.batch_norm.bias"]), red=bn_red[0])
+            bn_summed = True
+        else:
+            K.rowgemm(dx3, img2, dz, pro=K.RG_PRO_DROP, p_in=pd, s_in=1.0, st_in=_stream(salt, li, SITE_CONV_OUT),
+                      x_h=dpw2_h, seed=seed)
         if _WGRAD_PAIRS:   # paired with linear_out's (same (d, d) shape) in the attention backward below
             pend["dd"] = (dpw2_h, ctx["z_h"], G[L + "conv.pointwise_conv2.weight"].view(d, d),
                           G[L + "conv.pointwise_conv2.bias"])
@@ -696,10 +705,12 @@ def layer_backward(cfg, S: EncoderShapes, P, G, L, li, ctx, dout, pos_emb, lengt
     # the depthwise weight / bias gradient's fold of per-block partials runs on the weight-gradient stream
     dws = torch.empty(K.dwconv_bwd_ws(B, T, d, cfg.conv_kernel), device=dev)
     if bn_red is not None and cfg.conv_kernel in (15, 31):
-        # BN + SiLU backward: the sums, then their elementwise half applied on load by the depthwise backward
-        # (dy never stored); the sums' buffer comes from the ring, the launch zeroes the next one
+        # BN + SiLU backward: the sums (in pointwise_conv2's data-gradient epilogue when it ran on the
+        # row-streaming kernel), then their elementwise half applied on load by the depthwise backward (dy never
+        # stored); the sums' buffer comes from the ring, the launch zeroes the next one
         Pbw, Pbb = P[L + "conv.batch_norm.weight"], P[L + "conv.batch_norm.bias"]
-        K.bn_silu_bwd_reduce(dz, ctx["y"], ctx["bmean"], ctx["brstd"], Pbw, Pbb, bn_red[0])
+        if not bn_summed:
+            K.bn_silu_bwd_reduce(dz, ctx["y"], ctx["bmean"], ctx["brstd"], Pbw, Pbb, bn_red[0])
         K.dwconv_bwd_bn(dz, ctx["y"], ctx["bmean"], ctx["brstd"], Pbw, Pbb, bn_red[0], bn_red[1],
                         G[L + "conv.batch_norm.weight"], G[L + "conv.batch_norm.bias"], ctx["rm_batch"], ctx["g"],
                         P[L + "conv.depthwise_conv.weight"].view(d, -1), dg, dws, B, T, d, cfg.conv_kernel)

@@ -815,6 +815,16 @@ def rowgemm(x, img, out, *, pro=0, p_in=0.0, s_in=1.0, st_in=0, bn=None, x_h=Non
          float(rscale), float(p_out), int(st_out), ptr(seed), _s())
 
 
+def rowgemm_bnred(x, img, out, *, p_in=0.0, s_in=1.0, st_in=0, x_h=None, seed=None, bn, red):
+    """out = (drop'(x)) Wop^T (rowgemm PRO_DROP) with the BN-SiLU backward's sums red (2d f64, zero on entry)
+    accumulated in the epilogue (kdfm_rowgemm_bnred); bn = (y, mean, rstd, gamma, beta)."""
+    rows, d = x.shape
+    assert out.shape == (rows, d) and x.is_contiguous() and out.is_contiguous() and red.dtype == torch.float64
+    y, bm, br, bg, bb = bn
+    call("kdfm_rowgemm_bnred", ptr(_f32(x)), ptr(_bf16(img)), ptr(out), rows, d, float(p_in), float(s_in), int(st_in),
+         ptr(_bf16(x_h)), ptr(seed), ptr(_f32(y)), ptr(bm), ptr(br), ptr(bg), ptr(bb), ptr(red), _s())
+
+
 LNPROJ_QKV, LNPROJ_GLU = 0, 1
 IMG_FFN, IMG_LNPROJ, IMG_ROWGEMM = 0, 1, 2
 
