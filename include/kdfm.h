@@ -314,12 +314,6 @@ int kdfm_rowgemm(const float* x, const uint16_t* img, float* out, int64_t rows, 
                  const float* bn_g, const float* bn_b, uint16_t* x_h, int32_t epilogue, const float* bias,
                  const float* R, float rscale, float p_out, uint64_t stream_out, const uint64_t* seed,
                  void* stream);
-/* The pointwise_conv2 data gradient dz = drop'(x) W (prologue PRO_DROP) with the BatchNorm + SiLU backward's
- * sums in its epilogue: red (2d doubles, zero on entry) += (sum_r dz silu'(g xh + b), sum_r (same) xh),
- * xh = (y - mean) rstd -- kdfm_bn_silu_bwd_reduce fused (float atomics: not the deterministic mode's). */
-int kdfm_rowgemm_bnred(const float* x, const uint16_t* img, float* out, int64_t rows, int64_t d, float p_in, float s_in,
-                       uint64_t stream_in, uint16_t* x_h, const uint64_t* seed, const float* y, const float* mean,
-                       const float* rstd, const float* gamma, const float* beta, double* red, void* stream);
 int kdfm_lnproj_wprep(int32_t kind, const float* W, uint16_t* img, int64_t d, int32_t bwd, void* stream);
 int kdfm_ln_qkv_fwd(const float* x, const float* ln_g, const float* ln_b, float ln_eps, const uint16_t* img,
                     const float* bias, const float* pos_u, const float* pos_v, float* qu, float* qv, float* qkv,
@@ -659,14 +653,6 @@ int kdfm_glu_mask_bwd(const float* dg, const float* a, const int64_t* lengths, f
                       int64_t d, void* stream);
 int kdfm_dwconv_fwd(const float* g, const float* w, const float* bias, float* y, double* stats, int64_t B, int64_t T,
                     int64_t d, int64_t K, void* stream);
-/* kdfm_dwconv_fwd with the training BatchNorm finalize in the same launch: the last workgroup to add its
- * batch sums into stats (zero on entry; 2d doubles) forms mean / rstd (d floats each), updates the running
- * statistics with `momentum` (unbiased variance), and resets stats and *counter (a device uint32, zero on
- * entry) to zero for the next call -- kdfm_bn_finalize_running without its launch.  Deterministic mode:
- * the ordered statistics kernel and the finalize as separate launches, same results contract. */
-int kdfm_dwconv_fwd_bn(const float* g, const float* w, const float* bias, float* y, double* stats, uint32_t* counter,
-                       float* running_mean, float* running_var, float* mean, float* rstd, int64_t B, int64_t T,
-                       int64_t d, int64_t K, float eps, float momentum, void* stream);
 /* dg = conv^T(dy); dw, db accumulate (+=) */
 /* dw/db accumulated (+=) through per-block partials in ws (>= kdfm_dwconv_bwd_ws(B, T, d, K) floats);
  * dw == db == NULL: only dg, the partials are left in ws for kdfm_dwconv_bwd_fold (which may run on

@@ -89,23 +89,13 @@ __device__ __forceinline__ void tile_store(const float4 (&v)[TQ], float* tile, i
   }
 }
 
-// The training BatchNorm finalize riding on the statistics launch (kdfm_dwconv_fwd_bn): the last workgroup to
-// add its sums (a device-scope counter) forms the batch mean / rstd, updates the running statistics, re-zeroes
-// the sums and the counter -- the bn_finalize_running launch per layer disappears.
-struct BnFin {
-  unsigned* counter;   // NULL: no finalize
-  float* rm; float* rv; float* mean; float* rstd;
-  double count; float eps, momentum;
-};
-
 // y[b,t,c] = bias[c] + sum_k w[c,k] * g[b,t+k-pad,c]; stats[c] += (sum y, sum y^2)
 // Lane = channel, wave = 16-frame group; with KC > 0 a 16-frame register window slides over the
 // tile (one LDS read per 16 FMAs) with the taps in registers.
 template <int KC>
 __global__ __launch_bounds__(256) void dwconv_fwd_kernel(const float* __restrict__ g, const float* __restrict__ w,
                                                          const float* __restrict__ bias, float* __restrict__ y,
-                                                         double* stats, int64_t T, int64_t d, int Krt,
-                                                         BnFin fin) {
+                                                         double* __restrict__ stats, int64_t T, int64_t d, int Krt) {
   constexpr int KM = KC > 0 ? KC : KMAX;
   __shared__ __attribute__((aligned(16))) float tile[(TT + KM - 1) * CT];
   __shared__ double red[2][4][CT];
@@ -173,32 +163,6 @@ __global__ __launch_bounds__(256) void dwconv_fwd_kernel(const float* __restrict
     atomicAdd(stats + c0 + q, red[0][0][q] + red[0][1][q] + red[0][2][q] + red[0][3][q]);
     atomicAdd(stats + d + c0 + q, red[1][0][q] + red[1][1][q] + red[1][2][q] + red[1][3][q]);
   }
-  if (!fin.counter) return;
-  __shared__ unsigned last;
-  __threadfence();   // this workgroup's sums are visible device-wide before it counts itself in
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned nblk = gridDim.x * gridDim.y * gridDim.z;
-    last = (__hip_atomic_fetch_add(fin.counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == nblk - 1) ? 1u : 0u;
-  }
-  __syncthreads();
-  if (!last) return;
-  __threadfence();
-  for (int64_t ch = threadIdx.x; ch < d; ch += 256) {
-    const double s1 = __hip_atomic_load(stats + ch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const double s2 = __hip_atomic_load(stats + d + ch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    stats[ch] = 0.0;   // reset for the next layer's accumulation
-    stats[d + ch] = 0.0;
-    const double m = s1 / fin.count;
-    double var = s2 / fin.count - m * m;
-    if (var < 0.0) var = 0.0;
-    fin.mean[ch] = (float)m;
-    fin.rstd[ch] = (float)(1.0 / sqrt(var + (double)fin.eps));
-    const double unb = fin.count > 1.0 ? var * fin.count / (fin.count - 1.0) : var;
-    fin.rm[ch] = (float)((1.0 - fin.momentum) * fin.rm[ch] + fin.momentum * m);
-    fin.rv[ch] = (float)((1.0 - fin.momentum) * fin.rv[ch] + fin.momentum * unb);
-  }
-  if (threadIdx.x == 0) __hip_atomic_store(fin.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Deterministic-mode BatchNorm statistics: stats[c] += sum_r y[r,c], stats[d+c] += sum_r y[r,c]^2 with
@@ -549,31 +513,6 @@ __global__ __launch_bounds__(256) void dwconv_bwd_kernel(const float* __restrict
 }  // namespace
 }  // namespace kdfm
 
-namespace kdfm {
-namespace {
-int dwconv_fwd_run(const float* g, const float* w, const float* bias, float* y, double* stats, const BnFin& fin,
-                   int64_t B, int64_t T, int64_t d, int64_t K, hipStream_t st) {
-  dim3 grid((unsigned)ceil_div(T, TT), (unsigned)ceil_div(d, CT), (unsigned)B);
-  double* st_fused = deterministic() ? nullptr : stats;
-  BnFin f = fin;
-  if (!st_fused) f.counter = nullptr;   // deterministic statistics: ordered kernel, then the finalize launch
-  if (K == 31)
-    hipLaunchKernelGGL(dwconv_fwd_kernel<31>, grid, dim3(256), 0, st, g, w, bias, y, st_fused, T, d, (int)K, f);
-  else if (K == 15)
-    hipLaunchKernelGGL(dwconv_fwd_kernel<15>, grid, dim3(256), 0, st, g, w, bias, y, st_fused, T, d, (int)K, f);
-  else
-    hipLaunchKernelGGL(dwconv_fwd_kernel<0>, grid, dim3(256), 0, st, g, w, bias, y, st_fused, T, d, (int)K, f);
-  int rc = check_launch("kdfm_dwconv_fwd");
-  if (rc || !stats || st_fused) return rc;
-  hipLaunchKernelGGL(bn_stats_det_kernel, dim3((unsigned)ceil_div(d, 64)), dim3(256), 0, st, y, stats, B * T, d);
-  rc = check_launch("kdfm_dwconv_fwd(det stats)");
-  if (rc || !fin.counter) return rc;
-  hipLaunchKernelGGL(bn_finalize_running_kernel, dim3((unsigned)ceil_div(d, 256)), dim3(256), 0, st, stats, fin.rm,
-                     fin.rv, fin.mean, fin.rstd, d, fin.count, fin.eps, fin.momentum);
-  return check_launch("kdfm_dwconv_fwd_bn(finalize)");
-}
-}  // namespace
-}  // namespace kdfm
 
 extern "C" {
 
@@ -607,19 +546,19 @@ int kdfm_dwconv_fwd(const float* g, const float* w, const float* bias, float* y,
   KDFM_REQUIRE(K >= 1 && K <= KMAX && (K % 2) == 1, "kernel size must be odd and <= 63");
   KDFM_REQUIRE(d % 4 == 0 && (((uintptr_t)g) & 15) == 0, "channels must be a multiple of 4, input 16-B aligned");
   if (B * T * d == 0) return KDFM_OK;
-  return dwconv_fwd_run(g, w, bias, y, stats, BnFin{}, B, T, d, K, as_stream(stream));
-}
-
-int kdfm_dwconv_fwd_bn(const float* g, const float* w, const float* bias, float* y, double* stats, uint32_t* counter,
-                       float* running_mean, float* running_var, float* mean, float* rstd, int64_t B, int64_t T,
-                       int64_t d, int64_t K, float eps, float momentum, void* stream) {
-  using namespace kdfm;
-  KDFM_REQUIRE(g && w && y && stats && counter && running_mean && running_var && mean && rstd, "null pointer");
-  KDFM_REQUIRE(K >= 1 && K <= KMAX && (K % 2) == 1, "kernel size must be odd and <= 63");
-  KDFM_REQUIRE(d % 4 == 0 && (((uintptr_t)g) & 15) == 0, "channels must be a multiple of 4, input 16-B aligned");
-  KDFM_REQUIRE(B * T > 0 && d > 0, "empty batch");
-  const BnFin fin{counter, running_mean, running_var, mean, rstd, (double)(B * T), eps, momentum};
-  return dwconv_fwd_run(g, w, bias, y, stats, fin, B, T, d, K, as_stream(stream));
+  dim3 grid((unsigned)ceil_div(T, TT), (unsigned)ceil_div(d, CT), (unsigned)B);
+  double* st_fused = deterministic() ? nullptr : stats;
+  if (K == 31)
+    hipLaunchKernelGGL(dwconv_fwd_kernel<31>, grid, dim3(256), 0, as_stream(stream), g, w, bias, y, st_fused, T, d, (int)K);
+  else if (K == 15)
+    hipLaunchKernelGGL(dwconv_fwd_kernel<15>, grid, dim3(256), 0, as_stream(stream), g, w, bias, y, st_fused, T, d, (int)K);
+  else
+    hipLaunchKernelGGL(dwconv_fwd_kernel<0>, grid, dim3(256), 0, as_stream(stream), g, w, bias, y, st_fused, T, d, (int)K);
+  int rc = check_launch("kdfm_dwconv_fwd");
+  if (rc || !stats || st_fused) return rc;
+  hipLaunchKernelGGL(bn_stats_det_kernel, dim3((unsigned)ceil_div(d, 64)), dim3(256), 0, as_stream(stream), y, stats,
+                     B * T, d);
+  return check_launch("kdfm_dwconv_fwd(det stats)");
 }
 
 int64_t kdfm_dwconv_bwd_ws(int64_t B, int64_t T, int64_t d, int64_t K) {

@@ -22,7 +22,7 @@ using namespace lnb;
 constexpr int RG_NT = 128;      // 2 waves = 64 rows per workgroup
 constexpr int RG_ROWS = 64;
 enum { PRO_NONE = 0, PRO_DROP = 1, PRO_BNSILU = 2 };
-enum { EPI_NONE = 0, EPI_RESID = 1, EPI_BNRED = 2 };
+enum { EPI_NONE = 0, EPI_RESID = 1 };
 
 // image: fragment (mt, ks), lane (r, h), j: Wop[32 mt + r][16 ks + 8 h + j] with Wop = W (forward,
 // W (d, d) as [out][in]) or W^T (data gradient: Wop[o][i] = W[i][o])
@@ -45,10 +45,6 @@ struct RgArgs {
   uint16_t* x_h;                                                     // bf16 copy of the prologue output
   // epilogue
   const float* bias; const float* R; float rscale, p_out; uint64_t st_out;
-  // EPI_BNRED (the pointwise_conv2 data gradient dz): the BatchNorm + SiLU backward's sums over rows,
-  // red[n] += sum dz silu'(g xh + b), red[d + n] += sum (same) xh, xh = (y - mean) rstd, with the BN
-  // statistics in bn_mean / bn_rstd / bn_g / bn_b -- kdfm_bn_silu_bwd_reduce without its launch
-  const float* bn_y; double* bn_red;
 };
 
 template <int KS1, int DT, int PRO, int EPI>
@@ -119,34 +115,6 @@ __global__ __launch_bounds__(RG_NT) void rowgemm_kernel(RgArgs a) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int n0 = 32 * mt + 8 * q + 4 * h;
-      if constexpr (EPI == EPI_BNRED) {
-        // every lane takes part in the half-wave sums (rows / columns past the end contribute zero)
-        const bool vok = ok && n0 < d;
-        const int nn = n0 < d ? n0 : 0;
-        const float4 yv = *reinterpret_cast<const float4*>(a.bn_y + (vok ? row * d + nn : 0));
-        const float4 mu = *reinterpret_cast<const float4*>(a.bn_mean + nn);
-        const float4 rs = *reinterpret_cast<const float4*>(a.bn_rstd + nn);
-        const float4 gg = *reinterpret_cast<const float4*>(a.bn_g + nn);
-        const float4 bb = *reinterpret_cast<const float4*>(a.bn_b + nn);
-        const float yy[4] = {yv.x, yv.y, yv.z, yv.w}, mm[4] = {mu.x, mu.y, mu.z, mu.w};
-        const float rr[4] = {rs.x, rs.y, rs.z, rs.w}, g4[4] = {gg.x, gg.y, gg.z, gg.w}, b4[4] = {bb.x, bb.y, bb.z, bb.w};
-        const float vm = vok ? 1.f : 0.f;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float xh = (yy[i] - mm[i]) * rr[i];
-          const float dyb = acc[4 * q + i] * dsiluf_(g4[i] * xh + b4[i]) * vm;
-          float c1 = dyb, c2 = dyb * xh;
-#pragma unroll
-          for (int o = 1; o < 32; o <<= 1) {
-            c1 += __shfl_xor(c1, o, 64);
-            c2 += __shfl_xor(c2, o, 64);
-          }
-          if ((lane & 31) == 0 && n0 < d) {
-            atomicAdd(a.bn_red + n0 + i, (double)c1);
-            atomicAdd(a.bn_red + d + n0 + i, (double)c2);
-          }
-        }
-      }
       if (!ok || n0 >= d) continue;
       float o[4] = {acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]};
       if constexpr (EPI == EPI_RESID) {
@@ -182,7 +150,6 @@ int rg_launch(int pro, int epi, const RgArgs& a, hipStream_t st) {
   RG_CASE(PRO_NONE, EPI_RESID)
   RG_CASE(PRO_BNSILU, EPI_RESID)
   RG_CASE(PRO_DROP, EPI_NONE)
-  RG_CASE(PRO_DROP, EPI_BNRED)
   RG_CASE(PRO_NONE, EPI_NONE)
 #undef RG_CASE
   set_error("kdfm_rowgemm: unsupported prologue / epilogue combination");
@@ -229,33 +196,12 @@ int kdfm_rowgemm(const float* x, const uint16_t* img, float* out, int64_t rows, 
   KDFM_REQUIRE(p_in >= 0.f && p_in < 1.f && p_out >= 0.f && p_out < 1.f, "dropout p");
   KDFM_REQUIRE((p_in == 0.f && p_out == 0.f) || seed, "dropout needs a seed");
   if (rows <= 0) return KDFM_OK;
-  KDFM_REQUIRE(epilogue != EPI_BNRED, "the BN-sums epilogue is kdfm_rowgemm_bnred");
   RgArgs a{x, img, out, rows, (int)d, p_in, s_in, seed, stream_in, bn_mean, bn_rstd, bn_g, bn_b, x_h,
-           bias, R, rscale, p_out, stream_out, nullptr, nullptr};
+           bias, R, rscale, p_out, stream_out};
   hipStream_t st = as_stream(stream);
   if (KS1 == 6) return rg_launch<6, 3>(prologue, epilogue, a, st);
   if (KS1 == 11) return rg_launch<11, 6>(prologue, epilogue, a, st);
   return rg_launch<12, 6>(prologue, epilogue, a, st);
-}
-
-int kdfm_rowgemm_bnred(const float* x, const uint16_t* img, float* out, int64_t rows, int64_t d, float p_in, float s_in,
-                       uint64_t stream_in, uint16_t* x_h, const uint64_t* seed, const float* y, const float* mean,
-                       const float* rstd, const float* gamma, const float* beta, double* red, void* stream) {
-  using namespace kdfm;
-  using namespace kdfm::lnb;
-  KDFM_REQUIRE(x && img && out && y && mean && rstd && gamma && beta && red, "null pointer");
-  int KS1, DT;
-  KDFM_REQUIRE(ln_dims(d, KS1, DT) == 0, "unsupported d");
-  KDFM_REQUIRE(al16(x) && al16(img) && al16(out) && al16(x_h) && al16(y) && al16(mean) && al16(rstd) && al16(gamma) &&
-                   al16(beta), "operands must be 16-byte aligned");
-  KDFM_REQUIRE(p_in >= 0.f && p_in < 1.f && (p_in == 0.f || seed), "dropout p / seed");
-  if (rows <= 0) return KDFM_OK;
-  RgArgs a{x, img, out, rows, (int)d, p_in, s_in, seed, stream_in, mean, rstd, gamma, beta, x_h,
-           nullptr, nullptr, 1.f, 0.f, 0, y, red};
-  hipStream_t st = as_stream(stream);
-  if (KS1 == 6) return rg_launch<6, 3>(PRO_DROP, EPI_BNRED, a, st);
-  if (KS1 == 11) return rg_launch<11, 6>(PRO_DROP, EPI_BNRED, a, st);
-  return rg_launch<12, 6>(PRO_DROP, EPI_BNRED, a, st);
 }
 
 }  // extern "C"

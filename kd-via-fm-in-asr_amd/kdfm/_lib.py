@@ -94,7 +94,6 @@ SIGNATURES: dict[str, tuple] = {
     "kdfm_rowgemm_wprep": (_i32, [P, P, _i64, _i32, P]),
     "kdfm_rowgemm": (_i32, [P, P, P, _i64, _i64, _i32, _f32, _f32, C.c_uint64, P, P, P, P, P, _i32, P, P, _f32, _f32,
                             C.c_uint64, P, P]),
-    "kdfm_rowgemm_bnred": (_i32, [P, P, P, _i64, _i64, _f32, _f32, C.c_uint64, P, P, P, P, P, P, P, P, P]),
     "kdfm_lnproj_img_elems": (_i64, [_i32, _i64, _i32]),
     "kdfm_lnproj_wprep": (_i32, [_i32, P, P, _i64, _i32, P]),
     "kdfm_ln_qkv_fwd": (_i32, [P, P, P, _f32, P, P, P, P, P, P, P, P, P, P, _i64, _i64, P]),
@@ -170,7 +169,6 @@ SIGNATURES: dict[str, tuple] = {
     "kdfm_glu_mask_fwd": (_i32, [P, P, P, _i64, _i64, _i64, P]),
     "kdfm_glu_mask_bwd": (_i32, [P, P, P, P, _i64, _i64, _i64, P]),
     "kdfm_dwconv_fwd": (_i32, [P, P, P, P, P, _i64, _i64, _i64, _i64, P]),
-    "kdfm_dwconv_fwd_bn": (_i32, [P, P, P, P, P, P, P, P, P, P, _i64, _i64, _i64, _i64, _f32, _f32, P]),
     "kdfm_dwconv_bwd": (_i32, [P, P, P, P, P, P, P, _i64, _i64, _i64, _i64, P]),
     "kdfm_dwconv_bwd_fold": (_i32, [P, P, P, _i64, _i64, _i64, _i64, P]),
     "kdfm_dwconv_bwd_bn": (_i32, [P, P, P, P, P, P, P, P, P, P, _i32, P, P, P, P, _i64, _i64, _i64, _i64, P]),

@@ -112,7 +112,7 @@ def _out_linear_backward(S, P, G, pre, ctx, dx, y, *, seed, salt, ws):
         K.linear_dw(dlin, yv, Gout.view(d, S.F2 * C))
         K.convw_grad(Gout, G[pre + "pre_encode.out.weight"].view(d, C, S.F2))
         K.colsum(dlin, G[pre + "pre_encode.out.bias"])
-    WGRAD.run(out_wgrad, dlin, yv)
+    _side(out_wgrad, dlin, yv)
     g = _empty(y.shape[0], C, dev=dx.device)
     K.linear_dx(dlin, ws["wout_perm"].view(d, S.F2 * C), g.view(S.rows, S.F2 * C), epi=_lib.EPI_DRELU,
                 aux=y.view(S.rows, S.F2 * C))
@@ -182,6 +182,21 @@ def dw_subsampling_backward(cfg, S: EncoderShapes, P, G, pre, ctx, dx, *, seed, 
 # KDFM_SS_ONE_KERNEL=0: the two-kernel striding forward (conv1 to HBM, implicit-GEMM conv2) instead of the
 # one-kernel form
 _SS_ONE_KERNEL = __import__("os").environ.get("KDFM_SS_ONE_KERNEL", "1") == "1"
+# KDFM_SIDE_FOLDS=1: the LayerNorm / depthwise folds and the subsampling output's weight gradient go to the
+# weight-gradient stream (=0, default: they stay on the compute stream -- measured 2111 / 2116 vs 2074 / 2095
+# utt/s, profiles/r04/r4v: the extra launches there delay the compute stream's dispatch more than they save)
+_SIDE_FOLDS = __import__("os").environ.get("KDFM_SIDE_FOLDS", "0") == "1"
+
+
+def _side(fn, *keep):
+    if _SIDE_FOLDS:
+        WGRAD.run(fn, *keep)
+    else:
+        fn()
+
+
+# KDFM_BN_ON_LOAD=0: the BN-SiLU backward's elementwise half as its own launch (A/B switch)
+_BN_ON_LOAD = __import__("os").environ.get("KDFM_BN_ON_LOAD", "1") == "1"
 
 
 def subsampling_forward(cfg, S: EncoderShapes, P, pre, mel, mel_len, len1, len2, *, train, seed, salt, save, ws):
@@ -397,10 +412,9 @@ def layer_forward(cfg, S: EncoderShapes, P, L, li, x, out, pos_emb, lengths, *, 
                   bn_update=None, rm_batch=True, ppos=None, bn_stats=None):
     """x (rows, d) -> out (rows, d) (written in place).  Returns ctx for backward when save.
     ppos: this layer's projected positions linear_pos(pos_emb) (npos, d) when the caller computed
-    every layer's at once (pos_proj_all); otherwise projected here.  bn_stats: (sums (2d,) f64, counter (1,)
-    int32), both zero: the training BatchNorm finalize then rides on the depthwise-conv launch
-    (kdfm_dwconv_fwd_bn), which leaves them zero again -- the encoder's layers share one pair, no memset
-    or finalize launch per layer."""
+    every layer's at once (pos_proj_all); otherwise projected here.  bn_stats: a zeroed (2d,) f64 buffer
+    the BatchNorm batch sums may accumulate into when the training finalize runs (it leaves the buffer
+    zeroed again, so the encoder's layers reuse one buffer without a memset per layer)."""
     dev = x.device
     rows, d, H, dk, T, B, ff = S.rows, S.d, S.h, S.dk, S.T, S.B, S.ff
     pd = cfg.dropout if train else 0.0
@@ -511,20 +525,14 @@ def layer_forward(cfg, S: EncoderShapes, P, L, li, x, out, pos_emb, lengths, *, 
     bmean = _empty(d, dev=dev)
     brstd = _empty(d, dev=dev)
     rmn, rvr = bn_update if bn_update is not None else (None, None)
-    stats = None
     if fin_running and bn_stats is not None:
-        with K.span("dwconv", nbytes=4.0 * 2 * rows * d):   # read g + write y (f32), SURVEY.md §8(d)
-            K.dwconv_fwd_bn(g, P[L + "conv.depthwise_conv.weight"].view(d, -1), P[L + "conv.depthwise_conv.bias"], y,
-                            bn_stats[0], bn_stats[1], rmn, rvr, bmean, brstd, B, T, d, cfg.conv_kernel, cfg.bn_eps,
-                            cfg.bn_momentum)
+        stats = bn_stats   # zero on entry; kdfm_bn_finalize_running re-zeroes it after reading
     else:
         stats = torch.zeros(2 * d, device=dev, dtype=torch.float64) if rm_batch else None
-        with K.span("dwconv", nbytes=4.0 * 2 * rows * d):
-            K.dwconv_fwd(g, P[L + "conv.depthwise_conv.weight"].view(d, -1), P[L + "conv.depthwise_conv.bias"], y,
-                         stats, B, T, d, cfg.conv_kernel)
-    if stats is None and fin_running and bn_stats is not None:
-        pass   # finalized in the depthwise-conv launch
-    elif stats is not None and rm_batch and bn_update is not None and train:
+    with K.span("dwconv", nbytes=4.0 * 2 * rows * d):   # read g + write y (f32), SURVEY.md §8(d)
+        K.dwconv_fwd(g, P[L + "conv.depthwise_conv.weight"].view(d, -1), P[L + "conv.depthwise_conv.bias"], y,
+                     stats, B, T, d, cfg.conv_kernel)
+    if stats is not None and rm_batch and bn_update is not None and train:
         # batch statistics and the running-statistics update in one launch
         K.bn_finalize_running(stats, rmn, rvr, bmean, brstd, d, rows, cfg.bn_eps, cfg.bn_momentum)
     else:
@@ -588,7 +596,7 @@ class LnGrads:
         reused by the next layer before the join -- encoder_backward gives every layer its own."""
         if self.pending:
             pend, rows, d = self.pending, self.rows, self.d
-            WGRAD.run(lambda: K.ln_fold(pend, rows, d), self.buf)
+            _side(lambda: K.ln_fold(pend, rows, d), self.buf)
             self.pending = []
 
 
@@ -675,20 +683,11 @@ def layer_backward(cfg, S: EncoderShapes, P, G, L, li, ctx, dout, pos_emb, lengt
                         li, SITE_FF2_ACT, SITE_FF2_OUT, dev, lng, pend)
     del dx4
     # conv module: x3 = x2 + drop(pw2(z))
-    bn_fused = bn_red is not None and cfg.conv_kernel in (15, 31) and not K.get_deterministic()
-    bn_summed = False
     dz = _empty(rows, d, dev=dev)
     if ctx.get("z_h") is not None:   # dropout prologue + data gradient on the row-streaming kernel
         dpw2_h = torch.empty(rows, d, device=dev, dtype=torch.bfloat16)
-        img2 = K.rowgemm_img(P[L + "conv.pointwise_conv2.weight"].view(d, d), trans=True)
-        if bn_fused:   # + the BN-SiLU backward's sums in the epilogue (no reduce launch)
-            K.rowgemm_bnred(dx3, img2, dz, p_in=pd, s_in=1.0, st_in=_stream(salt, li, SITE_CONV_OUT), x_h=dpw2_h,
-                            seed=seed, bn=(ctx["y"], ctx["bmean"], ctx["brstd"], P[L + "conv.batch_norm.weight"],
-                                           P[L + "conv.batch_norm.bias"]), red=bn_red[0])
-            bn_summed = True
-        else:
-            K.rowgemm(dx3, img2, dz, pro=K.RG_PRO_DROP, p_in=pd, s_in=1.0, st_in=_stream(salt, li, SITE_CONV_OUT),
-                      x_h=dpw2_h, seed=seed)
+        K.rowgemm(dx3, K.rowgemm_img(P[L + "conv.pointwise_conv2.weight"].view(d, d), trans=True), dz,
+                  pro=K.RG_PRO_DROP, p_in=pd, s_in=1.0, st_in=_stream(salt, li, SITE_CONV_OUT), x_h=dpw2_h, seed=seed)
         if _WGRAD_PAIRS:   # paired with linear_out's (same (d, d) shape) in the attention backward below
             pend["dd"] = (dpw2_h, ctx["z_h"], G[L + "conv.pointwise_conv2.weight"].view(d, d),
                           G[L + "conv.pointwise_conv2.bias"])
@@ -704,13 +703,11 @@ def layer_backward(cfg, S: EncoderShapes, P, G, L, li, ctx, dout, pos_emb, lengt
     dg = _empty(rows, d, dev=dev)
     # the depthwise weight / bias gradient's fold of per-block partials runs on the weight-gradient stream
     dws = torch.empty(K.dwconv_bwd_ws(B, T, d, cfg.conv_kernel), device=dev)
-    if bn_red is not None and cfg.conv_kernel in (15, 31):
-        # BN + SiLU backward: the sums (in pointwise_conv2's data-gradient epilogue when it ran on the
-        # row-streaming kernel), then their elementwise half applied on load by the depthwise backward (dy never
-        # stored); the sums' buffer comes from the ring, the launch zeroes the next one
+    if _BN_ON_LOAD and bn_red is not None and cfg.conv_kernel in (15, 31):
+        # BN + SiLU backward: the sums, then their elementwise half applied on load by the depthwise backward
+        # (dy never stored); the sums' buffer comes from the ring, the launch zeroes the next one
         Pbw, Pbb = P[L + "conv.batch_norm.weight"], P[L + "conv.batch_norm.bias"]
-        if not bn_summed:
-            K.bn_silu_bwd_reduce(dz, ctx["y"], ctx["bmean"], ctx["brstd"], Pbw, Pbb, bn_red[0])
+        K.bn_silu_bwd_reduce(dz, ctx["y"], ctx["bmean"], ctx["brstd"], Pbw, Pbb, bn_red[0])
         K.dwconv_bwd_bn(dz, ctx["y"], ctx["bmean"], ctx["brstd"], Pbw, Pbb, bn_red[0], bn_red[1],
                         G[L + "conv.batch_norm.weight"], G[L + "conv.batch_norm.bias"], ctx["rm_batch"], ctx["g"],
                         P[L + "conv.depthwise_conv.weight"].view(d, -1), dg, dws, B, T, d, cfg.conv_kernel)
@@ -731,8 +728,8 @@ def layer_backward(cfg, S: EncoderShapes, P, G, L, li, ctx, dout, pos_emb, lengt
         K.dwconv_bwd(dy, ctx["g"], P[L + "conv.depthwise_conv.weight"].view(d, -1), dg, None, None, B, T, d,
                      cfg.conv_kernel, ws=dws)
         del dy
-    WGRAD.run(lambda: K.dwconv_bwd_fold(dws, G[L + "conv.depthwise_conv.weight"].view(d, -1),
-                                        G[L + "conv.depthwise_conv.bias"], B, T, d, cfg.conv_kernel), dws)
+    _side(lambda: K.dwconv_bwd_fold(dws, G[L + "conv.depthwise_conv.weight"].view(d, -1),
+                                    G[L + "conv.depthwise_conv.bias"], B, T, d, cfg.conv_kernel), dws)
     dx2 = _empty(rows, d, dev=dev)
     if ctx["ln3"] is None:   # fused LN + pointwise_conv1 + GLU forward: fused backward
         W1 = P[L + "conv.pointwise_conv1.weight"].view(2 * d, d)
@@ -958,8 +955,7 @@ def encoder_forward_steps(cfg, S: EncoderShapes, P, prefix, mel, mel_len, len1, 
     if train and bn_running is not None and use_batch_stats:
         bn_stats = ws.get("bn_stats")
         if bn_stats is None:
-            bn_stats = ws["bn_stats"] = (torch.zeros(2 * S.d, device=mel.device, dtype=torch.float64),
-                                         torch.zeros(1, device=mel.device, dtype=torch.int32))
+            bn_stats = ws["bn_stats"] = torch.zeros(2 * S.d, device=mel.device, dtype=torch.float64)
     for i in range(cfg.n_layers):
         L = f"{prefix}layers.{i}."
         bn = None

@@ -815,16 +815,6 @@ def rowgemm(x, img, out, *, pro=0, p_in=0.0, s_in=1.0, st_in=0, bn=None, x_h=Non
          float(rscale), float(p_out), int(st_out), ptr(seed), _s())
 
 
-def rowgemm_bnred(x, img, out, *, p_in=0.0, s_in=1.0, st_in=0, x_h=None, seed=None, bn, red):
-    """out = (drop'(x)) Wop^T (rowgemm PRO_DROP) with the BN-SiLU backward's sums red (2d f64, zero on entry)
-    accumulated in the epilogue (kdfm_rowgemm_bnred); bn = (y, mean, rstd, gamma, beta)."""
-    rows, d = x.shape
-    assert out.shape == (rows, d) and x.is_contiguous() and out.is_contiguous() and red.dtype == torch.float64
-    y, bm, br, bg, bb = bn
-    call("kdfm_rowgemm_bnred", ptr(_f32(x)), ptr(_bf16(img)), ptr(out), rows, d, float(p_in), float(s_in), int(st_in),
-         ptr(_bf16(x_h)), ptr(seed), ptr(_f32(y)), ptr(bm), ptr(br), ptr(bg), ptr(bb), ptr(red), _s())
-
-
 LNPROJ_QKV, LNPROJ_GLU = 0, 1
 IMG_FFN, IMG_LNPROJ, IMG_ROWGEMM = 0, 1, 2
 
@@ -1343,14 +1333,6 @@ def glu_mask_bwd(dg, a, lengths, da, B, T, d):
 
 def dwconv_fwd(g, w, bias, y, stats, B, T, d, K):
     call("kdfm_dwconv_fwd", ptr(g), ptr(w), ptr(bias), ptr(y), ptr(stats), B, T, d, K, _s())
-
-
-def dwconv_fwd_bn(g, w, bias, y, stats, counter, rm, rv, mean, rstd, B, T, d, K, eps, momentum):
-    """dwconv_fwd + the training BatchNorm finalize (batch mean / rstd, running statistics) in one launch;
-    stats (2d f64) and counter (1 int32) must be zero on entry and are zero again on exit."""
-    assert stats.dtype == torch.float64 and counter.dtype == torch.int32
-    call("kdfm_dwconv_fwd_bn", ptr(g), ptr(w), ptr(bias), ptr(y), ptr(stats), ptr(counter), ptr(rm), ptr(rv),
-         ptr(mean), ptr(rstd), B, T, d, K, float(eps), float(momentum), _s())
 
 
 def dwconv_bwd(dy, g, w, dg, dw, db, B, T, d, K, *, ws=None):

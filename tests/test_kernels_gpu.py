@@ -86,48 +86,6 @@ def test_dwconv_fwd_stats(B, T, d, k):
     torch.testing.assert_close(stats[d:], (r64 * r64).sum(0), rtol=1e-5, atol=1e-3)
 
 
-@pytest.mark.parametrize("det", [False, True])
-@pytest.mark.parametrize("B,T,d,k", [(3, 401, 88, 31), (2, 70, 40, 15)])
-def test_dwconv_fwd_bn_finalize(B, T, d, k, det):
-    """kdfm_dwconv_fwd_bn (the training BatchNorm finalize in the last workgroup of the depthwise conv) against
-    float64 batch statistics and the running-statistics update; the sums and the counter are zero again after
-    each call, so two layers' calls back to back on one pair agree with two separate references."""
-    K = _K()
-    from kdfm import _lib
-    g = torch.Generator().manual_seed(B * T + d + k + 7)
-    stats = torch.zeros(2 * d, dtype=torch.float64, device="cuda")
-    cnt = torch.zeros(1, dtype=torch.int32, device="cuda")
-    eps, mom = 1e-5, 0.1
-    _lib.lib().kdfm_set_deterministic(1 if det else 0)
-    try:
-        for call in range(2):
-            x = torch.randn(B, T, d, generator=g).cuda()
-            w = torch.randn(d, k, generator=g).cuda()
-            bias = torch.randn(d, generator=g).cuda()
-            rm0 = torch.randn(d, generator=g).cuda()
-            rv0 = torch.rand(d, generator=g).cuda() + 0.5
-            rm, rv = rm0.clone(), rv0.clone()
-            y = torch.empty_like(x)
-            mean = torch.empty(d, device="cuda")
-            rstd = torch.empty(d, device="cuda")
-            K.dwconv_fwd_bn(x, w, bias, y, stats, cnt, rm, rv, mean, rstd, B, T, d, k, eps, mom)
-            torch.cuda.synchronize()
-            ref = torch.nn.functional.conv1d(x.transpose(1, 2), w.unsqueeze(1), bias, padding=(k - 1) // 2,
-                                             groups=d).transpose(1, 2)
-            _close(y, ref)
-            r64 = ref.double().reshape(-1, d)
-            m = r64.mean(0)
-            var = r64.var(0, unbiased=False)
-            torch.testing.assert_close(mean.double(), m, rtol=1e-5, atol=1e-5)
-            torch.testing.assert_close(rstd.double(), 1.0 / torch.sqrt(var + eps), rtol=1e-5, atol=1e-5)
-            torch.testing.assert_close(rm.double(), (1 - mom) * rm0.double() + mom * m, rtol=1e-5, atol=1e-5)
-            torch.testing.assert_close(rv.double(), (1 - mom) * rv0.double() + mom * r64.var(0, unbiased=True),
-                                       rtol=1e-5, atol=1e-5)
-            assert int(cnt.item()) == 0 and bool((stats == 0).all()), (call, cnt.item())
-    finally:
-        _lib.lib().kdfm_set_deterministic(0)
-
-
 @pytest.mark.parametrize("batch_stats", [True, False])
 @pytest.mark.parametrize("B,T,d,k", [(3, 401, 88, 31), (2, 70, 40, 15)])
 def test_dwconv_bwd_bn_equals_separate(B, T, d, k, batch_stats):

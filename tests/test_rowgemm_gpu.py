@@ -78,33 +78,3 @@ def test_rowgemm_dropout_prologue_data_gradient():
     assert torch.equal(o1 == R, o2 == R)
     assert _rel(o1 - R, o2 - R) <= 1e-2
 
-
-@pytest.mark.parametrize("rows,d,p", [(12832, 88, 0.1), (1000, 176, 0.0), (77, 88, 0.1)])
-def test_rowgemm_bnred_matches_separate(rows, d, p):
-    """kdfm_rowgemm_bnred (pointwise_conv2's data gradient with the BN-SiLU backward's sums in its epilogue)
-    writes the same dz and bf16 operand as kdfm_rowgemm (PRO_DROP) bit for bit, and sums within f32 rounding
-    of kdfm_bn_silu_bwd_reduce over that dz."""
-    from kdfm import kernels as K
-    g = torch.Generator().manual_seed(rows + d)
-    x = torch.randn(rows, d, generator=g).cuda()
-    W = (torch.randn(d, d, generator=g) / d ** 0.5).cuda()
-    y = torch.randn(rows, d, generator=g).cuda()
-    mean = (torch.randn(d, generator=g) * 0.1).cuda()
-    rstd = (torch.rand(d, generator=g) + 0.5).cuda()
-    gm = torch.randn(d, generator=g).cuda()
-    bt = torch.randn(d, generator=g).cuda()
-    seed = torch.tensor([321], dtype=torch.int64, device="cuda")
-    img = K.rowgemm_img(W, trans=True)
-    dz0 = torch.empty(rows, d, device="cuda")
-    h0 = torch.empty(rows, d, device="cuda", dtype=torch.bfloat16)
-    K.rowgemm(x, img, dz0, pro=K.RG_PRO_DROP, p_in=p, s_in=1.0, st_in=5, x_h=h0, seed=seed)
-    red0 = torch.zeros(2 * d, dtype=torch.float64, device="cuda")
-    K.bn_silu_bwd_reduce(dz0, y, mean, rstd, gm, bt, red0)
-    dz1 = torch.empty(rows, d, device="cuda")
-    h1 = torch.empty(rows, d, device="cuda", dtype=torch.bfloat16)
-    red1 = torch.zeros(2 * d, dtype=torch.float64, device="cuda")
-    K.rowgemm_bnred(x, img, dz1, p_in=p, s_in=1.0, st_in=5, x_h=h1, seed=seed, bn=(y, mean, rstd, gm, bt), red=red1)
-    torch.cuda.synchronize()
-    assert torch.equal(dz0, dz1) and torch.equal(h0, h1)
-    err = (red1 - red0).abs().max().item()
-    assert err <= 1e-5 * red0.abs().max().item() + 1e-6, err
