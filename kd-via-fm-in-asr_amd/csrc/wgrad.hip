@@ -50,6 +50,8 @@ struct WrGeo {
   int64_t steps_per; // 32-row steps per split
   int64_t nmem;      // X columns in memory = ones_col if >= 0 else N
   int Msl;           // A columns (output rows) of one M slice (blockIdx.z), a multiple of 16
+  int ascal;         // f32 A whose rows are not 16-byte aligned or M % 4 != 0 (the decoder's 129 classes):
+                     // its staging units load 4 scalars each, columns past M masked to zero
 };
 
 // BIN: dY and X are bf16 in memory (the fused KD-head chains store their saved operands as bf16,
@@ -90,7 +92,8 @@ __global__ __launch_bounds__(WR_NT, 2) void wgr_kernel(GemmP p, WrGeo g) {
   }
   // B memory columns of this slice and the slab's staging units (4 rows x 4 columns each)
   const int ncols_mem = (int)((g.nmem - n0 < g.Nb) ? g.nmem - n0 : g.Nb);
-  const int units = 8 * ((mcols >> CWS) + (ncols_mem >> CWS));
+  const int ma4 = (BIN == 0 && g.ascal) ? (mcols + CW - 1) >> CWS : mcols >> CWS;   // A column groups
+  const int units = 8 * (ma4 + (ncols_mem >> CWS));
 
   // static image columns: A columns >= M and B columns beyond the memory columns are zero, the
   // ones column (bias gradient) is 1 in every row (rows past K contribute 0 through A)
@@ -127,8 +130,8 @@ __global__ __launch_bounds__(WR_NT, 2) void wgr_kernel(GemmP p, WrGeo g) {
   // counters are set up once and advanced by one slab per step: no 64-bit multiplies in the loop.
   // Rows past the split's end or outside the utterance (CONV taps) load from a clamped valid address
   // and are zeroed by a select (branch-free).
-  const int ma4 = mcols >> CWS;   // A column groups
   const char* src[UPT];   // byte pointers (ES-byte elements)
+  int acol[UPT];          // ascal: the unit's first A column (>= mcols: not an A unit)
   int64_t ld[UPT];        // row stride in bytes
   int tfr[UPT], toff[UPT];   // CONV: frame of the unit's first row in its utterance; tap - pad
   bool act[UPT];
@@ -140,9 +143,11 @@ __global__ __launch_bounds__(WR_NT, 2) void wgr_kernel(GemmP p, WrGeo g) {
     const int64_t r0 = kb + rg * 4;
     tfr[i] = 0;
     toff[i] = 0;
+    acol[i] = 1 << 30;
     if (cg < ma4) {
       src[i] = reinterpret_cast<const char*>(pA) + ES * (r0 * p.sAk + m0 + cg * CW);
       ld[i] = ES * p.sAk;
+      acol[i] = cg * CW;
     } else {
       const int64_t n = n0 + (int64_t)(cg - ma4) * CW;
       ld[i] = ES * p.sBk;
@@ -183,6 +188,17 @@ __global__ __launch_bounds__(WR_NT, 2) void wgr_kernel(GemmP p, WrGeo g) {
         if constexpr (BIN == 1) {
           const uint2 t = *reinterpret_cast<const uint2*>(q);
           r[i][j] = make_float4(__builtin_bit_cast(float, t.x), __builtin_bit_cast(float, t.y), 0.f, 0.f);
+        } else if constexpr (BIN == 0) {
+          if (g.ascal && acol[i] < mcols) {   // unaligned A row: 4 scalar loads, columns past M clamped + zeroed
+            const float* qa = reinterpret_cast<const float*>(q);
+            const int cb = acol[i];
+            float e[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) e[k] = qa[cb + k < mcols ? k : 0] * (cb + k < mcols ? 1.f : 0.f);
+            r[i][j] = make_float4(e[0], e[1], e[2], e[3]);
+          } else {
+            r[i][j] = *reinterpret_cast<const float4*>(q);
+          }
         } else {
           r[i][j] = *reinterpret_cast<const float4*>(q);
         }
@@ -540,7 +556,10 @@ bool wr_plan(const GemmP& p, int amode, int bmode, int64_t batch, WrPlan& pl, bo
   if (!enabled && !force) return false;
   if (batch != 1 || p.epi != KDFM_EPI_ATOMIC || amode != KDFM_LD_XC) return false;
   if (bmode != KDFM_LD_XC && bmode != KDFM_LD_CONV) return false;
-  if (p.sAm != 1 || (p.sAk & 3) || (p.M & 3) || (((uintptr_t)p.A) & 15)) return false;
+  // f32 A rows that are not 16-byte aligned (or M % 4 != 0): scalar A staging (WrGeo::ascal)
+  const bool ascal = !bf16in && ((p.sAk & 3) || (p.M & 3) || (((uintptr_t)p.A) & 15));
+  if (p.sAm != 1 || (bf16in && ((p.sAk & 3) || (p.M & 3) || (((uintptr_t)p.A) & 15)))) return false;
+  if (ascal && (((uintptr_t)p.A) & 3)) return false;
   if (p.sBn != 1 || (p.sBk & 3) || (((uintptr_t)p.B) & 15)) return false;
   const int nseg = p.nseg > 1 ? p.nseg : 1;
   if (p.ones_col >= 0 && p.ones_col != p.N - nseg) return false;
@@ -593,6 +612,7 @@ bool wr_plan(const GemmP& p, int amode, int bmode, int64_t batch, WrPlan& pl, bo
   pl.g.Nb = 16 * pl.w.nbw * pl.w.wn;
   pl.slices = ceil_div(p.N, pl.g.Nb);
   pl.g.nmem = nmem;
+  pl.g.ascal = ascal ? 1 : 0;
   // staging units per thread: the widest slice's slab
   const int64_t units = 8 * (pl.g.Msl / cw + (nmem < pl.g.Nb ? nmem : pl.g.Nb) / cw);
   pl.upt = (int)ceil_div(units, WR_NT);

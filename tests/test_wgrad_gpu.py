@@ -13,6 +13,8 @@ SHAPES = [  # rows, M (dY cols), N (X cols), bias
     (12832, 88, 352, True), (12832, 352, 88, True), (12832, 264, 88, True), (12832, 176, 88, True),
     (12832, 88, 88, True), (12832, 88, 1760, False), (25600, 88, 792, True), (205312 // 8, 96, 96, True),
     (205312 // 8, 96, 176, True), (205312 // 8, 176, 96, True), (4097, 96, 88, True), (2049, 128, 20, True),
+    # the decoder's 129 classes: rows of dY 4-byte aligned only, M % 4 != 0 (scalar A staging, WrGeo::ascal)
+    (12832, 129, 88, True), (5003, 131, 40, False),
 ]
 
 
