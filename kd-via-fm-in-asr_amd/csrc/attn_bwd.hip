@@ -141,10 +141,34 @@ __device__ __forceinline__ void put_rows(uint16_t* rc, uint16_t* cr, int ldt, co
   }
 }
 
+// fetch_rows as buffer loads: an out-of-range row's offset is AB_OOB (the load reads 0 without a memory
+// access), so no load is branched around and no 64-bit address is held per load; `rsrc` covers `src`
+template <int MAXI>
+__device__ __forceinline__ void fetch_rows_b(float4 (&v)[MAXI], __amdgpu_buffer_rsrc_t rsrc, int64_t ld,
+                                             int64_t base_row, int r0, int n, int lo, int hi, int64_t c0, int dk) {
+  const int cq = dk >> 2;
+#pragma unroll
+  for (int it = 0; it < MAXI; ++it) {
+    const int e = threadIdx.x + it * 256;
+    const int rr = e / cq, c4 = (e - rr * cq) * 4;
+    const int r = r0 + rr;
+    const bool ok = e < n * cq && r >= lo && r < hi;
+    const uint32_t off = ok ? (uint32_t)(((base_row + r) * ld + c0 + c4) * 4) : 0x80000000u;
+    v[it] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 0));
+  }
+}
+
 // zero columns [dk, 64) of rows [0, rows) of a [row][c] image, and every column of rows [z0, rows)
 __device__ __forceinline__ void zero_pad(uint16_t* img, int rows, int dk, int z0) {
   for (int e = threadIdx.x; e < rows * (BDK - dk); e += 256) img[(e / (BDK - dk)) * LR + dk + e % (BDK - dk)] = 0;
   for (int e = threadIdx.x; e < (rows - z0) * dk; e += 256) img[(z0 + e / dk) * LR + e % dk] = 0;
+}
+
+// zero a whole [rows][LR] image with 16-byte stores (the bwd2 kernels: a superset of zero_pad -- the data
+// columns of rows below z0 are rewritten by put_rows after a barrier -- without its per-element divisions)
+__device__ __forceinline__ void zero_img(uint16_t* img, int rows) {
+  static_assert((LR * 2) % 16 == 0, "row stride must be a multiple of 16 bytes");
+  for (int e = threadIdx.x; e < rows * LR / 8; e += 256) reinterpret_cast<uint4*>(img)[e] = make_uint4(0u, 0u, 0u, 0u);
 }
 
 // r[(b*H + h)*T + i] = sum_c dO[b*T + i][h*dk + c] * O[b*T + i][h*dk + c]; one wave per (row, head)
@@ -188,9 +212,15 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dq_kernel(AbP p
   const int nkb = (len + BK - 1) / BK;
   const int npos = 2 * T - 1;
   const int64_t hoff = h * p.dkh;
-  zero_pad(Ks, BK, dk, BK);
-  zero_pad(Vs, BK, dk, BK);
-  zero_pad(Pr, PB1, dk, 127);
+  if constexpr (SAVE) {
+    zero_img(Ks, BK);
+    zero_img(Vs, BK);
+    zero_img(Pr, PB1);
+  } else {
+    zero_pad(Ks, BK, dk, BK);
+    zero_pad(Vs, BK, dk, BK);
+    zero_pad(Pr, PB1, dk, 127);
+  }
 
   // this lane's query row (A-fragment row): Qu, Qv and dO fragments
   const int iq = i0 + w * 16 + (lane & 15);
@@ -219,28 +249,33 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dq_kernel(AbP p
 
   // next key block's operands in registers: V and K rows, the Ppos band
   float4 nv[NU], nk[NU], nb[2 * NU];
+  // bwd2 (SAVE): buffer loads over K / V (qkv rows) and the band (the entry checks the sizes fit 31 bits)
+  const int kvbytes = SAVE ? (int)((p.B * p.T * p.ldkv - p.d) * 4) : 0;
+  const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc((void*)p.k, (short)0, kvbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc((void*)p.v, (short)0, kvbytes - (int)(4 * p.d) * SAVE,
+                                                                      0x00020000);
+  const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc((void*)p.pos, (short)0,
+                                                                      SAVE ? (int)(npos * p.d * 4) : 0, 0x00020000);
   auto fetch = [&](int kb) {
     const int j0 = kb * BK;
     const int rbase = T - 1 - (i0 + BQ - 1) + j0;
-    fetch_rows<NU>(nv, p.v, p.ldkv, b * p.T, j0, BK, 0, len, hoff, dk);
-    fetch_rows<NU>(nk, p.k, p.ldkv, b * p.T, j0, BK, 0, len, hoff, dk);
-    fetch_rows<2 * NU>(nb, p.pos, p.d, 0, rbase, 127, 0, npos, hoff, dk);
+    if constexpr (SAVE) {
+      fetch_rows_b<NU>(nv, rv, p.ldkv, b * p.T, j0, BK, 0, len, hoff, dk);
+      fetch_rows_b<NU>(nk, rk, p.ldkv, b * p.T, j0, BK, 0, len, hoff, dk);
+      fetch_rows_b<2 * NU>(nb, rp, p.d, 0, rbase, 127, 0, npos, hoff, dk);
+    } else {
+      fetch_rows<NU>(nv, p.v, p.ldkv, b * p.T, j0, BK, 0, len, hoff, dk);
+      fetch_rows<NU>(nk, p.k, p.ldkv, b * p.T, j0, BK, 0, len, hoff, dk);
+      fetch_rows<2 * NU>(nb, p.pos, p.d, 0, rbase, 127, 0, npos, hoff, dk);
+    }
   };
+  if constexpr (SAVE) {   // the first block's loads in flight behind the centre and row-sum prologue
+    if (nkb > 0) fetch(0);
+  }
 
   // the forward's centring (attn_centre.h): K rows staged as K_j - kc (the scores, hence P = exp(s - lse),
   // are the forward's), V rows as V_j - vc with cs_i = dO_i . vc added back to dPd in f32
   kv_centre(p.k + b * p.T * p.ldkv + hoff, p.v + b * p.T * p.ldkv + hoff, p.ldkv, len, dk, Cn);
-  float4 ck[NU], cv[NU];
-  {
-    const int cq = dk >> 2;
-#pragma unroll
-    for (int it = 0; it < NU; ++it) {
-      const int e = threadIdx.x + it * 256;
-      const int c4 = (e - (e / cq) * cq) * 4;
-      ck[it] = *reinterpret_cast<const float4*>(&Cn[0][c4]);
-      cv[it] = *reinterpret_cast<const float4*>(&Cn[1][c4]);
-    }
-  }
   // cs_i for this lane's C-layout rows: row (lane & 15) of the wave's 16 dotted in f32 by its 4 lane groups
   // (16 columns each), summed across them, then picked up by the lanes owning each row.  With RIN (bwd2)
   // the row sums r_i = dO_i . O_i are formed the same way here instead of by attn_rowdot_kernel
@@ -280,14 +315,17 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dq_kernel(AbP p
 #pragma unroll
     for (int r = 0; r < 4; ++r) rs[r] = ib + r < len ? rin[r] : 0.f;
   }
-  // subtract the centre from the staged rows of keys [j0, j0 + BK) that are valid (rows past len stay 0)
-  auto centre = [&](float4 (&v)[NU], const float4 (&c)[NU], int j0) {
+  // subtract the centre (read back from LDS: holding it in registers spills the loop's staging addresses)
+  // from the staged rows of keys [j0, j0 + BK) that are valid (rows past len stay 0)
+  auto centre = [&](float4 (&v)[NU], const float* c, int j0) {
     const int cq = dk >> 2;
 #pragma unroll
     for (int it = 0; it < NU; ++it) {
       const int e = threadIdx.x + it * 256;
-      const bool ok = e < BK * cq && j0 + e / cq < len;
-      if (ok) v[it] = make_float4(v[it].x - c[it].x, v[it].y - c[it].y, v[it].z - c[it].z, v[it].w - c[it].w);
+      const int rr = e / cq;
+      const float m = (e < BK * cq && j0 + rr < len) ? 1.f : 0.f;   // a multiply: no branch around the read
+      const float4 cc = *reinterpret_cast<const float4*>(c + (e - rr * cq) * 4);
+      v[it] = make_float4(v[it].x - m * cc.x, v[it].y - m * cc.y, v[it].z - m * cc.z, v[it].w - m * cc.w);
     }
   };
 
@@ -301,13 +339,13 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dq_kernel(AbP p
   const int sbytes = SAVE ? (int)(p.B * p.H * p.T * p.ldt * 2) : 0;
   const __amdgpu_buffer_rsrc_t rds = __builtin_amdgcn_make_buffer_rsrc((void*)p.ds, (short)0, sbytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rpd = __builtin_amdgcn_make_buffer_rsrc((void*)p.pdo, (short)0, sbytes, 0x00020000);
-  if (nkb > 0) fetch(0);
+  if (!SAVE && nkb > 0) fetch(0);
   KPROBE(1);
   for (int kb = 0; kb < nkb; ++kb) {
     const int j0 = kb * BK;
     __syncthreads();
-    centre(nk, ck, j0);
-    centre(nv, cv, j0);
+    centre(nk, Cn[0], j0);
+    centre(nv, Cn[1], j0);
     put_rows<NU>(Vs, nullptr, 0, nv, BK, dk);
     put_rows<NU>(Ks, nullptr, 0, nk, BK, dk);
     put_rows<2 * NU>(Pr, nullptr, 0, nb, 127, dk);
@@ -347,7 +385,11 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dq_kernel(AbP p
         for (int r = 0; r < 4; ++r) {
           const int ii = 4 * (lane >> 4) + r, jj = 16 * t + (lane & 15);
           const float bd = G[ii * LG32 + jj - ii + 15];
-          s[t][r] = (j0 + jj < len) ? (ac[t][r] + bd) * p.scale : -3.0e38f;
+          if constexpr (SAVE) {   // masked by an add: a select on the read value is branched around it
+            s[t][r] = (ac[t][r] + bd) * p.scale + ((j0 + jj < len) ? 0.f : -3.0e38f);
+          } else {
+            s[t][r] = (j0 + jj < len) ? (ac[t][r] + bd) * p.scale : -3.0e38f;
+          }
         }
       wsync();   // the scratch is rewritten below
     }
@@ -771,8 +813,8 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dkv2_kernel(AbP
   const int j0 = (int)blk.x * BK;
   const int len = p.lens ? (int)min<int64_t>(p.lens[b], p.T) : T;
   const int64_t hoff = h * p.dkh;
-  zero_pad(Os, BQ, dk, BQ);
-  zero_pad(Qs, BQ, dk, BQ);
+  zero_img(Os, BQ);
+  zero_img(Qs, BQ);
   const int sbytes = (int)(p.B * p.H * p.T * p.ldt * 2);
   const __amdgpu_buffer_rsrc_t rds = __builtin_amdgcn_make_buffer_rsrc((void*)p.ds, (short)0, sbytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rpd = __builtin_amdgcn_make_buffer_rsrc((void*)p.pdo, (short)0, sbytes, 0x00020000);
@@ -1058,6 +1100,7 @@ int kdfm_relpos_attn_bwd2_dq(const float* dO, const float* O, const float* qu, c
   KDFM_REQUIRE(dO && O && qu && qv && qkv && pos && lse && ds && pd && dqu && dqv, "null pointer");
   KDFM_REQUIRE((((uintptr_t)dO | (uintptr_t)O | (uintptr_t)qu | (uintptr_t)qv | (uintptr_t)qkv | (uintptr_t)pos |
                  (uintptr_t)ds | (uintptr_t)pd) & 15) == 0, "operands must be 16-byte aligned");
+  KDFM_REQUIRE(B * T * 3 * d * 4 < (1ll << 31), "qkv larger than 2 GiB (buffer offsets)");
   AbP p;
   int rc = ab2_setup(p, qu, qv, qkv, lse, lengths, B, H, T, d, scale, dropout_p, seed, rng_stream);
   if (rc || B == 0) return rc;

@@ -20,7 +20,7 @@ static float* dev_rand(size_t n, float scale, unsigned seed) {
   return d;
 }
 
-static void run(int64_t B, int64_t T, int64_t d, int64_t H, KProbe& kp) {
+static void run(int64_t B, int64_t T, int64_t d, int64_t H, KProbe& kp, bool v2) {
   const int64_t rows = B * T;
   float* qu = dev_rand(rows * d, 1.f, 1);
   float* qv = dev_rand(rows * d, 1.f, 2);
@@ -51,7 +51,17 @@ static void run(int64_t B, int64_t T, int64_t d, int64_t H, KProbe& kp) {
   if (kdfm_relpos_attn_bwd_parts(dO, o, qu, qv, qkv, pos, lse, pt, mblk, lens, dqu, dqv, nullptr, nullptr, ws, wsl, B, H,
                                  T, d, scale, 0.1f, seed, 5, KDFM_ATTN_BWD_ROWDOT, nullptr))
     exit(4);
+  const int64_t ldt = kdfm_relpos_attn_bwd2_ldt(T);
+  uint16_t *ds2, *pd2;
+  (void)hipMalloc(&ds2, B * H * T * ldt * 2);
+  (void)hipMalloc(&pd2, B * H * T * ldt * 2);
   auto launch = [&]() {
+    if (v2) {
+      if (kdfm_relpos_attn_bwd2_dq(dO, o, qu, qv, qkv, pos, lse, lens, nullptr, ds2, pd2, dqu, dqv, B, H, T, d, scale,
+                                   0.1f, seed, 5, nullptr))
+        exit(6);
+      return;
+    }
     if (kdfm_relpos_attn_bwd_parts(dO, o, qu, qv, qkv, pos, lse, pt, mblk, lens, dqu, dqv, nullptr, nullptr, ws, wsl, B,
                                    H, T, d, scale, 0.1f, seed, 5, KDFM_ATTN_BWD_DQ, nullptr))
       exit(5);
@@ -71,15 +81,17 @@ static void run(int64_t B, int64_t T, int64_t d, int64_t H, KProbe& kp) {
   launch();
   (void)hipDeviceSynchronize();
   char title[128];
-  snprintf(title, sizeof title, "attn_bwd_dq B=%lld T=%lld d=%lld H=%lld", (long long)B, (long long)T, (long long)d,
+  snprintf(title, sizeof title, "attn_bwd%s_dq B=%lld T=%lld d=%lld H=%lld", v2 ? "2" : "", (long long)B, (long long)T, (long long)d,
            (long long)H);
+  (void)v2;
   kp.report(title, 1e3f * ms / 10);
 }
 
 int main() {
   KProbe kp;
   kp.alloc((size_t)7 * 32 * 2 * 4);
-  run(32, 401, 88, 2, kp);
-  run(1, 401, 88, 2, kp);
+  run(32, 401, 88, 2, kp, false);
+  run(32, 401, 88, 2, kp, true);
+  run(1, 401, 88, 2, kp, true);
   return 0;
 }

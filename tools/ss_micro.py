@@ -62,3 +62,15 @@ def both():
 
 
 print(f"student + teacher on two streams: {timed(both):7.1f} us")
+
+# the backward's direct conv2 data gradient with conv0's weight gradient fused (student, C = 88)
+C = 88
+w2 = torch.randn(C, C, 3, 3, device=dev, generator=g) * (1.0 / (3 * C ** 0.5))
+wt = torch.empty(K.subsample_dgrad_wprep_elems(C), device=dev, dtype=torch.bfloat16)
+K.subsample_dgrad_wprep(w2, wt)
+dy2 = torch.randn(B * T2 * F2, C, device=dev, generator=g)
+y1 = torch.randn(B * T1 * F1, C, device=dev, generator=g).to(torch.bfloat16)
+dw0 = torch.zeros(C, 9, device=dev)
+db0 = torch.zeros(C, device=dev)
+us = timed(lambda: K.subsample_conv2_dgrad_w0(dy2, wt, y1, B, T1, F1, C, mel, ml, Tm, F, 1, dw0, db0))
+print(f"C={C:3d} conv2 dgrad + conv0 wgrad isolated: {us:7.1f} us  ({2 * 2.25 * C * C * B * T1 * F1 / us / 1e6:6.1f} TFLOP/s)")
