@@ -365,18 +365,25 @@ __device__ __forceinline__ void sd_class(const SdGeo& g, __amdgpu_buffer_rsrc_t 
       j = rem - i * nF;
     }
     load_tap(fa, 0, ok, b, i, j);
+    // keep the tap-0 loads here, ahead of the mask loads: left alone the scheduler sinks each load next to
+    // its MFMA and waits for it there (one HBM round trip per fragment)
+    __builtin_amdgcn_sched_barrier(0);
     const int t1 = 2 * i + PT, f1 = 2 * j + PF;
     if (h == 0) {
       mp[r] = ok ? (b * g.T1 + t1) * g.F1 + f1 : -1;
       if (g.wpart) {
         const int t0 = 2 * t1 - g.pad, f0 = 2 * f1 - g.pad;
+        // every load unconditional at a clamped index and masked by a multiply: a conditional load is
+        // branched around and waited for one at a time (9 serialized HBM round trips per tile)
         const int tl = !ok ? 0 : (g.mel_len ? (int)min((int64_t)g.Tm, g.mel_len[b]) : g.Tm);
-        const float* mrow = g.mel + ((int64_t)b * g.Tm + t0) * g.Fm + f0;
+        const float* mb = g.mel + (int64_t)b * g.Tm * g.Fm;
         float xp[SD_PTS];
 #pragma unroll
         for (int tp = 0; tp < 9; ++tp) {
           const int tt = t0 + tp / 3, ff = f0 + tp % 3;
-          xp[tp] = (tt >= 0 && tt < tl && ff >= 0 && ff < g.Fm) ? mrow[(tp / 3) * g.Fm + tp % 3] : 0.f;
+          const bool in = tt >= 0 && tt < tl && ff >= 0 && ff < g.Fm;
+          const float x = mb[in ? tt * g.Fm + ff : 0];
+          xp[tp] = (in ? 1.f : 0.f) * x;
         }
         xp[9] = ok ? 1.f : 0.f;
         xp[10] = xp[11] = 0.f;
@@ -414,7 +421,10 @@ __device__ __forceinline__ void sd_class(const SdGeo& g, __amdgpu_buffer_rsrc_t 
       for (int e = 0; e < 16; ++e) acc[n][e] = 0.f;
 #pragma unroll
     for (int t = 0; t < NTAP; ++t) {
-      if (t > 0) load_tap(fa, t, ok, b, i, j);
+      if (t > 0) {
+        load_tap(fa, t, ok, b, i, j);
+        __builtin_amdgcn_sched_barrier(0);   // all of the tap's loads issued before the first wait
+      }
       bf16x8_t a[KS];
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
