@@ -123,16 +123,12 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void relpos_attn_fwd_kernel(A
       __builtin_amdgcn_make_buffer_rsrc((void*)p.mblk, (short)0, WPT ? (int)(p.B * p.H * p.T * nkb_all * 4) : 0, 0x00020000);
   const int64_t hoff = h * p.dk;
 
-  // zero the padded head-dim columns once (never overwritten afterwards)
-  for (int e = threadIdx.x; e < AKB * (DKP - dk); e += 256) {
-    const int r = e / (DKP - dk), c = dk + e % (DKP - dk);
-    Ks[r * LDR + c] = 0;
-  }
-  for (int e = threadIdx.x; e < BAND * (DKP - dk); e += 256) {
-    const int r = e / (DKP - dk), c = dk + e % (DKP - dk);
-    Pr[r * LDR + c] = 0;
-  }
-  for (int e = threadIdx.x; e < (DKP - dk) * LDVT; e += 256) Vt[dk * LDVT + e] = 0;
+  // zero the K / V^T / band images once with 16-byte stores (the padded head-dim columns are never
+  // overwritten afterwards; the data columns are rewritten by store_stage after a barrier)
+  static_assert((AKB * LDR) % 8 == 0 && (DKP * LDVT) % 8 == 0 && (BAND * LDR) % 8 == 0, "16-byte images");
+  for (int e = threadIdx.x; e < AKB * LDR / 8; e += 256) reinterpret_cast<uint4*>(Ks)[e] = make_uint4(0u, 0u, 0u, 0u);
+  for (int e = threadIdx.x; e < DKP * LDVT / 8; e += 256) reinterpret_cast<uint4*>(Vt)[e] = make_uint4(0u, 0u, 0u, 0u);
+  for (int e = threadIdx.x; e < BAND * LDR / 8; e += 256) reinterpret_cast<uint4*>(Pr)[e] = make_uint4(0u, 0u, 0u, 0u);
 
   // this lane's query row (A-fragment row) and its Qu / Qv fragments
   const int iq = i0 + w * 16 + (lane & 15);
@@ -185,13 +181,6 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void relpos_attn_fwd_kernel(A
   const float* pbase = p.pos + hoff;
   // key / value centring (attn_centre.h): K and V are staged as bf16(K_j - kc) and bf16(V_j - vc); the
   // scores (hence lse, p~, m_blk) are those of the centred keys, O gets (sum_j Pd_ij) vc back in f32
-  kv_centre(kbase, vbase, p.ldkv, min(len, T), dk, Cn);
-  float4 ck4[KU], cv4[KU];
-#pragma unroll
-  for (int i = 0; i < KU; ++i) {
-    ck4[i] = *reinterpret_cast<const float4*>(&Cn[0][kc[i]]);
-    cv4[i] = *reinterpret_cast<const float4*>(&Cn[1][kc[i]]);
-  }
   float4 rk[KU], rv[KU], rp[PU];
   uint32_t kok = 0u, pok = 0u;   // validity of the staged slots of the stage in flight
   auto load_stage = [&](int j0, bool with_v) {
@@ -221,10 +210,13 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void relpos_attn_fwd_kernel(A
     for (int i = 0; i < KU; ++i) {
       if ((kin >> i) & 1u) {
         const bool ok = (kok >> i) & 1u;
-        const float4 kk = make_float4(rk[i].x - ck4[i].x, rk[i].y - ck4[i].y, rk[i].z - ck4[i].z, rk[i].w - ck4[i].w);
+        // the centre read back from LDS (float4 copies held across the loop cost 24 VGPRs)
+        const float4 ck = *reinterpret_cast<const float4*>(&Cn[0][kc[i]]);
+        const float4 cv = *reinterpret_cast<const float4*>(&Cn[1][kc[i]]);
+        const float4 kk = make_float4(rk[i].x - ck.x, rk[i].y - ck.y, rk[i].z - ck.z, rk[i].w - ck.w);
         store4_bf16(Ks + kj[i] * LDR + kc[i], ok ? kk : z);
         if (with_v) {
-          const float4 vc = make_float4(rv[i].x - cv4[i].x, rv[i].y - cv4[i].y, rv[i].z - cv4[i].z, rv[i].w - cv4[i].w);
+          const float4 vc = make_float4(rv[i].x - cv.x, rv[i].y - cv.y, rv[i].z - cv.z, rv[i].w - cv.w);
           const float4 vv = ok ? vc : z;
           Vt[(kc[i] + 0) * LDVT + kj[i]] = f2bf(vv.x);
           Vt[(kc[i] + 1) * LDVT + kj[i]] = f2bf(vv.y);
@@ -279,8 +271,10 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void relpos_attn_fwd_kernel(A
   };
 
   // ---- pass 1 (two-pass mode): row max / sum ----
+  // (the first stage's loads are issued before the centre: they are raw rows, centred at store time)
   if (TWO_PASS && nkb > 0) load_stage(0, false);
   if (!TWO_PASS && nkb > 0) load_stage(0, true);
+  kv_centre(kbase, vbase, p.ldkv, min(len, T), dk, Cn);
   if constexpr (WPT) {
     // the loop body leaves its 4 m_blk + 16 p~ stores behind the next block's loads; the same number of
     // (range-dropped) stores behind the first block's loads lets the compiler's wait for a staged load
