@@ -234,7 +234,9 @@ int kdfm_relpos_attn_bwd(const float* dO, const float* O, const float* qu, const
  *        two plain products, no recompute of P, dP or the dropout mask;
  *   _dpos: dpos[r] = sum_{b,i} dS[i][r-T+1+i] qv_i (2T-1, d, overwritten) over per-utterance-chunk
  *        partials in ws (kdfm_relpos_attn_bwd2_dpos_ws floats) folded in chunk order.
- * _dkv and _dpos only read ds / pd: they may run concurrently on two streams after _dq. */
+ * _dkv and _dpos only read ds / pd: they may run concurrently on two streams after _dq.
+ * Limits (32-bit buffer offsets): B*H*T*ldt*2 bytes of ds / pd and B*T*3d*4 bytes of qkv below 2 GiB
+ * (KDFM_EINVAL otherwise). */
 int64_t kdfm_relpos_attn_bwd2_ldt(int64_t T);
 int64_t kdfm_relpos_attn_bwd2_dpos_ws(int64_t B, int64_t T, int64_t d);
 int kdfm_relpos_attn_bwd2_dq(const float* dO, const float* O, const float* qu, const float* qv, const float* qkv,
