@@ -125,8 +125,9 @@ __device__ __forceinline__ float epi_apply(const GemmP& p, int64_t bz, int64_t m
 // SILU_DROP: Conformer FFN up-projection (bias, SiLU, optional dropout, optional STORE_PRE);
 // DROP_RESID: FFN down / attention out / conv pw2 (bias, dropout, scaled residual).  Same
 // arithmetic and dropout index as epi_apply.
+// MSE: the flow-matching loss head (bias, diff = v - R, loss partial, rscale * diff), same as epi_apply.
 enum { SKC_EPI_GENERIC = 0, SKC_EPI_RELU = 1, SKC_EPI_RESID = 2, SKC_EPI_DRELU = 3, SKC_EPI_NONE = 4,
-       SKC_EPI_SILU_DROP = 5, SKC_EPI_DROP_RESID = 6 };
+       SKC_EPI_SILU_DROP = 5, SKC_EPI_DROP_RESID = 6, SKC_EPI_MSE = 7 };
 
 template <int EMODE>
 __device__ __forceinline__ float skc_epi(const GemmP& p, int64_t m, int64_t n, float v, float bn, float sv, bool rowok,
@@ -139,6 +140,11 @@ __device__ __forceinline__ float skc_epi(const GemmP& p, int64_t m, int64_t n, f
     if constexpr (EMODE == SKC_EPI_RELU) return fmaxf(v, 0.f);
     if constexpr (EMODE == SKC_EPI_RESID) return sv + p.rscale * v;
     if constexpr (EMODE == SKC_EPI_DRELU) return sv > 0.f ? v : 0.f;
+    if constexpr (EMODE == SKC_EPI_MSE) {
+      const float diff = v - sv;
+      mse_part += diff * diff;
+      return p.rscale * diff;
+    }
     if constexpr (EMODE == SKC_EPI_SILU_DROP || EMODE == SKC_EPI_DROP_RESID) {
       pre = v;
       if constexpr (EMODE == SKC_EPI_SILU_DROP) v = siluf_(v);
@@ -160,6 +166,7 @@ __host__ inline int skc_epi_mode(int epi) {
     case KDFM_EPI_RESID: return SKC_EPI_RESID;
     case KDFM_EPI_DRELU: return SKC_EPI_DRELU;
     case KDFM_EPI_RESID | KDFM_EPI_DROPOUT: return SKC_EPI_DROP_RESID;
+    case KDFM_EPI_MSE: return SKC_EPI_MSE;
     default: break;
   }
   if ((epi & ~(KDFM_EPI_BIAS | KDFM_EPI_DROPOUT | KDFM_EPI_STORE_PRE)) == KDFM_EPI_SILU) return SKC_EPI_SILU_DROP;

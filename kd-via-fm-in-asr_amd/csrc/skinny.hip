@@ -706,6 +706,7 @@ int sk_dispatch_nct(int nct, const GemmP& p, const SkGeo& g, int64_t gx, int64_t
           case SKC_EPI_RELU: return sk_launch<3, AMODE, WV, SKC_EPI_RELU>(p, g, gx, ncr, lds, st);
           case SKC_EPI_RESID: return sk_launch<3, AMODE, WV, SKC_EPI_RESID>(p, g, gx, ncr, lds, st);
           case SKC_EPI_DRELU: return sk_launch<3, AMODE, WV, SKC_EPI_DRELU>(p, g, gx, ncr, lds, st);
+          case SKC_EPI_MSE: return sk_launch<3, AMODE, WV, SKC_EPI_MSE>(p, g, gx, ncr, lds, st);
           default: break;
         }
       }
