@@ -583,7 +583,11 @@ bool wr_plan(const GemmP& p, int amode, int bmode, int64_t batch, WrPlan& pl, bo
   // rows 247 -> 164 us, tools/gpu_wgr_wgs.sh, profiles/r02/wgs_*.log); inside the step, where these
   // run on the weight-gradient stream beside the critical-path kernels, one per CU wins (bench
   // 1655 -> 1686 utt/s, tools/gpu_wgr_env_ab.sh, profiles/r02/envab_*.log)
-  static const int target = env_i("KDFM_WGR_WGS", 256);
+  static const int target_all = env_i("KDFM_WGR_WGS", 256);
+  // conv-mode products (the denoiser's k=3 convs over the stacked head rows, 4 per step) may take fewer
+  // workgroups so the compute stream's heads kernels keep CUs beside them (KDFM_WGR_CONV_WGS)
+  static const int target_conv = env_i("KDFM_WGR_CONV_WGS", target_all);
+  const int target = bmode == KDFM_LD_CONV ? target_conv : target_all;
   static const int min_steps = env_i("KDFM_WGR_STEPS", 4);
   // off by default: isolated the slices help (FFN W1 25 -> 19 us) but in the step the extra
   // workgroups queue behind the critical-path kernels (bench 1687 unsliced vs 1635 sliced at
