@@ -1,0 +1,12 @@
+# hardware queues per process: 4 (default) vs 8 vs 16, interleaved bench (confirmation of r4aq)
+set -o pipefail
+OUT=gpurun_out/r4ar
+mkdir -p $OUT
+export TMPDIR=/tmp
+v() { tail -1 $1 | cut -c1-140 | grep -o '"value": [0-9.]*'; }
+for r in 1 2 3; do
+  timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-f32-sensitivity > $OUT/bench_q4_$r.log 2>&1 || { echo "bench failed"; exit 7; }
+  GPU_MAX_HW_QUEUES=8 timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-f32-sensitivity > $OUT/bench_q8_$r.log 2>&1 || { echo "bench q8 failed"; exit 8; }
+  GPU_MAX_HW_QUEUES=16 timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-f32-sensitivity > $OUT/bench_q16_$r.log 2>&1 || { echo "bench q16 failed"; exit 9; }
+  echo "q4 $(v $OUT/bench_q4_$r.log)  q8 $(v $OUT/bench_q8_$r.log)  q16 $(v $OUT/bench_q16_$r.log)"
+done
