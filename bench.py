@@ -98,6 +98,25 @@ def parse():
     return ap.parse_args()
 
 
+def attn_ffn_gflop_per_utt(cfg, samples):
+    """SURVEY.md §8(d)'s MFMA-bound contractions per utterance, from the layer dimensions: per ConformerLayer
+    and utterance of T frames, the two FFNs (32 T d^2) + q|k|v and out projections (8 T d^2) + scores,
+    rel-pos band and P V (8 T^2 d); student forward + backward (x3) + teacher forward.  23.0 GFLOP/utt at the
+    Conformer-CTC-small bench shape (d 88 / 176, T 401)."""
+    from kdfm.config import sub_dims
+    T = sub_dims(cfg, samples // cfg.hop + 1)[-1][0]
+    per = lambda d: 40.0 * T * d * d + 8.0 * T * T * d  # noqa: E731
+    return (3 * cfg.n_layers * per(cfg.d_student) + cfg.n_layers * per(cfg.d_teacher)) / 1e9
+
+
+# FastConformer-XL layer shapes (BASELINE.json configs[4]; fast-conformer_ctc_bpe.yaml:29 XLarge row: d_model 1024,
+# 8 heads -> head dim 128, 24 layers, conv kernel 9, xscaling False; dw_striding x8 with 256 channels, :113-125)
+# for student and teacher: the one config change of the xl_shape_sensitivity line
+XL_SHAPES = dict(d_student=1024, heads_student=8, d_teacher=1024, heads_teacher=8, n_layers=24,
+                 subsampling="dw_striding", subsampling_factor=8, subsampling_conv_channels=256, conv_kernel=9,
+                 xscaling=False, sched_d_model=1024)
+
+
 def sensitivity(dev, samples, steps=3, **overrides):
     """utt/s of the same step with one configuration change (1 warm-up + `steps` timed eager steps on a
     separate engine): math="f32" -- exact-f32 MFMA arithmetic, the reference trains fp32
@@ -122,8 +141,13 @@ def sensitivity(dev, samples, steps=3, **overrides):
     el = time.perf_counter() - t0
     del eng
     torch.cuda.empty_cache()
-    return {"value": round(B_PER_GPU * steps / el, 3), "unit": "utterances/sec", "ms_per_step": round(1e3 * el / steps, 3),
+    utt = B_PER_GPU * steps / el
+    peak = MI355X_BF16_DENSE_TFLOPS if cfg.math == "bf16" else MI355X_F32_MFMA_TFLOPS
+    gf = attn_ffn_gflop_per_utt(cfg, samples)
+    return {"value": round(utt, 3), "unit": "utterances/sec", "ms_per_step": round(1e3 * el / steps, 3),
             "steps": steps, "issue": "eager", "config_change": overrides,
+            "attn_ffn_gflop_per_utt": round(gf, 2),
+            "attn_ffn_mfma_frac": round(gf * 1e9 * utt / (peak * 1e12), 5),
             "note": "same workload with this one change; sensitivity only, not the headline value"}
 
 
@@ -218,6 +242,32 @@ def rank_launch_cmd(argv, gpus: int, port: int) -> list:
             "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
 
 
+def visible_gpu_count(environ=None, kfd_nodes="/sys/class/kfd/kfd/topology/nodes"):
+    """GPUs this process could use, without initialising any GPU runtime (the launcher parent forks and
+    execs the ranks, so it must stay GPU-free by construction): the device list of HIP_VISIBLE_DEVICES /
+    ROCR_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES when one is set (the innermost mask HIP applies), else the
+    KFD topology nodes with a non-zero simd_count (CPU nodes report 0).  None when neither says."""
+    env = os.environ if environ is None else environ
+    for var in ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES"):
+        v = env.get(var)
+        if v is not None:
+            return len([t for t in v.split(",") if t.strip() and t.strip() != "-1"])
+    try:
+        nodes = os.listdir(kfd_nodes)
+    except OSError:
+        return None
+    n = 0
+    for node in nodes:
+        try:
+            with open(os.path.join(kfd_nodes, node, "properties")) as fh:
+                props = dict(ln.split(None, 1) for ln in fh.read().splitlines() if ln.strip())
+        except (OSError, ValueError):
+            continue
+        if int(props.get("simd_count", "0").strip() or 0) > 0:
+            n += 1
+    return n
+
+
 def launch_ranks(args, argv, run=None) -> int | None:
     """`bench.py --gpus N` outside a launcher (no WORLD_SIZE in the environment) with N > 1: start the N
     ranks as child processes and return their exit code (the reference trains with Lightning's
@@ -235,7 +285,7 @@ def launch_ranks(args, argv, run=None) -> int | None:
     if args.gpus == 1:
         return None
     backend = os.environ.get("KDFM_DIST_BACKEND", "nccl")
-    n_dev = torch.cuda.device_count()   # does not initialise the HIP runtime on this image
+    n_dev = visible_gpu_count()   # environment / sysfs only: nothing in the parent touches torch.cuda or HIP
     if backend == "nccl" and n_dev and n_dev < args.gpus:
         raise SystemExit(f"bench.py: --gpus {args.gpus} needs {args.gpus} visible GPUs, found {n_dev} "
                          f"(KDFM_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs)")
@@ -416,7 +466,7 @@ def main():
             threads = args.cpu_threads or _usable_cpus()
             cpu = cpu_baseline(threads, args.samples)
             cpu["cgroup_cpu_max"] = _cgroup_cpu_max()
-        f32 = v1024 = encfm = None
+        f32 = v1024 = encfm = xl = None
         if not args.no_f32_sensitivity and cfg.math == "bf16" and world == 1:
             _progress("f32 sensitivity")
             f32 = sensitivity(dev, args.samples, math="f32")
@@ -427,6 +477,11 @@ def main():
             encfm = sensitivity(dev, args.samples, kd_model="encfm")
             encfm["note"] = ("the asr_train.py model family on the same workload: router + flow matching on every "
                              "hooked layer pair instead of the ver5 latent heads; not the headline value")
+            _progress("FastConformer-XL shape sensitivity")
+            xl = sensitivity(dev, args.samples, **XL_SHAPES)
+            xl["note"] = ("BASELINE.json configs[4]'s layer shapes (FastConformer-XL: d_model 1024, 8 heads, head dim "
+                          "128, 24 layers, dw_striding x8, kernel 9, no xscaling) for student and teacher on the same "
+                          "16 s x B=32 workload, bf16 (fp8 is not built); not the headline value")
         line = {
             "metric": "utterances/sec (FM-distill train step, Conformer-CTC-small) at 1/2/4/8 MI355X",
             "value": round(utt, 3),
@@ -465,6 +520,7 @@ def main():
             "f32_sensitivity": f32,
             "vocab_1024_sensitivity": v1024,
             "encoder_fm_router_sensitivity": encfm,
+            "xl_shape_sensitivity": xl,
             "losses_last_step": [round(x, 5) for x in losses],
         }
         print(json.dumps(line))

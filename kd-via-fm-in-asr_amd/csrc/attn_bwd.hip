@@ -123,7 +123,7 @@ __device__ __forceinline__ void fetch_rows(float4 (&v)[MAXI], const float* src, 
     v[it] = ok ? *reinterpret_cast<const float4*>(src + (base_row + r) * ld + c0 + c4) : make_float4(0.f, 0.f, 0.f, 0.f);
   }
 }
-template <int MAXI>
+template <int MAXI, int LDR = LR>
 __device__ __forceinline__ void put_rows(uint16_t* rc, uint16_t* cr, int ldt, const float4 (&v)[MAXI], int n, int dk) {
   const int cq = dk >> 2;
 #pragma unroll
@@ -131,7 +131,7 @@ __device__ __forceinline__ void put_rows(uint16_t* rc, uint16_t* cr, int ldt, co
     const int e = threadIdx.x + it * 256;
     if (e >= n * cq) continue;
     const int rr = e / cq, c4 = (e - rr * cq) * 4;
-    if (rc) st4(rc + rr * LR + c4, v[it]);
+    if (rc) st4(rc + rr * LDR + c4, v[it]);
     if (cr) {
       cr[(c4 + 0) * ldt + rr] = f2bf(v[it].x);
       cr[(c4 + 1) * ldt + rr] = f2bf(v[it].y);
@@ -166,9 +166,10 @@ __device__ __forceinline__ void zero_pad(uint16_t* img, int rows, int dk, int z0
 
 // zero a whole [rows][LR] image with 16-byte stores (the bwd2 kernels: a superset of zero_pad -- the data
 // columns of rows below z0 are rewritten by put_rows after a barrier -- without its per-element divisions)
+template <int LDR = LR>
 __device__ __forceinline__ void zero_img(uint16_t* img, int rows) {
-  static_assert((LR * 2) % 16 == 0, "row stride must be a multiple of 16 bytes");
-  for (int e = threadIdx.x; e < rows * LR / 8; e += 256) reinterpret_cast<uint4*>(img)[e] = make_uint4(0u, 0u, 0u, 0u);
+  static_assert((LDR * 2) % 16 == 0, "row stride must be a multiple of 16 bytes");
+  for (int e = threadIdx.x; e < rows * LDR / 8; e += 256) reinterpret_cast<uint4*>(img)[e] = make_uint4(0u, 0u, 0u, 0u);
 }
 
 // r[(b*H + h)*T + i] = sum_c dO[b*T + i][h*dk + c] * O[b*T + i][h*dk + c]; one wave per (row, head)
@@ -190,16 +191,21 @@ __global__ __launch_bounds__(256) void attn_rowdot_kernel(const float* __restric
 // kernel 1: dQu, dQv
 // ---------------------------------------------------------------------------------------------
 // RIN: the row sums r_i are formed in the prologue from dO and O (p.O) instead of read from p.rsum
+// NU = 8 (head dim <= 128, FastConformer-XL): the head dim is padded to 4 MFMA k-steps (KS) instead of 2
 template <int NU, bool SAVE = false, bool RIN = false>
 __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dq_kernel(AbP p) {
-  __shared__ __attribute__((aligned(16))) uint16_t Ks[BK * LR];     // K block [key][c]
-  __shared__ __attribute__((aligned(16))) uint16_t Vs[BK * LR];     // V block [key][c]
-  __shared__ __attribute__((aligned(16))) uint16_t Pr[PB1 * LR];    // Ppos band [band row][c]
+  constexpr int KS = NU > 4 ? 4 : 2;
+  constexpr int DKP = 32 * KS;
+  constexpr int LRK = DKP + 8;
+  static_assert(SAVE || KS == 2, "the pre-bwd2 path covers head dims <= 64 only");
+  __shared__ __attribute__((aligned(16))) uint16_t Ks[BK * LRK];     // K block [key][c]
+  __shared__ __attribute__((aligned(16))) uint16_t Vs[BK * LRK];     // V block [key][c]
+  __shared__ __attribute__((aligned(16))) uint16_t Pr[PB1 * LRK];    // Ppos band [band row][c]
   __shared__ __attribute__((aligned(16))) float Wsc[4][WS1 / 4];    // per-wave scratch
   // SAVE (bwd2): per wave Pd tile [16][LW] bf16; dS and Pd leave as 16-byte buffer stores (fixed count per
   // lane and key block, out-of-range chunks dropped by the range check)
   __shared__ __attribute__((aligned(16))) uint16_t Pdw[SAVE ? 4 : 1][SAVE ? 16 * LW : 8];
-  __shared__ __attribute__((aligned(16))) float Cn[2][64];   // the forward's key / value centre (attn_centre.h)
+  __shared__ __attribute__((aligned(16))) float Cn[2][DKP];   // the forward's key / value centre (attn_centre.h)
 
   KPROBE(0);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -213,9 +219,9 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dq_kernel(AbP p
   const int npos = 2 * T - 1;
   const int64_t hoff = h * p.dkh;
   if constexpr (SAVE) {
-    zero_img(Ks, BK);
-    zero_img(Vs, BK);
-    zero_img(Pr, PB1);
+    zero_img<LRK>(Ks, BK);
+    zero_img<LRK>(Vs, BK);
+    zero_img<LRK>(Pr, PB1);
   } else {
     zero_pad(Ks, BK, dk, BK);
     zero_pad(Vs, BK, dk, BK);
@@ -224,9 +230,9 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dq_kernel(AbP p
 
   // this lane's query row (A-fragment row): Qu, Qv and dO fragments
   const int iq = i0 + w * 16 + (lane & 15);
-  bf16x8 fu[2], fv[2], fdo[2];
+  bf16x8 fu[KS], fv[KS], fdo[KS];
 #pragma unroll
-  for (int ks = 0; ks < 2; ++ks) {
+  for (int ks = 0; ks < KS; ++ks) {
     const int c0 = ks * 32 + 8 * (lane >> 4);
     const int valid = iq < T ? dk - c0 : 0;
     const int64_t off = (b * p.T + (iq < T ? iq : 0)) * p.ldq + hoff;
@@ -275,7 +281,7 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dq_kernel(AbP p
 
   // the forward's centring (attn_centre.h): K rows staged as K_j - kc (the scores, hence P = exp(s - lse),
   // are the forward's), V rows as V_j - vc with cs_i = dO_i . vc added back to dPd in f32
-  kv_centre(p.k + b * p.T * p.ldkv + hoff, p.v + b * p.T * p.ldkv + hoff, p.ldkv, len, dk, Cn);
+  kv_centre<DKP>(p.k + b * p.T * p.ldkv + hoff, p.v + b * p.T * p.ldkv + hoff, p.ldkv, len, dk, Cn);
   // cs_i for this lane's C-layout rows: row (lane & 15) of the wave's 16 dotted in f32 by its 4 lane groups
   // (16 columns each), summed across them, then picked up by the lanes owning each row.  With RIN (bwd2)
   // the row sums r_i = dO_i . O_i are formed the same way here instead of by attn_rowdot_kernel
@@ -287,8 +293,8 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dq_kernel(AbP p
       const float* dor = p.dO + (b * p.T + iq) * p.ldq + hoff;
       const float* orow = p.O + (b * p.T + iq) * p.ldq + hoff;
 #pragma unroll
-      for (int c4 = 0; c4 < 4; ++c4) {
-        const int c = 16 * q + 4 * c4;
+      for (int c4 = 0; c4 < DKP / 16; ++c4) {
+        const int c = (DKP / 4) * q + 4 * c4;
         if (c < dk) {
           const float4 g = *reinterpret_cast<const float4*>(dor + c);
           part += g.x * Cn[1][c] + g.y * Cn[1][c + 1] + g.z * Cn[1][c + 2] + g.w * Cn[1][c + 3];
@@ -346,9 +352,9 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dq_kernel(AbP p
     __syncthreads();
     centre(nk, Cn[0], j0);
     centre(nv, Cn[1], j0);
-    put_rows<NU>(Vs, nullptr, 0, nv, BK, dk);
-    put_rows<NU>(Ks, nullptr, 0, nk, BK, dk);
-    put_rows<2 * NU>(Pr, nullptr, 0, nb, 127, dk);
+    put_rows<NU, LRK>(Vs, nullptr, 0, nv, BK, dk);
+    put_rows<NU, LRK>(Ks, nullptr, 0, nk, BK, dk);
+    put_rows<2 * NU, LRK>(Pr, nullptr, 0, nb, 127, dk);
     __syncthreads();
     if (kb + 1 < nkb) fetch(kb + 1);
     KPROBE(2 + 4 * kb);
@@ -361,16 +367,16 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dq_kernel(AbP p
 #pragma unroll
       for (int t = 0; t < 5; ++t) g[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
+      for (int ks = 0; ks < KS; ++ks) {
         const int kof = ks * 32 + 8 * (lane >> 4);
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
-          const bf16x8 kbf = *reinterpret_cast<const bf16x8*>(Ks + (16 * t + (lane & 15)) * LR + kof);
+          const bf16x8 kbf = *reinterpret_cast<const bf16x8*>(Ks + (16 * t + (lane & 15)) * LRK + kof);
           ac[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fu[ks], kbf, ac[t], 0, 0, 0);
         }
 #pragma unroll
         for (int t = 0; t < 5; ++t) {
-          const bf16x8 pb = *reinterpret_cast<const bf16x8*>(Pr + (wb + 16 * t + (lane & 15)) * LR + kof);
+          const bf16x8 pb = *reinterpret_cast<const bf16x8*>(Pr + (wb + 16 * t + (lane & 15)) * LRK + kof);
           g[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fv[ks], pb, g[t], 0, 0, 0);
         }
       }
@@ -399,10 +405,10 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dq_kernel(AbP p
 #pragma unroll
     for (int t = 0; t < 4; ++t) a[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
+    for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
-        const bf16x8 vb = *reinterpret_cast<const bf16x8*>(Vs + (16 * t + (lane & 15)) * LR + ks * 32 + 8 * (lane >> 4));
+        const bf16x8 vb = *reinterpret_cast<const bf16x8*>(Vs + (16 * t + (lane & 15)) * LRK + ks * 32 + 8 * (lane >> 4));
         a[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fdo[ks], vb, a[t], 0, 0, 0);
       }
     for (int e = lane; e < 16 * LG / 2; e += 64) reinterpret_cast<uint32_t*>(Gk)[e] = 0u;
@@ -451,7 +457,7 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dq_kernel(AbP p
     for (int ks = 0; ks < 2; ++ks) {
       const bf16x8 da = *reinterpret_cast<const bf16x8*>(D + (lane & 15) * LW + ks * 32 + 8 * (lane >> 4));
 #pragma unroll
-      for (int u = 0; u < NU; ++u) aq[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, tr_frag(Ks, LR, ks * 32, 16 * u, lane),
+      for (int u = 0; u < NU; ++u) aq[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, tr_frag(Ks, LRK, ks * 32, 16 * u, lane),
                                                                                 aq[u], 0, 0, 0);
     }
 #pragma unroll
@@ -459,7 +465,7 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dq_kernel(AbP p
       const bf16x8 ga = *reinterpret_cast<const bf16x8*>(Gk + (lane & 15) * LG + ks * 32 + 8 * (lane >> 4));
 #pragma unroll
       for (int u = 0; u < NU; ++u)
-        av[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ga, tr_frag(Pr, LR, wb + ks * 32, 16 * u, lane), av[u], 0, 0, 0);
+        av[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ga, tr_frag(Pr, LRK, wb + ks * 32, 16 * u, lane), av[u], 0, 0, 0);
     }
     wsync();
     KPROBE(5 + 4 * kb);
@@ -800,8 +806,9 @@ __global__ __launch_bounds__(256) void attn_dpos_fold_kernel(const float* __rest
 // ---------------------------------------------------------------------------------------------
 template <int NU>
 __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dkv2_kernel(AbP p) {
-  __shared__ __attribute__((aligned(16))) uint16_t Os[BQ * LR];     // dO block [query][c]
-  __shared__ __attribute__((aligned(16))) uint16_t Qs[BQ * LR];     // Qu block [query][c]
+  constexpr int LRK = 32 * (NU > 4 ? 4 : 2) + 8;   // row stride of the [query][c] images (head dim padded)
+  __shared__ __attribute__((aligned(16))) uint16_t Os[BQ * LRK];     // dO block [query][c]
+  __shared__ __attribute__((aligned(16))) uint16_t Qs[BQ * LRK];     // Qu block [query][c]
   __shared__ __attribute__((aligned(16))) uint16_t Pq[BQ * LW];     // Pd block [query][key]
   __shared__ __attribute__((aligned(16))) uint16_t Dq[BQ * LW];     // dS block [query][key]
 
@@ -813,8 +820,8 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dkv2_kernel(AbP
   const int j0 = (int)blk.x * BK;
   const int len = p.lens ? (int)min<int64_t>(p.lens[b], p.T) : T;
   const int64_t hoff = h * p.dkh;
-  zero_img(Os, BQ);
-  zero_img(Qs, BQ);
+  zero_img<LRK>(Os, BQ);
+  zero_img<LRK>(Qs, BQ);
   const int sbytes = (int)(p.B * p.H * p.T * p.ldt * 2);
   const __amdgpu_buffer_rsrc_t rds = __builtin_amdgcn_make_buffer_rsrc((void*)p.ds, (short)0, sbytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rpd = __builtin_amdgcn_make_buffer_rsrc((void*)p.pdo, (short)0, sbytes, 0x00020000);
@@ -843,8 +850,8 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dkv2_kernel(AbP
   if (nqb > 0) fetch(0);
   for (int qb = 0; qb < nqb; ++qb) {
     __syncthreads();
-    put_rows<NU>(Os, nullptr, 0, ndo, BQ, dk);
-    put_rows<NU>(Qs, nullptr, 0, nqu, BQ, dk);
+    put_rows<NU, LRK>(Os, nullptr, 0, ndo, BQ, dk);
+    put_rows<NU, LRK>(Qs, nullptr, 0, nqu, BQ, dk);
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       const int c = threadIdx.x + 256 * q, row = c >> 3, c8 = c & 7;
@@ -859,8 +866,8 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dkv2_kernel(AbP
       const bf16x8 da = tr_frag(Dq, LW, ks * 32, 16 * w, lane);
 #pragma unroll
       for (int u = 0; u < NU; ++u) {
-        adv[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, tr_frag(Os, LR, ks * 32, 16 * u, lane), adv[u], 0, 0, 0);
-        adk[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, tr_frag(Qs, LR, ks * 32, 16 * u, lane), adk[u], 0, 0, 0);
+        adv[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, tr_frag(Os, LRK, ks * 32, 16 * u, lane), adv[u], 0, 0, 0);
+        adk[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, tr_frag(Qs, LRK, ks * 32, 16 * u, lane), adk[u], 0, 0, 0);
       }
     }
   }
@@ -886,7 +893,8 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dkv2_kernel(AbP
 template <int NU>
 __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dpos2_kernel(AbP p) {
   __shared__ __attribute__((aligned(16))) uint16_t Dl[NPQ * LDL];    // dS [i - ib0][j - jbase]
-  __shared__ __attribute__((aligned(16))) uint16_t Qt[BDK * LQ3];    // Qv^T [c][i - ib0]
+  constexpr int DKP = 32 * (NU > 4 ? 4 : 2);
+  __shared__ __attribute__((aligned(16))) uint16_t Qt[DKP * LQ3];    // Qv^T [c][i - ib0]
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int T = (int)p.T, dk = (int)p.dkh;
@@ -896,7 +904,7 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dpos2_kernel(Ab
   const int64_t h = blk.y;
   const int64_t bchunk = blk.z;
   const int64_t hoff = h * p.dkh;
-  for (int e = threadIdx.x; e < (BDK - dk) * LQ3; e += 256) Qt[dk * LQ3 + e] = 0;
+  for (int e = threadIdx.x; e < (DKP - dk) * LQ3; e += 256) Qt[dk * LQ3 + e] = 0;
   f32x4 acc[NU];
 #pragma unroll
   for (int u = 0; u < NU; ++u) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -1075,7 +1083,7 @@ int ab2_setup(AbP& p, const float* qu, const float* qv, const float* qkv, const 
               uint64_t rng_stream) {
   KDFM_REQUIRE(H > 0 && d % H == 0, "d must be a multiple of H");
   const int64_t dk = d / H;
-  KDFM_REQUIRE(dk <= 64 && dk % 4 == 0, "head dim must be a multiple of 4 and <= 64");
+  KDFM_REQUIRE(dk <= 128 && dk % 4 == 0, "head dim must be a multiple of 4 and <= 128");
   KDFM_REQUIRE(T > 0 && T <= 4096 && d % 4 == 0, "bad T / d");
   KDFM_REQUIRE(dropout_p == 0.f || seed, "dropout needs a seed");
   KDFM_REQUIRE(B * H * T * kdfm_relpos_attn_bwd2_ldt(T) * 2 < (1ll << 31), "dS / Pd larger than 2 GiB (buffer offsets)");
@@ -1106,7 +1114,9 @@ int kdfm_relpos_attn_bwd2_dq(const float* dO, const float* O, const float* qu, c
   if (rc || B == 0) return rc;
   p.dO = dO; p.pos = pos; p.rsum = rsum; p.dqu = dqu; p.dqv = dqv; p.ds = ds; p.pdo = pd; p.O = O;
   hipStream_t st = as_stream(stream);
-  if (p.dkh > 48)
+  if (p.dkh > 64)
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<8, true, true>), dim3((unsigned)ceil_div(T, BQ), (unsigned)(B * H)), dim3(256), 0, st, p);
+  else if (p.dkh > 48)
     hipLaunchKernelGGL((attn_bwd_dq_kernel<4, true, true>), dim3((unsigned)ceil_div(T, BQ), (unsigned)(B * H)), dim3(256), 0, st, p);
   else
     hipLaunchKernelGGL((attn_bwd_dq_kernel<3, true, true>), dim3((unsigned)ceil_div(T, BQ), (unsigned)(B * H)), dim3(256), 0, st, p);
@@ -1126,7 +1136,9 @@ int kdfm_relpos_attn_bwd2_dkv(const float* dO, const float* qu, const uint16_t* 
   p.dO = dO; p.ds = const_cast<uint16_t*>(ds); p.pdo = const_cast<uint16_t*>(pd);
   p.dk = dqkv + d; p.dv = dqkv + 2 * d;
   hipStream_t st = as_stream(stream);
-  if (p.dkh > 48)
+  if (p.dkh > 64)
+    hipLaunchKernelGGL(attn_bwd_dkv2_kernel<8>, dim3((unsigned)ceil_div(T, BK), (unsigned)(B * H)), dim3(256), 0, st, p);
+  else if (p.dkh > 48)
     hipLaunchKernelGGL(attn_bwd_dkv2_kernel<4>, dim3((unsigned)ceil_div(T, BK), (unsigned)(B * H)), dim3(256), 0, st, p);
   else
     hipLaunchKernelGGL(attn_bwd_dkv2_kernel<3>, dim3((unsigned)ceil_div(T, BK), (unsigned)(B * H)), dim3(256), 0, st, p);
@@ -1145,7 +1157,10 @@ int kdfm_relpos_attn_bwd2_dpos(const float* qv, const uint16_t* ds, const int64_
   const int chunks = (int)(B < DPOS_MAX_CHUNKS ? B : DPOS_MAX_CHUNKS);
   const int64_t npos = 2 * T - 1;
   hipStream_t st = as_stream(stream);
-  if (p.dkh > 48)
+  if (p.dkh > 64)
+    hipLaunchKernelGGL(attn_bwd_dpos2_kernel<8>, dim3((unsigned)ceil_div(npos, 64), (unsigned)H, (unsigned)chunks),
+                       dim3(256), 0, st, p);
+  else if (p.dkh > 48)
     hipLaunchKernelGGL(attn_bwd_dpos2_kernel<4>, dim3((unsigned)ceil_div(npos, 64), (unsigned)H, (unsigned)chunks),
                        dim3(256), 0, st, p);
   else

@@ -12,11 +12,13 @@
 
 namespace kdfm {
 
-// c[0][0..dk) = kc, c[1][0..dk) = vc (zeros for an empty utterance).  Every thread of the block must call
-// it (ends with a barrier); rows are summed in order by one thread per float4 column group, so the forward
-// and the backward compute the same bits.
+// c[0][0..dk) = kc, c[1][0..dk) = vc (zeros for an empty utterance); W >= dk is the centre table's width
+// (the kernel's padded head dim).  Every thread of the block must call it (ends with a barrier); rows are
+// summed in order by one thread per float4 column group, so the forward and the backward compute the same
+// bits.
+template <int W>
 __device__ __forceinline__ void kv_centre(const float* kbase, const float* vbase, int64_t ld, int len, int dk,
-                                          float (*c)[64]) {
+                                          float (*c)[W]) {
   const int cq = dk >> 2;
   const int t = threadIdx.x;
   if (t < 2 * cq) {

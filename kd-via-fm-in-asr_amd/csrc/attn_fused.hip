@@ -31,8 +31,6 @@ namespace {
 
 constexpr int AQ = 64;            // query rows per workgroup (4 waves x 16)
 constexpr int AKB = 64;           // keys per block
-constexpr int DKP = 64;           // head dim padded to 2 MFMA k-steps
-constexpr int LDR = DKP + 8;      // bf16 row stride of the [row][c] tiles (K, P band)
 constexpr int LDVT = AKB + 8;     // bf16 row stride of V^T [c][key]
 constexpr int LDPS = AKB + 8;     // bf16 row stride of the per-wave P tile [row][key]
 constexpr int BAND = 128;         // P rows staged per key block (127 used)
@@ -92,18 +90,22 @@ __device__ __forceinline__ float group16_sum(float v) {
   return v + dppmov<0x140>(v);
 }
 
-// NU: 16-column output tiles of the head dim (3: dk <= 48, 4: dk <= 64); WPT (single pass): p~ and m_blk
+// NU: 16-column output tiles of the head dim (3: dk <= 48, 4: dk <= 64, 8: dk <= 128 -- FastConformer-XL's
+// 1024 / 8 heads); the head dim is padded to KS MFMA k-steps of 32 (2, or 4 for NU = 8); WPT (single pass): p~ and m_blk
 // are written -- through buffer stores whose out-of-range lanes carry an offset past the buffer (dropped
 // by the range check) instead of a branch, so each key block issues a fixed number of stores and the
 // wait for the next block's staged loads counts past them instead of draining them (vmcnt(0))
 template <bool TWO_PASS, int NU, bool WPT = false>
 __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void relpos_attn_fwd_kernel(AttnP p) {
+  constexpr int KS = NU > 4 ? 4 : 2;   // MFMA k-steps over the padded head dim
+  constexpr int DKP = 32 * KS;         // head dim padded
+  constexpr int LDR = DKP + 8;         // bf16 row stride of the [row][c] tiles (K, P band)
   __shared__ __attribute__((aligned(16))) uint16_t Ks[AKB * LDR];
   __shared__ __attribute__((aligned(16))) uint16_t Vt[DKP * LDVT];
   __shared__ __attribute__((aligned(16))) uint16_t Pr[BAND * LDR];
   __shared__ __attribute__((aligned(16))) float Gs[4][16 * LDG];
   __shared__ __attribute__((aligned(16))) uint16_t Ps[4][16 * LDPS];
-  __shared__ __attribute__((aligned(16))) float Cn[2][64];   // key / value centre (attn_centre.h)
+  __shared__ __attribute__((aligned(16))) float Cn[2][DKP];   // key / value centre (attn_centre.h)
 
   KPROBE(0);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -132,9 +134,9 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void relpos_attn_fwd_kernel(A
 
   // this lane's query row (A-fragment row) and its Qu / Qv fragments
   const int iq = i0 + w * 16 + (lane & 15);
-  bf16x8 fu[2], fv[2];
+  bf16x8 fu[KS], fv[KS];
 #pragma unroll
-  for (int ks = 0; ks < 2; ++ks) {
+  for (int ks = 0; ks < KS; ++ks) {
     const int c0 = ks * 32 + 8 * (lane >> 4);
     const int valid = (iq < T) ? dk - c0 : 0;
     const int64_t off = (b * p.T + (iq < T ? iq : 0)) * p.ldq + hoff;
@@ -239,7 +241,7 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void relpos_attn_fwd_kernel(A
     for (int t = 0; t < 5; ++t) g[t] = f32x4{0.f, 0.f, 0.f, 0.f};
     const int wb = 48 - 16 * w;  // this wave's band offset inside Pr
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
+    for (int ks = 0; ks < KS; ++ks) {
       const int kof = ks * 32 + 8 * (lane >> 4);
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
@@ -274,7 +276,7 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void relpos_attn_fwd_kernel(A
   // (the first stage's loads are issued before the centre: they are raw rows, centred at store time)
   if (TWO_PASS && nkb > 0) load_stage(0, false);
   if (!TWO_PASS && nkb > 0) load_stage(0, true);
-  kv_centre(kbase, vbase, p.ldkv, min(len, T), dk, Cn);
+  kv_centre<DKP>(kbase, vbase, p.ldkv, min(len, T), dk, Cn);
   if constexpr (WPT) {
     // the loop body leaves its 4 m_blk + 16 p~ stores behind the next block's loads; the same number of
     // (range-dropped) stores behind the first block's loads lets the compiler's wait for a staged load
@@ -478,7 +480,9 @@ extern "C" int kdfm_relpos_attn_fwd(const float* qu, const float* qv, const floa
   KDFM_REQUIRE(qu && qv && qkv && pos && o, "null pointer");
   KDFM_REQUIRE(H > 0 && d % H == 0, "d must be a multiple of H");
   const int64_t dk = d / H;
-  KDFM_REQUIRE(dk <= 64 && dk % 4 == 0, "head dim must be a multiple of 4 and <= 64");
+  KDFM_REQUIRE(dk <= 128 && dk % 4 == 0, "head dim must be a multiple of 4 and <= 128");
+  KDFM_REQUIRE(dk <= 64 || !(P || Pdrop || p_tilde || m_blk),
+               "head dims > 64: single-pass forward with lse only (the bwd2 backward's form)");
   KDFM_REQUIRE(T > 0 && T <= 4096, "T out of range");
   KDFM_REQUIRE(d % 4 == 0, "d must be a multiple of 4");
   KDFM_REQUIRE(dropout_p == 0.f || seed, "dropout needs a seed");
@@ -493,7 +497,9 @@ extern "C" int kdfm_relpos_attn_fwd(const float* qu, const float* qv, const floa
   dim3 grid((unsigned)ceil_div(T, AQ), (unsigned)(B * H));
   const bool two = P || Pdrop, wide = dk > 48;
   KDFM_REQUIRE(!p_tilde || B * H * T * T * 2 <= (int64_t)INT32_MAX, "p~ exceeds the 2 GB buffer-offset range");
-  if (!two && p_tilde && !wide)
+  if (dk > 64)
+    hipLaunchKernelGGL((relpos_attn_fwd_kernel<false, 8>), grid, dim3(256), 0, as_stream(stream), p);
+  else if (!two && p_tilde && !wide)
     hipLaunchKernelGGL((relpos_attn_fwd_kernel<false, 3, true>), grid, dim3(256), 0, as_stream(stream), p);
   else if (!two && p_tilde)
     hipLaunchKernelGGL((relpos_attn_fwd_kernel<false, 4, true>), grid, dim3(256), 0, as_stream(stream), p);

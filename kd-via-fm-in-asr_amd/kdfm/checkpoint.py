@@ -46,6 +46,14 @@ def engine_state_dict(eng, *, teacher: bool = True, frontend: bool = True) -> "O
     # the student's BatchNorm layers saw one batch-statistics update per optimizer step; the frozen
     # teacher's counters are whatever was loaded (its BN runs on running statistics and never counts)
     nbt = torch.tensor(int(eng.step.item()), dtype=torch.int64)
+    # the conformer FM meta-encoder's BatchNorms run once per meta-encoder CALL: sum(S_i) calls per step
+    # (asr_train.py:1320-1336 loops the meta-encoder over every sampling step of every hooked layer), so the
+    # reference's counter advances by that much per optimizer step
+    meta_calls = 1
+    cfg = getattr(eng, "cfg", None)
+    if cfg is not None and getattr(cfg, "kd_model", None) == "encfm" and getattr(cfg, "encfm_meta", None) == "conformer":
+        from .config import encfm_fixed_steps
+        meta_calls = int(sum(encfm_fixed_steps(cfg)))
     loaded_nbt = getattr(eng, "bn_batches_tracked", {})
     for name, _ in eng.student.specs:
         sd[name] = eng.student.P[name].detach().cpu().clone()
@@ -62,6 +70,8 @@ def engine_state_dict(eng, *, teacher: bool = True, frontend: bool = True) -> "O
                 key = name[:-len("running_var")] + "num_batches_tracked"
                 if name.startswith("teacher."):
                     sd[key] = loaded_nbt.get(key, torch.tensor(0, dtype=torch.int64)).clone()
+                elif name.startswith("flow_matching.meta_encoder."):
+                    sd[key] = nbt * meta_calls
                 else:
                     sd[key] = nbt.clone()
     if teacher:

@@ -40,6 +40,17 @@ _ATTN_BWD2 = __import__("os").environ.get("KDFM_ATTN_BWD2", "1") == "1"
 _WGRAD_PAIRS = __import__("os").environ.get("KDFM_WGRAD_PAIRS", "1") == "1"
 
 
+def _attn_fused_ok(dk, save):
+    """bf16 math: the fused rel-pos attention (csrc/attn_fused.hip, attn_bwd.hip).  Head dims <= 64 in every
+    backward form; up to 128 (FastConformer-XL: d_model 1024 / 8 heads) with the bwd2 backward, whose forward
+    keeps only the per-row log-sum-exp."""
+    if K.get_math() != "bf16":
+        return False
+    if dk <= 64:
+        return True
+    return dk <= 128 and (not save or (_ATTN_BWD_FUSED and _ATTN_BWD2))
+
+
 def _stream(salt, layer, site):
     return salt * 4096 + (layer + 1) * 16 + site
 
@@ -452,7 +463,7 @@ def layer_forward(cfg, S: EncoderShapes, P, L, li, x, out, pos_emb, lengths, *, 
         ppos = _empty(npos, d, dev=dev)
         K.linear(pos_emb, P[L + "self_attn.linear_pos.weight"], None, ppos)
     o = _empty(rows, d, dev=dev)
-    if K.get_math() == "bf16" and dk <= 64:
+    if _attn_fused_ok(dk, save):
         # fused flash-style kernel: no AC / BD materialisation; P (and P_drop) only when the
         # backward needs them
         if _ATTN_BWD_FUSED:
@@ -498,7 +509,7 @@ def layer_forward(cfg, S: EncoderShapes, P, L, li, x, out, pos_emb, lengths, *, 
     else:
         K.linear(o, P[L + "self_attn.linear_out.weight"], P[L + "self_attn.linear_out.bias"], x2, epi=_lib.EPI_RESID,
                  R=x1, rscale=1.0, dropout_p=pd, seed=seed, rng_stream=_stream(salt, li, SITE_ATT_OUT))
-    fused_attn = K.get_math() == "bf16" and dk <= 64 and _ATTN_BWD_FUSED
+    fused_attn = _attn_fused_ok(dk, save) and _ATTN_BWD_FUSED
     keep(x1=x1, ln2=ln2, m2=m2, r2=r2, qkv=qkv, qu=qu, qv=qv, ppos=ppos, P=Pm, Pd=Pd, o=o, o_h=o_h, pa=pa,
          attn_fused=fused_attn, lse=lse if fused_attn else None, pt=pt if fused_attn else None,
          mblk=mblk if fused_attn else None)

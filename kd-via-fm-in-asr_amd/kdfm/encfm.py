@@ -135,6 +135,8 @@ def encfm_forward(cfg, P, sfeats, tfeats, ws: EncFMWorkspace, *, seed=None, trai
            K.ptr(P[fm + "shape_transformation_function.bias"]), ws.ca, ws.cv, Kmax,
            K.ptr(ws.X) if train else None, K.ptr(ws.A) if train else None, K.ptr(ws.nsx), K.ptr(ws.dtr),
            K.ptr(ws.xS), (L - 1) * B * T, K.ptr(ws.flow), L, B, T, Cs, Ct, K._s())
+    if not train:   # the reference's flow loss is 0.0 outside training (asr_train.py:1363-1364)
+        K.fill(ws.flow, 0.0)
     K.colsum(ws.flow.view(L, 1), ws.stats[0:1], accumulate=False)
     K.colsum(ws.rloss.view(L, 1), ws.stats[1:2], scale=cfg.router_weight, accumulate=False)
     K.colsum(ws.stats[0:2].view(2, 1), ws.stats[2:3], accumulate=False)

@@ -163,8 +163,13 @@ class Ver5Engine:
         return self._pos[key]
 
     def _encfm_ws(self, B, T):
+        """The encoder-level FM workspace for this batch shape.  Only the CURRENT shape is cached: a meta-encoder
+        workspace holds every step's saved activations (GBs at the bench shape), so one per padded length would
+        grow without bound over a real run; a new (B, T) drops the previous one (the allocator
+        reuses its blocks: the previous step's streams were joined before this forward)."""
         ws = self._encfm.get((B, T))
         if ws is None:
+            self._encfm.clear()
             if self.cfg.encfm_meta != "mlp":
                 from .fmmeta import MetaFMWorkspace
                 ws = self._encfm[(B, T)] = MetaFMWorkspace(self.cfg, B, T, self.device)

@@ -158,7 +158,9 @@ def _meta_bwd(ws, P, G, nm, k, dv, dembed, seed=None):
 
 def meta_forward(cfg, P, sfeats, tfeats, ws: MetaFMWorkspace, *, seed=None, bn_running=None, train=True):
     """All layers' FM chains.  sfeats (L, B*T, Cs) / tfeats (L, B*T, Ct) hook outputs; returns ws.xS, the
-    last layer's FM output.  ws.stats = [sum of flow losses, 0, total, mean steps] as encfm_forward."""
+    last layer's FM output.  ws.stats = [sum of flow losses, 0, total, mean steps] as encfm_forward.
+    train=False: only the chains and x_S -- the flow losses are 0 as the reference's eval forward returns
+    (asr_train.py:1363-1364), and noise_scheduled_x / the MSE / its gradient are not computed."""
     L, Cs, E, n = cfg.n_layers, cfg.d_student, cfg.time_embed_dim, ws.n
     fm = "flow_matching."
     nm = _names(ws.meta)
@@ -183,6 +185,8 @@ def meta_forward(cfg, P, sfeats, tfeats, ws: MetaFMWorkspace, *, seed=None, bn_r
         last = ws.embed[b0 + S - 1][:, :Cs]
         if i == L - 1:
             K.axpby(last, ws.vl, ws.xS, 1.0, -1.0 / S)
+        if not train:   # the reference's loss is 0.0 outside training (asr_train.py:1363-1364): no nsx / MSE
+            continue
         K.axpby(s_i, ws.vl, ws.nsx[i], ws.ca[i], ws.cv[i])              # noise_scheduled_x (:1366-1367)
         K.linear(ws.nsx[i], Wst, bst, ws.dtr[i], R=tfeats[i].view(n, -1), rscale=2.0 * ws.inv,
                  mse=(ws.flow[i:i + 1], ws.inv))                           # MSELoss and its gradient

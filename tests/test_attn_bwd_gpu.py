@@ -301,3 +301,73 @@ def test_attn_bwd2_common_mode_keys_values(p):
         assert _rel(o, o_ref) <= 1e-2, _rel(o, o_ref)
     for name, a, w in zip(("dQu", "dQv", "dK", "dV", "dPpos"), got, ref):
         assert _rel(a, w) <= 2e-2, (name, _rel(a, w))
+
+
+def _torch_o_grads_masked(qkv, qu, qv, ppos, do, lens, B, H, T, d, keep, p):
+    """float64 autograd of the attention with a given dropout keep mask (B, H, T, T) applied to P
+    (Pd = P * keep / (1 - p)): O and the five input gradients."""
+    dk = d // H
+    f = lambda t: t.double().detach().clone().requires_grad_(True)  # noqa: E731
+    q_u, q_v, k, v, pp = f(qu), f(qv), f(qkv[:, d:2 * d]), f(qkv[:, 2 * d:]), f(ppos)
+    sh = lambda t: t.view(B, T, H, dk).permute(0, 2, 1, 3)  # noqa: E731
+    ac = sh(q_u) @ sh(k).transpose(-1, -2)
+    bdf = torch.einsum("bhic,hrc->bhir", sh(q_v), pp.view(2 * T - 1, H, dk).permute(1, 0, 2))
+    idx = (T - 1 - torch.arange(T, device="cuda")[:, None] + torch.arange(T, device="cuda")[None, :])
+    bd = torch.gather(bdf, 3, idx.expand(B, H, T, T))
+    s = (ac + bd) / math.sqrt(dk)
+    keym = torch.arange(T, device="cuda")[None, :] < lens[:, None]
+    s = s.masked_fill(~keym[:, None, None, :], float("-inf"))
+    P = torch.softmax(s, -1)
+    P = torch.where(keym[:, None, :, None], P, torch.zeros_like(P))
+    if keep is not None:
+        P = P * keep.double() / (1.0 - p)
+    O = (P @ sh(v)).permute(0, 2, 1, 3).reshape(B * T, d)
+    loss = (O * do.double()).sum()
+    return O.detach(), torch.autograd.grad(loss, [q_u, q_v, k, v, pp])
+
+
+@pytest.mark.parametrize("B,H,T,d,p,kcm", [
+    # FastConformer-XL (fast-conformer_ctc_bpe.yaml:29: d_model 1024, 8 heads -> head dim 128)
+    (2, 8, 201, 1024, 0.0, 0.0),
+    (2, 8, 201, 1024, 0.1, 0.0),
+    (2, 8, 130, 1024, 0.0, 3.0),   # keys / values with a shared per-channel offset (attn_centre.h)
+    (3, 1, 401, 128, 0.0, 0.0),    # one head, the benchmark's 401 frames, ragged lengths
+    (2, 2, 77, 192, 0.1, 0.0),     # head dim 96: padded to the 128-wide kernels
+    (1, 1, 65, 100, 0.0, 0.0),     # head dim 100 (not a multiple of 16)
+])
+def test_attn_head_dim_128_matches_float64(B, H, T, d, p, kcm):
+    """Head dims 65..128 (the NU = 8 / 4-k-step instances of the single-pass forward and the bwd2 backward;
+    the engine's route for FastConformer-XL): O and every gradient against float64 autograd, rel. Frobenius
+    <= 2e-2 (bf16 operands, f32 accumulation).  With attention dropout the float64 reference applies the
+    kernel's own keep mask (read back from the saved Pd: zero exactly where a valid probability was dropped),
+    and the dropped fraction is checked against p; keys past a length get exactly zero dK / dV; the bwd2
+    kernels are bitwise reproducible and dPpos on a second stream equals the one-stream result."""
+    from kdfm import kernels as K
+    qkv, qu, qv, ppos, do, lens = _inputs(B, H, T, d, 7 * T + d)
+    if kcm:
+        g = torch.Generator(device="cuda").manual_seed(2)
+        qkv[:, d:] += kcm * torch.randn(1, 2 * d, device="cuda", generator=g)
+    seed = torch.tensor([4099], dtype=torch.int64, device="cuda")
+    one = _bwd2(K, qkv, qu, qv, ppos, do, lens, B, H, T, d, p, seed)
+    two = _bwd2(K, qkv, qu, qv, ppos, do, lens, B, H, T, d, p, seed, two_streams=True)
+    for a, b in zip(one, two):
+        assert torch.equal(a, b), "not bitwise reproducible / stream-order independent"
+    o, lse, dS, Pd, *got = one
+    keep = None
+    if p > 0:
+        valid = (torch.arange(T, device="cuda")[None, :] < lens[:, None])
+        vq = valid[:, None, :, None] & valid[:, None, None, :]
+        keep = (Pd.float() != 0) | ~vq
+        dropped = (~keep & vq).double().sum().item() / vq.double().sum().item() / H
+        assert 0.07 < dropped < 0.13, dropped
+    o_ref, ref = _torch_o_grads_masked(qkv, qu, qv, ppos, do, lens, B, H, T, d, keep, p)
+    valid_rows = (torch.arange(T, device="cuda")[None, :] < lens[:, None]).reshape(-1)
+    assert _rel(o[valid_rows], o_ref[valid_rows]) <= 2e-2, ("O", _rel(o[valid_rows], o_ref[valid_rows]))
+    for name, a, w in zip(("dQu", "dQv", "dK", "dV", "dPpos"), got, ref):
+        assert _rel(a, w) <= 2e-2, (name, _rel(a, w))
+    dk_, dv_ = got[2], got[3]
+    for bi in range(B):
+        L = int(lens[bi])
+        if L < T:
+            assert dk_.view(B, T, d)[bi, L:].abs().max().item() == 0.0
+            assert dv_.view(B, T, d)[bi, L:].abs().max().item() == 0.0

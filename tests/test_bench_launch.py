@@ -48,3 +48,33 @@ def test_world_mismatch_exits_nonzero_before_gpu():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", "--steps", "1"], env=env,
                        capture_output=True, text=True, timeout=300)
     assert r.returncode != 0 and "WORLD_SIZE=2" in r.stderr
+
+
+def test_gpu_count_from_environment_and_kfd(tmp_path):
+    assert bench.visible_gpu_count({"HIP_VISIBLE_DEVICES": "0,3,5"}, str(tmp_path)) == 3
+    assert bench.visible_gpu_count({"ROCR_VISIBLE_DEVICES": ""}, str(tmp_path)) == 0
+    for i, simds in enumerate((0, 1024, 1024)):   # node 0: the CPU
+        os.makedirs(tmp_path / str(i))
+        (tmp_path / str(i) / "properties").write_text(f"cpu_cores_count 64\nsimd_count {simds}\narray_count 32\n")
+    assert bench.visible_gpu_count({}, str(tmp_path)) == 2
+    assert bench.visible_gpu_count({}, str(tmp_path / "missing")) is None
+
+
+def test_launcher_parent_never_touches_torch_cuda(monkeypatch):
+    """The N-rank parent counts GPUs without torch.cuda (device_count / is_available / init would load HIP in
+    a process that then forks the ranks): every torch.cuda entry point raises here, and torch.cuda stays
+    uninitialised across the launch."""
+    import torch
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.delenv("KDFM_DIST_BACKEND", raising=False)   # the nccl path, which checks the GPU count
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0,1,2,3")
+
+    def boom(*a, **k):
+        raise AssertionError("the launcher parent called torch.cuda")
+    for name in ("device_count", "is_available", "init", "current_device", "set_device", "synchronize"):
+        monkeypatch.setattr(torch.cuda, name, boom)
+    seen = []
+    assert bench.launch_ranks(_args(4), ["--gpus", "4"], run=lambda c: seen.append(c) or 0) == 0
+    assert len(seen) == 1 and not torch.cuda.is_initialized()
+    with pytest.raises(SystemExit, match="needs 8 visible GPUs, found 4"):
+        bench.launch_ranks(_args(8), ["--gpus", "8"], run=lambda c: pytest.fail("must not spawn"))

@@ -172,3 +172,21 @@ def test_reference_style_ckpt_with_foreign_hyperparameters(eng, tmp_path):
     out = C.engine_state_dict(e2)
     assert int(out["teacher.encoder.layers.0.conv.batch_norm.num_batches_tracked"]) == 777
     assert int(out["encoder.layers.0.conv.batch_norm.num_batches_tracked"]) == 4567
+
+
+def test_conformer_meta_bn_counter_counts_module_calls():
+    """The conformer FM meta-encoder's BatchNorms run once per meta-encoder call, sum(S_i) times per step
+    (asr_train.py:1320-1336), so their num_batches_tracked is step x sum(S_i); the encoder's
+    BatchNorms still count optimizer steps."""
+    from kdfm.config import encfm_fixed_steps
+    cfg = replace(DEFAULT, n_layers=2, kd_model="encfm", encfm_dynamic=False, encfm_meta="conformer",
+                  encfm_steps_per_layer=(2, 3))
+    e = Ver5Engine(cfg, "cpu", init=False)
+    e.step.fill_(10)
+    sd = C.engine_state_dict(e, teacher=False)
+    meta = [k for k in sd if k.startswith("flow_matching.meta_encoder.") and k.endswith("num_batches_tracked")]
+    assert meta, "no meta-encoder BatchNorm in the state dict"
+    assert sum(encfm_fixed_steps(cfg)) == 5
+    for k in meta:
+        assert int(sd[k]) == 50, k
+    assert int(sd["encoder.layers.0.conv.batch_norm.num_batches_tracked"]) == 10

@@ -126,3 +126,45 @@ def test_meta_engine_step_matches_oracle(meta):
         if r > 1e-3:
             bad.append(f"{k}: {r:.3e}")
     assert not bad, bad
+
+
+@pytest.mark.parametrize("meta", ["swin", "conformer"])
+def test_meta_workspace_follows_batch_shape(meta):
+    """the engine keeps ONE meta-encoder workspace, the current batch shape's -- a new padded length
+    replaces the previous one instead of stacking another full set of saved activations (allocated memory
+    after steps at T1, T2, T1 stays within one workspace of the first step's peak) -- and an eval forward
+    reports zero flow losses (asr_train.py:1363-1364: loss 0.0 outside training)."""
+    import gc
+    import weakref
+
+    import test_step_parity_gpu as SP
+    cfg, eng, wav, wl, tg, tgl, g = SP._build(2, 2, 19200, [19200, 16123], 12, [12, 7],
+                                              sub=dict(kd_model="encfm", encfm_dynamic=False, encfm_meta=meta,
+                                                       encfm_steps_per_layer=(2, 3)))
+    wav2 = torch.cat([wav, wav[:, :6400]], 1)   # a longer padded batch: another T
+
+    def step(w):
+        ctx = eng.forward(w.cuda(), wl.cuda(), tg.cuda(), tgl.cuda(), train=True)
+        eng.backward(ctx)
+        del ctx
+        torch.cuda.synchronize()
+        gc.collect()
+
+    step(wav)
+    first = next(iter(eng._encfm.values()))
+    ref = weakref.ref(first)
+    del first
+    base = torch.cuda.memory_allocated()
+    step(wav2)
+    assert len(eng._encfm) == 1
+    gc.collect()
+    assert ref() is None, "the previous shape's workspace is still referenced"
+    step(wav)
+    assert len(eng._encfm) == 1
+    grown = torch.cuda.memory_allocated() - base
+    assert grown <= 0.05 * base + (1 << 20), (base, grown)
+    eng.forward(wav.cuda(), wl.cuda(), tg.cuda(), tgl.cuda(), train=False)
+    torch.cuda.synchronize()
+    ws = next(iter(eng._encfm.values()))
+    assert ws.flow.abs().max().item() == 0.0 and ws.stats[0].item() == 0.0
+    assert torch.isfinite(ws.xS).all()

@@ -52,7 +52,7 @@ def _oracle_params(cfg, eng):
                         kd_loss_type=cfg.kd_loss_type, use_diffkd=cfg.use_diffkd, diffkd_steps=cfg.diffkd_steps,
                         vocab=cfg.vocab, d_teacher=cfg.d_teacher, heads_teacher=cfg.heads_teacher,
                         d_student=cfg.d_student, heads_student=cfg.heads_student, conv_kernel=cfg.conv_kernel,
-                        kd_model=cfg.kd_model)
+                        kd_model=cfg.kd_model, xscaling=cfg.xscaling)
     p = {}
     p.update(O.frontend_buffers(ocfg))
     p.update(O.frontend_buffers(ocfg, "teacher.preprocessor.featurizer."))
@@ -81,19 +81,32 @@ def _close(a, b, tol, what, atol=1e-6, failures=None):
     assert err <= tol * scale + atol, msg
 
 
-def first_conv_ok(k, mine, ref, tol=2e-3, max_rows=2):
+def first_conv_ok(k, mine, ref, tol=2e-3, max_rows=2, row_tol=5e-3, rel_row_tol=5e-2):
     """The subsampling's first conv (the log-mel's only consumer): its weight / bias gradient rows are
     per output channel, and a conv0 output whose pre-activation cancels to within the f32 log-mel's
     rounding (GPU FFT vs the oracle's) can take the other side of the ReLU, moving that one channel's
-    row by one position's gradient (measured: 1 of 88 channels, 2.3e-3 of max, every other channel
-    within 1e-5 -- profiles/r04/conv0_diag.log).  Accept when at most `max_rows` channels exceed `tol`."""
+    row by one position's gradient (measured: 1 of 88 channels, 2.3e-3 / 3.5e-3 of max (overlapped), that
+    row's own max 0.37 / 0.24 of the tensor's, every other channel within 1e-5 -- profiles/r04/conv0_diag.log).
+    Accept when at most `max_rows` channels exceed `tol`, and each of them is still BOUNDED: its max error
+    within `row_tol` x the tensor's max (2.5x the regular tolerance; one position's gradient is a small
+    fraction of a row summed over ~10^4 positions) and, for weight rows, within `rel_row_tol` x that row's
+    own max (a 10 % corruption of any one channel fails: tests/test_first_conv_bound.py)."""
     if "pre_encode.conv.0." not in k:
         return False
     m = mine.detach().double().cpu().reshape(mine.shape[0], -1)
     r = ref.detach().double().cpu().reshape(ref.shape[0], -1)
     scale = r.abs().max().item()
-    rows_bad = ((m - r).abs().max(1).values > tol * scale + 1e-6).sum().item()
-    return rows_bad <= max_rows
+    err = (m - r).abs().max(1).values
+    bad = err > tol * scale + 1e-6
+    if bad.sum().item() > max_rows:
+        return False
+    if (err[bad] > row_tol * scale + 1e-6).any():
+        return False
+    if r.shape[1] > 1:
+        row_scale = r.abs().max(1).values
+        if (err[bad] > rel_row_tol * row_scale[bad] + 1e-6).any():
+            return False
+    return True
 
 
 DW4 = dict(subsampling="dw_striding", subsampling_factor=4)
@@ -106,6 +119,10 @@ FC = dict(d_student=512, heads_student=8, d_teacher=512, heads_teacher=8, subsam
 # 8 heads, 'striding' x4 with d_model conv channels, depthwise kernel 31) -- the 512-channel striding
 # subsampling runs the im2col + GEMM path (the one-kernel / implicit-GEMM kernels cover C <= 192)
 CL = dict(d_student=512, heads_student=8, d_teacher=512, heads_teacher=8, sched_d_model=512)
+# FastConformer-XL layer shapes (configs[4]; fast-conformer_ctc_bpe.yaml:29 XLarge row: d_model 1024, 8 heads ->
+# head dim 128, conv kernel 9, xscaling False; dw_striding x8 with 256 channels, :113-125) -- student and teacher
+XL = dict(d_student=1024, heads_student=8, d_teacher=1024, heads_teacher=8, subsampling="dw_striding",
+          subsampling_factor=8, subsampling_conv_channels=256, conv_kernel=9, xscaling=False, sched_d_model=1024)
 
 
 @pytest.mark.parametrize("n_layers,B,N,lens,U,tl,sub", [
@@ -135,11 +152,13 @@ CL = dict(d_student=512, heads_student=8, d_teacher=512, heads_teacher=8, sched_
     (2, 2, 32000, [32000, 24321], 12, [12, 7], FC),
     # Conformer-CTC-large shapes (f32 parity arithmetic)
     (2, 2, 19200, [19200, 16123], 12, [12, 7], CL),
+    # FastConformer-XL shapes (f32 parity arithmetic)
+    (2, 2, 32000, [32000, 24321], 12, [12, 7], XL),
     # the baseline logit-KD model family (DistilEncDecCTCModelBPE, asr_train_diffm.py:170-324): CTC + 0.1 KL
     (2, 2, 19200, [19200, 16123], 12, [12, 7], dict(kd_model="logitkd")),
 ], ids=["2L-1.2s", "16L-1s", "16L-16s", "16L-16s-overlapped", "2L-1.2s-dw4", "2L-1.2s-dw8-causal", "2L-1.2s-ver6", "2L-1.2s-ver7",
         "2L-1.2s-ver8-l1", "2L-1.2s-diffkd", "2L-1.2s-V1024", "2L-1.2s-equal-widths", "2L-2s-fastconformer-d512",
-        "2L-1.2s-conformer-large-d512", "2L-1.2s-logitkd"])
+        "2L-1.2s-conformer-large-d512", "2L-2s-fastconformer-xl-d1024", "2L-1.2s-logitkd"])
 def test_ver5_step_matches_oracle(n_layers, B, N, lens, U, tl, sub):
     from kdfm.config import sub_dims
     cfg, eng, wav, wl, tg, tgl, g = _build(n_layers, B, N, lens, U, tl, sub=sub)
@@ -219,11 +238,11 @@ def test_frontend_matches_oracle():
     _close(mel.cpu().transpose(1, 2), ref, 2e-4, "log-mel")
 
 
-@pytest.mark.parametrize("sub", [FC, CL, dict()], ids=["fastconformer-d512-h8", "conformer-large-d512-h8",
-                                                       "conformer-small"])
+@pytest.mark.parametrize("sub", [FC, CL, XL, dict()], ids=["fastconformer-d512-h8", "conformer-large-d512-h8",
+                                                           "fastconformer-xl-d1024-h8", "conformer-small"])
 def test_bf16_step_matches_float64_oracle(sub):
     """The bf16 benchmark kernels (fused LN-block FFN / projections where the width has them, the fused
-    rel-pos attention forward and the bwd2 backward -- at head dim 64 for the FastConformer shapes --,
+    rel-pos attention forward and the bwd2 backward -- at head dim 64 for the FastConformer shapes, 128 for XL --,
     bf16 weight gradients, the one-kernel striding subsampling for Conformer-small) through a whole
     2-layer step against the float64 oracle, dropout / SpecAugment / dither off, deterministic reductions.
     Tolerances are the bf16 step's (tests/test_bench_shape_gpu.py): losses rel 3e-3, layer outputs rel.
