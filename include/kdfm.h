@@ -648,6 +648,37 @@ int kdfm_relpos_attn_fwd(const float* qu, const float* qv, const float* qkv, con
                          float* m_blk, int64_t B, int64_t H,
                          int64_t T, int64_t d, float scale, float dropout_p, const uint64_t* seed,
                          uint64_t rng_stream, void* stream);
+/* The same forward over PREPARED bf16 operands (csrc/attn_fwd3.hip; single pass, lse only -- the bwd2
+ * backward's form -- or inference with lse NULL): O and lse are bitwise kdfm_relpos_attn_fwd's.  Every operand
+ * tile of a (64 queries, 64 keys) step is one contiguous range copied into LDS by LDS-DMA.
+ *   kdfm_attn_kv_prep: kb / vb (B*H, Tp, LR) bf16 with Tp = T rounded up to 64, LR = DKP + 8, DKP = 64 (dk <= 64)
+ *     or 128: rows j < T = bf16(K_j - kc) / bf16(V_j - vc) in columns < dk (the centring of
+ *     kdfm_relpos_attn_fwd), zeros elsewhere; centre (B*H, 2, DKP) f32 = (kc, vc).  Sizes:
+ *     kdfm_attn_kv_prep_elems / kdfm_attn_centre_elems (-1: unsupported).
+ *   kdfm_attn_band_prep: every layer's projected positions pos + l * ld_layer ((2T-1, d) each) as pb
+ *     (layers*H, NPB, LR) bf16, NPB = 64 + (2T-1) + 88, row 64 + r = position r, zeros around
+ *     (kdfm_attn_band_prep_elems); kdfm_relpos_attn_fwd3 takes one layer's (H, NPB, LR) slice.
+ * Replaces the per-layer attention call of NeMo RelPositionMultiHeadAttention (conformer_encoder.py:685-692,
+ * Appendix A.7) like kdfm_relpos_attn_fwd; dk <= 128. */
+int64_t kdfm_attn_kv_prep_elems(int64_t B, int64_t H, int64_t T, int64_t d);
+int64_t kdfm_attn_centre_elems(int64_t B, int64_t H, int64_t d);
+int64_t kdfm_attn_band_prep_elems(int64_t layers, int64_t H, int64_t T, int64_t d);
+int kdfm_attn_kv_prep(const float* qkv, const int64_t* lengths, uint16_t* kb, uint16_t* vb, float* centre, int64_t B,
+                      int64_t H, int64_t T, int64_t d, void* stream);
+int kdfm_attn_band_prep(const float* pos, int64_t ld_layer, int64_t layers, uint16_t* pb, int64_t H, int64_t T,
+                        int64_t d, void* stream);
+/* bwd2 part 1 (kdfm_relpos_attn_bwd2_dq) over the forward's prepared operands: K / V / band tiles and the
+ * centre from kdfm_attn_kv_prep / kdfm_attn_band_prep (the forward's own, kept for the backward) instead of
+ * qkv / pos -- the same dqu / dqv / dS / Pd (dS and Pd bitwise; dqu / dqv up to the sign of zero products). */
+int kdfm_relpos_attn_bwd2_dq3(const float* dO, const float* O, const float* qu, const float* qv, const uint16_t* kb,
+                              const uint16_t* vb, const float* centre, const uint16_t* pb, const float* lse,
+                              const int64_t* lengths, uint16_t* ds, uint16_t* pd, float* dqu, float* dqv, int64_t B,
+                              int64_t H, int64_t T, int64_t d, float scale, float dropout_p, const uint64_t* seed,
+                              uint64_t rng_stream, void* stream);
+int kdfm_relpos_attn_fwd3(const float* qu, const float* qv, const uint16_t* kb, const uint16_t* vb, const float* centre,
+                          const uint16_t* pb, const int64_t* lengths, float* o, float* lse, int64_t B, int64_t H,
+                          int64_t T, int64_t d, float scale, float dropout_p, const uint64_t* seed, uint64_t rng_stream,
+                          void* stream);
 /* conv module: GLU over channels + pad mask; depthwise conv (k odd) with optional f64 BN stats */
 int kdfm_glu_mask_fwd(const float* a, const int64_t* lengths, float* g, int64_t B, int64_t T, int64_t d,
                       void* stream);

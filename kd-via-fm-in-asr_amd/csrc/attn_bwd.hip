@@ -66,6 +66,9 @@ struct AbP {
   // bwd2: dS and Pd (dropout-applied P) as bf16 (B, H, T, ldt), written by kernel 1, read by kernels 2b / 3b
   uint16_t* ds; uint16_t* pdo; int64_t ldt;
   const float* O;   // bwd2: the forward output (row sums formed in the dQ kernel)
+  // bwd2 over prepared operands (csrc/attn_fwd3.hip): bf16 centred K / V tiles (B*H, Tp, LR), the centre
+  // (B*H, 2, DKP), this layer's band rows (H, npb, LR)
+  const uint16_t* kb; const uint16_t* vb; const float* cen; const uint16_t* pb; int64_t Tp, npb;
 };
 
 constexpr uint32_t AB_OOB = 0x80000000u;   // buffer offset past every buffer: the access is dropped / reads 0
@@ -191,16 +194,23 @@ __global__ __launch_bounds__(256) void attn_rowdot_kernel(const float* __restric
 // kernel 1: dQu, dQv
 // ---------------------------------------------------------------------------------------------
 // RIN: the row sums r_i are formed in the prologue from dO and O (p.O) instead of read from p.rsum
-// NU = 8 (head dim <= 128, FastConformer-XL): the head dim is padded to 4 MFMA k-steps (KS) instead of 2
-template <int NU, bool SAVE = false, bool RIN = false>
+// NU = 8 (head dim <= 128, FastConformer-XL): the head dim is padded to 4 MFMA k-steps (KS) instead of 2.
+// PREP (bwd2 only): K / V / band tiles copied by LDS-DMA from the forward's prepared bf16 operands
+// (kdfm_attn_kv_prep / kdfm_attn_band_prep, the same bf16(K - kc) / bf16(V - vc) values the register path
+// stages) and the centre read from them -- no staging registers, no conversion or centring pass
+template <int NU, bool SAVE = false, bool RIN = false, bool PREP = false>
 __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dq_kernel(AbP p) {
   constexpr int KS = NU > 4 ? 4 : 2;
   constexpr int DKP = 32 * KS;
   constexpr int LRK = DKP + 8;
   static_assert(SAVE || KS == 2, "the pre-bwd2 path covers head dims <= 64 only");
+  static_assert(!PREP || (SAVE && RIN), "prepared operands: the bwd2 dQ kernel only");
+  constexpr int KCH = BK * LRK * 2 / 1024;                  // 1 KB DMA chunks of a K / V tile
+  constexpr int PCH = (PB1 * LRK * 2 + 1023) / 1024;        // ... of the band (rows past 143 unused)
+  static_assert(BK * LRK * 2 % 1024 == 0, "K / V tiles must be whole 1 KB chunks");
   __shared__ __attribute__((aligned(16))) uint16_t Ks[BK * LRK];     // K block [key][c]
   __shared__ __attribute__((aligned(16))) uint16_t Vs[BK * LRK];     // V block [key][c]
-  __shared__ __attribute__((aligned(16))) uint16_t Pr[PB1 * LRK];    // Ppos band [band row][c]
+  __shared__ __attribute__((aligned(16))) uint16_t Pr[PREP ? PCH * 512 : PB1 * LRK];    // Ppos band [band row][c]
   __shared__ __attribute__((aligned(16))) float Wsc[4][WS1 / 4];    // per-wave scratch
   // SAVE (bwd2): per wave Pd tile [16][LW] bf16; dS and Pd leave as 16-byte buffer stores (fixed count per
   // lane and key block, out-of-range chunks dropped by the range check)
@@ -218,7 +228,9 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dq_kernel(AbP p
   const int nkb = (len + BK - 1) / BK;
   const int npos = 2 * T - 1;
   const int64_t hoff = h * p.dkh;
-  if constexpr (SAVE) {
+  if constexpr (PREP) {
+    // (the DMA'd tiles are complete images: padding columns / rows come zero from the preparation)
+  } else if constexpr (SAVE) {
     zero_img<LRK>(Ks, BK);
     zero_img<LRK>(Vs, BK);
     zero_img<LRK>(Pr, PB1);
@@ -265,7 +277,26 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dq_kernel(AbP p
   auto fetch = [&](int kb) {
     const int j0 = kb * BK;
     const int rbase = T - 1 - (i0 + BQ - 1) + j0;
-    if constexpr (SAVE) {
+    if constexpr (PREP) {
+      typedef __attribute__((address_space(3))) void lds_t;
+      typedef __attribute__((address_space(1))) void gl_t;
+      const uint4* ks = reinterpret_cast<const uint4*>(p.kb + (bh * p.Tp + j0) * LRK);
+      const uint4* vs = reinterpret_cast<const uint4*>(p.vb + (bh * p.Tp + j0) * LRK);
+      const uint4* bs = reinterpret_cast<const uint4*>(p.pb + (h * p.npb + rbase + 64) * LRK);
+#pragma unroll
+      for (int i = 0; i < (2 * KCH + PCH + 3) / 4; ++i) {
+        const int f = w + 4 * i;   // wave-uniform
+        if (f < KCH)
+          __builtin_amdgcn_global_load_lds((gl_t*)(ks + f * 64 + lane), (lds_t*)(reinterpret_cast<uint4*>(Ks) + f * 64),
+                                           16, 0, 0);
+        else if (f < 2 * KCH)
+          __builtin_amdgcn_global_load_lds((gl_t*)(vs + (f - KCH) * 64 + lane),
+                                           (lds_t*)(reinterpret_cast<uint4*>(Vs) + (f - KCH) * 64), 16, 0, 0);
+        else if (f < 2 * KCH + PCH)
+          __builtin_amdgcn_global_load_lds((gl_t*)(bs + (f - 2 * KCH) * 64 + lane),
+                                           (lds_t*)(reinterpret_cast<uint4*>(Pr) + (f - 2 * KCH) * 64), 16, 0, 0);
+      }
+    } else if constexpr (SAVE) {
       fetch_rows_b<NU>(nv, rv, p.ldkv, b * p.T, j0, BK, 0, len, hoff, dk);
       fetch_rows_b<NU>(nk, rk, p.ldkv, b * p.T, j0, BK, 0, len, hoff, dk);
       fetch_rows_b<2 * NU>(nb, rp, p.d, 0, rbase, 127, 0, npos, hoff, dk);
@@ -281,7 +312,12 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dq_kernel(AbP p
 
   // the forward's centring (attn_centre.h): K rows staged as K_j - kc (the scores, hence P = exp(s - lse),
   // are the forward's), V rows as V_j - vc with cs_i = dO_i . vc added back to dPd in f32
-  kv_centre<DKP>(p.k + b * p.T * p.ldkv + hoff, p.v + b * p.T * p.ldkv + hoff, p.ldkv, len, dk, Cn);
+  if constexpr (PREP) {
+    for (int e = threadIdx.x; e < 2 * DKP; e += 256) Cn[e / DKP][e % DKP] = p.cen[bh * 2 * DKP + e];
+    __syncthreads();
+  } else {
+    kv_centre<DKP>(p.k + b * p.T * p.ldkv + hoff, p.v + b * p.T * p.ldkv + hoff, p.ldkv, len, dk, Cn);
+  }
   // cs_i for this lane's C-layout rows: row (lane & 15) of the wave's 16 dotted in f32 by its 4 lane groups
   // (16 columns each), summed across them, then picked up by the lanes owning each row.  With RIN (bwd2)
   // the row sums r_i = dO_i . O_i are formed the same way here instead of by attn_rowdot_kernel
@@ -349,14 +385,23 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dq_kernel(AbP p
   KPROBE(1);
   for (int kb = 0; kb < nkb; ++kb) {
     const int j0 = kb * BK;
-    __syncthreads();
-    centre(nk, Cn[0], j0);
-    centre(nv, Cn[1], j0);
-    put_rows<NU, LRK>(Vs, nullptr, 0, nv, BK, dk);
-    put_rows<NU, LRK>(Ks, nullptr, 0, nk, BK, dk);
-    put_rows<2 * NU, LRK>(Pr, nullptr, 0, nb, 127, dk);
-    __syncthreads();
-    if (kb + 1 < nkb) fetch(kb + 1);
+    if constexpr (PREP) {
+      if (kb > 0) {
+        __syncthreads();   // every wave is done with the previous block's tiles
+        fetch(kb);
+      }
+      __builtin_amdgcn_s_waitcnt(0x70);   // vmcnt(0) lgkmcnt(0): this wave's DMA chunks (and its stores) landed
+      __syncthreads();
+    } else {
+      __syncthreads();
+      centre(nk, Cn[0], j0);
+      centre(nv, Cn[1], j0);
+      put_rows<NU, LRK>(Vs, nullptr, 0, nv, BK, dk);
+      put_rows<NU, LRK>(Ks, nullptr, 0, nk, BK, dk);
+      put_rows<2 * NU, LRK>(Pr, nullptr, 0, nb, 127, dk);
+      __syncthreads();
+      if (kb + 1 < nkb) fetch(kb + 1);
+    }
     KPROBE(2 + 4 * kb);
     // ---- S of this wave's 16 rows x 64 keys: the forward's scores (relpos_attn_fwd_kernel) ----
     float s[4][4];
@@ -1121,6 +1166,31 @@ int kdfm_relpos_attn_bwd2_dq(const float* dO, const float* O, const float* qu, c
   else
     hipLaunchKernelGGL((attn_bwd_dq_kernel<3, true, true>), dim3((unsigned)ceil_div(T, BQ), (unsigned)(B * H)), dim3(256), 0, st, p);
   return check_launch("kdfm_relpos_attn_bwd2_dq");
+}
+
+int kdfm_relpos_attn_bwd2_dq3(const float* dO, const float* O, const float* qu, const float* qv, const uint16_t* kb,
+                              const uint16_t* vb, const float* centre, const uint16_t* pb, const float* lse,
+                              const int64_t* lengths, uint16_t* ds, uint16_t* pd, float* dqu, float* dqv, int64_t B,
+                              int64_t H, int64_t T, int64_t d, float scale, float dropout_p, const uint64_t* seed,
+                              uint64_t rng_stream, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(dO && O && qu && qv && kb && vb && centre && pb && lse && ds && pd && dqu && dqv, "null pointer");
+  KDFM_REQUIRE((((uintptr_t)dO | (uintptr_t)O | (uintptr_t)qu | (uintptr_t)qv | (uintptr_t)kb | (uintptr_t)vb |
+                 (uintptr_t)pb | (uintptr_t)ds | (uintptr_t)pd) & 15) == 0, "operands must be 16-byte aligned");
+  AbP p;
+  int rc = ab2_setup(p, qu, qv, nullptr, lse, lengths, B, H, T, d, scale, dropout_p, seed, rng_stream);
+  if (rc || B == 0) return rc;
+  p.dO = dO; p.dqu = dqu; p.dqv = dqv; p.ds = ds; p.pdo = pd; p.O = O;
+  p.kb = kb; p.vb = vb; p.cen = centre; p.pb = pb; p.Tp = attn_prep_tp(T); p.npb = attn_prep_npb(T);
+  hipStream_t st = as_stream(stream);
+  const dim3 grid((unsigned)ceil_div(T, BQ), (unsigned)(B * H));
+  if (p.dkh > 64)
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<8, true, true, true>), grid, dim3(256), 0, st, p);
+  else if (p.dkh > 48)
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<4, true, true, true>), grid, dim3(256), 0, st, p);
+  else
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<3, true, true, true>), grid, dim3(256), 0, st, p);
+  return check_launch("kdfm_relpos_attn_bwd2_dq3");
 }
 
 int kdfm_relpos_attn_bwd2_dkv(const float* dO, const float* qu, const uint16_t* ds, const uint16_t* pd,

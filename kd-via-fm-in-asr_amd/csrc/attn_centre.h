@@ -44,4 +44,14 @@ __device__ __forceinline__ void kv_centre(const float* kbase, const float* vbase
   __syncthreads();
 }
 
+// Prepared bf16 operands of the attention kernels (csrc/attn_fwd3.hip kdfm_attn_kv_prep / kdfm_attn_band_prep):
+// key / value tiles (B*H, attn_prep_tp(T), LR) and band rows (layers*H, attn_prep_npb(T), LR) with
+// kAttnBandPad0 zero rows before position 0 and kAttnBandPad1 after the last (the forward stages 128 band
+// rows per step, the dQ kernel 144 rounded up to whole 1 KB DMA chunks: up to 149 rows past the step's first)
+constexpr int kAttnBandPad0 = 64;
+constexpr int kAttnBandPad1 = 88;
+__host__ __device__ inline int64_t attn_prep_tp(int64_t T) { return (T + 63) / 64 * 64; }
+__host__ __device__ inline int64_t attn_prep_npb(int64_t T) { return kAttnBandPad0 + (2 * T - 1) + kAttnBandPad1; }
+__host__ __device__ inline int attn_prep_dkp(int64_t dk) { return dk > 64 ? 128 : 64; }
+
 }  // namespace kdfm

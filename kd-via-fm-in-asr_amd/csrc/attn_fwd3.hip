@@ -1,0 +1,442 @@
+// Relative-position MHA forward over PREPARED bf16 operands (the single-pass / lse-only form the bwd2 backward
+// and inference use): the same arithmetic as relpos_attn_fwd_kernel<false, NU, false> (attn_fused.hip) -- same
+// bf16 operands, same MFMAs in the same order, same online softmax and counter-RNG dropout, so O and lse are
+// bitwise that kernel's -- restaged for occupancy:
+//   * kdfm_attn_kv_prep writes each utterance's centred keys / values (attn_centre.h) ONCE as bf16 tiles
+//     [b, h][key][c] with the LDS row stride (head dim padded to 32 KS, + 8), and the value centre;
+//     kdfm_attn_band_prep every layer's projected positions as bf16 rows [layer, h][64 + r][c] with zero rows
+//     around them.  Every operand tile of a (64 queries, 64 keys) step is then ONE contiguous byte range
+//     (K 64 rows, V 64 rows, the Ppos band 128 rows from r = T-1-(i0+63)+j0), copied into LDS by LDS-DMA
+//     (global_load_lds_dwordx4, 1 KB per wave-instruction): no staging registers, no conversion, no
+//     ds_write pass (the register-staged kernel spent ~30 % of a key block there, profiles/r03/final_attn_probe.log).
+//   * rel_shift as lane permutes: S_bd[ii][jj] = G[ii][jj - ii + 15] is read from the MFMA accumulators of G =
+//     Qv Pband^T with ds_bpermute (5 per row register) instead of an f32 G tile written to and read back from
+//     LDS (20.7 KB per workgroup and two wave syncs per key block).
+//   * P V reads V [key][c] transposed (ds_read_b64_tr_b16) instead of a transposed V^T image.
+// LDS per workgroup: 46 KB at head dim <= 64, 79 KB at 128; head dim <= 48 fits 3 workgroups (12 waves) per CU
+// in 168 registers (the register-staged kernel: 67 KB, 2 workgroups).
+#include "gemm_common.h"
+#include "attn_centre.h"
+
+namespace kdfm {
+namespace {
+
+typedef __attribute__((address_space(3))) void lds_void_t3;
+typedef __attribute__((address_space(1))) void gl_void_t3;
+typedef short v4s3 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4s3 lds_v4s3;
+
+constexpr int A3Q = 64;            // queries per workgroup (4 waves x 16)
+constexpr int A3K = 64;            // keys per step
+constexpr int A3BAND = 128;        // Ppos band rows staged per step (127 used)
+constexpr int A3PAD0 = kAttnBandPad0;   // zero rows before the first position row of a prepared band
+constexpr int A3LDP = A3K + 8;     // bf16 row stride of the per-wave P tile [16][64]
+
+template <int NU> struct A3Geo {
+  static constexpr int KS = NU > 4 ? 4 : 2;        // MFMA k-steps over the padded head dim
+  static constexpr int DKP = 32 * KS;
+  static constexpr int LR = DKP + 8;               // bf16 row stride (8-byte aligned transposed reads)
+  static constexpr int KCH = A3K * LR * 2 / 1024;  // 1 KB DMA chunks per K / V tile
+  static constexpr int BCH = A3BAND * LR * 2 / 1024;
+  static_assert(A3K * LR * 2 % 1024 == 0 && A3BAND * LR * 2 % 1024 == 0, "tiles must be whole 1 KB chunks");
+};
+
+__host__ __device__ inline int a3_dkp(int64_t dk) { return attn_prep_dkp(dk); }
+__host__ __device__ inline int64_t a3_tp(int64_t T) { return attn_prep_tp(T); }
+__host__ __device__ inline int64_t a3_npb(int64_t T) { return attn_prep_npb(T); }
+
+// ---- preparation --------------------------------------------------------------------------------------
+// kb / vb [b*H + h][Tp][LR]: rows j < T hold bf16(K_j - kc) / bf16(V_j - vc) in columns < dk, zeros elsewhere;
+// cen [b*H + h][2][DKP] = (kc, vc) f32 (zeros past dk).  One workgroup per (64 rows, b*H + h).
+template <int DKP>
+__global__ __launch_bounds__(256) void attn_kv_prep_kernel(const float* __restrict__ qkv, const int64_t* __restrict__ lens,
+                                                           uint16_t* __restrict__ kb, uint16_t* __restrict__ vb,
+                                                           float* __restrict__ cen, int64_t H, int T, int64_t d, int dk,
+                                                           int64_t Tp) {
+  constexpr int LR = DKP + 8, P8 = LR / 8;
+  __shared__ __attribute__((aligned(16))) float Cn[2][DKP];
+  const int64_t bh = blockIdx.y, b = bh / H, h = bh - b * H;
+  const int len = lens ? (int)min<int64_t>(lens[b], T) : T;
+  const float* kbase = qkv + b * T * 3 * d + d + h * dk;
+  const float* vbase = kbase + d;
+  for (int e = threadIdx.x; e < 2 * DKP; e += 256) Cn[e / DKP][e % DKP] = 0.f;
+  __syncthreads();
+  kv_centre<DKP>(kbase, vbase, 3 * d, len, dk, Cn);   // (ends with a barrier)
+  if (blockIdx.x == 0)
+    for (int e = threadIdx.x; e < 2 * DKP; e += 256) cen[bh * 2 * DKP + e] = Cn[e / DKP][e % DKP];
+  const int j0 = blockIdx.x * A3K;
+  for (int e = threadIdx.x; e < 2 * A3K * P8; e += 256) {
+    const int kind = e / (A3K * P8), rem = e - kind * (A3K * P8);
+    const int rr = rem / P8, c0 = (rem - rr * P8) * 8;
+    const int j = j0 + rr;
+    const float* src = (kind ? vbase : kbase) + (int64_t)(j < T ? j : 0) * 3 * d;
+    const float m0 = (j < T && c0 < dk) ? 1.f : 0.f, m1 = (j < T && c0 + 4 < dk) ? 1.f : 0.f;
+    const float4 a = *reinterpret_cast<const float4*>(src + (c0 < dk ? c0 : 0));
+    const float4 q = *reinterpret_cast<const float4*>(src + (c0 + 4 < dk ? c0 + 4 : 0));
+    const float* cc = Cn[kind];
+    const int ca = c0 < DKP ? c0 : 0, cb = c0 + 4 < DKP ? c0 + 4 : 0;
+    // (a - c) * m: the subtraction is the register-staged kernel's rk - ck, rounded to bf16 by the same RNE
+    const float t[8] = {(a.x - cc[ca]) * m0, (a.y - cc[ca + 1]) * m0, (a.z - cc[ca + 2]) * m0, (a.w - cc[ca + 3]) * m0,
+                        (q.x - cc[cb]) * m1, (q.y - cc[cb + 1]) * m1, (q.z - cc[cb + 2]) * m1, (q.w - cc[cb + 3]) * m1};
+    *reinterpret_cast<bf16x8*>((kind ? vb : kb) + (bh * Tp + j) * LR + c0) = pack_bf16x8<bf16x8>(t);
+  }
+}
+
+// pb [layer*H + h][NPB][LR]: row A3PAD0 + r = bf16(pos[layer][r][h*dk + c]) (c < dk), zeros elsewhere
+template <int DKP>
+__global__ __launch_bounds__(256) void attn_band_prep_kernel(const float* __restrict__ pos, int64_t ld_layer,
+                                                             uint16_t* __restrict__ pb, int64_t H, int64_t npos,
+                                                             int64_t d, int dk, int64_t npb) {
+  constexpr int LR = DKP + 8, P8 = LR / 8;
+  const int64_t lh = blockIdx.y, l = lh / H, h = lh - l * H;
+  const int64_t R0 = (int64_t)blockIdx.x * 64;
+  for (int e = threadIdx.x; e < 64 * P8; e += 256) {
+    const int rr = e / P8, c0 = (e - rr * P8) * 8;
+    const int64_t R = R0 + rr, r = R - A3PAD0;
+    if (R >= npb) continue;
+    const bool in = r >= 0 && r < npos;
+    const float* src = pos + l * ld_layer + (in ? r : 0) * d + h * dk;
+    const float m0 = (in && c0 < dk) ? 1.f : 0.f, m1 = (in && c0 + 4 < dk) ? 1.f : 0.f;
+    const float4 a = *reinterpret_cast<const float4*>(src + (c0 < dk ? c0 : 0));
+    const float4 q = *reinterpret_cast<const float4*>(src + (c0 + 4 < dk ? c0 + 4 : 0));
+    const float t[8] = {a.x * m0, a.y * m0, a.z * m0, a.w * m0, q.x * m1, q.y * m1, q.z * m1, q.w * m1};
+    *reinterpret_cast<bf16x8*>(pb + (lh * npb + R) * LR + c0) = pack_bf16x8<bf16x8>(t);
+  }
+}
+
+// ---- the forward --------------------------------------------------------------------------------------
+struct Attn3P {
+  const float* qu; const float* qv; const uint16_t* kb; const uint16_t* vb; const float* cen; const uint16_t* pb;
+  const int64_t* lens;
+  float* o; float* lse;
+  int64_t B, H, T, d, dk, Tp, npb;
+  float scale, p_drop;
+  const uint64_t* seed; uint64_t rng_stream;
+};
+
+__device__ __forceinline__ bf16x8 a3_frag8(const float* head, int c0, int valid) {
+  const float m0 = valid >= 4 ? 1.f : 0.f, m1 = valid >= 8 ? 1.f : 0.f;
+  const float4 a = *reinterpret_cast<const float4*>(head + (valid >= 4 ? c0 : 0));
+  const float4 b = *reinterpret_cast<const float4*>(head + (valid >= 8 ? c0 + 4 : 0));
+  const float t[8] = {a.x * m0, a.y * m0, a.z * m0, a.w * m0, b.x * m1, b.y * m1, b.z * m1, b.w * m1};
+  return pack_bf16x8<bf16x8>(t);
+}
+
+// B operand X[k][n] read transposed out of a [k][n] bf16 LDS image (attn_bwd.hip tr_frag)
+__device__ __forceinline__ bf16x8 a3_tr_frag(const uint16_t* img, int ld, int k0, int n0, int lane) {
+  const int li = lane & 15;
+  const uint16_t* a = img + (k0 + 8 * (lane >> 4) + (li >> 2)) * ld + n0 + 4 * (li & 3);
+  const v4s3 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s3*)a);
+  const v4s3 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s3*)(a + 4 * ld));
+  return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+template <int CTRL>
+__device__ __forceinline__ float a3_dpp(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float a3_max16(float v) {
+  v = fmaxf(v, a3_dpp<0xB1>(v));
+  v = fmaxf(v, a3_dpp<0x4E>(v));
+  v = fmaxf(v, a3_dpp<0x141>(v));
+  return fmaxf(v, a3_dpp<0x140>(v));
+}
+__device__ __forceinline__ float a3_sum16(float v) {
+  v += a3_dpp<0xB1>(v);
+  v += a3_dpp<0x4E>(v);
+  v += a3_dpp<0x141>(v);
+  return v + a3_dpp<0x140>(v);
+}
+
+template <int NU>
+__global__ __launch_bounds__(256, NU == 3 ? 3 : 2) void relpos_attn_fwd3_kernel(Attn3P p) {
+  using Gm = A3Geo<NU>;
+  constexpr int KS = Gm::KS, LR = Gm::LR, KCH = Gm::KCH, BCH = Gm::BCH, NCH = 2 * KCH + BCH;
+  __shared__ __attribute__((aligned(16))) uint16_t Ks[A3K * LR];
+  __shared__ __attribute__((aligned(16))) uint16_t Vs[A3K * LR];
+  __shared__ __attribute__((aligned(16))) uint16_t Pr[A3BAND * LR];
+  __shared__ __attribute__((aligned(16))) uint16_t Ps[4][16 * A3LDP];
+
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int T = (int)p.T, dk = (int)p.dk;
+  const Blk3 blk = xcd_block3();
+  const int64_t bh = blk.y;
+  const int64_t b = bh / p.H, h = bh - b * p.H;
+  const int i0 = (int)blk.x * A3Q;
+  const int len = p.lens ? (int)p.lens[b] : T;
+  const int nkb = (min(len, T) + A3K - 1) / A3K;
+  const int64_t hoff = h * p.dk;
+  const uint4* ksrc = reinterpret_cast<const uint4*>(p.kb + bh * p.Tp * LR);
+  const uint4* vsrc = reinterpret_cast<const uint4*>(p.vb + bh * p.Tp * LR);
+  const uint16_t* bsrc = p.pb + h * p.npb * LR;
+
+  // one key step's operands: K rows [j0, j0 + 64), V rows, band rows [rbase, rbase + 128) of the prepared
+  // band (row A3PAD0 + r holds position r) -- NCH 1 KB chunks, wave w takes chunks w, w + 4, ...
+  auto issue = [&](int j0) {
+    const int rb = T - 1 - (i0 + A3Q - 1) + j0 + A3PAD0;
+    const uint4* bs = reinterpret_cast<const uint4*>(bsrc + (int64_t)rb * LR);
+#pragma unroll
+    for (int i = 0; i < (NCH + 3) / 4; ++i) {
+      const int f = w + 4 * i;   // wave-uniform
+      if (f < KCH) {
+        __builtin_amdgcn_global_load_lds((gl_void_t3*)(ksrc + (int64_t)j0 * LR / 8 + f * 64 + lane),
+                                         (lds_void_t3*)(reinterpret_cast<uint4*>(Ks) + f * 64), 16, 0, 0);
+      } else if (f < 2 * KCH) {
+        __builtin_amdgcn_global_load_lds((gl_void_t3*)(vsrc + (int64_t)j0 * LR / 8 + (f - KCH) * 64 + lane),
+                                         (lds_void_t3*)(reinterpret_cast<uint4*>(Vs) + (f - KCH) * 64), 16, 0, 0);
+      } else if (f < NCH) {
+        __builtin_amdgcn_global_load_lds((gl_void_t3*)(bs + (f - 2 * KCH) * 64 + lane),
+                                         (lds_void_t3*)(reinterpret_cast<uint4*>(Pr) + (f - 2 * KCH) * 64), 16, 0, 0);
+      }
+    }
+  };
+  if (nkb > 0) issue(0);
+
+  // this lane's query row (A-fragment row): Qu / Qv fragments
+  const int iq = i0 + w * 16 + (lane & 15);
+  bf16x8 fu[KS], fv[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    const int c0 = ks * 32 + 8 * (lane >> 4);
+    const int valid = (iq < T) ? dk - c0 : 0;
+    const int64_t off = (b * p.T + (iq < T ? iq : 0)) * p.d + hoff;
+    fu[ks] = a3_frag8(p.qu + off, c0, valid);
+    fv[ks] = a3_frag8(p.qv + off, c0, valid);
+  }
+  const int q4 = lane >> 4, lo = lane & 15;
+  const int ib = i0 + w * 16 + 4 * q4;   // C-layout rows ib + r
+  float mrow[4], lrow[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) { mrow[r] = -3.0e38f; lrow[r] = 0.f; }
+  // rel_shift permute per row register r: S_bd(t, r) = G[t + (off >= 16)][r] of lane (off & 15) + 16 q4
+  int bsrc_lane[4];
+  bool bhi[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int off = lo - 4 * q4 - r + 15;   // 0 .. 30
+    bsrc_lane[r] = ((off & 15) + 16 * q4) * 4;
+    bhi[r] = off >= 16;
+  }
+
+  const uint64_t seed = (p.p_drop > 0.f) ? load_seed(p.seed) : 0ull;
+  const uint64_t dkey = rng_key(seed, p.rng_stream);
+  const float keep_scale = (p.p_drop > 0.f) ? 1.f / (1.f - p.p_drop) : 1.f;
+  const bool drop = p.p_drop > 0.f;
+  f32x4 oacc[NU];
+#pragma unroll
+  for (int u = 0; u < NU; ++u) oacc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int64_t prow0 = (bh * p.T + ib) * p.T;
+  float ps[4] = {0.f, 0.f, 0.f, 0.f};
+  uint16_t* Pw = Ps[w];
+
+  for (int kb = 0; kb < nkb; ++kb) {
+    const int j0 = kb * A3K;
+    if (kb > 0) {
+      __syncthreads();   // every wave is done with the previous step's tiles
+      issue(j0);
+    }
+    __builtin_amdgcn_s_waitcnt(0x70);   // vmcnt(0) lgkmcnt(0): this wave's DMA chunks landed
+    __syncthreads();                    // ... and every other wave's
+    // ---- scores of this wave's 16 rows x 64 keys (the register-staged kernel's MFMAs, same order) ----
+    f32x4 ac[4], g[5];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) ac[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 5; ++t) g[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int wb = 48 - 16 * w;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int kof = ks * 32 + 8 * q4;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const bf16x8 kbf = *reinterpret_cast<const bf16x8*>(Ks + (16 * t + lo) * LR + kof);
+        ac[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fu[ks], kbf, ac[t], 0, 0, 0);
+      }
+#pragma unroll
+      for (int t = 0; t < 5; ++t) {
+        const bf16x8 pbf = *reinterpret_cast<const bf16x8*>(Pr + (wb + 16 * t + lo) * LR + kof);
+        g[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fv[ks], pbf, g[t], 0, 0, 0);
+      }
+    }
+    float s[4][4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float X[5];
+#pragma unroll
+      for (int t = 0; t < 5; ++t)
+        X[t] = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(bsrc_lane[r], __builtin_bit_cast(int, g[t][r])));
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const float bd = bhi[r] ? X[t + 1] : X[t];
+        const int j = j0 + 16 * t + lo;
+        s[t][r] = (j < len && j < T) ? (ac[t][r] + bd) * p.scale : -3.0e38f;
+      }
+    }
+    // ---- online softmax: rescale the running sum and O to the new row max ----
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float mx = fmaxf(fmaxf(s[0][r], s[1][r]), fmaxf(s[2][r], s[3][r]));
+      mx = a3_max16(mx);
+      const float mn = fmaxf(mrow[r], mx);
+      const float corr = (mrow[r] > -1.0e38f) ? __expf(mrow[r] - mn) : 0.f;
+      float sum = 0.f;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) sum += (s[t][r] > -1.0e38f) ? __expf(s[t][r] - mn) : 0.f;
+      lrow[r] = lrow[r] * corr + a3_sum16(sum);
+      mrow[r] = mn;
+      ps[r] *= corr;
+#pragma unroll
+      for (int u = 0; u < NU; ++u) oacc[u][r] *= corr;
+    }
+    float pds[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ii = 4 * q4 + r, jj = 16 * t + lo;
+        const float pv = (s[t][r] > -1.0e38f) ? __expf(s[t][r] - mrow[r]) : 0.f;
+        float pdv = pv;
+        if (drop) {
+          pdv = dropout_keep_k(dkey, (uint64_t)(prow0 + (int64_t)r * p.T + j0 + jj), p.p_drop) ? pv * keep_scale : 0.f;
+          pds[r] += pdv;
+        }
+        Pw[ii * A3LDP + jj] = f2bf(pdv);
+      }
+    if (drop) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) ps[r] += a3_sum16(pds[r]);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    // ---- O += Pd V (V [key][c] read transposed) ----
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const bf16x8 pa = *reinterpret_cast<const bf16x8*>(Pw + lo * A3LDP + ks * 32 + 8 * q4);
+#pragma unroll
+      for (int u = 0; u < NU; ++u)
+        oacc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, a3_tr_frag(Vs, LR, ks * 32, 16 * u, lane), oacc[u], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();   // Pw is rewritten by the next step
+  }
+  // ---- per-row log-sum-exp (3e38 for rows without a valid key) and O = centred sum + S_i vc ----
+  if (p.lse && lo == 0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = ib + r;
+      if (i < T) p.lse[bh * p.T + i] = (i < len && lrow[r] > 0.f) ? mrow[r] + logf(lrow[r]) : 3.0e38f;
+    }
+  }
+  float fin[4], sv[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const bool rv_ok = ib + r < len && lrow[r] > 0.f;
+    fin[r] = rv_ok ? 1.f / lrow[r] : 0.f;
+    sv[r] = drop ? ps[r] * fin[r] : (rv_ok ? 1.f : 0.f);
+  }
+  const float* vc = p.cen + bh * 2 * Gm::DKP + Gm::DKP;
+#pragma unroll
+  for (int u = 0; u < NU; ++u) {
+    const int c = 16 * u + lo;
+    const float v0 = vc[c];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = ib + r;
+      if (i < T && c < dk) p.o[(b * p.T + i) * p.d + hoff + c] = oacc[u][r] * fin[r] + sv[r] * v0;
+    }
+  }
+}
+
+}  // namespace
+}  // namespace kdfm
+
+extern "C" {
+
+int64_t kdfm_attn_kv_prep_elems(int64_t B, int64_t H, int64_t T, int64_t d) {
+  if (H <= 0 || d % H) return -1;
+  return B * H * kdfm::a3_tp(T) * (kdfm::a3_dkp(d / H) + 8);
+}
+
+int64_t kdfm_attn_centre_elems(int64_t B, int64_t H, int64_t d) {
+  if (H <= 0 || d % H) return -1;
+  return B * H * 2 * kdfm::a3_dkp(d / H);
+}
+
+int64_t kdfm_attn_band_prep_elems(int64_t layers, int64_t H, int64_t T, int64_t d) {
+  if (H <= 0 || d % H) return -1;
+  return layers * H * kdfm::a3_npb(T) * (kdfm::a3_dkp(d / H) + 8);
+}
+
+int kdfm_attn_kv_prep(const float* qkv, const int64_t* lengths, uint16_t* kb, uint16_t* vb, float* centre, int64_t B,
+                      int64_t H, int64_t T, int64_t d, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(qkv && kb && vb && centre, "null pointer");
+  KDFM_REQUIRE(H > 0 && d % H == 0 && d % 4 == 0, "d must be a multiple of H and of 4");
+  const int64_t dk = d / H;
+  KDFM_REQUIRE(dk % 4 == 0 && dk <= 128, "head dim must be a multiple of 4 and <= 128");
+  KDFM_REQUIRE(T > 0 && T <= 4096, "T out of range");
+  KDFM_REQUIRE((((uintptr_t)qkv | (uintptr_t)kb | (uintptr_t)vb) & 15) == 0, "operands must be 16-byte aligned");
+  if (B == 0) return KDFM_OK;
+  const int64_t Tp = a3_tp(T);
+  const dim3 grid((unsigned)(Tp / A3K), (unsigned)(B * H));
+  if (a3_dkp(dk) == 128)
+    hipLaunchKernelGGL(attn_kv_prep_kernel<128>, grid, dim3(256), 0, as_stream(stream), qkv, lengths, kb, vb, centre, H,
+                       (int)T, d, (int)dk, Tp);
+  else
+    hipLaunchKernelGGL(attn_kv_prep_kernel<64>, grid, dim3(256), 0, as_stream(stream), qkv, lengths, kb, vb, centre, H,
+                       (int)T, d, (int)dk, Tp);
+  return check_launch("kdfm_attn_kv_prep");
+}
+
+int kdfm_attn_band_prep(const float* pos, int64_t ld_layer, int64_t layers, uint16_t* pb, int64_t H, int64_t T,
+                        int64_t d, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(pos && pb, "null pointer");
+  KDFM_REQUIRE(H > 0 && d % H == 0 && d % 4 == 0, "d must be a multiple of H and of 4");
+  const int64_t dk = d / H;
+  KDFM_REQUIRE(dk % 4 == 0 && dk <= 128, "head dim must be a multiple of 4 and <= 128");
+  KDFM_REQUIRE(T > 0 && T <= 4096 && layers > 0, "T / layers out of range");
+  KDFM_REQUIRE(layers == 1 || ld_layer >= (2 * T - 1) * d, "layer stride too small");
+  KDFM_REQUIRE((((uintptr_t)pos | (uintptr_t)pb) & 15) == 0 && ld_layer % 4 == 0, "operands must be 16-byte aligned");
+  const int64_t npb = a3_npb(T);
+  const dim3 grid((unsigned)ceil_div(npb, 64), (unsigned)(layers * H));
+  if (a3_dkp(dk) == 128)
+    hipLaunchKernelGGL(attn_band_prep_kernel<128>, grid, dim3(256), 0, as_stream(stream), pos, ld_layer, pb, H, 2 * T - 1, d,
+                       (int)dk, npb);
+  else
+    hipLaunchKernelGGL(attn_band_prep_kernel<64>, grid, dim3(256), 0, as_stream(stream), pos, ld_layer, pb, H, 2 * T - 1, d,
+                       (int)dk, npb);
+  return check_launch("kdfm_attn_band_prep");
+}
+
+int kdfm_relpos_attn_fwd3(const float* qu, const float* qv, const uint16_t* kb, const uint16_t* vb, const float* centre,
+                          const uint16_t* pb, const int64_t* lengths, float* o, float* lse, int64_t B, int64_t H,
+                          int64_t T, int64_t d, float scale, float dropout_p, const uint64_t* seed, uint64_t rng_stream,
+                          void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(qu && qv && kb && vb && centre && pb && o, "null pointer");
+  KDFM_REQUIRE(H > 0 && d % H == 0 && d % 4 == 0, "d must be a multiple of H and of 4");
+  const int64_t dk = d / H;
+  KDFM_REQUIRE(dk % 4 == 0 && dk <= 128, "head dim must be a multiple of 4 and <= 128");
+  KDFM_REQUIRE(T > 0 && T <= 4096, "T out of range");
+  KDFM_REQUIRE(dropout_p == 0.f || seed, "dropout needs a seed");
+  KDFM_REQUIRE((((uintptr_t)qu | (uintptr_t)qv | (uintptr_t)kb | (uintptr_t)vb | (uintptr_t)pb) & 15) == 0,
+               "operands must be 16-byte aligned");
+  if (B == 0) return KDFM_OK;
+  Attn3P p;
+  p.qu = qu; p.qv = qv; p.kb = kb; p.vb = vb; p.cen = centre; p.pb = pb; p.lens = lengths;
+  p.o = o; p.lse = lse;
+  p.B = B; p.H = H; p.T = T; p.d = d; p.dk = dk; p.Tp = a3_tp(T); p.npb = a3_npb(T);
+  p.scale = scale; p.p_drop = dropout_p; p.seed = seed; p.rng_stream = rng_stream;
+  const dim3 grid((unsigned)ceil_div(T, A3Q), (unsigned)(B * H));
+  hipStream_t st = as_stream(stream);
+  if (dk > 64)
+    hipLaunchKernelGGL(relpos_attn_fwd3_kernel<8>, grid, dim3(256), 0, st, p);
+  else if (dk > 48)
+    hipLaunchKernelGGL(relpos_attn_fwd3_kernel<4>, grid, dim3(256), 0, st, p);
+  else
+    hipLaunchKernelGGL(relpos_attn_fwd3_kernel<3>, grid, dim3(256), 0, st, p);
+  return check_launch("kdfm_relpos_attn_fwd3");
+}
+
+}  // extern "C"

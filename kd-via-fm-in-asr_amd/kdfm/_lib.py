@@ -77,6 +77,14 @@ SIGNATURES: dict[str, tuple] = {
     "kdfm_relpos_attn_bwd_ws": (_i64, [_i64, _i64, _i64, _i64]),
     "kdfm_relpos_attn_bwd": (_i32, [P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, _i64, _i64, _i64, _i64, _i64, _f32, _f32, P,
                                     C.c_uint64, P]),
+    "kdfm_attn_kv_prep_elems": (_i64, [_i64, _i64, _i64, _i64]),
+    "kdfm_attn_centre_elems": (_i64, [_i64, _i64, _i64]),
+    "kdfm_attn_band_prep_elems": (_i64, [_i64, _i64, _i64, _i64]),
+    "kdfm_attn_kv_prep": (_i32, [P, P, P, P, P, _i64, _i64, _i64, _i64, P]),
+    "kdfm_attn_band_prep": (_i32, [P, _i64, _i64, P, _i64, _i64, _i64, P]),
+    "kdfm_relpos_attn_bwd2_dq3": (_i32, [P, P, P, P, P, P, P, P, P, P, P, P, P, P, _i64, _i64, _i64, _i64, _f32, _f32, P,
+                                         C.c_uint64, P]),
+    "kdfm_relpos_attn_fwd3": (_i32, [P, P, P, P, P, P, P, P, P, _i64, _i64, _i64, _i64, _f32, _f32, P, C.c_uint64, P]),
     "kdfm_relpos_attn_bwd2_ldt": (_i64, [_i64]),
     "kdfm_relpos_attn_bwd2_dpos_ws": (_i64, [_i64, _i64, _i64]),
     "kdfm_relpos_attn_bwd2_dq": (_i32, [P, P, P, P, P, P, P, P, P, P, P, P, P, _i64, _i64, _i64, _i64, _f32, _f32, P,

@@ -38,6 +38,13 @@ _ATTN_BWD2 = __import__("os").environ.get("KDFM_ATTN_BWD2", "1") == "1"
 # linear1, pointwise_conv2 with linear_out) leave as paired launches (kdfm_wgrad_bf16_pair, each product
 # bitwise its single launch's); KDFM_WGRAD_PAIRS=0: one launch per product
 _WGRAD_PAIRS = __import__("os").environ.get("KDFM_WGRAD_PAIRS", "1") == "1"
+# bf16 math, single-pass forward (bwd2 training / inference): the attention forward over prepared bf16 operands
+# (csrc/attn_fwd3.hip: keys / values centred and tiled once per layer, the positional band once per encoder, LDS-DMA
+# staging, rel_shift by lane permutes) -- bitwise the register-staged kernel's O / lse (KDFM_ATTN_FWD3=0: that kernel)
+_ATTN_FWD3 = __import__("os").environ.get("KDFM_ATTN_FWD3", "1") == "1"
+# ... and the bwd2 dQ kernel over the same prepared operands, kept from the forward (KDFM_ATTN_DQ3=0: it stages
+# K / V / the band from qkv / pos itself)
+_ATTN_DQ3 = __import__("os").environ.get("KDFM_ATTN_DQ3", "1") == "1"
 
 
 def _attn_fused_ok(dk, save):
@@ -419,8 +426,13 @@ def _ffn_forward(cfg, P, L, which, norm, x, pd, seed, salt, li, site_act, site_o
     return out, False
 
 
+def _fwd3_ok(dk, save):
+    """The prepared-operand attention forward applies (bf16 fused attention, single pass)."""
+    return _ATTN_FWD3 and _attn_fused_ok(dk, save) and (not save or (_ATTN_BWD_FUSED and _ATTN_BWD2))
+
+
 def layer_forward(cfg, S: EncoderShapes, P, L, li, x, out, pos_emb, lengths, *, train, seed, salt, save,
-                  bn_update=None, rm_batch=True, ppos=None, bn_stats=None):
+                  bn_update=None, rm_batch=True, ppos=None, bn_stats=None, pband=None):
     """x (rows, d) -> out (rows, d) (written in place).  Returns ctx for backward when save.
     ppos: this layer's projected positions linear_pos(pos_emb) (npos, d) when the caller computed
     every layer's at once (pos_proj_all); otherwise projected here.  bn_stats: a zeroed (2d,) f64 buffer
@@ -463,7 +475,20 @@ def layer_forward(cfg, S: EncoderShapes, P, L, li, x, out, pos_emb, lengths, *, 
         ppos = _empty(npos, d, dev=dev)
         K.linear(pos_emb, P[L + "self_attn.linear_pos.weight"], None, ppos)
     o = _empty(rows, d, dev=dev)
-    if _attn_fused_ok(dk, save):
+    if _fwd3_ok(dk, save):
+        # prepared operands: bf16 centred K / V tiles of this layer, the encoder's band rows (pband, or this
+        # layer's own); lse for the bwd2 backward when training
+        Pm = Pd = pt = mblk = None
+        lse = torch.empty(B, H, T, device=dev) if save else None
+        prep = K.attn_kv_prep(qkv, lengths, B, H, T)
+        if pband is None:
+            pband = K.attn_band_prep(ppos, H, T)[0]
+        K.relpos_attn_fwd3(qu, qv, prep, pband, lengths, o, B, H, T, 1.0 / math.sqrt(dk), pa, seed,
+                           _stream(salt, li, SITE_ATT_P), lse=lse)
+        if save and _ATTN_DQ3:
+            keep(attn_prep=prep, attn_pband=pband)
+        del prep
+    elif _attn_fused_ok(dk, save):
         # fused flash-style kernel: no AC / BD materialisation; P (and P_drop) only when the
         # backward needs them
         if _ATTN_BWD_FUSED:
@@ -798,8 +823,14 @@ def layer_backward(cfg, S: EncoderShapes, P, G, L, li, ctx, dout, pos_emb, lengt
         lse, pt, mblk = ctx["lse"], ctx["pt"], ctx["mblk"]
         if pt is None:   # bwd2
             dS, Pdr = K.attn_bwd2_saved(B, H, T, dev)
-            K.relpos_attn_bwd2_dq(do, ctx["o"], qu, qv, qkv, ppos, lse, lengths, None, dS, Pdr, dqu, dqv, B, H, T, sc,
-                                  ctx["pa"], seed, st_att)
+            prep = ctx.pop("attn_prep", None)
+            if prep is not None:   # the forward's prepared bf16 operands (fwd3)
+                K.relpos_attn_bwd2_dq3(do, ctx["o"], qu, qv, prep, ctx.pop("attn_pband"), lse, lengths, dS, Pdr, dqu, dqv,
+                                       B, H, T, sc, ctx["pa"], seed, st_att)
+                del prep
+            else:
+                K.relpos_attn_bwd2_dq(do, ctx["o"], qu, qv, qkv, ppos, lse, lengths, None, dS, Pdr, dqu, dqv, B, H, T,
+                                      sc, ctx["pa"], seed, st_att)
             dpws = torch.empty(K.relpos_attn_bwd2_dpos_ws(B, T, d), device=dev)
 
             def dpos_and_wgrad2():
@@ -962,6 +993,8 @@ def encoder_forward_steps(cfg, S: EncoderShapes, P, prefix, mel, mel_len, len1, 
     # after the yield: the caller issues the layers under their own stream, and the projections must be
     # allocated (torch's per-stream pools) and written on the stream whose layers read them
     pp = pos_proj_all(cfg, P, prefix, pos_emb)
+    # every layer's positional band rows for the prepared-operand attention forward in one launch
+    pbands = K.attn_band_prep(pp, S.h, S.T) if (pp is not None and _fwd3_ok(S.dk, save)) else None
     bn_stats = None
     if train and bn_running is not None and use_batch_stats:
         bn_stats = ws.get("bn_stats")
@@ -974,7 +1007,7 @@ def encoder_forward_steps(cfg, S: EncoderShapes, P, prefix, mel, mel_len, len1, 
             bn = (bn_running[L + "conv.batch_norm.running_mean"], bn_running[L + "conv.batch_norm.running_var"])
         ctx = layer_forward(cfg, S, P, L, i, x, feats[i], pos_emb, len2, train=train, seed=seed, salt=salt,
                             save=save, bn_update=bn, rm_batch=use_batch_stats, ppos=None if pp is None else pp[i],
-                            bn_stats=bn_stats)
+                            bn_stats=bn_stats, pband=None if pbands is None else pbands[i])
         if save:
             run.layers.append(ctx)
         x = feats[i]

@@ -1260,6 +1260,26 @@ def relpos_attn_bwd2_dq(do, o, qu, qv, qkv, ppos, lse, lengths, rsum, ds, pd, dq
             ptr(dqu), ptr(dqv), B, H, T, d, float(scale), float(p), ptr(seed), int(rng_stream), _s())
 
 
+def relpos_attn_bwd2_dq3(do, o, qu, qv, prep, pband, lse, lengths, ds, pd, dqu, dqv, B, H, T, scale, p, seed,
+                         rng_stream):
+    """bwd2 part 1 over the forward's prepared operands (attn_kv_prep's triple and this layer's attn_band_prep
+    slice, kdfm_relpos_attn_bwd2_dq3): the same outputs as relpos_attn_bwd2_dq."""
+    rows, d = do.shape
+    kb, vb, cen = prep
+    assert rows == B * T and lse.shape == (B, H, T) and o.shape == do.shape
+    assert ds.dtype == torch.bfloat16 and pd.dtype == torch.bfloat16
+    assert ds.shape == pd.shape and ds.shape[:3] == (B, H, T) and ds.is_contiguous() and pd.is_contiguous()
+    for t in (do, o, qu, qv, lse, dqu, dqv):
+        assert t.is_contiguous()
+    tt = 2.0 * B * H * T * T * (d // H)
+    # scores (QK^T + band), dP, dQu, dQv: 5 T x T products; bytes: dO, O, qu, qv read, dqu, dqv written (f32), the
+    # bf16 K / V images read, dS and Pd written (bf16)
+    _traced("attn_bwd", 5 * tt, 4.0 * rows * d * 6 + 2.0 * 2 * kb.numel() + 2.0 * 2.0 * B * H * T * T,
+            "kdfm_relpos_attn_bwd2_dq3", ptr(do), ptr(o), ptr(qu), ptr(qv), ptr(kb), ptr(vb), ptr(cen), ptr(pband),
+            ptr(lse), ptr(_i64(lengths)), ptr(ds), ptr(pd), ptr(dqu), ptr(dqv), B, H, T, d, float(scale), float(p),
+            ptr(seed), int(rng_stream), _s())
+
+
 def relpos_attn_bwd2_dkv(do, qu, ds, pd, lengths, dqkv, B, H, T):
     """bwd2 part 2: dK / dV into dqkv[:, d:] / [:, 2d:] from the saved dS / Pd (no recompute)."""
     rows, d = do.shape
@@ -1309,6 +1329,61 @@ def relpos_attn_fwd(qu, qv, qkv, ppos, lengths, o, P, Pd, B, H, T, scale, p, see
     _traced("attn_fwd", fl, nb, "kdfm_relpos_attn_fwd", ptr(qu), ptr(qv), ptr(qkv), ptr(ppos), ptr(_i64(lengths)),
             ptr(o), ptr(P), ptr(Pd), ptr(lse), ptr(p_tilde), ptr(m_blk), B, H, T, d, float(scale), float(p), ptr(seed),
             rng_stream, _s())
+
+
+def attn_kv_prep(qkv, lengths, B, H, T, out=None):
+    """The bf16 centred key / value tiles and the centre of kdfm_relpos_attn_fwd3 (csrc/attn_fwd3.hip):
+    returns (kb, vb, centre); `out` reuses a previous triple of the same shape."""
+    rows, d3 = qkv.shape
+    d = d3 // 3
+    assert rows == B * T and qkv.is_contiguous() and qkv.dtype == torch.float32
+    n = int(_lib.lib().kdfm_attn_kv_prep_elems(B, H, T, d))
+    nc = int(_lib.lib().kdfm_attn_centre_elems(B, H, d))
+    if n < 0 or nc < 0:
+        raise _lib.KdfmError(f"attn_kv_prep: unsupported d={d} H={H}")
+    if out is None:
+        out = (torch.empty(n, dtype=torch.bfloat16, device=qkv.device),
+               torch.empty(n, dtype=torch.bfloat16, device=qkv.device), torch.empty(nc, device=qkv.device))
+    kb, vb, cen = out
+    assert kb.numel() >= n and vb.numel() >= n and cen.numel() >= nc
+    # read K, V (f32) once, write the two bf16 images (padded rows / columns)
+    _traced("attn_prep", 0.0, 4.0 * rows * 2 * d + 2.0 * 2 * n, "kdfm_attn_kv_prep", ptr(qkv), ptr(_i64(lengths)),
+            ptr(kb), ptr(vb), ptr(cen), B, H, T, d, _s())
+    return out
+
+
+def attn_band_prep(pos, H, T, out=None):
+    """Every layer's projected positions pos (layers, 2T-1, d) (or one layer's (2T-1, d)) as the bf16 band rows
+    of kdfm_relpos_attn_fwd3: returns pb (layers, H * NPB * LR) -- pb[l] is layer l's slice."""
+    if pos.dim() == 2:
+        pos = pos.unsqueeze(0)
+    L, npos, d = pos.shape
+    assert npos == 2 * T - 1 and pos.stride(2) == 1 and pos.stride(1) == d and pos.dtype == torch.float32
+    n = int(_lib.lib().kdfm_attn_band_prep_elems(1, H, T, d))
+    if n < 0:
+        raise _lib.KdfmError(f"attn_band_prep: unsupported d={d} H={H}")
+    if out is None:
+        out = torch.empty(L, n, dtype=torch.bfloat16, device=pos.device)
+    assert out.shape[0] >= L and out.shape[1] == n and out.is_contiguous()
+    _traced("attn_prep", 0.0, 4.0 * L * npos * d + 2.0 * L * n, "kdfm_attn_band_prep", ptr(pos),
+            pos.stride(0) if L > 1 else npos * d, L, ptr(out), H, T, d, _s())
+    return out
+
+
+def relpos_attn_fwd3(qu, qv, prep, pband, lengths, o, B, H, T, scale, p, seed, rng_stream, lse=None):
+    """kdfm_relpos_attn_fwd3: the single-pass fused forward over the prepared operands (attn_kv_prep's triple,
+    one layer's attn_band_prep slice); O / lse bitwise relpos_attn_fwd's single pass."""
+    rows, d = qu.shape
+    kb, vb, cen = prep
+    assert rows == B * T and o.shape == (rows, d) and qu.is_contiguous() and qv.is_contiguous()
+    assert lse is None or lse.shape == (B, H, T)
+    assert pband.dtype == torch.bfloat16 and pband.numel() == int(_lib.lib().kdfm_attn_band_prep_elems(1, H, T, d))
+    # algorithmic: QK^T, the positional band (one T x T-equivalent) and PV per (b, h); bytes: qu, qv, o (f32) and
+    # the bf16 key / value images once (+ lse)
+    fl = 2.0 * B * H * T * T * (d // H) * 3
+    nb = 4.0 * rows * d * 3 + 2.0 * 2 * kb.numel() + (4.0 * B * H * T if lse is not None else 0.0)
+    _traced("attn_fwd", fl, nb, "kdfm_relpos_attn_fwd3", ptr(qu), ptr(qv), ptr(kb), ptr(vb), ptr(cen), ptr(pband),
+            ptr(_i64(lengths)), ptr(o), ptr(lse), B, H, T, d, float(scale), float(p), ptr(seed), int(rng_stream), _s())
 
 
 def relpos_softmax_fwd(ac, bd, lengths, P, Pd, B, H, T, scale, p, seed, rng_stream):
