@@ -263,8 +263,12 @@ __global__ __launch_bounds__(256, NU == 3 ? 3 : 2) void relpos_attn_fwd3_kernel(
     for (int r = 0; r < 4; ++r) {
       float X[5];
 #pragma unroll
-      for (int t = 0; t < 5; ++t)
-        X[t] = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(bsrc_lane[r], __builtin_bit_cast(int, g[t][r])));
+      for (int t = 0; t < 5; ++t) {
+        // (the element is copied out first: __builtin_bit_cast of a vector-element lvalue read element 0 for
+        // every r on this compiler -- rows 4q+1..3 of every 16-row tile came out wrong)
+        const float gv = g[t][r];
+        X[t] = __int_as_float(__builtin_amdgcn_ds_bpermute(bsrc_lane[r], __float_as_int(gv)));
+      }
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         const float bd = bhi[r] ? X[t + 1] : X[t];

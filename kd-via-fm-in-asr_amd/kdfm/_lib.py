@@ -85,6 +85,8 @@ SIGNATURES: dict[str, tuple] = {
     "kdfm_relpos_attn_bwd2_dq3": (_i32, [P, P, P, P, P, P, P, P, P, P, P, P, P, P, _i64, _i64, _i64, _i64, _f32, _f32, P,
                                          C.c_uint64, P]),
     "kdfm_relpos_attn_fwd3": (_i32, [P, P, P, P, P, P, P, P, P, _i64, _i64, _i64, _i64, _f32, _f32, P, C.c_uint64, P]),
+    "kdfm_unfold1d": (_i32, [P, _i64, P, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _i32, P]),
+    "kdfm_fold1d": (_i32, [P, P, _i64, P, P, _i64, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _i32, P]),
     "kdfm_relpos_attn_bwd2_ldt": (_i64, [_i64]),
     "kdfm_relpos_attn_bwd2_dpos_ws": (_i64, [_i64, _i64, _i64]),
     "kdfm_relpos_attn_bwd2_dq": (_i32, [P, P, P, P, P, P, P, P, P, P, P, P, P, _i64, _i64, _i64, _i64, _f32, _f32, P,

@@ -66,8 +66,12 @@ class Ver5Config:
     # --sampling_steps_per_layer stops there); the engine runs the value that line names.
     encfm_flow_steps: int = 8
     # FlowMatchingModule meta_encoder_type (--meta_encoder_type, asr_train.py:1241-1279): "mlp" (router or
-    # fixed steps, kdfm/encfm.py) or "cnn" / "swin" (fixed steps, kdfm/fmmeta.py)
+    # fixed steps, kdfm/encfm.py) or "cnn" / "swin" / "conformer" / "unet" (fixed steps, kdfm/fmmeta.py;
+    # "unet" runs only at an even frame count, as in the reference)
     encfm_meta: str = "mlp"
+    # flow_cfg hidden_dim (--hidden_dim, asr_train.py:1753): the U-Net meta-encoder's base width (UNet1D
+    # base_ch, :1271-1276); the mlp meta-encoder and the router are built for 128 (ENCFM_HIDDEN)
+    encfm_hidden: int = 128
     router_max_steps: int = 8
     router_weight: float = 1.0
     flow_schedule: str = "rectified"
@@ -268,8 +272,37 @@ def meta_specs(cfg: Ver5Config) -> list:
     if cfg.encfm_meta == "conformer":   # ConformerEncoder (:1000-1020), kdfm/fmconf.py
         from .fmconf import conformer_specs
         return conformer_specs(Cs, E)
-    # "unet" (UNet1D, :880-917: odd frame counts crash the reference's update x - v / S) is not on the engine
-    raise ValueError(f"encfm_meta must be 'mlp', 'cnn', 'swin' or 'conformer', got {cfg.encfm_meta!r}")
+    if cfg.encfm_meta == "unet":   # UNet1D(in Ci, base hidden_dim, out Cs, 4 layers) (:880-917, 1271-1276)
+        return unet_specs(Cs, E, cfg.encfm_hidden)
+    raise ValueError(f"encfm_meta must be 'mlp', 'cnn', 'swin', 'conformer' or 'unet', got {cfg.encfm_meta!r}")
+
+
+UNET_LAYERS = 4   # UNet1D num_layers (asr_train.py:1275)
+
+
+def unet_channels(Cs, E, base, layers=UNET_LAYERS):
+    """UNet1D's widths: down i maps c_in[i] -> c_down[i] = base 2^i (Conv1d k 4 s 2 p 1); the bottleneck keeps
+    c_down[-1]; up j maps c_up_in[j] = c_prev + skip (deepest skip first) -> that skip's width."""
+    cin = [Cs + E] + [base * 2 ** i for i in range(layers - 1)]
+    cdown = [base * 2 ** i for i in range(layers)]
+    ups, ch = [], cdown[-1]
+    for skip in reversed(cdown):
+        ups.append((ch + skip, skip))
+        ch = skip
+    return cin, cdown, ups
+
+
+def unet_specs(Cs, E, base, layers=UNET_LAYERS):
+    me = "flow_matching.meta_encoder."
+    cin, cdown, ups = unet_channels(Cs, E, base, layers)
+    s = []
+    for i in range(layers):
+        s += [(me + f"downs.{i}.weight", (cdown[i], cin[i], 4)), (me + f"downs.{i}.bias", (cdown[i],))]
+    s += [(me + "bottleneck.weight", (cdown[-1], cdown[-1], 3)), (me + "bottleneck.bias", (cdown[-1],))]
+    for j, (ci, co) in enumerate(ups):   # ConvTranspose1d weight: (in, out, k)
+        s += [(me + f"ups.{j}.weight", (ci, co, 4)), (me + f"ups.{j}.bias", (co,))]
+    s += [(me + "final.weight", (Cs, cdown[0], 1)), (me + "final.bias", (Cs,))]
+    return s
 
 
 def meta_bn_specs(cfg: Ver5Config) -> list:

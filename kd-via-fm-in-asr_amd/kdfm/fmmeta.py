@@ -32,15 +32,16 @@ from .config import encfm_fixed_steps
 from .encfm import schedule_coeffs
 from .mha import mha_bwd, mha_fwd
 
-META_TYPES = ("mlp", "cnn", "swin", "conformer")
+META_TYPES = ("mlp", "cnn", "swin", "conformer", "unet")
 
 
 class MetaFMWorkspace:
     """Per-(B, T) resident buffers for the meta-encoder chain (fixed steps, so every size is static)."""
 
     def __init__(self, cfg, B, T, dev):
-        if cfg.encfm_meta not in ("cnn", "swin", "conformer"):
-            raise ValueError(f"MetaFMWorkspace is for the cnn / swin / conformer meta-encoders, got {cfg.encfm_meta!r}")
+        if cfg.encfm_meta not in ("cnn", "swin", "conformer", "unet"):
+            raise ValueError(f"MetaFMWorkspace is for the cnn / swin / conformer / unet meta-encoders, got "
+                             f"{cfg.encfm_meta!r}")
         L, Cs, Ct, E = cfg.n_layers, cfg.d_student, cfg.d_teacher, cfg.time_embed_dim
         if cfg.encfm_dynamic:
             raise ValueError("meta_encoder 'cnn' / 'swin' run with fixed step counts (encfm_dynamic=False)")
@@ -73,6 +74,8 @@ class MetaFMWorkspace:
         elif self.meta == "conformer":
             from .fmconf import ConformerMeta
             self.conf = ConformerMeta(cfg, n, B, T, N, dev)
+        elif self.meta == "unet":
+            self.unet = _UNetWs(cfg, B, T, N, dev)
         else:
             H = cfg.heads_student
             if Ci % H or (Ci // H) % 4 or Ci // H > 64:
@@ -96,9 +99,56 @@ class MetaFMWorkspace:
         return self.mha
 
 
+class _UNetWs:
+    """UNet1D (asr_train.py:880-917) buffers: per meta call k the concatenated up-path inputs of every level,
+    cat[l][k] = [x part | skip of level l] (B * L_l rows; the skip is the down conv's output, written straight
+    into its columns; the x part the bottleneck's (l = 4) or the next-deeper up's output, written by the fold,
+    its rows past 2 L_{l+1} the reference's zero pad), and the last up's output (B * 2 L_1, base); the backward
+    re-reads them (UNet1D has no nonlinearity: no other saves).  Scratch for the unfolded columns, the
+    transposed convs' GEMM outputs and the gradients is shared by the calls."""
+
+    def __init__(self, cfg, B, T, N, dev):
+        from .config import UNET_LAYERS, unet_channels
+        Cs, E, base = cfg.d_student, cfg.time_embed_dim, cfg.encfm_hidden
+        nl = UNET_LAYERS
+        L = [T]
+        for _ in range(nl):
+            L.append(L[-1] // 2)
+        if 2 * L[1] != T:
+            # the reference's update x - v / S then fails (asr_train.py:1358): UNet1D returns T - 1 frames
+            raise ValueError(f"meta_encoder 'unet' needs an even frame count: UNet1D returns {2 * L[1]} frames for "
+                             f"T={T} and the reference's x - velocity / S fails (RuntimeError: The size of tensor a "
+                             f"({T}) must match the size of tensor b ({2 * L[1]}) at non-singleton dimension 1)")
+        if any(v == 0 for v in L):
+            raise ValueError(f"meta_encoder 'unet': T={T} frames is too short for {nl} stride-2 levels")
+        if base % 4 or (Cs + E) % 4 or Cs % 4:
+            raise ValueError("meta_encoder 'unet': channel counts must be multiples of 4")
+        self.cin, self.cdown, self.ups = unet_channels(Cs, E, base, nl)
+        self.L, self.nl, self.B, self.T = L, nl, B, T
+        # x-part width per level l = 1..nl (index l): the bottleneck's at the deepest level, else the up output
+        self.cx = [0] + [self.cdown[l] for l in range(1, nl)] + [self.cdown[-1]]
+        f = lambda *s: torch.empty(*s, device=dev)  # noqa: E731
+        self.cat = [None] + [f(N, B * L[l], self.cx[l] + self.cdown[l - 1]) for l in range(1, nl + 1)]
+        self.up_last = f(N, B * 2 * L[1], self.cdown[0])
+        rows = max(B * L[i + 1] * 4 * self.cin[i] for i in range(nl))
+        zrows = max(B * L[nl - j] * 4 * co for j, (_, co) in enumerate(self.ups))
+        self.cols = f(max(rows, zrows))              # unfold / dZ scratch
+        self.z = f(zrows)                            # transposed convs' GEMM outputs
+        self.dcat = [None] + [f(B * L[l], self.cx[l] + self.cdown[l - 1]) for l in range(1, nl + 1)]
+        self.dup = f(B * 2 * L[1], self.cdown[0])
+        self.dbcols = f(max(B * 2 * L[l] * co for l, (_, co) in zip(range(nl, 0, -1), self.ups)))
+        # weight layouts (kdfm_convw_prep) and GEMM-layout gradient accumulators
+        self.wd = [f(self.cdown[i], 4 * self.cin[i]) for i in range(nl)]
+        self.gd = [f(self.cdown[i], 4 * self.cin[i]) for i in range(nl)]
+        cb = self.cdown[-1]
+        self.wbf, self.wbb, self.gb = f(cb, 3 * cb), f(cb, 3 * cb), f(cb, 3 * cb)
+        self.wu = [f(ci, 4 * co) for ci, co in self.ups]
+        self.gu = [f(ci, 4 * co) for ci, co in self.ups]
+
+
 def _names(meta):
     me = "flow_matching.meta_encoder."
-    if meta == "conformer":
+    if meta in ("conformer", "unet"):
         return {}
     if meta == "cnn":
         return dict(w0=me + "0.weight", b0=me + "0.bias", w2=me + "2.weight", b2=me + "2.bias")
@@ -107,10 +157,92 @@ def _names(meta):
                 w2=me + "linear2.weight", b2=me + "linear2.bias")
 
 
+UME = "flow_matching.meta_encoder."
+
+
+def _unet_prep(u, P):
+    """The step's GEMM weight layouts of the U-Net's convs (kdfm_convw_prep): downs (out, 4 in) tap-major, the
+    bottleneck's forward and flipped data-gradient layouts, the transposed convs (in, out, 4) as (in, 4 out)."""
+    for i in range(u.nl):
+        K.convw_prep(P[UME + f"downs.{i}.weight"], fwd=u.wd[i])
+    K.convw_prep(P[UME + "bottleneck.weight"], fwd=u.wbf, bwd=u.wbb)
+    for j in range(u.nl):
+        K.convw_prep(P[UME + f"ups.{j}.weight"], fwd=u.wu[j])
+
+
+def _unet_fwd(u, P, k, x, out, R, rscale):
+    """UNet1D on slab k's [x | e] rows (B * T, Ci) -> out = v (R None) or R + rscale * v (B * T, Cs)."""
+    B, L, nl = u.B, u.L, u.nl
+    inp = x
+    for i in range(nl):   # Conv1d(k 4, s 2, p 1): unfold + GEMM, straight into the level's skip columns
+        l = i + 1
+        cols = u.cols[:B * L[l] * 4 * u.cin[i]].view(B * L[l], 4 * u.cin[i])
+        K.unfold1d(inp, cols, B, L[i], L[l])
+        skip = u.cat[l][k][:, u.cx[l]:]
+        K.linear(cols, u.wd[i], P[UME + f"downs.{i}.bias"], skip)
+        inp = skip
+    # bottleneck Conv1d(k 3, p 1) into the deepest level's x part
+    K.conv3(inp, u.wbf, P[UME + "bottleneck.bias"], u.cat[nl][k][:, :u.cx[nl]], L[nl])
+    for j, (ci, co) in enumerate(u.ups):   # ConvTranspose1d(k 4, s 2, p 1) = GEMM + fold (zero pad past 2 L_l)
+        l = nl - j
+        Z = u.z[:B * L[l] * 4 * co].view(B * L[l], 4 * co)
+        K.linear_dx(u.cat[l][k], u.wu[j], Z)
+        dst, Lout = (u.cat[l - 1][k][:, :u.cx[l - 1]], L[l - 1]) if l > 1 else (u.up_last[k], 2 * L[1])
+        K.fold1d(Z, dst, B, L[l], Lout, bias=P[UME + f"ups.{j}.bias"], Lbias=2 * L[l])
+    epi = _lib.EPI_RESID if R is not None else 0
+    K.linear(u.up_last[k], P[UME + "final.weight"].view(out.shape[1], -1), P[UME + "final.bias"], out, epi=epi, R=R,
+             rscale=rscale)
+
+
+def _unet_bwd(u, P, G, k, x, dv, dembed):
+    """dembed = d/d[x | e] of slab k's U-Net given dv; parameter gradients into G (final / biases directly, the
+    conv weights into the GEMM-layout accumulators u.gd / u.gb / u.gu, re-laid out once in meta_backward)."""
+    B, L, nl = u.B, u.L, u.nl
+    Cs = dv.shape[1]
+    K.linear_dw(dv, u.up_last[k], G[UME + "final.weight"].view(Cs, -1), db=G[UME + "final.bias"])
+    K.linear_dx(dv, P[UME + "final.weight"].view(Cs, -1), u.dup)
+    for j in range(nl - 1, -1, -1):   # ups, last first: d_out -> dZ (unfold of the conv's own 2 L_l rows)
+        ci, co = u.ups[j]
+        l = nl - j
+        dout, Lout = (u.dcat[l - 1][:, :u.cx[l - 1]], L[l - 1]) if l > 1 else (u.dup, 2 * L[1])
+        # bias gradient: the sum over the 2 L_l frames the transposed conv writes (not the zero pad)
+        db = u.dbcols[:B * 2 * L[l] * co].view(B * 2 * L[l], co)
+        K.unfold1d(dout, db, B, Lout, 2 * L[l], K=1, S=1, P=0, Lvalid=2 * L[l])
+        K.colsum(db, G[UME + f"ups.{j}.bias"])
+        dZ = u.cols[:B * L[l] * 4 * co].view(B * L[l], 4 * co)
+        K.unfold1d(dout, dZ, B, Lout, L[l], Lvalid=2 * L[l])
+        K.linear_dw(u.cat[l][k], dZ, u.gu[j])
+        K.linear(dZ, u.wu[j], None, u.dcat[l])
+    # bottleneck: its output gradient is the deepest level's x part; the input is that level's skip
+    dy = u.dcat[nl][:, :u.cx[nl]]
+    skip = u.cat[nl][k][:, u.cx[nl]:]
+    K.conv3_dw(dy, skip, u.gb, L[nl], db=G[UME + "bottleneck.bias"])
+    # the skip columns of dcat[l] accumulate the skip's whole gradient in place (the up path's share, then the
+    # down path's: R aliases the output, each element read and written by one thread)
+    dsk = u.dcat[nl][:, u.cx[nl]:]
+    K.conv3(dy, u.wbb, None, dsk, L[nl], R=dsk, rscale=1.0)
+    for i in range(nl - 1, -1, -1):   # downs, deepest first: dW from the re-unfolded input, data grad = GEMM + fold
+        l = i + 1
+        inp = x if i == 0 else u.cat[i][k][:, u.cx[i]:]
+        cols = u.cols[:B * L[l] * 4 * u.cin[i]].view(B * L[l], 4 * u.cin[i])
+        K.unfold1d(inp, cols, B, L[i], L[l])
+        dy = u.dcat[l][:, u.cx[l]:]
+        K.linear_dw(dy, cols, u.gd[i], db=G[UME + f"downs.{i}.bias"])
+        K.linear_dx(dy, u.wd[i], cols)
+        if i == 0:
+            K.fold1d(cols, dembed, B, L[l], L[0])
+        else:
+            dprev = u.dcat[i][:, u.cx[i]:]
+            K.fold1d(cols, dprev, B, L[l], L[i], R=dprev)
+
+
 def _meta_fwd(ws, P, nm, k, out, R, rscale, seed=None, bn_running=None, train=True):
     """One meta-encoder evaluation on slab k: out = v (R None) or R + rscale * v."""
     Cs = out.shape[1]
     x = ws.embed[k]
+    if ws.meta == "unet":
+        _unet_fwd(ws.unet, P, k, x, out, R, rscale)
+        return
     epi = _lib.EPI_RESID if R is not None else 0
     if ws.meta == "conformer":
         from .fmconf import conformer_fwd
@@ -135,6 +267,9 @@ def _meta_bwd(ws, P, G, nm, k, dv, dembed, seed=None):
     """dembed = d/d[x | e] of slab k's meta-encoder given dv; parameter gradients accumulated into G."""
     Cs = dv.shape[1]
     x = ws.embed[k]
+    if ws.meta == "unet":
+        _unet_bwd(ws.unet, P, G, k, x, dv, dembed)
+        return
     if ws.meta == "conformer":
         from .fmconf import conformer_bwd
         conformer_bwd(ws.conf, P, G, k, x, dv, dembed, seed)
@@ -166,6 +301,8 @@ def meta_forward(cfg, P, sfeats, tfeats, ws: MetaFMWorkspace, *, seed=None, bn_r
     nm = _names(ws.meta)
     if ws.meta == "cnn":
         K.convw_prep(P[nm["w0"]], fwd=ws.w0f)
+    if ws.meta == "unet":
+        _unet_prep(ws.unet, P)
     wte, bte = P[fm + "time_embed.weight"].view(1, E), P[fm + "time_embed.bias"].view(1, E)
     Wst, bst = P[fm + "shape_transformation_function.weight"], P[fm + "shape_transformation_function.bias"]
     K.fill(ws.flow, 0.0)
@@ -209,6 +346,11 @@ def meta_backward(cfg, P, G, ws: MetaFMWorkspace, dfeats, gxS, *, seed=None):
     if ws.meta == "cnn":
         K.convw_prep(P[nm["w0"]], bwd=ws.w0b)
         K.fill(ws.g0, 0.0)
+    if ws.meta == "unet":
+        u = ws.unet
+        _unet_prep(u, P)   # (the forward's layouts of the same weights: re-prepared, the step may reuse them)
+        for g_ in u.gd + u.gu + [u.gb]:
+            K.fill(g_, 0.0)
     for i in range(L - 1, -1, -1):
         S, b0 = ws.steps[i], ws.base[i]
         K.linear_dx(ws.dtr[i], Wst, ws.dnsx)
@@ -234,6 +376,12 @@ def meta_backward(cfg, P, G, ws: MetaFMWorkspace, dfeats, gxS, *, seed=None):
         K.axpby(ws.gx, ws.dnsx, dfeats[i], 1.0, ws.ca[i])
     if ws.meta == "cnn":
         K.convw_grad(ws.g0, G[nm["w0"]])
+    if ws.meta == "unet":
+        u = ws.unet
+        for i in range(u.nl):
+            K.convw_grad(u.gd[i], G[UME + f"downs.{i}.weight"])
+            K.convw_grad(u.gu[i], G[UME + f"ups.{i}.weight"])
+        K.convw_grad(u.gb, G[UME + "bottleneck.weight"])
 
 
 __all__ = ["META_TYPES", "MetaFMWorkspace", "meta_forward", "meta_backward"]

@@ -552,6 +552,25 @@ def dropout(x, out, p, scale, seed, rng_stream):
     call("kdfm_dropout", ptr(x), ptr(out), x.numel(), float(p), float(scale), ptr(seed), int(rng_stream), _s())
 
 
+def unfold1d(x, cols, B, Lin, Lrows, K=4, S=2, P=1, Lvalid=None):
+    """cols[(b, i), k*C + c] = x[(b, S i - P + k), c] (0 outside [0, Lvalid), default Lin): x (B*Lin, C) rows, may be
+    a column slice of a wider buffer (x.stride(1) == 1)."""
+    C = x.shape[1]
+    assert x.shape[0] == B * Lin and x.stride(1) == 1 and cols.shape == (B * Lrows, K * C) and cols.is_contiguous()
+    call("kdfm_unfold1d", ptr(x), x.stride(0), ptr(cols), B, Lin, Lin if Lvalid is None else Lvalid, Lrows, C, K, S, P,
+         _s())
+
+
+def fold1d(cols, out, B, Lrows, Lout, *, K=4, S=2, P=1, bias=None, R=None, Lbias=None):
+    """out[(b, t), c] = R + bias (t < Lbias) + the taps of cols that land on t (transposed-conv overlap-add); out
+    (B*Lout, C) may be a column slice of a wider buffer; R may alias out."""
+    C = out.shape[1]
+    assert out.shape[0] == B * Lout and out.stride(1) == 1 and cols.shape == (B * Lrows, K * C) and cols.is_contiguous()
+    assert R is None or (R.shape == out.shape and R.stride(1) == 1)
+    call("kdfm_fold1d", ptr(cols), ptr(out), out.stride(0), ptr(bias), ptr(R), R.stride(0) if R is not None else 0, B,
+         Lrows, Lout, Lout if Lbias is None else Lbias, C, K, S, P, _s())
+
+
 def convw_prep(W, fwd=None, bwd=None):
     O, I, K = W.shape
     call("kdfm_convw_prep", ptr(W.contiguous()), ptr(fwd), ptr(bwd), O, I, K, _s())

@@ -161,7 +161,32 @@ def meta_velocity(P, e, meta="mlp", heads=2, bn_state=None):
         return _lin(torch.relu(_lin(ao, P, me + "linear1")), P, me + "linear2")
     if meta == "conformer":
         return _conformer_meta(P, e, heads, bn_state)
-    raise ValueError(f"meta-encoder {meta!r} not in the oracle (mlp, cnn, swin, conformer)")
+    if meta == "unet":
+        return _unet_meta(P, e)
+    raise ValueError(f"meta-encoder {meta!r} not in the oracle (mlp, cnn, swin, conformer, unet)")
+
+
+def _unet_meta(P, e, num_layers=4):
+    """UNet1D (asr_train.py:880-917) over the frames of each utterance, e (B, T, Cin) -> (B, T', Cs): num_layers
+    Conv1d(k 4, stride 2, pad 1) downs (each output kept as a skip), Conv1d(k 3, pad 1) bottleneck, then per
+    skip (deepest first) zero-pad x at the end to the skip's length, concatenate [x | skip] on channels and
+    ConvTranspose1d(k 4, stride 2, pad 1); Conv1d(k 1) final.  T' = 2 floor(T / 2): odd T gives T - 1 frames
+    (the reference's update x - v / S then fails to broadcast -- fm_forward raises likewise)."""
+    me = "flow_matching.meta_encoder."
+    F = torch.nn.functional
+    x = e.transpose(1, 2)
+    skips = []
+    for i in range(num_layers):
+        x = F.conv1d(x, P[me + f"downs.{i}.weight"], P[me + f"downs.{i}.bias"], stride=2, padding=1)
+        skips.append(x)
+    x = F.conv1d(x, P[me + "bottleneck.weight"], P[me + "bottleneck.bias"], padding=1)
+    for i in range(num_layers):
+        skip = skips.pop()
+        if x.shape[2] != skip.shape[2]:
+            x = F.pad(x, (0, skip.shape[2] - x.shape[2]))
+        x = F.conv_transpose1d(torch.cat([x, skip], dim=1), P[me + f"ups.{i}.weight"], P[me + f"ups.{i}.bias"],
+                               stride=2, padding=1)
+    return F.conv1d(x, P[me + "final.weight"], P[me + "final.bias"]).transpose(1, 2)
 
 
 def fm_forward(P, x0, tf, S, schedule="rectified", meta="mlp", heads=2, bn_state=None):

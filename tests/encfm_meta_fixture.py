@@ -32,9 +32,11 @@ def params(z, meta, seed=SEED, dtype=torch.float32):
     return out
 
 
-def inputs(z, seed=SEED, Cs=88, Ct=176):
-    """(s list, t list, R) of (B, T, C) float32 tensors, drawn as the generator drew them."""
-    L, B, T = int(z["meta.L"]), int(z["meta.B"]), int(z["meta.T"])
+def inputs(z, seed=SEED, Cs=88, Ct=176, T=None):
+    """(s list, t list, R) of (B, T, C) float32 tensors, drawn as the generator drew them (T: the unet entries'
+    own frame count, "unet.meta.T")."""
+    L, B = int(z["meta.L"]), int(z["meta.B"])
+    T = int(z["meta.T"]) if T is None else int(T)
     gi = torch.Generator().manual_seed(seed + 99)
     s = [0.5 * torch.randn(B, T, Cs, generator=gi) for _ in range(L)]
     t = [torch.randn(B, T, Ct, generator=gi) for _ in range(L)]

@@ -14,7 +14,10 @@ the FM output and the gradients of the objective w.r.t. every parameter and ever
 Combinations the reference cannot run are NOT fixtures (tests/golden/README-style notes in DESIGN.md):
 shape_transform "conv1d" applies Conv1d(88, 176, 1) to a (B, T, 88) tensor (RuntimeError unless T == 88),
 loss "cosine" calls CosineEmbeddingLoss without its target (TypeError), "unet" with an odd frame count
-returns T-1 frames and the update x - v / S fails to broadcast.
+returns T-1 frames and the update x - v / S fails to broadcast.  "unet" (UNet1D, :880-917) is written at an
+EVEN frame count (T = 36: its skip lengths 18, 9, 4, 2 exercise the up path's zero pad) with hidden_dim 8 (the
+U-Net's base width: 8 .. 64 channels instead of 128 .. 1024 keeps the fixture small; the layer structure is
+the same), under "unet.*" with its own "unet.meta.T" / "unet.meta.hidden".
 
 Usage:  python tests/golden/make_golden_encfm_meta.py
 """
@@ -62,10 +65,10 @@ def load_reference():
     return ns
 
 
-def run(ns, meta, L, B, T, steps, seed):
+def run(ns, meta, L, B, T, steps, seed, hidden=128):
     Cs, Ct = 88, 176
     torch.manual_seed(seed)
-    flow_cfg = {"meta_encoder_type": meta, "time_embed_dim": 32, "hidden_dim": 128, "training_sampling": 8,
+    flow_cfg = {"meta_encoder_type": meta, "time_embed_dim": 32, "hidden_dim": hidden, "training_sampling": 8,
                 "inference_sampling": 8, "weight": 1.0, "noise_schedule": "rectified", "loss": "mse",
                 "shape_transform": "linear", "student_dim": Cs, "teacher_dim": Ct, "student_head_num": 2,
                 "teacher_head_num": 4}
@@ -112,6 +115,11 @@ def main(L=2, B=2, T=32, steps=(2, 3), seed=7):
         got = run(ns, meta, L, B, T, steps, seed)
         arrays.update(got)
         print(meta, "params", len(got[meta + ".names"]), "total", float(got[meta + ".total"]))
+    unet_T, unet_hidden = 36, 8
+    got = run(ns, "unet", L, B, unet_T, steps, seed, hidden=unet_hidden)
+    arrays.update(got)
+    arrays.update({"unet.meta.T": np.array(unet_T), "unet.meta.hidden": np.array(unet_hidden)})
+    print("unet params", len(got["unet.names"]), "total", float(got["unet.total"]))
     np.savez_compressed(OUT, **arrays)
     print("wrote", OUT, os.path.getsize(OUT), "bytes")
 

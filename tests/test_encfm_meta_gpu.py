@@ -25,11 +25,11 @@ def _rel(a, b):
 # only (measured <= 1.6e-2).  swin: + the fused attention pair's bf16 P / dS, whose error the time
 # embedding and the in / out projections collect through both chained steps (measured 3.0-5.8e-2 against
 # the reference, 2-2.7e-2 with exact-f32 GEMMs around the same bf16 attention: profiles/r04/swin_diag.log).
-BF16_GRAD_TOL = {"cnn": 3e-2, "swin": 8e-2, "conformer": 8e-2}
+BF16_GRAD_TOL = {"cnn": 3e-2, "swin": 8e-2, "conformer": 8e-2, "unet": 3e-2}
 
 
 @pytest.mark.parametrize("math", ["f32", "bf16"])
-@pytest.mark.parametrize("meta", ["cnn", "swin", "conformer"])
+@pytest.mark.parametrize("meta", ["cnn", "swin", "conformer", "unet"])
 def test_meta_matches_reference(meta, math):
     """f32 math: every kernel on the path exact f32 (the attention in its unfused f32 form) -- losses rtol
     1e-5, FM output / feature gradients / parameter gradients relative Frobenius <= 1e-4 (BatchNorm's
@@ -41,13 +41,15 @@ def test_meta_matches_reference(meta, math):
     from kdfm.encfm import encfm_backward, encfm_forward
     from kdfm.fmmeta import MetaFMWorkspace
     z = FX.load()
-    L, B, T = int(z["meta.L"]), int(z["meta.B"]), int(z["meta.T"])
+    L, B = int(z["meta.L"]), int(z["meta.B"])
+    T = int(z.get(meta + ".meta.T", z["meta.T"]))   # (the unet fixture: its own even frame count)
     steps = tuple(int(x) for x in z["meta.steps"])
     cfg = replace(DEFAULT, n_layers=L, kd_model="encfm", encfm_meta=meta, encfm_dynamic=False,
-                  encfm_steps_per_layer=steps, heads_student=2, dropout=0.0)
+                  encfm_steps_per_layer=steps, heads_student=2, dropout=0.0,
+                  encfm_hidden=int(z.get(meta + ".meta.hidden", 128)))
     dev = torch.device("cuda")
     P = {k: v.to(dev).contiguous() for k, v in FX.params(z, meta).items()}
-    s, t, R = FX.inputs(z)
+    s, t, R = FX.inputs(z, T=T)
     sd = torch.stack([x.reshape(B * T, -1) for x in s]).to(dev).contiguous()
     td = torch.stack([x.reshape(B * T, -1) for x in t]).to(dev).contiguous()
     Rd = R.reshape(B * T, -1).to(dev).contiguous()
@@ -90,15 +92,17 @@ def test_meta_matches_reference(meta, math):
             assert _rel(v, z[pre + "buffer." + n]) <= 3e-2, n
 
 
-@pytest.mark.parametrize("meta", ["cnn", "swin", "conformer"])
+@pytest.mark.parametrize("meta", ["cnn", "swin", "conformer", "unet"])
 def test_meta_engine_step_matches_oracle(meta):
     import test_step_parity_gpu as SP
     from oracle import ver5 as O
-    n_layers, B, N = 2, 2, 19200
+    # (unet: 18 560 samples -> an even 30 subsampled frames, the only shapes UNet1D runs; base width 16)
+    n_layers, B, N = 2, 2, (18560 if meta == "unet" else 19200)
     steps = (2, 3)
-    cfg, eng, wav, wl, tg, tgl, g = SP._build(n_layers, B, N, [19200, 16123], 12, [12, 7],
+    extra = dict(encfm_hidden=16) if meta == "unet" else {}
+    cfg, eng, wav, wl, tg, tgl, g = SP._build(n_layers, B, N, [N, 16123], 12, [12, 7],
                                               sub=dict(kd_model="encfm", encfm_dynamic=False, encfm_meta=meta,
-                                                       encfm_steps_per_layer=steps))
+                                                       encfm_steps_per_layer=steps, **extra))
     ctx = eng.forward(wav.cuda(), wl.cuda(), tg.cuda(), tgl.cuda(), train=True)
     losses = eng.losses.detach().cpu().clone()
     eng.backward(ctx)
@@ -168,3 +172,69 @@ def test_meta_workspace_follows_batch_shape(meta):
     ws = next(iter(eng._encfm.values()))
     assert ws.flow.abs().max().item() == 0.0 and ws.stats[0].item() == 0.0
     assert torch.isfinite(ws.xS).all()
+
+
+def test_conformer_meta_dropout_gradient_matches_finite_differences():
+    """the conformer meta-encoder's dropout paths (FF activation / output masks with the 0.5 residual
+    scale, the conv-output mask, the attention-weight dropout) had no test.  With dropout 0.1 and a fixed seed
+    the engine's forward is a smooth deterministic function of the parameters (the masks come from the counter
+    RNG), so its backward must equal central finite differences of its own forward: the directional derivative
+    along a random direction over every flow_matching.* parameter, and along the meta-encoder's parameters only,
+    within 2e-2 relative (f32 math, exact-f32 kernels).  A forward / backward mask or stream-index mismatch moves
+    the gradient by O(p)."""
+    from kdfm import kernels as K
+    from kdfm.config import DEFAULT, encfm_specs, meta_bn_specs
+    from kdfm.encfm import encfm_backward, encfm_forward
+    from kdfm.fmmeta import MetaFMWorkspace
+    z = FX.load()
+    L, B, T = int(z["meta.L"]), int(z["meta.B"]), int(z["meta.T"])
+    steps = tuple(int(x) for x in z["meta.steps"])
+    cfg = replace(DEFAULT, n_layers=L, kd_model="encfm", encfm_meta="conformer", encfm_dynamic=False,
+                  encfm_steps_per_layer=steps, heads_student=2, dropout=0.1)
+    dev = torch.device("cuda")
+    P = {k: v.to(dev).contiguous() for k, v in FX.params(z, "conformer").items()}
+    s, t, R = FX.inputs(z)
+    sd = torch.stack([x.reshape(B * T, -1) for x in s]).to(dev).contiguous()
+    td = torch.stack([x.reshape(B * T, -1) for x in t]).to(dev).contiguous()
+    Rd = R.reshape(B * T, -1).to(dev).contiguous()
+    seed = torch.tensor([2024], dtype=torch.int64, device=dev)
+    ws = MetaFMWorkspace(cfg, B, T, dev)
+
+    def bn():
+        return {n: (torch.ones if n.endswith("running_var") else torch.zeros)(shape, device=dev)
+                for n, shape in meta_bn_specs(cfg)}
+
+    def loss(Pm):
+        encfm_forward(cfg, Pm, sd, td, ws, train=True, bn_running=bn(), seed=seed)
+        torch.cuda.synchronize()
+        return ws.stats[2].double().item() + (Rd.double() * ws.xS.double()).sum().item()
+
+    with K.mode("f32", True):
+        G = {n: torch.zeros(shape, device=dev) for n, shape in encfm_specs(cfg)}
+        loss(P)
+        dfeats = torch.empty(L * B * T, cfg.d_student, device=dev)
+        encfm_backward(cfg, P, G, ws, dfeats, Rd, lambda fn, *keep: fn(), seed=seed)
+        torch.cuda.synchronize()
+        g = torch.Generator(device=dev).manual_seed(11)
+        for subset in (lambda n: True, lambda n: n.startswith("flow_matching.meta_encoder.")):
+            names = [n for n in G if subset(n)]
+            v = {n: torch.randn(G[n].shape, device=dev, generator=g) * P[n].abs().mean().clamp_min(1e-3) for n in names}
+            analytic = sum((G[n].double() * v[n].double()).sum().item() for n in names)
+            eps = 1e-3
+            plus = {n: (P[n] + eps * v[n]) if n in v else P[n] for n in P}
+            minus = {n: (P[n] - eps * v[n]) if n in v else P[n] for n in P}
+            fd = (loss(plus) - loss(minus)) / (2 * eps)
+            assert abs(fd - analytic) <= 2e-2 * max(abs(analytic), abs(fd)), (len(names), fd, analytic)
+
+
+def test_unet_refuses_odd_frame_counts():
+    """UNet1D returns 2 floor(T / 2) frames, so at an odd T the reference's update x - v / S fails to broadcast
+    (asr_train.py:1358); the engine refuses that shape with the reference's error text instead of training a
+    different model."""
+    from kdfm.config import DEFAULT
+    from kdfm.fmmeta import MetaFMWorkspace
+    cfg = replace(DEFAULT, n_layers=2, kd_model="encfm", encfm_meta="unet", encfm_dynamic=False,
+                  encfm_steps_per_layer=(2, 3), encfm_hidden=16)
+    with pytest.raises(ValueError, match="even frame count"):
+        MetaFMWorkspace(cfg, 2, 31, torch.device("cuda"))
+    MetaFMWorkspace(cfg, 2, 30, torch.device("cuda"))

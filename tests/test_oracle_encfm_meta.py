@@ -14,12 +14,12 @@ import encfm_meta_fixture as FX
 from oracle import encfm as E
 
 
-@pytest.mark.parametrize("meta", ["cnn", "swin", "conformer"])
+@pytest.mark.parametrize("meta", ["cnn", "swin", "conformer", "unet"])
 def test_meta_oracle_matches_reference(meta):
     z = FX.load()
     steps = [int(x) for x in z["meta.steps"]]
     P = {k: v.double().requires_grad_(True) for k, v in FX.params(z, meta).items()}
-    s, t, R = FX.inputs(z)
+    s, t, R = FX.inputs(z, T=z.get(meta + ".meta.T"))
     s = [x.double().requires_grad_(True) for x in s]
     bn = FX.bn_init(z, meta)
     out = E.encfm_fixed_forward(P, s, [x.double() for x in t], steps, meta=meta, heads=2, bn_state=bn)
@@ -50,12 +50,12 @@ def test_meta_oracle_matches_reference(meta):
         close(grads[len(names) + i], z[pre + f"grad.s{i}"], f"s{i}")
 
 
-@pytest.mark.parametrize("meta", ["cnn", "swin", "conformer"])
+@pytest.mark.parametrize("meta", ["cnn", "swin", "conformer", "unet"])
 def test_meta_specs_match_reference(meta):
     from kdfm.config import DEFAULT, encfm_specs
     z = FX.load()
     cfg = replace(DEFAULT, kd_model="encfm", encfm_meta=meta, encfm_dynamic=False,
-                  encfm_steps_per_layer=(2,) * DEFAULT.n_layers)
+                  encfm_steps_per_layer=(2,) * DEFAULT.n_layers, encfm_hidden=int(z.get(meta + ".meta.hidden", 128)))
     specs = encfm_specs(cfg)
     assert [n for n, _ in specs] == [str(n) for n in z[meta + ".names"]]
     assert [str(tuple(s)) for _, s in specs] == [str(s) for s in z[meta + ".shapes"]]
@@ -65,7 +65,17 @@ def test_meta_refusals():
     from kdfm.config import DEFAULT, head_specs
     with pytest.raises(ValueError, match="fixed step counts"):
         head_specs(replace(DEFAULT, kd_model="encfm", encfm_meta="cnn", encfm_dynamic=True))
-    for meta in ("unet", "bogus"):
+    for meta in ("bogus",):
         with pytest.raises(ValueError, match="encfm_meta"):
             head_specs(replace(DEFAULT, kd_model="encfm", encfm_meta=meta, encfm_dynamic=False,
                                encfm_steps_per_layer=(2,) * DEFAULT.n_layers))
+
+
+def test_unet_odd_frames_fail_like_the_reference():
+    """UNet1D returns 2 floor(T / 2) frames: at an odd T the reference's update x - v / S cannot broadcast
+    (asr_train.py:1340-1358); the oracle raises there too (the engine refuses the shape, test_encfm_meta_gpu)."""
+    z = FX.load()
+    P = {k: v.double() for k, v in FX.params(z, "unet").items()}
+    s, t, _ = FX.inputs(z, T=35)
+    with pytest.raises(RuntimeError, match="size of tensor"):
+        E.fm_forward(P, s[0].double(), t[0].double(), 2, meta="unet")

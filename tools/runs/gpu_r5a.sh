@@ -5,8 +5,8 @@ OUT=gpurun_out/r5a
 mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 500 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_attn_fwd3_gpu.py \
-  tests/test_attn_bwd_gpu.py tests/test_attn_fused_gpu.py "tests/test_encfm_meta_gpu.py::test_meta_workspace_follows_batch_shape" \
-  tests/test_step_parity_gpu.py -k "fwd3 or dq3 or prepared or head_dim or bwd or fused or workspace or xl or 2L-1.2s-dw4 or conformer-small" > $OUT/tests.log 2>&1
+  tests/test_attn_bwd_gpu.py tests/test_attn_fused_gpu.py "tests/test_encfm_meta_gpu.py::test_meta_workspace_follows_batch_shape" "tests/test_encfm_meta_gpu.py::test_conformer_meta_dropout_gradient_matches_finite_differences" \
+  tests/test_step_parity_gpu.py -k "fwd3 or dq3 or prepared or head_dim or bwd or fused or workspace or dropout_gradient or xl or 2L-1.2s-dw4 or conformer-small" > $OUT/tests.log 2>&1
 rc=$?
 tail -3 $OUT/tests.log
 [ $rc -le 1 ] || exit 2
