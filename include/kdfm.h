@@ -784,13 +784,14 @@ int kdfm_l1(const float* a, const float* b, float* grad, float* loss_acc, int64_
  * p 1) ups = GEMM + fold; their data gradients the other way round).
  *   kdfm_unfold1d: cols[(b, i)][k C + c] = x[(b, S i - P + k)][c] for i < Lrows (0 outside [0, Lvalid)); utterance
  *     b's rows start at row b Lin (Lvalid <= Lin), x rows of stride ldx.
- *   kdfm_fold1d: out[(b, t)][c] = R[(b, t)][c] (when non-null, may alias out) + bias[c] (when non-null, t < Lbias)
- *     + sum over taps k with t + P - k = S i, 0 <= i < Lrows, of cols[(b, i)][k C + c], for t < Lout.
+ *   kdfm_fold1d: out[(b, t)][c] = R[(b, t)][c] (when non-null, may alias out) + [t < Lvalid] (bias[c] (when
+ *     non-null) + sum over taps k with t + P - k = S i, 0 <= i < Lrows, of cols[(b, i)][k C + c]), for t < Lout
+ *     (Lvalid: a transposed conv's own output length -- taps past it are cropped, rows past it the zero pad).
  * C, ldx, ldo, ldr multiples of 4; K <= 16. */
 int kdfm_unfold1d(const float* x, int64_t ldx, float* cols, int64_t B, int64_t Lin, int64_t Lvalid, int64_t Lrows,
                   int64_t C, int32_t K, int32_t S, int32_t P, void* stream);
 int kdfm_fold1d(const float* cols, float* out, int64_t ldo, const float* bias, const float* R, int64_t ldr, int64_t B,
-                int64_t Lrows, int64_t Lout, int64_t Lbias, int64_t C, int32_t K, int32_t S, int32_t P, void* stream);
+                int64_t Lrows, int64_t Lout, int64_t Lvalid, int64_t C, int32_t K, int32_t S, int32_t P, void* stream);
 int kdfm_convw_prep(const float* W, float* fwd, float* bwd, int64_t O, int64_t I, int64_t K, void* stream);
 /* dW(O,I,K) += alpha * G(O,K,I) */
 int kdfm_convw_grad(const float* G, float* dW, int64_t O, int64_t I, int64_t K, float alpha, void* stream);

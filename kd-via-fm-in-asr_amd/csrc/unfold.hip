@@ -28,11 +28,13 @@ __global__ __launch_bounds__(256) void unfold1d_kernel(const float* __restrict__
   *reinterpret_cast<float4*>(cols + row * K * C + (int64_t)k * C + c) = v;
 }
 
-// out[(b, t)][c] = (R ? R[(b, t)][c] : 0) + (bias && t < Lbias ? bias[c] : 0)
-//                  + sum_{k : (t + P - k) % S == 0, 0 <= i = (t + P - k) / S < Lrows} cols[(b, i)][k * C + c]
+// out[(b, t)][c] = (R ? R[(b, t)][c] : 0) + [t < Lvalid] (bias ? bias[c] : 0)
+//                  + [t < Lvalid] sum_{k : (t + P - k) % S == 0, 0 <= i = (t + P - k) / S < Lrows} cols[(b, i)][k * C + c]
+// (Lvalid: the transposed conv's own output length; rows past it are the up path's zero pad, and a tap that
+// would land there is cropped by the conv's padding, not added)
 __global__ __launch_bounds__(256) void fold1d_kernel(const float* __restrict__ cols, float* __restrict__ out, int64_t ldo,
                                                      const float* __restrict__ bias, const float* __restrict__ R,
-                                                     int64_t ldr, int64_t B, int64_t Lrows, int64_t Lout, int64_t Lbias,
+                                                     int64_t ldr, int64_t B, int64_t Lrows, int64_t Lout, int64_t Lvalid,
                                                      int64_t C, int K, int S, int P) {
   const int64_t c4n = C / 4;
   const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -42,17 +44,19 @@ __global__ __launch_bounds__(256) void fold1d_kernel(const float* __restrict__ c
   const int64_t b = row / Lout, t = row - b * Lout;
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   if (R) acc = *reinterpret_cast<const float4*>(R + row * ldr + c);
-  if (bias && t < Lbias) {
-    const float4 bb = *reinterpret_cast<const float4*>(bias + c);
-    acc.x += bb.x; acc.y += bb.y; acc.z += bb.z; acc.w += bb.w;
-  }
-  for (int k = 0; k < K; ++k) {   // taps in order: a fixed summation order
-    const int64_t u = t + P - k;
-    if (u < 0 || u % S) continue;
-    const int64_t i = u / S;
-    if (i >= Lrows) continue;
-    const float4 v = *reinterpret_cast<const float4*>(cols + (b * Lrows + i) * K * C + (int64_t)k * C + c);
-    acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+  if (t < Lvalid) {
+    if (bias) {
+      const float4 bb = *reinterpret_cast<const float4*>(bias + c);
+      acc.x += bb.x; acc.y += bb.y; acc.z += bb.z; acc.w += bb.w;
+    }
+    for (int k = 0; k < K; ++k) {   // taps in order: a fixed summation order
+      const int64_t u = t + P - k;
+      if (u < 0 || u % S) continue;
+      const int64_t i = u / S;
+      if (i >= Lrows) continue;
+      const float4 v = *reinterpret_cast<const float4*>(cols + (b * Lrows + i) * K * C + (int64_t)k * C + c);
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
   }
   *reinterpret_cast<float4*>(out + row * ldo + c) = acc;
 }
@@ -78,7 +82,7 @@ int kdfm_unfold1d(const float* x, int64_t ldx, float* cols, int64_t B, int64_t L
 }
 
 int kdfm_fold1d(const float* cols, float* out, int64_t ldo, const float* bias, const float* R, int64_t ldr, int64_t B,
-                int64_t Lrows, int64_t Lout, int64_t Lbias, int64_t C, int32_t K, int32_t S, int32_t P, void* stream) {
+                int64_t Lrows, int64_t Lout, int64_t Lvalid, int64_t C, int32_t K, int32_t S, int32_t P, void* stream) {
   using namespace kdfm;
   KDFM_REQUIRE(cols && out, "null pointer");
   KDFM_REQUIRE(C > 0 && C % 4 == 0 && ldo >= C && ldo % 4 == 0 && (!R || (ldr >= C && ldr % 4 == 0)),
@@ -89,7 +93,7 @@ int kdfm_fold1d(const float* cols, float* out, int64_t ldo, const float* bias, c
   const int64_t n = B * Lout * (C / 4);
   if (n == 0) return KDFM_OK;
   hipLaunchKernelGGL(fold1d_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, as_stream(stream), cols, out, ldo,
-                     bias, R, ldr, B, Lrows, Lout, Lbias, C, (int)K, (int)S, (int)P);
+                     bias, R, ldr, B, Lrows, Lout, Lvalid, C, (int)K, (int)S, (int)P);
   return check_launch("kdfm_fold1d");
 }
 

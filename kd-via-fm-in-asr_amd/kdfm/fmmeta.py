@@ -188,7 +188,7 @@ def _unet_fwd(u, P, k, x, out, R, rscale):
         Z = u.z[:B * L[l] * 4 * co].view(B * L[l], 4 * co)
         K.linear_dx(u.cat[l][k], u.wu[j], Z)
         dst, Lout = (u.cat[l - 1][k][:, :u.cx[l - 1]], L[l - 1]) if l > 1 else (u.up_last[k], 2 * L[1])
-        K.fold1d(Z, dst, B, L[l], Lout, bias=P[UME + f"ups.{j}.bias"], Lbias=2 * L[l])
+        K.fold1d(Z, dst, B, L[l], Lout, bias=P[UME + f"ups.{j}.bias"], Lvalid=2 * L[l])
     epi = _lib.EPI_RESID if R is not None else 0
     K.linear(u.up_last[k], P[UME + "final.weight"].view(out.shape[1], -1), P[UME + "final.bias"], out, epi=epi, R=R,
              rscale=rscale)

@@ -561,14 +561,14 @@ def unfold1d(x, cols, B, Lin, Lrows, K=4, S=2, P=1, Lvalid=None):
          _s())
 
 
-def fold1d(cols, out, B, Lrows, Lout, *, K=4, S=2, P=1, bias=None, R=None, Lbias=None):
-    """out[(b, t), c] = R + bias (t < Lbias) + the taps of cols that land on t (transposed-conv overlap-add); out
-    (B*Lout, C) may be a column slice of a wider buffer; R may alias out."""
+def fold1d(cols, out, B, Lrows, Lout, *, K=4, S=2, P=1, bias=None, R=None, Lvalid=None):
+    """out[(b, t), c] = R + [t < Lvalid] (bias + the taps of cols that land on t) (transposed-conv overlap-add;
+    Lvalid defaults to Lout); out (B*Lout, C) may be a column slice of a wider buffer; R may alias out."""
     C = out.shape[1]
     assert out.shape[0] == B * Lout and out.stride(1) == 1 and cols.shape == (B * Lrows, K * C) and cols.is_contiguous()
     assert R is None or (R.shape == out.shape and R.stride(1) == 1)
     call("kdfm_fold1d", ptr(cols), ptr(out), out.stride(0), ptr(bias), ptr(R), R.stride(0) if R is not None else 0, B,
-         Lrows, Lout, Lout if Lbias is None else Lbias, C, K, S, P, _s())
+         Lrows, Lout, Lout if Lvalid is None else Lvalid, C, K, S, P, _s())
 
 
 def convw_prep(W, fwd=None, bwd=None):

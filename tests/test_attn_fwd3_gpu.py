@@ -79,7 +79,7 @@ def test_prepared_images_and_batched_band():
     allb = K.attn_band_prep(pp, H, T)
     for l in range(3):
         assert torch.equal(allb[l], K.attn_band_prep(pp[l], H, T)[0])
-    band = allb[1].view(H, 64 + 2 * T - 1 + 80, LR).float().cpu()
+    band = allb[1].view(H, 64 + 2 * T - 1 + 88, LR).float().cpu()
     want = pp[1].view(2 * T - 1, H, dk).permute(1, 0, 2).bfloat16().float().cpu()
     assert torch.equal(band[:, 64:64 + 2 * T - 1, :dk], want)
     assert band[:, :64].abs().max() == 0 and band[:, 64 + 2 * T - 1:].abs().max() == 0 and band[:, :, dk:].abs().max() == 0

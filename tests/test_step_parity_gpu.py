@@ -273,9 +273,6 @@ def test_bf16_step_matches_float64_oracle(sub):
     def frob(a, b):
         a, b = a.detach().double().cpu(), b.detach().double().cpu()
         return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
-    for i in range(n_layers):
-        e = frob(sfeats[i].view(B, T, -1), out["s_feats"][i])
-        assert e <= 1.5e-2, (i, e)
     og = torch.autograd.grad(out["loss"], [p[k] for k in names], allow_unused=True)
     # the oracle's own sensitivity to bf16: the same float64 step with every matrix parameter rounded to
     # bf16 (the MFMA operands' rounding) -- with random weights many pre-activations sit near a ReLU /
@@ -283,6 +280,12 @@ def test_bf16_step_matches_float64_oracle(sub):
     pb = {k: (v.detach().bfloat16().double() if (k in names and v.dim() >= 2) else v.detach()).requires_grad_(k in names)
           if v.is_floating_point() else v for k, v in p.items()}
     out_b = O.ver5_step(pb, wav.double(), wl, tg, tgl, ocfg, eps_o.double())
+    # layer outputs: max(1.5e-2, 2.5 x the same sensitivity) -- at d_model 1024 (XL) the bf16-rounded weights alone
+    # move the second layer's output ~0.7 %
+    for i in range(n_layers):
+        e = frob(sfeats[i].view(B, T, -1), out["s_feats"][i])
+        sens = frob(out_b["s_feats"][i], out["s_feats"][i])
+        assert e <= max(1.5e-2, 2.5 * sens), (i, e, sens)
     gb = torch.autograd.grad(out_b["loss"], [pb[k] for k in names], allow_unused=True)
     bad = []
     for k, gr, grb in zip(names, og, gb):
