@@ -44,9 +44,11 @@ ROUTE_KERNELS = {"generic": ("gemm_kernel",), "skinny": ("sk_fwd_kernel", "skd_f
 # the fused kernels traced outside kdfm_gemm (kernels._traced tags) -> kernel-name stems
 FAMILY_KERNELS = {"ffn_fwd": ("ffn_fwd_kernel",), "ffn_bwd": ("ffn_bwd_kernel",),
                   "wgrad_bf16": ("wgr_kernel", "wgd_kernel", "wgr_fold_kernel"),
-                  "attn_fwd": ("relpos_attn_fwd_kernel",),
+                  "attn_fwd": ("relpos_attn_fwd_kernel", "relpos_attn_fwd3_kernel"),
+                  "attn_prep": ("attn_kv_prep_kernel", "attn_band_prep_kernel"),
                   "attn_bwd": ("attn_bwd_dq_kernel", "attn_bwd_dkv_kernel", "attn_bwd_dpos_kernel",
-                               "attn_rowdot_kernel", "attn_dpos_fold_kernel")}
+                               "attn_bwd_dkv2_kernel", "attn_bwd_dpos2_kernel", "attn_rowdot_kernel",
+                               "attn_dpos_fold_kernel")}
 # FLOPs per utterance of one training step (B=32, 16.0 s) and of its attention +
 # FFN dense contractions (student fwd+bwd + teacher fwd), the north-star MFMA roofline subject
 STEP_GFLOP_PER_UTT = 62.6
@@ -367,7 +369,7 @@ def main():
     # live per-kernel timing: one instrumented eager step right after the timed steps; every
     # kdfm_gemm launch (keyed by the kernel family libkdfm routed it to), the frontend and the
     # depthwise convs bracketed by HIP events on the stream they run on
-    trace = K.Trace(["*", "frontend", "dwconv", "ffn_fwd", "ffn_bwd", "wgrad_bf16", "attn_fwd", "attn_bwd"])
+    trace = K.Trace(["*", "frontend", "dwconv", "ffn_fwd", "ffn_bwd", "wgrad_bf16", "attn_fwd", "attn_prep", "attn_bwd"])
     with trace:
         eng.train_step(wav, wl, tg, tl, ar)
     torch.cuda.synchronize()
@@ -396,7 +398,7 @@ def main():
             for k in ("launches", "ms_total", "flops_total", "bytes_total"):
                 w[k] = w.get(k, 0) + tsum["wgrad_bf16"][k]
             routes["wgrad_rows"] = w
-        for fam in ("ffn_fwd", "ffn_bwd", "attn_fwd", "attn_bwd"):
+        for fam in ("ffn_fwd", "ffn_bwd", "attn_fwd", "attn_prep", "attn_bwd"):
             if fam in tsum:
                 routes[fam] = tsum[fam]
         by_route = {}
@@ -430,7 +432,7 @@ def main():
         # gradients (the teacher, weight gradients and CTC/KL overlap it on their own streams)
         csum = trace.summary(stream=eng.compute_stream.cuda_stream)
         croutes = {k[5:]: v for k, v in csum.items() if k.startswith("gemm:")}
-        for fam in ("ffn_fwd", "ffn_bwd", "attn_fwd", "attn_bwd", "wgrad_bf16"):
+        for fam in ("ffn_fwd", "ffn_bwd", "attn_fwd", "attn_prep", "attn_bwd", "wgrad_bf16"):
             if fam in csum:
                 croutes[fam] = csum[fam]
         crit = None
