@@ -47,38 +47,66 @@ __host__ __device__ inline int64_t a3_npb(int64_t T) { return attn_prep_npb(T); 
 
 // ---- preparation --------------------------------------------------------------------------------------
 // kb / vb [b*H + h][Tp][LR]: rows j < T hold bf16(K_j - kc) / bf16(V_j - vc) in columns < dk, zeros elsewhere;
-// cen [b*H + h][2][DKP] = (kc, vc) f32 (zeros past dk).  One workgroup per (64 rows, b*H + h).
+// cen [b*H + h][2][DKP] = (kc, vc) f32 (zeros past dk).  One workgroup per (64 rows, utterance b), every head:
+// the centres of all heads first (one thread per float4 column group of K | V summing the utterance's first n
+// rows in order -- attn_centre.h's kv_centre arithmetic, the same bits), then the 64 rows' conversion.  (One
+// workgroup per (64 rows, b, h) recomputed a head's centre with dk / 2 threads in 7 workgroups: 13.8 us per
+// launch in the step, profiles/r05/r5d_kernel_summary.txt.)
 template <int DKP>
 __global__ __launch_bounds__(256) void attn_kv_prep_kernel(const float* __restrict__ qkv, const int64_t* __restrict__ lens,
                                                            uint16_t* __restrict__ kb, uint16_t* __restrict__ vb,
                                                            float* __restrict__ cen, int64_t H, int T, int64_t d, int dk,
                                                            int64_t Tp) {
   constexpr int LR = DKP + 8, P8 = LR / 8;
-  __shared__ __attribute__((aligned(16))) float Cn[2][DKP];
-  const int64_t bh = blockIdx.y, b = bh / H, h = bh - b * H;
+  extern __shared__ __attribute__((aligned(16))) float Cn[];   // [kind][head][DKP]
+  const int64_t b = blockIdx.y;
+  const int Hh = (int)H;
   const int len = lens ? (int)min<int64_t>(lens[b], T) : T;
-  const float* kbase = qkv + b * T * 3 * d + d + h * dk;
-  const float* vbase = kbase + d;
-  for (int e = threadIdx.x; e < 2 * DKP; e += 256) Cn[e / DKP][e % DKP] = 0.f;
+  const float* kbase = qkv + b * T * 3 * d + d;   // row 0 of utterance b, K columns (V at + d)
+  const int n = len >= 16 ? 16 : len >= 8 ? 8 : len >= 4 ? 4 : len >= 2 ? 2 : (len > 0 ? 1 : 0);
+  const float inv = n > 0 ? 1.f / (float)n : 0.f;   // a power of two: exact
+  for (int e = threadIdx.x; e < 2 * Hh * DKP; e += 256) Cn[e] = 0.f;
   __syncthreads();
-  kv_centre<DKP>(kbase, vbase, 3 * d, len, dk, Cn);   // (ends with a barrier)
+  const int cq = dk >> 2;
+  for (int g = threadIdx.x; g < 2 * Hh * cq; g += 256) {   // (kind, head, float4 column group)
+    const int kind = g / (Hh * cq), rem = g - kind * (Hh * cq);
+    const int h = rem / cq, c4 = (rem - h * cq) * 4;
+    const float* src = kbase + (int64_t)kind * d + (int64_t)h * dk + c4;
+    float4 v[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = *reinterpret_cast<const float4*>(src + (int64_t)(r < n ? r : 0) * 3 * d);
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float m = r < n ? 1.f : 0.f;
+      s.x += m * v[r].x; s.y += m * v[r].y; s.z += m * v[r].z; s.w += m * v[r].w;
+    }
+    float* o = Cn + (kind * Hh + h) * DKP + c4;
+    o[0] = s.x * inv; o[1] = s.y * inv; o[2] = s.z * inv; o[3] = s.w * inv;
+  }
+  __syncthreads();
   if (blockIdx.x == 0)
-    for (int e = threadIdx.x; e < 2 * DKP; e += 256) cen[bh * 2 * DKP + e] = Cn[e / DKP][e % DKP];
-  const int j0 = blockIdx.x * A3K;
-  for (int e = threadIdx.x; e < 2 * A3K * P8; e += 256) {
-    const int kind = e / (A3K * P8), rem = e - kind * (A3K * P8);
-    const int rr = rem / P8, c0 = (rem - rr * P8) * 8;
+    for (int e = threadIdx.x; e < 2 * Hh * DKP; e += 256) {   // cen[(b H + h)][kind][c]
+      const int kind = e / (Hh * DKP), rem = e - kind * (Hh * DKP);
+      const int h = rem / DKP, c = rem - h * DKP;
+      cen[((b * H + h) * 2 + kind) * DKP + c] = Cn[e];
+    }
+  const int j0 = blockIdx.x * 64;
+  for (int e = threadIdx.x; e < 2 * Hh * 64 * P8; e += 256) {
+    const int kind = e / (Hh * 64 * P8), r1 = e - kind * (Hh * 64 * P8);
+    const int h = r1 / (64 * P8), r2 = r1 - h * (64 * P8);
+    const int rr = r2 / P8, c0 = (r2 - rr * P8) * 8;
     const int j = j0 + rr;
-    const float* src = (kind ? vbase : kbase) + (int64_t)(j < T ? j : 0) * 3 * d;
+    const float* src = kbase + (int64_t)kind * d + (int64_t)h * dk + (int64_t)(j < T ? j : 0) * 3 * d;
     const float m0 = (j < T && c0 < dk) ? 1.f : 0.f, m1 = (j < T && c0 + 4 < dk) ? 1.f : 0.f;
     const float4 a = *reinterpret_cast<const float4*>(src + (c0 < dk ? c0 : 0));
     const float4 q = *reinterpret_cast<const float4*>(src + (c0 + 4 < dk ? c0 + 4 : 0));
-    const float* cc = Cn[kind];
+    const float* cc = Cn + (kind * Hh + h) * DKP;
     const int ca = c0 < DKP ? c0 : 0, cb = c0 + 4 < DKP ? c0 + 4 : 0;
     // (a - c) * m: the subtraction is the register-staged kernel's rk - ck, rounded to bf16 by the same RNE
     const float t[8] = {(a.x - cc[ca]) * m0, (a.y - cc[ca + 1]) * m0, (a.z - cc[ca + 2]) * m0, (a.w - cc[ca + 3]) * m0,
                         (q.x - cc[cb]) * m1, (q.y - cc[cb + 1]) * m1, (q.z - cc[cb + 2]) * m1, (q.w - cc[cb + 3]) * m1};
-    *reinterpret_cast<bf16x8*>((kind ? vb : kb) + (bh * Tp + j) * LR + c0) = pack_bf16x8<bf16x8>(t);
+    *reinterpret_cast<bf16x8*>((kind ? vb : kb) + ((b * H + h) * Tp + j) * LR + c0) = pack_bf16x8<bf16x8>(t);
   }
 }
 
@@ -381,13 +409,15 @@ int kdfm_attn_kv_prep(const float* qkv, const int64_t* lengths, uint16_t* kb, ui
   KDFM_REQUIRE(T > 0 && T <= 4096, "T out of range");
   KDFM_REQUIRE((((uintptr_t)qkv | (uintptr_t)kb | (uintptr_t)vb) & 15) == 0, "operands must be 16-byte aligned");
   if (B == 0) return KDFM_OK;
+  KDFM_REQUIRE(H <= 64, "at most 64 heads");
   const int64_t Tp = a3_tp(T);
-  const dim3 grid((unsigned)(Tp / A3K), (unsigned)(B * H));
+  const dim3 grid((unsigned)(Tp / A3K), (unsigned)B);
+  const size_t lds = (size_t)2 * H * a3_dkp(dk) * sizeof(float);
   if (a3_dkp(dk) == 128)
-    hipLaunchKernelGGL(attn_kv_prep_kernel<128>, grid, dim3(256), 0, as_stream(stream), qkv, lengths, kb, vb, centre, H,
+    hipLaunchKernelGGL(attn_kv_prep_kernel<128>, grid, dim3(256), lds, as_stream(stream), qkv, lengths, kb, vb, centre, H,
                        (int)T, d, (int)dk, Tp);
   else
-    hipLaunchKernelGGL(attn_kv_prep_kernel<64>, grid, dim3(256), 0, as_stream(stream), qkv, lengths, kb, vb, centre, H,
+    hipLaunchKernelGGL(attn_kv_prep_kernel<64>, grid, dim3(256), lds, as_stream(stream), qkv, lengths, kb, vb, centre, H,
                        (int)T, d, (int)dk, Tp);
   return check_launch("kdfm_attn_kv_prep");
 }
