@@ -593,16 +593,11 @@ bool wr_plan(const GemmP& p, int amode, int bmode, int64_t batch, WrPlan& pl, bo
   // workgroups queue behind the critical-path kernels (bench 1687 unsliced vs 1635 sliced at
   // target 256, profiles/r02/envab_*.log).  Read per call: tests compare sliced / unsliced.
   const int msl_on = env_i("KDFM_WGR_MSL", 0);
-  // (A/B knobs, read per call: KDFM_WGR_SMAX caps the splits of the non-conv products -- fewer, longer row runs,
-  // so fewer f32 partials to fold -- and KDFM_WGR_MSL = n > 1 asks for n output-row slices instead of the
-  // workgroup-target-derived count, to keep the workgroups the cap removes)
-  const int smax_env = bmode == KDFM_LD_CONV ? 0 : env_i("KDFM_WGR_SMAX", 0);
-  int64_t smax = steps / min_steps > 0 ? steps / min_steps : 1;
-  if (smax_env > 0 && smax > smax_env) smax = smax_env;
+  const int64_t smax = steps / min_steps > 0 ? steps / min_steps : 1;
   {
     const int64_t s0 = target / pl.slices < 1 ? 1 : target / pl.slices;
     const int64_t s_est = s0 < smax ? s0 : smax;
-    int64_t ms = msl_on > 1 ? msl_on : msl_on ? target / (s_est * pl.slices) : 1;
+    int64_t ms = msl_on ? target / (s_est * pl.slices) : 1;
     const int64_t ms_cap = p.M / 32;   // slices of at least 32 output rows
     if (ms > ms_cap) ms = ms_cap;
     if (ms < 1) ms = 1;
