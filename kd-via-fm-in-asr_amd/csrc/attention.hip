@@ -67,8 +67,8 @@ __global__ __launch_bounds__(256) void relpos_softmax_fwd_kernel(
       const float pv = s[e] * inv;
       pr[j] = pv;
       if (pdr) {
-        const uint64_t idx = (uint64_t)row * (uint64_t)T + (uint64_t)j;
-        pdr[j] = (p_drop > 0.f && !dropout_keep(seed, rng_stream, idx, p_drop)) ? 0.f : pv * keep_scale;
+        pdr[j] = (p_drop > 0.f && !attn_drop_keep(rng_key(seed, rng_stream), attn_drop_rowpairs(row, T), j, p_drop))
+                     ? 0.f : pv * keep_scale;
       }
     }
   }
@@ -99,8 +99,7 @@ __global__ __launch_bounds__(256) void relpos_softmax_bwd_kernel(
       pv[e] = pr[j];
       float g = dr[j];
       if (p_drop > 0.f) {
-        const uint64_t idx = (uint64_t)row * (uint64_t)T + (uint64_t)j;
-        g = dropout_keep(seed, rng_stream, idx, p_drop) ? g * keep_scale : 0.f;
+        g = attn_drop_keep(rng_key(seed, rng_stream), attn_drop_rowpairs(row, T), j, p_drop) ? g * keep_scale : 0.f;
       }
       dv[e] = g;
       dot += pv[e] * g;

@@ -467,7 +467,7 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dq_kernel(AbP p
           float g = a[t][r] + cs[r];
           bool kp = true;
           if (p.p_drop > 0.f) {
-            kp = dropout_keep(seed, p.rng_stream, (uint64_t)(prow0 + (int64_t)r * p.T + j), p.p_drop);
+            kp = attn_drop_keep(rng_key(seed, p.rng_stream), attn_drop_rowpairs(bh * p.T + i, p.T), j, p.p_drop);
             g = kp ? g * keep : 0.f;
           }
           const float pe = __expf(s[t][r] - ls[r]);
@@ -637,8 +637,7 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dkv_kernel(AbP 
           float g = a[t][r];
           pd = pv;
           if (p.p_drop > 0.f) {
-            const uint64_t idx = (uint64_t)((bh * p.T + i) * p.T + j);
-            const bool kp = dropout_keep(seed, p.rng_stream, idx, p.p_drop);
+            const bool kp = attn_drop_keep(rng_key(seed, p.rng_stream), attn_drop_rowpairs(bh * p.T + i, p.T), j, p.p_drop);
             g = kp ? g * keep : 0.f;
             pd = kp ? pv * keep : 0.f;
           }
@@ -801,9 +800,9 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dpos_kernel(AbP
         const int i = cur_ib0 + il, j = jbase + jl;
         float ds = 0.f;
         if (i < cur_len && j >= 0 && j < cur_len) {
-          const int64_t idx = (bh * p.T + i) * p.T + j;
           float g = a[t][r];
-          if (p.p_drop > 0.f) g = dropout_keep(seed, p.rng_stream, (uint64_t)idx, p.p_drop) ? g * keep : 0.f;
+          if (p.p_drop > 0.f)
+            g = attn_drop_keep(rng_key(seed, p.rng_stream), attn_drop_rowpairs(bh * p.T + i, p.T), j, p.p_drop) ? g * keep : 0.f;
           ds = pcur[t][r] * Cs[il * 3 + ((j >> 6) - kb0)] * (g - Rs[il]) * p.scale;
         }
         Dl[il * LDL + jl] = f2bf(ds);

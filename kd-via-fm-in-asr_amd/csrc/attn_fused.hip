@@ -320,10 +320,12 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void relpos_attn_fwd_kernel(A
   const int64_t prow0 = (bh * p.T + ib) * p.T;  // P row of (ib, j = 0)
   // per owned row: flat index of its (i, j = 0) element (dropout counter, p~ offset) and whether i < T
   int64_t prow[4];
+  uint64_t dpair[4];   // attn_drop_rowpairs of the owned rows
   bool rowin[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     prow[r] = prow0 + (int64_t)r * p.T;
+    dpair[r] = attn_drop_rowpairs(bh * p.T + ib + r, p.T);
     rowin[r] = ib + r < T;
   }
   const bool drop = p.p_drop > 0.f;
@@ -394,7 +396,7 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void relpos_attn_fwd_kernel(A
                                                 0, 0);
         float pdv = pv;
         if (drop) {   // (a zero probability stays zero either way: no per-element branch on it)
-          pdv = dropout_keep_k(dkey, (uint64_t)(prow[r] + j), p.p_drop) ? pv * keep_scale : 0.f;
+          pdv = attn_drop_keep(dkey, dpair[r], j, p.p_drop) ? pv * keep_scale : 0.f;
           pds[r] += pdv;
         }
         if (TWO_PASS && i < T && j < T) {

@@ -30,7 +30,7 @@ constexpr int A3Q = 64;            // queries per workgroup (4 waves x 16)
 constexpr int A3K = 64;            // keys per step
 constexpr int A3BAND = 128;        // Ppos band rows staged per step (127 used)
 constexpr int A3PAD0 = kAttnBandPad0;   // zero rows before the first position row of a prepared band
-constexpr int A3LDP = A3K + 8;     // bf16 row stride of the per-wave P tile [16][64]
+constexpr int A3LDT = 20;          // bf16 row stride of the per-wave P^T tile [64 keys][16 rows]
 
 template <int NU> struct A3Geo {
   static constexpr int KS = NU > 4 ? 4 : 2;        // MFMA k-steps over the padded head dim
@@ -169,6 +169,31 @@ __device__ __forceinline__ float a3_max16(float v) {
   v = fmaxf(v, a3_dpp<0x141>(v));
   return fmaxf(v, a3_dpp<0x140>(v));
 }
+// the row max over the 16 lanes of each of the four C-tile rows at once: 16 DPP max instructions (the builtin
+// form costs a v_mov_dpp and a canonicalising v_max per stage, 48).  The leading s_nop covers the DPP read-
+// after-VALU-write hazard of the inputs; within the block each register's next DPP read is 4 instructions
+// after its write.
+__device__ __forceinline__ void a3_max16x4(float& a, float& b, float& c, float& d) {
+  asm volatile(
+      "s_nop 1\n"
+      "v_max_f32_dpp %0, %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n"
+      "v_max_f32_dpp %1, %1, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n"
+      "v_max_f32_dpp %2, %2, %2 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n"
+      "v_max_f32_dpp %3, %3, %3 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n"
+      "v_max_f32_dpp %0, %0, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n"
+      "v_max_f32_dpp %1, %1, %1 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n"
+      "v_max_f32_dpp %2, %2, %2 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n"
+      "v_max_f32_dpp %3, %3, %3 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n"
+      "v_max_f32_dpp %0, %0, %0 row_half_mirror row_mask:0xf bank_mask:0xf\n"
+      "v_max_f32_dpp %1, %1, %1 row_half_mirror row_mask:0xf bank_mask:0xf\n"
+      "v_max_f32_dpp %2, %2, %2 row_half_mirror row_mask:0xf bank_mask:0xf\n"
+      "v_max_f32_dpp %3, %3, %3 row_half_mirror row_mask:0xf bank_mask:0xf\n"
+      "v_max_f32_dpp %0, %0, %0 row_mirror row_mask:0xf bank_mask:0xf\n"
+      "v_max_f32_dpp %1, %1, %1 row_mirror row_mask:0xf bank_mask:0xf\n"
+      "v_max_f32_dpp %2, %2, %2 row_mirror row_mask:0xf bank_mask:0xf\n"
+      "v_max_f32_dpp %3, %3, %3 row_mirror row_mask:0xf bank_mask:0xf\n"
+      : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
+}
 __device__ __forceinline__ float a3_sum16(float v) {
   v += a3_dpp<0xB1>(v);
   v += a3_dpp<0x4E>(v);
@@ -180,10 +205,12 @@ template <int NU>
 __global__ __launch_bounds__(256, NU == 3 ? 3 : 2) void relpos_attn_fwd3_kernel(Attn3P p) {
   using Gm = A3Geo<NU>;
   constexpr int KS = Gm::KS, LR = Gm::LR, KCH = Gm::KCH, BCH = Gm::BCH, NCH = 2 * KCH + BCH;
-  __shared__ __attribute__((aligned(16))) uint16_t Ks[A3K * LR];
-  __shared__ __attribute__((aligned(16))) uint16_t Vs[A3K * LR];
-  __shared__ __attribute__((aligned(16))) uint16_t Pr[A3BAND * LR];
-  __shared__ __attribute__((aligned(16))) uint16_t Ps[4][16 * A3LDP];
+  // K tile | V tile | band rows, contiguous: 1 KB DMA chunk f lands at byte f * 1024 whichever tile it is
+  __shared__ __attribute__((aligned(16))) uint16_t Sm[(2 * A3K + A3BAND) * LR];
+  __shared__ __attribute__((aligned(16))) uint16_t Pt[4][A3K * A3LDT];   // per wave: P^T [key][row]
+  uint16_t* const Ks = Sm;
+  uint16_t* const Vs = Sm + A3K * LR;
+  uint16_t* const Pr = Sm + 2 * A3K * LR;
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int T = (int)p.T, dk = (int)p.dk;
@@ -192,7 +219,8 @@ __global__ __launch_bounds__(256, NU == 3 ? 3 : 2) void relpos_attn_fwd3_kernel(
   const int64_t b = bh / p.H, h = bh - b * p.H;
   const int i0 = (int)blk.x * A3Q;
   const int len = p.lens ? (int)p.lens[b] : T;
-  const int nkb = (min(len, T) + A3K - 1) / A3K;
+  const int lim = min(len, T);
+  const int nkb = (lim + A3K - 1) / A3K;
   const int64_t hoff = h * p.dk;
   const uint4* ksrc = reinterpret_cast<const uint4*>(p.kb + bh * p.Tp * LR);
   const uint4* vsrc = reinterpret_cast<const uint4*>(p.vb + bh * p.Tp * LR);
@@ -201,20 +229,20 @@ __global__ __launch_bounds__(256, NU == 3 ? 3 : 2) void relpos_attn_fwd3_kernel(
   // one key step's operands: K rows [j0, j0 + 64), V rows, band rows [rbase, rbase + 128) of the prepared
   // band (row A3PAD0 + r holds position r) -- NCH 1 KB chunks, wave w takes chunks w, w + 4, ...
   auto issue = [&](int j0) {
+    // wave-uniform chunk bases (SGPR address + this lane's 16-byte offset: no per-chunk 64-bit lane addresses
+    // held across the loop)
     const int rb = T - 1 - (i0 + A3Q - 1) + j0 + A3PAD0;
-    const uint4* bs = reinterpret_cast<const uint4*>(bsrc + (int64_t)rb * LR);
+    const char* kbase = reinterpret_cast<const char*>(ksrc) + (int64_t)j0 * LR * 2;
+    const char* vbase = reinterpret_cast<const char*>(vsrc) + (int64_t)j0 * LR * 2;
+    const char* bbase = reinterpret_cast<const char*>(bsrc + (int64_t)rb * LR);
+    const uint32_t loff = (uint32_t)lane * 16u;
 #pragma unroll
     for (int i = 0; i < (NCH + 3) / 4; ++i) {
       const int f = w + 4 * i;   // wave-uniform
-      if (f < KCH) {
-        __builtin_amdgcn_global_load_lds((gl_void_t3*)(ksrc + (int64_t)j0 * LR / 8 + f * 64 + lane),
-                                         (lds_void_t3*)(reinterpret_cast<uint4*>(Ks) + f * 64), 16, 0, 0);
-      } else if (f < 2 * KCH) {
-        __builtin_amdgcn_global_load_lds((gl_void_t3*)(vsrc + (int64_t)j0 * LR / 8 + (f - KCH) * 64 + lane),
-                                         (lds_void_t3*)(reinterpret_cast<uint4*>(Vs) + (f - KCH) * 64), 16, 0, 0);
-      } else if (f < NCH) {
-        __builtin_amdgcn_global_load_lds((gl_void_t3*)(bs + (f - 2 * KCH) * 64 + lane),
-                                         (lds_void_t3*)(reinterpret_cast<uint4*>(Pr) + (f - 2 * KCH) * 64), 16, 0, 0);
+      if (4 * i + 3 < NCH || f < NCH) {
+        const char* src = f < KCH ? kbase + f * 1024 : f < 2 * KCH ? vbase + (f - KCH) * 1024 : bbase + (f - 2 * KCH) * 1024;
+        __builtin_amdgcn_global_load_lds((gl_void_t3*)(src + loff), (lds_void_t3*)(reinterpret_cast<uint4*>(Sm) + f * 64),
+                                         16, 0, 0);
       }
     }
   };
@@ -233,9 +261,13 @@ __global__ __launch_bounds__(256, NU == 3 ? 3 : 2) void relpos_attn_fwd3_kernel(
   }
   const int q4 = lane >> 4, lo = lane & 15;
   const int ib = i0 + w * 16 + 4 * q4;   // C-layout rows ib + r
-  float mrow[4], lrow[4];
+  // online softmax state in the exp2 domain: m2 = running row max of s * scale * log2(e); per-LANE partial
+  // sums of exp2(s * sl2 - m2) (and of the dropped-out probabilities), reduced over the row's 16 lanes once
+  // after the loop (the row max is reduced every step -- the rescale needs it)
+  const float sl2 = p.scale * 1.4426950408889634f;
+  float m2[4], lsum[4], psum[4];
 #pragma unroll
-  for (int r = 0; r < 4; ++r) { mrow[r] = -3.0e38f; lrow[r] = 0.f; }
+  for (int r = 0; r < 4; ++r) { m2[r] = -3.0e38f; lsum[r] = 0.f; psum[r] = 0.f; }
   // rel_shift permute per row register r: S_bd(t, r) = G[t + (off >= 16)][r] of lane (off & 15) + 16 q4
   int bsrc_lane[4];
   bool bhi[4];
@@ -250,12 +282,19 @@ __global__ __launch_bounds__(256, NU == 3 ? 3 : 2) void relpos_attn_fwd3_kernel(
   const uint64_t dkey = rng_key(seed, p.rng_stream);
   const float keep_scale = (p.p_drop > 0.f) ? 1.f / (1.f - p.p_drop) : 1.f;
   const bool drop = p.p_drop > 0.f;
+  const uint32_t thr = drop_threshold(p.p_drop);
+  // dropout (common.h attn_drop_keep): keys 16 t + lo and 16 t + (lo ^ 1) share one pair hash, so this lane
+  // hashes two of its four rows (even lanes rows ib, ib + 1; odd lanes ib + 2, ib + 3) and takes the other
+  // two from its pair partner (DPP swap): 8 hashes per lane per key step, not 16
+  const bool odd = lo & 1;
+  uint64_t dpr[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) dpr[k] = attn_drop_rowpairs(bh * p.T + ib + (odd ? 2 : 0) + k, p.T) + (uint64_t)(lo >> 1);
+  const int hsh = odd ? 16 : 0;
   f32x4 oacc[NU];
 #pragma unroll
   for (int u = 0; u < NU; ++u) oacc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int64_t prow0 = (bh * p.T + ib) * p.T;
-  float ps[4] = {0.f, 0.f, 0.f, 0.f};
-  uint16_t* Pw = Ps[w];
+  uint16_t* Pw = Pt[w];
 
   for (int kb = 0; kb < nkb; ++kb) {
     const int j0 = kb * A3K;
@@ -265,7 +304,7 @@ __global__ __launch_bounds__(256, NU == 3 ? 3 : 2) void relpos_attn_fwd3_kernel(
     }
     __builtin_amdgcn_s_waitcnt(0x70);   // vmcnt(0) lgkmcnt(0): this wave's DMA chunks landed
     __syncthreads();                    // ... and every other wave's
-    // ---- scores of this wave's 16 rows x 64 keys (the register-staged kernel's MFMAs, same order) ----
+    // ---- scores of this wave's 16 rows x 64 keys: S_ac = Qu K^T, G = Qv Pband^T (fragments read first) ----
     f32x4 ac[4], g[5];
 #pragma unroll
     for (int t = 0; t < 4; ++t) ac[t] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -275,17 +314,17 @@ __global__ __launch_bounds__(256, NU == 3 ? 3 : 2) void relpos_attn_fwd3_kernel(
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       const int kof = ks * 32 + 8 * q4;
+      bf16x8 kf[4], pf[5];
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const bf16x8 kbf = *reinterpret_cast<const bf16x8*>(Ks + (16 * t + lo) * LR + kof);
-        ac[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fu[ks], kbf, ac[t], 0, 0, 0);
-      }
+      for (int t = 0; t < 4; ++t) kf[t] = *reinterpret_cast<const bf16x8*>(Ks + (16 * t + lo) * LR + kof);
 #pragma unroll
-      for (int t = 0; t < 5; ++t) {
-        const bf16x8 pbf = *reinterpret_cast<const bf16x8*>(Pr + (wb + 16 * t + lo) * LR + kof);
-        g[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fv[ks], pbf, g[t], 0, 0, 0);
-      }
+      for (int t = 0; t < 5; ++t) pf[t] = *reinterpret_cast<const bf16x8*>(Pr + (wb + 16 * t + lo) * LR + kof);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) ac[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fu[ks], kf[t], ac[t], 0, 0, 0);
+#pragma unroll
+      for (int t = 0; t < 5; ++t) g[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fv[ks], pf[t], g[t], 0, 0, 0);
     }
+    // raw scores s = S_ac + S_bd (unscaled), the rel_shift by lane permutes
     float s[4][4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -298,52 +337,69 @@ __global__ __launch_bounds__(256, NU == 3 ? 3 : 2) void relpos_attn_fwd3_kernel(
         X[t] = __int_as_float(__builtin_amdgcn_ds_bpermute(bsrc_lane[r], __float_as_int(gv)));
       }
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const float bd = bhi[r] ? X[t + 1] : X[t];
-        const int j = j0 + 16 * t + lo;
-        s[t][r] = (j < len && j < T) ? (ac[t][r] + bd) * p.scale : -3.0e38f;
-      }
+      for (int t = 0; t < 4; ++t) s[t][r] = ac[t][r] + (bhi[r] ? X[t + 1] : X[t]);
     }
-    // ---- online softmax: rescale the running sum and O to the new row max ----
+    if (j0 + A3K > lim) {   // the utterance's last key block: keys past its length score -inf
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        if (j0 + 16 * t + lo >= lim)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) s[t][r] = -3.0e38f;
+    }
+    // ---- online softmax (every key block holds a valid key, so the row max is finite after block 0) ----
+    float mx[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) mx[r] = fmaxf(fmaxf(s[0][r], s[1][r]), fmaxf(s[2][r], s[3][r]));
+    a3_max16x4(mx[0], mx[1], mx[2], mx[3]);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      float mx = fmaxf(fmaxf(s[0][r], s[1][r]), fmaxf(s[2][r], s[3][r]));
-      mx = a3_max16(mx);
-      const float mn = fmaxf(mrow[r], mx);
-      const float corr = (mrow[r] > -1.0e38f) ? __expf(mrow[r] - mn) : 0.f;
-      float sum = 0.f;
-#pragma unroll
-      for (int t = 0; t < 4; ++t) sum += (s[t][r] > -1.0e38f) ? __expf(s[t][r] - mn) : 0.f;
-      lrow[r] = lrow[r] * corr + a3_sum16(sum);
-      mrow[r] = mn;
-      ps[r] *= corr;
+      const float mn = fmaxf(m2[r], mx[r] * sl2);
+      const float corr = __builtin_amdgcn_exp2f(m2[r] - mn);
+      m2[r] = mn;
+      lsum[r] *= corr;
+      psum[r] *= corr;
 #pragma unroll
       for (int u = 0; u < NU; ++u) oacc[u][r] *= corr;
     }
-    float pds[4] = {0.f, 0.f, 0.f, 0.f};
+    float pv[4][4];
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int ii = 4 * q4 + r, jj = 16 * t + lo;
-        const float pv = (s[t][r] > -1.0e38f) ? __expf(s[t][r] - mrow[r]) : 0.f;
-        float pdv = pv;
-        if (drop) {
-          pdv = dropout_keep_k(dkey, (uint64_t)(prow0 + (int64_t)r * p.T + j0 + jj), p.p_drop) ? pv * keep_scale : 0.f;
-          pds[r] += pdv;
-        }
-        Pw[ii * A3LDP + jj] = f2bf(pdv);
+        pv[t][r] = __builtin_amdgcn_exp2f(__builtin_fmaf(s[t][r], sl2, -m2[r]));
+        lsum[r] += pv[t][r];
       }
     if (drop) {
+      uint32_t hk[4][2], hp[4][2];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) ps[r] += a3_sum16(pds[r]);
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int k = 0; k < 2; ++k) hk[t][k] = drop_pair_bits(dkey, dpr[k] + (uint64_t)((j0 >> 1) + 8 * t));
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int k = 0; k < 2; ++k) hp[t][k] = (uint32_t)__builtin_amdgcn_mov_dpp((int)hk[t][k], 0xB1, 0xF, 0xF, false);
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const uint32_t hv = ((r >> 1) == (int)odd) ? hk[t][r & 1] : hp[t][r & 1];
+          const bool keep = ((hv >> hsh) & 0xffffu) >= thr;
+          pv[t][r] = keep ? pv[t][r] * keep_scale : 0.f;
+          psum[r] += pv[t][r];
+        }
+    }
+    // ---- P^T to LDS: key 16 t + lo, rows 4 q4 .. +3 as one 8-byte write; O += Pd V ----
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const uint2 w2 = make_uint2(pack_bf16x2(pv[t][0], pv[t][1]), pack_bf16x2(pv[t][2], pv[t][3]));
+      *reinterpret_cast<uint2*>(Pw + (16 * t + lo) * A3LDT + 4 * q4) = w2;
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
-    // ---- O += Pd V (V [key][c] read transposed) ----
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      const bf16x8 pa = *reinterpret_cast<const bf16x8*>(Pw + lo * A3LDP + ks * 32 + 8 * q4);
+      const bf16x8 pa = a3_tr_frag(Pw, A3LDT, ks * 32, 0, lane);   // A[row lo][key ks 32 + 8 q4 + i]
 #pragma unroll
       for (int u = 0; u < NU; ++u)
         oacc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, a3_tr_frag(Vs, LR, ks * 32, 16 * u, lane), oacc[u], 0, 0, 0);
@@ -352,11 +408,17 @@ __global__ __launch_bounds__(256, NU == 3 ? 3 : 2) void relpos_attn_fwd3_kernel(
     __builtin_amdgcn_wave_barrier();   // Pw is rewritten by the next step
   }
   // ---- per-row log-sum-exp (3e38 for rows without a valid key) and O = centred sum + S_i vc ----
+  float lrow[4], prow_sum[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    lrow[r] = a3_sum16(lsum[r]);
+    prow_sum[r] = drop ? a3_sum16(psum[r]) : 0.f;
+  }
   if (p.lse && lo == 0) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int i = ib + r;
-      if (i < T) p.lse[bh * p.T + i] = (i < len && lrow[r] > 0.f) ? mrow[r] + logf(lrow[r]) : 3.0e38f;
+      if (i < T) p.lse[bh * p.T + i] = (i < len && lrow[r] > 0.f) ? m2[r] * 0.6931471805599453f + logf(lrow[r]) : 3.0e38f;
     }
   }
   float fin[4], sv[4];
@@ -364,7 +426,7 @@ __global__ __launch_bounds__(256, NU == 3 ? 3 : 2) void relpos_attn_fwd3_kernel(
   for (int r = 0; r < 4; ++r) {
     const bool rv_ok = ib + r < len && lrow[r] > 0.f;
     fin[r] = rv_ok ? 1.f / lrow[r] : 0.f;
-    sv[r] = drop ? ps[r] * fin[r] : (rv_ok ? 1.f : 0.f);
+    sv[r] = drop ? prow_sum[r] * fin[r] : (rv_ok ? 1.f : 0.f);
   }
   const float* vc = p.cen + bh * 2 * Gm::DKP + Gm::DKP;
 #pragma unroll

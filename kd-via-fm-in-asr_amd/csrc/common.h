@@ -130,6 +130,17 @@ __device__ __forceinline__ void dropout_keep2_k(uint64_t key, uint64_t idx_even,
 __device__ __forceinline__ bool dropout_keep(uint64_t seed, uint64_t stream, uint64_t idx, float p) {
   return dropout_keep_k(rng_key(seed, stream), idx, p);
 }
+// Attention-probability dropout of element (row, key j) of a T x T map, row = (b H + h) T + i: one hash per
+// (row, key pair j >> 1) -- pair index row * ceil(T / 2) + (j >> 1), so a pair never straddles two rows and
+// keys 2m, 2m + 1 (neighbouring lanes of an MFMA C tile) share it -- and 16 bits per key (j & 1 picks them).
+// Every attention kernel (fused forwards, bwd2, the unfused softmax) draws its mask through this.
+__host__ __device__ __forceinline__ uint64_t attn_drop_rowpairs(int64_t row, int64_t T) {
+  return (uint64_t)row * (uint64_t)((T + 1) >> 1);
+}
+__device__ __forceinline__ bool attn_drop_keep(uint64_t key, uint64_t rowpairs, int64_t j, float p) {
+  const uint32_t h = drop_pair_bits(key, rowpairs + (uint64_t)(j >> 1));
+  return ((j & 1) ? (h >> 16) : (h & 0xffffu)) >= drop_threshold(p);
+}
 __device__ __forceinline__ uint64_t load_seed(const uint64_t* seed_ptr) { return seed_ptr ? *seed_ptr : 0ull; }
 
 // ---- wave64 reductions --------------------------------------------------------------------------

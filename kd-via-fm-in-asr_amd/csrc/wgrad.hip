@@ -446,30 +446,11 @@ __global__ __launch_bounds__(64 * WF_WAVES) void wgr_fold4_kernel(GemmP p, int64
   const bool second = blockIdx.y == 1;   // paired launch: the second product
   float* Cout = second ? p.C2 : p.C;
   float* ones = second ? p.ones_out2 : p.ones_out;
-  float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f), a1 = a0, a2 = a0, a3 = a0;
-  auto add = [](float4& a, const float4 b) { a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w; };
-  if (e0 < MN) {
-    const float4* base = reinterpret_cast<const float4*>((second ? p.ws2 : p.ws) + e0);
-    const int64_t st = MN / 4;   // float4 stride between splits
-    int64_t s = w;
-    for (; s + 3 * WF_WAVES < S; s += 4 * WF_WAVES) {
-      add(a0, base[s * st]);
-      add(a1, base[(s + WF_WAVES) * st]);
-      add(a2, base[(s + 2 * WF_WAVES) * st]);
-      add(a3, base[(s + 3 * WF_WAVES) * st]);
-    }
-    for (; s < S; s += WF_WAVES) add(a0, base[s * st]);
-  }
-  add(a0, a1);
-  add(a2, a3);
-  add(a0, a2);
-  red4[w][lane] = a0;
-  __syncthreads();
+  // wave 0 fetches the 4 destination values before the partials, so their round trip overlaps the
+  // partials' (the destination is read and written by this block only)
+  float* dst[4] = {nullptr, nullptr, nullptr, nullptr};
+  float cur[4] = {0.f, 0.f, 0.f, 0.f};
   if (w == 0 && e0 < MN) {
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-    for (int i = 0; i < WF_WAVES; ++i) add(v, red4[i][lane]);
-    const float vv[4] = {v.x * p.alpha, v.y * p.alpha, v.z * p.alpha, v.w * p.alpha};
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int64_t e = e0 + q;
@@ -481,11 +462,44 @@ __global__ __launch_bounds__(64 * WF_WAVES) void wgr_fold4_kernel(GemmP p, int64
         m = e / p.N;
         n = e - m * p.N;
       }
-      if (p.ones_col >= 0 && n >= p.ones_col)
-        ones[(n - p.ones_col) * p.M + m] += vv[q];
-      else
-        Cout[m * p.sCm + n * p.sCn] += vv[q];
+      dst[q] = (p.ones_col >= 0 && n >= p.ones_col) ? ones + (n - p.ones_col) * p.M + m : Cout + m * p.sCm + n * p.sCn;
     }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) cur[q] = *dst[q];
+  }
+  float4 acc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) acc[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  auto add = [](float4& a, const float4 b) { a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w; };
+  // this wave's splits w, w + WF, ... (nw of them): split i of the wave goes to accumulator i % 4 while it is
+  // in a complete group of 4 (i < g4), the rest to accumulator 0 -- a fixed order.  Up to 16 partial loads
+  // are in flight per lane before the first add (one memory round trip per 16 splits, not per 4).
+  const int64_t nw = (e0 < MN && S > w) ? (S - w + WF_WAVES - 1) / WF_WAVES : 0;
+  const int64_t g4 = nw / 4 * 4;
+  const float4* base = reinterpret_cast<const float4*>((second ? p.ws2 : p.ws) + e0);
+  const int64_t st = MN / 4;   // float4 stride between splits
+  for (int64_t i0 = 0; i0 < nw; i0 += 16) {
+    float4 v[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      v[i] = i0 + i < nw ? base[(w + (i0 + i) * WF_WAVES) * st] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      if (i0 + i < nw) add(i0 + i < g4 ? acc[i & 3] : acc[0], v[i]);
+    }
+  }
+  add(acc[0], acc[1]);
+  add(acc[2], acc[3]);
+  add(acc[0], acc[2]);
+  red4[w][lane] = acc[0];
+  __syncthreads();
+  if (w == 0 && e0 < MN) {
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int i = 0; i < WF_WAVES; ++i) add(v, red4[i][lane]);
+    const float vv[4] = {v.x * p.alpha, v.y * p.alpha, v.z * p.alpha, v.w * p.alpha};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) *dst[q] = cur[q] + vv[q];
   }
 }
 

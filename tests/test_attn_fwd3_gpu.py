@@ -1,9 +1,12 @@
 """The prepared-operand attention forward (kdfm_relpos_attn_fwd3, csrc/attn_fwd3.hip: bf16 centred K / V tiles
-and positional band rows staged by LDS-DMA, rel_shift by lane permutes) against the register-staged single-pass
-forward (kdfm_relpos_attn_fwd) it replaces on the bwd2 / inference path: O and lse BITWISE equal -- same bf16
-operands, same MFMAs in the same order -- at the student / teacher / FastConformer / XL head dims, ragged
-lengths, with attention dropout, and without lse (inference); the batched band preparation of several layers
-equals the per-layer one; the prepared images hold exactly bf16(K - kc) / bf16(V - vc) with zero padding."""
+and positional band rows staged by LDS-DMA, rel_shift by lane permutes, the softmax in the exp2 domain with per-lane
+partial row sums, dropout pair hashes shared between neighbouring lanes) against the register-staged single-pass
+forward (kdfm_relpos_attn_fwd) it replaces on the bwd2 / inference path: the same bf16 operands and MFMAs and the
+same dropout mask (common.h attn_drop_keep), so O and lse agree to f32 rounding of the softmax (a bf16 rounding of
+a probability may flip: O within 1e-3, lse within 2e-6 relative) -- at the student / teacher / FastConformer / XL
+head dims, ragged lengths, with attention dropout, and without lse (inference); the batched band preparation of
+several layers equals the per-layer one; the prepared images hold exactly bf16(K - kc) / bf16(V - vc) with zero
+padding."""
 import math
 
 import pytest
@@ -33,7 +36,7 @@ def _inputs(B, H, T, d, seed, kcm=0.0):
     (3, 2, 77, 88, 0.0, True),      # T not a multiple of 64, short utterances
     (2, 1, 65, 100, 0.0, True),     # head dim 100
 ])
-def test_fwd3_bitwise_equals_register_staged(B, H, T, d, p, with_lse):
+def test_fwd3_matches_register_staged(B, H, T, d, p, with_lse):
     from kdfm import kernels as K
     qkv, qu, qv, ppos, lens = _inputs(B, H, T, d, 5 * T + d, kcm=2.0)
     seed = torch.tensor([321], dtype=torch.int64, device="cuda")
@@ -47,9 +50,10 @@ def test_fwd3_bitwise_equals_register_staged(B, H, T, d, p, with_lse):
     pb = K.attn_band_prep(ppos, H, T)[0]
     K.relpos_attn_fwd3(qu, qv, prep, pb, lens, o2, B, H, T, sc, p, seed, 17, lse=lse2)
     torch.cuda.synchronize()
-    assert torch.equal(o1, o2), (o1 - o2).abs().max().item()
+    assert not torch.isnan(o2).any()
+    torch.testing.assert_close(o2, o1, rtol=1e-3, atol=1e-3)
     if with_lse:
-        assert torch.equal(lse1, lse2)
+        torch.testing.assert_close(lse2, lse1, rtol=2e-6, atol=2e-6)
 
 
 def test_prepared_images_and_batched_band():

@@ -1,6 +1,7 @@
 """Isolated timing of the prepared-operand attention forward (kv prep + fwd3) at the bench's student (H 2,
 d 88) and teacher (H 4, d 176) shapes, B 32 x T 401, with and without attention dropout, and both shapes
-launched together on two streams (the step's overlap).  usage: python tools/attn3_micro.py"""
+launched together on two streams (the step's overlap).  usage: python tools/attn3_micro.py [--pmc]  (--pmc: only the teacher shape with dropout, a few launches,
+for rocprofv3 --pmc passes)"""
 import math
 import os
 import sys
@@ -26,11 +27,12 @@ def bench(name, fn, reps=30):
     print(f"{name:50s} {s.elapsed_time(e) / reps * 1e3:9.1f} us", flush=True)
 
 
+PMC = "--pmc" in sys.argv
 g = torch.Generator(device="cuda").manual_seed(0)
 B, T = 32, 401
 seed = torch.tensor([1], dtype=torch.int64, device="cuda")
 cases = {}
-for (H, d) in ((2, 88), (4, 176)):
+for (H, d) in (((4, 176),) if PMC else ((2, 88), (4, 176))):
     rows = B * T
     qkv = torch.randn(rows, 3 * d, device="cuda", generator=g)
     qu = torch.randn(rows, d, device="cuda", generator=g)
@@ -43,6 +45,11 @@ for (H, d) in ((2, 88), (4, 176)):
     prep = K.attn_kv_prep(qkv, lens, B, H, T)
     pb = K.attn_band_prep(ppos, H, T)[0]
     cases[H] = (qu, qv, prep, pb, lens, o, lse, sc, d, qkv)
+    if PMC:
+        for _ in range(4):
+            K.relpos_attn_fwd3(qu, qv, prep, pb, lens, o, B, H, T, sc, 0.1, seed, 5, lse=lse)
+        torch.cuda.synchronize()
+        sys.exit(0)
     bench(f"H={H} kv prep", lambda: K.attn_kv_prep(qkv, lens, B, H, T))
     for p in (0.0, 0.1):
         bench(f"H={H} fwd3 p={p}", lambda: K.relpos_attn_fwd3(qu, qv, prep, pb, lens, o, B, H, T, sc, p, seed, 5,
