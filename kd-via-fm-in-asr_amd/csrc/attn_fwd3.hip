@@ -30,7 +30,7 @@ constexpr int A3Q = 64;            // queries per workgroup (4 waves x 16)
 constexpr int A3K = 64;            // keys per step
 constexpr int A3BAND = 128;        // Ppos band rows staged per step (127 used)
 constexpr int A3PAD0 = kAttnBandPad0;   // zero rows before the first position row of a prepared band
-constexpr int A3LDT = 20;          // bf16 row stride of the per-wave P^T tile [64 keys][16 rows]
+constexpr int A3LDT = 16;          // bf16 row stride of the per-wave P^T tile [64 keys][16 rows]
 
 template <int NU> struct A3Geo {
   static constexpr int KS = NU > 4 ? 4 : 2;        // MFMA k-steps over the padded head dim
@@ -48,65 +48,100 @@ __host__ __device__ inline int64_t a3_npb(int64_t T) { return attn_prep_npb(T); 
 // ---- preparation --------------------------------------------------------------------------------------
 // kb / vb [b*H + h][Tp][LR]: rows j < T hold bf16(K_j - kc) / bf16(V_j - vc) in columns < dk, zeros elsewhere;
 // cen [b*H + h][2][DKP] = (kc, vc) f32 (zeros past dk).  One workgroup per (64 rows, utterance b), every head:
-// the centres of all heads first (one thread per float4 column group of K | V summing the utterance's first n
-// rows in order -- attn_centre.h's kv_centre arithmetic, the same bits), then the 64 rows' conversion.  (One
-// workgroup per (64 rows, b, h) recomputed a head's centre with dk / 2 threads in 7 workgroups: 13.8 us per
-// launch in the step, profiles/r05/r5d_kernel_summary.txt.)
+// the centres of all heads (one thread per float4 column group of K | V summing the utterance's first n rows in
+// order -- attn_centre.h's kv_centre arithmetic, the same bits), then the 64 rows' conversion, one (kind, head)
+// tile after the other with the next tile's loads issued before the current one is converted (and the first
+// tile's before the centres).  A thread owns fixed (row, 8-column group) items of every tile: compile-time
+// index arithmetic, PER x 2 float4 loads in flight per tile.
 template <int DKP>
 __global__ __launch_bounds__(256) void attn_kv_prep_kernel(const float* __restrict__ qkv, const int64_t* __restrict__ lens,
                                                            uint16_t* __restrict__ kb, uint16_t* __restrict__ vb,
                                                            float* __restrict__ cen, int64_t H, int T, int64_t d, int dk,
                                                            int64_t Tp) {
-  constexpr int LR = DKP + 8, P8 = LR / 8;
+  constexpr int LR = DKP + 8, P8 = LR / 8, ITEMS = 64 * P8, PER = (ITEMS + 255) / 256;
   extern __shared__ __attribute__((aligned(16))) float Cn[];   // [kind][head][DKP]
   const int64_t b = blockIdx.y;
-  const int Hh = (int)H;
+  const int Hh = (int)H, nkh = 2 * Hh;
   const int len = lens ? (int)min<int64_t>(lens[b], T) : T;
   const float* kbase = qkv + b * T * 3 * d + d;   // row 0 of utterance b, K columns (V at + d)
+  const int j0 = blockIdx.x * 64;
+  int rowoff[PER], c0q[PER];
+  float m0q[PER], m1q[PER];
+  bool itq[PER];
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    const int item = threadIdx.x + 256 * q;
+    itq[q] = item < ITEMS;
+    const int rr = item / P8, c0 = (item - rr * P8) * 8;
+    const int j = j0 + rr;
+    rowoff[q] = (j < T ? j : 0);
+    c0q[q] = c0;
+    m0q[q] = (j < T && c0 < dk) ? 1.f : 0.f;
+    m1q[q] = (j < T && c0 + 4 < dk) ? 1.f : 0.f;
+  }
+  auto load = [&](int kh, float4 (&a)[PER], float4 (&e)[PER]) {
+    const int kind = kh >= Hh ? 1 : 0, h = kh - kind * Hh;
+    const float* src = kbase + (int64_t)kind * d + (int64_t)h * dk;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      const float* rs = src + (int64_t)rowoff[q] * 3 * d;
+      const int c0 = c0q[q];
+      a[q] = itq[q] ? *reinterpret_cast<const float4*>(rs + (c0 < dk ? c0 : 0)) : make_float4(0.f, 0.f, 0.f, 0.f);
+      e[q] = itq[q] ? *reinterpret_cast<const float4*>(rs + (c0 + 4 < dk ? c0 + 4 : 0)) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  float4 a0[PER], e0[PER];
+  load(0, a0, e0);
+  // centres
   const int n = len >= 16 ? 16 : len >= 8 ? 8 : len >= 4 ? 4 : len >= 2 ? 2 : (len > 0 ? 1 : 0);
   const float inv = n > 0 ? 1.f / (float)n : 0.f;   // a power of two: exact
-  for (int e = threadIdx.x; e < 2 * Hh * DKP; e += 256) Cn[e] = 0.f;
+  for (int e = threadIdx.x; e < nkh * DKP; e += 256) Cn[e] = 0.f;
   __syncthreads();
   const int cq = dk >> 2;
-  for (int g = threadIdx.x; g < 2 * Hh * cq; g += 256) {   // (kind, head, float4 column group)
-    const int kind = g / (Hh * cq), rem = g - kind * (Hh * cq);
-    const int h = rem / cq, c4 = (rem - h * cq) * 4;
+  for (int g = threadIdx.x; g < nkh * cq; g += 256) {   // (kind, head, float4 column group)
+    const int kh = g / cq, c4 = (g - kh * cq) * 4;
+    const int kind = kh >= Hh ? 1 : 0, h = kh - kind * Hh;
     const float* src = kbase + (int64_t)kind * d + (int64_t)h * dk + c4;
     float4 v[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) v[r] = *reinterpret_cast<const float4*>(src + (int64_t)(r < n ? r : 0) * 3 * d);
-    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 sm = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const float m = r < n ? 1.f : 0.f;
-      s.x += m * v[r].x; s.y += m * v[r].y; s.z += m * v[r].z; s.w += m * v[r].w;
+      sm.x += m * v[r].x; sm.y += m * v[r].y; sm.z += m * v[r].z; sm.w += m * v[r].w;
     }
-    float* o = Cn + (kind * Hh + h) * DKP + c4;
-    o[0] = s.x * inv; o[1] = s.y * inv; o[2] = s.z * inv; o[3] = s.w * inv;
+    float* o = Cn + kh * DKP + c4;
+    o[0] = sm.x * inv; o[1] = sm.y * inv; o[2] = sm.z * inv; o[3] = sm.w * inv;
   }
   __syncthreads();
   if (blockIdx.x == 0)
-    for (int e = threadIdx.x; e < 2 * Hh * DKP; e += 256) {   // cen[(b H + h)][kind][c]
-      const int kind = e / (Hh * DKP), rem = e - kind * (Hh * DKP);
-      const int h = rem / DKP, c = rem - h * DKP;
+    for (int e = threadIdx.x; e < nkh * DKP; e += 256) {   // cen[(b H + h)][kind][c]
+      const int kh = e / DKP, c = e - kh * DKP;
+      const int kind = kh >= Hh ? 1 : 0, h = kh - kind * Hh;
       cen[((b * H + h) * 2 + kind) * DKP + c] = Cn[e];
     }
-  const int j0 = blockIdx.x * 64;
-  for (int e = threadIdx.x; e < 2 * Hh * 64 * P8; e += 256) {
-    const int kind = e / (Hh * 64 * P8), r1 = e - kind * (Hh * 64 * P8);
-    const int h = r1 / (64 * P8), r2 = r1 - h * (64 * P8);
-    const int rr = r2 / P8, c0 = (r2 - rr * P8) * 8;
-    const int j = j0 + rr;
-    const float* src = kbase + (int64_t)kind * d + (int64_t)h * dk + (int64_t)(j < T ? j : 0) * 3 * d;
-    const float m0 = (j < T && c0 < dk) ? 1.f : 0.f, m1 = (j < T && c0 + 4 < dk) ? 1.f : 0.f;
-    const float4 a = *reinterpret_cast<const float4*>(src + (c0 < dk ? c0 : 0));
-    const float4 q = *reinterpret_cast<const float4*>(src + (c0 + 4 < dk ? c0 + 4 : 0));
-    const float* cc = Cn + (kind * Hh + h) * DKP;
-    const int ca = c0 < DKP ? c0 : 0, cb = c0 + 4 < DKP ? c0 + 4 : 0;
-    // (a - c) * m: the subtraction is the register-staged kernel's rk - ck, rounded to bf16 by the same RNE
-    const float t[8] = {(a.x - cc[ca]) * m0, (a.y - cc[ca + 1]) * m0, (a.z - cc[ca + 2]) * m0, (a.w - cc[ca + 3]) * m0,
-                        (q.x - cc[cb]) * m1, (q.y - cc[cb + 1]) * m1, (q.z - cc[cb + 2]) * m1, (q.w - cc[cb + 3]) * m1};
-    *reinterpret_cast<bf16x8*>((kind ? vb : kb) + ((b * H + h) * Tp + j) * LR + c0) = pack_bf16x8<bf16x8>(t);
+  for (int kh = 0; kh < nkh; ++kh) {
+    float4 a1[PER], e1[PER];
+    if (kh + 1 < nkh) load(kh + 1, a1, e1);
+    const int kind = kh >= Hh ? 1 : 0, h = kh - kind * Hh;
+    const float* cc = Cn + kh * DKP;
+    uint16_t* dst = (kind ? vb : kb) + ((b * H + h) * Tp + j0) * LR;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      if (!itq[q]) continue;
+      const int item = threadIdx.x + 256 * q;
+      const int c0 = c0q[q];
+      const float4 a = a0[q], e = e0[q];
+      const float m0 = m0q[q], m1 = m1q[q];
+      const int ca = c0 < DKP ? c0 : 0, cb = c0 + 4 < DKP ? c0 + 4 : 0;
+      // (a - c) * m: the subtraction is the register-staged kernel's rk - ck, rounded to bf16 by the same RNE
+      const float t[8] = {(a.x - cc[ca]) * m0, (a.y - cc[ca + 1]) * m0, (a.z - cc[ca + 2]) * m0, (a.w - cc[ca + 3]) * m0,
+                          (e.x - cc[cb]) * m1, (e.y - cc[cb + 1]) * m1, (e.z - cc[cb + 2]) * m1, (e.w - cc[cb + 3]) * m1};
+      *reinterpret_cast<bf16x8*>(dst + item * 8) = pack_bf16x8<bf16x8>(t);   // row item / P8, column c0
+    }
+#pragma unroll
+    for (int q = 0; q < PER; ++q) { a0[q] = a1[q]; e0[q] = e1[q]; }
   }
 }
 
@@ -202,12 +237,14 @@ __device__ __forceinline__ float a3_sum16(float v) {
 }
 
 template <int NU>
-__global__ __launch_bounds__(256, NU == 3 ? 3 : 2) void relpos_attn_fwd3_kernel(Attn3P p) {
+__global__ __launch_bounds__(256, NU == 3 ? 4 : NU == 4 ? 3 : 2) void relpos_attn_fwd3_kernel(Attn3P p) {
   using Gm = A3Geo<NU>;
   constexpr int KS = Gm::KS, LR = Gm::LR, KCH = Gm::KCH, BCH = Gm::BCH, NCH = 2 * KCH + BCH;
-  // K tile | V tile | band rows, contiguous: 1 KB DMA chunk f lands at byte f * 1024 whichever tile it is
+  // K tile | V tile | band rows, contiguous (wave w's DMA chunks at fixed offsets).  The per-wave P^T tiles
+  // [key][row] reuse the K tile once every wave has read it (a barrier after the score MFMAs): 37 KB per
+  // workgroup, 4 workgroups per CU at head dim <= 48
+  static_assert(4 * A3K * A3LDT <= A3K * LR, "the P^T tiles must fit in the K tile");
   __shared__ __attribute__((aligned(16))) uint16_t Sm[(2 * A3K + A3BAND) * LR];
-  __shared__ __attribute__((aligned(16))) uint16_t Pt[4][A3K * A3LDT];   // per wave: P^T [key][row]
   uint16_t* const Ks = Sm;
   uint16_t* const Vs = Sm + A3K * LR;
   uint16_t* const Pr = Sm + 2 * A3K * LR;
@@ -228,23 +265,28 @@ __global__ __launch_bounds__(256, NU == 3 ? 3 : 2) void relpos_attn_fwd3_kernel(
 
   // one key step's operands: K rows [j0, j0 + 64), V rows, band rows [rbase, rbase + 128) of the prepared
   // band (row A3PAD0 + r holds position r) -- NCH 1 KB chunks, wave w takes chunks w, w + 4, ...
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  const uint32_t loff = (uint32_t)lane * 16u;
   auto issue = [&](int j0) {
-    // wave-uniform chunk bases (SGPR address + this lane's 16-byte offset: no per-chunk 64-bit lane addresses
-    // held across the loop)
+    // wave wu copies chunks wu, wu + 4, ... of each tile: uniform (SGPR) chunk addresses plus this lane's 16
+    // bytes, LDS destinations at compile-time offsets from the wave's first chunk
     const int rb = T - 1 - (i0 + A3Q - 1) + j0 + A3PAD0;
-    const char* kbase = reinterpret_cast<const char*>(ksrc) + (int64_t)j0 * LR * 2;
-    const char* vbase = reinterpret_cast<const char*>(vsrc) + (int64_t)j0 * LR * 2;
-    const char* bbase = reinterpret_cast<const char*>(bsrc + (int64_t)rb * LR);
-    const uint32_t loff = (uint32_t)lane * 16u;
+    const char* kbase = reinterpret_cast<const char*>(ksrc) + (int64_t)j0 * LR * 2 + wu * 1024;
+    const char* vbase = reinterpret_cast<const char*>(vsrc) + (int64_t)j0 * LR * 2 + wu * 1024;
+    const char* bbase = reinterpret_cast<const char*>(bsrc + (int64_t)rb * LR) + wu * 1024;
+    uint4* const ld0 = reinterpret_cast<uint4*>(Sm) + wu * 64;
 #pragma unroll
-    for (int i = 0; i < (NCH + 3) / 4; ++i) {
-      const int f = w + 4 * i;   // wave-uniform
-      if (4 * i + 3 < NCH || f < NCH) {
-        const char* src = f < KCH ? kbase + f * 1024 : f < 2 * KCH ? vbase + (f - KCH) * 1024 : bbase + (f - 2 * KCH) * 1024;
-        __builtin_amdgcn_global_load_lds((gl_void_t3*)(src + loff), (lds_void_t3*)(reinterpret_cast<uint4*>(Sm) + f * 64),
+    for (int i = 0; i < (KCH + 3) / 4; ++i)
+      if (4 * i + 3 < KCH || wu + 4 * i < KCH) {
+        __builtin_amdgcn_global_load_lds((gl_void_t3*)(kbase + i * 4096 + loff), (lds_void_t3*)(ld0 + i * 256), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((gl_void_t3*)(vbase + i * 4096 + loff), (lds_void_t3*)(ld0 + KCH * 64 + i * 256),
                                          16, 0, 0);
       }
-    }
+#pragma unroll
+    for (int i = 0; i < (BCH + 3) / 4; ++i)
+      if (4 * i + 3 < BCH || wu + 4 * i < BCH)
+        __builtin_amdgcn_global_load_lds((gl_void_t3*)(bbase + i * 4096 + loff),
+                                         (lds_void_t3*)(ld0 + 2 * KCH * 64 + i * 256), 16, 0, 0);
   };
   if (nkb > 0) issue(0);
 
@@ -294,7 +336,7 @@ __global__ __launch_bounds__(256, NU == 3 ? 3 : 2) void relpos_attn_fwd3_kernel(
   f32x4 oacc[NU];
 #pragma unroll
   for (int u = 0; u < NU; ++u) oacc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-  uint16_t* Pw = Pt[w];
+  uint16_t* Pw = Sm + w * (A3K * A3LDT);
 
   for (int kb = 0; kb < nkb; ++kb) {
     const int j0 = kb * A3K;
@@ -325,6 +367,7 @@ __global__ __launch_bounds__(256, NU == 3 ? 3 : 2) void relpos_attn_fwd3_kernel(
       for (int t = 0; t < 5; ++t) g[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fv[ks], pf[t], g[t], 0, 0, 0);
     }
     // raw scores s = S_ac + S_bd (unscaled), the rel_shift by lane permutes
+    __syncthreads();   // every wave has read the K tile: its space takes the P^T tiles below
     float s[4][4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {

@@ -1,6 +1,6 @@
 # PMC breakdown of the fwd3 attention forward (teacher shape, dropout 0.1), isolated
 set -o pipefail
-OUT=gpurun_out/r5i
+OUT=${OUT:-gpurun_out/r5i}
 mkdir -p $OUT
 export TMPDIR=/tmp
 rocprofv3 -L > $OUT/counters.txt 2>&1 || true
