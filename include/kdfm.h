@@ -581,6 +581,22 @@ int kdfm_subsample_conv2_dgrad_w0(const float* dy2, const uint16_t* wt, const ui
                                   int64_t ws_len, void* stream);
 int kdfm_subsample_conv2_dgrad(const float* dy2, const uint16_t* wt, const uint16_t* y1, float* dy1, int64_t B, int64_t T1,
                                int64_t F1, int64_t C, void* stream);
+/* The same with a bf16 dy2 (kdfm_ss_out_dgrad's output): one 16-byte load of 8 channels per k-step instead of
+ * two f32 ones (the tap re-reads of dy2 are the kernel's dominant traffic). */
+int kdfm_subsample_conv2_dgrad_w0_h(const uint16_t* dy2h, const uint16_t* wt, const uint16_t* y1, float* dy1, int64_t B,
+                                    int64_t T1, int64_t F1, int64_t C, const float* mel, const int64_t* mel_len,
+                                    int64_t Tm, int64_t Fm, int64_t pad, float* dw0, float* db0, float* ws,
+                                    int64_t ws_len, void* stream);
+/* Subsampling output Linear(C F2 -> d) backward into the conv2 output gradient (replaces linear_dx with the
+ * DRELU epilogue + a bf16 cast; conformer_encoder.py:381-390 ConvSubsampling.out): with the channels-last
+ * conv2 output y2 (rows, ncols = F2 C) f32 and dlin (rows, d) f32,
+ *   dy2h[r][n] = bf16([y2[r][n] > 0] * sum_{k < d} bf16(dlin[r][k]) bf16(W[k][n]))   (f32 accumulation).
+ * kdfm_ss_out_wprep writes wt = W^T as bf16 [ncols][32 ceil(d / 32)] (kdfm_ss_out_wprep_elems elements; W is
+ * the (d, ncols) re-laid output weight).  d <= 128, ncols % 4 == 0. */
+int64_t kdfm_ss_out_wprep_elems(int64_t d, int64_t ncols);
+int kdfm_ss_out_wprep(const float* W, uint16_t* wt, int64_t d, int64_t ncols, void* stream);
+int kdfm_ss_out_dgrad(const float* dlin, const uint16_t* wt, const float* y2, uint16_t* dy2h, int64_t rows, int64_t d,
+                      int64_t ncols, void* stream);
 
 /* ---------------- Evaluation path (ctc_models.py:625-692, wer.py) ---------
  * kdfm_ctc_greedy: CTC greedy decoding (Appendix A.9; WER.update wer.py:329-333): per utterance b,

@@ -24,6 +24,7 @@ namespace {
 
 typedef __attribute__((ext_vector_type(8))) short bf16x8_t;
 typedef __attribute__((ext_vector_type(16))) float f32x16_t;
+typedef __attribute__((ext_vector_type(4))) float f32x4_t;
 
 // ---- weight prep: W (C, C, 3, 3) f32 -> wb[n][tap][ci] bf16, n < Np (zero rows >= C), ci < Cp
 __global__ __launch_bounds__(256) void ss_wprep_kernel(const float* __restrict__ W, uint16_t* __restrict__ wb, int C,
@@ -302,7 +303,7 @@ struct SdFrag {
   float4 v[KS][2];
 };
 
-template <int NCT, int KS, int PT, int PF>
+template <int NCT, int KS, int PT, int PF, bool DBF>
 __device__ __forceinline__ void sd_class(const SdGeo& g, __amdgpu_buffer_rsrc_t rdy2, __amdgpu_buffer_rsrc_t ry1,
                                          __amdgpu_buffer_rsrc_t rdy1, bool has_dy1, uint16_t* lds, int cls,
                                          float (&wacc)[NCT][10]) {
@@ -333,22 +334,25 @@ __device__ __forceinline__ void sd_class(const SdGeo& g, __amdgpu_buffer_rsrc_t 
   const int ntile = (npos + 32 * SS_WAVES - 1) / (32 * SS_WAVES);
   const int tile0 = (int)(blockIdx.x - g.wg0[cls]) * SD_TPW;
   const int tend = min(tile0 + SD_TPW, ntile);
-  // lane's channel offsets (bytes) into dy2 rows per k-step s; padded channels (>= C) read out of range
+  // lane's channel offsets (bytes) into dy2 rows per k-step s; padded channels (>= C) read out of range.
+  // DBF: dy2 is bf16 (one 16-byte load of 8 channels per k-step, no conversion), else f32 (two, packed)
+  constexpr uint32_t EB = DBF ? 2u : 4u;
   uint32_t coff[KS];
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
     const int co = 16 * s + 8 * h;
-    coff[s] = co < g.C ? (uint32_t)co * 4u : SD_OOB;
+    coff[s] = co < g.C ? (uint32_t)co * EB : SD_OOB;
   }
   auto load_tap = [&](SdFrag<NCT, KS>& f, int t, bool ok, int b, int i, int j) {
     const int t2 = i + ((PT && (t / DF) == 0) ? 1 : 0), f2 = j + ((PF && (t % DF) == 0) ? 1 : 0);
     const bool in = ok && t2 < g.T2 && f2 < g.F2;
-    const uint32_t base = in ? (uint32_t)(((b * g.T2 + t2) * g.F2 + f2) * g.C) * 4u : SD_OOB;
+    const uint32_t base = in ? (uint32_t)(((b * g.T2 + t2) * g.F2 + f2) * g.C) * EB : SD_OOB;
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
       const uint32_t o = (base == SD_OOB || coff[s] == SD_OOB) ? SD_OOB : base + coff[s];
       f.v[s][0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rdy2, o, 0, 0));
-      f.v[s][1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rdy2, o == SD_OOB ? SD_OOB : o + 16, 0, 0));
+      if constexpr (!DBF)
+        f.v[s][1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rdy2, o == SD_OOB ? SD_OOB : o + 16, 0, 0));
     }
   };
   SdFrag<NCT, KS> fa;   // a tap's dy2 fragments (f32); tap 0's are loaded before the ReLU' masks
@@ -428,9 +432,13 @@ __device__ __forceinline__ void sd_class(const SdGeo& g, __amdgpu_buffer_rsrc_t 
       bf16x8_t a[KS];
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
-        const float q[8] = {fa.v[s][0].x, fa.v[s][0].y, fa.v[s][0].z, fa.v[s][0].w,
-                            fa.v[s][1].x, fa.v[s][1].y, fa.v[s][1].z, fa.v[s][1].w};
-        a[s] = pack_bf16x8<bf16x8_t>(q);
+        if constexpr (DBF) {
+          a[s] = __builtin_bit_cast(bf16x8_t, fa.v[s][0]);
+        } else {
+          const float q[8] = {fa.v[s][0].x, fa.v[s][0].y, fa.v[s][0].z, fa.v[s][0].w,
+                              fa.v[s][1].x, fa.v[s][1].y, fa.v[s][1].z, fa.v[s][1].w};
+          a[s] = pack_bf16x8<bf16x8_t>(q);
+        }
       }
       const uint16_t* bp = lds + (t * NP + r) * g.ldb + 8 * h;
 #pragma unroll
@@ -486,8 +494,8 @@ __device__ __forceinline__ void sd_class(const SdGeo& g, __amdgpu_buffer_rsrc_t 
   }
 }
 
-template <int NCT, int KS>
-__global__ __launch_bounds__(SS_NT, 1) void ss_dgrad_kernel(const float* __restrict__ dy2,
+template <int NCT, int KS, bool DBF>
+__global__ __launch_bounds__(SS_NT, 1) void ss_dgrad_kernel(const void* __restrict__ dy2,
                                                             const uint16_t* __restrict__ y1, float* __restrict__ dy1,
                                                             SdGeo g) {
   extern __shared__ __attribute__((aligned(16))) uint16_t sd_lds[];
@@ -496,7 +504,7 @@ __global__ __launch_bounds__(SS_NT, 1) void ss_dgrad_kernel(const float* __restr
   int cls = 0;
   while (cls < 3 && (int64_t)blockIdx.x >= g.wg0[cls + 1]) ++cls;
   const __amdgpu_buffer_rsrc_t rdy2 =
-      __builtin_amdgcn_make_buffer_rsrc((void*)dy2, (short)0, (int)((int64_t)g.B * g.T2 * g.F2 * g.C * 4), 0x00020000);
+      __builtin_amdgcn_make_buffer_rsrc((void*)dy2, (short)0, (int)((int64_t)g.B * g.T2 * g.F2 * g.C * (DBF ? 2 : 4)), 0x00020000);
   const __amdgpu_buffer_rsrc_t ry1 =
       __builtin_amdgcn_make_buffer_rsrc((void*)y1, (short)0, (int)((int64_t)g.B * g.T1 * g.F1 * g.C * 2), 0x00020000);
   const __amdgpu_buffer_rsrc_t rdy1 = __builtin_amdgcn_make_buffer_rsrc(
@@ -507,10 +515,10 @@ __global__ __launch_bounds__(SS_NT, 1) void ss_dgrad_kernel(const float* __restr
 #pragma unroll
     for (int k = 0; k < 10; ++k) wacc[n][k] = 0.f;
   switch (cls) {
-    case 0: sd_class<NCT, KS, 0, 0>(g, rdy2, ry1, rdy1, dy1 != nullptr, sd_lds, 0, wacc); break;
-    case 1: sd_class<NCT, KS, 0, 1>(g, rdy2, ry1, rdy1, dy1 != nullptr, sd_lds, 1, wacc); break;
-    case 2: sd_class<NCT, KS, 1, 0>(g, rdy2, ry1, rdy1, dy1 != nullptr, sd_lds, 2, wacc); break;
-    default: sd_class<NCT, KS, 1, 1>(g, rdy2, ry1, rdy1, dy1 != nullptr, sd_lds, 3, wacc); break;
+    case 0: sd_class<NCT, KS, 0, 0, DBF>(g, rdy2, ry1, rdy1, dy1 != nullptr, sd_lds, 0, wacc); break;
+    case 1: sd_class<NCT, KS, 0, 1, DBF>(g, rdy2, ry1, rdy1, dy1 != nullptr, sd_lds, 1, wacc); break;
+    case 2: sd_class<NCT, KS, 1, 0, DBF>(g, rdy2, ry1, rdy1, dy1 != nullptr, sd_lds, 2, wacc); break;
+    default: sd_class<NCT, KS, 1, 1, DBF>(g, rdy2, ry1, rdy1, dy1 != nullptr, sd_lds, 3, wacc); break;
   }
   if (!g.wpart) return;
   // per-workgroup partial: lanes r / r + 32 hold the same channels, then the 8 waves in order
@@ -539,20 +547,101 @@ __global__ __launch_bounds__(SS_NT, 1) void ss_dgrad_kernel(const float* __restr
   }
 }
 
-template <int NCT, int KS>
-int sd_launch(const float* dy2, const uint16_t* wt, const uint16_t* y1, float* dy1, SdGeo g, hipStream_t st) {
+// ---- the output Linear's data gradient as the bf16 conv2 output gradient -----------------------------
+// dy2h[r][n] = bf16( [y2[r][n] > 0] * sum_k dlin[r][k] W[k][n] ),  n < ncols = F2 * C, k < d <= 32 KS
+// (Linear(C F2 -> d) of the channels-last conv2 output, ReLU' of that output): was kdfm_gemm's linear_dx with
+// the DRELU epilogue writing f32 (90 MB at the bench shape, 118 us in the step) and a bf16 cast of it for the
+// conv2 weight gradient; here one pass writes the bf16 operand that the conv2 data gradient
+// (kdfm_subsample_conv2_dgrad_w0_h) and weight gradient both read.  C^T tiles (v_mfma_f32_16x16x32_bf16):
+// A = W^T, a slice of SO_TILES x 16 columns staged in LDS from the prepared bf16 [col][k] image
+// (kdfm_ss_out_wprep), B = 16 rows of dlin (f32 loads, rounded to bf16 as kdfm_gemm's bf16 math does), so a
+// lane ends with 4 consecutive columns of one row: one 16-byte load of y2 for the mask, one 8-byte store.
+constexpr int SO_TILES = 11;   // 176 columns per workgroup
+constexpr int SO_RT = 4;       // row tiles of 16 per wave (256 rows per workgroup)
+
+__global__ __launch_bounds__(256) void ss_out_wprep_kernel(const float* __restrict__ W, uint16_t* __restrict__ wt, int d,
+                                                           int64_t ncols, int KP) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;   // wt[n][k]
+  if (idx >= ncols * KP) return;
+  const int64_t n = idx / KP;
+  const int k = (int)(idx - n * KP);
+  wt[idx] = f2bf(k < d ? W[(int64_t)k * ncols + n] : 0.f);
+}
+
+template <int KS>
+__global__ __launch_bounds__(256) void ss_out_dgrad_kernel(const float* __restrict__ dlin, const uint16_t* __restrict__ wt,
+                                                           const float* __restrict__ y2, uint16_t* __restrict__ dy2h,
+                                                           int64_t rows, int d, int64_t ncols) {
+  constexpr int KP = 32 * KS, LDW = KP + 8, NCOL = SO_TILES * 16, C8 = KP / 8;
+  __shared__ __attribute__((aligned(16))) uint16_t Ws[NCOL * LDW];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, q = lane >> 4, lo = lane & 15;
+  const int64_t n0 = (int64_t)blockIdx.x * NCOL;
+  // stage the W^T slice [col][k] (columns past ncols read as zero)
+  constexpr int NCH = NCOL * C8, PER = (NCH + 255) / 256;
+  bf16x8_t st[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int e = threadIdx.x + 256 * i;
+    const int c = e / C8, k8 = (e - c * C8) * 8;
+    st[i] = (e < NCH && n0 + c < ncols) ? *reinterpret_cast<const bf16x8_t*>(wt + (n0 + c) * KP + k8) : bf16x8_t{};
+  }
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int e = threadIdx.x + 256 * i;
+    const int c = e / C8, k8 = (e - c * C8) * 8;
+    if (e < NCH) *reinterpret_cast<bf16x8_t*>(Ws + c * LDW + k8) = st[i];
+  }
+  __syncthreads();
+  for (int rt = 0; rt < SO_RT; ++rt) {
+    const int64_t rb = ((int64_t)blockIdx.y * 4 * SO_RT + w * SO_RT + rt) * 16;
+    if (rb >= rows) break;   // wave-uniform
+    const int64_t row = rb + lo;
+    const bool rin = row < rows;
+    // B fragments: dlin[row][32 ks + 8 q .. + 7]
+    bf16x8_t bfr[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int c0 = 32 * ks + 8 * q;
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = (rin && c0 + e < d) ? dlin[row * d + c0 + e] : 0.f;
+      bfr[ks] = pack_bf16x8<bf16x8_t>(v);
+    }
+#pragma unroll
+    for (int t = 0; t < SO_TILES; ++t) {
+      f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(Ws + (t * 16 + lo) * LDW + 32 * ks + 8 * q);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bfr[ks], acc, 0, 0, 0);
+      }
+      // acc[r] = C^T[column n0 + 16 t + 4 q + r][row]
+      const int64_t col = n0 + 16 * t + 4 * q;
+      if (rin && col < ncols) {
+        const float4 m = *reinterpret_cast<const float4*>(y2 + row * ncols + col);
+        const float a0 = acc[0], a1 = acc[1], a2 = acc[2], a3 = acc[3];
+        const uint2 o = make_uint2(pack_bf16x2(m.x > 0.f ? a0 : 0.f, m.y > 0.f ? a1 : 0.f),
+                                   pack_bf16x2(m.z > 0.f ? a2 : 0.f, m.w > 0.f ? a3 : 0.f));
+        *reinterpret_cast<uint2*>(dy2h + row * ncols + col) = o;
+      }
+    }
+  }
+}
+
+template <int NCT, int KS, bool DBF>
+int sd_launch(const void* dy2, const uint16_t* wt, const uint16_t* y1, float* dy1, SdGeo g, hipStream_t st) {
   g.wt = wt;
   // 4 tap slabs (the largest class) + per-wave patch / index buffers; the fold reuses the space
   size_t lds = (size_t)4 * 32 * NCT * g.ldb * sizeof(uint16_t) + (size_t)SS_WAVES * (32 * SD_PTS + 32) * 4;
   const size_t red = (size_t)SS_WAVES * NCT * 10 * 32 * sizeof(float);   // fused conv0 wgrad reduction
   if (g.wpart && red > lds) lds = red;
   static bool once = [] {
-    (void)hipFuncSetAttribute((const void*)ss_dgrad_kernel<NCT, KS>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)ss_dgrad_kernel<NCT, KS, DBF>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
     return true;
   }();
   (void)once;
-  hipLaunchKernelGGL((ss_dgrad_kernel<NCT, KS>), dim3((unsigned)g.wg0[4]), dim3(SS_NT), lds, st, dy2, y1, dy1, g);
+  hipLaunchKernelGGL((ss_dgrad_kernel<NCT, KS, DBF>), dim3((unsigned)g.wg0[4]), dim3(SS_NT), lds, st, dy2, y1, dy1, g);
   return check_launch("kdfm_subsample_conv2_dgrad");
 }
 
@@ -627,6 +716,8 @@ int kdfm_subsample_dgrad_wprep(const float* w2, uint16_t* wt, int64_t C, void* s
   return check_launch("kdfm_subsample_dgrad_wprep");
 }
 
+}  // extern "C"
+
 namespace kdfm {
 namespace {
 int sd_geo(SdGeo& g, int64_t B, int64_t T1, int64_t F1, int64_t C) {
@@ -643,17 +734,20 @@ int sd_geo(SdGeo& g, int64_t B, int64_t T1, int64_t F1, int64_t C) {
   g.mel = nullptr; g.mel_len = nullptr; g.Tm = g.Fm = g.pad = 0; g.wpart = nullptr; g.wt = nullptr;
   return 0;
 }
-int sd_dispatch(const float* dy2, const uint16_t* wt, const uint16_t* y1, float* dy1, const SdGeo& g, hipStream_t st) {
+template <bool DBF>
+int sd_dispatch(const void* dy2, const uint16_t* wt, const uint16_t* y1, float* dy1, const SdGeo& g, hipStream_t st) {
   const int nct = (int)ceil_div(g.C, 32), ks = g.Cp / 16;
-  if (nct == 3 && ks == 6) return sd_launch<3, 6>(dy2, wt, y1, dy1, g, st);    // d = 88 / 96
-  if (nct == 1 && ks == 1) return sd_launch<1, 1>(dy2, wt, y1, dy1, g, st);    // test sizes
-  if (nct == 1 && ks == 2) return sd_launch<1, 2>(dy2, wt, y1, dy1, g, st);
-  if (nct == 2 && ks == 4) return sd_launch<2, 4>(dy2, wt, y1, dy1, g, st);
+  if (nct == 3 && ks == 6) return sd_launch<3, 6, DBF>(dy2, wt, y1, dy1, g, st);    // d = 88 / 96
+  if (nct == 1 && ks == 1) return sd_launch<1, 1, DBF>(dy2, wt, y1, dy1, g, st);    // test sizes
+  if (nct == 1 && ks == 2) return sd_launch<1, 2, DBF>(dy2, wt, y1, dy1, g, st);
+  if (nct == 2 && ks == 4) return sd_launch<2, 4, DBF>(dy2, wt, y1, dy1, g, st);
   set_error("kdfm_subsample_conv2_dgrad: unsupported channel count");
   return KDFM_EUNSUPPORTED;
 }
 }  // namespace
 }  // namespace kdfm
+
+extern "C" {
 
 int64_t kdfm_subsample_conv2_dgrad_w0_ws(int64_t B, int64_t T1, int64_t F1, int64_t C) {
   kdfm::SdGeo g;
@@ -661,11 +755,14 @@ int64_t kdfm_subsample_conv2_dgrad_w0_ws(int64_t B, int64_t T1, int64_t F1, int6
   return g.wg0[4] * C * 10;
 }
 
-int kdfm_subsample_conv2_dgrad_w0(const float* dy2, const uint16_t* wt, const uint16_t* y1, float* dy1, int64_t B,
-                                  int64_t T1, int64_t F1, int64_t C, const float* mel, const int64_t* mel_len,
-                                  int64_t Tm, int64_t Fm, int64_t pad, float* dw0, float* db0, float* ws,
-                                  int64_t ws_len, void* stream) {
-  using namespace kdfm;
+}  // extern "C"
+
+namespace kdfm {
+namespace {
+template <bool DBF>
+int sd_w0(const void* dy2, const uint16_t* wt, const uint16_t* y1, float* dy1, int64_t B, int64_t T1, int64_t F1,
+          int64_t C, const float* mel, const int64_t* mel_len, int64_t Tm, int64_t Fm, int64_t pad, float* dw0,
+          float* db0, float* ws, int64_t ws_len, void* stream) {
   KDFM_REQUIRE(dy2 && wt && y1 && mel && dw0 && db0 && ws, "null pointer");
   KDFM_REQUIRE(C % 8 == 0 && B > 0 && T1 > 0 && F1 > 0, "C must be a multiple of 8");
   KDFM_REQUIRE(((((uintptr_t)dy2) | ((uintptr_t)wt)) & 15) == 0, "dy2 / wt must be 16-byte aligned");
@@ -677,10 +774,28 @@ int kdfm_subsample_conv2_dgrad_w0(const float* dy2, const uint16_t* wt, const ui
   KDFM_REQUIRE(ws_len >= g.wg0[4] * C * 10, "workspace too small (kdfm_subsample_conv2_dgrad_w0_ws)");
   g.mel = mel; g.mel_len = mel_len; g.Tm = (int)Tm; g.Fm = (int)Fm; g.pad = (int)pad; g.wpart = ws;
   hipStream_t st = as_stream(stream);
-  int rc = sd_dispatch(dy2, wt, y1, dy1, g, st);
+  int rc = sd_dispatch<DBF>(dy2, wt, y1, dy1, g, st);
   if (rc) return rc;
   // fixed-order fold of the per-workgroup partials: dW0 (C, 9) += sum_wg, db0 (C) += sum_wg
   return launch_colsum2(ws, dw0, C * 9, db0, g.wg0[4], C * 10, C * 10, 1.f, st);
+}
+}  // namespace
+}  // namespace kdfm
+
+extern "C" {
+
+int kdfm_subsample_conv2_dgrad_w0(const float* dy2, const uint16_t* wt, const uint16_t* y1, float* dy1, int64_t B,
+                                  int64_t T1, int64_t F1, int64_t C, const float* mel, const int64_t* mel_len,
+                                  int64_t Tm, int64_t Fm, int64_t pad, float* dw0, float* db0, float* ws,
+                                  int64_t ws_len, void* stream) {
+  return kdfm::sd_w0<false>(dy2, wt, y1, dy1, B, T1, F1, C, mel, mel_len, Tm, Fm, pad, dw0, db0, ws, ws_len, stream);
+}
+
+int kdfm_subsample_conv2_dgrad_w0_h(const uint16_t* dy2h, const uint16_t* wt, const uint16_t* y1, float* dy1, int64_t B,
+                                    int64_t T1, int64_t F1, int64_t C, const float* mel, const int64_t* mel_len,
+                                    int64_t Tm, int64_t Fm, int64_t pad, float* dw0, float* db0, float* ws,
+                                    int64_t ws_len, void* stream) {
+  return kdfm::sd_w0<true>(dy2h, wt, y1, dy1, B, T1, F1, C, mel, mel_len, Tm, Fm, pad, dw0, db0, ws, ws_len, stream);
 }
 
 int kdfm_subsample_conv2_dgrad(const float* dy2, const uint16_t* wt, const uint16_t* y1, float* dy1, int64_t B, int64_t T1,
@@ -693,7 +808,40 @@ int kdfm_subsample_conv2_dgrad(const float* dy2, const uint16_t* wt, const uint1
   sd_geo(g, B, T1, F1, C);
   KDFM_REQUIRE(g.wg0[4] < (1ll << 31) && B * T1 * F1 * C * 4 < (1ll << 31),
                "too large (32-bit buffer offsets: dy1 / y1 / dy2 < 2 GiB)");
-  return sd_dispatch(dy2, wt, y1, dy1, g, as_stream(stream));
+  return sd_dispatch<false>(dy2, wt, y1, dy1, g, as_stream(stream));
+}
+
+int64_t kdfm_ss_out_wprep_elems(int64_t d, int64_t ncols) {
+  if (d <= 0 || d > 128 || ncols <= 0) return -1;
+  return ncols * 32 * kdfm::ceil_div(d, 32);
+}
+
+int kdfm_ss_out_wprep(const float* W, uint16_t* wt, int64_t d, int64_t ncols, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(W && wt, "null pointer");
+  KDFM_REQUIRE(d > 0 && d <= 128 && ncols > 0, "d must be in (0, 128]");
+  const int KP = (int)(32 * ceil_div(d, 32));
+  const int64_t n = ncols * KP;
+  hipLaunchKernelGGL(ss_out_wprep_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, as_stream(stream), W, wt,
+                     (int)d, ncols, KP);
+  return check_launch("kdfm_ss_out_wprep");
+}
+
+int kdfm_ss_out_dgrad(const float* dlin, const uint16_t* wt, const float* y2, uint16_t* dy2h, int64_t rows, int64_t d,
+                      int64_t ncols, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(dlin && wt && y2 && dy2h, "null pointer");
+  KDFM_REQUIRE(d > 0 && d <= 128 && ncols > 0 && ncols % 4 == 0, "d in (0, 128], ncols a multiple of 4");
+  KDFM_REQUIRE((((uintptr_t)wt | (uintptr_t)y2) & 15) == 0 && ((uintptr_t)dy2h & 7) == 0, "operands misaligned");
+  if (rows == 0) return KDFM_OK;
+  const dim3 grid((unsigned)ceil_div(ncols, SO_TILES * 16), (unsigned)ceil_div(rows, 64 * SO_RT));
+  hipStream_t st = as_stream(stream);
+  const int ks = (int)ceil_div(d, 32);
+  if (ks == 1) hipLaunchKernelGGL(ss_out_dgrad_kernel<1>, grid, dim3(256), 0, st, dlin, wt, y2, dy2h, rows, (int)d, ncols);
+  else if (ks == 2) hipLaunchKernelGGL(ss_out_dgrad_kernel<2>, grid, dim3(256), 0, st, dlin, wt, y2, dy2h, rows, (int)d, ncols);
+  else if (ks == 3) hipLaunchKernelGGL(ss_out_dgrad_kernel<3>, grid, dim3(256), 0, st, dlin, wt, y2, dy2h, rows, (int)d, ncols);
+  else hipLaunchKernelGGL(ss_out_dgrad_kernel<4>, grid, dim3(256), 0, st, dlin, wt, y2, dy2h, rows, (int)d, ncols);
+  return check_launch("kdfm_ss_out_dgrad");
 }
 
 }  // extern "C"

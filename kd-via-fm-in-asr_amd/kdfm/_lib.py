@@ -129,6 +129,11 @@ SIGNATURES: dict[str, tuple] = {
     "kdfm_subsample_conv2_dgrad_w0_ws": (_i64, [_i64, _i64, _i64, _i64]),
     "kdfm_subsample_conv2_dgrad_w0": (_i32, [P, P, P, P, _i64, _i64, _i64, _i64, P, P, _i64, _i64, _i64, P, P, P, _i64,
                                               P]),
+    "kdfm_subsample_conv2_dgrad_w0_h": (_i32, [P, P, P, P, _i64, _i64, _i64, _i64, P, P, _i64, _i64, _i64, P, P, P, _i64,
+                                              P]),
+    "kdfm_ss_out_wprep_elems": (_i64, [_i64, _i64]),
+    "kdfm_ss_out_wprep": (_i32, [P, P, _i64, _i64, P]),
+    "kdfm_ss_out_dgrad": (_i32, [P, P, P, P, _i64, _i64, _i64, P]),
     "kdfm_denoise_chain_fwd": (_i32, [P, P, P, P, P, P, P, P, P, _i64, _i64, _i32, _i32, P]),
     "kdfm_denoise_chain_bwd": (_i32, [P, P, P, P, P, P, P, P, _i64, _i64, _i32, _i32, P]),
     "kdfm_range_pop": (_i32, []),

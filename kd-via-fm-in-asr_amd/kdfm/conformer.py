@@ -117,8 +117,9 @@ def _out_linear(cfg, S, P, pre, y, *, train, seed, salt, ws):
     return x, p_pre, xscale
 
 
-def _out_linear_backward(S, P, G, pre, ctx, dx, y, *, seed, salt, ws):
-    """-> gradient wrt the last stage's pre-activation (relu'(y) applied: y is a ReLU output)."""
+def _out_linear_backward(S, P, G, pre, ctx, dx, y, *, seed, salt, ws, bf16_out=False):
+    """-> gradient wrt the last stage's pre-activation (relu'(y) applied: y is a ReLU output); bf16_out: as a
+    bf16 tensor from one kdfm_ss_out_dgrad pass (the operand both conv2 gradients read)."""
     d, C = S.d, S.C
     dlin = _empty(S.rows, d, dev=dx.device)
     K.dropout(dx, dlin, ctx["p_pre"], ctx["xscale"], seed, _stream(salt, -1, SITE_PRE))
@@ -131,6 +132,12 @@ def _out_linear_backward(S, P, G, pre, ctx, dx, y, *, seed, salt, ws):
         K.convw_grad(Gout, G[pre + "pre_encode.out.weight"].view(d, C, S.F2))
         K.colsum(dlin, G[pre + "pre_encode.out.bias"])
     _side(out_wgrad, dlin, yv)
+    if bf16_out:
+        wt = ws["wout_t_bf16"]
+        K.ss_out_wprep(ws["wout_perm"].view(d, S.F2 * C), wt)
+        g = torch.empty(y.shape[0], C, device=dx.device, dtype=torch.bfloat16)
+        K.ss_out_dgrad(dlin, wt, yv, g.view(S.rows, S.F2 * C))
+        return g
     g = _empty(y.shape[0], C, dev=dx.device)
     K.linear_dx(dlin, ws["wout_perm"].view(d, S.F2 * C), g.view(S.rows, S.F2 * C), epi=_lib.EPI_DRELU,
                 aux=y.view(S.rows, S.F2 * C))
@@ -279,23 +286,33 @@ def subsampling_backward(cfg, S: EncoderShapes, P, G, pre, ctx, dx, len1, *, see
         return dw_subsampling_backward(cfg, S, P, G, pre, ctx, dx, seed=seed, salt=salt, ws=ws)
     dev = dx.device
     B, C = S.B, S.C
-    dy2 = _out_linear_backward(S, P, G, pre, ctx, dx, ctx["y2"], seed=seed, salt=salt, ws=ws)
     direct = K.get_math() == "bf16" and K.subsample_dgrad_supported(C) and ctx["cols1"] is None
+    # the direct path's conv2 gradients both read dy2 as bf16: the output Linear's backward writes it so
+    # (kdfm_ss_out_dgrad) instead of an f32 dy2 plus a cast
+    dy2h = None
+    if direct and "wout_t_bf16" in ws and B * S.T1 * S.F1 < (1 << 24):
+        dy2h = _out_linear_backward(S, P, G, pre, ctx, dx, ctx["y2"], seed=seed, salt=salt, ws=ws, bf16_out=True)
+        dy2 = None
+    else:
+        dy2 = _out_linear_backward(S, P, G, pre, ctx, dx, ctx["y2"], seed=seed, salt=salt, ws=ws)
     if direct:
         # conv2 weight gradient on the weight-gradient stream from bf16 operands: tap-major bf16
-        # columns of y1 (half the bytes of the f32 im2col) and a bf16 copy of dy2, one row-parallel
+        # columns of y1 (half the bytes of the f32 im2col) and the bf16 dy2, one row-parallel
         # launch into (C, 9, C) then re-laid out into (C, C, 3, 3)
         cols1 = torch.empty(B * S.T * S.F2, 9 * C, device=dev, dtype=torch.bfloat16)
-        dy2h = torch.empty(B * S.T * S.F2, C, device=dev, dtype=torch.bfloat16)
+        cast = dy2h is None
+        if cast:
+            dy2h = torch.empty(B * S.T * S.F2, C, device=dev, dtype=torch.bfloat16)
         gtm = ws["w2_tapmajor_grad"]
 
         def conv2_wgrad():
             K.im2col_3x3s2_tm_bf16(ctx["y1"], len1 if cfg.subsampling_mask else None, cols1, B, S.T1, S.F1, C)
-            K.cast_bf16(dy2, dy2h)
+            if cast:
+                K.cast_bf16(dy2, dy2h)
             K.fill(gtm, 0.0)
             K.wgrad_bf16(dy2h, cols1, gtm.view(C, 9 * C), db=G[pre + "pre_encode.conv.2.bias"])
             K.convw_grad(gtm.view(C, 9 * C), G[pre + "pre_encode.conv.2.weight"].view(C, C, 9))
-        WGRAD.run(conv2_wgrad, dy2, cols1, dy2h, ctx["y1"], len1)
+        WGRAD.run(conv2_wgrad, *(t for t in (dy2, cols1, dy2h, ctx["y1"], len1) if t is not None))
     else:
         if ctx["y1"] is not None and ctx["y1"].dtype == torch.bfloat16:   # fused forward kept only the bf16 y1
             ctx["y1"] = ctx["y1"].float()
@@ -317,9 +334,14 @@ def subsampling_backward(cfg, S: EncoderShapes, P, G, pre, ctx, dx, len1, *, see
         # epilogue: dy1 never reaches HBM
         wt = ws["w2_dgrad"]
         K.subsample_dgrad_wprep(P[pre + "pre_encode.conv.2.weight"].view(C, C, 3, 3), wt)
-        K.subsample_conv2_dgrad_w0(dy2, wt, ctx["y1"], B, S.T1, S.F1, C, ctx["mel"], ctx["mel_len"] if m else None,
-                                   S.Tm, cfg.nfilt, S.pad, G[pre + "pre_encode.conv.0.weight"].view(C, 9),
-                                   G[pre + "pre_encode.conv.0.bias"])
+        if dy2 is None:
+            K.subsample_conv2_dgrad_w0_h(dy2h, wt, ctx["y1"], B, S.T1, S.F1, C, ctx["mel"],
+                                         ctx["mel_len"] if m else None, S.Tm, cfg.nfilt, S.pad,
+                                         G[pre + "pre_encode.conv.0.weight"].view(C, 9), G[pre + "pre_encode.conv.0.bias"])
+        else:
+            K.subsample_conv2_dgrad_w0(dy2, wt, ctx["y1"], B, S.T1, S.F1, C, ctx["mel"], ctx["mel_len"] if m else None,
+                                       S.Tm, cfg.nfilt, S.pad, G[pre + "pre_encode.conv.0.weight"].view(C, 9),
+                                       G[pre + "pre_encode.conv.0.bias"])
         return
     dy1 = _empty(B * S.T1 * S.F1, C, dev=dev)
     if direct:
@@ -1098,6 +1120,8 @@ def make_workspace(S: EncoderShapes, dev):
         ws["w2_tapmajor"] = torch.empty(S.d, 9, S.d, device=dev)
         ws["w2_dgrad"] = torch.empty(K.subsample_dgrad_wprep_elems(S.d), device=dev, dtype=torch.bfloat16)
         ws["w2_tapmajor_grad"] = torch.empty(S.d, 9, S.d, device=dev)
+        if S.d <= 128 and (S.F2 * S.C) % 4 == 0:
+            ws["wout_t_bf16"] = torch.empty(K.ss_out_wprep_elems(S.d, S.F2 * S.C), device=dev, dtype=torch.bfloat16)
         if K.subsample_fused_supported(S.d):
             ws["ss_fused_w"] = torch.empty(K.subsample_fused_wprep_elems(S.d), device=dev, dtype=torch.bfloat16)
     return ws

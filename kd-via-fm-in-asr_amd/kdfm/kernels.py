@@ -1118,6 +1118,35 @@ def subsample_conv2_dgrad_w0(dy2, wt, y1, B, T1, F1, Cc, mel, mel_len, Tm, Fm, p
          ws.numel(), _s())
 
 
+def subsample_conv2_dgrad_w0_h(dy2h, wt, y1, B, T1, F1, Cc, mel, mel_len, Tm, Fm, pad, dw0, db0, dy1=None):
+    """subsample_conv2_dgrad_w0 over a bf16 dy2 (ss_out_dgrad's output)."""
+    assert dw0.numel() == Cc * 9 and dw0.is_contiguous() and db0.numel() == Cc
+    n = int(_lib.lib().kdfm_subsample_conv2_dgrad_w0_ws(B, T1, F1, Cc))
+    ws = scratch(dy2h.device, n)
+    call("kdfm_subsample_conv2_dgrad_w0_h", ptr(_bf16(dy2h, "dy2h")), ptr(wt), ptr(_bf16(y1, "y1 (bf16 conv1 output)")),
+         ptr(dy1), B, T1, F1, Cc, ptr(_f32(mel)), ptr(_i64(mel_len)), Tm, Fm, pad, ptr(_f32(dw0)), ptr(_f32(db0)),
+         ptr(ws), ws.numel(), _s())
+
+
+def ss_out_wprep_elems(d, ncols):
+    return int(_lib.lib().kdfm_ss_out_wprep_elems(d, ncols))
+
+
+def ss_out_wprep(W, wt):
+    """wt = bf16 W^T [ncols][32 ceil(d/32)] of the subsampling output weight W (d, ncols) (kdfm_ss_out_wprep)."""
+    d, ncols = W.shape
+    assert wt.dtype == torch.bfloat16 and wt.numel() >= int(_lib.lib().kdfm_ss_out_wprep_elems(d, ncols))
+    call("kdfm_ss_out_wprep", ptr(_f32(W.contiguous())), ptr(wt), d, ncols, _s())
+
+
+def ss_out_dgrad(dlin, wt, y2, dy2h):
+    """dy2h (rows, ncols) bf16 = [y2 > 0] * (dlin @ W) with wt from ss_out_wprep (kdfm_ss_out_dgrad)."""
+    rows, d = dlin.shape
+    ncols = y2.shape[1]
+    assert dlin.is_contiguous() and y2.shape[0] == rows and y2.is_contiguous() and dy2h.shape == (rows, ncols)
+    call("kdfm_ss_out_dgrad", ptr(_f32(dlin)), ptr(wt), ptr(_f32(y2)), ptr(_bf16(dy2h, "dy2h")), rows, d, ncols, _s())
+
+
 def subsample_dgrad_supported(Cc):
     """Channel counts the direct conv2 data-gradient kernel is instantiated for."""
     return Cc % 8 == 0 and ((-(-Cc // 32), -(-Cc // 16)) in ((3, 6), (1, 1), (1, 2), (2, 4)))

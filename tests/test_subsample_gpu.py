@@ -262,3 +262,57 @@ def test_subsample_dgrad_fused_conv0_wgrad(K, C, Tm, Fm):
     gw, gb = torch.autograd.grad(out, [w, bias], d1)
     assert _rel(dw0.cpu() - 0.5, gw.view(C, 9)) <= 1e-5
     assert _rel(db0.cpu(), gb) <= 1e-5
+
+
+@pytest.mark.parametrize("C,Tm,Fm", [(88, 801, 80), (88, 75, 27), (32, 61, 80)])
+def test_subsample_dgrad_bf16_dy2_equals_f32(K, C, Tm, Fm):
+    """kdfm_subsample_conv2_dgrad_w0_h (dy2 read as bf16) against kdfm_subsample_conv2_dgrad_w0 fed the same
+    values in f32: the f32 kernel rounds each dy2 fragment to bf16 on load, so on bf16-exact dy2 the two run
+    the same MFMAs on the same operands -- dy1, dW0 and db0 bitwise equal."""
+    g = torch.Generator().manual_seed(7 * C + Tm)
+    B = 3
+    T1, F1 = _lens(Tm), _lens(Fm)
+    T2, F2 = _lens(T1), _lens(F1)
+    mel = torch.randn(B, Tm, Fm, generator=g).cuda()
+    mel_len = torch.tensor([Tm, Tm - Tm // 3, Tm // 2], dtype=torch.int64).cuda()
+    y1 = torch.relu(torch.randn(B * T1 * F1, C, generator=g)).cuda().bfloat16()
+    dy2h = torch.randn(B * T2 * F2, C, generator=g).cuda().bfloat16()
+    w2 = torch.randn(C, C, 3, 3, generator=g) * (1.0 / (3 * C ** 0.5))
+    wt = torch.empty(K.subsample_dgrad_wprep_elems(C), device="cuda", dtype=torch.bfloat16)
+    K.subsample_dgrad_wprep(w2.cuda(), wt)
+    outs = []
+    for h in (False, True):
+        dy1 = torch.empty(B * T1 * F1, C, device="cuda")
+        dw0 = torch.full((C, 9), 0.25, device="cuda")
+        db0 = torch.zeros(C, device="cuda")
+        if h:
+            K.subsample_conv2_dgrad_w0_h(dy2h, wt, y1, B, T1, F1, C, mel, mel_len, Tm, Fm, 1, dw0, db0, dy1=dy1)
+        else:
+            K.subsample_conv2_dgrad_w0(dy2h.float(), wt, y1, B, T1, F1, C, mel, mel_len, Tm, Fm, 1, dw0, db0, dy1=dy1)
+        outs.append((dy1, dw0, db0))
+    torch.cuda.synchronize()
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("rows,d,F2,C", [(12832, 88, 20, 88), (300, 88, 20, 88), (77, 40, 5, 36), (1000, 128, 4, 64)])
+def test_ss_out_dgrad_matches_linear_dx(K, rows, d, F2, C):
+    """kdfm_ss_out_dgrad: the subsampling output Linear's data gradient with the ReLU' of the conv2 output, as
+    bf16: against the f32 product of the bf16-rounded dlin and W (what kdfm_gemm's bf16 math multiplies) with
+    the mask, rounded to bf16 -- equal but for f32 accumulation order (a bf16 rounding may flip: within one bf16
+    ulp, 2^-8 relative), masked entries exactly 0."""
+    g = torch.Generator().manual_seed(rows + d)
+    ncols = F2 * C
+    dlin = torch.randn(rows, d, generator=g)
+    W = torch.randn(d, ncols, generator=g) / d ** 0.5
+    y2 = torch.randn(rows, ncols, generator=g)
+    wt = torch.empty(K.ss_out_wprep_elems(d, ncols), device="cuda", dtype=torch.bfloat16)
+    K.ss_out_wprep(W.cuda(), wt)
+    out = torch.empty(rows, ncols, device="cuda", dtype=torch.bfloat16)
+    K.ss_out_dgrad(dlin.cuda(), wt, y2.cuda(), out)
+    torch.cuda.synchronize()
+    ref = (_bf(dlin).double() @ _bf(W).double()) * (y2 > 0).double()
+    got = out.float().double().cpu()
+    assert torch.equal(got[y2 <= 0], torch.zeros_like(got[y2 <= 0]))
+    err = (got - ref).abs()
+    assert (err <= ref.abs() * 2.0 ** -8 + 1e-6).all(), err.max().item()
