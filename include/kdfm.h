@@ -187,6 +187,18 @@ int64_t kdfm_wgrad_bf16_conv_ws(int64_t rows, int64_t M, int64_t C, int32_t taps
 int kdfm_wgrad_bf16_conv(const uint16_t* dY, const uint16_t* X, float* dW, int64_t ldc, float* db, int64_t rows,
                          int64_t M, int64_t C, int32_t taps, int32_t pad, int64_t T, float alpha, float* ws,
                          int64_t ws_len, void* stream);
+/* Deferred folds of the row-parallel weight gradients (kdfm_wgrad_bf16 / _pair / _seg / _conv / _dev), per
+ * stream: after kdfm_wgrad_set_fold_arena(stream, arena, len) the products issued on `stream` write their
+ * per-split partials into `arena` (len floats, caller-owned, 16-byte aligned; ws is then unused) and queue
+ * their ordered fold instead of launching it; kdfm_wgrad_fold_flush(stream) folds every queued product in one
+ * launch (up to 24 per launch), each exactly as its own fold would (bitwise equal gradients), and frees the
+ * arena for the stream's next products (stream order).  dW / db are final only after the flush.  A product
+ * whose partials do not fit the arena's remaining space folds at once as usual; queued products adding into
+ * overlapping gradient memory fold in queue order (separate launches).  arena = NULL ends deferral
+ * (the queue must be empty).  kdfm_wgrad_fold_pending: queued folds of the stream. */
+int kdfm_wgrad_set_fold_arena(void* stream, float* arena, int64_t len);
+int kdfm_wgrad_fold_flush(void* stream);
+int64_t kdfm_wgrad_fold_pending(void* stream);
 
 /* Fused FlowMatchingModule chain (asr_train_diffm.py:1368-1427, rectified, meta_encoder 'mlp',
  * shape_transform 'linear'; bf16 MFMA, f32 state; latent width L == 96).  Rows n:

@@ -21,6 +21,9 @@
 #include "gemm_common.h"
 
 #include <cstdlib>
+#include <mutex>
+#include <unordered_map>
+#include <vector>
 
 // timing probe points (tools/wgrad_probe.hip defines KPROBE; empty in the library)
 #ifndef KPROBE
@@ -436,16 +439,14 @@ __global__ __launch_bounds__(64 * WF_WAVES) void wgr_fold_kernel(GemmP p, int64_
 
 // The same fold with 4 consecutive output elements per lane (16-byte partial loads; M*N % 4 == 0): a block
 // owns 256 elements, so the launch has a quarter of the blocks and every load instruction moves 4x the
-// bytes -- the fold is load-issue bound (r4k: 162 launches per step at 7.3 us each).
-template <bool TRANS = false>
-__global__ __launch_bounds__(64 * WF_WAVES) void wgr_fold4_kernel(GemmP p, int64_t S) {
-  __shared__ float4 red4[WF_WAVES][64];
+// bytes -- the fold is load-issue bound (r4k: 162 launches per step at 7.3 us each).  One block's work as a
+// device function: the per-product kernel below and the batched fold (wgr_fold_batch_kernel) both run it.
+__device__ __forceinline__ void fold4_block(const float* __restrict__ ws_base, float* Cout, float* ones, int64_t M,
+                                            int64_t N, int64_t sCm, int64_t sCn, int64_t ones_col, float alpha,
+                                            int64_t S, bool trans, int64_t blk, float4 (*red4)[64]) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int64_t MN = p.M * p.N;
-  const int64_t e0 = ((int64_t)blockIdx.x * 64 + lane) * 4;
-  const bool second = blockIdx.y == 1;   // paired launch: the second product
-  float* Cout = second ? p.C2 : p.C;
-  float* ones = second ? p.ones_out2 : p.ones_out;
+  const int64_t MN = M * N;
+  const int64_t e0 = (blk * 64 + lane) * 4;
   // wave 0 fetches the 4 destination values before the partials, so their round trip overlaps the
   // partials' (the destination is read and written by this block only)
   float* dst[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -455,14 +456,14 @@ __global__ __launch_bounds__(64 * WF_WAVES) void wgr_fold4_kernel(GemmP p, int64
     for (int q = 0; q < 4; ++q) {
       const int64_t e = e0 + q;
       int64_t m, n;
-      if (TRANS) {
-        n = e / p.M;
-        m = e - n * p.M;
+      if (trans) {
+        n = e / M;
+        m = e - n * M;
       } else {
-        m = e / p.N;
-        n = e - m * p.N;
+        m = e / N;
+        n = e - m * N;
       }
-      dst[q] = (p.ones_col >= 0 && n >= p.ones_col) ? ones + (n - p.ones_col) * p.M + m : Cout + m * p.sCm + n * p.sCn;
+      dst[q] = (ones_col >= 0 && n >= ones_col) ? ones + (n - ones_col) * M + m : Cout + m * sCm + n * sCn;
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) cur[q] = *dst[q];
@@ -476,7 +477,7 @@ __global__ __launch_bounds__(64 * WF_WAVES) void wgr_fold4_kernel(GemmP p, int64
   // are in flight per lane before the first add (one memory round trip per 16 splits, not per 4).
   const int64_t nw = (e0 < MN && S > w) ? (S - w + WF_WAVES - 1) / WF_WAVES : 0;
   const int64_t g4 = nw / 4 * 4;
-  const float4* base = reinterpret_cast<const float4*>((second ? p.ws2 : p.ws) + e0);
+  const float4* base = reinterpret_cast<const float4*>(ws_base + e0);
   const int64_t st = MN / 4;   // float4 stride between splits
   for (int64_t i0 = 0; i0 < nw; i0 += 16) {
     float4 v[16];
@@ -497,10 +498,44 @@ __global__ __launch_bounds__(64 * WF_WAVES) void wgr_fold4_kernel(GemmP p, int64
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
     for (int i = 0; i < WF_WAVES; ++i) add(v, red4[i][lane]);
-    const float vv[4] = {v.x * p.alpha, v.y * p.alpha, v.z * p.alpha, v.w * p.alpha};
+    const float vv[4] = {v.x * alpha, v.y * alpha, v.z * alpha, v.w * alpha};
 #pragma unroll
     for (int q = 0; q < 4; ++q) *dst[q] = cur[q] + vv[q];
   }
+}
+
+template <bool TRANS = false>
+__global__ __launch_bounds__(64 * WF_WAVES) void wgr_fold4_kernel(GemmP p, int64_t S) {
+  __shared__ float4 red4[WF_WAVES][64];
+  const bool second = blockIdx.y == 1;   // paired launch: the second product
+  fold4_block(second ? p.ws2 : p.ws, second ? p.C2 : p.C, second ? p.ones_out2 : p.ones_out, p.M, p.N, p.sCm, p.sCn,
+              p.ones_col, p.alpha, S, TRANS, blockIdx.x, red4);
+}
+
+// Deferred folds (kdfm_wgrad_set_fold_arena / kdfm_wgrad_fold_flush): the row-parallel products of a stream
+// write their partials into a caller-owned arena and queue a fold job each; one launch then folds every
+// queued product (block ranges per job), each job exactly as its own wgr_fold4_kernel launch would (the
+// same fold4_block: bitwise equal results).  A Conformer layer's 8 weight gradients fold in one launch
+// instead of 6 (114 fold launches per step, 8-11 us each, mostly ramp and tail).
+constexpr int FB_MAXJ = 24;
+struct FoldJob {
+  const float* ws; float* C; float* ones;
+  int64_t M, N, sCm, sCn, ones_col, S;
+  float alpha; int trans;
+};
+struct FoldBatch {
+  FoldJob j[FB_MAXJ];
+  int64_t blk0[FB_MAXJ + 1];   // first block of each job; blk0[n] = grid
+  int n;
+};
+
+__global__ __launch_bounds__(64 * WF_WAVES) void wgr_fold_batch_kernel(FoldBatch fb) {
+  __shared__ float4 red4[WF_WAVES][64];
+  const int64_t b = blockIdx.x;
+  int j = 0;
+  while (j + 1 < fb.n && b >= fb.blk0[j + 1]) ++j;   // block-uniform
+  const FoldJob& J = fb.j[j];
+  fold4_block(J.ws, J.C, J.ones, J.M, J.N, J.sCm, J.sCn, J.ones_col, J.alpha, J.S, J.trans != 0, b - fb.blk0[j], red4);
 }
 
 // fold launch: the 4-wide kernel when the partial layout allows it (KDFM_WGR_FOLD4=0: the scalar one)
@@ -1095,11 +1130,59 @@ void conv_geometry(GemmP& p, int64_t C, int taps, int pad, int64_t T) {
   p.conv_t = T;
 }
 
+// ---- deferred folds: per-stream arena and job queue (host side) ----
+struct DeferState {
+  float* arena = nullptr;
+  int64_t len = 0, used = 0;
+  std::vector<FoldJob> jobs;
+};
+std::mutex g_defer_mu;
+std::unordered_map<void*, DeferState>& defer_map() {
+  static std::unordered_map<void*, DeferState> m;
+  return m;
+}
+
+// n floats of the stream's fold arena (16-byte aligned), or null when the stream does not defer / it is full
+float* defer_reserve(hipStream_t st, int64_t n) {
+  std::lock_guard<std::mutex> g(g_defer_mu);
+  auto it = defer_map().find((void*)st);
+  if (it == defer_map().end() || !it->second.arena) return nullptr;
+  DeferState& d = it->second;
+  const int64_t need = (n + 3) / 4 * 4;
+  if (d.used + need > d.len) return nullptr;
+  float* r = d.arena + d.used;
+  d.used += need;
+  return r;
+}
+
+void defer_push(hipStream_t st, const GemmP& p, const float* ws, float* C, float* ones, int64_t S, bool trans) {
+  FoldJob j;
+  j.ws = ws; j.C = C; j.ones = ones;
+  j.M = p.M; j.N = p.N; j.sCm = p.sCm; j.sCn = p.sCn; j.ones_col = p.ones_col; j.S = S;
+  j.alpha = p.alpha; j.trans = trans ? 1 : 0;
+  std::lock_guard<std::mutex> g(g_defer_mu);
+  defer_map()[(void*)st].jobs.push_back(j);
+}
+
+// the 4-wide fold applies (and the product keeps per-split partials)
+bool defer_ok(const GemmP& p, const WrPlan& pl) { return (p.M * p.N) % 4 == 0 && !wr_use_xslots(pl); }
+
 int wgrad_bf16_run(const GemmP& p, int bmode, hipStream_t st) {
   WrPlan pl;
   KDFM_REQUIRE(wr_plan(p, KDFM_LD_XC, bmode, 1, pl, true, true), "shape not supported by the row-parallel kernel");
   KDFM_REQUIRE(p.ws_len >= pl.S * p.M * p.N, "workspace too small (kdfm_wgrad_bf16*_ws)");
   set_route(ROUTE_WGRAD_ROWS);
+  // deferred fold: the partials go to the stream's arena and the fold joins the next kdfm_wgrad_fold_flush
+  float* dws = defer_ok(p, pl) ? defer_reserve(st, pl.S * p.M * p.N) : nullptr;
+  if (dws) {
+    GemmP q = p;
+    q.ws = dws;
+    const int rc = pl.dma ? wd_dispatch(q, pl, st)
+                          : (pl.bin == 2 ? wr_dispatch<2>(q, pl, bmode, st) : wr_dispatch<1>(q, pl, bmode, st));
+    if (rc) return rc;
+    defer_push(st, q, dws, q.C, q.ones_out, pl.S, pl.dma);
+    return KDFM_OK;
+  }
   if (pl.dma) {
     const int rc = wd_dispatch(p, pl, st);
     if (rc) return rc;
@@ -1168,8 +1251,19 @@ int kdfm_wgrad_bf16_pair(const uint16_t* dY, const uint16_t* X, float* dW, float
   p.ones_out2 = db2;
   p.ws2 = ws + one;
   set_route(ROUTE_WGRAD_ROWS);
+  const int64_t oner = (one + 3) / 4 * 4;
+  float* dws = defer_ok(p, pl) ? defer_reserve(st, 2 * oner) : nullptr;
+  if (dws) {   // deferred folds (both products' partials in the stream's arena)
+    p.ws = dws;
+    p.ws2 = dws + oner;
+  }
   const int rc = pl.bin == 2 ? wr_dispatch<2>(p, pl, KDFM_LD_XC, st) : wr_dispatch<1>(p, pl, KDFM_LD_XC, st);
   if (rc) return rc;
+  if (dws) {
+    defer_push(st, p, p.ws, p.C, p.ones_out, pl.S, false);
+    defer_push(st, p, p.ws2, p.C2, p.ones_out2, pl.S, false);
+    return KDFM_OK;
+  }
   return wr_fold(p, pl.S, st);
 }
 
@@ -1244,6 +1338,84 @@ int kdfm_wgrad_bf16_conv(const uint16_t* dY, const uint16_t* X, float* dW, int64
   GemmP p = wgrad_bf16_params(dY, X, dW, ldc, db, rows, M, taps * C, alpha, ws, ws_len);
   conv_geometry(p, C, taps, pad, T);
   return wgrad_bf16_run(p, KDFM_LD_CONV, as_stream(stream));
+}
+
+int kdfm_wgrad_set_fold_arena(void* stream, float* arena, int64_t len) {
+  using namespace kdfm;
+  KDFM_REQUIRE(!arena || (len > 0 && ((uintptr_t)arena & 15) == 0), "arena must be 16-byte aligned with len > 0");
+  std::lock_guard<std::mutex> g(g_defer_mu);
+  DeferState& d = defer_map()[stream];
+  KDFM_REQUIRE(d.jobs.empty(), "folds still queued on this stream: kdfm_wgrad_fold_flush first");
+  d.arena = arena;
+  d.len = arena ? len : 0;
+  d.used = 0;
+  return KDFM_OK;
+}
+
+int kdfm_wgrad_fold_flush(void* stream) {
+  using namespace kdfm;
+  std::vector<FoldJob> jobs;
+  {
+    std::lock_guard<std::mutex> g(g_defer_mu);
+    auto it = defer_map().find(stream);
+    if (it == defer_map().end()) return KDFM_OK;
+    jobs.swap(it->second.jobs);
+    it->second.used = 0;   // the stream's next products reuse the arena after these folds (stream order)
+  }
+  hipStream_t st = as_stream(stream);
+  // the byte ranges a job's fold writes (its gradient block, its bias row(s)): jobs in one launch run
+  // concurrently, so a job adding into memory an earlier queued job also adds into (two products into one
+  // gradient: the heads' layer halves, per-step products) starts a new launch -- stream order keeps the
+  // queue's order for them
+  auto ranges = [](const FoldJob& j, uintptr_t (&r)[2][2]) {
+    const int64_t nmem = j.ones_col >= 0 ? j.ones_col : j.N;
+    r[0][0] = (uintptr_t)j.C;
+    r[0][1] = (uintptr_t)(j.C + (j.M - 1) * j.sCm + (nmem - 1) * j.sCn) + sizeof(float);
+    r[1][0] = r[1][1] = 0;
+    if (j.ones_col >= 0 && j.ones) {
+      r[1][0] = (uintptr_t)j.ones;
+      r[1][1] = (uintptr_t)(j.ones + (j.N - j.ones_col) * j.M);
+    }
+  };
+  auto overlap = [](const uintptr_t (&a)[2][2], const uintptr_t (&b)[2][2]) {
+    for (int x = 0; x < 2; ++x)
+      for (int y = 0; y < 2; ++y)
+        if (a[x][1] > a[x][0] && b[y][1] > b[y][0] && a[x][0] < b[y][1] && b[y][0] < a[x][1]) return true;
+    return false;
+  };
+  FoldBatch fb{};
+  uintptr_t rg[FB_MAXJ][2][2];
+  auto launch = [&]() -> int {
+    if (fb.n == 0) return KDFM_OK;
+    hipLaunchKernelGGL(wgr_fold_batch_kernel, dim3((unsigned)fb.blk0[fb.n]), dim3(64 * WF_WAVES), 0, st, fb);
+    fb.n = 0;
+    fb.blk0[0] = 0;
+    return check_launch("kdfm_wgrad_fold_flush");
+  };
+  fb.blk0[0] = 0;
+  for (const FoldJob& job : jobs) {
+    uintptr_t r[2][2];
+    ranges(job, r);
+    bool clash = fb.n == FB_MAXJ;
+    for (int k = 0; k < fb.n && !clash; ++k) clash = overlap(r, rg[k]);
+    if (clash) {
+      const int rc = launch();
+      if (rc) return rc;
+    }
+    fb.j[fb.n] = job;
+    for (int x = 0; x < 2; ++x)
+      for (int y = 0; y < 2; ++y) rg[fb.n][x][y] = r[x][y];
+    fb.blk0[fb.n + 1] = fb.blk0[fb.n] + ceil_div(job.M * job.N, 256);
+    ++fb.n;
+  }
+  return launch();
+}
+
+int64_t kdfm_wgrad_fold_pending(void* stream) {
+  using namespace kdfm;
+  std::lock_guard<std::mutex> g(g_defer_mu);
+  auto it = defer_map().find(stream);
+  return it == defer_map().end() ? 0 : (int64_t)it->second.jobs.size();
 }
 
 }  // extern "C"

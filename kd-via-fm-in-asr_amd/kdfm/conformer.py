@@ -45,6 +45,11 @@ _ATTN_FWD3 = __import__("os").environ.get("KDFM_ATTN_FWD3", "1") == "1"
 # ... and the bwd2 dQ kernel over the same prepared operands, kept from the forward (KDFM_ATTN_DQ3=0: it stages
 # K / V / the band from qkv / pos itself)
 _ATTN_DQ3 = __import__("os").environ.get("KDFM_ATTN_DQ3", "1") == "1"
+# bf16 math: the encoder backward defers its layers' weight-gradient folds and folds each layer's products in one
+# launch (kdfm_wgrad_set_fold_arena / kdfm_wgrad_fold_flush; bitwise the per-product folds).  KDFM_FOLD_DEFER=0:
+# a fold launch per product (pair)
+_FOLD_DEFER = __import__("os").environ.get("KDFM_FOLD_DEFER", "1") == "1"
+_FOLD_ARENA_FLOATS = 64 << 20   # 256 MB: a layer's per-split partials at the bench shape are ~18M floats, the heads' ~40M
 
 
 def _attn_fused_ok(dk, save):
@@ -311,6 +316,7 @@ def subsampling_backward(cfg, S: EncoderShapes, P, G, pre, ctx, dx, len1, *, see
                 K.cast_bf16(dy2, dy2h)
             K.fill(gtm, 0.0)
             K.wgrad_bf16(dy2h, cols1, gtm.view(C, 9 * C), db=G[pre + "pre_encode.conv.2.bias"])
+            K.wgrad_fold_flush()   # gtm is read below (deferred folds, fold_arena)
             K.convw_grad(gtm.view(C, 9 * C), G[pre + "pre_encode.conv.2.weight"].view(C, C, 9))
         WGRAD.run(conv2_wgrad, *(t for t in (dy2, cols1, dy2h, ctx["y1"], len1) if t is not None))
     else:
@@ -1047,13 +1053,25 @@ def encoder_forward(cfg, S: EncoderShapes, P, prefix, mel, mel_len, len1, len2, 
     return run
 
 
+def fold_arena(ws, dev):
+    """The deferred weight-gradient folds' partial arena of an encoder workspace (bf16 math, KDFM_FOLD_DEFER)."""
+    if not _FOLD_DEFER or K.get_math() != "bf16":
+        return None
+    arena = ws.get("fold_arena")
+    if arena is None:
+        arena = ws["fold_arena"] = torch.empty(_FOLD_ARENA_FLOATS, device=dev)
+    return arena
+
+
 def encoder_backward(cfg, S: EncoderShapes, P, G, prefix, run: EncoderRun, dfeats, pos_emb, len1, len2, *, seed,
-                     salt, ws, on_layer_done=None, before_read=None):
+                     salt, ws, on_layer_done=None, before_read=None, arena_set=False):
     """dfeats (n_layers, rows, d): grads wrt every hooked layer output (heads + decoder), summed into
     the residual chain as the backward walks down the stack.  on_layer_done(i) is called once layer
     i's parameter gradients are all issued (bucketed all-reduce overlap, kdfm/ddp.py);
     before_read {j: fn}: fn() runs right before dfeats[j] is first read (a stream join for heads
-    gradients produced on another stream)."""
+    gradients produced on another stream).  Weight-gradient folds are deferred (fold_arena) and flushed once per
+    layer, before on_layer_done; arena_set: the caller already set the arena on the weight-gradient stream (its
+    own queued folds are flushed with the first layer's)."""
     dout, dout2 = dfeats[cfg.n_layers - 1], None
     n = cfg.n_layers
     ring = None
@@ -1061,6 +1079,9 @@ def encoder_backward(cfg, S: EncoderShapes, P, G, prefix, run: EncoderRun, dfeat
         ring = ws.get("bn_red_ring")
         if ring is None:
             ring = ws["bn_red_ring"] = torch.zeros(n, 2 * S.d, device=dfeats.device, dtype=torch.float64)
+    arena = fold_arena(ws, dfeats.device)
+    if arena is not None and not arena_set:
+        WGRAD.run(lambda: K.wgrad_set_fold_arena(arena), arena)
     for i in range(cfg.n_layers - 1, -1, -1):
         L = f"{prefix}layers.{i}."
         k = n - 1 - i
@@ -1072,6 +1093,8 @@ def encoder_backward(cfg, S: EncoderShapes, P, G, prefix, run: EncoderRun, dfeat
                             ln_buf=torch.empty(6, K.layernorm_bwd_ws(S.rows, S.d), device=dfeats.device),
                             dout2=dout2, bn_red=bn_red)
         run.layers[i] = None
+        if arena is not None:   # the layer's weight gradients are final after this (before its all-reduce)
+            WGRAD.run(K.wgrad_fold_flush)
         if on_layer_done is not None:
             on_layer_done(i)
         if i > 0:
@@ -1080,6 +1103,11 @@ def encoder_backward(cfg, S: EncoderShapes, P, G, prefix, run: EncoderRun, dfeat
             dout, dout2 = dfeats[i - 1], dx
     subsampling_backward(cfg, S, P, G, prefix, run.sub, dx, len1, seed=seed, salt=salt, ws=ws)
     run.sub = None
+    if arena is not None:
+        def _end():
+            K.wgrad_fold_flush()
+            K.wgrad_set_fold_arena(None)
+        WGRAD.run(_end)
     WGRAD.join()  # weight gradients computed on the side stream are complete before anyone reads G
 
 

@@ -190,6 +190,7 @@ def encfm_backward(cfg, P, G, ws: EncFMWorkspace, dfeats, gxS, wgrad_run, *, see
             K.linear_dw(ws.dhcat[:, H:2 * H], ws.tv, G[r + "tch_proj.0.weight"], db=G[r + "tch_proj.0.bias"],
                         math="f32")
         gemb = G[r + "layer_emb.weight"] if cfg.encfm_dynamic else ws.dsv   # ws.dsv: an unused sink when fixed
+        K.wgrad_fold_flush()   # gW1 is read below: a deferred fold of the products above completes first
         K.call("kdfm_encfm_time_bwd", K.ptr(gW1), gW1.stride(0), K.ptr(G[fm + "meta_encoder.0.bias"]), K.ptr(W1),
                K.ptr(P[fm + "time_embed.weight"]), K.ptr(P[fm + "time_embed.bias"]), K.ptr(G[fm + "time_embed.weight"]),
                K.ptr(G[fm + "time_embed.bias"]), K.ptr(ws.dhcat), K.ptr(gemb), L if cfg.encfm_dynamic else 0, B, Cs,

@@ -16,7 +16,7 @@ from . import _lib
 from . import kernels as K
 from .config import (Ver5Config, all_head_specs, bn_buffer_specs, diffkd_specs, meta_bn_specs, student_specs,
                      teacher_specs)
-from .conformer import EncoderRun, EncoderShapes, compute_lengths, encoder_backward, encoder_forward, \
+from .conformer import EncoderRun, EncoderShapes, compute_lengths, encoder_backward, encoder_forward, fold_arena, \
     encoder_forward_steps, layer_images, make_workspace
 from .frontend import FrontendConsts, frontend_forward, mel_frames, specaugment_
 from .encfm import EncFMWorkspace, encfm_backward, encfm_forward
@@ -496,6 +496,18 @@ class Ver5Engine:
         n = cfg.n_layers * Ss.rows
         self.student.zero_grad()
         dfeats = torch.empty(cfg.n_layers, Ss.rows, Ss.d, device=self.device)
+        # the heads' / decoder's weight-gradient folds join the encoder's deferred ones (conformer.fold_arena): one
+        # batched fold launch before each gradient-ready point
+        arena = fold_arena(self._enc_ws(Ss, "encoder."), self.device)
+        if arena is not None:
+            WGRAD.run(lambda: K.wgrad_set_fold_arena(arena), arena)
+            _ready = grad_ready
+
+            def grad_ready_flushed(offset):
+                WGRAD.run(K.wgrad_fold_flush)
+                if _ready is not None:
+                    _ready(offset)
+            grad_ready = grad_ready_flushed if grad_ready is not None else None
         dec0 = off["decoder.decoder_layers.0.weight"]
         g = ctx.pop("glogits")
         Cn = cfg.classes
@@ -555,7 +567,7 @@ class Ver5Engine:
                              ctx["len2"], seed=self.seed, salt=SALT_STUDENT, ws=self._enc_ws(Ss, "encoder."),
                              on_layer_done=layer_done,
                              before_read=None if join is None else {join[0]: lambda: torch.cuda.current_stream(
-                                 self.device).wait_stream(join[1])})
+                                 self.device).wait_stream(join[1])}, arena_set=arena is not None)
 
     def _decoder_dw(self, g, x):
         """The decoder's weight / bias gradient from the logits gradient g and its input x, on the

@@ -178,9 +178,13 @@ def _fm_backward(cfg, P, G, ws, c, gxs, dev):
         else:
             for j in range(S_):
                 WGRAD.run(lambda j=j: K.wgrad_bf16(DA[j], X[j], dW1x, db=dc[j]), DA, X)
-        # dc is produced on the side stream: fold it there too (no main-stream join)
-        WGRAD.run(lambda: K.fm_time_bwd(dc, evec, W1, dW1, G[pre + "meta_encoder.0.bias"],
-                                        G[pre + "time_embed.weight"].view(-1), G[pre + "time_embed.bias"], Lt, E, S_))
+        # dc is produced on the side stream: fold it there too (no main-stream join); a deferred fold of the
+        # products writing it completes first
+        def time_bwd():
+            K.wgrad_fold_flush()
+            K.fm_time_bwd(dc, evec, W1, dW1, G[pre + "meta_encoder.0.bias"], G[pre + "time_embed.weight"].view(-1),
+                          G[pre + "time_embed.bias"], Lt, E, S_)
+        WGRAD.run(time_bwd)
         return g
     fx, fa = c["fx"], c["fa"]
     dnsx = _empty(n, Lt, dev=dev)
@@ -289,6 +293,7 @@ def _denoise_backward(P, G, dn: _Deno, c, g, T, dev):
         K.fill(dn.g2, 0.0)
         K.wgrad_bf16_conv(DA.view(ds * n, Lt), X.view(ds * n, Lt), dn.g1, T, db=G[dn.b1])
         K.wgrad_bf16_conv(GV.view(ds * n, Lt), A.view(ds * n, Lt), dn.g2, T, alpha=-1.0 / ds, db=G[dn.b2])
+        K.wgrad_fold_flush()   # g1 / g2 are read below (deferred folds, conformer.fold_arena)
         K.convw_grad(dn.g1, G[dn.w1])
         K.convw_grad(dn.g2, G[dn.w2])
     WGRAD.run(wgrads, X, A, GV, DA)

@@ -683,6 +683,22 @@ def wgrad_bf16(dY, X, dW, *, db=None, alpha=1.0):
             ptr(_bf16(X)), ptr(_f32(dW)), dW.stride(0), ptr(db), rows, M, N, float(alpha), ptr(ws), ws.numel(), _s())
 
 
+def wgrad_set_fold_arena(arena):
+    """Defer the ordered folds of the row-parallel weight gradients issued on the current stream: their
+    partials go to `arena` (f32, None ends deferral) and wgrad_fold_flush() folds them in one launch."""
+    assert arena is None or (arena.dtype == torch.float32 and arena.is_contiguous())
+    call("kdfm_wgrad_set_fold_arena", _s(), ptr(arena), 0 if arena is None else arena.numel())
+
+
+def wgrad_fold_flush():
+    """Fold every weight gradient queued on the current stream (one launch per 24 products)."""
+    call("kdfm_wgrad_fold_flush", _s())
+
+
+def wgrad_fold_pending() -> int:
+    return int(_lib.lib().kdfm_wgrad_fold_pending(_s()))
+
+
 def wgrad_bf16_pair(dY, X, dW, db, dY2, X2, dW2, db2, *, alpha=1.0):
     """Two same-shape weight gradients in one launch (kdfm_wgrad_bf16_pair): each equal bit for bit to its
     own wgrad_bf16; db / db2 both given or both None; dW and dW2 share the row stride."""

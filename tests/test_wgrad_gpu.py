@@ -240,3 +240,88 @@ def test_wgrad_bf16_pair_bitwise(R, M, N, bias):
     torch.cuda.synchronize()
     assert torch.equal(single, pair)
     assert torch.equal(sb, pb)
+
+
+def test_deferred_folds_bitwise():
+    """kdfm_wgrad_set_fold_arena / kdfm_wgrad_fold_flush: a Conformer layer's worth of products (singles, a pair,
+    a segmented product, the LDS-DMA route, a conv-mode product) with their folds queued and run in one batched
+    launch equal the immediate folds bit for bit; gradients are untouched until the flush; a product whose
+    partials overflow the arena folds at once; more than 24 queued products take several launches."""
+    from kdfm import kernels as K
+    g = torch.Generator(device="cuda").manual_seed(11)
+    mk = lambda *s: torch.randn(*s, device="cuda", generator=g).to(torch.bfloat16)  # noqa: E731
+    R = 12832
+    prods = [(mk(R, 352), mk(R, 88), True), (mk(R, 88), mk(R, 352), True), (mk(R, 264), mk(R, 88), True),
+             (mk(R, 88), mk(R, 88), False)]
+    pa = (mk(R, 88), mk(R, 88), mk(R, 88), mk(R, 88))
+    seg = (mk(4 * 2048, 96), mk(4 * 2048, 96))
+    dma = (mk(205312, 96), mk(205312, 96))
+    conv = (mk(9 * 401, 96), mk(9 * 401, 96))
+
+    def run(outs):
+        i = 0
+        for dy, x, bias in prods:
+            K.wgrad_bf16(dy, x, outs[i][0], db=outs[i][1] if bias else None, alpha=0.5)
+            i += 1
+        K.wgrad_bf16_pair(pa[0], pa[1], outs[i][0], outs[i][1], pa[2], pa[3], outs[i + 1][0], outs[i + 1][1])
+        i += 2
+        K.wgrad_bf16_seg(seg[0], seg[1], outs[i][0], outs[i][1], 2048)
+        i += 1
+        K.wgrad_bf16(dma[0], dma[1], outs[i][0], db=outs[i][1])
+        i += 1
+        K.wgrad_bf16_conv(conv[0], conv[1], outs[i][0], 401, db=outs[i][1])
+
+    def fresh():
+        gg = torch.Generator(device="cuda").manual_seed(5)
+        shapes = [(352, 88), (88, 352), (264, 88), (88, 88), (88, 88), (88, 88), (96, 96), (96, 96), (96, 288)]
+        outs = [(torch.randn(m, n, device="cuda", generator=gg), torch.randn(m, device="cuda", generator=gg))
+                for m, n in shapes]
+        outs[6] = (outs[6][0], torch.randn(4, 96, device="cuda", generator=gg))   # seg: one bias row per segment
+        return outs
+
+    ref = fresh()
+    run(ref)
+    got = fresh()
+    before = [(a.clone(), b.clone()) for a, b in got]
+    arena = torch.empty(40 << 20, device="cuda")
+    K.wgrad_set_fold_arena(arena)
+    run(got)
+    assert K.wgrad_fold_pending() == 9
+    torch.cuda.synchronize()
+    for (a, b), (a0, b0) in zip(got, before):   # nothing folded yet
+        assert torch.equal(a, a0) and torch.equal(b, b0)
+    K.wgrad_fold_flush()
+    assert K.wgrad_fold_pending() == 0
+    torch.cuda.synchronize()
+    for (a, b), (ra, rb) in zip(got, ref):
+        assert torch.equal(a, ra) and torch.equal(b, rb)
+    # more than one batch launch, and an arena too small for one product: that one folds at once
+    got2 = [fresh() for _ in range(3)]
+    for o in got2:
+        run(o)
+    K.wgrad_fold_flush()
+    K.wgrad_set_fold_arena(None)
+    small = torch.empty(1 << 20, device="cuda")
+    K.wgrad_set_fold_arena(small)
+    got3 = fresh()
+    run(got3)
+    assert 0 < K.wgrad_fold_pending() < 9
+    K.wgrad_fold_flush()
+    K.wgrad_set_fold_arena(None)
+    torch.cuda.synchronize()
+    for o in got2 + [got3]:
+        for (a, b), (ra, rb) in zip(o, ref):
+            assert torch.equal(a, ra) and torch.equal(b, rb)
+    # two queued products adding into the same gradient (the heads' layer halves) fold in queue order
+    dWi = torch.randn(88, 88, device="cuda", generator=g)
+    dbi = torch.randn(88, device="cuda", generator=g)
+    dWd, dbd = dWi.clone(), dbi.clone()
+    for k in range(3):
+        K.wgrad_bf16(prods[3][0], pa[k], dWi, db=dbi, alpha=0.25 * (k + 1))
+    K.wgrad_set_fold_arena(arena)
+    for k in range(3):
+        K.wgrad_bf16(prods[3][0], pa[k], dWd, db=dbd, alpha=0.25 * (k + 1))
+    K.wgrad_fold_flush()
+    K.wgrad_set_fold_arena(None)
+    torch.cuda.synchronize()
+    assert torch.equal(dWi, dWd) and torch.equal(dbi, dbd)

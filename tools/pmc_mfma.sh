@@ -12,10 +12,10 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 timeout -s KILL 240 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES SQ_WAVE_CYCLES SQ_WAVES \
   --kernel-trace --output-format csv -d "$OUT/p1" -o run \
-  -- python3 -u bench.py --steps 2 --warmup 1 --no-cpu-baseline > "$OUT/p1.log" 2>&1 &&
+  -- python3 -u bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-f32-sensitivity > "$OUT/p1.log" 2>&1 &&
 echo "pass 1 ok" &&
 timeout -s KILL 240 rocprofv3 --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS \
   --kernel-trace --output-format csv -d "$OUT/p2" -o run \
-  -- python3 -u bench.py --steps 2 --warmup 1 --no-cpu-baseline > "$OUT/p2.log" 2>&1 &&
+  -- python3 -u bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-f32-sensitivity > "$OUT/p2.log" 2>&1 &&
 echo "pass 2 ok" &&
-python3 tools/pmc_mfma.py "$OUT" > "$OUT/mfma.txt" && head -40 "$OUT/mfma.txt"
+python3 tools/pmc_mfma.py "$OUT" > "$OUT/mfma.txt" && rm -rf "$OUT/p1" "$OUT/p2" && head -40 "$OUT/mfma.txt"
