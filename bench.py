@@ -40,10 +40,11 @@ PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r04_pmc_traffic.json")
 ROUTE_KERNELS = {"generic": ("gemm_kernel",), "skinny": ("sk_fwd_kernel", "skd_fwd_kernel"),
                  "rowstream_fwd": ("rs_fwd_kernel",), "wide_wgrad": ("rs_wgrad_kernel", "rs_fold_kernel"),
                  "split_fold": ("gemm_kernel", "rs_fold_kernel"), "slab_conv": ("skc_fwd_kernel",),
-                 "wgrad_rows": ("wgr_kernel", "wgd_kernel", "wgr_fold_kernel")}
+                 "wgrad_rows": ("wgr_kernel", "wgd_kernel", "wgr_fold_kernel", "wgr_fold4_kernel", "wgr_fold_batch_kernel")}
 # the fused kernels traced outside kdfm_gemm (kernels._traced tags) -> kernel-name stems
 FAMILY_KERNELS = {"ffn_fwd": ("ffn_fwd_kernel",), "ffn_bwd": ("ffn_bwd_kernel",),
-                  "wgrad_bf16": ("wgr_kernel", "wgd_kernel", "wgr_fold_kernel"),
+                  "wgrad_bf16": ("wgr_kernel", "wgd_kernel", "wgr_fold_kernel", "wgr_fold4_kernel",
+                                 "wgr_fold_batch_kernel"),
                   "attn_fwd": ("relpos_attn_fwd_kernel", "relpos_attn_fwd3_kernel"),
                   "attn_prep": ("attn_kv_prep_kernel", "attn_band_prep_kernel"),
                   "attn_bwd": ("attn_bwd_dq_kernel", "attn_bwd_dkv_kernel", "attn_bwd_dpos_kernel",
@@ -369,7 +370,8 @@ def main():
     # live per-kernel timing: one instrumented eager step right after the timed steps; every
     # kdfm_gemm launch (keyed by the kernel family libkdfm routed it to), the frontend and the
     # depthwise convs bracketed by HIP events on the stream they run on
-    trace = K.Trace(["*", "frontend", "dwconv", "ffn_fwd", "ffn_bwd", "wgrad_bf16", "attn_fwd", "attn_prep", "attn_bwd"])
+    trace = K.Trace(["*", "frontend", "dwconv", "ffn_fwd", "ffn_bwd", "wgrad_bf16", "wgrad_fold", "attn_fwd", "attn_prep",
+                     "attn_bwd"])
     with trace:
         eng.train_step(wav, wl, tg, tl, ar)
     torch.cuda.synchronize()
@@ -397,6 +399,11 @@ def main():
             w = dict(routes.get("wgrad_rows", empty))
             for k in ("launches", "ms_total", "flops_total", "bytes_total"):
                 w[k] = w.get(k, 0) + tsum["wgrad_bf16"][k]
+            # deferred folds (kdfm_wgrad_fold_flush: one batched launch per encoder layer) run outside the
+            # products' traced calls: their time joins the family, not their launch count (a call stays one
+            # product + its fold)
+            if "wgrad_fold" in tsum:
+                w["ms_total"] += tsum["wgrad_fold"]["ms_total"]
             routes["wgrad_rows"] = w
         for fam in ("ffn_fwd", "ffn_bwd", "attn_fwd", "attn_prep", "attn_bwd"):
             if fam in tsum:

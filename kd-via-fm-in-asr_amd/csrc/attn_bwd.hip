@@ -87,6 +87,15 @@ __device__ __forceinline__ bf16x8 frag8(const float* head, int c0, int valid) {
   return pack_bf16x8<bf16x8>(t);
 }
 
+typedef short bf16x4 __attribute__((ext_vector_type(4)));
+// 4 consecutive bf16 of a row (the 16-wide tail k-step over a head dim padded to 48); columns at or past
+// `valid` read as 0
+__device__ __forceinline__ bf16x4 frag4(const float* head, int c0, int valid) {
+  const float m = valid >= 4 ? 1.f : 0.f;
+  const float4 a = *reinterpret_cast<const float4*>(head + (valid >= 4 ? c0 : 0));
+  return __builtin_bit_cast(bf16x4, make_uint2(pack_bf16x2(a.x * m, a.y * m), pack_bf16x2(a.z * m, a.w * m)));
+}
+
 // MFMA 16x16x32 operand read TRANSPOSED out of a [k][n] bf16 LDS image (row stride ld elements):
 // lane l receives X[k0 + 8*(l>>4) + e][n0 + (l & 15)], e = 0..7 -- the B operand X[k][n], or the A
 // operand of X^T.  Two ds_read_b64_tr_b16: lane 4q+p of each 16-lane group addresses row q, columns
@@ -200,8 +209,11 @@ __global__ __launch_bounds__(256) void attn_rowdot_kernel(const float* __restric
 // stages) and the centre read from them -- no staging registers, no conversion or centring pass
 template <int NU, bool SAVE = false, bool RIN = false, bool PREP = false>
 __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dq_kernel(AbP p) {
-  constexpr int KS = NU > 4 ? 4 : 2;
-  constexpr int DKP = 32 * KS;
+  // the prepared tiles (PREP) pad head dims <= 48 to 48 (attn_prep_dkp): one 32-wide and one 16-wide MFMA
+  // k-step over the head dim; the register-staged forms pad to 64 / 128
+  constexpr int DKP = (PREP && NU == 3) ? 48 : 32 * (NU > 4 ? 4 : 2);
+  constexpr int KS = DKP / 32;
+  constexpr bool TAIL = DKP % 32 != 0;
   constexpr int LRK = DKP + 8;
   static_assert(SAVE || KS == 2, "the pre-bwd2 path covers head dims <= 64 only");
   static_assert(!PREP || (SAVE && RIN), "prepared operands: the bwd2 dQ kernel only");
@@ -212,9 +224,10 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dq_kernel(AbP p
   __shared__ __attribute__((aligned(16))) uint16_t Vs[BK * LRK];     // V block [key][c]
   __shared__ __attribute__((aligned(16))) uint16_t Pr[PREP ? PCH * 512 : PB1 * LRK];    // Ppos band [band row][c]
   __shared__ __attribute__((aligned(16))) float Wsc[4][WS1 / 4];    // per-wave scratch
-  // SAVE (bwd2): per wave Pd tile [16][LW] bf16; dS and Pd leave as 16-byte buffer stores (fixed count per
-  // lane and key block, out-of-range chunks dropped by the range check)
-  __shared__ __attribute__((aligned(16))) uint16_t Pdw[SAVE ? 4 : 1][SAVE ? 16 * LW : 8];
+  // SAVE (bwd2): per wave dS^T and Pd^T tiles [64 keys][16 rows] bf16 (4 rows of a key per 8-byte write); dS and
+  // Pd leave as 16-byte buffer stores of transposed reads (fixed count per lane and key block, out-of-range
+  // chunks dropped by the range check), the dS read doubling as dQu's A fragment
+  __shared__ __attribute__((aligned(16))) uint16_t Tw[SAVE ? 4 : 1][SAVE ? 2 * BK * 16 : 8];
   __shared__ __attribute__((aligned(16))) float Cn[2][DKP];   // the forward's key / value centre (attn_centre.h)
 
   KPROBE(0);
@@ -243,6 +256,7 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dq_kernel(AbP p
   // this lane's query row (A-fragment row): Qu, Qv and dO fragments
   const int iq = i0 + w * 16 + (lane & 15);
   bf16x8 fu[KS], fv[KS], fdo[KS];
+  bf16x4 fut = {}, fvt = {}, fdot = {};   // TAIL: columns 32 KS + 4 (lane >> 4) .. + 3
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks) {
     const int c0 = ks * 32 + 8 * (lane >> 4);
@@ -251,6 +265,14 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dq_kernel(AbP p
     fu[ks] = frag8(p.qu + off, c0, valid);
     fv[ks] = frag8(p.qv + off, c0, valid);
     fdo[ks] = frag8(p.dO + off, c0, valid);
+  }
+  if constexpr (TAIL) {
+    const int c0 = KS * 32 + 4 * (lane >> 4);
+    const int valid = iq < T ? dk - c0 : 0;
+    const int64_t off = (b * p.T + (iq < T ? iq : 0)) * p.ldq + hoff;
+    fut = frag4(p.qu + off, c0, valid);
+    fvt = frag4(p.qv + off, c0, valid);
+    fdot = frag4(p.dO + off, c0, valid);
   }
   const int ib = i0 + w * 16 + 4 * (lane >> 4);   // C-layout rows ib + r
   const int64_t prow0 = (bh * p.T + ib) * p.T;
@@ -264,6 +286,30 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dq_kernel(AbP p
     rs[r] = (ok && !RIN) ? p.rsum[bh * p.T + ib + r] : 0.f;
     ls[r] = ok ? p.lse[bh * p.T + ib + r] : 3.0e38f;
   }
+
+  // bwd2 (SAVE): the forward's softmax in the exp2 domain (P = exp2(s_raw scale log2e - lse log2e)), S_bd by lane
+  // permutes of the G accumulators (attn_fwd3.hip: S_bd(t, r) = G[t + (off >= 16)][r] of lane (off & 15) + 16 q4),
+  // and the dropout pair hashes shared between neighbouring lanes (common.h attn_drop_keep: keys 16 t + lo and
+  // 16 t + (lo ^ 1) share one; even lanes hash rows ib, ib + 1, odd lanes ib + 2, ib + 3)
+  const int q4 = lane >> 4, lo = lane & 15;
+  const bool odd = lo & 1;
+  const float sl2 = p.scale * 1.4426950408889634f;
+  float ls2[4];
+  int bsrc_lane[4];
+  bool bhi[4];
+  uint64_t dpr[2];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    ls2[r] = ls[r] * 1.4426950408889634f;
+    const int off = lo - 4 * q4 - r + 15;   // 0 .. 30
+    bsrc_lane[r] = ((off & 15) + 16 * q4) * 4;
+    bhi[r] = off >= 16;
+  }
+#pragma unroll
+  for (int k = 0; k < 2; ++k) dpr[k] = attn_drop_rowpairs(bh * p.T + ib + (odd ? 2 : 0) + k, p.T) + (uint64_t)(lo >> 1);
+  const uint64_t dkey = rng_key(seed, p.rng_stream);
+  const uint32_t thr = drop_threshold(p.p_drop);
+  const int hsh = odd ? 16 : 0;
 
   // next key block's operands in registers: V and K rows, the Ppos band
   float4 nv[NU], nk[NU], nb[2 * NU];
@@ -425,24 +471,47 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dq_kernel(AbP p
           g[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fv[ks], pb, g[t], 0, 0, 0);
         }
       }
+      if constexpr (TAIL) {
+        const int kof = KS * 32 + 4 * (lane >> 4);
 #pragma unroll
-      for (int t = 0; t < 5; ++t)
+        for (int t = 0; t < 4; ++t) {
+          const bf16x4 kbf = *reinterpret_cast<const bf16x4*>(Ks + (16 * t + (lane & 15)) * LRK + kof);
+          ac[t] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(fut, kbf, ac[t], 0, 0, 0);
+        }
 #pragma unroll
-        for (int r = 0; r < 4; ++r) G[(4 * (lane >> 4) + r) * LG32 + 16 * t + (lane & 15)] = g[t][r];
-      wsync();
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
+        for (int t = 0; t < 5; ++t) {
+          const bf16x4 pb = *reinterpret_cast<const bf16x4*>(Pr + (wb + 16 * t + (lane & 15)) * LRK + kof);
+          g[t] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(fvt, pb, g[t], 0, 0, 0);
+        }
+      }
+      if constexpr (SAVE) {   // raw scores ac + bd (the validity select and the scale come with the exp2 below)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int ii = 4 * (lane >> 4) + r, jj = 16 * t + (lane & 15);
-          const float bd = G[ii * LG32 + jj - ii + 15];
-          if constexpr (SAVE) {   // masked by an add: a select on the read value is branched around it
-            s[t][r] = (ac[t][r] + bd) * p.scale + ((j0 + jj < len) ? 0.f : -3.0e38f);
-          } else {
+          float X[5];
+#pragma unroll
+          for (int t = 0; t < 5; ++t) {
+            const float gv = g[t][r];   // (copied out: a bit_cast of the vector element read element 0)
+            X[t] = __int_as_float(__builtin_amdgcn_ds_bpermute(bsrc_lane[r], __float_as_int(gv)));
+          }
+#pragma unroll
+          for (int t = 0; t < 4; ++t) s[t][r] = ac[t][r] + (bhi[r] ? X[t + 1] : X[t]);
+        }
+      } else {
+#pragma unroll
+        for (int t = 0; t < 5; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) G[(4 * (lane >> 4) + r) * LG32 + 16 * t + (lane & 15)] = g[t][r];
+        wsync();
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int ii = 4 * (lane >> 4) + r, jj = 16 * t + (lane & 15);
+            const float bd = G[ii * LG32 + jj - ii + 15];
             s[t][r] = (j0 + jj < len) ? (ac[t][r] + bd) * p.scale : -3.0e38f;
           }
-        }
-      wsync();   // the scratch is rewritten below
+        wsync();   // the scratch is rewritten below
+      }
     }
     KPROBE(3 + 4 * kb);
     // ---- dPd = dO V^T ----
@@ -456,53 +525,100 @@ __global__ __launch_bounds__(256, NU == 3 ? 2 : 1) void attn_bwd_dq_kernel(AbP p
         const bf16x8 vb = *reinterpret_cast<const bf16x8*>(Vs + (16 * t + (lane & 15)) * LRK + ks * 32 + 8 * (lane >> 4));
         a[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fdo[ks], vb, a[t], 0, 0, 0);
       }
+    if constexpr (TAIL) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const bf16x4 vb = *reinterpret_cast<const bf16x4*>(Vs + (16 * t + (lane & 15)) * LRK + KS * 32 + 4 * (lane >> 4));
+        a[t] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(fdot, vb, a[t], 0, 0, 0);
+      }
+    }
     for (int e = lane; e < 16 * LG / 2; e += 64) reinterpret_cast<uint32_t*>(Gk)[e] = 0u;
+    bf16x8 dfr[2];   // dQu's A fragments (rows lane & 15, keys ks 32 + 8 q4 ..)
+    if constexpr (SAVE) {
+      uint16_t* Dt = Tw[w];             // dS^T [key][16 rows]
+      uint16_t* Pt = Tw[w] + BK * 16;   // Pd^T
+      uint32_t hk[4][2], hp[4][2];
+      if (p.p_drop > 0.f) {
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
+        for (int t = 0; t < 4; ++t)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int i = ib + r, j = j0 + 16 * t + (lane & 15);
-        float ds = 0.f, pdv = 0.f;
-        if (i < len && j < len) {
+          for (int k = 0; k < 2; ++k) hk[t][k] = drop_pair_bits(dkey, dpr[k] + (uint64_t)((j0 >> 1) + 8 * t));
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int k = 0; k < 2; ++k) hp[t][k] = (uint32_t)__builtin_amdgcn_mov_dpp((int)hk[t][k], 0xB1, 0xF, 0xF, false);
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int j = j0 + 16 * t + lo;
+        float dsv[4], pdv[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const bool ok = ib + r < len && j < len;
           float g = a[t][r] + cs[r];
           bool kp = true;
           if (p.p_drop > 0.f) {
-            kp = attn_drop_keep(rng_key(seed, p.rng_stream), attn_drop_rowpairs(bh * p.T + i, p.T), j, p.p_drop);
+            const uint32_t hv = ((r >> 1) == (int)odd) ? hk[t][r & 1] : hp[t][r & 1];
+            kp = ((hv >> hsh) & 0xffffu) >= thr;
             g = kp ? g * keep : 0.f;
           }
-          const float pe = __expf(s[t][r] - ls[r]);
-          ds = pe * (g - rs[r]) * p.scale;
-          pdv = kp ? pe * keep : 0.f;
+          const float pe = __builtin_amdgcn_exp2f(__builtin_fmaf(s[t][r], sl2, -ls2[r]));
+          dsv[r] = ok ? pe * (g - rs[r]) * p.scale : 0.f;
+          pdv[r] = (ok && kp) ? pe * keep : 0.f;
+          const int ii = 4 * q4 + r, jj = 16 * t + lo;
+          Gk[ii * LG + jj - ii + 15] = f2bf(dsv[r]);
         }
-        const int ii = 4 * (lane >> 4) + r, jj = 16 * t + (lane & 15);
-        const uint16_t bv = f2bf(ds);
-        D[ii * LW + jj] = bv;
-        Gk[ii * LG + jj - ii + 15] = bv;
-        if (SAVE) Pdw[w][ii * LW + jj] = f2bf(pdv);
+        *reinterpret_cast<uint2*>(Dt + (16 * t + lo) * 16 + 4 * q4) =
+            make_uint2(pack_bf16x2(dsv[0], dsv[1]), pack_bf16x2(dsv[2], dsv[3]));
+        *reinterpret_cast<uint2*>(Pt + (16 * t + lo) * 16 + 4 * q4) =
+            make_uint2(pack_bf16x2(pdv[0], pdv[1]), pack_bf16x2(pdv[2], pdv[3]));
       }
-    wsync();
-    if (SAVE) {
-      // this wave's 16 rows x 64 keys of dS and Pd: 128 16-byte chunks each, two per lane
+      wsync();
+      // this wave's 16 rows x 64 keys of dS and Pd: lane (q4, lo) stores row lo's keys ks 32 + 8 q4 .. + 7 (a
+      // transposed read of the [key][row] tile), two chunks per lane each
 #pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const int c = lane + 64 * q, row = c >> 3, c8 = c & 7;
-        const int i = i0 + w * 16 + row, jc = j0 + 8 * c8;
+      for (int ks = 0; ks < 2; ++ks) {
+        const int i = i0 + w * 16 + lo, jc = j0 + ks * 32 + 8 * q4;
         const uint32_t off = (i < T && jc < p.ldt) ? (uint32_t)(((bh * p.T + i) * p.ldt + jc) * 2) : AB_OOB;
-        const uint4 vd = *reinterpret_cast<const uint4*>(D + row * LW + 8 * c8);
-        const uint4 vp = *reinterpret_cast<const uint4*>(&Pdw[w][row * LW + 8 * c8]);
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, vd), rds,
-                                               off, 0, 0);
+        dfr[ks] = tr_frag(Dt, 16, ks * 32, 0, lane);
+        const bf16x8 vp = tr_frag(Pt, 16, ks * 32, 0, lane);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, dfr[ks]),
+                                               rds, off, 0, 0);
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, vp), rpd,
                                                off, 0, 0);
       }
+    } else {
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int i = ib + r, j = j0 + 16 * t + (lane & 15);
+          float ds = 0.f;
+          if (i < len && j < len) {
+            float g = a[t][r] + cs[r];
+            if (p.p_drop > 0.f) {
+              const bool kp = attn_drop_keep(dkey, attn_drop_rowpairs(bh * p.T + i, p.T), j, p.p_drop);
+              g = kp ? g * keep : 0.f;
+            }
+            const float pe = __expf(s[t][r] - ls[r]);
+            ds = pe * (g - rs[r]) * p.scale;
+          }
+          const int ii = 4 * (lane >> 4) + r, jj = 16 * t + (lane & 15);
+          const uint16_t bv = f2bf(ds);
+          D[ii * LW + jj] = bv;
+          Gk[ii * LG + jj - ii + 15] = bv;
+        }
+      wsync();
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        dfr[ks] = *reinterpret_cast<const bf16x8*>(D + (lane & 15) * LW + ks * 32 + 8 * (lane >> 4));
     }
     KPROBE(4 + 4 * kb);
     // ---- dQu += dS K (K read transposed), dQv += skew(dS) Pband (band read transposed) ----
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      const bf16x8 da = *reinterpret_cast<const bf16x8*>(D + (lane & 15) * LW + ks * 32 + 8 * (lane >> 4));
 #pragma unroll
-      for (int u = 0; u < NU; ++u) aq[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, tr_frag(Ks, LRK, ks * 32, 16 * u, lane),
+      for (int u = 0; u < NU; ++u) aq[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dfr[ks], tr_frag(Ks, LRK, ks * 32, 16 * u, lane),
                                                                                 aq[u], 0, 0, 0);
     }
 #pragma unroll

@@ -52,6 +52,8 @@ constexpr int kAttnBandPad0 = 64;
 constexpr int kAttnBandPad1 = 88;
 __host__ __device__ inline int64_t attn_prep_tp(int64_t T) { return (T + 63) / 64 * 64; }
 __host__ __device__ inline int64_t attn_prep_npb(int64_t T) { return kAttnBandPad0 + (2 * T - 1) + kAttnBandPad1; }
-__host__ __device__ inline int attn_prep_dkp(int64_t dk) { return dk > 64 ? 128 : 64; }
+// padded head dim of the prepared tiles: 48 (a 32-wide and a 16-wide MFMA k-step) for head dims <= 48 -- the
+// bench's student / teacher (44) -- else 64 or 128
+__host__ __device__ inline int attn_prep_dkp(int64_t dk) { return dk > 64 ? 128 : dk > 48 ? 64 : 48; }
 
 }  // namespace kdfm

@@ -33,8 +33,9 @@ constexpr int A3PAD0 = kAttnBandPad0;   // zero rows before the first position r
 constexpr int A3LDT = 16;          // bf16 row stride of the per-wave P^T tile [64 keys][16 rows]
 
 template <int NU> struct A3Geo {
-  static constexpr int KS = NU > 4 ? 4 : 2;        // MFMA k-steps over the padded head dim
-  static constexpr int DKP = 32 * KS;
+  static constexpr int DKP = NU == 3 ? 48 : NU > 4 ? 128 : 64;   // padded head dim (attn_prep_dkp)
+  static constexpr int KS = DKP / 32;              // 32-wide MFMA k-steps over it ...
+  static constexpr bool TAIL = DKP % 32 != 0;      // ... and one 16-wide (v_mfma_f32_16x16x16_bf16) at 48
   static constexpr int LR = DKP + 8;               // bf16 row stride (8-byte aligned transposed reads)
   static constexpr int KCH = A3K * LR * 2 / 1024;  // 1 KB DMA chunks per K / V tile
   static constexpr int BCH = A3BAND * LR * 2 / 1024;
@@ -185,6 +186,15 @@ __device__ __forceinline__ bf16x8 a3_frag8(const float* head, int c0, int valid)
   return pack_bf16x8<bf16x8>(t);
 }
 
+typedef short bf16x4 __attribute__((ext_vector_type(4)));
+// 4 consecutive bf16 of a row (the 16-wide tail k-step); columns at or past `valid` read as 0
+__device__ __forceinline__ bf16x4 a3_frag4(const float* head, int c0, int valid) {
+  const float m = valid >= 4 ? 1.f : 0.f;
+  const float4 a = *reinterpret_cast<const float4*>(head + (valid >= 4 ? c0 : 0));
+  const uint32_t lo = pack_bf16x2(a.x * m, a.y * m), hi = pack_bf16x2(a.z * m, a.w * m);
+  return __builtin_bit_cast(bf16x4, make_uint2(lo, hi));
+}
+
 // B operand X[k][n] read transposed out of a [k][n] bf16 LDS image (attn_bwd.hip tr_frag)
 __device__ __forceinline__ bf16x8 a3_tr_frag(const uint16_t* img, int ld, int k0, int n0, int lane) {
   const int li = lane & 15;
@@ -241,9 +251,9 @@ __global__ __launch_bounds__(256, NU == 3 ? 4 : NU == 4 ? 3 : 2) void relpos_att
   using Gm = A3Geo<NU>;
   constexpr int KS = Gm::KS, LR = Gm::LR, KCH = Gm::KCH, BCH = Gm::BCH, NCH = 2 * KCH + BCH;
   // K tile | V tile | band rows, contiguous (wave w's DMA chunks at fixed offsets).  The per-wave P^T tiles
-  // [key][row] reuse the K tile once every wave has read it (a barrier after the score MFMAs): 37 KB per
-  // workgroup, 4 workgroups per CU at head dim <= 48
-  static_assert(4 * A3K * A3LDT <= A3K * LR, "the P^T tiles must fit in the K tile");
+  // [key][row] reuse the band tile once every wave has read it (a barrier after the score MFMAs): 28 KB per
+  // workgroup at head dim <= 48 (row stride 56), 4 workgroups per CU
+  static_assert(4 * A3K * A3LDT <= A3BAND * LR, "the P^T tiles must fit in the band tile");
   __shared__ __attribute__((aligned(16))) uint16_t Sm[(2 * A3K + A3BAND) * LR];
   uint16_t* const Ks = Sm;
   uint16_t* const Vs = Sm + A3K * LR;
@@ -293,13 +303,22 @@ __global__ __launch_bounds__(256, NU == 3 ? 4 : NU == 4 ? 3 : 2) void relpos_att
   // this lane's query row (A-fragment row): Qu / Qv fragments
   const int iq = i0 + w * 16 + (lane & 15);
   bf16x8 fu[KS], fv[KS];
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks) {
-    const int c0 = ks * 32 + 8 * (lane >> 4);
-    const int valid = (iq < T) ? dk - c0 : 0;
+  bf16x4 fut = {}, fvt = {};   // the 16-wide tail step (TAIL): columns 32 KS + 4 (lane >> 4) .. + 3
+  {
     const int64_t off = (b * p.T + (iq < T ? iq : 0)) * p.d + hoff;
-    fu[ks] = a3_frag8(p.qu + off, c0, valid);
-    fv[ks] = a3_frag8(p.qv + off, c0, valid);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int c0 = ks * 32 + 8 * (lane >> 4);
+      const int valid = (iq < T) ? dk - c0 : 0;
+      fu[ks] = a3_frag8(p.qu + off, c0, valid);
+      fv[ks] = a3_frag8(p.qv + off, c0, valid);
+    }
+    if constexpr (Gm::TAIL) {
+      const int c0 = KS * 32 + 4 * (lane >> 4);
+      const int valid = (iq < T) ? dk - c0 : 0;
+      fut = a3_frag4(p.qu + off, c0, valid);
+      fvt = a3_frag4(p.qv + off, c0, valid);
+    }
   }
   const int q4 = lane >> 4, lo = lane & 15;
   const int ib = i0 + w * 16 + 4 * q4;   // C-layout rows ib + r
@@ -336,7 +355,7 @@ __global__ __launch_bounds__(256, NU == 3 ? 4 : NU == 4 ? 3 : 2) void relpos_att
   f32x4 oacc[NU];
 #pragma unroll
   for (int u = 0; u < NU; ++u) oacc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-  uint16_t* Pw = Sm + w * (A3K * A3LDT);
+  uint16_t* Pw = Pr + w * (A3K * A3LDT);
 
   for (int kb = 0; kb < nkb; ++kb) {
     const int j0 = kb * A3K;
@@ -366,8 +385,20 @@ __global__ __launch_bounds__(256, NU == 3 ? 4 : NU == 4 ? 3 : 2) void relpos_att
 #pragma unroll
       for (int t = 0; t < 5; ++t) g[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fv[ks], pf[t], g[t], 0, 0, 0);
     }
+    if constexpr (Gm::TAIL) {   // columns 32 KS .. 32 KS + 15: 8-byte fragments, one 16x16x16 MFMA per tile
+      const int kof = KS * 32 + 4 * q4;
+      bf16x4 kf[4], pf[5];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) kf[t] = *reinterpret_cast<const bf16x4*>(Ks + (16 * t + lo) * LR + kof);
+#pragma unroll
+      for (int t = 0; t < 5; ++t) pf[t] = *reinterpret_cast<const bf16x4*>(Pr + (wb + 16 * t + lo) * LR + kof);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) ac[t] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(fut, kf[t], ac[t], 0, 0, 0);
+#pragma unroll
+      for (int t = 0; t < 5; ++t) g[t] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(fvt, pf[t], g[t], 0, 0, 0);
+    }
     // raw scores s = S_ac + S_bd (unscaled), the rel_shift by lane permutes
-    __syncthreads();   // every wave has read the K tile: its space takes the P^T tiles below
+    __syncthreads();   // every wave has read the band tile: its space takes the P^T tiles below
     float s[4][4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -521,6 +552,9 @@ int kdfm_attn_kv_prep(const float* qkv, const int64_t* lengths, uint16_t* kb, ui
   if (a3_dkp(dk) == 128)
     hipLaunchKernelGGL(attn_kv_prep_kernel<128>, grid, dim3(256), lds, as_stream(stream), qkv, lengths, kb, vb, centre, H,
                        (int)T, d, (int)dk, Tp);
+  else if (a3_dkp(dk) == 48)
+    hipLaunchKernelGGL(attn_kv_prep_kernel<48>, grid, dim3(256), lds, as_stream(stream), qkv, lengths, kb, vb, centre, H,
+                       (int)T, d, (int)dk, Tp);
   else
     hipLaunchKernelGGL(attn_kv_prep_kernel<64>, grid, dim3(256), lds, as_stream(stream), qkv, lengths, kb, vb, centre, H,
                        (int)T, d, (int)dk, Tp);
@@ -541,6 +575,9 @@ int kdfm_attn_band_prep(const float* pos, int64_t ld_layer, int64_t layers, uint
   const dim3 grid((unsigned)ceil_div(npb, 64), (unsigned)(layers * H));
   if (a3_dkp(dk) == 128)
     hipLaunchKernelGGL(attn_band_prep_kernel<128>, grid, dim3(256), 0, as_stream(stream), pos, ld_layer, pb, H, 2 * T - 1, d,
+                       (int)dk, npb);
+  else if (a3_dkp(dk) == 48)
+    hipLaunchKernelGGL(attn_band_prep_kernel<48>, grid, dim3(256), 0, as_stream(stream), pos, ld_layer, pb, H, 2 * T - 1, d,
                        (int)dk, npb);
   else
     hipLaunchKernelGGL(attn_band_prep_kernel<64>, grid, dim3(256), 0, as_stream(stream), pos, ld_layer, pb, H, 2 * T - 1, d,

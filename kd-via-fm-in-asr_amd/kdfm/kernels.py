@@ -691,8 +691,9 @@ def wgrad_set_fold_arena(arena):
 
 
 def wgrad_fold_flush():
-    """Fold every weight gradient queued on the current stream (one launch per 24 products)."""
-    call("kdfm_wgrad_fold_flush", _s())
+    """Fold every weight gradient queued on the current stream (one launch per 24 products).  Traced as
+    "wgrad_fold" (no algorithmic bytes of its own: the folds' time belongs to the deferred products')."""
+    _traced("wgrad_fold", 0.0, 0.0, "kdfm_wgrad_fold_flush", _s())
 
 
 def wgrad_fold_pending() -> int:

@@ -62,10 +62,10 @@ def test_prepared_images_and_batched_band():
     dk = d // H
     qkv, qu, qv, ppos, lens = _inputs(B, H, T, d, 9, kcm=1.0)
     kb, vb, cen = K.attn_kv_prep(qkv, lens, B, H, T)
-    Tp, LR = 128, 72
+    Tp, LR = 128, 56   # head dim 44 -> padded to 48 (attn_prep_dkp) + 8
     kb = kb.view(B, H, Tp, LR).float().cpu()
     vb = vb.view(B, H, Tp, LR).float().cpu()
-    cen = cen.view(B, H, 2, 64).cpu()
+    cen = cen.view(B, H, 2, 48).cpu()
     x = qkv.view(B, T, 3, H, dk).cpu()
     for b in range(B):
         n = min(16, int(lens[b]))
@@ -93,8 +93,10 @@ def test_prepared_images_and_batched_band():
                                        (3, 2, 77, 88, 0.0)])
 def test_dq3_equals_register_staged_dq(B, H, T, d, p):
     """The bwd2 dQ kernel over the forward's prepared operands (kdfm_relpos_attn_bwd2_dq3) against the one that
-    stages K / V / the band from qkv / pos: dS and Pd bitwise; dqu / dqv equal up to the sign of zero products
-    (keys past a length hold K - kc in the prepared tiles, 0 in the staged ones, times dS = 0): max |diff| 0."""
+    stages K / V / the band from qkv / pos: the same bf16 operands and dropout mask; at head dims <= 48 the
+    prepared tiles are padded to 48 (a 32- and a 16-wide MFMA k-step) where the staged ones pad to 64, so the
+    scores differ by f32 summation order only: dS / Pd within a bf16 rounding (2^-7 relative + 1e-6),
+    dqu / dqv within 1e-3 relative Frobenius; bitwise at the other head dims."""
     from kdfm import kernels as K
     qkv, qu, qv, ppos, lens = _inputs(B, H, T, d, 3 * T + d, kcm=1.5)
     g = torch.Generator(device="cuda").manual_seed(T)
@@ -120,5 +122,12 @@ def test_dq3_equals_register_staged_dq(B, H, T, d, p):
         outs.append((dS, Pd, dqu, dqv))
     torch.cuda.synchronize()
     (a0, b0, c0, e0), (a1, b1, c1, e1) = outs
-    assert torch.equal(a0, a1) and torch.equal(b0, b1)
-    assert (c0 - c1).abs().max().item() == 0.0 and (e0 - e1).abs().max().item() == 0.0
+    if d // H > 48:
+        assert torch.equal(a0, a1) and torch.equal(b0, b1)
+        assert (c0 - c1).abs().max().item() == 0.0 and (e0 - e1).abs().max().item() == 0.0
+        return
+    for x, y in ((a0, a1), (b0, b1)):
+        x, y = x.float(), y.float()
+        assert ((x - y).abs() <= y.abs() * 2.0 ** -7 + 1e-6).all(), (x - y).abs().max().item()
+    for x, y in ((c0, c1), (e0, e1)):
+        assert ((x - y).norm() / y.norm()).item() <= 1e-3
