@@ -48,9 +48,9 @@ __host__ __device__ inline int64_t a3_npb(int64_t T) { return attn_prep_npb(T); 
 
 // ---- preparation --------------------------------------------------------------------------------------
 // kb / vb [b*H + h][Tp][LR]: rows j < T hold bf16(K_j - kc) / bf16(V_j - vc) in columns < dk, zeros elsewhere;
-// cen [b*H + h][2][DKP] = (kc, vc) f32 (zeros past dk).  One workgroup per (64 rows, utterance b), every head:
-// the centres of all heads (one thread per float4 column group of K | V summing the utterance's first n rows in
-// order -- attn_centre.h's kv_centre arithmetic, the same bits), then the 64 rows' conversion, one (kind, head)
+// cen [b*H + h][2][DKP] = (kc, vc) f32 (zeros past dk).  One workgroup per (64 rows, utterance b, hpw (kind,
+// head) tiles): the centres of its tiles (one thread per float4 column group summing the utterance's first n rows
+// in order -- attn_centre.h's kv_centre arithmetic, the same bits), then the 64 rows' conversion, one (kind, head)
 // tile after the other with the next tile's loads issued before the current one is converted (and the first
 // tile's before the centres).  A thread owns fixed (row, 8-column group) items of every tile: compile-time
 // index arithmetic, PER x 2 float4 loads in flight per tile.
@@ -58,11 +58,12 @@ template <int DKP>
 __global__ __launch_bounds__(256) void attn_kv_prep_kernel(const float* __restrict__ qkv, const int64_t* __restrict__ lens,
                                                            uint16_t* __restrict__ kb, uint16_t* __restrict__ vb,
                                                            float* __restrict__ cen, int64_t H, int T, int64_t d, int dk,
-                                                           int64_t Tp) {
+                                                           int64_t Tp, int hpw) {
   constexpr int LR = DKP + 8, P8 = LR / 8, ITEMS = 64 * P8, PER = (ITEMS + 255) / 256;
   extern __shared__ __attribute__((aligned(16))) float Cn[];   // [kind][head][DKP]
   const int64_t b = blockIdx.y;
-  const int Hh = (int)H, nkh = 2 * Hh;
+  const int Hh = (int)H;
+  const int kh0 = blockIdx.z * hpw, kh1 = min(2 * Hh, kh0 + hpw);   // this workgroup's (kind, head) tiles
   const int len = lens ? (int)min<int64_t>(lens[b], T) : T;
   const float* kbase = qkv + b * T * 3 * d + d;   // row 0 of utterance b, K columns (V at + d)
   const int j0 = blockIdx.x * 64;
@@ -92,15 +93,16 @@ __global__ __launch_bounds__(256) void attn_kv_prep_kernel(const float* __restri
     }
   };
   float4 a0[PER], e0[PER];
-  load(0, a0, e0);
+  load(kh0, a0, e0);
   // centres
   const int n = len >= 16 ? 16 : len >= 8 ? 8 : len >= 4 ? 4 : len >= 2 ? 2 : (len > 0 ? 1 : 0);
   const float inv = n > 0 ? 1.f / (float)n : 0.f;   // a power of two: exact
+  const int nkh = kh1 - kh0;
   for (int e = threadIdx.x; e < nkh * DKP; e += 256) Cn[e] = 0.f;
   __syncthreads();
   const int cq = dk >> 2;
   for (int g = threadIdx.x; g < nkh * cq; g += 256) {   // (kind, head, float4 column group)
-    const int kh = g / cq, c4 = (g - kh * cq) * 4;
+    const int kl = g / cq, c4 = (g - kl * cq) * 4, kh = kh0 + kl;
     const int kind = kh >= Hh ? 1 : 0, h = kh - kind * Hh;
     const float* src = kbase + (int64_t)kind * d + (int64_t)h * dk + c4;
     float4 v[16];
@@ -112,21 +114,21 @@ __global__ __launch_bounds__(256) void attn_kv_prep_kernel(const float* __restri
       const float m = r < n ? 1.f : 0.f;
       sm.x += m * v[r].x; sm.y += m * v[r].y; sm.z += m * v[r].z; sm.w += m * v[r].w;
     }
-    float* o = Cn + kh * DKP + c4;
+    float* o = Cn + kl * DKP + c4;
     o[0] = sm.x * inv; o[1] = sm.y * inv; o[2] = sm.z * inv; o[3] = sm.w * inv;
   }
   __syncthreads();
   if (blockIdx.x == 0)
     for (int e = threadIdx.x; e < nkh * DKP; e += 256) {   // cen[(b H + h)][kind][c]
-      const int kh = e / DKP, c = e - kh * DKP;
+      const int kl = e / DKP, c = e - kl * DKP, kh = kh0 + kl;
       const int kind = kh >= Hh ? 1 : 0, h = kh - kind * Hh;
       cen[((b * H + h) * 2 + kind) * DKP + c] = Cn[e];
     }
-  for (int kh = 0; kh < nkh; ++kh) {
+  for (int kh = kh0; kh < kh1; ++kh) {
     float4 a1[PER], e1[PER];
-    if (kh + 1 < nkh) load(kh + 1, a1, e1);
+    if (kh + 1 < kh1) load(kh + 1, a1, e1);
     const int kind = kh >= Hh ? 1 : 0, h = kh - kind * Hh;
-    const float* cc = Cn + kh * DKP;
+    const float* cc = Cn + (kh - kh0) * DKP;
     uint16_t* dst = (kind ? vb : kb) + ((b * H + h) * Tp + j0) * LR;
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
@@ -547,17 +549,22 @@ int kdfm_attn_kv_prep(const float* qkv, const int64_t* lengths, uint16_t* kb, ui
   if (B == 0) return KDFM_OK;
   KDFM_REQUIRE(H <= 64, "at most 64 heads");
   const int64_t Tp = a3_tp(T);
-  const dim3 grid((unsigned)(Tp / A3K), (unsigned)B);
-  const size_t lds = (size_t)2 * H * a3_dkp(dk) * sizeof(float);
+  static const int hpw_env = [] { const char* e = getenv("KDFM_KVPREP_HPW"); return e ? atoi(e) : 0; }();
+  // (kind, head) tiles per workgroup: every tile in one workgroup once (Tp / 64) x B fills the chip (the bench's
+  // B = 32: 1, 2 or 8 tiles measured the same step time), one tile per workgroup for small batches
+  int hpw = hpw_env > 0 ? hpw_env : (Tp / A3K) * B >= 256 ? (int)(2 * H) : 1;
+  if (hpw > 2 * H) hpw = (int)(2 * H);
+  const dim3 grid((unsigned)(Tp / A3K), (unsigned)B, (unsigned)((2 * H + hpw - 1) / hpw));
+  const size_t lds = (size_t)hpw * a3_dkp(dk) * sizeof(float);
   if (a3_dkp(dk) == 128)
     hipLaunchKernelGGL(attn_kv_prep_kernel<128>, grid, dim3(256), lds, as_stream(stream), qkv, lengths, kb, vb, centre, H,
-                       (int)T, d, (int)dk, Tp);
+                       (int)T, d, (int)dk, Tp, hpw);
   else if (a3_dkp(dk) == 48)
     hipLaunchKernelGGL(attn_kv_prep_kernel<48>, grid, dim3(256), lds, as_stream(stream), qkv, lengths, kb, vb, centre, H,
-                       (int)T, d, (int)dk, Tp);
+                       (int)T, d, (int)dk, Tp, hpw);
   else
     hipLaunchKernelGGL(attn_kv_prep_kernel<64>, grid, dim3(256), lds, as_stream(stream), qkv, lengths, kb, vb, centre, H,
-                       (int)T, d, (int)dk, Tp);
+                       (int)T, d, (int)dk, Tp, hpw);
   return check_launch("kdfm_attn_kv_prep");
 }
 

@@ -126,6 +126,12 @@ def test_logit_kd_module_training_step_matches_oracle():
     n_layers, B, N = 2, 2, 16000
     kw = dict(n_layers=n_layers, dither=0.0, spec_augment=False, dropout=0.0, dropout_pre_encoder=0.0,
               dropout_att=0.0)
+    # the decoders (ConvASRDecoder, torch's default Linear init) draw from the global generator: seeded so
+    # the step does not depend on the tests that ran before it.  The encoders' seeded init puts one conv0
+    # output (channel 54, first frame) within the log-mel's rounding of zero, and the gradient that reaches
+    # it through the decoder decides how far the first-conv carve-out is from its bound
+    # (tools/conv0_diag.py: 1-6 % of that channel's max over unseeded decoders)
+    torch.manual_seed(0)
     teacher = EncDecCTCModelBPE(d_model=176, n_heads=4, device="cuda", init_seed=0, **kw)
     model = DistilEncDecCTCModelBPE(teacher, kd_alpha=0.1, kd_temperature=1.0, device="cuda", init_seed=1, **kw)
     g = torch.Generator().manual_seed(14)

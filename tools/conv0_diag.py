@@ -19,6 +19,7 @@ def run(overlap):
     K.set_deterministic(True)
     n_layers, B, N = 2, 2, 16000
     kw = dict(n_layers=n_layers, dither=0.0, spec_augment=False, dropout=0.0, dropout_pre_encoder=0.0, dropout_att=0.0)
+    torch.manual_seed(int(os.environ.get("DIAG_SEED", "0")))   # the decoders' default init
     teacher = EncDecCTCModelBPE(d_model=176, n_heads=4, device="cuda", init_seed=0, **kw)
     model = DistilEncDecCTCModelBPE(teacher, kd_alpha=0.1, kd_temperature=1.0, device="cuda", init_seed=1, **kw)
     g = torch.Generator().manual_seed(14)
@@ -68,6 +69,18 @@ def run(overlap):
     # the student's mel vs the oracle's
     if "mel" in out:
         print("oracle mel shape", tuple(out["mel"].shape))
+        # the oracle's conv0 pre-activations nearest zero (a ReLU the GPU's f32 log-mel can flip)
+        mel = out["mel"].detach().double().transpose(1, 2).unsqueeze(1)   # (B, 1, T, F)
+        w0 = p64["encoder.pre_encode.conv.0.weight"].detach()
+        b0 = p64["encoder.pre_encode.conv.0.bias"].detach()
+        pre = torch.nn.functional.conv2d(mel, w0, b0, stride=2, padding=1)
+        flat = pre.abs().flatten()
+        idx = torch.topk(-flat, 4).indices
+        for i in idx.tolist():
+            b, rem = divmod(i, pre[0].numel())
+            c, rem = divmod(rem, pre.shape[2] * pre.shape[3])
+            t, f = divmod(rem, pre.shape[3])
+            print(f"   near-zero conv0 pre-activation: b={b} ch={c} t={t} f={f} value={pre[b, c, t, f].item():.3e}")
 
 
 if __name__ == "__main__":

@@ -10,9 +10,9 @@ OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/fetch" -o run \
-  -- python3 -u bench.py --steps 2 --warmup 1 --no-cpu-baseline > "$OUT/fetch.log" 2>&1 &&
+  -- python3 -u bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-f32-sensitivity > "$OUT/fetch.log" 2>&1 &&
 echo "fetch pass ok" &&
 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/write" -o run \
-  -- python3 -u bench.py --steps 2 --warmup 1 --no-cpu-baseline > "$OUT/write.log" 2>&1 &&
+  -- python3 -u bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-f32-sensitivity > "$OUT/write.log" 2>&1 &&
 echo "write pass ok" &&
-python3 tools/pmc_summary.py "$OUT" > "$OUT/traffic.txt" && head -40 "$OUT/traffic.txt"
+python3 tools/pmc_summary.py "$OUT" > "$OUT/traffic.txt" && rm -rf "$OUT/fetch" "$OUT/write" && head -40 "$OUT/traffic.txt"
