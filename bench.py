@@ -35,7 +35,7 @@ MI355X_F32_MFMA_TFLOPS = 157.3
 MI355X_HBM_GBPS = 8000.0            # MI355X_MICROARCH.md §HBM (8 TB/s spec peak)
 # PMC traffic per kernel (tools/pmc_traffic.sh -> tools/pmc_summary.py: separate --pmc FETCH_SIZE and
 # WRITE_SIZE passes, FETCH_SIZE doubled per the gfx950 correction), committed under profiles/
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r04_pmc_traffic.json")
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r05_pmc_traffic.json")
 # kdfm_gemm kernel family (kernels.ROUTES) -> kernel-name stems in the rocprofv3 / PMC summaries
 ROUTE_KERNELS = {"generic": ("gemm_kernel",), "skinny": ("sk_fwd_kernel", "skd_fwd_kernel"),
                  "rowstream_fwd": ("rs_fwd_kernel",), "wide_wgrad": ("rs_wgrad_kernel", "rs_fold_kernel"),
@@ -367,6 +367,9 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = max_over_ranks(time.perf_counter() - t0, dev)
+    if os.environ.get("KDFM_PLAN_KNOCKOUT") and rank == 0:   # what-if probe (kdfm/plan.py): not a bench line
+        print(f"KNOCKOUT {os.environ['KDFM_PLAN_KNOCKOUT']} ms_per_step {1e3 * elapsed / args.steps:.3f}", flush=True)
+        return
     # live per-kernel timing: one instrumented eager step right after the timed steps; every
     # kdfm_gemm launch (keyed by the kernel family libkdfm routed it to), the frontend and the
     # depthwise convs bracketed by HIP events on the stream they run on

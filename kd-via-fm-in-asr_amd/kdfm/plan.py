@@ -26,6 +26,8 @@ at record time, so a plan is never silently incomplete.
 from __future__ import annotations
 
 import ctypes as C
+import os
+import warnings
 
 import torch
 from torch.utils._python_dispatch import TorchDispatchMode
@@ -158,7 +160,14 @@ class StepPlan:
             raise PlanError(f"the step issues torch ops a plan cannot replay: {sorted(set(self._bad))[:8]}")
         # resolve the raw event handles once (events exist after their first record)
         ops = []
+        # KDFM_PLAN_KNOCKOUT=name[,name...]: drop those entries' launches from the replay -- a what-if probe
+        # of a kernel family's share of the step (tools/runs/knockout); the replayed step's results are wrong
+        knock = {n for n in os.environ.get("KDFM_PLAN_KNOCKOUT", "").split(",") if n}
+        if knock:
+            warnings.warn(f"KDFM_PLAN_KNOCKOUT={sorted(knock)}: the replayed step skips these launches (probe only)")
         for op in self.ops:
+            if op[0] == "k" and knock and op[1].__name__ in knock:
+                continue
             if op[0] in ("er", "ew"):
                 ops.append((op[0], C.c_void_p(op[1].cuda_event), C.c_void_p(op[2])))
             else:

@@ -102,9 +102,14 @@ def _worker(rank, world, port, out):
         p = eng.student.data.detach().cpu()
         both = [torch.empty_like(p) for _ in range(world)]
         dist.all_gather(both, p)
+        diff = (g_ddp - g_sum).abs()
+        worst = int(diff.argmax())
+        where = max(((o, k) for k, o in eng.student.offsets.items() if o <= worst), default=(0, "?"))[1]
         out[rank] = dict(
             grad_equal=bool(torch.equal(g_ddp, g_sum)),
-            grad_maxdiff=float((g_ddp - g_sum).abs().max()),
+            grad_maxdiff=float(diff.max()),
+            grad_where=(where, worst, int((diff > 0).sum()), float(g_sum.abs()[worst]),
+                        float(local[0].abs()[worst]), float(local[1].abs()[worst]), float(g_ddp[worst])),
             shard_differs=bool(not torch.equal(local[0], local[1])),
             scale=scale, launched_early=launched_early,
             ranks_equal=bool(torch.equal(both[0], both[1])),
@@ -123,7 +128,7 @@ def test_ddp_gradients_equal_sum_of_shard_gradients():
         o = out[r]
         assert o["finite"]
         assert o["shard_differs"], "the two shards must give different gradients"
-        assert o["grad_equal"], (r, o["grad_maxdiff"])
+        assert o["grad_equal"], (r, o["grad_maxdiff"], o["grad_where"])
         assert o["scale"] == 0.5
         assert o["launched_early"] >= 3, "buckets must be launched while the backward runs"
         assert o["ranks_equal"], "parameters diverged across ranks after the AdamW step"

@@ -121,14 +121,12 @@ def test_dwconv_bwd_bn_equals_separate(B, T, d, k, batch_stats):
     dw1, db1 = torch.zeros(d, k, device="cuda"), torch.zeros(d, device="cuda")
     K.dwconv_bwd_fold(ws, dw1, db1, B, T, d, k)
     torch.cuda.synchronize()
-    # the f64 sums are atomics (their order varies run to run): compare the affine grads to f32 rounding,
-    # and the rest exactly when the sums agree bit for bit
+    # the f64 sums are atomics (their order varies run to run): compare the affine grads to f32 rounding and
+    # the rest to 1e-5 -- not bitwise even when the sums agree: the fused kernel forms dy on load with its
+    # own FMA contraction of gamma rstd (dz silu' - m1 - xh m2), the separate BN-SiLU backward with another
     _close(dgm1, dgm0, rel=1e-6)
     _close(dbt1, dbt0, rel=1e-6)
     assert bool((red_next == 0).all())
-    if torch.equal(red, red1):
-        assert torch.equal(dg1, dg0) and torch.equal(dw1, dw0) and torch.equal(db1, db0)
-    else:
-        _close(dg1, dg0, rel=1e-5)
-        _close(dw1, dw0, rel=1e-5)
-        _close(db1, db0, rel=1e-5)
+    _close(dg1, dg0, rel=1e-5)
+    _close(dw1, dw0, rel=1e-5)
+    _close(db1, db0, rel=1e-5)
