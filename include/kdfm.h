@@ -677,10 +677,11 @@ int kdfm_relpos_attn_fwd(const float* qu, const float* qv, const float* qkv, con
                          int64_t T, int64_t d, float scale, float dropout_p, const uint64_t* seed,
                          uint64_t rng_stream, void* stream);
 /* The same forward over PREPARED bf16 operands (csrc/attn_fwd3.hip; single pass, lse only -- the bwd2
- * backward's form -- or inference with lse NULL): O and lse are bitwise kdfm_relpos_attn_fwd's.  Every operand
+ * backward's form -- or inference with lse NULL): the same bf16 operands, MFMAs and dropout mask as
+ * kdfm_relpos_attn_fwd, its softmax in the exp2 domain (O within 1e-3, lse within 2e-6 of it).  Every operand
  * tile of a (64 queries, 64 keys) step is one contiguous range copied into LDS by LDS-DMA.
- *   kdfm_attn_kv_prep: kb / vb (B*H, Tp, LR) bf16 with Tp = T rounded up to 64, LR = DKP + 8, DKP = 64 (dk <= 64)
- *     or 128: rows j < T = bf16(K_j - kc) / bf16(V_j - vc) in columns < dk (the centring of
+ *   kdfm_attn_kv_prep: kb / vb (B*H, Tp, LR) bf16 with Tp = T rounded up to 64, LR = DKP + 8, DKP = 48 (dk <= 48),
+ *     64 (dk <= 64) or 128: rows j < T = bf16(K_j - kc) / bf16(V_j - vc) in columns < dk (the centring of
  *     kdfm_relpos_attn_fwd), zeros elsewhere; centre (B*H, 2, DKP) f32 = (kc, vc).  Sizes:
  *     kdfm_attn_kv_prep_elems / kdfm_attn_centre_elems (-1: unsupported).
  *   kdfm_attn_band_prep: every layer's projected positions pos + l * ld_layer ((2T-1, d) each) as pb
@@ -697,7 +698,8 @@ int kdfm_attn_band_prep(const float* pos, int64_t ld_layer, int64_t layers, uint
                         int64_t d, void* stream);
 /* bwd2 part 1 (kdfm_relpos_attn_bwd2_dq) over the forward's prepared operands: K / V / band tiles and the
  * centre from kdfm_attn_kv_prep / kdfm_attn_band_prep (the forward's own, kept for the backward) instead of
- * qkv / pos -- the same dqu / dqv / dS / Pd (dS and Pd bitwise; dqu / dqv up to the sign of zero products). */
+ * qkv / pos -- the same dqu / dqv / dS / Pd (DKP 64 / 128: dS and Pd bitwise, dqu / dqv up to the sign of zero
+ * products; DKP 48: exp2-domain scores, dS / Pd within one bf16 rounding, dqu / dqv within 1e-3 relative). */
 int kdfm_relpos_attn_bwd2_dq3(const float* dO, const float* O, const float* qu, const float* qv, const uint16_t* kb,
                               const uint16_t* vb, const float* centre, const uint16_t* pb, const float* lse,
                               const int64_t* lengths, uint16_t* ds, uint16_t* pd, float* dqu, float* dqv, int64_t B,

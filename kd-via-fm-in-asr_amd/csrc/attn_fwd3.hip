@@ -1,9 +1,9 @@
 // Relative-position MHA forward over PREPARED bf16 operands (the single-pass / lse-only form the bwd2 backward
-// and inference use): the same arithmetic as relpos_attn_fwd_kernel<false, NU, false> (attn_fused.hip) -- same
-// bf16 operands, same MFMAs in the same order, same online softmax and counter-RNG dropout, so O and lse are
-// bitwise that kernel's -- restaged for occupancy:
+// and inference use): the operands, MFMAs and counter-RNG dropout mask of relpos_attn_fwd_kernel<false, NU, false>
+// (attn_fused.hip) with the online softmax in the exp2 domain (O within 1e-3, lse within 2e-6 of that kernel's),
+// restaged for occupancy:
 //   * kdfm_attn_kv_prep writes each utterance's centred keys / values (attn_centre.h) ONCE as bf16 tiles
-//     [b, h][key][c] with the LDS row stride (head dim padded to 32 KS, + 8), and the value centre;
+//     [b, h][key][c] with the LDS row stride (head dim padded to 48 / 64 / 128, + 8), and the value centre;
 //     kdfm_attn_band_prep every layer's projected positions as bf16 rows [layer, h][64 + r][c] with zero rows
 //     around them.  Every operand tile of a (64 queries, 64 keys) step is then ONE contiguous byte range
 //     (K 64 rows, V 64 rows, the Ppos band 128 rows from r = T-1-(i0+63)+j0), copied into LDS by LDS-DMA
@@ -13,8 +13,9 @@
 //     Qv Pband^T with ds_bpermute (5 per row register) instead of an f32 G tile written to and read back from
 //     LDS (20.7 KB per workgroup and two wave syncs per key block).
 //   * P V reads V [key][c] transposed (ds_read_b64_tr_b16) instead of a transposed V^T image.
-// LDS per workgroup: 46 KB at head dim <= 64, 79 KB at 128; head dim <= 48 fits 3 workgroups (12 waves) per CU
-// in 168 registers (the register-staged kernel: 67 KB, 2 workgroups).
+//   * each wave's P^T tile [64 keys][16 rows] goes into the band region once the score MFMAs have read it.
+// LDS per workgroup (K | V | band): 28 KB at head dim <= 48 (4 workgroups, 16 waves per CU, 117 registers),
+// 36 KB at <= 64, 68 KB at 128 (the register-staged kernel: 67 KB, 2 workgroups).
 #include "gemm_common.h"
 #include "attn_centre.h"
 
