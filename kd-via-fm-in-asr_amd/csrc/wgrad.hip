@@ -624,7 +624,7 @@ bool wr_plan(const GemmP& p, int amode, int bmode, int64_t batch, WrPlan& pl, bo
   pl.slices = ceil_div(Nb_all, 24);
   if (nseg > 1 && pl.slices != 1) return false;   // the segment columns live in the one slice
   const int64_t ncols_slice = ceil_div(Nb_all, pl.slices) * 16;
-  // short reductions (the 12,832-row Conformer products: S is capped by min_steps, ~100 splits)
+  // short reductions (the 12,832-row Conformer products: S is capped by min_steps, 66 splits)
   // leave most of the 256 CUs idle; slice the output rows too, so every CU gets a workgroup while
   // each workgroup's partial (and the fold's input) shrinks with its slice
   const int64_t steps = ceil_div(p.K, 32);
@@ -637,7 +637,10 @@ bool wr_plan(const GemmP& p, int amode, int bmode, int64_t batch, WrPlan& pl, bo
   // workgroups so the compute stream's heads kernels keep CUs beside them (KDFM_WGR_CONV_WGS)
   static const int target_conv = env_i("KDFM_WGR_CONV_WGS", target_all);
   const int target = bmode == KDFM_LD_CONV ? target_conv : target_all;
-  static const int min_steps = env_i("KDFM_WGR_STEPS", 4);
+  // at least 6 32-row steps per split: the 12 832-row products take 66 splits (4 -> 100 splits: 2303-2309 utt/s,
+  // 6: 2318-2325, 8: 2316-2318, 12: 2255, 16: 2150 -- profiles/r05/r5zh, r5zi; fewer partial bytes until the
+  // longer per-workgroup chains delay the weight-gradient stream's tail)
+  static const int min_steps = env_i("KDFM_WGR_STEPS", 6);
   // off by default: isolated the slices help (FFN W1 25 -> 19 us) but in the step the extra
   // workgroups queue behind the critical-path kernels (bench 1687 unsliced vs 1635 sliced at
   // target 256, profiles/r02/envab_*.log).  Read per call: tests compare sliced / unsliced.

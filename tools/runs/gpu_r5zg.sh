@@ -4,12 +4,15 @@ set -o pipefail
 OUT=gpurun_out/r5zg
 mkdir -p $OUT
 run() {
-  KDFM_PLAN_KNOCKOUT="$1" timeout -k 10 200 python3 -u bench.py --steps 15 --warmup 3 --no-cpu-baseline --no-f32-sensitivity > $OUT/run.log 2>&1 || { echo "run failed: $1"; tail -5 $OUT/run.log; exit 3; }
+  KDFM_PLAN_KNOCKOUT="$1" timeout -k 10 200 python3 -u bench.py --steps 15 --warmup 3 --no-cpu-baseline --no-f32-sensitivity > $OUT/run.log 2>&1
+  rc=$?
+  # a Python error (rc 1) is reported and the probe goes on; a crash, abort or time limit ends the call
+  [ $rc -le 1 ] || { echo "run died ($rc): $1"; tail -5 $OUT/run.log; exit 3; }
+  [ $rc -eq 0 ] || { echo "run failed: $1"; tail -2 $OUT/run.log; }
   grep KNOCKOUT $OUT/run.log || tail -1 $OUT/run.log | cut -c1-200
 }
 run ""
 run kdfm_wgrad_bf16,kdfm_wgrad_bf16_pair,kdfm_wgrad_fold_flush,kdfm_wgrad_bf16_seg,kdfm_wgrad_bf16_conv
-run kdfm_wgrad_fold_flush
 run kdfm_relpos_attn_fwd3,kdfm_attn_kv_prep
 run kdfm_relpos_attn_bwd2_dq3,kdfm_relpos_attn_bwd2_dkv,kdfm_relpos_attn_bwd2_dpos
 run kdfm_ffn_fwd
