@@ -187,6 +187,19 @@ int64_t kdfm_wgrad_bf16_conv_ws(int64_t rows, int64_t M, int64_t C, int32_t taps
 int kdfm_wgrad_bf16_conv(const uint16_t* dY, const uint16_t* X, float* dW, int64_t ldc, float* db, int64_t rows,
                          int64_t M, int64_t C, int32_t taps, int32_t pad, int64_t T, float alpha, float* ws,
                          int64_t ws_len, void* stream);
+/* The striding subsampling's second conv (Conv2d(C, C, 3, stride 2, padding 1), conformer_encoder.py:381-390,
+ * subsampling.py ConvSubsampling) weight gradient straight from its bf16 input, no column matrix:
+ *   dW[m][tap*C + c] += alpha * sum_{b,t2,f2} dY[(b,t2,f2)][m] * X[b][2 t2 - 1 + tap / 3][2 f2 - 1 + tap % 3][c]
+ *   db[m] += alpha * sum dY[.][m]
+ * X (B, T1, F1, C) bf16 channels-last, zero outside it and (len_in != NULL) at frames >= len_in[b];
+ * dY (B*T2*F2, C) bf16, T2 = (T1-1)/2+1, F2 = (F1-1)/2+1; dW (C, 9C) tap-major (kdfm_convw_grad re-lays it
+ * out).  The same sums, split plan and fold order as kdfm_wgrad_bf16 over kdfm_im2col_3x3s2_tm_from_bf16's
+ * columns (bitwise equal), without the column matrix's 9/4 x |X| write and read.  C % 8 == 0, F1 >= 7;
+ * ws: kdfm_wgrad_bf16_s2conv_ws floats (deferred folds apply). */
+int64_t kdfm_wgrad_bf16_s2conv_ws(int64_t B, int64_t T1, int64_t F1, int64_t C);
+int kdfm_wgrad_bf16_s2conv(const uint16_t* dY, const uint16_t* X, const int64_t* len_in, float* dW, float* db,
+                           int64_t B, int64_t T1, int64_t F1, int64_t C, float alpha, float* ws, int64_t ws_len,
+                           void* stream);
 /* Deferred folds of the row-parallel weight gradients (kdfm_wgrad_bf16 / _pair / _seg / _conv / _dev), per
  * stream: after kdfm_wgrad_set_fold_arena(stream, arena, len) the products issued on `stream` write their
  * per-split partials into `arena` (len floats, caller-owned, 16-byte aligned; ws is then unused) and queue

@@ -33,6 +33,10 @@ struct GemmP {
   // row-parallel wgrad, paired launch: a second product of the same shape (dY2, X2 -> C2 / ones_out2,
   // partials in ws2) in the same grid (blocks [S, 2S) and the fold's blockIdx.y == 1); A2 == NULL: none
   const float* A2; const float* B2; float* C2; float* ones_out2; float* ws2;
+  // row-parallel wgrad, 3x3 stride-2 conv gather (kdfm_wgrad_bf16_s2conv): B column n = tap * conv_c + c of row
+  // (b, t2, f2) reads X[b][2 t2 - 1 + tap / 3][2 f2 - 1 + tap % 3][c] of a (B, c2_T1, c2_F1, conv_c) image, zero
+  // outside it and at frames >= c2_len[b] (c2_len NULL: no length mask)
+  int64_t c2_T1, c2_F1, c2_T2, c2_F2; const int64_t* c2_len;
 };
 
 // Non-atomic epilogue for one output element.  v = alpha * acc (already scaled).  bz = batch

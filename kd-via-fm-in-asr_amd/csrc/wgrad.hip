@@ -62,8 +62,11 @@ struct WrGeo {
 // 4 rows x 4 columns (8-byte loads); BIN = 2 (every column count a multiple of 8): 4 rows x 8 columns,
 // 16-byte loads as in the f32 mode -- half the load instructions and half the units per slab, so
 // the slab fits one unit per thread and two slabs stay in flight.
-template <int MBW, int NBW, bool CONV, int PD, int UPT, int BIN = 0>
+// C2D (BIN == 2 only): the B operand is gathered from a 3x3 stride-2 conv input (GemmP::c2_*) instead of a
+// column matrix -- the striding subsampling's conv2 weight gradient without im2col
+template <int MBW, int NBW, bool CONV, int PD, int UPT, int BIN = 0, bool C2D = false>
 __global__ __launch_bounds__(WR_NT, 2) void wgr_kernel(GemmP p, WrGeo g) {
+  static_assert(!C2D || (BIN == 2 && !CONV), "the conv gather stages 8-column bf16 units");
   constexpr int ES = BIN ? 2 : 4;   // element size in memory
   constexpr int CW = BIN == 2 ? 8 : 4;   // columns per staging unit
   constexpr int CWS = BIN == 2 ? 3 : 2;  // log2(CW)
@@ -138,6 +141,15 @@ __global__ __launch_bounds__(WR_NT, 2) void wgr_kernel(GemmP p, WrGeo g) {
   int64_t ld[UPT];        // row stride in bytes
   int tfr[UPT], toff[UPT];   // CONV: frame of the unit's first row in its utterance; tap - pad
   bool act[UPT];
+  // C2D B units: tap offsets, channel and the (utterance, t2, f2) position of the unit's first row
+  int c2ky[UPT], c2kx[UPT], c2c[UPT], c2f[UPT], c2t[UPT], c2b[UPT];
+  int c2l0[UPT], c2l1[UPT];   // frame limits of utterances c2b and c2b + 1 (a slab's rows span at most two)
+  bool c2u[UPT];
+  auto c2lim = [&](int bb) -> int {
+    const int64_t nb = p.K / (p.c2_T2 * p.c2_F2);
+    if (bb >= nb) return 0;
+    return (int)(p.c2_len ? min(p.c2_len[bb], p.c2_T1) : p.c2_T1);
+  };
 #pragma unroll
   for (int i = 0; i < UPT; ++i) {
     const int u = threadIdx.x + i * WR_NT;
@@ -147,6 +159,8 @@ __global__ __launch_bounds__(WR_NT, 2) void wgr_kernel(GemmP p, WrGeo g) {
     tfr[i] = 0;
     toff[i] = 0;
     acol[i] = 1 << 30;
+    c2u[i] = false;
+    c2ky[i] = c2kx[i] = c2c[i] = c2f[i] = c2t[i] = c2b[i] = c2l0[i] = c2l1[i] = 0;
     if (cg < ma4) {
       src[i] = reinterpret_cast<const char*>(pA) + ES * (r0 * p.sAk + m0 + cg * CW);
       ld[i] = ES * p.sAk;
@@ -159,6 +173,19 @@ __global__ __launch_bounds__(WR_NT, 2) void wgr_kernel(GemmP p, WrGeo g) {
         toff[i] = (int)(tap - p.pad);
         tfr[i] = (int)(r0 % p.conv_t);
         src[i] = reinterpret_cast<const char*>(pB) + ES * ((r0 + toff[i]) * p.sBk + c);
+      } else if constexpr (C2D) {
+        const int64_t tap = n / p.conv_c;
+        ld[i] = 0;
+        c2u[i] = true;
+        c2ky[i] = (int)(tap / 3);
+        c2kx[i] = (int)(tap - 3 * (tap / 3));
+        c2c[i] = (int)(n - tap * p.conv_c);
+        c2f[i] = (int)(r0 % p.c2_F2);
+        c2t[i] = (int)((r0 / p.c2_F2) % p.c2_T2);
+        c2b[i] = (int)(r0 / (p.c2_F2 * p.c2_T2));
+        c2l0[i] = c2lim(c2b[i]);
+        c2l1[i] = c2lim(c2b[i] + 1);
+        src[i] = reinterpret_cast<const char*>(pB);
       } else {
         src[i] = reinterpret_cast<const char*>(pB) + ES * (r0 * p.sBk + n);
       }
@@ -188,6 +215,24 @@ __global__ __launch_bounds__(WR_NT, 2) void wgr_kernel(GemmP p, WrGeo g) {
           }
         }
         const char* q = ok ? src[i] + j * ld[i] : reinterpret_cast<const char*>(pB);   // any valid, aligned address
+        if constexpr (C2D) {
+          if (c2u[i]) {   // output position of row j -> the tap's input position (zero outside / past len)
+            int f2 = c2f[i] + j, t2 = c2t[i], bb = c2b[i];
+            if (f2 >= (int)p.c2_F2) {
+              f2 -= (int)p.c2_F2;
+              if (++t2 >= (int)p.c2_T2) {
+                t2 = 0;
+                ++bb;
+              }
+            }
+            const int t1 = 2 * t2 - 1 + c2ky[i], f1 = 2 * f2 - 1 + c2kx[i];
+            const int lim = bb == c2b[i] ? c2l0[i] : c2l1[i];
+            ok = ok && t1 >= 0 && t1 < lim && f1 >= 0 && f1 < p.c2_F1;
+            q = ok ? reinterpret_cast<const char*>(pB) +
+                         ES * ((((int64_t)bb * p.c2_T1 + t1) * p.c2_F1 + f1) * p.conv_c + c2c[i])
+                   : reinterpret_cast<const char*>(pB);
+          }
+        }
         if constexpr (BIN == 1) {
           const uint2 t = *reinterpret_cast<const uint2*>(q);
           r[i][j] = make_float4(__builtin_bit_cast(float, t.x), __builtin_bit_cast(float, t.y), 0.f, 0.f);
@@ -211,6 +256,18 @@ __global__ __launch_bounds__(WR_NT, 2) void wgr_kernel(GemmP p, WrGeo g) {
       if constexpr (CONV) {
         tfr[i] += 32;
         while (tfr[i] >= T) tfr[i] -= T;
+      }
+      if constexpr (C2D) {   // the next slab's first row
+        c2f[i] += 32;
+        while (c2f[i] >= (int)p.c2_F2) {
+          c2f[i] -= (int)p.c2_F2;
+          if (++c2t[i] >= (int)p.c2_T2) {
+            c2t[i] = 0;
+            ++c2b[i];
+            c2l0[i] = c2l1[i];
+            c2l1[i] = c2lim(c2b[i] + 1);   // needed from the next slab on: the wait lands there
+          }
+        }
       }
     }
   };
@@ -584,6 +641,10 @@ struct WdGeo {
   int aimg, slab;        // bf16 elements of the (1 KB padded) dY image and of one slab buffer
 };
 
+// private B-operand mode of the row-parallel kernel: the 3x3 stride-2 conv gather (GemmP::c2_*)
+constexpr int WR_LD_C2D = 16;
+inline int64_t nmem_c2d(const GemmP& p) { return p.ones_col >= 0 ? p.ones_col : p.N; }
+
 struct WrPlan {
   WrPick w;
   WrGeo g;
@@ -604,7 +665,10 @@ bool wr_plan(const GemmP& p, int amode, int bmode, int64_t batch, WrPlan& pl, bo
   static const int enabled = env_i("KDFM_WGR", 1);
   if (!enabled && !force) return false;
   if (batch != 1 || p.epi != KDFM_EPI_ATOMIC || amode != KDFM_LD_XC) return false;
-  if (bmode != KDFM_LD_XC && bmode != KDFM_LD_CONV) return false;
+  if (bmode != KDFM_LD_XC && bmode != KDFM_LD_CONV && bmode != WR_LD_C2D) return false;
+  if (bmode == WR_LD_C2D && (!bf16in || (p.conv_c & 7) || p.M % 8 || p.sAk % 8 || nmem_c2d(p) != 9 * p.conv_c ||
+                             p.c2_T2 != (p.c2_T1 - 1) / 2 + 1 || p.c2_F2 != (p.c2_F1 - 1) / 2 + 1 || p.c2_F2 < 4))
+    return false;
   // f32 A rows that are not 16-byte aligned (or M % 4 != 0): scalar A staging (WrGeo::ascal)
   const bool ascal = !bf16in && ((p.sAk & 3) || (p.M & 3) || (((uintptr_t)p.A) & 15));
   if (p.sAm != 1 || (bf16in && ((p.sAk & 3) || (p.M & 3) || (((uintptr_t)p.A) & 15)))) return false;
@@ -661,6 +725,7 @@ bool wr_plan(const GemmP& p, int amode, int bmode, int64_t batch, WrPlan& pl, bo
   pl.bin = !bf16in ? 0
            : (bin8 && p.M % 8 == 0 && nmem % 8 == 0 && p.sAk % 8 == 0 && p.sBk % 8 == 0 &&
               (bmode != KDFM_LD_CONV || p.conv_c % 8 == 0)) ? 2 : 1;
+  if (bmode == WR_LD_C2D && pl.bin != 2) return false;
   const int cw = pl.bin == 2 ? 8 : 4;
   pl.g.wm = pl.w.wm;
   pl.g.wn = pl.w.wn;
@@ -683,7 +748,7 @@ bool wr_plan(const GemmP& p, int amode, int bmode, int64_t batch, WrPlan& pl, bo
   return true;
 }
 
-template <int MBW, int NBW, bool CONV, int BIN = 0>
+template <int MBW, int NBW, bool CONV, int BIN = 0, bool C2D = false>
 int wr_launch(const GemmP& p, const WrPlan& pl, hipStream_t st) {
   static const int pd = env_i("KDFM_WGR_PD", 2);
   auto go = [&](auto kern) {
@@ -696,12 +761,12 @@ int wr_launch(const GemmP& p, const WrPlan& pl, hipStream_t st) {
                        dim3(WR_NT), pl.lds, st, p, pl.g);
   };
   if (pl.upt <= 1) {
-    if (pd >= 2) go(wgr_kernel<MBW, NBW, CONV, 2, 1, BIN>); else go(wgr_kernel<MBW, NBW, CONV, 1, 1, BIN>);
+    if (pd >= 2) go(wgr_kernel<MBW, NBW, CONV, 2, 1, BIN, C2D>); else go(wgr_kernel<MBW, NBW, CONV, 1, 1, BIN, C2D>);
   } else {
     // two slabs of two units each next to an 18-block accumulator tile exceed the 256 registers of
     // a 2-waves-per-SIMD wave (spills): one slab in flight there
-    if (pd >= 2 && MBW * NBW < 18) go(wgr_kernel<MBW, NBW, CONV, 2, 2, BIN>);
-    else go(wgr_kernel<MBW, NBW, CONV, 1, 2, BIN>);
+    if (pd >= 2 && MBW * NBW < 18) go(wgr_kernel<MBW, NBW, CONV, 2, 2, BIN, C2D>);
+    else go(wgr_kernel<MBW, NBW, CONV, 1, 2, BIN, C2D>);
   }
   return check_launch("kdfm_gemm(wgrad rows)");
 }
@@ -1080,6 +1145,17 @@ namespace {
 template <int BIN>
 int wr_dispatch(const GemmP& p, const WrPlan& pl, int bmode, hipStream_t st) {
   const int key = pl.w.mbw * 10 + pl.w.nbw;
+  if constexpr (BIN == 2) {
+    if (bmode == WR_LD_C2D) {
+      switch (key) {
+        case 32: return wr_launch<3, 2, false, 2, true>(p, pl, st);
+        case 33: return wr_launch<3, 3, false, 2, true>(p, pl, st);
+        case 34: return wr_launch<3, 4, false, 2, true>(p, pl, st);
+        case 36: return wr_launch<3, 6, false, 2, true>(p, pl, st);
+        default: return wr_launch<6, 3, false, 2, true>(p, pl, st);
+      }
+    }
+  }
   if (bmode == KDFM_LD_CONV) {
     switch (key) {
       case 32: return wr_launch<3, 2, true, BIN>(p, pl, st);
@@ -1222,6 +1298,29 @@ int kdfm_wgrad_bf16(const uint16_t* dY, const uint16_t* X, float* dW, int64_t ld
   KDFM_REQUIRE(ldc >= N, "ldc < N");
   GemmP p = wgrad_bf16_params(dY, X, dW, ldc, db, rows, M, N, alpha, ws, ws_len);
   return wgrad_bf16_run(p, KDFM_LD_XC, as_stream(stream));
+}
+
+int64_t kdfm_wgrad_bf16_s2conv_ws(int64_t B, int64_t T1, int64_t F1, int64_t C) {
+  const int64_t T2 = (T1 - 1) / 2 + 1, F2 = (F1 - 1) / 2 + 1;
+  return kdfm_wgrad_bf16_ws(B * T2 * F2, C, 9 * C, 1);
+}
+
+int kdfm_wgrad_bf16_s2conv(const uint16_t* dY, const uint16_t* X, const int64_t* len_in, float* dW, float* db,
+                           int64_t B, int64_t T1, int64_t F1, int64_t C, float alpha, float* ws, int64_t ws_len,
+                           void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(dY && X && dW && db && ws, "null pointer");
+  KDFM_REQUIRE(B > 0 && T1 > 0 && F1 >= 7 && C > 0 && C % 8 == 0, "B, T1 > 0, F1 >= 7, C a positive multiple of 8");
+  KDFM_REQUIRE(((((uintptr_t)dY) | ((uintptr_t)X)) & 15) == 0, "operands must be 16-byte aligned");
+  const int64_t T2 = (T1 - 1) / 2 + 1, F2 = (F1 - 1) / 2 + 1;
+  GemmP p = wgrad_bf16_params(dY, X, dW, 9 * C, db, B * T2 * F2, C, 9 * C, alpha, ws, ws_len);
+  p.conv_c = C;
+  p.c2_T1 = T1;
+  p.c2_F1 = F1;
+  p.c2_T2 = T2;
+  p.c2_F2 = F2;
+  p.c2_len = len_in;
+  return wgrad_bf16_run(p, WR_LD_C2D, as_stream(stream));
 }
 
 int kdfm_wgrad_bf16_pair(const uint16_t* dY, const uint16_t* X, float* dW, float* db, const uint16_t* dY2,

@@ -121,6 +121,8 @@ SIGNATURES: dict[str, tuple] = {
     "kdfm_wgrad_bf16_seg_ws": (_i64, [_i64, _i64, _i64, _i64]),
     "kdfm_wgrad_bf16_seg": (_i32, [P, P, P, _i64, P, _i64, _i64, _i64, _i64, _f32, P, _i64, P]),
     "kdfm_wgrad_bf16_conv_ws": (_i64, [_i64, _i64, _i64, _i32, _i32, _i64, _i32]),
+    "kdfm_wgrad_bf16_s2conv_ws": (_i64, [_i64, _i64, _i64, _i64]),
+    "kdfm_wgrad_bf16_s2conv": (_i32, [P, P, P, P, P, _i64, _i64, _i64, _i64, _f32, P, _i64, P]),
     "kdfm_wgrad_bf16_conv": (_i32, [P, P, P, _i64, P, _i64, _i64, _i64, _i32, _i32, _i64, _f32, P, _i64, P]),
     "kdfm_wgrad_set_fold_arena": (_i32, [P, P, _i64]),
     "kdfm_wgrad_fold_flush": (_i32, [P]),

@@ -212,6 +212,8 @@ def dw_subsampling_backward(cfg, S: EncoderShapes, P, G, pre, ctx, dx, *, seed, 
 # KDFM_SS_ONE_KERNEL=0: the two-kernel striding forward (conv1 to HBM, implicit-GEMM conv2) instead of the
 # one-kernel form
 _SS_ONE_KERNEL = __import__("os").environ.get("KDFM_SS_ONE_KERNEL", "1") == "1"
+# KDFM_SS_WGRAD_GATHER=0: the conv2 weight gradient over an im2col column matrix instead of the direct gather
+_SS_WGRAD_GATHER = __import__("os").environ.get("KDFM_SS_WGRAD_GATHER", "1") == "1"
 # KDFM_SIDE_FOLDS=1: the LayerNorm / depthwise folds and the subsampling output's weight gradient go to the
 # weight-gradient stream (=0, default: they stay on the compute stream -- measured 2111 / 2116 vs 2074 / 2095
 # utt/s, profiles/r04/r4v: the extra launches there delay the compute stream's dispatch more than they save)
@@ -301,24 +303,33 @@ def subsampling_backward(cfg, S: EncoderShapes, P, G, pre, ctx, dx, len1, *, see
     else:
         dy2 = _out_linear_backward(S, P, G, pre, ctx, dx, ctx["y2"], seed=seed, salt=salt, ws=ws)
     if direct:
-        # conv2 weight gradient on the weight-gradient stream from bf16 operands: tap-major bf16
-        # columns of y1 (half the bytes of the f32 im2col) and the bf16 dy2, one row-parallel
-        # launch into (C, 9, C) then re-laid out into (C, C, 3, 3)
-        cols1 = torch.empty(B * S.T * S.F2, 9 * C, device=dev, dtype=torch.bfloat16)
+        # conv2 weight gradient on the weight-gradient stream from bf16 operands and the bf16 dy2, one
+        # row-parallel launch into (C, 9, C) then re-laid out into (C, C, 3, 3): gathered straight from the
+        # bf16 y1 (kdfm_wgrad_bf16_s2conv) when the fused forward kept it so, else over tap-major bf16
+        # columns of y1 (KDFM_SS_WGRAD_GATHER=0: the column matrix, 9/4 x |y1| written and read back)
+        y1 = ctx["y1"]
+        gather = _SS_WGRAD_GATHER and y1.dtype == torch.bfloat16 and C % 8 == 0 and S.F1 >= 7
+        cols1 = None if gather else torch.empty(B * S.T * S.F2, 9 * C, device=dev, dtype=torch.bfloat16)
         cast = dy2h is None
         if cast:
             dy2h = torch.empty(B * S.T * S.F2, C, device=dev, dtype=torch.bfloat16)
         gtm = ws["w2_tapmajor_grad"]
+        lin = len1 if cfg.subsampling_mask else None
 
         def conv2_wgrad():
-            K.im2col_3x3s2_tm_bf16(ctx["y1"], len1 if cfg.subsampling_mask else None, cols1, B, S.T1, S.F1, C)
+            if not gather:
+                K.im2col_3x3s2_tm_bf16(y1, lin, cols1, B, S.T1, S.F1, C)
             if cast:
                 K.cast_bf16(dy2, dy2h)
             K.fill(gtm, 0.0)
-            K.wgrad_bf16(dy2h, cols1, gtm.view(C, 9 * C), db=G[pre + "pre_encode.conv.2.bias"])
+            if gather:
+                K.wgrad_bf16_s2conv(dy2h, y1, lin, gtm.view(C, 9 * C), G[pre + "pre_encode.conv.2.bias"], B, S.T1,
+                                    S.F1, C)
+            else:
+                K.wgrad_bf16(dy2h, cols1, gtm.view(C, 9 * C), db=G[pre + "pre_encode.conv.2.bias"])
             K.wgrad_fold_flush()   # gtm is read below (deferred folds, fold_arena)
             K.convw_grad(gtm.view(C, 9 * C), G[pre + "pre_encode.conv.2.weight"].view(C, C, 9))
-        WGRAD.run(conv2_wgrad, *(t for t in (dy2, cols1, dy2h, ctx["y1"], len1) if t is not None))
+        WGRAD.run(conv2_wgrad, *(t for t in (dy2, cols1, dy2h, y1, len1) if t is not None))
     else:
         if ctx["y1"] is not None and ctx["y1"].dtype == torch.bfloat16:   # fused forward kept only the bf16 y1
             ctx["y1"] = ctx["y1"].float()

@@ -1003,6 +1003,23 @@ def wgrad_bf16_conv(dY, X, dW, T, *, taps=3, pad=1, db=None, alpha=1.0):
          taps, pad, T, float(alpha), ptr(ws), ws.numel(), _s())
 
 
+def wgrad_bf16_s2conv(dY, X, len_in, dW, db, B, T1, F1, C, *, alpha=1.0):
+    """Striding subsampling conv2 weight gradient straight from its bf16 input X (B, T1, F1, C) (no column
+    matrix): dW (C, 9C) tap-major += alpha * sum dY[(b,t2,f2), m] X[b, 2t2-1+tap//3, 2f2-1+tap%3, c], db += colsum."""
+    T2, F2 = (T1 - 1) // 2 + 1, (F1 - 1) // 2 + 1
+    rows = B * T2 * F2
+    assert dY.shape == (rows, C) and X.numel() == B * T1 * F1 * C and dW.shape == (C, 9 * C) and dW.is_contiguous()
+    assert dY.is_contiguous() and X.is_contiguous() and db is not None
+    n = int(_lib.lib().kdfm_wgrad_bf16_s2conv_ws(B, T1, F1, C))
+    if n < 0:
+        raise _lib.KdfmError(f"kdfm_wgrad_bf16_s2conv: unsupported shape B={B} T1={T1} F1={F1} C={C}")
+    ws = scratch(dY.device, n)
+    # algorithmic bytes: dY and X once (bf16), the f32 gradient read + written
+    _traced("wgrad_bf16", 2.0 * rows * C * 9 * C, 2.0 * (rows * C + B * T1 * F1 * C) + 8.0 * 9 * C * C,
+            "kdfm_wgrad_bf16_s2conv", ptr(_bf16(dY)), ptr(_bf16(X)), ptr(_i64(len_in)), ptr(_f32(dW)), ptr(_f32(db)),
+            B, T1, F1, C, float(alpha), ptr(ws), ws.numel(), _s())
+
+
 def denoise_chain_fwd(z, W1, b1, W2, b2, X, A, out, T, S):
     """Fused SimpleDenoiser forward (S steps) over utterances of T frames; W1/W2 Conv1d (L, L, 3)."""
     n, L = z.shape

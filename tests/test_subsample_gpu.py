@@ -226,6 +226,40 @@ def test_im2col_tapmajor_bf16_matches_f32_im2col(K):
     assert torch.equal(got, want)
 
 
+@pytest.mark.parametrize("B,T1,F1,C,masked", [(3, 41, 40, 88, True), (2, 37, 39, 88, False), (4, 9, 7, 32, True),
+                                              (2, 401, 39, 88, True)])
+def test_s2conv_wgrad_gather_equals_im2col(K, B, T1, F1, C, masked):
+    """kdfm_wgrad_bf16_s2conv (the conv2 weight gradient gathered straight from the bf16 y1) = kdfm_wgrad_bf16
+    over kdfm_im2col_3x3s2_tm_from_bf16's column matrix, bit for bit (same split plan and fold order), with
+    and without the len_in frame mask, and with the folds deferred to an arena."""
+    g = torch.Generator().manual_seed(11 + T1)
+    T2, F2 = _lens(T1), _lens(F1)
+    rows = B * T2 * F2
+    X = torch.randn(B * T1 * F1, C, generator=g).bfloat16().cuda()
+    dY = torch.randn(rows, C, generator=g).bfloat16().cuda()
+    lin = torch.tensor([T1 - 3 * b if T1 - 3 * b > 0 else 1 for b in range(B)], dtype=torch.int64).cuda() if masked \
+        else None
+    cols = torch.empty(rows, 9 * C, device="cuda", dtype=torch.bfloat16)
+    K.im2col_3x3s2_tm_bf16(X, lin, cols, B, T1, F1, C)
+    dW0 = torch.randn(C, 9 * C, generator=g).cuda()
+    db0 = torch.randn(C, generator=g).cuda()
+    dW1, db1 = dW0.clone(), db0.clone()
+    K.wgrad_bf16(dY, cols, dW0, db=db0)
+    K.wgrad_bf16_s2conv(dY, X, lin, dW1, db1, B, T1, F1, C)
+    torch.cuda.synchronize()
+    assert torch.equal(dW1, dW0) and torch.equal(db1, db0)
+    dW2, db2 = dW0.clone(), db0.clone()
+    arena = torch.empty(1 << 24, device="cuda")
+    K.wgrad_set_fold_arena(arena)
+    K.wgrad_bf16_s2conv(dY, X, lin, dW2, db2, B, T1, F1, C)
+    K.wgrad_fold_flush()
+    K.wgrad_set_fold_arena(None)
+    dW3, db3 = dW0.clone(), db0.clone()
+    K.wgrad_bf16(dY, cols, dW3, db=db3)
+    torch.cuda.synchronize()
+    assert torch.equal(dW2, dW3) and torch.equal(db2, db3)
+
+
 @pytest.mark.parametrize("C,Tm,Fm", [(88, 801, 80), (88, 75, 27), (32, 61, 80), (64, 13, 9)])
 def test_subsample_dgrad_fused_conv0_wgrad(K, C, Tm, Fm):
     """kdfm_subsample_conv2_dgrad_w0: conv0's weight / bias gradient accumulated in the conv2 data
