@@ -22,6 +22,17 @@ __device__ __forceinline__ float lse2(float a, float b) {
   return m + log1pf(__expf(-fabsf(a - b)));
 }
 
+// the CTC recursions' log-add on the hardware exp / log (v_exp_f32, v_log_f32), branch-free: a frame of the
+// alpha / beta chain is this function twice per state, so its latency is the recursion's.  log(1 + e) for
+// e = exp(-|a - b|) in (0, 1] differs from log1pf(e) by < 1e-7 absolute, below the f32 resolution of the
+// running sums (|alpha| ~ 1e2..1e3); an operand of -inf returns the other exactly (e = 0, log(1) = 0)
+__device__ __forceinline__ float lse2_fast(float a, float b) {
+  const float m = fmaxf(a, b);
+  const float e = __expf(fminf(a, b) - m);
+  const float r = m + __logf(1.f + e);
+  return m == NEG_INF ? NEG_INF : r;
+}
+
 // one wave per row, NV = ceil(C / 64) values per lane in registers (vocabularies up to 4096 classes:
 // the decoder width V+1 comes from the teacher's tokenizer, conformer_ctc_bpe.yaml:87)
 template <int NV>
@@ -103,7 +114,7 @@ __global__ __launch_bounds__(256) void log_softmax_bwd_kernel(const float* __res
 //  ctc_grad_kernel, grid (B, ceil(T / CTC_FPB)): posteriors and the logits gradient, independent
 //    across frames.  Workspaces alpha / beta (B, T, 2 Umax + 1) in log space; nll (B);
 //    grad (B, T, C) = scale * (exp(lp) - posterior) for t < len, 0 beyond (all 0 / NaN if infeasible).
-// Same recursions, the same lse2 order and the same fixed-order posterior sums as a single-block
+// Same recursions, the same log-add order and the same fixed-order posterior sums as a single-block
 // formulation: the result is bitwise reproducible.
 constexpr int CTC_FPB = 4;
 
@@ -186,12 +197,13 @@ __global__ __launch_bounds__(1024) void ctc_ab_kernel(const float* __restrict__ 
           av[k][j] = NEG_INF;
           if (s < S) {
             float a = cur[s];
+            // branch-free: a missing predecessor enters as -inf (lse2_fast(a, -inf) == a exactly)
             if (!bwd) {
-              if (s >= 1) a = lse2(a, cur[s - 1]);
-              if (skip[k]) a = lse2(a, cur[s - 2]);
+              a = lse2_fast(a, s >= 1 ? cur[s >= 1 ? s - 1 : 0] : NEG_INF);
+              a = lse2_fast(a, skip[k] ? cur[s >= 2 ? s - 2 : 0] : NEG_INF);
             } else {
-              if (s + 1 < S) a = lse2(a, cur[s + 1]);
-              if (skip[k]) a = lse2(a, cur[s + 2]);
+              a = lse2_fast(a, s + 1 < S ? cur[s + 1] : NEG_INF);
+              a = lse2_fast(a, skip[k] ? cur[s + 2 < S ? s + 2 : s] : NEG_INF);
             }
             const float v = (a == NEG_INF) ? NEG_INF : a + em[k][j];
             nxt[s] = v;
