@@ -4,6 +4,7 @@
 //   from ctc_models.py:81-85) with its logits gradient exp(lp) - posterior,
 //   logit KD (asr_train_diffm.py:751-756: kl_div(log_softmax(s/T), softmax(t/T), 'batchmean') * T^2),
 //   and the final loss assembly (asr_train_diffm.py:803-811).
+#include <climits>
 #include <math.h>
 
 #include <type_traits>
@@ -272,19 +273,28 @@ __global__ __launch_bounds__(256) void ctc_grad_kernel(const float* __restrict__
   __shared__ float blank_sh;
   const float* lpb = lp + b * T * C;
   for (int64_t s = threadIdx.x; s < S; s += blockDim.x) lab[s] = ctc_label(targets + b * Umax, s, blank);
+  for (int c = threadIdx.x; c < C; c += blockDim.x) head[c] = INT_MAX;
   __syncthreads();
-  // per-label position lists: the posterior of class c is summed over its positions in ascending
-  // order, a fixed order (no LDS atomics), so the logits gradient is bitwise reproducible
-  if (threadIdx.x == 0) {
-    for (int c = 0; c < C; ++c) head[c] = -1;
-    for (int64_t s = S - 2; s >= 1; s -= 2) {
-      const int l = lab[s];
-      if (l >= 0 && l < C) {
-        nxt[s] = head[l];
-        head[l] = (int)s;
-      }
+  // per-label position lists: the posterior of class c is summed over its positions in ascending order, a
+  // fixed order, so the logits gradient is bitwise reproducible.  Built in parallel: head[c] = the first odd
+  // position of label c (an LDS atomic min: order-free), nxt[s] = the next odd position after s with the
+  // same label (a forward scan per position) -- one thread walking all positions cost ~6 us per block
+  for (int64_t s = 2 * threadIdx.x + 1; s < S; s += 2 * blockDim.x) {
+    const int l = lab[s];
+    if (l >= 0 && l < C) {
+      atomicMin(&head[l], (int)s);
+      int nx = -1;
+      for (int64_t s2 = s + 2; s2 < S; s2 += 2)
+        if (lab[s2] == l) {
+          nx = (int)s2;
+          break;
+        }
+      nxt[s] = nx;
     }
   }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += blockDim.x)
+    if (head[c] == INT_MAX) head[c] = -1;
   __syncthreads();
   for (int64_t t = t0; t < tv; ++t) {
     for (int64_t s = threadIdx.x; s < S; s += blockDim.x) {
@@ -310,14 +320,17 @@ __global__ __launch_bounds__(256) void ctc_grad_kernel(const float* __restrict__
 
 // grad += coef*(softmax(lp/T) - p_t) ; loss_acc += loss_scale * sum_c p_t (log p_t - log_softmax(lp/T))
 // teacher p_t = softmax(log_softmax(tl)/T)   (tl: teacher decoder logits)
+// Rows are strided over a fixed grid (each wave takes rows w, w + 4 gridDim, ...) and the loss partials meet
+// in LDS: one float atomic per workgroup -- an atomic per row (12 832 at the bench shape, all on one address)
+// serialised at the L2 and made this launch ~170 us in the step.
 template <int NV>
 __global__ __launch_bounds__(256) void kl_kernel(const float* __restrict__ lp, const float* __restrict__ tl,
                                                  float* __restrict__ grad, float* __restrict__ loss_acc, int64_t rows,
                                                  int C, float invT, float coef, float loss_scale) {
   const int lane = threadIdx.x & 63;
-  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  __shared__ float wsum[4];
   float contrib = 0.f;
-  if (r < rows) {
+  for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < rows; r += (int64_t)gridDim.x * 4) {
     float sv[NV], tv[NV];
     float ms = NEG_INF, mt = NEG_INF;
 #pragma unroll
@@ -364,7 +377,12 @@ __global__ __launch_bounds__(256) void kl_kernel(const float* __restrict__ lp, c
     }
   }
   contrib = wave_sum(contrib);
-  if (lane == 0 && r < rows) atomicAdd(loss_acc, contrib * loss_scale);
+  if (lane == 0) wsum[threadIdx.x >> 6] = contrib;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float t = (wsum[0] + wsum[1]) + (wsum[2] + wsum[3]);
+    if (t != 0.f) atomicAdd(loss_acc, t * loss_scale);
+  }
 }
 
 // out = [total, ctc, kl, recon, fm] ; ctc = mean_b nll ; total = ctc + kd_alpha*kl + recon + fm
@@ -471,7 +489,8 @@ int kdfm_kl_div_logits(const float* student_logp, const float* teacher_logits, f
   KDFM_REQUIRE(C > 0 && C <= 4096 && temperature > 0.f, "bad args");
   if (rows == 0) return KDFM_OK;
   return row_dispatch(C, [&](auto nv) {
-    hipLaunchKernelGGL(kl_kernel<decltype(nv)::value>, dim3((unsigned)ceil_div(rows, 4)), dim3(256), 0,
+    const int64_t nb = ceil_div(rows, 4);
+    hipLaunchKernelGGL(kl_kernel<decltype(nv)::value>, dim3((unsigned)(nb < 512 ? nb : 512)), dim3(256), 0,
                        as_stream(stream), student_logp, teacher_logits, grad, loss_acc, rows, (int)C, 1.f / temperature,
                        grad_coef, loss_scale);
     return check_launch("kdfm_kl_div_logits");
