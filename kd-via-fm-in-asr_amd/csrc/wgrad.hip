@@ -700,7 +700,10 @@ bool wr_plan(const GemmP& p, int amode, int bmode, int64_t batch, WrPlan& pl, bo
   // conv-mode products (the denoiser's k=3 convs over the stacked head rows, 4 per step) may take fewer
   // workgroups so the compute stream's heads kernels keep CUs beside them (KDFM_WGR_CONV_WGS)
   static const int target_conv = env_i("KDFM_WGR_CONV_WGS", target_all);
-  const int target = bmode == KDFM_LD_CONV ? target_conv : target_all;
+  // the striding subsampling's conv2 weight gradient (WR_LD_C2D) runs at the step's tail beside the conv2 data
+  // gradient, where nothing else waits for CUs: its 256 640 rows over 3 column slices get more, shorter splits
+  static const int target_c2d = env_i("KDFM_WGR_C2D_WGS", target_all);
+  const int target = bmode == KDFM_LD_CONV ? target_conv : bmode == WR_LD_C2D ? target_c2d : target_all;
   // at least 6 32-row steps per split: the 12 832-row products take 66 splits (4 -> 100 splits: 2303-2309 utt/s,
   // 6: 2318-2325, 8: 2316-2318, 12: 2255, 16: 2150 -- profiles/r05/r5zh, r5zi; fewer partial bytes until the
   // longer per-workgroup chains delay the weight-gradient stream's tail)
@@ -1301,8 +1304,18 @@ int kdfm_wgrad_bf16(const uint16_t* dY, const uint16_t* X, float* dW, int64_t ld
 }
 
 int64_t kdfm_wgrad_bf16_s2conv_ws(int64_t B, int64_t T1, int64_t F1, int64_t C) {
+  using namespace kdfm;
   const int64_t T2 = (T1 - 1) / 2 + 1, F2 = (F1 - 1) / 2 + 1;
-  return kdfm_wgrad_bf16_ws(B * T2 * F2, C, 9 * C, 1);
+  GemmP p = wgrad_bf16_params(reinterpret_cast<const uint16_t*>(16), reinterpret_cast<const uint16_t*>(16), nullptr,
+                              9 * C, reinterpret_cast<float*>(16), B * T2 * F2, C, 9 * C, 1.f, nullptr, 0);
+  p.conv_c = C;
+  p.c2_T1 = T1;
+  p.c2_F1 = F1;
+  p.c2_T2 = T2;
+  p.c2_F2 = F2;
+  WrPlan pl;
+  if (!wr_plan(p, KDFM_LD_XC, WR_LD_C2D, 1, pl, true, true)) return -1;
+  return pl.S * p.M * p.N;
 }
 
 int kdfm_wgrad_bf16_s2conv(const uint16_t* dY, const uint16_t* X, const int64_t* len_in, float* dW, float* db,
