@@ -449,7 +449,12 @@ class Ver5Engine:
         return self.cfg.deterministic if self.overlap_wgrad is None else not self.overlap_wgrad
 
     def _heads_half(self, train, save):
-        """h > 0: the heads run as layers [0, h) and [h, L) (KDFM_HEADS_SPLIT=0: one call over all)."""
+        """h > 0: the heads run as layers [0, h) and [h, L) (KDFM_HEADS_SPLIT=0: one call over all).  Not in the
+        serialised (deterministic) schedule: there the split's first half -- forward on its own stream, backward in
+        line -- made the lower layers' gradients differ between identical steps in 5 of 8 runs
+        (tools/ddp_equiv_repeat.py, profiles/r05/r5zz*; 0 of 8 unsplit); the overlapped schedule keeps it."""
+        if self._serial():
+            return 0
         return self.cfg.n_layers // 2 if self.heads_split and self.cfg.n_layers >= 2 else 0
 
     def _heads_stream(self, main):
@@ -598,6 +603,16 @@ class Ver5Engine:
         with self._on_stream():
             K.step_advance(None, self.seed)
 
+    def allreduce_grads(self, allreduce) -> float:
+        """allreduce(flat gradient) -- the buckets the backward has not launched yet, then the waits -- issued on
+        the engine's compute stream, so the last buckets' collectives are ordered after the backward's last
+        gradient writes and AdamW after the collectives by stream order.  (Called from the caller's stream
+        instead, the final buckets were read before the subsampling backward had finished in ~1 of 2 runs of
+        tests/test_ddp_equiv_gpu.py: tools/ddp_equiv_repeat.py, profiles/r05/r5zz.)  Returns the gradient
+        scale (1 / world)."""
+        with self._on_stream(), K.region("allreduce"):
+            return allreduce(self.student.grad)
+
     def train_step(self, wav, wav_len, targets, tgt_len, allreduce=None):
         """forward + backward + (all-reduce) + AdamW.  Returns the device loss vector."""
         self.advance_rng()
@@ -608,8 +623,7 @@ class Ver5Engine:
         del ctx
         scale = 1.0
         if allreduce is not None:
-            with K.region("allreduce"):
-                scale = allreduce(self.student.grad)
+            scale = self.allreduce_grads(allreduce)
         self.optimizer_step(scale)
         return self.losses
 
@@ -627,7 +641,7 @@ class Ver5Engine:
         box = {}
 
         def finish():
-            box["scale"] = allreduce(self.student.grad) if allreduce is not None else 1.0
+            box["scale"] = self.allreduce_grads(allreduce) if allreduce is not None else 1.0
 
         def step():
             self.advance_rng()

@@ -89,7 +89,7 @@ def _worker(rank, world, port, out):
         ar = BucketedGradAllReduce(eng.student.numel, buckets=4)
         _grad(eng, _shard(batch, rank, dev), ready=ar.ready)
         launched_early = len(ar._launched)
-        scale = ar(eng.student.grad)
+        scale = eng.allreduce_grads(ar)   # as Ver5Engine.train_step: on the engine's compute stream
         torch.cuda.synchronize()
         g_sum = local[0] + local[1]
         g_ddp = eng.student.grad.clone()

@@ -65,7 +65,7 @@ def _worker(rank, world, port, out):
     eng.backward(ctx, grad_ready=lambda o: ar.ready(grad, o))
     early = len(ar._launched)
     del ctx
-    scale = ar(grad)
+    scale = eng.allreduce_grads(ar)   # as Ver5Engine.train_step: on the engine's compute stream
     torch.cuda.synchronize()
     diff = (grad - ref).abs()
     worst = int(diff.argmax())
