@@ -449,12 +449,7 @@ class Ver5Engine:
         return self.cfg.deterministic if self.overlap_wgrad is None else not self.overlap_wgrad
 
     def _heads_half(self, train, save):
-        """h > 0: the heads run as layers [0, h) and [h, L) (KDFM_HEADS_SPLIT=0: one call over all).  Not in the
-        serialised (deterministic) schedule: there the split's first half -- forward on its own stream, backward in
-        line -- made the lower layers' gradients differ between identical steps in 5 of 8 runs
-        (tools/ddp_equiv_repeat.py, profiles/r05/r5zz*; 0 of 8 unsplit); the overlapped schedule keeps it."""
-        if self._serial():
-            return 0
+        """h > 0: the heads run as layers [0, h) and [h, L) (KDFM_HEADS_SPLIT=0: one call over all)."""
         return self.cfg.n_layers // 2 if self.heads_split and self.cfg.n_layers >= 2 else 0
 
     def _heads_stream(self, main):
@@ -467,9 +462,11 @@ class Ver5Engine:
         auto-encoder on the teacher stream)."""
         nb = h * Ss.rows
         hs = self._heads_stream(main)
+        # the teacher features / auto-encoder outputs of layers [0, h) come from the teacher stream: wait for it
+        # in line too (the serialised schedule once read them unjoined -- profiles/r05/r5zz*)
+        hs.wait_stream(side)
         if hs is not main:
             hs.wait_stream(main)
-            hs.wait_stream(side)
             for t in (sfeats, tfeats, *tae, acc) + (() if eps is None else (eps,)):
                 t.record_stream(hs)
         with K.on_stream(hs), K.region("heads_forward_first_half"):

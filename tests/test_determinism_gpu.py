@@ -22,7 +22,6 @@ def _run(cfg, wav, wl, tg, tl, eps, overlap=None):
     eng = Ver5Engine(cfg, "cuda", teacher_seed=0, student_seed=1, heads_seed=2)
     if overlap is not None:
         eng.overlap_wgrad = overlap
-        eng.heads_split = False   # the serialised schedule never splits the heads (Ver5Engine._heads_half)
     eng.set_seed(77)
     eng.advance_rng()
     ctx = eng.forward(wav, wl, tg, tl, train=True, eps=eps)
@@ -37,9 +36,7 @@ def test_step_is_bitwise_reproducible(which):
     """The third case runs the benchmark's
     schedule (weight gradients on the side stream, overlapping the data-gradient chain) in run 1 and
     every weight gradient in line in run 2, both with ordered reductions: the overlap changes when
-    kernels run, never what they compute, so any difference is a cross-stream race.  Both
-    runs call the heads over all layers at once: the serialised schedule never splits them, and a split
-    sums the heads' loss terms in another order."""
+    kernels run, never what they compute, so any difference is a cross-stream race."""
     from kdfm.config import DEFAULT, PARITY
     g = torch.Generator().manual_seed(21)
     if which == "f32-parity":
