@@ -370,18 +370,34 @@ def main():
     if os.environ.get("KDFM_PLAN_KNOCKOUT") and rank == 0:   # what-if probe (kdfm/plan.py): not a bench line
         print(f"KNOCKOUT {os.environ['KDFM_PLAN_KNOCKOUT']} ms_per_step {1e3 * elapsed / args.steps:.3f}", flush=True)
         return
-    # live per-kernel timing: one instrumented eager step right after the timed steps; every
-    # kdfm_gemm launch (keyed by the kernel family libkdfm routed it to), the frontend and the
-    # depthwise convs bracketed by HIP events on the stream they run on
+    # live per-kernel timing over the schedule that was timed: a second step plan recorded with
+    # every traced launch -- each kdfm_gemm launch (keyed by the kernel family libkdfm routed it to), the fused
+    # kernels, the frontend, the depthwise convs -- bracketed by HIP events on the stream it runs on.  The events
+    # are part of that plan (each replay re-records them in place), so the durations come from a REPLAYED step with
+    # the same four-stream overlap and contention as the timed ones (the round-5 line took them from an eager
+    # instrumented step: 1.3x more optimistic than the rocprof summary of the replayed step).  Eager / graph issue:
+    # one instrumented eager step.
     trace = K.Trace(["*", "frontend", "dwconv", "ffn_fwd", "ffn_bwd", "wgrad_bf16", "wgrad_fold", "attn_fwd", "attn_prep",
                      "attn_bwd"])
-    with trace:
-        eng.train_step(wav, wl, tg, tl, ar)
+    trace_issue = "eager instrumented step"
+    if not args.eager and not args.graph:
+        with trace:
+            tplan = eng.make_plan(wav, wl, tg, tl, ar)
+        tplan.replay()   # one warm replay; the events keep the timestamps of the last one
+        torch.cuda.synchronize()
+        tplan.replay()
+        trace_issue = f"replayed step plan with per-launch HIP events ({len(tplan)} ops)"
+    else:
+        with trace:
+            eng.train_step(wav, wl, tg, tl, ar)
     torch.cuda.synchronize()
     losses = eng.losses.detach().cpu().tolist()
     if not all(math.isfinite(x) for x in losses):
         raise RuntimeError(f"non-finite losses after the timed steps: {losses}")
     tsum = trace.summary()
+    # the plans keep their steps' activations alive: release them before the sensitivity engines are built
+    tplan = plan = run = None
+    torch.cuda.empty_cache()
     empty = {"launches": 0, "ms_total": 0.0, "flops_total": 0.0, "bytes_total": 0.0}
     if rank == 0:
         utt = world * args.batch * args.steps / elapsed
@@ -435,6 +451,7 @@ def main():
                                        "all of the family's kernels incl. folds, per call = per main-kernel launch)",
                      "kernel": f"{dom} family ({', '.join(stems)}): the kernel family with the largest aggregated "
                                f"time of the step (kdfm_gemm routes + the fused kernels, HIP events on their streams)",
+                     "timing_source": trace_issue,
                      "launches": n, "avg_ms": round(ms, 5), "bytes_per_launch": round(dt["bytes_total"] / n, 1),
                      "flops_per_launch": round(dt["flops_total"] / n, 1),
                      "arith_intensity_flop_per_byte": round(intensity, 2)})

@@ -150,6 +150,29 @@ typedef struct kdfm_gemm_desc {
 
 int kdfm_gemm(const kdfm_gemm_desc* d, void* stream);
 
+/* Large-tile bf16 GEMM (csrc/biggemm.hip) for the wide layer products (d_model >= 512: the Conformer-large /
+ * FastConformer(-XL) Linear layers, conformer_encoder.py:450-472 built at fast-conformer_ctc_bpe.yaml:29 widths),
+ * replacing kdfm_gemm's generic 64x64 route for them.  bf16 operands in HBM, f32 accumulation:
+ *   C[m][n] = epi(alpha * sum_k A(m, k) B(k, n)),  M x N x K from the descriptor,
+ *   layout KDFM_BIG_NT: A(m, k) = A[m * lda + k], B(k, n) = B[n * ldb + k]   (forward: x W^T)
+ *          KDFM_BIG_NN: A(m, k) = A[m * lda + k], B(k, n) = B[k * ldb + n]   (data gradient: dY W)
+ *          KDFM_BIG_TN: A(m, k) = A[k * lda + m], B(k, n) = B[k * ldb + n]   (weight gradient: dY^T X)
+ * The descriptor supplies C / strides and the epilogue (every kdfm_gemm flag except MSE, and at most one side
+ * operand); C16 != NULL writes bf16 C16[m * sCm + n * sCn] instead of C.  epi == KDFM_EPI_ATOMIC means
+ * ACCUMULATE: C += alpha * result, and ones_out[m] += alpha * sum_k A(m, k) when ones_out is set (the bias
+ * gradient) -- one writer per element, fixed summation order (deterministic, unlike kdfm_gemm's split-K).
+ * A, B 16-byte aligned, lda / ldb multiples of 8; kdfm_gemm_big_supported(M, N, K, layout) says whether the
+ * shape is taken (k-contiguous A: K % 64 == 0; k-major operands: their row length % 8 == 0). */
+#define KDFM_BIG_NT 0
+#define KDFM_BIG_NN 1
+#define KDFM_BIG_TN 2
+int kdfm_gemm_big_supported(int64_t M, int64_t N, int64_t K, int layout);
+int kdfm_gemm_big(const kdfm_gemm_desc* d, const uint16_t* A, int64_t lda, const uint16_t* B, int64_t ldb, int layout,
+                  uint16_t* C16, void* stream);
+/* dst[r * ldd + c] = bf16(src[r * lds + c]) for a rows x cols f32 matrix (cols, lds, ldd multiples of 4). */
+int kdfm_cast_bf16_2d(const float* src, int64_t lds, uint16_t* dst, int64_t ldd, int64_t rows, int64_t cols,
+                      void* stream);
+
 /* Row-parallel weight gradient with bf16 operands (the fused KD-head chains' saved operands):
  *   dW[m][n] += alpha * sum_r dY[r][m] * X[r][n]  (dW row stride ldc),  db[m] += alpha * sum_r dY[r][m]
  * dY (rows, M), X (rows, N) bf16 row-major, M % 4 == N % 4 == 0, 16-byte aligned; db may be NULL.
@@ -208,10 +231,16 @@ int kdfm_wgrad_bf16_s2conv(const uint16_t* dY, const uint16_t* X, const int64_t*
  * arena for the stream's next products (stream order).  dW / db are final only after the flush.  A product
  * whose partials do not fit the arena's remaining space folds at once as usual; queued products adding into
  * overlapping gradient memory fold in queue order (separate launches).  arena = NULL ends deferral
- * (the queue must be empty).  kdfm_wgrad_fold_pending: queued folds of the stream. */
+ * (the queue must be empty).  kdfm_wgrad_fold_pending: queued folds of the stream.  kdfm_wgrad_fold_stats:
+ * out3 = [queued folds, products that did not fit the arena and folded at once since it was set, the largest
+ * arena in floats the queue between two flushes would have needed] (host state, no device sync).
+ * kdfm_wgrad_fold_discard_all: error recovery -- drop every stream's queued folds (their gradients are then
+ * incomplete) and unset every arena; returns the number of jobs dropped. */
 int kdfm_wgrad_set_fold_arena(void* stream, float* arena, int64_t len);
 int kdfm_wgrad_fold_flush(void* stream);
 int64_t kdfm_wgrad_fold_pending(void* stream);
+int kdfm_wgrad_fold_stats(void* stream, int64_t* out3);
+int kdfm_wgrad_fold_discard_all(void);
 
 /* Fused FlowMatchingModule chain (asr_train_diffm.py:1368-1427, rectified, meta_encoder 'mlp',
  * shape_transform 'linear'; bf16 MFMA, f32 state; latent width L == 96).  Rows n:

@@ -1,0 +1,474 @@
+// Large-tile bf16 GEMM for the wide layer products (d_model >= 512: Conformer-large, FastConformer /
+// FastConformer-XL -- BASELINE.json configs[3] / [4]; fast-conformer_ctc_bpe.yaml:29 XLarge d=1024), where no
+// fused LN-block kernel applies and the products are large and MFMA-friendly (M = B*T' >= 4k rows, N, K >= 512).
+//
+// C[m][n] = epi(alpha * sum_k A(m, k) B(k, n)) with bf16 operands in HBM and f32 accumulation:
+//   * each operand is either K-CONTIGUOUS (A stored [m][k], B stored [n][k]: the forward's x W^T) or
+//     K-MAJOR (A stored [k][m], B stored [k][n]: the data gradient's W, the weight gradient's dY and X) --
+//     three instantiations cover every Linear: forward (A, B k-contiguous), data gradient (A k-contiguous,
+//     B = W k-major), weight gradient (both k-major, the reduction over rows);
+//   * workgroup tile BM x BN (256x256 / 256x128 / 128x128, picked per shape to fill the 256 CUs), 8 or 4 waves,
+//     each wave a (BM/WM) x (BN/WN) block of v_mfma_f32_16x16x32_bf16 tiles, K step 64;
+//   * operand tiles staged HBM -> LDS by LDS-DMA (global_load_lds_dwordx4: one wave-instruction moves 1 KB, no
+//     staging registers), two LDS stages, the next stage's DMA in flight while the current one's MFMAs run, one
+//     barrier per K step; the k-contiguous images are [row][64 k] with 128-byte rows whose 16-byte chunks are
+//     XOR-swizzled by (row >> 1) & 7 (conflict-free ds_read_b128 fragment reads), the k-major images are
+//     [64 k][cols] rows whose 8-byte units are XOR-swizzled by the row's (bits 0-1, bit 3) -- the fragments are
+//     read TRANSPOSED with ds_read_b64_tr_b16 (conflict-free); the swizzle is applied to the DMA's per-lane
+//     SOURCE address (the LDS destination of an LDS-DMA is lane-linear);
+//   * the fused epilogue is gemm_common.h's (bias, SiLU, ReLU, dropout, STORE_PRE, dReLU / dSiLU, residual,
+//     BETA, row mask: the same per-element semantics as every other kdfm_gemm route), f32 or bf16 output
+//     (a bf16 output is what the next product reads), or the weight-gradient accumulate C += alpha * acc with
+//     the bias gradient (row sums of A) from one extra MFMA per row tile against an all-ones operand.
+// Deterministic: every output element has one writer and a fixed summation order (no split-K, no atomics).
+#include "gemm_common.h"
+
+namespace kdfm {
+namespace {
+
+constexpr int BG_BK = 64;
+// epilogue modes beyond gemm_common.h's SKC_EPI_*: the weight-gradient accumulate, without / with the bias gradient
+// (the extra accumulators of the latter exist only in its instances: they cost 4 * FM registers)
+constexpr int BG_ACC = 98, BG_ACCB = 99;
+// the data gradient through a dropped-out SiLU (the FFN's linear2 dX: dh = drop(dY W2) * silu'(h)), flags
+// KDFM_EPI_DSILU | KDFM_EPI_DROPOUT with the pre-activation as aux: epi_apply's arithmetic in that order
+constexpr int BG_DSILU_DROP = 97;
+
+typedef short bg_v4s __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void bg_lds_void;
+typedef __attribute__((address_space(1))) void bg_gl_void;
+
+struct BigP {
+  const uint16_t* A;
+  const uint16_t* B;
+  int64_t lda, ldb;   // row strides (elements) of the stored operands
+  uint16_t* C16;      // bf16 output (row stride g.sCm) instead of g.C when non-null
+  float* ones_out;    // ones_out[m] += alpha * sum_k A(m, k) (accumulate mode)
+  int accum;          // C[m][n] += alpha * acc
+  int tn;             // column tiles
+  GemmP g;            // M, N, K, C, strides and the epilogue fields
+};
+
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) char*)p);
+}
+
+// 16-byte chunk swizzle of a k-contiguous image row (128 B = 8 chunks)
+__device__ __forceinline__ int kc_swz(int row) { return (row >> 1) & 7; }
+// 8-byte unit swizzle of a k-major image row: 4 * (row bits 0-1 | bit 3 << 2) (a multiple of 4 units, i.e. of
+// 2 chunks, so one 16-byte DMA chunk keeps its two units together)
+__device__ __forceinline__ int km_swz8(int row) { return 4 * ((row & 3) | (((row >> 3) & 1) << 2)); }
+
+template <int N>
+__device__ __forceinline__ void lgkm_wait() {
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// fragment of 16 rows x 32 k out of a k-contiguous [rows][64] image: lane l -> row r0 + (l & 15),
+// k = 32 hh + 8 (l >> 4) .. + 7
+__device__ __forceinline__ bf16x8 frag_kc(const uint16_t* img, int r0, int hh, int lane) {
+  const int r = r0 + (lane & 15);
+  const int p = ((lane >> 4) + 4 * hh) ^ kc_swz(r);
+  const uint32_t a = lds_addr(img + r * BG_BK + 8 * p);
+  bf16x8 v;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(a));
+  return v;
+}
+
+// fragment of 16 columns x 32 k out of a k-major [64][W] image: lane l (g = l >> 4, li = l & 15) -> column
+// c0 + li, k = 32 hh + 8 g + e (e < 4: first transposed read, rows 32 hh + 8 g + q; e >= 4: rows + 4)
+template <int W>
+__device__ __forceinline__ bf16x8 frag_km(const uint16_t* img, int c0, int hh, int lane) {
+  const int li = lane & 15, g = lane >> 4;
+  const int row = 32 * hh + 8 * g + (li >> 2);
+  const int u = ((c0 >> 2) + (li & 3)) ^ km_swz8(row);
+  const uint32_t a = lds_addr(img + row * W + 4 * u);
+  bg_v4s lo, hi;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(a));
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(hi) : "v"(a + 8u * (uint32_t)W));
+  return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+template <int BM, int BN, int WM, int WN, bool AT, bool BT, int EMODE>
+__global__ __launch_bounds__(WM* WN * 64) void big_gemm_kernel(BigP p) {
+  constexpr int NW = WM * WN;
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int FM = WTM / 16, FN = WTN / 16;
+  constexpr int AIMG = BM * BG_BK, BIMG = BN * BG_BK;   // elements per stage
+  constexpr int STAGE = AIMG + BIMG;
+  constexpr int PA = BM / 8, PB = BN / 8, PW = (PA + PB) / NW;   // 1 KB DMA pieces: A, B, per wave
+  static_assert((PA + PB) % NW == 0, "pieces per wave");
+  extern __shared__ __attribute__((aligned(16))) uint16_t bg_lds[];
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wr = wave / WN, wc = wave % WN;
+  const int64_t tile = xcd_block();
+  const int64_t tm = tile / p.tn, tnn = tile % p.tn;
+  const int64_t m0 = tm * BM, n0 = tnn * BN;
+  const int64_t M = p.g.M, N = p.g.N, K = p.g.K;
+  const int nk = (int)((K + BG_BK - 1) / BG_BK);
+
+  // DMA of K step t into stage buffer s: exactly PW wave-instructions per wave
+  auto issue = [&](int t, int s) {
+    const int64_t k0 = (int64_t)t * BG_BK;
+    uint16_t* buf = bg_lds + s * STAGE;
+#pragma unroll
+    for (int i = 0; i < PW; ++i) {
+      const int f = wave + NW * i;
+      const bool isa = f < PA;
+      const int fl = isa ? f : f - PA;
+      const uint16_t* X = isa ? p.A : p.B;
+      const int64_t ld = isa ? p.lda : p.ldb;
+      const int64_t R = isa ? M : N, r0 = isa ? m0 : n0;
+      const bool km = isa ? AT : BT;
+      const int W = isa ? BM : BN;
+      const uint16_t* src;
+      if (!km) {   // [row][64 k], 8 rows per piece
+        const int row = 8 * fl + (lane >> 3);
+        const int c = (lane & 7) ^ kc_swz(row);
+        int64_t gr = r0 + row;
+        gr = gr < R ? gr : R - 1;
+        src = X + gr * ld + k0 + 8 * c;
+      } else {     // [64 k][W cols], 1024 / (2 W) rows per piece
+        const int byte = 1024 * fl + 16 * lane;
+        const int row = byte / (2 * W);
+        const int v = (byte % (2 * W)) >> 4;
+        const int c = v ^ (km_swz8(row) >> 1);
+        int64_t gk = k0 + row;
+        gk = gk < K ? gk : K - 1;
+        int64_t gc = r0 + 8 * c;
+        gc = gc + 8 <= R ? gc : R - 8;
+        src = X + gk * ld + gc;
+      }
+      uint16_t* dst = buf + (isa ? 0 : AIMG) + 512 * fl;
+      __builtin_amdgcn_global_load_lds((bg_gl_void*)src, (bg_lds_void*)dst, 16, 0, 0);
+    }
+  };
+
+  constexpr bool BIAS = EMODE == BG_ACCB;
+  f32x4 acc[FM][FN];
+  f32x4 accb[BIAS ? FM : 1];
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    if constexpr (BIAS) accb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  const bool do_bias = BIAS && wc == 0 && tnn == 0;
+  bf16x8 ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = (short)0x3F80;   // bf16(1.0)
+
+  issue(0, 0);
+  for (int t = 0; t < nk; ++t) {
+    __builtin_amdgcn_s_waitcnt((0) | (7 << 4) | (15 << 8));   // vmcnt(0): this wave's pieces of step t landed
+    __builtin_amdgcn_s_barrier();                              // ... every wave's; step t - 1's reads are done
+    const int s = t & 1;
+    const uint16_t* abuf = bg_lds + s * STAGE;
+    const uint16_t* bbuf = abuf + AIMG;
+    if constexpr (AT || BT) {
+      const int64_t vr = K - (int64_t)t * BG_BK;
+      if (vr < BG_BK) {   // tail step: zero the k-major A (or B) rows past K (their DMA read clamped rows)
+        uint16_t* z = bg_lds + s * STAGE + (AT ? 0 : AIMG);
+        constexpr int ZW = AT ? BM : BN;
+        for (int e = threadIdx.x; e < (BG_BK - (int)vr) * ZW; e += NW * 64) z[(int)vr * ZW + e] = 0;
+        __syncthreads();
+      }
+    }
+    if (t + 1 < nk) issue(t + 1, s ^ 1);
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      bf16x8 af[FM], bfr[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int r = wr * WTM + 16 * i;
+        if constexpr (AT) af[i] = frag_km<BM>(abuf, r, hh, lane);
+        else af[i] = frag_kc(abuf, r, hh, lane);
+      }
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int c = wc * WTN + 16 * j;
+        if constexpr (BT) bfr[j] = frag_km<BN>(bbuf, c, hh, lane);
+        else bfr[j] = frag_kc(bbuf, c, hh, lane);
+      }
+      lgkm_wait<0>();
+#pragma unroll
+      for (int i = 0; i < FM; ++i) asm volatile("" : "+v"(af[i]));
+#pragma unroll
+      for (int j = 0; j < FN; ++j) asm volatile("" : "+v"(bfr[j]));
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        if constexpr (BIAS)
+          if (do_bias) accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], ones, accb[i], 0, 0, 0);
+      }
+    }
+  }
+
+  // ---- epilogue ----
+  const GemmP& g = p.g;
+  const float alpha = g.alpha;
+  if constexpr (EMODE == BG_ACC || EMODE == BG_ACCB) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int64_t mb = m0 + wr * WTM + 16 * i + 4 * (lane >> 4);
+      float old[FN][4];
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int64_t n = n0 + wc * WTN + 16 * j + (lane & 15);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) old[j][r] = (mb + r < M && n < N) ? g.C[(mb + r) * g.sCm + n * g.sCn] : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int64_t n = n0 + wc * WTN + 16 * j + (lane & 15);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (mb + r < M && n < N) g.C[(mb + r) * g.sCm + n * g.sCn] = old[j][r] + alpha * acc[i][j][r];
+      }
+      if constexpr (BIAS) {
+        if (do_bias && (lane & 15) == 0) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (mb + r < M) p.ones_out[mb + r] += alpha * accb[i][r];
+        }
+      }
+    }
+    return;
+  } else {
+  const int epi = g.epi;
+  const uint64_t seed = (epi & KDFM_EPI_DROPOUT) ? load_seed(g.seed) : 0ull;
+  const float keep_scale = (epi & KDFM_EPI_DROPOUT) ? 1.f / (1.f - g.dropout_p) : 1.f;
+  bool single;
+  const float* side = epi_side_src(g, single);
+  float mse_part = 0.f;
+  float bn[FN];
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int64_t n = n0 + wc * WTN + 16 * j + (lane & 15);
+    bn[j] = ((epi & KDFM_EPI_BIAS) && n < N) ? g.bias[n] : 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int64_t mb = m0 + wr * WTM + 16 * i + 4 * (lane >> 4);
+    bool rok[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) rok[r] = mb + r < M && epi_row_ok(g, mb + r < M ? mb + r : 0);
+    // side operands a column tile at a time when the epilogue is the generic one (its flag walk holds more
+    // registers beside the 4 * FM * FN accumulators), else all of the row tile's first
+    constexpr int SVJ = EMODE == SKC_EPI_GENERIC ? 1 : FN;
+#pragma unroll
+    for (int j0 = 0; j0 < FN; j0 += SVJ) {
+    float sv[SVJ][4];
+#pragma unroll
+    for (int jj = 0; jj < SVJ; ++jj) {
+      const int64_t n = n0 + wc * WTN + 16 * (j0 + jj) + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) sv[jj][r] = (side && mb + r < M && n < N) ? side[(mb + r) * g.sCm + n * g.sCn] : 0.f;
+    }
+#pragma unroll
+    for (int jj = 0; jj < SVJ; ++jj) {
+      const int j = j0 + jj;
+      const int64_t n = n0 + wc * WTN + 16 * j + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t m = mb + r;
+        if (m >= M || n >= N) continue;
+        const int64_t off = m * g.sCm + n * g.sCn;
+        float pre = 0.f;
+        float v;
+        if constexpr (EMODE == BG_DSILU_DROP) {
+          v = alpha * acc[i][j][r];
+          if (epi & KDFM_EPI_DROPOUT) {
+            const uint64_t idx = (uint64_t)m * (uint64_t)N + (uint64_t)n;
+            v = dropout_keep(seed, g.rng_stream, idx, g.dropout_p) ? v * keep_scale : 0.f;
+          }
+          v *= dsiluf_(sv[jj][r]);
+        } else {
+          v = skc_epi<EMODE>(g, m, n, alpha * acc[i][j][r], bn[j], sv[jj][r], rok[r], seed, keep_scale, mse_part, pre,
+                             0);
+        }
+        if (epi & KDFM_EPI_STORE_PRE) g.Cpre[off] = pre;
+        if (p.C16) p.C16[off] = f2bf(v);
+        else g.C[off] = v;
+      }
+    }
+    }
+  }
+  }
+}
+
+template <int BM, int BN, int WM, int WN, bool AT, bool BT, int EMODE>
+int big_launch(const BigP& p, hipStream_t st) {
+  auto kern = big_gemm_kernel<BM, BN, WM, WN, AT, BT, EMODE>;
+  constexpr int lds = 2 * (BM + BN) * BG_BK * 2;
+  static const bool once = [&] {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    return true;
+  }();
+  (void)once;
+  const int64_t tm = ceil_div(p.g.M, BM), tn = ceil_div(p.g.N, BN);
+  BigP q = p;
+  q.tn = (int)tn;
+  hipLaunchKernelGGL(kern, dim3((unsigned)(tm * tn)), dim3(WM * WN * 64), lds, st, q);
+  return check_launch("kdfm_gemm_big");
+}
+
+// compile-time epilogue per layout (the generic instance covers every flag set)
+template <int BM, int BN, int WM, int WN, bool AT, bool BT>
+int big_epi(const BigP& p, hipStream_t st) {
+  if constexpr (AT && BT) {   // the weight-gradient layout: accumulate only
+    if constexpr (BM == 256 && BN == 256) {   // big_dispatch never asks it for the bias gradient (spills)
+      return p.ones_out ? KDFM_EUNSUPPORTED : big_launch<BM, BN, WM, WN, AT, BT, BG_ACC>(p, st);
+    } else {
+      return p.ones_out ? big_launch<BM, BN, WM, WN, AT, BT, BG_ACCB>(p, st)
+                        : big_launch<BM, BN, WM, WN, AT, BT, BG_ACC>(p, st);
+    }
+  } else {
+  if ((p.g.epi & ~KDFM_EPI_DROPOUT) == KDFM_EPI_DSILU) return big_launch<BM, BN, WM, WN, AT, BT, BG_DSILU_DROP>(p, st);
+  const int em = skc_epi_mode(p.g.epi);
+  switch (em) {
+    case SKC_EPI_NONE: return big_launch<BM, BN, WM, WN, AT, BT, SKC_EPI_NONE>(p, st);
+    case SKC_EPI_SILU_DROP: return big_launch<BM, BN, WM, WN, AT, BT, SKC_EPI_SILU_DROP>(p, st);
+    case SKC_EPI_DROP_RESID: return big_launch<BM, BN, WM, WN, AT, BT, SKC_EPI_DROP_RESID>(p, st);
+    case SKC_EPI_RESID: return big_launch<BM, BN, WM, WN, AT, BT, SKC_EPI_RESID>(p, st);
+    default:
+      if constexpr (BM == 256 && BN == 256) return KDFM_EUNSUPPORTED;   // big_dispatch never picks it (spills)
+      else return big_launch<BM, BN, WM, WN, AT, BT, SKC_EPI_GENERIC>(p, st);
+  }
+  }
+}
+
+// does the compile-time epilogue set cover this descriptor (else the generic instance, which the 256 x 256 tile
+// does not carry: its flag walk beside 128 accumulators spills)
+bool big_epi_compiled(const BigP& p) {
+  if (p.accum) return true;
+  if ((p.g.epi & ~KDFM_EPI_DROPOUT) == KDFM_EPI_DSILU) return true;
+  const int em = skc_epi_mode(p.g.epi);
+  return em == SKC_EPI_NONE || em == SKC_EPI_SILU_DROP || em == SKC_EPI_DROP_RESID || em == SKC_EPI_RESID;
+}
+
+// tile shape: the one whose whole-chip rounds (tiles / 256 CUs, rounded up) times its per-tile MFMA work is least
+// (a 256x256 tile does 4x a 128x128 one's work at about 1.15x its rate per CU; 256x128 in between)
+int big_pick(int64_t M, int64_t N) {
+  const double eff[3] = {1.0, 0.93, 0.85};   // relative per-CU rate: 256x256, 256x128, 128x128
+  const int bm[3] = {256, 256, 128}, bn[3] = {256, 128, 128};
+  int best = 0;
+  double bt = 1e300;
+  for (int c = 0; c < 3; ++c) {
+    const int64_t tiles = ceil_div(M, bm[c]) * ceil_div(N, bn[c]);
+    const double rounds = (double)ceil_div(tiles, 256);
+    const double t = rounds * (double)bm[c] * bn[c] / eff[c];
+    if (t < bt - 1e-9) {
+      bt = t;
+      best = c;
+    }
+  }
+  return best;
+}
+
+template <bool AT, bool BT>
+int big_dispatch(const BigP& p, hipStream_t st) {
+  const char* e = getenv("KDFM_BIG_TILE");   // 0 / 1 / 2 forces a tile shape (A/B probes)
+  int c = e ? atoi(e) : big_pick(p.g.M, p.g.N);
+  // the 256 x 256 tile has no generic-epilogue instance, and its bias-gradient accumulators spill
+  if (c == 0 && (!big_epi_compiled(p) || p.ones_out)) c = 1;
+  if (c == 0) return big_epi<256, 256, 2, 4, AT, BT>(p, st);
+  if (c == 1) return big_epi<256, 128, 4, 2, AT, BT>(p, st);
+  return big_epi<128, 128, 2, 2, AT, BT>(p, st);
+}
+
+__global__ void cast2d_kernel(const float* __restrict__ src, int64_t lds, uint16_t* __restrict__ dst, int64_t ldd,
+                              int64_t rows, int64_t cols) {
+  const int64_t c4 = cols / 4;
+  const int64_t n = rows * c4;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / c4, c = (i - r * c4) * 4;
+    const float4 v = *reinterpret_cast<const float4*>(src + r * lds + c);
+    uint2 o;
+    o.x = pack_bf16x2(v.x, v.y);
+    o.y = pack_bf16x2(v.z, v.w);
+    *reinterpret_cast<uint2*>(dst + r * ldd + c) = o;
+  }
+}
+
+}  // namespace
+}  // namespace kdfm
+
+extern "C" {
+
+int kdfm_gemm_big_supported(int64_t M, int64_t N, int64_t K, int layout) {
+  using namespace kdfm;
+  if (M < 128 || N < 128 || K < 64 || layout < 0 || layout > 2) return 0;
+  if (layout == KDFM_BIG_NT || layout == KDFM_BIG_NN) {
+    if (K % BG_BK) return 0;   // the k-contiguous A image has no tail handling
+  }
+  if (layout == KDFM_BIG_NN && N % 8) return 0;
+  if (layout == KDFM_BIG_TN && (M % 8 || N % 8)) return 0;
+  return 1;
+}
+
+int kdfm_gemm_big(const kdfm_gemm_desc* d, const uint16_t* A, int64_t lda, const uint16_t* B, int64_t ldb, int layout,
+                  uint16_t* C16, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(d && A && B, "null argument");
+  KDFM_REQUIRE(kdfm_gemm_big_supported(d->M, d->N, d->K, layout), "shape / layout not supported by the big-tile GEMM");
+  KDFM_REQUIRE(d->batch1 == 1 && d->batch2 == 1 && d->splitk == 1, "unbatched, no split-K");
+  KDFM_REQUIRE(((((uintptr_t)A) | ((uintptr_t)B)) & 15) == 0 && lda % 8 == 0 && ldb % 8 == 0,
+               "operands 16-byte aligned with row strides multiple of 8 elements");
+  const bool accum = d->epi == KDFM_EPI_ATOMIC;
+  KDFM_REQUIRE(!(d->epi & KDFM_EPI_MSE), "the MSE epilogue is not supported here");
+  KDFM_REQUIRE(accum ? (C16 == nullptr && d->C != nullptr) : (d->C != nullptr || C16 != nullptr),
+               "accumulate mode needs the f32 C; otherwise C or C16");
+  KDFM_REQUIRE(d->ones_out == nullptr || accum, "the bias-gradient output needs accumulate mode");
+  KDFM_REQUIRE(!(d->epi & KDFM_EPI_BIAS) || d->bias, "EPI_BIAS without bias");
+  KDFM_REQUIRE(!(d->epi & KDFM_EPI_RESID) || d->R, "EPI_RESID without R");
+  KDFM_REQUIRE(!(d->epi & (KDFM_EPI_DRELU | KDFM_EPI_DSILU)) || d->aux, "derivative epilogue without aux");
+  KDFM_REQUIRE(!(d->epi & KDFM_EPI_STORE_PRE) || d->Cpre, "EPI_STORE_PRE without Cpre");
+  KDFM_REQUIRE(!(d->epi & KDFM_EPI_BETA) || (d->C && !C16), "EPI_BETA reads the f32 C");
+  KDFM_REQUIRE(!(d->epi & KDFM_EPI_ROWMASK) || (d->mask_len && d->mask_T > 0 && d->mask_div > 0), "ROWMASK fields");
+  BigP p{};
+  p.A = A; p.B = B; p.lda = lda; p.ldb = ldb; p.C16 = C16;
+  p.accum = accum ? 1 : 0;
+  p.ones_out = d->ones_out;
+  GemmP& g = p.g;
+  g.C = d->C; g.bias = d->bias; g.R = d->R; g.aux = d->aux; g.Cpre = d->Cpre;
+  g.M = d->M; g.N = d->N; g.K = d->K;
+  g.sCm = d->sCm; g.sCn = d->sCn;
+  g.alpha = d->alpha; g.beta = d->beta; g.rscale = d->rscale; g.dropout_p = d->dropout_p;
+  g.seed = d->seed; g.rng_stream = d->rng_stream;
+  g.epi = accum ? 0 : d->epi;
+  g.mask_len = d->mask_len; g.mask_T = d->mask_T; g.mask_div = d->mask_div;
+  g.ones_col = -1;
+  bool single;
+  (void)epi_side_src(g, single);
+  KDFM_REQUIRE(single, "at most one side operand (R, aux or C) per epilogue");
+  hipStream_t st = as_stream(stream);
+  set_route(ROUTE_BIG);
+  if (d->M == 0 || d->N == 0) return KDFM_OK;
+  KDFM_REQUIRE(accum == (layout == KDFM_BIG_TN), "the TN (weight-gradient) layout accumulates; NT / NN do not");
+  switch (layout) {
+    case KDFM_BIG_NT: return big_dispatch<false, false>(p, st);
+    case KDFM_BIG_NN: return big_dispatch<false, true>(p, st);
+    default: return big_dispatch<true, true>(p, st);
+  }
+}
+
+int kdfm_cast_bf16_2d(const float* src, int64_t lds, uint16_t* dst, int64_t ldd, int64_t rows, int64_t cols,
+                      void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(src && dst && rows >= 0 && cols >= 0, "bad arguments");
+  KDFM_REQUIRE(cols % 4 == 0 && lds % 4 == 0 && ldd % 4 == 0 && (((uintptr_t)src) & 15) == 0 &&
+                   (((uintptr_t)dst) & 7) == 0,
+               "cols / strides multiples of 4, src 16-B / dst 8-B aligned");
+  if (rows == 0 || cols == 0) return KDFM_OK;
+  const int64_t n = rows * (cols / 4);
+  const int64_t blocks = ceil_div(n, 256) < 8192 ? ceil_div(n, 256) : 8192;
+  hipLaunchKernelGGL(cast2d_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), src, lds, dst, ldd, rows,
+                     cols);
+  return check_launch("kdfm_cast_bf16_2d");
+}
+
+}  // extern "C"

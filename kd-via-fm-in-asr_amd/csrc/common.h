@@ -24,7 +24,7 @@ bool deterministic();
 // gradient (+ fold), 4 generic with ordered split-K fold, 5 LDS-slab k=3 conv, 6 row-parallel
 // weight gradient (+ ordered fold).
 enum { ROUTE_GENERIC = 0, ROUTE_SKINNY = 1, ROUTE_RS_FWD = 2, ROUTE_RS_WGRAD = 3, ROUTE_SPLIT_FOLD = 4,
-       ROUTE_SLAB_CONV = 5, ROUTE_WGRAD_ROWS = 6 };
+       ROUTE_SLAB_CONV = 5, ROUTE_WGRAD_ROWS = 6, ROUTE_BIG = 7 };
 void set_route(int r);
 
 #define KDFM_REQUIRE(cond, msg)                                  \

@@ -1216,6 +1216,9 @@ void conv_geometry(GemmP& p, int64_t C, int taps, int pad, int64_t T) {
 struct DeferState {
   float* arena = nullptr;
   int64_t len = 0, used = 0;
+  // since the arena was set: products that did not fit and folded at once (fallbacks), and the largest
+  // arena the queue between two flushes would have needed (demand: what a caller sizes the arena from)
+  int64_t want = 0, fallbacks = 0, peak_want = 0;
   std::vector<FoldJob> jobs;
 };
 std::mutex g_defer_mu;
@@ -1231,7 +1234,12 @@ float* defer_reserve(hipStream_t st, int64_t n) {
   if (it == defer_map().end() || !it->second.arena) return nullptr;
   DeferState& d = it->second;
   const int64_t need = (n + 3) / 4 * 4;
-  if (d.used + need > d.len) return nullptr;
+  d.want += need;
+  if (d.want > d.peak_want) d.peak_want = d.want;
+  if (d.used + need > d.len) {
+    ++d.fallbacks;
+    return nullptr;
+  }
   float* r = d.arena + d.used;
   d.used += need;
   return r;
@@ -1464,7 +1472,32 @@ int kdfm_wgrad_set_fold_arena(void* stream, float* arena, int64_t len) {
   d.arena = arena;
   d.len = arena ? len : 0;
   d.used = 0;
+  d.want = d.fallbacks = d.peak_want = 0;
   return KDFM_OK;
+}
+
+int kdfm_wgrad_fold_stats(void* stream, int64_t* out3) {
+  using namespace kdfm;
+  KDFM_REQUIRE(out3 != nullptr, "null output");
+  std::lock_guard<std::mutex> g(g_defer_mu);
+  auto it = defer_map().find(stream);
+  out3[0] = out3[1] = out3[2] = 0;
+  if (it == defer_map().end()) return KDFM_OK;
+  out3[0] = (int64_t)it->second.jobs.size();
+  out3[1] = it->second.fallbacks;
+  out3[2] = it->second.peak_want;
+  return KDFM_OK;
+}
+
+int kdfm_wgrad_fold_discard_all(void) {
+  using namespace kdfm;
+  std::lock_guard<std::mutex> g(g_defer_mu);
+  int n = 0;
+  for (auto& kv : defer_map()) {
+    n += (int)kv.second.jobs.size();
+    kv.second = DeferState{};
+  }
+  return n;
 }
 
 int kdfm_wgrad_fold_flush(void* stream) {
@@ -1476,6 +1509,7 @@ int kdfm_wgrad_fold_flush(void* stream) {
     if (it == defer_map().end()) return KDFM_OK;
     jobs.swap(it->second.jobs);
     it->second.used = 0;   // the stream's next products reuse the arena after these folds (stream order)
+    it->second.want = 0;
   }
   hipStream_t st = as_stream(stream);
   // the byte ranges a job's fold writes (its gradient block, its bias row(s)): jobs in one launch run

@@ -19,6 +19,7 @@ KDFM_MATH_F32 = 0
 KDFM_MATH_BF16 = 1
 
 LD_KC, LD_XC, LD_CONV = 0, 1, 2
+BIG_NT, BIG_NN, BIG_TN = 0, 1, 2   # kdfm_gemm_big operand layouts (include/kdfm.h KDFM_BIG_*)
 
 EPI_BIAS = 1 << 0
 EPI_STORE_PRE = 1 << 1
@@ -127,6 +128,8 @@ SIGNATURES: dict[str, tuple] = {
     "kdfm_wgrad_set_fold_arena": (_i32, [P, P, _i64]),
     "kdfm_wgrad_fold_flush": (_i32, [P]),
     "kdfm_wgrad_fold_pending": (_i64, [P]),
+    "kdfm_wgrad_fold_stats": (_i32, [P, P]),
+    "kdfm_wgrad_fold_discard_all": (_i32, []),
     "kdfm_denoise_wimg_elems": (_i64, []),
     "kdfm_subsample_dgrad_wprep_elems": (_i64, [_i64]),
     "kdfm_subsample_dgrad_wprep": (_i32, [P, P, _i64, P]),
@@ -147,6 +150,9 @@ SIGNATURES: dict[str, tuple] = {
     "kdfm_stream_create_cu_mask": (_i32, [_i32, C.POINTER(C.c_void_p)]),
     "kdfm_memset_async": (_i32, [P, _i32, _i64, P]),
     "kdfm_cast_bf16": (_i32, [P, P, _i64, P]),
+    "kdfm_cast_bf16_2d": (_i32, [P, _i64, P, _i64, _i64, _i64, P]),
+    "kdfm_gemm_big_supported": (_i32, [_i64, _i64, _i64, _i32]),
+    "kdfm_gemm_big": (_i32, [C.POINTER(GemmDesc), P, _i64, P, _i64, _i32, P, P]),
     "kdfm_cast_bf16_t": (_i32, [P, P, P, _i64, _i64, P]),
     "kdfm_colsum": (_i32, [P, P, _i64, _i64, _i64, _f32, _i32, P]),
     "kdfm_preemph_pad": (_i32, [P, P, P, _i64, _i64, _i64, _f32, _f32, P, C.c_uint64, P]),

@@ -50,6 +50,8 @@ _ATTN_DQ3 = __import__("os").environ.get("KDFM_ATTN_DQ3", "1") == "1"
 # a fold launch per product (pair)
 _FOLD_DEFER = __import__("os").environ.get("KDFM_FOLD_DEFER", "1") == "1"
 _FOLD_ARENA_FLOATS = 64 << 20   # 256 MB: a layer's per-split partials at the bench shape are ~18M floats, the heads' ~40M
+# (larger shapes -- the XL layers -- grow it: encoder_backward reads the library's demand / fallback counters before
+# it ends deferral and fold_arena sizes the next step's arena from them)
 
 
 def _attn_fused_ok(dk, save):
@@ -456,13 +458,22 @@ def _ffn_forward(cfg, P, L, which, norm, x, pd, seed, salt, li, site_act, site_o
         return out, out_ln is not None
     ln, m, r = _ln(x, P, norm, cfg.ln_eps, dev)
     h = _empty(rows, ff, dev=dev) if save else None
-    a = _empty(rows, ff, dev=dev)
+    # the hidden activation in bf16 when its producer and every consumer take the large-tile route (d_model >= 512):
+    # the values those products read are bf16-rounded anyway, so this halves its write and skips a cast per read
+    bf_mid = _big_all((rows, ff, d, _lib.BIG_NT), (rows, d, ff, _lib.BIG_NT)) and (
+        not save or _big_all((d, ff, rows, _lib.BIG_TN)))
+    a = torch.empty(rows, ff, device=dev, dtype=torch.bfloat16) if bf_mid else _empty(rows, ff, dev=dev)
     K.linear(ln, W1, P[L + which + ".linear1.bias"], a, epi=_lib.EPI_SILU | (_lib.EPI_STORE_PRE if save else 0), Cpre=h,
              dropout_p=pd, seed=seed, rng_stream=_stream(salt, li, site_act), tag="ffn_up")
     K.linear(a, W2, P[L + which + ".linear2.bias"], out, epi=_lib.EPI_RESID, R=x, rscale=0.5, dropout_p=pd, seed=seed,
              rng_stream=_stream(salt, li, site_out))
     keep(**{"ln" + tag: ln, "m" + tag: m, "r" + tag: r, "h" + tag: h, "a" + tag: a})
     return out, False
+
+
+def _big_all(*shapes):
+    """Every (M, N, K, layout) product takes the large-tile bf16 route (kernels.big_ok)."""
+    return all(K.big_ok(*sh) for sh in shapes)
 
 
 def _fwd3_ok(dk, save):
@@ -724,7 +735,9 @@ def _ffn_backward(P, G, L, which, dres_out, ctx, tag, x_in_ln, norm, pd, seed, s
     dlin2 = _empty(rows, d, dev=dev)
     K.dropout(dres_out, dlin2, pd, 0.5, seed, _stream(salt, li, site_out))
     WGRAD.run(lambda: K.linear_dw(dlin2, a, G[L + which + ".linear2.weight"], db=G[L + which + ".linear2.bias"]), dlin2, a)
-    dh = _empty(rows, ff, dev=dev)
+    # the hidden gradient in bf16 when its producer and both consumers take the large-tile route (as `a` above)
+    bf_mid = _big_all((rows, ff, d, _lib.BIG_NN), (rows, d, ff, _lib.BIG_NN), (ff, d, rows, _lib.BIG_TN))
+    dh = torch.empty(rows, ff, device=dev, dtype=torch.bfloat16) if bf_mid else _empty(rows, ff, dev=dev)
     K.linear_dx(dlin2, P[L + which + ".linear2.weight"], dh, epi=_lib.EPI_DSILU, aux=h, dropout_p=pd, seed=seed,
                 rng_stream=_stream(salt, li, site_act))
     del dlin2
@@ -1065,12 +1078,20 @@ def encoder_forward(cfg, S: EncoderShapes, P, prefix, mel, mel_len, len1, len2, 
 
 
 def fold_arena(ws, dev):
-    """The deferred weight-gradient folds' partial arena of an encoder workspace (bf16 math, KDFM_FOLD_DEFER)."""
+    """The deferred weight-gradient folds' partial arena of an encoder workspace (bf16 math, KDFM_FOLD_DEFER).
+    Sized _FOLD_ARENA_FLOATS, or -- when the previous backward had products that did not fit and folded at once
+    (silent fallbacks at the XL shapes) -- the largest demand the library counted between two flushes.
+    A replaced arena is only ever dropped between steps; a recorded step plan keeps the one it addresses
+    (Ver5Engine.make_plan)."""
     if not _FOLD_DEFER or K.get_math() != "bf16":
         return None
     arena = ws.get("fold_arena")
+    st = ws.pop("fold_stats", None)
+    if arena is not None and st is not None and st[1] > 0 and st[2] > arena.numel():
+        arena = None   # the next backward gets an arena its demand fits (stream order: the old one is idle)
     if arena is None:
-        arena = ws["fold_arena"] = torch.empty(_FOLD_ARENA_FLOATS, device=dev)
+        n = max(_FOLD_ARENA_FLOATS, 0 if st is None else (st[2] + (1 << 20)))
+        arena = ws["fold_arena"] = torch.empty(n, device=dev)
     return arena
 
 
@@ -1117,6 +1138,8 @@ def encoder_backward(cfg, S: EncoderShapes, P, G, prefix, run: EncoderRun, dfeat
     if arena is not None:
         def _end():
             K.wgrad_fold_flush()
+            # demand / fallback counters of this backward (host bookkeeping): fold_arena grows the next arena
+            ws["fold_stats"] = K.wgrad_fold_stats()
             K.wgrad_set_fold_arena(None)
         WGRAD.run(_end)
     WGRAD.join()  # weight gradients computed on the side stream are complete before anyone reads G

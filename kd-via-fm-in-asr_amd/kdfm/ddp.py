@@ -53,9 +53,14 @@ class BucketedGradAllReduce:
     every collective and returns the 1/world mean scale for the fused AdamW.  With no ready() calls
     it is exactly FlatGradAllReduce with `buckets` chunks.  Bucket edges are aligned to 64 floats."""
 
-    def __init__(self, numel: int, group=None, buckets: int = 4):
+    def __init__(self, numel: int, group=None, buckets: int = 4, force: bool = False):
+        """force: issue the collectives even in a world of one rank (they are then identities) -- test-only, so
+        the RCCL path (its own stream ordered behind the issuing one, Work.wait() as a device-side wait, a step
+        plan's replay of the ready() callbacks) runs on a one-GPU box (tests/test_rccl_gpu.py)."""
         self.group = group
         self.world = dist.get_world_size(group)
+        self.active = self.world > 1 or force
+        self.issued = 0   # collectives issued so far (tests count them)
         nb = max(1, int(buckets))
         step = -(-numel // nb)
         step = -(-step // 64) * 64
@@ -79,17 +84,18 @@ class BucketedGradAllReduce:
 
     def _issue(self, chunk: torch.Tensor, k: int):
         """The collective of bucket k, issued on the current (issuing) stream; returns its work handle."""
+        self.issued += 1
         return dist.all_reduce(chunk, group=self.group, async_op=True)
 
     def ready(self, flat: torch.Tensor, offset: int) -> None:
-        if self.world == 1:
+        if not self.active:
             return
         for k in range(len(self.edges) - 2, -1, -1):
             if k not in self._launched and self.edges[k] >= offset:
                 self._launch(flat, k)
 
     def __call__(self, flat: torch.Tensor) -> float:
-        if self.world == 1:
+        if not self.active:
             return 1.0
         for k in range(len(self.edges) - 2, -1, -1):
             if k not in self._launched:

@@ -488,7 +488,13 @@ class Ver5Engine:
         # overlap_wgrad says otherwise
         serial = self.cfg.deterministic if self.overlap_wgrad is None else not self.overlap_wgrad
         with self._on_stream(), self._mode(), WGRAD.serialized(serial), K.region("backward"):
-            self._backward(ctx, grad_ready)
+            try:
+                self._backward(ctx, grad_ready)
+            except BaseException:
+                # a backward that raises between setting the deferred-fold arena and ending deferral leaves
+                # queued folds pointing into the arena: drop them so the next backward starts clean
+                K.wgrad_fold_discard_all()
+                raise
 
     def _backward(self, ctx, grad_ready):
         cfg = self.cfg
@@ -603,10 +609,11 @@ class Ver5Engine:
     def allreduce_grads(self, allreduce) -> float:
         """allreduce(flat gradient) -- the buckets the backward has not launched yet, then the waits -- issued on
         the engine's compute stream, so the last buckets' collectives are ordered after the backward's last
-        gradient writes and AdamW after the collectives by stream order.  (Called from the caller's stream
-        instead, the final buckets were read before the subsampling backward had finished in ~1 of 2 runs of
-        tests/test_ddp_equiv_gpu.py: tools/ddp_equiv_repeat.py, profiles/r05/r5zz.)  Returns the gradient
-        scale (1 / world)."""
+        gradient writes and AdamW after the collectives by stream order.  (Issuing it from the caller's stream is
+        ordered too -- backward() makes that stream wait for the compute stream -- the round-5 intermittent DDP
+        mismatch was the first heads half reading unjoined teacher outputs, fixed in _heads_first_half: DESIGN.md
+        §10, profiles/r05/r5zz7; tools/race_check.py models both issue points.)  Returns the gradient scale
+        (1 / world)."""
         with self._on_stream(), K.region("allreduce"):
             return allreduce(self.student.grad)
 
@@ -652,7 +659,35 @@ class Ver5Engine:
 
         plan.record(step)
         plan.inputs = (wav, wav_len, targets, tgt_len)
+        # the recorded launches address the engine's cached workspaces too (encoder workspaces with the fold
+        # arena, the encoder-level FM workspace, the heads' workspaces): keep those tensors alive with the plan, so
+        # a later forward at another shape (which drops the encoder-FM workspace) or a grown fold arena cannot
+        # free memory a replay still writes
+        plan.keep.append(self._workspace_tensors())
         return plan
+
+    def _workspace_tensors(self):
+        """Every tensor reachable from the engine's lazily created workspaces."""
+        out, seen = [], set()
+
+        def walk(o, depth=0):
+            if depth > 4 or id(o) in seen:
+                return
+            seen.add(id(o))
+            if isinstance(o, torch.Tensor):
+                out.append(o)
+            elif isinstance(o, dict):
+                for v in o.values():
+                    walk(v, depth + 1)
+            elif isinstance(o, (list, tuple)):
+                for v in o:
+                    walk(v, depth + 1)
+            elif hasattr(o, "__dict__") and not isinstance(o, type):
+                for v in vars(o).values():
+                    walk(v, depth + 1)
+        for o in (self._ws, self._encfm, self._pos, self.hws, self.hws_b):
+            walk(o)
+        return out
 
 
 class GraphedTrainStep:

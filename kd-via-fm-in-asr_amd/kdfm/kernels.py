@@ -26,7 +26,7 @@ class _State:
 
 
 ROUTES = {0: "generic", 1: "skinny", 2: "rowstream_fwd", 3: "wide_wgrad", 4: "split_fold", 5: "slab_conv",
-          6: "wgrad_rows"}
+          6: "wgrad_rows", 7: "big"}
 
 
 class Trace:
@@ -370,7 +370,9 @@ def _p(t):
 def gemm(A, B, Cout, M, N, K, sAm, sAk, sBk, sBn, sCm, sCn, *, amode, bmode,
          batch=(1, 1), bA=(0, 0), bB=(0, 0), bC=(0, 0), alpha=1.0, epi=0, bias=None, R=None, rscale=1.0,
          aux=None, Cpre=None, beta=0.0, dropout_p=0.0, seed=None, rng_stream=0, splitk=1,
-         conv=None, math=None, rowmask=None, mse=None, tag=None, ones_out=None, Bh=None, nbytes=None):
+         conv=None, math=None, rowmask=None, mse=None, tag=None, ones_out=None, Bh=None, nbytes=None, big=None):
+    """big = (A16 address, lda, B16 address, ldb, layout, C16 address or 0): the descriptor's epilogue on the
+    large-tile bf16 kernel (kdfm_gemm_big) instead of kdfm_gemm's routes (see _big_linear)."""
     mth = math or _State.math
     bh, sbh = Bh if (Bh is not None and mth == "bf16") else (None, 0)
     ones_col = int(N) - 1 if ones_out is not None else -1
@@ -396,7 +398,11 @@ def gemm(A, B, Cout, M, N, K, sAm, sAk, sBk, sBn, sCm, sCn, *, amode, bmode,
             mlen, int(mT), int(mdiv), lacc, float(lscale), _p(ones_out), ones_col,
             0, 0, bh or 0, sbh]   # Bh: (device address, row stride) of the bf16 twin
     _GEMM_FMT.pack_into(_GEMM_BUF, 0, *vals)
-    if epi == _lib.EPI_ATOMIC and (math_id == _lib.KDFM_MATH_BF16 or (_State.deterministic and splitk > 1)):
+    if big is not None:
+        name, args = "kdfm_gemm_big", (_GEMM_DESC,) + tuple(big) + (_s(),)
+    else:
+        name, args = "kdfm_gemm", (_GEMM_DESC, _s())
+    if big is None and epi == _lib.EPI_ATOMIC and (math_id == _lib.KDFM_MATH_BF16 or (_State.deterministic and splitk > 1)):
         nws = _lib.lib().kdfm_gemm_ws(_GEMM_DESC)
         if nws > 0:
             ws = scratch(Cout.device, nws)
@@ -406,7 +412,7 @@ def gemm(A, B, Cout, M, N, K, sAm, sAk, sBk, sBn, sCm, sCn, *, amode, bmode,
         ev0 = torch.cuda.Event(enable_timing=True)
         ev1 = torch.cuda.Event(enable_timing=True)
         ev0.record()
-        call("kdfm_gemm", _GEMM_DESC, _s())
+        call(name, *args)
         ev1.record()
         if nbytes is None:   # fp32 storage: both operands and the output once, plus each side operand
             side = sum(1 for t in (R, aux, Cpre) if t is not None)
@@ -419,7 +425,59 @@ def gemm(A, B, Cout, M, N, K, sAm, sAk, sBk, sBn, sCm, sCn, *, amode, bmode,
             tr.events.append(("gemm:" + ROUTES.get(int(_lib.lib().kdfm_gemm_last_route()), "?"), fl, nbytes, ev0, ev1,
                               sp))
         return
-    call("kdfm_gemm", _GEMM_DESC, _s())
+    call(name, *args)
+
+
+# ------------------------------------------------------------------------------------------------
+# Large-tile bf16 route (csrc/biggemm.hip, kdfm_gemm_big) for the wide layer products (d_model >= 512:
+# Conformer-large, FastConformer(-XL)).  Operands are bf16 in HBM: a bf16 tensor is read in place, an f32 one is
+# cast into this stream's scratch first (kdfm_cast_bf16_2d); a bf16 `out` receives the product in bf16 (what the
+# next product reads: the FFN hidden activation and its gradient), which only this route can write.
+# KDFM_BIG_GEMM=0: the kdfm_gemm routes (f32 operands only).
+# ------------------------------------------------------------------------------------------------
+_BIG = os.environ.get("KDFM_BIG_GEMM", "1") == "1"
+_BIG_MIN_WORK = float(os.environ.get("KDFM_BIG_MIN_WORK", str(2 ** 31)))   # M * N * K
+
+
+def big_ok(M, N, K, layout) -> bool:
+    """The large-tile route takes this product (bf16 math, every dimension >= 512, M * N * K >= 2^31)."""
+    if not _BIG or _State.math != "bf16" or min(M, N, K) < 512 or float(M) * N * K < _BIG_MIN_WORK:
+        return False
+    return bool(_lib.lib().kdfm_gemm_big_supported(int(M), int(N), int(K), int(layout)))
+
+
+def _bf16_operands(ts):
+    """(address, row stride) of each 2-D operand as bf16: bf16 tensors in place, f32 ones cast into scratch."""
+    need = []
+    for t in ts:
+        if t.dtype == torch.bfloat16:
+            assert t.stride(1) == 1 and t.stride(0) % 8 == 0 and t.data_ptr() % 16 == 0, "bf16 operand layout"
+        else:
+            _f32(t)
+            need.append(t)
+    out = []
+    if need:
+        sizes = [(t.shape[0] * (-(-t.shape[1] // 8) * 8)) for t in need]
+        buf = scratch(need[0].device, (sum(sizes) + 8 * len(sizes)) // 2 + 8).view(torch.bfloat16)
+        off = 0
+        cast = {}
+        for t, n in zip(need, sizes):
+            ld = -(-t.shape[1] // 8) * 8
+            dst = buf.data_ptr() + 2 * off
+            call("kdfm_cast_bf16_2d", ptr(t), t.stride(0), dst, ld, t.shape[0], t.shape[1], _s())
+            cast[id(t)] = (dst, ld)
+            off += n
+    for t in ts:
+        out.append((t.data_ptr(), t.stride(0)) if t.dtype == torch.bfloat16 else cast[id(t)])
+    return out
+
+
+def _big_out(out):
+    """(f32 C tensor or None, bf16 C16 address or 0)."""
+    if out.dtype == torch.bfloat16:
+        assert out.stride(1) == 1
+        return None, out.data_ptr()
+    return _f32(out), 0
 
 
 def _splitk_for(M, N, K):
@@ -432,12 +490,25 @@ def _splitk_for(M, N, K):
 
 def linear(x, W, bias, out, *, epi=0, R=None, rscale=1.0, Cpre=None, dropout_p=0.0, seed=None, rng_stream=0,
            alpha=1.0, math=None, rowmask=None, mse=None, tag=None):
-    """out[M,N] = epi(alpha * x[M,K] @ W[N,K]^T + bias)   (W may be a strided view)"""
+    """out[M,N] = epi(alpha * x[M,K] @ W[N,K]^T + bias)   (W may be a strided view).  x / out may be bf16 on the
+    large-tile route (big_ok(M, N, K, NT))."""
     M, K = x.shape
     N = W.shape[0]
     assert W.shape[1] == K and out.shape[0] == M and out.shape[1] == N, (x.shape, W.shape, out.shape)
     if bias is not None:
         epi |= _lib.EPI_BIAS
+    if (math or _State.math) == "bf16" and mse is None and big_ok(M, N, K, _lib.BIG_NT):
+        (a16, lda), (w16, ldw) = _bf16_operands((x, W))
+        C, c16 = _big_out(out)
+        side = sum(1 for t in (R, Cpre) if t is not None)
+        nb = 2.0 * (M * K + N * K) + (2.0 if c16 else 4.0) * M * N + 4.0 * side * M * N
+        gemm(x, W, C if C is not None else out, M, N, K, 0, 0, 0, 0, out.stride(0), out.stride(1), amode=_lib.LD_KC,
+             bmode=_lib.LD_KC, epi=epi, bias=bias, R=R, rscale=rscale, Cpre=Cpre, dropout_p=dropout_p, seed=seed,
+             rng_stream=rng_stream, alpha=alpha, rowmask=rowmask, tag=tag, nbytes=nb,
+             big=(a16, lda, w16, ldw, _lib.BIG_NT, c16))
+        return
+    _f32(x, "x")
+    _f32(out, "out")
     gemm(x, W, out, M, N, K, x.stride(0), x.stride(1), W.stride(1), W.stride(0), out.stride(0), out.stride(1),
          amode=_lib.LD_KC, bmode=_lib.LD_KC, epi=epi, bias=bias, R=R, rscale=rscale, Cpre=Cpre,
          dropout_p=dropout_p, seed=seed, rng_stream=rng_stream, alpha=alpha, math=math, rowmask=rowmask, mse=mse,
@@ -446,12 +517,23 @@ def linear(x, W, bias, out, *, epi=0, R=None, rscale=1.0, Cpre=None, dropout_p=0
 
 def linear_dx(dy, W, dx, *, epi=0, aux=None, dropout_p=0.0, seed=None, rng_stream=0, R=None, rscale=1.0,
               alpha=1.0, math=None, rowmask=None):
-    """dx[M,K] = epi(alpha * dy[M,N] @ W[N,K])"""
+    """dx[M,K] = epi(alpha * dy[M,N] @ W[N,K]).  dy / dx may be bf16 on the large-tile route (big_ok(M, K, N, NN))."""
     M, N = dy.shape
     K = W.shape[1]
     assert W.shape[0] == N and dx.shape[0] == M and dx.shape[1] == K, (dy.shape, W.shape, dx.shape)
     if R is not None:
         epi |= _lib.EPI_RESID
+    if (math or _State.math) == "bf16" and big_ok(M, K, N, _lib.BIG_NN):
+        (a16, lda), (w16, ldw) = _bf16_operands((dy, W))
+        C, c16 = _big_out(dx)
+        side = sum(1 for t in (R, aux) if t is not None)
+        nb = 2.0 * (M * N + N * K) + (2.0 if c16 else 4.0) * M * K + 4.0 * side * M * K
+        gemm(dy, W, C if C is not None else dx, M, K, N, 0, 0, 0, 0, dx.stride(0), dx.stride(1), amode=_lib.LD_KC,
+             bmode=_lib.LD_XC, epi=epi, aux=aux, dropout_p=dropout_p, seed=seed, rng_stream=rng_stream, R=R,
+             rscale=rscale, alpha=alpha, rowmask=rowmask, nbytes=nb, big=(a16, lda, w16, ldw, _lib.BIG_NN, c16))
+        return
+    _f32(dy, "dy")
+    _f32(dx, "dx")
     gemm(dy, W, dx, M, K, N, dy.stride(0), dy.stride(1), W.stride(0), W.stride(1), dx.stride(0), dx.stride(1),
          amode=_lib.LD_KC, bmode=_lib.LD_XC, epi=epi, aux=aux, dropout_p=dropout_p, seed=seed,
          rng_stream=rng_stream, R=R, rscale=rscale, alpha=alpha, math=math, rowmask=rowmask,
@@ -464,6 +546,16 @@ def linear_dw(dy, x, dW, *, alpha=1.0, math=None, db=None):
     M, N = dy.shape
     K = x.shape[1]
     assert x.shape[0] == M and dW.shape[0] == N and dW.shape[1] == K, (dy.shape, x.shape, dW.shape)
+    if (math or _State.math) == "bf16" and big_ok(N, K, M, _lib.BIG_TN):
+        # dW[n][k] += alpha sum_r dy[r][n] x[r][k]: both operands k-major (the rows are the reduction), one writer
+        # per gradient element, the bias gradient from the same kernel (row sums of dy^T)
+        (a16, lda), (b16, ldb) = _bf16_operands((dy, x))
+        nb = 2.0 * M * (N + K) + 8.0 * N * K
+        gemm(dy, x, dW, N, K, M, 0, 0, 0, 0, dW.stride(0), dW.stride(1), amode=_lib.LD_XC, bmode=_lib.LD_XC,
+             epi=_lib.EPI_ATOMIC, alpha=alpha, ones_out=db, nbytes=nb, big=(a16, lda, b16, ldb, _lib.BIG_TN, 0))
+        return
+    _f32(dy, "dy")
+    _f32(x, "x")
     Kx = K + (1 if db is not None else 0)
     sk = _splitk_for(N, Kx, M)
     gemm(dy, x, dW, N, Kx, M, dy.stride(1), dy.stride(0), x.stride(0), x.stride(1), dW.stride(0), dW.stride(1),
@@ -698,6 +790,20 @@ def wgrad_fold_flush():
 
 def wgrad_fold_pending() -> int:
     return int(_lib.lib().kdfm_wgrad_fold_pending(_s()))
+
+
+def wgrad_fold_stats(stream=None):
+    """(queued folds, fallbacks since the arena was set, peak arena demand in floats) of `stream` (default: the
+    current one): host-side bookkeeping of libkdfm, no device sync."""
+    out = (C.c_int64 * 3)()
+    sp = _s() if stream is None else stream
+    _lib.check(_lib.lib().kdfm_wgrad_fold_stats(sp, out), "kdfm_wgrad_fold_stats")
+    return int(out[0]), int(out[1]), int(out[2])
+
+
+def wgrad_fold_discard_all() -> int:
+    """Error recovery: drop every stream's queued deferred folds and unset every fold arena."""
+    return int(_lib.lib().kdfm_wgrad_fold_discard_all())
 
 
 def wgrad_bf16_pair(dY, X, dW, db, dY2, X2, dW2, db2, *, alpha=1.0):

@@ -247,9 +247,33 @@ def test_bf16_step_matches_float64_oracle(sub):
     2-layer step against the float64 oracle, dropout / SpecAugment / dither off, deterministic reductions.
     Tolerances are the bf16 step's (tests/test_bench_shape_gpu.py): losses rel 3e-3, layer outputs rel.
     Frobenius 1.5e-2, every gradient rel. Frobenius max(5e-2, 2.5 x the oracle's own bf16 sensitivity)."""
-    from dataclasses import replace
-    n_layers, B, N, U = 2, 2, 32000, 12
-    cfg, eng, wav, wl, tg, tgl, g = _build(n_layers, B, N, [32000, 24321], U, [12, 7], sub=dict(sub, math="bf16"))
+    _bf16_step_check(sub, 2, 32000, [32000, 24321], 12, [12, 7])
+
+
+@pytest.mark.parametrize("sub,B,N,lens", [(XL, 8, 96000, [96000] * 7 + [71234]), (CL, 4, 96000, [96000, 80011, 96000, 90000])],
+                         ids=["fastconformer-xl-d1024-8x6s", "conformer-large-d512-4x6s"])
+def test_bf16_step_big_route_matches_float64_oracle(sub, B, N, lens, monkeypatch):
+    """The same check with enough rows (>= 512) that every wide Linear of the layers -- q|k|v, out, both FFNs'
+    up / down projections and the conv module's pointwise convs, their data and weight gradients -- takes the
+    large-tile bf16 route (csrc/biggemm.hip) with its bf16 FFN intermediates (the work floor M N K >= 2^31 is
+    lifted so the d x d products at these row counts take it too)."""
+    from kdfm import kernels as K
+    monkeypatch.setattr(K, "_BIG_MIN_WORK", 0.0)
+    n = {"big": 0}
+    orig = K.call
+
+    def call(name, *a):
+        if name == "kdfm_gemm_big":
+            n["big"] += 1
+        return orig(name, *a)
+    monkeypatch.setattr(K, "call", call)
+    _bf16_step_check(sub, B, N, lens, 12, [12, 7, 9, 5, 12, 11, 3, 8][:B])
+    assert n["big"] >= 2 * 6 * 3, n   # per layer: >= 6 wide products forward (teacher + student) + dX + dW
+
+
+def _bf16_step_check(sub, B, N, lens, U, tl):
+    n_layers = 2
+    cfg, eng, wav, wl, tg, tgl, g = _build(n_layers, B, N, lens, U, tl, sub=dict(sub, math="bf16"))
     from kdfm.config import sub_dims
     T = sub_dims(cfg, N // cfg.hop + 1)[-1][0]
     eps_rows = torch.randn(n_layers * B * T, cfg.latent, generator=g)

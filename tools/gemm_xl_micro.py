@@ -1,25 +1,34 @@
-"""Isolated timing of the FastConformer-XL layer products (d_model 1024, B=32 x 16 s at x8: 6 432 rows) on
-kdfm_gemm (bf16 math) -- the routes the XL step takes at d=1024, where no fused LN-block kernel applies --
-beside torch.matmul (hipBLASLt) on bf16 copies as the library yardstick.  Prints TFLOP/s per product."""
+"""Isolated timing of the FastConformer-XL layer products (d_model 1024, B=32 x 16 s at x8: 6 432 rows) -- the
+routes the XL step takes at d=1024, where no fused LN-block kernel applies -- beside torch.matmul (hipBLASLt) on bf16
+copies as the library yardstick.  Prints TFLOP/s per product and direction:
+  big     : kernels.linear / linear_dx / linear_dw on the large-tile route (csrc/biggemm.hip) with bf16 operands in
+            HBM (the kernel alone: what the XL step's bf16 intermediates feed it);
+  big+cast: the same from f32 operands (each f32 operand cast to bf16 scratch first, kdfm_cast_bf16_2d);
+  generic : the previous route (kdfm_gemm's 64x64 tile / row-parallel weight gradient), f32 operands.
+HIP events around N back-to-back launches (median of 3 rounds)."""
 import os
+import statistics
 import sys
-import time
 
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "kd-via-fm-in-asr_amd"))
 import kdfm  # noqa: E402,F401
 import torch  # noqa: E402
 from kdfm import kernels as K  # noqa: E402
-from kdfm import _lib  # noqa: E402
 
 
-def bench(fn, n=20):
+def bench(fn, n=20, rounds=3):
     fn()
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(n):
-        fn()
-    torch.cuda.synchronize()
-    return (time.perf_counter() - t0) / n
+    ts = []
+    for _ in range(rounds):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(n):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1) * 1e-3 / n)
+    return statistics.median(ts)
 
 
 def main():
@@ -27,24 +36,41 @@ def main():
     K.set_math("bf16")
     M, d = 6432, 1024
     g = torch.Generator(device=dev).manual_seed(0)
-    for (name, N, Kd) in [("ffn_up", 4096, d), ("ffn_down", d, 4096), ("qkv", 3 * d, d), ("out", d, d)]:
+    shapes = [("ffn_up", 4096, d), ("ffn_down", d, 4096), ("qkv", 3 * d, d), ("out", d, d)]
+    if len(sys.argv) > 1 and sys.argv[1] == "large":   # Conformer-large (configs[3] student): d 512, 12 832 rows
+        M, d = 12832, 512
+        shapes = [("ffn_up", 2048, d), ("ffn_down", d, 2048), ("qkv", 3 * d, d), ("out", d, d)]
+    for (name, N, Kd) in shapes:
+        fl = 2.0 * M * N * Kd
         x = torch.randn(M, Kd, device=dev, generator=g)
         W = torch.randn(N, Kd, device=dev, generator=g) * 0.02
         b = torch.randn(N, device=dev, generator=g)
-        y = torch.empty(M, N, device=dev)
-        t = bench(lambda: K.linear(x, W, b, y))
-        route = K.ROUTES.get(int(_lib.lib().kdfm_gemm_last_route()), "?")
         dy = torch.randn(M, N, device=dev, generator=g)
+        x16, dy16 = x.bfloat16(), dy.bfloat16()
+        y = torch.empty(M, N, device=dev)
         dx = torch.empty(M, Kd, device=dev)
-        tdx = bench(lambda: K.linear_dx(dy, W, dx))
         dW = torch.zeros(N, Kd, device=dev)
-        tdw = bench(lambda: K.linear_dw(dy, x, dW))
-        xb, Wb = x.bfloat16(), W.bfloat16()
-        tl = bench(lambda: torch.matmul(xb, Wb.t()))
-        fl = 2.0 * M * N * Kd
-        print(f"{name:9s} M={M} N={N} K={Kd}: fwd {t * 1e6:8.1f} us {fl / t / 1e12:6.1f} TF/s ({route}) | dx "
-              f"{tdx * 1e6:8.1f} us {fl / tdx / 1e12:6.1f} | dW {tdw * 1e6:8.1f} us {fl / tdw / 1e12:6.1f} | "
-              f"hipBLASLt bf16 {tl * 1e6:8.1f} us {fl / tl / 1e12:6.1f}", flush=True)
+        db = torch.zeros(N, device=dev)
+        res = {}
+        res["fwd big"] = bench(lambda: K.linear(x16, W, b, y))
+        res["fwd big+cast"] = bench(lambda: K.linear(x, W, b, y))
+        res["dx big"] = bench(lambda: K.linear_dx(dy16, W, dx))
+        res["dx big+cast"] = bench(lambda: K.linear_dx(dy, W, dx))
+        res["dW big"] = bench(lambda: K.linear_dw(dy16, x16, dW, db=db))
+        res["dW big+cast"] = bench(lambda: K.linear_dw(dy, x, dW, db=db))
+        K._BIG = False
+        try:
+            res["fwd generic"] = bench(lambda: K.linear(x, W, b, y))
+            res["dx generic"] = bench(lambda: K.linear_dx(dy, W, dx))
+            res["dW generic"] = bench(lambda: K.linear_dw(dy, x, dW, db=db))
+        finally:
+            K._BIG = True
+        Wb = W.bfloat16()
+        res["fwd hipBLASLt"] = bench(lambda: torch.matmul(x16, Wb.t()))
+        res["dx hipBLASLt"] = bench(lambda: torch.matmul(dy16, Wb))
+        res["dW hipBLASLt"] = bench(lambda: torch.matmul(dy16.t(), x16))
+        line = " | ".join(f"{k} {v * 1e6:7.1f} us {fl / v / 1e12:6.1f} TF/s" for k, v in res.items())
+        print(f"{name:9s} M={M} N={N} K={Kd}: {line}", flush=True)
 
 
 if __name__ == "__main__":

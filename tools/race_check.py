@@ -22,9 +22,12 @@ only if the old owner's stream never recorded itself on it (Tensor.record_stream
 wait for that stream in real time before reuse, which no stream edge shows).
 
 Usage (on the GPU box):  python tools/race_check.py [--layers N] [--batch B] [--seconds S] [--steps K] [--diffkd]
+    [--deterministic | --serial] [--plan] [--mutate heads_join|bucket_early|allreduce_caller]
 prints one line per distinct conflicting pair (issue site of both accesses) and exits 1 if any.
 tests/test_race_gpu.py runs it on the default overlapped schedule (KD heads in two layer halves, the
-bucketed all-reduce of a world of 2) with use_diffkd off and on.
+bucketed all-reduce of a world of 2) with use_diffkd off and on, on the serialised schedule (deterministic
+and overlap_wgrad=False, heads split on), on a step plan's recording step, and with each --mutate defect
+(which it must report; allreduce_caller is a negative control that must stay clean).
 """
 from __future__ import annotations
 
@@ -371,8 +374,12 @@ def _on_call(name, args):
     from kdfm import kernels as K
     s = _cur()
     site = _site()
-    if name == "kdfm_gemm":
+    if name in ("kdfm_gemm", "kdfm_gemm_big"):
         v = K._GEMM_FMT.unpack_from(K._GEMM_BUF, 0)
+        if name == "kdfm_gemm_big":   # its bf16 operands / output are arguments; the descriptor carries the rest
+            for a, fld, w in ((args[1], "A16", 0), (args[3], "B16", 0), (args[6], "C16", 1)):
+                if a:
+                    T.access(a, T.recent.get(a, a + 4), s, bool(w), site, f"gemm_big.{fld}")
         for idx, fld, w in ((0, "A", 0), (1, "B", 0), (2, "C", 1), (3, "bias", 0), (4, "R", 0), (5, "aux", 0),
                             (6, "Cpre", 1), (28, "seed", 0), (39, "mask_len", 0), (42, "loss_acc", 1),
                             (44, "ones_out", 1)):
@@ -477,8 +484,58 @@ def _on_aten(func, args, kwargs, out):
 # the scenario: the bench's overlapped bf16 step (+ the bucketed all-reduce of a world of 2)
 # ------------------------------------------------------------------------------------------------
 
+MUTATIONS = ("none", "heads_join", "bucket_early", "allreduce_caller")
+
+
+def mutate(kind, eng):
+    """Re-introduce an ordering defect into the step (checker self-test; the GPU then really runs the defect):
+    * heads_join -- the first KD-heads half no longer joins the teacher stream before it reads the teacher
+      features / auto-encoder outputs of layers [0, h) (the round-5 race, fixed in Ver5Engine._heads_first_half);
+    * bucket_early -- the bucketed all-reduce launches every bucket at the backward's first gradient-ready point
+      (after the KD heads), before the encoder layers' gradients are final: the collectives then read gradients
+      the weight-gradient and compute streams still write (a collective issued ahead of its bucket's gradients).
+      (Dropping only the weight-gradient stream's join with the compute stream before a bucket's collective is
+      NOT a race here: every weight-gradient launch already joins it, the last one right before ready() --
+      measured clean on the GPU, profiles/r06/r6a);
+    * allreduce_caller -- the final all-reduce is called from the caller's stream instead of through
+      Ver5Engine.allreduce_grads (the round-5 suspicion).  NOT a race by construction: backward() leaves the
+      caller's stream waiting for the compute stream, so the checker must stay clean (a negative control)."""
+    from kdfm.engine import Ver5Engine
+    from kdfm.overlap import WGRAD
+    if kind == "heads_join":
+        orig = Ver5Engine._heads_first_half
+
+        def heads_first_half(self, *a):
+            side = a[-1]
+            ws_orig = torch.cuda.Stream.wait_stream
+
+            def wait_stream(self_, other):
+                if other.cuda_stream == side.cuda_stream:
+                    return None   # the dropped join
+                return ws_orig(self_, other)
+            torch.cuda.Stream.wait_stream = wait_stream
+            try:
+                return orig(self, *a)
+            finally:
+                torch.cuda.Stream.wait_stream = ws_orig
+        Ver5Engine._heads_first_half = heads_first_half
+    elif kind == "bucket_early":
+        from kdfm.ddp import BucketedGradAllReduce
+        orig_ready = BucketedGradAllReduce.ready
+        BucketedGradAllReduce.ready = lambda self, flat, offset: orig_ready(self, flat, 0)
+    elif kind == "allreduce_caller":
+        def allreduce_grads(self, allreduce):
+            return allreduce(self.student.grad)
+        eng.allreduce_grads = allreduce_grads.__get__(eng)
+    elif kind != "none":
+        raise ValueError(kind)
+
+
 def run(layers=3, batch=8, seconds=16.0, steps=2, ddp=True, deterministic=False, math="bf16", verbose=True,
-        diffkd=False):
+        diffkd=False, serial=False, mutation="none", plan=False):
+    """serial: weight gradients and the first heads half in line (the deterministic schedule's stream structure
+    without its ordered reductions); plan: the checked steps are a step plan's recording step (its host
+    callbacks and launches as recorded) followed by eager steps."""
     from dataclasses import replace
 
     from kdfm import kernels as K
@@ -492,6 +549,9 @@ def run(layers=3, batch=8, seconds=16.0, steps=2, ddp=True, deterministic=False,
     tr = Tracer()
     install(tr)
     eng = Ver5Engine(cfg, dev)
+    if serial:
+        eng.overlap_wgrad = False
+    mutate(mutation, eng)
     eng.set_seed(5)
     n = int(16000 * seconds)
     wav, wl, tg, tl = synthetic_batch(cfg, batch, n, 40, dev, seed=11)
@@ -509,14 +569,17 @@ def run(layers=3, batch=8, seconds=16.0, steps=2, ddp=True, deterministic=False,
         roles[torch.cuda.current_stream().cuda_stream] = roles.get(torch.cuda.current_stream().cuda_stream, "caller")
         tr.roles.update(roles)
         tr.active = True
-        for _ in range(steps):
-            eng.train_step(wav, wl, tg, tl, allreduce=ar)
+        for i in range(steps):
+            if plan and i == 0:
+                eng.make_plan(wav, wl, tg, tl, ar)
+            else:
+                eng.train_step(wav, wl, tg, tl, allreduce=ar)
         tr.active = False
         torch.cuda.synchronize()
     if verbose:
         print(f"race_check: layers={layers} B={batch} {seconds}s steps={steps} ddp={ddp} math={math} "
-              f"deterministic={deterministic} diffkd={diffkd} heads_split={eng.heads_split}: {tr.naccess} accesses, "
-              f"{len(tr.vc)} streams, "
+              f"deterministic={deterministic} serial={eng._serial()} plan={plan} mutation={mutation} diffkd={diffkd} "
+              f"heads_split={eng.heads_split}: {tr.naccess} accesses, {len(tr.vc)} streams, "
               f"{len(tr.conflicts)} conflicting site pairs")
     return tr
 
@@ -531,8 +594,12 @@ def main():
     ap.add_argument("--math", default="bf16")
     ap.add_argument("--deterministic", action="store_true")
     ap.add_argument("--diffkd", action="store_true")
+    ap.add_argument("--serial", action="store_true", help="weight gradients in line (overlap_wgrad=False)")
+    ap.add_argument("--plan", action="store_true", help="the first checked step records a step plan")
+    ap.add_argument("--mutate", default="none", choices=MUTATIONS, help="checker self-test: re-introduce a defect")
     a = ap.parse_args()
-    tr = run(a.layers, a.batch, a.seconds, a.steps, not a.no_ddp, a.deterministic, a.math, diffkd=a.diffkd)
+    tr = run(a.layers, a.batch, a.seconds, a.steps, not a.no_ddp, a.deterministic, a.math, diffkd=a.diffkd,
+             serial=a.serial, mutation=a.mutate, plan=a.plan)
     n = tr.report()
     sys.exit(1 if n else 0)
 
