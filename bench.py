@@ -134,7 +134,7 @@ def sensitivity(dev, samples, steps=3, **overrides):
     eng = Ver5Engine(cfg, dev)
     eng.set_seed(1000)
     wav, wl, tg, tl = synthetic_batch(cfg, B_PER_GPU, samples, U_TOKENS, dev, seed=1234)
-    with K.mode(cfg.math):
+    with K.mode(cfg.math, fp8=cfg.linear_fp8):
         eng.train_step(wav, wl, tg, tl)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -495,7 +495,7 @@ def main():
             threads = args.cpu_threads or _usable_cpus()
             cpu = cpu_baseline(threads, args.samples)
             cpu["cgroup_cpu_max"] = _cgroup_cpu_max()
-        f32 = v1024 = encfm = xl = None
+        f32 = v1024 = encfm = xl = xl8 = None
         if not args.no_f32_sensitivity and cfg.math == "bf16" and world == 1:
             _progress("f32 sensitivity")
             f32 = sensitivity(dev, args.samples, math="f32")
@@ -510,7 +510,14 @@ def main():
             xl = sensitivity(dev, args.samples, **XL_SHAPES)
             xl["note"] = ("BASELINE.json configs[4]'s layer shapes (FastConformer-XL: d_model 1024, 8 heads, head dim "
                           "128, 24 layers, dw_striding x8, kernel 9, no xscaling) for student and teacher on the same "
-                          "16 s x B=32 workload, bf16 (fp8 is not built); not the headline value")
+                          "16 s x B=32 workload, bf16 (the wide Linear products on the large-tile route, "
+                          "csrc/biggemm.hip); not the headline value")
+            _progress("FastConformer-XL fp8 sensitivity")
+            xl8 = sensitivity(dev, args.samples, linear_fp8=True, **XL_SHAPES)
+            xl8["note"] = ("configs[4] at its stated precision: the same XL step with the wide Linear products' forward "
+                           "and data gradients on fp8 e4m3 operands (per-tensor current scaling, block-scaled MFMA "
+                           "v_mfma_scale_f32_16x16x128_f8f6f4); attention core and weight gradients bf16; not the "
+                           "headline value")
         line = {
             "metric": "utterances/sec (FM-distill train step, Conformer-CTC-small) at 1/2/4/8 MI355X",
             "value": round(utt, 3),
@@ -550,6 +557,7 @@ def main():
             "vocab_1024_sensitivity": v1024,
             "encoder_fm_router_sensitivity": encfm,
             "xl_shape_sensitivity": xl,
+            "xl_fp8_sensitivity": xl8,
             "losses_last_step": [round(x, 5) for x in losses],
         }
         print(json.dumps(line))

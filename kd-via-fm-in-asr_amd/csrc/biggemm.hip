@@ -46,6 +46,16 @@ struct BigP {
   float* ones_out;    // ones_out[m] += alpha * sum_k A(m, k) (accumulate mode)
   int accum;          // C[m][n] += alpha * acc
   int tn;             // column tiles
+  // split reduction (the weight-gradient layout when its tiles alone cannot fill the chip): split s sums K rows
+  // [s kchunk, min(K, (s + 1) kchunk)) into raw partials ws[s][m][n] (bias: wsb[s][m]), folded in split order by
+  // big_fold_kernel (deterministic)
+  int splits;
+  int64_t kchunk;
+  float* ws;
+  float* wsb;
+  // fp8 instance (e4m3 operands): per-tensor dequantisation factors (device scalars; C = alpha sa sb sum_k a b)
+  const float* sa;
+  const float* sb;
   GemmP g;            // M, N, K, C, strides and the epilogue fields
 };
 
@@ -75,6 +85,23 @@ __device__ __forceinline__ bf16x8 frag_kc(const uint16_t* img, int r0, int hh, i
   return v;
 }
 
+typedef int bg_v8i __attribute__((ext_vector_type(8)));
+
+// fp8 fragment of 16 rows x 128 k out of a k-contiguous [rows][128 bytes] image (the bf16 image's byte layout):
+// v_mfma_scale_f32_16x16x128_f8f6f4's operand map, lane l -> row r0 + (l & 15), k = 32 (l >> 4) + j (bytes
+// 32 (l >> 4) .. + 31 of the row: chunks 2 (l >> 4) and 2 (l >> 4) + 1; tools/fp8_probe.py measured the map)
+__device__ __forceinline__ bg_v8i frag_kc8(const uint16_t* img, int r0, int lane) {
+  const int r = r0 + (lane & 15);
+  const int g = lane >> 4;
+  const uint32_t a0 = lds_addr(img + r * BG_BK + 8 * ((2 * g) ^ kc_swz(r)));
+  const uint32_t a1 = lds_addr(img + r * BG_BK + 8 * ((2 * g + 1) ^ kc_swz(r)));
+  typedef int v4i __attribute__((ext_vector_type(4)));
+  v4i lo, hi;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(lo) : "v"(a0));
+  asm volatile("ds_read_b128 %0, %1" : "=v"(hi) : "v"(a1));
+  return bg_v8i{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
 // fragment of 16 columns x 32 k out of a k-major [64][W] image: lane l (g = l >> 4, li = l & 15) -> column
 // c0 + li, k = 32 hh + 8 g + e (e < 4: first transposed read, rows 32 hh + 8 g + q; e >= 4: rows + 4)
 template <int W>
@@ -89,8 +116,10 @@ __device__ __forceinline__ bf16x8 frag_km(const uint16_t* img, int c0, int hh, i
   return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
-template <int BM, int BN, int WM, int WN, bool AT, bool BT, int EMODE>
+template <int BM, int BN, int WM, int WN, bool AT, bool BT, int EMODE, bool F8 = false>
 __global__ __launch_bounds__(WM* WN * 64) void big_gemm_kernel(BigP p) {
+  static_assert(!F8 || (!AT && !BT), "the fp8 instance is k-contiguous only");
+  constexpr int KSTEP = F8 ? 2 * BG_BK : BG_BK;   // k per stage: 128-byte image rows either way
   constexpr int NW = WM * WN;
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int FM = WTM / 16, FN = WTN / 16;
@@ -102,15 +131,19 @@ __global__ __launch_bounds__(WM* WN * 64) void big_gemm_kernel(BigP p) {
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wr = wave / WN, wc = wave % WN;
-  const int64_t tile = xcd_block();
+  const int64_t blk = xcd_block();   // the splits of one tile are neighbours (one XCD)
+  const int64_t tile = blk / p.splits;
+  const int sp = (int)(blk - tile * p.splits);
   const int64_t tm = tile / p.tn, tnn = tile % p.tn;
   const int64_t m0 = tm * BM, n0 = tnn * BN;
-  const int64_t M = p.g.M, N = p.g.N, K = p.g.K;
-  const int nk = (int)((K + BG_BK - 1) / BG_BK);
+  const int64_t M = p.g.M, N = p.g.N;
+  const int64_t kb = (int64_t)sp * p.kchunk;
+  const int64_t K = (kb + p.kchunk < p.g.K) ? kb + p.kchunk : p.g.K;   // this split's end row
+  const int nk = K > kb ? (int)((K - kb + KSTEP - 1) / KSTEP) : 0;
 
   // DMA of K step t into stage buffer s: exactly PW wave-instructions per wave
   auto issue = [&](int t, int s) {
-    const int64_t k0 = (int64_t)t * BG_BK;
+    const int64_t k0 = kb + (int64_t)t * KSTEP;
     uint16_t* buf = bg_lds + s * STAGE;
 #pragma unroll
     for (int i = 0; i < PW; ++i) {
@@ -128,7 +161,10 @@ __global__ __launch_bounds__(WM* WN * 64) void big_gemm_kernel(BigP p) {
         const int c = (lane & 7) ^ kc_swz(row);
         int64_t gr = r0 + row;
         gr = gr < R ? gr : R - 1;
-        src = X + gr * ld + k0 + 8 * c;
+        if constexpr (F8)
+          src = reinterpret_cast<const uint16_t*>(reinterpret_cast<const char*>(X) + gr * ld + k0 + 16 * c);
+        else
+          src = X + gr * ld + k0 + 8 * c;
       } else {     // [64 k][W cols], 1024 / (2 W) rows per piece
         const int byte = 1024 * fl + 16 * lane;
         const int row = byte / (2 * W);
@@ -159,7 +195,7 @@ __global__ __launch_bounds__(WM* WN * 64) void big_gemm_kernel(BigP p) {
 #pragma unroll
   for (int e = 0; e < 8; ++e) ones[e] = (short)0x3F80;   // bf16(1.0)
 
-  issue(0, 0);
+  if (nk > 0) issue(0, 0);
   for (int t = 0; t < nk; ++t) {
     __builtin_amdgcn_s_waitcnt((0) | (7 << 4) | (15 << 8));   // vmcnt(0): this wave's pieces of step t landed
     __builtin_amdgcn_s_barrier();                              // ... every wave's; step t - 1's reads are done
@@ -167,7 +203,7 @@ __global__ __launch_bounds__(WM* WN * 64) void big_gemm_kernel(BigP p) {
     const uint16_t* abuf = bg_lds + s * STAGE;
     const uint16_t* bbuf = abuf + AIMG;
     if constexpr (AT || BT) {
-      const int64_t vr = K - (int64_t)t * BG_BK;
+      const int64_t vr = K - kb - (int64_t)t * BG_BK;
       if (vr < BG_BK) {   // tail step: zero the k-major A (or B) rows past K (their DMA read clamped rows)
         uint16_t* z = bg_lds + s * STAGE + (AT ? 0 : AIMG);
         constexpr int ZW = AT ? BM : BN;
@@ -176,9 +212,29 @@ __global__ __launch_bounds__(WM* WN * 64) void big_gemm_kernel(BigP p) {
       }
     }
     if (t + 1 < nk) issue(t + 1, s ^ 1);
+    if constexpr (F8) {   // one block-scaled fp8 MFMA per accumulator tile covers the stage's 128 k (unit scales)
+      bg_v8i af[FM], bfr[FN];
 #pragma unroll
-    for (int hh = 0; hh < 2; ++hh) {
-      bf16x8 af[FM], bfr[FN];
+      for (int i = 0; i < FM; ++i) af[i] = frag_kc8(abuf, wr * WTM + 16 * i, lane);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bfr[j] = frag_kc8(bbuf, wc * WTN + 16 * j, lane);
+      lgkm_wait<0>();
+#pragma unroll
+      for (int i = 0; i < FM; ++i) asm volatile("" : "+v"(af[i]));
+#pragma unroll
+      for (int j = 0; j < FN; ++j) asm volatile("" : "+v"(bfr[j]));
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[i], bfr[j], acc[i][j], 0, 0, 0, 0x7F7F7F7F, 0,
+                                                                       0x7F7F7F7F);
+      continue;
+    }
+    // fragment reads of a k half, then its MFMAs; with registers to spare (<= 16 accumulator tiles per wave) the
+    // second half's reads are issued before the first half's MFMAs, so their LDS latency hides behind them
+    auto read_frags = [&](int hh, bf16x8 (&af)[FM], bf16x8 (&bfr)[FN]) {
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
         const int r = wr * WTM + 16 * i;
@@ -191,12 +247,15 @@ __global__ __launch_bounds__(WM* WN * 64) void big_gemm_kernel(BigP p) {
         if constexpr (BT) bfr[j] = frag_km<BN>(bbuf, c, hh, lane);
         else bfr[j] = frag_kc(bbuf, c, hh, lane);
       }
-      lgkm_wait<0>();
+    };
+    auto tie = [&](bf16x8 (&af)[FM], bf16x8 (&bfr)[FN]) {
 #pragma unroll
       for (int i = 0; i < FM; ++i) asm volatile("" : "+v"(af[i]));
 #pragma unroll
       for (int j = 0; j < FN; ++j) asm volatile("" : "+v"(bfr[j]));
       __builtin_amdgcn_sched_barrier(0);
+    };
+    auto mfmas = [&](bf16x8 (&af)[FM], bf16x8 (&bfr)[FN]) {
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
 #pragma unroll
@@ -204,13 +263,57 @@ __global__ __launch_bounds__(WM* WN * 64) void big_gemm_kernel(BigP p) {
         if constexpr (BIAS)
           if (do_bias) accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], ones, accb[i], 0, 0, 0);
       }
+    };
+    constexpr bool PIPE = FM * FN <= 16;
+    if constexpr (PIPE) {
+      bf16x8 a0[FM], b0[FN], a1[FM], b1[FN];
+      read_frags(0, a0, b0);
+      lgkm_wait<0>();
+      read_frags(1, a1, b1);
+      tie(a0, b0);
+      mfmas(a0, b0);
+      lgkm_wait<0>();
+      tie(a1, b1);
+      mfmas(a1, b1);
+    } else {
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        bf16x8 af[FM], bfr[FN];
+        read_frags(hh, af, bfr);
+        lgkm_wait<0>();
+        tie(af, bfr);
+        mfmas(af, bfr);
+      }
     }
   }
 
   // ---- epilogue ----
   const GemmP& g = p.g;
-  const float alpha = g.alpha;
+  float alpha = g.alpha;
+  if constexpr (F8) alpha *= (p.sa ? *p.sa : 1.f) * (p.sb ? *p.sb : 1.f);
   if constexpr (EMODE == BG_ACC || EMODE == BG_ACCB) {
+    if (p.splits > 1) {   // raw partials of this split (plain stores; big_fold_kernel adds them in split order)
+      float* w = p.ws + (int64_t)sp * M * N;
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int64_t mb = m0 + wr * WTM + 16 * i + 4 * (lane >> 4);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int64_t n = n0 + wc * WTN + 16 * j + (lane & 15);
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (mb + r < M && n < N) w[(mb + r) * N + n] = acc[i][j][r];
+        }
+        if constexpr (BIAS) {
+          if (do_bias && (lane & 15) == 0) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (mb + r < M) p.wsb[(int64_t)sp * M + mb + r] = accb[i][r];
+          }
+        }
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
       const int64_t mb = m0 + wr * WTM + 16 * i + 4 * (lane >> 4);
@@ -244,6 +347,70 @@ __global__ __launch_bounds__(WM* WN * 64) void big_gemm_kernel(BigP p) {
   bool single;
   const float* side = epi_side_src(g, single);
   float mse_part = 0.f;
+  auto epi1 = [&](int64_t m, int64_t n, float a, float bnv, float svv, bool rokv, float& pre) -> float {
+    if constexpr (EMODE == BG_DSILU_DROP) {
+      float v = a;
+      if (epi & KDFM_EPI_DROPOUT) {
+        const uint64_t idx = (uint64_t)m * (uint64_t)N + (uint64_t)n;
+        v = dropout_keep(seed, g.rng_stream, idx, g.dropout_p) ? v * keep_scale : 0.f;
+      }
+      return v * dsiluf_(svv);
+    } else {
+      return skc_epi<EMODE>(g, m, n, a, bnv, svv, rokv, seed, keep_scale, mse_part, pre, 0);
+    }
+  };
+  // Row-contiguous epilogue: each 16-row strip of the wave's tile is transposed through LDS (free after the main
+  // loop) so a lane finishes 4 consecutive columns of one row -- 16-byte side-operand loads and output stores,
+  // 16 lanes per 256-byte row segment (the accumulator layout gives a lane 4 rows of one column: 4-byte stores).
+  constexpr int SLD = WTN + 4;   // strip row stride (floats)
+  const uintptr_t al = (uintptr_t)(p.C16 ? (const void*)p.C16 : (const void*)g.C) |
+                       (uintptr_t)((epi & KDFM_EPI_STORE_PRE) ? g.Cpre : nullptr) | (uintptr_t)side |
+                       (uintptr_t)((epi & KDFM_EPI_BIAS) ? g.bias : nullptr);
+  const bool vec = (N % 4) == 0 && g.sCn == 1 && (g.sCm % 4) == 0 && (al & (p.C16 ? 7 : 15)) == 0 &&
+                   (((uintptr_t)g.Cpre | (uintptr_t)side | (uintptr_t)g.bias) & 15) == 0;
+  if (vec) {
+    __syncthreads();   // every wave has finished reading the last stage: the LDS is reused below
+    float* strip = reinterpret_cast<float*>(bg_lds) + wave * (16 * SLD);
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) strip[(4 * (lane >> 4) + r) * SLD + 16 * j + (lane & 15)] = acc[i][j][r];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      constexpr int C4 = WTN / 4;   // float4 groups per strip row
+#pragma unroll
+      for (int q = 0; q < 16 * C4 / 64; ++q) {
+        const int f = q * 64 + lane;
+        const int row = f / C4, c4 = f % C4;
+        const float4 a4 = *reinterpret_cast<const float4*>(strip + row * SLD + 4 * c4);
+        const int64_t m = m0 + wr * WTM + 16 * i + row;
+        const int64_t n = n0 + wc * WTN + 4 * c4;
+        if (m >= M || n >= N) continue;
+        const int64_t off = m * g.sCm + n;
+        float4 b4 = make_float4(0.f, 0.f, 0.f, 0.f), s4 = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (epi & KDFM_EPI_BIAS) b4 = *reinterpret_cast<const float4*>(g.bias + n);
+        if (side) s4 = *reinterpret_cast<const float4*>(side + off);
+        const bool rokv = epi_row_ok(g, m);
+        float pre[4] = {0.f, 0.f, 0.f, 0.f};
+        const float o0 = epi1(m, n + 0, alpha * a4.x, b4.x, s4.x, rokv, pre[0]);
+        const float o1 = epi1(m, n + 1, alpha * a4.y, b4.y, s4.y, rokv, pre[1]);
+        const float o2 = epi1(m, n + 2, alpha * a4.z, b4.z, s4.z, rokv, pre[2]);
+        const float o3 = epi1(m, n + 3, alpha * a4.w, b4.w, s4.w, rokv, pre[3]);
+        if (epi & KDFM_EPI_STORE_PRE) *reinterpret_cast<float4*>(g.Cpre + off) = make_float4(pre[0], pre[1], pre[2], pre[3]);
+        if (p.C16) {
+          uint2 h;
+          h.x = pack_bf16x2(o0, o1);
+          h.y = pack_bf16x2(o2, o3);
+          *reinterpret_cast<uint2*>(p.C16 + off) = h;
+        } else {
+          *reinterpret_cast<float4*>(g.C + off) = make_float4(o0, o1, o2, o3);
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this strip's reads are done before the next writes
+    }
+    return;
+  }
   float bn[FN];
 #pragma unroll
   for (int j = 0; j < FN; ++j) {
@@ -278,18 +445,7 @@ __global__ __launch_bounds__(WM* WN * 64) void big_gemm_kernel(BigP p) {
         if (m >= M || n >= N) continue;
         const int64_t off = m * g.sCm + n * g.sCn;
         float pre = 0.f;
-        float v;
-        if constexpr (EMODE == BG_DSILU_DROP) {
-          v = alpha * acc[i][j][r];
-          if (epi & KDFM_EPI_DROPOUT) {
-            const uint64_t idx = (uint64_t)m * (uint64_t)N + (uint64_t)n;
-            v = dropout_keep(seed, g.rng_stream, idx, g.dropout_p) ? v * keep_scale : 0.f;
-          }
-          v *= dsiluf_(sv[jj][r]);
-        } else {
-          v = skc_epi<EMODE>(g, m, n, alpha * acc[i][j][r], bn[j], sv[jj][r], rok[r], seed, keep_scale, mse_part, pre,
-                             0);
-        }
+        const float v = epi1(m, n, alpha * acc[i][j][r], bn[j], sv[jj][r], rok[r], pre);
         if (epi & KDFM_EPI_STORE_PRE) g.Cpre[off] = pre;
         if (p.C16) p.C16[off] = f2bf(v);
         else g.C[off] = v;
@@ -300,9 +456,31 @@ __global__ __launch_bounds__(WM* WN * 64) void big_gemm_kernel(BigP p) {
   }
 }
 
-template <int BM, int BN, int WM, int WN, bool AT, bool BT, int EMODE>
+// C[m][n] += alpha sum_s ws[s][m][n] (s in order), 4 columns per thread; then ones_out[m] += alpha sum_s wsb[s][m]
+__global__ __launch_bounds__(256) void big_fold_kernel(float* C, int64_t sCm, const float* ws, const float* wsb,
+                                                       float* ones, int64_t M, int64_t N, int S, float alpha) {
+  const int64_t n4 = N / 4, MN = M * N;
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e < M * n4) {
+    const int64_t m = e / n4, n = (e - m * n4) * 4;
+    float4 a = *reinterpret_cast<const float4*>(ws + m * N + n);
+    for (int s = 1; s < S; ++s) {
+      const float4 b = *reinterpret_cast<const float4*>(ws + s * MN + m * N + n);
+      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    }
+    float* c = C + m * sCm + n;
+    c[0] += alpha * a.x; c[1] += alpha * a.y; c[2] += alpha * a.z; c[3] += alpha * a.w;
+  } else if (ones && e - M * n4 < M) {
+    const int64_t m = e - M * n4;
+    float a = wsb[m];
+    for (int s = 1; s < S; ++s) a += wsb[s * M + m];
+    ones[m] += alpha * a;
+  }
+}
+
+template <int BM, int BN, int WM, int WN, bool AT, bool BT, int EMODE, bool F8 = false>
 int big_launch(const BigP& p, hipStream_t st) {
-  auto kern = big_gemm_kernel<BM, BN, WM, WN, AT, BT, EMODE>;
+  auto kern = big_gemm_kernel<BM, BN, WM, WN, AT, BT, EMODE, F8>;
   constexpr int lds = 2 * (BM + BN) * BG_BK * 2;
   static const bool once = [&] {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
@@ -312,8 +490,16 @@ int big_launch(const BigP& p, hipStream_t st) {
   const int64_t tm = ceil_div(p.g.M, BM), tn = ceil_div(p.g.N, BN);
   BigP q = p;
   q.tn = (int)tn;
-  hipLaunchKernelGGL(kern, dim3((unsigned)(tm * tn)), dim3(WM * WN * 64), lds, st, q);
-  return check_launch("kdfm_gemm_big");
+  if (q.splits < 1) q.splits = 1;
+  q.kchunk = ceil_div(ceil_div(p.g.K, q.splits), BG_BK) * BG_BK;
+  if (F8) q.kchunk = p.g.K;
+  hipLaunchKernelGGL(kern, dim3((unsigned)(tm * tn * q.splits)), dim3(WM * WN * 64), lds, st, q);
+  int rc = check_launch("kdfm_gemm_big");
+  if (rc || q.splits == 1) return rc;
+  const int64_t n = p.g.M * (p.g.N / 4) + (p.ones_out ? p.g.M : 0);
+  hipLaunchKernelGGL(big_fold_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, st, p.g.C, p.g.sCm, q.ws, q.wsb,
+                     p.ones_out, p.g.M, p.g.N, q.splits, p.g.alpha);
+  return check_launch("kdfm_gemm_big (split fold)");
 }
 
 // compile-time epilogue per layout (the generic instance covers every flag set)
@@ -338,6 +524,20 @@ int big_epi(const BigP& p, hipStream_t st) {
       if constexpr (BM == 256 && BN == 256) return KDFM_EUNSUPPORTED;   // big_dispatch never picks it (spills)
       else return big_launch<BM, BN, WM, WN, AT, BT, SKC_EPI_GENERIC>(p, st);
   }
+  }
+}
+
+// fp8 instances: the forward and data-gradient products (k-contiguous operands), 256 x 128 / 128 x 128 tiles
+template <int BM, int BN, int WM, int WN>
+int big_epi_f8(const BigP& p, hipStream_t st) {
+  if ((p.g.epi & ~KDFM_EPI_DROPOUT) == KDFM_EPI_DSILU)
+    return big_launch<BM, BN, WM, WN, false, false, BG_DSILU_DROP, true>(p, st);
+  switch (skc_epi_mode(p.g.epi)) {
+    case SKC_EPI_NONE: return big_launch<BM, BN, WM, WN, false, false, SKC_EPI_NONE, true>(p, st);
+    case SKC_EPI_SILU_DROP: return big_launch<BM, BN, WM, WN, false, false, SKC_EPI_SILU_DROP, true>(p, st);
+    case SKC_EPI_DROP_RESID: return big_launch<BM, BN, WM, WN, false, false, SKC_EPI_DROP_RESID, true>(p, st);
+    case SKC_EPI_RESID: return big_launch<BM, BN, WM, WN, false, false, SKC_EPI_RESID, true>(p, st);
+    default: return big_launch<BM, BN, WM, WN, false, false, SKC_EPI_GENERIC, true>(p, st);
   }
 }
 
@@ -369,15 +569,112 @@ int big_pick(int64_t M, int64_t N) {
   return best;
 }
 
+// weight-gradient layout: the 256 x 128 tile, and split reductions when its tiles alone leave CUs idle (at least 8
+// K steps per split, at most 8 splits); KDFM_BIG_SPLIT forces a count
+int big_splits(int64_t M, int64_t N, int64_t K) {
+  const char* e = getenv("KDFM_BIG_SPLIT");
+  const int64_t tiles = ceil_div(M, 256) * ceil_div(N, 128);
+  int64_t S = e ? atoi(e) : (256 + tiles / 2) / tiles;
+  const int64_t smax = K / (8 * BG_BK);
+  if (S > 8) S = 8;
+  if (S > smax) S = smax;
+  if ((N % 4) != 0) S = 1;
+  return S < 1 ? 1 : (int)S;
+}
+
 template <bool AT, bool BT>
-int big_dispatch(const BigP& p, hipStream_t st) {
+int big_dispatch(BigP p, hipStream_t st) {
   const char* e = getenv("KDFM_BIG_TILE");   // 0 / 1 / 2 forces a tile shape (A/B probes)
   int c = e ? atoi(e) : big_pick(p.g.M, p.g.N);
+  if (AT && BT) {
+    if (!e) c = 1;
+    const int S = big_splits(p.g.M, p.g.N, p.g.K);
+    const int64_t need = (int64_t)S * p.g.M * p.g.N + (int64_t)S * p.g.M;
+    if (S > 1 && p.g.ws && p.g.ws_len >= need && p.g.sCn == 1) {
+      p.splits = S;
+      p.ws = p.g.ws;
+      p.wsb = p.g.ws + (int64_t)S * p.g.M * p.g.N;
+    }
+  }
   // the 256 x 256 tile has no generic-epilogue instance, and its bias-gradient accumulators spill
   if (c == 0 && (!big_epi_compiled(p) || p.ones_out)) c = 1;
   if (c == 0) return big_epi<256, 256, 2, 4, AT, BT>(p, st);
   if (c == 1) return big_epi<256, 128, 4, 2, AT, BT>(p, st);
   return big_epi<128, 128, 2, 2, AT, BT>(p, st);
+}
+
+// ---- fp8 e4m3 per-tensor quantisation (current scaling): amax, then q = sat(x * 448 / amax) ----
+__device__ __forceinline__ float bg_load(const void* src, int bf, int64_t i) {
+  return bf ? __uint_as_float(((uint32_t) reinterpret_cast<const uint16_t*>(src)[i]) << 16)
+            : reinterpret_cast<const float*>(src)[i];
+}
+
+__global__ __launch_bounds__(256) void amax_kernel(const void* src, int bf, int64_t rows, int64_t cols, int64_t ld,
+                                                   unsigned* out) {
+  float m = 0.f;
+  const int64_t n = rows * cols;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int64_t r = i / cols, c = i - r * cols;
+    m = fmaxf(m, fabsf(bg_load(src, bf, r * ld + c)));
+  }
+  m = wave_max(m);
+  __shared__ float red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    atomicMax(out, __float_as_uint(m));   // non-negative floats order as their bit patterns: exact, order-free
+  }
+}
+
+__device__ __forceinline__ float bg_qscale(const unsigned* amax) {
+  const float a = __uint_as_float(*amax);
+  return (a > 0.f && a < 3.0e38f) ? 448.f / a : 1.f;
+}
+
+// dst[r * ldd + c] (or, transposed, dst[c * ldd + r]) = e4m3(sat(x[r][c] * s)), s = 448 / amax; dscale = 1 / s.
+// The transposed form (weights for the data gradient: W^T rows) goes through a 64 x 64 LDS tile.
+template <bool TR>
+__global__ __launch_bounds__(256) void quant_kernel(const void* src, int bf, int64_t rows, int64_t cols, int64_t ld,
+                                                    uint8_t* dst, int64_t ldd, const unsigned* amax, float* dscale) {
+  const float sc = bg_qscale(amax);
+  if (blockIdx.x == 0 && threadIdx.x == 0 && dscale) *dscale = 1.f / sc;
+  auto q2 = [&](float a, float b) -> uint32_t {
+    a = fminf(fmaxf(a * sc, -448.f), 448.f);
+    b = fminf(fmaxf(b * sc, -448.f), 448.f);
+    return (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false) & 0xFFFFu;
+  };
+  if constexpr (!TR) {
+    const int64_t c4 = cols / 4, n = rows * c4;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+      const int64_t r = i / c4, c = (i - r * c4) * 4;
+      const int64_t o = r * ld + c;
+      const uint32_t w = q2(bg_load(src, bf, o), bg_load(src, bf, o + 1)) |
+                         (q2(bg_load(src, bf, o + 2), bg_load(src, bf, o + 3)) << 16);
+      *reinterpret_cast<uint32_t*>(dst + r * ldd + c) = w;
+    }
+  } else {
+    __shared__ float tile[64][65];
+    const int64_t tr = ceil_div(rows, 64), tc = ceil_div(cols, 64);
+    for (int64_t t = blockIdx.x; t < tr * tc; t += gridDim.x) {
+      const int64_t r0 = (t / tc) * 64, c0 = (t % tc) * 64;
+      for (int e = threadIdx.x; e < 64 * 64; e += 256) {
+        const int rr = e / 64, cc = e % 64;
+        tile[rr][cc] = (r0 + rr < rows && c0 + cc < cols) ? bg_load(src, bf, (r0 + rr) * ld + c0 + cc) : 0.f;
+      }
+      __syncthreads();
+      for (int e = threadIdx.x; e < 64 * 32; e += 256) {   // output row = source column, 2 elements per thread
+        const int cc = e / 32, rr = 2 * (e % 32);
+        if (c0 + cc < cols && r0 + rr + 1 < rows) {
+          const uint32_t w = q2(tile[rr][cc], tile[rr + 1][cc]);
+          *reinterpret_cast<uint16_t*>(dst + (c0 + cc) * ldd + r0 + rr) = (uint16_t)w;
+        } else if (c0 + cc < cols && r0 + rr < rows) {
+          dst[(c0 + cc) * ldd + r0 + rr] = (uint8_t)(q2(tile[rr][cc], 0.f) & 0xFF);
+        }
+      }
+      __syncthreads();
+    }
+  }
 }
 
 __global__ void cast2d_kernel(const float* __restrict__ src, int64_t lds, uint16_t* __restrict__ dst, int64_t ldd,
@@ -398,6 +695,13 @@ __global__ void cast2d_kernel(const float* __restrict__ src, int64_t lds, uint16
 }  // namespace kdfm
 
 extern "C" {
+
+int64_t kdfm_gemm_big_ws(int64_t M, int64_t N, int64_t K, int layout) {
+  using namespace kdfm;
+  if (layout != KDFM_BIG_TN || !kdfm_gemm_big_supported(M, N, K, layout)) return 0;
+  const int S = big_splits(M, N, K);
+  return S > 1 ? (int64_t)S * M * N + (int64_t)S * M : 0;
+}
 
 int kdfm_gemm_big_supported(int64_t M, int64_t N, int64_t K, int layout) {
   using namespace kdfm;
@@ -442,6 +746,8 @@ int kdfm_gemm_big(const kdfm_gemm_desc* d, const uint16_t* A, int64_t lda, const
   g.epi = accum ? 0 : d->epi;
   g.mask_len = d->mask_len; g.mask_T = d->mask_T; g.mask_div = d->mask_div;
   g.ones_col = -1;
+  g.ws = d->ws; g.ws_len = d->ws_len;
+  p.splits = 1;
   bool single;
   (void)epi_side_src(g, single);
   KDFM_REQUIRE(single, "at most one side operand (R, aux or C) per epilogue");
@@ -454,6 +760,70 @@ int kdfm_gemm_big(const kdfm_gemm_desc* d, const uint16_t* A, int64_t lda, const
     case KDFM_BIG_NN: return big_dispatch<false, true>(p, st);
     default: return big_dispatch<true, true>(p, st);
   }
+}
+
+int kdfm_fp8_quant(const void* src, int src_bf16, int64_t rows, int64_t cols, int64_t ld, uint8_t* dst, int64_t ldd,
+                   int transpose, unsigned* amax, float* dscale, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(src && dst && amax && rows > 0 && cols > 0 && ld >= cols, "bad arguments");
+  KDFM_REQUIRE(transpose ? (ldd >= rows && rows % 2 == 0 && (ldd % 2) == 0)
+                         : (ldd >= cols && cols % 4 == 0 && ld % 4 == 0 && ldd % 4 == 0),
+               "layout: cols % 4 (row-major) / rows % 2 (transposed)");
+  hipStream_t st = as_stream(stream);
+  if (hipMemsetAsync(amax, 0, sizeof(unsigned), st) != hipSuccess) return check_launch("kdfm_fp8_quant (memset)");
+  const int64_t n = rows * cols;
+  const unsigned blocks = (unsigned)(ceil_div(n, 256 * 8) < 2048 ? ceil_div(n, 256 * 8) : 2048);
+  hipLaunchKernelGGL(amax_kernel, dim3(blocks), dim3(256), 0, st, src, src_bf16, rows, cols, ld, amax);
+  int rc = check_launch("kdfm_fp8_quant (amax)");
+  if (rc) return rc;
+  if (transpose) {
+    const int64_t tiles = ceil_div(rows, 64) * ceil_div(cols, 64);
+    hipLaunchKernelGGL(quant_kernel<true>, dim3((unsigned)(tiles < 4096 ? tiles : 4096)), dim3(256), 0, st, src,
+                       src_bf16, rows, cols, ld, dst, ldd, amax, dscale);
+  } else {
+    const unsigned qb = (unsigned)(ceil_div(n / 4, 256) < 8192 ? ceil_div(n / 4, 256) : 8192);
+    hipLaunchKernelGGL(quant_kernel<false>, dim3(qb), dim3(256), 0, st, src, src_bf16, rows, cols, ld, dst, ldd, amax,
+                       dscale);
+  }
+  return check_launch("kdfm_fp8_quant");
+}
+
+int kdfm_gemm_big_fp8(const kdfm_gemm_desc* d, const uint8_t* A, int64_t lda, const uint8_t* B, int64_t ldb,
+                      const float* sa, const float* sb, uint16_t* C16, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(d && A && B, "null argument");
+  KDFM_REQUIRE(d->M >= 128 && d->N >= 128 && d->K >= 128 && d->K % 128 == 0, "fp8 route: M, N >= 128, K % 128 == 0");
+  KDFM_REQUIRE(d->batch1 == 1 && d->batch2 == 1 && d->splitk == 1 && d->epi != KDFM_EPI_ATOMIC,
+               "unbatched forward / data-gradient products only");
+  KDFM_REQUIRE(((((uintptr_t)A) | ((uintptr_t)B)) & 15) == 0 && lda % 16 == 0 && ldb % 16 == 0,
+               "operands 16-byte aligned, row strides multiples of 16 bytes");
+  KDFM_REQUIRE(!(d->epi & KDFM_EPI_MSE) && (d->C != nullptr || C16 != nullptr), "C or C16; no MSE");
+  KDFM_REQUIRE(!(d->epi & KDFM_EPI_BIAS) || d->bias, "EPI_BIAS without bias");
+  KDFM_REQUIRE(!(d->epi & KDFM_EPI_RESID) || d->R, "EPI_RESID without R");
+  KDFM_REQUIRE(!(d->epi & (KDFM_EPI_DRELU | KDFM_EPI_DSILU)) || d->aux, "derivative epilogue without aux");
+  KDFM_REQUIRE(!(d->epi & KDFM_EPI_STORE_PRE) || d->Cpre, "EPI_STORE_PRE without Cpre");
+  KDFM_REQUIRE(!(d->epi & KDFM_EPI_BETA) || (d->C && !C16), "EPI_BETA reads the f32 C");
+  BigP p{};
+  p.A = reinterpret_cast<const uint16_t*>(A);
+  p.B = reinterpret_cast<const uint16_t*>(B);
+  p.lda = lda; p.ldb = ldb; p.C16 = C16; p.sa = sa; p.sb = sb; p.splits = 1;
+  GemmP& g = p.g;
+  g.C = d->C; g.bias = d->bias; g.R = d->R; g.aux = d->aux; g.Cpre = d->Cpre;
+  g.M = d->M; g.N = d->N; g.K = d->K;
+  g.sCm = d->sCm; g.sCn = d->sCn;
+  g.alpha = d->alpha; g.beta = d->beta; g.rscale = d->rscale; g.dropout_p = d->dropout_p;
+  g.seed = d->seed; g.rng_stream = d->rng_stream; g.epi = d->epi;
+  g.mask_len = d->mask_len; g.mask_T = d->mask_T; g.mask_div = d->mask_div;
+  g.ones_col = -1;
+  bool single;
+  (void)epi_side_src(g, single);
+  KDFM_REQUIRE(single, "at most one side operand (R, aux or C) per epilogue");
+  set_route(ROUTE_BIG);
+  hipStream_t st = as_stream(stream);
+  const char* e = getenv("KDFM_BIG_TILE");
+  int c = e ? atoi(e) : big_pick(d->M, d->N);
+  if (c == 0) c = 1;   // the 256 x 256 fp8 tile's fragments do not fit beside its accumulators
+  return c == 1 ? big_epi_f8<256, 128, 4, 2>(p, st) : big_epi_f8<128, 128, 2, 2>(p, st);
 }
 
 int kdfm_cast_bf16_2d(const float* src, int64_t lds, uint16_t* dst, int64_t ldd, int64_t rows, int64_t cols,

@@ -22,6 +22,7 @@ _MATH = {"f32": _lib.KDFM_MATH_F32, "bf16": _lib.KDFM_MATH_BF16}
 class _State:
     math = "f32"
     deterministic = False
+    fp8 = False   # the large-tile route's forward / data-gradient products in fp8 e4m3 (Ver5Config.linear_fp8)
     ranges = os.environ.get("KDFM_ROCTX", "0") == "1"   # ROCTx ranges around engine phases
 
 
@@ -158,22 +159,35 @@ class mode:
     """Context manager: run a block in the given MFMA arithmetic / reduction mode and restore the
     previous process-global modes afterwards (the engine applies its config this way)."""
 
-    def __init__(self, math: str | None = None, deterministic: bool | None = None):
-        self.math, self.det = math, deterministic
+    def __init__(self, math: str | None = None, deterministic: bool | None = None, fp8: bool | None = None):
+        self.math, self.det, self.fp8 = math, deterministic, fp8
 
     def __enter__(self):
-        self._saved = (_State.math, _State.deterministic)
+        self._saved = (_State.math, _State.deterministic, _State.fp8)
         if self.math is not None:
             set_math(self.math)
         if self.det is not None and self.det != _State.deterministic:
             set_deterministic(self.det)
+        if self.fp8 is not None:
+            _State.fp8 = bool(self.fp8)
         return self
 
     def __exit__(self, *a):
-        m, d = self._saved
+        m, d, f8 = self._saved
         set_math(m)
         if d != _State.deterministic:
             set_deterministic(d)
+        _State.fp8 = f8
+
+
+def set_fp8(on: bool) -> None:
+    """fp8 e4m3 operands (per-tensor current scaling) for the large-tile route's forward and data-gradient products
+    (kdfm_gemm_big_fp8); weight gradients stay bf16.  Process-global like the math mode."""
+    _State.fp8 = bool(on)
+
+
+def get_fp8() -> bool:
+    return _State.fp8
 
 
 # host-issue fast paths: torch.cuda.current_stream() costs several µs per call in Python (device
@@ -263,13 +277,14 @@ _SCRATCH: dict = {}
 _RETIRED: list = []
 
 
-def scratch(dev, nfloats: int):
-    """f32 scratch for per-block reduction partials, one buffer per (device, stream).  Consumers
+def scratch(dev, nfloats: int, slot: int = 0):
+    """f32 scratch for per-block reduction partials, one buffer per (device, stream, slot).  Consumers
     use it strictly in stream order (kernel then fold), so one buffer serves every call site of a
-    stream (the weight-gradient side stream gets its own); it only grows."""
+    stream (the weight-gradient side stream gets its own); it only grows.  Slot 1: a second buffer for a
+    launch that needs two at once (the large-tile route's bf16 operand copies in slot 0, its split partials)."""
     import os
     idx = torch.device(dev).index if torch.device(dev).index is not None else torch.cuda.current_device()
-    key = (idx, _raw_stream(idx))
+    key = (idx, _raw_stream(idx)) if slot == 0 else (idx, _raw_stream(idx), slot)
     buf = _SCRATCH.get(key)
     if buf is None or buf.numel() < nfloats:
         if buf is not None and os.environ.get("KDFM_SCRATCH_RETIRE", "1") == "1":
@@ -370,7 +385,8 @@ def _p(t):
 def gemm(A, B, Cout, M, N, K, sAm, sAk, sBk, sBn, sCm, sCn, *, amode, bmode,
          batch=(1, 1), bA=(0, 0), bB=(0, 0), bC=(0, 0), alpha=1.0, epi=0, bias=None, R=None, rscale=1.0,
          aux=None, Cpre=None, beta=0.0, dropout_p=0.0, seed=None, rng_stream=0, splitk=1,
-         conv=None, math=None, rowmask=None, mse=None, tag=None, ones_out=None, Bh=None, nbytes=None, big=None):
+         conv=None, math=None, rowmask=None, mse=None, tag=None, ones_out=None, Bh=None, nbytes=None, big=None,
+         fp8=None):
     """big = (A16 address, lda, B16 address, ldb, layout, C16 address or 0): the descriptor's epilogue on the
     large-tile bf16 kernel (kdfm_gemm_big) instead of kdfm_gemm's routes (see _big_linear)."""
     mth = math or _State.math
@@ -398,11 +414,18 @@ def gemm(A, B, Cout, M, N, K, sAm, sAk, sBk, sBn, sCm, sCn, *, amode, bmode,
             mlen, int(mT), int(mdiv), lacc, float(lscale), _p(ones_out), ones_col,
             0, 0, bh or 0, sbh]   # Bh: (device address, row stride) of the bf16 twin
     _GEMM_FMT.pack_into(_GEMM_BUF, 0, *vals)
-    if big is not None:
+    if fp8 is not None:   # (A8, lda, B8, ldb, sa, sb, C16): kdfm_gemm_big_fp8
+        name, args = "kdfm_gemm_big_fp8", (_GEMM_DESC,) + tuple(fp8) + (_s(),)
+    elif big is not None:
         name, args = "kdfm_gemm_big", (_GEMM_DESC,) + tuple(big) + (_s(),)
+        if big[4] == _lib.BIG_TN:   # split-reduction partials (deterministic fold), when the shape asks for them
+            nws = _lib.lib().kdfm_gemm_big_ws(int(M), int(N), int(K), int(big[4]))
+            if nws > 0:
+                ws = scratch(Cout.device, nws, slot=1)
+                struct.pack_into("@Pq", _GEMM_BUF, _GEMM_WS_OFF, ws.data_ptr(), ws.numel())
     else:
         name, args = "kdfm_gemm", (_GEMM_DESC, _s())
-    if big is None and epi == _lib.EPI_ATOMIC and (math_id == _lib.KDFM_MATH_BF16 or (_State.deterministic and splitk > 1)):
+    if big is None and fp8 is None and epi == _lib.EPI_ATOMIC and (math_id == _lib.KDFM_MATH_BF16 or (_State.deterministic and splitk > 1)):
         nws = _lib.lib().kdfm_gemm_ws(_GEMM_DESC)
         if nws > 0:
             ws = scratch(Cout.device, nws)
@@ -472,6 +495,37 @@ def _bf16_operands(ts):
     return out
 
 
+def fp8_ok(M, N, K) -> bool:
+    """The fp8 instance takes this k-contiguous product (fp8 mode on, the large-tile route applies, K % 128 == 0)."""
+    return _State.fp8 and K % 128 == 0 and M >= 128 and N >= 128 and big_ok(M, N, K, _lib.BIG_NT)
+
+
+def _fp8_operands(specs):
+    """e4m3 copies of 2-D operands with per-tensor current scaling (kdfm_fp8_quant: amax, then quantise):
+    specs = [(tensor f32 / bf16, transpose)], the transposed copy being the data gradient's W^T rows.  Returns
+    [(address, row stride in bytes, dequantisation-factor address)]; the copies live in this stream's scratch."""
+    dev = specs[0][0].device
+    shapes = []
+    for t, tr in specs:
+        assert t.dim() == 2 and t.stride(1) == 1 and t.dtype in (torch.float32, torch.bfloat16)
+        r, c = (t.shape[1], t.shape[0]) if tr else (t.shape[0], t.shape[1])
+        ld = -(-c // 16) * 16
+        shapes.append((r, ld))
+    nbytes = sum(r * ld for r, ld in shapes)
+    buf = scratch(dev, nbytes // 4 + 16)
+    small = scratch(dev, 4 * len(specs) + 4, slot=2)   # per operand: amax (uint), dequantisation factor (f32)
+    out, off = [], 0
+    for i, ((t, tr), (r, ld)) in enumerate(zip(specs, shapes)):
+        dst = buf.data_ptr() + off
+        amax = small.data_ptr() + 16 * i
+        dsc = amax + 4
+        call("kdfm_fp8_quant", ptr(t), 1 if t.dtype == torch.bfloat16 else 0, t.shape[0], t.shape[1], t.stride(0), dst, ld,
+             1 if tr else 0, amax, dsc, _s())
+        out.append((dst, ld, dsc))
+        off += r * ld
+    return out
+
+
 def _big_out(out):
     """(f32 C tensor or None, bf16 C16 address or 0)."""
     if out.dtype == torch.bfloat16:
@@ -497,6 +551,16 @@ def linear(x, W, bias, out, *, epi=0, R=None, rscale=1.0, Cpre=None, dropout_p=0
     assert W.shape[1] == K and out.shape[0] == M and out.shape[1] == N, (x.shape, W.shape, out.shape)
     if bias is not None:
         epi |= _lib.EPI_BIAS
+    if (math or _State.math) == "bf16" and mse is None and fp8_ok(M, N, K):
+        (a8, lda, sa), (w8, ldw, sw) = _fp8_operands([(x, False), (W, False)])
+        C, c16 = _big_out(out)
+        side = sum(1 for t in (R, Cpre) if t is not None)
+        nb = 1.0 * (M * K + N * K) + (2.0 if c16 else 4.0) * M * N + 4.0 * side * M * N
+        gemm(x, W, C if C is not None else out, M, N, K, 0, 0, 0, 0, out.stride(0), out.stride(1), amode=_lib.LD_KC,
+             bmode=_lib.LD_KC, epi=epi, bias=bias, R=R, rscale=rscale, Cpre=Cpre, dropout_p=dropout_p, seed=seed,
+             rng_stream=rng_stream, alpha=alpha, rowmask=rowmask, tag=tag, nbytes=nb,
+             fp8=(a8, lda, w8, ldw, sa, sw, c16))
+        return
     if (math or _State.math) == "bf16" and mse is None and big_ok(M, N, K, _lib.BIG_NT):
         (a16, lda), (w16, ldw) = _bf16_operands((x, W))
         C, c16 = _big_out(out)
@@ -523,6 +587,16 @@ def linear_dx(dy, W, dx, *, epi=0, aux=None, dropout_p=0.0, seed=None, rng_strea
     assert W.shape[0] == N and dx.shape[0] == M and dx.shape[1] == K, (dy.shape, W.shape, dx.shape)
     if R is not None:
         epi |= _lib.EPI_RESID
+    if (math or _State.math) == "bf16" and fp8_ok(M, K, N):
+        # dx = dY (W^T)^T: the fp8 instance is k-contiguous only, so W is quantised transposed ([K][N] rows)
+        (a8, lda, sa), (w8, ldw, sw) = _fp8_operands([(dy, False), (W, True)])
+        C, c16 = _big_out(dx)
+        side = sum(1 for t in (R, aux) if t is not None)
+        nb = 1.0 * (M * N + N * K) + (2.0 if c16 else 4.0) * M * K + 4.0 * side * M * K
+        gemm(dy, W, C if C is not None else dx, M, K, N, 0, 0, 0, 0, dx.stride(0), dx.stride(1), amode=_lib.LD_KC,
+             bmode=_lib.LD_XC, epi=epi, aux=aux, dropout_p=dropout_p, seed=seed, rng_stream=rng_stream, R=R,
+             rscale=rscale, alpha=alpha, rowmask=rowmask, nbytes=nb, fp8=(a8, lda, w8, ldw, sa, sw, c16))
+        return
     if (math or _State.math) == "bf16" and big_ok(M, K, N, _lib.BIG_NN):
         (a16, lda), (w16, ldw) = _bf16_operands((dy, W))
         C, c16 = _big_out(dx)

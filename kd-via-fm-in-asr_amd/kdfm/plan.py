@@ -129,7 +129,7 @@ class StepPlan:
             orig_call(name, *args)
             if plan._paused:
                 return
-            if name in ("kdfm_gemm", "kdfm_gemm_big"):   # the descriptor buffer is shared by every launch: snapshot it
+            if name in ("kdfm_gemm", "kdfm_gemm_big", "kdfm_gemm_big_fp8"):   # the descriptor buffer is shared by every launch: snapshot it
                 buf = C.create_string_buffer(K._GEMM_BUF.raw, len(K._GEMM_BUF.raw))
                 plan.keep.append(buf)
                 args = (C.cast(buf, C.POINTER(_lib.GemmDesc)),) + tuple(args[1:])

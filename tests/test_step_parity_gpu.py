@@ -267,11 +267,71 @@ def test_bf16_step_big_route_matches_float64_oracle(sub, B, N, lens, monkeypatch
             n["big"] += 1
         return orig(name, *a)
     monkeypatch.setattr(K, "call", call)
-    _bf16_step_check(sub, B, N, lens, 12, [12, 7, 9, 5, 12, 11, 3, 8][:B])
+    _bf16_step_check(sub, B, N, lens, 12, [12, 7, 9, 5, 12, 11, 3, 8][:B], round_acts="bf16")
     assert n["big"] >= 2 * 6 * 3, n   # per layer: >= 6 wide products forward (teacher + student) + dX + dW
 
 
-def _bf16_step_check(sub, B, N, lens, U, tl):
+def test_fp8_xl_step_matches_float64_oracle(monkeypatch):
+    """BASELINE.json configs[4] at its stated precision: the FastConformer-XL 2-layer step with linear_fp8 -- every
+    wide Linear's forward and data gradient on e4m3 operands (per-tensor current scaling, block-scaled MFMA), the
+    attention core and weight gradients bf16 -- against the float64 oracle.  Tolerances derived from the oracle's own
+    fp8 sensitivity: the same float64 step with those products' operands rounded to per-tensor
+    scaled e4m3 (x and W; the weights everywhere else to bf16); losses rel max(3e-3, 2.5 x sens), layer outputs and
+    gradients rel. Frobenius max(floor, 2.5 x sens) with the bf16 test's floors."""
+    from kdfm import kernels as K
+    monkeypatch.setattr(K, "_BIG_MIN_WORK", 0.0)
+    n = {"fp8": 0}
+    orig = K.call
+
+    def call(name, *a):
+        if name == "kdfm_gemm_big_fp8":
+            n["fp8"] += 1
+        return orig(name, *a)
+    monkeypatch.setattr(K, "call", call)
+    _bf16_step_check(dict(XL, linear_fp8=True), 8, 96000, [96000] * 7 + [71234], 12, [12, 7, 9, 5, 12, 11, 3, 8],
+                     round_acts="fp8")
+    assert n["fp8"] >= 2 * 6 * 2, n
+
+
+class _RoundedF:
+    """torch.nn.functional for the oracle with the MFMA operand rounding of the wide products: F.linear and
+    pointwise (kernel 1) F.conv1d whose weight is >= 512 x 512 and whose input has >= 512 rows get their input and
+    weight rounded -- to bf16, or to e4m3 with per-tensor current scaling (448 / amax) -- straight-through for
+    autograd.  Everything else is torch's."""
+
+    def __init__(self, fmt):
+        self.fmt = fmt
+        self._F = torch.nn.functional
+
+    def __getattr__(self, n):
+        return getattr(self._F, n)
+
+    def _q(self, t):
+        if self.fmt == "bf16":
+            q = t.bfloat16().to(t.dtype)
+        else:
+            a = t.detach().abs().max().float()
+            sc = (torch.tensor(448.0, dtype=torch.float32) / a) if a > 0 else torch.tensor(1.0)
+            q = ((t.detach().float() * sc).clamp(-448, 448).to(torch.float8_e4m3fn).float() * (1.0 / sc)).to(t.dtype)
+        return t + (q - t).detach()
+
+    def _wide(self, rows, w):
+        return rows >= 512 and w.shape[0] >= 512 and w.shape[1] >= 512
+
+    def linear(self, x, w, b=None):
+        if self._wide(x.numel() // x.shape[-1], w):
+            x, w = self._q(x), self._q(w)
+        return self._F.linear(x, w, b)
+
+    def conv1d(self, x, w, b=None, *a, **kw):
+        if w.dim() == 3 and w.shape[-1] == 1 and x.dim() == 3 and self._wide(x.shape[0] * x.shape[2], w[:, :, 0]):
+            x, w = self._q(x), self._q(w)
+        return self._F.conv1d(x, w, b, *a, **kw)
+
+
+def _bf16_step_check(sub, B, N, lens, U, tl, round_acts=None):
+    """round_acts: also round the wide products' operands in the oracle's sensitivity run ("bf16" / "fp8", _RoundedF)
+    -- the GPU rounds activations at every MFMA, not only weights."""
     n_layers = 2
     cfg, eng, wav, wl, tg, tgl, g = _build(n_layers, B, N, lens, U, tl, sub=dict(sub, math="bf16"))
     from kdfm.config import sub_dims
@@ -292,7 +352,7 @@ def _bf16_step_check(sub, B, N, lens, U, tl):
     out = O.ver5_step(p, wav.double(), wl, tg, tgl, ocfg, eps_o.double())
     ref = torch.stack([out["loss"], out["ctc"], out["kl"], out["recon"], out["fm"]]).detach().double()
     rel = ((losses.double() - ref).abs() / ref.abs().clamp_min(1e-6)).max().item()
-    assert rel <= 3e-3, (rel, losses.tolist(), ref.tolist())
+    assert round_acts or rel <= 3e-3, (rel, losses.tolist(), ref.tolist())
 
     def frob(a, b):
         a, b = a.detach().double().cpu(), b.detach().double().cpu()
@@ -303,12 +363,24 @@ def _bf16_step_check(sub, B, N, lens, U, tl):
     # softmax boundary and some gradients move by several % from that alone (cf. test_dw_striding_gpu.py)
     pb = {k: (v.detach().bfloat16().double() if (k in names and v.dim() >= 2) else v.detach()).requires_grad_(k in names)
           if v.is_floating_point() else v for k, v in p.items()}
-    out_b = O.ver5_step(pb, wav.double(), wl, tg, tgl, ocfg, eps_o.double())
+    saved_F = O.F
+    if round_acts:
+        O.F = _RoundedF(round_acts)
+    try:
+        out_b = O.ver5_step(pb, wav.double(), wl, tg, tgl, ocfg, eps_o.double())
+    finally:
+        O.F = saved_F
+    if round_acts:
+        ref_b = torch.stack([out_b["loss"], out_b["ctc"], out_b["kl"], out_b["recon"], out_b["fm"]]).detach().double()
+        sens_l = ((ref_b - ref).abs() / ref.abs().clamp_min(1e-6)).max().item()
+        print(f"step losses: rel err {rel:.3e}, sensitivity {sens_l:.3e}")
+        assert rel <= max(3e-3, 2.5 * sens_l), (rel, sens_l)
     # layer outputs: max(1.5e-2, 2.5 x the same sensitivity) -- at d_model 1024 (XL) the bf16-rounded weights alone
     # move the second layer's output ~0.7 %
     for i in range(n_layers):
         e = frob(sfeats[i].view(B, T, -1), out["s_feats"][i])
         sens = frob(out_b["s_feats"][i], out["s_feats"][i])
+        print(f"layer {i} output: rel err {e:.3e}, sensitivity {sens:.3e}")
         assert e <= max(1.5e-2, 2.5 * sens), (i, e, sens)
     gb = torch.autograd.grad(out_b["loss"], [pb[k] for k in names], allow_unused=True)
     bad = []
@@ -317,6 +389,8 @@ def _bf16_step_check(sub, B, N, lens, U, tl):
             continue
         e = frob(grads[k], gr)
         sens = frob(grb, gr) if grb is not None else 0.0
+        if round_acts:
+            print(f"grad {k}: rel err {e:.3e}, sensitivity {sens:.3e}")
         if e > max(5e-2, 2.5 * sens):
             bad.append((k, e, sens))
     assert not bad, bad

@@ -1,0 +1,41 @@
+// Operand lane-map probe of the block-scaled fp8 MFMA v_mfma_scale_f32_16x16x128_f8f6f4 (e4m3 x e4m3, unit
+// e8m0 scales): every lane loads its 32 raw operand bytes of A and B from host-prepared arrays, one MFMA, and
+// writes its 4 accumulator values (C/D map: col = lane & 15, row = 4 (lane >> 4) + r, dtype-independent on gfx950).
+// tools/fp8_probe.py prepares the bytes under a hypothesised lane map and checks C against an exact reference.
+// Build: hipcc -O2 -shared -fPIC --offload-arch=gfx950 tools/fp8_probe.hip -o tools/fp8_probe.so
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef int v8i __attribute__((ext_vector_type(8)));
+typedef float v4f __attribute__((ext_vector_type(4)));
+
+__global__ void probe_kernel(const int* a, const int* b, float* c, int sa, int sb) {
+  const int l = threadIdx.x;
+  v8i av, bv;
+  for (int i = 0; i < 8; ++i) {
+    av[i] = a[l * 8 + i];
+    bv[i] = b[l * 8 + i];
+  }
+  v4f acc = {0.f, 0.f, 0.f, 0.f};
+  acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(av, bv, acc, 0, 0, 0, sa, 0, sb);
+  for (int r = 0; r < 4; ++r) c[l * 4 + r] = acc[r];
+}
+
+extern "C" int fp8_probe(const int* a, const int* b, float* c, int sa, int sb) {
+  hipLaunchKernelGGL(probe_kernel, dim3(1), dim3(64), 0, 0, a, b, c, sa, sb);
+  return (int)hipDeviceSynchronize();
+}
+
+// f32 -> fp8 conversion check: v_cvt_pk_fp8_f32 (the builtin biggemm.hip's quantizer uses) on n inputs, byte out
+__global__ void cvt_kernel(const float* x, unsigned char* y, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (2 * i + 1 >= n) return;
+  const int w = __builtin_amdgcn_cvt_pk_fp8_f32(x[2 * i], x[2 * i + 1], 0, false);
+  y[2 * i] = (unsigned char)(w & 0xFF);
+  y[2 * i + 1] = (unsigned char)((w >> 8) & 0xFF);
+}
+
+extern "C" int fp8_cvt(const float* x, unsigned char* y, int n) {
+  hipLaunchKernelGGL(cvt_kernel, dim3((n / 2 + 255) / 256), dim3(256), 0, 0, x, y, n);
+  return (int)hipDeviceSynchronize();
+}

@@ -1,0 +1,70 @@
+"""Which operand lane map does v_mfma_scale_f32_16x16x128_f8f6f4 use on gfx950?  Random small integers (exact in
+e4m3) for A (16 x 128) and B (128 x 16), placed into each lane's 32 operand bytes under several hypothesised maps,
+one MFMA each (tools/fp8_probe.hip, unit e8m0 scales 0x7F = 2^0); the map whose C equals the exact product is the
+one biggemm.hip's fp8 instance must stage.  Also checks a non-unit A scale (0x80 = 2^1) doubles C."""
+import ctypes as C
+import os
+import sys
+
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def maps():
+    """name -> fn(lane, byte j) -> k (the row / column is lane & 15 for both operands)"""
+    return {
+        "k = 32 (l>>4) + j": lambda l, j: 32 * (l >> 4) + j,
+        "k = 16 (l>>4) + j, +64 for bytes 16..31": lambda l, j: 16 * (l >> 4) + (j & 15) + 64 * (j >> 4),
+        "k = 8 (l>>4) + (j&7) + 32 (j>>3)": lambda l, j: 8 * (l >> 4) + (j & 7) + 32 * (j >> 3),
+    }
+
+
+def main():
+    lib = C.CDLL(os.path.join(HERE, "fp8_probe.so"))
+    dev = torch.device("cuda")
+    g = torch.Generator().manual_seed(1)
+    A = torch.randint(-3, 4, (16, 128), generator=g).float()
+    B = torch.randint(-3, 4, (128, 16), generator=g).float()
+    ref = (A.double() @ B.double())
+    ok_any = None
+    for name, f in maps().items():
+        ab = torch.zeros(64, 32, dtype=torch.uint8)
+        bb = torch.zeros(64, 32, dtype=torch.uint8)
+        for l in range(64):
+            for j in range(32):
+                k = f(l, j)
+                ab[l, j] = A[l & 15, k].to(torch.float8_e4m3fn).view(torch.uint8)
+                bb[l, j] = B[k, l & 15].to(torch.float8_e4m3fn).view(torch.uint8)
+        da = ab.view(torch.int32).contiguous().to(dev)
+        db = bb.view(torch.int32).contiguous().to(dev)
+        c = torch.zeros(64, 4, device=dev)
+        for sa, mult in ((0x7F7F7F7F, 1.0), (0x80808080, 2.0)):
+            rc = lib.fp8_probe(C.c_void_p(da.data_ptr()), C.c_void_p(db.data_ptr()), C.c_void_p(c.data_ptr()),
+                               C.c_int(sa), C.c_int(0x7F7F7F7F))
+            assert rc == 0, rc
+            got = torch.zeros(16, 16, dtype=torch.float64)
+            cc = c.cpu().double()
+            for l in range(64):
+                for r in range(4):
+                    got[4 * (l >> 4) + r, l & 15] = cc[l, r]
+            err = (got - mult * ref).abs().max().item()
+            print(f"map [{name}] scale_a x{mult:g}: max |C - ref| = {err:g}", flush=True)
+            if err == 0.0 and mult == 1.0:
+                ok_any = name
+    print("MATCH:", ok_any)
+    # v_cvt_pk_fp8_f32 against torch's OCP e4m3fn rounding (round to nearest even) on values inside +-448
+    x = torch.cat([torch.linspace(-448, 448, 20001), torch.randn(20000) * 3, torch.randn(20000) * 1e-2])
+    x = x[: (x.numel() // 2) * 2].contiguous()
+    dx = x.to(dev)
+    dy = torch.zeros(x.numel(), dtype=torch.uint8, device=dev)
+    rc = lib.fp8_cvt(C.c_void_p(dx.data_ptr()), C.c_void_p(dy.data_ptr()), C.c_int(x.numel()))
+    assert rc == 0, rc
+    ref = x.to(torch.float8_e4m3fn).view(torch.uint8)
+    bad = (dy.cpu() != ref).sum().item()
+    print(f"cvt_pk_fp8_f32 vs torch e4m3fn: {bad} of {x.numel()} bytes differ", flush=True)
+    sys.exit(0 if ok_any and bad == 0 else 1)
+
+
+if __name__ == "__main__":
+    main()

@@ -4,7 +4,8 @@ copies as the library yardstick.  Prints TFLOP/s per product and direction:
   big     : kernels.linear / linear_dx / linear_dw on the large-tile route (csrc/biggemm.hip) with bf16 operands in
             HBM (the kernel alone: what the XL step's bf16 intermediates feed it);
   big+cast: the same from f32 operands (each f32 operand cast to bf16 scratch first, kdfm_cast_bf16_2d);
-  generic : the previous route (kdfm_gemm's 64x64 tile / row-parallel weight gradient), f32 operands.
+  generic : the previous route (kdfm_gemm's 64x64 tile / row-parallel weight gradient), f32 operands;
+  fp8+quant: the fp8 e4m3 instance (linear_fp8) including the per-tensor quantisation of both operands.
 HIP events around N back-to-back launches (median of 3 rounds)."""
 import os
 import statistics
@@ -58,6 +59,12 @@ def main():
         res["dx big+cast"] = bench(lambda: K.linear_dx(dy, W, dx))
         res["dW big"] = bench(lambda: K.linear_dw(dy16, x16, dW, db=db))
         res["dW big+cast"] = bench(lambda: K.linear_dw(dy, x, dW, db=db))
+        K._State.fp8 = True
+        try:
+            res["fwd fp8+quant"] = bench(lambda: K.linear(x16, W, b, y))
+            res["dx fp8+quant"] = bench(lambda: K.linear_dx(dy16, W, dx))
+        finally:
+            K._State.fp8 = False
         K._BIG = False
         try:
             res["fwd generic"] = bench(lambda: K.linear(x, W, b, y))

@@ -374,10 +374,12 @@ def _on_call(name, args):
     from kdfm import kernels as K
     s = _cur()
     site = _site()
-    if name in ("kdfm_gemm", "kdfm_gemm_big"):
+    if name in ("kdfm_gemm", "kdfm_gemm_big", "kdfm_gemm_big_fp8"):
         v = K._GEMM_FMT.unpack_from(K._GEMM_BUF, 0)
-        if name == "kdfm_gemm_big":   # its bf16 operands / output are arguments; the descriptor carries the rest
-            for a, fld, w in ((args[1], "A16", 0), (args[3], "B16", 0), (args[6], "C16", 1)):
+        if name != "kdfm_gemm":   # its bf16 / fp8 operands and output are arguments; the descriptor carries the rest
+            ops = ((args[1], "A16", 0), (args[3], "B16", 0), (args[6], "C16", 1)) if name == "kdfm_gemm_big" else \
+                ((args[1], "A8", 0), (args[3], "B8", 0), (args[5], "sa", 0), (args[6], "sb", 0), (args[7], "C16", 1))
+            for a, fld, w in ops:
                 if a:
                     T.access(a, T.recent.get(a, a + 4), s, bool(w), site, f"gemm_big.{fld}")
         for idx, fld, w in ((0, "A", 0), (1, "B", 0), (2, "C", 1), (3, "bias", 0), (4, "R", 0), (5, "aux", 0),
