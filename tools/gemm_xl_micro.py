@@ -63,6 +63,19 @@ def main():
         try:
             res["fwd fp8+quant"] = bench(lambda: K.linear(x16, W, b, y))
             res["dx fp8+quant"] = bench(lambda: K.linear_dx(dy16, W, dx))
+            # the fp8 kernel alone on operands quantised once (kernels._fp8_operands into a private copy)
+            (a8, lda, sa), (w8, ldw, sw) = K._fp8_operands([(x16, False), (W, False)])
+            q = K.scratch(dev, 1)
+            keep = torch.empty(q.numel(), device=dev)
+            keep.copy_(q)
+            off = keep.data_ptr() - q.data_ptr()
+            sm = K.scratch(dev, 12, slot=2)
+            sk = sm.clone()
+            soff = sk.data_ptr() - sm.data_ptr()
+            import kdfm._lib as L
+            res["fwd fp8 kernel"] = bench(lambda: K.gemm(x16, W, y, M, N, Kd, 0, 0, 0, 0, y.stride(0), 1, amode=L.LD_KC,
+                                                         bmode=L.LD_KC, epi=L.EPI_BIAS, bias=b,
+                                                         fp8=(a8 + off, lda, w8 + off, ldw, sa + soff, sw + soff, 0)))
         finally:
             K._State.fp8 = False
         K._BIG = False
