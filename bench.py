@@ -515,9 +515,9 @@ def main():
             _progress("FastConformer-XL fp8 sensitivity")
             xl8 = sensitivity(dev, args.samples, linear_fp8=True, **XL_SHAPES)
             xl8["note"] = ("configs[4] at its stated precision: the same XL step with the wide Linear products' forward "
-                           "and data gradients on fp8 e4m3 operands (per-tensor current scaling, block-scaled MFMA "
-                           "v_mfma_scale_f32_16x16x128_f8f6f4); attention core and weight gradients bf16; not the "
-                           "headline value")
+                           "and data gradients on MX fp8 operands (e4m3 with an e8m0 scale per 32 contraction "
+                           "elements, applied by the block-scaled MFMA v_mfma_scale_f32_16x16x128_f8f6f4); attention "
+                           "core and weight gradients bf16; not the headline value")
         line = {
             "metric": "utterances/sec (FM-distill train step, Conformer-CTC-small) at 1/2/4/8 MI355X",
             "value": round(utt, 3),

@@ -173,18 +173,21 @@ int kdfm_gemm_big_supported(int64_t M, int64_t N, int64_t K, int layout);
 int64_t kdfm_gemm_big_ws(int64_t M, int64_t N, int64_t K, int layout);
 int kdfm_gemm_big(const kdfm_gemm_desc* d, const uint16_t* A, int64_t lda, const uint16_t* B, int64_t ldb, int layout,
                   uint16_t* C16, void* stream);
-/* fp8 e4m3 (OCP) products for FastConformer-XL at fp8 (BASELINE.json configs[4]: "fp8 MFMA attention/FFN"):
- * kdfm_fp8_quant: per-tensor current scaling of a rows x cols f32 (src_bf16 = 0) or bf16 (1) matrix with row stride
- * ld -- amax = max |x| (into *amax, one caller-owned uint: zeroed, then an order-free atomic max: deterministic),
- * s = 448 / amax, dst = e4m3(sat(x s)) row-major dst[r * ldd + c] or, transpose = 1, dst[c * ldd + r]; *dscale = 1 / s.
- * kdfm_gemm_big_fp8: the KDFM_BIG_NT product (A(m, k) = A[m * lda + k], B(k, n) = B[n * ldb + k], byte strides)
- * of e4m3 operands on the block-scaled MFMA v_mfma_scale_f32_16x16x128_f8f6f4 (unit block scales, 2x the bf16
- * MFMA rate) with the descriptor's epilogue applied to alpha * (*sa) * (*sb) * sum_k; K % 128 == 0.  The forward
- * x W^T and the data gradient dY (W^T)^T (B = W^T quantised transposed) take it; weight gradients stay bf16. */
-int kdfm_fp8_quant(const void* src, int src_bf16, int64_t rows, int64_t cols, int64_t ld, uint8_t* dst, int64_t ldd,
-                   int transpose, unsigned* amax, float* dscale, void* stream);
+/* fp8 e4m3 (OCP) products for FastConformer-XL at fp8 (BASELINE.json configs[4]: "fp8 MFMA attention/FFN"), MX
+ * block scaling: every 32 consecutive elements along the contraction share one e8m0 scale byte (2^(byte - 127)).
+ * kdfm_fp8_quant_mx: quantise a rows x cols f32 (src_bf16 = 0) or bf16 (1) matrix with row stride ld; the blocks run
+ * along cols (transpose = 0: dst[r * ldd + c]) or along rows with the output transposed (transpose = 1: dst[c * ldd +
+ * r], the data gradient's W^T); block exponent e = ceil(log2(amax / 448)), q = e4m3(x 2^-e) (no saturation), scale
+ * byte e + 127, stored stage-major: scales[((k / 128) * R + row) * 4 + (k / 32) % 4] for output row `row` of R and
+ * contraction index k.  The contraction length % 128 == 0.
+ * kdfm_gemm_big_fp8: the KDFM_BIG_NT product (A(m, k) = A[m * lda + k], B(k, n) = B[n * ldb + k], byte strides) of
+ * MX-quantised operands on the block-scaled MFMA v_mfma_scale_f32_16x16x128_f8f6f4 (2x the bf16 MFMA rate; the
+ * scales are applied by the MFMA) with the descriptor's epilogue; K % 128 == 0, M and N multiples of 4.  The
+ * forward x W^T and the data gradient dY (W^T)^T (B = W quantised transposed) take it; weight gradients stay bf16. */
+int kdfm_fp8_quant_mx(const void* src, int src_bf16, int64_t rows, int64_t cols, int64_t ld, uint8_t* dst, int64_t ldd,
+                      uint8_t* scales, int transpose, void* stream);
 int kdfm_gemm_big_fp8(const kdfm_gemm_desc* d, const uint8_t* A, int64_t lda, const uint8_t* B, int64_t ldb,
-                      const float* sa, const float* sb, uint16_t* C16, void* stream);
+                      const uint8_t* sa, const uint8_t* sb, uint16_t* C16, void* stream);
 /* dst[r * ldd + c] = bf16(src[r * lds + c]) for a rows x cols f32 matrix (cols, lds, ldd multiples of 4). */
 int kdfm_cast_bf16_2d(const float* src, int64_t lds, uint16_t* dst, int64_t ldd, int64_t rows, int64_t cols,
                       void* stream);

@@ -53,9 +53,10 @@ struct BigP {
   int64_t kchunk;
   float* ws;
   float* wsb;
-  // fp8 instance (e4m3 operands): per-tensor dequantisation factors (device scalars; C = alpha sa sb sum_k a b)
-  const float* sa;
-  const float* sb;
+  // fp8 instance (e4m3 operands, MX block scaling): one e8m0 scale byte per 32 consecutive k of a row, stored
+  // stage-major xs[((k / 128) * rows + row) * 4 + (k / 32) % 4] (kdfm_fp8_quant_mx), applied by the MFMA itself
+  const uint8_t* xsa;
+  const uint8_t* xsb;
   GemmP g;            // M, N, K, C, strides and the epilogue fields
 };
 
@@ -124,7 +125,8 @@ __global__ __launch_bounds__(WM* WN * 64) void big_gemm_kernel(BigP p) {
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int FM = WTM / 16, FN = WTN / 16;
   constexpr int AIMG = BM * BG_BK, BIMG = BN * BG_BK;   // elements per stage
-  constexpr int STAGE = AIMG + BIMG;
+  // fp8: each stage also holds the A and B scale bytes of its 128 k (4 per row: <= 1 KB each)
+  constexpr int STAGE = AIMG + BIMG + (F8 ? 1024 : 0);
   constexpr int PA = BM / 8, PB = BN / 8, PW = (PA + PB) / NW;   // 1 KB DMA pieces: A, B, per wave
   static_assert((PA + PB) % NW == 0, "pieces per wave");
   extern __shared__ __attribute__((aligned(16))) uint16_t bg_lds[];
@@ -179,6 +181,17 @@ __global__ __launch_bounds__(WM* WN * 64) void big_gemm_kernel(BigP p) {
       uint16_t* dst = buf + (isa ? 0 : AIMG) + 512 * fl;
       __builtin_amdgcn_global_load_lds((bg_gl_void*)src, (bg_lds_void*)dst, 16, 0, 0);
     }
+    if constexpr (F8) {   // waves 0 / 1: this stage's A / B scale bytes, 4 rows (16 B) per lane
+      if (wave < 2) {
+        const bool isa = wave == 0;
+        const int64_t R = isa ? M : N, r0 = isa ? m0 : n0;
+        int64_t r = r0 + 4 * lane;
+        r = r + 4 <= R ? r : R - 4;
+        const uint8_t* src = (isa ? p.xsa : p.xsb) + ((k0 / 128) * R + r) * 4;
+        uint16_t* dst = buf + AIMG + BIMG + (isa ? 0 : 512);
+        __builtin_amdgcn_global_load_lds((bg_gl_void*)src, (bg_lds_void*)dst, 16, 0, 0);
+      }
+    }
   };
 
   constexpr bool BIAS = EMODE == BG_ACCB;
@@ -212,24 +225,35 @@ __global__ __launch_bounds__(WM* WN * 64) void big_gemm_kernel(BigP p) {
       }
     }
     if (t + 1 < nk) issue(t + 1, s ^ 1);
-    if constexpr (F8) {   // one block-scaled fp8 MFMA per accumulator tile covers the stage's 128 k (unit scales)
+    if constexpr (F8) {   // one block-scaled fp8 MFMA per accumulator tile covers the stage's 128 k
       bg_v8i af[FM], bfr[FN];
+      int sca[FM], scb[FN];
+      // lane l's 32 operand bytes are k = 32 (l >> 4) .. + 31 of its row (frag_kc8), one MX block: its scale byte
+      const uint8_t* sbuf = reinterpret_cast<const uint8_t*>(abuf + AIMG + BIMG);
 #pragma unroll
-      for (int i = 0; i < FM; ++i) af[i] = frag_kc8(abuf, wr * WTM + 16 * i, lane);
+      for (int i = 0; i < FM; ++i) {
+        af[i] = frag_kc8(abuf, wr * WTM + 16 * i, lane);
+        const uint32_t sa_ = lds_addr(sbuf + (wr * WTM + 16 * i + (lane & 15)) * 4 + (lane >> 4));
+        asm volatile("ds_read_u8 %0, %1" : "=v"(sca[i]) : "v"(sa_));
+      }
 #pragma unroll
-      for (int j = 0; j < FN; ++j) bfr[j] = frag_kc8(bbuf, wc * WTN + 16 * j, lane);
+      for (int j = 0; j < FN; ++j) {
+        bfr[j] = frag_kc8(bbuf, wc * WTN + 16 * j, lane);
+        const uint32_t sb_ = lds_addr(sbuf + 1024 + (wc * WTN + 16 * j + (lane & 15)) * 4 + (lane >> 4));
+        asm volatile("ds_read_u8 %0, %1" : "=v"(scb[j]) : "v"(sb_));
+      }
       lgkm_wait<0>();
 #pragma unroll
-      for (int i = 0; i < FM; ++i) asm volatile("" : "+v"(af[i]));
+      for (int i = 0; i < FM; ++i) asm volatile("" : "+v"(af[i]), "+v"(sca[i]));
 #pragma unroll
-      for (int j = 0; j < FN; ++j) asm volatile("" : "+v"(bfr[j]));
+      for (int j = 0; j < FN; ++j) asm volatile("" : "+v"(bfr[j]), "+v"(scb[j]));
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[i], bfr[j], acc[i][j], 0, 0, 0, 0x7F7F7F7F, 0,
-                                                                       0x7F7F7F7F);
+          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[i], bfr[j], acc[i][j], 0, 0, 0, sca[i], 0,
+                                                                       scb[j]);
       continue;
     }
     // fragment reads of a k half, then its MFMAs; with registers to spare (<= 16 accumulator tiles per wave) the
@@ -290,7 +314,7 @@ __global__ __launch_bounds__(WM* WN * 64) void big_gemm_kernel(BigP p) {
   // ---- epilogue ----
   const GemmP& g = p.g;
   float alpha = g.alpha;
-  if constexpr (F8) alpha *= (p.sa ? *p.sa : 1.f) * (p.sb ? *p.sb : 1.f);
+
   if constexpr (EMODE == BG_ACC || EMODE == BG_ACCB) {
     if (p.splits > 1) {   // raw partials of this split (plain stores; big_fold_kernel adds them in split order)
       float* w = p.ws + (int64_t)sp * M * N;
@@ -603,77 +627,87 @@ int big_dispatch(BigP p, hipStream_t st) {
   return big_epi<128, 128, 2, 2, AT, BT>(p, st);
 }
 
-// ---- fp8 e4m3 per-tensor quantisation (current scaling): amax, then q = sat(x * 448 / amax) ----
 __device__ __forceinline__ float bg_load(const void* src, int bf, int64_t i) {
   return bf ? __uint_as_float(((uint32_t) reinterpret_cast<const uint16_t*>(src)[i]) << 16)
             : reinterpret_cast<const float*>(src)[i];
 }
 
-__global__ __launch_bounds__(256) void amax_kernel(const void* src, int bf, int64_t rows, int64_t cols, int64_t ld,
-                                                   unsigned* out) {
-  float m = 0.f;
-  const int64_t n = rows * cols;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-    const int64_t r = i / cols, c = i - r * cols;
-    m = fmaxf(m, fabsf(bg_load(src, bf, r * ld + c)));
-  }
-  m = wave_max(m);
-  __shared__ float red[4];
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-    atomicMax(out, __float_as_uint(m));   // non-negative floats order as their bit patterns: exact, order-free
+// ---- MX fp8 quantisation (OCP e4m3, e8m0 block scales over 32 consecutive k) ----
+// block exponent e = ceil(log2(amax / 448)) (clamped to the e8m0 range): every element of the block is then
+// exactly x 2^-e <= 448 in magnitude, no saturation; q = e4m3(x 2^-e) (round to nearest even), scale byte e + 127
+__device__ __forceinline__ int mx_exp(float amax) {
+  if (!(amax > 0.f)) return -127;
+  int ex;
+  const float m = frexpf(amax * (1.f / 448.f), &ex);   // amax / 448 = m 2^ex, m in [0.5, 1)
+  int e = m > 0.5f ? ex : ex - 1;
+  if (ldexpf(amax, -e) > 448.f) ++e;   // the 1/448 product's rounding
+  return e < -127 ? -127 : (e > 127 ? 127 : e);
+}
+__device__ __forceinline__ uint32_t mx_q4(float a, float b, float c, float d, int e) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(ldexpf(a, -e), ldexpf(b, -e), 0, false) & 0xFFFFu;
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(ldexpf(c, -e), ldexpf(d, -e), 0, false) & 0xFFFFu;
+  return lo | (hi << 16);
+}
+
+// row-major: block (row, kb) = src[row][32 kb .. +31]; 8 lanes per block, 4 elements each
+__global__ __launch_bounds__(256) void mx_quant_kernel(const void* src, int bf, int64_t rows, int64_t cols, int64_t ld,
+                                                       uint8_t* dst, int64_t ldd, uint8_t* xs) {
+  const int64_t nkb = cols / 32, nblk = rows * nkb;
+  const int sub = threadIdx.x & 7;
+  for (int64_t blk = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 3; blk < nblk + 0; blk += (int64_t)gridDim.x * 32) {
+    const int64_t r = blk / nkb, kb = blk - r * nkb;
+    const int64_t o = r * ld + 32 * kb + 4 * sub;
+    float v[4];
+    if (bf) {
+      const uint2 w = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(src) + o);
+      v[0] = __uint_as_float(w.x << 16); v[1] = __uint_as_float(w.x & 0xFFFF0000u);
+      v[2] = __uint_as_float(w.y << 16); v[3] = __uint_as_float(w.y & 0xFFFF0000u);
+    } else {
+      const float4 w = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(src) + o);
+      v[0] = w.x; v[1] = w.y; v[2] = w.z; v[3] = w.w;
+    }
+    float m = fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3])));
+    m = fmaxf(m, __shfl_xor(m, 1, 64));
+    m = fmaxf(m, __shfl_xor(m, 2, 64));
+    m = fmaxf(m, __shfl_xor(m, 4, 64));
+    const int e = mx_exp(m);
+    *reinterpret_cast<uint32_t*>(dst + r * ldd + 32 * kb + 4 * sub) = mx_q4(v[0], v[1], v[2], v[3], e);
+    if (sub == 0) xs[((kb >> 2) * rows + r) * 4 + (kb & 3)] = (uint8_t)(e + 127);
   }
 }
 
-__device__ __forceinline__ float bg_qscale(const unsigned* amax) {
-  const float a = __uint_as_float(*amax);
-  return (a > 0.f && a < 3.0e38f) ? 448.f / a : 1.f;
-}
-
-// dst[r * ldd + c] (or, transposed, dst[c * ldd + r]) = e4m3(sat(x[r][c] * s)), s = 448 / amax; dscale = 1 / s.
-// The transposed form (weights for the data gradient: W^T rows) goes through a 64 x 64 LDS tile.
-template <bool TR>
-__global__ __launch_bounds__(256) void quant_kernel(const void* src, int bf, int64_t rows, int64_t cols, int64_t ld,
-                                                    uint8_t* dst, int64_t ldd, const unsigned* amax, float* dscale) {
-  const float sc = bg_qscale(amax);
-  if (blockIdx.x == 0 && threadIdx.x == 0 && dscale) *dscale = 1.f / sc;
-  auto q2 = [&](float a, float b) -> uint32_t {
-    a = fminf(fmaxf(a * sc, -448.f), 448.f);
-    b = fminf(fmaxf(b * sc, -448.f), 448.f);
-    return (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false) & 0xFFFFu;
-  };
-  if constexpr (!TR) {
-    const int64_t c4 = cols / 4, n = rows * c4;
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-      const int64_t r = i / c4, c = (i - r * c4) * 4;
-      const int64_t o = r * ld + c;
-      const uint32_t w = q2(bg_load(src, bf, o), bg_load(src, bf, o + 1)) |
-                         (q2(bg_load(src, bf, o + 2), bg_load(src, bf, o + 3)) << 16);
-      *reinterpret_cast<uint32_t*>(dst + r * ldd + c) = w;
+// transposed (the data gradient's W^T rows): output row c = source column c, blocks over 32 source rows; a 32 x 64
+// source tile through LDS, 4 lanes per output block (8 elements each)
+__global__ __launch_bounds__(256) void mx_quant_t_kernel(const void* src, int bf, int64_t rows, int64_t cols,
+                                                         int64_t ld, uint8_t* dst, int64_t ldd, uint8_t* xs) {
+  __shared__ float tile[32][65];
+  const int64_t tr = rows / 32, tc = ceil_div(cols, 64);
+  for (int64_t t = blockIdx.x; t < tr * tc; t += gridDim.x) {
+    const int64_t r0 = (t / tc) * 32, c0 = (t % tc) * 64;
+    for (int e = threadIdx.x; e < 32 * 64; e += 256) {
+      const int rr = e / 64, cc = e % 64;
+      tile[rr][cc] = c0 + cc < cols ? bg_load(src, bf, (r0 + rr) * ld + c0 + cc) : 0.f;
     }
-  } else {
-    __shared__ float tile[64][65];
-    const int64_t tr = ceil_div(rows, 64), tc = ceil_div(cols, 64);
-    for (int64_t t = blockIdx.x; t < tr * tc; t += gridDim.x) {
-      const int64_t r0 = (t / tc) * 64, c0 = (t % tc) * 64;
-      for (int e = threadIdx.x; e < 64 * 64; e += 256) {
-        const int rr = e / 64, cc = e % 64;
-        tile[rr][cc] = (r0 + rr < rows && c0 + cc < cols) ? bg_load(src, bf, (r0 + rr) * ld + c0 + cc) : 0.f;
-      }
-      __syncthreads();
-      for (int e = threadIdx.x; e < 64 * 32; e += 256) {   // output row = source column, 2 elements per thread
-        const int cc = e / 32, rr = 2 * (e % 32);
-        if (c0 + cc < cols && r0 + rr + 1 < rows) {
-          const uint32_t w = q2(tile[rr][cc], tile[rr + 1][cc]);
-          *reinterpret_cast<uint16_t*>(dst + (c0 + cc) * ldd + r0 + rr) = (uint16_t)w;
-        } else if (c0 + cc < cols && r0 + rr < rows) {
-          dst[(c0 + cc) * ldd + r0 + rr] = (uint8_t)(q2(tile[rr][cc], 0.f) & 0xFF);
-        }
-      }
-      __syncthreads();
+    __syncthreads();
+    const int cc = threadIdx.x >> 2, q = threadIdx.x & 3;   // output row c0 + cc, elements 8 q .. + 7 of the block
+    float v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = tile[8 * q + i][cc];
+    float m = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) m = fmaxf(m, fabsf(v[i]));
+    m = fmaxf(m, __shfl_xor(m, 1, 64));
+    m = fmaxf(m, __shfl_xor(m, 2, 64));
+    const int e = mx_exp(m);
+    if (c0 + cc < cols) {
+      uint2 w;
+      w.x = mx_q4(v[0], v[1], v[2], v[3], e);
+      w.y = mx_q4(v[4], v[5], v[6], v[7], e);
+      *reinterpret_cast<uint2*>(dst + (c0 + cc) * ldd + r0 + 8 * q) = w;
+      const int64_t kb = r0 / 32;
+      if (q == 0) xs[((kb >> 2) * cols + c0 + cc) * 4 + (kb & 3)] = (uint8_t)(e + 127);
     }
+    __syncthreads();
   }
 }
 
@@ -762,37 +796,34 @@ int kdfm_gemm_big(const kdfm_gemm_desc* d, const uint16_t* A, int64_t lda, const
   }
 }
 
-int kdfm_fp8_quant(const void* src, int src_bf16, int64_t rows, int64_t cols, int64_t ld, uint8_t* dst, int64_t ldd,
-                   int transpose, unsigned* amax, float* dscale, void* stream) {
+int kdfm_fp8_quant_mx(const void* src, int src_bf16, int64_t rows, int64_t cols, int64_t ld, uint8_t* dst, int64_t ldd,
+                      uint8_t* scales, int transpose, void* stream) {
   using namespace kdfm;
-  KDFM_REQUIRE(src && dst && amax && rows > 0 && cols > 0 && ld >= cols, "bad arguments");
-  KDFM_REQUIRE(transpose ? (ldd >= rows && rows % 2 == 0 && (ldd % 2) == 0)
-                         : (ldd >= cols && cols % 4 == 0 && ld % 4 == 0 && ldd % 4 == 0),
-               "layout: cols % 4 (row-major) / rows % 2 (transposed)");
+  KDFM_REQUIRE(src && dst && scales && rows > 0 && cols > 0 && ld >= cols, "bad arguments");
+  const int64_t kdim = transpose ? rows : cols;   // the contraction length the 32-blocks run along
+  KDFM_REQUIRE(kdim % 128 == 0 && ld % 4 == 0 && ldd % 16 == 0, "contraction length % 128, ld % 4, ldd % 16");
+  KDFM_REQUIRE(transpose ? ldd >= rows : (ldd >= cols && (((uintptr_t)src) & (src_bf16 ? 7 : 15)) == 0),
+               "layout / alignment");
   hipStream_t st = as_stream(stream);
-  if (hipMemsetAsync(amax, 0, sizeof(unsigned), st) != hipSuccess) return check_launch("kdfm_fp8_quant (memset)");
-  const int64_t n = rows * cols;
-  const unsigned blocks = (unsigned)(ceil_div(n, 256 * 8) < 2048 ? ceil_div(n, 256 * 8) : 2048);
-  hipLaunchKernelGGL(amax_kernel, dim3(blocks), dim3(256), 0, st, src, src_bf16, rows, cols, ld, amax);
-  int rc = check_launch("kdfm_fp8_quant (amax)");
-  if (rc) return rc;
   if (transpose) {
-    const int64_t tiles = ceil_div(rows, 64) * ceil_div(cols, 64);
-    hipLaunchKernelGGL(quant_kernel<true>, dim3((unsigned)(tiles < 4096 ? tiles : 4096)), dim3(256), 0, st, src,
-                       src_bf16, rows, cols, ld, dst, ldd, amax, dscale);
+    const int64_t tiles = (rows / 32) * ceil_div(cols, 64);
+    hipLaunchKernelGGL(mx_quant_t_kernel, dim3((unsigned)(tiles < 8192 ? tiles : 8192)), dim3(256), 0, st, src,
+                       src_bf16, rows, cols, ld, dst, ldd, scales);
   } else {
-    const unsigned qb = (unsigned)(ceil_div(n / 4, 256) < 8192 ? ceil_div(n / 4, 256) : 8192);
-    hipLaunchKernelGGL(quant_kernel<false>, dim3(qb), dim3(256), 0, st, src, src_bf16, rows, cols, ld, dst, ldd, amax,
-                       dscale);
+    const int64_t blocks = ceil_div(rows * (cols / 32), 32);
+    hipLaunchKernelGGL(mx_quant_kernel, dim3((unsigned)(blocks < 16384 ? blocks : 16384)), dim3(256), 0, st, src,
+                       src_bf16, rows, cols, ld, dst, ldd, scales);
   }
-  return check_launch("kdfm_fp8_quant");
+  return check_launch("kdfm_fp8_quant_mx");
 }
 
 int kdfm_gemm_big_fp8(const kdfm_gemm_desc* d, const uint8_t* A, int64_t lda, const uint8_t* B, int64_t ldb,
-                      const float* sa, const float* sb, uint16_t* C16, void* stream) {
+                      const uint8_t* sa, const uint8_t* sb, uint16_t* C16, void* stream) {
   using namespace kdfm;
   KDFM_REQUIRE(d && A && B, "null argument");
-  KDFM_REQUIRE(d->M >= 128 && d->N >= 128 && d->K >= 128 && d->K % 128 == 0, "fp8 route: M, N >= 128, K % 128 == 0");
+  KDFM_REQUIRE(d->M >= 128 && d->N >= 128 && d->K >= 128 && d->K % 128 == 0 && d->M % 4 == 0 && d->N % 4 == 0,
+               "fp8 route: M, N >= 128 (multiples of 4), K % 128 == 0");
+  KDFM_REQUIRE(sa && sb, "the MX scale tensors are required");
   KDFM_REQUIRE(d->batch1 == 1 && d->batch2 == 1 && d->splitk == 1 && d->epi != KDFM_EPI_ATOMIC,
                "unbatched forward / data-gradient products only");
   KDFM_REQUIRE(((((uintptr_t)A) | ((uintptr_t)B)) & 15) == 0 && lda % 16 == 0 && ldb % 16 == 0,
@@ -806,7 +837,7 @@ int kdfm_gemm_big_fp8(const kdfm_gemm_desc* d, const uint8_t* A, int64_t lda, co
   BigP p{};
   p.A = reinterpret_cast<const uint16_t*>(A);
   p.B = reinterpret_cast<const uint16_t*>(B);
-  p.lda = lda; p.ldb = ldb; p.C16 = C16; p.sa = sa; p.sb = sb; p.splits = 1;
+  p.lda = lda; p.ldb = ldb; p.C16 = C16; p.xsa = sa; p.xsb = sb; p.splits = 1;
   GemmP& g = p.g;
   g.C = d->C; g.bias = d->bias; g.R = d->R; g.aux = d->aux; g.Cpre = d->Cpre;
   g.M = d->M; g.N = d->N; g.K = d->K;

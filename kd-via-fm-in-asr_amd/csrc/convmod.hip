@@ -550,6 +550,8 @@ int kdfm_dwconv_fwd(const float* g, const float* w, const float* bias, float* y,
   double* st_fused = deterministic() ? nullptr : stats;
   if (K == 31)
     hipLaunchKernelGGL(dwconv_fwd_kernel<31>, grid, dim3(256), 0, as_stream(stream), g, w, bias, y, st_fused, T, d, (int)K);
+  else if (K == 9)   // FastConformer(-XL), fast-conformer_ctc_bpe.yaml conv_kernel_size 9
+    hipLaunchKernelGGL(dwconv_fwd_kernel<9>, grid, dim3(256), 0, as_stream(stream), g, w, bias, y, st_fused, T, d, (int)K);
   else if (K == 15)
     hipLaunchKernelGGL(dwconv_fwd_kernel<15>, grid, dim3(256), 0, as_stream(stream), g, w, bias, y, st_fused, T, d, (int)K);
   else
@@ -581,6 +583,8 @@ int kdfm_dwconv_bwd(const float* dy, const float* g, const float* w, float* dg, 
   const BnApply none{};
   if (K == 31)
     hipLaunchKernelGGL(dwconv_bwd_kernel<31>, grid, dim3(256), 0, st, dy, g, w, dg, ws, T, d, (int)K, none);
+  else if (K == 9)
+    hipLaunchKernelGGL(dwconv_bwd_kernel<9>, grid, dim3(256), 0, st, dy, g, w, dg, ws, T, d, (int)K, none);
   else if (K == 15)
     hipLaunchKernelGGL(dwconv_bwd_kernel<15>, grid, dim3(256), 0, st, dy, g, w, dg, ws, T, d, (int)K, none);
   else
@@ -597,7 +601,7 @@ int kdfm_dwconv_bwd_bn(const float* dz, const float* y, const float* mean, const
   using namespace kdfm;
   KDFM_REQUIRE(dz && y && mean && rstd && gamma && beta && red && dgamma && dbeta && g && w && dg && ws,
                "null pointer");
-  KDFM_REQUIRE(K == 31 || K == 15, "BN-applied depthwise backward: kernel size 15 or 31");
+  KDFM_REQUIRE(K == 31 || K == 15 || K == 9, "BN-applied depthwise backward: kernel size 9, 15 or 31");
   KDFM_REQUIRE(d % 4 == 0 && ((((uintptr_t)g) | ((uintptr_t)dz) | ((uintptr_t)y)) & 15) == 0,
                "channels must be a multiple of 4, inputs 16-B aligned");
   KDFM_REQUIRE(red_next != red, "red_next must be another buffer");
@@ -608,6 +612,8 @@ int kdfm_dwconv_bwd_bn(const float* dz, const float* y, const float* mean, const
   const BnApply bn{y, mean, rstd, gamma, beta, red, (double)(B * T), batch_stats, dgamma, dbeta, red_next};
   if (K == 31)
     hipLaunchKernelGGL((dwconv_bwd_kernel<31, true>), grid, dim3(256), 0, st, dz, g, w, dg, ws, T, d, (int)K, bn);
+  else if (K == 9)
+    hipLaunchKernelGGL((dwconv_bwd_kernel<9, true>), grid, dim3(256), 0, st, dz, g, w, dg, ws, T, d, (int)K, bn);
   else
     hipLaunchKernelGGL((dwconv_bwd_kernel<15, true>), grid, dim3(256), 0, st, dz, g, w, dg, ws, T, d, (int)K, bn);
   return check_launch("kdfm_dwconv_bwd_bn");

@@ -54,6 +54,9 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
 // to part[block][2d]; kdfm_ln_fold (one launch for several LayerNorms) sums them in block order.
 constexpr int LN_RPW = 4;
 
+// Wide rows (V > 4 column groups per lane, d > 256: Conformer-large / FastConformer-XL) keep one row's values at a
+// time (3 V registers, the next row's loads issued before this row's reductions): holding all LN_RPW rows' dy, x and
+// residual (12 V floats) spilled at d = 1024 (116 us per 6 432-row LayerNorm, profiles/r06/r6e).
 template <int V>
 // dy2 (nullable): a second gradient summed into dy on load (the encoder backward's layer-input gradient
 // plus the hooked output's gradient, without an add launch in between)
@@ -63,6 +66,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ d
                                                      float* __restrict__ part, int64_t rows, int d,
                                                      const float* __restrict__ dy2) {
   __shared__ float red[2][4][64 * V];
+  constexpr int RB = V > 4 ? 1 : LN_RPW;   // rows whose values are held at once
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   float gl[V], pg[V], pb[V];
 #pragma unroll
@@ -73,44 +77,47 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ d
     pb[i] = 0.f;
   }
   const int64_t base = ((int64_t)blockIdx.x * 4 + w) * LN_RPW;
-  float dyv[LN_RPW][V], xv[LN_RPW][V], rv[LN_RPW][V], mu[LN_RPW], rs[LN_RPW];
 #pragma unroll
-  for (int j = 0; j < LN_RPW; ++j) {
-    const int64_t row = base + j;
-    const bool ok = row < rows;
-    mu[j] = ok ? mean[row] : 0.f;
-    rs[j] = ok ? rstd[row] : 0.f;
+  for (int j0 = 0; j0 < LN_RPW; j0 += RB) {
+    float dyv[RB][V], xv[RB][V], rv[RB][V], mu[RB], rs[RB];
 #pragma unroll
-    for (int i = 0; i < V; ++i) {
-      const int c = lane + 64 * i;
-      const bool in = ok && c < d;
-      dyv[j][i] = in ? dy[row * d + c] + (dy2 ? dy2[row * d + c] : 0.f) : 0.f;
-      xv[j][i] = in ? x[row * d + c] : 0.f;
-      rv[j][i] = (in && dres) ? dres[row * d + c] : 0.f;
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < LN_RPW; ++j) {
-    const int64_t row = base + j;
-    float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-    for (int i = 0; i < V; ++i) {
-      const int c = lane + 64 * i;
-      const float xh = (c < d) ? (xv[j][i] - mu[j]) * rs[j] : 0.f;
-      xv[j][i] = xh;
-      const float gy = dyv[j][i] * gl[i];
-      pg[i] += dyv[j][i] * xh;
-      pb[i] += dyv[j][i];
-      s1 += gy;
-      s2 += gy * xh;
-    }
-    s1 = wave_sum(s1) / d;
-    s2 = wave_sum(s2) / d;
-    if (row < rows) {
+    for (int j = 0; j < RB; ++j) {
+      const int64_t row = base + j0 + j;
+      const bool ok = row < rows;
+      mu[j] = ok ? mean[row] : 0.f;
+      rs[j] = ok ? rstd[row] : 0.f;
 #pragma unroll
       for (int i = 0; i < V; ++i) {
         const int c = lane + 64 * i;
-        if (c < d) dx[row * d + c] = rs[j] * (dyv[j][i] * gl[i] - s1 - xv[j][i] * s2) + rv[j][i];
+        const bool in = ok && c < d;
+        dyv[j][i] = in ? dy[row * d + c] + (dy2 ? dy2[row * d + c] : 0.f) : 0.f;
+        xv[j][i] = in ? x[row * d + c] : 0.f;
+        rv[j][i] = (in && dres) ? dres[row * d + c] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < RB; ++j) {
+      const int64_t row = base + j0 + j;
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int i = 0; i < V; ++i) {
+        const int c = lane + 64 * i;
+        const float xh = (c < d) ? (xv[j][i] - mu[j]) * rs[j] : 0.f;
+        xv[j][i] = xh;
+        const float gy = dyv[j][i] * gl[i];
+        pg[i] += dyv[j][i] * xh;
+        pb[i] += dyv[j][i];
+        s1 += gy;
+        s2 += gy * xh;
+      }
+      s1 = wave_sum(s1) / d;
+      s2 = wave_sum(s2) / d;
+      if (row < rows) {
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+          const int c = lane + 64 * i;
+          if (c < d) dx[row * d + c] = rs[j] * (dyv[j][i] * gl[i] - s1 - xv[j][i] * s2) + rv[j][i];
+        }
       }
     }
   }

@@ -153,7 +153,7 @@ SIGNATURES: dict[str, tuple] = {
     "kdfm_cast_bf16_2d": (_i32, [P, _i64, P, _i64, _i64, _i64, P]),
     "kdfm_gemm_big_supported": (_i32, [_i64, _i64, _i64, _i32]),
     "kdfm_gemm_big_ws": (_i64, [_i64, _i64, _i64, _i32]),
-    "kdfm_fp8_quant": (_i32, [P, _i32, _i64, _i64, _i64, P, _i64, _i32, P, P, P]),
+    "kdfm_fp8_quant_mx": (_i32, [P, _i32, _i64, _i64, _i64, P, _i64, P, _i32, P]),
     "kdfm_gemm_big_fp8": (_i32, [C.POINTER(GemmDesc), P, _i64, P, _i64, P, P, P, P]),
     "kdfm_gemm_big": (_i32, [C.POINTER(GemmDesc), P, _i64, P, _i64, _i32, P, P]),
     "kdfm_cast_bf16_t": (_i32, [P, P, P, _i64, _i64, P]),

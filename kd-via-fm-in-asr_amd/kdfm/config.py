@@ -103,7 +103,7 @@ class Ver5Config:
     # execution
     math: str = "bf16"               # MFMA arithmetic: "bf16" (throughput) or "f32" (parity)
     deterministic: bool = False      # ordered reductions (kdfm_set_deterministic): bitwise-reproducible runs
-    # fp8 e4m3 operands (per-tensor current scaling, block-scaled MFMA) for the wide Linear products' forward and data
+    # fp8 e4m3 operands (MX: an e8m0 scale per 32 contraction elements, block-scaled MFMA) for the wide Linear products' forward and data
     # gradients on the large-tile route (d_model >= 512: BASELINE.json configs[4] "fp8 MFMA attention/FFN" -- the
     # attention projections and the FFN; the attention core and the weight gradients stay bf16)
     linear_fp8: bool = False

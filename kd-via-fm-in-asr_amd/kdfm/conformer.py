@@ -791,7 +791,7 @@ def layer_backward(cfg, S: EncoderShapes, P, G, L, li, ctx, dout, pos_emb, lengt
     dg = _empty(rows, d, dev=dev)
     # the depthwise weight / bias gradient's fold of per-block partials runs on the weight-gradient stream
     dws = torch.empty(K.dwconv_bwd_ws(B, T, d, cfg.conv_kernel), device=dev)
-    if _BN_ON_LOAD and bn_red is not None and cfg.conv_kernel in (15, 31):
+    if _BN_ON_LOAD and bn_red is not None and cfg.conv_kernel in (9, 15, 31):
         # BN + SiLU backward: the sums, then their elementwise half applied on load by the depthwise backward
         # (dy never stored); the sums' buffer comes from the ring, the launch zeroes the next one
         Pbw, Pbb = P[L + "conv.batch_norm.weight"], P[L + "conv.batch_norm.bias"]

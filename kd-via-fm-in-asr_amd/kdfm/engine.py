@@ -211,7 +211,7 @@ class Ver5Engine:
     def forward(self, wav, wav_len, targets, tgt_len, *, train=True, eps=None, save=True):
         """One forward pass; returns the context backward() consumes.  eps: optional injected
         NoiseAdapter noise (n_layers*B*T', latent) for parity runs."""
-        with self._on_stream(), self._mode(), K.region("forward"):
+        with self._on_stream(), self._mode(), K.weight_epoch(), K.region("forward"):
             return self._forward(wav, wav_len, targets, tgt_len, train=train, eps=eps, save=save)
 
     def _forward(self, wav, wav_len, targets, tgt_len, *, train, eps, save):
@@ -391,7 +391,7 @@ class Ver5Engine:
         with BatchNorm running statistics and no dropout, decoder + log_softmax.  The reference's eval
         forward also runs the teacher encoder (:629-631) and discards it (only training_step reads
         the hooks), so it is skipped.  Returns log_probs (B, T', V+1) and enc_len (B,)."""
-        with self._on_stream(), self._mode():
+        with self._on_stream(), self._mode(), K.weight_epoch():
             return self._infer(wav, wav_len)
 
     def _infer(self, wav, wav_len):
@@ -487,7 +487,7 @@ class Ver5Engine:
         # deterministic mode keeps the weight-gradient products on the issuing stream unless
         # overlap_wgrad says otherwise
         serial = self.cfg.deterministic if self.overlap_wgrad is None else not self.overlap_wgrad
-        with self._on_stream(), self._mode(), WGRAD.serialized(serial), K.region("backward"):
+        with self._on_stream(), self._mode(), WGRAD.serialized(serial), K.weight_epoch(), K.region("backward"):
             try:
                 self._backward(ctx, grad_ready)
             except BaseException:

@@ -23,6 +23,9 @@ class _State:
     math = "f32"
     deterministic = False
     fp8 = False   # the large-tile route's forward / data-gradient products in fp8 e4m3 (Ver5Config.linear_fp8)
+    # weight epoch: while set (the engine advances it once per step, before the forward), each weight's bf16 copy of
+    # the large-tile route and its MX fp8 copies are made at its first use in the epoch and reused after; None
+    # (the module API, tests): every product converts its weight itself
     ranges = os.environ.get("KDFM_ROCTX", "0") == "1"   # ROCTx ranges around engine phases
 
 
@@ -181,13 +184,74 @@ class mode:
 
 
 def set_fp8(on: bool) -> None:
-    """fp8 e4m3 operands (per-tensor current scaling) for the large-tile route's forward and data-gradient products
+    """fp8 e4m3 operands (MX block scaling) for the large-tile route's forward and data-gradient products
     (kdfm_gemm_big_fp8); weight gradients stay bf16.  Process-global like the math mode."""
     _State.fp8 = bool(on)
 
 
 def get_fp8() -> bool:
     return _State.fp8
+
+
+_State.fp8_epoch = None
+_FP8_W = {}   # (address, rows, cols, row stride, transposed) -> [epoch, storage, (address, ld, scales)]
+_BF16_W = {}  # (address, rows, cols, row stride) -> [epoch, bf16 storage]
+
+
+_EPOCHS = [0]
+
+
+class weight_epoch:
+    """Context manager (the engine wraps each forward / backward / inference call in one): inside it, the weights
+    are constant, so the large-tile route converts each weight (bf16, MX fp8) once at its first use and reuses the
+    copy; outside (the module API, tests, after an optimizer step) every product converts its weight itself."""
+
+    def __enter__(self):
+        self._saved = _State.fp8_epoch
+        _EPOCHS[0] += 1
+        _State.fp8_epoch = _EPOCHS[0]
+        return self
+
+    def __exit__(self, *a):
+        _State.fp8_epoch = self._saved
+
+
+def _bf16_weight(W):
+    """The large-tile route's bf16 copy of a weight view for this epoch (cast on first use), or None outside an
+    epoch; persistent storage (a recorded plan replays the cast into it)."""
+    ep = _State.fp8_epoch
+    if ep is None or W.dtype != torch.float32:
+        return None
+    key = (W.data_ptr(), W.shape[0], W.shape[1], W.stride(0))
+    ent = _BF16_W.get(key)
+    ld = -(-W.shape[1] // 8) * 8
+    if ent is None:
+        ent = _BF16_W[key] = [None, torch.empty(W.shape[0], ld, dtype=torch.bfloat16, device=W.device)]
+    if ent[0] != ep:
+        call("kdfm_cast_bf16_2d", ptr(W), W.stride(0), ent[1].data_ptr(), ld, W.shape[0], W.shape[1], _s())
+        ent[0] = ep
+    return ent[1].data_ptr(), ld
+
+
+def _fp8_weight(W, tr):
+    """The MX copy of a weight view for this epoch (quantised on first use; kdfm_fp8_quant_mx), or None outside an
+    epoch.  The copies are persistent (a recorded step plan replays the quantisation launch into the same storage)."""
+    ep = _State.fp8_epoch
+    if ep is None:
+        return None
+    key = (W.data_ptr(), W.shape[0], W.shape[1], W.stride(0), bool(tr))
+    ent = _FP8_W.get(key)
+    r, kc = (W.shape[1], W.shape[0]) if tr else (W.shape[0], W.shape[1])
+    ld = -(-kc // 16) * 16
+    if ent is None:
+        buf = torch.empty(r * ld + -(-(r * kc // 32) // 16) * 16, dtype=torch.uint8, device=W.device)
+        ent = _FP8_W[key] = [None, buf, (buf.data_ptr(), ld, buf.data_ptr() + r * ld)]
+    if ent[0] != ep:
+        a, ld_, sc = ent[2]
+        call("kdfm_fp8_quant_mx", ptr(_f32(W)), 0, W.shape[0], W.shape[1], W.stride(0), a, ld_, sc, 1 if tr else 0,
+             _s())
+        ent[0] = ep
+    return ent[2]
 
 
 # host-issue fast paths: torch.cuda.current_stream() costs several µs per call in Python (device
@@ -414,7 +478,7 @@ def gemm(A, B, Cout, M, N, K, sAm, sAk, sBk, sBn, sCm, sCn, *, amode, bmode,
             mlen, int(mT), int(mdiv), lacc, float(lscale), _p(ones_out), ones_col,
             0, 0, bh or 0, sbh]   # Bh: (device address, row stride) of the bf16 twin
     _GEMM_FMT.pack_into(_GEMM_BUF, 0, *vals)
-    if fp8 is not None:   # (A8, lda, B8, ldb, sa, sb, C16): kdfm_gemm_big_fp8
+    if fp8 is not None:   # (A8, lda, B8, ldb, A scales, B scales, C16): kdfm_gemm_big_fp8
         name, args = "kdfm_gemm_big_fp8", (_GEMM_DESC,) + tuple(fp8) + (_s(),)
     elif big is not None:
         name, args = "kdfm_gemm_big", (_GEMM_DESC,) + tuple(big) + (_s(),)
@@ -469,8 +533,14 @@ def big_ok(M, N, K, layout) -> bool:
     return bool(_lib.lib().kdfm_gemm_big_supported(int(M), int(N), int(K), int(layout)))
 
 
-def _bf16_operands(ts):
-    """(address, row stride) of each 2-D operand as bf16: bf16 tensors in place, f32 ones cast into scratch."""
+def _bf16_operands(ts, weight=None):
+    """(address, row stride) of each 2-D operand as bf16: bf16 tensors in place, f32 ones cast into scratch; index
+    `weight` names a weight view, whose per-epoch copy (_bf16_weight) is used when there is one."""
+    wcopy = _bf16_weight(ts[weight]) if weight is not None else None
+    if wcopy is not None:
+        rest = _bf16_operands([t for i, t in enumerate(ts) if i != weight])
+        rest.insert(weight, wcopy)
+        return rest
     need = []
     for t in ts:
         if t.dtype == torch.bfloat16:
@@ -496,33 +566,33 @@ def _bf16_operands(ts):
 
 
 def fp8_ok(M, N, K) -> bool:
-    """The fp8 instance takes this k-contiguous product (fp8 mode on, the large-tile route applies, K % 128 == 0)."""
-    return _State.fp8 and K % 128 == 0 and M >= 128 and N >= 128 and big_ok(M, N, K, _lib.BIG_NT)
+    """The fp8 instance takes this k-contiguous product (fp8 mode on, the large-tile route applies, K % 128 == 0,
+    M and N multiples of 4)."""
+    return (_State.fp8 and K % 128 == 0 and M % 4 == 0 and N % 4 == 0 and M >= 128 and N >= 128
+            and big_ok(M, N, K, _lib.BIG_NT))
 
 
 def _fp8_operands(specs):
-    """e4m3 copies of 2-D operands with per-tensor current scaling (kdfm_fp8_quant: amax, then quantise):
+    """MX e4m3 copies of 2-D operands (kdfm_fp8_quant_mx: one e8m0 scale per 32 consecutive contraction elements):
     specs = [(tensor f32 / bf16, transpose)], the transposed copy being the data gradient's W^T rows.  Returns
-    [(address, row stride in bytes, dequantisation-factor address)]; the copies live in this stream's scratch."""
+    [(address, row stride in bytes, scale-tensor address)]; the copies live in this stream's scratch."""
     dev = specs[0][0].device
     shapes = []
     for t, tr in specs:
         assert t.dim() == 2 and t.stride(1) == 1 and t.dtype in (torch.float32, torch.bfloat16)
-        r, c = (t.shape[1], t.shape[0]) if tr else (t.shape[0], t.shape[1])
-        ld = -(-c // 16) * 16
-        shapes.append((r, ld))
-    nbytes = sum(r * ld for r, ld in shapes)
+        r, kc = (t.shape[1], t.shape[0]) if tr else (t.shape[0], t.shape[1])
+        shapes.append((r, -(-kc // 16) * 16, kc))
+    nbytes = sum(r * ld + -(-(r * kc // 32) // 16) * 16 for r, ld, kc in shapes)
     buf = scratch(dev, nbytes // 4 + 16)
-    small = scratch(dev, 4 * len(specs) + 4, slot=2)   # per operand: amax (uint), dequantisation factor (f32)
     out, off = [], 0
-    for i, ((t, tr), (r, ld)) in enumerate(zip(specs, shapes)):
+    for (t, tr), (r, ld, kc) in zip(specs, shapes):
         dst = buf.data_ptr() + off
-        amax = small.data_ptr() + 16 * i
-        dsc = amax + 4
-        call("kdfm_fp8_quant", ptr(t), 1 if t.dtype == torch.bfloat16 else 0, t.shape[0], t.shape[1], t.stride(0), dst, ld,
-             1 if tr else 0, amax, dsc, _s())
-        out.append((dst, ld, dsc))
         off += r * ld
+        sc = buf.data_ptr() + off
+        off += -(-(r * kc // 32) // 16) * 16
+        call("kdfm_fp8_quant_mx", ptr(t), 1 if t.dtype == torch.bfloat16 else 0, t.shape[0], t.shape[1], t.stride(0),
+             dst, ld, sc, 1 if tr else 0, _s())
+        out.append((dst, ld, sc))
     return out
 
 
@@ -552,7 +622,11 @@ def linear(x, W, bias, out, *, epi=0, R=None, rscale=1.0, Cpre=None, dropout_p=0
     if bias is not None:
         epi |= _lib.EPI_BIAS
     if (math or _State.math) == "bf16" and mse is None and fp8_ok(M, N, K):
-        (a8, lda, sa), (w8, ldw, sw) = _fp8_operands([(x, False), (W, False)])
+        wq = _fp8_weight(W, False)
+        if wq is None:
+            (a8, lda, sa), (w8, ldw, sw) = _fp8_operands([(x, False), (W, False)])
+        else:
+            ((a8, lda, sa),), (w8, ldw, sw) = _fp8_operands([(x, False)]), wq
         C, c16 = _big_out(out)
         side = sum(1 for t in (R, Cpre) if t is not None)
         nb = 1.0 * (M * K + N * K) + (2.0 if c16 else 4.0) * M * N + 4.0 * side * M * N
@@ -562,7 +636,7 @@ def linear(x, W, bias, out, *, epi=0, R=None, rscale=1.0, Cpre=None, dropout_p=0
              fp8=(a8, lda, w8, ldw, sa, sw, c16))
         return
     if (math or _State.math) == "bf16" and mse is None and big_ok(M, N, K, _lib.BIG_NT):
-        (a16, lda), (w16, ldw) = _bf16_operands((x, W))
+        (a16, lda), (w16, ldw) = _bf16_operands((x, W), weight=1)
         C, c16 = _big_out(out)
         side = sum(1 for t in (R, Cpre) if t is not None)
         nb = 2.0 * (M * K + N * K) + (2.0 if c16 else 4.0) * M * N + 4.0 * side * M * N
@@ -589,7 +663,11 @@ def linear_dx(dy, W, dx, *, epi=0, aux=None, dropout_p=0.0, seed=None, rng_strea
         epi |= _lib.EPI_RESID
     if (math or _State.math) == "bf16" and fp8_ok(M, K, N):
         # dx = dY (W^T)^T: the fp8 instance is k-contiguous only, so W is quantised transposed ([K][N] rows)
-        (a8, lda, sa), (w8, ldw, sw) = _fp8_operands([(dy, False), (W, True)])
+        wq = _fp8_weight(W, True)
+        if wq is None:
+            (a8, lda, sa), (w8, ldw, sw) = _fp8_operands([(dy, False), (W, True)])
+        else:
+            ((a8, lda, sa),), (w8, ldw, sw) = _fp8_operands([(dy, False)]), wq
         C, c16 = _big_out(dx)
         side = sum(1 for t in (R, aux) if t is not None)
         nb = 1.0 * (M * N + N * K) + (2.0 if c16 else 4.0) * M * K + 4.0 * side * M * K
@@ -598,7 +676,7 @@ def linear_dx(dy, W, dx, *, epi=0, aux=None, dropout_p=0.0, seed=None, rng_strea
              rscale=rscale, alpha=alpha, rowmask=rowmask, nbytes=nb, fp8=(a8, lda, w8, ldw, sa, sw, c16))
         return
     if (math or _State.math) == "bf16" and big_ok(M, K, N, _lib.BIG_NN):
-        (a16, lda), (w16, ldw) = _bf16_operands((dy, W))
+        (a16, lda), (w16, ldw) = _bf16_operands((dy, W), weight=1)
         C, c16 = _big_out(dx)
         side = sum(1 for t in (R, aux) if t is not None)
         nb = 2.0 * (M * N + N * K) + (2.0 if c16 else 4.0) * M * K + 4.0 * side * M * K

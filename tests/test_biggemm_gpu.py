@@ -196,42 +196,56 @@ def test_every_tile_shape(tile, monkeypatch):
     _check(db, _rb(y).sum(0), _rb(y).abs().sum(0))
 
 
-# ---- fp8 e4m3 instance (Ver5Config.linear_fp8; BASELINE.json configs[4]) ----
+# ---- fp8 e4m3 instance, MX block scaling (Ver5Config.linear_fp8; BASELINE.json configs[4]) ----
 
-def _q8(t):
-    """torch restatement of kdfm_fp8_quant: s = 448 / amax in f32, e4m3fn(sat(x s)); returns (bytes, 1 / s)"""
-    a = t.abs().max().float()
-    s = torch.tensor(448.0, dtype=torch.float32, device=t.device) / a
-    q = (t.float() * s).clamp(-448, 448).to(torch.float8_e4m3fn)
-    return q, (1.0 / s)
+def _mx(t):
+    """torch restatement of kdfm_fp8_quant_mx along the last dim: per 32-block e = ceil(log2(amax / 448)) (amax = 0:
+    -127), q = e4m3fn(x 2^-e); returns (q as e4m3fn, e per block as int), float64 math"""
+    x = t.double().reshape(t.shape[0], -1, 32)
+    amax = x.abs().max(2, keepdim=True).values
+    e = torch.ceil(torch.log2(amax.clamp_min(1e-300) / 448.0))
+    e = torch.where(amax > 0, e, torch.full_like(e, -127.0)).clamp(-127, 127)
+    q = (x / torch.pow(2.0, e)).float().to(torch.float8_e4m3fn).reshape(t.shape)
+    return q, e.squeeze(2).long()
 
 
-def test_fp8_quantisation_matches_torch():
+def _deq(q, e):
+    return (q.double().reshape(q.shape[0], -1, 32) * torch.pow(2.0, e.double()).unsqueeze(2)).reshape(q.shape)
+
+
+def _stage_major(e):
+    """[R][K/32] block exponents -> the kernel's stage-major scale bytes [(K/128)][R][4]"""
+    R, nb = e.shape
+    return (e + 127).to(torch.uint8).view(R, nb // 4, 4).permute(1, 0, 2).contiguous().view(-1)
+
+
+def test_fp8_mx_quantisation_matches_torch():
     K = _K()
     dev = "cuda"
     g = torch.Generator(device=dev).manual_seed(31)
     x = torch.randn(1000, 768, device=dev, generator=g) * 3
+    x[5, 64:96] = 0.0                       # an all-zero block
+    x[7, 0] = 1e4                           # an outlier block
     W = torch.randn(512, 768, device=dev, generator=g) * 0.02
-    (xa, lx, sx), (wa, lw, sw) = K._fp8_operands([(x, False), (W, True)])
+    (xa, lx, xs), (wa, lw, ws_) = K._fp8_operands([(x, False), (W, True)])
     torch.cuda.synchronize()
-    import ctypes as C
     buf = K.scratch(x.device, 1).view(torch.uint8)
     base = buf.data_ptr()
     xq = buf[xa - base: xa - base + 1000 * lx].view(1000, lx)[:, :768]
     wq = buf[wa - base: wa - base + 768 * lw].view(768, lw)[:, :512]
-    rx, dx = _q8(x)
-    rw, dw = _q8(W.t().contiguous())
-    assert torch.equal(xq, rx.view(torch.uint8)), "row-major quantisation differs from torch e4m3fn"
-    assert torch.equal(wq, rw.view(torch.uint8)), "transposed quantisation differs"
-    small = K.scratch(x.device, 12, slot=2)
-    got = small.view(-1)[: 8].cpu()
-    assert abs(float(got[1]) - float(dx)) <= 1e-7 * float(dx) and abs(float(got[5]) - float(dw)) <= 1e-7 * float(dw)
+    xsb = buf[xs - base: xs - base + 1000 * 768 // 32]
+    wsb = buf[ws_ - base: ws_ - base + 768 * 512 // 32]
+    rq, re = _mx(x)
+    rwq, rwe = _mx(W.t().contiguous())
+    assert torch.equal(xsb, _stage_major(re)), "row-major block scales differ"
+    assert torch.equal(xq, rq.view(torch.uint8)), "row-major MX quantisation differs from torch e4m3fn"
+    assert torch.equal(wsb, _stage_major(rwe)), "transposed block scales differ"
+    assert torch.equal(wq, rwq.view(torch.uint8)), "transposed MX quantisation differs"
 
 
-@pytest.mark.parametrize("M,N,K_", [(6432, 4096, 1024), (3001, 640, 512)])
+@pytest.mark.parametrize("M,N,K_", [(6432, 4096, 1024), (3000, 640, 512)])
 def test_fp8_linear_forward_and_dx(M, N, K_, monkeypatch):
     K = _K()
-    import kdfm._lib as L
     monkeypatch.setattr(K._State, "fp8", True)
     dev = "cuda"
     g = torch.Generator(device=dev).manual_seed(M)
@@ -247,22 +261,15 @@ def test_fp8_linear_forward_and_dx(M, N, K_, monkeypatch):
     monkeypatch.setattr(K, "call", call)
     y = torch.empty(M, N, device=dev)
     K.linear(x, W, b, y)
-    qx, dx_ = _q8(x)
-    qw, dw_ = _q8(W)
-    xd, wd = qx.double(), qw.double()
-    scale = float(dx_) * float(dw_)
-    ref = (xd @ wd.t()) * scale + b.double()
+    xd, wd = _deq(*_mx(x)), _deq(*_mx(W))
     # the block-scaled fp8 MFMA's accumulation is not an f32 fmaf chain over k: measured up to ~1.1e-5 of the
-    # absolute-product sum (tools: r6d), hence 2e-5 here (the e4m3 rounding itself is ~6e-2 relative)
-    _check(y, ref, (xd.abs() @ wd.abs().t()) * scale + b.double().abs(), 2e-5)
-    # data gradient: dy (fp8) times W^T quantised transposed
+    # absolute-product sum (profiles/r06), hence 2e-5 (the e4m3 rounding itself is ~6e-2 relative)
+    _check(y, xd @ wd.t() + b.double(), xd.abs() @ wd.abs().t() + b.double().abs(), 2e-5)
     dy = torch.randn(M, N, device=dev, generator=g)
     dxo = torch.empty(M, K_, device=dev)
     K.linear_dx(dy, W, dxo)
-    qd, sd = _q8(dy)
-    qwt, swt = _q8(W.t().contiguous())
-    ref = (qd.double() @ qwt.double().t()) * (float(sd) * float(swt))
-    _check(dxo, ref, (qd.double().abs() @ qwt.double().abs().t()) * (float(sd) * float(swt)), 2e-5)
+    dd, wtd = _deq(*_mx(dy)), _deq(*_mx(W.t().contiguous()))
+    _check(dxo, dd @ wtd.t(), dd.abs() @ wtd.abs().t(), 2e-5)
     assert n["fp8"] == 2, n
     y2 = torch.empty_like(y)
     K.linear(x, W, b, y2)
@@ -283,11 +290,8 @@ def test_fp8_silu_dropout_epilogue_bf16_out(monkeypatch):
     a16 = torch.empty(M, ff, device=dev, dtype=torch.bfloat16)
     h = torch.empty(M, ff, device=dev)
     K.linear(x, W1, b1, a16, epi=L.EPI_SILU | L.EPI_STORE_PRE, Cpre=h, dropout_p=0.1, seed=seed, rng_stream=9)
-    qx, sx = _q8(x)
-    qw, sw = _q8(W1)
-    sc = float(sx) * float(sw)
-    pre = (qx.double() @ qw.double().t()) * sc + b1.double()
-    _check(h, pre, (qx.double().abs() @ qw.double().abs().t()) * sc + b1.double().abs(), 2e-5)
+    xd, wd = _deq(*_mx(x)), _deq(*_mx(W1))
+    _check(h, xd @ wd.t() + b1.double(), xd.abs() @ wd.abs().t() + b1.double().abs(), 2e-5)
     monkeypatch.setattr(K._State, "fp8", False)
     K._BIG = False
     try:

@@ -273,10 +273,10 @@ def test_bf16_step_big_route_matches_float64_oracle(sub, B, N, lens, monkeypatch
 
 def test_fp8_xl_step_matches_float64_oracle(monkeypatch):
     """BASELINE.json configs[4] at its stated precision: the FastConformer-XL 2-layer step with linear_fp8 -- every
-    wide Linear's forward and data gradient on e4m3 operands (per-tensor current scaling, block-scaled MFMA), the
-    attention core and weight gradients bf16 -- against the float64 oracle.  Tolerances derived from the oracle's own
-    fp8 sensitivity: the same float64 step with those products' operands rounded to per-tensor
-    scaled e4m3 (x and W; the weights everywhere else to bf16); losses rel max(3e-3, 2.5 x sens), layer outputs and
+    wide Linear's forward and data gradient on MX e4m3 operands (an e8m0 scale per 32 contraction elements, block-
+    scaled MFMA), the attention core and weight gradients bf16 -- against the float64 oracle.  Tolerances derived from
+    the oracle's own fp8 sensitivity: the same float64 step with those products' operands
+    MX-rounded (x and W; the weights everywhere else to bf16); losses rel max(3e-3, 2.5 x sens), layer outputs and
     gradients rel. Frobenius max(floor, 2.5 x sens) with the bf16 test's floors."""
     from kdfm import kernels as K
     monkeypatch.setattr(K, "_BIG_MIN_WORK", 0.0)
@@ -296,8 +296,8 @@ def test_fp8_xl_step_matches_float64_oracle(monkeypatch):
 class _RoundedF:
     """torch.nn.functional for the oracle with the MFMA operand rounding of the wide products: F.linear and
     pointwise (kernel 1) F.conv1d whose weight is >= 512 x 512 and whose input has >= 512 rows get their input and
-    weight rounded -- to bf16, or to e4m3 with per-tensor current scaling (448 / amax) -- straight-through for
-    autograd.  Everything else is torch's."""
+    weight rounded -- to bf16, or to MX e4m3 (blocks of 32 along the contraction, block exponent
+    ceil(log2(amax / 448)), kdfm_fp8_quant_mx's rule) -- straight-through for autograd.  Everything else is torch's."""
 
     def __init__(self, fmt):
         self.fmt = fmt
@@ -306,13 +306,11 @@ class _RoundedF:
     def __getattr__(self, n):
         return getattr(self._F, n)
 
-    def _q(self, t):
+    def _q(self, t, dim=-1):
         if self.fmt == "bf16":
             q = t.bfloat16().to(t.dtype)
         else:
-            a = t.detach().abs().max().float()
-            sc = (torch.tensor(448.0, dtype=torch.float32) / a) if a > 0 else torch.tensor(1.0)
-            q = ((t.detach().float() * sc).clamp(-448, 448).to(torch.float8_e4m3fn).float() * (1.0 / sc)).to(t.dtype)
+            q = mx_round(t.detach().movedim(dim, -1)).movedim(-1, dim).to(t.dtype)
         return t + (q - t).detach()
 
     def _wide(self, rows, w):
@@ -325,8 +323,21 @@ class _RoundedF:
 
     def conv1d(self, x, w, b=None, *a, **kw):
         if w.dim() == 3 and w.shape[-1] == 1 and x.dim() == 3 and self._wide(x.shape[0] * x.shape[2], w[:, :, 0]):
-            x, w = self._q(x), self._q(w)
+            x, w = self._q(x, 1), self._q(w, 1)   # contraction = the input channels
         return self._F.conv1d(x, w, b, *a, **kw)
+
+
+def mx_round(t):
+    """MX e4m3 rounding along the last dim (blocks of 32; kdfm_fp8_quant_mx): e = ceil(log2(amax / 448)) per block,
+    q = e4m3(x 2^-e) 2^e, in float64."""
+    shp = t.shape
+    x = t.double().reshape(-1, 32)
+    amax = x.abs().max(1, keepdim=True).values
+    e = torch.ceil(torch.log2(amax.clamp_min(1e-300) / 448.0))
+    e = torch.where(amax > 0, e, torch.full_like(e, -127.0)).clamp(-127, 127)
+    sc = torch.pow(2.0, e)
+    q = (x / sc).float().to(torch.float8_e4m3fn).double() * sc
+    return q.reshape(shp)
 
 
 def _bf16_step_check(sub, B, N, lens, U, tl, round_acts=None):

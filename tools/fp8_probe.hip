@@ -9,8 +9,12 @@
 typedef int v8i __attribute__((ext_vector_type(8)));
 typedef float v4f __attribute__((ext_vector_type(4)));
 
-__global__ void probe_kernel(const int* a, const int* b, float* c, int sa, int sb) {
+__global__ void probe_kernel(const int* a, const int* b, float* c, int sa, int sb, const int* lsa, const int* lsb) {
   const int l = threadIdx.x;
+  if (lsa) {   // per-lane e8m0 scales (MX block scaling: one per lane = per 32 k-elements of one row / column)
+    sa = lsa[l];
+    sb = lsb[l];
+  }
   v8i av, bv;
   for (int i = 0; i < 8; ++i) {
     av[i] = a[l * 8 + i];
@@ -21,8 +25,8 @@ __global__ void probe_kernel(const int* a, const int* b, float* c, int sa, int s
   for (int r = 0; r < 4; ++r) c[l * 4 + r] = acc[r];
 }
 
-extern "C" int fp8_probe(const int* a, const int* b, float* c, int sa, int sb) {
-  hipLaunchKernelGGL(probe_kernel, dim3(1), dim3(64), 0, 0, a, b, c, sa, sb);
+extern "C" int fp8_probe(const int* a, const int* b, float* c, int sa, int sb, const int* lsa, const int* lsb) {
+  hipLaunchKernelGGL(probe_kernel, dim3(1), dim3(64), 0, 0, a, b, c, sa, sb, lsa, lsb);
   return (int)hipDeviceSynchronize();
 }
 

@@ -41,7 +41,7 @@ def main():
         c = torch.zeros(64, 4, device=dev)
         for sa, mult in ((0x7F7F7F7F, 1.0), (0x80808080, 2.0)):
             rc = lib.fp8_probe(C.c_void_p(da.data_ptr()), C.c_void_p(db.data_ptr()), C.c_void_p(c.data_ptr()),
-                               C.c_int(sa), C.c_int(0x7F7F7F7F))
+                               C.c_int(sa), C.c_int(0x7F7F7F7F), None, None)
             assert rc == 0, rc
             got = torch.zeros(16, 16, dtype=torch.float64)
             cc = c.cpu().double()
@@ -53,6 +53,38 @@ def main():
             if err == 0.0 and mult == 1.0:
                 ok_any = name
     print("MATCH:", ok_any)
+    # per-lane scales: lane l's e8m0 byte scales the 32 k-elements that lane holds (row / column l & 15, block
+    # l >> 4 under the first map) -- the MX block scaling biggemm.hip's fp8 instance relies on
+    f = maps()["k = 32 (l>>4) + j"]
+    ls_a = torch.randint(124, 131, (64,), generator=g, dtype=torch.int32)
+    ls_b = torch.randint(124, 131, (64,), generator=g, dtype=torch.int32)
+    ab = torch.zeros(64, 32, dtype=torch.uint8)
+    bb = torch.zeros(64, 32, dtype=torch.uint8)
+    for l in range(64):
+        for j in range(32):
+            ab[l, j] = A[l & 15, f(l, j)].to(torch.float8_e4m3fn).view(torch.uint8)
+            bb[l, j] = B[f(l, j), l & 15].to(torch.float8_e4m3fn).view(torch.uint8)
+    c = torch.zeros(64, 4, device=dev)
+    rc = lib.fp8_probe(C.c_void_p(ab.view(torch.int32).contiguous().to(dev).data_ptr()),
+                       C.c_void_p(bb.view(torch.int32).contiguous().to(dev).data_ptr()), C.c_void_p(c.data_ptr()),
+                       C.c_int(0), C.c_int(0), C.c_void_p(ls_a.to(dev).data_ptr()), C.c_void_p(ls_b.to(dev).data_ptr()))
+    torch.cuda.synchronize()
+    assert rc == 0, rc
+    exp = torch.zeros(16, 16, dtype=torch.float64)
+    for r in range(16):
+        for cc in range(16):
+            for gq in range(4):
+                ks = [f(16 * gq, j) for j in range(32)]
+                s_ = 2.0 ** (int(ls_a[16 * gq + r]) - 127) * 2.0 ** (int(ls_b[16 * gq + cc]) - 127)
+                exp[r, cc] += s_ * sum(float(A[r, k]) * float(B[k, cc]) for k in ks)
+    got = torch.zeros(16, 16, dtype=torch.float64)
+    cc_ = c.cpu().double()
+    for l in range(64):
+        for r in range(4):
+            got[4 * (l >> 4) + r, l & 15] = cc_[l, r]
+    lane_err = (got - exp).abs().max().item()
+    print(f"per-lane MX scales: max |C - ref| = {lane_err:g}", flush=True)
+    ok_any = ok_any if lane_err == 0.0 else None
     # v_cvt_pk_fp8_f32 against torch's OCP e4m3fn rounding (round to nearest even) on values inside +-448
     x = torch.cat([torch.linspace(-448, 448, 20001), torch.randn(20000) * 3, torch.randn(20000) * 1e-2])
     x = x[: (x.numel() // 2) * 2].contiguous()

@@ -5,7 +5,8 @@ copies as the library yardstick.  Prints TFLOP/s per product and direction:
             HBM (the kernel alone: what the XL step's bf16 intermediates feed it);
   big+cast: the same from f32 operands (each f32 operand cast to bf16 scratch first, kdfm_cast_bf16_2d);
   generic : the previous route (kdfm_gemm's 64x64 tile / row-parallel weight gradient), f32 operands;
-  fp8+quant: the fp8 e4m3 instance (linear_fp8) including the per-tensor quantisation of both operands.
+  fp8+quant: the fp8 e4m3 instance (linear_fp8) including the MX quantisation of both operands;
+  fp8 kernel: the fp8 kernel alone on operands quantised once.
 HIP events around N back-to-back launches (median of 3 rounds)."""
 import os
 import statistics
@@ -69,13 +70,10 @@ def main():
             keep = torch.empty(q.numel(), device=dev)
             keep.copy_(q)
             off = keep.data_ptr() - q.data_ptr()
-            sm = K.scratch(dev, 12, slot=2)
-            sk = sm.clone()
-            soff = sk.data_ptr() - sm.data_ptr()
             import kdfm._lib as L
             res["fwd fp8 kernel"] = bench(lambda: K.gemm(x16, W, y, M, N, Kd, 0, 0, 0, 0, y.stride(0), 1, amode=L.LD_KC,
                                                          bmode=L.LD_KC, epi=L.EPI_BIAS, bias=b,
-                                                         fp8=(a8 + off, lda, w8 + off, ldw, sa + soff, sw + soff, 0)))
+                                                         fp8=(a8 + off, lda, w8 + off, ldw, sa + off, sw + off, 0)))
         finally:
             K._State.fp8 = False
         K._BIG = False
