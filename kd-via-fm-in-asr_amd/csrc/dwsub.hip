@@ -31,6 +31,11 @@ __global__ void conv_lengths_kernel(const int64_t* __restrict__ in, int64_t* __r
 }
 
 // y[b, to, fo, c..c+3] = act(bias + sum_{i,j} w[c, i, j] * x[b, 2 to - pt + i, 2 fo - pf + j, c or 0])
+// A thread owns 4 channels of DWS_P consecutive output columns fo: its 36 taps and 4 biases are loaded once and
+// reused DWS_P times (one thread per output float4 re-read them from cache for every position: 45 loads per 4
+// outputs, 3.35 ms per FastConformer-XL first-stage launch, profiles/r06/r6e); lanes run over the channel groups,
+// so a wave's stores are contiguous and the broadcast input (BCAST) is one address per wave.
+constexpr int DWS_P = 8;
 template <bool BCAST>
 __global__ __launch_bounds__(DW_NT) void dws_fwd_kernel(const float* __restrict__ x, const int64_t* __restrict__ in_len,
                                                         const float* __restrict__ w, const float* __restrict__ bias,
@@ -38,50 +43,63 @@ __global__ __launch_bounds__(DW_NT) void dws_fwd_kernel(const float* __restrict_
                                                         int64_t B, int Ti, int Fi, int C, int To, int Fo, int pt, int pf,
                                                         int relu) {
   const int CV = C >> 2;
+  const int FB = (Fo + DWS_P - 1) / DWS_P;
   int64_t idx = (int64_t)blockIdx.x * DW_NT + threadIdx.x;
-  if (idx >= B * To * Fo * CV) return;
+  if (idx >= B * To * FB * CV) return;
   const int cg = (int)(idx % CV);
   int64_t r = idx / CV;
-  const int fo = (int)(r % Fo);
-  r /= Fo;
+  const int fb = (int)(r % FB);
+  r /= FB;
   const int to = (int)(r % To);
   const int64_t b = r / To;
   const int c = cg * 4;
-  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (!out_len || to < out_len[b]) {
-    acc = *reinterpret_cast<const float4*>(bias + c);
-    const int64_t lin = in_len ? in_len[b] : Ti;
+  const bool live = !out_len || to < out_len[b];
+  float wv[4][9];
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      const int ti = 2 * to - pt + i;
-      if (ti < 0 || ti >= Ti || ti >= lin) continue;
+  for (int q = 0; q < 4; ++q)
 #pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        const int fi = 2 * fo - pf + j;
-        if (fi < 0 || fi >= Fi) continue;
-        const int64_t pos = (b * Ti + ti) * Fi + fi;
-        float4 xv;
-        if constexpr (BCAST) {
-          const float s = x[pos];
-          xv = make_float4(s, s, s, s);
-        } else {
-          xv = *reinterpret_cast<const float4*>(x + pos * C + c);
+    for (int k = 0; k < 9; ++k) wv[q][k] = w[(c + q) * 9 + k];
+  const float4 bs = *reinterpret_cast<const float4*>(bias + c);
+  const int64_t lin = in_len ? in_len[b] : Ti;
+#pragma unroll
+  for (int pp = 0; pp < DWS_P; ++pp) {
+    const int fo = fb * DWS_P + pp;
+    if (fo >= Fo) break;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (live) {
+      acc = bs;
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        const int ti = 2 * to - pt + i;
+        if (ti < 0 || ti >= Ti || ti >= lin) continue;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          const int fi = 2 * fo - pf + j;
+          if (fi < 0 || fi >= Fi) continue;
+          const int64_t pos = (b * Ti + ti) * Fi + fi;
+          float4 xv;
+          if constexpr (BCAST) {
+            const float s = x[pos];
+            xv = make_float4(s, s, s, s);
+          } else {
+            xv = *reinterpret_cast<const float4*>(x + pos * C + c);
+          }
+          const int k = i * 3 + j;
+          acc.x += wv[0][k] * xv.x;
+          acc.y += wv[1][k] * xv.y;
+          acc.z += wv[2][k] * xv.z;
+          acc.w += wv[3][k] * xv.w;
         }
-        const int k = i * 3 + j;
-        acc.x += w[(c + 0) * 9 + k] * xv.x;
-        acc.y += w[(c + 1) * 9 + k] * xv.y;
-        acc.z += w[(c + 2) * 9 + k] * xv.z;
-        acc.w += w[(c + 3) * 9 + k] * xv.w;
+      }
+      if (relu) {
+        acc.x = fmaxf(acc.x, 0.f);
+        acc.y = fmaxf(acc.y, 0.f);
+        acc.z = fmaxf(acc.z, 0.f);
+        acc.w = fmaxf(acc.w, 0.f);
       }
     }
-    if (relu) {
-      acc.x = fmaxf(acc.x, 0.f);
-      acc.y = fmaxf(acc.y, 0.f);
-      acc.z = fmaxf(acc.z, 0.f);
-      acc.w = fmaxf(acc.w, 0.f);
-    }
+    *reinterpret_cast<float4*>(y + (((b * To + to) * Fo + fo) * (int64_t)C + c)) = acc;
   }
-  *reinterpret_cast<float4*>(y + idx * 4) = acc;
 }
 
 // dx[b, ti, fi, c] = relu'(xs) * sum over the (<= 2x2) outputs whose window covers (ti, fi) of
@@ -275,7 +293,7 @@ int kdfm_dwsub_conv(const float* x, const int64_t* in_len, const float* w, const
   KDFM_REQUIRE(((uintptr_t)bias | (uintptr_t)y | (Cin == 1 ? 0 : (uintptr_t)x)) % 16 == 0, "operands must be 16-byte aligned");
   int rc = dws_check(B, Ti, Fi, Cin, C, To, Fo, pad_t, pad_f);
   if (rc) return rc;
-  const int64_t n = B * To * Fo * (C / 4);
+  const int64_t n = B * To * ceil_div(Fo, DWS_P) * (C / 4);
   if (n == 0) return KDFM_OK;
   dim3 grid((unsigned)ceil_div(n, DW_NT));
   if (Cin == 1)

@@ -30,6 +30,25 @@ extern "C" int fp8_probe(const int* a, const int* b, float* c, int sa, int sb, c
   return (int)hipDeviceSynchronize();
 }
 
+// scale-slot probe: block t of the grid runs one MFMA on its own operands (a, b: [nb][64 lanes][8 words]) with its
+// own per-lane scales (lsa, lsb: [nb][64]) and writes its accumulators to c[t][64][4]
+__global__ void probe_batch_kernel(const int* a, const int* b, float* c, const int* lsa, const int* lsb) {
+  const int l = threadIdx.x, t = blockIdx.x;
+  v8i av, bv;
+  for (int i = 0; i < 8; ++i) {
+    av[i] = a[(t * 64 + l) * 8 + i];
+    bv[i] = b[(t * 64 + l) * 8 + i];
+  }
+  v4f acc = {0.f, 0.f, 0.f, 0.f};
+  acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(av, bv, acc, 0, 0, 0, lsa[t * 64 + l], 0, lsb[t * 64 + l]);
+  for (int r = 0; r < 4; ++r) c[(t * 64 + l) * 4 + r] = acc[r];
+}
+
+extern "C" int fp8_probe_batch(const int* a, const int* b, float* c, const int* lsa, const int* lsb, int nb) {
+  hipLaunchKernelGGL(probe_batch_kernel, dim3(nb), dim3(64), 0, 0, a, b, c, lsa, lsb);
+  return (int)hipDeviceSynchronize();
+}
+
 // f32 -> fp8 conversion check: v_cvt_pk_fp8_f32 (the builtin biggemm.hip's quantizer uses) on n inputs, byte out
 __global__ void cvt_kernel(const float* x, unsigned char* y, int n) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;

@@ -85,6 +85,57 @@ def main():
     lane_err = (got - exp).abs().max().item()
     print(f"per-lane MX scales: max |C - ref| = {lane_err:g}", flush=True)
     ok_any = ok_any if lane_err == 0.0 else None
+    # scale-slot map: for every operand slot (lane l, byte j) of A (then of B), a one-hot operand at that slot
+    # against ones in the partner operand's slots of the same byte and lane group, with lane L's scale 2^(L - 32):
+    # C's non-zero value names the lane whose scale byte the hardware applies to that slot
+    import numpy as np
+    one = 0x38   # 1.0 in e4m3
+    for opname in ("A", "B"):
+        a = np.zeros((2048, 64, 32), np.uint8)
+        b = np.zeros((2048, 64, 32), np.uint8)
+        for l0 in range(64):
+            for j0 in range(32):
+                t = l0 * 32 + j0
+                g = 16 * (l0 >> 4)
+                if opname == "A":
+                    a[t, l0, j0] = one
+                    b[t, g:g + 16, j0] = one
+                else:
+                    b[t, l0, j0] = one
+                    a[t, g:g + 16, j0] = one
+        lanes = (127 + np.arange(64) - 32).astype(np.int32)
+        unit = np.full(64, 127, np.int32)
+        lsa = np.tile(lanes if opname == "A" else unit, (2048, 1))
+        lsb = np.tile(unit if opname == "A" else lanes, (2048, 1))
+        da = torch.from_numpy(a.view(np.int32).copy()).to(dev)
+        db = torch.from_numpy(b.view(np.int32).copy()).to(dev)
+        dc = torch.zeros(2048, 64, 4, device=dev)
+        rc = lib.fp8_probe_batch(C.c_void_p(da.data_ptr()), C.c_void_p(db.data_ptr()), C.c_void_p(dc.data_ptr()),
+                                 C.c_void_p(torch.from_numpy(lsa.copy()).to(dev).data_ptr()),
+                                 C.c_void_p(torch.from_numpy(lsb.copy()).to(dev).data_ptr()), C.c_int(2048))
+        assert rc == 0, rc
+        cc = dc.cpu().numpy()
+        full = np.zeros((2048, 16, 16))
+        for l in range(64):
+            for r in range(4):
+                full[:, 4 * (l >> 4) + r, l & 15] = cc[:, l, r]
+        smap = np.full((64, 32), -1)
+        for l0 in range(64):
+            for j0 in range(32):
+                m = full[l0 * 32 + j0]
+                line = m[l0 & 15, :] if opname == "A" else m[:, l0 & 15]
+                vals = set(np.unique(line[line != 0]).tolist())
+                if len(vals) == 1 and (m != 0).sum() == 16:
+                    smap[l0, j0] = int(round(np.log2(vals.pop()))) + 32
+        print(f"scale lane for {opname} slot (lane, byte), lanes 0, 16, 32, 48 shown (-1 = inconsistent):", flush=True)
+        for l0 in (0, 1, 16, 32, 48):
+            print(f"  lane {l0:2d}: {smap[l0].tolist()}", flush=True)
+        for l0, j0 in ((0, 0), (1, 0), (5, 0), (16, 0), (32, 0), (0, 8), (0, 16), (0, 31)):
+            m = full[l0 * 32 + j0]
+            line = m[l0 & 15, :] if opname == "A" else m[:, l0 & 15]
+            print(f"  slot ({l0},{j0}) line as lanes: {[int(round(np.log2(v))) + 32 if v > 0 else None for v in line]}"
+                  f" nonzeros {(m != 0).sum()}", flush=True)
+        print(f"  slot scale lane == own lane: {(smap == np.arange(64)[:, None]).mean():.3f}", flush=True)
     # v_cvt_pk_fp8_f32 against torch's OCP e4m3fn rounding (round to nearest even) on values inside +-448
     x = torch.cat([torch.linspace(-448, 448, 20001), torch.randn(20000) * 3, torch.randn(20000) * 1e-2])
     x = x[: (x.numel() // 2) * 2].contiguous()
