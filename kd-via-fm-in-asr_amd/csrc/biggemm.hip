@@ -89,13 +89,15 @@ __device__ __forceinline__ bf16x8 frag_kc(const uint16_t* img, int r0, int hh, i
 typedef int bg_v8i __attribute__((ext_vector_type(8)));
 
 // fp8 fragment of 16 rows x 128 k out of a k-contiguous [rows][128 bytes] image (the bf16 image's byte layout):
-// v_mfma_scale_f32_16x16x128_f8f6f4's operand map, lane l -> row r0 + (l & 15), k = 32 (l >> 4) + j (bytes
-// 32 (l >> 4) .. + 31 of the row: chunks 2 (l >> 4) and 2 (l >> 4) + 1; tools/fp8_probe.py measured the map)
+// v_mfma_scale_f32_16x16x128_f8f6f4's operand map, lane l (g = l >> 4) -> row r0 + (l & 15), operand byte j -> k =
+// 16 g + j for j < 16 and 64 + 16 g + (j - 16) for j >= 16 (16-byte chunks g and 4 + g of the row); the e8m0 scale
+// of row r, 32-k block b is lane r + 16 b's scale byte (tools/fp8_scale_probe.py measured both on gfx950: each
+// lane's scale covers 16 bytes in each of two lanes, not its own 32 bytes)
 __device__ __forceinline__ bg_v8i frag_kc8(const uint16_t* img, int r0, int lane) {
   const int r = r0 + (lane & 15);
   const int g = lane >> 4;
-  const uint32_t a0 = lds_addr(img + r * BG_BK + 8 * ((2 * g) ^ kc_swz(r)));
-  const uint32_t a1 = lds_addr(img + r * BG_BK + 8 * ((2 * g + 1) ^ kc_swz(r)));
+  const uint32_t a0 = lds_addr(img + r * BG_BK + 8 * (g ^ kc_swz(r)));
+  const uint32_t a1 = lds_addr(img + r * BG_BK + 8 * ((4 + g) ^ kc_swz(r)));
   typedef int v4i __attribute__((ext_vector_type(4)));
   v4i lo, hi;
   asm volatile("ds_read_b128 %0, %1" : "=v"(lo) : "v"(a0));
@@ -228,7 +230,7 @@ __global__ __launch_bounds__(WM* WN * 64) void big_gemm_kernel(BigP p) {
     if constexpr (F8) {   // one block-scaled fp8 MFMA per accumulator tile covers the stage's 128 k
       bg_v8i af[FM], bfr[FN];
       int sca[FM], scb[FN];
-      // lane l's 32 operand bytes are k = 32 (l >> 4) .. + 31 of its row (frag_kc8), one MX block: its scale byte
+      // lane l supplies the scale byte of row l & 15, block l >> 4 (frag_kc8's map)
       const uint8_t* sbuf = reinterpret_cast<const uint8_t*>(abuf + AIMG + BIMG);
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
@@ -505,7 +507,7 @@ __global__ __launch_bounds__(256) void big_fold_kernel(float* C, int64_t sCm, co
 template <int BM, int BN, int WM, int WN, bool AT, bool BT, int EMODE, bool F8 = false>
 int big_launch(const BigP& p, hipStream_t st) {
   auto kern = big_gemm_kernel<BM, BN, WM, WN, AT, BT, EMODE, F8>;
-  constexpr int lds = 2 * (BM + BN) * BG_BK * 2;
+  constexpr int lds = 2 * ((BM + BN) * BG_BK + (F8 ? 1024 : 0)) * 2;   // two stages (big_gemm_kernel's STAGE)
   static const bool once = [&] {
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     return true;

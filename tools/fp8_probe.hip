@@ -44,7 +44,50 @@ __global__ void probe_batch_kernel(const int* a, const int* b, float* c, const i
   for (int r = 0; r < 4; ++r) c[(t * 64 + l) * 4 + r] = acc[r];
 }
 
+// the same with the accumulator read from c (so the destination registers are not the scale registers) and idle
+// cycles between the scale loads and the MFMA
+__global__ void probe_batch2_kernel(const int* a, const int* b, float* c, const int* lsa, const int* lsb) {
+  const int l = threadIdx.x, t = blockIdx.x;
+  v8i av, bv;
+  for (int i = 0; i < 8; ++i) {
+    av[i] = a[(t * 64 + l) * 8 + i];
+    bv[i] = b[(t * 64 + l) * 8 + i];
+  }
+  int sa = lsa[t * 64 + l], sb = lsb[t * 64 + l];
+  v4f acc;
+  for (int r = 0; r < 4; ++r) acc[r] = c[(t * 64 + l) * 4 + r];
+  asm volatile("s_waitcnt vmcnt(0)\n s_nop 7\n s_nop 7\n s_nop 7" : "+v"(sa), "+v"(sb), "+v"(acc));
+  acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(av, bv, acc, 0, 0, 0, sa, 0, sb);
+  for (int r = 0; r < 4; ++r) c[(t * 64 + l) * 4 + r] = acc[r];
+}
+
+// batch2 with the scale registers overwritten right after the MFMA issues (a write-after-read on the scale operands)
+__global__ void probe_batch3_kernel(const int* a, const int* b, float* c, const int* lsa, const int* lsb) {
+  const int l = threadIdx.x, t = blockIdx.x;
+  v8i av, bv;
+  for (int i = 0; i < 8; ++i) {
+    av[i] = a[(t * 64 + l) * 8 + i];
+    bv[i] = b[(t * 64 + l) * 8 + i];
+  }
+  int sa = lsa[t * 64 + l], sb = lsb[t * 64 + l];
+  v4f acc;
+  for (int r = 0; r < 4; ++r) acc[r] = c[(t * 64 + l) * 4 + r];
+  asm volatile("s_waitcnt vmcnt(0)\n s_nop 7" : "+v"(sa), "+v"(sb), "+v"(acc));
+  acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(av, bv, acc, 0, 0, 0, sa, 0, sb);
+  asm volatile("v_mov_b32 %0, 0\n v_mov_b32 %1, 0" : "+v"(sa), "+v"(sb));
+  for (int r = 0; r < 4; ++r) c[(t * 64 + l) * 4 + r] = acc[r] + 0.f * (float)(sa + sb);
+}
+
+extern "C" int fp8_probe_batch3(const int* a, const int* b, float* c, const int* lsa, const int* lsb, int nb) {
+  hipLaunchKernelGGL(probe_batch3_kernel, dim3(nb), dim3(64), 0, 0, a, b, c, lsa, lsb);
+  return (int)hipDeviceSynchronize();
+}
+
 extern "C" int fp8_probe_batch(const int* a, const int* b, float* c, const int* lsa, const int* lsb, int nb) {
+  if (nb < 0) {
+    hipLaunchKernelGGL(probe_batch2_kernel, dim3(-nb), dim3(64), 0, 0, a, b, c, lsa, lsb);
+    return (int)hipDeviceSynchronize();
+  }
   hipLaunchKernelGGL(probe_batch_kernel, dim3(nb), dim3(64), 0, 0, a, b, c, lsa, lsb);
   return (int)hipDeviceSynchronize();
 }
