@@ -678,6 +678,49 @@ __global__ __launch_bounds__(256) void mx_quant_kernel(const void* src, int bf, 
   }
 }
 
+// row-major, 16-byte rows (ld a multiple of 8 bf16 / 4 f32 elements, 16-byte aligned base): a workgroup pass is
+// 16 rows x one 128-column stage; a thread owns 8 consecutive elements (one 16-byte load of bf16, two of f32), 4
+// threads one MX block, 16 one stage row: each row's 128 output bytes and the 16 rows' 64 scale bytes (contiguous
+// in the stage-major layout) are written whole by the pass -- the 8-lanes-per-block kernel above wrote them in
+// 4-byte pieces and single scale bytes scattered over the stages
+__global__ __launch_bounds__(256) void mx_quant_rows_kernel(const void* src, int bf, int64_t rows, int64_t cols,
+                                                            int64_t ld, uint8_t* dst, int64_t ldd, uint8_t* xs) {
+  const int64_t nrt = (rows + 15) / 16, nt = nrt * (cols / 128);
+  const int j = threadIdx.x & 15;
+  for (int64_t t = blockIdx.x; t < nt; t += gridDim.x) {
+    const int64_t s = t / nrt, r = (t - s * nrt) * 16 + (threadIdx.x >> 4);
+    const bool ok = r < rows;
+    const int64_t o = (ok ? r : 0) * ld + 128 * s + 8 * j;
+    float v[8];
+    if (bf) {
+      const uint4 w = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(src) + o);
+      const uint32_t u[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        v[2 * i] = __uint_as_float(u[i] << 16);
+        v[2 * i + 1] = __uint_as_float(u[i] & 0xFFFF0000u);
+      }
+    } else {
+      const float4 a = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(src) + o);
+      const float4 b = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(src) + o + 4);
+      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+    }
+    float m = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) m = fmaxf(m, fabsf(v[i]));
+    m = fmaxf(m, __shfl_xor(m, 1, 64));
+    m = fmaxf(m, __shfl_xor(m, 2, 64));
+    const int e = mx_exp(m);
+    if (ok) {
+      uint2 w;
+      w.x = mx_q4(v[0], v[1], v[2], v[3], e);
+      w.y = mx_q4(v[4], v[5], v[6], v[7], e);
+      *reinterpret_cast<uint2*>(dst + r * ldd + 128 * s + 8 * j) = w;
+      if ((j & 3) == 0) xs[(s * rows + r) * 4 + (j >> 2)] = (uint8_t)(e + 127);
+    }
+  }
+}
+
 // transposed (the data gradient's W^T rows): output row c = source column c, blocks over 32 source rows; a 32 x 64
 // source tile through LDS, 4 lanes per output block (8 elements each)
 __global__ __launch_bounds__(256) void mx_quant_t_kernel(const void* src, int bf, int64_t rows, int64_t cols,
@@ -810,6 +853,10 @@ int kdfm_fp8_quant_mx(const void* src, int src_bf16, int64_t rows, int64_t cols,
   if (transpose) {
     const int64_t tiles = (rows / 32) * ceil_div(cols, 64);
     hipLaunchKernelGGL(mx_quant_t_kernel, dim3((unsigned)(tiles < 8192 ? tiles : 8192)), dim3(256), 0, st, src,
+                       src_bf16, rows, cols, ld, dst, ldd, scales);
+  } else if (((((uintptr_t)src) & 15) == 0) && ld % (src_bf16 ? 8 : 4) == 0) {
+    const int64_t tiles = ceil_div(rows, 16) * (cols / 128);
+    hipLaunchKernelGGL(mx_quant_rows_kernel, dim3((unsigned)(tiles < 16384 ? tiles : 16384)), dim3(256), 0, st, src,
                        src_bf16, rows, cols, ld, dst, ldd, scales);
   } else {
     const int64_t blocks = ceil_div(rows * (cols / 32), 32);

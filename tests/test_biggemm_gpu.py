@@ -241,6 +241,21 @@ def test_fp8_mx_quantisation_matches_torch():
     assert torch.equal(xq, rq.view(torch.uint8)), "row-major MX quantisation differs from torch e4m3fn"
     assert torch.equal(wsb, _stage_major(rwe)), "transposed block scales differ"
     assert torch.equal(wq, rwq.view(torch.uint8)), "transposed MX quantisation differs"
+    # bf16 sources (the large-tile route's activations): the row-tiled kernel (16-byte rows) and the
+    # 8-lanes-per-block kernel (a row stride that is not a multiple of 8 elements) give the same bytes
+    for cols_ld in (768, 772):
+        xb = torch.zeros(1000, cols_ld, device=dev, dtype=torch.bfloat16)
+        xb[:, :768] = x.bfloat16()
+        xv = xb[:, :768]
+        ((ba, lb, bs),) = K._fp8_operands([(xv, False)])
+        torch.cuda.synchronize()
+        buf = K.scratch(x.device, 1).view(torch.uint8)
+        base = buf.data_ptr()
+        bq = buf[ba - base: ba - base + 1000 * lb].view(1000, lb)[:, :768]
+        bsb = buf[bs - base: bs - base + 1000 * 768 // 32]
+        rbq, rbe = _mx(xv.float())
+        assert torch.equal(bsb, _stage_major(rbe)), f"bf16 block scales differ (ld {cols_ld})"
+        assert torch.equal(bq, rbq.view(torch.uint8)), f"bf16 MX quantisation differs (ld {cols_ld})"
 
 
 @pytest.mark.parametrize("M,N,K_", [(6432, 4096, 1024), (3000, 640, 512)])
