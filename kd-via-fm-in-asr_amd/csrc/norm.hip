@@ -4,6 +4,8 @@
 // per-block partials folded in block order (one fold launch can serve several LayerNorms).
 #include "common.h"
 
+#include <initializer_list>
+
 namespace kdfm {
 namespace {
 
@@ -134,6 +136,147 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ d
   }
 }
 
+// Wide rows with d % 256 == 0 (Conformer-large 512, FastConformer-XL 1024): the same two kernels on 16-byte lanes --
+// lane l owns columns 4 l + 256 i .. + 3 (NV = d / 256 float4 per row and tensor), so a row is NV 1 KB wave loads
+// instead of 4 NV 256-byte ones.  Same arithmetic per element; the row sums group the columns per lane differently.
+template <int NV>
+__global__ __launch_bounds__(256) void ln_fwd_v4_kernel(const float* __restrict__ x, const float* __restrict__ g,
+                                                        const float* __restrict__ b, float* __restrict__ y,
+                                                        float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                        int64_t rows, int d, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const float* xr = x + row * d;
+  float4 v[NV], gv[NV], bv[NV];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = 4 * lane + 256 * i;
+    v[i] = *reinterpret_cast<const float4*>(xr + c);
+    gv[i] = *reinterpret_cast<const float4*>(g + c);
+    bv[i] = *reinterpret_cast<const float4*>(b + c);
+  }
+#pragma unroll
+  for (int i = 0; i < NV; ++i) s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+  const float mu = wave_sum(s) / d;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const float a0 = v[i].x - mu, a1 = v[i].y - mu, a2 = v[i].z - mu, a3 = v[i].w - mu;
+    q += (a0 * a0 + a1 * a1) + (a2 * a2 + a3 * a3);
+  }
+  const float rs = rsqrtf(wave_sum(q) / d + eps);
+  float* yr = y + row * d;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = 4 * lane + 256 * i;
+    float4 o;
+    o.x = (v[i].x - mu) * rs * gv[i].x + bv[i].x;
+    o.y = (v[i].y - mu) * rs * gv[i].y + bv[i].y;
+    o.z = (v[i].z - mu) * rs * gv[i].z + bv[i].z;
+    o.w = (v[i].w - mu) * rs * gv[i].w + bv[i].w;
+    *reinterpret_cast<float4*>(yr + c) = o;
+  }
+  if (lane == 0) {
+    mean_out[row] = mu;
+    rstd_out[row] = rs;
+  }
+}
+
+template <int NV>
+__global__ __launch_bounds__(256) void ln_bwd_v4_kernel(const float* __restrict__ dy, const float* __restrict__ x,
+                                                        const float* __restrict__ g, const float* __restrict__ mean,
+                                                        const float* __restrict__ rstd, const float* dres, float* dx,
+                                                        float* __restrict__ part, int64_t rows, int d,
+                                                        const float* __restrict__ dy2) {
+  __shared__ float red[2][4][256 * NV];
+  constexpr int RB = NV > 2 ? 2 : LN_RPW;   // rows whose values are held at once
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float gl[NV][4], pg[NV][4], pb[NV][4];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const float4 t = *reinterpret_cast<const float4*>(g + 4 * lane + 256 * i);
+    gl[i][0] = t.x; gl[i][1] = t.y; gl[i][2] = t.z; gl[i][3] = t.w;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) pg[i][e] = pb[i][e] = 0.f;
+  }
+  const int64_t base = ((int64_t)blockIdx.x * 4 + w) * LN_RPW;
+#pragma unroll
+  for (int j0 = 0; j0 < LN_RPW; j0 += RB) {
+    float dyv[RB][NV][4], xv[RB][NV][4], rv[RB][NV][4], mu[RB], rs[RB];
+#pragma unroll
+    for (int j = 0; j < RB; ++j) {
+      const int64_t row = base + j0 + j;
+      const bool ok = row < rows;
+      const int64_t r = ok ? row : 0;
+      mu[j] = mean[r];
+      rs[j] = rstd[r];
+      const float m = ok ? 1.f : 0.f;
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        const int64_t o = r * d + 4 * lane + 256 * i;
+        float4 a = *reinterpret_cast<const float4*>(dy + o);
+        if (dy2) {
+          const float4 a2 = *reinterpret_cast<const float4*>(dy2 + o);
+          a.x += a2.x; a.y += a2.y; a.z += a2.z; a.w += a2.w;
+        }
+        const float4 xx = *reinterpret_cast<const float4*>(x + o);
+        const float4 rr = dres ? *reinterpret_cast<const float4*>(dres + o) : make_float4(0.f, 0.f, 0.f, 0.f);
+        dyv[j][i][0] = a.x * m; dyv[j][i][1] = a.y * m; dyv[j][i][2] = a.z * m; dyv[j][i][3] = a.w * m;
+        xv[j][i][0] = xx.x; xv[j][i][1] = xx.y; xv[j][i][2] = xx.z; xv[j][i][3] = xx.w;
+        rv[j][i][0] = rr.x; rv[j][i][1] = rr.y; rv[j][i][2] = rr.z; rv[j][i][3] = rr.w;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < RB; ++j) {
+      const int64_t row = base + j0 + j;
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int i = 0; i < NV; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float xh = (xv[j][i][e] - mu[j]) * rs[j];
+          xv[j][i][e] = xh;
+          const float gy = dyv[j][i][e] * gl[i][e];
+          pg[i][e] += dyv[j][i][e] * xh;
+          pb[i][e] += dyv[j][i][e];
+          s1 += gy;
+          s2 += gy * xh;
+        }
+      s1 = wave_sum(s1) / d;
+      s2 = wave_sum(s2) / d;
+      if (row < rows) {
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+          float o[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] = rs[j] * (dyv[j][i][e] * gl[i][e] - s1 - xv[j][i][e] * s2) + rv[j][i][e];
+          *reinterpret_cast<float4*>(dx + row * d + 4 * lane + 256 * i) = make_float4(o[0], o[1], o[2], o[3]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    *reinterpret_cast<float4*>(&red[0][w][4 * lane + 256 * i]) = make_float4(pg[i][0], pg[i][1], pg[i][2], pg[i][3]);
+    *reinterpret_cast<float4*>(&red[1][w][4 * lane + 256 * i]) = make_float4(pb[i][0], pb[i][1], pb[i][2], pb[i][3]);
+  }
+  __syncthreads();
+  float* pr = part + (int64_t)blockIdx.x * 2 * d;
+  for (int c = threadIdx.x; c < d; c += 256) {
+    pr[c] = (red[0][0][c] + red[0][1][c]) + (red[0][2][c] + red[0][3][c]);
+    pr[d + c] = (red[1][0][c] + red[1][1][c]) + (red[1][2][c] + red[1][3][c]);
+  }
+}
+
+__host__ inline bool ln_v4_ok(int64_t d, std::initializer_list<const void*> ptrs) {
+  if (d % 256 != 0 || d > 1024) return false;
+  for (const void* p : ptrs)
+    if (((uintptr_t)p) & 15) return false;
+  return true;
+}
+
 // Ordered fold of LayerNorm partials for up to KDFM_LN_FOLD_MAX LayerNorms in one launch:
 // dgamma_e[c] += sum_b part_e[b][c], dbeta_e[c] += sum_b part_e[b][d + c].  grid = (column groups of
 // 64 over 2d, entries); lane = column, the 4 waves stride the partial rows, fixed-order combine
@@ -198,6 +341,15 @@ int ln_bwd_launch(const float* dy, const float* x, const float* gamma, const flo
                   const float* dy2 = nullptr) {
   const int64_t blocks = ceil_div(rows, 4 * LN_RPW);
   const dim3 grid((unsigned)blocks), blk(256);
+  if (ln_v4_ok(d, {dy, x, gamma, dres, dx, dy2})) {
+#define LNB4(NV) hipLaunchKernelGGL(ln_bwd_v4_kernel<NV>, grid, blk, 0, st, dy, x, gamma, mean, rstd, dres, dx, part, rows, (int)d, dy2)
+    if (d == 256) LNB4(1);
+    else if (d == 512) LNB4(2);
+    else if (d == 768) LNB4(3);
+    else LNB4(4);
+#undef LNB4
+    return check_launch("kdfm_layernorm_bwd");
+  }
   const int64_t v = (d + 63) / 64;
 #define LNB(V) hipLaunchKernelGGL(ln_bwd_kernel<V>, grid, blk, 0, st, dy, x, gamma, mean, rstd, dres, dx, part, rows, (int)d, dy2)
   if (v == 1) LNB(1);
@@ -213,6 +365,15 @@ int ln_bwd_launch(const float* dy, const float* x, const float* gamma, const flo
 int ln_fwd_launch(const float* x, const float* gamma, const float* beta, float* y, float* mean, float* rstd,
                   int64_t rows, int64_t d, float eps, hipStream_t st) {
   const dim3 grid((unsigned)ceil_div(rows, 4)), blk(256);
+  if (ln_v4_ok(d, {x, gamma, beta, y})) {
+#define LNF4(NV) hipLaunchKernelGGL(ln_fwd_v4_kernel<NV>, grid, blk, 0, st, x, gamma, beta, y, mean, rstd, rows, (int)d, eps)
+    if (d == 256) LNF4(1);
+    else if (d == 512) LNF4(2);
+    else if (d == 768) LNF4(3);
+    else LNF4(4);
+#undef LNF4
+    return check_launch("kdfm_layernorm_fwd");
+  }
   const int64_t v = (d + 63) / 64;
 #define LNF(V) hipLaunchKernelGGL(ln_fwd_kernel<V>, grid, blk, 0, st, x, gamma, beta, y, mean, rstd, rows, (int)d, eps)
   if (v == 1) LNF(1);

@@ -48,15 +48,34 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const
   const float bc2 = 1.f - powf(b2, (float)ka);
   const float step_size = lr / bc1;
   const float bc2s = sqrtf(bc2);
+  auto upd = [&](float& pi, float gi, float& mi, float& vi) {
+    gi *= gscale;
+    pi *= (1.f - lr * wd);
+    mi = b1 * mi + (1.f - b1) * gi;
+    vi = b2 * vi + (1.f - b2) * gi * gi;
+    pi -= step_size * mi / (sqrtf(vi) / bc2s + eps);
+  };
   const int64_t stride = (int64_t)gridDim.x * 256;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
-    const float gi = g[i] * gscale;
-    float pi = p[i] * (1.f - lr * wd);
-    const float mi = b1 * m[i] + (1.f - b1) * gi;
-    const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
+  // 16-byte lanes when the four buffers are aligned (the flat parameter buffer is): the same per-element update
+  const bool vec = ((((uintptr_t)p) | ((uintptr_t)g) | ((uintptr_t)m) | ((uintptr_t)v)) & 15) == 0;
+  const int64_t n4 = vec ? n / 4 : 0;
+  for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < n4; q += stride) {
+    float4 pp = reinterpret_cast<float4*>(p)[q], mm = reinterpret_cast<float4*>(m)[q];
+    float4 vv = reinterpret_cast<float4*>(v)[q];
+    const float4 gg = reinterpret_cast<const float4*>(g)[q];
+    upd(pp.x, gg.x, mm.x, vv.x);
+    upd(pp.y, gg.y, mm.y, vv.y);
+    upd(pp.z, gg.z, mm.z, vv.z);
+    upd(pp.w, gg.w, mm.w, vv.w);
+    reinterpret_cast<float4*>(m)[q] = mm;
+    reinterpret_cast<float4*>(v)[q] = vv;
+    reinterpret_cast<float4*>(p)[q] = pp;
+  }
+  for (int64_t i = 4 * n4 + (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+    float pi = p[i], mi = m[i], vi = v[i];
+    upd(pi, g[i], mi, vi);
     m[i] = mi;
     v[i] = vi;
-    pi -= step_size * mi / (sqrtf(vi) / bc2s + eps);
     p[i] = pi;
   }
 }

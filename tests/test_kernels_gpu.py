@@ -18,7 +18,8 @@ def _close(a, b, rel=1e-4):
     assert err <= tol, f"max err {err} > {tol}"
 
 
-@pytest.mark.parametrize("rows,d", [(1, 88), (63, 88), (12832, 88), (1000, 176), (77, 256), (130, 40)])
+@pytest.mark.parametrize("rows,d", [(1, 88), (63, 88), (12832, 88), (1000, 176), (77, 256), (130, 40),
+                                    (1001, 512), (50, 768), (6432, 1024)])   # d % 256 == 0: the 16-byte-lane kernels
 def test_layernorm_bwd(rows, d):
     K = _K()
     g = torch.Generator().manual_seed(rows + d)
