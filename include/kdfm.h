@@ -162,7 +162,8 @@ int kdfm_gemm(const kdfm_gemm_desc* d, void* stream);
  * ACCUMULATE: C += alpha * result, and ones_out[m] += alpha * sum_k A(m, k) when ones_out is set (the bias
  * gradient) -- one writer per element, fixed summation order (deterministic, unlike kdfm_gemm's split-K).
  * A, B 16-byte aligned, lda / ldb multiples of 8; kdfm_gemm_big_supported(M, N, K, layout) says whether the
- * shape is taken (k-contiguous A: K % 64 == 0; k-major operands: their row length % 8 == 0). */
+ * shape is taken (M, N, K >= 64; k-contiguous operands: K % 8 == 0, the tail k-step zeroes the chunks past K;
+ * k-major operands: their row length % 8 == 0). */
 #define KDFM_BIG_NT 0
 #define KDFM_BIG_NN 1
 #define KDFM_BIG_TN 2

@@ -165,10 +165,13 @@ __global__ __launch_bounds__(WM* WN * 64) void big_gemm_kernel(BigP p) {
         const int c = (lane & 7) ^ kc_swz(row);
         int64_t gr = r0 + row;
         gr = gr < R ? gr : R - 1;
-        if constexpr (F8)
+        if constexpr (F8) {
           src = reinterpret_cast<const uint16_t*>(reinterpret_cast<const char*>(X) + gr * ld + k0 + 16 * c);
-        else
-          src = X + gr * ld + k0 + 8 * c;
+        } else {
+          // a chunk past K (K % 64 != 0, K % 8 == 0) reads the row's first chunk instead; the tail step zeroes it
+          const int64_t kk = k0 + 8 * c < K ? k0 + 8 * c : 0;
+          src = X + gr * ld + kk;
+        }
       } else {     // [64 k][W cols], 1024 / (2 W) rows per piece
         const int byte = 1024 * fl + 16 * lane;
         const int row = byte / (2 * W);
@@ -217,12 +220,26 @@ __global__ __launch_bounds__(WM* WN * 64) void big_gemm_kernel(BigP p) {
     const int s = t & 1;
     const uint16_t* abuf = bg_lds + s * STAGE;
     const uint16_t* bbuf = abuf + AIMG;
-    if constexpr (AT || BT) {
+    if constexpr (!F8) {
       const int64_t vr = K - kb - (int64_t)t * BG_BK;
-      if (vr < BG_BK) {   // tail step: zero the k-major A (or B) rows past K (their DMA read clamped rows)
-        uint16_t* z = bg_lds + s * STAGE + (AT ? 0 : AIMG);
-        constexpr int ZW = AT ? BM : BN;
-        for (int e = threadIdx.x; e < (BG_BK - (int)vr) * ZW; e += NW * 64) z[(int)vr * ZW + e] = 0;
+      if (vr < BG_BK) {   // tail step
+        if constexpr (AT || BT) {   // zero the k-major A (or B) rows past K (their DMA read clamped rows)
+          uint16_t* z = bg_lds + s * STAGE + (AT ? 0 : AIMG);
+          constexpr int ZW = AT ? BM : BN;
+          for (int e = threadIdx.x; e < (BG_BK - (int)vr) * ZW; e += NW * 64) z[(int)vr * ZW + e] = 0;
+        }
+        if constexpr (!AT || !BT) {   // zero the k-contiguous images' 16-byte chunks past K (a row's first chunk)
+          constexpr int ZR = (AT ? 0 : BM) + (BT ? 0 : BN);
+          for (int e = threadIdx.x; e < ZR * 8; e += NW * 64) {
+            const int row = e >> 3, pch = e & 7;
+            const int c = pch ^ kc_swz(row < (AT ? 0 : BM) ? row : row - (AT ? 0 : BM));
+            if (8 * c >= vr) {
+              uint16_t* img = bg_lds + s * STAGE + (row < (AT ? 0 : BM) ? 0 : AIMG);
+              const int rr = row < (AT ? 0 : BM) ? row : row - (AT ? 0 : BM);
+              *reinterpret_cast<uint4*>(img + rr * BG_BK + 8 * pch) = make_uint4(0u, 0u, 0u, 0u);
+            }
+          }
+        }
         __syncthreads();
       }
     }
@@ -784,9 +801,9 @@ int64_t kdfm_gemm_big_ws(int64_t M, int64_t N, int64_t K, int layout) {
 
 int kdfm_gemm_big_supported(int64_t M, int64_t N, int64_t K, int layout) {
   using namespace kdfm;
-  if (M < 128 || N < 128 || K < 64 || layout < 0 || layout > 2) return 0;
+  if (M < 64 || N < 64 || K < 64 || layout < 0 || layout > 2) return 0;
   if (layout == KDFM_BIG_NT || layout == KDFM_BIG_NN) {
-    if (K % BG_BK) return 0;   // the k-contiguous A image has no tail handling
+    if (K % 8) return 0;   // the k-contiguous images' tail step zeroes whole 16-byte chunks
   }
   if (layout == KDFM_BIG_NN && N % 8) return 0;
   if (layout == KDFM_BIG_TN && (M % 8 || N % 8)) return 0;

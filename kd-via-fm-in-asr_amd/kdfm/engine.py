@@ -206,7 +206,8 @@ class Ver5Engine:
     def _mode(self):
         """The config's MFMA arithmetic and reduction mode for the duration of a call (restored
         afterwards: the kernels' modes are process-global)."""
-        return K.mode(self.cfg.math, self.cfg.deterministic, fp8=self.cfg.linear_fp8)
+        return K.mode(self.cfg.math, self.cfg.deterministic, fp8=self.cfg.linear_fp8,
+                      wide=max(self.cfg.d_student, self.cfg.d_teacher) >= 512)
 
     def forward(self, wav, wav_len, targets, tgt_len, *, train=True, eps=None, save=True):
         """One forward pass; returns the context backward() consumes.  eps: optional injected

@@ -162,25 +162,36 @@ class mode:
     """Context manager: run a block in the given MFMA arithmetic / reduction mode and restore the
     previous process-global modes afterwards (the engine applies its config this way)."""
 
-    def __init__(self, math: str | None = None, deterministic: bool | None = None, fp8: bool | None = None):
-        self.math, self.det, self.fp8 = math, deterministic, fp8
+    def __init__(self, math: str | None = None, deterministic: bool | None = None, fp8: bool | None = None,
+                 wide: bool | None = None):
+        self.math, self.det, self.fp8, self.wide = math, deterministic, fp8, wide
 
     def __enter__(self):
-        self._saved = (_State.math, _State.deterministic, _State.fp8)
+        self._saved = (_State.math, _State.deterministic, _State.fp8, _State.wide)
         if self.math is not None:
             set_math(self.math)
         if self.det is not None and self.det != _State.deterministic:
             set_deterministic(self.det)
         if self.fp8 is not None:
             _State.fp8 = bool(self.fp8)
+        if self.wide is not None:
+            _State.wide = bool(self.wide)
         return self
 
     def __exit__(self, *a):
-        m, d, f8 = self._saved
+        m, d, f8, w = self._saved
         set_math(m)
         if d != _State.deterministic:
             set_deterministic(d)
         _State.fp8 = f8
+        _State.wide = w
+
+
+def set_wide(on: bool) -> None:
+    """Wide-model routing (d_model >= 512): the large-tile route also takes products with a dimension in
+    [64, 512) when another is >= 1024 (big_ok).  Process-global like the math mode; the engine sets it from
+    its config for the duration of a call."""
+    _State.wide = bool(on)
 
 
 def set_fp8(on: bool) -> None:
@@ -194,6 +205,7 @@ def get_fp8() -> bool:
 
 
 _State.fp8_epoch = None
+_State.wide = False
 _FP8_W = {}   # (address, rows, cols, row stride, transposed) -> [epoch, storage, (address, ld, scales)]
 _BF16_W = {}  # (address, rows, cols, row stride) -> [epoch, bf16 storage]
 
@@ -527,8 +539,13 @@ _BIG_MIN_WORK = float(os.environ.get("KDFM_BIG_MIN_WORK", str(2 ** 31)))   # M *
 
 
 def big_ok(M, N, K, layout) -> bool:
-    """The large-tile route takes this product (bf16 math, every dimension >= 512, M * N * K >= 2^31)."""
-    if not _BIG or _State.math != "bf16" or min(M, N, K) < 512 or float(M) * N * K < _BIG_MIN_WORK:
+    """The large-tile route takes this product (bf16 math, M * N * K >= 2^31, every dimension >= 512 -- or, in
+    the wide-model mode (set_wide: d_model >= 512, the engine's config), every dimension >= 64 and one >= 1024:
+    FastConformer-XL's 256-channel pointwise subsampling convs and its d -> 1024 distillation-head projections)."""
+    if not _BIG or _State.math != "bf16" or float(M) * N * K < _BIG_MIN_WORK:
+        return False
+    lo = min(M, N, K)
+    if lo < 512 and not (_State.wide and lo >= 64 and max(M, N, K) >= 1024):
         return False
     return bool(_lib.lib().kdfm_gemm_big_supported(int(M), int(N), int(K), int(layout)))
 
@@ -567,8 +584,9 @@ def _bf16_operands(ts, weight=None):
 
 def fp8_ok(M, N, K) -> bool:
     """The fp8 instance takes this k-contiguous product (fp8 mode on, the large-tile route applies, K % 128 == 0,
-    M and N multiples of 4)."""
-    return (_State.fp8 and K % 128 == 0 and M % 4 == 0 and N % 4 == 0 and M >= 128 and N >= 128
+    M and N multiples of 4, every dimension >= 512: the layer Linears; the wide-model mode's narrower products
+    (set_wide) stay bf16)."""
+    return (_State.fp8 and K % 128 == 0 and M % 4 == 0 and N % 4 == 0 and min(M, N, K) >= 512
             and big_ok(M, N, K, _lib.BIG_NT))
 
 

@@ -61,6 +61,34 @@ def test_linear_forward_plain_and_bias(M, N, K_):
     assert torch.equal(y, y2), "not deterministic"
 
 
+@pytest.mark.parametrize("M,N,K_", [(5000, 1024, 96), (4100, 96, 1024), (3000, 256, 200), (2000, 136, 264)])
+def test_wide_mode_narrow_products_and_k_tails(M, N, K_, monkeypatch):
+    """The wide-model mode (set_wide: FastConformer-XL) sends products with a dimension in [64, 512) to the large-tile
+    route: the distillation heads' d -> 1024 / 1024 -> d projections (K or N = 96), the 256-channel pointwise convs;
+    K % 64 != 0 exercises the k-contiguous images' zeroed tail step (forward NT over K, data gradient NN over N)."""
+    K = _K()
+    import kdfm._lib as L
+    monkeypatch.setattr(K._State, "wide", True)
+    dev = "cuda"
+    g = torch.Generator(device=dev).manual_seed(M + 7 * N + K_)
+    x = torch.randn(M, K_, device=dev, generator=g)
+    W = torch.randn(N, K_, device=dev, generator=g) * 0.05
+    b = torch.randn(N, device=dev, generator=g)
+    assert K.big_ok(M, N, K_, L.BIG_NT)
+    y = torch.empty(M, N, device=dev)
+    K.linear(x, W, b, y)
+    assert K.ROUTES[int(L.lib().kdfm_gemm_last_route())] == "big"
+    _check(y, _rb(x) @ _rb(W).t() + b.double(), _rb(x).abs() @ _rb(W).abs().t() + b.double().abs())
+    dy = torch.randn(M, N, device=dev, generator=g)
+    dx = torch.empty(M, K_, device=dev)
+    if K.big_ok(M, K_, N, L.BIG_NN):
+        K.linear_dx(dy, W, dx)
+        assert K.ROUTES[int(L.lib().kdfm_gemm_last_route())] == "big"
+        _check(dx, _rb(dy) @ _rb(W), _rb(dy).abs() @ _rb(W).abs())
+    monkeypatch.setattr(K._State, "wide", False)
+    assert not K.big_ok(M, N, K_, L.BIG_NT), "narrow products leave the large-tile route outside the wide mode"
+
+
 def test_linear_silu_dropout_store_pre_bf16_out_and_residual():
     K = _K()
     import kdfm._lib as L

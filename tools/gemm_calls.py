@@ -1,6 +1,7 @@
 """Which Python call sites issue the compute-stream kdfm_gemm launches of one bench step, with their
 shapes: one eager train step with K.call patched to log each kdfm_gemm descriptor (M, N, K, batch, modes,
-epilogue), its stream and the calling frames.  usage: python tools/gemm_calls.py [out.txt]"""
+epilogue), its stream and the calling frames.  usage: python tools/gemm_calls.py [out.txt] [xl]
+(xl: the FastConformer-XL shapes of bench.py's xl_shape_sensitivity line)"""
 import os
 import sys
 import traceback
@@ -14,9 +15,15 @@ from kdfm.config import DEFAULT  # noqa: E402
 from kdfm.engine import Ver5Engine, synthetic_batch  # noqa: E402
 
 dev = torch.device("cuda", 0)
-K.set_math(DEFAULT.math)
-eng = Ver5Engine(DEFAULT, dev)
-wav, wl, tg, tl = synthetic_batch(DEFAULT, 32, 256000, 100, dev, seed=1234)
+CFG = DEFAULT
+if len(sys.argv) > 2 and sys.argv[2] == "xl":
+    from dataclasses import replace
+    sys.path.insert(0, ROOT)
+    from bench import XL_SHAPES
+    CFG = replace(DEFAULT, **XL_SHAPES)
+K.set_math(CFG.math)
+eng = Ver5Engine(CFG, dev)
+wav, wl, tg, tl = synthetic_batch(CFG, 32, 256000, 100, dev, seed=1234)
 eng.train_step(wav, wl, tg, tl, None)
 torch.cuda.synchronize()
 names = {eng.compute_stream.cuda_stream: "compute", eng._side_stream().cuda_stream: "teacher"}
@@ -33,9 +40,12 @@ def call(name, *args):
         s = args[-1]
         s = s.value if hasattr(s, "value") else s
         fr = [f"{os.path.basename(f.filename)}:{f.lineno}:{f.name}" for f in traceback.extract_stack()[-6:-2]]
-        log.append(f"{names.get(s, s):8s} M={d.M} N={d.N} K={d.K} batch={d.batch1}x{d.batch2} amode={d.amode} "
-                   f"bmode={d.bmode} epi={d.epi} math={d.math} grid~({-(-d.M // 64)},{-(-d.N // 64)})  " + " < ".join(reversed(fr)))
+        route = None
     orig(name, *args)
+    if name == "kdfm_gemm":
+        route = K.ROUTES[int(K._lib.lib().kdfm_gemm_last_route())]
+        log.append(f"{names.get(s, s):8s} route={route} M={d.M} N={d.N} K={d.K} batch={d.batch1}x{d.batch2} amode={d.amode} "
+                   f"bmode={d.bmode} epi={d.epi} math={d.math} grid~({-(-d.M // 64)},{-(-d.N // 64)})  " + " < ".join(reversed(fr)))
 
 
 K.call = call
