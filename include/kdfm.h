@@ -686,6 +686,10 @@ int64_t kdfm_edit_distance(const int32_t* a, int64_t na, const int32_t* b, int64
 /* ---------------- ConformerLayer (Appendix A.5-A.8; layers built conformer_encoder.py:450-472) */
 int kdfm_layernorm_fwd(const float* x, const float* gamma, const float* beta, float* y, float* mean, float* rstd,
                        int64_t rows, int64_t d, float eps, void* stream);
+/* The same LayerNorm with a bf16 y (round to nearest even) for an LN output whose every consumer reads bf16 operands
+ * (the large-tile GEMM's forward and weight gradient, FastConformer(-XL)); d % 256 == 0, 16-byte aligned rows. */
+int kdfm_layernorm_fwd_bf16(const float* x, const float* gamma, const float* beta, uint16_t* y, float* mean,
+                            float* rstd, int64_t rows, int64_t d, float eps, void* stream);
 /* dx = LN'(dy) (+ dres if non-null); dgamma/dbeta accumulate (+=). */
 /* dgamma/dbeta are accumulated (+=) through per-block partials in ws, which must hold at least
  * kdfm_layernorm_bwd_ws(rows, d) floats (no zeroing needed) */

@@ -139,9 +139,11 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ d
 // Wide rows with d % 256 == 0 (Conformer-large 512, FastConformer-XL 1024): the same two kernels on 16-byte lanes --
 // lane l owns columns 4 l + 256 i .. + 3 (NV = d / 256 float4 per row and tensor), so a row is NV 1 KB wave loads
 // instead of 4 NV 256-byte ones.  Same arithmetic per element; the row sums group the columns per lane differently.
-template <int NV>
+// BF: y is bf16 (round to nearest even -- the bits the large-tile GEMM's cast of an f32 y would produce), for an LN
+// output whose every consumer reads bf16 operands (kdfm_layernorm_fwd_bf16)
+template <int NV, bool BF = false>
 __global__ __launch_bounds__(256) void ln_fwd_v4_kernel(const float* __restrict__ x, const float* __restrict__ g,
-                                                        const float* __restrict__ b, float* __restrict__ y,
+                                                        const float* __restrict__ b, void* __restrict__ yv,
                                                         float* __restrict__ mean_out, float* __restrict__ rstd_out,
                                                         int64_t rows, int d, float eps) {
   const int lane = threadIdx.x & 63;
@@ -167,7 +169,6 @@ __global__ __launch_bounds__(256) void ln_fwd_v4_kernel(const float* __restrict_
     q += (a0 * a0 + a1 * a1) + (a2 * a2 + a3 * a3);
   }
   const float rs = rsqrtf(wave_sum(q) / d + eps);
-  float* yr = y + row * d;
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     const int c = 4 * lane + 256 * i;
@@ -176,7 +177,11 @@ __global__ __launch_bounds__(256) void ln_fwd_v4_kernel(const float* __restrict_
     o.y = (v[i].y - mu) * rs * gv[i].y + bv[i].y;
     o.z = (v[i].z - mu) * rs * gv[i].z + bv[i].z;
     o.w = (v[i].w - mu) * rs * gv[i].w + bv[i].w;
-    *reinterpret_cast<float4*>(yr + c) = o;
+    if constexpr (BF)
+      *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(yv) + row * d + c) =
+          make_uint2(pack_bf16x2(o.x, o.y), pack_bf16x2(o.z, o.w));
+    else
+      *reinterpret_cast<float4*>(reinterpret_cast<float*>(yv) + row * d + c) = o;
   }
   if (lane == 0) {
     mean_out[row] = mu;
@@ -366,7 +371,7 @@ int ln_fwd_launch(const float* x, const float* gamma, const float* beta, float* 
                   int64_t rows, int64_t d, float eps, hipStream_t st) {
   const dim3 grid((unsigned)ceil_div(rows, 4)), blk(256);
   if (ln_v4_ok(d, {x, gamma, beta, y})) {
-#define LNF4(NV) hipLaunchKernelGGL(ln_fwd_v4_kernel<NV>, grid, blk, 0, st, x, gamma, beta, y, mean, rstd, rows, (int)d, eps)
+#define LNF4(NV) hipLaunchKernelGGL((ln_fwd_v4_kernel<NV, false>), grid, blk, 0, st, x, gamma, beta, (void*)y, mean, rstd, rows, (int)d, eps)
     if (d == 256) LNF4(1);
     else if (d == 512) LNF4(2);
     else if (d == 768) LNF4(3);
@@ -398,6 +403,23 @@ int kdfm_layernorm_fwd(const float* x, const float* gamma, const float* beta, fl
   KDFM_REQUIRE(d > 0 && d <= 64 * MAXV, "d must be in (0, 1024]");
   if (rows == 0) return KDFM_OK;
   return ln_fwd_launch(x, gamma, beta, y, mean, rstd, rows, d, eps, as_stream(stream));
+}
+
+int kdfm_layernorm_fwd_bf16(const float* x, const float* gamma, const float* beta, uint16_t* y, float* mean,
+                            float* rstd, int64_t rows, int64_t d, float eps, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(x && gamma && beta && y && mean && rstd, "null pointer");
+  KDFM_REQUIRE(ln_v4_ok(d, {x, gamma, beta, y}), "d % 256 == 0, d <= 1024, 16-byte aligned rows");
+  if (rows == 0) return KDFM_OK;
+  const dim3 grid((unsigned)ceil_div(rows, 4)), blk(256);
+  hipStream_t st = as_stream(stream);
+#define LNF4B(NV) hipLaunchKernelGGL((ln_fwd_v4_kernel<NV, true>), grid, blk, 0, st, x, gamma, beta, (void*)y, mean, rstd, rows, (int)d, eps)
+  if (d == 256) LNF4B(1);
+  else if (d == 512) LNF4B(2);
+  else if (d == 768) LNF4B(3);
+  else LNF4B(4);
+#undef LNF4B
+  return check_launch("kdfm_layernorm_fwd_bf16");
 }
 
 int64_t kdfm_layernorm_bwd_ws(int64_t rows, int64_t d) { return kdfm::ceil_div(rows, 4 * kdfm::LN_RPW) * 2 * d; }

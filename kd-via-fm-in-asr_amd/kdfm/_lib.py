@@ -185,6 +185,7 @@ SIGNATURES: dict[str, tuple] = {
     "kdfm_ctc_greedy": (_i32, [P, _i64, P, P, P, P, _i64, _i64, _i64, _i64, _i32, P]),
     "kdfm_edit_distance": (_i64, [P, _i64, P, _i64]),
     "kdfm_layernorm_fwd": (_i32, [P, P, P, P, P, P, _i64, _i64, _f32, P]),
+    "kdfm_layernorm_fwd_bf16": (_i32, [P, P, P, P, P, P, _i64, _i64, _f32, P]),
     "kdfm_layernorm_bwd": (_i32, [P, P, P, P, P, P, P, P, P, P, _i64, _i64, P]),
     "kdfm_layernorm_bwd_ws": (_i64, [_i64, _i64]),
     "kdfm_layernorm_bwd_part": (_i32, [P, P, P, P, P, P, P, P, _i64, _i64, P]),

@@ -395,9 +395,11 @@ def subsampling_backward(cfg, S: EncoderShapes, P, G, pre, ctx, dx, len1, *, see
 # One ConformerLayer
 # ------------------------------------------------------------------------------------------------
 
-def _ln(x, P, name, eps, dev, save_stats=True):
+def _ln(x, P, name, eps, dev, save_stats=True, bf16=False):
+    """bf16: the LN output in bf16 -- for an output whose every consumer is a large-tile product (_ln_bf16), which
+    reads bf16 operands: the same bits its cast of an f32 output gave, half the write and no cast per read."""
     rows, d = x.shape
-    y = _empty(rows, d, dev=dev)
+    y = torch.empty(rows, d, device=dev, dtype=torch.bfloat16) if bf16 else _empty(rows, d, dev=dev)
     m = _empty(rows, dev=dev)
     r = _empty(rows, dev=dev)
     K.layernorm_fwd(x, P[name + ".weight"], P[name + ".bias"], y, m, r, eps)
@@ -456,7 +458,7 @@ def _ffn_forward(cfg, P, L, which, norm, x, pd, seed, salt, li, site_act, site_o
                   st_act=_stream(salt, li, site_act), st_out=_stream(salt, li, site_out), out_ln=oln)
         keep(**{"m" + tag: m, "r" + tag: r, "ffn_img" + tag: img})
         return out, out_ln is not None
-    ln, m, r = _ln(x, P, norm, cfg.ln_eps, dev)
+    ln, m, r = _ln(x, P, norm, cfg.ln_eps, dev, bf16=_ln_bf16(rows, d, ff, save))
     h = _empty(rows, ff, dev=dev) if save else None
     # the hidden activation in bf16 when its producer and every consumer take the large-tile route (d_model >= 512):
     # the values those products read are bf16-rounded anyway, so this halves its write and skips a cast per read
@@ -474,6 +476,13 @@ def _ffn_forward(cfg, P, L, which, norm, x, pd, seed, salt, li, site_act, site_o
 def _big_all(*shapes):
     """Every (M, N, K, layout) product takes the large-tile bf16 route (kernels.big_ok)."""
     return all(K.big_ok(*sh) for sh in shapes)
+
+
+def _ln_bf16(rows, d, n, save):
+    """The LN output feeding a (d -> n) projection can be bf16: the projection (and, training, its weight gradient)
+    take the large-tile route, and the bf16 LN kernel applies."""
+    return K.layernorm_bf16_ok(d) and _big_all((rows, n, d, _lib.BIG_NT)) and (
+        not save or _big_all((n, d, rows, _lib.BIG_TN)))
 
 
 def _fwd3_ok(dk, save):
@@ -517,7 +526,7 @@ def layer_forward(cfg, S: EncoderShapes, P, L, li, x, out, pos_emb, lengths, *, 
                      K.lnproj_img(K.LNPROJ_QKV, P[L + "self_attn.qkv.weight"]), P[L + "self_attn.qkv.bias"],
                      P[L + "self_attn.pos_bias_u"], P[L + "self_attn.pos_bias_v"], qu, qv, qkv, m2, r2)
     else:
-        ln2, m2, r2 = _ln(x1, P, L + "norm_self_att", cfg.ln_eps, dev)
+        ln2, m2, r2 = _ln(x1, P, L + "norm_self_att", cfg.ln_eps, dev, bf16=_ln_bf16(rows, d, 3 * d, save))
         K.linear(ln2, P[L + "self_attn.qkv.weight"], P[L + "self_attn.qkv.bias"], qkv)
         K.qkv_prep(qkv, P[L + "self_attn.pos_bias_u"], P[L + "self_attn.pos_bias_v"], qu, qv)
     npos = 2 * T - 1
@@ -602,7 +611,7 @@ def layer_forward(cfg, S: EncoderShapes, P, L, li, x, out, pos_emb, lengths, *, 
                      K.lnproj_img(K.LNPROJ_GLU, P[L + "conv.pointwise_conv1.weight"].view(2 * d, d)),
                      P[L + "conv.pointwise_conv1.bias"], lengths, T, g, m3, r3)
     else:
-        ln3, m3, r3 = _ln(x2, P, L + "norm_conv", cfg.ln_eps, dev)
+        ln3, m3, r3 = _ln(x2, P, L + "norm_conv", cfg.ln_eps, dev, bf16=_ln_bf16(rows, d, 2 * d, save))
         a = _empty(rows, 2 * d, dev=dev)
         K.linear(ln3, P[L + "conv.pointwise_conv1.weight"].view(2 * d, d), P[L + "conv.pointwise_conv1.bias"], a)
         K.glu_mask_fwd(a, lengths, g, B, T, d)

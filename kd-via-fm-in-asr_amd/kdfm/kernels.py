@@ -1482,9 +1482,20 @@ def subsample_conv2_dgrad(dy2, wt, y1, dy1, B, T1, F1, Cc):
 # ------------------------------------------------------------------------------------------------
 
 def layernorm_fwd(x, g, b, y, mean, rstd, eps):
+    """y f32, or bf16 (d % 256 == 0: layernorm_bf16_ok) for an output only bf16-operand products read."""
     rows, d = x.shape
     assert x.is_contiguous() and y.is_contiguous() and mean.numel() == rows
+    if y.dtype == torch.bfloat16:
+        assert layernorm_bf16_ok(d)
+        call("kdfm_layernorm_fwd_bf16", ptr(x), ptr(g), ptr(b), y.data_ptr(), ptr(mean), ptr(rstd), rows, d,
+             float(eps), _s())
+        return
     call("kdfm_layernorm_fwd", ptr(x), ptr(g), ptr(b), ptr(y), ptr(mean), ptr(rstd), rows, d, float(eps), _s())
+
+
+def layernorm_bf16_ok(d) -> bool:
+    """kdfm_layernorm_fwd_bf16 takes this width (the 16-byte-lane kernel: d % 256 == 0, d <= 1024)."""
+    return d % 256 == 0 and d <= 1024
 
 
 def layernorm_bwd(dy, x, g, mean, rstd, dx, dg, db, dres=None):

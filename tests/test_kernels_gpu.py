@@ -44,6 +44,13 @@ def test_layernorm_bwd(rows, d):
     _close(dx, xr.grad + dres)
     _close(dg - 0.5, gr.grad)
     _close(db + 0.25, br.grad)
+    if K.layernorm_bf16_ok(d):   # the bf16-output forward: the same values rounded to nearest even
+        y16 = torch.empty(rows, d, device="cuda", dtype=torch.bfloat16)
+        m16, r16 = torch.empty_like(mean), torch.empty_like(rstd)
+        K.layernorm_fwd(x, gam, bet, y16, m16, r16, 1e-5)
+        torch.cuda.synchronize()
+        assert torch.equal(y16, y.bfloat16()), "bf16 LN output differs from the rounded f32 output"
+        assert torch.equal(m16, mean) and torch.equal(r16, rstd)
 
 
 @pytest.mark.parametrize("B,T,d,k", [(2, 26, 88, 31), (3, 401, 88, 31), (2, 130, 176, 31), (2, 70, 40, 15),
