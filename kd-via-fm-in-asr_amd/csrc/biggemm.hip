@@ -23,6 +23,8 @@
 // Deterministic: every output element has one writer and a fixed summation order (no split-K, no atomics).
 #include "gemm_common.h"
 
+#include <cstdlib>
+
 namespace kdfm {
 namespace {
 
@@ -700,40 +702,58 @@ __global__ __launch_bounds__(256) void mx_quant_kernel(const void* src, int bf, 
 // threads one MX block, 16 one stage row: each row's 128 output bytes and the 16 rows' 64 scale bytes (contiguous
 // in the stage-major layout) are written whole by the pass -- the 8-lanes-per-block kernel above wrote them in
 // 4-byte pieces and single scale bytes scattered over the stages
+__device__ __forceinline__ void mxr_load(const void* src, int bf, int64_t o, float (&v)[8]) {
+  if (bf) {
+    const uint4 w = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(src) + o);
+    const uint32_t u[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[2 * i] = __uint_as_float(u[i] << 16);
+      v[2 * i + 1] = __uint_as_float(u[i] & 0xFFFF0000u);
+    }
+  } else {
+    const float4 a = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(src) + o);
+    const float4 b = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(src) + o + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  }
+}
+
+// MXR_U tiles per loop iteration (their loads issued together), over a grid of at most a few workgroups per CU:
+// one tile per workgroup made the launch dispatch-bound (12 864 workgroups of 4 KB each at 6432 x 4096)
+constexpr int MXR_U = 4;
+
 __global__ __launch_bounds__(256) void mx_quant_rows_kernel(const void* src, int bf, int64_t rows, int64_t cols,
                                                             int64_t ld, uint8_t* dst, int64_t ldd, uint8_t* xs) {
   const int64_t nrt = (rows + 15) / 16, nt = nrt * (cols / 128);
   const int j = threadIdx.x & 15;
-  for (int64_t t = blockIdx.x; t < nt; t += gridDim.x) {
-    const int64_t s = t / nrt, r = (t - s * nrt) * 16 + (threadIdx.x >> 4);
-    const bool ok = r < rows;
-    const int64_t o = (ok ? r : 0) * ld + 128 * s + 8 * j;
-    float v[8];
-    if (bf) {
-      const uint4 w = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(src) + o);
-      const uint32_t u[4] = {w.x, w.y, w.z, w.w};
+  for (int64_t t0 = blockIdx.x; t0 < nt; t0 += (int64_t)MXR_U * gridDim.x) {
+    float v[MXR_U][8];
+    int64_t s[MXR_U], r[MXR_U];
+    bool ok[MXR_U];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        v[2 * i] = __uint_as_float(u[i] << 16);
-        v[2 * i + 1] = __uint_as_float(u[i] & 0xFFFF0000u);
-      }
-    } else {
-      const float4 a = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(src) + o);
-      const float4 b = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(src) + o + 4);
-      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+    for (int u = 0; u < MXR_U; ++u) {
+      const int64_t t = t0 + (int64_t)u * gridDim.x;
+      const int64_t tt = t < nt ? t : 0;
+      s[u] = tt / nrt;
+      r[u] = (tt - s[u] * nrt) * 16 + (threadIdx.x >> 4);
+      ok[u] = t < nt && r[u] < rows;
+      mxr_load(src, bf, (ok[u] ? r[u] : 0) * ld + 128 * s[u] + 8 * j, v[u]);
     }
-    float m = 0.f;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) m = fmaxf(m, fabsf(v[i]));
-    m = fmaxf(m, __shfl_xor(m, 1, 64));
-    m = fmaxf(m, __shfl_xor(m, 2, 64));
-    const int e = mx_exp(m);
-    if (ok) {
-      uint2 w;
-      w.x = mx_q4(v[0], v[1], v[2], v[3], e);
-      w.y = mx_q4(v[4], v[5], v[6], v[7], e);
-      *reinterpret_cast<uint2*>(dst + r * ldd + 128 * s + 8 * j) = w;
-      if ((j & 3) == 0) xs[(s * rows + r) * 4 + (j >> 2)] = (uint8_t)(e + 127);
+    for (int u = 0; u < MXR_U; ++u) {
+      float m = 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) m = fmaxf(m, fabsf(v[u][i]));
+      m = fmaxf(m, __shfl_xor(m, 1, 64));
+      m = fmaxf(m, __shfl_xor(m, 2, 64));
+      const int e = mx_exp(m);
+      if (ok[u]) {
+        uint2 w;
+        w.x = mx_q4(v[u][0], v[u][1], v[u][2], v[u][3], e);
+        w.y = mx_q4(v[u][4], v[u][5], v[u][6], v[u][7], e);
+        *reinterpret_cast<uint2*>(dst + r[u] * ldd + 128 * s[u] + 8 * j) = w;
+        if ((j & 3) == 0) xs[(s[u] * rows + r[u]) * 4 + (j >> 2)] = (uint8_t)(e + 127);
+      }
     }
   }
 }
@@ -873,7 +893,9 @@ int kdfm_fp8_quant_mx(const void* src, int src_bf16, int64_t rows, int64_t cols,
                        src_bf16, rows, cols, ld, dst, ldd, scales);
   } else if (((((uintptr_t)src) & 15) == 0) && ld % (src_bf16 ? 8 : 4) == 0) {
     const int64_t tiles = ceil_div(rows, 16) * (cols / 128);
-    hipLaunchKernelGGL(mx_quant_rows_kernel, dim3((unsigned)(tiles < 16384 ? tiles : 16384)), dim3(256), 0, st, src,
+    static const int64_t cap = [] { const char* e = getenv("KDFM_MXQ_GRID"); return e ? atoll(e) : 2048LL; }();
+    const int64_t g = ceil_div(tiles, MXR_U);
+    hipLaunchKernelGGL(mx_quant_rows_kernel, dim3((unsigned)(g < cap ? g : cap)), dim3(256), 0, st, src,
                        src_bf16, rows, cols, ld, dst, ldd, scales);
   } else {
     const int64_t blocks = ceil_div(rows * (cols / 32), 32);
