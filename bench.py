@@ -36,6 +36,10 @@ MI355X_HBM_GBPS = 8000.0            # MI355X_MICROARCH.md §HBM (8 TB/s spec pea
 # PMC traffic per kernel (tools/pmc_traffic.sh -> tools/pmc_summary.py: separate --pmc FETCH_SIZE and
 # WRITE_SIZE passes, FETCH_SIZE doubled per the gfx950 correction), committed under profiles/
 PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r05_pmc_traffic.json")
+# the committed rocprofv3 kernel summary of this bench command (tools/prof_summary.py over a kernel trace, whole
+# steps): each family's kernel ms/step from it is printed beside the HIP-event timing (tools/roofline_check.py)
+KERNEL_SUMMARY = [os.path.join(ROOT, "profiles", "r06", n) for n in ("final_kernel_summary.txt",
+                                                                        "close1_kernel_summary.txt")]
 # kdfm_gemm kernel family (kernels.ROUTES) -> kernel-name stems in the rocprofv3 / PMC summaries
 ROUTE_KERNELS = {"generic": ("gemm_kernel",), "skinny": ("sk_fwd_kernel", "skd_fwd_kernel"),
                  "rowstream_fwd": ("rs_fwd_kernel",), "wide_wgrad": ("rs_wgrad_kernel", "rs_fold_kernel"),
@@ -74,6 +78,35 @@ def pmc_traffic(stems):
     hit = [r for r in rows if any(name(r).endswith(st) for st in stems)]
     n = sum(r["launches"] for r in hit if _is_call_kernel(name(r)))
     return round(sum(r["bytes_total"] for r in hit) / n, 1) if n else None
+
+
+def _summary_path():
+    return next((pth for pth in KERNEL_SUMMARY if os.path.exists(pth)), None)
+
+
+def profile_ms(stems):
+    """A family's kernel ms/step in the committed kernel summary (None if absent): its lines
+    '<ms> ms/step <n>/step avg <us> us <kernel name>' whose kernel base name is one of `stems`."""
+    pth = _summary_path()
+    if pth is None:
+        return None
+    tot, hit = 0.0, False
+    with open(pth) as fh:
+        for ln in fh:
+            parts = ln.split()
+            if len(parts) < 7 or parts[1] != "ms/step":
+                continue
+            name = " ".join(parts[6:]).replace("void ", "").split("<")[0].split("(")[0].strip()
+            if name.split("::")[-1] in stems:
+                tot += float(parts[0])
+                hit = True
+    return round(tot, 3) if hit else None
+
+
+def _family_stems(fam):
+    if fam == "wgrad_rows":
+        return tuple(set(ROUTE_KERNELS["wgrad_rows"]) | set(FAMILY_KERNELS["wgrad_bf16"]))
+    return FAMILY_KERNELS.get(fam) or ROUTE_KERNELS.get(fam, (fam,))
 
 
 def parse():
@@ -433,7 +466,8 @@ def main():
             by_route[r] = {"launches": n, "ms_per_step": round(t["ms_total"], 3), "avg_ms": round(ms, 5),
                            "GB_per_s": round(gbps, 1), "TFLOP_per_s": round(tfl, 2),
                            "bytes_per_launch": round(t["bytes_total"] / n, 1),
-                           "flops_per_launch": round(t["flops_total"] / n, 1)}
+                           "flops_per_launch": round(t["flops_total"] / n, 1),
+                           "profile_ms_per_step": profile_ms(_family_stems(r))}
         dom = next(iter(by_route)) if by_route else "generic"
         dt = routes.get(dom, empty)
         n, ms, gbps, tfl = rate(dt)
@@ -452,6 +486,9 @@ def main():
                      "kernel": f"{dom} family ({', '.join(stems)}): the kernel family with the largest aggregated "
                                f"time of the step (kdfm_gemm routes + the fused kernels, HIP events on their streams)",
                      "timing_source": trace_issue,
+                     "profile_ms_per_step": profile_ms(_family_stems(dom)),
+                     "profile_source": (os.path.relpath(_summary_path(), ROOT) + " (rocprofv3 --kernel-trace of this "
+                                        "bench command, whole steps; tools/roofline_check.py)") if _summary_path() else None,
                      "launches": n, "avg_ms": round(ms, 5), "bytes_per_launch": round(dt["bytes_total"] / n, 1),
                      "flops_per_launch": round(dt["flops_total"] / n, 1),
                      "arith_intensity_flop_per_byte": round(intensity, 2)})
