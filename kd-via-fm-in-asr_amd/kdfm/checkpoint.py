@@ -128,6 +128,7 @@ def load_engine_state(eng, sd: dict, *, strict: bool = False, fb_atol: float = 1
     if strict and (missing or unexpected):
         raise KeyError(f"state dict mismatch: missing {missing[:8]}..., unexpected {unexpected[:8]}...")
     for st in (eng.student, eng.teacher):   # bf16 weight twins (opt-in direct-B GEMM path)
+        st.version += 1                     # the frozen teacher's large-tile copies (kernels.register_frozen)
         if st.data.is_cuda:
             st.refresh_bf16()
     return {"missing": missing, "unexpected": unexpected, "frontend_mismatch": fe_bad}

@@ -81,6 +81,7 @@ class Ver5Engine:
         dev = self.device
         self.student = FlatStore(student_specs(cfg), dev, with_grad=True, with_adam=True)
         self.teacher = FlatStore(teacher_specs(cfg), dev, with_grad=False)
+        K.register_frozen(self.teacher.data, self.teacher)   # the frozen teacher's large-tile weight copies persist
         # used but never-trained student-side parameters: DiffKD's encoder (its output is detached
         # before every use, asr_train_diffm.py:382-383, so AdamW never touches it)
         self.fixed = FlatStore(diffkd_specs(cfg, False) if cfg.use_diffkd else [], dev, with_grad=False)

@@ -228,10 +228,44 @@ class weight_epoch:
         _State.fp8_epoch = self._saved
 
 
+_FROZEN = []   # (first byte, end byte, weakref to the owner with .version, token): frozen parameter buffers
+_FROZEN_TOKENS = [0]
+
+
+def register_frozen(buf, owner) -> None:
+    """Declare `buf`'s parameters frozen (the distillation teacher): the large-tile route's bf16 / MX copies of its
+    weight views are made once and reused across engine calls until `owner.version` changes (FlatStore.load bumps
+    it).  A step plan recorded after the copies exist replays no conversion for them: reload the teacher before
+    recording plans.  Each registration has its own token, so a later buffer at the same address never matches an
+    earlier one's copies; dead owners' entries (and their copies) are dropped here."""
+    import weakref
+    dead = [f for f in _FROZEN if f[2]() is None]
+    for lo, hi, _, _ in dead:
+        for cache in (_BF16_W, _FP8_W):
+            for k in [k for k in cache if lo <= k[0] < hi]:
+                del cache[k]
+    lo = buf.data_ptr()
+    _FROZEN[:] = [f for f in _FROZEN if f[2]() is not None and f[0] != lo]
+    _FROZEN_TOKENS[0] += 1
+    _FROZEN.append((lo, lo + buf.numel() * buf.element_size(), weakref.ref(owner), _FROZEN_TOKENS[0]))
+
+
+def _epoch_of(W):
+    """The cache tag a weight view's converted copy is valid for: the owner's version for a frozen buffer, else
+    the current engine-call epoch (None outside one: convert per use)."""
+    p = W.data_ptr()
+    for lo, hi, ref, tok in _FROZEN:
+        if lo <= p < hi:
+            owner = ref()
+            if owner is not None:
+                return ("frozen", tok, owner.version)
+    return _State.fp8_epoch
+
+
 def _bf16_weight(W):
     """The large-tile route's bf16 copy of a weight view for this epoch (cast on first use), or None outside an
-    epoch; persistent storage (a recorded plan replays the cast into it)."""
-    ep = _State.fp8_epoch
+    epoch; persistent storage (a recorded plan replays the cast into it).  Frozen weights: once per version."""
+    ep = _epoch_of(W)
     if ep is None or W.dtype != torch.float32:
         return None
     key = (W.data_ptr(), W.shape[0], W.shape[1], W.stride(0))
@@ -247,8 +281,9 @@ def _bf16_weight(W):
 
 def _fp8_weight(W, tr):
     """The MX copy of a weight view for this epoch (quantised on first use; kdfm_fp8_quant_mx), or None outside an
-    epoch.  The copies are persistent (a recorded step plan replays the quantisation launch into the same storage)."""
-    ep = _State.fp8_epoch
+    epoch.  The copies are persistent (a recorded step plan replays the quantisation launch into the same storage).
+    Frozen weights (register_frozen): once per version."""
+    ep = _epoch_of(W)
     if ep is None:
         return None
     key = (W.data_ptr(), W.shape[0], W.shape[1], W.stride(0), bool(tr))

@@ -44,6 +44,8 @@ class FlatStore:
         off = -(-off // GROUP_ALIGN) * GROUP_ALIGN
         self.numel = off
         self.data = torch.zeros(self.numel, device=self.device, dtype=torch.float32)
+        # bumped by load(): a frozen store's derived weight copies (kernels.register_frozen) are rebuilt after it
+        self.version = 0
         self.grad = torch.zeros(self.numel, device=self.device, dtype=torch.float32) if with_grad else None
         self.exp_avg = torch.zeros_like(self.data) if with_adam else None
         self.exp_avg_sq = torch.zeros_like(self.data) if with_adam else None
@@ -120,6 +122,7 @@ class FlatStore:
             if tuple(t.shape) != tuple(shape):
                 raise ValueError(f"{name}: shape {tuple(t.shape)} != {tuple(shape)}")
             self.P[name].copy_(t.detach().to(torch.float32))
+        self.version += 1
         if strict and missing:
             raise KeyError(f"missing parameters: {missing[:5]}{'...' if len(missing) > 5 else ''}")
 

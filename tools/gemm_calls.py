@@ -34,7 +34,15 @@ log = []
 orig = K.call
 
 
+CASTS = {}
+
+
 def call(name, *args):
+    if name in ("kdfm_cast_bf16_2d", "kdfm_fp8_quant_mx"):
+        fr = [f"{os.path.basename(f.filename)}:{f.lineno}:{f.name}" for f in traceback.extract_stack()[-7:-2]]
+        rows, cols = (args[4], args[5]) if name == "kdfm_cast_bf16_2d" else (args[2], args[3])
+        key = f"{name} {rows}x{cols} " + " < ".join(reversed(fr))
+        CASTS[key] = CASTS.get(key, 0) + 1
     if name == "kdfm_gemm":
         d = K._GEMM_DESC.contents
         s = args[-1]
@@ -52,6 +60,7 @@ K.call = call
 eng.train_step(wav, wl, tg, tl, None)
 torch.cuda.synchronize()
 K.call = orig
+log += [f"{n:5d} x {k}" for k, n in sorted(CASTS.items(), key=lambda kv: -kv[1])]
 txt = "\n".join(log)
 out = sys.argv[1] if len(sys.argv) > 1 else None
 if out:
