@@ -32,8 +32,20 @@ from .overlap import WGRAD
 _PRIO = __import__("os").environ.get("KDFM_STREAM_PRIO", "0") == "1"
 
 
-def _crit_stream(dev):
-    return torch.cuda.Stream(dev, priority=-1) if _PRIO else torch.cuda.Stream(dev)
+# One stream per (device, role), shared by every engine of the process: torch hands out pool streams round-robin
+# and HIP maps streams onto the GPU_MAX_HW_QUEUES = 4 hardware queues in creation order, so a second engine's
+# fresh streams could share a queue with the weight-gradient stream (module-level, made once) and serialise
+# behind it -- measured: the same XL step 81.5 ms on a process's first engine, 91 ms on its second
+# (tools/xl_cmp.py, profiles/r06/xl_cmp_*.log).  Engines of one process run one after the other.
+_STREAMS = {}
+
+
+def _crit_stream(dev, role):
+    key = (str(torch.device(dev)), role)
+    s = _STREAMS.get(key)
+    if s is None:
+        s = _STREAMS[key] = torch.cuda.Stream(dev, priority=-1) if _PRIO else torch.cuda.Stream(dev)
+    return s
 from .store import FlatStore, init_uniform
 
 SALT_STUDENT, SALT_TEACHER, SALT_FRONT = 1, 2, 3
@@ -115,7 +127,7 @@ class Ver5Engine:
         # the step runs on a created (non-null) stream: ROCm makes the legacy null stream wait for a
         # HIP graph replayed on any other stream (tools/graph_probe.py), which serialised the whole-step
         # graph's branches behind the main stream
-        self.compute_stream = _crit_stream(dev) if dev.type == "cuda" else None
+        self.compute_stream = _crit_stream(dev, "compute") if dev.type == "cuda" else None
         self._link_in, self._link_out = K.StreamLink(), K.StreamLink()   # caller <-> compute stream
         # weight gradients on the side stream (the benchmark's schedule) or in line: None follows the
         # config (in line exactly when deterministic); the overlapped-vs-serialised determinism test
@@ -180,7 +192,7 @@ class Ver5Engine:
 
     def _side_stream(self):
         if getattr(self, "_side", None) is None:
-            self._side = _crit_stream(self.device)
+            self._side = _crit_stream(self.device, "side")
         return self._side
 
     def _teacher_forward(self, mel_t, mel_len, len1, len2, tfeats, tlogits, St, T):
@@ -442,7 +454,7 @@ class Ver5Engine:
         share a queue (a shared queue serialises its streams).  KDFM_AUX_STREAM=1: a stream of its own."""
         if getattr(self, "_aux", None) is None:
             own = __import__("os").environ.get("KDFM_AUX_STREAM", "0") == "1"
-            self._aux = _crit_stream(self.device) if own else self._side_stream()
+            self._aux = _crit_stream(self.device, "aux") if own else self._side_stream()
         return self._aux
 
     def _serial(self):
