@@ -35,7 +35,7 @@ MI355X_F32_MFMA_TFLOPS = 157.3
 MI355X_HBM_GBPS = 8000.0            # MI355X_MICROARCH.md §HBM (8 TB/s spec peak)
 # PMC traffic per kernel (tools/pmc_traffic.sh -> tools/pmc_summary.py: separate --pmc FETCH_SIZE and
 # WRITE_SIZE passes, FETCH_SIZE doubled per the gfx950 correction), committed under profiles/
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r05_pmc_traffic.json")
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r06_pmc_traffic.json")
 # the committed rocprofv3 kernel summary of this bench command (tools/prof_summary.py over a kernel trace, whole
 # steps): each family's kernel ms/step from it is printed beside the HIP-event timing (tools/roofline_check.py)
 KERNEL_SUMMARY = [os.path.join(ROOT, "profiles", "r06", n) for n in ("final_kernel_summary.txt",
