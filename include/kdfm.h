@@ -780,6 +780,10 @@ int kdfm_glu_mask_fwd(const float* a, const int64_t* lengths, float* g, int64_t 
                       void* stream);
 int kdfm_glu_mask_bwd(const float* dg, const float* a, const int64_t* lengths, float* da, int64_t B, int64_t T,
                       int64_t d, void* stream);
+/* The same with da rounded to bf16 (round to nearest even) for an operand only bf16-operand products read (the
+ * large-tile GEMM's data and weight gradients of pointwise_conv1, FastConformer(-XL)). */
+int kdfm_glu_mask_bwd_bf16(const float* dg, const float* a, const int64_t* lengths, uint16_t* da, int64_t B,
+                           int64_t T, int64_t d, void* stream);
 int kdfm_dwconv_fwd(const float* g, const float* w, const float* bias, float* y, double* stats, int64_t B, int64_t T,
                     int64_t d, int64_t K, void* stream);
 /* dg = conv^T(dy); dw, db accumulate (+=) */
@@ -815,6 +819,9 @@ int kdfm_bn_finalize_running(double* stats, float* running_mean, float* running_
                              int64_t d, int64_t count, float eps, float momentum, void* stream);
 int kdfm_bn_silu_fwd(const float* y, const float* mean, const float* rstd, const float* gamma, const float* beta,
                      float* z, int64_t rows, int64_t d, void* stream);
+/* z rounded to bf16 (the large-tile pointwise_conv2 and its weight gradient read bf16 operands). */
+int kdfm_bn_silu_fwd_bf16(const float* y, const float* mean, const float* rstd, const float* gamma, const float* beta,
+                          uint16_t* z, int64_t rows, int64_t d, void* stream);
 int kdfm_bn_silu_bwd(const float* dz, const float* y, const float* mean, const float* rstd, const float* gamma,
                      const float* beta, double* red_ws, float* dy, float* dgamma, float* dbeta, int64_t rows,
                      int64_t d, int32_t batch_stats, void* stream);
@@ -862,6 +869,10 @@ int kdfm_axpby(const float* a, int64_t lda, const float* b, int64_t ldb, float* 
                int64_t cols, float alpha, float beta, void* stream);
 int kdfm_dropout(const float* x, float* out, int64_t n, float p, float scale, const uint64_t* seed,
                  uint64_t rng_stream, void* stream);
+/* The same with out rounded to bf16 (the residual-branch dropout gradients the large-tile data and weight gradients
+ * read: one bf16 operand instead of an f32 tensor cast per consumer). */
+int kdfm_dropout_bf16(const float* x, uint16_t* out, int64_t n, float p, float scale, const uint64_t* seed,
+                      uint64_t rng_stream, void* stream);
 /* out[r,c] = alpha * x[r,c] * s[r / rows_per_s]  (s: device scalars, e.g. upstream loss grads) */
 int kdfm_rowscale(const float* x, float* out, int64_t rows, int64_t cols, const float* s, int64_t rows_per_s,
                   float alpha, void* stream);

@@ -28,8 +28,9 @@ __global__ __launch_bounds__(256) void glu_mask_fwd_kernel(const float* __restri
   g[idx] = v;
 }
 
+template <typename O>   // uint16_t: da rounded to bf16 (kdfm_glu_mask_bwd_bf16)
 __global__ __launch_bounds__(256) void glu_mask_bwd_kernel(const float* __restrict__ dg, const float* __restrict__ a,
-                                                           const int64_t* __restrict__ lens, float* __restrict__ da,
+                                                           const int64_t* __restrict__ lens, O* __restrict__ da,
                                                            int64_t rows, int64_t T, int64_t d) {
   const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (idx >= rows * d) return;
@@ -43,8 +44,13 @@ __global__ __launch_bounds__(256) void glu_mask_bwd_kernel(const float* __restri
     dx = gg * s;
     dyv = gg * x * s * (1.f - s);
   }
-  da[r * 2 * d + c] = dx;
-  da[r * 2 * d + d + c] = dyv;
+  if constexpr (sizeof(O) == 2) {
+    da[r * 2 * d + c] = f2bf(dx);
+    da[r * 2 * d + d + c] = f2bf(dyv);
+  } else {
+    da[r * 2 * d + c] = dx;
+    da[r * 2 * d + d + c] = dyv;
+  }
 }
 
 // Frame x channel tile staging shared by the depthwise-conv kernels: rows [t0 - pad, t0 + rows - pad)
@@ -241,15 +247,19 @@ __global__ __launch_bounds__(256) void bn_running_kernel(float* __restrict__ rm,
 }
 
 // z = silu(gamma * (y - mean) * rstd + beta)
+template <typename O>   // uint16_t: z rounded to bf16 (kdfm_bn_silu_fwd_bf16)
 __global__ __launch_bounds__(256) void bn_silu_fwd_kernel(const float* __restrict__ y, const float* __restrict__ mean,
                                                           const float* __restrict__ rstd, const float* __restrict__ gm,
-                                                          const float* __restrict__ bt, float* __restrict__ z,
+                                                          const float* __restrict__ bt, O* __restrict__ z,
                                                           int64_t n, int64_t d) {
   const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (idx >= n) return;
   const int64_t c = idx % d;
   const float pre = gm[c] * (y[idx] - mean[c]) * rstd[c] + bt[c];
-  z[idx] = siluf_(pre);
+  if constexpr (sizeof(O) == 2)
+    z[idx] = f2bf(siluf_(pre));
+  else
+    z[idx] = siluf_(pre);
 }
 
 // red[c] += sum dyb ; red[d+c] += sum dyb * xhat, with dyb = dz * silu'(pre)
@@ -533,9 +543,20 @@ int kdfm_glu_mask_bwd(const float* dg, const float* a, const int64_t* lengths, f
   KDFM_REQUIRE(dg && a && da, "null pointer");
   const int64_t n = B * T * d;
   if (n == 0) return KDFM_OK;
-  hipLaunchKernelGGL(glu_mask_bwd_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, as_stream(stream), dg, a,
-                     lengths, da, B * T, T, d);
+  hipLaunchKernelGGL(glu_mask_bwd_kernel<float>, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, as_stream(stream), dg,
+                     a, lengths, da, B * T, T, d);
   return check_launch("kdfm_glu_mask_bwd");
+}
+
+int kdfm_glu_mask_bwd_bf16(const float* dg, const float* a, const int64_t* lengths, uint16_t* da, int64_t B,
+                           int64_t T, int64_t d, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(dg && a && da, "null pointer");
+  const int64_t n = B * T * d;
+  if (n == 0) return KDFM_OK;
+  hipLaunchKernelGGL(glu_mask_bwd_kernel<uint16_t>, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, as_stream(stream),
+                     dg, a, lengths, da, B * T, T, d);
+  return check_launch("kdfm_glu_mask_bwd_bf16");
 }
 
 
@@ -677,9 +698,20 @@ int kdfm_bn_silu_fwd(const float* y, const float* mean, const float* rstd, const
   KDFM_REQUIRE(y && mean && rstd && gamma && beta && z, "null pointer");
   const int64_t n = rows * d;
   if (n == 0) return KDFM_OK;
-  hipLaunchKernelGGL(bn_silu_fwd_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, as_stream(stream), y, mean,
-                     rstd, gamma, beta, z, n, d);
+  hipLaunchKernelGGL(bn_silu_fwd_kernel<float>, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, as_stream(stream), y,
+                     mean, rstd, gamma, beta, z, n, d);
   return check_launch("kdfm_bn_silu_fwd");
+}
+
+int kdfm_bn_silu_fwd_bf16(const float* y, const float* mean, const float* rstd, const float* gamma, const float* beta,
+                          uint16_t* z, int64_t rows, int64_t d, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(y && mean && rstd && gamma && beta && z, "null pointer");
+  const int64_t n = rows * d;
+  if (n == 0) return KDFM_OK;
+  hipLaunchKernelGGL(bn_silu_fwd_kernel<uint16_t>, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, as_stream(stream),
+                     y, mean, rstd, gamma, beta, z, n, d);
+  return check_launch("kdfm_bn_silu_fwd_bf16");
 }
 
 int kdfm_bn_silu_bwd2(const float* dz, const float* y, const float* mean, const float* rstd, const float* gamma,

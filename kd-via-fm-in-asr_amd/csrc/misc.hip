@@ -77,13 +77,18 @@ __global__ __launch_bounds__(256) void l1_kernel(const float* __restrict__ a, co
 }
 
 // out = scale * dropout(x) with the flat-index mask of the GEMM epilogue (idx = r*cols + c)
-__global__ __launch_bounds__(256) void dropout_kernel(const float* x, float* out, int64_t n, float p, float scale,
+// O = uint16_t: the result rounded to bf16 (kdfm_dropout_bf16: an operand only bf16-operand products read)
+template <typename O>
+__global__ __launch_bounds__(256) void dropout_kernel(const float* x, O* out, int64_t n, float p, float scale,
                                                       const uint64_t* seed_ptr, uint64_t st) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
   float v = x[i] * scale;
   if (p > 0.f) v = dropout_keep(load_seed(seed_ptr), st, (uint64_t)i, p) ? v / (1.f - p) : 0.f;
-  out[i] = v;
+  if constexpr (sizeof(O) == 2)
+    out[i] = f2bf(v);
+  else
+    out[i] = v;
 }
 
 // qu[r, j] = qkv[r, j] + u[j]; qv[r, j] = qkv[r, j] + v[j]   (j = h*dk + c over d columns)
@@ -390,8 +395,17 @@ int kdfm_dropout(const float* x, float* out, int64_t n, float p, float scale, co
   using namespace kdfm;
   KDFM_REQUIRE(x && out, "null pointer");
   KDFM_REQUIRE(p >= 0.f && p < 1.f && (p == 0.f || seed), "dropout p / seed");
-  KDFM_1D(dropout_kernel, n, x, out, n, p, scale, seed, rng_stream);
+  KDFM_1D(dropout_kernel<float>, n, x, out, n, p, scale, seed, rng_stream);
   return check_launch("kdfm_dropout");
+}
+
+int kdfm_dropout_bf16(const float* x, uint16_t* out, int64_t n, float p, float scale, const uint64_t* seed,
+                      uint64_t rng_stream, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(x && out, "null pointer");
+  KDFM_REQUIRE(p >= 0.f && p < 1.f && (p == 0.f || seed), "dropout p / seed");
+  KDFM_1D(dropout_kernel<uint16_t>, n, x, out, n, p, scale, seed, rng_stream);
+  return check_launch("kdfm_dropout_bf16");
 }
 
 int kdfm_rowscale(const float* x, float* out, int64_t rows, int64_t cols, const float* s, int64_t rows_per_s,

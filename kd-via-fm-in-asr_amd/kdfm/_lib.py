@@ -198,6 +198,7 @@ SIGNATURES: dict[str, tuple] = {
     "kdfm_relpos_table": (_i32, [P, _i64, _i64, P]),
     "kdfm_glu_mask_fwd": (_i32, [P, P, P, _i64, _i64, _i64, P]),
     "kdfm_glu_mask_bwd": (_i32, [P, P, P, P, _i64, _i64, _i64, P]),
+    "kdfm_glu_mask_bwd_bf16": (_i32, [P, P, P, P, _i64, _i64, _i64, P]),
     "kdfm_dwconv_fwd": (_i32, [P, P, P, P, P, _i64, _i64, _i64, _i64, P]),
     "kdfm_dwconv_bwd": (_i32, [P, P, P, P, P, P, P, _i64, _i64, _i64, _i64, P]),
     "kdfm_dwconv_bwd_fold": (_i32, [P, P, P, _i64, _i64, _i64, _i64, P]),
@@ -208,6 +209,7 @@ SIGNATURES: dict[str, tuple] = {
     "kdfm_bn_running_update": (_i32, [P, P, P, _i64, _i64, _f32, P]),
     "kdfm_bn_finalize_running": (_i32, [P, P, P, P, P, _i64, _i64, _f32, _f32, P]),
     "kdfm_bn_silu_fwd": (_i32, [P, P, P, P, P, P, _i64, _i64, P]),
+    "kdfm_bn_silu_fwd_bf16": (_i32, [P, P, P, P, P, P, _i64, _i64, P]),
     "kdfm_bn_silu_bwd": (_i32, [P, P, P, P, P, P, P, P, P, P, _i64, _i64, _i32, P]),
     "kdfm_bn_silu_bwd2": (_i32, [P, P, P, P, P, P, P, P, P, P, P, _i64, _i64, _i32, P]),
     "kdfm_log_softmax": (_i32, [P, P, _i64, _i64, _i64, _i64, P]),
@@ -228,6 +230,7 @@ SIGNATURES: dict[str, tuple] = {
     "kdfm_mse": (_i32, [P, P, P, P, _i64, _f32, _f32, P]),
     "kdfm_l1": (_i32, [P, P, P, P, _i64, _f32, _f32, P]),
     "kdfm_dropout": (_i32, [P, P, _i64, _f32, _f32, P, C.c_uint64, P]),
+    "kdfm_dropout_bf16": (_i32, [P, P, _i64, _f32, _f32, P, C.c_uint64, P]),
     "kdfm_convw_prep": (_i32, [P, P, P, _i64, _i64, _i64, P]),
     "kdfm_convw_grad": (_i32, [P, P, _i64, _i64, _i64, _f32, P]),
     "kdfm_subsample_lengths": (_i32, [P, P, P, P, _i64, _i64, P]),

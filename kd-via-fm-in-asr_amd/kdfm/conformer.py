@@ -478,6 +478,16 @@ def _big_all(*shapes):
     return all(K.big_ok(*sh) for sh in shapes)
 
 
+def _grad_bf16(rows, n_out, k_in):
+    """A Linear's output gradient (rows, n_out) can be produced in bf16: its data gradient (rows, k_in) and its
+    weight gradient (n_out, k_in) both take the large-tile route, which reads bf16 operands anyway."""
+    return _big_all((rows, k_in, n_out, _lib.BIG_NN), (n_out, k_in, rows, _lib.BIG_TN))
+
+
+def _bf16_or_f32(use_bf16, rows, cols, dev):
+    return torch.empty(rows, cols, device=dev, dtype=torch.bfloat16) if use_bf16 else _empty(rows, cols, dev=dev)
+
+
 def _ln_bf16(rows, d, n, save):
     """The LN output feeding a (d -> n) projection can be bf16: the projection (and, training, its weight gradient)
     take the large-tile route, and the bf16 LN kernel applies."""
@@ -645,7 +655,9 @@ def layer_forward(cfg, S: EncoderShapes, P, L, li, x, out, pos_emb, lengths, *, 
                   epi=K.RG_EPI_RESID, bias=P[L + "conv.pointwise_conv2.bias"], R=x2, rscale=1.0, p_out=pd,
                   st_out=_stream(salt, li, SITE_CONV_OUT), seed=seed)
     else:
-        z = _empty(rows, d, dev=dev)
+        # z in bf16 when pointwise_conv2 and its weight gradient take the large-tile route (they read bf16)
+        z = _bf16_or_f32(_big_all((rows, d, d, _lib.BIG_NT)) and (not save or _big_all((d, d, rows, _lib.BIG_TN))),
+                         rows, d, dev)
         K.bn_silu_fwd(y, bmean, brstd, P[L + "conv.batch_norm.weight"], P[L + "conv.batch_norm.bias"], z)
         K.linear(z, P[L + "conv.pointwise_conv2.weight"].view(d, d), P[L + "conv.pointwise_conv2.bias"], x3,
                  epi=_lib.EPI_RESID, R=x2, rscale=1.0, dropout_p=pd, seed=seed,
@@ -741,7 +753,7 @@ def _ffn_backward(P, G, L, which, dres_out, ctx, tag, x_in_ln, norm, pd, seed, s
         return dx
     ln, h, a = ctx["ln" + tag], ctx["h" + tag], ctx["a" + tag]
     ff = h.shape[1]
-    dlin2 = _empty(rows, d, dev=dev)
+    dlin2 = _bf16_or_f32(_grad_bf16(rows, d, ff), rows, d, dev)
     K.dropout(dres_out, dlin2, pd, 0.5, seed, _stream(salt, li, site_out))
     WGRAD.run(lambda: K.linear_dw(dlin2, a, G[L + which + ".linear2.weight"], db=G[L + which + ".linear2.bias"]), dlin2, a)
     # the hidden gradient in bf16 when its producer and both consumers take the large-tile route (as `a` above)
@@ -792,7 +804,7 @@ def layer_backward(cfg, S: EncoderShapes, P, G, L, li, ctx, dout, pos_emb, lengt
             WGRAD.run(lambda: K.wgrad_bf16(dpw2_h, ctx["z_h"], G[L + "conv.pointwise_conv2.weight"].view(d, d),
                                            db=G[L + "conv.pointwise_conv2.bias"]), dpw2_h, ctx["z_h"])
     else:
-        dpw2 = _empty(rows, d, dev=dev)
+        dpw2 = _bf16_or_f32(_grad_bf16(rows, d, d), rows, d, dev)
         K.dropout(dx3, dpw2, pd, 1.0, seed, _stream(salt, li, SITE_CONV_OUT))
         WGRAD.run(lambda: K.linear_dw(dpw2, ctx["z"], G[L + "conv.pointwise_conv2.weight"].view(d, d), db=G[L + "conv.pointwise_conv2.bias"]), dpw2, ctx["z"])
         K.linear_dx(dpw2, P[L + "conv.pointwise_conv2.weight"].view(d, d), dz)
@@ -840,7 +852,7 @@ def layer_backward(cfg, S: EncoderShapes, P, G, L, li, ctx, dout, pos_emb, lengt
         WGRAD.run(lambda: K.wgrad_bf16(da_h, ln3_h, G[L + "conv.pointwise_conv1.weight"].view(2 * d, d),
                                        db=G[L + "conv.pointwise_conv1.bias"]), da_h, ln3_h)
     else:
-        da = _empty(rows, 2 * d, dev=dev)
+        da = _bf16_or_f32(_grad_bf16(rows, 2 * d, d), rows, 2 * d, dev)
         K.glu_mask_bwd(dg, ctx["a"], lengths, da, B, T, d)
         del dg
         WGRAD.run(lambda: K.linear_dw(da, ctx["ln3"], G[L + "conv.pointwise_conv1.weight"].view(2 * d, d), db=G[L + "conv.pointwise_conv1.bias"]), da, ctx["ln3"])
@@ -865,7 +877,7 @@ def layer_backward(cfg, S: EncoderShapes, P, G, L, li, ctx, dout, pos_emb, lengt
             WGRAD.run(lambda: K.wgrad_bf16(dlo_h, ctx["o_h"], G[L + "self_attn.linear_out.weight"],
                                            db=G[L + "self_attn.linear_out.bias"]), dlo_h, ctx["o_h"])
     else:
-        dlo = _empty(rows, d, dev=dev)
+        dlo = _bf16_or_f32(_grad_bf16(rows, d, d), rows, d, dev)
         K.dropout(dx2, dlo, pd, 1.0, seed, _stream(salt, li, SITE_ATT_OUT))
         WGRAD.run(lambda: K.linear_dw(dlo, ctx["o"], G[L + "self_attn.linear_out.weight"], db=G[L + "self_attn.linear_out.bias"]), dlo, ctx["o"])
         K.linear_dx(dlo, P[L + "self_attn.linear_out.weight"], do)

@@ -634,11 +634,12 @@ class Ver5Engine:
     def train_step(self, wav, wav_len, targets, tgt_len, allreduce=None):
         """forward + backward + (all-reduce) + AdamW.  Returns the device loss vector."""
         self.advance_rng()
-        ctx = self.forward(wav, wav_len, targets, tgt_len, train=True)
         ready = getattr(allreduce, "ready", None)
         grad = self.student.grad
-        self.backward(ctx, grad_ready=(lambda o: ready(grad, o)) if ready is not None else None)
-        del ctx
+        with K.weight_epoch():   # one epoch for forward + backward: the large-tile route converts each weight once
+            ctx = self.forward(wav, wav_len, targets, tgt_len, train=True)
+            self.backward(ctx, grad_ready=(lambda o: ready(grad, o)) if ready is not None else None)
+            del ctx
         scale = 1.0
         if allreduce is not None:
             scale = self.allreduce_grads(allreduce)
@@ -663,9 +664,10 @@ class Ver5Engine:
 
         def step():
             self.advance_rng()
-            ctx = self.forward(wav, wav_len, targets, tgt_len, train=True)
-            self.backward(ctx, grad_ready=(lambda o: plan.host(ready, grad, o)) if ready is not None else None)
-            del ctx
+            with K.weight_epoch():
+                ctx = self.forward(wav, wav_len, targets, tgt_len, train=True)
+                self.backward(ctx, grad_ready=(lambda o: plan.host(ready, grad, o)) if ready is not None else None)
+                del ctx
             if allreduce is not None:
                 with K.region("allreduce"):
                     plan.host(finish)

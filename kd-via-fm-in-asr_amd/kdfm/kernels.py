@@ -219,9 +219,12 @@ class weight_epoch:
     copy; outside (the module API, tests, after an optimizer step) every product converts its weight itself."""
 
     def __enter__(self):
+        # nested inside an open epoch (the engine's train_step around its forward and backward): join it -- the
+        # weights cannot change before the outer one closes, so the backward reuses the forward's copies
         self._saved = _State.fp8_epoch
-        _EPOCHS[0] += 1
-        _State.fp8_epoch = _EPOCHS[0]
+        if self._saved is None:
+            _EPOCHS[0] += 1
+            _State.fp8_epoch = _EPOCHS[0]
         return self
 
     def __exit__(self, *a):
@@ -845,7 +848,12 @@ def l1(a, b, loss_acc, scale, grad=None, gscale=0.0):
 
 
 def dropout(x, out, p, scale, seed, rng_stream):
+    """out f32, or bf16 (rounded to nearest even: an operand only bf16-operand products read)."""
     assert x.is_contiguous() and out.is_contiguous() and x.numel() == out.numel()
+    if out.dtype == torch.bfloat16:
+        call("kdfm_dropout_bf16", ptr(x), out.data_ptr(), x.numel(), float(p), float(scale), ptr(seed),
+             int(rng_stream), _s())
+        return
     call("kdfm_dropout", ptr(x), ptr(out), x.numel(), float(p), float(scale), ptr(seed), int(rng_stream), _s())
 
 
@@ -1807,6 +1815,10 @@ def glu_mask_fwd(a, lengths, g, B, T, d):
 
 
 def glu_mask_bwd(dg, a, lengths, da, B, T, d):
+    """da f32, or bf16 (rounded to nearest even)."""
+    if da.dtype == torch.bfloat16:
+        call("kdfm_glu_mask_bwd_bf16", ptr(dg), ptr(a), ptr(_i64(lengths)), da.data_ptr(), B, T, d, _s())
+        return
     call("kdfm_glu_mask_bwd", ptr(dg), ptr(a), ptr(_i64(lengths)), ptr(da), B, T, d, _s())
 
 
@@ -1861,7 +1873,11 @@ def bn_finalize_running(stats, rm, rv, mean, rstd, d, count, eps, momentum):
 
 
 def bn_silu_fwd(y, mean, rstd, g, b, z):
+    """z f32, or bf16 (rounded to nearest even)."""
     rows, d = y.shape
+    if z.dtype == torch.bfloat16:
+        call("kdfm_bn_silu_fwd_bf16", ptr(y), ptr(mean), ptr(rstd), ptr(g), ptr(b), z.data_ptr(), rows, d, _s())
+        return
     call("kdfm_bn_silu_fwd", ptr(y), ptr(mean), ptr(rstd), ptr(g), ptr(b), ptr(z), rows, d, _s())
 
 
