@@ -601,8 +601,16 @@ def layer_forward(cfg, S: EncoderShapes, P, L, li, x, out, pos_emb, lengths, *, 
                   bias=P[L + "self_attn.linear_out.bias"], R=x1, rscale=1.0, p_out=pd,
                   st_out=_stream(salt, li, SITE_ATT_OUT), seed=seed)
     else:
-        K.linear(o, P[L + "self_attn.linear_out.weight"], P[L + "self_attn.linear_out.bias"], x2, epi=_lib.EPI_RESID,
+        o_in = o
+        if _big_all((rows, d, d, _lib.BIG_NT)) and save and _big_all((d, d, rows, _lib.BIG_TN)):
+            # linear_out and its weight gradient read bf16: one cast, kept for the backward (o itself stays f32 for
+            # the attention backward's row sums)
+            o_in = torch.empty(rows, d, device=dev, dtype=torch.bfloat16)
+            K.cast_bf16(o, o_in)
+            keep(o16=o_in)
+        K.linear(o_in, P[L + "self_attn.linear_out.weight"], P[L + "self_attn.linear_out.bias"], x2, epi=_lib.EPI_RESID,
                  R=x1, rscale=1.0, dropout_p=pd, seed=seed, rng_stream=_stream(salt, li, SITE_ATT_OUT))
+        del o_in
     fused_attn = _attn_fused_ok(dk, save) and _ATTN_BWD_FUSED
     keep(x1=x1, ln2=ln2, m2=m2, r2=r2, qkv=qkv, qu=qu, qv=qv, ppos=ppos, P=Pm, Pd=Pd, o=o, o_h=o_h, pa=pa,
          attn_fused=fused_attn, lse=lse if fused_attn else None, pt=pt if fused_attn else None,
@@ -879,7 +887,8 @@ def layer_backward(cfg, S: EncoderShapes, P, G, L, li, ctx, dout, pos_emb, lengt
     else:
         dlo = _bf16_or_f32(_grad_bf16(rows, d, d), rows, d, dev)
         K.dropout(dx2, dlo, pd, 1.0, seed, _stream(salt, li, SITE_ATT_OUT))
-        WGRAD.run(lambda: K.linear_dw(dlo, ctx["o"], G[L + "self_attn.linear_out.weight"], db=G[L + "self_attn.linear_out.bias"]), dlo, ctx["o"])
+        o_w = ctx.get("o16") if ctx.get("o16") is not None else ctx["o"]
+        WGRAD.run(lambda: K.linear_dw(dlo, o_w, G[L + "self_attn.linear_out.weight"], db=G[L + "self_attn.linear_out.bias"]), dlo, o_w)
         K.linear_dx(dlo, P[L + "self_attn.linear_out.weight"], do)
         del dlo
     qkv, Pm, Pd, qu, qv, ppos = ctx["qkv"], ctx["P"], ctx["Pd"], ctx["qu"], ctx["qv"], ctx["ppos"]
@@ -984,6 +993,11 @@ def _attn_bwd_tail(P, G, L, ctx, dqkv, dqu, dqv, dppos, pos_emb, dx2, lng, cfg, 
         K.colsum(dqv, G[L + "self_attn.pos_bias_v"].view(-1))
         K.axpby(dqu, dqv, dqkv[:, :d], 1.0, 1.0)
         del dqu, dqv
+        if _grad_bf16(rows, 3 * d, d):   # both consumers read bf16: one cast instead of one per consumer
+            dq16 = torch.empty(rows, 3 * d, device=dev, dtype=torch.bfloat16)
+            K.cast_bf16(dqkv, dq16)
+            dqkv = dq16
+            del dq16
         WGRAD.run(lambda: K.linear_dw(dqkv, ctx["ln2"], G[L + "self_attn.qkv.weight"], db=G[L + "self_attn.qkv.bias"]), dqkv, ctx["ln2"])
         dln2 = _empty(rows, d, dev=dev)
         K.linear_dx(dqkv, P[L + "self_attn.qkv.weight"], dln2)
