@@ -189,6 +189,11 @@ __global__ __launch_bounds__(256) void ln_fwd_v4_kernel(const float* __restrict_
   }
 }
 
+// rows per wave of the 16-byte-lane backward: one -- 6 432-row LayerNorms then run as 1 608 workgroups (4 rows
+// each) instead of 402 (1.6 waves per SIMD at 221 registers: latency-bound, 62 us in the XL step), at four times the
+// dgamma / dbeta partial rows (ln_rows_per_block)
+constexpr int LN_RPW_V4 = 1;
+
 template <int NV>
 __global__ __launch_bounds__(256) void ln_bwd_v4_kernel(const float* __restrict__ dy, const float* __restrict__ x,
                                                         const float* __restrict__ g, const float* __restrict__ mean,
@@ -196,7 +201,8 @@ __global__ __launch_bounds__(256) void ln_bwd_v4_kernel(const float* __restrict_
                                                         float* __restrict__ part, int64_t rows, int d,
                                                         const float* __restrict__ dy2) {
   __shared__ float red[2][4][256 * NV];
-  constexpr int RB = NV > 2 ? 2 : LN_RPW;   // rows whose values are held at once
+  constexpr int RPW = LN_RPW_V4;
+  constexpr int RB = RPW;   // rows whose values are held at once
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   float gl[NV][4], pg[NV][4], pb[NV][4];
 #pragma unroll
@@ -206,9 +212,9 @@ __global__ __launch_bounds__(256) void ln_bwd_v4_kernel(const float* __restrict_
 #pragma unroll
     for (int e = 0; e < 4; ++e) pg[i][e] = pb[i][e] = 0.f;
   }
-  const int64_t base = ((int64_t)blockIdx.x * 4 + w) * LN_RPW;
+  const int64_t base = ((int64_t)blockIdx.x * 4 + w) * RPW;
 #pragma unroll
-  for (int j0 = 0; j0 < LN_RPW; j0 += RB) {
+  for (int j0 = 0; j0 < RPW; j0 += RB) {
     float dyv[RB][NV][4], xv[RB][NV][4], rv[RB][NV][4], mu[RB], rs[RB];
 #pragma unroll
     for (int j = 0; j < RB; ++j) {
@@ -282,6 +288,12 @@ __host__ inline bool ln_v4_ok(int64_t d, std::initializer_list<const void*> ptrs
   return true;
 }
 
+// rows per dgamma / dbeta partial row of the backward (the workspace and the fold follow it): 4 waves x LN_RPW rows,
+// or 4 x LN_RPW_V4 on the 16-byte-lane path (d % 256 == 0, which then requires 16-byte aligned operands)
+__host__ inline int64_t ln_rows_per_block(int64_t d) {
+  return (d % 256 == 0 && d <= 1024) ? 4 * LN_RPW_V4 : 4 * LN_RPW;
+}
+
 // Ordered fold of LayerNorm partials for up to KDFM_LN_FOLD_MAX LayerNorms in one launch:
 // dgamma_e[c] += sum_b part_e[b][c], dbeta_e[c] += sum_b part_e[b][d + c].  grid = (column groups of
 // 64 over 2d, entries); lane = column, the 4 waves stride the partial rows, fixed-order combine
@@ -344,9 +356,10 @@ int ln_fold(const float* const* parts, float* const* dgs, float* const* dbs, int
 int ln_bwd_launch(const float* dy, const float* x, const float* gamma, const float* mean, const float* rstd,
                   const float* dres, float* dx, float* part, int64_t rows, int64_t d, hipStream_t st,
                   const float* dy2 = nullptr) {
-  const int64_t blocks = ceil_div(rows, 4 * LN_RPW);
+  const int64_t blocks = ceil_div(rows, ln_rows_per_block(d));
   const dim3 grid((unsigned)blocks), blk(256);
-  if (ln_v4_ok(d, {dy, x, gamma, dres, dx, dy2})) {
+  if (d % 256 == 0 && d <= 1024) {
+    KDFM_REQUIRE(ln_v4_ok(d, {dy, x, gamma, dres, dx, dy2}), "d % 256 == 0: 16-byte aligned operands");
 #define LNB4(NV) hipLaunchKernelGGL(ln_bwd_v4_kernel<NV>, grid, blk, 0, st, dy, x, gamma, mean, rstd, dres, dx, part, rows, (int)d, dy2)
     if (d == 256) LNB4(1);
     else if (d == 512) LNB4(2);
@@ -422,7 +435,7 @@ int kdfm_layernorm_fwd_bf16(const float* x, const float* gamma, const float* bet
   return check_launch("kdfm_layernorm_fwd_bf16");
 }
 
-int64_t kdfm_layernorm_bwd_ws(int64_t rows, int64_t d) { return kdfm::ceil_div(rows, 4 * kdfm::LN_RPW) * 2 * d; }
+int64_t kdfm_layernorm_bwd_ws(int64_t rows, int64_t d) { return kdfm::ceil_div(rows, kdfm::ln_rows_per_block(d)) * 2 * d; }
 
 int kdfm_layernorm_bwd(const float* dy, const float* x, const float* gamma, const float* mean, const float* rstd,
                        const float* dres, float* dx, float* dgamma, float* dbeta, float* ws, int64_t rows, int64_t d,
@@ -437,7 +450,7 @@ int kdfm_layernorm_bwd(const float* dy, const float* x, const float* gamma, cons
   const float* parts[1] = {ws};
   float* dgs[1] = {dgamma};
   float* dbs[1] = {dbeta};
-  return ln_fold(parts, dgs, dbs, 1, ceil_div(rows, 4 * LN_RPW), d, st);
+  return ln_fold(parts, dgs, dbs, 1, ceil_div(rows, ln_rows_per_block(d)), d, st);
 }
 
 int kdfm_layernorm_bwd_part(const float* dy, const float* x, const float* gamma, const float* mean,
@@ -466,7 +479,7 @@ int kdfm_ln_fold(const float* const* parts, float* const* dgamma, float* const* 
   KDFM_REQUIRE(parts && dgamma && dbeta && n >= 1 && n <= KDFM_LN_FOLD_MAX, "1..KDFM_LN_FOLD_MAX LayerNorms");
   for (int i = 0; i < n; ++i) KDFM_REQUIRE(parts[i] && dgamma[i] && dbeta[i], "null pointer");
   if (rows == 0) return KDFM_OK;
-  return ln_fold(parts, dgamma, dbeta, n, ceil_div(rows, 4 * LN_RPW), d, as_stream(stream));
+  return ln_fold(parts, dgamma, dbeta, n, ceil_div(rows, ln_rows_per_block(d)), d, as_stream(stream));
 }
 
 }  // extern "C"
