@@ -922,6 +922,12 @@ int kdfm_adamw_noam(float* params, const float* grads, float* exp_avg, float* ex
                     const int64_t* step, int64_t* adam_base, float base_lr, float d_model,
                     float warmup_steps, float min_lr, float beta1, float beta2, float eps, float weight_decay,
                     float grad_scale, float* lr_out, const float* gstats, void* stream);
+/* The same update also writing the new parameters as bf16 (round to nearest even) into params_bf16, a mirror of the
+ * flat buffer the large-tile GEMM reads its weight operands from (FastConformer(-XL): no per-weight cast per step). */
+int kdfm_adamw_noam_bf16(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, uint16_t* params_bf16,
+                         int64_t n, const int64_t* step, int64_t* adam_base, float base_lr, float d_model,
+                         float warmup_steps, float min_lr, float beta1, float beta2, float eps, float weight_decay,
+                         float grad_scale, float* lr_out, const float* gstats, void* stream);
 /* out2 = [sum_i (scale g_i)^2 over the finite entries, number of non-finite entries] of the flat gradient
  * buffer (the all-reduced sum with scale = 1/world: the global gradient norm^2 and the
  * skip flag of kdfm_adamw_noam); fixed-order two-stage reduction (deterministic).  ws: kdfm_grad_stats_ws

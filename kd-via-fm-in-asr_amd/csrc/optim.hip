@@ -26,13 +26,15 @@ __device__ __forceinline__ float noam_lr(int64_t k, float base, float d_model, f
   return (float)lr;
 }
 
+// p16 (nullable): the updated parameters also written as bf16 (round to nearest even) into a mirror of the flat
+// buffer -- the large-tile GEMM's weight operands (kdfm_adamw_noam_bf16), so no per-weight cast per step
 __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                     float* __restrict__ m, float* __restrict__ v, int64_t n,
                                                     const int64_t* __restrict__ step,
                                                     int64_t* __restrict__ adam_base, float base, float d_model,
                                                     float warmup, float min_lr, float b1, float b2, float eps, float wd,
                                                     float gscale, float* __restrict__ lr_out,
-                                                    const float* __restrict__ gstats) {
+                                                    const float* __restrict__ gstats, uint16_t* __restrict__ p16) {
   const int64_t k = step[0];
   const float lr = noam_lr(k, base, d_model, warmup, min_lr);
   if (lr_out && blockIdx.x == 0 && threadIdx.x == 0) lr_out[0] = lr;
@@ -57,7 +59,8 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const
   };
   const int64_t stride = (int64_t)gridDim.x * 256;
   // 16-byte lanes when the four buffers are aligned (the flat parameter buffer is): the same per-element update
-  const bool vec = ((((uintptr_t)p) | ((uintptr_t)g) | ((uintptr_t)m) | ((uintptr_t)v)) & 15) == 0;
+  const bool vec = ((((uintptr_t)p) | ((uintptr_t)g) | ((uintptr_t)m) | ((uintptr_t)v)) & 15) == 0 &&
+                   (((uintptr_t)p16) & 7) == 0;
   const int64_t n4 = vec ? n / 4 : 0;
   for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < n4; q += stride) {
     float4 pp = reinterpret_cast<float4*>(p)[q], mm = reinterpret_cast<float4*>(m)[q];
@@ -70,6 +73,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const
     reinterpret_cast<float4*>(m)[q] = mm;
     reinterpret_cast<float4*>(v)[q] = vv;
     reinterpret_cast<float4*>(p)[q] = pp;
+    if (p16) reinterpret_cast<uint2*>(p16)[q] = make_uint2(pack_bf16x2(pp.x, pp.y), pack_bf16x2(pp.z, pp.w));
   }
   for (int64_t i = 4 * n4 + (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
     float pi = p[i], mi = m[i], vi = v[i];
@@ -77,6 +81,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const
     m[i] = mi;
     v[i] = vi;
     p[i] = pi;
+    if (p16) p16[i] = f2bf(pi);
   }
 }
 
@@ -175,6 +180,22 @@ extern "C" int kdfm_adamw_noam(float* params, const float* grads, float* exp_avg
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(adamw_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), params, grads, exp_avg,
                      exp_avg_sq, n, step, adam_base, base_lr, d_model, warmup_steps, min_lr, beta1, beta2, eps, weight_decay,
-                     grad_scale, lr_out, gstats);
+                     grad_scale, lr_out, gstats, (uint16_t*)nullptr);
   return check_launch("kdfm_adamw_noam");
+}
+
+extern "C" int kdfm_adamw_noam_bf16(float* params, const float* grads, float* exp_avg, float* exp_avg_sq,
+                                    uint16_t* params_bf16, int64_t n, const int64_t* step, int64_t* adam_base,
+                                    float base_lr, float d_model, float warmup_steps, float min_lr, float beta1,
+                                    float beta2, float eps, float weight_decay, float grad_scale, float* lr_out,
+                                    const float* gstats, void* stream) {
+  using namespace kdfm;
+  KDFM_REQUIRE(params && grads && exp_avg && exp_avg_sq && step && params_bf16, "null pointer");
+  if (n == 0) return KDFM_OK;
+  int64_t blocks = ceil_div(n, 256);
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(adamw_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), params, grads, exp_avg,
+                     exp_avg_sq, n, step, adam_base, base_lr, d_model, warmup_steps, min_lr, beta1, beta2, eps, weight_decay,
+                     grad_scale, lr_out, gstats, params_bf16);
+  return check_launch("kdfm_adamw_noam_bf16");
 }

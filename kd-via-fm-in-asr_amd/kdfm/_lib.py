@@ -236,6 +236,8 @@ SIGNATURES: dict[str, tuple] = {
     "kdfm_subsample_lengths": (_i32, [P, P, P, P, _i64, _i64, P]),
     "kdfm_step_advance": (_i32, [P, P, P]),
     "kdfm_adamw_noam": (_i32, [P, P, P, P, _i64, P, P, _f32, _f32, _f32, _f32, _f32, _f32, _f32, _f32, _f32, P, P, P]),
+    "kdfm_adamw_noam_bf16": (_i32, [P, P, P, P, P, _i64, P, P, _f32, _f32, _f32, _f32, _f32, _f32, _f32, _f32, _f32, P, P,
+                                    P]),
     "kdfm_wgrad_bf16_dev": (_i32, [P, P, P, _i64, P, _i64, P, _i64, _i64, _f32, P, _i64, P]),
     "kdfm_encfm_time_prep": (_i32, [P, _i64, P, P, P, _i32, _i32, _i32, P, P]),
     "kdfm_encfm_router_fwd": (_i32, [P, P, P, P, P, P, P, P, P, P, P, P, P, C.c_uint64, _i32, P, P, P, P, P, P, P,

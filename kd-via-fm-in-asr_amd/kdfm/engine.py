@@ -121,6 +121,13 @@ class Ver5Engine:
         if K.twins_enabled():   # opt-in direct-B skinny path (KDFM_SKINNY_DIRECT_MIN_M)
             self.student.enable_bf16_twins()
             self.teacher.enable_bf16_twins()
+        # KDFM_BF16_MIRROR=1 (wide models, d_model >= 512): the student's weights also live as a bf16 mirror the
+        # optimizer writes in its own pass (kdfm_adamw_noam_bf16), read by the large-tile products without a cast
+        # per weight per step.  Off by default: measured neutral on the XL bf16 step (82.0-82.2 vs 82.0-82.9 ms,
+        # interleaved, profiles/r06/r6ac_bf16_mirror_ab.log) -- the casts it removes were not on the critical path
+        if (dev.type == "cuda" and max(cfg.d_student, cfg.d_teacher) >= 512
+                and __import__("os").environ.get("KDFM_BF16_MIRROR", "0") == "1"):
+            self.student.enable_bf16_mirror()
         self._pos = {}
         self._imgs = None   # kernels.WeightImages of the student and the teacher encoders (bf16 math)
         self._ws = {}
@@ -614,7 +621,8 @@ class Ver5Engine:
             K.grad_stats(st.grad, grad_scale, self.grad_stats)
         K.adamw_noam(st.data, st.grad, st.exp_avg, st.exp_avg_sq, self.step, cfg.lr, cfg.sched_d_model,
                      cfg.warmup_steps, cfg.min_lr, cfg.betas[0], cfg.betas[1], cfg.adam_eps, cfg.weight_decay,
-                     grad_scale, self.lr, adam_base=self.adam_base, gstats=self.grad_stats)
+                     grad_scale, self.lr, adam_base=self.adam_base, gstats=self.grad_stats,
+                     p16=getattr(st, "mirror", None))
 
     def advance_rng(self):
         with self._on_stream():

@@ -265,9 +265,35 @@ def _epoch_of(W):
     return _State.fp8_epoch
 
 
+_MIRRORS = []   # (first byte, end byte, bf16 mirror tensor): flat parameter buffers with a maintained bf16 mirror
+
+
+def register_bf16_mirror(buf, mirror) -> None:
+    """`mirror` (bf16, same element layout) is kept equal to bf16(buf) by its owner (FlatStore: refreshed on load,
+    written by AdamW in the same pass, kdfm_adamw_noam_bf16): the large-tile route reads weight views of `buf` from
+    it directly -- no cast per engine call."""
+    lo = buf.data_ptr()
+    _MIRRORS[:] = [m for m in _MIRRORS if m[0] != lo]
+    _MIRRORS.append((lo, lo + buf.numel() * 4, mirror))
+
+
+def _mirror_of(W):
+    p = W.data_ptr()
+    for lo, hi, mir in _MIRRORS:
+        if lo <= p < hi and W.dtype == torch.float32 and W.stride(1) == 1 and W.stride(0) % 8 == 0:
+            a = mir.data_ptr() + (p - lo) // 2
+            if a % 16 == 0:
+                return a, W.stride(0)
+    return None
+
+
 def _bf16_weight(W):
     """The large-tile route's bf16 copy of a weight view for this epoch (cast on first use), or None outside an
-    epoch; persistent storage (a recorded plan replays the cast into it).  Frozen weights: once per version."""
+    epoch; persistent storage (a recorded plan replays the cast into it).  Frozen weights: once per version.  A
+    weight inside a mirrored flat buffer (register_bf16_mirror): its mirror view, no copy."""
+    m = _mirror_of(W)
+    if m is not None:
+        return m
     ep = _epoch_of(W)
     if ep is None or W.dtype != torch.float32:
         return None
@@ -1956,11 +1982,17 @@ def fm_time_bwd(dc, evec, W1, dW1, db1, dw_te, db_te, L, E, steps):
 
 
 def adamw_noam(p, g, m, v, step, base_lr, d_model, warmup, min_lr, beta1, beta2, eps, wd, grad_scale, lr_out=None,
-               adam_base=None, gstats=None):
+               adam_base=None, gstats=None, p16=None):
     """Fused AdamW + Noam (csrc/optim.hip); with `gstats` (grad_stats' output) the update is skipped
-    when the gradient holds a non-finite value."""
+    when the gradient holds a non-finite value.  p16: the flat buffer's bf16 mirror, written in the same pass."""
     assert p.numel() == g.numel() == m.numel() == v.numel()
     assert gstats is None or (gstats.numel() >= 2 and gstats.dtype == torch.float32)
+    if p16 is not None:
+        assert p16.numel() == p.numel() and p16.dtype == torch.bfloat16
+        call("kdfm_adamw_noam_bf16", ptr(p), ptr(g), ptr(m), ptr(v), p16.data_ptr(), p.numel(), ptr(step),
+             ptr(adam_base), float(base_lr), float(d_model), float(warmup), float(min_lr), float(beta1), float(beta2),
+             float(eps), float(wd), float(grad_scale), ptr(lr_out), ptr(gstats), _s())
+        return
     call("kdfm_adamw_noam", ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), ptr(step), ptr(adam_base), float(base_lr),
          float(d_model),
          float(warmup), float(min_lr), float(beta1), float(beta2), float(eps), float(wd), float(grad_scale),

@@ -100,7 +100,18 @@ class FlatStore:
         self._tblocks = blk
         K.register_bf16_twin(self.data, self.h, self.ht, entries)
 
+    def enable_bf16_mirror(self) -> None:
+        """A bf16 mirror of the whole buffer (same layout) for the large-tile GEMM's weight operands, kept current by
+        load() / refresh_bf16() and by the optimizer (kdfm_adamw_noam_bf16 writes it in the same pass)."""
+        if getattr(self, "mirror", None) is not None:
+            return
+        self.mirror = torch.empty(self.numel, device=self.device, dtype=torch.bfloat16)
+        K.cast_bf16(self.data, self.mirror)
+        K.register_bf16_mirror(self.data, self.mirror)
+
     def refresh_bf16(self) -> None:
+        if getattr(self, "mirror", None) is not None:
+            K.cast_bf16(self.data, self.mirror)
         if getattr(self, "h", None) is None:
             return
         K.cast_bf16(self.data, self.h)
@@ -123,6 +134,8 @@ class FlatStore:
                 raise ValueError(f"{name}: shape {tuple(t.shape)} != {tuple(shape)}")
             self.P[name].copy_(t.detach().to(torch.float32))
         self.version += 1
+        if getattr(self, "mirror", None) is not None:
+            K.cast_bf16(self.data, self.mirror)
         if strict and missing:
             raise KeyError(f"missing parameters: {missing[:5]}{'...' if len(missing) > 5 else ''}")
 

@@ -161,3 +161,26 @@ def test_resumed_moments_restart_bias_correction():
     ref.grad = grad.clone()
     opt.step()
     torch.testing.assert_close(p.cpu(), ref.detach(), rtol=1e-5, atol=1e-6)
+
+
+def test_adamw_bf16_mirror_written_in_the_same_pass():
+    """kdfm_adamw_noam_bf16 (the wide models' student): the same f32 update as kdfm_adamw_noam, bit for bit, and the
+    mirror equal to the updated parameters rounded to bf16 -- also for a length that is not a multiple of 4."""
+    from kdfm import kernels as K
+    dev = "cuda"
+    for n in (1 << 20, 12345):
+        g = torch.Generator(device=dev).manual_seed(n)
+        p0 = torch.randn(n, device=dev, generator=g)
+        gr = torch.randn(n, device=dev, generator=g)
+        m0 = torch.randn(n, device=dev, generator=g) * 0.1
+        v0 = torch.rand(n, device=dev, generator=g) * 0.1
+        step = torch.tensor([7], dtype=torch.int64, device=dev)
+        outs = []
+        for mirror in (False, True):
+            p, m, v = p0.clone(), m0.clone(), v0.clone()
+            p16 = torch.empty(n, device=dev, dtype=torch.bfloat16) if mirror else None
+            K.adamw_noam(p, gr, m, v, step, 5.0, 176.0, 10000.0, 1e-6, 0.9, 0.98, 1e-9, 1e-3, 1.0, p16=p16)
+            torch.cuda.synchronize()
+            outs.append((p, m, v, p16))
+        assert all(torch.equal(a, b) for a, b in zip(outs[0][:3], outs[1][:3]))
+        assert torch.equal(outs[1][3], outs[1][0].bfloat16())
