@@ -277,7 +277,25 @@ __global__ __launch_bounds__(256) void bn_silu_bwd_reduce_kernel(const float* __
   double s1 = 0.0, s2 = 0.0;
   if (c < d) {
     const float mu = mean[c], rs = rstd[c], g = gm[c], b = bt[c];
-    for (int64_t r = r0 + w; r < r1; r += 4) {
+    // 4 rows per wave per pass, their 8 loads issued together (clamped, masked): one dependent load per row made
+    // the loop one memory round trip per row (13 us for 12 832 x 88); same per-row terms, same summation order
+    int64_t r = r0 + w;
+    for (; r + 12 < r1; r += 16) {
+      float yv[4], zv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        yv[u] = y[(r + 4 * u) * d + c];
+        zv[u] = dz[(r + 4 * u) * d + c];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float xh = (yv[u] - mu) * rs;
+        const float dyb = zv[u] * dsiluf_(g * xh + b);
+        s1 += dyb;
+        s2 += (double)dyb * xh;
+      }
+    }
+    for (; r < r1; r += 4) {
       const float xh = (y[r * d + c] - mu) * rs;
       const float dyb = dz[r * d + c] * dsiluf_(g * xh + b);
       s1 += dyb;

@@ -316,18 +316,21 @@ __global__ __launch_bounds__(64 * LNF_WAVES) void ln_fold_kernel(LnFold f, int64
   const int c = blockIdx.x * 64 + lane;
   const float* part = f.part[e];
   const int64_t ld = 2 * (int64_t)d;
-  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  // eight independent accumulators (eight loads in flight per lane; four left the 16-wave fold latency-bound at
+  // ~12 us for a layer's six 802-row partial sets), combined in a fixed order
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if (c < 2 * d) {
     int64_t b = w;
-    for (; b + 3 * LNF_WAVES < nparts; b += 4 * LNF_WAVES) {
-      s0 += part[b * ld + c];
-      s1 += part[(b + LNF_WAVES) * ld + c];
-      s2 += part[(b + 2 * LNF_WAVES) * ld + c];
-      s3 += part[(b + 3 * LNF_WAVES) * ld + c];
+    for (; b + 7 * LNF_WAVES < nparts; b += 8 * LNF_WAVES) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = part[(b + u * LNF_WAVES) * ld + c];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s[u] += v[u];
     }
-    for (; b < nparts; b += LNF_WAVES) s0 += part[b * ld + c];
+    for (; b < nparts; b += LNF_WAVES) s[0] += part[b * ld + c];
   }
-  red[w][lane] = (s0 + s1) + (s2 + s3);
+  red[w][lane] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
   __syncthreads();
   if (w == 0 && c < 2 * d) {
     float v = 0.f;
