@@ -7,6 +7,8 @@
 // BatchNorm statistics accumulate in f64.
 #include "common.h"
 
+#include <initializer_list>
+
 namespace kdfm {
 namespace {
 
@@ -26,6 +28,83 @@ __global__ __launch_bounds__(256) void glu_mask_fwd_kernel(const float* __restri
     v = x * sigmoidf_(y);
   }
   g[idx] = v;
+}
+
+// 16-byte-lane forms of the GLU mask kernels and the BN-SiLU forward (d % 4 == 0, aligned, fewer than 2^31
+// float4 groups): 4 channels per thread and 32-bit index math -- the scalar kernels spend three 64-bit divisions per
+// element (FastConformer-XL: 6 432 x 1024 GLU forward 35 us).  Same per-element arithmetic.
+__device__ __forceinline__ float4 glu4(float4 x, float4 y) {
+  return make_float4(x.x * sigmoidf_(y.x), x.y * sigmoidf_(y.y), x.z * sigmoidf_(y.z), x.w * sigmoidf_(y.w));
+}
+
+__global__ __launch_bounds__(256) void glu_mask_fwd4_kernel(const float* __restrict__ a, const int64_t* __restrict__ lens,
+                                                            float* __restrict__ g, int n4, int T, int d4) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n4) return;
+  const int r = i / d4, c = i - r * d4;
+  const int b = r / T, t = r - b * T;
+  float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (!lens || t < lens[b]) {
+    const float4* ar = reinterpret_cast<const float4*>(a) + (int64_t)r * 2 * d4;
+    v = glu4(ar[c], ar[d4 + c]);
+  }
+  reinterpret_cast<float4*>(g)[i] = v;
+}
+
+template <typename O>
+__global__ __launch_bounds__(256) void glu_mask_bwd4_kernel(const float* __restrict__ dg, const float* __restrict__ a,
+                                                            const int64_t* __restrict__ lens, O* __restrict__ da, int n4,
+                                                            int T, int d4) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n4) return;
+  const int r = i / d4, c = i - r * d4;
+  const int b = r / T, t = r - b * T;
+  float dx[4] = {0.f, 0.f, 0.f, 0.f}, dyv[4] = {0.f, 0.f, 0.f, 0.f};
+  if (!lens || t < lens[b]) {
+    const float4* ar = reinterpret_cast<const float4*>(a) + (int64_t)r * 2 * d4;
+    const float4 x4 = ar[c], y4 = ar[d4 + c], g4 = reinterpret_cast<const float4*>(dg)[i];
+    const float xs[4] = {x4.x, x4.y, x4.z, x4.w}, ys[4] = {y4.x, y4.y, y4.z, y4.w}, gs[4] = {g4.x, g4.y, g4.z, g4.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float s = sigmoidf_(ys[e]);
+      dx[e] = gs[e] * s;
+      dyv[e] = gs[e] * xs[e] * s * (1.f - s);
+    }
+  }
+  const int64_t o = (int64_t)r * 2 * d4 * 4 + 4 * c;
+  if constexpr (sizeof(O) == 2) {
+    *reinterpret_cast<uint2*>(da + o) = make_uint2(pack_bf16x2(dx[0], dx[1]), pack_bf16x2(dx[2], dx[3]));
+    *reinterpret_cast<uint2*>(da + o + 4 * d4) = make_uint2(pack_bf16x2(dyv[0], dyv[1]), pack_bf16x2(dyv[2], dyv[3]));
+  } else {
+    *reinterpret_cast<float4*>(da + o) = make_float4(dx[0], dx[1], dx[2], dx[3]);
+    *reinterpret_cast<float4*>(da + o + 4 * d4) = make_float4(dyv[0], dyv[1], dyv[2], dyv[3]);
+  }
+}
+
+template <typename O>
+__global__ __launch_bounds__(256) void bn_silu_fwd4_kernel(const float* __restrict__ y, const float* __restrict__ mean,
+                                                           const float* __restrict__ rstd, const float* __restrict__ gm,
+                                                           const float* __restrict__ bt, O* __restrict__ z, int n4,
+                                                           int d4) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n4) return;
+  const int c = i % d4;
+  const float4 yv = reinterpret_cast<const float4*>(y)[i], mu = reinterpret_cast<const float4*>(mean)[c];
+  const float4 rs = reinterpret_cast<const float4*>(rstd)[c], g = reinterpret_cast<const float4*>(gm)[c];
+  const float4 b = reinterpret_cast<const float4*>(bt)[c];
+  const float o0 = siluf_(g.x * (yv.x - mu.x) * rs.x + b.x), o1 = siluf_(g.y * (yv.y - mu.y) * rs.y + b.y);
+  const float o2 = siluf_(g.z * (yv.z - mu.z) * rs.z + b.z), o3 = siluf_(g.w * (yv.w - mu.w) * rs.w + b.w);
+  if constexpr (sizeof(O) == 2)
+    reinterpret_cast<uint2*>(z)[i] = make_uint2(pack_bf16x2(o0, o1), pack_bf16x2(o2, o3));
+  else
+    reinterpret_cast<float4*>(z)[i] = make_float4(o0, o1, o2, o3);
+}
+
+__host__ inline bool ew4_ok(int64_t rows, int64_t d, std::initializer_list<const void*> ptrs) {
+  if (d % 4 || rows * (d / 4) >= ((int64_t)1 << 31)) return false;
+  for (const void* p : ptrs)
+    if (((uintptr_t)p) & 15) return false;
+  return true;
 }
 
 template <typename O>   // uint16_t: da rounded to bf16 (kdfm_glu_mask_bwd_bf16)
@@ -550,6 +629,12 @@ int kdfm_glu_mask_fwd(const float* a, const int64_t* lengths, float* g, int64_t 
   KDFM_REQUIRE(a && g, "null pointer");
   const int64_t n = B * T * d;
   if (n == 0) return KDFM_OK;
+  if (ew4_ok(B * T, d, {a, g}) && T < ((int64_t)1 << 31)) {
+    const int64_t n4 = n / 4;
+    hipLaunchKernelGGL(glu_mask_fwd4_kernel, dim3((unsigned)ceil_div(n4, 256)), dim3(256), 0, as_stream(stream), a,
+                       lengths, g, (int)n4, (int)T, (int)(d / 4));
+    return check_launch("kdfm_glu_mask_fwd");
+  }
   hipLaunchKernelGGL(glu_mask_fwd_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, as_stream(stream), a,
                      lengths, g, B * T, T, d);
   return check_launch("kdfm_glu_mask_fwd");
@@ -561,6 +646,12 @@ int kdfm_glu_mask_bwd(const float* dg, const float* a, const int64_t* lengths, f
   KDFM_REQUIRE(dg && a && da, "null pointer");
   const int64_t n = B * T * d;
   if (n == 0) return KDFM_OK;
+  if (ew4_ok(B * T, d, {dg, a, da})) {
+    const int64_t n4 = n / 4;
+    hipLaunchKernelGGL(glu_mask_bwd4_kernel<float>, dim3((unsigned)ceil_div(n4, 256)), dim3(256), 0, as_stream(stream), dg,
+                       a, lengths, da, (int)n4, (int)T, (int)(d / 4));
+    return check_launch("kdfm_glu_mask_bwd");
+  }
   hipLaunchKernelGGL(glu_mask_bwd_kernel<float>, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, as_stream(stream), dg,
                      a, lengths, da, B * T, T, d);
   return check_launch("kdfm_glu_mask_bwd");
@@ -572,6 +663,12 @@ int kdfm_glu_mask_bwd_bf16(const float* dg, const float* a, const int64_t* lengt
   KDFM_REQUIRE(dg && a && da, "null pointer");
   const int64_t n = B * T * d;
   if (n == 0) return KDFM_OK;
+  if (ew4_ok(B * T, d, {dg, a, da})) {
+    const int64_t n4 = n / 4;
+    hipLaunchKernelGGL(glu_mask_bwd4_kernel<uint16_t>, dim3((unsigned)ceil_div(n4, 256)), dim3(256), 0, as_stream(stream), dg,
+                       a, lengths, da, (int)n4, (int)T, (int)(d / 4));
+    return check_launch("kdfm_glu_mask_bwd");
+  }
   hipLaunchKernelGGL(glu_mask_bwd_kernel<uint16_t>, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, as_stream(stream),
                      dg, a, lengths, da, B * T, T, d);
   return check_launch("kdfm_glu_mask_bwd_bf16");
@@ -716,6 +813,12 @@ int kdfm_bn_silu_fwd(const float* y, const float* mean, const float* rstd, const
   KDFM_REQUIRE(y && mean && rstd && gamma && beta && z, "null pointer");
   const int64_t n = rows * d;
   if (n == 0) return KDFM_OK;
+  if (ew4_ok(rows, d, {y, mean, rstd, gamma, beta, z})) {
+    const int64_t n4 = n / 4;
+    hipLaunchKernelGGL(bn_silu_fwd4_kernel<float>, dim3((unsigned)ceil_div(n4, 256)), dim3(256), 0, as_stream(stream), y,
+                       mean, rstd, gamma, beta, z, (int)n4, (int)(d / 4));
+    return check_launch("kdfm_bn_silu_fwd");
+  }
   hipLaunchKernelGGL(bn_silu_fwd_kernel<float>, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, as_stream(stream), y,
                      mean, rstd, gamma, beta, z, n, d);
   return check_launch("kdfm_bn_silu_fwd");
@@ -727,6 +830,12 @@ int kdfm_bn_silu_fwd_bf16(const float* y, const float* mean, const float* rstd, 
   KDFM_REQUIRE(y && mean && rstd && gamma && beta && z, "null pointer");
   const int64_t n = rows * d;
   if (n == 0) return KDFM_OK;
+  if (ew4_ok(rows, d, {y, mean, rstd, gamma, beta, z})) {
+    const int64_t n4 = n / 4;
+    hipLaunchKernelGGL(bn_silu_fwd4_kernel<uint16_t>, dim3((unsigned)ceil_div(n4, 256)), dim3(256), 0, as_stream(stream), y,
+                       mean, rstd, gamma, beta, z, (int)n4, (int)(d / 4));
+    return check_launch("kdfm_bn_silu_fwd");
+  }
   hipLaunchKernelGGL(bn_silu_fwd_kernel<uint16_t>, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, as_stream(stream),
                      y, mean, rstd, gamma, beta, z, n, d);
   return check_launch("kdfm_bn_silu_fwd_bf16");
