@@ -7,6 +7,7 @@
 // BatchNorm statistics accumulate in f64.
 #include "common.h"
 
+#include <cstdlib>
 #include <initializer_list>
 
 namespace kdfm {
@@ -617,6 +618,302 @@ __global__ __launch_bounds__(256) void dwconv_bwd_kernel(const float* __restrict
   }
 }
 
+// The same backward with a lane owning a channel PAIR (channels c0 + 2 lane, +1: 128 channels per workgroup,
+// 8-byte LDS window reads, every FMA a packed v_pk_fma_f32 over the two channels).  The Conformer's d = 88 took
+// 2 channel tiles of 64 (the second 24/64 used) and 1 792 waves at 160 VGPRs (1.75 per SIMD, contending for
+// issue); here d <= 128 is one tile: 224 workgroups x 4 waves at the bench shape, each wave's instruction
+// count about that of one wave before.  Per output element the same operations in the same order as
+// dwconv_bwd_kernel (the tap chain of dg, the frame chain of each dw tap, the wave-slot combine, the BN
+// apply): bitwise its results.  The dw reduction reuses the tile LDS after the last window read.
+constexpr int CP = 128;   // channels per workgroup (64 lanes x 2)
+// Channel pairs for d <= 128 (one workgroup column): the d = 88 backward with BN-SiLU on load 20.3 -> 16.6 us
+// isolated (profiles/r06/r6an); at d = 176 the 128 + 48 split is slower than the one-channel kernel's 64 + 64 + 48
+// tiles (29.4 -> 36.6 us).  The forward only without the fused f64 statistics (7.7 -> 7.2 us; with them 10.8 ->
+// 11.6 us: two channels' f64 sums per lane).  KDFM_DWC_P2=0: never, =2: always (read per call: tests compare)
+inline int dwc_mode() {
+  const char* e = getenv("KDFM_DWC_P2");
+  return e ? atoi(e) : 1;
+}
+inline bool dwc_p2(int64_t d, bool fused_stats = false) {
+  const int m = dwc_mode();
+  return m == 2 || (m == 1 && d <= CP && !fused_stats);
+}
+typedef float pf2 __attribute__((ext_vector_type(2)));
+
+template <int KC>
+constexpr int p2_rows() { return TT + KC - 1; }
+template <int KC, int NT>
+constexpr int p2_tq() { return (p2_rows<KC>() * (CP / 4) + NT - 1) / NT; }
+
+template <int KC, int NT>
+__device__ __forceinline__ void p2_tile_load(float4 (&v)[(p2_tq<KC, NT>())], const float* __restrict__ src, int64_t b,
+                                             int64_t t0, int64_t T, int64_t d, int64_t c0) {
+  constexpr int pad = (KC - 1) / 2, rows = p2_rows<KC>();
+#pragma unroll
+  for (int i = 0; i < p2_tq<KC, NT>(); ++i) {
+    const int q = threadIdx.x + i * NT;
+    const int rr = q >> 5, c4 = (q & 31) * 4;
+    const int64_t t = t0 + rr - pad, c = c0 + c4;
+    const bool ok = rr < rows && t >= 0 && t < T && c < d;
+    const float m = ok ? 1.f : 0.f;
+    const float4 x = *reinterpret_cast<const float4*>(src + (b * T + (ok ? t : 0)) * d + (ok ? c : 0));
+    v[i] = make_float4(x.x * m, x.y * m, x.z * m, x.w * m);
+  }
+}
+
+template <int KC, int NT>
+__device__ __forceinline__ void p2_tile_store(const float4 (&v)[(p2_tq<KC, NT>())], float* tile) {
+  constexpr int rows = p2_rows<KC>();
+#pragma unroll
+  for (int i = 0; i < p2_tq<KC, NT>(); ++i) {
+    const int q = threadIdx.x + i * NT;
+    const int rr = q >> 5, c4 = (q & 31) * 4;
+    if (rr < rows) *reinterpret_cast<float4*>(tile + rr * CP + c4) = v[i];
+  }
+}
+
+// Forward with a lane owning a channel pair (as dwconv_bwd_p2_kernel), 8 waves of 8 frames: y = bias + the tap
+// chain in dwconv_fwd_kernel's order (bitwise its y); the BatchNorm sums per channel in f64, this wave's frames in
+// order, the 8 waves added in order before the one atomic per channel and workgroup.
+constexpr int P2_NT = 512;
+template <int KC>
+__global__ __launch_bounds__(P2_NT) void dwconv_fwd_p2_kernel(const float* __restrict__ g, const float* __restrict__ w,
+                                                              const float* __restrict__ bias, float* __restrict__ y,
+                                                              double* __restrict__ stats, int64_t T, int64_t d) {
+  constexpr int rows = p2_rows<KC>(), TQW = p2_tq<KC, P2_NT>(), FW = TT / 8;
+  __shared__ __attribute__((aligned(16))) float tile[rows * CP];
+  __shared__ double red[2][8][CP];
+  const int64_t b = blockIdx.z;
+  const int64_t t0 = (int64_t)blockIdx.x * TT;
+  const int64_t c0 = (int64_t)blockIdx.y * CP;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int f0 = wave * FW;
+  const int64_t c = c0 + 2 * lane;
+  const bool cok = c < d;
+  pf2 wv[KC];
+  pf2 bc = pf2{0.f, 0.f};
+  {
+    float4 v[TQW];
+    p2_tile_load<KC, P2_NT>(v, g, b, t0, T, d, c0);
+    const float mm = cok ? 1.f : 0.f;
+    const float* wa = w + (cok ? c : 0) * KC;
+    const float* wb = w + (cok ? c + 1 : 0) * KC;
+#pragma unroll
+    for (int k = 0; k < KC; ++k) wv[k] = pf2{wa[k] * mm, wb[k] * mm};
+    if (bias) bc = pf2{bias[cok ? c : 0] * mm, bias[cok ? c + 1 : 0] * mm};
+    p2_tile_store<KC, P2_NT>(v, tile);
+  }
+  __syncthreads();
+  auto rd = [&](int r) { return *reinterpret_cast<const pf2*>(tile + r * CP + 2 * lane); };
+  pf2 acc[FW], win[FW];
+#pragma unroll
+  for (int tt = 0; tt < FW; ++tt) {
+    acc[tt] = bc;
+    win[tt] = rd(f0 + tt);
+  }
+#pragma unroll
+  for (int k = 0; k < KC; ++k) {
+    const pf2 wk = wv[k];
+#pragma unroll
+    for (int tt = 0; tt < FW; ++tt) acc[tt] = __builtin_elementwise_fma(wk, win[tt], acc[tt]);
+    if (k + 1 < KC) {
+#pragma unroll
+      for (int tt = 0; tt < FW - 1; ++tt) win[tt] = win[tt + 1];
+      win[FW - 1] = rd(f0 + k + FW);
+    }
+  }
+  double s1a = 0.0, s2a = 0.0, s1b = 0.0, s2b = 0.0;
+  if (cok) {
+#pragma unroll
+    for (int tt = 0; tt < FW; ++tt) {
+      const int64_t t = t0 + f0 + tt;
+      if (t < T) {
+        *reinterpret_cast<pf2*>(y + (b * T + t) * d + c) = acc[tt];
+        s1a += acc[tt].x;
+        s2a += (double)acc[tt].x * acc[tt].x;
+        s1b += acc[tt].y;
+        s2b += (double)acc[tt].y * acc[tt].y;
+      }
+    }
+  }
+  if (!stats) return;
+  red[0][wave][2 * lane] = s1a;
+  red[0][wave][2 * lane + 1] = s1b;
+  red[1][wave][2 * lane] = s2a;
+  red[1][wave][2 * lane + 1] = s2b;
+  __syncthreads();
+  if (threadIdx.x < 2 * CP && c0 + (threadIdx.x & (CP - 1)) < d) {
+    const int q = threadIdx.x & (CP - 1), m = threadIdx.x >> 7;   // m: sum (0) or sum of squares (1)
+    double v = 0.0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v += red[m][i][q];
+    atomicAdd(stats + m * d + c0 + q, v);
+  }
+}
+
+// 8 waves: waves 0-3 form dg of frame groups 0-3, waves 4-7 the dw / db sums of the same groups -- each wave half the
+// serial chain of a 4-wave workgroup's, two waves per SIMD, and no sum regrouped (bitwise as before)
+template <int KC, bool BN>
+__global__ __launch_bounds__(P2_NT) void dwconv_bwd_p2_kernel(const float* __restrict__ dy, const float* __restrict__ g,
+                                                              const float* __restrict__ w, float* __restrict__ dg,
+                                                              float* __restrict__ part, int64_t T, int64_t d, BnApply bn) {
+  constexpr int K = KC, pad = (KC - 1) / 2, rows = p2_rows<KC>(), TQW = p2_tq<KC, P2_NT>();
+  __shared__ __attribute__((aligned(16))) float lds[2 * rows * CP];
+  float* tdy = lds;
+  float* tg = lds + rows * CP;
+  const int64_t b = blockIdx.z;
+  const int64_t t0 = (int64_t)blockIdx.x * TT;
+  const int64_t c0 = (int64_t)blockIdx.y * CP;
+  const int lane = threadIdx.x & 63, slot = (threadIdx.x >> 6) & 3;
+  const bool dwave = threadIdx.x >= 256;   // a dw / db wave
+  const int f0 = slot * 16;   // this wave's first frame in the tile
+  const int64_t c = c0 + 2 * lane;
+  const bool cok = c < d;     // d % 4 == 0: a pair is wholly in or out
+  pf2 wv[KC];
+  {
+    float4 v1[TQW], v2[TQW];
+    if constexpr (BN) {
+      // BN + SiLU backward applied on load (tile_load_bn over 128-channel rows)
+      const int c4 = (threadIdx.x & 31) * 4;
+      const int64_t cb = c0 + c4 < d ? c0 + c4 : 0;
+      float mu[4], rs[4], gm[4], bt[4], m1[4], m2[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        mu[j] = bn.mean[cb + j];
+        rs[j] = bn.rstd[cb + j];
+        gm[j] = bn.gm[cb + j];
+        bt[j] = bn.bt[cb + j];
+        m1[j] = bn.batch_stats ? (float)(bn.red[cb + j] / bn.count) : 0.f;
+        m2[j] = bn.batch_stats ? (float)(bn.red[d + cb + j] / bn.count) : 0.f;
+      }
+      float4 z[TQW], yv[TQW];
+      float mk[TQW];
+#pragma unroll
+      for (int i = 0; i < TQW; ++i) {
+        const int q = threadIdx.x + i * P2_NT;
+        const int rr = q >> 5;
+        const int64_t t = t0 + rr - pad, cc = c0 + c4;
+        const bool ok = rr < rows && t >= 0 && t < T && cc < d;
+        mk[i] = ok ? 1.f : 0.f;
+        const int64_t off = (b * T + (ok ? t : 0)) * d + (ok ? cc : 0);
+        z[i] = *reinterpret_cast<const float4*>(dy + off);
+        yv[i] = *reinterpret_cast<const float4*>(bn.y + off);
+      }
+      p2_tile_load<KC, P2_NT>(v2, g, b, t0, T, d, c0);
+#pragma unroll
+      for (int i = 0; i < TQW; ++i) {
+        const float zz[4] = {z[i].x, z[i].y, z[i].z, z[i].w};
+        const float yy[4] = {yv[i].x, yv[i].y, yv[i].z, yv[i].w};
+        float o[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float xh = (yy[j] - mu[j]) * rs[j];
+          const float dyb = zz[j] * dsiluf_(gm[j] * xh + bt[j]);
+          o[j] = gm[j] * rs[j] * (dyb - m1[j] - xh * m2[j]) * mk[i];
+        }
+        v1[i] = make_float4(o[0], o[1], o[2], o[3]);
+      }
+      if (blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0) {
+        for (int64_t ch = threadIdx.x; ch < d; ch += P2_NT) {
+          bn.dgamma[ch] += (float)bn.red[d + ch];
+          bn.dbeta[ch] += (float)bn.red[ch];
+          if (bn.red_next) {
+            bn.red_next[ch] = 0.0;
+            bn.red_next[d + ch] = 0.0;
+          }
+        }
+      }
+    } else {
+      p2_tile_load<KC, P2_NT>(v1, dy, b, t0, T, d, c0);
+      p2_tile_load<KC, P2_NT>(v2, g, b, t0, T, d, c0);
+    }
+    {   // the taps of the lane's two channels (zero past d)
+      const float mm = cok ? 1.f : 0.f;
+      const float* wa = w + (cok ? c : 0) * KC;
+      const float* wb = w + (cok ? c + 1 : 0) * KC;
+#pragma unroll
+      for (int k = 0; k < KC; ++k) wv[k] = pf2{wa[k] * mm, wb[k] * mm};
+    }
+    p2_tile_store<KC, P2_NT>(v1, tdy);
+    p2_tile_store<KC, P2_NT>(v2, tg);
+  }
+  __syncthreads();
+  auto rd = [&](const float* tile, int r) { return *reinterpret_cast<const pf2*>(tile + r * CP + 2 * lane); };
+  pf2 sk[KC];
+  pf2 bsum = pf2{0.f, 0.f};
+  if (!dwave) {
+  // dg[f0+tt] = sum_kk w[K-1-kk] * tdy[f0 + tt + kk]
+  pf2 win[16], acc[16];
+#pragma unroll
+  for (int tt = 0; tt < 16; ++tt) {
+    win[tt] = rd(tdy, f0 + tt);
+    acc[tt] = pf2{0.f, 0.f};
+  }
+#pragma unroll
+  for (int kk = 0; kk < KC; ++kk) {
+    const pf2 wk = wv[KC - 1 - kk];
+#pragma unroll
+    for (int tt = 0; tt < 16; ++tt) acc[tt] = __builtin_elementwise_fma(wk, win[tt], acc[tt]);
+    if (kk + 1 < KC) {
+#pragma unroll
+      for (int tt = 0; tt < 15; ++tt) win[tt] = win[tt + 1];
+      win[15] = rd(tdy, f0 + kk + 16);
+    }
+  }
+  if (cok) {
+#pragma unroll
+    for (int tt = 0; tt < 16; ++tt) {
+      const int64_t t = t0 + f0 + tt;
+      if (t < T) *reinterpret_cast<pf2*>(dg + (b * T + t) * d + c) = acc[tt];
+    }
+  }
+  } else {
+  // dw[k] = sum_tt dy[f0+tt] * tg[f0 + tt + k]; db = sum_tt dy[f0+tt].  Frames outermost, a KC-row window of tg
+  // sliding down them: the KC tap sums are independent chains (a tap's 16-frame chain back to back would stall
+  // the packed FMA's dependency latency), each still summed over tt in order
+  pf2 wg[KC];
+#pragma unroll
+  for (int k = 0; k < KC; ++k) {
+    wg[k] = rd(tg, f0 + k);
+    sk[k] = pf2{0.f, 0.f};
+  }
+#pragma unroll
+  for (int tt = 0; tt < 16; ++tt) {
+    const pf2 dyv = rd(tdy, f0 + tt + pad);
+    bsum += dyv;
+#pragma unroll
+    for (int k = 0; k < KC; ++k) sk[k] = __builtin_elementwise_fma(dyv, wg[k], sk[k]);
+    if (tt + 1 < 16) {
+#pragma unroll
+      for (int k = 0; k < KC - 1; ++k) wg[k] = wg[k + 1];
+      wg[KC - 1] = rd(tg, f0 + tt + KC);
+    }
+  }
+  }
+  __syncthreads();   // every wave is past its last tile read: the tiles' LDS takes the wave slots
+  float* red = lds;  // red[slot][k][CP], k = K: the bias sums
+  if (dwave) {
+#pragma unroll
+    for (int k = 0; k < KC; ++k) *reinterpret_cast<pf2*>(red + (slot * (K + 1) + k) * CP + 2 * lane) = sk[k];
+    *reinterpret_cast<pf2*>(red + (slot * (K + 1) + K) * CP + 2 * lane) = bsum;
+  }
+  __syncthreads();
+  const int64_t ld = d * (K + 1);
+  float* pr = part + (b * gridDim.x + blockIdx.x) * ld;
+  for (int e = threadIdx.x; e < (K + 1) * CP; e += P2_NT) {
+    const int q = e / (K + 1), k = e % (K + 1);
+    const int64_t cq = c0 + q;
+    if (cq >= d) continue;
+    const float* rq = red + k * CP + q;
+    const int sl = (K + 1) * CP;
+    const float v = (rq[0] + rq[sl]) + (rq[2 * sl] + rq[3 * sl]);
+    if (k < K)
+      pr[cq * K + k] = v;
+    else
+      pr[d * K + cq] = v;
+  }
+}
+
 }  // namespace
 }  // namespace kdfm
 
@@ -684,7 +981,15 @@ int kdfm_dwconv_fwd(const float* g, const float* w, const float* bias, float* y,
   if (B * T * d == 0) return KDFM_OK;
   dim3 grid((unsigned)ceil_div(T, TT), (unsigned)ceil_div(d, CT), (unsigned)B);
   double* st_fused = deterministic() ? nullptr : stats;
-  if (K == 31)
+  if (dwc_p2(d, st_fused != nullptr) && (K == 31 || K == 15 || K == 9)) {
+    const dim3 g2((unsigned)ceil_div(T, TT), (unsigned)ceil_div(d, CP), (unsigned)B);
+    if (K == 31)
+      hipLaunchKernelGGL(dwconv_fwd_p2_kernel<31>, g2, dim3(P2_NT), 0, as_stream(stream), g, w, bias, y, st_fused, T, d);
+    else if (K == 9)
+      hipLaunchKernelGGL(dwconv_fwd_p2_kernel<9>, g2, dim3(P2_NT), 0, as_stream(stream), g, w, bias, y, st_fused, T, d);
+    else
+      hipLaunchKernelGGL(dwconv_fwd_p2_kernel<15>, g2, dim3(P2_NT), 0, as_stream(stream), g, w, bias, y, st_fused, T, d);
+  } else if (K == 31)
     hipLaunchKernelGGL(dwconv_fwd_kernel<31>, grid, dim3(256), 0, as_stream(stream), g, w, bias, y, st_fused, T, d, (int)K);
   else if (K == 9)   // FastConformer(-XL), fast-conformer_ctc_bpe.yaml conv_kernel_size 9
     hipLaunchKernelGGL(dwconv_fwd_kernel<9>, grid, dim3(256), 0, as_stream(stream), g, w, bias, y, st_fused, T, d, (int)K);
@@ -717,7 +1022,15 @@ int kdfm_dwconv_bwd(const float* dy, const float* g, const float* w, float* dg, 
   const int64_t ntt = ceil_div(T, TT);
   dim3 grid((unsigned)ntt, (unsigned)ceil_div(d, CT), (unsigned)B);
   const BnApply none{};
-  if (K == 31)
+  if (dwc_p2(d) && (K == 31 || K == 15 || K == 9)) {
+    const dim3 g2((unsigned)ntt, (unsigned)ceil_div(d, CP), (unsigned)B);
+    if (K == 31)
+      hipLaunchKernelGGL((dwconv_bwd_p2_kernel<31, false>), g2, dim3(P2_NT), 0, st, dy, g, w, dg, ws, T, d, none);
+    else if (K == 15)
+      hipLaunchKernelGGL((dwconv_bwd_p2_kernel<15, false>), g2, dim3(P2_NT), 0, st, dy, g, w, dg, ws, T, d, none);
+    else
+      hipLaunchKernelGGL((dwconv_bwd_p2_kernel<9, false>), g2, dim3(P2_NT), 0, st, dy, g, w, dg, ws, T, d, none);
+  } else if (K == 31)
     hipLaunchKernelGGL(dwconv_bwd_kernel<31>, grid, dim3(256), 0, st, dy, g, w, dg, ws, T, d, (int)K, none);
   else if (K == 9)
     hipLaunchKernelGGL(dwconv_bwd_kernel<9>, grid, dim3(256), 0, st, dy, g, w, dg, ws, T, d, (int)K, none);
@@ -746,6 +1059,16 @@ int kdfm_dwconv_bwd_bn(const float* dz, const float* y, const float* mean, const
   const int64_t ntt = ceil_div(T, TT);
   dim3 grid((unsigned)ntt, (unsigned)ceil_div(d, CT), (unsigned)B);
   const BnApply bn{y, mean, rstd, gamma, beta, red, (double)(B * T), batch_stats, dgamma, dbeta, red_next};
+  if (dwc_p2(d)) {
+    const dim3 g2((unsigned)ntt, (unsigned)ceil_div(d, CP), (unsigned)B);
+    if (K == 31)
+      hipLaunchKernelGGL((dwconv_bwd_p2_kernel<31, true>), g2, dim3(P2_NT), 0, st, dz, g, w, dg, ws, T, d, bn);
+    else if (K == 9)
+      hipLaunchKernelGGL((dwconv_bwd_p2_kernel<9, true>), g2, dim3(P2_NT), 0, st, dz, g, w, dg, ws, T, d, bn);
+    else
+      hipLaunchKernelGGL((dwconv_bwd_p2_kernel<15, true>), g2, dim3(P2_NT), 0, st, dz, g, w, dg, ws, T, d, bn);
+    return check_launch("kdfm_dwconv_bwd_bn");
+  }
   if (K == 31)
     hipLaunchKernelGGL((dwconv_bwd_kernel<31, true>), grid, dim3(256), 0, st, dz, g, w, dg, ws, T, d, (int)K, bn);
   else if (K == 9)

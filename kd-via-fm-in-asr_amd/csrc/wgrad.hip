@@ -55,7 +55,32 @@ struct WrGeo {
   int Msl;           // A columns (output rows) of one M slice (blockIdx.z), a multiple of 16
   int ascal;         // f32 A whose rows are not 16-byte aligned or M % 4 != 0 (the decoder's 129 classes):
                      // its staging units load 4 scalars each, columns past M masked to zero
+  int xgrp;          // column slices of one split on one XCD (wr_block): they read the same rows
 };
+
+// (split, column slice) of this workgroup.  Workgroups go to the XCDs round-robin in dispatch order (x
+// fastest), so with the plain grid the column slices of a split -- which read the same dY rows and (the
+// strided conv gather) overlapping input rows -- land on different XCDs and fetch them through different
+// L2s.  xgrp renumbers the grid in groups of 8 splits x all slices: dispatch slot L of a group goes to
+// split 8 grp + (L % 8), slice L / 8, so a split's slices share the XCD L % 8 and run together; the
+// splits past the last whole group keep the plain order.  A bijection of the grid (every partial is
+// written by exactly one workgroup as before: results bitwise unchanged).
+__device__ __forceinline__ void wr_block(const WrGeo& g, int& bx, int& by) {
+  bx = (int)blockIdx.x;
+  by = (int)blockIdx.y;
+  if (!g.xgrp) return;
+  const int S = (int)gridDim.x, nsl = (int)gridDim.y;
+  const int L = bx + S * by, P = 8 * nsl, full = (S / 8) * P;
+  if (L < full) {
+    const int grp = L / P, r = L - grp * P;
+    bx = grp * 8 + (r & 7);
+    by = r >> 3;
+  } else {
+    const int t = L - full, rem = S - (S / 8) * 8;
+    bx = (S / 8) * 8 + t % rem;
+    by = t / rem;
+  }
+}
 
 // BIN: dY and X are bf16 in memory (the fused KD-head chains store their saved operands as bf16,
 // exactly the values the f32 path would round at staging), no conversion.  BIN = 1: staging units of
@@ -78,13 +103,15 @@ __global__ __launch_bounds__(WR_NT, 2) void wgr_kernel(GemmP p, WrGeo g) {
   const int ia = g.Ma * WR_LDK, ib = g.Nb * WR_LDK;   // image sizes (elements) of one buffer
   const int bufsz = ia + ib;                           // buffer b: A at b*bufsz, B at b*bufsz + ia
   // paired launch: blocks [S, 2S) compute the second product (same shape, its own operands / partials)
+  int bx, by;
+  wr_block(g, bx, by);
   const int64_t S_ = p.A2 ? (int64_t)gridDim.x / 2 : (int64_t)gridDim.x;
-  const bool second = (int64_t)blockIdx.x >= S_;
-  const int64_t split = second ? (int64_t)blockIdx.x - S_ : (int64_t)blockIdx.x;
+  const bool second = (int64_t)bx >= S_;
+  const int64_t split = second ? (int64_t)bx - S_ : (int64_t)bx;
   const float* pA = second ? p.A2 : p.A;
   const float* pB = second ? p.B2 : p.B;
   float* pws = second ? p.ws2 : p.ws;
-  const int64_t n0 = (int64_t)blockIdx.y * g.Nb;       // first output column of this slice
+  const int64_t n0 = (int64_t)by * g.Nb;               // first output column of this slice
   // M slice: output rows m0 .. m0 + mcols - 1 (dY columns); more workgroups for short reductions
   // without growing any workgroup's partial
   const int m0 = (int)blockIdx.z * g.Msl;
@@ -748,6 +775,9 @@ bool wr_plan(const GemmP& p, int amode, int bmode, int64_t batch, WrPlan& pl, bo
   if (S > smax) S = smax;
   pl.g.steps_per = ceil_div(steps, S);
   pl.S = ceil_div(steps, pl.g.steps_per);
+  // per call (tests compare both orders).  Off by default: isolated the s2conv gather 192 -> 184 us and a 5-slice
+  // linear product 33.2 -> 31.9 us, but the step 2374 / 2378 -> 2366 / 2369 utt/s (profiles/r06/r6aj/); KDFM_WGR_XGRP=1
+  pl.g.xgrp = (pl.slices > 1 && pl.mslices == 1 && env_i("KDFM_WGR_XGRP", 0)) ? 1 : 0;
   return true;
 }
 

@@ -138,3 +138,68 @@ def test_dwconv_bwd_bn_equals_separate(B, T, d, k, batch_stats):
     _close(dg1, dg0, rel=1e-5)
     _close(dw1, dw0, rel=1e-5)
     _close(db1, db0, rel=1e-5)
+
+
+@pytest.mark.parametrize("B,T,d,k", [(3, 401, 88, 31), (2, 26, 88, 31), (2, 130, 176, 31), (2, 70, 40, 15),
+                                     (2, 93, 1024, 9), (2, 65, 136, 31)])
+def test_dwconv_bwd_channel_pairs_bitwise(B, T, d, k, monkeypatch):
+    """The channel-pair depthwise backward (dwconv_bwd_p2_kernel: a lane owns 2 channels, 128 per workgroup,
+    packed FMAs) equals the one-channel-per-lane kernel bit for bit -- dg, the weight / bias partials and
+    their fold, plain and with the BN-SiLU backward applied on load (both schedules of the statistics),
+    over one and several channel tiles and ragged frame tails."""
+    K = _K()
+    g = torch.Generator().manual_seed(B * T + d + k + 23)
+    dz = torch.randn(B * T, d, generator=g).cuda()
+    y = torch.randn(B * T, d, generator=g).cuda()
+    gin = torch.randn(B * T, d, generator=g).cuda()
+    w = torch.randn(d, k, generator=g).cuda()
+    mean = torch.randn(d, generator=g).cuda() * 0.1
+    rstd = torch.rand(d, generator=g).cuda() + 0.5
+    gm = torch.randn(d, generator=g).cuda()
+    bt = torch.randn(d, generator=g).cuda()
+    red = torch.zeros(2 * d, dtype=torch.float64, device="cuda")
+    K.bn_silu_bwd_reduce(dz, y, mean, rstd, gm, bt, red)
+    outs = []
+    for flag in ("0", "2"):
+        monkeypatch.setenv("KDFM_DWC_P2", flag)
+        dg = torch.empty(B * T, d, device="cuda")
+        dw, db = torch.zeros(d, k, device="cuda"), torch.zeros(d, device="cuda")
+        K.dwconv_bwd(dz, gin, w, dg, dw, db, B, T, d, k)
+        res = [dg, dw, db]
+        for bs in (True, False):
+            red_next = torch.full((2 * d,), 7.0, dtype=torch.float64, device="cuda")
+            dgm, dbt = torch.zeros(d, device="cuda"), torch.zeros(d, device="cuda")
+            dg1 = torch.empty(B * T, d, device="cuda")
+            ws = torch.full((K.dwconv_bwd_ws(B, T, d, k),), float("nan"), device="cuda")
+            K.dwconv_bwd_bn(dz, y, mean, rstd, gm, bt, red, red_next, dgm, dbt, bs, gin, w, dg1, ws, B, T, d, k)
+            dw1, db1 = torch.zeros(d, k, device="cuda"), torch.zeros(d, device="cuda")
+            K.dwconv_bwd_fold(ws, dw1, db1, B, T, d, k)
+            res += [dg1, dw1, db1, dgm, dbt, red_next]
+        outs.append(res)
+    torch.cuda.synchronize()
+    for i, (a, b) in enumerate(zip(*outs)):
+        assert torch.equal(a, b), f"output {i} differs"
+    assert bool(torch.isfinite(outs[1][0]).all())
+
+
+@pytest.mark.parametrize("B,T,d,k", [(3, 401, 88, 31), (2, 130, 176, 31), (2, 70, 40, 15), (2, 93, 1024, 9)])
+def test_dwconv_fwd_channel_pairs(B, T, d, k, monkeypatch):
+    """The channel-pair depthwise forward (dwconv_fwd_p2_kernel) writes bitwise the one-channel-per-lane kernel's y;
+    its f64 BatchNorm sums (atomics: order varies) agree to 1e-12 relative."""
+    K = _K()
+    g = torch.Generator().manual_seed(B * T + d + k + 29)
+    x = torch.randn(B * T, d, generator=g).cuda()
+    w = torch.randn(d, k, generator=g).cuda()
+    bias = torch.randn(d, generator=g).cuda()
+    outs = []
+    for flag in ("0", "2"):
+        monkeypatch.setenv("KDFM_DWC_P2", flag)
+        y = torch.empty(B * T, d, device="cuda")
+        stats = torch.zeros(2 * d, dtype=torch.float64, device="cuda")
+        K.dwconv_fwd(x, w, bias, y, stats, B, T, d, k)
+        y2 = torch.empty(B * T, d, device="cuda")
+        K.dwconv_fwd(x, w, None, y2, None, B, T, d, k)
+        outs.append((y, stats, y2))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][2], outs[1][2])
+    torch.testing.assert_close(outs[1][1], outs[0][1], rtol=1e-12, atol=1e-9)

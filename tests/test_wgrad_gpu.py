@@ -325,3 +325,49 @@ def test_deferred_folds_bitwise():
     K.wgrad_set_fold_arena(None)
     torch.cuda.synchronize()
     assert torch.equal(dWi, dWd) and torch.equal(dbi, dbd)
+
+
+@pytest.mark.parametrize("R,M,N", [(12832, 88, 1760), (25600, 88, 792), (12831, 96, 800)])
+def test_xcd_grouped_slices_bitwise(R, M, N, monkeypatch):
+    """The XCD-grouped dispatch order of multi-slice products (WrGeo::xgrp: a split's column slices on one
+    XCD) renumbers the grid, nothing else: bitwise the plain order's result, single and paired launches,
+    and the 3x3 stride-2 gather (conv2's weight gradient, 3 column slices)."""
+    from kdfm import kernels as K
+    g = torch.Generator(device="cuda").manual_seed(R + 5 * N)
+    dy = torch.randn(R, M, device="cuda", generator=g).to(torch.bfloat16)
+    x = torch.randn(R, N, device="cuda", generator=g).to(torch.bfloat16)
+    dy2 = torch.randn(R, M, device="cuda", generator=g).to(torch.bfloat16)
+    x2 = torch.randn(R, N, device="cuda", generator=g).to(torch.bfloat16)
+    out = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("KDFM_WGR_XGRP", flag)
+        dW, db = torch.zeros(M, N, device="cuda"), torch.zeros(M, device="cuda")
+        K.wgrad_bf16(dy, x, dW, db=db, alpha=0.5)
+        dWa, dba = torch.zeros(M, N, device="cuda"), torch.zeros(M, device="cuda")
+        dWb, dbb = torch.zeros(M, N, device="cuda"), torch.zeros(M, device="cuda")
+        K.wgrad_bf16_pair(dy, x, dWa, dba, dy2, x2, dWb, dbb, alpha=0.5)
+        out.append((dW, db, dWa, dba, dWb, dbb))
+    torch.cuda.synchronize()
+    rw = 0.5 * (dy.double().T @ x.double())
+    assert (out[1][0].double() - rw).abs().max().item() <= 1e-5 * rw.abs().max().item() + 1e-6
+    for a, b in zip(out[0], out[1]):
+        assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("B,T1,F1", [(4, 801, 80), (3, 41, 40)])
+def test_xcd_grouped_s2conv_bitwise(B, T1, F1, monkeypatch):
+    from kdfm import kernels as K
+    C = 88
+    T2, F2 = (T1 - 1) // 2 + 1, (F1 - 1) // 2 + 1
+    g = torch.Generator().manual_seed(T1 + F1)
+    X = torch.randn(B * T1 * F1, C, generator=g).bfloat16().cuda()
+    dY = torch.randn(B * T2 * F2, C, generator=g).bfloat16().cuda()
+    lin = torch.tensor([T1 - 5 * b for b in range(B)], dtype=torch.int64).cuda()
+    out = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("KDFM_WGR_XGRP", flag)
+        dW, db = torch.zeros(C, 9 * C, device="cuda"), torch.zeros(C, device="cuda")
+        K.wgrad_bf16_s2conv(dY, X, lin, dW, db, B, T1, F1, C)
+        out.append((dW, db))
+    torch.cuda.synchronize()
+    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])

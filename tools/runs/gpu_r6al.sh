@@ -1,0 +1,15 @@
+# channel-pair depthwise backward: kernel tests, micro A/B, bench A/B (KDFM_DWC_P2)
+set -o pipefail
+OUT=gpurun_out/r6al
+mkdir -p $OUT
+export PYTHONUNBUFFERED=1
+timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_kernels_gpu.py > $OUT/tests.log 2>&1 || { echo tests failed; tail -30 $OUT/tests.log; exit 1; }
+tail -1 $OUT/tests.log
+timeout -k 10 200 python tools/dwconv_micro.py 20 > $OUT/micro.log 2>&1 || { cat $OUT/micro.log; exit 1; }
+cat $OUT/micro.log
+for f in 0 1 0 1; do
+  KDFM_DWC_P2=$f timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-f32-sensitivity > $OUT/bench_$f.log 2>&1 || { tail -20 $OUT/bench_$f.log; exit 1; }
+  echo "P2=$f $(grep -o '"value": [0-9.]*' $OUT/bench_$f.log | head -1) $(grep -o '"ms_per_step": [0-9.]*' $OUT/bench_$f.log | head -1)"
+done
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_step_parity_gpu.py tests/test_bench_shape_gpu.py > $OUT/step.log 2>&1 || { echo step failed; tail -30 $OUT/step.log; exit 1; }
+tail -1 $OUT/step.log
