@@ -29,7 +29,10 @@ from .overlap import WGRAD
 # the dispatcher hands freed CUs to the critical path first when both have workgroups waiting.
 # Off by default: measured 19.2 -> 25.8 ms per step on ROCm 7 (profiles/r02/prio_bench_*.log) --
 # the high-priority streams lose their overlap with each other.
-_PRIO = __import__("os").environ.get("KDFM_STREAM_PRIO", "0") == "1"
+# KDFM_STREAM_PRIO=compute[,side][,aux]: only the named roles high-priority (the round-6 A/B: the compute stream alone,
+# so the student chain takes freed CUs ahead of the teacher and the weight gradients)
+_PRIO_ENV = __import__("os").environ.get("KDFM_STREAM_PRIO", "0")
+_PRIO = {"compute", "side", "aux"} if _PRIO_ENV == "1" else {r for r in _PRIO_ENV.split(",") if r not in ("", "0")}
 
 
 # One stream per (device, role), shared by every engine of the process: torch hands out pool streams round-robin
@@ -44,7 +47,7 @@ def _crit_stream(dev, role):
     key = (str(torch.device(dev)), role)
     s = _STREAMS.get(key)
     if s is None:
-        s = _STREAMS[key] = torch.cuda.Stream(dev, priority=-1) if _PRIO else torch.cuda.Stream(dev)
+        s = _STREAMS[key] = torch.cuda.Stream(dev, priority=-1) if role in _PRIO else torch.cuda.Stream(dev)
     return s
 from .store import FlatStore, init_uniform
 
