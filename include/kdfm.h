@@ -238,11 +238,12 @@ int kdfm_wgrad_bf16_conv(const uint16_t* dY, const uint16_t* X, float* dW, int64
  * dY (B*T2*F2, C) bf16, T2 = (T1-1)/2+1, F2 = (F1-1)/2+1; dW (C, 9C) tap-major (kdfm_convw_grad re-lays it
  * out).  The same sums, split plan and fold order as kdfm_wgrad_bf16 over kdfm_im2col_3x3s2_tm_from_bf16's
  * columns (bitwise equal), without the column matrix's 9/4 x |X| write and read.  C % 8 == 0, F1 >= 7;
+ * ldx: X's row stride in elements (a multiple of 8, >= C; kdfm_subsample_fused's padded y1 rows);
  * ws: kdfm_wgrad_bf16_s2conv_ws floats (deferred folds apply). */
 int64_t kdfm_wgrad_bf16_s2conv_ws(int64_t B, int64_t T1, int64_t F1, int64_t C);
-int kdfm_wgrad_bf16_s2conv(const uint16_t* dY, const uint16_t* X, const int64_t* len_in, float* dW, float* db,
-                           int64_t B, int64_t T1, int64_t F1, int64_t C, float alpha, float* ws, int64_t ws_len,
-                           void* stream);
+int kdfm_wgrad_bf16_s2conv(const uint16_t* dY, const uint16_t* X, int64_t ldx, const int64_t* len_in, float* dW,
+                           float* db, int64_t B, int64_t T1, int64_t F1, int64_t C, float alpha, float* ws,
+                           int64_t ws_len, void* stream);
 /* Deferred folds of the row-parallel weight gradients (kdfm_wgrad_bf16 / _pair / _seg / _conv / _dev), per
  * stream: after kdfm_wgrad_set_fold_arena(stream, arena, len) the products issued on `stream` write their
  * per-split partials into `arena` (len floats, caller-owned, 16-byte aligned; ws is then unused) and queue
@@ -565,8 +566,9 @@ int kdfm_im2col_3x3s2(const float* X, const int64_t* len_in, float* cols, int64_
  * y2 = mask2(ReLU(conv2(mask1(ReLU(conv1(mask0(mel))))))) with conv1 / conv2 = Conv2d(3x3, stride 2,
  * pad 1), mel (B, Tm, F = 80) f32, y2 (B * T2 * 20, C) f32 channels-last rows; conv1 is computed on the
  * fly per workgroup (MFMA over hi/lo bf16 splits of the mel taps and weights, f32 accumulation) and never
- * leaves LDS, except that y1 (optional, (B * T1 * 40, C) bf16) receives the conv1 output for a trained
- * student's backward.  mel_len / len1 / len2 (optional): the frame masks.  wp: kdfm_subsample_fused_wprep's
+ * leaves LDS, except that y1 (optional, (B * T1 * 40, ldy1) bf16) receives the conv1 output for a trained
+ * student's backward: ldy1 a multiple of 8 in [C, 32 ceil(C / 32)], channels [C, ldy1) written as zeros (96 at
+ * C = 88: whole 64-byte row segments per 32-channel chunk).  y1, y2, wp 16-byte aligned.  mel_len / len1 / len2 (optional): the frame masks.  wp: kdfm_subsample_fused_wprep's
  * operand image of (w0 (C,1,3,3), w2 (C,C,3,3)), kdfm_subsample_fused_wprep_elems(C) bf16.
  * C in {88, 96, 176, 192} (kdfm_subsample_fused_supported). */
 int kdfm_subsample_fused_supported(int64_t C, int64_t F);
@@ -574,7 +576,7 @@ int64_t kdfm_subsample_fused_wprep_elems(int64_t C);
 int kdfm_subsample_fused_wprep(const float* w0, const float* w2, uint16_t* wp, int64_t C, void* stream);
 int kdfm_subsample_fused(const float* mel, const int64_t* mel_len, const int64_t* len1, const int64_t* len2,
                          const uint16_t* wp, const float* b0, const float* b2, float* y2, uint16_t* y1, int64_t B,
-                         int64_t Tm, int64_t F, int64_t C, void* stream);
+                         int64_t Tm, int64_t F, int64_t C, int64_t ldy1, void* stream);
 /* Tap-major bf16 columns: cols[(b,t2,f2), tap*C + c] = bf16(X[b, 2 t2 - 1 + ky, 2 f2 - 1 + kx, c]) (0 outside /
  * beyond len_in), C % 8 == 0; the bf16 step's conv2 weight-gradient operand. */
 /* the same tap-major bf16 columns from a bf16 source (the saved bf16 conv1 output y1) */
@@ -647,20 +649,21 @@ int kdfm_subsample_dgrad_wprep(const float* w2, uint16_t* wt, int64_t C, void* s
  * striding path: conv0 = Conv2d(1 -> C, 3x3, stride 2, pad) over the (B, Tm, Fm) mel frames, frames
  * t >= mel_len[b] read as zero; mel_len may be null): dw0 (C, 9) += sum dy1 x_patch, db0 (C) += sum dy1,
  * from per-workgroup partials in ws (kdfm_subsample_conv2_dgrad_w0_ws floats) folded in workgroup order.
- * dy1 may be null (not written).  Requires B T1 F1 < 2^24. */
+ * dy1 may be null (not written).  Requires B T1 F1 < 2^24.  ldy1 (>= C): y1's row stride in elements (the fused
+ * forward's padded rows); dy1 is (B T1 F1, C). */
 int64_t kdfm_subsample_conv2_dgrad_w0_ws(int64_t B, int64_t T1, int64_t F1, int64_t C);
 int kdfm_subsample_conv2_dgrad_w0(const float* dy2, const uint16_t* wt, const uint16_t* y1, float* dy1, int64_t B,
-                                  int64_t T1, int64_t F1, int64_t C, const float* mel, const int64_t* mel_len,
-                                  int64_t Tm, int64_t Fm, int64_t pad, float* dw0, float* db0, float* ws,
-                                  int64_t ws_len, void* stream);
+                                  int64_t T1, int64_t F1, int64_t C, int64_t ldy1, const float* mel,
+                                  const int64_t* mel_len, int64_t Tm, int64_t Fm, int64_t pad, float* dw0, float* db0,
+                                  float* ws, int64_t ws_len, void* stream);
 int kdfm_subsample_conv2_dgrad(const float* dy2, const uint16_t* wt, const uint16_t* y1, float* dy1, int64_t B, int64_t T1,
-                               int64_t F1, int64_t C, void* stream);
+                               int64_t F1, int64_t C, int64_t ldy1, void* stream);
 /* The same with a bf16 dy2 (kdfm_ss_out_dgrad's output): one 16-byte load of 8 channels per k-step instead of
  * two f32 ones (the tap re-reads of dy2 are the kernel's dominant traffic). */
 int kdfm_subsample_conv2_dgrad_w0_h(const uint16_t* dy2h, const uint16_t* wt, const uint16_t* y1, float* dy1, int64_t B,
-                                    int64_t T1, int64_t F1, int64_t C, const float* mel, const int64_t* mel_len,
-                                    int64_t Tm, int64_t Fm, int64_t pad, float* dw0, float* db0, float* ws,
-                                    int64_t ws_len, void* stream);
+                                    int64_t T1, int64_t F1, int64_t C, int64_t ldy1, const float* mel,
+                                    const int64_t* mel_len, int64_t Tm, int64_t Fm, int64_t pad, float* dw0, float* db0,
+                                    float* ws, int64_t ws_len, void* stream);
 /* Subsampling output Linear(C F2 -> d) backward into the conv2 output gradient (replaces linear_dx with the
  * DRELU epilogue + a bf16 cast; conformer_encoder.py:381-390 ConvSubsampling.out): with the channels-last
  * conv2 output y2 (rows, ncols = F2 C) f32 and dlin (rows, d) f32,

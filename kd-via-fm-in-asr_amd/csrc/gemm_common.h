@@ -37,6 +37,7 @@ struct GemmP {
   // (b, t2, f2) reads X[b][2 t2 - 1 + tap / 3][2 f2 - 1 + tap % 3][c] of a (B, c2_T1, c2_F1, conv_c) image, zero
   // outside it and at frames >= c2_len[b] (c2_len NULL: no length mask)
   int64_t c2_T1, c2_F1, c2_T2, c2_F2; const int64_t* c2_len;
+  int64_t c2_ld;   // the image's row stride (elements, >= conv_c)
 };
 
 // Non-atomic epilogue for one output element.  v = alpha * acc (already scaled).  bz = batch

@@ -55,8 +55,9 @@ struct FsArgs {
   const uint16_t* w2p;         // conv2 B operand [9 taps][NCH chunks][NPAD co][32 ci] bf16
   const float* b2;
   float* y2;                   // (B*T2*F2, C) f32
-  uint16_t* y1;                // optional (B*T1*F1, C) bf16
+  uint16_t* y1;                // optional (B*T1*F1, ldy1) bf16, channels [C, ldy1) written as zeros
   int B, Tm, F, T1, F1, T2, F2;
+  int ldy1;                    // y1 row stride (elements): C <= ldy1 <= NCH * 32, a multiple of 8
 };
 
 __device__ __forceinline__ float bf_round(float x) { return (float)(__bf16)x; }
@@ -233,8 +234,8 @@ __global__ __launch_bounds__(FS_NT, 1) void ss_fused_kernel(FsArgs a) {
         const int g = u & 3, pos = u >> 2;
         const int i = 1 + pos / 40, f1 = pos - (pos / 40) * 40;
         const int t1 = t1a + i, ch = c * FS_CK + 8 * g;
-        if (t1 < a.T1 && ch < C)
-          *reinterpret_cast<bf16x8*>(a.y1 + (((int64_t)b * a.T1 + t1) * a.F1 + f1) * C + ch) =
+        if (t1 < a.T1 && ch < a.ldy1)
+          *reinterpret_cast<bf16x8*>(a.y1 + (((int64_t)b * a.T1 + t1) * a.F1 + f1) * a.ldy1 + ch) =
               *reinterpret_cast<const bf16x8*>(y1s + (i * FS_F1C + f1 + 1) * FS_CKP + 8 * g);
       }
     }
@@ -284,7 +285,12 @@ __global__ __launch_bounds__(FS_NT, 1) void ss_fused_kernel(FsArgs a) {
   }
   KPROBE(30);
 
-  // ---- epilogue: bias + ReLU + len2 mask, f32 rows (b, t2, f2) x C
+  // ---- epilogue: bias + ReLU + len2 mask, f32 rows (b, t2, f2) x C.  The workgroup's output rows are ONE
+  // contiguous range of y2 (utterance b, rows t2a .. t2a + R - 1, all 20 columns, all C channels): the tile goes
+  // through LDS (dead after the last chunk's barrier) and leaves as 16-byte stores over that range, whole
+  // 64-byte segments, instead of the accumulators' 64-byte column runs (a 352-byte row at C = 88 puts half of
+  // those across two segments)
+  float* ys = reinterpret_cast<float*>(fs_lds);   // [MROWS][C]
 #pragma unroll
   for (int j = 0; j < NT; ++j) {
     const int n = (wn * NT + j) * 16 + r16;
@@ -294,13 +300,21 @@ __global__ __launch_bounds__(FS_NT, 1) void ss_fused_kernel(FsArgs a) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int p = (wm * MT + i) * 16 + 4 * kq + e;
-        const int t2 = t2a + p / FS_F2, f2 = p - (p / FS_F2) * FS_F2;
-        if (p < MROWS && t2 < a.T2 && n < C) {
+        const int t2 = t2a + p / FS_F2;
+        if (p < MROWS && n < C) {
           const float v = fmaxf(acc[i][j][e] + bn, 0.f);
-          a.y2[(((int64_t)b * a.T2 + t2) * a.F2 + f2) * C + n] = t2 < l2 ? v : 0.f;
+          ys[p * C + n] = t2 < l2 ? v : 0.f;
         }
       }
     }
+  }
+  __syncthreads();
+  {
+    const int nr = min(R, a.T2 - t2a) * FS_F2;   // rows of this workgroup inside the utterance
+    const int n4 = nr * C / 4;
+    float4* dst = reinterpret_cast<float4*>(a.y2 + ((int64_t)b * a.T2 + t2a) * a.F2 * C);
+    const float4* src = reinterpret_cast<const float4*>(ys);
+    for (int u = threadIdx.x; u < n4; u += FS_NT) dst[u] = src[u];
   }
   KPROBE(31);
 }
@@ -311,7 +325,9 @@ int fs_launch(const FsArgs& a, hipStream_t st) {
   constexpr int Y1_BYTES = ((NPT * 16 * FS_CKP * 2 + 1023) / 1024) * 1024;
   constexpr int NPAD = NT * 16 * WN, WS_BYTES = 9 * NPAD * FS_CK * 2;
   constexpr size_t base = (size_t)Y1_BYTES + (size_t)NPT * 1024;
-  constexpr size_t lds = base + (base + WS_BYTES <= 160 * 1024 ? (size_t)WS_BYTES : 0);   // STAGEB (kernel)
+  constexpr size_t lds0 = base + (base + WS_BYTES <= 160 * 1024 ? (size_t)WS_BYTES : 0);   // STAGEB (kernel)
+  constexpr size_t Y2_BYTES = (size_t)FS_F2 * R * C * 4;   // the epilogue's output tile
+  constexpr size_t lds = lds0 > Y2_BYTES ? lds0 : Y2_BYTES;
   static_assert(lds <= 160 * 1024, "LDS");
   static bool once = [] {
     (void)hipFuncSetAttribute((const void*)ss_fused_kernel<C, R, WM, WN, MT, NT>,
@@ -390,19 +406,22 @@ int kdfm_subsample_fused_wprep(const float* w0, const float* w2, uint16_t* wp, i
 
 int kdfm_subsample_fused(const float* mel, const int64_t* mel_len, const int64_t* len1, const int64_t* len2,
                          const uint16_t* wp, const float* b0, const float* b2, float* y2, uint16_t* y1, int64_t B,
-                         int64_t Tm, int64_t F, int64_t C, void* stream) {
+                         int64_t Tm, int64_t F, int64_t C, int64_t ldy1, void* stream) {
   using namespace kdfm;
   KDFM_REQUIRE(mel && wp && b0 && b2 && y2, "null pointer");
   int nch, npad;
   KDFM_REQUIRE(F == 80 && fs_config(C, nch, npad), "unsupported shape (F = 80, C in {88, 96, 176, 192})");
   KDFM_REQUIRE(B > 0 && Tm > 0, "empty batch");
-  KDFM_REQUIRE(((((uintptr_t)wp) | ((uintptr_t)y1)) & 15) == 0, "wp / y1 must be 16-byte aligned");
+  KDFM_REQUIRE(((((uintptr_t)wp) | ((uintptr_t)y1) | ((uintptr_t)y2)) & 15) == 0, "wp / y1 / y2 must be 16-byte aligned");
+  KDFM_REQUIRE(y1 == nullptr || (ldy1 >= C && ldy1 <= nch * 32 && ldy1 % 8 == 0),
+               "ldy1 must be a multiple of 8 in [C, 32 * ceil(C / 32)]");
   FsArgs a;
   a.mel = mel; a.mel_len = mel_len; a.len1 = len1; a.len2 = len2;
   a.w1p = wp; a.b0 = b0; a.w2p = wp + (int64_t)nch * 32 * 32; a.b2 = b2; a.y2 = y2; a.y1 = y1;
   a.B = (int)B; a.Tm = (int)Tm; a.F = (int)F;
   a.T1 = (int)((Tm - 1) / 2 + 1); a.F1 = (int)((F - 1) / 2 + 1);
   a.T2 = (a.T1 - 1) / 2 + 1; a.F2 = (a.F1 - 1) / 2 + 1;
+  a.ldy1 = (int)(y1 ? ldy1 : C);
   KDFM_REQUIRE(a.F2 == FS_F2, "F2 must be 20");
   hipStream_t st = as_stream(stream);
   switch (C) {

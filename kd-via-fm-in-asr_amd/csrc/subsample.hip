@@ -272,6 +272,7 @@ struct SdGeo {
   // wpart[wg][C * 9 + C] = (sum dy1 x_patch | sum dy1), folded in workgroup order on the host side
   const float* mel; const int64_t* mel_len; int Tm, Fm, pad; float* wpart;
   const uint16_t* wt;   // tap slabs [tap][ci (Np)][co (Cp)] bf16 (ss_dgrad_wprep)
+  int ldy;              // y1 row stride (elements, >= C: the fused forward's padded rows)
 };
 
 __global__ __launch_bounds__(256) void ss_dgrad_wprep_kernel(const float* __restrict__ W, uint16_t* __restrict__ wt,
@@ -401,6 +402,7 @@ __device__ __forceinline__ void sd_class(const SdGeo& g, __amdgpu_buffer_rsrc_t 
     // y1 row indices of the accumulator rows (positions 8 (e / 4) + 4 h + e % 4) and their ReLU' masks
     auto rows4 = [&](int q) { return *reinterpret_cast<const int4*>(mp + 8 * q + 4 * h); };
     uint32_t mask[NCT];
+    const uint32_t ldy2 = 2u * (uint32_t)g.ldy;   // y1 row stride in bytes
 #pragma unroll
     for (int n = 0; n < NCT; ++n) mask[n] = 0;
 #pragma unroll
@@ -412,7 +414,7 @@ __device__ __forceinline__ void sd_class(const SdGeo& g, __amdgpu_buffer_rsrc_t 
         const int ci = 32 * n + r;
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          const uint32_t o = (mq[u] >= 0 && ci < g.C) ? (uint32_t)(mq[u] * g.C + ci) * 2u : SD_OOB;
+          const uint32_t o = (mq[u] >= 0 && ci < g.C) ? (uint32_t)mq[u] * ldy2 + 2u * (uint32_t)ci : SD_OOB;
           const uint16_t yb = __builtin_amdgcn_raw_buffer_load_b16(ry1, o, 0, 0);
           mask[n] |= ((yb & 0x7fff) != 0 && !(yb & 0x8000)) ? (1u << (4 * q + u)) : 0u;   // ReLU' from the bf16 sign
         }
@@ -506,7 +508,7 @@ __global__ __launch_bounds__(SS_NT, 1) void ss_dgrad_kernel(const void* __restri
   const __amdgpu_buffer_rsrc_t rdy2 =
       __builtin_amdgcn_make_buffer_rsrc((void*)dy2, (short)0, (int)((int64_t)g.B * g.T2 * g.F2 * g.C * (DBF ? 2 : 4)), 0x00020000);
   const __amdgpu_buffer_rsrc_t ry1 =
-      __builtin_amdgcn_make_buffer_rsrc((void*)y1, (short)0, (int)((int64_t)g.B * g.T1 * g.F1 * g.C * 2), 0x00020000);
+      __builtin_amdgcn_make_buffer_rsrc((void*)y1, (short)0, (int)((int64_t)g.B * g.T1 * g.F1 * g.ldy * 2), 0x00020000);
   const __amdgpu_buffer_rsrc_t rdy1 = __builtin_amdgcn_make_buffer_rsrc(
       (void*)dy1, (short)0, dy1 ? (int)((int64_t)g.B * g.T1 * g.F1 * g.C * 4) : 0, 0x00020000);
   float wacc[NCT][10];
@@ -722,6 +724,7 @@ namespace kdfm {
 namespace {
 int sd_geo(SdGeo& g, int64_t B, int64_t T1, int64_t F1, int64_t C) {
   g.B = (int)B; g.T1 = (int)T1; g.F1 = (int)F1; g.C = (int)C;
+  g.ldy = (int)C;
   g.T2 = (int)((T1 - 1) / 2 + 1); g.F2 = (int)((F1 - 1) / 2 + 1);
   g.Cp = (int)(ceil_div(C, 16) * 16);
   g.ldb = g.Cp + 8;
@@ -761,15 +764,18 @@ namespace kdfm {
 namespace {
 template <bool DBF>
 int sd_w0(const void* dy2, const uint16_t* wt, const uint16_t* y1, float* dy1, int64_t B, int64_t T1, int64_t F1,
-          int64_t C, const float* mel, const int64_t* mel_len, int64_t Tm, int64_t Fm, int64_t pad, float* dw0,
+          int64_t C, int64_t ldy1, const float* mel, const int64_t* mel_len, int64_t Tm, int64_t Fm, int64_t pad, float* dw0,
           float* db0, float* ws, int64_t ws_len, void* stream) {
   KDFM_REQUIRE(dy2 && wt && y1 && mel && dw0 && db0 && ws, "null pointer");
   KDFM_REQUIRE(C % 8 == 0 && B > 0 && T1 > 0 && F1 > 0, "C must be a multiple of 8");
   KDFM_REQUIRE(((((uintptr_t)dy2) | ((uintptr_t)wt)) & 15) == 0, "dy2 / wt must be 16-byte aligned");
   KDFM_REQUIRE(T1 == (Tm + 2 * pad - 3) / 2 + 1 && F1 == (Fm + 2 * pad - 3) / 2 + 1, "conv0 geometry");
+  KDFM_REQUIRE(ldy1 >= C, "ldy1 < C");
   SdGeo g;
   sd_geo(g, B, T1, F1, C);
-  KDFM_REQUIRE(g.wg0[4] < (1ll << 31) && B * T1 * F1 * C * 4 < (1ll << 31) && B * Tm * Fm < (1ll << 31),
+  g.ldy = (int)ldy1;
+  KDFM_REQUIRE(g.wg0[4] < (1ll << 31) && B * T1 * F1 * C * 4 < (1ll << 31) && B * T1 * F1 * ldy1 * 2 < (1ll << 31) &&
+               B * Tm * Fm < (1ll << 31),
                "too large (32-bit buffer offsets: dy1 / y1 / dy2 < 2 GiB)");
   KDFM_REQUIRE(ws_len >= g.wg0[4] * C * 10, "workspace too small (kdfm_subsample_conv2_dgrad_w0_ws)");
   g.mel = mel; g.mel_len = mel_len; g.Tm = (int)Tm; g.Fm = (int)Fm; g.pad = (int)pad; g.wpart = ws;
@@ -785,28 +791,30 @@ int sd_w0(const void* dy2, const uint16_t* wt, const uint16_t* y1, float* dy1, i
 extern "C" {
 
 int kdfm_subsample_conv2_dgrad_w0(const float* dy2, const uint16_t* wt, const uint16_t* y1, float* dy1, int64_t B,
-                                  int64_t T1, int64_t F1, int64_t C, const float* mel, const int64_t* mel_len,
+                                  int64_t T1, int64_t F1, int64_t C, int64_t ldy1, const float* mel, const int64_t* mel_len,
                                   int64_t Tm, int64_t Fm, int64_t pad, float* dw0, float* db0, float* ws,
                                   int64_t ws_len, void* stream) {
-  return kdfm::sd_w0<false>(dy2, wt, y1, dy1, B, T1, F1, C, mel, mel_len, Tm, Fm, pad, dw0, db0, ws, ws_len, stream);
+  return kdfm::sd_w0<false>(dy2, wt, y1, dy1, B, T1, F1, C, ldy1, mel, mel_len, Tm, Fm, pad, dw0, db0, ws, ws_len, stream);
 }
 
 int kdfm_subsample_conv2_dgrad_w0_h(const uint16_t* dy2h, const uint16_t* wt, const uint16_t* y1, float* dy1, int64_t B,
-                                    int64_t T1, int64_t F1, int64_t C, const float* mel, const int64_t* mel_len,
+                                    int64_t T1, int64_t F1, int64_t C, int64_t ldy1, const float* mel, const int64_t* mel_len,
                                     int64_t Tm, int64_t Fm, int64_t pad, float* dw0, float* db0, float* ws,
                                     int64_t ws_len, void* stream) {
-  return kdfm::sd_w0<true>(dy2h, wt, y1, dy1, B, T1, F1, C, mel, mel_len, Tm, Fm, pad, dw0, db0, ws, ws_len, stream);
+  return kdfm::sd_w0<true>(dy2h, wt, y1, dy1, B, T1, F1, C, ldy1, mel, mel_len, Tm, Fm, pad, dw0, db0, ws, ws_len, stream);
 }
 
 int kdfm_subsample_conv2_dgrad(const float* dy2, const uint16_t* wt, const uint16_t* y1, float* dy1, int64_t B, int64_t T1,
-                               int64_t F1, int64_t C, void* stream) {
+                               int64_t F1, int64_t C, int64_t ldy1, void* stream) {
   using namespace kdfm;
   KDFM_REQUIRE(dy2 && wt && y1 && dy1, "null pointer");
   KDFM_REQUIRE(C % 8 == 0 && B > 0 && T1 > 0 && F1 > 0, "C must be a multiple of 8");
+  KDFM_REQUIRE(ldy1 >= C, "ldy1 < C");
   KDFM_REQUIRE(((((uintptr_t)dy2) | ((uintptr_t)wt)) & 15) == 0, "dy2 / wt must be 16-byte aligned");
   SdGeo g;
   sd_geo(g, B, T1, F1, C);
-  KDFM_REQUIRE(g.wg0[4] < (1ll << 31) && B * T1 * F1 * C * 4 < (1ll << 31),
+  g.ldy = (int)ldy1;
+  KDFM_REQUIRE(g.wg0[4] < (1ll << 31) && B * T1 * F1 * C * 4 < (1ll << 31) && B * T1 * F1 * ldy1 * 2 < (1ll << 31),
                "too large (32-bit buffer offsets: dy1 / y1 / dy2 < 2 GiB)");
   return sd_dispatch<false>(dy2, wt, y1, dy1, g, as_stream(stream));
 }

@@ -256,7 +256,7 @@ __global__ __launch_bounds__(WR_NT, 2) void wgr_kernel(GemmP p, WrGeo g) {
             const int lim = bb == c2b[i] ? c2l0[i] : c2l1[i];
             ok = ok && t1 >= 0 && t1 < lim && f1 >= 0 && f1 < p.c2_F1;
             q = ok ? reinterpret_cast<const char*>(pB) +
-                         ES * ((((int64_t)bb * p.c2_T1 + t1) * p.c2_F1 + f1) * p.conv_c + c2c[i])
+                         ES * ((((int64_t)bb * p.c2_T1 + t1) * p.c2_F1 + f1) * p.c2_ld + c2c[i])
                    : reinterpret_cast<const char*>(pB);
           }
         }
@@ -1356,12 +1356,13 @@ int64_t kdfm_wgrad_bf16_s2conv_ws(int64_t B, int64_t T1, int64_t F1, int64_t C) 
   return pl.S * p.M * p.N;
 }
 
-int kdfm_wgrad_bf16_s2conv(const uint16_t* dY, const uint16_t* X, const int64_t* len_in, float* dW, float* db,
-                           int64_t B, int64_t T1, int64_t F1, int64_t C, float alpha, float* ws, int64_t ws_len,
-                           void* stream) {
+int kdfm_wgrad_bf16_s2conv(const uint16_t* dY, const uint16_t* X, int64_t ldx, const int64_t* len_in, float* dW,
+                           float* db, int64_t B, int64_t T1, int64_t F1, int64_t C, float alpha, float* ws,
+                           int64_t ws_len, void* stream) {
   using namespace kdfm;
   KDFM_REQUIRE(dY && X && dW && db && ws, "null pointer");
   KDFM_REQUIRE(B > 0 && T1 > 0 && F1 >= 7 && C > 0 && C % 8 == 0, "B, T1 > 0, F1 >= 7, C a positive multiple of 8");
+  KDFM_REQUIRE(ldx >= C && ldx % 8 == 0, "ldx must be a multiple of 8, >= C");
   KDFM_REQUIRE(((((uintptr_t)dY) | ((uintptr_t)X)) & 15) == 0, "operands must be 16-byte aligned");
   const int64_t T2 = (T1 - 1) / 2 + 1, F2 = (F1 - 1) / 2 + 1;
   GemmP p = wgrad_bf16_params(dY, X, dW, 9 * C, db, B * T2 * F2, C, 9 * C, alpha, ws, ws_len);
@@ -1371,6 +1372,7 @@ int kdfm_wgrad_bf16_s2conv(const uint16_t* dY, const uint16_t* X, const int64_t*
   p.c2_T2 = T2;
   p.c2_F2 = F2;
   p.c2_len = len_in;
+  p.c2_ld = ldx;
   return wgrad_bf16_run(p, WR_LD_C2D, as_stream(stream));
 }
 

@@ -123,7 +123,7 @@ SIGNATURES: dict[str, tuple] = {
     "kdfm_wgrad_bf16_seg": (_i32, [P, P, P, _i64, P, _i64, _i64, _i64, _i64, _f32, P, _i64, P]),
     "kdfm_wgrad_bf16_conv_ws": (_i64, [_i64, _i64, _i64, _i32, _i32, _i64, _i32]),
     "kdfm_wgrad_bf16_s2conv_ws": (_i64, [_i64, _i64, _i64, _i64]),
-    "kdfm_wgrad_bf16_s2conv": (_i32, [P, P, P, P, P, _i64, _i64, _i64, _i64, _f32, P, _i64, P]),
+    "kdfm_wgrad_bf16_s2conv": (_i32, [P, P, _i64, P, P, P, _i64, _i64, _i64, _i64, _f32, P, _i64, P]),
     "kdfm_wgrad_bf16_conv": (_i32, [P, P, P, _i64, P, _i64, _i64, _i64, _i32, _i32, _i64, _f32, P, _i64, P]),
     "kdfm_wgrad_set_fold_arena": (_i32, [P, P, _i64]),
     "kdfm_wgrad_fold_flush": (_i32, [P]),
@@ -133,12 +133,12 @@ SIGNATURES: dict[str, tuple] = {
     "kdfm_denoise_wimg_elems": (_i64, []),
     "kdfm_subsample_dgrad_wprep_elems": (_i64, [_i64]),
     "kdfm_subsample_dgrad_wprep": (_i32, [P, P, _i64, P]),
-    "kdfm_subsample_conv2_dgrad": (_i32, [P, P, P, P, _i64, _i64, _i64, _i64, P]),
+    "kdfm_subsample_conv2_dgrad": (_i32, [P, P, P, P, _i64, _i64, _i64, _i64, _i64, P]),
     "kdfm_subsample_conv2_dgrad_w0_ws": (_i64, [_i64, _i64, _i64, _i64]),
-    "kdfm_subsample_conv2_dgrad_w0": (_i32, [P, P, P, P, _i64, _i64, _i64, _i64, P, P, _i64, _i64, _i64, P, P, P, _i64,
-                                              P]),
-    "kdfm_subsample_conv2_dgrad_w0_h": (_i32, [P, P, P, P, _i64, _i64, _i64, _i64, P, P, _i64, _i64, _i64, P, P, P, _i64,
-                                              P]),
+    "kdfm_subsample_conv2_dgrad_w0": (_i32, [P, P, P, P, _i64, _i64, _i64, _i64, _i64, P, P, _i64, _i64, _i64, P, P, P,
+                                              _i64, P]),
+    "kdfm_subsample_conv2_dgrad_w0_h": (_i32, [P, P, P, P, _i64, _i64, _i64, _i64, _i64, P, P, _i64, _i64, _i64, P, P, P,
+                                                _i64, P]),
     "kdfm_ss_out_wprep_elems": (_i64, [_i64, _i64]),
     "kdfm_ss_out_wprep": (_i32, [P, P, _i64, _i64, P]),
     "kdfm_ss_out_dgrad": (_i32, [P, P, P, P, _i64, _i64, _i64, P]),
@@ -181,7 +181,7 @@ SIGNATURES: dict[str, tuple] = {
     "kdfm_subsample_fused_supported": (_i32, [_i64, _i64]),
     "kdfm_subsample_fused_wprep_elems": (_i64, [_i64]),
     "kdfm_subsample_fused_wprep": (_i32, [P, P, P, _i64, P]),
-    "kdfm_subsample_fused": (_i32, [P, P, P, P, P, P, P, P, P, _i64, _i64, _i64, _i64, P]),
+    "kdfm_subsample_fused": (_i32, [P, P, P, P, P, P, P, P, P, _i64, _i64, _i64, _i64, _i64, P]),
     "kdfm_ctc_greedy": (_i32, [P, _i64, P, P, P, P, _i64, _i64, _i64, _i64, _i32, P]),
     "kdfm_edit_distance": (_i64, [P, _i64, P, _i64]),
     "kdfm_layernorm_fwd": (_i32, [P, P, P, P, P, P, _i64, _i64, _f32, P]),

@@ -229,6 +229,9 @@ def _side(fn, *keep):
         fn()
 
 
+# KDFM_SS_Y1_PAD=0: the fused subsampling forward's bf16 y1 rows unpadded (C channels; A/B switch)
+_SS_Y1_PAD = __import__("os").environ.get("KDFM_SS_Y1_PAD", "1") == "1"
+
 # KDFM_BN_ON_LOAD=0: the BN-SiLU backward's elementwise half as its own launch (A/B switch)
 _BN_ON_LOAD = __import__("os").environ.get("KDFM_BN_ON_LOAD", "1") == "1"
 
@@ -248,7 +251,10 @@ def subsampling_forward(cfg, S: EncoderShapes, P, pre, mel, mel_len, len1, len2,
         # one kernel (csrc/ssfused.hip): conv1 computed per workgroup into LDS (MFMA over hi/lo bf16 splits),
         # conv2 as an implicit GEMM over it; y1 reaches HBM only as the trained student's bf16 side output
         # (the backward's ReLU' sign and conv2 weight-gradient columns)
-        y1b = torch.empty(B * S.T1 * S.F1, C, device=dev, dtype=torch.bfloat16) if save else None
+        # y1 rows padded to whole 32-channel chunks (96 at C = 88; zeros past C): each chunk's stores are then
+        # whole 64-byte segments instead of runs straddling the 176-byte rows (KDFM_SS_Y1_PAD=0: unpadded)
+        ldy1 = -(-C // 32) * 32 if _SS_Y1_PAD else C
+        y1b = torch.empty(B * S.T1 * S.F1, ldy1, device=dev, dtype=torch.bfloat16) if save else None
         wp = ws["ss_fused_w"]
         K.subsample_fused_wprep(P[pre + "pre_encode.conv.0.weight"], P[pre + "pre_encode.conv.2.weight"], wp)
         K.subsample_fused(mel, m0, m1, m2, wp, P[pre + "pre_encode.conv.0.bias"], P[pre + "pre_encode.conv.2.bias"],
@@ -334,7 +340,7 @@ def subsampling_backward(cfg, S: EncoderShapes, P, G, pre, ctx, dx, len1, *, see
         WGRAD.run(conv2_wgrad, *(t for t in (dy2, cols1, dy2h, y1, len1) if t is not None))
     else:
         if ctx["y1"] is not None and ctx["y1"].dtype == torch.bfloat16:   # fused forward kept only the bf16 y1
-            ctx["y1"] = ctx["y1"].float()
+            ctx["y1"] = ctx["y1"][:, :C].float().contiguous()
         cols1 = ctx["cols1"]
         rebuild = cols1 is None
         if rebuild:   # fused forward: the im2col operand of the conv2 weight gradient is rebuilt on the

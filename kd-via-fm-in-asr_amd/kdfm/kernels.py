@@ -1348,12 +1348,22 @@ def wgrad_bf16_conv(dY, X, dW, T, *, taps=3, pad=1, db=None, alpha=1.0):
          taps, pad, T, float(alpha), ptr(ws), ws.numel(), _s())
 
 
+def _img_ld(X, npos, C, what):
+    """Row stride of a channels-last image of npos positions whose rows may be padded past C channels
+    (kdfm_subsample_fused writes y1 rows of 32 ceil(C / 32) channels)."""
+    ld = X.numel() // max(npos, 1)
+    if ld * npos != X.numel() or ld < C or ld % 8 and ld != C:
+        raise _lib.KdfmError(f"{what}: {X.numel()} elements are not {npos} rows of >= {C} channels")
+    return ld
+
+
 def wgrad_bf16_s2conv(dY, X, len_in, dW, db, B, T1, F1, C, *, alpha=1.0):
-    """Striding subsampling conv2 weight gradient straight from its bf16 input X (B, T1, F1, C) (no column
+    """Striding subsampling conv2 weight gradient straight from its bf16 input X (B, T1, F1, ldx >= C) (no column
     matrix): dW (C, 9C) tap-major += alpha * sum dY[(b,t2,f2), m] X[b, 2t2-1+tap//3, 2f2-1+tap%3, c], db += colsum."""
     T2, F2 = (T1 - 1) // 2 + 1, (F1 - 1) // 2 + 1
     rows = B * T2 * F2
-    assert dY.shape == (rows, C) and X.numel() == B * T1 * F1 * C and dW.shape == (C, 9 * C) and dW.is_contiguous()
+    ldx = _img_ld(X, B * T1 * F1, C, "wgrad_bf16_s2conv X")
+    assert dY.shape == (rows, C) and dW.shape == (C, 9 * C) and dW.is_contiguous()
     assert dY.is_contiguous() and X.is_contiguous() and db is not None
     n = int(_lib.lib().kdfm_wgrad_bf16_s2conv_ws(B, T1, F1, C))
     if n < 0:
@@ -1361,7 +1371,7 @@ def wgrad_bf16_s2conv(dY, X, len_in, dW, db, B, T1, F1, C, *, alpha=1.0):
     ws = scratch(dY.device, n)
     # algorithmic bytes: dY and X once (bf16), the f32 gradient read + written
     _traced("wgrad_bf16", 2.0 * rows * C * 9 * C, 2.0 * (rows * C + B * T1 * F1 * C) + 8.0 * 9 * C * C,
-            "kdfm_wgrad_bf16_s2conv", ptr(_bf16(dY)), ptr(_bf16(X)), ptr(_i64(len_in)), ptr(_f32(dW)), ptr(_f32(db)),
+            "kdfm_wgrad_bf16_s2conv", ptr(_bf16(dY)), ptr(_bf16(X)), ldx, ptr(_i64(len_in)), ptr(_f32(dW)), ptr(_f32(db)),
             B, T1, F1, C, float(alpha), ptr(ws), ws.numel(), _s())
 
 
@@ -1470,16 +1480,17 @@ def subsample_fused_wprep(w0, w2, wp):
 
 
 def subsample_fused(mel, mel_len, len1, len2, wp, b0, b2, y2, y1, B, Tm, F, Cc):
-    """Striding subsampling forward in one kernel: y2 (B*T2*F2, C) f32; y1 (optional, (B*T1*F1, C) bf16)
-    receives the conv1 output (kdfm_subsample_fused)."""
+    """Striding subsampling forward in one kernel: y2 (B*T2*F2, C) f32; y1 (optional, (B*T1*F1, ldy1) bf16, ldy1 in
+    [C, 32 ceil(C / 32)], the padding channels written as zeros) receives the conv1 output (kdfm_subsample_fused)."""
     T1, F1 = (Tm - 1) // 2 + 1, (F - 1) // 2 + 1
     T2, F2 = (T1 - 1) // 2 + 1, (F1 - 1) // 2 + 1
     assert mel.numel() == B * Tm * F and mel.is_contiguous() and wp.dtype == torch.bfloat16
     assert y2.numel() == B * T2 * F2 * Cc and y2.is_contiguous()
-    assert y1 is None or (y1.dtype == torch.bfloat16 and y1.numel() == B * T1 * F1 * Cc)
+    assert y1 is None or (y1.dtype == torch.bfloat16 and y1.is_contiguous())
+    ldy1 = Cc if y1 is None else _img_ld(y1, B * T1 * F1, Cc, "subsample_fused y1")
     assert b0.numel() == Cc and b2.numel() == Cc
     call("kdfm_subsample_fused", ptr(_f32(mel)), ptr(_i64(mel_len)), ptr(_i64(len1)), ptr(_i64(len2)), ptr(wp),
-         ptr(_f32(b0)), ptr(_f32(b2)), ptr(_f32(y2)), ptr(y1), B, Tm, F, Cc, _s())
+         ptr(_f32(b0)), ptr(_f32(b2)), ptr(_f32(y2)), ptr(y1), B, Tm, F, Cc, ldy1, _s())
 
 
 def subsample_dgrad_wprep_elems(Cc):
@@ -1492,8 +1503,9 @@ def subsample_conv2_dgrad_w0(dy2, wt, y1, B, T1, F1, Cc, mel, mel_len, Tm, Fm, p
     assert dw0.numel() == Cc * 9 and dw0.is_contiguous() and db0.numel() == Cc
     n = int(_lib.lib().kdfm_subsample_conv2_dgrad_w0_ws(B, T1, F1, Cc))
     ws = scratch(dy2.device, n)
+    ldy1 = _img_ld(y1, B * T1 * F1, Cc, "subsample_conv2_dgrad_w0 y1")
     call("kdfm_subsample_conv2_dgrad_w0", ptr(_f32(dy2)), ptr(wt), ptr(_bf16(y1, "y1 (bf16 conv1 output)")), ptr(dy1),
-         B, T1, F1, Cc, ptr(_f32(mel)), ptr(_i64(mel_len)), Tm, Fm, pad, ptr(_f32(dw0)), ptr(_f32(db0)), ptr(ws),
+         B, T1, F1, Cc, ldy1, ptr(_f32(mel)), ptr(_i64(mel_len)), Tm, Fm, pad, ptr(_f32(dw0)), ptr(_f32(db0)), ptr(ws),
          ws.numel(), _s())
 
 
@@ -1502,8 +1514,9 @@ def subsample_conv2_dgrad_w0_h(dy2h, wt, y1, B, T1, F1, Cc, mel, mel_len, Tm, Fm
     assert dw0.numel() == Cc * 9 and dw0.is_contiguous() and db0.numel() == Cc
     n = int(_lib.lib().kdfm_subsample_conv2_dgrad_w0_ws(B, T1, F1, Cc))
     ws = scratch(dy2h.device, n)
+    ldy1 = _img_ld(y1, B * T1 * F1, Cc, "subsample_conv2_dgrad_w0_h y1")
     call("kdfm_subsample_conv2_dgrad_w0_h", ptr(_bf16(dy2h, "dy2h")), ptr(wt), ptr(_bf16(y1, "y1 (bf16 conv1 output)")),
-         ptr(dy1), B, T1, F1, Cc, ptr(_f32(mel)), ptr(_i64(mel_len)), Tm, Fm, pad, ptr(_f32(dw0)), ptr(_f32(db0)),
+         ptr(dy1), B, T1, F1, Cc, ldy1, ptr(_f32(mel)), ptr(_i64(mel_len)), Tm, Fm, pad, ptr(_f32(dw0)), ptr(_f32(db0)),
          ptr(ws), ws.numel(), _s())
 
 
@@ -1541,9 +1554,10 @@ def subsample_conv2_dgrad(dy2, wt, y1, dy1, B, T1, F1, Cc):
     """dy1 = [y1 > 0] * conv2^T(dy2) (stride-2 3x3 transposed conv, no im2col); dy2 (B T2 F2, C),
     y1 / dy1 (B T1 F1, C) channels-last f32."""
     T2, F2 = (T1 - 1) // 2 + 1, (F1 - 1) // 2 + 1
-    assert dy2.numel() == B * T2 * F2 * Cc and y1.numel() == B * T1 * F1 * Cc and dy1.numel() == y1.numel()
+    ldy1 = _img_ld(y1, B * T1 * F1, Cc, "subsample_conv2_dgrad y1")
+    assert dy2.numel() == B * T2 * F2 * Cc and dy1.numel() == B * T1 * F1 * Cc
     call("kdfm_subsample_conv2_dgrad", ptr(_f32(dy2)), ptr(wt), ptr(_bf16(y1, "y1 (bf16 conv1 output)")), ptr(_f32(dy1)),
-         B, T1, F1, Cc, _s())
+         B, T1, F1, Cc, ldy1, _s())
 
 
 # ------------------------------------------------------------------------------------------------

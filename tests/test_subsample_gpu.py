@@ -350,3 +350,60 @@ def test_ss_out_dgrad_matches_linear_dx(K, rows, d, F2, C):
     assert torch.equal(got[y2 <= 0], torch.zeros_like(got[y2 <= 0]))
     err = (got - ref).abs()
     assert (err <= ref.abs() * 2.0 ** -8 + 1e-6).all(), err.max().item()
+
+
+@pytest.mark.parametrize("C,Tm,lens", [(88, 1601, (1601, 1600, 5)), (88, 57, (57, 40, 23)), (176, 73, (73, 8, 3))])
+def test_subsample_padded_y1_rows(K, C, Tm, lens):
+    """kdfm_subsample_fused with y1 rows padded to whole 32-channel chunks (ldy1 = 32 ceil(C / 32), the training
+    step's layout) against the unpadded form: y2 and y1[:, :C] bitwise equal, the padding channels exactly 0;
+    its consumers over the padded rows -- the conv2 weight gradient gathered from y1 (kdfm_wgrad_bf16_s2conv) and
+    the conv2 data gradient with the fused conv0 weight gradient (kdfm_subsample_conv2_dgrad_w0_h, its ReLU' read
+    from y1) -- bitwise equal to the same calls over the unpadded y1."""
+    g = torch.Generator().manual_seed(3 * C + Tm)
+    B, Fq = 3, 80
+    mel = torch.randn(B, Tm, Fq, generator=g).cuda()
+    mel_len = torch.tensor(lens, dtype=torch.int64).cuda()
+    len1 = _lens(mel_len)
+    len2 = _lens(len1)
+    w0 = torch.randn(C, 1, 3, 3, generator=g) * 0.3
+    b0 = (torch.randn(C, generator=g) * 0.1).cuda()
+    w2 = torch.randn(C, C, 3, 3, generator=g) * (1.0 / (3 * C ** 0.5))
+    b2 = (torch.randn(C, generator=g) * 0.1).cuda()
+    T1, F1 = _lens(Tm), _lens(Fq)
+    T2, F2 = _lens(T1), _lens(F1)
+    ld = -(-C // 32) * 32
+    wp = torch.empty(K.subsample_fused_wprep_elems(C), device="cuda", dtype=torch.bfloat16)
+    K.subsample_fused_wprep(w0.cuda(), w2.cuda(), wp)
+    args = (mel, mel_len, len1, len2, wp, b0, b2)
+    y1u = torch.full((B * T1 * F1, C), float("nan"), device="cuda").bfloat16()
+    y2u = torch.full((B * T2 * F2, C), float("nan"), device="cuda")
+    K.subsample_fused(*args, y2u, y1u, B, Tm, Fq, C)
+    y1p = torch.full((B * T1 * F1, ld), float("nan"), device="cuda").bfloat16()
+    y2p = torch.full((B * T2 * F2, C), float("nan"), device="cuda")
+    K.subsample_fused(*args, y2p, y1p, B, Tm, Fq, C)
+    torch.cuda.synchronize()
+    assert torch.equal(y2p, y2u)
+    assert torch.equal(y1p[:, :C], y1u)
+    if ld > C:
+        assert torch.equal(y1p[:, C:].float(), torch.zeros(B * T1 * F1, ld - C, device="cuda"))
+    if C > 96:   # the consumers run for the trained student's widths
+        return
+    dY = torch.randn(B * T2 * F2, C, generator=g).bfloat16().cuda()
+    outs = []
+    for y1 in (y1u, y1p):
+        dW = torch.zeros(C, 9 * C, device="cuda")
+        db = torch.zeros(C, device="cuda")
+        K.wgrad_bf16_s2conv(dY, y1, len1, dW, db, B, T1, F1, C)
+        outs.append((dW, db))
+    if K.subsample_dgrad_supported(C):
+        wt = torch.empty(K.subsample_dgrad_wprep_elems(C), device="cuda", dtype=torch.bfloat16)
+        K.subsample_dgrad_wprep(w2.cuda(), wt)
+        for i, y1 in enumerate((y1u, y1p)):
+            dy1 = torch.empty(B * T1 * F1, C, device="cuda")
+            dw0 = torch.zeros(C, 9, device="cuda")
+            db0 = torch.zeros(C, device="cuda")
+            K.subsample_conv2_dgrad_w0_h(dY, wt, y1, B, T1, F1, C, mel, mel_len, Tm, Fq, 1, dw0, db0, dy1=dy1)
+            outs[i] = outs[i] + (dy1, dw0, db0)
+    torch.cuda.synchronize()
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)

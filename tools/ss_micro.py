@@ -28,7 +28,8 @@ for C, side in ((88, True), (176, False)):
     wp = torch.empty(K.subsample_fused_wprep_elems(C), device=dev, dtype=torch.bfloat16)
     K.subsample_fused_wprep(w0, w2, wp)
     y2 = torch.empty(B * T2 * F2, C, device=dev)
-    y1 = torch.empty(B * T1 * F1, C, device=dev, dtype=torch.bfloat16) if side else None
+    ld = int(os.environ.get("SS_Y1_LD", str(C)))   # y1 row stride (96: the step's padded rows)
+    y1 = torch.empty(B * T1 * F1, ld, device=dev, dtype=torch.bfloat16) if side else None
     runs[C] = lambda wp=wp, b0=b0, b2=b2, y2=y2, y1=y1, C=C: K.subsample_fused(mel, ml, l1, l2, wp, b0, b2, y2, y1,
                                                                             B, Tm, F, C)
 
