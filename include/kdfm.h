@@ -63,6 +63,11 @@ int32_t kdfm_range_pop(void);
  * kernels.  `event` is a hipEvent_t, `stream` a hipStream_t, both owned by the caller. */
 int kdfm_event_record(void* event, void* stream);
 int kdfm_stream_wait_event(void* stream, void* event);
+/* Cross-stream link events: *event = a hipEvent_t created with hipEventDisableTiming | flags (flags: the HIP
+ * release-scope flags, e.g. hipEventReleaseToDevice 0x40000000 or hipEventDisableSystemFence 0x20000000 -- a
+ * link between two streams of one device needs no system-scope fence); destroy with kdfm_event_destroy. */
+int kdfm_event_create(void** event, uint32_t flags);
+int kdfm_event_destroy(void* event);
 /* A HIP stream restricted to n_cus CUs spread uniformly over the device (hipExtStreamCreateWithCUMask);
  * *out receives the hipStream_t (the caller destroys it with hipStreamDestroy). */
 int kdfm_stream_create_cu_mask(int32_t n_cus, void** out);

@@ -124,6 +124,28 @@ int kdfm_event_record(void* event, void* stream) {
   return KDFM_OK;
 }
 
+// cross-stream link events: hipEventDisableTiming plus the caller's release scope flags (the step's links pass
+// hipEventReleaseToDevice / hipEventDisableSystemFence: a consumer on another stream of the same device needs the
+// device-scope release every kernel boundary already has, not a system-scope fence)
+int kdfm_event_create(void** event, uint32_t flags) {
+  KDFM_REQUIRE(event, "null pointer");
+  hipEvent_t e = nullptr;
+  if (hipEventCreateWithFlags(&e, hipEventDisableTiming | flags) != hipSuccess) {
+    kdfm::set_error("kdfm_event_create: hipEventCreateWithFlags failed");
+    return KDFM_ELAUNCH;
+  }
+  *event = e;
+  return KDFM_OK;
+}
+
+int kdfm_event_destroy(void* event) {
+  if (event && hipEventDestroy(static_cast<hipEvent_t>(event)) != hipSuccess) {
+    kdfm::set_error("kdfm_event_destroy: hipEventDestroy failed");
+    return KDFM_ELAUNCH;
+  }
+  return KDFM_OK;
+}
+
 int kdfm_stream_wait_event(void* stream, void* event) {
   if (hipStreamWaitEvent(kdfm::as_stream(stream), static_cast<hipEvent_t>(event), 0) != hipSuccess) {
     kdfm::set_error("kdfm_stream_wait_event: hipStreamWaitEvent failed");

@@ -147,6 +147,8 @@ SIGNATURES: dict[str, tuple] = {
     "kdfm_range_pop": (_i32, []),
     "kdfm_event_record": (_i32, [P, P]),
     "kdfm_stream_wait_event": (_i32, [P, P]),
+    "kdfm_event_create": (_i32, [P, C.c_uint32]),
+    "kdfm_event_destroy": (_i32, [P]),
     "kdfm_stream_create_cu_mask": (_i32, [_i32, C.POINTER(C.c_void_p)]),
     "kdfm_memset_async": (_i32, [P, _i32, _i64, P]),
     "kdfm_cast_bf16": (_i32, [P, P, _i64, P]),

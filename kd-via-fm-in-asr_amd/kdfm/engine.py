@@ -286,12 +286,12 @@ class Ver5Engine:
             tae = (torch.empty(n_st, cfg.latent, device=dev), torch.empty(n_st, St.d, device=dev))
         if own_mel:
             # the teacher's own (undithered) frontend goes to the teacher stream with its encoder
-            side.wait_stream(main)
+            K.wait_stream(side, main)
             with torch.cuda.stream(side), K.region("teacher_frontend"):
                 mel_t = frontend_forward(cfg, self.fe, wav, wav_len, mel_len, dither=0.0)
         else:
             mel_t = frontend_forward(cfg, self.fe, wav, wav_len, mel_len, dither=0.0)
-            side.wait_stream(main)
+            K.wait_stream(side, main)
         tgen = encoder_forward_steps(cfg, St, self.teacher.P, "teacher.encoder.", mel_t, mel_len, len1, len2,
                                      tfeats, self._pos_emb(T, St.d), train=False, seed=seed, salt=SALT_TEACHER,
                                      save=False, bn_running=self.bn.P, use_batch_stats=False, ws=self._enc_ws(St, "teacher.encoder."))
@@ -352,7 +352,7 @@ class Ver5Engine:
         if encfm:
             # asr_train.py: the router + flow matching over every hooked layer pair (it needs the teacher's
             # features), and the decoder reads the last layer's FM output (:595-666)
-            main.wait_stream(side)
+            K.wait_stream(main, side)
             ews = self._encfm_ws(B, T)
             with K.region("encfm_forward"):
                 dec_in = encfm_forward(cfg, self.student.P, sfeats, tfeats, ews, seed=seed, train=train,
@@ -364,11 +364,11 @@ class Ver5Engine:
         lp = torch.empty(rows, Cn, device=dev)
         K.log_softmax(logits, lp)
         if not encfm:
-            main.wait_stream(side)
+            K.wait_stream(main, side)
         # ---- CTC + logit KD on a third stream: they only need the two logit tensors, and their
         # result is first needed after the KD heads' forward, so the serial CTC recursion overlaps it ----
         aux = self._aux_stream()
-        aux.wait_stream(main)
+        K.wait_stream(aux, main)
         Umax = targets.shape[1]
         nll = torch.empty(B, device=dev)
         glogits = torch.empty(rows, Cn, device=dev)
@@ -396,7 +396,7 @@ class Ver5Engine:
                                        save=save, Pfix=self.fixed.P, acc_diffkd=acc[6:7], tae=(tae[0][nb:], tae[1][nb:]),
                                        layers=cfg.n_layers - h)
                 if h:
-                    main.wait_stream(self._heads_stream(main))   # the first half's loss terms
+                    K.wait_stream(main, self._heads_stream(main))   # the first half's loss terms
                     K.axpby(acc_h[2:7].view(1, 5), acc[2:7].view(1, 5), acc[2:7].view(1, 5), 1.0, 1.0)
                 hctx = (hctx_b, hctx_a, h) if save else None
                 K.colsum(acc[2:7].view(5, 1), acc[7:8], accumulate=False)
@@ -488,9 +488,9 @@ class Ver5Engine:
         hs = self._heads_stream(main)
         # the teacher features / auto-encoder outputs of layers [0, h) come from the teacher stream: wait for it
         # in line too (the serialised schedule once read them unjoined -- profiles/r05/r5zz*)
-        hs.wait_stream(side)
+        K.wait_stream(hs, side)
         if hs is not main:
-            hs.wait_stream(main)
+            K.wait_stream(hs, main)
             for t in (sfeats, tfeats, *tae, acc) + (() if eps is None else (eps,)):
                 t.record_stream(hs)
         with K.on_stream(hs), K.region("heads_forward_first_half"):
@@ -501,7 +501,7 @@ class Ver5Engine:
 
     def _join_losses(self, ctx):
         """Join the CTC/KL stream and assemble the loss vector (total, ctc, kl, recon, fm)."""
-        torch.cuda.current_stream(self.device).wait_stream(self._aux_stream())
+        K.wait_stream(torch.cuda.current_stream(self.device), self._aux_stream())
         acc = ctx["acc"]
         K.loss_combine(ctx["nll"], acc[0:1], acc[1:2], acc[7:8], self.cfg.kd_alpha, self.losses)
 
@@ -573,7 +573,7 @@ class Ver5Engine:
                 side = main = torch.cuda.current_stream(self.device)
                 if not self._serial():
                     side = self._side_stream()
-                    side.wait_stream(main)
+                    K.wait_stream(side, main)
                     dfeats.record_stream(side)
                 with K.on_stream(side), K.region("heads_backward_first_half"):
                     heads_backward(cfg, P, G, hctx_b, self.hws_b, dfv[:nb], seed=self.seed)
@@ -598,8 +598,8 @@ class Ver5Engine:
             encoder_backward(cfg, Ss, P, G, "encoder.", ctx.pop("srun"), dfeats, ctx["pos_s"], ctx["len1"],
                              ctx["len2"], seed=self.seed, salt=SALT_STUDENT, ws=self._enc_ws(Ss, "encoder."),
                              on_layer_done=layer_done,
-                             before_read=None if join is None else {join[0]: lambda: torch.cuda.current_stream(
-                                 self.device).wait_stream(join[1])}, arena_set=arena is not None)
+                             before_read=None if join is None else {join[0]: lambda: K.wait_stream(
+                                 torch.cuda.current_stream(self.device), join[1])}, arena_set=arena is not None)
 
     def _decoder_dw(self, g, x):
         """The decoder's weight / bias gradient from the logits gradient g and its input x, on the

@@ -91,7 +91,7 @@ class WgradOverlap:
     def fence(self, stream) -> None:
         """`stream` waits for every side-stream launch issued so far (no effect when none pending)."""
         if self._pending:
-            stream.wait_stream(self._stream(stream.device))
+            K.wait_stream(stream, self._stream(stream.device))
 
     def serialized(self, on: bool = True):
         """Context manager: with on=True every weight-gradient product runs in line on the issuing

@@ -37,7 +37,14 @@ def sname(s):
 evs, rec_by = {}, {}
 lines = []
 for i, op in enumerate(plan.ops):
-    if op[0] == "k":
+    if op[0] == "k" and getattr(op[1], "__name__", "") == "kdfm_event_record":   # K.LinkEvent (event, stream)
+        e = evs.setdefault(op[2][0], len(evs))
+        rec_by[e] = sname(op[2][1])
+        lines.append(f"{i:5d} R {sname(op[2][1]):8s} ev{e}")
+    elif op[0] == "k" and getattr(op[1], "__name__", "") == "kdfm_stream_wait_event":   # (stream, event)
+        e = evs.setdefault(op[2][1], len(evs))
+        lines.append(f"{i:5d} W {sname(op[2][0]):8s} ev{e} (recorded on {rec_by.get(e, '?')})")
+    elif op[0] == "k":
         nm = getattr(op[1], "__name__", "?")
         s = op[2][-1] if op[2] else None
         lines.append(f"{i:5d} K {sname(s):8s} {nm}")

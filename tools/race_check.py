@@ -341,6 +341,21 @@ def install(tracer: Tracer):
         return sync(device)
 
     E.record, E.wait, E.synchronize, S.synchronize, torch.cuda.synchronize = record, wait, esync, ssync, dsync
+    # the step's device-scope link events (KDFM_LINK_EVENTS): the same edges
+    L = K.LinkEvent
+    l_record, l_wait = L.record, L.wait
+
+    def lrecord(self, stream=None):
+        if T.active:
+            T.record(self, _stream_ptr(stream))
+        return l_record(self, stream)
+
+    def lwait(self, stream=None):
+        if T.active:
+            T.wait(self, _stream_ptr(stream))
+        return l_wait(self, stream)
+
+    L.record, L.wait = lrecord, lwait
 
     def all_reduce(tensor, op=None, group=None, async_op=False):
         s = _cur()
@@ -374,6 +389,8 @@ def _on_call(name, args):
     from kdfm import kernels as K
     s = _cur()
     site = _site()
+    if name in ("kdfm_event_record", "kdfm_stream_wait_event"):   # K.LinkEvent: ordering, hooked below
+        return
     if name in ("kdfm_gemm", "kdfm_gemm_big", "kdfm_gemm_big_fp8"):
         v = K._GEMM_FMT.unpack_from(K._GEMM_BUF, 0)
         if name != "kdfm_gemm":   # its bf16 / fp8 operands and output are arguments; the descriptor carries the rest
@@ -508,18 +525,19 @@ def mutate(kind, eng):
         orig = Ver5Engine._heads_first_half
 
         def heads_first_half(self, *a):
+            from kdfm import kernels as K
             side = a[-1]
-            ws_orig = torch.cuda.Stream.wait_stream
+            ws_orig = K.wait_stream   # the engine's joins go through kernels.wait_stream (either link-event kind)
 
-            def wait_stream(self_, other):
-                if other.cuda_stream == side.cuda_stream:
+            def wait_stream(dst, src):
+                if src.cuda_stream == side.cuda_stream:
                     return None   # the dropped join
-                return ws_orig(self_, other)
-            torch.cuda.Stream.wait_stream = wait_stream
+                return ws_orig(dst, src)
+            K.wait_stream = wait_stream
             try:
                 return orig(self, *a)
             finally:
-                torch.cuda.Stream.wait_stream = ws_orig
+                K.wait_stream = ws_orig
         Ver5Engine._heads_first_half = heads_first_half
     elif kind == "bucket_early":
         from kdfm.ddp import BucketedGradAllReduce

@@ -80,6 +80,36 @@ def producer(step, main, t_prev_end, t_next, slack_us=8.0):
     return best
 
 
+def seq(path):
+    """The busiest stream's kernels of the last full step in issue order: gap before each, duration, name; then
+    the gap histogram (kernel-boundary idle time by size)."""
+    rows = load(path)
+    ends = [e for s, e, q, n in rows if "adamw_kernel" in n]
+    if len(ends) < 3:
+        print("need >= 3 steps in the trace")
+        return
+    t0, t1 = ends[-3], ends[-2]
+    step = [(s, e, q, n) for s, e, q, n in rows if s >= t0 and e <= t1]
+    busy = defaultdict(float)
+    for s, e, q, n in step:
+        busy[q] += e - s
+    main_sid = max(busy, key=busy.get)
+    prev = t0
+    hist = defaultdict(float)
+    nh = defaultdict(int)
+    for s, e, q, n in step:
+        if q != main_sid:
+            continue
+        g = max(0, s - prev) / 1e3
+        b = "<5" if g < 5 else "5-10" if g < 10 else "10-30" if g < 30 else ">=30"
+        hist[b] += g
+        nh[b] += 1
+        print(f"{g:8.1f} {(e - s) / 1e3:8.1f}  {n[:70]}")
+        prev = e
+    print("gaps before main-stream kernels (us): " + ", ".join(f"{k}: {nh[k]} / {hist[k]:.0f}" for k in
+                                                             ("<5", "5-10", "10-30", ">=30")))
+
+
 def gaps(path, main_sid=None, min_us=30.0):
     """Main-stream idle gaps inside the last full step, each attributed to the producer it waited on
     (producer()): cross-stream waits summed per producer stream / kernel, the rest as host issue."""
@@ -130,3 +160,5 @@ if __name__ == "__main__":
     main()
     if len(sys.argv) > 2 and sys.argv[2] == "gaps":
         gaps(sys.argv[1])
+    elif len(sys.argv) > 2 and sys.argv[2] == "seq":
+        seq(sys.argv[1])
