@@ -44,6 +44,76 @@ class PlanError(RuntimeError):
     pass
 
 
+# KDFM_PLAN_ELIDE=0: replay every recorded cross-stream link (A/B switch)
+_ELIDE = os.environ.get("KDFM_PLAN_ELIDE", "1") == "1"
+
+
+def _link(op):
+    """("r" | "w", event handle, stream handle) of a link op (torch events "er" / "ew", or K.LinkEvent's
+    kdfm_event_record / kdfm_stream_wait_event launches), else None."""
+    if op[0] in ("er", "ew"):
+        return op[0][1], op[1].value, op[2].value
+    if op[0] == "k":
+        nm = getattr(op[1], "__name__", "")
+        if nm == "kdfm_event_record":
+            return "r", op[2][0], op[2][1]
+        if nm == "kdfm_stream_wait_event":
+            return "w", op[2][1], op[2][0]
+    return None
+
+
+def _raw(v):
+    return v.value if isinstance(v, C.c_void_p) else v
+
+
+def _elide_links(ops):
+    """Drop a link that repeats the previous one: an event re-recorded on stream S with nothing issued on S
+    since its last record there, and the waits on it by streams that already waited on that earlier record
+    (a wait binds to the latest record, which now marks the same point of S).  The recorded step makes these
+    when two weight-gradient jobs fork off one compute-stream point; each record / wait is a packet on its
+    stream's queue, between kernels.  Conservative: a launch is attributed to a stream only when one of its
+    arguments is a stream the links use; a launch naming none of them, and a host callback, end every run."""
+    streams = set()
+    for op in ops:
+        lk = _link(op)
+        if lk is not None:
+            streams.add(lk[2])
+    out = []
+    last = {}        # event -> (stream, ops issued on it up to and including the record, streams waited since)
+    issued = {}      # stream -> ops issued on it so far
+    dropped = set()  # events whose latest record was dropped
+    for op in ops:
+        lk = _link(op)
+        if lk is None:
+            hit = [a for a in (op[2] if op[0] == "k" else ()) if isinstance(a, (int, C.c_void_p)) and _raw(a) in streams]
+            if not hit:
+                last.clear()
+                dropped.clear()
+            for a in hit[-1:]:
+                issued[_raw(a)] = issued.get(_raw(a), 0) + 1
+            out.append(op)
+            continue
+        kind, ev, s = lk
+        if kind == "r":
+            prev = last.get(ev)
+            if prev is not None and prev[0] == s and prev[1] == issued.get(s, 0):
+                dropped.add(ev)   # the same point of s as the record the waiters already bound to
+                continue
+            dropped.discard(ev)
+            issued[s] = issued.get(s, 0) + 1
+            last[ev] = (s, issued[s], set())
+            out.append(op)
+        else:
+            prev = last.get(ev)
+            if ev in dropped and prev is not None and s in prev[2]:
+                continue          # this stream already waits for that point
+            if prev is not None:
+                prev[2].add(s)
+            issued[s] = issued.get(s, 0) + 1
+            out.append(op)
+    return out
+
+
 class _Recorder(TorchDispatchMode):
     def __init__(self, plan):
         super().__init__()
@@ -172,7 +242,7 @@ class StepPlan:
                 ops.append((op[0], C.c_void_p(op[1].cuda_event), C.c_void_p(op[2])))
             else:
                 ops.append(op)
-        self.ops = ops
+        self.ops = _elide_links(ops) if _ELIDE else ops
         return self
 
     # ---- replay ---------------------------------------------------------------------------------
