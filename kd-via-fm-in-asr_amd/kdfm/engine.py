@@ -8,6 +8,8 @@ teacher preprocessor + encoder under no_grad, decoder] -> CTC (:740-746) -> logi
 """
 from __future__ import annotations
 
+import contextlib
+
 import math
 
 import torch
@@ -32,6 +34,7 @@ from .overlap import WGRAD
 # KDFM_STREAM_PRIO=compute[,side][,aux]: only the named roles high-priority (the round-6 A/B: the compute stream alone,
 # so the student chain takes freed CUs ahead of the teacher and the weight gradients)
 _PRIO_ENV = __import__("os").environ.get("KDFM_STREAM_PRIO", "0")
+_STEP_BRACKET = __import__("os").environ.get("KDFM_STEP_BRACKET", "1") == "1"
 _PRIO = {"compute", "side", "aux"} if _PRIO_ENV == "1" else {r for r in _PRIO_ENV.split(",") if r not in ("", "0")}
 
 
@@ -644,17 +647,21 @@ class Ver5Engine:
 
     def train_step(self, wav, wav_len, targets, tgt_len, allreduce=None):
         """forward + backward + (all-reduce) + AdamW.  Returns the device loss vector."""
-        self.advance_rng()
         ready = getattr(allreduce, "ready", None)
         grad = self.student.grad
-        with K.weight_epoch():   # one epoch for forward + backward: the large-tile route converts each weight once
-            ctx = self.forward(wav, wav_len, targets, tgt_len, train=True)
-            self.backward(ctx, grad_ready=(lambda o: ready(grad, o)) if ready is not None else None)
-            del ctx
-        scale = 1.0
-        if allreduce is not None:
-            scale = self.allreduce_grads(allreduce)
-        self.optimizer_step(scale)
+        # one caller <-> compute-stream bracket for the whole step (the inner calls' brackets are then no-ops):
+        # the forward -> backward -> optimizer hand-overs stay on the compute stream instead of each making a
+        # round trip through the caller's stream (KDFM_STEP_BRACKET=0: per-call brackets)
+        with (self._on_stream() if _STEP_BRACKET else contextlib.nullcontext()):
+            self.advance_rng()
+            with K.weight_epoch():   # one epoch for forward + backward: the large-tile route converts each weight once
+                ctx = self.forward(wav, wav_len, targets, tgt_len, train=True)
+                self.backward(ctx, grad_ready=(lambda o: ready(grad, o)) if ready is not None else None)
+                del ctx
+            scale = 1.0
+            if allreduce is not None:
+                scale = self.allreduce_grads(allreduce)
+            self.optimizer_step(scale)
         return self.losses
 
 
@@ -674,15 +681,16 @@ class Ver5Engine:
             box["scale"] = self.allreduce_grads(allreduce) if allreduce is not None else 1.0
 
         def step():
-            self.advance_rng()
-            with K.weight_epoch():
-                ctx = self.forward(wav, wav_len, targets, tgt_len, train=True)
-                self.backward(ctx, grad_ready=(lambda o: plan.host(ready, grad, o)) if ready is not None else None)
-                del ctx
-            if allreduce is not None:
-                with K.region("allreduce"):
-                    plan.host(finish)
-            self.optimizer_step(box.get("scale", 1.0))
+            with (self._on_stream() if _STEP_BRACKET else contextlib.nullcontext()):   # as train_step
+                self.advance_rng()
+                with K.weight_epoch():
+                    ctx = self.forward(wav, wav_len, targets, tgt_len, train=True)
+                    self.backward(ctx, grad_ready=(lambda o: plan.host(ready, grad, o)) if ready is not None else None)
+                    del ctx
+                if allreduce is not None:
+                    with K.region("allreduce"):
+                        plan.host(finish)
+                self.optimizer_step(box.get("scale", 1.0))
 
         plan.record(step)
         plan.inputs = (wav, wav_len, targets, tgt_len)
