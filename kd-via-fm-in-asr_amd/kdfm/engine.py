@@ -35,6 +35,9 @@ from .overlap import WGRAD
 # so the student chain takes freed CUs ahead of the teacher and the weight gradients)
 _PRIO_ENV = __import__("os").environ.get("KDFM_STREAM_PRIO", "0")
 _STEP_BRACKET = __import__("os").environ.get("KDFM_STEP_BRACKET", "1") == "1"
+# the frozen teacher's bf16 weight twins and fused-kernel images are rebuilt on the teacher stream after it forks
+# (KDFM_TEACHER_PREP_SIDE=0: on the compute stream before the fork, delaying both chains)
+_TEACHER_PREP_SIDE = __import__("os").environ.get("KDFM_TEACHER_PREP_SIDE", "1") == "1"
 _PRIO = {"compute", "side", "aux"} if _PRIO_ENV == "1" else {r for r in _PRIO_ENV.split(",") if r not in ("", "0")}
 
 
@@ -259,9 +262,9 @@ class Ver5Engine:
         # kl | recon, kd_pre, fm_pre, kd_post, fm_post (heads.RECON..FM_POST) | diffkd | sum of the layer-KD
         # terms and diffkd (zeroed before the teacher stream forks: its auto-encoder adds the recon term)
         acc = torch.zeros(8, device=dev)
+        teacher_prep = None
         if K.get_math() == "bf16":   # bf16 twins of the weights the skinny products stream
             self.student.refresh_bf16()
-            self.teacher.refresh_bf16()
             # fragment images of the fused Conformer kernels (ffn / lnproj / rowgemm): one launch each
             if self._imgs is None:
                 self._imgs = (layer_images(cfg, self.student.P, "encoder.", cfg.d_student, train=True, dev=dev),
@@ -269,7 +272,14 @@ class Ver5Engine:
                                            dev=dev))
             for im in self._imgs:
                 im.register()
-                im.refresh()
+            self._imgs[0].refresh()
+
+            def teacher_prep():
+                self.teacher.refresh_bf16()
+                self._imgs[1].refresh()
+            if not _TEACHER_PREP_SIDE:   # KDFM_TEACHER_PREP_SIDE=0: on this stream, before the teacher forks
+                teacher_prep()
+                teacher_prep = None
         # ---- frontends (teacher preprocessor is in eval mode: no dither) ----
         dither = cfg.dither if train else 0.0
         own_mel = train and (dither > 0.0 or not cfg.share_frontend)   # the student computes its own mel
@@ -288,13 +298,19 @@ class Ver5Engine:
         if heads:
             tae = (torch.empty(n_st, cfg.latent, device=dev), torch.empty(n_st, St.d, device=dev))
         if own_mel:
-            # the teacher's own (undithered) frontend goes to the teacher stream with its encoder
+            # the teacher's own (undithered) frontend goes to the teacher stream with its encoder (and the
+            # teacher's weight twins / images: read by teacher-stream kernels only)
             K.wait_stream(side, main)
             with torch.cuda.stream(side), K.region("teacher_frontend"):
+                if teacher_prep is not None:
+                    teacher_prep()
                 mel_t = frontend_forward(cfg, self.fe, wav, wav_len, mel_len, dither=0.0)
         else:
             mel_t = frontend_forward(cfg, self.fe, wav, wav_len, mel_len, dither=0.0)
             K.wait_stream(side, main)
+            if teacher_prep is not None:
+                with torch.cuda.stream(side):
+                    teacher_prep()
         tgen = encoder_forward_steps(cfg, St, self.teacher.P, "teacher.encoder.", mel_t, mel_len, len1, len2,
                                      tfeats, self._pos_emb(T, St.d), train=False, seed=seed, salt=SALT_TEACHER,
                                      save=False, bn_running=self.bn.P, use_batch_stats=False, ws=self._enc_ws(St, "teacher.encoder."))
